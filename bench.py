@@ -1,0 +1,161 @@
+#!/usr/bin/env python3
+"""Headline benchmark: RCCL all-reduce bus bandwidth on MI355X (+ node-ready latency).
+
+BASELINE.json metric: "node scale-out-ready latency (s) + rccl all-reduce busbw GB/s at
+1/2/4/8 GPU", config "L3 mode, 8xMI355X single node: all xGMI + host RoCE links configured,
+rccl-tests 8-GPU all-reduce".
+
+* One process per GPU (``torchrun --nproc-per-node N``), ``torch.distributed`` backend
+  ``nccl`` (= RCCL over xGMI on ROCm).  A *step* is one in-place bf16 all-reduce of
+  ``--bytes`` per rank (default 1 GiB, rccl-tests' large-message regime); ``--warmup``
+  untimed steps, then exactly ``--steps`` timed steps bracketed by barrier +
+  ``torch.cuda.synchronize()``, max over ranks.
+* ``value`` is busbw = algbw * 2(n-1)/n (rccl-tests definition).  At n = 1 there are no
+  links and busbw is 0 by definition; algbw and latency are still reported.
+* Before timing, the result of one all-reduce of rank-specific patterns is verified exactly
+  with the HIP kernels in ``libnetop_hip.so`` (fails loudly if the library is missing).
+* The node-ready latency half of the metric needs a private network namespace (root /
+  user namespaces + AF_PACKET); it runs with ``--node-ready`` where that is available and is
+  reported as null with the reason otherwise (the GPU pool's boxes run unprivileged).
+* Data are synthetic (RCCL moves the same bytes whatever their values).
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import socket
+import sys
+import time
+
+METRIC = "node scale-out-ready latency (s) + rccl all-reduce busbw GB/s at 1/2/4/8 GPU"
+CONFIG_NAME = ("L3 mode, 8xMI355X single node: all xGMI + host RoCE links configured, "
+               "rccl-tests 8-GPU all-reduce")
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--bytes", type=int, default=1 << 30, help="all-reduce message size per rank")
+    ap.add_argument("--sweep", default="4096,1048576,67108864", help="extra sizes (bytes) reported alongside")
+    ap.add_argument("--node-ready", choices=["auto", "on", "off"], default="auto")
+    ap.add_argument("--node-ready-runs", type=int, default=5)
+    args = ap.parse_args(argv)
+
+    import torch
+    import torch.distributed as dist
+
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from network_operator_amd.parallel import collectives as C
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"warning: --gpus={args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", str(_free_port()))
+    if not torch.cuda.is_available():
+        print("bench.py needs an MI355X GPU (torch.cuda.is_available() is False)", file=sys.stderr)
+        return 2
+    torch.cuda.set_device(local_rank)
+    device = torch.device("cuda", local_rank)
+    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=device)
+
+    # 1. Correctness of the collective path (exact, HIP pattern kernels).
+    verified, errors = C.verify_all_reduce(min(args.bytes // 2, 64 << 20), device)
+
+    # 2. Headline: K timed all-reduce steps of --bytes per rank.
+    numel = (args.bytes // 2) // 8 * 8
+    buf = torch.zeros(numel, dtype=torch.bfloat16, device=device)
+    for _ in range(args.warmup):
+        dist.all_reduce(buf)
+    dist.barrier()
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        dist.all_reduce(buf)
+    torch.cuda.synchronize(device)
+    dt = time.perf_counter() - t0
+    dist.barrier()
+    t = torch.tensor([dt], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dt = float(t.item())
+    per_step = dt / max(args.steps, 1)
+    nbytes = numel * 2
+    algbw, busbw = C.bandwidths("all_reduce", nbytes, world, per_step)
+    del buf
+
+    # 3. Size sweep (latency / medium messages), same definitions.
+    sweep = []
+    sizes = [int(s) for s in args.sweep.split(",") if s.strip()]
+    if sizes:
+        for r in C.run_sweep("all_reduce", sizes, iters=max(args.steps, 10), warmup=max(args.warmup, 3), device=device):
+            sweep.append({"bytes": r.bytes, "time_us": r.time_s * 1e6, "algbw_GBps": r.algbw_GBps,
+                          "busbw_GBps": r.busbw_GBps})
+
+    node_ready = None
+    node_ready_note = None
+    if rank == 0 and args.node_ready != "off":
+        try:
+            from network_operator_amd.testing import netns
+
+            ok, why = netns.available()
+            if ok:
+                node_ready = netns.node_ready_bench(n_nics=max(world, 1), runs=args.node_ready_runs)
+            else:
+                node_ready_note = why
+                if args.node_ready == "on":
+                    raise RuntimeError(why)
+        except Exception as e:  # the collective result stands on its own
+            node_ready_note = f"node-ready harness unavailable: {e}"
+
+    dist.barrier()
+    ceiling = C.xgmi_busbw_ceiling_GBps(world)
+    if rank == 0:
+        line = {
+            "metric": METRIC,
+            "value": round(busbw, 3),
+            "unit": "GB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": per_step * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic (zeros for the timed loop; exact pattern check before timing)",
+            "config": {"model": CONFIG_NAME, "global_batch": None, "seq_len": None,
+                       "parallelism": f"dp{world}", "message_bytes_per_rank": nbytes, "op": "all_reduce(sum)",
+                       "backend": "torch.distributed nccl (RCCL)"},
+            "algbw_GBps": algbw,
+            "busbw_GBps": busbw,
+            "busbw_ceiling_GBps": ceiling,
+            "busbw_vs_ceiling": (busbw / ceiling) if ceiling else None,
+            "verified": verified,
+            "verify_errors": errors,
+            "sweep": sweep,
+            "node_ready": node_ready,
+            "notes": ("n=1: busbw is 0 by definition (rccl-tests factor 2(n-1)/n); reference publishes no numbers "
+                      "(BASELINE.md) so vs_baseline is null") + (f"; {node_ready_note}" if node_ready_note else ""),
+            "rccl_version": ".".join(str(x) for x in torch.cuda.nccl.version()) if hasattr(torch.cuda, "nccl") else None,
+        }
+        print(json.dumps(line), flush=True)
+    dist.destroy_process_group()
+    return 0 if verified else 1
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,308 @@
+// MI355X validation kernels for the network operator (gfx950, wave64).
+//
+// The operator's job ends at "RCCL sees every link".  These kernels are what the node
+// tooling and the bench use to *prove* it on the GPU side:
+//
+//   * netop_fill_pattern / netop_verify_sum — bf16 all-reduce correctness check.  Each rank
+//     fills a deterministic small-integer pattern (exact in bf16 for any reduction order);
+//     the verifier recomputes Σ_ranks pattern and counts mismatches.  16-byte vector
+//     accesses (8 x bf16 per lane), grid-stride, one atomic per workgroup.
+//   * netop_copy — 16-B/lane streaming copy used by the xGMI link probe: with peer access
+//     enabled the loads of a peer pointer travel over the xGMI link to that peer, so one
+//     copy per peer on its own stream drives all 7 links of an MI355X concurrently.
+//
+// No CUDA/hipify heritage: plain HIP for gfx950, 256-thread workgroups (4 waves), grids
+// sized as a multiple of the 256 CUs.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <vector>
+
+namespace {
+
+constexpr int kThreads = 256;
+
+__device__ __forceinline__ uint32_t mix(uint64_t i, uint32_t seed) {
+    // 32-bit avalanche of (index, seed); cheap integer ALU, no tables.
+    uint32_t x = uint32_t(i) * 0x9E3779B1u ^ uint32_t(i >> 32) * 0x85EBCA77u ^ seed * 0xC2B2AE3Du;
+    x ^= x >> 15;
+    x *= 0x2C1B3C6Du;
+    x ^= x >> 12;
+    return x;
+}
+
+// Pattern value for (element, rank): an integer in [-4, 4] -> exact in bf16, sums of up to
+// 64 ranks stay exact (|sum| <= 256 < 2^8).
+__device__ __forceinline__ int pattern(uint64_t i, uint32_t seed, int rank) {
+    return int(mix(i, seed + 0x632BE5ABu * uint32_t(rank + 1)) % 9u) - 4;
+}
+
+__device__ __forceinline__ uint16_t int_to_bf16(int v) {
+    // Small integers are exact; convert through f32 bits (truncation is exact here).
+    float f = float(v);
+    return uint16_t(__float_as_uint(f) >> 16);
+}
+
+__device__ __forceinline__ float bf16_to_float(uint16_t h) { return __uint_as_float(uint32_t(h) << 16); }
+
+__global__ __launch_bounds__(kThreads) void fill_kernel(uint4* __restrict__ out, uint64_t n_vec, uint32_t seed, int rank,
+                                                        int scale_ranks) {
+    const uint64_t stride = uint64_t(gridDim.x) * kThreads;
+    for (uint64_t v = uint64_t(blockIdx.x) * kThreads + threadIdx.x; v < n_vec; v += stride) {
+        uint32_t w[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            uint64_t e = v * 8 + uint64_t(k) * 2;
+            int a, b;
+            if (scale_ranks > 0) {  // "sum of all ranks" expectation pre-computed in place
+                a = b = 0;
+                for (int r = 0; r < scale_ranks; ++r) {
+                    a += pattern(e, seed, r);
+                    b += pattern(e + 1, seed, r);
+                }
+            } else {
+                a = pattern(e, seed, rank);
+                b = pattern(e + 1, seed, rank);
+            }
+            w[k] = uint32_t(int_to_bf16(a)) | (uint32_t(int_to_bf16(b)) << 16);
+        }
+        out[v] = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+}
+
+__global__ __launch_bounds__(kThreads) void verify_kernel(const uint4* __restrict__ in, uint64_t n_vec, uint32_t seed,
+                                                          int world, unsigned long long* __restrict__ errors) {
+    __shared__ unsigned int wave_err[kThreads / 64];
+    const uint64_t stride = uint64_t(gridDim.x) * kThreads;
+    unsigned int err = 0;
+    for (uint64_t v = uint64_t(blockIdx.x) * kThreads + threadIdx.x; v < n_vec; v += stride) {
+        uint4 q = in[v];
+        uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            uint64_t e = v * 8 + uint64_t(k) * 2;
+            int a = 0, b = 0;
+            for (int r = 0; r < world; ++r) {
+                a += pattern(e, seed, r);
+                b += pattern(e + 1, seed, r);
+            }
+            err += bf16_to_float(uint16_t(w[k] & 0xffff)) != float(a);
+            err += bf16_to_float(uint16_t(w[k] >> 16)) != float(b);
+        }
+    }
+    // wave64 reduction, then one atomic per workgroup.
+    for (int off = 32; off > 0; off >>= 1) err += __shfl_down(err, off, 64);
+    if ((threadIdx.x & 63) == 0) wave_err[threadIdx.x >> 6] = err;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned int s = 0;
+        for (int i = 0; i < kThreads / 64; ++i) s += wave_err[i];
+        if (s) atomicAdd(errors, (unsigned long long)s);
+    }
+}
+
+__global__ __launch_bounds__(kThreads) void copy_kernel(const uint4* __restrict__ src, uint4* __restrict__ dst,
+                                                        uint64_t n_vec) {
+    const uint64_t stride = uint64_t(gridDim.x) * kThreads;
+    uint64_t v = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
+    // Two independent 16-B loads in flight per lane per iteration.
+    for (; v + stride < n_vec; v += 2 * stride) {
+        uint4 a = src[v];
+        uint4 b = src[v + stride];
+        dst[v] = a;
+        dst[v + stride] = b;
+    }
+    if (v < n_vec) dst[v] = src[v];
+}
+
+int grid_for(uint64_t n_vec, int per_cu = 8) {
+    // CU count per device, cached: hipGetDeviceProperties is far too slow for a launch path.
+    static int cached[64] = {};
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < 64) {
+        if (!cached[dev]) {
+            int c = 0;
+            if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && c > 0) cached[dev] = c;
+        }
+        if (cached[dev]) cus = cached[dev];
+    }
+    uint64_t need = (n_vec + kThreads - 1) / kThreads;
+    uint64_t cap = uint64_t(cus) * per_cu;
+    return int(need < cap ? (need ? need : 1) : cap);
+}
+
+}  // namespace
+
+extern "C" {
+
+// All functions return a hipError_t value (0 = success).  Sizes are in bf16 elements and
+// must be multiples of 8 (16-byte vectors); pointers must be 16-byte aligned.
+
+int netop_hip_version() { return 1; }
+
+int netop_fill_pattern(void* buf, uint64_t n_elems, uint32_t seed, int rank, hipStream_t stream) {
+    if ((n_elems & 7) || (reinterpret_cast<uintptr_t>(buf) & 15)) return int(hipErrorInvalidValue);
+    uint64_t nv = n_elems / 8;
+    hipLaunchKernelGGL(fill_kernel, dim3(grid_for(nv)), dim3(kThreads), 0, stream, static_cast<uint4*>(buf), nv, seed,
+                       rank, 0);
+    return int(hipGetLastError());
+}
+
+int netop_fill_expected_sum(void* buf, uint64_t n_elems, uint32_t seed, int world, hipStream_t stream) {
+    if ((n_elems & 7) || (reinterpret_cast<uintptr_t>(buf) & 15) || world < 1) return int(hipErrorInvalidValue);
+    uint64_t nv = n_elems / 8;
+    hipLaunchKernelGGL(fill_kernel, dim3(grid_for(nv)), dim3(kThreads), 0, stream, static_cast<uint4*>(buf), nv, seed, 0,
+                       world);
+    return int(hipGetLastError());
+}
+
+// Counts elements that differ from Σ_{r<world} pattern(i, r).  `errors` is a device pointer
+// to one uint64 that the caller zeroes.
+int netop_verify_sum(const void* buf, uint64_t n_elems, uint32_t seed, int world, unsigned long long* errors,
+                     hipStream_t stream) {
+    if ((n_elems & 7) || (reinterpret_cast<uintptr_t>(buf) & 15) || world < 1) return int(hipErrorInvalidValue);
+    uint64_t nv = n_elems / 8;
+    hipLaunchKernelGGL(verify_kernel, dim3(grid_for(nv)), dim3(kThreads), 0, stream, static_cast<const uint4*>(buf), nv,
+                       seed, world, errors);
+    return int(hipGetLastError());
+}
+
+int netop_copy(const void* src, void* dst, uint64_t bytes, hipStream_t stream) {
+    if ((bytes & 15) || (reinterpret_cast<uintptr_t>(src) & 15) || (reinterpret_cast<uintptr_t>(dst) & 15))
+        return int(hipErrorInvalidValue);
+    uint64_t nv = bytes / 16;
+    hipLaunchKernelGGL(copy_kernel, dim3(grid_for(nv)), dim3(kThreads), 0, stream, static_cast<const uint4*>(src),
+                       static_cast<uint4*>(dst), nv);
+    return int(hipGetLastError());
+}
+
+// xGMI link probe, single process, all visible GPUs.  For every ordered pair (dst, src) with
+// src != dst (or the loopback dst == src when only one GPU is visible) GPU `dst` pulls
+// `bytes` from GPU `src` with netop_copy, `iters` times.  Two phases:
+//   phase 1: one pair at a time           -> per-link GB/s in bw_single[dst * n + src]
+//   phase 2: every dst pulls from all of its peers concurrently (one stream per peer)
+//            -> aggregate GB/s per dst in bw_all[dst]
+// Data integrity is checked on every pull (pattern fill + verify on the destination).
+// Returns hipSuccess, or the first error.  `n_out` receives the number of GPUs probed.
+int netop_xgmi_probe(uint64_t bytes, int iters, int max_gpus, double* bw_single, double* bw_all, int* n_out,
+                     unsigned long long* total_errors) {
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess) return int(e);
+    if (max_gpus > 0 && n > max_gpus) n = max_gpus;
+    *n_out = n;
+    *total_errors = 0;
+    bytes &= ~uint64_t(15);
+    if (n == 0 || bytes == 0 || iters < 1) return int(hipErrorInvalidValue);
+
+    void* src[64] = {};
+    void* dst[64] = {};
+    unsigned long long* err[64] = {};
+    for (int d = 0; d < n; ++d) {
+        if ((e = hipSetDevice(d)) != hipSuccess) return int(e);
+        for (int p = 0; p < n; ++p) {
+            if (p == d) continue;
+            int can = 0;
+            hipDeviceCanAccessPeer(&can, d, p);
+            if (can) {
+                hipError_t pe = hipDeviceEnablePeerAccess(p, 0);
+                if (pe != hipSuccess && pe != hipErrorPeerAccessAlreadyEnabled) return int(pe);
+                (void)hipGetLastError();
+            }
+        }
+        // Each dst needs one receive buffer per peer for the concurrent phase.
+        if ((e = hipMalloc(&src[d], bytes)) != hipSuccess) return int(e);
+        if ((e = hipMalloc(&dst[d], bytes * size_t(n > 1 ? n - 1 : 1))) != hipSuccess) return int(e);
+        if ((e = hipMalloc(&err[d], sizeof(unsigned long long))) != hipSuccess) return int(e);
+        if ((e = (hipError_t)netop_fill_pattern(src[d], bytes / 2, 1234u, d, nullptr)) != hipSuccess) return int(e);
+        if ((e = hipDeviceSynchronize()) != hipSuccess) return int(e);
+    }
+
+    // Phase 1: single links.
+    for (int d = 0; d < n; ++d) {
+        hipSetDevice(d);
+        hipStream_t s;
+        hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+        hipEvent_t t0, t1;
+        hipEventCreate(&t0);
+        hipEventCreate(&t1);
+        for (int p = 0; p < n; ++p) {
+            if (p == d && n > 1) {
+                bw_single[d * n + p] = 0;
+                continue;
+            }
+            netop_copy(src[p], dst[d], bytes, s);  // warm-up
+            hipEventRecord(t0, s);
+            for (int it = 0; it < iters; ++it) netop_copy(src[p], dst[d], bytes, s);
+            hipEventRecord(t1, s);
+            if ((e = hipEventSynchronize(t1)) != hipSuccess) return int(e);
+            float ms = 0;
+            hipEventElapsedTime(&ms, t0, t1);
+            bw_single[d * n + p] = ms > 0 ? double(bytes) * iters / (double(ms) * 1e-3) / 1e9 : 0;
+        }
+        hipEventDestroy(t0);
+        hipEventDestroy(t1);
+        hipStreamDestroy(s);
+    }
+
+    // Phase 2: all peers concurrently into distinct buffers, then verify each buffer.
+    for (int d = 0; d < n; ++d) {
+        hipSetDevice(d);
+        int peers = n > 1 ? n - 1 : 1;
+        hipStream_t ss[64];
+        for (int k = 0; k < peers; ++k) hipStreamCreateWithFlags(&ss[k], hipStreamNonBlocking);
+        hipEvent_t t0, t1;
+        hipEventCreate(&t0);
+        hipEventCreate(&t1);
+        hipEventRecord(t0, nullptr);
+        for (int k = 0; k < peers; ++k) hipStreamWaitEvent(ss[k], t0, 0);
+        for (int it = 0; it < iters; ++it) {
+            int k = 0;
+            for (int p = 0; p < n; ++p) {
+                if (p == d && n > 1) continue;
+                netop_copy(src[p], static_cast<char*>(dst[d]) + size_t(k) * bytes, bytes, ss[k]);
+                ++k;
+            }
+        }
+        for (int k = 0; k < peers; ++k) {
+            hipEvent_t done;
+            hipEventCreate(&done);
+            hipEventRecord(done, ss[k]);
+            hipStreamWaitEvent(nullptr, done, 0);
+            hipEventDestroy(done);
+        }
+        hipEventRecord(t1, nullptr);
+        if ((e = hipEventSynchronize(t1)) != hipSuccess) return int(e);
+        float ms = 0;
+        hipEventElapsedTime(&ms, t0, t1);
+        bw_all[d] = ms > 0 ? double(bytes) * iters * peers / (double(ms) * 1e-3) / 1e9 : 0;
+        // Integrity: buffer k must equal peer p's source bytes (host compare: this is a
+        // validation path, not a hot path).
+        std::vector<uint8_t> got(bytes), want(bytes);
+        int k = 0;
+        for (int p = 0; p < n; ++p) {
+            if (p == d && n > 1) continue;
+            hipMemcpy(got.data(), static_cast<char*>(dst[d]) + size_t(k) * bytes, bytes, hipMemcpyDeviceToHost);
+            hipSetDevice(p);
+            hipMemcpy(want.data(), src[p], bytes, hipMemcpyDeviceToHost);
+            hipSetDevice(d);
+            unsigned long long h = 0;
+            for (size_t i = 0; i < bytes; ++i) h += got[i] != want[i];
+            *total_errors += h;
+            ++k;
+        }
+        hipEventDestroy(t0);
+        hipEventDestroy(t1);
+        for (int k2 = 0; k2 < peers; ++k2) hipStreamDestroy(ss[k2]);
+    }
+    for (int d = 0; d < n; ++d) {
+        hipSetDevice(d);
+        hipFree(src[d]);
+        hipFree(dst[d]);
+        hipFree(err[d]);
+    }
+    return int(hipSuccess);
+}
+
+}  // extern "C"

@@ -1,0 +1,132 @@
+// The node agent ("discover") state machine.
+//
+// Reference: cmd/discover/main.go:cmdRun (:161-259) — sanitize, pre-cleanup, discover,
+// [unmanage from NM], links up, MTU, flush IPv4, [L3: LLDP -> /30 + routes -> artifacts],
+// readiness label, idle until SIGTERM, post-cleanup.
+//
+// MI355X-first differences (each documented at its call site):
+//   * LLDP frames are consumed from one epoll loop and each NIC is configured the moment
+//     its frame arrives (Config::pipeline), instead of a barrier over all NICs
+//     (main.go:84-122);
+//   * scale-out NICs are found by PCIe affinity to amdgpu functions (topology.hpp);
+//   * RCCL artifacts replace gaudinet.json; RoCE v2 GID indices are resolved per NIC;
+//   * optional xGMI-mesh verification gates the readiness label;
+//   * in L3 mode zero LLDP peers is an error instead of a silently-published label
+//     (main.go:212,239-246) unless Config::label_without_peers (compat) is set.
+#pragma once
+
+#include <cstdint>
+#include <functional>
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "netop/artifacts.hpp"
+#include "netop/l3.hpp"
+#include "netop/lldp.hpp"
+#include "netop/netlink.hpp"
+#include "netop/nm.hpp"
+#include "netop/packet.hpp"
+#include "netop/state.hpp"
+#include "netop/topology.hpp"
+
+namespace netop::agent {
+
+struct Config {
+    // Reference flags (cmd/discover/main.go:281-298) with the same defaults.
+    std::string mode = "L3";
+    bool configure = false;
+    bool disable_nm = false;
+    std::string interfaces;              // comma separated extra interfaces
+    int64_t wait_ns = 30LL * 1000000000; // --wait
+    std::string rccl_net;                // --rccl-net (alias --gaudinet)
+    bool keep_running = false;
+    std::string networkd;                // --systemd-networkd
+    int mtu = 1500;
+
+    // MI355X additions.
+    topo::DiscoveryOptions discovery;
+    std::string sysfs_root;              // "" = $SYSFS_ROOT or /sys/
+    l3::TokenPolicy token_policy = l3::TokenPolicy::CompatThenLast;
+    bool lldp_promisc = false;
+    bool pipeline = true;
+    bool label_without_peers = false;
+    artifacts::Labels labels;
+    std::string rccl_env;                // --rccl-env
+    std::string status_file;             // --status-file (JSON)
+    std::string nm_keyfile_dir;          // --nm-keyfile-dir
+    int xgmi_expect_links = -1;          // -1 off; 0 = full mesh among discovered GPUs; N = exact pairs
+    int64_t link_wait_ns = 3LL * 1000000000;  // netlink echo wait (network.go:251)
+};
+
+// Sanitises in place (MTU clamp to [1500, 9000], mode upper-cased); throws on a bad mode.
+void sanitize(Config& c);
+
+// Source of LLDP frames (AF_PACKET in production, scripted in tests).
+class LldpSource {
+   public:
+    virtual ~LldpSource() = default;
+    virtual void add(const std::string& ifname, int ifindex, const MacAddr& own_mac) = 0;
+    virtual pkt::ListenResult run(int64_t deadline,
+                                  const std::function<bool(const std::string&, const lldp::Frame&)>& on_frame,
+                                  int stop_fd) = 0;
+};
+std::unique_ptr<LldpSource> make_packet_source(bool promisc);
+
+using NmFactory = std::function<std::unique_ptr<nm::NetworkManagerIf>()>;
+
+class AgentError : public std::runtime_error {
+   public:
+    using std::runtime_error::runtime_error;
+};
+
+class Agent {
+   public:
+    Agent(Config cfg, nl::NetOps& ops, std::unique_ptr<LldpSource> lldp, NmFactory nm_factory);
+
+    // Runs the whole state machine.  `stop_fd` becomes readable on SIGTERM/SIGINT (a
+    // signalfd in production, a pipe/eventfd in tests).  Throws AgentError on fatal errors.
+    void run(int stop_fd);
+
+    const std::vector<NicState>& nics() const { return nics_; }
+    const std::map<std::string, int64_t>& phases() const { return phases_; }
+    bool ready() const { return ready_; }
+    const topo::XgmiReport& xgmi() const { return xgmi_; }
+
+    // Exposed for unit tests (reference-named helpers).
+    void interfaces_up();
+    void interfaces_restore_down();
+    void interfaces_set_mtu();
+    void remove_existing_ips();
+    bool configure_interface(NicState& n);
+    int configure_all();  // returns number configured
+
+   private:
+    void pre_cleanups();
+    void post_cleanups();
+    std::vector<std::string> collect_interfaces();
+    void get_network_configs(const std::vector<std::string>& names);
+    void detect_lldp(int stop_fd);
+    void on_lldp(NicState& n, const lldp::Frame& f);
+    void add_route(NicState& n, int mask);
+    void write_artifacts();
+    void check_xgmi();
+    void log_results();
+    void mark(const std::string& phase);
+    void write_status();
+
+    Config cfg_;
+    nl::NetOps& ops_;
+    std::unique_ptr<LldpSource> lldp_;
+    NmFactory nm_factory_;
+    std::vector<NicState> nics_;
+    topo::DiscoveryResult disc_;
+    topo::XgmiReport xgmi_;
+    std::map<std::string, int64_t> phases_;
+    int64_t t0_ = 0, t_last_ = 0;
+    bool ready_ = false;
+    bool aborted_ = false;
+};
+
+}  // namespace netop::agent

@@ -1,0 +1,140 @@
+// Raw rtnetlink client (NETLINK_ROUTE) — no libnl, no external deps.
+//
+// Replaces the reference's vishvananda/netlink function table
+// (reference cmd/discover/network.go:41-63).  `NetOps` is the injectable
+// interface (the reference swaps `networkLink.*` function pointers in tests,
+// network_test.go:276,364-366); `Rtnl` is the real implementation over one
+// ACKed request socket, and `LinkWatcher` a separate RTNLGRP_LINK multicast
+// socket used to wait for link-state echoes (network.go:242-283).
+#pragma once
+
+#include <linux/rtnetlink.h>
+
+#include <cstdint>
+#include <functional>
+#include <memory>
+#include <optional>
+#include <string>
+#include <vector>
+
+#include "netop/common.hpp"
+
+namespace netop::nl {
+
+struct LinkInfo {
+    int index = 0;
+    std::string name;
+    unsigned flags = 0;  // IFF_*
+    int mtu = 0;
+    MacAddr mac;
+    uint8_t operstate = 0;  // IF_OPER_*
+    std::string kind;       // IFLA_INFO_KIND ("veth", ...) when present
+    int master = 0;
+    bool up() const;
+    bool lower_up() const;
+    std::string flags_str() const;  // "up|broadcast|multicast" (Go net.Flags.String() style)
+    std::string operstate_str() const;
+};
+
+struct AddrInfo {
+    int ifindex = 0;
+    int family = 0;
+    Ipv4 address;  // IFA_ADDRESS (peer for p2p links)
+    Ipv4 local;    // IFA_LOCAL
+    int prefixlen = 0;
+    uint8_t scope = 0;
+    std::string label;
+    Ipv4Prefix prefix() const { return Ipv4Prefix{local, prefixlen}; }
+};
+
+struct RouteSpec {
+    int ifindex = 0;
+    Ipv4Prefix dst{};
+    std::optional<Ipv4> gateway;
+    std::optional<Ipv4> prefsrc;
+    uint8_t scope = RT_SCOPE_UNIVERSE;
+    uint8_t protocol = RTPROT_BOOT;  // vishvananda/netlink's NewRtMsg default
+    uint8_t table = RT_TABLE_MAIN;
+    uint8_t type = RTN_UNICAST;
+    uint32_t priority = 0;
+    std::string str() const;
+};
+
+using RouteInfo = RouteSpec;
+
+struct LinkEvent {
+    bool deleted = false;
+    LinkInfo link;
+};
+
+class LinkWatcher {
+   public:
+    virtual ~LinkWatcher() = default;
+    // Blocks until at least one event or the absolute CLOCK_MONOTONIC deadline; returns
+    // all events read (possibly empty on timeout).
+    virtual std::vector<LinkEvent> wait(int64_t deadline_mono_ns) = 0;
+};
+
+// The injectable operation table.  Every method throws SysError on failure.
+class NetOps {
+   public:
+    virtual ~NetOps() = default;
+    virtual LinkInfo link_by_name(const std::string& name) = 0;
+    virtual std::vector<AddrInfo> addr_list(int ifindex, int family) = 0;  // family: AF_INET / AF_UNSPEC
+    virtual void addr_add(int ifindex, const Ipv4Prefix& addr) = 0;
+    virtual void addr_del(const AddrInfo& addr) = 0;
+    virtual void route_append(const RouteSpec& r) = 0;
+    virtual void link_set_up(int ifindex) = 0;
+    virtual void link_set_down(int ifindex) = 0;
+    virtual void link_set_mtu(int ifindex, int mtu) = 0;
+    virtual std::unique_ptr<LinkWatcher> subscribe_links() = 0;
+};
+
+class Rtnl final : public NetOps {
+   public:
+    Rtnl();
+    ~Rtnl() override;
+    Rtnl(const Rtnl&) = delete;
+    Rtnl& operator=(const Rtnl&) = delete;
+
+    LinkInfo link_by_name(const std::string& name) override;
+    std::vector<AddrInfo> addr_list(int ifindex, int family) override;
+    void addr_add(int ifindex, const Ipv4Prefix& addr) override;
+    void addr_del(const AddrInfo& addr) override;
+    void route_append(const RouteSpec& r) override;
+    void link_set_up(int ifindex) override;
+    void link_set_down(int ifindex) override;
+    void link_set_mtu(int ifindex, int mtu) override;
+    std::unique_ptr<LinkWatcher> subscribe_links() override;
+
+    // Extra operations (harness / diagnostics; not part of the injectable table).
+    LinkInfo link_by_index(int ifindex);
+    std::vector<LinkInfo> link_list();
+    std::vector<RouteInfo> route_list(uint8_t table = RT_TABLE_MAIN);
+    void route_del(const RouteSpec& r);
+    void veth_add(const std::string& name, const std::string& peer);
+    void link_del(int ifindex);
+    void link_set_netns_fd(int ifindex, int netns_fd);
+    void link_set_netns_pid(int ifindex, int pid);
+    void link_set_mac(int ifindex, const MacAddr& mac);
+    void link_set_name(int ifindex, const std::string& name);
+
+    // Number of request round trips done on this socket (observability / bench).
+    uint64_t round_trips() const { return rtts_; }
+
+   private:
+    struct Msg;
+    void transact(Msg& m, const std::function<void(const nlmsghdr*)>& on_reply);
+    void dump(Msg& m, const std::function<void(const nlmsghdr*)>& on_item);
+    void set_link(int ifindex, unsigned flags, unsigned change, const std::function<void(Msg&)>& attrs);
+
+    int fd_ = -1;
+    uint32_t seq_ = 1;
+    uint32_t portid_ = 0;
+    uint64_t rtts_ = 0;
+};
+
+// Parses an RTM_NEWLINK/RTM_DELLINK payload.
+LinkInfo parse_link(const nlmsghdr* h);
+
+}  // namespace netop::nl

@@ -1,0 +1,49 @@
+// Per-interface state carried through the agent's pipeline.
+//
+// Mirrors the reference's networkConfiguration (cmd/discover/network.go:65-74) and adds
+// the MI355X-specific fields: the paired GPU, the RDMA device / RoCE v2 GID index and
+// per-NIC timestamps used by the node-ready latency measurement.
+#pragma once
+
+#include <cstdint>
+#include <optional>
+#include <string>
+
+#include "netop/common.hpp"
+#include "netop/l3.hpp"
+#include "netop/netlink.hpp"
+
+namespace netop {
+
+struct NicState {
+    std::string ifname;
+    nl::LinkInfo link;
+    unsigned orig_flags = 0;
+    bool expect_response = false;
+
+    // LLDP
+    bool lldp_seen = false;
+    std::string port_description;
+    std::optional<MacAddr> peer_mac;
+    std::string peer_system_name;
+    std::string peer_port_id;
+
+    // L3
+    std::optional<l3::P2pAddressing> addr;
+    std::string addr_error;
+    bool configured = false;
+    std::string config_error;
+
+    // Topology
+    int gpu_index = -1;
+    std::string gpu_bdf;
+    std::string rdma_dev;
+    int rdma_port = 1;
+    std::optional<int> gid_index;
+
+    // Timing (CLOCK_MONOTONIC ns; 0 = never)
+    int64_t t_lldp = 0;
+    int64_t t_configured = 0;
+};
+
+}  // namespace netop

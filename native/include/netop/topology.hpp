@@ -1,0 +1,128 @@
+// Node topology discovery from sysfs: amdgpu GPUs, scale-out NICs, GPU<->NIC PCIe
+// affinity, RDMA devices / RoCE GID indices, and the xGMI mesh from the KFD topology.
+//
+// Reference: the Gaudi agent globs netdevs *under* the accelerator's PCI function
+// ($SYSFS_ROOT/bus/pci/drivers/habanalabs/????:??:??.?/net/*, cmd/discover/network.go:84-119)
+// because Gaudi NICs are integrated.  MI355X has no integrated NICs: each OAM GPU sits
+// behind a PCIe switch together with a discrete RoCE NIC, so the scale-out NICs are the
+// netdevs that share a PCIe switch with an amdgpu function.  The reference-compatible
+// "netdevs under the accelerator function" mode is kept (DiscoveryMode::Accel) and the
+// SYSFS_ROOT override is preserved for fake-sysfs tests.
+#pragma once
+
+#include <cstdint>
+#include <map>
+#include <optional>
+#include <string>
+#include <vector>
+
+#include "netop/common.hpp"
+
+namespace netop::topo {
+
+std::string sysfs_root();  // $SYSFS_ROOT or "/sys/"
+
+struct PciDev {
+    std::string bdf;                 // "0000:0a:00.0"
+    std::string path;                // resolved path, e.g. <root>/devices/pci0000:00/.../0000:0a:00.0
+    std::vector<std::string> chain;  // path components from the host bridge ("pci0000:00") down to bdf
+    std::string driver;
+    uint32_t vendor = 0, device = 0, pci_class = 0;
+    int numa = -1;
+};
+
+struct Gpu {
+    int index = 0;  // ordinal (sorted by BDF), matches HIP/RCCL enumeration on a standard node
+    PciDev pci;
+};
+
+struct Nic {
+    std::string ifname;
+    PciDev pci;
+    MacAddr mac;
+    std::string rdma_dev;  // e.g. "mlx5_3" (empty when not an RDMA NIC)
+    int rdma_port = 1;
+};
+
+// NCCL/RCCL path types, ordered best-first.
+enum class PathType { PIX = 0, PXB = 1, PHB = 2, NODE = 3, SYS = 4 };
+const char* to_string(PathType p);
+
+struct GpuNicPair {
+    int gpu = -1;  // index into gpus
+    int nic = -1;  // index into nics
+    PathType path = PathType::SYS;
+    int common_depth = 0;
+};
+
+enum class DiscoveryMode { Affine, Accel, None };
+std::optional<DiscoveryMode> parse_discovery_mode(std::string_view s);
+
+struct DiscoveryOptions {
+    DiscoveryMode mode = DiscoveryMode::Affine;
+    std::string accel_driver = "amdgpu";
+    // Empty = any PCI network driver.
+    std::vector<std::string> nic_drivers{"mlx5_core", "bnxt_en", "ionic", "ice", "irdma", "i40e", "qede", "cxgb4"};
+    PathType max_path = PathType::PXB;  // NICs farther than this from every GPU are not scale-out NICs
+};
+
+std::optional<PciDev> read_pci_dev(const std::string& root, const std::string& device_path);
+std::vector<Gpu> discover_gpus(const std::string& root, const std::string& driver = "amdgpu");
+std::vector<Nic> discover_pci_nics(const std::string& root, const std::vector<std::string>& drivers);
+PathType path_between(const PciDev& a, const PciDev& b, int* common_depth = nullptr);
+// Greedy best-first unique pairing: each GPU gets the closest free NIC within max_path.
+std::vector<GpuNicPair> pair_gpus_nics(const std::vector<Gpu>& gpus, const std::vector<Nic>& nics, PathType max_path);
+
+// Reference-compatible: netdev names found under the accelerator driver's PCI functions.
+std::vector<std::string> accel_netdevs(const std::string& root, const std::string& driver);
+
+struct DiscoveryResult {
+    std::vector<Gpu> gpus;
+    std::vector<Nic> nics;            // every candidate PCI NIC seen
+    std::vector<GpuNicPair> pairs;    // GPU -> NIC assignment (Affine mode)
+    std::vector<std::string> ifnames; // selected scale-out interfaces, in GPU order
+};
+DiscoveryResult discover(const DiscoveryOptions& opt, const std::string& root = sysfs_root());
+
+// RoCE v2 GID index on (rdma_dev, port) whose GID is the IPv4-mapped address `ip`.
+std::optional<int> find_rocev2_gid_index(const std::string& root, const std::string& rdma_dev, int port, Ipv4 ip);
+
+// ---------------------------------------------------------------------------
+// xGMI mesh from the KFD topology (/sys/class/kfd/kfd/topology/nodes/*)
+// ---------------------------------------------------------------------------
+constexpr int kIoLinkTypeXgmi = 11;  // HSA_IOLINK_TYPE_XGMI (hsakmttypes.h)
+constexpr int kIoLinkTypePcie = 2;
+
+struct KfdNode {
+    int node = -1;
+    uint32_t gpu_id = 0;
+    uint32_t simd_count = 0;
+    uint32_t vendor_id = 0, device_id = 0;
+    uint32_t location_id = 0, domain = 0;
+    uint64_t hive_id = 0;
+    uint32_t num_xcc = 0;
+    std::string bdf() const;  // from domain + location_id
+    bool is_gpu() const { return simd_count > 0; }
+};
+
+struct KfdLink {
+    int from = -1, to = -1, type = 0, weight = 0;
+    uint32_t min_bw_mbs = 0, max_bw_mbs = 0;
+};
+
+struct XgmiReport {
+    std::vector<KfdNode> gpus;              // GPU nodes, sorted by BDF
+    std::vector<KfdLink> links;             // every xGMI link seen (either direction)
+    int pairs_expected = 0;                 // n*(n-1)/2 among GPUs of the same hive
+    int pairs_connected = 0;                // unordered GPU pairs with an xGMI link
+    std::vector<std::pair<std::string, std::string>> missing;  // BDF pairs without a link
+    uint64_t min_link_bw_mbs = 0;           // slowest advertised xGMI link
+    bool full_mesh() const { return pairs_connected == pairs_expected; }
+    // Per-GPU aggregate advertised xGMI bandwidth (MB/s, one direction) — the busbw ceiling
+    // input for the all-reduce validation.
+    uint64_t per_gpu_bw_mbs() const;
+};
+
+XgmiReport read_xgmi(const std::string& root = sysfs_root());
+
+}  // namespace netop::topo

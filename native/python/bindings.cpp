@@ -1,0 +1,229 @@
+// pybind11 module `_netop_native`: exposes the agent's native building blocks to Python
+// for the netns integration harness, the fake-sysfs topology tests and property-based
+// (hypothesis) fuzzing of the LLDP codec / Port-Description parser.
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+#include <sys/socket.h>
+
+#include "netop/artifacts.hpp"
+#include "netop/dbus.hpp"
+#include "netop/l3.hpp"
+#include "netop/lldp.hpp"
+#include "netop/netlink.hpp"
+#include "netop/packet.hpp"
+#include "netop/topology.hpp"
+
+namespace py = pybind11;
+using namespace netop;
+
+static MacAddr mac_of(const std::string& s) {
+    auto m = MacAddr::parse(s);
+    if (!m) throw py::value_error("bad MAC address '" + s + "'");
+    return *m;
+}
+
+static py::dict link_dict(const nl::LinkInfo& l) {
+    py::dict d;
+    d["index"] = l.index;
+    d["name"] = l.name;
+    d["flags"] = l.flags;
+    d["up"] = l.up();
+    d["mtu"] = l.mtu;
+    d["mac"] = l.mac.str();
+    d["operstate"] = l.operstate_str();
+    d["kind"] = l.kind;
+    return d;
+}
+
+static py::dict frame_dict(const lldp::Frame& f) {
+    py::dict d;
+    d["dst"] = f.dst.str();
+    d["src"] = f.src.str();
+    d["chassis_subtype"] = f.chassis_subtype;
+    d["chassis_id"] = py::bytes(f.chassis_id);
+    d["port_subtype"] = f.port_subtype;
+    d["port_id"] = py::bytes(f.port_id);
+    d["ttl"] = f.ttl;
+    d["port_description"] = f.port_description ? py::object(py::str(*f.port_description)) : py::none();
+    d["system_name"] = f.system_name ? py::object(py::str(*f.system_name)) : py::none();
+    d["system_description"] = f.system_description ? py::object(py::str(*f.system_description)) : py::none();
+    auto pm = f.peer_mac();
+    d["peer_mac"] = pm ? py::object(py::str(pm->str())) : py::none();
+    d["vlan"] = f.vlan ? py::object(py::int_(*f.vlan)) : py::none();
+    d["management"] = py::int_(f.management.size());
+    d["org"] = py::int_(f.org.size());
+    return d;
+}
+
+PYBIND11_MODULE(_netop_native, m) {
+    m.doc() = "Native building blocks of the AMD MI355X network operator agent";
+    m.attr("__version__") = NETOP_VERSION;
+
+    py::register_exception<SysError>(m, "SysError", PyExc_OSError);
+
+    // ---- LLDP -------------------------------------------------------------
+    m.def("lldp_switch_frame", [](const std::string& mac, const std::string& sysname, const std::string& port,
+                                  const std::string& desc, int ttl, py::object vlan) {
+        auto f = lldp::make_switch_frame(mac_of(mac), sysname, port, desc, uint16_t(ttl));
+        if (!vlan.is_none()) f.vlan = uint16_t(vlan.cast<int>());
+        auto b = lldp::encode(f);
+        return py::bytes(reinterpret_cast<const char*>(b.data()), b.size());
+    }, py::arg("mac"), py::arg("system_name"), py::arg("port"), py::arg("port_description"), py::arg("ttl") = 120,
+       py::arg("vlan") = py::none());
+    m.def("lldp_encode", [](const std::string& src, int chassis_subtype, const py::bytes& chassis_id, int port_subtype,
+                            const py::bytes& port_id, int ttl, py::object port_desc, py::object sysname) {
+        lldp::Frame f;
+        f.src = mac_of(src);
+        f.chassis_subtype = uint8_t(chassis_subtype);
+        f.chassis_id = std::string(chassis_id);
+        f.port_subtype = uint8_t(port_subtype);
+        f.port_id = std::string(port_id);
+        f.ttl = uint16_t(ttl);
+        if (!port_desc.is_none()) f.port_description = port_desc.cast<std::string>();
+        if (!sysname.is_none()) f.system_name = sysname.cast<std::string>();
+        auto b = lldp::encode(f);
+        return py::bytes(reinterpret_cast<const char*>(b.data()), b.size());
+    }, py::arg("src"), py::arg("chassis_subtype"), py::arg("chassis_id"), py::arg("port_subtype"), py::arg("port_id"),
+       py::arg("ttl") = 120, py::arg("port_description") = py::none(), py::arg("system_name") = py::none());
+    m.def("lldp_decode", [](const py::bytes& data) -> py::object {
+        std::string s(data);
+        lldp::DecodeError e;
+        auto f = lldp::decode(reinterpret_cast<const uint8_t*>(s.data()), s.size(), &e);
+        if (!f) throw py::value_error(lldp::to_string(e));
+        return frame_dict(*f);
+    });
+
+    // ---- L3 ---------------------------------------------------------------
+    m.def("parse_port_description", [](const std::string& desc, const std::string& policy) -> py::object {
+        auto p = l3::parse_token_policy(policy);
+        if (!p) throw py::value_error("bad token policy");
+        std::string err;
+        auto a = l3::parse_port_description(desc, *p, &err);
+        if (!a) throw py::value_error(err);
+        py::dict d;
+        d["peer"] = a->peer.str();
+        d["local"] = a->local.str();
+        d["prefix"] = a->prefix;
+        d["p2p_network"] = a->p2p_network().str();
+        d["routed_network"] = a->routed_network().str();
+        return d;
+    }, py::arg("description"), py::arg("policy") = "compat-then-last");
+
+    // ---- rtnetlink ----------------------------------------------------------
+    py::class_<nl::Rtnl>(m, "Rtnl")
+        .def(py::init<>())
+        .def("link_by_name", [](nl::Rtnl& r, const std::string& n) { return link_dict(r.link_by_name(n)); })
+        .def("link_list", [](nl::Rtnl& r) {
+            py::list l;
+            for (auto& x : r.link_list()) l.append(link_dict(x));
+            return l;
+        })
+        .def("addr_list", [](nl::Rtnl& r, int ifindex) {
+            py::list l;
+            for (auto& a : r.addr_list(ifindex, AF_INET)) l.append(a.prefix().str());
+            return l;
+        }, py::arg("ifindex") = 0)
+        .def("addr_add", [](nl::Rtnl& r, int ifindex, const std::string& cidr) {
+            auto p = Ipv4Prefix::parse(cidr);
+            if (!p) throw py::value_error("bad CIDR");
+            r.addr_add(ifindex, *p);
+        })
+        .def("route_list", [](nl::Rtnl& r) {
+            py::list l;
+            for (auto& x : r.route_list()) {
+                py::dict d;
+                d["dst"] = x.dst.masked().str();
+                d["gateway"] = x.gateway ? py::object(py::str(x.gateway->str())) : py::none();
+                d["prefsrc"] = x.prefsrc ? py::object(py::str(x.prefsrc->str())) : py::none();
+                d["ifindex"] = x.ifindex;
+                d["protocol"] = x.protocol;
+                d["scope"] = x.scope;
+                l.append(d);
+            }
+            return l;
+        })
+        .def("link_set_up", &nl::Rtnl::link_set_up)
+        .def("link_set_down", &nl::Rtnl::link_set_down)
+        .def("link_set_mtu", &nl::Rtnl::link_set_mtu)
+        .def("link_set_mac", [](nl::Rtnl& r, int idx, const std::string& mac) { r.link_set_mac(idx, mac_of(mac)); })
+        .def("veth_add", &nl::Rtnl::veth_add)
+        .def("link_del", &nl::Rtnl::link_del)
+        .def("link_set_netns_pid", &nl::Rtnl::link_set_netns_pid)
+        .def("link_set_netns_fd", &nl::Rtnl::link_set_netns_fd)
+        .def("round_trips", &nl::Rtnl::round_trips);
+
+    m.def("lldp_send", [](const std::string& ifname, const py::bytes& frame) {
+        nl::Rtnl r;
+        auto l = r.link_by_name(ifname);
+        pkt::LldpSocket s(ifname, l.index, l.mac, false);
+        std::string b(frame);
+        s.send(std::vector<uint8_t>(b.begin(), b.end()));
+    });
+
+    // ---- topology -----------------------------------------------------------
+    m.def("discover", [](const std::string& root, const std::string& mode, py::object drivers, const std::string& accel) {
+        topo::DiscoveryOptions o;
+        auto md = topo::parse_discovery_mode(mode);
+        if (!md) throw py::value_error("bad mode");
+        o.mode = *md;
+        o.accel_driver = accel;
+        if (!drivers.is_none()) o.nic_drivers = drivers.cast<std::vector<std::string>>();
+        auto r = topo::discover(o, root);
+        py::dict d;
+        py::list gpus, nics, pairs;
+        for (auto& g : r.gpus) {
+            py::dict x;
+            x["index"] = g.index;
+            x["bdf"] = g.pci.bdf;
+            x["device"] = g.pci.device;
+            x["numa"] = g.pci.numa;
+            gpus.append(x);
+        }
+        for (auto& n : r.nics) {
+            py::dict x;
+            x["ifname"] = n.ifname;
+            x["bdf"] = n.pci.bdf;
+            x["driver"] = n.pci.driver;
+            x["rdma_dev"] = n.rdma_dev;
+            x["mac"] = n.mac.str();
+            nics.append(x);
+        }
+        for (auto& p : r.pairs) {
+            py::dict x;
+            x["gpu"] = r.gpus[size_t(p.gpu)].pci.bdf;
+            x["nic"] = r.nics[size_t(p.nic)].ifname;
+            x["path"] = topo::to_string(p.path);
+            x["common_depth"] = p.common_depth;
+            pairs.append(x);
+        }
+        d["gpus"] = gpus;
+        d["nics"] = nics;
+        d["pairs"] = pairs;
+        d["ifnames"] = r.ifnames;
+        return d;
+    }, py::arg("root"), py::arg("mode") = "affine", py::arg("drivers") = py::none(), py::arg("accel_driver") = "amdgpu");
+    m.def("read_xgmi", [](const std::string& root) {
+        auto x = topo::read_xgmi(root);
+        py::dict d;
+        py::list g;
+        for (auto& n : x.gpus) g.append(n.bdf());
+        d["gpus"] = g;
+        d["links"] = x.links.size();
+        d["pairs_expected"] = x.pairs_expected;
+        d["pairs_connected"] = x.pairs_connected;
+        d["full_mesh"] = x.full_mesh();
+        d["min_link_bw_mbs"] = x.min_link_bw_mbs;
+        d["per_gpu_bw_mbs"] = x.per_gpu_bw_mbs();
+        py::list miss;
+        for (auto& [a, b] : x.missing) miss.append(py::make_tuple(a, b));
+        d["missing"] = miss;
+        return d;
+    });
+    m.def("find_rocev2_gid_index", [](const std::string& root, const std::string& dev, int port, const std::string& ip) -> py::object {
+        auto a = Ipv4::parse(ip);
+        if (!a) throw py::value_error("bad IPv4");
+        auto r = topo::find_rocev2_gid_index(root, dev, port, *a);
+        return r ? py::object(py::int_(*r)) : py::none();
+    });
+
+}

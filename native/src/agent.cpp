@@ -1,0 +1,550 @@
+#include "netop/agent.hpp"
+
+#include <errno.h>
+#include <linux/if.h>
+#include <poll.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cstring>
+
+#include "netop/log.hpp"
+
+namespace netop::agent {
+
+void sanitize(Config& c) {
+    if (c.mtu < 1500) {
+        NLOG_I("Forcing MTU value 1500 (old %d)", c.mtu);
+        c.mtu = 1500;
+    } else if (c.mtu > 9000) {
+        NLOG_I("Limiting MTU value 9000 (old %d)", c.mtu);
+        c.mtu = 9000;
+    }
+    std::string m = to_upper(c.mode);
+    if (m != "L2" && m != "L3") throw AgentError("Invalid mode '" + c.mode + "'");
+    c.mode = m;
+}
+
+// ---------------------------------------------------------------------------
+// LLDP source over AF_PACKET
+// ---------------------------------------------------------------------------
+namespace {
+class PacketSource final : public LldpSource {
+   public:
+    explicit PacketSource(bool promisc) : promisc_(promisc) {}
+    void add(const std::string& ifname, int ifindex, const MacAddr& own) override {
+        listener_.add(ifname, ifindex, own, promisc_);
+    }
+    pkt::ListenResult run(int64_t deadline, const std::function<bool(const std::string&, const lldp::Frame&)>& cb,
+                          int stop_fd) override {
+        auto r = listener_.run(deadline, cb, stop_fd);
+        auto& s = listener_.stats();
+        NLOG_V(2, "LLDP listener: %llu frames, %llu own, %llu malformed, %llu wakeups", (unsigned long long)s.frames,
+               (unsigned long long)s.own, (unsigned long long)s.malformed, (unsigned long long)s.wakeups);
+        return r;
+    }
+
+   private:
+    bool promisc_;
+    pkt::LldpListener listener_;
+};
+
+bool fd_readable(int fd) {
+    if (fd < 0) return false;
+    pollfd p{fd, POLLIN, 0};
+    return ::poll(&p, 1, 0) > 0;
+}
+}  // namespace
+
+std::unique_ptr<LldpSource> make_packet_source(bool promisc) { return std::make_unique<PacketSource>(promisc); }
+
+// ---------------------------------------------------------------------------
+// Agent
+// ---------------------------------------------------------------------------
+Agent::Agent(Config cfg, nl::NetOps& ops, std::unique_ptr<LldpSource> lldp, NmFactory nm_factory)
+    : cfg_(std::move(cfg)), ops_(ops), lldp_(std::move(lldp)), nm_factory_(std::move(nm_factory)) {}
+
+void Agent::mark(const std::string& phase) {
+    int64_t now = mono_ns();
+    phases_[phase] = now - t_last_;
+    t_last_ = now;
+}
+
+void Agent::pre_cleanups() {
+    // Stale label from a previous (crashed) run: the node is not ready until we say so.
+    if (path_exists(cfg_.labels.path())) {
+        NLOG_I("NFD label file already exists, removing it...");
+        if (!artifacts::remove_labels(cfg_.labels)) NLOG_W("Failed to remove NFD label file: %s", std::strerror(errno));
+    }
+    if (!cfg_.networkd.empty()) {
+        try {
+            mkdir_p(cfg_.networkd);
+        } catch (const std::exception& e) {
+            throw AgentError(std::string("Failed to pre-cleanup: Cannot create systemd-networkd directory: ") + e.what());
+        }
+        NLOG_I("Created systemd-networkd directory %s", cfg_.networkd.c_str());
+    }
+}
+
+void Agent::post_cleanups() {
+    NLOG_I("Clean up before exiting...");
+    if (!artifacts::remove_labels(cfg_.labels)) NLOG_W("Failed to remove NFD label file: %s", std::strerror(errno));
+    NLOG_I("Restoring interfaces to original state...");
+    try {
+        remove_existing_ips();
+    } catch (const std::exception& e) {
+        NLOG_W("Failed to remove any existing IPs from interfaces: %s", e.what());
+    }
+    try {
+        interfaces_restore_down();
+    } catch (const std::exception& e) {
+        NLOG_W("Failed to restore interfaces to original state: %s", e.what());
+    }
+}
+
+std::vector<std::string> Agent::collect_interfaces() {
+    std::string root = cfg_.sysfs_root.empty() ? topo::sysfs_root() : cfg_.sysfs_root;
+    disc_ = topo::discover(cfg_.discovery, root);
+    std::vector<std::string> names = disc_.ifnames;
+    for (auto& p : disc_.pairs) {
+        const auto& g = disc_.gpus[size_t(p.gpu)];
+        const auto& n = disc_.nics[size_t(p.nic)];
+        NLOG_I("GPU %d (%s) <-> NIC %s (%s, %s, path %s)", g.index, g.pci.bdf.c_str(), n.ifname.c_str(), n.pci.bdf.c_str(),
+               n.rdma_dev.empty() ? "no rdma" : n.rdma_dev.c_str(), topo::to_string(p.path));
+    }
+    if (!cfg_.interfaces.empty()) {
+        for (auto& i : split(cfg_.interfaces, ',')) {
+            auto t = trim(i);
+            if (t.empty()) continue;
+            if (std::find(names.begin(), names.end(), t) == names.end()) names.push_back(t);  // dedupe
+        }
+    }
+    return names;
+}
+
+void Agent::get_network_configs(const std::vector<std::string>& names) {
+    nics_.clear();
+    for (auto& name : names) {
+        NicState n;
+        n.ifname = name;
+        try {
+            n.link = ops_.link_by_name(name);
+        } catch (const std::exception& e) {
+            NLOG_W("Link '%s' not found: %s", name.c_str(), e.what());
+            continue;
+        }
+        n.orig_flags = n.link.flags;
+        for (auto& p : disc_.pairs) {
+            const auto& nic = disc_.nics[size_t(p.nic)];
+            if (nic.ifname != name) continue;
+            n.gpu_index = disc_.gpus[size_t(p.gpu)].index;
+            n.gpu_bdf = disc_.gpus[size_t(p.gpu)].pci.bdf;
+            n.rdma_dev = nic.rdma_dev;
+            n.rdma_port = nic.rdma_port;
+        }
+        nics_.push_back(std::move(n));
+    }
+}
+
+void Agent::interfaces_up() {
+    auto watcher = ops_.subscribe_links();
+    for (auto& n : nics_) {
+        n.expect_response = false;
+        if (n.link.up()) continue;
+        try {
+            ops_.link_set_up(n.link.index);
+            n.expect_response = true;
+        } catch (const std::exception& e) {
+            NLOG_W("Cannot set link '%s' up: %s", n.ifname.c_str(), e.what());
+        }
+    }
+    // Wait for the RTM_NEWLINK echoes (network.go:242-257); a timeout is not fatal.
+    int64_t deadline = mono_ns() + cfg_.link_wait_ns;
+    auto pending = [&] {
+        return std::any_of(nics_.begin(), nics_.end(), [](const NicState& n) { return n.expect_response; });
+    };
+    while (pending()) {
+        auto evs = watcher->wait(deadline);
+        if (evs.empty() && mono_ns() >= deadline) break;
+        for (auto& ev : evs) {
+            if (ev.deleted) continue;
+            for (auto& n : nics_) {
+                if (n.link.index == ev.link.index && n.expect_response) {
+                    n.link.flags = ev.link.flags;
+                    n.link.operstate = ev.link.operstate;
+                    if (n.link.up()) n.expect_response = false;
+                }
+            }
+        }
+    }
+    for (auto& n : nics_) {
+        if (!n.expect_response) continue;
+        NLOG_W("timeout waiting for netlink reply for '%s'", n.ifname.c_str());
+        try {  // re-read: the echo may have been lost in an overrun
+            auto l = ops_.link_by_name(n.ifname);
+            n.link.flags = l.flags;
+        } catch (...) {
+        }
+        n.expect_response = false;
+    }
+}
+
+void Agent::interfaces_restore_down() {
+    std::unique_ptr<nl::LinkWatcher> watcher;
+    std::string subscribe_err;
+    try {
+        watcher = ops_.subscribe_links();
+    } catch (const std::exception& e) {
+        subscribe_err = e.what();
+    }
+    for (auto& n : nics_) {
+        n.expect_response = false;
+        if (!(n.orig_flags & IFF_UP) && n.link.up()) {
+            try {
+                ops_.link_set_down(n.link.index);
+                NLOG_I("Setting link '%s' back down", n.ifname.c_str());
+                n.expect_response = true;
+            } catch (const std::exception& e) {
+                NLOG_W("Cannot set link '%s' back down: %s", n.ifname.c_str(), e.what());
+            }
+        }
+    }
+    if (!subscribe_err.empty()) throw AgentError(subscribe_err);
+    int64_t deadline = mono_ns() + cfg_.link_wait_ns;
+    while (std::any_of(nics_.begin(), nics_.end(), [](const NicState& n) { return n.expect_response; })) {
+        auto evs = watcher->wait(deadline);
+        if (evs.empty() && mono_ns() >= deadline) break;
+        for (auto& ev : evs)
+            for (auto& n : nics_)
+                if (n.link.index == ev.link.index && n.expect_response && !(ev.link.flags & IFF_UP)) {
+                    n.link.flags = ev.link.flags;
+                    n.expect_response = false;
+                }
+    }
+    for (auto& n : nics_) {
+        if (n.expect_response) n.link.flags &= ~unsigned(IFF_UP);
+        n.expect_response = false;
+    }
+}
+
+void Agent::interfaces_set_mtu() {
+    for (auto& n : nics_) {
+        if (n.link.mtu == cfg_.mtu) continue;  // already right: skip the netlink round trip
+        try {
+            ops_.link_set_mtu(n.link.index, cfg_.mtu);
+            n.link.mtu = cfg_.mtu;
+        } catch (const std::exception& e) {
+            NLOG_W("Could not set MTU %d for interface '%s': %s", cfg_.mtu, n.ifname.c_str(), e.what());
+        }
+    }
+}
+
+void Agent::remove_existing_ips() {
+    for (auto& n : nics_) {
+        auto addrs = ops_.addr_list(n.link.index, AF_INET);
+        for (auto& a : addrs) ops_.addr_del(a);
+    }
+}
+
+void Agent::add_route(NicState& n, int mask) {
+    nl::RouteSpec r;
+    r.ifindex = n.link.index;
+    if (!n.addr) throw AgentError("interface '" + n.ifname + "' has no local address");
+    r.dst = Ipv4Prefix{n.addr->local, mask}.masked();
+    std::string desc = r.dst.str();
+    if (mask == l3::kRoutedNetworkMask) {
+        r.gateway = n.addr->peer;  // protocol left at the netlink library default (boot)
+        desc += " gateway " + n.addr->peer.str();
+    } else {
+        r.protocol = RTPROT_KERNEL;  // identical to the route the kernel adds with the address
+        r.scope = RT_SCOPE_LINK;
+        r.prefsrc = n.addr->local;
+    }
+    try {
+        ops_.route_append(r);
+        NLOG_V(3, "Configured route %s for interface '%s'", desc.c_str(), n.ifname.c_str());
+    } catch (const SysError& e) {
+        if (e.code() == EEXIST) {
+            NLOG_V(3, "Route %s already exists for interface '%s'", desc.c_str(), n.ifname.c_str());
+            return;
+        }
+        NLOG_W("Could not add route %s for interface '%s': %s", desc.c_str(), n.ifname.c_str(), e.what());
+        throw;
+    }
+}
+
+bool Agent::configure_interface(NicState& n) {
+    if (!n.addr || n.configured) return n.configured;
+    std::vector<nl::AddrInfo> addrs;
+    try {
+        addrs = ops_.addr_list(n.link.index, AF_INET);
+    } catch (const std::exception& e) {
+        n.config_error = e.what();
+        NLOG_W("Could not get addresses for link '%s': %s", n.ifname.c_str(), e.what());
+        return false;
+    }
+    bool existing = std::any_of(addrs.begin(), addrs.end(), [&](const nl::AddrInfo& a) { return a.local == n.addr->local; });
+    try {
+        if (!existing) {
+            // The kernel adds the /30 connected route along with the address.
+            ops_.addr_add(n.link.index, n.addr->local_prefix());
+            NLOG_I("Configured address and route %s for interface '%s'", n.addr->local_prefix().str().c_str(), n.ifname.c_str());
+        } else {
+            NLOG_I("Interface '%s' already configured with address %s", n.ifname.c_str(), n.addr->local_prefix().str().c_str());
+            add_route(n, l3::kPointToPointMask);
+        }
+        add_route(n, l3::kRoutedNetworkMask);
+    } catch (const std::exception& e) {
+        n.config_error = e.what();
+        if (!existing) NLOG_W("Could not configure address %s for interface '%s': %s", n.addr->local.str().c_str(), n.ifname.c_str(), e.what());
+        return false;
+    }
+    n.configured = true;
+    n.config_error.clear();
+    n.t_configured = mono_ns();
+    return true;
+}
+
+int Agent::configure_all() {
+    NLOG_I("Configuring interfaces...");
+    int c = 0;
+    for (auto& n : nics_)
+        if (configure_interface(n)) ++c;
+    return c;
+}
+
+void Agent::on_lldp(NicState& n, const lldp::Frame& f) {
+    n.lldp_seen = true;
+    n.t_lldp = mono_ns();
+    n.port_description = f.port_description.value_or("");
+    n.peer_mac = f.peer_mac();
+    n.peer_system_name = f.system_name.value_or("");
+    n.peer_port_id = f.port_id_str();
+    std::string err;
+    n.addr = l3::parse_port_description(n.port_description, cfg_.token_policy, &err);
+    if (!n.addr) {
+        n.addr_error = err;
+        NLOG_W("interface '%s': %s", n.ifname.c_str(), err.c_str());
+    } else {
+        n.addr_error.clear();
+    }
+}
+
+void Agent::detect_lldp(int stop_fd) {
+    int listening = 0;
+    for (auto& n : nics_) {
+        if (!n.link.up()) {
+            NLOG_I("Link '%s' %s, cannot start LLDP", n.ifname.c_str(), n.link.operstate_str().c_str());
+            continue;
+        }
+        try {
+            lldp_->add(n.ifname, n.link.index, n.link.mac);
+            ++listening;
+            NLOG_I("Started LLDP discovery for '%s'...", n.ifname.c_str());
+        } catch (const std::exception& e) {
+            NLOG_I("Cannot start LLDP client: %s", e.what());
+        }
+    }
+    if (!listening) return;
+    int remaining = listening;
+    auto cb = [&](const std::string& ifname, const lldp::Frame& f) -> bool {
+        for (auto& n : nics_) {
+            if (n.ifname != ifname || n.lldp_seen) continue;  // first frame per NIC wins (client.go:141-142)
+            on_lldp(n, f);
+            if (cfg_.pipeline && cfg_.configure && n.addr) configure_interface(n);
+            --remaining;
+        }
+        return remaining == 0;
+    };
+    auto r = lldp_->run(mono_ns() + cfg_.wait_ns, cb, stop_fd);
+    if (r == pkt::ListenResult::Interrupted) aborted_ = true;
+    if (r == pkt::ListenResult::Deadline) NLOG_I("LLDP wait of %s expired with %d interface(s) silent", format_go_duration(cfg_.wait_ns).c_str(), remaining);
+}
+
+void Agent::write_artifacts() {
+    std::string root = cfg_.sysfs_root.empty() ? topo::sysfs_root() : cfg_.sysfs_root;
+    for (auto& n : nics_) {
+        if (n.rdma_dev.empty() || !n.addr) continue;
+        n.gid_index = topo::find_rocev2_gid_index(root, n.rdma_dev, n.rdma_port, n.addr->local);
+    }
+    if (!cfg_.rccl_net.empty()) {
+        try {
+            artifacts::write_rccl_net(cfg_.rccl_net, nics_);
+        } catch (const std::exception& e) {
+            NLOG_E("Error: %s", e.what());  // not fatal (main.go:220-224)
+        }
+    }
+    if (!cfg_.rccl_env.empty()) {
+        try {
+            artifacts::write_rccl_env(cfg_.rccl_env, nics_, "");
+        } catch (const std::exception& e) {
+            NLOG_E("Error writing RCCL env: %s", e.what());
+        }
+    }
+    if (!cfg_.networkd.empty()) {
+        try {
+            artifacts::write_networkd(cfg_.networkd, nics_);
+        } catch (const std::exception& e) {
+            throw AgentError(std::string("Could not create systemd-networkd configuration files: ") + e.what());
+        }
+    }
+}
+
+void Agent::check_xgmi() {
+    if (cfg_.xgmi_expect_links < 0) return;
+    std::string root = cfg_.sysfs_root.empty() ? topo::sysfs_root() : cfg_.sysfs_root;
+    xgmi_ = topo::read_xgmi(root);
+    int expect = cfg_.xgmi_expect_links == 0 ? xgmi_.pairs_expected : cfg_.xgmi_expect_links;
+    NLOG_I("xGMI: %zu GPUs, %d/%d GPU pairs linked, %llu MB/s per GPU advertised", xgmi_.gpus.size(), xgmi_.pairs_connected,
+           xgmi_.pairs_expected, (unsigned long long)xgmi_.per_gpu_bw_mbs());
+    for (auto& [a, b] : xgmi_.missing) NLOG_W("xGMI: no link between %s and %s", a.c_str(), b.c_str());
+    if (xgmi_.pairs_connected < expect)
+        throw AgentError(strfmt("xGMI mesh incomplete: %d of %d GPU pairs linked", xgmi_.pairs_connected, expect));
+}
+
+void Agent::log_results() {
+    for (auto& n : nics_) {
+        NLOG_V(3, "Interface '%s' %s:", n.ifname.c_str(), n.link.flags_str().c_str());
+        std::string s = "\tConfigured addresses: ";
+        std::vector<nl::AddrInfo> addrs;
+        try {
+            addrs = ops_.addr_list(n.link.index, AF_UNSPEC);
+        } catch (...) {
+        }
+        if (addrs.empty()) s += "no addresses";
+        for (auto& a : addrs) {
+            s += a.prefix().str();
+            if (n.addr && a.local == n.addr->local) s += "(matches lldp)";
+            s += " ";
+        }
+        NLOG_V(3, "%s", s.c_str());
+        if (cfg_.mode == "L3") {
+            NLOG_V(3, "\tPeer MAC address: %s", n.peer_mac ? n.peer_mac->str().c_str() : "none");
+            NLOG_V(3, "\tPeer LLDP address: %s", n.addr ? n.addr->peer.str().c_str() : "none");
+            NLOG_V(3, "\tLocal /30 LLDP address: %s", n.addr ? n.addr->local.str().c_str() : "none");
+        }
+    }
+}
+
+void Agent::write_status() {
+    if (cfg_.status_file.empty()) return;
+    try {
+        write_file_atomic(cfg_.status_file, artifacts::generate_status(nics_, phases_, t0_, cfg_.mode, ready_) + "\n");
+    } catch (const std::exception& e) {
+        NLOG_W("Could not write status file: %s", e.what());
+    }
+}
+
+void Agent::run(int stop_fd) {
+    t0_ = t_last_ = mono_ns();
+    sanitize(cfg_);
+    pre_cleanups();
+
+    auto names = collect_interfaces();
+    if (names.empty()) throw AgentError("No interfaces found");
+    get_network_configs(names);
+    if (nics_.size() < names.size()) throw AgentError("Not all interfaces were found in the system");
+    mark("discover");
+
+    if (cfg_.disable_nm) {
+        if (!cfg_.nm_keyfile_dir.empty()) {
+            try {
+                auto p = nm::write_keyfile(cfg_.nm_keyfile_dir, names);
+                if (!p.empty()) NLOG_I("Wrote NetworkManager keyfile %s", p.c_str());
+            } catch (const std::exception& e) {
+                NLOG_W("Could not write NetworkManager keyfile: %s", e.what());
+            }
+        }
+        std::unique_ptr<nm::NetworkManagerIf> nmapi;
+        try {
+            nmapi = nm_factory_();
+        } catch (const std::exception& e) {
+            throw AgentError(std::string("Failed to create NetworkManager: ") + e.what());
+        }
+        try {
+            nm::disable_for_interfaces(*nmapi, names);
+        } catch (const std::exception& e) {
+            throw AgentError(std::string("Failed to disable interfaces in NetworkManager: ") + e.what());
+        }
+        mark("networkmanager");
+    }
+
+    interfaces_up();
+    mark("link_up");
+    interfaces_set_mtu();
+    mark("mtu");
+    try {
+        remove_existing_ips();
+    } catch (const std::exception& e) {
+        throw AgentError(std::string("Failed to remove any existing IPs from interfaces: ") + e.what());
+    }
+    mark("flush");
+
+    if (cfg_.mode == "L3") {
+        detect_lldp(stop_fd);
+        mark("lldp");
+        if (aborted_) {
+            NLOG_I("Interrupted while waiting for LLDP");
+            post_cleanups();
+            return;
+        }
+        bool found = std::any_of(nics_.begin(), nics_.end(), [](const NicState& n) { return bool(n.addr); });
+        if (cfg_.configure && found) {
+            int configured = configure_all();  // pipelined NICs are already done; this is a no-op for them
+            int total = int(nics_.size());
+            mark("configure");
+            if (configured < total) {
+                write_status();
+                throw AgentError(strfmt("Not all interfaces were configured (%d/%d).", configured, total));
+            }
+            NLOG_I("Configured %d of %d interfaces", configured, total);
+        } else if (cfg_.configure && !found && !cfg_.label_without_peers) {
+            write_status();
+            throw AgentError("No LLDP peers with a /30 Port Description were found");
+        }
+        write_artifacts();
+        mark("artifacts");
+    }
+
+    check_xgmi();
+    log_results();
+
+    if (!cfg_.configure) {
+        interfaces_restore_down();
+        write_status();
+        return;
+    }
+    if (!cfg_.keep_running) {
+        write_status();
+        return;
+    }
+    std::map<std::string, std::string> extra;
+    int nconf = int(std::count_if(nics_.begin(), nics_.end(), [](const NicState& n) { return n.configured; }));
+    extra["amd.feature.node.kubernetes.io/gpu-scale-out.mode"] = cfg_.mode;
+    extra["amd.feature.node.kubernetes.io/gpu-scale-out.nics"] = std::to_string(cfg_.mode == "L3" ? nconf : int(nics_.size()));
+    if (cfg_.xgmi_expect_links >= 0)
+        extra["amd.feature.node.kubernetes.io/gpu-xgmi.pairs"] = std::to_string(xgmi_.pairs_connected);
+    try {
+        if (artifacts::write_labels(cfg_.labels, extra)) NLOG_I("Published readiness label %s", cfg_.labels.path().c_str());
+    } catch (const std::exception& e) {
+        throw AgentError(std::string("Failed to write NFD label to indicate scale-out readiness: ") + e.what());
+    }
+    ready_ = true;
+    phases_["total_ready"] = mono_ns() - t0_;
+    write_status();
+    NLOG_I("Configurations done. Idling...");
+
+    // Idle until SIGTERM / SIGINT.
+    while (!fd_readable(stop_fd)) {
+        if (stop_fd < 0) {
+            ::pause();
+            continue;
+        }
+        pollfd p{stop_fd, POLLIN, 0};
+        ::poll(&p, 1, -1);
+    }
+    post_cleanups();
+}
+
+}  // namespace netop::agent

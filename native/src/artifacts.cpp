@@ -1,0 +1,293 @@
+#include "netop/artifacts.hpp"
+
+#include <unistd.h>
+
+#include <algorithm>
+#include <cmath>
+#include <set>
+
+#include "netop/log.hpp"
+
+namespace netop::artifacts {
+
+// ---------------------------------------------------------------------------
+// Json
+// ---------------------------------------------------------------------------
+std::string Json::escape(const std::string& s) {
+    std::string o;
+    o.reserve(s.size() + 2);
+    for (unsigned char c : s) {
+        switch (c) {
+            case '"': o += "\\\""; break;
+            case '\\': o += "\\\\"; break;
+            case '\n': o += "\\n"; break;
+            case '\r': o += "\\r"; break;
+            case '\t': o += "\\t"; break;
+            case '<': o += "\\u003c"; break;  // Go's HTML-safe escaping
+            case '>': o += "\\u003e"; break;
+            case '&': o += "\\u0026"; break;
+            default:
+                if (c < 0x20)
+                    o += strfmt("\\u%04x", c);
+                else
+                    o += char(c);
+        }
+    }
+    return o;
+}
+
+void Json::sep() {
+    if (after_key_) {
+        after_key_ = false;
+        return;
+    }
+    if (!first_.back()) out_ += ',';
+    first_.back() = false;
+}
+Json& Json::begin_object() {
+    sep();
+    out_ += '{';
+    first_.push_back(true);
+    return *this;
+}
+Json& Json::end_object() {
+    out_ += '}';
+    first_.pop_back();
+    return *this;
+}
+Json& Json::begin_array() {
+    sep();
+    out_ += '[';
+    first_.push_back(true);
+    return *this;
+}
+Json& Json::end_array() {
+    out_ += ']';
+    first_.pop_back();
+    return *this;
+}
+Json& Json::key(const std::string& k) {
+    sep();
+    out_ += '"' + escape(k) + "\":";
+    after_key_ = true;
+    return *this;
+}
+Json& Json::value(const std::string& s) {
+    sep();
+    out_ += '"' + escape(s) + '"';
+    return *this;
+}
+Json& Json::value(int64_t v) {
+    sep();
+    out_ += std::to_string(v);
+    return *this;
+}
+Json& Json::value(uint64_t v) {
+    sep();
+    out_ += std::to_string(v);
+    return *this;
+}
+Json& Json::value(double v) {
+    sep();
+    if (!std::isfinite(v))
+        out_ += "null";
+    else
+        out_ += strfmt("%.9g", v);
+    return *this;
+}
+Json& Json::value(bool b) {
+    sep();
+    out_ += b ? "true" : "false";
+    return *this;
+}
+Json& Json::null() {
+    sep();
+    out_ += "null";
+    return *this;
+}
+
+// ---------------------------------------------------------------------------
+// RCCL artifacts
+// ---------------------------------------------------------------------------
+static std::vector<const NicState*> sorted(const std::vector<NicState>& nics) {
+    std::vector<const NicState*> v;
+    for (auto& n : nics) v.push_back(&n);
+    std::stable_sort(v.begin(), v.end(), [](const NicState* a, const NicState* b) {
+        int ga = a->gpu_index < 0 ? 1 << 30 : a->gpu_index, gb = b->gpu_index < 0 ? 1 << 30 : b->gpu_index;
+        return ga != gb ? ga < gb : a->ifname < b->ifname;
+    });
+    return v;
+}
+
+std::string generate_rccl_net(const std::vector<NicState>& nics, bool extended) {
+    Json j;
+    j.begin_object().key("NIC_NET_CONFIG").begin_array();
+    for (const NicState* n : sorted(nics)) {
+        if (!n->addr) {
+            NLOG_W("Interface '%s' has no LLDP address when creating RCCL network file, skipping...", n->ifname.c_str());
+            continue;
+        }
+        if (!n->peer_mac) {
+            NLOG_W("Interface '%s' has no peer MAC address when creating RCCL network file, skipping...", n->ifname.c_str());
+            continue;
+        }
+        j.begin_object();
+        j.key("NIC_MAC").value(n->link.mac.str());
+        j.key("NIC_IP").value(n->addr->local.str());
+        j.key("SUBNET_MASK").value(l3::mask_string(n->addr->prefix));
+        j.key("GATEWAY_MAC").value(n->peer_mac->str());
+        if (extended) {
+            j.key("NIC_NAME").value(n->ifname);
+            j.key("GATEWAY_IP").value(n->addr->peer.str());
+            if (!n->gpu_bdf.empty()) j.key("GPU_BDF").value(n->gpu_bdf);
+            if (n->gpu_index >= 0) j.key("GPU_INDEX").value(n->gpu_index);
+            if (!n->rdma_dev.empty()) {
+                j.key("RDMA_DEV").value(n->rdma_dev);
+                j.key("RDMA_PORT").value(n->rdma_port);
+            }
+            if (n->gid_index) j.key("GID_INDEX").value(*n->gid_index);
+        }
+        j.end_object();
+    }
+    j.end_array().end_object();
+    return j.str();
+}
+
+void write_rccl_net(const std::string& path, const std::vector<NicState>& nics, bool extended) {
+    if (path.empty()) throw std::runtime_error("no file name when saving the RCCL network file");
+    write_file_atomic(path, generate_rccl_net(nics, extended), 0644);
+}
+
+std::string generate_rccl_env(const std::vector<NicState>& nics, const std::string& topo_file) {
+    std::vector<std::string> hcas;
+    std::set<int> gids;
+    for (const NicState* n : sorted(nics)) {
+        if (n->rdma_dev.empty() || !n->configured) continue;
+        hcas.push_back(n->rdma_dev + ":" + std::to_string(n->rdma_port));
+        if (n->gid_index) gids.insert(*n->gid_index);
+    }
+    std::string out = "# Generated by the AMD network operator link-discovery agent.\n"
+                      "# Source this file (or pass it as an env-file) in RCCL jobs on this node.\n";
+    if (!hcas.empty()) out += "NCCL_IB_HCA==" + join(hcas, ",") + "\n";
+    if (gids.size() == 1) out += "NCCL_IB_GID_INDEX=" + std::to_string(*gids.begin()) + "\n";
+    if (!hcas.empty()) out += "NCCL_IB_DISABLE=0\n";
+    if (!topo_file.empty()) out += "NCCL_TOPO_FILE=" + topo_file + "\n";
+    return out;
+}
+
+void write_rccl_env(const std::string& path, const std::vector<NicState>& nics, const std::string& topo_file) {
+    write_file_atomic(path, generate_rccl_env(nics, topo_file), 0644);
+}
+
+// ---------------------------------------------------------------------------
+// systemd-networkd
+// ---------------------------------------------------------------------------
+std::string networkd_filename(const std::string& dir, const std::string& ifname) {
+    return path_join(dir, ifname + ".network");
+}
+
+std::string generate_networkd(const NicState& n) {
+    Ipv4Prefix routed = n.addr->routed_network();
+    return strfmt(
+        "[Match]\n"
+        "MACAddress=%s\n"
+        "\n"
+        "[Network]\n"
+        "Description=Networkd configuration for %s created by network-operator\n"
+        "Address=%s/%d\n"
+        "\n"
+        "[Route]\n"
+        "Destination=%s/%d\n",
+        n.link.mac.str().c_str(), n.ifname.c_str(), n.addr->local.str().c_str(), n.addr->prefix,
+        routed.addr.str().c_str(), routed.len);
+}
+
+std::vector<std::string> write_networkd(const std::string& dir, const std::vector<NicState>& nics) {
+    for (auto& n : nics) {
+        if (n.link.index == 0 && n.link.name.empty()) throw std::runtime_error("no link information for " + n.ifname);
+        if (!n.addr) throw std::runtime_error("no local address for " + n.ifname);
+        if (n.link.mac.is_zero()) throw std::runtime_error("no local hw address for " + n.ifname);
+    }
+    std::vector<std::string> written;
+    for (const NicState* n : sorted(nics)) {
+        std::string fn = networkd_filename(dir, n->ifname);
+        try {
+            write_file_atomic(fn, generate_networkd(*n), 0644);
+        } catch (const std::exception& e) {
+            delete_networkd(dir, written);
+            throw std::runtime_error("could not write networkd config file '" + fn + "': " + e.what());
+        }
+        written.push_back(n->ifname);
+    }
+    return written;
+}
+
+void delete_networkd(const std::string& dir, const std::vector<std::string>& ifnames) {
+    for (auto& i : ifnames) ::unlink(networkd_filename(dir, i).c_str());
+}
+
+// ---------------------------------------------------------------------------
+// NFD labels
+// ---------------------------------------------------------------------------
+const char* const kScaleOutReadyLabel = "amd.feature.node.kubernetes.io/gpu-scale-out=true";
+
+std::string Labels::path() const { return path_join(dir, file); }
+
+std::string generate_labels(const std::map<std::string, std::string>& extra) {
+    std::string out = std::string(kScaleOutReadyLabel) + "\n";
+    for (auto& [k, v] : extra) out += k + "=" + v + "\n";
+    return out;
+}
+
+bool write_labels(const Labels& l, const std::map<std::string, std::string>& extra) {
+    if (!is_dir(l.dir)) return false;
+    write_file_atomic(l.path(), generate_labels(extra), 0644);
+    return true;
+}
+
+bool remove_labels(const Labels& l) { return ::unlink(l.path().c_str()) == 0; }
+
+// ---------------------------------------------------------------------------
+// Status document
+// ---------------------------------------------------------------------------
+std::string generate_status(const std::vector<NicState>& nics, const std::map<std::string, int64_t>& phases_ns,
+                            int64_t t0, const std::string& mode, bool ready) {
+    Json j;
+    j.begin_object();
+    j.key("mode").value(mode);
+    j.key("ready").value(ready);
+    j.key("phases_ms").begin_object();
+    for (auto& [k, v] : phases_ns) j.key(k).value(double(v) / 1e6);
+    j.end_object();
+    j.key("interfaces").begin_array();
+    for (const NicState* n : sorted(nics)) {
+        j.begin_object();
+        j.key("name").value(n->ifname);
+        j.key("mac").value(n->link.mac.str());
+        j.key("gpu_index").value(n->gpu_index);
+        if (!n->gpu_bdf.empty()) j.key("gpu_bdf").value(n->gpu_bdf);
+        if (!n->rdma_dev.empty()) j.key("rdma_dev").value(n->rdma_dev);
+        j.key("lldp").value(n->lldp_seen);
+        if (n->lldp_seen) {
+            j.key("port_description").value(n->port_description);
+            if (n->peer_mac) j.key("peer_mac").value(n->peer_mac->str());
+            j.key("peer_system").value(n->peer_system_name);
+        }
+        if (n->addr) {
+            j.key("local").value(n->addr->local_prefix().str());
+            j.key("gateway").value(n->addr->peer.str());
+        }
+        if (!n->addr_error.empty()) j.key("addr_error").value(n->addr_error);
+        j.key("configured").value(n->configured);
+        if (!n->config_error.empty()) j.key("config_error").value(n->config_error);
+        if (n->gid_index) j.key("gid_index").value(*n->gid_index);
+        if (n->t_lldp) j.key("t_lldp_ms").value(double(n->t_lldp - t0) / 1e6);
+        if (n->t_configured) j.key("t_configured_ms").value(double(n->t_configured - t0) / 1e6);
+        j.end_object();
+    }
+    j.end_array();
+    j.end_object();
+    return j.str();
+}
+
+}  // namespace netop::artifacts

@@ -1,0 +1,358 @@
+#include "netop/topology.hpp"
+
+#include <algorithm>
+#include <cstdlib>
+#include <set>
+
+#include "netop/log.hpp"
+
+namespace netop::topo {
+
+std::string sysfs_root() {
+    const char* r = std::getenv("SYSFS_ROOT");
+    return (r && *r) ? std::string(r) : std::string("/sys/");
+}
+
+const char* to_string(PathType p) {
+    switch (p) {
+        case PathType::PIX: return "PIX";
+        case PathType::PXB: return "PXB";
+        case PathType::PHB: return "PHB";
+        case PathType::NODE: return "NODE";
+        case PathType::SYS: return "SYS";
+    }
+    return "SYS";
+}
+
+std::optional<DiscoveryMode> parse_discovery_mode(std::string_view s) {
+    if (s == "affine" || s.empty()) return DiscoveryMode::Affine;
+    if (s == "accel") return DiscoveryMode::Accel;
+    if (s == "none") return DiscoveryMode::None;
+    return std::nullopt;
+}
+
+static bool looks_like_bdf(std::string_view s) {
+    // dddd:bb:dd.f
+    if (s.size() != 12) return false;
+    auto hex = [](char c) { return (c >= '0' && c <= '9') || (c >= 'a' && c <= 'f') || (c >= 'A' && c <= 'F'); };
+    for (size_t i = 0; i < 12; ++i) {
+        if (i == 4 || i == 7) {
+            if (s[i] != ':') return false;
+        } else if (i == 10) {
+            if (s[i] != '.') return false;
+        } else if (!hex(s[i])) {
+            return false;
+        }
+    }
+    return true;
+}
+
+static uint32_t read_hex(const std::string& path) {
+    auto s = read_file(path);
+    if (!s) return 0;
+    return uint32_t(std::strtoul(trim(*s).c_str(), nullptr, 16));
+}
+
+static int read_int(const std::string& path, int dflt) {
+    auto s = read_file(path);
+    if (!s) return dflt;
+    auto t = trim(*s);
+    if (t.empty()) return dflt;
+    return int(std::strtol(t.c_str(), nullptr, 10));
+}
+
+std::optional<PciDev> read_pci_dev(const std::string& root, const std::string& device_path) {
+    auto real = realpath_of(device_path);
+    if (!real) return std::nullopt;
+    PciDev d;
+    d.path = *real;
+    d.bdf = path_basename(*real);
+    if (!looks_like_bdf(d.bdf)) return std::nullopt;
+    auto pos = real->find("/devices/");
+    if (pos == std::string::npos) return std::nullopt;
+    for (auto& c : split(real->substr(pos + 9), '/'))
+        if (!c.empty()) d.chain.push_back(c);
+    if (auto drv = realpath_of(path_join(*real, "driver"))) d.driver = path_basename(*drv);
+    d.vendor = read_hex(path_join(*real, "vendor"));
+    d.device = read_hex(path_join(*real, "device"));
+    d.pci_class = read_hex(path_join(*real, "class"));
+    d.numa = read_int(path_join(*real, "numa_node"), -1);
+    (void)root;
+    return d;
+}
+
+std::vector<Gpu> discover_gpus(const std::string& root, const std::string& driver) {
+    std::vector<Gpu> out;
+    std::string dir = path_join(root, "bus/pci/drivers/" + driver);
+    for (auto& name : list_dir(dir)) {
+        if (!looks_like_bdf(name)) continue;
+        auto d = read_pci_dev(root, path_join(dir, name));
+        if (!d) {
+            NLOG_W("Expected '%s' to be a symlink to a PCI device", path_join(dir, name).c_str());
+            continue;
+        }
+        if (d->driver.empty()) d->driver = driver;
+        Gpu g;
+        g.pci = *d;
+        out.push_back(std::move(g));
+    }
+    std::sort(out.begin(), out.end(), [](const Gpu& a, const Gpu& b) { return a.pci.bdf < b.pci.bdf; });
+    for (size_t i = 0; i < out.size(); ++i) out[i].index = int(i);
+    return out;
+}
+
+std::vector<Nic> discover_pci_nics(const std::string& root, const std::vector<std::string>& drivers) {
+    std::vector<Nic> out;
+    std::string cls = path_join(root, "class/net");
+    for (auto& ifname : list_dir(cls)) {
+        auto real = realpath_of(path_join(cls, ifname));
+        if (!real) continue;
+        // <pci device dir>/net/<ifname>
+        std::string netdir = path_dirname(*real);
+        if (path_basename(netdir) != "net") continue;
+        std::string devdir = path_dirname(netdir);
+        if (!looks_like_bdf(path_basename(devdir))) continue;  // virtual / non-PCI netdev
+        auto d = read_pci_dev(root, devdir);
+        if (!d) continue;
+        if (!drivers.empty() && std::find(drivers.begin(), drivers.end(), d->driver) == drivers.end()) continue;
+        Nic n;
+        n.ifname = ifname;
+        n.pci = *d;
+        if (auto a = read_file(path_join(*real, "address")))
+            if (auto m = MacAddr::parse(trim(*a))) n.mac = *m;
+        auto ib = list_dir(path_join(devdir, "infiniband"));
+        if (!ib.empty()) n.rdma_dev = ib.front();
+        n.rdma_port = read_int(path_join(*real, "dev_port"), 0) + 1;
+        out.push_back(std::move(n));
+    }
+    std::sort(out.begin(), out.end(), [](const Nic& a, const Nic& b) {
+        return a.pci.bdf != b.pci.bdf ? a.pci.bdf < b.pci.bdf : a.ifname < b.ifname;
+    });
+    return out;
+}
+
+PathType path_between(const PciDev& a, const PciDev& b, int* common_depth) {
+    size_t n = 0;
+    while (n < a.chain.size() && n < b.chain.size() && a.chain[n] == b.chain[n]) ++n;
+    if (common_depth) *common_depth = int(n);
+    // chain[0] = host bridge "pciDDDD:BB", chain[1] = root port, chain[2..] = switch ports.
+    // Sharing a component past the root port means both sit below one PCIe switch.
+    if (n >= 3) {
+        // Diverging right below one switch's upstream port ([downstream port, endpoint] left on
+        // each side) is a single bridge (PIX); anything deeper crosses several switches (PXB).
+        size_t da = a.chain.size() - n, db = b.chain.size() - n;
+        return (da <= 2 && db <= 2) ? PathType::PIX : PathType::PXB;
+    }
+    if (n >= 1) return PathType::PHB;
+    if (a.numa >= 0 && a.numa == b.numa) return PathType::NODE;
+    return PathType::SYS;
+}
+
+std::vector<GpuNicPair> pair_gpus_nics(const std::vector<Gpu>& gpus, const std::vector<Nic>& nics, PathType max_path) {
+    std::vector<GpuNicPair> out;
+    std::vector<bool> used(nics.size(), false);
+    for (size_t g = 0; g < gpus.size(); ++g) {
+        int best = -1, best_depth = -1;
+        PathType best_path = PathType::SYS;
+        for (size_t n = 0; n < nics.size(); ++n) {
+            if (used[n]) continue;
+            int depth = 0;
+            PathType p = path_between(gpus[g].pci, nics[n].pci, &depth);
+            if (int(p) > int(max_path)) continue;
+            if (best < 0 || int(p) < int(best_path) || (p == best_path && depth > best_depth)) {
+                best = int(n);
+                best_depth = depth;
+                best_path = p;
+            }
+        }
+        if (best >= 0) {
+            used[size_t(best)] = true;
+            out.push_back(GpuNicPair{int(g), best, best_path, best_depth});
+        }
+    }
+    return out;
+}
+
+std::vector<std::string> accel_netdevs(const std::string& root, const std::string& driver) {
+    std::vector<std::string> out;
+    std::string dir = path_join(root, "bus/pci/drivers/" + driver);
+    for (auto& name : list_dir(dir)) {
+        if (!looks_like_bdf(name)) continue;
+        auto real = realpath_of(path_join(dir, name));
+        if (!real) {
+            NLOG_W("Expected '%s' to be a symlink", path_join(dir, name).c_str());
+            continue;
+        }
+        for (auto& n : list_dir(path_join(*real, "net"))) out.push_back(n);
+    }
+    return out;
+}
+
+DiscoveryResult discover(const DiscoveryOptions& opt, const std::string& root) {
+    DiscoveryResult r;
+    if (opt.mode == DiscoveryMode::None) return r;
+    if (opt.mode == DiscoveryMode::Accel) {
+        r.ifnames = accel_netdevs(root, opt.accel_driver);
+        return r;
+    }
+    r.gpus = discover_gpus(root, opt.accel_driver);
+    r.nics = discover_pci_nics(root, opt.nic_drivers);
+    r.pairs = pair_gpus_nics(r.gpus, r.nics, opt.max_path);
+    for (auto& p : r.pairs) r.ifnames.push_back(r.nics[size_t(p.nic)].ifname);
+    return r;
+}
+
+static std::optional<std::array<uint8_t, 16>> parse_gid(const std::string& s) {
+    // "0000:0000:0000:0000:0000:ffff:0a00:0001"
+    auto parts = split(trim(s), ':');
+    if (parts.size() != 8) return std::nullopt;
+    std::array<uint8_t, 16> g{};
+    for (size_t i = 0; i < 8; ++i) {
+        if (parts[i].empty() || parts[i].size() > 4) return std::nullopt;
+        char* end = nullptr;
+        unsigned long v = std::strtoul(parts[i].c_str(), &end, 16);
+        if (*end) return std::nullopt;
+        g[i * 2] = uint8_t(v >> 8);
+        g[i * 2 + 1] = uint8_t(v);
+    }
+    return g;
+}
+
+std::optional<int> find_rocev2_gid_index(const std::string& root, const std::string& rdma_dev, int port, Ipv4 ip) {
+    std::string pdir = path_join(root, "class/infiniband/" + rdma_dev + "/ports/" + std::to_string(port));
+    auto names = list_dir(path_join(pdir, "gids"));
+    std::vector<int> idx;
+    for (auto& n : names) {
+        char* end = nullptr;
+        long v = std::strtol(n.c_str(), &end, 10);
+        if (*end == 0) idx.push_back(int(v));
+    }
+    std::sort(idx.begin(), idx.end());
+    std::array<uint8_t, 16> want{};
+    want[10] = want[11] = 0xff;
+    ip.to_net(&want[12]);
+    for (int i : idx) {
+        auto g = read_file(path_join(pdir, "gids/" + std::to_string(i)));
+        if (!g) continue;
+        auto gid = parse_gid(*g);
+        if (!gid || *gid != want) continue;
+        auto type = read_file(path_join(pdir, "gid_attrs/types/" + std::to_string(i)));
+        if (type && trim(*type) == "RoCE v2") return i;
+    }
+    return std::nullopt;
+}
+
+// ---------------------------------------------------------------------------
+// KFD topology
+// ---------------------------------------------------------------------------
+static std::map<std::string, std::string> read_props(const std::string& path) {
+    std::map<std::string, std::string> m;
+    auto s = read_file(path);
+    if (!s) return m;
+    for (auto& line : split(*s, '\n')) {
+        auto f = split_ws(line);
+        if (f.size() >= 2) m[f[0]] = f[1];
+    }
+    return m;
+}
+
+static uint64_t prop_u64(const std::map<std::string, std::string>& m, const char* k) {
+    auto it = m.find(k);
+    return it == m.end() ? 0 : std::strtoull(it->second.c_str(), nullptr, 10);
+}
+
+std::string KfdNode::bdf() const {
+    return strfmt("%04x:%02x:%02x.%x", domain, (location_id >> 8) & 0xff, (location_id >> 3) & 0x1f, location_id & 7);
+}
+
+uint64_t XgmiReport::per_gpu_bw_mbs() const {
+    if (gpus.empty()) return 0;
+    uint64_t best = UINT64_MAX;
+    for (auto& g : gpus) {
+        uint64_t sum = 0;
+        std::set<int> peers;
+        for (auto& l : links) {
+            int peer = l.from == g.node ? l.to : (l.to == g.node ? l.from : -1);
+            if (peer < 0 || !peers.insert(peer).second) continue;
+            sum += l.max_bw_mbs;
+        }
+        best = std::min(best, sum);
+    }
+    return best == UINT64_MAX ? 0 : best;
+}
+
+XgmiReport read_xgmi(const std::string& root) {
+    XgmiReport r;
+    std::string base = path_join(root, "class/kfd/kfd/topology/nodes");
+    std::map<int, KfdNode> nodes;
+    std::vector<KfdLink> all;
+    for (auto& n : list_dir(base)) {
+        char* end = nullptr;
+        long id = std::strtol(n.c_str(), &end, 10);
+        if (*end) continue;
+        auto props = read_props(path_join(base, n + "/properties"));
+        KfdNode k;
+        k.node = int(id);
+        k.simd_count = uint32_t(prop_u64(props, "simd_count"));
+        k.vendor_id = uint32_t(prop_u64(props, "vendor_id"));
+        k.device_id = uint32_t(prop_u64(props, "device_id"));
+        k.location_id = uint32_t(prop_u64(props, "location_id"));
+        k.domain = uint32_t(prop_u64(props, "domain"));
+        k.hive_id = prop_u64(props, "hive_id");
+        k.num_xcc = uint32_t(prop_u64(props, "num_xcc"));
+        if (auto g = read_file(path_join(base, n + "/gpu_id"))) k.gpu_id = uint32_t(std::strtoul(trim(*g).c_str(), nullptr, 10));
+        nodes[k.node] = k;
+        for (const char* sub : {"io_links", "p2p_links"}) {
+            std::string ldir = path_join(base, n + "/" + sub);
+            for (auto& l : list_dir(ldir)) {
+                auto lp = read_props(path_join(ldir, l + "/properties"));
+                if (lp.empty()) continue;  // unreadable (e.g. filtered in a container)
+                KfdLink link;
+                link.type = int(prop_u64(lp, "type"));
+                link.from = int(prop_u64(lp, "node_from"));
+                link.to = int(prop_u64(lp, "node_to"));
+                link.weight = int(prop_u64(lp, "weight"));
+                link.min_bw_mbs = uint32_t(prop_u64(lp, "min_bandwidth"));
+                link.max_bw_mbs = uint32_t(prop_u64(lp, "max_bandwidth"));
+                all.push_back(link);
+            }
+        }
+    }
+    // A GPU node whose properties were filtered reads simd_count 0; a node that is the
+    // endpoint of an xGMI link is a GPU regardless.
+    std::set<int> xgmi_nodes;
+    for (auto& l : all)
+        if (l.type == kIoLinkTypeXgmi) {
+            xgmi_nodes.insert(l.from);
+            xgmi_nodes.insert(l.to);
+        }
+    for (auto& [id, k] : nodes)
+        if (k.is_gpu() || xgmi_nodes.count(id)) r.gpus.push_back(k);
+    std::sort(r.gpus.begin(), r.gpus.end(), [](const KfdNode& a, const KfdNode& b) {
+        return a.is_gpu() != b.is_gpu() ? a.is_gpu() : (a.location_id != b.location_id ? a.location_id < b.location_id : a.node < b.node);
+    });
+
+    std::set<std::pair<int, int>> connected;
+    uint64_t minbw = UINT64_MAX;
+    for (auto& l : all) {
+        if (l.type != kIoLinkTypeXgmi) continue;
+        r.links.push_back(l);
+        connected.insert({std::min(l.from, l.to), std::max(l.from, l.to)});
+        if (l.max_bw_mbs) minbw = std::min<uint64_t>(minbw, l.max_bw_mbs);
+    }
+    r.min_link_bw_mbs = minbw == UINT64_MAX ? 0 : minbw;
+    int n = int(r.gpus.size());
+    r.pairs_expected = n * (n - 1) / 2;
+    for (int i = 0; i < n; ++i)
+        for (int j = i + 1; j < n; ++j) {
+            int a = std::min(r.gpus[size_t(i)].node, r.gpus[size_t(j)].node);
+            int b = std::max(r.gpus[size_t(i)].node, r.gpus[size_t(j)].node);
+            if (connected.count({a, b}))
+                ++r.pairs_connected;
+            else
+                r.missing.emplace_back(r.gpus[size_t(i)].bdf(), r.gpus[size_t(j)].bdf());
+        }
+    return r;
+}
+
+}  // namespace netop::topo

@@ -1,0 +1,127 @@
+// In-memory NetOps with per-operation fault injection — the C++ counterpart of the
+// reference's function-table fakes (reference cmd/discover/network_test.go:276,364-366,
+// 405,429,516-519,555-558,595,605).
+#pragma once
+
+#include <linux/if.h>
+#include <sys/socket.h>
+
+#include <algorithm>
+#include <deque>
+#include <map>
+#include <set>
+
+#include "netop/netlink.hpp"
+
+struct FakeNetOps : netop::nl::NetOps {
+    std::map<std::string, netop::nl::LinkInfo> links;
+    std::vector<netop::nl::AddrInfo> addrs;
+    std::vector<netop::nl::RouteSpec> routes;
+    std::set<std::string> fail;  // op names that throw: "link_by_name", "addr_list", ...
+    int fail_errno = EPERM;
+    bool echo_links = true;      // emit RTM_NEWLINK on set up/down
+    std::deque<netop::nl::LinkEvent> events;
+    std::map<std::string, int> calls;
+
+    void add_link(const std::string& name, int index, const char* mac, bool up) {
+        netop::nl::LinkInfo l;
+        l.name = name;
+        l.index = index;
+        l.mac = *netop::MacAddr::parse(mac);
+        l.flags = IFF_BROADCAST | IFF_MULTICAST | (up ? IFF_UP : 0);
+        l.mtu = 1500;
+        links[name] = l;
+    }
+    netop::nl::LinkInfo* by_index(int idx) {
+        for (auto& [n, l] : links)
+            if (l.index == idx) return &l;
+        return nullptr;
+    }
+    void maybe_fail(const std::string& op) {
+        ++calls[op];
+        if (fail.count(op)) throw netop::SysError(fail_errno, "injected " + op);
+    }
+    netop::nl::LinkInfo link_by_name(const std::string& name) override {
+        maybe_fail("link_by_name");
+        auto it = links.find(name);
+        if (it == links.end()) throw netop::SysError(ENODEV, "link '" + name + "' not found");
+        return it->second;
+    }
+    std::vector<netop::nl::AddrInfo> addr_list(int ifindex, int family) override {
+        maybe_fail("addr_list");
+        std::vector<netop::nl::AddrInfo> out;
+        for (auto& a : addrs)
+            if (a.ifindex == ifindex) out.push_back(a);
+        return out;
+    }
+    void addr_add(int ifindex, const netop::Ipv4Prefix& p) override {
+        maybe_fail("addr_add");
+        for (auto& a : addrs)
+            if (a.ifindex == ifindex && a.local == p.addr) throw netop::SysError(EEXIST, "addr exists");
+        netop::nl::AddrInfo a;
+        a.ifindex = ifindex;
+        a.family = AF_INET;
+        a.local = a.address = p.addr;
+        a.prefixlen = p.len;
+        addrs.push_back(a);
+        // the kernel's connected route
+        netop::nl::RouteSpec r;
+        r.ifindex = ifindex;
+        r.dst = p.masked();
+        r.prefsrc = p.addr;
+        r.protocol = RTPROT_KERNEL;
+        r.scope = RT_SCOPE_LINK;
+        routes.push_back(r);
+    }
+    void addr_del(const netop::nl::AddrInfo& a) override {
+        maybe_fail("addr_del");
+        auto it = std::find_if(addrs.begin(), addrs.end(), [&](const netop::nl::AddrInfo& x) {
+            return x.ifindex == a.ifindex && x.local == a.local;
+        });
+        if (it == addrs.end()) throw netop::SysError(EADDRNOTAVAIL, "no such address");
+        routes.erase(std::remove_if(routes.begin(), routes.end(), [&](const netop::nl::RouteSpec& r) {
+                         return r.ifindex == a.ifindex && (r.prefsrc == std::optional<netop::Ipv4>(a.local) ||
+                                                            (r.gateway && netop::Ipv4Prefix{a.local, a.prefixlen}.contains(*r.gateway)));
+                     }),
+                     routes.end());
+        addrs.erase(it);
+    }
+    void route_append(const netop::nl::RouteSpec& r) override {
+        maybe_fail("route_append");
+        for (auto& x : routes)
+            if (x.ifindex == r.ifindex && x.dst.masked() == r.dst.masked() && x.gateway == r.gateway)
+                throw netop::SysError(EEXIST, "route exists");
+        routes.push_back(r);
+    }
+    void set_flag(int ifindex, bool up) {
+        auto* l = by_index(ifindex);
+        if (!l) throw netop::SysError(ENODEV, "no link");
+        l->flags = up ? (l->flags | IFF_UP) : (l->flags & ~unsigned(IFF_UP));
+        if (echo_links) events.push_back({false, *l});
+    }
+    void link_set_up(int ifindex) override {
+        maybe_fail("link_set_up");
+        set_flag(ifindex, true);
+    }
+    void link_set_down(int ifindex) override {
+        maybe_fail("link_set_down");
+        set_flag(ifindex, false);
+    }
+    void link_set_mtu(int ifindex, int mtu) override {
+        maybe_fail("link_set_mtu");
+        if (auto* l = by_index(ifindex)) l->mtu = mtu;
+    }
+    struct Watcher : netop::nl::LinkWatcher {
+        FakeNetOps* f;
+        explicit Watcher(FakeNetOps* ff) : f(ff) {}
+        std::vector<netop::nl::LinkEvent> wait(int64_t) override {
+            std::vector<netop::nl::LinkEvent> out(f->events.begin(), f->events.end());
+            f->events.clear();
+            return out;
+        }
+    };
+    std::unique_ptr<netop::nl::LinkWatcher> subscribe_links() override {
+        maybe_fail("subscribe_links");
+        return std::make_unique<Watcher>(this);
+    }
+};

@@ -1,0 +1,373 @@
+#include <unistd.h>
+
+#include "check.hpp"
+#include "fake_netops.hpp"
+#include "netop/agent.hpp"
+#include "tmpdir.hpp"
+
+using namespace netop;
+
+namespace {
+struct ScriptedLldp : agent::LldpSource {
+    std::map<std::string, lldp::Frame> frames;
+    std::vector<std::string> added;
+    pkt::ListenResult result_if_unfinished = pkt::ListenResult::Deadline;
+    void add(const std::string& ifname, int, const MacAddr&) override { added.push_back(ifname); }
+    pkt::ListenResult run(int64_t, const std::function<bool(const std::string&, const lldp::Frame&)>& cb, int) override {
+        for (auto& i : added) {
+            auto it = frames.find(i);
+            if (it != frames.end() && cb(i, it->second)) return pkt::ListenResult::Stopped;
+        }
+        return result_if_unfinished;
+    }
+};
+
+struct MockDevice : nm::DeviceIf {
+    std::string name;
+    bool fail_set = false;
+    bool* managed;
+    std::string get_interface() override { return name; }
+    void set_managed(bool m) override {
+        if (fail_set) throw std::runtime_error("set failed");
+        *managed = m;
+    }
+};
+struct MockNm : nm::NetworkManagerIf {
+    bool fail_version = false, fail_devices = false, fail_set = false;
+    std::map<std::string, bool> managed{{"ens0", true}, {"ens1", true}, {"eth9", true}};
+    std::map<std::string, bool>* shared = nullptr;  // outlives the mock (the agent drops it)
+    std::string get_version() override {
+        if (fail_version) throw std::runtime_error("no NM");
+        return "1.46.0";
+    }
+    std::vector<std::unique_ptr<nm::DeviceIf>> get_all_devices() override {
+        if (fail_devices) throw std::runtime_error("devices failed");
+        std::vector<std::unique_ptr<nm::DeviceIf>> v;
+        auto& table = shared ? *shared : managed;
+        if (shared && shared->empty()) *shared = managed;
+        for (auto& [n, m] : table) {
+            auto d = std::make_unique<MockDevice>();
+            d->name = n;
+            d->managed = &m;
+            d->fail_set = fail_set;
+            v.push_back(std::move(d));
+        }
+        return v;
+    }
+};
+
+struct Pipe {
+    int fd[2];
+    Pipe() {
+        if (::pipe(fd) != 0) throw std::runtime_error("pipe");
+    }
+    ~Pipe() {
+        ::close(fd[0]);
+        ::close(fd[1]);
+    }
+    void fire() { (void)!::write(fd[1], "x", 1); }
+};
+
+lldp::Frame sw(const char* mac, const char* desc) { return lldp::make_switch_frame(*MacAddr::parse(mac), "tor", "p", desc); }
+
+struct Fixture {
+    TmpDir tmp;
+    FakeNetOps ops;
+    agent::Config cfg;
+    Fixture() {
+        ops.add_link("ens0", 10, "02:00:00:00:00:10", false);
+        ops.add_link("ens1", 11, "02:00:00:00:00:11", true);
+        ops.add_link("ens2", 12, "02:00:00:00:00:12", false);
+        cfg.discovery.mode = topo::DiscoveryMode::None;
+        cfg.interfaces = "ens0,ens1,ens2";
+        cfg.configure = true;
+        cfg.keep_running = true;
+        cfg.wait_ns = 100000000;
+        cfg.link_wait_ns = 20000000;
+        cfg.labels.dir = tmp.path + "/features.d";
+        tmp.mkdir("features.d");
+        cfg.rccl_net = tmp.path + "/rccl-net.json";
+        cfg.status_file = tmp.path + "/status.json";
+    }
+    std::unique_ptr<ScriptedLldp> all_valid() {
+        auto s = std::make_unique<ScriptedLldp>();
+        s->frames["ens0"] = sw("02:aa:00:00:00:00", "no-alert 10.200.0.2/30");
+        s->frames["ens1"] = sw("02:aa:00:00:00:01", "no-alert 10.200.0.6/30");
+        s->frames["ens2"] = sw("02:aa:00:00:00:02", "no-alert 10.200.0.9/30");
+        return s;
+    }
+    agent::NmFactory nm(std::map<std::string, bool>* out = nullptr) {
+        return [out]() {
+            auto m = std::make_unique<MockNm>();
+            if (out) m->shared = out;
+            return m;
+        };
+    }
+};
+
+bool has_route(FakeNetOps& o, int idx, const char* dst, const char* gw) {
+    for (auto& r : o.routes)
+        if (r.ifindex == idx && r.dst.masked().str() == dst && (gw ? (r.gateway && r.gateway->str() == gw) : !r.gateway))
+            return true;
+    return false;
+}
+}  // namespace
+
+TEST(agent_l3_happy_path_and_sigterm_cleanup) {
+    Fixture f;
+    f.cfg.mtu = 9000;
+    Pipe stop;
+    stop.fire();  // SIGTERM already pending: run() returns right after publishing readiness
+    agent::Agent a(f.cfg, f.ops, f.all_valid(), f.nm());
+    // Observe the label while "idling": write_status happens before idle, label too.
+    a.run(stop.fd[0]);
+    CHECK(a.ready());
+    for (auto& n : a.nics()) CHECK(n.configured);
+    // After SIGTERM cleanup: no label, no IPv4, originally-down links down again.
+    CHECK(!path_exists(f.cfg.labels.path()));
+    CHECK(f.ops.addrs.empty());
+    CHECK(!(f.ops.links["ens0"].flags & IFF_UP));
+    CHECK(f.ops.links["ens1"].flags & IFF_UP);
+    CHECK(!(f.ops.links["ens2"].flags & IFF_UP));
+    CHECK_EQ(f.ops.links["ens0"].mtu, 9000);
+    auto j = read_file(f.cfg.rccl_net);
+    CHECK(j && j->find("\"NIC_IP\":\"10.200.0.1\"") != std::string::npos);
+    CHECK(j->find("\"NIC_IP\":\"10.200.0.10\"") != std::string::npos);
+    auto st = read_file(f.cfg.status_file);
+    CHECK(st && st->find("\"ready\":true") != std::string::npos && st->find("total_ready") != std::string::npos);
+}
+
+TEST(agent_l3_routes_and_label_while_running) {
+    Fixture f;
+    f.cfg.keep_running = false;  // configure and exit: state stays in place for inspection
+    agent::Agent a(f.cfg, f.ops, f.all_valid(), f.nm());
+    a.run(-1);
+    CHECK(has_route(f.ops, 10, "10.200.0.0/30", nullptr));
+    CHECK(has_route(f.ops, 10, "10.200.0.0/16", "10.200.0.2"));
+    CHECK(has_route(f.ops, 11, "10.200.0.4/30", nullptr));
+    CHECK(has_route(f.ops, 11, "10.200.0.0/16", "10.200.0.6"));
+    CHECK(has_route(f.ops, 12, "10.200.0.8/30", nullptr));
+    CHECK(has_route(f.ops, 12, "10.200.0.0/16", "10.200.0.9"));
+    CHECK_EQ(f.ops.addrs.size(), size_t(3));
+    CHECK(!path_exists(f.cfg.labels.path()));  // label only with --keep-running (main.go:239)
+}
+
+TEST(agent_reference_fixture_partial_failure) {
+    // network_test.go:138-202: one valid NIC, one garbage Port Description.
+    Fixture f;
+    auto s = f.all_valid();
+    s->frames["ens1"] = sw("02:aa:00:00:00:01", "garbage");
+    agent::Agent a(f.cfg, f.ops, std::move(s), f.nm());
+    bool threw = false;
+    try {
+        a.run(-1);
+    } catch (const agent::AgentError& e) {
+        threw = true;
+        CHECK(std::string(e.what()).find("Not all interfaces were configured (2/3)") != std::string::npos);
+    }
+    CHECK(threw);
+    CHECK(!path_exists(f.cfg.labels.path()));
+}
+
+TEST(agent_no_peers_is_an_error_unless_compat) {
+    Fixture f;
+    auto s = std::make_unique<ScriptedLldp>();
+    agent::Agent a(f.cfg, f.ops, std::move(s), f.nm());
+    CHECK_THROWS(a.run(-1));
+    Fixture g;
+    g.cfg.label_without_peers = true;  // reference quirk (main.go:212,239-246)
+    g.cfg.keep_running = true;
+    Pipe stop;
+    stop.fire();
+    std::string label_seen;
+    agent::Agent b(g.cfg, g.ops, std::make_unique<ScriptedLldp>(), g.nm());
+    b.run(stop.fd[0]);
+    CHECK(b.ready());
+}
+
+TEST(agent_l2_mode) {
+    Fixture f;
+    f.cfg.mode = "l2";
+    f.cfg.keep_running = false;
+    f.ops.addrs.push_back(nl::AddrInfo{10, AF_INET, *Ipv4::parse("192.168.1.5"), *Ipv4::parse("192.168.1.5"), 24, 0, ""});
+    agent::Agent a(f.cfg, f.ops, std::make_unique<ScriptedLldp>(), f.nm());
+    a.run(-1);
+    CHECK(f.ops.addrs.empty());  // existing IPv4 flushed, no new ones
+    CHECK(f.ops.links["ens0"].flags & IFF_UP);
+    CHECK(f.ops.links["ens2"].flags & IFF_UP);
+}
+
+TEST(agent_diagnostic_run_restores_down) {
+    Fixture f;
+    f.cfg.configure = false;
+    agent::Agent a(f.cfg, f.ops, f.all_valid(), f.nm());
+    a.run(-1);
+    CHECK(f.ops.addrs.empty());
+    CHECK(!(f.ops.links["ens0"].flags & IFF_UP));
+    CHECK(f.ops.links["ens1"].flags & IFF_UP);
+    for (auto& n : a.nics()) CHECK(n.addr);  // addresses were derived but not applied
+}
+
+TEST(agent_missing_or_no_interfaces) {
+    Fixture f;
+    f.cfg.interfaces = "ens0,nope";
+    agent::Agent a(f.cfg, f.ops, f.all_valid(), f.nm());
+    bool threw = false;
+    try {
+        a.run(-1);
+    } catch (const agent::AgentError& e) {
+        threw = std::string(e.what()) == "Not all interfaces were found in the system";
+    }
+    CHECK(threw);
+    Fixture g;
+    g.cfg.interfaces = "";
+    agent::Agent b(g.cfg, g.ops, g.all_valid(), g.nm());
+    threw = false;
+    try {
+        b.run(-1);
+    } catch (const agent::AgentError& e) {
+        threw = std::string(e.what()) == "No interfaces found";
+    }
+    CHECK(threw);
+    // Duplicates are de-duplicated (the reference would fail them as "not found").
+    Fixture h;
+    h.cfg.interfaces = "ens0,ens0, ens1 ,ens2";
+    h.cfg.keep_running = false;
+    agent::Agent c(h.cfg, h.ops, h.all_valid(), h.nm());
+    c.run(-1);
+    CHECK_EQ(c.nics().size(), size_t(3));
+}
+
+TEST(agent_sanitize) {
+    agent::Config c;
+    c.mtu = 100;
+    c.mode = "l3";
+    agent::sanitize(c);
+    CHECK_EQ(c.mtu, 1500);
+    CHECK_EQ(c.mode, std::string("L3"));
+    c.mtu = 100000;
+    agent::sanitize(c);
+    CHECK_EQ(c.mtu, 9000);
+    c.mode = "L4";
+    CHECK_THROWS(agent::sanitize(c));
+}
+
+TEST(agent_fault_injection_nonfatal_ops) {
+    for (const char* op : {"link_set_up", "link_set_mtu"}) {
+        Fixture f;
+        f.cfg.keep_running = false;
+        f.cfg.interfaces = "ens1";  // already up: LLDP still runs
+        f.ops.fail.insert(op);
+        agent::Agent a(f.cfg, f.ops, f.all_valid(), f.nm());
+        a.run(-1);
+        CHECK(a.nics()[0].configured);
+    }
+}
+
+TEST(agent_fault_injection_fatal_ops) {
+    for (const char* op : {"addr_list", "subscribe_links"}) {
+        Fixture f;
+        f.ops.fail.insert(op);
+        agent::Agent a(f.cfg, f.ops, f.all_valid(), f.nm());
+        CHECK_THROWS(a.run(-1));
+    }
+    Fixture g;
+    g.ops.addrs.push_back(nl::AddrInfo{10, AF_INET, *Ipv4::parse("192.168.1.5"), *Ipv4::parse("192.168.1.5"), 24, 0, ""});
+    g.ops.fail.insert("addr_del");
+    agent::Agent b(g.cfg, g.ops, g.all_valid(), g.nm());
+    bool threw = false;
+    try {
+        b.run(-1);
+    } catch (const agent::AgentError& e) {
+        threw = std::string(e.what()).find("Failed to remove any existing IPs") == 0;
+    }
+    CHECK(threw);
+}
+
+TEST(agent_configure_interface_paths) {
+    Fixture f;
+    agent::Agent a(f.cfg, f.ops, f.all_valid(), f.nm());
+    f.cfg.keep_running = false;
+    // Build state through a diagnostic run, then drive configure_interface directly.
+    agent::Config c = f.cfg;
+    c.configure = false;
+    agent::Agent d(c, f.ops, f.all_valid(), f.nm());
+    d.run(-1);
+    auto nics = d.nics();
+    // Already-configured address: the /30 route must be ensured explicitly (network.go:446-452).
+    f.ops.links["ens1"].flags |= IFF_UP;
+    f.ops.addrs.push_back(nl::AddrInfo{11, AF_INET, *Ipv4::parse("10.200.0.5"), *Ipv4::parse("10.200.0.5"), 30, 0, ""});
+    agent::Agent e(c, f.ops, f.all_valid(), f.nm());
+    NicState n = nics[1];
+    CHECK(e.configure_interface(n));
+    CHECK(has_route(f.ops, 11, "10.200.0.4/30", nullptr));
+    CHECK(has_route(f.ops, 11, "10.200.0.0/16", "10.200.0.6"));
+    // Second call: EEXIST on both routes is success.
+    n.configured = false;
+    CHECK(e.configure_interface(n));
+    // addr_add failure -> not configured
+    NicState m = nics[0];
+    f.ops.fail.insert("addr_add");
+    CHECK(!e.configure_interface(m));
+    f.ops.fail.clear();
+    f.ops.fail.insert("route_append");
+    CHECK(!e.configure_interface(m));
+    CHECK(!m.config_error.empty());
+}
+
+TEST(agent_interrupted_during_lldp) {
+    Fixture f;
+    auto s = std::make_unique<ScriptedLldp>();
+    s->result_if_unfinished = pkt::ListenResult::Interrupted;
+    agent::Agent a(f.cfg, f.ops, std::move(s), f.nm());
+    a.run(-1);
+    CHECK(!a.ready());
+    CHECK(!(f.ops.links["ens0"].flags & IFF_UP));
+    CHECK(!path_exists(f.cfg.labels.path()));
+}
+
+TEST(agent_networkmanager_paths) {
+    Fixture f;
+    f.cfg.disable_nm = true;
+    f.cfg.keep_running = false;
+    f.cfg.nm_keyfile_dir = f.tmp.path + "/NetworkManager/conf.d";
+    f.tmp.mkdir("NetworkManager");
+    std::map<std::string, bool> seen;
+    agent::Agent a(f.cfg, f.ops, f.all_valid(), f.nm(&seen));
+    a.run(-1);
+    CHECK_EQ(seen.size(), size_t(3));
+    CHECK(!seen["ens0"]);
+    CHECK(!seen["ens1"]);
+    CHECK(seen["eth9"]);
+    auto kf = read_file(f.cfg.nm_keyfile_dir + "/99-amd-network-operator.conf");
+    CHECK(kf && kf->find("unmanaged-devices=interface-name:ens0;interface-name:ens1;interface-name:ens2") != std::string::npos);
+
+    // NM absent (version query fails) -> silently skipped (networkmanager.go:81-86).
+    MockNm nm1;
+    nm1.fail_version = true;
+    CHECK(nm::disable_for_interfaces(nm1, {"ens0"}).empty());
+    CHECK(nm1.managed["ens0"]);
+    MockNm nm2;
+    nm2.fail_devices = true;
+    CHECK_THROWS(nm::disable_for_interfaces(nm2, {"ens0"}));
+    MockNm nm3;
+    nm3.fail_set = true;
+    CHECK_THROWS(nm::disable_for_interfaces(nm3, {"ens0"}));
+    // Factory failure is fatal.
+    Fixture g;
+    g.cfg.disable_nm = true;
+    agent::Agent b(g.cfg, g.ops, g.all_valid(), []() -> std::unique_ptr<nm::NetworkManagerIf> { throw std::runtime_error("no bus"); });
+    CHECK_THROWS(b.run(-1));
+}
+
+TEST(agent_stale_label_removed_and_networkd) {
+    Fixture f;
+    f.tmp.write("features.d/scale-out-readiness.txt", "stale\n");
+    f.cfg.keep_running = false;
+    f.cfg.networkd = f.tmp.path + "/networkd";
+    agent::Agent a(f.cfg, f.ops, f.all_valid(), f.nm());
+    a.run(-1);
+    CHECK(!path_exists(f.cfg.labels.path()));
+    CHECK(path_exists(f.cfg.networkd + "/ens0.network"));
+    CHECK(path_exists(f.cfg.networkd + "/ens2.network"));
+}

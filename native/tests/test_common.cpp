@@ -1,0 +1,93 @@
+#include "check.hpp"
+#include "netop/cli.hpp"
+#include "netop/common.hpp"
+
+using namespace netop;
+
+TEST(mac_parse_and_format) {
+    auto m = MacAddr::parse("AA:bb:0c:dd:ee:0F");
+    CHECK(m);
+    CHECK_EQ(m->str(), std::string("aa:bb:0c:dd:ee:0f"));
+    CHECK(!MacAddr::parse("aa:bb:cc:dd:ee"));
+    CHECK(!MacAddr::parse("aa:bb:cc:dd:ee:gg"));
+    CHECK(MacAddr::parse("00-11-22-33-44-55"));
+}
+
+TEST(ipv4_parse_strict) {
+    CHECK_EQ(Ipv4::parse("10.200.10.2")->str(), std::string("10.200.10.2"));
+    CHECK(!Ipv4::parse("10.200.10"));
+    CHECK(!Ipv4::parse("10.200.10.256"));
+    CHECK(!Ipv4::parse("10.200.010.2"));  // leading zero rejected like Go
+    CHECK(!Ipv4::parse("10.200.10.2 "));
+    CHECK(!Ipv4::parse(""));
+}
+
+TEST(prefix_parse_and_mask) {
+    auto p = Ipv4Prefix::parse("10.200.10.2/30");
+    CHECK(p);
+    CHECK_EQ(p->len, 30);
+    CHECK_EQ(p->network().str(), std::string("10.200.10.0"));
+    CHECK_EQ(p->mask().str(), std::string("255.255.255.252"));
+    CHECK(!Ipv4Prefix::parse("10.0.0.1/33"));
+    CHECK(!Ipv4Prefix::parse("10.0.0.1/"));
+    CHECK(!Ipv4Prefix::parse("10.0.0.1/030"));
+    CHECK(!Ipv4Prefix::parse("10.0.0.1"));
+    CHECK_EQ(Ipv4Prefix::parse("10.200.10.1/16")->masked().str(), std::string("10.200.0.0/16"));
+}
+
+TEST(split_semantics_match_go) {
+    auto v = split("a  b", ' ');
+    CHECK_EQ(v.size(), size_t(3));
+    CHECK_EQ(v[1], std::string(""));
+    CHECK_EQ(split("", ' ').size(), size_t(1));
+    auto f = split_ws("  a \t b  ");
+    CHECK_EQ(f.size(), size_t(2));
+    CHECK_EQ(f[1], std::string("b"));
+}
+
+TEST(go_durations) {
+    CHECK_EQ(*parse_go_duration("90s"), int64_t(90) * 1000000000);
+    CHECK_EQ(*parse_go_duration("1m30s"), int64_t(90) * 1000000000);
+    CHECK_EQ(*parse_go_duration("250ms"), int64_t(250) * 1000000);
+    CHECK_EQ(*parse_go_duration("1.5s"), int64_t(1500) * 1000000);
+    CHECK_EQ(*parse_go_duration("0"), int64_t(0));
+    CHECK_EQ(*parse_go_duration("2h"), int64_t(7200) * 1000000000);
+    CHECK(!parse_go_duration("90"));
+    CHECK(!parse_go_duration("s"));
+    CHECK(!parse_go_duration("5x"));
+    CHECK_EQ(format_go_duration(int64_t(90) * 1000000000), std::string("1m30s"));
+    CHECK_EQ(format_go_duration(int64_t(30) * 1000000000), std::string("30s"));
+}
+
+TEST(flagset_pflag_semantics) {
+    std::string mode = "L3", ifaces;
+    bool configure = false, keep = false;
+    int mtu = 1500, v = 0;
+    int64_t wait = 30000000000LL;
+    cli::FlagSet fs("discover");
+    fs.add_string("mode", &mode, "");
+    fs.add_bool("configure", &configure, "");
+    fs.add_bool("keep-running", &keep, "");
+    fs.add_string("interfaces", &ifaces, "");
+    fs.add_int("mtu", &mtu, "");
+    fs.add_int("v", &v, "");
+    fs.shorthand('v', "v");
+    fs.add_duration("wait", &wait, "");
+    fs.alias("gaudinet", "interfaces");
+    const char* argv[] = {"discover", "--configure=true", "--keep-running", "--mode", "l2", "--mtu=9000",
+                          "-v", "3", "--wait=90s", "--gaudinet=x"};
+    fs.parse(10, const_cast<char**>(argv));
+    CHECK(configure);
+    CHECK(keep);
+    CHECK_EQ(mode, std::string("l2"));
+    CHECK_EQ(mtu, 9000);
+    CHECK_EQ(v, 3);
+    CHECK_EQ(wait, int64_t(90) * 1000000000);
+    CHECK_EQ(ifaces, std::string("x"));
+    const char* bad[] = {"discover", "--nope"};
+    CHECK_THROWS(fs.parse(2, const_cast<char**>(bad)));
+    const char* badbool[] = {"discover", "--configure=maybe"};
+    CHECK_THROWS(fs.parse(2, const_cast<char**>(badbool)));
+    const char* baddur[] = {"discover", "--wait=90"};
+    CHECK_THROWS(fs.parse(2, const_cast<char**>(baddur)));
+}

@@ -1,0 +1,147 @@
+#include "check.hpp"
+#include "netop/topology.hpp"
+#include "tmpdir.hpp"
+
+using namespace netop;
+using namespace netop::topo;
+
+namespace {
+// Builds a fake sysfs PCI device directory with a driver symlink.
+void pci(const TmpDir& t, const std::string& path, const char* driver, const char* vendor, const char* device, int numa) {
+    t.mkdir("devices/" + path);
+    t.write("devices/" + path + "/vendor", std::string(vendor) + "\n");
+    t.write("devices/" + path + "/device", std::string(device) + "\n");
+    t.write("devices/" + path + "/numa_node", std::to_string(numa) + "\n");
+    t.mkdir(std::string("bus/pci/drivers/") + driver);
+    t.symlink(std::string("bus/pci/drivers/") + driver, "devices/" + path + "/driver");
+}
+void netdev(const TmpDir& t, const std::string& pcipath, const std::string& ifname, const char* mac) {
+    t.write("devices/" + pcipath + "/net/" + ifname + "/address", std::string(mac) + "\n");
+    t.symlink("devices/" + pcipath + "/net/" + ifname, "class/net/" + ifname);
+}
+void build_node(const TmpDir& t) {
+    // Two GPUs, each behind a switch with a NIC (same layout as a real MI355X node), plus a
+    // management NIC on its own root port and a virtual interface.
+    const std::string g0 = "pci0000:00/0000:00:01.1/0000:01:00.0/0000:02:08.0/0000:06:00.0/0000:07:10.0/0000:08:00.0/0000:09:00.0/0000:0a:00.0";
+    const std::string n0 = "pci0000:00/0000:00:01.1/0000:01:00.0/0000:02:00.0/0000:03:00.0/0000:04:10.0/0000:05:00.0";
+    const std::string g1 = "pci0000:19/0000:19:01.1/0000:1a:00.0/0000:1b:08.0/0000:1f:00.0/0000:20:10.0/0000:21:00.0/0000:22:00.0/0000:23:00.0";
+    const std::string n1 = "pci0000:19/0000:19:01.1/0000:1a:00.0/0000:1b:00.0/0000:1c:00.0/0000:1d:10.0/0000:1e:00.0";
+    const std::string mg = "pci0000:37/0000:37:01.1/0000:38:00.0";
+    pci(t, g0, "amdgpu", "0x1002", "0x75a3", 0);
+    pci(t, g1, "amdgpu", "0x1002", "0x75a3", 0);
+    pci(t, n0, "mlx5_core", "0x15b3", "0x1021", 0);
+    pci(t, n1, "mlx5_core", "0x15b3", "0x1021", 0);
+    pci(t, mg, "mlx5_core", "0x15b3", "0x1021", 0);
+    t.symlink("devices/" + g0, "bus/pci/drivers/amdgpu/0000:0a:00.0");
+    t.symlink("devices/" + g1, "bus/pci/drivers/amdgpu/0000:23:00.0");
+    netdev(t, n0, "enp5s0np0", "02:00:00:00:00:05");
+    netdev(t, n1, "enp30s0np0", "02:00:00:00:00:30");
+    netdev(t, mg, "ens9np0", "02:00:00:00:00:09");
+    t.mkdir("devices/" + n1 + "/infiniband/mlx5_3");
+    t.mkdir("devices/" + n0 + "/infiniband/mlx5_1");
+    t.write("devices/virtual/net/lo/address", "00:00:00:00:00:00\n");
+    t.symlink("devices/virtual/net/lo", "class/net/lo");
+}
+}  // namespace
+
+TEST(topology_affine_pairing_excludes_mgmt_nic) {
+    TmpDir t;
+    build_node(t);
+    DiscoveryOptions opt;
+    auto r = discover(opt, t.path);
+    CHECK_EQ(r.gpus.size(), size_t(2));
+    CHECK_EQ(r.gpus[0].pci.bdf, std::string("0000:0a:00.0"));
+    CHECK_EQ(r.gpus[0].pci.device, uint32_t(0x75a3));
+    CHECK_EQ(r.nics.size(), size_t(3));
+    CHECK_EQ(r.pairs.size(), size_t(2));
+    CHECK_EQ(r.ifnames.size(), size_t(2));
+    CHECK_EQ(r.ifnames[0], std::string("enp5s0np0"));
+    CHECK_EQ(r.ifnames[1], std::string("enp30s0np0"));
+    CHECK_EQ(r.nics[size_t(r.pairs[1].nic)].rdma_dev, std::string("mlx5_3"));
+    CHECK(r.pairs[0].path == PathType::PXB);
+    CHECK_EQ(r.pairs[0].common_depth, 3);
+    // Accepting anything up to SYS would still pair each GPU with its own switch-local NIC.
+    opt.max_path = PathType::SYS;
+    auto r2 = discover(opt, t.path);
+    CHECK_EQ(r2.ifnames[0], std::string("enp5s0np0"));
+    // Driver allow-list filters NICs.
+    opt.nic_drivers = {"bnxt_en"};
+    CHECK(discover(opt, t.path).ifnames.empty());
+}
+
+TEST(topology_accel_mode_reference_compatible) {
+    TmpDir t;
+    // habanalabs-style: netdevs directly under the accelerator PCI function.
+    const std::string d = "pci0000:00/0000:00:02.0/0000:33:00.0";
+    pci(t, d, "habanalabs", "0x1da3", "0x1020", 0);
+    t.symlink("devices/" + d, "bus/pci/drivers/habanalabs/0000:33:00.0");
+    t.write("devices/" + d + "/net/eth_a/address", "02:00:00:00:00:01\n");
+    t.write("devices/" + d + "/net/eth_b/address", "02:00:00:00:00:02\n");
+    DiscoveryOptions opt;
+    opt.mode = DiscoveryMode::Accel;
+    opt.accel_driver = "habanalabs";
+    auto r = discover(opt, t.path);
+    CHECK_EQ(r.ifnames.size(), size_t(2));
+    CHECK(discover(opt, t.path + "/nonexistent").ifnames.empty());
+}
+
+TEST(topology_path_types) {
+    PciDev a, b;
+    a.chain = {"pci0000:00", "0000:00:01.1", "0000:01:00.0", "0000:02:00.0", "0000:03:00.0"};
+    b.chain = {"pci0000:00", "0000:00:01.1", "0000:01:00.0", "0000:02:04.0", "0000:04:00.0"};
+    CHECK(path_between(a, b) == PathType::PIX);
+    b.chain = {"pci0000:00", "0000:00:03.1", "0000:05:00.0"};
+    CHECK(path_between(a, b) == PathType::PHB);
+    b.chain = {"pci0000:40", "0000:40:01.1", "0000:41:00.0"};
+    a.numa = b.numa = 1;
+    CHECK(path_between(a, b) == PathType::NODE);
+    b.numa = 0;
+    CHECK(path_between(a, b) == PathType::SYS);
+}
+
+TEST(topology_rocev2_gid_lookup) {
+    TmpDir t;
+    std::string p = "class/infiniband/mlx5_1/ports/1/";
+    t.write(p + "gids/0", "fe80:0000:0000:0000:0000:00ff:fe00:0005\n");
+    t.write(p + "gid_attrs/types/0", "IB/RoCE v1\n");
+    t.write(p + "gids/1", "fe80:0000:0000:0000:0000:00ff:fe00:0005\n");
+    t.write(p + "gid_attrs/types/1", "RoCE v2\n");
+    t.write(p + "gids/2", "0000:0000:0000:0000:0000:ffff:0ac8:0001\n");
+    t.write(p + "gid_attrs/types/2", "IB/RoCE v1\n");
+    t.write(p + "gids/3", "0000:0000:0000:0000:0000:ffff:0ac8:0001\n");
+    t.write(p + "gid_attrs/types/3", "RoCE v2\n");
+    auto idx = find_rocev2_gid_index(t.path, "mlx5_1", 1, *Ipv4::parse("10.200.0.1"));
+    CHECK(idx);
+    CHECK_EQ(*idx, 3);
+    CHECK(!find_rocev2_gid_index(t.path, "mlx5_1", 1, *Ipv4::parse("10.200.0.5")));
+    CHECK(!find_rocev2_gid_index(t.path, "mlx5_9", 1, *Ipv4::parse("10.200.0.1")));
+}
+
+TEST(topology_kfd_xgmi_mesh) {
+    TmpDir t;
+    std::string base = "class/kfd/kfd/topology/nodes/";
+    t.write(base + "0/properties", "cpu_cores_count 96\nsimd_count 0\n");
+    int n = 4;
+    for (int g = 1; g <= n; ++g) {
+        t.write(base + std::to_string(g) + "/properties",
+                strfmt("simd_count 1024\nvendor_id 4098\ndevice_id 30115\nlocation_id %d\ndomain 0\nhive_id 77\n", (g * 0x10) << 8));
+        int li = 0;
+        t.write(base + std::to_string(g) + "/io_links/" + std::to_string(li++) + "/properties", "type 2\nnode_from " + std::to_string(g) + "\nnode_to 0\nmax_bandwidth 64000\n");
+        for (int h = 1; h <= n; ++h) {
+            if (h == g || (g == 1 && h == 4) || (g == 4 && h == 1)) continue;  // 1<->4 missing
+            t.write(base + std::to_string(g) + "/io_links/" + std::to_string(li++) + "/properties",
+                    strfmt("type 11\nnode_from %d\nnode_to %d\nweight 15\nmin_bandwidth 76000\nmax_bandwidth 76000\n", g, h));
+        }
+    }
+    auto x = read_xgmi(t.path);
+    CHECK_EQ(x.gpus.size(), size_t(4));
+    CHECK_EQ(x.gpus[0].bdf(), std::string("0000:10:00.0"));
+    CHECK_EQ(x.pairs_expected, 6);
+    CHECK_EQ(x.pairs_connected, 5);
+    CHECK(!x.full_mesh());
+    CHECK_EQ(x.missing.size(), size_t(1));
+    CHECK_EQ(x.missing[0].first, std::string("0000:10:00.0"));
+    CHECK_EQ(x.missing[0].second, std::string("0000:40:00.0"));
+    CHECK_EQ(x.min_link_bw_mbs, uint64_t(76000));
+    CHECK_EQ(x.per_gpu_bw_mbs(), uint64_t(2 * 76000));
+}

@@ -1,0 +1,125 @@
+// `discover` — the MI355X network operator's node agent (DaemonSet container entrypoint).
+//
+// Reference: cmd/discover/main.go (cobra command `discover`).  Same flag names and
+// defaults (:281-298) plus klog's -v/--v; MI355X additions are documented in --help.
+#include <signal.h>
+#include <sys/signalfd.h>
+#include <unistd.h>
+
+#include <cstdio>
+#include <cstring>
+#include <iostream>
+
+#include "netop/agent.hpp"
+#include "netop/cli.hpp"
+#include "netop/log.hpp"
+
+using namespace netop;
+
+int main(int argc, char** argv) {
+    agent::Config cfg;
+    int verbosity = 0;
+    bool show_help = false, show_version = false, logtostderr = true, skip_headers = false;
+    std::string log_file, logging_format = "text", discovery_mode = "affine", nic_drivers, token_policy = "compat-then-last",
+                                         max_path = "PXB", vmodule, stderrthreshold;
+
+    cli::FlagSet fs("discover");
+    // klog flags first (the reference adds the Go flag set before its own, SortFlags=false).
+    fs.add_int("v", &verbosity, "number for the log level verbosity");
+    fs.shorthand('v', "v");
+    fs.add_bool("logtostderr", &logtostderr, "log to standard error instead of files");
+    fs.add_bool("alsologtostderr", &logtostderr, "log to standard error as well as files", true);
+    fs.add_string("log_file", &log_file, "If non-empty, use this log file");
+    fs.add_bool("skip_headers", &skip_headers, "If true, avoid header prefixes in the log messages");
+    fs.add_string("vmodule", &vmodule, "comma-separated list of pattern=N settings (accepted, ignored)", true);
+    fs.add_string("stderrthreshold", &stderrthreshold, "accepted for klog compatibility", true);
+    fs.add_string("logging-format", &logging_format, "log format: text (klog) or json");
+
+    fs.add_string("mode", &cfg.mode, "'L2' for network layer 2 or 'L3' for network layer 3 (L3) using LLDP");
+    fs.add_bool("configure", &cfg.configure, "Configure L3 network with LLDP or set interfaces up with L2 networks");
+    fs.add_bool("disable-networkmanager", &cfg.disable_nm, "Disable Host's NetworkManager for interfaces");
+    fs.add_string("interfaces", &cfg.interfaces, "Comma separated list of additional network interfaces");
+    fs.add_duration("wait", &cfg.wait_ns, "Time to wait for LLDP packets");
+    fs.add_string("rccl-net", &cfg.rccl_net, "RCCL scale-out NIC file path (NIC_NET_CONFIG JSON)");
+    fs.alias("gaudinet", "rccl-net");
+    fs.add_bool("keep-running", &cfg.keep_running, "Keep running after any configurations are done");
+    fs.add_string("systemd-networkd", &cfg.networkd, "Write systemd networkd configuration files to given directory");
+    fs.add_int("mtu", &cfg.mtu, "MTU value to set for interfaces");
+
+    fs.add_string("nic-discovery", &discovery_mode, "scale-out NIC discovery: affine (NICs sharing a PCIe switch with an amdgpu GPU), accel (netdevs under the accelerator PCI function), none");
+    fs.add_string("accel-driver", &cfg.discovery.accel_driver, "accelerator PCI driver to enumerate");
+    fs.add_string("nic-drivers", &nic_drivers, "comma separated NIC driver allow-list for affine discovery (default: common RoCE drivers)");
+    fs.add_string("max-path", &max_path, "farthest GPU<->NIC PCIe path type accepted: PIX, PXB, PHB, NODE, SYS");
+    fs.add_string("token-policy", &token_policy, "Port Description address token: compat (token 1), compat-then-last, any");
+    fs.add_bool("lldp-promisc", &cfg.lldp_promisc, "put interfaces in promiscuous mode while listening for LLDP");
+    fs.add_bool("pipeline", &cfg.pipeline, "configure each interface as soon as its LLDP frame arrives");
+    fs.add_bool("label-without-peers", &cfg.label_without_peers, "publish the readiness label even when no LLDP peer was found (reference behaviour)");
+    fs.add_string("nfd-features-dir", &cfg.labels.dir, "NFD local feature source directory");
+    fs.add_string("nfd-label-file", &cfg.labels.file, "readiness label file name inside the features directory");
+    fs.add_string("rccl-env", &cfg.rccl_env, "write an RCCL environment file (NCCL_IB_HCA, NCCL_IB_GID_INDEX, ...)");
+    fs.add_string("status-file", &cfg.status_file, "write a JSON status document (per-NIC results, phase timings)");
+    fs.add_string("nm-keyfile-dir", &cfg.nm_keyfile_dir, "with --disable-networkmanager, also persist an unmanaged-devices keyfile here");
+    fs.add_int("xgmi-expect", &cfg.xgmi_expect_links, "verify the xGMI mesh before labelling: -1 off, 0 full mesh, N GPU pairs");
+    fs.add_duration("link-wait", &cfg.link_wait_ns, "time to wait for link state echoes from the kernel");
+    fs.add_bool("help", &show_help, "help for discover");
+    fs.shorthand('h', "help");
+    fs.add_bool("version", &show_version, "print version");
+
+    try {
+        fs.parse(argc, argv);
+    } catch (const std::invalid_argument& e) {
+        std::fprintf(stderr, "Error: %s\n%s", e.what(), fs.usage().c_str());
+        return 2;
+    }
+    if (show_help) {
+        std::cout << "Discover and optionally configure network devices\n\n" << fs.usage();
+        return 0;
+    }
+    if (show_version) {
+        std::cout << "discover (amd network operator) " << NETOP_VERSION << "\n";
+        return 0;
+    }
+    log::set_verbosity(verbosity);
+    log::set_skip_headers(skip_headers);
+    if (!log_file.empty()) log::set_log_file(log_file);
+    if (logging_format == "json") log::set_format(log::Format::Json);
+
+    auto dm = topo::parse_discovery_mode(discovery_mode);
+    auto tp = l3::parse_token_policy(token_policy);
+    if (!dm || !tp) {
+        std::fprintf(stderr, "Error: invalid --nic-discovery or --token-policy\n");
+        return 2;
+    }
+    cfg.discovery.mode = *dm;
+    cfg.token_policy = *tp;
+    if (!nic_drivers.empty()) cfg.discovery.nic_drivers = split(nic_drivers, ',');
+    static const std::map<std::string, topo::PathType> paths{{"PIX", topo::PathType::PIX}, {"PXB", topo::PathType::PXB},
+                                                             {"PHB", topo::PathType::PHB}, {"NODE", topo::PathType::NODE},
+                                                             {"SYS", topo::PathType::SYS}};
+    auto pit = paths.find(to_upper(max_path));
+    if (pit == paths.end()) {
+        std::fprintf(stderr, "Error: invalid --max-path '%s'\n", max_path.c_str());
+        return 2;
+    }
+    cfg.discovery.max_path = pit->second;
+
+    // SIGTERM/SIGINT are consumed through a signalfd so every wait in the state machine
+    // (LLDP epoll, idle) can observe them without async-signal-safety concerns.
+    sigset_t mask;
+    sigemptyset(&mask);
+    sigaddset(&mask, SIGTERM);
+    sigaddset(&mask, SIGINT);
+    sigprocmask(SIG_BLOCK, &mask, nullptr);
+    int sfd = signalfd(-1, &mask, SFD_CLOEXEC | SFD_NONBLOCK);
+
+    try {
+        nl::Rtnl rtnl;
+        agent::Agent a(cfg, rtnl, agent::make_packet_source(cfg.lldp_promisc), [] { return nm::connect_system_bus(); });
+        a.run(sfd);
+    } catch (const std::exception& e) {
+        NLOG_E("%s", e.what());
+        std::fprintf(stderr, "Error: %s\n", e.what());
+        return 1;
+    }
+    return 0;
+}

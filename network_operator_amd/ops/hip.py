@@ -1,0 +1,117 @@
+"""ctypes binding of ``libnetop_hip.so`` (native/hip/netop_hip.hip, gfx950).
+
+The kernels validate what the operator configures: all-reduce results over RCCL (bf16
+pattern fill / verify, exact for any reduction order) and xGMI link integrity and bandwidth
+(peer-pull copy).  Every entry point raises if the library is missing — on a GPU box these
+ops never fall back to eager PyTorch.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import threading
+
+from ..utils.paths import hip_library
+
+_lib = None
+_lock = threading.Lock()
+
+
+class HipError(RuntimeError):
+    pass
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    with _lock:
+        if _lib is None:
+            L = ctypes.CDLL(str(hip_library()))
+            u64, i32, u32, vp = ctypes.c_uint64, ctypes.c_int, ctypes.c_uint32, ctypes.c_void_p
+            L.netop_hip_version.restype = i32
+            L.netop_fill_pattern.argtypes = [vp, u64, u32, i32, vp]
+            L.netop_fill_pattern.restype = i32
+            L.netop_fill_expected_sum.argtypes = [vp, u64, u32, i32, vp]
+            L.netop_fill_expected_sum.restype = i32
+            L.netop_verify_sum.argtypes = [vp, u64, u32, i32, vp, vp]
+            L.netop_verify_sum.restype = i32
+            L.netop_copy.argtypes = [vp, vp, u64, vp]
+            L.netop_copy.restype = i32
+            L.netop_xgmi_probe.argtypes = [u64, i32, i32, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
+                                           ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_ulonglong)]
+            L.netop_xgmi_probe.restype = i32
+            _lib = L
+    return _lib
+
+
+def _check(rc: int, what: str) -> None:
+    if rc != 0:
+        raise HipError(f"{what} failed with hipError {rc}")
+
+
+def _stream(tensor):
+    import torch
+
+    return ctypes.c_void_p(torch.cuda.current_stream(tensor.device).cuda_stream)
+
+
+def _check_buf(t):
+    import torch
+
+    if t.dtype != torch.bfloat16 or not t.is_cuda or not t.is_contiguous():
+        raise ValueError("expected a contiguous bfloat16 CUDA tensor")
+    if t.numel() % 8 or t.data_ptr() % 16:
+        raise ValueError("numel must be a multiple of 8 and the buffer 16-byte aligned")
+
+
+def fill_pattern(t, seed: int, rank: int) -> None:
+    """Fill ``t`` (bf16) with rank ``rank``'s deterministic integer pattern in [-4, 4]."""
+    _check_buf(t)
+    _check(lib().netop_fill_pattern(ctypes.c_void_p(t.data_ptr()), t.numel(), seed & 0xFFFFFFFF, rank, _stream(t)),
+           "netop_fill_pattern")
+
+
+def fill_expected_sum(t, seed: int, world: int) -> None:
+    """Fill ``t`` with Σ_{r<world} pattern(r) — what an all-reduce(sum) must produce."""
+    _check_buf(t)
+    _check(lib().netop_fill_expected_sum(ctypes.c_void_p(t.data_ptr()), t.numel(), seed & 0xFFFFFFFF, world, _stream(t)),
+           "netop_fill_expected_sum")
+
+
+def verify_sum(t, seed: int, world: int) -> int:
+    """Number of elements of ``t`` that differ from the expected all-reduce sum (synchronises)."""
+    import torch
+
+    _check_buf(t)
+    err = torch.zeros(1, dtype=torch.int64, device=t.device)
+    _check(lib().netop_verify_sum(ctypes.c_void_p(t.data_ptr()), t.numel(), seed & 0xFFFFFFFF, world,
+                                  ctypes.c_void_p(err.data_ptr()), _stream(t)), "netop_verify_sum")
+    return int(err.item())
+
+
+def copy(src, dst) -> None:
+    """16-byte-vector device copy (src may live on a peer GPU with peer access enabled)."""
+    nbytes = src.numel() * src.element_size()
+    if dst.numel() * dst.element_size() < nbytes:
+        raise ValueError("destination too small")
+    _check(lib().netop_copy(ctypes.c_void_p(src.data_ptr()), ctypes.c_void_p(dst.data_ptr()), nbytes, _stream(dst)),
+           "netop_copy")
+
+
+def xgmi_probe(nbytes: int = 256 << 20, iters: int = 10, max_gpus: int = 8) -> dict:
+    """Pull-bandwidth and integrity probe over every visible GPU pair (see netop_hip.hip)."""
+    n = 64
+    single = (ctypes.c_double * (n * n))()
+    agg = (ctypes.c_double * n)()
+    n_out = ctypes.c_int(0)
+    errors = ctypes.c_ulonglong(0)
+    _check(lib().netop_xgmi_probe(nbytes, iters, max_gpus, single, agg, ctypes.byref(n_out), ctypes.byref(errors)),
+           "netop_xgmi_probe")
+    g = n_out.value
+    return {
+        "gpus": g,
+        "bytes": nbytes,
+        "iters": iters,
+        "errors": errors.value,
+        "link_GBps": [[single[d * g + p] for p in range(g)] for d in range(g)],
+        "aggregate_GBps": [agg[d] for d in range(g)],
+    }
