@@ -58,6 +58,10 @@ struct Config {
     std::string nm_keyfile_dir;          // --nm-keyfile-dir
     int xgmi_expect_links = -1;          // -1 off; 0 = full mesh among discovered GPUs; N = exact pairs
     int64_t link_wait_ns = 3LL * 1000000000;  // netlink echo wait (network.go:251)
+    bool lldp_announce = true;           // transmit our own LLDPDU (triggers switch fast start)
+    int64_t announce_interval_ns = 1000000000LL;  // re-announce to still-silent NICs
+    int announce_count = 3;
+    std::string node_name;               // LLDP System Name ($NODE_NAME, else hostname)
 };
 
 // Sanitises in place (MTU clamp to [1500, 9000], mode upper-cased); throws on a bad mode.
@@ -71,7 +75,16 @@ class LldpSource {
     virtual pkt::ListenResult run(int64_t deadline,
                                   const std::function<bool(const std::string&, const lldp::Frame&)>& on_frame,
                                   int stop_fd) = 0;
+    // Transmits our own LLDPDU on an interface (no-op for sources that cannot transmit).
+    virtual void announce(const std::string& ifname, const std::vector<uint8_t>& frame) {}
 };
+
+// The LLDPDU the agent advertises for one of its NICs.  Announcing ourselves makes an
+// IEEE 802.1AB-2009 switch see a *new neighbour* and enter fast transmission (txFast), so
+// its Port Description arrives within ~1 s instead of up to msgTxInterval (30 s).
+// ttl = 0 builds the shutdown LLDPDU sent on cleanup.
+lldp::Frame make_node_frame(const std::string& node_name, const std::string& ifname, const MacAddr& mac,
+                            const std::string& gpu_bdf, uint16_t ttl = 120);
 std::unique_ptr<LldpSource> make_packet_source(bool promisc);
 
 using NmFactory = std::function<std::unique_ptr<nm::NetworkManagerIf>()>;

@@ -63,6 +63,8 @@ class LldpListener {
     ~LldpListener();
     void add(const std::string& ifname, int ifindex, const MacAddr& own_mac, bool promisc);
     void remove(const std::string& ifname);
+    // Transmits a frame on a listened interface; false if the interface is unknown.
+    bool send(const std::string& ifname, const std::vector<uint8_t>& frame);
     size_t size() const { return socks_.size(); }
 
     // Runs until `on_frame` returns true (stop), the absolute CLOCK_MONOTONIC deadline

@@ -44,6 +44,9 @@ class PacketSource final : public LldpSource {
                (unsigned long long)s.own, (unsigned long long)s.malformed, (unsigned long long)s.wakeups);
         return r;
     }
+    void announce(const std::string& ifname, const std::vector<uint8_t>& frame) override {
+        listener_.send(ifname, frame);
+    }
 
    private:
     bool promisc_;
@@ -58,6 +61,23 @@ bool fd_readable(int fd) {
 }  // namespace
 
 std::unique_ptr<LldpSource> make_packet_source(bool promisc) { return std::make_unique<PacketSource>(promisc); }
+
+lldp::Frame make_node_frame(const std::string& node_name, const std::string& ifname, const MacAddr& mac,
+                            const std::string& gpu_bdf, uint16_t ttl) {
+    lldp::Frame f;
+    f.dst = lldp::kNearestBridge;
+    f.src = mac;
+    f.chassis_subtype = lldp::kChassisLocal;
+    f.chassis_id = node_name.empty() ? mac.str() : node_name;
+    f.port_subtype = lldp::kPortIfName;
+    f.port_id = ifname;
+    f.ttl = ttl;
+    f.port_description = gpu_bdf.empty() ? "scale-out NIC" : "scale-out NIC of GPU " + gpu_bdf;
+    f.system_name = node_name;
+    f.system_description = "AMD Instinct MI355X node (amd-network-operator link discovery)";
+    f.capabilities = std::make_pair(uint16_t(0x0080), uint16_t(0x0080));  // station only
+    return f;
+}
 
 // ---------------------------------------------------------------------------
 // Agent
@@ -89,6 +109,16 @@ void Agent::pre_cleanups() {
 
 void Agent::post_cleanups() {
     NLOG_I("Clean up before exiting...");
+    if (cfg_.lldp_announce && cfg_.mode == "L3") {
+        // Shutdown LLDPDU (TTL 0): the switch drops us from its neighbour table right away.
+        for (auto& n : nics_) {
+            if (!n.link.up()) continue;
+            try {
+                lldp_->announce(n.ifname, lldp::encode(make_node_frame(cfg_.node_name, n.ifname, n.link.mac, n.gpu_bdf, 0)));
+            } catch (...) {
+            }
+        }
+    }
     if (!artifacts::remove_labels(cfg_.labels)) NLOG_W("Failed to remove NFD label file: %s", std::strerror(errno));
     NLOG_I("Restoring interfaces to original state...");
     try {
@@ -349,6 +379,7 @@ void Agent::detect_lldp(int stop_fd) {
     if (!listening) return;
     int remaining = listening;
     auto cb = [&](const std::string& ifname, const lldp::Frame& f) -> bool {
+        if (f.ttl == 0) return false;  // shutdown LLDPDU: the neighbour is going away
         for (auto& n : nics_) {
             if (n.ifname != ifname || n.lldp_seen) continue;  // first frame per NIC wins (client.go:141-142)
             on_lldp(n, f);
@@ -357,7 +388,26 @@ void Agent::detect_lldp(int stop_fd) {
         }
         return remaining == 0;
     };
-    auto r = lldp_->run(mono_ns() + cfg_.wait_ns, cb, stop_fd);
+    const int64_t deadline = mono_ns() + cfg_.wait_ns;
+    int announced = 0;
+    pkt::ListenResult r = pkt::ListenResult::Deadline;
+    for (;;) {
+        int64_t slice_end = deadline;
+        if (cfg_.lldp_announce && announced < cfg_.announce_count) {
+            for (auto& n : nics_) {
+                if (!n.link.up() || n.lldp_seen) continue;
+                try {
+                    lldp_->announce(n.ifname, lldp::encode(make_node_frame(cfg_.node_name, n.ifname, n.link.mac, n.gpu_bdf)));
+                } catch (const std::exception& e) {
+                    NLOG_V(2, "LLDP announce on %s failed: %s", n.ifname.c_str(), e.what());
+                }
+            }
+            ++announced;
+            slice_end = std::min(deadline, mono_ns() + cfg_.announce_interval_ns);
+        }
+        r = lldp_->run(slice_end, cb, stop_fd);
+        if (r != pkt::ListenResult::Deadline || mono_ns() >= deadline) break;
+    }
     if (r == pkt::ListenResult::Interrupted) aborted_ = true;
     if (r == pkt::ListenResult::Deadline) NLOG_I("LLDP wait of %s expired with %d interface(s) silent", format_go_duration(cfg_.wait_ns).c_str(), remaining);
 }

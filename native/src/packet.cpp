@@ -150,6 +150,16 @@ void LldpListener::remove(const std::string& ifname) {
     }
 }
 
+bool LldpListener::send(const std::string& ifname, const std::vector<uint8_t>& frame) {
+    for (auto& s : socks_) {
+        if (s && s->ifname() == ifname) {
+            s->send(frame);
+            return true;
+        }
+    }
+    return false;
+}
+
 ListenResult LldpListener::run(int64_t deadline,
                                const std::function<bool(const std::string&, const lldp::Frame&)>& on_frame,
                                int interrupt_fd) {

@@ -61,6 +61,8 @@ int main(int argc, char** argv) {
     fs.add_string("nm-keyfile-dir", &cfg.nm_keyfile_dir, "with --disable-networkmanager, also persist an unmanaged-devices keyfile here");
     fs.add_int("xgmi-expect", &cfg.xgmi_expect_links, "verify the xGMI mesh before labelling: -1 off, 0 full mesh, N GPU pairs");
     fs.add_duration("link-wait", &cfg.link_wait_ns, "time to wait for link state echoes from the kernel");
+    fs.add_bool("lldp-announce", &cfg.lldp_announce, "transmit our own LLDPDU on each NIC (makes 802.1AB-2009 switches answer within ~1s)");
+    fs.add_string("node-name", &cfg.node_name, "LLDP System Name (default $NODE_NAME, else the hostname)");
     fs.add_bool("help", &show_help, "help for discover");
     fs.shorthand('h', "help");
     fs.add_bool("version", &show_version, "print version");
@@ -102,6 +104,14 @@ int main(int argc, char** argv) {
         return 2;
     }
     cfg.discovery.max_path = pit->second;
+    if (cfg.node_name.empty()) {
+        const char* nn = std::getenv("NODE_NAME");  // set by the DaemonSet (downward API)
+        char host[256] = {};
+        if (nn && *nn)
+            cfg.node_name = nn;
+        else if (::gethostname(host, sizeof host - 1) == 0)
+            cfg.node_name = host;
+    }
 
     // SIGTERM/SIGINT are consumed through a signalfd so every wait in the state machine
     // (LLDP epoll, idle) can observe them without async-signal-safety concerns.

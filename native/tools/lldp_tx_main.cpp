@@ -1,18 +1,29 @@
-// `netop-lldp-tx` — synthetic ToR switch: transmits LLDPDUs on one or more interfaces.
+// `netop-lldp-tx` — synthetic ToR switch for the netns harness.
 //
-// Used by the netns harness (node-ready latency bench, integration tests) to play the
-// switch side of the reference's contract: a Port Description TLV carrying
-// "<tag> a.b.c.d/30" per switch port (reference README.md:19-25).
+// Plays the switch side of the reference's contract: every switch port advertises a Port
+// Description "<tag> a.b.c.d/30" (reference README.md:19-25).  Models an IEEE 802.1AB-2009
+// LLDP agent:
+//   * periodic transmission every --interval (msgTxInterval, 30 s on real switches), with the
+//     first frame at a random phase in [0, interval) when --phase=random (a switch that has
+//     been running for a while), or immediately with --phase=zero;
+//   * optional fast start (--fast-start): when an LLDPDU from a *new neighbour* arrives on a
+//     port, the port transmits immediately and then --tx-fast-init frames at --fast-interval
+//     (txFastInit = 4, msgFastTx = 1 s in the standard);
+//   * --assign-ip puts the peer address of the Port Description on the switch port so the
+//     node's /30 is actually reachable.
 //
-//   netop-lldp-tx --port sw0=no-alert\ 10.200.0.2/30 --port sw1=... [--interval 1s] [--count N]
-//                 [--delay 0s] [--system-name tor1] [--mac-from-port]
+//   netop-lldp-tx --port sw0='no-alert 10.200.0.2/30' --port sw1=... [--interval 30s]
+//                 [--phase random|zero] [--fast-start] [--count N] [--assign-ip] [--seed S]
 #include <signal.h>
+#include <sys/epoll.h>
 #include <unistd.h>
 
 #include <cstdio>
-#include <thread>
+#include <random>
+#include <set>
 
 #include "netop/cli.hpp"
+#include "netop/l3.hpp"
 #include "netop/lldp.hpp"
 #include "netop/log.hpp"
 #include "netop/netlink.hpp"
@@ -25,11 +36,10 @@ static void on_sig(int) { g_stop = 1; }
 
 int main(int argc, char** argv) {
     std::vector<std::pair<std::string, std::string>> ports;
-    int64_t interval = 1000000000LL, delay = 0;
-    int count = 0;  // 0 = forever
-    std::string sysname = "tor-synthetic";
-    int ttl = 120, verbosity = 0;
-    bool chassis_mac_is_port = true;
+    int64_t interval = 30LL * 1000000000, fast_interval = 1000000000LL;
+    int count = 0, tx_fast_init = 4, ttl = 120, verbosity = 0, seed = 0;
+    std::string sysname = "tor-synthetic", phase = "random", mtu_str;
+    bool fast_start = false, assign_ip = false;
 
     cli::FlagSet fs("netop-lldp-tx");
     fs.add_func("port", true, [&](const std::string& v) {
@@ -37,12 +47,16 @@ int main(int argc, char** argv) {
         if (eq == std::string::npos) throw std::invalid_argument("--port wants IFNAME=PORT_DESCRIPTION");
         ports.emplace_back(v.substr(0, eq), v.substr(eq + 1));
     }, "IFNAME=PORT_DESCRIPTION (repeatable)");
-    fs.add_duration("interval", &interval, "transmit interval");
-    fs.add_duration("delay", &delay, "delay before the first frame");
-    fs.add_int("count", &count, "frames per port (0 = until SIGTERM)");
+    fs.add_duration("interval", &interval, "msgTxInterval");
+    fs.add_string("phase", &phase, "first periodic frame: random (U[0,interval)) or zero");
+    fs.add_bool("fast-start", &fast_start, "802.1AB-2009 fast transmission on new neighbours");
+    fs.add_duration("fast-interval", &fast_interval, "msgFastTx");
+    fs.add_int("tx-fast-init", &tx_fast_init, "txFastInit");
+    fs.add_int("count", &count, "periodic frames per port before exiting (0 = until SIGTERM)");
     fs.add_string("system-name", &sysname, "System Name TLV");
     fs.add_int("ttl", &ttl, "TTL TLV");
-    fs.add_bool("mac-from-port", &chassis_mac_is_port, "chassis ID = sending port MAC");
+    fs.add_bool("assign-ip", &assign_ip, "assign the Port Description address to the switch port");
+    fs.add_int("seed", &seed, "RNG seed for the random phase (0 = time based)");
     fs.add_int("v", &verbosity, "log verbosity");
     try {
         fs.parse(argc, argv);
@@ -57,37 +71,96 @@ int main(int argc, char** argv) {
     }
     signal(SIGTERM, on_sig);
     signal(SIGINT, on_sig);
+    std::mt19937_64 rng(seed ? uint64_t(seed) : uint64_t(wall_ns()));
 
-    struct Tx {
+    struct Port {
         std::unique_ptr<pkt::LldpSocket> sock;
         std::vector<uint8_t> frame;
+        int64_t next = 0;
+        int fast_left = 0;
+        int periodic_sent = 0;
+        std::set<std::string> neighbours;
     };
-    std::vector<Tx> txs;
+    std::vector<Port> ps;
+    int ep = ::epoll_create1(EPOLL_CLOEXEC);
     try {
         nl::Rtnl rtnl;
+        int64_t now = mono_ns();
         for (auto& [ifname, desc] : ports) {
             auto link = rtnl.link_by_name(ifname);
             if (!link.up()) rtnl.link_set_up(link.index);
-            auto f = lldp::make_switch_frame(link.mac, sysname, ifname, desc, uint16_t(ttl));
-            txs.push_back({std::make_unique<pkt::LldpSocket>(ifname, link.index, link.mac, false), lldp::encode(f)});
+            if (assign_ip) {
+                if (auto a = l3::parse_port_description(desc, l3::TokenPolicy::CompatThenLast, nullptr)) {
+                    try {
+                        rtnl.addr_add(link.index, Ipv4Prefix{a->peer, a->prefix});
+                    } catch (const SysError& e) {
+                        if (e.code() != EEXIST) throw;
+                    }
+                }
+            }
+            Port p;
+            p.sock = std::make_unique<pkt::LldpSocket>(ifname, link.index, link.mac, false);
+            p.frame = lldp::encode(lldp::make_switch_frame(link.mac, sysname, ifname, desc, uint16_t(ttl)));
+            p.next = phase == "zero" ? now : now + int64_t(std::uniform_real_distribution<double>(0, 1)(rng) * double(interval));
+            // Scheduled first periodic frame (CLOCK_MONOTONIC ns): lets the harness model an
+            // agent that never solicits fast start (the reference's) on the same run.
+            std::printf("first %s %lld\n", ifname.c_str(), (long long)p.next);
+            epoll_event ev{};
+            ev.events = EPOLLIN;
+            ev.data.u64 = ps.size();
+            ::epoll_ctl(ep, EPOLL_CTL_ADD, p.sock->fd(), &ev);
+            ps.push_back(std::move(p));
         }
     } catch (const std::exception& e) {
         std::fprintf(stderr, "Error: %s\n", e.what());
         return 1;
     }
-    if (delay > 0) std::this_thread::sleep_for(std::chrono::nanoseconds(delay));
-    for (int n = 0; !g_stop && (count == 0 || n < count); ++n) {
-        for (auto& t : txs) {
+    std::printf("ready\n");
+    std::fflush(stdout);
+
+    pkt::ListenerStats st;
+    while (!g_stop) {
+        int64_t now = mono_ns(), next = INT64_MAX;
+        bool all_done = count > 0;
+        for (auto& p : ps) {
+            if (count > 0 && p.periodic_sent >= count && p.fast_left == 0) continue;
+            all_done = false;
+            next = std::min(next, p.next);
+        }
+        if (all_done) break;
+        int timeout = next <= now ? 0 : int(std::min<int64_t>((next - now + 999999) / 1000000, 1000));
+        epoll_event evs[16];
+        int n = ::epoll_wait(ep, evs, 16, timeout);
+        now = mono_ns();
+        for (int i = 0; i < n; ++i) {
+            auto& p = ps[size_t(evs[i].data.u64)];
+            for (auto& f : p.sock->drain(&st)) {
+                std::string who = f.src.str();
+                if (fast_start && f.ttl > 0 && p.neighbours.insert(who).second) {
+                    NLOG_V(1, "%s: new neighbour %s -> fast start", p.sock->ifname().c_str(), who.c_str());
+                    p.fast_left = tx_fast_init;
+                    p.next = now;
+                }
+                if (f.ttl == 0) p.neighbours.erase(who);  // shutdown LLDPDU
+            }
+        }
+        for (auto& p : ps) {
+            if (p.next > now) continue;
+            if (count > 0 && p.periodic_sent >= count && p.fast_left == 0) continue;
             try {
-                t.sock->send(t.frame);
-                NLOG_V(2, "sent LLDP on %s", t.sock->ifname().c_str());
+                p.sock->send(p.frame);
             } catch (const std::exception& e) {
                 NLOG_W("send failed: %s", e.what());
             }
+            if (p.fast_left > 0) {
+                --p.fast_left;
+                p.next = now + fast_interval;
+            } else {
+                ++p.periodic_sent;
+                p.next = now + interval;
+            }
         }
-        if (count != 0 && n + 1 >= count) break;
-        int64_t until = mono_ns() + interval;
-        while (!g_stop && mono_ns() < until) std::this_thread::sleep_for(std::chrono::milliseconds(std::min<int64_t>(50, (until - mono_ns()) / 1000000 + 1)));
     }
+    ::close(ep);
     return 0;
 }

@@ -1,0 +1,126 @@
+"""Fake sysfs trees for the node agent (``SYSFS_ROOT``).
+
+``build_mi355x_node`` reproduces the PCIe / KFD topology of a real 8x MI355X node (captured
+from a GPU box, see ``tests/fixtures/mi355x_node_topology.json``): eight 0x75a3 GPUs, each
+behind a PCIe switch shared with one mlx5 RoCE NIC, two management NICs on their own root
+ports, and the KFD io_links of the 28-pair xGMI mesh.  NIC netdev names can be remapped so
+the agent's affinity discovery finds the veth "NICs" of the netns harness.
+
+The reference's equivalent is its tmpdir + ``SYSFS_ROOT`` fake tree
+(reference cmd/discover/network_test.go:94-116,226-252).
+"""
+
+from __future__ import annotations
+
+import json
+import os
+from pathlib import Path
+from typing import Dict, Optional
+
+FIXTURE = Path(__file__).resolve().parents[2] / "tests" / "fixtures" / "mi355x_node_topology.json"
+
+
+def _w(path: Path, content: str) -> None:
+    path.parent.mkdir(parents=True, exist_ok=True)
+    path.write_text(content)
+
+
+def _link(target: Path, link: Path) -> None:
+    link.parent.mkdir(parents=True, exist_ok=True)
+    if not link.exists() and not link.is_symlink():
+        os.symlink(os.path.relpath(target, link.parent), link)
+
+
+def _pci(root: Path, pcipath: str, driver: str, vendor: str, device: str, numa: int, cls: str) -> Path:
+    d = root / "devices" / pcipath
+    d.mkdir(parents=True, exist_ok=True)
+    _w(d / "vendor", vendor + "\n")
+    _w(d / "device", device + "\n")
+    _w(d / "numa_node", f"{numa}\n")
+    _w(d / "class", cls + "\n")
+    drv = root / "bus" / "pci" / "drivers" / driver
+    drv.mkdir(parents=True, exist_ok=True)
+    _link(drv, d / "driver")
+    return d
+
+
+def build_mi355x_node(root: Path, nic_names: Optional[Dict[str, str]] = None, nic_macs: Optional[Dict[str, str]] = None,
+                      n_gpus: int = 8, with_kfd: bool = True, drop_xgmi_pairs=()) -> dict:
+    """Writes the tree under ``root``; returns the fixture (with applied renames).
+
+    nic_names: {original ifname -> new ifname}; nic_macs: {new ifname -> MAC}.
+    drop_xgmi_pairs: iterable of (gpu_i, gpu_j) KFD-order indices whose xGMI link is removed.
+    """
+    fx = json.loads(FIXTURE.read_text())
+    nic_names = nic_names or {}
+    nic_macs = nic_macs or {}
+    root = Path(root)
+    gpus = sorted(fx["gpus"], key=lambda g: g["bdf"])[:n_gpus]
+    for g in gpus:
+        d = _pci(root, g["path"], "amdgpu", g["vendor"], g["device"], g["numa"], "0x120000")
+        _link(d, root / "bus" / "pci" / "drivers" / "amdgpu" / g["bdf"])
+    nics = []
+    for n in fx["nics"]:
+        name = nic_names.get(n["ifname"], n["ifname"])
+        d = _pci(root, n["pcipath"], n["driver"], "0x15b3", "0x1021", 0 if n["pcipath"] < "pci0000:80" else 1, "0x020000")
+        net = d / "net" / name
+        _w(net / "address", nic_macs.get(name, n["mac"]) + "\n")
+        _w(net / "dev_port", "0\n")
+        _link(net, root / "class" / "net" / name)
+        nics.append(dict(n, ifname=name))
+    for r in fx["rdma"]:
+        d = root / "devices" / r["pcipath"] / "infiniband" / r["dev"]
+        d.mkdir(parents=True, exist_ok=True)
+        _link(d, root / "class" / "infiniband" / r["dev"])
+    _w(root / "devices" / "virtual" / "net" / "lo" / "address", "00:00:00:00:00:00\n")
+    _link(root / "devices" / "virtual" / "net" / "lo", root / "class" / "net" / "lo")
+
+    if with_kfd:
+        base = root / "class" / "kfd" / "kfd" / "topology" / "nodes"
+        _w(base / "0" / "properties", "cpu_cores_count 128\nsimd_count 0\n")
+        _w(base / "1" / "properties", "cpu_cores_count 128\nsimd_count 0\n")
+        drop = {tuple(sorted(p)) for p in drop_xgmi_pairs}
+        for i, g in enumerate(gpus):
+            node = i + 2
+            bus, dev, fn = (int(x, 16) for x in g["bdf"][5:].replace(".", ":").split(":"))
+            loc = (bus << 8) | (dev << 3) | fn
+            _w(base / str(node) / "properties",
+               f"simd_count 1024\nvendor_id 4098\ndevice_id {int(g['device'], 16)}\nlocation_id {loc}\ndomain 0\n"
+               f"hive_id {fx['kfd_gpu_node']['hive_id']}\nnum_xcc 8\n")
+            _w(base / str(node) / "gpu_id", f"{1000 + i}\n")
+            li = 0
+            _w(base / str(node) / "io_links" / str(li) / "properties",
+               f"type 2\nnode_from {node}\nnode_to {g['numa']}\nweight 20\nmax_bandwidth 64000\n")
+            li += 1
+            for j in range(len(gpus)):
+                if j == i or tuple(sorted((i, j))) in drop:
+                    continue
+                _w(base / str(node) / "io_links" / str(li) / "properties",
+                   f"type 11\nnode_from {node}\nnode_to {j + 2}\nweight 15\nmin_bandwidth 76000\nmax_bandwidth 76000\n")
+                li += 1
+    fx["nics"] = nics
+    fx["gpus"] = gpus
+    return fx
+
+
+def add_rocev2_gids(root: Path, rdma_dev: str, ips, port: int = 1) -> None:
+    """Populates a GID table like mlx5 does after an IPv4 address is configured."""
+    p = Path(root) / "class" / "infiniband" / rdma_dev / "ports" / str(port)
+    _w(p / "gids" / "0", "fe80:0000:0000:0000:0000:00ff:fe00:0001\n")
+    _w(p / "gid_attrs" / "types" / "0", "IB/RoCE v1\n")
+    _w(p / "gids" / "1", "fe80:0000:0000:0000:0000:00ff:fe00:0001\n")
+    _w(p / "gid_attrs" / "types" / "1", "RoCE v2\n")
+    idx = 2
+    for ip in ips:
+        a, b, c, d = (int(x) for x in ip.split("."))
+        gid = f"0000:0000:0000:0000:0000:ffff:{a:02x}{b:02x}:{c:02x}{d:02x}"
+        for t in ("IB/RoCE v1", "RoCE v2"):
+            _w(p / "gids" / str(idx), gid + "\n")
+            _w(p / "gid_attrs" / "types" / str(idx), t + "\n")
+            idx += 1
+
+
+def real_nic_order() -> list:
+    """Fixture's scale-out NIC names in GPU (BDF) order — what affine discovery returns."""
+    fx = json.loads(FIXTURE.read_text())
+    return [n["ifname"] for n in fx["nics"] if n["ifname"].startswith("enp")]

@@ -1,33 +1,289 @@
 """Synthetic-switch network-namespace harness (veth pairs + injected LLDP).
 
-Full harness: see ``NodeSim`` below.  ``available()`` reports whether this process can
-create private network namespaces and raw packet sockets (root in the build container;
-the unprivileged GPU boxes cannot).
+What it builds (all inside ``unshare -rn``, so nothing touches the host network):
+
+    node netns (this process)                 switch netns (forked child)
+    enp5s0np0 ... (one veth end per NIC)  <->  swp0 ... (netop-lldp-tx: LLDP with
+    discover (the real C++ agent binary)        "<tag> a.b.c.d/30" Port Descriptions)
+    SYSFS_ROOT = fake MI355X node tree          optional 802.1AB-2009 fast start
+
+Node-side veths are named like the real node's mlx5 scale-out NICs, and the fake sysfs
+(``fakesysfs.build_mi355x_node``) places them behind the same PCIe switches as the GPUs,
+so the agent runs its normal affinity discovery, xGMI verification and L3 configuration.
+
+Measured: t(agent start) -> t(NFD readiness label visible), plus the agent's own phase
+timings.  For the same run the harness also reports the *reference model*: the time the
+switch's first periodic LLDPDU reaches the last NIC (what an agent that never solicits
+fast start, like the reference's pcap listener, waits for at best).
+
+The reference has no such harness ("How multi-node is tested without a
+cluster: it isn't").
 """
 
 from __future__ import annotations
 
+import argparse
 import ctypes
 import ctypes.util
+import json
 import os
+import random
 import shutil
-import socket
+import signal
+import statistics
 import subprocess
+import sys
+import tempfile
+import time
+from pathlib import Path
 
 CLONE_NEWNET = 0x40000000
-CLONE_NEWUSER = 0x10000000
+
+
+def unshare_cmd() -> list[str]:
+    """Real root: a plain network namespace (a user namespace would lose DAC access to
+    directories owned by other users); otherwise user + network namespaces."""
+    return ["unshare", "-n"] if os.geteuid() == 0 else ["unshare", "-rn"]
 
 
 def available() -> tuple[bool, str]:
-    """True when ``unshare -rn`` works and AF_PACKET sockets can be opened inside it."""
+    """True when a private network namespace with AF_PACKET sockets can be created."""
     if not shutil.which("unshare"):
         return False, "unshare(1) not installed"
     probe = ("import socket; s=socket.socket(socket.AF_PACKET, socket.SOCK_RAW, 0); "
              "n=socket.socket(socket.AF_NETLINK, socket.SOCK_RAW, 0); print('ok')")
     try:
-        r = subprocess.run(["unshare", "-rn", "python3", "-c", probe], capture_output=True, text=True, timeout=60)
+        r = subprocess.run([*unshare_cmd(), sys.executable, "-c", probe], capture_output=True, text=True, timeout=60)
     except Exception as e:  # pragma: no cover
         return False, f"unshare failed: {e}"
     if r.returncode != 0 or "ok" not in r.stdout:
         return False, (r.stderr.strip().splitlines() or ["unshare -rn failed"])[-1]
     return True, "ok"
+
+
+# ---------------------------------------------------------------------------
+# Address plans
+# ---------------------------------------------------------------------------
+def random_plan(n: int, rng: random.Random) -> list[dict]:
+    """n distinct /30 links inside one random /16; peer is .1 or .2 of each /30."""
+    second = rng.randrange(0, 256)
+    blocks = rng.sample(range(16384), n)
+    tags = ["no-alert", "scale-out", "gpu-fabric", "leaf-port"]
+    plan = []
+    for b in blocks:
+        base = (10 << 24) | (second << 16) | (b * 4)
+        host = rng.choice((1, 2))
+        peer = base + host
+        local = peer ^ 3
+        fmt = lambda v: ".".join(str((v >> s) & 255) for s in (24, 16, 8, 0))  # noqa: E731
+        plan.append({"peer": fmt(peer), "local": fmt(local), "p2p": fmt(base) + "/30",
+                     "routed": f"10.{second}.0.0/16", "desc": f"{rng.choice(tags)} {fmt(peer)}/30"})
+    return plan
+
+
+# ---------------------------------------------------------------------------
+# Inside the namespace
+# ---------------------------------------------------------------------------
+def _native():
+    here = Path(__file__).resolve().parents[2]
+    if str(here) not in sys.path:
+        sys.path.insert(0, str(here))
+    from network_operator_amd.agent import native
+
+    return native()
+
+
+def _wait_for(path: Path, timeout: float, proc=None, poll: float = 0.0005) -> float | None:
+    """Monotonic time at which `path` appeared; None on timeout or if `proc` exited first."""
+    end = time.monotonic() + timeout
+    while time.monotonic() < end:
+        if path.exists():
+            return time.monotonic()
+        if proc is not None and proc.poll() is not None:
+            return time.monotonic() if path.exists() else None
+        time.sleep(poll)
+    return None
+
+
+def run_scenario(n_nics: int = 8, mode: str = "L3", seed: int | None = None, interval: str = "30s",
+                 fast_start: bool = True, announce: bool = True, phase: str = "random", wait: str = "90s",
+                 mtu: int = 9000, pipeline: bool = True, bad_nics: int = 0, silent_nics: int = 0,
+                 xgmi_expect: int = 0, keep_tmp: bool = False, sigterm: bool = True, verbose: int = 2,
+                 drop_xgmi: list | None = None, extra_args: list | None = None) -> dict:
+    """Runs one node bring-up.  Must already be inside a private user+net namespace."""
+    from . import fakesysfs
+
+    nat = _native()
+    from ..utils.paths import native_bin
+
+    rng = random.Random(seed)
+    rt = nat.Rtnl()
+    rt.link_set_up(rt.link_by_name("lo")["index"])
+    tmp = Path(tempfile.mkdtemp(prefix="netop-sim-"))
+    try:
+        fx = fakesysfs.build_mi355x_node(tmp / "sys", n_gpus=n_nics,
+                                         drop_xgmi_pairs=[tuple(p) for p in (drop_xgmi or [])])
+        pairs = nat.discover(str(tmp / "sys"))["pairs"]
+        nic_names = [p["nic"] for p in pairs][:n_nics]
+        plan = random_plan(len(nic_names), rng)
+        for i, p in enumerate(plan):
+            if i < bad_nics:
+                p["desc"] = "no-alert not-an-address"
+        rdma = {n["ifname"]: "" for n in fx["nics"]}
+        # GID tables as mlx5 would populate them once the address is configured.
+        disc = nat.discover(str(tmp / "sys"))
+        for n in disc["nics"]:
+            if n["ifname"] in nic_names and n["rdma_dev"]:
+                fakesysfs.add_rocev2_gids(tmp / "sys", n["rdma_dev"], [plan[nic_names.index(n["ifname"])]["local"]])
+                rdma[n["ifname"]] = n["rdma_dev"]
+
+        # Switch namespace: forked child unshares its netns, waits for its ports, execs lldp-tx.
+        sw_ports = [f"swp{i}" for i in range(len(nic_names))]
+        tx_args = [str(native_bin("netop-lldp-tx")), f"--interval={interval}", f"--phase={phase}", "--assign-ip",
+                   f"--seed={rng.randrange(1, 1 << 30)}"]
+        if fast_start:
+            tx_args.append("--fast-start")
+        for i, (sp, p) in enumerate(zip(sw_ports, plan)):
+            if i >= len(plan) - silent_nics:
+                continue  # switch port that never sends LLDP
+            tx_args.append(f"--port={sp}={p['desc']}")
+        has_ports = any(a.startswith("--port=") for a in tx_args)
+        libc = ctypes.CDLL(ctypes.util.find_library("c"), use_errno=True)
+        r1, w1 = os.pipe()
+        r2, w2 = os.pipe()
+        out_r, out_w = os.pipe()
+        pid = os.fork()
+        if pid == 0:  # switch
+            try:
+                os.close(r1)
+                os.close(w2)
+                os.close(out_r)
+                if libc.unshare(CLONE_NEWNET) != 0:
+                    os._exit(3)
+                os.write(w1, b"1")
+                os.read(r2, 1)
+                os.dup2(out_w, 1)
+                if not has_ports:  # no port sends anything
+                    signal.pause()
+                os.execv(tx_args[0], tx_args)
+            finally:
+                os._exit(4)
+        os.close(w1)
+        os.close(r2)
+        os.close(out_w)
+        os.read(r1, 1)
+        for node_if, sp in zip(nic_names, sw_ports):
+            rt.veth_add(node_if, sp)
+            rt.link_set_netns_pid(rt.link_by_name(sp)["index"], pid)
+        t_switch = time.monotonic()
+        os.write(w2, b"1")
+        sw_out = os.fdopen(out_r)
+        first_periodic = {}
+        if has_ports:
+            for line in sw_out:
+                if line.startswith("first "):
+                    _, ifn, ns = line.split()
+                    first_periodic[ifn] = int(ns) / 1e9
+                if line.strip() == "ready":
+                    break
+
+        feat = tmp / "features.d"
+        feat.mkdir()
+        label = feat / "scale-out-readiness.txt"
+        args = [str(native_bin("discover")), "--configure=true", "--keep-running", f"--mode={mode}", f"--mtu={mtu}",
+                f"--wait={wait}", f"--rccl-net={tmp / 'rccl-net.json'}", f"--rccl-env={tmp / 'rccl.env'}",
+                f"--status-file={tmp / 'status.json'}", f"--nfd-features-dir={feat}", f"--xgmi-expect={xgmi_expect}",
+                f"--pipeline={'true' if pipeline else 'false'}", f"--lldp-announce={'true' if announce else 'false'}",
+                f"--systemd-networkd={tmp / 'networkd'}", f"-v={verbose}", *(extra_args or [])]
+        env = dict(os.environ, SYSFS_ROOT=str(tmp / "sys"), NODE_NAME="mi355x-node-0")
+        t0 = time.monotonic()
+        agent = subprocess.Popen(args, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+        budget = 5.0 + float(wait.rstrip("s"))
+        t_ready = _wait_for(label, budget, agent)
+        res: dict = {"n_nics": len(nic_names), "mode": mode, "fast_start": fast_start, "announce": announce,
+                     "interval": interval, "pipeline": pipeline, "plan": plan, "nics": nic_names}
+        res["ready"] = t_ready is not None
+        res["latency_s"] = (t_ready - t0) if t_ready else None
+        if first_periodic:
+            res["reference_model_s"] = max(0.0, max(first_periodic.values()) - t0)
+        # Inspect the configured node.
+        state = {}
+        for node_if, p in zip(nic_names, plan):
+            try:
+                link = rt.link_by_name(node_if)
+                state[node_if] = {"up": link["up"], "mtu": link["mtu"], "addrs": rt.addr_list(link["index"]),
+                                  "routes": [r for r in rt.route_list() if r["ifindex"] == link["index"]]}
+            except OSError as e:
+                state[node_if] = {"error": str(e)}
+        res["state"] = state
+        for f in ("rccl-net.json", "status.json"):
+            fp = tmp / f
+            res[f.split(".")[0].replace("-", "_")] = json.loads(fp.read_text()) if fp.exists() else None
+        res["rccl_env"] = (tmp / "rccl.env").read_text() if (tmp / "rccl.env").exists() else None
+        res["label"] = label.read_text() if label.exists() else None
+        res["networkd_files"] = sorted(os.listdir(tmp / "networkd")) if (tmp / "networkd").exists() else []
+        if sigterm and agent.poll() is None:
+            agent.send_signal(signal.SIGTERM)
+        try:
+            out, _ = agent.communicate(timeout=20)
+        except subprocess.TimeoutExpired:
+            agent.kill()
+            out, _ = agent.communicate()
+        res["agent_rc"] = agent.returncode
+        res["agent_log"] = out[-6000:]
+        after = {}
+        for node_if in nic_names:
+            link = rt.link_by_name(node_if)
+            after[node_if] = {"up": link["up"], "addrs": rt.addr_list(link["index"])}
+        res["after_sigterm"] = after
+        res["label_after_sigterm"] = label.exists()
+        os.kill(pid, signal.SIGTERM)
+        os.waitpid(pid, 0)
+        res["switch_start_offset_s"] = t0 - t_switch
+        return res
+    finally:
+        if not keep_tmp:
+            shutil.rmtree(tmp, ignore_errors=True)
+
+
+# ---------------------------------------------------------------------------
+# From outside: spawn into a fresh namespace
+# ---------------------------------------------------------------------------
+def run_isolated(timeout: float = 300, **kw) -> dict:
+    """Runs ``run_scenario(**kw)`` in a new user+net namespace and returns its result."""
+    cmd = [*unshare_cmd(), sys.executable, "-m", "network_operator_amd.testing.netns", "--json", json.dumps(kw)]
+    root = Path(__file__).resolve().parents[2]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, cwd=root,
+                       env=dict(os.environ, PYTHONPATH=str(root)))
+    if r.returncode != 0:
+        raise RuntimeError(f"scenario failed rc={r.returncode}: {r.stderr[-3000:]}")
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+def node_ready_bench(n_nics: int = 8, runs: int = 5, interval: str = "30s", seed: int = 1) -> dict:
+    """Node-ready latency over `runs` fresh bring-ups, with and without switch fast start."""
+    out = {"n_nics": n_nics, "runs": runs, "interval": interval}
+    for label, fs in (("fast_start_switch", True), ("legacy_switch", False)):
+        lat, ref = [], []
+        for k in range(runs):
+            r = run_isolated(n_nics=n_nics, seed=seed * 1000 + k, interval=interval, fast_start=fs, verbose=0)
+            if not r["ready"]:
+                raise RuntimeError(f"run {k} did not become ready: {r['agent_log'][-2000:]}")
+            lat.append(r["latency_s"])
+            ref.append(r.get("reference_model_s"))
+        out[label] = {"latency_s": lat, "p50_s": statistics.median(lat), "max_s": max(lat),
+                      "reference_model_s": ref, "reference_model_p50_s": statistics.median([x for x in ref if x is not None])}
+    return out
+
+
+def _main(argv=None) -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--json", default="{}", help="run_scenario kwargs")
+    a = ap.parse_args(argv)
+    res = run_scenario(**json.loads(a.json))
+    print(json.dumps(res))
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(_main())

@@ -1,0 +1,151 @@
+"""Native agent building blocks: C++ unit suite, pybind11 bindings, property-based fuzzing,
+and discovery on a fake sysfs copy of a real 8x MI355X node."""
+
+import ipaddress
+import json
+import subprocess
+
+import pytest
+from hypothesis import given, settings
+from hypothesis import strategies as st
+
+from network_operator_amd.testing import fakesysfs
+from network_operator_amd.utils import native_bin
+
+
+def test_cpp_unit_suite():
+    r = subprocess.run([str(native_bin("netop-unit-tests"))], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-2000:]
+    assert "FAIL" not in r.stdout
+
+
+def test_discover_help_lists_reference_flags():
+    out = subprocess.run([str(native_bin("discover")), "--help"], capture_output=True, text=True).stdout
+    for flag in ("--mode", "--configure", "--disable-networkmanager", "--interfaces", "--wait", "--keep-running",
+                 "--systemd-networkd", "--mtu", "--rccl-net", "--v"):
+        assert flag in out, flag
+
+
+def test_discover_rejects_bad_flags():
+    r = subprocess.run([str(native_bin("discover")), "--wait=90"], capture_output=True, text=True)
+    assert r.returncode == 2 and "invalid duration" in r.stderr
+    r = subprocess.run([str(native_bin("discover")), "--mode=L4", "--nic-discovery=none", "--interfaces=lo"],
+                       capture_output=True, text=True)
+    assert r.returncode == 1 and "Invalid mode 'L4'" in r.stderr
+
+
+# --- LLDP codec ------------------------------------------------------------------------------
+MAC = st.lists(st.integers(0, 255), min_size=6, max_size=6).map(lambda b: ":".join(f"{x:02x}" for x in b))
+TEXT = st.text(alphabet=st.characters(min_codepoint=32, max_codepoint=126), max_size=200)
+
+
+@settings(max_examples=300, deadline=None)
+@given(mac=MAC, sysname=TEXT, port=TEXT.filter(bool), desc=TEXT, ttl=st.integers(0, 65535),
+       vlan=st.one_of(st.none(), st.integers(1, 4094)))
+def test_lldp_roundtrip_property(native, mac, sysname, port, desc, ttl, vlan):
+    frame = native.lldp_switch_frame(mac, sysname, port, desc, ttl, vlan)
+    d = native.lldp_decode(frame)
+    assert d["port_description"] == desc
+    assert d["system_name"] == sysname
+    assert d["port_id"] == port.encode()[:255]
+    assert d["ttl"] == ttl
+    assert d["peer_mac"] == mac
+    assert d["vlan"] == vlan
+
+
+@settings(max_examples=500, deadline=None)
+@given(data=st.binary(max_size=300))
+def test_lldp_decode_never_crashes_on_garbage(native, data):
+    frame = bytes.fromhex("0180c200000e020000aabbcc88cc") + data
+    try:
+        native.lldp_decode(frame)
+    except ValueError:
+        pass
+
+
+def test_lldp_peer_mac_port_overrides_chassis(native):
+    f = native.lldp_encode("02:00:00:00:00:01", 4, bytes.fromhex("020000000001"), 3, bytes.fromhex("020000000002"))
+    assert native.lldp_decode(f)["peer_mac"] == "02:00:00:00:00:02"
+    f = native.lldp_encode("02:00:00:00:00:01", 4, bytes.fromhex("020000000001"), 5, b"Ethernet1")
+    assert native.lldp_decode(f)["peer_mac"] == "02:00:00:00:00:01"
+
+
+# --- Port Description -> /30 -------------------------------------------------------------------
+@settings(max_examples=400, deadline=None)
+@given(a=st.integers(0, 2**32 - 1), tag=st.sampled_from(["no-alert", "x", "uplink-7"]))
+def test_port_description_matches_ipaddress_model(native, a, tag):
+    ip = ipaddress.IPv4Address(a)
+    desc = f"{tag} {ip}/30"
+    net = ipaddress.IPv4Network(f"{ip}/30", strict=False)
+    if ip in (net.network_address, net.broadcast_address):
+        with pytest.raises(ValueError):
+            native.parse_port_description(desc, "compat")
+        return
+    r = native.parse_port_description(desc, "compat")
+    local = ipaddress.IPv4Address(int(ip) ^ 3)
+    assert r["peer"] == str(ip) and r["local"] == str(local)
+    assert r["p2p_network"] == str(net)
+    assert r["routed_network"] == str(ipaddress.IPv4Network(f"{local}/16", strict=False))
+
+
+@pytest.mark.parametrize("desc,policy,local", [
+    ("no-alert 10.200.10.2/30", "compat", "10.200.10.1"),
+    ("to leaf1 eth1/1 10.1.1.2/30", "compat-then-last", "10.1.1.1"),
+    ("uplink 7 10.5.5.6/30 via tor", "any", "10.5.5.5"),
+])
+def test_port_description_policies(native, desc, policy, local):
+    assert native.parse_port_description(desc, policy)["local"] == local
+
+
+@pytest.mark.parametrize("desc", ["no-alert", "a 10.0.0.2/24", "a 10.0.0.0/30", "a  10.0.0.2/30", "a 1.2.3/30"])
+def test_port_description_compat_rejects(native, desc):
+    with pytest.raises(ValueError):
+        native.parse_port_description(desc, "compat")
+
+
+# --- Topology on the real MI355X node layout ------------------------------------------------
+def test_real_mi355x_topology_discovery(native, tmp_path):
+    fx = fakesysfs.build_mi355x_node(tmp_path)
+    d = native.discover(str(tmp_path))
+    assert [g["bdf"] for g in d["gpus"]] == sorted(g["bdf"] for g in fx["gpus"])
+    assert all(g["device"] == 0x75A3 for g in d["gpus"])
+    assert len(d["pairs"]) == 8
+    # Every GPU pairs with the mlx5 NIC behind its own PCIe switch; management NICs excluded.
+    assert "ens9np0" not in d["ifnames"] and "ens49np1" not in d["ifnames"]
+    for p in d["pairs"]:
+        assert p["path"] == "PXB" and p["common_depth"] == 3
+        g = [x for x in fx["gpus"] if x["bdf"] == p["gpu"]][0]
+        n = [x for x in fx["nics"] if x["ifname"] == p["nic"]][0]
+        assert g["path"].split("/")[:3] == n["pcipath"].split("/")[:3]
+    x = native.read_xgmi(str(tmp_path))
+    assert x["pairs_expected"] == 28 and x["pairs_connected"] == 28 and x["full_mesh"]
+    assert x["per_gpu_bw_mbs"] == 7 * 76000
+
+
+def test_topo_tool_json(tmp_path):
+    fakesysfs.build_mi355x_node(tmp_path, drop_xgmi_pairs=[(1, 2)])
+    out = subprocess.run([str(native_bin("netop-topo")), f"--sysfs-root={tmp_path}"], capture_output=True, text=True,
+                         check=True).stdout
+    j = json.loads(out)
+    assert len(j["gpus"]) == 8 and len(j["pairs"]) == 8
+    assert j["xgmi"]["pairs_connected"] == 27 and not j["xgmi"]["full_mesh"]
+
+
+def test_accel_mode_reference_layout(native, tmp_path):
+    # Reference fixture layout: netdevs directly under the accelerator function
+    # (reference cmd/discover/network_test.go:94-116).
+    dev = tmp_path / "devices" / "pci0000:00" / "0000:00:02.0" / "0000:33:00.0"
+    for n in ("eth_a", "eth_b"):
+        (dev / "net" / n).mkdir(parents=True)
+    drv = tmp_path / "bus" / "pci" / "drivers" / "habanalabs"
+    drv.mkdir(parents=True)
+    (drv / "0000:33:00.0").symlink_to(dev)
+    d = native.discover(str(tmp_path), mode="accel", accel_driver="habanalabs")
+    assert sorted(d["ifnames"]) == ["eth_a", "eth_b"]
+
+
+def test_gid_lookup(native, tmp_path):
+    fakesysfs.add_rocev2_gids(tmp_path, "mlx5_0", ["10.9.8.1", "10.9.8.5"])
+    assert native.find_rocev2_gid_index(str(tmp_path), "mlx5_0", 1, "10.9.8.1") == 3
+    assert native.find_rocev2_gid_index(str(tmp_path), "mlx5_0", 1, "10.9.8.5") == 5
+    assert native.find_rocev2_gid_index(str(tmp_path), "mlx5_0", 1, "10.9.8.9") is None

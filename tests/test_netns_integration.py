@@ -1,0 +1,112 @@
+"""End-to-end node bring-up in private network namespaces (veth "NICs" + synthetic switch).
+
+Runs the real ``discover`` binary against a fake sysfs copy of an 8x MI355X node.  Needs
+root or user namespaces (available in the build container; skipped elsewhere).
+"""
+
+import ipaddress
+
+import pytest
+
+from network_operator_amd.testing import netns
+
+pytestmark = pytest.mark.netns
+
+
+def _check_configured(r):
+    assert r["ready"], r["agent_log"][-3000:]
+    for nic, p in zip(r["nics"], r["plan"]):
+        st = r["state"][nic]
+        assert st["up"] and st["mtu"] == 9000
+        assert st["addrs"] == [p["local"] + "/30"]
+        routes = {(x["dst"], x["gateway"]) for x in st["routes"]}
+        assert (p["p2p"], None) in routes, routes
+        assert (p["routed"], p["peer"]) in routes, routes
+        kernel = [x for x in st["routes"] if x["dst"] == p["p2p"]][0]
+        assert kernel["prefsrc"] == p["local"] and kernel["scope"] == 253  # link scope
+    entries = r["rccl_net"]["NIC_NET_CONFIG"]
+    assert len(entries) == len(r["nics"])
+    by_name = {e["NIC_NAME"]: e for e in entries}
+    for nic, p in zip(r["nics"], r["plan"]):
+        e = by_name[nic]
+        assert e["NIC_IP"] == p["local"] and e["GATEWAY_IP"] == p["peer"]
+        assert e["SUBNET_MASK"] == "255.255.255.252"
+        assert e["GID_INDEX"] == 3 and e["RDMA_DEV"].startswith("mlx5_")
+    # GPU order: entry i belongs to GPU i.
+    assert [e["GPU_INDEX"] for e in entries] == list(range(len(entries)))
+
+
+def test_l3_fast_start_switch_full_node():
+    r = netns.run_isolated(n_nics=8, seed=11, interval="30s", fast_start=True)
+    _check_configured(r)
+    assert r["latency_s"] < 3.0, r["latency_s"]  # answered by fast start, not the 30 s timer
+    assert r["label"].startswith("amd.feature.node.kubernetes.io/gpu-scale-out=true\n")
+    assert "gpu-xgmi.pairs=28" in r["label"]
+    assert "NCCL_IB_GID_INDEX=3" in r["rccl_env"]
+    assert len(r["networkd_files"]) == 8
+    # SIGTERM: label removed, addresses flushed, links back down.
+    assert r["agent_rc"] == 0
+    assert not r["label_after_sigterm"]
+    for nic in r["nics"]:
+        assert r["after_sigterm"][nic] == {"up": False, "addrs": []}
+    st = r["status"]
+    assert st["ready"] and all(i["configured"] for i in st["interfaces"])
+
+
+def test_l3_legacy_switch_periodic_only():
+    r = netns.run_isolated(n_nics=4, seed=12, interval="1s", fast_start=False)
+    _check_configured(r)
+    assert r["latency_s"] < 1.0 + 1.5
+
+
+def test_without_announce_waits_for_periodic_frames():
+    r = netns.run_isolated(n_nics=2, seed=13, interval="1500ms", phase="zero", fast_start=True, announce=False)
+    _check_configured(r)
+
+
+def test_pipeline_off_barrier_mode():
+    r = netns.run_isolated(n_nics=3, seed=14, interval="1s", fast_start=True, pipeline=False)
+    _check_configured(r)
+
+
+def test_bad_port_description_fails_without_label():
+    r = netns.run_isolated(n_nics=3, seed=15, interval="1s", fast_start=True, bad_nics=1, wait="5s")
+    assert not r["ready"]
+    assert r["agent_rc"] == 1
+    assert "Not all interfaces were configured (2/3)" in r["agent_log"]
+
+
+def test_silent_switch_port_times_out():
+    r = netns.run_isolated(n_nics=2, seed=16, interval="1s", fast_start=True, silent_nics=1, wait="2s")
+    assert not r["ready"]
+    assert r["agent_rc"] == 1
+    assert "expired with 1 interface(s) silent" in r["agent_log"]
+
+
+def test_l2_mode_no_addresses():
+    r = netns.run_isolated(n_nics=2, seed=17, mode="L2", interval="1s")
+    assert r["ready"], r["agent_log"][-2000:]
+    for nic in r["nics"]:
+        assert r["state"][nic]["up"] and r["state"][nic]["addrs"] == []
+    assert "gpu-scale-out.mode=L2" in r["label"]
+
+
+def test_incomplete_xgmi_mesh_blocks_readiness():
+    r = netns.run_isolated(n_nics=8, seed=18, interval="1s", drop_xgmi=[[0, 5]], wait="5s")
+    assert not r["ready"]
+    assert "xGMI mesh incomplete: 27 of 28" in r["agent_log"]
+
+
+def test_random_plans_are_valid():
+    import random
+
+    for s in range(20):
+        plan = netns.random_plan(8, random.Random(s))
+        nets = set()
+        for p in plan:
+            peer, local = ipaddress.ip_address(p["peer"]), ipaddress.ip_address(p["local"])
+            net = ipaddress.ip_network(p["p2p"])
+            assert peer in net and local in net and peer != local
+            assert peer not in (net.network_address, net.broadcast_address)
+            nets.add(net)
+        assert len(nets) == 8
