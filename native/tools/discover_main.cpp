@@ -63,6 +63,8 @@ int main(int argc, char** argv) {
     fs.add_duration("link-wait", &cfg.link_wait_ns, "time to wait for link state echoes from the kernel");
     fs.add_bool("lldp-announce", &cfg.lldp_announce, "transmit our own LLDPDU on each NIC (makes 802.1AB-2009 switches answer within ~1s)");
     fs.add_string("node-name", &cfg.node_name, "LLDP System Name (default $NODE_NAME, else the hostname)");
+    bool ready_check = false;
+    fs.add_bool("ready-check", &ready_check, "exit 0 if the readiness label is published, 1 otherwise (readinessProbe)");
     fs.add_bool("help", &show_help, "help for discover");
     fs.shorthand('h', "help");
     fs.add_bool("version", &show_version, "print version");
@@ -77,6 +79,7 @@ int main(int argc, char** argv) {
         std::cout << "Discover and optionally configure network devices\n\n" << fs.usage();
         return 0;
     }
+    if (ready_check) return path_exists(cfg.labels.path()) ? 0 : 1;
     if (show_version) {
         std::cout << "discover (amd network operator) " << NETOP_VERSION << "\n";
         return 0;

@@ -1,0 +1,223 @@
+"""CRD manifest for ``networkclusterpolicies.amd.com`` and a structural-schema validator.
+
+The schema is the single source of truth: ``python -m network_operator_amd.api.v1alpha1.crd``
+regenerates ``config/operator/crd/bases/amd.com_networkclusterpolicies.yaml`` and the Helm
+chart copy (both are checked for drift by the test-suite, the job controller-gen does for
+the reference: reference config/operator/crd/bases/intel.com_networkclusterpolicies.yaml).
+
+``validate(obj)`` applies the same OpenAPI v3 rules the API server enforces (types, enums,
+minimum/maximum, required, additionalProperties) — the fake API server uses it so tests see
+the same 422 Invalid answers a real cluster would give.
+"""
+
+from __future__ import annotations
+
+import sys
+from pathlib import Path
+from typing import Any, List
+
+import yaml
+
+from . import types as T
+
+_API_VERSION_DESC = (
+    "APIVersion defines the versioned schema of this representation of an object.\n"
+    "Servers should convert recognized schemas to the latest internal value, and\n"
+    "may reject unrecognized values.\n"
+    "More info: https://git.k8s.io/community/contributors/devel/sig-architecture/api-conventions.md#resources")
+_KIND_DESC = (
+    "Kind is a string value representing the REST resource this object represents.\n"
+    "Servers may infer this from the endpoint the client submits requests to.\n"
+    "Cannot be updated.\n"
+    "In CamelCase.\n"
+    "More info: https://git.k8s.io/community/contributors/devel/sig-architecture/api-conventions.md#types-kinds")
+
+
+def openapi_schema() -> dict:
+    amd_so = {
+        "description": "AMD MI355X scale-out specific settings. Only valid when configuration type is 'amd-so'",
+        "type": "object",
+        "properties": {
+            "disableNetworkManager": {
+                "description": "Take the scale-out interfaces away from NetworkManager on nodes where it would\n"
+                               "otherwise try to configure them.",
+                "type": "boolean"},
+            "image": {"description": "Container image of the link-discovery agent on the worker nodes.", "type": "string"},
+            "layer": {"description": "Layer where the configuration should occur. Possible options: L2 and L3.",
+                      "enum": list(T.LAYERS), "type": "string"},
+            "mtu": {"description": "MTU for the scale-out interfaces.", "maximum": T.MTU_MAX, "minimum": T.MTU_MIN,
+                    "type": "integer"},
+            "pullPolicy": {"description": "Image pull policy used in the resulting daemonset.",
+                           "enum": list(T.PULL_POLICIES), "type": "string"},
+            "xgmiCheck": {"description": "Publish the readiness label only when the node's xGMI mesh is complete\n"
+                                         "(every GPU pair linked, read from the KFD topology).",
+                          "type": "boolean"},
+            "lldpAnnounce": {"description": "Transmit an LLDPDU from every scale-out NIC so IEEE 802.1AB-2009 switches\n"
+                                            "answer with fast transmission (default true).",
+                             "type": "boolean"},
+            "interfaces": {"description": "Additional interfaces to configure besides the GPU-affine NICs.",
+                           "items": {"type": "string", "maxLength": 15}, "type": "array"},
+            "nicDrivers": {"description": "NIC driver allow-list for GPU-affinity discovery (default: common RoCE drivers).",
+                           "items": {"type": "string"}, "type": "array"},
+        },
+    }
+    spec = {
+        "description": "NetworkClusterPolicySpec defines the desired state of NetworkClusterPolicy",
+        "type": "object",
+        "properties": {
+            "configurationType": {
+                "description": "Configuration type that the operator will configure to the nodes. Possible options: amd-so.\n"
+                               "Reserved for future use: host-nic",
+                "enum": list(T.CONFIGURATION_TYPES), "type": "string"},
+            "amdScaleOut": amd_so,
+            "logLevel": {"description": "LogLevel sets the agent's log level.", "maximum": T.LOG_LEVEL_MAX,
+                         "minimum": T.LOG_LEVEL_MIN, "type": "integer"},
+            "nodeSelector": {"additionalProperties": {"type": "string"},
+                             "description": "Select which nodes the operator should target. Align with labels created by NFD.",
+                             "type": "object"},
+        },
+        "required": ["configurationType"],
+    }
+    status = {
+        "description": "NetworkClusterPolicyStatus defines the observed state of NetworkClusterPolicy",
+        "type": "object",
+        "properties": {
+            "errors": {"items": {"type": "string"}, "type": "array"},
+            "ready": {"format": "int32", "type": "integer"},
+            "state": {"type": "string"},
+            "targets": {"format": "int32", "type": "integer"},
+        },
+        "required": ["errors", "ready", "state", "targets"],
+    }
+    return {
+        "description": "NetworkClusterPolicy is the Schema for the networkclusterpolicies API",
+        "type": "object",
+        "properties": {
+            "apiVersion": {"description": _API_VERSION_DESC, "type": "string"},
+            "kind": {"description": _KIND_DESC, "type": "string"},
+            "metadata": {"type": "object"},
+            "spec": spec,
+            "status": status,
+        },
+    }
+
+
+def crd_manifest() -> dict:
+    return {
+        "apiVersion": "apiextensions.k8s.io/v1",
+        "kind": "CustomResourceDefinition",
+        "metadata": {"name": f"{T.PLURAL}.{T.GROUP}",
+                     "annotations": {"amd.com/generated-by": "network_operator_amd.api.v1alpha1.crd"}},
+        "spec": {
+            "group": T.GROUP,
+            "names": {"kind": T.KIND, "listKind": T.LIST_KIND, "plural": T.PLURAL, "singular": T.SINGULAR,
+                      "shortNames": ["ncp"]},
+            "scope": "Cluster",
+            "versions": [{
+                "name": T.VERSION,
+                "served": True,
+                "storage": True,
+                "schema": {"openAPIV3Schema": openapi_schema()},
+                "subresources": {"status": {}},
+                "additionalPrinterColumns": [
+                    {"name": "Layer", "type": "string", "jsonPath": ".spec.amdScaleOut.layer"},
+                    {"name": "Targets", "type": "integer", "jsonPath": ".status.targets"},
+                    {"name": "Ready", "type": "integer", "jsonPath": ".status.ready"},
+                    {"name": "State", "type": "string", "jsonPath": ".status.state"},
+                    {"name": "Age", "type": "date", "jsonPath": ".metadata.creationTimestamp"},
+                ],
+            }],
+        },
+    }
+
+
+def render_yaml() -> str:
+    return "---\n" + yaml.safe_dump(crd_manifest(), sort_keys=True, width=100)
+
+
+# ---------------------------------------------------------------------------
+# Structural-schema validation (subset of OpenAPI v3 used by CRDs)
+# ---------------------------------------------------------------------------
+_PY_TYPES = {"string": (str,), "integer": (int,), "boolean": (bool,), "object": (dict,), "array": (list,),
+             "number": (int, float)}
+
+
+def _validate(value: Any, schema: dict, path: str, errs: List[str]) -> None:
+    t = schema.get("type")
+    if t:
+        ok = isinstance(value, _PY_TYPES[t]) and not (t in ("integer", "number") and isinstance(value, bool))
+        if not ok:
+            errs.append(f"{path}: Invalid value: {value!r}: {path} in body must be of type {t}")
+            return
+    if "enum" in schema and value not in schema["enum"]:
+        allowed = ", ".join(f'"{x}"' for x in schema["enum"])
+        errs.append(f"{path}: Unsupported value: {value!r}: supported values: {allowed}")
+    if "minimum" in schema and isinstance(value, (int, float)) and value < schema["minimum"]:
+        errs.append(f"{path}: Invalid value: {value}: {path} in body should be greater than or equal to {schema['minimum']}")
+    if "maximum" in schema and isinstance(value, (int, float)) and value > schema["maximum"]:
+        errs.append(f"{path}: Invalid value: {value}: {path} in body should be less than or equal to {schema['maximum']}")
+    if "maxLength" in schema and isinstance(value, str) and len(value) > schema["maxLength"]:
+        errs.append(f"{path}: Too long: may not be longer than {schema['maxLength']}")
+    if isinstance(value, dict):
+        for r in schema.get("required", []):
+            if r not in value:
+                errs.append(f"{path}.{r}: Required value")
+        props = schema.get("properties", {})
+        addl = schema.get("additionalProperties")
+        for k, v in value.items():
+            if k in props:
+                _validate(v, props[k], f"{path}.{k}", errs)
+            elif isinstance(addl, dict):
+                _validate(v, addl, f"{path}.{k}", errs)
+    if isinstance(value, list) and "items" in schema:
+        for i, v in enumerate(value):
+            _validate(v, schema["items"], f"{path}[{i}]", errs)
+
+
+def prune(value: Any, schema: dict) -> Any:
+    """Drops fields unknown to a structural schema (what the API server does on write)."""
+    if isinstance(value, dict) and schema.get("type") == "object":
+        props = schema.get("properties")
+        addl = schema.get("additionalProperties")
+        if props is None and addl is None:
+            return value  # e.g. metadata: opaque
+        out = {}
+        for k, v in value.items():
+            if props and k in props:
+                out[k] = prune(v, props[k])
+            elif isinstance(addl, dict):
+                out[k] = prune(v, addl)
+        return out
+    if isinstance(value, list) and "items" in schema:
+        return [prune(v, schema["items"]) for v in value]
+    return value
+
+
+def validate(obj: dict) -> List[str]:
+    """Returns the API-server style field errors for a NetworkClusterPolicy object."""
+    errs: List[str] = []
+    schema = openapi_schema()
+    body = {k: v for k, v in obj.items() if k in ("apiVersion", "kind", "metadata", "spec", "status")}
+    # status is validated through the status subresource only
+    body.pop("status", None)
+    _validate(body, schema, "", errs)
+    return [e[1:] if e.startswith(".") else e for e in errs]
+
+
+def main(argv=None) -> int:
+    root = Path(__file__).resolve().parents[3]
+    text = render_yaml()
+    targets = [root / "config/operator/crd/bases/amd.com_networkclusterpolicies.yaml",
+               root / "charts/network-operator/crds/networkclusterpolicy-crd.yaml"]
+    if argv and argv[0] == "--stdout":
+        sys.stdout.write(text)
+        return 0
+    for t in targets:
+        t.parent.mkdir(parents=True, exist_ok=True)
+        t.write_text(text)
+        print(f"wrote {t}")
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main(sys.argv[1:]))

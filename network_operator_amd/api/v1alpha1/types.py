@@ -1,0 +1,193 @@
+"""v1alpha1 ``NetworkClusterPolicy`` — cluster-scoped, group ``amd.com``.
+
+Field-for-field counterpart of the reference's CRD types
+(reference api/v1alpha1/networkconfiguration_types.go:24-100) with the Gaudi specifics
+renamed for MI355X:
+
+=====================================  ==============================================
+reference                              this API
+=====================================  ==============================================
+configurationType enum ``gaudi-so``    ``amd-so`` (``host-nic`` reserved, types.go:26)
+spec.gaudiScaleOut                     spec.amdScaleOut (same sub-fields)
+status {targets, ready, state, errors} identical
+=====================================  ==============================================
+
+``amdScaleOut`` adds optional MI355X fields (all additive, absent = previous behaviour):
+``xgmiCheck`` (gate readiness on the xGMI mesh), ``lldpAnnounce`` (self-announce to trigger
+switch fast start), ``interfaces`` (extra NICs) and ``nicDrivers`` (affinity allow-list).
+
+Objects are plain dataclasses with lossless ``to_dict`` / ``from_dict`` (unknown fields are
+preserved in ``extra`` so a round trip never drops data written by a newer client).
+"""
+
+from __future__ import annotations
+
+import copy
+from dataclasses import dataclass, field
+from typing import Any, Dict, List, Optional
+
+GROUP = "amd.com"
+VERSION = "v1alpha1"
+API_VERSION = f"{GROUP}/{VERSION}"
+KIND = "NetworkClusterPolicy"
+LIST_KIND = "NetworkClusterPolicyList"
+PLURAL = "networkclusterpolicies"
+SINGULAR = "networkclusterpolicy"
+
+CONFIG_AMD_SCALE_OUT = "amd-so"
+CONFIGURATION_TYPES = (CONFIG_AMD_SCALE_OUT,)
+LAYERS = ("L2", "L3")
+PULL_POLICIES = ("Never", "Always", "IfNotPresent")
+MTU_MIN, MTU_MAX = 1500, 9000
+LOG_LEVEL_MIN, LOG_LEVEL_MAX = 0, 8
+DEFAULT_AGENT_IMAGE = "amd/amd-network-linkdiscovery:latest"
+
+
+@dataclass
+class AmdScaleOutSpec:
+    disableNetworkManager: bool = False
+    layer: str = ""
+    image: str = ""
+    pullPolicy: str = ""
+    mtu: int = 0
+    # MI355X additions
+    xgmiCheck: bool = False
+    lldpAnnounce: Optional[bool] = None
+    interfaces: List[str] = field(default_factory=list)
+    nicDrivers: List[str] = field(default_factory=list)
+    extra: Dict[str, Any] = field(default_factory=dict)
+
+    _FIELDS = ("disableNetworkManager", "layer", "image", "pullPolicy", "mtu", "xgmiCheck", "lldpAnnounce",
+               "interfaces", "nicDrivers")
+
+    def to_dict(self) -> dict:
+        d: dict = {}
+        # omitempty semantics, like the Go struct tags
+        if self.disableNetworkManager:
+            d["disableNetworkManager"] = True
+        for k in ("layer", "image", "pullPolicy"):
+            if getattr(self, k):
+                d[k] = getattr(self, k)
+        if self.mtu:
+            d["mtu"] = self.mtu
+        if self.xgmiCheck:
+            d["xgmiCheck"] = True
+        if self.lldpAnnounce is not None:
+            d["lldpAnnounce"] = self.lldpAnnounce
+        if self.interfaces:
+            d["interfaces"] = list(self.interfaces)
+        if self.nicDrivers:
+            d["nicDrivers"] = list(self.nicDrivers)
+        d.update(copy.deepcopy(self.extra))
+        return d
+
+    @classmethod
+    def from_dict(cls, d: Optional[dict]) -> "AmdScaleOutSpec":
+        d = dict(d or {})
+        s = cls(
+            disableNetworkManager=bool(d.pop("disableNetworkManager", False)),
+            layer=d.pop("layer", "") or "",
+            image=d.pop("image", "") or "",
+            pullPolicy=d.pop("pullPolicy", "") or "",
+            mtu=int(d.pop("mtu", 0) or 0),
+            xgmiCheck=bool(d.pop("xgmiCheck", False)),
+            lldpAnnounce=d.pop("lldpAnnounce", None),
+            interfaces=list(d.pop("interfaces", []) or []),
+            nicDrivers=list(d.pop("nicDrivers", []) or []),
+        )
+        s.extra = d
+        return s
+
+
+@dataclass
+class NetworkClusterPolicySpec:
+    configurationType: str = ""
+    nodeSelector: Dict[str, str] = field(default_factory=dict)
+    amdScaleOut: AmdScaleOutSpec = field(default_factory=AmdScaleOutSpec)
+    logLevel: int = 0
+    extra: Dict[str, Any] = field(default_factory=dict)
+
+    def to_dict(self) -> dict:
+        d: dict = {"configurationType": self.configurationType}
+        if self.nodeSelector:
+            d["nodeSelector"] = dict(self.nodeSelector)
+        so = self.amdScaleOut.to_dict()
+        d["amdScaleOut"] = so  # struct without omitempty pointer: always serialised
+        if self.logLevel:
+            d["logLevel"] = self.logLevel
+        d.update(copy.deepcopy(self.extra))
+        return d
+
+    @classmethod
+    def from_dict(cls, d: Optional[dict]) -> "NetworkClusterPolicySpec":
+        d = dict(d or {})
+        s = cls(
+            configurationType=d.pop("configurationType", "") or "",
+            nodeSelector=dict(d.pop("nodeSelector", {}) or {}),
+            amdScaleOut=AmdScaleOutSpec.from_dict(d.pop("amdScaleOut", None)),
+            logLevel=int(d.pop("logLevel", 0) or 0),
+        )
+        s.extra = d
+        return s
+
+
+@dataclass
+class NetworkClusterPolicyStatus:
+    targets: int = 0
+    ready: int = 0
+    state: str = ""
+    errors: List[str] = field(default_factory=list)
+
+    def to_dict(self) -> dict:
+        return {"targets": self.targets, "ready": self.ready, "state": self.state, "errors": list(self.errors)}
+
+    @classmethod
+    def from_dict(cls, d: Optional[dict]) -> "NetworkClusterPolicyStatus":
+        d = d or {}
+        return cls(targets=int(d.get("targets", 0) or 0), ready=int(d.get("ready", 0) or 0),
+                   state=d.get("state", "") or "", errors=list(d.get("errors") or []))
+
+
+@dataclass
+class NetworkClusterPolicy:
+    metadata: Dict[str, Any] = field(default_factory=dict)
+    spec: NetworkClusterPolicySpec = field(default_factory=NetworkClusterPolicySpec)
+    status: NetworkClusterPolicyStatus = field(default_factory=NetworkClusterPolicyStatus)
+    has_status: bool = False
+
+    apiVersion = API_VERSION
+    kind = KIND
+
+    @property
+    def name(self) -> str:
+        return self.metadata.get("name", "")
+
+    @property
+    def uid(self) -> str:
+        return self.metadata.get("uid", "")
+
+    def to_dict(self) -> dict:
+        d = {"apiVersion": API_VERSION, "kind": KIND, "metadata": copy.deepcopy(self.metadata),
+             "spec": self.spec.to_dict()}
+        if self.has_status or self.status.state or self.status.targets or self.status.ready:
+            d["status"] = self.status.to_dict()
+        return d
+
+    @classmethod
+    def from_dict(cls, d: dict) -> "NetworkClusterPolicy":
+        return cls(metadata=copy.deepcopy(d.get("metadata", {})), spec=NetworkClusterPolicySpec.from_dict(d.get("spec")),
+                   status=NetworkClusterPolicyStatus.from_dict(d.get("status")), has_status="status" in d)
+
+    def deepcopy(self) -> "NetworkClusterPolicy":
+        """DeepCopy (reference zz_generated.deepcopy.go): maps and slices are copied, not shared."""
+        return copy.deepcopy(self)
+
+
+def new_policy(name: str, layer: str = "L3", node_selector: Optional[dict] = None, **so) -> NetworkClusterPolicy:
+    """Convenience constructor used by samples, the Helm renderer and tests."""
+    return NetworkClusterPolicy(
+        metadata={"name": name},
+        spec=NetworkClusterPolicySpec(configurationType=CONFIG_AMD_SCALE_OUT,
+                                      nodeSelector=dict({"amd.feature.node.kubernetes.io/gpu-ready": "true"}
+                                                        if node_selector is None else node_selector),
+                                      amdScaleOut=AmdScaleOutSpec(layer=layer, **so)))

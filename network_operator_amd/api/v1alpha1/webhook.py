@@ -1,0 +1,187 @@
+"""Defaulting and validating admission logic for ``NetworkClusterPolicy``.
+
+Mirrors the reference webhook (reference api/v1alpha1/networkconfiguration_webhook.go):
+
+* ``default``: for ``amd-so`` with an empty image, set the default agent image (:65-74).
+* ``validate_create`` / ``validate_update``: nodeSelector must be non-empty; every key
+  <= 253 and value <= 63 characters; key prefix / name / value must match the same regular
+  expressions (:83-85,91-119) — including the reference's quirk that the *prefix* regex
+  does not accept ``-``; unknown ``configurationType`` -> ``UnknownConfigurationError``
+  (:121-132).  ``validate_delete`` always allows (:149-153).
+* ``admission_review``: the wire protocol (admission.k8s.io/v1 AdmissionReview) for the
+  HTTPS server in ``network_operator_amd.operator.webhook_server``.  The mutating reply is
+  an RFC 6902 JSONPatch.
+
+The webhooks are registered for the *plural* resource ``networkclusterpolicies`` (the
+reference registers the singular, so the API server never calls them — SURVEY.md §3.6).
+"""
+
+from __future__ import annotations
+
+import base64
+import copy
+import json
+import logging
+import re
+from typing import List, Optional, Tuple
+
+from . import types as T
+
+log = logging.getLogger("networkclusterpolicy-resource")
+
+MUTATE_PATH = "/mutate-amd-com-v1alpha1-networkclusterpolicy"
+VALIDATE_PATH = "/validate-amd-com-v1alpha1-networkclusterpolicy"
+
+LABEL_HOST_RE = re.compile(r"^([A-Za-z0-9][A-Za-z0-9_\.]*)?[A-Za-z0-9]$")
+LABEL_PATH_RE = re.compile(r"^([A-Za-z0-9][A-Za-z0-9-\._\/]*)?[A-Za-z0-9]$")
+LABEL_VALUE_RE = re.compile(r"^(([A-Za-z0-9][-A-Za-z0-9_.]*)?[A-Za-z0-9])?$")
+
+
+class ValidationError(ValueError):
+    message = "validation error"
+
+    def __str__(self) -> str:  # same texts as the reference error types (:35-51)
+        return self.message
+
+
+class EmptyNodeSelectorError(ValidationError):
+    message = "empty node-selector"
+
+
+class InvalidNodeSelectorError(ValidationError):
+    message = "invalid node selector"
+
+
+class UnknownConfigurationError(ValidationError):
+    message = "unknown error"
+
+
+class InvalidInterfaceError(ValidationError):
+    def __init__(self, name: str):
+        super().__init__(name)
+        self.message = f"invalid interface name {name!r}"
+
+
+def default(policy: T.NetworkClusterPolicy) -> T.NetworkClusterPolicy:
+    log.info("default name=%s", policy.name)
+    if policy.spec.configurationType == T.CONFIG_AMD_SCALE_OUT and not policy.spec.amdScaleOut.image:
+        policy.spec.amdScaleOut.image = T.DEFAULT_AGENT_IMAGE
+    return policy
+
+
+def validate_node_selector(ns: dict) -> None:
+    if not ns:
+        raise EmptyNodeSelectorError()
+    for k, v in ns.items():
+        if not isinstance(k, str) or not isinstance(v, str):
+            raise InvalidNodeSelectorError()
+        if len(k) > 253 or len(v) > 63:
+            raise InvalidNodeSelectorError()
+        if not LABEL_VALUE_RE.match(v):
+            raise InvalidNodeSelectorError()
+        parts = k.split("/", 1)
+        if len(parts) == 1:
+            if not LABEL_HOST_RE.match(parts[0]):
+                raise InvalidNodeSelectorError()
+        else:
+            if not LABEL_HOST_RE.match(parts[0]) or not LABEL_PATH_RE.match(parts[1]):
+                raise InvalidNodeSelectorError()
+
+
+def validate_amd_so_spec(s: T.AmdScaleOutSpec) -> List[str]:
+    """Returns admission warnings.  (The reference's validateGaudiSoSpec is a no-op, :87-89.)"""
+    warnings = []
+    if s.layer == "L2" and s.xgmiCheck is False and s.lldpAnnounce is not None:
+        warnings.append("lldpAnnounce has no effect in L2 mode")
+    for i in s.interfaces:
+        if not i or len(i) > 15 or "/" in i or " " in i or "," in i:
+            raise InvalidInterfaceError(i)
+    return warnings
+
+
+def validate_spec(spec: T.NetworkClusterPolicySpec) -> List[str]:
+    validate_node_selector(spec.nodeSelector)
+    if spec.configurationType == T.CONFIG_AMD_SCALE_OUT:
+        return validate_amd_so_spec(spec.amdScaleOut)
+    raise UnknownConfigurationError()
+
+
+def validate_create(policy: T.NetworkClusterPolicy) -> List[str]:
+    log.info("validate create name=%s", policy.name)
+    return validate_spec(policy.spec)
+
+
+def validate_update(policy: T.NetworkClusterPolicy, old: Optional[T.NetworkClusterPolicy] = None) -> List[str]:
+    log.info("validate update name=%s", policy.name)
+    return validate_spec(policy.spec)
+
+
+def validate_delete(policy: T.NetworkClusterPolicy) -> List[str]:
+    log.info("validate delete name=%s", policy.name)
+    return []
+
+
+# ---------------------------------------------------------------------------
+# AdmissionReview wire protocol
+# ---------------------------------------------------------------------------
+def json_patch(before, after, path: str = "") -> list:
+    """Minimal RFC 6902 diff (add / replace / remove) between two JSON documents."""
+    ops = []
+    if isinstance(before, dict) and isinstance(after, dict):
+        for k in before:
+            p = f"{path}/{_esc(k)}"
+            if k not in after:
+                ops.append({"op": "remove", "path": p})
+            else:
+                ops.extend(json_patch(before[k], after[k], p))
+        for k in after:
+            if k not in before:
+                ops.append({"op": "add", "path": f"{path}/{_esc(k)}", "value": after[k]})
+        return ops
+    if before != after:
+        ops.append({"op": "replace", "path": path or "/", "value": after})
+    return ops
+
+
+def _esc(k: str) -> str:
+    return str(k).replace("~", "~0").replace("/", "~1")
+
+
+def admission_review(review: dict, mutate: bool) -> dict:
+    """Handles one admission.k8s.io/v1 AdmissionReview request and returns the response review."""
+    req = review.get("request") or {}
+    uid = req.get("uid", "")
+    resp: dict = {"uid": uid, "allowed": True}
+    op = req.get("operation", "")
+    try:
+        if mutate:
+            obj = req.get("object") or {}
+            before = copy.deepcopy(obj)
+            pol = default(T.NetworkClusterPolicy.from_dict(obj))
+            after = copy.deepcopy(obj)
+            after["spec"] = pol.spec.to_dict()
+            ops = json_patch(before, after)
+            if ops:
+                resp["patchType"] = "JSONPatch"
+                resp["patch"] = base64.b64encode(json.dumps(ops).encode()).decode()
+        else:
+            warnings: List[str] = []
+            if op == "CREATE":
+                warnings = validate_create(T.NetworkClusterPolicy.from_dict(req.get("object") or {}))
+            elif op == "UPDATE":
+                warnings = validate_update(T.NetworkClusterPolicy.from_dict(req.get("object") or {}),
+                                           T.NetworkClusterPolicy.from_dict(req.get("oldObject") or {}))
+            elif op == "DELETE":
+                warnings = validate_delete(T.NetworkClusterPolicy.from_dict(req.get("oldObject") or {}))
+            if warnings:
+                resp["warnings"] = warnings
+    except ValueError as e:
+        resp = {"uid": uid, "allowed": False, "status": {"code": 403, "message": str(e), "reason": "Forbidden"}}
+    return {"apiVersion": "admission.k8s.io/v1", "kind": "AdmissionReview", "response": resp}
+
+
+def decode_patch(resp_review: dict) -> Tuple[Optional[str], list]:
+    r = resp_review.get("response", {})
+    if "patch" not in r:
+        return None, []
+    return r.get("patchType"), json.loads(base64.b64decode(r["patch"]))

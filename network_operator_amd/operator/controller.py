@@ -1,0 +1,132 @@
+"""Controller: informers + work queue + workers around the reconciler.
+
+The reference builds this with ``ctrl.NewControllerManagedBy(mgr).For(&NetworkClusterPolicy{})
+.Owns(&apps.DaemonSet{})`` (reference internal/controller/networkconfiguration_controller.go:407-429):
+events on a policy enqueue the policy; events on a DaemonSet enqueue the policy that controls
+it.  Reconcile errors are retried with per-item exponential backoff, ``Result.requeue`` is
+rate-limited, ``Result.requeue_after`` is delayed, success forgets the item's backoff.
+"""
+
+from __future__ import annotations
+
+import asyncio
+import logging
+import time
+from typing import List, Optional
+
+from ..api.v1alpha1 import types as T
+from . import kube
+from .informer import Informer, controller_of
+from .kube import ApiClient
+from .metrics import OperatorMetrics
+from .reconciler import OWNER_KEY, EventRecorder, NetworkClusterPolicyReconciler, policy_owner_index
+from .workqueue import RateLimitingQueue
+
+log = logging.getLogger("controller")
+
+CONTROLLER_NAME = "networkclusterpolicy"
+
+
+class PolicyController:
+    def __init__(self, client: ApiClient, namespace: str, is_openshift: bool = False, workers: int = 2,
+                 metrics: Optional[OperatorMetrics] = None, record_events: bool = True):
+        self.client = client
+        self.namespace = namespace
+        self.workers = workers
+        self.metrics = metrics or OperatorMetrics()
+        self.policies = Informer(client, kube.NETWORKCLUSTERPOLICIES)
+        self.daemonsets = Informer(client, kube.DAEMONSETS, namespace=namespace)
+        self.daemonsets.add_index(OWNER_KEY, policy_owner_index)
+        self.queue = RateLimitingQueue(CONTROLLER_NAME)
+        self.reconciler = NetworkClusterPolicyReconciler(
+            client, namespace, is_openshift,
+            get_policy=lambda name: self.policies.get(name),
+            list_owned=lambda name: self.daemonsets.by_index(OWNER_KEY, name),
+            recorder=EventRecorder(client, namespace) if record_events else None)
+        self.policies.add_handler(self._on_policy)
+        self.daemonsets.add_handler(self._on_daemonset)
+        self._tasks: List[asyncio.Task] = []
+        self.reconciles = 0
+
+    async def _on_policy(self, ev: str, obj: dict, old: Optional[dict]) -> None:
+        await self._enqueue(obj["metadata"]["name"])
+
+    async def _on_daemonset(self, ev: str, obj: dict, old: Optional[dict]) -> None:
+        ref = controller_of(obj)
+        if ref and ref.get("kind") == T.KIND and ref.get("apiVersion") == T.API_VERSION:
+            await self._enqueue(ref["name"])
+
+    async def _enqueue(self, name: str) -> None:
+        await self.queue.add(name)
+        self.metrics.queue_adds.labels(CONTROLLER_NAME).inc()
+        self.metrics.queue_depth.labels(CONTROLLER_NAME).set(self.queue.depth)
+
+    async def _worker(self) -> None:
+        while True:
+            name = await self.queue.get()
+            if name is None:
+                return
+            self.metrics.queue_depth.labels(CONTROLLER_NAME).set(self.queue.depth)
+            t0 = time.perf_counter()
+            try:
+                res = await self.reconciler.reconcile(name)
+            except asyncio.CancelledError:
+                await self.queue.done(name)
+                raise
+            except Exception as e:
+                log.error("Reconciler error for %s: %s", name, e)
+                self.metrics.reconcile_errors.labels(CONTROLLER_NAME).inc()
+                self.metrics.reconcile_total.labels(CONTROLLER_NAME, "error").inc()
+                self.metrics.queue_retries.labels(CONTROLLER_NAME).inc()
+                await self.queue.add_rate_limited(name)
+            else:
+                if res.requeue_after > 0:
+                    self.queue.forget(name)
+                    await self.queue.add_after(name, res.requeue_after)
+                    self.metrics.reconcile_total.labels(CONTROLLER_NAME, "requeue_after").inc()
+                elif res.requeue:
+                    await self.queue.add_rate_limited(name)
+                    self.metrics.queue_retries.labels(CONTROLLER_NAME).inc()
+                    self.metrics.reconcile_total.labels(CONTROLLER_NAME, "requeue").inc()
+                else:
+                    self.queue.forget(name)
+                    self.metrics.reconcile_total.labels(CONTROLLER_NAME, "success").inc()
+                self._export_policy(name)
+            finally:
+                self.reconciles += 1
+                self.metrics.reconcile_time.labels(CONTROLLER_NAME).observe(time.perf_counter() - t0)
+            await self.queue.done(name)
+
+    def _export_policy(self, name: str) -> None:
+        p = self.policies.get(name)
+        if p is None:
+            for g in (self.metrics.policy_targets, self.metrics.policy_ready):
+                try:
+                    g.remove(name)
+                except KeyError:
+                    pass
+            return
+        st = p.get("status") or {}
+        self.metrics.policy_targets.labels(name).set(st.get("targets", 0) or 0)
+        self.metrics.policy_ready.labels(name).set(st.get("ready", 0) or 0)
+
+    async def start(self) -> None:
+        self._tasks.append(self.policies.start())
+        self._tasks.append(self.daemonsets.start())
+        await asyncio.gather(self.policies.synced.wait(), self.daemonsets.synced.wait())
+        for _ in range(self.workers):
+            self._tasks.append(asyncio.ensure_future(self._worker()))
+
+    def has_synced(self) -> bool:
+        return self.policies.synced.is_set() and self.daemonsets.synced.is_set()
+
+    async def stop(self) -> None:
+        await self.queue.shutdown()
+        for t in self._tasks:
+            t.cancel()
+        for t in self._tasks:
+            try:
+                await t
+            except (asyncio.CancelledError, Exception):
+                pass
+        self._tasks.clear()

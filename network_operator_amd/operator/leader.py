@@ -1,0 +1,159 @@
+"""Lease-based leader election (coordination.k8s.io/v1), client-go ``leaderelection`` semantics.
+
+The reference manager enables it with ``--leader-elect`` and ID ``9a8a7ba6.intel.com``
+(reference cmd/operator/main.go:98-100,174-175).  Here: ID ``9a8a7ba6.amd.com``, lease
+duration 15 s, renew deadline 10 s, retry period 2 s (controller-runtime defaults).
+Expiry is judged on the *locally observed* time of the last record change, as client-go
+does, so clock skew between replicas does not matter.
+"""
+
+from __future__ import annotations
+
+import asyncio
+import datetime as dt
+import logging
+import os
+import socket
+import uuid
+from typing import Awaitable, Callable, Optional
+
+from . import kube
+from .kube import ApiClient, ApiError, is_already_exists, is_conflict, is_not_found
+
+log = logging.getLogger("leaderelection")
+
+DEFAULT_LEASE_ID = "9a8a7ba6.amd.com"
+
+
+def _now_str() -> str:
+    return dt.datetime.now(dt.timezone.utc).strftime("%Y-%m-%dT%H:%M:%S.%fZ")
+
+
+def default_identity() -> str:
+    return f"{socket.gethostname()}_{uuid.uuid4()}"
+
+
+class LeaderElector:
+    def __init__(self, client: ApiClient, namespace: str, name: str = DEFAULT_LEASE_ID,
+                 identity: Optional[str] = None, lease_duration: float = 15.0, renew_deadline: float = 10.0,
+                 retry_period: float = 2.0, release_on_cancel: bool = True, clock=None):
+        self.client = client
+        self.namespace = namespace
+        self.name = name
+        self.identity = identity or default_identity()
+        self.lease_duration = lease_duration
+        self.renew_deadline = renew_deadline
+        self.retry_period = retry_period
+        self.release_on_cancel = release_on_cancel
+        self._loop_time = clock or (lambda: asyncio.get_event_loop().time())
+        self._observed_record: Optional[dict] = None
+        self._observed_time = 0.0
+        self.is_leader = False
+        self.transitions = 0
+
+    def _lease_body(self, prev: Optional[dict]) -> dict:
+        spec_prev = (prev or {}).get("spec", {}) or {}
+        same_holder = spec_prev.get("holderIdentity") == self.identity
+        transitions = int(spec_prev.get("leaseTransitions", 0) or 0) + (0 if same_holder or not prev else 1)
+        body = {
+            "apiVersion": "coordination.k8s.io/v1", "kind": "Lease",
+            "metadata": {"name": self.name, "namespace": self.namespace},
+            "spec": {"holderIdentity": self.identity, "leaseDurationSeconds": int(self.lease_duration),
+                     "acquireTime": spec_prev.get("acquireTime") if same_holder else _now_str(),
+                     "renewTime": _now_str(), "leaseTransitions": transitions},
+        }
+        if prev:
+            body["metadata"]["resourceVersion"] = prev["metadata"].get("resourceVersion")
+        return body
+
+    async def try_acquire_or_renew(self) -> bool:
+        try:
+            lease = await self.client.get(kube.LEASES, self.name, self.namespace)
+        except ApiError as e:
+            if not is_not_found(e):
+                log.warning("error retrieving lease %s: %s", self.name, e)
+                return False
+            try:
+                await self.client.create(kube.LEASES, self._lease_body(None), namespace=self.namespace)
+            except ApiError as ce:
+                if is_already_exists(ce):
+                    return False
+                raise
+            self._observe(None)
+            return True
+        spec = lease.get("spec", {}) or {}
+        if self._observed_record != spec:
+            self._observed_record = dict(spec)
+            self._observed_time = self._loop_time()
+        holder = spec.get("holderIdentity") or ""
+        duration = float(spec.get("leaseDurationSeconds") or self.lease_duration)
+        if holder and holder != self.identity and self._observed_time + duration > self._loop_time():
+            return False  # held by someone else and not expired
+        try:
+            updated = await self.client.replace(kube.LEASES, self._lease_body(lease))
+        except ApiError as e:
+            if is_conflict(e):
+                return False
+            raise
+        if holder != self.identity:
+            self.transitions += 1
+        self._observe(updated)
+        return True
+
+    def _observe(self, lease: Optional[dict]) -> None:
+        self._observed_record = dict((lease or {}).get("spec", {}) or {}) if lease else None
+        self._observed_time = self._loop_time()
+
+    async def release(self) -> None:
+        try:
+            lease = await self.client.get(kube.LEASES, self.name, self.namespace)
+            if (lease.get("spec", {}) or {}).get("holderIdentity") != self.identity:
+                return
+            lease["spec"]["holderIdentity"] = ""
+            lease["spec"]["leaseDurationSeconds"] = 1
+            await self.client.replace(kube.LEASES, lease)
+        except Exception as e:
+            log.info("lease release failed: %s", e)
+
+    async def run(self, on_started_leading: Callable[[], Awaitable[None]],
+                  on_stopped_leading: Optional[Callable[[], Awaitable[None]]] = None) -> None:
+        """Blocks: acquire, run ``on_started_leading`` concurrently while renewing; returns when
+        leadership is lost (the caller then exits, like controller-runtime)."""
+        while True:
+            try:
+                if await self.try_acquire_or_renew():
+                    break
+            except Exception as e:
+                log.warning("acquire failed: %s", e)
+            await asyncio.sleep(self.retry_period)
+        self.is_leader = True
+        log.info("successfully acquired lease %s/%s as %s", self.namespace, self.name, self.identity)
+        work = asyncio.ensure_future(on_started_leading())
+        try:
+            last_ok = self._loop_time()
+            while True:
+                if work.done():
+                    await work  # propagate errors from the leader's work
+                    return
+                await asyncio.sleep(self.retry_period)
+                try:
+                    ok = await self.try_acquire_or_renew()
+                except Exception as e:
+                    log.warning("renew failed: %s", e)
+                    ok = False
+                if ok:
+                    last_ok = self._loop_time()
+                elif self._loop_time() - last_ok > self.renew_deadline:
+                    log.error("leader election lost")
+                    return
+        finally:
+            self.is_leader = False
+            work.cancel()
+            try:
+                await work
+            except (asyncio.CancelledError, Exception):
+                pass
+            if on_stopped_leading:
+                await on_stopped_leading()
+            if self.release_on_cancel:
+                await self.release()

@@ -1,0 +1,142 @@
+"""``manager`` — the operator process (Deployment, one active replica via leader election).
+
+Reference entrypoint: cmd/operator/main.go.  Same flags (:95-112):
+``--metrics-bind-address`` (default "0" = off), ``--health-probe-bind-address`` (":8081"),
+``--leader-elect``, ``--metrics-secure``, ``--enable-http2`` plus zap logging flags; same
+environment: ``OPERATOR_NAMESPACE`` (default ``amd-network-operator``), ``ENABLE_WEBHOOKS``
+("false" disables the webhook server).  OpenShift is detected from the API server's groups
+(``route.openshift.io`` / ``security.openshift.io``, :64-87) — through the same client
+configuration as everything else, so detection also works out of cluster.
+"""
+
+from __future__ import annotations
+
+import argparse
+import asyncio
+import logging
+import os
+import signal
+import sys
+from typing import List, Optional
+
+from .controller import PolicyController
+from .kube import ApiClient, load_config
+from .leader import DEFAULT_LEASE_ID, LeaderElector
+from .metrics import OperatorMetrics
+from .servers import DEFAULT_CERT_DIR, Servers
+
+log = logging.getLogger("setup")
+
+DEFAULT_OPERATOR_NAMESPACE = "amd-network-operator"
+OPENSHIFT_GROUPS = ("route.openshift.io", "security.openshift.io")
+
+
+async def is_openshift(client: ApiClient) -> bool:
+    groups = await client.server_groups()
+    return any(g in OPENSHIFT_GROUPS for g in groups)
+
+
+def build_parser() -> argparse.ArgumentParser:
+    ap = argparse.ArgumentParser(prog="manager", description="AMD MI355X network operator")
+    ap.add_argument("--metrics-bind-address", default="0",
+                    help="The address the metrics endpoint binds to. Use :8443 for HTTPS or :8080 for HTTP, "
+                         "or leave as 0 to disable the metrics service.")
+    ap.add_argument("--health-probe-bind-address", default=":8081", help="The address the probe endpoint binds to.")
+    ap.add_argument("--leader-elect", action="store_true",
+                    help="Enable leader election for controller manager.")
+    ap.add_argument("--metrics-secure", action="store_true", help="If set the metrics endpoint is served securely")
+    ap.add_argument("--enable-http2", action="store_true",
+                    help="If set, HTTP/2 would be enabled for the metrics and webhook servers (HTTP/1.1 only here)")
+    ap.add_argument("--kubeconfig", default=None)
+    ap.add_argument("--master", default=None, help="API server URL (overrides kubeconfig; tests)")
+    ap.add_argument("--webhook-port", type=int, default=9443)
+    ap.add_argument("--webhook-cert-dir", default=DEFAULT_CERT_DIR)
+    ap.add_argument("--workers", type=int, default=2, help="concurrent reconciles")
+    ap.add_argument("--leader-election-id", default=DEFAULT_LEASE_ID)
+    ap.add_argument("--zap-devel", action="store_true", default=True)
+    ap.add_argument("--zap-log-level", default="info")
+    ap.add_argument("--zap-encoder", default="console", choices=["console", "json"])
+    return ap
+
+
+def setup_logging(level: str, encoder: str) -> None:
+    lvl = {"debug": logging.DEBUG, "info": logging.INFO, "error": logging.ERROR}.get(level, logging.INFO)
+    if level.isdigit():
+        lvl = max(1, logging.INFO - int(level))
+    fmt = ('{"ts":"%(asctime)s","level":"%(levelname)s","logger":"%(name)s","msg":"%(message)s"}'
+           if encoder == "json" else "%(asctime)s\t%(levelname)s\t%(name)s\t%(message)s")
+    logging.basicConfig(level=lvl, format=fmt, stream=sys.stderr, force=True)
+
+
+async def run(argv: Optional[List[str]] = None, stop: Optional[asyncio.Event] = None,
+              started: Optional[asyncio.Event] = None) -> int:
+    opts = build_parser().parse_args(argv)
+    setup_logging(opts.zap_log_level, opts.zap_encoder)
+    ns = os.environ.get("OPERATOR_NAMESPACE") or DEFAULT_OPERATOR_NAMESPACE
+    log.info("Using namespace: %s", ns)
+    stop = stop or asyncio.Event()
+    loop = asyncio.get_event_loop()
+    for sig in (signal.SIGTERM, signal.SIGINT):
+        try:
+            loop.add_signal_handler(sig, stop.set)
+        except (NotImplementedError, RuntimeError):  # not the main thread (tests)
+            pass
+
+    client = ApiClient(load_config(opts.kubeconfig, opts.master))
+    try:
+        try:
+            openshift = await is_openshift(client)
+        except Exception as e:
+            log.error("unable to check if running in OpenShift: %s", e)
+            return 1
+        if openshift:
+            log.info("Detected OpenShift environment")
+        metrics = OperatorMetrics()
+        controller = PolicyController(client, ns, openshift, workers=opts.workers, metrics=metrics)
+        servers = Servers(metrics, ready_check=lambda: True, client=client)
+        webhooks = os.environ.get("ENABLE_WEBHOOKS", "") != "false"
+        await servers.start(opts.health_probe_bind_address, opts.metrics_bind_address, opts.metrics_secure,
+                            opts.webhook_port if webhooks else None, opts.webhook_cert_dir)
+
+        async def lead() -> None:
+            await controller.start()
+            if started:
+                started.set()
+            log.info("starting manager")
+            await stop.wait()
+
+        try:
+            if opts.leader_elect:
+                elector = LeaderElector(client, ns, opts.leader_election_id)
+                metrics.leader.labels(opts.leader_election_id).set(0)
+
+                async def lead_with_metric() -> None:
+                    metrics.leader.labels(opts.leader_election_id).set(1)
+                    await lead()
+
+                runner = asyncio.ensure_future(elector.run(lead_with_metric))
+                stopper = asyncio.ensure_future(stop.wait())
+                done, _ = await asyncio.wait({runner, stopper}, return_when=asyncio.FIRST_COMPLETED)
+                if runner not in done:
+                    runner.cancel()
+                    try:
+                        await runner
+                    except (asyncio.CancelledError, Exception):
+                        pass
+                stopper.cancel()
+            else:
+                await lead()
+        finally:
+            await controller.stop()
+            await servers.stop()
+        return 0
+    finally:
+        await client.close()
+
+
+def main(argv: Optional[List[str]] = None) -> int:
+    return asyncio.run(run(argv))
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,39 @@
+"""Prometheus metrics of the control plane.
+
+controller-runtime exports reconcile counters / latency and work-queue gauges on the
+metrics endpoint (reference cmd/operator/main.go:157-167); the same metric
+names are used here so existing dashboards keep working, plus per-policy readiness gauges.
+"""
+
+from __future__ import annotations
+
+from prometheus_client import CollectorRegistry, Counter, Gauge, Histogram, generate_latest
+from prometheus_client.exposition import CONTENT_TYPE_LATEST
+
+
+class OperatorMetrics:
+    def __init__(self, registry: CollectorRegistry | None = None):
+        self.registry = registry or CollectorRegistry()
+        r = self.registry
+        self.reconcile_total = Counter("controller_runtime_reconcile_total", "Total number of reconciliations per controller",
+                                       ["controller", "result"], registry=r)
+        self.reconcile_errors = Counter("controller_runtime_reconcile_errors_total",
+                                        "Total number of reconciliation errors per controller", ["controller"], registry=r)
+        self.reconcile_time = Histogram("controller_runtime_reconcile_time_seconds",
+                                        "Length of time per reconciliation per controller", ["controller"],
+                                        buckets=(0.001, 0.0025, 0.005, 0.01, 0.025, 0.05, 0.1, 0.25, 0.5, 1, 2.5, 5, 10),
+                                        registry=r)
+        self.queue_depth = Gauge("workqueue_depth", "Current depth of workqueue", ["name"], registry=r)
+        self.queue_adds = Counter("workqueue_adds_total", "Total number of adds handled by workqueue", ["name"], registry=r)
+        self.queue_retries = Counter("workqueue_retries_total", "Total number of retries handled by workqueue", ["name"],
+                                     registry=r)
+        self.leader = Gauge("leader_election_master_status", "1 if this instance is the leader", ["name"], registry=r)
+        self.policy_targets = Gauge("amd_network_operator_policy_targets", "Nodes targeted by a NetworkClusterPolicy",
+                                    ["policy"], registry=r)
+        self.policy_ready = Gauge("amd_network_operator_policy_ready",
+                                  "Nodes whose agent published the scale-out readiness label", ["policy"], registry=r)
+
+    def render(self) -> bytes:
+        return generate_latest(self.registry)
+
+    content_type = CONTENT_TYPE_LATEST

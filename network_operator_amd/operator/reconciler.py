@@ -1,0 +1,297 @@
+"""``NetworkClusterPolicy`` reconciler.
+
+Behavioural counterpart of the reference controller
+(reference internal/controller/networkconfiguration_controller.go):
+
+* one DaemonSet per policy, named after the policy, in the operator namespace, owned by the
+  policy (controller ownerReference -> garbage-collected with it);
+* agent arguments are fully recomputed from the spec on every reconcile, in the reference
+  order ``--configure=true --keep-running --mode=<L> [--v=N] [--mtu=N]
+  [--disable-networkmanager] [L3: --wait=90s --rccl-net=... ]`` (:164-204), followed by the
+  MI355X options;
+* hostPath volumes are added by name with type DirectoryOrCreate in the reference order
+  (nfd-features, [var-run-dbus, networkmanager], [artifact dir]) (:69-107);
+* status mirrors the DaemonSet: targets = desiredNumberScheduled, ready = numberReady,
+  state "No targets" / "Working on it.." / "All good", errors [] (:267-307); a status
+  write conflict requeues;
+* OpenShift: ServiceAccount ``<name>-sa`` + RoleBinding ``<name>-sa-rb`` to
+  ``system:openshift:scc:privileged`` (:109-162).
+
+Deliberate fixes (SURVEY.md §7.6 "fix" list): ``pullPolicy`` is applied; volumes that are no
+longer wanted are removed; the agent has a readinessProbe (in the template) so ``ready``
+counts *configured* nodes; ``AlreadyExists`` on create falls back to the update path; and
+Kubernetes Events are emitted (RBAC for them was granted but unused by the reference).
+"""
+
+from __future__ import annotations
+
+import copy
+import logging
+from dataclasses import dataclass
+from typing import Callable, List, Optional
+
+from .. import discovery
+from ..api.v1alpha1 import types as T
+from . import kube
+from .kube import ApiClient, ApiError, is_already_exists, is_conflict, is_not_found
+
+log = logging.getLogger("controller")
+
+OWNER_KEY = ".metadata.controller"
+ARTIFACT_DIR_HOST = "/etc/amd/scale-out"
+ARTIFACT_DIR_CONTAINER = "/host" + ARTIFACT_DIR_HOST
+RCCL_NET_FILE = "rccl-net.json"
+RCCL_ENV_FILE = "rccl.env"
+L3_WAIT = "90s"
+
+STATE_NO_TARGETS = "No targets"
+STATE_WORKING = "Working on it.."
+STATE_ALL_GOOD = "All good"
+
+# Volumes the reconciler manages (the template's nfd-features is never touched).
+MANAGED_VOLUMES = ("var-run-dbus", "networkmanager", "rccl-artifacts")
+
+
+@dataclass
+class Result:
+    requeue: bool = False
+    requeue_after: float = 0.0
+
+
+def owner_reference(owner: dict) -> dict:
+    md = owner["metadata"]
+    return {"apiVersion": owner.get("apiVersion", T.API_VERSION), "kind": owner.get("kind", T.KIND), "name": md["name"],
+            "uid": md.get("uid", ""), "controller": True, "blockOwnerDeletion": True}
+
+
+def set_controller_reference(owner: dict, obj: dict) -> None:
+    """ctrl.SetControllerReference: replace any existing controller reference."""
+    refs = [r for r in obj.setdefault("metadata", {}).get("ownerReferences", []) or [] if not r.get("controller")]
+    refs.append(owner_reference(owner))
+    obj["metadata"]["ownerReferences"] = refs
+
+
+def policy_owner_index(obj: dict) -> List[str]:
+    """indexDaemonSets (:364-383): DaemonSets -> name of the owning NetworkClusterPolicy."""
+    for ref in obj.get("metadata", {}).get("ownerReferences", []) or []:
+        if ref.get("controller") and ref.get("apiVersion") == T.API_VERSION and ref.get("kind") == T.KIND:
+            return [ref["name"]]
+    return []
+
+
+def add_host_volume(ds: dict, name: str, host_path: str, container_path: str,
+                    volume_type: str = "DirectoryOrCreate") -> None:
+    spec = ds["spec"]["template"]["spec"]
+    vols = spec.setdefault("volumes", [])
+    if any(v.get("name") == name for v in vols):
+        return
+    vols.append({"name": name, "hostPath": {"path": host_path, "type": volume_type}})
+    containers = spec.get("containers") or []
+    if containers:
+        containers[0].setdefault("volumeMounts", []).append({"name": name, "mountPath": container_path})
+
+
+def remove_volume(ds: dict, name: str) -> None:
+    spec = ds["spec"]["template"]["spec"]
+    spec["volumes"] = [v for v in spec.get("volumes", []) if v.get("name") != name]
+    for c in spec.get("containers") or []:
+        if "volumeMounts" in c:
+            c["volumeMounts"] = [m for m in c["volumeMounts"] if m.get("name") != name]
+
+
+def agent_args(p: T.NetworkClusterPolicy) -> List[str]:
+    so = p.spec.amdScaleOut
+    args = ["--configure=true", "--keep-running", f"--mode={so.layer}"]
+    if p.spec.logLevel > 0:
+        args.append(f"--v={p.spec.logLevel}")
+    if so.mtu > 0:
+        args.append(f"--mtu={so.mtu}")
+    if so.disableNetworkManager:
+        args += ["--disable-networkmanager", "--nm-keyfile-dir=/etc/NetworkManager/conf.d"]
+    if so.layer == "L3":
+        args += [f"--wait={L3_WAIT}", f"--rccl-net={ARTIFACT_DIR_CONTAINER}/{RCCL_NET_FILE}",
+                 f"--rccl-env={ARTIFACT_DIR_CONTAINER}/{RCCL_ENV_FILE}"]
+    # MI355X options
+    if so.xgmiCheck:
+        args.append("--xgmi-expect=0")
+    if so.lldpAnnounce is False:
+        args.append("--lldp-announce=false")
+    if so.interfaces:
+        args.append("--interfaces=" + ",".join(so.interfaces))
+    if so.nicDrivers:
+        args.append("--nic-drivers=" + ",".join(so.nicDrivers))
+    return args
+
+
+def update_amd_scale_out_daemonset(ds: dict, p: T.NetworkClusterPolicy, namespace: str) -> None:
+    """updateGaudiScaleOutDaemonSet (:164-204) for amd-so."""
+    md = ds.setdefault("metadata", {})
+    md["name"] = p.name
+    md["namespace"] = namespace
+    pod = ds["spec"]["template"]["spec"]
+    if p.spec.nodeSelector:
+        pod["nodeSelector"] = dict(p.spec.nodeSelector)
+    c = pod["containers"][0]
+    so = p.spec.amdScaleOut
+    if so.image:
+        c["image"] = so.image
+    if so.pullPolicy:
+        c["imagePullPolicy"] = so.pullPolicy
+    wanted = set()
+    if so.disableNetworkManager:
+        add_host_volume(ds, "var-run-dbus", "/var/run/dbus", "/var/run/dbus")
+        add_host_volume(ds, "networkmanager", "/etc/NetworkManager", "/etc/NetworkManager")
+        wanted |= {"var-run-dbus", "networkmanager"}
+    if so.layer == "L3":
+        add_host_volume(ds, "rccl-artifacts", ARTIFACT_DIR_HOST, ARTIFACT_DIR_CONTAINER)
+        wanted.add("rccl-artifacts")
+    for v in MANAGED_VOLUMES:
+        if v not in wanted:
+            remove_volume(ds, v)
+    c["args"] = agent_args(p)
+
+
+def status_for(targets: int, ready: int) -> str:
+    if targets == 0:
+        return STATE_NO_TARGETS
+    if ready < targets:
+        return STATE_WORKING
+    return STATE_ALL_GOOD
+
+
+class EventRecorder:
+    """Best-effort core/v1 Events on the policy (failures are only logged)."""
+
+    def __init__(self, client: ApiClient, namespace: str, component: str = "amd-network-operator"):
+        self.client, self.namespace, self.component = client, namespace, component
+        self.sent = 0
+
+    async def event(self, obj: dict, type_: str, reason: str, message: str) -> None:
+        md = obj.get("metadata", {})
+        body = {
+            "apiVersion": "v1", "kind": "Event",
+            "metadata": {"generateName": f"{md.get('name', 'obj')}.", "namespace": self.namespace},
+            "involvedObject": {"apiVersion": obj.get("apiVersion"), "kind": obj.get("kind"), "name": md.get("name"),
+                               "uid": md.get("uid")},
+            "type": type_, "reason": reason, "message": message, "source": {"component": self.component},
+            "count": 1,
+        }
+        try:
+            await self.client.create(kube.EVENTS, body, namespace=self.namespace)
+            self.sent += 1
+        except Exception as e:  # events must never fail a reconcile
+            log.debug("event not recorded: %s", e)
+
+
+class NetworkClusterPolicyReconciler:
+    def __init__(self, client: ApiClient, namespace: str, is_openshift: bool,
+                 get_policy: Callable[[str], Optional[dict]], list_owned: Callable[[str], List[dict]],
+                 recorder: Optional[EventRecorder] = None):
+        self.client = client
+        self.namespace = namespace
+        self.is_openshift = is_openshift
+        self._get_policy = get_policy
+        self._list_owned = list_owned
+        self.recorder = recorder
+
+    async def _event(self, obj: dict, type_: str, reason: str, msg: str) -> None:
+        if self.recorder:
+            await self.recorder.event(obj, type_, reason, msg)
+
+    # -- create ----------------------------------------------------------------------------------
+    async def _create_openshift_collateral(self, parent: dict, sa_name: str) -> None:
+        sa = discovery.linkdiscovery_service_account()
+        sa["metadata"]["name"] = sa_name
+        sa["metadata"]["namespace"] = self.namespace
+        set_controller_reference(parent, sa)
+        try:
+            await self.client.create(kube.SERVICEACCOUNTS, sa, namespace=self.namespace)
+        except ApiError as e:
+            if not is_already_exists(e):
+                log.error("unable to create service account: %s", e)
+                return
+        rb = discovery.openshift_role_binding()
+        rb["metadata"]["name"] = sa_name + "-rb"
+        rb["metadata"]["namespace"] = self.namespace
+        rb["subjects"] = [{"kind": "ServiceAccount", "name": sa_name, "namespace": self.namespace}]
+        set_controller_reference(parent, rb)
+        try:
+            await self.client.create(kube.ROLEBINDINGS, rb, namespace=self.namespace)
+        except ApiError as e:
+            if not is_already_exists(e):
+                log.error("unable to create role binding: %s", e)
+
+    async def _create_daemonset(self, raw: dict, p: T.NetworkClusterPolicy) -> Result:
+        if p.spec.configurationType != T.CONFIG_AMD_SCALE_OUT:
+            log.info("Unknown configuration type, this shouldn't happen! type=%s", p.spec.configurationType)
+            raise ValueError(f"unknown configuration type {p.spec.configurationType!r}")
+        ds = discovery.discovery_daemonset()
+        sa_name = p.name + "-sa" if self.is_openshift else ""
+        if sa_name:
+            ds["spec"]["template"]["spec"]["serviceAccountName"] = sa_name
+        update_amd_scale_out_daemonset(ds, p, self.namespace)
+        set_controller_reference(raw, ds)
+        log.info("Creating AMD scale-out DaemonSet name=%s", p.name)
+        try:
+            created = await self.client.create(kube.DAEMONSETS, ds, namespace=self.namespace)
+        except ApiError as e:
+            if not is_already_exists(e):
+                raise
+            # Our cache has not seen it yet: continue on the update path with the live object.
+            created = await self.client.get(kube.DAEMONSETS, p.name, self.namespace)
+            return await self._update(raw, p, created)
+        await self._event(raw, "Normal", "DaemonSetCreated", f"Created DaemonSet {self.namespace}/{p.name}")
+        if sa_name:
+            await self._create_openshift_collateral(raw, sa_name)
+        return await self._update_status(raw, p, created)
+
+    # -- update ----------------------------------------------------------------------------------
+    async def _update(self, raw: dict, p: T.NetworkClusterPolicy, ds: dict) -> Result:
+        original = copy.deepcopy(ds)
+        if p.spec.configurationType != T.CONFIG_AMD_SCALE_OUT:
+            raise ValueError(f"unknown configuration type {p.spec.configurationType!r}")
+        update_amd_scale_out_daemonset(ds, p, self.namespace)
+        if original["spec"]["template"]["spec"] != ds["spec"]["template"]["spec"]:
+            log.info("DS difference for %s", p.name)
+            ds = await self.client.replace(kube.DAEMONSETS, ds)
+            await self._event(raw, "Normal", "DaemonSetUpdated", f"Updated DaemonSet {self.namespace}/{p.name}")
+        return await self._update_status(raw, p, ds)
+
+    async def _update_status(self, raw: dict, p: T.NetworkClusterPolicy, ds: dict) -> Result:
+        st = ds.get("status", {}) or {}
+        targets = int(st.get("desiredNumberScheduled", 0) or 0)
+        ready = int(st.get("numberReady", 0) or 0)
+        cur = p.status
+        updated = not p.has_status or not cur.state
+        if cur.targets != targets or cur.ready != ready:
+            updated = True
+        new_state = status_for(targets, ready)
+        if cur.state != new_state or cur.errors:
+            updated = True
+        if not updated:
+            return Result()
+        body = copy.deepcopy(raw)
+        body["status"] = {"targets": targets, "ready": ready, "state": new_state, "errors": []}
+        try:
+            await self.client.replace_status(kube.NETWORKCLUSTERPOLICIES, body)
+        except ApiError as e:
+            if is_conflict(e):
+                return Result(requeue=True)
+            if is_not_found(e):
+                return Result()
+            log.error("unable to update network conf status: %s", e)
+            raise
+        if cur.state != new_state and new_state == STATE_ALL_GOOD:
+            await self._event(raw, "Normal", "AllNodesReady", f"{ready}/{targets} nodes configured")
+        return Result()
+
+    # -- entry point -------------------------------------------------------------------------------
+    async def reconcile(self, name: str) -> Result:
+        raw = self._get_policy(name)
+        if raw is None:
+            return Result()  # deleted; ownerRef GC removes the DaemonSet
+        p = T.NetworkClusterPolicy.from_dict(raw)
+        owned = self._list_owned(name)
+        if not owned:
+            return await self._create_daemonset(raw, p)
+        return await self._update(raw, p, copy.deepcopy(owned[0]))

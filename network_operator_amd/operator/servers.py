@@ -1,0 +1,187 @@
+"""HTTP(S) endpoints of the manager: health probes, Prometheus metrics, admission webhooks.
+
+Reference wiring (reference cmd/operator/main.go:117-167,219-226):
+* probes ``/healthz`` and ``/readyz`` on ``--health-probe-bind-address`` (":8081");
+* metrics on ``--metrics-bind-address`` ("0" = disabled), HTTPS with authentication
+  (TokenReview) and authorization (SubjectAccessReview on nonResourceURL /metrics) when
+  ``--metrics-secure``;
+* webhook server on :9443 with the serving certificate from
+  ``/tmp/k8s-webhook-server/serving-certs/tls.{crt,key}``;
+* TLS 1.2 only with two ECDHE AES-256-GCM suites; HTTP/2 is not offered (the reference
+  disables it unless ``--enable-http2``; aiohttp only speaks HTTP/1.1).
+"""
+
+from __future__ import annotations
+
+import asyncio
+import json
+import logging
+import ssl
+import subprocess
+import time
+from pathlib import Path
+from typing import Callable, Dict, Optional, Tuple
+
+from aiohttp import web
+
+from ..api.v1alpha1 import webhook as W
+from . import kube
+from .kube import ApiClient
+from .metrics import OperatorMetrics
+
+log = logging.getLogger("servers")
+
+TLS_CIPHERS = "ECDHE-RSA-AES256-GCM-SHA384:ECDHE-ECDSA-AES256-GCM-SHA384"
+DEFAULT_CERT_DIR = "/tmp/k8s-webhook-server/serving-certs"
+
+
+def server_tls_context(cert_file: str, key_file: str) -> ssl.SSLContext:
+    ctx = ssl.SSLContext(ssl.PROTOCOL_TLS_SERVER)
+    ctx.minimum_version = ssl.TLSVersion.TLSv1_2
+    ctx.maximum_version = ssl.TLSVersion.TLSv1_2
+    ctx.set_ciphers(TLS_CIPHERS)
+    ctx.set_alpn_protocols(["http/1.1"])
+    ctx.load_cert_chain(cert_file, key_file)
+    return ctx
+
+
+def generate_self_signed(cert_dir: Path, cn: str = "localhost", sans=("DNS:localhost", "IP:127.0.0.1")) -> Tuple[Path, Path]:
+    """Self-signed serving certificate (tests / local runs; in clusters cert-manager issues it)."""
+    cert_dir.mkdir(parents=True, exist_ok=True)
+    crt, key = cert_dir / "tls.crt", cert_dir / "tls.key"
+    subprocess.run(["openssl", "req", "-x509", "-newkey", "rsa:2048", "-nodes", "-keyout", str(key), "-out", str(crt),
+                    "-days", "2", "-subj", f"/CN={cn}", "-addext", "subjectAltName=" + ",".join(sans)],
+                   check=True, capture_output=True)
+    return crt, key
+
+
+def parse_bind(addr: str) -> Optional[Tuple[str, int]]:
+    """":8081" -> ("0.0.0.0", 8081); "0" -> None (disabled)."""
+    if addr in ("", "0"):
+        return None
+    host, _, port = addr.rpartition(":")
+    return (host or "0.0.0.0", int(port))
+
+
+class TokenAuthorizer:
+    """controller-runtime's WithAuthenticationAndAuthorization filter for /metrics."""
+
+    def __init__(self, client: ApiClient, ttl: float = 30.0):
+        self.client = client
+        self.ttl = ttl
+        self._cache: Dict[str, Tuple[float, bool]] = {}
+
+    async def allowed(self, token: str, path: str) -> bool:
+        hit = self._cache.get(token)
+        if hit and hit[0] > time.monotonic():
+            return hit[1]
+        ok = False
+        try:
+            tr = await self.client.create(kube.TOKENREVIEWS, {"apiVersion": "authentication.k8s.io/v1",
+                                                             "kind": "TokenReview", "spec": {"token": token}})
+            st = tr.get("status", {})
+            if st.get("authenticated"):
+                user = st.get("user", {})
+                sar = await self.client.create(kube.SUBJECTACCESSREVIEWS, {
+                    "apiVersion": "authorization.k8s.io/v1", "kind": "SubjectAccessReview",
+                    "spec": {"user": user.get("username"), "groups": user.get("groups", []), "uid": user.get("uid"),
+                             "nonResourceAttributes": {"path": path, "verb": "get"}}})
+                ok = bool(sar.get("status", {}).get("allowed"))
+        except Exception as e:
+            log.warning("metrics authn/authz failed: %s", e)
+        self._cache[token] = (time.monotonic() + self.ttl, ok)
+        return ok
+
+
+class Servers:
+    def __init__(self, metrics: OperatorMetrics, ready_check: Callable[[], bool] = lambda: True,
+                 client: Optional[ApiClient] = None):
+        self.metrics = metrics
+        self.ready_check = ready_check
+        self.client = client
+        self.runners: list = []
+        self.ports: Dict[str, int] = {}
+
+    # -- apps ------------------------------------------------------------------------------------
+    def probes_app(self) -> web.Application:
+        app = web.Application()
+
+        async def healthz(_):
+            return web.Response(text="ok")
+
+        async def readyz(_):
+            return web.Response(text="ok") if self.ready_check() else web.Response(status=500, text="not ready")
+
+        app.router.add_get("/healthz", healthz)
+        app.router.add_get("/readyz", readyz)
+        return app
+
+    def metrics_app(self, secure: bool) -> web.Application:
+        app = web.Application()
+        authz = TokenAuthorizer(self.client) if secure and self.client else None
+
+        async def metrics(req: web.Request):
+            if authz is not None:
+                auth = req.headers.get("Authorization", "")
+                if not auth.startswith("Bearer "):
+                    return web.Response(status=401, text="Unauthorized")
+                if not await authz.allowed(auth[7:], req.path):
+                    return web.Response(status=403, text="Forbidden")
+            return web.Response(body=self.metrics.render(), headers={"Content-Type": self.metrics.content_type})
+
+        app.router.add_get("/metrics", metrics)
+        return app
+
+    @staticmethod
+    def webhook_app() -> web.Application:
+        app = web.Application()
+
+        def handler(mutate: bool):
+            async def h(req: web.Request):
+                try:
+                    review = await req.json()
+                except json.JSONDecodeError:
+                    return web.Response(status=400, text="bad AdmissionReview")
+                return web.json_response(W.admission_review(review, mutate))
+            return h
+
+        app.router.add_post(W.MUTATE_PATH, handler(True))
+        app.router.add_post(W.VALIDATE_PATH, handler(False))
+        return app
+
+    # -- lifecycle -------------------------------------------------------------------------------
+    async def _serve(self, name: str, app: web.Application, host: str, port: int,
+                     ssl_ctx: Optional[ssl.SSLContext] = None) -> int:
+        runner = web.AppRunner(app, access_log=None)
+        await runner.setup()
+        site = web.TCPSite(runner, host, port, ssl_context=ssl_ctx)
+        await site.start()
+        self.runners.append(runner)
+        sock = site._server.sockets[0]  # type: ignore[union-attr]
+        self.ports[name] = sock.getsockname()[1]
+        log.info("serving %s on %s:%d%s", name, host, self.ports[name], " (TLS)" if ssl_ctx else "")
+        return self.ports[name]
+
+    async def start(self, probe_addr: str = ":8081", metrics_addr: str = "0", metrics_secure: bool = False,
+                    webhook_port: Optional[int] = None, cert_dir: str = DEFAULT_CERT_DIR) -> None:
+        b = parse_bind(probe_addr)
+        if b:
+            await self._serve("probes", self.probes_app(), *b)
+        b = parse_bind(metrics_addr)
+        if b:
+            ctx = None
+            if metrics_secure:
+                cd = Path(cert_dir)
+                if not (cd / "tls.crt").exists():
+                    generate_self_signed(cd)  # controller-runtime also self-signs the metrics cert
+                ctx = server_tls_context(str(cd / "tls.crt"), str(cd / "tls.key"))
+            await self._serve("metrics", self.metrics_app(metrics_secure), *b, ssl_ctx=ctx)
+        if webhook_port is not None:
+            cd = Path(cert_dir)
+            ctx = server_tls_context(str(cd / "tls.crt"), str(cd / "tls.key"))
+            await self._serve("webhook", self.webhook_app(), "0.0.0.0", webhook_port, ssl_ctx=ctx)
+
+    async def stop(self) -> None:
+        for r in self.runners:
+            await r.cleanup()
+        self.runners.clear()

@@ -1,0 +1,695 @@
+"""In-process fake Kubernetes API server (aiohttp) for control-plane tests.
+
+The reference tests its controller against envtest — a real etcd + kube-apiserver without
+controllers (reference internal/controller/suite_test.go:61-102).  Neither is available
+here, so this server implements the API-server behaviour the operator depends on:
+
+* discovery (``/api``, ``/apis``, group/version resource lists; optional OpenShift groups);
+* CRUD on any registered resource, cluster-scoped and namespaced, ``generateName``;
+* ``metadata.resourceVersion`` optimistic concurrency (409 Conflict), ``uid``,
+  ``generation`` bumped on spec changes, no-op updates do not bump the version;
+* the ``status`` subresource (main writes keep status, status writes keep spec);
+* JSON merge patch and RFC 6902 JSON patch;
+* LIST with label / field selectors; WATCH with replay from a resourceVersion, BOOKMARK
+  events, ``410 Gone`` for compacted history, ``timeoutSeconds``;
+* CRD structural-schema validation of NetworkClusterPolicies (422 Invalid) and pruning;
+* admission: calls Mutating/ValidatingWebhookConfigurations registered in the store (by
+  ``clientConfig.url``) and applies the returned JSONPatch — including the *rules* match on
+  the resource plural, so a webhook registered for a wrong resource is never called;
+* background garbage collection of dependents through ``ownerReferences``;
+* a DaemonSet controller simulation: ``desiredNumberScheduled`` from Nodes matching the pod
+  template's nodeSelector, ``numberReady`` from per-node agent readiness set by the test;
+* TokenReview / SubjectAccessReview answers from a token table (metrics authn/authz);
+* fault injection: fail the next N matching requests, drop all watch streams, compact.
+"""
+
+from __future__ import annotations
+
+import asyncio
+import base64
+import copy
+import datetime as dt
+import json
+import re
+import ssl
+import tempfile
+import uuid
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Tuple
+
+import aiohttp
+from aiohttp import web
+
+from ..api.v1alpha1 import crd as CRD
+from ..api.v1alpha1 import types as T
+from ..operator import kube
+from ..operator.kube import Resource
+
+
+def _now() -> str:
+    return dt.datetime.now(dt.timezone.utc).strftime("%Y-%m-%dT%H:%M:%SZ")
+
+
+def _status(code: int, reason: str, message: str, details: Optional[dict] = None) -> web.Response:
+    body = {"kind": "Status", "apiVersion": "v1", "status": "Failure", "message": message, "reason": reason,
+            "code": code}
+    if details:
+        body["details"] = details
+    return web.json_response(body, status=code)
+
+
+def merge_patch(target, patch):
+    """RFC 7386."""
+    if not isinstance(patch, dict):
+        return copy.deepcopy(patch)
+    out = copy.deepcopy(target) if isinstance(target, dict) else {}
+    for k, v in patch.items():
+        if v is None:
+            out.pop(k, None)
+        else:
+            out[k] = merge_patch(out.get(k), v)
+    return out
+
+
+def _ptr(doc, path: str):
+    parts = [p.replace("~1", "/").replace("~0", "~") for p in path.lstrip("/").split("/")] if path not in ("", "/") else []
+    parent = None
+    cur = doc
+    for p in parts:
+        parent = cur
+        cur = cur[int(p)] if isinstance(cur, list) else cur.get(p) if isinstance(cur, dict) else None
+    return parent, (parts[-1] if parts else None), cur
+
+
+def json_patch_apply(doc, ops):
+    """RFC 6902 subset: add, replace, remove, test."""
+    doc = copy.deepcopy(doc)
+    for op in ops:
+        parent, key, cur = _ptr(doc, op["path"])
+        kind = op["op"]
+        if kind == "test":
+            if cur != op["value"]:
+                raise ValueError(f"test failed at {op['path']}")
+            continue
+        if parent is None:
+            if kind in ("add", "replace"):
+                doc = copy.deepcopy(op["value"])
+                continue
+            raise ValueError("cannot remove the root")
+        if isinstance(parent, list):
+            idx = len(parent) if key == "-" else int(key)
+            if kind == "add":
+                parent.insert(idx, copy.deepcopy(op["value"]))
+            elif kind == "replace":
+                parent[idx] = copy.deepcopy(op["value"])
+            elif kind == "remove":
+                parent.pop(idx)
+        else:
+            if kind in ("add", "replace"):
+                if kind == "replace" and key not in parent:
+                    raise ValueError(f"replace of missing path {op['path']}")
+                parent[key] = copy.deepcopy(op["value"])
+            elif kind == "remove":
+                if key not in parent:
+                    raise ValueError(f"remove of missing path {op['path']}")
+                del parent[key]
+    return doc
+
+
+def match_labels(labels: dict, selector: str) -> bool:
+    for term in [t.strip() for t in selector.split(",") if t.strip()]:
+        if "!=" in term:
+            k, v = term.split("!=", 1)
+            if labels.get(k) == v:
+                return False
+        elif "==" in term or "=" in term:
+            k, v = re.split("==?", term, maxsplit=1)
+            if labels.get(k) != v:
+                return False
+        elif term.startswith("!"):
+            if term[1:] in labels:
+                return False
+        elif term not in labels:
+            return False
+    return True
+
+
+def _match_fields(obj: dict, selector: str) -> bool:
+    md = obj.get("metadata", {})
+    for term in [t.strip() for t in selector.split(",") if t.strip()]:
+        neg = "!=" in term
+        k, v = re.split("!=|==|=", term, maxsplit=1)
+        actual = {"metadata.name": md.get("name"), "metadata.namespace": md.get("namespace")}.get(k)
+        if (actual == v) == neg:
+            return False
+    return True
+
+
+@dataclass
+class _Watch:
+    res: Resource
+    namespace: Optional[str]
+    label_selector: Optional[str]
+    queue: asyncio.Queue = field(default_factory=asyncio.Queue)
+
+
+@dataclass
+class _Fault:
+    method: str
+    pattern: re.Pattern
+    status: int
+    count: int
+    reason: str = "InternalError"
+
+
+class FakeApiServer:
+    STATUS_SUBRESOURCE = {kube.NETWORKCLUSTERPOLICIES, kube.DAEMONSETS}
+
+    def __init__(self, openshift: bool = False, history: int = 10000, bookmark_interval: float = 1.0,
+                 gc_delay: float = 0.0, agent_ready_delay: Optional[float] = None):
+        self.resources: List[Resource] = list(kube.ALL_RESOURCES)
+        self.openshift = openshift
+        self.objects: Dict[Tuple[str, str, str], Dict[Tuple[str, str], dict]] = {}
+        self.rv = 100
+        self.events: List[Tuple[int, Resource, str, dict]] = []
+        self.history = history
+        self.compacted_before = 0
+        self.watches: List[_Watch] = []
+        self.bookmark_interval = bookmark_interval
+        self.gc_delay = gc_delay
+        self.agent_ready_delay = agent_ready_delay
+        self.node_ready: Dict[Tuple[str, str], bool] = {}   # (ds ns/name, node) -> ready
+        self.tokens: Dict[str, dict] = {}                    # bearer -> {"username", "groups", "allowed"}
+        self.faults: List[_Fault] = []
+        self.requests: List[Tuple[str, str]] = []
+        self.admission_calls: List[Tuple[str, str]] = []
+        self._runner: Optional[web.AppRunner] = None
+        self.url = ""
+        self._bg: List[asyncio.Task] = []
+        self._closing = False
+
+    # ------------------------------------------------------------------------------------------
+    # lifecycle
+    # ------------------------------------------------------------------------------------------
+    async def start(self, host: str = "127.0.0.1", port: int = 0) -> str:
+        app = web.Application(client_max_size=8 << 20)
+        app.router.add_route("*", "/{tail:.*}", self._dispatch)
+        self._runner = web.AppRunner(app, access_log=None)
+        await self._runner.setup()
+        site = web.TCPSite(self._runner, host, port)
+        await site.start()
+        sock = site._server.sockets[0]  # type: ignore[union-attr]
+        self.url = f"http://{host}:{sock.getsockname()[1]}"
+        return self.url
+
+    async def stop(self) -> None:
+        self._closing = True
+        self.drop_watches()
+        for t in self._bg:
+            t.cancel()
+        if self._runner:
+            await self._runner.cleanup()
+
+    # ------------------------------------------------------------------------------------------
+    # test helpers
+    # ------------------------------------------------------------------------------------------
+    @staticmethod
+    def _rkey(res: Resource) -> Tuple[str, str, str]:
+        return (res.group, res.version, res.plural)
+
+    def _table(self, res: Resource) -> Dict[Tuple[str, str], dict]:
+        return self.objects.setdefault(self._rkey(res), {})
+
+    def get_object(self, res: Resource, name: str, namespace: Optional[str] = None) -> Optional[dict]:
+        o = self._table(res).get((namespace or "", name))
+        return copy.deepcopy(o) if o else None
+
+    def list_objects(self, res: Resource) -> List[dict]:
+        return [copy.deepcopy(o) for o in self._table(res).values()]
+
+    def add_node(self, name: str, labels: Optional[dict] = None) -> dict:
+        node = {"apiVersion": "v1", "kind": "Node", "metadata": {"name": name, "labels": dict(labels or {})}}
+        obj = self._create(kube.NODES, node, None)
+        self._sync_daemonsets()
+        return obj
+
+    def set_node_labels(self, name: str, labels: dict) -> None:
+        o = self._table(kube.NODES)[("", name)]
+        new = copy.deepcopy(o)
+        new["metadata"]["labels"] = dict(labels)
+        self._store(kube.NODES, new, "MODIFIED")
+        self._sync_daemonsets()
+
+    def set_agent_ready(self, node: str, ready: bool = True, daemonset: Optional[str] = None) -> None:
+        """Simulates the agent pod's readinessProbe on `node` (all DaemonSets if none given)."""
+        for (ns, name), _ in self._table(kube.DAEMONSETS).items():
+            if daemonset is None or daemonset in (name, f"{ns}/{name}"):
+                self.node_ready[(f"{ns}/{name}", node)] = ready
+        self._sync_daemonsets()
+
+    def fail_next(self, method: str, path_regex: str, status: int = 500, count: int = 1,
+                  reason: str = "InternalError") -> None:
+        self.faults.append(_Fault(method.upper(), re.compile(path_regex), status, count, reason))
+
+    def drop_watches(self) -> None:
+        for w in self.watches:
+            w.queue.put_nowait(None)
+        self.watches.clear()
+
+    def compact(self) -> None:
+        """Forget event history (etcd compaction + API-server restart): every watch resuming
+        from any resourceVersion issued so far gets 410 Gone and must relist."""
+        self.compacted_before = self.rv + 2
+        self.events.clear()
+        self.drop_watches()
+
+    # ------------------------------------------------------------------------------------------
+    # storage core
+    # ------------------------------------------------------------------------------------------
+    def _next_rv(self) -> str:
+        self.rv += 1
+        return str(self.rv)
+
+    def _emit(self, res: Resource, typ: str, obj: dict) -> None:
+        rv = int(obj["metadata"]["resourceVersion"]) if typ != "DELETED" else self.rv
+        self.events.append((rv, res, typ, copy.deepcopy(obj)))
+        if len(self.events) > self.history:
+            drop = len(self.events) - self.history
+            self.compacted_before = self.events[drop - 1][0] + 1
+            del self.events[:drop]
+        for w in list(self.watches):
+            if w.res == res and self._visible(w, obj):
+                w.queue.put_nowait((typ, copy.deepcopy(obj)))
+
+    @staticmethod
+    def _visible(w: _Watch, obj: dict) -> bool:
+        md = obj.get("metadata", {})
+        if w.namespace and md.get("namespace") != w.namespace:
+            return False
+        if w.label_selector and not match_labels(md.get("labels", {}) or {}, w.label_selector):
+            return False
+        return True
+
+    def _store(self, res: Resource, obj: dict, typ: str) -> dict:
+        obj["metadata"]["resourceVersion"] = self._next_rv()
+        self._table(res)[(obj["metadata"].get("namespace", "") if res.namespaced else "", obj["metadata"]["name"])] = obj
+        self._emit(res, typ, obj)
+        return obj
+
+    def _create(self, res: Resource, obj: dict, namespace: Optional[str]) -> dict:
+        obj = copy.deepcopy(obj)
+        md = obj.setdefault("metadata", {})
+        if not md.get("name"):
+            if md.get("generateName"):
+                md["name"] = md["generateName"] + uuid.uuid4().hex[:5]
+            else:
+                raise web.HTTPUnprocessableEntity(text="name or generateName is required")
+        if res.namespaced:
+            md["namespace"] = namespace or md.get("namespace") or "default"
+        else:
+            md.pop("namespace", None)
+        key = (md.get("namespace", "") if res.namespaced else "", md["name"])
+        if key in self._table(res):
+            raise _Conflict(409, "AlreadyExists", f'{res.plural}.{res.group or "core"} "{md["name"]}" already exists',
+                            {"name": md["name"], "kind": res.plural})
+        md["uid"] = str(uuid.uuid4())
+        md["creationTimestamp"] = _now()
+        md["generation"] = 1
+        obj.setdefault("apiVersion", res.api_version)
+        obj.setdefault("kind", res.kind)
+        if res in self.STATUS_SUBRESOURCE:
+            obj.pop("status", None)
+        if res == kube.DAEMONSETS:
+            obj["status"] = {"currentNumberScheduled": 0, "desiredNumberScheduled": 0, "numberMisscheduled": 0,
+                             "numberReady": 0, "observedGeneration": 1}
+        stored = self._store(res, obj, "ADDED")
+        if res in (kube.DAEMONSETS, kube.NODES):
+            self._sync_daemonsets()
+        return self._table(res)[key]
+
+    def _delete(self, res: Resource, name: str, namespace: str) -> dict:
+        key = (namespace if res.namespaced else "", name)
+        obj = self._table(res).pop(key)
+        obj = copy.deepcopy(obj)
+        self._next_rv()
+        obj["metadata"]["resourceVersion"] = str(self.rv)
+        self._emit(res, "DELETED", obj)
+        uid = obj["metadata"].get("uid")
+        if self.gc_delay <= 0:
+            self._collect(uid)
+        else:
+            self._bg.append(asyncio.ensure_future(self._collect_later(uid)))
+        if res == kube.DAEMONSETS:
+            self.node_ready = {k: v for k, v in self.node_ready.items() if k[0] != f"{namespace}/{name}"}
+        return obj
+
+    async def _collect_later(self, uid: str) -> None:
+        await asyncio.sleep(self.gc_delay)
+        self._collect(uid)
+
+    def _collect(self, uid: str) -> None:
+        """Background cascading deletion of dependents (garbage collector)."""
+        for res in self.resources:
+            for (ns, name), o in list(self._table(res).items()):
+                refs = o.get("metadata", {}).get("ownerReferences") or []
+                if any(r.get("uid") == uid for r in refs):
+                    self._delete(res, name, ns)
+
+    # ------------------------------------------------------------------------------------------
+    # DaemonSet controller simulation
+    # ------------------------------------------------------------------------------------------
+    def _sync_daemonsets(self) -> None:
+        nodes = list(self._table(kube.NODES).values())
+        for (ns, name), ds in list(self._table(kube.DAEMONSETS).items()):
+            sel = ds["spec"]["template"]["spec"].get("nodeSelector") or {}
+            matching = [n["metadata"]["name"] for n in nodes
+                        if all((n["metadata"].get("labels") or {}).get(k) == v for k, v in sel.items())]
+            ready = sum(1 for n in matching if self.node_ready.get((f"{ns}/{name}", n)))
+            st = {"currentNumberScheduled": len(matching), "desiredNumberScheduled": len(matching),
+                  "numberMisscheduled": 0, "numberReady": ready,
+                  "numberAvailable": ready, "observedGeneration": ds["metadata"].get("generation", 1)}
+            if ds.get("status") != st:
+                new = copy.deepcopy(ds)
+                new["status"] = st
+                self._store(kube.DAEMONSETS, new, "MODIFIED")
+            if self.agent_ready_delay is not None:
+                for n in matching:
+                    if (f"{ns}/{name}", n) not in self.node_ready:
+                        self.node_ready[(f"{ns}/{name}", n)] = False
+                        self._bg.append(asyncio.ensure_future(self._auto_ready(f"{ns}/{name}", n)))
+
+    async def _auto_ready(self, ds_key: str, node: str) -> None:
+        await asyncio.sleep(self.agent_ready_delay or 0)
+        if (ds_key, node) in self.node_ready:
+            self.node_ready[(ds_key, node)] = True
+            self._sync_daemonsets()
+
+    # ------------------------------------------------------------------------------------------
+    # HTTP routing
+    # ------------------------------------------------------------------------------------------
+    def _parse(self, path: str) -> Tuple[Optional[Resource], Optional[str], Optional[str], Optional[str]]:
+        parts = [p for p in path.split("/") if p]
+        if parts[:2] == ["api", "v1"]:
+            group, version, rest = "", "v1", parts[2:]
+        elif len(parts) >= 3 and parts[0] == "apis":
+            group, version, rest = parts[1], parts[2], parts[3:]
+        else:
+            return None, None, None, None
+        by_plural = {(r.group, r.version, r.plural): r for r in self.resources}
+        ns = None
+        if len(rest) >= 3 and rest[0] == "namespaces" and (group, version, rest[2]) in by_plural:
+            ns, rest = rest[1], rest[2:]
+        if not rest:
+            return None, None, None, None
+        res = by_plural.get((group, version, rest[0]))
+        name = rest[1] if len(rest) > 1 else None
+        sub = rest[2] if len(rest) > 2 else None
+        return res, ns, name, sub
+
+    async def _dispatch(self, req: web.Request) -> web.StreamResponse:
+        path = req.path
+        self.requests.append((req.method, path))
+        for f in list(self.faults):
+            if f.method in (req.method, "*") and f.pattern.search(path):
+                f.count -= 1
+                if f.count <= 0:
+                    self.faults.remove(f)
+                return _status(f.status, f.reason, "injected fault")
+        try:
+            if path == "/api":
+                return web.json_response({"kind": "APIVersions", "versions": ["v1"]})
+            if path == "/apis":
+                return web.json_response(self._group_list())
+            if path == "/version":
+                return web.json_response({"major": "1", "minor": "31", "gitVersion": "v1.31.0-fake"})
+            res, ns, name, sub = self._parse(path)
+            if res is None:
+                return self._discovery(path)
+            if res.namespaced and ns is None and req.method not in ("GET",):
+                ns = None
+            m = req.method
+            if m == "GET" and name is None:
+                if req.query.get("watch") in ("true", "1"):
+                    return await self._watch(req, res, ns)
+                return self._list(req, res, ns)
+            if m == "GET":
+                o = self._table(res).get((ns or "", name))
+                if o is None:
+                    return _status(404, "NotFound", f'{res.plural} "{name}" not found', {"name": name, "kind": res.plural})
+                return web.json_response(o)
+            if m == "POST":
+                return await self._post(req, res, ns)
+            if m == "PUT":
+                return await self._put(req, res, ns, name, sub)
+            if m == "PATCH":
+                return await self._patch(req, res, ns, name, sub)
+            if m == "DELETE":
+                if (ns or "", name) not in self._table(res):
+                    return _status(404, "NotFound", f'{res.plural} "{name}" not found')
+                return web.json_response(self._delete(res, name, ns or ""))
+            return _status(405, "MethodNotAllowed", m)
+        except _Conflict as c:
+            return _status(c.code, c.reason, c.message, c.details)
+        except web.HTTPException as e:
+            return _status(e.status, "Invalid" if e.status == 422 else "BadRequest", e.text or "")
+
+    def _group_list(self) -> dict:
+        groups: Dict[str, List[str]] = {}
+        for r in self.resources:
+            if r.group:
+                groups.setdefault(r.group, [])
+                if r.version not in groups[r.group]:
+                    groups[r.group].append(r.version)
+        if self.openshift:
+            groups.setdefault("route.openshift.io", ["v1"])
+            groups.setdefault("security.openshift.io", ["v1"])
+        return {"kind": "APIGroupList", "apiVersion": "v1", "groups": [
+            {"name": g, "versions": [{"groupVersion": f"{g}/{v}", "version": v} for v in vs],
+             "preferredVersion": {"groupVersion": f"{g}/{vs[0]}", "version": vs[0]}} for g, vs in sorted(groups.items())]}
+
+    def _discovery(self, path: str) -> web.Response:
+        parts = [p for p in path.split("/") if p]
+        if parts == ["api", "v1"]:
+            g, v = "", "v1"
+        elif len(parts) == 3 and parts[0] == "apis":
+            g, v = parts[1], parts[2]
+        else:
+            return _status(404, "NotFound", f"the server could not find the requested resource {path}")
+        rs = [r for r in self.resources if r.group == g and r.version == v]
+        if not rs:
+            return _status(404, "NotFound", path)
+        return web.json_response({"kind": "APIResourceList", "groupVersion": f"{g}/{v}" if g else v, "resources": [
+            {"name": r.plural, "namespaced": r.namespaced, "kind": r.kind,
+             "verbs": ["create", "delete", "get", "list", "patch", "update", "watch"]} for r in rs]})
+
+    # -- LIST / WATCH ---------------------------------------------------------------------------
+    def _list(self, req: web.Request, res: Resource, ns: Optional[str]) -> web.Response:
+        items = []
+        for (ons, _), o in sorted(self._table(res).items()):
+            if res.namespaced and ns and ons != ns:
+                continue
+            if req.query.get("labelSelector") and not match_labels(o["metadata"].get("labels") or {},
+                                                                    req.query["labelSelector"]):
+                continue
+            if req.query.get("fieldSelector") and not _match_fields(o, req.query["fieldSelector"]):
+                continue
+            items.append(o)
+        return web.json_response({"kind": res.kind + "List", "apiVersion": res.api_version,
+                                  "metadata": {"resourceVersion": str(self.rv)}, "items": items})
+
+    async def _watch(self, req: web.Request, res: Resource, ns: Optional[str]) -> web.StreamResponse:
+        since = int(req.query.get("resourceVersion") or 0)
+        timeout = float(req.query.get("timeoutSeconds") or 300)
+        bookmarks = req.query.get("allowWatchBookmarks") in ("true", "1")
+        resp = web.StreamResponse(headers={"Content-Type": "application/json"})
+        await resp.prepare(req)
+        if since and since < self.compacted_before - 1:
+            err = {"type": "ERROR", "object": {"kind": "Status", "apiVersion": "v1", "status": "Failure", "code": 410,
+                                                "reason": "Expired", "message": f"too old resource version: {since}"}}
+            await resp.write((json.dumps(err) + "\n").encode())
+            return resp
+        w = _Watch(res, ns, req.query.get("labelSelector"))
+        for rv, r, typ, obj in self.events:
+            if r == res and rv > since and self._visible(w, obj):
+                w.queue.put_nowait((typ, obj))
+        self.watches.append(w)
+        loop = asyncio.get_event_loop()
+        end = loop.time() + timeout
+        try:
+            while not self._closing:
+                remaining = end - loop.time()
+                if remaining <= 0:
+                    break
+                try:
+                    item = await asyncio.wait_for(w.queue.get(), timeout=min(remaining, self.bookmark_interval))
+                except asyncio.TimeoutError:
+                    if bookmarks:
+                        bm = {"type": "BOOKMARK", "object": {"kind": res.kind, "apiVersion": res.api_version,
+                                                             "metadata": {"resourceVersion": str(self.rv)}}}
+                        await resp.write((json.dumps(bm) + "\n").encode())
+                    continue
+                if item is None:
+                    break
+                typ, obj = item
+                await resp.write((json.dumps({"type": typ, "object": obj}) + "\n").encode())
+        except (ConnectionResetError, asyncio.CancelledError):
+            pass
+        finally:
+            if w in self.watches:
+                self.watches.remove(w)
+        return resp
+
+    # -- admission ------------------------------------------------------------------------------
+    async def _admit(self, res: Resource, op: str, obj: dict, old: Optional[dict]) -> dict:
+        for cfg_res, mutating in ((kube.MUTATINGWEBHOOKS, True), (kube.VALIDATINGWEBHOOKS, False)):
+            for cfg in list(self._table(cfg_res).values()):
+                for wh in cfg.get("webhooks", []) or []:
+                    if not any(self._rule_matches(rule, res, op) for rule in wh.get("rules", []) or []):
+                        continue
+                    url = (wh.get("clientConfig") or {}).get("url")
+                    if not url:
+                        continue  # service references cannot be resolved here
+                    self.admission_calls.append((wh.get("name", ""), op))
+                    review = {"apiVersion": "admission.k8s.io/v1", "kind": "AdmissionReview", "request": {
+                        "uid": str(uuid.uuid4()), "kind": {"group": res.group, "version": res.version, "kind": res.kind},
+                        "resource": {"group": res.group, "version": res.version, "resource": res.plural},
+                        "operation": op, "object": obj, "oldObject": old, "name": obj.get("metadata", {}).get("name")}}
+                    ctx: Optional[ssl.SSLContext] = None
+                    ca = (wh.get("clientConfig") or {}).get("caBundle")
+                    if url.startswith("https"):
+                        ctx = ssl.create_default_context()
+                        if ca:
+                            with tempfile.NamedTemporaryFile("wb", suffix=".pem", delete=False) as f:
+                                f.write(base64.b64decode(ca))
+                            ctx.load_verify_locations(f.name)
+                    try:
+                        async with aiohttp.ClientSession() as s:
+                            async with s.post(url, json=review, ssl=ctx if ctx else False,
+                                              timeout=aiohttp.ClientTimeout(total=10)) as r:
+                                out = await r.json()
+                    except Exception as e:
+                        if wh.get("failurePolicy", "Fail") == "Ignore":
+                            continue
+                        raise _Conflict(500, "InternalError", f'failed calling webhook "{wh.get("name")}": {e}')
+                    resp = out.get("response", {})
+                    if not resp.get("allowed", False):
+                        msg = (resp.get("status") or {}).get("message", "denied")
+                        raise _Conflict(403, "Forbidden",
+                                        f'admission webhook "{wh.get("name")}" denied the request: {msg}')
+                    if mutating and resp.get("patch"):
+                        obj = json_patch_apply(obj, json.loads(base64.b64decode(resp["patch"])))
+        return obj
+
+    @staticmethod
+    def _rule_matches(rule: dict, res: Resource, op: str) -> bool:
+        def ok(vals, v):
+            return "*" in (vals or []) or v in (vals or [])
+        return (ok(rule.get("apiGroups"), res.group) and ok(rule.get("apiVersions"), res.version)
+                and ok(rule.get("operations"), op) and ok(rule.get("resources"), res.plural))
+
+    def _validate_schema(self, res: Resource, obj: dict) -> dict:
+        if res != kube.NETWORKCLUSTERPOLICIES:
+            return obj
+        errs = CRD.validate(obj)
+        if errs:
+            raise _Conflict(422, "Invalid", f'{T.KIND} "{obj.get("metadata", {}).get("name")}" is invalid: '
+                            + "; ".join(errs), {"causes": [{"message": e} for e in errs]})
+        pruned = CRD.prune(obj, CRD.openapi_schema())
+        pruned["metadata"] = obj["metadata"]
+        return pruned
+
+    # -- writes ---------------------------------------------------------------------------------
+    async def _body(self, req: web.Request) -> dict:
+        try:
+            return await req.json()
+        except json.JSONDecodeError:
+            raise web.HTTPBadRequest(text="invalid JSON body")
+
+    async def _post(self, req: web.Request, res: Resource, ns: Optional[str]) -> web.Response:
+        obj = await self._body(req)
+        if res == kube.TOKENREVIEWS:
+            info = self.tokens.get(obj.get("spec", {}).get("token", ""))
+            obj["status"] = ({"authenticated": True, "user": {"username": info["username"], "groups": info.get("groups", [])}}
+                             if info else {"authenticated": False})
+            return web.json_response(obj, status=201)
+        if res == kube.SUBJECTACCESSREVIEWS:
+            user = obj.get("spec", {}).get("user")
+            allowed = any(i["username"] == user and i.get("allowed") for i in self.tokens.values())
+            obj["status"] = {"allowed": allowed}
+            return web.json_response(obj, status=201)
+        obj = self._validate_schema(res, obj)
+        obj = await self._admit(res, "CREATE", obj, None)
+        obj = self._validate_schema(res, obj)
+        created = self._create(res, obj, ns)
+        return web.json_response(created, status=201)
+
+    def _update(self, res: Resource, ns: Optional[str], name: str, sub: Optional[str], new: dict) -> dict:
+        key = (ns or "" if res.namespaced else "", name)
+        cur = self._table(res).get(key)
+        if cur is None:
+            raise _Conflict(404, "NotFound", f'{res.plural} "{name}" not found')
+        want_rv = new.get("metadata", {}).get("resourceVersion")
+        if want_rv and want_rv != cur["metadata"]["resourceVersion"]:
+            raise _Conflict(409, "Conflict", f'Operation cannot be fulfilled on {res.plural} "{name}": the object has '
+                                             "been modified; please apply your changes to the latest version and try again")
+        out = copy.deepcopy(cur)
+        if sub == "status":
+            out["status"] = copy.deepcopy(new.get("status"))
+        else:
+            for k, v in new.items():
+                if k in ("metadata", "status"):
+                    continue
+                out[k] = copy.deepcopy(v)
+            for k in list(out):
+                if k not in new and k not in ("metadata", "status", "apiVersion", "kind"):
+                    del out[k]
+            md_new = new.get("metadata", {})
+            for k in ("labels", "annotations", "ownerReferences", "finalizers"):
+                if k in md_new:
+                    out["metadata"][k] = copy.deepcopy(md_new[k])
+                else:
+                    out["metadata"].pop(k, None)
+            if res not in self.STATUS_SUBRESOURCE and "status" in new:
+                out["status"] = copy.deepcopy(new["status"])
+            if out.get("spec") != cur.get("spec"):
+                out["metadata"]["generation"] = cur["metadata"].get("generation", 1) + 1
+        if out == cur:
+            return cur  # no-op: resourceVersion unchanged, no event
+        stored = self._store(res, out, "MODIFIED")
+        if res in (kube.DAEMONSETS, kube.NODES) and sub != "status":
+            self._sync_daemonsets()
+        return self._table(res)[key]
+
+    async def _put(self, req: web.Request, res: Resource, ns: Optional[str], name: str, sub: Optional[str]) -> web.Response:
+        new = await self._body(req)
+        if sub is None:
+            new = self._validate_schema(res, new)
+            cur = self._table(res).get((ns or "" if res.namespaced else "", name))
+            if cur is not None and res == kube.NETWORKCLUSTERPOLICIES:
+                new = await self._admit(res, "UPDATE", new, cur)
+                new = self._validate_schema(res, new)
+        return web.json_response(self._update(res, ns, name, sub, new))
+
+    async def _patch(self, req: web.Request, res: Resource, ns: Optional[str], name: str, sub: Optional[str]) -> web.Response:
+        cur = self._table(res).get((ns or "" if res.namespaced else "", name))
+        if cur is None:
+            return _status(404, "NotFound", f'{res.plural} "{name}" not found')
+        patch = await self._body(req)
+        ct = req.headers.get("Content-Type", "")
+        try:
+            if "json-patch" in ct:
+                new = json_patch_apply(cur, patch)
+            else:
+                new = merge_patch(cur, patch)
+        except (ValueError, KeyError, IndexError) as e:
+            return _status(422, "Invalid", f"patch failed: {e}")
+        new.setdefault("metadata", {})["resourceVersion"] = cur["metadata"]["resourceVersion"]
+        if sub is None:
+            new = self._validate_schema(res, new)
+        return web.json_response(self._update(res, ns, name, sub, new))
+
+
+class _Conflict(Exception):
+    def __init__(self, code: int, reason: str, message: str, details: Optional[dict] = None):
+        super().__init__(message)
+        self.code, self.reason, self.message, self.details = code, reason, message, details

@@ -1,0 +1,333 @@
+"""Control-plane tests against the in-process fake API server.
+
+Mirrors the reference's envtest suite (reference internal/controller/networkconfiguration_controller_test.go)
+and adds what envtest could not show: DaemonSet status -> policy status with node targeting,
+ownerRef garbage collection, conflicts, watch recovery, leader election, metrics.
+"""
+
+import asyncio
+import contextlib
+import os
+
+import pytest
+
+from network_operator_amd.api.v1alpha1 import types as T
+from network_operator_amd.operator import kube
+from network_operator_amd.operator.controller import PolicyController
+from network_operator_amd.operator.kube import ApiClient, ApiError, KubeConfig
+from network_operator_amd.operator.leader import LeaderElector
+from network_operator_amd.operator.reconciler import agent_args
+from network_operator_amd.testing.fakeapi import FakeApiServer
+
+NS = "amd-network-operator"
+
+
+def run(coro, timeout=60):
+    return asyncio.run(asyncio.wait_for(coro, timeout))
+
+
+async def eventually(fn, timeout=5.0, interval=0.02):
+    end = asyncio.get_event_loop().time() + timeout
+    last = None
+    while True:
+        try:
+            r = fn()
+            if asyncio.iscoroutine(r):
+                r = await r
+            if r is not False:
+                return r
+        except (AssertionError, KeyError, TypeError, ApiError) as e:
+            last = e
+        if asyncio.get_event_loop().time() > end:
+            raise AssertionError(f"condition not met: {last!r}")
+        await asyncio.sleep(interval)
+
+
+async def value(fn, timeout=5.0):
+    """Waits until fn() returns something other than None / False and returns it."""
+    out = []
+
+    def check():
+        v = fn()
+        assert v not in (None, False)
+        out.append(v)
+    await eventually(check, timeout)
+    return out[-1]
+
+
+@contextlib.asynccontextmanager
+async def cluster(openshift=True, workers=2, **fake_kw):
+    fake = FakeApiServer(openshift=openshift, **fake_kw)
+    url = await fake.start()
+    client = ApiClient(KubeConfig(host=url))
+    ctl = PolicyController(client, NS, is_openshift=openshift, workers=workers)
+    await ctl.start()
+    try:
+        yield fake, client, ctl
+    finally:
+        await ctl.stop()
+        await client.close()
+        await fake.stop()
+
+
+def policy(name="policy", layer="L3", **so):
+    p = T.new_policy(name, layer=layer, node_selector={"foo": "bar"}, **so)
+    return p.to_dict()
+
+
+def test_reconcile_lifecycle_reference_parity():
+    async def body():
+        async with cluster(openshift=True) as (fake, client, ctl):
+            await client.create(kube.NETWORKCLUSTERPOLICIES, policy(image="amd/my-linkdiscovery:latest", mtu=8000))
+
+            def status_ok():
+                p = fake.get_object(kube.NETWORKCLUSTERPOLICIES, "policy")
+                assert p["spec"]["configurationType"] == "amd-so"
+                assert p["status"]["targets"] == 0 and p["status"]["state"] == "No targets"
+                assert p["status"]["errors"] == []
+            await eventually(status_ok)
+
+            def ds_ok():
+                ds = fake.get_object(kube.DAEMONSETS, "policy", NS)
+                pod = ds["spec"]["template"]["spec"]
+                assert pod["serviceAccountName"] == "policy-sa"
+                c = pod["containers"]
+                assert len(c) == 1 and c[0]["image"] == "amd/my-linkdiscovery:latest"
+                assert c[0]["args"] == ["--configure=true", "--keep-running", "--mode=L3", "--mtu=8000", "--wait=90s",
+                                        "--rccl-net=/host/etc/amd/scale-out/rccl-net.json",
+                                        "--rccl-env=/host/etc/amd/scale-out/rccl.env"]
+                assert [v["name"] for v in pod["volumes"]] == ["nfd-features", "rccl-artifacts"]
+                assert [m["name"] for m in c[0]["volumeMounts"]] == ["nfd-features", "rccl-artifacts"]
+                assert pod["nodeSelector"] == {"foo": "bar"}
+                ref = ds["metadata"]["ownerReferences"][0]
+                assert ref["kind"] == "NetworkClusterPolicy" and ref["controller"] is True
+                sa = fake.get_object(kube.SERVICEACCOUNTS, "policy-sa", NS)
+                rb = fake.get_object(kube.ROLEBINDINGS, "policy-sa-rb", NS)
+                assert sa and rb["subjects"] == [{"kind": "ServiceAccount", "name": "policy-sa", "namespace": NS}]
+                assert rb["roleRef"]["name"] == "system:openshift:scc:privileged"
+            await eventually(ds_ok)
+
+            # update to L2: 4 args (reference controller_test.go:138-151 has 4 with no mtu)
+            cur = await client.get(kube.NETWORKCLUSTERPOLICIES, "policy")
+            cur["spec"]["amdScaleOut"] = {"layer": "L2", "image": "amd/my-linkdiscovery:latest"}
+            await client.replace(kube.NETWORKCLUSTERPOLICIES, cur)
+
+            def l2_ok():
+                ds = fake.get_object(kube.DAEMONSETS, "policy", NS)
+                c = ds["spec"]["template"]["spec"]["containers"][0]
+                assert c["args"] == ["--configure=true", "--keep-running", "--mode=L2"]
+                # fix vs reference: the L3 artifact volume is removed again
+                assert [v["name"] for v in ds["spec"]["template"]["spec"]["volumes"]] == ["nfd-features"]
+            await eventually(l2_ok)
+
+            # L3 + disableNetworkManager + mtu 0: volumes in stable order (controller_test.go:153-180)
+            cur = await client.get(kube.NETWORKCLUSTERPOLICIES, "policy")
+            cur["spec"]["amdScaleOut"] = {"layer": "L3", "disableNetworkManager": True, "pullPolicy": "Always"}
+            cur["spec"]["logLevel"] = 4
+            await client.replace(kube.NETWORKCLUSTERPOLICIES, cur)
+
+            def l3nm_ok():
+                ds = fake.get_object(kube.DAEMONSETS, "policy", NS)
+                c = ds["spec"]["template"]["spec"]["containers"][0]
+                assert c["args"][:6] == ["--configure=true", "--keep-running", "--mode=L3", "--v=4",
+                                         "--disable-networkmanager", "--nm-keyfile-dir=/etc/NetworkManager/conf.d"]
+                assert c["args"][6] == "--wait=90s"
+                assert c["imagePullPolicy"] == "Always"  # fix: pullPolicy applied
+                assert [v["name"] for v in ds["spec"]["template"]["spec"]["volumes"]] == \
+                    ["nfd-features", "var-run-dbus", "networkmanager", "rccl-artifacts"]
+                assert all(v["hostPath"]["type"] == "DirectoryOrCreate"
+                           for v in ds["spec"]["template"]["spec"]["volumes"])
+            await eventually(l3nm_ok)
+
+            # delete: ownerRef GC removes DaemonSet, ServiceAccount, RoleBinding
+            await client.delete(kube.NETWORKCLUSTERPOLICIES, "policy")
+
+            def gone():
+                assert fake.get_object(kube.DAEMONSETS, "policy", NS) is None
+                assert fake.get_object(kube.SERVICEACCOUNTS, "policy-sa", NS) is None
+                assert fake.get_object(kube.ROLEBINDINGS, "policy-sa-rb", NS) is None
+            await eventually(gone)
+    run(body())
+
+
+def test_status_tracks_targets_and_agent_readiness():
+    async def body():
+        async with cluster(openshift=False) as (fake, client, ctl):
+            for i in range(4):
+                fake.add_node(f"gpu-node-{i}", {"foo": "bar"} if i < 3 else {"foo": "other"})
+            await client.create(kube.NETWORKCLUSTERPOLICIES, policy())
+
+            def working():
+                st = fake.get_object(kube.NETWORKCLUSTERPOLICIES, "policy")["status"]
+                assert st == {"targets": 3, "ready": 0, "state": "Working on it..", "errors": []}
+            await eventually(working)
+            assert "serviceAccountName" not in fake.get_object(kube.DAEMONSETS, "policy", NS)["spec"]["template"]["spec"]
+            for i in range(3):
+                fake.set_agent_ready(f"gpu-node-{i}")
+
+            def good():
+                st = fake.get_object(kube.NETWORKCLUSTERPOLICIES, "policy")["status"]
+                assert st["ready"] == 3 and st["state"] == "All good"
+            await eventually(good)
+            # a node loses its label file (agent not ready) -> back to working
+            fake.set_agent_ready("gpu-node-1", False)
+            await eventually(lambda: fake.get_object(kube.NETWORKCLUSTERPOLICIES, "policy")["status"]["ready"] == 2)
+            # a new matching node joins
+            fake.set_node_labels("gpu-node-3", {"foo": "bar"})
+            await eventually(lambda: fake.get_object(kube.NETWORKCLUSTERPOLICIES, "policy")["status"]["targets"] == 4)
+            events = [e for e in fake.list_objects(kube.EVENTS)]
+            assert any(e["reason"] == "DaemonSetCreated" for e in events)
+            assert any(e["reason"] == "AllNodesReady" for e in events)
+    run(body())
+
+
+def test_manual_daemonset_drift_is_reverted():
+    async def body():
+        async with cluster(openshift=False) as (fake, client, ctl):
+            await client.create(kube.NETWORKCLUSTERPOLICIES, policy(mtu=9000))
+            ds = await value(lambda: fake.get_object(kube.DAEMONSETS, "policy", NS))
+            ds["spec"]["template"]["spec"]["containers"][0]["args"] = ["--hacked"]
+            await client.replace(kube.DAEMONSETS, ds)
+            await eventually(lambda: fake.get_object(kube.DAEMONSETS, "policy", NS)["spec"]["template"]["spec"]
+                             ["containers"][0]["args"][0] == "--configure=true")
+    run(body())
+
+
+def test_status_conflict_is_retried_and_api_errors_back_off():
+    async def body():
+        async with cluster(openshift=False) as (fake, client, ctl):
+            fake.fail_next("PUT", r"/networkclusterpolicies/policy/status$", status=409, count=2, reason="Conflict")
+            fake.fail_next("POST", r"/daemonsets$", status=500, count=2)
+            await client.create(kube.NETWORKCLUSTERPOLICIES, policy())
+            await eventually(lambda: fake.get_object(kube.NETWORKCLUSTERPOLICIES, "policy").get("status", {})
+                             .get("state") == "No targets", timeout=10)
+            assert ctl.queue.retries_total >= 2
+    run(body())
+
+
+def test_watch_interruptions_and_compaction_recover():
+    async def body():
+        async with cluster(openshift=False) as (fake, client, ctl):
+            await client.create(kube.NETWORKCLUSTERPOLICIES, policy("a"))
+            await value(lambda: fake.get_object(kube.DAEMONSETS, "a", NS))
+            fake.drop_watches()
+            await client.create(kube.NETWORKCLUSTERPOLICIES, policy("b"))
+            await value(lambda: fake.get_object(kube.DAEMONSETS, "b", NS))
+            fake.compact()
+            await client.create(kube.NETWORKCLUSTERPOLICIES, policy("c"))
+            await value(lambda: fake.get_object(kube.DAEMONSETS, "c", NS))
+            assert ctl.policies.relists >= 2
+    run(body())
+
+
+def test_schema_validation_rejects_bad_specs():
+    async def body():
+        fake = FakeApiServer()
+        url = await fake.start()
+        async with ApiClient(KubeConfig(host=url)) as client:
+            bad = [
+                ({"amdScaleOut": {"layer": "L4"}}, "Unsupported value"),
+                ({"amdScaleOut": {"layer": "L3", "mtu": 100}}, "greater than or equal to 1500"),
+                ({"amdScaleOut": {"layer": "L3", "mtu": 9001}}, "less than or equal to 9000"),
+                ({"logLevel": 9}, "less than or equal to 8"),
+                ({"amdScaleOut": {"layer": "L3", "pullPolicy": "Sometimes"}}, "Unsupported value"),
+                ({"configurationType": "gaudi-so"}, "Unsupported value"),
+            ]
+            for i, (patch, msg) in enumerate(bad):
+                p = policy(f"p{i}")
+                for k, v in patch.items():
+                    p["spec"][k] = v
+                with pytest.raises(ApiError) as ei:
+                    await client.create(kube.NETWORKCLUSTERPOLICIES, p)
+                assert ei.value.status == 422 and msg in ei.value.message, ei.value.message
+            p = policy("missing")
+            del p["spec"]["configurationType"]
+            with pytest.raises(ApiError):
+                await client.create(kube.NETWORKCLUSTERPOLICIES, p)
+            # unknown fields are pruned, not stored
+            p = policy("pruned")
+            p["spec"]["bogus"] = 1
+            created = await client.create(kube.NETWORKCLUSTERPOLICIES, p)
+            assert "bogus" not in created["spec"]
+        await fake.stop()
+    run(body())
+
+
+def test_agent_args_mi355x_options():
+    p = T.new_policy("x", layer="L3", xgmiCheck=True, lldpAnnounce=False, interfaces=["ens1", "ens2"],
+                     nicDrivers=["mlx5_core"])
+    a = agent_args(p)
+    assert a[-4:] == ["--xgmi-expect=0", "--lldp-announce=false", "--interfaces=ens1,ens2", "--nic-drivers=mlx5_core"]
+
+
+def test_leader_election_single_active_and_failover():
+    async def body():
+        fake = FakeApiServer()
+        url = await fake.start()
+        c1, c2 = ApiClient(KubeConfig(host=url)), ApiClient(KubeConfig(host=url))
+        e1 = LeaderElector(c1, NS, identity="one", lease_duration=0.6, renew_deadline=0.4, retry_period=0.1)
+        e2 = LeaderElector(c2, NS, identity="two", lease_duration=0.6, renew_deadline=0.4, retry_period=0.1,
+                           release_on_cancel=False)
+        leading = []
+        stop1 = asyncio.Event()
+
+        async def work(name, stop):
+            leading.append(name)
+            await stop.wait()
+
+        t1 = asyncio.ensure_future(e1.run(lambda: work("one", stop1)))
+        await eventually(lambda: leading == ["one"])
+        stop2 = asyncio.Event()
+        t2 = asyncio.ensure_future(e2.run(lambda: work("two", stop2)))
+        await asyncio.sleep(1.0)
+        assert leading == ["one"]  # lease held and renewed
+        lease = fake.get_object(kube.LEASES, "9a8a7ba6.amd.com", NS)
+        assert lease["spec"]["holderIdentity"] == "one"
+        # leader 1 stops voluntarily -> releases -> 2 takes over quickly
+        stop1.set()
+        await t1
+        await eventually(lambda: leading == ["one", "two"], timeout=5)
+        lease = fake.get_object(kube.LEASES, "9a8a7ba6.amd.com", NS)
+        assert lease["spec"]["holderIdentity"] == "two" and lease["spec"]["leaseTransitions"] >= 1
+        stop2.set()
+        await t2
+        await c1.close()
+        await c2.close()
+        await fake.stop()
+    run(body())
+
+
+def test_fake_api_server_semantics():
+    async def body():
+        fake = FakeApiServer()
+        url = await fake.start()
+        async with ApiClient(KubeConfig(host=url)) as c:
+            sa = {"apiVersion": "v1", "kind": "ServiceAccount", "metadata": {"name": "x", "labels": {"a": "1"}}}
+            o = await c.create(kube.SERVICEACCOUNTS, sa, namespace="ns1")
+            with pytest.raises(ApiError) as ei:
+                await c.create(kube.SERVICEACCOUNTS, sa, namespace="ns1")
+            assert kube.is_already_exists(ei.value)
+            stale = dict(o)
+            o["metadata"]["labels"]["b"] = "2"
+            o2 = await c.replace(kube.SERVICEACCOUNTS, o)
+            assert int(o2["metadata"]["resourceVersion"]) > int(o["metadata"]["resourceVersion"])
+            stale["metadata"] = dict(stale["metadata"], labels={"z": "9"}, resourceVersion=o["metadata"]["resourceVersion"])
+            with pytest.raises(ApiError) as ei:
+                await c.replace(kube.SERVICEACCOUNTS, stale)
+            assert kube.is_conflict(ei.value)
+            assert len((await c.list(kube.SERVICEACCOUNTS, "ns1", label_selector="a=1,b=2"))["items"]) == 1
+            assert len((await c.list(kube.SERVICEACCOUNTS, "ns1", label_selector="a=2"))["items"]) == 0
+            p = await c.patch(kube.SERVICEACCOUNTS, "x", {"metadata": {"labels": {"a": None}}}, namespace="ns1")
+            assert p["metadata"]["labels"] == {"b": "2"}
+            p = await c.patch(kube.SERVICEACCOUNTS, "x", [{"op": "add", "path": "/metadata/labels/c", "value": "3"}],
+                              namespace="ns1", patch_type="json")
+            assert p["metadata"]["labels"] == {"b": "2", "c": "3"}
+            groups = await c.server_groups()
+            assert "amd.com" in groups and "route.openshift.io" not in groups
+            # watch replays from a resourceVersion
+            seen = []
+            async for typ, obj in c.watch(kube.SERVICEACCOUNTS, "ns1", resource_version="1", timeout_seconds=1):
+                seen.append(typ)
+            assert seen[:3] == ["ADDED", "MODIFIED", "MODIFIED"]
+        await fake.stop()
+    run(body())
