@@ -1,0 +1,127 @@
+"""The ``manager`` process end to end: flags, OpenShift detection, probes, metrics (plain and
+authenticated), leader election, reconcile through the fake API server."""
+
+import asyncio
+import os
+import ssl
+
+import aiohttp
+
+from network_operator_amd.api.v1alpha1 import types as T
+from network_operator_amd.operator import kube, manager
+from network_operator_amd.operator.kube import ApiClient, KubeConfig
+from network_operator_amd.testing.fakeapi import FakeApiServer
+
+
+def _free_port():
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+async def _until(fn, timeout=8.0):
+    end = asyncio.get_event_loop().time() + timeout
+    while asyncio.get_event_loop().time() < end:
+        try:
+            if fn():
+                return
+        except (KeyError, TypeError):
+            pass
+        await asyncio.sleep(0.02)
+    raise AssertionError("timeout")
+
+
+def test_manager_end_to_end(tmp_path, monkeypatch):
+    monkeypatch.setenv("OPERATOR_NAMESPACE", "netop-test")
+    monkeypatch.setenv("ENABLE_WEBHOOKS", "false")
+    probe, metrics = _free_port(), _free_port()
+
+    async def body():
+        fake = FakeApiServer(openshift=True)
+        url = await fake.start()
+        fake.add_node("n1", {"amd.feature.node.kubernetes.io/gpu-ready": "true"})
+        stop, started = asyncio.Event(), asyncio.Event()
+        task = asyncio.ensure_future(manager.run(
+            ["--master", url, "--leader-elect", f"--health-probe-bind-address=127.0.0.1:{probe}",
+             f"--metrics-bind-address=127.0.0.1:{metrics}"], stop=stop, started=started))
+        await asyncio.wait_for(started.wait(), 10)
+        async with ApiClient(KubeConfig(host=url)) as c:
+            await c.create(kube.NETWORKCLUSTERPOLICIES, T.new_policy("gpu-l3").to_dict())
+            await _until(lambda: fake.get_object(kube.DAEMONSETS, "gpu-l3", "netop-test") is not None)
+            # OpenShift detected from the API groups -> SA + RB
+            await _until(lambda: fake.get_object(kube.ROLEBINDINGS, "gpu-l3-sa-rb", "netop-test") is not None)
+            fake.set_agent_ready("n1")
+            await _until(lambda: fake.get_object(kube.NETWORKCLUSTERPOLICIES, "gpu-l3")["status"]["state"] == "All good")
+        async with aiohttp.ClientSession() as s:
+            async with s.get(f"http://127.0.0.1:{probe}/healthz") as r:
+                assert r.status == 200 and await r.text() == "ok"
+            async with s.get(f"http://127.0.0.1:{probe}/readyz") as r:
+                assert r.status == 200
+            async with s.get(f"http://127.0.0.1:{metrics}/metrics") as r:
+                text = await r.text()
+        assert 'controller_runtime_reconcile_total{controller="networkclusterpolicy",result="success"}' in text
+        assert 'amd_network_operator_policy_ready{policy="gpu-l3"} 1.0' in text
+        assert 'leader_election_master_status{name="9a8a7ba6.amd.com"} 1.0' in text
+        lease = fake.get_object(kube.LEASES, "9a8a7ba6.amd.com", "netop-test")
+        assert lease["spec"]["holderIdentity"]
+        stop.set()
+        assert await asyncio.wait_for(task, 10) == 0
+        # released on shutdown
+        lease = fake.get_object(kube.LEASES, "9a8a7ba6.amd.com", "netop-test")
+        assert lease["spec"]["holderIdentity"] == ""
+        await fake.stop()
+
+    asyncio.run(asyncio.wait_for(body(), 60))
+
+
+def test_secure_metrics_authn_authz(tmp_path, monkeypatch):
+    monkeypatch.setenv("ENABLE_WEBHOOKS", "false")
+    metrics = _free_port()
+
+    async def body():
+        fake = FakeApiServer()
+        fake.tokens = {"good": {"username": "system:serviceaccount:monitoring:prometheus", "allowed": True},
+                       "nope": {"username": "someone", "allowed": False}}
+        url = await fake.start()
+        stop, started = asyncio.Event(), asyncio.Event()
+        task = asyncio.ensure_future(manager.run(
+            ["--master", url, "--health-probe-bind-address=0", f"--metrics-bind-address=127.0.0.1:{metrics}",
+             "--metrics-secure", f"--webhook-cert-dir={tmp_path}/certs"], stop=stop, started=started))
+        await asyncio.wait_for(started.wait(), 10)
+        ctx = ssl.create_default_context()
+        ctx.check_hostname = False
+        ctx.verify_mode = ssl.CERT_NONE
+        async with aiohttp.ClientSession() as s:
+            u = f"https://127.0.0.1:{metrics}/metrics"
+            async with s.get(u, ssl=ctx) as r:
+                assert r.status == 401
+            async with s.get(u, ssl=ctx, headers={"Authorization": "Bearer nope"}) as r:
+                assert r.status == 403
+            async with s.get(u, ssl=ctx, headers={"Authorization": "Bearer good"}) as r:
+                assert r.status == 200 and "workqueue_adds_total" in await r.text()
+            # TLS 1.2 only
+            ctx13 = ssl.create_default_context()
+            ctx13.check_hostname = False
+            ctx13.verify_mode = ssl.CERT_NONE
+            ctx13.minimum_version = ssl.TLSVersion.TLSv1_3
+            try:
+                async with s.get(u, ssl=ctx13) as r:
+                    raise AssertionError("TLS 1.3 must be refused")
+            except aiohttp.ClientError:
+                pass
+        stop.set()
+        await asyncio.wait_for(task, 10)
+        await fake.stop()
+
+    asyncio.run(asyncio.wait_for(body(), 60))
+
+
+def test_openshift_detection_failure_exits_nonzero():
+    async def body():
+        return await manager.run(["--master", "http://127.0.0.1:1", "--health-probe-bind-address=0"])
+
+    assert asyncio.run(body()) == 1

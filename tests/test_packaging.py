@@ -1,0 +1,137 @@
+"""Deployment artefacts: Helm chart, kustomize tree, samples, NFD rule, Dockerfiles.
+
+Rendered with the offline renderers in ``network_operator_amd.testing.render`` (no helm /
+kustomize binaries in this environment)."""
+
+from pathlib import Path
+
+import pytest
+import yaml
+
+from network_operator_amd.api.v1alpha1 import crd as CRD
+from network_operator_amd.api.v1alpha1 import types as T
+from network_operator_amd.api.v1alpha1 import webhook as W
+from network_operator_amd.testing.render import RenderError, helm_template, kustomize_build, render_template
+
+ROOT = Path(__file__).resolve().parent.parent
+CHART = ROOT / "charts" / "network-operator"
+
+
+def _by_kind(docs, kind):
+    return [d for d in docs if d["kind"] == kind]
+
+
+def _rules_allow(roles, group, resource, verb):
+    for r in roles:
+        for rule in r.get("rules", []):
+            if group in rule.get("apiGroups", []) and resource in rule.get("resources", []) and verb in rule.get("verbs", []):
+                return True
+    return False
+
+
+def test_render_template_subset():
+    src = '{{- $v := list "a" "b" }}x: {{ .Values.k | default "d" | quote }}\n{{- if has .Values.m $v }}\nok: {{ .Values.n }}\n{{- else }}\nno\n{{- end }}'
+    assert render_template(src, {"k": "", "m": "a", "n": 3}) == 'x: "d"\nok: 3'
+    assert render_template(src, {"k": "z", "m": "q"}) == 'x: "z"\nno'
+
+
+def test_helm_defaults():
+    docs = helm_template(CHART, namespace="amd-net")
+    kinds = {d["kind"] for d in docs}
+    assert {"Deployment", "ClusterRole", "Role", "RoleBinding", "ClusterRoleBinding", "Service", "Certificate", "Issuer",
+            "ServiceAccount", "MutatingWebhookConfiguration", "ValidatingWebhookConfiguration",
+            "CustomResourceDefinition", "NodeFeatureRule"} <= kinds
+    assert not _by_kind(docs, "NetworkClusterPolicy")  # config.amd.enabled defaults to false
+    dep = _by_kind(docs, "Deployment")[0]
+    assert dep["metadata"]["namespace"] == "amd-net"
+    c = dep["spec"]["template"]["spec"]["containers"][0]
+    assert c["args"] == ["--metrics-secure", "--metrics-bind-address=:8443", "--leader-elect",
+                         "--health-probe-bind-address=:8081"]
+    assert c["image"] == "amd/amd-network-operator:0.1.0"
+    for wh in _by_kind(docs, "MutatingWebhookConfiguration") + _by_kind(docs, "ValidatingWebhookConfiguration"):
+        rule = wh["webhooks"][0]["rules"][0]
+        assert rule["resources"] == [T.PLURAL]  # fixed: the reference registers the singular
+        path = wh["webhooks"][0]["clientConfig"]["service"]["path"]
+        assert path in (W.MUTATE_PATH, W.VALIDATE_PATH)
+    roles = _by_kind(docs, "ClusterRole") + _by_kind(docs, "Role")
+    for res, verb in (("daemonsets", "create"), ("daemonsets", "update"), ("serviceaccounts", "create"),
+                      ("events", "create"), ("networkclusterpolicies", "watch")):
+        grp = {"daemonsets": "apps", "networkclusterpolicies": "amd.com"}.get(res, "")
+        assert _rules_allow(roles, grp, res, verb), (res, verb)
+    assert _rules_allow(roles, "amd.com", "networkclusterpolicies/status", "update")
+    assert _rules_allow(roles, "rbac.authorization.k8s.io", "rolebindings", "create")
+    assert _rules_allow(roles, "coordination.k8s.io", "leases", "update")
+    assert _rules_allow(roles, "authentication.k8s.io", "tokenreviews", "create")
+
+
+def test_helm_policy_rendering_and_validation():
+    docs = helm_template(CHART, {"config": {"amd": {"enabled": True, "mode": "L3", "mtu": 9000}}})
+    cr = _by_kind(docs, "NetworkClusterPolicy")[0]
+    assert CRD.validate(cr) == []
+    assert W.validate_create(T.NetworkClusterPolicy.from_dict(cr)) == []
+    assert cr["spec"]["amdScaleOut"]["image"] == "amd/amd-network-linkdiscovery:0.1.0"
+    assert cr["spec"]["nodeSelector"] == {"amd.feature.node.kubernetes.io/gpu-ready": "true"}
+    assert cr["spec"]["amdScaleOut"]["xgmiCheck"] is True
+    with pytest.raises(RenderError, match="Invalid layer mode"):
+        helm_template(CHART, {"config": {"amd": {"enabled": True, "mode": "L4"}}})
+    for mtu in (1499, 9001):
+        with pytest.raises(RenderError, match="MTU must be between 1500 and 9000"):
+            helm_template(CHART, {"config": {"amd": {"enabled": True, "mtu": mtu}}})
+
+
+def test_kustomize_default_build():
+    docs = kustomize_build(ROOT / "config/operator/default")
+    dep = _by_kind(docs, "Deployment")[0]
+    assert dep["metadata"]["name"] == "amd-network-controller-manager"
+    assert dep["metadata"]["namespace"] == "amd-network-operator"
+    pod = dep["spec"]["template"]["spec"]
+    c = pod["containers"][0]
+    assert c["image"] == "amd/amd-network-operator:0.1.0"
+    assert "--metrics-bind-address=:8443" in c["args"] and "--leader-elect" in c["args"]
+    assert {"containerPort": 9443, "name": "webhook-server", "protocol": "TCP"} in c["ports"]
+    assert pod["volumes"][0]["secret"]["secretName"] == "webhook-server-cert"
+    assert pod["serviceAccountName"] == "amd-network-controller-manager"
+    ns = _by_kind(docs, "Namespace")[0]
+    assert ns["metadata"]["name"] == "amd-network-operator"
+    for crb in _by_kind(docs, "ClusterRoleBinding") + _by_kind(docs, "RoleBinding"):
+        for s in crb["subjects"]:
+            assert s["namespace"] == "amd-network-operator"
+        if crb["roleRef"]["kind"] != "ClusterRole" or not crb["roleRef"]["name"].startswith("system:"):
+            assert crb["roleRef"]["name"].startswith("amd-network-")
+    for wh in _by_kind(docs, "MutatingWebhookConfiguration"):
+        svc = wh["webhooks"][0]["clientConfig"]["service"]
+        assert svc == {"name": "amd-network-webhook-service", "namespace": "amd-network-operator",
+                       "path": W.MUTATE_PATH}
+        assert wh["webhooks"][0]["rules"][0]["resources"] == [T.PLURAL]
+        assert wh["metadata"]["annotations"]["cert-manager.io/inject-ca-from"].endswith("amd-network-serving-cert")
+    crd = _by_kind(docs, "CustomResourceDefinition")[0]
+    assert crd == yaml.safe_load(CRD.render_yaml())
+    names = {d["metadata"]["name"] for d in docs}
+    assert "amd-network-controller-manager-metrics-service" in names
+
+
+def test_kustomize_manifests_and_samples_validate():
+    docs = kustomize_build(ROOT / "config/operator/manifests")
+    crs = _by_kind(docs, "NetworkClusterPolicy")
+    assert {c["spec"]["amdScaleOut"]["layer"] for c in crs} == {"L2", "L3"}
+    for c in crs:
+        assert CRD.validate(c) == []
+        assert W.validate_create(T.NetworkClusterPolicy.from_dict(c)) == []
+
+
+def test_nfd_rules_consistent():
+    kz = yaml.safe_load((ROOT / "config/nfd/amd-gpu-device-rule.yaml").read_text())
+    helm = [d for d in helm_template(CHART) if d["kind"] == "NodeFeatureRule"][0]
+    assert kz["spec"] == helm["spec"]
+    devs = kz["spec"]["rules"][0]["matchFeatures"][0]["matchExpressions"]["device"]["value"]
+    assert "75a3" in devs  # MI355X, verified on hardware (tests/fixtures/mi355x_node_topology.json)
+    ready = kz["spec"]["rules"][1]
+    assert ready["labels"] == {"amd.feature.node.kubernetes.io/gpu-ready": "true"}
+
+
+def test_dockerfiles_build_the_native_agent():
+    op = (ROOT / "build/Dockerfile.operator").read_text()
+    agent = (ROOT / "build/Dockerfile.linkdiscovery").read_text()
+    assert "network_operator_amd.operator" in op and "USER 65532" in op
+    assert "discover" in agent and "cmake" in agent
+    assert "setcap" not in agent  # capabilities come from the DaemonSet, not file caps in the image
