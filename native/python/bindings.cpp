@@ -10,6 +10,7 @@
 #include "netop/l3.hpp"
 #include "netop/lldp.hpp"
 #include "netop/netlink.hpp"
+#include "netop/nm.hpp"
 #include "netop/packet.hpp"
 #include "netop/topology.hpp"
 
@@ -219,6 +220,27 @@ PYBIND11_MODULE(_netop_native, m) {
         d["missing"] = miss;
         return d;
     });
+    // ---- NetworkManager over the D-Bus wire client ------------------------------------
+    // The GIL is released: the peer may be a Python thread in this process (tests).
+    m.def("nm_disable_interfaces", [](const std::string& address, const std::vector<std::string>& ifaces) {
+        py::gil_scoped_release nogil;
+        auto nm = nm::connect_system_bus(address);
+        return nm::disable_for_interfaces(*nm, ifaces);
+    }, py::arg("address"), py::arg("interfaces"));
+    m.def("dbus_call_get_property", [](const std::string& address, const std::string& dest, const std::string& path,
+                                       const std::string& iface, const std::string& prop) {
+        dbus::Value v;
+        {
+            py::gil_scoped_release nogil;
+            dbus::Connection c(address);
+            v = c.get_property(dest, path, iface, prop);
+        }
+        if (v.sig == "s" || v.sig == "o") return py::object(py::str(v.as_string()));
+        if (v.sig == "b") return py::object(py::bool_(v.as_bool()));
+        if (v.sig == "u") return py::object(py::int_(v.as_u32()));
+        return py::object(py::str("<" + v.sig + ">"));
+    });
+
     m.def("find_rocev2_gid_index", [](const std::string& root, const std::string& dev, int port, const std::string& ip) -> py::object {
         auto a = Ipv4::parse(ip);
         if (!a) throw py::value_error("bad IPv4");
