@@ -81,6 +81,14 @@ def main(argv=None) -> int:
     buf = torch.zeros(numel, dtype=torch.bfloat16, device=device)
     for _ in range(args.warmup):
         dist.all_reduce(buf)
+    smi_before, smi_note = None, None
+    if rank == 0:  # xGMI counters (amd-smi), outside the timed region
+        try:
+            from network_operator_amd.ops import smi
+
+            smi_before = smi.snapshot()
+        except Exception as e:
+            smi_note = f"amd-smi counters unavailable: {e}"
     dist.barrier()
     torch.cuda.synchronize(device)
     t0 = time.perf_counter()
@@ -89,6 +97,12 @@ def main(argv=None) -> int:
     torch.cuda.synchronize(device)
     dt = time.perf_counter() - t0
     dist.barrier()
+    xgmi_traffic = None
+    if rank == 0 and smi_before is not None:
+        try:
+            xgmi_traffic = smi.traffic(smi_before, smi.snapshot())
+        except Exception as e:
+            smi_note = f"amd-smi counters unavailable: {e}"
     t = torch.tensor([dt], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dt = float(t.item())
@@ -148,8 +162,13 @@ def main(argv=None) -> int:
             "verify_errors": errors,
             "sweep": sweep,
             "node_ready": node_ready,
+            "xgmi_traffic": ({"links_up": xgmi_traffic["links_up"],
+                              "links_with_traffic": xgmi_traffic["links_with_traffic"],
+                              "GB_per_gpu": [round(sum(g["bytes_per_link"]) / 1e9, 3) for g in xgmi_traffic["gpus"]]}
+                             if xgmi_traffic else None),
             "notes": ("n=1: busbw is 0 by definition (rccl-tests factor 2(n-1)/n); reference publishes no numbers "
-                      "(BASELINE.md) so vs_baseline is null") + (f"; {node_ready_note}" if node_ready_note else ""),
+                      "(BASELINE.md) so vs_baseline is null") + (f"; {node_ready_note}" if node_ready_note else "")
+                     + (f"; {smi_note}" if smi_note else ""),
             "rccl_version": ".".join(str(x) for x in torch.cuda.nccl.version()) if hasattr(torch.cuda, "nccl") else None,
         }
         print(json.dumps(line), flush=True)

@@ -496,6 +496,10 @@ void Agent::run(int stop_fd) {
     get_network_configs(names);
     if (nics_.size() < names.size()) throw AgentError("Not all interfaces were found in the system");
     mark("discover");
+    // The xGMI mesh does not depend on LLDP: verify it up front, so a broken mesh fails in
+    // milliseconds instead of after the LLDP wait, and nothing is left for the critical path.
+    check_xgmi();
+    mark("xgmi");
 
     if (cfg_.disable_nm) {
         if (!cfg_.nm_keyfile_dir.empty()) {
@@ -557,7 +561,6 @@ void Agent::run(int stop_fd) {
         mark("artifacts");
     }
 
-    check_xgmi();
     log_results();
 
     if (!cfg_.configure) {

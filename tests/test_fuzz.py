@@ -1,0 +1,96 @@
+"""Fuzzing the control plane (the reference fuzzes CR fields against a live cluster and
+watches the operator log for crashes: reference test/fuzz/fuzz_test.go, README.md:3-8).
+
+Here the oracle is stronger: random create / update / delete sequences with random (valid
+and invalid) specs go through the fake API server (schema validation included) while the
+real controller runs; afterwards every surviving policy has exactly one DaemonSet whose agent
+arguments equal ``agent_args(policy)``, no DaemonSet outlives its policy, and every worker
+is still alive.
+"""
+
+import asyncio
+
+from hypothesis import HealthCheck, given, settings
+from hypothesis import strategies as st
+
+from network_operator_amd.api.v1alpha1 import types as T
+from network_operator_amd.operator import kube
+from network_operator_amd.operator.controller import PolicyController
+from network_operator_amd.operator.kube import ApiClient, ApiError, KubeConfig
+from network_operator_amd.operator.reconciler import agent_args
+from network_operator_amd.testing.fakeapi import FakeApiServer
+
+NS = "fuzz"
+
+so_strategy = st.fixed_dictionaries({}, optional={
+    "layer": st.sampled_from(["L2", "L3", "L3BGP", ""]),
+    "mtu": st.one_of(st.integers(1000, 10000), st.just(0)),
+    "image": st.sampled_from(["", "amd/x:1", "registry.local/agent@sha256:abc"]),
+    "pullPolicy": st.sampled_from(["", "Always", "Never", "IfNotPresent", "Sometimes"]),
+    "disableNetworkManager": st.booleans(),
+    "xgmiCheck": st.booleans(),
+    "lldpAnnounce": st.booleans(),
+})
+spec_strategy = st.fixed_dictionaries({
+    "configurationType": st.sampled_from(["amd-so", "amd-so", "amd-so", "host-nic"]),
+    "amdScaleOut": so_strategy,
+    "nodeSelector": st.dictionaries(st.sampled_from(["a", "b/c", "amd.feature.node.kubernetes.io/gpu-ready"]),
+                                    st.sampled_from(["true", "x"]), min_size=0, max_size=2),
+}, optional={"logLevel": st.integers(-1, 9)})
+op_strategy = st.tuples(st.sampled_from(["create", "update", "delete"]), st.sampled_from(["p0", "p1", "p2"]), spec_strategy)
+
+
+@settings(max_examples=12, deadline=None, suppress_health_check=[HealthCheck.too_slow])
+@given(ops=st.lists(op_strategy, min_size=1, max_size=12))
+def test_random_policy_churn_converges(ops):
+    async def body():
+        fake = FakeApiServer()
+        url = await fake.start()
+        client = ApiClient(KubeConfig(host=url))
+        ctl = PolicyController(client, NS, workers=3, record_events=False)
+        await ctl.start()
+        try:
+            for op, name, spec in ops:
+                try:
+                    if op == "create":
+                        await client.create(kube.NETWORKCLUSTERPOLICIES, {"apiVersion": T.API_VERSION, "kind": T.KIND,
+                                                                           "metadata": {"name": name}, "spec": spec})
+                    elif op == "update":
+                        cur = await client.get(kube.NETWORKCLUSTERPOLICIES, name)
+                        cur["spec"] = spec
+                        await client.replace(kube.NETWORKCLUSTERPOLICIES, cur)
+                    else:
+                        await client.delete(kube.NETWORKCLUSTERPOLICIES, name)
+                except ApiError as e:
+                    assert e.status in (404, 409, 422), e
+                await asyncio.sleep(0.005)  # 5 ms apart, like the reference fuzzer
+
+            async def converged():
+                pols = {p["metadata"]["name"]: p for p in fake.list_objects(kube.NETWORKCLUSTERPOLICIES)}
+                dss = {d["metadata"]["name"]: d for d in fake.list_objects(kube.DAEMONSETS)}
+                assert set(dss) <= set(pols), "orphan DaemonSet"
+                for name, p in pols.items():
+                    pol = T.NetworkClusterPolicy.from_dict(p)
+                    if pol.spec.configurationType != T.CONFIG_AMD_SCALE_OUT:
+                        continue  # unknown types never get a DaemonSet (they error and back off)
+                    assert name in dss, f"no DaemonSet for {name}"
+                    assert dss[name]["spec"]["template"]["spec"]["containers"][0]["args"] == agent_args(pol)
+                    assert p.get("status", {}).get("state") == "No targets"
+                return True
+
+            end = asyncio.get_event_loop().time() + 10
+            while True:
+                try:
+                    await converged()
+                    break
+                except AssertionError:
+                    if asyncio.get_event_loop().time() > end:
+                        raise
+                    await asyncio.sleep(0.05)
+            assert all(not t.done() for t in ctl._tasks), "a controller task died"
+        finally:
+            await ctl.stop()
+            await client.close()
+            await fake.stop()
+
+    asyncio.run(asyncio.wait_for(body(), 60))

@@ -93,3 +93,17 @@ def test_rccl_all_reduce_verified(cuda_device, single_rank_pg):
     res = C.run_sweep("all_reduce", [1 << 20], iters=5, warmup=2, device=cuda_device)
     assert res[0].busbw_GBps == 0.0  # n = 1
     assert res[0].time_s > 0
+
+
+def test_amd_smi_xgmi_links_visible(cuda_device):
+    """The MI355X in an 8-GPU hive reports 7 xGMI links up (one slot is the disabled self-link)."""
+    from network_operator_amd.ops import smi
+
+    snap = smi.snapshot()
+    assert snap["gpus"], snap
+    g = snap["gpus"][0]
+    assert len(g["xgmi_read_kb"]) == 8
+    if "link_status" in g:
+        assert g["link_status"].count("U") in (0, 7), g["link_status"]
+    t = smi.traffic(snap, smi.snapshot())
+    assert t["gpus"] and t["links_with_traffic"] == 0  # idle: nothing moved

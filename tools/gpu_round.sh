@@ -13,6 +13,7 @@ timeout -k 10 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/b
 tail -1 gpurun_out/bench.log
 timeout -k 10 300 "$(dirname "$0")/../network_operator_amd/_lib/netop-xgmi-probe" --bytes=268435456 --iters=10 > gpurun_out/xgmi_probe.json 2>&1 || { cat gpurun_out/xgmi_probe.json; exit 1; }
 cat gpurun_out/xgmi_probe.json
+timeout -k 10 120 network_operator_amd/_lib/netop-xgmi-counters > gpurun_out/xgmi_counters.json 2>&1 && head -c 1500 gpurun_out/xgmi_counters.json && echo
 cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/prof -o bench --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --gpus 1 --steps 10 --warmup 3 > $GRAFT_REPO_ROOT/gpurun_out/prof.log 2>&1 || { tail -20 $GRAFT_REPO_ROOT/gpurun_out/prof.log; exit 1; }
 echo PROF OK
 find $GRAFT_REPO_ROOT/gpurun_out/prof -name '*stats*' | head
