@@ -51,6 +51,10 @@ def main(argv=None) -> int:
     ap.add_argument("--sweep", default="4096,1048576,67108864", help="extra sizes (bytes) reported alongside")
     ap.add_argument("--node-ready", choices=["auto", "on", "off"], default="auto")
     ap.add_argument("--node-ready-runs", type=int, default=5)
+    ap.add_argument("--collectives", default="all_gather,reduce_scatter,all_to_all",
+                    help="other collectives reported at --bytes (n > 1 only)")
+    # CPU rehearsal of the multi-rank path (tests): gloo backend, fp32 on the host.
+    ap.add_argument("--device", choices=["cuda", "cpu"], default="cuda", help=argparse.SUPPRESS)
     args = ap.parse_args(argv)
 
     import torch
@@ -66,23 +70,28 @@ def main(argv=None) -> int:
         print(f"warning: --gpus={args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", str(_free_port()))
-    if not torch.cuda.is_available():
-        print("bench.py needs an MI355X GPU (torch.cuda.is_available() is False)", file=sys.stderr)
-        return 2
-    torch.cuda.set_device(local_rank)
-    device = torch.device("cuda", local_rank)
-    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=device)
+    if args.device == "cpu":
+        device, dtype = torch.device("cpu"), torch.float32
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    else:
+        if not torch.cuda.is_available():
+            print("bench.py needs an MI355X GPU (torch.cuda.is_available() is False)", file=sys.stderr)
+            return 2
+        torch.cuda.set_device(local_rank)
+        device, dtype = torch.device("cuda", local_rank), torch.bfloat16
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=device)
+    esize = torch.tensor([], dtype=dtype).element_size()
 
-    # 1. Correctness of the collective path (exact, HIP pattern kernels).
+    # 1. Correctness of the collective path (exact, HIP pattern kernels on the GPU).
     verified, errors = C.verify_all_reduce(min(args.bytes // 2, 64 << 20), device)
 
     # 2. Headline: K timed all-reduce steps of --bytes per rank.
-    numel = (args.bytes // 2) // 8 * 8
-    buf = torch.zeros(numel, dtype=torch.bfloat16, device=device)
+    numel = (args.bytes // esize) // 8 * 8
+    buf = torch.zeros(numel, dtype=dtype, device=device)
     for _ in range(args.warmup):
         dist.all_reduce(buf)
     smi_before, smi_note = None, None
-    if rank == 0:  # xGMI counters (amd-smi), outside the timed region
+    if rank == 0 and args.device == "cuda":  # xGMI counters (amd-smi), outside the timed region
         try:
             from network_operator_amd.ops import smi
 
@@ -90,11 +99,11 @@ def main(argv=None) -> int:
         except Exception as e:
             smi_note = f"amd-smi counters unavailable: {e}"
     dist.barrier()
-    torch.cuda.synchronize(device)
+    C.sync(device)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         dist.all_reduce(buf)
-    torch.cuda.synchronize(device)
+    C.sync(device)
     dt = time.perf_counter() - t0
     dist.barrier()
     xgmi_traffic = None
@@ -107,7 +116,7 @@ def main(argv=None) -> int:
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dt = float(t.item())
     per_step = dt / max(args.steps, 1)
-    nbytes = numel * 2
+    nbytes = numel * esize
     algbw, busbw = C.bandwidths("all_reduce", nbytes, world, per_step)
     del buf
 
@@ -115,9 +124,18 @@ def main(argv=None) -> int:
     sweep = []
     sizes = [int(s) for s in args.sweep.split(",") if s.strip()]
     if sizes:
-        for r in C.run_sweep("all_reduce", sizes, iters=max(args.steps, 10), warmup=max(args.warmup, 3), device=device):
+        for r in C.run_sweep("all_reduce", sizes, iters=max(args.steps, 10), warmup=max(args.warmup, 3), device=device,
+                             dtype=dtype):
             sweep.append({"bytes": r.bytes, "time_us": r.time_s * 1e6, "algbw_GBps": r.algbw_GBps,
                           "busbw_GBps": r.busbw_GBps})
+
+    # 4. The other collectives RCCL runs over the same links (rccl-tests definitions), n > 1.
+    others = []
+    if world > 1:
+        for op in [o.strip() for o in args.collectives.split(",") if o.strip()]:
+            r = C.run_sweep(op, [nbytes], iters=max(args.steps // 2, 5), warmup=2, device=device, dtype=dtype)[0]
+            others.append({"op": op, "bytes": r.bytes, "time_us": r.time_s * 1e6, "algbw_GBps": r.algbw_GBps,
+                           "busbw_GBps": r.busbw_GBps})
 
     node_ready = None
     node_ready_note = None
@@ -127,7 +145,7 @@ def main(argv=None) -> int:
 
             ok, why = netns.available()
             if ok:
-                node_ready = netns.node_ready_bench(n_nics=max(world, 1), runs=args.node_ready_runs)
+                node_ready = netns.node_ready_bench(n_nics=max(world, 1), runs=args.node_ready_runs, legacy=False)
             else:
                 node_ready_note = why
                 if args.node_ready == "on":
@@ -149,11 +167,13 @@ def main(argv=None) -> int:
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "bf16",
+            "dtype": "bf16" if args.device == "cuda" else "fp32",
             "data": "synthetic (zeros for the timed loop; exact pattern check before timing)",
             "config": {"model": CONFIG_NAME, "global_batch": None, "seq_len": None,
                        "parallelism": f"dp{world}", "message_bytes_per_rank": nbytes, "op": "all_reduce(sum)",
-                       "backend": "torch.distributed nccl (RCCL)"},
+                       "backend": ("torch.distributed nccl (RCCL)" if args.device == "cuda"
+                                   else "torch.distributed gloo (CPU rehearsal)")},
+            "collectives": others,
             "algbw_GBps": algbw,
             "busbw_GBps": busbw,
             "busbw_ceiling_GBps": ceiling,
@@ -169,7 +189,8 @@ def main(argv=None) -> int:
             "notes": ("n=1: busbw is 0 by definition (rccl-tests factor 2(n-1)/n); reference publishes no numbers "
                       "(BASELINE.md) so vs_baseline is null") + (f"; {node_ready_note}" if node_ready_note else "")
                      + (f"; {smi_note}" if smi_note else ""),
-            "rccl_version": ".".join(str(x) for x in torch.cuda.nccl.version()) if hasattr(torch.cuda, "nccl") else None,
+            "rccl_version": (".".join(str(x) for x in torch.cuda.nccl.version())
+                             if args.device == "cuda" and hasattr(torch.cuda, "nccl") else None),
         }
         print(json.dumps(line), flush=True)
     dist.destroy_process_group()

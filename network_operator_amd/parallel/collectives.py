@@ -105,32 +105,66 @@ def time_collective(op: str, tensor, iters: int, warmup: int, group=None, out=No
         once()
     if dist.is_initialized():
         dist.barrier(group=group)
-    torch.cuda.synchronize(tensor.device)
+    sync(tensor.device)
     t0 = time.perf_counter()
     for _ in range(iters):
         once()
-    torch.cuda.synchronize(tensor.device)
+    sync(tensor.device)
     dt = (time.perf_counter() - t0) / max(iters, 1)
     if dist.is_initialized():
         dist.barrier(group=group)
     return _max_over_ranks(dt, tensor.device) if world > 1 else dt
 
 
+def sync(device) -> None:
+    import torch
+
+    if getattr(device, "type", str(device)) == "cuda":
+        torch.cuda.synchronize(device)
+
+
+def pattern_reference(n: int, seed: int, rank: int):
+    """PyTorch (CPU) reference of the HIP pattern in native/hip/netop_hip.hip (mix / pattern)."""
+    import torch
+
+    M32 = 0xFFFFFFFF
+    i = torch.arange(n, dtype=torch.int64)
+    s = (seed + 0x632BE5AB * (rank + 1)) & M32
+    x = ((i & M32) * 0x9E3779B1) & M32
+    x = x ^ ((((i >> 32) & M32) * 0x85EBCA77) & M32)
+    x = x ^ ((s * 0xC2B2AE3D) & M32)
+    x = x ^ (x >> 15)
+    x = (x * 0x2C1B3C6D) & M32
+    x = x ^ (x >> 12)
+    return ((x % 9) - 4).to(torch.float32)
+
+
 def verify_all_reduce(numel: int, device, seed: int = 2024, group=None) -> tuple[bool, int]:
-    """Fills rank-specific bf16 patterns with the HIP kernel, all-reduces, verifies Σ exactly."""
+    """Fills rank-specific patterns, all-reduces, verifies Σ over ranks exactly.
+
+    On a GPU the fill and the check are the HIP kernels of ``libnetop_hip.so`` (bf16; no
+    fallback — a missing library raises).  On the CPU (gloo rehearsals of the multi-rank
+    path) the same pattern comes from ``pattern_reference`` in fp32."""
     import torch
     import torch.distributed as dist
-
-    from ..ops import hip
 
     numel -= numel % 8
     rank = dist.get_rank(group) if dist.is_initialized() else 0
     world = dist.get_world_size(group) if dist.is_initialized() else 1
-    buf = torch.empty(numel, dtype=torch.bfloat16, device=device)
-    hip.fill_pattern(buf, seed, rank)
-    if dist.is_initialized():
-        dist.all_reduce(buf, group=group)
-    errors = hip.verify_sum(buf, seed, world)
+    if getattr(device, "type", str(device)) == "cuda":
+        from ..ops import hip
+
+        buf = torch.empty(numel, dtype=torch.bfloat16, device=device)
+        hip.fill_pattern(buf, seed, rank)
+        if dist.is_initialized():
+            dist.all_reduce(buf, group=group)
+        errors = hip.verify_sum(buf, seed, world)
+    else:
+        buf = pattern_reference(numel, seed, rank)
+        if dist.is_initialized():
+            dist.all_reduce(buf, group=group)
+        want = sum(pattern_reference(numel, seed, r) for r in range(world))
+        errors = int((buf != want).sum().item())
     total = int(_max_over_ranks(float(errors), device)) if world > 1 else errors
     return total == 0, total
 
@@ -153,16 +187,21 @@ def run_sweep(op: str, sizes: Iterable[int], iters: int, warmup: int, device, gr
     esize = torch.tensor([], dtype=dtype).element_size()
     results = []
     for nbytes in sizes:
+        # rccl-tests "size": the full buffer — all_gather's output, reduce_scatter's input,
+        # all_to_all's per-rank send (= receive) buffer, the all_reduce buffer.
         numel = max(1, nbytes // esize)
         numel = int(math.ceil(numel / world) * world)
-        t = torch.zeros(numel, dtype=dtype, device=device)
         out = None
         if op == "all_gather":
-            out = torch.empty(numel * world, dtype=dtype, device=device)
-        elif op in ("reduce_scatter",):
+            t = torch.zeros(numel // world, dtype=dtype, device=device)
+            out = torch.empty(numel, dtype=dtype, device=device)
+        elif op == "reduce_scatter":
+            t = torch.zeros(numel, dtype=dtype, device=device)
             out = torch.empty(numel // world, dtype=dtype, device=device)
-        elif op == "all_to_all":
-            out = torch.empty_like(t)
+        else:
+            t = torch.zeros(numel, dtype=dtype, device=device)
+            if op == "all_to_all":
+                out = torch.empty_like(t)
         dt = time_collective(op, t, iters, warmup, group=group, out=out)
         algbw, busbw = bandwidths(op, numel * esize, world, dt)
         results.append(CollectiveResult(op, numel * esize, world, iters, dt, algbw, busbw))

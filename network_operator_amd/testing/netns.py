@@ -260,10 +260,10 @@ def run_isolated(timeout: float = 300, **kw) -> dict:
     return json.loads(r.stdout.strip().splitlines()[-1])
 
 
-def node_ready_bench(n_nics: int = 8, runs: int = 5, interval: str = "30s", seed: int = 1) -> dict:
-    """Node-ready latency over `runs` fresh bring-ups, with and without switch fast start."""
+def node_ready_bench(n_nics: int = 8, runs: int = 5, interval: str = "30s", seed: int = 1, legacy: bool = True) -> dict:
+    """Node-ready latency over `runs` fresh bring-ups, with (and optionally without) switch fast start."""
     out = {"n_nics": n_nics, "runs": runs, "interval": interval}
-    for label, fs in (("fast_start_switch", True), ("legacy_switch", False)):
+    for label, fs in (("fast_start_switch", True), ("legacy_switch", False))[: 2 if legacy else 1]:
         lat, ref = [], []
         for k in range(runs):
             r = run_isolated(n_nics=n_nics, seed=seed * 1000 + k, interval=interval, fast_start=fs, verbose=0)

@@ -1,0 +1,95 @@
+"""bench.py driver contract and the multi-rank collective path, rehearsed on the CPU with gloo
+(world size 2 and 4) — the N-GPU path is the same code with backend nccl (RCCL)."""
+
+import json
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parent.parent
+REQUIRED = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+            "vs_baseline", "dtype", "data", "config"}
+
+
+def _free_port():
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.parametrize("n", [2, 4])
+def test_bench_torchrun_cpu_rehearsal(n, tmp_path):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}", "--master-addr",
+           "127.0.0.1", "--master-port", str(_free_port()), str(ROOT / "bench.py"), "--gpus", str(n), "--steps", "4",
+           "--warmup", "1", "--device", "cpu", "--bytes", str(1 << 20), "--sweep", "4096", "--node-ready", "off"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=tmp_path,
+                       env=dict(os.environ, OMP_NUM_THREADS="1"))
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout  # rank 0 only
+    j = json.loads(lines[0])
+    assert REQUIRED <= set(j)
+    assert j["n_gpus"] == n and j["steps"] == 4 and j["warmup"] == 1
+    assert j["verified"] is True and j["verify_errors"] == 0
+    assert j["value"] == pytest.approx(j["algbw_GBps"] * 2 * (n - 1) / n, abs=1e-3)
+    assert j["config"]["parallelism"] == f"dp{n}"
+    assert {c["op"] for c in j["collectives"]} == {"all_gather", "reduce_scatter", "all_to_all"}
+    assert j["busbw_ceiling_GBps"] == pytest.approx((n - 1) * 76.0)
+
+
+def _worker(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+
+    sys.path.insert(0, str(ROOT))
+    from network_operator_amd.parallel import collectives as C
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    ok, err = C.verify_all_reduce(4096, torch.device("cpu"))
+    # a rank that contributes the wrong pattern must be detected on every rank
+    buf = C.pattern_reference(4096, 2024, rank if rank else 99)
+    dist.all_reduce(buf)
+    want = sum(C.pattern_reference(4096, 2024, r) for r in range(world))
+    bad = int((buf != want).sum())
+    res = C.run_sweep("all_gather", [1 << 16], iters=2, warmup=1, device=torch.device("cpu"), dtype=torch.float32)[0]
+    q.put((rank, ok, err, bad, res.bytes, res.n_ranks))
+    dist.destroy_process_group()
+
+
+def test_collectives_gloo_world2():
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    out = [q.get(timeout=120) for _ in ps]
+    for p in ps:
+        p.join(60)
+    for rank, ok, err, bad, nbytes, n in out:
+        assert ok and err == 0
+        assert bad > 0
+        assert nbytes == 1 << 16 and n == 2
+
+
+def test_bus_factors_and_ceiling():
+    from network_operator_amd.parallel import collectives as C
+
+    assert C.bus_factor("all_reduce", 8) == pytest.approx(1.75)
+    assert C.bus_factor("all_gather", 8) == pytest.approx(0.875)
+    assert C.bus_factor("all_reduce", 1) == 0
+    algbw, busbw = C.bandwidths("all_reduce", 1 << 30, 8, 0.01)
+    assert algbw == pytest.approx((1 << 30) / 0.01 / 1e9) and busbw == pytest.approx(algbw * 1.75)
+    assert C.xgmi_busbw_ceiling_GBps(8) == pytest.approx(532.0)
+    assert C.xgmi_busbw_ceiling_GBps(1) == 0
+    assert C.sweep_sizes(8, 64) == [16, 32, 64]
