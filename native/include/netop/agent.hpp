@@ -62,6 +62,12 @@ struct Config {
     int64_t announce_interval_ns = 1000000000LL;  // re-announce to still-silent NICs
     int announce_count = 3;
     std::string node_name;               // LLDP System Name ($NODE_NAME, else hostname)
+    // Keep-running monitor: LLDP keep-alive transmission, link-failure detection (the label is
+    // withdrawn while a NIC is down and republished when it recovers), re-configuration when a
+    // switch port's Port Description changes.  The reference only waits for SIGTERM.
+    bool monitor = true;
+    int64_t lldp_tx_interval_ns = 30LL * 1000000000;  // msgTxInterval
+    int64_t monitor_tick_ns = 200LL * 1000000;        // link-event polling granularity
 };
 
 // Sanitises in place (MTU clamp to [1500, 9000], mode upper-cased); throws on a bad mode.
@@ -107,6 +113,11 @@ class Agent {
     bool ready() const { return ready_; }
     const topo::XgmiReport& xgmi() const { return xgmi_; }
 
+    // Test hook: called once per monitor iteration (lets tests inject link events / stop).
+    std::function<void(int)> on_monitor_tick;
+    int link_flaps() const { return flaps_; }
+    int reconfigurations() const { return reconfigs_; }
+
     // Exposed for unit tests (reference-named helpers).
     void interfaces_up();
     void interfaces_restore_down();
@@ -128,6 +139,14 @@ class Agent {
     void log_results();
     void mark(const std::string& phase);
     void write_status();
+    void monitor(int stop_fd);
+    bool publish_label();
+    void announce_all(uint16_t ttl);
+    bool nic_healthy(const NicState& n) const;
+
+    std::map<std::string, std::string> labels_extra_;
+    int flaps_ = 0;
+    int reconfigs_ = 0;
 
     Config cfg_;
     nl::NetOps& ops_;

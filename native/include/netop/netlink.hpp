@@ -73,6 +73,8 @@ class LinkWatcher {
     // Blocks until at least one event or the absolute CLOCK_MONOTONIC deadline; returns
     // all events read (possibly empty on timeout).
     virtual std::vector<LinkEvent> wait(int64_t deadline_mono_ns) = 0;
+    // Pollable descriptor that becomes readable when events are pending (-1 if none).
+    virtual int fd() const { return -1; }
 };
 
 // The injectable operation table.  Every method throws SysError on failure.

@@ -41,6 +41,10 @@ struct NicState {
     int rdma_port = 1;
     std::optional<int> gid_index;
 
+    // Monitor
+    bool degraded = false;  // link went down / lost carrier after readiness
+    int flaps = 0;
+
     // Timing (CLOCK_MONOTONIC ns; 0 = never)
     int64_t t_lldp = 0;
     int64_t t_configured = 0;

@@ -3,6 +3,7 @@
 #include <errno.h>
 #include <linux/if.h>
 #include <poll.h>
+#include <sys/epoll.h>
 #include <sys/socket.h>
 #include <unistd.h>
 
@@ -572,32 +573,172 @@ void Agent::run(int stop_fd) {
         write_status();
         return;
     }
-    std::map<std::string, std::string> extra;
     int nconf = int(std::count_if(nics_.begin(), nics_.end(), [](const NicState& n) { return n.configured; }));
-    extra["amd.feature.node.kubernetes.io/gpu-scale-out.mode"] = cfg_.mode;
-    extra["amd.feature.node.kubernetes.io/gpu-scale-out.nics"] = std::to_string(cfg_.mode == "L3" ? nconf : int(nics_.size()));
+    labels_extra_["amd.feature.node.kubernetes.io/gpu-scale-out.mode"] = cfg_.mode;
+    labels_extra_["amd.feature.node.kubernetes.io/gpu-scale-out.nics"] =
+        std::to_string(cfg_.mode == "L3" ? nconf : int(nics_.size()));
     if (cfg_.xgmi_expect_links >= 0)
-        extra["amd.feature.node.kubernetes.io/gpu-xgmi.pairs"] = std::to_string(xgmi_.pairs_connected);
+        labels_extra_["amd.feature.node.kubernetes.io/gpu-xgmi.pairs"] = std::to_string(xgmi_.pairs_connected);
     try {
-        if (artifacts::write_labels(cfg_.labels, extra)) NLOG_I("Published readiness label %s", cfg_.labels.path().c_str());
+        if (publish_label()) NLOG_I("Published readiness label %s", cfg_.labels.path().c_str());
     } catch (const std::exception& e) {
         throw AgentError(std::string("Failed to write NFD label to indicate scale-out readiness: ") + e.what());
     }
     ready_ = true;
     phases_["total_ready"] = mono_ns() - t0_;
     write_status();
-    NLOG_I("Configurations done. Idling...");
+    NLOG_I("Configurations done. %s...", cfg_.monitor ? "Monitoring" : "Idling");
 
-    // Idle until SIGTERM / SIGINT.
-    while (!fd_readable(stop_fd)) {
-        if (stop_fd < 0) {
-            ::pause();
-            continue;
+    if (cfg_.monitor) {
+        monitor(stop_fd);
+    } else {
+        // Idle until SIGTERM / SIGINT (reference behaviour).
+        while (!fd_readable(stop_fd)) {
+            if (stop_fd < 0) {
+                ::pause();
+                continue;
+            }
+            pollfd p{stop_fd, POLLIN, 0};
+            ::poll(&p, 1, -1);
         }
-        pollfd p{stop_fd, POLLIN, 0};
-        ::poll(&p, 1, -1);
     }
     post_cleanups();
+}
+
+bool Agent::publish_label() { return artifacts::write_labels(cfg_.labels, labels_extra_); }
+
+void Agent::announce_all(uint16_t ttl) {
+    if (!cfg_.lldp_announce || cfg_.mode != "L3") return;
+    for (auto& n : nics_) {
+        if (!n.link.up()) continue;
+        try {
+            lldp_->announce(n.ifname, lldp::encode(make_node_frame(cfg_.node_name, n.ifname, n.link.mac, n.gpu_bdf, ttl)));
+        } catch (const std::exception& e) {
+            NLOG_V(2, "LLDP announce on %s failed: %s", n.ifname.c_str(), e.what());
+        }
+    }
+}
+
+bool Agent::nic_healthy(const NicState& n) const {
+    if (!n.link.up() || n.degraded) return false;
+    return cfg_.mode != "L3" || n.configured;
+}
+
+void Agent::monitor(int stop_fd) {
+    std::unique_ptr<nl::LinkWatcher> watcher;
+    try {
+        watcher = ops_.subscribe_links();
+    } catch (const std::exception& e) {
+        NLOG_W("link monitoring disabled: %s", e.what());
+    }
+    // Carrier baseline: only a 1 -> 0 transition of IFF_LOWER_UP counts as a failure (a NIC
+    // whose carrier was never reported up — e.g. a driver without carrier reporting — is not
+    // flagged), IFF_UP going away always does.
+    std::map<int, bool> carrier;
+    for (auto& n : nics_) carrier[n.link.index] = n.link.lower_up();
+    int64_t next_tx = mono_ns() + cfg_.lldp_tx_interval_ns;
+    bool labelled = true;
+    // One pollable fd for "stop or link event": the LLDP wait returns as soon as either
+    // fires, so a link failure is acted on in about a millisecond, not at the next tick.
+    int wake = ::epoll_create1(EPOLL_CLOEXEC);
+    struct CloseFd {
+        int fd;
+        ~CloseFd() {
+            if (fd >= 0) ::close(fd);
+        }
+    } wake_guard{wake};
+    for (int f : {stop_fd, watcher ? watcher->fd() : -1}) {
+        if (f < 0 || wake < 0) continue;
+        epoll_event ev{};
+        ev.events = EPOLLIN;
+        ev.data.fd = f;
+        ::epoll_ctl(wake, EPOLL_CTL_ADD, f, &ev);
+    }
+    int wait_fd = wake >= 0 ? wake : stop_fd;
+    for (int tick = 0;; ++tick) {
+        if (on_monitor_tick) on_monitor_tick(tick);
+        if (fd_readable(stop_fd)) return;
+        int64_t now = mono_ns();
+        if (now >= next_tx) {
+            announce_all(120);  // keep our neighbour entry alive on the switch (TTL 120 s)
+            next_tx = now + cfg_.lldp_tx_interval_ns;
+        }
+        // LLDP: a changed Port Description means the switch port was re-addressed.
+        bool changed = false;
+        auto on_frame = [&](const std::string& ifname, const lldp::Frame& f) -> bool {
+            if (f.ttl == 0) return false;
+            for (auto& n : nics_) {
+                if (n.ifname != ifname) continue;
+                std::string desc = f.port_description.value_or("");
+                if (desc == n.port_description) continue;
+                NLOG_I("Port Description of '%s' changed: '%s' -> '%s'", ifname.c_str(), n.port_description.c_str(), desc.c_str());
+                auto old = n.addr;
+                on_lldp(n, f);
+                if (n.addr && old && n.addr->local == old->local) continue;
+                // drop the old address (its /30 and /16 routes go with it), configure the new one
+                try {
+                    for (auto& a : ops_.addr_list(n.link.index, AF_INET)) ops_.addr_del(a);
+                } catch (const std::exception& e) {
+                    NLOG_W("could not remove old address of '%s': %s", ifname.c_str(), e.what());
+                }
+                n.configured = false;
+                if (n.addr) configure_interface(n);
+                ++reconfigs_;
+                changed = true;
+            }
+            return false;
+        };
+        lldp_->run(std::min(next_tx, mono_ns() + cfg_.monitor_tick_ns), on_frame, wait_fd);
+        if (fd_readable(stop_fd)) return;
+        // Link state.
+        if (watcher) {
+            for (auto& ev : watcher->wait(mono_ns())) {
+                for (auto& n : nics_) {
+                    if (n.link.index != ev.link.index) continue;
+                    bool was_up = n.link.up(), had_carrier = carrier[n.link.index];
+                    n.link.flags = ev.link.flags;
+                    n.link.operstate = ev.link.operstate;
+                    bool up = n.link.up(), lower = n.link.lower_up();
+                    if (ev.deleted || (was_up && !up) || (had_carrier && !lower)) {
+                        if (!n.degraded) {
+                            NLOG_W("Interface '%s' lost link (%s)", n.ifname.c_str(), ev.deleted ? "removed" : n.link.flags_str().c_str());
+                            n.degraded = true;
+                            ++n.flaps;
+                            ++flaps_;
+                            changed = true;
+                        }
+                    } else if (n.degraded && up && (lower || !had_carrier)) {
+                        NLOG_I("Interface '%s' recovered", n.ifname.c_str());
+                        n.degraded = false;
+                        // Administrative down flushes the routes: ensure address and routes again.
+                        if (cfg_.mode == "L3" && n.addr) {
+                            n.configured = false;
+                            configure_interface(n);
+                        }
+                        changed = true;
+                    }
+                    if (lower) carrier[n.link.index] = true;
+                }
+            }
+        }
+        if (changed) {
+            bool healthy = std::all_of(nics_.begin(), nics_.end(), [&](const NicState& n) { return nic_healthy(n); });
+            if (healthy && !labelled) {
+                if (cfg_.mode == "L3") write_artifacts();
+                labelled = publish_label();
+                if (labelled) NLOG_I("All scale-out interfaces healthy again: readiness label republished");
+                announce_all(120);
+            } else if (!healthy && labelled) {
+                artifacts::remove_labels(cfg_.labels);
+                labelled = false;
+                NLOG_W("Scale-out degraded: readiness label withdrawn");
+            } else if (healthy && labelled && cfg_.mode == "L3") {
+                write_artifacts();  // re-addressed NIC: refresh the RCCL artifacts
+            }
+            ready_ = labelled;
+            write_status();
+        }
+    }
 }
 
 }  // namespace netop::agent

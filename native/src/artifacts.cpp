@@ -279,6 +279,8 @@ std::string generate_status(const std::vector<NicState>& nics, const std::map<st
         }
         if (!n->addr_error.empty()) j.key("addr_error").value(n->addr_error);
         j.key("configured").value(n->configured);
+        j.key("degraded").value(n->degraded);
+        if (n->flaps) j.key("flaps").value(n->flaps);
         if (!n->config_error.empty()) j.key("config_error").value(n->config_error);
         if (n->gid_index) j.key("gid_index").value(*n->gid_index);
         if (n->t_lldp) j.key("t_lldp_ms").value(double(n->t_lldp - t0) / 1e6);

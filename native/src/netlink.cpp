@@ -577,6 +577,7 @@ class RtnlLinkWatcher final : public LinkWatcher {
    public:
     RtnlLinkWatcher() { fd_ = open_rtnl_socket(RTMGRP_LINK, nullptr); }
     ~RtnlLinkWatcher() override { ::close(fd_); }
+    int fd() const override { return fd_; }
 
     std::vector<LinkEvent> wait(int64_t deadline) override {
         std::vector<LinkEvent> out;

@@ -371,3 +371,88 @@ TEST(agent_stale_label_removed_and_networkd) {
     CHECK(path_exists(f.cfg.networkd + "/ens0.network"));
     CHECK(path_exists(f.cfg.networkd + "/ens2.network"));
 }
+
+TEST(agent_monitor_link_failure_withdraws_and_restores_label) {
+    Fixture f;
+    f.cfg.monitor_tick_ns = 1000000;
+    Pipe stop;
+    auto src = f.all_valid();
+    agent::Agent a(f.cfg, f.ops, std::move(src), f.nm());
+    bool saw_withdrawn = false, saw_restored = false;
+    a.on_monitor_tick = [&](int tick) {
+        auto& l = f.ops.links["ens2"];
+        if (tick == 1) {
+            CHECK(path_exists(f.cfg.labels.path()));
+            // the link goes administratively down: the kernel flushes its routes
+            l.flags &= ~unsigned(IFF_UP);
+            f.ops.routes.erase(std::remove_if(f.ops.routes.begin(), f.ops.routes.end(),
+                                              [&](const nl::RouteSpec& r) { return r.ifindex == l.index; }),
+                               f.ops.routes.end());
+            f.ops.events.push_back({false, l});
+        } else if (tick == 3) {
+            saw_withdrawn = !path_exists(f.cfg.labels.path());
+            l.flags |= IFF_UP;
+            f.ops.events.push_back({false, l});
+        } else if (tick == 5) {
+            saw_restored = path_exists(f.cfg.labels.path());
+            stop.fire();
+        }
+    };
+    a.run(stop.fd[0]);
+    CHECK(saw_withdrawn);
+    CHECK(saw_restored);
+    CHECK_EQ(a.link_flaps(), 1);
+}
+
+TEST(agent_monitor_route_reensured_after_recovery) {
+    Fixture f;
+    f.cfg.monitor_tick_ns = 1000000;
+    f.cfg.keep_running = true;
+    Pipe stop;
+    agent::Agent a(f.cfg, f.ops, f.all_valid(), f.nm());
+    bool routes_back = false;
+    a.on_monitor_tick = [&](int tick) {
+        auto& l = f.ops.links["ens0"];
+        if (tick == 1) {
+            l.flags &= ~unsigned(IFF_UP);
+            f.ops.routes.clear();
+            f.ops.events.push_back({false, l});
+        } else if (tick == 2) {
+            l.flags |= IFF_UP;
+            f.ops.events.push_back({false, l});
+        } else if (tick == 4) {
+            routes_back = has_route(f.ops, 10, "10.200.0.0/16", "10.200.0.2") && has_route(f.ops, 10, "10.200.0.0/30", nullptr);
+            stop.fire();
+        }
+    };
+    a.run(stop.fd[0]);
+    CHECK(routes_back);
+}
+
+TEST(agent_monitor_port_description_change_reconfigures) {
+    Fixture f;
+    f.cfg.monitor_tick_ns = 1000000;
+    Pipe stop;
+    auto src = f.all_valid();
+    ScriptedLldp* raw = src.get();
+    agent::Agent a(f.cfg, f.ops, std::move(src), f.nm());
+    bool moved = false;
+    a.on_monitor_tick = [&](int tick) {
+        if (tick == 1) raw->frames["ens1"] = sw("02:aa:00:00:00:01", "no-alert 10.201.7.2/30");
+        if (tick == 3) {
+            bool has_new = false, has_old = false;
+            for (auto& ad : f.ops.addrs) {
+                if (ad.ifindex != 11) continue;
+                has_new |= ad.local.str() == "10.201.7.1";
+                has_old |= ad.local.str() == "10.200.0.5";
+            }
+            moved = has_new && !has_old && has_route(f.ops, 11, "10.201.0.0/16", "10.201.7.2");
+            stop.fire();
+        }
+    };
+    a.run(stop.fd[0]);
+    CHECK(moved);
+    CHECK_EQ(a.reconfigurations(), 1);
+    auto j = read_file(f.cfg.rccl_net);
+    CHECK(j && j->find("10.201.7.1") != std::string::npos);
+}

@@ -63,6 +63,8 @@ int main(int argc, char** argv) {
     fs.add_duration("link-wait", &cfg.link_wait_ns, "time to wait for link state echoes from the kernel");
     fs.add_bool("lldp-announce", &cfg.lldp_announce, "transmit our own LLDPDU on each NIC (makes 802.1AB-2009 switches answer within ~1s)");
     fs.add_string("node-name", &cfg.node_name, "LLDP System Name (default $NODE_NAME, else the hostname)");
+    fs.add_bool("monitor", &cfg.monitor, "with --keep-running: keep announcing LLDP, withdraw the label on link loss, re-configure on Port Description changes");
+    fs.add_duration("lldp-tx-interval", &cfg.lldp_tx_interval_ns, "LLDP keep-alive transmit interval while monitoring");
     bool ready_check = false;
     fs.add_bool("ready-check", &ready_check, "exit 0 if the readiness label is published, 1 otherwise (readinessProbe)");
     fs.add_bool("help", &show_help, "help for discover");

@@ -105,11 +105,38 @@ def _wait_for(path: Path, timeout: float, proc=None, poll: float = 0.0005) -> fl
     return None
 
 
+def _in_netns(pid: int, fn) -> int:
+    """Runs fn() in a forked child that joined the network namespace of `pid`."""
+    libc = ctypes.CDLL(ctypes.util.find_library("c"), use_errno=True)
+    child = os.fork()
+    if child == 0:
+        code = 1
+        try:
+            fd = os.open(f"/proc/{pid}/ns/net", os.O_RDONLY)
+            if libc.setns(fd, CLONE_NEWNET) != 0:
+                os._exit(3)
+            fn()
+            code = 0
+        finally:
+            os._exit(code)
+    _, status = os.waitpid(child, 0)
+    return os.waitstatus_to_exitcode(status)
+
+
+def set_switch_port(pid: int, port: str, up: bool) -> None:
+    def go():
+        rt = _native().Rtnl()
+        idx = rt.link_by_name(port)["index"]
+        (rt.link_set_up if up else rt.link_set_down)(idx)
+    if _in_netns(pid, go) != 0:
+        raise RuntimeError(f"could not set {port} {'up' if up else 'down'} in the switch namespace")
+
+
 def run_scenario(n_nics: int = 8, mode: str = "L3", seed: int | None = None, interval: str = "30s",
                  fast_start: bool = True, announce: bool = True, phase: str = "random", wait: str = "90s",
                  mtu: int = 9000, pipeline: bool = True, bad_nics: int = 0, silent_nics: int = 0,
                  xgmi_expect: int = 0, keep_tmp: bool = False, sigterm: bool = True, verbose: int = 2,
-                 drop_xgmi: list | None = None, extra_args: list | None = None) -> dict:
+                 drop_xgmi: list | None = None, extra_args: list | None = None, flap_port: int | None = None) -> dict:
     """Runs one node bring-up.  Must already be inside a private user+net namespace."""
     from . import fakesysfs
 
@@ -222,6 +249,26 @@ def run_scenario(n_nics: int = 8, mode: str = "L3", seed: int | None = None, int
         res["rccl_env"] = (tmp / "rccl.env").read_text() if (tmp / "rccl.env").exists() else None
         res["label"] = label.read_text() if label.exists() else None
         res["networkd_files"] = sorted(os.listdir(tmp / "networkd")) if (tmp / "networkd").exists() else []
+        if flap_port is not None and t_ready:
+            # Carrier loss on one switch port: the agent must withdraw the label, then restore
+            # it (and the NIC's routes) once the port is back.
+            sp = sw_ports[flap_port]
+            t_down = time.monotonic()
+            set_switch_port(pid, sp, False)
+            gone = None
+            end = t_down + 10
+            while time.monotonic() < end:
+                if not label.exists():
+                    gone = time.monotonic()
+                    break
+                time.sleep(0.001)
+            res["flap_withdraw_s"] = (gone - t_down) if gone else None
+            t_up = time.monotonic()
+            set_switch_port(pid, sp, True)
+            back = _wait_for(label, 10, agent)
+            res["flap_restore_s"] = (back - t_up) if back else None
+            link = rt.link_by_name(nic_names[flap_port])
+            res["flap_routes_after"] = [r for r in rt.route_list() if r["ifindex"] == link["index"]]
         if sigterm and agent.poll() is None:
             agent.send_signal(signal.SIGTERM)
         try:

@@ -110,3 +110,14 @@ def test_random_plans_are_valid():
             assert peer not in (net.network_address, net.broadcast_address)
             nets.add(net)
         assert len(nets) == 8
+
+
+def test_carrier_loss_withdraws_and_restores_readiness():
+    r = netns.run_isolated(n_nics=4, seed=19, interval="1s", fast_start=True, flap_port=2)
+    _check_configured(r)
+    assert r["flap_withdraw_s"] is not None and r["flap_withdraw_s"] < 1.0, r["agent_log"][-3000:]
+    assert r["flap_restore_s"] is not None and r["flap_restore_s"] < 2.0, r["agent_log"][-3000:]
+    p = r["plan"][2]
+    routes = {(x["dst"], x["gateway"]) for x in r["flap_routes_after"]}
+    assert (p["routed"], p["peer"]) in routes and (p["p2p"], None) in routes
+    assert "lost link" in r["agent_log"] and "readiness label republished" in r["agent_log"]
