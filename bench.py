@@ -53,6 +53,7 @@ def main(argv=None) -> int:
     ap.add_argument("--node-ready-runs", type=int, default=5)
     ap.add_argument("--collectives", default="all_gather,reduce_scatter,all_to_all",
                     help="other collectives reported at --bytes (n > 1 only)")
+    ap.add_argument("--xgmi-probe", type=int, default=1, help="run the HIP xGMI link probe on rank 0 (n > 1)")
     # CPU rehearsal of the multi-rank path (tests): gloo backend, fp32 on the host.
     ap.add_argument("--device", choices=["cuda", "cpu"], default="cuda", help=argparse.SUPPRESS)
     args = ap.parse_args(argv)
@@ -137,6 +138,21 @@ def main(argv=None) -> int:
             others.append({"op": op, "bytes": r.bytes, "time_us": r.time_s * 1e6, "algbw_GBps": r.algbw_GBps,
                            "busbw_GBps": r.busbw_GBps})
 
+    # 5. xGMI link probe (rank 0, single process over every GPU it can see): per-link pull
+    #    bandwidth and all-peers-concurrent aggregate, byte-exact.  Runs after the timed loop.
+    probe = None
+    if rank == 0 and world > 1 and args.device == "cuda" and args.xgmi_probe:
+        try:
+            from network_operator_amd.ops import hip as H
+
+            r = H.xgmi_probe(64 << 20, iters=5, max_gpus=world)
+            links = sorted(x for d, row in enumerate(r["link_GBps"]) for p, x in enumerate(row) if p != d)
+            probe = {"gpus": r["gpus"], "errors": r["errors"],
+                     "link_GBps": {"min": links[0], "median": links[len(links) // 2], "max": links[-1]} if links else None,
+                     "aggregate_GBps": {"min": min(r["aggregate_GBps"]), "max": max(r["aggregate_GBps"])}}
+        except Exception as e:
+            probe = {"error": str(e)}
+
     node_ready = None
     node_ready_note = None
     if rank == 0 and args.node_ready != "off":
@@ -174,6 +190,7 @@ def main(argv=None) -> int:
                        "backend": ("torch.distributed nccl (RCCL)" if args.device == "cuda"
                                    else "torch.distributed gloo (CPU rehearsal)")},
             "collectives": others,
+            "xgmi_probe": probe,
             "algbw_GBps": algbw,
             "busbw_GBps": busbw,
             "busbw_ceiling_GBps": ceiling,
