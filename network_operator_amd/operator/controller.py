@@ -19,7 +19,8 @@ from . import kube
 from .informer import Informer, controller_of
 from .kube import ApiClient
 from .metrics import OperatorMetrics
-from .reconciler import OWNER_KEY, EventRecorder, NetworkClusterPolicyReconciler, policy_owner_index
+from .reconciler import (OWNER_KEY, EventRecorder, NetworkClusterPolicyReconciler, daemonset_owner_index,
+                         policy_owner_index)
 from .workqueue import RateLimitingQueue
 
 log = logging.getLogger("controller")
@@ -37,14 +38,20 @@ class PolicyController:
         self.policies = Informer(client, kube.NETWORKCLUSTERPOLICIES)
         self.daemonsets = Informer(client, kube.DAEMONSETS, namespace=namespace)
         self.daemonsets.add_index(OWNER_KEY, policy_owner_index)
+        # Agent pods (indexPods in the reference, :385-404): their Ready condition explains
+        # which nodes are not configured yet (status.errors).
+        self.pods = Informer(client, kube.PODS, namespace=namespace, label_selector="app=amd-network-tools")
+        self.pods.add_index(OWNER_KEY, daemonset_owner_index)
         self.queue = RateLimitingQueue(CONTROLLER_NAME)
         self.reconciler = NetworkClusterPolicyReconciler(
             client, namespace, is_openshift,
             get_policy=lambda name: self.policies.get(name),
             list_owned=lambda name: self.daemonsets.by_index(OWNER_KEY, name),
-            recorder=EventRecorder(client, namespace) if record_events else None)
+            recorder=EventRecorder(client, namespace) if record_events else None,
+            list_pods=lambda ds: self.pods.by_index(OWNER_KEY, ds))
         self.policies.add_handler(self._on_policy)
         self.daemonsets.add_handler(self._on_daemonset)
+        self.pods.add_handler(self._on_pod)
         self._tasks: List[asyncio.Task] = []
         self.reconciles = 0
 
@@ -55,6 +62,14 @@ class PolicyController:
         ref = controller_of(obj)
         if ref and ref.get("kind") == T.KIND and ref.get("apiVersion") == T.API_VERSION:
             await self._enqueue(ref["name"])
+
+    async def _on_pod(self, ev: str, obj: dict, old: Optional[dict]) -> None:
+        ref = controller_of(obj)
+        if ref and ref.get("kind") == "DaemonSet":
+            ds = self.daemonsets.get(ref["name"], self.namespace)
+            owner = controller_of(ds) if ds else None
+            if owner and owner.get("kind") == T.KIND:
+                await self._enqueue(owner["name"])
 
     async def _enqueue(self, name: str) -> None:
         await self.queue.add(name)
@@ -113,12 +128,13 @@ class PolicyController:
     async def start(self) -> None:
         self._tasks.append(self.policies.start())
         self._tasks.append(self.daemonsets.start())
-        await asyncio.gather(self.policies.synced.wait(), self.daemonsets.synced.wait())
+        self._tasks.append(self.pods.start())
+        await asyncio.gather(self.policies.synced.wait(), self.daemonsets.synced.wait(), self.pods.synced.wait())
         for _ in range(self.workers):
             self._tasks.append(asyncio.ensure_future(self._worker()))
 
     def has_synced(self) -> bool:
-        return self.policies.synced.is_set() and self.daemonsets.synced.is_set()
+        return all(i.synced.is_set() for i in (self.policies, self.daemonsets, self.pods))
 
     async def stop(self) -> None:
         await self.queue.shutdown()

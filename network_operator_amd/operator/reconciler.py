@@ -79,6 +79,14 @@ def policy_owner_index(obj: dict) -> List[str]:
     return []
 
 
+def daemonset_owner_index(obj: dict) -> List[str]:
+    """indexPods (:385-404): Pods -> name of the owning DaemonSet."""
+    for ref in obj.get("metadata", {}).get("ownerReferences", []) or []:
+        if ref.get("controller") and ref.get("apiVersion") == "apps/v1" and ref.get("kind") == "DaemonSet":
+            return [ref["name"]]
+    return []
+
+
 def add_host_volume(ds: dict, name: str, host_path: str, container_path: str,
                     volume_type: str = "DirectoryOrCreate") -> None:
     spec = ds["spec"]["template"]["spec"]
@@ -186,13 +194,32 @@ class EventRecorder:
 class NetworkClusterPolicyReconciler:
     def __init__(self, client: ApiClient, namespace: str, is_openshift: bool,
                  get_policy: Callable[[str], Optional[dict]], list_owned: Callable[[str], List[dict]],
-                 recorder: Optional[EventRecorder] = None):
+                 recorder: Optional[EventRecorder] = None,
+                 list_pods: Optional[Callable[[str], List[dict]]] = None):
         self.client = client
         self.namespace = namespace
         self.is_openshift = is_openshift
         self._get_policy = get_policy
         self._list_owned = list_owned
+        self._list_pods = list_pods
         self.recorder = recorder
+
+    def _node_errors(self, ds_name: str, limit: int = 16) -> List[str]:
+        """Per-node agent problems from the agent Pods' Ready condition (the reference indexes
+        Pods by owner but never reads them and always reports ``errors: []``)."""
+        if self._list_pods is None:
+            return []
+        errs = []
+        for pod in sorted(self._list_pods(ds_name), key=lambda p: p.get("spec", {}).get("nodeName", "")):
+            conds = {c.get("type"): c for c in (pod.get("status", {}) or {}).get("conditions", []) or []}
+            ready = conds.get("Ready", {})
+            if ready.get("status") == "True":
+                continue
+            node = pod.get("spec", {}).get("nodeName") or pod["metadata"]["name"]
+            errs.append(f"{node}: scale-out not ready ({ready.get('reason') or pod.get('status', {}).get('phase', 'Pending')})")
+        if len(errs) > limit:
+            errs = errs[:limit] + [f"... and {len(errs) - limit} more"]
+        return errs
 
     async def _event(self, obj: dict, type_: str, reason: str, msg: str) -> None:
         if self.recorder:
@@ -266,12 +293,13 @@ class NetworkClusterPolicyReconciler:
         if cur.targets != targets or cur.ready != ready:
             updated = True
         new_state = status_for(targets, ready)
-        if cur.state != new_state or cur.errors:
+        errors = self._node_errors(ds["metadata"]["name"]) if targets and ready < targets else []
+        if cur.state != new_state or cur.errors != errors:
             updated = True
         if not updated:
             return Result()
         body = copy.deepcopy(raw)
-        body["status"] = {"targets": targets, "ready": ready, "state": new_state, "errors": []}
+        body["status"] = {"targets": targets, "ready": ready, "state": new_state, "errors": errors}
         try:
             await self.client.replace_status(kube.NETWORKCLUSTERPOLICIES, body)
         except ApiError as e:

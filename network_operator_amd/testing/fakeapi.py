@@ -372,11 +372,40 @@ class FakeApiServer:
                 new = copy.deepcopy(ds)
                 new["status"] = st
                 self._store(kube.DAEMONSETS, new, "MODIFIED")
+            self._sync_pods(ns, name, ds, matching)
             if self.agent_ready_delay is not None:
                 for n in matching:
                     if (f"{ns}/{name}", n) not in self.node_ready:
                         self.node_ready[(f"{ns}/{name}", n)] = False
                         self._bg.append(asyncio.ensure_future(self._auto_ready(f"{ns}/{name}", n)))
+
+    def _sync_pods(self, ns: str, name: str, ds: dict, nodes: List[str]) -> None:
+        """One agent Pod per targeted node, owned by the DaemonSet, with a Ready condition that
+        mirrors the agent's readinessProbe."""
+        pods = self._table(kube.PODS)
+        want = {f"{name}-{n}": n for n in nodes}
+        for (pns, pname), p in list(pods.items()):
+            refs = p["metadata"].get("ownerReferences") or []
+            if pns == ns and any(r.get("uid") == ds["metadata"]["uid"] for r in refs) and pname not in want:
+                self._delete(kube.PODS, pname, pns)
+        for pname, node in want.items():
+            ready = bool(self.node_ready.get((f"{ns}/{name}", node)))
+            cond = [{"type": "Ready", "status": "True" if ready else "False",
+                     **({} if ready else {"reason": "ContainersNotReady",
+                                          "message": "containers with unready status: [configurator]"})}]
+            cur = pods.get((ns, pname))
+            labels = dict((ds["spec"]["template"].get("metadata") or {}).get("labels") or {})
+            if cur is None:
+                pod = {"apiVersion": "v1", "kind": "Pod",
+                       "metadata": {"name": pname, "namespace": ns, "labels": labels,
+                                    "ownerReferences": [{"apiVersion": "apps/v1", "kind": "DaemonSet", "name": name,
+                                                         "uid": ds["metadata"]["uid"], "controller": True}]},
+                       "spec": {"nodeName": node}, "status": {"phase": "Running", "conditions": cond}}
+                self._create(kube.PODS, pod, ns)
+            elif cur.get("status", {}).get("conditions") != cond:
+                new = copy.deepcopy(cur)
+                new["status"]["conditions"] = cond
+                self._store(kube.PODS, new, "MODIFIED")
 
     async def _auto_ready(self, ds_key: str, node: str) -> None:
         await asyncio.sleep(self.agent_ready_delay or 0)

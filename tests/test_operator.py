@@ -159,7 +159,9 @@ def test_status_tracks_targets_and_agent_readiness():
 
             def working():
                 st = fake.get_object(kube.NETWORKCLUSTERPOLICIES, "policy")["status"]
-                assert st == {"targets": 3, "ready": 0, "state": "Working on it..", "errors": []}
+                assert st["targets"] == 3 and st["ready"] == 0 and st["state"] == "Working on it.."
+                # per-node explanation from the agent pods' Ready condition
+                assert st["errors"] == [f"gpu-node-{i}: scale-out not ready (ContainersNotReady)" for i in range(3)]
             await eventually(working)
             assert "serviceAccountName" not in fake.get_object(kube.DAEMONSETS, "policy", NS)["spec"]["template"]["spec"]
             for i in range(3):
@@ -167,11 +169,15 @@ def test_status_tracks_targets_and_agent_readiness():
 
             def good():
                 st = fake.get_object(kube.NETWORKCLUSTERPOLICIES, "policy")["status"]
-                assert st["ready"] == 3 and st["state"] == "All good"
+                assert st["ready"] == 3 and st["state"] == "All good" and st["errors"] == []
             await eventually(good)
-            # a node loses its label file (agent not ready) -> back to working
+            # a node loses its label file (agent not ready) -> back to working, with the node named
             fake.set_agent_ready("gpu-node-1", False)
-            await eventually(lambda: fake.get_object(kube.NETWORKCLUSTERPOLICIES, "policy")["status"]["ready"] == 2)
+
+            def one_down():
+                st = fake.get_object(kube.NETWORKCLUSTERPOLICIES, "policy")["status"]
+                assert st["ready"] == 2 and st["errors"] == ["gpu-node-1: scale-out not ready (ContainersNotReady)"]
+            await eventually(one_down)
             # a new matching node joins
             fake.set_node_labels("gpu-node-3", {"foo": "bar"})
             await eventually(lambda: fake.get_object(kube.NETWORKCLUSTERPOLICIES, "policy")["status"]["targets"] == 4)
