@@ -23,6 +23,7 @@
 #include <vector>
 
 #include "netop/artifacts.hpp"
+#include "netop/httpd.hpp"
 #include "netop/l3.hpp"
 #include "netop/lldp.hpp"
 #include "netop/netlink.hpp"
@@ -68,6 +69,7 @@ struct Config {
     bool monitor = true;
     int64_t lldp_tx_interval_ns = 30LL * 1000000000;  // msgTxInterval
     int64_t monitor_tick_ns = 200LL * 1000000;        // link-event polling granularity
+    std::string metrics_addr;                         // "" = off; e.g. ":9102" (/metrics, /healthz, /readyz)
 };
 
 // Sanitises in place (MTU clamp to [1500, 9000], mode upper-cased); throws on a bad mode.
@@ -83,6 +85,7 @@ class LldpSource {
                                   int stop_fd) = 0;
     // Transmits our own LLDPDU on an interface (no-op for sources that cannot transmit).
     virtual void announce(const std::string& ifname, const std::vector<uint8_t>& frame) {}
+    virtual pkt::ListenerStats stats() const { return {}; }
 };
 
 // The LLDPDU the agent advertises for one of its NICs.  Announcing ourselves makes an
@@ -147,6 +150,12 @@ class Agent {
     std::map<std::string, std::string> labels_extra_;
     int flaps_ = 0;
     int reconfigs_ = 0;
+    std::unique_ptr<httpd::Server> httpd_;
+
+   public:
+    // Prometheus text exposition of the agent state (served on Config::metrics_addr).
+    std::string render_metrics() const;
+    int metrics_port() const;
 
     Config cfg_;
     nl::NetOps& ops_;

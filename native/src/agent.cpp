@@ -48,6 +48,7 @@ class PacketSource final : public LldpSource {
     void announce(const std::string& ifname, const std::vector<uint8_t>& frame) override {
         listener_.send(ifname, frame);
     }
+    pkt::ListenerStats stats() const override { return listener_.stats(); }
 
    private:
     bool promisc_;
@@ -478,7 +479,47 @@ void Agent::log_results() {
     }
 }
 
+int Agent::metrics_port() const { return httpd_ ? httpd_->port() : 0; }
+
+std::string Agent::render_metrics() const {
+    std::string o;
+    auto metric = [&](const char* name, const char* type, const char* help) {
+        o += strfmt("# HELP %s %s\n# TYPE %s %s\n", name, help, name, type);
+    };
+    metric("netop_agent_ready", "gauge", "1 while the scale-out readiness label is published");
+    o += strfmt("netop_agent_ready{mode=\"%s\"} %d\n", cfg_.mode.c_str(), ready_ ? 1 : 0);
+    metric("netop_agent_nic_configured", "gauge", "1 when the NIC carries its LLDP-derived /30 and routes (L3) / is up (L2)");
+    for (auto& n : nics_)
+        o += strfmt("netop_agent_nic_configured{nic=\"%s\",gpu=\"%s\",rdma=\"%s\"} %d\n",
+                    httpd::escape_label(n.ifname).c_str(), n.gpu_bdf.c_str(), n.rdma_dev.c_str(),
+                    (cfg_.mode == "L3" ? n.configured : n.link.up()) ? 1 : 0);
+    metric("netop_agent_nic_degraded", "gauge", "1 while the NIC has lost link after readiness");
+    for (auto& n : nics_)
+        o += strfmt("netop_agent_nic_degraded{nic=\"%s\"} %d\n", httpd::escape_label(n.ifname).c_str(), n.degraded ? 1 : 0);
+    metric("netop_agent_link_flaps_total", "counter", "link losses observed after readiness");
+    o += strfmt("netop_agent_link_flaps_total %d\n", flaps_);
+    metric("netop_agent_reconfigurations_total", "counter", "NIC re-addressings after a Port Description change");
+    o += strfmt("netop_agent_reconfigurations_total %d\n", reconfigs_);
+    auto st = lldp_ ? lldp_->stats() : pkt::ListenerStats{};
+    metric("netop_agent_lldp_frames_total", "counter", "LLDP frames received, by outcome");
+    o += strfmt("netop_agent_lldp_frames_total{outcome=\"accepted\"} %llu\n", (unsigned long long)st.frames);
+    o += strfmt("netop_agent_lldp_frames_total{outcome=\"own\"} %llu\n", (unsigned long long)st.own);
+    o += strfmt("netop_agent_lldp_frames_total{outcome=\"malformed\"} %llu\n", (unsigned long long)st.malformed);
+    metric("netop_agent_phase_seconds", "gauge", "duration of each bring-up phase");
+    for (auto& [k, v] : phases_) o += strfmt("netop_agent_phase_seconds{phase=\"%s\"} %.9f\n", k.c_str(), double(v) / 1e9);
+    if (cfg_.xgmi_expect_links >= 0) {
+        metric("netop_agent_xgmi_pairs", "gauge", "GPU pairs with an xGMI link (KFD topology)");
+        o += strfmt("netop_agent_xgmi_pairs{state=\"connected\"} %d\n", xgmi_.pairs_connected);
+        o += strfmt("netop_agent_xgmi_pairs{state=\"expected\"} %d\n", xgmi_.pairs_expected);
+    }
+    return o;
+}
+
 void Agent::write_status() {
+    if (httpd_) {
+        httpd_->set_metrics(render_metrics());
+        httpd_->set_ready(ready_);
+    }
     if (cfg_.status_file.empty()) return;
     try {
         write_file_atomic(cfg_.status_file, artifacts::generate_status(nics_, phases_, t0_, cfg_.mode, ready_) + "\n");
@@ -490,6 +531,15 @@ void Agent::write_status() {
 void Agent::run(int stop_fd) {
     t0_ = t_last_ = mono_ns();
     sanitize(cfg_);
+    if (!cfg_.metrics_addr.empty() && !httpd_) {
+        try {
+            httpd_ = std::make_unique<httpd::Server>(cfg_.metrics_addr);
+            NLOG_I("Serving metrics on %s (port %d)", cfg_.metrics_addr.c_str(), httpd_->port());
+        } catch (const std::exception& e) {
+            NLOG_W("metrics endpoint disabled: %s", e.what());
+        }
+        write_status();
+    }
     pre_cleanups();
 
     auto names = collect_interfaces();

@@ -1,3 +1,6 @@
+#include <arpa/inet.h>
+#include <netinet/in.h>
+#include <sys/socket.h>
 #include <unistd.h>
 
 #include "check.hpp"
@@ -455,4 +458,41 @@ TEST(agent_monitor_port_description_change_reconfigures) {
     CHECK_EQ(a.reconfigurations(), 1);
     auto j = read_file(f.cfg.rccl_net);
     CHECK(j && j->find("10.201.7.1") != std::string::npos);
+}
+
+TEST(agent_metrics_endpoint) {
+    Fixture f;
+    f.cfg.metrics_addr = "127.0.0.1:0";
+    f.cfg.monitor_tick_ns = 1000000;
+    Pipe stop;
+    agent::Agent a(f.cfg, f.ops, f.all_valid(), f.nm());
+    std::string body, ready;
+    a.on_monitor_tick = [&](int tick) {
+        if (tick != 1) return;
+        auto get = [&](const char* path) {
+            int fd = ::socket(AF_INET, SOCK_STREAM, 0);
+            sockaddr_in sa{};
+            sa.sin_family = AF_INET;
+            sa.sin_port = htons(uint16_t(a.metrics_port()));
+            sa.sin_addr.s_addr = htonl(0x7f000001);
+            if (::connect(fd, reinterpret_cast<sockaddr*>(&sa), sizeof sa) != 0) return std::string();
+            std::string req = std::string("GET ") + path + " HTTP/1.1\r\nHost: x\r\n\r\n";
+            (void)!::write(fd, req.data(), req.size());
+            std::string out;
+            char buf[4096];
+            ssize_t n;
+            while ((n = ::read(fd, buf, sizeof buf)) > 0) out.append(buf, size_t(n));
+            ::close(fd);
+            return out;
+        };
+        body = get("/metrics");
+        ready = get("/readyz");
+        stop.fire();
+    };
+    a.run(stop.fd[0]);
+    CHECK(body.find("HTTP/1.1 200 OK") == 0);
+    CHECK(body.find("netop_agent_ready{mode=\"L3\"} 1") != std::string::npos);
+    CHECK(body.find("netop_agent_nic_configured{nic=\"ens0\"") != std::string::npos);
+    CHECK(body.find("netop_agent_phase_seconds{phase=\"lldp\"}") != std::string::npos);
+    CHECK(ready.find("200 OK") != std::string::npos);
 }

@@ -149,3 +149,13 @@ def test_gid_lookup(native, tmp_path):
     assert native.find_rocev2_gid_index(str(tmp_path), "mlx5_0", 1, "10.9.8.1") == 3
     assert native.find_rocev2_gid_index(str(tmp_path), "mlx5_0", 1, "10.9.8.5") == 5
     assert native.find_rocev2_gid_index(str(tmp_path), "mlx5_0", 1, "10.9.8.9") is None
+
+
+def test_topology_model(tmp_path):
+    from network_operator_amd.models import NodeTopology
+
+    fakesysfs.build_mi355x_node(tmp_path)
+    t = NodeTopology.discover(str(tmp_path))
+    assert len(t.gpus) == 8 and len(t.pairs) == 8 and t.xgmi.full_mesh
+    assert t.nic_for_gpu("0000:0a:00.0") == "enp5s0np0"
+    assert t.xgmi.busbw_ceiling_GBps() == 532.0
