@@ -54,6 +54,7 @@ def main(argv=None) -> int:
     ap.add_argument("--collectives", default="all_gather,reduce_scatter,all_to_all",
                     help="other collectives reported at --bytes (n > 1 only)")
     ap.add_argument("--xgmi-probe", type=int, default=1, help="run the HIP xGMI link probe on rank 0 (n > 1)")
+    ap.add_argument("--native-rccl", type=int, default=1, help="also run the native netop-rccl-bench harness on rank 0")
     # CPU rehearsal of the multi-rank path (tests): gloo backend, fp32 on the host.
     ap.add_argument("--device", choices=["cuda", "cpu"], default="cuda", help=argparse.SUPPRESS)
     args = ap.parse_args(argv)
@@ -153,6 +154,22 @@ def main(argv=None) -> int:
         except Exception as e:
             probe = {"error": str(e)}
 
+    # 6. Native RCCL harness (rank 0, one process over the first `world` GPUs, RCCL linked
+    #    directly, every size checked exactly): a second opinion on the same links that does not
+    #    go through torch.distributed.  Runs after the timed loop; failures are reported, not fatal.
+    native = None
+    if rank == 0 and args.device == "cuda" and args.native_rccl:
+        try:
+            from network_operator_amd.parallel import rccl_bench
+
+            rows = rccl_bench.run(op="all_reduce", gpus=world, min_bytes=1 << 20, max_bytes=1 << 30, factor=32,
+                                  iters=20, warmup=5, timeout=240)
+            native = {"rows": [{"bytes": r.bytes, "time_us": r.time_us, "algbw_GBps": r.algbw_GBps,
+                                "busbw_GBps": r.busbw_GBps, "wrong": r.wrong} for r in rows],
+                      "peak_busbw_GBps": max((r.busbw_GBps for r in rows), default=0.0)}
+        except Exception as e:
+            native = {"error": str(e)[-500:]}
+
     node_ready = None
     node_ready_note = None
     if rank == 0 and args.node_ready != "off":
@@ -191,6 +208,7 @@ def main(argv=None) -> int:
                                    else "torch.distributed gloo (CPU rehearsal)")},
             "collectives": others,
             "xgmi_probe": probe,
+            "native_rccl": native,
             "algbw_GBps": algbw,
             "busbw_GBps": busbw,
             "busbw_ceiling_GBps": ceiling,

@@ -46,25 +46,26 @@ __device__ __forceinline__ uint16_t int_to_bf16(int v) {
 
 __device__ __forceinline__ float bf16_to_float(uint16_t h) { return __uint_as_float(uint32_t(h) << 16); }
 
-__global__ __launch_bounds__(kThreads) void fill_kernel(uint4* __restrict__ out, uint64_t n_vec, uint32_t seed, int rank,
-                                                        int scale_ranks) {
+// Σ_{r in [rank_lo, rank_lo + n_ranks)} pattern(e, r): one rank's data (n_ranks = 1) or the
+// reduction over a contiguous rank range (all-reduce / reduce-scatter expectation).
+__device__ __forceinline__ int pattern_sum(uint64_t e, uint32_t seed, int rank_lo, int n_ranks) {
+    int s = 0;
+    for (int r = rank_lo; r < rank_lo + n_ranks; ++r) s += pattern(e, seed, r);
+    return s;
+}
+
+// Element e of the buffer holds pattern_sum(e + elem_offset, ...): the offset lets a chunk of
+// a collective's output be checked against the slice of the global pattern it came from.
+__global__ __launch_bounds__(kThreads) void fill_kernel(uint4* __restrict__ out, uint64_t n_vec, uint32_t seed, int rank_lo,
+                                                        int n_ranks, uint64_t elem_offset) {
     const uint64_t stride = uint64_t(gridDim.x) * kThreads;
     for (uint64_t v = uint64_t(blockIdx.x) * kThreads + threadIdx.x; v < n_vec; v += stride) {
         uint32_t w[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            uint64_t e = v * 8 + uint64_t(k) * 2;
-            int a, b;
-            if (scale_ranks > 0) {  // "sum of all ranks" expectation pre-computed in place
-                a = b = 0;
-                for (int r = 0; r < scale_ranks; ++r) {
-                    a += pattern(e, seed, r);
-                    b += pattern(e + 1, seed, r);
-                }
-            } else {
-                a = pattern(e, seed, rank);
-                b = pattern(e + 1, seed, rank);
-            }
+            uint64_t e = elem_offset + v * 8 + uint64_t(k) * 2;
+            int a = pattern_sum(e, seed, rank_lo, n_ranks);
+            int b = pattern_sum(e + 1, seed, rank_lo, n_ranks);
             w[k] = uint32_t(int_to_bf16(a)) | (uint32_t(int_to_bf16(b)) << 16);
         }
         out[v] = make_uint4(w[0], w[1], w[2], w[3]);
@@ -72,7 +73,8 @@ __global__ __launch_bounds__(kThreads) void fill_kernel(uint4* __restrict__ out,
 }
 
 __global__ __launch_bounds__(kThreads) void verify_kernel(const uint4* __restrict__ in, uint64_t n_vec, uint32_t seed,
-                                                          int world, unsigned long long* __restrict__ errors) {
+                                                          int rank_lo, int n_ranks, uint64_t elem_offset,
+                                                          unsigned long long* __restrict__ errors) {
     __shared__ unsigned int wave_err[kThreads / 64];
     const uint64_t stride = uint64_t(gridDim.x) * kThreads;
     unsigned int err = 0;
@@ -81,12 +83,9 @@ __global__ __launch_bounds__(kThreads) void verify_kernel(const uint4* __restric
         uint32_t w[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            uint64_t e = v * 8 + uint64_t(k) * 2;
-            int a = 0, b = 0;
-            for (int r = 0; r < world; ++r) {
-                a += pattern(e, seed, r);
-                b += pattern(e + 1, seed, r);
-            }
+            uint64_t e = elem_offset + v * 8 + uint64_t(k) * 2;
+            int a = pattern_sum(e, seed, rank_lo, n_ranks);
+            int b = pattern_sum(e + 1, seed, rank_lo, n_ranks);
             err += bf16_to_float(uint16_t(w[k] & 0xffff)) != float(a);
             err += bf16_to_float(uint16_t(w[k] >> 16)) != float(b);
         }
@@ -136,31 +135,43 @@ extern "C" {
 
 int netop_hip_version() { return 1; }
 
-int netop_fill_pattern(void* buf, uint64_t n_elems, uint32_t seed, int rank, hipStream_t stream) {
-    if ((n_elems & 7) || (reinterpret_cast<uintptr_t>(buf) & 15)) return int(hipErrorInvalidValue);
+// General forms: element i holds Σ_{r in [rank_lo, rank_lo+n_ranks)} pattern(i + elem_offset, r).
+// elem_offset must be a multiple of 8 as well.
+int netop_fill_pattern_at(void* buf, uint64_t n_elems, uint32_t seed, int rank_lo, int n_ranks, uint64_t elem_offset,
+                          hipStream_t stream) {
+    if ((n_elems & 7) || (elem_offset & 7) || (reinterpret_cast<uintptr_t>(buf) & 15) || n_ranks < 1 || rank_lo < 0)
+        return int(hipErrorInvalidValue);
     uint64_t nv = n_elems / 8;
+    if (nv == 0) return int(hipSuccess);
     hipLaunchKernelGGL(fill_kernel, dim3(grid_for(nv)), dim3(kThreads), 0, stream, static_cast<uint4*>(buf), nv, seed,
-                       rank, 0);
+                       rank_lo, n_ranks, elem_offset);
     return int(hipGetLastError());
+}
+
+// Adds the number of mismatching elements to *errors (a device pointer the caller zeroes).
+int netop_verify_pattern_at(const void* buf, uint64_t n_elems, uint32_t seed, int rank_lo, int n_ranks,
+                            uint64_t elem_offset, unsigned long long* errors, hipStream_t stream) {
+    if ((n_elems & 7) || (elem_offset & 7) || (reinterpret_cast<uintptr_t>(buf) & 15) || n_ranks < 1 || rank_lo < 0)
+        return int(hipErrorInvalidValue);
+    uint64_t nv = n_elems / 8;
+    if (nv == 0) return int(hipSuccess);
+    hipLaunchKernelGGL(verify_kernel, dim3(grid_for(nv)), dim3(kThreads), 0, stream, static_cast<const uint4*>(buf), nv,
+                       seed, rank_lo, n_ranks, elem_offset, errors);
+    return int(hipGetLastError());
+}
+
+int netop_fill_pattern(void* buf, uint64_t n_elems, uint32_t seed, int rank, hipStream_t stream) {
+    return netop_fill_pattern_at(buf, n_elems, seed, rank, 1, 0, stream);
 }
 
 int netop_fill_expected_sum(void* buf, uint64_t n_elems, uint32_t seed, int world, hipStream_t stream) {
-    if ((n_elems & 7) || (reinterpret_cast<uintptr_t>(buf) & 15) || world < 1) return int(hipErrorInvalidValue);
-    uint64_t nv = n_elems / 8;
-    hipLaunchKernelGGL(fill_kernel, dim3(grid_for(nv)), dim3(kThreads), 0, stream, static_cast<uint4*>(buf), nv, seed, 0,
-                       world);
-    return int(hipGetLastError());
+    return netop_fill_pattern_at(buf, n_elems, seed, 0, world, 0, stream);
 }
 
-// Counts elements that differ from Σ_{r<world} pattern(i, r).  `errors` is a device pointer
-// to one uint64 that the caller zeroes.
+// Counts elements that differ from Σ_{r<world} pattern(i, r).
 int netop_verify_sum(const void* buf, uint64_t n_elems, uint32_t seed, int world, unsigned long long* errors,
                      hipStream_t stream) {
-    if ((n_elems & 7) || (reinterpret_cast<uintptr_t>(buf) & 15) || world < 1) return int(hipErrorInvalidValue);
-    uint64_t nv = n_elems / 8;
-    hipLaunchKernelGGL(verify_kernel, dim3(grid_for(nv)), dim3(kThreads), 0, stream, static_cast<const uint4*>(buf), nv,
-                       seed, world, errors);
-    return int(hipGetLastError());
+    return netop_verify_pattern_at(buf, n_elems, seed, 0, world, 0, errors, stream);
 }
 
 int netop_copy(const void* src, void* dst, uint64_t bytes, hipStream_t stream) {

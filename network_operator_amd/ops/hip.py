@@ -34,6 +34,10 @@ def lib() -> ctypes.CDLL:
             L.netop_fill_expected_sum.restype = i32
             L.netop_verify_sum.argtypes = [vp, u64, u32, i32, vp, vp]
             L.netop_verify_sum.restype = i32
+            L.netop_fill_pattern_at.argtypes = [vp, u64, u32, i32, i32, u64, vp]
+            L.netop_fill_pattern_at.restype = i32
+            L.netop_verify_pattern_at.argtypes = [vp, u64, u32, i32, i32, u64, vp, vp]
+            L.netop_verify_pattern_at.restype = i32
             L.netop_copy.argtypes = [vp, vp, u64, vp]
             L.netop_copy.restype = i32
             L.netop_xgmi_probe.argtypes = [u64, i32, i32, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
@@ -85,6 +89,30 @@ def verify_sum(t, seed: int, world: int) -> int:
     err = torch.zeros(1, dtype=torch.int64, device=t.device)
     _check(lib().netop_verify_sum(ctypes.c_void_p(t.data_ptr()), t.numel(), seed & 0xFFFFFFFF, world,
                                   ctypes.c_void_p(err.data_ptr()), _stream(t)), "netop_verify_sum")
+    return int(err.item())
+
+
+def fill_pattern_at(t, seed: int, rank_lo: int, n_ranks: int = 1, elem_offset: int = 0) -> None:
+    """``t[i] = Σ_{r in [rank_lo, rank_lo+n_ranks)} pattern(i + elem_offset, r)`` — the slice of the
+    global pattern a collective's output chunk must equal (all-gather / reduce-scatter / all-to-all)."""
+    _check_buf(t)
+    if elem_offset % 8:
+        raise ValueError("elem_offset must be a multiple of 8")
+    _check(lib().netop_fill_pattern_at(ctypes.c_void_p(t.data_ptr()), t.numel(), seed & 0xFFFFFFFF, rank_lo, n_ranks,
+                                       elem_offset, _stream(t)), "netop_fill_pattern_at")
+
+
+def verify_pattern_at(t, seed: int, rank_lo: int, n_ranks: int = 1, elem_offset: int = 0) -> int:
+    """Mismatch count of ``t`` against :func:`fill_pattern_at`'s definition (synchronises)."""
+    import torch
+
+    _check_buf(t)
+    if elem_offset % 8:
+        raise ValueError("elem_offset must be a multiple of 8")
+    err = torch.zeros(1, dtype=torch.int64, device=t.device)
+    _check(lib().netop_verify_pattern_at(ctypes.c_void_p(t.data_ptr()), t.numel(), seed & 0xFFFFFFFF, rank_lo, n_ranks,
+                                         elem_offset, ctypes.c_void_p(err.data_ptr()), _stream(t)),
+           "netop_verify_pattern_at")
     return int(err.item())
 
 

@@ -1,0 +1,69 @@
+"""Driver for the native RCCL harness ``netop-rccl-bench`` (native/hip/rccl_bench.cpp).
+
+The harness links RCCL directly (``ncclCommInitAll`` for every local GPU in one process, or
+``ncclCommInitRank`` with a file-based unique-id exchange for one process per GPU), sweeps
+message sizes like rccl-tests and checks every result exactly with the bf16 pattern kernels.
+This module runs it and parses its JSON lines; ``bench.py --native-rccl`` reports it next to
+the torch.distributed numbers.
+"""
+
+from __future__ import annotations
+
+import json
+import subprocess
+from dataclasses import dataclass
+from typing import List, Optional
+
+from ..utils.paths import native_bin
+
+OPS = ("all_reduce", "all_gather", "reduce_scatter", "broadcast", "alltoall")
+
+
+@dataclass
+class Row:
+    op: str
+    bytes: int
+    count: int
+    ranks: int
+    time_us: float
+    algbw_GBps: float
+    busbw_GBps: float
+    wrong: int
+    checked: bool
+    inplace: bool
+    graph: bool
+
+
+def command(op: str = "all_reduce", gpus: int = 1, min_bytes: int = 8, max_bytes: int = 128 << 20, factor: float = 2,
+            iters: int = 20, warmup: int = 5, check: bool = True, inplace: bool = False, graph: bool = False,
+            dtype: str = "bf16", nranks: Optional[int] = None, rank: Optional[int] = None,
+            device: Optional[int] = None, id_file: Optional[str] = None) -> List[str]:
+    if op not in OPS:
+        raise ValueError(f"unknown op {op!r}")
+    cmd = [str(native_bin("netop-rccl-bench")), "-o", op, "-g", str(gpus), "-b", str(min_bytes), "-e", str(max_bytes),
+           "-f", str(factor), "-n", str(iters), "-w", str(warmup), "-c", "1" if check else "0", "-d", dtype]
+    if inplace:
+        cmd.append("--inplace")
+    if graph:
+        cmd.append("--graph")
+    if nranks is not None:
+        cmd += ["--nranks", str(nranks), "--rank", str(rank), "--device", str(device or 0), "--id-file", str(id_file)]
+    return cmd
+
+
+def parse(stdout: str) -> List[Row]:
+    rows = []
+    for line in stdout.splitlines():
+        line = line.strip()
+        if line.startswith("{"):
+            d = json.loads(line)
+            rows.append(Row(d["op"], d["bytes"], d["count"], d["ranks"], d["time_us"], d["algbw_GBps"], d["busbw_GBps"],
+                            d["wrong"], d["checked"], d["inplace"], d["graph"]))
+    return rows
+
+
+def run(timeout: float = 300, **kw) -> List[Row]:
+    r = subprocess.run(command(**kw), capture_output=True, text=True, timeout=timeout)
+    if r.returncode not in (0, 3):
+        raise RuntimeError(f"netop-rccl-bench failed ({r.returncode}): {r.stderr[-2000:]}")
+    return parse(r.stdout)

@@ -107,3 +107,29 @@ def test_amd_smi_xgmi_links_visible(cuda_device):
         assert g["link_status"].count("U") in (0, 7), g["link_status"]
     t = smi.traffic(snap, smi.snapshot())
     assert t["gpus"] and t["links_with_traffic"] == 0  # idle: nothing moved
+
+
+def test_pattern_at_offsets(cuda_device):
+    import torch
+
+    from network_operator_amd.ops import hip
+
+    n = 4096
+    t = torch.empty(n, dtype=torch.bfloat16, device=cuda_device)
+    hip.fill_pattern_at(t, 9, 2, 3, elem_offset=1024)
+    ref = sum(_ref_pattern(n + 1024, 9, r)[1024:] for r in (2, 3, 4))
+    torch.testing.assert_close(t.float().cpu(), ref, rtol=0, atol=0)
+    assert hip.verify_pattern_at(t, 9, 2, 3, 1024) == 0
+    assert hip.verify_pattern_at(t, 9, 2, 3, 1032) > 0
+
+
+@pytest.mark.parametrize("op", ["all_reduce", "all_gather", "reduce_scatter", "broadcast", "alltoall"])
+@pytest.mark.parametrize("inplace,graph", [(False, False), (True, False), (False, True)])
+def test_native_rccl_bench(cuda_device, op, inplace, graph):
+    from network_operator_amd.parallel import rccl_bench
+
+    rows = rccl_bench.run(op=op, gpus=1, min_bytes=1024, max_bytes=4 << 20, factor=16, iters=5, warmup=1,
+                          inplace=inplace, graph=graph, timeout=120)
+    assert [r.bytes for r in rows] == [1024, 16384, 262144, 4194304]
+    assert all(r.checked and r.wrong == 0 and r.time_us > 0 for r in rows)
+    assert all(r.busbw_GBps == 0.0 for r in rows) or op == "broadcast"  # n=1 bus factor

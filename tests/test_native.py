@@ -159,3 +159,22 @@ def test_topology_model(tmp_path):
     assert len(t.gpus) == 8 and len(t.pairs) == 8 and t.xgmi.full_mesh
     assert t.nic_for_gpu("0000:0a:00.0") == "enp5s0np0"
     assert t.xgmi.busbw_ceiling_GBps() == 532.0
+
+
+def test_rccl_bench_cli():
+    exe = str(native_bin("netop-rccl-bench"))
+    r = subprocess.run([exe, "--help"], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0 and "--id-file" in r.stderr
+    r = subprocess.run([exe, "-o", "gather"], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 2
+
+
+def test_rccl_bench_command_and_parse():
+    from network_operator_amd.parallel import rccl_bench
+
+    cmd = rccl_bench.command(op="alltoall", gpus=8, max_bytes=1 << 30, graph=True)
+    assert cmd[1:5] == ["-o", "alltoall", "-g", "8"] and "--graph" in cmd
+    rows = rccl_bench.parse('# x\n{"op":"all_reduce","bytes":8,"count":8,"dtype":"bf16","ranks":2,"time_us":9.5,'
+                            '"algbw_GBps":0.001,"busbw_GBps":0.001,"wrong":0,"checked":true,"inplace":false,'
+                            '"graph":false}\n')
+    assert rows[0].ranks == 2 and rows[0].time_us == 9.5
