@@ -23,6 +23,7 @@
 #include <vector>
 
 #include "netop/artifacts.hpp"
+#include "netop/ethtool.hpp"
 #include "netop/httpd.hpp"
 #include "netop/l3.hpp"
 #include "netop/lldp.hpp"
@@ -70,6 +71,10 @@ struct Config {
     int64_t lldp_tx_interval_ns = 30LL * 1000000000;  // msgTxInterval
     int64_t monitor_tick_ns = 200LL * 1000000;        // link-event polling granularity
     std::string metrics_addr;                         // "" = off; e.g. ":9102" (/metrics, /healthz, /readyz)
+    // Turn off NIC-firmware LLDP agents (ethtool private flags) while the agent runs, so the
+    // switch's LLDPDUs reach the host (ethtool.hpp).  L3 only.
+    bool disable_fw_lldp = false;
+    std::string fw_lldp_flags;                        // extra rules "NAME=0|1,..."
 };
 
 // Sanitises in place (MTU clamp to [1500, 9000], mode upper-cased); throws on a bad mode.
@@ -116,6 +121,10 @@ class Agent {
     bool ready() const { return ready_; }
     const topo::XgmiReport& xgmi() const { return xgmi_; }
 
+    // Replaces the ethtool ioctl table (tests inject fakes).
+    void set_ethtool_ops(std::unique_ptr<ethtool::Ops> ops) { ethtool_ = std::move(ops); }
+    const std::vector<ethtool::FwLldpResult>& fw_lldp() const { return fw_lldp_; }
+
     // Test hook: called once per monitor iteration (lets tests inject link events / stop).
     std::function<void(int)> on_monitor_tick;
     int link_flaps() const { return flaps_; }
@@ -151,6 +160,9 @@ class Agent {
     int flaps_ = 0;
     int reconfigs_ = 0;
     std::unique_ptr<httpd::Server> httpd_;
+    std::unique_ptr<ethtool::Ops> ethtool_;
+    std::vector<ethtool::FwLldpResult> fw_lldp_;
+    void disable_fw_lldp();
 
    public:
     // Prometheus text exposition of the agent state (served on Config::metrics_addr).

@@ -41,6 +41,9 @@ struct NicState {
     int rdma_port = 1;
     std::optional<int> gid_index;
 
+    // NIC firmware LLDP agent (--disable-fw-lldp): summary of what was done
+    std::string fw_lldp;
+
     // Monitor
     bool degraded = false;  // link went down / lost carrier after readiness
     int flaps = 0;

@@ -109,8 +109,34 @@ void Agent::pre_cleanups() {
     }
 }
 
+void Agent::disable_fw_lldp() {
+    std::vector<ethtool::FlagRule> rules;
+    try {
+        rules = ethtool::parse_rules(cfg_.fw_lldp_flags);
+    } catch (const std::exception& e) {
+        throw AgentError(std::string("Invalid --fw-lldp-priv-flag: ") + e.what());
+    }
+    if (!ethtool_) {
+        try {
+            ethtool_ = ethtool::make_ioctl_ops();
+        } catch (const std::exception& e) {
+            NLOG_W("ethtool unavailable, firmware LLDP agents left alone: %s", e.what());
+            return;
+        }
+    }
+    for (auto& n : nics_) {
+        auto r = ethtool::disable_fw_lldp(*ethtool_, n.ifname, rules);
+        n.fw_lldp = r.summary();
+        if (!r.error.empty()) NLOG_W("%s: firmware LLDP: %s", n.ifname.c_str(), r.error.c_str());
+        NLOG_V(2, "%s: driver %s, firmware LLDP: %s", n.ifname.c_str(), r.driver.c_str(), n.fw_lldp.c_str());
+        fw_lldp_.push_back(std::move(r));
+    }
+}
+
 void Agent::post_cleanups() {
     NLOG_I("Clean up before exiting...");
+    if (ethtool_)
+        for (const auto& r : fw_lldp_) ethtool::restore(*ethtool_, r);
     if (cfg_.lldp_announce && cfg_.mode == "L3") {
         // Shutdown LLDPDU (TTL 0): the switch drops us from its neighbour table right away.
         for (auto& n : nics_) {
@@ -575,6 +601,10 @@ void Agent::run(int stop_fd) {
         mark("networkmanager");
     }
 
+    if (cfg_.mode == "L3" && cfg_.disable_fw_lldp) {
+        disable_fw_lldp();  // before link-up: some drivers reset the port when the flag flips
+        mark("fw_lldp");
+    }
     interfaces_up();
     mark("link_up");
     interfaces_set_mtu();

@@ -267,6 +267,7 @@ std::string generate_status(const std::vector<NicState>& nics, const std::map<st
         j.key("gpu_index").value(n->gpu_index);
         if (!n->gpu_bdf.empty()) j.key("gpu_bdf").value(n->gpu_bdf);
         if (!n->rdma_dev.empty()) j.key("rdma_dev").value(n->rdma_dev);
+        if (!n->fw_lldp.empty()) j.key("fw_lldp").value(n->fw_lldp);
         j.key("lldp").value(n->lldp_seen);
         if (n->lldp_seen) {
             j.key("port_description").value(n->port_description);

@@ -1,0 +1,164 @@
+#include "netop/ethtool.hpp"
+
+#include <linux/ethtool.h>
+#include <linux/sockios.h>
+#include <net/if.h>
+#include <sys/ioctl.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <cctype>
+#include <cerrno>
+#include <cstring>
+#include <stdexcept>
+
+#include "netop/common.hpp"
+#include "netop/log.hpp"
+
+namespace netop::ethtool {
+
+int PrivFlags::index_of(const std::string& name) const {
+    for (size_t i = 0; i < names.size(); ++i)
+        if (names[i] == name) return int(i);
+    return -1;
+}
+
+namespace {
+
+class IoctlOps final : public Ops {
+   public:
+    IoctlOps() : fd_(::socket(AF_INET, SOCK_DGRAM | SOCK_CLOEXEC, 0)) {
+        if (fd_ < 0) throw SysError(errno, "ethtool socket");
+    }
+    ~IoctlOps() override { ::close(fd_); }
+
+    std::string driver(const std::string& ifname) override {
+        ethtool_drvinfo info{};
+        info.cmd = ETHTOOL_GDRVINFO;
+        if (!call(ifname, &info, false)) return "";
+        return std::string(info.driver, strnlen(info.driver, sizeof info.driver));
+    }
+
+    PrivFlags get(const std::string& ifname) override {
+        PrivFlags pf;
+        // Number of private-flag strings: ETHTOOL_GSSET_INFO with the PRIV_FLAGS bit.
+        alignas(8) uint8_t ssbuf[sizeof(ethtool_sset_info) + sizeof(uint32_t)] = {};
+        auto* ss = reinterpret_cast<ethtool_sset_info*>(ssbuf);
+        ss->cmd = ETHTOOL_GSSET_INFO;
+        ss->sset_mask = 1ull << ETH_SS_PRIV_FLAGS;
+        call(ifname, ss, true);
+        uint32_t n = 0;
+        if (ss->sset_mask & (1ull << ETH_SS_PRIV_FLAGS)) std::memcpy(&n, ssbuf + sizeof(ethtool_sset_info), sizeof n);
+        if (n == 0) return pf;
+        if (n > 32) n = 32;  // the flags word is 32 bits wide
+        std::vector<uint8_t> buf(sizeof(ethtool_gstrings) + size_t(n) * ETH_GSTRING_LEN);
+        auto* gs = reinterpret_cast<ethtool_gstrings*>(buf.data());
+        gs->cmd = ETHTOOL_GSTRINGS;
+        gs->string_set = ETH_SS_PRIV_FLAGS;
+        gs->len = n;
+        call(ifname, gs, true);
+        for (uint32_t i = 0; i < gs->len && i < n; ++i) {
+            const char* s = reinterpret_cast<const char*>(gs->data) + size_t(i) * ETH_GSTRING_LEN;
+            pf.names.emplace_back(s, strnlen(s, ETH_GSTRING_LEN));
+        }
+        ethtool_value v{};
+        v.cmd = ETHTOOL_GPFLAGS;
+        call(ifname, &v, true);
+        pf.bits = v.data;
+        return pf;
+    }
+
+    void set(const std::string& ifname, uint32_t bits) override {
+        ethtool_value v{};
+        v.cmd = ETHTOOL_SPFLAGS;
+        v.data = bits;
+        call(ifname, &v, true);
+    }
+
+   private:
+    bool call(const std::string& ifname, void* data, bool throw_on_error) {
+        ifreq ifr{};
+        if (ifname.size() >= IFNAMSIZ) throw SysError(EINVAL, "interface name too long: " + ifname);
+        std::memcpy(ifr.ifr_name, ifname.c_str(), ifname.size());
+        ifr.ifr_data = static_cast<char*>(data);
+        if (::ioctl(fd_, SIOCETHTOOL, &ifr) == 0) return true;
+        if (throw_on_error) throw SysError(errno, "SIOCETHTOOL " + ifname);
+        return false;
+    }
+    int fd_;
+};
+
+}  // namespace
+
+std::unique_ptr<Ops> make_ioctl_ops() { return std::make_unique<IoctlOps>(); }
+
+std::vector<FlagRule> builtin_rules() { return {{"disable-fw-lldp", true}, {"fw-lldp-agent", false}}; }
+
+std::vector<FlagRule> parse_rules(const std::string& spec) {
+    std::vector<FlagRule> out;
+    for (const auto& item : split(spec, ',')) {
+        std::string t = trim(item);
+        if (t.empty()) continue;
+        auto eq = t.find('=');
+        if (eq == std::string::npos || eq == 0) throw std::invalid_argument("bad private-flag rule '" + t + "' (want NAME=0|1)");
+        std::string v = trim(t.substr(eq + 1));
+        for (auto& c : v) c = char(std::tolower(static_cast<unsigned char>(c)));
+        FlagRule r{trim(t.substr(0, eq)), true};
+        if (v == "1" || v == "on" || v == "true")
+            r.value = true;
+        else if (v == "0" || v == "off" || v == "false")
+            r.value = false;
+        else
+            throw std::invalid_argument("bad private-flag value in '" + t + "'");
+        out.push_back(r);
+    }
+    for (const auto& b : builtin_rules()) out.push_back(b);
+    return out;
+}
+
+std::string FwLldpResult::summary() const {
+    if (!error.empty()) return "error: " + error;
+    if (flag.empty()) return "no firmware LLDP flag";
+    return (changed ? "set " : "already ") + flag;
+}
+
+FwLldpResult disable_fw_lldp(Ops& ops, const std::string& ifname, const std::vector<FlagRule>& rules) {
+    FwLldpResult r;
+    r.ifname = ifname;
+    try {
+        r.driver = ops.driver(ifname);
+        PrivFlags pf = ops.get(ifname);
+        r.original_bits = pf.bits;
+        for (const auto& rule : rules) {
+            int i = pf.index_of(rule.name);
+            if (i < 0) continue;
+            r.flag = rule.name + (rule.value ? "=on" : "=off");
+            uint32_t bit = 1u << i;
+            uint32_t want = rule.value ? (pf.bits | bit) : (pf.bits & ~bit);
+            if (want != pf.bits) {
+                ops.set(ifname, want);
+                r.changed = true;
+                NLOG_I("%s (%s): firmware LLDP agent off via private flag %s", ifname.c_str(), r.driver.c_str(),
+                       r.flag.c_str());
+            }
+            break;
+        }
+    } catch (const SysError& e) {
+        // EOPNOTSUPP: the driver has no private flags at all (veth, virtio, ...): nothing to do.
+        if (e.code() != EOPNOTSUPP) r.error = e.what();
+    } catch (const std::exception& e) {
+        r.error = e.what();
+    }
+    return r;
+}
+
+void restore(Ops& ops, const FwLldpResult& r) {
+    if (!r.changed) return;
+    try {
+        ops.set(r.ifname, r.original_bits);
+    } catch (const std::exception& e) {
+        NLOG_W("%s: could not restore private flags: %s", r.ifname.c_str(), e.what());
+    }
+}
+
+}  // namespace netop::ethtool

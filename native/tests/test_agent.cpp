@@ -496,3 +496,86 @@ TEST(agent_metrics_endpoint) {
     CHECK(body.find("netop_agent_phase_seconds{phase=\"lldp\"}") != std::string::npos);
     CHECK(ready.find("200 OK") != std::string::npos);
 }
+
+namespace {
+// ethtool private-flag table per interface; "eopnotsupp" NICs have no private flags at all.
+struct FakeEthtool : ethtool::Ops {
+    std::map<std::string, ethtool::PrivFlags> flags;
+    std::map<std::string, std::string> drivers;
+    std::vector<std::pair<std::string, uint32_t>> sets;
+    std::string driver(const std::string& i) override { return drivers.count(i) ? drivers[i] : ""; }
+    ethtool::PrivFlags get(const std::string& i) override {
+        auto it = flags.find(i);
+        if (it == flags.end()) throw SysError(EOPNOTSUPP, "no private flags");
+        return it->second;
+    }
+    void set(const std::string& i, uint32_t bits) override {
+        sets.emplace_back(i, bits);
+        flags[i].bits = bits;
+    }
+};
+}  // namespace
+
+TEST(ethtool_rules_parse) {
+    auto r = ethtool::parse_rules(" lldp-offload=off, my-flag=1 ");
+    CHECK_EQ(r.size(), size_t(4));
+    CHECK_EQ(r[0].name, std::string("lldp-offload"));
+    CHECK(!r[0].value && r[1].value);
+    CHECK_EQ(r[2].name, std::string("disable-fw-lldp"));  // built-ins come after user rules
+    CHECK_THROWS(ethtool::parse_rules("novalue"));
+    CHECK_THROWS(ethtool::parse_rules("x=maybe"));
+    CHECK_EQ(ethtool::parse_rules("").size(), size_t(2));
+}
+
+TEST(ethtool_disable_fw_lldp_per_driver) {
+    FakeEthtool e;
+    e.drivers = {{"i40e0", "i40e"}, {"ice0", "ice"}, {"mlx0", "mlx5_core"}};
+    e.flags["i40e0"] = {{"MFP", "total-port-shutdown", "LinkPolling", "flow-director-atr", "veb-stats", "hw-atr-eviction",
+                         "link-down-on-close", "legacy-rx", "disable-source-pruning", "disable-fw-lldp", "rs-fec"},
+                        0x1};
+    e.flags["ice0"] = {{"link-down-on-close", "fw-lldp-agent", "vf-true-promisc-support"}, 0x2};
+    e.flags["mlx0"] = {{"rx_cqe_moder", "tx_cqe_moder", "rx_cqe_compress"}, 0x1};
+    auto rules = ethtool::builtin_rules();
+    auto a = ethtool::disable_fw_lldp(e, "i40e0", rules);
+    CHECK(a.changed && a.error.empty());
+    CHECK_EQ(e.flags["i40e0"].bits, uint32_t(0x1 | (1u << 9)));
+    auto b = ethtool::disable_fw_lldp(e, "ice0", rules);
+    CHECK(b.changed);
+    CHECK_EQ(e.flags["ice0"].bits, uint32_t(0));
+    auto c = ethtool::disable_fw_lldp(e, "mlx0", rules);
+    CHECK(!c.changed && c.flag.empty() && c.error.empty());
+    CHECK_EQ(c.summary(), std::string("no firmware LLDP flag"));
+    auto d = ethtool::disable_fw_lldp(e, "veth0", rules);  // EOPNOTSUPP: not an error
+    CHECK(!d.changed && d.error.empty());
+    auto again = ethtool::disable_fw_lldp(e, "i40e0", rules);  // idempotent
+    CHECK(!again.changed && again.summary() == "already disable-fw-lldp=on");
+    ethtool::restore(e, a);
+    ethtool::restore(e, b);
+    ethtool::restore(e, c);
+    CHECK_EQ(e.flags["i40e0"].bits, uint32_t(0x1));
+    CHECK_EQ(e.flags["ice0"].bits, uint32_t(0x2));
+    CHECK_EQ(e.sets.size(), size_t(4));
+}
+
+TEST(agent_disable_fw_lldp_and_restore_on_exit) {
+    Fixture f;
+    f.cfg.disable_fw_lldp = true;
+    auto eth = std::make_unique<FakeEthtool>();
+    eth->drivers = {{"ens0", "ice"}, {"ens1", "ice"}};
+    eth->flags["ens0"] = {{"link-down-on-close", "fw-lldp-agent"}, 0x2};
+    eth->flags["ens1"] = {{"link-down-on-close", "fw-lldp-agent"}, 0x0};
+    FakeEthtool* raw = eth.get();
+    Pipe stop;
+    stop.fire();
+    agent::Agent a(f.cfg, f.ops, f.all_valid(), f.nm());
+    a.set_ethtool_ops(std::move(eth));
+    a.run(stop.fd[0]);
+    CHECK(a.ready());
+    CHECK_EQ(a.fw_lldp().size(), size_t(3));
+    CHECK(a.fw_lldp()[0].changed && !a.fw_lldp()[1].changed);
+    CHECK_EQ(raw->flags["ens0"].bits, uint32_t(0x2));  // restored by post_cleanups
+    CHECK_EQ(raw->sets.size(), size_t(2));
+    auto st = read_file(f.cfg.status_file);
+    CHECK(st && st->find("\"fw_lldp\":\"set fw-lldp-agent=off\"") != std::string::npos);
+    CHECK(st->find("\"fw_lldp\":\"already fw-lldp-agent=off\"") != std::string::npos);
+}

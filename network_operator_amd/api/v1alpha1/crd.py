@@ -59,6 +59,12 @@ def openapi_schema() -> dict:
                            "items": {"type": "string", "maxLength": 15}, "type": "array"},
             "nicDrivers": {"description": "NIC driver allow-list for GPU-affinity discovery (default: common RoCE drivers).",
                            "items": {"type": "string"}, "type": "array"},
+            "disableFirmwareLldp": {"description": "L3: turn off NIC-firmware LLDP agents (ethtool private flags, e.g. i40e\n"
+                                                   "disable-fw-lldp, ice fw-lldp-agent) while the agent runs, so switch\n"
+                                                   "LLDPDUs reach the host.",
+                                    "type": "boolean"},
+            "metricsPort": {"description": "Serve agent metrics (/metrics, /healthz, /readyz) on this host port (0 = off).",
+                            "maximum": 65535, "minimum": 0, "type": "integer"},
         },
     }
     spec = {

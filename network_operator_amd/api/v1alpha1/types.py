@@ -55,10 +55,12 @@ class AmdScaleOutSpec:
     lldpAnnounce: Optional[bool] = None
     interfaces: List[str] = field(default_factory=list)
     nicDrivers: List[str] = field(default_factory=list)
+    disableFirmwareLldp: bool = False
+    metricsPort: int = 0
     extra: Dict[str, Any] = field(default_factory=dict)
 
     _FIELDS = ("disableNetworkManager", "layer", "image", "pullPolicy", "mtu", "xgmiCheck", "lldpAnnounce",
-               "interfaces", "nicDrivers")
+               "interfaces", "nicDrivers", "disableFirmwareLldp", "metricsPort")
 
     def to_dict(self) -> dict:
         d: dict = {}
@@ -78,6 +80,10 @@ class AmdScaleOutSpec:
             d["interfaces"] = list(self.interfaces)
         if self.nicDrivers:
             d["nicDrivers"] = list(self.nicDrivers)
+        if self.disableFirmwareLldp:
+            d["disableFirmwareLldp"] = True
+        if self.metricsPort:
+            d["metricsPort"] = self.metricsPort
         d.update(copy.deepcopy(self.extra))
         return d
 
@@ -94,6 +100,8 @@ class AmdScaleOutSpec:
             lldpAnnounce=d.pop("lldpAnnounce", None),
             interfaces=list(d.pop("interfaces", []) or []),
             nicDrivers=list(d.pop("nicDrivers", []) or []),
+            disableFirmwareLldp=bool(d.pop("disableFirmwareLldp", False)),
+            metricsPort=int(d.pop("metricsPort", 0) or 0),
         )
         s.extra = d
         return s

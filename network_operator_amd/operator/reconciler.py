@@ -128,6 +128,10 @@ def agent_args(p: T.NetworkClusterPolicy) -> List[str]:
         args.append("--interfaces=" + ",".join(so.interfaces))
     if so.nicDrivers:
         args.append("--nic-drivers=" + ",".join(so.nicDrivers))
+    if so.disableFirmwareLldp and so.layer == "L3":
+        args.append("--disable-fw-lldp")
+    if so.metricsPort:
+        args.append(f"--metrics-bind-address=:{so.metricsPort}")
     return args
 
 
@@ -156,6 +160,14 @@ def update_amd_scale_out_daemonset(ds: dict, p: T.NetworkClusterPolicy, namespac
     for v in MANAGED_VOLUMES:
         if v not in wanted:
             remove_volume(ds, v)
+    # Agent metrics port (hostNetwork: the container port is the node port).
+    ports = [x for x in c.get("ports", []) if x.get("name") != "metrics"]
+    if so.metricsPort:
+        ports.append({"name": "metrics", "containerPort": so.metricsPort, "protocol": "TCP"})
+    if ports:
+        c["ports"] = ports
+    else:
+        c.pop("ports", None)
     c["args"] = agent_args(p)
 
 

@@ -121,3 +121,11 @@ def test_carrier_loss_withdraws_and_restores_readiness():
     routes = {(x["dst"], x["gateway"]) for x in r["flap_routes_after"]}
     assert (p["routed"], p["peer"]) in routes and (p["p2p"], None) in routes
     assert "lost link" in r["agent_log"] and "readiness label republished" in r["agent_log"]
+
+
+def test_disable_fw_lldp_on_real_veths():
+    """Real SIOCETHTOOL on veths: no private flags -> nothing changed, node still ready."""
+    r = netns.run_isolated(n_nics=2, seed=19, interval="1s", fast_start=True,
+                           extra_args=["--disable-fw-lldp", "--fw-lldp-priv-flag=lldp-offload=off"])
+    _check_configured(r)
+    assert [i["fw_lldp"] for i in r["status"]["interfaces"]] == ["no firmware LLDP flag"] * 2

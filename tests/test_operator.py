@@ -337,3 +337,24 @@ def test_fake_api_server_semantics():
             assert seen[:3] == ["ADDED", "MODIFIED", "MODIFIED"]
         await fake.stop()
     run(body())
+
+
+def test_agent_args_fw_lldp_and_metrics_port():
+    from network_operator_amd.api.v1alpha1 import types as T
+    from network_operator_amd.discovery import discovery_daemonset as daemonset
+    from network_operator_amd.operator.reconciler import agent_args, update_amd_scale_out_daemonset
+
+    p = T.new_policy("p", layer="L3")
+    p.spec.amdScaleOut.disableFirmwareLldp = True
+    p.spec.amdScaleOut.metricsPort = 9102
+    args = agent_args(p)
+    assert "--disable-fw-lldp" in args and "--metrics-bind-address=:9102" in args
+    ds = daemonset()
+    update_amd_scale_out_daemonset(ds, p, "ns")
+    c = ds["spec"]["template"]["spec"]["containers"][0]
+    assert c["ports"] == [{"name": "metrics", "containerPort": 9102, "protocol": "TCP"}]
+    p.spec.amdScaleOut.metricsPort = 0
+    p.spec.amdScaleOut.layer = "L2"
+    update_amd_scale_out_daemonset(ds, p, "ns")
+    assert "ports" not in c and "--disable-fw-lldp" not in c["args"]
+    assert T.NetworkClusterPolicy.from_dict(p.to_dict()).spec.amdScaleOut.disableFirmwareLldp
