@@ -167,6 +167,8 @@ def main(argv=None) -> int:
             native = {"rows": [{"bytes": r.bytes, "time_us": r.time_us, "algbw_GBps": r.algbw_GBps,
                                 "busbw_GBps": r.busbw_GBps, "wrong": r.wrong} for r in rows],
                       "peak_busbw_GBps": max((r.busbw_GBps for r in rows), default=0.0)}
+            if world > 1:  # sensitivity of the large-message busbw to RCCL knobs (diagnostic only)
+                native["env_probe"] = rccl_bench.env_probe(world, 1 << 30)
         except Exception as e:
             native = {"error": str(e)[-500:]}
 

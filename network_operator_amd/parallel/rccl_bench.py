@@ -10,6 +10,7 @@ the torch.distributed numbers.
 from __future__ import annotations
 
 import json
+import os
 import subprocess
 from dataclasses import dataclass
 from typing import List, Optional
@@ -51,6 +52,32 @@ def command(op: str = "all_reduce", gpus: int = 1, min_bytes: int = 8, max_bytes
     return cmd
 
 
+# RCCL knobs whose effect on large intra-node all-reduce is worth knowing per node type.
+ENV_PROBES = (
+    {},
+    {"NCCL_MIN_NCHANNELS": "64"},
+    {"NCCL_MIN_NCHANNELS": "112"},
+    {"NCCL_BUFFSIZE": str(8 << 20)},
+    {"NCCL_ALGO": "Ring"},
+    {"HSA_NO_SCRATCH_RECLAIM": "1"},
+)
+
+
+def env_probe(gpus: int, nbytes: int, iters: int = 10, probes=ENV_PROBES, timeout: float = 120) -> List[dict]:
+    """busbw of one all-reduce size under each RCCL environment variant (fresh process each:
+    RCCL caches its parameters at first use)."""
+    out = []
+    for extra in probes:
+        try:
+            rows = run(op="all_reduce", gpus=gpus, min_bytes=nbytes, max_bytes=nbytes, iters=iters, warmup=3,
+                       check=False, env=extra, timeout=timeout)
+            out.append({"env": extra, "busbw_GBps": rows[-1].busbw_GBps if rows else None,
+                        "time_us": rows[-1].time_us if rows else None})
+        except Exception as e:
+            out.append({"env": extra, "error": str(e)[-300:]})
+    return out
+
+
 def parse(stdout: str) -> List[Row]:
     rows = []
     for line in stdout.splitlines():
@@ -62,8 +89,10 @@ def parse(stdout: str) -> List[Row]:
     return rows
 
 
-def run(timeout: float = 300, **kw) -> List[Row]:
-    r = subprocess.run(command(**kw), capture_output=True, text=True, timeout=timeout)
+def run(timeout: float = 300, env: Optional[dict] = None, **kw) -> List[Row]:
+    """Runs the harness; ``env`` adds variables (RCCL knobs) on top of this process's environment."""
+    full_env = dict(os.environ, **(env or {}))
+    r = subprocess.run(command(**kw), capture_output=True, text=True, timeout=timeout, env=full_env)
     if r.returncode not in (0, 3):
         raise RuntimeError(f"netop-rccl-bench failed ({r.returncode}): {r.stderr[-2000:]}")
     return parse(r.stdout)
