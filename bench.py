@@ -55,6 +55,8 @@ def main(argv=None) -> int:
                     help="other collectives reported at --bytes (n > 1 only)")
     ap.add_argument("--xgmi-probe", type=int, default=1, help="run the HIP xGMI link probe on rank 0 (n > 1)")
     ap.add_argument("--native-rccl", type=int, default=1, help="also run the native netop-rccl-bench harness on rank 0")
+    ap.add_argument("--xgmi-allreduce", type=int, default=1,
+                    help="also run the direct two-shot xGMI all-reduce on rank 0 (n > 1)")
     # CPU rehearsal of the multi-rank path (tests): gloo backend, fp32 on the host.
     ap.add_argument("--device", choices=["cuda", "cpu"], default="cuda", help=argparse.SUPPRESS)
     args = ap.parse_args(argv)
@@ -172,6 +174,17 @@ def main(argv=None) -> int:
         except Exception as e:
             native = {"error": str(e)[-500:]}
 
+    # 7. Direct two-shot xGMI all-reduce (hand-written HIP, all 7 links at once, pull and push),
+    #    rank 0 over the first `world` GPUs, exact check of three seeds per size (n > 1).
+    direct = None
+    if rank == 0 and world > 1 and args.device == "cuda" and args.xgmi_allreduce:
+        try:
+            from network_operator_amd.parallel import xgmi_allreduce as XA
+
+            direct = XA.run(ranks=world, min_bytes=nbytes, max_bytes=nbytes, iters=10, warmup=3, timeout=240)
+        except Exception as e:
+            direct = {"error": str(e)[-500:]}
+
     node_ready = None
     node_ready_note = None
     if rank == 0 and args.node_ready != "off":
@@ -211,6 +224,7 @@ def main(argv=None) -> int:
             "collectives": others,
             "xgmi_probe": probe,
             "native_rccl": native,
+            "xgmi_allreduce": direct,
             "algbw_GBps": algbw,
             "busbw_GBps": busbw,
             "busbw_ceiling_GBps": ceiling,

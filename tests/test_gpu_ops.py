@@ -133,3 +133,17 @@ def test_native_rccl_bench(cuda_device, op, inplace, graph):
     assert [r.bytes for r in rows] == [1024, 16384, 262144, 4194304]
     assert all(r.checked and r.wrong == 0 and r.time_us > 0 for r in rows)
     assert all(r.busbw_GBps == 0.0 for r in rows) or op == "broadcast"  # n=1 bus factor
+
+
+@pytest.mark.parametrize("ranks", [1, 3, 8])
+def test_xgmi_allreduce_algorithm_virtual_ranks(cuda_device, ranks):
+    """The n-rank two-shot algorithm (pull and push) with every rank mapped onto the one GPU:
+    chunking, phase ordering and buffer reuse are checked exactly over three seeds per size."""
+    from network_operator_amd.parallel import xgmi_allreduce as X
+
+    rows = X.run(ranks=ranks, min_bytes=1000, max_bytes=32 << 20, factor=32, iters=2, warmup=1, timeout=180)
+    assert {r["mode"] for r in rows} == {"pull", "push"}
+    assert len(rows) == 2 * 4  # 1000 B .. 32 MB, x32
+    for r in rows:
+        assert r["ranks"] == ranks and r["wrong"] == 0, r
+        assert r["bytes"] % (16 * ranks) == 0

@@ -178,3 +178,13 @@ def test_rccl_bench_command_and_parse():
                             '"algbw_GBps":0.001,"busbw_GBps":0.001,"wrong":0,"checked":true,"inplace":false,'
                             '"graph":false}\n')
     assert rows[0].ranks == 2 and rows[0].time_us == 9.5
+
+
+def test_xgmi_allreduce_cli():
+    from network_operator_amd.parallel import xgmi_allreduce as X
+
+    r = subprocess.run(X.command(mode="pull")[:1] + ["--help"], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0 and "--mode" in r.stderr
+    assert "--ranks" in X.command(ranks=8)
+    with pytest.raises(ValueError):
+        X.command(mode="ring")
