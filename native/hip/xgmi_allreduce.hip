@@ -231,8 +231,8 @@ class Node {
     void allreduce(uint64_t bytes, bool push) {
         const uint64_t chunk = bytes / n_;     // bytes per chunk
         const uint64_t cvec = chunk / 16;      // 16-B vectors per chunk
-        // Inputs of the previous phase (filled on each rank's stream) must be complete everywhere.
-        barrier();
+        // Entry condition: every rank's input is complete (the previous round ended with a
+        // barrier, and fill() ends with one).
         if (!push) {
             for (int d = 0; d < n_; ++d) {
                 Rank& r = ranks_[d];
@@ -271,6 +271,7 @@ class Node {
             HIPCHECK(hipError_t(netop_fill_pattern_at(r.in, bytes / 2, seed, d, 1, 0, r.stream)));
             HIPCHECK(hipMemsetAsync(r.out, 0xff, bytes, r.stream));  // poison: a missed chunk cannot pass
         }
+        barrier();
     }
 
     unsigned long long verify(uint32_t seed, uint64_t bytes) {
