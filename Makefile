@@ -4,10 +4,18 @@ JOBS   ?= 8
 IMG_OPERATOR ?= amd/amd-network-operator:0.1.0
 IMG_AGENT    ?= amd/amd-network-linkdiscovery:0.1.0
 
-.PHONY: all build native hip test test-native test-netns test-gpu manifests deployments bench bench-node-ready \
-        images sanitize clean
+KUBECTL ?= kubectl
+VERSION ?= 0.1.0
+BUNDLE_IMG ?= amd/amd-network-operator-bundle:v$(VERSION)
+
+.PHONY: all help build native hip test test-native test-netns test-gpu manifests deployments bench bench-node-ready \
+        images sanitize clean fmt vet lint fuzz run build-installer install uninstall deploy undeploy bundle \
+        bundle-build helm-package-chart
 
 all: build
+
+help:                       ## list targets
+	@grep -E '^[a-zA-Z_-]+:.*## ' $(MAKEFILE_LIST) | awk -F':.*## ' '{printf "  %-20s %s\n", $$1, $$2}'
 
 build:                      ## C++ agent + pybind module + HIP (gfx950) library, in-tree
 	$(PYTHON) -c 'import __graft_entry__ as g; g.build()'
@@ -48,9 +56,50 @@ bench:                      ## 1-GPU RCCL bench (driver contract); N GPUs: torch
 bench-node-ready:           ## node scale-out-ready latency in the netns harness
 	$(PYTHON) bench/node_ready.py --nics 8 --runs 5
 
+fmt:                        ## clang-format the native sources (if installed)
+	@command -v clang-format >/dev/null && clang-format -i native/src/*.cpp native/include/netop/*.hpp native/tests/*.cpp native/tools/*.cpp || echo "clang-format not installed"
+
+vet:                        ## byte-compile Python, warnings-as-errors C++ build of the agent
+	$(PYTHON) -m compileall -q network_operator_amd bench bench.py __graft_entry__.py
+	cmake -S native -B _build-vet -G Ninja -DNETOP_PYTHON=OFF -DCMAKE_CXX_FLAGS=-Werror -DNETOP_OUT=$(CURDIR)/_build-vet/out && \
+	cmake --build _build-vet -j$(JOBS)
+
+lint: vet                   ## vet + drift checks (CRD, rendered deployments)
+	$(PYTHON) -m pytest tests/test_packaging.py -q
+
+fuzz:                       ## property-based CR churn + LLDP / Port Description fuzzing
+	$(PYTHON) -m pytest tests/test_fuzz.py tests/test_native.py -q -k "fuzz or property or garbage or churn"
+
+run:                        ## run the operator against the current kubeconfig (webhooks off)
+	ENABLE_WEBHOOKS=false $(PYTHON) -m network_operator_amd.operator --health-probe-bind-address=:8081
+
+build-installer:            ## dist/install.yaml: CRD + RBAC + webhooks + Deployment in one file
+	$(PYTHON) -m network_operator_amd.packaging installer --out dist/install.yaml $(if $(IMG),--img $(IMG))
+
+install: manifests          ## install the CRD into the current cluster
+	$(KUBECTL) apply -f config/operator/crd/bases/amd.com_networkclusterpolicies.yaml
+
+uninstall:                  ## remove the CRD from the current cluster
+	$(KUBECTL) delete --ignore-not-found -f config/operator/crd/bases/amd.com_networkclusterpolicies.yaml
+
+deploy: build-installer     ## deploy the operator into the current cluster
+	$(KUBECTL) apply -f dist/install.yaml
+
+undeploy:                   ## remove the operator from the current cluster
+	$(KUBECTL) delete --ignore-not-found -f dist/install.yaml
+
+bundle:                     ## OLM bundle (bundle/manifests, bundle/metadata, bundle.Dockerfile)
+	$(PYTHON) -m network_operator_amd.packaging bundle --out bundle --version $(VERSION) --img $(IMG_OPERATOR)
+
+bundle-build: bundle        ## build the OLM bundle image
+	docker build -f bundle.Dockerfile -t $(BUNDLE_IMG) .
+
+helm-package-chart:         ## .charts/<chart>-<version>.tgz
+	$(PYTHON) -m network_operator_amd.packaging helm --out .charts
+
 images:
 	docker build -f build/Dockerfile.operator -t $(IMG_OPERATOR) .
 	docker build -f build/Dockerfile.linkdiscovery -t $(IMG_AGENT) .
 
 clean:
-	rm -rf _build _build-asan network_operator_amd/_lib deployments
+	rm -rf _build _build-asan _build-vet network_operator_amd/_lib deployments dist bundle bundle.Dockerfile .charts

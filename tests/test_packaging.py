@@ -3,6 +3,7 @@
 Rendered with the offline renderers in ``network_operator_amd.testing.render`` (no helm /
 kustomize binaries in this environment)."""
 
+import json
 from pathlib import Path
 
 import pytest
@@ -135,3 +136,57 @@ def test_dockerfiles_build_the_native_agent():
     assert "network_operator_amd.operator" in op and "USER 65532" in op
     assert "discover" in agent and "cmake" in agent
     assert "setcap" not in agent  # capabilities come from the DaemonSet, not file caps in the image
+
+
+def test_build_installer_single_file(tmp_path):
+    from network_operator_amd import packaging
+
+    docs = packaging.installer(img="registry.local/op:1.2")
+    kinds = [d["kind"] for d in docs]
+    assert kinds.count("CustomResourceDefinition") == 1 and "Deployment" in kinds
+    assert "MutatingWebhookConfiguration" in kinds and "ValidatingWebhookConfiguration" in kinds
+    dep = [d for d in docs if d["kind"] == "Deployment"][0]
+    assert dep["spec"]["template"]["spec"]["containers"][0]["image"] == "registry.local/op:1.2"
+    assert packaging.main(["installer", "--out", str(tmp_path / "install.yaml")]) == 0
+    assert len(list(yaml.safe_load_all((tmp_path / "install.yaml").read_text()))) == len(docs)
+
+
+def test_olm_bundle_matches_installer(tmp_path):
+    from network_operator_amd import packaging
+
+    b = packaging.bundle(version="0.2.0", img="x/op:0.2.0")
+    csv = b["manifests"]["amd-network-operator.clusterserviceversion.yaml"]
+    assert csv["metadata"]["name"] == "amd-network-operator.v0.2.0" and csv["spec"]["version"] == "0.2.0"
+    assert csv["spec"]["customresourcedefinitions"]["owned"][0]["name"] == "networkclusterpolicies.amd.com"
+    perms = csv["spec"]["install"]["spec"]
+    rules = perms["clusterPermissions"][0]["rules"]
+    assert any("daemonsets" in r.get("resources", []) for r in rules)
+    assert any("networkclusterpolicies/status" in r.get("resources", []) for r in rules)
+    assert any("leases" in r.get("resources", []) for r in perms["permissions"][0]["rules"])
+    dep = perms["deployments"][0]
+    assert dep["spec"]["template"]["spec"]["containers"][0]["image"] == "x/op:0.2.0"
+    assert all(v["name"] != "cert" for v in dep["spec"]["template"]["spec"].get("volumes", []))
+    hooks = csv["spec"]["webhookdefinitions"]
+    assert {h["type"] for h in hooks} == {"MutatingAdmissionWebhook", "ValidatingAdmissionWebhook"}
+    assert all(h["rules"][0]["resources"] == ["networkclusterpolicies"] for h in hooks)  # plural (fix)
+    examples = json.loads(csv["metadata"]["annotations"]["alm-examples"])
+    assert {e["spec"]["amdScaleOut"]["layer"] for e in examples} == {"L2", "L3"}
+    ann = b["metadata"]["annotations.yaml"]["annotations"]
+    assert ann["operators.operatorframework.io.bundle.package.v1"] == "amd-network-operator"
+    files = packaging.write_bundle(tmp_path / "bundle")
+    assert (tmp_path / "bundle.Dockerfile").read_text().startswith("FROM scratch")
+    assert len(files) == 5
+
+
+def test_helm_package_archive(tmp_path):
+    import tarfile
+
+    from network_operator_amd import packaging
+
+    out = packaging.helm_package(tmp_path)
+    assert out.name == "amd-network-operator-0.1.0.tgz"
+    with tarfile.open(out) as t:
+        names = t.getnames()
+    assert "amd-network-operator/Chart.yaml" in names and "amd-network-operator/templates/amd.yaml" in names
+    again = packaging.helm_package(tmp_path / "again")
+    assert again.read_bytes() == out.read_bytes()  # deterministic
