@@ -190,3 +190,14 @@ def test_helm_package_archive(tmp_path):
     assert "amd-network-operator/Chart.yaml" in names and "amd-network-operator/templates/amd.yaml" in names
     again = packaging.helm_package(tmp_path / "again")
     assert again.read_bytes() == out.read_bytes()  # deterministic
+
+
+def test_ci_workflows_parse_and_cover_reference_jobs():
+    wf = Path(__file__).resolve().parent.parent / ".github" / "workflows"
+    docs = {p.name: yaml.safe_load(p.read_text()) for p in wf.glob("*.y*ml")}
+    assert {"ci.yaml", "codeql.yml", "scorecard.yml", "helm-publish.yaml"} <= set(docs)
+    ci = docs["ci.yaml"]["jobs"]
+    assert {"build-test", "netns", "trivy"} <= set(ci)
+    steps = " ".join(str(s.get("run", "")) for s in ci["build-test"]["steps"])
+    for target in ("sanitize", "vet", "build-installer", "bundle", "helm-package-chart"):
+        assert target in steps, target
