@@ -84,6 +84,9 @@ def main(argv=None) -> int:
         torch.cuda.set_device(local_rank)
         device, dtype = torch.device("cuda", local_rank), torch.bfloat16
         dist.init_process_group("nccl", rank=rank, world_size=world, device_id=device)
+    # Host-side group for waiting while rank 0 runs its extra GPU tools: an RCCL barrier would
+    # leave a spinning kernel on every other GPU and disturb what those tools measure.
+    host_pg = dist.new_group(backend="gloo") if args.device == "cuda" else None
     esize = torch.tensor([], dtype=dtype).element_size()
 
     # 1. Correctness of the collective path (exact, HIP pattern kernels on the GPU).
@@ -201,7 +204,7 @@ def main(argv=None) -> int:
         except Exception as e:  # the collective result stands on its own
             node_ready_note = f"node-ready harness unavailable: {e}"
 
-    dist.barrier()
+    dist.barrier(group=host_pg)
     ceiling = C.xgmi_busbw_ceiling_GBps(world)
     if rank == 0:
         line = {
