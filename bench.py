@@ -156,6 +156,9 @@ def main(argv=None) -> int:
             probe = {"gpus": r["gpus"], "errors": r["errors"],
                      "link_GBps": {"min": links[0], "median": links[len(links) // 2], "max": links[-1]} if links else None,
                      "aggregate_GBps": {"min": min(r["aggregate_GBps"]), "max": max(r["aggregate_GBps"])}}
+            p = H.xgmi_probe_push(64 << 20, iters=5, max_gpus=world)
+            probe["push_aggregate_GBps"] = {"min": min(p["push_aggregate_GBps"]), "max": max(p["push_aggregate_GBps"])}
+            probe["errors"] += p["errors"]
         except Exception as e:
             probe = {"error": str(e)}
 

@@ -311,4 +311,89 @@ int netop_xgmi_probe(uint64_t bytes, int iters, int max_gpus, double* bw_single,
     return int(hipSuccess);
 }
 
+// Push counterpart of phase 2: GPU `src` runs one copy per peer, each on its own stream,
+// writing into the peer's memory (remote stores over the link to that peer), all peers at
+// once.  bw_push[src] = aggregate GB/s leaving GPU src.  xGMI writes are posted and may reach a
+// different bandwidth than reads; the direct all-reduce has a pull and a push mode for that
+// reason.  Integrity is checked byte-exact on every destination.
+int netop_xgmi_probe_push(uint64_t bytes, int iters, int max_gpus, double* bw_push, int* n_out,
+                          unsigned long long* total_errors) {
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess) return int(e);
+    if (max_gpus > 0 && n > max_gpus) n = max_gpus;
+    *n_out = n;
+    *total_errors = 0;
+    bytes &= ~uint64_t(15);
+    if (n == 0 || bytes == 0 || iters < 1 || n > 64) return int(hipErrorInvalidValue);
+    std::vector<void*> src(n, nullptr), dst(n, nullptr);
+    const int peers = n > 1 ? n - 1 : 1;
+    for (int d = 0; d < n; ++d) {
+        if ((e = hipSetDevice(d)) != hipSuccess) return int(e);
+        for (int p = 0; p < n; ++p) {
+            if (p == d) continue;
+            hipError_t pe = hipDeviceEnablePeerAccess(p, 0);
+            if (pe != hipSuccess && pe != hipErrorPeerAccessAlreadyEnabled) return int(pe);
+            (void)hipGetLastError();
+        }
+        if ((e = hipMalloc(&src[d], bytes)) != hipSuccess) return int(e);
+        // Receive area: one slot per possible writer.
+        if ((e = hipMalloc(&dst[d], bytes * size_t(n))) != hipSuccess) return int(e);
+        if ((e = (hipError_t)netop_fill_pattern(src[d], bytes / 2, 4321u, d, nullptr)) != hipSuccess) return int(e);
+        if ((e = hipDeviceSynchronize()) != hipSuccess) return int(e);
+    }
+    for (int s = 0; s < n; ++s) {
+        hipSetDevice(s);
+        std::vector<hipStream_t> ss(peers);
+        for (auto& st : ss) hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
+        hipEvent_t t0, t1;
+        hipEventCreate(&t0);
+        hipEventCreate(&t1);
+        hipEventRecord(t0, nullptr);
+        for (auto& st : ss) hipStreamWaitEvent(st, t0, 0);
+        for (int it = 0; it < iters; ++it) {
+            int k = 0;
+            for (int p = 0; p < n; ++p) {
+                if (p == s && n > 1) continue;
+                netop_copy(src[s], static_cast<char*>(dst[p]) + size_t(s) * bytes, bytes, ss[k++]);
+            }
+        }
+        for (auto& st : ss) {
+            hipEvent_t done;
+            hipEventCreate(&done);
+            hipEventRecord(done, st);
+            hipStreamWaitEvent(nullptr, done, 0);
+            hipEventDestroy(done);
+        }
+        hipEventRecord(t1, nullptr);
+        if ((e = hipEventSynchronize(t1)) != hipSuccess) return int(e);
+        float ms = 0;
+        hipEventElapsedTime(&ms, t0, t1);
+        bw_push[s] = ms > 0 ? double(bytes) * iters * peers / (double(ms) * 1e-3) / 1e9 : 0;
+        hipEventDestroy(t0);
+        hipEventDestroy(t1);
+        for (auto& st : ss) hipStreamDestroy(st);
+    }
+    // Integrity: slot s of every destination p must equal src[s].
+    std::vector<uint8_t> got(bytes), want(bytes);
+    for (int s = 0; s < n; ++s) {
+        hipSetDevice(s);
+        hipMemcpy(want.data(), src[s], bytes, hipMemcpyDeviceToHost);
+        for (int p = 0; p < n; ++p) {
+            if (p == s && n > 1) continue;
+            hipSetDevice(p);
+            hipMemcpy(got.data(), static_cast<char*>(dst[p]) + size_t(s) * bytes, bytes, hipMemcpyDeviceToHost);
+            unsigned long long h = 0;
+            for (size_t i = 0; i < bytes; ++i) h += got[i] != want[i];
+            *total_errors += h;
+        }
+    }
+    for (int d = 0; d < n; ++d) {
+        hipSetDevice(d);
+        hipFree(src[d]);
+        hipFree(dst[d]);
+    }
+    return int(hipSuccess);
+}
+
 }  // extern "C"

@@ -11,6 +11,8 @@
 
 extern "C" int netop_xgmi_probe(uint64_t bytes, int iters, int max_gpus, double* bw_single, double* bw_all, int* n_out,
                                 unsigned long long* total_errors);
+extern "C" int netop_xgmi_probe_push(uint64_t bytes, int iters, int max_gpus, double* bw_push, int* n_out,
+                                     unsigned long long* total_errors);
 
 int main(int argc, char** argv) {
     uint64_t bytes = 256ull << 20;
@@ -42,6 +44,17 @@ int main(int argc, char** argv) {
     }
     std::printf("],\"aggregate_GBps\":[");
     for (int d = 0; d < n; ++d) std::printf("%s%.1f", d ? "," : "", all[size_t(d)]);
-    std::printf("]}\n");
-    return errors ? 3 : 0;
+    // Push: every GPU writes to all of its peers at once.
+    std::vector<double> push(64, 0.0);
+    int n2 = 0;
+    unsigned long long perr = 0;
+    rc = netop_xgmi_probe_push(bytes, iters, max_gpus, push.data(), &n2, &perr);
+    if (rc != 0) {
+        std::fprintf(stderr, "netop_xgmi_probe_push failed: hip error %d\n", rc);
+        return 1;
+    }
+    std::printf("],\"push_aggregate_GBps\":[");
+    for (int d = 0; d < n2; ++d) std::printf("%s%.1f", d ? "," : "", push[size_t(d)]);
+    std::printf("],\"push_errors\":%llu}\n", perr);
+    return errors || perr ? 3 : 0;
 }

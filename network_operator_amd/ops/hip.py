@@ -43,6 +43,9 @@ def lib() -> ctypes.CDLL:
             L.netop_xgmi_probe.argtypes = [u64, i32, i32, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                                            ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_ulonglong)]
             L.netop_xgmi_probe.restype = i32
+            L.netop_xgmi_probe_push.argtypes = [u64, i32, i32, ctypes.POINTER(ctypes.c_double),
+                                                ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_ulonglong)]
+            L.netop_xgmi_probe_push.restype = i32
             _lib = L
     return _lib
 
@@ -143,3 +146,14 @@ def xgmi_probe(nbytes: int = 256 << 20, iters: int = 10, max_gpus: int = 8) -> d
         "link_GBps": [[single[d * g + p] for p in range(g)] for d in range(g)],
         "aggregate_GBps": [agg[d] for d in range(g)],
     }
+
+
+def xgmi_probe_push(nbytes: int = 256 << 20, iters: int = 10, max_gpus: int = 8) -> dict:
+    """Every GPU writes to all of its peers at once (remote stores): aggregate GB/s per GPU."""
+    push = (ctypes.c_double * 64)()
+    n_out = ctypes.c_int(0)
+    errors = ctypes.c_ulonglong(0)
+    _check(lib().netop_xgmi_probe_push(nbytes, iters, max_gpus, push, ctypes.byref(n_out), ctypes.byref(errors)),
+           "netop_xgmi_probe_push")
+    return {"gpus": n_out.value, "bytes": nbytes, "iters": iters, "errors": errors.value,
+            "push_aggregate_GBps": [push[d] for d in range(n_out.value)]}

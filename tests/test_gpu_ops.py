@@ -147,3 +147,11 @@ def test_xgmi_allreduce_algorithm_virtual_ranks(cuda_device, ranks):
     for r in rows:
         assert r["ranks"] == ranks and r["wrong"] == 0, r
         assert r["bytes"] % (16 * ranks) == 0
+
+
+def test_xgmi_probe_push_loopback(cuda_device):
+    from network_operator_amd.ops import hip
+
+    r = hip.xgmi_probe_push(32 << 20, iters=3)
+    assert r["gpus"] >= 1 and r["errors"] == 0
+    assert r["push_aggregate_GBps"][0] > 100
