@@ -63,6 +63,7 @@ struct Config {
     bool lldp_announce = true;           // transmit our own LLDPDU (triggers switch fast start)
     int64_t announce_interval_ns = 1000000000LL;  // re-announce to still-silent NICs
     int announce_count = 3;
+    bool announce_shutdown_first = true;  // clear a stale neighbour entry left by a crashed run
     std::string node_name;               // LLDP System Name ($NODE_NAME, else hostname)
     // Keep-running monitor: LLDP keep-alive transmission, link-failure detection (the label is
     // withdrawn while a NIC is down and republished when it recovers), re-configuration when a

@@ -425,6 +425,12 @@ void Agent::detect_lldp(int stop_fd) {
             for (auto& n : nics_) {
                 if (!n.link.up() || n.lldp_seen) continue;
                 try {
+                    // After a crash the switch still holds our old neighbour entry and would not
+                    // treat us as new (no fast start).  A shutdown LLDPDU first deletes that entry
+                    // (802.1AB-2009 9.2.7.7.1), so the next LLDPDU is a new neighbour again.
+                    if (announced == 0 && cfg_.announce_shutdown_first)
+                        lldp_->announce(n.ifname,
+                                        lldp::encode(make_node_frame(cfg_.node_name, n.ifname, n.link.mac, n.gpu_bdf, 0)));
                     lldp_->announce(n.ifname, lldp::encode(make_node_frame(cfg_.node_name, n.ifname, n.link.mac, n.gpu_bdf)));
                 } catch (const std::exception& e) {
                     NLOG_V(2, "LLDP announce on %s failed: %s", n.ifname.c_str(), e.what());

@@ -62,6 +62,7 @@ int main(int argc, char** argv) {
     fs.add_int("xgmi-expect", &cfg.xgmi_expect_links, "verify the xGMI mesh before labelling: -1 off, 0 full mesh, N GPU pairs");
     fs.add_duration("link-wait", &cfg.link_wait_ns, "time to wait for link state echoes from the kernel");
     fs.add_bool("lldp-announce", &cfg.lldp_announce, "transmit our own LLDPDU on each NIC (makes 802.1AB-2009 switches answer within ~1s)");
+    fs.add_bool("lldp-restart-fast", &cfg.announce_shutdown_first, "send a shutdown LLDPDU before the first announcement so a switch holding a stale entry (agent restart) fast-starts again");
     fs.add_string("node-name", &cfg.node_name, "LLDP System Name (default $NODE_NAME, else the hostname)");
     fs.add_bool("monitor", &cfg.monitor, "with --keep-running: keep announcing LLDP, withdraw the label on link loss, re-configure on Port Description changes");
     fs.add_duration("lldp-tx-interval", &cfg.lldp_tx_interval_ns, "LLDP keep-alive transmit interval while monitoring");

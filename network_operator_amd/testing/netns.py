@@ -136,7 +136,8 @@ def run_scenario(n_nics: int = 8, mode: str = "L3", seed: int | None = None, int
                  fast_start: bool = True, announce: bool = True, phase: str = "random", wait: str = "90s",
                  mtu: int = 9000, pipeline: bool = True, bad_nics: int = 0, silent_nics: int = 0,
                  xgmi_expect: int = 0, keep_tmp: bool = False, sigterm: bool = True, verbose: int = 2,
-                 drop_xgmi: list | None = None, extra_args: list | None = None, flap_port: int | None = None) -> dict:
+                 drop_xgmi: list | None = None, extra_args: list | None = None, flap_port: int | None = None,
+                 crash_restart: bool = False, crash_after_s: float = 0.0) -> dict:
     """Runs one node bring-up.  Must already be inside a private user+net namespace."""
     from . import fakesysfs
 
@@ -249,6 +250,28 @@ def run_scenario(n_nics: int = 8, mode: str = "L3", seed: int | None = None, int
         res["rccl_env"] = (tmp / "rccl.env").read_text() if (tmp / "rccl.env").exists() else None
         res["label"] = label.read_text() if label.exists() else None
         res["networkd_files"] = sorted(os.listdir(tmp / "networkd")) if (tmp / "networkd").exists() else []
+        if crash_restart and t_ready:
+            # The agent dies without cleaning up (OOM kill, node agent crash): the label, the
+            # addresses and the switch's neighbour entry are all stale.  The restarted agent
+            # must start from scratch and still be ready in fast-start time.
+            time.sleep(crash_after_s)  # e.g. let the switch's fast-transmission window run out
+            agent.kill()
+            agent.communicate()
+            res["stale_label_after_crash"] = label.exists()
+            wall = time.time_ns()
+            t_r = time.monotonic()
+            agent = subprocess.Popen(args, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+            back = None
+            end = t_r + budget
+            while time.monotonic() < end and agent.poll() is None:
+                try:
+                    if label.stat().st_mtime_ns >= wall:
+                        back = time.monotonic()
+                        break
+                except FileNotFoundError:
+                    pass
+                time.sleep(0.0005)
+            res["restart_latency_s"] = (back - t_r) if back else None
         if flap_port is not None and t_ready:
             # Carrier loss on one switch port: the agent must withdraw the label, then restore
             # it (and the NIC's routes) once the port is back.

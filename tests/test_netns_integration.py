@@ -129,3 +129,24 @@ def test_disable_fw_lldp_on_real_veths():
                            extra_args=["--disable-fw-lldp", "--fw-lldp-priv-flag=lldp-offload=off"])
     _check_configured(r)
     assert [i["fw_lldp"] for i in r["status"]["interfaces"]] == ["no firmware LLDP flag"] * 2
+
+
+def test_crash_restart_reconfigures_in_fast_start_time():
+    """SIGKILL after readiness, then restart: stale label removed, node ready again quickly even
+    though the switch still lists the dead agent as a neighbour (shutdown LLDPDU first).  Phase
+    "zero" + 30 s interval: the switch's next periodic frame is ~25 s away at restart."""
+    r = netns.run_isolated(n_nics=4, seed=20, interval="30s", phase="zero", fast_start=True, crash_restart=True,
+                           crash_after_s=5.0)
+    _check_configured(r)
+    assert r["stale_label_after_crash"]
+    assert r["restart_latency_s"] is not None and r["restart_latency_s"] < 3.0, r["restart_latency_s"]
+    assert r["agent_rc"] == 0 and not r["label_after_sigterm"]
+
+
+def test_crash_restart_without_shutdown_first_is_not_fast_started():
+    """Control: same run without the shutdown LLDPDU — the switch still knows the neighbour, so
+    no fast start, and nothing arrives within the 3 s wait."""
+    r = netns.run_isolated(n_nics=2, seed=21, interval="30s", phase="zero", fast_start=True, crash_restart=True,
+                           crash_after_s=5.0, wait="3s", extra_args=["--lldp-restart-fast=false"])
+    assert r["stale_label_after_crash"]
+    assert r["restart_latency_s"] is None
