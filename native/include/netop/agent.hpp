@@ -74,6 +74,9 @@ struct Config {
     std::string metrics_addr;                         // "" = off; e.g. ":9102" (/metrics, /healthz, /readyz)
     // Turn off NIC-firmware LLDP agents (ethtool private flags) while the agent runs, so the
     // switch's LLDPDUs reach the host (ethtool.hpp).  L3 only.
+    // GPUDirect RDMA: "" = report only; "any" = require peer-memory or dma-buf; "peermem" /
+    // "dmabuf" = require that mechanism.  Checked before LLDP, like the xGMI mesh.
+    std::string require_gdr;
     bool disable_fw_lldp = false;
     std::string fw_lldp_flags;                        // extra rules "NAME=0|1,..."
 };
@@ -121,6 +124,7 @@ class Agent {
     const std::map<std::string, int64_t>& phases() const { return phases_; }
     bool ready() const { return ready_; }
     const topo::XgmiReport& xgmi() const { return xgmi_; }
+    const topo::GdrReport& gdr() const { return gdr_; }
 
     // Replaces the ethtool ioctl table (tests inject fakes).
     void set_ethtool_ops(std::unique_ptr<ethtool::Ops> ops) { ethtool_ = std::move(ops); }
@@ -177,6 +181,9 @@ class Agent {
     std::vector<NicState> nics_;
     topo::DiscoveryResult disc_;
     topo::XgmiReport xgmi_;
+    topo::GdrReport gdr_;
+    void check_gdr();
+    std::map<std::string, std::string> status_node() const;
     std::map<std::string, int64_t> phases_;
     int64_t t0_ = 0, t_last_ = 0;
     bool ready_ = false;

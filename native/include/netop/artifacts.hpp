@@ -73,6 +73,7 @@ bool remove_labels(const Labels& l);
 
 // Agent status document (phase timings, per-NIC results) for observability and the bench.
 std::string generate_status(const std::vector<NicState>& nics, const std::map<std::string, int64_t>& phases_ns,
-                            int64_t t0_mono, const std::string& mode, bool ready);
+                            int64_t t0_mono, const std::string& mode, bool ready,
+                            const std::map<std::string, std::string>& node = {});
 
 }  // namespace netop::artifacts

@@ -125,4 +125,22 @@ struct XgmiReport {
 
 XgmiReport read_xgmi(const std::string& root = sysfs_root());
 
+// GPUDirect RDMA readiness: can the RoCE NICs DMA straight into MI355X HBM?  Without it RCCL
+// stages every inter-node transfer through host memory, costing bandwidth and latency.
+// Two mechanisms exist on ROCm:
+//   * peer-memory: the amdgpu driver registers "amdkfd" with ib_core's peer-memory client API
+//     (/sys/kernel/mm/memory_peers/amdkfd/version, MLNX_OFED / amdgpu-dkms);
+//   * dma-buf:     upstream RDMA dma-buf memory regions, kernel >= 5.12 with ib_uverbs loaded.
+struct GdrReport {
+    bool peer_mem = false;
+    std::string peer_mem_version;
+    bool ib_uverbs = false;
+    std::string kernel;          // release string the dma-buf decision used
+    bool dmabuf = false;
+    std::string mode() const { return peer_mem ? "peermem" : dmabuf ? "dmabuf" : "none"; }
+};
+// `kernel_release` = "" reads uname(2).
+GdrReport detect_gdr(const std::string& root = sysfs_root(), const std::string& kernel_release = "");
+bool kernel_at_least(const std::string& release, int major, int minor);
+
 }  // namespace netop::topo

@@ -220,6 +220,17 @@ PYBIND11_MODULE(_netop_native, m) {
         d["missing"] = miss;
         return d;
     });
+    m.def("detect_gdr", [](const std::string& root, const std::string& kernel) {
+        auto g = topo::detect_gdr(root, kernel);
+        py::dict d;
+        d["mode"] = g.mode();
+        d["peer_mem"] = g.peer_mem;
+        d["peer_mem_version"] = g.peer_mem_version;
+        d["ib_uverbs"] = g.ib_uverbs;
+        d["dmabuf"] = g.dmabuf;
+        d["kernel"] = g.kernel;
+        return d;
+    }, py::arg("root") = "/sys/", py::arg("kernel") = "");
     // ---- NetworkManager over the D-Bus wire client ------------------------------------
     // The GIL is released: the peer may be a Python thread in this process (tests).
     m.def("nm_disable_interfaces", [](const std::string& address, const std::vector<std::string>& ifaces) {

@@ -487,6 +487,33 @@ void Agent::check_xgmi() {
         throw AgentError(strfmt("xGMI mesh incomplete: %d of %d GPU pairs linked", xgmi_.pairs_connected, expect));
 }
 
+std::map<std::string, std::string> Agent::status_node() const {
+    std::map<std::string, std::string> m;
+    if (!cfg_.node_name.empty()) m["node"] = cfg_.node_name;
+    if (!gdr_.kernel.empty()) {
+        m["gpudirect_rdma"] = gdr_.mode();
+        m["kernel"] = gdr_.kernel;
+    }
+    if (cfg_.xgmi_expect_links >= 0)
+        m["xgmi_pairs"] = std::to_string(xgmi_.pairs_connected) + "/" + std::to_string(xgmi_.pairs_expected);
+    return m;
+}
+
+void Agent::check_gdr() {
+    std::string root = cfg_.sysfs_root.empty() ? topo::sysfs_root() : cfg_.sysfs_root;
+    gdr_ = topo::detect_gdr(root);
+    NLOG_I("GPUDirect RDMA: %s (peer-memory %s, ib_uverbs %s, kernel %s)", gdr_.mode().c_str(),
+           gdr_.peer_mem ? gdr_.peer_mem_version.c_str() : "absent", gdr_.ib_uverbs ? "loaded" : "absent",
+           gdr_.kernel.c_str());
+    const std::string& want = cfg_.require_gdr;
+    if (want.empty()) return;
+    bool ok = want == "any" ? gdr_.mode() != "none" : want == "peermem" ? gdr_.peer_mem : want == "dmabuf" ? gdr_.dmabuf : false;
+    if (want != "any" && want != "peermem" && want != "dmabuf") throw AgentError("Invalid --require-gdr '" + want + "'");
+    if (!ok)
+        throw AgentError("GPUDirect RDMA unavailable (" + gdr_.mode() + ", required: " + want +
+                         "): RCCL would stage inter-node traffic through host memory");
+}
+
 void Agent::log_results() {
     for (auto& n : nics_) {
         NLOG_V(3, "Interface '%s' %s:", n.ifname.c_str(), n.link.flags_str().c_str());
@@ -539,6 +566,11 @@ std::string Agent::render_metrics() const {
     o += strfmt("netop_agent_lldp_frames_total{outcome=\"malformed\"} %llu\n", (unsigned long long)st.malformed);
     metric("netop_agent_phase_seconds", "gauge", "duration of each bring-up phase");
     for (auto& [k, v] : phases_) o += strfmt("netop_agent_phase_seconds{phase=\"%s\"} %.9f\n", k.c_str(), double(v) / 1e9);
+    if (!gdr_.kernel.empty()) {
+        metric("netop_agent_gpudirect_rdma", "gauge", "GPUDirect RDMA mechanism available to RCCL (1 = this one)");
+        for (const char* m : {"peermem", "dmabuf", "none"})
+            o += strfmt("netop_agent_gpudirect_rdma{mode=\"%s\"} %d\n", m, gdr_.mode() == m ? 1 : 0);
+    }
     if (cfg_.xgmi_expect_links >= 0) {
         metric("netop_agent_xgmi_pairs", "gauge", "GPU pairs with an xGMI link (KFD topology)");
         o += strfmt("netop_agent_xgmi_pairs{state=\"connected\"} %d\n", xgmi_.pairs_connected);
@@ -554,7 +586,7 @@ void Agent::write_status() {
     }
     if (cfg_.status_file.empty()) return;
     try {
-        write_file_atomic(cfg_.status_file, artifacts::generate_status(nics_, phases_, t0_, cfg_.mode, ready_) + "\n");
+        write_file_atomic(cfg_.status_file, artifacts::generate_status(nics_, phases_, t0_, cfg_.mode, ready_, status_node()) + "\n");
     } catch (const std::exception& e) {
         NLOG_W("Could not write status file: %s", e.what());
     }
@@ -583,6 +615,10 @@ void Agent::run(int stop_fd) {
     // milliseconds instead of after the LLDP wait, and nothing is left for the critical path.
     check_xgmi();
     mark("xgmi");
+    if (cfg_.mode == "L3" || !cfg_.require_gdr.empty()) {
+        check_gdr();
+        mark("gdr");
+    }
 
     if (cfg_.disable_nm) {
         if (!cfg_.nm_keyfile_dir.empty()) {
@@ -665,6 +701,7 @@ void Agent::run(int stop_fd) {
         std::to_string(cfg_.mode == "L3" ? nconf : int(nics_.size()));
     if (cfg_.xgmi_expect_links >= 0)
         labels_extra_["amd.feature.node.kubernetes.io/gpu-xgmi.pairs"] = std::to_string(xgmi_.pairs_connected);
+    if (!gdr_.kernel.empty()) labels_extra_["amd.feature.node.kubernetes.io/gpu-scale-out.gdr"] = gdr_.mode();
     try {
         if (publish_label()) NLOG_I("Published readiness label %s", cfg_.labels.path().c_str());
     } catch (const std::exception& e) {

@@ -251,11 +251,13 @@ bool remove_labels(const Labels& l) { return ::unlink(l.path().c_str()) == 0; }
 // Status document
 // ---------------------------------------------------------------------------
 std::string generate_status(const std::vector<NicState>& nics, const std::map<std::string, int64_t>& phases_ns,
-                            int64_t t0, const std::string& mode, bool ready) {
+                            int64_t t0, const std::string& mode, bool ready,
+                            const std::map<std::string, std::string>& node) {
     Json j;
     j.begin_object();
     j.key("mode").value(mode);
     j.key("ready").value(ready);
+    for (auto& [k, v] : node) j.key(k).value(v);
     j.key("phases_ms").begin_object();
     for (auto& [k, v] : phases_ns) j.key(k).value(double(v) / 1e6);
     j.end_object();

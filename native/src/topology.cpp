@@ -1,5 +1,7 @@
 #include "netop/topology.hpp"
 
+#include <sys/utsname.h>
+
 #include <algorithm>
 #include <cstdlib>
 #include <set>
@@ -353,6 +355,31 @@ XgmiReport read_xgmi(const std::string& root) {
                 r.missing.emplace_back(r.gpus[size_t(i)].bdf(), r.gpus[size_t(j)].bdf());
         }
     return r;
+}
+
+// ---------------------------------------------------------------------------
+// GPUDirect RDMA
+// ---------------------------------------------------------------------------
+bool kernel_at_least(const std::string& release, int major, int minor) {
+    int ma = 0, mi = 0;
+    if (std::sscanf(release.c_str(), "%d.%d", &ma, &mi) != 2) return false;
+    return ma > major || (ma == major && mi >= minor);
+}
+
+GdrReport detect_gdr(const std::string& root, const std::string& kernel_release) {
+    GdrReport g;
+    if (auto v = read_file(path_join(root, "kernel/mm/memory_peers/amdkfd/version"))) {
+        g.peer_mem = true;
+        g.peer_mem_version = trim(*v);
+    }
+    g.ib_uverbs = path_exists(path_join(root, "module/ib_uverbs"));
+    g.kernel = kernel_release;
+    if (g.kernel.empty()) {
+        utsname u{};
+        if (::uname(&u) == 0) g.kernel = u.release;
+    }
+    g.dmabuf = g.ib_uverbs && kernel_at_least(g.kernel, 5, 12);
+    return g;
 }
 
 }  // namespace netop::topo

@@ -579,3 +579,25 @@ TEST(agent_disable_fw_lldp_and_restore_on_exit) {
     CHECK(st && st->find("\"fw_lldp\":\"set fw-lldp-agent=off\"") != std::string::npos);
     CHECK(st->find("\"fw_lldp\":\"already fw-lldp-agent=off\"") != std::string::npos);
 }
+
+TEST(agent_require_gdr) {
+    Fixture f;
+    f.cfg.sysfs_root = f.tmp.path + "/sys";
+    f.tmp.mkdir("sys");
+    f.cfg.require_gdr = "any";
+    Pipe stop;
+    stop.fire();
+    {
+        agent::Agent a(f.cfg, f.ops, f.all_valid(), f.nm());
+        CHECK_THROWS(a.run(stop.fd[0]));  // neither peer-memory nor ib_uverbs in the fake sysfs
+    }
+    f.tmp.mkdir("sys/kernel/mm/memory_peers/amdkfd");
+    f.tmp.write("sys/kernel/mm/memory_peers/amdkfd/version", "1.2\n");
+    agent::Agent a(f.cfg, f.ops, f.all_valid(), f.nm());
+    a.run(stop.fd[0]);
+    CHECK(a.ready());
+    CHECK_EQ(a.gdr().mode(), std::string("peermem"));
+    auto st = read_file(f.cfg.status_file);
+    CHECK(st && st->find("\"gpudirect_rdma\":\"peermem\"") != std::string::npos);
+    CHECK(a.render_metrics().find("netop_agent_gpudirect_rdma{mode=\"peermem\"} 1") != std::string::npos);
+}

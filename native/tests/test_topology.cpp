@@ -145,3 +145,19 @@ TEST(topology_kfd_xgmi_mesh) {
     CHECK_EQ(x.min_link_bw_mbs, uint64_t(76000));
     CHECK_EQ(x.per_gpu_bw_mbs(), uint64_t(2 * 76000));
 }
+
+TEST(topology_gdr_detection) {
+    TmpDir t;
+    auto g = topo::detect_gdr(t.path, "6.8.0-45-generic");
+    CHECK_EQ(g.mode(), std::string("none"));
+    t.mkdir("module/ib_uverbs");
+    CHECK_EQ(topo::detect_gdr(t.path, "6.8.0-45-generic").mode(), std::string("dmabuf"));
+    CHECK_EQ(topo::detect_gdr(t.path, "5.4.0-150-generic").mode(), std::string("none"));  // no RDMA dma-buf MRs
+    t.mkdir("kernel/mm/memory_peers/amdkfd");
+    t.write("kernel/mm/memory_peers/amdkfd/version", "1.0\n");
+    auto p = topo::detect_gdr(t.path, "5.4.0");
+    CHECK_EQ(p.mode(), std::string("peermem"));
+    CHECK_EQ(p.peer_mem_version, std::string("1.0"));
+    CHECK(topo::kernel_at_least("5.12.0", 5, 12) && !topo::kernel_at_least("5.11.22", 5, 12));
+    CHECK(topo::kernel_at_least("10.0", 5, 12) && !topo::kernel_at_least("garbage", 5, 12));
+}

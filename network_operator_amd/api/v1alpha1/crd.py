@@ -63,6 +63,9 @@ def openapi_schema() -> dict:
                                                    "disable-fw-lldp, ice fw-lldp-agent) while the agent runs, so switch\n"
                                                    "LLDPDUs reach the host.",
                                     "type": "boolean"},
+            "gpuDirectRdma": {"description": "Require GPUDirect RDMA before labelling the node: Any, PeerMem (amdkfd\n"
+                                             "peer-memory client) or DmaBuf (RDMA dma-buf MRs).  Empty: report only.",
+                              "enum": ["Any", "PeerMem", "DmaBuf"], "type": "string"},
             "metricsPort": {"description": "Serve agent metrics (/metrics, /healthz, /readyz) on this host port (0 = off).",
                             "maximum": 65535, "minimum": 0, "type": "integer"},
         },

@@ -57,10 +57,11 @@ class AmdScaleOutSpec:
     nicDrivers: List[str] = field(default_factory=list)
     disableFirmwareLldp: bool = False
     metricsPort: int = 0
+    gpuDirectRdma: str = ""
     extra: Dict[str, Any] = field(default_factory=dict)
 
     _FIELDS = ("disableNetworkManager", "layer", "image", "pullPolicy", "mtu", "xgmiCheck", "lldpAnnounce",
-               "interfaces", "nicDrivers", "disableFirmwareLldp", "metricsPort")
+               "interfaces", "nicDrivers", "disableFirmwareLldp", "metricsPort", "gpuDirectRdma")
 
     def to_dict(self) -> dict:
         d: dict = {}
@@ -84,6 +85,8 @@ class AmdScaleOutSpec:
             d["disableFirmwareLldp"] = True
         if self.metricsPort:
             d["metricsPort"] = self.metricsPort
+        if self.gpuDirectRdma:
+            d["gpuDirectRdma"] = self.gpuDirectRdma
         d.update(copy.deepcopy(self.extra))
         return d
 
@@ -102,6 +105,7 @@ class AmdScaleOutSpec:
             nicDrivers=list(d.pop("nicDrivers", []) or []),
             disableFirmwareLldp=bool(d.pop("disableFirmwareLldp", False)),
             metricsPort=int(d.pop("metricsPort", 0) or 0),
+            gpuDirectRdma=d.pop("gpuDirectRdma", "") or "",
         )
         s.extra = d
         return s

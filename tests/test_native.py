@@ -188,3 +188,10 @@ def test_xgmi_allreduce_cli():
     assert "--ranks" in X.command(ranks=8)
     with pytest.raises(ValueError):
         X.command(mode="ring")
+
+
+def test_gdr_detection_binding(native, tmp_path):
+    assert native.detect_gdr(str(tmp_path), "6.8.0")["mode"] == "none"
+    (tmp_path / "module" / "ib_uverbs").mkdir(parents=True)
+    d = native.detect_gdr(str(tmp_path), "6.8.0")
+    assert d["mode"] == "dmabuf" and d["kernel"] == "6.8.0"

@@ -358,3 +358,13 @@ def test_agent_args_fw_lldp_and_metrics_port():
     update_amd_scale_out_daemonset(ds, p, "ns")
     assert "ports" not in c and "--disable-fw-lldp" not in c["args"]
     assert T.NetworkClusterPolicy.from_dict(p.to_dict()).spec.amdScaleOut.disableFirmwareLldp
+
+
+def test_agent_args_gpudirect_rdma():
+    from network_operator_amd.api.v1alpha1 import types as T
+    from network_operator_amd.operator.reconciler import agent_args
+
+    p = T.new_policy("p", layer="L3")
+    p.spec.amdScaleOut.gpuDirectRdma = "PeerMem"
+    assert "--require-gdr=peermem" in agent_args(p)
+    assert T.NetworkClusterPolicy.from_dict(p.to_dict()).spec.amdScaleOut.gpuDirectRdma == "PeerMem"
