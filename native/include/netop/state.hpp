@@ -40,6 +40,8 @@ struct NicState {
     std::string rdma_dev;
     int rdma_port = 1;
     std::optional<int> gid_index;
+    int numa_node = -1;     // NUMA node of the GPU (pin the rank's CPU threads there)
+    std::string pcie_path;  // GPU <-> NIC PCIe path type (PIX / PXB / ...)
 
     // NIC firmware LLDP agent (--disable-fw-lldp): summary of what was done
     std::string fw_lldp;

@@ -200,6 +200,8 @@ void Agent::get_network_configs(const std::vector<std::string>& names) {
             n.gpu_bdf = disc_.gpus[size_t(p.gpu)].pci.bdf;
             n.rdma_dev = nic.rdma_dev;
             n.rdma_port = nic.rdma_port;
+            n.numa_node = disc_.gpus[size_t(p.gpu)].pci.numa;
+            n.pcie_path = topo::to_string(p.path);
         }
         nics_.push_back(std::move(n));
     }

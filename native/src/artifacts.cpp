@@ -146,6 +146,8 @@ std::string generate_rccl_net(const std::vector<NicState>& nics, bool extended) 
                 j.key("RDMA_PORT").value(n->rdma_port);
             }
             if (n->gid_index) j.key("GID_INDEX").value(*n->gid_index);
+            if (n->numa_node >= 0) j.key("NUMA_NODE").value(n->numa_node);
+            if (!n->pcie_path.empty()) j.key("PCIE_PATH").value(n->pcie_path);
         }
         j.end_object();
     }

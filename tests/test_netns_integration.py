@@ -32,6 +32,7 @@ def _check_configured(r):
         assert e["NIC_IP"] == p["local"] and e["GATEWAY_IP"] == p["peer"]
         assert e["SUBNET_MASK"] == "255.255.255.252"
         assert e["GID_INDEX"] == 3 and e["RDMA_DEV"].startswith("mlx5_")
+        assert e["PCIE_PATH"] == "PXB" and e["NUMA_NODE"] == (0 if e["GPU_INDEX"] < 4 else 1)
     # GPU order: entry i belongs to GPU i.
     assert [e["GPU_INDEX"] for e in entries] == list(range(len(entries)))
 
