@@ -330,19 +330,28 @@ def run_isolated(timeout: float = 300, **kw) -> dict:
     return json.loads(r.stdout.strip().splitlines()[-1])
 
 
-def node_ready_bench(n_nics: int = 8, runs: int = 5, interval: str = "30s", seed: int = 1, legacy: bool = True) -> dict:
+def _pct(xs, q):
+    s = sorted(xs)
+    return s[min(len(s) - 1, max(0, int(round(q * (len(s) - 1)))))]
+
+
+def node_ready_bench(n_nics: int = 8, runs: int = 5, interval: str = "30s", seed: int = 1, legacy: bool = True,
+                     mode: str = "L3") -> dict:
     """Node-ready latency over `runs` fresh bring-ups, with (and optionally without) switch fast start."""
-    out = {"n_nics": n_nics, "runs": runs, "interval": interval}
+    out = {"n_nics": n_nics, "runs": runs, "interval": interval, "mode": mode}
     for label, fs in (("fast_start_switch", True), ("legacy_switch", False))[: 2 if legacy else 1]:
         lat, ref = [], []
         for k in range(runs):
-            r = run_isolated(n_nics=n_nics, seed=seed * 1000 + k, interval=interval, fast_start=fs, verbose=0)
+            r = run_isolated(n_nics=n_nics, seed=seed * 1000 + k, interval=interval, fast_start=fs, verbose=0,
+                             mode=mode)
             if not r["ready"]:
                 raise RuntimeError(f"run {k} did not become ready: {r['agent_log'][-2000:]}")
             lat.append(r["latency_s"])
             ref.append(r.get("reference_model_s"))
-        out[label] = {"latency_s": lat, "p50_s": statistics.median(lat), "max_s": max(lat),
-                      "reference_model_s": ref, "reference_model_p50_s": statistics.median([x for x in ref if x is not None])}
+        refs = [x for x in ref if x is not None]
+        out[label] = {"latency_s": lat, "p50_s": statistics.median(lat), "p95_s": _pct(lat, 0.95), "max_s": max(lat),
+                      "reference_model_s": ref,
+                      "reference_model_p50_s": statistics.median(refs) if refs else None}
     return out
 
 
