@@ -151,6 +151,7 @@ PYBIND11_MODULE(_netop_native, m) {
         .def("link_del", &nl::Rtnl::link_del)
         .def("link_set_netns_pid", &nl::Rtnl::link_set_netns_pid)
         .def("link_set_netns_fd", &nl::Rtnl::link_set_netns_fd)
+        .def("link_set_name", &nl::Rtnl::link_set_name)
         .def("round_trips", &nl::Rtnl::round_trips);
 
     m.def("lldp_send", [](const std::string& ifname, const py::bytes& frame) {

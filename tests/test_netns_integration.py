@@ -151,3 +151,19 @@ def test_crash_restart_without_shutdown_first_is_not_fast_started():
                            crash_after_s=5.0, wait="3s", extra_args=["--lldp-restart-fast=false"])
     assert r["stale_label_after_crash"]
     assert r["restart_latency_s"] is None
+
+
+def test_two_nodes_l3_fabric_carries_a_collective():
+    """BASELINE config "L3 mode, 2 nodes": two agents configure their nodes from one routing
+    switch; a gloo all-reduce then runs node A <-> node B over the scale-out /30s and /16 routes."""
+    from network_operator_amd.testing import twonode
+
+    r = twonode.run_isolated_two_nodes(n_nics=2, seed=7)
+    b = r["B"]
+    assert r["A_ready_s"] is not None and b["ready_s"] is not None, r.get("A_agent_log")
+    assert r["A_worker_rc"] == 0 and b["worker_rc"] == 0, (r.get("A_worker"), b.get("worker"))
+    assert r["A_worker"]["ok"] and b["worker"]["ok"]
+    # /16 via the switch port of every NIC, on both nodes.
+    for routes, plan in ((r["A_routes"], r["plan"][:2]), (b["routes"], r["plan"][2:])):
+        assert sorted(x["gateway"] for x in routes if x["dst"].endswith("/16")) == sorted(p["peer"] for p in plan)
+    assert r["A_agent_rc"] == 0 and b["agent_rc"] == 0
