@@ -13,7 +13,6 @@ Reference wiring (reference cmd/operator/main.go:117-167,219-226):
 
 from __future__ import annotations
 
-import asyncio
 import json
 import logging
 import ssl

@@ -13,7 +13,7 @@ import os
 import socket
 import struct
 import threading
-from typing import Dict, List, Optional, Tuple
+from typing import Dict, List, Tuple
 
 
 # ---------------------------------------------------------------------------
