@@ -71,6 +71,11 @@ class PolicyController:
             if owner and owner.get("kind") == T.KIND:
                 await self._enqueue(owner["name"])
 
+    async def requeue_all(self) -> None:
+        """Reconcile every policy again (e.g. after a cluster dependency appeared or vanished)."""
+        for p in self.policies.list():
+            await self.queue.add(p["metadata"]["name"])
+
     async def _enqueue(self, name: str) -> None:
         await self.queue.add(name)
         self.metrics.queue_adds.labels(CONTROLLER_NAME).inc()

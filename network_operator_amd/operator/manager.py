@@ -17,7 +17,7 @@ import logging
 import os
 import signal
 import sys
-from typing import List, Optional
+from typing import Dict, List, Optional
 
 from .controller import PolicyController
 from .kube import ApiClient, load_config
@@ -29,6 +29,47 @@ log = logging.getLogger("setup")
 
 DEFAULT_OPERATOR_NAMESPACE = "amd-network-operator"
 OPENSHIFT_GROUPS = ("route.openshift.io", "security.openshift.io")
+
+
+# Add-ons the operator depends on (reference README "Dependencies"), by API group.
+#   node-feature-discovery: the default nodeSelector label (gpu-ready) and the readiness label
+#                           (local feature files) are both NFD's; without it no node is ever
+#                           selected or reported ready.
+#   cert-manager:           serving certificates of the admission webhooks (kustomize / chart).
+DEPENDENCIES = {"node-feature-discovery": "nfd.k8s-sigs.io", "cert-manager": "cert-manager.io"}
+# Missing dependencies that break policies (surface in status.errors); the others are logged.
+POLICY_DEPENDENCIES = ("node-feature-discovery",)
+
+
+async def check_dependencies(client: ApiClient) -> Dict[str, bool]:
+    groups = set(await client.server_groups())
+    return {name: group in groups for name, group in DEPENDENCIES.items()}
+
+
+async def watch_dependencies(client: ApiClient, controller, metrics, stop: asyncio.Event, interval: float,
+                             webhooks: bool) -> None:
+    """Checks the cluster add-ons now and every `interval` seconds; on a change the policies are
+    reconciled again so their status reflects it."""
+    last: Optional[Dict[str, bool]] = None
+    while not stop.is_set():
+        try:
+            present = await check_dependencies(client)
+            for name, ok in present.items():
+                metrics.dependency.labels(name).set(1 if ok else 0)
+            if present != last:
+                for name, ok in present.items():
+                    if not ok and (name != "cert-manager" or webhooks):
+                        log.warning("dependency missing: %s (API group %s not served)", name, DEPENDENCIES[name])
+                controller.reconciler.missing_dependencies = [n for n in POLICY_DEPENDENCIES if not present.get(n, True)]
+                if last is not None:
+                    await controller.requeue_all()
+                last = present
+        except Exception as e:  # discovery hiccups must not stop the manager
+            log.debug("dependency check failed: %s", e)
+        try:
+            await asyncio.wait_for(stop.wait(), timeout=interval)
+        except asyncio.TimeoutError:
+            pass
 
 
 async def is_openshift(client: ApiClient) -> bool:
@@ -52,6 +93,8 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--webhook-port", type=int, default=9443)
     ap.add_argument("--webhook-cert-dir", default=DEFAULT_CERT_DIR)
     ap.add_argument("--workers", type=int, default=2, help="concurrent reconciles")
+    ap.add_argument("--dependency-check-interval", type=float, default=60.0,
+                    help="seconds between checks for Node Feature Discovery / cert-manager (0 = off)")
     ap.add_argument("--leader-election-id", default=DEFAULT_LEASE_ID)
     ap.add_argument("--zap-devel", action="store_true", default=True)
     ap.add_argument("--zap-log-level", default="info")
@@ -98,6 +141,18 @@ async def run(argv: Optional[List[str]] = None, stop: Optional[asyncio.Event] = 
         await servers.start(opts.health_probe_bind_address, opts.metrics_bind_address, opts.metrics_secure,
                             opts.webhook_port if webhooks else None, opts.webhook_cert_dir)
 
+        dep_task = None
+        if opts.dependency_check_interval > 0:
+            # First result before the controller starts, so the first status already has it.
+            try:
+                present = await check_dependencies(client)
+                controller.reconciler.missing_dependencies = [n for n in POLICY_DEPENDENCIES
+                                                             if not present.get(n, True)]
+            except Exception as e:
+                log.debug("dependency check failed: %s", e)
+            dep_task = asyncio.ensure_future(watch_dependencies(client, controller, metrics, stop,
+                                                                opts.dependency_check_interval, webhooks))
+
         async def lead() -> None:
             await controller.start()
             if started:
@@ -127,6 +182,8 @@ async def run(argv: Optional[List[str]] = None, stop: Optional[asyncio.Event] = 
             else:
                 await lead()
         finally:
+            if dep_task is not None:
+                dep_task.cancel()
             await controller.stop()
             await servers.stop()
         return 0

@@ -27,6 +27,8 @@ class OperatorMetrics:
         self.queue_adds = Counter("workqueue_adds_total", "Total number of adds handled by workqueue", ["name"], registry=r)
         self.queue_retries = Counter("workqueue_retries_total", "Total number of retries handled by workqueue", ["name"],
                                      registry=r)
+        self.dependency = Gauge("amd_network_operator_dependency_present",
+                                "1 if a cluster add-on the operator relies on is installed", ["dependency"], registry=r)
         self.leader = Gauge("leader_election_master_status", "1 if this instance is the leader", ["name"], registry=r)
         self.policy_targets = Gauge("amd_network_operator_policy_targets", "Nodes targeted by a NetworkClusterPolicy",
                                     ["policy"], registry=r)

@@ -213,6 +213,9 @@ class NetworkClusterPolicyReconciler:
         self.client = client
         self.namespace = namespace
         self.is_openshift = is_openshift
+        # Cluster add-ons the policy cannot work without (set by the manager's dependency check;
+        # the reference only lists them in its README).
+        self.missing_dependencies: List[str] = []
         self._get_policy = get_policy
         self._list_owned = list_owned
         self._list_pods = list_pods
@@ -307,7 +310,8 @@ class NetworkClusterPolicyReconciler:
         if cur.targets != targets or cur.ready != ready:
             updated = True
         new_state = status_for(targets, ready)
-        errors = self._node_errors(ds["metadata"]["name"]) if targets and ready < targets else []
+        errors = [f"dependency missing: {d}" for d in self.missing_dependencies]
+        errors += self._node_errors(ds["metadata"]["name"]) if targets and ready < targets else []
         if cur.state != new_state or cur.errors != errors:
             updated = True
         if not updated:

@@ -166,7 +166,8 @@ class FakeApiServer:
     STATUS_SUBRESOURCE = {kube.NETWORKCLUSTERPOLICIES, kube.DAEMONSETS}
 
     def __init__(self, openshift: bool = False, history: int = 10000, bookmark_interval: float = 1.0,
-                 gc_delay: float = 0.0, agent_ready_delay: Optional[float] = None):
+                 gc_delay: float = 0.0, agent_ready_delay: Optional[float] = None,
+                 extra_groups: Optional[List[str]] = None):
         self.resources: List[Resource] = list(kube.ALL_RESOURCES)
         self.openshift = openshift
         self.objects: Dict[Tuple[str, str, str], Dict[Tuple[str, str], dict]] = {}
@@ -178,6 +179,8 @@ class FakeApiServer:
         self.bookmark_interval = bookmark_interval
         self.gc_delay = gc_delay
         self.agent_ready_delay = agent_ready_delay
+        # API groups of add-ons installed in the fake cluster (e.g. "nfd.k8s-sigs.io").
+        self.extra_groups: List[str] = list(extra_groups or [])
         self.node_ready: Dict[Tuple[str, str], bool] = {}   # (ds ns/name, node) -> ready
         self.tokens: Dict[str, dict] = {}                    # bearer -> {"username", "groups", "allowed"}
         self.faults: List[_Fault] = []
@@ -489,6 +492,8 @@ class FakeApiServer:
                 groups.setdefault(r.group, [])
                 if r.version not in groups[r.group]:
                     groups[r.group].append(r.version)
+        for g in self.extra_groups:
+            groups.setdefault(g, ["v1"])
         if self.openshift:
             groups.setdefault("route.openshift.io", ["v1"])
             groups.setdefault("security.openshift.io", ["v1"])

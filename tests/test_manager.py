@@ -125,3 +125,43 @@ def test_openshift_detection_failure_exits_nonzero():
         return await manager.run(["--master", "http://127.0.0.1:1", "--health-probe-bind-address=0"])
 
     assert asyncio.run(body()) == 1
+
+
+def test_dependency_check_reports_missing_nfd(monkeypatch):
+    """Node Feature Discovery missing -> status.errors says so; once its API group is served the
+    policies are reconciled again and the error disappears (metric follows)."""
+    monkeypatch.setenv("OPERATOR_NAMESPACE", "netop-test")
+    monkeypatch.setenv("ENABLE_WEBHOOKS", "false")
+    probe, metrics = _free_port(), _free_port()
+
+    async def body():
+        fake = FakeApiServer(extra_groups=["cert-manager.io"])
+        url = await fake.start()
+        fake.add_node("n1", {"amd.feature.node.kubernetes.io/gpu-ready": "true"})
+        stop, started = asyncio.Event(), asyncio.Event()
+        task = asyncio.ensure_future(manager.run(
+            ["--master", url, f"--health-probe-bind-address=127.0.0.1:{probe}",
+             f"--metrics-bind-address=127.0.0.1:{metrics}", "--dependency-check-interval=0.2"],
+            stop=stop, started=started))
+        await asyncio.wait_for(started.wait(), 10)
+        async with ApiClient(KubeConfig(host=url)) as c:
+            await c.create(kube.NETWORKCLUSTERPOLICIES, T.new_policy("gpu-l3").to_dict())
+            await _until(lambda: fake.get_object(kube.DAEMONSETS, "gpu-l3", "netop-test") is not None)
+            fake.set_agent_ready("n1")
+
+            def errors():
+                return fake.get_object(kube.NETWORKCLUSTERPOLICIES, "gpu-l3")["status"]["errors"]
+
+            await _until(lambda: "dependency missing: node-feature-discovery" in errors())
+            async with aiohttp.ClientSession() as s:
+                async with s.get(f"http://127.0.0.1:{metrics}/metrics") as r:
+                    text = await r.text()
+            assert 'amd_network_operator_dependency_present{dependency="node-feature-discovery"} 0.0' in text
+            assert 'amd_network_operator_dependency_present{dependency="cert-manager"} 1.0' in text
+            fake.extra_groups.append("nfd.k8s-sigs.io")
+            await _until(lambda: errors() == [])
+        stop.set()
+        assert await asyncio.wait_for(task, 10) == 0
+        await fake.stop()
+
+    asyncio.run(body())
