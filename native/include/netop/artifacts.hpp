@@ -62,10 +62,12 @@ void delete_networkd(const std::string& dir, const std::vector<std::string>& ifn
 struct Labels {
     std::string dir = "/etc/kubernetes/node-feature-discovery/features.d/";
     std::string file = "scale-out-readiness.txt";
+    std::string key = "amd.feature.node.kubernetes.io/gpu-scale-out";  // published as "<key>=true"
     std::string path() const;
 };
 extern const char* const kScaleOutReadyLabel;  // "amd.feature.node.kubernetes.io/gpu-scale-out=true"
-std::string generate_labels(const std::map<std::string, std::string>& extra);
+std::string generate_labels(const std::map<std::string, std::string>& extra,
+                            const std::string& key = "amd.feature.node.kubernetes.io/gpu-scale-out");
 // Writes the label file only when the features.d directory exists (main.go:240).  Returns
 // true when written.
 bool write_labels(const Labels& l, const std::map<std::string, std::string>& extra);

@@ -55,7 +55,10 @@ struct GpuNicPair {
     int common_depth = 0;
 };
 
-enum class DiscoveryMode { Affine, Accel, None };
+// Affine: GPU-paired scale-out NICs.  Accel: reference layout (netdevs under the accelerator
+// function).  Rdma: every RDMA-capable NIC of the driver allow-list, no GPU pairing (the
+// host-nic configuration type).  None: --interfaces only.
+enum class DiscoveryMode { Affine, Accel, Rdma, None };
 std::optional<DiscoveryMode> parse_discovery_mode(std::string_view s);
 
 struct DiscoveryOptions {

@@ -203,6 +203,13 @@ void Agent::get_network_configs(const std::vector<std::string>& names) {
             n.numa_node = disc_.gpus[size_t(p.gpu)].pci.numa;
             n.pcie_path = topo::to_string(p.path);
         }
+        if (n.rdma_dev.empty())  // host NICs (rdma discovery): no GPU, but still an RDMA device
+            for (auto& nic : disc_.nics)
+                if (nic.ifname == name) {
+                    n.rdma_dev = nic.rdma_dev;
+                    n.rdma_port = nic.rdma_port;
+                    n.numa_node = nic.pci.numa;
+                }
         nics_.push_back(std::move(n));
     }
 }
@@ -698,12 +705,12 @@ void Agent::run(int stop_fd) {
         return;
     }
     int nconf = int(std::count_if(nics_.begin(), nics_.end(), [](const NicState& n) { return n.configured; }));
-    labels_extra_["amd.feature.node.kubernetes.io/gpu-scale-out.mode"] = cfg_.mode;
-    labels_extra_["amd.feature.node.kubernetes.io/gpu-scale-out.nics"] =
+    labels_extra_[cfg_.labels.key + ".mode"] = cfg_.mode;
+    labels_extra_[cfg_.labels.key + ".nics"] =
         std::to_string(cfg_.mode == "L3" ? nconf : int(nics_.size()));
     if (cfg_.xgmi_expect_links >= 0)
         labels_extra_["amd.feature.node.kubernetes.io/gpu-xgmi.pairs"] = std::to_string(xgmi_.pairs_connected);
-    if (!gdr_.kernel.empty()) labels_extra_["amd.feature.node.kubernetes.io/gpu-scale-out.gdr"] = gdr_.mode();
+    if (!gdr_.kernel.empty()) labels_extra_[cfg_.labels.key + ".gdr"] = gdr_.mode();
     try {
         if (publish_label()) NLOG_I("Published readiness label %s", cfg_.labels.path().c_str());
     } catch (const std::exception& e) {

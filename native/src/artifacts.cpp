@@ -235,15 +235,15 @@ const char* const kScaleOutReadyLabel = "amd.feature.node.kubernetes.io/gpu-scal
 
 std::string Labels::path() const { return path_join(dir, file); }
 
-std::string generate_labels(const std::map<std::string, std::string>& extra) {
-    std::string out = std::string(kScaleOutReadyLabel) + "\n";
+std::string generate_labels(const std::map<std::string, std::string>& extra, const std::string& key) {
+    std::string out = key + "=true\n";
     for (auto& [k, v] : extra) out += k + "=" + v + "\n";
     return out;
 }
 
 bool write_labels(const Labels& l, const std::map<std::string, std::string>& extra) {
     if (!is_dir(l.dir)) return false;
-    write_file_atomic(l.path(), generate_labels(extra), 0644);
+    write_file_atomic(l.path(), generate_labels(extra, l.key), 0644);
     return true;
 }
 

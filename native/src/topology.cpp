@@ -29,6 +29,7 @@ const char* to_string(PathType p) {
 std::optional<DiscoveryMode> parse_discovery_mode(std::string_view s) {
     if (s == "affine" || s.empty()) return DiscoveryMode::Affine;
     if (s == "accel") return DiscoveryMode::Accel;
+    if (s == "rdma") return DiscoveryMode::Rdma;
     if (s == "none") return DiscoveryMode::None;
     return std::nullopt;
 }
@@ -195,6 +196,14 @@ DiscoveryResult discover(const DiscoveryOptions& opt, const std::string& root) {
     if (opt.mode == DiscoveryMode::None) return r;
     if (opt.mode == DiscoveryMode::Accel) {
         r.ifnames = accel_netdevs(root, opt.accel_driver);
+        return r;
+    }
+    if (opt.mode == DiscoveryMode::Rdma) {
+        for (auto& n : discover_pci_nics(root, opt.nic_drivers))
+            if (!n.rdma_dev.empty()) {
+                r.ifnames.push_back(n.ifname);
+                r.nics.push_back(std::move(n));
+            }
         return r;
     }
     r.gpus = discover_gpus(root, opt.accel_driver);

@@ -161,3 +161,26 @@ TEST(topology_gdr_detection) {
     CHECK(topo::kernel_at_least("5.12.0", 5, 12) && !topo::kernel_at_least("5.11.22", 5, 12));
     CHECK(topo::kernel_at_least("10.0", 5, 12) && !topo::kernel_at_least("garbage", 5, 12));
 }
+
+TEST(topology_rdma_mode_lists_host_rdma_nics) {
+    TmpDir t;
+    // Two mlx5 NICs with RDMA devices, one without (plain Ethernet function), one foreign driver.
+    auto nic = [&](const char* bdf, const char* ifname, const char* driver, const char* rdma) {
+        std::string dev = std::string("pci0000:00/0000:00:01.0/") + bdf;
+        pci(t, dev, driver, "0x15b3", "0x1021", 0);
+        netdev(t, dev, ifname, "02:00:00:00:01:01");
+        if (rdma) t.mkdir("devices/" + dev + "/infiniband/" + rdma);
+    };
+    nic("0000:01:00.0", "ens1f0np0", "mlx5_core", "mlx5_0");
+    nic("0000:01:00.1", "ens1f1np1", "mlx5_core", "mlx5_1");
+    nic("0000:02:00.0", "eno1", "mlx5_core", nullptr);
+    nic("0000:03:00.0", "eth7", "e1000e", nullptr);
+    DiscoveryOptions o;
+    o.mode = DiscoveryMode::Rdma;
+    auto r = discover(o, t.path);
+    CHECK_EQ(r.ifnames.size(), size_t(2));
+    CHECK_EQ(r.ifnames[0], std::string("ens1f0np0"));
+    CHECK_EQ(r.nics[1].rdma_dev, std::string("mlx5_1"));
+    CHECK(r.pairs.empty() && r.gpus.empty());
+    CHECK(parse_discovery_mode("rdma") == DiscoveryMode::Rdma);
+}

@@ -46,7 +46,7 @@ int main(int argc, char** argv) {
     fs.add_string("systemd-networkd", &cfg.networkd, "Write systemd networkd configuration files to given directory");
     fs.add_int("mtu", &cfg.mtu, "MTU value to set for interfaces");
 
-    fs.add_string("nic-discovery", &discovery_mode, "scale-out NIC discovery: affine (NICs sharing a PCIe switch with an amdgpu GPU), accel (netdevs under the accelerator PCI function), none");
+    fs.add_string("nic-discovery", &discovery_mode, "scale-out NIC discovery: affine (NICs sharing a PCIe switch with an amdgpu GPU), accel (netdevs under the accelerator PCI function), rdma (every RDMA-capable NIC of --nic-drivers: host NICs), none");
     fs.add_string("accel-driver", &cfg.discovery.accel_driver, "accelerator PCI driver to enumerate");
     fs.add_string("nic-drivers", &nic_drivers, "comma separated NIC driver allow-list for affine discovery (default: common RoCE drivers)");
     fs.add_string("max-path", &max_path, "farthest GPU<->NIC PCIe path type accepted: PIX, PXB, PHB, NODE, SYS");
@@ -56,6 +56,7 @@ int main(int argc, char** argv) {
     fs.add_bool("label-without-peers", &cfg.label_without_peers, "publish the readiness label even when no LLDP peer was found (reference behaviour)");
     fs.add_string("nfd-features-dir", &cfg.labels.dir, "NFD local feature source directory");
     fs.add_string("nfd-label-file", &cfg.labels.file, "readiness label file name inside the features directory");
+    fs.add_string("nfd-label", &cfg.labels.key, "readiness label key (published as KEY=true; KEY.mode, KEY.nics, ... alongside)");
     fs.add_string("rccl-env", &cfg.rccl_env, "write an RCCL environment file (NCCL_IB_HCA, NCCL_IB_GID_INDEX, ...)");
     fs.add_string("status-file", &cfg.status_file, "write a JSON status document (per-NIC results, phase timings)");
     fs.add_string("nm-keyfile-dir", &cfg.nm_keyfile_dir, "with --disable-networkmanager, also persist an unmanaged-devices keyfile here");

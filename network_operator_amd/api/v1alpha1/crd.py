@@ -70,15 +70,40 @@ def openapi_schema() -> dict:
                             "maximum": 65535, "minimum": 0, "type": "integer"},
         },
     }
+    host_nic = {
+        "description": "HostNic configures the node's own RDMA NICs (not paired with a GPU); used with\n"
+                       "configurationType host-nic.",
+        "type": "object",
+        "properties": {
+            "layer": {"description": "L2: links up only; L3: LLDP-driven /30 addressing.", "enum": list(T.LAYERS),
+                      "type": "string"},
+            "mtu": {"description": "MTU for the host NICs.", "maximum": T.MTU_MAX, "minimum": T.MTU_MIN,
+                    "type": "integer"},
+            "image": {"description": "Container image of the link-discovery agent.", "type": "string"},
+            "pullPolicy": {"description": "Image pull policy of the agent and driver containers.",
+                           "enum": list(T.PULL_POLICIES), "type": "string"},
+            "disableNetworkManager": {"description": "Take the host NICs away from NetworkManager.",
+                                      "type": "boolean"},
+            "interfaces": {"description": "Host NICs to configure (default: every RDMA NIC of nicDrivers).",
+                           "items": {"type": "string", "maxLength": 15}, "type": "array"},
+            "nicDrivers": {"description": "NIC driver allow-list for RDMA NIC discovery.",
+                           "items": {"type": "string"}, "type": "array"},
+            "driverImage": {"description": "Optional NIC kernel-driver (KMD) container, run as a privileged init\n"
+                                           "container before the agent; it must load the driver and exit 0.",
+                            "type": "string"},
+        },
+        "required": ["layer"],
+    }
     spec = {
         "description": "NetworkClusterPolicySpec defines the desired state of NetworkClusterPolicy",
         "type": "object",
         "properties": {
             "configurationType": {
-                "description": "Configuration type that the operator will configure to the nodes. Possible options: amd-so.\n"
-                               "Reserved for future use: host-nic",
+                "description": "Configuration type that the operator will configure to the nodes. Possible options:\n"
+                               "amd-so (GPU scale-out NICs), host-nic (the node's own RDMA NICs)",
                 "enum": list(T.CONFIGURATION_TYPES), "type": "string"},
             "amdScaleOut": amd_so,
+            "hostNic": host_nic,
             "logLevel": {"description": "LogLevel sets the agent's log level.", "maximum": T.LOG_LEVEL_MAX,
                          "minimum": T.LOG_LEVEL_MIN, "type": "integer"},
             "nodeSelector": {"additionalProperties": {"type": "string"},

@@ -7,7 +7,8 @@ renamed for MI355X:
 =====================================  ==============================================
 reference                              this API
 =====================================  ==============================================
-configurationType enum ``gaudi-so``    ``amd-so`` (``host-nic`` reserved, types.go:26)
+configurationType enum ``gaudi-so``    ``amd-so``; ``host-nic`` (the reference's TODO, types.go:26,
+                                       README "Future work") implemented as spec.hostNic
 spec.gaudiScaleOut                     spec.amdScaleOut (same sub-fields)
 status {targets, ready, state, errors} identical
 =====================================  ==============================================
@@ -35,7 +36,8 @@ PLURAL = "networkclusterpolicies"
 SINGULAR = "networkclusterpolicy"
 
 CONFIG_AMD_SCALE_OUT = "amd-so"
-CONFIGURATION_TYPES = (CONFIG_AMD_SCALE_OUT,)
+CONFIG_HOST_NIC = "host-nic"
+CONFIGURATION_TYPES = (CONFIG_AMD_SCALE_OUT, CONFIG_HOST_NIC)
 LAYERS = ("L2", "L3")
 PULL_POLICIES = ("Never", "Always", "IfNotPresent")
 MTU_MIN, MTU_MAX = 1500, 9000
@@ -112,10 +114,53 @@ class AmdScaleOutSpec:
 
 
 @dataclass
+class HostNicSpec:
+    """``host-nic``: the node's own RDMA NICs (frontend / storage / scale-out NICs not paired
+    with a GPU), configured by the same agent in ``--nic-discovery=rdma`` mode, optionally after
+    a driver container installed the NIC's kernel driver (KMD)."""
+    layer: str = ""
+    mtu: int = 0
+    image: str = ""
+    pullPolicy: str = ""
+    disableNetworkManager: bool = False
+    interfaces: List[str] = field(default_factory=list)
+    nicDrivers: List[str] = field(default_factory=list)
+    driverImage: str = ""
+    extra: Dict[str, Any] = field(default_factory=dict)
+
+    def to_dict(self) -> dict:
+        d: dict = {}
+        for k in ("layer", "image", "pullPolicy", "driverImage"):
+            if getattr(self, k):
+                d[k] = getattr(self, k)
+        if self.mtu:
+            d["mtu"] = self.mtu
+        if self.disableNetworkManager:
+            d["disableNetworkManager"] = True
+        if self.interfaces:
+            d["interfaces"] = list(self.interfaces)
+        if self.nicDrivers:
+            d["nicDrivers"] = list(self.nicDrivers)
+        d.update(copy.deepcopy(self.extra))
+        return d
+
+    @classmethod
+    def from_dict(cls, d: Optional[dict]) -> "HostNicSpec":
+        d = dict(d or {})
+        s = cls(layer=d.pop("layer", "") or "", mtu=int(d.pop("mtu", 0) or 0), image=d.pop("image", "") or "",
+                pullPolicy=d.pop("pullPolicy", "") or "", disableNetworkManager=bool(d.pop("disableNetworkManager", False)),
+                interfaces=list(d.pop("interfaces", []) or []), nicDrivers=list(d.pop("nicDrivers", []) or []),
+                driverImage=d.pop("driverImage", "") or "")
+        s.extra = d
+        return s
+
+
+@dataclass
 class NetworkClusterPolicySpec:
     configurationType: str = ""
     nodeSelector: Dict[str, str] = field(default_factory=dict)
     amdScaleOut: AmdScaleOutSpec = field(default_factory=AmdScaleOutSpec)
+    hostNic: Optional[HostNicSpec] = None
     logLevel: int = 0
     extra: Dict[str, Any] = field(default_factory=dict)
 
@@ -125,6 +170,8 @@ class NetworkClusterPolicySpec:
             d["nodeSelector"] = dict(self.nodeSelector)
         so = self.amdScaleOut.to_dict()
         d["amdScaleOut"] = so  # struct without omitempty pointer: always serialised
+        if self.hostNic is not None:
+            d["hostNic"] = self.hostNic.to_dict()
         if self.logLevel:
             d["logLevel"] = self.logLevel
         d.update(copy.deepcopy(self.extra))
@@ -137,6 +184,7 @@ class NetworkClusterPolicySpec:
             configurationType=d.pop("configurationType", "") or "",
             nodeSelector=dict(d.pop("nodeSelector", {}) or {}),
             amdScaleOut=AmdScaleOutSpec.from_dict(d.pop("amdScaleOut", None)),
+            hostNic=HostNicSpec.from_dict(d.pop("hostNic")) if d.get("hostNic") is not None else None,
             logLevel=int(d.pop("logLevel", 0) or 0),
         )
         s.extra = d
@@ -203,3 +251,13 @@ def new_policy(name: str, layer: str = "L3", node_selector: Optional[dict] = Non
                                       nodeSelector=dict({"amd.feature.node.kubernetes.io/gpu-ready": "true"}
                                                         if node_selector is None else node_selector),
                                       amdScaleOut=AmdScaleOutSpec(layer=layer, **so)))
+
+
+def new_host_nic_policy(name: str, layer: str = "L3", node_selector: Optional[dict] = None,
+                        **hn) -> NetworkClusterPolicy:
+    return NetworkClusterPolicy(
+        metadata={"name": name},
+        spec=NetworkClusterPolicySpec(configurationType=CONFIG_HOST_NIC,
+                                      nodeSelector=dict({"amd.feature.node.kubernetes.io/gpu-ready": "true"}
+                                                        if node_selector is None else node_selector),
+                                      hostNic=HostNicSpec(layer=layer, **hn)))

@@ -66,6 +66,9 @@ def default(policy: T.NetworkClusterPolicy) -> T.NetworkClusterPolicy:
     log.info("default name=%s", policy.name)
     if policy.spec.configurationType == T.CONFIG_AMD_SCALE_OUT and not policy.spec.amdScaleOut.image:
         policy.spec.amdScaleOut.image = T.DEFAULT_AGENT_IMAGE
+    if policy.spec.configurationType == T.CONFIG_HOST_NIC and policy.spec.hostNic is not None \
+            and not policy.spec.hostNic.image:
+        policy.spec.hostNic.image = T.DEFAULT_AGENT_IMAGE
     return policy
 
 
@@ -99,10 +102,29 @@ def validate_amd_so_spec(s: T.AmdScaleOutSpec) -> List[str]:
     return warnings
 
 
+class MissingHostNicSpecError(ValidationError):
+    message = "configurationType host-nic needs spec.hostNic with a layer"
+
+
+def validate_host_nic_spec(s: Optional[T.HostNicSpec]) -> List[str]:
+    if s is None or s.layer not in T.LAYERS:
+        raise MissingHostNicSpecError()
+    for i in s.interfaces:
+        if not i or len(i) > 15 or "/" in i or " " in i or "," in i:
+            raise InvalidInterfaceError(i)
+    warnings = []
+    if not s.interfaces and not s.nicDrivers:
+        warnings.append("hostNic: no interfaces or nicDrivers given; every RDMA NIC of the default driver list "
+                        "will be configured")
+    return warnings
+
+
 def validate_spec(spec: T.NetworkClusterPolicySpec) -> List[str]:
     validate_node_selector(spec.nodeSelector)
     if spec.configurationType == T.CONFIG_AMD_SCALE_OUT:
         return validate_amd_so_spec(spec.amdScaleOut)
+    if spec.configurationType == T.CONFIG_HOST_NIC:
+        return validate_host_nic_spec(spec.hostNic)
     raise UnknownConfigurationError()
 
 

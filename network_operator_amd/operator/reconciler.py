@@ -159,9 +159,18 @@ def update_amd_scale_out_daemonset(ds: dict, p: T.NetworkClusterPolicy, namespac
     if so.layer == "L3":
         add_host_volume(ds, "rccl-artifacts", ARTIFACT_DIR_HOST, ARTIFACT_DIR_CONTAINER)
         wanted.add("rccl-artifacts")
-    for v in MANAGED_VOLUMES:
+    for v in MANAGED_VOLUMES + ("host-lib-modules",):
         if v not in wanted:
             remove_volume(ds, v)
+    # A policy that switched from host-nic: no driver container, default readiness probe.
+    inits = [x for x in pod.get("initContainers", []) if x.get("name") != "nic-driver"]
+    if inits:
+        pod["initContainers"] = inits
+    else:
+        pod.pop("initContainers", None)
+    probe = c.get("readinessProbe", {}).get("exec")
+    if probe:
+        probe["command"] = probe["command"][:1] + ["--ready-check"]
     # Agent metrics port (hostNetwork: the container port is the node port).
     ports = [x for x in c.get("ports", []) if x.get("name") != "metrics"]
     if so.metricsPort:
@@ -171,6 +180,87 @@ def update_amd_scale_out_daemonset(ds: dict, p: T.NetworkClusterPolicy, namespac
     else:
         c.pop("ports", None)
     c["args"] = agent_args(p)
+
+
+HOST_NIC_LABEL = "amd.feature.node.kubernetes.io/host-nic-ready"
+HOST_NIC_LABEL_FILE = "host-nic-readiness.txt"
+DRIVER_CONTAINER = "nic-driver"
+
+
+def host_nic_agent_args(p: T.NetworkClusterPolicy) -> List[str]:
+    """Agent flags for ``host-nic``: RDMA NIC discovery instead of GPU affinity, its own readiness
+    label and file (so it can coexist with an ``amd-so`` policy on the same node)."""
+    hn = p.spec.hostNic or T.HostNicSpec()
+    args = ["--configure=true", "--keep-running", f"--mode={hn.layer}",
+            "--nic-discovery=" + ("none" if hn.interfaces else "rdma"),
+            f"--nfd-label-file={HOST_NIC_LABEL_FILE}", f"--nfd-label={HOST_NIC_LABEL}"]
+    if p.spec.logLevel > 0:
+        args.append(f"--v={p.spec.logLevel}")
+    if hn.mtu > 0:
+        args.append(f"--mtu={hn.mtu}")
+    if hn.disableNetworkManager:
+        args += ["--disable-networkmanager", "--nm-keyfile-dir=/etc/NetworkManager/conf.d"]
+    if hn.layer == "L3":
+        args.append(f"--wait={L3_WAIT}")
+    if hn.interfaces:
+        args.append("--interfaces=" + ",".join(hn.interfaces))
+    if hn.nicDrivers:
+        args.append("--nic-drivers=" + ",".join(hn.nicDrivers))
+    return args
+
+
+def update_host_nic_daemonset(ds: dict, p: T.NetworkClusterPolicy, namespace: str) -> None:
+    """The ``host-nic`` branch (the reference's "Future work": Host-NIC use + KMD install)."""
+    hn = p.spec.hostNic or T.HostNicSpec()
+    md = ds.setdefault("metadata", {})
+    md["name"] = p.name
+    md["namespace"] = namespace
+    pod = ds["spec"]["template"]["spec"]
+    if p.spec.nodeSelector:
+        pod["nodeSelector"] = dict(p.spec.nodeSelector)
+    c = pod["containers"][0]
+    if hn.image:
+        c["image"] = hn.image
+    if hn.pullPolicy:
+        c["imagePullPolicy"] = hn.pullPolicy
+    wanted = set()
+    if hn.disableNetworkManager:
+        add_host_volume(ds, "var-run-dbus", "/var/run/dbus", "/var/run/dbus")
+        add_host_volume(ds, "networkmanager", "/etc/NetworkManager", "/etc/NetworkManager")
+        wanted |= {"var-run-dbus", "networkmanager"}
+    # Optional kernel-driver container: privileged, sees the host's modules, runs to completion
+    # before the agent starts (init container), so the NICs exist when discovery runs.
+    inits = [x for x in pod.get("initContainers", []) if x.get("name") != DRIVER_CONTAINER]
+    if hn.driverImage:
+        spec_vols = pod.setdefault("volumes", [])
+        if not any(v.get("name") == "host-lib-modules" for v in spec_vols):
+            spec_vols.append({"name": "host-lib-modules", "hostPath": {"path": "/lib/modules", "type": "Directory"}})
+        wanted.add("host-lib-modules")
+        inits.append({"name": DRIVER_CONTAINER, "image": hn.driverImage,
+                      "imagePullPolicy": hn.pullPolicy or "IfNotPresent",
+                      "securityContext": {"privileged": True},
+                      "volumeMounts": [{"name": "host-lib-modules", "mountPath": "/lib/modules"}]})
+    if inits:
+        pod["initContainers"] = inits
+    else:
+        pod.pop("initContainers", None)
+    for v in MANAGED_VOLUMES + ("host-lib-modules",):
+        if v not in wanted:
+            remove_volume(ds, v)
+    probe = c.get("readinessProbe", {}).get("exec")
+    if probe:
+        probe["command"] = [probe["command"][0], "--ready-check", f"--nfd-label-file={HOST_NIC_LABEL_FILE}"]
+    c["args"] = host_nic_agent_args(p)
+
+
+def update_daemonset_for(ds: dict, p: T.NetworkClusterPolicy, namespace: str) -> None:
+    """createDaemonSet / updateDaemonSet dispatch on configurationType (:243-265)."""
+    if p.spec.configurationType == T.CONFIG_AMD_SCALE_OUT:
+        update_amd_scale_out_daemonset(ds, p, namespace)
+    elif p.spec.configurationType == T.CONFIG_HOST_NIC:
+        update_host_nic_daemonset(ds, p, namespace)
+    else:
+        raise ValueError(f"unknown configuration type {p.spec.configurationType!r}")
 
 
 def status_for(targets: int, ready: int) -> str:
@@ -266,16 +356,16 @@ class NetworkClusterPolicyReconciler:
                 log.error("unable to create role binding: %s", e)
 
     async def _create_daemonset(self, raw: dict, p: T.NetworkClusterPolicy) -> Result:
-        if p.spec.configurationType != T.CONFIG_AMD_SCALE_OUT:
+        if p.spec.configurationType not in T.CONFIGURATION_TYPES:
             log.info("Unknown configuration type, this shouldn't happen! type=%s", p.spec.configurationType)
             raise ValueError(f"unknown configuration type {p.spec.configurationType!r}")
         ds = discovery.discovery_daemonset()
         sa_name = p.name + "-sa" if self.is_openshift else ""
         if sa_name:
             ds["spec"]["template"]["spec"]["serviceAccountName"] = sa_name
-        update_amd_scale_out_daemonset(ds, p, self.namespace)
+        update_daemonset_for(ds, p, self.namespace)
         set_controller_reference(raw, ds)
-        log.info("Creating AMD scale-out DaemonSet name=%s", p.name)
+        log.info("Creating %s DaemonSet name=%s", p.spec.configurationType, p.name)
         try:
             created = await self.client.create(kube.DAEMONSETS, ds, namespace=self.namespace)
         except ApiError as e:
@@ -292,9 +382,7 @@ class NetworkClusterPolicyReconciler:
     # -- update ----------------------------------------------------------------------------------
     async def _update(self, raw: dict, p: T.NetworkClusterPolicy, ds: dict) -> Result:
         original = copy.deepcopy(ds)
-        if p.spec.configurationType != T.CONFIG_AMD_SCALE_OUT:
-            raise ValueError(f"unknown configuration type {p.spec.configurationType!r}")
-        update_amd_scale_out_daemonset(ds, p, self.namespace)
+        update_daemonset_for(ds, p, self.namespace)
         if original["spec"]["template"]["spec"] != ds["spec"]["template"]["spec"]:
             log.info("DS difference for %s", p.name)
             ds = await self.client.replace(kube.DAEMONSETS, ds)

@@ -95,8 +95,11 @@ def test_empty_and_unknown():
     with pytest.raises(W.EmptyNodeSelectorError):
         W.validate_create(_p({}))
     with pytest.raises(W.UnknownConfigurationError) as ei:
-        W.validate_create(_p(ctype="host-nic"))
+        W.validate_create(_p(ctype="gaudi-so"))
     assert str(ei.value) == "unknown error"
+    # host-nic (reserved in the reference) is implemented here and needs spec.hostNic.
+    with pytest.raises(W.MissingHostNicSpecError):
+        W.validate_create(_p(ctype="host-nic"))
 
 
 @pytest.mark.parametrize("sel", [

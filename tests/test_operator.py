@@ -368,3 +368,55 @@ def test_agent_args_gpudirect_rdma():
     p.spec.amdScaleOut.gpuDirectRdma = "PeerMem"
     assert "--require-gdr=peermem" in agent_args(p)
     assert T.NetworkClusterPolicy.from_dict(p.to_dict()).spec.amdScaleOut.gpuDirectRdma == "PeerMem"
+
+
+def test_host_nic_daemonset_branch():
+    """configurationType host-nic (the reference's future-work branch): RDMA NIC discovery, its own
+    label/file + readinessProbe, optional privileged KMD init container; switching back cleans up."""
+    from network_operator_amd.api.v1alpha1 import types as T
+    from network_operator_amd.discovery import discovery_daemonset
+    from network_operator_amd.operator.reconciler import update_daemonset_for
+
+    p = T.new_host_nic_policy("storage", layer="L3", mtu=9000, nicDrivers=["mlx5_core"],
+                              driverImage="registry/nic-kmd:6.8", pullPolicy="Always")
+    ds = discovery_daemonset()
+    update_daemonset_for(ds, p, "ns")
+    pod = ds["spec"]["template"]["spec"]
+    c = pod["containers"][0]
+    assert c["args"][:6] == ["--configure=true", "--keep-running", "--mode=L3", "--nic-discovery=rdma",
+                             "--nfd-label-file=host-nic-readiness.txt",
+                             "--nfd-label=amd.feature.node.kubernetes.io/host-nic-ready"]
+    assert "--mtu=9000" in c["args"] and "--nic-drivers=mlx5_core" in c["args"] and "--wait=90s" in c["args"]
+    assert not any(a.startswith("--rccl-net") for a in c["args"])
+    assert c["readinessProbe"]["exec"]["command"][1:] == ["--ready-check", "--nfd-label-file=host-nic-readiness.txt"]
+    init = pod["initContainers"][0]
+    assert init["name"] == "nic-driver" and init["securityContext"]["privileged"] and init["imagePullPolicy"] == "Always"
+    assert any(v["name"] == "host-lib-modules" for v in pod["volumes"])
+    # Explicit interfaces: no discovery, just those.
+    p.spec.hostNic.interfaces = ["ens1f0np0"]
+    p.spec.hostNic.driverImage = ""
+    update_daemonset_for(ds, p, "ns")
+    assert "--nic-discovery=none" in c["args"] and "--interfaces=ens1f0np0" in c["args"]
+    assert "initContainers" not in pod and all(v["name"] != "host-lib-modules" for v in pod["volumes"])
+    # Back to amd-so: default probe, scale-out args.
+    q = T.new_policy("storage", layer="L3")
+    update_daemonset_for(ds, q, "ns")
+    assert c["readinessProbe"]["exec"]["command"][1:] == ["--ready-check"]
+    assert any(a.startswith("--rccl-net") for a in c["args"])
+
+
+def test_host_nic_webhook_rules():
+    import pytest
+
+    from network_operator_amd.api.v1alpha1 import types as T
+    from network_operator_amd.api.v1alpha1 import webhook as W
+
+    p = T.new_host_nic_policy("h", layer="L2")
+    W.default(p)
+    assert p.spec.hostNic.image == T.DEFAULT_AGENT_IMAGE
+    assert W.validate_create(p)  # warning: no interfaces / drivers
+    p.spec.hostNic = None
+    with pytest.raises(W.MissingHostNicSpecError):
+        W.validate_create(p)
+    rt = T.NetworkClusterPolicy.from_dict(T.new_host_nic_policy("h", driverImage="x").to_dict())
+    assert rt.spec.configurationType == "host-nic" and rt.spec.hostNic.driverImage == "x"

@@ -114,7 +114,8 @@ def test_kustomize_default_build():
 def test_kustomize_manifests_and_samples_validate():
     docs = kustomize_build(ROOT / "config/operator/manifests")
     crs = _by_kind(docs, "NetworkClusterPolicy")
-    assert {c["spec"]["amdScaleOut"]["layer"] for c in crs} == {"L2", "L3"}
+    assert {c["spec"].get("amdScaleOut", c["spec"].get("hostNic", {}))["layer"] for c in crs} == {"L2", "L3"}
+    assert {c["spec"]["configurationType"] for c in crs} == {"amd-so", "host-nic"}
     for c in crs:
         assert CRD.validate(c) == []
         assert W.validate_create(T.NetworkClusterPolicy.from_dict(c)) == []
@@ -170,7 +171,7 @@ def test_olm_bundle_matches_installer(tmp_path):
     assert {h["type"] for h in hooks} == {"MutatingAdmissionWebhook", "ValidatingAdmissionWebhook"}
     assert all(h["rules"][0]["resources"] == ["networkclusterpolicies"] for h in hooks)  # plural (fix)
     examples = json.loads(csv["metadata"]["annotations"]["alm-examples"])
-    assert {e["spec"]["amdScaleOut"]["layer"] for e in examples} == {"L2", "L3"}
+    assert {e["spec"]["configurationType"] for e in examples} == {"amd-so", "host-nic"}
     ann = b["metadata"]["annotations.yaml"]["annotations"]
     assert ann["operators.operatorframework.io.bundle.package.v1"] == "amd-network-operator"
     files = packaging.write_bundle(tmp_path / "bundle")
@@ -201,3 +202,16 @@ def test_ci_workflows_parse_and_cover_reference_jobs():
     steps = " ".join(str(s.get("run", "")) for s in ci["build-test"]["steps"])
     for target in ("sanitize", "vet", "build-installer", "bundle", "helm-package-chart"):
         assert target in steps, target
+
+
+def test_helm_host_nic_policy():
+    docs = helm_template(ROOT / "charts" / "network-operator",
+                         {"config": {"hostNic": {"enabled": True, "mode": "L3", "driverImage": "r/kmd:1"}}})
+    hn = [d for d in docs if d.get("kind") == "NetworkClusterPolicy"]
+    assert len(hn) == 1 and hn[0]["spec"]["configurationType"] == "host-nic"
+    assert hn[0]["spec"]["hostNic"]["layer"] == "L3" and hn[0]["spec"]["hostNic"]["driverImage"] == "r/kmd:1"
+    from network_operator_amd.api.v1alpha1 import crd as CRD_
+
+    assert CRD_.validate(hn[0]) == []
+    with pytest.raises(RenderError):
+        helm_template(ROOT / "charts" / "network-operator", {"config": {"hostNic": {"enabled": True, "mode": "L4"}}})
