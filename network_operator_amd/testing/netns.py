@@ -232,6 +232,12 @@ def run_scenario(n_nics: int = 8, mode: str = "L3", seed: int | None = None, int
                      "interval": interval, "pipeline": pipeline, "plan": plan, "nics": nic_names}
         res["ready"] = t_ready is not None
         res["latency_s"] = (t_ready - t0) if t_ready else None
+        try:  # resource envelope (the DaemonSet requests 45Mi / limits 90Mi, like the reference)
+            st = Path(f"/proc/{agent.pid}/status").read_text()
+            res["agent_rss_kib"] = int(next(x for x in st.splitlines() if x.startswith("VmHWM:")).split()[1])
+            res["agent_threads"] = int(next(x for x in st.splitlines() if x.startswith("Threads:")).split()[1])
+        except (OSError, StopIteration, ValueError):
+            res["agent_rss_kib"] = None
         if first_periodic:
             res["reference_model_s"] = max(0.0, max(first_periodic.values()) - t0)
         # Inspect the configured node.

@@ -165,3 +165,41 @@ def test_dependency_check_reports_missing_nfd(monkeypatch):
         await fake.stop()
 
     asyncio.run(body())
+
+
+def test_operator_memory_within_deployment_limit(tmp_path):
+    """The manager (+ the in-process fake API server, 50 nodes, 10 policies) stays far below the
+    Deployment's 128Mi limit (reference config/operator/manager/manager.yaml:95-101)."""
+    import subprocess
+    import sys
+    import textwrap
+
+    script = tmp_path / "rss.py"
+    script.write_text(textwrap.dedent('''
+        import asyncio, os, resource
+        from network_operator_amd.operator import manager, kube
+        from network_operator_amd.operator.kube import ApiClient, KubeConfig
+        from network_operator_amd.testing.fakeapi import FakeApiServer
+        from network_operator_amd.api.v1alpha1 import types as T
+        os.environ["ENABLE_WEBHOOKS"] = "false"
+        async def main():
+            fake = FakeApiServer(); url = await fake.start()
+            for i in range(50):
+                fake.add_node(f"n{i}", {"amd.feature.node.kubernetes.io/gpu-ready": "true"})
+            stop, started = asyncio.Event(), asyncio.Event()
+            t = asyncio.ensure_future(manager.run(["--master", url, "--health-probe-bind-address=127.0.0.1:0",
+                                                   "--metrics-bind-address=127.0.0.1:0"], stop=stop, started=started))
+            await started.wait()
+            async with ApiClient(KubeConfig(host=url)) as c:
+                for i in range(10):
+                    await c.create(kube.NETWORKCLUSTERPOLICIES, T.new_policy(f"p{i}").to_dict())
+            await asyncio.sleep(1.5)
+            stop.set(); await t; await fake.stop()
+            print(resource.getrusage(resource.RUSAGE_SELF).ru_maxrss // 1024)
+        asyncio.run(main())
+    '''))
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, str(script)], capture_output=True, text=True, timeout=120,
+                       env=dict(os.environ, PYTHONPATH=root))
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert int(r.stdout.strip().splitlines()[-1]) < 100, r.stdout

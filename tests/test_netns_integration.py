@@ -52,6 +52,8 @@ def test_l3_fast_start_switch_full_node():
         assert r["after_sigterm"][nic] == {"up": False, "addrs": []}
     st = r["status"]
     assert st["ready"] and all(i["configured"] for i in st["interfaces"])
+    # Resource envelope: far inside the DaemonSet's 45Mi request (reference daemonset.yaml:37-43).
+    assert r["agent_rss_kib"] is not None and r["agent_rss_kib"] < 16 * 1024
 
 
 def test_l3_legacy_switch_periodic_only():
