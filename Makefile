@@ -9,7 +9,7 @@ VERSION ?= 0.1.0
 BUNDLE_IMG ?= amd/amd-network-operator-bundle:v$(VERSION)
 
 .PHONY: all help build native hip test test-native test-netns test-gpu manifests deployments bench bench-node-ready \
-        images sanitize clean fmt vet lint fuzz run build-installer install uninstall deploy undeploy bundle \
+        images sanitize tsan clean fmt vet lint fuzz run build-installer install uninstall deploy undeploy bundle \
         bundle-build helm-package-chart
 
 all: build
@@ -41,6 +41,10 @@ test-gpu:                   ## on an MI355X box
 sanitize:                   ## host-side ASan+UBSan build of the agent and its unit suite
 	cmake -S native -B _build-asan -G Ninja -DNETOP_SANITIZE=ON -DNETOP_PYTHON=OFF -DNETOP_OUT=$(CURDIR)/_build-asan/out && \
 	cmake --build _build-asan -j$(JOBS) && _build-asan/out/bin/netop-unit-tests
+
+tsan:                       ## ThreadSanitizer build of the agent and its unit suite (metrics thread)
+	cmake -S native -B _build-tsan -G Ninja -DNETOP_TSAN=ON -DNETOP_PYTHON=OFF -DNETOP_OUT=$(CURDIR)/_build-tsan/out && \
+	cmake --build _build-tsan -j$(JOBS) && TSAN_OPTIONS=halt_on_error=1 _build-tsan/out/bin/netop-unit-tests
 
 manifests:                  ## regenerate the CRD (kustomize base + Helm chart copy)
 	$(PYTHON) -m network_operator_amd.api.v1alpha1.crd
