@@ -42,6 +42,45 @@ def _free_port() -> int:
     return p
 
 
+def _rccl_autotune(rank: int, world: int, nbytes: int, started: float = time.time()) -> dict:
+    """RCCL parameters are read once per process, at communicator creation, so they have to be
+    chosen before init_process_group.  Rank 0 measures the knob variants of
+    ``rccl_bench.ENV_PROBES`` with the native harness over the node's first `world` GPUs (a fresh
+    process per variant).  It publishes the winner through a file in /tmp keyed by the rendezvous
+    port, and every rank exports it.  A variant must beat the defaults by >= 3 % to be used."""
+    path = f"/tmp/netop-rccl-autotune-{os.environ.get('MASTER_PORT', '0')}.json"
+    if rank == 0:
+        from network_operator_amd.parallel import rccl_bench
+
+        probes = rccl_bench.env_probe(world, nbytes)
+        base = next((p.get("busbw_GBps") for p in probes if p["env"] == {}), None) or 0.0
+        best = max((p for p in probes if p.get("busbw_GBps")), key=lambda p: p["busbw_GBps"], default=None)
+        chosen = best["env"] if best and base and best["busbw_GBps"] >= 1.03 * base else {}
+        doc = {"created": time.time(), "chosen": chosen, "baseline_busbw_GBps": base, "probes": probes}
+        tmp = path + f".{os.getpid()}"
+        with open(tmp, "w") as f:
+            json.dump(doc, f)
+        os.replace(tmp, path)
+    else:
+        deadline = time.time() + 600
+        doc = None
+        while time.time() < deadline:
+            try:
+                with open(path) as f:
+                    d = json.load(f)
+                if d.get("created", 0) >= started - 30:  # not a stale file from an earlier run
+                    doc = d
+                    break
+            except (OSError, ValueError):
+                pass
+            time.sleep(0.2)
+        if doc is None:
+            return {"error": "rank 0 published no autotune result", "chosen": {}}
+    for k, v in doc["chosen"].items():
+        os.environ[k] = v
+    return doc
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1)
@@ -55,6 +94,9 @@ def main(argv=None) -> int:
                     help="other collectives reported at --bytes (n > 1 only)")
     ap.add_argument("--xgmi-probe", type=int, default=1, help="run the HIP xGMI link probe on rank 0 (n > 1)")
     ap.add_argument("--native-rccl", type=int, default=1, help="also run the native netop-rccl-bench harness on rank 0")
+    ap.add_argument("--rccl-autotune", type=int, default=0,
+                    help="n > 1: before RCCL starts, rank 0 measures RCCL knob variants with the native harness "
+                         "and every rank uses the fastest (>= 3%% better than defaults) for the run")
     ap.add_argument("--xgmi-allreduce", type=int, default=1,
                     help="also run the direct two-shot xGMI all-reduce on rank 0 (n > 1)")
     # CPU rehearsal of the multi-rank path (tests): gloo backend, fp32 on the host.
@@ -83,6 +125,7 @@ def main(argv=None) -> int:
             return 2
         torch.cuda.set_device(local_rank)
         device, dtype = torch.device("cuda", local_rank), torch.bfloat16
+        tuned = _rccl_autotune(rank, world, args.bytes) if args.rccl_autotune and world > 1 else None
         dist.init_process_group("nccl", rank=rank, world_size=world, device_id=device)
     # Host-side group for waiting while rank 0 runs its extra GPU tools: an RCCL barrier would
     # leave a spinning kernel on every other GPU and disturb what those tools measure.
@@ -230,6 +273,7 @@ def main(argv=None) -> int:
             "collectives": others,
             "xgmi_probe": probe,
             "native_rccl": native,
+            "rccl_autotune": tuned if args.device == "cuda" else None,
             "xgmi_allreduce": direct,
             "algbw_GBps": algbw,
             "busbw_GBps": busbw,
