@@ -10,6 +10,8 @@
 //   * netop_copy — 16-B/lane streaming copy used by the xGMI link probe: with peer access
 //     enabled the loads of a peer pointer travel over the xGMI link to that peer, so one
 //     copy per peer on its own stream drives all 7 links of an MI355X concurrently.
+//   * netop_sum_bf16 — n-way bf16 sum with fp32 accumulation (the reduce-scatter step of the
+//     direct xGMI all-reduce, sources are peer pointers there).
 //
 // No CUDA/hipify heritage: plain HIP for gfx950, 256-thread workgroups (4 waves), grids
 // sized as a multiple of the 256 CUs.
@@ -110,6 +112,76 @@ __global__ __launch_bounds__(kThreads) void copy_kernel(const uint4* __restrict_
     for (uint64_t v = uint64_t(blockIdx.x) * kThreads + threadIdx.x; v < n_vec; v += stride) dst[v] = src[v];
 }
 
+// ---- n-way bf16 sum (reduce-scatter step of the direct xGMI all-reduce) ----------------------
+constexpr int kMaxSrc = 8;
+struct SrcPtrs {
+    const uint4* p[kMaxSrc];
+};
+
+__device__ __forceinline__ void add_bf16x8(float (&acc)[8], const uint4& v) {
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        acc[2 * k] += __uint_as_float(w[k] << 16);
+        acc[2 * k + 1] += __uint_as_float(w[k] & 0xffff0000u);
+    }
+}
+
+__device__ __forceinline__ uint32_t pack_bf16x2_rne(float a, float b) {
+    uint32_t ua = __float_as_uint(a), ub = __float_as_uint(b);
+    // NaN stays NaN (quiet), everything else rounds to nearest even.
+    ua = (ua & 0x7fffffffu) > 0x7f800000u ? (ua | 0x00400000u) : ua + 0x7fffu + ((ua >> 16) & 1u);
+    ub = (ub & 0x7fffffffu) > 0x7f800000u ? (ub | 0x00400000u) : ub + 0x7fffu + ((ub >> 16) & 1u);
+    return (ua >> 16) | (ub & 0xffff0000u);
+}
+
+// dst[i] = Σ_s src[s][i] in fp32 (s = 0..NSRC-1, in order), bf16 RNE out.  All NSRC x UNROLL
+// 16-B loads of a lane are issued before the adds: with peer pointers those are remote xGMI
+// reads, and having many in flight per lane is what hides the link round trip.
+template <int NSRC, int UNROLL>
+__global__ __launch_bounds__(kThreads) void sum_bf16_kernel(SrcPtrs src, uint4* __restrict__ dst, uint64_t n_vec) {
+    const uint64_t stride = uint64_t(gridDim.x) * kThreads * UNROLL;
+    for (uint64_t base = uint64_t(blockIdx.x) * kThreads * UNROLL + threadIdx.x; base < n_vec; base += stride) {
+        uint4 v[UNROLL][NSRC];
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u) {
+            const uint64_t i = base + uint64_t(u) * kThreads;
+            if (i < n_vec) {
+#pragma unroll
+                for (int s = 0; s < NSRC; ++s) v[u][s] = src.p[s][i];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u) {
+            const uint64_t i = base + uint64_t(u) * kThreads;
+            if (i >= n_vec) continue;
+            float acc[8] = {};
+#pragma unroll
+            for (int s = 0; s < NSRC; ++s) add_bf16x8(acc, v[u][s]);
+            dst[i] = make_uint4(pack_bf16x2_rne(acc[0], acc[1]), pack_bf16x2_rne(acc[2], acc[3]),
+                                pack_bf16x2_rne(acc[4], acc[5]), pack_bf16x2_rne(acc[6], acc[7]));
+        }
+    }
+}
+
+using SumFn = void (*)(SrcPtrs, uint4*, uint64_t);
+template <int N>
+SumFn sum_for() {
+    return sum_bf16_kernel<N, 2>;
+}
+SumFn sum_fn(int n) {
+    switch (n) {
+        case 1: return sum_for<1>();
+        case 2: return sum_for<2>();
+        case 3: return sum_for<3>();
+        case 4: return sum_for<4>();
+        case 5: return sum_for<5>();
+        case 6: return sum_for<6>();
+        case 7: return sum_for<7>();
+        default: return sum_for<8>();
+    }
+}
+
 int grid_for(uint64_t n_vec, int per_cu = 8) {
     // CU count per device, cached: hipGetDeviceProperties is far too slow for a launch path.
     static int cached[64] = {};
@@ -172,6 +244,24 @@ int netop_fill_expected_sum(void* buf, uint64_t n_elems, uint32_t seed, int worl
 int netop_verify_sum(const void* buf, uint64_t n_elems, uint32_t seed, int world, unsigned long long* errors,
                      hipStream_t stream) {
     return netop_verify_pattern_at(buf, n_elems, seed, 0, world, 0, errors, stream);
+}
+
+// dst = Σ srcs (bf16, fp32 accumulation in source order, RNE).  1 <= nsrc <= 8; sizes in bf16
+// elements, multiple of 8; all pointers 16-byte aligned (sources may be peer pointers).
+// wg_per_cu <= 0 selects the default (4 workgroups per CU).
+int netop_sum_bf16(const void* const* srcs, int nsrc, void* dst, uint64_t n_elems, int wg_per_cu, hipStream_t stream) {
+    if (nsrc < 1 || nsrc > kMaxSrc || (n_elems & 7) || (reinterpret_cast<uintptr_t>(dst) & 15))
+        return int(hipErrorInvalidValue);
+    SrcPtrs p{};
+    for (int s = 0; s < nsrc; ++s) {
+        if (!srcs[s] || (reinterpret_cast<uintptr_t>(srcs[s]) & 15)) return int(hipErrorInvalidValue);
+        p.p[s] = static_cast<const uint4*>(srcs[s]);
+    }
+    const uint64_t nv = n_elems / 8;
+    if (nv == 0) return int(hipSuccess);
+    hipLaunchKernelGGL(sum_fn(nsrc), dim3(grid_for((nv + 1) / 2, wg_per_cu > 0 ? wg_per_cu : 4)), dim3(kThreads), 0,
+                       stream, p, static_cast<uint4*>(dst), nv);
+    return int(hipGetLastError());
 }
 
 int netop_copy(const void* src, void* dst, uint64_t bytes, hipStream_t stream) {

@@ -42,6 +42,7 @@ int netop_fill_pattern_at(void* buf, uint64_t n_elems, uint32_t seed, int rank_l
                           hipStream_t stream);
 int netop_verify_pattern_at(const void* buf, uint64_t n_elems, uint32_t seed, int rank_lo, int n_ranks,
                             uint64_t elem_offset, unsigned long long* errors, hipStream_t stream);
+int netop_sum_bf16(const void* const* srcs, int nsrc, void* dst, uint64_t n_elems, int wg_per_cu, hipStream_t stream);
 }
 
 namespace {
@@ -65,76 +66,12 @@ struct DstPtrs {
     uint4* p[kMaxRanks];
 };
 
-__device__ __forceinline__ void add_bf16x8(float (&acc)[8], const uint4& v) {
-    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        acc[2 * k] += __uint_as_float(w[k] << 16);
-        acc[2 * k + 1] += __uint_as_float(w[k] & 0xffff0000u);
-    }
-}
-
-__device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
-    // Round to nearest even (inputs here are finite).
-    uint32_t ua = __float_as_uint(a), ub = __float_as_uint(b);
-    ua += 0x7fffu + ((ua >> 16) & 1u);
-    ub += 0x7fffu + ((ub >> 16) & 1u);
-    return (ua >> 16) | (ub & 0xffff0000u);
-}
-
-// dst[i] = Σ_s src[s][i], bf16 in, fp32 accumulate, bf16 out.  All NSRC 16-byte loads of
-// an element group are issued before any add, so each lane has NSRC (x UNROLL) remote loads
-// in flight, which hides the xGMI round trip.
-template <int NSRC, int UNROLL>
-__global__ __launch_bounds__(kThreads) void reduce_kernel(Ptrs src, uint4* __restrict__ dst, uint64_t n_vec) {
-    const uint64_t stride = uint64_t(gridDim.x) * kThreads * UNROLL;
-    for (uint64_t base = uint64_t(blockIdx.x) * kThreads * UNROLL + threadIdx.x; base < n_vec; base += stride) {
-        uint4 v[UNROLL][NSRC];
-#pragma unroll
-        for (int u = 0; u < UNROLL; ++u) {
-            uint64_t i = base + uint64_t(u) * kThreads;
-            if (i < n_vec) {
-#pragma unroll
-                for (int s = 0; s < NSRC; ++s) v[u][s] = src.p[s][i];
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < UNROLL; ++u) {
-            uint64_t i = base + uint64_t(u) * kThreads;
-            if (i >= n_vec) continue;
-            float acc[8] = {};
-#pragma unroll
-            for (int s = 0; s < NSRC; ++s) add_bf16x8(acc, v[u][s]);
-            dst[i] = make_uint4(pack_bf16x2(acc[0], acc[1]), pack_bf16x2(acc[2], acc[3]), pack_bf16x2(acc[4], acc[5]),
-                                pack_bf16x2(acc[6], acc[7]));
-        }
-    }
-}
-
 // Several independent copies in one launch: blockIdx.y selects the (src, dst) pair.
 __global__ __launch_bounds__(kThreads) void multi_copy_kernel(Ptrs src, DstPtrs dst, uint64_t n_vec) {
     const uint4* __restrict__ s = src.p[blockIdx.y];
     uint4* __restrict__ d = dst.p[blockIdx.y];
     const uint64_t stride = uint64_t(gridDim.x) * kThreads;
     for (uint64_t i = uint64_t(blockIdx.x) * kThreads + threadIdx.x; i < n_vec; i += stride) d[i] = s[i];
-}
-
-using ReduceFn = void (*)(Ptrs, uint4*, uint64_t);
-template <int N>
-ReduceFn reduce_for() {
-    return reduce_kernel<N, 2>;
-}
-ReduceFn reduce_fn(int n) {
-    switch (n) {
-        case 1: return reduce_for<1>();
-        case 2: return reduce_for<2>();
-        case 3: return reduce_for<3>();
-        case 4: return reduce_for<4>();
-        case 5: return reduce_for<5>();
-        case 6: return reduce_for<6>();
-        case 7: return reduce_for<7>();
-        default: return reduce_for<8>();
-    }
 }
 
 struct Rank {
@@ -302,8 +239,11 @@ class Node {
         return int(std::max<uint64_t>(1, std::min(need, cap)));
     }
     void launch_reduce(Rank& r, const Ptrs& src, uint4* dst, uint64_t cvec) {
-        hipLaunchKernelGGL(reduce_fn(n_), dim3(grid(r, cvec / 2)), dim3(kThreads), 0, r.stream, src, dst, cvec);
-        HIPCHECK(hipGetLastError());
+        // The n-way sum is the library kernel (libnetop_hip.so: netop_sum_bf16), numerics-tested
+        // against PyTorch; here its sources are peer pointers.
+        const void* srcs[kMaxRanks];
+        for (int s = 0; s < n_; ++s) srcs[s] = src.p[s];
+        HIPCHECK(hipError_t(netop_sum_bf16(srcs, n_, dst, cvec * 8, per_cu_, r.stream)));
     }
     void gather_pull(int d, uint64_t chunk, uint64_t cvec) {
         if (n_ == 1) return;

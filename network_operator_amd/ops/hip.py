@@ -38,6 +38,8 @@ def lib() -> ctypes.CDLL:
             L.netop_fill_pattern_at.restype = i32
             L.netop_verify_pattern_at.argtypes = [vp, u64, u32, i32, i32, u64, vp, vp]
             L.netop_verify_pattern_at.restype = i32
+            L.netop_sum_bf16.argtypes = [ctypes.POINTER(vp), i32, vp, u64, i32, vp]
+            L.netop_sum_bf16.restype = i32
             L.netop_copy.argtypes = [vp, vp, u64, vp]
             L.netop_copy.restype = i32
             L.netop_xgmi_probe.argtypes = [u64, i32, i32, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
@@ -117,6 +119,20 @@ def verify_pattern_at(t, seed: int, rank_lo: int, n_ranks: int = 1, elem_offset:
                                          elem_offset, ctypes.c_void_p(err.data_ptr()), _stream(t)),
            "netop_verify_pattern_at")
     return int(err.item())
+
+
+def sum_bf16(srcs, out, wg_per_cu: int = 0) -> None:
+    """``out = Σ srcs`` for 1..8 bf16 tensors of equal size: fp32 accumulation in list order,
+    round-to-nearest-even to bf16 (the reduce step of the direct xGMI all-reduce)."""
+    if not 1 <= len(srcs) <= 8:
+        raise ValueError("1..8 sources")
+    for t in (*srcs, out):
+        _check_buf(t)
+        if t.numel() != out.numel():
+            raise ValueError("all tensors must have the same number of elements")
+    arr = (ctypes.c_void_p * len(srcs))(*[t.data_ptr() for t in srcs])
+    _check(lib().netop_sum_bf16(arr, len(srcs), ctypes.c_void_p(out.data_ptr()), out.numel(), wg_per_cu, _stream(out)),
+           "netop_sum_bf16")
 
 
 def copy(src, dst) -> None:

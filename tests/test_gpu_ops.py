@@ -155,3 +155,38 @@ def test_xgmi_probe_push_loopback(cuda_device):
     r = hip.xgmi_probe_push(32 << 20, iters=3)
     assert r["gpus"] >= 1 and r["errors"] == 0
     assert r["push_aggregate_GBps"][0] > 100
+
+
+@pytest.mark.parametrize("nsrc", [1, 2, 3, 8])
+def test_sum_bf16_matches_torch_fp32(cuda_device, nsrc):
+    """n-way bf16 sum (fp32 accumulation, RNE) against a PyTorch fp32 reference of the same op."""
+    import torch
+
+    from network_operator_amd.ops import hip
+
+    g = torch.Generator(device="cpu").manual_seed(nsrc)
+    n = (1 << 20) + 64
+    srcs_cpu = [torch.randn(n, generator=g).to(torch.bfloat16) for _ in range(nsrc)]
+    srcs = [s.to(cuda_device) for s in srcs_cpu]
+    out = torch.empty(n, dtype=torch.bfloat16, device=cuda_device)
+    hip.sum_bf16(srcs, out)
+    torch.cuda.synchronize()
+    acc = torch.zeros(n, dtype=torch.float32)
+    for s in srcs_cpu:  # same order as the kernel: exact match expected
+        acc += s.float()
+    torch.testing.assert_close(out.cpu(), acc.to(torch.bfloat16), rtol=0, atol=0)
+    # and within bf16 rounding of an order-independent fp64 reference
+    ref = torch.stack([s.double() for s in srcs_cpu]).sum(0)
+    torch.testing.assert_close(out.cpu().double(), ref, rtol=2 ** -7, atol=1e-6)
+
+
+def test_sum_bf16_rejects_bad_args(cuda_device):
+    import torch
+
+    from network_operator_amd.ops import hip
+
+    a = torch.zeros(16, dtype=torch.bfloat16, device=cuda_device)
+    with pytest.raises(ValueError):
+        hip.sum_bf16([a] * 9, a)
+    with pytest.raises(ValueError):
+        hip.sum_bf16([a, torch.zeros(24, dtype=torch.bfloat16, device=cuda_device)], a)
