@@ -176,7 +176,7 @@ def test_operator_memory_within_deployment_limit(tmp_path):
 
     script = tmp_path / "rss.py"
     script.write_text(textwrap.dedent('''
-        import asyncio, os, resource
+        import asyncio, os
         from network_operator_amd.operator import manager, kube
         from network_operator_amd.operator.kube import ApiClient, KubeConfig
         from network_operator_amd.testing.fakeapi import FakeApiServer
@@ -195,7 +195,10 @@ def test_operator_memory_within_deployment_limit(tmp_path):
                     await c.create(kube.NETWORKCLUSTERPOLICIES, T.new_policy(f"p{i}").to_dict())
             await asyncio.sleep(1.5)
             stop.set(); await t; await fake.stop()
-            print(resource.getrusage(resource.RUSAGE_SELF).ru_maxrss // 1024)
+            # VmHWM, not ru_maxrss: the latter survives execve and would report the forking
+            # (pytest) parent's high-water mark.
+            hwm = next(l for l in open("/proc/self/status") if l.startswith("VmHWM:"))
+            print(int(hwm.split()[1]) // 1024)
         asyncio.run(main())
     '''))
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
