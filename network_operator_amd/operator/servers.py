@@ -13,8 +13,10 @@ Reference wiring (reference cmd/operator/main.go:117-167,219-226):
 
 from __future__ import annotations
 
+import asyncio
 import json
 import logging
+import os
 import ssl
 import subprocess
 import time
@@ -42,6 +44,56 @@ def server_tls_context(cert_file: str, key_file: str) -> ssl.SSLContext:
     ctx.set_alpn_protocols(["http/1.1"])
     ctx.load_cert_chain(cert_file, key_file)
     return ctx
+
+
+class CertWatcher:
+    """Reloads a serving certificate into a live SSLContext when its files change
+    (controller-runtime's certwatcher): cert-manager rotates the webhook certificate in place,
+    and an operator that kept the old one would start failing admission once it expires.
+    New handshakes use the new pair; established connections keep theirs."""
+
+    def __init__(self, ctx: ssl.SSLContext, cert_file: str, key_file: str, interval: float = 10.0):
+        self.ctx, self.cert_file, self.key_file, self.interval = ctx, cert_file, key_file, interval
+        self.reloads = 0
+        self._stamp = self._read_stamp()
+        self._task: Optional[asyncio.Task] = None
+
+    def _read_stamp(self):
+        try:
+            return tuple((os.stat(f).st_mtime_ns, os.stat(f).st_size, os.stat(f).st_ino)
+                         for f in (self.cert_file, self.key_file))
+        except OSError:
+            return None
+
+    def check(self) -> bool:
+        """Reloads if the files changed since the last successful load; True when reloaded."""
+        stamp = self._read_stamp()
+        if stamp is None or stamp == self._stamp:
+            return False
+        try:
+            self.ctx.load_cert_chain(self.cert_file, self.key_file)
+        except (ssl.SSLError, OSError) as e:  # half-written pair: retry at the next tick
+            log.warning("certificate reload failed (will retry): %s", e)
+            return False
+        self._stamp = stamp
+        self.reloads += 1
+        log.info("reloaded serving certificate %s", self.cert_file)
+        return True
+
+    def start(self) -> None:
+        async def loop():
+            while True:
+                await asyncio.sleep(self.interval)
+                self.check()
+        self._task = asyncio.ensure_future(loop())
+
+    async def stop(self) -> None:
+        if self._task:
+            self._task.cancel()
+            try:
+                await self._task
+            except asyncio.CancelledError:
+                pass
 
 
 def generate_self_signed(cert_dir: Path, cn: str = "localhost", sans=("DNS:localhost", "IP:127.0.0.1")) -> Tuple[Path, Path]:
@@ -100,6 +152,9 @@ class Servers:
         self.client = client
         self.runners: list = []
         self.ports: Dict[str, int] = {}
+        self.cert_watcher: Optional[CertWatcher] = None  # the webhook's
+        self.watchers: list = []
+        self.cert_reload_interval = 10.0
 
     # -- apps ------------------------------------------------------------------------------------
     def probes_app(self) -> web.Application:
@@ -174,13 +229,24 @@ class Servers:
                 if not (cd / "tls.crt").exists():
                     generate_self_signed(cd)  # controller-runtime also self-signs the metrics cert
                 ctx = server_tls_context(str(cd / "tls.crt"), str(cd / "tls.key"))
+                self._watch(ctx, cd)
             await self._serve("metrics", self.metrics_app(metrics_secure), *b, ssl_ctx=ctx)
         if webhook_port is not None:
             cd = Path(cert_dir)
             ctx = server_tls_context(str(cd / "tls.crt"), str(cd / "tls.key"))
             await self._serve("webhook", self.webhook_app(), "0.0.0.0", webhook_port, ssl_ctx=ctx)
+            self.cert_watcher = self._watch(ctx, cd)
+
+    def _watch(self, ctx: ssl.SSLContext, cert_dir: Path) -> CertWatcher:
+        w = CertWatcher(ctx, str(cert_dir / "tls.crt"), str(cert_dir / "tls.key"), self.cert_reload_interval)
+        w.start()
+        self.watchers.append(w)
+        return w
 
     async def stop(self) -> None:
+        for w in self.watchers:
+            await w.stop()
+        self.watchers.clear()
         for r in self.runners:
             await r.cleanup()
         self.runners.clear()

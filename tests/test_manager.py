@@ -206,3 +206,40 @@ def test_operator_memory_within_deployment_limit(tmp_path):
                        env=dict(os.environ, PYTHONPATH=root))
     assert r.returncode == 0, r.stderr[-2000:]
     assert int(r.stdout.strip().splitlines()[-1]) < 100, r.stdout
+
+
+def test_webhook_certificate_rotation_is_picked_up(tmp_path):
+    """cert-manager rewrites tls.crt/tls.key in place; the webhook server must serve the new
+    certificate without a restart (controller-runtime certwatcher)."""
+    import hashlib
+
+    from network_operator_amd.operator.metrics import OperatorMetrics
+    from network_operator_amd.operator.servers import Servers, generate_self_signed
+
+    generate_self_signed(tmp_path)
+
+    async def peer_cert(port):
+        ctx = ssl.create_default_context()
+        ctx.check_hostname = False
+        ctx.verify_mode = ssl.CERT_NONE
+        _, w = await asyncio.open_connection("127.0.0.1", port, ssl=ctx)
+        der = w.get_extra_info("ssl_object").getpeercert(binary_form=True)
+        w.close()
+        return hashlib.sha256(der).hexdigest()
+
+    async def body():
+        s = Servers(OperatorMetrics())
+        s.cert_reload_interval = 0.05
+        await s.start(probe_addr="0", webhook_port=0, cert_dir=str(tmp_path))
+        port = s.ports["webhook"]
+        first = await peer_cert(port)
+        generate_self_signed(tmp_path, cn="rotated")
+        for _ in range(100):
+            await asyncio.sleep(0.05)
+            if s.cert_watcher.reloads:
+                break
+        second = await peer_cert(port)
+        await s.stop()
+        assert s.cert_watcher.reloads >= 1 and first != second
+
+    asyncio.run(body())
