@@ -60,6 +60,9 @@ struct Config {
     std::string nm_keyfile_dir;          // --nm-keyfile-dir
     int xgmi_expect_links = -1;          // -1 off; 0 = full mesh among discovered GPUs; N = exact pairs
     int64_t link_wait_ns = 3LL * 1000000000;  // netlink echo wait (network.go:251)
+    // The RDMA core adds the RoCE v2 GID of a new IPv4 address asynchronously (netdev notifier
+    // -> GID cache work item); wait this long for it before writing rccl.env without a GID.
+    int64_t gid_wait_ns = 3LL * 1000000000;
     bool lldp_announce = true;           // transmit our own LLDPDU (triggers switch fast start)
     int64_t announce_interval_ns = 1000000000LL;  // re-announce to still-silent NICs
     int announce_count = 3;

@@ -457,10 +457,23 @@ void Agent::detect_lldp(int stop_fd) {
 
 void Agent::write_artifacts() {
     std::string root = cfg_.sysfs_root.empty() ? topo::sysfs_root() : cfg_.sysfs_root;
-    for (auto& n : nics_) {
-        if (n.rdma_dev.empty() || !n.addr) continue;
-        n.gid_index = topo::find_rocev2_gid_index(root, n.rdma_dev, n.rdma_port, n.addr->local);
+    // Poll all configured RDMA NICs together until each has its RoCE v2 GID or the wait ends.
+    const int64_t gid_deadline = mono_ns() + cfg_.gid_wait_ns;
+    for (;;) {
+        bool missing = false;
+        for (auto& n : nics_) {
+            if (n.rdma_dev.empty() || !n.addr || !n.configured || n.gid_index) continue;
+            n.gid_index = topo::find_rocev2_gid_index(root, n.rdma_dev, n.rdma_port, n.addr->local);
+            missing |= !n.gid_index;
+        }
+        if (!missing || mono_ns() >= gid_deadline) break;
+        ::usleep(2000);
     }
+    for (auto& n : nics_)
+        if (!n.rdma_dev.empty() && n.addr && n.configured && !n.gid_index)
+            NLOG_W("%s (%s): no RoCE v2 GID for %s after %s; rccl.env gets no NCCL_IB_GID_INDEX for it",
+                   n.ifname.c_str(), n.rdma_dev.c_str(), n.addr->local.str().c_str(),
+                   format_go_duration(cfg_.gid_wait_ns).c_str());
     if (!cfg_.rccl_net.empty()) {
         try {
             artifacts::write_rccl_net(cfg_.rccl_net, nics_);
@@ -814,6 +827,7 @@ void Agent::monitor(int stop_fd) {
                     NLOG_W("could not remove old address of '%s': %s", ifname.c_str(), e.what());
                 }
                 n.configured = false;
+                n.gid_index.reset();  // the GID follows the address
                 if (n.addr) configure_interface(n);
                 ++reconfigs_;
                 changed = true;

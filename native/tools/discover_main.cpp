@@ -62,6 +62,7 @@ int main(int argc, char** argv) {
     fs.add_string("nm-keyfile-dir", &cfg.nm_keyfile_dir, "with --disable-networkmanager, also persist an unmanaged-devices keyfile here");
     fs.add_int("xgmi-expect", &cfg.xgmi_expect_links, "verify the xGMI mesh before labelling: -1 off, 0 full mesh, N GPU pairs");
     fs.add_duration("link-wait", &cfg.link_wait_ns, "time to wait for link state echoes from the kernel");
+    fs.add_duration("gid-wait", &cfg.gid_wait_ns, "time to wait for the RoCE v2 GID of a newly configured address");
     fs.add_bool("lldp-announce", &cfg.lldp_announce, "transmit our own LLDPDU on each NIC (makes 802.1AB-2009 switches answer within ~1s)");
     fs.add_bool("lldp-restart-fast", &cfg.announce_shutdown_first, "send a shutdown LLDPDU before the first announcement so a switch holding a stale entry (agent restart) fast-starts again");
     fs.add_string("node-name", &cfg.node_name, "LLDP System Name (default $NODE_NAME, else the hostname)");

@@ -137,7 +137,7 @@ def run_scenario(n_nics: int = 8, mode: str = "L3", seed: int | None = None, int
                  mtu: int = 9000, pipeline: bool = True, bad_nics: int = 0, silent_nics: int = 0,
                  xgmi_expect: int = 0, keep_tmp: bool = False, sigterm: bool = True, verbose: int = 2,
                  drop_xgmi: list | None = None, extra_args: list | None = None, flap_port: int | None = None,
-                 crash_restart: bool = False, crash_after_s: float = 0.0) -> dict:
+                 crash_restart: bool = False, crash_after_s: float = 0.0, gid_delay_s: float = 0.0) -> dict:
     """Runs one node bring-up.  Must already be inside a private user+net namespace."""
     from . import fakesysfs
 
@@ -160,10 +160,23 @@ def run_scenario(n_nics: int = 8, mode: str = "L3", seed: int | None = None, int
         rdma = {n["ifname"]: "" for n in fx["nics"]}
         # GID tables as mlx5 would populate them once the address is configured.
         disc = nat.discover(str(tmp / "sys"))
+        gid_jobs = []
         for n in disc["nics"]:
             if n["ifname"] in nic_names and n["rdma_dev"]:
-                fakesysfs.add_rocev2_gids(tmp / "sys", n["rdma_dev"], [plan[nic_names.index(n["ifname"])]["local"]])
+                gid_jobs.append((n["rdma_dev"], plan[nic_names.index(n["ifname"])]["local"]))
                 rdma[n["ifname"]] = n["rdma_dev"]
+
+        def add_gids():
+            for dev, ip in gid_jobs:
+                fakesysfs.add_rocev2_gids(tmp / "sys", dev, [ip])
+
+        if gid_delay_s > 0:
+            # Like the RDMA core: the RoCE v2 GID shows up a little after the address is added.
+            import threading
+
+            threading.Timer(gid_delay_s, add_gids).start()
+        else:
+            add_gids()
 
         # Switch namespace: forked child unshares its netns, waits for its ports, execs lldp-tx.
         sw_ports = [f"swp{i}" for i in range(len(nic_names))]

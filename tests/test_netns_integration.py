@@ -169,3 +169,11 @@ def test_two_nodes_l3_fabric_carries_a_collective():
     for routes, plan in ((r["A_routes"], r["plan"][:2]), (b["routes"], r["plan"][2:])):
         assert sorted(x["gateway"] for x in routes if x["dst"].endswith("/16")) == sorted(p["peer"] for p in plan)
     assert r["A_agent_rc"] == 0 and b["agent_rc"] == 0
+
+
+def test_late_rocev2_gids_are_waited_for():
+    """GIDs appear 300 ms after the agent starts (the RDMA core populates them asynchronously):
+    the agent waits for them instead of writing rccl.env without NCCL_IB_GID_INDEX."""
+    r = netns.run_isolated(n_nics=2, seed=22, interval="1s", gid_delay_s=0.3)
+    _check_configured(r)
+    assert "NCCL_IB_GID_INDEX=3" in r["rccl_env"]
