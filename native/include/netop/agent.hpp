@@ -155,6 +155,7 @@ class Agent {
     void on_lldp(NicState& n, const lldp::Frame& f);
     void add_route(NicState& n, int mask);
     void write_artifacts();
+    void write_l2_artifacts();
     void check_xgmi();
     void log_results();
     void mark(const std::string& phase);

@@ -143,6 +143,9 @@ struct GdrReport {
     std::string mode() const { return peer_mem ? "peermem" : dmabuf ? "dmabuf" : "none"; }
 };
 // `kernel_release` = "" reads uname(2).
+// L2 mode (no IPv4 on the NICs): the RoCE v2 GID of the port's IPv6 link-local address
+// (fe80::/64) is the one RCCL must use.
+std::optional<int> find_rocev2_linklocal_gid_index(const std::string& root, const std::string& rdma_dev, int port);
 GdrReport detect_gdr(const std::string& root = sysfs_root(), const std::string& kernel_release = "");
 bool kernel_at_least(const std::string& release, int major, int minor);
 

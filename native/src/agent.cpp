@@ -455,6 +455,27 @@ void Agent::detect_lldp(int stop_fd) {
     if (r == pkt::ListenResult::Deadline) NLOG_I("LLDP wait of %s expired with %d interface(s) silent", format_go_duration(cfg_.wait_ns).c_str(), remaining);
 }
 
+void Agent::write_l2_artifacts() {
+    std::string root = cfg_.sysfs_root.empty() ? topo::sysfs_root() : cfg_.sysfs_root;
+    for (auto& n : nics_) n.configured = n.link.up();
+    const int64_t deadline = mono_ns() + cfg_.gid_wait_ns;
+    for (;;) {
+        bool missing = false;
+        for (auto& n : nics_) {
+            if (n.rdma_dev.empty() || !n.configured || n.gid_index) continue;
+            n.gid_index = topo::find_rocev2_linklocal_gid_index(root, n.rdma_dev, n.rdma_port);
+            missing |= !n.gid_index;
+        }
+        if (!missing || mono_ns() >= deadline) break;
+        ::usleep(2000);
+    }
+    try {
+        artifacts::write_rccl_env(cfg_.rccl_env, nics_, "");
+    } catch (const std::exception& e) {
+        NLOG_E("Error writing RCCL env: %s", e.what());
+    }
+}
+
 void Agent::write_artifacts() {
     std::string root = cfg_.sysfs_root.empty() ? topo::sysfs_root() : cfg_.sysfs_root;
     // Poll all configured RDMA NICs together until each has its RoCE v2 GID or the wait ends.
@@ -703,6 +724,11 @@ void Agent::run(int stop_fd) {
             throw AgentError("No LLDP peers with a /30 Port Description were found");
         }
         write_artifacts();
+        mark("artifacts");
+    } else if (cfg_.configure && !cfg_.rccl_env.empty()) {
+        // L2 (MI355X addition): RCCL still has to know which HCAs are the scale-out ones and which
+        // GID to use; without IPv4 that is the RoCE v2 GID of the IPv6 link-local address.
+        write_l2_artifacts();
         mark("artifacts");
     }
 

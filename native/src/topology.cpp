@@ -229,6 +229,26 @@ static std::optional<std::array<uint8_t, 16>> parse_gid(const std::string& s) {
     return g;
 }
 
+std::optional<int> find_rocev2_linklocal_gid_index(const std::string& root, const std::string& rdma_dev, int port) {
+    std::string pdir = path_join(root, "class/infiniband/" + rdma_dev + "/ports/" + std::to_string(port));
+    std::vector<int> idx;
+    for (auto& n : list_dir(path_join(pdir, "gids"))) {
+        char* end = nullptr;
+        long v = std::strtol(n.c_str(), &end, 10);
+        if (*end == 0) idx.push_back(int(v));
+    }
+    std::sort(idx.begin(), idx.end());
+    for (int i : idx) {
+        auto g = read_file(path_join(pdir, "gids/" + std::to_string(i)));
+        if (!g) continue;
+        auto gid = parse_gid(*g);
+        if (!gid || (*gid)[0] != 0xfe || ((*gid)[1] & 0xc0) != 0x80) continue;  // fe80::/10
+        auto type = read_file(path_join(pdir, "gid_attrs/types/" + std::to_string(i)));
+        if (type && trim(*type) == "RoCE v2") return i;
+    }
+    return std::nullopt;
+}
+
 std::optional<int> find_rocev2_gid_index(const std::string& root, const std::string& rdma_dev, int port, Ipv4 ip) {
     std::string pdir = path_join(root, "class/infiniband/" + rdma_dev + "/ports/" + std::to_string(port));
     auto names = list_dir(path_join(pdir, "gids"));

@@ -107,6 +107,20 @@ def remove_volume(ds: dict, name: str) -> None:
             c["volumeMounts"] = [m for m in c["volumeMounts"] if m.get("name") != name]
 
 
+def order_managed_volumes(ds: dict) -> None:
+    """Volumes (and the agent's mounts) in one canonical order: the template's own first, then
+    NetworkManager, then artifacts, then the driver container's -- the order the reference
+    produces from scratch (controller_test.go:170-179), kept stable however the spec evolves."""
+    rank = {n: i for i, n in enumerate(MANAGED_VOLUMES + ("host-lib-modules",))}
+    key = lambda x: (x.get("name") in rank, rank.get(x.get("name"), 0))  # noqa: E731 (stable sort)
+    pod = ds["spec"]["template"]["spec"]
+    if "volumes" in pod:
+        pod["volumes"] = sorted(pod["volumes"], key=key)
+    for c in pod.get("containers") or []:
+        if "volumeMounts" in c:
+            c["volumeMounts"] = sorted(c["volumeMounts"], key=key)
+
+
 def agent_args(p: T.NetworkClusterPolicy) -> List[str]:
     so = p.spec.amdScaleOut
     args = ["--configure=true", "--keep-running", f"--mode={so.layer}"]
@@ -119,6 +133,10 @@ def agent_args(p: T.NetworkClusterPolicy) -> List[str]:
     if so.layer == "L3":
         args += [f"--wait={L3_WAIT}", f"--rccl-net={ARTIFACT_DIR_CONTAINER}/{RCCL_NET_FILE}",
                  f"--rccl-env={ARTIFACT_DIR_CONTAINER}/{RCCL_ENV_FILE}"]
+    else:
+        # MI355X: RCCL needs the HCA list and the link-local RoCE v2 GID in L2 as well (Gaudi's
+        # firmware did not, so the reference passes nothing in L2).
+        args.append(f"--rccl-env={ARTIFACT_DIR_CONTAINER}/{RCCL_ENV_FILE}")
     # MI355X options
     if so.xgmiCheck:
         args.append("--xgmi-expect=0")
@@ -156,12 +174,12 @@ def update_amd_scale_out_daemonset(ds: dict, p: T.NetworkClusterPolicy, namespac
         add_host_volume(ds, "var-run-dbus", "/var/run/dbus", "/var/run/dbus")
         add_host_volume(ds, "networkmanager", "/etc/NetworkManager", "/etc/NetworkManager")
         wanted |= {"var-run-dbus", "networkmanager"}
-    if so.layer == "L3":
-        add_host_volume(ds, "rccl-artifacts", ARTIFACT_DIR_HOST, ARTIFACT_DIR_CONTAINER)
-        wanted.add("rccl-artifacts")
+    add_host_volume(ds, "rccl-artifacts", ARTIFACT_DIR_HOST, ARTIFACT_DIR_CONTAINER)  # L2 too (rccl.env)
+    wanted.add("rccl-artifacts")
     for v in MANAGED_VOLUMES + ("host-lib-modules",):
         if v not in wanted:
             remove_volume(ds, v)
+    order_managed_volumes(ds)
     # A policy that switched from host-nic: no driver container, default readiness probe.
     inits = [x for x in pod.get("initContainers", []) if x.get("name") != "nic-driver"]
     if inits:
@@ -247,6 +265,7 @@ def update_host_nic_daemonset(ds: dict, p: T.NetworkClusterPolicy, namespace: st
     for v in MANAGED_VOLUMES + ("host-lib-modules",):
         if v not in wanted:
             remove_volume(ds, v)
+    order_managed_volumes(ds)
     probe = c.get("readinessProbe", {}).get("exec")
     if probe:
         probe["command"] = [probe["command"][0], "--ready-check", f"--nfd-label-file={HOST_NIC_LABEL_FILE}"]

@@ -92,6 +92,8 @@ def test_l2_mode_no_addresses():
     for nic in r["nics"]:
         assert r["state"][nic]["up"] and r["state"][nic]["addrs"] == []
     assert "gpu-scale-out.mode=L2" in r["label"]
+    # MI355X L2: RCCL still gets the scale-out HCAs and the RoCE v2 link-local GID index.
+    assert "NCCL_IB_GID_INDEX=1" in r["rccl_env"] and "NCCL_IB_HCA==mlx5_" in r["rccl_env"]
 
 
 def test_incomplete_xgmi_mesh_blocks_readiness():

@@ -107,7 +107,8 @@ def test_reconcile_lifecycle_reference_parity():
                 assert rb["roleRef"]["name"] == "system:openshift:scc:privileged"
             await eventually(ds_ok)
 
-            # update to L2: 4 args (reference controller_test.go:138-151 has 4 with no mtu)
+            # update to L2: the reference's 3 args (+ --v; controller_test.go:138-151), plus rccl.env:
+            # on MI355X RCCL needs the scale-out HCAs and the link-local RoCE v2 GID in L2 too
             cur = await client.get(kube.NETWORKCLUSTERPOLICIES, "policy")
             cur["spec"]["amdScaleOut"] = {"layer": "L2", "image": "amd/my-linkdiscovery:latest"}
             await client.replace(kube.NETWORKCLUSTERPOLICIES, cur)
@@ -115,9 +116,10 @@ def test_reconcile_lifecycle_reference_parity():
             def l2_ok():
                 ds = fake.get_object(kube.DAEMONSETS, "policy", NS)
                 c = ds["spec"]["template"]["spec"]["containers"][0]
-                assert c["args"] == ["--configure=true", "--keep-running", "--mode=L2"]
-                # fix vs reference: the L3 artifact volume is removed again
-                assert [v["name"] for v in ds["spec"]["template"]["spec"]["volumes"]] == ["nfd-features"]
+                assert c["args"] == ["--configure=true", "--keep-running", "--mode=L2",
+                                     "--rccl-env=/host/etc/amd/scale-out/rccl.env"]
+                assert [v["name"] for v in ds["spec"]["template"]["spec"]["volumes"]] == ["nfd-features",
+                                                                                          "rccl-artifacts"]
             await eventually(l2_ok)
 
             # L3 + disableNetworkManager + mtu 0: volumes in stable order (controller_test.go:153-180)
