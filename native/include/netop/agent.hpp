@@ -82,6 +82,7 @@ struct Config {
     std::string require_gdr;
     bool disable_fw_lldp = false;
     std::string fw_lldp_flags;                        // extra rules "NAME=0|1,..."
+    std::string rccl_env_extra;                       // "KEY=VALUE,..." appended to rccl.env
 };
 
 // Sanitises in place (MTU clamp to [1500, 9000], mode upper-cased); throws on a bad mode.
@@ -171,6 +172,7 @@ class Agent {
     std::unique_ptr<httpd::Server> httpd_;
     std::unique_ptr<ethtool::Ops> ethtool_;
     std::vector<ethtool::FwLldpResult> fw_lldp_;
+    std::vector<std::pair<std::string, std::string>> rccl_env_extra_;
     void disable_fw_lldp();
 
    public:

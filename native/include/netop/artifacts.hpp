@@ -48,8 +48,14 @@ class Json {
 std::string generate_rccl_net(const std::vector<NicState>& nics, bool extended = true);
 void write_rccl_net(const std::string& path, const std::vector<NicState>& nics, bool extended = true);
 
-std::string generate_rccl_env(const std::vector<NicState>& nics, const std::string& topo_file);
-void write_rccl_env(const std::string& path, const std::vector<NicState>& nics, const std::string& topo_file);
+// `extra`: site settings appended verbatim (e.g. NCCL_IB_TC for the fabric's RoCE traffic class);
+// keys must look like NCCL_* / RCCL_* / HSA_*, values must be single-line (parse_env_extra).
+std::string generate_rccl_env(const std::vector<NicState>& nics, const std::string& topo_file,
+                              const std::vector<std::pair<std::string, std::string>>& extra = {});
+void write_rccl_env(const std::string& path, const std::vector<NicState>& nics, const std::string& topo_file,
+                    const std::vector<std::pair<std::string, std::string>>& extra = {});
+// "K=V,K2=V2" -> pairs; throws std::invalid_argument on a bad key or value.
+std::vector<std::pair<std::string, std::string>> parse_env_extra(const std::string& spec);
 
 std::string networkd_filename(const std::string& dir, const std::string& ifname);
 std::string generate_networkd(const NicState& nic);

@@ -470,7 +470,7 @@ void Agent::write_l2_artifacts() {
         ::usleep(2000);
     }
     try {
-        artifacts::write_rccl_env(cfg_.rccl_env, nics_, "");
+        artifacts::write_rccl_env(cfg_.rccl_env, nics_, "", rccl_env_extra_);
     } catch (const std::exception& e) {
         NLOG_E("Error writing RCCL env: %s", e.what());
     }
@@ -504,7 +504,7 @@ void Agent::write_artifacts() {
     }
     if (!cfg_.rccl_env.empty()) {
         try {
-            artifacts::write_rccl_env(cfg_.rccl_env, nics_, "");
+            artifacts::write_rccl_env(cfg_.rccl_env, nics_, "", rccl_env_extra_);
         } catch (const std::exception& e) {
             NLOG_E("Error writing RCCL env: %s", e.what());
         }
@@ -638,6 +638,11 @@ void Agent::write_status() {
 void Agent::run(int stop_fd) {
     t0_ = t_last_ = mono_ns();
     sanitize(cfg_);
+    try {
+        rccl_env_extra_ = artifacts::parse_env_extra(cfg_.rccl_env_extra);
+    } catch (const std::exception& e) {
+        throw AgentError(std::string("Invalid --rccl-env-extra: ") + e.what());
+    }
     if (!cfg_.metrics_addr.empty() && !httpd_) {
         try {
             httpd_ = std::make_unique<httpd::Server>(cfg_.metrics_addr);

@@ -160,7 +160,27 @@ void write_rccl_net(const std::string& path, const std::vector<NicState>& nics, 
     write_file_atomic(path, generate_rccl_net(nics, extended), 0644);
 }
 
-std::string generate_rccl_env(const std::vector<NicState>& nics, const std::string& topo_file) {
+std::vector<std::pair<std::string, std::string>> parse_env_extra(const std::string& spec) {
+    std::vector<std::pair<std::string, std::string>> out;
+    for (const auto& item : split(spec, ',')) {
+        std::string t = trim(item);
+        if (t.empty()) continue;
+        auto eq = t.find('=');
+        if (eq == std::string::npos) throw std::invalid_argument("bad RCCL env entry '" + t + "' (want KEY=VALUE)");
+        std::string k = t.substr(0, eq), v = t.substr(eq + 1);
+        bool prefix = k.rfind("NCCL_", 0) == 0 || k.rfind("RCCL_", 0) == 0 || k.rfind("HSA_", 0) == 0;
+        bool chars = !k.empty() && std::all_of(k.begin(), k.end(), [](char c) {
+            return (c >= 'A' && c <= 'Z') || (c >= '0' && c <= '9') || c == '_';
+        });
+        if (!prefix || !chars) throw std::invalid_argument("RCCL env key '" + k + "' must be NCCL_*, RCCL_* or HSA_*");
+        if (v.find_first_of("\n\r") != std::string::npos) throw std::invalid_argument("multi-line value for " + k);
+        out.emplace_back(k, v);
+    }
+    return out;
+}
+
+std::string generate_rccl_env(const std::vector<NicState>& nics, const std::string& topo_file,
+                              const std::vector<std::pair<std::string, std::string>>& extra) {
     std::vector<std::string> hcas;
     std::set<int> gids;
     for (const NicState* n : sorted(nics)) {
@@ -174,11 +194,13 @@ std::string generate_rccl_env(const std::vector<NicState>& nics, const std::stri
     if (gids.size() == 1) out += "NCCL_IB_GID_INDEX=" + std::to_string(*gids.begin()) + "\n";
     if (!hcas.empty()) out += "NCCL_IB_DISABLE=0\n";
     if (!topo_file.empty()) out += "NCCL_TOPO_FILE=" + topo_file + "\n";
+    for (auto& [k, v] : extra) out += k + "=" + v + "\n";
     return out;
 }
 
-void write_rccl_env(const std::string& path, const std::vector<NicState>& nics, const std::string& topo_file) {
-    write_file_atomic(path, generate_rccl_env(nics, topo_file), 0644);
+void write_rccl_env(const std::string& path, const std::vector<NicState>& nics, const std::string& topo_file,
+                    const std::vector<std::pair<std::string, std::string>>& extra) {
+    write_file_atomic(path, generate_rccl_env(nics, topo_file, extra), 0644);
 }
 
 // ---------------------------------------------------------------------------

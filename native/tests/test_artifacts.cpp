@@ -125,3 +125,19 @@ TEST(json_escaping) {
     j.key("arr").begin_array().value(true).null().end_array().end_object();
     CHECK_EQ(j.str(), std::string("{\"a\\\"b\":\"x\\u003cy\\u003e\\u0026\\n\\u0001\",\"n\":-3,\"d\":0.5,\"arr\":[true,null]}"));
 }
+
+TEST(rccl_env_extra_settings) {
+    auto ex = parse_env_extra("NCCL_IB_TC=106, NCCL_IB_QPS_PER_CONNECTION=4,HSA_NO_SCRATCH_RECLAIM=1");
+    CHECK_EQ(ex.size(), size_t(3));
+    NicState a;
+    a.ifname = "e0";
+    a.rdma_dev = "mlx5_0";
+    a.configured = true;
+    auto env = generate_rccl_env({a}, "", ex);
+    CHECK(env.find("NCCL_IB_TC=106\n") != std::string::npos);
+    CHECK(env.find("HSA_NO_SCRATCH_RECLAIM=1\n") != std::string::npos);
+    CHECK_THROWS(parse_env_extra("PATH=/tmp"));
+    CHECK_THROWS(parse_env_extra("NCCL_x=1"));
+    CHECK_THROWS(parse_env_extra("NCCL_IB_TC"));
+    CHECK(parse_env_extra("").empty());
+}

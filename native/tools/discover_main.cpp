@@ -58,6 +58,7 @@ int main(int argc, char** argv) {
     fs.add_string("nfd-label-file", &cfg.labels.file, "readiness label file name inside the features directory");
     fs.add_string("nfd-label", &cfg.labels.key, "readiness label key (published as KEY=true; KEY.mode, KEY.nics, ... alongside)");
     fs.add_string("rccl-env", &cfg.rccl_env, "write an RCCL environment file (NCCL_IB_HCA, NCCL_IB_GID_INDEX, ...)");
+    fs.add_string("rccl-env-extra", &cfg.rccl_env_extra, "site settings appended to the RCCL environment file: KEY=VALUE[,...] (NCCL_*, RCCL_*, HSA_*)");
     fs.add_string("status-file", &cfg.status_file, "write a JSON status document (per-NIC results, phase timings)");
     fs.add_string("nm-keyfile-dir", &cfg.nm_keyfile_dir, "with --disable-networkmanager, also persist an unmanaged-devices keyfile here");
     fs.add_int("xgmi-expect", &cfg.xgmi_expect_links, "verify the xGMI mesh before labelling: -1 off, 0 full mesh, N GPU pairs");

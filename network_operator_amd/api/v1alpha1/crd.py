@@ -66,6 +66,9 @@ def openapi_schema() -> dict:
             "gpuDirectRdma": {"description": "Require GPUDirect RDMA before labelling the node: Any, PeerMem (amdkfd\n"
                                              "peer-memory client) or DmaBuf (RDMA dma-buf MRs).  Empty: report only.",
                               "enum": ["Any", "PeerMem", "DmaBuf"], "type": "string"},
+            "rcclEnv": {"description": "Site settings appended to rccl.env (e.g. NCCL_IB_TC for the fabric's RoCE\n"
+                                       "traffic class).  Keys: NCCL_*, RCCL_*, HSA_*.",
+                        "additionalProperties": {"type": "string"}, "type": "object"},
             "metricsPort": {"description": "Serve agent metrics (/metrics, /healthz, /readyz) on this host port (0 = off).",
                             "maximum": 65535, "minimum": 0, "type": "integer"},
         },

@@ -60,10 +60,11 @@ class AmdScaleOutSpec:
     disableFirmwareLldp: bool = False
     metricsPort: int = 0
     gpuDirectRdma: str = ""
+    rcclEnv: Dict[str, str] = field(default_factory=dict)
     extra: Dict[str, Any] = field(default_factory=dict)
 
     _FIELDS = ("disableNetworkManager", "layer", "image", "pullPolicy", "mtu", "xgmiCheck", "lldpAnnounce",
-               "interfaces", "nicDrivers", "disableFirmwareLldp", "metricsPort", "gpuDirectRdma")
+               "interfaces", "nicDrivers", "disableFirmwareLldp", "metricsPort", "gpuDirectRdma", "rcclEnv")
 
     def to_dict(self) -> dict:
         d: dict = {}
@@ -89,6 +90,8 @@ class AmdScaleOutSpec:
             d["metricsPort"] = self.metricsPort
         if self.gpuDirectRdma:
             d["gpuDirectRdma"] = self.gpuDirectRdma
+        if self.rcclEnv:
+            d["rcclEnv"] = dict(self.rcclEnv)
         d.update(copy.deepcopy(self.extra))
         return d
 
@@ -108,6 +111,7 @@ class AmdScaleOutSpec:
             disableFirmwareLldp=bool(d.pop("disableFirmwareLldp", False)),
             metricsPort=int(d.pop("metricsPort", 0) or 0),
             gpuDirectRdma=d.pop("gpuDirectRdma", "") or "",
+            rcclEnv=dict(d.pop("rcclEnv", {}) or {}),
         )
         s.extra = d
         return s

@@ -91,6 +91,16 @@ def validate_node_selector(ns: dict) -> None:
                 raise InvalidNodeSelectorError()
 
 
+RCCL_ENV_KEY_RE = re.compile(r"^(NCCL|RCCL|HSA)_[A-Z0-9_]+$")
+
+
+class InvalidRcclEnvError(ValidationError):
+    def __init__(self, key: str):
+        super().__init__(key)
+        self.message = f"invalid rcclEnv entry {key!r}: keys must be NCCL_*, RCCL_* or HSA_*, values one line " \
+                       "without ','"
+
+
 def validate_amd_so_spec(s: T.AmdScaleOutSpec) -> List[str]:
     """Returns admission warnings.  (The reference's validateGaudiSoSpec is a no-op, :87-89.)"""
     warnings = []
@@ -99,6 +109,9 @@ def validate_amd_so_spec(s: T.AmdScaleOutSpec) -> List[str]:
     for i in s.interfaces:
         if not i or len(i) > 15 or "/" in i or " " in i or "," in i:
             raise InvalidInterfaceError(i)
+    for k, v in s.rcclEnv.items():
+        if not RCCL_ENV_KEY_RE.match(str(k)) or not isinstance(v, str) or any(c in v for c in "\n\r,"):
+            raise InvalidRcclEnvError(str(k))
     return warnings
 
 

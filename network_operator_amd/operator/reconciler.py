@@ -150,6 +150,8 @@ def agent_args(p: T.NetworkClusterPolicy) -> List[str]:
         args.append("--disable-fw-lldp")
     if so.metricsPort:
         args.append(f"--metrics-bind-address=:{so.metricsPort}")
+    if so.rcclEnv:
+        args.append("--rccl-env-extra=" + ",".join(f"{k}={v}" for k, v in sorted(so.rcclEnv.items())))
     if so.gpuDirectRdma:
         args.append("--require-gdr=" + {"Any": "any", "PeerMem": "peermem", "DmaBuf": "dmabuf"}[so.gpuDirectRdma])
     return args

@@ -422,3 +422,22 @@ def test_host_nic_webhook_rules():
         W.validate_create(p)
     rt = T.NetworkClusterPolicy.from_dict(T.new_host_nic_policy("h", driverImage="x").to_dict())
     assert rt.spec.configurationType == "host-nic" and rt.spec.hostNic.driverImage == "x"
+
+
+def test_rccl_env_extra_settings_validated_and_passed():
+    import pytest
+
+    from network_operator_amd.api.v1alpha1 import types as T
+    from network_operator_amd.api.v1alpha1 import webhook as W
+    from network_operator_amd.operator.reconciler import agent_args
+
+    p = T.new_policy("p", layer="L3")
+    p.spec.amdScaleOut.rcclEnv = {"NCCL_IB_TC": "106", "NCCL_IB_QPS_PER_CONNECTION": "4"}
+    assert W.validate_create(p) == []
+    assert "--rccl-env-extra=NCCL_IB_QPS_PER_CONNECTION=4,NCCL_IB_TC=106" in agent_args(p)
+    p.spec.amdScaleOut.rcclEnv = {"LD_PRELOAD": "/x.so"}
+    with pytest.raises(W.InvalidRcclEnvError):
+        W.validate_create(p)
+    p.spec.amdScaleOut.rcclEnv = {"NCCL_DEBUG": "INFO,WARN"}
+    with pytest.raises(W.InvalidRcclEnvError):
+        W.validate_create(p)
