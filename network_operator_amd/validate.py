@@ -1,0 +1,140 @@
+"""Post-configuration fabric validation of one MI355X node (``python -m network_operator_amd.validate``).
+
+The agent configures the node and checks what it can see without touching a GPU: the KFD
+xGMI topology, GPUDirect RDMA support and LLDP peers.  This is the GPU-side counterpart.  It
+runs where the GPUs are (a Job with ``amd.com/gpu: 8``, see ``config/validation/``) and
+answers one question: do the links actually carry collectives at the expected speed?  It runs
+five checks:
+
+1. **Topology.**  KFD: every GPU pair is xGMI-linked.
+2. **xGMI probe** (``netop-xgmi-probe``).  Per-link pull bandwidth, all-peers pull and push
+   aggregates, all byte-exact.
+3. **RCCL** (``netop-rccl-bench``).  An all-reduce size sweep, every result checked exactly.
+   With n > 1 the large-message busbw must reach ``--min-busbw``.
+4. **Counters** (amd-smi).  Every up xGMI link moved data during the RCCL run.  This is the
+   "RCCL sees every link" check from BASELINE.json.
+5. **Optionally, the label.**  If everything passed, the NFD label
+   ``amd.feature.node.kubernetes.io/gpu-fabric-validated=true`` is written, along with the
+   measured busbw.
+
+The reference has no equivalent; its README only says the fabric is validated "with the
+vendor's tests".  Prints one JSON report and exits 0 only if every check passed.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+from pathlib import Path
+from typing import List, Optional
+
+from .utils.paths import native_bin
+
+LABEL = "amd.feature.node.kubernetes.io/gpu-fabric-validated"
+LABEL_FILE = "gpu-fabric-validation.txt"
+
+
+def _check(name: str, ok: bool, **detail) -> dict:
+    return {"check": name, "ok": bool(ok), **detail}
+
+
+def run(gpus: int, min_busbw: float, min_link_GBps: float, max_bytes: int, sysfs_root: str = "/sys/",
+        nfd_dir: Optional[str] = None, timeout: float = 600) -> dict:
+    checks: List[dict] = []
+    report: dict = {"gpus": gpus, "started": time.time()}
+
+    # 1. topology (no GPU needed)
+    try:
+        from .agent import native
+
+        x = native().read_xgmi(sysfs_root)
+        need = x["pairs_expected"] if gpus == len(x["gpus"]) else gpus * (gpus - 1) // 2
+        checks.append(_check("xgmi_topology", x["pairs_connected"] >= need, pairs=x["pairs_connected"],
+                             expected=need, per_gpu_bw_mbs=x["per_gpu_bw_mbs"]))
+    except Exception as e:
+        checks.append(_check("xgmi_topology", False, error=str(e)))
+
+    # 2. xGMI probe (pull + push, byte exact)
+    try:
+        r = subprocess.run([str(native_bin("netop-xgmi-probe")), "--bytes=67108864", "--iters=5",
+                            f"--max-gpus={gpus}"], capture_output=True, text=True, timeout=timeout)
+        p = json.loads(r.stdout.strip().splitlines()[-1])
+        n = p["gpus"]
+        links = [p["link_GBps"][d][q] for d in range(n) for q in range(n) if d != q]
+        ok = r.returncode == 0 and p["errors"] == 0 and p.get("push_errors", 0) == 0
+        if links:
+            ok = ok and min(links) >= min_link_GBps
+        checks.append(_check("xgmi_probe", ok, gpus=n, min_link_GBps=min(links) if links else None,
+                             pull_aggregate_GBps=p["aggregate_GBps"], push_aggregate_GBps=p.get("push_aggregate_GBps"),
+                             errors=p["errors"] + p.get("push_errors", 0)))
+    except Exception as e:
+        checks.append(_check("xgmi_probe", False, error=str(e)[-500:]))
+
+    # 3 + 4. RCCL sweep with counters around it
+    before = None
+    try:
+        from .ops import smi
+
+        before = smi.snapshot()
+    except Exception as e:
+        report["smi_error"] = str(e)
+    try:
+        from .parallel import rccl_bench
+
+        rows = rccl_bench.run(op="all_reduce", gpus=gpus, min_bytes=1 << 20, max_bytes=max_bytes, factor=8,
+                              iters=20, warmup=5, timeout=timeout)
+        wrong = sum(r.wrong for r in rows)
+        peak = max((r.busbw_GBps for r in rows), default=0.0)
+        ok = bool(rows) and wrong == 0 and (gpus == 1 or peak >= min_busbw)
+        checks.append(_check("rccl_all_reduce", ok, peak_busbw_GBps=peak, wrong=wrong, min_busbw_GBps=min_busbw,
+                             sizes=[{"bytes": r.bytes, "time_us": r.time_us, "busbw_GBps": r.busbw_GBps} for r in rows]))
+        report["busbw_GBps"] = peak
+    except Exception as e:
+        checks.append(_check("rccl_all_reduce", False, error=str(e)[-500:]))
+    if before is not None:
+        try:
+            t = smi.traffic(before, smi.snapshot())
+            # Only GPUs taking part can be expected to move data; with n == 8 every up link must.
+            ok = gpus < 8 or t["links_with_traffic"] >= t["links_up"]
+            checks.append(_check("xgmi_counters", ok, links_up=t["links_up"],
+                                 links_with_traffic=t["links_with_traffic"]))
+        except Exception as e:
+            checks.append(_check("xgmi_counters", False, error=str(e)))
+
+    report["checks"] = checks
+    report["ok"] = all(c["ok"] for c in checks)
+    report["seconds"] = time.time() - report.pop("started")
+    if nfd_dir:
+        path = Path(nfd_dir) / LABEL_FILE
+        if report["ok"]:
+            Path(nfd_dir).mkdir(parents=True, exist_ok=True)
+            tmp = path.with_suffix(".tmp")
+            tmp.write_text(f"{LABEL}=true\n{LABEL}.busbw-gbps={int(report.get('busbw_GBps', 0))}\n")
+            os.replace(tmp, path)
+        elif path.exists():
+            path.unlink()
+        report["label_file"] = str(path) if report["ok"] else None
+    return report
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(prog="python -m network_operator_amd.validate", description=__doc__.split("\n")[0])
+    ap.add_argument("--gpus", type=int, default=8)
+    ap.add_argument("--min-busbw", type=float, default=0.0,
+                    help="required large-message all-reduce busbw in GB/s (n > 1); 0 = only correctness")
+    ap.add_argument("--min-link", type=float, default=0.0, help="required per-link pull GB/s (n > 1)")
+    ap.add_argument("--max-bytes", type=int, default=1 << 30)
+    ap.add_argument("--sysfs-root", default=os.environ.get("SYSFS_ROOT", "/sys/"))
+    ap.add_argument("--nfd-features-dir", default=None, help="write the validation label here when all checks pass")
+    a = ap.parse_args(argv)
+    rep = run(a.gpus, a.min_busbw, a.min_link, a.max_bytes, a.sysfs_root, a.nfd_features_dir)
+    print(json.dumps(rep))
+    return 0 if rep["ok"] else 1
+
+
+if __name__ == "__main__":
+    sys.exit(main())

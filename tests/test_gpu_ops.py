@@ -190,3 +190,14 @@ def test_sum_bf16_rejects_bad_args(cuda_device):
         hip.sum_bf16([a] * 9, a)
     with pytest.raises(ValueError):
         hip.sum_bf16([a, torch.zeros(24, dtype=torch.bfloat16, device=cuda_device)], a)
+
+
+def test_fabric_validation_single_gpu(cuda_device, tmp_path):
+    """validate.run on the 1-GPU box: topology from the real KFD, probe, RCCL sweep, counters."""
+    from network_operator_amd import validate
+
+    rep = validate.run(gpus=1, min_busbw=0, min_link_GBps=0, max_bytes=64 << 20, nfd_dir=str(tmp_path))
+    assert rep["ok"], rep
+    names = [c["check"] for c in rep["checks"]]
+    assert names[:3] == ["xgmi_topology", "xgmi_probe", "rccl_all_reduce"]
+    assert (tmp_path / validate.LABEL_FILE).read_text().startswith(validate.LABEL + "=true\n")

@@ -215,3 +215,11 @@ def test_helm_host_nic_policy():
     assert CRD_.validate(hn[0]) == []
     with pytest.raises(RenderError):
         helm_template(ROOT / "charts" / "network-operator", {"config": {"hostNic": {"enabled": True, "mode": "L4"}}})
+
+
+def test_validation_job_manifest():
+    job = yaml.safe_load((ROOT / "config" / "validation" / "validation-job.yaml").read_text())
+    c = job["spec"]["template"]["spec"]["containers"][0]
+    assert c["resources"]["limits"]["amd.com/gpu"] == 8
+    assert c["command"][:3] == ["python3", "-m", "network_operator_amd.validate"]
+    assert job["spec"]["template"]["spec"]["nodeSelector"] == {"amd.feature.node.kubernetes.io/gpu-scale-out": "true"}
