@@ -3,6 +3,7 @@ PYTHON ?= python3
 JOBS   ?= 8
 IMG_OPERATOR ?= amd/amd-network-operator:0.1.0
 IMG_AGENT    ?= amd/amd-network-linkdiscovery:0.1.0
+IMG_VALIDATION ?= amd/amd-network-validation:0.1.0
 
 KUBECTL ?= kubectl
 VERSION ?= 0.1.0
@@ -104,6 +105,7 @@ helm-package-chart:         ## .charts/<chart>-<version>.tgz
 images:
 	docker build -f build/Dockerfile.operator -t $(IMG_OPERATOR) .
 	docker build -f build/Dockerfile.linkdiscovery -t $(IMG_AGENT) .
+	docker build -f build/Dockerfile.validation -t $(IMG_VALIDATION) .
 
 clean:
 	rm -rf _build _build-asan _build-vet network_operator_amd/_lib deployments dist bundle bundle.Dockerfile .charts
