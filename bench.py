@@ -94,6 +94,9 @@ def main(argv=None) -> int:
                     help="other collectives reported at --bytes (n > 1 only)")
     ap.add_argument("--xgmi-probe", type=int, default=1, help="run the HIP xGMI link probe on rank 0 (n > 1)")
     ap.add_argument("--native-rccl", type=int, default=1, help="also run the native netop-rccl-bench harness on rank 0")
+    ap.add_argument("--extras-budget", type=float, default=240.0,
+                    help="seconds rank 0 may spend on the diagnostics after the timed loop (probe, native "
+                         "harness, knob probe, direct all-reduce); later ones are skipped once it is spent")
     ap.add_argument("--rccl-autotune", type=int, default=0,
                     help="n > 1: before RCCL starts, rank 0 measures RCCL knob variants with the native harness "
                          "and every rank uses the fastest (>= 3%% better than defaults) for the run")
@@ -190,6 +193,11 @@ def main(argv=None) -> int:
     # 5. xGMI link probe (rank 0, single process over every GPU it can see): per-link pull
     #    bandwidth and all-peers-concurrent aggregate, byte-exact.  Runs after the timed loop.
     probe = None
+    t_extras = time.monotonic()
+
+    def budget_left() -> bool:
+        return time.monotonic() - t_extras < args.extras_budget
+
     if rank == 0 and world > 1 and args.device == "cuda" and args.xgmi_probe:
         try:
             from network_operator_amd.ops import hip as H
@@ -209,7 +217,7 @@ def main(argv=None) -> int:
     #    directly, every size checked exactly): a second opinion on the same links that does not
     #    go through torch.distributed.  Runs after the timed loop; failures are reported, not fatal.
     native = None
-    if rank == 0 and args.device == "cuda" and args.native_rccl:
+    if rank == 0 and args.device == "cuda" and args.native_rccl and budget_left():
         try:
             from network_operator_amd.parallel import rccl_bench
 
@@ -218,7 +226,7 @@ def main(argv=None) -> int:
             native = {"rows": [{"bytes": r.bytes, "time_us": r.time_us, "algbw_GBps": r.algbw_GBps,
                                 "busbw_GBps": r.busbw_GBps, "wrong": r.wrong} for r in rows],
                       "peak_busbw_GBps": max((r.busbw_GBps for r in rows), default=0.0)}
-            if world > 1:  # sensitivity of the large-message busbw to RCCL knobs (diagnostic only)
+            if world > 1 and budget_left():  # sensitivity of the 1 GiB busbw to RCCL knobs (diagnostic only)
                 native["env_probe"] = rccl_bench.env_probe(world, 1 << 30)
         except Exception as e:
             native = {"error": str(e)[-500:]}
@@ -226,7 +234,7 @@ def main(argv=None) -> int:
     # 7. Direct two-shot xGMI all-reduce (hand-written HIP, all 7 links at once, pull and push),
     #    rank 0 over the first `world` GPUs, exact check of three seeds per size (n > 1).
     direct = None
-    if rank == 0 and world > 1 and args.device == "cuda" and args.xgmi_allreduce:
+    if rank == 0 and world > 1 and args.device == "cuda" and args.xgmi_allreduce and budget_left():
         try:
             from network_operator_amd.parallel import xgmi_allreduce as XA
 
