@@ -11,7 +11,7 @@ BUNDLE_IMG ?= amd/amd-network-operator-bundle:v$(VERSION)
 
 .PHONY: all help build native hip test test-native test-netns test-gpu manifests deployments bench bench-node-ready \
         images sanitize tsan clean fmt vet lint fuzz run build-installer install uninstall deploy undeploy bundle \
-        bundle-build helm-package-chart
+        bundle-build helm-package-chart fuzz-native
 
 all: build
 
@@ -109,3 +109,20 @@ images:
 
 clean:
 	rm -rf _build _build-asan _build-vet network_operator_amd/_lib deployments dist bundle bundle.Dockerfile .charts
+
+FUZZ_CXX ?= /opt/rocm/lib/llvm/bin/clang++
+FUZZ_TIME ?= 60
+fuzz-native:                ## libFuzzer (+ASan/UBSan) on the LLDP, D-Bus, Port Description and netlink parsers
+	mkdir -p _build-fuzz
+	for t in 1:lldp 2:dbus 3:portdesc 4:netlink; do id=$${t%%:*}; name=$${t##*:}; \
+	  $(FUZZ_CXX) -std=c++17 -O1 -g -fsanitize=fuzzer,address,undefined -fno-sanitize-recover=undefined \
+	    -mllvm -asan-globals=0 \
+	    -DNETOP_FUZZ_TARGET=$$id -DNETOP_VERSION='"fuzz"' -Inative/include native/fuzz/fuzz_targets.cpp \
+	    native/src/common.cpp native/src/log.cpp native/src/lldp.cpp native/src/l3.cpp native/src/netlink.cpp \
+	    native/src/dbus.cpp -o _build-fuzz/fuzz_$$name -lpthread || exit 1; \
+	  mkdir -p _build-fuzz/corpus_$$name; \
+	  _build-fuzz/fuzz_$$name -max_total_time=$(FUZZ_TIME) -rss_limit_mb=2048 \
+	    -print_final_stats=1 _build-fuzz/corpus_$$name > _build-fuzz/$$name.log 2>&1; rc=$$?; \
+	  grep -E "stat::number_of_executed_units|SUMMARY|ERROR" _build-fuzz/$$name.log | sed "s/^/$$name: /"; \
+	  [ $$rc -eq 0 ] || exit $$rc; \
+	done

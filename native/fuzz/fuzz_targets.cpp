@@ -1,0 +1,68 @@
+// libFuzzer targets for every parser that reads bytes the agent does not control.
+//
+//   lldp      frames from the switch (AF_PACKET) — untrusted, L2-adjacent attacker
+//   dbus      messages from the system bus peer
+//   portdesc  the switch's Port Description string (operator-configured, still untrusted)
+//   netlink   RTM_NEWLINK payloads (kernel, but parsed with length arithmetic)
+//
+// Built by `make fuzz-native` with amdclang++ -fsanitize=fuzzer,address,undefined (one binary
+// per target, selected by NETOP_FUZZ_TARGET at compile time).  Each target must never crash,
+// hang or trip a sanitizer on any input.
+#include <linux/netlink.h>
+#include <linux/rtnetlink.h>
+
+#include <cstdint>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "netop/dbus.hpp"
+#include "netop/l3.hpp"
+#include "netop/lldp.hpp"
+#include "netop/netlink.hpp"
+
+using namespace netop;
+
+extern "C" int LLVMFuzzerTestOneInput(const uint8_t* data, size_t size) {
+#if NETOP_FUZZ_TARGET == 1
+    lldp::DecodeError err;
+    auto f = lldp::decode(data, size, &err);
+    if (f) {
+        // Whatever decodes must re-encode and decode to the same fields.
+        auto bytes = lldp::encode(*f);
+        auto again = lldp::decode(bytes.data(), bytes.size());
+        if (!again || again->port_description != f->port_description || again->ttl != f->ttl) __builtin_trap();
+    }
+#elif NETOP_FUZZ_TARGET == 2
+    dbus::Message m;
+    size_t used = 0;
+    try {
+        used = dbus::unmarshal(data, size, &m);
+    } catch (const std::exception&) {
+        return 0;
+    }
+    if (used > size) __builtin_trap();
+#elif NETOP_FUZZ_TARGET == 3
+    std::string s(reinterpret_cast<const char*>(data), size);
+    for (auto p : {l3::TokenPolicy::Compat, l3::TokenPolicy::CompatThenLast, l3::TokenPolicy::AnyToken}) {
+        std::string err;
+        auto a = l3::parse_port_description(s, p, &err);
+        if (a && (a->local.v ^ a->peer.v) != 3u) __builtin_trap();
+    }
+#elif NETOP_FUZZ_TARGET == 4
+    // Wrap the input as the payload of one RTM_NEWLINK message with a consistent header.
+    if (size > 1 << 16) return 0;
+    std::vector<uint8_t> buf(NLMSG_HDRLEN + size);
+    auto* h = reinterpret_cast<nlmsghdr*>(buf.data());
+    h->nlmsg_len = uint32_t(buf.size());
+    h->nlmsg_type = RTM_NEWLINK;
+    std::memcpy(buf.data() + NLMSG_HDRLEN, data, size);
+    try {
+        (void)nl::parse_link(h);
+    } catch (const std::exception&) {
+    }
+#else
+#error "define NETOP_FUZZ_TARGET"
+#endif
+    return 0;
+}

@@ -198,7 +198,7 @@ void Rtnl::transact(Msg& m, const std::function<void(const nlmsghdr*)>& on_reply
             if (errno == EINTR) continue;
             throw_errno(std::string("netlink recv ") + msg_name(type));
         }
-        size_t len = size_t(n);
+        long len = long(n);  // signed: NLMSG_NEXT must not wrap on a short final message
         for (auto* h = reinterpret_cast<nlmsghdr*>(buf); NLMSG_OK(h, len); h = NLMSG_NEXT(h, len)) {
             if (h->nlmsg_seq != seq) continue;  // stale reply to an earlier request
             if (h->nlmsg_type == NLMSG_ERROR) {
@@ -232,7 +232,7 @@ void Rtnl::dump(Msg& m, const std::function<void(const nlmsghdr*)>& on_item) {
                 if (errno == EINTR) continue;
                 throw_errno("netlink dump recv");
             }
-            size_t len = size_t(n);
+            long len = long(n);  // signed: NLMSG_NEXT must not wrap on a short final message
             for (auto* h = reinterpret_cast<nlmsghdr*>(buf); NLMSG_OK(h, len); h = NLMSG_NEXT(h, len)) {
                 if (h->nlmsg_seq != seq) continue;
                 if (h->nlmsg_flags & NLM_F_DUMP_INTR) interrupted = true;
@@ -262,14 +262,26 @@ void Rtnl::dump(Msg& m, const std::function<void(const nlmsghdr*)>& on_item) {
 // ---------------------------------------------------------------------------
 // Parsing
 // ---------------------------------------------------------------------------
+// A message must hold its fixed header before any of it is read: the kernel never sends less,
+// but the parser must not trust that (fuzzing found the unchecked read).
+template <class T>
+static const T* fixed_header(const nlmsghdr* h, const char* what) {
+    if (h->nlmsg_len < NLMSG_LENGTH(sizeof(T))) throw SysError(EBADMSG, std::string("truncated ") + what + " message");
+    return reinterpret_cast<const T*>(NLMSG_DATA(h));
+}
+
 template <class F>
-static void for_each_attr(const rtattr* a, size_t len, F&& f) {
+static void for_each_attr(const rtattr* a, size_t total, F&& f) {
+    // Signed remaining length: RTA_NEXT subtracts the *aligned* attribute length, which can
+    // exceed what is left for the last attribute; with an unsigned length that wraps and
+    // RTA_OK would walk off the buffer (found by the netlink fuzz target).
+    long len = total > size_t(1) << 30 ? 0 : long(total);
     for (; RTA_OK(a, len); a = RTA_NEXT(a, len)) f(a);
 }
 
 LinkInfo parse_link(const nlmsghdr* h) {
     LinkInfo li;
-    const auto* ifi = reinterpret_cast<const ifinfomsg*>(NLMSG_DATA(h));
+    const auto* ifi = fixed_header<ifinfomsg>(h, "link");
     li.index = ifi->ifi_index;
     li.flags = ifi->ifi_flags;
     size_t len = h->nlmsg_len - NLMSG_LENGTH(sizeof(ifinfomsg));
@@ -303,7 +315,7 @@ LinkInfo parse_link(const nlmsghdr* h) {
 
 static AddrInfo parse_addr(const nlmsghdr* h) {
     AddrInfo ai;
-    const auto* ifa = reinterpret_cast<const ifaddrmsg*>(NLMSG_DATA(h));
+    const auto* ifa = fixed_header<ifaddrmsg>(h, "address");
     ai.ifindex = int(ifa->ifa_index);
     ai.family = ifa->ifa_family;
     ai.prefixlen = ifa->ifa_prefixlen;
@@ -333,7 +345,7 @@ static AddrInfo parse_addr(const nlmsghdr* h) {
 
 static RouteInfo parse_route(const nlmsghdr* h) {
     RouteInfo r;
-    const auto* rtm = reinterpret_cast<const rtmsg*>(NLMSG_DATA(h));
+    const auto* rtm = fixed_header<rtmsg>(h, "route");
     r.dst.len = rtm->rtm_dst_len;
     r.scope = rtm->rtm_scope;
     r.protocol = rtm->rtm_protocol;
@@ -598,7 +610,7 @@ class RtnlLinkWatcher final : public LinkWatcher {
                 if (errno == ENOBUFS) continue;  // overrun: events lost; caller re-reads state
                 throw_errno("recv(link watcher)");
             }
-            size_t len = size_t(n);
+            long len = long(n);  // signed: NLMSG_NEXT must not wrap on a short final message
             for (auto* h = reinterpret_cast<nlmsghdr*>(buf); NLMSG_OK(h, len); h = NLMSG_NEXT(h, len)) {
                 if (h->nlmsg_type != RTM_NEWLINK && h->nlmsg_type != RTM_DELLINK) continue;
                 LinkEvent ev;

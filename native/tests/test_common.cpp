@@ -91,3 +91,29 @@ TEST(flagset_pflag_semantics) {
     const char* baddur[] = {"discover", "--wait=90"};
     CHECK_THROWS(fs.parse(2, const_cast<char**>(baddur)));
 }
+
+#include <linux/netlink.h>
+#include <linux/rtnetlink.h>
+
+#include "netop/netlink.hpp"
+
+TEST(netlink_parse_link_rejects_truncated_and_unaligned_input) {
+    // Regressions found by the netlink fuzz target (make fuzz-native).
+    std::vector<uint8_t> buf(NLMSG_HDRLEN + 4, 0);
+    auto* h = reinterpret_cast<nlmsghdr*>(buf.data());
+    h->nlmsg_len = uint32_t(buf.size());  // shorter than nlmsghdr + ifinfomsg
+    h->nlmsg_type = RTM_NEWLINK;
+    CHECK_THROWS(netop::nl::parse_link(h));
+    // ifinfomsg + one IFLA_IFNAME attribute whose unaligned length ends the message exactly:
+    // RTA_NEXT's aligned step is larger than what is left and must not wrap the length.
+    std::vector<uint8_t> m(NLMSG_LENGTH(sizeof(ifinfomsg)) + 5, 0);
+    auto* h2 = reinterpret_cast<nlmsghdr*>(m.data());
+    h2->nlmsg_len = uint32_t(m.size());
+    h2->nlmsg_type = RTM_NEWLINK;
+    auto* a = reinterpret_cast<rtattr*>(m.data() + NLMSG_LENGTH(sizeof(ifinfomsg)));
+    a->rta_len = 5;
+    a->rta_type = IFLA_IFNAME;
+    m.back() = 'x';
+    auto li = netop::nl::parse_link(h2);
+    CHECK_EQ(li.name, std::string("x"));
+}
