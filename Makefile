@@ -121,7 +121,8 @@ fuzz-native:                ## libFuzzer (+ASan/UBSan) on the LLDP, D-Bus, Port 
 	    native/src/common.cpp native/src/log.cpp native/src/lldp.cpp native/src/l3.cpp native/src/netlink.cpp \
 	    native/src/dbus.cpp -o _build-fuzz/fuzz_$$name -lpthread || exit 1; \
 	  mkdir -p _build-fuzz/corpus_$$name; \
-	  _build-fuzz/fuzz_$$name -max_total_time=$(FUZZ_TIME) -rss_limit_mb=2048 \
+	  _build-fuzz/fuzz_$$name native/fuzz/regressions/* > _build-fuzz/$$name.replay.log 2>&1 || { tail -20 _build-fuzz/$$name.replay.log; exit 1; }; \
+	  _build-fuzz/fuzz_$$name -artifact_prefix=_build-fuzz/$$name- -max_total_time=$(FUZZ_TIME) -rss_limit_mb=2048 \
 	    -print_final_stats=1 _build-fuzz/corpus_$$name > _build-fuzz/$$name.log 2>&1; rc=$$?; \
 	  grep -E "stat::number_of_executed_units|SUMMARY|ERROR" _build-fuzz/$$name.log | sed "s/^/$$name: /"; \
 	  [ $$rc -eq 0 ] || exit $$rc; \

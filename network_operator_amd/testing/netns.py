@@ -263,6 +263,15 @@ def run_scenario(n_nics: int = 8, mode: str = "L3", seed: int | None = None, int
             except OSError as e:
                 state[node_if] = {"error": str(e)}
         res["state"] = state
+        if t_ready:  # the agent writes status.json (ready=true) right after the label
+            end = time.monotonic() + 5
+            while time.monotonic() < end and agent.poll() is None:
+                try:
+                    if json.loads((tmp / "status.json").read_text()).get("ready"):
+                        break
+                except (OSError, ValueError):
+                    pass
+                time.sleep(0.001)
         for f in ("rccl-net.json", "status.json"):
             fp = tmp / f
             res[f.split(".")[0].replace("-", "_")] = json.loads(fp.read_text()) if fp.exists() else None
