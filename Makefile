@@ -54,6 +54,8 @@ deployments:                ## render kustomize + Helm offline into deployments/
 	mkdir -p deployments
 	$(PYTHON) -c 'from network_operator_amd.testing.render import *; open("deployments/operator.yaml","w").write(dump_all(kustomize_build("config/operator/default")))'
 	$(PYTHON) -c 'from network_operator_amd.testing.render import *; open("deployments/helm-default.yaml","w").write(dump_all(helm_template("charts/network-operator", {"config":{"amd":{"enabled":True}}}, "amd-network-operator")))'
+	$(PYTHON) -m network_operator_amd.testing.render --discovery config/operator/samples/amd-l3.yaml > deployments/discovery.yaml
+	$(PYTHON) -m network_operator_amd.testing.render --discovery config/operator/samples/amd-host-nic.yaml > deployments/discovery-host-nic.yaml
 
 bench:                      ## 1-GPU RCCL bench (driver contract); N GPUs: torchrun --nproc-per-node N bench.py --gpus N
 	$(PYTHON) bench.py --gpus 1 --steps 20 --warmup 5

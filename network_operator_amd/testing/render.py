@@ -356,3 +356,30 @@ def kustomize_build(d) -> List[dict]:
 
 def dump_all(docs: List[dict]) -> str:
     return "---\n".join(yaml.safe_dump(d, sort_keys=False) for d in docs)
+
+
+def discovery_for(policy_file, namespace: str = "amd-network-operator") -> List[dict]:
+    """The agent DaemonSet (+ ServiceAccount) the reconciler would create for a policy file —
+    what `make deployments` writes to deployments/discovery*.yaml for the Trivy config scan
+    (reference trivy.yaml scans its discovery.yaml the same way)."""
+    from network_operator_amd import discovery
+    from network_operator_amd.api.v1alpha1 import types as T
+    from network_operator_amd.operator import reconciler as R
+
+    p = T.NetworkClusterPolicy.from_dict(yaml.safe_load(Path(policy_file).read_text()))
+    ds = discovery.discovery_daemonset()
+    R.update_daemonset_for(ds, p, namespace)
+    sa = discovery.linkdiscovery_service_account()
+    sa.setdefault("metadata", {})["namespace"] = namespace
+    return [sa, ds]
+
+
+if __name__ == "__main__":
+    import argparse
+    import sys
+
+    ap = argparse.ArgumentParser(description="offline renderers")
+    ap.add_argument("--discovery", metavar="POLICY_YAML", help="agent DaemonSet for a NetworkClusterPolicy")
+    a = ap.parse_args()
+    if a.discovery:
+        sys.stdout.write(dump_all(discovery_for(a.discovery)))

@@ -223,3 +223,36 @@ def test_validation_job_manifest():
     assert c["resources"]["limits"]["amd.com/gpu"] == 8
     assert c["command"][:3] == ["python3", "-m", "network_operator_amd.validate"]
     assert job["spec"]["template"]["spec"]["nodeSelector"] == {"amd.feature.node.kubernetes.io/gpu-scale-out": "true"}
+
+
+def test_project_metadata_matches_crd():
+    """PROJECT (kubebuilder-style layout metadata) names the same API as the generated CRD."""
+    proj = yaml.safe_load((ROOT / "PROJECT").read_text())
+    crd = CRD.crd_manifest()
+    (res,) = proj["resources"]
+    assert res["group"] == crd["spec"]["group"] == proj["domain"]
+    assert res["kind"] == crd["spec"]["names"]["kind"]
+    assert res["plural"] == crd["spec"]["names"]["plural"]
+    assert res["scope"] == crd["spec"]["scope"]
+    assert [v["name"] for v in crd["spec"]["versions"]] == [res["version"]]
+
+
+def test_trivy_ignores_reference_rendered_files():
+    """Every path the Trivy ignore file names exists (rendered by `make deployments` or in-tree),
+    and the renderer for the agent DaemonSet produces the objects those entries are about."""
+    from network_operator_amd.testing.render import discovery_for
+
+    ign = yaml.safe_load((ROOT / ".trivyignore.yaml").read_text())
+    paths = {p for m in ign["misconfigurations"] for p in m.get("paths", [])}
+    rendered = {"deployments/operator.yaml", "deployments/helm-default.yaml", "deployments/discovery.yaml",
+                "deployments/discovery-host-nic.yaml"}
+    assert paths - rendered == {"build/Dockerfile.linkdiscovery"}
+    assert (ROOT / "build/Dockerfile.linkdiscovery").exists()
+    docs = discovery_for(ROOT / "config/operator/samples/amd-l3.yaml")
+    ds = _by_kind(docs, "DaemonSet")[0]
+    pod = ds["spec"]["template"]["spec"]
+    assert pod["hostNetwork"] is True
+    caps = pod["containers"][0]["securityContext"]["capabilities"]
+    assert sorted(caps["add"]) == ["NET_ADMIN", "NET_RAW"] and caps["drop"] == ["ALL"]
+    hn = _by_kind(discovery_for(ROOT / "config/operator/samples/amd-host-nic.yaml"), "DaemonSet")[0]
+    assert hn["spec"]["template"]["spec"]["containers"][0]["args"]
