@@ -47,8 +47,9 @@ tsan:                       ## ThreadSanitizer build of the agent and its unit s
 	cmake -S native -B _build-tsan -G Ninja -DNETOP_TSAN=ON -DNETOP_PYTHON=OFF -DNETOP_OUT=$(CURDIR)/_build-tsan/out && \
 	cmake --build _build-tsan -j$(JOBS) && TSAN_OPTIONS=halt_on_error=1 _build-tsan/out/bin/netop-unit-tests
 
-manifests:                  ## regenerate the CRD (kustomize base + Helm chart copy)
+manifests:                  ## regenerate the CRD and every generated kustomize / Helm manifest
 	$(PYTHON) -m network_operator_amd.api.v1alpha1.crd
+	$(PYTHON) -m network_operator_amd.packaging.manifests
 
 deployments:                ## render kustomize + Helm offline into deployments/
 	mkdir -p deployments
@@ -71,7 +72,8 @@ vet:                        ## byte-compile Python, warnings-as-errors C++ build
 	cmake -S native -B _build-vet -G Ninja -DNETOP_PYTHON=OFF -DCMAKE_CXX_FLAGS=-Werror -DNETOP_OUT=$(CURDIR)/_build-vet/out && \
 	cmake --build _build-vet -j$(JOBS)
 
-lint: vet                   ## vet + drift checks (CRD, rendered deployments)
+lint: vet                   ## vet + drift checks (CRD, generated manifests, rendered deployments)
+	$(PYTHON) -m network_operator_amd.packaging.manifests --check
 	$(PYTHON) -m pytest tests/test_packaging.py -q
 
 fuzz:                       ## property-based CR churn + LLDP / Port Description fuzzing

@@ -1,48 +1,107 @@
-"""Embedded workload templates for the link-discovery agent.
+"""Workload objects of the link-discovery agent, built in code.
 
-Counterpart of the reference's ``go:embed`` templates (reference config/discovery/discovery.go:26-81):
-the YAML files next to this module are parsed once at import time — a malformed template
-raises immediately, the equivalent of the reference's panic — and every accessor returns a
-fresh deep copy so callers can mutate freely.
+The reference embeds YAML templates with ``go:embed`` and panics if one does not parse
+(reference config/discovery/discovery.go:26-81, config/discovery/base/daemonset.yaml).  Here
+the objects are constructed from the constants below, so there is nothing to parse at run
+time; the reconciler specialises a fresh copy per policy
+(``operator/reconciler.py::update_daemonset_for``).
+
+What the agent pod needs, and why:
+
+* ``hostNetwork`` — it configures the node's own NICs and exchanges LLDP on them;
+* ``NET_ADMIN`` (rtnetlink) and ``NET_RAW`` (AF_PACKET), every other capability dropped,
+  read-only root filesystem, no privilege escalation;
+* the NFD ``features.d`` directory of the host, where the readiness label file goes;
+* a readiness probe (``discover --ready-check``) so ``status.ready`` counts nodes that are
+  actually configured, not pods that merely started (the reference's agent has no probe);
+* the resource envelope of the reference's DaemonSet (40m / 45Mi requested, 100m / 90Mi
+  limit), which the agent's measured 4.5 MiB peak RSS sits far inside.
 """
 
 from __future__ import annotations
 
-import copy
-from pathlib import Path
+from typing import Dict, List
 
-import yaml
-
-_DIR = Path(__file__).resolve().parent
-
-
-def _load(rel: str, kind: str) -> dict:
-    obj = yaml.safe_load((_DIR / rel).read_text())
-    if not isinstance(obj, dict) or obj.get("kind") != kind:
-        raise RuntimeError(f"embedded template {rel} is not a {kind}")
-    return obj
-
-
-_DAEMONSET = _load("base/daemonset.yaml", "DaemonSet")
-_SERVICE_ACCOUNT = _load("generic/linkdiscovery-serviceaccount.yaml", "ServiceAccount")
-_OPENSHIFT_ROLEBINDING = _load("openshift/rolebinding.yaml", "RoleBinding")
+AGENT_APP_LABEL = "amd-network-tools"  # pod label; the operator's pod informer selects on it
+AGENT_CONTAINER = "configurator"
+AGENT_IMAGE = "amd/amd-network-linkdiscovery:latest"
+AGENT_BINARY = "/usr/local/bin/discover"
+AGENT_SERVICE_ACCOUNT = "linkdiscovery-sa"
+OPENSHIFT_PRIVILEGED_SCC = "system:openshift:scc:privileged"
 
 LABEL_FEATURES_DIR = "/etc/kubernetes/node-feature-discovery/features.d/"
 
-
-def discovery_daemonset() -> dict:
-    """The agent DaemonSet (reference GaudiDiscoveryDaemonSet, discovery.go:35)."""
-    return copy.deepcopy(_DAEMONSET)
-
-
-def linkdiscovery_service_account() -> dict:
-    """reference GaudiLinkDiscoveryServiceAccount (discovery.go:39)."""
-    return copy.deepcopy(_SERVICE_ACCOUNT)
+AGENT_REQUESTS = {"cpu": "40m", "memory": "45Mi"}
+AGENT_LIMITS = {"cpu": "100m", "memory": "90Mi"}
+AGENT_CAPABILITIES = ["NET_ADMIN", "NET_RAW"]
+TERMINATION_GRACE_S = 10
 
 
-def openshift_role_binding() -> dict:
-    """reference OpenShiftRoleBinding (discovery.go:43)."""
-    return copy.deepcopy(_OPENSHIFT_ROLEBINDING)
+def _host_dir(name: str, path: str) -> Dict:
+    return {"name": name, "hostPath": {"path": path, "type": "DirectoryOrCreate"}}
 
 
-__all__ = ["LABEL_FEATURES_DIR", "discovery_daemonset", "linkdiscovery_service_account", "openshift_role_binding"]
+def _agent_container() -> Dict:
+    return {
+        "name": AGENT_CONTAINER,
+        "image": AGENT_IMAGE,
+        "imagePullPolicy": "IfNotPresent",
+        # NODE_NAME names the node in the agent's status file and logs (unused by the reference).
+        "env": [{"name": "NODE_NAME",
+                 "valueFrom": {"fieldRef": {"apiVersion": "v1", "fieldPath": "spec.nodeName"}}}],
+        "readinessProbe": {"exec": {"command": [AGENT_BINARY, "--ready-check"]},
+                           "initialDelaySeconds": 1, "periodSeconds": 5, "failureThreshold": 1},
+        "resources": {"limits": dict(AGENT_LIMITS), "requests": dict(AGENT_REQUESTS)},
+        "volumeMounts": [{"mountPath": LABEL_FEATURES_DIR, "name": "nfd-features"}],
+        "securityContext": {"allowPrivilegeEscalation": False, "readOnlyRootFilesystem": True,
+                            "capabilities": {"drop": ["ALL"], "add": list(AGENT_CAPABILITIES)}},
+    }
+
+
+def discovery_daemonset() -> Dict:
+    """The agent DaemonSet before specialisation (reference GaudiDiscoveryDaemonSet,
+    discovery.go:35).  One node at a time is updated (maxUnavailable 1, no surge: two agents
+    must never configure the same NICs at once)."""
+    labels = {"app": AGENT_APP_LABEL}
+    return {
+        "apiVersion": "apps/v1",
+        "kind": "DaemonSet",
+        "metadata": {"name": AGENT_APP_LABEL, "labels": dict(labels)},
+        "spec": {
+            "selector": {"matchLabels": dict(labels)},
+            "updateStrategy": {"type": "RollingUpdate", "rollingUpdate": {"maxSurge": 0, "maxUnavailable": 1}},
+            "template": {
+                "metadata": {"labels": dict(labels)},
+                "spec": {
+                    "hostNetwork": True,
+                    "volumes": [_host_dir("nfd-features", LABEL_FEATURES_DIR)],
+                    "containers": [_agent_container()],
+                    "terminationGracePeriodSeconds": TERMINATION_GRACE_S,
+                },
+            },
+        },
+    }
+
+
+def linkdiscovery_service_account() -> Dict:
+    """ServiceAccount of the agent pods (reference GaudiLinkDiscoveryServiceAccount, discovery.go:39)."""
+    return {"apiVersion": "v1", "kind": "ServiceAccount", "metadata": {"name": AGENT_SERVICE_ACCOUNT}}
+
+
+def openshift_role_binding(namespace: str = "") -> Dict:
+    """Binds the agent ServiceAccount to OpenShift's privileged SCC (reference
+    OpenShiftRoleBinding, discovery.go:43); the reconciler names it ``<policy>-sa-rb``."""
+    subject: Dict[str, str] = {"kind": "ServiceAccount", "name": AGENT_SERVICE_ACCOUNT}
+    if namespace:
+        subject["namespace"] = namespace
+    return {
+        "apiVersion": "rbac.authorization.k8s.io/v1",
+        "kind": "RoleBinding",
+        "metadata": {"name": "linkdiscovery-openshift-privileged"},
+        "roleRef": {"apiGroup": "rbac.authorization.k8s.io", "kind": "ClusterRole", "name": OPENSHIFT_PRIVILEGED_SCC},
+        "subjects": [subject],
+    }
+
+
+__all__: List[str] = ["AGENT_APP_LABEL", "LABEL_FEATURES_DIR", "discovery_daemonset", "linkdiscovery_service_account",
+                      "openshift_role_binding"]

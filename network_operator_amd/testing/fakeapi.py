@@ -77,7 +77,10 @@ def _ptr(doc, path: str):
     cur = doc
     for p in parts:
         parent = cur
-        cur = cur[int(p)] if isinstance(cur, list) else cur.get(p) if isinstance(cur, dict) else None
+        if isinstance(cur, list):
+            cur = None if p == "-" else cur[int(p)]  # "-": one past the end (RFC 6902 add)
+        else:
+            cur = cur.get(p) if isinstance(cur, dict) else None
     return parent, (parts[-1] if parts else None), cur
 
 
@@ -185,6 +188,7 @@ class FakeApiServer:
         self.tokens: Dict[str, dict] = {}                    # bearer -> {"username", "groups", "allowed"}
         self.faults: List[_Fault] = []
         self.requests: List[Tuple[str, str]] = []
+        self.accesses: set = set()                           # (verb, group, resource[/sub])
         self.admission_calls: List[Tuple[str, str]] = []
         self._runner: Optional[web.AppRunner] = None
         self.url = ""
@@ -457,6 +461,11 @@ class FakeApiServer:
             res, ns, name, sub = self._parse(path)
             if res is None:
                 return self._discovery(path)
+            verb = {"POST": "create", "PUT": "update", "PATCH": "patch", "DELETE": "delete"}.get(req.method)
+            if verb is None:
+                verb = "get" if name else ("watch" if req.query.get("watch") in ("true", "1") else "list")
+            # RBAC audit: what a ServiceAccount making these requests would need.
+            self.accesses.add((verb, res.group, res.plural + (f"/{sub}" if sub else "")))
             if res.namespaced and ns is None and req.method not in ("GET",):
                 ns = None
             m = req.method

@@ -243,3 +243,66 @@ def test_webhook_certificate_rotation_is_picked_up(tmp_path):
         assert s.cert_watcher.reloads >= 1 and first != second
 
     asyncio.run(body())
+
+
+def test_operator_requests_stay_within_generated_rbac(tmp_path, monkeypatch):
+    """Every API request the running operator makes — reconciling amd-so L2/L3 and host-nic
+    policies on OpenShift, updating and deleting them, leader election, events, authenticated
+    metrics — is allowed by the rules of operator/rbac.py, i.e. by the RBAC that the generated
+    kustomize tree and Helm chart grant its ServiceAccount.  (The reference writes role.yaml from
+    kubebuilder markers and never checks it against behaviour.)"""
+    from network_operator_amd.operator import rbac
+
+    monkeypatch.setenv("OPERATOR_NAMESPACE", "netop-test")
+    monkeypatch.setenv("ENABLE_WEBHOOKS", "false")
+    metrics = _free_port()
+
+    async def body():
+        fake = FakeApiServer(openshift=True)
+        fake.tokens = {"good": {"username": "system:serviceaccount:monitoring:prometheus", "allowed": True}}
+        url = await fake.start()
+        fake.add_node("n1", {"amd.feature.node.kubernetes.io/gpu-ready": "true"})
+        stop, started = asyncio.Event(), asyncio.Event()
+        task = asyncio.ensure_future(manager.run(
+            ["--master", url, "--leader-elect", "--health-probe-bind-address=0",
+             f"--metrics-bind-address=127.0.0.1:{metrics}", "--metrics-secure",
+             f"--webhook-cert-dir={tmp_path}/certs"], stop=stop, started=started))
+        await asyncio.wait_for(started.wait(), 10)
+        # Test-side writes go straight into the store, so only the operator's requests are audited.
+        P = kube.NETWORKCLUSTERPOLICIES
+        fake._create(P, T.new_policy("l3").to_dict(), None)
+        fake._create(P, T.new_policy("l2", layer="L2", disableNetworkManager=True).to_dict(), None)
+        fake._create(P, T.new_host_nic_policy("hn", driverImage="r/kmd:1").to_dict(), None)
+        for n in ("l3", "l2", "hn"):
+            await _until(lambda n=n: fake.get_object(kube.DAEMONSETS, n, "netop-test") is not None)
+        fake.set_agent_ready("n1")
+        await _until(lambda: fake.get_object(P, "l3")["status"]["state"] == "All good")
+        cur = fake.get_object(P, "l3")
+        cur["spec"]["amdScaleOut"]["mtu"] = 4200
+        fake._update(P, None, "l3", None, cur)
+        await _until(lambda: "--mtu=4200" in fake.get_object(kube.DAEMONSETS, "l3", "netop-test")
+                     ["spec"]["template"]["spec"]["containers"][0]["args"])
+        fake._delete(P, "hn", "")
+        ctx = ssl.create_default_context()
+        ctx.check_hostname = False
+        ctx.verify_mode = ssl.CERT_NONE
+        async with aiohttp.ClientSession() as s:
+            async with s.get(f"https://127.0.0.1:{metrics}/metrics", ssl=ctx,
+                             headers={"Authorization": "Bearer good"}) as r:
+                assert r.status == 200
+        await asyncio.sleep(0.3)
+        stop.set()
+        assert await asyncio.wait_for(task, 10) == 0
+        await fake.stop()
+        return fake.accesses
+
+    accesses = asyncio.run(asyncio.wait_for(body(), 60))
+    granted = rbac.rules(rbac.OPERATOR_CLUSTER_RULES + rbac.LEADER_ELECTION_RULES + rbac.METRICS_AUTH_RULES)
+    denied = sorted(a for a in accesses if not rbac.allows(granted, *a))
+    assert not denied, denied
+    # The audit saw the interesting paths (not a vacuous pass).
+    for a in (("create", "apps", "daemonsets"), ("update", "amd.com", "networkclusterpolicies/status"),
+              ("create", "rbac.authorization.k8s.io", "rolebindings"), ("create", "", "serviceaccounts"),
+              ("create", "coordination.k8s.io", "leases"), ("create", "authentication.k8s.io", "tokenreviews"),
+              ("watch", "", "pods"), ("create", "", "events")):
+        assert a in accesses, (a, sorted(accesses))

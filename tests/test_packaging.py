@@ -12,6 +12,7 @@ import yaml
 from network_operator_amd.api.v1alpha1 import crd as CRD
 from network_operator_amd.api.v1alpha1 import types as T
 from network_operator_amd.api.v1alpha1 import webhook as W
+from network_operator_amd.packaging import manifests as M
 from network_operator_amd.testing.render import RenderError, helm_template, kustomize_build, render_template
 
 ROOT = Path(__file__).resolve().parent.parent
@@ -46,9 +47,13 @@ def test_helm_defaults():
     dep = _by_kind(docs, "Deployment")[0]
     assert dep["metadata"]["namespace"] == "amd-net"
     c = dep["spec"]["template"]["spec"]["containers"][0]
-    assert c["args"] == ["--metrics-secure", "--metrics-bind-address=:8443", "--leader-elect",
-                         "--health-probe-bind-address=:8081"]
+    assert c["args"] == M.operator_args(metrics=True)
+    assert "--metrics-bind-address=:8443" in c["args"] and "--leader-elect" in c["args"]
     assert c["image"] == "amd/amd-network-operator:0.1.0"
+    assert c["resources"] == M.RESOURCES and c["imagePullPolicy"] == "IfNotPresent"
+    cert = _by_kind(docs, "Certificate")[0]
+    assert cert["spec"]["dnsNames"][0] == "amd-network-webhook.amd-net.svc"
+    assert dep["spec"]["template"]["spec"]["volumes"][0]["secret"]["secretName"] == cert["spec"]["secretName"]
     for wh in _by_kind(docs, "MutatingWebhookConfiguration") + _by_kind(docs, "ValidatingWebhookConfiguration"):
         rule = wh["webhooks"][0]["rules"][0]
         assert rule["resources"] == [T.PLURAL]  # fixed: the reference registers the singular
@@ -83,15 +88,22 @@ def test_helm_policy_rendering_and_validation():
 def test_kustomize_default_build():
     docs = kustomize_build(ROOT / "config/operator/default")
     dep = _by_kind(docs, "Deployment")[0]
-    assert dep["metadata"]["name"] == "amd-network-controller-manager"
+    assert dep["metadata"]["name"] == "amd-network-operator"
     assert dep["metadata"]["namespace"] == "amd-network-operator"
     pod = dep["spec"]["template"]["spec"]
     c = pod["containers"][0]
     assert c["image"] == "amd/amd-network-operator:0.1.0"
-    assert "--metrics-bind-address=:8443" in c["args"] and "--leader-elect" in c["args"]
-    assert {"containerPort": 9443, "name": "webhook-server", "protocol": "TCP"} in c["ports"]
-    assert pod["volumes"][0]["secret"]["secretName"] == "webhook-server-cert"
-    assert pod["serviceAccountName"] == "amd-network-controller-manager"
+    assert c["args"] == M.operator_args(metrics=True)  # the default overlay's metrics patch
+    assert {"containerPort": 9443, "name": "webhook", "protocol": "TCP"} in c["ports"]
+    assert {"containerPort": 8443, "name": "metrics", "protocol": "TCP"} in c["ports"]
+    assert pod["volumes"][0]["secret"]["secretName"] == "amd-network-webhook-tls"
+    assert c["volumeMounts"][0]["mountPath"] == M.CERT_DIR
+    assert pod["serviceAccountName"] == "amd-network-operator"
+    cert = _by_kind(docs, "Certificate")[0]
+    assert cert["spec"]["secretName"] == "amd-network-webhook-tls"
+    assert cert["spec"]["issuerRef"]["name"] in {d["metadata"]["name"] for d in _by_kind(docs, "Issuer")}
+    svc_names = {d["metadata"]["name"] for d in _by_kind(docs, "Service")}
+    assert cert["spec"]["dnsNames"][0].split(".")[0] in svc_names
     ns = _by_kind(docs, "Namespace")[0]
     assert ns["metadata"]["name"] == "amd-network-operator"
     for crb in _by_kind(docs, "ClusterRoleBinding") + _by_kind(docs, "RoleBinding"):
@@ -101,14 +113,41 @@ def test_kustomize_default_build():
             assert crb["roleRef"]["name"].startswith("amd-network-")
     for wh in _by_kind(docs, "MutatingWebhookConfiguration"):
         svc = wh["webhooks"][0]["clientConfig"]["service"]
-        assert svc == {"name": "amd-network-webhook-service", "namespace": "amd-network-operator",
+        assert svc == {"name": "amd-network-webhook", "namespace": "amd-network-operator",
                        "path": W.MUTATE_PATH}
         assert wh["webhooks"][0]["rules"][0]["resources"] == [T.PLURAL]
-        assert wh["metadata"]["annotations"]["cert-manager.io/inject-ca-from"].endswith("amd-network-serving-cert")
+        assert wh["metadata"]["annotations"]["cert-manager.io/inject-ca-from"] == \
+            "amd-network-operator/" + cert["metadata"]["name"]
     crd = _by_kind(docs, "CustomResourceDefinition")[0]
     assert crd == yaml.safe_load(CRD.render_yaml())
     names = {d["metadata"]["name"] for d in docs}
-    assert "amd-network-controller-manager-metrics-service" in names
+    assert "amd-network-operator-metrics" in names
+
+
+def test_generated_manifests_up_to_date():
+    """Every generated kustomize / Helm file matches the generator (`make manifests`), and no
+    stale file from an earlier layout is left in a generated directory."""
+    assert M.check() == []
+
+
+def test_kustomize_and_helm_install_the_same_operator():
+    """The two install paths come from one description: same RBAC rules, same Deployment pod
+    apart from the Helm placeholders, same webhook registrations."""
+    kz = kustomize_build(ROOT / "config/operator/default")
+    hm = helm_template(CHART, namespace="amd-network-operator")
+
+    def rules(docs):
+        return sorted((r["metadata"]["name"], yaml.safe_dump(r["rules"])) for r in _by_kind(docs, "ClusterRole"))
+
+    assert rules(kz) == rules(hm)
+    kp = _by_kind(kz, "Deployment")[0]["spec"]["template"]["spec"]
+    hp = _by_kind(hm, "Deployment")[0]["spec"]["template"]["spec"]
+    kc, hc = kp["containers"][0], hp["containers"][0]
+    assert kc["args"] == hc["args"] and kc["ports"] == hc["ports"] and kc["resources"] == hc["resources"]
+    assert kp["volumes"] == hp["volumes"] and kp["serviceAccountName"] == hp["serviceAccountName"]
+    for kind in ("MutatingWebhookConfiguration", "ValidatingWebhookConfiguration"):
+        assert _by_kind(kz, kind)[0]["webhooks"] == _by_kind(hm, kind)[0]["webhooks"]
+        assert _by_kind(kz, kind)[0]["metadata"]["annotations"] == _by_kind(hm, kind)[0]["metadata"]["annotations"]
 
 
 def test_kustomize_manifests_and_samples_validate():
