@@ -94,7 +94,9 @@ def main(argv=None) -> int:
                     help="other collectives reported at --bytes (n > 1 only)")
     ap.add_argument("--xgmi-probe", type=int, default=1, help="run the HIP xGMI link probe on rank 0 (n > 1)")
     ap.add_argument("--native-rccl", type=int, default=1, help="also run the native netop-rccl-bench harness on rank 0")
-    ap.add_argument("--extras-budget", type=float, default=240.0,
+    ap.add_argument("--rccl-env-probe", type=int, default=0,
+                    help="n > 1: also measure the 1 GiB busbw under RCCL knob variants (a fresh process each)")
+    ap.add_argument("--extras-budget", type=float, default=150.0,
                     help="seconds rank 0 may spend on the diagnostics after the timed loop (probe, native "
                          "harness, knob probe, direct all-reduce); later ones are skipped once it is spent")
     ap.add_argument("--rccl-autotune", type=int, default=0,
@@ -222,11 +224,11 @@ def main(argv=None) -> int:
             from network_operator_amd.parallel import rccl_bench
 
             rows = rccl_bench.run(op="all_reduce", gpus=world, min_bytes=1 << 20, max_bytes=1 << 30, factor=32,
-                                  iters=20, warmup=5, timeout=240)
+                                  iters=20, warmup=5, timeout=120)
             native = {"rows": [{"bytes": r.bytes, "time_us": r.time_us, "algbw_GBps": r.algbw_GBps,
                                 "busbw_GBps": r.busbw_GBps, "wrong": r.wrong} for r in rows],
                       "peak_busbw_GBps": max((r.busbw_GBps for r in rows), default=0.0)}
-            if world > 1 and budget_left():  # sensitivity of the 1 GiB busbw to RCCL knobs (diagnostic only)
+            if world > 1 and args.rccl_env_probe and budget_left():  # knob sensitivity (diagnostic only)
                 native["env_probe"] = rccl_bench.env_probe(world, 1 << 30)
         except Exception as e:
             native = {"error": str(e)[-500:]}
@@ -238,7 +240,7 @@ def main(argv=None) -> int:
         try:
             from network_operator_amd.parallel import xgmi_allreduce as XA
 
-            direct = XA.run(ranks=world, min_bytes=nbytes, max_bytes=nbytes, iters=10, warmup=3, timeout=240)
+            direct = XA.run(ranks=world, min_bytes=nbytes, max_bytes=nbytes, iters=10, warmup=3, timeout=120)
         except Exception as e:
             direct = {"error": str(e)[-500:]}
 
