@@ -244,6 +244,18 @@ def main(argv=None) -> int:
         except Exception as e:
             direct = {"error": str(e)[-500:]}
 
+    # 8. The same algorithm the way jobs run it: one process per GPU, HIP IPC symmetric buffers,
+    #    host-ordered phases (parallel/xgmi_comm.py), in its own process group so a failure there
+    #    cannot take this run down.  Exact check of three seeds per size, both algorithms.
+    direct_mp = None
+    if rank == 0 and world > 1 and args.device == "cuda" and args.xgmi_allreduce and budget_left():
+        try:
+            from network_operator_amd.parallel import xgmi_comm
+
+            direct_mp = xgmi_comm.run(world, nbytes=nbytes, min_bytes=1 << 20, iters=10, warmup=3, timeout=120)
+        except Exception as e:
+            direct_mp = {"error": str(e)[-500:]}
+
     node_ready = None
     node_ready_note = None
     if rank == 0 and args.node_ready != "off":
@@ -285,6 +297,7 @@ def main(argv=None) -> int:
             "native_rccl": native,
             "rccl_autotune": tuned if args.device == "cuda" else None,
             "xgmi_allreduce": direct,
+            "xgmi_allreduce_multiprocess": direct_mp,
             "algbw_GBps": algbw,
             "busbw_GBps": busbw,
             "busbw_ceiling_GBps": ceiling,

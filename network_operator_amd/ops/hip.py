@@ -48,6 +48,24 @@ def lib() -> ctypes.CDLL:
             L.netop_xgmi_probe_push.argtypes = [u64, i32, i32, ctypes.POINTER(ctypes.c_double),
                                                 ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_ulonglong)]
             L.netop_xgmi_probe_push.restype = i32
+            # xgmi_comm.hip: IPC buffers, multi-pair copy, node-local barrier
+            L.netop_ipc_handle_size.restype = i32
+            L.netop_ipc_export.argtypes = [vp, vp, ctypes.POINTER(u64)]
+            L.netop_ipc_export.restype = i32
+            L.netop_ipc_open.argtypes = [vp, u64, ctypes.POINTER(vp), ctypes.POINTER(vp)]
+            L.netop_ipc_open.restype = i32
+            L.netop_ipc_close.argtypes = [vp]
+            L.netop_ipc_close.restype = i32
+            L.netop_multi_copy.argtypes = [ctypes.POINTER(vp), ctypes.POINTER(vp), i32, u64, i32, vp]
+            L.netop_multi_copy.restype = i32
+            L.netop_shm_barrier_open.argtypes = [ctypes.c_char_p, i32, i32]
+            L.netop_shm_barrier_open.restype = vp
+            L.netop_shm_barrier_wait.argtypes = [vp, i32]
+            L.netop_shm_barrier_wait.restype = i32
+            L.netop_shm_barrier_close.argtypes = [vp]
+            L.netop_shm_barrier_close.restype = None
+            L.netop_shm_unlink.argtypes = [ctypes.c_char_p]
+            L.netop_shm_unlink.restype = i32
             _lib = L
     return _lib
 

@@ -1,0 +1,347 @@
+"""Direct xGMI all-reduce for one-process-per-GPU jobs (the way torch.distributed runs).
+
+An MI355X node is a full mesh: every GPU has its own xGMI link to each of its 7 peers.  A
+two-shot all-reduce in which every GPU reads from every peer at once loads all 7 links by
+construction (ring algorithms need many concurrent rings to do the same):
+
+    reduce-scatter  rank d sums chunk d of all n inputs, read straight from the peers' input
+                    buffers over xGMI (peer pointers, fp32 accumulation, bf16 RNE);
+    all-gather      rank d pulls every other reduced chunk from the rank that owns it.
+
+``one_shot`` instead has every rank sum the whole message from all inputs (one phase, n-1 times
+the link traffic): the better choice for small messages, where phase overhead dominates.
+
+Each rank owns two *symmetric* buffers (input, output) allocated once, exported with HIP IPC
+and mapped by every peer (``native/hip/xgmi_comm.hip``).  Callers write the message into
+``comm.input(numel)`` and read the result from the returned ``comm.output(numel)`` view, as
+with symmetric-memory collectives.  Phases are ordered on the host — stream synchronize, a
+node-local shared-memory barrier, next launch — so no kernel spins on a peer's flag: a rank
+that dies costs its peers a barrier timeout (an exception), not a hung GPU.
+
+Bootstrap needs only a host process group (gloo) for the handle exchange; RCCL is not used.
+Reference counterpart: none — the reference only writes the collective library's config
+(reference cmd/discover/gaudinet.go); this is the MI355X-side proof that the fabric the
+operator verified carries collectives at link speed.
+
+    python -m network_operator_amd.parallel.xgmi_comm --world 8 --bytes 1073741824
+    python -m network_operator_amd.parallel.xgmi_comm --world 2 --devices 0,0   # virtual ranks
+"""
+
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import socket
+import subprocess
+import sys
+import tempfile
+import time
+import uuid
+from typing import List, Optional
+
+from ..ops import hip as H
+
+ALGOS = ("two_shot", "one_shot")
+MAX_RANKS = 8
+
+
+class ShmBarrier:
+    """Node-local sense-reversing barrier in POSIX shared memory (a few µs, vs ~100 µs for a
+    gloo barrier).  Rank 0 creates the segment and unlinks its name once everyone mapped it."""
+
+    def __init__(self, rank: int, world: int, group, name: Optional[str] = None):
+        import torch.distributed as dist
+
+        L = H.lib()
+        names: List[Optional[str]] = [name or f"/netop-xgmi-{uuid.uuid4().hex[:16]}"]
+        dist.broadcast_object_list(names, src=0, group=group)
+        self.name = names[0]
+        self._h = None
+        if rank == 0:
+            self._h = L.netop_shm_barrier_open(self.name.encode(), world, 1)
+            if not self._h:
+                raise OSError(ctypes.get_errno(), f"shm_open({self.name}) failed")
+        dist.barrier(group=group)
+        if rank != 0:
+            self._h = L.netop_shm_barrier_open(self.name.encode(), world, 0)
+        ok = [bool(self._h)]
+        oks: List[Optional[List[bool]]] = [None] * world
+        dist.all_gather_object(oks, ok, group=group)
+        if rank == 0:
+            L.netop_shm_unlink(self.name.encode())  # mappings stay; nothing is left in /dev/shm
+        if not all(o[0] for o in oks):
+            self.close()
+            raise OSError(f"could not map the barrier segment {self.name} on every rank")
+
+    def wait(self, timeout_s: float = 60.0) -> None:
+        rc = H.lib().netop_shm_barrier_wait(self._h, int(timeout_s * 1000))
+        if rc:
+            raise TimeoutError(f"xGMI all-reduce barrier: a peer did not arrive within {timeout_s} s (rc {rc})")
+
+    def close(self) -> None:
+        if self._h:
+            H.lib().netop_shm_barrier_close(self._h)
+            self._h = None
+
+
+class XgmiAllReduce:
+    """Symmetric-buffer all-reduce over the node's xGMI mesh (bf16 sum)."""
+
+    def __init__(self, capacity_bytes: int, group=None, device=None, timeout_s: float = 60.0, wg_per_cu: int = 4):
+        import torch
+        import torch.distributed as dist
+
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        if not 1 <= self.world <= MAX_RANKS:
+            raise ValueError(f"1..{MAX_RANKS} ranks (one node) supported, got {self.world}")
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.timeout_s = timeout_s
+        self.wg_per_cu = wg_per_cu
+        self.capacity = (int(capacity_bytes) + 255) // 256 * 256
+        L = H.lib()
+        self.inp = torch.empty(self.capacity, dtype=torch.uint8, device=self.device)
+        self.out = torch.empty(self.capacity, dtype=torch.uint8, device=self.device)
+        hsz = L.netop_ipc_handle_size()
+        mine = []
+        for t in (self.inp, self.out):
+            h = ctypes.create_string_buffer(hsz)
+            off = ctypes.c_uint64()
+            H._check(L.netop_ipc_export(ctypes.c_void_p(t.data_ptr()), h, ctypes.byref(off)), "netop_ipc_export")
+            mine.append((h.raw, off.value))
+        allh: List[Optional[list]] = [None] * self.world
+        dist.all_gather_object(allh, mine, group=group)
+        self._opened: List[int] = []
+        self.peer_in: List[int] = []
+        self.peer_out: List[int] = []
+        try:
+            for p in range(self.world):
+                if p == self.rank:
+                    self.peer_in.append(self.inp.data_ptr())
+                    self.peer_out.append(self.out.data_ptr())
+                    continue
+                for (raw, off), dst in zip(allh[p], (self.peer_in, self.peer_out)):
+                    ptr, base = ctypes.c_void_p(), ctypes.c_void_p()
+                    H._check(L.netop_ipc_open(raw, off, ctypes.byref(ptr), ctypes.byref(base)), "netop_ipc_open")
+                    self._opened.append(base.value)
+                    dst.append(ptr.value)
+            self.barrier = ShmBarrier(self.rank, self.world, group)
+        except Exception:
+            self._close_handles()
+            raise
+
+    # -- buffers ----------------------------------------------------------------------------------
+    def _view(self, buf, numel: int):
+        import torch
+
+        if numel * 2 > self.capacity:
+            raise ValueError(f"{numel} bf16 elements exceed the {self.capacity}-byte symmetric buffer")
+        return buf[: numel * 2].view(torch.bfloat16)
+
+    def input(self, numel: int):
+        """This rank's contribution goes here (a bf16 view of the symmetric input buffer)."""
+        return self._view(self.inp, numel)
+
+    def output(self, numel: int):
+        return self._view(self.out, numel)
+
+    # -- collective -------------------------------------------------------------------------------
+    def _sync_and_wait(self, stream) -> None:
+        stream.synchronize()
+        self.barrier.wait(self.timeout_s)
+
+    def all_reduce(self, numel: int, algo: str = "two_shot"):
+        """Sum of every rank's ``input(numel)``, returned as ``output(numel)`` on every rank."""
+        import torch
+
+        if algo not in ALGOS:
+            raise ValueError(f"algo must be one of {ALGOS}")
+        n, d = self.world, self.rank
+        align = 8 * n if algo == "two_shot" else 8
+        if numel % align:
+            raise ValueError(f"numel must be a multiple of {align} for {algo}")
+        self._view(self.inp, numel)  # capacity check
+        L = H.lib()
+        stream = torch.cuda.current_stream(self.device)
+        s = ctypes.c_void_p(stream.cuda_stream)
+        vp = ctypes.c_void_p
+        self._sync_and_wait(stream)  # every input is complete
+        if algo == "one_shot" or n == 1:
+            srcs = (vp * n)(*[vp(p) for p in self.peer_in])
+            H._check(L.netop_sum_bf16(srcs, n, vp(self.out.data_ptr()), numel, self.wg_per_cu, s), "netop_sum_bf16")
+            self._sync_and_wait(stream)  # nobody reads my input any more
+            return self.output(numel)
+        chunk = numel // n
+        cb = chunk * 2
+        srcs = (vp * n)(*[vp(p + d * cb) for p in self.peer_in])
+        H._check(L.netop_sum_bf16(srcs, n, vp(self.out.data_ptr() + d * cb), chunk, self.wg_per_cu, s),
+                 "netop_sum_bf16")
+        self._sync_and_wait(stream)  # every reduced chunk is complete
+        peers = [p for p in range(n) if p != d]
+        src = (vp * len(peers))(*[vp(self.peer_out[p] + p * cb) for p in peers])
+        dst = (vp * len(peers))(*[vp(self.out.data_ptr() + p * cb) for p in peers])
+        H._check(L.netop_multi_copy(src, dst, len(peers), cb, self.wg_per_cu, s), "netop_multi_copy")
+        self._sync_and_wait(stream)  # nobody reads my output any more
+        return self.output(numel)
+
+    # -- lifetime ---------------------------------------------------------------------------------
+    def _close_handles(self) -> None:
+        L = H.lib()
+        for base in self._opened:
+            L.netop_ipc_close(ctypes.c_void_p(base))
+        self._opened = []
+
+    def close(self) -> None:
+        import torch.distributed as dist
+
+        # Peers may still be mapped onto our buffers until they are past their last phase.
+        dist.barrier(group=self.group)
+        self._close_handles()
+        if getattr(self, "barrier", None):
+            self.barrier.close()
+
+
+# ---------------------------------------------------------------------------------------------
+# Benchmark / self-test: `--world N` spawns N ranks (env RANK / WORLD_SIZE, gloo bootstrap)
+# ---------------------------------------------------------------------------------------------
+def _worker(args) -> int:
+    import torch
+    import torch.distributed as dist
+
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    devices = [int(x) for x in args.devices.split(",")] if args.devices else list(range(world))
+    dev = torch.device("cuda", devices[rank % len(devices)])
+    torch.cuda.set_device(dev)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sizes = []
+    b = args.min_bytes
+    while b <= args.bytes:
+        sizes.append(b)
+        b *= 4
+    if not sizes or sizes[-1] != args.bytes:
+        sizes.append(args.bytes)
+    comm = XgmiAllReduce(args.bytes, device=dev, timeout_s=args.timeout)
+    rows = []
+    for nbytes in sizes:
+        for algo in args.algos.split(","):
+            align = 8 * world if algo == "two_shot" else 8
+            numel = max(align, nbytes // 2 // align * align)
+            wrong = 0
+            for seed in (11, 12, 13):  # same buffers, three seeds: stale peer lines cannot pass
+                H.fill_pattern(comm.input(numel), seed, rank)
+                outv = comm.all_reduce(numel, algo)
+                wrong += H.verify_sum(outv, seed, world)
+            for _ in range(args.warmup):
+                comm.all_reduce(numel, algo)
+            torch.cuda.synchronize(dev)
+            comm.barrier.wait(args.timeout)
+            t0 = time.perf_counter()
+            for _ in range(args.iters):
+                comm.all_reduce(numel, algo)
+            torch.cuda.synchronize(dev)
+            dt = (time.perf_counter() - t0) / args.iters
+            t = torch.tensor([dt], dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            w = torch.tensor([wrong], dtype=torch.int64)
+            dist.all_reduce(w, op=dist.ReduceOp.SUM)
+            dt, wrong = float(t[0]), int(w[0])
+            algbw = numel * 2 / dt / 1e9
+            rows.append({"algo": algo, "bytes": numel * 2, "time_us": dt * 1e6, "algbw_GBps": algbw,
+                         "busbw_GBps": algbw * 2 * (world - 1) / world, "wrong": wrong})
+    comm.close()
+    if rank == 0:
+        devs = sorted({devices[r % len(devices)] for r in range(world)})
+        print(json.dumps({"ranks": world, "gpus": devs, "rows": rows,
+                          "peak_busbw_GBps": max((r["busbw_GBps"] for r in rows), default=0.0),
+                          "wrong": sum(r["wrong"] for r in rows)}), flush=True)
+    dist.destroy_process_group()
+    return 0
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+_LAUNCHER_ENV = ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK", "ROLE_WORLD_SIZE",
+                 "MASTER_ADDR", "MASTER_PORT", "GROUP_WORLD_SIZE", "ROLE_NAME")
+
+
+def run(world: int, nbytes: int = 1 << 30, min_bytes: Optional[int] = None, iters: int = 10, warmup: int = 3,
+        algos: str = "two_shot,one_shot", devices: Optional[str] = None, timeout: float = 120.0) -> dict:
+    """Spawns `world` rank processes (one per GPU unless `devices` maps several onto one) and
+    returns rank 0's result.  Safe to call from inside another distributed job: the children
+    get their own rendezvous and none of the parent's launcher variables."""
+    port = _free_port()
+    base = {k: v for k, v in os.environ.items() if k not in _LAUNCHER_ENV and not k.startswith("TORCHELASTIC_")}
+    base.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world))
+    cmd = [sys.executable, "-m", "network_operator_amd.parallel.xgmi_comm", "--worker", "--bytes", str(nbytes),
+           "--min-bytes", str(min_bytes or nbytes), "--iters", str(iters), "--warmup", str(warmup), "--algos", algos,
+           "--timeout", str(min(timeout, 60.0))]
+    if devices:
+        cmd += ["--devices", devices]
+    root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    base["PYTHONPATH"] = root + (os.pathsep + base["PYTHONPATH"] if base.get("PYTHONPATH") else "")
+    # Output goes to temporary files, not pipes: a rank blocked on a full pipe would stall the
+    # barrier of every other rank.
+    logs = [tempfile.TemporaryFile(mode="w+") for _ in range(world)]
+    procs = [subprocess.Popen(cmd, env=dict(base, RANK=str(r), LOCAL_RANK=str(r)), stdout=logs[r],
+                              stderr=subprocess.STDOUT, text=True, cwd=root) for r in range(world)]
+    deadline = time.monotonic() + timeout
+    try:
+        for p in procs:
+            p.wait(timeout=max(1.0, deadline - time.monotonic()))
+    except subprocess.TimeoutExpired:
+        for p in procs:
+            p.kill()
+        for p in procs:
+            p.wait()
+        raise TimeoutError(f"xGMI all-reduce benchmark did not finish within {timeout} s")
+    outs = []
+    for f in logs:
+        f.seek(0)
+        outs.append(f.read())
+        f.close()
+    bad = [(r, p.returncode, o[-1500:]) for r, (p, o) in enumerate(zip(procs, outs)) if p.returncode != 0]
+    if bad:
+        raise RuntimeError(f"rank {bad[0][0]} exited {bad[0][1]}: {bad[0][2]}")
+    line = [x for x in outs[0].splitlines() if x.startswith("{")]
+    if not line:
+        raise RuntimeError(f"no result from rank 0: {outs[0][-1500:]}")
+    return json.loads(line[-1])
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(prog="python -m network_operator_amd.parallel.xgmi_comm")
+    ap.add_argument("--world", type=int, default=0, help="spawn this many ranks (0: all visible GPUs)")
+    ap.add_argument("--worker", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--bytes", type=int, default=1 << 30)
+    ap.add_argument("--min-bytes", type=int, default=0)
+    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--algos", default="two_shot,one_shot")
+    ap.add_argument("--devices", default="", help="comma list of GPU ids per rank (repeats allowed: virtual ranks)")
+    ap.add_argument("--timeout", type=float, default=120.0)
+    a = ap.parse_args(argv)
+    if a.worker:
+        if not a.min_bytes:
+            a.min_bytes = a.bytes
+        return _worker(a)
+    world = a.world
+    if world <= 0:
+        import torch
+
+        world = torch.cuda.device_count()
+    print(json.dumps(run(world, a.bytes, a.min_bytes or None, a.iters, a.warmup, a.algos, a.devices or None,
+                         a.timeout)))
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

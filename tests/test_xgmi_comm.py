@@ -1,0 +1,63 @@
+"""Multi-process direct xGMI all-reduce (network_operator_amd/parallel/xgmi_comm.py).
+
+CPU: the node-local shared-memory barrier that orders the phases, across real processes
+(tests/xgmi_barrier_worker.py).  GPU: the full IPC all-reduce with several rank processes
+mapped onto the one GPU of the test box ("virtual ranks"), exact against the pattern sum for
+three seeds on reused buffers, both algorithms, and a non-power-of-two rank count."""
+
+import json
+import os
+import socket
+import subprocess
+import sys
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parent.parent
+WORKER = Path(__file__).resolve().parent / "xgmi_barrier_worker.py"
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _ranks(world, args):
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_port()), WORLD_SIZE=str(world),
+               PYTHONPATH=str(ROOT))
+    procs = [subprocess.Popen([sys.executable, str(WORKER), *args], env=dict(env, RANK=str(r)),
+                              stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for r in range(world)]
+    outs = [p.communicate(timeout=120) for p in procs]
+    for p, (_, err) in zip(procs, outs):
+        assert p.returncode == 0, err[-2000:]
+    # each rank's "RESULT ..." line (gloo logs to stdout as well)
+    return [next((ln[len("RESULT "):] for ln in o.splitlines() if ln.startswith("RESULT ")), "") for o, _ in outs]
+
+
+def test_shm_barrier_orders_phases_across_processes(tmp_path):
+    outs = _ranks(4, ["order", str(tmp_path)])
+    assert all(o.startswith("ok") for o in outs)
+    name = outs[0].split()[1]
+    assert not Path("/dev/shm" + name).exists()  # unlinked once every rank had mapped it
+
+
+def test_shm_barrier_times_out_instead_of_hanging():
+    word, secs = _ranks(2, ["timeout"])[0].split()
+    assert word == "timeout" and 0.4 <= float(secs) < 5
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3])
+def test_xgmi_allreduce_multiprocess_virtual_ranks(cuda_device, world):
+    from network_operator_amd.parallel import xgmi_comm
+
+    r = xgmi_comm.run(world, nbytes=16 << 20, min_bytes=1 << 12, iters=3, warmup=1,
+                      devices=",".join(["0"] * world), timeout=110)
+    assert r["ranks"] == world and r["gpus"] == [0]
+    assert r["wrong"] == 0, json.dumps(r)
+    assert {x["algo"] for x in r["rows"]} == {"two_shot", "one_shot"}
+    assert all(x["time_us"] > 0 for x in r["rows"])
