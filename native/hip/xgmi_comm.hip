@@ -40,8 +40,9 @@ struct CopyPairs {
 __global__ __launch_bounds__(kThreads) void multi_copy_kernel(CopyPairs pairs, uint64_t n_vec) {
     const uint4* __restrict__ s = pairs.src[blockIdx.y];
     uint4* __restrict__ d = pairs.dst[blockIdx.y];
+    // Each workgroup covers 2 x kThreads consecutive vectors per step.
     const uint64_t stride = uint64_t(gridDim.x) * kThreads * 2;
-    for (uint64_t i = uint64_t(blockIdx.x) * kThreads + threadIdx.x; i < n_vec; i += stride) {
+    for (uint64_t i = uint64_t(blockIdx.x) * kThreads * 2 + threadIdx.x; i < n_vec; i += stride) {
         const uint64_t j = i + uint64_t(kThreads);
         uint4 a = s[i];
         uint4 b;

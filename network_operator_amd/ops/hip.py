@@ -162,6 +162,27 @@ def copy(src, dst) -> None:
            "netop_copy")
 
 
+def multi_copy(srcs, dsts, wg_per_cu: int = 0) -> None:
+    """``dsts[k] <- srcs[k]`` for up to 8 equal-size pairs in one launch (the all-gather step of
+    the multi-process xGMI all-reduce; sources may be peer memory)."""
+    if len(srcs) != len(dsts) or len(srcs) > 8:
+        raise ValueError("up to 8 (src, dst) pairs")
+    if not srcs:
+        return
+    nbytes = srcs[0].numel() * srcs[0].element_size()
+    for s, d in zip(srcs, dsts):
+        if not (s.is_cuda and d.is_cuda and s.is_contiguous() and d.is_contiguous()):
+            raise ValueError("contiguous CUDA tensors expected")
+        if s.numel() * s.element_size() != nbytes or d.numel() * d.element_size() != nbytes:
+            raise ValueError("all pairs must have the same byte size")
+        if s.data_ptr() % 16 or d.data_ptr() % 16 or nbytes % 16:
+            raise ValueError("16-byte aligned buffers and sizes expected")
+    vp = ctypes.c_void_p
+    a = (vp * len(srcs))(*[vp(s.data_ptr()) for s in srcs])
+    b = (vp * len(dsts))(*[vp(d.data_ptr()) for d in dsts])
+    _check(lib().netop_multi_copy(a, b, len(srcs), nbytes, wg_per_cu, _stream(dsts[0])), "netop_multi_copy")
+
+
 def xgmi_probe(nbytes: int = 256 << 20, iters: int = 10, max_gpus: int = 8) -> dict:
     """Pull-bandwidth and integrity probe over every visible GPU pair (see netop_hip.hip)."""
     n = 64

@@ -201,3 +201,22 @@ def test_fabric_validation_single_gpu(cuda_device, tmp_path):
     names = [c["check"] for c in rep["checks"]]
     assert names[:3] == ["xgmi_topology", "xgmi_probe", "rccl_all_reduce"]
     assert (tmp_path / validate.LABEL_FILE).read_text().startswith(validate.LABEL + "=true\n")
+
+
+@pytest.mark.parametrize("pairs,nbytes,wg", [(1, 16, 0), (3, 4096 + 16, 0), (7, 3 << 20, 0), (8, (5 << 20) + 48, 1)])
+def test_multi_copy_matches_torch(cuda_device, pairs, nbytes, wg):
+    """One launch copying up to 8 pairs: sizes that need one, several and many workgroups per
+    pair (the grid-stride indexing covers every vector exactly once), vs torch's copy."""
+    import torch
+
+    from network_operator_amd.ops import hip
+
+    g = torch.Generator(device=cuda_device).manual_seed(pairs)
+    srcs = [torch.randint(0, 256, (nbytes,), dtype=torch.uint8, device=cuda_device, generator=g) for _ in range(pairs)]
+    dsts = [torch.zeros(nbytes, dtype=torch.uint8, device=cuda_device) for _ in range(pairs)]
+    hip.multi_copy(srcs, dsts, wg_per_cu=wg)
+    torch.cuda.synchronize()
+    for s, d in zip(srcs, dsts):
+        assert torch.equal(s, d)
+    with pytest.raises(ValueError):
+        hip.multi_copy(srcs[:1], [torch.zeros(nbytes + 16, dtype=torch.uint8, device=cuda_device)])
