@@ -3,7 +3,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 300 python3 -u -m pytest tests/test_xgmi_comm.py -m gpu -x -v --timeout 150 --timeout-method thread > gpurun_out/xcomm_pytest.log 2>&1; rc=$?
+timeout -k 10 300 python3 -u -m pytest tests/test_xgmi_comm.py tests/test_gpu_ops.py -k "multi_copy or multiprocess" -m gpu -x -v --timeout 150 --timeout-method thread > gpurun_out/xcomm_pytest.log 2>&1; rc=$?
 tail -8 gpurun_out/xcomm_pytest.log
 [ $rc -eq 0 ] || exit $rc
 timeout -k 10 240 python3 -m network_operator_amd.parallel.xgmi_comm --world 8 --devices 0,0,0,0,0,0,0,0 \
