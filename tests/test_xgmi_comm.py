@@ -61,3 +61,16 @@ def test_xgmi_allreduce_multiprocess_virtual_ranks(cuda_device, world):
     assert r["wrong"] == 0, json.dumps(r)
     assert {x["algo"] for x in r["rows"]} == {"two_shot", "one_shot"}
     assert all(x["time_us"] > 0 for x in r["rows"])
+
+
+@pytest.mark.gpu
+def test_xgmi_allreduce_spawned_from_inside_a_torchrun_job(cuda_device):
+    """bench.py's n > 1 path: a torchrun-launched rank starts the multi-process all-reduce in
+    its own process group; the launcher's RANK / MASTER_PORT / TORCHELASTIC_* must not leak."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1", "--master-addr",
+           "127.0.0.1", "--master-port", str(_port()), str(WORKER), "nested"]
+    r = subprocess.run(cmd, env=dict(os.environ, PYTHONPATH=str(ROOT)), capture_output=True, text=True, timeout=140)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = next(ln for ln in r.stdout.splitlines() if ln.startswith("RESULT "))
+    res = json.loads(line[len("RESULT "):])
+    assert res == {"launcher_rank": "0", "wrong": 0, "ranks": 2}

@@ -41,5 +41,17 @@ def main() -> None:
     dist.destroy_process_group()
 
 
+def nested() -> None:
+    """Inside a torchrun-launched rank (as bench.py rank 0 does): spawn a 2-rank virtual
+    all-reduce on GPU 0 with its own rendezvous, untouched by this job's launcher variables."""
+    import json
+
+    from network_operator_amd.parallel import xgmi_comm
+
+    r = xgmi_comm.run(2, nbytes=4 << 20, min_bytes=4 << 20, iters=2, warmup=1, devices="0,0", timeout=100)
+    print("RESULT " + json.dumps({"launcher_rank": os.environ.get("RANK"), "wrong": r["wrong"], "ranks": r["ranks"]}),
+          flush=True)
+
+
 if __name__ == "__main__":
-    main()
+    nested() if sys.argv[1:] == ["nested"] else main()
