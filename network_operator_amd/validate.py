@@ -4,7 +4,7 @@ The agent configures the node and checks what it can see without touching a GPU:
 xGMI topology, GPUDirect RDMA support and LLDP peers.  This is the GPU-side counterpart.  It
 runs where the GPUs are (a Job with ``amd.com/gpu: 8``, see ``config/validation/``) and
 answers one question: do the links actually carry collectives at the expected speed?  It runs
-five checks:
+these checks:
 
 1. **Topology.**  KFD: every GPU pair is xGMI-linked.
 2. **xGMI probe** (``netop-xgmi-probe``).  Per-link pull bandwidth, all-peers pull and push
@@ -13,7 +13,10 @@ five checks:
    With n > 1 the large-message busbw must reach ``--min-busbw``.
 4. **Counters** (amd-smi).  Every up xGMI link moved data during the RCCL run.  This is the
    "RCCL sees every link" check from BASELINE.json.
-5. **Optionally, the label.**  If everything passed, the NFD label
+5. **Direct xGMI all-reduce** (``parallel/xgmi_comm.py``).  The one-process-per-GPU
+   all-reduce over HIP IPC buffers that jobs can use, every size checked exactly (after the
+   counter window, so check 4 still sees RCCL traffic only).
+6. **Optionally, the label.**  If everything passed, the NFD label
    ``amd.feature.node.kubernetes.io/gpu-fabric-validated=true`` is written, along with the
    measured busbw.
 
@@ -105,6 +108,16 @@ def run(gpus: int, min_busbw: float, min_link_GBps: float, max_bytes: int, sysfs
         except Exception as e:
             checks.append(_check("xgmi_counters", False, error=str(e)))
 
+    # 5. The direct xGMI all-reduce jobs can use (one process per GPU, HIP IPC buffers), exact.
+    try:
+        from .parallel import xgmi_comm
+
+        d = xgmi_comm.run(gpus, nbytes=max_bytes, min_bytes=1 << 20, iters=5, warmup=2, timeout=min(timeout, 300))
+        checks.append(_check("xgmi_direct_all_reduce", d["wrong"] == 0, peak_busbw_GBps=d["peak_busbw_GBps"],
+                             wrong=d["wrong"], sizes=[{k: r[k] for k in ("algo", "bytes", "time_us", "busbw_GBps")}
+                                                      for r in d["rows"]]))
+    except Exception as e:
+        checks.append(_check("xgmi_direct_all_reduce", False, error=str(e)[-500:]))
     report["checks"] = checks
     report["ok"] = all(c["ok"] for c in checks)
     report["seconds"] = time.time() - report.pop("started")

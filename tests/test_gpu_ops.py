@@ -200,6 +200,7 @@ def test_fabric_validation_single_gpu(cuda_device, tmp_path):
     assert rep["ok"], rep
     names = [c["check"] for c in rep["checks"]]
     assert names[:3] == ["xgmi_topology", "xgmi_probe", "rccl_all_reduce"]
+    assert names[-1] == "xgmi_direct_all_reduce"
     assert (tmp_path / validate.LABEL_FILE).read_text().startswith(validate.LABEL + "=true\n")
 
 
