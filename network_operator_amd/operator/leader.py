@@ -12,7 +12,6 @@ from __future__ import annotations
 import asyncio
 import datetime as dt
 import logging
-import os
 import socket
 import uuid
 from typing import Awaitable, Callable, Optional

@@ -7,7 +7,6 @@ ownerRef garbage collection, conflicts, watch recovery, leader election, metrics
 
 import asyncio
 import contextlib
-import os
 
 import pytest
 
