@@ -119,7 +119,28 @@ def openapi_schema() -> dict:
         "description": "NetworkClusterPolicyStatus defines the observed state of NetworkClusterPolicy",
         "type": "object",
         "properties": {
+            "conditions": {
+                "description": ("Standard conditions: Ready (every targeted node is configured and "
+                                "labelled) and Degraded (node or dependency errors; see errors)."),
+                "type": "array",
+                "x-kubernetes-list-type": "map",
+                "x-kubernetes-list-map-keys": ["type"],
+                "items": {
+                    "type": "object",
+                    "properties": {
+                        "type": {"type": "string", "maxLength": 316},
+                        "status": {"type": "string", "enum": ["True", "False", "Unknown"]},
+                        "observedGeneration": {"type": "integer", "format": "int64", "minimum": 0},
+                        "lastTransitionTime": {"type": "string", "format": "date-time"},
+                        "reason": {"type": "string", "maxLength": 1024},
+                        "message": {"type": "string", "maxLength": 32768},
+                    },
+                    "required": ["type", "status", "lastTransitionTime", "reason", "message"],
+                },
+            },
             "errors": {"items": {"type": "string"}, "type": "array"},
+            "observedGeneration": {"description": "The spec generation the status describes.",
+                                   "format": "int64", "type": "integer"},
             "ready": {"format": "int32", "type": "integer"},
             "state": {"type": "string"},
             "targets": {"format": "int32", "type": "integer"},

@@ -201,15 +201,28 @@ class NetworkClusterPolicyStatus:
     ready: int = 0
     state: str = ""
     errors: List[str] = field(default_factory=list)
+    # Additive (not in the reference): standard conditions and the generation they describe.
+    conditions: List[dict] = field(default_factory=list)
+    observedGeneration: int = 0
 
     def to_dict(self) -> dict:
-        return {"targets": self.targets, "ready": self.ready, "state": self.state, "errors": list(self.errors)}
+        d = {"targets": self.targets, "ready": self.ready, "state": self.state, "errors": list(self.errors)}
+        if self.conditions:
+            d["conditions"] = [dict(c) for c in self.conditions]
+        if self.observedGeneration:
+            d["observedGeneration"] = self.observedGeneration
+        return d
 
     @classmethod
     def from_dict(cls, d: Optional[dict]) -> "NetworkClusterPolicyStatus":
         d = d or {}
         return cls(targets=int(d.get("targets", 0) or 0), ready=int(d.get("ready", 0) or 0),
-                   state=d.get("state", "") or "", errors=list(d.get("errors") or []))
+                   state=d.get("state", "") or "", errors=list(d.get("errors") or []),
+                   conditions=[dict(c) for c in d.get("conditions") or []],
+                   observedGeneration=int(d.get("observedGeneration", 0) or 0))
+
+    def condition(self, type_: str) -> Optional[dict]:
+        return next((c for c in self.conditions if c.get("type") == type_), None)
 
 
 @dataclass

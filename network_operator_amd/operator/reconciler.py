@@ -47,6 +47,8 @@ L3_WAIT = "90s"
 STATE_NO_TARGETS = "No targets"
 STATE_WORKING = "Working on it.."
 STATE_ALL_GOOD = "All good"
+COND_READY = "Ready"
+COND_DEGRADED = "Degraded"
 
 # Volumes the reconciler manages (the template's nfd-features is never touched).
 MANAGED_VOLUMES = ("var-run-dbus", "networkmanager", "rccl-artifacts")
@@ -292,6 +294,49 @@ def status_for(targets: int, ready: int) -> str:
     return STATE_ALL_GOOD
 
 
+def _now_rfc3339() -> str:
+    import datetime
+
+    return datetime.datetime.now(datetime.timezone.utc).strftime("%Y-%m-%dT%H:%M:%SZ")
+
+
+def _set_condition(conds: List[dict], type_: str, status: str, reason: str, message: str, generation: int,
+                   now: str) -> None:
+    """meta.SetStatusCondition: lastTransitionTime moves only when the status flips."""
+    for c in conds:
+        if c["type"] == type_:
+            if c.get("status") != status:
+                c["lastTransitionTime"] = now
+            c.update(status=status, reason=reason, message=message, observedGeneration=generation)
+            return
+    conds.append({"type": type_, "status": status, "observedGeneration": generation, "lastTransitionTime": now,
+                  "reason": reason, "message": message})
+
+
+def policy_conditions(current: List[dict], targets: int, ready: int, errors: List[str], generation: int,
+                      now: Optional[str] = None) -> List[dict]:
+    """The policy's Ready / Degraded conditions (additive to the reference's state string,
+    which stays as it is for parity, reference networkconfiguration_controller.go:289-295)."""
+    now = now or _now_rfc3339()
+    conds = [dict(c) for c in current if c.get("type") in (COND_READY, COND_DEGRADED)]
+    if targets == 0:
+        _set_condition(conds, COND_READY, "False", "NoTargets", "no node matches the nodeSelector", generation, now)
+    elif ready < targets:
+        _set_condition(conds, COND_READY, "False", "NodesNotReady", f"{ready}/{targets} nodes configured",
+                       generation, now)
+    else:
+        _set_condition(conds, COND_READY, "True", "AllNodesReady", f"{ready}/{targets} nodes configured",
+                       generation, now)
+    if any(e.startswith("dependency missing") for e in errors):
+        _set_condition(conds, COND_DEGRADED, "True", "DependencyMissing", "; ".join(errors)[:1024], generation, now)
+    elif errors:
+        _set_condition(conds, COND_DEGRADED, "True", "AgentErrors", "; ".join(errors)[:1024], generation, now)
+    else:
+        _set_condition(conds, COND_DEGRADED, "False", "AsExpected", "", generation, now)
+    conds.sort(key=lambda c: c["type"] != COND_READY)
+    return conds
+
+
 class EventRecorder:
     """Best-effort core/v1 Events on the policy (failures are only logged)."""
 
@@ -423,10 +468,15 @@ class NetworkClusterPolicyReconciler:
         errors += self._node_errors(ds["metadata"]["name"]) if targets and ready < targets else []
         if cur.state != new_state or cur.errors != errors:
             updated = True
+        generation = int(raw.get("metadata", {}).get("generation", 0) or 0)
+        conditions = policy_conditions(cur.conditions, targets, ready, errors, generation)
+        if conditions != cur.conditions or cur.observedGeneration != generation:
+            updated = True
         if not updated:
             return Result()
         body = copy.deepcopy(raw)
-        body["status"] = {"targets": targets, "ready": ready, "state": new_state, "errors": errors}
+        body["status"] = {"targets": targets, "ready": ready, "state": new_state, "errors": errors,
+                          "conditions": conditions, "observedGeneration": generation}
         try:
             await self.client.replace_status(kube.NETWORKCLUSTERPOLICIES, body)
         except ApiError as e:

@@ -440,3 +440,50 @@ def test_rccl_env_extra_settings_validated_and_passed():
     p.spec.amdScaleOut.rcclEnv = {"NCCL_DEBUG": "INFO,WARN"}
     with pytest.raises(W.InvalidRcclEnvError):
         W.validate_create(p)
+
+
+def test_status_conditions_ready_degraded_and_observed_generation():
+    """Additive status: Ready / Degraded conditions with stable lastTransitionTime, and
+    observedGeneration following spec changes (the reference only has the state string)."""
+    from network_operator_amd.operator.reconciler import policy_conditions
+
+    async def body():
+        async with cluster(openshift=False) as (fake, client, ctl):
+            for i in range(2):
+                fake.add_node(f"gpu-node-{i}", {"foo": "bar"})
+            await client.create(kube.NETWORKCLUSTERPOLICIES, policy())
+
+            def conds():
+                st = fake.get_object(kube.NETWORKCLUSTERPOLICIES, "policy")["status"]
+                return st, {c["type"]: c for c in st.get("conditions", [])}
+
+            def not_ready():
+                st, c = conds()
+                assert c["Ready"]["status"] == "False" and c["Ready"]["reason"] == "NodesNotReady"
+                assert c["Degraded"]["status"] == "True" and c["Degraded"]["reason"] == "AgentErrors"
+                assert st["observedGeneration"] == 1 and c["Ready"]["observedGeneration"] == 1
+            await eventually(not_ready)
+            degraded_since = conds()[1]["Degraded"]["lastTransitionTime"]
+            fake.set_agent_ready("gpu-node-0")
+
+            def one_ready():
+                st, c = conds()
+                assert st["ready"] == 1 and c["Ready"]["message"] == "1/2 nodes configured"
+            await eventually(one_ready)
+            assert conds()[1]["Degraded"]["lastTransitionTime"] == degraded_since  # no flip, no move
+            fake.set_agent_ready("gpu-node-1")
+
+            def ready():
+                st, c = conds()
+                assert c["Ready"]["status"] == "True" and c["Ready"]["reason"] == "AllNodesReady"
+                assert c["Degraded"]["status"] == "False" and c["Degraded"]["reason"] == "AsExpected"
+            await eventually(ready)
+            cur = await client.get(kube.NETWORKCLUSTERPOLICIES, "policy")
+            cur["spec"]["amdScaleOut"]["mtu"] = 4000
+            await client.replace(kube.NETWORKCLUSTERPOLICIES, cur)
+            await eventually(lambda: conds()[0]["observedGeneration"] == 2)
+    run(body())
+    # No targets; a missing dependency is reported as such.
+    c = {x["type"]: x for x in policy_conditions([], 0, 0, ["dependency missing: node-feature-discovery"], 3, "T0")}
+    assert c["Ready"]["reason"] == "NoTargets" and c["Degraded"]["reason"] == "DependencyMissing"
+    assert c["Ready"]["lastTransitionTime"] == "T0" and c["Ready"]["observedGeneration"] == 3
