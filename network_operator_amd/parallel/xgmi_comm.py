@@ -8,6 +8,8 @@ construction (ring algorithms need many concurrent rings to do the same):
                     buffers over xGMI (peer pointers, fp32 accumulation, bf16 RNE);
     all-gather      rank d pulls every other reduced chunk from the rank that owns it.
 
+``two_shot_push`` does the all-gather with remote stores instead (rank d writes its reduced
+chunk into every peer's output): xGMI read and write bandwidth differ, so both are measured.
 ``one_shot`` instead has every rank sum the whole message from all inputs (one phase, n-1 times
 the link traffic): the better choice for small messages, where phase overhead dominates.
 
@@ -43,7 +45,7 @@ from typing import List, Optional
 
 from ..ops import hip as H
 
-ALGOS = ("two_shot", "one_shot")
+ALGOS = ("two_shot", "two_shot_push", "one_shot")
 MAX_RANKS = 8
 
 
@@ -160,7 +162,7 @@ class XgmiAllReduce:
         if algo not in ALGOS:
             raise ValueError(f"algo must be one of {ALGOS}")
         n, d = self.world, self.rank
-        align = 8 * n if algo == "two_shot" else 8
+        align = 8 if algo == "one_shot" else 8 * n
         if numel % align:
             raise ValueError(f"numel must be a multiple of {align} for {algo}")
         self._view(self.inp, numel)  # capacity check
@@ -181,10 +183,14 @@ class XgmiAllReduce:
                  "netop_sum_bf16")
         self._sync_and_wait(stream)  # every reduced chunk is complete
         peers = [p for p in range(n) if p != d]
-        src = (vp * len(peers))(*[vp(self.peer_out[p] + p * cb) for p in peers])
-        dst = (vp * len(peers))(*[vp(self.out.data_ptr() + p * cb) for p in peers])
+        if algo == "two_shot":  # all-gather by remote loads: pull chunk p from its owner
+            src = (vp * len(peers))(*[vp(self.peer_out[p] + p * cb) for p in peers])
+            dst = (vp * len(peers))(*[vp(self.out.data_ptr() + p * cb) for p in peers])
+        else:  # two_shot_push: remote stores of my reduced chunk into every peer's output
+            src = (vp * len(peers))(*[vp(self.out.data_ptr() + d * cb) for _ in peers])
+            dst = (vp * len(peers))(*[vp(self.peer_out[p] + d * cb) for p in peers])
         H._check(L.netop_multi_copy(src, dst, len(peers), cb, self.wg_per_cu, s), "netop_multi_copy")
-        self._sync_and_wait(stream)  # nobody reads my output any more
+        self._sync_and_wait(stream)  # every chunk has arrived; nobody touches my buffers any more
         return self.output(numel)
 
     # -- lifetime ---------------------------------------------------------------------------------
@@ -227,7 +233,7 @@ def _worker(args) -> int:
     rows = []
     for nbytes in sizes:
         for algo in args.algos.split(","):
-            align = 8 * world if algo == "two_shot" else 8
+            align = 8 if algo == "one_shot" else 8 * world
             numel = max(align, nbytes // 2 // align * align)
             wrong = 0
             for seed in (11, 12, 13):  # same buffers, three seeds: stale peer lines cannot pass
@@ -274,7 +280,7 @@ _LAUNCHER_ENV = ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_
 
 
 def run(world: int, nbytes: int = 1 << 30, min_bytes: Optional[int] = None, iters: int = 10, warmup: int = 3,
-        algos: str = "two_shot,one_shot", devices: Optional[str] = None, timeout: float = 120.0) -> dict:
+        algos: str = ",".join(ALGOS), devices: Optional[str] = None, timeout: float = 120.0) -> dict:
     """Spawns `world` rank processes (one per GPU unless `devices` maps several onto one) and
     returns rank 0's result.  Safe to call from inside another distributed job: the children
     get their own rendezvous and none of the parent's launcher variables."""
@@ -325,7 +331,7 @@ def main(argv=None) -> int:
     ap.add_argument("--min-bytes", type=int, default=0)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--algos", default="two_shot,one_shot")
+    ap.add_argument("--algos", default=",".join(ALGOS))
     ap.add_argument("--devices", default="", help="comma list of GPU ids per rank (repeats allowed: virtual ranks)")
     ap.add_argument("--timeout", type=float, default=120.0)
     a = ap.parse_args(argv)
