@@ -46,7 +46,24 @@ from typing import List, Optional
 from ..ops import hip as H
 
 ALGOS = ("two_shot", "two_shot_push", "one_shot")
+# Below this size one phase beats two: one_shot moves (n-1)x the bytes but pays one barrier
+# less (virtual-rank measurements on MI355X: one_shot wins up to 16 MiB, two_shot from 64 MiB,
+# profiles/r1_xgmi_comm_virtual8_n1gpu.json).  Over real xGMI links the crossover is lower.
+ONE_SHOT_MAX_BYTES = 4 << 20
 MAX_RANKS = 8
+
+
+def choose_algo(numel: int, world: int, algo: str = "auto") -> str:
+    """Validates (numel, algo) and resolves ``auto``: one_shot up to ONE_SHOT_MAX_BYTES (or when
+    numel does not split into `world` chunks of whole 16-B vectors), two_shot above."""
+    if algo == "auto":
+        algo = "one_shot" if numel * 2 <= ONE_SHOT_MAX_BYTES or numel % (8 * world) else "two_shot"
+    if algo not in ALGOS:
+        raise ValueError(f"algo must be one of {ALGOS} or auto")
+    align = 8 if algo == "one_shot" else 8 * world
+    if numel % align:
+        raise ValueError(f"numel must be a multiple of {align} for {algo}")
+    return algo
 
 
 class ShmBarrier:
@@ -155,16 +172,13 @@ class XgmiAllReduce:
         stream.synchronize()
         self.barrier.wait(self.timeout_s)
 
-    def all_reduce(self, numel: int, algo: str = "two_shot"):
-        """Sum of every rank's ``input(numel)``, returned as ``output(numel)`` on every rank."""
+    def all_reduce(self, numel: int, algo: str = "auto"):
+        """Sum of every rank's ``input(numel)``, returned as ``output(numel)`` on every rank
+        (``algo``: see :func:`choose_algo`)."""
         import torch
 
-        if algo not in ALGOS:
-            raise ValueError(f"algo must be one of {ALGOS}")
+        algo = choose_algo(numel, self.world, algo)
         n, d = self.world, self.rank
-        align = 8 if algo == "one_shot" else 8 * n
-        if numel % align:
-            raise ValueError(f"numel must be a multiple of {align} for {algo}")
         self._view(self.inp, numel)  # capacity check
         L = H.lib()
         stream = torch.cuda.current_stream(self.device)

@@ -74,3 +74,19 @@ def test_xgmi_allreduce_spawned_from_inside_a_torchrun_job(cuda_device):
     line = next(ln for ln in r.stdout.splitlines() if ln.startswith("RESULT "))
     res = json.loads(line[len("RESULT "):])
     assert res == {"launcher_rank": "0", "wrong": 0, "ranks": 2}
+
+
+def test_algorithm_choice_and_alignment():
+    from network_operator_amd.parallel.xgmi_comm import ONE_SHOT_MAX_BYTES, choose_algo
+
+    assert choose_algo(64, 8) == "one_shot"
+    assert choose_algo(ONE_SHOT_MAX_BYTES // 2, 8) == "one_shot"
+    assert choose_algo(ONE_SHOT_MAX_BYTES, 8) == "two_shot"
+    assert choose_algo(ONE_SHOT_MAX_BYTES + 8, 8) == "one_shot"  # does not split into 8 whole chunks
+    assert choose_algo(72, 8, "one_shot") == "one_shot"
+    with pytest.raises(ValueError, match="algo must be one of"):
+        choose_algo(64, 8, "ring")
+    with pytest.raises(ValueError, match="multiple of 64"):
+        choose_algo(72, 8, "two_shot_push")
+    with pytest.raises(ValueError, match="multiple of 8"):
+        choose_algo(12, 8, "one_shot")
