@@ -426,29 +426,94 @@ void Agent::detect_lldp(int stop_fd) {
         return remaining == 0;
     };
     const int64_t deadline = mono_ns() + cfg_.wait_ns;
-    int announced = 0;
-    pkt::ListenResult r = pkt::ListenResult::Deadline;
-    for (;;) {
-        int64_t slice_end = deadline;
-        if (cfg_.lldp_announce && announced < cfg_.announce_count) {
-            for (auto& n : nics_) {
-                if (!n.link.up() || n.lldp_seen) continue;
+    std::map<int, int> announces;  // ifindex -> LLDPDUs sent
+    auto announce_nic = [&](NicState& n) {
+        try {
+            // After a crash the switch still holds our old neighbour entry and would not treat us
+            // as new (no fast start).  A shutdown LLDPDU first deletes that entry (802.1AB-2009
+            // 9.2.7.7.1), so the next LLDPDU is a new neighbour again.
+            if (announces[n.link.index] == 0 && cfg_.announce_shutdown_first)
+                lldp_->announce(n.ifname, lldp::encode(make_node_frame(cfg_.node_name, n.ifname, n.link.mac, n.gpu_bdf, 0)));
+            lldp_->announce(n.ifname, lldp::encode(make_node_frame(cfg_.node_name, n.ifname, n.link.mac, n.gpu_bdf)));
+        } catch (const std::exception& e) {
+            NLOG_V(2, "LLDP announce on %s failed: %s", n.ifname.c_str(), e.what());
+        }
+        ++announces[n.link.index];
+    };
+    // A frame sent before the kernel can transmit on the link is dropped without an error:
+    // admin-up is not enough, the device is usable once linkwatch has attached its qdisc and
+    // set operstate UP — and linkwatch batches that work up to a second apart.  So each NIC is
+    // announced the moment its own RTM_NEWLINK says it is operational, not all at link-up.
+    std::unique_ptr<nl::LinkWatcher> watcher;
+    if (cfg_.lldp_announce) {
+        try {
+            watcher = ops_.subscribe_links();
+        } catch (const std::exception& e) {
+            NLOG_V(2, "link events unavailable, announcing on admin-up links: %s", e.what());
+        }
+        if (watcher && watcher->fd() < 0) watcher.reset();  // no pollable events: announce right away
+        if (watcher) {
+            for (auto& n : nics_) {  // state after subscribing: no transition can be missed
                 try {
-                    // After a crash the switch still holds our old neighbour entry and would not
-                    // treat us as new (no fast start).  A shutdown LLDPDU first deletes that entry
-                    // (802.1AB-2009 9.2.7.7.1), so the next LLDPDU is a new neighbour again.
-                    if (announced == 0 && cfg_.announce_shutdown_first)
-                        lldp_->announce(n.ifname,
-                                        lldp::encode(make_node_frame(cfg_.node_name, n.ifname, n.link.mac, n.gpu_bdf, 0)));
-                    lldp_->announce(n.ifname, lldp::encode(make_node_frame(cfg_.node_name, n.ifname, n.link.mac, n.gpu_bdf)));
-                } catch (const std::exception& e) {
-                    NLOG_V(2, "LLDP announce on %s failed: %s", n.ifname.c_str(), e.what());
+                    auto l = ops_.link_by_name(n.ifname);
+                    n.link.flags = l.flags;
+                    n.link.operstate = l.operstate;
+                } catch (const std::exception&) {
                 }
             }
-            ++announced;
-            slice_end = std::min(deadline, mono_ns() + cfg_.announce_interval_ns);
         }
-        r = lldp_->run(slice_end, cb, stop_fd);
+    }
+    auto can_tx = [&](const NicState& n) {
+        if (!watcher) return n.link.up();
+        return n.link.up() && (n.link.operstate == IF_OPER_UP || (n.link.operstate == IF_OPER_UNKNOWN && n.link.lower_up()));
+    };
+    int wake = -1;  // stop_fd or link events
+    if (watcher) {
+        wake = ::epoll_create1(EPOLL_CLOEXEC);
+        for (int f : {stop_fd, watcher->fd()}) {
+            if (f < 0 || wake < 0) continue;
+            epoll_event ev{};
+            ev.events = EPOLLIN;
+            ev.data.fd = f;
+            ::epoll_ctl(wake, EPOLL_CTL_ADD, f, &ev);
+        }
+    }
+    struct CloseFd {
+        int fd;
+        ~CloseFd() {
+            if (fd >= 0) ::close(fd);
+        }
+    } wake_guard{wake};
+    const int wait_fd = wake >= 0 ? wake : stop_fd;
+    int rounds = 0;
+    int64_t next_round = mono_ns();
+    pkt::ListenResult r = pkt::ListenResult::Deadline;
+    for (;;) {
+        if (cfg_.lldp_announce && rounds < cfg_.announce_count && mono_ns() >= next_round) {
+            // Round 0: every NIC that can transmit.  Later rounds (1 s apart): every NIC still
+            // silent, operational or not — a lost frame or a driver without operstate.
+            for (auto& n : nics_)
+                if (n.link.up() && !n.lldp_seen && (rounds > 0 || can_tx(n))) announce_nic(n);
+            ++rounds;
+            next_round = mono_ns() + cfg_.announce_interval_ns;
+        }
+        const int64_t slice_end = cfg_.lldp_announce && rounds < cfg_.announce_count ? std::min(deadline, next_round) : deadline;
+        r = lldp_->run(slice_end, cb, wait_fd);
+        if (r == pkt::ListenResult::Interrupted && watcher && !fd_readable(stop_fd)) {
+            for (auto& ev : watcher->wait(mono_ns())) {  // link events: announce on newly operational NICs
+                for (auto& n : nics_) {
+                    if (n.link.index != ev.link.index || ev.deleted) continue;
+                    n.link.flags = ev.link.flags;
+                    n.link.operstate = ev.link.operstate;
+                    if (!n.lldp_seen && announces[n.link.index] == 0 && can_tx(n)) announce_nic(n);
+                }
+            }
+            if (mono_ns() >= deadline) {
+                r = pkt::ListenResult::Deadline;
+                break;
+            }
+            continue;
+        }
         if (r != pkt::ListenResult::Deadline || mono_ns() >= deadline) break;
     }
     if (r == pkt::ListenResult::Interrupted) aborted_ = true;
