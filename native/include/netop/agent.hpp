@@ -54,6 +54,7 @@ struct Config {
     bool lldp_promisc = false;
     bool pipeline = true;
     bool label_without_peers = false;
+    bool fsync_artifacts = false;  // fsync every artifact / label / status write (see set_durable_writes)
     artifacts::Labels labels;
     std::string rccl_env;                // --rccl-env
     std::string status_file;             // --status-file (JSON)

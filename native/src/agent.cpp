@@ -703,6 +703,7 @@ void Agent::write_status() {
 void Agent::run(int stop_fd) {
     t0_ = t_last_ = mono_ns();
     sanitize(cfg_);
+    set_durable_writes(cfg_.fsync_artifacts);
     try {
         rccl_env_extra_ = artifacts::parse_env_extra(cfg_.rccl_env_extra);
     } catch (const std::exception& e) {

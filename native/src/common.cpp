@@ -1,5 +1,7 @@
 #include "netop/common.hpp"
 
+#include <atomic>
+
 #include <dirent.h>
 #include <fcntl.h>
 #include <sys/stat.h>
@@ -273,6 +275,10 @@ std::optional<std::string> read_file(const std::string& path) {
     return out;
 }
 
+static std::atomic<bool> g_durable_writes{false};
+
+void set_durable_writes(bool on) { g_durable_writes.store(on, std::memory_order_relaxed); }
+
 void write_file_atomic(const std::string& path, std::string_view content, unsigned mode) {
     std::string tmp = path + ".tmp." + std::to_string(::getpid());
     int fd = ::open(tmp.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, mode);
@@ -290,7 +296,7 @@ void write_file_atomic(const std::string& path, std::string_view content, unsign
         off += size_t(n);
     }
     ::fchmod(fd, mode);  // umask-independent, like Go os.WriteFile on a new file with 0644
-    ::fsync(fd);
+    if (g_durable_writes.load(std::memory_order_relaxed)) ::fsync(fd);
     ::close(fd);
     if (::rename(tmp.c_str(), path.c_str()) != 0) {
         int e = errno;

@@ -54,6 +54,7 @@ int main(int argc, char** argv) {
     fs.add_bool("lldp-promisc", &cfg.lldp_promisc, "put interfaces in promiscuous mode while listening for LLDP");
     fs.add_bool("pipeline", &cfg.pipeline, "configure each interface as soon as its LLDP frame arrives");
     fs.add_bool("label-without-peers", &cfg.label_without_peers, "publish the readiness label even when no LLDP peer was found (reference behaviour)");
+    fs.add_bool("fsync-artifacts", &cfg.fsync_artifacts, "fsync artifact, label and status files before renaming them into place (off: they are rewritten on every start)");
     fs.add_string("nfd-features-dir", &cfg.labels.dir, "NFD local feature source directory");
     fs.add_string("nfd-label-file", &cfg.labels.file, "readiness label file name inside the features directory");
     fs.add_string("nfd-label", &cfg.labels.key, "readiness label key (published as KEY=true; KEY.mode, KEY.nics, ... alongside)");
