@@ -495,7 +495,12 @@ void Agent::detect_lldp(int stop_fd) {
             for (auto& n : nics_)
                 if (n.link.up() && !n.lldp_seen && (rounds > 0 || can_tx(n))) announce_nic(n);
             ++rounds;
-            next_round = mono_ns() + cfg_.announce_interval_ns;
+            // Retry early, then back off: a lost first frame costs 0.1 s, not a full interval
+            // (a switch that heard us answers at once; one that did not hears the retry).
+            const int64_t step = rounds == 1 ? cfg_.announce_interval_ns / 10
+                                 : rounds == 2 ? cfg_.announce_interval_ns * 3 / 10
+                                               : cfg_.announce_interval_ns;
+            next_round = mono_ns() + step;
         }
         const int64_t slice_end = cfg_.lldp_announce && rounds < cfg_.announce_count ? std::min(deadline, next_round) : deadline;
         r = lldp_->run(slice_end, cb, wait_fd);
