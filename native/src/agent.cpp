@@ -427,12 +427,15 @@ void Agent::detect_lldp(int stop_fd) {
     };
     const int64_t deadline = mono_ns() + cfg_.wait_ns;
     std::map<int, int> announces;  // ifindex -> LLDPDUs sent
-    auto announce_nic = [&](NicState& n) {
+    auto announce_nic = [&](NicState& n, bool retry) {
         try {
             // After a crash the switch still holds our old neighbour entry and would not treat us
             // as new (no fast start).  A shutdown LLDPDU first deletes that entry (802.1AB-2009
-            // 9.2.7.7.1), so the next LLDPDU is a new neighbour again.
-            if (announces[n.link.index] == 0 && cfg_.announce_shutdown_first)
+            // 9.2.7.7.1), so the next LLDPDU is a new neighbour again.  Retries do the same: if
+            // the switch heard us but its immediate answer was lost (its port was not
+            // transmitting yet), only a "new" neighbour makes it answer again before its next
+            // fast-transmit tick.
+            if ((announces[n.link.index] == 0 || retry) && cfg_.announce_shutdown_first)
                 lldp_->announce(n.ifname, lldp::encode(make_node_frame(cfg_.node_name, n.ifname, n.link.mac, n.gpu_bdf, 0)));
             lldp_->announce(n.ifname, lldp::encode(make_node_frame(cfg_.node_name, n.ifname, n.link.mac, n.gpu_bdf)));
         } catch (const std::exception& e) {
@@ -493,7 +496,7 @@ void Agent::detect_lldp(int stop_fd) {
             // Round 0: every NIC that can transmit.  Later rounds (1 s apart): every NIC still
             // silent, operational or not — a lost frame or a driver without operstate.
             for (auto& n : nics_)
-                if (n.link.up() && !n.lldp_seen && (rounds > 0 || can_tx(n))) announce_nic(n);
+                if (n.link.up() && !n.lldp_seen && (rounds > 0 || can_tx(n))) announce_nic(n, rounds > 0);
             ++rounds;
             // Retry early, then back off: a lost first frame costs 0.1 s, not a full interval
             // (a switch that heard us answers at once; one that did not hears the retry).
@@ -510,7 +513,7 @@ void Agent::detect_lldp(int stop_fd) {
                     if (n.link.index != ev.link.index || ev.deleted) continue;
                     n.link.flags = ev.link.flags;
                     n.link.operstate = ev.link.operstate;
-                    if (!n.lldp_seen && announces[n.link.index] == 0 && can_tx(n)) announce_nic(n);
+                    if (!n.lldp_seen && announces[n.link.index] == 0 && can_tx(n)) announce_nic(n, false);
                 }
             }
             if (mono_ns() >= deadline) {

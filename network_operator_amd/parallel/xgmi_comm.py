@@ -142,11 +142,16 @@ class XgmiAllReduce:
                     self.peer_in.append(self.inp.data_ptr())
                     self.peer_out.append(self.out.data_ptr())
                     continue
+                # Small buffers can share one caching-allocator segment, i.e. one IPC handle:
+                # map each distinct handle once and address both buffers inside it.
+                bases = {}
                 for (raw, off), dst in zip(allh[p], (self.peer_in, self.peer_out)):
-                    ptr, base = ctypes.c_void_p(), ctypes.c_void_p()
-                    H._check(L.netop_ipc_open(raw, off, ctypes.byref(ptr), ctypes.byref(base)), "netop_ipc_open")
-                    self._opened.append(base.value)
-                    dst.append(ptr.value)
+                    if raw not in bases:
+                        ptr, base = ctypes.c_void_p(), ctypes.c_void_p()
+                        H._check(L.netop_ipc_open(raw, 0, ctypes.byref(ptr), ctypes.byref(base)), "netop_ipc_open")
+                        self._opened.append(base.value)
+                        bases[raw] = base.value
+                    dst.append(bases[raw] + off)
             self.barrier = ShmBarrier(self.rank, self.world, group)
         except Exception:
             self._close_handles()

@@ -64,6 +64,16 @@ def test_xgmi_allreduce_multiprocess_virtual_ranks(cuda_device, world):
 
 
 @pytest.mark.gpu
+def test_xgmi_allreduce_small_buffers_share_one_ipc_segment(cuda_device):
+    """64 KiB symmetric buffers come from one caching-allocator segment, so both have the same
+    IPC handle: each peer maps it once and addresses both buffers inside it."""
+    from network_operator_amd.parallel import xgmi_comm
+
+    r = xgmi_comm.run(2, nbytes=64 << 10, min_bytes=1 << 12, iters=2, warmup=1, devices="0,0", timeout=100)
+    assert r["wrong"] == 0, json.dumps(r)
+
+
+@pytest.mark.gpu
 def test_xgmi_allreduce_spawned_from_inside_a_torchrun_job(cuda_device):
     """bench.py's n > 1 path: a torchrun-launched rank starts the multi-process all-reduce in
     its own process group; the launcher's RANK / MASTER_PORT / TORCHELASTIC_* must not leak."""
