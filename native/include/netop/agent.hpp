@@ -66,7 +66,7 @@ struct Config {
     int64_t gid_wait_ns = 3LL * 1000000000;
     bool lldp_announce = true;           // transmit our own LLDPDU (triggers switch fast start)
     int64_t announce_interval_ns = 1000000000LL;  // re-announce to still-silent NICs
-    int announce_count = 5;  // rounds at 0, +0.1, +0.4, +1.4, +2.4 s (interval 1 s)
+    int announce_count = 6;  // rounds at 0, +25 ms, +125 ms, +425 ms, +1.4 s, +2.4 s (interval 1 s)
     bool announce_shutdown_first = true;  // clear a stale neighbour entry left by a crashed run
     std::string node_name;               // LLDP System Name ($NODE_NAME, else hostname)
     // Keep-running monitor: LLDP keep-alive transmission, link-failure detection (the label is

@@ -498,10 +498,11 @@ void Agent::detect_lldp(int stop_fd) {
             for (auto& n : nics_)
                 if (n.link.up() && !n.lldp_seen && (rounds > 0 || can_tx(n))) announce_nic(n, rounds > 0);
             ++rounds;
-            // Retry early, then back off: a lost first frame costs 0.1 s, not a full interval
-            // (a switch that heard us answers at once; one that did not hears the retry).
-            const int64_t step = rounds == 1 ? cfg_.announce_interval_ns / 10
-                                 : rounds == 2 ? cfg_.announce_interval_ns * 3 / 10
+            // Retry early, then back off (25 ms, 100 ms, 300 ms, then the interval): a lost
+            // frame or answer costs tens of milliseconds, not a full interval.
+            const int64_t step = rounds == 1   ? cfg_.announce_interval_ns / 40
+                                 : rounds == 2 ? cfg_.announce_interval_ns / 10
+                                 : rounds == 3 ? cfg_.announce_interval_ns * 3 / 10
                                                : cfg_.announce_interval_ns;
             next_round = mono_ns() + step;
         }
