@@ -1,0 +1,127 @@
+#!/usr/bin/env python3
+"""Control-plane scale: how fast the operator converges on a large cluster, and its footprint.
+
+A fake API server (``testing/fakeapi.py``: watch, status subresource, DaemonSet and pod
+simulation) runs in this process with N GPU nodes; the real manager runs as a separate process
+(``python -m network_operator_amd.operator.manager``) against it, so its RSS is its own.
+Measured:
+
+* ``daemonsets_s``:  P policies created -> P agent DaemonSets exist;
+* ``targets_s``:     -> every policy's status.targets == N;
+* ``all_good_s``:    every agent on every node reports ready -> every policy "All good";
+* ``manager_rss_mib``: the manager's peak RSS (VmHWM), against the Deployment's 128Mi limit
+  (reference config/operator/manager/manager.yaml:95-101);
+* ``requests``: API requests the manager made (informers, not polling).
+
+The reference has no equivalent measurement (controller-runtime + envtest, no scale test).
+
+    python bench/control_plane.py --nodes 1000 --policies 4
+"""
+
+import argparse
+import asyncio
+import json
+import os
+import socket
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from network_operator_amd.api.v1alpha1 import types as T  # noqa: E402
+from network_operator_amd.operator import kube  # noqa: E402
+from network_operator_amd.testing.fakeapi import FakeApiServer  # noqa: E402
+
+LABEL = "amd.feature.node.kubernetes.io/gpu-ready"
+
+
+def _port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _hwm_mib(pid: int) -> float:
+    with open(f"/proc/{pid}/status") as f:
+        line = next(x for x in f if x.startswith("VmHWM:"))
+    return int(line.split()[1]) / 1024
+
+
+async def _until(pred, timeout: float) -> float:
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < timeout:
+        if pred():
+            return time.perf_counter() - t0
+        await asyncio.sleep(0.005)
+    raise TimeoutError("did not converge")
+
+
+async def run(nodes: int, policies: int, timeout: float) -> dict:
+    fake = FakeApiServer(bookmark_interval=5.0)
+    url = await fake.start()
+    for i in range(nodes):
+        fake.add_node(f"gpu-node-{i:04d}", {LABEL: "true"})
+    env = dict(os.environ, PYTHONPATH=ROOT, OPERATOR_NAMESPACE="amd-network-operator", ENABLE_WEBHOOKS="false")
+    proc = subprocess.Popen([sys.executable, "-m", "network_operator_amd.operator.manager", "--master", url,
+                             f"--health-probe-bind-address=127.0.0.1:{_port()}", "--metrics-bind-address=0"],
+                            env=env, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True)
+    try:
+        await asyncio.sleep(1.0)  # manager start: informers list + watch
+        n_req0 = len(fake.requests)
+        P = kube.NETWORKCLUSTERPOLICIES
+        names = [f"policy-{k}" for k in range(policies)]
+        t0 = time.perf_counter()
+        for n in names:
+            fake._create(P, T.new_policy(n).to_dict(), None)
+
+        def ds_all():
+            return all(fake.get_object(kube.DAEMONSETS, n, "amd-network-operator") for n in names)
+
+        def targets_all():
+            return all((fake.get_object(P, n).get("status") or {}).get("targets") == nodes for n in names)
+
+        await _until(ds_all, timeout)
+        t_ds = time.perf_counter() - t0
+        await _until(targets_all, timeout)
+        t_targets = time.perf_counter() - t0
+        t1 = time.perf_counter()
+        for i in range(nodes):
+            for n in names:
+                fake.node_ready[(f"amd-network-operator/{n}", f"gpu-node-{i:04d}")] = True
+        fake._sync_daemonsets()
+
+        def good_all():
+            return all((fake.get_object(P, n).get("status") or {}).get("state") == "All good" for n in names)
+
+        await _until(good_all, timeout)
+        t_good = time.perf_counter() - t1
+        await asyncio.sleep(0.5)
+        rss = _hwm_mib(proc.pid)
+        return {"nodes": nodes, "policies": policies, "pods": nodes * policies, "daemonsets_s": round(t_ds, 4),
+                "targets_s": round(t_targets, 4), "all_good_s": round(t_good, 4), "manager_rss_mib": round(rss, 1),
+                "manager_limit_mib": 128, "requests": len(fake.requests) - n_req0}
+    finally:
+        proc.terminate()
+        try:
+            proc.wait(10)
+        except subprocess.TimeoutExpired:
+            proc.kill()
+        await fake.stop()
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
+    ap.add_argument("--nodes", type=int, default=1000)
+    ap.add_argument("--policies", type=int, default=4)
+    ap.add_argument("--timeout", type=float, default=300)
+    a = ap.parse_args()
+    print(json.dumps(asyncio.run(run(a.nodes, a.policies, a.timeout))))
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -306,3 +306,18 @@ def test_operator_requests_stay_within_generated_rbac(tmp_path, monkeypatch):
               ("create", "coordination.k8s.io", "leases"), ("create", "authentication.k8s.io", "tokenreviews"),
               ("watch", "", "pods"), ("create", "", "events")):
         assert a in accesses, (a, sorted(accesses))
+
+
+def test_control_plane_scale_bench_converges():
+    """bench/control_plane.py at a CI-sized scale: 300 nodes x 3 policies converge to "All good"
+    within seconds, and the separate manager process stays inside its Deployment limit."""
+    import importlib.util
+    from pathlib import Path
+
+    path = Path(__file__).resolve().parent.parent / "bench" / "control_plane.py"
+    spec = importlib.util.spec_from_file_location("control_plane_bench", path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    r = asyncio.run(mod.run(300, 3, timeout=60))
+    assert r["pods"] == 900 and r["all_good_s"] < 10 and r["targets_s"] < 10, r
+    assert r["manager_rss_mib"] < r["manager_limit_mib"], r
