@@ -81,7 +81,7 @@ class ShmBarrier:
         if rank == 0:
             self._h = L.netop_shm_barrier_open(self.name.encode(), world, 1)
             if not self._h:
-                raise OSError(ctypes.get_errno(), f"shm_open({self.name}) failed")
+                raise OSError(f"shm_open({self.name}) failed: cannot create the barrier segment in /dev/shm")
         dist.barrier(group=group)
         if rank != 0:
             self._h = L.netop_shm_barrier_open(self.name.encode(), world, 0)
