@@ -182,6 +182,8 @@ def crd_manifest() -> dict:
                     {"name": "Targets", "type": "integer", "jsonPath": ".status.targets"},
                     {"name": "Ready", "type": "integer", "jsonPath": ".status.ready"},
                     {"name": "State", "type": "string", "jsonPath": ".status.state"},
+                    {"name": "Degraded", "type": "string", "priority": 1,
+                     "jsonPath": '.status.conditions[?(@.type=="Degraded")].status'},
                     {"name": "Age", "type": "date", "jsonPath": ".metadata.creationTimestamp"},
                 ],
             }],
