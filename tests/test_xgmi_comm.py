@@ -100,3 +100,12 @@ def test_algorithm_choice_and_alignment():
         choose_algo(72, 8, "two_shot_push")
     with pytest.raises(ValueError, match="multiple of 8"):
         choose_algo(12, 8, "one_shot")
+
+
+@pytest.mark.gpu
+def test_ddp_hook_trains_like_the_default_allreduce(cuda_device):
+    """DDP with the xGMI hook (2 ranks on the box's GPU): parameters after three SGD steps match
+    DDP's default fp32 all-reduce within bf16 compression error and are identical on both ranks."""
+    res = json.loads(_ranks(2, ["ddp"])[0])
+    assert res["ranks_identical"], res
+    assert res["max_abs_diff"] < 5e-3, res

@@ -53,5 +53,46 @@ def nested() -> None:
           flush=True)
 
 
+def ddp() -> None:
+    """Two data-parallel ranks on GPU 0: three SGD steps with DDP reducing gradients through the
+    xGMI hook (bf16 on the wire) vs DDP's default all-reduce (fp32 over gloo)."""
+    import json
+
+    import torch
+    from torch.nn.parallel import DistributedDataParallel as DDP
+
+    from network_operator_amd.parallel.ddp_hooks import xgmi_bf16_allreduce_hook
+    from network_operator_amd.parallel.xgmi_comm import XgmiAllReduce
+
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    params = {}
+    for mode in ("reference", "xgmi"):
+        torch.manual_seed(0)
+        net = torch.nn.Sequential(torch.nn.Linear(64, 256), torch.nn.ReLU(), torch.nn.Linear(256, 8)).to(dev)
+        model = DDP(net)
+        comm = None
+        if mode == "xgmi":
+            comm = XgmiAllReduce(1 << 20, device=dev)
+            model.register_comm_hook(comm, xgmi_bf16_allreduce_hook)
+        opt = torch.optim.SGD(model.parameters(), lr=0.1)
+        g = torch.Generator().manual_seed(100 + rank)  # different data per rank
+        for _ in range(3):
+            x, y = torch.randn(32, 64, generator=g).to(dev), torch.randn(32, 8, generator=g).to(dev)
+            opt.zero_grad()
+            ((model(x) - y) ** 2).mean().backward()
+            opt.step()
+        params[mode] = torch.cat([p.detach().flatten() for p in model.parameters()]).cpu()
+        if comm is not None:
+            comm.close()
+    gathered = [torch.zeros_like(params["xgmi"]) for _ in range(world)]
+    dist.all_gather(gathered, params["xgmi"])
+    print("RESULT " + json.dumps({"max_abs_diff": float((params["xgmi"] - params["reference"]).abs().max()),
+                                  "ranks_identical": all(torch.equal(gathered[0], t) for t in gathered)}), flush=True)
+    dist.destroy_process_group()
+
+
 if __name__ == "__main__":
-    nested() if sys.argv[1:] == ["nested"] else main()
+    {"nested": nested, "ddp": ddp}.get(sys.argv[1] if len(sys.argv) > 1 else "", main)()
