@@ -212,6 +212,45 @@ class XgmiAllReduce:
         self._sync_and_wait(stream)  # every chunk has arrived; nobody touches my buffers any more
         return self.output(numel)
 
+    def reduce_scatter(self, numel: int):
+        """Rank d gets chunk d of the sum of every rank's ``input(numel)`` (numel / n elements,
+        the first phase of the two-shot all-reduce), as a view into its output buffer."""
+        import torch
+
+        choose_algo(numel, self.world, "two_shot")  # numel splits into n whole-vector chunks
+        self._view(self.inp, numel)
+        n, d = self.world, self.rank
+        chunk = numel // n
+        cb = chunk * 2
+        stream = torch.cuda.current_stream(self.device)
+        vp = ctypes.c_void_p
+        self._sync_and_wait(stream)
+        srcs = (vp * n)(*[vp(p + d * cb) for p in self.peer_in])
+        H._check(H.lib().netop_sum_bf16(srcs, n, vp(self.out.data_ptr() + d * cb), chunk, self.wg_per_cu,
+                                        vp(stream.cuda_stream)), "netop_sum_bf16")
+        self._sync_and_wait(stream)  # nobody reads my input any more
+        return self.output(numel)[d * chunk:(d + 1) * chunk]
+
+    def all_gather(self, chunk: int):
+        """Every rank's ``input(chunk)``, concatenated in rank order, on every rank (a view of
+        ``output(n * chunk)``); each rank pulls the n-1 peer chunks over their own links."""
+        import torch
+
+        if chunk % 8:
+            raise ValueError("chunk must be a multiple of 8 elements")
+        n, d = self.world, self.rank
+        self._view(self.out, n * chunk)
+        cb = chunk * 2
+        stream = torch.cuda.current_stream(self.device)
+        vp = ctypes.c_void_p
+        self._sync_and_wait(stream)  # every contribution is complete
+        src = (vp * n)(*[vp(self.peer_in[p]) for p in range(n)])  # own chunk too: a local copy
+        dst = (vp * n)(*[vp(self.out.data_ptr() + p * cb) for p in range(n)])
+        H._check(H.lib().netop_multi_copy(src, dst, n, cb, self.wg_per_cu, vp(stream.cuda_stream)),
+                 "netop_multi_copy")
+        self._sync_and_wait(stream)  # nobody reads my input any more
+        return self.output(n * chunk)
+
     # -- lifetime ---------------------------------------------------------------------------------
     def _close_handles(self) -> None:
         L = H.lib()

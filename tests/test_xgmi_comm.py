@@ -109,3 +109,9 @@ def test_ddp_hook_trains_like_the_default_allreduce(cuda_device):
     res = json.loads(_ranks(2, ["ddp"])[0])
     assert res["ranks_identical"], res
     assert res["max_abs_diff"] < 5e-3, res
+
+
+@pytest.mark.gpu
+def test_reduce_scatter_and_all_gather_exact(cuda_device):
+    for res in (json.loads(r) for r in _ranks(3, ["collectives"])):
+        assert res == {"reduce_scatter": 0, "all_gather": 0}, res
