@@ -288,39 +288,62 @@ def _worker(args) -> int:
     if not sizes or sizes[-1] != args.bytes:
         sizes.append(args.bytes)
     comm = XgmiAllReduce(args.bytes, device=dev, timeout_s=args.timeout)
+
+    def measure(op, check, nbytes: int, factor: float, **row) -> dict:
+        """Three exact checks (seeds on reused buffers), warmup, `iters` timed calls; max time
+        and summed mismatches over the ranks."""
+        wrong = sum(check(seed) for seed in (11, 12, 13))
+        for _ in range(args.warmup):
+            op()
+        torch.cuda.synchronize(dev)
+        comm.barrier.wait(args.timeout)
+        t0 = time.perf_counter()
+        for _ in range(args.iters):
+            op()
+        torch.cuda.synchronize(dev)
+        t = torch.tensor([(time.perf_counter() - t0) / args.iters], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        w = torch.tensor([wrong], dtype=torch.int64)
+        dist.all_reduce(w, op=dist.ReduceOp.SUM)
+        dt = float(t[0])
+        algbw = nbytes / dt / 1e9
+        return dict(row, bytes=nbytes, time_us=dt * 1e6, algbw_GBps=algbw, busbw_GBps=algbw * factor, wrong=int(w[0]))
+
     rows = []
     for nbytes in sizes:
         for algo in args.algos.split(","):
             align = 8 if algo == "one_shot" else 8 * world
             numel = max(align, nbytes // 2 // align * align)
-            wrong = 0
-            for seed in (11, 12, 13):  # same buffers, three seeds: stale peer lines cannot pass
+
+            def check_ar(seed, numel=numel, algo=algo):
                 H.fill_pattern(comm.input(numel), seed, rank)
-                outv = comm.all_reduce(numel, algo)
-                wrong += H.verify_sum(outv, seed, world)
-            for _ in range(args.warmup):
-                comm.all_reduce(numel, algo)
-            torch.cuda.synchronize(dev)
-            comm.barrier.wait(args.timeout)
-            t0 = time.perf_counter()
-            for _ in range(args.iters):
-                comm.all_reduce(numel, algo)
-            torch.cuda.synchronize(dev)
-            dt = (time.perf_counter() - t0) / args.iters
-            t = torch.tensor([dt], dtype=torch.float64)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            w = torch.tensor([wrong], dtype=torch.int64)
-            dist.all_reduce(w, op=dist.ReduceOp.SUM)
-            dt, wrong = float(t[0]), int(w[0])
-            algbw = numel * 2 / dt / 1e9
-            rows.append({"algo": algo, "bytes": numel * 2, "time_us": dt * 1e6, "algbw_GBps": algbw,
-                         "busbw_GBps": algbw * 2 * (world - 1) / world, "wrong": wrong})
+                return H.verify_sum(comm.all_reduce(numel, algo), seed, world)
+
+            rows.append(measure(lambda numel=numel, algo=algo: comm.all_reduce(numel, algo), check_ar, numel * 2,
+                                2 * (world - 1) / world, algo=algo))
+    # The two phases as collectives of their own, at the largest size (rccl-tests sizes: the
+    # full input of reduce_scatter, the full output of all_gather; bus factor (n-1)/n).
+    numel = max(8 * world, args.bytes // 2 // (8 * world) * (8 * world))
+    chunk = numel // world
+
+    def check_rs(seed):
+        H.fill_pattern(comm.input(numel), seed, rank)
+        return H.verify_pattern_at(comm.reduce_scatter(numel), seed, 0, world, rank * chunk)
+
+    def check_ag(seed):
+        H.fill_pattern_at(comm.input(chunk), seed, rank, 1, rank * chunk)
+        out = comm.all_gather(chunk)
+        return sum(H.verify_pattern_at(out[p * chunk:(p + 1) * chunk], seed, p, 1, p * chunk) for p in range(world))
+
+    collectives = [measure(lambda: comm.reduce_scatter(numel), check_rs, numel * 2, (world - 1) / world,
+                           op="reduce_scatter"),
+                   measure(lambda: comm.all_gather(chunk), check_ag, numel * 2, (world - 1) / world, op="all_gather")]
     comm.close()
     if rank == 0:
         devs = sorted({devices[r % len(devices)] for r in range(world)})
-        print(json.dumps({"ranks": world, "gpus": devs, "rows": rows,
+        print(json.dumps({"ranks": world, "gpus": devs, "rows": rows, "collectives": collectives,
                           "peak_busbw_GBps": max((r["busbw_GBps"] for r in rows), default=0.0),
-                          "wrong": sum(r["wrong"] for r in rows)}), flush=True)
+                          "wrong": sum(r["wrong"] for r in rows + collectives)}), flush=True)
     dist.destroy_process_group()
     return 0
 

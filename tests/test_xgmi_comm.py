@@ -61,6 +61,8 @@ def test_xgmi_allreduce_multiprocess_virtual_ranks(cuda_device, world):
     assert r["wrong"] == 0, json.dumps(r)
     assert {x["algo"] for x in r["rows"]} == {"two_shot", "two_shot_push", "one_shot"}
     assert all(x["time_us"] > 0 for x in r["rows"])
+    assert [c["op"] for c in r["collectives"]] == ["reduce_scatter", "all_gather"]
+    assert all(c["wrong"] == 0 and c["time_us"] > 0 for c in r["collectives"])
 
 
 @pytest.mark.gpu
