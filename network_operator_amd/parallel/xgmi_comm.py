@@ -289,17 +289,17 @@ def _worker(args) -> int:
         sizes.append(args.bytes)
     comm = XgmiAllReduce(args.bytes, device=dev, timeout_s=args.timeout)
 
-    def measure(op, check, nbytes: int, factor: float, **row) -> dict:
+    def measure(fn, check, nbytes: int, factor: float, **row) -> dict:
         """Three exact checks (seeds on reused buffers), warmup, `iters` timed calls; max time
         and summed mismatches over the ranks."""
         wrong = sum(check(seed) for seed in (11, 12, 13))
         for _ in range(args.warmup):
-            op()
+            fn()
         torch.cuda.synchronize(dev)
         comm.barrier.wait(args.timeout)
         t0 = time.perf_counter()
         for _ in range(args.iters):
-            op()
+            fn()
         torch.cuda.synchronize(dev)
         t = torch.tensor([(time.perf_counter() - t0) / args.iters], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
