@@ -1,4 +1,6 @@
 #include <arpa/inet.h>
+#include <fcntl.h>
+#include <poll.h>
 #include <netinet/in.h>
 #include <sys/socket.h>
 #include <unistd.h>
@@ -6,6 +8,7 @@
 #include "check.hpp"
 #include "fake_netops.hpp"
 #include "netop/agent.hpp"
+#include "netop/common.hpp"
 #include "tmpdir.hpp"
 
 using namespace netop;
@@ -600,4 +603,125 @@ TEST(agent_require_gdr) {
     auto st = read_file(f.cfg.status_file);
     CHECK(st && st->find("\"gpudirect_rdma\":\"peermem\"") != std::string::npos);
     CHECK(a.render_metrics().find("netop_agent_gpudirect_rdma{mode=\"peermem\"} 1") != std::string::npos);
+}
+
+namespace {
+// Link events on a pollable descriptor, like the rtnetlink watcher's socket.
+struct PollableNetOps : FakeNetOps {
+    Pipe pipe;
+    PollableNetOps() { ::fcntl(pipe.fd[0], F_SETFL, O_NONBLOCK); }
+    struct Watcher : nl::LinkWatcher {
+        PollableNetOps* f;
+        explicit Watcher(PollableNetOps* ff) : f(ff) {}
+        std::vector<nl::LinkEvent> wait(int64_t) override {
+            char buf[64];
+            while (::read(f->pipe.fd[0], buf, sizeof buf) > 0) {
+            }
+            std::vector<nl::LinkEvent> out(f->events.begin(), f->events.end());
+            f->events.clear();
+            return out;
+        }
+        int fd() const override { return f->pipe.fd[0]; }
+    };
+    std::unique_ptr<nl::LinkWatcher> subscribe_links() override {
+        maybe_fail("subscribe_links");
+        return std::make_unique<Watcher>(this);
+    }
+    void operational(const std::string& name) {  // linkwatch: qdisc attached, operstate UP
+        auto& l = links[name];
+        l.operstate = IF_OPER_UP;
+        l.flags |= IFF_LOWER_UP | IFF_RUNNING;
+        events.push_back({false, l});
+        pipe.fire();
+    }
+};
+
+// A switch that answers a NIC only after hearing our LLDPDU on it (fast start).
+struct AnsweringSwitch : agent::LldpSource {
+    std::map<std::string, lldp::Frame> frames;
+    std::vector<std::string> added;
+    std::vector<std::pair<std::string, int>> sent;  // (ifname, TTL) of every LLDPDU we sent
+    std::set<std::string> heard;
+    std::function<void(int)> on_run;
+    int runs = 0;
+    void add(const std::string& ifname, int, const MacAddr&) override { added.push_back(ifname); }
+    void announce(const std::string& ifname, const std::vector<uint8_t>& frame) override {
+        auto f = lldp::decode(frame.data(), frame.size());
+        sent.emplace_back(ifname, f ? int(f->ttl) : -1);
+        if (f && f->ttl) heard.insert(ifname);
+    }
+    pkt::ListenResult run(int64_t deadline, const std::function<bool(const std::string&, const lldp::Frame&)>& cb,
+                          int wait_fd) override {
+        if (on_run) on_run(runs);
+        ++runs;
+        for (auto& i : added)
+            if (heard.count(i) && cb(i, frames[i])) return pkt::ListenResult::Stopped;
+        int64_t ms = std::max<int64_t>(0, (deadline - mono_ns()) / 1000000);
+        pollfd p{wait_fd, POLLIN, 0};
+        if (wait_fd >= 0 && ::poll(&p, 1, int(ms)) > 0) return pkt::ListenResult::Interrupted;
+        if (wait_fd < 0) ::usleep(useconds_t(ms * 1000));
+        return pkt::ListenResult::Deadline;
+    }
+};
+}  // namespace
+
+TEST(agent_announces_each_nic_when_it_becomes_operational) {
+    Fixture f;
+    PollableNetOps ops;
+    ops.add_link("ens0", 10, "02:00:00:00:00:10", false);
+    ops.add_link("ens1", 11, "02:00:00:00:00:11", false);
+    f.cfg.interfaces = "ens0,ens1";
+    f.cfg.lldp_announce = true;
+    f.cfg.keep_running = false;
+    f.cfg.wait_ns = 2000000000LL;
+    auto sw_ = std::make_unique<AnsweringSwitch>();
+    sw_->frames["ens0"] = sw("02:aa:00:00:00:00", "no-alert 10.200.0.2/30");
+    sw_->frames["ens1"] = sw("02:aa:00:00:00:01", "no-alert 10.200.0.6/30");
+    auto* s = sw_.get();
+    std::vector<std::pair<std::string, int>> sent_before_up;
+    s->on_run = [&](int run) {
+        if (run == 0) {  // admin-up but not operational yet: nothing may have been sent
+            sent_before_up = s->sent;
+            ops.operational("ens0");
+            ops.operational("ens1");
+        }
+    };
+    agent::Agent a(f.cfg, ops, std::move(sw_), f.nm());
+    int64_t t0 = mono_ns();
+    a.run(-1);
+    CHECK(sent_before_up.empty());
+    // shutdown + announce per NIC, sent on its operstate-UP event, answered at once: no retry round.
+    CHECK_EQ(s->sent.size(), size_t(4));
+    for (auto& n : a.nics()) CHECK(n.configured);
+    CHECK(mono_ns() - t0 < 250000000LL);
+}
+
+TEST(agent_retries_with_a_fresh_neighbour_when_the_answer_is_lost) {
+    Fixture f;
+    PollableNetOps ops;
+    ops.add_link("ens0", 10, "02:00:00:00:00:10", true);
+    ops.links["ens0"].operstate = IF_OPER_UP;
+    f.cfg.interfaces = "ens0";
+    f.cfg.lldp_announce = true;
+    f.cfg.keep_running = false;
+    f.cfg.wait_ns = 2000000000LL;
+    auto sw_ = std::make_unique<AnsweringSwitch>();
+    sw_->frames["ens0"] = sw("02:aa:00:00:00:00", "no-alert 10.200.0.2/30");
+    auto* s = sw_.get();
+    bool dropped = false;
+    s->on_run = [&](int) {
+        if (!dropped && !s->heard.empty()) {  // the switch heard us, its answer is lost
+            s->heard.clear();
+            dropped = true;
+        }
+    };
+    agent::Agent a(f.cfg, ops, std::move(sw_), f.nm());
+    int64_t t0 = mono_ns();
+    a.run(-1);
+    for (auto& n : a.nics()) CHECK(n.configured);
+    // First round: shutdown + announce; the 25 ms retry: shutdown + announce again (new neighbour).
+    CHECK_EQ(s->sent.size(), size_t(4));
+    CHECK_EQ(s->sent[2].second, 0);
+    int64_t dt = mono_ns() - t0;
+    CHECK(dt >= 20000000LL && dt < 200000000LL);
 }
