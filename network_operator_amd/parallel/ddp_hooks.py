@@ -36,3 +36,46 @@ def xgmi_bf16_allreduce_hook(comm: XgmiAllReduce, bucket):
     fut: torch.futures.Future = torch.futures.Future()
     fut.set_result(buf)
     return fut
+
+
+class XgmiOverlapState:
+    """State for :func:`xgmi_bf16_allreduce_hook_overlapped`: one communication stream and one
+    worker thread, so buckets are reduced in DDP's launch order (the same on every rank) while
+    the autograd thread keeps computing the next gradients."""
+
+    def __init__(self, comm: XgmiAllReduce):
+        import concurrent.futures
+
+        import torch
+
+        self.comm = comm
+        self.stream = torch.cuda.Stream(device=comm.device)
+        self.pool = concurrent.futures.ThreadPoolExecutor(max_workers=1, thread_name_prefix="xgmi-ddp")
+
+    def close(self) -> None:
+        self.pool.shutdown(wait=True)
+
+
+def xgmi_bf16_allreduce_hook_overlapped(state: XgmiOverlapState, bucket):
+    """Like :func:`xgmi_bf16_allreduce_hook`, but the bucket's all-reduce runs on the state's
+    stream from its worker thread and the hook returns at once: communication overlaps the rest
+    of the backward pass, and DDP waits on the returned future only when it needs the result."""
+    import torch
+
+    buf = bucket.buffer()
+    ready = torch.cuda.Event()
+    ready.record(torch.cuda.current_stream(state.comm.device))  # the bucket's gradients are complete
+    fut: torch.futures.Future = torch.futures.Future()
+
+    def work() -> None:
+        try:
+            with torch.cuda.stream(state.stream):
+                state.stream.wait_event(ready)
+                xgmi_bf16_allreduce_hook(state.comm, bucket).wait()
+                state.stream.synchronize()
+            fut.set_result(buf)
+        except BaseException as e:  # surfaces in DDP's wait, on the training thread
+            fut.set_exception(e)
+
+    state.pool.submit(work)
+    return fut

@@ -109,7 +109,7 @@ def test_ddp_hook_trains_like_the_default_allreduce(cuda_device):
     """DDP with the xGMI hook (2 ranks on the box's GPU): parameters after three SGD steps match
     DDP's default fp32 all-reduce within bf16 compression error and are identical on both ranks."""
     res = json.loads(_ranks(2, ["ddp"])[0])
-    assert res["ranks_identical"], res
+    assert res["ranks_identical"] and res["overlapped_equals_sync"], res
     assert res["max_abs_diff"] < 5e-3, res
 
 

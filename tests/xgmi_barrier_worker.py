@@ -61,7 +61,8 @@ def ddp() -> None:
     import torch
     from torch.nn.parallel import DistributedDataParallel as DDP
 
-    from network_operator_amd.parallel.ddp_hooks import xgmi_bf16_allreduce_hook
+    from network_operator_amd.parallel.ddp_hooks import (XgmiOverlapState, xgmi_bf16_allreduce_hook,
+                                                         xgmi_bf16_allreduce_hook_overlapped)
     from network_operator_amd.parallel.xgmi_comm import XgmiAllReduce
 
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
@@ -69,14 +70,18 @@ def ddp() -> None:
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     params = {}
-    for mode in ("reference", "xgmi"):
+    for mode in ("reference", "xgmi", "xgmi_overlapped"):
         torch.manual_seed(0)
         net = torch.nn.Sequential(torch.nn.Linear(64, 256), torch.nn.ReLU(), torch.nn.Linear(256, 8)).to(dev)
         model = DDP(net)
-        comm = None
+        comm = state = None
         if mode == "xgmi":
             comm = XgmiAllReduce(1 << 20, device=dev)
             model.register_comm_hook(comm, xgmi_bf16_allreduce_hook)
+        elif mode == "xgmi_overlapped":
+            comm = XgmiAllReduce(1 << 20, device=dev)
+            state = XgmiOverlapState(comm)
+            model.register_comm_hook(state, xgmi_bf16_allreduce_hook_overlapped)
         opt = torch.optim.SGD(model.parameters(), lr=0.1)
         g = torch.Generator().manual_seed(100 + rank)  # different data per rank
         for _ in range(3):
@@ -85,11 +90,14 @@ def ddp() -> None:
             ((model(x) - y) ** 2).mean().backward()
             opt.step()
         params[mode] = torch.cat([p.detach().flatten() for p in model.parameters()]).cpu()
+        if state is not None:
+            state.close()
         if comm is not None:
             comm.close()
     gathered = [torch.zeros_like(params["xgmi"]) for _ in range(world)]
     dist.all_gather(gathered, params["xgmi"])
     print("RESULT " + json.dumps({"max_abs_diff": float((params["xgmi"] - params["reference"]).abs().max()),
+                                  "overlapped_equals_sync": bool(torch.equal(params["xgmi"], params["xgmi_overlapped"])),
                                   "ranks_identical": all(torch.equal(gathered[0], t) for t in gathered)}), flush=True)
     dist.destroy_process_group()
 
