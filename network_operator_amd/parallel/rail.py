@@ -1,0 +1,71 @@
+"""Rail-aligned two-level all-reduce for multi-node jobs on MI355X nodes.
+
+The operator gives every GPU its own scale-out NIC (the GPU-affine RoCE NIC behind the same
+PCIe switch, ``rccl.env``'s ``NCCL_IB_HCA`` in GPU order) and routes each rail's /30s through
+the switch's /16.  A data-parallel all-reduce over several such nodes then splits naturally:
+
+1. **intra-node reduce-scatter over xGMI** (:class:`XgmiAllReduce`): local rank d ends up with
+   chunk d of its node's sum, read from all 7 peers at once;
+2. **inter-node all-reduce of chunk d on rail d**: only ranks with the same local rank talk
+   across nodes (``torch.distributed`` group per rail, RCCL over that GPU's own NIC), so the 8
+   NICs of a node carry 8 different chunks in parallel and no bytes cross PCIe to another GPU's NIC;
+3. **intra-node all-gather over xGMI** of the final chunks.
+
+Each NIC moves 2(N-1)/N of 1/8 of the message for N nodes — the bandwidth-optimal split for
+8 rails — while xGMI does the rest.  Reference counterpart: none (the reference stops at
+writing the collective library's configuration, cmd/discover/gaudinet.go).
+"""
+
+from __future__ import annotations
+
+import os
+from typing import Optional, Tuple
+
+from .xgmi_comm import XgmiAllReduce
+
+
+def node_and_rail_groups(local_size: Optional[int] = None) -> Tuple[object, object]:
+    """(this rank's node group, this rank's rail group) for a job laid out node-major
+    (global rank = node * local_size + local_rank, as torchrun assigns).  Collective: every rank
+    creates every group, in the same order."""
+    import torch.distributed as dist
+
+    world, rank = dist.get_world_size(), dist.get_rank()
+    local_size = local_size or int(os.environ.get("LOCAL_WORLD_SIZE", world))
+    if world % local_size:
+        raise ValueError(f"world size {world} is not a multiple of the node size {local_size}")
+    nodes = world // local_size
+    node_group = rail_group = None
+    for node in range(nodes):
+        g = dist.new_group(list(range(node * local_size, (node + 1) * local_size)))
+        if rank // local_size == node:
+            node_group = g
+    for lr in range(local_size):
+        g = dist.new_group([node * local_size + lr for node in range(nodes)])
+        if rank % local_size == lr:
+            rail_group = g
+    return node_group, rail_group
+
+
+class RailAllReduce:
+    """bf16 sum over every rank of a multi-node job: xGMI inside a node, one rail per chunk
+    across nodes."""
+
+    def __init__(self, capacity_bytes: int, node_group, rail_group, device=None, timeout_s: float = 60.0):
+        self.intra = XgmiAllReduce(capacity_bytes, group=node_group, device=device, timeout_s=timeout_s)
+        self.rail = rail_group
+
+    def input(self, numel: int):
+        return self.intra.input(numel)
+
+    def all_reduce(self, numel: int):
+        import torch
+        import torch.distributed as dist
+
+        mine = self.intra.reduce_scatter(numel)  # chunk `local rank` of this node's sum
+        dist.all_reduce(mine, group=self.rail)   # that chunk across nodes, on this GPU's rail
+        torch.cuda.current_stream(self.intra.device).synchronize()
+        return self.intra.all_gather_inplace(numel)
+
+    def close(self) -> None:
+        self.intra.close()

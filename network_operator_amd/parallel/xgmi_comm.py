@@ -75,7 +75,8 @@ class ShmBarrier:
 
         L = H.lib()
         names: List[Optional[str]] = [name or f"/netop-xgmi-{uuid.uuid4().hex[:16]}"]
-        dist.broadcast_object_list(names, src=0, group=group)
+        # `src` is a global rank: the group's rank 0 (a node's local group need not contain rank 0).
+        dist.broadcast_object_list(names, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
         self.name = names[0]
         self._h = None
         if rank == 0:
@@ -250,6 +251,27 @@ class XgmiAllReduce:
                  "netop_multi_copy")
         self._sync_and_wait(stream)  # nobody reads my input any more
         return self.output(n * chunk)
+
+    def all_gather_inplace(self, numel: int):
+        """Every rank p already holds chunk p of the message at ``output(numel)[p*chunk:]``
+        (e.g. after :meth:`reduce_scatter` and a cross-node step on that chunk); fill in the
+        other n-1 chunks from their owners — the second phase of the two-shot all-reduce."""
+        import torch
+
+        choose_algo(numel, self.world, "two_shot")
+        self._view(self.out, numel)
+        n, d = self.world, self.rank
+        cb = numel // n * 2
+        stream = torch.cuda.current_stream(self.device)
+        vp = ctypes.c_void_p
+        self._sync_and_wait(stream)  # every owned chunk is final
+        peers = [p for p in range(n) if p != d]
+        src = (vp * len(peers))(*[vp(self.peer_out[p] + p * cb) for p in peers])
+        dst = (vp * len(peers))(*[vp(self.out.data_ptr() + p * cb) for p in peers])
+        H._check(H.lib().netop_multi_copy(src, dst, len(peers), cb, self.wg_per_cu, vp(stream.cuda_stream)),
+                 "netop_multi_copy")
+        self._sync_and_wait(stream)
+        return self.output(numel)
 
     # -- lifetime ---------------------------------------------------------------------------------
     def _close_handles(self) -> None:

@@ -26,8 +26,8 @@ def _port():
     return p
 
 
-def _ranks(world, args):
-    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_port()), WORLD_SIZE=str(world),
+def _ranks(world, args, **extra):
+    env = dict(os.environ, **extra, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_port()), WORLD_SIZE=str(world),
                PYTHONPATH=str(ROOT))
     procs = [subprocess.Popen([sys.executable, str(WORKER), *args], env=dict(env, RANK=str(r)),
                               stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for r in range(world)]
@@ -117,3 +117,18 @@ def test_ddp_hook_trains_like_the_default_allreduce(cuda_device):
 def test_reduce_scatter_and_all_gather_exact(cuda_device):
     for res in (json.loads(r) for r in _ranks(3, ["collectives"])):
         assert res == {"reduce_scatter": 0, "all_gather": 0}, res
+
+
+def test_rail_groups_split_a_two_node_job():
+    """node_and_rail_groups for 4 ranks laid out as 2 nodes x 2: node groups {0,1},{2,3}; rail
+    groups {0,2},{1,3}; the node group's shm barrier works although its rank 0 is global rank 2."""
+    outs = [json.loads(o) for o in _ranks(4, ["rail_groups"], LOCAL_WORLD_SIZE="2")]
+    for r, o in enumerate(outs):
+        base = 2 * (r // 2)
+        assert o == {"node": base + base + 1, "node_size": 2, "rail": (r % 2) + (r % 2 + 2), "rail_size": 2}, (r, o)
+
+
+@pytest.mark.gpu
+def test_rail_allreduce_two_virtual_nodes_exact(cuda_device):
+    for res in (json.loads(r) for r in _ranks(4, ["rail"], LOCAL_WORLD_SIZE="2")):
+        assert res == {"wrong": 0}, res

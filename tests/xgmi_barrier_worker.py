@@ -133,5 +133,59 @@ def collectives() -> None:
     dist.destroy_process_group()
 
 
+def rail_groups() -> None:
+    """node_and_rail_groups on gloo (CPU): with LOCAL_WORLD_SIZE=2 and 4 ranks, the node group
+    of rank r is {2*(r//2), 2*(r//2)+1} and its rail group {r%2, r%2+2}; report each group's
+    sum of member ranks."""
+    import json
+
+    import torch
+
+    from network_operator_amd.parallel.rail import node_and_rail_groups
+
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    node, rail = node_and_rail_groups()
+    sums = {}
+    for name, g in (("node", node), ("rail", rail)):
+        t = torch.tensor([float(rank)])
+        dist.all_reduce(t, group=g)
+        sums[name] = int(t.item())
+        sums[name + "_size"] = dist.get_world_size(g)
+    # the shared-memory barrier of a node group whose rank 0 is not global rank 0
+    bar = ShmBarrier(dist.get_rank(node), dist.get_world_size(node), node)
+    for _ in range(20):
+        bar.wait(20)
+    bar.close()
+    print("RESULT " + json.dumps(sums), flush=True)
+    dist.destroy_process_group()
+
+
+def rail() -> None:
+    """RailAllReduce, 4 ranks on GPU 0 laid out as 2 "nodes" x 2 local ranks (gloo carries the
+    cross-node step): the result equals the pattern sum over all 4 ranks, three seeds."""
+    import json
+
+    import torch
+
+    from network_operator_amd.ops import hip as H
+    from network_operator_amd.parallel.rail import RailAllReduce, node_and_rail_groups
+
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    node, rail_g = node_and_rail_groups()
+    comm = RailAllReduce(8 << 20, node, rail_g, device=dev)
+    wrong = 0
+    for numel in (64 * world, (1 << 20) * world):
+        for seed in (31, 32, 33):
+            H.fill_pattern(comm.input(numel), seed, rank)
+            wrong += H.verify_pattern_at(comm.all_reduce(numel), seed, 0, world, 0)
+    comm.close()
+    print("RESULT " + json.dumps({"wrong": wrong}), flush=True)
+    dist.destroy_process_group()
+
+
 if __name__ == "__main__":
-    {"nested": nested, "ddp": ddp, "collectives": collectives}.get(sys.argv[1] if len(sys.argv) > 1 else "", main)()
+    {"nested": nested, "ddp": ddp, "collectives": collectives, "rail_groups": rail_groups, "rail": rail}.get(sys.argv[1] if len(sys.argv) > 1 else "", main)()
