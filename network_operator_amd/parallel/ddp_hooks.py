@@ -11,7 +11,10 @@ PyTorch's ``bf16_compress_hook``), summed over the xGMI mesh, and written back a
 
 The hook completes before it returns (the all-reduce orders its phases on the host), so it
 trades DDP's backward/communication overlap for the direct mesh path; it is meant for
-intra-node data parallelism with large buckets.
+intra-node data parallelism with large buckets.  Across nodes, pass a
+:class:`~network_operator_amd.parallel.rail.RailAllReduce` instead (xGMI inside the node, one
+RoCE rail per chunk between nodes); the hooks only use ``input`` / ``all_reduce`` / ``world`` /
+``device``.
 """
 
 from __future__ import annotations

@@ -52,13 +52,21 @@ class RailAllReduce:
     across nodes."""
 
     def __init__(self, capacity_bytes: int, node_group, rail_group, device=None, timeout_s: float = 60.0):
+        import torch.distributed as dist
+
         self.intra = XgmiAllReduce(capacity_bytes, group=node_group, device=device, timeout_s=timeout_s)
         self.rail = rail_group
+        # the same surface as XgmiAllReduce, so the DDP hooks (ddp_hooks.py) take either
+        self.device = self.intra.device
+        self.world = self.intra.world * dist.get_world_size(rail_group)
 
     def input(self, numel: int):
         return self.intra.input(numel)
 
-    def all_reduce(self, numel: int):
+    def all_reduce(self, numel: int, algo: str = "two_shot"):
+        """Sum over every rank of ``input(numel)``; ``numel`` must split into whole 8-element
+        vectors per local rank.  ``algo`` is accepted for the hooks' sake; the split is always
+        two-shot (the cross-node step needs the scattered chunks)."""
         import torch
         import torch.distributed as dist
 

@@ -131,4 +131,4 @@ def test_rail_groups_split_a_two_node_job():
 @pytest.mark.gpu
 def test_rail_allreduce_two_virtual_nodes_exact(cuda_device):
     for res in (json.loads(r) for r in _ranks(4, ["rail"], LOCAL_WORLD_SIZE="2")):
-        assert res == {"wrong": 0}, res
+        assert res == {"wrong": 0, "hook_ok": True}, res

@@ -182,8 +182,21 @@ def rail() -> None:
         for seed in (31, 32, 33):
             H.fill_pattern(comm.input(numel), seed, rank)
             wrong += H.verify_pattern_at(comm.all_reduce(numel), seed, 0, world, 0)
+    # the DDP hook takes the rail all-reduce too: fp32 bucket of (rank + 1) averages to 2.5
+    from network_operator_amd.parallel.ddp_hooks import xgmi_bf16_allreduce_hook
+
+    class Bucket:
+        def __init__(self, t):
+            self.t = t
+
+        def buffer(self):
+            return self.t
+
+    grads = torch.full((1000,), float(rank + 1), device=dev)
+    out = xgmi_bf16_allreduce_hook(comm, Bucket(grads)).wait()
+    hook_ok = bool(torch.all(out == (world + 1) / 2).item())
     comm.close()
-    print("RESULT " + json.dumps({"wrong": wrong}), flush=True)
+    print("RESULT " + json.dumps({"wrong": wrong, "hook_ok": hook_ok}), flush=True)
     dist.destroy_process_group()
 
 
