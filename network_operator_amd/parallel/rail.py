@@ -51,8 +51,11 @@ class RailAllReduce:
     """bf16 sum over every rank of a multi-node job: xGMI inside a node, one rail per chunk
     across nodes."""
 
-    def __init__(self, capacity_bytes: int, node_group, rail_group, device=None, timeout_s: float = 60.0):
+    def __init__(self, capacity_bytes: int, node_group, rail_group, device=None, timeout_s: float = 60.0,
+                 segments: int = 4, min_segment_bytes: int = 4 << 20):
         import torch.distributed as dist
+
+        self.segments, self.min_segment_bytes = segments, min_segment_bytes
 
         self.intra = XgmiAllReduce(capacity_bytes, group=node_group, device=device, timeout_s=timeout_s)
         self.rail = rail_group
@@ -63,17 +66,36 @@ class RailAllReduce:
     def input(self, numel: int):
         return self.intra.input(numel)
 
+    def segments_for(self, numel: int) -> int:
+        """How many pipeline segments ``numel`` is cut into: up to ``self.segments``, each at
+        least ``self.min_segment_bytes`` and splitting into whole 8-element vectors per local rank."""
+        align = 8 * self.intra.world
+        for k in range(max(self.segments, 1), 1, -1):
+            if numel % (k * align) == 0 and numel * 2 // k >= self.min_segment_bytes:
+                return k
+        return 1
+
     def all_reduce(self, numel: int, algo: str = "two_shot"):
         """Sum over every rank of ``input(numel)``; ``numel`` must split into whole 8-element
         vectors per local rank.  ``algo`` is accepted for the hooks' sake; the split is always
-        two-shot (the cross-node step needs the scattered chunks)."""
-        import torch
+        two-shot (the cross-node step needs the scattered chunks).
+
+        Pipelined over :meth:`segments_for` segments: segment k's cross-node all-reduce is
+        issued asynchronously (RCCL's own stream, the rail NIC) while the xGMI reduce-scatter of
+        segment k+1 runs, and segment k's xGMI all-gather overlaps the later segments' rail
+        traffic — the two fabrics work at the same time instead of taking turns."""
         import torch.distributed as dist
 
-        mine = self.intra.reduce_scatter(numel)  # chunk `local rank` of this node's sum
-        dist.all_reduce(mine, group=self.rail)   # that chunk across nodes, on this GPU's rail
-        torch.cuda.current_stream(self.intra.device).synchronize()
-        return self.intra.all_gather_inplace(numel)
+        k = self.segments_for(numel)
+        seg = numel // k
+        works = []
+        for s in range(k):
+            mine = self.intra.reduce_scatter(seg, offset=s * seg)  # chunk `local rank` of this node's sum
+            works.append(dist.all_reduce(mine, group=self.rail, async_op=True))  # that chunk, this GPU's rail
+        for s, w in enumerate(works):
+            w.wait()  # the current stream orders after the rail step; the gather synchronises it
+            self.intra.all_gather_inplace(seg, offset=s * seg)
+        return self.intra.output(numel)
 
     def close(self) -> None:
         self.intra.close()

@@ -213,24 +213,28 @@ class XgmiAllReduce:
         self._sync_and_wait(stream)  # every chunk has arrived; nobody touches my buffers any more
         return self.output(numel)
 
-    def reduce_scatter(self, numel: int):
-        """Rank d gets chunk d of the sum of every rank's ``input(numel)`` (numel / n elements,
-        the first phase of the two-shot all-reduce), as a view into its output buffer."""
+    def reduce_scatter(self, numel: int, offset: int = 0):
+        """Rank d gets chunk d of the sum of every rank's ``input(offset + numel)[offset:]``
+        (numel / n elements, the first phase of the two-shot all-reduce), as a view into its
+        output buffer at ``output(...)[offset + d*chunk:]``.  ``offset`` (a multiple of 8
+        elements) lets a caller reduce a long message segment by segment."""
         import torch
 
         choose_algo(numel, self.world, "two_shot")  # numel splits into n whole-vector chunks
-        self._view(self.inp, numel)
+        if offset % 8:
+            raise ValueError("offset must be a multiple of 8 elements")
+        self._view(self.inp, offset + numel)
         n, d = self.world, self.rank
         chunk = numel // n
-        cb = chunk * 2
+        cb, ob = chunk * 2, offset * 2
         stream = torch.cuda.current_stream(self.device)
         vp = ctypes.c_void_p
         self._sync_and_wait(stream)
-        srcs = (vp * n)(*[vp(p + d * cb) for p in self.peer_in])
-        H._check(H.lib().netop_sum_bf16(srcs, n, vp(self.out.data_ptr() + d * cb), chunk, self.wg_per_cu,
+        srcs = (vp * n)(*[vp(p + ob + d * cb) for p in self.peer_in])
+        H._check(H.lib().netop_sum_bf16(srcs, n, vp(self.out.data_ptr() + ob + d * cb), chunk, self.wg_per_cu,
                                         vp(stream.cuda_stream)), "netop_sum_bf16")
         self._sync_and_wait(stream)  # nobody reads my input any more
-        return self.output(numel)[d * chunk:(d + 1) * chunk]
+        return self.output(offset + numel)[offset + d * chunk:offset + (d + 1) * chunk]
 
     def all_gather(self, chunk: int):
         """Every rank's ``input(chunk)``, concatenated in rank order, on every rank (a view of
@@ -252,26 +256,29 @@ class XgmiAllReduce:
         self._sync_and_wait(stream)  # nobody reads my input any more
         return self.output(n * chunk)
 
-    def all_gather_inplace(self, numel: int):
-        """Every rank p already holds chunk p of the message at ``output(numel)[p*chunk:]``
+    def all_gather_inplace(self, numel: int, offset: int = 0):
+        """Every rank p already holds chunk p of the message at ``output(...)[offset + p*chunk:]``
         (e.g. after :meth:`reduce_scatter` and a cross-node step on that chunk); fill in the
-        other n-1 chunks from their owners — the second phase of the two-shot all-reduce."""
+        other n-1 chunks from their owners — the second phase of the two-shot all-reduce.
+        Returns the whole ``numel``-element message at ``offset``."""
         import torch
 
         choose_algo(numel, self.world, "two_shot")
-        self._view(self.out, numel)
+        if offset % 8:
+            raise ValueError("offset must be a multiple of 8 elements")
+        self._view(self.out, offset + numel)
         n, d = self.world, self.rank
-        cb = numel // n * 2
+        cb, ob = numel // n * 2, offset * 2
         stream = torch.cuda.current_stream(self.device)
         vp = ctypes.c_void_p
         self._sync_and_wait(stream)  # every owned chunk is final
         peers = [p for p in range(n) if p != d]
-        src = (vp * len(peers))(*[vp(self.peer_out[p] + p * cb) for p in peers])
-        dst = (vp * len(peers))(*[vp(self.out.data_ptr() + p * cb) for p in peers])
+        src = (vp * len(peers))(*[vp(self.peer_out[p] + ob + p * cb) for p in peers])
+        dst = (vp * len(peers))(*[vp(self.out.data_ptr() + ob + p * cb) for p in peers])
         H._check(H.lib().netop_multi_copy(src, dst, len(peers), cb, self.wg_per_cu, vp(stream.cuda_stream)),
                  "netop_multi_copy")
         self._sync_and_wait(stream)
-        return self.output(numel)
+        return self.output(offset + numel)[offset:]
 
     # -- lifetime ---------------------------------------------------------------------------------
     def _close_handles(self) -> None:

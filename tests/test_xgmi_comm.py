@@ -132,3 +132,18 @@ def test_rail_groups_split_a_two_node_job():
 def test_rail_allreduce_two_virtual_nodes_exact(cuda_device):
     for res in (json.loads(r) for r in _ranks(4, ["rail"], LOCAL_WORLD_SIZE="2")):
         assert res == {"wrong": 0, "hook_ok": True}, res
+
+
+def test_rail_segments_stay_vector_aligned():
+    from types import SimpleNamespace
+
+    from network_operator_amd.parallel.rail import RailAllReduce
+
+    r = RailAllReduce.__new__(RailAllReduce)
+    r.intra, r.segments, r.min_segment_bytes = SimpleNamespace(world=8), 4, 4 << 20
+    assert r.segments_for(64 << 20) == 4           # 128 MiB of bf16
+    assert r.segments_for(3 << 20) == 1            # 6 MiB: two 3 MiB segments would be under the minimum
+    assert r.segments_for((8 << 20) + 128) == 2    # 4 or 3 segments would not split into whole vectors
+    assert r.segments_for(192 * 65537) == 3
+    r.segments = 1
+    assert r.segments_for(64 << 20) == 1

@@ -176,9 +176,11 @@ def rail() -> None:
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     node, rail_g = node_and_rail_groups()
-    comm = RailAllReduce(8 << 20, node, rail_g, device=dev)
+    comm = RailAllReduce(8 << 20, node, rail_g, device=dev, segments=4, min_segment_bytes=1 << 12)
     wrong = 0
-    for numel in (64 * world, (1 << 20) * world):
+    # 256 elements: one segment; 48048: 3 segments (4 would not split into whole vectors per
+    # local rank); 8 MiB: 4 pipelined segments
+    for numel in (64 * world, 48048, (1 << 20) * world):
         for seed in (31, 32, 33):
             H.fill_pattern(comm.input(numel), seed, rank)
             wrong += H.verify_pattern_at(comm.all_reduce(numel), seed, 0, world, 0)
