@@ -18,10 +18,62 @@ writing the collective library's configuration, cmd/discover/gaudinet.go).
 
 from __future__ import annotations
 
+import json
 import os
-from typing import Optional, Tuple
+from typing import Dict, Optional, Tuple
 
 from .xgmi_comm import XgmiAllReduce
+
+ARTIFACT_DIR = "/etc/amd/scale-out"  # where the agent writes rccl-net.json / rccl.env on the host
+
+
+def device_bdf(device_index: int) -> str:
+    """PCI address (``dddd:bb:dd.f``) of HIP device ``device_index``.  HIP numbers GPUs in KFD
+    order, which is not PCI order on MI355X nodes, so rails are matched by address."""
+    import torch
+
+    p = torch.cuda.get_device_properties(device_index)
+    return f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}.0"
+
+
+def read_env_file(path: str) -> Dict[str, str]:
+    """``KEY=VALUE`` lines of an env file such as the agent's ``rccl.env`` (comments skipped)."""
+    out: Dict[str, str] = {}
+    with open(path) as f:
+        for line in f:
+            line = line.strip()
+            if line and not line.startswith("#") and "=" in line:
+                k, v = line.split("=", 1)
+                out[k.strip()] = v
+    return out
+
+
+def rail_env(gpu_bdf: Optional[str] = None, gpu_index: Optional[int] = None,
+             artifact_dir: str = ARTIFACT_DIR) -> Dict[str, str]:
+    """RCCL settings that pin this rank's cross-node traffic to its own rail: the node-wide
+    ``rccl.env`` with ``NCCL_IB_HCA`` narrowed to the RDMA device of the NIC the agent paired
+    with this GPU (``rccl-net.json`` entry with the same ``GPU_BDF``, else ``GPU_INDEX`` — the
+    agent's PCI-order index).  Apply before the rail group's communicator is created, e.g.
+    ``os.environ.update(rail_env(device_bdf(local_rank)))`` ahead of ``init_process_group``.
+    The setting is per process, so the job-wide communicator also sends this GPU's traffic
+    through its own NIC — what RCCL's topology search picks for GPU-affine NICs anyway.
+    Raises ``LookupError`` when no configured NIC belongs to this GPU."""
+    env_path = os.path.join(artifact_dir, "rccl.env")
+    env = read_env_file(env_path) if os.path.exists(env_path) else {}
+    with open(os.path.join(artifact_dir, "rccl-net.json")) as f:
+        entries = json.load(f).get("NIC_NET_CONFIG", [])
+    want = gpu_bdf.lower() if gpu_bdf else None
+    mine = next((e for e in entries if want and e.get("GPU_BDF", "").lower() == want), None)
+    if mine is None and gpu_index is not None:
+        mine = next((e for e in entries if e.get("GPU_INDEX") == gpu_index), None)
+    if mine is None or not mine.get("RDMA_DEV"):
+        raise LookupError(f"no configured RDMA NIC for GPU {gpu_bdf or gpu_index} in {artifact_dir}/rccl-net.json")
+    env["NCCL_IB_HCA"] = f"={mine['RDMA_DEV']}:{mine.get('RDMA_PORT', 1)}"  # '=': exact name match
+    if "GID_INDEX" in mine:
+        env["NCCL_IB_GID_INDEX"] = str(mine["GID_INDEX"])
+    # NCCL_SOCKET_IFNAME stays as it is: bootstrap of the job-wide communicator needs a network
+    # every node shares, and different rails need not route to each other.
+    return env
 
 
 def node_and_rail_groups(local_size: Optional[int] = None) -> Tuple[object, object]:
@@ -56,7 +108,6 @@ class RailAllReduce:
         import torch.distributed as dist
 
         self.segments, self.min_segment_bytes = segments, min_segment_bytes
-
         self.intra = XgmiAllReduce(capacity_bytes, group=node_group, device=device, timeout_s=timeout_s)
         self.rail = rail_group
         # the same surface as XgmiAllReduce, so the DDP hooks (ddp_hooks.py) take either

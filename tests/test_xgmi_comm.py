@@ -147,3 +147,33 @@ def test_rail_segments_stay_vector_aligned():
     assert r.segments_for(192 * 65537) == 3
     r.segments = 1
     assert r.segments_for(64 << 20) == 1
+
+
+def test_rail_env_pins_each_gpu_to_its_own_nic(tmp_path):
+    """rail_env reads the agent's artifacts: NCCL_IB_HCA narrowed to the GPU's paired NIC, by PCI
+    address first (HIP order is not PCI order), by the agent's GPU index as a fallback."""
+    from network_operator_amd.parallel.rail import rail_env
+
+    entries = [{"NIC_MAC": "02:00:00:00:00:0%d" % i, "NIC_IP": "10.0.%d.1" % i, "SUBNET_MASK": "255.255.255.252",
+                "GATEWAY_MAC": "02:00:00:00:01:0%d" % i, "NIC_NAME": "ens%d" % i, "GPU_BDF": bdf, "GPU_INDEX": i,
+                "RDMA_DEV": "rdma%d" % i, "RDMA_PORT": 1, "GID_INDEX": 3}
+               for i, bdf in enumerate(["0000:05:00.0", "0000:26:00.0", "0000:75:00.0"])]
+    (tmp_path / "rccl-net.json").write_text(json.dumps({"NIC_NET_CONFIG": entries}))
+    (tmp_path / "rccl.env").write_text("# generated\nNCCL_IB_HCA==rdma0:1,rdma1:1,rdma2:1\nNCCL_IB_GID_INDEX=3\n"
+                                       "NCCL_IB_DISABLE=0\nNCCL_IB_TC=106\n")
+    env = rail_env("0000:75:00.0", artifact_dir=str(tmp_path))
+    assert env == {"NCCL_IB_HCA": "=rdma2:1", "NCCL_IB_GID_INDEX": "3", "NCCL_IB_DISABLE": "0", "NCCL_IB_TC": "106"}
+    assert rail_env(None, gpu_index=1, artifact_dir=str(tmp_path))["NCCL_IB_HCA"] == "=rdma1:1"
+    with pytest.raises(LookupError):
+        rail_env("0000:dc:00.0", artifact_dir=str(tmp_path))
+
+
+@pytest.mark.gpu
+def test_device_bdf_names_the_gpu(cuda_device):
+    import re
+
+    from network_operator_amd.parallel.rail import device_bdf
+
+    bdf = device_bdf(0)
+    assert re.fullmatch(r"[0-9a-f]{4}:[0-9a-f]{2}:[0-9a-f]{2}\.0", bdf), bdf
+    assert os.path.exists(f"/sys/bus/pci/devices/{bdf}")
