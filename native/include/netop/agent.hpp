@@ -84,6 +84,12 @@ struct Config {
     bool disable_fw_lldp = false;
     std::string fw_lldp_flags;                        // extra rules "NAME=0|1,..."
     std::string rccl_env_extra;                       // "KEY=VALUE,..." appended to rccl.env
+    // Per-rail source routing (L3): NIC k gets routing table base+k (k = its GPU index) holding
+    // its /30 and its /16 via the switch, and a rule "from <local>/32 lookup base+k" at
+    // priority base+k.  Traffic sourced from a rail's address then leaves through that rail
+    // even though every rail's /16 route is also in the main table.  0 = off (the reference's
+    // main-table-only routing).
+    int rail_table_base = 0;
 };
 
 // Sanitises in place (MTU clamp to [1500, 9000], mode upper-cased); throws on a bad mode.
@@ -156,6 +162,9 @@ class Agent {
     void detect_lldp(int stop_fd);
     void on_lldp(NicState& n, const lldp::Frame& f);
     void add_route(NicState& n, int mask);
+    uint32_t rail_table(const NicState& n) const;
+    void add_rail_routing(NicState& n);
+    void remove_rail_routing();
     void write_artifacts();
     void write_l2_artifacts();
     void check_xgmi();

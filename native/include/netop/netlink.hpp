@@ -62,6 +62,18 @@ struct RouteSpec {
 
 using RouteInfo = RouteSpec;
 
+// Source-address policy rule (`ip rule add from <src> lookup <table> priority <priority>`),
+// used for per-rail routing tables.
+struct RuleSpec {
+    Ipv4Prefix src{};
+    uint32_t table = 0;
+    uint32_t priority = 0;
+    bool operator==(const RuleSpec& o) const {
+        return src.masked() == o.src.masked() && table == o.table && priority == o.priority;
+    }
+    std::string str() const;
+};
+
 struct LinkEvent {
     bool deleted = false;
     LinkInfo link;
@@ -86,6 +98,11 @@ class NetOps {
     virtual void addr_add(int ifindex, const Ipv4Prefix& addr) = 0;
     virtual void addr_del(const AddrInfo& addr) = 0;
     virtual void route_append(const RouteSpec& r) = 0;
+    virtual void route_del(const RouteSpec& r) = 0;
+    // Rules: add fails with EEXIST for an identical rule (NLM_F_EXCL); list returns IPv4 rules.
+    virtual void rule_add(const RuleSpec& r) = 0;
+    virtual void rule_del(const RuleSpec& r) = 0;
+    virtual std::vector<RuleSpec> rule_list() = 0;
     virtual void link_set_up(int ifindex) = 0;
     virtual void link_set_down(int ifindex) = 0;
     virtual void link_set_mtu(int ifindex, int mtu) = 0;
@@ -104,6 +121,10 @@ class Rtnl final : public NetOps {
     void addr_add(int ifindex, const Ipv4Prefix& addr) override;
     void addr_del(const AddrInfo& addr) override;
     void route_append(const RouteSpec& r) override;
+    void route_del(const RouteSpec& r) override;
+    void rule_add(const RuleSpec& r) override;
+    void rule_del(const RuleSpec& r) override;
+    std::vector<RuleSpec> rule_list() override;
     void link_set_up(int ifindex) override;
     void link_set_down(int ifindex) override;
     void link_set_mtu(int ifindex, int mtu) override;
@@ -113,7 +134,6 @@ class Rtnl final : public NetOps {
     LinkInfo link_by_index(int ifindex);
     std::vector<LinkInfo> link_list();
     std::vector<RouteInfo> route_list(uint8_t table = RT_TABLE_MAIN);
-    void route_del(const RouteSpec& r);
     void veth_add(const std::string& name, const std::string& peer);
     void link_del(int ifindex);
     void link_set_netns_fd(int ifindex, int netns_fd);
@@ -126,6 +146,7 @@ class Rtnl final : public NetOps {
 
    private:
     struct Msg;
+    void rule_request(uint16_t type, uint16_t flags, const RuleSpec& r);
     void transact(Msg& m, const std::function<void(const nlmsghdr*)>& on_reply);
     void dump(Msg& m, const std::function<void(const nlmsghdr*)>& on_item);
     void set_link(int ifindex, unsigned flags, unsigned change, const std::function<void(Msg&)>& attrs);

@@ -129,9 +129,20 @@ PYBIND11_MODULE(_netop_native, m) {
             if (!p) throw py::value_error("bad CIDR");
             r.addr_add(ifindex, *p);
         })
-        .def("route_list", [](nl::Rtnl& r) {
+        .def("rule_list", [](nl::Rtnl& r) {
             py::list l;
-            for (auto& x : r.route_list()) {
+            for (auto& x : r.rule_list()) {
+                py::dict d;
+                d["src"] = x.src.masked().str();
+                d["table"] = x.table;
+                d["priority"] = x.priority;
+                l.append(d);
+            }
+            return l;
+        })
+        .def("route_list", [](nl::Rtnl& r, int table) {
+            py::list l;
+            for (auto& x : r.route_list(uint8_t(table))) {
                 py::dict d;
                 d["dst"] = x.dst.masked().str();
                 d["gateway"] = x.gateway ? py::object(py::str(x.gateway->str())) : py::none();
@@ -139,10 +150,11 @@ PYBIND11_MODULE(_netop_native, m) {
                 d["ifindex"] = x.ifindex;
                 d["protocol"] = x.protocol;
                 d["scope"] = x.scope;
+                d["table"] = x.table;
                 l.append(d);
             }
             return l;
-        })
+        }, py::arg("table") = int(RT_TABLE_MAIN))
         .def("link_set_up", &nl::Rtnl::link_set_up)
         .def("link_set_down", &nl::Rtnl::link_set_down)
         .def("link_set_mtu", &nl::Rtnl::link_set_mtu)

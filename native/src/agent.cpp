@@ -149,6 +149,7 @@ void Agent::post_cleanups() {
     }
     if (!artifacts::remove_labels(cfg_.labels)) NLOG_W("Failed to remove NFD label file: %s", std::strerror(errno));
     NLOG_I("Restoring interfaces to original state...");
+    remove_rail_routing();
     try {
         remove_existing_ips();
     } catch (const std::exception& e) {
@@ -341,6 +342,79 @@ void Agent::add_route(NicState& n, int mask) {
     }
 }
 
+uint32_t Agent::rail_table(const NicState& n) const {
+    int k = n.gpu_index >= 0 ? n.gpu_index : int(&n - nics_.data());
+    return uint32_t(cfg_.rail_table_base + k);
+}
+
+void Agent::add_rail_routing(NicState& n) {
+    const uint32_t t = rail_table(n);
+    nl::RuleSpec rule{Ipv4Prefix{n.addr->local, 32}, t, t};
+    // A previous address of this rail (agent restart, Port Description change): its rule and
+    // its table's routes go first, so the table only ever describes the current /30.
+    for (const auto& r : ops_.rule_list())
+        if ((r.priority == t || r.table == t) && !(r == rule)) ops_.rule_del(r);
+    for (int mask : {l3::kRoutedNetworkMask, l3::kPointToPointMask}) {
+        for (int i = 0; i < 8; ++i) {  // RTM_DELROUTE without a gateway takes the first match
+            nl::RouteSpec old;
+            old.table = uint8_t(t);
+            old.dst = Ipv4Prefix{n.addr->local, mask}.masked();
+            try {
+                ops_.route_del(old);
+            } catch (const SysError&) {
+                break;
+            }
+        }
+    }
+    nl::RouteSpec p2p;
+    p2p.ifindex = n.link.index;
+    p2p.dst = n.addr->local_prefix().masked();
+    p2p.scope = RT_SCOPE_LINK;
+    p2p.prefsrc = n.addr->local;
+    p2p.table = uint8_t(t);
+    nl::RouteSpec routed;
+    routed.ifindex = n.link.index;
+    routed.dst = Ipv4Prefix{n.addr->local, l3::kRoutedNetworkMask}.masked();
+    routed.gateway = n.addr->peer;
+    routed.prefsrc = n.addr->local;
+    routed.table = uint8_t(t);
+    for (const auto& r : {p2p, routed}) {
+        try {
+            ops_.route_append(r);
+        } catch (const SysError& e) {
+            if (e.code() != EEXIST) throw;
+        }
+    }
+    try {
+        ops_.rule_add(rule);
+    } catch (const SysError& e) {
+        if (e.code() != EEXIST) throw;
+    }
+    NLOG_V(3, "Rail routing for '%s': table %u, rule %s", n.ifname.c_str(), t, rule.str().c_str());
+}
+
+void Agent::remove_rail_routing() {
+    if (cfg_.rail_table_base <= 0) return;
+    for (auto& n : nics_) {
+        if (!n.addr) continue;
+        const uint32_t t = rail_table(n);
+        try {
+            ops_.rule_del(nl::RuleSpec{Ipv4Prefix{n.addr->local, 32}, t, t});
+        } catch (const SysError& e) {
+            if (e.code() != ENOENT) NLOG_W("Could not remove the rail rule of '%s': %s", n.ifname.c_str(), e.what());
+        }
+        for (int mask : {l3::kRoutedNetworkMask, l3::kPointToPointMask}) {
+            nl::RouteSpec r;
+            r.table = uint8_t(t);
+            r.dst = Ipv4Prefix{n.addr->local, mask}.masked();
+            try {
+                ops_.route_del(r);
+            } catch (...) {  // already gone with the address / link
+            }
+        }
+    }
+}
+
 bool Agent::configure_interface(NicState& n) {
     if (!n.addr || n.configured) return n.configured;
     std::vector<nl::AddrInfo> addrs;
@@ -362,6 +436,7 @@ bool Agent::configure_interface(NicState& n) {
             add_route(n, l3::kPointToPointMask);
         }
         add_route(n, l3::kRoutedNetworkMask);
+        if (cfg_.rail_table_base > 0) add_rail_routing(n);
     } catch (const std::exception& e) {
         n.config_error = e.what();
         if (!existing) NLOG_W("Could not configure address %s for interface '%s': %s", n.addr->local.str().c_str(), n.ifname.c_str(), e.what());

@@ -62,6 +62,10 @@ std::string RouteSpec::str() const {
     return s;
 }
 
+std::string RuleSpec::str() const {
+    return strfmt("from %s lookup %u priority %u", src.masked().str().c_str(), table, priority);
+}
+
 // ---------------------------------------------------------------------------
 // Message builder
 // ---------------------------------------------------------------------------
@@ -522,6 +526,58 @@ std::vector<RouteInfo> Rtnl::route_list(uint8_t table) {
     return out;
 }
 
+namespace {
+// FIB rule messages: struct fib_rule_hdr (linux/fib_rules.h) shares rtmsg's layout for the
+// fields used here (family, dst_len, src_len, tos, table, res1, res2, action, flags).
+constexpr uint16_t kFraSrc = 2, kFraPriority = 6, kFraTable = 15;  // FRA_SRC, FRA_PRIORITY, FRA_TABLE
+constexpr uint8_t kFrActToTbl = 1;                                  // FR_ACT_TO_TBL
+struct FibRuleHdr {
+    uint8_t family, dst_len, src_len, tos, table, res1, res2, action;
+    uint32_t flags;
+};
+}  // namespace
+
+void Rtnl::rule_request(uint16_t type, uint16_t flags, const RuleSpec& r) {
+    Msg m(type, flags);
+    FibRuleHdr frh{};
+    frh.family = AF_INET;
+    frh.src_len = uint8_t(r.src.len);
+    frh.table = r.table < 256 ? uint8_t(r.table) : uint8_t(RT_TABLE_UNSPEC);
+    frh.action = kFrActToTbl;
+    m.put(frh);
+    if (r.src.len) m.attr_ip(kFraSrc, r.src.network());
+    m.attr_u32(kFraTable, r.table);
+    if (r.priority) m.attr_u32(kFraPriority, r.priority);
+    transact(m, nullptr);
+}
+
+void Rtnl::rule_add(const RuleSpec& r) { rule_request(RTM_NEWRULE, NLM_F_CREATE | NLM_F_EXCL, r); }
+
+void Rtnl::rule_del(const RuleSpec& r) { rule_request(RTM_DELRULE, 0, r); }
+
+std::vector<RuleSpec> Rtnl::rule_list() {
+    Msg m(RTM_GETRULE, 0);
+    FibRuleHdr frh{};
+    frh.family = AF_INET;
+    m.put(frh);
+    std::vector<RuleSpec> out;
+    dump(m, [&](const nlmsghdr* h) {
+        if (h->nlmsg_type != RTM_NEWRULE || h->nlmsg_len < NLMSG_LENGTH(sizeof(FibRuleHdr))) return;
+        const auto* f = reinterpret_cast<const FibRuleHdr*>(NLMSG_DATA(h));
+        RuleSpec r;
+        r.src.len = f->src_len;
+        r.table = f->table;
+        const auto* first = reinterpret_cast<const rtattr*>(reinterpret_cast<const char*>(f) + NLMSG_ALIGN(sizeof(FibRuleHdr)));
+        for_each_attr(first, h->nlmsg_len - NLMSG_LENGTH(NLMSG_ALIGN(sizeof(FibRuleHdr))), [&](const rtattr* a) {
+            if (a->rta_type == kFraSrc && RTA_PAYLOAD(a) == 4) r.src.addr = Ipv4::from_net(RTA_DATA(a));
+            if (a->rta_type == kFraPriority && RTA_PAYLOAD(a) >= 4) std::memcpy(&r.priority, RTA_DATA(a), 4);
+            if (a->rta_type == kFraTable && RTA_PAYLOAD(a) >= 4) std::memcpy(&r.table, RTA_DATA(a), 4);
+        });
+        out.push_back(r);
+    });
+    return out;
+}
+
 void Rtnl::set_link(int ifindex, unsigned flags, unsigned change, const std::function<void(Msg&)>& attrs) {
     Msg m(RTM_NEWLINK, 0);
     ifinfomsg ifi{};
@@ -629,3 +685,4 @@ class RtnlLinkWatcher final : public LinkWatcher {
 std::unique_ptr<LinkWatcher> Rtnl::subscribe_links() { return std::make_unique<RtnlLinkWatcher>(); }
 
 }  // namespace netop::nl
+

@@ -17,6 +17,7 @@ struct FakeNetOps : netop::nl::NetOps {
     std::map<std::string, netop::nl::LinkInfo> links;
     std::vector<netop::nl::AddrInfo> addrs;
     std::vector<netop::nl::RouteSpec> routes;
+    std::vector<netop::nl::RuleSpec> rules;
     std::set<std::string> fail;  // op names that throw: "link_by_name", "addr_list", ...
     int fail_errno = EPERM;
     bool echo_links = true;      // emit RTM_NEWLINK on set up/down
@@ -89,9 +90,33 @@ struct FakeNetOps : netop::nl::NetOps {
     void route_append(const netop::nl::RouteSpec& r) override {
         maybe_fail("route_append");
         for (auto& x : routes)
-            if (x.ifindex == r.ifindex && x.dst.masked() == r.dst.masked() && x.gateway == r.gateway)
+            if (x.ifindex == r.ifindex && x.dst.masked() == r.dst.masked() && x.gateway == r.gateway && x.table == r.table)
                 throw netop::SysError(EEXIST, "route exists");
         routes.push_back(r);
+    }
+    void route_del(const netop::nl::RouteSpec& r) override {
+        maybe_fail("route_del");
+        auto it = std::find_if(routes.begin(), routes.end(), [&](const netop::nl::RouteSpec& x) {
+            return x.dst.masked() == r.dst.masked() && x.table == r.table && (!r.gateway || x.gateway == r.gateway) &&
+                   (r.ifindex <= 0 || x.ifindex == r.ifindex);
+        });
+        if (it == routes.end()) throw netop::SysError(ESRCH, "no such route");
+        routes.erase(it);
+    }
+    void rule_add(const netop::nl::RuleSpec& r) override {
+        maybe_fail("rule_add");
+        if (std::find(rules.begin(), rules.end(), r) != rules.end()) throw netop::SysError(EEXIST, "rule exists");
+        rules.push_back(r);
+    }
+    void rule_del(const netop::nl::RuleSpec& r) override {
+        maybe_fail("rule_del");
+        auto it = std::find(rules.begin(), rules.end(), r);
+        if (it == rules.end()) throw netop::SysError(ENOENT, "no such rule");
+        rules.erase(it);
+    }
+    std::vector<netop::nl::RuleSpec> rule_list() override {
+        maybe_fail("rule_list");
+        return rules;
     }
     void set_flag(int ifindex, bool up) {
         auto* l = by_index(ifindex);

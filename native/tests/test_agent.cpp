@@ -158,6 +158,59 @@ TEST(agent_l3_routes_and_label_while_running) {
     CHECK(!path_exists(f.cfg.labels.path()));  // label only with --keep-running (main.go:239)
 }
 
+bool has_table_route(FakeNetOps& o, int idx, const char* dst, const char* gw, int table) {
+    for (auto& r : o.routes)
+        if (r.table == table && r.ifindex == idx && r.dst.masked().str() == dst &&
+            (gw ? (r.gateway && r.gateway->str() == gw) : !r.gateway))
+            return true;
+    return false;
+}
+
+TEST(agent_rail_tables_route_each_source_through_its_nic) {
+    Fixture f;
+    f.cfg.keep_running = false;
+    f.cfg.rail_table_base = 100;
+    f.ops.rules.push_back(nl::RuleSpec{*Ipv4Prefix::parse("10.9.9.9/32"), 100, 100});  // a previous run's address
+    agent::Agent a(f.cfg, f.ops, f.all_valid(), f.nm());
+    a.run(-1);
+    // main table unchanged (the reference's routes), plus one table per rail
+    CHECK(has_route(f.ops, 10, "10.200.0.0/16", "10.200.0.2"));
+    CHECK(has_table_route(f.ops, 10, "10.200.0.0/30", nullptr, 100));
+    CHECK(has_table_route(f.ops, 10, "10.200.0.0/16", "10.200.0.2", 100));
+    CHECK(has_table_route(f.ops, 11, "10.200.0.4/30", nullptr, 101));
+    CHECK(has_table_route(f.ops, 11, "10.200.0.0/16", "10.200.0.6", 101));
+    CHECK(has_table_route(f.ops, 12, "10.200.0.0/16", "10.200.0.9", 102));
+    CHECK_EQ(f.ops.rules.size(), size_t(3));  // the stale rule of table 100 is gone
+    CHECK(f.ops.rules[0] == (nl::RuleSpec{*Ipv4Prefix::parse("10.200.0.1/32"), 100, 100}));
+    CHECK(f.ops.rules[2] == (nl::RuleSpec{*Ipv4Prefix::parse("10.200.0.10/32"), 102, 102}));
+    CHECK(a.nics()[1].configured);
+}
+
+TEST(agent_rail_tables_removed_on_sigterm) {
+    Fixture f;
+    f.cfg.rail_table_base = 100;
+    Pipe stop;
+    stop.fire();
+    agent::Agent a(f.cfg, f.ops, f.all_valid(), f.nm());
+    a.run(stop.fd[0]);
+    CHECK(a.ready());
+    CHECK(f.ops.rules.empty());
+    for (auto& r : f.ops.routes) CHECK(r.table < 100 || r.table > 102);
+}
+
+TEST(agent_rail_rule_failure_leaves_nic_unconfigured) {
+    Fixture f;
+    f.cfg.keep_running = false;
+    f.cfg.rail_table_base = 100;
+    f.ops.fail.insert("rule_add");
+    agent::Agent a(f.cfg, f.ops, f.all_valid(), f.nm());
+    try {
+        a.run(-1);
+    } catch (...) {
+    }
+    for (auto& n : a.nics()) CHECK(!n.configured && !n.config_error.empty());
+}
+
 TEST(agent_reference_fixture_partial_failure) {
     // network_test.go:138-202: one valid NIC, one garbage Port Description.
     Fixture f;

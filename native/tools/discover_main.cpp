@@ -59,6 +59,8 @@ int main(int argc, char** argv) {
     fs.add_string("nfd-label-file", &cfg.labels.file, "readiness label file name inside the features directory");
     fs.add_string("nfd-label", &cfg.labels.key, "readiness label key (published as KEY=true; KEY.mode, KEY.nics, ... alongside)");
     fs.add_string("rccl-env", &cfg.rccl_env, "write an RCCL environment file (NCCL_IB_HCA, NCCL_IB_GID_INDEX, ...)");
+    fs.add_int("rail-table-base", &cfg.rail_table_base,
+               "L3: per-rail source routing; NIC k (its GPU index) gets routing table and rule priority base+k (0 = off)");
     fs.add_string("rccl-env-extra", &cfg.rccl_env_extra, "site settings appended to the RCCL environment file: KEY=VALUE[,...] (NCCL_*, RCCL_*, HSA_*)");
     fs.add_string("status-file", &cfg.status_file, "write a JSON status document (per-NIC results, phase timings)");
     fs.add_string("nm-keyfile-dir", &cfg.nm_keyfile_dir, "with --disable-networkmanager, also persist an unmanaged-devices keyfile here");
@@ -104,6 +106,10 @@ int main(int argc, char** argv) {
     auto tp = l3::parse_token_policy(token_policy);
     if (!dm || !tp) {
         std::fprintf(stderr, "Error: invalid --nic-discovery or --token-policy\n");
+        return 2;
+    }
+    if (cfg.rail_table_base < 0 || cfg.rail_table_base > 200) {
+        std::fprintf(stderr, "Error: --rail-table-base must be 0 (off) or 1..200\n");
         return 2;
     }
     cfg.discovery.mode = *dm;

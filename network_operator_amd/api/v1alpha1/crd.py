@@ -71,6 +71,10 @@ def openapi_schema() -> dict:
                         "additionalProperties": {"type": "string"}, "type": "object"},
             "metricsPort": {"description": "Serve agent metrics (/metrics, /healthz, /readyz) on this host port (0 = off).",
                             "maximum": 65535, "minimum": 0, "type": "integer"},
+            "railTableBase": {"description": "L3: per-rail source routing.  The NIC of GPU k gets routing table and rule\n"
+                                             "priority railTableBase+k (its /30 and its /16 via the switch), so traffic\n"
+                                             "from a rail's address leaves through that rail.  0 = off.",
+                              "maximum": 200, "minimum": 0, "type": "integer"},
         },
     }
     host_nic = {

@@ -61,10 +61,12 @@ class AmdScaleOutSpec:
     metricsPort: int = 0
     gpuDirectRdma: str = ""
     rcclEnv: Dict[str, str] = field(default_factory=dict)
+    railTableBase: int = 0
     extra: Dict[str, Any] = field(default_factory=dict)
 
     _FIELDS = ("disableNetworkManager", "layer", "image", "pullPolicy", "mtu", "xgmiCheck", "lldpAnnounce",
-               "interfaces", "nicDrivers", "disableFirmwareLldp", "metricsPort", "gpuDirectRdma", "rcclEnv")
+               "interfaces", "nicDrivers", "disableFirmwareLldp", "metricsPort", "gpuDirectRdma", "rcclEnv",
+               "railTableBase")
 
     def to_dict(self) -> dict:
         d: dict = {}
@@ -92,6 +94,8 @@ class AmdScaleOutSpec:
             d["gpuDirectRdma"] = self.gpuDirectRdma
         if self.rcclEnv:
             d["rcclEnv"] = dict(self.rcclEnv)
+        if self.railTableBase:
+            d["railTableBase"] = self.railTableBase
         d.update(copy.deepcopy(self.extra))
         return d
 
@@ -112,6 +116,7 @@ class AmdScaleOutSpec:
             metricsPort=int(d.pop("metricsPort", 0) or 0),
             gpuDirectRdma=d.pop("gpuDirectRdma", "") or "",
             rcclEnv=dict(d.pop("rcclEnv", {}) or {}),
+            railTableBase=int(d.pop("railTableBase", 0) or 0),
         )
         s.extra = d
         return s

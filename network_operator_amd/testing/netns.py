@@ -263,6 +263,8 @@ def run_scenario(n_nics: int = 8, mode: str = "L3", seed: int | None = None, int
             except OSError as e:
                 state[node_if] = {"error": str(e)}
         res["state"] = state
+        res["rules"] = [r for r in rt.rule_list() if 0 < r["priority"] < 32766]  # not the kernel's defaults
+        res["rail_tables"] = {r["table"]: rt.route_list(r["table"]) for r in res["rules"]}
         if t_ready:  # the agent writes status.json (ready=true) right after the label
             end = time.monotonic() + 5
             while time.monotonic() < end and agent.poll() is None:
@@ -334,6 +336,7 @@ def run_scenario(n_nics: int = 8, mode: str = "L3", seed: int | None = None, int
             link = rt.link_by_name(node_if)
             after[node_if] = {"up": link["up"], "addrs": rt.addr_list(link["index"])}
         res["after_sigterm"] = after
+        res["rules_after_sigterm"] = [r for r in rt.rule_list() if 0 < r["priority"] < 32766]
         res["label_after_sigterm"] = label.exists()
         os.kill(pid, signal.SIGTERM)
         os.waitpid(pid, 0)

@@ -190,3 +190,21 @@ def test_late_rocev2_gids_are_waited_for():
     r = netns.run_isolated(n_nics=2, seed=22, interval="1s", gid_delay_s=0.3)
     _check_configured(r)
     assert "NCCL_IB_GID_INDEX=3" in r["rccl_env"]
+
+
+def test_rail_tables_in_the_kernel():
+    """--rail-table-base: one routing table per NIC (its /30 and its /16 via the switch port) and
+    a source rule per NIC address in the real kernel; all removed on SIGTERM."""
+    r = netns.run_isolated(n_nics=3, seed=23, interval="1s", fast_start=True, extra_args=["--rail-table-base=100"])
+    _check_configured(r)
+    rules = sorted(r["rules"], key=lambda x: x["priority"])
+    assert [x["priority"] for x in rules] == [100, 101, 102], rules
+    by_src = {x["src"]: x["table"] for x in rules}
+    for nic, p in zip(r["nics"], r["plan"]):
+        table = by_src[p["local"] + "/32"]
+        routes = r["rail_tables"][str(table)]  # JSON object keys
+        assert sorted(x["dst"] for x in routes) == sorted([p["p2p"], p["routed"]]), routes
+        gw = [x for x in routes if x["gateway"]]
+        assert len(gw) == 1 and gw[0]["gateway"] == p["peer"], routes
+        assert all(x["ifindex"] == routes[0]["ifindex"] for x in routes)
+    assert r["rules_after_sigterm"] == []

@@ -487,3 +487,16 @@ def test_status_conditions_ready_degraded_and_observed_generation():
     c = {x["type"]: x for x in policy_conditions([], 0, 0, ["dependency missing: node-feature-discovery"], 3, "T0")}
     assert c["Ready"]["reason"] == "NoTargets" and c["Degraded"]["reason"] == "DependencyMissing"
     assert c["Ready"]["lastTransitionTime"] == "T0" and c["Ready"]["observedGeneration"] == 3
+
+
+def test_agent_args_rail_tables_l3_only():
+    from network_operator_amd.api.v1alpha1 import types as T
+    from network_operator_amd.operator.reconciler import agent_args
+
+    p = T.new_policy("p", layer="L3")
+    assert not any(a.startswith("--rail-table-base") for a in agent_args(p))
+    p.spec.amdScaleOut.railTableBase = 100
+    assert "--rail-table-base=100" in agent_args(p)
+    assert T.NetworkClusterPolicy.from_dict(p.to_dict()).spec.amdScaleOut.railTableBase == 100
+    p.spec.amdScaleOut.layer = "L2"  # no addresses in L2: nothing to route
+    assert not any(a.startswith("--rail-table-base") for a in agent_args(p))
