@@ -132,12 +132,43 @@ def set_switch_port(pid: int, port: str, up: bool) -> None:
         raise RuntimeError(f"could not set {port} {'up' if up else 'down'} in the switch namespace")
 
 
+def _tx_packets() -> dict:
+    """Transmitted packets per interface of this network namespace (/proc/net/dev follows it)."""
+    out = {}
+    for line in Path("/proc/net/dev").read_text().splitlines()[2:]:
+        name, data = line.split(":", 1)
+        out[name.strip()] = int(data.split()[9])
+    return out
+
+
+def egress_matrix(nic_names: list, plan: list, packets: int = 20) -> list:
+    """For each NIC k: send UDP datagrams from a socket bound to NIC k's address to an off-link
+    address of the routed /16 and count which NICs transmitted them.  Row k is the per-NIC
+    packet delta; with per-rail tables all of row k lands on NIC k."""
+    import ipaddress
+    import socket
+
+    rows = []
+    for p in plan:
+        dst = str(ipaddress.ip_network(p["routed"]).broadcast_address - 1)  # x.y.255.254: behind the switch
+        before = _tx_packets()
+        with socket.socket(socket.AF_INET, socket.SOCK_DGRAM) as s:
+            s.bind((p["local"], 0))
+            for _ in range(packets):
+                s.sendto(b"rail-probe", (dst, 9))
+        time.sleep(0.05)
+        after = _tx_packets()
+        rows.append([after.get(n, 0) - before.get(n, 0) for n in nic_names])
+    return rows
+
+
 def run_scenario(n_nics: int = 8, mode: str = "L3", seed: int | None = None, interval: str = "30s",
                  fast_start: bool = True, announce: bool = True, phase: str = "random", wait: str = "90s",
                  mtu: int = 9000, pipeline: bool = True, bad_nics: int = 0, silent_nics: int = 0,
                  xgmi_expect: int = 0, keep_tmp: bool = False, sigterm: bool = True, verbose: int = 2,
                  drop_xgmi: list | None = None, extra_args: list | None = None, flap_port: int | None = None,
-                 crash_restart: bool = False, crash_after_s: float = 0.0, gid_delay_s: float = 0.0) -> dict:
+                 crash_restart: bool = False, crash_after_s: float = 0.0, gid_delay_s: float = 0.0,
+                 egress_probe: bool = False) -> dict:
     """Runs one node bring-up.  Must already be inside a private user+net namespace."""
     from . import fakesysfs
 
@@ -264,6 +295,8 @@ def run_scenario(n_nics: int = 8, mode: str = "L3", seed: int | None = None, int
                 state[node_if] = {"error": str(e)}
         res["state"] = state
         res["rules"] = [r for r in rt.rule_list() if 0 < r["priority"] < 32766]  # not the kernel's defaults
+        if egress_probe and t_ready:
+            res["egress"] = egress_matrix(nic_names, plan)
         res["rail_tables"] = {r["table"]: rt.route_list(r["table"]) for r in res["rules"]}
         if t_ready:  # the agent writes status.json (ready=true) right after the label
             end = time.monotonic() + 5

@@ -195,8 +195,13 @@ def test_late_rocev2_gids_are_waited_for():
 def test_rail_tables_in_the_kernel():
     """--rail-table-base: one routing table per NIC (its /30 and its /16 via the switch port) and
     a source rule per NIC address in the real kernel; all removed on SIGTERM."""
-    r = netns.run_isolated(n_nics=3, seed=23, interval="1s", fast_start=True, extra_args=["--rail-table-base=100"])
+    r = netns.run_isolated(n_nics=3, seed=23, interval="1s", fast_start=True, extra_args=["--rail-table-base=100"],
+                           egress_probe=True)
     _check_configured(r)
+    # the kernel's routing decision: datagrams from NIC k's address leave through NIC k only
+    for k, row in enumerate(r["egress"]):
+        # (a few stray frames — LLDP announces, IPv6 ND — can land anywhere)
+        assert row[k] >= 20 and max(x for j, x in enumerate(row) if j != k) <= 5, r["egress"]
     rules = sorted(r["rules"], key=lambda x: x["priority"])
     assert [x["priority"] for x in rules] == [100, 101, 102], rules
     by_src = {x["src"]: x["table"] for x in rules}
@@ -208,3 +213,13 @@ def test_rail_tables_in_the_kernel():
         assert len(gw) == 1 and gw[0]["gateway"] == p["peer"], routes
         assert all(x["ifindex"] == routes[0]["ifindex"] for x in routes)
     assert r["rules_after_sigterm"] == []
+
+
+def test_without_rail_tables_sources_share_one_egress():
+    """The reference's main-table-only routing: every NIC's /16 route has the same prefix and
+    metric, so the kernel sends all off-link traffic through one NIC whatever the source
+    address — the case --rail-table-base exists for."""
+    r = netns.run_isolated(n_nics=3, seed=23, interval="1s", fast_start=True, egress_probe=True)
+    _check_configured(r)
+    busiest = [max(range(len(row)), key=row.__getitem__) for row in r["egress"]]
+    assert len(set(busiest)) == 1 and all(row[busiest[0]] >= 20 for row in r["egress"]), r["egress"]
