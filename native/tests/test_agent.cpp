@@ -516,6 +516,46 @@ TEST(agent_monitor_port_description_change_reconfigures) {
     CHECK(j && j->find("10.201.7.1") != std::string::npos);
 }
 
+TEST(agent_monitor_rail_tables_follow_flaps_and_readdressing) {
+    Fixture f;
+    f.cfg.monitor_tick_ns = 1000000;
+    f.cfg.rail_table_base = 100;
+    Pipe stop;
+    auto src = f.all_valid();
+    ScriptedLldp* raw = src.get();
+    agent::Agent a(f.cfg, f.ops, std::move(src), f.nm());
+    bool back = false, moved = false;
+    a.on_monitor_tick = [&](int tick) {
+        auto& l = f.ops.links["ens0"];
+        if (tick == 1) {  // admin down flushes every route of the device, in every table
+            l.flags &= ~unsigned(IFF_UP);
+            f.ops.routes.erase(std::remove_if(f.ops.routes.begin(), f.ops.routes.end(),
+                                              [](const nl::RouteSpec& r) { return r.ifindex == 10; }),
+                               f.ops.routes.end());
+            f.ops.events.push_back({false, l});
+        } else if (tick == 2) {
+            l.flags |= IFF_UP;
+            f.ops.events.push_back({false, l});
+        } else if (tick == 4) {
+            back = has_table_route(f.ops, 10, "10.200.0.0/16", "10.200.0.2", 100) &&
+                   has_table_route(f.ops, 10, "10.200.0.0/30", nullptr, 100);
+            raw->frames["ens1"] = sw("02:aa:00:00:00:01", "no-alert 10.201.7.2/30");
+        } else if (tick == 6) {
+            bool new_rule = false, old_rule = false;
+            for (auto& r : f.ops.rules) {
+                new_rule |= r == nl::RuleSpec{*Ipv4Prefix::parse("10.201.7.1/32"), 101, 101};
+                old_rule |= r.src.addr.str() == "10.200.0.5";
+            }
+            moved = new_rule && !old_rule && has_table_route(f.ops, 11, "10.201.0.0/16", "10.201.7.2", 101);
+            stop.fire();
+        }
+    };
+    a.run(stop.fd[0]);
+    CHECK(back);
+    CHECK(moved);
+    CHECK(f.ops.rules.empty());  // SIGTERM cleanup
+}
+
 TEST(agent_metrics_endpoint) {
     Fixture f;
     f.cfg.metrics_addr = "127.0.0.1:0";
