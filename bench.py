@@ -5,13 +5,17 @@ BASELINE.json metric: "node scale-out-ready latency (s) + rccl all-reduce busbw 
 1/2/4/8 GPU", config "L3 mode, 8xMI355X single node: all xGMI + host RoCE links configured,
 rccl-tests 8-GPU all-reduce".
 
-* One process per GPU (``torchrun --nproc-per-node N``), ``torch.distributed`` backend
-  ``nccl`` (= RCCL over xGMI on ROCm).  A *step* is one in-place bf16 all-reduce of
+* One process per GPU, ``torch.distributed`` backend ``nccl`` (= RCCL over xGMI on ROCm).
+  Under ``torchrun --nproc-per-node N`` the launcher's ranks are used (WORLD_SIZE must equal
+  ``--gpus``); a bare ``python bench.py --gpus N`` starts the N rank processes itself.
+  ``config.model`` names the BASELINE.json config of the world size that actually ran.  A *step* is one in-place bf16 all-reduce of
   ``--bytes`` per rank (default 1 GiB, rccl-tests' large-message regime); ``--warmup``
   untimed steps, then exactly ``--steps`` timed steps bracketed by barrier +
   ``torch.cuda.synchronize()``, max over ranks.
-* ``value`` is busbw = algbw * 2(n-1)/n (rccl-tests definition).  At n = 1 there are no
-  links and busbw is 0 by definition; algbw and latency are still reported.
+* ``value`` is busbw = algbw * 2(n-1)/n (rccl-tests definition, per rank;
+  ``aggregate_busbw_GBps`` is n times that).  At n = 1 there are no links and busbw is 0 by
+  definition; the single-rank all-reduce is a no-op, so algbw is reported as null with the
+  reason and ``node_ready_gpu_side`` times the agent phases that run unprivileged on the box.
 * Before timing, the result of one all-reduce of rank-specific patterns is verified exactly
   with the HIP kernels in ``libnetop_hip.so`` (fails loudly if the library is missing).
 * The node-ready latency half of the metric needs a private network namespace (root /
@@ -30,8 +34,17 @@ import sys
 import time
 
 METRIC = "node scale-out-ready latency (s) + rccl all-reduce busbw GB/s at 1/2/4/8 GPU"
-CONFIG_NAME = ("L3 mode, 8xMI355X single node: all xGMI + host RoCE links configured, "
-               "rccl-tests 8-GPU all-reduce")
+
+
+def config_name(n: int) -> str:
+    """The BASELINE.json config this run measures, from the world size actually running."""
+    if n == 1:  # BASELINE.json configs[1]
+        return "L3 mode, 1xMI355X: mock-switch LLDP /30 Port-Description -> one NIC up + NFD scale-out label"
+    if n == 8:  # BASELINE.json configs[2]
+        return ("L3 mode, 8xMI355X single node: all xGMI + host RoCE links configured, "
+                "rccl-tests 8-GPU all-reduce")
+    return (f"L3 mode, {n}xMI355X single node (first {n} GPUs of the 8-GPU node): xGMI links among {n} GPUs, "
+            f"rccl-tests {n}-GPU all-reduce")
 
 
 def _free_port() -> int:
@@ -40,6 +53,96 @@ def _free_port() -> int:
     p = s.getsockname()[1]
     s.close()
     return p
+
+
+def _spawn_ranks(n: int, argv: list[str], device: str) -> int:
+    """``python bench.py --gpus N`` without a launcher: start N rank processes (one per GPU,
+    torchrun-style env) and wait for them.  This process never touches the GPU (counting devices
+    does not initialise HIP on this image), so the ranks are ordinary children, not an exec.
+    Only rank 0 prints the JSON line; if any rank fails the others are stopped."""
+    import signal
+    import subprocess
+
+    if device == "cuda":
+        import torch
+
+        have = torch.cuda.device_count()
+        if have < n:
+            print(f"bench.py --gpus {n}: only {have} GPU(s) visible", file=sys.stderr)
+            return 2
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env))
+    rc = 0
+    try:
+        while procs:
+            for p in list(procs):
+                code = p.poll()
+                if code is None:
+                    continue
+                procs.remove(p)
+                if code != 0 and rc == 0:
+                    rc = code if code > 0 else 128 - code
+                    for q in procs:  # one rank died: the rest would hang in the next collective
+                        q.send_signal(signal.SIGTERM)
+            time.sleep(0.05)
+    except KeyboardInterrupt:
+        for q in procs:
+            q.send_signal(signal.SIGTERM)
+        raise
+    finally:
+        for q in procs:
+            try:
+                q.wait(30)
+            except subprocess.TimeoutExpired:
+                q.kill()
+    return rc
+
+
+def node_ready_gpu_side(sysfs: str = "/sys/") -> dict:
+    """Times the node agent's phases that need no privileges, against the real sysfs of the
+    box: GPU<->NIC PCIe-affinity discovery, KFD xGMI mesh check, GPUDirect RDMA detection,
+    and the RCCL artifacts (rccl.env + NCCL_TOPO_FILE XML) and NFD label written to a scratch
+    directory.  A component of node-ready latency, not the metric: link-up, LLDP and the netlink
+    writes need NET_ADMIN/NET_RAW and run in the netns harness (``--node-ready``)."""
+    import tempfile
+
+    from network_operator_amd.agent import native
+
+    m = native()
+    out: dict = {"what": "agent phases that need no privileges, real /sys of this box (component, not the metric)",
+                 "phases_ms": {}}
+
+    def timed(name, fn):
+        t = time.perf_counter()
+        r = fn()
+        out["phases_ms"][name] = round((time.perf_counter() - t) * 1e3, 4)
+        return r
+
+    d = timed("discover", lambda: m.discover(sysfs, "affine"))
+    x = timed("xgmi", lambda: m.read_xgmi(sysfs))
+    g = timed("gdr", lambda: m.detect_gdr(sysfs))
+    with tempfile.TemporaryDirectory() as tmp:
+        if hasattr(m, "write_node_artifacts"):
+            a = timed("artifacts", lambda: m.write_node_artifacts(sysfs, tmp))
+            out["artifacts"] = {k: os.path.basename(v) for k, v in a.items()}
+        lab = os.path.join(tmp, "scale-out-readiness.txt")
+
+        def label():
+            with open(lab + ".tmp", "w") as f:
+                f.write("amd.feature.node.kubernetes.io/gpu-scale-out=true\n")
+            os.replace(lab + ".tmp", lab)
+
+        timed("label", label)
+    out["total_ms"] = round(sum(out["phases_ms"].values()), 4)
+    out["gpus"] = len(d["gpus"])
+    out["nics_paired"] = len(d["pairs"])
+    out["xgmi_pairs"] = f"{x['pairs_connected']}/{x['pairs_expected']}"
+    out["gpudirect_rdma"] = g["mode"]
+    return out
 
 
 def _rccl_autotune(rank: int, world: int, nbytes: int, started: float = time.time()) -> dict:
@@ -106,19 +209,26 @@ def main(argv=None) -> int:
                     help="also run the direct two-shot xGMI all-reduce on rank 0 (n > 1)")
     # CPU rehearsal of the multi-rank path (tests): gloo backend, fp32 on the host.
     ap.add_argument("--device", choices=["cuda", "cpu"], default="cuda", help=argparse.SUPPRESS)
-    args = ap.parse_args(argv)
+    raw_argv = list(sys.argv[1:] if argv is None else argv)
+    args = ap.parse_args(raw_argv)
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return _spawn_ranks(args.gpus, raw_argv, args.device)
 
     import torch
     import torch.distributed as dist
 
-    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     from network_operator_amd.parallel import collectives as C
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        print(f"warning: --gpus={args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+        print(f"bench.py: --gpus={args.gpus} but the launcher started WORLD_SIZE={world} ranks", file=sys.stderr)
+        return 2
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", str(_free_port()))
     if args.device == "cpu":
@@ -256,6 +366,13 @@ def main(argv=None) -> int:
         except Exception as e:
             direct_mp = {"error": str(e)[-500:]}
 
+    gpu_side = None
+    if rank == 0:
+        try:
+            gpu_side = node_ready_gpu_side()
+        except Exception as e:
+            gpu_side = {"error": str(e)[-300:]}
+
     node_ready = None
     node_ready_note = None
     if rank == 0 and args.node_ready != "off":
@@ -274,6 +391,15 @@ def main(argv=None) -> int:
 
     dist.barrier(group=host_pg)
     ceiling = C.xgmi_busbw_ceiling_GBps(world)
+    # A single-rank in-place all-reduce moves no bytes (RCCL returns at once): bytes/time would be
+    # a number with no meaning (round 1 printed 93 TB/s, 12x HBM peak).  Report null and why.
+    algbw_note = None
+    if world == 1:
+        algbw = None
+        algbw_note = ("n=1: the timed in-place all-reduce is a no-op in RCCL (no peer, no copy), so algbw is "
+                      "not a bandwidth; ms_per_step is its launch latency. busbw is 0 by definition")
+        for row in sweep:
+            row["algbw_GBps"] = None
     if rank == 0:
         line = {
             "metric": METRIC,
@@ -288,8 +414,9 @@ def main(argv=None) -> int:
             "vs_baseline": None,
             "dtype": "bf16" if args.device == "cuda" else "fp32",
             "data": "synthetic (zeros for the timed loop; exact pattern check before timing)",
-            "config": {"model": CONFIG_NAME, "global_batch": None, "seq_len": None,
-                       "parallelism": f"dp{world}", "message_bytes_per_rank": nbytes, "op": "all_reduce(sum)",
+            "config": {"model": config_name(world), "global_batch": None, "seq_len": None,
+                       "parallelism": f"dp{world}", "gpus": world, "message_bytes_per_rank": nbytes,
+                       "op": "all_reduce(sum)",
                        "backend": ("torch.distributed nccl (RCCL)" if args.device == "cuda"
                                    else "torch.distributed gloo (CPU rehearsal)")},
             "collectives": others,
@@ -299,19 +426,23 @@ def main(argv=None) -> int:
             "xgmi_allreduce": direct,
             "xgmi_allreduce_multiprocess": direct_mp,
             "algbw_GBps": algbw,
+            "algbw_note": algbw_note,
             "busbw_GBps": busbw,
+            # rccl-tests busbw is per rank; the whole job moves n times that over the links.
+            "aggregate_busbw_GBps": busbw * world,
             "busbw_ceiling_GBps": ceiling,
             "busbw_vs_ceiling": (busbw / ceiling) if ceiling else None,
             "verified": verified,
             "verify_errors": errors,
             "sweep": sweep,
             "node_ready": node_ready,
+            "node_ready_gpu_side": gpu_side,
             "xgmi_traffic": ({"links_up": xgmi_traffic["links_up"],
                               "links_with_traffic": xgmi_traffic["links_with_traffic"],
                               "GB_per_gpu": [round(sum(g["bytes_per_link"]) / 1e9, 3) for g in xgmi_traffic["gpus"]]}
                              if xgmi_traffic else None),
-            "notes": ("n=1: busbw is 0 by definition (rccl-tests factor 2(n-1)/n); reference publishes no numbers "
-                      "(BASELINE.md) so vs_baseline is null") + (f"; {node_ready_note}" if node_ready_note else "")
+            "notes": (("n=1: busbw is 0 by definition (rccl-tests factor 2(n-1)/n); " if world == 1 else "")
+                      + "reference publishes no numbers (BASELINE.md) so vs_baseline is null") + (f"; {node_ready_note}" if node_ready_note else "")
                      + (f"; {smi_note}" if smi_note else ""),
             "rccl_version": (".".join(str(x) for x in torch.cuda.nccl.version())
                              if args.device == "cuda" and hasattr(torch.cuda, "nccl") else None),

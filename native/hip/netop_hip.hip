@@ -198,6 +198,18 @@ int grid_for(uint64_t n_vec, int per_cu = 8) {
     return int(need < cap ? (need ? need : 1) : cap);
 }
 
+// The probes walk every GPU with hipSetDevice; the caller (a torch.distributed rank) must get
+// its own current device back on every return path, or its next collective runs elsewhere.
+struct DeviceRestore {
+    int prev = -1;
+    DeviceRestore() {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    }
+    ~DeviceRestore() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
 }  // namespace
 
 extern "C" {
@@ -283,6 +295,7 @@ int netop_copy(const void* src, void* dst, uint64_t bytes, hipStream_t stream) {
 // Returns hipSuccess, or the first error.  `n_out` receives the number of GPUs probed.
 int netop_xgmi_probe(uint64_t bytes, int iters, int max_gpus, double* bw_single, double* bw_all, int* n_out,
                      unsigned long long* total_errors) {
+    DeviceRestore restore;
     int n = 0;
     hipError_t e = hipGetDeviceCount(&n);
     if (e != hipSuccess) return int(e);
@@ -408,6 +421,7 @@ int netop_xgmi_probe(uint64_t bytes, int iters, int max_gpus, double* bw_single,
 // reason.  Integrity is checked byte-exact on every destination.
 int netop_xgmi_probe_push(uint64_t bytes, int iters, int max_gpus, double* bw_push, int* n_out,
                           unsigned long long* total_errors) {
+    DeviceRestore restore;
     int n = 0;
     hipError_t e = hipGetDeviceCount(&n);
     if (e != hipSuccess) return int(e);

@@ -44,6 +44,49 @@ def test_bench_torchrun_cpu_rehearsal(n, tmp_path):
     assert j["busbw_ceiling_GBps"] == pytest.approx((n - 1) * 76.0)
 
 
+def _bench_line(r):
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout  # rank 0 only
+    return json.loads(lines[0])
+
+
+@pytest.mark.parametrize("n", [4, 8])
+def test_bench_spawns_ranks_without_launcher(n, tmp_path):
+    """The driver's per-N runs may call ``python bench.py --gpus N`` with no launcher: bench.py
+    must start N ranks itself (round 1 silently measured one)."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    cmd = [sys.executable, str(ROOT / "bench.py"), "--gpus", str(n), "--steps", "3", "--warmup", "1", "--device", "cpu",
+           "--bytes", str(1 << 18), "--sweep", "", "--collectives", "all_gather", "--node-ready", "off"]
+    j = _bench_line(subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=tmp_path,
+                                   env=dict(env, OMP_NUM_THREADS="1")))
+    assert j["n_gpus"] == n and j["config"]["gpus"] == n and j["config"]["parallelism"] == f"dp{n}"
+    assert f"{n}xMI355X" in j["config"]["model"]
+    assert j["verified"] is True and j["verify_errors"] == 0
+    assert j["value"] > 0 and j["value"] == pytest.approx(j["algbw_GBps"] * 2 * (n - 1) / n, abs=1e-3)
+    assert j["aggregate_busbw_GBps"] == pytest.approx(j["busbw_GBps"] * n)
+
+
+def test_bench_single_rank_reports_no_fake_bandwidth(tmp_path):
+    cmd = [sys.executable, str(ROOT / "bench.py"), "--gpus", "1", "--steps", "3", "--warmup", "1", "--device", "cpu",
+           "--bytes", str(1 << 18), "--sweep", "4096", "--node-ready", "off"]
+    j = _bench_line(subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=tmp_path))
+    assert j["n_gpus"] == 1 and j["value"] == 0.0
+    assert j["config"]["model"].startswith("L3 mode, 1xMI355X")
+    assert j["algbw_GBps"] is None and "no-op" in j["algbw_note"]
+    assert all(row["algbw_GBps"] is None for row in j["sweep"])
+    side = j["node_ready_gpu_side"]
+    assert set(side["phases_ms"]) >= {"discover", "xgmi", "gdr", "label"} and side["total_ms"] >= 0
+
+
+def test_bench_rejects_world_mismatch(tmp_path):
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
+               MASTER_PORT=str(_free_port()))
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "4", "--device", "cpu"], capture_output=True,
+                       text=True, timeout=120, cwd=tmp_path, env=env)
+    assert r.returncode == 2 and "WORLD_SIZE=2" in r.stderr
+
+
 def _worker(rank, world, port, q):
     import torch
     import torch.distributed as dist
