@@ -126,9 +126,13 @@ def node_ready_gpu_side(sysfs: str = "/sys/") -> dict:
     x = timed("xgmi", lambda: m.read_xgmi(sysfs))
     g = timed("gdr", lambda: m.detect_gdr(sysfs))
     with tempfile.TemporaryDirectory() as tmp:
-        if hasattr(m, "write_node_artifacts"):
-            a = timed("artifacts", lambda: m.write_node_artifacts(sysfs, tmp))
-            out["artifacts"] = {k: os.path.basename(v) for k, v in a.items()}
+        def topo_file():
+            xml = m.rccl_topo_xml(sysfs)
+            with open(os.path.join(tmp, "rccl-topo.xml"), "w") as f:
+                f.write(xml)
+            return xml
+
+        out["rccl_topo_xml_bytes"] = len(timed("rccl_topo", topo_file))
         lab = os.path.join(tmp, "scale-out-readiness.txt")
 
         def label():

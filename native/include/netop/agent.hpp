@@ -57,6 +57,12 @@ struct Config {
     bool fsync_artifacts = false;  // fsync every artifact / label / status write (see set_durable_writes)
     artifacts::Labels labels;
     std::string rccl_env;                // --rccl-env
+    std::string rccl_topo;               // --rccl-topo: NCCL_TOPO_FILE XML written here
+    std::string rccl_topo_env_path;      // --rccl-topo-env-path: path jobs see (default rccl_topo)
+    // --rccl-socket-ifname: NCCL_SOCKET_IFNAME in rccl.env.  "auto": L3 -> the configured scale-out
+    // NICs in GPU order (every node lists rail 0 first, so bootstrap meets on one /16); L2 -> not
+    // written (no IPv4).  "none" / "" -> not written.  Anything else: a literal interface list.
+    std::string socket_ifname = "auto";
     std::string status_file;             // --status-file (JSON)
     std::string nm_keyfile_dir;          // --nm-keyfile-dir
     int xgmi_expect_links = -1;          // -1 off; 0 = full mesh among discovered GPUs; N = exact pairs
@@ -167,6 +173,9 @@ class Agent {
     void remove_rail_routing();
     void write_artifacts();
     void write_l2_artifacts();
+    void write_rccl_env_file();
+    std::string write_topo();  // returns the NCCL_TOPO_FILE value for rccl.env ("" = none)
+    std::vector<std::string> socket_ifnames() const;
     void check_xgmi();
     void log_results();
     void mark(const std::string& phase);

@@ -1,11 +1,14 @@
 // Node-local artifacts written by the agent.
 //
-//   rccl-net.json   RCCL scale-out NIC contract.  Same NIC_NET_CONFIG entry schema as the
-//                   reference's gaudinet.json (cmd/discover/gaudinet.go:28-37) — NIC_MAC,
-//                   NIC_IP, SUBNET_MASK, GATEWAY_MAC first, in that order — extended with
-//                   NIC_NAME, GATEWAY_IP, GPU_BDF, RDMA_DEV and GID_INDEX.
-//   rccl.env        KEY=VALUE environment for RCCL jobs on this node (NCCL_IB_HCA in GPU
-//                   order, NCCL_IB_GID_INDEX for RoCE v2, ...).
+//   rccl-net.json   This operator's own per-node NIC contract (RCCL does not read it): the
+//                   reference's gaudinet.json entry schema (cmd/discover/gaudinet.go:28-37) —
+//                   NIC_MAC, NIC_IP, SUBNET_MASK, GATEWAY_MAC first, in that order — extended
+//                   with NIC_NAME, GATEWAY_IP, GPU_BDF, RDMA_DEV and GID_INDEX.  Consumers:
+//                   the validation tooling (parallel/rail.py, validate.py) and users' launchers.
+//   rccl.env        KEY=VALUE environment for RCCL jobs on this node — what RCCL itself
+//                   consumes: NCCL_IB_HCA in GPU order, NCCL_IB_GID_INDEX for RoCE v2,
+//                   NCCL_SOCKET_IFNAME, NCCL_TOPO_FILE.
+//   rccl-topo.xml   NCCL_TOPO_FILE (generate_rccl_topo below).
 //   *.network       systemd-networkd units (cmd/discover/systemd-networkd.go:49-74), same text.
 //   NFD label file  features.d readiness label (cmd/discover/main.go:43-45,239-246).
 #pragma once
@@ -15,6 +18,7 @@
 #include <vector>
 
 #include "netop/state.hpp"
+#include "netop/topology.hpp"
 
 namespace netop::artifacts {
 
@@ -50,10 +54,47 @@ void write_rccl_net(const std::string& path, const std::vector<NicState>& nics, 
 
 // `extra`: site settings appended verbatim (e.g. NCCL_IB_TC for the fabric's RoCE traffic class);
 // keys must look like NCCL_* / RCCL_* / HSA_*, values must be single-line (parse_env_extra).
+// `socket_ifnames`: NCCL_SOCKET_IFNAME (exact-match list, "=a,b"): the interfaces RCCL bootstraps
+// over and, without RDMA, moves data over.  Empty = not written.
 std::string generate_rccl_env(const std::vector<NicState>& nics, const std::string& topo_file,
-                              const std::vector<std::pair<std::string, std::string>>& extra = {});
+                              const std::vector<std::pair<std::string, std::string>>& extra = {},
+                              const std::vector<std::string>& socket_ifnames = {});
 void write_rccl_env(const std::string& path, const std::vector<NicState>& nics, const std::string& topo_file,
-                    const std::vector<std::pair<std::string, std::string>>& extra = {});
+                    const std::vector<std::pair<std::string, std::string>>& extra = {},
+                    const std::vector<std::string>& socket_ifnames = {});
+
+// NCCL_TOPO_FILE: the node's PCIe tree as RCCL models it (RCCL's topology-XML dialect, the
+// format NCCL_TOPO_DUMP_FILE writes): one <cpu numaid> per root-complex NUMA node, the switches
+// above each GPU and scale-out NIC folded the way RCCL folds them (topo::rccl_pci_parents), the
+// GPUs' PCI functions, and under each NIC's function a <nic><net name=...> whose name is what
+// RCCL's network plugin calls the device (the RDMA device for the IB plugin, else the netdev).
+// RCCL loads the file, then fills every attribute the file leaves out (GPU dev/rank/arch, link
+// speeds, NIC speed/GDR) from the running system and drops devices its job does not use, so the
+// file pins the PCIe affinity — which NIC is next to which GPU — without ever naming a device
+// index that differs per job.  The <cpu> nodes carry arch / vendor / familyid / modelid / affinity
+// because RCCL does not fill those for CPU nodes it reads from a file and fails init without
+// them (measured on the box: "Attribute arch of node cpu not found").  xGMI links are left out:
+// RCCL detects them itself for the GPUs of each communicator, and whether it would also keep
+// file-provided links (doubling the link count it plans rings with) cannot be checked without
+// a multi-GPU run.  Verified on an MI355X box with torch's RCCL 2.26.6 and ROCm's 2.27.7: the
+// file loads and RCCL's dump places the GPU exactly as the file does (profiles/r2_rccl_topo_box.md).
+constexpr int kRcclTopoXmlVersion = 2;  // <system version="2">: RCCL 2.26 / 2.27 (ROCm 7)
+struct TopoNic {
+    topo::PciDev pci;
+    std::string net_name;  // RCCL network device name
+    int port = 0;          // RDMA port (0 = not written)
+};
+// `cpu` goes on every <cpu> node (RCCL requires arch / vendor / familyid / modelid there), with
+// the NUMA node's cpumap from `sysfs_root` as its affinity.
+std::string generate_rccl_topo(const std::vector<topo::Gpu>& gpus, const std::vector<TopoNic>& nics,
+                               const topo::CpuIdentity& cpu, const std::string& sysfs_root,
+                               int version = kRcclTopoXmlVersion);
+void write_rccl_topo(const std::string& path, const std::vector<topo::Gpu>& gpus, const std::vector<TopoNic>& nics,
+                     const topo::CpuIdentity& cpu, const std::string& sysfs_root, int version = kRcclTopoXmlVersion);
+// The NICs of `names` as RCCL sees them: PCI function from the discovery result (or sysfs for an
+// extra --interfaces NIC), net name = RDMA device when the NIC has one, else the netdev name.
+std::vector<TopoNic> topo_nics(const topo::DiscoveryResult& d, const std::vector<std::string>& names,
+                               const std::string& sysfs_root);
 // "K=V,K2=V2" -> pairs; throws std::invalid_argument on a bad key or value.
 std::vector<std::pair<std::string, std::string>> parse_env_extra(const std::string& spec);
 

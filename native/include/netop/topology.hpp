@@ -28,6 +28,7 @@ struct PciDev {
     std::vector<std::string> chain;  // path components from the host bridge ("pci0000:00") down to bdf
     std::string driver;
     uint32_t vendor = 0, device = 0, pci_class = 0;
+    uint32_t subsystem_vendor = 0, subsystem_device = 0;
     int numa = -1;
 };
 
@@ -70,6 +71,29 @@ struct DiscoveryOptions {
 };
 
 std::optional<PciDev> read_pci_dev(const std::string& root, const std::string& device_path);
+// The PCI device behind a netdev (<root>/class/net/<ifname>/device); nullopt for virtual links.
+std::optional<PciDev> netdev_pci(const std::string& root, const std::string& ifname);
+// The ancestors RCCL puts above `d` in its topology tree, outermost first.  RCCL (NCCL's
+// ncclTopoGetXmlFromSys) climbs the sysfs path two components at a time — a switch's downstream
+// port and the switch above it count as one bridge — and stops at the root complex, whose
+// "pciDDDD:BB" component is not a BDF; the CPU node there is the outermost ancestor's NUMA node.
+// Mirroring that walk keeps a topology file the agent writes identical to RCCL's own view.
+std::vector<PciDev> rccl_pci_parents(const PciDev& d);
+
+// The CPU identity RCCL records on each <cpu> node of its topology (NCCL's ncclTopoGetXmlFromCpu):
+// uname machine, and on x86_64 the CPUID vendor string and family / model ids computed the way
+// NCCL does (family + extended family << 4, model + extended model << 4 — e.g. 191 / 2 on the
+// MI355X boxes' Zen 5 CPUs, not /proc/cpuinfo's 26).  RCCL refuses a topology file whose <cpu>
+// lacks them ("Attribute arch of node cpu not found"): it fills CPU attributes only for CPU
+// nodes it creates itself.
+struct CpuIdentity {
+    std::string arch;    // "x86_64"
+    std::string vendor;  // "AuthenticAMD"
+    int family = -1, model = -1;
+};
+CpuIdentity cpu_identity();  // of the machine running this code
+// <root>/devices/system/node/node<N>/cpumap ("ffffffff,..."); "" if unknown.
+std::string numa_cpumap(const std::string& root, int numa);
 std::vector<Gpu> discover_gpus(const std::string& root, const std::string& driver = "amdgpu");
 std::vector<Nic> discover_pci_nics(const std::string& root, const std::vector<std::string>& drivers);
 PathType path_between(const PciDev& a, const PciDev& b, int* common_depth = nullptr);

@@ -216,6 +216,37 @@ PYBIND11_MODULE(_netop_native, m) {
         d["ifnames"] = r.ifnames;
         return d;
     }, py::arg("root"), py::arg("mode") = "affine", py::arg("drivers") = py::none(), py::arg("accel_driver") = "amdgpu");
+    m.def("rccl_topo_xml", [](const std::string& root, const std::string& mode, py::object interfaces, int version,
+                              py::object cpu) {
+        topo::DiscoveryOptions o;
+        auto md = topo::parse_discovery_mode(mode);
+        if (!md) throw py::value_error("bad mode");
+        o.mode = *md;
+        auto d = topo::discover(o, root);
+        std::vector<std::string> names = d.ifnames;
+        if (!interfaces.is_none())
+            for (auto& i : interfaces.cast<std::vector<std::string>>())
+                if (std::find(names.begin(), names.end(), i) == names.end()) names.push_back(i);
+        topo::CpuIdentity id = topo::cpu_identity();
+        if (!cpu.is_none()) {  // tests: a fixed identity instead of this machine's CPUID
+            auto c = cpu.cast<py::dict>();
+            id.arch = c["arch"].cast<std::string>();
+            id.vendor = c["vendor"].cast<std::string>();
+            id.family = c["family"].cast<int>();
+            id.model = c["model"].cast<int>();
+        }
+        return artifacts::generate_rccl_topo(d.gpus, artifacts::topo_nics(d, names, root), id, root, version);
+    }, py::arg("root"), py::arg("mode") = "affine", py::arg("interfaces") = py::none(),
+       py::arg("version") = artifacts::kRcclTopoXmlVersion, py::arg("cpu") = py::none());
+    m.def("cpu_identity", [] {
+        auto c = topo::cpu_identity();
+        py::dict d;
+        d["arch"] = c.arch;
+        d["vendor"] = c.vendor;
+        d["family"] = c.family;
+        d["model"] = c.model;
+        return d;
+    });
     m.def("read_xgmi", [](const std::string& root) {
         auto x = topo::read_xgmi(root);
         py::dict d;

@@ -618,8 +618,51 @@ void Agent::write_l2_artifacts() {
         if (!missing || mono_ns() >= deadline) break;
         ::usleep(2000);
     }
+    write_rccl_env_file();
+}
+
+std::string Agent::write_topo() {
+    if (cfg_.rccl_topo.empty()) return "";
+    std::string root = cfg_.sysfs_root.empty() ? topo::sysfs_root() : cfg_.sysfs_root;
+    std::vector<std::string> names;
+    for (const auto& n : nics_) names.push_back(n.ifname);
     try {
-        artifacts::write_rccl_env(cfg_.rccl_env, nics_, "", rccl_env_extra_);
+        artifacts::write_rccl_topo(cfg_.rccl_topo, disc_.gpus, artifacts::topo_nics(disc_, names, root),
+                                   topo::cpu_identity(), root);
+    } catch (const std::exception& e) {
+        NLOG_E("Error writing RCCL topology file: %s", e.what());  // rccl.env then names no topology
+        return "";
+    }
+    return cfg_.rccl_topo_env_path.empty() ? cfg_.rccl_topo : cfg_.rccl_topo_env_path;
+}
+
+std::vector<std::string> Agent::socket_ifnames() const {
+    const std::string& s = cfg_.socket_ifname;
+    if (s.empty() || s == "none") return {};
+    if (s != "auto") {
+        std::vector<std::string> out;
+        for (auto& i : split(s, ','))
+            if (!trim(i).empty()) out.push_back(trim(i));
+        return out;
+    }
+    if (cfg_.mode != "L3") return {};
+    std::vector<const NicState*> v;
+    for (const auto& n : nics_)
+        if (n.configured && n.addr) v.push_back(&n);
+    std::stable_sort(v.begin(), v.end(), [](const NicState* a, const NicState* b) {
+        int ga = a->gpu_index < 0 ? 1 << 30 : a->gpu_index, gb = b->gpu_index < 0 ? 1 << 30 : b->gpu_index;
+        return ga != gb ? ga < gb : a->ifname < b->ifname;
+    });
+    std::vector<std::string> out;
+    for (const NicState* n : v) out.push_back(n->ifname);
+    return out;
+}
+
+void Agent::write_rccl_env_file() {
+    const std::string topo_env = write_topo();
+    if (cfg_.rccl_env.empty()) return;
+    try {
+        artifacts::write_rccl_env(cfg_.rccl_env, nics_, topo_env, rccl_env_extra_, socket_ifnames());
     } catch (const std::exception& e) {
         NLOG_E("Error writing RCCL env: %s", e.what());
     }
@@ -651,13 +694,7 @@ void Agent::write_artifacts() {
             NLOG_E("Error: %s", e.what());  // not fatal (main.go:220-224)
         }
     }
-    if (!cfg_.rccl_env.empty()) {
-        try {
-            artifacts::write_rccl_env(cfg_.rccl_env, nics_, "", rccl_env_extra_);
-        } catch (const std::exception& e) {
-            NLOG_E("Error writing RCCL env: %s", e.what());
-        }
-    }
+    write_rccl_env_file();
     if (!cfg_.networkd.empty()) {
         try {
             artifacts::write_networkd(cfg_.networkd, nics_);
@@ -880,7 +917,7 @@ void Agent::run(int stop_fd) {
         }
         write_artifacts();
         mark("artifacts");
-    } else if (cfg_.configure && !cfg_.rccl_env.empty()) {
+    } else if (cfg_.configure && (!cfg_.rccl_env.empty() || !cfg_.rccl_topo.empty())) {
         // L2 (MI355X addition): RCCL still has to know which HCAs are the scale-out ones and which
         // GID to use; without IPv4 that is the RoCE v2 GID of the IPv6 link-local address.
         write_l2_artifacts();

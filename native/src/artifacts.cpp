@@ -4,6 +4,8 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
+#include <memory>
 #include <set>
 
 #include "netop/log.hpp"
@@ -180,7 +182,8 @@ std::vector<std::pair<std::string, std::string>> parse_env_extra(const std::stri
 }
 
 std::string generate_rccl_env(const std::vector<NicState>& nics, const std::string& topo_file,
-                              const std::vector<std::pair<std::string, std::string>>& extra) {
+                              const std::vector<std::pair<std::string, std::string>>& extra,
+                              const std::vector<std::string>& socket_ifnames) {
     std::vector<std::string> hcas;
     std::set<int> gids;
     for (const NicState* n : sorted(nics)) {
@@ -193,14 +196,144 @@ std::string generate_rccl_env(const std::vector<NicState>& nics, const std::stri
     if (!hcas.empty()) out += "NCCL_IB_HCA==" + join(hcas, ",") + "\n";
     if (gids.size() == 1) out += "NCCL_IB_GID_INDEX=" + std::to_string(*gids.begin()) + "\n";
     if (!hcas.empty()) out += "NCCL_IB_DISABLE=0\n";
+    if (!socket_ifnames.empty()) out += "NCCL_SOCKET_IFNAME==" + join(socket_ifnames, ",") + "\n";
     if (!topo_file.empty()) out += "NCCL_TOPO_FILE=" + topo_file + "\n";
     for (auto& [k, v] : extra) out += k + "=" + v + "\n";
     return out;
 }
 
 void write_rccl_env(const std::string& path, const std::vector<NicState>& nics, const std::string& topo_file,
-                    const std::vector<std::pair<std::string, std::string>>& extra) {
-    write_file_atomic(path, generate_rccl_env(nics, topo_file, extra), 0644);
+                    const std::vector<std::pair<std::string, std::string>>& extra,
+                    const std::vector<std::string>& socket_ifnames) {
+    write_file_atomic(path, generate_rccl_env(nics, topo_file, extra, socket_ifnames), 0644);
+}
+
+// ---------------------------------------------------------------------------
+// NCCL_TOPO_FILE
+// ---------------------------------------------------------------------------
+namespace {
+struct XmlPci {
+    topo::PciDev dev;
+    std::vector<std::unique_ptr<XmlPci>> kids;
+    std::vector<const TopoNic*> nets;
+};
+
+XmlPci& child(std::vector<std::unique_ptr<XmlPci>>& level, const topo::PciDev& d) {
+    for (auto& k : level)
+        if (k->dev.bdf == d.bdf) return *k;
+    level.push_back(std::make_unique<XmlPci>());
+    level.back()->dev = d;
+    return *level.back();
+}
+
+std::string xml_attr(const std::string& s) {
+    std::string o;
+    for (char c : s) {
+        switch (c) {
+            case '"': o += "&quot;"; break;
+            case '&': o += "&amp;"; break;
+            case '<': o += "&lt;"; break;
+            case '>': o += "&gt;"; break;
+            default: o += c;
+        }
+    }
+    return o;
+}
+
+void emit_pci(std::string& out, XmlPci& n, int depth) {
+    std::sort(n.kids.begin(), n.kids.end(), [](const auto& a, const auto& b) { return a->dev.bdf < b->dev.bdf; });
+    const std::string ind(size_t(depth) * 2, ' ');
+    const auto& d = n.dev;
+    out += ind + "<pci busid=\"" + xml_attr(d.bdf) + "\"";
+    if (d.pci_class) out += strfmt(" class=\"0x%06x\"", d.pci_class);
+    if (d.vendor) out += strfmt(" vendor=\"0x%04x\"", d.vendor);
+    if (d.device) out += strfmt(" device=\"0x%04x\"", d.device);
+    if (d.subsystem_vendor) out += strfmt(" subsystem_vendor=\"0x%04x\"", d.subsystem_vendor);
+    if (d.subsystem_device) out += strfmt(" subsystem_device=\"0x%04x\"", d.subsystem_device);
+    if (n.kids.empty() && n.nets.empty()) {
+        out += "/>\n";
+        return;
+    }
+    out += ">\n";
+    for (auto& k : n.kids) emit_pci(out, *k, depth + 1);
+    if (!n.nets.empty()) {
+        out += ind + "  <nic>\n";
+        for (const TopoNic* t : n.nets) {
+            out += ind + "    <net name=\"" + xml_attr(t->net_name) + "\"";
+            if (t->port > 0) out += strfmt(" port=\"%d\"", t->port);
+            out += "/>\n";
+        }
+        out += ind + "  </nic>\n";
+    }
+    out += ind + "</pci>\n";
+}
+}  // namespace
+
+std::string generate_rccl_topo(const std::vector<topo::Gpu>& gpus, const std::vector<TopoNic>& nics,
+                               const topo::CpuIdentity& cpu, const std::string& sysfs_root, int version) {
+    std::map<int, std::vector<std::unique_ptr<XmlPci>>> cpus;  // numaid -> top-level PCI nodes
+    auto place = [&](const topo::PciDev& leaf) -> XmlPci& {
+        auto parents = topo::rccl_pci_parents(leaf);
+        auto* level = &cpus[parents.empty() ? leaf.numa : parents.front().numa];
+        for (const auto& p : parents) level = &child(*level, p).kids;
+        return child(*level, leaf);
+    };
+    for (const auto& g : gpus) place(g.pci);
+    for (const auto& n : nics) {
+        if (n.net_name.empty() || n.pci.bdf.empty()) continue;
+        place(n.pci).nets.push_back(&n);
+    }
+    std::string out = strfmt("<system version=\"%d\">\n", version);
+    for (auto& [numa, tops] : cpus) {
+        out += strfmt("  <cpu numaid=\"%d\"", numa);
+        const std::string aff = topo::numa_cpumap(sysfs_root, numa);
+        if (!aff.empty()) out += " affinity=\"" + xml_attr(aff) + "\"";
+        if (!cpu.arch.empty()) out += " arch=\"" + xml_attr(cpu.arch) + "\"";
+        if (!cpu.vendor.empty()) out += " vendor=\"" + xml_attr(cpu.vendor) + "\"";
+        if (cpu.family >= 0) out += strfmt(" familyid=\"%d\"", cpu.family);
+        if (cpu.model >= 0) out += strfmt(" modelid=\"%d\"", cpu.model);
+        out += ">\n";
+        std::sort(tops.begin(), tops.end(), [](const auto& a, const auto& b) { return a->dev.bdf < b->dev.bdf; });
+        for (auto& t : tops) emit_pci(out, *t, 2);
+        out += "  </cpu>\n";
+    }
+    out += "</system>\n";
+    return out;
+}
+
+void write_rccl_topo(const std::string& path, const std::vector<topo::Gpu>& gpus, const std::vector<TopoNic>& nics,
+                     const topo::CpuIdentity& cpu, const std::string& sysfs_root, int version) {
+    write_file_atomic(path, generate_rccl_topo(gpus, nics, cpu, sysfs_root, version), 0644);
+}
+
+std::vector<TopoNic> topo_nics(const topo::DiscoveryResult& d, const std::vector<std::string>& names,
+                               const std::string& sysfs_root) {
+    std::vector<TopoNic> out;
+    for (const auto& name : names) {
+        TopoNic t;
+        bool found = false;
+        for (const auto& n : d.nics) {
+            if (n.ifname != name) continue;
+            t.pci = n.pci;
+            t.net_name = n.rdma_dev.empty() ? n.ifname : n.rdma_dev;
+            t.port = n.rdma_dev.empty() ? 0 : n.rdma_port;
+            found = true;
+            break;
+        }
+        if (!found) {
+            auto p = topo::netdev_pci(sysfs_root, name);
+            if (!p) continue;  // virtual link: nothing PCIe to pin
+            t.pci = *p;
+            auto ib = list_dir(path_join(p->path, "infiniband"));
+            t.net_name = ib.empty() ? name : ib.front();
+            if (!ib.empty()) {
+                auto port = read_file(path_join(sysfs_root, "class/net/" + name + "/dev_port"));
+                t.port = (port ? std::atoi(trim(*port).c_str()) : 0) + 1;
+            }
+        }
+        out.push_back(std::move(t));
+    }
+    return out;
 }
 
 // ---------------------------------------------------------------------------

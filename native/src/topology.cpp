@@ -1,9 +1,13 @@
 #include "netop/topology.hpp"
 
 #include <sys/utsname.h>
+#if defined(__x86_64__)
+#include <cpuid.h>
+#endif
 
 #include <algorithm>
 #include <cstdlib>
+#include <cstring>
 #include <set>
 
 #include "netop/log.hpp"
@@ -79,9 +83,65 @@ std::optional<PciDev> read_pci_dev(const std::string& root, const std::string& d
     d.vendor = read_hex(path_join(*real, "vendor"));
     d.device = read_hex(path_join(*real, "device"));
     d.pci_class = read_hex(path_join(*real, "class"));
+    d.subsystem_vendor = read_hex(path_join(*real, "subsystem_vendor"));
+    d.subsystem_device = read_hex(path_join(*real, "subsystem_device"));
     d.numa = read_int(path_join(*real, "numa_node"), -1);
     (void)root;
     return d;
+}
+
+CpuIdentity cpu_identity() {
+    CpuIdentity c;
+    utsname u{};
+    if (::uname(&u) == 0) c.arch = u.machine;
+#if defined(__x86_64__)
+    unsigned a = 0, b = 0, cx = 0, d = 0;
+    if (__get_cpuid(0, &a, &b, &cx, &d)) {
+        char v[13] = {};
+        std::memcpy(v, &b, 4);
+        std::memcpy(v + 4, &d, 4);
+        std::memcpy(v + 8, &cx, 4);
+        c.vendor = v;
+    }
+    if (__get_cpuid(1, &a, &b, &cx, &d)) {
+        unsigned model = (a >> 4) & 0xf, family = (a >> 8) & 0xf, ext_model = (a >> 16) & 0xf, ext_family = (a >> 20) & 0xff;
+        c.family = int(family + (ext_family << 4));
+        c.model = int(model + (ext_model << 4));
+    }
+#endif
+    return c;
+}
+
+std::string numa_cpumap(const std::string& root, int numa) {
+    if (numa < 0) return "";
+    auto s = read_file(path_join(root, "devices/system/node/node" + std::to_string(numa) + "/cpumap"));
+    return s ? trim(*s) : "";
+}
+
+std::optional<PciDev> netdev_pci(const std::string& root, const std::string& ifname) {
+    if (ifname.empty() || ifname.find('/') != std::string::npos) return std::nullopt;
+    return read_pci_dev(root, path_join(root, "class/net/" + ifname + "/device"));
+}
+
+std::vector<PciDev> rccl_pci_parents(const PciDev& d) {
+    std::vector<PciDev> out;
+    auto pos = d.path.find("/devices/");
+    if (pos == std::string::npos || d.chain.empty()) return out;
+    const std::string prefix = d.path.substr(0, pos + 8);  // ".../devices"
+    auto dir_of = [&](size_t k) {
+        std::string p = prefix;
+        for (size_t i = 0; i <= k; ++i) p += "/" + d.chain[i];
+        return p;
+    };
+    size_t i = d.chain.size() - 1;
+    while (i >= 2 && looks_like_bdf(d.chain[i - 1]) && looks_like_bdf(d.chain[i - 2])) {
+        i -= 2;
+        auto p = read_pci_dev("", dir_of(i));
+        if (!p) break;  // unreadable bridge: RCCL would stop there too (no sysfs entry)
+        out.push_back(std::move(*p));
+    }
+    std::reverse(out.begin(), out.end());
+    return out;
 }
 
 std::vector<Gpu> discover_gpus(const std::string& root, const std::string& driver) {

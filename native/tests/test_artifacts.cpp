@@ -141,3 +141,62 @@ TEST(rccl_env_extra_settings) {
     CHECK_THROWS(parse_env_extra("NCCL_IB_TC"));
     CHECK(parse_env_extra("").empty());
 }
+
+TEST(rccl_topo_xml_tree) {
+    TmpDir t;
+    auto dev = [&](const std::string& path, const char* cls, const char* vendor, const char* device, int numa) {
+        t.mkdir("devices/" + path);
+        t.write("devices/" + path + "/class", std::string(cls) + "\n");
+        t.write("devices/" + path + "/vendor", std::string(vendor) + "\n");
+        t.write("devices/" + path + "/device", std::string(device) + "\n");
+        t.write("devices/" + path + "/subsystem_vendor", std::string(vendor) + "\n");
+        t.write("devices/" + path + "/subsystem_device", std::string(device) + "\n");
+        t.write("devices/" + path + "/numa_node", std::to_string(numa) + "\n");
+    };
+    const std::string rp = "pci0000:e7/0000:e7:01.1/0000:e8:00.0";
+    dev(rp, "0x060400", "0x1000", "0xc030", 1);
+    dev(rp + "/0000:e9:08.0/0000:f0:00.0", "0x060400", "0x1000", "0xc030", 1);
+    dev(rp + "/0000:e9:08.0/0000:f0:00.0/0000:f1:10.0/0000:f2:00.0", "0x060400", "0x1022", "0x1500", 1);
+    const std::string g = rp + "/0000:e9:08.0/0000:f0:00.0/0000:f1:10.0/0000:f2:00.0/0000:f3:00.0/0000:f4:00.0";
+    dev(g, "0x120000", "0x1002", "0x75a3", 1);
+    dev(rp + "/0000:e9:00.0/0000:ea:00.0", "0x060400", "0x1000", "0xc030", 1);
+    dev(rp + "/0000:e9:00.0/0000:ea:00.0/0000:eb:10.0/0000:ec:00.0", "0x060400", "0x1000", "0xc030", 1);
+    const std::string n = rp + "/0000:e9:00.0/0000:ea:00.0/0000:eb:10.0/0000:ec:00.0/0000:ed:01.0/0000:ef:00.0";
+    dev(n, "0x020000", "0x15b3", "0x1021", 1);
+    topo::Gpu gpu;
+    gpu.pci = *topo::read_pci_dev(t.path, t.path + "/devices/" + g);
+    TopoNic tn;
+    tn.pci = *topo::read_pci_dev(t.path, t.path + "/devices/" + n);
+    tn.net_name = "mlx5_7";
+    tn.port = 1;
+    t.write("devices/system/node/node1/cpumap", "ffffffff,00000000\n");
+    topo::CpuIdentity cpu{"x86_64", "AuthenticAMD", 191, 2};
+    std::string x = generate_rccl_topo({gpu}, {tn}, cpu, t.path);
+    const std::string want =
+        "<system version=\"2\">\n"
+        "  <cpu numaid=\"1\" affinity=\"ffffffff,00000000\" arch=\"x86_64\" vendor=\"AuthenticAMD\" familyid=\"191\" modelid=\"2\">\n"
+        "    <pci busid=\"0000:e8:00.0\" class=\"0x060400\" vendor=\"0x1000\" device=\"0xc030\" subsystem_vendor=\"0x1000\" subsystem_device=\"0xc030\">\n"
+        "      <pci busid=\"0000:ea:00.0\" class=\"0x060400\" vendor=\"0x1000\" device=\"0xc030\" subsystem_vendor=\"0x1000\" subsystem_device=\"0xc030\">\n"
+        "        <pci busid=\"0000:ec:00.0\" class=\"0x060400\" vendor=\"0x1000\" device=\"0xc030\" subsystem_vendor=\"0x1000\" subsystem_device=\"0xc030\">\n"
+        "          <pci busid=\"0000:ef:00.0\" class=\"0x020000\" vendor=\"0x15b3\" device=\"0x1021\" subsystem_vendor=\"0x15b3\" subsystem_device=\"0x1021\">\n"
+        "            <nic>\n"
+        "              <net name=\"mlx5_7\" port=\"1\"/>\n"
+        "            </nic>\n"
+        "          </pci>\n"
+        "        </pci>\n"
+        "      </pci>\n"
+        "      <pci busid=\"0000:f0:00.0\" class=\"0x060400\" vendor=\"0x1000\" device=\"0xc030\" subsystem_vendor=\"0x1000\" subsystem_device=\"0xc030\">\n"
+        "        <pci busid=\"0000:f2:00.0\" class=\"0x060400\" vendor=\"0x1022\" device=\"0x1500\" subsystem_vendor=\"0x1022\" subsystem_device=\"0x1500\">\n"
+        "          <pci busid=\"0000:f4:00.0\" class=\"0x120000\" vendor=\"0x1002\" device=\"0x75a3\" subsystem_vendor=\"0x1002\" subsystem_device=\"0x75a3\"/>\n"
+        "        </pci>\n"
+        "      </pci>\n"
+        "    </pci>\n"
+        "  </cpu>\n"
+        "</system>\n";
+    CHECK_EQ(x, want);
+    // rccl.env points RCCL at it and pins the socket interfaces.
+    auto a = nic("enp239s0np0", "02:00:00:00:00:01", "x 10.0.0.2/30", "02:00:00:00:01:01", 7);
+    auto env = generate_rccl_env({a}, "/etc/amd/scale-out/rccl-topo.xml", {}, {"enp239s0np0", "enp8s0np0"});
+    CHECK(env.find("NCCL_TOPO_FILE=/etc/amd/scale-out/rccl-topo.xml\n") != std::string::npos);
+    CHECK(env.find("NCCL_SOCKET_IFNAME==enp239s0np0,enp8s0np0\n") != std::string::npos);
+}

@@ -184,3 +184,33 @@ TEST(topology_rdma_mode_lists_host_rdma_nics) {
     CHECK(r.pairs.empty() && r.gpus.empty());
     CHECK(parse_discovery_mode("rdma") == DiscoveryMode::Rdma);
 }
+
+TEST(topology_rccl_parents_fold_like_rccl) {
+    // Layout of GPU 0000:f4:00.0 on a live MI355X box, whose RCCL topology dump
+    // (NCCL_TOPO_DUMP_FILE) nests it cpu(numa 1) > e8:00.0 > f0:00.0 > f2:00.0 > f4:00.0.
+    TmpDir t;
+    const std::string g = "pci0000:e7/0000:e7:01.1/0000:e8:00.0/0000:e9:08.0/0000:f0:00.0/0000:f1:10.0/0000:f2:00.0/0000:f3:00.0/0000:f4:00.0";
+    const std::string n = "pci0000:e7/0000:e7:01.1/0000:e8:00.0/0000:e9:00.0/0000:ea:00.0/0000:eb:10.0/0000:ec:00.0/0000:ed:01.0/0000:ef:00.0";
+    const std::string m = "pci0000:37/0000:37:01.1/0000:38:00.0";  // NIC straight on a root port
+    pci(t, g, "amdgpu", "0x1002", "0x75a3", 1);
+    pci(t, n, "ionic", "0x1dd8", "0x1002", 1);
+    pci(t, m, "mlx5_core", "0x15b3", "0x1021", 0);
+    for (const char* b : {"0000:e8:00.0", "0000:e8:00.0/0000:e9:08.0/0000:f0:00.0"})
+        t.write("devices/pci0000:e7/0000:e7:01.1/" + std::string(b) + "/class", "0x060400\n");
+    auto gd = read_pci_dev(t.path, t.path + "/devices/" + g);
+    CHECK(gd.has_value());
+    auto p = rccl_pci_parents(*gd);
+    CHECK_EQ(p.size(), size_t(3));
+    CHECK_EQ(p[0].bdf, std::string("0000:e8:00.0"));
+    CHECK_EQ(p[0].pci_class, uint32_t(0x060400));
+    CHECK_EQ(p[1].bdf, std::string("0000:f0:00.0"));
+    CHECK_EQ(p[2].bdf, std::string("0000:f2:00.0"));
+    auto nd = read_pci_dev(t.path, t.path + "/devices/" + n);
+    auto q = rccl_pci_parents(*nd);
+    CHECK_EQ(q.size(), size_t(3));
+    CHECK_EQ(q[0].bdf, std::string("0000:e8:00.0"));  // shared with the GPU: RCCL's PXB
+    CHECK_EQ(q[1].bdf, std::string("0000:ea:00.0"));
+    CHECK_EQ(q[2].bdf, std::string("0000:ec:00.0"));
+    auto md = read_pci_dev(t.path, t.path + "/devices/" + m);
+    CHECK(rccl_pci_parents(*md).empty());  // its parent is the CPU
+}

@@ -59,6 +59,9 @@ int main(int argc, char** argv) {
     fs.add_string("nfd-label-file", &cfg.labels.file, "readiness label file name inside the features directory");
     fs.add_string("nfd-label", &cfg.labels.key, "readiness label key (published as KEY=true; KEY.mode, KEY.nics, ... alongside)");
     fs.add_string("rccl-env", &cfg.rccl_env, "write an RCCL environment file (NCCL_IB_HCA, NCCL_IB_GID_INDEX, ...)");
+    fs.add_string("rccl-topo", &cfg.rccl_topo, "write an RCCL topology file (NCCL_TOPO_FILE XML: the PCIe tree of the GPUs and scale-out NICs)");
+    fs.add_string("rccl-topo-env-path", &cfg.rccl_topo_env_path, "NCCL_TOPO_FILE value written into the RCCL environment file (the path jobs mount; default --rccl-topo)");
+    fs.add_string("rccl-socket-ifname", &cfg.socket_ifname, "NCCL_SOCKET_IFNAME in the RCCL environment file: auto (L3: the configured scale-out NICs, GPU order), none, or a list");
     fs.add_int("rail-table-base", &cfg.rail_table_base,
                "L3: per-rail source routing; NIC k (its GPU index) gets routing table and rule priority base+k (0 = off)");
     fs.add_string("rccl-env-extra", &cfg.rccl_env_extra, "site settings appended to the RCCL environment file: KEY=VALUE[,...] (NCCL_*, RCCL_*, HSA_*)");

@@ -42,6 +42,7 @@ ARTIFACT_DIR_HOST = "/etc/amd/scale-out"
 ARTIFACT_DIR_CONTAINER = "/host" + ARTIFACT_DIR_HOST
 RCCL_NET_FILE = "rccl-net.json"
 RCCL_ENV_FILE = "rccl.env"
+RCCL_TOPO_FILE = "rccl-topo.xml"
 L3_WAIT = "90s"
 
 STATE_NO_TARGETS = "No targets"
@@ -139,6 +140,10 @@ def agent_args(p: T.NetworkClusterPolicy) -> List[str]:
         # MI355X: RCCL needs the HCA list and the link-local RoCE v2 GID in L2 as well (Gaudi's
         # firmware did not, so the reference passes nothing in L2).
         args.append(f"--rccl-env={ARTIFACT_DIR_CONTAINER}/{RCCL_ENV_FILE}")
+    # NCCL_TOPO_FILE: written through the agent's mount, named in rccl.env by the host path jobs
+    # mount (the reference's HCCL contract is gaudinet.json, controller.go:198-200).
+    args += [f"--rccl-topo={ARTIFACT_DIR_CONTAINER}/{RCCL_TOPO_FILE}",
+             f"--rccl-topo-env-path={ARTIFACT_DIR_HOST}/{RCCL_TOPO_FILE}"]
     # MI355X options
     if so.xgmiCheck:
         args.append("--xgmi-expect=0")

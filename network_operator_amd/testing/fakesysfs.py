@@ -38,6 +38,20 @@ def _pci(root: Path, pcipath: str, driver: str, vendor: str, device: str, numa: 
     _w(d / "device", device + "\n")
     _w(d / "numa_node", f"{numa}\n")
     _w(d / "class", cls + "\n")
+    _w(d / "subsystem_vendor", vendor + "\n")
+    _w(d / "subsystem_device", device + "\n")
+    # Bridges above the function (root port, switch up/downstream ports): the attributes RCCL's
+    # topology reads from each of them (Broadcom PEX switch ports, like the live node).
+    parts = pcipath.split("/")
+    for k in range(1, len(parts) - 1):
+        b = root / "devices" / "/".join(parts[: k + 1])
+        if not (b / "class").exists():
+            _w(b / "class", "0x060400\n")
+            _w(b / "vendor", "0x1000\n")
+            _w(b / "device", "0xc030\n")
+            _w(b / "subsystem_vendor", "0x1000\n")
+            _w(b / "subsystem_device", "0x0072\n")
+            _w(b / "numa_node", f"{numa}\n")
     drv = root / "bus" / "pci" / "drivers" / driver
     drv.mkdir(parents=True, exist_ok=True)
     _link(drv, d / "driver")
@@ -72,6 +86,11 @@ def build_mi355x_node(root: Path, nic_names: Optional[Dict[str, str]] = None, ni
         d = root / "devices" / r["pcipath"] / "infiniband" / r["dev"]
         d.mkdir(parents=True, exist_ok=True)
         _link(d, root / "class" / "infiniband" / r["dev"])
+    # Two NUMA nodes of 128 CPUs each, interleaved like the live box's cpumaps.
+    _w(root / "devices" / "system" / "node" / "node0" / "cpumap",
+       "00000000,00000000,ffffffff,ffffffff,00000000,00000000,ffffffff,ffffffff\n")
+    _w(root / "devices" / "system" / "node" / "node1" / "cpumap",
+       "ffffffff,ffffffff,00000000,00000000,ffffffff,ffffffff,00000000,00000000\n")
     _w(root / "devices" / "virtual" / "net" / "lo" / "address", "00:00:00:00:00:00\n")
     _link(root / "devices" / "virtual" / "net" / "lo", root / "class" / "net" / "lo")
 
@@ -118,6 +137,11 @@ def add_rocev2_gids(root: Path, rdma_dev: str, ips, port: int = 1) -> None:
             _w(p / "gids" / str(idx), gid + "\n")
             _w(p / "gid_attrs" / "types" / str(idx), t + "\n")
             idx += 1
+
+
+# CPU identity of the live MI355X boxes as RCCL records it (its topology dump: Zen 5,
+# familyid 191 / modelid 2) -- fixed so golden files do not depend on the build machine's CPU.
+MI355X_HOST_CPU = {"arch": "x86_64", "vendor": "AuthenticAMD", "family": 191, "model": 2}
 
 
 def real_nic_order() -> list:

@@ -264,7 +264,7 @@ def run_scenario(n_nics: int = 8, mode: str = "L3", seed: int | None = None, int
         label = feat / "scale-out-readiness.txt"
         args = [str(native_bin("discover")), "--configure=true", "--keep-running", f"--mode={mode}", f"--mtu={mtu}",
                 f"--wait={wait}", f"--rccl-net={tmp / 'rccl-net.json'}", f"--rccl-env={tmp / 'rccl.env'}",
-                f"--status-file={tmp / 'status.json'}", f"--nfd-features-dir={feat}", f"--xgmi-expect={xgmi_expect}",
+                f"--rccl-topo={tmp / 'rccl-topo.xml'}", f"--status-file={tmp / 'status.json'}", f"--nfd-features-dir={feat}", f"--xgmi-expect={xgmi_expect}",
                 f"--pipeline={'true' if pipeline else 'false'}", f"--lldp-announce={'true' if announce else 'false'}",
                 f"--systemd-networkd={tmp / 'networkd'}", f"-v={verbose}", *(extra_args or [])]
         env = dict(os.environ, SYSFS_ROOT=str(tmp / "sys"), NODE_NAME="mi355x-node-0")
@@ -311,6 +311,7 @@ def run_scenario(n_nics: int = 8, mode: str = "L3", seed: int | None = None, int
             fp = tmp / f
             res[f.split(".")[0].replace("-", "_")] = json.loads(fp.read_text()) if fp.exists() else None
         res["rccl_env"] = (tmp / "rccl.env").read_text() if (tmp / "rccl.env").exists() else None
+        res["rccl_topo"] = (tmp / "rccl-topo.xml").read_text() if (tmp / "rccl-topo.xml").exists() else None
         res["label"] = label.read_text() if label.exists() else None
         res["networkd_files"] = sorted(os.listdir(tmp / "networkd")) if (tmp / "networkd").exists() else []
         if crash_restart and t_ready:

@@ -45,6 +45,15 @@ def test_l3_fast_start_switch_full_node():
     assert r["label"].startswith("amd.feature.node.kubernetes.io/gpu-scale-out=true\n")
     assert "gpu-xgmi.pairs=28" in r["label"]
     assert "NCCL_IB_GID_INDEX=3" in r["rccl_env"]
+    # RCCL-consumed topology: the file exists, rccl.env names it, and bootstrap goes over the
+    # rails in GPU order (rail 0 first on every node).
+    topo_line = [l for l in r["rccl_env"].splitlines() if l.startswith("NCCL_TOPO_FILE=")]
+    assert len(topo_line) == 1 and topo_line[0].endswith("/rccl-topo.xml")
+    assert "NCCL_SOCKET_IFNAME==" + ",".join(r["nics"]) + "\n" in r["rccl_env"]
+    import xml.etree.ElementTree as ET
+
+    topo = ET.fromstring(r["rccl_topo"])
+    assert len([n for n in topo.iter("net")]) == 8 and len([p for p in topo.iter("pci") if p.get("class") == "0x120000"]) == 8
     assert len(r["networkd_files"]) == 8
     # SIGTERM: label removed, addresses flushed, links back down.
     assert r["agent_rc"] == 0

@@ -18,6 +18,8 @@ from network_operator_amd.operator.leader import LeaderElector
 from network_operator_amd.operator.reconciler import agent_args
 from network_operator_amd.testing.fakeapi import FakeApiServer
 
+TOPO_ARGS = ["--rccl-topo=/host/etc/amd/scale-out/rccl-topo.xml", "--rccl-topo-env-path=/etc/amd/scale-out/rccl-topo.xml"]
+
 NS = "amd-network-operator"
 
 
@@ -94,7 +96,7 @@ def test_reconcile_lifecycle_reference_parity():
                 assert len(c) == 1 and c[0]["image"] == "amd/my-linkdiscovery:latest"
                 assert c[0]["args"] == ["--configure=true", "--keep-running", "--mode=L3", "--mtu=8000", "--wait=90s",
                                         "--rccl-net=/host/etc/amd/scale-out/rccl-net.json",
-                                        "--rccl-env=/host/etc/amd/scale-out/rccl.env"]
+                                        "--rccl-env=/host/etc/amd/scale-out/rccl.env", *TOPO_ARGS]
                 assert [v["name"] for v in pod["volumes"]] == ["nfd-features", "rccl-artifacts"]
                 assert [m["name"] for m in c[0]["volumeMounts"]] == ["nfd-features", "rccl-artifacts"]
                 assert pod["nodeSelector"] == {"foo": "bar"}
@@ -116,7 +118,7 @@ def test_reconcile_lifecycle_reference_parity():
                 ds = fake.get_object(kube.DAEMONSETS, "policy", NS)
                 c = ds["spec"]["template"]["spec"]["containers"][0]
                 assert c["args"] == ["--configure=true", "--keep-running", "--mode=L2",
-                                     "--rccl-env=/host/etc/amd/scale-out/rccl.env"]
+                                     "--rccl-env=/host/etc/amd/scale-out/rccl.env", *TOPO_ARGS]
                 assert [v["name"] for v in ds["spec"]["template"]["spec"]["volumes"]] == ["nfd-features",
                                                                                           "rccl-artifacts"]
             await eventually(l2_ok)

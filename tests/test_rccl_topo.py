@@ -1,0 +1,173 @@
+"""NCCL_TOPO_FILE written by the agent (native/src/artifacts.cpp generate_rccl_topo).
+
+CPU: golden XML for the captured 8x MI355X node (tests/fixtures/mi355x_node_topology.json ->
+fake sysfs), the structure RCCL needs (GPU and NIC functions folded under the same switch as
+RCCL folds them), and the agent's rccl.env pointing at it.
+
+GPU (-m gpu): RCCL itself loads the file generated from the box's real /sys — a fresh process
+per case, because RCCL reads NCCL_TOPO_FILE once at communicator init — and its topology dump
+(NCCL_TOPO_DUMP_FILE) must place the GPU (and, when RCCL's network plugin can use one of the
+file's NICs, that NIC) exactly where the file put it.  The reference's counterpart is the
+HCCL-consumed gaudinet.json (reference cmd/discover/gaudinet.go:28-89).
+"""
+
+import json
+import os
+import subprocess
+import sys
+import textwrap
+import xml.etree.ElementTree as ET
+from pathlib import Path
+
+import pytest
+
+from network_operator_amd.testing import fakesysfs
+
+ROOT = Path(__file__).resolve().parent.parent
+GOLDEN = ROOT / "tests" / "fixtures" / "mi355x_rccl_topo.xml"
+
+
+def _chain(root: ET.Element, busid: str):
+    """[cpu numaid, outer pci busid, ..., busid] for the pci element `busid`, or None."""
+    def walk(el, path):
+        for c in el:
+            here = path + [c.get("numaid") if c.tag == "cpu" else c.get("busid")] if c.tag in ("cpu", "pci") else path
+            if c.tag == "pci" and c.get("busid") == busid:
+                return here
+            r = walk(c, here)
+            if r:
+                return r
+        return None
+    return walk(root, [])
+
+
+def _net_chain(root: ET.Element, name: str):
+    def walk(el, path):
+        for c in el:
+            if c.tag == "net" and c.get("name") == name:
+                return path
+            here = path + [c.get("numaid") if c.tag == "cpu" else c.get("busid")] if c.tag in ("cpu", "pci") else path
+            r = walk(c, here)
+            if r:
+                return r
+        return None
+    return walk(root, [])
+
+
+def test_topo_xml_golden_for_captured_node(native, tmp_path):
+    fakesysfs.build_mi355x_node(tmp_path)
+    xml = native.rccl_topo_xml(str(tmp_path) + "/", cpu=fakesysfs.MI355X_HOST_CPU)
+    assert xml == GOLDEN.read_text()
+
+
+def test_topo_xml_gpu_and_nic_share_rccl_switch(native, tmp_path):
+    fx = fakesysfs.build_mi355x_node(tmp_path)
+    root = ET.fromstring(native.rccl_topo_xml(str(tmp_path) + "/", cpu=fakesysfs.MI355X_HOST_CPU))
+    assert root.tag == "system" and root.get("version") == "2"
+    for cpu in root.iter("cpu"):  # RCCL refuses a <cpu> without these (its xml.h "Attribute arch ... not found")
+        assert {"numaid", "affinity", "arch", "vendor", "familyid", "modelid"} <= set(cpu.keys())
+    gpus = [p.get("busid") for p in root.iter("pci") if p.get("class") == "0x120000"]
+    assert sorted(gpus) == sorted(g["bdf"] for g in fx["gpus"])
+    nets = [n.get("name") for n in root.iter("net")]
+    assert len(nets) == 8 and len(set(nets)) == 8  # the scale-out NICs only, not the management ports
+    assert not list(root.iter("xgmi")) and not list(root.iter("gpu"))  # left to RCCL (see artifacts.hpp)
+    pairs = {p["gpu"]: p["nic"] for p in native.discover(str(tmp_path) + "/")["pairs"]}
+    rdma = {n["ifname"]: n["rdma_dev"] for n in native.discover(str(tmp_path) + "/")["nics"]}
+    for gpu, nic in pairs.items():
+        g, n = _chain(root, gpu), _net_chain(root, rdma[nic])
+        assert g[0] == n[0] and g[1] == n[1], (gpu, nic, g, n)  # same CPU, same top switch
+        assert len(g) == 5 and len(n) == 4  # cpu > 01 > 06 > 08 > GPU;  cpu > 01 > 03 > NIC (RCCL folding)
+
+
+def test_topo_xml_extra_interface_without_rdma(native, tmp_path):
+    fakesysfs.build_mi355x_node(tmp_path)
+    root = ET.fromstring(native.rccl_topo_xml(str(tmp_path) + "/", interfaces=["ens9np0", "lo"], cpu=fakesysfs.MI355X_HOST_CPU))
+    # ens9np0 (a management port, not GPU-affine) is listed under its RDMA device name, the
+    # name RCCL's IB plugin gives it; lo is virtual -> nothing PCIe to pin.
+    names = [n.get("name") for n in root.iter("net")]
+    assert "mlx5_8" in names and len(names) == 9 and "lo" not in names
+    # Without an RDMA device the socket plugin's name (the netdev) is used.
+    import shutil
+
+    for ib in tmp_path.glob("devices/**/infiniband/mlx5_8"):
+        shutil.rmtree(ib)
+    root = ET.fromstring(native.rccl_topo_xml(str(tmp_path) + "/", interfaces=["ens9np0"], cpu=fakesysfs.MI355X_HOST_CPU))
+    assert "ens9np0" in [n.get("name") for n in root.iter("net")]
+
+
+# ------------------------------------------------------------------------------------------
+# On the GPU box: RCCL loads the file.
+# ------------------------------------------------------------------------------------------
+_RCCL_INIT = textwrap.dedent("""
+    import os, sys, torch, torch.distributed as dist
+    d = torch.device("cuda", 0); torch.cuda.set_device(d)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=d)
+    x = torch.ones(4096, device=d); dist.all_reduce(x); torch.cuda.synchronize()
+    dist.destroy_process_group()
+""")
+
+
+def _rccl_dump(tmp_path, topo_file, extra_env=None, tag="run"):
+    dump = tmp_path / f"dump_{tag}.xml"
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(29700 + hash(tag) % 200),
+               NCCL_TOPO_DUMP_FILE=str(dump), NCCL_DEBUG="INFO", NCCL_DEBUG_SUBSYS="INIT,GRAPH,NET")
+    if topo_file:
+        env["NCCL_TOPO_FILE"] = str(topo_file)
+    env.update(extra_env or {})
+    r = subprocess.run([sys.executable, "-c", _RCCL_INIT], env=env, capture_output=True, text=True, timeout=110)
+    return r, (ET.parse(dump).getroot() if dump.exists() else None)
+
+
+def _ipv4_ifaces():
+    import psutil
+
+    out = {}
+    for name, addrs in psutil.net_if_addrs().items():
+        for a in addrs:
+            if a.family == 2:
+                out[name] = a.address
+    return out
+
+
+@pytest.mark.gpu
+def test_rccl_loads_generated_topology(native, tmp_path):
+    xml = native.rccl_topo_xml("/sys/")
+    topo = tmp_path / "rccl-topo.xml"
+    topo.write_text(xml)
+    mine = ET.fromstring(xml)
+    r, dump = _rccl_dump(tmp_path, topo, tag="file")
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert f"Loading topology file {topo}" in r.stdout + r.stderr or "NCCL_TOPO_FILE set by environment" in r.stdout + r.stderr
+    assert dump is not None and dump.get("version") == mine.get("version")
+    # the visible GPU's pci element in the dump, and its ancestry there vs in our file
+    seen = [p.get("busid") for p in dump.iter("pci") if p.find("gpu") is not None]
+    assert len(seen) == 1, ET.tostring(dump)[:2000]
+    busid = seen[0]
+    assert _chain(dump, busid) == _chain(mine, busid), (ET.tostring(dump)[:3000], _chain(mine, busid))
+    # RCCL's own detection without the file agrees with it (the file mirrors RCCL's folding).
+    r0, auto = _rccl_dump(tmp_path, None, tag="auto")
+    assert r0.returncode == 0, r0.stderr[-2000:]
+    assert _chain(auto, busid) == _chain(mine, busid)
+    (ROOT / "gpurun_out").mkdir(exist_ok=True)
+    (ROOT / "gpurun_out" / "rccl_topo_loaded.json").write_text(json.dumps({
+        "gpu_busid": busid, "chain_in_file": _chain(mine, busid), "chain_in_rccl_dump": _chain(dump, busid),
+        "dump_version": dump.get("version"), "nets_in_dump": [n.get("name") for n in dump.iter("net")]}, indent=1))
+
+
+@pytest.mark.gpu
+def test_rccl_places_socket_nic_from_topology_file(native, tmp_path):
+    """With NCCL_SOCKET_IFNAME on one of the file's NICs, RCCL's socket plugin uses it and the
+    dump shows that net where the file put it (under the GPU's switch for a rail NIC)."""
+    d = native.discover("/sys/")
+    ipv4 = _ipv4_ifaces()
+    usable = [p["nic"] for p in d["pairs"] if p["nic"] in ipv4]
+    if not usable:
+        pytest.skip(f"no scale-out NIC of this box has an IPv4 address in this network namespace "
+                    f"(paired: {[p['nic'] for p in d['pairs']]}; with IPv4: {sorted(ipv4)})")
+    nic = usable[0]
+    xml = native.rccl_topo_xml("/sys/")
+    topo = tmp_path / "rccl-topo.xml"
+    topo.write_text(xml)
+    r, dump = _rccl_dump(tmp_path, topo, {"NCCL_SOCKET_IFNAME": "=" + nic, "NCCL_IB_DISABLE": "1"}, tag="nic")
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert _net_chain(dump, nic) == _net_chain(ET.fromstring(xml), nic)
