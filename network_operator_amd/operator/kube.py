@@ -69,9 +69,16 @@ MUTATINGWEBHOOKS = Resource("admissionregistration.k8s.io", "v1", "mutatingwebho
 VALIDATINGWEBHOOKS = Resource("admissionregistration.k8s.io", "v1", "validatingwebhookconfigurations",
                               "ValidatingWebhookConfiguration", False)
 CRDS = Resource("apiextensions.k8s.io", "v1", "customresourcedefinitions", "CustomResourceDefinition", False)
+CLUSTERROLES = Resource("rbac.authorization.k8s.io", "v1", "clusterroles", "ClusterRole", False)
+CLUSTERROLEBINDINGS = Resource("rbac.authorization.k8s.io", "v1", "clusterrolebindings", "ClusterRoleBinding", False)
+ROLES = Resource("rbac.authorization.k8s.io", "v1", "roles", "Role", True)
+SERVICES = Resource("", "v1", "services", "Service", True)
+CONFIGMAPS = Resource("", "v1", "configmaps", "ConfigMap", True)
+DEPLOYMENTS = Resource("apps", "v1", "deployments", "Deployment", True)
 
 ALL_RESOURCES = [NETWORKCLUSTERPOLICIES, DAEMONSETS, PODS, NODES, NAMESPACES, SERVICEACCOUNTS, EVENTS, ROLEBINDINGS,
-                 LEASES, TOKENREVIEWS, SUBJECTACCESSREVIEWS, MUTATINGWEBHOOKS, VALIDATINGWEBHOOKS, CRDS]
+                 LEASES, TOKENREVIEWS, SUBJECTACCESSREVIEWS, MUTATINGWEBHOOKS, VALIDATINGWEBHOOKS, CRDS,
+                 CLUSTERROLES, CLUSTERROLEBINDINGS, ROLES, SERVICES, CONFIGMAPS, DEPLOYMENTS]
 
 
 # ---------------------------------------------------------------------------

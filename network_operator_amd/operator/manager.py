@@ -23,6 +23,7 @@ from .controller import PolicyController
 from .kube import ApiClient, load_config
 from .leader import DEFAULT_LEASE_ID, LeaderElector
 from .metrics import OperatorMetrics
+from .seeder import PolicySeeder
 from .servers import DEFAULT_CERT_DIR, Servers
 
 log = logging.getLogger("setup")
@@ -96,6 +97,13 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--dependency-check-interval", type=float, default=60.0,
                     help="seconds between checks for Node Feature Discovery / cert-manager (0 = off)")
     ap.add_argument("--leader-election-id", default=DEFAULT_LEASE_ID)
+    ap.add_argument("--policies-file", default="",
+                    help="YAML file ({policies: [NetworkClusterPolicy, ...]}, the Helm chart's ConfigMap) whose "
+                         "policies the leader creates / updates / deletes through the API server")
+    ap.add_argument("--policies-owner", default="",
+                    help="ClusterRole/<name>: cluster-scoped owner of the seeded policies (uninstalling it "
+                         "garbage-collects them)")
+    ap.add_argument("--policies-interval", type=float, default=10.0, help="seconds between --policies-file passes")
     ap.add_argument("--zap-devel", action="store_true", default=True)
     ap.add_argument("--zap-log-level", default="info")
     ap.add_argument("--zap-encoder", default="console", choices=["console", "json"])
@@ -155,10 +163,20 @@ async def run(argv: Optional[List[str]] = None, stop: Optional[asyncio.Event] = 
 
         async def lead() -> None:
             await controller.start()
+            seed = None
+            if opts.policies_file:
+                # Only the leader writes policies; the webhook server is already serving, so the
+                # API server can admit them (see seeder.py for why the chart does not create them).
+                seeder = PolicySeeder(client, opts.policies_file, opts.policies_owner, opts.policies_interval)
+                seed = asyncio.ensure_future(seeder.run(stop))
             if started:
                 started.set()
             log.info("starting manager")
-            await stop.wait()
+            try:
+                await stop.wait()
+            finally:
+                if seed is not None:
+                    seed.cancel()
 
         try:
             if opts.leader_elect:

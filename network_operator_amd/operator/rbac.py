@@ -47,6 +47,13 @@ METRICS_AUTH_RULES = (
     ("authorization.k8s.io", ("subjectaccessreviews",), ("create",)),
 )
 
+# Helm install only: the policy seeder (operator/seeder.py) reads its own ClusterRole, the owner it
+# makes the chart's policies dependents of.  Scoped to that one object by resourceNames.
+def policy_owner_rule(cluster_role: str) -> dict:
+    return {"apiGroups": ["rbac.authorization.k8s.io"], "resources": ["clusterroles"], "verbs": ["get"],
+            "resourceNames": [cluster_role]}
+
+
 # Aggregated user-facing roles for NetworkClusterPolicy.
 POLICY_EDITOR_RULES = (
     ("amd.com", ("networkclusterpolicies",), READ + WRITE),

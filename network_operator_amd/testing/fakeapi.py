@@ -13,9 +13,12 @@ here, so this server implements the API-server behaviour the operator depends on
 * LIST with label / field selectors; WATCH with replay from a resourceVersion, BOOKMARK
   events, ``410 Gone`` for compacted history, ``timeoutSeconds``;
 * CRD structural-schema validation of NetworkClusterPolicies (422 Invalid) and pruning;
-* admission: calls Mutating/ValidatingWebhookConfigurations registered in the store (by
-  ``clientConfig.url``) and applies the returned JSONPatch — including the *rules* match on
-  the resource plural, so a webhook registered for a wrong resource is never called;
+* admission: calls Mutating/ValidatingWebhookConfigurations registered in the store — by
+  ``clientConfig.url``, or by ``clientConfig.service`` resolved through the stored Service and a
+  test-set ready endpoint (``service_endpoints``), failing per ``failurePolicy`` while the
+  Service or its endpoint is missing, as a real API server does before the operator pod
+  serves — and applies the returned JSONPatch, including the *rules* match on the resource
+  plural, so a webhook registered for a wrong resource is never called;
 * background garbage collection of dependents through ``ownerReferences``;
 * a DaemonSet controller simulation: ``desiredNumberScheduled`` from Nodes matching the pod
   template's nodeSelector, ``numberReady`` from per-node agent readiness set by the test;
@@ -190,6 +193,8 @@ class FakeApiServer:
         self.requests: List[Tuple[str, str]] = []
         self.accesses: set = set()                           # (verb, group, resource[/sub])
         self.admission_calls: List[Tuple[str, str]] = []
+        # (namespace, service) -> "https://host:port" of a ready endpoint (service-referenced webhooks)
+        self.service_endpoints: Dict[Tuple[str, str], str] = {}
         self._runner: Optional[web.AppRunner] = None
         self.url = ""
         self._bg: List[asyncio.Task] = []
@@ -589,18 +594,26 @@ class FakeApiServer:
                 for wh in cfg.get("webhooks", []) or []:
                     if not any(self._rule_matches(rule, res, op) for rule in wh.get("rules", []) or []):
                         continue
-                    url = (wh.get("clientConfig") or {}).get("url")
+                    cc = wh.get("clientConfig") or {}
+                    url, unreachable = cc.get("url"), None
                     if not url:
-                        continue  # service references cannot be resolved here
+                        url, unreachable = self._service_url(cc.get("service") or {})
                     self.admission_calls.append((wh.get("name", ""), op))
+                    if unreachable:
+                        if wh.get("failurePolicy", "Fail") == "Ignore":
+                            continue
+                        raise _Conflict(500, "InternalError", f'Internal error occurred: failed calling webhook '
+                                                              f'"{wh.get("name")}": failed to call webhook: {unreachable}')
                     review = {"apiVersion": "admission.k8s.io/v1", "kind": "AdmissionReview", "request": {
                         "uid": str(uuid.uuid4()), "kind": {"group": res.group, "version": res.version, "kind": res.kind},
                         "resource": {"group": res.group, "version": res.version, "resource": res.plural},
                         "operation": op, "object": obj, "oldObject": old, "name": obj.get("metadata", {}).get("name")}}
                     ctx: Optional[ssl.SSLContext] = None
-                    ca = (wh.get("clientConfig") or {}).get("caBundle")
+                    ca = cc.get("caBundle")
                     if url.startswith("https"):
                         ctx = ssl.create_default_context()
+                        if cc.get("service"):
+                            ctx.check_hostname = False  # endpoints are 127.0.0.1 here, not <svc>.<ns>.svc
                         if ca:
                             with tempfile.NamedTemporaryFile("wb", suffix=".pem", delete=False) as f:
                                 f.write(base64.b64decode(ca))
@@ -622,6 +635,20 @@ class FakeApiServer:
                     if mutating and resp.get("patch"):
                         obj = json_patch_apply(obj, json.loads(base64.b64decode(resp["patch"])))
         return obj
+
+    def _service_url(self, svc: dict) -> Tuple[str, Optional[str]]:
+        """A service-referenced webhook, the way the API server reaches it: the Service must exist
+        and have a ready endpoint (``service_endpoints``, set by the test when the operator pod
+        is serving); otherwise the call fails and ``failurePolicy`` decides."""
+        ns, name, path = svc.get("namespace", ""), svc.get("name", ""), svc.get("path", "/")
+        port = svc.get("port", 443)
+        shown = f'Post "https://{name}.{ns}.svc:{port}{path}?timeout=10s"'
+        if (ns, name) not in self._table(kube.SERVICES):
+            return "", f'{shown}: service "{name}" not found'
+        base = self.service_endpoints.get((ns, name))
+        if not base:
+            return "", f'{shown}: no endpoints available for service "{name}"'
+        return base.rstrip("/") + path, None
 
     @staticmethod
     def _rule_matches(rule: dict, res: Resource, op: str) -> bool:

@@ -1,0 +1,210 @@
+"""``helm install --set config.amd.enabled=true`` on a fresh cluster, end to end in the fake API
+server: every object of the rendered chart is applied in Helm's install order, then the operator
+pod "starts" (its webhook certificate issued, its Service gaining an endpoint after it serves).
+
+The fake API server resolves service-referenced webhooks (round 1 skipped them), so it now has
+the race a real cluster has. A NetworkClusterPolicy created in the same release, as the
+reference chart does (reference charts/network-operator/templates/gaudi.yaml:1-22,
+README.md:22-26), is rejected by the Fail-policy webhook while no operator pod serves. The chart
+therefore ships its policies in a ConfigMap, and the operator applies them itself once its
+webhook is up (operator/seeder.py). This test drives install, upgrade, disable and uninstall.
+"""
+
+import asyncio
+import base64
+import socket
+from pathlib import Path
+
+import pytest
+import yaml
+
+from network_operator_amd.operator import kube, manager
+from network_operator_amd.operator.kube import ApiClient, ApiError, KubeConfig, Resource
+from network_operator_amd.operator.servers import generate_self_signed
+from network_operator_amd.packaging import manifests as M
+from network_operator_amd.testing.fakeapi import FakeApiServer
+from network_operator_amd.testing.render import helm_template
+
+ROOT = Path(__file__).resolve().parent.parent
+CHART = ROOT / "charts" / "network-operator"
+NS = "amd-network-operator"
+P = kube.NETWORKCLUSTERPOLICIES
+
+# Add-on kinds the chart uses (cert-manager, NFD): served by the fake like installed CRDs.
+ISSUERS = Resource("cert-manager.io", "v1", "issuers", "Issuer", True)
+CERTIFICATES = Resource("cert-manager.io", "v1", "certificates", "Certificate", True)
+NODEFEATURERULES = Resource("nfd.k8s-sigs.io", "v1alpha1", "nodefeaturerules", "NodeFeatureRule", False)
+BY_KIND = {r.kind: r for r in kube.ALL_RESOURCES + [ISSUERS, CERTIFICATES, NODEFEATURERULES]}
+
+# Helm's InstallOrder (pkg/releaseutil/kind_sorter.go); kinds it does not list go last.
+HELM_ORDER = ["Namespace", "NetworkPolicy", "ResourceQuota", "LimitRange", "PodSecurityPolicy", "PodDisruptionBudget",
+              "ServiceAccount", "Secret", "SecretList", "ConfigMap", "StorageClass", "PersistentVolume",
+              "PersistentVolumeClaim", "CustomResourceDefinition", "ClusterRole", "ClusterRoleList",
+              "ClusterRoleBinding", "ClusterRoleBindingList", "Role", "RoleList", "RoleBinding", "RoleBindingList",
+              "Service", "DaemonSet", "Pod", "ReplicationController", "ReplicaSet", "Deployment",
+              "HorizontalPodAutoscaler", "StatefulSet", "Job", "CronJob", "IngressClass", "Ingress", "APIService",
+              "MutatingWebhookConfiguration", "ValidatingWebhookConfiguration"]
+
+
+def helm_install_order(docs):
+    rank = {k: i for i, k in enumerate(HELM_ORDER)}
+    return sorted(docs, key=lambda d: rank.get(d["kind"], len(HELM_ORDER)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+async def _until(fn, timeout=15.0):
+    end = asyncio.get_event_loop().time() + timeout
+    last = None
+    while asyncio.get_event_loop().time() < end:
+        try:
+            if fn():
+                return
+        except (KeyError, TypeError, IndexError) as e:
+            last = e
+        await asyncio.sleep(0.02)
+    raise AssertionError(f"timeout ({last!r})")
+
+
+def _policies_file(docs, path: Path) -> None:
+    """What the kubelet projects from the ConfigMap volume into the operator container."""
+    cm = [d for d in docs if d["kind"] == "ConfigMap" and d["metadata"]["name"] == M.POLICIES_CONFIGMAP][0]
+    tmp = path.with_suffix(".tmp")
+    tmp.write_text(cm["data"]["policies.yaml"])
+    tmp.replace(path)
+
+
+def _dep_args(docs):
+    dep = [d for d in docs if d["kind"] == "Deployment"][0]
+    return dep["spec"]["template"]["spec"]["containers"][0]["args"]
+
+
+def test_reference_style_policy_in_the_release_fails_while_the_operator_is_down():
+    """The bug class the fake could not see in round 1: Fail-policy webhooks registered in the
+    same release as the CR, no operator endpoint yet -> the API server refuses the CR."""
+    async def body():
+        fake = FakeApiServer(extra_groups=["cert-manager.io", "nfd.k8s-sigs.io"])
+        fake.resources += [ISSUERS, CERTIFICATES, NODEFEATURERULES]
+        url = await fake.start()
+        try:
+            docs = helm_install_order(helm_template(CHART, {"config": {"amd": {"enabled": True}}}, NS))
+            async with ApiClient(KubeConfig(host=url)) as c:
+                for d in docs:
+                    await c.create(BY_KIND[d["kind"]], d, d["metadata"].get("namespace"))
+                policy = yaml.safe_load(_configmap_text(docs))["policies"][0]
+                with pytest.raises(ApiError) as e:
+                    await c.create(P, policy)
+                assert e.value.status == 500 and "no endpoints available" in str(e.value)
+        finally:
+            await fake.stop()
+
+    asyncio.run(asyncio.wait_for(body(), 60))
+
+
+def _configmap_text(docs):
+    return [d for d in docs if d["kind"] == "ConfigMap" and d["metadata"]["name"] == M.POLICIES_CONFIGMAP][0][
+        "data"]["policies.yaml"]
+
+
+def test_one_release_helm_install_upgrade_and_uninstall(tmp_path, monkeypatch):
+    monkeypatch.setenv("OPERATOR_NAMESPACE", NS)
+    hook_port = _free_port()
+
+    async def body():
+        fake = FakeApiServer(extra_groups=["cert-manager.io", "nfd.k8s-sigs.io"])
+        fake.resources += [ISSUERS, CERTIFICATES, NODEFEATURERULES]
+        url = await fake.start()
+        fake.add_node("mi355x-0", {"amd.feature.node.kubernetes.io/gpu-ready": "true"})
+        stop, started = asyncio.Event(), asyncio.Event()
+        task = None
+        try:
+            docs = helm_install_order(helm_template(CHART, {"config": {"amd": {"enabled": True, "mtu": 9000}}}, NS))
+            assert not [d for d in docs if d["kind"] == "NetworkClusterPolicy"]
+            async with ApiClient(KubeConfig(host=url)) as c:
+                # 1. `helm install`: every release object, Helm's order, nothing else running.
+                for d in docs:
+                    await c.create(BY_KIND[d["kind"]], d, d["metadata"].get("namespace"))
+                assert not fake.list_objects(P)
+
+                # 2. cert-manager issues the serving certificate and injects its CA.
+                certs = tmp_path / "certs"
+                crt, _ = generate_self_signed(certs, cn=f"amd-network-webhook.{NS}.svc")
+                ca = base64.b64encode(crt.read_bytes()).decode()
+                for res in (kube.MUTATINGWEBHOOKS, kube.VALIDATINGWEBHOOKS):
+                    for cfg in fake.list_objects(res):
+                        for wh in cfg["webhooks"]:
+                            wh["clientConfig"]["caBundle"] = ca
+                        await c.replace(res, cfg)
+
+                # 3. The operator pod starts with the Deployment's own args (the ConfigMap volume
+                #    projected to a file); the Service gets its endpoint a moment after it serves.
+                pfile = tmp_path / "policies.yaml"
+                _policies_file(docs, pfile)
+                args = [a for a in _dep_args(docs) if not a.startswith(("--policies-file", "--webhook-port",
+                                                                         "--webhook-cert-dir", "--metrics-bind",
+                                                                         "--health-probe"))]
+                assert "--policies-owner=ClusterRole/amd-network-operator" in args
+                task = asyncio.ensure_future(manager.run(
+                    args + ["--master", url, f"--policies-file={pfile}", "--policies-interval=0.2",
+                            f"--webhook-port={hook_port}", f"--webhook-cert-dir={certs}",
+                            "--health-probe-bind-address=0", "--dependency-check-interval=0"],
+                    stop=stop, started=started))
+                await asyncio.wait_for(started.wait(), 10)
+                await asyncio.sleep(0.3)  # readiness probe period: creates before this fail and retry
+                fake.service_endpoints[(NS, "amd-network-webhook")] = f"https://127.0.0.1:{hook_port}"
+
+                # The policy exists, went through both webhooks, and is reconciled.
+                await _until(lambda: fake.get_object(P, "netconf-amd-scale-out") is not None)
+                assert ("default.networkclusterpolicies.amd.com", "CREATE") in fake.admission_calls
+                assert ("validate.networkclusterpolicies.amd.com", "CREATE") in fake.admission_calls
+                await _until(lambda: fake.get_object(kube.DAEMONSETS, "netconf-amd-scale-out", NS) is not None)
+                pol = fake.get_object(P, "netconf-amd-scale-out")
+                role = fake.get_object(kube.CLUSTERROLES, "amd-network-operator")
+                assert pol["metadata"]["ownerReferences"] == [{"apiVersion": "rbac.authorization.k8s.io/v1",
+                                                               "kind": "ClusterRole", "name": "amd-network-operator",
+                                                               "uid": role["metadata"]["uid"]}]
+                assert pol["spec"]["amdScaleOut"]["mtu"] == 9000
+
+                # 4. `helm upgrade --set config.amd.mtu=4200`: the projected file changes.
+                up = helm_template(CHART, {"config": {"amd": {"enabled": True, "mtu": 4200}}}, NS)
+                _policies_file(up, pfile)
+                await _until(lambda: "--mtu=4200" in fake.get_object(kube.DAEMONSETS, "netconf-amd-scale-out", NS)
+                             ["spec"]["template"]["spec"]["containers"][0]["args"])
+
+                # A user's own policy is never touched by the seeder.
+                mine = yaml.safe_load(_configmap_text(up))["policies"][0]
+                mine["metadata"] = {"name": "user-policy"}
+                await c.create(P, mine)
+
+                # 5. `helm upgrade --set config.amd.enabled=false`: the policy and its DaemonSet go.
+                _policies_file(helm_template(CHART, {}, NS), pfile)
+                await _until(lambda: fake.get_object(P, "netconf-amd-scale-out") is None)
+                await _until(lambda: fake.get_object(kube.DAEMONSETS, "netconf-amd-scale-out", NS) is None)
+                assert fake.get_object(P, "user-policy") is not None
+
+                # 6. Re-enable, then `helm uninstall`: the release's ClusterRole goes, and the
+                #    garbage collector takes the seeded policy and its DaemonSet with it.
+                _policies_file(docs, pfile)
+                await _until(lambda: fake.get_object(kube.DAEMONSETS, "netconf-amd-scale-out", NS) is not None)
+                stop.set()
+                assert await asyncio.wait_for(task, 10) == 0
+                task = None
+                for d in reversed(docs):
+                    if d["kind"] != "CustomResourceDefinition":  # Helm keeps crds/ on uninstall
+                        await c.delete(BY_KIND[d["kind"]], d["metadata"]["name"], d["metadata"].get("namespace"))
+                assert fake.get_object(P, "netconf-amd-scale-out") is None
+                assert fake.get_object(kube.DAEMONSETS, "netconf-amd-scale-out", NS) is None
+                assert fake.get_object(P, "user-policy") is not None
+        finally:
+            stop.set()
+            if task is not None:
+                await asyncio.wait_for(task, 10)
+            await fake.stop()
+
+    asyncio.run(asyncio.wait_for(body(), 90))

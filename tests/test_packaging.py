@@ -23,6 +23,16 @@ def _by_kind(docs, kind):
     return [d for d in docs if d["kind"] == kind]
 
 
+def _chart_policies(docs):
+    """The policies a Helm release asks for: the ConfigMap the operator seeds them from."""
+    cm = [d for d in docs if d["kind"] == "ConfigMap" and d["metadata"]["name"] == M.POLICIES_CONFIGMAP]
+    assert len(cm) == 1
+    return (yaml.safe_load(cm[0]["data"]["policies.yaml"]) or {}).get("policies") or []
+
+
+HELM_SEED_ARGS = [f"--policies-file={M.POLICIES_DIR}/policies.yaml", "--policies-owner=ClusterRole/amd-network-operator"]
+
+
 def _rules_allow(roles, group, resource, verb):
     for r in roles:
         for rule in r.get("rules", []):
@@ -43,11 +53,14 @@ def test_helm_defaults():
     assert {"Deployment", "ClusterRole", "Role", "RoleBinding", "ClusterRoleBinding", "Service", "Certificate", "Issuer",
             "ServiceAccount", "MutatingWebhookConfiguration", "ValidatingWebhookConfiguration",
             "CustomResourceDefinition", "NodeFeatureRule"} <= kinds
-    assert not _by_kind(docs, "NetworkClusterPolicy")  # config.amd.enabled defaults to false
+    assert not _by_kind(docs, "NetworkClusterPolicy")  # never a release object (see operator/seeder.py)
+    assert _chart_policies(docs) == []  # config.amd.enabled defaults to false
     dep = _by_kind(docs, "Deployment")[0]
     assert dep["metadata"]["namespace"] == "amd-net"
     c = dep["spec"]["template"]["spec"]["containers"][0]
-    assert c["args"] == M.operator_args(metrics=True)
+    assert c["args"] == M.operator_args(metrics=True) + HELM_SEED_ARGS
+    assert {"name": "policies", "configMap": {"name": M.POLICIES_CONFIGMAP, "optional": True}} in \
+        dep["spec"]["template"]["spec"]["volumes"]
     assert "--metrics-bind-address=:8443" in c["args"] and "--leader-elect" in c["args"]
     assert c["image"] == "amd/amd-network-operator:0.1.0"
     assert c["resources"] == M.RESOURCES and c["imagePullPolicy"] == "IfNotPresent"
@@ -72,7 +85,8 @@ def test_helm_defaults():
 
 def test_helm_policy_rendering_and_validation():
     docs = helm_template(CHART, {"config": {"amd": {"enabled": True, "mode": "L3", "mtu": 9000}}})
-    cr = _by_kind(docs, "NetworkClusterPolicy")[0]
+    assert not _by_kind(docs, "NetworkClusterPolicy")
+    cr = _chart_policies(docs)[0]
     assert CRD.validate(cr) == []
     assert W.validate_create(T.NetworkClusterPolicy.from_dict(cr)) == []
     assert cr["spec"]["amdScaleOut"]["image"] == "amd/amd-network-linkdiscovery:0.1.0"
@@ -137,14 +151,19 @@ def test_kustomize_and_helm_install_the_same_operator():
     hm = helm_template(CHART, namespace="amd-network-operator")
 
     def rules(docs):
-        return sorted((r["metadata"]["name"], yaml.safe_dump(r["rules"])) for r in _by_kind(docs, "ClusterRole"))
+        # The Helm operator's one extra rule: reading its own ClusterRole (the seeded policies' owner).
+        seed = M.rbac.policy_owner_rule("amd-network-operator")
+        return sorted((r["metadata"]["name"], yaml.safe_dump([x for x in r["rules"] if x != seed]))
+                      for r in _by_kind(docs, "ClusterRole"))
 
     assert rules(kz) == rules(hm)
     kp = _by_kind(kz, "Deployment")[0]["spec"]["template"]["spec"]
     hp = _by_kind(hm, "Deployment")[0]["spec"]["template"]["spec"]
     kc, hc = kp["containers"][0], hp["containers"][0]
-    assert kc["args"] == hc["args"] and kc["ports"] == hc["ports"] and kc["resources"] == hc["resources"]
-    assert kp["volumes"] == hp["volumes"] and kp["serviceAccountName"] == hp["serviceAccountName"]
+    # Helm alone seeds the release's policies (kustomize users apply config/operator/samples).
+    assert kc["args"] + HELM_SEED_ARGS == hc["args"] and kc["ports"] == hc["ports"] and kc["resources"] == hc["resources"]
+    assert kp["volumes"] == [v for v in hp["volumes"] if v["name"] != "policies"]
+    assert kp["serviceAccountName"] == hp["serviceAccountName"]
     for kind in ("MutatingWebhookConfiguration", "ValidatingWebhookConfiguration"):
         assert _by_kind(kz, kind)[0]["webhooks"] == _by_kind(hm, kind)[0]["webhooks"]
         assert _by_kind(kz, kind)[0]["metadata"]["annotations"] == _by_kind(hm, kind)[0]["metadata"]["annotations"]
@@ -227,7 +246,7 @@ def test_helm_package_archive(tmp_path):
     assert out.name == "amd-network-operator-0.1.0.tgz"
     with tarfile.open(out) as t:
         names = t.getnames()
-    assert "amd-network-operator/Chart.yaml" in names and "amd-network-operator/templates/amd.yaml" in names
+    assert "amd-network-operator/Chart.yaml" in names and "amd-network-operator/templates/policies.yaml" in names
     again = packaging.helm_package(tmp_path / "again")
     assert again.read_bytes() == out.read_bytes()  # deterministic
 
@@ -246,7 +265,7 @@ def test_ci_workflows_parse_and_cover_reference_jobs():
 def test_helm_host_nic_policy():
     docs = helm_template(ROOT / "charts" / "network-operator",
                          {"config": {"hostNic": {"enabled": True, "mode": "L3", "driverImage": "r/kmd:1"}}})
-    hn = [d for d in docs if d.get("kind") == "NetworkClusterPolicy"]
+    hn = _chart_policies(docs)
     assert len(hn) == 1 and hn[0]["spec"]["configurationType"] == "host-nic"
     assert hn[0]["spec"]["hostNic"]["layer"] == "L3" and hn[0]["spec"]["hostNic"]["driverImage"] == "r/kmd:1"
     from network_operator_amd.api.v1alpha1 import crd as CRD_
