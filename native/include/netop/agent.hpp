@@ -65,6 +65,7 @@ struct Config {
     std::string socket_ifname = "auto";
     std::string status_file;             // --status-file (JSON)
     std::string nm_keyfile_dir;          // --nm-keyfile-dir
+    bool nm_restore = true;              // --nm-restore: Managed=true again on exit
     int xgmi_expect_links = -1;          // -1 off; 0 = full mesh among discovered GPUs; N = exact pairs
     int64_t link_wait_ns = 3LL * 1000000000;  // netlink echo wait (network.go:251)
     // The RDMA core adds the RoCE v2 GID of a new IPv4 address asynchronously (netdev notifier
@@ -193,6 +194,9 @@ class Agent {
     std::vector<ethtool::FwLldpResult> fw_lldp_;
     std::vector<std::pair<std::string, std::string>> rccl_env_extra_;
     void disable_fw_lldp();
+    void restore_network_manager();
+    bool nm_keyfile_written_ = false;
+    std::vector<std::string> nm_unmanaged_;
 
    public:
     // Prometheus text exposition of the agent state (served on Config::metrics_addr).

@@ -38,5 +38,11 @@ std::vector<std::string> disable_for_interfaces(NetworkManagerIf& nm, const std:
 std::string keyfile_snippet(const std::vector<std::string>& ifaces);
 // Writes <conf_dir>/99-amd-network-operator.conf if conf_dir's parent exists; returns the path or "".
 std::string write_keyfile(const std::string& conf_dir, const std::vector<std::string>& ifaces);
+// Teardown: removes that keyfile if it is ours (starts with the agent's header line), so the NICs
+// go back to NetworkManager at its next start.  True when a file was removed.
+bool remove_keyfile(const std::string& conf_dir);
+// Teardown of the runtime change: Managed=true again on the named devices NM knows.  Returns the
+// interfaces re-managed.  Throws on device errors.
+std::vector<std::string> restore_for_interfaces(NetworkManagerIf& nm, const std::vector<std::string>& ifaces);
 
 }  // namespace netop::nm

@@ -56,6 +56,25 @@ static py::dict frame_dict(const lldp::Frame& f) {
     return d;
 }
 
+// Demarshalled D-Bus value -> Python (strings, booleans, integers, arrays / structs as lists).
+static py::object dbus_to_py(const dbus::Value& v) {
+    const char c = v.sig.empty() ? '?' : v.sig[0];
+    if (c == 's' || c == 'o' || c == 'g') return py::str(v.as_string());
+    if (c == 'b') return py::bool_(v.as_bool());
+    if (c == 'v') return dbus_to_py(v.variant_inner());
+    if (c == 'a' || c == '(') {
+        py::list l;
+        for (auto& x : v.as_array()) l.append(dbus_to_py(x));
+        return l;
+    }
+    if (auto p = std::get_if<uint32_t>(&v.v)) return py::int_(*p);
+    if (auto p = std::get_if<int32_t>(&v.v)) return py::int_(*p);
+    if (auto p = std::get_if<uint8_t>(&v.v)) return py::int_(*p);
+    if (auto p = std::get_if<int64_t>(&v.v)) return py::int_(*p);
+    if (auto p = std::get_if<uint64_t>(&v.v)) return py::int_(*p);
+    return py::str("<" + v.sig + ">");
+}
+
 PYBIND11_MODULE(_netop_native, m) {
     m.doc() = "Native building blocks of the AMD MI355X network operator agent";
     m.attr("__version__") = NETOP_VERSION;
@@ -282,6 +301,11 @@ PYBIND11_MODULE(_netop_native, m) {
         auto nm = nm::connect_system_bus(address);
         return nm::disable_for_interfaces(*nm, ifaces);
     }, py::arg("address"), py::arg("interfaces"));
+    m.def("nm_restore_interfaces", [](const std::string& address, const std::vector<std::string>& ifaces) {
+        py::gil_scoped_release nogil;
+        auto nm = nm::connect_system_bus(address);
+        return nm::restore_for_interfaces(*nm, ifaces);
+    }, py::arg("address"), py::arg("interfaces"));
     m.def("dbus_call_get_property", [](const std::string& address, const std::string& dest, const std::string& path,
                                        const std::string& iface, const std::string& prop) {
         dbus::Value v;
@@ -290,10 +314,21 @@ PYBIND11_MODULE(_netop_native, m) {
             dbus::Connection c(address);
             v = c.get_property(dest, path, iface, prop);
         }
-        if (v.sig == "s" || v.sig == "o") return py::object(py::str(v.as_string()));
-        if (v.sig == "b") return py::object(py::bool_(v.as_bool()));
-        if (v.sig == "u") return py::object(py::int_(v.as_u32()));
-        return py::object(py::str("<" + v.sig + ">"));
+        return dbus_to_py(v);
+    });
+    m.def("dbus_call", [](const std::string& address, const std::string& dest, const std::string& path,
+                          const std::string& iface, const std::string& member) {
+        std::vector<dbus::Value> out;
+        std::string unique;
+        {
+            py::gil_scoped_release nogil;
+            dbus::Connection c(address);
+            unique = c.unique_name();
+            out = c.call(dest, path, iface, member);
+        }
+        py::list l;
+        for (auto& v : out) l.append(dbus_to_py(v));
+        return py::make_tuple(unique, l);
     });
 
     m.def("find_rocev2_gid_index", [](const std::string& root, const std::string& dev, int port, const std::string& ip) -> py::object {

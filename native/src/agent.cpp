@@ -160,6 +160,24 @@ void Agent::post_cleanups() {
     } catch (const std::exception& e) {
         NLOG_W("Failed to restore interfaces to original state: %s", e.what());
     }
+    restore_network_manager();
+}
+
+void Agent::restore_network_manager() {
+    // The reference's Managed=false is runtime-only and left behind; this agent also persisted it
+    // in a keyfile, so undo both: after the policy is gone the NICs belong to the host again.
+    if (nm_keyfile_written_ && nm::remove_keyfile(cfg_.nm_keyfile_dir)) {
+        NLOG_I("Removed NetworkManager keyfile from %s", cfg_.nm_keyfile_dir.c_str());
+        nm_keyfile_written_ = false;
+    }
+    if (nm_unmanaged_.empty() || !cfg_.nm_restore) return;
+    try {
+        auto nmapi = nm_factory_();
+        nm::restore_for_interfaces(*nmapi, nm_unmanaged_);
+        nm_unmanaged_.clear();
+    } catch (const std::exception& e) {
+        NLOG_W("Could not hand the interfaces back to NetworkManager: %s", e.what());
+    }
 }
 
 std::vector<std::string> Agent::collect_interfaces() {
@@ -859,7 +877,10 @@ void Agent::run(int stop_fd) {
         if (!cfg_.nm_keyfile_dir.empty()) {
             try {
                 auto p = nm::write_keyfile(cfg_.nm_keyfile_dir, names);
-                if (!p.empty()) NLOG_I("Wrote NetworkManager keyfile %s", p.c_str());
+                if (!p.empty()) {
+                    NLOG_I("Wrote NetworkManager keyfile %s", p.c_str());
+                    nm_keyfile_written_ = true;
+                }
             } catch (const std::exception& e) {
                 NLOG_W("Could not write NetworkManager keyfile: %s", e.what());
             }
@@ -871,7 +892,7 @@ void Agent::run(int stop_fd) {
             throw AgentError(std::string("Failed to create NetworkManager: ") + e.what());
         }
         try {
-            nm::disable_for_interfaces(*nmapi, names);
+            nm_unmanaged_ = nm::disable_for_interfaces(*nmapi, names);
         } catch (const std::exception& e) {
             throw AgentError(std::string("Failed to disable interfaces in NetworkManager: ") + e.what());
         }

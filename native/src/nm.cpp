@@ -1,5 +1,7 @@
 #include "netop/nm.hpp"
 
+#include <unistd.h>
+
 #include <algorithm>
 
 #include "netop/common.hpp"
@@ -66,10 +68,38 @@ std::vector<std::string> disable_for_interfaces(NetworkManagerIf& nm, const std:
     return done;
 }
 
+static const char* const kKeyfileHeader = "# Written by the AMD network operator: scale-out NICs are configured by its agent.\n";
+static const char* const kKeyfileName = "99-amd-network-operator.conf";
+
+std::vector<std::string> restore_for_interfaces(NetworkManagerIf& nm, const std::vector<std::string>& ifaces) {
+    std::vector<std::string> done;
+    try {
+        nm.get_version();
+    } catch (const std::exception&) {
+        return done;  // NetworkManager gone meanwhile: nothing to give back
+    }
+    for (auto& dev : nm.get_all_devices()) {
+        std::string name = dev->get_interface();
+        if (std::find(ifaces.begin(), ifaces.end(), name) == ifaces.end()) continue;
+        dev->set_managed(true);
+        NLOG_I("Re-enabled NetworkManager for interface %s", name.c_str());
+        done.push_back(name);
+    }
+    return done;
+}
+
+bool remove_keyfile(const std::string& conf_dir) {
+    if (conf_dir.empty()) return false;
+    std::string path = path_join(conf_dir, kKeyfileName);
+    auto s = read_file(path);
+    if (!s || s->rfind(kKeyfileHeader, 0) != 0) return false;  // absent, or not written by us
+    return ::unlink(path.c_str()) == 0;
+}
+
 std::string keyfile_snippet(const std::vector<std::string>& ifaces) {
     std::vector<std::string> items;
     for (auto& i : ifaces) items.push_back("interface-name:" + i);
-    return "# Written by the AMD network operator: scale-out NICs are configured by its agent.\n"
+    return std::string(kKeyfileHeader) +
            "[keyfile]\n"
            "unmanaged-devices=" +
            join(items, ";") + "\n";
@@ -78,7 +108,7 @@ std::string keyfile_snippet(const std::vector<std::string>& ifaces) {
 std::string write_keyfile(const std::string& conf_dir, const std::vector<std::string>& ifaces) {
     if (ifaces.empty() || !is_dir(path_dirname(conf_dir))) return "";
     mkdir_p(conf_dir);
-    std::string path = path_join(conf_dir, "99-amd-network-operator.conf");
+    std::string path = path_join(conf_dir, kKeyfileName);
     write_file_atomic(path, keyfile_snippet(ifaces), 0644);
     return path;
 }

@@ -419,6 +419,41 @@ TEST(agent_networkmanager_paths) {
     CHECK_THROWS(b.run(-1));
 }
 
+TEST(agent_networkmanager_changes_undone_on_sigterm) {
+    Fixture f;
+    f.cfg.disable_nm = true;
+    f.cfg.nm_keyfile_dir = f.tmp.path + "/NetworkManager/conf.d";
+    f.tmp.mkdir("NetworkManager");
+    std::map<std::string, bool> seen;
+    Pipe stop;
+    stop.fire();  // SIGTERM pending: run() configures, publishes, then cleans up
+    agent::Agent a(f.cfg, f.ops, f.all_valid(), f.nm(&seen));
+    a.run(stop.fd[0]);
+    CHECK(a.ready());
+    // The persistent keyfile is gone and NetworkManager manages the NICs again.
+    CHECK(!path_exists(f.cfg.nm_keyfile_dir + "/99-amd-network-operator.conf"));
+    CHECK(seen["ens0"] && seen["ens1"] && seen["eth9"]);
+
+    // --nm-restore=false keeps the runtime change (reference behaviour), still drops the file.
+    Fixture g;
+    g.cfg.disable_nm = true;
+    g.cfg.nm_restore = false;
+    g.cfg.nm_keyfile_dir = g.tmp.path + "/NetworkManager/conf.d";
+    g.tmp.mkdir("NetworkManager");
+    std::map<std::string, bool> seen2;
+    Pipe stop2;
+    stop2.fire();
+    agent::Agent b(g.cfg, g.ops, g.all_valid(), g.nm(&seen2));
+    b.run(stop2.fd[0]);
+    CHECK(!path_exists(g.cfg.nm_keyfile_dir + "/99-amd-network-operator.conf"));
+    CHECK(!seen2["ens0"] && !seen2["ens1"] && seen2["eth9"]);
+
+    // A file of that name the agent did not write is never deleted.
+    g.tmp.write("NetworkManager/conf.d/99-amd-network-operator.conf", "[keyfile]\nunmanaged-devices=mac:aa\n");
+    CHECK(!nm::remove_keyfile(g.cfg.nm_keyfile_dir));
+    CHECK(path_exists(g.cfg.nm_keyfile_dir + "/99-amd-network-operator.conf"));
+}
+
 TEST(agent_stale_label_removed_and_networkd) {
     Fixture f;
     f.tmp.write("features.d/scale-out-readiness.txt", "stale\n");

@@ -66,7 +66,8 @@ int main(int argc, char** argv) {
                "L3: per-rail source routing; NIC k (its GPU index) gets routing table and rule priority base+k (0 = off)");
     fs.add_string("rccl-env-extra", &cfg.rccl_env_extra, "site settings appended to the RCCL environment file: KEY=VALUE[,...] (NCCL_*, RCCL_*, HSA_*)");
     fs.add_string("status-file", &cfg.status_file, "write a JSON status document (per-NIC results, phase timings)");
-    fs.add_string("nm-keyfile-dir", &cfg.nm_keyfile_dir, "with --disable-networkmanager, also persist an unmanaged-devices keyfile here");
+    fs.add_string("nm-keyfile-dir", &cfg.nm_keyfile_dir, "with --disable-networkmanager, also persist an unmanaged-devices keyfile here (removed on exit)");
+    fs.add_bool("nm-restore", &cfg.nm_restore, "with --disable-networkmanager: set the interfaces managed by NetworkManager again on exit");
     fs.add_int("xgmi-expect", &cfg.xgmi_expect_links, "verify the xGMI mesh before labelling: -1 off, 0 full mesh, N GPU pairs");
     fs.add_duration("link-wait", &cfg.link_wait_ns, "time to wait for link state echoes from the kernel");
     fs.add_duration("gid-wait", &cfg.gid_wait_ns, "time to wait for the RoCE v2 GID of a newly configured address");

@@ -1,19 +1,29 @@
-"""A fake system bus that impersonates NetworkManager, speaking the D-Bus wire protocol.
+"""NetworkManager over D-Bus for the agent's tests: a fake bus and a service on a real bus.
 
-Independent (Python) implementation of the protocol subset the agent's C++ client uses —
-SASL EXTERNAL, Hello, method calls / returns / errors, little-endian marshalling of
-s o g b u i y v a() — so the client is checked against a second implementation rather than
-against itself.  Replaces the reference's "needs a real system D-Bus" test
-(reference internal/nm/networkmanager_test.go:49-62).
+``FakeNetworkManagerBus`` is an independent Python implementation of the protocol subset the
+agent's C++ client uses. It covers SASL EXTERNAL, Hello, method calls / returns / errors, and
+little-endian marshalling of s o g b u i y v a(). It serves the client directly, as if it were
+the bus, so the client is checked against a second implementation rather than against itself.
+
+A second implementation by the same author can share a misreading of the specification. So
+``BusDaemon`` also starts the real reference implementation, ``dbus-daemon``, on a private
+socket. ``NetworkManagerOnBus`` then joins it as an ordinary client that owns
+``org.freedesktop.NetworkManager``. The agent's client has to authenticate to the real daemon and
+pass its message validation. Its calls are routed to the service with the daemon's sender and
+destination headers. This is the reference's "needs a real system D-Bus" test
+(reference internal/nm/networkmanager_test.go:49-62) without needing the host's bus.
 """
 
 from __future__ import annotations
 
 import os
+import shutil
 import socket
 import struct
+import subprocess
 import threading
-from typing import Dict, List, Tuple
+from pathlib import Path
+from typing import Dict, List, Optional, Tuple
 
 
 # ---------------------------------------------------------------------------
@@ -272,11 +282,14 @@ class FakeNetworkManagerBus:
             c.close()
 
     def _err(self, m, serial, name, text):
-        return encode(3, serial, {"reply_serial": m["serial"], "error_name": name}, "s", (text,))
+        # Through a real bus a reply must be addressed to the caller's unique name.
+        return encode(3, serial, {"reply_serial": m["serial"], "error_name": name, "destination": m.get("sender")},
+                      "s", (text,))
 
     def _handle(self, m, serial) -> bytes:
         self.calls.append((m.get("path", ""), m.get("interface", ""), m.get("member", "")))
-        ret = lambda sig="", body=(): encode(2, serial, {"reply_serial": m["serial"]}, sig, body)  # noqa: E731
+        ret = lambda sig="", body=(): encode(2, serial, {"reply_serial": m["serial"],  # noqa: E731
+                                                         "destination": m.get("sender")}, sig, body)
         member, iface, path = m.get("member"), m.get("interface"), m.get("path", "")
         if iface == "org.freedesktop.DBus" and member == "Hello":
             return ret("s", (":1.42",))
@@ -302,3 +315,146 @@ class FakeNetworkManagerBus:
                 self.devices[names[int(path.rsplit("/", 1)[1]) - 1]] = bool(val)
                 return ret()
         return self._err(m, serial, "org.freedesktop.DBus.Error.UnknownMethod", f"no method {iface}.{member}")
+
+
+class NetworkManagerOnBus(FakeNetworkManagerBus):
+    """Owns ``org.freedesktop.NetworkManager`` on a real bus (a client of ``dbus-daemon``) and
+    answers the same calls as ``FakeNetworkManagerBus``."""
+
+    def __init__(self, address: str, devices: Dict[str, bool], fail_set: bool = False):  # noqa: super not called
+        self.devices = dict(devices)
+        self.nm_running = True
+        self.fail_set = fail_set
+        self.calls: List[Tuple[str, str, str]] = []
+        self.auth_lines: List[str] = []
+        self._stop = False
+        path = address.split("unix:path=", 1)[1].split(",", 1)[0]
+        self._c = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
+        self._c.connect(path)
+        self._c.sendall(b"\0AUTH EXTERNAL " + str(os.getuid()).encode().hex().encode() + b"\r\n")
+        line = self._line()
+        if not line.startswith("OK "):
+            raise RuntimeError(f"dbus-daemon refused the service: {line}")
+        self._c.sendall(b"BEGIN\r\n")
+        self._buf = b""
+        self._serial = 0
+        self.unique_name = self._call("org.freedesktop.DBus", "/org/freedesktop/DBus", "org.freedesktop.DBus", "Hello")[0]
+        # flags 4 = DBUS_NAME_FLAG_DO_NOT_QUEUE; reply 1 = PRIMARY_OWNER
+        owner = self._call("org.freedesktop.DBus", "/org/freedesktop/DBus", "org.freedesktop.DBus", "RequestName",
+                           "su", (self.NM, 4))[0]
+        if owner != 1:
+            raise RuntimeError(f"could not own {self.NM}: RequestName -> {owner}")
+        self._thread = threading.Thread(target=self._loop, daemon=True)
+        self._thread.start()
+
+    @property
+    def address(self) -> str:  # the bus the agent must use is the daemon's, not ours
+        raise AttributeError("use BusDaemon.address")
+
+    def _line(self) -> str:
+        b = b""
+        while not b.endswith(b"\r\n"):
+            d = self._c.recv(1)
+            if not d:
+                raise RuntimeError("bus closed during authentication")
+            b += d
+        return b[:-2].decode()
+
+    def _read(self):
+        while True:
+            m, used = decode(self._buf)
+            if m is not None:
+                self._buf = self._buf[used:]
+                return m
+            d = self._c.recv(65536)
+            if not d:
+                return None
+            self._buf += d
+
+    def _call(self, dest, path, iface, member, sig="", body=()):
+        self._serial += 1
+        self._c.sendall(encode(1, self._serial, {"path": path, "interface": iface, "member": member,
+                                                 "destination": dest}, sig, body))
+        while True:
+            m = self._read()
+            if m is None:
+                raise RuntimeError("bus closed")
+            if m["type"] in (2, 3) and m.get("reply_serial") == self._serial:
+                if m["type"] == 3:
+                    raise RuntimeError(f"{m.get('error_name')}: {m['body']}")
+                return m["body"]
+
+    def _loop(self):
+        serial = 5000
+        try:
+            while not self._stop:
+                m = self._read()
+                if m is None:
+                    return
+                if m["type"] != 1:  # signals (NameAcquired, ...) and stray replies
+                    continue
+                serial += 1
+                self._c.sendall(self._handle(m, serial))
+        except OSError:
+            return
+
+    def stop(self):
+        self._stop = True
+        try:
+            self._c.shutdown(socket.SHUT_RDWR)
+            self._c.close()
+        except OSError:
+            pass
+
+
+class BusDaemon:
+    """A private ``dbus-daemon`` (freedesktop's reference bus) on a UNIX socket under ``tmpdir``."""
+
+    CONFIG = """<!DOCTYPE busconfig PUBLIC "-//freedesktop//DTD D-Bus Bus Configuration 1.0//EN"
+ "http://www.freedesktop.org/standards/dbus/1.0/busconfig.dtd">
+<busconfig>
+  <type>system</type>
+  <listen>unix:path={path}</listen>
+  <auth>EXTERNAL</auth>
+  <policy context="default">
+    <allow user="*"/>
+    <allow own="*"/>
+    <allow send_type="method_call"/>
+    <allow receive_type="method_call"/>
+    <allow send_destination="*"/>
+    <allow receive_type="method_return"/>
+    <allow receive_type="error"/>
+    <allow receive_type="signal"/>
+  </policy>
+</busconfig>
+"""
+
+    @staticmethod
+    def available() -> Optional[str]:
+        return shutil.which("dbus-daemon")
+
+    def __init__(self, tmpdir: str):
+        exe = self.available()
+        if not exe:
+            raise FileNotFoundError("dbus-daemon not installed")
+        d = Path(tmpdir)
+        self.socket_path = str(d / "system_bus_socket")
+        conf = d / "bus.conf"
+        conf.write_text(self.CONFIG.format(path=self.socket_path))
+        self.proc = subprocess.Popen([exe, f"--config-file={conf}", "--nofork", "--nopidfile", "--print-address"],
+                                     stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+        line = self.proc.stdout.readline().strip()
+        if not line.startswith("unix:"):
+            err = self.proc.stderr.read() if self.proc.poll() is not None else ""
+            self.stop()
+            raise RuntimeError(f"dbus-daemon did not start: {line!r} {err}")
+        self.address = line
+
+    def stop(self):
+        if self.proc.poll() is None:
+            self.proc.terminate()
+            try:
+                self.proc.wait(5)
+            except subprocess.TimeoutExpired:
+                self.proc.kill()
+                self.proc.wait()

@@ -168,8 +168,12 @@ def run_scenario(n_nics: int = 8, mode: str = "L3", seed: int | None = None, int
                  xgmi_expect: int = 0, keep_tmp: bool = False, sigterm: bool = True, verbose: int = 2,
                  drop_xgmi: list | None = None, extra_args: list | None = None, flap_port: int | None = None,
                  crash_restart: bool = False, crash_after_s: float = 0.0, gid_delay_s: float = 0.0,
-                 egress_probe: bool = False) -> dict:
-    """Runs one node bring-up.  Must already be inside a private user+net namespace."""
+                 egress_probe: bool = False, nm_bus: bool = False) -> dict:
+    """Runs one node bring-up.  Must already be inside a private user+net namespace.
+
+    nm_bus: run the agent with --disable-networkmanager against a real ``dbus-daemon`` on which a
+    NetworkManager stand-in owns the name (testing/fakedbus.py), with an NM keyfile directory,
+    and record both before and after SIGTERM."""
     from . import fakesysfs
 
     nat = _native()
@@ -268,6 +272,17 @@ def run_scenario(n_nics: int = 8, mode: str = "L3", seed: int | None = None, int
                 f"--pipeline={'true' if pipeline else 'false'}", f"--lldp-announce={'true' if announce else 'false'}",
                 f"--systemd-networkd={tmp / 'networkd'}", f"-v={verbose}", *(extra_args or [])]
         env = dict(os.environ, SYSFS_ROOT=str(tmp / "sys"), NODE_NAME="mi355x-node-0")
+        bus = nm = None
+        keyfile = tmp / "NetworkManager" / "conf.d" / "99-amd-network-operator.conf"
+        if nm_bus:
+            from .fakedbus import BusDaemon, NetworkManagerOnBus
+
+            (tmp / "dbus").mkdir()
+            (tmp / "NetworkManager").mkdir()
+            bus = BusDaemon(str(tmp / "dbus"))
+            nm = NetworkManagerOnBus(bus.address, {**{n: True for n in nic_names}, "eth9": True})
+            env["DBUS_SYSTEM_BUS_ADDRESS"] = bus.address
+            args += ["--disable-networkmanager", f"--nm-keyfile-dir={keyfile.parent}"]
         t0 = time.monotonic()
         agent = subprocess.Popen(args, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
         budget = 5.0 + float(wait.rstrip("s"))
@@ -313,6 +328,9 @@ def run_scenario(n_nics: int = 8, mode: str = "L3", seed: int | None = None, int
         res["rccl_env"] = (tmp / "rccl.env").read_text() if (tmp / "rccl.env").exists() else None
         res["rccl_topo"] = (tmp / "rccl-topo.xml").read_text() if (tmp / "rccl-topo.xml").exists() else None
         res["label"] = label.read_text() if label.exists() else None
+        if nm is not None:
+            res["nm_keyfile_while_ready"] = keyfile.read_text() if keyfile.exists() else None
+            res["nm_managed_while_ready"] = dict(nm.devices)
         res["networkd_files"] = sorted(os.listdir(tmp / "networkd")) if (tmp / "networkd").exists() else []
         if crash_restart and t_ready:
             # The agent dies without cleaning up (OOM kill, node agent crash): the label, the
@@ -372,6 +390,11 @@ def run_scenario(n_nics: int = 8, mode: str = "L3", seed: int | None = None, int
         res["after_sigterm"] = after
         res["rules_after_sigterm"] = [r for r in rt.rule_list() if 0 < r["priority"] < 32766]
         res["label_after_sigterm"] = label.exists()
+        if nm is not None:
+            res["nm_keyfile_after_sigterm"] = keyfile.exists()
+            res["nm_managed_after_sigterm"] = dict(nm.devices)
+            nm.stop()
+            bus.stop()
         os.kill(pid, signal.SIGTERM)
         os.waitpid(pid, 0)
         res["switch_start_offset_s"] = t0 - t_switch

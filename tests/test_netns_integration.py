@@ -232,3 +232,20 @@ def test_without_rail_tables_sources_share_one_egress():
     _check_configured(r)
     busiest = [max(range(len(row)), key=row.__getitem__) for row in r["egress"]]
     assert len(set(busiest)) == 1 and all(row[busiest[0]] >= 20 for row in r["egress"]), r["egress"]
+
+
+def test_networkmanager_unmanaged_while_ready_and_handed_back_on_sigterm():
+    """--disable-networkmanager through a real dbus-daemon: the NICs are unmanaged (runtime
+    Managed=false + the persistent keyfile) while the node is ready; SIGTERM (policy deleted)
+    removes the keyfile and hands the NICs back (the reference leaves Managed=false behind,
+    reference cmd/discover/main.go:143-159)."""
+    from network_operator_amd.testing.fakedbus import BusDaemon
+
+    if not BusDaemon.available():
+        pytest.skip("dbus-daemon not installed")
+    r = netns.run_isolated(n_nics=4, seed=5, interval="30s", fast_start=True, nm_bus=True)
+    assert r["label"] and r["agent_rc"] == 0
+    assert "unmanaged-devices=" + ";".join(f"interface-name:{n}" for n in r["nics"]) in r["nm_keyfile_while_ready"]
+    assert r["nm_managed_while_ready"] == {**{n: False for n in r["nics"]}, "eth9": True}
+    assert r["nm_keyfile_after_sigterm"] is False
+    assert r["nm_managed_after_sigterm"] == {**{n: True for n in r["nics"]}, "eth9": True}
