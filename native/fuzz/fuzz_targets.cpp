@@ -61,6 +61,13 @@ extern "C" int LLVMFuzzerTestOneInput(const uint8_t* data, size_t size) {
         (void)nl::parse_link(h);
     } catch (const std::exception&) {
     }
+    // The same bytes as an extended-ACK error (nlmsgerr + echoed request + attributes), both with
+    // and without the capped echo.
+    h->nlmsg_type = NLMSG_ERROR;
+    for (uint16_t flags : {uint16_t(NLM_F_ACK_TLVS), uint16_t(NLM_F_ACK_TLVS | NLM_F_CAPPED)}) {
+        h->nlmsg_flags = flags;
+        (void)nl::ext_ack_msg(h);
+    }
 #else
 #error "define NETOP_FUZZ_TARGET"
 #endif

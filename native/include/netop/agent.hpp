@@ -91,13 +91,19 @@ struct Config {
     bool disable_fw_lldp = false;
     std::string fw_lldp_flags;                        // extra rules "NAME=0|1,..."
     std::string rccl_env_extra;                       // "KEY=VALUE,..." appended to rccl.env
-    // Per-rail source routing (L3): NIC k gets routing table base+k (k = its GPU index) holding
-    // its /30 and its /16 via the switch, and a rule "from <local>/32 lookup base+k" at
-    // priority base+k.  Traffic sourced from a rail's address then leaves through that rail
-    // even though every rail's /16 route is also in the main table.  0 = off (the reference's
-    // main-table-only routing).
+    // Per-rail source routing (L3): NIC k gets routing table base+k (k = its GPU index; NICs
+    // without a GPU get the indices after the last GPU's) holding its /30 and its /16 via the
+    // switch, and a rule "from <local>/32 lookup base+k" at priority base+k.  Traffic sourced
+    // from a rail's address then leaves through that rail even though every rail's /16 route is
+    // also in the main table.  Tables and priorities base..base+N-1 are reserved for the agent;
+    // its rules and routes carry protocol kRailProtocol and it never deletes any other.  0 = off
+    // (the reference's main-table-only routing).
     int rail_table_base = 0;
 };
+
+// FRA_PROTOCOL / rtm_protocol tag on the agent's rail rules and rail-table routes ("installed by
+// the AMD network operator"): cleanup only ever removes rules and routes carrying it.
+constexpr uint8_t kRailProtocol = 0xa3;
 
 // Sanitises in place (MTU clamp to [1500, 9000], mode upper-cased); throws on a bad mode.
 void sanitize(Config& c);
@@ -160,6 +166,7 @@ class Agent {
     void remove_existing_ips();
     bool configure_interface(NicState& n);
     int configure_all();  // returns number configured
+    void assign_rail_indices();
 
    private:
     void pre_cleanups();
@@ -171,7 +178,8 @@ class Agent {
     void add_route(NicState& n, int mask);
     uint32_t rail_table(const NicState& n) const;
     void add_rail_routing(NicState& n);
-    void remove_rail_routing();
+    void remove_rail_routing(NicState& n);  // what was installed for n
+    void remove_rail_routing();             // every NIC's
     void write_artifacts();
     void write_l2_artifacts();
     void write_rccl_env_file();

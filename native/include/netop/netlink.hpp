@@ -68,8 +68,11 @@ struct RuleSpec {
     Ipv4Prefix src{};
     uint32_t table = 0;
     uint32_t priority = 0;
+    // FRA_PROTOCOL (Linux >= 4.17): who installed the rule.  0 = unspecified (matches any on
+    // delete).  The agent tags its rail rules so it only ever removes rules it added.
+    uint8_t protocol = 0;
     bool operator==(const RuleSpec& o) const {
-        return src.masked() == o.src.masked() && table == o.table && priority == o.priority;
+        return src.masked() == o.src.masked() && table == o.table && priority == o.priority && protocol == o.protocol;
     }
     std::string str() const;
 };
@@ -103,6 +106,8 @@ class NetOps {
     virtual void rule_add(const RuleSpec& r) = 0;
     virtual void rule_del(const RuleSpec& r) = 0;
     virtual std::vector<RuleSpec> rule_list() = 0;
+    // IPv4 routes of one table (0 = every table).
+    virtual std::vector<RouteSpec> route_list(uint8_t table) = 0;
     virtual void link_set_up(int ifindex) = 0;
     virtual void link_set_down(int ifindex) = 0;
     virtual void link_set_mtu(int ifindex, int mtu) = 0;
@@ -133,7 +138,7 @@ class Rtnl final : public NetOps {
     // Extra operations (harness / diagnostics; not part of the injectable table).
     LinkInfo link_by_index(int ifindex);
     std::vector<LinkInfo> link_list();
-    std::vector<RouteInfo> route_list(uint8_t table = RT_TABLE_MAIN);
+    std::vector<RouteInfo> route_list(uint8_t table = RT_TABLE_MAIN) override;
     void veth_add(const std::string& name, const std::string& peer);
     void link_del(int ifindex);
     void link_set_netns_fd(int ifindex, int netns_fd);
@@ -159,5 +164,8 @@ class Rtnl final : public NetOps {
 
 // Parses an RTM_NEWLINK/RTM_DELLINK payload.
 LinkInfo parse_link(const nlmsghdr* h);
+// The NLMSGERR_ATTR_MSG string of an extended ACK (NLMSG_ERROR with NLM_F_ACK_TLVS); "" if
+// absent.  `h->nlmsg_len` bytes must be readable; every inner length is bounds-checked.
+std::string ext_ack_msg(const nlmsghdr* h);
 
 }  // namespace netop::nl

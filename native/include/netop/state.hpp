@@ -8,6 +8,7 @@
 #include <cstdint>
 #include <optional>
 #include <string>
+#include <vector>
 
 #include "netop/common.hpp"
 #include "netop/l3.hpp"
@@ -42,6 +43,11 @@ struct NicState {
     std::optional<int> gid_index;
     int numa_node = -1;     // NUMA node of the GPU (pin the rank's CPU threads there)
     std::string pcie_path;  // GPU <-> NIC PCIe path type (PIX / PXB / ...)
+    // Per-rail source routing: this NIC's rail k (its GPU index; NICs without a GPU get indices
+    // above every GPU's) and what the agent installed for it, so exactly that is removed later.
+    int rail_index = -1;
+    std::optional<nl::RuleSpec> rail_rule;
+    std::vector<nl::RouteSpec> rail_routes;
 
     // NIC firmware LLDP agent (--disable-fw-lldp): summary of what was done
     std::string fw_lldp;

@@ -155,6 +155,7 @@ PYBIND11_MODULE(_netop_native, m) {
                 d["src"] = x.src.masked().str();
                 d["table"] = x.table;
                 d["priority"] = x.priority;
+                d["protocol"] = x.protocol;
                 l.append(d);
             }
             return l;

@@ -9,6 +9,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <set>
 
 #include "netop/log.hpp"
 
@@ -231,6 +232,7 @@ void Agent::get_network_configs(const std::vector<std::string>& names) {
                 }
         nics_.push_back(std::move(n));
     }
+    assign_rail_indices();
 }
 
 void Agent::interfaces_up() {
@@ -360,77 +362,101 @@ void Agent::add_route(NicState& n, int mask) {
     }
 }
 
-uint32_t Agent::rail_table(const NicState& n) const {
-    int k = n.gpu_index >= 0 ? n.gpu_index : int(&n - nics_.data());
-    return uint32_t(cfg_.rail_table_base + k);
+uint32_t Agent::rail_table(const NicState& n) const { return uint32_t(cfg_.rail_table_base + n.rail_index); }
+
+void Agent::assign_rail_indices() {
+    // GPU-paired NICs keep their GPU index; the others (extra --interfaces, a GPU without a NIC
+    // in reach) follow the highest GPU index, so no two NICs ever share a table.
+    int next = -1;
+    std::set<int> used;
+    for (auto& n : nics_)
+        if (n.gpu_index >= 0 && used.insert(n.gpu_index).second) {
+            n.rail_index = n.gpu_index;
+            next = std::max(next, n.gpu_index);
+        } else {
+            n.rail_index = -1;
+        }
+    for (auto& n : nics_)
+        if (n.rail_index < 0) n.rail_index = ++next;
 }
 
 void Agent::add_rail_routing(NicState& n) {
     const uint32_t t = rail_table(n);
-    nl::RuleSpec rule{Ipv4Prefix{n.addr->local, 32}, t, t};
-    // A previous address of this rail (agent restart, Port Description change): its rule and
-    // its table's routes go first, so the table only ever describes the current /30.
+    nl::RuleSpec rule{Ipv4Prefix{n.addr->local, 32}, t, t, kRailProtocol};
+    // What this agent installed for an earlier address of this rail (Port Description change).
+    if (n.rail_rule && !(*n.rail_rule == rule)) remove_rail_routing(n);
+    // Leftovers of an earlier agent run (crash, restart with another NIC set): only rules and
+    // routes tagged with our protocol, and only for this rail's table / priority.
     for (const auto& r : ops_.rule_list())
-        if ((r.priority == t || r.table == t) && !(r == rule)) ops_.rule_del(r);
-    for (int mask : {l3::kRoutedNetworkMask, l3::kPointToPointMask}) {
-        for (int i = 0; i < 8; ++i) {  // RTM_DELROUTE without a gateway takes the first match
-            nl::RouteSpec old;
-            old.table = uint8_t(t);
-            old.dst = Ipv4Prefix{n.addr->local, mask}.masked();
+        if (r.protocol == kRailProtocol && (r.table == t || r.priority == t) && !(r == rule)) {
             try {
-                ops_.route_del(old);
-            } catch (const SysError&) {
-                break;
+                ops_.rule_del(r);
+            } catch (const SysError& e) {
+                if (e.code() != ENOENT) throw;
             }
         }
-    }
     nl::RouteSpec p2p;
     p2p.ifindex = n.link.index;
     p2p.dst = n.addr->local_prefix().masked();
     p2p.scope = RT_SCOPE_LINK;
     p2p.prefsrc = n.addr->local;
     p2p.table = uint8_t(t);
+    p2p.protocol = kRailProtocol;
     nl::RouteSpec routed;
     routed.ifindex = n.link.index;
     routed.dst = Ipv4Prefix{n.addr->local, l3::kRoutedNetworkMask}.masked();
     routed.gateway = n.addr->peer;
     routed.prefsrc = n.addr->local;
     routed.table = uint8_t(t);
+    routed.protocol = kRailProtocol;
+    auto same = [](const nl::RouteSpec& a, const nl::RouteSpec& b) {
+        return a.dst.masked() == b.dst.masked() && a.gateway == b.gateway && a.ifindex == b.ifindex;
+    };
+    for (const auto& r : ops_.route_list(uint8_t(t))) {
+        if (r.protocol != kRailProtocol || same(r, p2p) || same(r, routed)) continue;
+        try {
+            ops_.route_del(r);
+        } catch (const SysError&) {
+        }
+    }
+    n.rail_routes.clear();
     for (const auto& r : {p2p, routed}) {
         try {
             ops_.route_append(r);
         } catch (const SysError& e) {
             if (e.code() != EEXIST) throw;
         }
+        n.rail_routes.push_back(r);
     }
     try {
         ops_.rule_add(rule);
     } catch (const SysError& e) {
         if (e.code() != EEXIST) throw;
     }
+    n.rail_rule = rule;
     NLOG_V(3, "Rail routing for '%s': table %u, rule %s", n.ifname.c_str(), t, rule.str().c_str());
 }
 
-void Agent::remove_rail_routing() {
-    if (cfg_.rail_table_base <= 0) return;
-    for (auto& n : nics_) {
-        if (!n.addr) continue;
-        const uint32_t t = rail_table(n);
+void Agent::remove_rail_routing(NicState& n) {
+    if (n.rail_rule) {
         try {
-            ops_.rule_del(nl::RuleSpec{Ipv4Prefix{n.addr->local, 32}, t, t});
+            ops_.rule_del(*n.rail_rule);
         } catch (const SysError& e) {
             if (e.code() != ENOENT) NLOG_W("Could not remove the rail rule of '%s': %s", n.ifname.c_str(), e.what());
         }
-        for (int mask : {l3::kRoutedNetworkMask, l3::kPointToPointMask}) {
-            nl::RouteSpec r;
-            r.table = uint8_t(t);
-            r.dst = Ipv4Prefix{n.addr->local, mask}.masked();
-            try {
-                ops_.route_del(r);
-            } catch (...) {  // already gone with the address / link
-            }
+        n.rail_rule.reset();
+    }
+    for (const auto& r : n.rail_routes) {
+        try {
+            ops_.route_del(r);
+        } catch (...) {  // already gone with the address / link
         }
     }
+    n.rail_routes.clear();
+}
+
+void Agent::remove_rail_routing() {
+    for (auto& n : nics_) remove_rail_routing(n);
 }
 
 bool Agent::configure_interface(NicState& n) {
@@ -1059,7 +1085,9 @@ void Agent::monitor(int stop_fd) {
                 auto old = n.addr;
                 on_lldp(n, f);
                 if (n.addr && old && n.addr->local == old->local) continue;
-                // drop the old address (its /30 and /16 routes go with it), configure the new one
+                // drop the old address (its /30 and /16 routes go with it) and the rail rule and
+                // routes installed for it, then configure the new one
+                remove_rail_routing(n);
                 try {
                     for (auto& a : ops_.addr_list(n.link.index, AF_INET)) ops_.addr_del(a);
                 } catch (const std::exception& e) {

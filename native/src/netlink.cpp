@@ -150,18 +150,29 @@ Rtnl::~Rtnl() {
     if (fd_ >= 0) ::close(fd_);
 }
 
-static std::string ext_ack_msg(const nlmsghdr* h) {
-    if (!(h->nlmsg_flags & NLM_F_ACK_TLVS)) return {};
+std::string ext_ack_msg(const nlmsghdr* h) {
+    // Extended ACK (NLM_F_ACK_TLVS): nlmsgerr, then the echoed request (unless NLM_F_CAPPED),
+    // then attributes.  Every length comes from the peer, so each is checked against the bytes
+    // the message actually has before it is used.
+    if (h->nlmsg_len < NLMSG_LENGTH(sizeof(nlmsgerr)) || !(h->nlmsg_flags & NLM_F_ACK_TLVS)) return {};
     const auto* err = reinterpret_cast<const nlmsgerr*>(NLMSG_DATA(h));
     size_t off = NLMSG_HDRLEN + sizeof(nlmsgerr);
-    if (!(h->nlmsg_flags & NLM_F_CAPPED)) off += err->msg.nlmsg_len - sizeof(nlmsghdr);
+    if (!(h->nlmsg_flags & NLM_F_CAPPED)) {
+        if (err->msg.nlmsg_len < sizeof(nlmsghdr)) return {};
+        off += err->msg.nlmsg_len - sizeof(nlmsghdr);
+    }
+    off = NLMSG_ALIGN(off);  // the kernel pads the echoed request; a peer might not: copy, never cast
+    const size_t end = h->nlmsg_len;
     const auto* base = reinterpret_cast<const uint8_t*>(h);
-    while (off + sizeof(rtattr) <= h->nlmsg_len) {
-        const auto* a = reinterpret_cast<const rtattr*>(base + off);
-        if (a->rta_len < sizeof(rtattr)) break;
-        if (a->rta_type == 1 /* NLMSGERR_ATTR_MSG */)
-            return std::string(reinterpret_cast<const char*>(RTA_DATA(a)), strnlen(reinterpret_cast<const char*>(RTA_DATA(a)), RTA_PAYLOAD(a)));
-        off += RTA_ALIGN(a->rta_len);
+    while (off <= end && end - off >= sizeof(rtattr)) {
+        rtattr a;
+        std::memcpy(&a, base + off, sizeof a);
+        if (a.rta_len < sizeof(rtattr) || a.rta_len > end - off) break;
+        if (a.rta_type == 1 /* NLMSGERR_ATTR_MSG */) {
+            const char* s = reinterpret_cast<const char*>(base + off + RTA_LENGTH(0));
+            return std::string(s, strnlen(s, a.rta_len - RTA_LENGTH(0)));
+        }
+        off += RTA_ALIGN(a.rta_len);
     }
     return {};
 }
@@ -530,6 +541,7 @@ namespace {
 // FIB rule messages: struct fib_rule_hdr (linux/fib_rules.h) shares rtmsg's layout for the
 // fields used here (family, dst_len, src_len, tos, table, res1, res2, action, flags).
 constexpr uint16_t kFraSrc = 2, kFraPriority = 6, kFraTable = 15;  // FRA_SRC, FRA_PRIORITY, FRA_TABLE
+constexpr uint16_t kFraProtocol = 21;                               // FRA_PROTOCOL (u8)
 constexpr uint8_t kFrActToTbl = 1;                                  // FR_ACT_TO_TBL
 struct FibRuleHdr {
     uint8_t family, dst_len, src_len, tos, table, res1, res2, action;
@@ -548,6 +560,7 @@ void Rtnl::rule_request(uint16_t type, uint16_t flags, const RuleSpec& r) {
     if (r.src.len) m.attr_ip(kFraSrc, r.src.network());
     m.attr_u32(kFraTable, r.table);
     if (r.priority) m.attr_u32(kFraPriority, r.priority);
+    if (r.protocol) m.attr(kFraProtocol, &r.protocol, 1);
     transact(m, nullptr);
 }
 
@@ -572,6 +585,7 @@ std::vector<RuleSpec> Rtnl::rule_list() {
             if (a->rta_type == kFraSrc && RTA_PAYLOAD(a) == 4) r.src.addr = Ipv4::from_net(RTA_DATA(a));
             if (a->rta_type == kFraPriority && RTA_PAYLOAD(a) >= 4) std::memcpy(&r.priority, RTA_DATA(a), 4);
             if (a->rta_type == kFraTable && RTA_PAYLOAD(a) >= 4) std::memcpy(&r.table, RTA_DATA(a), 4);
+            if (a->rta_type == kFraProtocol && RTA_PAYLOAD(a) >= 1) r.protocol = *static_cast<const uint8_t*>(RTA_DATA(a));
         });
         out.push_back(r);
     });

@@ -118,6 +118,13 @@ struct FakeNetOps : netop::nl::NetOps {
         maybe_fail("rule_list");
         return rules;
     }
+    std::vector<netop::nl::RouteSpec> route_list(uint8_t table) override {
+        maybe_fail("route_list");
+        std::vector<netop::nl::RouteSpec> out;
+        for (auto& r : routes)
+            if (!table || r.table == table) out.push_back(r);
+        return out;
+    }
     void set_flag(int ifindex, bool up) {
         auto* l = by_index(ifindex);
         if (!l) throw netop::SysError(ENODEV, "no link");

@@ -170,7 +170,11 @@ TEST(agent_rail_tables_route_each_source_through_its_nic) {
     Fixture f;
     f.cfg.keep_running = false;
     f.cfg.rail_table_base = 100;
-    f.ops.rules.push_back(nl::RuleSpec{*Ipv4Prefix::parse("10.9.9.9/32"), 100, 100});  // a previous run's address
+    // A previous run's rule for rail 0 (tagged with the agent's protocol) and a host rule that
+    // happens to use priority 101 and table 100 (not the agent's: must survive).
+    f.ops.rules.push_back(nl::RuleSpec{*Ipv4Prefix::parse("10.9.9.9/32"), 100, 100, agent::kRailProtocol});
+    const nl::RuleSpec foreign{*Ipv4Prefix::parse("192.168.5.0/24"), 100, 101};
+    f.ops.rules.push_back(foreign);
     agent::Agent a(f.cfg, f.ops, f.all_valid(), f.nm());
     a.run(-1);
     // main table unchanged (the reference's routes), plus one table per rail
@@ -180,10 +184,52 @@ TEST(agent_rail_tables_route_each_source_through_its_nic) {
     CHECK(has_table_route(f.ops, 11, "10.200.0.4/30", nullptr, 101));
     CHECK(has_table_route(f.ops, 11, "10.200.0.0/16", "10.200.0.6", 101));
     CHECK(has_table_route(f.ops, 12, "10.200.0.0/16", "10.200.0.9", 102));
-    CHECK_EQ(f.ops.rules.size(), size_t(3));  // the stale rule of table 100 is gone
-    CHECK(f.ops.rules[0] == (nl::RuleSpec{*Ipv4Prefix::parse("10.200.0.1/32"), 100, 100}));
-    CHECK(f.ops.rules[2] == (nl::RuleSpec{*Ipv4Prefix::parse("10.200.0.10/32"), 102, 102}));
+    CHECK_EQ(f.ops.rules.size(), size_t(4));  // the agent's stale rule of table 100 is gone, the host's stays
+    CHECK(f.ops.rules[0] == foreign);
+    CHECK(f.ops.rules[1] == (nl::RuleSpec{*Ipv4Prefix::parse("10.200.0.1/32"), 100, 100, agent::kRailProtocol}));
+    CHECK(f.ops.rules[3] == (nl::RuleSpec{*Ipv4Prefix::parse("10.200.0.10/32"), 102, 102, agent::kRailProtocol}));
+    for (auto& r : f.ops.routes)
+        if (r.table >= 100 && r.table <= 102) CHECK_EQ(int(r.protocol), int(agent::kRailProtocol));
     CHECK(a.nics()[1].configured);
+}
+
+TEST(agent_rail_indices_unique_with_unpaired_nics) {
+    // Paired NICs keep their GPU index; NICs without a GPU (extra --interfaces, a GPU with no
+    // NIC in reach) take the indices after the highest GPU's: no two rails share a table.
+    Fixture f;
+    agent::Agent a(f.cfg, f.ops, f.all_valid(), f.nm());
+    a.nics_.resize(5);
+    int gpu[] = {3, -1, 0, -1, 1};
+    for (int i = 0; i < 5; ++i) a.nics_[size_t(i)].gpu_index = gpu[i];
+    a.assign_rail_indices();
+    std::vector<int> got;
+    for (auto& n : a.nics_) got.push_back(n.rail_index);
+    CHECK((got == std::vector<int>{3, 4, 0, 5, 1}));
+}
+
+TEST(agent_rail_routing_removed_with_the_address_it_was_installed_for) {
+    // A Port Description change that yields no usable address: the old rail rule (built from the
+    // old address) must still be removed -- from the record, not from n.addr.
+    Fixture f;
+    f.cfg.monitor_tick_ns = 1000000;
+    f.cfg.rail_table_base = 100;
+    Pipe stop;
+    auto src = f.all_valid();
+    ScriptedLldp* raw = src.get();
+    agent::Agent a(f.cfg, f.ops, std::move(src), f.nm());
+    bool gone = false;
+    a.on_monitor_tick = [&](int tick) {
+        if (tick == 1) raw->frames["ens1"] = sw("02:aa:00:00:00:01", "no-alert not-an-address");
+        if (tick == 3) {
+            gone = true;
+            for (auto& r : f.ops.rules) gone &= r.src.addr.str() != "10.200.0.5";
+            for (auto& r : f.ops.routes) gone &= r.table != 101;
+            stop.fire();
+        }
+    };
+    a.run(stop.fd[0]);
+    CHECK(gone);
+    CHECK(f.ops.rules.empty());
 }
 
 TEST(agent_rail_tables_removed_on_sigterm) {
@@ -578,7 +624,7 @@ TEST(agent_monitor_rail_tables_follow_flaps_and_readdressing) {
         } else if (tick == 6) {
             bool new_rule = false, old_rule = false;
             for (auto& r : f.ops.rules) {
-                new_rule |= r == nl::RuleSpec{*Ipv4Prefix::parse("10.201.7.1/32"), 101, 101};
+                new_rule |= r == nl::RuleSpec{*Ipv4Prefix::parse("10.201.7.1/32"), 101, 101, agent::kRailProtocol};
                 old_rule |= r.src.addr.str() == "10.200.0.5";
             }
             moved = new_rule && !old_rule && has_table_route(f.ops, 11, "10.201.0.0/16", "10.201.7.2", 101);

@@ -213,6 +213,9 @@ def test_rail_tables_in_the_kernel():
         assert row[k] >= 20 and max(x for j, x in enumerate(row) if j != k) <= 5, r["egress"]
     rules = sorted(r["rules"], key=lambda x: x["priority"])
     assert [x["priority"] for x in rules] == [100, 101, 102], rules
+    # Tagged (FRA_PROTOCOL) so cleanup can tell the agent's rules and routes from the host's.
+    assert {x["protocol"] for x in rules} == {0xa3}, rules
+    assert all(x["protocol"] == 0xa3 for t in r["rail_tables"].values() for x in t), r["rail_tables"]
     by_src = {x["src"]: x["table"] for x in rules}
     for nic, p in zip(r["nics"], r["plan"]):
         table = by_src[p["local"] + "/32"]
