@@ -11,7 +11,7 @@ BUNDLE_IMG ?= amd/amd-network-operator-bundle:v$(VERSION)
 
 .PHONY: all help build native hip test test-native test-netns test-gpu manifests deployments bench bench-node-ready \
         images sanitize tsan clean fmt vet lint fuzz run build-installer install uninstall deploy undeploy bundle \
-        bundle-build helm-package-chart fuzz-native
+        bundle-build helm-package-chart fuzz-native check-hardening catalog-build catalog-push bundle-push
 
 all: build
 
@@ -32,6 +32,9 @@ test:                       ## everything that runs without a GPU
 
 test-native:
 	network_operator_amd/_lib/bin/netop-unit-tests
+
+check-hardening:            ## PIE / full RELRO / NX stack / stack protector / FORTIFY on the agent binaries (checksec gate)
+	$(PYTHON) tools/check_hardening.py network_operator_amd/_lib/bin/discover network_operator_amd/_lib/bin/netop-topo network_operator_amd/_lib/bin/netop-lldp-tx
 
 test-netns:                 ## veth + synthetic-switch integration (root or user namespaces)
 	$(PYTHON) -m pytest tests/test_netns_integration.py -q
@@ -106,6 +109,24 @@ bundle:                     ## OLM bundle (bundle/manifests, bundle/metadata, bu
 
 bundle-build: bundle        ## build the OLM bundle image
 	docker build -f bundle.Dockerfile -t $(BUNDLE_IMG) .
+
+bundle-push:                ## push the OLM bundle image
+	docker push $(BUNDLE_IMG)
+
+# OLM catalog (file-based catalog index) from the bundle image(s); needs `opm` on PATH
+# (the reference downloads it, Makefile:300-335; there is no network here, so bring your own).
+OPM ?= opm
+CATALOG_IMG ?= amd/amd-network-operator-catalog:v$(VERSION)
+BUNDLE_IMGS ?= $(BUNDLE_IMG)
+ifneq ($(origin CATALOG_BASE_IMG), undefined)
+FROM_INDEX_OPT := --from-index $(CATALOG_BASE_IMG)
+endif
+
+catalog-build:              ## build a catalog image containing $(BUNDLE_IMGS) (opm index add)
+	$(OPM) index add --container-tool docker --mode semver --tag $(CATALOG_IMG) --bundles $(BUNDLE_IMGS) $(FROM_INDEX_OPT)
+
+catalog-push:               ## push the catalog image
+	docker push $(CATALOG_IMG)
 
 helm-package-chart:         ## .charts/<chart>-<version>.tgz
 	$(PYTHON) -m network_operator_amd.packaging helm --out .charts
