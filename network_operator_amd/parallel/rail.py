@@ -49,30 +49,42 @@ def read_env_file(path: str) -> Dict[str, str]:
 
 
 def rail_env(gpu_bdf: Optional[str] = None, gpu_index: Optional[int] = None,
-             artifact_dir: str = ARTIFACT_DIR) -> Dict[str, str]:
+             artifact_dir: str = ARTIFACT_DIR, sysfs_root: str = "/sys/") -> Dict[str, str]:
     """RCCL settings that pin this rank's cross-node traffic to its own rail: the node-wide
     ``rccl.env`` with ``NCCL_IB_HCA`` narrowed to the RDMA device of the NIC the agent paired
-    with this GPU (``rccl-net.json`` entry with the same ``GPU_BDF``, else ``GPU_INDEX`` — the
-    agent's PCI-order index).  Apply before the rail group's communicator is created, e.g.
+    with this GPU -- the ``rccl-net.json`` entry with the same ``GPU_BDF``, else ``GPU_INDEX`` (the
+    agent's PCI-order index), else (no ``rccl-net.json``: L2 mode writes none) the node topology
+    discovered from sysfs (``models.topology.NodeTopology``, the agent's own pairing).  Apply
+    before the rail group's communicator is created, e.g.
     ``os.environ.update(rail_env(device_bdf(local_rank)))`` ahead of ``init_process_group``.
     The setting is per process, so the job-wide communicator also sends this GPU's traffic
-    through its own NIC — what RCCL's topology search picks for GPU-affine NICs anyway.
-    Raises ``LookupError`` when no configured NIC belongs to this GPU."""
+    through its own NIC -- what RCCL's topology search picks for GPU-affine NICs anyway.
+    Raises ``LookupError`` when no RDMA NIC belongs to this GPU."""
     env_path = os.path.join(artifact_dir, "rccl.env")
     env = read_env_file(env_path) if os.path.exists(env_path) else {}
-    with open(os.path.join(artifact_dir, "rccl-net.json")) as f:
-        entries = json.load(f).get("NIC_NET_CONFIG", [])
+    entries = []
+    net_path = os.path.join(artifact_dir, "rccl-net.json")
+    if os.path.exists(net_path):
+        with open(net_path) as f:
+            entries = json.load(f).get("NIC_NET_CONFIG", [])
     want = gpu_bdf.lower() if gpu_bdf else None
     mine = next((e for e in entries if want and e.get("GPU_BDF", "").lower() == want), None)
     if mine is None and gpu_index is not None:
         mine = next((e for e in entries if e.get("GPU_INDEX") == gpu_index), None)
+    if mine is None and want:
+        from ..models.topology import NodeTopology
+
+        hit = NodeTopology.discover(sysfs_root, with_xgmi=False).rdma_for_gpu(want)
+        if hit:
+            mine = {"RDMA_DEV": hit[0], "RDMA_PORT": hit[1]}
     if mine is None or not mine.get("RDMA_DEV"):
-        raise LookupError(f"no configured RDMA NIC for GPU {gpu_bdf or gpu_index} in {artifact_dir}/rccl-net.json")
+        raise LookupError(f"no configured RDMA NIC for GPU {gpu_bdf or gpu_index} in {net_path} or {sysfs_root}")
     env["NCCL_IB_HCA"] = f"={mine['RDMA_DEV']}:{mine.get('RDMA_PORT', 1)}"  # '=': exact name match
     if "GID_INDEX" in mine:
         env["NCCL_IB_GID_INDEX"] = str(mine["GID_INDEX"])
-    # NCCL_SOCKET_IFNAME stays as it is: bootstrap of the job-wide communicator needs a network
-    # every node shares, and different rails need not route to each other.
+    # NCCL_SOCKET_IFNAME stays as the agent wrote it: every node lists its rails in GPU order, so
+    # bootstrap meets on rail 0, a network every node shares (different rails need not route to
+    # each other).
     return env
 
 

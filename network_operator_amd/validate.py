@@ -6,7 +6,10 @@ runs where the GPUs are (a Job with ``amd.com/gpu: 8``, see ``config/validation/
 answers one question: do the links actually carry collectives at the expected speed?  It runs
 these checks:
 
-1. **Topology.**  KFD: every GPU pair is xGMI-linked.
+1. **Topology.**  KFD: every GPU pair is xGMI-linked; every GPU has its own scale-out NIC
+   within one PCIe switch (the agent's pairing, ``models.topology.NodeTopology``); and, when
+   the agent wrote one, its ``NCCL_TOPO_FILE`` places each pair under the same switch the live
+   PCIe tree does.
 2. **xGMI probe** (``netop-xgmi-probe``).  Per-link pull bandwidth, all-peers pull and push
    aggregates, all byte-exact.
 3. **RCCL** (``netop-rccl-bench``).  An all-reduce size sweep, every result checked exactly.
@@ -45,19 +48,49 @@ def _check(name: str, ok: bool, **detail) -> dict:
     return {"check": name, "ok": bool(ok), **detail}
 
 
+def topo_file_agrees(xml_text: str, topo) -> dict:
+    """Whether an RCCL topology file (the agent's rccl-topo.xml) nests each GPU and its paired
+    NIC under the same outermost switch as the live PCIe tree, and lists every GPU."""
+    import xml.etree.ElementTree as ET
+
+    root = ET.fromstring(xml_text)
+    top_of: dict = {}
+    for cpu in root.findall("cpu"):
+        for top in cpu.findall("pci"):
+            for p in top.iter("pci"):
+                top_of[p.get("busid")] = top.get("busid")
+            for net in top.iter("net"):
+                top_of["net:" + net.get("name", "")] = top.get("busid")
+    missing = [g for g in topo.gpus if g not in top_of]
+    split = []
+    for p in topo.pairs:
+        name = topo.rdma.get(p.nic) or p.nic
+        if top_of.get(p.gpu_bdf) != top_of.get("net:" + name):
+            split.append((p.gpu_bdf, name))
+    return {"ok": not missing and not split, "gpus_missing": missing, "pairs_split": split}
+
+
 def run(gpus: int, min_busbw: float, min_link_GBps: float, max_bytes: int, sysfs_root: str = "/sys/",
-        nfd_dir: Optional[str] = None, timeout: float = 600) -> dict:
+        nfd_dir: Optional[str] = None, timeout: float = 600, artifact_dir: str = "/etc/amd/scale-out") -> dict:
     checks: List[dict] = []
     report: dict = {"gpus": gpus, "started": time.time()}
 
     # 1. topology (no GPU needed)
     try:
-        from .agent import native
+        from .models.topology import NodeTopology
 
-        x = native().read_xgmi(sysfs_root)
-        need = x["pairs_expected"] if gpus == len(x["gpus"]) else gpus * (gpus - 1) // 2
-        checks.append(_check("xgmi_topology", x["pairs_connected"] >= need, pairs=x["pairs_connected"],
-                             expected=need, per_gpu_bw_mbs=x["per_gpu_bw_mbs"]))
+        topo = NodeTopology.discover(sysfs_root)
+        x = topo.xgmi
+        need = x.pairs_expected if gpus == len(x.gpus) else gpus * (gpus - 1) // 2
+        checks.append(_check("xgmi_topology", x.pairs_connected >= need, pairs=x.pairs_connected,
+                             expected=need, per_gpu_bw_mbs=x.per_gpu_bw_mbs))
+        checks.append(_check("gpu_nic_affinity", bool(topo.pairs) and not topo.unpaired_gpus,
+                             pairs={p.gpu_bdf: f"{p.nic} ({p.path})" for p in topo.pairs},
+                             unpaired_gpus=topo.unpaired_gpus))
+        tf = Path(artifact_dir) / "rccl-topo.xml"
+        if tf.exists():
+            agree = topo_file_agrees(tf.read_text(), topo)
+            checks.append(_check("rccl_topology_file", agree.pop("ok"), path=str(tf), **agree))
     except Exception as e:
         checks.append(_check("xgmi_topology", False, error=str(e)))
 
@@ -143,8 +176,10 @@ def main(argv=None) -> int:
     ap.add_argument("--max-bytes", type=int, default=1 << 30)
     ap.add_argument("--sysfs-root", default=os.environ.get("SYSFS_ROOT", "/sys/"))
     ap.add_argument("--nfd-features-dir", default=None, help="write the validation label here when all checks pass")
+    ap.add_argument("--artifact-dir", default="/etc/amd/scale-out", help="the agent's RCCL artifacts (rccl-topo.xml)")
     a = ap.parse_args(argv)
-    rep = run(a.gpus, a.min_busbw, a.min_link, a.max_bytes, a.sysfs_root, a.nfd_features_dir)
+    rep = run(a.gpus, a.min_busbw, a.min_link, a.max_bytes, a.sysfs_root, a.nfd_features_dir,
+              artifact_dir=a.artifact_dir)
     print(json.dumps(rep))
     return 0 if rep["ok"] else 1
 

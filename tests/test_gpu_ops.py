@@ -193,13 +193,19 @@ def test_sum_bf16_rejects_bad_args(cuda_device):
 
 
 def test_fabric_validation_single_gpu(cuda_device, tmp_path):
-    """validate.run on the 1-GPU box: topology from the real KFD, probe, RCCL sweep, counters."""
+    """validate.run on the 1-GPU box: topology from the real KFD and PCIe tree (the agent's
+    NCCL_TOPO_FILE for this box must agree with it), probe, RCCL sweep, counters."""
     from network_operator_amd import validate
+    from network_operator_amd.agent import native
 
-    rep = validate.run(gpus=1, min_busbw=0, min_link_GBps=0, max_bytes=64 << 20, nfd_dir=str(tmp_path))
+    art = tmp_path / "art"
+    art.mkdir()
+    (art / "rccl-topo.xml").write_text(native().rccl_topo_xml("/sys/"))
+    rep = validate.run(gpus=1, min_busbw=0, min_link_GBps=0, max_bytes=64 << 20, nfd_dir=str(tmp_path),
+                       artifact_dir=str(art))
     assert rep["ok"], rep
     names = [c["check"] for c in rep["checks"]]
-    assert names[:3] == ["xgmi_topology", "xgmi_probe", "rccl_all_reduce"]
+    assert names[:5] == ["xgmi_topology", "gpu_nic_affinity", "rccl_topology_file", "xgmi_probe", "rccl_all_reduce"]
     assert names[-1] == "xgmi_direct_all_reduce"
     assert (tmp_path / validate.LABEL_FILE).read_text().startswith(validate.LABEL + "=true\n")
 

@@ -79,6 +79,22 @@ def test_topo_xml_gpu_and_nic_share_rccl_switch(native, tmp_path):
         assert len(g) == 5 and len(n) == 4  # cpu > 01 > 06 > 08 > GPU;  cpu > 01 > 03 > NIC (RCCL folding)
 
 
+def test_validate_checks_topology_file_against_live_tree(native, tmp_path):
+    """validate.py's rccl_topology_file check: the golden file agrees with the fixture node; a
+    file that puts a rail NIC under another GPU's switch does not."""
+    from network_operator_amd import validate
+    from network_operator_amd.models.topology import NodeTopology
+
+    fakesysfs.build_mi355x_node(tmp_path)
+    topo = NodeTopology.discover(str(tmp_path) + "/")
+    good = GOLDEN.read_text()
+    assert validate.topo_file_agrees(good, topo)["ok"]
+    bad = good.replace('<net name="mlx5_1" port="1"/>', '<net name="tmp" port="1"/>').replace(
+        '<net name="mlx5_3" port="1"/>', '<net name="mlx5_1" port="1"/>')
+    r = validate.topo_file_agrees(bad, topo)
+    assert not r["ok"] and len(r["pairs_split"]) == 2, r
+
+
 def test_topo_xml_extra_interface_without_rdma(native, tmp_path):
     fakesysfs.build_mi355x_node(tmp_path)
     root = ET.fromstring(native.rccl_topo_xml(str(tmp_path) + "/", interfaces=["ens9np0", "lo"], cpu=fakesysfs.MI355X_HOST_CPU))

@@ -165,7 +165,27 @@ def test_rail_env_pins_each_gpu_to_its_own_nic(tmp_path):
     assert env == {"NCCL_IB_HCA": "=rdma2:1", "NCCL_IB_GID_INDEX": "3", "NCCL_IB_DISABLE": "0", "NCCL_IB_TC": "106"}
     assert rail_env(None, gpu_index=1, artifact_dir=str(tmp_path))["NCCL_IB_HCA"] == "=rdma1:1"
     with pytest.raises(LookupError):
-        rail_env("0000:dc:00.0", artifact_dir=str(tmp_path))
+        rail_env("0000:dc:00.0", artifact_dir=str(tmp_path), sysfs_root=str(tmp_path / "no-sysfs") + "/")
+
+
+def test_rail_env_without_rccl_net_uses_the_node_topology(tmp_path):
+    """L2 mode writes rccl.env but no rccl-net.json: the GPU's rail NIC then comes from the node
+    topology (models/topology.NodeTopology over sysfs), i.e. the agent's own GPU<->NIC pairing."""
+    from network_operator_amd.models.topology import NodeTopology
+    from network_operator_amd.parallel.rail import rail_env
+    from network_operator_amd.testing import fakesysfs
+
+    sysfs = tmp_path / "sys"
+    fakesysfs.build_mi355x_node(sysfs)
+    art = tmp_path / "art"
+    art.mkdir()
+    (art / "rccl.env").write_text("NCCL_IB_HCA==mlx5_1:1,mlx5_3:1\nNCCL_IB_GID_INDEX=1\n")
+    topo = NodeTopology.discover(str(sysfs) + "/")
+    assert topo.xgmi.full_mesh and not topo.unpaired_gpus and len(topo.pairs) == 8
+    gpu = topo.gpus[3]
+    dev, port = topo.rdma_for_gpu(gpu)
+    env = rail_env(gpu, artifact_dir=str(art), sysfs_root=str(sysfs) + "/")
+    assert env["NCCL_IB_HCA"] == f"={dev}:{port}" and env["NCCL_IB_GID_INDEX"] == "1"
 
 
 @pytest.mark.gpu
