@@ -55,3 +55,31 @@ def test_images_gate_on_hardening_and_run_without_pip():
     final = op.rsplit("FROM ", 1)[1]  # the runtime stage
     assert "distroless" in final.splitlines()[0] and "nonroot" in final.splitlines()[0]
     assert "pip" not in final and "USER 65532" in final
+
+
+def test_operator_image_file_set_is_self_contained(tmp_path):
+    """The operator image copies only some packages (build/Dockerfile.operator).  The manager
+    must import and parse its flags from exactly that file set, which is what the image's
+    build-time import check does, here without docker."""
+    import re
+
+    df = (ROOT / "build" / "Dockerfile.operator").read_text()
+    copies = re.findall(r"^COPY (network_operator_amd\S*) (\S+)$", df, re.M)
+    assert copies, df
+    app = tmp_path / "app"
+    for src, dst in copies:
+        s, d = ROOT / src, app / dst
+        if s.is_dir():
+            shutil.copytree(s, d, ignore=shutil.ignore_patterns("__pycache__", "*.so"))
+        else:
+            d.parent.mkdir(parents=True, exist_ok=True)
+            shutil.copy(s, d)
+    r = subprocess.run([sys.executable, "-c", "import network_operator_amd.operator.manager as m; "
+                        "m.build_parser().parse_args(['--policies-file=/x', '--leader-elect'])"],
+                       cwd=str(tmp_path), env={"PYTHONPATH": str(app), "PATH": "/usr/bin:/bin"},
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    r = subprocess.run([sys.executable, "-m", "network_operator_amd.operator", "--help"], cwd=str(tmp_path),
+                       env={"PYTHONPATH": str(app), "PATH": "/usr/bin:/bin"}, capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode == 0 and "--policies-file" in r.stdout, r.stderr[-2000:]
