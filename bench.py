@@ -149,27 +149,33 @@ def node_ready_gpu_side(sysfs: str = "/sys/") -> dict:
     return out
 
 
-def _rccl_autotune(rank: int, world: int, nbytes: int, started: float = time.time()) -> dict:
-    """RCCL parameters are read once per process, at communicator creation, so they have to be
-    chosen before init_process_group.  Rank 0 measures the knob variants of
-    ``rccl_bench.ENV_PROBES`` with the native harness over the node's first `world` GPUs (a fresh
-    process per variant).  It publishes the winner through a file in /tmp keyed by the rendezvous
-    port, and every rank exports it.  A variant must beat the defaults by >= 3 % to be used."""
+def _rccl_autotune(rank: int, world: int, nbytes: int, budget_s: float = 120.0,
+                   started: float = time.time()) -> dict:
+    """RCCL reads its parameters once per process, at communicator creation, so they must be
+    chosen before init_process_group.
+
+    Rank 0 measures the knob variants of ``rccl_bench.ENV_PROBES`` with the native harness over
+    the node's first `world` GPUs. Each variant runs in a fresh process, and all of them must fit
+    in ``budget_s``. Rank 0 publishes the winner through a file in /tmp keyed by the rendezvous
+    port, and every rank exports it. A variant must beat the defaults by >= 3 %
+    (``rccl_bench.choose_env``). This is how the validation Job tunes a node's ``rccl.env``
+    (``validate.py --tune-rccl``). It is still RCCL: only its documented environment changes."""
     path = f"/tmp/netop-rccl-autotune-{os.environ.get('MASTER_PORT', '0')}.json"
     if rank == 0:
-        from network_operator_amd.parallel import rccl_bench
+        try:
+            from network_operator_amd.parallel import rccl_bench
 
-        probes = rccl_bench.env_probe(world, nbytes)
-        base = next((p.get("busbw_GBps") for p in probes if p["env"] == {}), None) or 0.0
-        best = max((p for p in probes if p.get("busbw_GBps")), key=lambda p: p["busbw_GBps"], default=None)
-        chosen = best["env"] if best and base and best["busbw_GBps"] >= 1.03 * base else {}
-        doc = {"created": time.time(), "chosen": chosen, "baseline_busbw_GBps": base, "probes": probes}
+            probes = rccl_bench.env_probe(world, nbytes, budget_s=budget_s)
+            doc = dict(rccl_bench.choose_env(probes), probes=probes)
+        except Exception as e:  # never leave the other ranks waiting: defaults, and say why
+            doc = {"chosen": {}, "error": str(e)[-300:]}
+        doc["created"] = time.time()
         tmp = path + f".{os.getpid()}"
         with open(tmp, "w") as f:
             json.dump(doc, f)
         os.replace(tmp, path)
     else:
-        deadline = time.time() + 600
+        deadline = time.time() + budget_s + 300
         doc = None
         while time.time() < deadline:
             try:
@@ -206,9 +212,11 @@ def main(argv=None) -> int:
     ap.add_argument("--extras-budget", type=float, default=150.0,
                     help="seconds rank 0 may spend on the diagnostics after the timed loop (probe, native "
                          "harness, knob probe, direct all-reduce); later ones are skipped once it is spent")
-    ap.add_argument("--rccl-autotune", type=int, default=0,
+    ap.add_argument("--rccl-autotune", type=int, default=1,
                     help="n > 1: before RCCL starts, rank 0 measures RCCL knob variants with the native harness "
-                         "and every rank uses the fastest (>= 3%% better than defaults) for the run")
+                         "(within --rccl-autotune-budget s) and every rank uses the fastest (>= 3%% better than "
+                         "the defaults) for the run; 0 = RCCL defaults")
+    ap.add_argument("--rccl-autotune-budget", type=float, default=120.0)
     ap.add_argument("--xgmi-allreduce", type=int, default=1,
                     help="also run the direct two-shot xGMI all-reduce on rank 0 (n > 1)")
     # CPU rehearsal of the multi-rank path (tests): gloo backend, fp32 on the host.
@@ -244,7 +252,8 @@ def main(argv=None) -> int:
             return 2
         torch.cuda.set_device(local_rank)
         device, dtype = torch.device("cuda", local_rank), torch.bfloat16
-        tuned = _rccl_autotune(rank, world, args.bytes) if args.rccl_autotune and world > 1 else None
+        tuned = (_rccl_autotune(rank, world, args.bytes, args.rccl_autotune_budget)
+                 if args.rccl_autotune and world > 1 else None)
         dist.init_process_group("nccl", rank=rank, world_size=world, device_id=device)
     # Host-side group for waiting while rank 0 runs its extra GPU tools: an RCCL barrier would
     # leave a spinning kernel on every other GPU and disturb what those tools measure.

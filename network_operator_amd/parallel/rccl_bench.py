@@ -63,11 +63,19 @@ ENV_PROBES = (
 )
 
 
-def env_probe(gpus: int, nbytes: int, iters: int = 10, probes=ENV_PROBES, timeout: float = 120) -> List[dict]:
+def env_probe(gpus: int, nbytes: int, iters: int = 10, probes=ENV_PROBES, timeout: float = 120,
+              budget_s: Optional[float] = None) -> List[dict]:
     """busbw of one all-reduce size under each RCCL environment variant (fresh process each:
-    RCCL caches its parameters at first use)."""
+    RCCL caches its parameters at first use).  Variants not started within ``budget_s`` seconds
+    are reported as skipped."""
+    import time
+
     out = []
+    t0 = time.monotonic()
     for extra in probes:
+        if budget_s is not None and time.monotonic() - t0 > budget_s:
+            out.append({"env": extra, "skipped": "time budget spent"})
+            continue
         try:
             rows = run(op="all_reduce", gpus=gpus, min_bytes=nbytes, max_bytes=nbytes, iters=iters, warmup=3,
                        check=False, env=extra, timeout=timeout)
@@ -76,6 +84,17 @@ def env_probe(gpus: int, nbytes: int, iters: int = 10, probes=ENV_PROBES, timeou
         except Exception as e:
             out.append({"env": extra, "error": str(e)[-300:]})
     return out
+
+
+def choose_env(probes: List[dict], min_gain: float = 1.03) -> dict:
+    """The variant to use: the fastest measured one if it beats the defaults ({}) by at least
+    ``min_gain``, else the defaults.  Returns {"chosen": env, "baseline_busbw_GBps": x,
+    "best_busbw_GBps": y}."""
+    base = next((p.get("busbw_GBps") for p in probes if p["env"] == {}), None) or 0.0
+    best = max((p for p in probes if p.get("busbw_GBps")), key=lambda p: p["busbw_GBps"], default=None)
+    chosen = best["env"] if best and base and best["busbw_GBps"] >= min_gain * base else {}
+    return {"chosen": dict(chosen), "baseline_busbw_GBps": base,
+            "best_busbw_GBps": best["busbw_GBps"] if best else None}
 
 
 def parse(stdout: str) -> List[Row]:

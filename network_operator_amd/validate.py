@@ -19,7 +19,12 @@ these checks:
 5. **Direct xGMI all-reduce** (``parallel/xgmi_comm.py``).  The one-process-per-GPU
    all-reduce over HIP IPC buffers that jobs can use, every size checked exactly (after the
    counter window, so check 4 still sees RCCL traffic only).
-6. **Optionally, the label.**  If everything passed, the NFD label
+6. **Optionally, RCCL tuning** (``--tune-rccl``, n > 1).  The 1 GiB all-reduce under the
+   knob variants of ``parallel/rccl_bench.ENV_PROBES``, each in a fresh process.  A variant
+   that beats RCCL's defaults by at least 3 % is written to ``<artifact-dir>/rccl-tuned.env``,
+   for jobs to source after the agent's ``rccl.env``.  ``bench.py`` does the same before its
+   timed run.
+7. **Optionally, the label.**  If everything passed, the NFD label
    ``amd.feature.node.kubernetes.io/gpu-fabric-validated=true`` is written, along with the
    measured busbw.
 
@@ -71,7 +76,8 @@ def topo_file_agrees(xml_text: str, topo) -> dict:
 
 
 def run(gpus: int, min_busbw: float, min_link_GBps: float, max_bytes: int, sysfs_root: str = "/sys/",
-        nfd_dir: Optional[str] = None, timeout: float = 600, artifact_dir: str = "/etc/amd/scale-out") -> dict:
+        nfd_dir: Optional[str] = None, timeout: float = 600, artifact_dir: str = "/etc/amd/scale-out",
+        tune_rccl: bool = False) -> dict:
     checks: List[dict] = []
     report: dict = {"gpus": gpus, "started": time.time()}
 
@@ -151,6 +157,25 @@ def run(gpus: int, min_busbw: float, min_link_GBps: float, max_bytes: int, sysfs
                                                       for r in d["rows"]]))
     except Exception as e:
         checks.append(_check("xgmi_direct_all_reduce", False, error=str(e)[-500:]))
+    if tune_rccl and gpus > 1:
+        try:
+            from .parallel import rccl_bench
+
+            probes = rccl_bench.env_probe(gpus, max_bytes, budget_s=min(timeout, 300))
+            pick = rccl_bench.choose_env(probes)
+            report["rccl_tuning"] = dict(pick, probes=probes)
+            out = Path(artifact_dir) / "rccl-tuned.env"
+            if pick["chosen"]:
+                out.parent.mkdir(parents=True, exist_ok=True)
+                tmp = out.with_suffix(".tmp")
+                tmp.write_text("# Measured by the fabric validation Job (validate.py --tune-rccl): "
+                               f"{pick['best_busbw_GBps']:.1f} vs {pick['baseline_busbw_GBps']:.1f} GB/s busbw "
+                               "with RCCL's defaults\n" + "".join(f"{k}={v}\n" for k, v in sorted(pick["chosen"].items())))
+                os.replace(tmp, out)
+            elif out.exists():
+                out.unlink()  # the defaults are best now: drop a stale override
+        except Exception as e:
+            report["rccl_tuning"] = {"error": str(e)[-500:]}
     report["checks"] = checks
     report["ok"] = all(c["ok"] for c in checks)
     report["seconds"] = time.time() - report.pop("started")
@@ -177,9 +202,11 @@ def main(argv=None) -> int:
     ap.add_argument("--sysfs-root", default=os.environ.get("SYSFS_ROOT", "/sys/"))
     ap.add_argument("--nfd-features-dir", default=None, help="write the validation label here when all checks pass")
     ap.add_argument("--artifact-dir", default="/etc/amd/scale-out", help="the agent's RCCL artifacts (rccl-topo.xml)")
+    ap.add_argument("--tune-rccl", action="store_true",
+                    help="measure RCCL knob variants and write the winner to <artifact-dir>/rccl-tuned.env")
     a = ap.parse_args(argv)
     rep = run(a.gpus, a.min_busbw, a.min_link, a.max_bytes, a.sysfs_root, a.nfd_features_dir,
-              artifact_dir=a.artifact_dir)
+              artifact_dir=a.artifact_dir, tune_rccl=a.tune_rccl)
     print(json.dumps(rep))
     return 0 if rep["ok"] else 1
 

@@ -136,3 +136,15 @@ def test_bus_factors_and_ceiling():
     assert C.xgmi_busbw_ceiling_GBps(8) == pytest.approx(532.0)
     assert C.xgmi_busbw_ceiling_GBps(1) == 0
     assert C.sweep_sizes(8, 64) == [16, 32, 64]
+
+
+def test_rccl_knob_choice_needs_a_real_gain():
+    from network_operator_amd.parallel import rccl_bench as R
+
+    probes = [{"env": {}, "busbw_GBps": 300.0}, {"env": {"NCCL_MIN_NCHANNELS": "64"}, "busbw_GBps": 305.0},
+              {"env": {"NCCL_ALGO": "Ring"}, "error": "boom"}, {"env": {"X": "1"}, "skipped": "time budget spent"}]
+    assert R.choose_env(probes)["chosen"] == {}  # +1.7 % is noise
+    probes.append({"env": {"NCCL_MIN_NCHANNELS": "112"}, "busbw_GBps": 330.0})
+    pick = R.choose_env(probes)
+    assert pick["chosen"] == {"NCCL_MIN_NCHANNELS": "112"} and pick["baseline_busbw_GBps"] == 300.0
+    assert R.choose_env([{"env": {"A": "1"}, "busbw_GBps": 1.0}])["chosen"] == {}  # no baseline, no choice

@@ -135,6 +135,17 @@ def test_native_rccl_bench(cuda_device, op, inplace, graph):
     assert all(r.busbw_GBps == 0.0 for r in rows) or op == "broadcast"  # n=1 bus factor
 
 
+def test_rccl_env_probe_runs_every_variant(cuda_device):
+    """bench.py's --rccl-autotune / validate.py --tune-rccl path: every knob variant starts RCCL
+    in a fresh process and completes; at n = 1 busbw is 0, so the defaults stay chosen."""
+    from network_operator_amd.parallel import rccl_bench
+
+    probes = rccl_bench.env_probe(1, 16 << 20, iters=3, timeout=60, budget_s=90)
+    assert [p["env"] for p in probes] == list(rccl_bench.ENV_PROBES)
+    assert all("busbw_GBps" in p and p["time_us"] > 0 for p in probes), probes
+    assert rccl_bench.choose_env(probes)["chosen"] == {}
+
+
 @pytest.mark.parametrize("ranks", [1, 3, 8])
 def test_xgmi_allreduce_algorithm_virtual_ranks(cuda_device, ranks):
     """The n-rank two-shot algorithm (pull and push) with every rank mapped onto the one GPU:
