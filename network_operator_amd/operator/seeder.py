@@ -35,6 +35,7 @@ from typing import Dict, List, Optional
 import yaml
 
 from ..api.v1alpha1 import types as T
+from ..api.v1alpha1 import webhook as W
 from . import kube
 from .kube import ApiClient, ApiError, is_not_found
 
@@ -61,7 +62,9 @@ def load_policies(path: str) -> Optional[List[dict]]:
     for i, item in enumerate(items):
         if not isinstance(item, dict) or not (item.get("metadata") or {}).get("name"):
             raise ValueError(f"{path}: policies[{i}] has no metadata.name")
-        pol = T.NetworkClusterPolicy.from_dict(item).to_dict()  # normalised, unknown fields kept
+        # Normalised and defaulted exactly as the mutating webhook will (unknown fields kept), so
+        # the stored object compares equal and a steady state issues no updates.
+        pol = W.default(T.NetworkClusterPolicy.from_dict(item)).to_dict()
         pol["apiVersion"], pol["kind"] = T.API_VERSION, T.KIND
         md = pol.setdefault("metadata", {})
         md["labels"] = dict(md.get("labels") or {}, **{MANAGED_BY_KEY: MANAGED_BY})
@@ -75,6 +78,7 @@ class PolicySeeder:
         self.client, self.path, self.interval, self.max_backoff = client, path, interval, max_backoff
         self.owner = owner  # "ClusterRole/<name>" or ""
         self.applied = 0    # successful sync passes (tests, metrics)
+        self.writes = 0     # creates + updates + deletes issued
         self.last_error = ""
 
     async def _owner_reference(self) -> Optional[dict]:
@@ -116,6 +120,7 @@ class PolicySeeder:
                 if not is_not_found(e):
                     raise
                 await self.client.create(P, desired)
+                self.writes += 1
                 log.info("created policy %s from %s", name, self.path)
                 continue
             if not self._managed(cur):
@@ -133,6 +138,7 @@ class PolicySeeder:
                 md["ownerReferences"] = others + [ref]
             if new != cur:
                 await self.client.replace(P, new)
+                self.writes += 1
                 log.info("updated policy %s from %s", name, self.path)
         listed = await self.client.list(P, label_selector=f"{MANAGED_BY_KEY}={MANAGED_BY}")
         for cur in listed.get("items") or []:
@@ -140,6 +146,7 @@ class PolicySeeder:
             if name not in names:
                 try:
                     await self.client.delete(P, name)
+                    self.writes += 1
                     log.info("deleted policy %s (no longer in %s)", name, self.path)
                 except ApiError as e:
                     if not is_not_found(e):

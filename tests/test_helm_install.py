@@ -170,6 +170,13 @@ def test_one_release_helm_install_upgrade_and_uninstall(tmp_path, monkeypatch):
                                                                "kind": "ClusterRole", "name": "amd-network-operator",
                                                                "uid": role["metadata"]["uid"]}]
                 assert pol["spec"]["amdScaleOut"]["mtu"] == 9000
+                # Steady state: the seeder (0.2 s interval) rewrites nothing.
+                replaces = sum(1 for m, path in fake.requests if m == "PUT" and "/networkclusterpolicies/" in path
+                               and not path.endswith("/status"))
+                await asyncio.sleep(1.0)
+                assert sum(1 for m, path in fake.requests if m == "PUT" and "/networkclusterpolicies/" in path
+                           and not path.endswith("/status")) == replaces
+                assert fake.get_object(P, "netconf-amd-scale-out")["metadata"]["generation"] == 1
 
                 # 4. `helm upgrade --set config.amd.mtu=4200`: the projected file changes.
                 up = helm_template(CHART, {"config": {"amd": {"enabled": True, "mtu": 4200}}}, NS)
