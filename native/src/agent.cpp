@@ -382,6 +382,9 @@ void Agent::assign_rail_indices() {
 
 void Agent::add_rail_routing(NicState& n) {
     const uint32_t t = rail_table(n);
+    // Routes carry an 8-bit table id here, and 253..255 are the kernel's default / main / local.
+    if (t == 0 || t >= RT_TABLE_DEFAULT)
+        throw AgentError(strfmt("rail table %u of '%s' is outside 1..252 (lower --rail-table-base)", t, n.ifname.c_str()));
     nl::RuleSpec rule{Ipv4Prefix{n.addr->local, 32}, t, t, kRailProtocol};
     // What this agent installed for an earlier address of this rail (Port Description change).
     if (n.rail_rule && !(*n.rail_rule == rule)) remove_rail_routing(n);
