@@ -167,7 +167,8 @@ async def run(argv: Optional[List[str]] = None, stop: Optional[asyncio.Event] = 
             if opts.policies_file:
                 # Only the leader writes policies; the webhook server is already serving, so the
                 # API server can admit them (see seeder.py for why the chart does not create them).
-                seeder = PolicySeeder(client, opts.policies_file, opts.policies_owner, opts.policies_interval)
+                seeder = PolicySeeder(client, opts.policies_file, opts.policies_owner, opts.policies_interval,
+                                      metrics=metrics)
                 seed = asyncio.ensure_future(seeder.run(stop))
             if started:
                 started.set()

@@ -34,6 +34,12 @@ class OperatorMetrics:
                                     ["policy"], registry=r)
         self.policy_ready = Gauge("amd_network_operator_policy_ready",
                                   "Nodes whose agent published the scale-out readiness label", ["policy"], registry=r)
+        self.seed_in_sync = Gauge("amd_network_operator_policies_file_in_sync",
+                                  "1 when the policies of --policies-file (the Helm release's) match the cluster",
+                                  registry=r)
+        self.seed_errors = Counter("amd_network_operator_policies_file_errors_total",
+                                   "Failed passes applying --policies-file (webhook not serving yet, rejected spec, ...)",
+                                   registry=r)
 
     def render(self) -> bytes:
         return generate_latest(self.registry)

@@ -74,9 +74,10 @@ def load_policies(path: str) -> Optional[List[dict]]:
 
 class PolicySeeder:
     def __init__(self, client: ApiClient, path: str, owner: str = "", interval: float = 10.0,
-                 max_backoff: float = 10.0):
+                 max_backoff: float = 10.0, metrics=None):
         self.client, self.path, self.interval, self.max_backoff = client, path, interval, max_backoff
         self.owner = owner  # "ClusterRole/<name>" or ""
+        self.metrics = metrics
         self.applied = 0    # successful sync passes (tests, metrics)
         self.writes = 0     # creates + updates + deletes issued
         self.last_error = ""
@@ -160,10 +161,15 @@ class PolicySeeder:
                 await self.sync_once()
                 self.applied += 1
                 self.last_error = ""
+                if self.metrics is not None:
+                    self.metrics.seed_in_sync.set(1)
                 backoff = 0.2
                 delay = self.interval
             except Exception as e:  # webhook endpoint not up yet, API hiccup, bad file
                 msg = str(e)
+                if self.metrics is not None:
+                    self.metrics.seed_in_sync.set(0)
+                    self.metrics.seed_errors.inc()
                 if msg != self.last_error:
                     log.warning("applying %s failed (retrying): %s", self.path, msg)
                 self.last_error = msg
