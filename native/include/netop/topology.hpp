@@ -30,6 +30,14 @@ struct PciDev {
     uint32_t vendor = 0, device = 0, pci_class = 0;
     uint32_t subsystem_vendor = 0, subsystem_device = 0;
     int numa = -1;
+    // PCIe link capability of the function and of the port above it (sysfs max_link_speed /
+    // max_link_width of the device and of its parent directory); "" / 0 when unreadable.
+    std::string max_link_speed, port_max_link_speed;  // e.g. "32.0 GT/s PCIe"
+    int max_link_width = 0, port_max_link_width = 0;
+    // The link as RCCL records it (NCCL xml.cc): the slower of device and port speed (the
+    // device's string when neither parses), the narrower width.
+    std::string rccl_link_speed() const;
+    int rccl_link_width() const;
 };
 
 struct Gpu {

@@ -250,6 +250,11 @@ void emit_pci(std::string& out, XmlPci& n, int depth) {
     if (d.device) out += strfmt(" device=\"0x%04x\"", d.device);
     if (d.subsystem_vendor) out += strfmt(" subsystem_vendor=\"0x%04x\"", d.subsystem_vendor);
     if (d.subsystem_device) out += strfmt(" subsystem_device=\"0x%04x\"", d.subsystem_device);
+    // Always written: RCCL fills link attributes only on the PCI nodes it walks up from a GPU,
+    // not on a NIC's node that it finds in the file by name, and refuses a node without them
+    // ("Attribute link_width of node pci not found", measured on the box).
+    out += " link_speed=\"" + xml_attr(d.rccl_link_speed()) + "\"";
+    out += strfmt(" link_width=\"%d\"", d.rccl_link_width());
     if (n.kids.empty() && n.nets.empty()) {
         out += "/>\n";
         return;

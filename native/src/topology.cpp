@@ -7,6 +7,8 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <cfloat>
+#include <cstdio>
 #include <cstring>
 #include <set>
 
@@ -86,9 +88,27 @@ std::optional<PciDev> read_pci_dev(const std::string& root, const std::string& d
     d.subsystem_vendor = read_hex(path_join(*real, "subsystem_vendor"));
     d.subsystem_device = read_hex(path_join(*real, "subsystem_device"));
     d.numa = read_int(path_join(*real, "numa_node"), -1);
+    auto str = [](const std::string& p) {
+        auto v = read_file(p);
+        return v ? trim(*v) : std::string();
+    };
+    d.max_link_speed = str(path_join(*real, "max_link_speed"));
+    d.max_link_width = read_int(path_join(*real, "max_link_width"), 0);
+    const std::string port = path_dirname(*real);
+    d.port_max_link_speed = str(path_join(port, "max_link_speed"));
+    d.port_max_link_width = read_int(path_join(port, "max_link_width"), 0);
     (void)root;
     return d;
 }
+
+std::string PciDev::rccl_link_speed() const {
+    float dev = FLT_MAX, port = FLT_MAX;
+    std::sscanf(max_link_speed.c_str(), "%f GT/s", &dev);
+    std::sscanf(port_max_link_speed.c_str(), "%f GT/s", &port);
+    return port < dev ? port_max_link_speed : max_link_speed;
+}
+
+int PciDev::rccl_link_width() const { return std::min(max_link_width, port_max_link_width); }
 
 CpuIdentity cpu_identity() {
     CpuIdentity c;

@@ -175,19 +175,19 @@ TEST(rccl_topo_xml_tree) {
     const std::string want =
         "<system version=\"2\">\n"
         "  <cpu numaid=\"1\" affinity=\"ffffffff,00000000\" arch=\"x86_64\" vendor=\"AuthenticAMD\" familyid=\"191\" modelid=\"2\">\n"
-        "    <pci busid=\"0000:e8:00.0\" class=\"0x060400\" vendor=\"0x1000\" device=\"0xc030\" subsystem_vendor=\"0x1000\" subsystem_device=\"0xc030\">\n"
-        "      <pci busid=\"0000:ea:00.0\" class=\"0x060400\" vendor=\"0x1000\" device=\"0xc030\" subsystem_vendor=\"0x1000\" subsystem_device=\"0xc030\">\n"
-        "        <pci busid=\"0000:ec:00.0\" class=\"0x060400\" vendor=\"0x1000\" device=\"0xc030\" subsystem_vendor=\"0x1000\" subsystem_device=\"0xc030\">\n"
-        "          <pci busid=\"0000:ef:00.0\" class=\"0x020000\" vendor=\"0x15b3\" device=\"0x1021\" subsystem_vendor=\"0x15b3\" subsystem_device=\"0x1021\">\n"
+        "    <pci busid=\"0000:e8:00.0\" class=\"0x060400\" vendor=\"0x1000\" device=\"0xc030\" subsystem_vendor=\"0x1000\" subsystem_device=\"0xc030\" link_speed=\"\" link_width=\"0\">\n"
+        "      <pci busid=\"0000:ea:00.0\" class=\"0x060400\" vendor=\"0x1000\" device=\"0xc030\" subsystem_vendor=\"0x1000\" subsystem_device=\"0xc030\" link_speed=\"\" link_width=\"0\">\n"
+        "        <pci busid=\"0000:ec:00.0\" class=\"0x060400\" vendor=\"0x1000\" device=\"0xc030\" subsystem_vendor=\"0x1000\" subsystem_device=\"0xc030\" link_speed=\"\" link_width=\"0\">\n"
+        "          <pci busid=\"0000:ef:00.0\" class=\"0x020000\" vendor=\"0x15b3\" device=\"0x1021\" subsystem_vendor=\"0x15b3\" subsystem_device=\"0x1021\" link_speed=\"\" link_width=\"0\">\n"
         "            <nic>\n"
         "              <net name=\"mlx5_7\" port=\"1\"/>\n"
         "            </nic>\n"
         "          </pci>\n"
         "        </pci>\n"
         "      </pci>\n"
-        "      <pci busid=\"0000:f0:00.0\" class=\"0x060400\" vendor=\"0x1000\" device=\"0xc030\" subsystem_vendor=\"0x1000\" subsystem_device=\"0xc030\">\n"
-        "        <pci busid=\"0000:f2:00.0\" class=\"0x060400\" vendor=\"0x1022\" device=\"0x1500\" subsystem_vendor=\"0x1022\" subsystem_device=\"0x1500\">\n"
-        "          <pci busid=\"0000:f4:00.0\" class=\"0x120000\" vendor=\"0x1002\" device=\"0x75a3\" subsystem_vendor=\"0x1002\" subsystem_device=\"0x75a3\"/>\n"
+        "      <pci busid=\"0000:f0:00.0\" class=\"0x060400\" vendor=\"0x1000\" device=\"0xc030\" subsystem_vendor=\"0x1000\" subsystem_device=\"0xc030\" link_speed=\"\" link_width=\"0\">\n"
+        "        <pci busid=\"0000:f2:00.0\" class=\"0x060400\" vendor=\"0x1022\" device=\"0x1500\" subsystem_vendor=\"0x1022\" subsystem_device=\"0x1500\" link_speed=\"\" link_width=\"0\">\n"
+        "          <pci busid=\"0000:f4:00.0\" class=\"0x120000\" vendor=\"0x1002\" device=\"0x75a3\" subsystem_vendor=\"0x1002\" subsystem_device=\"0x75a3\" link_speed=\"\" link_width=\"0\"/>\n"
         "        </pci>\n"
         "      </pci>\n"
         "    </pci>\n"

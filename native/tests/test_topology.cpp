@@ -214,3 +214,21 @@ TEST(topology_rccl_parents_fold_like_rccl) {
     auto md = read_pci_dev(t.path, t.path + "/devices/" + m);
     CHECK(rccl_pci_parents(*md).empty());  // its parent is the CPU
 }
+
+TEST(topology_rccl_link_is_the_slower_of_device_and_port) {
+    // NCCL xml.cc: link_speed = the slower of the device's and its port's max_link_speed (as the
+    // string read), link_width = the narrower width; missing files read as "" / 0.
+    PciDev d;
+    d.max_link_speed = "32.0 GT/s PCIe";
+    d.port_max_link_speed = "5.0 GT/s PCIe";
+    d.max_link_width = 16;
+    d.port_max_link_width = 8;
+    CHECK_EQ(d.rccl_link_speed(), std::string("5.0 GT/s PCIe"));
+    CHECK_EQ(d.rccl_link_width(), 8);
+    d.port_max_link_speed = "";
+    CHECK_EQ(d.rccl_link_speed(), std::string("32.0 GT/s PCIe"));
+    d.max_link_speed = "";
+    CHECK_EQ(d.rccl_link_speed(), std::string(""));
+    d.port_max_link_width = 0;
+    CHECK_EQ(d.rccl_link_width(), 0);
+}

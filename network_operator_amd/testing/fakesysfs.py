@@ -40,6 +40,8 @@ def _pci(root: Path, pcipath: str, driver: str, vendor: str, device: str, numa: 
     _w(d / "class", cls + "\n")
     _w(d / "subsystem_vendor", vendor + "\n")
     _w(d / "subsystem_device", device + "\n")
+    _w(d / "max_link_speed", "32.0 GT/s PCIe\n")
+    _w(d / "max_link_width", "16\n")
     # Bridges above the function (root port, switch up/downstream ports): the attributes RCCL's
     # topology reads from each of them (Broadcom PEX switch ports, like the live node).
     parts = pcipath.split("/")
@@ -52,6 +54,9 @@ def _pci(root: Path, pcipath: str, driver: str, vendor: str, device: str, numa: 
             _w(b / "subsystem_vendor", "0x1000\n")
             _w(b / "subsystem_device", "0x0072\n")
             _w(b / "numa_node", f"{numa}\n")
+            # PCIe 5 x16 on every port
+            _w(b / "max_link_speed", "32.0 GT/s PCIe\n")
+            _w(b / "max_link_width", "16\n")
     drv = root / "bus" / "pci" / "drivers" / driver
     drv.mkdir(parents=True, exist_ok=True)
     _link(drv, d / "driver")

@@ -164,6 +164,17 @@ def test_rccl_loads_generated_topology(native, tmp_path):
     r0, auto = _rccl_dump(tmp_path, None, tag="auto")
     assert r0.returncode == 0, r0.stderr[-2000:]
     assert _chain(auto, busid) == _chain(mine, busid)
+    # Attribute by attribute, the file says what RCCL would have read from sysfs itself
+    # (NCCL's link rule included: slower of device and port speed, narrower width).
+    attrs = ("class", "vendor", "device", "subsystem_vendor", "subsystem_device", "link_speed", "link_width")
+    by_bus = lambda root: {p.get("busid"): p for p in root.iter("pci")}  # noqa: E731
+    for b in _chain(mine, busid)[1:]:
+        got, want = by_bus(auto)[b], by_bus(mine)[b]
+        assert {a: got.get(a) for a in attrs} == {a: want.get(a) for a in attrs}, b
+    cpu_auto = [c for c in auto.iter("cpu") if c.get("numaid") == _chain(mine, busid)[0]][0]
+    cpu_mine = [c for c in mine.iter("cpu") if c.get("numaid") == _chain(mine, busid)[0]][0]
+    for a in ("affinity", "arch", "vendor", "familyid", "modelid"):
+        assert cpu_auto.get(a) == cpu_mine.get(a), a
     (ROOT / "gpurun_out").mkdir(exist_ok=True)
     (ROOT / "gpurun_out" / "rccl_topo_loaded.json").write_text(json.dumps({
         "gpu_busid": busid, "chain_in_file": _chain(mine, busid), "chain_in_rccl_dump": _chain(dump, busid),
@@ -187,3 +198,42 @@ def test_rccl_places_socket_nic_from_topology_file(native, tmp_path):
     r, dump = _rccl_dump(tmp_path, topo, {"NCCL_SOCKET_IFNAME": "=" + nic, "NCCL_IB_DISABLE": "1"}, tag="nic")
     assert r.returncode == 0, r.stderr[-3000:]
     assert _net_chain(dump, nic) == _net_chain(ET.fromstring(xml), nic)
+
+
+@pytest.mark.gpu
+def test_rccl_takes_nic_placement_from_the_topology_file(native, tmp_path, cuda_device):
+    """The mechanism the agent's file relies on, shown on a box whose rail NICs RCCL cannot use:
+    RCCL places a network device where the topology file puts it.  The file generated from this
+    box's sysfs names the visible GPU's rail NIC; here that <net> is renamed to the interface
+    RCCL's socket plugin really uses (a container veth without a PCI path), and RCCL's dump must
+    show that interface under the rail NIC's PCI function, i.e. behind the GPU's PCIe switch."""
+    from network_operator_amd.parallel.rail import device_bdf
+
+    gpu = device_bdf(0)
+    d = native.discover("/sys/")
+    pair = next((p for p in d["pairs"] if p["gpu"].lower() == gpu.lower()), None)
+    if pair is None:
+        pytest.skip(f"visible GPU {gpu} has no GPU-affine NIC on this box")
+    rdma = {n["ifname"]: n["rdma_dev"] for n in d["nics"]}
+    rail_name = rdma.get(pair["nic"]) or pair["nic"]
+    socket_if = next((i for i in sorted(_ipv4_ifaces()) if i != "lo"), None)
+    if socket_if is None:
+        pytest.skip("no IPv4 interface for RCCL's socket plugin")
+    xml = native.rccl_topo_xml("/sys/").replace(f'<net name="{rail_name}"', f'<net name="{socket_if}"')
+    mine = ET.fromstring(xml)
+    want = _net_chain(mine, socket_if)
+    nic_bdf = next(n["bdf"] for n in d["nics"] if n["ifname"] == pair["nic"])
+    assert want and want[-1] == nic_bdf, (want, nic_bdf)
+    topo = tmp_path / "rccl-topo.xml"
+    topo.write_text(xml)
+    r, dump = _rccl_dump(tmp_path, topo, {"NCCL_SOCKET_IFNAME": "=" + socket_if, "NCCL_IB_DISABLE": "1"},
+                         tag="placed")
+    assert r.returncode == 0, r.stderr[-3000:]
+    got = _net_chain(dump, socket_if)
+    assert got == want, (got, want, ET.tostring(dump)[:3000])
+    # ... and that is the GPU's switch: GPU and NIC share the outermost switch below the CPU.
+    assert _chain(dump, gpu.lower())[:2] == got[:2]
+    (ROOT / "gpurun_out").mkdir(exist_ok=True)
+    (ROOT / "gpurun_out" / "rccl_topo_nic_placed.json").write_text(json.dumps(
+        {"gpu": gpu, "rail_nic": pair["nic"], "socket_if": socket_if, "net_chain_in_file": want,
+         "net_chain_in_rccl_dump": got, "gpu_chain_in_rccl_dump": _chain(dump, gpu.lower())}, indent=1))
