@@ -198,20 +198,63 @@ def decode(buf: bytes):
 # ---------------------------------------------------------------------------
 # server
 # ---------------------------------------------------------------------------
-class FakeNetworkManagerBus:
-    """Serves one or more clients on a UNIX socket until ``stop``."""
+class NetworkManagerModel:
+    """The NetworkManager subset the agent uses (Version, GetAllDevices, Device.Interface and
+    Device.Managed), answering decoded method calls with encoded replies."""
 
     NM = "org.freedesktop.NetworkManager"
     NM_PATH = "/org/freedesktop/NetworkManager"
     DEV_IFACE = "org.freedesktop.NetworkManager.Device"
 
-    def __init__(self, path: str, devices: Dict[str, bool], nm_running: bool = True, fail_set: bool = False):
-        self.path = path
+    def __init__(self, devices: Dict[str, bool], nm_running: bool = True, fail_set: bool = False):
         self.devices = dict(devices)  # ifname -> Managed
         self.nm_running = nm_running
         self.fail_set = fail_set
         self.calls: List[Tuple[str, str, str]] = []
         self.auth_lines: List[str] = []
+
+    def _err(self, m, serial, name, text):
+        # Through a real bus a reply must be addressed to the caller's unique name.
+        return encode(3, serial, {"reply_serial": m["serial"], "error_name": name, "destination": m.get("sender")},
+                      "s", (text,))
+
+    def _handle(self, m, serial) -> bytes:
+        self.calls.append((m.get("path", ""), m.get("interface", ""), m.get("member", "")))
+        ret = lambda sig="", body=(): encode(2, serial, {"reply_serial": m["serial"],  # noqa: E731
+                                                         "destination": m.get("sender")}, sig, body)
+        member, iface, path = m.get("member"), m.get("interface"), m.get("path", "")
+        if iface == "org.freedesktop.DBus" and member == "Hello":
+            return ret("s", (":1.42",))
+        if m.get("destination") == self.NM and not self.nm_running:
+            return self._err(m, serial, "org.freedesktop.DBus.Error.ServiceUnknown",
+                             "The name org.freedesktop.NetworkManager was not provided by any .service files")
+        names = sorted(self.devices)
+        if iface == self.NM and member == "GetAllDevices":
+            return ret("ao", ([f"{self.NM_PATH}/Devices/{i + 1}" for i in range(len(names))],))
+        if iface == "org.freedesktop.DBus.Properties" and member == "Get":
+            want_iface, prop = m["body"]
+            if path == self.NM_PATH and prop == "Version":
+                return ret("v", (("s", "1.46.0"),))
+            if path.startswith(self.NM_PATH + "/Devices/") and prop == "Interface":
+                return ret("v", (("s", names[int(path.rsplit("/", 1)[1]) - 1]),))
+            if path.startswith(self.NM_PATH + "/Devices/") and prop == "Managed":
+                return ret("v", (("b", self.devices[names[int(path.rsplit("/", 1)[1]) - 1]]),))
+        if iface == "org.freedesktop.DBus.Properties" and member == "Set":
+            _, prop, (sig, val) = m["body"]
+            if prop == "Managed" and path.startswith(self.NM_PATH + "/Devices/"):
+                if self.fail_set:
+                    return self._err(m, serial, "org.freedesktop.NetworkManager.PermissionDenied", "not authorized")
+                self.devices[names[int(path.rsplit("/", 1)[1]) - 1]] = bool(val)
+                return ret()
+        return self._err(m, serial, "org.freedesktop.DBus.Error.UnknownMethod", f"no method {iface}.{member}")
+
+
+class FakeNetworkManagerBus(NetworkManagerModel):
+    """Serves one or more clients on a UNIX socket until ``stop``, as if it were the bus."""
+
+    def __init__(self, path: str, devices: Dict[str, bool], nm_running: bool = True, fail_set: bool = False):
+        super().__init__(devices, nm_running, fail_set)
+        self.path = path
         self._sock = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
         if os.path.exists(path):
             os.unlink(path)
@@ -281,52 +324,13 @@ class FakeNetworkManagerBus:
         finally:
             c.close()
 
-    def _err(self, m, serial, name, text):
-        # Through a real bus a reply must be addressed to the caller's unique name.
-        return encode(3, serial, {"reply_serial": m["serial"], "error_name": name, "destination": m.get("sender")},
-                      "s", (text,))
 
-    def _handle(self, m, serial) -> bytes:
-        self.calls.append((m.get("path", ""), m.get("interface", ""), m.get("member", "")))
-        ret = lambda sig="", body=(): encode(2, serial, {"reply_serial": m["serial"],  # noqa: E731
-                                                         "destination": m.get("sender")}, sig, body)
-        member, iface, path = m.get("member"), m.get("interface"), m.get("path", "")
-        if iface == "org.freedesktop.DBus" and member == "Hello":
-            return ret("s", (":1.42",))
-        if m.get("destination") == self.NM and not self.nm_running:
-            return self._err(m, serial, "org.freedesktop.DBus.Error.ServiceUnknown",
-                             "The name org.freedesktop.NetworkManager was not provided by any .service files")
-        names = sorted(self.devices)
-        if iface == self.NM and member == "GetAllDevices":
-            return ret("ao", ([f"{self.NM_PATH}/Devices/{i + 1}" for i in range(len(names))],))
-        if iface == "org.freedesktop.DBus.Properties" and member == "Get":
-            want_iface, prop = m["body"]
-            if path == self.NM_PATH and prop == "Version":
-                return ret("v", (("s", "1.46.0"),))
-            if path.startswith(self.NM_PATH + "/Devices/") and prop == "Interface":
-                return ret("v", (("s", names[int(path.rsplit("/", 1)[1]) - 1]),))
-            if path.startswith(self.NM_PATH + "/Devices/") and prop == "Managed":
-                return ret("v", (("b", self.devices[names[int(path.rsplit("/", 1)[1]) - 1]]),))
-        if iface == "org.freedesktop.DBus.Properties" and member == "Set":
-            _, prop, (sig, val) = m["body"]
-            if prop == "Managed" and path.startswith(self.NM_PATH + "/Devices/"):
-                if self.fail_set:
-                    return self._err(m, serial, "org.freedesktop.NetworkManager.PermissionDenied", "not authorized")
-                self.devices[names[int(path.rsplit("/", 1)[1]) - 1]] = bool(val)
-                return ret()
-        return self._err(m, serial, "org.freedesktop.DBus.Error.UnknownMethod", f"no method {iface}.{member}")
-
-
-class NetworkManagerOnBus(FakeNetworkManagerBus):
+class NetworkManagerOnBus(NetworkManagerModel):
     """Owns ``org.freedesktop.NetworkManager`` on a real bus (a client of ``dbus-daemon``) and
     answers the same calls as ``FakeNetworkManagerBus``."""
 
-    def __init__(self, address: str, devices: Dict[str, bool], fail_set: bool = False):  # noqa: super not called
-        self.devices = dict(devices)
-        self.nm_running = True
-        self.fail_set = fail_set
-        self.calls: List[Tuple[str, str, str]] = []
-        self.auth_lines: List[str] = []
+    def __init__(self, address: str, devices: Dict[str, bool], fail_set: bool = False):
+        super().__init__(devices, nm_running=True, fail_set=fail_set)
         self._stop = False
         path = address.split("unix:path=", 1)[1].split(",", 1)[0]
         self._c = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
@@ -346,10 +350,6 @@ class NetworkManagerOnBus(FakeNetworkManagerBus):
             raise RuntimeError(f"could not own {self.NM}: RequestName -> {owner}")
         self._thread = threading.Thread(target=self._loop, daemon=True)
         self._thread.start()
-
-    @property
-    def address(self) -> str:  # the bus the agent must use is the daemon's, not ours
-        raise AttributeError("use BusDaemon.address")
 
     def _line(self) -> str:
         b = b""
