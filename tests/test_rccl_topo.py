@@ -20,6 +20,8 @@ import xml.etree.ElementTree as ET
 from pathlib import Path
 
 import pytest
+from hypothesis import given, settings
+from hypothesis import strategies as st
 
 from network_operator_amd.testing import fakesysfs
 
@@ -237,3 +239,59 @@ def test_rccl_takes_nic_placement_from_the_topology_file(native, tmp_path, cuda_
     (ROOT / "gpurun_out" / "rccl_topo_nic_placed.json").write_text(json.dumps(
         {"gpu": gpu, "rail_nic": pair["nic"], "socket_if": socket_if, "net_chain_in_file": want,
          "net_chain_in_rccl_dump": got, "gpu_chain_in_rccl_dump": _chain(dump, gpu.lower())}, indent=1))
+
+
+def _nccl_fold(components):
+    """Independent re-statement of NCCL's ncclTopoGetXmlFromSys parent walk (src/graph/xml.cc):
+    from a device's sysfs path, strip one component at a time; a non-BDF component is the root
+    complex (-> CPU); every second BDF component is the next parent.  Returns the parents,
+    outermost first."""
+    path = list(components)
+    parents = []
+    while True:
+        count = 0
+        parent = None
+        while len(path) > 1:
+            path.pop()
+            count += 1
+            last = path[-1]
+            is_bdf = len(last) == 12 and last[4] == ":" and last[7] == ":" and last[10] == "."
+            if not is_bdf:
+                return list(reversed(parents))  # CPU
+            if count == 2:
+                parent = last
+                break
+        if parent is None:
+            return list(reversed(parents))
+        parents.append(parent)
+
+
+@settings(max_examples=60, deadline=None)
+@given(depth=st.integers(min_value=1, max_value=9), seed=st.integers(min_value=0, max_value=2 ** 16))
+def test_pci_folding_matches_nccl_walk(native, depth, seed):
+    import random
+    import tempfile
+
+    rng = random.Random(seed)
+    bus = rng.randrange(0, 0xe0)
+    comps = [f"pci0000:{bus:02x}"] + [f"0000:{(bus + i) % 256:02x}:{rng.randrange(32):02x}.{rng.randrange(8)}"
+                                      for i in range(depth)]
+    with tempfile.TemporaryDirectory() as t:
+        root = Path(t)
+        d = root / "devices" / "/".join(comps)
+        for k in range(1, len(comps) + 1):
+            p = root / "devices" / "/".join(comps[:k])
+            p.mkdir(parents=True, exist_ok=True)
+            if k > 1:
+                (p / "class").write_text("0x060400\n")
+                (p / "numa_node").write_text("0\n")
+        (d / "class").write_text("0x120000\n")
+        (d / "vendor").write_text("0x1002\n")
+        drv = root / "bus" / "pci" / "drivers" / "amdgpu"
+        drv.mkdir(parents=True)
+        (drv / comps[-1]).symlink_to(d)
+        (d / "driver").symlink_to(drv)
+        xml = ET.fromstring(native.rccl_topo_xml(str(root) + "/", cpu=fakesysfs.MI355X_HOST_CPU))
+        chain = _chain(xml, comps[-1])
+        assert chain is not None
+        assert chain[1:-1] == _nccl_fold(comps), (comps, chain)
