@@ -12,6 +12,8 @@ the same 422 Invalid answers a real cluster would give.
 
 from __future__ import annotations
 
+import re
+
 import sys
 from pathlib import Path
 from typing import Any, List
@@ -75,6 +77,12 @@ def openapi_schema() -> dict:
                                              "priority railTableBase+k (its /30 and its /16 via the switch), so traffic\n"
                                              "from a rail's address leaves through that rail.  0 = off.",
                               "maximum": 200, "minimum": 0, "type": "integer"},
+            "rcclSocketIfname": {"description": "NCCL_SOCKET_IFNAME written into rccl.env: auto (L3: the configured\n"
+                                                "scale-out NICs in GPU order, so bootstrap meets on rail 0; L2: not set),\n"
+                                                "none (not set: RCCL picks, usually the management network), or a\n"
+                                                "comma-separated interface list.  Empty = auto.",
+                                 "pattern": r"^(auto|none|[A-Za-z0-9_.:@-]{1,15}(,[A-Za-z0-9_.:@-]{1,15})*)$",
+                                 "type": "string"},
         },
     }
     host_nic = {
@@ -222,6 +230,8 @@ def _validate(value: Any, schema: dict, path: str, errs: List[str]) -> None:
         errs.append(f"{path}: Invalid value: {value}: {path} in body should be less than or equal to {schema['maximum']}")
     if "maxLength" in schema and isinstance(value, str) and len(value) > schema["maxLength"]:
         errs.append(f"{path}: Too long: may not be longer than {schema['maxLength']}")
+    if "pattern" in schema and isinstance(value, str) and not re.search(schema["pattern"], value):
+        errs.append(f'{path}: Invalid value: "{value}": {path} in body should match \'{schema["pattern"]}\'')
     if isinstance(value, dict):
         for r in schema.get("required", []):
             if r not in value:

@@ -62,11 +62,12 @@ class AmdScaleOutSpec:
     gpuDirectRdma: str = ""
     rcclEnv: Dict[str, str] = field(default_factory=dict)
     railTableBase: int = 0
+    rcclSocketIfname: str = ""
     extra: Dict[str, Any] = field(default_factory=dict)
 
     _FIELDS = ("disableNetworkManager", "layer", "image", "pullPolicy", "mtu", "xgmiCheck", "lldpAnnounce",
                "interfaces", "nicDrivers", "disableFirmwareLldp", "metricsPort", "gpuDirectRdma", "rcclEnv",
-               "railTableBase")
+               "railTableBase", "rcclSocketIfname")
 
     def to_dict(self) -> dict:
         d: dict = {}
@@ -96,6 +97,8 @@ class AmdScaleOutSpec:
             d["rcclEnv"] = dict(self.rcclEnv)
         if self.railTableBase:
             d["railTableBase"] = self.railTableBase
+        if self.rcclSocketIfname:
+            d["rcclSocketIfname"] = self.rcclSocketIfname
         d.update(copy.deepcopy(self.extra))
         return d
 
@@ -117,6 +120,7 @@ class AmdScaleOutSpec:
             gpuDirectRdma=d.pop("gpuDirectRdma", "") or "",
             rcclEnv=dict(d.pop("rcclEnv", {}) or {}),
             railTableBase=int(d.pop("railTableBase", 0) or 0),
+            rcclSocketIfname=d.pop("rcclSocketIfname", "") or "",
         )
         s.extra = d
         return s

@@ -159,6 +159,8 @@ def agent_args(p: T.NetworkClusterPolicy) -> List[str]:
         args.append(f"--metrics-bind-address=:{so.metricsPort}")
     if so.railTableBase and so.layer == "L3":
         args.append(f"--rail-table-base={so.railTableBase}")
+    if so.rcclSocketIfname:
+        args.append(f"--rccl-socket-ifname={so.rcclSocketIfname}")
     if so.rcclEnv:
         args.append("--rccl-env-extra=" + ",".join(f"{k}={v}" for k, v in sorted(so.rcclEnv.items())))
     if so.gpuDirectRdma:

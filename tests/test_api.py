@@ -227,3 +227,22 @@ def test_webhooks_end_to_end(tmp_path, resource, called):
         await fake.stop()
 
     asyncio.run(asyncio.wait_for(body(), 60))
+
+
+def test_rccl_socket_ifname_field_validated_and_passed_to_the_agent():
+    from network_operator_amd.api.v1alpha1 import crd as CRD2
+    from network_operator_amd.operator.reconciler import agent_args
+
+    def pol(v):
+        p = T.new_policy("p", rcclSocketIfname=v).to_dict()
+        return p, CRD2.validate(p)
+
+    for ok in ("auto", "none", "enp8s0np0", "enp8s0np0,enp33s0np0"):
+        p, errs = pol(ok)
+        assert errs == [], (ok, errs)
+        assert f"--rccl-socket-ifname={ok}" in agent_args(T.NetworkClusterPolicy.from_dict(p))
+    for bad in ("", "a b", "x,", "waytoolonginterfacename0", "eth0;rm -rf"):
+        if bad == "":
+            assert "--rccl-socket-ifname" not in " ".join(agent_args(T.new_policy("p")))
+            continue
+        assert pol(bad)[1], bad
