@@ -99,6 +99,13 @@ struct Config {
     // its rules and routes carry protocol kRailProtocol and it never deletes any other.  0 = off
     // (the reference's main-table-only routing).
     int rail_table_base = 0;
+    // LLDP cache (artifacts.hpp): configure from the last confirmed Port Description at start,
+    // then require a real frame to confirm it within lldp_cache_confirm_ns (else the NIC counts
+    // as degraded and the label is withdrawn until one arrives).  "" = off.  Used only with
+    // --keep-running and the monitor (which does the confirming).
+    std::string lldp_cache;
+    int64_t lldp_cache_max_age_ns = 7LL * 24 * 3600 * 1000000000;  // older entries are ignored
+    int64_t lldp_cache_confirm_ns = 95LL * 1000000000;              // 3 x msgTxInterval + 5 s
 };
 
 // FRA_PROTOCOL / rtm_protocol tag on the agent's rail rules and rail-table routes ("installed by
@@ -203,6 +210,11 @@ class Agent {
     std::vector<std::pair<std::string, std::string>> rccl_env_extra_;
     void disable_fw_lldp();
     void restore_network_manager();
+    int apply_lldp_cache();  // NICs addressed from the cache
+    // A frame for a NIC that already has an address: confirms a cached Port Description or moves
+    // the NIC to the new one.  True when the NIC's status changed.
+    bool refresh_from_frame(NicState& n, const lldp::Frame& f);
+    void save_lldp_cache();
     bool nm_keyfile_written_ = false;
     std::vector<std::string> nm_unmanaged_;
 

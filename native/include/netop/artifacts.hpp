@@ -120,6 +120,19 @@ std::string generate_labels(const std::map<std::string, std::string>& extra,
 bool write_labels(const Labels& l, const std::map<std::string, std::string>& extra);
 bool remove_labels(const Labels& l);
 
+// LLDP cache (--lldp-cache): the last Port Description each NIC confirmed from a real frame,
+// so a restarted agent (DaemonSet upgrade, crash, node reboot) configures at once instead of
+// waiting up to msgTxInterval for a switch that does not fast-start; the monitor then expects
+// the switch to confirm it.  One line per NIC, tab-separated:
+//   <nic mac> <ifname> <unix seconds> <peer mac|-> <system name> <port id> <port description>
+struct LldpCacheEntry {
+    std::string nic_mac, ifname;
+    int64_t unix_s = 0;
+    std::string peer_mac, system_name, port_id, port_description;
+};
+std::vector<LldpCacheEntry> read_lldp_cache(const std::string& path);  // [] when absent / unreadable
+void write_lldp_cache(const std::string& path, const std::vector<LldpCacheEntry>& entries);
+
 // Agent status document (phase timings, per-NIC results) for observability and the bench.
 std::string generate_status(const std::vector<NicState>& nics, const std::map<std::string, int64_t>& phases_ns,
                             int64_t t0_mono, const std::string& mode, bool ready,

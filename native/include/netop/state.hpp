@@ -28,6 +28,9 @@ struct NicState {
     std::optional<MacAddr> peer_mac;
     std::string peer_system_name;
     std::string peer_port_id;
+    bool lldp_from_cache = false;  // addressed from --lldp-cache, not yet confirmed by a frame
+    bool cache_stale = false;      // the switch did not confirm the cached Port Description in time
+    int64_t t_cache_applied = 0;
 
     // L3
     std::optional<l3::P2pAddressing> addr;

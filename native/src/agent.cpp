@@ -9,6 +9,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <ctime>
 #include <set>
 
 #include "netop/log.hpp"
@@ -520,6 +521,97 @@ void Agent::on_lldp(NicState& n, const lldp::Frame& f) {
     }
 }
 
+bool Agent::refresh_from_frame(NicState& n, const lldp::Frame& f) {
+    std::string desc = f.port_description.value_or("");
+    bool changed = false;
+    if (n.lldp_from_cache) {
+        n.lldp_from_cache = false;
+        changed = true;  // status: lldp_source and, if it was flagged, cache_unconfirmed
+        n.cache_stale = false;
+        if (desc == n.port_description) {
+            NLOG_I("interface '%s': the switch confirmed the cached Port Description", n.ifname.c_str());
+            n.peer_mac = f.peer_mac();
+            n.peer_system_name = f.system_name.value_or("");
+            n.peer_port_id = f.port_id_str();
+            save_lldp_cache();
+            return changed;
+        }
+    }
+    if (desc == n.port_description) return changed;
+    NLOG_I("Port Description of '%s' changed: '%s' -> '%s'", n.ifname.c_str(), n.port_description.c_str(), desc.c_str());
+    auto old = n.addr;
+    on_lldp(n, f);
+    if (n.addr && old && n.addr->local == old->local) return changed;
+    // drop the old address (its /30 and /16 routes go with it) and the rail rule and routes
+    // installed for it, then configure the new one
+    remove_rail_routing(n);
+    try {
+        for (auto& a : ops_.addr_list(n.link.index, AF_INET)) ops_.addr_del(a);
+    } catch (const std::exception& e) {
+        NLOG_W("could not remove old address of '%s': %s", n.ifname.c_str(), e.what());
+    }
+    n.configured = false;
+    n.gid_index.reset();  // the GID follows the address
+    if (n.addr) configure_interface(n);
+    ++reconfigs_;
+    save_lldp_cache();
+    return true;
+}
+
+int Agent::apply_lldp_cache() {
+    if (cfg_.lldp_cache.empty() || !cfg_.keep_running || !cfg_.monitor) return 0;
+    const auto entries = artifacts::read_lldp_cache(cfg_.lldp_cache);
+    const int64_t now = int64_t(::time(nullptr));
+    int applied = 0;
+    for (auto& n : nics_) {
+        if (!n.link.up() || n.lldp_seen) continue;
+        for (const auto& e : entries) {
+            if (e.ifname != n.ifname || e.nic_mac != n.link.mac.str()) continue;  // another NIC now
+            if (now - e.unix_s > cfg_.lldp_cache_max_age_ns / 1000000000 || e.unix_s > now + 60) break;
+            std::string err;
+            auto addr = l3::parse_port_description(e.port_description, cfg_.token_policy, &err);
+            if (!addr) break;
+            n.lldp_seen = true;
+            n.lldp_from_cache = true;
+            n.t_lldp = n.t_cache_applied = mono_ns();
+            n.port_description = e.port_description;
+            n.peer_mac = MacAddr::parse(e.peer_mac);
+            n.peer_system_name = e.system_name;
+            n.peer_port_id = e.port_id;
+            n.addr = addr;
+            n.addr_error.clear();
+            NLOG_I("interface '%s': Port Description '%s' from the LLDP cache (%llds old), awaiting confirmation",
+                   n.ifname.c_str(), e.port_description.c_str(), (long long)(now - e.unix_s));
+            if (cfg_.pipeline && cfg_.configure) configure_interface(n);
+            ++applied;
+            break;
+        }
+    }
+    return applied;
+}
+
+void Agent::save_lldp_cache() {
+    if (cfg_.lldp_cache.empty()) return;
+    const auto old = artifacts::read_lldp_cache(cfg_.lldp_cache);
+    std::vector<artifacts::LldpCacheEntry> out;
+    const int64_t now = int64_t(::time(nullptr));
+    for (const auto& n : nics_) {
+        if (!n.lldp_seen || !n.addr) continue;
+        if (n.lldp_from_cache) {  // not confirmed yet: keep the entry (and its age) as it was
+            for (const auto& e : old)
+                if (e.ifname == n.ifname && e.nic_mac == n.link.mac.str()) out.push_back(e);
+            continue;
+        }
+        out.push_back({n.link.mac.str(), n.ifname, now, n.peer_mac ? n.peer_mac->str() : "", n.peer_system_name,
+                       n.peer_port_id, n.port_description});
+    }
+    try {
+        artifacts::write_lldp_cache(cfg_.lldp_cache, out);
+    } catch (const std::exception& e) {
+        NLOG_W("Could not write the LLDP cache: %s", e.what());
+    }
+}
+
 void Agent::detect_lldp(int stop_fd) {
     int listening = 0;
     for (auto& n : nics_) {
@@ -536,11 +628,20 @@ void Agent::detect_lldp(int stop_fd) {
         }
     }
     if (!listening) return;
-    int remaining = listening;
+    int remaining = listening - apply_lldp_cache();
+    if (remaining <= 0) {
+        NLOG_I("Every listening interface was configured from the LLDP cache; the switch confirms it while monitoring");
+        return;
+    }
     auto cb = [&](const std::string& ifname, const lldp::Frame& f) -> bool {
         if (f.ttl == 0) return false;  // shutdown LLDPDU: the neighbour is going away
         for (auto& n : nics_) {
-            if (n.ifname != ifname || n.lldp_seen) continue;  // first frame per NIC wins (client.go:141-142)
+            if (n.ifname != ifname) continue;
+            if (n.lldp_from_cache) {  // configured from the cache: confirm it, or readdress now
+                refresh_from_frame(n, f);
+                continue;
+            }
+            if (n.lldp_seen) continue;  // first frame per NIC wins (client.go:141-142)
             on_lldp(n, f);
             if (cfg_.pipeline && cfg_.configure && n.addr) configure_interface(n);
             --remaining;
@@ -742,6 +843,7 @@ void Agent::write_artifacts() {
         }
     }
     write_rccl_env_file();
+    save_lldp_cache();
     if (!cfg_.networkd.empty()) {
         try {
             artifacts::write_networkd(cfg_.networkd, nics_);
@@ -1033,7 +1135,7 @@ void Agent::announce_all(uint16_t ttl) {
 }
 
 bool Agent::nic_healthy(const NicState& n) const {
-    if (!n.link.up() || n.degraded) return false;
+    if (!n.link.up() || n.degraded || n.cache_stale) return false;
     return cfg_.mode != "L3" || n.configured;
 }
 
@@ -1080,32 +1182,19 @@ void Agent::monitor(int stop_fd) {
         bool changed = false;
         auto on_frame = [&](const std::string& ifname, const lldp::Frame& f) -> bool {
             if (f.ttl == 0) return false;
-            for (auto& n : nics_) {
-                if (n.ifname != ifname) continue;
-                std::string desc = f.port_description.value_or("");
-                if (desc == n.port_description) continue;
-                NLOG_I("Port Description of '%s' changed: '%s' -> '%s'", ifname.c_str(), n.port_description.c_str(), desc.c_str());
-                auto old = n.addr;
-                on_lldp(n, f);
-                if (n.addr && old && n.addr->local == old->local) continue;
-                // drop the old address (its /30 and /16 routes go with it) and the rail rule and
-                // routes installed for it, then configure the new one
-                remove_rail_routing(n);
-                try {
-                    for (auto& a : ops_.addr_list(n.link.index, AF_INET)) ops_.addr_del(a);
-                } catch (const std::exception& e) {
-                    NLOG_W("could not remove old address of '%s': %s", ifname.c_str(), e.what());
-                }
-                n.configured = false;
-                n.gid_index.reset();  // the GID follows the address
-                if (n.addr) configure_interface(n);
-                ++reconfigs_;
-                changed = true;
-            }
+            for (auto& n : nics_)
+                if (n.ifname == ifname && refresh_from_frame(n, f)) changed = true;
             return false;
         };
         lldp_->run(std::min(next_tx, mono_ns() + cfg_.monitor_tick_ns), on_frame, wait_fd);
         if (fd_readable(stop_fd)) return;
+        for (auto& n : nics_) {  // a cached Port Description the switch never confirmed
+            if (!n.lldp_from_cache || n.cache_stale || mono_ns() - n.t_cache_applied < cfg_.lldp_cache_confirm_ns) continue;
+            NLOG_W("interface '%s': no LLDP frame confirmed the cached Port Description within %s",
+                   n.ifname.c_str(), format_go_duration(cfg_.lldp_cache_confirm_ns).c_str());
+            n.cache_stale = true;
+            changed = true;
+        }
         // Link state.
         if (watcher) {
             for (auto& ev : watcher->wait(mono_ns())) {

@@ -410,6 +410,49 @@ bool write_labels(const Labels& l, const std::map<std::string, std::string>& ext
 bool remove_labels(const Labels& l) { return ::unlink(l.path().c_str()) == 0; }
 
 // ---------------------------------------------------------------------------
+// LLDP cache
+// ---------------------------------------------------------------------------
+static const char* const kLldpCacheHeader = "# netop-lldp-cache v1";
+
+static std::string one_field(const std::string& s) {
+    std::string o = s;
+    for (char& c : o)
+        if (c == '\t' || c == '\n' || c == '\r') c = ' ';
+    return o.empty() ? "-" : o;
+}
+
+std::vector<LldpCacheEntry> read_lldp_cache(const std::string& path) {
+    std::vector<LldpCacheEntry> out;
+    auto text = read_file(path);
+    if (!text) return out;
+    auto lines = split(*text, '\n');
+    if (lines.empty() || trim(lines[0]) != kLldpCacheHeader) return out;  // unknown format: ignore
+    for (size_t i = 1; i < lines.size(); ++i) {
+        auto f = split(lines[i], '\t');
+        if (f.size() != 7) continue;
+        LldpCacheEntry e;
+        e.nic_mac = f[0];
+        e.ifname = f[1];
+        e.unix_s = std::strtoll(f[2].c_str(), nullptr, 10);
+        e.peer_mac = f[3] == "-" ? "" : f[3];
+        e.system_name = f[4] == "-" ? "" : f[4];
+        e.port_id = f[5] == "-" ? "" : f[5];
+        e.port_description = f[6] == "-" ? "" : f[6];
+        out.push_back(std::move(e));
+    }
+    return out;
+}
+
+void write_lldp_cache(const std::string& path, const std::vector<LldpCacheEntry>& entries) {
+    std::string out = std::string(kLldpCacheHeader) + "\n";
+    for (const auto& e : entries)
+        out += one_field(e.nic_mac) + "\t" + one_field(e.ifname) + "\t" + std::to_string(e.unix_s) + "\t" +
+               one_field(e.peer_mac) + "\t" + one_field(e.system_name) + "\t" + one_field(e.port_id) + "\t" +
+               one_field(e.port_description) + "\n";
+    write_file_atomic(path, out, 0644);
+}
+
+// ---------------------------------------------------------------------------
 // Status document
 // ---------------------------------------------------------------------------
 std::string generate_status(const std::vector<NicState>& nics, const std::map<std::string, int64_t>& phases_ns,
@@ -434,6 +477,8 @@ std::string generate_status(const std::vector<NicState>& nics, const std::map<st
         if (!n->fw_lldp.empty()) j.key("fw_lldp").value(n->fw_lldp);
         j.key("lldp").value(n->lldp_seen);
         if (n->lldp_seen) {
+            j.key("lldp_source").value(n->lldp_from_cache ? "cache" : "frame");
+            if (n->cache_stale) j.key("cache_unconfirmed").value(true);
             j.key("port_description").value(n->port_description);
             if (n->peer_mac) j.key("peer_mac").value(n->peer_mac->str());
             j.key("peer_system").value(n->peer_system_name);

@@ -1,4 +1,5 @@
 #include <arpa/inet.h>
+#include <ctime>
 #include <fcntl.h>
 #include <poll.h>
 #include <netinet/in.h>
@@ -8,6 +9,7 @@
 #include "check.hpp"
 #include "fake_netops.hpp"
 #include "netop/agent.hpp"
+#include "netop/artifacts.hpp"
 #include "netop/common.hpp"
 #include "tmpdir.hpp"
 
@@ -898,4 +900,144 @@ TEST(agent_retries_with_a_fresh_neighbour_when_the_answer_is_lost) {
     CHECK_EQ(s->sent[2].second, 0);
     int64_t dt = mono_ns() - t0;
     CHECK(dt >= 20000000LL && dt < 200000000LL);
+}
+
+namespace {
+void write_cache(Fixture& f, int64_t age_s, const char* ens1_desc = "no-alert 10.200.0.6/30") {
+    int64_t t = int64_t(::time(nullptr)) - age_s;
+    artifacts::write_lldp_cache(f.cfg.lldp_cache,
+                                {{"02:00:00:00:00:10", "ens0", t, "02:aa:00:00:00:00", "tor", "p", "no-alert 10.200.0.2/30"},
+                                 {"02:00:00:00:00:11", "ens1", t, "02:aa:00:00:00:01", "tor", "p", ens1_desc},
+                                 {"02:00:00:00:00:12", "ens2", t, "02:aa:00:00:00:02", "tor", "p", "no-alert 10.200.0.9/30"}});
+}
+}  // namespace
+
+TEST(lldp_cache_roundtrip_sanitises_fields) {
+    TmpDir tmp;
+    std::string p = tmp.path + "/lldp-cache";
+    artifacts::write_lldp_cache(p, {{"02:00:00:00:00:10", "ens0", 1700000000, "", "tor\tA", "", "no-alert\n10.0.0.2/30"}});
+    auto e = artifacts::read_lldp_cache(p);
+    CHECK_EQ(e.size(), size_t(1));
+    CHECK_EQ(e[0].unix_s, int64_t(1700000000));
+    CHECK_EQ(e[0].peer_mac, std::string(""));
+    CHECK_EQ(e[0].system_name, std::string("tor A"));
+    CHECK_EQ(e[0].port_description, std::string("no-alert 10.0.0.2/30"));
+    write_file_atomic(p, "something else\n", 0644);  // unknown format: ignored, not misparsed
+    CHECK(artifacts::read_lldp_cache(p).empty());
+    CHECK(artifacts::read_lldp_cache(tmp.path + "/absent").empty());
+}
+
+TEST(agent_lldp_cache_configures_before_any_frame_then_the_switch_confirms) {
+    Fixture f;
+    f.cfg.monitor_tick_ns = 1000000;
+    f.cfg.lldp_cache = f.tmp.path + "/lldp-cache";
+    write_cache(f, 3600);
+    Pipe stop;
+    auto src = std::make_unique<ScriptedLldp>();  // the switch stays silent at first
+    ScriptedLldp* raw = src.get();
+    agent::Agent a(f.cfg, f.ops, std::move(src), f.nm());
+    bool ready_from_cache = false, confirmed = false;
+    a.on_monitor_tick = [&](int tick) {
+        if (tick == 0) {
+            ready_from_cache = path_exists(f.cfg.labels.path()) && f.ops.addrs.size() == 3;
+            auto st = read_file(f.cfg.status_file);
+            ready_from_cache &= st && st->find("\"lldp_source\":\"cache\"") != std::string::npos;
+            auto s2 = f.all_valid();
+            raw->frames = s2->frames;
+        } else if (tick == 2) {
+            auto st = read_file(f.cfg.status_file);
+            confirmed = st && st->find("\"lldp_source\":\"cache\"") == std::string::npos &&
+                        st->find("\"lldp_source\":\"frame\"") != std::string::npos;
+            stop.fire();
+        }
+    };
+    a.run(stop.fd[0]);
+    CHECK(ready_from_cache);
+    CHECK(confirmed);
+    CHECK_EQ(a.reconfigurations(), 0);
+    for (auto& e : artifacts::read_lldp_cache(f.cfg.lldp_cache))  // confirmed: timestamps refreshed
+        CHECK(e.unix_s > int64_t(::time(nullptr)) - 60);
+}
+
+TEST(agent_lldp_cache_unconfirmed_withdraws_the_label_until_a_frame_arrives) {
+    Fixture f;
+    f.cfg.monitor_tick_ns = 1000000;
+    f.cfg.lldp_cache = f.tmp.path + "/lldp-cache";
+    f.cfg.lldp_cache_confirm_ns = 30000000;  // 30 ms
+    write_cache(f, 60);
+    Pipe stop;
+    auto src = std::make_unique<ScriptedLldp>();
+    ScriptedLldp* raw = src.get();
+    agent::Agent a(f.cfg, f.ops, std::move(src), f.nm());
+    bool withdrawn = false, restored = false;
+    int64_t t_start = mono_ns();
+    int phase = 0;
+    a.on_monitor_tick = [&](int) {
+        if (phase == 0 && mono_ns() - t_start > 200000000) {
+            withdrawn = !path_exists(f.cfg.labels.path());
+            auto st = read_file(f.cfg.status_file);
+            withdrawn &= st && st->find("\"cache_unconfirmed\":true") != std::string::npos;
+            auto s2 = f.all_valid();
+            raw->frames = s2->frames;
+            phase = 1;
+        } else if (phase == 1 && path_exists(f.cfg.labels.path())) {
+            restored = true;
+            stop.fire();
+        } else if (mono_ns() - t_start > 2000000000LL) {
+            stop.fire();
+        }
+    };
+    a.run(stop.fd[0]);
+    CHECK(withdrawn);
+    CHECK(restored);
+}
+
+TEST(agent_lldp_cache_wrong_entry_is_corrected_by_the_first_frame) {
+    Fixture f;
+    f.cfg.monitor_tick_ns = 1000000;
+    f.cfg.lldp_cache = f.tmp.path + "/lldp-cache";
+    write_cache(f, 60, "no-alert 10.201.7.2/30");  // ens1's port was re-addressed while we were down
+    Pipe stop;
+    agent::Agent a(f.cfg, f.ops, f.all_valid(), f.nm());
+    a.on_monitor_tick = [&](int tick) {
+        if (tick == 1) stop.fire();
+    };
+    a.run(stop.fd[0]);
+    bool has_new = false, has_old = false;
+    for (auto& n : a.nics())
+        if (n.ifname == "ens1") has_new = n.addr && n.addr->local.str() == "10.200.0.5";
+    for (auto& ad : f.ops.addrs) has_old |= ad.local.str() == "10.201.7.1";
+    CHECK(has_new);
+    CHECK(!has_old);
+    for (auto& e : artifacts::read_lldp_cache(f.cfg.lldp_cache))
+        if (e.ifname == "ens1") CHECK_EQ(e.port_description, std::string("no-alert 10.200.0.6/30"));
+    CHECK_EQ(a.reconfigurations(), 1);
+}
+
+TEST(agent_lldp_cache_ignores_old_foreign_and_unmonitored_entries) {
+    for (int variant = 0; variant < 3; ++variant) {
+        Fixture f;
+        f.cfg.lldp_cache = f.tmp.path + "/lldp-cache";
+        f.cfg.wait_ns = 20000000;
+        if (variant == 0) write_cache(f, 8 * 24 * 3600);  // older than max age
+        if (variant == 1) {                              // the NICs were swapped: different MACs
+            write_cache(f, 60);
+            auto e = artifacts::read_lldp_cache(f.cfg.lldp_cache);
+            for (auto& x : e) x.nic_mac = "02:00:00:00:99:99";
+            artifacts::write_lldp_cache(f.cfg.lldp_cache, e);
+        }
+        if (variant == 2) {  // no monitor to confirm it: the cache is not used
+            write_cache(f, 60);
+            f.cfg.keep_running = false;
+        }
+        agent::Agent a(f.cfg, f.ops, std::make_unique<ScriptedLldp>(), f.nm());
+        Pipe stop;
+        stop.fire();
+        try {
+            a.run(stop.fd[0]);
+        } catch (const std::exception&) {
+        }
+        CHECK(f.ops.addrs.empty());
+        CHECK(!a.ready());
+    }
 }

@@ -73,6 +73,9 @@ int main(int argc, char** argv) {
     fs.add_duration("gid-wait", &cfg.gid_wait_ns, "time to wait for the RoCE v2 GID of a newly configured address");
     fs.add_bool("lldp-announce", &cfg.lldp_announce, "transmit our own LLDPDU on each NIC (makes 802.1AB-2009 switches answer within ~1s)");
     fs.add_bool("lldp-restart-fast", &cfg.announce_shutdown_first, "send a shutdown LLDPDU before the first announcement so a switch holding a stale entry (agent restart) fast-starts again");
+    fs.add_string("lldp-cache", &cfg.lldp_cache, "with --keep-running: remember each NIC's confirmed Port Description in this file and configure from it at start (the switch must confirm it within --lldp-cache-confirm)");
+    fs.add_duration("lldp-cache-max-age", &cfg.lldp_cache_max_age_ns, "ignore LLDP cache entries older than this");
+    fs.add_duration("lldp-cache-confirm", &cfg.lldp_cache_confirm_ns, "withdraw readiness if no LLDP frame confirms a cached Port Description within this time");
     fs.add_string("node-name", &cfg.node_name, "LLDP System Name (default $NODE_NAME, else the hostname)");
     fs.add_bool("monitor", &cfg.monitor, "with --keep-running: keep announcing LLDP, withdraw the label on link loss, re-configure on Port Description changes");
     fs.add_duration("lldp-tx-interval", &cfg.lldp_tx_interval_ns, "LLDP keep-alive transmit interval while monitoring");

@@ -83,6 +83,11 @@ def openapi_schema() -> dict:
                                                 "comma-separated interface list.  Empty = auto.",
                                  "pattern": r"^(auto|none|[A-Za-z0-9_.:@-]{1,15}(,[A-Za-z0-9_.:@-]{1,15})*)$",
                                  "type": "string"},
+            "lldpCache": {"description": "L3: remember each NIC's last confirmed Port Description on the node, so a\n"
+                                         "restarted agent configures at once instead of waiting for the switch's next\n"
+                                         "periodic LLDPDU (switches without fast start).  The switch must confirm it\n"
+                                         "within 95 s, else the readiness label is withdrawn until it does.",
+                          "type": "boolean"},
         },
     }
     host_nic = {

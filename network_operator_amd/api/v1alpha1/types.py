@@ -63,11 +63,12 @@ class AmdScaleOutSpec:
     rcclEnv: Dict[str, str] = field(default_factory=dict)
     railTableBase: int = 0
     rcclSocketIfname: str = ""
+    lldpCache: bool = False
     extra: Dict[str, Any] = field(default_factory=dict)
 
     _FIELDS = ("disableNetworkManager", "layer", "image", "pullPolicy", "mtu", "xgmiCheck", "lldpAnnounce",
                "interfaces", "nicDrivers", "disableFirmwareLldp", "metricsPort", "gpuDirectRdma", "rcclEnv",
-               "railTableBase", "rcclSocketIfname")
+               "railTableBase", "rcclSocketIfname", "lldpCache")
 
     def to_dict(self) -> dict:
         d: dict = {}
@@ -99,6 +100,8 @@ class AmdScaleOutSpec:
             d["railTableBase"] = self.railTableBase
         if self.rcclSocketIfname:
             d["rcclSocketIfname"] = self.rcclSocketIfname
+        if self.lldpCache:
+            d["lldpCache"] = True
         d.update(copy.deepcopy(self.extra))
         return d
 
@@ -121,6 +124,7 @@ class AmdScaleOutSpec:
             rcclEnv=dict(d.pop("rcclEnv", {}) or {}),
             railTableBase=int(d.pop("railTableBase", 0) or 0),
             rcclSocketIfname=d.pop("rcclSocketIfname", "") or "",
+            lldpCache=bool(d.pop("lldpCache", False)),
         )
         s.extra = d
         return s

@@ -43,6 +43,7 @@ ARTIFACT_DIR_CONTAINER = "/host" + ARTIFACT_DIR_HOST
 RCCL_NET_FILE = "rccl-net.json"
 RCCL_ENV_FILE = "rccl.env"
 RCCL_TOPO_FILE = "rccl-topo.xml"
+LLDP_CACHE_FILE = "lldp-cache"  # --lldp-cache, beside the artifacts so it survives pod restarts
 L3_WAIT = "90s"
 
 STATE_NO_TARGETS = "No targets"
@@ -161,6 +162,8 @@ def agent_args(p: T.NetworkClusterPolicy) -> List[str]:
         args.append(f"--rail-table-base={so.railTableBase}")
     if so.rcclSocketIfname:
         args.append(f"--rccl-socket-ifname={so.rcclSocketIfname}")
+    if so.lldpCache and so.layer == "L3":
+        args.append(f"--lldp-cache={ARTIFACT_DIR_CONTAINER}/{LLDP_CACHE_FILE}")
     if so.rcclEnv:
         args.append("--rccl-env-extra=" + ",".join(f"{k}={v}" for k, v in sorted(so.rcclEnv.items())))
     if so.gpuDirectRdma:

@@ -168,12 +168,15 @@ def run_scenario(n_nics: int = 8, mode: str = "L3", seed: int | None = None, int
                  xgmi_expect: int = 0, keep_tmp: bool = False, sigterm: bool = True, verbose: int = 2,
                  drop_xgmi: list | None = None, extra_args: list | None = None, flap_port: int | None = None,
                  crash_restart: bool = False, crash_after_s: float = 0.0, gid_delay_s: float = 0.0,
-                 egress_probe: bool = False, nm_bus: bool = False) -> dict:
+                 egress_probe: bool = False, nm_bus: bool = False, lldp_cache: bool = False) -> dict:
     """Runs one node bring-up.  Must already be inside a private user+net namespace.
 
     nm_bus: run the agent with --disable-networkmanager against a real ``dbus-daemon`` on which a
     NetworkManager stand-in owns the name (testing/fakedbus.py), with an NM keyfile directory,
-    and record both before and after SIGTERM."""
+    and record both before and after SIGTERM.
+
+    lldp_cache: run the agent with --lldp-cache; with crash_restart, also record how long after
+    the restart the switch's frames confirmed every cached Port Description."""
     from . import fakesysfs
 
     nat = _native()
@@ -271,6 +274,8 @@ def run_scenario(n_nics: int = 8, mode: str = "L3", seed: int | None = None, int
                 f"--rccl-topo={tmp / 'rccl-topo.xml'}", f"--status-file={tmp / 'status.json'}", f"--nfd-features-dir={feat}", f"--xgmi-expect={xgmi_expect}",
                 f"--pipeline={'true' if pipeline else 'false'}", f"--lldp-announce={'true' if announce else 'false'}",
                 f"--systemd-networkd={tmp / 'networkd'}", f"-v={verbose}", *(extra_args or [])]
+        if lldp_cache:
+            args.append(f"--lldp-cache={tmp / 'lldp-cache'}")
         env = dict(os.environ, SYSFS_ROOT=str(tmp / "sys"), NODE_NAME="mi355x-node-0")
         bus = nm = None
         keyfile = tmp / "NetworkManager" / "conf.d" / "99-amd-network-operator.conf"
@@ -354,6 +359,24 @@ def run_scenario(n_nics: int = 8, mode: str = "L3", seed: int | None = None, int
                     pass
                 time.sleep(0.0005)
             res["restart_latency_s"] = (back - t_r) if back else None
+            if lldp_cache and back:
+                def sources():
+                    try:
+                        st = json.loads((tmp / "status.json").read_text())
+                    except (OSError, ValueError):
+                        return None
+                    return [i.get("lldp_source") for i in st["interfaces"]]
+
+                time.sleep(0.05)  # status.json follows the label
+                res["restart_lldp_sources"] = sources()
+                confirmed = None
+                while time.monotonic() < end and agent.poll() is None:
+                    if sources() == ["frame"] * len(nic_names):
+                        confirmed = time.monotonic()
+                        break
+                    time.sleep(0.01)
+                res["cache_confirmed_s"] = (confirmed - t_r) if confirmed else None
+                res["restart_rccl_net"] = json.loads((tmp / "rccl-net.json").read_text())
         if flap_port is not None and t_ready:
             # Carrier loss on one switch port: the agent must withdraw the label, then restore
             # it (and the NIC's routes) once the port is back.

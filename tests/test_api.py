@@ -246,3 +246,16 @@ def test_rccl_socket_ifname_field_validated_and_passed_to_the_agent():
             assert "--rccl-socket-ifname" not in " ".join(agent_args(T.new_policy("p")))
             continue
         assert pol(bad)[1], bad
+
+
+def test_lldp_cache_field_passed_to_the_agent_in_l3_only():
+    from network_operator_amd.api.v1alpha1 import crd as CRD2
+    from network_operator_amd.operator.reconciler import agent_args
+
+    p = T.new_policy("p", lldpCache=True).to_dict()
+    assert CRD2.validate(p) == [] and p["spec"]["amdScaleOut"]["lldpCache"] is True
+    assert "--lldp-cache=/host/etc/amd/scale-out/lldp-cache" in agent_args(T.NetworkClusterPolicy.from_dict(p))
+    assert "--lldp-cache" not in " ".join(agent_args(T.new_policy("p")))
+    l2 = T.new_policy("p", lldpCache=True, layer="L2")
+    assert "--lldp-cache" not in " ".join(agent_args(l2))
+    assert CRD2.validate(dict(p, spec=dict(p["spec"], amdScaleOut={"lldpCache": "yes"})))

@@ -177,6 +177,24 @@ def test_crash_restart_without_shutdown_first_is_not_fast_started():
     assert r["restart_latency_s"] is None
 
 
+def test_lldp_cache_restart_against_a_switch_without_fast_start():
+    """A switch that only sends periodic LLDP (no fast start, 10 s interval): a restarted agent
+    without the cache waits for the next periodic frame; with --lldp-cache it configures from the
+    last confirmed Port Descriptions at once, and the next periodic frame confirms them."""
+    kw = dict(n_nics=2, seed=22, interval="10s", phase="zero", fast_start=False, crash_restart=True,
+              crash_after_s=1.0)
+    cached = netns.run_isolated(lldp_cache=True, **kw)
+    _check_configured(cached)
+    assert cached["restart_latency_s"] is not None and cached["restart_latency_s"] < 1.0, cached["restart_latency_s"]
+    assert cached["restart_lldp_sources"] == ["cache", "cache"], cached["agent_log"]
+    assert cached["cache_confirmed_s"] is not None, cached["agent_log"]
+    ips = lambda j: [n["NIC_IP"] for n in j["NIC_NET_CONFIG"]]  # noqa: E731
+    assert ips(cached["restart_rccl_net"]) == ips(cached["rccl_net"])
+    assert cached["agent_rc"] == 0 and not cached["label_after_sigterm"]
+    control = netns.run_isolated(**kw)
+    assert control["restart_latency_s"] is not None and control["restart_latency_s"] > 5.0, control["restart_latency_s"]
+
+
 def test_two_nodes_l3_fabric_carries_a_collective():
     """BASELINE config "L3 mode, 2 nodes": two agents configure their nodes from one routing
     switch; a gloo all-reduce then runs node A <-> node B over the scale-out /30s and /16 routes."""
