@@ -631,6 +631,10 @@ void Agent::detect_lldp(int stop_fd) {
     int remaining = listening - apply_lldp_cache();
     if (remaining <= 0) {
         NLOG_I("Every listening interface was configured from the LLDP cache; the switch confirms it while monitoring");
+        // Still introduce ourselves as a new neighbour, so a fast-start switch confirms now rather
+        // than at its next periodic frame.
+        if (cfg_.announce_shutdown_first) announce_all(0);
+        announce_all(120);
         return;
     }
     auto cb = [&](const std::string& ifname, const lldp::Frame& f) -> bool {

@@ -193,6 +193,11 @@ def test_lldp_cache_restart_against_a_switch_without_fast_start():
     assert cached["agent_rc"] == 0 and not cached["label_after_sigterm"]
     control = netns.run_isolated(**kw)
     assert control["restart_latency_s"] is not None and control["restart_latency_s"] > 5.0, control["restart_latency_s"]
+    # A fast-start switch: the restarted agent still announces itself as a new neighbour, so the
+    # switch's answer confirms the cache within about a second, not at its next periodic frame.
+    fast = netns.run_isolated(lldp_cache=True, **dict(kw, fast_start=True, interval="30s"))
+    assert fast["restart_lldp_sources"] == ["cache", "cache"], fast["agent_log"]
+    assert fast["cache_confirmed_s"] is not None and fast["cache_confirmed_s"] < 2.0, fast["cache_confirmed_s"]
 
 
 def test_two_nodes_l3_fabric_carries_a_collective():
