@@ -17,8 +17,10 @@
 
 #include <cstdint>
 #include <functional>
+#include <future>
 #include <map>
 #include <memory>
+#include <optional>
 #include <string>
 #include <vector>
 
@@ -191,6 +193,12 @@ class Agent {
     void write_l2_artifacts();
     void write_rccl_env_file();
     std::string write_topo();  // returns the NCCL_TOPO_FILE value for rccl.env ("" = none)
+    // The topology XML depends only on sysfs and the NIC set, both fixed once discovery is done:
+    // it is generated on a worker thread from then on (overlapping link-up and the LLDP wait)
+    // and written at artifact time, so its sysfs walk is off the node-ready critical path.
+    void start_topo();
+    void write_host_config();  // systemd-networkd files and the LLDP cache
+    const std::string& topo_xml();  // joins the worker; "" when generation failed
     std::vector<std::string> socket_ifnames() const;
     void check_xgmi();
     void log_results();
@@ -229,6 +237,8 @@ class Agent {
     NmFactory nm_factory_;
     std::vector<NicState> nics_;
     topo::DiscoveryResult disc_;
+    std::future<std::string> topo_future_;
+    std::optional<std::string> topo_xml_;
     topo::XgmiReport xgmi_;
     topo::GdrReport gdr_;
     void check_gdr();

@@ -34,6 +34,7 @@ struct PciDev {
     // max_link_width of the device and of its parent directory); "" / 0 when unreadable.
     std::string max_link_speed, port_max_link_speed;  // e.g. "32.0 GT/s PCIe"
     int max_link_width = 0, port_max_link_width = 0;
+    bool topo_attrs = false;  // subsystem ids and link attributes were read (read_pci_dev(..., true))
     // The link as RCCL records it (NCCL xml.cc): the slower of device and port speed (the
     // device's string when neither parses), the narrower width.
     std::string rccl_link_speed() const;
@@ -78,7 +79,11 @@ struct DiscoveryOptions {
     PathType max_path = PathType::PXB;  // NICs farther than this from every GPU are not scale-out NICs
 };
 
-std::optional<PciDev> read_pci_dev(const std::string& root, const std::string& device_path);
+// `topo_attrs`: also read the subsystem ids and the link attributes, which only the topology
+// file needs (discovery skips them: six fewer sysfs reads per device on the critical path).
+std::optional<PciDev> read_pci_dev(const std::string& root, const std::string& device_path, bool topo_attrs = true);
+// The same for a path that is already canonical (no symlink to resolve), e.g. PciDev::path.
+std::optional<PciDev> read_pci_dir(const std::string& canonical_path, bool topo_attrs = true);
 // The PCI device behind a netdev (<root>/class/net/<ifname>/device); nullopt for virtual links.
 std::optional<PciDev> netdev_pci(const std::string& root, const std::string& ifname);
 // The ancestors RCCL puts above `d` in its topology tree, outermost first.  RCCL (NCCL's
@@ -86,7 +91,8 @@ std::optional<PciDev> netdev_pci(const std::string& root, const std::string& ifn
 // port and the switch above it count as one bridge — and stops at the root complex, whose
 // "pciDDDD:BB" component is not a BDF; the CPU node there is the outermost ancestor's NUMA node.
 // Mirroring that walk keeps a topology file the agent writes identical to RCCL's own view.
-std::vector<PciDev> rccl_pci_parents(const PciDev& d);
+// `cache` (optional) holds bridges already read, by sysfs path: GPUs and NICs share switches.
+std::vector<PciDev> rccl_pci_parents(const PciDev& d, std::map<std::string, PciDev>* cache = nullptr);
 
 // The CPU identity RCCL records on each <cpu> node of its topology (NCCL's ncclTopoGetXmlFromCpu):
 // uname machine, and on x86_64 the CPUID vendor string and family / model ids computed the way

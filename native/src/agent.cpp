@@ -773,16 +773,39 @@ void Agent::write_l2_artifacts() {
     write_rccl_env_file();
 }
 
-std::string Agent::write_topo() {
-    if (cfg_.rccl_topo.empty()) return "";
+void Agent::start_topo() {
+    if (cfg_.rccl_topo.empty() || topo_future_.valid() || topo_xml_) return;
     std::string root = cfg_.sysfs_root.empty() ? topo::sysfs_root() : cfg_.sysfs_root;
     std::vector<std::string> names;
     for (const auto& n : nics_) names.push_back(n.ifname);
+    // Inputs are copied: the worker shares nothing with the agent thread.
+    topo_future_ = std::async(std::launch::async, [disc = disc_, names = std::move(names), root = std::move(root)] {
+        return artifacts::generate_rccl_topo(disc.gpus, artifacts::topo_nics(disc, names, root), topo::cpu_identity(),
+                                             root);
+    });
+}
+
+const std::string& Agent::topo_xml() {
+    if (!topo_xml_) {
+        if (!topo_future_.valid()) start_topo();
+        try {
+            topo_xml_ = topo_future_.get();
+        } catch (const std::exception& e) {
+            NLOG_E("Error generating the RCCL topology file: %s", e.what());
+            topo_xml_ = std::string();
+        }
+    }
+    return *topo_xml_;
+}
+
+std::string Agent::write_topo() {
+    if (cfg_.rccl_topo.empty()) return "";
+    const std::string& xml = topo_xml();
+    if (xml.empty()) return "";  // rccl.env then names no topology
     try {
-        artifacts::write_rccl_topo(cfg_.rccl_topo, disc_.gpus, artifacts::topo_nics(disc_, names, root),
-                                   topo::cpu_identity(), root);
+        write_file_atomic(cfg_.rccl_topo, xml, 0644);
     } catch (const std::exception& e) {
-        NLOG_E("Error writing RCCL topology file: %s", e.what());  // rccl.env then names no topology
+        NLOG_E("Error writing RCCL topology file: %s", e.what());
         return "";
     }
     return cfg_.rccl_topo_env_path.empty() ? cfg_.rccl_topo : cfg_.rccl_topo_env_path;
@@ -847,6 +870,11 @@ void Agent::write_artifacts() {
         }
     }
     write_rccl_env_file();
+}
+
+void Agent::write_host_config() {
+    // What the node needs after a reboot or an agent restart, not what a job needs now: written
+    // after the readiness label, off the node-ready critical path.
     save_lldp_cache();
     if (!cfg_.networkd.empty()) {
         try {
@@ -1038,6 +1066,7 @@ void Agent::run(int stop_fd) {
         disable_fw_lldp();  // before link-up: some drivers reset the port when the flag flips
         mark("fw_lldp");
     }
+    start_topo();  // overlaps link-up and the LLDP wait, which mostly sleep in the kernel
     interfaces_up();
     mark("link_up");
     interfaces_set_mtu();
@@ -1083,11 +1112,13 @@ void Agent::run(int stop_fd) {
     log_results();
 
     if (!cfg_.configure) {
+        if (cfg_.mode == "L3") write_host_config();
         interfaces_restore_down();
         write_status();
         return;
     }
     if (!cfg_.keep_running) {
+        if (cfg_.mode == "L3") write_host_config();
         write_status();
         return;
     }
@@ -1105,6 +1136,7 @@ void Agent::run(int stop_fd) {
     }
     ready_ = true;
     phases_["total_ready"] = mono_ns() - t0_;
+    if (cfg_.mode == "L3") write_host_config();
     write_status();
     NLOG_I("Configurations done. %s...", cfg_.monitor ? "Monitoring" : "Idling");
 
@@ -1236,6 +1268,7 @@ void Agent::monitor(int stop_fd) {
                 if (cfg_.mode == "L3") write_artifacts();
                 labelled = publish_label();
                 if (labelled) NLOG_I("All scale-out interfaces healthy again: readiness label republished");
+                if (cfg_.mode == "L3") write_host_config();
                 announce_all(120);
             } else if (!healthy && labelled) {
                 artifacts::remove_labels(cfg_.labels);
@@ -1243,6 +1276,7 @@ void Agent::monitor(int stop_fd) {
                 NLOG_W("Scale-out degraded: readiness label withdrawn");
             } else if (healthy && labelled && cfg_.mode == "L3") {
                 write_artifacts();  // re-addressed NIC: refresh the RCCL artifacts
+                write_host_config();
             }
             ready_ = labelled;
             write_status();

@@ -277,8 +277,12 @@ void emit_pci(std::string& out, XmlPci& n, int depth) {
 std::string generate_rccl_topo(const std::vector<topo::Gpu>& gpus, const std::vector<TopoNic>& nics,
                                const topo::CpuIdentity& cpu, const std::string& sysfs_root, int version) {
     std::map<int, std::vector<std::unique_ptr<XmlPci>>> cpus;  // numaid -> top-level PCI nodes
-    auto place = [&](const topo::PciDev& leaf) -> XmlPci& {
-        auto parents = topo::rccl_pci_parents(leaf);
+    std::map<std::string, topo::PciDev> bridges;
+    auto place = [&](const topo::PciDev& found) -> XmlPci& {
+        std::optional<topo::PciDev> full;  // discovery reads devices without the topology attributes
+        if (!found.topo_attrs) full = topo::read_pci_dir(found.path);
+        const topo::PciDev& leaf = full ? *full : found;
+        auto parents = topo::rccl_pci_parents(leaf, &bridges);
         auto* level = &cpus[parents.empty() ? leaf.numa : parents.front().numa];
         for (const auto& p : parents) level = &child(*level, p).kids;
         return child(*level, leaf);

@@ -1,6 +1,10 @@
 #include "netop/topology.hpp"
 
+#include <fcntl.h>
 #include <sys/utsname.h>
+#include <unistd.h>
+#include <cerrno>
+#include <climits>
 #if defined(__x86_64__)
 #include <cpuid.h>
 #endif
@@ -56,48 +60,80 @@ static bool looks_like_bdf(std::string_view s) {
     return true;
 }
 
-static uint32_t read_hex(const std::string& path) {
-    auto s = read_file(path);
+// A sysfs attribute: at most a page, returned by a single read().  `dirfd` (optional) is an
+// open directory the name is relative to: a device's attributes are then looked up one
+// component deep instead of walking the whole sysfs path again for each of them.
+static std::optional<std::string> read_attr(const std::string& path, int dirfd = AT_FDCWD) {
+    int fd = ::openat(dirfd, path.c_str(), O_RDONLY | O_CLOEXEC);
+    if (fd < 0) return std::nullopt;
+    char buf[4096];
+    ssize_t n;
+    do {
+        n = ::read(fd, buf, sizeof buf);
+    } while (n < 0 && errno == EINTR);
+    ::close(fd);
+    if (n < 0) return std::nullopt;
+    return std::string(buf, size_t(n));
+}
+
+static uint32_t read_hex(const std::string& path, int dirfd = AT_FDCWD) {
+    auto s = read_attr(path, dirfd);
     if (!s) return 0;
     return uint32_t(std::strtoul(trim(*s).c_str(), nullptr, 16));
 }
 
-static int read_int(const std::string& path, int dflt) {
-    auto s = read_file(path);
+static int read_int(const std::string& path, int dflt, int dirfd = AT_FDCWD) {
+    auto s = read_attr(path, dirfd);
     if (!s) return dflt;
     auto t = trim(*s);
     if (t.empty()) return dflt;
     return int(std::strtol(t.c_str(), nullptr, 10));
 }
 
-std::optional<PciDev> read_pci_dev(const std::string& root, const std::string& device_path) {
+std::optional<PciDev> read_pci_dev(const std::string& root, const std::string& device_path, bool topo_attrs) {
+    (void)root;
     auto real = realpath_of(device_path);
     if (!real) return std::nullopt;
+    return read_pci_dir(*real, topo_attrs);
+}
+
+std::optional<PciDev> read_pci_dir(const std::string& real, bool topo_attrs) {
     PciDev d;
-    d.path = *real;
-    d.bdf = path_basename(*real);
+    d.path = real;
+    d.bdf = path_basename(real);
     if (!looks_like_bdf(d.bdf)) return std::nullopt;
-    auto pos = real->find("/devices/");
+    auto pos = real.find("/devices/");
     if (pos == std::string::npos) return std::nullopt;
-    for (auto& c : split(real->substr(pos + 9), '/'))
+    const int dir = ::open(real.c_str(), O_PATH | O_DIRECTORY | O_CLOEXEC);
+    if (dir < 0) return std::nullopt;
+    struct CloseDir {
+        int fd;
+        ~CloseDir() { ::close(fd); }
+    } guard{dir};
+    for (auto& c : split(real.substr(pos + 9), '/'))
         if (!c.empty()) d.chain.push_back(c);
-    if (auto drv = realpath_of(path_join(*real, "driver"))) d.driver = path_basename(*drv);
-    d.vendor = read_hex(path_join(*real, "vendor"));
-    d.device = read_hex(path_join(*real, "device"));
-    d.pci_class = read_hex(path_join(*real, "class"));
-    d.subsystem_vendor = read_hex(path_join(*real, "subsystem_vendor"));
-    d.subsystem_device = read_hex(path_join(*real, "subsystem_device"));
-    d.numa = read_int(path_join(*real, "numa_node"), -1);
-    auto str = [](const std::string& p) {
-        auto v = read_file(p);
+    {  // "driver" is a symlink to .../drivers/<name>: its last component is all we need
+        char buf[PATH_MAX];
+        ssize_t n = ::readlinkat(dir, "driver", buf, sizeof buf - 1);
+        if (n > 0) d.driver = path_basename(std::string(buf, size_t(n)));
+    }
+    d.vendor = read_hex("vendor", dir);
+    d.device = read_hex("device", dir);
+    d.pci_class = read_hex("class", dir);
+    d.numa = read_int("numa_node", -1, dir);
+    if (!topo_attrs) return d;
+    d.topo_attrs = true;
+    d.subsystem_vendor = read_hex("subsystem_vendor", dir);
+    d.subsystem_device = read_hex("subsystem_device", dir);
+    auto str = [dir](const char* name) {
+        auto v = read_attr(name, dir);
         return v ? trim(*v) : std::string();
     };
-    d.max_link_speed = str(path_join(*real, "max_link_speed"));
-    d.max_link_width = read_int(path_join(*real, "max_link_width"), 0);
-    const std::string port = path_dirname(*real);
-    d.port_max_link_speed = str(path_join(port, "max_link_speed"));
-    d.port_max_link_width = read_int(path_join(port, "max_link_width"), 0);
-    (void)root;
+    d.max_link_speed = str("max_link_speed");
+    d.max_link_width = read_int("max_link_width", 0, dir);
+    // The port above: the parent directory (the path is canonical, so ".." is its dirname).
+    d.port_max_link_speed = str("../max_link_speed");
+    d.port_max_link_width = read_int("../max_link_width", 0, dir);
     return d;
 }
 
@@ -143,7 +179,7 @@ std::optional<PciDev> netdev_pci(const std::string& root, const std::string& ifn
     return read_pci_dev(root, path_join(root, "class/net/" + ifname + "/device"));
 }
 
-std::vector<PciDev> rccl_pci_parents(const PciDev& d) {
+std::vector<PciDev> rccl_pci_parents(const PciDev& d, std::map<std::string, PciDev>* cache) {
     std::vector<PciDev> out;
     auto pos = d.path.find("/devices/");
     if (pos == std::string::npos || d.chain.empty()) return out;
@@ -156,8 +192,17 @@ std::vector<PciDev> rccl_pci_parents(const PciDev& d) {
     size_t i = d.chain.size() - 1;
     while (i >= 2 && looks_like_bdf(d.chain[i - 1]) && looks_like_bdf(d.chain[i - 2])) {
         i -= 2;
-        auto p = read_pci_dev("", dir_of(i));
+        const std::string dir = dir_of(i);
+        if (cache) {
+            auto it = cache->find(dir);
+            if (it != cache->end()) {
+                out.push_back(it->second);
+                continue;
+            }
+        }
+        auto p = read_pci_dir(dir);
         if (!p) break;  // unreadable bridge: RCCL would stop there too (no sysfs entry)
+        if (cache) cache->emplace(dir, *p);
         out.push_back(std::move(*p));
     }
     std::reverse(out.begin(), out.end());
@@ -169,7 +214,7 @@ std::vector<Gpu> discover_gpus(const std::string& root, const std::string& drive
     std::string dir = path_join(root, "bus/pci/drivers/" + driver);
     for (auto& name : list_dir(dir)) {
         if (!looks_like_bdf(name)) continue;
-        auto d = read_pci_dev(root, path_join(dir, name));
+        auto d = read_pci_dev(root, path_join(dir, name), false);
         if (!d) {
             NLOG_W("Expected '%s' to be a symlink to a PCI device", path_join(dir, name).c_str());
             continue;
@@ -195,7 +240,7 @@ std::vector<Nic> discover_pci_nics(const std::string& root, const std::vector<st
         if (path_basename(netdir) != "net") continue;
         std::string devdir = path_dirname(netdir);
         if (!looks_like_bdf(path_basename(devdir))) continue;  // virtual / non-PCI netdev
-        auto d = read_pci_dev(root, devdir);
+        auto d = read_pci_dev(root, devdir, false);
         if (!d) continue;
         if (!drivers.empty() && std::find(drivers.begin(), drivers.end(), d->driver) == drivers.end()) continue;
         Nic n;
@@ -319,11 +364,11 @@ std::optional<int> find_rocev2_linklocal_gid_index(const std::string& root, cons
     }
     std::sort(idx.begin(), idx.end());
     for (int i : idx) {
-        auto g = read_file(path_join(pdir, "gids/" + std::to_string(i)));
+        auto g = read_attr(path_join(pdir, "gids/" + std::to_string(i)));
         if (!g) continue;
         auto gid = parse_gid(*g);
         if (!gid || (*gid)[0] != 0xfe || ((*gid)[1] & 0xc0) != 0x80) continue;  // fe80::/10
-        auto type = read_file(path_join(pdir, "gid_attrs/types/" + std::to_string(i)));
+        auto type = read_attr(path_join(pdir, "gid_attrs/types/" + std::to_string(i)));
         if (type && trim(*type) == "RoCE v2") return i;
     }
     return std::nullopt;
@@ -343,11 +388,11 @@ std::optional<int> find_rocev2_gid_index(const std::string& root, const std::str
     want[10] = want[11] = 0xff;
     ip.to_net(&want[12]);
     for (int i : idx) {
-        auto g = read_file(path_join(pdir, "gids/" + std::to_string(i)));
+        auto g = read_attr(path_join(pdir, "gids/" + std::to_string(i)));
         if (!g) continue;
         auto gid = parse_gid(*g);
         if (!gid || *gid != want) continue;
-        auto type = read_file(path_join(pdir, "gid_attrs/types/" + std::to_string(i)));
+        auto type = read_attr(path_join(pdir, "gid_attrs/types/" + std::to_string(i)));
         if (type && trim(*type) == "RoCE v2") return i;
     }
     return std::nullopt;

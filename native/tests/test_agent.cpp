@@ -1041,3 +1041,18 @@ TEST(agent_lldp_cache_ignores_old_foreign_and_unmonitored_entries) {
         CHECK(!a.ready());
     }
 }
+
+TEST(agent_topology_file_generated_off_the_critical_path) {
+    Fixture f;
+    f.cfg.keep_running = false;
+    f.cfg.rccl_topo = f.tmp.path + "/rccl-topo.xml";
+    f.cfg.rccl_topo_env_path = "/etc/amd/scale-out/rccl-topo.xml";
+    f.cfg.rccl_env = f.tmp.path + "/rccl.env";
+    f.cfg.sysfs_root = f.tmp.path + "/sys/";  // no PCI devices: a tree with no GPUs
+    agent::Agent a(f.cfg, f.ops, f.all_valid(), f.nm());
+    a.run(-1);
+    auto xml = read_file(f.cfg.rccl_topo);
+    CHECK(xml && xml->rfind("<system version=\"2\">", 0) == 0);
+    auto env = read_file(f.cfg.rccl_env);
+    CHECK(env && env->find("NCCL_TOPO_FILE=/etc/amd/scale-out/rccl-topo.xml\n") != std::string::npos);
+}
