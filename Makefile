@@ -9,7 +9,7 @@ KUBECTL ?= kubectl
 VERSION ?= 0.1.0
 BUNDLE_IMG ?= amd/amd-network-operator-bundle:v$(VERSION)
 
-.PHONY: all help build native hip test test-native test-netns test-gpu manifests deployments bench bench-node-ready \
+.PHONY: all help build native hip test test-native test-netns test-gpu manifests deployments bench bench-node-ready bench-e2e \
         images sanitize tsan clean fmt vet lint fuzz run build-installer install uninstall deploy undeploy bundle \
         bundle-build helm-package-chart fuzz-native check-hardening catalog-build catalog-push bundle-push
 
@@ -70,6 +70,9 @@ bench:                      ## 1-GPU RCCL bench (driver contract); N GPUs: torch
 
 bench-node-ready:           ## node scale-out-ready latency in the netns harness
 	$(PYTHON) bench/node_ready.py --nics 8 --runs 5
+
+bench-e2e:                  ## policy created -> Node labelled / status All good (operator + simulated node + agent)
+	$(PYTHON) bench/node_ready.py --e2e --nics 8 --runs 20
 
 fmt:                        ## clang-format the native sources (if installed)
 	@command -v clang-format >/dev/null && clang-format -i native/src/*.cpp native/include/netop/*.hpp native/tests/*.cpp native/tools/*.cpp || echo "clang-format not installed"

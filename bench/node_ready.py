@@ -12,6 +12,10 @@ For every run the harness also reports ``reference_model_s``: when the switch's 
 *periodic* LLDPDU reached the last NIC — the earliest an agent that never transmits
 (the reference's pcap listener) could have configured the node, before adding libpcap's
 delivery delay.  Prints one JSON document.
+
+``--e2e`` measures the same from the control plane's side: the time from creating the
+NetworkClusterPolicy to the scale-out label on the Node object and to the policy's
+``All good`` (operator, DaemonSet, simulated kubelet + NFD, real agent; ``testing/e2e.py``).
 """
 import argparse
 import json
@@ -32,11 +36,31 @@ def main() -> int:
     ap.add_argument("--mode", choices=["L2", "L3"], default="L3")
     ap.add_argument("--matrix", action="store_true",
                     help="L2 and L3 x {1,2,4,8} NICs, fast-start switch only (BASELINE.md measurement plan)")
+    ap.add_argument("--e2e", action="store_true",
+                    help="whole chain from `kubectl apply` of the policy: operator, DaemonSet, simulated kubelet and "
+                         "NFD, real agent (testing/e2e.py); reports policy -> Node label and -> status 'All good'")
     a = ap.parse_args()
     ok, why = netns.available()
     if not ok:
         print(json.dumps({"error": f"netns harness unavailable: {why}"}))
         return 2
+    if a.e2e:
+        import statistics
+
+        from network_operator_amd.testing import e2e
+
+        keys = ("policy_to_daemonset_s", "policy_to_agent_start_s", "policy_to_node_label_s", "policy_to_all_good_s",
+                "delete_to_agent_stopped_s", "delete_to_label_removed_s")
+        runs = [e2e.run_isolated(n_nics=a.nics, mode=a.mode, seed=a.seed * 1000 + k, interval=a.interval)
+                for k in range(a.runs)]
+        out = {"mode": a.mode, "nics": a.nics, "runs": a.runs, "interval": a.interval}
+        for k in keys:
+            xs = [r[k] for r in runs]
+            ok_xs = sorted(x for x in xs if x is not None)
+            out[k] = {"p50": statistics.median(ok_xs) if ok_xs else None, "max": ok_xs[-1] if ok_xs else None,
+                      "failed": sum(1 for x in xs if x is None), "all": xs}
+        print(json.dumps(out))
+        return 0
     if a.matrix:
         rows = []
         for mode in ("L2", "L3"):

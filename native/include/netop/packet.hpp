@@ -39,6 +39,11 @@ class LldpSocket {
     LldpSocket& operator=(const LldpSocket&) = delete;
 
     int fd() const { return fd_; }
+    int release_fd() {  // the caller closes it
+        int f = fd_;
+        fd_ = -1;
+        return f;
+    }
     const std::string& ifname() const { return ifname_; }
     int ifindex() const { return ifindex_; }
     const MacAddr& own_mac() const { return own_; }

@@ -1,0 +1,193 @@
+"""Whole-system run: operator + fake API server + simulated node + real agent + synthetic switch.
+
+The chain a user starts with ``kubectl apply`` of a NetworkClusterPolicy, end to end, in one
+private user+network namespace:
+
+    policy created --(operator: watch, reconcile)--> DaemonSet --(fake API: DS controller)--> Pod
+    --(nodesim kubelet)--> discover (real binary, veth NICs, fake MI355X sysfs) --LLDP--> switch
+    --> NICs addressed, RCCL artifacts, features.d label --(nodesim NFD)--> Node label
+    --(readinessProbe: discover --ready-check)--> Pod Ready --> DaemonSet numberReady
+    --(operator)--> policy status "All good"
+
+and back on deletion: policy deleted --(garbage collector)--> DaemonSet, Pod --> agent SIGTERM
+--> addresses and label removed --> Node label gone.
+
+Measured from the moment the policy is created: the DaemonSet, the agent's start, the Node
+label (scale-out readiness as a job scheduler sees it), and the policy's ``All good``.  This
+is the control-plane-inclusive version of the node-ready metric; ``netns.py`` measures the agent
+alone.  BASELINE.json configs[0] ("L2 mode on kind/envtest with fake LLDP frames over veth
+pairs") and the L3 equivalent.
+"""
+
+from __future__ import annotations
+
+import argparse
+import asyncio
+import json
+import os
+import random
+import shutil
+import sys
+import tempfile
+import time
+from pathlib import Path
+from typing import Optional
+
+from . import fakesysfs, netns
+
+READY_LABEL = "amd.feature.node.kubernetes.io/gpu-scale-out"
+
+
+async def _until(fn, timeout: float, poll: float = 0.001) -> Optional[float]:
+    end = time.monotonic() + timeout
+    while time.monotonic() < end:
+        if fn():
+            return time.monotonic()
+        await asyncio.sleep(poll)
+    return None
+
+
+async def _scenario(tmp: Path, n_nics: int, mode: str, seed: int, interval: str, fast_start: bool,
+                    teardown: bool, node_name: str, policy_kw: dict, update_mtu: int) -> dict:
+    from ..api.v1alpha1 import types as T
+    from ..operator import kube, manager
+    from ..operator.kube import ApiClient, KubeConfig
+    from .fakeapi import FakeApiServer
+    from .nodesim import SimNode
+
+    rng = random.Random(seed)
+    rt = netns._native().Rtnl()
+    rt.link_set_up(rt.link_by_name("lo")["index"])
+    fakesysfs.build_mi355x_node(tmp / "sys", n_gpus=n_nics)
+    nat = netns._native()
+    nic_names = [p["nic"] for p in nat.discover(str(tmp / "sys"))["pairs"]][:n_nics]
+    plan = netns.random_plan(len(nic_names), rng)
+    for n in nat.discover(str(tmp / "sys"))["nics"]:  # RoCE v2 GIDs as the RDMA core adds them
+        if n["ifname"] in nic_names and n["rdma_dev"]:
+            fakesysfs.add_rocev2_gids(tmp / "sys", n["rdma_dev"], [plan[nic_names.index(n["ifname"])]["local"]])
+    sw = netns.SyntheticSwitch(nic_names, plan, rng, interval=interval, phase="random", fast_start=fast_start)
+    sw.start(rt)
+
+    res: dict = {"n_nics": len(nic_names), "mode": mode, "plan": plan, "nics": nic_names, "fast_start": fast_start}
+    fake = FakeApiServer(extra_groups=["nfd.k8s-sigs.io", "cert-manager.io"])
+    url = await fake.start()
+    os.environ["ENABLE_WEBHOOKS"] = "false"
+    os.environ["OPERATOR_NAMESPACE"] = "amd-network-operator"
+    stop = asyncio.Event()
+    started = asyncio.Event()
+    op = asyncio.ensure_future(manager.run(["--master", url, "--health-probe-bind-address=0",
+                                            "--metrics-bind-address=0", "--dependency-check-interval=0"],
+                                           stop=stop, started=started))
+    node = SimNode(fake, node_name, {"amd.feature.node.kubernetes.io/gpu-ready": "true"}, tmp / "host",
+                   sysfs_root=tmp / "sys")
+    P, DS = kube.NETWORKCLUSTERPOLICIES, kube.DAEMONSETS
+    ns = "amd-network-operator"
+    name = "scale-out"
+    try:
+        await asyncio.wait_for(started.wait(), 20)
+        await node.start()
+        async with ApiClient(KubeConfig(host=url)) as c:
+            pol = T.new_policy(name, layer=mode, mtu=9000, **policy_kw).to_dict()
+            t0 = time.monotonic()
+            await c.create(P, pol)
+            t_ds = await _until(lambda: fake.get_object(DS, name, ns) is not None, 10)
+            t_agent = await _until(lambda: any(x.proc is not None for x in node.containers.values()), 10)
+            t_label = await _until(lambda: node.node_labels().get(READY_LABEL) == "true", 30)
+
+            def all_good():
+                st = (fake.get_object(P, name) or {}).get("status") or {}
+                return st.get("state") == "All good" and st.get("ready") == 1
+
+            t_good = await _until(all_good, 30)
+            rel = lambda t: round(t - t0, 6) if t else None  # noqa: E731
+            res.update(policy_to_daemonset_s=rel(t_ds), policy_to_agent_start_s=rel(t_agent),
+                       policy_to_node_label_s=rel(t_label), policy_to_all_good_s=rel(t_good))
+            res["policy_status"] = (fake.get_object(P, name) or {}).get("status")
+            res["node_labels"] = node.node_labels()
+            res["agent_argv"] = next(iter(node.containers.values())).argv if node.containers else None
+            art = node.host_path("/etc/amd/scale-out")
+            res["artifacts"] = sorted(os.listdir(art)) if art.exists() else []
+            res["rccl_env"] = (art / "rccl.env").read_text() if (art / "rccl.env").exists() else None
+            state = {}
+            for nif in nic_names:
+                link = rt.link_by_name(nif)
+                state[nif] = {"up": link["up"], "mtu": link["mtu"], "addrs": rt.addr_list(link["index"])}
+            res["state"] = state
+            if update_mtu:
+                # `kubectl edit`: new MTU -> DaemonSet template changes -> the kubelet replaces the
+                # agent -> the new agent configures the NICs again and republishes the label.
+                t1 = time.monotonic()
+                cur = await c.get(P, name)
+                cur["spec"]["amdScaleOut"]["mtu"] = update_mtu
+                await c.replace(P, cur)
+
+                def mtu_applied():
+                    return all(rt.link_by_name(nif)["mtu"] == update_mtu for nif in nic_names)
+
+                t_mtu = await _until(mtu_applied, 30)
+                t_relabel = await _until(lambda: node.node_labels().get(READY_LABEL) == "true" and all_good(), 30)
+                res["update_to_mtu_applied_s"] = round(t_mtu - t1, 6) if t_mtu else None
+                res["update_to_ready_again_s"] = round(t_relabel - t1, 6) if t_relabel else None
+                res["agent_starts"] = sum(len(x.started_at) for x in node.containers.values()) + len(node.exited)
+            if teardown:
+                t1 = time.monotonic()
+                await c.delete(P, name)
+                t_gone = await _until(lambda: not node.containers and fake.get_object(DS, name, ns) is None, 30)
+                t_unlabel = await _until(lambda: READY_LABEL not in node.node_labels(), 10)
+                res["delete_to_agent_stopped_s"] = round(t_gone - t1, 6) if t_gone else None
+                res["delete_to_label_removed_s"] = round(t_unlabel - t1, 6) if t_unlabel else None
+                res["after_delete"] = {nif: rt.addr_list(rt.link_by_name(nif)["index"]) for nif in nic_names}
+                res["agent_exit_codes"] = [e["rc"] for e in node.exited]
+                res["agent_sigterm_to_exit_s"] = [e["sigterm_to_exit_s"] for e in node.exited]
+    finally:
+        res["agent_log"] = "".join(e["log"] for e in node.exited)[-6000:]
+        if not res["agent_log"]:
+            for f in sorted((tmp / "pod-logs").glob("*.log")) if (tmp / "pod-logs").exists() else []:
+                res["agent_log"] += f.read_text(errors="replace")[-6000:]
+        await node.stop()
+        stop.set()
+        try:
+            res["operator_rc"] = await asyncio.wait_for(op, 20)
+        except Exception as e:  # pragma: no cover
+            res["operator_rc"] = repr(e)
+        await fake.stop()
+        sw.stop()
+    return res
+
+
+def run_scenario(n_nics: int = 2, mode: str = "L3", seed: int = 1, interval: str = "30s", fast_start: bool = True,
+                 teardown: bool = True, node_name: str = "mi355x-0", policy_kw: Optional[dict] = None,
+                 update_mtu: int = 0, keep_tmp: bool = False) -> dict:
+    """Must already run inside a private user+net namespace (``run_isolated``)."""
+    tmp = Path(tempfile.mkdtemp(prefix="netop-e2e-"))
+    try:
+        return asyncio.run(_scenario(tmp, n_nics, mode, seed, interval, fast_start, teardown, node_name,
+                                     dict(policy_kw or {}), update_mtu))
+    finally:
+        if not keep_tmp:
+            shutil.rmtree(tmp, ignore_errors=True)
+
+
+def run_isolated(timeout: float = 300, **kw) -> dict:
+    """``run_scenario(**kw)`` in a fresh user+net namespace."""
+    import subprocess
+
+    cmd = [*netns.unshare_cmd(), sys.executable, "-m", "network_operator_amd.testing.e2e", "--json", json.dumps(kw)]
+    root = Path(__file__).resolve().parents[2]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, cwd=root,
+                       env=dict(os.environ, PYTHONPATH=str(root)))
+    if r.returncode != 0:
+        raise RuntimeError(f"e2e scenario failed rc={r.returncode}: {r.stderr[-3000:]}")
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+def _main(argv=None) -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--json", default="{}", help="run_scenario kwargs")
+    a = ap.parse_args(argv)
+    print(json.dumps(run_scenario(**json.loads(a.json))))
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(_main())

@@ -162,6 +162,83 @@ def egress_matrix(nic_names: list, plan: list, packets: int = 20) -> list:
     return rows
 
 
+class SyntheticSwitch:
+    """The switch namespace: a forked child unshares its network namespace, receives one veth peer
+    (``swp<i>``) per node NIC, and runs ``netop-lldp-tx`` with each port's Port Description from
+    `plan`.  The last `silent_nics` ports send no LLDP."""
+
+    def __init__(self, nic_names: list, plan: list, rng: random.Random, interval: str = "30s", phase: str = "random",
+                 fast_start: bool = True, silent_nics: int = 0):
+        from ..utils.paths import native_bin
+
+        self.nic_names, self.plan = list(nic_names), plan
+        self.ports = [f"swp{i}" for i in range(len(self.nic_names))]
+        self.args = [str(native_bin("netop-lldp-tx")), f"--interval={interval}", f"--phase={phase}", "--assign-ip",
+                     f"--seed={rng.randrange(1, 1 << 30)}"]
+        if fast_start:
+            self.args.append("--fast-start")
+        for i, (sp, p) in enumerate(zip(self.ports, plan)):
+            if i >= len(plan) - silent_nics:
+                continue  # switch port that never sends LLDP
+            self.args.append(f"--port={sp}={p['desc']}")
+        self.pid = 0
+        self.first_periodic: dict = {}  # port -> seconds (switch clock) of its first periodic frame
+        self._out = None
+
+    def start(self, rt) -> float:
+        """Creates the veth pairs (node ends keep the NIC names) and starts the switch; returns the
+        monotonic time at which the switch got its ports."""
+        has_ports = any(a.startswith("--port=") for a in self.args)
+        libc = ctypes.CDLL(ctypes.util.find_library("c"), use_errno=True)
+        r1, w1 = os.pipe()
+        r2, w2 = os.pipe()
+        out_r, out_w = os.pipe()
+        pid = os.fork()
+        if pid == 0:  # switch: own netns, wait for the ports, exec lldp-tx
+            try:
+                os.close(r1)
+                os.close(w2)
+                os.close(out_r)
+                if libc.unshare(CLONE_NEWNET) != 0:
+                    os._exit(3)
+                os.write(w1, b"1")
+                os.read(r2, 1)
+                os.dup2(out_w, 1)
+                if not has_ports:  # no port sends anything
+                    signal.pause()
+                os.execv(self.args[0], self.args)
+            finally:
+                os._exit(4)
+        self.pid = pid
+        os.close(w1)
+        os.close(r2)
+        os.close(out_w)
+        os.read(r1, 1)
+        for node_if, sp in zip(self.nic_names, self.ports):
+            rt.veth_add(node_if, sp)
+            rt.link_set_netns_pid(rt.link_by_name(sp)["index"], pid)
+        t_switch = time.monotonic()
+        os.write(w2, b"1")
+        self._out = os.fdopen(out_r)
+        if has_ports:
+            for line in self._out:
+                if line.startswith("first "):
+                    _, ifn, ns = line.split()
+                    self.first_periodic[ifn] = int(ns) / 1e9
+                if line.strip() == "ready":
+                    break
+        return t_switch
+
+    def stop(self) -> None:
+        if self.pid:
+            os.kill(self.pid, signal.SIGTERM)
+            os.waitpid(self.pid, 0)
+            self.pid = 0
+        if self._out is not None:
+            self._out.close()
+            self._out = None
+
+
 def run_scenario(n_nics: int = 8, mode: str = "L3", seed: int | None = None, interval: str = "30s",
                  fast_start: bool = True, announce: bool = True, phase: str = "random", wait: str = "90s",
                  mtu: int = 9000, pipeline: bool = True, bad_nics: int = 0, silent_nics: int = 0,
@@ -216,55 +293,10 @@ def run_scenario(n_nics: int = 8, mode: str = "L3", seed: int | None = None, int
         else:
             add_gids()
 
-        # Switch namespace: forked child unshares its netns, waits for its ports, execs lldp-tx.
-        sw_ports = [f"swp{i}" for i in range(len(nic_names))]
-        tx_args = [str(native_bin("netop-lldp-tx")), f"--interval={interval}", f"--phase={phase}", "--assign-ip",
-                   f"--seed={rng.randrange(1, 1 << 30)}"]
-        if fast_start:
-            tx_args.append("--fast-start")
-        for i, (sp, p) in enumerate(zip(sw_ports, plan)):
-            if i >= len(plan) - silent_nics:
-                continue  # switch port that never sends LLDP
-            tx_args.append(f"--port={sp}={p['desc']}")
-        has_ports = any(a.startswith("--port=") for a in tx_args)
-        libc = ctypes.CDLL(ctypes.util.find_library("c"), use_errno=True)
-        r1, w1 = os.pipe()
-        r2, w2 = os.pipe()
-        out_r, out_w = os.pipe()
-        pid = os.fork()
-        if pid == 0:  # switch
-            try:
-                os.close(r1)
-                os.close(w2)
-                os.close(out_r)
-                if libc.unshare(CLONE_NEWNET) != 0:
-                    os._exit(3)
-                os.write(w1, b"1")
-                os.read(r2, 1)
-                os.dup2(out_w, 1)
-                if not has_ports:  # no port sends anything
-                    signal.pause()
-                os.execv(tx_args[0], tx_args)
-            finally:
-                os._exit(4)
-        os.close(w1)
-        os.close(r2)
-        os.close(out_w)
-        os.read(r1, 1)
-        for node_if, sp in zip(nic_names, sw_ports):
-            rt.veth_add(node_if, sp)
-            rt.link_set_netns_pid(rt.link_by_name(sp)["index"], pid)
-        t_switch = time.monotonic()
-        os.write(w2, b"1")
-        sw_out = os.fdopen(out_r)
-        first_periodic = {}
-        if has_ports:
-            for line in sw_out:
-                if line.startswith("first "):
-                    _, ifn, ns = line.split()
-                    first_periodic[ifn] = int(ns) / 1e9
-                if line.strip() == "ready":
-                    break
+        sw = SyntheticSwitch(nic_names, plan, rng, interval=interval, phase=phase, fast_start=fast_start,
+                             silent_nics=silent_nics)
+        t_switch = sw.start(rt)
+        pid, sw_ports, first_periodic = sw.pid, sw.ports, sw.first_periodic
 
         feat = tmp / "features.d"
         feat.mkdir()
@@ -397,13 +429,16 @@ def run_scenario(n_nics: int = 8, mode: str = "L3", seed: int | None = None, int
             res["flap_restore_s"] = (back - t_up) if back else None
             link = rt.link_by_name(nic_names[flap_port])
             res["flap_routes_after"] = [r for r in rt.route_list() if r["ifindex"] == link["index"]]
+        t_term = None
         if sigterm and agent.poll() is None:
+            t_term = time.monotonic()
             agent.send_signal(signal.SIGTERM)
         try:
             out, _ = agent.communicate(timeout=20)
         except subprocess.TimeoutExpired:
             agent.kill()
             out, _ = agent.communicate()
+        res["sigterm_to_exit_s"] = (time.monotonic() - t_term) if t_term else None
         res["agent_rc"] = agent.returncode
         res["agent_log"] = out[-6000:]
         after = {}
@@ -418,8 +453,7 @@ def run_scenario(n_nics: int = 8, mode: str = "L3", seed: int | None = None, int
             res["nm_managed_after_sigterm"] = dict(nm.devices)
             nm.stop()
             bus.stop()
-        os.kill(pid, signal.SIGTERM)
-        os.waitpid(pid, 0)
+        sw.stop()
         res["switch_start_offset_s"] = t0 - t_switch
         return res
     finally:

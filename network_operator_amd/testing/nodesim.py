@@ -1,0 +1,278 @@
+"""A simulated Kubernetes node for the fake API server: kubelet + NFD worker, real agent.
+
+``FakeApiServer`` already plays the DaemonSet controller (one Pod per matching node, Ready
+condition from ``set_agent_ready``).  ``SimNode`` plays what runs *on* the node:
+
+* **kubelet** -- for every Pod bound to this node it starts the DaemonSet's container as a local
+  process: the real ``discover`` binary with the container's ``args`` and ``NODE_NAME`` from the
+  downward API.  hostPath volumes are mapped under ``host_root`` and every argument that names a
+  path under a mountPath is rewritten to the mapped directory.  The container's exec
+  ``readinessProbe`` runs every ``probe_period`` seconds and drives the Pod's Ready condition.
+  A process that exits is restarted with backoff (``restartPolicy: Always``).  A changed pod
+  template restarts the agent (rolling update, one node).  When the Pod goes away the agent gets
+  SIGTERM and ``terminationGracePeriodSeconds`` before SIGKILL.
+* **NFD worker** -- the mapped ``features.d`` directory is scanned every ``nfd_period`` seconds
+  and its ``name=value`` lines become Node labels, added and removed as the files change (NFD's
+  local feature source).
+
+Not simulated: init containers (the host-nic driver container), image pulls, and the probes'
+``initialDelaySeconds`` / ``periodSeconds`` (``probe_period`` replaces both, so the control plane
+is measured rather than probe timers).  The node's NICs are whatever the calling network
+namespace holds (``testing/e2e.py`` builds veths to a synthetic switch).
+
+The reference's only end-to-end test deploys the operator into kind and checks that the
+controller pod runs (reference test/e2e/e2e_test.go:51-120); it never runs an agent.
+"""
+
+from __future__ import annotations
+
+import asyncio
+import copy
+import json
+import logging
+import os
+import signal
+import subprocess
+import time
+from dataclasses import dataclass, field
+from pathlib import Path
+from typing import Dict, List, Optional, Tuple
+
+from .. import discovery
+from ..operator import kube
+from ..utils.paths import native_bin
+
+log = logging.getLogger("nodesim")
+
+
+@dataclass
+class _Container:
+    pod: Tuple[str, str]            # (namespace, pod name)
+    daemonset: str                  # "<ns>/<name>"
+    template: str                   # JSON of the pod template spec it was started from
+    argv: List[str]
+    probe: Optional[List[str]]
+    env: Dict[str, str]
+    grace_s: float
+    log_path: Path
+    proc: Optional[subprocess.Popen] = None
+    restarts: int = 0
+    next_start: float = 0.0
+    backoff: float = 0.1
+    ready: bool = False
+    started_at: List[float] = field(default_factory=list)
+
+
+class SimNode:
+    def __init__(self, fake, name: str, labels: Dict[str, str], host_root: Path, sysfs_root: Optional[Path] = None,
+                 probe_period: float = 0.02, nfd_period: float = 0.01, env: Optional[Dict[str, str]] = None):
+        self.fake, self.name = fake, name
+        self.base_labels = dict(labels)
+        self.host_root = Path(host_root)
+        self.sysfs_root = sysfs_root
+        self.probe_period, self.nfd_period = probe_period, nfd_period
+        self.extra_env = dict(env or {})
+        self.containers: Dict[Tuple[str, str], _Container] = {}
+        self.features: Dict[str, str] = {}
+        self.exited: List[dict] = []      # {"pod", "rc", "log"} of every agent process that ended
+        self._tasks: List[asyncio.Task] = []
+        self._stop = asyncio.Event()
+
+    # -- paths ---------------------------------------------------------------------------------
+    def host_path(self, path: str) -> Path:
+        """Where a host path of the simulated node lives in this process's filesystem."""
+        return self.host_root / path.lstrip("/")
+
+    @staticmethod
+    def _mounts(pod_spec: dict, container: dict) -> List[Tuple[str, str]]:
+        """(mountPath, hostPath) of the container's hostPath mounts, longest mountPath first."""
+        vols = {v["name"]: v["hostPath"]["path"] for v in pod_spec.get("volumes") or [] if "hostPath" in v}
+        out = [(m["mountPath"].rstrip("/") or "/", vols[m["name"]]) for m in container.get("volumeMounts") or []
+               if m.get("name") in vols]
+        return sorted(out, key=lambda x: -len(x[0]))
+
+    def _rewrite(self, value: str, mounts: List[Tuple[str, str]]) -> str:
+        for mp, hp in mounts:
+            if value == mp or value.startswith(mp + "/"):
+                return str(self.host_path(hp)) + value[len(mp):]
+        return value
+
+    def _rewrite_arg(self, arg: str, mounts) -> str:
+        if arg.startswith("--") and "=" in arg:
+            k, v = arg.split("=", 1)
+            return f"{k}={self._rewrite(v, mounts)}"
+        return self._rewrite(arg, mounts)
+
+    def _agent_argv(self, cmd: List[str], mounts) -> List[str]:
+        # The image's entrypoint (and the probe's absolute binary path) is the agent binary.
+        argv = [str(native_bin("discover"))] + [self._rewrite_arg(a, mounts) for a in cmd]
+        # The agent's built-in default label directory is a container path: name it explicitly.
+        if not any(a.startswith("--nfd-features-dir") for a in argv):
+            feat = self._rewrite(discovery.LABEL_FEATURES_DIR.rstrip("/"), mounts)
+            argv.append(f"--nfd-features-dir={feat}/")
+        return argv
+
+    # -- kubelet ---------------------------------------------------------------------------------
+    def _spec_for(self, pod: dict) -> Optional[_Container]:
+        ns, pname = pod["metadata"].get("namespace", ""), pod["metadata"]["name"]
+        ref = next((r for r in pod["metadata"].get("ownerReferences") or [] if r.get("kind") == "DaemonSet"), None)
+        if ref is None:
+            return None
+        ds = self.fake.get_object(kube.DAEMONSETS, ref["name"], ns)
+        if ds is None:
+            return None
+        spec = ds["spec"]["template"]["spec"]
+        c = spec["containers"][0]
+        mounts = self._mounts(spec, c)
+        for _, hp in mounts:  # hostPath type DirectoryOrCreate
+            self.host_path(hp).mkdir(parents=True, exist_ok=True)
+        env = {}
+        for e in c.get("env") or []:
+            if "value" in e:
+                env[e["name"]] = e["value"]
+            elif (e.get("valueFrom") or {}).get("fieldRef", {}).get("fieldPath") == "spec.nodeName":
+                env[e["name"]] = self.name
+        probe = (c.get("readinessProbe") or {}).get("exec", {}).get("command")
+        logs = self.host_root.parent / "pod-logs"
+        logs.mkdir(parents=True, exist_ok=True)
+        return _Container(pod=(ns, pname), daemonset=f"{ns}/{ref['name']}",
+                          template=json.dumps(spec, sort_keys=True),
+                          argv=self._agent_argv(list(c.get("command") or [])[1:] + list(c.get("args") or []), mounts),
+                          probe=self._agent_argv(probe[1:], mounts) if probe else None, env=env,
+                          grace_s=float(spec.get("terminationGracePeriodSeconds", 30)),
+                          log_path=logs / f"{pname}.log")
+
+    def _start(self, c: _Container) -> None:
+        env = dict(os.environ, **self.extra_env, **c.env)
+        if self.sysfs_root is not None:
+            env["SYSFS_ROOT"] = str(self.sysfs_root)
+        with open(c.log_path, "ab") as f:
+            c.proc = subprocess.Popen(c.argv, env=env, stdout=f, stderr=subprocess.STDOUT)
+        c.started_at.append(time.monotonic())
+        log.info("node %s: started %s (pid %d)", self.name, c.pod[1], c.proc.pid)
+
+    async def _terminate(self, c: _Container) -> None:
+        p = c.proc
+        if p is None or p.poll() is not None:
+            return
+        t = time.monotonic()
+        p.send_signal(signal.SIGTERM)
+        end = t + c.grace_s
+        while p.poll() is None and time.monotonic() < end:
+            await asyncio.sleep(0.001)
+        if p.poll() is None:
+            p.kill()
+            p.wait()
+        self._record_exit(c, time.monotonic() - t)
+
+    def _record_exit(self, c: _Container, sigterm_to_exit_s: Optional[float] = None) -> None:
+        try:
+            text = c.log_path.read_text(errors="replace")[-4000:]
+        except OSError:
+            text = ""
+        self.exited.append({"pod": c.pod[1], "rc": c.proc.returncode if c.proc else None, "log": text,
+                            "sigterm_to_exit_s": sigterm_to_exit_s})
+
+    def _set_ready(self, c: _Container, ready: bool) -> None:
+        if c.ready != ready:
+            c.ready = ready
+            self.fake.set_agent_ready(self.name, ready, daemonset=c.daemonset)
+
+    async def _kubelet(self) -> None:
+        while not self._stop.is_set():
+            pods = {(p["metadata"].get("namespace", ""), p["metadata"]["name"]): p
+                    for p in self.fake.list_objects(kube.PODS) if (p.get("spec") or {}).get("nodeName") == self.name}
+            for key in list(self.containers):
+                if key not in pods:  # Pod deleted (DaemonSet gone or node deselected)
+                    await self._terminate(self.containers[key])
+                    del self.containers[key]
+            for key, pod in pods.items():
+                want = self._spec_for(pod)
+                if want is None:
+                    continue
+                c = self.containers.get(key)
+                if c is not None and c.template != want.template:  # rolling update of this node
+                    self._set_ready(c, False)
+                    await self._terminate(c)
+                    c = None
+                if c is None:
+                    self.containers[key] = c = want
+                    self._start(c)
+                elif c.proc is not None and c.proc.poll() is not None:  # crashed: restartPolicy Always
+                    if c.next_start == 0.0:
+                        self._record_exit(c)
+                        self._set_ready(c, False)
+                        c.next_start = time.monotonic() + c.backoff
+                        c.backoff = min(c.backoff * 2, 5.0)
+                    elif time.monotonic() >= c.next_start:
+                        c.next_start = 0.0
+                        c.restarts += 1
+                        self._start(c)
+            await asyncio.sleep(0.005)
+
+    async def _prober(self) -> None:
+        while not self._stop.is_set():
+            for c in list(self.containers.values()):
+                if c.probe is None or c.proc is None or c.proc.poll() is not None:
+                    continue
+                env = dict(os.environ, **self.extra_env, **c.env)
+                p = await asyncio.create_subprocess_exec(*c.probe, env=env, stdout=asyncio.subprocess.DEVNULL,
+                                                         stderr=asyncio.subprocess.DEVNULL)
+                rc = await p.wait()
+                if c is self.containers.get(c.pod):
+                    self._set_ready(c, rc == 0)
+            await asyncio.sleep(self.probe_period)
+
+    # -- NFD worker --------------------------------------------------------------------------------
+    def _read_features(self) -> Dict[str, str]:
+        feats: Dict[str, str] = {}
+        d = self.host_path(discovery.LABEL_FEATURES_DIR)
+        try:
+            names = sorted(os.listdir(d))
+        except OSError:
+            return feats
+        for n in names:
+            if n.startswith(".") or ".tmp" in n:
+                continue
+            try:
+                text = (d / n).read_text()
+            except OSError:
+                continue
+            for line in text.splitlines():
+                line = line.strip()
+                if not line or line.startswith("#"):
+                    continue
+                k, _, v = line.partition("=")
+                feats[k.strip()] = v.strip() if _ else "true"
+        return feats
+
+    async def _nfd(self) -> None:
+        while not self._stop.is_set():
+            feats = self._read_features()
+            if feats != self.features:
+                self.features = feats
+                self.fake.set_node_labels(self.name, dict(self.base_labels, **feats))
+            await asyncio.sleep(self.nfd_period)
+
+    # -- lifecycle ---------------------------------------------------------------------------------
+    def node_labels(self) -> Dict[str, str]:
+        n = self.fake.get_object(kube.NODES, self.name)
+        return dict((n or {}).get("metadata", {}).get("labels") or {})
+
+    async def start(self) -> None:
+        if self.fake.get_object(kube.NODES, self.name) is None:
+            self.fake.add_node(self.name, copy.deepcopy(self.base_labels))
+        self._tasks = [asyncio.ensure_future(t()) for t in (self._kubelet, self._prober, self._nfd)]
+
+    async def stop(self) -> None:
+        """Node shutdown: every agent gets SIGTERM (and its grace period)."""
+        self._stop.set()
+        for t in self._tasks:
+            t.cancel()
+        for t in self._tasks:
+            try:
+                await t
+            except asyncio.CancelledError:
+                pass
+        for key in list(self.containers):
+            await self._terminate(self.containers.pop(key))

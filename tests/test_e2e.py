@@ -1,0 +1,60 @@
+"""The whole chain in one namespace: NetworkClusterPolicy -> operator -> DaemonSet -> Pod -> real
+agent on veth NICs -> synthetic switch LLDP -> NFD label on the Node -> policy "All good", and back
+on deletion (``testing/e2e.py``, ``testing/nodesim.py``).
+
+The reference's e2e suite deploys the operator into kind and checks that its pod runs
+(reference test/e2e/e2e_test.go:51-120); no agent, NIC or label is involved.
+"""
+
+import pytest
+
+from network_operator_amd.testing import e2e
+
+pytestmark = pytest.mark.netns
+
+
+def _check_nics(r, layer):
+    for nic, p in zip(r["nics"], r["plan"]):
+        st = r["state"][nic]
+        assert st["up"] and st["mtu"] == 9000
+        assert st["addrs"] == ([p["local"] + "/30"] if layer == "L3" else [])
+
+
+def test_l3_policy_labels_the_node_and_deletion_undoes_it():
+    r = e2e.run_isolated(n_nics=4, mode="L3", seed=3)
+    assert r["policy_to_node_label_s"] is not None, r["agent_log"]
+    assert r["policy_to_all_good_s"] is not None, (r["policy_status"], r["agent_log"])
+    assert r["policy_to_daemonset_s"] <= r["policy_to_agent_start_s"] <= r["policy_to_node_label_s"]
+    assert r["policy_to_node_label_s"] < 2.0, r["policy_to_node_label_s"]  # fast-start switch
+    st = r["policy_status"]
+    assert (st["targets"], st["ready"], st["state"], st["errors"]) == (1, 1, "All good", [])
+    labels = r["node_labels"]
+    assert labels["amd.feature.node.kubernetes.io/gpu-scale-out"] == "true"
+    assert labels["amd.feature.node.kubernetes.io/gpu-scale-out.mode"] == "L3"
+    assert labels["amd.feature.node.kubernetes.io/gpu-scale-out.nics"] == "4"
+    _check_nics(r, "L3")
+    assert r["artifacts"] == ["rccl-net.json", "rccl-topo.xml", "rccl.env"]
+    assert "NCCL_TOPO_FILE=/etc/amd/scale-out/rccl-topo.xml" in r["rccl_env"]
+    # The agent ran with the DaemonSet's own args, host paths mapped.
+    assert "--mode=L3" in r["agent_argv"] and "--rccl-topo-env-path=/etc/amd/scale-out/rccl-topo.xml" in r["agent_argv"]
+    # Deletion: garbage collection -> SIGTERM -> addresses and the Node label gone.
+    assert r["delete_to_agent_stopped_s"] is not None and r["delete_to_label_removed_s"] is not None
+    assert all(a == [] for a in r["after_delete"].values())
+    assert r["agent_exit_codes"] == [0] and r["operator_rc"] == 0
+
+
+def test_l2_policy_labels_the_node():
+    r = e2e.run_isolated(n_nics=2, mode="L2", seed=4)
+    assert r["policy_to_all_good_s"] is not None, (r["policy_status"], r["agent_log"])
+    assert r["node_labels"]["amd.feature.node.kubernetes.io/gpu-scale-out.mode"] == "L2"
+    _check_nics(r, "L2")
+    assert r["artifacts"] == ["rccl-topo.xml", "rccl.env"]
+    assert all(a == [] for a in r["after_delete"].values())
+
+
+def test_policy_edit_rolls_the_agent_and_the_node_is_ready_again():
+    r = e2e.run_isolated(n_nics=2, mode="L3", seed=5, update_mtu=4200)
+    assert r["update_to_mtu_applied_s"] is not None, r["agent_log"]
+    assert r["update_to_ready_again_s"] is not None, (r["policy_status"], r["agent_log"])
+    assert r["agent_starts"] == 2  # the first agent was replaced, not restarted on a crash
+    assert r["agent_exit_codes"] == [0, 0]
