@@ -12,6 +12,11 @@ private user+network namespace:
 and back on deletion: policy deleted --(garbage collector)--> DaemonSet, Pod --> agent SIGTERM
 --> addresses and label removed --> Node label gone.
 
+``config_type="host-nic"`` runs BASELINE.json configs[4]: the node's two host NICs have no
+driver bound until the policy's driver container (KMD install, an init container mapped to a
+command that binds them in the fake sysfs) has run; the agent then discovers them as RDMA NICs
+of the ``ionic`` driver and publishes the host-nic label.
+
 Measured from the moment the policy is created: the DaemonSet, the agent's start, the Node
 label (scale-out readiness as a job scheduler sees it), and the policy's ``All good``.  This
 is the control-plane-inclusive version of the node-ready metric; ``netns.py`` measures the agent
@@ -36,6 +41,12 @@ from typing import Optional
 from . import fakesysfs, netns
 
 READY_LABEL = "amd.feature.node.kubernetes.io/gpu-scale-out"
+HOST_NIC_READY_LABEL = "amd.feature.node.kubernetes.io/host-nic-ready"
+# host-nic scenario: the two management-side NICs of the fixture node, driverless until the
+# driver container (the KMD install of BASELINE.json configs[4]) binds them.
+HOST_NICS = ("ens9np0", "ens49np1")
+KMD_IMAGE = "example.com/amd/ionic-kmd:1.0"
+KMD_DRIVER = "ionic"
 
 
 async def _until(fn, timeout: float, poll: float = 0.001) -> Optional[float]:
@@ -48,7 +59,7 @@ async def _until(fn, timeout: float, poll: float = 0.001) -> Optional[float]:
 
 
 async def _scenario(tmp: Path, n_nics: int, mode: str, seed: int, interval: str, fast_start: bool,
-                    teardown: bool, node_name: str, policy_kw: dict, update_mtu: int) -> dict:
+                    teardown: bool, node_name: str, policy_kw: dict, update_mtu: int, config_type: str) -> dict:
     from ..api.v1alpha1 import types as T
     from ..operator import kube, manager
     from ..operator.kube import ApiClient, KubeConfig
@@ -60,7 +71,14 @@ async def _scenario(tmp: Path, n_nics: int, mode: str, seed: int, interval: str,
     rt.link_set_up(rt.link_by_name("lo")["index"])
     fakesysfs.build_mi355x_node(tmp / "sys", n_gpus=n_nics)
     nat = netns._native()
-    nic_names = [p["nic"] for p in nat.discover(str(tmp / "sys"))["pairs"]][:n_nics]
+    host_nic = config_type == "host-nic"
+    label_key = HOST_NIC_READY_LABEL if host_nic else READY_LABEL
+    if host_nic:
+        nic_names = list(HOST_NICS)
+        for nif in nic_names:
+            fakesysfs.unbind_driver(tmp / "sys", nif)
+    else:
+        nic_names = [p["nic"] for p in nat.discover(str(tmp / "sys"))["pairs"]][:n_nics]
     plan = netns.random_plan(len(nic_names), rng)
     for n in nat.discover(str(tmp / "sys"))["nics"]:  # RoCE v2 GIDs as the RDMA core adds them
         if n["ifname"] in nic_names and n["rdma_dev"]:
@@ -78,8 +96,10 @@ async def _scenario(tmp: Path, n_nics: int, mode: str, seed: int, interval: str,
     op = asyncio.ensure_future(manager.run(["--master", url, "--health-probe-bind-address=0",
                                             "--metrics-bind-address=0", "--dependency-check-interval=0"],
                                            stop=stop, started=started))
+    kmd = [sys.executable, "-m", "network_operator_amd.testing.fakesysfs", "bind", KMD_DRIVER, *nic_names]
     node = SimNode(fake, node_name, {"amd.feature.node.kubernetes.io/gpu-ready": "true"}, tmp / "host",
-                   sysfs_root=tmp / "sys")
+                   sysfs_root=tmp / "sys", init_images={KMD_IMAGE: kmd},
+                   env={"PYTHONPATH": str(Path(__file__).resolve().parents[2])})
     P, DS = kube.NETWORKCLUSTERPOLICIES, kube.DAEMONSETS
     ns = "amd-network-operator"
     name = "scale-out"
@@ -87,12 +107,16 @@ async def _scenario(tmp: Path, n_nics: int, mode: str, seed: int, interval: str,
         await asyncio.wait_for(started.wait(), 20)
         await node.start()
         async with ApiClient(KubeConfig(host=url)) as c:
-            pol = T.new_policy(name, layer=mode, mtu=9000, **policy_kw).to_dict()
+            if host_nic:
+                pol = T.new_host_nic_policy(name, layer=mode, mtu=9000, nicDrivers=[KMD_DRIVER],
+                                            driverImage=KMD_IMAGE, **policy_kw).to_dict()
+            else:
+                pol = T.new_policy(name, layer=mode, mtu=9000, **policy_kw).to_dict()
             t0 = time.monotonic()
             await c.create(P, pol)
             t_ds = await _until(lambda: fake.get_object(DS, name, ns) is not None, 10)
             t_agent = await _until(lambda: any(x.proc is not None for x in node.containers.values()), 10)
-            t_label = await _until(lambda: node.node_labels().get(READY_LABEL) == "true", 30)
+            t_label = await _until(lambda: node.node_labels().get(label_key) == "true", 30)
 
             def all_good():
                 st = (fake.get_object(P, name) or {}).get("status") or {}
@@ -103,6 +127,8 @@ async def _scenario(tmp: Path, n_nics: int, mode: str, seed: int, interval: str,
             res.update(policy_to_daemonset_s=rel(t_ds), policy_to_agent_start_s=rel(t_agent),
                        policy_to_node_label_s=rel(t_label), policy_to_all_good_s=rel(t_good))
             res["policy_status"] = (fake.get_object(P, name) or {}).get("status")
+            res["init_runs"] = [dict(r, t_start=rel(r["t_start"]), t_end=rel(r["t_end"])) for r in node.init_runs]
+            res["agent_started_s"] = [rel(t) for x in node.containers.values() for t in x.started_at]
             res["node_labels"] = node.node_labels()
             res["agent_argv"] = next(iter(node.containers.values())).argv if node.containers else None
             art = node.host_path("/etc/amd/scale-out")
@@ -125,7 +151,7 @@ async def _scenario(tmp: Path, n_nics: int, mode: str, seed: int, interval: str,
                     return all(rt.link_by_name(nif)["mtu"] == update_mtu for nif in nic_names)
 
                 t_mtu = await _until(mtu_applied, 30)
-                t_relabel = await _until(lambda: node.node_labels().get(READY_LABEL) == "true" and all_good(), 30)
+                t_relabel = await _until(lambda: node.node_labels().get(label_key) == "true" and all_good(), 30)
                 res["update_to_mtu_applied_s"] = round(t_mtu - t1, 6) if t_mtu else None
                 res["update_to_ready_again_s"] = round(t_relabel - t1, 6) if t_relabel else None
                 res["agent_starts"] = sum(len(x.started_at) for x in node.containers.values()) + len(node.exited)
@@ -133,7 +159,7 @@ async def _scenario(tmp: Path, n_nics: int, mode: str, seed: int, interval: str,
                 t1 = time.monotonic()
                 await c.delete(P, name)
                 t_gone = await _until(lambda: not node.containers and fake.get_object(DS, name, ns) is None, 30)
-                t_unlabel = await _until(lambda: READY_LABEL not in node.node_labels(), 10)
+                t_unlabel = await _until(lambda: label_key not in node.node_labels(), 10)
                 res["delete_to_agent_stopped_s"] = round(t_gone - t1, 6) if t_gone else None
                 res["delete_to_label_removed_s"] = round(t_unlabel - t1, 6) if t_unlabel else None
                 res["after_delete"] = {nif: rt.addr_list(rt.link_by_name(nif)["index"]) for nif in nic_names}
@@ -157,12 +183,12 @@ async def _scenario(tmp: Path, n_nics: int, mode: str, seed: int, interval: str,
 
 def run_scenario(n_nics: int = 2, mode: str = "L3", seed: int = 1, interval: str = "30s", fast_start: bool = True,
                  teardown: bool = True, node_name: str = "mi355x-0", policy_kw: Optional[dict] = None,
-                 update_mtu: int = 0, keep_tmp: bool = False) -> dict:
+                 update_mtu: int = 0, config_type: str = "amd-so", keep_tmp: bool = False) -> dict:
     """Must already run inside a private user+net namespace (``run_isolated``)."""
     tmp = Path(tempfile.mkdtemp(prefix="netop-e2e-"))
     try:
         return asyncio.run(_scenario(tmp, n_nics, mode, seed, interval, fast_start, teardown, node_name,
-                                     dict(policy_kw or {}), update_mtu))
+                                     dict(policy_kw or {}), update_mtu, config_type))
     finally:
         if not keep_tmp:
             shutil.rmtree(tmp, ignore_errors=True)

@@ -149,7 +149,49 @@ def add_rocev2_gids(root: Path, rdma_dev: str, ips, port: int = 1) -> None:
 MI355X_HOST_CPU = {"arch": "x86_64", "vendor": "AuthenticAMD", "family": 191, "model": 2}
 
 
+def nic_pci_dir(root: Path, ifname: str) -> Path:
+    """The PCI function directory behind a netdev of the tree."""
+    return (Path(root) / "class" / "net" / ifname).resolve().parent.parent
+
+
+def unbind_driver(root: Path, ifname: str) -> None:
+    """The NIC's kernel driver is not loaded: the function has no ``driver`` link."""
+    (nic_pci_dir(root, ifname) / "driver").unlink(missing_ok=True)
+
+
+def bind_driver(root: Path, ifname: str, driver: str) -> None:
+    """What loading a NIC driver (the host-nic KMD container) does to sysfs: the function binds."""
+    drv = Path(root) / "bus" / "pci" / "drivers" / driver
+    drv.mkdir(parents=True, exist_ok=True)
+    link = nic_pci_dir(root, ifname) / "driver"
+    link.unlink(missing_ok=True)
+    os.symlink(os.path.relpath(drv, link.parent), link)
+
+
+def _main(argv=None) -> int:
+    """``python -m network_operator_amd.testing.fakesysfs bind <driver> <ifname>...`` against
+    $SYSFS_ROOT: the simulated driver container of the end-to-end harness (testing/e2e.py)."""
+    import argparse
+
+    ap = argparse.ArgumentParser()
+    ap.add_argument("op", choices=["bind"])
+    ap.add_argument("driver")
+    ap.add_argument("ifnames", nargs="+")
+    a = ap.parse_args(argv)
+    root = Path(os.environ["SYSFS_ROOT"])
+    for i in a.ifnames:
+        bind_driver(root, i, a.driver)
+    print(f"bound {', '.join(a.ifnames)} to {a.driver}")
+    return 0
+
+
 def real_nic_order() -> list:
     """Fixture's scale-out NIC names in GPU (BDF) order — what affine discovery returns."""
     fx = json.loads(FIXTURE.read_text())
     return [n["ifname"] for n in fx["nics"] if n["ifname"].startswith("enp")]
+
+
+if __name__ == "__main__":
+    import sys
+
+    sys.exit(_main())

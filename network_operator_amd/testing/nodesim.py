@@ -15,7 +15,9 @@ condition from ``set_agent_ready``).  ``SimNode`` plays what runs *on* the node:
   and its ``name=value`` lines become Node labels, added and removed as the files change (NFD's
   local feature source).
 
-Not simulated: init containers (the host-nic driver container), image pulls, and the probes'
+Init containers (the host-nic driver container) run to completion, in order, before the agent
+starts; their images are mapped to local commands by ``init_images`` (an unmapped image fails
+like an image that cannot be pulled).  Not simulated: image pulls, and the probes'
 ``initialDelaySeconds`` / ``periodSeconds`` (``probe_period`` replaces both, so the control plane
 is measured rather than probe timers).  The node's NICs are whatever the calling network
 namespace holds (``testing/e2e.py`` builds veths to a synthetic switch).
@@ -61,17 +63,22 @@ class _Container:
     backoff: float = 0.1
     ready: bool = False
     started_at: List[float] = field(default_factory=list)
+    inits: List[dict] = field(default_factory=list)  # {"name", "image", "argv"} in order
+    inits_done: bool = False
 
 
 class SimNode:
     def __init__(self, fake, name: str, labels: Dict[str, str], host_root: Path, sysfs_root: Optional[Path] = None,
-                 probe_period: float = 0.02, nfd_period: float = 0.01, env: Optional[Dict[str, str]] = None):
+                 probe_period: float = 0.02, nfd_period: float = 0.01, env: Optional[Dict[str, str]] = None,
+                 init_images: Optional[Dict[str, List[str]]] = None):
         self.fake, self.name = fake, name
         self.base_labels = dict(labels)
         self.host_root = Path(host_root)
         self.sysfs_root = sysfs_root
         self.probe_period, self.nfd_period = probe_period, nfd_period
         self.extra_env = dict(env or {})
+        self.init_images = dict(init_images or {})
+        self.init_runs: List[dict] = []   # {"pod", "name", "rc", "t_start", "t_end"}
         self.containers: Dict[Tuple[str, str], _Container] = {}
         self.features: Dict[str, str] = {}
         self.exited: List[dict] = []      # {"pod", "rc", "log"} of every agent process that ended
@@ -135,17 +142,42 @@ class SimNode:
         probe = (c.get("readinessProbe") or {}).get("exec", {}).get("command")
         logs = self.host_root.parent / "pod-logs"
         logs.mkdir(parents=True, exist_ok=True)
+        inits = []
+        for ic in spec.get("initContainers") or []:
+            cmd = self.init_images.get(ic.get("image", ""))
+            inits.append({"name": ic["name"], "image": ic.get("image", ""),
+                          "argv": list(cmd) + list(ic.get("args") or []) if cmd is not None else None})
         return _Container(pod=(ns, pname), daemonset=f"{ns}/{ref['name']}",
                           template=json.dumps(spec, sort_keys=True),
                           argv=self._agent_argv(list(c.get("command") or [])[1:] + list(c.get("args") or []), mounts),
                           probe=self._agent_argv(probe[1:], mounts) if probe else None, env=env,
                           grace_s=float(spec.get("terminationGracePeriodSeconds", 30)),
-                          log_path=logs / f"{pname}.log")
+                          log_path=logs / f"{pname}.log", inits=inits, inits_done=not inits)
 
-    def _start(self, c: _Container) -> None:
+    def _env(self, c: _Container) -> Dict[str, str]:
         env = dict(os.environ, **self.extra_env, **c.env)
         if self.sysfs_root is not None:
             env["SYSFS_ROOT"] = str(self.sysfs_root)
+        return env
+
+    async def _run_inits(self, c: _Container) -> bool:
+        """Init containers in order, each to completion; False when one fails (retried later)."""
+        for ic in c.inits:
+            t = time.monotonic()
+            if ic["argv"] is None:
+                rc = -1  # ErrImagePull: no command for this image
+            else:
+                with open(c.log_path, "ab") as f:
+                    p = await asyncio.create_subprocess_exec(*ic["argv"], env=self._env(c), stdout=f, stderr=f)
+                    rc = await p.wait()
+            self.init_runs.append({"pod": c.pod[1], "name": ic["name"], "image": ic["image"], "rc": rc,
+                                   "t_start": t, "t_end": time.monotonic()})
+            if rc != 0:
+                return False
+        return True
+
+    def _start(self, c: _Container) -> None:
+        env = self._env(c)
         with open(c.log_path, "ab") as f:
             c.proc = subprocess.Popen(c.argv, env=env, stdout=f, stderr=subprocess.STDOUT)
         c.started_at.append(time.monotonic())
@@ -197,8 +229,18 @@ class SimNode:
                     c = None
                 if c is None:
                     self.containers[key] = c = want
+                if not c.inits_done:  # Init: the driver container before the agent
+                    if time.monotonic() < c.next_start:
+                        continue
+                    if await self._run_inits(c):
+                        c.inits_done, c.next_start = True, 0.0
+                    else:  # Init:CrashLoopBackOff
+                        c.next_start = time.monotonic() + c.backoff
+                        c.backoff = min(c.backoff * 2, 5.0)
+                        continue
+                if c.proc is None:
                     self._start(c)
-                elif c.proc is not None and c.proc.poll() is not None:  # crashed: restartPolicy Always
+                elif c.proc.poll() is not None:  # crashed: restartPolicy Always
                     if c.next_start == 0.0:
                         self._record_exit(c)
                         self._set_ready(c, False)
@@ -215,8 +257,7 @@ class SimNode:
             for c in list(self.containers.values()):
                 if c.probe is None or c.proc is None or c.proc.poll() is not None:
                     continue
-                env = dict(os.environ, **self.extra_env, **c.env)
-                p = await asyncio.create_subprocess_exec(*c.probe, env=env, stdout=asyncio.subprocess.DEVNULL,
+                p = await asyncio.create_subprocess_exec(*c.probe, env=self._env(c), stdout=asyncio.subprocess.DEVNULL,
                                                          stderr=asyncio.subprocess.DEVNULL)
                 rc = await p.wait()
                 if c is self.containers.get(c.pod):

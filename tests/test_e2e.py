@@ -58,3 +58,18 @@ def test_policy_edit_rolls_the_agent_and_the_node_is_ready_again():
     assert r["update_to_ready_again_s"] is not None, (r["policy_status"], r["agent_log"])
     assert r["agent_starts"] == 2  # the first agent was replaced, not restarted on a crash
     assert r["agent_exit_codes"] == [0, 0]
+
+
+def test_host_nic_policy_runs_the_driver_container_before_the_agent():
+    """BASELINE configs[4]: host-nic with a KMD driver container.  The host NICs are driverless
+    until the init container binds them; the agent starts after it and finds them."""
+    r = e2e.run_isolated(mode="L3", seed=6, config_type="host-nic")
+    assert r["policy_to_all_good_s"] is not None, (r["policy_status"], r["agent_log"])
+    assert [(x["name"], x["rc"]) for x in r["init_runs"]] == [("nic-driver", 0)]
+    assert r["agent_started_s"] and r["agent_started_s"][0] >= r["init_runs"][0]["t_end"]
+    assert r["node_labels"]["amd.feature.node.kubernetes.io/host-nic-ready"] == "true"
+    assert "amd.feature.node.kubernetes.io/gpu-scale-out" not in r["node_labels"]
+    assert r["nics"] == list(e2e.HOST_NICS)
+    _check_nics(r, "L3")
+    assert all(a == [] for a in r["after_delete"].values())
+    assert r["agent_exit_codes"] == [0]
