@@ -21,6 +21,7 @@
 #include <map>
 #include <memory>
 #include <optional>
+#include <set>
 #include <string>
 #include <vector>
 
@@ -218,7 +219,7 @@ class Agent {
     std::vector<std::pair<std::string, std::string>> rccl_env_extra_;
     void disable_fw_lldp();
     void restore_network_manager();
-    int apply_lldp_cache();  // NICs addressed from the cache
+    int apply_lldp_cache(const std::set<int>& listening);  // NICs addressed from the cache (by ifindex)
     // A frame for a NIC that already has an address: confirms a cached Port Description or moves
     // the NIC to the new one.  True when the NIC's status changed.
     bool refresh_from_frame(NicState& n, const lldp::Frame& f);

@@ -558,13 +558,14 @@ bool Agent::refresh_from_frame(NicState& n, const lldp::Frame& f) {
     return true;
 }
 
-int Agent::apply_lldp_cache() {
+int Agent::apply_lldp_cache(const std::set<int>& listening) {
     if (cfg_.lldp_cache.empty() || !cfg_.keep_running || !cfg_.monitor) return 0;
     const auto entries = artifacts::read_lldp_cache(cfg_.lldp_cache);
     const int64_t now = int64_t(::time(nullptr));
     int applied = 0;
     for (auto& n : nics_) {
-        if (!n.link.up() || n.lldp_seen) continue;
+        // Only NICs with an LLDP socket: nothing else could ever confirm the entry.
+        if (!listening.count(n.link.index) || n.lldp_seen) continue;
         for (const auto& e : entries) {
             if (e.ifname != n.ifname || e.nic_mac != n.link.mac.str()) continue;  // another NIC now
             if (now - e.unix_s > cfg_.lldp_cache_max_age_ns / 1000000000 || e.unix_s > now + 60) break;
@@ -614,6 +615,7 @@ void Agent::save_lldp_cache() {
 
 void Agent::detect_lldp(int stop_fd) {
     int listening = 0;
+    std::set<int> listened;
     for (auto& n : nics_) {
         if (!n.link.up()) {
             NLOG_I("Link '%s' %s, cannot start LLDP", n.ifname.c_str(), n.link.operstate_str().c_str());
@@ -622,13 +624,14 @@ void Agent::detect_lldp(int stop_fd) {
         try {
             lldp_->add(n.ifname, n.link.index, n.link.mac);
             ++listening;
+            listened.insert(n.link.index);
             NLOG_I("Started LLDP discovery for '%s'...", n.ifname.c_str());
         } catch (const std::exception& e) {
             NLOG_I("Cannot start LLDP client: %s", e.what());
         }
     }
     if (!listening) return;
-    int remaining = listening - apply_lldp_cache();
+    int remaining = listening - apply_lldp_cache(listened);
     if (remaining <= 0) {
         NLOG_I("Every listening interface was configured from the LLDP cache; the switch confirms it while monitoring");
         // Still introduce ourselves as a new neighbour, so a fast-start switch confirms now rather
