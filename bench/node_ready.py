@@ -39,6 +39,8 @@ def main() -> int:
     ap.add_argument("--e2e", action="store_true",
                     help="whole chain from `kubectl apply` of the policy: operator, DaemonSet, simulated kubelet and "
                          "NFD, real agent (testing/e2e.py); reports policy -> Node label and -> status 'All good'")
+    ap.add_argument("--fabric-nodes", type=int, default=0,
+                    help="with --e2e: N simulated nodes on one routing leaf, one policy (testing/e2e.py run_fabric)")
     a = ap.parse_args()
     ok, why = netns.available()
     if not ok:
@@ -49,6 +51,17 @@ def main() -> int:
 
         from network_operator_amd.testing import e2e
 
+        if a.fabric_nodes:
+            runs = [e2e.run_isolated(fabric=True, n_nodes=a.fabric_nodes, n_nics=a.nics, seed=a.seed * 1000 + k,
+                                     collective=False) for k in range(a.runs)]
+            out = {"nodes": a.fabric_nodes, "nics_per_node": a.nics, "runs": a.runs}
+            for k in ("policy_to_all_nodes_labelled_s", "policy_to_all_good_s", "delete_to_all_nodes_clean_s"):
+                xs = [r[k] for r in runs]
+                ok_xs = sorted(x for x in xs if x is not None)
+                out[k] = {"p50": statistics.median(ok_xs) if ok_xs else None, "max": ok_xs[-1] if ok_xs else None,
+                          "failed": sum(1 for x in xs if x is None), "all": xs}
+            print(json.dumps(out))
+            return 0
         keys = ("policy_to_daemonset_s", "policy_to_agent_start_s", "policy_to_node_label_s", "policy_to_all_good_s",
                 "delete_to_agent_stopped_s", "delete_to_label_removed_s")
         runs = [e2e.run_isolated(n_nics=a.nics, mode=a.mode, seed=a.seed * 1000 + k, interval=a.interval)

@@ -181,6 +181,143 @@ async def _scenario(tmp: Path, n_nics: int, mode: str, seed: int, interval: str,
     return res
 
 
+async def _fabric_scenario(tmp: Path, n_nodes: int, n_nics: int, seed: int, collective: bool) -> dict:
+    """`n_nodes` nodes on one routing leaf switch, one policy: the operator's DaemonSet lands on
+    every node, each node's agent addresses its NICs, the policy reports n/n, and (2 nodes) a
+    gloo all-reduce runs between the nodes over the configured /16 routes."""
+    from ..api.v1alpha1 import types as T
+    from ..operator import kube, manager
+    from ..operator.kube import ApiClient, KubeConfig
+    from . import twonode
+    from .fakeapi import FakeApiServer
+    from .nodesim import SimNode
+
+    rng = random.Random(seed)
+    nat = netns._native()
+    rt = nat.Rtnl()
+    rt.link_set_up(rt.link_by_name("lo")["index"])
+    holders = [None] + [netns.NetnsHolder() for _ in range(n_nodes - 1)]
+    res: dict = {"n_nodes": n_nodes, "n_nics": n_nics}
+    sw = None
+    fake = nodes = op = None
+    stop = asyncio.Event()
+    try:
+        for j, h in enumerate(holders):
+            fakesysfs.build_mi355x_node(tmp / f"sys{j}", n_gpus=n_nics)
+            if h is not None:
+                h.run(lambda: nat.Rtnl().link_set_up(nat.Rtnl().link_by_name("lo")["index"]))
+        nic_names = [p["nic"] for p in nat.discover(str(tmp / "sys0"))["pairs"]][:n_nics]
+        plan = netns.random_plan(n_nodes * n_nics, rng)  # node j owns plan[j*n : (j+1)*n]
+        for j in range(n_nodes):
+            for n in nat.discover(str(tmp / f"sys{j}"))["nics"]:
+                if n["ifname"] in nic_names and n["rdma_dev"]:
+                    ip = plan[j * n_nics + nic_names.index(n["ifname"])]["local"]
+                    fakesysfs.add_rocev2_gids(tmp / f"sys{j}", n["rdma_dev"], [ip])
+        remote = [(h.pid, nif) for h in holders[1:] for nif in nic_names]
+        sw = netns.SyntheticSwitch(nic_names, plan, rng, interval="30s", phase="random", fast_start=True,
+                                   remote=remote, forward=True)
+        sw.start(rt)
+        res["plan"], res["nics"] = plan, nic_names
+
+        fake = FakeApiServer(extra_groups=["nfd.k8s-sigs.io", "cert-manager.io"])
+        url = await fake.start()
+        os.environ["ENABLE_WEBHOOKS"] = "false"
+        os.environ["OPERATOR_NAMESPACE"] = "amd-network-operator"
+        started = asyncio.Event()
+        op = asyncio.ensure_future(manager.run(["--master", url, "--health-probe-bind-address=0",
+                                                "--metrics-bind-address=0", "--dependency-check-interval=0"],
+                                               stop=stop, started=started))
+        await asyncio.wait_for(started.wait(), 20)
+        nodes = [SimNode(fake, f"mi355x-{j}", {"amd.feature.node.kubernetes.io/gpu-ready": "true"}, tmp / f"host{j}",
+                         sysfs_root=tmp / f"sys{j}", netns=h) for j, h in enumerate(holders)]
+        for nd in nodes:
+            await nd.start()
+        P = kube.NETWORKCLUSTERPOLICIES
+        async with ApiClient(KubeConfig(host=url)) as c:
+            t0 = time.monotonic()
+            await c.create(P, T.new_policy("fabric", layer="L3", mtu=9000).to_dict())
+
+            def all_labelled():
+                return all(nd.node_labels().get(READY_LABEL) == "true" for nd in nodes)
+
+            def all_good():
+                st = (fake.get_object(P, "fabric") or {}).get("status") or {}
+                return st.get("state") == "All good" and st.get("ready") == n_nodes
+
+            t_lab = await _until(all_labelled, 30)
+            t_good = await _until(all_good, 30)
+            res["policy_to_all_nodes_labelled_s"] = round(t_lab - t0, 6) if t_lab else None
+            res["policy_to_all_good_s"] = round(t_good - t0, 6) if t_good else None
+            res["policy_status"] = (fake.get_object(P, "fabric") or {}).get("status")
+            res["node_labels"] = {nd.name: nd.node_labels() for nd in nodes}
+            addrs = []
+            for j, h in enumerate(holders):
+                out = tmp / f"addrs{j}.json"
+
+                def dump(path=out):
+                    r = nat.Rtnl()
+                    path.write_text(json.dumps({nif: r.addr_list(r.link_by_name(nif)["index"]) for nif in nic_names}))
+                if h is None:
+                    dump()
+                else:
+                    h.run(dump)
+                addrs.append(json.loads(out.read_text()))
+            res["addrs"] = addrs
+            if collective and t_good and n_nodes == 2:
+                # One rank per node, bound to its first scale-out NIC, rendezvous on node 0's
+                # first rail address: the bytes cross NIC, /16 route, the leaf's forwarding, NIC.
+                port = 29500 + rng.randrange(0, 400)
+                master = plan[0]["local"]
+                procs = []
+                for j, h in enumerate(holders):
+                    procs.append(await asyncio.create_subprocess_exec(
+                        sys.executable, "-c", twonode._WORKER, env=twonode._worker_env(j, nic_names[0], master, port),
+                        stdout=asyncio.subprocess.PIPE, stderr=asyncio.subprocess.PIPE,
+                        preexec_fn=h.enter if h else None))
+                outs = [await asyncio.wait_for(p.communicate(), 180) for p in procs]
+                res["collective"] = []
+                for p, (o, e) in zip(procs, outs):
+                    text = o.decode().strip().splitlines()
+                    res["collective"].append(json.loads(text[-1]) if p.returncode == 0 and text else
+                                             {"rc": p.returncode, "stderr": e.decode()[-2000:]})
+            t1 = time.monotonic()
+            await c.delete(P, "fabric")
+            t_gone = await _until(lambda: all(not nd.containers for nd in nodes)
+                                  and not any(READY_LABEL in nd.node_labels() for nd in nodes), 30)
+            res["delete_to_all_nodes_clean_s"] = round(t_gone - t1, 6) if t_gone else None
+            res["agent_exit_codes"] = [[e["rc"] for e in nd.exited] for nd in nodes]
+    finally:
+        if nodes:
+            res["agent_logs"] = ["".join(e["log"] for e in nd.exited)[-3000:] for nd in nodes]
+            for nd in nodes:
+                await nd.stop()
+        stop.set()
+        if op is not None:
+            try:
+                res["operator_rc"] = await asyncio.wait_for(op, 20)
+            except Exception as e:  # pragma: no cover
+                res["operator_rc"] = repr(e)
+        if fake is not None:
+            await fake.stop()
+        if sw is not None:
+            sw.stop()
+        for h in holders:
+            if h is not None:
+                h.stop()
+    return res
+
+
+def run_fabric(n_nodes: int = 2, n_nics: int = 2, seed: int = 1, collective: bool = True,
+               keep_tmp: bool = False) -> dict:
+    """Must already run inside a private user+net namespace (``run_isolated(fabric=True, ...)``)."""
+    tmp = Path(tempfile.mkdtemp(prefix="netop-fabric-"))
+    try:
+        return asyncio.run(_fabric_scenario(tmp, n_nodes, n_nics, seed, collective))
+    finally:
+        if not keep_tmp:
+            shutil.rmtree(tmp, ignore_errors=True)
+
+
 def run_scenario(n_nics: int = 2, mode: str = "L3", seed: int = 1, interval: str = "30s", fast_start: bool = True,
                  teardown: bool = True, node_name: str = "mi355x-0", policy_kw: Optional[dict] = None,
                  update_mtu: int = 0, config_type: str = "amd-so", keep_tmp: bool = False) -> dict:
@@ -211,7 +348,8 @@ def _main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--json", default="{}", help="run_scenario kwargs")
     a = ap.parse_args(argv)
-    print(json.dumps(run_scenario(**json.loads(a.json))))
+    kw = json.loads(a.json)
+    print(json.dumps(run_fabric(**kw) if kw.pop("fabric", False) else run_scenario(**kw)))
     return 0
 
 

@@ -36,6 +36,7 @@ import sys
 import tempfile
 import time
 from pathlib import Path
+from typing import Optional
 
 CLONE_NEWNET = 0x40000000
 
@@ -162,17 +163,62 @@ def egress_matrix(nic_names: list, plan: list, packets: int = 20) -> list:
     return rows
 
 
+class NetnsHolder:
+    """An empty network namespace kept alive by a sleeping child (another node of the fabric).
+    ``enter()`` is a ``preexec_fn`` that moves a new child process into it."""
+
+    def __init__(self):
+        libc = ctypes.CDLL(ctypes.util.find_library("c"), use_errno=True)
+        r, w = os.pipe()
+        pid = os.fork()
+        if pid == 0:
+            try:
+                os.close(r)
+                if libc.unshare(CLONE_NEWNET) != 0:
+                    os._exit(3)
+                os.write(w, b"1")
+                signal.pause()
+            finally:
+                os._exit(0)
+        os.close(w)
+        os.read(r, 1)
+        os.close(r)
+        self.pid = pid
+
+    def enter(self) -> None:
+        libc = ctypes.CDLL(ctypes.util.find_library("c"), use_errno=True)
+        fd = os.open(f"/proc/{self.pid}/ns/net", os.O_RDONLY)
+        if libc.setns(fd, CLONE_NEWNET) != 0:
+            raise OSError(ctypes.get_errno(), "setns")
+        os.close(fd)
+
+    def run(self, fn) -> int:
+        """fn() in a forked child inside the namespace; its exit code."""
+        return _in_netns(self.pid, fn)
+
+    def stop(self) -> None:
+        if self.pid:
+            os.kill(self.pid, signal.SIGKILL)
+            os.waitpid(self.pid, 0)
+            self.pid = 0
+
+
 class SyntheticSwitch:
     """The switch namespace: a forked child unshares its network namespace, receives one veth peer
     (``swp<i>``) per node NIC, and runs ``netop-lldp-tx`` with each port's Port Description from
     `plan`.  The last `silent_nics` ports send no LLDP."""
 
     def __init__(self, nic_names: list, plan: list, rng: random.Random, interval: str = "30s", phase: str = "random",
-                 fast_start: bool = True, silent_nics: int = 0):
+                 fast_start: bool = True, silent_nics: int = 0, remote: Optional[list] = None, forward: bool = False):
+        """`remote`: (network-namespace pid, ifname) of NICs of other nodes, wired to the ports after
+        this namespace's `nic_names` (`plan` covers both).  `forward`: the switch routes between its
+        /30s (a leaf of an L3 fabric), so nodes reach each other over their /16 routes."""
         from ..utils.paths import native_bin
 
         self.nic_names, self.plan = list(nic_names), plan
-        self.ports = [f"swp{i}" for i in range(len(self.nic_names))]
+        self.remote = list(remote or [])
+        self.forward = forward
+        self.ports = [f"swp{i}" for i in range(len(self.nic_names) + len(self.remote))]
         self.args = [str(native_bin("netop-lldp-tx")), f"--interval={interval}", f"--phase={phase}", "--assign-ip",
                      f"--seed={rng.randrange(1, 1 << 30)}"]
         if fast_start:
@@ -201,6 +247,9 @@ class SyntheticSwitch:
                 os.close(out_r)
                 if libc.unshare(CLONE_NEWNET) != 0:
                     os._exit(3)
+                if self.forward:
+                    with open("/proc/sys/net/ipv4/ip_forward", "w") as f:
+                        f.write("1")
                 os.write(w1, b"1")
                 os.read(r2, 1)
                 os.dup2(out_w, 1)
@@ -217,6 +266,17 @@ class SyntheticSwitch:
         for node_if, sp in zip(self.nic_names, self.ports):
             rt.veth_add(node_if, sp)
             rt.link_set_netns_pid(rt.link_by_name(sp)["index"], pid)
+        for k, ((node_pid, node_if), sp) in enumerate(zip(self.remote, self.ports[len(self.nic_names):])):
+            tmp_if = f"rn{k}"  # created here, moved, then renamed inside the node's namespace
+            rt.veth_add(tmp_if, sp)
+            rt.link_set_netns_pid(rt.link_by_name(sp)["index"], pid)
+            rt.link_set_netns_pid(rt.link_by_name(tmp_if)["index"], node_pid)
+
+            def rename(old=tmp_if, new=node_if):
+                r = _native().Rtnl()
+                r.link_set_name(r.link_by_name(old)["index"], new)
+            if _in_netns(node_pid, rename) != 0:
+                raise RuntimeError(f"could not name {node_if} in namespace of pid {node_pid}")
         t_switch = time.monotonic()
         os.write(w2, b"1")
         self._out = os.fdopen(out_r)

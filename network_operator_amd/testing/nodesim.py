@@ -19,8 +19,9 @@ Init containers (the host-nic driver container) run to completion, in order, bef
 starts; their images are mapped to local commands by ``init_images`` (an unmapped image fails
 like an image that cannot be pulled).  Not simulated: image pulls, and the probes'
 ``initialDelaySeconds`` / ``periodSeconds`` (``probe_period`` replaces both, so the control plane
-is measured rather than probe timers).  The node's NICs are whatever the calling network
-namespace holds (``testing/e2e.py`` builds veths to a synthetic switch).
+is measured rather than probe timers).  The node's NICs are whatever its network namespace
+holds: the calling process's, or ``netns`` (a ``NetnsHolder``) for the other nodes of a fabric;
+``testing/e2e.py`` builds veths to a synthetic switch.
 
 The reference's only end-to-end test deploys the operator into kind and checks that the
 controller pod runs (reference test/e2e/e2e_test.go:51-120); it never runs an agent.
@@ -70,7 +71,7 @@ class _Container:
 class SimNode:
     def __init__(self, fake, name: str, labels: Dict[str, str], host_root: Path, sysfs_root: Optional[Path] = None,
                  probe_period: float = 0.02, nfd_period: float = 0.01, env: Optional[Dict[str, str]] = None,
-                 init_images: Optional[Dict[str, List[str]]] = None):
+                 init_images: Optional[Dict[str, List[str]]] = None, netns=None):
         self.fake, self.name = fake, name
         self.base_labels = dict(labels)
         self.host_root = Path(host_root)
@@ -78,6 +79,9 @@ class SimNode:
         self.probe_period, self.nfd_period = probe_period, nfd_period
         self.extra_env = dict(env or {})
         self.init_images = dict(init_images or {})
+        # hostNetwork pods join the node's network namespace: None = this process's, else a
+        # testing.netns.NetnsHolder of another simulated node.
+        self.netns = netns
         self.init_runs: List[dict] = []   # {"pod", "name", "rc", "t_start", "t_end"}
         self.containers: Dict[Tuple[str, str], _Container] = {}
         self.features: Dict[str, str] = {}
@@ -168,7 +172,8 @@ class SimNode:
                 rc = -1  # ErrImagePull: no command for this image
             else:
                 with open(c.log_path, "ab") as f:
-                    p = await asyncio.create_subprocess_exec(*ic["argv"], env=self._env(c), stdout=f, stderr=f)
+                    p = await asyncio.create_subprocess_exec(*ic["argv"], env=self._env(c), stdout=f, stderr=f,
+                                                             preexec_fn=self.netns.enter if self.netns else None)
                     rc = await p.wait()
             self.init_runs.append({"pod": c.pod[1], "name": ic["name"], "image": ic["image"], "rc": rc,
                                    "t_start": t, "t_end": time.monotonic()})
@@ -179,7 +184,8 @@ class SimNode:
     def _start(self, c: _Container) -> None:
         env = self._env(c)
         with open(c.log_path, "ab") as f:
-            c.proc = subprocess.Popen(c.argv, env=env, stdout=f, stderr=subprocess.STDOUT)
+            c.proc = subprocess.Popen(c.argv, env=env, stdout=f, stderr=subprocess.STDOUT,
+                                      preexec_fn=self.netns.enter if self.netns else None)
         c.started_at.append(time.monotonic())
         log.info("node %s: started %s (pid %d)", self.name, c.pod[1], c.proc.pid)
 

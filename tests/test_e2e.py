@@ -73,3 +73,26 @@ def test_host_nic_policy_runs_the_driver_container_before_the_agent():
     _check_nics(r, "L3")
     assert all(a == [] for a in r["after_delete"].values())
     assert r["agent_exit_codes"] == [0]
+
+
+def test_one_policy_two_nodes_then_a_collective_across_them():
+    """BASELINE configs[3] through the control plane: one policy, two simulated nodes on one
+    routing leaf.  Both agents address their rails, the policy reports 2/2, and a gloo
+    all-reduce between the nodes runs over the configured /30s and /16 routes."""
+    r = e2e.run_isolated(fabric=True, n_nodes=2, n_nics=2, seed=7)
+    assert r["policy_to_all_good_s"] is not None, r.get("agent_logs")
+    assert (r["policy_status"]["targets"], r["policy_status"]["ready"]) == (2, 2)
+    for j, addrs in enumerate(r["addrs"]):
+        for k, nic in enumerate(r["nics"]):
+            assert addrs[nic] == [r["plan"][j * len(r["nics"]) + k]["local"] + "/30"]
+    assert [c.get("ok") for c in r["collective"]] == [True, True], r["collective"]
+    assert r["delete_to_all_nodes_clean_s"] is not None
+    assert r["agent_exit_codes"] == [[0], [0]] and r["operator_rc"] == 0
+
+
+def test_one_policy_four_nodes():
+    r = e2e.run_isolated(fabric=True, n_nodes=4, n_nics=2, seed=8, collective=False)
+    assert r["policy_to_all_good_s"] is not None, r.get("agent_logs")
+    assert (r["policy_status"]["targets"], r["policy_status"]["ready"]) == (4, 4)
+    assert all(len(set(map(tuple, a.values()))) == 2 for a in r["addrs"])
+    assert r["agent_exit_codes"] == [[0]] * 4
