@@ -59,7 +59,8 @@ async def _until(fn, timeout: float, poll: float = 0.001) -> Optional[float]:
 
 
 async def _scenario(tmp: Path, n_nics: int, mode: str, seed: int, interval: str, fast_start: bool,
-                    teardown: bool, node_name: str, policy_kw: dict, update_mtu: int, config_type: str) -> dict:
+                    teardown: bool, node_name: str, policy_kw: dict, update_mtu: int, config_type: str,
+                    flap: bool) -> dict:
     from ..api.v1alpha1 import types as T
     from ..operator import kube, manager
     from ..operator.kube import ApiClient, KubeConfig
@@ -139,6 +140,23 @@ async def _scenario(tmp: Path, n_nics: int, mode: str, seed: int, interval: str,
                 link = rt.link_by_name(nif)
                 state[nif] = {"up": link["up"], "mtu": link["mtu"], "addrs": rt.addr_list(link["index"])}
             res["state"] = state
+            if flap:
+                # Carrier loss on one switch port: the agent withdraws the label, the probe fails,
+                # the operator reports the node; the port comes back and so does everything else.
+                t1 = time.monotonic()
+                netns.set_switch_port(sw.pid, sw.ports[0], False)
+
+                def degraded():
+                    st = (fake.get_object(P, name) or {}).get("status") or {}
+                    return label_key not in node.node_labels() and st.get("state") != "All good" and st.get("errors")
+
+                t_deg = await _until(degraded, 10)
+                res["flap_status"] = (fake.get_object(P, name) or {}).get("status")
+                t2 = time.monotonic()
+                netns.set_switch_port(sw.pid, sw.ports[0], True)
+                t_back = await _until(lambda: node.node_labels().get(label_key) == "true" and all_good(), 10)
+                res["port_down_to_status_degraded_s"] = round(t_deg - t1, 6) if t_deg else None
+                res["port_up_to_all_good_s"] = round(t_back - t2, 6) if t_back else None
             if update_mtu:
                 # `kubectl edit`: new MTU -> DaemonSet template changes -> the kubelet replaces the
                 # agent -> the new agent configures the NICs again and republishes the label.
@@ -320,12 +338,12 @@ def run_fabric(n_nodes: int = 2, n_nics: int = 2, seed: int = 1, collective: boo
 
 def run_scenario(n_nics: int = 2, mode: str = "L3", seed: int = 1, interval: str = "30s", fast_start: bool = True,
                  teardown: bool = True, node_name: str = "mi355x-0", policy_kw: Optional[dict] = None,
-                 update_mtu: int = 0, config_type: str = "amd-so", keep_tmp: bool = False) -> dict:
+                 update_mtu: int = 0, config_type: str = "amd-so", flap: bool = False, keep_tmp: bool = False) -> dict:
     """Must already run inside a private user+net namespace (``run_isolated``)."""
     tmp = Path(tempfile.mkdtemp(prefix="netop-e2e-"))
     try:
         return asyncio.run(_scenario(tmp, n_nics, mode, seed, interval, fast_start, teardown, node_name,
-                                     dict(policy_kw or {}), update_mtu, config_type))
+                                     dict(policy_kw or {}), update_mtu, config_type, flap))
     finally:
         if not keep_tmp:
             shutil.rmtree(tmp, ignore_errors=True)

@@ -96,3 +96,16 @@ def test_one_policy_four_nodes():
     assert (r["policy_status"]["targets"], r["policy_status"]["ready"]) == (4, 4)
     assert all(len(set(map(tuple, a.values()))) == 2 for a in r["addrs"])
     assert r["agent_exit_codes"] == [[0]] * 4
+
+
+def test_link_failure_is_reported_by_the_policy_and_recovers():
+    """Failure detection end to end: carrier loss on one switch port -> the agent withdraws the
+    label -> readiness probe fails -> Pod not Ready -> the policy names the node in its errors;
+    the port comes back -> label, Pod Ready, "All good"."""
+    r = e2e.run_isolated(n_nics=2, mode="L3", seed=10, flap=True)
+    assert r["port_down_to_status_degraded_s"] is not None, (r.get("flap_status"), r["agent_log"])
+    st = r["flap_status"]
+    assert st["state"] == "Working on it.." and st["ready"] == 0 and st["targets"] == 1
+    assert st["errors"] == ["mi355x-0: scale-out not ready (ContainersNotReady)"]
+    assert any(c["type"] == "Degraded" and c["status"] == "True" for c in st["conditions"])
+    assert r["port_up_to_all_good_s"] is not None, r["agent_log"]
