@@ -36,8 +36,8 @@ test-native:
 check-hardening:            ## PIE / full RELRO / NX stack / stack protector / FORTIFY on the agent binaries (checksec gate)
 	$(PYTHON) tools/check_hardening.py network_operator_amd/_lib/bin/discover network_operator_amd/_lib/bin/netop-topo network_operator_amd/_lib/bin/netop-lldp-tx
 
-test-netns:                 ## veth + synthetic-switch integration (root or user namespaces)
-	$(PYTHON) -m pytest tests/test_netns_integration.py -q
+test-netns:                 ## veth + synthetic-switch integration and the end-to-end runs (root or user namespaces)
+	$(PYTHON) -m pytest tests/test_netns_integration.py tests/test_e2e.py -q
 
 test-gpu:                   ## on an MI355X box
 	$(PYTHON) -m pytest tests -q -m gpu
