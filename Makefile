@@ -44,7 +44,7 @@ test-gpu:                   ## on an MI355X box
 
 test-netns-asan: sanitize   ## the veth + synthetic-switch scenarios against the ASan+UBSan agent
 	NETOP_BIN_DIR=$(CURDIR)/_build-asan/out/bin ASAN_OPTIONS=detect_leaks=1:abort_on_error=1 \
-	  $(PYTHON) -m pytest tests/test_netns_integration.py -q
+	  $(PYTHON) -m pytest tests/test_netns_integration.py tests/test_e2e.py -q
 
 sanitize:                   ## host-side ASan+UBSan build of the agent and its unit suite
 	cmake -S native -B _build-asan -G Ninja -DNETOP_SANITIZE=ON -DNETOP_PYTHON=OFF -DNETOP_OUT=$(CURDIR)/_build-asan/out && \
