@@ -56,12 +56,16 @@ void write_rccl_net(const std::string& path, const std::vector<NicState>& nics, 
 // keys must look like NCCL_* / RCCL_* / HSA_*, values must be single-line (parse_env_extra).
 // `socket_ifnames`: NCCL_SOCKET_IFNAME (exact-match list, "=a,b"): the interfaces RCCL bootstraps
 // over and, without RDMA, moves data over.  Empty = not written.
+// GID: one index shared by every scale-out NIC is pinned with NCCL_IB_GID_INDEX.  When the
+// indices differ (or one is not known yet) RCCL's own per-NIC selection is steered instead:
+// NCCL_IB_ROCE_VERSION_NUM=2 and NCCL_IB_ADDR_FAMILY = AF_INET (L3 /30s) or AF_INET6
+// (`link_local`, L2: the fe80:: GID), both read by RCCL 2.26 / 2.27.
 std::string generate_rccl_env(const std::vector<NicState>& nics, const std::string& topo_file,
                               const std::vector<std::pair<std::string, std::string>>& extra = {},
-                              const std::vector<std::string>& socket_ifnames = {});
+                              const std::vector<std::string>& socket_ifnames = {}, bool link_local = false);
 void write_rccl_env(const std::string& path, const std::vector<NicState>& nics, const std::string& topo_file,
                     const std::vector<std::pair<std::string, std::string>>& extra = {},
-                    const std::vector<std::string>& socket_ifnames = {});
+                    const std::vector<std::string>& socket_ifnames = {}, bool link_local = false);
 
 // NCCL_TOPO_FILE: the node's PCIe tree as RCCL models it (RCCL's topology-XML dialect, the
 // format NCCL_TOPO_DUMP_FILE writes): one <cpu numaid> per root-complex NUMA node, the switches

@@ -840,7 +840,7 @@ void Agent::write_rccl_env_file() {
     const std::string topo_env = write_topo();
     if (cfg_.rccl_env.empty()) return;
     try {
-        artifacts::write_rccl_env(cfg_.rccl_env, nics_, topo_env, rccl_env_extra_, socket_ifnames());
+        artifacts::write_rccl_env(cfg_.rccl_env, nics_, topo_env, rccl_env_extra_, socket_ifnames(), cfg_.mode != "L3");
     } catch (const std::exception& e) {
         NLOG_E("Error writing RCCL env: %s", e.what());
     }

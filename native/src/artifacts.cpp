@@ -183,18 +183,27 @@ std::vector<std::pair<std::string, std::string>> parse_env_extra(const std::stri
 
 std::string generate_rccl_env(const std::vector<NicState>& nics, const std::string& topo_file,
                               const std::vector<std::pair<std::string, std::string>>& extra,
-                              const std::vector<std::string>& socket_ifnames) {
+                              const std::vector<std::string>& socket_ifnames, bool link_local) {
     std::vector<std::string> hcas;
     std::set<int> gids;
+    bool gid_unknown = false;
     for (const NicState* n : sorted(nics)) {
         if (n->rdma_dev.empty() || !n->configured) continue;
         hcas.push_back(n->rdma_dev + ":" + std::to_string(n->rdma_port));
-        if (n->gid_index) gids.insert(*n->gid_index);
+        if (n->gid_index)
+            gids.insert(*n->gid_index);
+        else
+            gid_unknown = true;
     }
     std::string out = "# Generated by the AMD network operator link-discovery agent.\n"
                       "# Source this file (or pass it as an env-file) in RCCL jobs on this node.\n";
     if (!hcas.empty()) out += "NCCL_IB_HCA==" + join(hcas, ",") + "\n";
-    if (gids.size() == 1) out += "NCCL_IB_GID_INDEX=" + std::to_string(*gids.begin()) + "\n";
+    if (gids.size() == 1 && !gid_unknown) {
+        out += "NCCL_IB_GID_INDEX=" + std::to_string(*gids.begin()) + "\n";
+    } else if (!hcas.empty()) {
+        out += "NCCL_IB_ROCE_VERSION_NUM=2\n";
+        out += std::string("NCCL_IB_ADDR_FAMILY=") + (link_local ? "AF_INET6" : "AF_INET") + "\n";
+    }
     if (!hcas.empty()) out += "NCCL_IB_DISABLE=0\n";
     if (!socket_ifnames.empty()) out += "NCCL_SOCKET_IFNAME==" + join(socket_ifnames, ",") + "\n";
     if (!topo_file.empty()) out += "NCCL_TOPO_FILE=" + topo_file + "\n";
@@ -204,8 +213,8 @@ std::string generate_rccl_env(const std::vector<NicState>& nics, const std::stri
 
 void write_rccl_env(const std::string& path, const std::vector<NicState>& nics, const std::string& topo_file,
                     const std::vector<std::pair<std::string, std::string>>& extra,
-                    const std::vector<std::string>& socket_ifnames) {
-    write_file_atomic(path, generate_rccl_env(nics, topo_file, extra, socket_ifnames), 0644);
+                    const std::vector<std::string>& socket_ifnames, bool link_local) {
+    write_file_atomic(path, generate_rccl_env(nics, topo_file, extra, socket_ifnames, link_local), 0644);
 }
 
 // ---------------------------------------------------------------------------

@@ -73,9 +73,15 @@ TEST(rccl_env_contents) {
     CHECK(env.find("NCCL_IB_HCA==mlx5_1:1,mlx5_3:1\n") != std::string::npos);
     CHECK(env.find("NCCL_IB_GID_INDEX=3\n") != std::string::npos);
     CHECK(env.find("NCCL_TOPO_FILE=/etc/amd/scale-out/rccl-topo.xml\n") != std::string::npos);
-    b.gid_index = 5;  // inconsistent GID indices: leave it to RCCL's own selection
+    CHECK(env.find("NCCL_IB_ADDR_FAMILY") == std::string::npos);
+    b.gid_index = 5;  // inconsistent GID indices: steer RCCL's own per-NIC selection instead
     env = generate_rccl_env({a, b}, "");
     CHECK(env.find("NCCL_IB_GID_INDEX") == std::string::npos);
+    CHECK(env.find("NCCL_IB_ROCE_VERSION_NUM=2\nNCCL_IB_ADDR_FAMILY=AF_INET\n") != std::string::npos);
+    b.gid_index.reset();  // one GID not found yet: never pin the other NIC's index for both
+    env = generate_rccl_env({a, b}, "", {}, {}, true);
+    CHECK(env.find("NCCL_IB_GID_INDEX") == std::string::npos);
+    CHECK(env.find("NCCL_IB_ADDR_FAMILY=AF_INET6\n") != std::string::npos);
 }
 
 TEST(networkd_golden_and_rollback) {
