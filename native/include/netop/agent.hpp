@@ -106,6 +106,9 @@ struct Config {
     // then require a real frame to confirm it within lldp_cache_confirm_ns (else the NIC counts
     // as degraded and the label is withdrawn until one arrives).  "" = off.  Used only with
     // --keep-running and the monitor (which does the confirming).
+    // Discovery, the xGMI / GPUDirect checks and the topology file only; no link, address, NM
+    // or label change and no LLDP (no privileges needed): what the agent would configure here.
+    bool dry_run = false;
     std::string lldp_cache;
     int64_t lldp_cache_max_age_ns = 7LL * 24 * 3600 * 1000000000;  // older entries are ignored
     int64_t lldp_cache_confirm_ns = 95LL * 1000000000;              // 3 x msgTxInterval + 5 s
@@ -199,6 +202,7 @@ class Agent {
     // and written at artifact time, so its sysfs walk is off the node-ready critical path.
     void start_topo();
     void write_host_config();  // systemd-networkd files and the LLDP cache
+    void dry_run_report();
     const std::string& topo_xml();  // joins the worker; "" when generation failed
     std::vector<std::string> socket_ifnames() const;
     void check_xgmi();
@@ -238,6 +242,7 @@ class Agent {
     NmFactory nm_factory_;
     std::vector<NicState> nics_;
     topo::DiscoveryResult disc_;
+    std::vector<std::string> dry_run_missing_;  // discovered, but not in this network namespace
     std::future<std::string> topo_future_;
     std::optional<std::string> topo_xml_;
     topo::XgmiReport xgmi_;

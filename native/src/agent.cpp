@@ -776,11 +776,33 @@ void Agent::write_l2_artifacts() {
     write_rccl_env_file();
 }
 
+void Agent::dry_run_report() {
+    for (const auto& n : nics_) {
+        NLOG_I("dry run: %s (%s, mtu %d -> %d, %s): GPU %d %s, RDMA %s, path %s", n.ifname.c_str(),
+               n.link.up() ? "up" : "down", n.link.mtu, cfg_.mtu, n.link.mac.str().c_str(), n.gpu_index,
+               n.gpu_bdf.empty() ? "-" : n.gpu_bdf.c_str(), n.rdma_dev.empty() ? "-" : n.rdma_dev.c_str(),
+               n.pcie_path.empty() ? "-" : n.pcie_path.c_str());
+    }
+    if (!cfg_.rccl_topo.empty()) {
+        start_topo();
+        const std::string env = write_topo();
+        mark("rccl_topo");
+        NLOG_I("dry run: NCCL_TOPO_FILE %s (%zu bytes)%s", cfg_.rccl_topo.c_str(), topo_xml().size(),
+               env.empty() ? " not written" : "");
+    }
+    write_status();
+    NLOG_I("dry run: %zu interface(s) would be configured in %s mode; nothing was changed", nics_.size(),
+           cfg_.mode.c_str());
+}
+
 void Agent::start_topo() {
     if (cfg_.rccl_topo.empty() || topo_future_.valid() || topo_xml_) return;
     std::string root = cfg_.sysfs_root.empty() ? topo::sysfs_root() : cfg_.sysfs_root;
     std::vector<std::string> names;
     for (const auto& n : nics_) names.push_back(n.ifname);
+    if (cfg_.dry_run)  // also the discovered NICs that are not in this network namespace
+        for (const auto& i : disc_.ifnames)
+            if (std::find(names.begin(), names.end(), i) == names.end()) names.push_back(i);
     // Inputs are copied: the worker shares nothing with the agent thread.
     topo_future_ = std::async(std::launch::async, [disc = disc_, names = std::move(names), root = std::move(root)] {
         return artifacts::generate_rccl_topo(disc.gpus, artifacts::topo_nics(disc, names, root), topo::cpu_identity(),
@@ -909,6 +931,10 @@ std::map<std::string, std::string> Agent::status_node() const {
     }
     if (cfg_.xgmi_expect_links >= 0)
         m["xgmi_pairs"] = std::to_string(xgmi_.pairs_connected) + "/" + std::to_string(xgmi_.pairs_expected);
+    if (cfg_.dry_run) {
+        m["dry_run"] = "true";
+        if (!dry_run_missing_.empty()) m["not_in_netns"] = join(dry_run_missing_, ",");
+    }
     return m;
 }
 
@@ -1023,12 +1049,19 @@ void Agent::run(int stop_fd) {
         }
         write_status();
     }
-    pre_cleanups();
+    if (!cfg_.dry_run) pre_cleanups();
 
     auto names = collect_interfaces();
     if (names.empty()) throw AgentError("No interfaces found");
     get_network_configs(names);
-    if (nics_.size() < names.size()) throw AgentError("Not all interfaces were found in the system");
+    if (nics_.size() < names.size()) {
+        if (!cfg_.dry_run) throw AgentError("Not all interfaces were found in the system");
+        NLOG_W("dry run: %zu of %zu discovered interfaces are not in this network namespace", names.size() - nics_.size(),
+               names.size());
+        for (const auto& i : names)
+            if (std::none_of(nics_.begin(), nics_.end(), [&](const NicState& n) { return n.ifname == i; }))
+                dry_run_missing_.push_back(i);
+    }
     mark("discover");
     // The xGMI mesh does not depend on LLDP: verify it up front, so a broken mesh fails in
     // milliseconds instead of after the LLDP wait, and nothing is left for the critical path.
@@ -1037,6 +1070,10 @@ void Agent::run(int stop_fd) {
     if (cfg_.mode == "L3" || !cfg_.require_gdr.empty()) {
         check_gdr();
         mark("gdr");
+    }
+    if (cfg_.dry_run) {
+        dry_run_report();
+        return;
     }
 
     if (cfg_.disable_nm) {

@@ -1056,3 +1056,24 @@ TEST(agent_topology_file_generated_off_the_critical_path) {
     auto env = read_file(f.cfg.rccl_env);
     CHECK(env && env->find("NCCL_TOPO_FILE=/etc/amd/scale-out/rccl-topo.xml\n") != std::string::npos);
 }
+
+TEST(agent_dry_run_changes_nothing) {
+    Fixture f;
+    f.cfg.dry_run = true;
+    f.cfg.rccl_topo = f.tmp.path + "/rccl-topo.xml";
+    f.cfg.sysfs_root = f.tmp.path + "/sys/";
+    f.cfg.interfaces = "ens0,ens1,ens2,ens404";  // one not in this namespace: reported, not fatal
+    auto before = f.ops.links;
+    write_file_atomic(f.cfg.labels.path(), "stale=true\n", 0644);
+    agent::Agent a(f.cfg, f.ops, f.all_valid(), f.nm());
+    a.run(-1);
+    CHECK(f.ops.addrs.empty());
+    CHECK(f.ops.routes.empty());
+    for (auto& [name, l] : before) CHECK_EQ(f.ops.links[name].flags, l.flags);
+    CHECK(path_exists(f.cfg.labels.path()));  // not even the stale label is touched
+    CHECK(path_exists(f.cfg.rccl_topo));
+    auto st = read_file(f.cfg.status_file);
+    CHECK(st && st->find("\"dry_run\":\"true\"") != std::string::npos);
+    CHECK(st->find("\"not_in_netns\":\"ens404\"") != std::string::npos);
+    CHECK(!a.ready());
+}
