@@ -11,6 +11,7 @@
 #include <cstring>
 #include <ctime>
 #include <set>
+#include <system_error>
 
 #include "netop/log.hpp"
 
@@ -804,10 +805,16 @@ void Agent::start_topo() {
         for (const auto& i : disc_.ifnames)
             if (std::find(names.begin(), names.end(), i) == names.end()) names.push_back(i);
     // Inputs are copied: the worker shares nothing with the agent thread.
-    topo_future_ = std::async(std::launch::async, [disc = disc_, names = std::move(names), root = std::move(root)] {
+    auto work = [disc = disc_, names = std::move(names), root = std::move(root)] {
         return artifacts::generate_rccl_topo(disc.gpus, artifacts::topo_nics(disc, names, root), topo::cpu_identity(),
                                              root);
-    });
+    };
+    try {
+        topo_future_ = std::async(std::launch::async, work);
+    } catch (const std::system_error& e) {  // no thread to spare: generate it when it is needed
+        NLOG_V(2, "topology worker thread unavailable (%s): generating on demand", e.what());
+        topo_future_ = std::async(std::launch::deferred, work);
+    }
 }
 
 const std::string& Agent::topo_xml() {

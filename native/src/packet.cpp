@@ -138,7 +138,7 @@ LldpListener::~LldpListener() {
         if (!s) continue;
         try {
             closers.emplace_back([p = s.get()] { ::close(p->release_fd()); });
-        } catch (const std::system_error&) {  // no thread: close it here
+        } catch (...) {  // no thread (destructors must not throw): close it here
             ::close(s->release_fd());
         }
     }
