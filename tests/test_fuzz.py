@@ -9,6 +9,7 @@ is still alive.
 """
 
 import asyncio
+import os
 
 from hypothesis import HealthCheck, given, settings
 from hypothesis import strategies as st
@@ -17,7 +18,7 @@ from network_operator_amd.api.v1alpha1 import types as T
 from network_operator_amd.operator import kube
 from network_operator_amd.operator.controller import PolicyController
 from network_operator_amd.operator.kube import ApiClient, ApiError, KubeConfig
-from network_operator_amd.operator.reconciler import agent_args
+from network_operator_amd.operator.reconciler import agent_args, host_nic_agent_args
 from network_operator_amd.testing.fakeapi import FakeApiServer
 
 NS = "fuzz"
@@ -40,7 +41,9 @@ spec_strategy = st.fixed_dictionaries({
 op_strategy = st.tuples(st.sampled_from(["create", "update", "delete"]), st.sampled_from(["p0", "p1", "p2"]), spec_strategy)
 
 
-@settings(max_examples=12, deadline=None, suppress_health_check=[HealthCheck.too_slow])
+# NETOP_FUZZ_EXAMPLES raises the count for a longer soak (`NETOP_FUZZ_EXAMPLES=200 make fuzz`).
+@settings(max_examples=int(os.environ.get("NETOP_FUZZ_EXAMPLES", "12")), deadline=None,
+          suppress_health_check=[HealthCheck.too_slow])
 @given(ops=st.lists(op_strategy, min_size=1, max_size=12))
 def test_random_policy_churn_converges(ops):
     async def body():
@@ -71,10 +74,12 @@ def test_random_policy_churn_converges(ops):
                 assert set(dss) <= set(pols), "orphan DaemonSet"
                 for name, p in pols.items():
                     pol = T.NetworkClusterPolicy.from_dict(p)
-                    if pol.spec.configurationType != T.CONFIG_AMD_SCALE_OUT:
+                    want = {T.CONFIG_AMD_SCALE_OUT: agent_args, T.CONFIG_HOST_NIC: host_nic_agent_args}.get(
+                        pol.spec.configurationType)
+                    if want is None:
                         continue  # unknown types never get a DaemonSet (they error and back off)
                     assert name in dss, f"no DaemonSet for {name}"
-                    assert dss[name]["spec"]["template"]["spec"]["containers"][0]["args"] == agent_args(pol)
+                    assert dss[name]["spec"]["template"]["spec"]["containers"][0]["args"] == want(pol)
                     assert p.get("status", {}).get("state") == "No targets"
                 return True
 
