@@ -15,11 +15,14 @@
 //     (main.go:212,239-246) unless Config::label_without_peers (compat) is set.
 #pragma once
 
+#include <sys/types.h>
+
 #include <cstdint>
 #include <functional>
 #include <future>
 #include <map>
 #include <memory>
+#include <mutex>
 #include <optional>
 #include <set>
 #include <string>
@@ -243,6 +246,12 @@ class Agent {
     std::vector<NicState> nics_;
     topo::DiscoveryResult disc_;
     std::vector<std::string> dry_run_missing_;  // discovered, but not in this network namespace
+    struct TopoWorker {  // the topology thread's Linux tid, for its priority
+        std::mutex mu;
+        pid_t tid = 0;
+        bool running = false;
+    };
+    std::shared_ptr<TopoWorker> topo_worker_;
     std::future<std::string> topo_future_;
     std::optional<std::string> topo_xml_;
     topo::XgmiReport xgmi_;

