@@ -83,7 +83,9 @@ struct DiscoveryOptions {
 // file needs (discovery skips them: six fewer sysfs reads per device on the critical path).
 std::optional<PciDev> read_pci_dev(const std::string& root, const std::string& device_path, bool topo_attrs = true);
 // The same for a path that is already canonical (no symlink to resolve), e.g. PciDev::path.
-std::optional<PciDev> read_pci_dir(const std::string& canonical_path, bool topo_attrs = true);
+std::optional<PciDev> read_pci_dir(const std::string& canonical_path, bool topo_attrs = true, bool with_driver = true);
+// Adds the topology attributes to a device discovery read without them; false if unreadable.
+bool read_topo_attrs(PciDev& d);
 // The PCI device behind a netdev (<root>/class/net/<ifname>/device); nullopt for virtual links.
 std::optional<PciDev> netdev_pci(const std::string& root, const std::string& ifname);
 // The ancestors RCCL puts above `d` in its topology tree, outermost first.  RCCL (NCCL's

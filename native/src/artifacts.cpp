@@ -289,7 +289,10 @@ std::string generate_rccl_topo(const std::vector<topo::Gpu>& gpus, const std::ve
     std::map<std::string, topo::PciDev> bridges;
     auto place = [&](const topo::PciDev& found) -> XmlPci& {
         std::optional<topo::PciDev> full;  // discovery reads devices without the topology attributes
-        if (!found.topo_attrs) full = topo::read_pci_dir(found.path);
+        if (!found.topo_attrs) {
+            full = found;
+            topo::read_topo_attrs(*full);
+        }
         const topo::PciDev& leaf = full ? *full : found;
         auto parents = topo::rccl_pci_parents(leaf, &bridges);
         auto* level = &cpus[parents.empty() ? leaf.numa : parents.front().numa];

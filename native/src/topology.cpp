@@ -97,7 +97,31 @@ std::optional<PciDev> read_pci_dev(const std::string& root, const std::string& d
     return read_pci_dir(*real, topo_attrs);
 }
 
-std::optional<PciDev> read_pci_dir(const std::string& real, bool topo_attrs) {
+static void topo_attrs_at(int dir, PciDev& d) {
+    d.topo_attrs = true;
+    d.subsystem_vendor = read_hex("subsystem_vendor", dir);
+    d.subsystem_device = read_hex("subsystem_device", dir);
+    auto str = [dir](const char* name) {
+        auto v = read_attr(name, dir);
+        return v ? trim(*v) : std::string();
+    };
+    d.max_link_speed = str("max_link_speed");
+    d.max_link_width = read_int("max_link_width", 0, dir);
+    // The port above: the parent directory (the path is canonical, so ".." is its dirname).
+    d.port_max_link_speed = str("../max_link_speed");
+    d.port_max_link_width = read_int("../max_link_width", 0, dir);
+}
+
+bool read_topo_attrs(PciDev& d) {
+    if (d.topo_attrs) return true;
+    const int dir = ::open(d.path.c_str(), O_PATH | O_DIRECTORY | O_CLOEXEC);
+    if (dir < 0) return false;
+    topo_attrs_at(dir, d);
+    ::close(dir);
+    return true;
+}
+
+std::optional<PciDev> read_pci_dir(const std::string& real, bool topo_attrs, bool with_driver) {
     PciDev d;
     d.path = real;
     d.bdf = path_basename(real);
@@ -112,7 +136,7 @@ std::optional<PciDev> read_pci_dir(const std::string& real, bool topo_attrs) {
     } guard{dir};
     for (auto& c : split(real.substr(pos + 9), '/'))
         if (!c.empty()) d.chain.push_back(c);
-    {  // "driver" is a symlink to .../drivers/<name>: its last component is all we need
+    if (with_driver) {  // "driver" is a symlink to .../drivers/<name>: its last component is all we need
         char buf[PATH_MAX];
         ssize_t n = ::readlinkat(dir, "driver", buf, sizeof buf - 1);
         if (n > 0) d.driver = path_basename(std::string(buf, size_t(n)));
@@ -121,19 +145,7 @@ std::optional<PciDev> read_pci_dir(const std::string& real, bool topo_attrs) {
     d.device = read_hex("device", dir);
     d.pci_class = read_hex("class", dir);
     d.numa = read_int("numa_node", -1, dir);
-    if (!topo_attrs) return d;
-    d.topo_attrs = true;
-    d.subsystem_vendor = read_hex("subsystem_vendor", dir);
-    d.subsystem_device = read_hex("subsystem_device", dir);
-    auto str = [dir](const char* name) {
-        auto v = read_attr(name, dir);
-        return v ? trim(*v) : std::string();
-    };
-    d.max_link_speed = str("max_link_speed");
-    d.max_link_width = read_int("max_link_width", 0, dir);
-    // The port above: the parent directory (the path is canonical, so ".." is its dirname).
-    d.port_max_link_speed = str("../max_link_speed");
-    d.port_max_link_width = read_int("../max_link_width", 0, dir);
+    if (topo_attrs) topo_attrs_at(dir, d);
     return d;
 }
 
@@ -200,7 +212,7 @@ std::vector<PciDev> rccl_pci_parents(const PciDev& d, std::map<std::string, PciD
                 continue;
             }
         }
-        auto p = read_pci_dir(dir);
+        auto p = read_pci_dir(dir, true, false);  // a bridge's driver (pcieport) is not needed
         if (!p) break;  // unreadable bridge: RCCL would stop there too (no sysfs entry)
         if (cache) cache->emplace(dir, *p);
         out.push_back(std::move(*p));
