@@ -252,6 +252,9 @@ class Agent {
         bool running = false;
     };
     std::shared_ptr<TopoWorker> topo_worker_;
+    std::string topo_fp_;        // inputs of the topology file (its ".key" sidecar)
+    bool topo_reused_ = false;   // the file on disk is current: nothing to write
+    std::string topo_fingerprint(const std::vector<std::string>& names) const;
     std::future<std::string> topo_future_;
     std::optional<std::string> topo_xml_;
     topo::XgmiReport xgmi_;

@@ -799,6 +799,24 @@ void Agent::dry_run_report() {
            cfg_.mode.c_str());
 }
 
+std::string Agent::topo_fingerprint(const std::vector<std::string>& names) const {
+    // Everything the file is generated from that can change without a reboot: the generator,
+    // the GPUs and the NICs (name, PCI function, RDMA device).  The PCIe tree above them is
+    // fixed until the next boot, hence the boot id.
+    std::string root = cfg_.sysfs_root.empty() ? topo::sysfs_root() : cfg_.sysfs_root;
+    std::string fp = strfmt("netop-rccl-topo v%d\n", artifacts::kRcclTopoXmlVersion);
+    auto boot = read_file("/proc/sys/kernel/random/boot_id");
+    fp += "boot " + (boot ? trim(*boot) : std::string("?")) + "\nroot " + root + "\n";
+    for (const auto& g : disc_.gpus) fp += "gpu " + g.pci.path + "\n";
+    for (const auto& n : names) {
+        std::string where = "-";
+        for (const auto& d : disc_.nics)
+            if (d.ifname == n) where = d.pci.path + " " + d.rdma_dev + ":" + std::to_string(d.rdma_port);
+        fp += "nic " + n + " " + where + "\n";
+    }
+    return fp;
+}
+
 void Agent::start_topo() {
     if (cfg_.rccl_topo.empty() || topo_future_.valid() || topo_xml_) return;
     std::string root = cfg_.sysfs_root.empty() ? topo::sysfs_root() : cfg_.sysfs_root;
@@ -807,6 +825,18 @@ void Agent::start_topo() {
     if (cfg_.dry_run)  // also the discovered NICs that are not in this network namespace
         for (const auto& i : disc_.ifnames)
             if (std::find(names.begin(), names.end(), i) == names.end()) names.push_back(i);
+    // A restart within the same boot (DaemonSet rollout, crash) finds the file it wrote last time:
+    // reuse it when it was generated from the same inputs.
+    topo_fp_ = topo_fingerprint(names);
+    auto key = read_file(cfg_.rccl_topo + ".key");
+    if (key && *key == topo_fp_) {
+        if (auto xml = read_file(cfg_.rccl_topo); xml && !xml->empty()) {
+            topo_xml_ = *xml;
+            topo_reused_ = true;
+            NLOG_V(2, "RCCL topology file %s is current (same boot and devices): reused", cfg_.rccl_topo.c_str());
+            return;
+        }
+    }
     // Inputs are copied: the worker shares nothing with the agent thread.
     auto worker = std::make_shared<TopoWorker>();
     topo_worker_ = worker;
@@ -862,11 +892,16 @@ std::string Agent::write_topo() {
     if (cfg_.rccl_topo.empty()) return "";
     const std::string& xml = topo_xml();
     if (xml.empty()) return "";  // rccl.env then names no topology
-    try {
-        write_file_atomic(cfg_.rccl_topo, xml, 0644);
-    } catch (const std::exception& e) {
-        NLOG_E("Error writing RCCL topology file: %s", e.what());
-        return "";
+    if (!topo_reused_) {
+        try {
+            ::unlink((cfg_.rccl_topo + ".key").c_str());  // never a key next to a file it does not describe
+            write_file_atomic(cfg_.rccl_topo, xml, 0644);
+            if (!topo_fp_.empty()) write_file_atomic(cfg_.rccl_topo + ".key", topo_fp_, 0644);
+        } catch (const std::exception& e) {
+            NLOG_E("Error writing RCCL topology file: %s", e.what());
+            return "";
+        }
+        topo_reused_ = true;  // written: later refreshes (re-addressing) keep it
     }
     return cfg_.rccl_topo_env_path.empty() ? cfg_.rccl_topo : cfg_.rccl_topo_env_path;
 }

@@ -1077,3 +1077,42 @@ TEST(agent_dry_run_changes_nothing) {
     CHECK(st->find("\"not_in_netns\":\"ens404\"") != std::string::npos);
     CHECK(!a.ready());
 }
+
+TEST(agent_topology_file_reused_within_a_boot) {
+    Fixture f;
+    f.cfg.keep_running = false;
+    f.cfg.rccl_topo = f.tmp.path + "/rccl-topo.xml";
+    f.cfg.rccl_env = f.tmp.path + "/rccl.env";
+    f.cfg.sysfs_root = f.tmp.path + "/sys/";
+    {
+        agent::Agent a(f.cfg, f.ops, f.all_valid(), f.nm());
+        a.run(-1);
+    }
+    auto key = read_file(f.cfg.rccl_topo + ".key");
+    CHECK(key && key->find("boot ") != std::string::npos);
+    // A restart in the same boot with the same devices keeps the file it finds.
+    write_file_atomic(f.cfg.rccl_topo, "<system version=\"2\">\n<!-- kept -->\n</system>\n", 0644);
+    {
+        FakeNetOps ops2;
+        ops2.add_link("ens0", 10, "02:00:00:00:00:10", false);
+        ops2.add_link("ens1", 11, "02:00:00:00:00:11", true);
+        ops2.add_link("ens2", 12, "02:00:00:00:00:12", false);
+        agent::Agent a(f.cfg, ops2, f.all_valid(), f.nm());
+        a.run(-1);
+    }
+    CHECK(read_file(f.cfg.rccl_topo)->find("kept") != std::string::npos);
+    auto env = read_file(f.cfg.rccl_env);
+    CHECK(env && env->find("NCCL_TOPO_FILE=") != std::string::npos);
+    // Another boot (or other devices): regenerated.
+    write_file_atomic(f.cfg.rccl_topo + ".key", "netop-rccl-topo v2\nboot another\n", 0644);
+    {
+        FakeNetOps ops3;
+        ops3.add_link("ens0", 10, "02:00:00:00:00:10", false);
+        ops3.add_link("ens1", 11, "02:00:00:00:00:11", true);
+        ops3.add_link("ens2", 12, "02:00:00:00:00:12", false);
+        agent::Agent a(f.cfg, ops3, f.all_valid(), f.nm());
+        a.run(-1);
+    }
+    CHECK(read_file(f.cfg.rccl_topo)->find("kept") == std::string::npos);
+    CHECK(*read_file(f.cfg.rccl_topo + ".key") == *key);
+}

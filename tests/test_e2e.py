@@ -33,7 +33,7 @@ def test_l3_policy_labels_the_node_and_deletion_undoes_it():
     assert labels["amd.feature.node.kubernetes.io/gpu-scale-out.mode"] == "L3"
     assert labels["amd.feature.node.kubernetes.io/gpu-scale-out.nics"] == "4"
     _check_nics(r, "L3")
-    assert r["artifacts"] == ["rccl-net.json", "rccl-topo.xml", "rccl.env"]
+    assert r["artifacts"] == ["rccl-net.json", "rccl-topo.xml", "rccl-topo.xml.key", "rccl.env"]
     assert "NCCL_TOPO_FILE=/etc/amd/scale-out/rccl-topo.xml" in r["rccl_env"]
     # The agent ran with the DaemonSet's own args, host paths mapped.
     assert "--mode=L3" in r["agent_argv"] and "--rccl-topo-env-path=/etc/amd/scale-out/rccl-topo.xml" in r["agent_argv"]
@@ -48,7 +48,7 @@ def test_l2_policy_labels_the_node():
     assert r["policy_to_all_good_s"] is not None, (r["policy_status"], r["agent_log"])
     assert r["node_labels"]["amd.feature.node.kubernetes.io/gpu-scale-out.mode"] == "L2"
     _check_nics(r, "L2")
-    assert r["artifacts"] == ["rccl-topo.xml", "rccl.env"]
+    assert r["artifacts"] == ["rccl-topo.xml", "rccl-topo.xml.key", "rccl.env"]
     assert all(a == [] for a in r["after_delete"].values())
 
 
