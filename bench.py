@@ -149,23 +149,71 @@ def node_ready_gpu_side(sysfs: str = "/sys/") -> dict:
     return out
 
 
+_LAUNCH_ENV = ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK", "ROLE_WORLD_SIZE",
+               "MASTER_ADDR", "MASTER_PORT")
+
+
+def torch_env_probe(world: int, nbytes: int, budget_s: float, device: str = "cuda", variants=None,
+                    steps: int = 5) -> list:
+    """busbw of the timed loop itself (torch.distributed, this torch's RCCL, bf16, `nbytes`) under
+    each RCCL knob variant of ``rccl_bench.ENV_PROBES``: bench.py runs again in a fresh set of
+    `world` rank processes per variant, with the variant in its environment and every extra
+    measurement off.  Variants not started within `budget_s` are reported as skipped.  A hung
+    variant is killed with its whole process group (its ranks hold GPUs)."""
+    import signal
+    import subprocess
+
+    from network_operator_amd.parallel import rccl_bench
+
+    base = {k: v for k, v in os.environ.items() if k not in _LAUNCH_ENV and not k.startswith("TORCHELASTIC_")}
+    out = []
+    t0 = time.monotonic()
+    for extra in (variants if variants is not None else rccl_bench.ENV_PROBES):
+        left = budget_s - (time.monotonic() - t0)
+        if left <= 0:
+            out.append({"env": extra, "skipped": "time budget spent"})
+            continue
+        cmd = [sys.executable, os.path.abspath(__file__), "--gpus", str(world), "--steps", str(steps), "--warmup", "2",
+               "--bytes", str(nbytes), "--sweep", "", "--collectives", "", "--node-ready", "off", "--xgmi-probe", "0",
+               "--native-rccl", "0", "--xgmi-allreduce", "0", "--rccl-autotune", "0", "--gpu-side", "0",
+               "--device", device]
+        p = subprocess.Popen(cmd, env=dict(base, **extra), stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                             start_new_session=True)
+        try:
+            so, se = p.communicate(timeout=left + 30)
+        except subprocess.TimeoutExpired:
+            os.killpg(p.pid, signal.SIGKILL)
+            p.communicate()
+            out.append({"env": extra, "error": "timed out"})
+            continue
+        lines = [x for x in so.splitlines() if x.startswith("{")]
+        if p.returncode != 0 or not lines:
+            out.append({"env": extra, "error": f"rc={p.returncode}: {se[-300:]}"})
+            continue
+        j = json.loads(lines[-1])
+        out.append({"env": extra, "busbw_GBps": j["busbw_GBps"], "time_us": j["ms_per_step"] * 1e3})
+    return out
+
+
 def _rccl_autotune(rank: int, world: int, nbytes: int, budget_s: float = 120.0,
-                   started: float = time.time()) -> dict:
+                   started: float = time.time(), device: str = "cuda", variants=None) -> dict:
     """RCCL reads its parameters once per process, at communicator creation, so they must be
     chosen before init_process_group.
 
-    Rank 0 measures the knob variants of ``rccl_bench.ENV_PROBES`` with the native harness over
-    the node's first `world` GPUs. Each variant runs in a fresh process, and all of them must fit
-    in ``budget_s``. Rank 0 publishes the winner through a file in /tmp keyed by the rendezvous
-    port, and every rank exports it. A variant must beat the defaults by >= 3 %
-    (``rccl_bench.choose_env``). This is how the validation Job tunes a node's ``rccl.env``
-    (``validate.py --tune-rccl``). It is still RCCL: only its documented environment changes."""
+    Rank 0 measures the knob variants of ``rccl_bench.ENV_PROBES`` with bench.py itself
+    (``torch_env_probe``: the same torch, RCCL build, dtype and message as the timed loop) over
+    the node's first `world` GPUs.  Each variant runs in fresh processes, and all of them must
+    fit in ``budget_s``.  Rank 0 publishes the winner through a file in /tmp keyed by the
+    rendezvous port, and every rank exports it.  A variant must beat the defaults by >= 3 %
+    (``rccl_bench.choose_env``).  (The validation Job tunes a node's ``rccl.env`` the same way
+    with the native harness, ``validate.py --tune-rccl``.)  It is still RCCL: only its documented
+    environment changes."""
     path = f"/tmp/netop-rccl-autotune-{os.environ.get('MASTER_PORT', '0')}.json"
     if rank == 0:
         try:
             from network_operator_amd.parallel import rccl_bench
 
-            probes = rccl_bench.env_probe(world, nbytes, budget_s=budget_s)
+            probes = torch_env_probe(world, nbytes, budget_s, device=device, variants=variants)
             doc = dict(rccl_bench.choose_env(probes), probes=probes)
         except Exception as e:  # never leave the other ranks waiting: defaults, and say why
             doc = {"chosen": {}, "error": str(e)[-300:]}
@@ -217,6 +265,9 @@ def main(argv=None) -> int:
                          "(within --rccl-autotune-budget s) and every rank uses the fastest (>= 3%% better than "
                          "the defaults) for the run; 0 = RCCL defaults")
     ap.add_argument("--rccl-autotune-budget", type=float, default=120.0)
+    ap.add_argument("--gpu-side", type=int, default=1, help="rank 0: time the agent's unprivileged phases on this box")
+    # CPU rehearsal of the autotune plumbing (tests): run it with gloo too, on the first K variants.
+    ap.add_argument("--autotune-cpu-variants", type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument("--xgmi-allreduce", type=int, default=1,
                     help="also run the direct two-shot xGMI all-reduce on rank 0 (n > 1)")
     # CPU rehearsal of the multi-rank path (tests): gloo backend, fp32 on the host.
@@ -243,8 +294,14 @@ def main(argv=None) -> int:
         return 2
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", str(_free_port()))
+    tuned = None
     if args.device == "cpu":
         device, dtype = torch.device("cpu"), torch.float32
+        if args.autotune_cpu_variants and world > 1:
+            from network_operator_amd.parallel import rccl_bench
+
+            tuned = _rccl_autotune(rank, world, args.bytes, args.rccl_autotune_budget, device="cpu",
+                                   variants=rccl_bench.ENV_PROBES[:args.autotune_cpu_variants])
         dist.init_process_group("gloo", rank=rank, world_size=world)
     else:
         if not torch.cuda.is_available():
@@ -380,7 +437,7 @@ def main(argv=None) -> int:
             direct_mp = {"error": str(e)[-500:]}
 
     gpu_side = None
-    if rank == 0:
+    if rank == 0 and args.gpu_side:
         try:
             gpu_side = node_ready_gpu_side()
         except Exception as e:
@@ -435,7 +492,7 @@ def main(argv=None) -> int:
             "collectives": others,
             "xgmi_probe": probe,
             "native_rccl": native,
-            "rccl_autotune": tuned if args.device == "cuda" else None,
+            "rccl_autotune": tuned,
             "xgmi_allreduce": direct,
             "xgmi_allreduce_multiprocess": direct_mp,
             "algbw_GBps": algbw,

@@ -148,3 +148,39 @@ def test_rccl_knob_choice_needs_a_real_gain():
     pick = R.choose_env(probes)
     assert pick["chosen"] == {"NCCL_MIN_NCHANNELS": "112"} and pick["baseline_busbw_GBps"] == 300.0
     assert R.choose_env([{"env": {"A": "1"}, "busbw_GBps": 1.0}])["chosen"] == {}  # no baseline, no choice
+
+
+def test_autotune_measures_variants_with_bench_itself(tmp_path):
+    """The RCCL knob autotune runs bench.py again per variant (fresh rank processes with the
+    variant in their environment) and publishes the choice to every rank before init."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    cmd = [sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1", "--device", "cpu",
+           "--bytes", str(1 << 18), "--sweep", "", "--collectives", "", "--node-ready", "off",
+           "--autotune-cpu-variants", "2", "--rccl-autotune-budget", "120"]
+    j = _bench_line(subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=tmp_path,
+                                   env=dict(env, OMP_NUM_THREADS="1")))
+    t = j["rccl_autotune"]
+    assert [p["env"] for p in t["probes"]] == [{}, {"NCCL_MIN_NCHANNELS": "64"}]
+    assert all(p.get("busbw_GBps", 0) > 0 for p in t["probes"]), t["probes"]
+    assert t["baseline_busbw_GBps"] == t["probes"][0]["busbw_GBps"]
+    assert isinstance(t["chosen"], dict)
+    assert j["verified"] is True
+
+
+def test_autotune_budget_skips_late_variants(tmp_path):
+    sys.path.insert(0, str(ROOT))
+    import bench
+
+    out = bench.torch_env_probe(2, 1 << 16, budget_s=0.0, device="cpu", variants=[{}, {"A": "1"}])
+    assert out == [{"env": {}, "skipped": "time budget spent"}, {"env": {"A": "1"}, "skipped": "time budget spent"}]
+
+
+@pytest.mark.gpu
+def test_autotune_probe_runs_the_cuda_bench():
+    """The variant runner's command line is accepted by the cuda path (n = 1 on the box: busbw 0)."""
+    sys.path.insert(0, str(ROOT))
+    import bench
+
+    out = bench.torch_env_probe(1, 1 << 20, budget_s=90, device="cuda", variants=[{}, {"NCCL_MIN_NCHANNELS": "64"}])
+    assert [o.get("error") for o in out] == [None, None], out
+    assert all(o["busbw_GBps"] == 0.0 and o["time_us"] > 0 for o in out)
