@@ -261,9 +261,9 @@ def main(argv=None) -> int:
                     help="seconds rank 0 may spend on the diagnostics after the timed loop (probe, native "
                          "harness, knob probe, direct all-reduce); later ones are skipped once it is spent")
     ap.add_argument("--rccl-autotune", type=int, default=1,
-                    help="n > 1: before RCCL starts, rank 0 measures RCCL knob variants with the native harness "
-                         "(within --rccl-autotune-budget s) and every rank uses the fastest (>= 3%% better than "
-                         "the defaults) for the run; 0 = RCCL defaults")
+                    help="n > 1: before RCCL starts, rank 0 measures RCCL knob variants by running this bench "
+                         "again per variant (within --rccl-autotune-budget s) and every rank uses the fastest "
+                         "(>= 3%% better than the defaults) for the run; 0 = RCCL defaults")
     ap.add_argument("--rccl-autotune-budget", type=float, default=120.0)
     ap.add_argument("--gpu-side", type=int, default=1, help="rank 0: time the agent's unprivileged phases on this box")
     # CPU rehearsal of the autotune plumbing (tests): run it with gloo too, on the first K variants.
