@@ -12,7 +12,7 @@ from __future__ import annotations
 import asyncio
 import logging
 import time
-from typing import List, Optional
+from typing import Dict, List, Optional
 
 from ..api.v1alpha1 import types as T
 from . import kube
@@ -26,6 +26,11 @@ from .workqueue import RateLimitingQueue
 log = logging.getLogger("controller")
 
 CONTROLLER_NAME = "networkclusterpolicy"
+
+
+def pod_ready(pod: Optional[dict]) -> bool:
+    conds = ((pod or {}).get("status") or {}).get("conditions") or []
+    return any(c.get("type") == "Ready" and c.get("status") == "True" for c in conds)
 
 
 class PolicyController:
@@ -54,6 +59,7 @@ class PolicyController:
         self.pods.add_handler(self._on_pod)
         self._tasks: List[asyncio.Task] = []
         self.reconciles = 0
+        self._pod_seen: Dict[str, float] = {}  # agent Pod uid -> monotonic time first seen, until Ready
 
     async def _on_policy(self, ev: str, obj: dict, old: Optional[dict]) -> None:
         await self._enqueue(obj["metadata"]["name"])
@@ -69,7 +75,22 @@ class PolicyController:
             ds = self.daemonsets.get(ref["name"], self.namespace)
             owner = controller_of(ds) if ds else None
             if owner and owner.get("kind") == T.KIND:
+                self._observe_readiness(owner["name"], ev, obj, old)
                 await self._enqueue(owner["name"])
+
+    def _observe_readiness(self, policy: str, ev: str, obj: dict, old: Optional[dict]) -> None:
+        uid = obj.get("metadata", {}).get("uid", "")
+        if ev == "DELETED":
+            self._pod_seen.pop(uid, None)
+            return
+        now, was = time.monotonic(), pod_ready(old) if old else False
+        ready = pod_ready(obj)
+        if not ready:
+            self._pod_seen.setdefault(uid, now)
+            if was:
+                self.metrics.agent_unready.labels(policy).inc()
+        elif not was and uid in self._pod_seen:
+            self.metrics.agent_ready_time.labels(policy).observe(now - self._pod_seen.pop(uid))
 
     async def requeue_all(self) -> None:
         """Reconcile every policy again (e.g. after a cluster dependency appeared or vanished)."""

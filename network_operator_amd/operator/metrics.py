@@ -34,6 +34,15 @@ class OperatorMetrics:
                                     ["policy"], registry=r)
         self.policy_ready = Gauge("amd_network_operator_policy_ready",
                                   "Nodes whose agent published the scale-out readiness label", ["policy"], registry=r)
+        # Node readiness as the operator sees it: the agent Pod's Ready condition (the readiness
+        # probe checks the scale-out label), per policy.
+        self.agent_ready_time = Histogram(
+            "amd_network_operator_agent_ready_seconds",
+            "Time from the operator first seeing an agent Pod to its Ready condition (node scale-out ready)",
+            ["policy"], buckets=(0.05, 0.1, 0.25, 0.5, 1, 2.5, 5, 10, 15, 30, 60, 120, 300, 600), registry=r)
+        self.agent_unready = Counter("amd_network_operator_agent_unready_total",
+                                     "Agent Pods that went from Ready to not Ready (link loss, lost peer, ...)",
+                                     ["policy"], registry=r)
         self.seed_in_sync = Gauge("amd_network_operator_policies_file_in_sync",
                                   "1 when the policies of --policies-file (the Helm release's) match the cluster",
                                   registry=r)

@@ -187,6 +187,11 @@ def test_status_tracks_targets_and_agent_readiness():
             events = [e for e in fake.list_objects(kube.EVENTS)]
             assert any(e["reason"] == "DaemonSetCreated" for e in events)
             assert any(e["reason"] == "AllNodesReady" for e in events)
+            # Node readiness as the operator measured it: three Pods went Ready, one went unready.
+            reg = ctl.metrics.registry
+            assert reg.get_sample_value("amd_network_operator_agent_ready_seconds_count", {"policy": "policy"}) == 3
+            assert reg.get_sample_value("amd_network_operator_agent_ready_seconds_sum", {"policy": "policy"}) > 0
+            assert reg.get_sample_value("amd_network_operator_agent_unready_total", {"policy": "policy"}) == 1
     run(body())
 
 
