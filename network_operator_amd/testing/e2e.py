@@ -58,6 +58,31 @@ async def _until(fn, timeout: float, poll: float = 0.001) -> Optional[float]:
     return None
 
 
+def _free_port() -> int:
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+async def _scrape(port: int, names) -> dict:
+    """The operator's own /metrics (plain HTTP: no --metrics-secure here), selected series."""
+    import aiohttp
+
+    out: dict = {}
+    async with aiohttp.ClientSession() as s:
+        async with s.get(f"http://127.0.0.1:{port}/metrics") as r:
+            text = await r.text()
+    for line in text.splitlines():
+        for n in names:
+            if line.startswith(n + "{") or line.startswith(n + " "):
+                out[line.rsplit(" ", 1)[0]] = float(line.rsplit(" ", 1)[1])
+    return out
+
+
 async def _scenario(tmp: Path, n_nics: int, mode: str, seed: int, interval: str, fast_start: bool,
                     teardown: bool, node_name: str, policy_kw: dict, update_mtu: int, config_type: str,
                     flap: bool) -> dict:
@@ -94,8 +119,10 @@ async def _scenario(tmp: Path, n_nics: int, mode: str, seed: int, interval: str,
     os.environ["OPERATOR_NAMESPACE"] = "amd-network-operator"
     stop = asyncio.Event()
     started = asyncio.Event()
+    metrics_port = _free_port()
     op = asyncio.ensure_future(manager.run(["--master", url, "--health-probe-bind-address=0",
-                                            "--metrics-bind-address=0", "--dependency-check-interval=0"],
+                                            f"--metrics-bind-address=127.0.0.1:{metrics_port}",
+                                            "--dependency-check-interval=0"],
                                            stop=stop, started=started))
     kmd = [sys.executable, "-m", "network_operator_amd.testing.fakesysfs", "bind", KMD_DRIVER, *nic_names]
     node = SimNode(fake, node_name, {"amd.feature.node.kubernetes.io/gpu-ready": "true"}, tmp / "host",
@@ -128,6 +155,9 @@ async def _scenario(tmp: Path, n_nics: int, mode: str, seed: int, interval: str,
             res.update(policy_to_daemonset_s=rel(t_ds), policy_to_agent_start_s=rel(t_agent),
                        policy_to_node_label_s=rel(t_label), policy_to_all_good_s=rel(t_good))
             res["policy_status"] = (fake.get_object(P, name) or {}).get("status")
+            res["operator_metrics"] = await _scrape(metrics_port, ("amd_network_operator_agent_ready_seconds_count",
+                                                                   "amd_network_operator_agent_ready_seconds_sum",
+                                                                   "amd_network_operator_policy_ready"))
             res["init_runs"] = [dict(r, t_start=rel(r["t_start"]), t_end=rel(r["t_end"])) for r in node.init_runs]
             res["agent_started_s"] = [rel(t) for x in node.containers.values() for t in x.started_at]
             res["node_labels"] = node.node_labels()

@@ -34,6 +34,10 @@ def test_l3_policy_labels_the_node_and_deletion_undoes_it():
     assert labels["amd.feature.node.kubernetes.io/gpu-scale-out.nics"] == "4"
     _check_nics(r, "L3")
     assert r["artifacts"] == ["rccl-net.json", "rccl-topo.xml", "rccl-topo.xml.key", "rccl.env"]
+    # The operator measured the node's readiness itself (agent Pod seen -> Ready).
+    m = r["operator_metrics"]
+    assert m['amd_network_operator_agent_ready_seconds_count{policy="scale-out"}'] == 1
+    assert 0 < m['amd_network_operator_agent_ready_seconds_sum{policy="scale-out"}'] < 5
     assert "NCCL_TOPO_FILE=/etc/amd/scale-out/rccl-topo.xml" in r["rccl_env"]
     # The agent ran with the DaemonSet's own args, host paths mapped.
     assert "--mode=L3" in r["agent_argv"] and "--rccl-topo-env-path=/etc/amd/scale-out/rccl-topo.xml" in r["agent_argv"]
