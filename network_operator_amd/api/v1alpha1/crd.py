@@ -83,6 +83,22 @@ def openapi_schema() -> dict:
                                                 "comma-separated interface list.  Empty = auto.",
                                  "pattern": r"^(auto|none|[A-Za-z0-9_.:@-]{1,15}(,[A-Za-z0-9_.:@-]{1,15})*)$",
                                  "type": "string"},
+            "validation": {"description": "Post-configuration fabric validation: once a node's agent is ready, run the\n"
+                                          "validation Job there (exact all-reduce, busbw and xGMI link floors, RCCL loading\n"
+                                          "the topology file) and report it in the FabricValidated condition.",
+                           "type": "object",
+                           "properties": {
+                               "enabled": {"type": "boolean"},
+                               "image": {"description": "Validation image (default amd/amd-network-validation).",
+                                         "type": "string"},
+                               "gpus": {"description": "GPUs to validate per node (default 8).", "minimum": 1,
+                                        "maximum": 8, "type": "integer"},
+                               "minBusbw": {"description": "Required 1 GiB all-reduce busbw in GB/s (0: correctness only).",
+                                            "minimum": 0, "type": "integer"},
+                               "minLink": {"description": "Required per-link xGMI pull bandwidth in GB/s (0: not checked).",
+                                           "minimum": 0, "type": "integer"},
+                           },
+                           "required": ["enabled"]},
             "lldpCache": {"description": "L3: remember each NIC's last confirmed Port Description on the node, so a\n"
                                          "restarted agent configures at once instead of waiting for the switch's next\n"
                                          "periodic LLDPDU (switches without fast start).  The switch must confirm it\n"

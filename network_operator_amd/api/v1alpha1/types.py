@@ -45,6 +45,37 @@ LOG_LEVEL_MIN, LOG_LEVEL_MAX = 0, 8
 DEFAULT_AGENT_IMAGE = "amd/amd-network-linkdiscovery:latest"
 
 
+DEFAULT_VALIDATION_IMAGE = "amd/amd-network-validation:0.1.0"
+
+
+@dataclass
+class ValidationSpec:
+    """Post-configuration fabric validation (MI355X addition): once a node's agent is ready, the
+    operator runs ``python -m network_operator_amd.validate`` there as a Job (all-reduce checked
+    exactly, busbw and xGMI link floors, NCCL_TOPO_FILE loaded by RCCL) and reports the result in
+    the policy's ``FabricValidated`` condition; a passing node gets the
+    ``gpu-fabric-validated`` label."""
+    enabled: bool = False
+    image: str = ""
+    gpus: int = 0           # 0 = 8 (the whole node)
+    minBusbw: int = 0       # GB/s, large-message all-reduce; 0 = correctness only
+    minLink: int = 0        # GB/s per xGMI link (pull); 0 = not checked
+
+    def to_dict(self) -> dict:
+        d: dict = {"enabled": self.enabled}
+        for k in ("image", "gpus", "minBusbw", "minLink"):
+            if getattr(self, k):
+                d[k] = getattr(self, k)
+        return d
+
+    @classmethod
+    def from_dict(cls, d: Optional[dict]) -> Optional["ValidationSpec"]:
+        if d is None:
+            return None
+        return cls(enabled=bool(d.get("enabled", False)), image=d.get("image", "") or "", gpus=int(d.get("gpus", 0) or 0),
+                   minBusbw=int(d.get("minBusbw", 0) or 0), minLink=int(d.get("minLink", 0) or 0))
+
+
 @dataclass
 class AmdScaleOutSpec:
     disableNetworkManager: bool = False
@@ -64,11 +95,16 @@ class AmdScaleOutSpec:
     railTableBase: int = 0
     rcclSocketIfname: str = ""
     lldpCache: bool = False
+    validation: Optional[ValidationSpec] = None
     extra: Dict[str, Any] = field(default_factory=dict)
+
+    def __post_init__(self):
+        if isinstance(self.validation, dict):  # new_policy(validation={...})
+            self.validation = ValidationSpec.from_dict(self.validation)
 
     _FIELDS = ("disableNetworkManager", "layer", "image", "pullPolicy", "mtu", "xgmiCheck", "lldpAnnounce",
                "interfaces", "nicDrivers", "disableFirmwareLldp", "metricsPort", "gpuDirectRdma", "rcclEnv",
-               "railTableBase", "rcclSocketIfname", "lldpCache")
+               "railTableBase", "rcclSocketIfname", "lldpCache", "validation")
 
     def to_dict(self) -> dict:
         d: dict = {}
@@ -102,6 +138,8 @@ class AmdScaleOutSpec:
             d["rcclSocketIfname"] = self.rcclSocketIfname
         if self.lldpCache:
             d["lldpCache"] = True
+        if self.validation is not None:
+            d["validation"] = self.validation.to_dict()
         d.update(copy.deepcopy(self.extra))
         return d
 
@@ -125,6 +163,7 @@ class AmdScaleOutSpec:
             railTableBase=int(d.pop("railTableBase", 0) or 0),
             rcclSocketIfname=d.pop("rcclSocketIfname", "") or "",
             lldpCache=bool(d.pop("lldpCache", False)),
+            validation=ValidationSpec.from_dict(d.pop("validation", None)),
         )
         s.extra = d
         return s

@@ -19,8 +19,8 @@ from . import kube
 from .informer import Informer, controller_of
 from .kube import ApiClient
 from .metrics import OperatorMetrics
-from .reconciler import (OWNER_KEY, EventRecorder, NetworkClusterPolicyReconciler, daemonset_owner_index,
-                         policy_owner_index)
+from .reconciler import (OWNER_KEY, VALIDATION_APP, EventRecorder, NetworkClusterPolicyReconciler,
+                         daemonset_owner_index, policy_owner_index)
 from .workqueue import RateLimitingQueue
 
 log = logging.getLogger("controller")
@@ -47,16 +47,21 @@ class PolicyController:
         # which nodes are not configured yet (status.errors).
         self.pods = Informer(client, kube.PODS, namespace=namespace, label_selector="app=amd-network-tools")
         self.pods.add_index(OWNER_KEY, daemonset_owner_index)
+        # Fabric validation Jobs (amdScaleOut.validation): their outcome is the FabricValidated condition.
+        self.jobs = Informer(client, kube.JOBS, namespace=namespace, label_selector=f"app={VALIDATION_APP}")
+        self.jobs.add_index(OWNER_KEY, policy_owner_index)
         self.queue = RateLimitingQueue(CONTROLLER_NAME)
         self.reconciler = NetworkClusterPolicyReconciler(
             client, namespace, is_openshift,
             get_policy=lambda name: self.policies.get(name),
             list_owned=lambda name: self.daemonsets.by_index(OWNER_KEY, name),
             recorder=EventRecorder(client, namespace) if record_events else None,
-            list_pods=lambda ds: self.pods.by_index(OWNER_KEY, ds))
+            list_pods=lambda ds: self.pods.by_index(OWNER_KEY, ds),
+            list_jobs=lambda name: self.jobs.by_index(OWNER_KEY, name))
         self.policies.add_handler(self._on_policy)
         self.daemonsets.add_handler(self._on_daemonset)
         self.pods.add_handler(self._on_pod)
+        self.jobs.add_handler(self._on_job)
         self._tasks: List[asyncio.Task] = []
         self.reconciles = 0
         self._pod_seen: Dict[str, float] = {}  # agent Pod uid -> monotonic time first seen, until Ready
@@ -77,6 +82,11 @@ class PolicyController:
             if owner and owner.get("kind") == T.KIND:
                 self._observe_readiness(owner["name"], ev, obj, old)
                 await self._enqueue(owner["name"])
+
+    async def _on_job(self, ev: str, obj: dict, old: Optional[dict]) -> None:
+        ref = controller_of(obj)
+        if ref and ref.get("kind") == T.KIND:
+            await self._enqueue(ref["name"])
 
     def _observe_readiness(self, policy: str, ev: str, obj: dict, old: Optional[dict]) -> None:
         uid = obj.get("metadata", {}).get("uid", "")
@@ -155,12 +165,14 @@ class PolicyController:
         self._tasks.append(self.policies.start())
         self._tasks.append(self.daemonsets.start())
         self._tasks.append(self.pods.start())
-        await asyncio.gather(self.policies.synced.wait(), self.daemonsets.synced.wait(), self.pods.synced.wait())
+        self._tasks.append(self.jobs.start())
+        await asyncio.gather(self.policies.synced.wait(), self.daemonsets.synced.wait(), self.pods.synced.wait(),
+                             self.jobs.synced.wait())
         for _ in range(self.workers):
             self._tasks.append(asyncio.ensure_future(self._worker()))
 
     def has_synced(self) -> bool:
-        return all(i.synced.is_set() for i in (self.policies, self.daemonsets, self.pods))
+        return all(i.synced.is_set() for i in (self.policies, self.daemonsets, self.pods, self.jobs))
 
     async def stop(self) -> None:
         await self.queue.shutdown()

@@ -75,10 +75,11 @@ ROLES = Resource("rbac.authorization.k8s.io", "v1", "roles", "Role", True)
 SERVICES = Resource("", "v1", "services", "Service", True)
 CONFIGMAPS = Resource("", "v1", "configmaps", "ConfigMap", True)
 DEPLOYMENTS = Resource("apps", "v1", "deployments", "Deployment", True)
+JOBS = Resource("batch", "v1", "jobs", "Job", True)
 
 ALL_RESOURCES = [NETWORKCLUSTERPOLICIES, DAEMONSETS, PODS, NODES, NAMESPACES, SERVICEACCOUNTS, EVENTS, ROLEBINDINGS,
                  LEASES, TOKENREVIEWS, SUBJECTACCESSREVIEWS, MUTATINGWEBHOOKS, VALIDATINGWEBHOOKS, CRDS,
-                 CLUSTERROLES, CLUSTERROLEBINDINGS, ROLES, SERVICES, CONFIGMAPS, DEPLOYMENTS]
+                 CLUSTERROLES, CLUSTERROLEBINDINGS, ROLES, SERVICES, CONFIGMAPS, DEPLOYMENTS, JOBS]
 
 
 # ---------------------------------------------------------------------------

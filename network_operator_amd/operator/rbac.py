@@ -31,6 +31,8 @@ OPERATOR_CLUSTER_RULES: Tuple[Tuple[str, Tuple[str, ...], Tuple[str, ...]], ...]
     # Agent ServiceAccount + OpenShift SCC RoleBinding (created on OpenShift only).
     ("", ("serviceaccounts",), ("get", "list", "create", "update", "delete")),
     ("rbac.authorization.k8s.io", ("rolebindings",), ("get", "list", "create", "update", "delete")),
+    # Fabric validation Jobs (amdScaleOut.validation), one per ready node, owned by the policy.
+    ("batch", ("jobs",), READ + ("create", "delete")),
     # Events on the policies (the reference grants read only and never emits any).
     ("", ("events",), ("create", "patch") + READ),
 )

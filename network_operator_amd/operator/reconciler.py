@@ -51,6 +51,8 @@ STATE_WORKING = "Working on it.."
 STATE_ALL_GOOD = "All good"
 COND_READY = "Ready"
 COND_DEGRADED = "Degraded"
+COND_VALIDATED = "FabricValidated"
+VALIDATION_APP = "amd-gpu-fabric-validation"  # Job label; the operator's Job informer selects on it
 
 # Volumes the reconciler manages (the template's nfd-features is never touched).
 MANAGED_VOLUMES = ("var-run-dbus", "networkmanager", "rccl-artifacts")
@@ -349,6 +351,73 @@ def policy_conditions(current: List[dict], targets: int, ready: int, errors: Lis
     return conds
 
 
+# ---------------------------------------------------------------------------------------------
+# Fabric validation Jobs (amdScaleOut.validation, MI355X addition)
+# ---------------------------------------------------------------------------------------------
+def validation_job_name(policy: str, node: str, generation: int) -> str:
+    """DNS-1123, <= 63 characters, unique per (policy, node, policy generation)."""
+    import hashlib
+
+    h = hashlib.sha256(f"{policy}/{node}".encode()).hexdigest()[:10]
+    return f"{policy[:36].rstrip('-')}-val-{h}-g{generation}"
+
+
+def validation_job(p: T.NetworkClusterPolicy, node: str, generation: int, namespace: str) -> dict:
+    """``python -m network_operator_amd.validate`` on one node, all its GPUs, the agent's artifacts
+    read-only, the label through NFD (config/validation/validation-job.yaml, pinned to a node)."""
+    v = p.spec.amdScaleOut.validation or T.ValidationSpec()
+    gpus = v.gpus or 8
+    args = [f"--gpus={gpus}", f"--min-busbw={v.minBusbw}", f"--min-link={v.minLink}",
+            f"--nfd-features-dir={discovery.LABEL_FEATURES_DIR}", f"--artifact-dir={ARTIFACT_DIR_HOST}"]
+    labels = {"app": VALIDATION_APP, "amd.com/policy": p.name[:63]}
+    return {
+        "apiVersion": "batch/v1", "kind": "Job",
+        "metadata": {"name": validation_job_name(p.name, node, generation), "namespace": namespace,
+                     "labels": dict(labels),
+                     "annotations": {"amd.com/node": node, "amd.com/policy-generation": str(generation)}},
+        "spec": {
+            "backoffLimit": 0,  # kept (no TTL) while the policy generation is current: its result is the status
+            "template": {
+                "metadata": {"labels": dict(labels)},
+                "spec": {
+                    "restartPolicy": "Never",
+                    "nodeName": node,
+                    "containers": [{
+                        "name": "validate",
+                        "image": v.image or T.DEFAULT_VALIDATION_IMAGE,
+                        "imagePullPolicy": p.spec.amdScaleOut.pullPolicy or "IfNotPresent",
+                        "command": ["python3", "-m", "network_operator_amd.validate"],
+                        "args": args,
+                        "resources": {"limits": {"amd.com/gpu": gpus}},
+                        "volumeMounts": [
+                            {"name": "nfd-features", "mountPath": discovery.LABEL_FEATURES_DIR},
+                            {"name": "rccl-artifacts", "mountPath": ARTIFACT_DIR_HOST, "readOnly": True},
+                        ],
+                    }],
+                    "volumes": [
+                        {"name": "nfd-features",
+                         "hostPath": {"path": discovery.LABEL_FEATURES_DIR, "type": "DirectoryOrCreate"}},
+                        {"name": "rccl-artifacts", "hostPath": {"path": ARTIFACT_DIR_HOST, "type": "DirectoryOrCreate"}},
+                    ],
+                },
+            },
+        },
+    }
+
+
+def job_outcome(job: dict) -> str:
+    """"succeeded", "failed" or "running"."""
+    st = job.get("status") or {}
+    if int(st.get("succeeded", 0) or 0) > 0:
+        return "succeeded"
+    if int(st.get("failed", 0) or 0) > 0:
+        return "failed"
+    for c in st.get("conditions") or []:
+        if c.get("status") == "True" and c.get("type") in ("Complete", "Failed"):
+            return "succeeded" if c["type"] == "Complete" else "failed"
+    return "running"
+
+
 class EventRecorder:
     """Best-effort core/v1 Events on the policy (failures are only logged)."""
 
@@ -377,7 +446,8 @@ class NetworkClusterPolicyReconciler:
     def __init__(self, client: ApiClient, namespace: str, is_openshift: bool,
                  get_policy: Callable[[str], Optional[dict]], list_owned: Callable[[str], List[dict]],
                  recorder: Optional[EventRecorder] = None,
-                 list_pods: Optional[Callable[[str], List[dict]]] = None):
+                 list_pods: Optional[Callable[[str], List[dict]]] = None,
+                 list_jobs: Optional[Callable[[str], List[dict]]] = None):
         self.client = client
         self.namespace = namespace
         self.is_openshift = is_openshift
@@ -387,6 +457,7 @@ class NetworkClusterPolicyReconciler:
         self._get_policy = get_policy
         self._list_owned = list_owned
         self._list_pods = list_pods
+        self._list_jobs = list_jobs  # validation Jobs of a policy (by its name)
         self.recorder = recorder
 
     def _node_errors(self, ds_name: str, limit: int = 16) -> List[str]:
@@ -405,6 +476,51 @@ class NetworkClusterPolicyReconciler:
         if len(errs) > limit:
             errs = errs[:limit] + [f"... and {len(errs) - limit} more"]
         return errs
+
+    async def _reconcile_validation(self, raw: dict, p: T.NetworkClusterPolicy, ds: dict, generation: int,
+                                    errors: List[str]) -> Optional[tuple]:
+        """One validation Job per node whose agent is ready, for the policy's current generation;
+        Jobs of older generations are removed.  Returns the FabricValidated (status, reason,
+        message) or None when validation is off; failed nodes are added to `errors`."""
+        v = p.spec.amdScaleOut.validation
+        if self._list_jobs is None or self._list_pods is None:
+            return None
+        enabled = p.spec.configurationType == T.CONFIG_AMD_SCALE_OUT and v is not None and v.enabled
+        jobs = {}
+        for j in self._list_jobs(p.name):
+            ann = j["metadata"].get("annotations") or {}
+            if not enabled or ann.get("amd.com/policy-generation") != str(generation):
+                try:  # a result for a spec that no longer exists
+                    await self.client.delete(kube.JOBS, j["metadata"]["name"], self.namespace)
+                except ApiError as e:
+                    if not is_not_found(e):
+                        raise
+                continue
+            jobs[ann.get("amd.com/node", "")] = j
+        if not enabled:
+            return None
+        ready_nodes = sorted(pod.get("spec", {}).get("nodeName", "") for pod in self._list_pods(ds["metadata"]["name"])
+                             if any(c.get("type") == "Ready" and c.get("status") == "True"
+                                    for c in (pod.get("status") or {}).get("conditions") or []))
+        for node in ready_nodes:
+            if node and node not in jobs:
+                job = validation_job(p, node, generation, self.namespace)
+                set_controller_reference(raw, job)
+                try:
+                    await self.client.create(kube.JOBS, job, namespace=self.namespace)
+                    log.info("Created fabric validation Job %s for node %s", job["metadata"]["name"], node)
+                except ApiError as e:
+                    if not is_already_exists(e):
+                        raise
+        outcome = {n: job_outcome(j) for n, j in jobs.items()}
+        failed = sorted(n for n, o in outcome.items() if o == "failed")
+        passed = sum(1 for o in outcome.values() if o == "succeeded")
+        errors += [f"{n}: fabric validation failed" for n in failed]
+        if failed:
+            return ("False", "ValidationFailed", f"{len(failed)} node(s) failed: {', '.join(failed)[:900]}")
+        if ready_nodes and passed >= len(ready_nodes):
+            return ("True", "AllNodesValidated", f"{passed}/{len(ready_nodes)} nodes validated")
+        return ("Unknown", "ValidationRunning", f"{passed}/{len(ready_nodes)} ready nodes validated")
 
     async def _event(self, obj: dict, type_: str, reason: str, msg: str) -> None:
         if self.recorder:
@@ -481,7 +597,13 @@ class NetworkClusterPolicyReconciler:
         if cur.state != new_state or cur.errors != errors:
             updated = True
         generation = int(raw.get("metadata", {}).get("generation", 0) or 0)
+        validated = await self._reconcile_validation(raw, p, ds, generation, errors)
         conditions = policy_conditions(cur.conditions, targets, ready, errors, generation)
+        if validated is not None:
+            now = _now_rfc3339()
+            old_v = [dict(c) for c in cur.conditions if c.get("type") == COND_VALIDATED]
+            _set_condition(old_v, COND_VALIDATED, *validated, generation, now)
+            conditions = conditions + old_v
         if conditions != cur.conditions or cur.observedGeneration != generation:
             updated = True
         if not updated:

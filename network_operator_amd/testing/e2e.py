@@ -47,6 +47,18 @@ HOST_NIC_READY_LABEL = "amd.feature.node.kubernetes.io/host-nic-ready"
 HOST_NICS = ("ens9np0", "ens49np1")
 KMD_IMAGE = "example.com/amd/ionic-kmd:1.0"
 KMD_DRIVER = "ionic"
+VALIDATED_LABEL = "amd.feature.node.kubernetes.io/gpu-fabric-validated"
+# Stand-in for the validation image on a CPU-only harness: what validate.py does with its verdict
+# (the label file through NFD on success, exit status = result).  validate.py itself runs on the
+# MI355X box (tests/test_gpu_ops.py); here the Job plumbing around it is under test.
+_VALIDATE_STUB = (
+    "import sys, pathlib\n"
+    "ok = sys.argv[1] == 'pass'\n"
+    "d = [a.split('=', 1)[1] for a in sys.argv[2:] if a.startswith('--nfd-features-dir=')][0]\n"
+    "if ok:\n"
+    "    pathlib.Path(d, 'gpu-fabric-validation.txt').write_text("
+    "'amd.feature.node.kubernetes.io/gpu-fabric-validated=true\\n')\n"
+    "sys.exit(0 if ok else 1)\n")
 
 
 async def _until(fn, timeout: float, poll: float = 0.001) -> Optional[float]:
@@ -85,7 +97,7 @@ async def _scrape(port: int, names) -> dict:
 
 async def _scenario(tmp: Path, n_nics: int, mode: str, seed: int, interval: str, fast_start: bool,
                     teardown: bool, node_name: str, policy_kw: dict, update_mtu: int, config_type: str,
-                    flap: bool) -> dict:
+                    flap: bool, validation: str) -> dict:
     from ..api.v1alpha1 import types as T
     from ..operator import kube, manager
     from ..operator.kube import ApiClient, KubeConfig
@@ -125,9 +137,14 @@ async def _scenario(tmp: Path, n_nics: int, mode: str, seed: int, interval: str,
                                             "--dependency-check-interval=0"],
                                            stop=stop, started=started))
     kmd = [sys.executable, "-m", "network_operator_amd.testing.fakesysfs", "bind", KMD_DRIVER, *nic_names]
+    from ..api.v1alpha1 import types as T0
+
     node = SimNode(fake, node_name, {"amd.feature.node.kubernetes.io/gpu-ready": "true"}, tmp / "host",
                    sysfs_root=tmp / "sys", init_images={KMD_IMAGE: kmd},
-                   env={"PYTHONPATH": str(Path(__file__).resolve().parents[2])})
+                   env={"PYTHONPATH": str(Path(__file__).resolve().parents[2])},
+                   job_images={T0.DEFAULT_VALIDATION_IMAGE: [sys.executable, "-c", _VALIDATE_STUB, validation or "pass"]})
+    if validation and not host_nic:
+        policy_kw = dict(policy_kw, validation={"enabled": True, "minBusbw": 300})
     P, DS = kube.NETWORKCLUSTERPOLICIES, kube.DAEMONSETS
     ns = "amd-network-operator"
     name = "scale-out"
@@ -155,6 +172,19 @@ async def _scenario(tmp: Path, n_nics: int, mode: str, seed: int, interval: str,
             res.update(policy_to_daemonset_s=rel(t_ds), policy_to_agent_start_s=rel(t_agent),
                        policy_to_node_label_s=rel(t_label), policy_to_all_good_s=rel(t_good))
             res["policy_status"] = (fake.get_object(P, name) or {}).get("status")
+            if validation:
+                def validated():
+                    st = (fake.get_object(P, name) or {}).get("status") or {}
+                    c = {x["type"]: x for x in st.get("conditions", [])}.get("FabricValidated") or {}
+                    return c.get("status") in ("True", "False") and c
+                t_val = await _until(validated, 30)
+                res["policy_to_validated_s"] = rel(t_val)
+                res["validation_condition"] = validated() or None
+                res["validation_jobs"] = [{"node": (j["metadata"].get("annotations") or {}).get("amd.com/node"),
+                                           "status": j.get("status")} for j in fake.list_objects(kube.JOBS)]
+                res["job_runs"] = node.job_runs
+                await _until(lambda: validation != "pass" or VALIDATED_LABEL in node.node_labels(), 5)
+                res["node_labels"] = node.node_labels()
             res["operator_metrics"] = await _scrape(metrics_port, ("amd_network_operator_agent_ready_seconds_count",
                                                                    "amd_network_operator_agent_ready_seconds_sum",
                                                                    "amd_network_operator_policy_ready"))
@@ -368,12 +398,13 @@ def run_fabric(n_nodes: int = 2, n_nics: int = 2, seed: int = 1, collective: boo
 
 def run_scenario(n_nics: int = 2, mode: str = "L3", seed: int = 1, interval: str = "30s", fast_start: bool = True,
                  teardown: bool = True, node_name: str = "mi355x-0", policy_kw: Optional[dict] = None,
-                 update_mtu: int = 0, config_type: str = "amd-so", flap: bool = False, keep_tmp: bool = False) -> dict:
+                 update_mtu: int = 0, config_type: str = "amd-so", flap: bool = False, validation: str = "",
+                 keep_tmp: bool = False) -> dict:
     """Must already run inside a private user+net namespace (``run_isolated``)."""
     tmp = Path(tempfile.mkdtemp(prefix="netop-e2e-"))
     try:
         return asyncio.run(_scenario(tmp, n_nics, mode, seed, interval, fast_start, teardown, node_name,
-                                     dict(policy_kw or {}), update_mtu, config_type, flap))
+                                     dict(policy_kw or {}), update_mtu, config_type, flap, validation))
     finally:
         if not keep_tmp:
             shutil.rmtree(tmp, ignore_errors=True)

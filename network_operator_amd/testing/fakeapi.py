@@ -259,6 +259,15 @@ class FakeApiServer:
                 self.node_ready[(f"{ns}/{name}", node)] = ready
         self._sync_daemonsets()
 
+    def set_job_result(self, name: str, namespace: str, succeeded: bool) -> None:
+        """What the Job controller records when the Job's only Pod ends (backoffLimit 0)."""
+        o = self._table(kube.JOBS)[(namespace, name)]
+        new = copy.deepcopy(o)
+        cond = "Complete" if succeeded else "Failed"
+        new["status"] = {"succeeded" if succeeded else "failed": 1,
+                         "conditions": [{"type": cond, "status": "True", "lastTransitionTime": _now()}]}
+        self._store(kube.JOBS, new, "MODIFIED")
+
     def fail_next(self, method: str, path_regex: str, status: int = 500, count: int = 1,
                   reason: str = "InternalError") -> None:
         self.faults.append(_Fault(method.upper(), re.compile(path_regex), status, count, reason))

@@ -15,7 +15,9 @@ condition from ``set_agent_ready``).  ``SimNode`` plays what runs *on* the node:
   and its ``name=value`` lines become Node labels, added and removed as the files change (NFD's
   local feature source).
 
-Init containers (the host-nic driver container) run to completion, in order, before the agent
+Jobs pinned to the node (the fabric validation Jobs) run once, their image mapped to a local
+command by ``job_images``, and their exit status becomes the Job's status.  Init containers
+(the host-nic driver container) run to completion, in order, before the agent
 starts; their images are mapped to local commands by ``init_images`` (an unmapped image fails
 like an image that cannot be pulled).  Not simulated: image pulls, and the probes'
 ``initialDelaySeconds`` / ``periodSeconds`` (``probe_period`` replaces both, so the control plane
@@ -71,7 +73,8 @@ class _Container:
 class SimNode:
     def __init__(self, fake, name: str, labels: Dict[str, str], host_root: Path, sysfs_root: Optional[Path] = None,
                  probe_period: float = 0.02, nfd_period: float = 0.01, env: Optional[Dict[str, str]] = None,
-                 init_images: Optional[Dict[str, List[str]]] = None, netns=None):
+                 init_images: Optional[Dict[str, List[str]]] = None, netns=None,
+                 job_images: Optional[Dict[str, List[str]]] = None):
         self.fake, self.name = fake, name
         self.base_labels = dict(labels)
         self.host_root = Path(host_root)
@@ -83,6 +86,11 @@ class SimNode:
         # testing.netns.NetnsHolder of another simulated node.
         self.netns = netns
         self.init_runs: List[dict] = []   # {"pod", "name", "rc", "t_start", "t_end"}
+        # Jobs pinned to this node (spec.template.spec.nodeName): image -> command, run once each,
+        # their exit status recorded on the Job (the fabric validation Jobs).
+        self.job_images = dict(job_images or {})
+        self.job_runs: List[dict] = []    # {"job", "rc", "t_start", "t_end"}
+        self._jobs_started: set = set()
         self.containers: Dict[Tuple[str, str], _Container] = {}
         self.features: Dict[str, str] = {}
         self.exited: List[dict] = []      # {"pod", "rc", "log"} of every agent process that ended
@@ -258,6 +266,43 @@ class SimNode:
                         self._start(c)
             await asyncio.sleep(0.005)
 
+    async def _run_job(self, job: dict) -> None:
+        ns, name = job["metadata"].get("namespace", ""), job["metadata"]["name"]
+        spec = job["spec"]["template"]["spec"]
+        c = spec["containers"][0]
+        mounts = self._mounts(spec, c)
+        for _, hp in mounts:
+            self.host_path(hp).mkdir(parents=True, exist_ok=True)
+        cmd = self.job_images.get(c.get("image", ""))
+        t = time.monotonic()
+        rc = -1  # ErrImagePull: no command for this image
+        if cmd is not None:
+            argv = list(cmd) + [self._rewrite_arg(a, mounts) for a in c.get("args") or []]
+            env = dict(os.environ, **self.extra_env, NODE_NAME=self.name)
+            if self.sysfs_root is not None:
+                env["SYSFS_ROOT"] = str(self.sysfs_root)
+            logs = self.host_root.parent / "pod-logs"
+            logs.mkdir(parents=True, exist_ok=True)
+            with open(logs / f"{name}.log", "ab") as f:
+                p = await asyncio.create_subprocess_exec(*argv, env=env, stdout=f, stderr=f,
+                                                         preexec_fn=self.netns.enter if self.netns else None)
+                rc = await p.wait()
+        self.job_runs.append({"job": name, "rc": rc, "t_start": t, "t_end": time.monotonic()})
+        if self.fake.get_object(kube.JOBS, name, ns) is not None:
+            self.fake.set_job_result(name, ns, rc == 0)
+
+    async def _jobs(self) -> None:
+        while not self._stop.is_set():
+            for job in self.fake.list_objects(kube.JOBS):
+                spec = job["spec"]["template"]["spec"]
+                uid = job["metadata"].get("uid")
+                if spec.get("nodeName") != self.name or uid in self._jobs_started or job.get("status", {}).get(
+                        "conditions"):
+                    continue
+                self._jobs_started.add(uid)
+                self._tasks.append(asyncio.ensure_future(self._run_job(job)))
+            await asyncio.sleep(0.01)
+
     async def _prober(self) -> None:
         while not self._stop.is_set():
             for c in list(self.containers.values()):
@@ -309,7 +354,7 @@ class SimNode:
     async def start(self) -> None:
         if self.fake.get_object(kube.NODES, self.name) is None:
             self.fake.add_node(self.name, copy.deepcopy(self.base_labels))
-        self._tasks = [asyncio.ensure_future(t()) for t in (self._kubelet, self._prober, self._nfd)]
+        self._tasks = [asyncio.ensure_future(t()) for t in (self._kubelet, self._prober, self._nfd, self._jobs)]
 
     async def stop(self) -> None:
         """Node shutdown: every agent gets SIGTERM (and its grace period)."""

@@ -113,3 +113,21 @@ def test_link_failure_is_reported_by_the_policy_and_recovers():
     assert st["errors"] == ["mi355x-0: scale-out not ready (ContainersNotReady)"]
     assert any(c["type"] == "Degraded" and c["status"] == "True" for c in st["conditions"])
     assert r["port_up_to_all_good_s"] is not None, r["agent_log"]
+
+
+@pytest.mark.parametrize("outcome", ["pass", "fail"])
+def test_fabric_validation_job_runs_on_the_ready_node(outcome):
+    """amdScaleOut.validation end to end: the node becomes ready, the operator starts a validation
+    Job pinned to it, the simulated kubelet runs it, and its result becomes the policy's
+    FabricValidated condition (and, on success, the gpu-fabric-validated Node label)."""
+    r = e2e.run_isolated(n_nics=2, mode="L3", seed=11, validation=outcome)
+    assert r["policy_to_validated_s"] is not None, (r.get("policy_status"), r["agent_log"])
+    c = r["validation_condition"]
+    jobs = r["validation_jobs"]
+    assert [j["node"] for j in jobs] == ["mi355x-0"] and [x["rc"] for x in r["job_runs"]] == [0 if outcome == "pass" else 1]
+    if outcome == "pass":
+        assert (c["status"], c["reason"]) == ("True", "AllNodesValidated")
+        assert r["node_labels"].get(e2e.VALIDATED_LABEL) == "true"
+    else:
+        assert (c["status"], c["reason"]) == ("False", "ValidationFailed")
+        assert e2e.VALIDATED_LABEL not in r["node_labels"]

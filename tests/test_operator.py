@@ -507,3 +507,66 @@ def test_agent_args_rail_tables_l3_only():
     assert T.NetworkClusterPolicy.from_dict(p.to_dict()).spec.amdScaleOut.railTableBase == 100
     p.spec.amdScaleOut.layer = "L2"  # no addresses in L2: nothing to route
     assert not any(a.startswith("--rail-table-base") for a in agent_args(p))
+
+
+def test_fabric_validation_jobs_follow_ready_nodes_and_report_a_condition():
+    """amdScaleOut.validation: one validation Job per node whose agent is ready, pinned to it, for
+    the policy's current generation; the outcome is the FabricValidated condition."""
+    async def body():
+        async with cluster(openshift=False) as (fake, client, ctl):
+            for i in range(2):
+                fake.add_node(f"gpu-node-{i}", {"foo": "bar"})
+            await client.create(kube.NETWORKCLUSTERPOLICIES,
+                                policy(validation={"enabled": True, "minBusbw": 300, "gpus": 8}))
+            await eventually(lambda: fake.get_object(kube.DAEMONSETS, "policy", NS) is not None)
+            fake.set_agent_ready("gpu-node-0")
+
+            def jobs():
+                return {j["metadata"]["annotations"]["amd.com/node"]: j for j in fake.list_objects(kube.JOBS)}
+
+            await eventually(lambda: set(jobs()) == {"gpu-node-0"})  # only ready nodes are validated
+            j = jobs()["gpu-node-0"]
+            spec = j["spec"]["template"]["spec"]
+            assert spec["nodeName"] == "gpu-node-0" and spec["restartPolicy"] == "Never"
+            c = spec["containers"][0]
+            assert c["command"] == ["python3", "-m", "network_operator_amd.validate"]
+            assert "--min-busbw=300" in c["args"] and "--gpus=8" in c["args"]
+            assert c["resources"]["limits"] == {"amd.com/gpu": 8}
+            assert j["metadata"]["ownerReferences"][0]["kind"] == "NetworkClusterPolicy"
+
+            def cond():
+                st = fake.get_object(kube.NETWORKCLUSTERPOLICIES, "policy").get("status") or {}
+                return {c["type"]: c for c in st.get("conditions", [])}.get("FabricValidated")
+
+            await eventually(lambda: cond() and cond()["status"] == "Unknown")
+            fake.set_agent_ready("gpu-node-1")
+            await eventually(lambda: set(jobs()) == {"gpu-node-0", "gpu-node-1"})
+            fake.set_job_result(jobs()["gpu-node-0"]["metadata"]["name"], NS, True)
+            fake.set_job_result(jobs()["gpu-node-1"]["metadata"]["name"], NS, False)
+
+            def failed():
+                st = fake.get_object(kube.NETWORKCLUSTERPOLICIES, "policy")["status"]
+                c = cond()
+                return c["status"] == "False" and c["reason"] == "ValidationFailed" and \
+                    "gpu-node-1: fabric validation failed" in st["errors"]
+            await eventually(failed)
+
+            # A new spec (generation 2): the old results go, both nodes are validated again.
+            old_names = {j["metadata"]["name"] for j in jobs().values()}
+            cur = await client.get(kube.NETWORKCLUSTERPOLICIES, "policy")
+            cur["spec"]["amdScaleOut"]["mtu"] = 4200
+            await client.replace(kube.NETWORKCLUSTERPOLICIES, cur)
+            await eventually(lambda: set(jobs()) == {"gpu-node-0", "gpu-node-1"}
+                             and not old_names & {j["metadata"]["name"] for j in jobs().values()})
+            for j in jobs().values():
+                fake.set_job_result(j["metadata"]["name"], NS, True)
+            await eventually(lambda: cond()["status"] == "True" and cond()["reason"] == "AllNodesValidated")
+            st = fake.get_object(kube.NETWORKCLUSTERPOLICIES, "policy")["status"]
+            assert st["state"] == "All good" and st["errors"] == []
+
+            # Validation off: no Jobs, no condition.
+            cur = await client.get(kube.NETWORKCLUSTERPOLICIES, "policy")
+            cur["spec"]["amdScaleOut"]["validation"] = {"enabled": False}
+            await client.replace(kube.NETWORKCLUSTERPOLICIES, cur)
+            await eventually(lambda: cond() is None and not fake.list_objects(kube.JOBS))
+    run(body())
