@@ -512,7 +512,9 @@ class NetworkClusterPolicyReconciler:
                 except ApiError as e:
                     if not is_already_exists(e):
                         raise
-        outcome = {n: job_outcome(j) for n, j in jobs.items()}
+        # Judged over the nodes ready now: a node that left keeps its Job (and result) until the
+        # next generation, but no longer counts either way.
+        outcome = {n: job_outcome(jobs[n]) for n in ready_nodes if n in jobs}
         failed = sorted(n for n, o in outcome.items() if o == "failed")
         passed = sum(1 for o in outcome.values() if o == "succeeded")
         errors += [f"{n}: fabric validation failed" for n in failed]
