@@ -97,7 +97,7 @@ async def _scrape(port: int, names) -> dict:
 
 async def _scenario(tmp: Path, n_nics: int, mode: str, seed: int, interval: str, fast_start: bool,
                     teardown: bool, node_name: str, policy_kw: dict, update_mtu: int, config_type: str,
-                    flap: bool, validation: str) -> dict:
+                    flap: bool, validation: str, crash_agent: bool) -> dict:
     from ..api.v1alpha1 import types as T
     from ..operator import kube, manager
     from ..operator.kube import ApiClient, KubeConfig
@@ -200,6 +200,20 @@ async def _scenario(tmp: Path, n_nics: int, mode: str, seed: int, interval: str,
                 link = rt.link_by_name(nif)
                 state[nif] = {"up": link["up"], "mtu": link["mtu"], "addrs": rt.addr_list(link["index"])}
             res["state"] = state
+            if crash_agent:
+                # The agent dies without cleaning up (OOM kill): the kubelet restarts the container,
+                # the new agent removes the stale label, configures again and is ready again.
+                c0 = next(iter(node.containers.values()))
+                t1 = time.monotonic()
+                c0.proc.kill()
+                t_unready = await _until(lambda: not all_good(), 10)
+                t_back = await _until(lambda: len(c0.started_at) == 2 and c0.ready and all_good()
+                                      and node.node_labels().get(label_key) == "true", 30)
+                res["crash_to_unready_s"] = round(t_unready - t1, 6) if t_unready else None
+                res["crash_to_all_good_s"] = round(t_back - t1, 6) if t_back else None
+                res["agent_restarts"] = c0.restarts
+                res["operator_metrics_after_crash"] = await _scrape(metrics_port, (
+                    "amd_network_operator_agent_unready_total", "amd_network_operator_agent_ready_seconds_count"))
             if flap:
                 # Carrier loss on one switch port: the agent withdraws the label, the probe fails,
                 # the operator reports the node; the port comes back and so does everything else.
@@ -399,12 +413,13 @@ def run_fabric(n_nodes: int = 2, n_nics: int = 2, seed: int = 1, collective: boo
 def run_scenario(n_nics: int = 2, mode: str = "L3", seed: int = 1, interval: str = "30s", fast_start: bool = True,
                  teardown: bool = True, node_name: str = "mi355x-0", policy_kw: Optional[dict] = None,
                  update_mtu: int = 0, config_type: str = "amd-so", flap: bool = False, validation: str = "",
-                 keep_tmp: bool = False) -> dict:
+                 crash_agent: bool = False, keep_tmp: bool = False) -> dict:
     """Must already run inside a private user+net namespace (``run_isolated``)."""
     tmp = Path(tempfile.mkdtemp(prefix="netop-e2e-"))
     try:
         return asyncio.run(_scenario(tmp, n_nics, mode, seed, interval, fast_start, teardown, node_name,
-                                     dict(policy_kw or {}), update_mtu, config_type, flap, validation))
+                                     dict(policy_kw or {}), update_mtu, config_type, flap, validation,
+                                     crash_agent))
     finally:
         if not keep_tmp:
             shutil.rmtree(tmp, ignore_errors=True)

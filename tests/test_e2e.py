@@ -131,3 +131,14 @@ def test_fabric_validation_job_runs_on_the_ready_node(outcome):
     else:
         assert (c["status"], c["reason"]) == ("False", "ValidationFailed")
         assert e2e.VALIDATED_LABEL not in r["node_labels"]
+
+
+def test_agent_killed_is_restarted_and_the_node_recovers():
+    """SIGKILL of the agent (OOM kill): the Pod goes unready, the kubelet restarts the container,
+    the new agent clears the stale label and configures again; the operator counts the outage."""
+    r = e2e.run_isolated(n_nics=4, mode="L3", seed=12, crash_agent=True)
+    assert r["crash_to_unready_s"] is not None and r["crash_to_all_good_s"] is not None, r["agent_log"]
+    assert r["agent_restarts"] == 1
+    m = r["operator_metrics_after_crash"]
+    assert m['amd_network_operator_agent_unready_total{policy="scale-out"}'] == 1
+    assert m['amd_network_operator_agent_ready_seconds_count{policy="scale-out"}'] == 2
