@@ -110,13 +110,17 @@ async def _scenario(tmp: Path, n_nics: int, mode: str, seed: int, interval: str,
     fakesysfs.build_mi355x_node(tmp / "sys", n_gpus=n_nics)
     nat = netns._native()
     host_nic = config_type == "host-nic"
+    both = config_type == "both"  # an amd-so policy and a host-nic policy on the same node
     label_key = HOST_NIC_READY_LABEL if host_nic else READY_LABEL
     if host_nic:
         nic_names = list(HOST_NICS)
-        for nif in nic_names:
-            fakesysfs.unbind_driver(tmp / "sys", nif)
     else:
         nic_names = [p["nic"] for p in nat.discover(str(tmp / "sys"))["pairs"]][:n_nics]
+    if both:
+        nic_names += list(HOST_NICS)
+    for nif in nic_names:
+        if nif in HOST_NICS:
+            fakesysfs.unbind_driver(tmp / "sys", nif)
     plan = netns.random_plan(len(nic_names), rng)
     for n in nat.discover(str(tmp / "sys"))["nics"]:  # RoCE v2 GIDs as the RDMA core adds them
         if n["ifname"] in nic_names and n["rdma_dev"]:
@@ -136,7 +140,8 @@ async def _scenario(tmp: Path, n_nics: int, mode: str, seed: int, interval: str,
                                             f"--metrics-bind-address=127.0.0.1:{metrics_port}",
                                             "--dependency-check-interval=0"],
                                            stop=stop, started=started))
-    kmd = [sys.executable, "-m", "network_operator_amd.testing.fakesysfs", "bind", KMD_DRIVER, *nic_names]
+    kmd = [sys.executable, "-m", "network_operator_amd.testing.fakesysfs", "bind", KMD_DRIVER,
+           *[n for n in nic_names if n in HOST_NICS]]
     from ..api.v1alpha1 import types as T0
 
     node = SimNode(fake, node_name, {"amd.feature.node.kubernetes.io/gpu-ready": "true"}, tmp / "host",
@@ -162,6 +167,17 @@ async def _scenario(tmp: Path, n_nics: int, mode: str, seed: int, interval: str,
             t_ds = await _until(lambda: fake.get_object(DS, name, ns) is not None, 10)
             t_agent = await _until(lambda: any(x.proc is not None for x in node.containers.values()), 10)
             t_label = await _until(lambda: node.node_labels().get(label_key) == "true", 30)
+
+            if both:
+                await c.create(P, T.new_host_nic_policy("host-nics", layer=mode, mtu=9000, nicDrivers=[KMD_DRIVER],
+                                                        driverImage=KMD_IMAGE).to_dict())
+
+                def host_good():
+                    st = (fake.get_object(P, "host-nics") or {}).get("status") or {}
+                    return st.get("state") == "All good" and node.node_labels().get(HOST_NIC_READY_LABEL) == "true"
+                t_host = await _until(host_good, 30)
+                res["host_nic_policy_all_good_s"] = round(t_host - t0, 6) if t_host else None
+                res["host_nic_status"] = (fake.get_object(P, "host-nics") or {}).get("status")
 
             def all_good():
                 st = (fake.get_object(P, name) or {}).get("status") or {}
@@ -250,7 +266,8 @@ async def _scenario(tmp: Path, n_nics: int, mode: str, seed: int, interval: str,
             if teardown:
                 t1 = time.monotonic()
                 await c.delete(P, name)
-                t_gone = await _until(lambda: not node.containers and fake.get_object(DS, name, ns) is None, 30)
+                t_gone = await _until(lambda: fake.get_object(DS, name, ns) is None and not any(
+                    x.daemonset == f"{ns}/{name}" for x in node.containers.values()), 30)
                 t_unlabel = await _until(lambda: label_key not in node.node_labels(), 10)
                 res["delete_to_agent_stopped_s"] = round(t_gone - t1, 6) if t_gone else None
                 res["delete_to_label_removed_s"] = round(t_unlabel - t1, 6) if t_unlabel else None

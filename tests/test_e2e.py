@@ -142,3 +142,19 @@ def test_agent_killed_is_restarted_and_the_node_recovers():
     m = r["operator_metrics_after_crash"]
     assert m['amd_network_operator_agent_unready_total{policy="scale-out"}'] == 1
     assert m['amd_network_operator_agent_ready_seconds_count{policy="scale-out"}'] == 2
+
+
+def test_scale_out_and_host_nic_policies_share_a_node():
+    """Both configuration types on one node: two DaemonSets, two agents with their own NIC sets,
+    labels and label files, each policy "All good"; deleting the amd-so policy leaves the host
+    NICs configured."""
+    r = e2e.run_isolated(n_nics=2, mode="L3", seed=13, config_type="both")
+    assert r["policy_to_all_good_s"] is not None and r["host_nic_policy_all_good_s"] is not None, r["agent_log"]
+    labels = r["node_labels"]
+    assert labels["amd.feature.node.kubernetes.io/gpu-scale-out"] == "true"
+    assert labels["amd.feature.node.kubernetes.io/host-nic-ready"] == "true"
+    assert labels["amd.feature.node.kubernetes.io/gpu-scale-out.nics"] == "2"
+    _check_nics(r, "L3")  # all four NICs: the two rails and the two host NICs
+    scale_out = r["nics"][:2]
+    assert all(r["after_delete"][n] == [] for n in scale_out)
+    assert all(r["after_delete"][n] != [] for n in e2e.HOST_NICS)
