@@ -154,6 +154,11 @@ class AgentError : public std::runtime_error {
 
 class Agent {
    public:
+    struct TopoResult {  // what the topology worker hands back
+        std::string xml, fp;            // the file and its inputs (the ".key" sidecar)
+        std::vector<std::string> names;  // the interfaces it was generated for
+        bool reused = false;             // the file on disk is current: nothing to write
+    };
     Agent(Config cfg, nl::NetOps& ops, std::unique_ptr<LldpSource> lldp, NmFactory nm_factory);
 
     // Runs the whole state machine.  `stop_fd` becomes readable on SIGTERM/SIGINT (a
@@ -245,6 +250,7 @@ class Agent {
     NmFactory nm_factory_;
     std::vector<NicState> nics_;
     topo::DiscoveryResult disc_;
+    double cpu_ms_at_ready_ = -1;  // user + system CPU of the process when the label went up
     std::vector<std::string> dry_run_missing_;  // discovered, but not in this network namespace
     struct TopoWorker {  // the topology thread's Linux tid, for its priority
         std::mutex mu;
@@ -252,11 +258,8 @@ class Agent {
         bool running = false;
     };
     std::shared_ptr<TopoWorker> topo_worker_;
-    std::string topo_fp_;        // inputs of the topology file (its ".key" sidecar)
-    bool topo_reused_ = false;   // the file on disk is current: nothing to write
-    std::string topo_fingerprint(const std::vector<std::string>& names) const;
-    std::future<std::string> topo_future_;
-    std::optional<std::string> topo_xml_;
+    std::future<TopoResult> topo_future_;
+    std::optional<TopoResult> topo_;
     topo::XgmiReport xgmi_;
     topo::GdrReport gdr_;
     void check_gdr();

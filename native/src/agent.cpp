@@ -4,6 +4,7 @@
 #include <linux/if.h>
 #include <poll.h>
 #include <sys/epoll.h>
+#include <sys/resource.h>
 #include <sys/socket.h>
 #include <unistd.h>
 
@@ -799,52 +800,76 @@ void Agent::dry_run_report() {
            cfg_.mode.c_str());
 }
 
-std::string Agent::topo_fingerprint(const std::vector<std::string>& names) const {
-    // Everything the file is generated from that can change without a reboot: the generator,
-    // the GPUs and the NICs (name, PCI function, RDMA device).  The PCIe tree above them is
-    // fixed until the next boot, hence the boot id.
-    std::string root = cfg_.sysfs_root.empty() ? topo::sysfs_root() : cfg_.sysfs_root;
+namespace {
+// Everything the file is generated from that can change without a reboot: the generator, the
+// GPUs and the NICs (name, PCI function, RDMA device).  The PCIe tree above them is fixed until
+// the next boot, hence the boot id.
+std::string topo_fingerprint(const topo::DiscoveryResult& disc, const std::vector<std::string>& names,
+                             const std::string& root) {
     std::string fp = strfmt("netop-rccl-topo v%d\n", artifacts::kRcclTopoXmlVersion);
     auto boot = read_file("/proc/sys/kernel/random/boot_id");
     fp += "boot " + (boot ? trim(*boot) : std::string("?")) + "\nroot " + root + "\n";
-    for (const auto& g : disc_.gpus) fp += "gpu " + g.pci.path + "\n";
+    for (const auto& g : disc.gpus) fp += "gpu " + g.pci.path + "\n";
     for (const auto& n : names) {
         std::string where = "-";
-        for (const auto& d : disc_.nics)
+        for (const auto& d : disc.nics)
             if (d.ifname == n) where = d.pci.path + " " + d.rdma_dev + ":" + std::to_string(d.rdma_port);
         fp += "nic " + n + " " + where + "\n";
     }
     return fp;
 }
 
-void Agent::start_topo() {
-    if (cfg_.rccl_topo.empty() || topo_future_.valid() || topo_xml_) return;
-    std::string root = cfg_.sysfs_root.empty() ? topo::sysfs_root() : cfg_.sysfs_root;
-    std::vector<std::string> names;
-    for (const auto& n : nics_) names.push_back(n.ifname);
-    if (cfg_.dry_run)  // also the discovered NICs that are not in this network namespace
-        for (const auto& i : disc_.ifnames)
-            if (std::find(names.begin(), names.end(), i) == names.end()) names.push_back(i);
-    // A restart within the same boot (DaemonSet rollout, crash) finds the file it wrote last time:
-    // reuse it when it was generated from the same inputs.
-    topo_fp_ = topo_fingerprint(names);
-    auto key = read_file(cfg_.rccl_topo + ".key");
-    if (key && *key == topo_fp_) {
-        if (auto xml = read_file(cfg_.rccl_topo); xml && !xml->empty()) {
-            topo_xml_ = *xml;
-            topo_reused_ = true;
-            NLOG_V(2, "RCCL topology file %s is current (same boot and devices): reused", cfg_.rccl_topo.c_str());
-            return;
+// The interface names the agent works on: discovery's, then --interfaces (collect_interfaces).
+std::vector<std::string> topo_names(const topo::DiscoveryResult& disc, const std::string& interfaces) {
+    std::vector<std::string> names = disc.ifnames;
+    for (auto& i : split(interfaces, ',')) {
+        auto t = trim(i);
+        if (!t.empty() && std::find(names.begin(), names.end(), t) == names.end()) names.push_back(t);
+    }
+    return names;
+}
+
+// The whole job of the topology worker: the file a previous run of this boot left (same inputs),
+// or a fresh sysfs walk above the discovered GPUs and NICs.
+Agent::TopoResult make_topology(const topo::DiscoveryResult& disc, const std::string& interfaces,
+                                const std::string& root, const std::string& path) {
+    Agent::TopoResult r;
+    r.names = topo_names(disc, interfaces);
+    r.fp = topo_fingerprint(disc, r.names, root);
+    auto key = read_file(path + ".key");
+    if (key && *key == r.fp) {
+        if (auto xml = read_file(path); xml && !xml->empty()) {
+            r.xml = *xml;
+            r.reused = true;
+            return r;
         }
     }
+    r.xml = artifacts::generate_rccl_topo(disc.gpus, artifacts::topo_nics(disc, r.names, root), topo::cpu_identity(),
+                                          root);
+    return r;
+}
+}  // namespace
+
+void Agent::start_topo() {
+    if (cfg_.rccl_topo.empty() || topo_future_.valid() || topo_) return;
+    std::string root = cfg_.sysfs_root.empty() ? topo::sysfs_root() : cfg_.sysfs_root;
     // Inputs are copied: the worker shares nothing with the agent thread.
     auto worker = std::make_shared<TopoWorker>();
     topo_worker_ = worker;
-    auto work = [disc = disc_, names = std::move(names), root = std::move(root), worker] {
+    const int main_cpu = ::sched_getcpu();
+    auto work = [disc = disc_, interfaces = cfg_.interfaces, root = std::move(root), path = cfg_.rccl_topo,
+                 worker, main_cpu] {
+        // Off the agent thread's CPU: at idle priority on the same CPU it would only run when the
+        // agent thread blocks (measured: the join then waited ~4 ms in L3).
+        cpu_set_t set;
+        if (main_cpu >= 0 && ::sched_getaffinity(0, sizeof set, &set) == 0 && CPU_COUNT(&set) > 1) {
+            CPU_CLR(main_cpu, &set);
+            (void)::sched_setaffinity(0, sizeof set, &set);
+        }
         // Background priority (SCHED_IDLE): on a busy or CPU-limited node the critical path
-        // (link-up, LLDP) runs first and this fills its gaps instead of competing with it.
-        // Measured in the netns harness, 8 NICs, L3: total_ready +5.6 ms over no topology file at
-        // normal priority, +1 ms at SCHED_IDLE.  topo_xml() raises it back before it waits.
+        // (discovery, link-up, LLDP) runs first and this fills its gaps instead of competing with
+        // it.  Measured in the netns harness, 8 NICs, L3: total_ready +5.6 ms over no topology file
+        // at normal priority, +1 ms at SCHED_IDLE.  topo_xml() raises it back before it waits.
         {
             std::lock_guard<std::mutex> lk(worker->mu);
             worker->tid = pid_t(::syscall(SYS_gettid));
@@ -859,8 +884,7 @@ void Agent::start_topo() {
                 w.running = false;
             }
         } done{*worker};
-        return artifacts::generate_rccl_topo(disc.gpus, artifacts::topo_nics(disc, names, root), topo::cpu_identity(),
-                                             root);
+        return make_topology(disc, interfaces, root, path);
     };
     try {
         topo_future_ = std::async(std::launch::async, work);
@@ -871,7 +895,7 @@ void Agent::start_topo() {
 }
 
 const std::string& Agent::topo_xml() {
-    if (!topo_xml_) {
+    if (!topo_) {
         if (!topo_future_.valid()) start_topo();
         if (auto w = topo_worker_) {  // we are about to wait for it: normal priority again
             std::lock_guard<std::mutex> lk(w->mu);
@@ -879,29 +903,42 @@ const std::string& Agent::topo_xml() {
             if (w->running) (void)::sched_setscheduler(w->tid, SCHED_OTHER, &sp);
         }
         try {
-            topo_xml_ = topo_future_.get();
+            topo_ = topo_future_.get();
+            // The worker's interface list is the agent's (same discovery); kept as a guard.
+            std::vector<std::string> mine = topo_names(disc_, cfg_.interfaces);
+            if (topo_->names != mine) {
+                NLOG_I("Interfaces changed while the topology file was generated: generating it again");
+                std::string root = cfg_.sysfs_root.empty() ? topo::sysfs_root() : cfg_.sysfs_root;
+                topo_->names = mine;
+                topo_->fp = topo_fingerprint(disc_, mine, root);
+                topo_->xml = artifacts::generate_rccl_topo(disc_.gpus, artifacts::topo_nics(disc_, mine, root),
+                                                           topo::cpu_identity(), root);
+                topo_->reused = false;
+            } else if (topo_->reused) {
+                NLOG_V(2, "RCCL topology file %s is current (same boot and devices): reused", cfg_.rccl_topo.c_str());
+            }
         } catch (const std::exception& e) {
             NLOG_E("Error generating the RCCL topology file: %s", e.what());
-            topo_xml_ = std::string();
+            topo_ = TopoResult{};
         }
     }
-    return *topo_xml_;
+    return topo_->xml;
 }
 
 std::string Agent::write_topo() {
     if (cfg_.rccl_topo.empty()) return "";
     const std::string& xml = topo_xml();
     if (xml.empty()) return "";  // rccl.env then names no topology
-    if (!topo_reused_) {
+    if (!topo_->reused) {
         try {
             ::unlink((cfg_.rccl_topo + ".key").c_str());  // never a key next to a file it does not describe
             write_file_atomic(cfg_.rccl_topo, xml, 0644);
-            if (!topo_fp_.empty()) write_file_atomic(cfg_.rccl_topo + ".key", topo_fp_, 0644);
+            if (!topo_->fp.empty()) write_file_atomic(cfg_.rccl_topo + ".key", topo_->fp, 0644);
         } catch (const std::exception& e) {
             NLOG_E("Error writing RCCL topology file: %s", e.what());
             return "";
         }
-        topo_reused_ = true;  // written: later refreshes (re-addressing) keep it
+        topo_->reused = true;  // written: later refreshes (re-addressing) keep it
     }
     return cfg_.rccl_topo_env_path.empty() ? cfg_.rccl_topo : cfg_.rccl_topo_env_path;
 }
@@ -1001,6 +1038,7 @@ std::map<std::string, std::string> Agent::status_node() const {
     }
     if (cfg_.xgmi_expect_links >= 0)
         m["xgmi_pairs"] = std::to_string(xgmi_.pairs_connected) + "/" + std::to_string(xgmi_.pairs_expected);
+    if (cpu_ms_at_ready_ >= 0) m["cpu_ms_at_ready"] = strfmt("%.3f", cpu_ms_at_ready_);
     if (cfg_.dry_run) {
         m["dry_run"] = "true";
         if (!dry_run_missing_.empty()) m["not_in_netns"] = join(dry_run_missing_, ",");
@@ -1133,8 +1171,9 @@ void Agent::run(int stop_fd) {
                 dry_run_missing_.push_back(i);
     }
     mark("discover");
-    // At background priority from here: overlaps the checks, link-up and the LLDP wait.
-    if (!cfg_.dry_run) start_topo();
+    // From the agent's discovery, at background priority on another CPU: overlaps the checks,
+    // link-up and the LLDP wait.
+    start_topo();
     // The xGMI mesh does not depend on LLDP: verify it up front, so a broken mesh fails in
     // milliseconds instead of after the LLDP wait, and nothing is left for the critical path.
     check_xgmi();
@@ -1247,6 +1286,12 @@ void Agent::run(int stop_fd) {
     }
     ready_ = true;
     phases_["total_ready"] = mono_ns() - t0_;
+    {  // CPU the bring-up used, all threads (the DaemonSet's limit is a CFS quota per 100 ms period)
+        rusage ru{};
+        if (::getrusage(RUSAGE_SELF, &ru) == 0)
+            cpu_ms_at_ready_ = double(ru.ru_utime.tv_sec + ru.ru_stime.tv_sec) * 1e3 +
+                               double(ru.ru_utime.tv_usec + ru.ru_stime.tv_usec) / 1e3;
+    }
     if (cfg_.mode == "L3") write_host_config();
     write_status();
     NLOG_I("Configurations done. %s...", cfg_.monitor ? "Monitoring" : "Idling");

@@ -388,6 +388,11 @@ def run_scenario(n_nics: int = 8, mode: str = "L3", seed: int | None = None, int
                      "interval": interval, "pipeline": pipeline, "plan": plan, "nics": nic_names}
         res["ready"] = t_ready is not None
         res["latency_s"] = (t_ready - t0) if t_ready else None
+        try:  # CPU of the process so far (coarse: clock ticks; the status has getrusage at readiness)
+            f = Path(f"/proc/{agent.pid}/stat").read_text().rsplit(")", 1)[1].split()
+            res["agent_cpu_ms"] = (int(f[11]) + int(f[12])) * 1000.0 / os.sysconf("SC_CLK_TCK")
+        except (OSError, IndexError, ValueError):
+            res["agent_cpu_ms"] = None
         try:  # resource envelope (the DaemonSet requests 45Mi / limits 90Mi, like the reference)
             st = Path(f"/proc/{agent.pid}/status").read_text()
             res["agent_rss_kib"] = int(next(x for x in st.splitlines() if x.startswith("VmHWM:")).split()[1])
