@@ -1388,17 +1388,22 @@ void Agent::monitor(int stop_fd) {
             changed = true;
         }
         // Link state.
+        std::string removed;
         if (watcher) {
             for (auto& ev : watcher->wait(mono_ns())) {
                 for (auto& n : nics_) {
                     if (n.link.index != ev.link.index) continue;
+                    if (ev.deleted) {  // driver reload, hot-unplug: the NIC will come back as a new ifindex
+                        removed = n.ifname;
+                        continue;
+                    }
                     bool was_up = n.link.up(), had_carrier = carrier[n.link.index];
                     n.link.flags = ev.link.flags;
                     n.link.operstate = ev.link.operstate;
                     bool up = n.link.up(), lower = n.link.lower_up();
-                    if (ev.deleted || (was_up && !up) || (had_carrier && !lower)) {
+                    if ((was_up && !up) || (had_carrier && !lower)) {
                         if (!n.degraded) {
-                            NLOG_W("Interface '%s' lost link (%s)", n.ifname.c_str(), ev.deleted ? "removed" : n.link.flags_str().c_str());
+                            NLOG_W("Interface '%s' lost link (%s)", n.ifname.c_str(), n.link.flags_str().c_str());
                             n.degraded = true;
                             ++n.flaps;
                             ++flaps_;
@@ -1417,6 +1422,20 @@ void Agent::monitor(int stop_fd) {
                     if (lower) carrier[n.link.index] = true;
                 }
             }
+        }
+        if (!removed.empty()) {
+            // Everything this agent knows about the NIC (ifindex, LLDP socket, RDMA device, GID) is
+            // gone with it.  Tear down and exit: the kubelet restarts the container, and the new agent
+            // discovers the node again once the NIC is back (until then it fails to start and
+            // retries; the node stays unlabelled).  Monitoring on would otherwise stay degraded for good.
+            NLOG_W("Interface '%s' was removed: cleaning up and exiting so that a restarted agent discovers the node again",
+                   removed.c_str());
+            nics_.erase(std::remove_if(nics_.begin(), nics_.end(), [&](const NicState& n) { return n.ifname == removed; }),
+                        nics_.end());
+            ready_ = false;
+            post_cleanups();
+            write_status();
+            throw AgentError("Interface '" + removed + "' was removed");
         }
         if (changed) {
             bool healthy = std::all_of(nics_.begin(), nics_.end(), [&](const NicState& n) { return nic_healthy(n); });

@@ -1116,3 +1116,35 @@ TEST(agent_topology_file_reused_within_a_boot) {
     CHECK(read_file(f.cfg.rccl_topo)->find("kept") == std::string::npos);
     CHECK(*read_file(f.cfg.rccl_topo + ".key") == *key);
 }
+
+TEST(agent_monitor_exits_when_a_nic_is_removed) {
+    Fixture f;
+    f.cfg.monitor_tick_ns = 1000000;
+    Pipe stop;
+    agent::Agent a(f.cfg, f.ops, f.all_valid(), f.nm());
+    bool labelled_before = false;
+    a.on_monitor_tick = [&](int tick) {
+        if (tick == 1) {
+            labelled_before = path_exists(f.cfg.labels.path());
+            auto l = f.ops.links["ens2"];
+            f.ops.links.erase("ens2");  // driver reload: the netdev is gone (it returns as a new ifindex)
+            f.ops.addrs.erase(std::remove_if(f.ops.addrs.begin(), f.ops.addrs.end(),
+                                             [&](const nl::AddrInfo& x) { return x.ifindex == l.index; }),
+                              f.ops.addrs.end());
+            f.ops.events.push_back({true, l});
+        } else if (tick > 20) {
+            stop.fire();  // not reached: the agent leaves by itself
+        }
+    };
+    bool threw = false;
+    try {
+        a.run(stop.fd[0]);
+    } catch (const agent::AgentError& e) {
+        threw = std::string(e.what()).find("ens2") != std::string::npos;
+    }
+    CHECK(labelled_before);
+    CHECK(threw);
+    CHECK(!path_exists(f.cfg.labels.path()));
+    CHECK(f.ops.addrs.empty());  // the other NICs were cleaned up too
+    CHECK(!a.ready());
+}

@@ -83,24 +83,32 @@ int main(int argc, char** argv) {
     };
     std::vector<Port> ps;
     int ep = ::epoll_create1(EPOLL_CLOEXEC);
-    try {
-        nl::Rtnl rtnl;
-        int64_t now = mono_ns();
-        for (auto& [ifname, desc] : ports) {
-            auto link = rtnl.link_by_name(ifname);
-            if (!link.up()) rtnl.link_set_up(link.index);
-            if (assign_ip) {
-                if (auto a = l3::parse_port_description(desc, l3::TokenPolicy::CompatThenLast, nullptr)) {
-                    try {
-                        rtnl.addr_add(link.index, Ipv4Prefix{a->peer, a->prefix});
-                    } catch (const SysError& e) {
-                        if (e.code() != EEXIST) throw;
-                    }
+    std::unique_ptr<nl::Rtnl> rtnl_holder;
+    // Bring a port up (and give it the switch side of its /30): at start, and again when the port
+    // was re-created (the peer NIC's driver reload in the end-to-end harness).
+    auto open_port = [&](nl::Rtnl& rtnl, const std::string& ifname, const std::string& desc, Port& p) {
+        auto link = rtnl.link_by_name(ifname);
+        if (!link.up()) rtnl.link_set_up(link.index);
+        if (assign_ip) {
+            if (auto a = l3::parse_port_description(desc, l3::TokenPolicy::CompatThenLast, nullptr)) {
+                try {
+                    rtnl.addr_add(link.index, Ipv4Prefix{a->peer, a->prefix});
+                } catch (const SysError& e) {
+                    if (e.code() != EEXIST) throw;
                 }
             }
+        }
+        p.sock = std::make_unique<pkt::LldpSocket>(ifname, link.index, link.mac, false);
+        p.frame = lldp::encode(lldp::make_switch_frame(link.mac, sysname, ifname, desc, uint16_t(ttl)));
+        p.neighbours.clear();
+    };
+    try {
+        rtnl_holder = std::make_unique<nl::Rtnl>();
+        nl::Rtnl& rtnl = *rtnl_holder;
+        int64_t now = mono_ns();
+        for (auto& [ifname, desc] : ports) {
             Port p;
-            p.sock = std::make_unique<pkt::LldpSocket>(ifname, link.index, link.mac, false);
-            p.frame = lldp::encode(lldp::make_switch_frame(link.mac, sysname, ifname, desc, uint16_t(ttl)));
+            open_port(rtnl, ifname, desc, p);
             p.next = phase == "zero" ? now : now + int64_t(std::uniform_real_distribution<double>(0, 1)(rng) * double(interval));
             // Scheduled first periodic frame (CLOCK_MONOTONIC ns): lets the harness model an
             // agent that never solicits fast start (the reference's) on the same run.
@@ -119,8 +127,26 @@ int main(int argc, char** argv) {
     std::fflush(stdout);
 
     pkt::ListenerStats st;
+    int64_t next_port_check = mono_ns() + 100000000;
     while (!g_stop) {
         int64_t now = mono_ns(), next = INT64_MAX;
+        if (now >= next_port_check) {  // a re-created port has a new ifindex: follow it
+            next_port_check = now + 100000000;
+            for (size_t i = 0; i < ps.size(); ++i) {
+                const auto& [ifname, desc] = ports[i];
+                try {
+                    auto link = rtnl_holder->link_by_name(ifname);
+                    if (link.index == ps[i].sock->ifindex()) continue;
+                    open_port(*rtnl_holder, ifname, desc, ps[i]);
+                    epoll_event ev{};
+                    ev.events = EPOLLIN;
+                    ev.data.u64 = i;
+                    ::epoll_ctl(ep, EPOLL_CTL_ADD, ps[i].sock->fd(), &ev);
+                    NLOG_V(1, "%s: port re-created, following it (ifindex %d)", ifname.c_str(), link.index);
+                } catch (const std::exception&) {  // gone for now
+                }
+            }
+        }
         bool all_done = count > 0;
         for (auto& p : ps) {
             if (count > 0 && p.periodic_sent >= count && p.fast_left == 0) continue;

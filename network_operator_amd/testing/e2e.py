@@ -97,7 +97,7 @@ async def _scrape(port: int, names) -> dict:
 
 async def _scenario(tmp: Path, n_nics: int, mode: str, seed: int, interval: str, fast_start: bool,
                     teardown: bool, node_name: str, policy_kw: dict, update_mtu: int, config_type: str,
-                    flap: bool, validation: str, crash_agent: bool) -> dict:
+                    flap: bool, validation: str, crash_agent: bool, driver_reload: bool) -> dict:
     from ..api.v1alpha1 import types as T
     from ..operator import kube, manager
     from ..operator.kube import ApiClient, KubeConfig
@@ -216,6 +216,24 @@ async def _scenario(tmp: Path, n_nics: int, mode: str, seed: int, interval: str,
                 link = rt.link_by_name(nif)
                 state[nif] = {"up": link["up"], "mtu": link["mtu"], "addrs": rt.addr_list(link["index"])}
             res["state"] = state
+            if driver_reload:
+                # The first NIC's driver is reloaded: its netdev disappears and comes back with a new
+                # ifindex.  The agent tears down and exits, the kubelet restarts it (it keeps failing
+                # while the NIC is missing), and once the NIC is back the node is ready again.
+                c0 = next(iter(node.containers.values()))
+                nif, port = nic_names[0], sw.ports[0]
+                t1 = time.monotonic()
+                rt.link_del(rt.link_by_name(nif)["index"])  # takes the switch end with it
+                t_unlabel = await _until(lambda: label_key not in node.node_labels(), 10)
+                await asyncio.sleep(0.3)  # the driver takes a moment
+                rt.veth_add(nif, port)
+                rt.link_set_netns_pid(rt.link_by_name(port)["index"], sw.pid)
+                t_back = await _until(lambda: all_good() and node.node_labels().get(label_key) == "true", 30)
+                res["reload_to_unlabelled_s"] = round(t_unlabel - t1, 6) if t_unlabel else None
+                res["reload_to_all_good_s"] = round(t_back - t1, 6) if t_back else None
+                res["agent_starts_after_reload"] = len(c0.started_at)
+                link = rt.link_by_name(nif)
+                res["reloaded_nic_addrs"] = rt.addr_list(link["index"])
             if crash_agent:
                 # The agent dies without cleaning up (OOM kill): the kubelet restarts the container,
                 # the new agent removes the stale label, configures again and is ready again.
@@ -430,13 +448,13 @@ def run_fabric(n_nodes: int = 2, n_nics: int = 2, seed: int = 1, collective: boo
 def run_scenario(n_nics: int = 2, mode: str = "L3", seed: int = 1, interval: str = "30s", fast_start: bool = True,
                  teardown: bool = True, node_name: str = "mi355x-0", policy_kw: Optional[dict] = None,
                  update_mtu: int = 0, config_type: str = "amd-so", flap: bool = False, validation: str = "",
-                 crash_agent: bool = False, keep_tmp: bool = False) -> dict:
+                 crash_agent: bool = False, driver_reload: bool = False, keep_tmp: bool = False) -> dict:
     """Must already run inside a private user+net namespace (``run_isolated``)."""
     tmp = Path(tempfile.mkdtemp(prefix="netop-e2e-"))
     try:
         return asyncio.run(_scenario(tmp, n_nics, mode, seed, interval, fast_start, teardown, node_name,
                                      dict(policy_kw or {}), update_mtu, config_type, flap, validation,
-                                     crash_agent))
+                                     crash_agent, driver_reload))
     finally:
         if not keep_tmp:
             shutil.rmtree(tmp, ignore_errors=True)

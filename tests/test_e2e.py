@@ -158,3 +158,14 @@ def test_scale_out_and_host_nic_policies_share_a_node():
     scale_out = r["nics"][:2]
     assert all(r["after_delete"][n] == [] for n in scale_out)
     assert all(r["after_delete"][n] != [] for n in e2e.HOST_NICS)
+
+
+def test_nic_driver_reload_is_survived():
+    """A NIC disappears and comes back with a new ifindex (driver reload): the agent tears down
+    and exits, the kubelet restarts it until the NIC is back, and the node is ready again with
+    the same address (round 1's agent stayed degraded for good: it tracked the old ifindex)."""
+    r = e2e.run_isolated(n_nics=4, mode="L3", seed=14, driver_reload=True)
+    assert r["reload_to_unlabelled_s"] is not None and r["reload_to_all_good_s"] is not None, r["agent_log"]
+    assert r["agent_starts_after_reload"] >= 2
+    assert r["reloaded_nic_addrs"] == [r["plan"][0]["local"] + "/30"]
+    assert f"Interface '{r['nics'][0]}' was removed" in r["agent_log"]
