@@ -12,6 +12,8 @@ from __future__ import annotations
 import asyncio
 import datetime as dt
 import logging
+import math
+import os
 import socket
 import uuid
 from typing import Awaitable, Callable, Optional
@@ -29,7 +31,9 @@ def _now_str() -> str:
 
 
 def default_identity() -> str:
-    return f"{socket.gethostname()}_{uuid.uuid4()}"
+    """``<pod>_<uuid>`` as controller-runtime builds it: the pod name (``POD_NAME`` from the
+    downward API, else the hostname, which is the pod name in a pod)."""
+    return f"{os.environ.get('POD_NAME') or socket.gethostname()}_{uuid.uuid4()}"
 
 
 class LeaderElector:
@@ -57,7 +61,7 @@ class LeaderElector:
         body = {
             "apiVersion": "coordination.k8s.io/v1", "kind": "Lease",
             "metadata": {"name": self.name, "namespace": self.namespace},
-            "spec": {"holderIdentity": self.identity, "leaseDurationSeconds": int(self.lease_duration),
+            "spec": {"holderIdentity": self.identity, "leaseDurationSeconds": max(1, math.ceil(self.lease_duration)),
                      "acquireTime": spec_prev.get("acquireTime") if same_holder else _now_str(),
                      "renewTime": _now_str(), "leaseTransitions": transitions},
         }

@@ -97,6 +97,14 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--dependency-check-interval", type=float, default=60.0,
                     help="seconds between checks for Node Feature Discovery / cert-manager (0 = off)")
     ap.add_argument("--leader-election-id", default=DEFAULT_LEASE_ID)
+    # kube-controller-manager's names for client-go's LeaderElectionConfig timings; the defaults
+    # are controller-runtime's (the reference does not expose them, main.go:174-175).
+    ap.add_argument("--leader-elect-lease-duration", type=float, default=15.0,
+                    help="seconds a standby waits after the last observed renewal before taking over")
+    ap.add_argument("--leader-elect-renew-deadline", type=float, default=10.0,
+                    help="seconds the leader keeps trying to renew before it gives up leading")
+    ap.add_argument("--leader-elect-retry-period", type=float, default=2.0,
+                    help="seconds between acquire / renew attempts")
     ap.add_argument("--policies-file", default="",
                     help="YAML file ({policies: [NetworkClusterPolicy, ...]}, the Helm chart's ConfigMap) whose "
                          "policies the leader creates / updates / deletes through the API server")
@@ -181,7 +189,14 @@ async def run(argv: Optional[List[str]] = None, stop: Optional[asyncio.Event] = 
 
         try:
             if opts.leader_elect:
-                elector = LeaderElector(client, ns, opts.leader_election_id)
+                if not (opts.leader_elect_lease_duration > opts.leader_elect_renew_deadline
+                        > opts.leader_elect_retry_period > 0):
+                    log.error("leader election needs lease duration > renew deadline > retry period > 0")
+                    return 1
+                elector = LeaderElector(client, ns, opts.leader_election_id,
+                                        lease_duration=opts.leader_elect_lease_duration,
+                                        renew_deadline=opts.leader_elect_renew_deadline,
+                                        retry_period=opts.leader_elect_retry_period)
                 metrics.leader.labels(opts.leader_election_id).set(0)
 
                 async def lead_with_metric() -> None:

@@ -95,9 +95,142 @@ async def _scrape(port: int, names) -> dict:
     return out
 
 
+# HA run: lease timings short enough for a test (controller-runtime's are 15 s / 10 s / 2 s).
+_LEASE_ARGS = ("--leader-elect-lease-duration=2", "--leader-elect-renew-deadline=1.5",
+               "--leader-elect-retry-period=0.25")
+
+
+def _port_open(port: int) -> bool:
+    import socket
+
+    with socket.socket() as s:
+        s.settimeout(0.2)
+        return s.connect_ex(("127.0.0.1", port)) == 0
+
+
+def _lease_holder(fake, ns: str) -> str:
+    from ..operator import kube
+    from ..operator.leader import DEFAULT_LEASE_ID
+
+    return ((fake.get_object(kube.LEASES, DEFAULT_LEASE_ID, ns) or {}).get("spec") or {}).get("holderIdentity") or ""
+
+
+async def _start_replicas(tmp: Path, url: str, ns: str, n: int = 2) -> list:
+    """The operator Deployment with ``replicas: n``: separate processes (so the leader can be
+    SIGKILLed), ``--leader-elect``, webhooks on with one serving certificate (the Secret that
+    cert-manager issues, mounted in every pod)."""
+    from ..operator.servers import generate_self_signed
+
+    generate_self_signed(tmp / "certs")
+    root = Path(__file__).resolve().parents[2]
+    out = []
+    for i in range(n):
+        r = {"name": f"operator-{chr(ord('a') + i)}", "webhook": _free_port(), "metrics": _free_port()}
+        r["log"] = tmp / f"{r['name']}.log"
+        env = dict(os.environ, ENABLE_WEBHOOKS="true", OPERATOR_NAMESPACE=ns, POD_NAME=r["name"],
+                   PYTHONPATH=str(root))
+        with open(r["log"], "wb") as logf:
+            r["proc"] = await asyncio.create_subprocess_exec(
+                sys.executable, "-m", "network_operator_amd.operator", "--master", url, "--leader-elect",
+                *_LEASE_ARGS, f"--webhook-port={r['webhook']}", f"--webhook-cert-dir={tmp / 'certs'}",
+                "--health-probe-bind-address=0", f"--metrics-bind-address=127.0.0.1:{r['metrics']}",
+                "--dependency-check-interval=0", env=env, stdout=asyncio.subprocess.DEVNULL, stderr=logf)
+        out.append(r)
+    return out
+
+
+async def _stop_replicas(replicas: list) -> list:
+    rcs = []
+    for r in replicas:
+        p = r["proc"]
+        if p.returncode is None:
+            p.terminate()
+            try:
+                await asyncio.wait_for(p.wait(), 20)
+            except asyncio.TimeoutError:  # pragma: no cover
+                p.kill()
+                await p.wait()
+        rcs.append(p.returncode)
+    return rcs
+
+
+async def _register_webhooks(fake, c, tmp: Path, ns: str, replica: dict) -> dict:
+    """What the kustomize tree installs for admission: the webhook Service and the two
+    configurations exactly as packaged (service-routed, plural resource), the CA bundle filled
+    in as cert-manager's CA injector does, and the Service's endpoint the first replica's pod
+    (set once it serves, as the endpoints controller would)."""
+    import base64
+
+    from ..operator import kube
+    from ..packaging import manifests as M
+
+    ca = base64.b64encode((tmp / "certs" / "tls.crt").read_bytes()).decode()
+    svc, names = "", []
+    for o in M.finalize([M.webhook_service(), *M.webhook_configurations()], ns):
+        if o["kind"] == "Service":
+            await c.create(kube.SERVICES, o, namespace=ns)
+            svc = o["metadata"]["name"]
+            continue
+        for wh in o["webhooks"]:
+            wh["clientConfig"]["caBundle"] = ca
+        await c.create(kube.MUTATINGWEBHOOKS if o["kind"].startswith("Mutating") else kube.VALIDATINGWEBHOOKS, o)
+        names.append(o["metadata"]["name"])
+    assert await _until(lambda: _port_open(replica["webhook"]), 30, poll=0.05), f"{replica['name']} not serving"
+    fake.service_endpoints[(ns, svc)] = f"https://127.0.0.1:{replica['webhook']}"
+    return {"service": svc, "configurations": names, "endpoint": replica["name"]}
+
+
+async def _ha_checks(fake, c, rt, node, replicas: list, ns: str, name: str, mode: str, nic_names: list,
+                     label_key: str, all_good, new_mtu: int) -> dict:
+    """Admission and fail-over with the node already ready: the stored policy was defaulted by
+    the mutating webhook, an invalid one is refused by the validating webhook; then the leader
+    is SIGKILLed (no lease release), the policy is edited, and the standby must take the lease
+    and roll the edit out to the node."""
+    from ..api.v1alpha1 import types as T
+    from ..operator import kube
+    from ..operator.kube import ApiError
+    from ..operator.leader import DEFAULT_LEASE_ID
+
+    P = kube.NETWORKCLUSTERPOLICIES
+    out: dict = {"admission_calls": len(fake.admission_calls)}
+    out["defaulted_image"] = ((fake.get_object(P, name) or {}).get("spec") or {}).get("amdScaleOut", {}).get("image")
+    try:
+        await c.create(P, T.new_policy("bad", layer=mode, node_selector={"foo.com": "_bar"}).to_dict())
+        out["bad_policy"] = "admitted"
+    except ApiError as e:
+        out["bad_policy"] = {"status": e.status, "message": e.message}
+    holder = _lease_holder(fake, ns)
+    leader = next(r for r in replicas if holder.startswith(r["name"] + "_"))
+    standby = next(r for r in replicas if r is not leader)
+    t1 = time.monotonic()
+    leader["proc"].kill()
+    await leader["proc"].wait()
+    for k in list(fake.service_endpoints):  # the endpoints controller drops the dead pod
+        fake.service_endpoints[k] = f"https://127.0.0.1:{standby['webhook']}"
+    cur = await c.get(P, name)
+    cur["spec"]["amdScaleOut"]["mtu"] = new_mtu
+    gen = (await c.replace(P, cur))["metadata"]["generation"]
+    t_lead = await _until(lambda: _lease_holder(fake, ns).startswith(standby["name"] + "_"), 30)
+    t_mtu = await _until(lambda: all(rt.link_by_name(n)["mtu"] == new_mtu for n in nic_names), 30)
+
+    def rolled_out():
+        st = (fake.get_object(P, name) or {}).get("status") or {}
+        return (st.get("observedGeneration") == gen and all_good()
+                and node.node_labels().get(label_key) == "true")
+    t_ready = await _until(rolled_out, 30)
+    rel = lambda t: round(t - t1, 6) if t else None  # noqa: E731
+    lease = fake.get_object(kube.LEASES, DEFAULT_LEASE_ID, ns) or {}
+    out["failover"] = {"killed": leader["name"], "new_leader": _lease_holder(fake, ns).split("_")[0],
+                       "lease_transitions": (lease.get("spec") or {}).get("leaseTransitions"),
+                       "kill_to_new_leader_s": rel(t_lead), "kill_to_mtu_applied_s": rel(t_mtu),
+                       "kill_to_ready_again_s": rel(t_ready), "generation": gen,
+                       "admission_calls": len(fake.admission_calls)}
+    return out
+
+
 async def _scenario(tmp: Path, n_nics: int, mode: str, seed: int, interval: str, fast_start: bool,
                     teardown: bool, node_name: str, policy_kw: dict, update_mtu: int, config_type: str,
-                    flap: bool, validation: str, crash_agent: bool, driver_reload: bool) -> dict:
+                    flap: bool, validation: str, crash_agent: bool, driver_reload: bool, ha: bool) -> dict:
     from ..api.v1alpha1 import types as T
     from ..operator import kube, manager
     from ..operator.kube import ApiClient, KubeConfig
@@ -136,10 +269,15 @@ async def _scenario(tmp: Path, n_nics: int, mode: str, seed: int, interval: str,
     stop = asyncio.Event()
     started = asyncio.Event()
     metrics_port = _free_port()
-    op = asyncio.ensure_future(manager.run(["--master", url, "--health-probe-bind-address=0",
-                                            f"--metrics-bind-address=127.0.0.1:{metrics_port}",
-                                            "--dependency-check-interval=0"],
-                                           stop=stop, started=started))
+    replicas: list = []
+    if ha:
+        op = None
+        replicas = await _start_replicas(tmp, url, "amd-network-operator")
+    else:
+        op = asyncio.ensure_future(manager.run(["--master", url, "--health-probe-bind-address=0",
+                                                f"--metrics-bind-address=127.0.0.1:{metrics_port}",
+                                                "--dependency-check-interval=0"],
+                                               stop=stop, started=started))
     kmd = [sys.executable, "-m", "network_operator_amd.testing.fakesysfs", "bind", KMD_DRIVER,
            *[n for n in nic_names if n in HOST_NICS]]
     from ..api.v1alpha1 import types as T0
@@ -154,7 +292,14 @@ async def _scenario(tmp: Path, n_nics: int, mode: str, seed: int, interval: str,
     ns = "amd-network-operator"
     name = "scale-out"
     try:
-        await asyncio.wait_for(started.wait(), 20)
+        if ha:
+            async with ApiClient(KubeConfig(host=url)) as c:
+                res["webhook_registration"] = await _register_webhooks(fake, c, tmp, ns, replicas[0])
+            leader = await _until(lambda: _lease_holder(fake, ns), 20)
+            assert leader, "no operator replica took the lease"
+            metrics_port = next(r for r in replicas if _lease_holder(fake, ns).startswith(r["name"] + "_"))["metrics"]
+        else:
+            await asyncio.wait_for(started.wait(), 20)
         await node.start()
         async with ApiClient(KubeConfig(host=url)) as c:
             if host_nic:
@@ -204,6 +349,9 @@ async def _scenario(tmp: Path, n_nics: int, mode: str, seed: int, interval: str,
             res["operator_metrics"] = await _scrape(metrics_port, ("amd_network_operator_agent_ready_seconds_count",
                                                                    "amd_network_operator_agent_ready_seconds_sum",
                                                                    "amd_network_operator_policy_ready"))
+            if ha:
+                res.update(await _ha_checks(fake, c, rt, node, replicas, ns, name, mode, nic_names, label_key,
+                                            all_good, update_mtu or 4200))
             res["init_runs"] = [dict(r, t_start=rel(r["t_start"]), t_end=rel(r["t_end"])) for r in node.init_runs]
             res["agent_started_s"] = [rel(t) for x in node.containers.values() for t in x.started_at]
             res["node_labels"] = node.node_labels()
@@ -299,10 +447,14 @@ async def _scenario(tmp: Path, n_nics: int, mode: str, seed: int, interval: str,
                 res["agent_log"] += f.read_text(errors="replace")[-6000:]
         await node.stop()
         stop.set()
-        try:
-            res["operator_rc"] = await asyncio.wait_for(op, 20)
-        except Exception as e:  # pragma: no cover
-            res["operator_rc"] = repr(e)
+        if op is not None:
+            try:
+                res["operator_rc"] = await asyncio.wait_for(op, 20)
+            except Exception as e:  # pragma: no cover
+                res["operator_rc"] = repr(e)
+        if replicas:
+            res["operator_rc"] = await _stop_replicas(replicas)
+            res["operator_logs"] = {r["name"]: r["log"].read_text(errors="replace")[-3000:] for r in replicas}
         await fake.stop()
         sw.stop()
     return res
@@ -448,13 +600,14 @@ def run_fabric(n_nodes: int = 2, n_nics: int = 2, seed: int = 1, collective: boo
 def run_scenario(n_nics: int = 2, mode: str = "L3", seed: int = 1, interval: str = "30s", fast_start: bool = True,
                  teardown: bool = True, node_name: str = "mi355x-0", policy_kw: Optional[dict] = None,
                  update_mtu: int = 0, config_type: str = "amd-so", flap: bool = False, validation: str = "",
-                 crash_agent: bool = False, driver_reload: bool = False, keep_tmp: bool = False) -> dict:
+                 crash_agent: bool = False, driver_reload: bool = False, ha: bool = False,
+                 keep_tmp: bool = False) -> dict:
     """Must already run inside a private user+net namespace (``run_isolated``)."""
     tmp = Path(tempfile.mkdtemp(prefix="netop-e2e-"))
     try:
         return asyncio.run(_scenario(tmp, n_nics, mode, seed, interval, fast_start, teardown, node_name,
                                      dict(policy_kw or {}), update_mtu, config_type, flap, validation,
-                                     crash_agent, driver_reload))
+                                     crash_agent, driver_reload, ha))
     finally:
         if not keep_tmp:
             shutil.rmtree(tmp, ignore_errors=True)

@@ -8,6 +8,7 @@ The reference's e2e suite deploys the operator into kind and checks that its pod
 
 import pytest
 
+from network_operator_amd.api.v1alpha1 import types as T
 from network_operator_amd.testing import e2e
 
 pytestmark = pytest.mark.netns
@@ -169,3 +170,21 @@ def test_nic_driver_reload_is_survived():
     assert r["agent_starts_after_reload"] >= 2
     assert r["reloaded_nic_addrs"] == [r["plan"][0]["local"] + "/30"]
     assert f"Interface '{r['nics'][0]}' was removed" in r["agent_log"]
+
+
+def test_two_operator_replicas_with_webhooks_fail_over():
+    """The operator as installed: two replicas with ``--leader-elect`` and the admission webhooks
+    registered exactly as packaged (Service-routed, CA injected).  The stored policy carries the
+    mutating webhook's defaults and an invalid one is refused.  Then the leader is SIGKILLed (no
+    lease release) and the policy edited: the standby takes the lease after it expires, admits
+    the edit and rolls it out to the node."""
+    r = e2e.run_isolated(n_nics=2, mode="L3", seed=15, ha=True, update_mtu=0, teardown=True)
+    assert r["policy_to_all_good_s"] is not None, (r["agent_log"], r.get("operator_logs"))
+    assert r["defaulted_image"] == T.DEFAULT_AGENT_IMAGE
+    assert r["bad_policy"]["status"] == 403 and "invalid node selector" in r["bad_policy"]["message"]
+    f = r["failover"]
+    assert f["new_leader"] != f["killed"] and f["lease_transitions"] >= 1
+    assert f["kill_to_new_leader_s"] is not None and f["kill_to_new_leader_s"] < 10, f
+    assert f["kill_to_mtu_applied_s"] is not None and f["kill_to_ready_again_s"] is not None, r["operator_logs"]
+    assert f["admission_calls"] > r["admission_calls"]  # the edit went through the standby's webhook
+    assert r["delete_to_label_removed_s"] is not None

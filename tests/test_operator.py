@@ -311,6 +311,28 @@ def test_leader_election_single_active_and_failover():
     run(body())
 
 
+def test_leader_election_timings_are_flags_and_checked(monkeypatch):
+    """``--leader-elect-{lease-duration,renew-deadline,retry-period}`` reach the elector; an
+    order that client-go would reject (lease <= renew deadline) stops the manager."""
+    from network_operator_amd.operator import manager
+
+    opts = manager.build_parser().parse_args(["--leader-elect-lease-duration=4", "--leader-elect-renew-deadline=3",
+                                              "--leader-elect-retry-period=0.5"])
+    assert (opts.leader_elect_lease_duration, opts.leader_elect_renew_deadline,
+            opts.leader_elect_retry_period) == (4, 3, 0.5)
+    monkeypatch.setenv("ENABLE_WEBHOOKS", "false")
+
+    async def body():
+        fake = FakeApiServer()
+        url = await fake.start()
+        rc = await manager.run(["--master", url, "--health-probe-bind-address=0", "--dependency-check-interval=0",
+                                "--leader-elect", "--leader-elect-lease-duration=2",
+                                "--leader-elect-renew-deadline=2"])
+        await fake.stop()
+        return rc
+    assert run(body()) == 1
+
+
 def test_fake_api_server_semantics():
     async def body():
         fake = FakeApiServer()
