@@ -63,6 +63,10 @@ def test_helm_defaults():
         dep["spec"]["template"]["spec"]["volumes"]
     assert "--metrics-bind-address=:8443" in c["args"] and "--leader-elect" in c["args"]
     assert c["image"] == "amd/amd-network-operator:0.1.0"
+    assert dep["spec"]["replicas"] == 1
+    assert {"name": "POD_NAME", "valueFrom": {"fieldRef": {"fieldPath": "metadata.name"}}} in c["env"]
+    two = _by_kind(helm_template(CHART, {"operator": {"replicas": 2}}, "amd-net"), "Deployment")[0]
+    assert two["spec"]["replicas"] == 2  # an integer, not the string "2"
     assert c["resources"] == M.RESOURCES and c["imagePullPolicy"] == "IfNotPresent"
     cert = _by_kind(docs, "Certificate")[0]
     assert cert["spec"]["dnsNames"][0] == "amd-network-webhook.amd-net.svc"
