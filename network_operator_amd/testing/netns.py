@@ -305,7 +305,8 @@ def run_scenario(n_nics: int = 8, mode: str = "L3", seed: int | None = None, int
                  xgmi_expect: int = 0, keep_tmp: bool = False, sigterm: bool = True, verbose: int = 2,
                  drop_xgmi: list | None = None, extra_args: list | None = None, flap_port: int | None = None,
                  crash_restart: bool = False, crash_after_s: float = 0.0, gid_delay_s: float = 0.0,
-                 egress_probe: bool = False, nm_bus: bool = False, lldp_cache: bool = False) -> dict:
+                 egress_probe: bool = False, nm_bus: bool = False, lldp_cache: bool = False,
+                 soak_cycles: int = 0) -> dict:
     """Runs one node bring-up.  Must already be inside a private user+net namespace.
 
     nm_bus: run the agent with --disable-networkmanager against a real ``dbus-daemon`` on which a
@@ -380,8 +381,15 @@ def run_scenario(n_nics: int = 8, mode: str = "L3", seed: int | None = None, int
             nm = NetworkManagerOnBus(bus.address, {**{n: True for n in nic_names}, "eth9": True})
             env["DBUS_SYSTEM_BUS_ADDRESS"] = bus.address
             args += ["--disable-networkmanager", f"--nm-keyfile-dir={keyfile.parent}"]
+        # The agent's log goes to a file, not a pipe nobody reads until the end: a long run
+        # (soak_cycles) logs more than a pipe buffer holds and would block the agent.
+        agent_log = tmp / "agent.log"
+
+        def spawn():
+            with open(agent_log, "a") as logf:
+                return subprocess.Popen(args, env=env, stdout=logf, stderr=subprocess.STDOUT, text=True)
         t0 = time.monotonic()
-        agent = subprocess.Popen(args, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+        agent = spawn()
         budget = 5.0 + float(wait.rstrip("s"))
         t_ready = _wait_for(label, budget, agent)
         res: dict = {"n_nics": len(nic_names), "mode": mode, "fast_start": fast_start, "announce": announce,
@@ -440,11 +448,11 @@ def run_scenario(n_nics: int = 8, mode: str = "L3", seed: int | None = None, int
             # must start from scratch and still be ready in fast-start time.
             time.sleep(crash_after_s)  # e.g. let the switch's fast-transmission window run out
             agent.kill()
-            agent.communicate()
+            agent.wait()
             res["stale_label_after_crash"] = label.exists()
             wall = time.time_ns()
             t_r = time.monotonic()
-            agent = subprocess.Popen(args, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+            agent = spawn()
             back = None
             end = t_r + budget
             while time.monotonic() < end and agent.poll() is None:
@@ -494,15 +502,55 @@ def run_scenario(n_nics: int = 8, mode: str = "L3", seed: int | None = None, int
             res["flap_restore_s"] = (back - t_up) if back else None
             link = rt.link_by_name(nic_names[flap_port])
             res["flap_routes_after"] = [r for r in rt.route_list() if r["ifindex"] == link["index"]]
+        if soak_cycles and t_ready:
+            # Carrier loss on a random port, over and over, with the agent in monitor mode: every
+            # cycle must withdraw and restore the label, and the agent must not leak descriptors,
+            # threads or memory.  The baseline is taken after the first cycle (lazy allocations).
+            def proc_stat():
+                time.sleep(0.1)  # let the agent finish the status write that follows the label
+                st = Path(f"/proc/{agent.pid}/status").read_text().splitlines()
+                val = {x.split(":")[0]: x.split()[1] for x in st if x.startswith(("VmRSS:", "Threads:"))}
+                return {"fds": len(os.listdir(f"/proc/{agent.pid}/fd")), "rss_kib": int(val["VmRSS"]),
+                        "threads": int(val["Threads"])}
+            withdraw, restore, base = [], [], None
+            for k in range(soak_cycles):
+                i = rng.randrange(len(nic_names))
+                t_down = time.monotonic()
+                set_switch_port(pid, sw_ports[i], False)
+                gone = None
+                end = t_down + 10
+                while time.monotonic() < end and agent.poll() is None:
+                    if not label.exists():
+                        gone = time.monotonic()
+                        break
+                    time.sleep(0.0005)
+                t_up = time.monotonic()
+                set_switch_port(pid, sw_ports[i], True)
+                back = _wait_for(label, 10, agent)
+                if gone is None or back is None:
+                    break
+                withdraw.append(gone - t_down)
+                restore.append(back - t_up)
+                if k == 0:
+                    base = proc_stat()
+            fin = proc_stat() if agent.poll() is None else None
+            addrs_ok = all(rt.addr_list(rt.link_by_name(n)["index"]) == [p["local"] + "/30"]
+                           for n, p in zip(nic_names, plan)) if mode == "L3" else None
+            res["soak"] = {"cycles": len(withdraw), "asked": soak_cycles, "first": base, "last": fin,
+                           "withdraw_p50_s": _pct(withdraw, 0.5) if withdraw else None,
+                           "withdraw_max_s": max(withdraw) if withdraw else None,
+                           "restore_p50_s": _pct(restore, 0.5) if restore else None,
+                           "restore_max_s": max(restore) if restore else None, "addrs_ok": addrs_ok}
         t_term = None
         if sigterm and agent.poll() is None:
             t_term = time.monotonic()
             agent.send_signal(signal.SIGTERM)
         try:
-            out, _ = agent.communicate(timeout=20)
+            agent.wait(timeout=20)
         except subprocess.TimeoutExpired:
             agent.kill()
-            out, _ = agent.communicate()
+            agent.wait()
+        out = agent_log.read_text(errors="replace") if agent_log.exists() else ""
         res["sigterm_to_exit_s"] = (time.monotonic() - t_term) if t_term else None
         res["agent_rc"] = agent.returncode
         res["agent_log"] = out[-6000:]

@@ -150,6 +150,21 @@ def test_carrier_loss_withdraws_and_restores_readiness():
     assert "lost link" in r["agent_log"] and "readiness label republished" in r["agent_log"]
 
 
+def test_repeated_carrier_loss_soak_leaks_nothing():
+    """40 carrier-loss cycles on random ports under the monitor: each withdraws and restores the
+    label, and descriptors, threads and RSS after the last cycle equal those after the first."""
+    r = netns.run_isolated(n_nics=8, seed=21, interval="1s", fast_start=True, soak_cycles=40)
+    _check_configured(r)
+    s = r["soak"]
+    assert s["cycles"] == 40, r["agent_log"][-3000:]
+    assert s["addrs_ok"]
+    assert s["last"]["fds"] == s["first"]["fds"] and s["last"]["threads"] == s["first"]["threads"], s
+    if "ASAN_OPTIONS" not in os.environ:  # ASan's quarantine holds freed memory; LSan checks at exit
+        assert s["last"]["rss_kib"] - s["first"]["rss_kib"] <= 256, s  # page-granular noise only
+    assert s["withdraw_max_s"] < 1.0 and s["restore_max_s"] < 2.0, s
+    assert r["agent_rc"] == 0
+
+
 def test_disable_fw_lldp_on_real_veths():
     """Real SIOCETHTOOL on veths: no private flags -> nothing changed, node still ready."""
     r = netns.run_isolated(n_nics=2, seed=19, interval="1s", fast_start=True,
