@@ -28,6 +28,7 @@
 #include <string>
 #include <vector>
 
+#include "netop/arp.hpp"
 #include "netop/artifacts.hpp"
 #include "netop/ethtool.hpp"
 #include "netop/httpd.hpp"
@@ -77,6 +78,10 @@ struct Config {
     // The RDMA core adds the RoCE v2 GID of a new IPv4 address asynchronously (netdev notifier
     // -> GID cache work item); wait this long for it before writing rccl.env without a GID.
     int64_t gid_wait_ns = 3LL * 1000000000;
+    // L3: before the label, every configured NIC's switch-side /30 address must answer ARP
+    // within this time (0 = no check, the reference's behaviour); requests every retry.
+    int64_t verify_peers_ns = 0;
+    int64_t verify_peers_retry_ns = 100LL * 1000000;
     bool lldp_announce = true;           // transmit our own LLDPDU (triggers switch fast start)
     int64_t announce_interval_ns = 1000000000LL;  // re-announce to still-silent NICs
     int announce_count = 6;  // rounds at 0, +25 ms, +125 ms, +425 ms, +1.4 s, +2.4 s (interval 1 s)
@@ -160,6 +165,7 @@ class Agent {
         bool reused = false;             // the file on disk is current: nothing to write
     };
     Agent(Config cfg, nl::NetOps& ops, std::unique_ptr<LldpSource> lldp, NmFactory nm_factory);
+    ~Agent();
 
     // Runs the whole state machine.  `stop_fd` becomes readable on SIGTERM/SIGINT (a
     // signalfd in production, a pipe/eventfd in tests).  Throws AgentError on fatal errors.
@@ -177,6 +183,8 @@ class Agent {
 
     // Test hook: called once per monitor iteration (lets tests inject link events / stop).
     std::function<void(int)> on_monitor_tick;
+    // The ARP prober behind --verify-peers (arp::probe_all; tests inject a fake switch).
+    std::function<bool(std::vector<arp::Probe>&, int64_t timeout_ns, int64_t retry_ns, int stop_fd)> arp_probe;
     int link_flaps() const { return flaps_; }
     int reconfigurations() const { return reconfigs_; }
 
@@ -221,6 +229,9 @@ class Agent {
     bool publish_label();
     void announce_all(uint16_t ttl);
     bool nic_healthy(const NicState& n) const;
+    // --verify-peers: ARP-probes the switch side of every NIC in `which`; returns how many did
+    // not answer (-1 when interrupted by stop_fd).
+    int verify_peers(const std::vector<NicState*>& which, int stop_fd);
 
     std::map<std::string, std::string> labels_extra_;
     int flaps_ = 0;
@@ -248,6 +259,7 @@ class Agent {
     nl::NetOps& ops_;
     std::unique_ptr<LldpSource> lldp_;
     NmFactory nm_factory_;
+    std::unique_ptr<arp::Prober> arp_;  // --verify-peers sockets, opened on first use
     std::vector<NicState> nics_;
     topo::DiscoveryResult disc_;
     double cpu_ms_at_ready_ = -1;  // user + system CPU of the process when the label went up

@@ -37,6 +37,11 @@ struct NicState {
     std::string addr_error;
     bool configured = false;
     std::string config_error;
+    // --verify-peers: the switch-side /30 address answered ARP (0 = not checked / no answer)
+    bool peer_verified = false;
+    int64_t peer_rtt_ns = 0;
+    std::optional<MacAddr> peer_arp_mac;
+    std::string peer_error;
 
     // Topology
     int gpu_index = -1;

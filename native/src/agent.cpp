@@ -92,7 +92,21 @@ lldp::Frame make_node_frame(const std::string& node_name, const std::string& ifn
 // Agent
 // ---------------------------------------------------------------------------
 Agent::Agent(Config cfg, nl::NetOps& ops, std::unique_ptr<LldpSource> lldp, NmFactory nm_factory)
-    : cfg_(std::move(cfg)), ops_(ops), lldp_(std::move(lldp)), nm_factory_(std::move(nm_factory)) {}
+    : cfg_(std::move(cfg)), ops_(ops), lldp_(std::move(lldp)), nm_factory_(std::move(nm_factory)) {
+    arp_probe = [this](std::vector<arp::Probe>& ps, int64_t timeout_ns, int64_t retry_ns, int stop_fd) {
+        if (!arp_) arp_ = std::make_unique<arp::Prober>();
+        return arp_->probe(ps, timeout_ns, retry_ns, stop_fd);
+    };
+}
+
+Agent::~Agent() {
+    // Both socket sets wait for an RCU grace period when closed: overlap the two waits, so
+    // --verify-peers adds nothing to SIGTERM -> exit.
+    std::thread closing;
+    if (arp_) closing = arp_->close_async();
+    lldp_.reset();
+    if (closing.joinable()) closing.join();
+}
 
 void Agent::mark(const std::string& phase) {
     int64_t now = mono_ns();
@@ -556,6 +570,7 @@ bool Agent::refresh_from_frame(NicState& n, const lldp::Frame& f) {
         NLOG_W("could not remove old address of '%s': %s", n.ifname.c_str(), e.what());
     }
     n.configured = false;
+    n.peer_verified = false;  // a new /30: a new peer to ask
     n.gid_index.reset();  // the GID follows the address
     if (n.addr) configure_interface(n);
     ++reconfigs_;
@@ -1246,6 +1261,23 @@ void Agent::run(int stop_fd) {
                 throw AgentError(strfmt("Not all interfaces were configured (%d/%d).", configured, total));
             }
             NLOG_I("Configured %d of %d interfaces", configured, total);
+            if (cfg_.verify_peers_ns > 0) {
+                std::vector<NicState*> all;
+                for (auto& n : nics_) all.push_back(&n);
+                const int bad = verify_peers(all, stop_fd);
+                mark("verify_peers");
+                if (bad < 0) {
+                    NLOG_I("Interrupted while verifying the switch-side peers");
+                    post_cleanups();
+                    return;
+                }
+                if (bad > 0) {
+                    write_status();
+                    auto first = std::find_if(nics_.begin(), nics_.end(), [](const NicState& n) { return !n.peer_error.empty(); });
+                    throw AgentError(strfmt("%d of %d switch-side peers did not answer ARP (%s: %s)", bad, total,
+                                            first->ifname.c_str(), first->peer_error.c_str()));
+                }
+            }
         } else if (cfg_.configure && !found && !cfg_.label_without_peers) {
             write_status();
             throw AgentError("No LLDP peers with a /30 Port Description were found");
@@ -1326,8 +1358,60 @@ void Agent::announce_all(uint16_t ttl) {
     }
 }
 
+int Agent::verify_peers(const std::vector<NicState*>& which, int stop_fd) {
+    std::vector<arp::Probe> probes;
+    std::vector<NicState*> owners;
+    for (NicState* n : which) {
+        if (!n->addr || !n->configured) continue;
+        arp::Probe p;
+        p.ifname = n->ifname;
+        p.ifindex = n->link.index;
+        p.mac = n->link.mac;
+        p.local = n->addr->local;
+        p.peer = n->addr->peer;
+        probes.push_back(p);
+        owners.push_back(n);
+    }
+    if (probes.empty()) return 0;
+    bool finished = false;
+    try {
+        finished = arp_probe(probes, cfg_.verify_peers_ns, cfg_.verify_peers_retry_ns, stop_fd);
+    } catch (const std::exception& e) {
+        for (NicState* n : owners) {
+            n->peer_verified = false;
+            n->peer_error = e.what();
+        }
+        NLOG_W("Could not verify the switch-side peers: %s", e.what());
+        return int(owners.size());
+    }
+    if (!finished) return -1;
+    int failed = 0;
+    for (size_t i = 0; i < probes.size(); ++i) {
+        const arp::Probe& p = probes[i];
+        NicState& n = *owners[i];
+        n.peer_verified = p.answered;
+        if (p.answered) {
+            n.peer_rtt_ns = p.rtt_ns;
+            n.peer_arp_mac = p.peer_mac;
+            n.peer_error.clear();
+            NLOG_V(1, "interface '%s': peer %s (%s) answered ARP after %.3f ms", n.ifname.c_str(), p.peer.str().c_str(),
+                   p.peer_mac.str().c_str(), double(p.rtt_ns) / 1e6);
+            continue;
+        }
+        ++failed;
+        n.peer_error = !p.error.empty() ? p.error
+                                        : strfmt("peer %s did not answer ARP within %s (%d requests): is the switch port "
+                                                 "addressed as its Port Description says?",
+                                                 p.peer.str().c_str(), format_go_duration(cfg_.verify_peers_ns).c_str(),
+                                                 p.requests);
+        NLOG_W("interface '%s': %s", n.ifname.c_str(), n.peer_error.c_str());
+    }
+    return failed;
+}
+
 bool Agent::nic_healthy(const NicState& n) const {
     if (!n.link.up() || n.degraded || n.cache_stale) return false;
+    if (cfg_.mode == "L3" && cfg_.verify_peers_ns > 0 && !n.peer_verified) return false;
     return cfg_.mode != "L3" || n.configured;
 }
 
@@ -1344,6 +1428,7 @@ void Agent::monitor(int stop_fd) {
     std::map<int, bool> carrier;
     for (auto& n : nics_) carrier[n.link.index] = n.link.lower_up();
     int64_t next_tx = mono_ns() + cfg_.lldp_tx_interval_ns;
+    int64_t next_verify = 0;
     bool labelled = true;
     // One pollable fd for "stop or link event": the LLDP wait returns as soon as either
     // fires, so a link failure is acted on in about a millisecond, not at the next tick.
@@ -1415,6 +1500,7 @@ void Agent::monitor(int stop_fd) {
                         // Administrative down flushes the routes: ensure address and routes again.
                         if (cfg_.mode == "L3" && n.addr) {
                             n.configured = false;
+                            n.peer_verified = false;  // the switch port may have come back different
                             configure_interface(n);
                         }
                         changed = true;
@@ -1436,6 +1522,19 @@ void Agent::monitor(int stop_fd) {
             post_cleanups();
             write_status();
             throw AgentError("Interface '" + removed + "' was removed");
+        }
+        if (cfg_.mode == "L3" && cfg_.verify_peers_ns > 0 && mono_ns() >= next_verify) {
+            // NICs whose peer has not answered (yet): a recovered link, a new /30, or a switch
+            // port still without its address.  Failed NICs are asked again a second later.
+            std::vector<NicState*> todo;
+            for (auto& n : nics_)
+                if (n.configured && !n.peer_verified && n.link.up() && !n.degraded) todo.push_back(&n);
+            if (!todo.empty()) {
+                const int bad = verify_peers(todo, stop_fd);
+                if (bad < 0) return;
+                changed = true;
+                next_verify = bad > 0 ? mono_ns() + 1000000000LL : 0;
+            }
         }
         if (changed) {
             bool healthy = std::all_of(nics_.begin(), nics_.end(), [&](const NicState& n) { return nic_healthy(n); });

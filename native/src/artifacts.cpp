@@ -508,6 +508,12 @@ std::string generate_status(const std::vector<NicState>& nics, const std::map<st
         j.key("degraded").value(n->degraded);
         if (n->flaps) j.key("flaps").value(n->flaps);
         if (!n->config_error.empty()) j.key("config_error").value(n->config_error);
+        if (n->peer_verified) {
+            j.key("peer_verified").value(true);
+            j.key("peer_arp_ms").value(double(n->peer_rtt_ns) / 1e6);
+            if (n->peer_arp_mac) j.key("peer_arp_mac").value(n->peer_arp_mac->str());
+        }
+        if (!n->peer_error.empty()) j.key("peer_error").value(n->peer_error);
         if (n->gid_index) j.key("gid_index").value(*n->gid_index);
         if (n->t_lldp) j.key("t_lldp_ms").value(double(n->t_lldp - t0) / 1e6);
         if (n->t_configured) j.key("t_configured_ms").value(double(n->t_configured - t0) / 1e6);

@@ -1148,3 +1148,139 @@ TEST(agent_monitor_exits_when_a_nic_is_removed) {
     CHECK(f.ops.addrs.empty());  // the other NICs were cleaned up too
     CHECK(!a.ready());
 }
+
+// --- --verify-peers -------------------------------------------------------------------------
+TEST(arp_request_encoding_and_reply_parsing) {
+    auto req = arp::encode_request(*MacAddr::parse("02:00:00:00:00:10"), *Ipv4::parse("10.200.0.1"), *Ipv4::parse("10.200.0.2"));
+    CHECK_EQ(req.size(), arp::kPayloadLen);
+    const uint8_t head[8] = {0, 1, 8, 0, 6, 4, 0, 1};  // Ethernet, IPv4, 6, 4, who-has
+    CHECK(std::equal(head, head + 8, req.begin()));
+    CHECK_EQ(MacAddr::from_bytes(&req[8]).str(), std::string("02:00:00:00:00:10"));
+    CHECK_EQ(Ipv4::from_net(&req[14]).str(), std::string("10.200.0.1"));
+    CHECK(MacAddr::from_bytes(&req[18]).is_zero());
+    CHECK_EQ(Ipv4::from_net(&req[24]).str(), std::string("10.200.0.2"));
+    CHECK(!arp::parse_reply(req.data(), req.size()));  // a request is not a reply
+    // the peer's answer: op 2, sender = the peer
+    std::vector<uint8_t> rep(req);
+    rep[7] = 2;
+    const uint8_t peer_mac[6] = {0x02, 0xaa, 0, 0, 0, 0};
+    std::copy(peer_mac, peer_mac + 6, rep.begin() + 8);
+    Ipv4::parse("10.200.0.2")->to_net(&rep[14]);
+    std::copy(req.begin() + 8, req.begin() + 14, rep.begin() + 18);
+    Ipv4::parse("10.200.0.1")->to_net(&rep[24]);
+    auto r = arp::parse_reply(rep.data(), rep.size());
+    CHECK(r && r->sender_ip.str() == "10.200.0.2" && r->target_ip.str() == "10.200.0.1");
+    CHECK_EQ(r->sender_mac.str(), std::string("02:aa:00:00:00:00"));
+    CHECK(!arp::parse_reply(rep.data(), rep.size() - 1));  // truncated
+    rep[1] = 6;                                              // IEEE 802 hardware type
+    CHECK(!arp::parse_reply(rep.data(), rep.size()));
+}
+
+namespace {
+// A switch whose ports answer ARP except those in `silent`; records what was asked.
+struct FakeArpSwitch {
+    std::set<std::string> silent;
+    std::vector<std::pair<std::string, std::string>> asked;  // (ifname, peer)
+    bool operator()(std::vector<arp::Probe>& ps, int64_t, int64_t, int) {
+        for (auto& p : ps) {
+            asked.push_back({p.ifname, p.peer.str()});
+            p.requests = 3;
+            if (silent.count(p.ifname)) continue;
+            p.answered = true;
+            p.rtt_ns = 120000;
+            p.peer_mac = *MacAddr::parse("02:aa:00:00:00:99");
+        }
+        return true;
+    }
+};
+}  // namespace
+
+TEST(agent_verify_peers_all_answer) {
+    Fixture f;
+    f.cfg.keep_running = true;
+    f.cfg.verify_peers_ns = 500000000;
+    Pipe stop;
+    stop.fire();
+    FakeArpSwitch swi;
+    agent::Agent a(f.cfg, f.ops, f.all_valid(), f.nm());
+    a.arp_probe = [&](std::vector<arp::Probe>& ps, int64_t t, int64_t r, int s) { return swi(ps, t, r, s); };
+    a.run(stop.fd[0]);
+    CHECK(a.ready());
+    CHECK_EQ(swi.asked.size(), size_t(3));
+    std::set<std::string> peers;
+    for (auto& [i, p] : swi.asked) peers.insert(i + "=" + p);
+    CHECK(peers == (std::set<std::string>{"ens0=10.200.0.2", "ens1=10.200.0.6", "ens2=10.200.0.9"}));
+    auto st = read_file(f.cfg.status_file);
+    CHECK(st && st->find("\"peer_verified\":true") != std::string::npos && st->find("verify_peers") != std::string::npos);
+}
+
+TEST(agent_verify_peers_silent_peer_blocks_readiness) {
+    Fixture f;
+    f.cfg.keep_running = true;
+    f.cfg.verify_peers_ns = 500000000;
+    FakeArpSwitch swi;
+    swi.silent = {"ens2"};
+    agent::Agent a(f.cfg, f.ops, f.all_valid(), f.nm());
+    a.arp_probe = [&](std::vector<arp::Probe>& ps, int64_t t, int64_t r, int s) { return swi(ps, t, r, s); };
+    bool threw = false;
+    try {
+        a.run(-1);
+    } catch (const agent::AgentError& e) {
+        threw = std::string(e.what()).find("1 of 3 switch-side peers did not answer ARP (ens2") != std::string::npos;
+    }
+    CHECK(threw);
+    CHECK(!a.ready());
+    CHECK(!path_exists(f.cfg.labels.path()));
+    auto st = read_file(f.cfg.status_file);
+    CHECK(st && st->find("\"peer_error\":\"peer 10.200.0.9 did not answer ARP") != std::string::npos);
+}
+
+TEST(agent_verify_peers_off_by_default_asks_nothing) {
+    Fixture f;
+    f.cfg.keep_running = false;
+    FakeArpSwitch swi;
+    agent::Agent a(f.cfg, f.ops, f.all_valid(), f.nm());
+    a.arp_probe = [&](std::vector<arp::Probe>& ps, int64_t t, int64_t r, int s) { return swi(ps, t, r, s); };
+    a.run(-1);
+    CHECK(swi.asked.empty());
+}
+
+TEST(agent_monitor_reverifies_a_recovered_nic_before_relabelling) {
+    Fixture f;
+    f.cfg.monitor_tick_ns = 1000000;
+    f.cfg.verify_peers_ns = 500000000;
+    Pipe stop;
+    FakeArpSwitch swi;
+    agent::Agent a(f.cfg, f.ops, f.all_valid(), f.nm());
+    a.arp_probe = [&](std::vector<arp::Probe>& ps, int64_t t, int64_t r, int s) { return swi(ps, t, r, s); };
+    bool withdrawn = false, held_back = false, restored = false;
+    size_t asked_before = 0;
+    int64_t t_fixed = 0;
+    a.on_monitor_tick = [&](int tick) {
+        auto& l = f.ops.links["ens2"];
+        if (tick == 1) {
+            CHECK(path_exists(f.cfg.labels.path()));
+            l.flags &= ~unsigned(IFF_UP);
+            f.ops.events.push_back({false, l});
+        } else if (tick == 3) {
+            withdrawn = !path_exists(f.cfg.labels.path());
+            swi.silent = {"ens2"};  // the port comes back without its address
+            asked_before = swi.asked.size();
+            l.flags |= IFF_UP;
+            f.ops.events.push_back({false, l});
+        } else if (tick == 6) {
+            held_back = !path_exists(f.cfg.labels.path()) && swi.asked.size() > asked_before;
+            swi.silent.clear();
+            t_fixed = mono_ns();
+        } else if (tick > 6 && path_exists(f.cfg.labels.path())) {
+            restored = true;  // asked again a second after the failure; answered
+            stop.fire();
+        } else if (tick > 6 && mono_ns() - t_fixed > 3000000000LL) {
+            stop.fire();
+        }
+    };
+    a.run(stop.fd[0]);
+    CHECK(withdrawn);
+    CHECK(held_back);
+    CHECK(restored);
+}

@@ -70,6 +70,8 @@ int main(int argc, char** argv) {
     fs.add_bool("nm-restore", &cfg.nm_restore, "with --disable-networkmanager: set the interfaces managed by NetworkManager again on exit");
     fs.add_int("xgmi-expect", &cfg.xgmi_expect_links, "verify the xGMI mesh before labelling: -1 off, 0 full mesh, N GPU pairs");
     fs.add_duration("link-wait", &cfg.link_wait_ns, "time to wait for link state echoes from the kernel");
+    fs.add_duration("verify-peers", &cfg.verify_peers_ns,
+                    "L3: before publishing readiness, require every NIC's switch-side /30 address to answer ARP within this time (0 = off)");
     fs.add_duration("gid-wait", &cfg.gid_wait_ns, "time to wait for the RoCE v2 GID of a newly configured address");
     fs.add_bool("lldp-announce", &cfg.lldp_announce, "transmit our own LLDPDU on each NIC (makes 802.1AB-2009 switches answer within ~1s)");
     fs.add_bool("lldp-restart-fast", &cfg.announce_shutdown_first, "send a shutdown LLDPDU before the first announcement so a switch holding a stale entry (agent restart) fast-starts again");

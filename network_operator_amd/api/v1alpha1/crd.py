@@ -104,6 +104,10 @@ def openapi_schema() -> dict:
                                          "periodic LLDPDU (switches without fast start).  The switch must confirm it\n"
                                          "within 95 s, else the readiness label is withdrawn until it does.",
                           "type": "boolean"},
+            "verifyPeers": {"description": "L3: before labelling the node, require every NIC's switch-side /30 address\n"
+                                           "to answer ARP (within 2 s).  Catches a switch port whose Port Description\n"
+                                           "and interface address disagree, which LLDP alone cannot.",
+                            "type": "boolean"},
         },
     }
     host_nic = {

@@ -95,6 +95,7 @@ class AmdScaleOutSpec:
     railTableBase: int = 0
     rcclSocketIfname: str = ""
     lldpCache: bool = False
+    verifyPeers: bool = False
     validation: Optional[ValidationSpec] = None
     extra: Dict[str, Any] = field(default_factory=dict)
 
@@ -104,7 +105,7 @@ class AmdScaleOutSpec:
 
     _FIELDS = ("disableNetworkManager", "layer", "image", "pullPolicy", "mtu", "xgmiCheck", "lldpAnnounce",
                "interfaces", "nicDrivers", "disableFirmwareLldp", "metricsPort", "gpuDirectRdma", "rcclEnv",
-               "railTableBase", "rcclSocketIfname", "lldpCache", "validation")
+               "railTableBase", "rcclSocketIfname", "lldpCache", "verifyPeers", "validation")
 
     def to_dict(self) -> dict:
         d: dict = {}
@@ -138,6 +139,8 @@ class AmdScaleOutSpec:
             d["rcclSocketIfname"] = self.rcclSocketIfname
         if self.lldpCache:
             d["lldpCache"] = True
+        if self.verifyPeers:
+            d["verifyPeers"] = True
         if self.validation is not None:
             d["validation"] = self.validation.to_dict()
         d.update(copy.deepcopy(self.extra))
@@ -163,6 +166,7 @@ class AmdScaleOutSpec:
             railTableBase=int(d.pop("railTableBase", 0) or 0),
             rcclSocketIfname=d.pop("rcclSocketIfname", "") or "",
             lldpCache=bool(d.pop("lldpCache", False)),
+            verifyPeers=bool(d.pop("verifyPeers", False)),
             validation=ValidationSpec.from_dict(d.pop("validation", None)),
         )
         s.extra = d

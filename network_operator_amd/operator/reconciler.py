@@ -43,6 +43,9 @@ ARTIFACT_DIR_CONTAINER = "/host" + ARTIFACT_DIR_HOST
 RCCL_NET_FILE = "rccl-net.json"
 RCCL_ENV_FILE = "rccl.env"
 RCCL_TOPO_FILE = "rccl-topo.xml"
+# --verify-peers: a switch answers ARP in well under a millisecond; 2 s covers a port that is
+# still coming up, and stays far below the kubelet's restart back-off.
+VERIFY_PEERS_TIMEOUT = "2s"
 LLDP_CACHE_FILE = "lldp-cache"  # --lldp-cache, beside the artifacts so it survives pod restarts
 L3_WAIT = "90s"
 
@@ -166,6 +169,8 @@ def agent_args(p: T.NetworkClusterPolicy) -> List[str]:
         args.append(f"--rccl-socket-ifname={so.rcclSocketIfname}")
     if so.lldpCache and so.layer == "L3":
         args.append(f"--lldp-cache={ARTIFACT_DIR_CONTAINER}/{LLDP_CACHE_FILE}")
+    if so.verifyPeers and so.layer == "L3":
+        args.append(f"--verify-peers={VERIFY_PEERS_TIMEOUT}")
     if so.rcclEnv:
         args.append("--rccl-env-extra=" + ",".join(f"{k}={v}" for k, v in sorted(so.rcclEnv.items())))
     if so.gpuDirectRdma:

@@ -306,7 +306,7 @@ def run_scenario(n_nics: int = 8, mode: str = "L3", seed: int | None = None, int
                  drop_xgmi: list | None = None, extra_args: list | None = None, flap_port: int | None = None,
                  crash_restart: bool = False, crash_after_s: float = 0.0, gid_delay_s: float = 0.0,
                  egress_probe: bool = False, nm_bus: bool = False, lldp_cache: bool = False,
-                 soak_cycles: int = 0) -> dict:
+                 soak_cycles: int = 0, arp_silent_ports: int = 0) -> dict:
     """Runs one node bring-up.  Must already be inside a private user+net namespace.
 
     nm_bus: run the agent with --disable-networkmanager against a real ``dbus-daemon`` on which a
@@ -358,6 +358,13 @@ def run_scenario(n_nics: int = 8, mode: str = "L3", seed: int | None = None, int
                              silent_nics=silent_nics)
         t_switch = sw.start(rt)
         pid, sw_ports, first_periodic = sw.pid, sw.ports, sw.first_periodic
+        for sp in sw_ports[len(sw_ports) - arp_silent_ports:] if arp_silent_ports else []:
+            # A switch port that has its LLDP Port Description but does not answer on that /30
+            # (arp_ignore 8: no ARP replies at all) — what --verify-peers is for.
+            def mute(port=sp):
+                Path(f"/proc/sys/net/ipv4/conf/{port}/arp_ignore").write_text("8")
+            if _in_netns(pid, mute) != 0:
+                raise RuntimeError(f"could not silence ARP on {sp}")
 
         feat = tmp / "features.d"
         feat.mkdir()

@@ -165,6 +165,27 @@ def test_repeated_carrier_loss_soak_leaks_nothing():
     assert r["agent_rc"] == 0
 
 
+def test_verify_peers_asks_every_switch_port_over_arp():
+    """--verify-peers on real veths: every NIC's switch-side /30 answers a who-has from the NIC's
+    address; the status records the answer (and the port's MAC) and the node is ready."""
+    r = netns.run_isolated(n_nics=8, seed=23, interval="1s", fast_start=True, extra_args=["--verify-peers=2s"])
+    _check_configured(r)
+    assert "verify_peers" in r["status"]["phases_ms"]
+    for i in r["status"]["interfaces"]:
+        assert i["peer_verified"] is True and i["peer_arp_ms"] < 1000 and i["peer_arp_mac"], i
+
+
+def test_verify_peers_refuses_a_port_that_does_not_answer():
+    """A switch port with the right Port Description that does not answer on that /30: without
+    the check the node would be labelled; with it the agent fails and names the NIC."""
+    r = netns.run_isolated(n_nics=4, seed=23, interval="1s", fast_start=True, extra_args=["--verify-peers=300ms"],
+                           arp_silent_ports=1)
+    assert not r["ready"] and r["agent_rc"] == 1
+    silent = r["nics"][-1]
+    assert f"({silent}: peer {r['plan'][-1]['peer']} did not answer ARP within 300ms" in r["agent_log"]
+    assert r["label"] is None  # (the kubelet restarts the agent, which flushes and starts over)
+
+
 def test_disable_fw_lldp_on_real_veths():
     """Real SIOCETHTOOL on veths: no private flags -> nothing changed, node still ready."""
     r = netns.run_isolated(n_nics=2, seed=19, interval="1s", fast_start=True,

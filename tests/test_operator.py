@@ -531,6 +531,22 @@ def test_agent_args_rail_tables_l3_only():
     assert not any(a.startswith("--rail-table-base") for a in agent_args(p))
 
 
+def test_agent_args_verify_peers_l3_only():
+    from network_operator_amd.api.v1alpha1 import crd as CRD
+    from network_operator_amd.api.v1alpha1 import types as T
+    from network_operator_amd.operator.reconciler import agent_args
+
+    p = T.new_policy("p", layer="L3")
+    assert not any(a.startswith("--verify-peers") for a in agent_args(p))
+    p.spec.amdScaleOut.verifyPeers = True
+    assert "--verify-peers=2s" in agent_args(p)
+    d = p.to_dict()
+    assert d["spec"]["amdScaleOut"]["verifyPeers"] is True and CRD.validate(d) == []
+    assert T.NetworkClusterPolicy.from_dict(d).spec.amdScaleOut.verifyPeers is True
+    p.spec.amdScaleOut.layer = "L2"  # no /30 in L2: no peer address to ask
+    assert not any(a.startswith("--verify-peers") for a in agent_args(p))
+
+
 def test_fabric_validation_jobs_follow_ready_nodes_and_report_a_condition():
     """amdScaleOut.validation: one validation Job per node whose agent is ready, pinned to it, for
     the policy's current generation; the outcome is the FabricValidated condition."""
