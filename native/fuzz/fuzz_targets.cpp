@@ -4,6 +4,7 @@
 //   dbus      messages from the system bus peer
 //   portdesc  the switch's Port Description string (operator-configured, still untrusted)
 //   netlink   RTM_NEWLINK payloads (kernel, but parsed with length arithmetic)
+//   arp       ARP payloads from the switch port (--verify-peers) — untrusted, L2-adjacent
 //
 // Built by `make fuzz-native` with amdclang++ -fsanitize=fuzzer,address,undefined (one binary
 // per target, selected by NETOP_FUZZ_TARGET at compile time).  Each target must never crash,
@@ -16,6 +17,7 @@
 #include <string>
 #include <vector>
 
+#include "netop/arp.hpp"
 #include "netop/dbus.hpp"
 #include "netop/l3.hpp"
 #include "netop/lldp.hpp"
@@ -67,6 +69,16 @@ extern "C" int LLVMFuzzerTestOneInput(const uint8_t* data, size_t size) {
     for (uint16_t flags : {uint16_t(NLM_F_ACK_TLVS), uint16_t(NLM_F_ACK_TLVS | NLM_F_CAPPED)}) {
         h->nlmsg_flags = flags;
         (void)nl::ext_ack_msg(h);
+    }
+#elif NETOP_FUZZ_TARGET == 5
+    auto r = arp::parse_reply(data, size);
+    if (r) {
+        // A reply always carries Ethernet/IPv4 sizes, op 2, and the addresses at their offsets.
+        if (size < arp::kPayloadLen || data[7] != 2 || Ipv4::from_net(data + 14) != r->sender_ip) __builtin_trap();
+    }
+    if (size >= 10) {  // requests from arbitrary addresses always encode to a fixed-size payload
+        auto req = arp::encode_request(MacAddr::from_bytes(data), Ipv4::from_net(data + 2), Ipv4::from_net(data + 6));
+        if (req.size() != arp::kPayloadLen || arp::parse_reply(req.data(), req.size())) __builtin_trap();
     }
 #else
 #error "define NETOP_FUZZ_TARGET"
