@@ -177,9 +177,11 @@ def test_two_operator_replicas_with_webhooks_fail_over():
     registered exactly as packaged (Service-routed, CA injected).  The stored policy carries the
     mutating webhook's defaults and an invalid one is refused.  Then the leader is SIGKILLed (no
     lease release) and the policy edited: the standby takes the lease after it expires, admits
-    the edit and rolls it out to the node."""
-    r = e2e.run_isolated(n_nics=2, mode="L3", seed=15, ha=True, update_mtu=0, teardown=True)
+    the edit and rolls it out to the node.  The policy also turns on ``verifyPeers``."""
+    r = e2e.run_isolated(n_nics=2, mode="L3", seed=15, ha=True, update_mtu=0, teardown=True,
+                         policy_kw={"verifyPeers": True})
     assert r["policy_to_all_good_s"] is not None, (r["agent_log"], r.get("operator_logs"))
+    assert "--verify-peers=2s" in r["agent_argv"]  # and the switch ports answered ARP
     assert r["defaulted_image"] == T.DEFAULT_AGENT_IMAGE
     assert r["bad_policy"]["status"] == 403 and "invalid node selector" in r["bad_policy"]["message"]
     f = r["failover"]
