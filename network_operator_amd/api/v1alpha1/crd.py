@@ -131,6 +131,8 @@ def openapi_schema() -> dict:
             "driverImage": {"description": "Optional NIC kernel-driver (KMD) container, run as a privileged init\n"
                                            "container before the agent; it must load the driver and exit 0.",
                             "type": "string"},
+            "verifyPeers": {"description": "L3: label only once every NIC's switch-side /30 address answers ARP.",
+                            "type": "boolean"},
         },
         "required": ["layer"],
     }

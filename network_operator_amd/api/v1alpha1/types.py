@@ -186,6 +186,7 @@ class HostNicSpec:
     interfaces: List[str] = field(default_factory=list)
     nicDrivers: List[str] = field(default_factory=list)
     driverImage: str = ""
+    verifyPeers: bool = False
     extra: Dict[str, Any] = field(default_factory=dict)
 
     def to_dict(self) -> dict:
@@ -201,6 +202,8 @@ class HostNicSpec:
             d["interfaces"] = list(self.interfaces)
         if self.nicDrivers:
             d["nicDrivers"] = list(self.nicDrivers)
+        if self.verifyPeers:
+            d["verifyPeers"] = True
         d.update(copy.deepcopy(self.extra))
         return d
 
@@ -210,7 +213,7 @@ class HostNicSpec:
         s = cls(layer=d.pop("layer", "") or "", mtu=int(d.pop("mtu", 0) or 0), image=d.pop("image", "") or "",
                 pullPolicy=d.pop("pullPolicy", "") or "", disableNetworkManager=bool(d.pop("disableNetworkManager", False)),
                 interfaces=list(d.pop("interfaces", []) or []), nicDrivers=list(d.pop("nicDrivers", []) or []),
-                driverImage=d.pop("driverImage", "") or "")
+                driverImage=d.pop("driverImage", "") or "", verifyPeers=bool(d.pop("verifyPeers", False)))
         s.extra = d
         return s
 

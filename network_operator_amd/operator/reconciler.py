@@ -243,6 +243,8 @@ def host_nic_agent_args(p: T.NetworkClusterPolicy) -> List[str]:
         args += ["--disable-networkmanager", "--nm-keyfile-dir=/etc/NetworkManager/conf.d"]
     if hn.layer == "L3":
         args.append(f"--wait={L3_WAIT}")
+        if hn.verifyPeers:
+            args.append(f"--verify-peers={VERIFY_PEERS_TIMEOUT}")
     if hn.interfaces:
         args.append("--interfaces=" + ",".join(hn.interfaces))
     if hn.nicDrivers:

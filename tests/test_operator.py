@@ -534,7 +534,7 @@ def test_agent_args_rail_tables_l3_only():
 def test_agent_args_verify_peers_l3_only():
     from network_operator_amd.api.v1alpha1 import crd as CRD
     from network_operator_amd.api.v1alpha1 import types as T
-    from network_operator_amd.operator.reconciler import agent_args
+    from network_operator_amd.operator.reconciler import agent_args, host_nic_agent_args
 
     p = T.new_policy("p", layer="L3")
     assert not any(a.startswith("--verify-peers") for a in agent_args(p))
@@ -545,6 +545,10 @@ def test_agent_args_verify_peers_l3_only():
     assert T.NetworkClusterPolicy.from_dict(d).spec.amdScaleOut.verifyPeers is True
     p.spec.amdScaleOut.layer = "L2"  # no /30 in L2: no peer address to ask
     assert not any(a.startswith("--verify-peers") for a in agent_args(p))
+    h = T.new_host_nic_policy("h", layer="L3", verifyPeers=True)
+    assert "--verify-peers=2s" in host_nic_agent_args(h)
+    assert T.NetworkClusterPolicy.from_dict(h.to_dict()).spec.hostNic.verifyPeers is True
+    assert CRD.validate(h.to_dict()) == []
 
 
 def test_fabric_validation_jobs_follow_ready_nodes_and_report_a_condition():
