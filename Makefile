@@ -6,12 +6,19 @@ IMG_AGENT    ?= amd/amd-network-linkdiscovery:0.1.0
 IMG_VALIDATION ?= amd/amd-network-validation:0.1.0
 
 KUBECTL ?= kubectl
+CONTAINER_TOOL ?= docker
+HELM ?= helm
+RELEASE_REGISTRY ?= ghcr.io/amd/network-operator
+# MI355X hosts are x86-64; the operator image is pure Python and builds for arm64 too.
+PLATFORMS ?= linux/amd64
 VERSION ?= 0.1.0
 BUNDLE_IMG ?= amd/amd-network-operator-bundle:v$(VERSION)
 
 .PHONY: all help build native hip test test-native test-netns test-gpu manifests deployments bench bench-node-ready bench-e2e \
         images sanitize tsan clean fmt vet lint fuzz run build-installer install uninstall deploy undeploy bundle \
-        bundle-build helm-package-chart fuzz-native check-hardening catalog-build catalog-push bundle-push
+        bundle-build helm-package-chart fuzz-native check-hardening catalog-build catalog-push bundle-push \
+        generate test-e2e lint-fix operator-image operator-push discover-image discover-push validation-image \
+        validation-push docker-buildx helm-update-dependencies helm-push-chart
 
 all: build
 
@@ -29,6 +36,9 @@ hip:
 
 test:                       ## everything that runs without a GPU
 	$(PYTHON) -m pytest tests -q -m "not gpu"
+
+test-e2e:                   ## end-to-end: operator + simulated kubelet/NFD + real agent in network namespaces
+	$(PYTHON) -m pytest tests/test_e2e.py tests/test_helm_install.py -v
 
 test-native:
 	network_operator_amd/_lib/bin/netop-unit-tests
@@ -58,6 +68,8 @@ manifests:                  ## regenerate the CRD and every generated kustomize 
 	$(PYTHON) -m network_operator_amd.api.v1alpha1.crd
 	$(PYTHON) -m network_operator_amd.packaging.manifests
 
+generate: manifests         ## alias: the CRD, webhook and RBAC manifests are generated from the Python types (no deepcopy codegen: copy.deepcopy)
+
 deployments:                ## render kustomize + Helm offline into deployments/
 	mkdir -p deployments
 	$(PYTHON) -c 'from network_operator_amd.testing.render import *; open("deployments/operator.yaml","w").write(dump_all(kustomize_build("config/operator/default")))'
@@ -85,6 +97,8 @@ vet:                        ## byte-compile Python, warnings-as-errors C++ build
 lint: vet                   ## vet + drift checks (CRD, generated manifests, rendered deployments)
 	$(PYTHON) -m network_operator_amd.packaging.manifests --check
 	$(PYTHON) -m pytest tests/test_packaging.py -q
+
+lint-fix: fmt manifests deployments  ## rewrite what lint checks: formatting, generated manifests, rendered deployments
 
 fuzz:                       ## property-based CR churn + LLDP / Port Description fuzzing
 	$(PYTHON) -m pytest tests/test_fuzz.py tests/test_native.py -q -k "fuzz or property or garbage or churn"
@@ -131,13 +145,42 @@ catalog-build:              ## build a catalog image containing $(BUNDLE_IMGS) (
 catalog-push:               ## push the catalog image
 	docker push $(CATALOG_IMG)
 
+helm-update-dependencies:   ## fetch the NFD subchart (needs helm and the network)
+	$(HELM) dependency update charts/network-operator
+
 helm-package-chart:         ## .charts/<chart>-<version>.tgz
 	$(PYTHON) -m network_operator_amd.packaging helm --out .charts
 
-images:
-	docker build -f build/Dockerfile.operator -t $(IMG_OPERATOR) .
-	docker build -f build/Dockerfile.linkdiscovery -t $(IMG_AGENT) .
-	docker build -f build/Dockerfile.validation -t $(IMG_VALIDATION) .
+helm-push-chart: helm-package-chart  ## push the packaged chart to oci://$(RELEASE_REGISTRY)
+	for c in .charts/*.tgz; do $(HELM) push $$c oci://$(RELEASE_REGISTRY) || exit 1; done
+
+images: operator-image discover-image validation-image  ## all three images
+
+operator-image:             ## control-plane image (distroless, nonroot)
+	$(CONTAINER_TOOL) build -f build/Dockerfile.operator -t $(IMG_OPERATOR) .
+
+operator-push:
+	$(CONTAINER_TOOL) push $(IMG_OPERATOR)
+
+discover-image:             ## node agent image (unit suite + hardening gate run in the build)
+	$(CONTAINER_TOOL) build -f build/Dockerfile.linkdiscovery -t $(IMG_AGENT) .
+
+discover-push:
+	$(CONTAINER_TOOL) push $(IMG_AGENT)
+
+validation-image:           ## fabric validation Job image (RCCL + HIP, gfx950)
+	$(CONTAINER_TOOL) build -f build/Dockerfile.validation -t $(IMG_VALIDATION) .
+
+validation-push:
+	$(CONTAINER_TOOL) push $(IMG_VALIDATION)
+
+# Multi-platform build and push of the operator image.  The Dockerfile already names its
+# stages' bases, so buildx only needs --platform; a throwaway builder keeps the host's default.
+docker-buildx:              ## build and push the operator image for $(PLATFORMS)
+	- $(CONTAINER_TOOL) buildx create --name amd-netop-builder
+	$(CONTAINER_TOOL) buildx use amd-netop-builder
+	- $(CONTAINER_TOOL) buildx build --push --platform=$(PLATFORMS) --tag $(IMG_OPERATOR) -f build/Dockerfile.operator .
+	- $(CONTAINER_TOOL) buildx rm amd-netop-builder
 
 clean:
 	rm -rf _build _build-asan _build-vet network_operator_amd/_lib deployments dist bundle bundle.Dockerfile .charts

@@ -318,3 +318,26 @@ def test_trivy_ignores_reference_rendered_files():
     assert sorted(caps["add"]) == ["NET_ADMIN", "NET_RAW"] and caps["drop"] == ["ALL"]
     hn = _by_kind(discovery_for(ROOT / "config/operator/samples/amd-host-nic.yaml"), "DaemonSet")[0]
     assert hn["spec"]["template"]["spec"]["containers"][0]["args"]
+
+
+# The developer-facing targets of the reference Makefile (Makefile:100-351), under the same names.
+# Tool-download targets (controller-gen, kustomize, envtest, golangci-lint, operator-sdk, opm) have
+# no counterpart: the manifests are generated by Python and the renderers are in-tree.
+REFERENCE_MAKE_TARGETS = ("manifests", "generate", "fmt", "vet", "test", "test-e2e", "lint", "lint-fix", "fuzz",
+                          "deployments", "build", "run", "operator-image", "operator-push", "discover-image",
+                          "docker-buildx", "build-installer", "install", "uninstall", "bundle", "bundle-build",
+                          "bundle-push", "catalog-build", "catalog-push", "helm-update-dependencies",
+                          "helm-package-chart", "helm-push-chart")
+
+
+def test_makefile_has_the_reference_targets():
+    """Every reference target exists and expands (make -n: nothing runs)."""
+    import shutil
+    import subprocess
+
+    if not shutil.which("make"):
+        pytest.skip("make not installed")
+    for t in REFERENCE_MAKE_TARGETS:
+        r = subprocess.run(["make", "-n", "-C", str(ROOT), t], capture_output=True, text=True)
+        assert r.returncode == 0, f"make -n {t}: {r.stderr}"
+        assert r.stdout.strip(), t
