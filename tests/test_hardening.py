@@ -2,6 +2,8 @@
 reference's checksec gate (reference build/Dockerfile.linkdiscovery:36-41,
 build/Dockerfile.operator:36-41), and the images' use of it."""
 
+import json
+import os
 import shutil
 import subprocess
 import sys
@@ -12,6 +14,8 @@ import pytest
 ROOT = Path(__file__).resolve().parent.parent
 sys.path.insert(0, str(ROOT / "tools"))
 import check_hardening as H  # noqa: E402
+
+from network_operator_amd.utils.paths import native_bin  # noqa: E402
 
 BIN = ROOT / "network_operator_amd" / "_lib" / "bin"
 
@@ -83,3 +87,72 @@ def test_operator_image_file_set_is_self_contained(tmp_path):
                        env={"PYTHONPATH": str(app), "PATH": "/usr/bin:/bin"}, capture_output=True, text=True,
                        timeout=120)
     assert r.returncode == 0 and "--policies-file" in r.stdout, r.stderr[-2000:]
+
+
+# What the agent image's runtime base (ubuntu:22.04) ships as shared libraries without any
+# apt install: libc6, libgcc-s1 and libstdc++6 are all in the minimal image (apt needs them).
+UBUNTU_BASE_LIBS = {"libc.so.6", "libm.so.6", "libstdc++.so.6", "libgcc_s.so.1", "ld-linux-x86-64.so.2",
+                    "libpthread.so.0", "libdl.so.2", "librt.so.1"}
+
+
+def _ldd(path):
+    """soname -> resolved path of every shared library `path` loads (ldd, transitive)."""
+    out = subprocess.run(["ldd", str(path)], capture_output=True, text=True, check=True).stdout
+    libs = {}
+    for line in out.splitlines():
+        parts = line.split()
+        if "=>" in parts and len(parts) >= 3 and parts[2].startswith("/"):
+            libs[parts[0]] = parts[2]
+        elif parts and parts[0].startswith("/"):  # the interpreter
+            libs[os.path.basename(parts[0])] = parts[0]
+    return libs
+
+
+@pytest.mark.skipif(not hasattr(os, "geteuid") or os.geteuid() != 0, reason="chroot needs root")
+def test_agent_image_runtime_stage_runs_in_its_own_rootfs(tmp_path):
+    """The agent image, without docker: a root filesystem holding exactly what the runtime stage
+    of build/Dockerfile.linkdiscovery copies, plus only the libraries its ubuntu:22.04 base ships.
+    The ENTRYPOINT must start there (--version) and do a real dry run (netlink link dump, sysfs
+    discovery, topology and status files) inside the chroot."""
+    import re
+
+    df = (ROOT / "build" / "Dockerfile.linkdiscovery").read_text()
+    final = df.rsplit("\nFROM ", 1)[1]
+    assert final.splitlines()[0].strip() == "ubuntu:22.04"
+    (copy,) = re.findall(r"^COPY --from=builder (.+)$", final, re.M)
+    *srcs, dest = copy.split()
+    entry = json.loads(re.search(r"^ENTRYPOINT (\[.*\])$", final, re.M).group(1))
+    root = tmp_path / "rootfs"
+    for s in srcs:
+        assert s.startswith("/out/bin/"), s
+        binary = native_bin(os.path.basename(s))
+        d = root / dest.lstrip("/")
+        d.mkdir(parents=True, exist_ok=True)
+        shutil.copy2(binary, d / binary.name)
+        libs = _ldd(binary)
+        assert set(libs) <= UBUNTU_BASE_LIBS, f"{binary.name} needs libraries the base image lacks: " \
+                                              f"{sorted(set(libs) - UBUNTU_BASE_LIBS)}"
+        for lib in libs.values():
+            t = root / lib.lstrip("/")
+            t.parent.mkdir(parents=True, exist_ok=True)
+            shutil.copy2(os.path.realpath(lib), t)
+    for lib64 in ("lib64",):  # the interpreter path the ELF names
+        if (Path("/") / lib64).is_symlink() and not (root / lib64).exists():
+            (root / lib64).symlink_to(os.readlink(Path("/") / lib64))
+    for d in ("tmp", "sys-empty", "var/lib/amd-network"):
+        (root / d).mkdir(parents=True, exist_ok=True)
+    env = {"PATH": "/usr/local/bin:/usr/bin:/bin", "SYSFS_ROOT": "/sys-empty/"}
+
+    def enter():  # in the child, before exec: the image's filesystem is all it can see
+        os.chroot(str(root))
+        os.chdir("/")
+
+    r = subprocess.run(entry + ["--version"], capture_output=True, text=True, timeout=30, env=env, preexec_fn=enter)
+    assert r.returncode == 0 and "0.1.0" in r.stdout, r.stderr
+    r = subprocess.run([*entry, "--dry-run", "--interfaces=lo", "--mode=L3", "--xgmi-expect=0",
+                        "--status-file=/var/lib/amd-network/status.json", "--rccl-topo=/var/lib/amd-network/topo.xml"],
+                       capture_output=True, text=True, timeout=60, env=env, preexec_fn=enter)
+    assert r.returncode == 0, r.stderr[-2000:]
+    st = json.loads((root / "var/lib/amd-network/status.json").read_text())
+    assert st["dry_run"] == "true" and [i["name"] for i in st["interfaces"]] == ["lo"]
+    assert (root / "var/lib/amd-network/topo.xml").read_text().startswith("<system")
