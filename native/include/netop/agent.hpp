@@ -229,9 +229,9 @@ class Agent {
     bool publish_label();
     void announce_all(uint16_t ttl);
     bool nic_healthy(const NicState& n) const;
-    // --verify-peers: ARP-probes the switch side of every NIC in `which`; returns how many did
-    // not answer (-1 when interrupted by stop_fd).
-    int verify_peers(const std::vector<NicState*>& which, int stop_fd);
+    // --verify-peers: ARP-probes the switch side of every NIC in `which` for up to `timeout_ns`;
+    // returns how many did not answer (-1 when interrupted by stop_fd).
+    int verify_peers(const std::vector<NicState*>& which, int64_t timeout_ns, int stop_fd);
 
     std::map<std::string, std::string> labels_extra_;
     int flaps_ = 0;

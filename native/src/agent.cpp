@@ -34,6 +34,11 @@ void sanitize(Config& c) {
     c.mode = m;
 }
 
+namespace {
+// Longest a --verify-peers re-probe may hold the monitor loop (see Agent::monitor).
+constexpr int64_t kMonitorVerifyNs = 250LL * 1000000;
+}  // namespace
+
 // ---------------------------------------------------------------------------
 // LLDP source over AF_PACKET
 // ---------------------------------------------------------------------------
@@ -1264,7 +1269,7 @@ void Agent::run(int stop_fd) {
             if (cfg_.verify_peers_ns > 0) {
                 std::vector<NicState*> all;
                 for (auto& n : nics_) all.push_back(&n);
-                const int bad = verify_peers(all, stop_fd);
+                const int bad = verify_peers(all, cfg_.verify_peers_ns, stop_fd);
                 mark("verify_peers");
                 if (bad < 0) {
                     NLOG_I("Interrupted while verifying the switch-side peers");
@@ -1358,7 +1363,7 @@ void Agent::announce_all(uint16_t ttl) {
     }
 }
 
-int Agent::verify_peers(const std::vector<NicState*>& which, int stop_fd) {
+int Agent::verify_peers(const std::vector<NicState*>& which, int64_t timeout_ns, int stop_fd) {
     std::vector<arp::Probe> probes;
     std::vector<NicState*> owners;
     for (NicState* n : which) {
@@ -1375,7 +1380,7 @@ int Agent::verify_peers(const std::vector<NicState*>& which, int stop_fd) {
     if (probes.empty()) return 0;
     bool finished = false;
     try {
-        finished = arp_probe(probes, cfg_.verify_peers_ns, cfg_.verify_peers_retry_ns, stop_fd);
+        finished = arp_probe(probes, timeout_ns, std::min(cfg_.verify_peers_retry_ns, timeout_ns), stop_fd);
     } catch (const std::exception& e) {
         for (NicState* n : owners) {
             n->peer_verified = false;
@@ -1402,7 +1407,7 @@ int Agent::verify_peers(const std::vector<NicState*>& which, int stop_fd) {
         n.peer_error = !p.error.empty() ? p.error
                                         : strfmt("peer %s did not answer ARP within %s (%d requests): is the switch port "
                                                  "addressed as its Port Description says?",
-                                                 p.peer.str().c_str(), format_go_duration(cfg_.verify_peers_ns).c_str(),
+                                                 p.peer.str().c_str(), format_go_duration(timeout_ns).c_str(),
                                                  p.requests);
         NLOG_W("interface '%s': %s", n.ifname.c_str(), n.peer_error.c_str());
     }
@@ -1525,12 +1530,15 @@ void Agent::monitor(int stop_fd) {
         }
         if (cfg_.mode == "L3" && cfg_.verify_peers_ns > 0 && mono_ns() >= next_verify) {
             // NICs whose peer has not answered (yet): a recovered link, a new /30, or a switch
-            // port still without its address.  Failed NICs are asked again a second later.
+            // port still without its address.  Failed NICs are asked again a second later.  The
+            // probe blocks this loop, so it is capped well below the start-up timeout: a switch
+            // answers ARP in microseconds, and a port that is still coming up gets the next round
+            // instead of delaying the other NICs' link and LLDP events by the whole --verify-peers.
             std::vector<NicState*> todo;
             for (auto& n : nics_)
                 if (n.configured && !n.peer_verified && n.link.up() && !n.degraded) todo.push_back(&n);
             if (!todo.empty()) {
-                const int bad = verify_peers(todo, stop_fd);
+                const int bad = verify_peers(todo, std::min(cfg_.verify_peers_ns, kMonitorVerifyNs), stop_fd);
                 if (bad < 0) return;
                 changed = true;
                 next_verify = bad > 0 ? mono_ns() + 1000000000LL : 0;

@@ -1181,7 +1181,9 @@ namespace {
 struct FakeArpSwitch {
     std::set<std::string> silent;
     std::vector<std::pair<std::string, std::string>> asked;  // (ifname, peer)
-    bool operator()(std::vector<arp::Probe>& ps, int64_t, int64_t, int) {
+    std::vector<int64_t> timeouts;                           // per probe_all call
+    bool operator()(std::vector<arp::Probe>& ps, int64_t timeout_ns, int64_t, int) {
+        timeouts.push_back(timeout_ns);
         for (auto& p : ps) {
             asked.push_back({p.ifname, p.peer.str()});
             p.requests = 3;
@@ -1283,4 +1285,35 @@ TEST(agent_monitor_reverifies_a_recovered_nic_before_relabelling) {
     CHECK(withdrawn);
     CHECK(held_back);
     CHECK(restored);
+}
+
+TEST(agent_monitor_reprobe_never_holds_the_loop_for_the_startup_timeout) {
+    // Start-up waits the whole --verify-peers for a port to answer; in monitor mode a silent
+    // peer is asked in short rounds so link and LLDP events on the other NICs are not delayed.
+    Fixture f;
+    f.cfg.monitor_tick_ns = 1000000;
+    f.cfg.verify_peers_ns = 2000000000;
+    Pipe stop;
+    FakeArpSwitch swi;
+    agent::Agent a(f.cfg, f.ops, f.all_valid(), f.nm());
+    a.arp_probe = [&](std::vector<arp::Probe>& ps, int64_t t, int64_t r, int s) { return swi(ps, t, r, s); };
+    a.on_monitor_tick = [&](int tick) {
+        auto& l = f.ops.links["ens1"];
+        if (tick == 1) {
+            swi.silent = {"ens1"};
+            l.flags &= ~unsigned(IFF_UP);
+            f.ops.events.push_back({false, l});
+        } else if (tick == 2) {
+            l.flags |= IFF_UP;
+            f.ops.events.push_back({false, l});
+        } else if (tick > 2 && swi.timeouts.size() >= 2) {
+            stop.fire();
+        } else if (tick > 5000) {
+            stop.fire();
+        }
+    };
+    a.run(stop.fd[0]);
+    CHECK(swi.timeouts.size() >= 2);
+    CHECK_EQ(swi.timeouts.front(), int64_t(2000000000));  // start-up: the configured timeout
+    for (size_t i = 1; i < swi.timeouts.size(); ++i) CHECK(swi.timeouts[i] <= 250000000);
 }
