@@ -30,7 +30,7 @@ import asyncio
 import copy
 import logging
 from pathlib import Path
-from typing import Dict, List, Optional
+from typing import List, Optional
 
 import yaml
 
