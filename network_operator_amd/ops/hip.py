@@ -11,7 +11,7 @@ from __future__ import annotations
 import ctypes
 import threading
 
-from ..utils.paths import hip_library
+from ..utils.paths import hip_library, native_bin
 
 _lib = None
 _lock = threading.Lock()
@@ -201,6 +201,22 @@ def xgmi_probe(nbytes: int = 256 << 20, iters: int = 10, max_gpus: int = 8) -> d
         "link_GBps": [[single[d * g + p] for p in range(g)] for d in range(g)],
         "aggregate_GBps": [agg[d] for d in range(g)],
     }
+
+
+def xgmi_probe_isolated(nbytes: int = 256 << 20, iters: int = 10, max_gpus: int = 8, timeout: float = 120) -> dict:
+    """``xgmi_probe`` + ``xgmi_probe_push`` in a child process (``netop-xgmi-probe``): the caller
+    keeps no context on the peer GPUs, and a fault or hang in the probe ends the child, not the
+    caller (bench.py's rank 0 still has to print its result).  Byte errors come back as data
+    (exit status 3), any other failure raises."""
+    import json
+    import subprocess
+
+    r = subprocess.run([str(native_bin("netop-xgmi-probe")), f"--bytes={nbytes}", f"--iters={iters}",
+                        f"--max-gpus={max_gpus}"], capture_output=True, text=True, timeout=timeout)
+    lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
+    if r.returncode not in (0, 3) or not lines:
+        raise RuntimeError(f"netop-xgmi-probe rc={r.returncode}: {r.stderr[-400:]}")
+    return json.loads(lines[-1])
 
 
 def xgmi_probe_push(nbytes: int = 256 << 20, iters: int = 10, max_gpus: int = 8) -> dict:

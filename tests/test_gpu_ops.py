@@ -160,6 +160,16 @@ def test_xgmi_allreduce_algorithm_virtual_ranks(cuda_device, ranks):
         assert r["bytes"] % (16 * ranks) == 0
 
 
+def test_xgmi_probe_isolated_matches_the_in_process_fields(cuda_device):
+    """bench.py runs the probe out of process (rank 0 must outlive a faulting probe)."""
+    from network_operator_amd.ops import hip
+
+    r = hip.xgmi_probe_isolated(32 << 20, iters=3, max_gpus=1, timeout=120)
+    assert r["gpus"] == 1 and r["errors"] == 0 and r["push_errors"] == 0
+    assert r["aggregate_GBps"][0] > 100 and r["push_aggregate_GBps"][0] > 100
+    assert len(r["link_GBps"]) == 1
+
+
 def test_xgmi_probe_push_loopback(cuda_device):
     from network_operator_amd.ops import hip
 
