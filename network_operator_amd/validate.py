@@ -18,7 +18,8 @@ these checks:
    "RCCL sees every link" check from BASELINE.json.
 5. **Direct xGMI all-reduce** (``parallel/xgmi_comm.py``).  The one-process-per-GPU
    all-reduce over HIP IPC buffers that jobs can use, every size checked exactly (after the
-   counter window, so check 4 still sees RCCL traffic only).
+   counter window, so check 4 still sees RCCL traffic only).  Without PyTorch (the validation
+   image) the native single-process harness runs the same algorithm instead.
 6. **Optionally, RCCL tuning** (``--tune-rccl``, n > 1).  The 1 GiB all-reduce under the
    knob variants of ``parallel/rccl_bench.ENV_PROBES``, each in a fresh process.  A variant
    that beats RCCL's defaults by at least 3 % is written to ``<artifact-dir>/rccl-tuned.env``,
@@ -51,6 +52,41 @@ LABEL_FILE = "gpu-fabric-validation.txt"
 
 def _check(name: str, ok: bool, **detail) -> dict:
     return {"check": name, "ok": bool(ok), **detail}
+
+
+def _have_torch() -> bool:
+    import importlib.util
+
+    return importlib.util.find_spec("torch") is not None
+
+
+def direct_all_reduce_check(gpus: int, max_bytes: int, timeout: float) -> dict:
+    """Check 5.  With PyTorch present it runs the way jobs run it (``parallel/xgmi_comm.py``: one
+    process per GPU, torch.distributed rendezvous, HIP IPC buffers).  The validation image is a
+    plain ROCm image without PyTorch; there the same two-shot algorithm runs from the native
+    single-process harness (``netop-xgmi-allreduce``: every GPU in one process, peer access),
+    still checked exactly, instead of failing the node for a missing Python package."""
+    try:
+        if _have_torch():
+            from .parallel import xgmi_comm
+
+            d = xgmi_comm.run(gpus, nbytes=max_bytes, min_bytes=1 << 20, iters=5, warmup=2, timeout=timeout)
+            return _check("xgmi_direct_all_reduce", d["wrong"] == 0, runner="xgmi_comm (one process per GPU)",
+                          peak_busbw_GBps=d["peak_busbw_GBps"], wrong=d["wrong"],
+                          sizes=[{k: r[k] for k in ("algo", "bytes", "time_us", "busbw_GBps")} for r in d["rows"]])
+        from .parallel import xgmi_allreduce as XA
+
+        rows = XA.run(ranks=gpus, min_bytes=min(1 << 20, max_bytes), max_bytes=max_bytes, factor=32, iters=5, warmup=2,
+                      timeout=timeout)
+        if not rows:
+            return _check("xgmi_direct_all_reduce", False, runner="netop-xgmi-allreduce", error="no result rows")
+        wrong = sum(int(r["wrong"]) for r in rows)
+        return _check("xgmi_direct_all_reduce", wrong == 0, runner="netop-xgmi-allreduce (one process, no PyTorch)",
+                      peak_busbw_GBps=max(float(r["busbw_GBps"]) for r in rows), wrong=wrong,
+                      sizes=[{"algo": r["mode"], "bytes": r["bytes"], "time_us": r["time_us"],
+                              "busbw_GBps": r["busbw_GBps"]} for r in rows])
+    except Exception as e:
+        return _check("xgmi_direct_all_reduce", False, error=str(e)[-500:])
 
 
 def topo_file_agrees(xml_text: str, topo) -> dict:
@@ -148,15 +184,7 @@ def run(gpus: int, min_busbw: float, min_link_GBps: float, max_bytes: int, sysfs
             checks.append(_check("xgmi_counters", False, error=str(e)))
 
     # 5. The direct xGMI all-reduce jobs can use (one process per GPU, HIP IPC buffers), exact.
-    try:
-        from .parallel import xgmi_comm
-
-        d = xgmi_comm.run(gpus, nbytes=max_bytes, min_bytes=1 << 20, iters=5, warmup=2, timeout=min(timeout, 300))
-        checks.append(_check("xgmi_direct_all_reduce", d["wrong"] == 0, peak_busbw_GBps=d["peak_busbw_GBps"],
-                             wrong=d["wrong"], sizes=[{k: r[k] for k in ("algo", "bytes", "time_us", "busbw_GBps")}
-                                                      for r in d["rows"]]))
-    except Exception as e:
-        checks.append(_check("xgmi_direct_all_reduce", False, error=str(e)[-500:]))
+    checks.append(direct_all_reduce_check(gpus, max_bytes, min(timeout, 300)))
     if tune_rccl and gpus > 1:
         try:
             from .parallel import rccl_bench

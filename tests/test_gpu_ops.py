@@ -231,6 +231,16 @@ def test_fabric_validation_single_gpu(cuda_device, tmp_path):
     assert (tmp_path / validate.LABEL_FILE).read_text().startswith(validate.LABEL + "=true\n")
 
 
+def test_fabric_validation_direct_check_without_pytorch(cuda_device, monkeypatch):
+    """Check 5 as the validation image runs it (no PyTorch): the native harness, exact."""
+    from network_operator_amd import validate
+
+    monkeypatch.setattr(validate, "_have_torch", lambda: False)
+    c = validate.direct_all_reduce_check(1, 64 << 20, 120)
+    assert c["ok"] and c["wrong"] == 0 and "no PyTorch" in c["runner"], c
+    assert [s["bytes"] for s in c["sizes"] if s["algo"] == "pull"][-1] <= 64 << 20
+
+
 @pytest.mark.parametrize("pairs,nbytes,wg", [(1, 16, 0), (3, 4096 + 16, 0), (7, 3 << 20, 0), (8, (5 << 20) + 48, 1)])
 def test_multi_copy_matches_torch(cuda_device, pairs, nbytes, wg):
     """One launch copying up to 8 pairs: sizes that need one, several and many workgroups per

@@ -341,3 +341,49 @@ def test_makefile_has_the_reference_targets():
         r = subprocess.run(["make", "-n", "-C", str(ROOT), t], capture_output=True, text=True)
         assert r.returncode == 0, f"make -n {t}: {r.stderr}"
         assert r.stdout.strip(), t
+
+
+def test_validation_direct_check_without_pytorch(monkeypatch):
+    """The validation image has no PyTorch: check 5 runs the native harness instead of failing."""
+    from network_operator_amd import validate as V
+    from network_operator_amd.parallel import xgmi_allreduce as XA
+
+    calls = []
+
+    def fake_run(**kw):
+        calls.append(kw)
+        return [{"mode": "pull", "bytes": 1 << 20, "time_us": 10.0, "busbw_GBps": 150.0, "wrong": 0},
+                {"mode": "push", "bytes": 1 << 30, "time_us": 9000.0, "busbw_GBps": 260.0, "wrong": 0}]
+
+    monkeypatch.setattr(V, "_have_torch", lambda: False)
+    monkeypatch.setattr(XA, "run", fake_run)
+    c = V.direct_all_reduce_check(8, 1 << 30, 300)
+    assert c["ok"] and c["peak_busbw_GBps"] == 260.0 and "no PyTorch" in c["runner"]
+    assert calls[0]["ranks"] == 8 and calls[0]["max_bytes"] == 1 << 30 and calls[0]["timeout"] == 300
+    monkeypatch.setattr(XA, "run", lambda **kw: [dict(fake_run(**kw)[0], wrong=5)])
+    c = V.direct_all_reduce_check(8, 1 << 30, 300)
+    assert not c["ok"] and c["wrong"] == 5
+    monkeypatch.setattr(XA, "run", lambda **kw: [])
+    assert not V.direct_all_reduce_check(8, 1 << 30, 300)["ok"]
+
+
+def test_validation_image_file_set_runs_without_pytorch(tmp_path):
+    """build/Dockerfile.validation copies the whole package onto a ROCm image without PyTorch or
+    any other third-party Python package: the entrypoint and every module a validation run
+    imports must load with those unimportable."""
+    import subprocess
+    import sys
+
+    df = (ROOT / "build" / "Dockerfile.validation").read_text()
+    final = df.rsplit("\nFROM ", 1)[1]
+    assert "pytorch" not in final.splitlines()[0].lower()
+    assert 'ENTRYPOINT ["python3", "-m", "network_operator_amd.validate"]' in final
+    block = ("import sys, runpy\n"
+             "for m in ('torch', 'numpy', 'yaml', 'aiohttp', 'prometheus_client'): sys.modules[m] = None\n"
+             "import network_operator_amd.models.topology, network_operator_amd.ops.smi, network_operator_amd.ops.hip\n"
+             "import network_operator_amd.parallel.rccl_bench, network_operator_amd.parallel.xgmi_allreduce\n"
+             "sys.argv = ['validate', '--help']\n"
+             "runpy.run_module('network_operator_amd.validate', run_name='__main__')")
+    r = subprocess.run([sys.executable, "-c", block], cwd=str(tmp_path), env={"PYTHONPATH": str(ROOT), "PATH": "/usr/bin:/bin"},
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "--tune-rccl" in r.stdout, r.stderr[-2000:]
