@@ -195,6 +195,10 @@ def torch_env_probe(world: int, nbytes: int, budget_s: float, device: str = "cud
     return out
 
 
+def autotune_file() -> str:
+    return f"/tmp/netop-rccl-autotune-{os.environ.get('MASTER_PORT', '0')}-{os.getppid()}.json"
+
+
 def _rccl_autotune(rank: int, world: int, nbytes: int, budget_s: float = 120.0,
                    started: float = time.time(), device: str = "cuda", variants=None) -> dict:
     """RCCL reads its parameters once per process, at communicator creation, so they must be
@@ -208,7 +212,10 @@ def _rccl_autotune(rank: int, world: int, nbytes: int, budget_s: float = 120.0,
     (``rccl_bench.choose_env``).  (The validation Job tunes a node's ``rccl.env`` the same way
     with the native harness, ``validate.py --tune-rccl``.)  It is still RCCL: only its documented
     environment changes."""
-    path = f"/tmp/netop-rccl-autotune-{os.environ.get('MASTER_PORT', '0')}.json"
+    # Keyed by the launcher's pid as well as the port: every rank of one run shares its parent
+    # (torchrun's agent or _spawn_ranks), so a file left by an earlier run on the same port
+    # (the driver's N = 2, 4, 8 runs back to back) can never hand this run another world's knobs.
+    path = autotune_file()
     if rank == 0:
         try:
             from network_operator_amd.parallel import rccl_bench
@@ -518,6 +525,11 @@ def main(argv=None) -> int:
         }
         print(json.dumps(line), flush=True)
     dist.destroy_process_group()
+    if rank == 0 and tuned is not None:
+        try:
+            os.unlink(autotune_file())
+        except OSError:
+            pass
     return 0 if verified else 1
 
 

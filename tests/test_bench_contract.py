@@ -184,3 +184,33 @@ def test_autotune_probe_runs_the_cuda_bench():
     out = bench.torch_env_probe(1, 1 << 20, budget_s=90, device="cuda", variants=[{}, {"NCCL_MIN_NCHANNELS": "64"}])
     assert [o.get("error") for o in out] == [None, None], out
     assert all(o["busbw_GBps"] == 0.0 and o["time_us"] > 0 for o in out)
+
+
+def test_autotune_handoff_ignores_another_runs_file(monkeypatch):
+    """The driver runs N = 2, 4, 8 back to back, possibly on one port: a non-zero rank must only
+    take the knobs its own rank 0 published (same launcher), never a fresh file of another run."""
+    import json as _json
+    import time as _time
+
+    sys.path.insert(0, str(ROOT))
+    import bench
+
+    monkeypatch.setenv("MASTER_PORT", str(_free_port()))
+    mine = bench.autotune_file()
+    other = mine.rsplit("-", 1)[0] + f"-{os.getppid() + 1}.json"
+    assert other != mine
+    try:
+        with open(other, "w") as f:
+            _json.dump({"chosen": {"NCCL_ALGO": "Tree"}, "created": _time.time()}, f)
+        monkeypatch.delenv("NCCL_ALGO", raising=False)
+        got = bench._rccl_autotune(1, 2, 1 << 20, budget_s=-299.5)  # waits 0.5 s
+        assert got["chosen"] == {} and "no autotune result" in got["error"]
+        assert "NCCL_ALGO" not in os.environ
+        with open(mine, "w") as f:
+            _json.dump({"chosen": {"NCCL_ALGO": "Ring"}, "created": _time.time()}, f)
+        got = bench._rccl_autotune(1, 2, 1 << 20, budget_s=-299.5)
+        assert got["chosen"] == {"NCCL_ALGO": "Ring"} and os.environ["NCCL_ALGO"] == "Ring"
+    finally:
+        for p in (mine, other):
+            if os.path.exists(p):
+                os.unlink(p)
