@@ -1138,6 +1138,17 @@ std::string Agent::render_metrics() const {
         for (const char* m : {"peermem", "dmabuf", "none"})
             o += strfmt("netop_agent_gpudirect_rdma{mode=\"%s\"} %d\n", m, gdr_.mode() == m ? 1 : 0);
     }
+    if (cfg_.mode == "L3" && cfg_.verify_peers_ns > 0) {
+        metric("netop_agent_peer_verified", "gauge", "1 when the NIC's switch-side /30 address answered ARP (--verify-peers)");
+        for (auto& n : nics_)
+            o += strfmt("netop_agent_peer_verified{nic=\"%s\"} %d\n", httpd::escape_label(n.ifname).c_str(),
+                        n.peer_verified ? 1 : 0);
+        metric("netop_agent_peer_arp_rtt_seconds", "gauge", "first ARP request to the peer's answer, last verification");
+        for (auto& n : nics_)
+            if (n.peer_verified)
+                o += strfmt("netop_agent_peer_arp_rtt_seconds{nic=\"%s\"} %.9f\n", httpd::escape_label(n.ifname).c_str(),
+                            double(n.peer_rtt_ns) / 1e9);
+    }
     if (cfg_.xgmi_expect_links >= 0) {
         metric("netop_agent_xgmi_pairs", "gauge", "GPU pairs with an xGMI link (KFD topology)");
         o += strfmt("netop_agent_xgmi_pairs{state=\"connected\"} %d\n", xgmi_.pairs_connected);

@@ -1214,6 +1214,9 @@ TEST(agent_verify_peers_all_answer) {
     CHECK(peers == (std::set<std::string>{"ens0=10.200.0.2", "ens1=10.200.0.6", "ens2=10.200.0.9"}));
     auto st = read_file(f.cfg.status_file);
     CHECK(st && st->find("\"peer_verified\":true") != std::string::npos && st->find("verify_peers") != std::string::npos);
+    const std::string m = a.render_metrics();
+    CHECK(m.find("netop_agent_peer_verified{nic=\"ens1\"} 1") != std::string::npos);
+    CHECK(m.find("netop_agent_peer_arp_rtt_seconds{nic=\"ens2\"} 0.000120000") != std::string::npos);
 }
 
 TEST(agent_verify_peers_silent_peer_blocks_readiness) {
@@ -1235,6 +1238,9 @@ TEST(agent_verify_peers_silent_peer_blocks_readiness) {
     CHECK(!path_exists(f.cfg.labels.path()));
     auto st = read_file(f.cfg.status_file);
     CHECK(st && st->find("\"peer_error\":\"peer 10.200.0.9 did not answer ARP") != std::string::npos);
+    const std::string m = a.render_metrics();
+    CHECK(m.find("netop_agent_peer_verified{nic=\"ens2\"} 0") != std::string::npos);
+    CHECK(m.find("netop_agent_peer_arp_rtt_seconds{nic=\"ens2\"}") == std::string::npos);
 }
 
 TEST(agent_verify_peers_off_by_default_asks_nothing) {
