@@ -57,6 +57,10 @@ def _agent_container() -> Dict:
                            "initialDelaySeconds": 1, "periodSeconds": 5, "failureThreshold": 1},
         "resources": {"limits": dict(AGENT_LIMITS), "requests": dict(AGENT_REQUESTS)},
         "volumeMounts": [{"mountPath": LABEL_FEATURES_DIR, "name": "nfd-features"}],
+        # A failed start ends with the agent's one-line "Error: ..." on stderr; with this policy the
+        # kubelet keeps the log tail as the container's termination message, and the operator
+        # quotes it in the policy's status.errors (not in the reference).
+        "terminationMessagePolicy": "FallbackToLogsOnError",
         "securityContext": {"allowPrivilegeEscalation": False, "readOnlyRootFilesystem": True,
                             "capabilities": {"drop": ["ALL"], "add": list(AGENT_CAPABILITIES)}},
     }

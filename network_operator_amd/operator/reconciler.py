@@ -334,6 +334,24 @@ def _set_condition(conds: List[dict], type_: str, status: str, reason: str, mess
                   "reason": reason, "message": message})
 
 
+def agent_exit_reason(pod: dict, limit: int = 300) -> Optional[str]:
+    """Why the agent container last exited, from the Pod's container status: the agent's own
+    one-line "Error: ..." from the termination message (the DaemonSet sets
+    FallbackToLogsOnError, so that is the log tail of a failed start), else the exit code."""
+    for cs in (pod.get("status", {}) or {}).get("containerStatuses") or []:
+        t = (cs.get("state") or {}).get("terminated") or (cs.get("lastState") or {}).get("terminated")
+        if not t:
+            continue
+        lines = [ln.strip() for ln in (t.get("message") or "").splitlines() if ln.strip()]
+        fatal = [ln[len("Error: "):] for ln in lines if ln.startswith("Error: ")]
+        if fatal:
+            return fatal[-1][:limit]
+        code = t.get("exitCode")
+        if code:
+            return f"agent exited with code {code}" + (f" ({t['reason']})" if t.get("reason") not in (None, "Error") else "")
+    return None
+
+
 def policy_conditions(current: List[dict], targets: int, ready: int, errors: List[str], generation: int,
                       now: Optional[str] = None) -> List[dict]:
     """The policy's Ready / Degraded conditions (additive to the reference's state string,
@@ -479,7 +497,9 @@ class NetworkClusterPolicyReconciler:
             if ready.get("status") == "True":
                 continue
             node = pod.get("spec", {}).get("nodeName") or pod["metadata"]["name"]
-            errs.append(f"{node}: scale-out not ready ({ready.get('reason') or pod.get('status', {}).get('phase', 'Pending')})")
+            err = f"{node}: scale-out not ready ({ready.get('reason') or pod.get('status', {}).get('phase', 'Pending')})"
+            why = agent_exit_reason(pod)
+            errs.append(f"{err}: {why}" if why else err)
         if len(errs) > limit:
             errs = errs[:limit] + [f"... and {len(errs) - limit} more"]
         return errs

@@ -389,6 +389,13 @@ async def _scenario(tmp: Path, n_nics: int, mode: str, seed: int, interval: str,
                 t1 = time.monotonic()
                 c0.proc.kill()
                 t_unready = await _until(lambda: not all_good(), 10)
+
+                def crash_errors():
+                    return [e for e in ((fake.get_object(P, name) or {}).get("status") or {}).get("errors") or []
+                            if "exited with code" in e]
+
+                await _until(lambda: bool(crash_errors()), 5)
+                res["crash_status_errors"] = crash_errors()
                 t_back = await _until(lambda: len(c0.started_at) == 2 and c0.ready and all_good()
                                       and node.node_labels().get(label_key) == "true", 30)
                 res["crash_to_unready_s"] = round(t_unready - t1, 6) if t_unready else None

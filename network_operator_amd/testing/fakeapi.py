@@ -188,6 +188,8 @@ class FakeApiServer:
         # API groups of add-ons installed in the fake cluster (e.g. "nfd.k8s-sigs.io").
         self.extra_groups: List[str] = list(extra_groups or [])
         self.node_ready: Dict[Tuple[str, str], bool] = {}   # (ds ns/name, node) -> ready
+        # (ds ns/name, node) -> the agent container's restartCount and lastState.terminated
+        self.node_last_exit: Dict[Tuple[str, str], dict] = {}
         self.tokens: Dict[str, dict] = {}                    # bearer -> {"username", "groups", "allowed"}
         self.faults: List[_Fault] = []
         self.requests: List[Tuple[str, str]] = []
@@ -252,11 +254,19 @@ class FakeApiServer:
         self._store(kube.NODES, new, "MODIFIED")
         self._sync_daemonsets()
 
-    def set_agent_ready(self, node: str, ready: bool = True, daemonset: Optional[str] = None) -> None:
-        """Simulates the agent pod's readinessProbe on `node` (all DaemonSets if none given)."""
+    def set_agent_ready(self, node: str, ready: bool = True, daemonset: Optional[str] = None,
+                        terminated: Optional[dict] = None) -> None:
+        """Simulates the agent pod's readinessProbe on `node` (all DaemonSets if none given).
+        `terminated` ({exitCode, reason, message}) is what the kubelet records when the agent
+        container exits: it becomes the container's ``lastState.terminated`` and the restart
+        count goes up."""
         for (ns, name), _ in self._table(kube.DAEMONSETS).items():
             if daemonset is None or daemonset in (name, f"{ns}/{name}"):
                 self.node_ready[(f"{ns}/{name}", node)] = ready
+                if terminated is not None:
+                    prev = self.node_last_exit.get((f"{ns}/{name}", node), {})
+                    self.node_last_exit[(f"{ns}/{name}", node)] = {
+                        "restartCount": prev.get("restartCount", -1) + 1, "terminated": dict(terminated)}
         self._sync_daemonsets()
 
     def set_job_result(self, name: str, namespace: str, succeeded: bool) -> None:
@@ -362,6 +372,7 @@ class FakeApiServer:
             self._bg.append(asyncio.ensure_future(self._collect_later(uid)))
         if res == kube.DAEMONSETS:
             self.node_ready = {k: v for k, v in self.node_ready.items() if k[0] != f"{namespace}/{name}"}
+            self.node_last_exit = {k: v for k, v in self.node_last_exit.items() if k[0] != f"{namespace}/{name}"}
         return obj
 
     async def _collect_later(self, uid: str) -> None:
@@ -414,6 +425,12 @@ class FakeApiServer:
             cond = [{"type": "Ready", "status": "True" if ready else "False",
                      **({} if ready else {"reason": "ContainersNotReady",
                                           "message": "containers with unready status: [configurator]"})}]
+            status = {"phase": "Running", "conditions": cond}
+            last = self.node_last_exit.get((f"{ns}/{name}", node))
+            if last:
+                cname = ((ds["spec"]["template"].get("spec") or {}).get("containers") or [{}])[0].get("name", "agent")
+                status["containerStatuses"] = [{"name": cname, "ready": ready, "restartCount": last["restartCount"],
+                                                "lastState": {"terminated": last["terminated"]}}]
             cur = pods.get((ns, pname))
             labels = dict((ds["spec"]["template"].get("metadata") or {}).get("labels") or {})
             if cur is None:
@@ -421,11 +438,11 @@ class FakeApiServer:
                        "metadata": {"name": pname, "namespace": ns, "labels": labels,
                                     "ownerReferences": [{"apiVersion": "apps/v1", "kind": "DaemonSet", "name": name,
                                                          "uid": ds["metadata"]["uid"], "controller": True}]},
-                       "spec": {"nodeName": node}, "status": {"phase": "Running", "conditions": cond}}
+                       "spec": {"nodeName": node}, "status": status}
                 self._create(kube.PODS, pod, ns)
-            elif cur.get("status", {}).get("conditions") != cond:
+            elif cur.get("status") != status:
                 new = copy.deepcopy(cur)
-                new["status"]["conditions"] = cond
+                new["status"] = status
                 self._store(kube.PODS, new, "MODIFIED")
 
     async def _auto_ready(self, ds_key: str, node: str) -> None:

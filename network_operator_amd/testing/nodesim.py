@@ -68,6 +68,8 @@ class _Container:
     started_at: List[float] = field(default_factory=list)
     inits: List[dict] = field(default_factory=list)  # {"name", "image", "argv"} in order
     inits_done: bool = False
+    log_start: int = 0               # size of the log file when the current run started
+    fallback_to_logs: bool = False   # terminationMessagePolicy: FallbackToLogsOnError
 
 
 class SimNode:
@@ -164,7 +166,8 @@ class SimNode:
                           argv=self._agent_argv(list(c.get("command") or [])[1:] + list(c.get("args") or []), mounts),
                           probe=self._agent_argv(probe[1:], mounts) if probe else None, env=env,
                           grace_s=float(spec.get("terminationGracePeriodSeconds", 30)),
-                          log_path=logs / f"{pname}.log", inits=inits, inits_done=not inits)
+                          log_path=logs / f"{pname}.log", inits=inits, inits_done=not inits,
+                          fallback_to_logs=c.get("terminationMessagePolicy") == "FallbackToLogsOnError")
 
     def _env(self, c: _Container) -> Dict[str, str]:
         env = dict(os.environ, **self.extra_env, **c.env)
@@ -192,6 +195,7 @@ class SimNode:
     def _start(self, c: _Container) -> None:
         env = self._env(c)
         with open(c.log_path, "ab") as f:
+            c.log_start = f.tell()
             c.proc = subprocess.Popen(c.argv, env=env, stdout=f, stderr=subprocess.STDOUT,
                                       preexec_fn=self.netns.enter if self.netns else None)
         c.started_at.append(time.monotonic())
@@ -223,6 +227,23 @@ class SimNode:
         if c.ready != ready:
             c.ready = ready
             self.fake.set_agent_ready(self.name, ready, daemonset=c.daemonset)
+
+    def _terminated(self, c: _Container) -> dict:
+        """``lastState.terminated`` as the kubelet records it: the exit code (128 + signal for a
+        killed process) and, under FallbackToLogsOnError after a failure, the log tail of this
+        run (at most 80 lines and 2048 bytes, whichever is smaller)."""
+        rc = c.proc.returncode if c.proc else 0
+        code = 128 - rc if rc < 0 else rc
+        out = {"exitCode": code, "reason": "Completed" if code == 0 else "Error"}
+        if code != 0 and c.fallback_to_logs:
+            try:
+                with open(c.log_path, "rb") as f:
+                    f.seek(c.log_start)
+                    tail = f.read()[-2048:]
+            except OSError:
+                tail = b""
+            out["message"] = "\n".join(tail.decode(errors="replace").splitlines()[-80:])
+        return out
 
     async def _kubelet(self) -> None:
         while not self._stop.is_set():
@@ -257,7 +278,8 @@ class SimNode:
                 elif c.proc.poll() is not None:  # crashed: restartPolicy Always
                     if c.next_start == 0.0:
                         self._record_exit(c)
-                        self._set_ready(c, False)
+                        c.ready = False
+                        self.fake.set_agent_ready(self.name, False, daemonset=c.daemonset, terminated=self._terminated(c))
                         c.next_start = time.monotonic() + c.backoff
                         c.backoff = min(c.backoff * 2, 5.0)
                     elif time.monotonic() >= c.next_start:

@@ -140,6 +140,8 @@ def test_agent_killed_is_restarted_and_the_node_recovers():
     r = e2e.run_isolated(n_nics=4, mode="L3", seed=12, crash_agent=True)
     assert r["crash_to_unready_s"] is not None and r["crash_to_all_good_s"] is not None, r["agent_log"]
     assert r["agent_restarts"] == 1
+    # the kubelet's record of the exit reaches the policy: SIGKILL is exit code 128 + 9
+    assert r["crash_status_errors"] == ["mi355x-0: scale-out not ready (ContainersNotReady): agent exited with code 137"]
     m = r["operator_metrics_after_crash"]
     assert m['amd_network_operator_agent_unready_total{policy="scale-out"}'] == 1
     assert m['amd_network_operator_agent_ready_seconds_count{policy="scale-out"}'] == 2

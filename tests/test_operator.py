@@ -612,3 +612,23 @@ def test_fabric_validation_jobs_follow_ready_nodes_and_report_a_condition():
             await client.replace(kube.NETWORKCLUSTERPOLICIES, cur)
             await eventually(lambda: cond() is None and not fake.list_objects(kube.JOBS))
     run(body())
+
+
+def test_agent_exit_reason_quotes_the_agents_error_line():
+    """The DaemonSet keeps a failed agent's log tail as its termination message
+    (FallbackToLogsOnError); the policy's errors quote the agent's "Error: ..." line."""
+    from network_operator_amd import discovery
+    from network_operator_amd.operator.reconciler import agent_exit_reason
+
+    c = discovery.discovery_daemonset()["spec"]["template"]["spec"]["containers"][0]
+    assert c["terminationMessagePolicy"] == "FallbackToLogsOnError"
+    msg = ("I1017 00:31:06.157259 3794 agent.cpp:1040] xGMI: 8 GPUs\n"
+           "W1017 00:31:08.1 3794 agent.cpp:1407] interface 'ens2': peer 10.200.0.9 did not answer ARP\n"
+           "Error: 1 of 8 switch-side peers did not answer ARP (ens2: peer 10.200.0.9 did not answer ARP)\n")
+    pod = {"status": {"containerStatuses": [{"name": "configurator", "restartCount": 3, "lastState": {
+        "terminated": {"exitCode": 1, "reason": "Error", "message": msg}}}]}}
+    assert agent_exit_reason(pod) == "1 of 8 switch-side peers did not answer ARP (ens2: peer 10.200.0.9 did not answer ARP)"
+    pod["status"]["containerStatuses"][0]["lastState"]["terminated"] = {"exitCode": 137, "reason": "OOMKilled"}
+    assert agent_exit_reason(pod) == "agent exited with code 137 (OOMKilled)"
+    assert agent_exit_reason({"status": {"containerStatuses": [{"name": "configurator", "ready": False}]}}) is None
+    assert agent_exit_reason({"status": {}}) is None
