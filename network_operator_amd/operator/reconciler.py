@@ -651,6 +651,9 @@ class NetworkClusterPolicyReconciler:
             raise
         if cur.state != new_state and new_state == STATE_ALL_GOOD:
             await self._event(raw, "Normal", "AllNodesReady", f"{ready}/{targets} nodes configured")
+        for e in errors:  # an agent that exited, with its reason: once per new message
+            if e not in cur.errors and "scale-out not ready (" in e and "): " in e:
+                await self._event(raw, "Warning", "AgentFailed", e[:1024])
         return Result()
 
     # -- entry point -------------------------------------------------------------------------------

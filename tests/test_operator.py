@@ -632,3 +632,27 @@ def test_agent_exit_reason_quotes_the_agents_error_line():
     assert agent_exit_reason(pod) == "agent exited with code 137 (OOMKilled)"
     assert agent_exit_reason({"status": {"containerStatuses": [{"name": "configurator", "ready": False}]}}) is None
     assert agent_exit_reason({"status": {}}) is None
+
+
+def test_agent_exit_reason_reaches_status_and_events():
+    async def body():
+        async with cluster(openshift=False) as (fake, client, ctl):
+            fake.add_node("gpu-node-0", {"foo": "bar"})
+            await client.create(kube.NETWORKCLUSTERPOLICIES, policy())
+            await eventually(lambda: fake.get_object(kube.NETWORKCLUSTERPOLICIES, "policy")["status"]["targets"] == 1)
+            fake.set_agent_ready("gpu-node-0", False, terminated={
+                "exitCode": 1, "reason": "Error",
+                "message": "E1017 agent.cpp:1283] boom\nError: No LLDP peers with a /30 Port Description were found\n"})
+            want = ("gpu-node-0: scale-out not ready (ContainersNotReady): "
+                    "No LLDP peers with a /30 Port Description were found")
+
+            def reported():
+                assert fake.get_object(kube.NETWORKCLUSTERPOLICIES, "policy")["status"]["errors"] == [want]
+                ev = [e for e in fake.list_objects(kube.EVENTS) if e["reason"] == "AgentFailed"]
+                assert len(ev) == 1 and ev[0]["type"] == "Warning" and ev[0]["message"] == want
+            await eventually(reported)
+            pod = [p for p in fake.list_objects(kube.PODS)][0]
+            assert pod["status"]["containerStatuses"][0]["restartCount"] == 0
+            fake.set_agent_ready("gpu-node-0")
+            await eventually(lambda: fake.get_object(kube.NETWORKCLUSTERPOLICIES, "policy")["status"]["errors"] == [])
+    run(body())
