@@ -1,26 +1,42 @@
 #!/usr/bin/env python3
-"""Headline benchmark: RCCL all-reduce bus bandwidth on MI355X (+ node-ready latency).
+"""Headline benchmark: RCCL all-reduce bus bandwidth on MI355X *with the operator's artifacts
+applied* (+ node-ready latency).
 
 BASELINE.json metric: "node scale-out-ready latency (s) + rccl all-reduce busbw GB/s at
 1/2/4/8 GPU", config "L3 mode, 8xMI355X single node: all xGMI + host RoCE links configured,
 rccl-tests 8-GPU all-reduce".
 
+* **What is measured is the configured fabric, not stock RCCL.**  Before any rank creates an
+  RCCL communicator, rank 0 runs the node agent itself, unprivileged, on this node
+  (``discover --dry-run --rccl-topo=… --rccl-env=…``: its ``NCCL_TOPO_FILE`` and the
+  intra-node part of ``rccl.env``), and hands the files to every rank through the rendezvous
+  store; every rank exports them, and rank 0 also sets ``NCCL_TOPO_DUMP_FILE``.  The reference's
+  node artifact exists for the collective library in the same way (HCCL reads gaudinet.json,
+  reference cmd/discover/gaudinet.go:28-89).  ``--artifacts DIR`` applies an existing artifact
+  directory instead (``rccl.env`` + ``rccl-tuned.env``, e.g. /etc/amd/scale-out on a configured
+  node); ``--artifacts off`` runs RCCL's defaults.
 * One process per GPU, ``torch.distributed`` backend ``nccl`` (= RCCL over xGMI on ROCm).
   Under ``torchrun --nproc-per-node N`` the launcher's ranks are used (WORLD_SIZE must equal
   ``--gpus``); a bare ``python bench.py --gpus N`` starts the N rank processes itself.
-  ``config.model`` names the BASELINE.json config of the world size that actually ran.  A *step* is one in-place bf16 all-reduce of
-  ``--bytes`` per rank (default 1 GiB, rccl-tests' large-message regime); ``--warmup``
-  untimed steps, then exactly ``--steps`` timed steps bracketed by barrier +
-  ``torch.cuda.synchronize()``, max over ranks.
-* ``value`` is busbw = algbw * 2(n-1)/n (rccl-tests definition, per rank;
-  ``aggregate_busbw_GBps`` is n times that).  At n = 1 there are no links and busbw is 0 by
-  definition; the single-rank all-reduce is a no-op, so algbw is reported as null with the
-  reason and ``node_ready_gpu_side`` times the agent phases that run unprivileged on the box.
-* Before timing, the result of one all-reduce of rank-specific patterns is verified exactly
-  with the HIP kernels in ``libnetop_hip.so`` (fails loudly if the library is missing).
-* The node-ready latency half of the metric needs a private network namespace (root /
-  user namespaces + AF_PACKET); it runs with ``--node-ready`` where that is available and is
-  reported as null with the reason otherwise (the GPU pool's boxes run unprivileged).
+  ``config.model`` names the BASELINE.json config of the world size that actually ran.  A
+  *step* is one in-place bf16 all-reduce of ``--bytes`` per rank (default 1 GiB, rccl-tests'
+  large-message regime); ``--warmup`` untimed steps, then exactly ``--steps`` timed steps
+  bracketed by barrier + ``torch.cuda.synchronize()``, max over ranks.
+* ``value`` is busbw = algbw * 2(n-1)/n (rccl-tests definition, per rank) with the artifacts
+  applied; ``busbw_rccl_defaults_GBps`` is the same loop in fresh rank processes without them.
+  ``agent_artifacts`` says what was applied (file bytes, per-rank record) and what RCCL made of
+  it (its dump: xGMI links seen per GPU — n-1 expected — and GPU / NIC ancestry vs the file's).
+  At n > 1 the run exits non-zero (after printing its line) when RCCL sees fewer xGMI links
+  under the file than n-1 (or than without it).
+* Order and deadline: verification and the timed loop come first; every diagnostic after it
+  (RCCL defaults, xGMI probe, native harness, direct / IPC all-reduce, netns node-ready) is a
+  child process killed at ``--deadline-s`` (``parallel/bench_extras.py``), and a watchdog in
+  rank 0 prints the line with whatever was measured when the deadline passes.  Exactly one JSON
+  line, always.
+* At n = 1 there are no links and busbw is 0 by definition; the single-rank all-reduce is a
+  no-op, so algbw is reported as null with the reason, and ``node_ready_gpu_side`` times the
+  agent phases that run unprivileged on the box.  The netns node-ready harness needs a private
+  network namespace and is reported null with the reason where that is unavailable.
 * Data are synthetic (RCCL moves the same bytes whatever their values).
 """
 
@@ -29,11 +45,17 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import shutil
 import socket
 import sys
+import tempfile
+import threading
 import time
 
 METRIC = "node scale-out-ready latency (s) + rccl all-reduce busbw GB/s at 1/2/4/8 GPU"
+STORE_KEY = "netop/bench/artifacts"
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 
 def config_name(n: int) -> str:
@@ -55,11 +77,12 @@ def _free_port() -> int:
     return p
 
 
-def _spawn_ranks(n: int, argv: list[str], device: str) -> int:
+def _spawn_ranks(n: int, argv: list[str], device: str, deadline: float) -> int:
     """``python bench.py --gpus N`` without a launcher: start N rank processes (one per GPU,
     torchrun-style env) and wait for them.  This process never touches the GPU (counting devices
     does not initialise HIP on this image), so the ranks are ordinary children, not an exec.
-    Only rank 0 prints the JSON line; if any rank fails the others are stopped."""
+    Only rank 0 prints the JSON line; if any rank fails the others are stopped, and ranks still
+    alive 30 s after the deadline (rank 0's watchdog has printed by then) are killed."""
     import signal
     import subprocess
 
@@ -71,30 +94,34 @@ def _spawn_ranks(n: int, argv: list[str], device: str) -> int:
             print(f"bench.py --gpus {n}: only {have} GPU(s) visible", file=sys.stderr)
             return 2
     port = _free_port()
-    procs = []
+    procs = {}
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                    GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env))
-    rc = 0
+        procs[r] = subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env)
+    rc, killed = 0, set()
     try:
         while procs:
-            for p in list(procs):
+            for r, p in list(procs.items()):
                 code = p.poll()
                 if code is None:
                     continue
-                procs.remove(p)
-                if code != 0 and rc == 0:
+                del procs[r]
+                if code != 0 and rc == 0 and r not in killed:
                     rc = code if code > 0 else 128 - code
-                    for q in procs:  # one rank died: the rest would hang in the next collective
+                    for q in procs.values():  # one rank died: the rest would hang in the next collective
                         q.send_signal(signal.SIGTERM)
+            if procs and time.monotonic() > deadline + 30:
+                for r, q in procs.items():
+                    killed.add(r)
+                    q.kill()
             time.sleep(0.05)
     except KeyboardInterrupt:
-        for q in procs:
+        for q in procs.values():
             q.send_signal(signal.SIGTERM)
         raise
     finally:
-        for q in procs:
+        for q in procs.values():
             try:
                 q.wait(30)
             except subprocess.TimeoutExpired:
@@ -108,8 +135,6 @@ def node_ready_gpu_side(sysfs: str = "/sys/") -> dict:
     and the RCCL artifacts (rccl.env + NCCL_TOPO_FILE XML) and NFD label written to a scratch
     directory.  A component of node-ready latency, not the metric: link-up, LLDP and the netlink
     writes need NET_ADMIN/NET_RAW and run in the netns harness (``--node-ready``)."""
-    import tempfile
-
     from network_operator_amd.agent import native
 
     m = native()
@@ -153,44 +178,35 @@ _LAUNCH_ENV = ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RA
                "MASTER_ADDR", "MASTER_PORT")
 
 
+def _probe_cmd(world: int, nbytes: int, steps: int, device: str, warmup: int = 2) -> list:
+    """bench.py as a bare measurement of the timed loop: every extra and diagnostic off."""
+    return [sys.executable, os.path.abspath(__file__), "--gpus", str(world), "--steps", str(steps), "--warmup",
+            str(warmup), "--bytes", str(nbytes), "--sweep", "", "--collectives", "", "--node-ready", "off",
+            "--xgmi-probe", "0", "--native-rccl", "0", "--xgmi-allreduce", "0", "--rccl-autotune", "0",
+            "--gpu-side", "0", "--rccl-defaults", "0", "--device", device]
+
+
 def torch_env_probe(world: int, nbytes: int, budget_s: float, device: str = "cuda", variants=None,
                     steps: int = 5) -> list:
     """busbw of the timed loop itself (torch.distributed, this torch's RCCL, bf16, `nbytes`) under
     each RCCL knob variant of ``rccl_bench.ENV_PROBES``: bench.py runs again in a fresh set of
     `world` rank processes per variant, with the variant in its environment and every extra
     measurement off.  Variants not started within `budget_s` are reported as skipped.  A hung
-    variant is killed with its whole process group (its ranks hold GPUs)."""
-    import signal
-    import subprocess
+    variant is killed with its whole process tree (its ranks hold GPUs)."""
+    from network_operator_amd.parallel import bench_extras, rccl_bench
 
-    from network_operator_amd.parallel import rccl_bench
-
-    base = {k: v for k, v in os.environ.items() if k not in _LAUNCH_ENV and not k.startswith("TORCHELASTIC_")}
+    runner = bench_extras.Runner(time.monotonic() + budget_s + 30, margin_s=0)
     out = []
     t0 = time.monotonic()
     for extra in (variants if variants is not None else rccl_bench.ENV_PROBES):
-        left = budget_s - (time.monotonic() - t0)
-        if left <= 0:
+        if budget_s - (time.monotonic() - t0) <= 0:
             out.append({"env": extra, "skipped": "time budget spent"})
             continue
-        cmd = [sys.executable, os.path.abspath(__file__), "--gpus", str(world), "--steps", str(steps), "--warmup", "2",
-               "--bytes", str(nbytes), "--sweep", "", "--collectives", "", "--node-ready", "off", "--xgmi-probe", "0",
-               "--native-rccl", "0", "--xgmi-allreduce", "0", "--rccl-autotune", "0", "--gpu-side", "0",
-               "--device", device]
-        p = subprocess.Popen(cmd, env=dict(base, **extra), stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
-                             start_new_session=True)
-        try:
-            so, se = p.communicate(timeout=left + 30)
-        except subprocess.TimeoutExpired:
-            os.killpg(p.pid, signal.SIGKILL)
-            p.communicate()
-            out.append({"env": extra, "error": "timed out"})
+        j = runner.run("autotune", _probe_cmd(world, nbytes, steps, device) + ["--artifacts", "off"],
+                       cap_s=budget_s + 30, env=extra)
+        if "error" in j:
+            out.append({"env": extra, "error": j["error"] if j["error"] != "deadline" else "timed out"})
             continue
-        lines = [x for x in so.splitlines() if x.startswith("{")]
-        if p.returncode != 0 or not lines:
-            out.append({"env": extra, "error": f"rc={p.returncode}: {se[-300:]}"})
-            continue
-        j = json.loads(lines[-1])
         out.append({"env": extra, "busbw_GBps": j["busbw_GBps"], "time_us": j["ms_per_step"] * 1e3})
     return out
 
@@ -201,17 +217,16 @@ def autotune_file() -> str:
 
 def _rccl_autotune(rank: int, world: int, nbytes: int, budget_s: float = 120.0,
                    started: float = time.time(), device: str = "cuda", variants=None) -> dict:
-    """RCCL reads its parameters once per process, at communicator creation, so they must be
-    chosen before init_process_group.
+    """Opt-in (``--rccl-autotune 1``).  RCCL reads its parameters once per process, at
+    communicator creation, so they must be chosen before init_process_group.
 
     Rank 0 measures the knob variants of ``rccl_bench.ENV_PROBES`` with bench.py itself
     (``torch_env_probe``: the same torch, RCCL build, dtype and message as the timed loop) over
     the node's first `world` GPUs.  Each variant runs in fresh processes, and all of them must
     fit in ``budget_s``.  Rank 0 publishes the winner through a file in /tmp keyed by the
     rendezvous port, and every rank exports it.  A variant must beat the defaults by >= 3 %
-    (``rccl_bench.choose_env``).  (The validation Job tunes a node's ``rccl.env`` the same way
-    with the native harness, ``validate.py --tune-rccl``.)  It is still RCCL: only its documented
-    environment changes."""
+    (``rccl_bench.choose_env``).  On a node, the validation Job tunes ``rccl-tuned.env`` the
+    same way (``validate.py --tune-rccl``) and ``--artifacts DIR`` applies it."""
     # Keyed by the launcher's pid as well as the port: every rank of one run shares its parent
     # (torchrun's agent or _spawn_ranks), so a file left by an earlier run on the same port
     # (the driver's N = 2, 4, 8 runs back to back) can never hand this run another world's knobs.
@@ -249,28 +264,195 @@ def _rccl_autotune(rank: int, world: int, nbytes: int, budget_s: float = 120.0,
     return doc
 
 
+# ------------------------------------------------------------------------------------------
+# The operator's artifacts, before RCCL starts
+# ------------------------------------------------------------------------------------------
+def _store(world: int, timeout_s: float):
+    """The rendezvous store (torchrun's agent store under torchrun; rank 0 hosts it otherwise),
+    shared with init_process_group: it carries the artifacts from rank 0 to every rank before
+    any RCCL communicator exists."""
+    from datetime import timedelta
+
+    import torch.distributed as dist
+
+    store, _, _ = next(dist.rendezvous("env://", timeout=timedelta(seconds=timeout_s)))
+    return store
+
+
+def _artifacts(store, rank: int, args) -> dict:
+    """Rank 0 produces (``--artifacts agent``) or loads (``--artifacts DIR``) the RCCL artifacts
+    and publishes them; every rank applies them to its environment before RCCL initialises.
+    Returns rank 0's description (with ``applied``) and this rank's record."""
+    from network_operator_amd.parallel import fabric_artifacts as FA
+
+    if rank == 0:
+        try:
+            if args.artifacts == "agent":
+                work = tempfile.mkdtemp(prefix="netop-bench-")
+                doc = FA.generate(work, sysfs_root=args.sysfs_root or None)
+                doc.update(dir=work, scratch=True)
+            else:
+                env = FA.load_env_dir(args.artifacts)
+                doc = {"source": f"artifact directory {args.artifacts}", "dir": args.artifacts, "env": env,
+                       "topo_file": env.get("NCCL_TOPO_FILE")}
+                if not env:
+                    doc["error"] = f"no {FA.ENV_FILE} in {args.artifacts}"
+                tf = env.get("NCCL_TOPO_FILE")
+                doc["topo_file_bytes"] = os.path.getsize(tf) if tf and os.path.isfile(tf) else 0
+                doc["topo_sha256"] = FA._sha256(tf) if tf else None
+        except Exception as e:
+            doc = {"error": f"{type(e).__name__}: {str(e)[-500:]}"}
+        store.set(STORE_KEY, json.dumps(doc))
+    else:
+        doc = json.loads(store.get(STORE_KEY))
+    if "error" in doc:
+        return {"doc": doc, "record": {"rank": rank, "applied": False}}
+    rec = FA.apply(doc["env"])
+    rec.update(rank=rank, applied=True)
+    return {"doc": doc, "record": rec}
+
+
+class _Once:
+    """Rank 0's single JSON line: printed once, by the main thread or the deadline watchdog."""
+
+    def __init__(self):
+        self.lock = threading.Lock()
+        self.done = False
+
+    def emit(self, line: dict) -> bool:
+        with self.lock:
+            if self.done:
+                return False
+            print(json.dumps(line), flush=True)
+            self.done = True
+            return True
+
+
+def _line(args, world: int, st: dict) -> dict:
+    """The JSON line from whatever has been measured so far (``st``)."""
+    h = st.get("headline")
+    cuda = args.device == "cuda"
+    from network_operator_amd.parallel import collectives as C
+
+    ceiling = C.xgmi_busbw_ceiling_GBps(world)
+    busbw = h["busbw"] if h else None
+    line = {
+        "metric": METRIC,
+        "value": round(busbw, 3) if h else None,
+        "unit": "GB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": h["per_step"] * 1e3 if h else None,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "bf16" if cuda else "fp32",
+        "data": "synthetic (zeros for the timed loop; exact pattern check before timing)",
+        "config": {"model": config_name(world), "global_batch": None, "seq_len": None,
+                   "parallelism": f"dp{world}", "gpus": world, "message_bytes_per_rank": h["nbytes"] if h else None,
+                   "op": "all_reduce(sum)",
+                   "backend": "torch.distributed nccl (RCCL)" if cuda else "torch.distributed gloo (CPU rehearsal)",
+                   "rccl_env": ("agent artifacts (discover --dry-run)" if args.artifacts == "agent"
+                                else "RCCL defaults" if args.artifacts == "off" else f"artifacts from {args.artifacts}")},
+        "agent_artifacts": st.get("artifacts"),
+        "busbw_GBps": busbw,
+        "busbw_rccl_defaults_GBps": (st.get("rccl_defaults") or {}).get("busbw_GBps"),
+        "rccl_defaults": st.get("rccl_defaults"),
+        "algbw_GBps": h["algbw"] if h else None,
+        "algbw_note": h.get("algbw_note") if h else None,
+        # rccl-tests busbw is per rank; the whole job moves n times that over the links.
+        "aggregate_busbw_GBps": busbw * world if h else None,
+        "busbw_ceiling_GBps": ceiling,
+        "busbw_vs_ceiling": (busbw / ceiling) if h and ceiling else None,
+        "verified": st.get("verified"),
+        "verify_errors": st.get("verify_errors"),
+        "sweep": st.get("sweep", []),
+        "collectives": st.get("collectives", []),
+        "xgmi_probe": st.get("xgmi_probe"),
+        "native_rccl": st.get("native_rccl"),
+        "rccl_autotune": st.get("tuned"),
+        "xgmi_allreduce": st.get("xgmi_allreduce"),
+        "xgmi_allreduce_multiprocess": st.get("xgmi_comm"),
+        "node_ready": st.get("node_ready"),
+        "node_ready_gpu_side": st.get("gpu_side"),
+        "xgmi_traffic": st.get("xgmi_traffic"),
+        "deadline_s": args.deadline_s,
+        "elapsed_s": round(time.monotonic() - st["t_start"], 2),
+        "extras_log": st.get("extras_log", []),
+        "notes": "; ".join(x for x in [
+            "n=1: busbw is 0 by definition (rccl-tests factor 2(n-1)/n)" if world == 1 else "",
+            "reference publishes no numbers (BASELINE.md) so vs_baseline is null",
+            st.get("node_ready_note") or "", st.get("smi_note") or ""] if x),
+        "rccl_version": st.get("rccl_version"),
+    }
+    if st.get("error"):
+        line["error"] = st["error"]
+    return line
+
+
+def _watchdog(rank: int, deadline: float, st: dict, once: _Once, runner_box: list, args, world: int) -> None:
+    """At the deadline: rank 0 kills every running extra and prints the line with what has been
+    measured; every rank then exits (0 if the timed loop finished, 1 if it never did)."""
+    def fire():
+        delay = deadline - time.monotonic() + (0 if rank == 0 else 20)
+        if delay > 0:
+            time.sleep(delay)
+        if st.get("finished"):  # printed; only a hung teardown is left
+            sys.stdout.flush()
+            os._exit(st.get("rc", 0))
+        if rank == 0:
+            if runner_box:
+                runner_box[0].kill_all()
+            for name in st.get("pending", ()):
+                st.setdefault(name, {"error": "deadline", "detail": "killed at --deadline-s"})
+            if not st.get("headline"):
+                st["error"] = f"deadline ({args.deadline_s} s) passed before the timed loop finished"
+            if once.emit(_line(args, world, st)):
+                print(f"bench.py: --deadline-s {args.deadline_s} reached; printed what was measured", file=sys.stderr)
+        sys.stdout.flush()
+        sys.stderr.flush()
+        os._exit(0 if st.get("headline") else 1)
+
+    threading.Thread(target=fire, name="bench-deadline", daemon=True).start()
+
+
 def main(argv=None) -> int:
+    t_start = time.monotonic()
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--bytes", type=int, default=1 << 30, help="all-reduce message size per rank")
+    ap.add_argument("--artifacts", default="agent",
+                    help="RCCL environment of the timed loop: 'agent' (run discover --dry-run on this node and apply "
+                         "its NCCL_TOPO_FILE / rccl.env), an artifact directory (rccl.env + rccl-tuned.env), or 'off' "
+                         "(RCCL defaults)")
+    ap.add_argument("--sysfs-root", default=os.environ.get("SYSFS_ROOT", ""),
+                    help="sysfs the agent reads for --artifacts agent (default the real /sys)")
+    ap.add_argument("--topo-dump", default="", help="with --artifacts off: RCCL topology dump path (rank 0)")
+    ap.add_argument("--rccl-defaults", type=int, default=1,
+                    help="also run the timed loop in fresh rank processes with RCCL's defaults (the A/B)")
+    ap.add_argument("--strict", type=int, default=1,
+                    help="GPU, n > 1: exit 1 (after printing the line) when the artifacts could not be applied or RCCL "
+                         "sees fewer than n-1 xGMI links per GPU under them")
+    ap.add_argument("--deadline-s", type=float, default=420.0,
+                    help="hard wall-clock limit: extras are killed and the line printed by then")
     ap.add_argument("--sweep", default="4096,1048576,67108864", help="extra sizes (bytes) reported alongside")
     ap.add_argument("--node-ready", choices=["auto", "on", "off"], default="auto")
     ap.add_argument("--node-ready-runs", type=int, default=5)
     ap.add_argument("--collectives", default="all_gather,reduce_scatter,all_to_all",
                     help="other collectives reported at --bytes (n > 1 only)")
     ap.add_argument("--xgmi-probe", type=int, default=1, help="run the HIP xGMI link probe on rank 0 (n > 1)")
-    ap.add_argument("--native-rccl", type=int, default=1, help="also run the native netop-rccl-bench harness on rank 0")
+    ap.add_argument("--native-rccl", type=int, default=1,
+                    help="also run the native netop-rccl-bench harness (ROCm's RCCL, artifacts applied) on rank 0")
     ap.add_argument("--rccl-env-probe", type=int, default=0,
                     help="n > 1: also measure the 1 GiB busbw under RCCL knob variants (a fresh process each)")
-    ap.add_argument("--extras-budget", type=float, default=150.0,
-                    help="seconds rank 0 may spend on the diagnostics after the timed loop (probe, native "
-                         "harness, knob probe, direct all-reduce); later ones are skipped once it is spent")
-    ap.add_argument("--rccl-autotune", type=int, default=1,
+    ap.add_argument("--extras-budget", type=float, default=0.0, help=argparse.SUPPRESS)  # superseded by --deadline-s
+    ap.add_argument("--rccl-autotune", type=int, default=0,
                     help="n > 1: before RCCL starts, rank 0 measures RCCL knob variants by running this bench "
                          "again per variant (within --rccl-autotune-budget s) and every rank uses the fastest "
-                         "(>= 3%% better than the defaults) for the run; 0 = RCCL defaults")
+                         "(>= 3%% better than the defaults) for the run; 0 = the artifacts' environment only")
     ap.add_argument("--rccl-autotune-budget", type=float, default=120.0)
     ap.add_argument("--gpu-side", type=int, default=1, help="rank 0: time the agent's unprivileged phases on this box")
     # CPU rehearsal of the autotune plumbing (tests): run it with gloo too, on the first K variants.
@@ -283,15 +465,13 @@ def main(argv=None) -> int:
     args = ap.parse_args(raw_argv)
     if args.gpus < 1:
         ap.error("--gpus must be >= 1")
+    deadline = t_start + args.deadline_s
 
-    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from network_operator_amd.parallel import bench_extras
+
+    bench_extras.maybe_hang()
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
-        return _spawn_ranks(args.gpus, raw_argv, args.device)
-
-    import torch
-    import torch.distributed as dist
-
-    from network_operator_amd.parallel import collectives as C
+        return _spawn_ranks(args.gpus, raw_argv, args.device, deadline)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -299,47 +479,82 @@ def main(argv=None) -> int:
     if world != args.gpus:
         print(f"bench.py: --gpus={args.gpus} but the launcher started WORLD_SIZE={world} ranks", file=sys.stderr)
         return 2
+    base_env = dict(os.environ)  # before any artifact or knob is exported: what the extras start from
+    os.environ.setdefault("RANK", "0")
+    os.environ.setdefault("WORLD_SIZE", "1")
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", str(_free_port()))
-    tuned = None
-    if args.device == "cpu":
-        device, dtype = torch.device("cpu"), torch.float32
-        if args.autotune_cpu_variants and world > 1:
-            from network_operator_amd.parallel import rccl_bench
 
-            tuned = _rccl_autotune(rank, world, args.bytes, args.rccl_autotune_budget, device="cpu",
-                                   variants=rccl_bench.ENV_PROBES[:args.autotune_cpu_variants])
-        dist.init_process_group("gloo", rank=rank, world_size=world)
-    else:
-        if not torch.cuda.is_available():
-            print("bench.py needs an MI355X GPU (torch.cuda.is_available() is False)", file=sys.stderr)
-            return 2
+    import torch
+    import torch.distributed as dist
+
+    from network_operator_amd.parallel import collectives as C
+    from network_operator_amd.parallel import fabric_artifacts as FA
+
+    st: dict = {"t_start": t_start, "pending": []}
+    once = _Once()
+    runner_box: list = []
+    _watchdog(rank, deadline, st, once, runner_box, args, world)
+
+    cuda = args.device == "cuda"
+    if cuda and not torch.cuda.is_available():
+        print("bench.py needs an MI355X GPU (torch.cuda.is_available() is False)", file=sys.stderr)
+        return 2
+
+    # 0. RCCL's environment, fixed before any communicator exists: the autotune (opt-in), then the
+    #    operator's artifacts, handed to every rank through the rendezvous store.
+    if world > 1 and (args.rccl_autotune if cuda else args.autotune_cpu_variants):
+        from network_operator_amd.parallel import rccl_bench
+
+        variants = None if cuda else rccl_bench.ENV_PROBES[:args.autotune_cpu_variants]
+        st["tuned"] = _rccl_autotune(rank, world, args.bytes, args.rccl_autotune_budget, device=args.device,
+                                     variants=variants)
+    store = _store(world, timeout_s=max(60.0, deadline - time.monotonic()))
+    art, dump_path = None, None
+    if args.artifacts != "off":
+        art = _artifacts(store, rank, args)
+        doc = art["doc"]
+        if rank == 0 and "error" not in doc:
+            dump_path = os.path.join(doc["dir"] if doc.get("scratch") else tempfile.mkdtemp(prefix="netop-bench-"),
+                                     FA.DUMP_FILE)
+    elif rank == 0 and args.topo_dump:
+        dump_path = args.topo_dump
+    if dump_path:
+        os.environ["NCCL_TOPO_DUMP_FILE"] = dump_path
+
+    if cuda:
         torch.cuda.set_device(local_rank)
         device, dtype = torch.device("cuda", local_rank), torch.bfloat16
-        tuned = (_rccl_autotune(rank, world, args.bytes, args.rccl_autotune_budget)
-                 if args.rccl_autotune and world > 1 else None)
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=device)
-    # Host-side group for waiting while rank 0 runs its extra GPU tools: an RCCL barrier would
-    # leave a spinning kernel on every other GPU and disturb what those tools measure.
-    host_pg = dist.new_group(backend="gloo") if args.device == "cuda" else None
+        dist.init_process_group("nccl", store=store, rank=rank, world_size=world, device_id=device)
+        # Host-side group for waiting while rank 0 runs its extras: an RCCL barrier would leave a
+        # spinning kernel on every other GPU and disturb what those tools measure.
+        host_pg = dist.new_group(backend="gloo")
+        st["rccl_version"] = ".".join(str(x) for x in torch.cuda.nccl.version()) if hasattr(torch.cuda, "nccl") else None
+    else:
+        device, dtype = torch.device("cpu"), torch.float32
+        dist.init_process_group("gloo", store=store, rank=rank, world_size=world)
+        host_pg = None
     esize = torch.tensor([], dtype=dtype).element_size()
+    records = [None] * world
+    dist.all_gather_object(records, art["record"] if art else {"rank": rank, "applied": False}, group=host_pg)
 
     # 1. Correctness of the collective path (exact, HIP pattern kernels on the GPU).
     verified, errors = C.verify_all_reduce(min(args.bytes // 2, 64 << 20), device)
+    st["verified"], st["verify_errors"] = verified, errors
 
     # 2. Headline: K timed all-reduce steps of --bytes per rank.
     numel = (args.bytes // esize) // 8 * 8
     buf = torch.zeros(numel, dtype=dtype, device=device)
     for _ in range(args.warmup):
         dist.all_reduce(buf)
-    smi_before, smi_note = None, None
-    if rank == 0 and args.device == "cuda":  # xGMI counters (amd-smi), outside the timed region
+    smi_before = None
+    if rank == 0 and cuda:  # xGMI counters (amd-smi), outside the timed region
         try:
             from network_operator_amd.ops import smi
 
             smi_before = smi.snapshot()
         except Exception as e:
-            smi_note = f"amd-smi counters unavailable: {e}"
+            st["smi_note"] = f"amd-smi counters unavailable: {e}"
     dist.barrier()
     C.sync(device)
     t0 = time.perf_counter()
@@ -348,189 +563,153 @@ def main(argv=None) -> int:
     C.sync(device)
     dt = time.perf_counter() - t0
     dist.barrier()
-    xgmi_traffic = None
     if rank == 0 and smi_before is not None:
         try:
-            xgmi_traffic = smi.traffic(smi_before, smi.snapshot())
+            t = smi.traffic(smi_before, smi.snapshot())
+            st["xgmi_traffic"] = {"links_up": t["links_up"], "links_with_traffic": t["links_with_traffic"],
+                                  "GB_per_gpu": [round(sum(g["bytes_per_link"]) / 1e9, 3) for g in t["gpus"]]}
         except Exception as e:
-            smi_note = f"amd-smi counters unavailable: {e}"
+            st["smi_note"] = f"amd-smi counters unavailable: {e}"
     t = torch.tensor([dt], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    dt = float(t.item())
-    per_step = dt / max(args.steps, 1)
+    per_step = float(t.item()) / max(args.steps, 1)
     nbytes = numel * esize
     algbw, busbw = C.bandwidths("all_reduce", nbytes, world, per_step)
     del buf
+    headline = {"busbw": busbw, "algbw": algbw, "per_step": per_step, "nbytes": nbytes}
+    if world == 1:
+        # A single-rank in-place all-reduce moves no bytes (RCCL returns at once): bytes/time would
+        # be a number with no meaning (round 1 printed 93 TB/s, 12x HBM peak).  Null, and why.
+        headline["algbw"] = None
+        headline["algbw_note"] = ("n=1: the timed in-place all-reduce is a no-op in RCCL (no peer, no copy), so algbw "
+                                  "is not a bandwidth; ms_per_step is its launch latency. busbw is 0 by definition")
+    st["headline"] = headline
+    if rank == 0 and os.environ.get(bench_extras.HANG_ENV) == "rank0-after-headline":  # test hook: a hung step
+        while True:
+            time.sleep(3600)
 
     # 3. Size sweep (latency / medium messages), same definitions.
-    sweep = []
     sizes = [int(s) for s in args.sweep.split(",") if s.strip()]
     if sizes:
-        for r in C.run_sweep("all_reduce", sizes, iters=max(args.steps, 10), warmup=max(args.warmup, 3), device=device,
-                             dtype=dtype):
-            sweep.append({"bytes": r.bytes, "time_us": r.time_s * 1e6, "algbw_GBps": r.algbw_GBps,
-                          "busbw_GBps": r.busbw_GBps})
+        st["sweep"] = [{"bytes": r.bytes, "time_us": r.time_s * 1e6, "algbw_GBps": None if world == 1 else r.algbw_GBps,
+                        "busbw_GBps": r.busbw_GBps}
+                       for r in C.run_sweep("all_reduce", sizes, iters=max(args.steps, 10), warmup=max(args.warmup, 3),
+                                            device=device, dtype=dtype)]
 
     # 4. The other collectives RCCL runs over the same links (rccl-tests definitions), n > 1.
-    others = []
     if world > 1:
+        others = []
         for op in [o.strip() for o in args.collectives.split(",") if o.strip()]:
             r = C.run_sweep(op, [nbytes], iters=max(args.steps // 2, 5), warmup=2, device=device, dtype=dtype)[0]
             others.append({"op": op, "bytes": r.bytes, "time_us": r.time_s * 1e6, "algbw_GBps": r.algbw_GBps,
                            "busbw_GBps": r.busbw_GBps})
+        st["collectives"] = others
 
-    # 5. xGMI link probe (rank 0, single process over every GPU it can see): per-link pull
-    #    bandwidth and all-peers-concurrent aggregate, byte-exact.  Runs after the timed loop.
-    probe = None
-    t_extras = time.monotonic()
-
-    def budget_left() -> bool:
-        return time.monotonic() - t_extras < args.extras_budget
-
-    #    In a child process: this rank holds an RCCL communicator and must survive to print.
-    if rank == 0 and world > 1 and args.device == "cuda" and args.xgmi_probe:
-        try:
-            from network_operator_amd.ops import hip as H
-
-            r = H.xgmi_probe_isolated(64 << 20, iters=5, max_gpus=world, timeout=120)
-            links = sorted(x for d, row in enumerate(r["link_GBps"]) for p, x in enumerate(row) if p != d)
-            probe = {"gpus": r["gpus"], "errors": r["errors"] + r["push_errors"],
-                     "link_GBps": {"min": links[0], "median": links[len(links) // 2], "max": links[-1]} if links else None,
-                     "aggregate_GBps": {"min": min(r["aggregate_GBps"]), "max": max(r["aggregate_GBps"])},
-                     "push_aggregate_GBps": {"min": min(r["push_aggregate_GBps"]), "max": max(r["push_aggregate_GBps"])}}
-        except Exception as e:
-            probe = {"error": str(e)[-500:]}
-
-    # 6. Native RCCL harness (rank 0, one process over the first `world` GPUs, RCCL linked
-    #    directly, every size checked exactly): a second opinion on the same links that does not
-    #    go through torch.distributed.  Runs after the timed loop; failures are reported, not fatal.
-    native = None
-    if rank == 0 and args.device == "cuda" and args.native_rccl and budget_left():
-        try:
-            from network_operator_amd.parallel import rccl_bench
-
-            rows = rccl_bench.run(op="all_reduce", gpus=world, min_bytes=1 << 20, max_bytes=1 << 30, factor=32,
-                                  iters=20, warmup=5, timeout=120)
-            native = {"rows": [{"bytes": r.bytes, "time_us": r.time_us, "algbw_GBps": r.algbw_GBps,
-                                "busbw_GBps": r.busbw_GBps, "wrong": r.wrong} for r in rows],
-                      "peak_busbw_GBps": max((r.busbw_GBps for r in rows), default=0.0)}
-            if world > 1 and args.rccl_env_probe and budget_left():  # knob sensitivity (diagnostic only)
-                native["env_probe"] = rccl_bench.env_probe(world, 1 << 30)
-        except Exception as e:
-            native = {"error": str(e)[-500:]}
-
-    # 7. Direct two-shot xGMI all-reduce (hand-written HIP, all 7 links at once, pull and push),
-    #    rank 0 over the first `world` GPUs, exact check of three seeds per size (n > 1).
-    direct = None
-    if rank == 0 and world > 1 and args.device == "cuda" and args.xgmi_allreduce and budget_left():
-        try:
-            from network_operator_amd.parallel import xgmi_allreduce as XA
-
-            direct = XA.run(ranks=world, min_bytes=nbytes, max_bytes=nbytes, iters=10, warmup=3, timeout=120)
-        except Exception as e:
-            direct = {"error": str(e)[-500:]}
-
-    # 8. The same algorithm the way jobs run it: one process per GPU, HIP IPC symmetric buffers,
-    #    host-ordered phases (parallel/xgmi_comm.py), in its own process group so a failure there
-    #    cannot take this run down.  Exact check of three seeds per size, both algorithms.
-    direct_mp = None
-    if rank == 0 and world > 1 and args.device == "cuda" and args.xgmi_allreduce and budget_left():
-        try:
-            from network_operator_amd.parallel import xgmi_comm
-
-            direct_mp = xgmi_comm.run(world, nbytes=nbytes, min_bytes=1 << 20, iters=10, warmup=3, timeout=120)
-        except Exception as e:
-            direct_mp = {"error": str(e)[-500:]}
-
-    gpu_side = None
-    if rank == 0 and args.gpu_side:
-        try:
-            gpu_side = node_ready_gpu_side()
-        except Exception as e:
-            gpu_side = {"error": str(e)[-300:]}
-
-    node_ready = None
-    node_ready_note = None
-    if rank == 0 and args.node_ready != "off":
-        try:
-            from network_operator_amd.testing import netns
-
-            ok, why = netns.available()
-            if ok:
-                node_ready = netns.node_ready_bench(n_nics=max(world, 1), runs=args.node_ready_runs, legacy=False)
-            else:
-                node_ready_note = why
-                if args.node_ready == "on":
-                    raise RuntimeError(why)
-        except Exception as e:  # the collective result stands on its own
-            node_ready_note = f"node-ready harness unavailable: {e}"
-
-    dist.barrier(group=host_pg)
-    ceiling = C.xgmi_busbw_ceiling_GBps(world)
-    # A single-rank in-place all-reduce moves no bytes (RCCL returns at once): bytes/time would be
-    # a number with no meaning (round 1 printed 93 TB/s, 12x HBM peak).  Report null and why.
-    algbw_note = None
-    if world == 1:
-        algbw = None
-        algbw_note = ("n=1: the timed in-place all-reduce is a no-op in RCCL (no peer, no copy), so algbw is "
-                      "not a bandwidth; ms_per_step is its launch latency. busbw is 0 by definition")
-        for row in sweep:
-            row["algbw_GBps"] = None
+    # 5. What was applied, and what RCCL made of it (rank 0).
     if rank == 0:
-        line = {
-            "metric": METRIC,
-            "value": round(busbw, 3),
-            "unit": "GB/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": per_step * 1e3,
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "bf16" if args.device == "cuda" else "fp32",
-            "data": "synthetic (zeros for the timed loop; exact pattern check before timing)",
-            "config": {"model": config_name(world), "global_batch": None, "seq_len": None,
-                       "parallelism": f"dp{world}", "gpus": world, "message_bytes_per_rank": nbytes,
-                       "op": "all_reduce(sum)",
-                       "backend": ("torch.distributed nccl (RCCL)" if args.device == "cuda"
-                                   else "torch.distributed gloo (CPU rehearsal)")},
-            "collectives": others,
-            "xgmi_probe": probe,
-            "native_rccl": native,
-            "rccl_autotune": tuned,
-            "xgmi_allreduce": direct,
-            "xgmi_allreduce_multiprocess": direct_mp,
-            "algbw_GBps": algbw,
-            "algbw_note": algbw_note,
-            "busbw_GBps": busbw,
-            # rccl-tests busbw is per rank; the whole job moves n times that over the links.
-            "aggregate_busbw_GBps": busbw * world,
-            "busbw_ceiling_GBps": ceiling,
-            "busbw_vs_ceiling": (busbw / ceiling) if ceiling else None,
-            "verified": verified,
-            "verify_errors": errors,
-            "sweep": sweep,
-            "node_ready": node_ready,
-            "node_ready_gpu_side": gpu_side,
-            "xgmi_traffic": ({"links_up": xgmi_traffic["links_up"],
-                              "links_with_traffic": xgmi_traffic["links_with_traffic"],
-                              "GB_per_gpu": [round(sum(g["bytes_per_link"]) / 1e9, 3) for g in xgmi_traffic["gpus"]]}
-                             if xgmi_traffic else None),
-            "notes": (("n=1: busbw is 0 by definition (rccl-tests factor 2(n-1)/n); " if world == 1 else "")
-                      + "reference publishes no numbers (BASELINE.md) so vs_baseline is null") + (f"; {node_ready_note}" if node_ready_note else "")
-                     + (f"; {smi_note}" if smi_note else ""),
-            "rccl_version": (".".join(str(x) for x in torch.cuda.nccl.version())
-                             if args.device == "cuda" and hasattr(torch.cuda, "nccl") else None),
-        }
-        print(json.dumps(line), flush=True)
+        if art is not None:
+            doc = dict(art["doc"])
+            doc.pop("scratch", None)
+            recs = [r for r in records if r]
+            shas = {r.get("topo_sha256") for r in recs if r.get("applied")}
+            doc.update(applied=bool(recs) and all(r.get("applied") for r in recs) and "error" not in doc,
+                       ranks_applied=sum(1 for r in recs if r.get("applied")), ranks_same_file=len(shas) <= 1,
+                       per_rank=[{"rank": r["rank"], "applied": r.get("applied"),
+                                  "NCCL_TOPO_FILE": (r.get("env") or {}).get("NCCL_TOPO_FILE"),
+                                  "topo_sha256": r.get("topo_sha256")} for r in recs])
+            st["artifacts"] = doc
+        else:
+            st["artifacts"] = {"applied": False, "source": "RCCL defaults (--artifacts off)"}
+        if dump_path:
+            st["artifacts"]["rccl_dump"] = (FA.read_view(dump_path, st["artifacts"].get("topo_file"))
+                                            or {"error": f"RCCL wrote no topology dump to {dump_path}"}) \
+                if cuda else {"note": "gloo: no RCCL topology on the CPU rehearsal"}
+
+    # 6. Diagnostics, rank 0, each a child process bounded by the deadline (bench_extras.Runner).
+    if rank == 0:
+        runner = bench_extras.Runner(deadline, base_env=base_env)
+        runner_box.append(runner)
+        art_env = art["doc"]["env"] if art and "error" not in art["doc"] else {}
+        plan = []
+        if args.rccl_defaults and args.artifacts != "off":
+            plan.append("rccl_defaults")
+        if cuda and args.native_rccl:
+            plan.append("native_rccl")
+        if cuda and world > 1 and args.xgmi_probe:
+            plan.append("xgmi_probe")
+        if cuda and world > 1 and args.xgmi_allreduce:
+            plan += ["xgmi_allreduce", "xgmi_comm"]
+        if args.node_ready != "off":
+            plan.append("node_ready")
+        st["pending"] = list(plan)
+        for name in plan:
+            if name == "rccl_defaults":
+                ddump = os.path.join(tempfile.mkdtemp(prefix="netop-bench-defaults-"), "rccl-topo-dump-defaults.xml")
+                cmd = _probe_cmd(world, args.bytes, args.steps, args.device, warmup=args.warmup) + [
+                    "--artifacts", "off", "--topo-dump", ddump, "--deadline-s", str(max(runner.left() - 2, 10)),
+                    "--strict", "0"]
+                j = runner.run(name, cmd, cap_s=180)
+                res = j if "error" in j else {
+                    "busbw_GBps": j.get("busbw_GBps"), "ms_per_step": j.get("ms_per_step"),
+                    "verified": j.get("verified"), "rccl_dump": (j.get("agent_artifacts") or {}).get("rccl_dump")}
+                shutil.rmtree(os.path.dirname(ddump), ignore_errors=True)
+            elif name == "native_rccl":
+                res = runner.extra(name, 150, env=art_env, world=world, env_probe=bool(args.rccl_env_probe))
+                res["with_artifacts"] = bool(art_env)
+            elif name == "xgmi_probe":
+                res = runner.extra(name, 120, world=world)
+            elif name in ("xgmi_allreduce", "xgmi_comm"):
+                res = runner.extra(name, 120, world=world, nbytes=nbytes)
+            else:  # node_ready
+                res = runner.extra(name, 150, n_nics=world, runs=args.node_ready_runs, required=args.node_ready == "on")
+                if "unavailable" in res:
+                    st["node_ready_note"] = f"node-ready harness unavailable: {res['unavailable']}"
+                    res = None
+                elif "result" in res:
+                    res = res["result"]
+                elif "error" in res:
+                    st["node_ready_note"] = f"node-ready harness failed: {res['error']}"
+                    res = None
+            st[name] = res
+            st["pending"].remove(name)
+        st["extras_log"] = runner.log
+        if args.gpu_side:
+            try:
+                st["gpu_side"] = node_ready_gpu_side()
+            except Exception as e:
+                st["gpu_side"] = {"error": str(e)[-300:]}
+
+    # 7. The link check: RCCL must see >= n-1 xGMI links per GPU under the agent's file.
+    rc = 0 if verified else 1
+    if rank == 0 and cuda and art is not None:
+        a = st["artifacts"]
+        v = FA.links_verdict(world, a.get("rccl_dump"), (st.get("rccl_defaults") or {}).get("rccl_dump"))
+        a["xgmi_links_check"] = v
+        if world > 1 and args.strict and (not a.get("applied") or v["status"] == "failed"):
+            why = v.get("why") if a.get("applied") else f"artifacts not applied: {a.get('error')}"
+            st["error"] = f"agent artifacts check failed: {why}"
+            rc = 1
+
+    try:  # everyone waits for rank 0's extras on the host (no spinning RCCL kernel)
+        dist.barrier(group=host_pg)
+    except Exception as e:  # rank 0 already gone (watchdog): the measurement stands
+        if rank != 0:
+            print(f"bench.py rank {rank}: final barrier: {e}", file=sys.stderr)
+    if rank == 0:
+        once.emit(_line(args, world, st))
+        if st.get("error"):
+            print(f"bench.py: {st['error']}", file=sys.stderr)
+    st["rc"] = rc
+    st["finished"] = True
     dist.destroy_process_group()
-    if rank == 0 and tuned is not None:
+    if rank == 0 and st.get("tuned") is not None:
         try:
             os.unlink(autotune_file())
         except OSError:
             pass
-    return 0 if verified else 1
+    if rank == 0 and art is not None and art["doc"].get("scratch"):
+        shutil.rmtree(art["doc"]["dir"], ignore_errors=True)
+    return rc
 
 
 if __name__ == "__main__":

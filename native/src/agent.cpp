@@ -815,6 +815,13 @@ void Agent::dry_run_report() {
         NLOG_I("dry run: NCCL_TOPO_FILE %s (%zu bytes)%s", cfg_.rccl_topo.c_str(), topo_xml().size(),
                env.empty() ? " not written" : "");
     }
+    if (!cfg_.rccl_env.empty()) {
+        // The intra-node part of rccl.env: NCCL_TOPO_FILE and the site settings.  Nothing was
+        // configured, so no HCA, GID or socket interface is named (a job on this node could not
+        // use them yet); bench.py and validate.py apply exactly this file to their RCCL runs.
+        write_rccl_env_file();
+        NLOG_I("dry run: RCCL environment file %s", cfg_.rccl_env.c_str());
+    }
     write_status();
     NLOG_I("dry run: %zu interface(s) would be configured in %s mode; nothing was changed", nics_.size(),
            cfg_.mode.c_str());

@@ -1078,6 +1078,26 @@ TEST(agent_dry_run_changes_nothing) {
     CHECK(!a.ready());
 }
 
+TEST(agent_dry_run_writes_intra_node_rccl_env) {
+    Fixture f;
+    f.cfg.dry_run = true;
+    f.cfg.rccl_topo = f.tmp.path + "/rccl-topo.xml";
+    f.cfg.rccl_env = f.tmp.path + "/rccl.env";
+    f.cfg.rccl_env_extra = "NCCL_MIN_NCHANNELS=64";
+    f.cfg.socket_ifname = "auto";
+    f.cfg.sysfs_root = f.tmp.path + "/sys/";
+    agent::Agent a(f.cfg, f.ops, f.all_valid(), f.nm());
+    a.run(-1);
+    auto env = read_file(f.cfg.rccl_env);
+    CHECK(env && env->find("NCCL_TOPO_FILE=" + f.cfg.rccl_topo + "\n") != std::string::npos);
+    CHECK(env->find("NCCL_MIN_NCHANNELS=64\n") != std::string::npos);
+    // nothing configured: no HCA, GID or socket interface a job could not use yet
+    CHECK(env->find("NCCL_IB_HCA") == std::string::npos);
+    CHECK(env->find("NCCL_SOCKET_IFNAME") == std::string::npos);
+    CHECK(env->find("NCCL_IB_GID_INDEX") == std::string::npos);
+    CHECK(f.ops.addrs.empty());
+}
+
 TEST(agent_topology_file_reused_within_a_boot) {
     Fixture f;
     f.cfg.keep_running = false;

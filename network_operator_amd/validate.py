@@ -12,8 +12,12 @@ these checks:
    PCIe tree does.
 2. **xGMI probe** (``netop-xgmi-probe``).  Per-link pull bandwidth, all-peers pull and push
    aggregates, all byte-exact.
-3. **RCCL** (``netop-rccl-bench``).  An all-reduce size sweep, every result checked exactly.
-   With n > 1 the large-message busbw must reach ``--min-busbw``.
+3. **RCCL** (``netop-rccl-bench``) with the agent's artifacts applied: ``<artifact-dir>/rccl.env``
+   (its ``NCCL_TOPO_FILE`` included) and ``rccl-tuned.env`` are sourced, as a job on the node
+   sources them.  An all-reduce size sweep, every result checked exactly; with n > 1 the
+   large-message busbw must reach ``--min-busbw``.  RCCL's topology dump of that run must show
+   >= n-1 xGMI links per GPU and place every GPU / NIC where the file does
+   (``parallel/fabric_artifacts.py``).
 4. **Counters** (amd-smi).  Every up xGMI link moved data during the RCCL run.  This is the
    "RCCL sees every link" check from BASELINE.json.
 5. **Direct xGMI all-reduce** (``parallel/xgmi_comm.py``).  The one-process-per-GPU
@@ -38,8 +42,10 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import shutil
 import subprocess
 import sys
+import tempfile
 import time
 from pathlib import Path
 from typing import List, Optional
@@ -111,6 +117,38 @@ def topo_file_agrees(xml_text: str, topo) -> dict:
     return {"ok": not missing and not split, "gpus_missing": missing, "pairs_split": split}
 
 
+def rccl_links_check(gpus: int, dump: str, art_env: dict, scratch: str, timeout: float) -> dict:
+    """RCCL sees >= n-1 xGMI links per GPU under the agent's NCCL_TOPO_FILE, and its dump places
+    every GPU (and NIC) where the file does.  Only when that fails is RCCL initialised once more
+    without the artifacts, to tell "the file costs links" from "RCCL does not record them"."""
+    from .parallel import fabric_artifacts as FA
+    from .parallel import rccl_bench
+
+    view = FA.read_view(dump, art_env.get("NCCL_TOPO_FILE"))
+    verdict = FA.links_verdict(gpus, view, None)
+    base = None
+    if verdict["status"] == "failed" and gpus > 1:
+        bdump = os.path.join(scratch, "rccl-topo-dump-defaults.xml")
+        env = {k: v for k, v in os.environ.items() if k not in art_env}
+        env["NCCL_TOPO_DUMP_FILE"] = bdump
+        try:
+            subprocess.run(rccl_bench.command(op="all_reduce", gpus=gpus, min_bytes=1 << 20, max_bytes=1 << 20,
+                                              iters=2, warmup=1, check=False),
+                           env=env, capture_output=True, text=True, timeout=timeout)
+            base = FA.read_view(bdump)
+        except Exception as e:
+            base = {"error": str(e)[-300:]}
+        verdict = FA.links_verdict(gpus, view, base)
+    ok = verdict["status"] != "failed" and bool(view) and "error" not in view \
+        and view.get("gpu_ancestry_equal", True) and view.get("nic_ancestry_equal") is not False
+    return _check("rccl_xgmi_links", ok, **verdict,
+                  rccl_dump={k: view.get(k) for k in ("gpus", "xgmi_links_per_gpu", "gpu_ancestry_equal",
+                                                      "nic_ancestry_equal", "gpu_ancestry_diff", "nic_ancestry_diff",
+                                                      "error")} if view else None,
+                  rccl_dump_defaults={k: base.get(k) for k in ("gpus", "min_xgmi_links", "xgmi_elements", "error")}
+                  if base else None)
+
+
 def run(gpus: int, min_busbw: float, min_link_GBps: float, max_bytes: int, sysfs_root: str = "/sys/",
         nfd_dir: Optional[str] = None, timeout: float = 600, artifact_dir: str = "/etc/amd/scale-out",
         tune_rccl: bool = False) -> dict:
@@ -160,19 +198,31 @@ def run(gpus: int, min_busbw: float, min_link_GBps: float, max_bytes: int, sysfs
         before = smi.snapshot()
     except Exception as e:
         report["smi_error"] = str(e)
+    #    RCCL runs the way jobs on this node run it: with the agent's rccl.env (its NCCL_TOPO_FILE
+    #    included) and rccl-tuned.env sourced, and RCCL's own topology dump read back.
+    from .parallel import fabric_artifacts as FA
+
+    art_env = FA.load_env_dir(artifact_dir)
+    scratch = tempfile.mkdtemp(prefix="netop-validate-")
     try:
         from .parallel import rccl_bench
 
+        dump = os.path.join(scratch, FA.DUMP_FILE)
         rows = rccl_bench.run(op="all_reduce", gpus=gpus, min_bytes=1 << 20, max_bytes=max_bytes, factor=8,
-                              iters=20, warmup=5, timeout=timeout)
+                              iters=20, warmup=5, timeout=timeout, env=dict(art_env, NCCL_TOPO_DUMP_FILE=dump))
         wrong = sum(r.wrong for r in rows)
         peak = max((r.busbw_GBps for r in rows), default=0.0)
         ok = bool(rows) and wrong == 0 and (gpus == 1 or peak >= min_busbw)
         checks.append(_check("rccl_all_reduce", ok, peak_busbw_GBps=peak, wrong=wrong, min_busbw_GBps=min_busbw,
+                             rccl_env=art_env, artifacts_applied=bool(art_env),
                              sizes=[{"bytes": r.bytes, "time_us": r.time_us, "busbw_GBps": r.busbw_GBps} for r in rows]))
         report["busbw_GBps"] = peak
+        if art_env:
+            checks.append(rccl_links_check(gpus, dump, art_env, scratch, timeout))
     except Exception as e:
         checks.append(_check("rccl_all_reduce", False, error=str(e)[-500:]))
+    finally:
+        shutil.rmtree(scratch, ignore_errors=True)
     if before is not None:
         try:
             t = smi.traffic(before, smi.snapshot())

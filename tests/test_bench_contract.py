@@ -214,3 +214,166 @@ def test_autotune_handoff_ignores_another_runs_file(monkeypatch):
         for p in (mine, other):
             if os.path.exists(p):
                 os.unlink(p)
+
+
+# ------------------------------------------------------------------------------------------
+# The operator's artifacts applied to the timed loop (VERDICT r2 "measure the configured fabric")
+# ------------------------------------------------------------------------------------------
+def _spawn_env(**extra):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    return dict(env, OMP_NUM_THREADS="1", **extra)
+
+
+@pytest.fixture(scope="module")
+def node_sysfs(tmp_path_factory):
+    from network_operator_amd.testing import fakesysfs
+
+    root = tmp_path_factory.mktemp("sys")
+    fakesysfs.build_mi355x_node(root)
+    return str(root) + "/"
+
+
+@pytest.mark.parametrize("n", [2, 4, 8])
+def test_bench_applies_agent_artifacts_on_every_rank(n, tmp_path, node_sysfs):
+    """Rank 0 runs the agent (discover --dry-run) on the node's sysfs before RCCL starts; every
+    rank exports the same NCCL_TOPO_FILE from its rccl.env; a fresh-process run without them is
+    the A/B."""
+    cmd = [sys.executable, str(ROOT / "bench.py"), "--gpus", str(n), "--steps", "3", "--warmup", "1", "--device", "cpu",
+           "--bytes", str(1 << 16), "--sweep", "", "--collectives", "", "--node-ready", "off",
+           "--sysfs-root", node_sysfs]
+    j = _bench_line(subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=tmp_path, env=_spawn_env()))
+    a = j["agent_artifacts"]
+    assert a["applied"] is True, a
+    assert a["ranks_applied"] == n and a["ranks_same_file"] is True
+    assert a["topo_file_bytes"] > 1000 and a["env"] == {"NCCL_TOPO_FILE": a["topo_file"]}
+    assert a["agent_status"]["xgmi_pairs"] == "28/28"
+    assert [r["rank"] for r in a["per_rank"]] == list(range(n))
+    assert {r["NCCL_TOPO_FILE"] for r in a["per_rank"]} == {a["topo_file"]}
+    assert {r["topo_sha256"] for r in a["per_rank"]} == {a["topo_sha256"]}
+    assert j["config"]["rccl_env"].startswith("agent artifacts")
+    assert j["busbw_rccl_defaults_GBps"] > 0 and j["rccl_defaults"]["verified"] is True
+    assert j["value"] > 0 and j["extras_log"][0]["extra"] == "rccl_defaults"
+    assert not os.path.exists(a["dir"])  # scratch removed
+
+
+def test_bench_applies_an_artifact_directory(tmp_path, node_sysfs):
+    """--artifacts DIR: what a job on a configured node sources (rccl.env, then rccl-tuned.env)."""
+    from network_operator_amd.parallel import fabric_artifacts as FA
+
+    d = tmp_path / "scale-out"
+    doc = FA.generate(str(d), sysfs_root=node_sysfs, env_extra="NCCL_MIN_NCHANNELS=32")
+    assert "error" not in doc, doc
+    (d / "rccl-tuned.env").write_text("# tuned\nNCCL_MIN_NCHANNELS=64\n")
+    cmd = [sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1", "--device", "cpu",
+           "--bytes", str(1 << 16), "--sweep", "", "--collectives", "", "--node-ready", "off", "--rccl-defaults", "0",
+           "--artifacts", str(d)]
+    j = _bench_line(subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=tmp_path, env=_spawn_env()))
+    a = j["agent_artifacts"]
+    assert a["applied"] and a["env"] == {"NCCL_TOPO_FILE": str(d / "rccl-topo.xml"), "NCCL_MIN_NCHANNELS": "64"}
+    assert a["ranks_applied"] == 2 and j["rccl_defaults"] is None
+    assert (d / "rccl.env").exists()  # never removed: not the bench's scratch
+
+
+def test_bench_hung_extra_still_prints_one_line(tmp_path, node_sysfs):
+    """A diagnostic that hangs on first contact (here the RCCL-defaults A/B) is killed at the
+    deadline with its whole process tree; the headline line still comes out, rc 0."""
+    import time as _t
+
+    cmd = [sys.executable, str(ROOT / "bench.py"), "--gpus", "4", "--steps", "3", "--warmup", "1", "--device", "cpu",
+           "--bytes", str(1 << 16), "--sweep", "", "--collectives", "", "--node-ready", "off",
+           "--sysfs-root", node_sysfs, "--deadline-s", "30"]
+    t = _t.monotonic()
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=120, cwd=tmp_path,
+                       env=_spawn_env(NETOP_BENCH_HANG_EXTRA="rccl_defaults"))
+    took = _t.monotonic() - t
+    j = _bench_line(r)
+    assert took < 30 + 15, took
+    assert j["value"] > 0 and j["verified"] is True and j["agent_artifacts"]["applied"]
+    assert j["rccl_defaults"]["error"] == "deadline" and j["busbw_rccl_defaults_GBps"] is None
+    assert j["extras_log"] == [dict(j["rccl_defaults"], extra="rccl_defaults")]
+
+
+def test_bench_watchdog_prints_when_rank0_hangs(tmp_path):
+    """Rank 0 stuck after the timed loop: the deadline watchdog prints the measured line and every
+    rank exits 0."""
+    cmd = [sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1", "--device", "cpu",
+           "--bytes", str(1 << 16), "--sweep", "", "--collectives", "", "--node-ready", "off", "--deadline-s", "20"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=120, cwd=tmp_path,
+                       env=_spawn_env(NETOP_BENCH_HANG_EXTRA="rank0-after-headline"))
+    j = _bench_line(r)
+    assert j["value"] > 0 and j["n_gpus"] == 2 and "deadline" in r.stderr
+
+
+def test_extras_runner_kills_the_whole_tree():
+    import time as _t
+
+    import psutil
+
+    from network_operator_amd.parallel import bench_extras as E
+
+    runner = E.Runner(_t.monotonic() + 60)
+    # a child that starts a grandchild in a session of its own, then hangs
+    code = ("import subprocess,sys,time; p=subprocess.Popen([sys.executable,'-c','import time; time.sleep(600)'],"
+            "start_new_session=True); print(p.pid, flush=True); time.sleep(600)")
+    before = {p.pid for p in psutil.process_iter()}
+    got = runner.run("t", [sys.executable, "-c", code], cap_s=3)
+    assert got["error"] == "timed out" and got["limit_s"] == 3
+    _t.sleep(0.5)
+    left = [p for p in psutil.process_iter(["cmdline"]) if p.pid not in before
+            and "time.sleep(600)" in " ".join(p.info["cmdline"] or [])]
+    assert not left, left
+    assert runner.extra("sleep", 30, seconds=0.1) == {"slept": 0.1}
+    late = E.Runner(_t.monotonic() + 1)
+    assert late.extra("sleep", 30, seconds=0.1)["error"] == "deadline"
+
+
+def _dump(gpus, links, nets=()):
+    """An RCCL-style topology dump: gpus = [(busid, chain)], links = {busid: [targets]}."""
+    body = []
+    for b, chain in gpus:
+        x = "".join(f'<xgmi target="{t}" count="1" tclass="0x038000"/>' for t in links.get(b, []))
+        inner = f'<pci busid="{b}" class="0x120000"><gpu dev="0" rank="0" gcn="gfx950">{x}</gpu></pci>'
+        for c in reversed(chain):
+            inner = f'<pci busid="{c}" class="0x060400">{inner}</pci>'
+        body.append(inner)
+    n = "".join(f'<pci busid="{c}"><nic><net name="{nm}"/></nic></pci>' for nm, c in nets)
+    return f'<system version="2"><cpu numaid="0">{"".join(body)}{n}</cpu></system>'
+
+
+def test_rccl_view_counts_xgmi_links_and_compares_ancestry():
+    from network_operator_amd.parallel import fabric_artifacts as FA
+
+    g = [("0000:0a:00.0", ["0000:01:00.0"]), ("0000:23:00.0", ["0000:1c:00.0"]), ("0000:5a:00.0", ["0000:53:00.0"])]
+    full = {a: [b for b, _ in g if b != a] + ["0000:f1:00.0"] for a, _ in g}  # + a GPU outside the job
+    dump = _dump(g, full, nets=[("mlx5_1", "0000:05:00.0")])
+    v = FA.rccl_view(dump, _dump(g, {}, nets=[("mlx5_1", "0000:05:00.0")]))
+    assert v["gpus"] == 3 and v["min_xgmi_links"] == 2 and v["xgmi_elements"] == 9
+    assert v["gpu_ancestry_equal"] and v["nic_ancestry_equal"] and v["nets_from_file"] == ["mlx5_1"]
+    assert FA.links_verdict(3, v, None)["status"] == "ok"
+    # the file moved one GPU under another switch
+    moved = FA.rccl_view(dump, _dump([g[0], ("0000:23:00.0", ["0000:99:00.0"]), g[2]], {}))
+    assert not moved["gpu_ancestry_equal"] and list(moved["gpu_ancestry_diff"]) == ["0000:23:00.0"]
+    # one GPU lost a link under the file, while RCCL sees all of them without it: fail
+    lost = dict(full, **{"0000:0a:00.0": ["0000:23:00.0"]})
+    bad = FA.rccl_view(_dump(g, lost))
+    verdict = FA.links_verdict(3, bad, v)
+    assert verdict["status"] == "failed" and "costs links" in verdict["why"]
+    assert FA.links_verdict(3, bad, None)["status"] == "failed"
+    # the dump misses a GPU of the job
+    assert FA.links_verdict(4, v, None)["status"] == "failed"
+    # no <xgmi> elements at all, with and without the file: this RCCL records them elsewhere
+    none = FA.rccl_view(_dump(g, {}))
+    assert FA.links_verdict(3, none, none)["status"] == "unverifiable"
+    assert FA.links_verdict(3, None, v)["status"] == "failed"
+    assert FA.links_verdict(1, None, None)["status"] == "ok"
+
+
+def test_env_file_parsing_keeps_exact_match_prefix(tmp_path):
+    from network_operator_amd.parallel import fabric_artifacts as FA
+
+    (tmp_path / "rccl.env").write_text("# c\nNCCL_IB_HCA==mlx5_0:1,mlx5_1:1\n\nexport NCCL_TOPO_FILE=/x.xml\nBAD\n")
+    (tmp_path / "rccl-tuned.env").write_text("NCCL_MIN_NCHANNELS=64\n")
+    assert FA.load_env_dir(str(tmp_path)) == {"NCCL_IB_HCA": "=mlx5_0:1,mlx5_1:1", "NCCL_TOPO_FILE": "/x.xml",
+                                              "NCCL_MIN_NCHANNELS": "64"}
+    env = {"NCCL_TOPO_FILE": "/x.xml", "NCCL_TOPO_DUMP_FILE": "/d", "PATH": "/bin"}
+    assert FA.strip(env, ["NCCL_TOPO_FILE"]) == {"PATH": "/bin"}

@@ -217,16 +217,20 @@ def test_fabric_validation_single_gpu(cuda_device, tmp_path):
     """validate.run on the 1-GPU box: topology from the real KFD and PCIe tree (the agent's
     NCCL_TOPO_FILE for this box must agree with it), probe, RCCL sweep, counters."""
     from network_operator_amd import validate
-    from network_operator_amd.agent import native
+    from network_operator_amd.parallel import fabric_artifacts as FA
 
     art = tmp_path / "art"
-    art.mkdir()
-    (art / "rccl-topo.xml").write_text(native().rccl_topo_xml("/sys/"))
+    doc = FA.generate(str(art))  # the agent itself (discover --dry-run): rccl-topo.xml + rccl.env
+    assert "error" not in doc, doc
     rep = validate.run(gpus=1, min_busbw=0, min_link_GBps=0, max_bytes=64 << 20, nfd_dir=str(tmp_path),
                        artifact_dir=str(art))
     assert rep["ok"], rep
     names = [c["check"] for c in rep["checks"]]
-    assert names[:5] == ["xgmi_topology", "gpu_nic_affinity", "rccl_topology_file", "xgmi_probe", "rccl_all_reduce"]
+    assert names[:6] == ["xgmi_topology", "gpu_nic_affinity", "rccl_topology_file", "xgmi_probe", "rccl_all_reduce",
+                         "rccl_xgmi_links"]
+    by = {c["check"]: c for c in rep["checks"]}
+    assert by["rccl_all_reduce"]["artifacts_applied"] and by["rccl_all_reduce"]["rccl_env"]["NCCL_TOPO_FILE"]
+    assert by["rccl_xgmi_links"]["rccl_dump"]["gpus"] == 1 and by["rccl_xgmi_links"]["rccl_dump"]["gpu_ancestry_equal"]
     assert names[-1] == "xgmi_direct_all_reduce"
     assert (tmp_path / validate.LABEL_FILE).read_text().startswith(validate.LABEL + "=true\n")
 

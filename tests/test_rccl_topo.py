@@ -295,3 +295,26 @@ def test_pci_folding_matches_nccl_walk(native, depth, seed):
         chain = _chain(xml, comps[-1])
         assert chain is not None
         assert chain[1:-1] == _nccl_fold(comps), (comps, chain)
+
+
+@pytest.mark.gpu
+def test_bench_measures_with_the_agents_file_and_reads_rccl_dump(tmp_path):
+    """bench.py's headline runs RCCL with the agent's NCCL_TOPO_FILE / rccl.env (discover
+    --dry-run on this box) and reads RCCL's dump back: the GPU where the file puts it, and the
+    xGMI link check (n - 1 = 0 here).  The RCCL-defaults A/B dumps too, for comparison."""
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "1", "--steps", "3", "--warmup", "1",
+                        "--sweep", "", "--node-ready", "off", "--native-rccl", "0", "--gpu-side", "0",
+                        "--deadline-s", "100"], capture_output=True, text=True, timeout=115, cwd=tmp_path)
+    assert r.returncode == 0, r.stderr[-3000:]
+    j = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    a = j["agent_artifacts"]
+    assert a["applied"] is True and a["ranks_applied"] == 1 and a["topo_file_bytes"] > 1000, a
+    d = a["rccl_dump"]
+    assert "error" not in d, d
+    assert d["gpus"] == 1 and d["gpu_ancestry_equal"] is True, d
+    assert a["xgmi_links_check"]["status"] == "ok"
+    base = j["rccl_defaults"]["rccl_dump"]
+    assert base["gpus"] == 1 and base["gpu_busids"] == d["gpu_busids"]
+    (ROOT / "gpurun_out").mkdir(exist_ok=True)
+    (ROOT / "gpurun_out" / "bench_artifacts_n1.json").write_text(json.dumps(
+        {"agent_artifacts": a, "rccl_defaults": j["rccl_defaults"], "ms_per_step": j["ms_per_step"]}, indent=1))
