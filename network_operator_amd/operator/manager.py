@@ -112,6 +112,9 @@ def build_parser() -> argparse.ArgumentParser:
                     help="ClusterRole/<name>: cluster-scoped owner of the seeded policies (uninstalling it "
                          "garbage-collects them)")
     ap.add_argument("--policies-interval", type=float, default=10.0, help="seconds between --policies-file passes")
+    ap.add_argument("--policies-seed-id", default="",
+                    help="without --policies-owner: the id (label amd.com/policy-seeder) marking this operator's "
+                         "seeded policies (default <namespace>.<leader election id>)")
     ap.add_argument("--zap-devel", action="store_true", default=True)
     ap.add_argument("--zap-log-level", default="info")
     ap.add_argument("--zap-encoder", default="console", choices=["console", "json"])
@@ -176,7 +179,8 @@ async def run(argv: Optional[List[str]] = None, stop: Optional[asyncio.Event] = 
                 # Only the leader writes policies; the webhook server is already serving, so the
                 # API server can admit them (see seeder.py for why the chart does not create them).
                 seeder = PolicySeeder(client, opts.policies_file, opts.policies_owner, opts.policies_interval,
-                                      metrics=metrics)
+                                      metrics=metrics,
+                                      seed_id=opts.policies_seed_id or f"{ns}.{opts.leader_election_id}")
                 seed = asyncio.ensure_future(seeder.run(stop))
             if started:
                 started.set()

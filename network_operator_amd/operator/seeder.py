@@ -16,19 +16,33 @@ through the operator's own webhooks, once that server is up.  The seeder repeats
 endpoints is retried with backoff.  The seeder:
 
 * creates missing policies and brings changed ones back to the file's spec, labels and
-  annotations; it only touches policies carrying ``app.kubernetes.io/managed-by: amd-network-
-  operator`` (a user's policy of the same name is left alone, with a warning);
-* deletes managed policies that left the file (``config.amd.enabled=false`` on upgrade);
+  annotations;
+* deletes its own policies that left the file (``config.amd.enabled=false`` on upgrade);
 * makes each policy a dependent of a release-owned, cluster-scoped anchor (``--policies-owner``,
   the chart's operator ClusterRole), so ``helm uninstall`` garbage-collects the policies and
   then their DaemonSets, as uninstalling the reference's release deletes its CR.
+
+Ownership is release-scoped, never decided by the generic ``app.kubernetes.io/managed-by``
+label (a user who copies a seeded policy's YAML copies that label too, and a second release or a
+dev operator on the same cluster carries the same one).  A policy is this seeder's when
+
+* with ``--policies-owner``: its ownerReferences hold *this* anchor's uid (a ClusterRole of
+  another release has another uid; a copied policy has no reference, or a stale one);
+* without an owner: it carries ``amd.com/policy-seeder: <seed id>`` with this operator's id
+  (``--policies-seed-id``, default ``<namespace>.<leader election id>``).
+
+Anything else of the same name is left alone, with a warning.  While the anchor is missing
+(an uninstall in progress) the seeder writes nothing: it could neither prove ownership nor give
+a new policy an owner the garbage collector will honour.
 """
 
 from __future__ import annotations
 
 import asyncio
 import copy
+import hashlib
 import logging
+import re
 from pathlib import Path
 from typing import List, Optional
 
@@ -43,6 +57,17 @@ log = logging.getLogger("seeder")
 
 MANAGED_BY_KEY = "app.kubernetes.io/managed-by"
 MANAGED_BY = "amd-network-operator"
+SEEDER_KEY = "amd.com/policy-seeder"
+
+
+def seed_id_label(seed_id: str) -> str:
+    """A label value (<= 63 chars of [A-Za-z0-9._-], alphanumeric at both ends) naming one
+    operator instance; long or odd ids are shortened with a hash, so distinct ids stay distinct."""
+    v = re.sub(r"[^A-Za-z0-9._-]", "-", seed_id).strip("-._")
+    if v != seed_id or len(v) > 63:
+        h = hashlib.sha256(seed_id.encode()).hexdigest()[:10]
+        v = (v[:52].strip("-._") + "-" + h).strip("-._")
+    return v or "default"
 OWNER_KINDS = {"ClusterRole": kube.CLUSTERROLES}
 
 
@@ -74,9 +99,10 @@ def load_policies(path: str) -> Optional[List[dict]]:
 
 class PolicySeeder:
     def __init__(self, client: ApiClient, path: str, owner: str = "", interval: float = 10.0,
-                 max_backoff: float = 10.0, metrics=None):
+                 max_backoff: float = 10.0, metrics=None, seed_id: str = "default"):
         self.client, self.path, self.interval, self.max_backoff = client, path, interval, max_backoff
         self.owner = owner  # "ClusterRole/<name>" or ""
+        self.seed_id = seed_id_label(seed_id)
         self.metrics = metrics
         self.applied = 0    # successful sync passes (tests, metrics)
         self.writes = 0     # creates + updates + deletes issued
@@ -97,9 +123,13 @@ class PolicySeeder:
             raise
         return {"apiVersion": res.api_version, "kind": res.kind, "name": name, "uid": o["metadata"]["uid"]}
 
-    @staticmethod
-    def _managed(obj: dict) -> bool:
-        return (obj.get("metadata", {}).get("labels") or {}).get(MANAGED_BY_KEY) == MANAGED_BY
+    def _ours(self, obj: dict, ref: Optional[dict]) -> bool:
+        """Release-scoped ownership (module docstring): the anchor's uid when there is an owner,
+        this operator's seeder id otherwise.  The generic managed-by label never decides."""
+        md = obj.get("metadata", {})
+        if self.owner:
+            return ref is not None and any(r.get("uid") == ref["uid"] for r in md.get("ownerReferences") or [])
+        return (md.get("labels") or {}).get(SEEDER_KEY) == self.seed_id
 
     async def sync_once(self) -> bool:
         """One pass; True when the cluster matches the file (or there is no file)."""
@@ -107,12 +137,16 @@ class PolicySeeder:
         if want is None:
             return True
         ref = await self._owner_reference()
+        if self.owner and ref is None:
+            log.info("policies owner %s not found (uninstall in progress?): nothing seeded this pass", self.owner)
+            return True
         P = kube.NETWORKCLUSTERPOLICIES
         names = set()
         for pol in want:
             name = pol["metadata"]["name"]
             names.add(name)
             desired = copy.deepcopy(pol)
+            desired["metadata"]["labels"][SEEDER_KEY] = self.seed_id
             if ref:
                 desired["metadata"]["ownerReferences"] = [ref]
             try:
@@ -124,8 +158,9 @@ class PolicySeeder:
                 self.writes += 1
                 log.info("created policy %s from %s", name, self.path)
                 continue
-            if not self._managed(cur):
-                log.warning("policy %s exists and is not managed by the operator: left as it is", name)
+            if not self._ours(cur, ref):
+                log.warning("policy %s exists and is not this operator's (%s): left as it is", name,
+                            f"owner {self.owner}" if self.owner else f"{SEEDER_KEY}={self.seed_id}")
                 continue
             new = copy.deepcopy(cur)
             new["spec"] = desired.get("spec", {})
@@ -141,10 +176,10 @@ class PolicySeeder:
                 await self.client.replace(P, new)
                 self.writes += 1
                 log.info("updated policy %s from %s", name, self.path)
-        listed = await self.client.list(P, label_selector=f"{MANAGED_BY_KEY}={MANAGED_BY}")
+        listed = await self.client.list(P, label_selector=None if self.owner else f"{SEEDER_KEY}={self.seed_id}")
         for cur in listed.get("items") or []:
             name = cur["metadata"]["name"]
-            if name not in names:
+            if name not in names and self._ours(cur, ref):
                 try:
                     await self.client.delete(P, name)
                     self.writes += 1

@@ -215,3 +215,93 @@ def test_one_release_helm_install_upgrade_and_uninstall(tmp_path, monkeypatch):
             await fake.stop()
 
     asyncio.run(asyncio.wait_for(body(), 90))
+
+
+def _policy(name, mtu=9000):
+    return {"apiVersion": "amd.com/v1alpha1", "kind": "NetworkClusterPolicy", "metadata": {"name": name},
+            "spec": {"configurationType": "amd-so", "nodeSelector": {"amd.feature.node.kubernetes.io/gpu-ready": "true"},
+                     "amdScaleOut": {"layer": "L3", "mtu": mtu}}}
+
+
+def test_seeder_ownership_is_release_scoped(tmp_path):
+    """ownership is decided by the release's anchor (ownerReference uid), or
+    by a release-unique seeder id without one — never by the generic managed-by label.  A user's
+    copy of a seeded policy (labels included) survives; a second operator instance with another
+    owner leaves the first one's policies alone, and vice versa."""
+    from network_operator_amd.operator.seeder import MANAGED_BY, MANAGED_BY_KEY, SEEDER_KEY, PolicySeeder
+
+    async def body():
+        fake = FakeApiServer()
+        url = await fake.start()
+        try:
+            async with ApiClient(KubeConfig(host=url)) as c:
+                for role in ("release-a", "release-b"):
+                    await c.create(kube.CLUSTERROLES, {"apiVersion": "rbac.authorization.k8s.io/v1",
+                                                       "kind": "ClusterRole", "metadata": {"name": role}, "rules": []})
+                fa, fb = tmp_path / "a.yaml", tmp_path / "b.yaml"
+                fa.write_text(yaml.safe_dump({"policies": [_policy("pol-a")]}))
+                fb.write_text(yaml.safe_dump({"policies": [_policy("pol-b", 4200)]}))
+                a = PolicySeeder(c, str(fa), owner="ClusterRole/release-a", interval=0.1)
+                b = PolicySeeder(c, str(fb), owner="ClusterRole/release-b", interval=0.1)
+                await a.sync_once()
+                seeded = fake.get_object(P, "pol-a")
+                assert seeded["metadata"]["labels"][MANAGED_BY_KEY] == MANAGED_BY
+                # The user copies the seeded YAML, labels included, under another name.
+                copy_ = {"apiVersion": seeded["apiVersion"], "kind": seeded["kind"],
+                         "metadata": {"name": "user-copy", "labels": dict(seeded["metadata"]["labels"])},
+                         "spec": seeded["spec"]}
+                await c.create(P, copy_)
+                await a.sync_once()
+                assert fake.get_object(P, "user-copy") is not None
+                # A second operator instance (another release) on the same cluster.
+                await b.sync_once()
+                await a.sync_once()
+                await b.sync_once()
+                assert fake.get_object(P, "pol-a") is not None and fake.get_object(P, "pol-b") is not None
+                assert fake.get_object(P, "pol-b")["spec"]["amdScaleOut"]["mtu"] == 4200
+                # B may not take over A's policy of the same name either.
+                fb.write_text(yaml.safe_dump({"policies": [_policy("pol-b", 4200), _policy("pol-a", 1500)]}))
+                await b.sync_once()
+                assert fake.get_object(P, "pol-a")["spec"]["amdScaleOut"]["mtu"] == 9000
+                # A disabled: only A's own policy goes.
+                fa.write_text(yaml.safe_dump({"policies": []}))
+                await a.sync_once()
+                assert fake.get_object(P, "pol-a") is None
+                assert fake.get_object(P, "pol-b") is not None and fake.get_object(P, "user-copy") is not None
+                # B's anchor gone (uninstall in progress): B writes nothing, deletes nothing.
+                await c.delete(kube.CLUSTERROLES, "release-b")
+                fb.write_text(yaml.safe_dump({"policies": []}))
+                writes = b.writes
+                await b.sync_once()
+                assert b.writes == writes
+
+                # Without an owner: a release-unique seeder id decides.
+                fx, fy = tmp_path / "x.yaml", tmp_path / "y.yaml"
+                fx.write_text(yaml.safe_dump({"policies": [_policy("pol-x")]}))
+                fy.write_text(yaml.safe_dump({"policies": []}))
+                x = PolicySeeder(c, str(fx), seed_id="ns-x.lease")
+                y = PolicySeeder(c, str(fy), seed_id="ns-y.lease")
+                await x.sync_once()
+                assert fake.get_object(P, "pol-x")["metadata"]["labels"][SEEDER_KEY] == "ns-x.lease"
+                await y.sync_once()  # lists nothing of its own: pol-x stays
+                assert fake.get_object(P, "pol-x") is not None
+                fx.write_text(yaml.safe_dump({"policies": []}))
+                await x.sync_once()
+                assert fake.get_object(P, "pol-x") is None and fake.get_object(P, "user-copy") is not None
+        finally:
+            await fake.stop()
+
+    asyncio.run(asyncio.wait_for(body(), 60))
+
+
+def test_seed_id_label_is_a_valid_distinct_label_value():
+    from network_operator_amd.operator.seeder import seed_id_label
+
+    assert seed_id_label("amd-network-operator.9a8a7ba6.amd.com") == "amd-network-operator.9a8a7ba6.amd.com"
+    long_a, long_b = "n" * 70 + "a", "n" * 70 + "b"
+    la, lb = seed_id_label(long_a), seed_id_label(long_b)
+    assert la != lb and len(la) <= 63 and len(lb) <= 63
+    odd = seed_id_label("ns/with spaces")
+    import re
+
+    assert re.fullmatch(r"[A-Za-z0-9]([A-Za-z0-9._-]*[A-Za-z0-9])?", odd) and odd != seed_id_label("ns/with-spaces")
