@@ -60,6 +60,7 @@ def _pci(root: Path, pcipath: str, driver: str, vendor: str, device: str, numa: 
     drv = root / "bus" / "pci" / "drivers" / driver
     drv.mkdir(parents=True, exist_ok=True)
     _link(drv, d / "driver")
+    _link(d, root / "bus" / "pci" / "devices" / d.name)  # /sys/bus/pci/devices/<bdf>, as on a host
     return d
 
 
@@ -85,6 +86,7 @@ def build_mi355x_node(root: Path, nic_names: Optional[Dict[str, str]] = None, ni
         net = d / "net" / name
         _w(net / "address", nic_macs.get(name, n["mac"]) + "\n")
         _w(net / "dev_port", "0\n")
+        _link(d, net / "device")  # /sys/class/net/<if>/device -> the PCI function, as on a host
         _link(net, root / "class" / "net" / name)
         nics.append(dict(n, ifname=name))
     for r in fx["rdma"]:

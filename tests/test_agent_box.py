@@ -17,9 +17,8 @@ import pytest
 from network_operator_amd.agent import native
 from network_operator_amd.utils.paths import native_bin
 
-pytestmark = pytest.mark.gpu
 
-
+@pytest.mark.gpu
 def test_agent_dry_run_on_this_node(tmp_path):
     topo, status = tmp_path / "rccl-topo.xml", tmp_path / "status.json"
     r = subprocess.run([str(native_bin("discover")), "--dry-run", "--mode=L3", "--mtu=9000", "--xgmi-expect=0",
@@ -41,3 +40,129 @@ def test_agent_dry_run_on_this_node(tmp_path):
     if out.is_dir():  # evidence for profiles/ when run through gpurun
         (out / "agent_dry_run_box.json").write_text(json.dumps({"status": st, "pairs": pairs,
                                                                 "log_tail": r.stderr[-4000:]}, indent=1))
+
+
+# ------------------------------------------------------------------------------------------
+# An independent oracle for the GPU <-> NIC pairing: plain Python over sysfs, no native code.
+# ------------------------------------------------------------------------------------------
+_BDF = re.compile(r"^[0-9a-f]{4}:[0-9a-f]{2}:[0-9a-f]{2}\.[0-7]$")
+
+
+def _read(path, default=""):
+    try:
+        with open(path) as f:
+            return f.read().strip()
+    except OSError:
+        return default
+
+
+def sysfs_oracle(root="/sys/"):
+    """GPUs (amdgpu PCI functions), RDMA-capable PCI NICs and, per GPU, the NICs behind the same
+    PCIe switch, from realpaths alone.  The rule, stated independently of the agent: a NIC is
+    affine to a GPU when their deepest common PCI ancestor is below the root port (a switch
+    port); among those, the closest (deepest common ancestor) is the GPU's rail NIC."""
+    root = root.rstrip("/")
+
+    def chain(dev_path):
+        real = os.path.realpath(dev_path)
+        parts = real.split("/devices/", 1)[1].split("/") if "/devices/" in real else []
+        return [p for p in parts if p]
+
+    gpus = {}
+    drv = os.path.join(root, "bus/pci/drivers/amdgpu")
+    for name in sorted(os.listdir(drv)) if os.path.isdir(drv) else []:
+        if _BDF.match(name):
+            dev = os.path.join(root, "bus/pci/devices", name)
+            gpus[name] = {"chain": chain(dev), "numa": _read(os.path.join(dev, "numa_node"), "-1")}
+    nics = {}
+    cls = os.path.join(root, "class/net")
+    for ifname in sorted(os.listdir(cls)) if os.path.isdir(cls) else []:
+        dev = os.path.join(cls, ifname, "device")
+        if not os.path.exists(dev):
+            continue  # virtual
+        c = chain(dev)
+        if not c or not _BDF.match(c[-1]):
+            continue
+        ib = os.path.join(dev, "infiniband")
+        rdma = sorted(os.listdir(ib)) if os.path.isdir(ib) else []
+        if not rdma:
+            continue  # not RDMA-capable: not a scale-out candidate
+        nics[ifname] = {"chain": c, "bdf": c[-1], "rdma": rdma[0], "numa": _read(os.path.join(dev, "numa_node"), "-1"),
+                        "driver": os.path.basename(os.path.realpath(os.path.join(dev, "driver")))}
+    affine = {}
+    for g, gd in gpus.items():
+        cands = []
+        for n, nd in nics.items():
+            k = 0
+            while k < min(len(gd["chain"]), len(nd["chain"])) and gd["chain"][k] == nd["chain"][k]:
+                k += 1
+            # chain[0] is the host bridge (pciDDDD:BB), chain[1] the root port: a common
+            # component past those is a switch both sit below.
+            if k >= 3:
+                cands.append((k, n))
+        best = max((k for k, _ in cands), default=None)
+        affine[g] = {"closest": sorted(n for k, n in cands if k == best), "all": sorted(n for _, n in cands)}
+    return {"gpus": gpus, "nics": nics, "affine": affine}
+
+
+@pytest.mark.gpu
+def test_pairing_matches_an_independent_sysfs_oracle(tmp_path):
+    """the agent's pairs (the `discover` binary's log and its NCCL_TOPO_FILE)
+    checked against plain-Python sysfs walking, whichever NIC family (mlx5, ionic, ...) the box
+    has."""
+    import xml.etree.ElementTree as ET
+
+    root = os.environ.get("SYSFS_ROOT", "/sys/")
+    o = sysfs_oracle(root)
+    if not o["gpus"]:
+        pytest.skip("no amdgpu GPU in this sysfs")
+    topo = tmp_path / "rccl-topo.xml"
+    r = subprocess.run([str(native_bin("discover")), "--dry-run", "--xgmi-expect=-1", f"--rccl-topo={topo}"],
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr[-3000:]
+    pairs = re.findall(r"GPU (\d+) \((\S+)\) <-> NIC (\S+) \((\S+), (\S+), path (\w+)\)", r.stderr)
+    got = {b: n for _, b, n, _, _, _ in pairs}
+    # 1. every GPU with an affine RDMA NIC is paired, with one of its closest NICs (or, when a
+    #    closer one went to an earlier GPU, another affine one); no NIC twice.
+    assert len(set(got.values())) == len(got)
+    for g, a in o["affine"].items():
+        if not a["all"]:
+            assert g not in got, (g, got.get(g))
+            continue
+        assert g in got, (g, a)
+        assert got[g] in a["all"], (g, got[g], a)
+        if got[g] not in a["closest"]:
+            assert all(n in got.values() for n in a["closest"]), (g, got[g], a)
+    # 2. each pair's PCI function and RDMA device as sysfs has them
+    for _, b, n, bdf, rdma, _ in pairs:
+        assert o["nics"][n]["bdf"] == bdf and o["nics"][n]["rdma"] == rdma, (n, o["nics"][n], bdf, rdma)
+        assert o["nics"][n]["numa"] == o["gpus"][b]["numa"], (n, b)
+    # 3. the NCCL_TOPO_FILE names each pair's RDMA device under the GPU's own top switch
+    xml = ET.fromstring(topo.read_text())
+    top_of = {}
+    for cpu in xml.findall("cpu"):
+        for top in cpu.findall("pci"):
+            for p in top.iter("pci"):
+                top_of[p.get("busid")] = top.get("busid")
+            for net in top.iter("net"):
+                top_of["net:" + net.get("name")] = top.get("busid")
+    for _, b, n, _, rdma, _ in pairs:
+        assert top_of.get("net:" + rdma) == top_of.get(b), (b, n, rdma)
+    families = sorted({o["nics"][n]["driver"] for n in got.values()})
+    out = Path(os.environ.get("GRAFT_REPO_ROOT", ".")) / "gpurun_out"
+    if out.is_dir():
+        (out / "pairing_oracle_box.json").write_text(json.dumps(
+            {"nic_families_paired": families, "pairs": pairs, "oracle_affine": o["affine"],
+             "rdma_nics": {n: {k: v for k, v in d.items() if k != "chain"} for n, d in o["nics"].items()}}, indent=1))
+
+
+def test_oracle_agrees_with_agent_on_the_captured_node(tmp_path):
+    """The oracle itself, against the fake tree of the captured 8x MI355X node (CPU-side
+    counterpart of the box test; the fixture's rail NICs are mlx5)."""
+    from network_operator_amd.testing import fakesysfs
+
+    fakesysfs.build_mi355x_node(tmp_path)
+    o = sysfs_oracle(str(tmp_path) + "/")
+    want = native().discover(str(tmp_path) + "/", "affine")
+    assert len(o["gpus"]) == 8 and all(len(a["closest"]) == 1 for a in o["affine"].values())
+    assert {p["gpu"]: p["nic"] for p in want["pairs"]} == {g: a["closest"][0] for g, a in o["affine"].items()}
