@@ -140,6 +140,11 @@ class LldpSource {
     // Transmits our own LLDPDU on an interface (no-op for sources that cannot transmit).
     virtual void announce(const std::string& ifname, const std::vector<uint8_t>& frame) {}
     virtual pkt::ListenerStats stats() const { return {}; }
+    // Per-interface counters; nullopt for sources that keep none.
+    virtual std::optional<pkt::ListenerStats> stats_for(const std::string& ifname) const {
+        (void)ifname;
+        return std::nullopt;
+    }
 };
 
 // The LLDPDU the agent advertises for one of its NICs.  Announcing ourselves makes an
@@ -203,6 +208,8 @@ class Agent {
     std::vector<std::string> collect_interfaces();
     void get_network_configs(const std::vector<std::string>& names);
     void detect_lldp(int stop_fd);
+    void diagnose_silent();            // after --wait expired: why each silent NIC heard nothing
+    std::string silent_summary() const;  // "" or "LLDP silent on k NIC(s): ..." for the exit error
     void on_lldp(NicState& n, const lldp::Frame& f);
     void add_route(NicState& n, int mask);
     uint32_t rail_table(const NicState& n) const;

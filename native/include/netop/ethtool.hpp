@@ -11,9 +11,10 @@
 //   ice  (E810):            fw-lldp-agent   = off
 //   anything else:          --fw-lldp-priv-flag NAME=0|1 (site-specific)
 //
-// mlx5 (ConnectX) hands LLDP to the host unless its firmware DCBX/LLDP agent was enabled
-// with mlxconfig (LLDP_NB_DCBX_P*), which is a persistent firmware setting outside the
-// scope of a DaemonSet; the agent reports "no firmware LLDP flag" for it.
+// mlx5 (ConnectX) and ionic (Pensando): no private flag is known to the agent; a firmware
+// LLDP agent there is a persistent NIC setting outside the scope of a DaemonSet (unverified on
+// this pool: parity unpinned).  The agent reports "no firmware LLDP flag" for them, and a NIC
+// that stays silent is diagnosed after --wait (Agent::diagnose_silent).
 #pragma once
 
 #include <cstdint>

@@ -36,6 +36,15 @@ struct LinkInfo {
     std::string operstate_str() const;
 };
 
+// Receive counters of a link (IFLA_STATS64): used to tell a NIC that hears nothing from one
+// that hears traffic but no LLDP (a NIC-firmware LLDP agent consuming the frames).
+struct LinkStats {
+    uint64_t rx_packets = 0;
+    uint64_t rx_bytes = 0;
+    uint64_t multicast = 0;
+    uint64_t rx_dropped = 0;
+};
+
 struct AddrInfo {
     int ifindex = 0;
     int family = 0;
@@ -112,6 +121,11 @@ class NetOps {
     virtual void link_set_down(int ifindex) = 0;
     virtual void link_set_mtu(int ifindex, int mtu) = 0;
     virtual std::unique_ptr<LinkWatcher> subscribe_links() = 0;
+    // Receive counters; nullopt where the source has none (fakes, old kernels).
+    virtual std::optional<LinkStats> link_stats(int ifindex) {
+        (void)ifindex;
+        return std::nullopt;
+    }
 };
 
 class Rtnl final : public NetOps {
@@ -134,6 +148,7 @@ class Rtnl final : public NetOps {
     void link_set_down(int ifindex) override;
     void link_set_mtu(int ifindex, int mtu) override;
     std::unique_ptr<LinkWatcher> subscribe_links() override;
+    std::optional<LinkStats> link_stats(int ifindex) override;
 
     // Extra operations (harness / diagnostics; not part of the injectable table).
     LinkInfo link_by_index(int ifindex);
@@ -164,6 +179,8 @@ class Rtnl final : public NetOps {
 
 // Parses an RTM_NEWLINK/RTM_DELLINK payload.
 LinkInfo parse_link(const nlmsghdr* h);
+// IFLA_STATS64 (else IFLA_STATS) of an RTM_NEWLINK message; nullopt when it carries neither.
+std::optional<LinkStats> parse_link_stats(const nlmsghdr* h);
 // The NLMSGERR_ATTR_MSG string of an extended ACK (NLMSG_ERROR with NLM_F_ACK_TLVS); "" if
 // absent.  `h->nlmsg_len` bytes must be readable; every inner length is bounds-checked.
 std::string ext_ack_msg(const nlmsghdr* h);

@@ -47,6 +47,7 @@ class LldpSocket {
     const std::string& ifname() const { return ifname_; }
     int ifindex() const { return ifindex_; }
     const MacAddr& own_mac() const { return own_; }
+    const ListenerStats& stats() const { return stats_; }  // this socket's share
 
     // Reads every queued frame without blocking; returns the decoded LLDPDUs that
     // did not come from our own MAC.
@@ -58,6 +59,7 @@ class LldpSocket {
     std::string ifname_;
     int ifindex_ = 0;
     MacAddr own_;
+    ListenerStats stats_;
 };
 
 enum class ListenResult { Stopped, Deadline, Interrupted };
@@ -78,6 +80,8 @@ class LldpListener {
                      const std::function<bool(const std::string& ifname, const lldp::Frame& frame)>& on_frame,
                      int interrupt_fd = -1);
     const ListenerStats& stats() const { return stats_; }
+    // One interface's counters (a default-constructed record for an unknown one).
+    ListenerStats stats_for(const std::string& ifname) const;
 
    private:
     int epfd_ = -1;

@@ -59,6 +59,11 @@ struct NicState {
 
     // NIC firmware LLDP agent (--disable-fw-lldp): summary of what was done
     std::string fw_lldp;
+    // L3, --wait expired without a frame: the NIC's driver and what it did hear meanwhile
+    // (Agent::diagnose_silent), e.g. "mlx5_core: no LLDPDU in 90s while 412 frames arrived ...".
+    std::string driver;
+    std::optional<uint64_t> rx_at_listen;  // link rx_packets when the LLDP wait began
+    std::string lldp_silent;
 
     // Monitor
     bool degraded = false;  // link went down / lost carrier after readiness

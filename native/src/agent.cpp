@@ -61,6 +61,9 @@ class PacketSource final : public LldpSource {
         listener_.send(ifname, frame);
     }
     pkt::ListenerStats stats() const override { return listener_.stats(); }
+    std::optional<pkt::ListenerStats> stats_for(const std::string& ifname) const override {
+        return listener_.stats_for(ifname);
+    }
 
    private:
     bool promisc_;
@@ -656,6 +659,9 @@ void Agent::detect_lldp(int stop_fd) {
         }
     }
     if (!listening) return;
+    for (auto& n : nics_)  // what each NIC hears while we wait: the diagnosis of a silent one
+        if (listened.count(n.link.index))
+            if (auto s = ops_.link_stats(n.link.index)) n.rx_at_listen = s->rx_packets;
     int remaining = listening - apply_lldp_cache(listened);
     if (remaining <= 0) {
         NLOG_I("Every listening interface was configured from the LLDP cache; the switch confirms it while monitoring");
@@ -781,7 +787,58 @@ void Agent::detect_lldp(int stop_fd) {
         if (r != pkt::ListenResult::Deadline || mono_ns() >= deadline) break;
     }
     if (r == pkt::ListenResult::Interrupted) aborted_ = true;
-    if (r == pkt::ListenResult::Deadline) NLOG_I("LLDP wait of %s expired with %d interface(s) silent", format_go_duration(cfg_.wait_ns).c_str(), remaining);
+    if (r == pkt::ListenResult::Deadline) {
+        NLOG_I("LLDP wait of %s expired with %d interface(s) silent", format_go_duration(cfg_.wait_ns).c_str(), remaining);
+        diagnose_silent();
+    }
+}
+
+void Agent::diagnose_silent() {
+    // The reference's barrier times out without saying why (cmd/discover/main.go:84-122).  On
+    // RoCE NICs the usual cause is the NIC firmware's own LLDP/DCBX agent consuming the
+    // switch's LLDPDUs; tell that apart from a dead link or an undecodable
+    // frame with what the NIC did hear while we waited.
+    std::string root = cfg_.sysfs_root.empty() ? topo::sysfs_root() : cfg_.sysfs_root;
+    const std::string waited = format_go_duration(cfg_.wait_ns);
+    for (auto& n : nics_) {
+        if (n.lldp_seen || n.lldp_from_cache) continue;
+        if (auto d = topo::netdev_pci(root, n.ifname)) n.driver = d->driver;
+        if (n.driver.empty() && ethtool_) n.driver = ethtool_->driver(n.ifname);
+        const std::string drv = n.driver.empty() ? "unknown driver" : n.driver;
+        if (!n.link.up()) {
+            n.lldp_silent = drv + ": link down, nothing listened";
+            NLOG_W("%s: %s", n.ifname.c_str(), n.lldp_silent.c_str());
+            continue;
+        }
+        std::optional<uint64_t> rx;
+        if (n.rx_at_listen)
+            if (auto s = ops_.link_stats(n.link.index)) rx = s->rx_packets >= *n.rx_at_listen ? s->rx_packets - *n.rx_at_listen : 0;
+        auto ls = lldp_->stats_for(n.ifname);
+        std::string heard = rx ? strfmt("%llu frame(s) arrived meanwhile", (unsigned long long)*rx)
+                               : std::string("receive counters unavailable");
+        std::string why;
+        if (ls && ls->malformed) {
+            why = strfmt("%llu LLDPDU(s) did not decode", (unsigned long long)ls->malformed);
+        } else if (rx && *rx == 0) {
+            why = "the link received nothing: check the cable, the switch port and its LLDP transmit setting";
+        } else if (n.driver == "i40e" || n.driver == "ice") {
+            why = cfg_.disable_fw_lldp ? "NIC-firmware LLDP agent suspected although --disable-fw-lldp ran (" + n.fw_lldp + ")"
+                                       : "NIC-firmware LLDP agent suspected: run with --disable-fw-lldp";
+        } else {
+            why = "NIC-firmware LLDP agent suspected (no verified switch for this driver; see the user guide, "
+                  "\"Silent LLDP\")";
+        }
+        n.lldp_silent = strfmt("%s: no LLDPDU in %s, %s; %s", drv.c_str(), waited.c_str(), heard.c_str(), why.c_str());
+        NLOG_W("%s: %s", n.ifname.c_str(), n.lldp_silent.c_str());
+    }
+}
+
+std::string Agent::silent_summary() const {
+    std::vector<std::string> parts;
+    for (const auto& n : nics_)
+        if (!n.lldp_silent.empty()) parts.push_back(n.ifname + " (" + n.lldp_silent + ")");
+    if (parts.empty()) return "";
+    return strfmt("LLDP silent on %zu NIC(s): ", parts.size()) + join(parts, "; ");
 }
 
 void Agent::write_l2_artifacts() {
@@ -1133,6 +1190,13 @@ std::string Agent::render_metrics() const {
     o += strfmt("netop_agent_link_flaps_total %d\n", flaps_);
     metric("netop_agent_reconfigurations_total", "counter", "NIC re-addressings after a Port Description change");
     o += strfmt("netop_agent_reconfigurations_total %d\n", reconfigs_);
+    if (cfg_.mode == "L3") {
+        metric("netop_agent_lldp_silent", "gauge",
+               "1 when the LLDP wait expired without a frame on the NIC (driver: its PCI driver)");
+        for (auto& n : nics_)
+            o += strfmt("netop_agent_lldp_silent{nic=\"%s\",driver=\"%s\"} %d\n", httpd::escape_label(n.ifname).c_str(),
+                        httpd::escape_label(n.driver).c_str(), n.lldp_silent.empty() ? 0 : 1);
+    }
     auto st = lldp_ ? lldp_->stats() : pkt::ListenerStats{};
     metric("netop_agent_lldp_frames_total", "counter", "LLDP frames received, by outcome");
     o += strfmt("netop_agent_lldp_frames_total{outcome=\"accepted\"} %llu\n", (unsigned long long)st.frames);
@@ -1281,7 +1345,9 @@ void Agent::run(int stop_fd) {
             mark("configure");
             if (configured < total) {
                 write_status();
-                throw AgentError(strfmt("Not all interfaces were configured (%d/%d).", configured, total));
+                const std::string why = silent_summary();
+                throw AgentError(strfmt("Not all interfaces were configured (%d/%d).", configured, total) +
+                                 (why.empty() ? "" : " " + why));
             }
             NLOG_I("Configured %d of %d interfaces", configured, total);
             if (cfg_.verify_peers_ns > 0) {
@@ -1303,7 +1369,8 @@ void Agent::run(int stop_fd) {
             }
         } else if (cfg_.configure && !found && !cfg_.label_without_peers) {
             write_status();
-            throw AgentError("No LLDP peers with a /30 Port Description were found");
+            const std::string why = silent_summary();
+            throw AgentError("No LLDP peers with a /30 Port Description were found" + (why.empty() ? "" : ". " + why));
         }
         write_artifacts();
         mark("artifacts");

@@ -434,6 +434,41 @@ LinkInfo Rtnl::link_by_index(int ifindex) {
     return *out;
 }
 
+std::optional<LinkStats> parse_link_stats(const nlmsghdr* h) {
+    const auto* ifi = fixed_header<ifinfomsg>(h, "link");
+    size_t len = h->nlmsg_len - NLMSG_LENGTH(sizeof(ifinfomsg));
+    std::optional<LinkStats> s64, s32;
+    for_each_attr(IFLA_RTA(ifi), len, [&](const rtattr* a) {
+        if (a->rta_type == IFLA_STATS64 && RTA_PAYLOAD(a) >= sizeof(rtnl_link_stats64)) {
+            rtnl_link_stats64 st;
+            std::memcpy(&st, RTA_DATA(a), sizeof st);
+            s64 = LinkStats{st.rx_packets, st.rx_bytes, st.multicast, st.rx_dropped};
+        } else if (a->rta_type == IFLA_STATS && RTA_PAYLOAD(a) >= sizeof(rtnl_link_stats)) {
+            rtnl_link_stats st;
+            std::memcpy(&st, RTA_DATA(a), sizeof st);
+            s32 = LinkStats{st.rx_packets, st.rx_bytes, st.multicast, st.rx_dropped};
+        }
+    });
+    return s64 ? s64 : s32;
+}
+
+std::optional<LinkStats> Rtnl::link_stats(int ifindex) {
+    Msg m(RTM_GETLINK, 0);
+    ifinfomsg ifi{};
+    ifi.ifi_family = AF_UNSPEC;
+    ifi.ifi_index = ifindex;
+    m.put(ifi);
+    std::optional<LinkStats> out;
+    try {
+        transact(m, [&](const nlmsghdr* h) {
+            if (h->nlmsg_type == RTM_NEWLINK) out = parse_link_stats(h);
+        });
+    } catch (const SysError&) {
+        return std::nullopt;
+    }
+    return out;
+}
+
 std::vector<LinkInfo> Rtnl::link_list() {
     Msg m(RTM_GETLINK, 0);
     ifinfomsg ifi{};

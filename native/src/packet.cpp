@@ -93,16 +93,19 @@ std::vector<lldp::Frame> LldpSocket::drain(ListenerStats* stats) {
         }
         if (from.sll_pkttype == PACKET_OUTGOING) continue;
         if (n >= 12 && std::memcmp(buf + 6, own_.b.data(), 6) == 0) {
+            ++stats_.own;
             if (stats) ++stats->own;
             continue;
         }
         lldp::DecodeError err;
         auto f = lldp::decode(buf, size_t(n), &err);
         if (!f) {
+            ++stats_.malformed;
             if (stats) ++stats->malformed;
             NLOG_V(4, "%s: dropping malformed LLDP frame (%zd bytes): %s", ifname_.c_str(), n, lldp::to_string(err));
             continue;
         }
+        ++stats_.frames;
         if (stats) ++stats->frames;
         out.push_back(std::move(*f));
     }
@@ -163,6 +166,12 @@ void LldpListener::remove(const std::string& ifname) {
             s.reset();  // keep slot indices stable for epoll data
         }
     }
+}
+
+ListenerStats LldpListener::stats_for(const std::string& ifname) const {
+    for (auto& s : socks_)
+        if (s && s->ifname() == ifname) return s->stats();
+    return {};
 }
 
 bool LldpListener::send(const std::string& ifname, const std::vector<uint8_t>& frame) {

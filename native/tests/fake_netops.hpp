@@ -152,6 +152,18 @@ struct FakeNetOps : netop::nl::NetOps {
             return out;
         }
     };
+    // Receive counters: rx[ifindex] is returned and then advanced by rx_step[ifindex] per call
+    // (traffic arriving while the agent waits); links without an entry have no counters.
+    std::map<int, uint64_t> rx, rx_step;
+    std::optional<netop::nl::LinkStats> link_stats(int ifindex) override {
+        ++calls["link_stats"];
+        auto it = rx.find(ifindex);
+        if (it == rx.end()) return std::nullopt;
+        netop::nl::LinkStats s;
+        s.rx_packets = it->second;
+        it->second += rx_step[ifindex];
+        return s;
+    }
     std::unique_ptr<netop::nl::LinkWatcher> subscribe_links() override {
         maybe_fail("subscribe_links");
         return std::make_unique<Watcher>(this);

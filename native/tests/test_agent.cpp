@@ -18,6 +18,12 @@ using namespace netop;
 namespace {
 struct ScriptedLldp : agent::LldpSource {
     std::map<std::string, lldp::Frame> frames;
+    std::map<std::string, pkt::ListenerStats> per_if;  // what stats_for reports
+    std::optional<pkt::ListenerStats> stats_for(const std::string& ifname) const override {
+        auto it = per_if.find(ifname);
+        if (it == per_if.end()) return std::nullopt;
+        return it->second;
+    }
     std::vector<std::string> added;
     pkt::ListenResult result_if_unfinished = pkt::ListenResult::Deadline;
     void add(const std::string& ifname, int, const MacAddr&) override { added.push_back(ifname); }
@@ -274,6 +280,65 @@ TEST(agent_reference_fixture_partial_failure) {
     }
     CHECK(threw);
     CHECK(!path_exists(f.cfg.labels.path()));
+}
+
+TEST(agent_silent_nics_are_diagnosed_in_the_error_status_and_metrics) {
+    // when --wait expires, say per NIC which driver it has and what it heard.
+    Fixture f;
+    f.cfg.wait_ns = 1000000;
+    f.cfg.sysfs_root = f.tmp.path + "/sys/";
+    // ens1 is an ionic NIC (sysfs device/driver); ens0 and ens2 have no PCI device.
+    f.tmp.mkdir("sys/devices/pci0000:00/0000:00:01.0/0000:01:00.0/net/ens1");
+    f.tmp.mkdir("sys/bus/pci/drivers/ionic");
+    f.tmp.symlink("sys/bus/pci/drivers/ionic", "sys/devices/pci0000:00/0000:00:01.0/0000:01:00.0/driver");
+    f.tmp.symlink("sys/devices/pci0000:00/0000:00:01.0/0000:01:00.0/net/ens1", "sys/class/net/ens1");
+    f.tmp.symlink("sys/devices/pci0000:00/0000:00:01.0/0000:01:00.0",
+                  "sys/devices/pci0000:00/0000:00:01.0/0000:01:00.0/net/ens1/device");
+    auto s = f.all_valid();
+    s->frames.erase("ens1");  // traffic, but no LLDPDU: a firmware agent eats them
+    s->frames.erase("ens2");  // nothing at all
+    f.ops.rx[11] = 100;
+    f.ops.rx_step[11] = 412;
+    f.ops.rx[12] = 7;
+    agent::Agent a(f.cfg, f.ops, std::move(s), f.nm());
+    std::string err;
+    try {
+        a.run(-1);
+    } catch (const agent::AgentError& e) {
+        err = e.what();
+    }
+    CHECK(err.find("Not all interfaces were configured (1/3). LLDP silent on 2 NIC(s): ") == 0);
+    CHECK(err.find("ens1 (ionic: no LLDPDU in 1ms, 412 frame(s) arrived meanwhile; NIC-firmware LLDP agent suspected") !=
+          std::string::npos);
+    CHECK(err.find("ens2 (unknown driver: no LLDPDU in 1ms, 0 frame(s) arrived meanwhile; the link received nothing") !=
+          std::string::npos);
+    auto st = read_file(f.cfg.status_file);
+    CHECK(st && st->find("\"driver\":\"ionic\",\"lldp_silent\":\"ionic: no LLDPDU") != std::string::npos);
+    auto m = a.render_metrics();
+    CHECK(m.find("netop_agent_lldp_silent{nic=\"ens1\",driver=\"ionic\"} 1") != std::string::npos);
+    CHECK(m.find("netop_agent_lldp_silent{nic=\"ens2\",driver=\"\"} 1") != std::string::npos);
+    CHECK(m.find("netop_agent_lldp_silent{nic=\"ens0\",driver=\"\"} 0") != std::string::npos);
+
+    // Frames that do not decode, and an i40e NIC (a known firmware-LLDP switch exists).
+    Fixture g;
+    g.cfg.wait_ns = 1000000;
+    auto t = std::make_unique<ScriptedLldp>();
+    pkt::ListenerStats bad;
+    bad.malformed = 3;
+    t->per_if["ens0"] = bad;
+    g.ops.rx[10] = 0;
+    g.ops.rx_step[10] = 5;
+    agent::Agent b(g.cfg, g.ops, std::move(t), g.nm());
+    err.clear();
+    try {
+        b.run(-1);
+    } catch (const agent::AgentError& e) {
+        err = e.what();
+    }
+    CHECK(err.find("No LLDP peers with a /30 Port Description were found. LLDP silent on 3 NIC(s): ") == 0);
+    CHECK(err.find("ens0 (unknown driver: no LLDPDU in 1ms, 5 frame(s) arrived meanwhile; 3 LLDPDU(s) did not decode)") !=
+          std::string::npos);
+    CHECK(err.find("ens1 (unknown driver: no LLDPDU in 1ms, receive counters unavailable; NIC-firmware") != std::string::npos);
 }
 
 TEST(agent_no_peers_is_an_error_unless_compat) {

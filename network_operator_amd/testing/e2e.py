@@ -230,7 +230,8 @@ async def _ha_checks(fake, c, rt, node, replicas: list, ns: str, name: str, mode
 
 async def _scenario(tmp: Path, n_nics: int, mode: str, seed: int, interval: str, fast_start: bool,
                     teardown: bool, node_name: str, policy_kw: dict, update_mtu: int, config_type: str,
-                    flap: bool, validation: str, crash_agent: bool, driver_reload: bool, ha: bool) -> dict:
+                    flap: bool, validation: str, crash_agent: bool, driver_reload: bool, ha: bool,
+                    silent_nics: int = 0, lldp_wait: str = "") -> dict:
     from ..api.v1alpha1 import types as T
     from ..operator import kube, manager
     from ..operator.kube import ApiClient, KubeConfig
@@ -258,7 +259,8 @@ async def _scenario(tmp: Path, n_nics: int, mode: str, seed: int, interval: str,
     for n in nat.discover(str(tmp / "sys"))["nics"]:  # RoCE v2 GIDs as the RDMA core adds them
         if n["ifname"] in nic_names and n["rdma_dev"]:
             fakesysfs.add_rocev2_gids(tmp / "sys", n["rdma_dev"], [plan[nic_names.index(n["ifname"])]["local"]])
-    sw = netns.SyntheticSwitch(nic_names, plan, rng, interval=interval, phase="random", fast_start=fast_start)
+    sw = netns.SyntheticSwitch(nic_names, plan, rng, interval=interval, phase="random", fast_start=fast_start,
+                               silent_nics=silent_nics)
     sw.start(rt)
 
     res: dict = {"n_nics": len(nic_names), "mode": mode, "plan": plan, "nics": nic_names, "fast_start": fast_start}
@@ -285,7 +287,8 @@ async def _scenario(tmp: Path, n_nics: int, mode: str, seed: int, interval: str,
     node = SimNode(fake, node_name, {"amd.feature.node.kubernetes.io/gpu-ready": "true"}, tmp / "host",
                    sysfs_root=tmp / "sys", init_images={KMD_IMAGE: kmd},
                    env={"PYTHONPATH": str(Path(__file__).resolve().parents[2])},
-                   job_images={T0.DEFAULT_VALIDATION_IMAGE: [sys.executable, "-c", _VALIDATE_STUB, validation or "pass"]})
+                   job_images={T0.DEFAULT_VALIDATION_IMAGE: [sys.executable, "-c", _VALIDATE_STUB, validation or "pass"]},
+                   agent_arg_overrides={"--wait": lldp_wait} if lldp_wait else None)
     if validation and not host_nic:
         policy_kw = dict(policy_kw, validation={"enabled": True, "minBusbw": 300})
     P, DS = kube.NETWORKCLUSTERPOLICIES, kube.DAEMONSETS
@@ -311,6 +314,19 @@ async def _scenario(tmp: Path, n_nics: int, mode: str, seed: int, interval: str,
             await c.create(P, pol)
             t_ds = await _until(lambda: fake.get_object(DS, name, ns) is not None, 10)
             t_agent = await _until(lambda: any(x.proc is not None for x in node.containers.values()), 10)
+            if silent_nics:
+                # A switch port that never sends LLDP: the agent's exit error names the NIC, its
+                # driver and what it heard, and the operator puts that into status.errors.
+                def silent_errors():
+                    st = (fake.get_object(P, name) or {}).get("status") or {}
+                    return [e for e in st.get("errors") or [] if "LLDP silent" in e]
+                t_err = await _until(lambda: bool(silent_errors()), 30)
+                res["policy_to_silent_error_s"] = round(t_err - t0, 6) if t_err else None
+                await _until(lambda: any(e.get("reason") == "AgentFailed" for e in fake.list_objects(kube.EVENTS)), 5)
+                res["policy_status"] = (fake.get_object(P, name) or {}).get("status")
+                res["node_labels"] = node.node_labels()
+                res["events"] = [e.get("reason") + ": " + e.get("message", "") for e in fake.list_objects(kube.EVENTS)]
+                return res
             t_label = await _until(lambda: node.node_labels().get(label_key) == "true", 30)
 
             if both:
@@ -608,13 +624,13 @@ def run_scenario(n_nics: int = 2, mode: str = "L3", seed: int = 1, interval: str
                  teardown: bool = True, node_name: str = "mi355x-0", policy_kw: Optional[dict] = None,
                  update_mtu: int = 0, config_type: str = "amd-so", flap: bool = False, validation: str = "",
                  crash_agent: bool = False, driver_reload: bool = False, ha: bool = False,
-                 keep_tmp: bool = False) -> dict:
+                 silent_nics: int = 0, lldp_wait: str = "", keep_tmp: bool = False) -> dict:
     """Must already run inside a private user+net namespace (``run_isolated``)."""
     tmp = Path(tempfile.mkdtemp(prefix="netop-e2e-"))
     try:
         return asyncio.run(_scenario(tmp, n_nics, mode, seed, interval, fast_start, teardown, node_name,
                                      dict(policy_kw or {}), update_mtu, config_type, flap, validation,
-                                     crash_agent, driver_reload, ha))
+                                     crash_agent, driver_reload, ha, silent_nics, lldp_wait))
     finally:
         if not keep_tmp:
             shutil.rmtree(tmp, ignore_errors=True)

@@ -76,8 +76,10 @@ class SimNode:
     def __init__(self, fake, name: str, labels: Dict[str, str], host_root: Path, sysfs_root: Optional[Path] = None,
                  probe_period: float = 0.02, nfd_period: float = 0.01, env: Optional[Dict[str, str]] = None,
                  init_images: Optional[Dict[str, List[str]]] = None, netns=None,
-                 job_images: Optional[Dict[str, List[str]]] = None):
+                 job_images: Optional[Dict[str, List[str]]] = None, agent_arg_overrides: Optional[Dict[str, str]] = None):
         self.fake, self.name = fake, name
+        # "--flag" -> value replacing the DaemonSet's own (tests shorten e.g. --wait=90s)
+        self.agent_arg_overrides = dict(agent_arg_overrides or {})
         self.base_labels = dict(labels)
         self.host_root = Path(host_root)
         self.sysfs_root = sysfs_root
@@ -127,6 +129,8 @@ class SimNode:
     def _agent_argv(self, cmd: List[str], mounts) -> List[str]:
         # The image's entrypoint (and the probe's absolute binary path) is the agent binary.
         argv = [str(native_bin("discover"))] + [self._rewrite_arg(a, mounts) for a in cmd]
+        for k, v in self.agent_arg_overrides.items():
+            argv = [a for a in argv if a != k and not a.startswith(k + "=")] + [f"{k}={v}"]
         # The agent's built-in default label directory is a container path: name it explicitly.
         if not any(a.startswith("--nfd-features-dir") for a in argv):
             feat = self._rewrite(discovery.LABEL_FEATURES_DIR.rstrip("/"), mounts)

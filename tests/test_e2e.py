@@ -116,6 +116,21 @@ def test_link_failure_is_reported_by_the_policy_and_recovers():
     assert r["port_up_to_all_good_s"] is not None, r["agent_log"]
 
 
+def test_silent_switch_port_reaches_the_policy_status():
+    """one switch port never sends LLDP.  The agent's exit error names the NIC, its
+    driver (the fake node's rail NICs are mlx5_core) and what it heard; the operator puts it in
+    the policy's status.errors and an AgentFailed event, and the node is never labelled."""
+    r = e2e.run_isolated(n_nics=2, mode="L3", seed=21, interval="1s", silent_nics=1, lldp_wait="2s")
+    assert r["policy_to_silent_error_s"] is not None, (r["policy_status"], r["agent_log"])
+    silent = r["nics"][-1]
+    errs = [e for e in r["policy_status"]["errors"] if "LLDP silent" in e]
+    assert errs and errs[0].startswith("mi355x-0: scale-out not ready (ContainersNotReady): Not all interfaces were "
+                                       "configured (1/2). LLDP silent on 1 NIC(s): "
+                                       f"{silent} (mlx5_core: no LLDPDU in 2s, "), errs
+    assert "amd.feature.node.kubernetes.io/gpu-scale-out" not in r["node_labels"]
+    assert any(e.startswith("AgentFailed: ") and "LLDP silent" in e for e in r["events"]), r["events"]
+
+
 @pytest.mark.parametrize("outcome", ["pass", "fail"])
 def test_fabric_validation_job_runs_on_the_ready_node(outcome):
     """amdScaleOut.validation end to end: the node becomes ready, the operator starts a validation

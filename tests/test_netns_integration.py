@@ -102,10 +102,20 @@ def test_bad_port_description_fails_without_label():
 
 
 def test_silent_switch_port_times_out():
+    """The silent NIC is named with its driver (the fake node's rail NICs are mlx5_core) and what
+    it heard meanwhile, in the exit error (-> policy status.errors) and the status file."""
     r = netns.run_isolated(n_nics=2, seed=16, interval="1s", fast_start=True, silent_nics=1, wait="2s")
     assert not r["ready"]
     assert r["agent_rc"] == 1
     assert "expired with 1 interface(s) silent" in r["agent_log"]
+    silent = r["nics"][-1]
+    err = [ln for ln in r["agent_log"].splitlines() if ln.startswith("Error: ")][-1]
+    assert err.startswith("Error: Not all interfaces were configured (1/2). LLDP silent on 1 NIC(s): "
+                          f"{silent} (mlx5_core: no LLDPDU in 2s, "), err
+    assert "frame(s) arrived meanwhile" in err
+    st = {i["name"]: i for i in r["status"]["interfaces"]}
+    assert st[silent]["driver"] == "mlx5_core" and st[silent]["lldp_silent"].startswith("mlx5_core: no LLDPDU in 2s")
+    assert "lldp_silent" not in st[r["nics"][0]]
 
 
 def test_l2_mode_no_addresses():
