@@ -480,10 +480,8 @@ def main(argv=None) -> int:
         print(f"bench.py: --gpus={args.gpus} but the launcher started WORLD_SIZE={world} ranks", file=sys.stderr)
         return 2
     base_env = dict(os.environ)  # before any artifact or knob is exported: what the extras start from
-    os.environ.setdefault("RANK", "0")
-    os.environ.setdefault("WORLD_SIZE", "1")
-    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-    os.environ.setdefault("MASTER_PORT", str(_free_port()))
+    if "WORLD_SIZE" not in os.environ:  # one rank, no launcher: a rendezvous of its own, on a free port
+        os.environ.update(RANK="0", WORLD_SIZE="1", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
 
     import torch
     import torch.distributed as dist

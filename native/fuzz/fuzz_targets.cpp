@@ -63,6 +63,10 @@ extern "C" int LLVMFuzzerTestOneInput(const uint8_t* data, size_t size) {
         (void)nl::parse_link(h);
     } catch (const std::exception&) {
     }
+    try {
+        (void)nl::parse_link_stats(h);
+    } catch (const std::exception&) {
+    }
     // The same bytes as an extended-ACK error (nlmsgerr + echoed request + attributes), both with
     // and without the capped echo.
     h->nlmsg_type = NLMSG_ERROR;
@@ -75,6 +79,18 @@ extern "C" int LLVMFuzzerTestOneInput(const uint8_t* data, size_t size) {
     if (r) {
         // A reply always carries Ethernet/IPv4 sizes, op 2, and the addresses at their offsets.
         if (size < arp::kPayloadLen || data[7] != 2 || Ipv4::from_net(data + 14) != r->sender_ip) __builtin_trap();
+        // The acceptance rule: only a reply from the peer to our own address verifies a NIC.
+        if (size >= arp::kPayloadLen + 8) {
+            arp::Probe p;
+            p.local = Ipv4::from_net(data + arp::kPayloadLen);
+            p.peer = Ipv4::from_net(data + arp::kPayloadLen + 4);
+            const bool ok = arp::answers(p, *r);
+            if (ok != (r->sender_ip == p.peer && r->target_ip == p.local)) __builtin_trap();
+            if (ok) {
+                arp::record_answer(p, *r, 3000, 1000, 2000);
+                if (!p.answered || p.rtt_ns != 1000 || p.verify_ns != 2000 || !(p.peer_mac == r->sender_mac)) __builtin_trap();
+            }
+        }
     }
     if (size >= 10) {  // requests from arbitrary addresses always encode to a fixed-size payload
         auto req = arp::encode_request(MacAddr::from_bytes(data), Ipv4::from_net(data + 2), Ipv4::from_net(data + 6));

@@ -46,7 +46,8 @@ struct Probe {
     Ipv4 peer;       // the switch-side /30 address that must answer
     // results
     bool answered = false;
-    int64_t rtt_ns = 0;  // first request to the answer
+    int64_t rtt_ns = 0;     // round trip: the last request sent before the answer, to the answer
+    int64_t verify_ns = 0;  // time to verify: the first request to the answer (retries included)
     MacAddr peer_mac;
     int requests = 0;
     std::string error;  // socket errors; empty when the peer just stayed silent
@@ -75,6 +76,13 @@ class Prober {
     int socket_for(int ifindex);
     std::map<int, int> fds_;  // ifindex -> fd
 };
+
+// Whether `r` answers probe `p`: a reply from the peer's address *to our own* address.  A reply
+// aimed at another local address (another NIC on the segment, a stale exchange) or a gratuitous
+// one (target = sender) does not verify that this NIC's /30 works.
+bool answers(const Probe& p, const Reply& r);
+// Records an accepted reply at `now` (both times from the requests' send times).
+void record_answer(Probe& p, const Reply& r, int64_t now, int64_t first_sent, int64_t last_sent);
 
 // One-shot: a Prober for one call (its sockets are closed before returning).
 bool probe_all(std::vector<Probe>& probes, int64_t timeout_ns, int64_t retry_ns, int stop_fd = -1);

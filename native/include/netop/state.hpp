@@ -39,7 +39,12 @@ struct NicState {
     std::string config_error;
     // --verify-peers: the switch-side /30 address answered ARP (0 = not checked / no answer)
     bool peer_verified = false;
-    int64_t peer_rtt_ns = 0;
+    int64_t peer_rtt_ns = 0;      // last ARP request -> answer
+    int64_t peer_verify_ns = 0;   // first ARP request -> answer (retries included)
+    // The ARP answer came from another MAC than the LLDP peer's (ChassisID/PortID MAC): a
+    // proxy-ARP or misaddressed port, or a switch answering from its router MAC.  Reported, not
+    // fatal (switches may legitimately answer ARP from a different MAC than their LLDP one).
+    bool peer_mac_mismatch = false;
     std::optional<MacAddr> peer_arp_mac;
     std::string peer_error;
 

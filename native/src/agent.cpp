@@ -1214,11 +1214,22 @@ std::string Agent::render_metrics() const {
         for (auto& n : nics_)
             o += strfmt("netop_agent_peer_verified{nic=\"%s\"} %d\n", httpd::escape_label(n.ifname).c_str(),
                         n.peer_verified ? 1 : 0);
-        metric("netop_agent_peer_arp_rtt_seconds", "gauge", "first ARP request to the peer's answer, last verification");
+        metric("netop_agent_peer_arp_rtt_seconds", "gauge", "ARP round trip to the peer: last request to its answer");
         for (auto& n : nics_)
             if (n.peer_verified)
                 o += strfmt("netop_agent_peer_arp_rtt_seconds{nic=\"%s\"} %.9f\n", httpd::escape_label(n.ifname).c_str(),
                             double(n.peer_rtt_ns) / 1e9);
+        metric("netop_agent_peer_verify_seconds", "gauge", "time to verify the peer: first ARP request to its answer");
+        for (auto& n : nics_)
+            if (n.peer_verified)
+                o += strfmt("netop_agent_peer_verify_seconds{nic=\"%s\"} %.9f\n", httpd::escape_label(n.ifname).c_str(),
+                            double(n.peer_verify_ns) / 1e9);
+        metric("netop_agent_peer_mac_mismatch", "gauge",
+               "1 when the peer answered ARP from another MAC than its LLDP ChassisID/PortID MAC");
+        for (auto& n : nics_)
+            if (n.peer_verified)
+                o += strfmt("netop_agent_peer_mac_mismatch{nic=\"%s\"} %d\n", httpd::escape_label(n.ifname).c_str(),
+                            n.peer_mac_mismatch ? 1 : 0);
     }
     if (cfg_.xgmi_expect_links >= 0) {
         metric("netop_agent_xgmi_pairs", "gauge", "GPU pairs with an xGMI link (KFD topology)");
@@ -1482,10 +1493,19 @@ int Agent::verify_peers(const std::vector<NicState*>& which, int64_t timeout_ns,
         n.peer_verified = p.answered;
         if (p.answered) {
             n.peer_rtt_ns = p.rtt_ns;
+            n.peer_verify_ns = p.verify_ns;
             n.peer_arp_mac = p.peer_mac;
             n.peer_error.clear();
-            NLOG_V(1, "interface '%s': peer %s (%s) answered ARP after %.3f ms", n.ifname.c_str(), p.peer.str().c_str(),
-                   p.peer_mac.str().c_str(), double(p.rtt_ns) / 1e6);
+            NLOG_V(1, "interface '%s': peer %s (%s) answered ARP: rtt %.3f ms, verified after %.3f ms", n.ifname.c_str(),
+                   p.peer.str().c_str(), p.peer_mac.str().c_str(), double(p.rtt_ns) / 1e6, double(p.verify_ns) / 1e6);
+            // The LLDP peer MAC (PortID MAC over ChassisID MAC, reference pkg/lldp/client.go:114-129)
+            // is the switch port; an ARP answer from elsewhere deserves a look, not a failure.
+            const bool mismatch = n.peer_mac && !(*n.peer_mac == p.peer_mac);
+            if (mismatch && !n.peer_mac_mismatch)
+                NLOG_W("interface '%s': peer %s answered ARP from %s, but its LLDP MAC is %s (proxy ARP or a "
+                       "misaddressed port?)", n.ifname.c_str(), p.peer.str().c_str(), p.peer_mac.str().c_str(),
+                       n.peer_mac->str().c_str());
+            n.peer_mac_mismatch = mismatch;
             continue;
         }
         ++failed;

@@ -142,6 +142,15 @@ int Prober::socket_for(int ifindex) {
     return fd;
 }
 
+bool answers(const Probe& p, const Reply& r) { return r.sender_ip == p.peer && r.target_ip == p.local; }
+
+void record_answer(Probe& p, const Reply& r, int64_t now, int64_t first_sent, int64_t last_sent) {
+    p.answered = true;
+    p.peer_mac = r.sender_mac;
+    p.verify_ns = first_sent ? now - first_sent : 0;
+    p.rtt_ns = last_sent ? now - last_sent : p.verify_ns;
+}
+
 bool Prober::probe(std::vector<Probe>& probes, int64_t timeout_ns, int64_t retry_ns, int stop_fd) {
     Fd ep{::epoll_create1(EPOLL_CLOEXEC)};
     if (ep.fd < 0) throw_errno("epoll_create1");
@@ -154,7 +163,7 @@ bool Prober::probe(std::vector<Probe>& probes, int64_t timeout_ns, int64_t retry
     uint8_t buf[256];
     const int64_t t0 = mono_ns();
     std::vector<int> fds(probes.size(), -1);
-    std::vector<int64_t> first_sent(probes.size(), 0);
+    std::vector<int64_t> first_sent(probes.size(), 0), last_sent(probes.size(), 0);
     for (size_t i = 0; i < probes.size(); ++i) {
         Probe& p = probes[i];
         p.answered = false;
@@ -186,7 +195,8 @@ bool Prober::probe(std::vector<Probe>& probes, int64_t timeout_ns, int64_t retry
                 if (p.answered || !p.error.empty()) continue;
                 const int err = send_request(fds[i], p);
                 if (err == 0) {
-                    if (p.requests++ == 0) first_sent[i] = mono_ns();
+                    last_sent[i] = mono_ns();
+                    if (p.requests++ == 0) first_sent[i] = last_sent[i];
                 } else if (err != ENETDOWN && err != ENXIO && err != ENOBUFS && err != EAGAIN) {
                     // (a link that is down may come back within the timeout: those retry)
                     p.error = "sendto(ARP) " + p.ifname + ": " + std::strerror(err);
@@ -210,10 +220,8 @@ bool Prober::probe(std::vector<Probe>& probes, int64_t timeout_ns, int64_t retry
                 ssize_t n = ::recv(fds[i], buf, sizeof buf, MSG_DONTWAIT);
                 if (n < 0) break;  // EAGAIN: drained
                 auto r = parse_reply(buf, size_t(n));
-                if (!r || p.answered || r->sender_ip != p.peer) continue;
-                p.answered = true;
-                p.peer_mac = r->sender_mac;
-                p.rtt_ns = mono_ns() - (first_sent[i] ? first_sent[i] : t0);
+                if (!r || p.answered || !answers(p, *r)) continue;
+                record_answer(p, *r, mono_ns(), first_sent[i] ? first_sent[i] : t0, last_sent[i]);
             }
         }
     }

@@ -513,7 +513,9 @@ std::string generate_status(const std::vector<NicState>& nics, const std::map<st
         if (n->peer_verified) {
             j.key("peer_verified").value(true);
             j.key("peer_arp_ms").value(double(n->peer_rtt_ns) / 1e6);
+            j.key("peer_verify_ms").value(double(n->peer_verify_ns) / 1e6);
             if (n->peer_arp_mac) j.key("peer_arp_mac").value(n->peer_arp_mac->str());
+            if (n->peer_mac_mismatch) j.key("peer_mac_mismatch").value(true);
         }
         if (!n->peer_error.empty()) j.key("peer_error").value(n->peer_error);
         if (n->gid_index) j.key("gid_index").value(*n->gid_index);

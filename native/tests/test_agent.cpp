@@ -1265,6 +1265,7 @@ namespace {
 // A switch whose ports answer ARP except those in `silent`; records what was asked.
 struct FakeArpSwitch {
     std::set<std::string> silent;
+    std::set<std::string> proxy;  // ports answering from another MAC than their LLDP one
     std::vector<std::pair<std::string, std::string>> asked;  // (ifname, peer)
     std::vector<int64_t> timeouts;                           // per probe_all call
     bool operator()(std::vector<arp::Probe>& ps, int64_t timeout_ns, int64_t, int) {
@@ -1275,7 +1276,10 @@ struct FakeArpSwitch {
             if (silent.count(p.ifname)) continue;
             p.answered = true;
             p.rtt_ns = 120000;
-            p.peer_mac = *MacAddr::parse("02:aa:00:00:00:99");
+            p.verify_ns = 220000;
+            // the switch port's own MAC (Fixture: 02:aa:00:00:00:0k for ensk), or a proxy's
+            p.peer_mac = *MacAddr::parse(proxy.count(p.ifname) ? "02:aa:00:00:00:99"
+                                                               : "02:aa:00:00:00:0" + p.ifname.substr(3));
         }
         return true;
     }
@@ -1302,6 +1306,52 @@ TEST(agent_verify_peers_all_answer) {
     const std::string m = a.render_metrics();
     CHECK(m.find("netop_agent_peer_verified{nic=\"ens1\"} 1") != std::string::npos);
     CHECK(m.find("netop_agent_peer_arp_rtt_seconds{nic=\"ens2\"} 0.000120000") != std::string::npos);
+    CHECK(m.find("netop_agent_peer_verify_seconds{nic=\"ens2\"} 0.000220000") != std::string::npos);
+    CHECK(m.find("netop_agent_peer_mac_mismatch{nic=\"ens0\"} 0") != std::string::npos);
+    CHECK(st->find("\"peer_verify_ms\":0.22") != std::string::npos && st->find("peer_mac_mismatch") == std::string::npos);
+}
+
+TEST(agent_verify_peers_flags_a_proxy_arp_answer) {
+    // The ARP answer comes from another MAC than the LLDP peer's: flagged, not fatal.
+    Fixture f;
+    f.cfg.keep_running = true;
+    f.cfg.verify_peers_ns = 500000000;
+    Pipe stop;
+    stop.fire();
+    FakeArpSwitch swi;
+    swi.proxy = {"ens1"};
+    agent::Agent a(f.cfg, f.ops, f.all_valid(), f.nm());
+    a.arp_probe = [&](std::vector<arp::Probe>& ps, int64_t t, int64_t r, int s) { return swi(ps, t, r, s); };
+    a.run(stop.fd[0]);
+    CHECK(a.ready());
+    const std::string m = a.render_metrics();
+    CHECK(m.find("netop_agent_peer_mac_mismatch{nic=\"ens1\"} 1") != std::string::npos);
+    CHECK(m.find("netop_agent_peer_mac_mismatch{nic=\"ens2\"} 0") != std::string::npos);
+    auto st = read_file(f.cfg.status_file);
+    CHECK(st && st->find("\"peer_arp_mac\":\"02:aa:00:00:00:99\",\"peer_mac_mismatch\":true") != std::string::npos);
+}
+
+TEST(arp_reply_must_answer_our_own_address) {
+    arp::Probe p;
+    p.local = *Ipv4::parse("10.200.0.1");
+    p.peer = *Ipv4::parse("10.200.0.2");
+    arp::Reply r;
+    r.sender_mac = *MacAddr::parse("02:aa:00:00:00:00");
+    r.sender_ip = p.peer;
+    r.target_ip = p.local;
+    CHECK(arp::answers(p, r));
+    r.target_ip = *Ipv4::parse("10.200.0.5");  // aimed at another local address (another NIC)
+    CHECK(!arp::answers(p, r));
+    r.target_ip = p.peer;  // gratuitous: target = sender
+    CHECK(!arp::answers(p, r));
+    r.target_ip = p.local;
+    r.sender_ip = *Ipv4::parse("10.200.0.6");  // someone else's peer
+    CHECK(!arp::answers(p, r));
+    // RTT vs time to verify: requests at t=1000 (first) and t=5000 (last), answer at t=5300.
+    r.sender_ip = p.peer;
+    arp::record_answer(p, r, 5300, 1000, 5000);
+    CHECK(p.answered && p.rtt_ns == 300 && p.verify_ns == 4300);
+    CHECK_EQ(p.peer_mac.str(), std::string("02:aa:00:00:00:00"));
 }
 
 TEST(agent_verify_peers_silent_peer_blocks_readiness) {
