@@ -156,3 +156,60 @@ def test_agent_image_runtime_stage_runs_in_its_own_rootfs(tmp_path):
     st = json.loads((root / "var/lib/amd-network/status.json").read_text())
     assert st["dry_run"] == "true" and [i["name"] for i in st["interfaces"]] == ["lo"]
     assert (root / "var/lib/amd-network/topo.xml").read_text().startswith("<system")
+
+
+@pytest.mark.skipif(not hasattr(os, "geteuid") or os.geteuid() != 0, reason="chroot needs root")
+def test_validation_image_file_set_runs_in_its_own_rootfs(tmp_path):
+    """The validation image (build/Dockerfile.validation), without docker: a root filesystem
+    holding the Python interpreter and its standard library only (the ROCm base image has no
+    PyTorch, PyYAML or pip packages) plus exactly what the runtime stage copies.  The
+    ENTRYPOINT must answer --help there, and check 1's topology discovery must run on a fake
+    node through the in-tree native module."""
+    import re
+
+    from network_operator_amd.testing import fakesysfs
+
+    df = (ROOT / "build" / "Dockerfile.validation").read_text()
+    final = df.rsplit("\nFROM ", 1)[1]
+    copies = re.findall(r"^COPY --from=builder /src/(\S+) (\S+)$", final, re.M)
+    assert copies == [("network_operator_amd", "/opt/netop/network_operator_amd")], copies
+    pypath = re.search(r"^ENV PYTHONPATH=(\S+)$", final, re.M).group(1)
+    entry = json.loads(re.search(r"^ENTRYPOINT (\[.*\])$", final, re.M).group(1))
+    assert entry[:3] == ["python3", "-m", "network_operator_amd.validate"]
+    root = tmp_path / "rootfs"
+    for src, dst in copies:
+        shutil.copytree(ROOT / src, root / dst.lstrip("/"), symlinks=True,
+                        ignore=shutil.ignore_patterns("__pycache__"))
+    # the interpreter, its stdlib (no site / dist-packages) and the libraries they load
+    py = os.path.realpath(shutil.which("python3"))
+    stdlib = Path(os.path.dirname(os.__file__))
+    shutil.copytree(stdlib, root / str(stdlib).lstrip("/"), symlinks=True,
+                    ignore=shutil.ignore_patterns("__pycache__", "dist-packages", "site-packages", "test", "idlelib",
+                                                  "tkinter", "turtledemo"))
+    (root / "usr/bin").mkdir(parents=True, exist_ok=True)
+    shutil.copy2(py, root / "usr/bin/python3")
+    elfs = [Path(py)] + sorted((stdlib / "lib-dynload").glob("*.so")) + [
+        p for p in (root / "opt/netop/network_operator_amd/_lib").glob("*.so")]
+    for e in elfs:
+        for lib in _ldd(e).values():
+            t = root / lib.lstrip("/")
+            if not t.exists():
+                t.parent.mkdir(parents=True, exist_ok=True)
+                shutil.copy2(os.path.realpath(lib), t)
+    if Path("/lib64").is_symlink() and not (root / "lib64").exists():
+        (root / "lib64").symlink_to(os.readlink("/lib64"))
+    fakesysfs.build_mi355x_node(root / "sys-fake")
+    (root / "tmp").mkdir(exist_ok=True)
+    env = {"PATH": "/usr/bin:/bin", "PYTHONPATH": pypath, "PYTHONNOUSERSITE": "1"}
+
+    def enter():
+        os.chroot(str(root))
+        os.chdir("/")
+
+    r = subprocess.run([*entry, "--help"], capture_output=True, text=True, timeout=60, env=env, preexec_fn=enter)
+    assert r.returncode == 0 and "--artifact-dir" in r.stdout, r.stderr[-2000:]
+    code = ("import sys; from network_operator_amd.models.topology import NodeTopology; "
+            "t = NodeTopology.discover('/sys-fake/'); print(len(t.gpus), len(t.pairs), t.xgmi.pairs_connected); "
+            "assert 'torch' not in sys.modules and 'yaml' not in sys.modules")
+    r = subprocess.run(["python3", "-c", code], capture_output=True, text=True, timeout=60, env=env, preexec_fn=enter)
+    assert r.returncode == 0 and r.stdout.split() == ["8", "8", "28"], (r.stdout, r.stderr[-2000:])
