@@ -72,7 +72,11 @@ struct Config {
     std::string socket_ifname = "auto";
     std::string status_file;             // --status-file (JSON)
     std::string nm_keyfile_dir;          // --nm-keyfile-dir
-    bool nm_restore = true;              // --nm-restore: Managed=true again on exit
+    // --nm-restore: on exit, remove the keyfile and set Managed=true again.  Off by default: an
+    // agent exits on every rolling update, drain and reboot, and NetworkManager must not reclaim
+    // the scale-out NICs (and start DHCP on them) before the next agent runs; the reference
+    // leaves Managed=false in place too.  For handing the NICs back when the policy goes.
+    bool nm_restore = false;
     int xgmi_expect_links = -1;          // -1 off; 0 = full mesh among discovered GPUs; N = exact pairs
     int64_t link_wait_ns = 3LL * 1000000000;  // netlink echo wait (network.go:251)
     // The RDMA core adds the RoCE v2 GID of a new IPv4 address asynchronously (netdev notifier
@@ -271,12 +275,6 @@ class Agent {
     topo::DiscoveryResult disc_;
     double cpu_ms_at_ready_ = -1;  // user + system CPU of the process when the label went up
     std::vector<std::string> dry_run_missing_;  // discovered, but not in this network namespace
-    struct TopoWorker {  // the topology thread's Linux tid, for its priority
-        std::mutex mu;
-        pid_t tid = 0;
-        bool running = false;
-    };
-    std::shared_ptr<TopoWorker> topo_worker_;
     std::future<TopoResult> topo_future_;
     std::optional<TopoResult> topo_;
     topo::XgmiReport xgmi_;

@@ -193,13 +193,14 @@ void Agent::post_cleanups() {
 }
 
 void Agent::restore_network_manager() {
-    // The reference's Managed=false is runtime-only and left behind; this agent also persisted it
-    // in a keyfile, so undo both: after the policy is gone the NICs belong to the host again.
+    // Only with --nm-restore: the reference leaves its runtime Managed=false behind, and this
+    // agent's keyfile keeps the NICs unmanaged across agent restarts and reboots (Config::nm_restore).
+    if (!cfg_.nm_restore) return;
     if (nm_keyfile_written_ && nm::remove_keyfile(cfg_.nm_keyfile_dir)) {
         NLOG_I("Removed NetworkManager keyfile from %s", cfg_.nm_keyfile_dir.c_str());
         nm_keyfile_written_ = false;
     }
-    if (nm_unmanaged_.empty() || !cfg_.nm_restore) return;
+    if (nm_unmanaged_.empty()) return;
     try {
         auto nmapi = nm_factory_();
         nm::restore_for_interfaces(*nmapi, nm_unmanaged_);
@@ -938,54 +939,39 @@ void Agent::start_topo() {
     if (cfg_.rccl_topo.empty() || topo_future_.valid() || topo_) return;
     std::string root = cfg_.sysfs_root.empty() ? topo::sysfs_root() : cfg_.sysfs_root;
     // Inputs are copied: the worker shares nothing with the agent thread.
-    auto worker = std::make_shared<TopoWorker>();
-    topo_worker_ = worker;
     const int main_cpu = ::sched_getcpu();
     auto work = [disc = disc_, interfaces = cfg_.interfaces, root = std::move(root), path = cfg_.rccl_topo,
-                 worker, main_cpu] {
-        // Off the agent thread's CPU: at idle priority on the same CPU it would only run when the
+                 main_cpu](bool background) {
+        if (!background) return make_topology(disc, interfaces, root, path);  // on the agent thread
+        // Off the agent thread's CPU: at low priority on the same CPU it would only run when the
         // agent thread blocks (measured: the join then waited ~4 ms in L3).
         cpu_set_t set;
         if (main_cpu >= 0 && ::sched_getaffinity(0, sizeof set, &set) == 0 && CPU_COUNT(&set) > 1) {
             CPU_CLR(main_cpu, &set);
             (void)::sched_setaffinity(0, sizeof set, &set);
         }
-        // Background priority (SCHED_IDLE): on a busy or CPU-limited node the critical path
-        // (discovery, link-up, LLDP) runs first and this fills its gaps instead of competing with
-        // it.  Measured in the netns harness, 8 NICs, L3: total_ready +5.6 ms over no topology file
-        // at normal priority, +1 ms at SCHED_IDLE.  topo_xml() raises it back before it waits.
-        {
-            std::lock_guard<std::mutex> lk(worker->mu);
-            worker->tid = pid_t(::syscall(SYS_gettid));
-            worker->running = true;
-            sched_param sp{};
-            (void)::sched_setscheduler(worker->tid, SCHED_IDLE, &sp);
-        }
-        struct Done {
-            TopoWorker& w;
-            ~Done() {
-                std::lock_guard<std::mutex> lk(w.mu);
-                w.running = false;
-            }
-        } done{*worker};
+        // Background priority: on a busy or CPU-limited node the critical path (discovery,
+        // link-up, LLDP) runs first and this fills its gaps instead of competing with it.
+        // nice 19 under SCHED_OTHER, not SCHED_IDLE: the agent never has to raise it again
+        // (leaving SCHED_IDLE or lowering a nice value needs CAP_SYS_NICE, which the DaemonSet
+        // does not grant), and when the agent thread blocks on the result this thread gets the
+        // whole CPU quota of the container anyway.  Measured in the netns harness, 8 NICs, L3:
+        // total_ready +5.6 ms over no topology file at normal priority, +1 ms at idle priority.
+        if (::setpriority(PRIO_PROCESS, pid_t(::syscall(SYS_gettid)), 19) != 0)
+            NLOG_V(2, "topology worker: setpriority(19): %s", std::strerror(errno));
         return make_topology(disc, interfaces, root, path);
     };
     try {
-        topo_future_ = std::async(std::launch::async, work);
+        topo_future_ = std::async(std::launch::async, work, true);
     } catch (const std::system_error& e) {  // no thread to spare: generate it when it is needed
         NLOG_V(2, "topology worker thread unavailable (%s): generating on demand", e.what());
-        topo_future_ = std::async(std::launch::deferred, work);
+        topo_future_ = std::async(std::launch::deferred, work, false);
     }
 }
 
 const std::string& Agent::topo_xml() {
     if (!topo_) {
         if (!topo_future_.valid()) start_topo();
-        if (auto w = topo_worker_) {  // we are about to wait for it: normal priority again
-            std::lock_guard<std::mutex> lk(w->mu);
-            sched_param sp{};
-            if (w->running) (void)::sched_setscheduler(w->tid, SCHED_OTHER, &sp);
-        }
         try {
             topo_ = topo_future_.get();
             // The worker's interface list is the agent's (same discovery); kept as a guard.
@@ -1626,6 +1612,10 @@ void Agent::monitor(int stop_fd) {
             // retries; the node stays unlabelled).  Monitoring on would otherwise stay degraded for good.
             NLOG_W("Interface '%s' was removed: cleaning up and exiting so that a restarted agent discovers the node again",
                    removed.c_str());
+            // Its rail rule is not tied to the link and would outlive it (its routes went with the
+            // link): remove what was installed for it before forgetting the NIC.
+            for (auto& n : nics_)
+                if (n.ifname == removed) remove_rail_routing(n);
             nics_.erase(std::remove_if(nics_.begin(), nics_.end(), [&](const NicState& n) { return n.ifname == removed; }),
                         nics_.end());
             ready_ = false;

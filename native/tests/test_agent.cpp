@@ -535,6 +535,7 @@ TEST(agent_networkmanager_paths) {
 TEST(agent_networkmanager_changes_undone_on_sigterm) {
     Fixture f;
     f.cfg.disable_nm = true;
+    f.cfg.nm_restore = true;
     f.cfg.nm_keyfile_dir = f.tmp.path + "/NetworkManager/conf.d";
     f.tmp.mkdir("NetworkManager");
     std::map<std::string, bool> seen;
@@ -547,10 +548,11 @@ TEST(agent_networkmanager_changes_undone_on_sigterm) {
     CHECK(!path_exists(f.cfg.nm_keyfile_dir + "/99-amd-network-operator.conf"));
     CHECK(seen["ens0"] && seen["ens1"] && seen["eth9"]);
 
-    // --nm-restore=false keeps the runtime change (reference behaviour), still drops the file.
+    // By default (--nm-restore=false) both stay: an ordinary restart (rolling update, drain,
+    // reboot) must not hand the NICs back to NetworkManager (reference behaviour for Managed).
     Fixture g;
     g.cfg.disable_nm = true;
-    g.cfg.nm_restore = false;
+    CHECK(!g.cfg.nm_restore);
     g.cfg.nm_keyfile_dir = g.tmp.path + "/NetworkManager/conf.d";
     g.tmp.mkdir("NetworkManager");
     std::map<std::string, bool> seen2;
@@ -558,8 +560,9 @@ TEST(agent_networkmanager_changes_undone_on_sigterm) {
     stop2.fire();
     agent::Agent b(g.cfg, g.ops, g.all_valid(), g.nm(&seen2));
     b.run(stop2.fd[0]);
-    CHECK(!path_exists(g.cfg.nm_keyfile_dir + "/99-amd-network-operator.conf"));
+    CHECK(path_exists(g.cfg.nm_keyfile_dir + "/99-amd-network-operator.conf"));
     CHECK(!seen2["ens0"] && !seen2["ens1"] && seen2["eth9"]);
+    ::unlink((g.cfg.nm_keyfile_dir + "/99-amd-network-operator.conf").c_str());
 
     // A file of that name the agent did not write is never deleted.
     g.tmp.write("NetworkManager/conf.d/99-amd-network-operator.conf", "[keyfile]\nunmanaged-devices=mac:aa\n");
@@ -1205,12 +1208,15 @@ TEST(agent_topology_file_reused_within_a_boot) {
 TEST(agent_monitor_exits_when_a_nic_is_removed) {
     Fixture f;
     f.cfg.monitor_tick_ns = 1000000;
+    f.cfg.rail_table_base = 100;  // per-rail rules: the removed NIC's must not outlive it
+    bool had_rules = false;
     Pipe stop;
     agent::Agent a(f.cfg, f.ops, f.all_valid(), f.nm());
     bool labelled_before = false;
     a.on_monitor_tick = [&](int tick) {
         if (tick == 1) {
             labelled_before = path_exists(f.cfg.labels.path());
+            had_rules = f.ops.rules.size() == 3;
             auto l = f.ops.links["ens2"];
             f.ops.links.erase("ens2");  // driver reload: the netdev is gone (it returns as a new ifindex)
             f.ops.addrs.erase(std::remove_if(f.ops.addrs.begin(), f.ops.addrs.end(),
@@ -1231,6 +1237,8 @@ TEST(agent_monitor_exits_when_a_nic_is_removed) {
     CHECK(threw);
     CHECK(!path_exists(f.cfg.labels.path()));
     CHECK(f.ops.addrs.empty());  // the other NICs were cleaned up too
+    CHECK(had_rules);
+    CHECK(f.ops.rules.empty());  // the removed NIC's rail rule included
     CHECK(!a.ready());
 }
 

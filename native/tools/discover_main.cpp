@@ -67,7 +67,7 @@ int main(int argc, char** argv) {
     fs.add_string("rccl-env-extra", &cfg.rccl_env_extra, "site settings appended to the RCCL environment file: KEY=VALUE[,...] (NCCL_*, RCCL_*, HSA_*)");
     fs.add_string("status-file", &cfg.status_file, "write a JSON status document (per-NIC results, phase timings)");
     fs.add_string("nm-keyfile-dir", &cfg.nm_keyfile_dir, "with --disable-networkmanager, also persist an unmanaged-devices keyfile here (removed on exit)");
-    fs.add_bool("nm-restore", &cfg.nm_restore, "with --disable-networkmanager: set the interfaces managed by NetworkManager again on exit");
+    fs.add_bool("nm-restore", &cfg.nm_restore, "with --disable-networkmanager: on exit, remove the keyfile and set the interfaces managed by NetworkManager again (default: they stay unmanaged across restarts)");
     fs.add_int("xgmi-expect", &cfg.xgmi_expect_links, "verify the xGMI mesh before labelling: -1 off, 0 full mesh, N GPU pairs");
     fs.add_duration("link-wait", &cfg.link_wait_ns, "time to wait for link state echoes from the kernel");
     fs.add_duration("verify-peers", &cfg.verify_peers_ns,

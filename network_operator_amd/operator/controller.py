@@ -20,7 +20,7 @@ from .informer import Informer, controller_of
 from .kube import ApiClient
 from .metrics import OperatorMetrics
 from .reconciler import (OWNER_KEY, VALIDATION_APP, EventRecorder, NetworkClusterPolicyReconciler,
-                         daemonset_owner_index, policy_owner_index)
+                         daemonset_owner_index, job_owner_index, policy_owner_index)
 from .workqueue import RateLimitingQueue
 
 log = logging.getLogger("controller")
@@ -50,6 +50,9 @@ class PolicyController:
         # Fabric validation Jobs (amdScaleOut.validation): their outcome is the FabricValidated condition.
         self.jobs = Informer(client, kube.JOBS, namespace=namespace, label_selector=f"app={VALIDATION_APP}")
         self.jobs.add_index(OWNER_KEY, policy_owner_index)
+        # Their Pods: a Pod the kubelet refused to run is not a validation verdict.
+        self.job_pods = Informer(client, kube.PODS, namespace=namespace, label_selector=f"app={VALIDATION_APP}")
+        self.job_pods.add_index(OWNER_KEY, job_owner_index)
         self.queue = RateLimitingQueue(CONTROLLER_NAME)
         self.reconciler = NetworkClusterPolicyReconciler(
             client, namespace, is_openshift,
@@ -57,11 +60,13 @@ class PolicyController:
             list_owned=lambda name: self.daemonsets.by_index(OWNER_KEY, name),
             recorder=EventRecorder(client, namespace) if record_events else None,
             list_pods=lambda ds: self.pods.by_index(OWNER_KEY, ds),
-            list_jobs=lambda name: self.jobs.by_index(OWNER_KEY, name))
+            list_jobs=lambda name: self.jobs.by_index(OWNER_KEY, name),
+            list_job_pods=lambda job: self.job_pods.by_index(OWNER_KEY, job))
         self.policies.add_handler(self._on_policy)
         self.daemonsets.add_handler(self._on_daemonset)
         self.pods.add_handler(self._on_pod)
         self.jobs.add_handler(self._on_job)
+        self.job_pods.add_handler(self._on_job_pod)
         self._tasks: List[asyncio.Task] = []
         self.reconciles = 0
         self._pod_seen: Dict[str, float] = {}  # agent Pod uid -> monotonic time first seen, until Ready
@@ -87,6 +92,14 @@ class PolicyController:
         ref = controller_of(obj)
         if ref and ref.get("kind") == T.KIND:
             await self._enqueue(ref["name"])
+
+    async def _on_job_pod(self, ev: str, obj: dict, old: Optional[dict]) -> None:
+        ref = controller_of(obj)
+        if ref and ref.get("kind") == "Job":
+            job = self.jobs.get(ref["name"], self.namespace)
+            owner = controller_of(job) if job else None
+            if owner and owner.get("kind") == T.KIND:
+                await self._enqueue(owner["name"])
 
     def _observe_readiness(self, policy: str, ev: str, obj: dict, old: Optional[dict]) -> None:
         uid = obj.get("metadata", {}).get("uid", "")
@@ -166,13 +179,14 @@ class PolicyController:
         self._tasks.append(self.daemonsets.start())
         self._tasks.append(self.pods.start())
         self._tasks.append(self.jobs.start())
+        self._tasks.append(self.job_pods.start())
         await asyncio.gather(self.policies.synced.wait(), self.daemonsets.synced.wait(), self.pods.synced.wait(),
-                             self.jobs.synced.wait())
+                             self.jobs.synced.wait(), self.job_pods.synced.wait())
         for _ in range(self.workers):
             self._tasks.append(asyncio.ensure_future(self._worker()))
 
     def has_synced(self) -> bool:
-        return all(i.synced.is_set() for i in (self.policies, self.daemonsets, self.pods, self.jobs))
+        return all(i.synced.is_set() for i in (self.policies, self.daemonsets, self.pods, self.jobs, self.job_pods))
 
     async def stop(self) -> None:
         await self.queue.shutdown()

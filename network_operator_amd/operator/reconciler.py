@@ -26,6 +26,7 @@ Kubernetes Events are emitted (RBAC for them was granted but unused by the refer
 from __future__ import annotations
 
 import copy
+import time
 import logging
 from dataclasses import dataclass
 from typing import Callable, List, Optional
@@ -84,6 +85,14 @@ def policy_owner_index(obj: dict) -> List[str]:
     """indexDaemonSets (:364-383): DaemonSets -> name of the owning NetworkClusterPolicy."""
     for ref in obj.get("metadata", {}).get("ownerReferences", []) or []:
         if ref.get("controller") and ref.get("apiVersion") == T.API_VERSION and ref.get("kind") == T.KIND:
+            return [ref["name"]]
+    return []
+
+
+def job_owner_index(obj: dict) -> List[str]:
+    """Pods -> name of the owning Job (the validation Jobs' Pods)."""
+    for ref in obj.get("metadata", {}).get("ownerReferences", []) or []:
+        if ref.get("controller") and ref.get("apiVersion") == "batch/v1" and ref.get("kind") == "Job":
             return [ref["name"]]
     return []
 
@@ -379,15 +388,62 @@ def policy_conditions(current: List[dict], targets: int, ready: int, errors: Lis
 # ---------------------------------------------------------------------------------------------
 # Fabric validation Jobs (amdScaleOut.validation, MI355X addition)
 # ---------------------------------------------------------------------------------------------
-def validation_job_name(policy: str, node: str, generation: int) -> str:
-    """DNS-1123, <= 63 characters, unique per (policy, node, policy generation)."""
+AGENT_EPOCH_ANN = "amd.com/agent-ready-since"  # the agent readiness the Job validates
+ATTEMPT_ANN = "amd.com/attempt"                # re-runs of a Job the kubelet did not admit
+# Pod status reasons of a validation Pod the kubelet refused to run (it never validated
+# anything): the GPUs are allocated to workloads (OutOfamd.com/gpu), a device plugin error
+# (UnexpectedAdmissionError), the node no longer fits, or it was evicted / preempted.
+NOT_ADMITTED_REASONS = ("OutOf", "UnexpectedAdmissionError", "NodeAffinity", "NodeName", "NodePorts", "Evicted",
+                        "Preempting", "Terminated", "Shutdown")
+NOT_ADMITTED_RETRY_S = (30.0, 600.0)  # back-off base and cap of re-running a Job that was not admitted
+
+
+def validation_job_name(policy: str, node: str, generation: int, epoch: str = "", attempt: int = 0) -> str:
+    """DNS-1123, <= 63 characters, unique per (policy, node, policy generation, agent readiness,
+    attempt): a re-run never collides with the Job it replaces while that one is being deleted."""
     import hashlib
 
     h = hashlib.sha256(f"{policy}/{node}".encode()).hexdigest()[:10]
-    return f"{policy[:36].rstrip('-')}-val-{h}-g{generation}"
+    name = f"{policy[:30].rstrip('-')}-val-{h}-g{generation}"
+    if epoch or attempt:
+        name += "-" + hashlib.sha256(f"{epoch}/{attempt}".encode()).hexdigest()[:6]
+    return name
 
 
-def validation_job(p: T.NetworkClusterPolicy, node: str, generation: int, namespace: str) -> dict:
+def agent_epoch(pod: dict) -> str:
+    """When the node's agent last became Ready: the Pod uid and its Ready condition's
+    lastTransitionTime.  A new value (agent restarted, fault cleared, Pod replaced) means the
+    node's fabric may differ from what an earlier validation saw."""
+    ready = next((c for c in (pod.get("status") or {}).get("conditions") or [] if c.get("type") == "Ready"), {})
+    return f"{pod.get('metadata', {}).get('uid', '')}@{ready.get('lastTransitionTime', '')}"
+
+
+def job_not_admitted(pods: List[dict]) -> Optional[str]:
+    """The kubelet's reason when it refused the Job's Pod (not a validation verdict), else None."""
+    for pod in pods:
+        st = pod.get("status") or {}
+        reason = st.get("reason") or ""
+        if st.get("phase") == "Failed" and reason.startswith(NOT_ADMITTED_REASONS):
+            msg = st.get("message") or ""
+            return f"{reason}: {msg}"[:200] if msg else reason
+    return None
+
+
+def _job_finished_at(job: dict) -> Optional[float]:
+    import datetime
+
+    for c in (job.get("status") or {}).get("conditions") or []:
+        if c.get("type") in ("Failed", "Complete") and c.get("status") == "True" and c.get("lastTransitionTime"):
+            try:
+                return datetime.datetime.strptime(c["lastTransitionTime"], "%Y-%m-%dT%H:%M:%SZ").replace(
+                    tzinfo=datetime.timezone.utc).timestamp()
+            except ValueError:
+                return None
+    return None
+
+
+def validation_job(p: T.NetworkClusterPolicy, node: str, generation: int, namespace: str, epoch: str = "",
+                   attempt: int = 0) -> dict:
     """``python -m network_operator_amd.validate`` on one node, all its GPUs, the agent's artifacts
     read-only, the label through NFD (config/validation/validation-job.yaml, pinned to a node)."""
     v = p.spec.amdScaleOut.validation or T.ValidationSpec()
@@ -397,9 +453,10 @@ def validation_job(p: T.NetworkClusterPolicy, node: str, generation: int, namesp
     labels = {"app": VALIDATION_APP, "amd.com/policy": p.name[:63]}
     return {
         "apiVersion": "batch/v1", "kind": "Job",
-        "metadata": {"name": validation_job_name(p.name, node, generation), "namespace": namespace,
+        "metadata": {"name": validation_job_name(p.name, node, generation, epoch, attempt), "namespace": namespace,
                      "labels": dict(labels),
-                     "annotations": {"amd.com/node": node, "amd.com/policy-generation": str(generation)}},
+                     "annotations": {"amd.com/node": node, "amd.com/policy-generation": str(generation),
+                                     AGENT_EPOCH_ANN: epoch, ATTEMPT_ANN: str(attempt)}},
         "spec": {
             "backoffLimit": 0,  # kept (no TTL) while the policy generation is current: its result is the status
             "template": {
@@ -472,7 +529,9 @@ class NetworkClusterPolicyReconciler:
                  get_policy: Callable[[str], Optional[dict]], list_owned: Callable[[str], List[dict]],
                  recorder: Optional[EventRecorder] = None,
                  list_pods: Optional[Callable[[str], List[dict]]] = None,
-                 list_jobs: Optional[Callable[[str], List[dict]]] = None):
+                 list_jobs: Optional[Callable[[str], List[dict]]] = None,
+                 list_job_pods: Optional[Callable[[str], List[dict]]] = None,
+                 clock: Callable[[], float] = time.time):
         self.client = client
         self.namespace = namespace
         self.is_openshift = is_openshift
@@ -483,6 +542,8 @@ class NetworkClusterPolicyReconciler:
         self._list_owned = list_owned
         self._list_pods = list_pods
         self._list_jobs = list_jobs  # validation Jobs of a policy (by its name)
+        self._list_job_pods = list_job_pods  # the Pods of a validation Job (by its name)
+        self._clock = clock
         self.recorder = recorder
 
     def _node_errors(self, ds_name: str, limit: int = 16) -> List[str]:
@@ -504,34 +565,75 @@ class NetworkClusterPolicyReconciler:
             errs = errs[:limit] + [f"... and {len(errs) - limit} more"]
         return errs
 
+    async def _delete_job(self, j: dict) -> None:
+        try:
+            await self.client.delete(kube.JOBS, j["metadata"]["name"], self.namespace)
+        except ApiError as e:
+            if not is_not_found(e):
+                raise
+
     async def _reconcile_validation(self, raw: dict, p: T.NetworkClusterPolicy, ds: dict, generation: int,
                                     errors: List[str]) -> Optional[tuple]:
-        """One validation Job per node whose agent is ready, for the policy's current generation;
-        Jobs of older generations are removed.  Returns the FabricValidated (status, reason,
-        message) or None when validation is off; failed nodes are added to `errors`."""
+        """One validation Job per node whose agent is ready, for the policy's current generation
+        and the agent's current readiness (``agent_epoch``): a Job that validated an earlier
+        readiness of the node (agent restarted, fault cleared, Pod replaced) is replaced, so a
+        failure is never stuck until the next spec change.  A Job whose Pod the kubelet refused
+        (GPUs allocated to workloads, device-plugin error) is not a verdict: it is re-created
+        after a back-off (``NOT_ADMITTED_RETRY_S``) and reported as not admitted.  Jobs of older
+        generations are removed.  Returns ((status, reason, message), requeue_after) or None
+        when validation is off; failed nodes are added to `errors`."""
         v = p.spec.amdScaleOut.validation
         if self._list_jobs is None or self._list_pods is None:
             return None
         enabled = p.spec.configurationType == T.CONFIG_AMD_SCALE_OUT and v is not None and v.enabled
+        ready_pods = {pod.get("spec", {}).get("nodeName", ""): pod for pod in self._list_pods(ds["metadata"]["name"])
+                      if any(c.get("type") == "Ready" and c.get("status") == "True"
+                             for c in (pod.get("status") or {}).get("conditions") or [])}
+        ready_pods.pop("", None)
         jobs = {}
         for j in self._list_jobs(p.name):
             ann = j["metadata"].get("annotations") or {}
+            node = ann.get("amd.com/node", "")
             if not enabled or ann.get("amd.com/policy-generation") != str(generation):
-                try:  # a result for a spec that no longer exists
-                    await self.client.delete(kube.JOBS, j["metadata"]["name"], self.namespace)
-                except ApiError as e:
-                    if not is_not_found(e):
-                        raise
+                await self._delete_job(j)  # a result for a spec that no longer exists
                 continue
-            jobs[ann.get("amd.com/node", "")] = j
+            if node in ready_pods and ann.get(AGENT_EPOCH_ANN, "") != agent_epoch(ready_pods[node]):
+                log.info("Agent on %s became ready again since validation Job %s: validating again", node,
+                         j["metadata"]["name"])
+                await self._delete_job(j)
+                continue
+            if node in jobs:  # keep the newest attempt
+                if int(ann.get(ATTEMPT_ANN, 0) or 0) <= int((jobs[node]["metadata"].get("annotations") or {})
+                                                             .get(ATTEMPT_ANN, 0) or 0):
+                    continue
+            jobs[node] = j
         if not enabled:
             return None
-        ready_nodes = sorted(pod.get("spec", {}).get("nodeName", "") for pod in self._list_pods(ds["metadata"]["name"])
-                             if any(c.get("type") == "Ready" and c.get("status") == "True"
-                                    for c in (pod.get("status") or {}).get("conditions") or []))
+        ready_nodes = sorted(ready_pods)
+        requeue_after = 0.0
+        not_admitted = {}
+        now = self._clock()
         for node in ready_nodes:
-            if node and node not in jobs:
-                job = validation_job(p, node, generation, self.namespace)
+            j = jobs.get(node)
+            attempt = 0
+            if j is not None and job_outcome(j) == "failed" and self._list_job_pods is not None:
+                why = job_not_admitted(self._list_job_pods(j["metadata"]["name"]))
+                if why:
+                    attempt = int((j["metadata"].get("annotations") or {}).get(ATTEMPT_ANN, 0) or 0)
+                    base, cap = NOT_ADMITTED_RETRY_S
+                    wait = min(base * 2 ** attempt, cap)
+                    left = (_job_finished_at(j) or now) + wait - now
+                    if left > 0:
+                        not_admitted[node] = f"{why}; retrying in {int(left + 0.999)}s"
+                        requeue_after = min(requeue_after, left) if requeue_after else left
+                        continue
+                    log.info("Validation Job %s on %s was not admitted (%s): re-creating it", j["metadata"]["name"],
+                             node, why)
+                    await self._delete_job(j)
+                    del jobs[node]
+                    attempt += 1
+            if node not in jobs:
+                job = validation_job(p, node, generation, self.namespace, agent_epoch(ready_pods[node]), attempt)
                 set_controller_reference(raw, job)
                 try:
                     await self.client.create(kube.JOBS, job, namespace=self.namespace)
@@ -541,15 +643,19 @@ class NetworkClusterPolicyReconciler:
                         raise
         # Judged over the nodes ready now: a node that left keeps its Job (and result) until the
         # next generation, but no longer counts either way.
-        outcome = {n: job_outcome(jobs[n]) for n in ready_nodes if n in jobs}
+        outcome = {n: job_outcome(jobs[n]) for n in ready_nodes if n in jobs and n not in not_admitted}
         failed = sorted(n for n, o in outcome.items() if o == "failed")
         passed = sum(1 for o in outcome.values() if o == "succeeded")
         errors += [f"{n}: fabric validation failed" for n in failed]
         if failed:
-            return ("False", "ValidationFailed", f"{len(failed)} node(s) failed: {', '.join(failed)[:900]}")
+            return ("False", "ValidationFailed", f"{len(failed)} node(s) failed: {', '.join(failed)[:900]}"), requeue_after
         if ready_nodes and passed >= len(ready_nodes):
-            return ("True", "AllNodesValidated", f"{passed}/{len(ready_nodes)} nodes validated")
-        return ("Unknown", "ValidationRunning", f"{passed}/{len(ready_nodes)} ready nodes validated")
+            return ("True", "AllNodesValidated", f"{passed}/{len(ready_nodes)} nodes validated"), requeue_after
+        if not_admitted:
+            msg = "; ".join(f"{n}: {w}" for n, w in sorted(not_admitted.items()))
+            return ("Unknown", "ValidationNotAdmitted",
+                    f"{passed}/{len(ready_nodes)} ready nodes validated; not admitted: {msg}"[:1024]), requeue_after
+        return ("Unknown", "ValidationRunning", f"{passed}/{len(ready_nodes)} ready nodes validated"), requeue_after
 
     async def _event(self, obj: dict, type_: str, reason: str, msg: str) -> None:
         if self.recorder:
@@ -623,10 +729,13 @@ class NetworkClusterPolicyReconciler:
         new_state = status_for(targets, ready)
         errors = [f"dependency missing: {d}" for d in self.missing_dependencies]
         errors += self._node_errors(ds["metadata"]["name"]) if targets and ready < targets else []
+        generation = int(raw.get("metadata", {}).get("generation", 0) or 0)
+        # Validation first: it adds its failed nodes to `errors`, and the comparison with the stored
+        # status must see the whole list (else every reconcile rewrites an unchanged status).
+        v = await self._reconcile_validation(raw, p, ds, generation, errors)
+        validated, requeue_after = v if v is not None else (None, 0.0)
         if cur.state != new_state or cur.errors != errors:
             updated = True
-        generation = int(raw.get("metadata", {}).get("generation", 0) or 0)
-        validated = await self._reconcile_validation(raw, p, ds, generation, errors)
         conditions = policy_conditions(cur.conditions, targets, ready, errors, generation)
         if validated is not None:
             now = _now_rfc3339()
@@ -636,7 +745,7 @@ class NetworkClusterPolicyReconciler:
         if conditions != cur.conditions or cur.observedGeneration != generation:
             updated = True
         if not updated:
-            return Result()
+            return Result(requeue_after=requeue_after)
         body = copy.deepcopy(raw)
         body["status"] = {"targets": targets, "ready": ready, "state": new_state, "errors": errors,
                           "conditions": conditions, "observedGeneration": generation}
@@ -654,7 +763,7 @@ class NetworkClusterPolicyReconciler:
         for e in errors:  # an agent that exited, with its reason: once per new message
             if e not in cur.errors and "scale-out not ready (" in e and "): " in e:
                 await self._event(raw, "Warning", "AgentFailed", e[:1024])
-        return Result()
+        return Result(requeue_after=requeue_after)
 
     # -- entry point -------------------------------------------------------------------------------
     async def reconcile(self, name: str) -> Result:

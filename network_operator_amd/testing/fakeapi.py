@@ -269,13 +269,29 @@ class FakeApiServer:
                         "restartCount": prev.get("restartCount", -1) + 1, "terminated": dict(terminated)}
         self._sync_daemonsets()
 
-    def set_job_result(self, name: str, namespace: str, succeeded: bool) -> None:
-        """What the Job controller records when the Job's only Pod ends (backoffLimit 0)."""
+    def set_job_result(self, name: str, namespace: str, succeeded: bool, pod_reason: Optional[str] = None,
+                       pod_message: str = "", finished: Optional[str] = None) -> None:
+        """What the Job controller records when the Job's only Pod ends (backoffLimit 0).  With
+        `pod_reason` the Pod also exists, Failed with that kubelet reason (e.g. the admission
+        rejection "OutOfamd.com/gpu"); `finished` overrides the condition's time (RFC 3339)."""
         o = self._table(kube.JOBS)[(namespace, name)]
+        if pod_reason is not None:
+            labels = dict((o["spec"]["template"].get("metadata") or {}).get("labels") or {})
+            pod = {"apiVersion": "v1", "kind": "Pod",
+                   "metadata": {"name": f"{name}-pod", "namespace": namespace, "labels": labels,
+                                "ownerReferences": [{"apiVersion": "batch/v1", "kind": "Job", "name": name,
+                                                     "uid": o["metadata"]["uid"], "controller": True}]},
+                   "spec": {"nodeName": (o["spec"]["template"].get("spec") or {}).get("nodeName", "")},
+                   "status": {"phase": "Failed", "reason": pod_reason, "message": pod_message}}
+            cur = self._table(kube.PODS).get((namespace, pod["metadata"]["name"]))
+            if cur is None:
+                self._create(kube.PODS, pod, namespace)
+            else:
+                self._store(kube.PODS, dict(copy.deepcopy(cur), status=pod["status"]), "MODIFIED")
         new = copy.deepcopy(o)
         cond = "Complete" if succeeded else "Failed"
         new["status"] = {"succeeded" if succeeded else "failed": 1,
-                         "conditions": [{"type": cond, "status": "True", "lastTransitionTime": _now()}]}
+                         "conditions": [{"type": cond, "status": "True", "lastTransitionTime": finished or _now()}]}
         self._store(kube.JOBS, new, "MODIFIED")
 
     def fail_next(self, method: str, path_regex: str, status: int = 500, count: int = 1,
@@ -422,7 +438,13 @@ class FakeApiServer:
                 self._delete(kube.PODS, pname, pns)
         for pname, node in want.items():
             ready = bool(self.node_ready.get((f"{ns}/{name}", node)))
-            cond = [{"type": "Ready", "status": "True" if ready else "False",
+            cur = pods.get((ns, pname))
+            # lastTransitionTime moves only when the condition flips (the kubelet's status manager)
+            old_ready = next((c for c in ((cur or {}).get("status") or {}).get("conditions") or []
+                              if c.get("type") == "Ready"), None)
+            since = old_ready.get("lastTransitionTime") if old_ready and \
+                (old_ready.get("status") == "True") == ready else self._transition_time()
+            cond = [{"type": "Ready", "status": "True" if ready else "False", "lastTransitionTime": since,
                      **({} if ready else {"reason": "ContainersNotReady",
                                           "message": "containers with unready status: [configurator]"})}]
             status = {"phase": "Running", "conditions": cond}
@@ -431,7 +453,6 @@ class FakeApiServer:
                 cname = ((ds["spec"]["template"].get("spec") or {}).get("containers") or [{}])[0].get("name", "agent")
                 status["containerStatuses"] = [{"name": cname, "ready": ready, "restartCount": last["restartCount"],
                                                 "lastState": {"terminated": last["terminated"]}}]
-            cur = pods.get((ns, pname))
             labels = dict((ds["spec"]["template"].get("metadata") or {}).get("labels") or {})
             if cur is None:
                 pod = {"apiVersion": "v1", "kind": "Pod",
@@ -444,6 +465,15 @@ class FakeApiServer:
                 new = copy.deepcopy(cur)
                 new["status"] = status
                 self._store(kube.PODS, new, "MODIFIED")
+
+    def _transition_time(self) -> str:
+        """RFC 3339 seconds like the API server, made unique per transition (a real cluster's
+        transitions of one Pod are seconds apart; the tests' are milliseconds)."""
+        import datetime
+
+        self._transitions = getattr(self, "_transitions", 0) + 1
+        t = datetime.datetime(2026, 1, 1, tzinfo=datetime.timezone.utc) + datetime.timedelta(seconds=self._transitions)
+        return t.strftime("%Y-%m-%dT%H:%M:%SZ")
 
     async def _auto_ready(self, ds_key: str, node: str) -> None:
         await asyncio.sleep(self.agent_ready_delay or 0)

@@ -305,7 +305,7 @@ def run_scenario(n_nics: int = 8, mode: str = "L3", seed: int | None = None, int
                  xgmi_expect: int = 0, keep_tmp: bool = False, sigterm: bool = True, verbose: int = 2,
                  drop_xgmi: list | None = None, extra_args: list | None = None, flap_port: int | None = None,
                  crash_restart: bool = False, crash_after_s: float = 0.0, gid_delay_s: float = 0.0,
-                 egress_probe: bool = False, nm_bus: bool = False, lldp_cache: bool = False,
+                 egress_probe: bool = False, nm_bus: bool = False, nm_restore: bool = True, lldp_cache: bool = False,
                  soak_cycles: int = 0, arp_silent_ports: int = 0) -> dict:
     """Runs one node bring-up.  Must already be inside a private user+net namespace.
 
@@ -388,6 +388,8 @@ def run_scenario(n_nics: int = 8, mode: str = "L3", seed: int | None = None, int
             nm = NetworkManagerOnBus(bus.address, {**{n: True for n in nic_names}, "eth9": True})
             env["DBUS_SYSTEM_BUS_ADDRESS"] = bus.address
             args += ["--disable-networkmanager", f"--nm-keyfile-dir={keyfile.parent}"]
+            if nm_restore:
+                args.append("--nm-restore")
         # The agent's log goes to a file, not a pipe nobody reads until the end: a long run
         # (soak_cycles) logs more than a pipe buffer holds and would block the agent.
         agent_log = tmp / "agent.log"

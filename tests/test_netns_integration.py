@@ -309,9 +309,9 @@ def test_without_rail_tables_sources_share_one_egress():
 
 
 def test_networkmanager_unmanaged_while_ready_and_handed_back_on_sigterm():
-    """--disable-networkmanager through a real dbus-daemon: the NICs are unmanaged (runtime
-    Managed=false + the persistent keyfile) while the node is ready; SIGTERM (policy deleted)
-    removes the keyfile and hands the NICs back (the reference leaves Managed=false behind,
+    """--disable-networkmanager --nm-restore through a real dbus-daemon: the NICs are unmanaged
+    (runtime Managed=false + the persistent keyfile) while the node is ready; SIGTERM removes the
+    keyfile and hands the NICs back (opt-in; the reference leaves Managed=false behind,
     reference cmd/discover/main.go:143-159)."""
     from network_operator_amd.testing.fakedbus import BusDaemon
 
@@ -323,3 +323,17 @@ def test_networkmanager_unmanaged_while_ready_and_handed_back_on_sigterm():
     assert r["nm_managed_while_ready"] == {**{n: False for n in r["nics"]}, "eth9": True}
     assert r["nm_keyfile_after_sigterm"] is False
     assert r["nm_managed_after_sigterm"] == {**{n: True for n in r["nics"]}, "eth9": True}
+
+
+def test_networkmanager_stays_off_the_nics_across_an_ordinary_restart():
+    """Default (the DaemonSet's args): SIGTERM from a rolling update, drain or reboot leaves the
+    keyfile and Managed=false, so NetworkManager cannot reclaim the scale-out NICs (and start DHCP
+    on them) before the next agent runs."""
+    from network_operator_amd.testing.fakedbus import BusDaemon
+
+    if not BusDaemon.available():
+        pytest.skip("dbus-daemon not installed")
+    r = netns.run_isolated(n_nics=2, seed=6, interval="30s", fast_start=True, nm_bus=True, nm_restore=False)
+    assert r["label"] and r["agent_rc"] == 0
+    assert r["nm_keyfile_after_sigterm"] is True
+    assert r["nm_managed_after_sigterm"] == {**{n: False for n in r["nics"]}, "eth9": True}

@@ -614,6 +614,68 @@ def test_fabric_validation_jobs_follow_ready_nodes_and_report_a_condition():
     run(body())
 
 
+def test_validation_job_not_admitted_is_retried_and_a_new_agent_readiness_revalidates():
+    """a validation Pod the kubelet refused (GPUs allocated to workloads:
+    OutOfamd.com/gpu) is not a fabric verdict: reported as not admitted and re-created after a
+    back-off.  A genuine failure stays until the node's agent becomes ready again (restart or
+    cleared fault), which validates the node again.  A persisting failure does not rewrite the
+    policy status on every reconcile."""
+    from network_operator_amd.operator.reconciler import AGENT_EPOCH_ANN, ATTEMPT_ANN
+
+    async def body():
+        async with cluster(openshift=False) as (fake, client, ctl):
+            fake.add_node("gpu-node-0", {"foo": "bar"})
+            await client.create(kube.NETWORKCLUSTERPOLICIES, policy(validation={"enabled": True}))
+            await eventually(lambda: fake.get_object(kube.DAEMONSETS, "policy", NS) is not None)
+            fake.set_agent_ready("gpu-node-0")
+            await eventually(lambda: len(fake.list_objects(kube.JOBS)) == 1)
+
+            def cond():
+                st = fake.get_object(kube.NETWORKCLUSTERPOLICIES, "policy").get("status") or {}
+                return {c["type"]: c for c in st.get("conditions", [])}.get("FabricValidated") or {}
+
+            # 1. Not admitted just now: reported, not a failure, retry pending.
+            j0 = fake.list_objects(kube.JOBS)[0]
+            fake.set_job_result(j0["metadata"]["name"], NS, False, pod_reason="OutOfamd.com/gpu",
+                                pod_message="Node didn't have enough resource: amd.com/gpu")
+            await eventually(lambda: cond().get("reason") == "ValidationNotAdmitted")
+            st = fake.get_object(kube.NETWORKCLUSTERPOLICIES, "policy")["status"]
+            assert cond()["status"] == "Unknown" and "OutOfamd.com/gpu" in cond()["message"]
+            assert "retrying in" in cond()["message"] and st["errors"] == []
+            assert [j["metadata"]["name"] for j in fake.list_objects(kube.JOBS)] == [j0["metadata"]["name"]]
+            # 2. Its back-off has passed (it failed long ago): a new attempt replaces it.
+            fake.set_job_result(j0["metadata"]["name"], NS, False, pod_reason="OutOfamd.com/gpu",
+                                finished="2000-01-01T00:00:00Z")
+            await eventually(lambda: [j["metadata"]["annotations"][ATTEMPT_ANN] for j in fake.list_objects(kube.JOBS)]
+                             == ["1"])
+            j1 = fake.list_objects(kube.JOBS)[0]
+            assert j1["metadata"]["name"] != j0["metadata"]["name"]
+            assert j1["metadata"]["annotations"][AGENT_EPOCH_ANN] == j0["metadata"]["annotations"][AGENT_EPOCH_ANN]
+            # 3. A genuine failure: reported, and the status is not rewritten while nothing changes.
+            fake.set_job_result(j1["metadata"]["name"], NS, False)
+            await eventually(lambda: cond().get("reason") == "ValidationFailed")
+            assert fake.get_object(kube.NETWORKCLUSTERPOLICIES, "policy")["status"]["errors"] == [
+                "gpu-node-0: fabric validation failed"]
+            writes = sum(1 for m, path in fake.requests if m == "PUT" and path.endswith("/status"))
+            for _ in range(5):  # unrelated events: every one reconciles the policy
+                await ctl.requeue_all()
+                await asyncio.sleep(0.05)
+            assert sum(1 for m, path in fake.requests if m == "PUT" and path.endswith("/status")) == writes
+            # 4. The agent restarts (not ready, then ready again): the node is validated again.
+            fake.set_agent_ready("gpu-node-0", False)
+            await eventually(lambda: fake.get_object(kube.NETWORKCLUSTERPOLICIES, "policy")["status"]["ready"] == 0)
+            fake.set_agent_ready("gpu-node-0")
+            await eventually(lambda: [j["metadata"]["name"] for j in fake.list_objects(kube.JOBS)] not in
+                             ([], [j1["metadata"]["name"]]))
+            j2 = fake.list_objects(kube.JOBS)[0]
+            assert j2["metadata"]["annotations"][AGENT_EPOCH_ANN] != j1["metadata"]["annotations"][AGENT_EPOCH_ANN]
+            await eventually(lambda: cond().get("reason") == "ValidationRunning")
+            fake.set_job_result(j2["metadata"]["name"], NS, True)
+            await eventually(lambda: cond().get("status") == "True")
+            assert fake.get_object(kube.NETWORKCLUSTERPOLICIES, "policy")["status"]["errors"] == []
+    run(body())
+
+
 def test_agent_exit_reason_quotes_the_agents_error_line():
     """The DaemonSet keeps a failed agent's log tail as its termination message
     (FallbackToLogsOnError); the policy's errors quote the agent's "Error: ..." line."""
