@@ -54,6 +54,10 @@ import time
 
 METRIC = "node scale-out-ready latency (s) + rccl all-reduce busbw GB/s at 1/2/4/8 GPU"
 STORE_KEY = "netop/bench/artifacts"
+# Test hooks (CPU rehearsal of the xGMI link check): XML files read as RCCL's topology dump of the
+# run with the artifacts / of the RCCL-defaults run.
+FAKE_DUMP_ENV = "NETOP_BENCH_FAKE_RCCL_DUMP"
+FAKE_DUMP_DEFAULTS_ENV = "NETOP_BENCH_FAKE_RCCL_DUMP_DEFAULTS"
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
@@ -619,9 +623,11 @@ def main(argv=None) -> int:
         else:
             st["artifacts"] = {"applied": False, "source": "RCCL defaults (--artifacts off)"}
         if dump_path:
-            st["artifacts"]["rccl_dump"] = (FA.read_view(dump_path, st["artifacts"].get("topo_file"))
+            # CPU rehearsal of the link check (tests): a prepared file stands in for RCCL's dump.
+            fake = os.environ.get(FAKE_DUMP_ENV if art is not None else FAKE_DUMP_DEFAULTS_ENV)
+            st["artifacts"]["rccl_dump"] = (FA.read_view(fake or dump_path, st["artifacts"].get("topo_file"))
                                             or {"error": f"RCCL wrote no topology dump to {dump_path}"}) \
-                if cuda else {"note": "gloo: no RCCL topology on the CPU rehearsal"}
+                if cuda or fake else {"note": "gloo: no RCCL topology on the CPU rehearsal"}
 
     # 6. Diagnostics, rank 0, each a child process bounded by the deadline (bench_extras.Runner).
     if rank == 0:
@@ -679,7 +685,7 @@ def main(argv=None) -> int:
 
     # 7. The link check: RCCL must see >= n-1 xGMI links per GPU under the agent's file.
     rc = 0 if verified else 1
-    if rank == 0 and cuda and art is not None:
+    if rank == 0 and (cuda or os.environ.get(FAKE_DUMP_ENV)) and art is not None:
         a = st["artifacts"]
         v = FA.links_verdict(world, a.get("rccl_dump"), (st.get("rccl_defaults") or {}).get("rccl_dump"))
         a["xgmi_links_check"] = v

@@ -377,3 +377,30 @@ def test_env_file_parsing_keeps_exact_match_prefix(tmp_path):
                                               "NCCL_MIN_NCHANNELS": "64"}
     env = {"NCCL_TOPO_FILE": "/x.xml", "NCCL_TOPO_DUMP_FILE": "/d", "PATH": "/bin"}
     assert FA.strip(env, ["NCCL_TOPO_FILE"]) == {"PATH": "/bin"}
+
+
+@pytest.mark.parametrize("lost", [False, True])
+def test_bench_fails_loudly_when_the_file_costs_xgmi_links(lost, tmp_path, node_sysfs):
+    """n > 1: RCCL's dump under the agent's file must show n-1 xGMI peers per GPU.  Rehearsed on
+    the CPU with prepared dumps standing in for RCCL's: the line is still printed, with the
+    measurement, and the run exits 1 naming the cause."""
+    g = [("0000:0a:00.0", ["0000:01:00.0"]), ("0000:23:00.0", ["0000:1c:00.0"])]
+    full = {"0000:0a:00.0": ["0000:23:00.0"], "0000:23:00.0": ["0000:0a:00.0"]}
+    (tmp_path / "with.xml").write_text(_dump(g, {} if lost else full))
+    (tmp_path / "without.xml").write_text(_dump(g, full))
+    cmd = [sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1", "--device", "cpu",
+           "--bytes", str(1 << 16), "--sweep", "", "--collectives", "", "--node-ready", "off",
+           "--sysfs-root", node_sysfs]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=tmp_path,
+                       env=_spawn_env(NETOP_BENCH_FAKE_RCCL_DUMP=str(tmp_path / "with.xml"),
+                                      NETOP_BENCH_FAKE_RCCL_DUMP_DEFAULTS=str(tmp_path / "without.xml")))
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, (r.stdout, r.stderr[-2000:])
+    j = json.loads(lines[0])
+    chk = j["agent_artifacts"]["xgmi_links_check"]
+    assert j["value"] > 0 and j["rccl_defaults"]["rccl_dump"]["min_xgmi_links"] == 1
+    if lost:
+        assert r.returncode == 1 and chk["status"] == "failed" and "costs links" in chk["why"]
+        assert j["error"].startswith("agent artifacts check failed") and "costs links" in r.stderr
+    else:
+        assert r.returncode == 0 and chk["status"] == "ok" and chk["min_with_file"] == 1 and "error" not in j
