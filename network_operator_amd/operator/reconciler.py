@@ -597,7 +597,8 @@ class NetworkClusterPolicyReconciler:
             if not enabled or ann.get("amd.com/policy-generation") != str(generation):
                 await self._delete_job(j)  # a result for a spec that no longer exists
                 continue
-            if node in ready_pods and ann.get(AGENT_EPOCH_ANN, "") != agent_epoch(ready_pods[node]):
+            if node in ready_pods and ann.get(AGENT_EPOCH_ANN, "") != agent_epoch(ready_pods[node]) \
+                    and job_outcome(j) != "running":  # a running one finishes first: no kill/restart loop on flaps
                 log.info("Agent on %s became ready again since validation Job %s: validating again", node,
                          j["metadata"]["name"])
                 await self._delete_job(j)

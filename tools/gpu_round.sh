@@ -11,6 +11,10 @@ timeout -k 10 300 python3 -c 'import __graft_entry__ as g; g.smoke()' > gpurun_o
 tail -2 gpurun_out/smoke.log
 timeout -k 10 400 python3 bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/bench.log 2>&1 || { tail -20 gpurun_out/bench.log; exit 1; }
 tail -1 gpurun_out/bench.log
+# The driver's launcher path (torchrun's agent store carries the agent's artifacts to the ranks).
+timeout -k 10 400 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 \
+  --master-port 29561 bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/bench_torchrun.log 2>&1 || { tail -20 gpurun_out/bench_torchrun.log; exit 1; }
+grep '^{' gpurun_out/bench_torchrun.log | tail -1 | head -c 600; echo
 timeout -k 10 300 network_operator_amd/_lib/netop-xgmi-probe --bytes=268435456 --iters=10 > gpurun_out/xgmi_probe.json 2>&1 || { cat gpurun_out/xgmi_probe.json; exit 1; }
 cat gpurun_out/xgmi_probe.json
 timeout -k 10 120 network_operator_amd/_lib/netop-xgmi-counters > gpurun_out/xgmi_counters.json 2>&1 && head -c 1500 gpurun_out/xgmi_counters.json && echo
