@@ -25,10 +25,13 @@ def _free_port():
 
 
 @pytest.mark.parametrize("n", [2, 4])
-def test_bench_torchrun_cpu_rehearsal(n, tmp_path):
+def test_bench_torchrun_cpu_rehearsal(n, tmp_path, node_sysfs):
+    """The driver's launcher path: torchrun's agent store carries the agent's artifacts to the
+    ranks before any communicator exists."""
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}", "--master-addr",
            "127.0.0.1", "--master-port", str(_free_port()), str(ROOT / "bench.py"), "--gpus", str(n), "--steps", "4",
-           "--warmup", "1", "--device", "cpu", "--bytes", str(1 << 20), "--sweep", "4096", "--node-ready", "off"]
+           "--warmup", "1", "--device", "cpu", "--bytes", str(1 << 20), "--sweep", "4096", "--node-ready", "off",
+           "--sysfs-root", node_sysfs]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=tmp_path,
                        env=dict(os.environ, OMP_NUM_THREADS="1"))
     assert r.returncode == 0, r.stderr[-3000:]
@@ -42,6 +45,9 @@ def test_bench_torchrun_cpu_rehearsal(n, tmp_path):
     assert j["config"]["parallelism"] == f"dp{n}"
     assert {c["op"] for c in j["collectives"]} == {"all_gather", "reduce_scatter", "all_to_all"}
     assert j["busbw_ceiling_GBps"] == pytest.approx((n - 1) * 76.0)
+    a = j["agent_artifacts"]
+    assert a["applied"] is True and a["ranks_applied"] == n and a["ranks_same_file"] is True
+    assert j["busbw_rccl_defaults_GBps"] > 0
 
 
 def _bench_line(r):
