@@ -538,7 +538,13 @@ def main(argv=None) -> int:
         host_pg = None
     esize = torch.tensor([], dtype=dtype).element_size()
     records = [None] * world
-    dist.all_gather_object(records, art["record"] if art else {"rank": rank, "applied": False}, group=host_pg)
+    mine = dict(art["record"] if art else {"rank": rank, "applied": False})
+    if cuda:
+        from network_operator_amd.parallel.rail import device_bdf
+
+        mine["bdf"] = device_bdf(local_rank)
+    dist.all_gather_object(records, mine, group=host_pg)
+    job_bdfs = [r.get("bdf") for r in records if r and r.get("bdf")]
 
     # 1. Correctness of the collective path (exact, HIP pattern kernels on the GPU).
     verified, errors = C.verify_all_reduce(min(args.bytes // 2, 64 << 20), device)
@@ -569,7 +575,8 @@ def main(argv=None) -> int:
         try:
             t = smi.traffic(smi_before, smi.snapshot())
             st["xgmi_traffic"] = {"links_up": t["links_up"], "links_with_traffic": t["links_with_traffic"],
-                                  "GB_per_gpu": [round(sum(g["bytes_per_link"]) / 1e9, 3) for g in t["gpus"]]}
+                                  "GB_per_gpu": [round(sum(g["bytes_per_link"]) / 1e9, 3) for g in t["gpus"]],
+                                  "job": FA.traffic_view(job_bdfs, t)}
         except Exception as e:
             st["smi_note"] = f"amd-smi counters unavailable: {e}"
     t = torch.tensor([dt], dtype=torch.float64, device=device)
@@ -687,7 +694,8 @@ def main(argv=None) -> int:
     rc = 0 if verified else 1
     if rank == 0 and (cuda or os.environ.get(FAKE_DUMP_ENV)) and art is not None:
         a = st["artifacts"]
-        v = FA.links_verdict(world, a.get("rccl_dump"), (st.get("rccl_defaults") or {}).get("rccl_dump"))
+        v = FA.links_verdict(world, a.get("rccl_dump"), (st.get("rccl_defaults") or {}).get("rccl_dump"),
+                             (st.get("xgmi_traffic") or {}).get("job"))
         a["xgmi_links_check"] = v
         if world > 1 and args.strict and (not a.get("applied") or v["status"] == "failed"):
             why = v.get("why") if a.get("applied") else f"artifacts not applied: {a.get('error')}"

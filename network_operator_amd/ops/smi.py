@@ -47,6 +47,7 @@ def traffic(before: dict, after: dict, min_bytes: int = 1 << 20) -> dict:
         if not p or "xgmi_read_kb" not in g:
             continue
         status: Optional[str] = g.get("link_status")
+        peers = [(ln.get("peer") or "").lower() for ln in g.get("links") or []]
         per_link = []
         for i, (r, w) in enumerate(zip(g["xgmi_read_kb"], g["xgmi_write_kb"])):
             d = ((r - p["xgmi_read_kb"][i]) + (w - p["xgmi_write_kb"][i])) * 1024
@@ -54,5 +55,6 @@ def traffic(before: dict, after: dict, min_bytes: int = 1 << 20) -> dict:
             up = status is not None and i < len(status) and status[i] == "U"
             out["links_up"] += int(up)
             out["links_with_traffic"] += int(up and d >= min_bytes)
-        out["gpus"].append({"bdf": g["bdf"], "link_status": status, "bytes_per_link": per_link})
+        out["gpus"].append({"bdf": g["bdf"], "link_status": status, "bytes_per_link": per_link,
+                            "peer_per_link": peers[:len(per_link)]})
     return out

@@ -192,7 +192,46 @@ def read_view(dump_path: str, file_path: Optional[str] = None) -> Optional[dict]
         return {"error": f"unparseable RCCL topology dump {dump_path}: {e}"}
 
 
-def links_verdict(n: int, with_file: Optional[dict], defaults: Optional[dict]) -> dict:
+def traffic_view(job_bdfs: List[str], traffic: Optional[dict], min_bytes: int = 1 << 20) -> Optional[dict]:
+    """From amd-smi's per-link counters around the timed loop (``ops.smi.traffic``): for each of
+    the job's GPUs, the xGMI links *to another GPU of the job* that moved at least ``min_bytes``.
+    Hardware's account of what RCCL used, independent of RCCL's dump."""
+    if not traffic or not traffic.get("gpus"):
+        return None
+    job = {b.lower() for b in job_bdfs}
+    per = {}
+    for g in traffic["gpus"]:
+        b = g["bdf"].lower()
+        if b not in job:
+            continue
+        peers = g.get("peer_per_link") or []
+        per[b] = sum(1 for i, d in enumerate(g["bytes_per_link"])
+                     if i < len(peers) and peers[i] in job and peers[i] != b and d >= min_bytes)
+    if not per:
+        return None
+    return {"gpus": len(per), "links_with_traffic_per_gpu": per, "min_links_with_traffic": min(per.values())}
+
+
+def links_verdict(n: int, with_file: Optional[dict], defaults: Optional[dict],
+                  traffic: Optional[dict] = None) -> dict:
+    """The dump-based verdict (:func:`dump_verdict`), with the hardware counters as the tie
+    breaker: when every one of the job's GPUs moved data over n-1 xGMI links during the timed
+    loop (``traffic_view``), RCCL used every link, whatever its dump says."""
+    v = dump_verdict(n, with_file, defaults)
+    if traffic is not None:
+        v["min_links_with_traffic"] = traffic["min_links_with_traffic"]
+        counters_ok = traffic["gpus"] >= n and traffic["min_links_with_traffic"] >= max(n - 1, 0)
+        if v["status"] != "ok" and counters_ok:
+            v = dict(v, status="ok", dump_status=v["status"],
+                     why=f"amd-smi: every GPU moved data over {n - 1} xGMI link(s) to the others during the timed "
+                         f"loop (RCCL's dump: {v['status']}: {v.get('why', '')})")
+        elif v["status"] == "ok" and n > 1 and not counters_ok:
+            v = dict(v, status="failed", why=f"amd-smi: a GPU moved data over only {traffic['min_links_with_traffic']} "
+                                              f"of {n - 1} xGMI links during the timed loop")
+    return v
+
+
+def dump_verdict(n: int, with_file: Optional[dict], defaults: Optional[dict]) -> dict:
     """"RCCL sees at least n-1 xGMI links per GPU under the agent's file."
 
     * ``ok`` — every GPU of the dump has >= n-1 xGMI peers among the job's GPUs (and the dump

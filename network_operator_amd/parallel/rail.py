@@ -38,14 +38,10 @@ def device_bdf(device_index: int) -> str:
 
 def read_env_file(path: str) -> Dict[str, str]:
     """``KEY=VALUE`` lines of an env file such as the agent's ``rccl.env`` (comments skipped)."""
-    out: Dict[str, str] = {}
+    from .fabric_artifacts import parse_env_text
+
     with open(path) as f:
-        for line in f:
-            line = line.strip()
-            if line and not line.startswith("#") and "=" in line:
-                k, v = line.split("=", 1)
-                out[k.strip()] = v
-    return out
+        return parse_env_text(f.read())
 
 
 def rail_env(gpu_bdf: Optional[str] = None, gpu_index: Optional[int] = None,

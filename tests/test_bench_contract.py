@@ -410,3 +410,32 @@ def test_bench_fails_loudly_when_the_file_costs_xgmi_links(lost, tmp_path, node_
         assert j["error"].startswith("agent artifacts check failed") and "costs links" in r.stderr
     else:
         assert r.returncode == 0 and chk["status"] == "ok" and chk["min_with_file"] == 1 and "error" not in j
+
+
+def test_link_verdict_takes_the_hardware_counters_as_tie_breaker():
+    """amd-smi's per-link counters around the timed loop are the hardware's account of what RCCL
+    used: they settle a dump the parser cannot read, and catch a link the dump claims but RCCL
+    never used."""
+    from network_operator_amd.parallel import fabric_artifacts as FA
+
+    bdfs = ["0000:0a:00.0", "0000:23:00.0", "0000:5a:00.0"]
+
+    def traffic(moved):
+        return {"gpus": [{"bdf": b, "bytes_per_link": [moved.get((b, p), 0) for p in bdfs + ["0000:f1:00.0"]],
+                          "peer_per_link": bdfs + ["0000:f1:00.0"]} for b in bdfs]}
+
+    all_used = {(a, b): 5 << 30 for a in bdfs for b in bdfs if a != b}
+    tv = FA.traffic_view(bdfs[:3], traffic(all_used))
+    assert tv["min_links_with_traffic"] == 2 and tv["gpus"] == 3
+    g = [(b, ["0000:01:00.0"]) for b in bdfs]
+    no_xgmi = FA.rccl_view(_dump(g, {}))
+    assert FA.links_verdict(3, no_xgmi, no_xgmi)["status"] == "unverifiable"
+    v = FA.links_verdict(3, no_xgmi, no_xgmi, tv)
+    assert v["status"] == "ok" and v["dump_status"] == "unverifiable" and "amd-smi" in v["why"]
+    # the dump claims every link, but one pair never moved a byte
+    full = FA.rccl_view(_dump(g, {a: [b for b in bdfs if b != a] for a in bdfs}))
+    idle = dict(all_used)
+    idle.pop(("0000:0a:00.0", "0000:5a:00.0"))
+    v = FA.links_verdict(3, full, None, FA.traffic_view(bdfs, traffic(idle)))
+    assert v["status"] == "failed" and "only 1 of 2" in v["why"]
+    assert FA.traffic_view(bdfs, None) is None and FA.traffic_view(["0000:99:00.0"], traffic(all_used)) is None
