@@ -51,6 +51,7 @@ import sys
 import tempfile
 import threading
 import time
+from typing import Optional
 
 METRIC = "node scale-out-ready latency (s) + rccl all-reduce busbw GB/s at 1/2/4/8 GPU"
 STORE_KEY = "netop/bench/artifacts"
@@ -191,78 +192,60 @@ def _probe_cmd(world: int, nbytes: int, steps: int, device: str, warmup: int = 2
 
 
 def torch_env_probe(world: int, nbytes: int, budget_s: float, device: str = "cuda", variants=None,
-                    steps: int = 5) -> list:
+                    steps: int = 5, artifacts: str = "off", base_env: Optional[dict] = None) -> list:
     """busbw of the timed loop itself (torch.distributed, this torch's RCCL, bf16, `nbytes`) under
     each RCCL knob variant of ``rccl_bench.ENV_PROBES``: bench.py runs again in a fresh set of
-    `world` rank processes per variant, with the variant in its environment and every extra
-    measurement off.  Variants not started within `budget_s` are reported as skipped.  A hung
-    variant is killed with its whole process tree (its ranks hold GPUs)."""
+    `world` rank processes per variant, with the variant in its environment on top of
+    `artifacts` (an artifact directory, or "off") and every extra measurement off.  Variants not
+    started within `budget_s` are reported as skipped.  A hung variant is killed with its whole
+    process tree (its ranks hold GPUs)."""
     from network_operator_amd.parallel import bench_extras, rccl_bench
 
-    runner = bench_extras.Runner(time.monotonic() + budget_s + 30, margin_s=0)
+    runner = bench_extras.Runner(time.monotonic() + budget_s + 30, base_env=base_env, margin_s=0)
     out = []
     t0 = time.monotonic()
     for extra in (variants if variants is not None else rccl_bench.ENV_PROBES):
         if budget_s - (time.monotonic() - t0) <= 0:
             out.append({"env": extra, "skipped": "time budget spent"})
             continue
-        j = runner.run("autotune", _probe_cmd(world, nbytes, steps, device) + ["--artifacts", "off"],
+        j = runner.run("autotune", _probe_cmd(world, nbytes, steps, device) + ["--artifacts", artifacts],
                        cap_s=budget_s + 30, env=extra)
         if "error" in j:
             out.append({"env": extra, "error": j["error"] if j["error"] != "deadline" else "timed out"})
             continue
-        out.append({"env": extra, "busbw_GBps": j["busbw_GBps"], "time_us": j["ms_per_step"] * 1e3})
+        out.append({"env": extra, "busbw_GBps": j["busbw_GBps"], "time_us": j["ms_per_step"] * 1e3,
+                    "artifacts_applied": bool((j.get("agent_artifacts") or {}).get("applied"))})
     return out
 
 
-def autotune_file() -> str:
-    return f"/tmp/netop-rccl-autotune-{os.environ.get('MASTER_PORT', '0')}-{os.getppid()}.json"
+AUTOTUNE_KEY = "netop/bench/autotune"
 
 
-def _rccl_autotune(rank: int, world: int, nbytes: int, budget_s: float = 120.0,
-                   started: float = time.time(), device: str = "cuda", variants=None) -> dict:
-    """Opt-in (``--rccl-autotune 1``).  RCCL reads its parameters once per process, at
-    communicator creation, so they must be chosen before init_process_group.
+def _rccl_autotune(store, rank: int, world: int, nbytes: int, budget_s: float = 150.0, device: str = "cuda",
+                   variants=None, artifacts: str = "off", base_env: Optional[dict] = None) -> dict:
+    """RCCL reads its parameters once per process, at communicator creation, so they must be
+    chosen before init_process_group.
 
     Rank 0 measures the knob variants of ``rccl_bench.ENV_PROBES`` with bench.py itself
-    (``torch_env_probe``: the same torch, RCCL build, dtype and message as the timed loop) over
-    the node's first `world` GPUs.  Each variant runs in fresh processes, and all of them must
-    fit in ``budget_s``.  Rank 0 publishes the winner through a file in /tmp keyed by the
-    rendezvous port, and every rank exports it.  A variant must beat the defaults by >= 3 %
-    (``rccl_bench.choose_env``).  On a node, the validation Job tunes ``rccl-tuned.env`` the
-    same way (``validate.py --tune-rccl``) and ``--artifacts DIR`` applies it."""
-    # Keyed by the launcher's pid as well as the port: every rank of one run shares its parent
-    # (torchrun's agent or _spawn_ranks), so a file left by an earlier run on the same port
-    # (the driver's N = 2, 4, 8 runs back to back) can never hand this run another world's knobs.
-    path = autotune_file()
+    (``torch_env_probe``: the same torch, RCCL build, dtype, message *and the same agent
+    artifacts* as the timed loop) over the node's first `world` GPUs.  Each variant runs in fresh
+    processes, and all of them must fit in ``budget_s``.  A variant must beat the artifacts alone
+    by >= 3 % (``rccl_bench.choose_env``).  Rank 0 publishes the choice through the rendezvous
+    store (one per launcher run, so the driver's back-to-back N = 2, 4, 8 runs cannot see each
+    other's), and every rank exports it.  This is what the validation Job writes to a node's
+    ``rccl-tuned.env`` (``validate.py --tune-rccl``): what jobs on a configured node source."""
     if rank == 0:
         try:
             from network_operator_amd.parallel import rccl_bench
 
-            probes = torch_env_probe(world, nbytes, budget_s, device=device, variants=variants)
+            probes = torch_env_probe(world, nbytes, budget_s, device=device, variants=variants, artifacts=artifacts,
+                                     base_env=base_env)
             doc = dict(rccl_bench.choose_env(probes), probes=probes)
-        except Exception as e:  # never leave the other ranks waiting: defaults, and say why
+        except Exception as e:  # never leave the other ranks waiting: no knobs, and say why
             doc = {"chosen": {}, "error": str(e)[-300:]}
-        doc["created"] = time.time()
-        tmp = path + f".{os.getpid()}"
-        with open(tmp, "w") as f:
-            json.dump(doc, f)
-        os.replace(tmp, path)
+        store.set(AUTOTUNE_KEY, json.dumps(doc))
     else:
-        deadline = time.time() + budget_s + 300
-        doc = None
-        while time.time() < deadline:
-            try:
-                with open(path) as f:
-                    d = json.load(f)
-                if d.get("created", 0) >= started - 30:  # not a stale file from an earlier run
-                    doc = d
-                    break
-            except (OSError, ValueError):
-                pass
-            time.sleep(0.2)
-        if doc is None:
-            return {"error": "rank 0 published no autotune result", "chosen": {}}
+        doc = json.loads(store.get(AUTOTUNE_KEY))
     for k, v in doc["chosen"].items():
         os.environ[k] = v
     return doc
@@ -358,7 +341,9 @@ def _line(args, world: int, st: dict) -> dict:
                    "op": "all_reduce(sum)",
                    "backend": "torch.distributed nccl (RCCL)" if cuda else "torch.distributed gloo (CPU rehearsal)",
                    "rccl_env": ("agent artifacts (discover --dry-run)" if args.artifacts == "agent"
-                                else "RCCL defaults" if args.artifacts == "off" else f"artifacts from {args.artifacts}")},
+                                else "RCCL defaults" if args.artifacts == "off" else f"artifacts from {args.artifacts}")
+                   + (f" + autotuned {(st.get('tuned') or {}).get('chosen')}" if (st.get("tuned") or {}).get("chosen")
+                      else "")},
         "agent_artifacts": st.get("artifacts"),
         "busbw_GBps": busbw,
         "busbw_rccl_defaults_GBps": (st.get("rccl_defaults") or {}).get("busbw_GBps"),
@@ -453,11 +438,12 @@ def main(argv=None) -> int:
     ap.add_argument("--rccl-env-probe", type=int, default=0,
                     help="n > 1: also measure the 1 GiB busbw under RCCL knob variants (a fresh process each)")
     ap.add_argument("--extras-budget", type=float, default=0.0, help=argparse.SUPPRESS)  # superseded by --deadline-s
-    ap.add_argument("--rccl-autotune", type=int, default=0,
-                    help="n > 1: before RCCL starts, rank 0 measures RCCL knob variants by running this bench "
-                         "again per variant (within --rccl-autotune-budget s) and every rank uses the fastest "
-                         "(>= 3%% better than the defaults) for the run; 0 = the artifacts' environment only")
-    ap.add_argument("--rccl-autotune-budget", type=float, default=120.0)
+    ap.add_argument("--rccl-autotune", type=int, default=1,
+                    help="GPU, n > 1: before RCCL starts, rank 0 measures RCCL knob variants on top of the agent's "
+                         "artifacts by running this bench again per variant (within --rccl-autotune-budget s) and "
+                         "every rank uses the fastest (>= 3%% better than the artifacts alone): what the validation "
+                         "Job writes to rccl-tuned.env; 0 = the artifacts' environment only")
+    ap.add_argument("--rccl-autotune-budget", type=float, default=150.0)
     ap.add_argument("--gpu-side", type=int, default=1, help="rank 0: time the agent's unprivileged phases on this box")
     # CPU rehearsal of the autotune plumbing (tests): run it with gloo too, on the first K variants.
     ap.add_argument("--autotune-cpu-variants", type=int, default=0, help=argparse.SUPPRESS)
@@ -505,12 +491,6 @@ def main(argv=None) -> int:
 
     # 0. RCCL's environment, fixed before any communicator exists: the autotune (opt-in), then the
     #    operator's artifacts, handed to every rank through the rendezvous store.
-    if world > 1 and (args.rccl_autotune if cuda else args.autotune_cpu_variants):
-        from network_operator_amd.parallel import rccl_bench
-
-        variants = None if cuda else rccl_bench.ENV_PROBES[:args.autotune_cpu_variants]
-        st["tuned"] = _rccl_autotune(rank, world, args.bytes, args.rccl_autotune_budget, device=args.device,
-                                     variants=variants)
     store = _store(world, timeout_s=max(60.0, deadline - time.monotonic()))
     art, dump_path = None, None
     if args.artifacts != "off":
@@ -521,6 +501,13 @@ def main(argv=None) -> int:
                                      FA.DUMP_FILE)
     elif rank == 0 and args.topo_dump:
         dump_path = args.topo_dump
+    if world > 1 and (args.rccl_autotune if cuda else args.autotune_cpu_variants):
+        from network_operator_amd.parallel import rccl_bench
+
+        variants = None if cuda else rccl_bench.ENV_PROBES[:args.autotune_cpu_variants]
+        art_dir = art["doc"].get("dir") if art and "error" not in art["doc"] else None
+        st["tuned"] = _rccl_autotune(store, rank, world, args.bytes, args.rccl_autotune_budget, device=args.device,
+                                     variants=variants, artifacts=art_dir or "off", base_env=base_env)
     if dump_path:
         os.environ["NCCL_TOPO_DUMP_FILE"] = dump_path
 
@@ -714,11 +701,6 @@ def main(argv=None) -> int:
     st["rc"] = rc
     st["finished"] = True
     dist.destroy_process_group()
-    if rank == 0 and st.get("tuned") is not None:
-        try:
-            os.unlink(autotune_file())
-        except OSError:
-            pass
     if rank == 0 and art is not None and art["doc"].get("scratch"):
         shutil.rmtree(art["doc"]["dir"], ignore_errors=True)
     return rc

@@ -156,13 +156,14 @@ def test_rccl_knob_choice_needs_a_real_gain():
     assert R.choose_env([{"env": {"A": "1"}, "busbw_GBps": 1.0}])["chosen"] == {}  # no baseline, no choice
 
 
-def test_autotune_measures_variants_with_bench_itself(tmp_path):
+def test_autotune_measures_variants_with_bench_itself(tmp_path, node_sysfs):
     """The RCCL knob autotune runs bench.py again per variant (fresh rank processes with the
-    variant in their environment) and publishes the choice to every rank before init."""
+    variant in their environment, on top of the same agent artifacts as the timed loop) and
+    publishes the choice to every rank before init."""
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
     cmd = [sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1", "--device", "cpu",
            "--bytes", str(1 << 18), "--sweep", "", "--collectives", "", "--node-ready", "off",
-           "--autotune-cpu-variants", "2", "--rccl-autotune-budget", "120"]
+           "--autotune-cpu-variants", "2", "--rccl-autotune-budget", "120", "--sysfs-root", node_sysfs]
     j = _bench_line(subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=tmp_path,
                                    env=dict(env, OMP_NUM_THREADS="1")))
     t = j["rccl_autotune"]
@@ -170,6 +171,7 @@ def test_autotune_measures_variants_with_bench_itself(tmp_path):
     assert all(p.get("busbw_GBps", 0) > 0 for p in t["probes"]), t["probes"]
     assert t["baseline_busbw_GBps"] == t["probes"][0]["busbw_GBps"]
     assert isinstance(t["chosen"], dict)
+    assert all(p["artifacts_applied"] for p in t["probes"]), t["probes"]
     assert j["verified"] is True
 
 
@@ -192,34 +194,22 @@ def test_autotune_probe_runs_the_cuda_bench():
     assert all(o["busbw_GBps"] == 0.0 and o["time_us"] > 0 for o in out)
 
 
-def test_autotune_handoff_ignores_another_runs_file(monkeypatch):
-    """The driver runs N = 2, 4, 8 back to back, possibly on one port: a non-zero rank must only
-    take the knobs its own rank 0 published (same launcher), never a fresh file of another run."""
-    import json as _json
-    import time as _time
+def test_autotune_handoff_through_the_rendezvous_store():
+    """Rank 0 publishes the knob choice through the run's own rendezvous store (the driver's
+    back-to-back N = 2, 4, 8 runs each have theirs), every rank exports it before RCCL starts."""
+    import torch.distributed as dist
 
     sys.path.insert(0, str(ROOT))
     import bench
 
-    monkeypatch.setenv("MASTER_PORT", str(_free_port()))
-    mine = bench.autotune_file()
-    other = mine.rsplit("-", 1)[0] + f"-{os.getppid() + 1}.json"
-    assert other != mine
+    store = dist.HashStore()
+    store.set(bench.AUTOTUNE_KEY, json.dumps({"chosen": {"NCCL_ALGO": "Ring"}, "probes": []}))
+    os.environ.pop("NCCL_ALGO", None)
     try:
-        with open(other, "w") as f:
-            _json.dump({"chosen": {"NCCL_ALGO": "Tree"}, "created": _time.time()}, f)
-        monkeypatch.delenv("NCCL_ALGO", raising=False)
-        got = bench._rccl_autotune(1, 2, 1 << 20, budget_s=-299.5)  # waits 0.5 s
-        assert got["chosen"] == {} and "no autotune result" in got["error"]
-        assert "NCCL_ALGO" not in os.environ
-        with open(mine, "w") as f:
-            _json.dump({"chosen": {"NCCL_ALGO": "Ring"}, "created": _time.time()}, f)
-        got = bench._rccl_autotune(1, 2, 1 << 20, budget_s=-299.5)
+        got = bench._rccl_autotune(store, 1, 2, 1 << 20)
         assert got["chosen"] == {"NCCL_ALGO": "Ring"} and os.environ["NCCL_ALGO"] == "Ring"
     finally:
-        for p in (mine, other):
-            if os.path.exists(p):
-                os.unlink(p)
+        os.environ.pop("NCCL_ALGO", None)
 
 
 # ------------------------------------------------------------------------------------------
