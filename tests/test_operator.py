@@ -656,6 +656,12 @@ def test_validation_job_not_admitted_is_retried_and_a_new_agent_readiness_revali
             await eventually(lambda: cond().get("reason") == "ValidationFailed")
             assert fake.get_object(kube.NETWORKCLUSTERPOLICIES, "policy")["status"]["errors"] == [
                 "gpu-node-0: fabric validation failed"]
+            # the controller's cache has the stored status (a reconcile on a stale cache would send
+            # a write the API server refuses with a conflict, which still counts as a request)
+            rv = fake.get_object(kube.NETWORKCLUSTERPOLICIES, "policy")["metadata"]["resourceVersion"]
+            await eventually(lambda: ((ctl.policies.get("policy") or {}).get("metadata") or {}).get("resourceVersion")
+                             == rv)
+            await asyncio.sleep(0.2)
             writes = sum(1 for m, path in fake.requests if m == "PUT" and path.endswith("/status"))
             for _ in range(5):  # unrelated events: every one reconciles the policy
                 await ctl.requeue_all()
