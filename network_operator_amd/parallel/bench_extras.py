@@ -128,8 +128,8 @@ class Runner:
             except Exception:
                 pass
             hit_deadline = budget < cap_s
-            rec = {"error": "deadline" if hit_deadline else "timed out", "seconds": round(time.monotonic() - t0, 1),
-                   "limit_s": round(budget, 1)}
+            rec = {"error": "deadline" if hit_deadline else "timed out", "timed_out": True,
+                   "seconds": round(time.monotonic() - t0, 1), "limit_s": round(budget, 1)}
             self.log.append({"extra": name, **rec})
             return rec
         finally:

@@ -285,7 +285,8 @@ def test_bench_hung_extra_still_prints_one_line(tmp_path, node_sysfs):
     j = _bench_line(r)
     assert took < 30 + 15, took
     assert j["value"] > 0 and j["verified"] is True and j["agent_artifacts"]["applied"]
-    assert j["rccl_defaults"]["error"] == "deadline" and j["busbw_rccl_defaults_GBps"] is None
+    assert j["rccl_defaults"]["error"] == "deadline" and j["rccl_defaults"]["timed_out"] is True
+    assert j["busbw_rccl_defaults_GBps"] is None
     assert j["extras_log"] == [dict(j["rccl_defaults"], extra="rccl_defaults")]
 
 
