@@ -188,7 +188,7 @@ def _probe_cmd(world: int, nbytes: int, steps: int, device: str, warmup: int = 2
     return [sys.executable, os.path.abspath(__file__), "--gpus", str(world), "--steps", str(steps), "--warmup",
             str(warmup), "--bytes", str(nbytes), "--sweep", "", "--collectives", "", "--node-ready", "off",
             "--xgmi-probe", "0", "--native-rccl", "0", "--xgmi-allreduce", "0", "--rccl-autotune", "0",
-            "--gpu-side", "0", "--rccl-defaults", "0", "--device", device]
+            "--gpu-side", "0", "--rccl-defaults", "0", "--strict", "0", "--device", device]
 
 
 def torch_env_probe(world: int, nbytes: int, budget_s: float, device: str = "cuda", variants=None,
@@ -644,8 +644,7 @@ def main(argv=None) -> int:
             if name == "rccl_defaults":
                 ddump = os.path.join(tempfile.mkdtemp(prefix="netop-bench-defaults-"), "rccl-topo-dump-defaults.xml")
                 cmd = _probe_cmd(world, args.bytes, args.steps, args.device, warmup=args.warmup) + [
-                    "--artifacts", "off", "--topo-dump", ddump, "--deadline-s", str(max(runner.left() - 2, 10)),
-                    "--strict", "0"]
+                    "--artifacts", "off", "--topo-dump", ddump, "--deadline-s", str(max(runner.left() - 2, 10))]
                 j = runner.run(name, cmd, cap_s=180)
                 res = j if "error" in j else {
                     "busbw_GBps": j.get("busbw_GBps"), "ms_per_step": j.get("ms_per_step"),
