@@ -425,7 +425,7 @@ def main(argv=None) -> int:
     ap.add_argument("--strict", type=int, default=1,
                     help="GPU, n > 1: exit 1 (after printing the line) when the artifacts could not be applied or RCCL "
                          "sees fewer than n-1 xGMI links per GPU under them")
-    ap.add_argument("--deadline-s", type=float, default=420.0,
+    ap.add_argument("--deadline-s", type=float, default=360.0,
                     help="hard wall-clock limit: extras are killed and the line printed by then")
     ap.add_argument("--sweep", default="4096,1048576,67108864", help="extra sizes (bytes) reported alongside")
     ap.add_argument("--node-ready", choices=["auto", "on", "off"], default="auto")
