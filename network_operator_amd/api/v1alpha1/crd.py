@@ -22,6 +22,12 @@ import yaml
 
 from . import types as T
 
+LLDP_WAIT_SCHEMA = {
+    "description": "L3: how long the agent waits for every NIC's first LLDPDU (a Go duration, 1s..30m;\n"
+                   "default 90s, the reference's fixed value).  Shorter with fast-start switches, so a\n"
+                   "silent NIC is diagnosed sooner; longer for switches with a long transmit interval.",
+    "pattern": T.LLDP_WAIT_PATTERN, "type": "string"}
+
 _API_VERSION_DESC = (
     "APIVersion defines the versioned schema of this representation of an object.\n"
     "Servers should convert recognized schemas to the latest internal value, and\n"
@@ -108,6 +114,7 @@ def openapi_schema() -> dict:
                                            "to answer ARP (within 2 s).  Catches a switch port whose Port Description\n"
                                            "and interface address disagree, which LLDP alone cannot.",
                             "type": "boolean"},
+            "lldpWait": LLDP_WAIT_SCHEMA,
         },
     }
     host_nic = {
@@ -133,6 +140,7 @@ def openapi_schema() -> dict:
                             "type": "string"},
             "verifyPeers": {"description": "L3: label only once every NIC's switch-side /30 address answers ARP.",
                             "type": "boolean"},
+            "lldpWait": LLDP_WAIT_SCHEMA,
         },
         "required": ["layer"],
     }

@@ -39,6 +39,20 @@ CONFIG_AMD_SCALE_OUT = "amd-so"
 CONFIG_HOST_NIC = "host-nic"
 CONFIGURATION_TYPES = (CONFIG_AMD_SCALE_OUT, CONFIG_HOST_NIC)
 LAYERS = ("L2", "L3")
+# lldpWait: a Go duration the agent's --wait accepts (units h, m, s, ms), checked 1s..30m by the webhook
+LLDP_WAIT_PATTERN = r"^([0-9]+(\.[0-9]+)?(h|m|s|ms))+$"
+LLDP_WAIT_MIN_S, LLDP_WAIT_MAX_S = 1.0, 1800.0
+
+
+def parse_go_duration(s: str) -> float:
+    """Seconds of a Go duration string limited to h/m/s/ms units ("90s", "1m30s", "1.5s");
+    raises ValueError otherwise."""
+    import re
+
+    if not re.fullmatch(LLDP_WAIT_PATTERN, s or ""):
+        raise ValueError(f"not a duration: {s!r}")
+    unit = {"h": 3600.0, "m": 60.0, "s": 1.0, "ms": 1e-3}
+    return sum(float(v) * unit[u] for v, u in re.findall(r"([0-9]+(?:\.[0-9]+)?)(ms|h|m|s)", s))
 PULL_POLICIES = ("Never", "Always", "IfNotPresent")
 MTU_MIN, MTU_MAX = 1500, 9000
 LOG_LEVEL_MIN, LOG_LEVEL_MAX = 0, 8
@@ -96,6 +110,7 @@ class AmdScaleOutSpec:
     rcclSocketIfname: str = ""
     lldpCache: bool = False
     verifyPeers: bool = False
+    lldpWait: str = ""  # L3 LLDP wait (Go duration); "" = the reference's 90s
     validation: Optional[ValidationSpec] = None
     extra: Dict[str, Any] = field(default_factory=dict)
 
@@ -105,7 +120,7 @@ class AmdScaleOutSpec:
 
     _FIELDS = ("disableNetworkManager", "layer", "image", "pullPolicy", "mtu", "xgmiCheck", "lldpAnnounce",
                "interfaces", "nicDrivers", "disableFirmwareLldp", "metricsPort", "gpuDirectRdma", "rcclEnv",
-               "railTableBase", "rcclSocketIfname", "lldpCache", "verifyPeers", "validation")
+               "railTableBase", "rcclSocketIfname", "lldpCache", "verifyPeers", "lldpWait", "validation")
 
     def to_dict(self) -> dict:
         d: dict = {}
@@ -141,6 +156,8 @@ class AmdScaleOutSpec:
             d["lldpCache"] = True
         if self.verifyPeers:
             d["verifyPeers"] = True
+        if self.lldpWait:
+            d["lldpWait"] = self.lldpWait
         if self.validation is not None:
             d["validation"] = self.validation.to_dict()
         d.update(copy.deepcopy(self.extra))
@@ -167,6 +184,7 @@ class AmdScaleOutSpec:
             rcclSocketIfname=d.pop("rcclSocketIfname", "") or "",
             lldpCache=bool(d.pop("lldpCache", False)),
             verifyPeers=bool(d.pop("verifyPeers", False)),
+            lldpWait=d.pop("lldpWait", "") or "",
             validation=ValidationSpec.from_dict(d.pop("validation", None)),
         )
         s.extra = d
@@ -187,11 +205,12 @@ class HostNicSpec:
     nicDrivers: List[str] = field(default_factory=list)
     driverImage: str = ""
     verifyPeers: bool = False
+    lldpWait: str = ""
     extra: Dict[str, Any] = field(default_factory=dict)
 
     def to_dict(self) -> dict:
         d: dict = {}
-        for k in ("layer", "image", "pullPolicy", "driverImage"):
+        for k in ("layer", "image", "pullPolicy", "driverImage", "lldpWait"):
             if getattr(self, k):
                 d[k] = getattr(self, k)
         if self.mtu:
@@ -213,7 +232,8 @@ class HostNicSpec:
         s = cls(layer=d.pop("layer", "") or "", mtu=int(d.pop("mtu", 0) or 0), image=d.pop("image", "") or "",
                 pullPolicy=d.pop("pullPolicy", "") or "", disableNetworkManager=bool(d.pop("disableNetworkManager", False)),
                 interfaces=list(d.pop("interfaces", []) or []), nicDrivers=list(d.pop("nicDrivers", []) or []),
-                driverImage=d.pop("driverImage", "") or "", verifyPeers=bool(d.pop("verifyPeers", False)))
+                driverImage=d.pop("driverImage", "") or "", verifyPeers=bool(d.pop("verifyPeers", False)),
+                lldpWait=d.pop("lldpWait", "") or "")
         s.extra = d
         return s
 

@@ -101,6 +101,24 @@ class InvalidRcclEnvError(ValidationError):
                        "without ','"
 
 
+class InvalidLldpWaitError(ValidationError):
+    def __init__(self, value: str):
+        super().__init__()
+        self.message = (f"invalid lldpWait {value!r}: a duration such as 90s or 2m, between "
+                        f"{int(T.LLDP_WAIT_MIN_S)}s and {int(T.LLDP_WAIT_MAX_S // 60)}m")
+
+
+def validate_lldp_wait(value: str) -> None:
+    if not value:
+        return
+    try:
+        secs = T.parse_go_duration(value)
+    except ValueError:
+        raise InvalidLldpWaitError(value) from None
+    if not T.LLDP_WAIT_MIN_S <= secs <= T.LLDP_WAIT_MAX_S:
+        raise InvalidLldpWaitError(value)
+
+
 def validate_amd_so_spec(s: T.AmdScaleOutSpec) -> List[str]:
     """Returns admission warnings.  (The reference's validateGaudiSoSpec is a no-op, :87-89.)"""
     warnings = []
@@ -112,6 +130,9 @@ def validate_amd_so_spec(s: T.AmdScaleOutSpec) -> List[str]:
     for k, v in s.rcclEnv.items():
         if not RCCL_ENV_KEY_RE.match(str(k)) or not isinstance(v, str) or any(c in v for c in "\n\r,"):
             raise InvalidRcclEnvError(str(k))
+    validate_lldp_wait(s.lldpWait)
+    if s.lldpWait and s.layer == "L2":
+        warnings.append("lldpWait has no effect in L2 mode")
     return warnings
 
 
@@ -125,6 +146,7 @@ def validate_host_nic_spec(s: Optional[T.HostNicSpec]) -> List[str]:
     for i in s.interfaces:
         if not i or len(i) > 15 or "/" in i or " " in i or "," in i:
             raise InvalidInterfaceError(i)
+    validate_lldp_wait(s.lldpWait)
     warnings = []
     if not s.interfaces and not s.nicDrivers:
         warnings.append("hostNic: no interfaces or nicDrivers given; every RDMA NIC of the default driver list "

@@ -149,7 +149,7 @@ def agent_args(p: T.NetworkClusterPolicy) -> List[str]:
     if so.disableNetworkManager:
         args += ["--disable-networkmanager", "--nm-keyfile-dir=/etc/NetworkManager/conf.d"]
     if so.layer == "L3":
-        args += [f"--wait={L3_WAIT}", f"--rccl-net={ARTIFACT_DIR_CONTAINER}/{RCCL_NET_FILE}",
+        args += [f"--wait={so.lldpWait or L3_WAIT}", f"--rccl-net={ARTIFACT_DIR_CONTAINER}/{RCCL_NET_FILE}",
                  f"--rccl-env={ARTIFACT_DIR_CONTAINER}/{RCCL_ENV_FILE}"]
     else:
         # MI355X: RCCL needs the HCA list and the link-local RoCE v2 GID in L2 as well (Gaudi's
@@ -251,7 +251,7 @@ def host_nic_agent_args(p: T.NetworkClusterPolicy) -> List[str]:
     if hn.disableNetworkManager:
         args += ["--disable-networkmanager", "--nm-keyfile-dir=/etc/NetworkManager/conf.d"]
     if hn.layer == "L3":
-        args.append(f"--wait={L3_WAIT}")
+        args.append(f"--wait={hn.lldpWait or L3_WAIT}")
         if hn.verifyPeers:
             args.append(f"--verify-peers={VERIFY_PEERS_TIMEOUT}")
     if hn.interfaces:

@@ -120,7 +120,7 @@ def test_silent_switch_port_reaches_the_policy_status():
     """one switch port never sends LLDP.  The agent's exit error names the NIC, its
     driver (the fake node's rail NICs are mlx5_core) and what it heard; the operator puts it in
     the policy's status.errors and an AgentFailed event, and the node is never labelled."""
-    r = e2e.run_isolated(n_nics=2, mode="L3", seed=21, interval="1s", silent_nics=1, lldp_wait="2s")
+    r = e2e.run_isolated(n_nics=2, mode="L3", seed=21, interval="1s", silent_nics=1, policy_kw={"lldpWait": "2s"})
     assert r["policy_to_silent_error_s"] is not None, (r["policy_status"], r["agent_log"])
     silent = r["nics"][-1]
     errs = [e for e in r["policy_status"]["errors"] if "LLDP silent" in e]

@@ -471,6 +471,40 @@ def test_rccl_env_extra_settings_validated_and_passed():
         W.validate_create(p)
 
 
+def test_lldp_wait_validated_and_passed():
+    """amdScaleOut.lldpWait / hostNic.lldpWait: the agent's --wait (the reference fixes 90s,
+    controller.go:198); a Go duration, 1s..30m, checked by the CRD pattern and the webhook."""
+    from network_operator_amd.api.v1alpha1 import crd as CRD
+    from network_operator_amd.api.v1alpha1 import webhook as W
+    from network_operator_amd.operator.reconciler import host_nic_agent_args
+
+    p = T.new_policy("p", layer="L3")
+    assert "--wait=90s" in agent_args(p)
+    for value, secs in (("5s", 5), ("1m30s", 90), ("1.5s", 1.5), ("30m", 1800), ("1000ms", 1)):
+        p.spec.amdScaleOut.lldpWait = value
+        assert T.parse_go_duration(value) == pytest.approx(secs)
+        assert W.validate_create(p) == [] and f"--wait={value}" in agent_args(p)
+        d = p.to_dict()
+        assert d["spec"]["amdScaleOut"]["lldpWait"] == value and CRD.validate(d) == []
+        assert T.NetworkClusterPolicy.from_dict(d).spec.amdScaleOut.lldpWait == value
+    for bad in ("500ms", "31m", "2h", "90", "1d", "-5s", " 5s"):
+        p.spec.amdScaleOut.lldpWait = bad
+        with pytest.raises(W.InvalidLldpWaitError):
+            W.validate_create(p)
+    p.spec.amdScaleOut.lldpWait = "90"
+    assert CRD.validate(p.to_dict())  # the schema pattern refuses it too
+    p.spec.amdScaleOut.lldpWait, p.spec.amdScaleOut.layer = "5s", "L2"
+    assert W.validate_create(p) == ["lldpWait has no effect in L2 mode"]
+    assert not any(a.startswith("--wait") for a in agent_args(p))
+    h = T.new_host_nic_policy("h", layer="L3", lldpWait="20s")
+    assert "--wait=20s" in host_nic_agent_args(h) and W.validate_create(h) == [
+        "hostNic: no interfaces or nicDrivers given; every RDMA NIC of the default driver list will be configured"]
+    assert T.NetworkClusterPolicy.from_dict(h.to_dict()).spec.hostNic.lldpWait == "20s"
+    h.spec.hostNic.lldpWait = "0s"
+    with pytest.raises(W.InvalidLldpWaitError):
+        W.validate_create(h)
+
+
 def test_status_conditions_ready_degraded_and_observed_generation():
     """Additive status: Ready / Degraded conditions with stable lastTransitionTime, and
     observedGeneration following spec changes (the reference only has the state string)."""

@@ -96,6 +96,9 @@ def test_helm_policy_rendering_and_validation():
     assert cr["spec"]["amdScaleOut"]["image"] == "amd/amd-network-linkdiscovery:0.1.0"
     assert cr["spec"]["nodeSelector"] == {"amd.feature.node.kubernetes.io/gpu-ready": "true"}
     assert cr["spec"]["amdScaleOut"]["xgmiCheck"] is True
+    assert "lldpWait" not in cr["spec"]["amdScaleOut"]  # the agent's 90s
+    waited = _chart_policies(helm_template(CHART, {"config": {"amd": {"enabled": True, "lldpWait": "15s"}}}))[0]
+    assert waited["spec"]["amdScaleOut"]["lldpWait"] == "15s" and CRD.validate(waited) == []
     with pytest.raises(RenderError, match="Invalid layer mode"):
         helm_template(CHART, {"config": {"amd": {"enabled": True, "mode": "L4"}}})
     for mtu in (1499, 9001):
