@@ -596,9 +596,21 @@ def main(argv=None) -> int:
     if world > 1:
         others = []
         for op in [o.strip() for o in args.collectives.split(",") if o.strip()]:
+            before = None
+            if rank == 0 and smi_before is not None:  # no collective starts before rank 0 joins it
+                try:
+                    before = smi.snapshot()
+                except Exception:
+                    before = None
             r = C.run_sweep(op, [nbytes], iters=max(args.steps // 2, 5), warmup=2, device=device, dtype=dtype)[0]
-            others.append({"op": op, "bytes": r.bytes, "time_us": r.time_s * 1e6, "algbw_GBps": r.algbw_GBps,
-                           "busbw_GBps": r.busbw_GBps})
+            row = {"op": op, "bytes": r.bytes, "time_us": r.time_s * 1e6, "algbw_GBps": r.algbw_GBps,
+                   "busbw_GBps": r.busbw_GBps}
+            if before is not None:  # does this collective use every xGMI link of the job too?
+                try:
+                    row["xgmi_links"] = FA.traffic_view(job_bdfs, smi.traffic(before, smi.snapshot()))
+                except Exception as e:
+                    row["xgmi_links"] = {"error": str(e)[-200:]}
+            others.append(row)
         st["collectives"] = others
 
     # 5. What was applied, and what RCCL made of it (rank 0).
