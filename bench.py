@@ -489,8 +489,9 @@ def main(argv=None) -> int:
         print("bench.py needs an MI355X GPU (torch.cuda.is_available() is False)", file=sys.stderr)
         return 2
 
-    # 0. RCCL's environment, fixed before any communicator exists: the autotune (opt-in), then the
-    #    operator's artifacts, handed to every rank through the rendezvous store.
+    # 0. RCCL's environment, fixed before any communicator exists: the operator's artifacts, then
+    #    (n > 1) the knob autotune on top of them, both handed to every rank through the rendezvous
+    #    store.
     store = _store(world, timeout_s=max(60.0, deadline - time.monotonic()))
     art, dump_path = None, None
     if args.artifacts != "off":
