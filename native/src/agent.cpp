@@ -660,9 +660,13 @@ void Agent::detect_lldp(int stop_fd) {
         }
     }
     if (!listening) return;
-    for (auto& n : nics_)  // what each NIC hears while we wait: the diagnosis of a silent one
-        if (listened.count(n.link.index))
+    for (auto& n : nics_) {  // what each NIC hears while we wait: the diagnosis of a silent one
+        if (!listened.count(n.link.index)) continue;
+        try {
             if (auto s = ops_.link_stats(n.link.index)) n.rx_at_listen = s->rx_packets;
+        } catch (const std::exception&) {  // diagnostics only
+        }
+    }
     int remaining = listening - apply_lldp_cache(listened);
     if (remaining <= 0) {
         NLOG_I("Every listening interface was configured from the LLDP cache; the switch confirms it while monitoring");
@@ -803,8 +807,11 @@ void Agent::diagnose_silent() {
     const std::string waited = format_go_duration(cfg_.wait_ns);
     for (auto& n : nics_) {
         if (n.lldp_seen || n.lldp_from_cache) continue;
-        if (auto d = topo::netdev_pci(root, n.ifname)) n.driver = d->driver;
-        if (n.driver.empty() && ethtool_) n.driver = ethtool_->driver(n.ifname);
+        try {
+            if (auto d = topo::netdev_pci(root, n.ifname)) n.driver = d->driver;
+            if (n.driver.empty() && ethtool_) n.driver = ethtool_->driver(n.ifname);
+        } catch (const std::exception&) {
+        }
         const std::string drv = n.driver.empty() ? "unknown driver" : n.driver;
         if (!n.link.up()) {
             n.lldp_silent = drv + ": link down, nothing listened";
@@ -812,8 +819,12 @@ void Agent::diagnose_silent() {
             continue;
         }
         std::optional<uint64_t> rx;
-        if (n.rx_at_listen)
-            if (auto s = ops_.link_stats(n.link.index)) rx = s->rx_packets >= *n.rx_at_listen ? s->rx_packets - *n.rx_at_listen : 0;
+        try {
+            if (n.rx_at_listen)
+                if (auto s = ops_.link_stats(n.link.index))
+                    rx = s->rx_packets >= *n.rx_at_listen ? s->rx_packets - *n.rx_at_listen : 0;
+        } catch (const std::exception&) {
+        }
         auto ls = lldp_->stats_for(n.ifname);
         std::string heard = rx ? strfmt("%llu frame(s) arrived meanwhile", (unsigned long long)*rx)
                                : std::string("receive counters unavailable");

@@ -463,7 +463,7 @@ std::optional<LinkStats> Rtnl::link_stats(int ifindex) {
         transact(m, [&](const nlmsghdr* h) {
             if (h->nlmsg_type == RTM_NEWLINK) out = parse_link_stats(h);
         });
-    } catch (const SysError&) {
+    } catch (const std::exception&) {  // counters are diagnostics: never fatal
         return std::nullopt;
     }
     return out;
