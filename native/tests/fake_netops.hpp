@@ -156,7 +156,7 @@ struct FakeNetOps : netop::nl::NetOps {
     // (traffic arriving while the agent waits); links without an entry have no counters.
     std::map<int, uint64_t> rx, rx_step;
     std::optional<netop::nl::LinkStats> link_stats(int ifindex) override {
-        ++calls["link_stats"];
+        maybe_fail("link_stats");
         auto it = rx.find(ifindex);
         if (it == rx.end()) return std::nullopt;
         netop::nl::LinkStats s;

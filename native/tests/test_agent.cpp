@@ -339,6 +339,20 @@ TEST(agent_silent_nics_are_diagnosed_in_the_error_status_and_metrics) {
     CHECK(err.find("ens0 (unknown driver: no LLDPDU in 1ms, 5 frame(s) arrived meanwhile; 3 LLDPDU(s) did not decode)") !=
           std::string::npos);
     CHECK(err.find("ens1 (unknown driver: no LLDPDU in 1ms, receive counters unavailable; NIC-firmware") != std::string::npos);
+
+    // The counters themselves failing is only less information, never an agent failure of its own.
+    Fixture h;
+    h.cfg.wait_ns = 1000000;
+    h.ops.fail.insert("link_stats");
+    agent::Agent c(h.cfg, h.ops, std::make_unique<ScriptedLldp>(), h.nm());
+    err.clear();
+    try {
+        c.run(-1);
+    } catch (const agent::AgentError& e) {
+        err = e.what();
+    }
+    CHECK(err.find("No LLDP peers with a /30 Port Description were found. LLDP silent on 3 NIC(s): ") == 0);
+    CHECK(err.find("receive counters unavailable") != std::string::npos);
 }
 
 TEST(agent_no_peers_is_an_error_unless_compat) {
