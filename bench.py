@@ -447,8 +447,11 @@ def main(argv=None) -> int:
     ap.add_argument("--gpu-side", type=int, default=1, help="rank 0: time the agent's unprivileged phases on this box")
     # CPU rehearsal of the autotune plumbing (tests): run it with gloo too, on the first K variants.
     ap.add_argument("--autotune-cpu-variants", type=int, default=0, help=argparse.SUPPRESS)
-    ap.add_argument("--xgmi-allreduce", type=int, default=1,
-                    help="also run the direct two-shot xGMI all-reduce on rank 0 (n > 1)")
+    ap.add_argument("--xgmi-allreduce", choices=["0", "1", "auto"], default="auto",
+                    help="also run the hand-written direct xGMI all-reduces (single process and one process per "
+                         "GPU over HIP IPC) after the headline; auto = only when the job spans every visible GPU "
+                         "(the last of the driver's N = 1, 2, 4, 8 runs): their first contact with real peers must "
+                         "not be able to leave a GPU in a state that costs a later run its number")
     # CPU rehearsal of the multi-rank path (tests): gloo backend, fp32 on the host.
     ap.add_argument("--device", choices=["cuda", "cpu"], default="cuda", help=argparse.SUPPRESS)
     raw_argv = list(sys.argv[1:] if argv is None else argv)
@@ -648,7 +651,9 @@ def main(argv=None) -> int:
             plan.append("native_rccl")
         if cuda and world > 1 and args.xgmi_probe:
             plan.append("xgmi_probe")
-        if cuda and world > 1 and args.xgmi_allreduce:
+        direct = args.xgmi_allreduce == "1" or (args.xgmi_allreduce == "auto" and world == torch.cuda.device_count()) \
+            if cuda else False
+        if cuda and world > 1 and direct:
             plan += ["xgmi_allreduce", "xgmi_comm"]
         if args.node_ready != "off":
             plan.append("node_ready")
