@@ -390,3 +390,66 @@ def test_validation_image_file_set_runs_without_pytorch(tmp_path):
     r = subprocess.run([sys.executable, "-c", block], cwd=str(tmp_path), env={"PYTHONPATH": str(ROOT), "PATH": "/usr/bin:/bin"},
                        capture_output=True, text=True, timeout=120)
     assert r.returncode == 0 and "--tune-rccl" in r.stdout, r.stderr[-2000:]
+
+
+def test_validation_rccl_sweep_sources_the_agents_artifacts(monkeypatch, tmp_path):
+    """validate.py check 3 runs RCCL the way jobs on the node do: with <artifact-dir>/rccl.env
+    (and rccl-tuned.env) in its environment, NCCL_TOPO_FILE included, and reads RCCL's dump of that
+    run back (rccl_xgmi_links).  RCCL is faked here: it writes a dump with the given xGMI links."""
+    from network_operator_amd import validate as V
+    from network_operator_amd.parallel import rccl_bench
+
+    art = tmp_path / "scale-out"
+    art.mkdir()
+    topo = '<system version="2"><cpu numaid="0"><pci busid="0000:01:00.0"><pci busid="0000:0a:00.0"/></pci>' \
+           '<pci busid="0000:1c:00.0"><pci busid="0000:23:00.0"/></pci></cpu></system>'
+    (art / "rccl-topo.xml").write_text(topo)
+    (art / "rccl.env").write_text(f"NCCL_TOPO_FILE={art}/rccl-topo.xml\n")
+    (art / "rccl-tuned.env").write_text("NCCL_MIN_NCHANNELS=64\n")
+    seen = []
+
+    def dump(links):  # links: True (to the peer), False (none), "elsewhere" (only to a GPU outside the job)
+        def g(b, p, t):
+            x = {True: f'<xgmi target="{t}" count="1"/>', False: "",
+                 "elsewhere": '<xgmi target="0000:99:00.0" count="1"/>'}[links]
+            return f'<pci busid="{p}"><pci busid="{b}"><gpu dev="0" rank="0">{x}</gpu></pci></pci>'
+
+        return (f'<system version="2"><cpu numaid="0">{g("0000:0a:00.0", "0000:01:00.0", "0000:23:00.0")}'
+                f'{g("0000:23:00.0", "0000:1c:00.0", "0000:0a:00.0")}</cpu></system>')
+
+    def fake_run(timeout=300, env=None, **kw):
+        seen.append(dict(env))
+        with open(env["NCCL_TOPO_DUMP_FILE"], "w") as f:
+            f.write(dump(links=True))
+        return [rccl_bench.Row("all_reduce", 1 << 30, 1 << 29, 2, 5000.0, 200.0, 200.0, 0, True, False, False)]
+
+    monkeypatch.setattr(rccl_bench, "run", fake_run)
+    monkeypatch.setattr(V, "direct_all_reduce_check", lambda *a, **k: V._check("xgmi_direct_all_reduce", True))
+    monkeypatch.setattr(V.subprocess, "run", lambda *a, **k: (_ for _ in ()).throw(FileNotFoundError("no probe")))
+    rep = V.run(gpus=2, min_busbw=0, min_link_GBps=0, max_bytes=1 << 30, sysfs_root=str(tmp_path / "nosys") + "/",
+                artifact_dir=str(art))
+    by = {c["check"]: c for c in rep["checks"]}
+    assert seen[0]["NCCL_TOPO_FILE"] == f"{art}/rccl-topo.xml" and seen[0]["NCCL_MIN_NCHANNELS"] == "64"
+    assert by["rccl_all_reduce"]["ok"] and by["rccl_all_reduce"]["artifacts_applied"]
+    assert by["rccl_xgmi_links"]["ok"] and by["rccl_xgmi_links"]["status"] == "ok"
+    assert by["rccl_xgmi_links"]["rccl_dump"]["gpu_ancestry_equal"] is True
+
+    # RCCL under the file sees no peer of the job: the check fails.  No <xgmi> element at all, and
+    # no defaults run to compare with: reported as unverifiable, not failed.
+    def run_with(links):
+        def run(timeout=300, env=None, **kw):
+            with open(env["NCCL_TOPO_DUMP_FILE"], "w") as f:
+                f.write(dump(links=links))
+            return [rccl_bench.Row("all_reduce", 1 << 30, 1 << 29, 2, 5000.0, 200.0, 200.0, 0, True, False, False)]
+        return run
+
+    monkeypatch.setattr(rccl_bench, "run", run_with(False))
+    rep = V.run(gpus=2, min_busbw=0, min_link_GBps=0, max_bytes=1 << 30, sysfs_root=str(tmp_path / "nosys") + "/",
+                artifact_dir=str(art))
+    c = {x["check"]: x for x in rep["checks"]}["rccl_xgmi_links"]
+    assert c["ok"] and c["status"] == "unverifiable"
+    monkeypatch.setattr(rccl_bench, "run", run_with("elsewhere"))
+    rep = V.run(gpus=2, min_busbw=0, min_link_GBps=0, max_bytes=1 << 30, sysfs_root=str(tmp_path / "nosys") + "/",
+                artifact_dir=str(art))
+    by = {c["check"]: c for c in rep["checks"]}
+    assert not by["rccl_xgmi_links"]["ok"] and by["rccl_xgmi_links"]["status"] == "failed" and not rep["ok"]
