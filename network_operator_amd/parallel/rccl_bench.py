@@ -64,10 +64,10 @@ ENV_PROBES = (
 
 
 def env_probe(gpus: int, nbytes: int, iters: int = 10, probes=ENV_PROBES, timeout: float = 120,
-              budget_s: Optional[float] = None) -> List[dict]:
+              budget_s: Optional[float] = None, base_env: Optional[dict] = None) -> List[dict]:
     """busbw of one all-reduce size under each RCCL environment variant (fresh process each:
-    RCCL caches its parameters at first use).  Variants not started within ``budget_s`` seconds
-    are reported as skipped."""
+    RCCL caches its parameters at first use), on top of ``base_env`` (the agent's artifacts).
+    Variants not started within ``budget_s`` seconds are reported as skipped."""
     import time
 
     out = []
@@ -78,7 +78,7 @@ def env_probe(gpus: int, nbytes: int, iters: int = 10, probes=ENV_PROBES, timeou
             continue
         try:
             rows = run(op="all_reduce", gpus=gpus, min_bytes=nbytes, max_bytes=nbytes, iters=iters, warmup=3,
-                       check=False, env=extra, timeout=timeout)
+                       check=False, env=dict(base_env or {}, **extra), timeout=timeout)
             out.append({"env": extra, "busbw_GBps": rows[-1].busbw_GBps if rows else None,
                         "time_us": rows[-1].time_us if rows else None})
         except Exception as e:

@@ -239,7 +239,10 @@ def run(gpus: int, min_busbw: float, min_link_GBps: float, max_bytes: int, sysfs
         try:
             from .parallel import rccl_bench
 
-            probes = rccl_bench.env_probe(gpus, max_bytes, budget_s=min(timeout, 300))
+            # on top of the agent's rccl.env (its NCCL_TOPO_FILE): the environment jobs run with
+            probes = rccl_bench.env_probe(gpus, max_bytes, budget_s=min(timeout, 300),
+                                          base_env=FA.parse_env_text((Path(artifact_dir) / FA.ENV_FILE).read_text())
+                                          if (Path(artifact_dir) / FA.ENV_FILE).is_file() else {})
             pick = rccl_bench.choose_env(probes)
             report["rccl_tuning"] = dict(pick, probes=probes)
             out = Path(artifact_dir) / "rccl-tuned.env"
