@@ -225,9 +225,10 @@ def links_verdict(n: int, with_file: Optional[dict], defaults: Optional[dict],
             v = dict(v, status="ok", dump_status=v["status"],
                      why=f"amd-smi: every GPU moved data over {n - 1} xGMI link(s) to the others during the timed "
                          f"loop (RCCL's dump: {v['status']}: {v.get('why', '')})")
-        elif v["status"] == "ok" and n > 1 and not counters_ok:
-            v = dict(v, status="failed", why=f"amd-smi: a GPU moved data over only {traffic['min_links_with_traffic']} "
-                                              f"of {n - 1} xGMI links during the timed loop")
+        elif n > 1 and not counters_ok:  # the hardware says a link stayed idle, whatever the dump says
+            v = dict(v, status="failed", dump_status=v["status"],
+                     why=f"amd-smi: a GPU moved data over only {traffic['min_links_with_traffic']} of {n - 1} xGMI "
+                         "links during the timed loop")
     return v
 
 

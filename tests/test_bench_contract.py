@@ -429,4 +429,7 @@ def test_link_verdict_takes_the_hardware_counters_as_tie_breaker():
     idle.pop(("0000:0a:00.0", "0000:5a:00.0"))
     v = FA.links_verdict(3, full, None, FA.traffic_view(bdfs, traffic(idle)))
     assert v["status"] == "failed" and "only 1 of 2" in v["why"]
+    # no <xgmi> in the dump either way and an idle link: the counters decide, failed
+    v = FA.links_verdict(3, no_xgmi, no_xgmi, FA.traffic_view(bdfs, traffic(idle)))
+    assert v["status"] == "failed" and v["dump_status"] == "unverifiable"
     assert FA.traffic_view(bdfs, None) is None and FA.traffic_view(["0000:99:00.0"], traffic(all_used)) is None
