@@ -214,9 +214,10 @@ def traffic_view(job_bdfs: List[str], traffic: Optional[dict], min_bytes: int = 
 
 def links_verdict(n: int, with_file: Optional[dict], defaults: Optional[dict],
                   traffic: Optional[dict] = None) -> dict:
-    """The dump-based verdict (:func:`dump_verdict`), with the hardware counters as the tie
-    breaker: when every one of the job's GPUs moved data over n-1 xGMI links during the timed
-    loop (``traffic_view``), RCCL used every link, whatever its dump says."""
+    """The dump-based verdict (:func:`dump_verdict`), with the hardware counters as a one-way
+    tie breaker: when every one of the job's GPUs moved data over n-1 xGMI links during the timed
+    loop (``traffic_view``), RCCL used every link, whatever its dump says.  Fewer used links do
+    not fail the check (RCCL's rings may leave a link idle); they are reported."""
     v = dump_verdict(n, with_file, defaults)
     if traffic is not None:
         v["min_links_with_traffic"] = traffic["min_links_with_traffic"]
@@ -225,10 +226,12 @@ def links_verdict(n: int, with_file: Optional[dict], defaults: Optional[dict],
             v = dict(v, status="ok", dump_status=v["status"],
                      why=f"amd-smi: every GPU moved data over {n - 1} xGMI link(s) to the others during the timed "
                          f"loop (RCCL's dump: {v['status']}: {v.get('why', '')})")
-        elif n > 1 and not counters_ok:  # the hardware says a link stayed idle, whatever the dump says
-            v = dict(v, status="failed", dump_status=v["status"],
-                     why=f"amd-smi: a GPU moved data over only {traffic['min_links_with_traffic']} of {n - 1} xGMI "
-                         "links during the timed loop")
+        elif n > 1 and not counters_ok:
+            # Informational only: which links a collective uses is RCCL's choice of rings and
+            # channels (a 4-GPU ring may leave the diagonals idle).  "RCCL sees the link" is the
+            # topology's question, answered by the dump.
+            v = dict(v, counters_note=f"amd-smi: a GPU moved data over {traffic['min_links_with_traffic']} of "
+                                      f"{n - 1} xGMI links during the timed loop")
     return v
 
 
