@@ -425,7 +425,7 @@ def main(argv=None) -> int:
     ap.add_argument("--strict", type=int, default=1,
                     help="GPU, n > 1: exit 1 (after printing the line) when the artifacts could not be applied or RCCL "
                          "sees fewer than n-1 xGMI links per GPU under them")
-    ap.add_argument("--deadline-s", type=float, default=360.0,
+    ap.add_argument("--deadline-s", type=float, default=450.0,
                     help="hard wall-clock limit: extras are killed and the line printed by then")
     ap.add_argument("--sweep", default="4096,1048576,67108864", help="extra sizes (bytes) reported alongside")
     ap.add_argument("--node-ready", choices=["auto", "on", "off"], default="auto")
@@ -443,7 +443,7 @@ def main(argv=None) -> int:
                          "artifacts by running this bench again per variant (within --rccl-autotune-budget s) and "
                          "every rank uses the fastest (>= 3%% better than the artifacts alone): what the validation "
                          "Job writes to rccl-tuned.env; 0 = the artifacts' environment only")
-    ap.add_argument("--rccl-autotune-budget", type=float, default=150.0)
+    ap.add_argument("--rccl-autotune-budget", type=float, default=120.0)
     ap.add_argument("--gpu-side", type=int, default=1, help="rank 0: time the agent's unprivileged phases on this box")
     # CPU rehearsal of the autotune plumbing (tests): run it with gloo too, on the first K variants.
     ap.add_argument("--autotune-cpu-variants", type=int, default=0, help=argparse.SUPPRESS)
