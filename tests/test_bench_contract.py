@@ -24,7 +24,7 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("n", [2, 4])
+@pytest.mark.parametrize("n", [2, 4, 8])
 def test_bench_torchrun_cpu_rehearsal(n, tmp_path, node_sysfs):
     """The driver's launcher path: torchrun's agent store carries the agent's artifacts to the
     ranks before any communicator exists."""
