@@ -433,3 +433,17 @@ def test_link_verdict_takes_the_hardware_counters_as_tie_breaker():
     v = FA.links_verdict(3, no_xgmi, no_xgmi, FA.traffic_view(bdfs, traffic(idle)))
     assert v["status"] == "unverifiable" and "counters_note" in v
     assert FA.traffic_view(bdfs, None) is None and FA.traffic_view(["0000:99:00.0"], traffic(all_used)) is None
+
+
+def test_bench_reports_an_agent_that_cannot_run(tmp_path):
+    """No GPU in the sysfs the agent reads: the artifacts are reported as not applied, with the
+    agent's own error, the headline still comes out (RCCL defaults), and the other ranks were not
+    left waiting for them."""
+    (tmp_path / "empty-sys").mkdir()
+    cmd = [sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1", "--device", "cpu",
+           "--bytes", str(1 << 16), "--sweep", "", "--collectives", "", "--node-ready", "off", "--rccl-defaults", "0",
+           "--sysfs-root", str(tmp_path / "empty-sys") + "/"]
+    j = _bench_line(subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=tmp_path, env=_spawn_env()))
+    a = j["agent_artifacts"]
+    assert a["applied"] is False and "No interfaces found" in a["error"] and a["ranks_applied"] == 0
+    assert j["value"] > 0 and j["verified"] is True
