@@ -563,10 +563,12 @@ def run_scenario(n_nics: int = 8, mode: str = "L3", seed: int | None = None, int
         res["sigterm_to_exit_s"] = (time.monotonic() - t_term) if t_term else None
         res["agent_rc"] = agent.returncode
         res["agent_log"] = out[-6000:]
-        try:
-            res["status"] = json.loads((tmp / "status.json").read_text())
+        try:  # the agent's last word (a failed start never wrote a ready-time status)
+            res["status_at_exit"] = json.loads((tmp / "status.json").read_text())
         except (OSError, ValueError):
-            res["status"] = None
+            res["status_at_exit"] = None
+        if res.get("status") is None:
+            res["status"] = res["status_at_exit"]
         after = {}
         for node_if in nic_names:
             link = rt.link_by_name(node_if)

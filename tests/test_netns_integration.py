@@ -55,8 +55,9 @@ def test_l3_fast_start_switch_full_node():
     topo = ET.fromstring(r["rccl_topo"])
     assert len([n for n in topo.iter("net")]) == 8 and len([p for p in topo.iter("pci") if p.get("class") == "0x120000"]) == 8
     assert len(r["networkd_files"]) == 8
-    # CPU of the bring-up, for the DaemonSet's CPU limit (500m; discovery/__init__.py).
-    assert 0 < float(r["status"]["cpu_ms_at_ready"]) < 50
+    # CPU of the bring-up, for the DaemonSet's CPU limit (500m; discovery/__init__.py).  Sanitizer
+    # builds (make test-netns-asan) run several times slower.
+    assert 0 < float(r["status"]["cpu_ms_at_ready"]) < (50 if not os.environ.get("NETOP_BIN_DIR") else 500)
     # SIGTERM: label removed, addresses flushed, links back down.
     assert r["agent_rc"] == 0
     assert not r["label_after_sigterm"]
