@@ -114,13 +114,23 @@ struct Config {
     // its rules and routes carry protocol kRailProtocol and it never deletes any other.  0 = off
     // (the reference's main-table-only routing).
     int rail_table_base = 0;
+    // Discovery, the xGMI / GPUDirect checks and the topology file only; no link, address, NM
+    // or label change and no LLDP (no privileges needed): what the agent would configure here.
+    bool dry_run = false;
+    // Keep the data plane across agent restarts (rolling updates, drains, agent crashes): on exit
+    // only the readiness label is withdrawn; addresses, routes, rail rules and link state stay,
+    // and the next agent adopts them (the /30 its LLDP cache holds for a NIC is not flushed, so
+    // RoCE QPs bound to it survive).  The reference tears everything down on every SIGTERM
+    // (main.go:143-159), which breaks running RCCL jobs whenever the DaemonSet rolls.
+    bool keep_config = false;
+    // One-shot teardown of what --keep-config agents left on the node (the operator runs it when
+    // the policy is deleted): IPv4 addresses of the discovered NICs, rules and routes tagged
+    // kRailProtocol, the label, the agent's artifacts, LLDP cache and networkd files.
+    bool cleanup = false;
     // LLDP cache (artifacts.hpp): configure from the last confirmed Port Description at start,
     // then require a real frame to confirm it within lldp_cache_confirm_ns (else the NIC counts
     // as degraded and the label is withdrawn until one arrives).  "" = off.  Used only with
     // --keep-running and the monitor (which does the confirming).
-    // Discovery, the xGMI / GPUDirect checks and the topology file only; no link, address, NM
-    // or label change and no LLDP (no privileges needed): what the agent would configure here.
-    bool dry_run = false;
     std::string lldp_cache;
     int64_t lldp_cache_max_age_ns = 7LL * 24 * 3600 * 1000000000;  // older entries are ignored
     int64_t lldp_cache_confirm_ns = 95LL * 1000000000;              // 3 x msgTxInterval + 5 s
@@ -201,7 +211,7 @@ class Agent {
     void interfaces_up();
     void interfaces_restore_down();
     void interfaces_set_mtu();
-    void remove_existing_ips();
+    void remove_existing_ips(const std::map<std::string, Ipv4Prefix>& keep = {});
     bool configure_interface(NicState& n);
     int configure_all();  // returns number configured
     void assign_rail_indices();
@@ -209,6 +219,8 @@ class Agent {
    private:
     void pre_cleanups();
     void post_cleanups();
+    void cleanup_node();                    // --cleanup
+    std::map<std::string, Ipv4Prefix> cached_addresses() const;  // --keep-config: addresses to adopt
     std::vector<std::string> collect_interfaces();
     void get_network_configs(const std::vector<std::string>& names);
     void detect_lldp(int stop_fd);

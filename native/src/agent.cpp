@@ -166,7 +166,7 @@ void Agent::post_cleanups() {
     NLOG_I("Clean up before exiting...");
     if (ethtool_)
         for (const auto& r : fw_lldp_) ethtool::restore(*ethtool_, r);
-    if (cfg_.lldp_announce && cfg_.mode == "L3") {
+    if (cfg_.lldp_announce && cfg_.mode == "L3" && !cfg_.keep_config) {
         // Shutdown LLDPDU (TTL 0): the switch drops us from its neighbour table right away.
         for (auto& n : nics_) {
             if (!n.link.up()) continue;
@@ -177,6 +177,11 @@ void Agent::post_cleanups() {
         }
     }
     if (!artifacts::remove_labels(cfg_.labels)) NLOG_W("Failed to remove NFD label file: %s", std::strerror(errno));
+    if (cfg_.keep_config) {
+        // The next agent adopts addresses, routes and rail rules; jobs keep their links meanwhile.
+        NLOG_I("Keeping addresses, routes and links for the next agent (--keep-config)");
+        return;
+    }
     NLOG_I("Restoring interfaces to original state...");
     remove_rail_routing();
     try {
@@ -357,11 +362,35 @@ void Agent::interfaces_set_mtu() {
     }
 }
 
-void Agent::remove_existing_ips() {
+void Agent::remove_existing_ips(const std::map<std::string, Ipv4Prefix>& keep) {
     for (auto& n : nics_) {
+        auto k = keep.find(n.ifname);
         auto addrs = ops_.addr_list(n.link.index, AF_INET);
-        for (auto& a : addrs) ops_.addr_del(a);
+        for (auto& a : addrs) {
+            if (k != keep.end() && a.local == k->second.addr && a.prefixlen == k->second.len) {
+                NLOG_I("Interface '%s': keeping %s from the previous agent (--keep-config)", n.ifname.c_str(),
+                       a.prefix().str().c_str());
+                continue;
+            }
+            ops_.addr_del(a);
+        }
     }
+}
+
+std::map<std::string, Ipv4Prefix> Agent::cached_addresses() const {
+    // The same validity rules as apply_lldp_cache: this NIC (name and MAC), not too old, parses.
+    std::map<std::string, Ipv4Prefix> out;
+    if (cfg_.lldp_cache.empty()) return out;
+    const int64_t now = int64_t(::time(nullptr));
+    for (const auto& e : artifacts::read_lldp_cache(cfg_.lldp_cache)) {
+        for (const auto& n : nics_) {
+            if (e.ifname != n.ifname || e.nic_mac != n.link.mac.str()) continue;
+            if (now - e.unix_s > cfg_.lldp_cache_max_age_ns / 1000000000 || e.unix_s > now + 60) continue;
+            if (auto addr = l3::parse_port_description(e.port_description, cfg_.token_policy, nullptr))
+                out[n.ifname] = addr->local_prefix();
+        }
+    }
+    return out;
 }
 
 void Agent::add_route(NicState& n, int mask) {
@@ -1281,6 +1310,10 @@ void Agent::run(int stop_fd) {
                 dry_run_missing_.push_back(i);
     }
     mark("discover");
+    if (cfg_.cleanup) {
+        cleanup_node();
+        return;
+    }
     // From the agent's discovery, at background priority on another CPU: overlaps the checks,
     // link-up and the LLDP wait.
     start_topo();
@@ -1332,7 +1365,8 @@ void Agent::run(int stop_fd) {
     interfaces_set_mtu();
     mark("mtu");
     try {
-        remove_existing_ips();
+        remove_existing_ips(cfg_.keep_config && cfg_.mode == "L3" ? cached_addresses()
+                                                                   : std::map<std::string, Ipv4Prefix>{});
     } catch (const std::exception& e) {
         throw AgentError(std::string("Failed to remove any existing IPs from interfaces: ") + e.what());
     }
@@ -1443,6 +1477,61 @@ void Agent::run(int stop_fd) {
 }
 
 bool Agent::publish_label() { return artifacts::write_labels(cfg_.labels, labels_extra_); }
+
+void Agent::cleanup_node() {
+    // What agents running with --keep-config left behind, once the policy is gone.  Nothing here
+    // depends on a previous run's memory: addresses of the discovered NICs, rules and routes
+    // carrying the agent's protocol tag, and the agent's own files.
+    NLOG_I("Cleaning up the node (--cleanup): %zu interface(s)", nics_.size());
+    if (!artifacts::remove_labels(cfg_.labels)) NLOG_W("Failed to remove NFD label file: %s", std::strerror(errno));
+    int errors = 0;
+    try {
+        remove_existing_ips();
+    } catch (const std::exception& e) {
+        NLOG_W("Failed to remove IPv4 addresses: %s", e.what());
+        ++errors;
+    }
+    try {
+        for (const auto& r : ops_.rule_list())
+            if (r.protocol == kRailProtocol) ops_.rule_del(r);
+        for (const auto& r : ops_.route_list(0))
+            if (r.protocol == kRailProtocol) {
+                try {
+                    ops_.route_del(r);
+                } catch (const SysError&) {  // gone with its address
+                }
+            }
+    } catch (const std::exception& e) {
+        NLOG_W("Failed to remove the rail rules / routes: %s", e.what());
+        ++errors;
+    }
+    for (const std::string& f : {cfg_.rccl_env, cfg_.rccl_net, cfg_.lldp_cache, cfg_.rccl_topo,
+                                 cfg_.rccl_topo.empty() ? std::string() : cfg_.rccl_topo + ".key"})
+        if (!f.empty() && ::unlink(f.c_str()) != 0 && errno != ENOENT) {
+            NLOG_W("Could not remove %s: %s", f.c_str(), std::strerror(errno));
+            ++errors;
+        }
+    if (!cfg_.networkd.empty()) {
+        std::vector<std::string> names;
+        for (const auto& n : nics_) names.push_back(n.ifname);
+        try {
+            artifacts::delete_networkd(cfg_.networkd, names);
+        } catch (const std::exception& e) {
+            NLOG_W("Could not remove systemd-networkd files: %s", e.what());
+            ++errors;
+        }
+    }
+    if (cfg_.disable_nm) {
+        nm_keyfile_written_ = true;  // a file of ours from an earlier run (remove_keyfile checks it)
+        nm_unmanaged_.clear();
+        for (const auto& n : nics_) nm_unmanaged_.push_back(n.ifname);
+        restore_network_manager();
+    }
+    mark("cleanup");
+    write_status();
+    if (errors) throw AgentError(strfmt("Node cleanup incomplete (%d error(s))", errors));
+    NLOG_I("Node cleanup done");
+}
 
 void Agent::announce_all(uint16_t ttl) {
     if (!cfg_.lldp_announce || cfg_.mode != "L3") return;

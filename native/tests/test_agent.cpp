@@ -1480,3 +1480,110 @@ TEST(agent_monitor_reprobe_never_holds_the_loop_for_the_startup_timeout) {
     CHECK_EQ(swi.timeouts.front(), int64_t(2000000000));  // start-up: the configured timeout
     for (size_t i = 1; i < swi.timeouts.size(); ++i) CHECK(swi.timeouts[i] <= 250000000);
 }
+
+TEST(agent_keep_config_leaves_the_data_plane_and_the_next_agent_adopts_it) {
+    // Rolling update with --keep-config: the first agent exits withdrawing only its label; the
+    // second finds the addresses its LLDP cache names and keeps them (no addr_del, no addr_add),
+    // so QPs bound to them never see their source address disappear.
+    Fixture f;
+    f.cfg.keep_config = true;
+    f.cfg.rail_table_base = 100;
+    f.cfg.monitor_tick_ns = 1000000;
+    f.cfg.lldp_cache = f.tmp.path + "/lldp-cache";
+    {
+        Pipe stop;
+        stop.fire();
+        agent::Agent a(f.cfg, f.ops, f.all_valid(), f.nm());
+        a.run(stop.fd[0]);
+        CHECK(a.ready());
+    }
+    CHECK(!path_exists(f.cfg.labels.path()));
+    CHECK_EQ(f.ops.addrs.size(), size_t(3));
+    CHECK_EQ(f.ops.rules.size(), size_t(3));
+    CHECK(has_table_route(f.ops, 11, "10.200.0.0/16", "10.200.0.6", 101));
+    CHECK(f.ops.links["ens0"].flags & IFF_UP);  // not put down again
+    CHECK_EQ(artifacts::read_lldp_cache(f.cfg.lldp_cache).size(), size_t(3));
+    // A foreign address on ens2 (not the cached /30) is still flushed.
+    f.ops.addrs.push_back(nl::AddrInfo{12, AF_INET, *Ipv4::parse("192.168.77.1"), *Ipv4::parse("192.168.77.1"), 24, 0, ""});
+    f.ops.calls.clear();
+    {
+        Pipe stop;
+        auto src = std::make_unique<ScriptedLldp>();  // the switch is silent while we restart
+        ScriptedLldp* raw = src.get();
+        agent::Agent b(f.cfg, f.ops, std::move(src), f.nm());
+        bool ready_before_frame = false;
+        b.on_monitor_tick = [&](int tick) {
+            if (tick == 0) {
+                ready_before_frame = path_exists(f.cfg.labels.path());
+                raw->frames = f.all_valid()->frames;
+            }
+            if (tick == 2) stop.fire();
+        };
+        b.run(stop.fd[0]);
+        CHECK(ready_before_frame);
+    }
+    CHECK_EQ(f.ops.calls["addr_del"], 1);  // the foreign 192.168.77.1/24 only
+    CHECK_EQ(f.ops.calls["addr_add"], 0);
+    CHECK_EQ(f.ops.addrs.size(), size_t(3));
+    for (auto& a : f.ops.addrs) CHECK(a.local.str() != "192.168.77.1");
+    CHECK_EQ(f.ops.rules.size(), size_t(3));
+}
+
+TEST(agent_keep_config_does_not_adopt_a_stale_or_foreign_cache_entry) {
+    Fixture f;
+    f.cfg.keep_config = true;
+    f.cfg.lldp_cache = f.tmp.path + "/lldp-cache";
+    f.cfg.keep_running = false;
+    write_cache(f, 3600);
+    auto e = artifacts::read_lldp_cache(f.cfg.lldp_cache);
+    e[1].nic_mac = "02:00:00:00:00:99";  // ens1 is another card now
+    e[2].unix_s -= 30LL * 24 * 3600;      // ens2's entry is too old
+    artifacts::write_lldp_cache(f.cfg.lldp_cache, e);
+    f.ops.addrs.push_back(nl::AddrInfo{10, AF_INET, *Ipv4::parse("10.200.0.1"), *Ipv4::parse("10.200.0.1"), 30, 0, ""});
+    f.ops.addrs.push_back(nl::AddrInfo{11, AF_INET, *Ipv4::parse("10.200.0.5"), *Ipv4::parse("10.200.0.5"), 30, 0, ""});
+    f.ops.addrs.push_back(nl::AddrInfo{12, AF_INET, *Ipv4::parse("10.200.0.10"), *Ipv4::parse("10.200.0.10"), 30, 0, ""});
+    agent::Agent a(f.cfg, f.ops, f.all_valid(), f.nm());
+    a.run(-1);
+    CHECK_EQ(f.ops.calls["addr_del"], 2);  // ens1 and ens2 re-learn their address from LLDP
+    CHECK_EQ(f.ops.addrs.size(), size_t(3));
+}
+
+TEST(agent_cleanup_mode_removes_what_kept_agents_left) {
+    Fixture f;
+    f.cfg.keep_config = true;
+    f.cfg.rail_table_base = 100;
+    f.cfg.lldp_cache = f.tmp.path + "/lldp-cache";
+    f.cfg.rccl_env = f.tmp.path + "/rccl.env";
+    {
+        Pipe stop;
+        stop.fire();
+        agent::Agent a(f.cfg, f.ops, f.all_valid(), f.nm());
+        a.run(stop.fd[0]);
+        CHECK(a.ready());
+    }
+    // A host rule and route the agent never made survive the cleanup.
+    const nl::RuleSpec foreign{*Ipv4Prefix::parse("192.168.5.0/24"), 100, 101};
+    f.ops.rules.push_back(foreign);
+    nl::RouteSpec host;
+    host.ifindex = 11;
+    host.dst = *Ipv4Prefix::parse("172.16.0.0/12");
+    host.table = 101;
+    f.ops.routes.push_back(host);
+    CHECK(path_exists(f.cfg.rccl_env) && path_exists(f.cfg.rccl_net) && path_exists(f.cfg.lldp_cache));
+    write_file_atomic(f.cfg.labels.path(), "stale=true\n");
+    agent::Config c = f.cfg;
+    c.cleanup = true;
+    c.keep_config = false;
+    agent::Agent k(c, f.ops, std::make_unique<ScriptedLldp>(), f.nm());
+    k.run(-1);
+    CHECK(f.ops.addrs.empty());
+    CHECK_EQ(f.ops.rules.size(), size_t(1));
+    CHECK(f.ops.rules[0] == foreign);
+    for (auto& r : f.ops.routes) CHECK(r.protocol != agent::kRailProtocol);
+    CHECK(std::any_of(f.ops.routes.begin(), f.ops.routes.end(), [](const nl::RouteSpec& r) { return r.table == 101; }));
+    CHECK(!path_exists(f.cfg.labels.path()));
+    CHECK(!path_exists(f.cfg.rccl_env) && !path_exists(f.cfg.rccl_net) && !path_exists(f.cfg.lldp_cache));
+    CHECK_EQ(k.ready(), false);
+    auto st = read_file(f.cfg.status_file);
+    CHECK(st && st->find("cleanup") != std::string::npos);
+}

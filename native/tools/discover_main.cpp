@@ -75,6 +75,8 @@ int main(int argc, char** argv) {
     fs.add_duration("gid-wait", &cfg.gid_wait_ns, "time to wait for the RoCE v2 GID of a newly configured address");
     fs.add_bool("lldp-announce", &cfg.lldp_announce, "transmit our own LLDPDU on each NIC (makes 802.1AB-2009 switches answer within ~1s)");
     fs.add_bool("lldp-restart-fast", &cfg.announce_shutdown_first, "send a shutdown LLDPDU before the first announcement so a switch holding a stale entry (agent restart) fast-starts again");
+    fs.add_bool("keep-config", &cfg.keep_config, "on exit withdraw only the readiness label: addresses, routes, rail rules and links stay for the next agent, which adopts the /30 its LLDP cache confirms (hitless agent restarts; needs --lldp-cache in L3)");
+    fs.add_bool("cleanup", &cfg.cleanup, "one-shot: remove what --keep-config agents left on the node (IPv4 addresses of the discovered NICs, tagged rail rules and routes, label, artifacts, LLDP cache, networkd files) and exit");
     fs.add_bool("dry-run", &cfg.dry_run, "discover, check xGMI / GPUDirect RDMA and write the topology file and status only: no link, address, NetworkManager or label change, no LLDP (needs no privileges)");
     fs.add_string("lldp-cache", &cfg.lldp_cache, "with --keep-running: remember each NIC's confirmed Port Description in this file and configure from it at start (the switch must confirm it within --lldp-cache-confirm)");
     fs.add_duration("lldp-cache-max-age", &cfg.lldp_cache_max_age_ns, "ignore LLDP cache entries older than this");

@@ -115,6 +115,13 @@ def openapi_schema() -> dict:
                                            "and interface address disagree, which LLDP alone cannot.",
                             "type": "boolean"},
             "lldpWait": LLDP_WAIT_SCHEMA,
+            "keepConfigOnRestart": {
+                "description": "Keep addresses, routes and links when an agent exits (rolling update, drain,\n"
+                               "crash), so RCCL jobs keep their RoCE connections; the next agent adopts them\n"
+                               "(L3: from the LLDP cache, which this turns on).  The operator removes the\n"
+                               "configuration with a cleanup Job per node when the policy is deleted or a\n"
+                               "node leaves it (finalizer amd.com/node-cleanup).",
+                "type": "boolean"},
         },
     }
     host_nic = {
@@ -186,6 +193,9 @@ def openapi_schema() -> dict:
                 },
             },
             "errors": {"items": {"type": "string"}, "type": "array"},
+            "keptNodes": {"description": "keepConfigOnRestart: nodes whose configuration a cleanup Job still has to\n"
+                                         "remove when the policy is deleted or the node leaves it.",
+                          "items": {"type": "string"}, "type": "array"},
             "observedGeneration": {"description": "The spec generation the status describes.",
                                    "format": "int64", "type": "integer"},
             "ready": {"format": "int32", "type": "integer"},

@@ -111,6 +111,9 @@ class AmdScaleOutSpec:
     lldpCache: bool = False
     verifyPeers: bool = False
     lldpWait: str = ""  # L3 LLDP wait (Go duration); "" = the reference's 90s
+    # Hitless agent restarts: addresses / routes stay when an agent exits; the operator cleans the
+    # nodes up (cleanup Jobs) when the policy is deleted or a node leaves it.
+    keepConfigOnRestart: bool = False
     validation: Optional[ValidationSpec] = None
     extra: Dict[str, Any] = field(default_factory=dict)
 
@@ -120,7 +123,8 @@ class AmdScaleOutSpec:
 
     _FIELDS = ("disableNetworkManager", "layer", "image", "pullPolicy", "mtu", "xgmiCheck", "lldpAnnounce",
                "interfaces", "nicDrivers", "disableFirmwareLldp", "metricsPort", "gpuDirectRdma", "rcclEnv",
-               "railTableBase", "rcclSocketIfname", "lldpCache", "verifyPeers", "lldpWait", "validation")
+               "railTableBase", "rcclSocketIfname", "lldpCache", "verifyPeers", "lldpWait", "keepConfigOnRestart",
+               "validation")
 
     def to_dict(self) -> dict:
         d: dict = {}
@@ -158,6 +162,8 @@ class AmdScaleOutSpec:
             d["verifyPeers"] = True
         if self.lldpWait:
             d["lldpWait"] = self.lldpWait
+        if self.keepConfigOnRestart:
+            d["keepConfigOnRestart"] = True
         if self.validation is not None:
             d["validation"] = self.validation.to_dict()
         d.update(copy.deepcopy(self.extra))
@@ -183,6 +189,7 @@ class AmdScaleOutSpec:
             railTableBase=int(d.pop("railTableBase", 0) or 0),
             rcclSocketIfname=d.pop("rcclSocketIfname", "") or "",
             lldpCache=bool(d.pop("lldpCache", False)),
+            keepConfigOnRestart=bool(d.pop("keepConfigOnRestart", False)),
             verifyPeers=bool(d.pop("verifyPeers", False)),
             lldpWait=d.pop("lldpWait", "") or "",
             validation=ValidationSpec.from_dict(d.pop("validation", None)),
@@ -283,6 +290,8 @@ class NetworkClusterPolicyStatus:
     # Additive (not in the reference): standard conditions and the generation they describe.
     conditions: List[dict] = field(default_factory=list)
     observedGeneration: int = 0
+    # keepConfigOnRestart: nodes whose agents may have left configuration behind (cleanup owed).
+    keptNodes: List[str] = field(default_factory=list)
 
     def to_dict(self) -> dict:
         d = {"targets": self.targets, "ready": self.ready, "state": self.state, "errors": list(self.errors)}
@@ -290,6 +299,8 @@ class NetworkClusterPolicyStatus:
             d["conditions"] = [dict(c) for c in self.conditions]
         if self.observedGeneration:
             d["observedGeneration"] = self.observedGeneration
+        if self.keptNodes:
+            d["keptNodes"] = list(self.keptNodes)
         return d
 
     @classmethod
@@ -298,7 +309,8 @@ class NetworkClusterPolicyStatus:
         return cls(targets=int(d.get("targets", 0) or 0), ready=int(d.get("ready", 0) or 0),
                    state=d.get("state", "") or "", errors=list(d.get("errors") or []),
                    conditions=[dict(c) for c in d.get("conditions") or []],
-                   observedGeneration=int(d.get("observedGeneration", 0) or 0))
+                   observedGeneration=int(d.get("observedGeneration", 0) or 0),
+                   keptNodes=list(d.get("keptNodes") or []))
 
     def condition(self, type_: str) -> Optional[dict]:
         return next((c for c in self.conditions if c.get("type") == type_), None)

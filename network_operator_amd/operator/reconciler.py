@@ -176,8 +176,11 @@ def agent_args(p: T.NetworkClusterPolicy) -> List[str]:
         args.append(f"--rail-table-base={so.railTableBase}")
     if so.rcclSocketIfname:
         args.append(f"--rccl-socket-ifname={so.rcclSocketIfname}")
-    if so.lldpCache and so.layer == "L3":
+    if (so.lldpCache or so.keepConfigOnRestart) and so.layer == "L3":
+        # keepConfigOnRestart: the cache is what lets the next agent adopt the addresses it finds
         args.append(f"--lldp-cache={ARTIFACT_DIR_CONTAINER}/{LLDP_CACHE_FILE}")
+    if so.keepConfigOnRestart:
+        args.append("--keep-config")
     if so.verifyPeers and so.layer == "L3":
         args.append(f"--verify-peers={VERIFY_PEERS_TIMEOUT}")
     if so.rcclEnv:
@@ -429,6 +432,62 @@ def job_not_admitted(pods: List[dict]) -> Optional[str]:
     return None
 
 
+# keepConfigOnRestart: agents leave their configuration in place when they exit, so the operator
+# owes each node it ever configured a cleanup (the agent in --cleanup mode, as a Job pinned to the
+# node) when the policy is deleted (finalizer) or the node leaves the policy (its agent Pod has
+# been gone for KEPT_ORPHAN_GRACE_S: longer than any DaemonSet roll, drain or reboot).
+FINALIZER = "amd.com/node-cleanup"
+CLEANUP_APP = "amd-network-cleanup"
+KEPT_ORPHAN_GRACE_S = 600.0
+CLEANUP_TIMEOUT_S = 600.0  # a cleanup Job not finished by then (node gone, image missing) is given up
+CLEANUP_POLL_S = 2.0       # cleanup Jobs are not watched: poll while some are running
+
+
+def keeps_config(p: T.NetworkClusterPolicy) -> bool:
+    return p.spec.configurationType == T.CONFIG_AMD_SCALE_OUT and p.spec.amdScaleOut.keepConfigOnRestart
+
+
+def cleanup_job_name(policy: str, node: str) -> str:
+    import hashlib
+
+    return f"{policy[:30].rstrip('-')}-clean-{hashlib.sha256(f'{policy}/{node}'.encode()).hexdigest()[:10]}"
+
+
+def cleanup_job(p: T.NetworkClusterPolicy, node: str, namespace: str) -> dict:
+    """The agent's own Pod template (image, privileges, host paths, discovery flags) run once on
+    ``node`` with ``--cleanup``: it removes what --keep-config agents left there (addresses of
+    the NICs it discovers, its tagged rail rules and routes, label, artifacts, LLDP cache)."""
+    ds = discovery.discovery_daemonset()
+    update_daemonset_for(ds, p, namespace)
+    pod = copy.deepcopy(ds["spec"]["template"]["spec"])
+    pod.pop("initContainers", None)  # the NIC driver is loaded already, or there is nothing to clean
+    pod["restartPolicy"] = "Never"
+    pod["nodeName"] = node
+    pod.pop("nodeSelector", None)  # the node may have left the policy's selector
+    c = pod["containers"][0]
+    for k in ("readinessProbe", "livenessProbe", "startupProbe"):
+        c.pop(k, None)
+    c["args"] = [a for a in c.get("args") or [] if a not in ("--keep-running", "--keep-config")] + \
+        ["--cleanup", f"--nfd-features-dir={discovery.LABEL_FEATURES_DIR}"]
+    labels = {"app": CLEANUP_APP, "amd.com/policy": p.name[:63]}
+    return {
+        "apiVersion": "batch/v1", "kind": "Job",
+        "metadata": {"name": cleanup_job_name(p.name, node), "namespace": namespace, "labels": dict(labels),
+                     "annotations": {"amd.com/node": node}},
+        "spec": {"backoffLimit": 2, "activeDeadlineSeconds": int(CLEANUP_TIMEOUT_S),
+                 "template": {"metadata": {"labels": dict(labels)}, "spec": pod}},
+    }
+
+
+def _rfc3339_to_unix(ts: str) -> Optional[float]:
+    import datetime
+
+    try:
+        return datetime.datetime.strptime(ts, "%Y-%m-%dT%H:%M:%SZ").replace(tzinfo=datetime.timezone.utc).timestamp()
+    except (TypeError, ValueError):
+        return None
+
+
 def _job_finished_at(job: dict) -> Optional[float]:
     import datetime
 
@@ -545,6 +604,8 @@ class NetworkClusterPolicyReconciler:
         self._list_job_pods = list_job_pods  # the Pods of a validation Job (by its name)
         self._clock = clock
         self.recorder = recorder
+        # keepConfigOnRestart: (policy, node) -> when the node's agent Pod was first seen missing
+        self._missing_since: dict = {}
 
     def _node_errors(self, ds_name: str, limit: int = 16) -> List[str]:
         """Per-node agent problems from the agent Pods' Ready condition (the reference indexes
@@ -571,6 +632,115 @@ class NetworkClusterPolicyReconciler:
         except ApiError as e:
             if not is_not_found(e):
                 raise
+
+    async def _cleanup_jobs(self, policy: str) -> dict:
+        out = {}
+        lst = await self.client.list(kube.JOBS, self.namespace,
+                                     label_selector=f"app={CLEANUP_APP},amd.com/policy={policy[:63]}")
+        for j in lst.get("items") or []:
+            out[(j["metadata"].get("annotations") or {}).get("amd.com/node", "")] = j
+        return out
+
+    async def _run_cleanups(self, raw: dict, p: T.NetworkClusterPolicy, nodes: List[str]) -> List[str]:
+        """Cleanup Jobs for ``nodes``: created when missing, deleted (and their node done) once
+        finished or past CLEANUP_TIMEOUT_S.  Returns the nodes still in progress."""
+        jobs = await self._cleanup_jobs(p.name)
+        now = self._clock()
+        pending = []
+        for node in nodes:
+            j = jobs.get(node)
+            if j is None:
+                job = cleanup_job(p, node, self.namespace)
+                set_controller_reference(raw, job)
+                try:
+                    await self.client.create(kube.JOBS, job, namespace=self.namespace)
+                    log.info("Created node cleanup Job %s for node %s", job["metadata"]["name"], node)
+                except ApiError as e:
+                    if not is_already_exists(e):
+                        raise
+                pending.append(node)
+                continue
+            outcome = job_outcome(j)
+            created = _rfc3339_to_unix(j["metadata"].get("creationTimestamp", "")) or now
+            if outcome == "running" and now - created < CLEANUP_TIMEOUT_S:
+                pending.append(node)
+                continue
+            if outcome == "succeeded":
+                log.info("Node %s cleaned up (Job %s)", node, j["metadata"]["name"])
+            else:
+                why = "timed out" if outcome == "running" else "failed"
+                await self._event(raw, "Warning", "NodeCleanupFailed",
+                                  f"{node}: cleanup Job {j['metadata']['name']} {why}; addresses and routes the agent "
+                                  "left may remain (run the agent with --cleanup on the node)")
+            await self._delete_job(j)
+        return pending
+
+    async def _kept_nodes(self, raw: dict, p: T.NetworkClusterPolicy, ds: dict) -> tuple:
+        """keepConfigOnRestart bookkeeping: (status.keptNodes, requeue_after).  A node joins when
+        its agent is Ready; it leaves after its cleanup Job, which runs once its agent Pod has been
+        gone for KEPT_ORPHAN_GRACE_S."""
+        cur = list(p.status.keptNodes)
+        if not keeps_config(p) and not cur:
+            return [], 0.0
+        pods = self._list_pods(ds["metadata"]["name"]) if self._list_pods is not None else []
+        with_pod = {pod.get("spec", {}).get("nodeName", "") for pod in pods}
+        ready = {pod.get("spec", {}).get("nodeName", "") for pod in pods
+                 if any(c.get("type") == "Ready" and c.get("status") == "True"
+                        for c in (pod.get("status") or {}).get("conditions") or [])}
+        kept = set(cur) | ((ready - {""}) if keeps_config(p) else set())
+        now = self._clock()
+        due, requeue_after = [], 0.0
+        for node in sorted(kept):
+            key = (p.name, node)
+            if node in with_pod:
+                self._missing_since.pop(key, None)
+                continue
+            left = self._missing_since.setdefault(key, now) + KEPT_ORPHAN_GRACE_S - now
+            if left <= 0:
+                due.append(node)
+            else:
+                requeue_after = min(requeue_after, left) if requeue_after else left
+        if due:
+            pending = set(await self._run_cleanups(raw, p, due))
+            for node in due:
+                if node not in pending:
+                    kept.discard(node)
+                    self._missing_since.pop((p.name, node), None)
+            if pending:
+                requeue_after = min(requeue_after, CLEANUP_POLL_S) if requeue_after else CLEANUP_POLL_S
+        return sorted(kept), requeue_after
+
+    async def _finalize(self, raw: dict, p: T.NetworkClusterPolicy) -> Result:
+        """The policy is being deleted and carries FINALIZER: stop the agents (delete the
+        DaemonSet and wait for its Pods to go), clean every kept node, then release the policy."""
+        fins = list(raw["metadata"].get("finalizers") or [])
+        if FINALIZER not in fins:
+            return Result()
+        for ds in self._list_owned(p.name):
+            try:
+                await self.client.delete(kube.DAEMONSETS, ds["metadata"]["name"], self.namespace)
+                log.info("Policy %s is being deleted: removed DaemonSet %s", p.name, ds["metadata"]["name"])
+            except ApiError as e:
+                if not is_not_found(e):
+                    raise
+        if self._list_pods is not None and self._list_pods(p.name):
+            return Result(requeue_after=1.0)  # agents still exiting: a cleanup must not race them
+        pending = await self._run_cleanups(raw, p, list(p.status.keptNodes))
+        if pending:
+            return Result(requeue_after=CLEANUP_POLL_S)
+        body = copy.deepcopy(raw)
+        body["metadata"]["finalizers"] = [f for f in fins if f != FINALIZER]
+        try:
+            await self.client.replace(kube.NETWORKCLUSTERPOLICIES, body)
+        except ApiError as e:
+            if is_conflict(e):
+                return Result(requeue=True)
+            if not is_not_found(e):
+                raise
+        for k in [k for k in self._missing_since if k[0] == p.name]:
+            del self._missing_since[k]
+        log.info("Policy %s: %d node(s) cleaned up, finalizer removed", p.name, len(p.status.keptNodes))
+        return Result()
 
     async def _reconcile_validation(self, raw: dict, p: T.NetworkClusterPolicy, ds: dict, generation: int,
                                     errors: List[str]) -> Optional[tuple]:
@@ -735,7 +905,10 @@ class NetworkClusterPolicyReconciler:
         # status must see the whole list (else every reconcile rewrites an unchanged status).
         v = await self._reconcile_validation(raw, p, ds, generation, errors)
         validated, requeue_after = v if v is not None else (None, 0.0)
-        if cur.state != new_state or cur.errors != errors:
+        kept, kept_requeue = await self._kept_nodes(raw, p, ds)
+        if kept_requeue:
+            requeue_after = min(requeue_after, kept_requeue) if requeue_after else kept_requeue
+        if cur.state != new_state or cur.errors != errors or cur.keptNodes != kept:
             updated = True
         conditions = policy_conditions(cur.conditions, targets, ready, errors, generation)
         if validated is not None:
@@ -750,6 +923,8 @@ class NetworkClusterPolicyReconciler:
         body = copy.deepcopy(raw)
         body["status"] = {"targets": targets, "ready": ready, "state": new_state, "errors": errors,
                           "conditions": conditions, "observedGeneration": generation}
+        if kept:
+            body["status"]["keptNodes"] = kept
         try:
             await self.client.replace_status(kube.NETWORKCLUSTERPOLICIES, body)
         except ApiError as e:
@@ -772,6 +947,21 @@ class NetworkClusterPolicyReconciler:
         if raw is None:
             return Result()  # deleted; ownerRef GC removes the DaemonSet
         p = T.NetworkClusterPolicy.from_dict(raw)
+        if raw["metadata"].get("deletionTimestamp"):
+            return await self._finalize(raw, p)
+        fins = list(raw["metadata"].get("finalizers") or [])
+        want = keeps_config(p) or bool(p.status.keptNodes)  # released only once every kept node is clean
+        if want != (FINALIZER in fins):
+            body = copy.deepcopy(raw)
+            body["metadata"]["finalizers"] = fins + [FINALIZER] if want else [f for f in fins if f != FINALIZER]
+            try:
+                raw = await self.client.replace(kube.NETWORKCLUSTERPOLICIES, body)
+            except ApiError as e:
+                if is_conflict(e):
+                    return Result(requeue=True)
+                if is_not_found(e):
+                    return Result()
+                raise
         owned = self._list_owned(name)
         if not owned:
             return await self._create_daemonset(raw, p)

@@ -439,6 +439,23 @@ async def _scenario(tmp: Path, n_nics: int, mode: str, seed: int, interval: str,
             if update_mtu:
                 # `kubectl edit`: new MTU -> DaemonSet template changes -> the kubelet replaces the
                 # agent -> the new agent configures the NICs again and republishes the label.
+                # Sampled every ~0.5 ms through the roll: how long a NIC was without its /30 (what
+                # an RCCL job's RoCE QPs bound to it would have seen).
+                want = {nif: [p["local"] + "/30"] for nif, p in zip(nic_names, plan)} if mode == "L3" else {}
+                samples = {"n": 0, "missing": 0, "first": None, "last": None}
+                sampling = asyncio.Event()
+
+                async def sample():
+                    idx = {nif: rt.link_by_name(nif)["index"] for nif in want}
+                    while not sampling.is_set():
+                        now = time.monotonic()
+                        samples["n"] += 1
+                        if any(rt.addr_list(i) != want[nif] for nif, i in idx.items()):
+                            samples["missing"] += 1
+                            samples["first"] = samples["first"] or now
+                            samples["last"] = now
+                        await asyncio.sleep(0.0005)
+                sampler = asyncio.ensure_future(sample())
                 t1 = time.monotonic()
                 cur = await c.get(P, name)
                 cur["spec"]["amdScaleOut"]["mtu"] = update_mtu
@@ -449,6 +466,11 @@ async def _scenario(tmp: Path, n_nics: int, mode: str, seed: int, interval: str,
 
                 t_mtu = await _until(mtu_applied, 30)
                 t_relabel = await _until(lambda: node.node_labels().get(label_key) == "true" and all_good(), 30)
+                sampling.set()
+                await sampler
+                res["roll_address_samples"] = samples["n"]
+                res["roll_address_missing_samples"] = samples["missing"]
+                res["roll_address_gap_s"] = round(samples["last"] - samples["first"], 6) if samples["first"] else 0.0
                 res["update_to_mtu_applied_s"] = round(t_mtu - t1, 6) if t_mtu else None
                 res["update_to_ready_again_s"] = round(t_relabel - t1, 6) if t_relabel else None
                 res["agent_starts"] = sum(len(x.started_at) for x in node.containers.values()) + len(node.exited)
@@ -460,6 +482,18 @@ async def _scenario(tmp: Path, n_nics: int, mode: str, seed: int, interval: str,
                 t_unlabel = await _until(lambda: label_key not in node.node_labels(), 10)
                 res["delete_to_agent_stopped_s"] = round(t_gone - t1, 6) if t_gone else None
                 res["delete_to_label_removed_s"] = round(t_unlabel - t1, 6) if t_unlabel else None
+                if policy_kw.get("keepConfigOnRestart"):
+                    # The agent left its addresses; the finalizer holds the policy until the
+                    # cleanup Job (the agent with --cleanup) has removed them.
+                    def cleaned():
+                        return fake.get_object(P, name) is None and all(
+                            rt.addr_list(rt.link_by_name(nif)["index"]) == [] for nif in nic_names)
+                    t_clean = await _until(cleaned, 30)
+                    res["delete_to_cleaned_and_policy_gone_s"] = round(t_clean - t1, 6) if t_clean else None
+                    res["cleanup_job_runs"] = [dict(j, t_start=round(j["t_start"] - t1, 6), t_end=round(j["t_end"] - t1, 6))
+                                               for j in node.job_runs]
+                    art = node.host_path("/etc/amd/scale-out")
+                    res["artifacts_after_cleanup"] = sorted(os.listdir(art)) if art.exists() else []
                 res["after_delete"] = {nif: rt.addr_list(rt.link_by_name(nif)["index"]) for nif in nic_names}
                 res["agent_exit_codes"] = [e["rc"] for e in node.exited]
                 res["agent_sigterm_to_exit_s"] = [e["sigterm_to_exit_s"] for e in node.exited]

@@ -391,6 +391,20 @@ class FakeApiServer:
             self.node_last_exit = {k: v for k, v in self.node_last_exit.items() if k[0] != f"{namespace}/{name}"}
         return obj
 
+    def _delete_or_mark(self, res: Resource, name: str, namespace: str) -> dict:
+        """DELETE as the API server does it: an object with finalizers is only marked
+        (deletionTimestamp) and goes once its last finalizer is removed (see _update)."""
+        key = (namespace if res.namespaced else "", name)
+        cur = self._table(res)[key]
+        if not cur["metadata"].get("finalizers"):
+            return self._delete(res, name, namespace)
+        if not cur["metadata"].get("deletionTimestamp"):
+            new = copy.deepcopy(cur)
+            new["metadata"]["deletionTimestamp"] = _now()
+            new["metadata"]["deletionGracePeriodSeconds"] = 0
+            self._store(res, new, "MODIFIED")
+        return self._table(res)[key]
+
     async def _collect_later(self, uid: str) -> None:
         await asyncio.sleep(self.gc_delay)
         self._collect(uid)
@@ -400,8 +414,8 @@ class FakeApiServer:
         for res in self.resources:
             for (ns, name), o in list(self._table(res).items()):
                 refs = o.get("metadata", {}).get("ownerReferences") or []
-                if any(r.get("uid") == uid for r in refs):
-                    self._delete(res, name, ns)
+                if any(r.get("uid") == uid for r in refs) and (ns, name) in self._table(res):
+                    self._delete_or_mark(res, name, ns)
 
     # ------------------------------------------------------------------------------------------
     # DaemonSet controller simulation
@@ -548,7 +562,7 @@ class FakeApiServer:
             if m == "DELETE":
                 if (ns or "", name) not in self._table(res):
                     return _status(404, "NotFound", f'{res.plural} "{name}" not found')
-                return web.json_response(self._delete(res, name, ns or ""))
+                return web.json_response(self._delete_or_mark(res, name, ns or ""))
             return _status(405, "MethodNotAllowed", m)
         except _Conflict as c:
             return _status(c.code, c.reason, c.message, c.details)
@@ -781,6 +795,9 @@ class FakeApiServer:
                 out["metadata"]["generation"] = cur["metadata"].get("generation", 1) + 1
         if out == cur:
             return cur  # no-op: resourceVersion unchanged, no event
+        if cur["metadata"].get("deletionTimestamp") and not out["metadata"].get("finalizers"):
+            self._store(res, out, "MODIFIED")
+            return self._delete(res, name, key[0])  # the last finalizer is gone
         stored = self._store(res, out, "MODIFIED")
         if res in (kube.DAEMONSETS, kube.NODES) and sub != "status":
             self._sync_daemonsets()

@@ -45,6 +45,7 @@ from typing import Dict, List, Optional, Tuple
 
 from .. import discovery
 from ..operator import kube
+from ..operator.reconciler import CLEANUP_APP
 from ..utils.paths import native_bin
 
 log = logging.getLogger("nodesim")
@@ -300,10 +301,23 @@ class SimNode:
         for _, hp in mounts:
             self.host_path(hp).mkdir(parents=True, exist_ok=True)
         cmd = self.job_images.get(c.get("image", ""))
+        cleanup = (job["metadata"].get("labels") or {}).get("app") == CLEANUP_APP
+        if cleanup:  # the agent image, run as the node's agent binary (like the DaemonSet's Pods)
+            cmd = []
+            # The fake API server removes a deleted Pod at once; a real one keeps it until the
+            # kubelet has stopped its containers, so the operator's "no agent Pods left" means the
+            # agents have exited.  Keep that order here.
+            ds = f"{ns}/{(job['metadata'].get('labels') or {}).get('amd.com/policy', '')}"
+            while any(x.daemonset == ds and x.proc is not None and x.proc.poll() is None
+                      for x in self.containers.values()):
+                await asyncio.sleep(0.005)
         t = time.monotonic()
         rc = -1  # ErrImagePull: no command for this image
         if cmd is not None:
-            argv = list(cmd) + [self._rewrite_arg(a, mounts) for a in c.get("args") or []]
+            if cleanup:
+                argv = self._agent_argv(list(c.get("command") or [])[1:] + list(c.get("args") or []), mounts)
+            else:
+                argv = list(cmd) + [self._rewrite_arg(a, mounts) for a in c.get("args") or []]
             env = dict(os.environ, **self.extra_env, NODE_NAME=self.name)
             if self.sysfs_root is not None:
                 env["SYSFS_ROOT"] = str(self.sysfs_root)

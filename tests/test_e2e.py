@@ -63,6 +63,26 @@ def test_policy_edit_rolls_the_agent_and_the_node_is_ready_again():
     assert r["update_to_ready_again_s"] is not None, (r["policy_status"], r["agent_log"])
     assert r["agent_starts"] == 2  # the first agent was replaced, not restarted on a crash
     assert r["agent_exit_codes"] == [0, 0]
+    # The reference's behaviour (and the default): the old agent removes the addresses on SIGTERM,
+    # the new one adds them again; a job's QPs bound to them lose their source address meanwhile.
+    assert r["roll_address_missing_samples"] > 0 and r["roll_address_gap_s"] > 0
+
+
+def test_keep_config_rolls_the_agent_without_touching_the_addresses_and_deletion_cleans_up():
+    """amdScaleOut.keepConfigOnRestart: the same edit rolls the agent, but no NIC loses its /30 at
+    any sample (the new agent adopts what its LLDP cache confirms).  Deleting the policy stops the
+    agent, which leaves the addresses; the finalizer holds the policy until the operator's cleanup
+    Job (the agent with --cleanup, on the node) has removed them and the agent's files."""
+    r = e2e.run_isolated(n_nics=2, mode="L3", seed=22, update_mtu=4200, teardown=True,
+                         policy_kw={"keepConfigOnRestart": True})
+    assert r["update_to_ready_again_s"] is not None, (r["policy_status"], r["agent_log"])
+    assert "--keep-config" in r["agent_argv"]
+    assert r["roll_address_samples"] > 20 and r["roll_address_missing_samples"] == 0, r
+    assert r["policy_status"]["keptNodes"] == ["mi355x-0"]
+    assert r["delete_to_cleaned_and_policy_gone_s"] is not None, (r["agent_log"], r.get("cleanup_job_runs"))
+    assert [j["rc"] for j in r["cleanup_job_runs"]] == [0]
+    assert all(a == [] for a in r["after_delete"].values())
+    assert r["artifacts_after_cleanup"] == []
 
 
 def test_host_nic_policy_runs_the_driver_container_before_the_agent():

@@ -758,3 +758,63 @@ def test_agent_exit_reason_reaches_status_and_events():
             fake.set_agent_ready("gpu-node-0")
             await eventually(lambda: fake.get_object(kube.NETWORKCLUSTERPOLICIES, "policy")["status"]["errors"] == [])
     run(body())
+
+
+def test_keep_config_policy_cleans_nodes_through_jobs_on_deletion_and_departure(monkeypatch):
+    """keepConfigOnRestart: agents run with --keep-config (and the LLDP cache that lets the next
+    agent adopt the addresses).  The operator records the nodes it configured, and owes each a
+    cleanup Job (the agent with --cleanup, pinned to the node): when the node leaves the policy,
+    after a grace period, and when the policy is deleted, which its finalizer holds until then."""
+    from network_operator_amd.operator import reconciler as R
+
+    monkeypatch.setattr(R, "KEPT_ORPHAN_GRACE_S", 0.3)
+    monkeypatch.setattr(R, "CLEANUP_POLL_S", 0.05)
+
+    async def body():
+        async with cluster(openshift=False) as (fake, client, ctl):
+            for i in range(3):
+                fake.add_node(f"gpu-node-{i}", {"foo": "bar"})
+            await client.create(kube.NETWORKCLUSTERPOLICIES, policy(keepConfigOnRestart=True))
+            await client.create(kube.NETWORKCLUSTERPOLICIES, policy("plain"))
+            await eventually(lambda: fake.get_object(kube.DAEMONSETS, "policy", NS) is not None)
+            args = fake.get_object(kube.DAEMONSETS, "policy", NS)["spec"]["template"]["spec"]["containers"][0]["args"]
+            assert "--keep-config" in args and "--lldp-cache=/host/etc/amd/scale-out/lldp-cache" in args
+            for i in range(3):
+                fake.set_agent_ready(f"gpu-node-{i}", daemonset=f"{NS}/policy")
+
+            def pol(name="policy"):
+                return fake.get_object(kube.NETWORKCLUSTERPOLICIES, name)
+            await eventually(lambda: pol()["status"].get("keptNodes") == [f"gpu-node-{i}" for i in range(3)])
+            assert pol()["metadata"]["finalizers"] == [R.FINALIZER]
+            assert not pol("plain")["metadata"].get("finalizers") and "keptNodes" not in pol("plain")["status"]
+
+            # gpu-node-2 leaves the policy: its agent Pod goes; after the grace period, a cleanup Job
+            fake.set_node_labels("gpu-node-2", {"foo": "other"})
+            job = await value(lambda: next(iter(fake.list_objects(kube.JOBS)), None), timeout=5)
+            spec = job["spec"]["template"]["spec"]
+            c = spec["containers"][0]
+            assert spec["nodeName"] == "gpu-node-2" and spec["restartPolicy"] == "Never" and spec["hostNetwork"]
+            assert "--cleanup" in c["args"] and "--keep-running" not in c["args"] and "--keep-config" not in c["args"]
+            assert "readinessProbe" not in c and "nodeSelector" not in spec
+            assert job["metadata"]["ownerReferences"][0]["name"] == "policy"
+            await asyncio.sleep(0.2)
+            assert pol()["status"]["keptNodes"] == [f"gpu-node-{i}" for i in range(3)]  # owed until it ran
+            fake.set_job_result(job["metadata"]["name"], NS, True)
+            await eventually(lambda: pol()["status"].get("keptNodes") == ["gpu-node-0", "gpu-node-1"])
+            await eventually(lambda: fake.list_objects(kube.JOBS) == [])
+
+            # deletion: the finalizer holds the policy until both remaining nodes ran their cleanup
+            await client.delete(kube.NETWORKCLUSTERPOLICIES, "policy")
+            await eventually(lambda: fake.get_object(kube.DAEMONSETS, "policy", NS) is None)
+            await eventually(lambda: sorted(j["spec"]["template"]["spec"]["nodeName"]
+                                            for j in fake.list_objects(kube.JOBS)) == ["gpu-node-0", "gpu-node-1"])
+            assert pol()["metadata"]["deletionTimestamp"]
+            for j in fake.list_objects(kube.JOBS):
+                fake.set_job_result(j["metadata"]["name"], NS, j["spec"]["template"]["spec"]["nodeName"] == "gpu-node-0")
+            await eventually(lambda: pol() is None)
+            ev = [e for e in fake.list_objects(kube.EVENTS) if e["reason"] == "NodeCleanupFailed"]
+            assert len(ev) == 1 and ev[0]["message"].startswith("gpu-node-1: cleanup Job")
+            assert pol("plain") is not None
+            await client.delete(kube.NETWORKCLUSTERPOLICIES, "plain")  # no finalizer: gone at once
+            assert pol("plain") is None
+    run(body())

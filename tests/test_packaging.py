@@ -99,6 +99,17 @@ def test_helm_policy_rendering_and_validation():
     assert "lldpWait" not in cr["spec"]["amdScaleOut"]  # the agent's 90s
     waited = _chart_policies(helm_template(CHART, {"config": {"amd": {"enabled": True, "lldpWait": "15s"}}}))[0]
     assert waited["spec"]["amdScaleOut"]["lldpWait"] == "15s" and CRD.validate(waited) == []
+    assert "keepConfigOnRestart" not in cr["spec"]["amdScaleOut"] and not [
+        d for d in docs if d["kind"] == "Job"]  # no pre-delete hook without keepConfigOnRestart
+    keep_docs = helm_template(CHART, {"config": {"amd": {"enabled": True, "keepConfigOnRestart": True}}})
+    kept = _chart_policies(keep_docs)[0]
+    assert kept["spec"]["amdScaleOut"]["keepConfigOnRestart"] is True and CRD.validate(kept) == []
+    hook = _by_kind(keep_docs, "Job")
+    assert len(hook) == 1 and hook[0]["metadata"]["annotations"]["helm.sh/hook"] == "pre-delete"
+    c = hook[0]["spec"]["template"]["spec"]["containers"][0]
+    assert c["command"] == ["python3", "-m", "network_operator_amd.operator.predelete"]
+    assert "--owner=ClusterRole/amd-network-operator" in c["args"]
+    assert hook[0]["spec"]["template"]["spec"]["serviceAccountName"] == "amd-network-operator"
     with pytest.raises(RenderError, match="Invalid layer mode"):
         helm_template(CHART, {"config": {"amd": {"enabled": True, "mode": "L4"}}})
     for mtu in (1499, 9001):
