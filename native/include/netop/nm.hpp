@@ -34,13 +34,20 @@ std::unique_ptr<NetworkManagerIf> connect_system_bus(const std::string& address 
 // Returns the interfaces that were switched to unmanaged.  Throws on device errors.
 std::vector<std::string> disable_for_interfaces(NetworkManagerIf& nm, const std::vector<std::string>& ifaces);
 
-// Keyfile snippet for /etc/NetworkManager/conf.d/.
+// Keyfile snippet for /etc/NetworkManager/conf.d/.  The list is appended to
+// ("unmanaged-devices+="), so the files of two agents on one node (an amd-so and a host-nic
+// policy) and the host's own setting all apply; a plain "=" in a later file would replace them.
 std::string keyfile_snippet(const std::vector<std::string>& ifaces);
-// Writes <conf_dir>/99-amd-network-operator.conf if conf_dir's parent exists; returns the path or "".
-std::string write_keyfile(const std::string& conf_dir, const std::vector<std::string>& ifaces);
+// The keyfile's name for an agent publishing `label_file`: 99-amd-network-operator.conf for the
+// default scale-out label file, 99-amd-network-operator-<label file stem>.conf otherwise (one
+// file per agent, so one agent's teardown never removes another's).
+std::string keyfile_name(const std::string& label_file);
+// Writes <conf_dir>/<name> if conf_dir's parent exists; returns the path or "".
+std::string write_keyfile(const std::string& conf_dir, const std::vector<std::string>& ifaces,
+                          const std::string& name = keyfile_name(""));
 // Teardown: removes that keyfile if it is ours (starts with the agent's header line), so the NICs
 // go back to NetworkManager at its next start.  True when a file was removed.
-bool remove_keyfile(const std::string& conf_dir);
+bool remove_keyfile(const std::string& conf_dir, const std::string& name = keyfile_name(""));
 // Teardown of the runtime change: Managed=true again on the named devices NM knows.  Returns the
 // interfaces re-managed.  Throws on device errors.
 std::vector<std::string> restore_for_interfaces(NetworkManagerIf& nm, const std::vector<std::string>& ifaces);

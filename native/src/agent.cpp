@@ -201,7 +201,7 @@ void Agent::restore_network_manager() {
     // Only with --nm-restore: the reference leaves its runtime Managed=false behind, and this
     // agent's keyfile keeps the NICs unmanaged across agent restarts and reboots (Config::nm_restore).
     if (!cfg_.nm_restore) return;
-    if (nm_keyfile_written_ && nm::remove_keyfile(cfg_.nm_keyfile_dir)) {
+    if (nm_keyfile_written_ && nm::remove_keyfile(cfg_.nm_keyfile_dir, nm::keyfile_name(cfg_.labels.file))) {
         NLOG_I("Removed NetworkManager keyfile from %s", cfg_.nm_keyfile_dir.c_str());
         nm_keyfile_written_ = false;
     }
@@ -1333,7 +1333,7 @@ void Agent::run(int stop_fd) {
     if (cfg_.disable_nm) {
         if (!cfg_.nm_keyfile_dir.empty()) {
             try {
-                auto p = nm::write_keyfile(cfg_.nm_keyfile_dir, names);
+                auto p = nm::write_keyfile(cfg_.nm_keyfile_dir, names, nm::keyfile_name(cfg_.labels.file));
                 if (!p.empty()) {
                     NLOG_I("Wrote NetworkManager keyfile %s", p.c_str());
                     nm_keyfile_written_ = true;

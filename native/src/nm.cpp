@@ -3,6 +3,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <cctype>
 
 #include "netop/common.hpp"
 #include "netop/dbus.hpp"
@@ -88,9 +89,17 @@ std::vector<std::string> restore_for_interfaces(NetworkManagerIf& nm, const std:
     return done;
 }
 
-bool remove_keyfile(const std::string& conf_dir) {
+std::string keyfile_name(const std::string& label_file) {
+    if (label_file.empty() || label_file == "scale-out-readiness.txt") return kKeyfileName;
+    std::string stem = label_file.substr(0, label_file.rfind('.'));
+    for (char& c : stem)
+        if (!std::isalnum(static_cast<unsigned char>(c)) && c != '-' && c != '_') c = '-';
+    return "99-amd-network-operator-" + stem + ".conf";
+}
+
+bool remove_keyfile(const std::string& conf_dir, const std::string& name) {
     if (conf_dir.empty()) return false;
-    std::string path = path_join(conf_dir, kKeyfileName);
+    std::string path = path_join(conf_dir, name);
     auto s = read_file(path);
     if (!s || s->rfind(kKeyfileHeader, 0) != 0) return false;  // absent, or not written by us
     return ::unlink(path.c_str()) == 0;
@@ -101,14 +110,15 @@ std::string keyfile_snippet(const std::vector<std::string>& ifaces) {
     for (auto& i : ifaces) items.push_back("interface-name:" + i);
     return std::string(kKeyfileHeader) +
            "[keyfile]\n"
-           "unmanaged-devices=" +
+           "unmanaged-devices+=" +
            join(items, ";") + "\n";
 }
 
-std::string write_keyfile(const std::string& conf_dir, const std::vector<std::string>& ifaces) {
+std::string write_keyfile(const std::string& conf_dir, const std::vector<std::string>& ifaces,
+                          const std::string& name) {
     if (ifaces.empty() || !is_dir(path_dirname(conf_dir))) return "";
     mkdir_p(conf_dir);
-    std::string path = path_join(conf_dir, kKeyfileName);
+    std::string path = path_join(conf_dir, name);
     write_file_atomic(path, keyfile_snippet(ifaces), 0644);
     return path;
 }

@@ -526,7 +526,7 @@ TEST(agent_networkmanager_paths) {
     CHECK(!seen["ens1"]);
     CHECK(seen["eth9"]);
     auto kf = read_file(f.cfg.nm_keyfile_dir + "/99-amd-network-operator.conf");
-    CHECK(kf && kf->find("unmanaged-devices=interface-name:ens0;interface-name:ens1;interface-name:ens2") != std::string::npos);
+    CHECK(kf && kf->find("unmanaged-devices+=interface-name:ens0;interface-name:ens1;interface-name:ens2") != std::string::npos);
 
     // NM absent (version query fails) -> silently skipped (networkmanager.go:81-86).
     MockNm nm1;
@@ -582,6 +582,37 @@ TEST(agent_networkmanager_changes_undone_on_sigterm) {
     g.tmp.write("NetworkManager/conf.d/99-amd-network-operator.conf", "[keyfile]\nunmanaged-devices=mac:aa\n");
     CHECK(!nm::remove_keyfile(g.cfg.nm_keyfile_dir));
     CHECK(path_exists(g.cfg.nm_keyfile_dir + "/99-amd-network-operator.conf"));
+}
+
+TEST(agent_networkmanager_keyfiles_of_two_agents_on_one_node_coexist) {
+    // An amd-so and a host-nic agent on one node, both taking their NICs from NetworkManager:
+    // each has its own keyfile, both append to the unmanaged list, and one's hand-back leaves the
+    // other's NICs unmanaged.
+    CHECK_EQ(nm::keyfile_name(""), std::string("99-amd-network-operator.conf"));
+    CHECK_EQ(nm::keyfile_name("scale-out-readiness.txt"), std::string("99-amd-network-operator.conf"));
+    CHECK_EQ(nm::keyfile_name("host-nic-readiness.txt"), std::string("99-amd-network-operator-host-nic-readiness.conf"));
+    Fixture f;
+    f.cfg.disable_nm = true;
+    f.cfg.nm_restore = true;
+    f.cfg.nm_keyfile_dir = f.tmp.path + "/NetworkManager/conf.d";
+    f.tmp.mkdir("NetworkManager");
+    agent::Config host = f.cfg;
+    host.interfaces = "ens2";
+    host.labels.file = "host-nic-readiness.txt";
+    host.labels.key = "amd.feature.node.kubernetes.io/host-nic-ready";
+    host.keep_running = false;
+    f.cfg.interfaces = "ens0,ens1";
+    {
+        agent::Agent h(host, f.ops, f.all_valid(), f.nm());
+        h.run(-1);
+    }
+    Pipe stop;
+    stop.fire();
+    agent::Agent a(f.cfg, f.ops, f.all_valid(), f.nm());
+    a.run(stop.fd[0]);  // configures, then SIGTERM with --nm-restore: removes only its own file
+    CHECK(!path_exists(f.cfg.nm_keyfile_dir + "/99-amd-network-operator.conf"));
+    auto kf = read_file(f.cfg.nm_keyfile_dir + "/99-amd-network-operator-host-nic-readiness.conf");
+    CHECK(kf && kf->find("unmanaged-devices+=interface-name:ens2\n") != std::string::npos);
 }
 
 TEST(agent_stale_label_removed_and_networkd) {
@@ -1574,8 +1605,18 @@ TEST(agent_cleanup_mode_removes_what_kept_agents_left) {
     agent::Config c = f.cfg;
     c.cleanup = true;
     c.keep_config = false;
-    agent::Agent k(c, f.ops, std::make_unique<ScriptedLldp>(), f.nm());
+    // NetworkManager: the agents left the NICs unmanaged (keyfile + Managed=false); the
+    // policy-deletion cleanup (--nm-restore) hands them back.
+    c.disable_nm = true;
+    c.nm_restore = true;
+    c.nm_keyfile_dir = f.tmp.path + "/NetworkManager/conf.d";
+    f.tmp.mkdir("NetworkManager");
+    CHECK(!nm::write_keyfile(c.nm_keyfile_dir, {"ens0", "ens1", "ens2"}).empty());
+    std::map<std::string, bool> managed{{"ens0", false}, {"ens1", false}, {"eth9", true}};  // what NM knows
+    agent::Agent k(c, f.ops, std::make_unique<ScriptedLldp>(), f.nm(&managed));
     k.run(-1);
+    CHECK(!path_exists(c.nm_keyfile_dir + "/99-amd-network-operator.conf"));
+    CHECK(managed["ens0"] && managed["ens1"] && managed["eth9"]);
     CHECK(f.ops.addrs.empty());
     CHECK_EQ(f.ops.rules.size(), size_t(1));
     CHECK(f.ops.rules[0] == foreign);

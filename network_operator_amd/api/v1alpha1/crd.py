@@ -193,8 +193,9 @@ def openapi_schema() -> dict:
                 },
             },
             "errors": {"items": {"type": "string"}, "type": "array"},
-            "keptNodes": {"description": "keepConfigOnRestart: nodes whose configuration a cleanup Job still has to\n"
-                                         "remove when the policy is deleted or the node leaves it.",
+            "keptNodes": {"description": "Nodes whose agents left configuration behind (keepConfigOnRestart: addresses\n"
+                                         "and routes; disableNetworkManager: NICs unmanaged) that a cleanup Job still\n"
+                                         "has to remove when the policy is deleted or the node leaves it.",
                           "items": {"type": "string"}, "type": "array"},
             "observedGeneration": {"description": "The spec generation the status describes.",
                                    "format": "int64", "type": "integer"},

@@ -290,7 +290,8 @@ class NetworkClusterPolicyStatus:
     # Additive (not in the reference): standard conditions and the generation they describe.
     conditions: List[dict] = field(default_factory=list)
     observedGeneration: int = 0
-    # keepConfigOnRestart: nodes whose agents may have left configuration behind (cleanup owed).
+    # Nodes whose agents left configuration behind (keepConfigOnRestart, disableNetworkManager):
+    # a cleanup Job is owed to each (reconciler.needs_node_cleanup).
     keptNodes: List[str] = field(default_factory=list)
 
     def to_dict(self) -> dict:

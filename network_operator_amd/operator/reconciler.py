@@ -447,6 +447,19 @@ def keeps_config(p: T.NetworkClusterPolicy) -> bool:
     return p.spec.configurationType == T.CONFIG_AMD_SCALE_OUT and p.spec.amdScaleOut.keepConfigOnRestart
 
 
+def disables_nm(p: T.NetworkClusterPolicy) -> bool:
+    if p.spec.configurationType == T.CONFIG_AMD_SCALE_OUT:
+        return p.spec.amdScaleOut.disableNetworkManager
+    return p.spec.configurationType == T.CONFIG_HOST_NIC and bool(p.spec.hostNic and p.spec.hostNic.disableNetworkManager)
+
+
+def needs_node_cleanup(p: T.NetworkClusterPolicy) -> bool:
+    """The agents leave something on the node that only a cleanup Job removes: the data plane
+    (keepConfigOnRestart) or NetworkManager's hands off the NICs (disableNetworkManager: kept
+    across agent restarts on purpose, handed back once the policy no longer covers the node)."""
+    return keeps_config(p) or disables_nm(p)
+
+
 def cleanup_job_name(policy: str, node: str) -> str:
     import hashlib
 
@@ -468,7 +481,7 @@ def cleanup_job(p: T.NetworkClusterPolicy, node: str, namespace: str) -> dict:
     for k in ("readinessProbe", "livenessProbe", "startupProbe"):
         c.pop(k, None)
     c["args"] = [a for a in c.get("args") or [] if a not in ("--keep-running", "--keep-config")] + \
-        ["--cleanup", f"--nfd-features-dir={discovery.LABEL_FEATURES_DIR}"]
+        ["--cleanup", f"--nfd-features-dir={discovery.LABEL_FEATURES_DIR}"] + (["--nm-restore"] if disables_nm(p) else [])
     labels = {"app": CLEANUP_APP, "amd.com/policy": p.name[:63]}
     return {
         "apiVersion": "batch/v1", "kind": "Job",
@@ -680,14 +693,14 @@ class NetworkClusterPolicyReconciler:
         its agent is Ready; it leaves after its cleanup Job, which runs once its agent Pod has been
         gone for KEPT_ORPHAN_GRACE_S."""
         cur = list(p.status.keptNodes)
-        if not keeps_config(p) and not cur:
+        if not needs_node_cleanup(p) and not cur:
             return [], 0.0
         pods = self._list_pods(ds["metadata"]["name"]) if self._list_pods is not None else []
         with_pod = {pod.get("spec", {}).get("nodeName", "") for pod in pods}
         ready = {pod.get("spec", {}).get("nodeName", "") for pod in pods
                  if any(c.get("type") == "Ready" and c.get("status") == "True"
                         for c in (pod.get("status") or {}).get("conditions") or [])}
-        kept = set(cur) | ((ready - {""}) if keeps_config(p) else set())
+        kept = set(cur) | ((ready - {""}) if needs_node_cleanup(p) else set())
         now = self._clock()
         due, requeue_after = [], 0.0
         for node in sorted(kept):
@@ -950,7 +963,7 @@ class NetworkClusterPolicyReconciler:
         if raw["metadata"].get("deletionTimestamp"):
             return await self._finalize(raw, p)
         fins = list(raw["metadata"].get("finalizers") or [])
-        want = keeps_config(p) or bool(p.status.keptNodes)  # released only once every kept node is clean
+        want = needs_node_cleanup(p) or bool(p.status.keptNodes)  # released only once every kept node is clean
         if want != (FINALIZER in fins):
             body = copy.deepcopy(raw)
             body["metadata"]["finalizers"] = fins + [FINALIZER] if want else [f for f in fins if f != FINALIZER]

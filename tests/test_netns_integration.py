@@ -320,7 +320,7 @@ def test_networkmanager_unmanaged_while_ready_and_handed_back_on_sigterm():
         pytest.skip("dbus-daemon not installed")
     r = netns.run_isolated(n_nics=4, seed=5, interval="30s", fast_start=True, nm_bus=True)
     assert r["label"] and r["agent_rc"] == 0
-    assert "unmanaged-devices=" + ";".join(f"interface-name:{n}" for n in r["nics"]) in r["nm_keyfile_while_ready"]
+    assert "unmanaged-devices+=" + ";".join(f"interface-name:{n}" for n in r["nics"]) in r["nm_keyfile_while_ready"]
     assert r["nm_managed_while_ready"] == {**{n: False for n in r["nics"]}, "eth9": True}
     assert r["nm_keyfile_after_sigterm"] is False
     assert r["nm_managed_after_sigterm"] == {**{n: True for n in r["nics"]}, "eth9": True}

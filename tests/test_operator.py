@@ -818,3 +818,34 @@ def test_keep_config_policy_cleans_nodes_through_jobs_on_deletion_and_departure(
             await client.delete(kube.NETWORKCLUSTERPOLICIES, "plain")  # no finalizer: gone at once
             assert pol("plain") is None
     run(body())
+
+
+def test_network_manager_is_handed_back_when_the_policy_goes():
+    """disableNetworkManager keeps the NICs unmanaged across agent restarts: the
+    hand-back happens once, when the policy is deleted: a cleanup Job with --nm-restore per node
+    that ran the agent, held by the node-cleanup finalizer.  host-nic policies alike."""
+    from network_operator_amd.operator import reconciler as R
+
+    async def body():
+        async with cluster(openshift=False) as (fake, client, ctl):
+            fake.add_node("gpu-node-0", {"foo": "bar"})
+            await client.create(kube.NETWORKCLUSTERPOLICIES, policy(disableNetworkManager=True))
+            hn = T.new_host_nic_policy("hosts", layer="L2", node_selector={"foo": "bar"}, disableNetworkManager=True)
+            await client.create(kube.NETWORKCLUSTERPOLICIES, hn.to_dict())
+            for name in ("policy", "hosts"):
+                await eventually(lambda: fake.get_object(kube.DAEMONSETS, name, NS) is not None)
+                fake.set_agent_ready("gpu-node-0", daemonset=f"{NS}/{name}")
+            for name in ("policy", "hosts"):
+                await eventually(lambda: (fake.get_object(kube.NETWORKCLUSTERPOLICIES, name).get("status") or {})
+                                 .get("keptNodes") == ["gpu-node-0"])
+                assert fake.get_object(kube.NETWORKCLUSTERPOLICIES, name)["metadata"]["finalizers"] == [R.FINALIZER]
+                await client.delete(kube.NETWORKCLUSTERPOLICIES, name)
+                job = await value(lambda: next((j for j in fake.list_objects(kube.JOBS)
+                                                if j["metadata"]["labels"]["amd.com/policy"] == name), None))
+                args = job["spec"]["template"]["spec"]["containers"][0]["args"]
+                assert "--cleanup" in args and "--nm-restore" in args and "--disable-networkmanager" in args
+                if name == "hosts":  # its own label file, hence its own NetworkManager keyfile
+                    assert "--nfd-label-file=host-nic-readiness.txt" in args
+                fake.set_job_result(job["metadata"]["name"], NS, True)
+                await eventually(lambda: fake.get_object(kube.NETWORKCLUSTERPOLICIES, name) is None)
+    run(body())
