@@ -134,6 +134,14 @@ struct Config {
     std::string lldp_cache;
     int64_t lldp_cache_max_age_ns = 7LL * 24 * 3600 * 1000000000;  // older entries are ignored
     int64_t lldp_cache_confirm_ns = 95LL * 1000000000;              // 3 x msgTxInterval + 5 s
+    // Node-wide mutual exclusion between agents that configure the same NICs (an exiting and a
+    // starting agent, an agent and the --cleanup Job, two policies selecting one node): an
+    // abstract unix socket of this name, held for the agent's lifetime.  hostNetwork Pods share
+    // the node's network namespace, so the name is node-wide, and the kernel releases it when the
+    // process dies, SIGKILL included.  "" = off (discover's --node-lock defaults it from the
+    // label file, so an amd-so and a host-nic agent never wait for each other).
+    std::string node_lock;
+    int64_t node_lock_wait_ns = 60LL * 1000000000;
 };
 
 // FRA_PROTOCOL / rtm_protocol tag on the agent's rail rules and rail-table routes ("installed by
@@ -272,6 +280,8 @@ class Agent {
     void save_lldp_cache();
     bool nm_keyfile_written_ = false;
     std::vector<std::string> nm_unmanaged_;
+    int node_lock_fd_ = -1;
+    void acquire_node_lock(int stop_fd);
 
    public:
     // Prometheus text exposition of the agent state (served on Config::metrics_addr).

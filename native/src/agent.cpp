@@ -6,7 +6,10 @@
 #include <sys/epoll.h>
 #include <sys/resource.h>
 #include <sys/socket.h>
+#include <sys/un.h>
 #include <unistd.h>
+
+#include <cstddef>
 
 #include <algorithm>
 #include <cstring>
@@ -107,7 +110,44 @@ Agent::Agent(Config cfg, nl::NetOps& ops, std::unique_ptr<LldpSource> lldp, NmFa
     };
 }
 
+void Agent::acquire_node_lock(int stop_fd) {
+    if (cfg_.node_lock.empty() || node_lock_fd_ >= 0) return;
+    sockaddr_un sa{};
+    sa.sun_family = AF_UNIX;
+    const std::string name = "netop-agent:" + cfg_.node_lock;
+    const size_t n = std::min(name.size(), sizeof sa.sun_path - 1);
+    std::memcpy(sa.sun_path + 1, name.data(), n);  // abstract: sun_path[0] == 0
+    const socklen_t len = socklen_t(offsetof(sockaddr_un, sun_path) + 1 + n);
+    const int64_t deadline = mono_ns() + cfg_.node_lock_wait_ns;
+    bool waited = false;
+    for (;;) {
+        int fd = ::socket(AF_UNIX, SOCK_STREAM | SOCK_CLOEXEC, 0);
+        if (fd < 0) throw AgentError(std::string("node lock: socket: ") + std::strerror(errno));
+        if (::bind(fd, reinterpret_cast<sockaddr*>(&sa), len) == 0) {
+            node_lock_fd_ = fd;
+            if (waited) NLOG_I("Node lock '%s' acquired", cfg_.node_lock.c_str());
+            return;
+        }
+        const int err = errno;
+        ::close(fd);
+        if (err != EADDRINUSE) throw AgentError(std::string("node lock: bind: ") + std::strerror(err));
+        if (!waited) NLOG_I("Node lock '%s' is held by another agent on this node: waiting", cfg_.node_lock.c_str());
+        waited = true;
+        if (mono_ns() >= deadline)
+            throw AgentError("Another agent (or its cleanup) holds the node lock '" + cfg_.node_lock +
+                             "': two policies of one configuration type select this node, or the previous agent is "
+                             "still exiting");
+        if (stop_fd >= 0) {
+            pollfd p{stop_fd, POLLIN, 0};
+            if (::poll(&p, 1, 100) > 0) throw AgentError("Interrupted while waiting for the node lock");
+        } else {
+            ::usleep(100000);
+        }
+    }
+}
+
 Agent::~Agent() {
+    if (node_lock_fd_ >= 0) ::close(node_lock_fd_);
     // Both socket sets wait for an RCU grace period when closed: overlap the two waits, so
     // --verify-peers adds nothing to SIGTERM -> exit.
     std::thread closing;
@@ -1296,7 +1336,11 @@ void Agent::run(int stop_fd) {
         }
         write_status();
     }
-    if (!cfg_.dry_run) pre_cleanups();
+    if (!cfg_.dry_run) {
+        acquire_node_lock(stop_fd);
+        mark("node_lock");
+        pre_cleanups();
+    }
 
     auto names = collect_interfaces();
     if (names.empty()) throw AgentError("No interfaces found");

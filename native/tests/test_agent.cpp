@@ -4,7 +4,11 @@
 #include <poll.h>
 #include <netinet/in.h>
 #include <sys/socket.h>
+#include <sys/un.h>
 #include <unistd.h>
+
+#include <cstddef>
+#include <cstring>
 
 #include "check.hpp"
 #include "fake_netops.hpp"
@@ -1627,4 +1631,43 @@ TEST(agent_cleanup_mode_removes_what_kept_agents_left) {
     CHECK_EQ(k.ready(), false);
     auto st = read_file(f.cfg.status_file);
     CHECK(st && st->find("cleanup") != std::string::npos);
+}
+
+TEST(agent_node_lock_keeps_two_agents_of_one_kind_apart) {
+    // The lock is an abstract unix socket: held by a live agent (here: by the test), a second
+    // agent with the same name waits, then fails naming the cause; free, it is taken at once.
+    Fixture f;
+    f.cfg.keep_running = false;
+    f.cfg.node_lock = "test-lock-" + std::to_string(::getpid());
+    f.cfg.node_lock_wait_ns = 150000000;  // 150 ms
+    sockaddr_un sa{};
+    sa.sun_family = AF_UNIX;
+    const std::string name = "netop-agent:" + f.cfg.node_lock;
+    std::memcpy(sa.sun_path + 1, name.data(), name.size());
+    int holder = ::socket(AF_UNIX, SOCK_STREAM, 0);
+    CHECK(::bind(holder, reinterpret_cast<sockaddr*>(&sa), socklen_t(offsetof(sockaddr_un, sun_path) + 1 + name.size())) == 0);
+    {
+        agent::Agent a(f.cfg, f.ops, f.all_valid(), f.nm());
+        const int64_t t0 = mono_ns();
+        bool threw = false;
+        try {
+            a.run(-1);
+        } catch (const agent::AgentError& e) {
+            threw = std::string(e.what()).find("holds the node lock") != std::string::npos;
+        }
+        CHECK(threw);
+        CHECK(mono_ns() - t0 >= 140000000LL);
+        CHECK(f.ops.addrs.empty());  // touched nothing
+    }
+    ::close(holder);  // the other agent exits (or dies): the kernel frees the name
+    agent::Agent b(f.cfg, f.ops, f.all_valid(), f.nm());
+    b.run(-1);
+    CHECK_EQ(f.ops.addrs.size(), size_t(3));
+    // Another name (a host-nic agent next to the scale-out one) never waits.
+    agent::Config other = f.cfg;
+    other.node_lock = f.cfg.node_lock + "-host-nic";
+    agent::Agent c(other, f.ops, f.all_valid(), f.nm());
+    const int64_t t1 = mono_ns();
+    c.run(-1);
+    CHECK(mono_ns() - t1 < 140000000LL);
 }

@@ -77,6 +77,9 @@ int main(int argc, char** argv) {
     fs.add_bool("lldp-restart-fast", &cfg.announce_shutdown_first, "send a shutdown LLDPDU before the first announcement so a switch holding a stale entry (agent restart) fast-starts again");
     fs.add_bool("keep-config", &cfg.keep_config, "on exit withdraw only the readiness label: addresses, routes, rail rules and links stay for the next agent, which adopts the /30 its LLDP cache confirms (hitless agent restarts; needs --lldp-cache in L3)");
     fs.add_bool("cleanup", &cfg.cleanup, "one-shot: remove what --keep-config agents left on the node (IPv4 addresses of the discovered NICs, tagged rail rules and routes, label, artifacts, LLDP cache, networkd files) and exit");
+    std::string node_lock = "auto";
+    fs.add_string("node-lock", &node_lock, "node-wide lock (abstract unix socket) held while the agent runs, so agents configuring the same NICs never overlap (exiting vs starting agent, agent vs --cleanup, two policies on one node): auto (named after --nfd-label-file), none, or a name");
+    fs.add_duration("node-lock-wait", &cfg.node_lock_wait_ns, "how long to wait for the node lock before failing");
     fs.add_bool("dry-run", &cfg.dry_run, "discover, check xGMI / GPUDirect RDMA and write the topology file and status only: no link, address, NetworkManager or label change, no LLDP (needs no privileges)");
     fs.add_string("lldp-cache", &cfg.lldp_cache, "with --keep-running: remember each NIC's confirmed Port Description in this file and configure from it at start (the switch must confirm it within --lldp-cache-confirm)");
     fs.add_duration("lldp-cache-max-age", &cfg.lldp_cache_max_age_ns, "ignore LLDP cache entries older than this");
@@ -124,6 +127,10 @@ int main(int argc, char** argv) {
         std::fprintf(stderr, "Error: --rail-table-base must be 0 (off) or 1..200\n");
         return 2;
     }
+    if (node_lock == "auto")
+        cfg.node_lock = cfg.labels.file;
+    else if (node_lock != "none")
+        cfg.node_lock = node_lock;
     cfg.discovery.mode = *dm;
     cfg.token_policy = *tp;
     if (!nic_drivers.empty()) cfg.discovery.nic_drivers = split(nic_drivers, ',');

@@ -70,6 +70,23 @@ async def _until(fn, timeout: float, poll: float = 0.001) -> Optional[float]:
     return None
 
 
+async def _edit(c, res, name: str, change, attempts: int = 50) -> dict:
+    """kubectl edit: get, change, replace, again on a conflict (the operator writes the status
+    and its finalizer concurrently)."""
+    from ..operator.kube import ApiError
+
+    for _ in range(attempts):
+        cur = await c.get(res, name)
+        change(cur)
+        try:
+            return await c.replace(res, cur)
+        except ApiError as e:
+            if e.status != 409:
+                raise
+            await asyncio.sleep(0.01)
+    raise RuntimeError(f"edit of {name} kept conflicting")
+
+
 def _free_port() -> int:
     import socket
 
@@ -207,9 +224,7 @@ async def _ha_checks(fake, c, rt, node, replicas: list, ns: str, name: str, mode
     await leader["proc"].wait()
     for k in list(fake.service_endpoints):  # the endpoints controller drops the dead pod
         fake.service_endpoints[k] = f"https://127.0.0.1:{standby['webhook']}"
-    cur = await c.get(P, name)
-    cur["spec"]["amdScaleOut"]["mtu"] = new_mtu
-    gen = (await c.replace(P, cur))["metadata"]["generation"]
+    gen = (await _edit(c, P, name, lambda cur: cur["spec"]["amdScaleOut"].update(mtu=new_mtu)))["metadata"]["generation"]
     t_lead = await _until(lambda: _lease_holder(fake, ns).startswith(standby["name"] + "_"), 30)
     t_mtu = await _until(lambda: all(rt.link_by_name(n)["mtu"] == new_mtu for n in nic_names), 30)
 
@@ -231,7 +246,7 @@ async def _ha_checks(fake, c, rt, node, replicas: list, ns: str, name: str, mode
 async def _scenario(tmp: Path, n_nics: int, mode: str, seed: int, interval: str, fast_start: bool,
                     teardown: bool, node_name: str, policy_kw: dict, update_mtu: int, config_type: str,
                     flap: bool, validation: str, crash_agent: bool, driver_reload: bool, ha: bool,
-                    silent_nics: int = 0, lldp_wait: str = "") -> dict:
+                    silent_nics: int = 0, lldp_wait: str = "", duplicate_policy: bool = False) -> dict:
     from ..api.v1alpha1 import types as T
     from ..operator import kube, manager
     from ..operator.kube import ApiClient, KubeConfig
@@ -288,7 +303,8 @@ async def _scenario(tmp: Path, n_nics: int, mode: str, seed: int, interval: str,
                    sysfs_root=tmp / "sys", init_images={KMD_IMAGE: kmd},
                    env={"PYTHONPATH": str(Path(__file__).resolve().parents[2])},
                    job_images={T0.DEFAULT_VALIDATION_IMAGE: [sys.executable, "-c", _VALIDATE_STUB, validation or "pass"]},
-                   agent_arg_overrides={"--wait": lldp_wait} if lldp_wait else None)
+                   agent_arg_overrides={**({"--wait": lldp_wait} if lldp_wait else {}),
+                                        **({"--node-lock-wait": "1s"} if duplicate_policy else {})} or None)
     if validation and not host_nic:
         policy_kw = dict(policy_kw, validation={"enabled": True, "minBusbw": 300})
     P, DS = kube.NETWORKCLUSTERPOLICIES, kube.DAEMONSETS
@@ -365,6 +381,25 @@ async def _scenario(tmp: Path, n_nics: int, mode: str, seed: int, interval: str,
             res["operator_metrics"] = await _scrape(metrics_port, ("amd_network_operator_agent_ready_seconds_count",
                                                                    "amd_network_operator_agent_ready_seconds_sum",
                                                                    "amd_network_operator_policy_ready"))
+            if duplicate_policy:
+                # A second amd-so policy selecting the same node: its agent would flush and
+                # re-address the same NICs.  The node lock keeps it out: it fails, the reason
+                # reaches that policy's status, and the first policy's node stays configured.
+                addrs_before = {nif: rt.addr_list(rt.link_by_name(nif)["index"]) for nif in nic_names}
+                await c.create(P, T.new_policy("scale-out-dup", layer=mode, mtu=9000, **policy_kw).to_dict())
+
+                def dup_error():
+                    st = (fake.get_object(P, "scale-out-dup") or {}).get("status") or {}
+                    return [e for e in st.get("errors") or [] if "node lock" in e]
+                await _until(lambda: bool(dup_error()), 20)
+                res["duplicate_policy_errors"] = dup_error()
+                res["duplicate_policy_status"] = (fake.get_object(P, "scale-out-dup") or {}).get("status")
+                res["first_policy_status_after_duplicate"] = (fake.get_object(P, name) or {}).get("status")
+                res["addrs_unchanged_by_duplicate"] = addrs_before == {
+                    nif: rt.addr_list(rt.link_by_name(nif)["index"]) for nif in nic_names}
+                res["label_after_duplicate"] = node.node_labels().get(label_key)
+                await c.delete(P, "scale-out-dup")
+                await _until(lambda: not any(x.daemonset == f"{ns}/scale-out-dup" for x in node.containers.values()), 10)
             if ha:
                 res.update(await _ha_checks(fake, c, rt, node, replicas, ns, name, mode, nic_names, label_key,
                                             all_good, update_mtu or 4200))
@@ -457,9 +492,7 @@ async def _scenario(tmp: Path, n_nics: int, mode: str, seed: int, interval: str,
                         await asyncio.sleep(0.0005)
                 sampler = asyncio.ensure_future(sample())
                 t1 = time.monotonic()
-                cur = await c.get(P, name)
-                cur["spec"]["amdScaleOut"]["mtu"] = update_mtu
-                await c.replace(P, cur)
+                await _edit(c, P, name, lambda cur: cur["spec"]["amdScaleOut"].update(mtu=update_mtu))
 
                 def mtu_applied():
                     return all(rt.link_by_name(nif)["mtu"] == update_mtu for nif in nic_names)
@@ -658,13 +691,14 @@ def run_scenario(n_nics: int = 2, mode: str = "L3", seed: int = 1, interval: str
                  teardown: bool = True, node_name: str = "mi355x-0", policy_kw: Optional[dict] = None,
                  update_mtu: int = 0, config_type: str = "amd-so", flap: bool = False, validation: str = "",
                  crash_agent: bool = False, driver_reload: bool = False, ha: bool = False,
-                 silent_nics: int = 0, lldp_wait: str = "", keep_tmp: bool = False) -> dict:
+                 silent_nics: int = 0, lldp_wait: str = "", keep_tmp: bool = False,
+                 duplicate_policy: bool = False) -> dict:
     """Must already run inside a private user+net namespace (``run_isolated``)."""
     tmp = Path(tempfile.mkdtemp(prefix="netop-e2e-"))
     try:
         return asyncio.run(_scenario(tmp, n_nics, mode, seed, interval, fast_start, teardown, node_name,
                                      dict(policy_kw or {}), update_mtu, config_type, flap, validation,
-                                     crash_agent, driver_reload, ha, silent_nics, lldp_wait))
+                                     crash_agent, driver_reload, ha, silent_nics, lldp_wait, duplicate_policy))
     finally:
         if not keep_tmp:
             shutil.rmtree(tmp, ignore_errors=True)

@@ -227,3 +227,15 @@ def test_two_operator_replicas_with_webhooks_fail_over():
     assert f["kill_to_mtu_applied_s"] is not None and f["kill_to_ready_again_s"] is not None, r["operator_logs"]
     assert f["admission_calls"] > r["admission_calls"]  # the edit went through the standby's webhook
     assert r["delete_to_label_removed_s"] is not None
+
+
+def test_second_policy_of_one_type_on_a_node_is_kept_off_the_nics():
+    """Two amd-so policies select one node.  The reference would run two agents flushing and
+    re-addressing the same NICs.  Here the second agent cannot take the node lock: it fails with
+    the cause, that policy's status says so, and the first policy's addresses and label stay."""
+    r = e2e.run_isolated(n_nics=2, mode="L3", seed=24, duplicate_policy=True)
+    assert r["duplicate_policy_errors"], (r.get("duplicate_policy_status"), r["agent_log"])
+    assert "holds the node lock" in r["duplicate_policy_errors"][0]
+    assert r["addrs_unchanged_by_duplicate"] and r["label_after_duplicate"] == "true"
+    st = r["first_policy_status_after_duplicate"]
+    assert (st["state"], st["errors"]) == ("All good", [])

@@ -71,6 +71,21 @@ async def cluster(openshift=True, workers=2, **fake_kw):
         await fake.stop()
 
 
+async def edit(client, name, change, attempts=20):
+    """kubectl edit: get, change, replace; a write of the operator's in between (status,
+    finalizer) is a conflict, and the edit is retried on the new object, as a client does."""
+    for _ in range(attempts):
+        cur = await client.get(kube.NETWORKCLUSTERPOLICIES, name)
+        change(cur)
+        try:
+            return await client.replace(kube.NETWORKCLUSTERPOLICIES, cur)
+        except ApiError as e:
+            if e.status != 409:
+                raise
+            await asyncio.sleep(0.01)
+    raise AssertionError(f"edit of {name} kept conflicting")
+
+
 def policy(name="policy", layer="L3", **so):
     p = T.new_policy(name, layer=layer, node_selector={"foo": "bar"}, **so)
     return p.to_dict()
@@ -110,9 +125,8 @@ def test_reconcile_lifecycle_reference_parity():
 
             # update to L2: the reference's 3 args (+ --v; controller_test.go:138-151), plus rccl.env:
             # on MI355X RCCL needs the scale-out HCAs and the link-local RoCE v2 GID in L2 too
-            cur = await client.get(kube.NETWORKCLUSTERPOLICIES, "policy")
-            cur["spec"]["amdScaleOut"] = {"layer": "L2", "image": "amd/my-linkdiscovery:latest"}
-            await client.replace(kube.NETWORKCLUSTERPOLICIES, cur)
+            await edit(client, "policy", lambda cur: cur["spec"].update(
+                amdScaleOut={"layer": "L2", "image": "amd/my-linkdiscovery:latest"}))
 
             def l2_ok():
                 ds = fake.get_object(kube.DAEMONSETS, "policy", NS)
@@ -124,10 +138,8 @@ def test_reconcile_lifecycle_reference_parity():
             await eventually(l2_ok)
 
             # L3 + disableNetworkManager + mtu 0: volumes in stable order (controller_test.go:153-180)
-            cur = await client.get(kube.NETWORKCLUSTERPOLICIES, "policy")
-            cur["spec"]["amdScaleOut"] = {"layer": "L3", "disableNetworkManager": True, "pullPolicy": "Always"}
-            cur["spec"]["logLevel"] = 4
-            await client.replace(kube.NETWORKCLUSTERPOLICIES, cur)
+            await edit(client, "policy", lambda cur: cur["spec"].update(
+                amdScaleOut={"layer": "L3", "disableNetworkManager": True, "pullPolicy": "Always"}, logLevel=4))
 
             def l3nm_ok():
                 ds = fake.get_object(kube.DAEMONSETS, "policy", NS)
@@ -541,9 +553,7 @@ def test_status_conditions_ready_degraded_and_observed_generation():
                 assert c["Ready"]["status"] == "True" and c["Ready"]["reason"] == "AllNodesReady"
                 assert c["Degraded"]["status"] == "False" and c["Degraded"]["reason"] == "AsExpected"
             await eventually(ready)
-            cur = await client.get(kube.NETWORKCLUSTERPOLICIES, "policy")
-            cur["spec"]["amdScaleOut"]["mtu"] = 4000
-            await client.replace(kube.NETWORKCLUSTERPOLICIES, cur)
+            await edit(client, "policy", lambda cur: cur["spec"]["amdScaleOut"].update(mtu=4000))
             await eventually(lambda: conds()[0]["observedGeneration"] == 2)
     run(body())
     # No targets; a missing dependency is reported as such.
@@ -629,9 +639,7 @@ def test_fabric_validation_jobs_follow_ready_nodes_and_report_a_condition():
 
             # A new spec (generation 2): the old results go, both nodes are validated again.
             old_names = {j["metadata"]["name"] for j in jobs().values()}
-            cur = await client.get(kube.NETWORKCLUSTERPOLICIES, "policy")
-            cur["spec"]["amdScaleOut"]["mtu"] = 4200
-            await client.replace(kube.NETWORKCLUSTERPOLICIES, cur)
+            await edit(client, "policy", lambda cur: cur["spec"]["amdScaleOut"].update(mtu=4200))
             await eventually(lambda: set(jobs()) == {"gpu-node-0", "gpu-node-1"}
                              and not old_names & {j["metadata"]["name"] for j in jobs().values()})
             for j in jobs().values():
@@ -641,9 +649,7 @@ def test_fabric_validation_jobs_follow_ready_nodes_and_report_a_condition():
             assert st["state"] == "All good" and st["errors"] == []
 
             # Validation off: no Jobs, no condition.
-            cur = await client.get(kube.NETWORKCLUSTERPOLICIES, "policy")
-            cur["spec"]["amdScaleOut"]["validation"] = {"enabled": False}
-            await client.replace(kube.NETWORKCLUSTERPOLICIES, cur)
+            await edit(client, "policy", lambda cur: cur["spec"]["amdScaleOut"].update(validation={"enabled": False}))
             await eventually(lambda: cond() is None and not fake.list_objects(kube.JOBS))
     run(body())
 
