@@ -62,6 +62,7 @@ class PolicyController:
             list_pods=lambda ds: self.pods.by_index(OWNER_KEY, ds),
             list_jobs=lambda name: self.jobs.by_index(OWNER_KEY, name),
             list_job_pods=lambda job: self.job_pods.by_index(OWNER_KEY, job))
+        self.reconciler.on_cleanup = lambda policy, outcome: self.metrics.node_cleanups.labels(policy, outcome).inc()
         self.policies.add_handler(self._on_policy)
         self.daemonsets.add_handler(self._on_daemonset)
         self.pods.add_handler(self._on_pod)
@@ -164,7 +165,7 @@ class PolicyController:
     def _export_policy(self, name: str) -> None:
         p = self.policies.get(name)
         if p is None:
-            for g in (self.metrics.policy_targets, self.metrics.policy_ready):
+            for g in (self.metrics.policy_targets, self.metrics.policy_ready, self.metrics.nodes_owing_cleanup):
                 try:
                     g.remove(name)
                 except KeyError:
@@ -173,6 +174,7 @@ class PolicyController:
         st = p.get("status") or {}
         self.metrics.policy_targets.labels(name).set(st.get("targets", 0) or 0)
         self.metrics.policy_ready.labels(name).set(st.get("ready", 0) or 0)
+        self.metrics.nodes_owing_cleanup.labels(name).set(len(st.get("keptNodes") or []))
 
     async def start(self) -> None:
         self._tasks.append(self.policies.start())

@@ -43,6 +43,13 @@ class OperatorMetrics:
         self.agent_unready = Counter("amd_network_operator_agent_unready_total",
                                      "Agent Pods that went from Ready to not Ready (link loss, lost peer, ...)",
                                      ["policy"], registry=r)
+        # keepConfigOnRestart / disableNetworkManager: nodes owing a cleanup and how cleanups ended.
+        self.nodes_owing_cleanup = Gauge("amd_network_operator_nodes_owing_cleanup",
+                                         "Nodes whose agents left configuration a cleanup Job still has to remove",
+                                         ["policy"], registry=r)
+        self.node_cleanups = Counter("amd_network_operator_node_cleanups_total",
+                                     "Node cleanup Jobs that ended, by outcome (succeeded, failed, timed_out)",
+                                     ["policy", "outcome"], registry=r)
         self.seed_in_sync = Gauge("amd_network_operator_policies_file_in_sync",
                                   "1 when the policies of --policies-file (the Helm release's) match the cluster",
                                   registry=r)

@@ -619,6 +619,7 @@ class NetworkClusterPolicyReconciler:
         self.recorder = recorder
         # keepConfigOnRestart: (policy, node) -> when the node's agent Pod was first seen missing
         self._missing_since: dict = {}
+        self.on_cleanup: Optional[Callable[[str, str], None]] = None  # (policy, outcome): metrics
 
     def _node_errors(self, ds_name: str, limit: int = 16) -> List[str]:
         """Per-node agent problems from the agent Pods' Ready condition (the reference indexes
@@ -678,6 +679,8 @@ class NetworkClusterPolicyReconciler:
             if outcome == "running" and now - created < CLEANUP_TIMEOUT_S:
                 pending.append(node)
                 continue
+            if self.on_cleanup is not None:
+                self.on_cleanup(p.name, "timed_out" if outcome == "running" else outcome)
             if outcome == "succeeded":
                 log.info("Node %s cleaned up (Job %s)", node, j["metadata"]["name"])
             else:

@@ -793,6 +793,8 @@ def test_keep_config_policy_cleans_nodes_through_jobs_on_deletion_and_departure(
             await eventually(lambda: pol()["status"].get("keptNodes") == [f"gpu-node-{i}" for i in range(3)])
             assert pol()["metadata"]["finalizers"] == [R.FINALIZER]
             assert not pol("plain")["metadata"].get("finalizers") and "keptNodes" not in pol("plain")["status"]
+            await eventually(lambda: ctl.metrics.registry.get_sample_value(
+                "amd_network_operator_nodes_owing_cleanup", {"policy": "policy"}) == 3)
 
             # gpu-node-2 leaves the policy: its agent Pod goes; after the grace period, a cleanup Job
             fake.set_node_labels("gpu-node-2", {"foo": "other"})
@@ -820,6 +822,11 @@ def test_keep_config_policy_cleans_nodes_through_jobs_on_deletion_and_departure(
             await eventually(lambda: pol() is None)
             ev = [e for e in fake.list_objects(kube.EVENTS) if e["reason"] == "NodeCleanupFailed"]
             assert len(ev) == 1 and ev[0]["message"].startswith("gpu-node-1: cleanup Job")
+            reg = ctl.metrics.registry
+            assert reg.get_sample_value("amd_network_operator_node_cleanups_total",
+                                        {"policy": "policy", "outcome": "succeeded"}) == 2
+            assert reg.get_sample_value("amd_network_operator_node_cleanups_total",
+                                        {"policy": "policy", "outcome": "failed"}) == 1
             assert pol("plain") is not None
             await client.delete(kube.NETWORKCLUSTERPOLICIES, "plain")  # no finalizer: gone at once
             assert pol("plain") is None
