@@ -148,6 +148,8 @@ def openapi_schema() -> dict:
             "verifyPeers": {"description": "L3: label only once every NIC's switch-side /30 address answers ARP.",
                             "type": "boolean"},
             "lldpWait": LLDP_WAIT_SCHEMA,
+            "keepConfigOnRestart": {"description": "As amdScaleOut.keepConfigOnRestart, for the host NICs.",
+                                    "type": "boolean"},
         },
         "required": ["layer"],
     }

@@ -213,6 +213,7 @@ class HostNicSpec:
     driverImage: str = ""
     verifyPeers: bool = False
     lldpWait: str = ""
+    keepConfigOnRestart: bool = False
     extra: Dict[str, Any] = field(default_factory=dict)
 
     def to_dict(self) -> dict:
@@ -230,6 +231,8 @@ class HostNicSpec:
             d["nicDrivers"] = list(self.nicDrivers)
         if self.verifyPeers:
             d["verifyPeers"] = True
+        if self.keepConfigOnRestart:
+            d["keepConfigOnRestart"] = True
         d.update(copy.deepcopy(self.extra))
         return d
 
@@ -240,7 +243,8 @@ class HostNicSpec:
                 pullPolicy=d.pop("pullPolicy", "") or "", disableNetworkManager=bool(d.pop("disableNetworkManager", False)),
                 interfaces=list(d.pop("interfaces", []) or []), nicDrivers=list(d.pop("nicDrivers", []) or []),
                 driverImage=d.pop("driverImage", "") or "", verifyPeers=bool(d.pop("verifyPeers", False)),
-                lldpWait=d.pop("lldpWait", "") or "")
+                lldpWait=d.pop("lldpWait", "") or "",
+                keepConfigOnRestart=bool(d.pop("keepConfigOnRestart", False)))
         s.extra = d
         return s
 

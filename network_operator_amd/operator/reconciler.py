@@ -237,6 +237,7 @@ def update_amd_scale_out_daemonset(ds: dict, p: T.NetworkClusterPolicy, namespac
 
 HOST_NIC_LABEL = "amd.feature.node.kubernetes.io/host-nic-ready"
 HOST_NIC_LABEL_FILE = "host-nic-readiness.txt"
+HOST_NIC_LLDP_CACHE_FILE = "host-nic-lldp-cache"
 DRIVER_CONTAINER = "nic-driver"
 
 
@@ -261,6 +262,10 @@ def host_nic_agent_args(p: T.NetworkClusterPolicy) -> List[str]:
         args.append("--interfaces=" + ",".join(hn.interfaces))
     if hn.nicDrivers:
         args.append("--nic-drivers=" + ",".join(hn.nicDrivers))
+    if hn.keepConfigOnRestart:
+        if hn.layer == "L3":  # its own cache beside the scale-out agent's
+            args.append(f"--lldp-cache={ARTIFACT_DIR_CONTAINER}/{HOST_NIC_LLDP_CACHE_FILE}")
+        args.append("--keep-config")
     return args
 
 
@@ -283,6 +288,9 @@ def update_host_nic_daemonset(ds: dict, p: T.NetworkClusterPolicy, namespace: st
         add_host_volume(ds, "var-run-dbus", "/var/run/dbus", "/var/run/dbus")
         add_host_volume(ds, "networkmanager", "/etc/NetworkManager", "/etc/NetworkManager")
         wanted |= {"var-run-dbus", "networkmanager"}
+    if hn.keepConfigOnRestart and hn.layer == "L3":  # the LLDP cache outlives the Pod
+        add_host_volume(ds, "rccl-artifacts", ARTIFACT_DIR_HOST, ARTIFACT_DIR_CONTAINER)
+        wanted.add("rccl-artifacts")
     # Optional kernel-driver container: privileged, sees the host's modules, runs to completion
     # before the agent starts (init container), so the NICs exist when discovery runs.
     inits = [x for x in pod.get("initContainers", []) if x.get("name") != DRIVER_CONTAINER]
@@ -444,7 +452,9 @@ CLEANUP_POLL_S = 2.0       # cleanup Jobs are not watched: poll while some are r
 
 
 def keeps_config(p: T.NetworkClusterPolicy) -> bool:
-    return p.spec.configurationType == T.CONFIG_AMD_SCALE_OUT and p.spec.amdScaleOut.keepConfigOnRestart
+    if p.spec.configurationType == T.CONFIG_AMD_SCALE_OUT:
+        return p.spec.amdScaleOut.keepConfigOnRestart
+    return p.spec.configurationType == T.CONFIG_HOST_NIC and bool(p.spec.hostNic and p.spec.hostNic.keepConfigOnRestart)
 
 
 def disables_nm(p: T.NetworkClusterPolicy) -> bool:

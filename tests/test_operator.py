@@ -862,3 +862,22 @@ def test_network_manager_is_handed_back_when_the_policy_goes():
                 fake.set_job_result(job["metadata"]["name"], NS, True)
                 await eventually(lambda: fake.get_object(kube.NETWORKCLUSTERPOLICIES, name) is None)
     run(body())
+
+
+def test_host_nic_keep_config_args_volume_and_cleanup():
+    from network_operator_amd.operator import reconciler as R
+
+    p = T.new_host_nic_policy("hosts", layer="L3", keepConfigOnRestart=True, nicDrivers=["mlx5_core"])
+    args = R.host_nic_agent_args(p)
+    assert args[-2:] == ["--lldp-cache=/host/etc/amd/scale-out/host-nic-lldp-cache", "--keep-config"]
+    assert R.keeps_config(p) and R.needs_node_cleanup(p)
+    job = R.cleanup_job(p, "n0", NS)
+    spec = job["spec"]["template"]["spec"]
+    c = spec["containers"][0]
+    assert "--cleanup" in c["args"] and "--keep-config" not in c["args"] and "--nm-restore" not in c["args"]
+    assert "--nfd-label-file=host-nic-readiness.txt" in c["args"]  # its own lock, label and keyfile
+    assert "rccl-artifacts" in [v["name"] for v in spec["volumes"]]
+    l2 = T.new_host_nic_policy("hosts", layer="L2", keepConfigOnRestart=True)
+    assert R.host_nic_agent_args(l2)[-1] == "--keep-config" and not any("lldp-cache" in a for a in R.host_nic_agent_args(l2))
+    plain = T.new_host_nic_policy("hosts", layer="L3")
+    assert not R.needs_node_cleanup(plain) and "--keep-config" not in R.host_nic_agent_args(plain)
