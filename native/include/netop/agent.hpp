@@ -233,7 +233,7 @@ class Agent {
     void get_network_configs(const std::vector<std::string>& names);
     void detect_lldp(int stop_fd);
     void diagnose_silent();            // after --wait expired: why each silent NIC heard nothing
-    std::string silent_summary() const;  // "" or "LLDP silent on k NIC(s): ..." for the exit error
+    std::string silent_summary() const;  // "" or "LLDP silent on k NIC(s): ... Not configured: ..." for the exit error
     void on_lldp(NicState& n, const lldp::Frame& f);
     void add_route(NicState& n, int mask);
     uint32_t rail_table(const NicState& n) const;

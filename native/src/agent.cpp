@@ -562,6 +562,19 @@ void Agent::remove_rail_routing() {
 
 bool Agent::configure_interface(NicState& n) {
     if (!n.addr || n.configured) return n.configured;
+    // Two switch ports describing the same /30 (a copy-pasted port description, two cables on
+    // one link): the kernel would take the address twice and ARP and routing would pick either
+    // NIC.  The first NIC keeps it; this one stays unconfigured, and the error says why.
+    const Ipv4Prefix net = n.addr->local_prefix().masked();
+    for (const auto& m : nics_) {
+        if (&m == &n || !m.addr || !(m.addr->local_prefix().masked() == net)) continue;
+        if (!m.configured && &m > &n) continue;  // neither configured yet: the earlier NIC wins
+        n.config_error = strfmt("its switch port describes %s, the link of %s too (two ports, one /30: check the "
+                                "switch's Port Descriptions and the cabling)",
+                                n.addr->local_prefix().str().c_str(), m.ifname.c_str());
+        NLOG_W("Interface '%s' not configured: %s", n.ifname.c_str(), n.config_error.c_str());
+        return false;
+    }
     std::vector<nl::AddrInfo> addrs;
     try {
         addrs = ops_.addr_list(n.link.index, AF_INET);
@@ -915,11 +928,14 @@ void Agent::diagnose_silent() {
 }
 
 std::string Agent::silent_summary() const {
-    std::vector<std::string> parts;
-    for (const auto& n : nics_)
+    std::vector<std::string> parts, failed;
+    for (const auto& n : nics_) {
         if (!n.lldp_silent.empty()) parts.push_back(n.ifname + " (" + n.lldp_silent + ")");
-    if (parts.empty()) return "";
-    return strfmt("LLDP silent on %zu NIC(s): ", parts.size()) + join(parts, "; ");
+        if (n.addr && !n.configured && !n.config_error.empty()) failed.push_back(n.ifname + ": " + n.config_error);
+    }
+    std::string out = parts.empty() ? "" : strfmt("LLDP silent on %zu NIC(s): ", parts.size()) + join(parts, "; ");
+    if (!failed.empty()) out += (out.empty() ? "" : " ") + strfmt("Not configured: %s", join(failed, "; ").c_str());
+    return out;
 }
 
 void Agent::write_l2_artifacts() {

@@ -1671,3 +1671,34 @@ TEST(agent_node_lock_keeps_two_agents_of_one_kind_apart) {
     c.run(-1);
     CHECK(mono_ns() - t1 < 140000000LL);
 }
+
+TEST(agent_two_ports_describing_one_link_are_refused_and_named) {
+    // ens2's switch port carries ens0's Port Description (copy-paste on the switch): ens0 keeps
+    // the /30, ens2 is not configured, and the exit error says which NIC and why.
+    for (bool pipeline : {true, false}) {
+        Fixture f;
+        f.cfg.keep_running = false;
+        f.cfg.pipeline = pipeline;
+        auto src = f.all_valid();
+        src->frames["ens2"] = sw("02:aa:00:00:00:02", "no-alert 10.200.0.2/30");
+        agent::Agent a(f.cfg, f.ops, std::move(src), f.nm());
+        std::string err;
+        try {
+            a.run(-1);
+        } catch (const agent::AgentError& e) {
+            err = e.what();
+        }
+        CHECK(err.find("Not all interfaces were configured (2/3).") != std::string::npos);
+        CHECK(err.find("Not configured: ens2: its switch port describes 10.200.0.1/30, the link of ens0 too") !=
+              std::string::npos);
+        int on_ens0 = 0, on_ens2 = 0;
+        for (auto& x : f.ops.addrs) {
+            on_ens0 += x.ifindex == 10;
+            on_ens2 += x.ifindex == 12;
+        }
+        CHECK_EQ(on_ens0, 1);
+        CHECK_EQ(on_ens2, 0);
+        auto st = read_file(f.cfg.status_file);
+        CHECK(st && st->find("the link of ens0 too") != std::string::npos);
+    }
+}
