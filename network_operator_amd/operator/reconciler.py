@@ -702,18 +702,16 @@ class NetworkClusterPolicyReconciler:
         return pending
 
     async def _kept_nodes(self, raw: dict, p: T.NetworkClusterPolicy, ds: dict) -> tuple:
-        """keepConfigOnRestart bookkeeping: (status.keptNodes, requeue_after).  A node joins when
-        its agent is Ready; it leaves after its cleanup Job, which runs once its agent Pod has been
-        gone for KEPT_ORPHAN_GRACE_S."""
+        """keepConfigOnRestart / disableNetworkManager bookkeeping: (status.keptNodes,
+        requeue_after).  A node joins when an agent Pod runs there (ready or not: an agent that
+        failed half-way may have configured some NICs); it leaves after its cleanup Job, which runs
+        once its agent Pod has been gone for KEPT_ORPHAN_GRACE_S."""
         cur = list(p.status.keptNodes)
         if not needs_node_cleanup(p) and not cur:
             return [], 0.0
         pods = self._list_pods(ds["metadata"]["name"]) if self._list_pods is not None else []
         with_pod = {pod.get("spec", {}).get("nodeName", "") for pod in pods}
-        ready = {pod.get("spec", {}).get("nodeName", "") for pod in pods
-                 if any(c.get("type") == "Ready" and c.get("status") == "True"
-                        for c in (pod.get("status") or {}).get("conditions") or [])}
-        kept = set(cur) | ((ready - {""}) if needs_node_cleanup(p) else set())
+        kept = set(cur) | ((with_pod - {""}) if needs_node_cleanup(p) else set())
         now = self._clock()
         due, requeue_after = [], 0.0
         for node in sorted(kept):
@@ -742,7 +740,25 @@ class NetworkClusterPolicyReconciler:
         fins = list(raw["metadata"].get("finalizers") or [])
         if FINALIZER not in fins:
             return Result()
-        for ds in self._list_owned(p.name):
+        owned = self._list_owned(p.name)
+        if owned and self._list_pods is not None:
+            # Every node with an agent Pod now owes a cleanup, whether or not the status has
+            # recorded it yet: record them before the Pods (the only other trace) go.
+            nodes = {pod.get("spec", {}).get("nodeName", "") for pod in self._list_pods(owned[0]["metadata"]["name"])}
+            kept = sorted((nodes - {""}) | set(p.status.keptNodes))
+            if kept != sorted(p.status.keptNodes):
+                body = copy.deepcopy(raw)
+                body["status"] = dict(raw.get("status") or {}, keptNodes=kept)
+                try:
+                    await self.client.replace_status(kube.NETWORKCLUSTERPOLICIES, body)
+                except ApiError as e:
+                    if is_conflict(e):
+                        return Result(requeue=True)
+                    if is_not_found(e):
+                        return Result()
+                    raise
+                return Result(requeue=True)  # continue from the stored status
+        for ds in owned:
             try:
                 await self.client.delete(kube.DAEMONSETS, ds["metadata"]["name"], self.namespace)
                 log.info("Policy %s is being deleted: removed DaemonSet %s", p.name, ds["metadata"]["name"])

@@ -881,3 +881,45 @@ def test_host_nic_keep_config_args_volume_and_cleanup():
     assert R.host_nic_agent_args(l2)[-1] == "--keep-config" and not any("lldp-cache" in a for a in R.host_nic_agent_args(l2))
     plain = T.new_host_nic_policy("hosts", layer="L3")
     assert not R.needs_node_cleanup(plain) and "--keep-config" not in R.host_nic_agent_args(plain)
+
+
+def test_deleted_before_the_status_recorded_its_nodes_still_cleans_them():
+    """A keepConfigOnRestart policy deleted before any status write listed its nodes: the
+    finalizer first records every node with an agent Pod (ready or not), then removes the
+    DaemonSet, so the cleanup Jobs cover nodes the status never mentioned."""
+    from network_operator_amd.operator import reconciler as R
+
+    async def body():
+        fake = FakeApiServer()
+        url = await fake.start()
+        try:
+            for i in range(2):
+                fake.add_node(f"gpu-node-{i}", {"foo": "bar"})
+            async with ApiClient(KubeConfig(host=url)) as client:
+                pol = policy(keepConfigOnRestart=True)
+                pol["metadata"]["finalizers"] = [R.FINALIZER]
+                raw = await client.create(kube.NETWORKCLUSTERPOLICIES, pol)
+                ds = R.discovery.discovery_daemonset()
+                R.update_daemonset_for(ds, T.NetworkClusterPolicy.from_dict(raw), NS)
+                R.set_controller_reference(raw, ds)
+                await client.create(kube.DAEMONSETS, ds, namespace=NS)
+                pods = lambda name: [p for p in fake.list_objects(kube.PODS)  # noqa: E731
+                                     if p["metadata"]["name"].startswith(name + "-")]
+                assert len(pods("policy")) == 2  # not ready, status empty
+                rec = R.NetworkClusterPolicyReconciler(
+                    client, NS, False, get_policy=lambda n: fake.get_object(kube.NETWORKCLUSTERPOLICIES, n),
+                    list_owned=lambda n: [d for d in [fake.get_object(kube.DAEMONSETS, n, NS)] if d],
+                    list_pods=pods)
+                await client.delete(kube.NETWORKCLUSTERPOLICIES, "policy")
+                for _ in range(10):
+                    await rec.reconcile("policy")
+                    if fake.list_objects(kube.JOBS):
+                        break
+                assert fake.get_object(kube.NETWORKCLUSTERPOLICIES, "policy")["status"]["keptNodes"] == [
+                    "gpu-node-0", "gpu-node-1"]
+                assert fake.get_object(kube.DAEMONSETS, "policy", NS) is None
+                assert sorted(j["spec"]["template"]["spec"]["nodeName"] for j in fake.list_objects(kube.JOBS)) == [
+                    "gpu-node-0", "gpu-node-1"]
+        finally:
+            await fake.stop()
+    run(body())
