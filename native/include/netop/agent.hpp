@@ -141,6 +141,11 @@ struct Config {
     // process dies, SIGKILL included.  "" = off (discover's --node-lock defaults it from the
     // label file, so an amd-so and a host-nic agent never wait for each other).
     std::string node_lock;
+    // Rail cabling check (L3): the NIC of GPU k must be cabled to a switch whose LLDP System Name
+    // matches this ECMAScript regex with "{rail}" replaced by k (e.g. "leaf-r{rail}-.*" for a
+    // rail-optimized fabric).  A NIC on the wrong leaf still works but crosses the spine, so a
+    // mismatch leaves it unconfigured and is named in the error.  "" = off.
+    std::string rail_switch_pattern;
     int64_t node_lock_wait_ns = 60LL * 1000000000;
 };
 

@@ -17,6 +17,7 @@
 #include <sched.h>
 #include <sys/syscall.h>
 #include <mutex>
+#include <regex>
 #include <set>
 #include <system_error>
 
@@ -574,6 +575,23 @@ bool Agent::configure_interface(NicState& n) {
                                 n.addr->local_prefix().str().c_str(), m.ifname.c_str());
         NLOG_W("Interface '%s' not configured: %s", n.ifname.c_str(), n.config_error.c_str());
         return false;
+    }
+    if (!cfg_.rail_switch_pattern.empty() && n.gpu_index >= 0) {
+        std::string want = cfg_.rail_switch_pattern;
+        for (size_t at; (at = want.find("{rail}")) != std::string::npos;) want.replace(at, 6, std::to_string(n.gpu_index));
+        bool ok = false;
+        try {
+            ok = std::regex_match(n.peer_system_name, std::regex(want, std::regex::ECMAScript));
+        } catch (const std::regex_error& e) {
+            throw AgentError("Invalid --rail-switch-pattern '" + cfg_.rail_switch_pattern + "': " + e.what());
+        }
+        if (!ok) {
+            n.config_error = strfmt("rail %d is cabled to switch '%s' port '%s', not to one matching '%s' (a NIC on "
+                                    "another rail's leaf crosses the spine: check the cabling)",
+                                    n.gpu_index, n.peer_system_name.c_str(), n.peer_port_id.c_str(), want.c_str());
+            NLOG_W("Interface '%s' not configured: %s", n.ifname.c_str(), n.config_error.c_str());
+            return false;
+        }
     }
     std::vector<nl::AddrInfo> addrs;
     try {
@@ -1342,6 +1360,15 @@ void Agent::run(int stop_fd) {
         rccl_env_extra_ = artifacts::parse_env_extra(cfg_.rccl_env_extra);
     } catch (const std::exception& e) {
         throw AgentError(std::string("Invalid --rccl-env-extra: ") + e.what());
+    }
+    if (!cfg_.rail_switch_pattern.empty()) {
+        try {
+            std::string probe = cfg_.rail_switch_pattern;
+            for (size_t at; (at = probe.find("{rail}")) != std::string::npos;) probe.replace(at, 6, "0");
+            std::regex(probe, std::regex::ECMAScript);
+        } catch (const std::regex_error& e) {
+            throw AgentError("Invalid --rail-switch-pattern '" + cfg_.rail_switch_pattern + "': " + e.what());
+        }
     }
     if (!cfg_.metrics_addr.empty() && !httpd_) {
         try {

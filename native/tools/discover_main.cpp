@@ -80,6 +80,7 @@ int main(int argc, char** argv) {
     std::string node_lock = "auto";
     fs.add_string("node-lock", &node_lock, "node-wide lock (abstract unix socket) held while the agent runs, so agents configuring the same NICs never overlap (exiting vs starting agent, agent vs --cleanup, two policies on one node): auto (named after --nfd-label-file), none, or a name");
     fs.add_duration("node-lock-wait", &cfg.node_lock_wait_ns, "how long to wait for the node lock before failing");
+    fs.add_string("rail-switch-pattern", &cfg.rail_switch_pattern, "L3 rail cabling check: the NIC of GPU k must reach a switch whose LLDP System Name matches this ECMAScript regex with {rail} = k (e.g. 'leaf-r{rail}-.*'); a mismatch leaves the NIC unconfigured");
     fs.add_bool("dry-run", &cfg.dry_run, "discover, check xGMI / GPUDirect RDMA and write the topology file and status only: no link, address, NetworkManager or label change, no LLDP (needs no privileges)");
     fs.add_string("lldp-cache", &cfg.lldp_cache, "with --keep-running: remember each NIC's confirmed Port Description in this file and configure from it at start (the switch must confirm it within --lldp-cache-confirm)");
     fs.add_duration("lldp-cache-max-age", &cfg.lldp_cache_max_age_ns, "ignore LLDP cache entries older than this");

@@ -12,6 +12,10 @@
 //   * --assign-ip puts the peer address of the Port Description on the switch port so the
 //     node's /30 is actually reachable.
 //
+//   * --system-name may contain "{port}" (the port's position in the --port list), so one
+//     process can play one leaf switch per rail; --port-system-name IFNAME=NAME overrides one
+//     port's (a miscabled NIC in the rail-check tests).
+//
 //   netop-lldp-tx --port sw0='no-alert 10.200.0.2/30' --port sw1=... [--interval 30s]
 //                 [--phase random|zero] [--fast-start] [--count N] [--assign-ip] [--seed S]
 #include <signal.h>
@@ -19,6 +23,7 @@
 #include <unistd.h>
 
 #include <cstdio>
+#include <map>
 #include <random>
 #include <set>
 
@@ -53,7 +58,13 @@ int main(int argc, char** argv) {
     fs.add_duration("fast-interval", &fast_interval, "msgFastTx");
     fs.add_int("tx-fast-init", &tx_fast_init, "txFastInit");
     fs.add_int("count", &count, "periodic frames per port before exiting (0 = until SIGTERM)");
-    fs.add_string("system-name", &sysname, "System Name TLV");
+    fs.add_string("system-name", &sysname, "System Name TLV (\"{port}\" = the port's index)");
+    std::map<std::string, std::string> port_sysname;
+    fs.add_func("port-system-name", true, [&](const std::string& v) {
+        auto eq = v.find('=');
+        if (eq == std::string::npos) throw std::invalid_argument("--port-system-name wants IFNAME=NAME");
+        port_sysname[v.substr(0, eq)] = v.substr(eq + 1);
+    }, "IFNAME=NAME: this port's System Name (repeatable)");
     fs.add_int("ttl", &ttl, "TTL TLV");
     fs.add_bool("assign-ip", &assign_ip, "assign the Port Description address to the switch port");
     fs.add_int("seed", &seed, "RNG seed for the random phase (0 = time based)");
@@ -99,7 +110,15 @@ int main(int argc, char** argv) {
             }
         }
         p.sock = std::make_unique<pkt::LldpSocket>(ifname, link.index, link.mac, false);
-        p.frame = lldp::encode(lldp::make_switch_frame(link.mac, sysname, ifname, desc, uint16_t(ttl)));
+        std::string name = sysname;
+        if (auto it = port_sysname.find(ifname); it != port_sysname.end()) {
+            name = it->second;
+        } else if (auto at = name.find("{port}"); at != std::string::npos) {
+            size_t idx = 0;
+            while (idx < ports.size() && ports[idx].first != ifname) ++idx;
+            name.replace(at, 6, std::to_string(idx));
+        }
+        p.frame = lldp::encode(lldp::make_switch_frame(link.mac, name, ifname, desc, uint16_t(ttl)));
         p.neighbours.clear();
     };
     try {

@@ -122,6 +122,12 @@ def openapi_schema() -> dict:
                                "configuration with a cleanup Job per node when the policy is deleted or a\n"
                                "node leaves it (finalizer amd.com/node-cleanup).",
                 "type": "boolean"},
+            "railSwitchPattern": {
+                "description": "L3 rail cabling check: the NIC of GPU k must be cabled to a switch whose LLDP System\n"
+                               "Name matches this regular expression with {rail} replaced by k, e.g.\n"
+                               "'leaf-r{rail}-.*' on a rail-optimized fabric.  A NIC on another rail's leaf is\n"
+                               "left unconfigured and named in status.errors.",
+                "maxLength": 253, "type": "string"},
         },
     }
     host_nic = {

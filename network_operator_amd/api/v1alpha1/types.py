@@ -114,6 +114,8 @@ class AmdScaleOutSpec:
     # Hitless agent restarts: addresses / routes stay when an agent exits; the operator cleans the
     # nodes up (cleanup Jobs) when the policy is deleted or a node leaves it.
     keepConfigOnRestart: bool = False
+    # L3 rail cabling check: regex over the LLDP System Name, "{rail}" = GPU index ("" = off)
+    railSwitchPattern: str = ""
     validation: Optional[ValidationSpec] = None
     extra: Dict[str, Any] = field(default_factory=dict)
 
@@ -124,7 +126,7 @@ class AmdScaleOutSpec:
     _FIELDS = ("disableNetworkManager", "layer", "image", "pullPolicy", "mtu", "xgmiCheck", "lldpAnnounce",
                "interfaces", "nicDrivers", "disableFirmwareLldp", "metricsPort", "gpuDirectRdma", "rcclEnv",
                "railTableBase", "rcclSocketIfname", "lldpCache", "verifyPeers", "lldpWait", "keepConfigOnRestart",
-               "validation")
+               "railSwitchPattern", "validation")
 
     def to_dict(self) -> dict:
         d: dict = {}
@@ -164,6 +166,8 @@ class AmdScaleOutSpec:
             d["lldpWait"] = self.lldpWait
         if self.keepConfigOnRestart:
             d["keepConfigOnRestart"] = True
+        if self.railSwitchPattern:
+            d["railSwitchPattern"] = self.railSwitchPattern
         if self.validation is not None:
             d["validation"] = self.validation.to_dict()
         d.update(copy.deepcopy(self.extra))
@@ -190,6 +194,7 @@ class AmdScaleOutSpec:
             rcclSocketIfname=d.pop("rcclSocketIfname", "") or "",
             lldpCache=bool(d.pop("lldpCache", False)),
             keepConfigOnRestart=bool(d.pop("keepConfigOnRestart", False)),
+            railSwitchPattern=d.pop("railSwitchPattern", "") or "",
             verifyPeers=bool(d.pop("verifyPeers", False)),
             lldpWait=d.pop("lldpWait", "") or "",
             validation=ValidationSpec.from_dict(d.pop("validation", None)),

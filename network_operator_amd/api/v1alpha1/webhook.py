@@ -108,6 +108,28 @@ class InvalidLldpWaitError(ValidationError):
                         f"{int(T.LLDP_WAIT_MIN_S)}s and {int(T.LLDP_WAIT_MAX_S // 60)}m")
 
 
+class InvalidRailSwitchPatternError(ValidationError):
+    def __init__(self, value: str, why: str):
+        super().__init__()
+        self.message = f"invalid railSwitchPattern {value!r}: {why}"
+
+
+def validate_rail_switch_pattern(value: str) -> None:
+    """A regular expression over the switch's LLDP System Name, "{rail}" standing for the GPU
+    index.  The agent matches with ECMAScript std::regex; Python's re accepts the same common
+    subset, so a pattern Python rejects is refused here rather than crash-looping the agents."""
+    import re
+
+    if not value:
+        return
+    if len(value) > 253 or any(c in value for c in "\n\r"):
+        raise InvalidRailSwitchPatternError(value, "at most 253 characters on one line")
+    try:
+        re.compile(value.replace("{rail}", "0"))
+    except re.error as e:
+        raise InvalidRailSwitchPatternError(value, str(e)) from None
+
+
 def validate_lldp_wait(value: str) -> None:
     if not value:
         return
@@ -133,6 +155,9 @@ def validate_amd_so_spec(s: T.AmdScaleOutSpec) -> List[str]:
     validate_lldp_wait(s.lldpWait)
     if s.lldpWait and s.layer == "L2":
         warnings.append("lldpWait has no effect in L2 mode")
+    validate_rail_switch_pattern(s.railSwitchPattern)
+    if s.railSwitchPattern and s.layer == "L2":
+        warnings.append("railSwitchPattern has no effect in L2 mode (no LLDP)")
     return warnings
 
 

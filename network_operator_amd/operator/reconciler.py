@@ -181,6 +181,8 @@ def agent_args(p: T.NetworkClusterPolicy) -> List[str]:
         args.append(f"--lldp-cache={ARTIFACT_DIR_CONTAINER}/{LLDP_CACHE_FILE}")
     if so.keepConfigOnRestart:
         args.append("--keep-config")
+    if so.railSwitchPattern and so.layer == "L3":
+        args.append(f"--rail-switch-pattern={so.railSwitchPattern}")
     if so.verifyPeers and so.layer == "L3":
         args.append(f"--verify-peers={VERIFY_PEERS_TIMEOUT}")
     if so.rcclEnv:

@@ -209,7 +209,8 @@ class SyntheticSwitch:
     `plan`.  The last `silent_nics` ports send no LLDP."""
 
     def __init__(self, nic_names: list, plan: list, rng: random.Random, interval: str = "30s", phase: str = "random",
-                 fast_start: bool = True, silent_nics: int = 0, remote: Optional[list] = None, forward: bool = False):
+                 fast_start: bool = True, silent_nics: int = 0, remote: Optional[list] = None, forward: bool = False,
+                 system_name: str = "", port_system_names: Optional[dict] = None):
         """`remote`: (network-namespace pid, ifname) of NICs of other nodes, wired to the ports after
         this namespace's `nic_names` (`plan` covers both).  `forward`: the switch routes between its
         /30s (a leaf of an L3 fabric), so nodes reach each other over their /16 routes."""
@@ -223,6 +224,10 @@ class SyntheticSwitch:
                      f"--seed={rng.randrange(1, 1 << 30)}"]
         if fast_start:
             self.args.append("--fast-start")
+        if system_name:  # "{port}": one leaf per rail
+            self.args.append(f"--system-name={system_name}")
+        for sp, name in (port_system_names or {}).items():
+            self.args.append(f"--port-system-name={sp}={name}")
         for i, (sp, p) in enumerate(zip(self.ports, plan)):
             if i >= len(plan) - silent_nics:
                 continue  # switch port that never sends LLDP
@@ -306,7 +311,8 @@ def run_scenario(n_nics: int = 8, mode: str = "L3", seed: int | None = None, int
                  drop_xgmi: list | None = None, extra_args: list | None = None, flap_port: int | None = None,
                  crash_restart: bool = False, crash_after_s: float = 0.0, gid_delay_s: float = 0.0,
                  egress_probe: bool = False, nm_bus: bool = False, nm_restore: bool = True, lldp_cache: bool = False,
-                 soak_cycles: int = 0, arp_silent_ports: int = 0) -> dict:
+                 soak_cycles: int = 0, arp_silent_ports: int = 0, switch_name: str = "",
+                 port_switch_names: dict | None = None) -> dict:
     """Runs one node bring-up.  Must already be inside a private user+net namespace.
 
     nm_bus: run the agent with --disable-networkmanager against a real ``dbus-daemon`` on which a
@@ -355,7 +361,7 @@ def run_scenario(n_nics: int = 8, mode: str = "L3", seed: int | None = None, int
             add_gids()
 
         sw = SyntheticSwitch(nic_names, plan, rng, interval=interval, phase=phase, fast_start=fast_start,
-                             silent_nics=silent_nics)
+                             silent_nics=silent_nics, system_name=switch_name, port_system_names=port_switch_names)
         t_switch = sw.start(rt)
         pid, sw_ports, first_periodic = sw.pid, sw.ports, sw.first_periodic
         for sp in sw_ports[len(sw_ports) - arp_silent_ports:] if arp_silent_ports else []:

@@ -338,3 +338,20 @@ def test_networkmanager_stays_off_the_nics_across_an_ordinary_restart():
     assert r["label"] and r["agent_rc"] == 0
     assert r["nm_keyfile_after_sigterm"] is True
     assert r["nm_managed_after_sigterm"] == {**{n: False for n in r["nics"]}, "eth9": True}
+
+
+def test_rail_cabling_check_names_a_nic_on_another_rails_leaf():
+    """railSwitchPattern: every rail has its own leaf ("leaf-r<k>"), and the NIC of GPU k must
+    reach leaf k.  Correct cabling labels the node; a NIC cabled to rail 3's leaf instead of rail
+    2's is left unconfigured, and the error names it, the switch and its port."""
+    ok = netns.run_isolated(n_nics=4, seed=31, interval="1s", fast_start=True, switch_name="leaf-r{port}",
+                            extra_args=["--rail-switch-pattern=leaf-r{rail}"])
+    _check_configured(ok)
+    bad = netns.run_isolated(n_nics=4, seed=31, interval="1s", fast_start=True, switch_name="leaf-r{port}",
+                             port_switch_names={"swp2": "leaf-r3"}, extra_args=["--rail-switch-pattern=leaf-r{rail}"])
+    assert not bad["ready"] and bad["agent_rc"] == 1
+    nic = bad["nics"][2]
+    err = [ln for ln in bad["agent_log"].splitlines() if ln.startswith("Error: ")][-1]
+    assert err.startswith("Error: Not all interfaces were configured (3/4). Not configured: "
+                          f"{nic}: rail 2 is cabled to switch 'leaf-r3' port 'swp2', not to one matching 'leaf-r2'"), err
+    assert bad["state"][nic]["addrs"] == [] and all(bad["state"][n]["addrs"] for n in bad["nics"] if n != nic)

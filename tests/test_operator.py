@@ -923,3 +923,18 @@ def test_deleted_before_the_status_recorded_its_nodes_still_cleans_them():
         finally:
             await fake.stop()
     run(body())
+
+
+def test_rail_switch_pattern_validated_and_passed():
+    from network_operator_amd.api.v1alpha1 import webhook as W
+
+    p = T.new_policy("p", layer="L3", railSwitchPattern="leaf-r{rail}-su[0-9]+")
+    assert "--rail-switch-pattern=leaf-r{rail}-su[0-9]+" in agent_args(p)
+    assert W.validate_create(p) == []
+    assert not any("rail-switch" in a for a in agent_args(T.new_policy("p", layer="L2", railSwitchPattern="x")))
+    assert W.validate_create(T.new_policy("p", layer="L2", railSwitchPattern="x")) == [
+        "railSwitchPattern has no effect in L2 mode (no LLDP)"]
+    with pytest.raises(W.InvalidRailSwitchPatternError, match="invalid railSwitchPattern"):
+        W.validate_create(T.new_policy("p", layer="L3", railSwitchPattern="leaf-(r{rail}"))
+    rt = T.NetworkClusterPolicy.from_dict(p.to_dict())
+    assert rt.spec.amdScaleOut.railSwitchPattern == "leaf-r{rail}-su[0-9]+"

@@ -464,3 +464,9 @@ def test_validation_rccl_sweep_sources_the_agents_artifacts(monkeypatch, tmp_pat
                 artifact_dir=str(art))
     by = {c["check"]: c for c in rep["checks"]}
     assert not by["rccl_xgmi_links"]["ok"] and by["rccl_xgmi_links"]["status"] == "failed" and not rep["ok"]
+
+
+def test_helm_rail_switch_pattern_renders_quoted():
+    docs = helm_template(CHART, {"config": {"amd": {"enabled": True, "railSwitchPattern": "leaf-r{rail}-.*"}}})
+    cr = _chart_policies(docs)[0]
+    assert cr["spec"]["amdScaleOut"]["railSwitchPattern"] == "leaf-r{rail}-.*" and CRD.validate(cr) == []
