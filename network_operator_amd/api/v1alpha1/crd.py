@@ -169,6 +169,13 @@ def openapi_schema() -> dict:
                 "enum": list(T.CONFIGURATION_TYPES), "type": "string"},
             "amdScaleOut": amd_so,
             "hostNic": host_nic,
+            "maxUnavailable": {
+                "description": "Agent Pods the DaemonSet may replace at once during a rolling update: a number or\n"
+                               "a percentage of the targeted nodes (default 1, as in the reference).  Larger\n"
+                               "values roll big clusters faster; with keepConfigOnRestart the roll does not\n"
+                               "disturb running jobs.",
+                "anyOf": [{"type": "integer"}, {"type": "string"}], "pattern": "^(100|[1-9][0-9]?)%$",
+                "x-kubernetes-int-or-string": True},
             "logLevel": {"description": "LogLevel sets the agent's log level.", "maximum": T.LOG_LEVEL_MAX,
                          "minimum": T.LOG_LEVEL_MIN, "type": "integer"},
             "nodeSelector": {"additionalProperties": {"type": "string"},
@@ -269,6 +276,13 @@ _PY_TYPES = {"string": (str,), "integer": (int,), "boolean": (bool,), "object": 
 
 
 def _validate(value: Any, schema: dict, path: str, errs: List[str]) -> None:
+    if schema.get("x-kubernetes-int-or-string"):
+        if isinstance(value, bool) or not isinstance(value, (int, str)):
+            errs.append(f"{path}: Invalid value: {value!r}: {path} in body must be of type integer or string")
+            return
+        if isinstance(value, str) and "pattern" in schema and not re.search(schema["pattern"], value):
+            errs.append(f'{path}: Invalid value: "{value}": {path} in body should match \'{schema["pattern"]}\'')
+        return
     t = schema.get("type")
     if t:
         ok = isinstance(value, _PY_TYPES[t]) and not (t in ("integer", "number") and isinstance(value, bool))

@@ -25,7 +25,7 @@ from __future__ import annotations
 
 import copy
 from dataclasses import dataclass, field
-from typing import Any, Dict, List, Optional
+from typing import Any, Dict, List, Optional, Union
 
 GROUP = "amd.com"
 VERSION = "v1alpha1"
@@ -261,6 +261,8 @@ class NetworkClusterPolicySpec:
     amdScaleOut: AmdScaleOutSpec = field(default_factory=AmdScaleOutSpec)
     hostNic: Optional[HostNicSpec] = None
     logLevel: int = 0
+    # DaemonSet rollingUpdate.maxUnavailable: int >= 1 or "N%" (None = 1, the reference's default)
+    maxUnavailable: Optional[Union[int, str]] = None
     extra: Dict[str, Any] = field(default_factory=dict)
 
     def to_dict(self) -> dict:
@@ -273,6 +275,8 @@ class NetworkClusterPolicySpec:
             d["hostNic"] = self.hostNic.to_dict()
         if self.logLevel:
             d["logLevel"] = self.logLevel
+        if self.maxUnavailable is not None:
+            d["maxUnavailable"] = self.maxUnavailable
         d.update(copy.deepcopy(self.extra))
         return d
 
@@ -285,6 +289,7 @@ class NetworkClusterPolicySpec:
             amdScaleOut=AmdScaleOutSpec.from_dict(d.pop("amdScaleOut", None)),
             hostNic=HostNicSpec.from_dict(d.pop("hostNic")) if d.get("hostNic") is not None else None,
             logLevel=int(d.pop("logLevel", 0) or 0),
+            maxUnavailable=d.pop("maxUnavailable", None),
         )
         s.extra = d
         return s

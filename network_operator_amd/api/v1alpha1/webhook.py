@@ -130,6 +130,22 @@ def validate_rail_switch_pattern(value: str) -> None:
         raise InvalidRailSwitchPatternError(value, str(e)) from None
 
 
+class InvalidMaxUnavailableError(ValidationError):
+    def __init__(self, value):
+        super().__init__()
+        self.message = f"invalid maxUnavailable {value!r}: a number >= 1 or a percentage 1%..100%"
+
+
+def validate_max_unavailable(value) -> None:
+    import re
+
+    if value is None:
+        return
+    if isinstance(value, bool) or not (isinstance(value, int) and value >= 1 or
+                                       isinstance(value, str) and re.fullmatch(r"(100|[1-9][0-9]?)%", value)):
+        raise InvalidMaxUnavailableError(value)
+
+
 def validate_lldp_wait(value: str) -> None:
     if not value:
         return
@@ -181,6 +197,7 @@ def validate_host_nic_spec(s: Optional[T.HostNicSpec]) -> List[str]:
 
 def validate_spec(spec: T.NetworkClusterPolicySpec) -> List[str]:
     validate_node_selector(spec.nodeSelector)
+    validate_max_unavailable(spec.maxUnavailable)
     if spec.configurationType == T.CONFIG_AMD_SCALE_OUT:
         return validate_amd_so_spec(spec.amdScaleOut)
     if spec.configurationType == T.CONFIG_HOST_NIC:

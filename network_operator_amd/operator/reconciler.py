@@ -320,7 +320,10 @@ def update_host_nic_daemonset(ds: dict, p: T.NetworkClusterPolicy, namespace: st
 
 
 def update_daemonset_for(ds: dict, p: T.NetworkClusterPolicy, namespace: str) -> None:
-    """createDaemonSet / updateDaemonSet dispatch on configurationType (:243-265)."""
+    """createDaemonSet / updateDaemonSet dispatch on configurationType (:243-265).  Also the
+    rolling-update width (spec.maxUnavailable; 1 when unset, like the reference's DaemonSet)."""
+    ds["spec"].setdefault("updateStrategy", {"type": "RollingUpdate"}).setdefault("rollingUpdate", {})[
+        "maxUnavailable"] = p.spec.maxUnavailable if p.spec.maxUnavailable is not None else 1
     if p.spec.configurationType == T.CONFIG_AMD_SCALE_OUT:
         update_amd_scale_out_daemonset(ds, p, namespace)
     elif p.spec.configurationType == T.CONFIG_HOST_NIC:
@@ -927,7 +930,8 @@ class NetworkClusterPolicyReconciler:
     async def _update(self, raw: dict, p: T.NetworkClusterPolicy, ds: dict) -> Result:
         original = copy.deepcopy(ds)
         update_daemonset_for(ds, p, self.namespace)
-        if original["spec"]["template"]["spec"] != ds["spec"]["template"]["spec"]:
+        if original["spec"]["template"]["spec"] != ds["spec"]["template"]["spec"] or \
+                original["spec"].get("updateStrategy") != ds["spec"].get("updateStrategy"):
             log.info("DS difference for %s", p.name)
             ds = await self.client.replace(kube.DAEMONSETS, ds)
             await self._event(raw, "Normal", "DaemonSetUpdated", f"Updated DaemonSet {self.namespace}/{p.name}")

@@ -938,3 +938,30 @@ def test_rail_switch_pattern_validated_and_passed():
         W.validate_create(T.new_policy("p", layer="L3", railSwitchPattern="leaf-(r{rail}"))
     rt = T.NetworkClusterPolicy.from_dict(p.to_dict())
     assert rt.spec.amdScaleOut.railSwitchPattern == "leaf-r{rail}-su[0-9]+"
+
+
+def test_max_unavailable_sets_the_rollout_width():
+    from network_operator_amd.api.v1alpha1 import crd as CRD
+    from network_operator_amd.api.v1alpha1 import webhook as W
+
+    async def body():
+        async with cluster(openshift=False) as (fake, client, ctl):
+            await client.create(kube.NETWORKCLUSTERPOLICIES, policy())
+
+            def width():
+                ds = fake.get_object(kube.DAEMONSETS, "policy", NS)
+                return ds and ds["spec"]["updateStrategy"]["rollingUpdate"]
+            await eventually(lambda: width() == {"maxSurge": 0, "maxUnavailable": 1})  # the reference's default
+            await edit(client, "policy", lambda cur: cur["spec"].update(maxUnavailable="10%"))
+            await eventually(lambda: width() == {"maxSurge": 0, "maxUnavailable": "10%"})
+            await edit(client, "policy", lambda cur: cur["spec"].update(maxUnavailable=4))
+            await eventually(lambda: width()["maxUnavailable"] == 4)
+    run(body())
+    for bad in (0, "0%", "150%", "ten", True):
+        with pytest.raises(W.InvalidMaxUnavailableError):
+            W.validate_max_unavailable(bad)
+    pol = policy()
+    pol["spec"]["maxUnavailable"] = "25%"
+    assert CRD.validate(pol) == []
+    pol["spec"]["maxUnavailable"] = "25 percent"
+    assert CRD.validate(pol) and "should match" in CRD.validate(pol)[0]

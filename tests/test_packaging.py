@@ -470,3 +470,10 @@ def test_helm_rail_switch_pattern_renders_quoted():
     docs = helm_template(CHART, {"config": {"amd": {"enabled": True, "railSwitchPattern": "leaf-r{rail}-.*"}}})
     cr = _chart_policies(docs)[0]
     assert cr["spec"]["amdScaleOut"]["railSwitchPattern"] == "leaf-r{rail}-.*" and CRD.validate(cr) == []
+
+
+def test_helm_max_unavailable_renders():
+    docs = helm_template(CHART, {"config": {"amd": {"enabled": True, "maxUnavailable": "10%"}}})
+    cr = _chart_policies(docs)[0]
+    assert cr["spec"]["maxUnavailable"] == "10%" and CRD.validate(cr) == []
+    assert "maxUnavailable" not in _chart_policies(helm_template(CHART, {"config": {"amd": {"enabled": True}}}))[0]["spec"]
