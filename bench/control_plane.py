@@ -11,7 +11,14 @@ Measured:
 * ``all_good_s``:    every agent on every node reports ready -> every policy "All good";
 * ``manager_rss_mib``: the manager's peak RSS (VmHWM), against the Deployment's 128Mi limit
   (reference config/operator/manager/manager.yaml:95-101);
-* ``requests``: API requests the manager made (informers, not polling).
+* ``requests``: API requests the manager made (informers, not polling);
+* ``manager_cpu_s``: the manager's own CPU time over the run.  The wall-clock phases include the
+  fake API server, a single Python process that also plays the DaemonSet controller and streams
+  every Pod (realistic ones, kilobytes each) to the watchers.
+
+With ``--keep-config`` the policies use ``keepConfigOnRestart``, and the run goes on to delete
+them: ``delete_to_cleanup_jobs_s`` (every node's cleanup Job exists), then the simulated kubelets
+complete them, and ``cleanup_done_to_gone_s`` (every policy finalized and gone).
 
 The reference has no equivalent measurement (controller-runtime + envtest, no scale test).
 
@@ -45,38 +52,51 @@ def _port() -> int:
     return p
 
 
+def _cpu_s(pid: int) -> float:
+    """utime + stime of the process (the manager's own CPU, apart from the fake API server's)."""
+    with open(f"/proc/{pid}/stat") as f:
+        fields = f.read().rsplit(")", 1)[1].split()
+    return (int(fields[11]) + int(fields[12])) / os.sysconf("SC_CLK_TCK")
+
+
 def _hwm_mib(pid: int) -> float:
     with open(f"/proc/{pid}/status") as f:
         line = next(x for x in f if x.startswith("VmHWM:"))
     return int(line.split()[1]) / 1024
 
 
-async def _until(pred, timeout: float) -> float:
+async def _until(pred, timeout: float, poll: float = 0.005) -> float:
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < timeout:
         if pred():
             return time.perf_counter() - t0
-        await asyncio.sleep(0.005)
-    raise TimeoutError("did not converge")
+        await asyncio.sleep(poll)
+    raise TimeoutError(f"did not converge: {getattr(pred, '__name__', pred)} at line {pred.__code__.co_firstlineno}")
 
 
-async def run(nodes: int, policies: int, timeout: float) -> dict:
+async def run(nodes: int, policies: int, timeout: float, keep: bool = False) -> dict:
     fake = FakeApiServer(bookmark_interval=5.0)
     url = await fake.start()
     for i in range(nodes):
         fake.add_node(f"gpu-node-{i:04d}", {LABEL: "true"})
     env = dict(os.environ, PYTHONPATH=ROOT, OPERATOR_NAMESPACE="amd-network-operator", ENABLE_WEBHOOKS="false")
+    # The manager's log goes to a file: a pipe nobody reads fills up and blocks it (one log line
+    # per cleanup Job at scale).
+    import tempfile
+
+    log = tempfile.NamedTemporaryFile(prefix="netop-cp-manager-", suffix=".log", delete=False)
     proc = subprocess.Popen([sys.executable, "-m", "network_operator_amd.operator.manager", "--master", url,
                              f"--health-probe-bind-address=127.0.0.1:{_port()}", "--metrics-bind-address=0"],
-                            env=env, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True)
+                            env=env, stdout=subprocess.DEVNULL, stderr=log)
     try:
         await asyncio.sleep(1.0)  # manager start: informers list + watch
         n_req0 = len(fake.requests)
+        cpu0 = _cpu_s(proc.pid)
         P = kube.NETWORKCLUSTERPOLICIES
         names = [f"policy-{k}" for k in range(policies)]
         t0 = time.perf_counter()
         for n in names:
-            fake._create(P, T.new_policy(n).to_dict(), None)
+            fake._create(P, T.new_policy(n, keepConfigOnRestart=keep).to_dict(), None)
 
         def ds_all():
             return all(fake.get_object(kube.DAEMONSETS, n, "amd-network-operator") for n in names)
@@ -100,10 +120,30 @@ async def run(nodes: int, policies: int, timeout: float) -> dict:
         await _until(good_all, timeout)
         t_good = time.perf_counter() - t1
         await asyncio.sleep(0.5)
+        out = {"nodes": nodes, "policies": policies, "pods": nodes * policies, "daemonsets_s": round(t_ds, 4),
+               "targets_s": round(t_targets, 4), "all_good_s": round(t_good, 4)}
+        if keep:
+            await _until(lambda: all(len((fake.get_object(P, n).get("status") or {}).get("keptNodes") or []) == nodes
+                                     for n in names), timeout)
+            t2 = time.perf_counter()
+            for n in names:
+                fake._delete_or_mark(P, n, "")
+            await _until(lambda: len(fake._table(kube.JOBS)) == nodes * policies, timeout, poll=0.05)
+            out["delete_to_cleanup_jobs_s"] = round(time.perf_counter() - t2, 4)
+            t3 = time.perf_counter()
+            for j in fake.list_objects(kube.JOBS):
+                fake.set_job_result(j["metadata"]["name"], "amd-network-operator", True)
+            await _until(lambda: not any(fake.get_object(P, n) for n in names), timeout, poll=0.05)
+            out["cleanup_done_to_gone_s"] = round(time.perf_counter() - t3, 4)
+        await asyncio.sleep(0.5)
         rss = _hwm_mib(proc.pid)
-        return {"nodes": nodes, "policies": policies, "pods": nodes * policies, "daemonsets_s": round(t_ds, 4),
-                "targets_s": round(t_targets, 4), "all_good_s": round(t_good, 4), "manager_rss_mib": round(rss, 1),
-                "manager_limit_mib": 128, "requests": len(fake.requests) - n_req0}
+        out.update(manager_rss_mib=round(rss, 1), manager_limit_mib=128, requests=len(fake.requests) - n_req0,
+                   manager_cpu_s=round(_cpu_s(proc.pid) - cpu0, 2))
+        return out
+    except Exception:
+        log.flush()
+        print(open(log.name, errors="replace").read()[-4000:], file=sys.stderr)
+        raise
     finally:
         proc.terminate()
         try:
@@ -118,8 +158,9 @@ def main() -> int:
     ap.add_argument("--nodes", type=int, default=1000)
     ap.add_argument("--policies", type=int, default=4)
     ap.add_argument("--timeout", type=float, default=300)
+    ap.add_argument("--keep-config", action="store_true", help="keepConfigOnRestart policies, then delete them")
     a = ap.parse_args()
-    print(json.dumps(asyncio.run(run(a.nodes, a.policies, a.timeout))))
+    print(json.dumps(asyncio.run(run(a.nodes, a.policies, a.timeout, a.keep_config))))
     return 0
 
 

@@ -16,7 +16,7 @@ from typing import Dict, List, Optional
 
 from ..api.v1alpha1 import types as T
 from . import kube
-from .informer import Informer, controller_of
+from .informer import Informer, controller_of, slim_pod
 from .kube import ApiClient
 from .metrics import OperatorMetrics
 from .reconciler import (OWNER_KEY, VALIDATION_APP, EventRecorder, NetworkClusterPolicyReconciler,
@@ -45,13 +45,15 @@ class PolicyController:
         self.daemonsets.add_index(OWNER_KEY, policy_owner_index)
         # Agent pods (indexPods in the reference, :385-404): their Ready condition explains
         # which nodes are not configured yet (status.errors).
-        self.pods = Informer(client, kube.PODS, namespace=namespace, label_selector="app=amd-network-tools")
+        self.pods = Informer(client, kube.PODS, namespace=namespace, label_selector="app=amd-network-tools",
+                             transform=slim_pod)
         self.pods.add_index(OWNER_KEY, daemonset_owner_index)
         # Fabric validation Jobs (amdScaleOut.validation): their outcome is the FabricValidated condition.
         self.jobs = Informer(client, kube.JOBS, namespace=namespace, label_selector=f"app={VALIDATION_APP}")
         self.jobs.add_index(OWNER_KEY, policy_owner_index)
         # Their Pods: a Pod the kubelet refused to run is not a validation verdict.
-        self.job_pods = Informer(client, kube.PODS, namespace=namespace, label_selector=f"app={VALIDATION_APP}")
+        self.job_pods = Informer(client, kube.PODS, namespace=namespace, label_selector=f"app={VALIDATION_APP}",
+                                 transform=slim_pod)
         self.job_pods.add_index(OWNER_KEY, job_owner_index)
         self.queue = RateLimitingQueue(CONTROLLER_NAME)
         self.reconciler = NetworkClusterPolicyReconciler(

@@ -7,7 +7,10 @@ internal/controller/networkconfiguration_controller.go:364-404 registers a field
 * initial LIST, then WATCH from the list's resourceVersion; bookmarks advance it;
 * 410 Gone (compacted history) -> relist and emit synthetic adds/updates/deletes for the diff;
 * any other stream end -> reconnect with jittered backoff;
-* ``add_index(name, fn)`` / ``by_index(name, value)`` for owner lookups.
+* ``add_index(name, fn)`` / ``by_index(name, value)`` for owner lookups;
+* ``transform``: what is cached (client-go's SetTransform), e.g. ``slim_pod``: one agent Pod per
+  node and policy is tens of thousands of Pods on a large cluster, and a full Pod object
+  (containers, volumes, tolerations, managedFields) costs kilobytes of Python heap each.
 """
 
 from __future__ import annotations
@@ -30,6 +33,28 @@ def obj_key(obj: dict) -> str:
     return f"{ns}/{md['name']}" if ns else md["name"]
 
 
+_POD_META = ("name", "namespace", "uid", "resourceVersion", "labels", "ownerReferences", "creationTimestamp",
+             "deletionTimestamp")
+_CONTAINER_STATUS = ("name", "ready", "restartCount", "state", "lastState")
+
+
+def slim_pod(pod: dict) -> dict:
+    """The fields the operator reads from a Pod (node, Ready condition, phase / admission reason,
+    container exit records, owner), nothing else."""
+    md = pod.get("metadata") or {}
+    st = pod.get("status") or {}
+    out_st = {k: st[k] for k in ("phase", "reason", "message") if k in st}
+    conds = [c for c in st.get("conditions") or [] if c.get("type") == "Ready"]
+    if conds:
+        out_st["conditions"] = conds
+    cs = [{k: c[k] for k in _CONTAINER_STATUS if k in c} for c in st.get("containerStatuses") or []]
+    if cs:
+        out_st["containerStatuses"] = cs
+    return {"apiVersion": pod.get("apiVersion", "v1"), "kind": pod.get("kind", "Pod"),
+            "metadata": {k: md[k] for k in _POD_META if k in md},
+            "spec": {"nodeName": (pod.get("spec") or {}).get("nodeName", "")}, "status": out_st}
+
+
 def controller_of(obj: dict) -> Optional[dict]:
     """metav1.GetControllerOf."""
     for ref in obj.get("metadata", {}).get("ownerReferences", []) or []:
@@ -40,8 +65,10 @@ def controller_of(obj: dict) -> Optional[dict]:
 
 class Informer:
     def __init__(self, client: ApiClient, res: Resource, namespace: Optional[str] = None,
-                 label_selector: Optional[str] = None, resync_timeout: int = 300):
+                 label_selector: Optional[str] = None, resync_timeout: int = 300,
+                 transform: Optional[Callable[[dict], dict]] = None):
         self.client = client
+        self.transform = transform
         self.res = res
         self.namespace = namespace
         self.label_selector = label_selector
@@ -100,6 +127,8 @@ class Informer:
                 log.exception("informer handler failed")
 
     async def _apply(self, ev: str, obj: dict) -> None:
+        if self.transform is not None:
+            obj = self.transform(obj)
         key = obj_key(obj)
         old = self.store.get(key)
         if ev == "DELETED":

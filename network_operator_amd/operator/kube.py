@@ -264,8 +264,13 @@ class ApiClient:
         return await self.request("GET", res.path(namespace, name))
 
     async def list(self, res: Resource, namespace: Optional[str] = None, label_selector: Optional[str] = None,
-                   field_selector: Optional[str] = None, resource_version: Optional[str] = None) -> dict:
+                   field_selector: Optional[str] = None, resource_version: Optional[str] = None,
+                   limit: int = 0, continue_: str = "") -> dict:
         params = {}
+        if limit:
+            params["limit"] = str(limit)
+        if continue_:
+            params["continue"] = continue_
         if label_selector:
             params["labelSelector"] = label_selector
         if field_selector:

@@ -25,6 +25,7 @@ Kubernetes Events are emitted (RBAC for them was granted but unused by the refer
 
 from __future__ import annotations
 
+import asyncio
 import copy
 import time
 import logging
@@ -454,6 +455,8 @@ CLEANUP_APP = "amd-network-cleanup"
 KEPT_ORPHAN_GRACE_S = 600.0
 CLEANUP_TIMEOUT_S = 600.0  # a cleanup Job not finished by then (node gone, image missing) is given up
 CLEANUP_POLL_S = 2.0       # cleanup Jobs are not watched: poll while some are running
+CLEANUP_CREATE_CONCURRENCY = 32
+CLEANUP_LIST_PAGE = 500
 
 
 def keeps_config(p: T.NetworkClusterPolicy) -> bool:
@@ -635,6 +638,8 @@ class NetworkClusterPolicyReconciler:
         # keepConfigOnRestart: (policy, node) -> when the node's agent Pod was first seen missing
         self._missing_since: dict = {}
         self.on_cleanup: Optional[Callable[[str, str], None]] = None  # (policy, outcome): metrics
+        self._cleanups_reported: set = set()  # finished cleanup Jobs already counted / reported
+        self._cleanup_jobs_exist: set = set()  # policies with cleanup Jobs left to finish or delete
 
     def _node_errors(self, ds_name: str, limit: int = 16) -> List[str]:
         """Per-node agent problems from the agent Pods' Ready condition (the reference indexes
@@ -663,47 +668,88 @@ class NetworkClusterPolicyReconciler:
                 raise
 
     async def _cleanup_jobs(self, policy: str) -> dict:
-        out = {}
-        lst = await self.client.list(kube.JOBS, self.namespace,
-                                     label_selector=f"app={CLEANUP_APP},amd.com/policy={policy[:63]}")
-        for j in lst.get("items") or []:
-            out[(j["metadata"].get("annotations") or {}).get("amd.com/node", "")] = j
-        return out
+        """node -> the policy's cleanup Job, reduced to what is used (name, creation time,
+        status), read in pages: a thousand-node policy's Jobs in one LIST would be megabytes
+        of JSON parsed at once, against the operator's 128 MiB limit."""
+        out, cont = {}, ""
+        while True:
+            lst = await self.client.list(kube.JOBS, self.namespace, limit=CLEANUP_LIST_PAGE, continue_=cont,
+                                         label_selector=f"app={CLEANUP_APP},amd.com/policy={policy[:63]}")
+            for j in lst.get("items") or []:
+                md = j["metadata"]
+                out[(md.get("annotations") or {}).get("amd.com/node", "")] = {
+                    "metadata": {"name": md["name"], "creationTimestamp": md.get("creationTimestamp", "")},
+                    "status": j.get("status") or {}}
+            cont = (lst.get("metadata") or {}).get("continue") or ""
+            if not cont:
+                return out
 
     async def _run_cleanups(self, raw: dict, p: T.NetworkClusterPolicy, nodes: List[str]) -> List[str]:
-        """Cleanup Jobs for ``nodes``: created when missing, deleted (and their node done) once
-        finished or past CLEANUP_TIMEOUT_S.  Returns the nodes still in progress."""
+        """Cleanup Jobs for ``nodes``: created when missing; a node whose Job finished (or ran
+        past CLEANUP_TIMEOUT_S) is done.  Returns the nodes still in progress.  A finished Job is
+        kept until a later pass finds its node no longer asked for, i.e. until the caller has
+        recorded the node as done: deleting it at once would make the next pass, reading a
+        status written before, take the node for one without a Job and clean it again."""
         jobs = await self._cleanup_jobs(p.name)
         now = self._clock()
-        pending = []
+        want = set(nodes)
+        stale = [j for node, j in jobs.items() if node not in want]
+        pending = [node for node in nodes if node not in jobs]
+        if pending:
+            # One template for all of them (only the node differs); CLEANUP_CREATE_CONCURRENCY
+            # creates in flight, so a thousand-node policy is cleaned in seconds, not minutes.
+            template = cleanup_job(p, "", self.namespace)
+            set_controller_reference(raw, template)
+            sem = asyncio.Semaphore(CLEANUP_CREATE_CONCURRENCY)
+
+            async def create(node: str) -> None:
+                async with sem:  # built inside: at most CLEANUP_CREATE_CONCURRENCY bodies exist at once
+                    job = copy.deepcopy(template)
+                    job["metadata"]["name"] = cleanup_job_name(p.name, node)
+                    job["metadata"]["annotations"]["amd.com/node"] = node
+                    job["spec"]["template"]["spec"]["nodeName"] = node
+                    try:
+                        await self.client.create(kube.JOBS, job, namespace=self.namespace)
+                    except ApiError as e:
+                        if not is_already_exists(e):
+                            raise
+            await asyncio.gather(*(create(n) for n in pending))
+            log.info("Created %d node cleanup Job(s) for policy %s", len(pending), p.name)
+        done = 0
         for node in nodes:
             j = jobs.get(node)
             if j is None:
-                job = cleanup_job(p, node, self.namespace)
-                set_controller_reference(raw, job)
-                try:
-                    await self.client.create(kube.JOBS, job, namespace=self.namespace)
-                    log.info("Created node cleanup Job %s for node %s", job["metadata"]["name"], node)
-                except ApiError as e:
-                    if not is_already_exists(e):
-                        raise
-                pending.append(node)
                 continue
             outcome = job_outcome(j)
             created = _rfc3339_to_unix(j["metadata"].get("creationTimestamp", "")) or now
             if outcome == "running" and now - created < CLEANUP_TIMEOUT_S:
                 pending.append(node)
                 continue
+            done += 1
+            if j["metadata"]["name"] in self._cleanups_reported:
+                continue
+            self._cleanups_reported.add(j["metadata"]["name"])
             if self.on_cleanup is not None:
                 self.on_cleanup(p.name, "timed_out" if outcome == "running" else outcome)
-            if outcome == "succeeded":
-                log.info("Node %s cleaned up (Job %s)", node, j["metadata"]["name"])
-            else:
+            if outcome != "succeeded":
                 why = "timed out" if outcome == "running" else "failed"
                 await self._event(raw, "Warning", "NodeCleanupFailed",
                                   f"{node}: cleanup Job {j['metadata']['name']} {why}; addresses and routes the agent "
                                   "left may remain (run the agent with --cleanup on the node)")
-            await self._delete_job(j)
+        if done:
+            log.info("Policy %s: %d node cleanup(s) finished, %d in progress", p.name, done, len(pending))
+        if stale:
+            sem = asyncio.Semaphore(CLEANUP_CREATE_CONCURRENCY)
+
+            async def delete(j: dict) -> None:
+                async with sem:
+                    await self._delete_job(j)
+                self._cleanups_reported.discard(j["metadata"]["name"])
+            await asyncio.gather(*(delete(j) for j in stale))
+        if len(jobs) - len(stale) + (len(nodes) - len([n for n in nodes if n in jobs])):
+            self._cleanup_jobs_exist.add(p.name)
+        else:
+            self._cleanup_jobs_exist.discard(p.name)
         return pending
 
     async def _kept_nodes(self, raw: dict, p: T.NetworkClusterPolicy, ds: dict) -> tuple:
@@ -729,7 +775,7 @@ class NetworkClusterPolicyReconciler:
                 due.append(node)
             else:
                 requeue_after = min(requeue_after, left) if requeue_after else left
-        if due:
+        if due or p.name in self._cleanup_jobs_exist:  # (finished Jobs of done nodes are deleted here)
             pending = set(await self._run_cleanups(raw, p, due))
             for node in due:
                 if node not in pending:
@@ -774,6 +820,16 @@ class NetworkClusterPolicyReconciler:
             return Result(requeue_after=1.0)  # agents still exiting: a cleanup must not race them
         pending = await self._run_cleanups(raw, p, list(p.status.keptNodes))
         if pending:
+            if sorted(pending) != sorted(p.status.keptNodes):
+                # Nodes whose cleanup finished leave the list now; the next pass deletes their
+                # Jobs (see _run_cleanups) instead of taking them for nodes without a Job.
+                body = copy.deepcopy(raw)
+                body["status"] = dict(raw.get("status") or {}, keptNodes=sorted(pending))
+                try:
+                    await self.client.replace_status(kube.NETWORKCLUSTERPOLICIES, body)
+                except ApiError as e:
+                    if not (is_conflict(e) or is_not_found(e)):
+                        raise
             return Result(requeue_after=CLEANUP_POLL_S)
         body = copy.deepcopy(raw)
         body["metadata"]["finalizers"] = [f for f in fins if f != FINALIZER]
@@ -786,6 +842,9 @@ class NetworkClusterPolicyReconciler:
                 raise
         for k in [k for k in self._missing_since if k[0] == p.name]:
             del self._missing_since[k]
+        self._cleanup_jobs_exist.discard(p.name)
+        prefix = cleanup_job_name(p.name, "")[:-10]
+        self._cleanups_reported = {n for n in self._cleanups_reported if not n.startswith(prefix)}
         log.info("Policy %s: %d node(s) cleaned up, finalizer removed", p.name, len(p.status.keptNodes))
         return Result()
 

@@ -177,6 +177,7 @@ class FakeApiServer:
         self.resources: List[Resource] = list(kube.ALL_RESOURCES)
         self.openshift = openshift
         self.objects: Dict[Tuple[str, str, str], Dict[Tuple[str, str], dict]] = {}
+        self._owned: Dict[str, set] = {}  # owner uid -> {(resource, namespace, name)} (garbage collector)
         self.rv = 100
         self.events: List[Tuple[int, Resource, str, dict]] = []
         self.history = history
@@ -319,14 +320,16 @@ class FakeApiServer:
 
     def _emit(self, res: Resource, typ: str, obj: dict) -> None:
         rv = int(obj["metadata"]["resourceVersion"]) if typ != "DELETED" else self.rv
-        self.events.append((rv, res, typ, copy.deepcopy(obj)))
+        # One snapshot, shared by the history and every watcher (they only serialise it).
+        snap = json.loads(json.dumps(obj))
+        self.events.append((rv, res, typ, snap))
         if len(self.events) > self.history:
             drop = len(self.events) - self.history
             self.compacted_before = self.events[drop - 1][0] + 1
             del self.events[:drop]
         for w in list(self.watches):
             if w.res == res and self._visible(w, obj):
-                w.queue.put_nowait((typ, copy.deepcopy(obj)))
+                w.queue.put_nowait((typ, snap))
 
     @staticmethod
     def _visible(w: _Watch, obj: dict) -> bool:
@@ -338,6 +341,12 @@ class FakeApiServer:
         return True
 
     def _store(self, res: Resource, obj: dict, typ: str) -> dict:
+        # Owner index for the garbage collector (a scan of every object per deletion is
+        # quadratic at thousands of Pods and Jobs); entries are re-checked when used.
+        for r in obj["metadata"].get("ownerReferences") or []:
+            if r.get("uid"):
+                self._owned.setdefault(r["uid"], set()).add(
+                    (res, obj["metadata"].get("namespace", "") if res.namespaced else "", obj["metadata"]["name"]))
         obj["metadata"]["resourceVersion"] = self._next_rv()
         self._table(res)[(obj["metadata"].get("namespace", "") if res.namespaced else "", obj["metadata"]["name"])] = obj
         self._emit(res, typ, obj)
@@ -411,11 +420,10 @@ class FakeApiServer:
 
     def _collect(self, uid: str) -> None:
         """Background cascading deletion of dependents (garbage collector)."""
-        for res in self.resources:
-            for (ns, name), o in list(self._table(res).items()):
-                refs = o.get("metadata", {}).get("ownerReferences") or []
-                if any(r.get("uid") == uid for r in refs) and (ns, name) in self._table(res):
-                    self._delete_or_mark(res, name, ns)
+        for res, ns, name in sorted(self._owned.pop(uid, ()), key=lambda k: (k[0].plural, k[1], k[2])):
+            o = self._table(res).get((ns, name))
+            if o is not None and any(r.get("uid") == uid for r in o.get("metadata", {}).get("ownerReferences") or []):
+                self._delete_or_mark(res, name, ns)
 
     # ------------------------------------------------------------------------------------------
     # DaemonSet controller simulation
@@ -473,12 +481,51 @@ class FakeApiServer:
                        "metadata": {"name": pname, "namespace": ns, "labels": labels,
                                     "ownerReferences": [{"apiVersion": "apps/v1", "kind": "DaemonSet", "name": name,
                                                          "uid": ds["metadata"]["uid"], "controller": True}]},
-                       "spec": {"nodeName": node}, "status": status}
+                       "spec": self._pod_spec(ds, node), "status": status}
                 self._create(kube.PODS, pod, ns)
             elif cur.get("status") != status:
                 new = copy.deepcopy(cur)
                 new["status"] = status
                 self._store(kube.PODS, new, "MODIFIED")
+
+    _DS_TOLERATIONS = [{"key": k, "operator": "Exists", "effect": e} for k, e in (
+        ("node.kubernetes.io/not-ready", "NoExecute"), ("node.kubernetes.io/unreachable", "NoExecute"),
+        ("node.kubernetes.io/disk-pressure", "NoSchedule"), ("node.kubernetes.io/memory-pressure", "NoSchedule"),
+        ("node.kubernetes.io/pid-pressure", "NoSchedule"), ("node.kubernetes.io/unschedulable", "NoSchedule"),
+        ("node.kubernetes.io/network-unavailable", "NoSchedule"))]
+
+    def _pod_spec(self, ds: dict, node: str) -> dict:
+        """What the DaemonSet controller and the API server put in a Pod: the template, the node
+        affinity pin, the DaemonSet tolerations and the service-account token volume.  Real Pods
+        are kilobytes each, and an operator caching them whole feels it at scale.  The template
+        part is built once per DaemonSet generation and shared (stored objects are copied before
+        any change, never mutated in place)."""
+        key = (ds["metadata"].get("uid"), ds["metadata"].get("generation"))
+        cache = self.__dict__.setdefault("_pod_spec_cache", {})
+        if key not in cache:
+            if len(cache) > 64:
+                cache.clear()
+            cache[key] = self._pod_spec_base(ds)
+        spec = dict(cache[key])
+        spec["nodeName"] = node
+        spec["affinity"] = {"nodeAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": {"nodeSelectorTerms": [
+            {"matchFields": [{"key": "metadata.name", "operator": "In", "values": [node]}]}]}}}
+        return spec
+
+    @classmethod
+    def _pod_spec_base(cls, ds: dict) -> dict:
+        spec = copy.deepcopy(ds["spec"]["template"].get("spec") or {})
+        spec["tolerations"] = list(spec.get("tolerations") or []) + [dict(t) for t in cls._DS_TOLERATIONS]
+        spec.setdefault("volumes", []).append(
+            {"name": "kube-api-access-x7k2p", "projected": {"defaultMode": 420, "sources": [
+                {"serviceAccountToken": {"expirationSeconds": 3607, "path": "token"}},
+                {"configMap": {"name": "kube-root-ca.crt", "items": [{"key": "ca.crt", "path": "ca.crt"}]}},
+                {"downwardAPI": {"items": [{"path": "namespace", "fieldRef": {"apiVersion": "v1",
+                                                                              "fieldPath": "metadata.namespace"}}]}}]}})
+        spec.update(dnsPolicy="ClusterFirstWithHostNet", restartPolicy="Always", schedulerName="default-scheduler",
+                    serviceAccountName=spec.get("serviceAccountName", "default"), enableServiceLinks=True,
+                    preemptionPolicy="PreemptLowerPriority", priority=0)
+        return spec
 
     def _transition_time(self) -> str:
         """RFC 3339 seconds like the API server, made unique per transition (a real cluster's
@@ -602,8 +649,18 @@ class FakeApiServer:
 
     # -- LIST / WATCH ---------------------------------------------------------------------------
     def _list(self, req: web.Request, res: Resource, ns: Optional[str]) -> web.Response:
+        """LIST, with the API server's chunking: ``limit`` items per page and an opaque
+        ``continue`` token (here: the last key served) in ``metadata.continue``."""
         items = []
-        for (ons, _), o in sorted(self._table(res).items()):
+        limit = int(req.query.get("limit") or 0)
+        after = None
+        if req.query.get("continue"):
+            after = tuple(json.loads(base64.urlsafe_b64decode(req.query["continue"].encode())))
+        more = ""
+        for key, o in sorted(self._table(res).items()):
+            (ons, _) = key
+            if after is not None and key <= after:
+                continue
             if res.namespaced and ns and ons != ns:
                 continue
             if req.query.get("labelSelector") and not match_labels(o["metadata"].get("labels") or {},
@@ -611,9 +668,16 @@ class FakeApiServer:
                 continue
             if req.query.get("fieldSelector") and not _match_fields(o, req.query["fieldSelector"]):
                 continue
+            if limit and len(items) == limit:
+                more = base64.urlsafe_b64encode(json.dumps(list(last)).encode()).decode()
+                break
             items.append(o)
-        return web.json_response({"kind": res.kind + "List", "apiVersion": res.api_version,
-                                  "metadata": {"resourceVersion": str(self.rv)}, "items": items})
+            last = key
+        md = {"resourceVersion": str(self.rv)}
+        if more:
+            md["continue"] = more
+        return web.json_response({"kind": res.kind + "List", "apiVersion": res.api_version, "metadata": md,
+                                  "items": items})
 
     async def _watch(self, req: web.Request, res: Resource, ns: Optional[str]) -> web.StreamResponse:
         since = int(req.query.get("resourceVersion") or 0)

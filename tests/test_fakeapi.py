@@ -177,3 +177,35 @@ def test_daemonset_status_counts_matching_nodes_and_ready_pods():
         st = (await c.get(DS, "d", "ns"))["status"]
         assert st["desiredNumberScheduled"] == 3
     _run(body)
+
+
+def test_list_in_chunks_with_limit_and_continue():
+    async def body(fake, c):
+        for i in range(7):
+            await c.create(P, _policy(f"p{i}"))
+        seen, cont, pages = [], "", 0
+        while True:
+            lst = await c.list(P, limit=3, continue_=cont)
+            seen += [x["metadata"]["name"] for x in lst["items"]]
+            pages += 1
+            cont = lst["metadata"].get("continue", "")
+            if not cont:
+                break
+        assert seen == [f"p{i}" for i in range(7)] and pages == 3
+        assert "continue" not in (await c.list(P))["metadata"]  # no limit: one page
+    _run(body)
+
+
+def test_finalizers_hold_deletion_and_the_gc_respects_them():
+    async def body(fake, c):
+        pol = _policy()
+        pol["metadata"]["finalizers"] = ["x/y"]
+        p = await c.create(P, pol)
+        await c.delete(P, "p")
+        held = fake.get_object(P, "p")
+        assert held["metadata"]["deletionTimestamp"] and held["metadata"]["finalizers"] == ["x/y"]
+        held = dict(held, metadata=dict(held["metadata"], finalizers=[]))
+        await c.replace(P, held)  # the last finalizer goes: so does the object
+        assert fake.get_object(P, "p") is None
+        assert p["metadata"]["uid"] not in fake._owned
+    _run(body)

@@ -6,6 +6,7 @@ ownerRef garbage collection, conflicts, watch recovery, leader election, metrics
 """
 
 import asyncio
+import json
 import contextlib
 
 import pytest
@@ -965,3 +966,36 @@ def test_max_unavailable_sets_the_rollout_width():
     assert CRD.validate(pol) == []
     pol["spec"]["maxUnavailable"] = "25 percent"
     assert CRD.validate(pol) and "should match" in CRD.validate(pol)[0]
+
+
+def test_pod_informer_caches_only_what_the_operator_reads():
+    """3000 nodes x 4 policies of whole Pods took the manager over its 128 MiB limit
+    (profiles/r3_control_plane_3000n_4p.json); the informer keeps the fields the reconciler and
+    the metrics read, and the exit-reason / readiness / admission logic still works on them."""
+    from network_operator_amd.operator.informer import slim_pod
+    from network_operator_amd.operator.reconciler import agent_epoch, agent_exit_reason, job_not_admitted
+
+    pod = {"apiVersion": "v1", "kind": "Pod",
+           "metadata": {"name": "p-n0", "namespace": NS, "uid": "u1", "resourceVersion": "7", "labels": {"app": "x"},
+                        "ownerReferences": [{"kind": "DaemonSet", "name": "p", "uid": "d", "controller": True}],
+                        "managedFields": [{"manager": "kubelet", "fieldsV1": {"f:status": {}}}] * 5},
+           "spec": {"nodeName": "n0", "containers": [{"name": "c", "image": "i", "env": [{"name": "A", "value": "b"}]}],
+                    "volumes": [{"name": "v", "hostPath": {"path": "/x"}}] * 4, "tolerations": [{"key": "k"}] * 7},
+           "status": {"phase": "Running", "hostIP": "10.0.0.1", "podIP": "10.0.0.1",
+                      "conditions": [{"type": "Initialized", "status": "True"},
+                                     {"type": "Ready", "status": "False", "reason": "ContainersNotReady",
+                                      "lastTransitionTime": "2026-01-01T00:00:01Z"}],
+                      "containerStatuses": [{"name": "c", "ready": False, "restartCount": 2, "image": "i",
+                                             "imageID": "sha256:abc", "containerID": "containerd://x",
+                                             "lastState": {"terminated": {"exitCode": 1, "reason": "Error",
+                                                                          "message": "Error: no LLDP peers"}}}]}}
+    s = slim_pod(pod)
+    assert set(s["metadata"]) == {"name", "namespace", "uid", "resourceVersion", "labels", "ownerReferences"}
+    assert s["spec"] == {"nodeName": "n0"}
+    assert [c["type"] for c in s["status"]["conditions"]] == ["Ready"]
+    assert "imageID" not in s["status"]["containerStatuses"][0] and "podIP" not in s["status"]
+    assert agent_exit_reason(s) == agent_exit_reason(pod) == "no LLDP peers"
+    assert agent_epoch(s) == agent_epoch(pod)
+    assert len(json.dumps(s)) < len(json.dumps(pod)) / 2
+    refused = {"status": {"phase": "Failed", "reason": "OutOfamd.com/gpu", "message": "no GPUs"}, "metadata": {"name": "j"}}
+    assert job_not_admitted([slim_pod(refused)]) == job_not_admitted([refused])
