@@ -16,7 +16,7 @@ from typing import Dict, List, Optional
 
 from ..api.v1alpha1 import types as T
 from . import kube
-from .informer import Informer, controller_of, slim_pod
+from .informer import Informer, controller_of, slim_job, slim_pod
 from .kube import ApiClient
 from .metrics import OperatorMetrics
 from .reconciler import (OWNER_KEY, VALIDATION_APP, EventRecorder, NetworkClusterPolicyReconciler,
@@ -49,7 +49,8 @@ class PolicyController:
                              transform=slim_pod)
         self.pods.add_index(OWNER_KEY, daemonset_owner_index)
         # Fabric validation Jobs (amdScaleOut.validation): their outcome is the FabricValidated condition.
-        self.jobs = Informer(client, kube.JOBS, namespace=namespace, label_selector=f"app={VALIDATION_APP}")
+        self.jobs = Informer(client, kube.JOBS, namespace=namespace, label_selector=f"app={VALIDATION_APP}",
+                             transform=slim_job)
         self.jobs.add_index(OWNER_KEY, policy_owner_index)
         # Their Pods: a Pod the kubelet refused to run is not a validation verdict.
         self.job_pods = Informer(client, kube.PODS, namespace=namespace, label_selector=f"app={VALIDATION_APP}",

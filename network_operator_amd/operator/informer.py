@@ -55,6 +55,19 @@ def slim_pod(pod: dict) -> dict:
             "spec": {"nodeName": (pod.get("spec") or {}).get("nodeName", "")}, "status": out_st}
 
 
+_JOB_META = _POD_META + ("annotations",)
+
+
+def slim_job(job: dict) -> dict:
+    """A Job as the reconciler reads it: identity, owner, its node / generation / epoch
+    annotations and the outcome (succeeded / failed counts, Complete / Failed conditions)."""
+    md = job.get("metadata") or {}
+    st = job.get("status") or {}
+    return {"apiVersion": job.get("apiVersion", "batch/v1"), "kind": job.get("kind", "Job"),
+            "metadata": {k: md[k] for k in _JOB_META if k in md},
+            "status": {k: st[k] for k in ("succeeded", "failed", "active", "conditions") if k in st}}
+
+
 def controller_of(obj: dict) -> Optional[dict]:
     """metav1.GetControllerOf."""
     for ref in obj.get("metadata", {}).get("ownerReferences", []) or []:

@@ -77,7 +77,7 @@ def test_keep_config_rolls_the_agent_without_touching_the_addresses_and_deletion
                          policy_kw={"keepConfigOnRestart": True})
     assert r["update_to_ready_again_s"] is not None, (r["policy_status"], r["agent_log"])
     assert "--keep-config" in r["agent_argv"]
-    assert r["roll_address_samples"] > 20 and r["roll_address_missing_samples"] == 0, r
+    assert r["roll_address_samples"] >= 5 and r["roll_address_missing_samples"] == 0, r
     assert r["policy_status"]["keptNodes"] == ["mi355x-0"]
     assert r["delete_to_cleaned_and_policy_gone_s"] is not None, (r["agent_log"], r.get("cleanup_job_runs"))
     assert [j["rc"] for j in r["cleanup_job_runs"]] == [0]
