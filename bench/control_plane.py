@@ -74,7 +74,7 @@ async def _until(pred, timeout: float, poll: float = 0.005) -> float:
     raise TimeoutError(f"did not converge: {getattr(pred, '__name__', pred)} at line {pred.__code__.co_firstlineno}")
 
 
-async def run(nodes: int, policies: int, timeout: float, keep: bool = False) -> dict:
+async def run(nodes: int, policies: int, timeout: float, keep: bool = False, validation: bool = False) -> dict:
     fake = FakeApiServer(bookmark_interval=5.0)
     url = await fake.start()
     for i in range(nodes):
@@ -96,7 +96,8 @@ async def run(nodes: int, policies: int, timeout: float, keep: bool = False) -> 
         names = [f"policy-{k}" for k in range(policies)]
         t0 = time.perf_counter()
         for n in names:
-            fake._create(P, T.new_policy(n, keepConfigOnRestart=keep).to_dict(), None)
+            fake._create(P, T.new_policy(n, keepConfigOnRestart=keep,
+                                         validation={"enabled": True} if validation else None).to_dict(), None)
 
         def ds_all():
             return all(fake.get_object(kube.DAEMONSETS, n, "amd-network-operator") for n in names)
@@ -119,9 +120,26 @@ async def run(nodes: int, policies: int, timeout: float, keep: bool = False) -> 
 
         await _until(good_all, timeout)
         t_good = time.perf_counter() - t1
+        if validation:  # every ready node gets its validation Job; the simulated kubelets pass them
+            t_v = time.perf_counter()
+            await _until(lambda: len(fake._table(kube.JOBS)) == nodes * policies, timeout, poll=0.05)
+            jobs_s = time.perf_counter() - t_v
+            for j in fake.list_objects(kube.JOBS):
+                fake.set_job_result(j["metadata"]["name"], "amd-network-operator", True)
+
+            def validated_all():
+                for n in names:
+                    c = {x["type"]: x for x in (fake.get_object(P, n).get("status") or {}).get("conditions") or []}
+                    if (c.get("FabricValidated") or {}).get("reason") != "AllNodesValidated":
+                        return False
+                return True
+            await _until(validated_all, timeout, poll=0.05)
         await asyncio.sleep(0.5)
         out = {"nodes": nodes, "policies": policies, "pods": nodes * policies, "daemonsets_s": round(t_ds, 4),
                "targets_s": round(t_targets, 4), "all_good_s": round(t_good, 4)}
+        if validation:
+            out.update(ready_to_validation_jobs_s=round(jobs_s, 4),
+                       jobs_done_to_validated_s=round(time.perf_counter() - t_v - jobs_s, 4))
         if keep:
             await _until(lambda: all(len((fake.get_object(P, n).get("status") or {}).get("keptNodes") or []) == nodes
                                      for n in names), timeout)
@@ -159,8 +177,9 @@ def main() -> int:
     ap.add_argument("--policies", type=int, default=4)
     ap.add_argument("--timeout", type=float, default=300)
     ap.add_argument("--keep-config", action="store_true", help="keepConfigOnRestart policies, then delete them")
+    ap.add_argument("--validation", action="store_true", help="fabric validation Jobs on every ready node")
     a = ap.parse_args()
-    print(json.dumps(asyncio.run(run(a.nodes, a.policies, a.timeout, a.keep_config))))
+    print(json.dumps(asyncio.run(run(a.nodes, a.policies, a.timeout, a.keep_config, a.validation))))
     return 0
 
 

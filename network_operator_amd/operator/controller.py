@@ -54,7 +54,8 @@ class PolicyController:
         self.jobs.add_index(OWNER_KEY, policy_owner_index)
         # Their Pods: a Pod the kubelet refused to run is not a validation verdict.
         self.job_pods = Informer(client, kube.PODS, namespace=namespace, label_selector=f"app={VALIDATION_APP}",
-                                 transform=slim_pod)
+                                 transform=slim_pod,
+                                 keep=lambda p: (p.get("status") or {}).get("phase") == "Failed")
         self.job_pods.add_index(OWNER_KEY, job_owner_index)
         self.queue = RateLimitingQueue(CONTROLLER_NAME)
         self.reconciler = NetworkClusterPolicyReconciler(

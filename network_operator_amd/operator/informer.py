@@ -18,6 +18,7 @@ from __future__ import annotations
 import asyncio
 import logging
 import random
+import sys
 from typing import Awaitable, Callable, Dict, List, Optional
 
 from .kube import ApiClient, ApiError, Resource, is_gone
@@ -33,9 +34,30 @@ def obj_key(obj: dict) -> str:
     return f"{ns}/{md['name']}" if ns else md["name"]
 
 
-_POD_META = ("name", "namespace", "uid", "resourceVersion", "labels", "ownerReferences", "creationTimestamp",
-             "deletionTimestamp")
+# (labels: the informers select on them server-side; nothing reads them from the cache)
+_POD_META = ("name", "namespace", "uid", "resourceVersion", "ownerReferences", "deletionTimestamp")
 _CONTAINER_STATUS = ("name", "ready", "restartCount", "state", "lastState")
+
+
+def _shared(v):
+    """Interns the keys and short string values of a slimmed object: tens of thousands of cached
+    Pods and Jobs repeat the same namespace, owner uid, kind, annotation keys and condition
+    types, and each JSON decode makes its own copies."""
+    if isinstance(v, str):
+        return sys.intern(v) if len(v) <= 96 else v
+    if isinstance(v, dict):
+        return {sys.intern(k): _shared(x) for k, x in v.items()}
+    if isinstance(v, list):
+        return [_shared(x) for x in v]
+    return v
+
+
+def _slim_meta(md: dict, keys) -> dict:
+    out = {k: md[k] for k in keys if k in md}
+    if "ownerReferences" in out:
+        out["ownerReferences"] = [{k: r[k] for k in ("apiVersion", "kind", "name", "uid", "controller") if k in r}
+                                  for r in out["ownerReferences"]]
+    return out
 
 
 def slim_pod(pod: dict) -> dict:
@@ -50,9 +72,9 @@ def slim_pod(pod: dict) -> dict:
     cs = [{k: c[k] for k in _CONTAINER_STATUS if k in c} for c in st.get("containerStatuses") or []]
     if cs:
         out_st["containerStatuses"] = cs
-    return {"apiVersion": pod.get("apiVersion", "v1"), "kind": pod.get("kind", "Pod"),
-            "metadata": {k: md[k] for k in _POD_META if k in md},
-            "spec": {"nodeName": (pod.get("spec") or {}).get("nodeName", "")}, "status": out_st}
+    return _shared({"apiVersion": pod.get("apiVersion", "v1"), "kind": pod.get("kind", "Pod"),
+                    "metadata": _slim_meta(md, _POD_META),
+                    "spec": {"nodeName": (pod.get("spec") or {}).get("nodeName", "")}, "status": out_st})
 
 
 _JOB_META = _POD_META + ("annotations",)
@@ -63,9 +85,11 @@ def slim_job(job: dict) -> dict:
     annotations and the outcome (succeeded / failed counts, Complete / Failed conditions)."""
     md = job.get("metadata") or {}
     st = job.get("status") or {}
-    return {"apiVersion": job.get("apiVersion", "batch/v1"), "kind": job.get("kind", "Job"),
-            "metadata": {k: md[k] for k in _JOB_META if k in md},
-            "status": {k: st[k] for k in ("succeeded", "failed", "active", "conditions") if k in st}}
+    return _shared({"apiVersion": job.get("apiVersion", "batch/v1"), "kind": job.get("kind", "Job"),
+            "metadata": _slim_meta(md, _JOB_META),
+            "status": {k: st[k] for k in ("succeeded", "failed", "active") if k in st} |
+            ({"conditions": [{k: c[k] for k in ("type", "status", "lastTransitionTime") if k in c}
+                             for c in st["conditions"]]} if st.get("conditions") else {})})
 
 
 def controller_of(obj: dict) -> Optional[dict]:
@@ -79,9 +103,13 @@ def controller_of(obj: dict) -> Optional[dict]:
 class Informer:
     def __init__(self, client: ApiClient, res: Resource, namespace: Optional[str] = None,
                  label_selector: Optional[str] = None, resync_timeout: int = 300,
-                 transform: Optional[Callable[[dict], dict]] = None):
+                 transform: Optional[Callable[[dict], dict]] = None,
+                 keep: Optional[Callable[[dict], bool]] = None):
         self.client = client
         self.transform = transform
+        # Objects failing `keep` are not cached (as if deleted): e.g. only the failed Pods of the
+        # validation Jobs, the ones whose admission reason matters.
+        self.keep = keep
         self.res = res
         self.namespace = namespace
         self.label_selector = label_selector
@@ -140,6 +168,10 @@ class Informer:
                 log.exception("informer handler failed")
 
     async def _apply(self, ev: str, obj: dict) -> None:
+        if self.keep is not None and ev != "DELETED" and not self.keep(obj):
+            if obj_key(obj) not in self.store:
+                return
+            ev = "DELETED"
         if self.transform is not None:
             obj = self.transform(obj)
         key = obj_key(obj)

@@ -990,7 +990,7 @@ def test_pod_informer_caches_only_what_the_operator_reads():
                                              "lastState": {"terminated": {"exitCode": 1, "reason": "Error",
                                                                           "message": "Error: no LLDP peers"}}}]}}
     s = slim_pod(pod)
-    assert set(s["metadata"]) == {"name", "namespace", "uid", "resourceVersion", "labels", "ownerReferences"}
+    assert set(s["metadata"]) == {"name", "namespace", "uid", "resourceVersion", "ownerReferences"}
     assert s["spec"] == {"nodeName": "n0"}
     assert [c["type"] for c in s["status"]["conditions"]] == ["Ready"]
     assert "imageID" not in s["status"]["containerStatuses"][0] and "podIP" not in s["status"]
