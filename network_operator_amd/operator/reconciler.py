@@ -890,6 +890,7 @@ class NetworkClusterPolicyReconciler:
         requeue_after = 0.0
         not_admitted = {}
         now = self._clock()
+        to_create = []
         for node in ready_nodes:
             j = jobs.get(node)
             attempt = 0
@@ -910,14 +911,24 @@ class NetworkClusterPolicyReconciler:
                     del jobs[node]
                     attempt += 1
             if node not in jobs:
-                job = validation_job(p, node, generation, self.namespace, agent_epoch(ready_pods[node]), attempt)
-                set_controller_reference(raw, job)
-                try:
-                    await self.client.create(kube.JOBS, job, namespace=self.namespace)
-                    log.info("Created fabric validation Job %s for node %s", job["metadata"]["name"], node)
-                except ApiError as e:
-                    if not is_already_exists(e):
-                        raise
+                to_create.append((node, attempt))
+        if to_create:
+            # CLEANUP_CREATE_CONCURRENCY creates in flight: a cluster that comes up at once gets
+            # its thousands of validation Jobs in seconds.
+            sem = asyncio.Semaphore(CLEANUP_CREATE_CONCURRENCY)
+
+            async def create(node: str, attempt: int) -> None:
+                async with sem:
+                    job = validation_job(p, node, generation, self.namespace, agent_epoch(ready_pods[node]), attempt)
+                    set_controller_reference(raw, job)
+                    try:
+                        await self.client.create(kube.JOBS, job, namespace=self.namespace)
+                        log.debug("Created fabric validation Job %s for node %s", job["metadata"]["name"], node)
+                    except ApiError as e:
+                        if not is_already_exists(e):
+                            raise
+            await asyncio.gather(*(create(n, a) for n, a in to_create))
+            log.info("Created %d fabric validation Job(s) for policy %s", len(to_create), p.name)
         # Judged over the nodes ready now: a node that left keeps its Job (and result) until the
         # next generation, but no longer counts either way.
         outcome = {n: job_outcome(jobs[n]) for n in ready_nodes if n in jobs and n not in not_admitted}
