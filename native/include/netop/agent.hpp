@@ -146,6 +146,12 @@ struct Config {
     // rail-optimized fabric).  A NIC on the wrong leaf still works but crosses the spine, so a
     // mismatch leaves it unconfigured and is named in the error.  "" = off.
     std::string rail_switch_pattern;
+    // Minimum negotiated link speed (Mb/s, sysfs class/net/<if>/speed): a 400G rail that came up
+    // at 200G (a marginal cable or optic, a port renegotiated down) halves that GPU's scale-out
+    // bandwidth while everything else looks healthy.  A slower NIC is left unconfigured (L3) or
+    // fails the start (L2), named in the error; a speed the driver does not report is allowed
+    // with a warning.  0 = off.
+    int64_t min_link_speed_mbps = 0;
     int64_t node_lock_wait_ns = 60LL * 1000000000;
 };
 
@@ -238,6 +244,7 @@ class Agent {
     void get_network_configs(const std::vector<std::string>& names);
     void detect_lldp(int stop_fd);
     void diagnose_silent();            // after --wait expired: why each silent NIC heard nothing
+    std::string check_link_speed(NicState& n);  // "" or why n is below --min-link-speed-gbps
     std::string silent_summary() const;  // "" or "LLDP silent on k NIC(s): ... Not configured: ..." for the exit error
     void on_lldp(NicState& n, const lldp::Frame& f);
     void add_route(NicState& n, int mask);

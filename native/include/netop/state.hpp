@@ -50,6 +50,7 @@ struct NicState {
 
     // Topology
     int gpu_index = -1;
+    int64_t speed_mbps = -1;  // negotiated link speed when checked (--min-link-speed-gbps), -1 unknown
     std::string gpu_bdf;
     std::string rdma_dev;
     int rdma_port = 1;

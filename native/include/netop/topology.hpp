@@ -88,6 +88,9 @@ std::optional<PciDev> read_pci_dir(const std::string& canonical_path, bool topo_
 bool read_topo_attrs(PciDev& d);
 // The PCI device behind a netdev (<root>/class/net/<ifname>/device); nullopt for virtual links.
 std::optional<PciDev> netdev_pci(const std::string& root, const std::string& ifname);
+// The negotiated link speed in Mb/s (<root>/class/net/<if>/speed), or -1 when the driver does not
+// report one (link down, virtual NIC, no such file).
+int64_t netdev_speed_mbps(const std::string& root, const std::string& ifname);
 // The ancestors RCCL puts above `d` in its topology tree, outermost first.  RCCL (NCCL's
 // ncclTopoGetXmlFromSys) climbs the sysfs path two components at a time — a switch's downstream
 // port and the switch above it count as one bridge — and stops at the root complex, whose

@@ -39,6 +39,8 @@ void sanitize(Config& c) {
 }
 
 namespace {
+std::string format_gbps(int64_t mbps) { return strfmt("%g", double(mbps) / 1000.0); }
+
 // Longest a --verify-peers re-probe may hold the monitor loop (see Agent::monitor).
 constexpr int64_t kMonitorVerifyNs = 250LL * 1000000;
 }  // namespace
@@ -576,6 +578,11 @@ bool Agent::configure_interface(NicState& n) {
         NLOG_W("Interface '%s' not configured: %s", n.ifname.c_str(), n.config_error.c_str());
         return false;
     }
+    if (std::string why = check_link_speed(n); !why.empty()) {
+        n.config_error = why;
+        NLOG_W("Interface '%s' not configured: %s", n.ifname.c_str(), n.config_error.c_str());
+        return false;
+    }
     if (!cfg_.rail_switch_pattern.empty() && n.gpu_index >= 0) {
         std::string want = cfg_.rail_switch_pattern;
         for (size_t at; (at = want.find("{rail}")) != std::string::npos;) want.replace(at, 6, std::to_string(n.gpu_index));
@@ -945,6 +952,20 @@ void Agent::diagnose_silent() {
     }
 }
 
+std::string Agent::check_link_speed(NicState& n) {
+    if (cfg_.min_link_speed_mbps <= 0) return "";
+    const std::string root = cfg_.sysfs_root.empty() ? topo::sysfs_root() : cfg_.sysfs_root;
+    n.speed_mbps = topo::netdev_speed_mbps(root, n.ifname);
+    if (n.speed_mbps < 0) {
+        NLOG_W("Interface '%s': the driver reports no link speed; --min-link-speed-gbps not checked", n.ifname.c_str());
+        return "";
+    }
+    if (n.speed_mbps >= cfg_.min_link_speed_mbps) return "";
+    return strfmt("link negotiated at %s Gb/s, below the required %s Gb/s (a marginal cable or optic, or a port "
+                  "renegotiated down: reseat or replace it)",
+                  format_gbps(n.speed_mbps).c_str(), format_gbps(cfg_.min_link_speed_mbps).c_str());
+}
+
 std::string Agent::silent_summary() const {
     std::vector<std::string> parts, failed;
     for (const auto& n : nics_) {
@@ -1286,6 +1307,13 @@ std::string Agent::render_metrics() const {
     metric("netop_agent_nic_degraded", "gauge", "1 while the NIC has lost link after readiness");
     for (auto& n : nics_)
         o += strfmt("netop_agent_nic_degraded{nic=\"%s\"} %d\n", httpd::escape_label(n.ifname).c_str(), n.degraded ? 1 : 0);
+    if (cfg_.min_link_speed_mbps > 0) {
+        metric("netop_agent_nic_speed_mbps", "gauge", "Negotiated link speed of the NIC (checked against --min-link-speed-gbps)");
+        for (const auto& n : nics_)
+            if (n.speed_mbps >= 0)
+                o += strfmt("netop_agent_nic_speed_mbps{nic=\"%s\"} %lld\n", httpd::escape_label(n.ifname).c_str(),
+                            (long long)n.speed_mbps);
+    }
     metric("netop_agent_link_flaps_total", "counter", "link losses observed after readiness");
     o += strfmt("netop_agent_link_flaps_total %d\n", flaps_);
     metric("netop_agent_reconfigurations_total", "counter", "NIC re-addressings after a Port Description change");
@@ -1459,6 +1487,16 @@ void Agent::run(int stop_fd) {
     }
     mark("flush");
 
+    if (cfg_.mode == "L2" && cfg_.configure && cfg_.min_link_speed_mbps > 0) {
+        // L3 checks each NIC as it configures it; L2 has no per-NIC step, so all at once here.
+        std::vector<std::string> slow;
+        for (auto& n : nics_)
+            if (std::string why = check_link_speed(n); !why.empty()) slow.push_back(n.ifname + ": " + why);
+        if (!slow.empty()) {
+            write_status();
+            throw AgentError(strfmt("%zu NIC(s) below the required link speed: ", slow.size()) + join(slow, "; "));
+        }
+    }
     if (cfg_.mode == "L3") {
         detect_lldp(stop_fd);
         mark("lldp");

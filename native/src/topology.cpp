@@ -191,6 +191,18 @@ std::optional<PciDev> netdev_pci(const std::string& root, const std::string& ifn
     return read_pci_dev(root, path_join(root, "class/net/" + ifname + "/device"));
 }
 
+int64_t netdev_speed_mbps(const std::string& root, const std::string& ifname) {
+    if (ifname.empty() || ifname.find('/') != std::string::npos) return -1;
+    auto s = read_file(path_join(root, "class/net/" + ifname + "/speed"));
+    if (!s) return -1;
+    try {
+        const long long v = std::stoll(trim(*s));
+        return v > 0 ? int64_t(v) : -1;  // the kernel reports -1 (SPEED_UNKNOWN) while down
+    } catch (const std::exception&) {
+        return -1;
+    }
+}
+
 std::vector<PciDev> rccl_pci_parents(const PciDev& d, std::map<std::string, PciDev>* cache) {
     std::vector<PciDev> out;
     auto pos = d.path.find("/devices/");

@@ -15,6 +15,7 @@
 #include "netop/agent.hpp"
 #include "netop/artifacts.hpp"
 #include "netop/common.hpp"
+#include "netop/topology.hpp"
 #include "tmpdir.hpp"
 
 using namespace netop;
@@ -1701,4 +1702,36 @@ TEST(agent_two_ports_describing_one_link_are_refused_and_named) {
         auto st = read_file(f.cfg.status_file);
         CHECK(st && st->find("the link of ens0 too") != std::string::npos);
     }
+}
+
+TEST(agent_min_link_speed_refuses_a_nic_that_came_up_slow) {
+    // ens1 negotiated 200G on a 400G fabric: left unconfigured (L3) and named; ens2 reports no
+    // speed (allowed, warned); L2 fails the start with the same reason.
+    for (const char* mode : {"L3", "L2"}) {
+        Fixture f;
+        f.cfg.mode = mode;
+        f.cfg.keep_running = false;
+        f.cfg.min_link_speed_mbps = 400000;
+        f.cfg.sysfs_root = f.tmp.path + "/sys";
+        f.tmp.write("sys/class/net/ens0/speed", "400000\n");
+        f.tmp.write("sys/class/net/ens1/speed", "200000\n");
+        agent::Agent a(f.cfg, f.ops, f.all_valid(), f.nm());
+        std::string err;
+        try {
+            a.run(-1);
+        } catch (const agent::AgentError& e) {
+            err = e.what();
+        }
+        const std::string why = "ens1: link negotiated at 200 Gb/s, below the required 400 Gb/s";
+        CHECK(err.find(why) != std::string::npos);
+        if (std::string(mode) == "L3") {
+            CHECK(err.find("Not all interfaces were configured (2/3).") != std::string::npos);
+            for (auto& x : f.ops.addrs) CHECK(x.ifindex != 11);
+        } else {
+            CHECK(err.find("1 NIC(s) below the required link speed") != std::string::npos);
+        }
+        auto st = read_file(f.cfg.status_file);
+        CHECK(st && st->find("\"speed_mbps\":200000") != std::string::npos);
+    }
+    CHECK_EQ(topo::netdev_speed_mbps("/nonexistent", "ens0"), -1);
 }

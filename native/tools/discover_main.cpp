@@ -80,6 +80,8 @@ int main(int argc, char** argv) {
     std::string node_lock = "auto";
     fs.add_string("node-lock", &node_lock, "node-wide lock (abstract unix socket) held while the agent runs, so agents configuring the same NICs never overlap (exiting vs starting agent, agent vs --cleanup, two policies on one node): auto (named after --nfd-label-file), none, or a name");
     fs.add_duration("node-lock-wait", &cfg.node_lock_wait_ns, "how long to wait for the node lock before failing");
+    int min_speed_gbps = 0;
+    fs.add_int("min-link-speed-gbps", &min_speed_gbps, "minimum negotiated link speed of every scale-out NIC (sysfs speed); a slower NIC is left unconfigured (L3) or fails the start (L2); 0 = off");
     fs.add_string("rail-switch-pattern", &cfg.rail_switch_pattern, "L3 rail cabling check: the NIC of GPU k must reach a switch whose LLDP System Name matches this ECMAScript regex with {rail} = k (e.g. 'leaf-r{rail}-.*'); a mismatch leaves the NIC unconfigured");
     fs.add_bool("dry-run", &cfg.dry_run, "discover, check xGMI / GPUDirect RDMA and write the topology file and status only: no link, address, NetworkManager or label change, no LLDP (needs no privileges)");
     fs.add_string("lldp-cache", &cfg.lldp_cache, "with --keep-running: remember each NIC's confirmed Port Description in this file and configure from it at start (the switch must confirm it within --lldp-cache-confirm)");
@@ -132,6 +134,11 @@ int main(int argc, char** argv) {
         cfg.node_lock = cfg.labels.file;
     else if (node_lock != "none")
         cfg.node_lock = node_lock;
+    if (min_speed_gbps < 0 || min_speed_gbps > 3200) {
+        std::fprintf(stderr, "Error: --min-link-speed-gbps must be 0 (off) or 1..3200\n");
+        return 2;
+    }
+    cfg.min_link_speed_mbps = int64_t(min_speed_gbps) * 1000;
     cfg.discovery.mode = *dm;
     cfg.token_policy = *tp;
     if (!nic_drivers.empty()) cfg.discovery.nic_drivers = split(nic_drivers, ',');

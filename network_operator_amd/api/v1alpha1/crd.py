@@ -128,6 +128,11 @@ def openapi_schema() -> dict:
                                "'leaf-r{rail}-.*' on a rail-optimized fabric.  A NIC on another rail's leaf is\n"
                                "left unconfigured and named in status.errors.",
                 "maxLength": 253, "type": "string"},
+            "minLinkSpeedGbps": {
+                "description": "Minimum negotiated link speed of every scale-out NIC in Gb/s (e.g. 400).  A NIC that\n"
+                               "came up slower (a marginal cable or optic, a port renegotiated down) is left\n"
+                               "unconfigured and named in status.errors.  0 = not checked.",
+                "minimum": 0, "maximum": 3200, "type": "integer"},
         },
     }
     host_nic = {

@@ -116,6 +116,8 @@ class AmdScaleOutSpec:
     keepConfigOnRestart: bool = False
     # L3 rail cabling check: regex over the LLDP System Name, "{rail}" = GPU index ("" = off)
     railSwitchPattern: str = ""
+    # Minimum negotiated link speed of every scale-out NIC, Gb/s (0 = off)
+    minLinkSpeedGbps: int = 0
     validation: Optional[ValidationSpec] = None
     extra: Dict[str, Any] = field(default_factory=dict)
 
@@ -126,7 +128,7 @@ class AmdScaleOutSpec:
     _FIELDS = ("disableNetworkManager", "layer", "image", "pullPolicy", "mtu", "xgmiCheck", "lldpAnnounce",
                "interfaces", "nicDrivers", "disableFirmwareLldp", "metricsPort", "gpuDirectRdma", "rcclEnv",
                "railTableBase", "rcclSocketIfname", "lldpCache", "verifyPeers", "lldpWait", "keepConfigOnRestart",
-               "railSwitchPattern", "validation")
+               "railSwitchPattern", "minLinkSpeedGbps", "validation")
 
     def to_dict(self) -> dict:
         d: dict = {}
@@ -168,6 +170,8 @@ class AmdScaleOutSpec:
             d["keepConfigOnRestart"] = True
         if self.railSwitchPattern:
             d["railSwitchPattern"] = self.railSwitchPattern
+        if self.minLinkSpeedGbps:
+            d["minLinkSpeedGbps"] = self.minLinkSpeedGbps
         if self.validation is not None:
             d["validation"] = self.validation.to_dict()
         d.update(copy.deepcopy(self.extra))
@@ -195,6 +199,7 @@ class AmdScaleOutSpec:
             lldpCache=bool(d.pop("lldpCache", False)),
             keepConfigOnRestart=bool(d.pop("keepConfigOnRestart", False)),
             railSwitchPattern=d.pop("railSwitchPattern", "") or "",
+            minLinkSpeedGbps=int(d.pop("minLinkSpeedGbps", 0) or 0),
             verifyPeers=bool(d.pop("verifyPeers", False)),
             lldpWait=d.pop("lldpWait", "") or "",
             validation=ValidationSpec.from_dict(d.pop("validation", None)),

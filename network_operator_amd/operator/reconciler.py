@@ -184,6 +184,8 @@ def agent_args(p: T.NetworkClusterPolicy) -> List[str]:
         args.append("--keep-config")
     if so.railSwitchPattern and so.layer == "L3":
         args.append(f"--rail-switch-pattern={so.railSwitchPattern}")
+    if so.minLinkSpeedGbps:
+        args.append(f"--min-link-speed-gbps={so.minLinkSpeedGbps}")
     if so.verifyPeers and so.layer == "L3":
         args.append(f"--verify-peers={VERIFY_PEERS_TIMEOUT}")
     if so.rcclEnv:

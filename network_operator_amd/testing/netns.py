@@ -312,7 +312,7 @@ def run_scenario(n_nics: int = 8, mode: str = "L3", seed: int | None = None, int
                  crash_restart: bool = False, crash_after_s: float = 0.0, gid_delay_s: float = 0.0,
                  egress_probe: bool = False, nm_bus: bool = False, nm_restore: bool = True, lldp_cache: bool = False,
                  soak_cycles: int = 0, arp_silent_ports: int = 0, switch_name: str = "",
-                 port_switch_names: dict | None = None) -> dict:
+                 port_switch_names: dict | None = None, nic_speeds_mbps: list | None = None) -> dict:
     """Runs one node bring-up.  Must already be inside a private user+net namespace.
 
     nm_bus: run the agent with --disable-networkmanager against a real ``dbus-daemon`` on which a
@@ -336,6 +336,8 @@ def run_scenario(n_nics: int = 8, mode: str = "L3", seed: int | None = None, int
         pairs = nat.discover(str(tmp / "sys"))["pairs"]
         nic_names = [p["nic"] for p in pairs][:n_nics]
         plan = random_plan(len(nic_names), rng)
+        for nif, mbps in zip(nic_names, nic_speeds_mbps or []):  # what the NIC driver negotiated
+            (tmp / "sys" / "class" / "net" / nif / "speed").write_text(f"{mbps}\n")
         for i, p in enumerate(plan):
             if i < bad_nics:
                 p["desc"] = "no-alert not-an-address"

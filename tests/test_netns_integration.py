@@ -355,3 +355,19 @@ def test_rail_cabling_check_names_a_nic_on_another_rails_leaf():
     assert err.startswith("Error: Not all interfaces were configured (3/4). Not configured: "
                           f"{nic}: rail 2 is cabled to switch 'leaf-r3' port 'swp2', not to one matching 'leaf-r2'"), err
     assert bad["state"][nic]["addrs"] == [] and all(bad["state"][n]["addrs"] for n in bad["nics"] if n != nic)
+
+
+def test_min_link_speed_names_a_nic_that_came_up_slow():
+    """minLinkSpeedGbps: on a 400G fabric one NIC negotiated 200G.  It is left unconfigured and
+    named, with its speed in status.json; at full speed the node is labelled."""
+    fast = netns.run_isolated(n_nics=4, seed=32, interval="1s", fast_start=True, nic_speeds_mbps=[400000] * 4,
+                              extra_args=["--min-link-speed-gbps=400"])
+    _check_configured(fast)
+    slow = netns.run_isolated(n_nics=4, seed=32, interval="1s", fast_start=True,
+                              nic_speeds_mbps=[400000, 200000, 400000, 400000], extra_args=["--min-link-speed-gbps=400"])
+    assert not slow["ready"] and slow["agent_rc"] == 1
+    nic = slow["nics"][1]
+    err = [ln for ln in slow["agent_log"].splitlines() if ln.startswith("Error: ")][-1]
+    assert f"Not configured: {nic}: link negotiated at 200 Gb/s, below the required 400 Gb/s" in err, err
+    st = {i["name"]: i for i in slow["status"]["interfaces"]}
+    assert st[nic]["speed_mbps"] == 200000 and st[slow["nics"][0]]["speed_mbps"] == 400000

@@ -999,3 +999,13 @@ def test_pod_informer_caches_only_what_the_operator_reads():
     assert len(json.dumps(s)) < len(json.dumps(pod)) / 2
     refused = {"status": {"phase": "Failed", "reason": "OutOfamd.com/gpu", "message": "no GPUs"}, "metadata": {"name": "j"}}
     assert job_not_admitted([slim_pod(refused)]) == job_not_admitted([refused])
+
+
+def test_min_link_speed_passed_in_both_layers():
+    from network_operator_amd.api.v1alpha1 import crd as CRD
+
+    for layer in ("L2", "L3"):
+        assert "--min-link-speed-gbps=400" in agent_args(T.new_policy("p", layer=layer, minLinkSpeedGbps=400))
+    assert not any("min-link-speed" in a for a in agent_args(T.new_policy("p")))
+    bad = policy(minLinkSpeedGbps=5000)
+    assert any("less than or equal to 3200" in e for e in CRD.validate(bad))
