@@ -152,6 +152,10 @@ struct Config {
     // fails the start (L2), named in the error; a speed the driver does not report is allowed
     // with a warning.  0 = off.
     int64_t min_link_speed_mbps = 0;
+    // Refuse a NIC whose switch port advertises (LLDP 802.3 Maximum Frame Size TLV) a maximum
+    // frame smaller than the NIC's MTU plus its Ethernet header: jumbo RoCE frames would be
+    // dropped by the switch, which shows as hung or crawling RCCL jobs rather than as an error.
+    bool check_peer_mtu = true;
     int64_t node_lock_wait_ns = 60LL * 1000000000;
 };
 

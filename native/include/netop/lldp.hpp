@@ -95,6 +95,11 @@ struct Frame {
     std::optional<MacAddr> peer_mac() const;
     std::string chassis_id_str() const;  // MAC → "aa:bb:..", textual subtypes verbatim
     std::string port_id_str() const;
+    // IEEE 802.3 organizationally specific TLV "Maximum Frame Size" (OUI 00-12-0F, subtype 4):
+    // the largest frame the switch port accepts, Ethernet header and FCS included (1518 for a
+    // 1500-byte MTU, e.g. 9216 on a jumbo port).  nullopt when the switch does not send it.
+    std::optional<uint16_t> max_frame_size() const;
+    void set_max_frame_size(uint16_t bytes);
 };
 
 enum class DecodeError {

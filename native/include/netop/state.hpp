@@ -50,7 +50,8 @@ struct NicState {
 
     // Topology
     int gpu_index = -1;
-    int64_t speed_mbps = -1;  // negotiated link speed when checked (--min-link-speed-gbps), -1 unknown
+    int64_t speed_mbps = -1;
+    int peer_max_frame = -1;  // the switch port's LLDP 802.3 Maximum Frame Size, -1 when not sent  // negotiated link speed when checked (--min-link-speed-gbps), -1 unknown
     std::string gpu_bdf;
     std::string rdma_dev;
     int rdma_port = 1;

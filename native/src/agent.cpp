@@ -578,6 +578,13 @@ bool Agent::configure_interface(NicState& n) {
         NLOG_W("Interface '%s' not configured: %s", n.ifname.c_str(), n.config_error.c_str());
         return false;
     }
+    if (cfg_.check_peer_mtu && n.peer_max_frame > 0 && n.peer_max_frame < cfg_.mtu + 14) {
+        n.config_error = strfmt("its switch port accepts frames up to %d bytes, but MTU %d needs %d: jumbo RoCE frames "
+                                "would be dropped (raise the switch port's MTU, or lower the policy's mtu)",
+                                n.peer_max_frame, cfg_.mtu, cfg_.mtu + 14);
+        NLOG_W("Interface '%s' not configured: %s", n.ifname.c_str(), n.config_error.c_str());
+        return false;
+    }
     if (std::string why = check_link_speed(n); !why.empty()) {
         n.config_error = why;
         NLOG_W("Interface '%s' not configured: %s", n.ifname.c_str(), n.config_error.c_str());
@@ -646,6 +653,7 @@ void Agent::on_lldp(NicState& n, const lldp::Frame& f) {
     n.peer_mac = f.peer_mac();
     n.peer_system_name = f.system_name.value_or("");
     n.peer_port_id = f.port_id_str();
+    n.peer_max_frame = f.max_frame_size() ? int(*f.max_frame_size()) : -1;
     std::string err;
     n.addr = l3::parse_port_description(n.port_description, cfg_.token_policy, &err);
     if (!n.addr) {
@@ -658,6 +666,7 @@ void Agent::on_lldp(NicState& n, const lldp::Frame& f) {
 
 bool Agent::refresh_from_frame(NicState& n, const lldp::Frame& f) {
     std::string desc = f.port_description.value_or("");
+    n.peer_max_frame = f.max_frame_size() ? int(*f.max_frame_size()) : -1;  // checked at the next (re)configuration
     bool changed = false;
     if (n.lldp_from_cache) {
         n.lldp_from_cache = false;

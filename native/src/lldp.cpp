@@ -1,5 +1,7 @@
 #include "netop/lldp.hpp"
 
+#include <algorithm>
+
 namespace netop::lldp {
 
 const MacAddr kNearestBridge{{0x01, 0x80, 0xc2, 0x00, 0x00, 0x0e}};
@@ -262,6 +264,23 @@ std::vector<uint8_t> encode(const Frame& f) {
     out.push_back(0);
     if (out.size() < 60) out.resize(60, 0);
     return out;
+}
+
+constexpr uint32_t kOui8023 = 0x00120F;
+constexpr uint8_t kMaxFrameSizeSubtype = 4;
+
+std::optional<uint16_t> Frame::max_frame_size() const {
+    for (const auto& o : org)
+        if (o.oui == kOui8023 && o.subtype == kMaxFrameSizeSubtype && o.info.size() == 2)
+            return uint16_t((uint8_t(o.info[0]) << 8) | uint8_t(o.info[1]));
+    return std::nullopt;
+}
+
+void Frame::set_max_frame_size(uint16_t bytes) {
+    org.erase(std::remove_if(org.begin(), org.end(),
+                             [](const OrgTlv& o) { return o.oui == kOui8023 && o.subtype == kMaxFrameSizeSubtype; }),
+              org.end());
+    org.push_back(OrgTlv{kOui8023, kMaxFrameSizeSubtype, std::string{char(bytes >> 8), char(bytes & 0xff)}});
 }
 
 Frame make_switch_frame(const MacAddr& switch_port_mac, const std::string& system_name, const std::string& port_name,

@@ -1735,3 +1735,52 @@ TEST(agent_min_link_speed_refuses_a_nic_that_came_up_slow) {
     }
     CHECK_EQ(topo::netdev_speed_mbps("/nonexistent", "ens0"), -1);
 }
+
+TEST(lldp_max_frame_size_tlv_roundtrip) {
+    auto f = lldp::make_switch_frame(*MacAddr::parse("02:aa:00:00:00:01"), "tor", "p1", "no-alert 10.200.0.6/30");
+    CHECK(!f.max_frame_size());
+    f.set_max_frame_size(9216);
+    f.set_max_frame_size(1518);  // replaces, never duplicates
+    auto bytes = lldp::encode(f);
+    auto d = lldp::decode(bytes.data(), bytes.size());
+    CHECK(d && d->max_frame_size() && *d->max_frame_size() == 1518);
+    CHECK(d && d->org.size() == 1);
+}
+
+TEST(agent_switch_port_with_a_smaller_max_frame_than_the_mtu_is_refused) {
+    // MTU 9000: ens1's switch port still accepts only 1518-byte frames (jumbo not enabled on
+    // it) -> refused and named; 9216 and "not advertised" pass.  At MTU 1500, 1518 is enough.
+    for (int mtu : {9000, 1500}) {
+        Fixture f;
+        f.cfg.keep_running = false;
+        f.cfg.mtu = mtu;
+        auto src = f.all_valid();
+        src->frames["ens0"].set_max_frame_size(9216);
+        src->frames["ens1"].set_max_frame_size(1518);
+        agent::Agent a(f.cfg, f.ops, std::move(src), f.nm());
+        std::string err;
+        try {
+            a.run(-1);
+        } catch (const agent::AgentError& e) {
+            err = e.what();
+        }
+        if (mtu == 9000) {
+            CHECK(err.find("Not configured: ens1: its switch port accepts frames up to 1518 bytes, but MTU 9000 needs "
+                           "9014") != std::string::npos);
+            auto st = read_file(f.cfg.status_file);
+            CHECK(st && st->find("\"peer_max_frame\":1518") != std::string::npos);
+        } else {
+            CHECK(err.empty());
+            CHECK_EQ(f.ops.addrs.size(), size_t(3));
+        }
+    }
+    Fixture g;  // the check can be turned off
+    g.cfg.keep_running = false;
+    g.cfg.mtu = 9000;
+    g.cfg.check_peer_mtu = false;
+    auto src = g.all_valid();
+    src->frames["ens1"].set_max_frame_size(1518);
+    agent::Agent b(g.cfg, g.ops, std::move(src), g.nm());
+    b.run(-1);
+    CHECK_EQ(g.ops.addrs.size(), size_t(3));
+}

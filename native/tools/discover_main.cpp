@@ -80,6 +80,7 @@ int main(int argc, char** argv) {
     std::string node_lock = "auto";
     fs.add_string("node-lock", &node_lock, "node-wide lock (abstract unix socket) held while the agent runs, so agents configuring the same NICs never overlap (exiting vs starting agent, agent vs --cleanup, two policies on one node): auto (named after --nfd-label-file), none, or a name");
     fs.add_duration("node-lock-wait", &cfg.node_lock_wait_ns, "how long to wait for the node lock before failing");
+    fs.add_bool("check-peer-mtu", &cfg.check_peer_mtu, "refuse a NIC whose switch port advertises (LLDP 802.3 Maximum Frame Size) frames smaller than its MTU needs");
     int min_speed_gbps = 0;
     fs.add_int("min-link-speed-gbps", &min_speed_gbps, "minimum negotiated link speed of every scale-out NIC (sysfs speed); a slower NIC is left unconfigured (L3) or fails the start (L2); 0 = off");
     fs.add_string("rail-switch-pattern", &cfg.rail_switch_pattern, "L3 rail cabling check: the NIC of GPU k must reach a switch whose LLDP System Name matches this ECMAScript regex with {rail} = k (e.g. 'leaf-r{rail}-.*'); a mismatch leaves the NIC unconfigured");

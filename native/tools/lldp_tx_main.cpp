@@ -66,6 +66,8 @@ int main(int argc, char** argv) {
         port_sysname[v.substr(0, eq)] = v.substr(eq + 1);
     }, "IFNAME=NAME: this port's System Name (repeatable)");
     fs.add_int("ttl", &ttl, "TTL TLV");
+    int max_frame = 0;
+    fs.add_int("max-frame-size", &max_frame, "IEEE 802.3 Maximum Frame Size TLV (bytes; 0 = not sent)");
     fs.add_bool("assign-ip", &assign_ip, "assign the Port Description address to the switch port");
     fs.add_int("seed", &seed, "RNG seed for the random phase (0 = time based)");
     fs.add_int("v", &verbosity, "log verbosity");
@@ -118,7 +120,9 @@ int main(int argc, char** argv) {
             while (idx < ports.size() && ports[idx].first != ifname) ++idx;
             name.replace(at, 6, std::to_string(idx));
         }
-        p.frame = lldp::encode(lldp::make_switch_frame(link.mac, name, ifname, desc, uint16_t(ttl)));
+        auto frame = lldp::make_switch_frame(link.mac, name, ifname, desc, uint16_t(ttl));
+        if (max_frame > 0) frame.set_max_frame_size(uint16_t(max_frame));
+        p.frame = lldp::encode(frame);
         p.neighbours.clear();
     };
     try {

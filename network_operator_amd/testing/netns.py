@@ -210,7 +210,7 @@ class SyntheticSwitch:
 
     def __init__(self, nic_names: list, plan: list, rng: random.Random, interval: str = "30s", phase: str = "random",
                  fast_start: bool = True, silent_nics: int = 0, remote: Optional[list] = None, forward: bool = False,
-                 system_name: str = "", port_system_names: Optional[dict] = None):
+                 system_name: str = "", port_system_names: Optional[dict] = None, max_frame_size: int = 0):
         """`remote`: (network-namespace pid, ifname) of NICs of other nodes, wired to the ports after
         this namespace's `nic_names` (`plan` covers both).  `forward`: the switch routes between its
         /30s (a leaf of an L3 fabric), so nodes reach each other over their /16 routes."""
@@ -224,6 +224,8 @@ class SyntheticSwitch:
                      f"--seed={rng.randrange(1, 1 << 30)}"]
         if fast_start:
             self.args.append("--fast-start")
+        if max_frame_size:  # LLDP 802.3 Maximum Frame Size TLV (the switch ports' MTU)
+            self.args.append(f"--max-frame-size={max_frame_size}")
         if system_name:  # "{port}": one leaf per rail
             self.args.append(f"--system-name={system_name}")
         for sp, name in (port_system_names or {}).items():
@@ -312,7 +314,8 @@ def run_scenario(n_nics: int = 8, mode: str = "L3", seed: int | None = None, int
                  crash_restart: bool = False, crash_after_s: float = 0.0, gid_delay_s: float = 0.0,
                  egress_probe: bool = False, nm_bus: bool = False, nm_restore: bool = True, lldp_cache: bool = False,
                  soak_cycles: int = 0, arp_silent_ports: int = 0, switch_name: str = "",
-                 port_switch_names: dict | None = None, nic_speeds_mbps: list | None = None) -> dict:
+                 port_switch_names: dict | None = None, nic_speeds_mbps: list | None = None,
+                 switch_max_frame: int = 0) -> dict:
     """Runs one node bring-up.  Must already be inside a private user+net namespace.
 
     nm_bus: run the agent with --disable-networkmanager against a real ``dbus-daemon`` on which a
@@ -363,7 +366,8 @@ def run_scenario(n_nics: int = 8, mode: str = "L3", seed: int | None = None, int
             add_gids()
 
         sw = SyntheticSwitch(nic_names, plan, rng, interval=interval, phase=phase, fast_start=fast_start,
-                             silent_nics=silent_nics, system_name=switch_name, port_system_names=port_switch_names)
+                             silent_nics=silent_nics, system_name=switch_name, port_system_names=port_switch_names,
+                             max_frame_size=switch_max_frame)
         t_switch = sw.start(rt)
         pid, sw_ports, first_periodic = sw.pid, sw.ports, sw.first_periodic
         for sp in sw_ports[len(sw_ports) - arp_silent_ports:] if arp_silent_ports else []:

@@ -371,3 +371,17 @@ def test_min_link_speed_names_a_nic_that_came_up_slow():
     assert f"Not configured: {nic}: link negotiated at 200 Gb/s, below the required 400 Gb/s" in err, err
     st = {i["name"]: i for i in slow["status"]["interfaces"]}
     assert st[nic]["speed_mbps"] == 200000 and st[slow["nics"][0]]["speed_mbps"] == 400000
+
+
+def test_switch_without_jumbo_frames_is_caught_before_jobs_hang():
+    """The switch ports advertise (LLDP 802.3 Maximum Frame Size) 1518-byte frames while the
+    policy asks for MTU 9000: jumbo RoCE frames would be dropped.  Every NIC is refused with the
+    numbers; with 9216-byte ports the node comes up."""
+    ok = netns.run_isolated(n_nics=2, seed=33, interval="1s", fast_start=True, mtu=9000, switch_max_frame=9216)
+    _check_configured(ok)
+    assert all(i["peer_max_frame"] == 9216 for i in ok["status"]["interfaces"])
+    bad = netns.run_isolated(n_nics=2, seed=33, interval="1s", fast_start=True, mtu=9000, switch_max_frame=1518)
+    assert not bad["ready"] and bad["agent_rc"] == 1
+    err = [ln for ln in bad["agent_log"].splitlines() if ln.startswith("Error: ")][-1]
+    assert err.startswith("Error: Not all interfaces were configured (0/2). Not configured: "), err
+    assert "its switch port accepts frames up to 1518 bytes, but MTU 9000 needs 9014" in err
