@@ -34,6 +34,7 @@ extern "C" int LLVMFuzzerTestOneInput(const uint8_t* data, size_t size) {
         auto bytes = lldp::encode(*f);
         auto again = lldp::decode(bytes.data(), bytes.size());
         if (!again || again->port_description != f->port_description || again->ttl != f->ttl) __builtin_trap();
+        if (again->max_frame_size() != f->max_frame_size()) __builtin_trap();  // 802.3 org TLV survives
     }
 #elif NETOP_FUZZ_TARGET == 2
     dbus::Message m;

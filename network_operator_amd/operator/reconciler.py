@@ -362,7 +362,7 @@ def _set_condition(conds: List[dict], type_: str, status: str, reason: str, mess
                   "reason": reason, "message": message})
 
 
-def agent_exit_reason(pod: dict, limit: int = 300) -> Optional[str]:
+def agent_exit_reason(pod: dict, limit: int = 1500) -> Optional[str]:
     """Why the agent container last exited, from the Pod's container status: the agent's own
     one-line "Error: ..." from the termination message (the DaemonSet sets
     FallbackToLogsOnError, so that is the log tail of a failed start), else the exit code."""
