@@ -1423,7 +1423,13 @@ void Agent::run(int stop_fd) {
     }
 
     auto names = collect_interfaces();
-    if (names.empty()) throw AgentError("No interfaces found");
+    if (names.empty()) {
+        // A dry run still describes the GPUs and their xGMI mesh (the intra-node topology file a
+        // job on a node without scale-out NICs uses); configuring needs NICs.
+        if (!cfg_.dry_run || disc_.gpus.empty()) throw AgentError("No interfaces found");
+        NLOG_W("dry run: no scale-out interfaces found; describing the %zu GPU(s) and the xGMI mesh only",
+               disc_.gpus.size());
+    }
     get_network_configs(names);
     if (nics_.size() < names.size()) {
         if (!cfg_.dry_run) throw AgentError("Not all interfaces were found in the system");

@@ -447,3 +447,22 @@ def test_bench_reports_an_agent_that_cannot_run(tmp_path):
     a = j["agent_artifacts"]
     assert a["applied"] is False and "No interfaces found" in a["error"] and a["ranks_applied"] == 0
     assert j["value"] > 0 and j["verified"] is True
+
+
+def test_bench_applies_gpu_only_artifacts_on_a_node_without_scale_out_nics(tmp_path, node_sysfs):
+    """A node whose GPUs have no scale-out NIC (a compute-only node in the driver's pool): the
+    agent's dry run still writes the GPU / xGMI topology file and an intra-node rccl.env, so the
+    measurement runs with the agent's artifacts instead of failing the strict check."""
+    import shutil
+
+    sysfs = tmp_path / "sys"
+    shutil.copytree(node_sysfs, sysfs, symlinks=True)
+    for d in (sysfs / "class" / "net").iterdir():
+        shutil.rmtree(d) if d.is_dir() and not d.is_symlink() else d.unlink()
+    cmd = [sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1", "--device", "cpu",
+           "--bytes", str(1 << 16), "--sweep", "", "--collectives", "", "--node-ready", "off", "--rccl-defaults", "0",
+           "--sysfs-root", str(sysfs) + "/"]
+    j = _bench_line(subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=tmp_path, env=_spawn_env()))
+    a = j["agent_artifacts"]
+    assert a["applied"] is True and a["ranks_applied"] == 2, a
+    assert a["agent_status"]["xgmi_pairs"] == "28/28" and a["topo_file_bytes"] > 1000
