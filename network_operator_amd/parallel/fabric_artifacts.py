@@ -242,6 +242,7 @@ def dump_verdict(n: int, with_file: Optional[dict], defaults: Optional[dict]) ->
       holds all n GPUs), and the file did not cost a link RCCL sees without it.
     * ``failed`` — fewer, while RCCL without the file sees more (the file lost links), or the
       dump is missing / shows fewer than n-1 with xGMI elements present.
+    * ``degraded`` — fewer than n-1, but the same without the file: the node's mesh, not the file.
     * ``unverifiable`` — RCCL's dump carries no ``<xgmi>`` elements with *or* without the file
       (this RCCL build records the links elsewhere): the file cannot be blamed, say so.
     """
@@ -266,4 +267,9 @@ def dump_verdict(n: int, with_file: Optional[dict], defaults: Optional[dict]) ->
         return dict(out, status="unverifiable",
                     why="RCCL's topology dump has no <xgmi> elements with the agent's file, and "
                         + ("none without it either" if base is not None else "no dump without it to compare"))
+    if base is not None and base == got:
+        # RCCL sees the same deficit without the file: the node's mesh (or how this RCCL build
+        # records it), not the agent's artifacts.  Reported, not blamed on the file.
+        return dict(out, status="degraded",
+                    why=f"RCCL sees {got} xGMI peers per GPU (min) of {need}, with and without the agent's file")
     return dict(out, status="failed", why=f"RCCL sees {got} xGMI peers per GPU (min), {need} expected")

@@ -466,3 +466,13 @@ def test_bench_applies_gpu_only_artifacts_on_a_node_without_scale_out_nics(tmp_p
     a = j["agent_artifacts"]
     assert a["applied"] is True and a["ranks_applied"] == 2, a
     assert a["agent_status"]["xgmi_pairs"] == "28/28" and a["topo_file_bytes"] > 1000
+
+
+def test_link_deficit_seen_without_the_file_too_is_not_blamed_on_it():
+    from network_operator_amd.parallel import fabric_artifacts as FA
+
+    view = {"gpus": 8, "xgmi_elements": 48, "min_xgmi_links": 6}
+    v = FA.dump_verdict(8, view, dict(view))
+    assert v["status"] == "degraded" and "with and without the agent's file" in v["why"]
+    assert FA.dump_verdict(8, view, dict(view, min_xgmi_links=7))["status"] == "failed"  # the file costs a link
+    assert FA.dump_verdict(8, dict(view, min_xgmi_links=7), dict(view, min_xgmi_links=7))["status"] == "ok"
