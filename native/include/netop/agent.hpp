@@ -159,6 +159,10 @@ struct Config {
     int64_t node_lock_wait_ns = 60LL * 1000000000;
 };
 
+// Where the agent leaves the one-line reason the node is not ready (beside --status-file), and
+// what `discover --ready-check --status-file=...` prints when it fails.
+std::string reason_path(const std::string& status_file);
+
 // FRA_PROTOCOL / rtm_protocol tag on the agent's rail rules and rail-table routes ("installed by
 // the AMD network operator"): cleanup only ever removes rules and routes carrying it.
 constexpr uint8_t kRailProtocol = 0xa3;
@@ -249,7 +253,8 @@ class Agent {
     void detect_lldp(int stop_fd);
     void diagnose_silent();            // after --wait expired: why each silent NIC heard nothing
     std::string check_link_speed(NicState& n);  // "" or why n is below --min-link-speed-gbps
-    std::string silent_summary() const;  // "" or "LLDP silent on k NIC(s): ... Not configured: ..." for the exit error
+    std::string silent_summary() const;
+    std::string not_ready_reason() const;  // per NIC, for the readiness probe ("" when none known)  // "" or "LLDP silent on k NIC(s): ... Not configured: ..." for the exit error
     void on_lldp(NicState& n, const lldp::Frame& f);
     void add_route(NicState& n, int mask);
     uint32_t rail_table(const NicState& n) const;

@@ -1384,9 +1384,41 @@ void Agent::write_status() {
     if (cfg_.status_file.empty()) return;
     try {
         write_file_atomic(cfg_.status_file, artifacts::generate_status(nics_, phases_, t0_, cfg_.mode, ready_, status_node()) + "\n");
+        // Beside it, one line for the readiness probe to print while the node is not ready: the
+        // kubelet records probe output in the Pod's events ("Readiness probe failed: ...").
+        const std::string why = ready_ ? "" : not_ready_reason();
+        if (why.empty())
+            ::unlink(reason_path(cfg_.status_file).c_str());
+        else
+            write_file_atomic(reason_path(cfg_.status_file), why + "\n");
     } catch (const std::exception& e) {
         NLOG_W("Could not write status file: %s", e.what());
     }
+}
+
+std::string reason_path(const std::string& status_file) { return status_file + ".not-ready"; }
+
+std::string Agent::not_ready_reason() const {
+    std::vector<std::string> parts;
+    for (const auto& n : nics_) {
+        std::string why;
+        if (n.degraded)
+            why = "link down";
+        else if (!n.lldp_silent.empty())
+            why = n.lldp_silent;
+        else if (!n.config_error.empty())
+            why = n.config_error;
+        else if (!n.addr_error.empty() && !n.configured)
+            why = n.addr_error;
+        else if (n.cache_stale)
+            why = "the switch has not confirmed the cached Port Description";
+        else if (!n.peer_error.empty())
+            why = n.peer_error;
+        else if (cfg_.mode == "L3" && !n.configured)
+            why = n.lldp_seen ? "not configured yet" : "waiting for LLDP";
+        if (!why.empty()) parts.push_back(n.ifname + ": " + why);
+    }
+    return join(parts, "; ");
 }
 
 void Agent::run(int stop_fd) {

@@ -651,10 +651,13 @@ TEST(agent_monitor_link_failure_withdraws_and_restores_label) {
             f.ops.events.push_back({false, l});
         } else if (tick == 3) {
             saw_withdrawn = !path_exists(f.cfg.labels.path());
+            // what the readiness probe prints (the kubelet puts it in the Pod's events)
+            auto why = read_file(agent::reason_path(f.cfg.status_file));
+            saw_withdrawn &= why && *why == "ens2: link down\n";
             l.flags |= IFF_UP;
             f.ops.events.push_back({false, l});
         } else if (tick == 5) {
-            saw_restored = path_exists(f.cfg.labels.path());
+            saw_restored = path_exists(f.cfg.labels.path()) && !path_exists(agent::reason_path(f.cfg.status_file));
             stop.fire();
         }
     };

@@ -111,7 +111,16 @@ int main(int argc, char** argv) {
         std::cout << "Discover and optionally configure network devices\n\n" << fs.usage();
         return 0;
     }
-    if (ready_check) return path_exists(cfg.labels.path()) ? 0 : 1;
+    if (ready_check) {
+        if (path_exists(cfg.labels.path())) return 0;
+        // The kubelet keeps a failing probe's output in the Pod's events: say why.
+        std::optional<std::string> why;
+        if (!cfg.status_file.empty()) why = read_file(agent::reason_path(cfg.status_file));
+        std::string line = why ? trim(*why) : "readiness label " + cfg.labels.path() + " not published";
+        if (line.size() > 900) line = line.substr(0, 900) + " ...";
+        std::printf("not ready: %s\n", line.c_str());
+        return 1;
+    }
     if (show_version) {
         std::cout << "discover (amd network operator) " << NETOP_VERSION << "\n";
         return 0;

@@ -34,6 +34,10 @@ AGENT_SERVICE_ACCOUNT = "linkdiscovery-sa"
 OPENSHIFT_PRIVILEGED_SCC = "system:openshift:scc:privileged"
 
 LABEL_FEATURES_DIR = "/etc/kubernetes/node-feature-discovery/features.d/"
+# The agent's status file, in a per-Pod emptyDir: the readiness probe prints the reason the node
+# is not ready from beside it, and the kubelet keeps that output in the Pod's events.
+AGENT_RUN_DIR = "/run/amd-network-agent"
+AGENT_STATUS_FILE = AGENT_RUN_DIR + "/status.json"
 
 AGENT_REQUESTS = {"cpu": "40m", "memory": "45Mi"}
 AGENT_LIMITS = {"cpu": "500m", "memory": "90Mi"}
@@ -53,10 +57,11 @@ def _agent_container() -> Dict:
         # NODE_NAME names the node in the agent's status file and logs (unused by the reference).
         "env": [{"name": "NODE_NAME",
                  "valueFrom": {"fieldRef": {"apiVersion": "v1", "fieldPath": "spec.nodeName"}}}],
-        "readinessProbe": {"exec": {"command": [AGENT_BINARY, "--ready-check"]},
+        "readinessProbe": {"exec": {"command": [AGENT_BINARY, "--ready-check", f"--status-file={AGENT_STATUS_FILE}"]},
                            "initialDelaySeconds": 1, "periodSeconds": 5, "failureThreshold": 1},
         "resources": {"limits": dict(AGENT_LIMITS), "requests": dict(AGENT_REQUESTS)},
-        "volumeMounts": [{"mountPath": LABEL_FEATURES_DIR, "name": "nfd-features"}],
+        "volumeMounts": [{"mountPath": LABEL_FEATURES_DIR, "name": "nfd-features"},
+                         {"mountPath": AGENT_RUN_DIR, "name": "agent-run"}],
         # A failed start ends with the agent's one-line "Error: ..." on stderr; with this policy the
         # kubelet keeps the log tail as the container's termination message, and the operator
         # quotes it in the policy's status.errors (not in the reference).
@@ -82,7 +87,8 @@ def discovery_daemonset() -> Dict:
                 "metadata": {"labels": dict(labels)},
                 "spec": {
                     "hostNetwork": True,
-                    "volumes": [_host_dir("nfd-features", LABEL_FEATURES_DIR)],
+                    "volumes": [_host_dir("nfd-features", LABEL_FEATURES_DIR),
+                                {"name": "agent-run", "emptyDir": {"medium": "Memory", "sizeLimit": "1Mi"}}],
                     "containers": [_agent_container()],
                     "terminationGracePeriodSeconds": TERMINATION_GRACE_S,
                 },

@@ -186,6 +186,7 @@ def agent_args(p: T.NetworkClusterPolicy) -> List[str]:
         args.append(f"--rail-switch-pattern={so.railSwitchPattern}")
     if so.minLinkSpeedGbps:
         args.append(f"--min-link-speed-gbps={so.minLinkSpeedGbps}")
+    args.append(f"--status-file={discovery.AGENT_STATUS_FILE}")
     if so.verifyPeers and so.layer == "L3":
         args.append(f"--verify-peers={VERIFY_PEERS_TIMEOUT}")
     if so.rcclEnv:
@@ -228,7 +229,7 @@ def update_amd_scale_out_daemonset(ds: dict, p: T.NetworkClusterPolicy, namespac
         pod.pop("initContainers", None)
     probe = c.get("readinessProbe", {}).get("exec")
     if probe:
-        probe["command"] = probe["command"][:1] + ["--ready-check"]
+        probe["command"] = probe["command"][:1] + ["--ready-check", f"--status-file={discovery.AGENT_STATUS_FILE}"]
     # Agent metrics port (hostNetwork: the container port is the node port).
     ports = [x for x in c.get("ports", []) if x.get("name") != "metrics"]
     if so.metricsPort:
@@ -271,6 +272,7 @@ def host_nic_agent_args(p: T.NetworkClusterPolicy) -> List[str]:
         if hn.layer == "L3":  # its own cache beside the scale-out agent's
             args.append(f"--lldp-cache={ARTIFACT_DIR_CONTAINER}/{HOST_NIC_LLDP_CACHE_FILE}")
         args.append("--keep-config")
+    args.append(f"--status-file={discovery.AGENT_STATUS_FILE}")
     return args
 
 
@@ -318,7 +320,8 @@ def update_host_nic_daemonset(ds: dict, p: T.NetworkClusterPolicy, namespace: st
     order_managed_volumes(ds)
     probe = c.get("readinessProbe", {}).get("exec")
     if probe:
-        probe["command"] = [probe["command"][0], "--ready-check", f"--nfd-label-file={HOST_NIC_LABEL_FILE}"]
+        probe["command"] = [probe["command"][0], "--ready-check", f"--nfd-label-file={HOST_NIC_LABEL_FILE}",
+                            f"--status-file={discovery.AGENT_STATUS_FILE}"]
     c["args"] = host_nic_agent_args(p)
 
 

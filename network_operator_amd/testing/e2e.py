@@ -32,6 +32,7 @@ import json
 import os
 import random
 import shutil
+import subprocess
 import sys
 import tempfile
 import time
@@ -466,6 +467,10 @@ async def _scenario(tmp: Path, n_nics: int, mode: str, seed: int, interval: str,
 
                 t_deg = await _until(degraded, 10)
                 res["flap_status"] = (fake.get_object(P, name) or {}).get("status")
+                # The readiness probe's output, which the kubelet puts in the Pod's events.
+                c0 = next(iter(node.containers.values()))
+                pr = subprocess.run(c0.probe, capture_output=True, text=True, timeout=10)
+                res["probe_while_degraded"] = {"rc": pr.returncode, "stdout": pr.stdout.strip()}
                 t2 = time.monotonic()
                 netns.set_switch_port(sw.pid, sw.ports[0], True)
                 t_back = await _until(lambda: node.node_labels().get(label_key) == "true" and all_good(), 10)

@@ -108,9 +108,12 @@ class SimNode:
         return self.host_root / path.lstrip("/")
 
     @staticmethod
-    def _mounts(pod_spec: dict, container: dict) -> List[Tuple[str, str]]:
-        """(mountPath, hostPath) of the container's hostPath mounts, longest mountPath first."""
+    def _mounts(pod_spec: dict, container: dict, pod: str = "") -> List[Tuple[str, str]]:
+        """(mountPath, host path) of the container's hostPath mounts, and of its emptyDir mounts
+        (a per-Pod directory, as the kubelet's), longest mountPath first."""
         vols = {v["name"]: v["hostPath"]["path"] for v in pod_spec.get("volumes") or [] if "hostPath" in v}
+        vols.update({v["name"]: f"/var/lib/kubelet/pods/{pod or 'pod'}/volumes/{v['name']}"
+                     for v in pod_spec.get("volumes") or [] if "emptyDir" in v})
         out = [(m["mountPath"].rstrip("/") or "/", vols[m["name"]]) for m in container.get("volumeMounts") or []
                if m.get("name") in vols]
         return sorted(out, key=lambda x: -len(x[0]))
@@ -149,7 +152,7 @@ class SimNode:
             return None
         spec = ds["spec"]["template"]["spec"]
         c = spec["containers"][0]
-        mounts = self._mounts(spec, c)
+        mounts = self._mounts(spec, c, pname)
         for _, hp in mounts:  # hostPath type DirectoryOrCreate
             self.host_path(hp).mkdir(parents=True, exist_ok=True)
         env = {}
@@ -297,7 +300,7 @@ class SimNode:
         ns, name = job["metadata"].get("namespace", ""), job["metadata"]["name"]
         spec = job["spec"]["template"]["spec"]
         c = spec["containers"][0]
-        mounts = self._mounts(spec, c)
+        mounts = self._mounts(spec, c, name)
         for _, hp in mounts:
             self.host_path(hp).mkdir(parents=True, exist_ok=True)
         cmd = self.job_images.get(c.get("image", ""))

@@ -134,6 +134,8 @@ def test_link_failure_is_reported_by_the_policy_and_recovers():
     assert st["errors"] == ["mi355x-0: scale-out not ready (ContainersNotReady)"]
     assert any(c["type"] == "Degraded" and c["status"] == "True" for c in st["conditions"])
     assert r["port_up_to_all_good_s"] is not None, r["agent_log"]
+    # kubectl describe pod: "Readiness probe failed: not ready: <nic>: link down"
+    assert r["probe_while_degraded"] == {"rc": 1, "stdout": f"not ready: {r['nics'][0]}: link down"}
 
 
 def test_silent_switch_port_reaches_the_policy_status():

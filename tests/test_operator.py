@@ -20,6 +20,7 @@ from network_operator_amd.operator.reconciler import agent_args
 from network_operator_amd.testing.fakeapi import FakeApiServer
 
 TOPO_ARGS = ["--rccl-topo=/host/etc/amd/scale-out/rccl-topo.xml", "--rccl-topo-env-path=/etc/amd/scale-out/rccl-topo.xml"]
+STATUS_ARG = "--status-file=/run/amd-network-agent/status.json"  # the probe prints why a node is not ready
 
 NS = "amd-network-operator"
 
@@ -112,9 +113,9 @@ def test_reconcile_lifecycle_reference_parity():
                 assert len(c) == 1 and c[0]["image"] == "amd/my-linkdiscovery:latest"
                 assert c[0]["args"] == ["--configure=true", "--keep-running", "--mode=L3", "--mtu=8000", "--wait=90s",
                                         "--rccl-net=/host/etc/amd/scale-out/rccl-net.json",
-                                        "--rccl-env=/host/etc/amd/scale-out/rccl.env", *TOPO_ARGS]
-                assert [v["name"] for v in pod["volumes"]] == ["nfd-features", "rccl-artifacts"]
-                assert [m["name"] for m in c[0]["volumeMounts"]] == ["nfd-features", "rccl-artifacts"]
+                                        "--rccl-env=/host/etc/amd/scale-out/rccl.env", *TOPO_ARGS, STATUS_ARG]
+                assert [v["name"] for v in pod["volumes"]] == ["nfd-features", "agent-run", "rccl-artifacts"]
+                assert [m["name"] for m in c[0]["volumeMounts"]] == ["nfd-features", "agent-run", "rccl-artifacts"]
                 assert pod["nodeSelector"] == {"foo": "bar"}
                 ref = ds["metadata"]["ownerReferences"][0]
                 assert ref["kind"] == "NetworkClusterPolicy" and ref["controller"] is True
@@ -133,8 +134,8 @@ def test_reconcile_lifecycle_reference_parity():
                 ds = fake.get_object(kube.DAEMONSETS, "policy", NS)
                 c = ds["spec"]["template"]["spec"]["containers"][0]
                 assert c["args"] == ["--configure=true", "--keep-running", "--mode=L2",
-                                     "--rccl-env=/host/etc/amd/scale-out/rccl.env", *TOPO_ARGS]
-                assert [v["name"] for v in ds["spec"]["template"]["spec"]["volumes"]] == ["nfd-features",
+                                     "--rccl-env=/host/etc/amd/scale-out/rccl.env", *TOPO_ARGS, STATUS_ARG]
+                assert [v["name"] for v in ds["spec"]["template"]["spec"]["volumes"]] == ["nfd-features", "agent-run",
                                                                                           "rccl-artifacts"]
             await eventually(l2_ok)
 
@@ -150,9 +151,9 @@ def test_reconcile_lifecycle_reference_parity():
                 assert c["args"][6] == "--wait=90s"
                 assert c["imagePullPolicy"] == "Always"  # fix: pullPolicy applied
                 assert [v["name"] for v in ds["spec"]["template"]["spec"]["volumes"]] == \
-                    ["nfd-features", "var-run-dbus", "networkmanager", "rccl-artifacts"]
+                    ["nfd-features", "agent-run", "var-run-dbus", "networkmanager", "rccl-artifacts"]
                 assert all(v["hostPath"]["type"] == "DirectoryOrCreate"
-                           for v in ds["spec"]["template"]["spec"]["volumes"])
+                           for v in ds["spec"]["template"]["spec"]["volumes"] if "hostPath" in v)
             await eventually(l3nm_ok)
 
             # delete: ownerRef GC removes DaemonSet, ServiceAccount, RoleBinding
@@ -284,7 +285,8 @@ def test_agent_args_mi355x_options():
     p = T.new_policy("x", layer="L3", xgmiCheck=True, lldpAnnounce=False, interfaces=["ens1", "ens2"],
                      nicDrivers=["mlx5_core"])
     a = agent_args(p)
-    assert a[-4:] == ["--xgmi-expect=0", "--lldp-announce=false", "--interfaces=ens1,ens2", "--nic-drivers=mlx5_core"]
+    assert a[-5:] == ["--xgmi-expect=0", "--lldp-announce=false", "--interfaces=ens1,ens2", "--nic-drivers=mlx5_core",
+                      STATUS_ARG]
 
 
 def test_leader_election_single_active_and_failover():
@@ -431,7 +433,8 @@ def test_host_nic_daemonset_branch():
                              "--nfd-label=amd.feature.node.kubernetes.io/host-nic-ready"]
     assert "--mtu=9000" in c["args"] and "--nic-drivers=mlx5_core" in c["args"] and "--wait=90s" in c["args"]
     assert not any(a.startswith("--rccl-net") for a in c["args"])
-    assert c["readinessProbe"]["exec"]["command"][1:] == ["--ready-check", "--nfd-label-file=host-nic-readiness.txt"]
+    assert c["readinessProbe"]["exec"]["command"][1:] == ["--ready-check", "--nfd-label-file=host-nic-readiness.txt",
+                                                          STATUS_ARG]
     init = pod["initContainers"][0]
     assert init["name"] == "nic-driver" and init["securityContext"]["privileged"] and init["imagePullPolicy"] == "Always"
     assert any(v["name"] == "host-lib-modules" for v in pod["volumes"])
@@ -444,7 +447,7 @@ def test_host_nic_daemonset_branch():
     # Back to amd-so: default probe, scale-out args.
     q = T.new_policy("storage", layer="L3")
     update_daemonset_for(ds, q, "ns")
-    assert c["readinessProbe"]["exec"]["command"][1:] == ["--ready-check"]
+    assert c["readinessProbe"]["exec"]["command"][1:] == ["--ready-check", STATUS_ARG]
     assert any(a.startswith("--rccl-net") for a in c["args"])
 
 
@@ -870,7 +873,7 @@ def test_host_nic_keep_config_args_volume_and_cleanup():
 
     p = T.new_host_nic_policy("hosts", layer="L3", keepConfigOnRestart=True, nicDrivers=["mlx5_core"])
     args = R.host_nic_agent_args(p)
-    assert args[-2:] == ["--lldp-cache=/host/etc/amd/scale-out/host-nic-lldp-cache", "--keep-config"]
+    assert args[-3:] == ["--lldp-cache=/host/etc/amd/scale-out/host-nic-lldp-cache", "--keep-config", STATUS_ARG]
     assert R.keeps_config(p) and R.needs_node_cleanup(p)
     job = R.cleanup_job(p, "n0", NS)
     spec = job["spec"]["template"]["spec"]
@@ -879,7 +882,7 @@ def test_host_nic_keep_config_args_volume_and_cleanup():
     assert "--nfd-label-file=host-nic-readiness.txt" in c["args"]  # its own lock, label and keyfile
     assert "rccl-artifacts" in [v["name"] for v in spec["volumes"]]
     l2 = T.new_host_nic_policy("hosts", layer="L2", keepConfigOnRestart=True)
-    assert R.host_nic_agent_args(l2)[-1] == "--keep-config" and not any("lldp-cache" in a for a in R.host_nic_agent_args(l2))
+    assert R.host_nic_agent_args(l2)[-2] == "--keep-config" and not any("lldp-cache" in a for a in R.host_nic_agent_args(l2))
     plain = T.new_host_nic_policy("hosts", layer="L3")
     assert not R.needs_node_cleanup(plain) and "--keep-config" not in R.host_nic_agent_args(plain)
 

@@ -477,3 +477,23 @@ def test_helm_max_unavailable_renders():
     cr = _chart_policies(docs)[0]
     assert cr["spec"]["maxUnavailable"] == "10%" and CRD.validate(cr) == []
     assert "maxUnavailable" not in _chart_policies(helm_template(CHART, {"config": {"amd": {"enabled": True}}}))[0]["spec"]
+
+
+def test_rendered_deployments_are_up_to_date():
+    """deployments/ is what `make deployments` renders (kustomize, the chart, the agent
+    DaemonSets of the samples); a CRD or template change must be re-rendered."""
+    import subprocess
+    import sys
+
+    from network_operator_amd.testing.render import dump_all
+
+    want = {
+        "operator.yaml": dump_all(kustomize_build(ROOT / "config/operator/default")),
+        "helm-default.yaml": dump_all(helm_template(CHART, {"config": {"amd": {"enabled": True}}}, "amd-network-operator")),
+    }
+    for name, sample in (("discovery.yaml", "amd-l3.yaml"), ("discovery-host-nic.yaml", "amd-host-nic.yaml")):
+        want[name] = subprocess.run([sys.executable, "-m", "network_operator_amd.testing.render", "--discovery",
+                                     str(ROOT / "config/operator/samples" / sample)], capture_output=True, text=True,
+                                    check=True, cwd=ROOT).stdout
+    stale = [n for n, text in want.items() if (ROOT / "deployments" / n).read_text() != text]
+    assert not stale, f"run `make deployments`: {stale}"
