@@ -16,7 +16,7 @@ from typing import Dict, List, Optional
 
 from ..api.v1alpha1 import types as T
 from . import kube
-from .informer import Informer, controller_of, slim_job, slim_pod
+from .informer import Informer, controller_of, slim_event, slim_job, slim_pod
 from .kube import ApiClient
 from .metrics import OperatorMetrics
 from .reconciler import (OWNER_KEY, VALIDATION_APP, EventRecorder, NetworkClusterPolicyReconciler,
@@ -26,6 +26,7 @@ from .workqueue import RateLimitingQueue
 log = logging.getLogger("controller")
 
 CONTROLLER_NAME = "networkclusterpolicy"
+PROBE_EVENT_KEY = "involvedObject.name"
 
 
 def pod_ready(pod: Optional[dict]) -> bool:
@@ -57,6 +58,11 @@ class PolicyController:
                                  transform=slim_pod,
                                  keep=lambda p: (p.get("status") or {}).get("phase") == "Failed")
         self.job_pods.add_index(OWNER_KEY, job_owner_index)
+        # The kubelet's readiness-probe failures on agent Pods: the probe prints the agent's
+        # reason, so status.errors can say why a running node withdrew its label.
+        self.probe_events = Informer(client, kube.EVENTS, namespace=namespace, transform=slim_event,
+                                     field_selector="involvedObject.kind=Pod,reason=Unhealthy")
+        self.probe_events.add_index(PROBE_EVENT_KEY, lambda e: [(e.get("involvedObject") or {}).get("name", "")])
         self.queue = RateLimitingQueue(CONTROLLER_NAME)
         self.reconciler = NetworkClusterPolicyReconciler(
             client, namespace, is_openshift,
@@ -65,13 +71,15 @@ class PolicyController:
             recorder=EventRecorder(client, namespace) if record_events else None,
             list_pods=lambda ds: self.pods.by_index(OWNER_KEY, ds),
             list_jobs=lambda name: self.jobs.by_index(OWNER_KEY, name),
-            list_job_pods=lambda job: self.job_pods.by_index(OWNER_KEY, job))
+            list_job_pods=lambda job: self.job_pods.by_index(OWNER_KEY, job),
+            list_probe_events=lambda pod: self.probe_events.by_index(PROBE_EVENT_KEY, pod))
         self.reconciler.on_cleanup = lambda policy, outcome: self.metrics.node_cleanups.labels(policy, outcome).inc()
         self.policies.add_handler(self._on_policy)
         self.daemonsets.add_handler(self._on_daemonset)
         self.pods.add_handler(self._on_pod)
         self.jobs.add_handler(self._on_job)
         self.job_pods.add_handler(self._on_job_pod)
+        self.probe_events.add_handler(self._on_probe_event)
         self._tasks: List[asyncio.Task] = []
         self.reconciles = 0
         self._pod_seen: Dict[str, float] = {}  # agent Pod uid -> monotonic time first seen, until Ready
@@ -97,6 +105,16 @@ class PolicyController:
         ref = controller_of(obj)
         if ref and ref.get("kind") == T.KIND:
             await self._enqueue(ref["name"])
+
+    async def _on_probe_event(self, ev: str, obj: dict, old: Optional[dict]) -> None:
+        io = obj.get("involvedObject") or {}
+        pod = self.pods.get(io.get("name", ""), io.get("namespace") or self.namespace)
+        ref = controller_of(pod) if pod else None
+        if ref and ref.get("kind") == "DaemonSet":
+            ds = self.daemonsets.get(ref["name"], self.namespace)
+            owner = controller_of(ds) if ds else None
+            if owner and owner.get("kind") == T.KIND:
+                await self._enqueue(owner["name"])
 
     async def _on_job_pod(self, ev: str, obj: dict, old: Optional[dict]) -> None:
         ref = controller_of(obj)
@@ -186,13 +204,15 @@ class PolicyController:
         self._tasks.append(self.pods.start())
         self._tasks.append(self.jobs.start())
         self._tasks.append(self.job_pods.start())
+        self._tasks.append(self.probe_events.start())
         await asyncio.gather(self.policies.synced.wait(), self.daemonsets.synced.wait(), self.pods.synced.wait(),
-                             self.jobs.synced.wait(), self.job_pods.synced.wait())
+                             self.jobs.synced.wait(), self.job_pods.synced.wait(), self.probe_events.synced.wait())
         for _ in range(self.workers):
             self._tasks.append(asyncio.ensure_future(self._worker()))
 
     def has_synced(self) -> bool:
-        return all(i.synced.is_set() for i in (self.policies, self.daemonsets, self.pods, self.jobs, self.job_pods))
+        return all(i.synced.is_set() for i in (self.policies, self.daemonsets, self.pods, self.jobs, self.job_pods,
+                                               self.probe_events))
 
     async def stop(self) -> None:
         await self.queue.shutdown()

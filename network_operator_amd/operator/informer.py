@@ -92,6 +92,17 @@ def slim_job(job: dict) -> dict:
                              for c in st["conditions"]]} if st.get("conditions") else {})})
 
 
+def slim_event(ev: dict) -> dict:
+    """A kubelet probe Event: what it is about, its message and when."""
+    io = ev.get("involvedObject") or {}
+    return _shared({"apiVersion": "v1", "kind": "Event",
+                    "metadata": _slim_meta(ev.get("metadata") or {}, ("name", "namespace", "uid", "resourceVersion")),
+                    "involvedObject": {k: io[k] for k in ("kind", "name", "namespace") if k in io},
+                    "reason": ev.get("reason", ""), "message": ev.get("message", ""),
+                    "lastTimestamp": ev.get("lastTimestamp") or ev.get("eventTime") or "",
+                    "count": ev.get("count", 1)})
+
+
 def controller_of(obj: dict) -> Optional[dict]:
     """metav1.GetControllerOf."""
     for ref in obj.get("metadata", {}).get("ownerReferences", []) or []:
@@ -104,7 +115,7 @@ class Informer:
     def __init__(self, client: ApiClient, res: Resource, namespace: Optional[str] = None,
                  label_selector: Optional[str] = None, resync_timeout: int = 300,
                  transform: Optional[Callable[[dict], dict]] = None,
-                 keep: Optional[Callable[[dict], bool]] = None):
+                 keep: Optional[Callable[[dict], bool]] = None, field_selector: Optional[str] = None):
         self.client = client
         self.transform = transform
         # Objects failing `keep` are not cached (as if deleted): e.g. only the failed Pods of the
@@ -113,6 +124,7 @@ class Informer:
         self.res = res
         self.namespace = namespace
         self.label_selector = label_selector
+        self.field_selector = field_selector
         self.resync_timeout = resync_timeout
         self.store: Dict[str, dict] = {}
         self.resource_version: Optional[str] = None
@@ -189,7 +201,8 @@ class Informer:
         await self._emit("ADDED" if old is None else "MODIFIED", obj, old)
 
     async def _relist(self) -> None:
-        lst = await self.client.list(self.res, self.namespace, label_selector=self.label_selector)
+        lst = await self.client.list(self.res, self.namespace, label_selector=self.label_selector,
+                                     field_selector=self.field_selector)
         self.relists += 1
         fresh = {obj_key(o): o for o in lst.get("items", [])}
         for key in list(self.store):
@@ -214,7 +227,8 @@ class Informer:
                     need_list = False
                 async for ev, obj in self.client.watch(self.res, self.namespace, self.resource_version,
                                                        timeout_seconds=self.resync_timeout,
-                                                       label_selector=self.label_selector):
+                                                       label_selector=self.label_selector,
+                                                       field_selector=self.field_selector):
                     rv = obj.get("metadata", {}).get("resourceVersion")
                     if ev == "BOOKMARK":
                         self.resource_version = rv

@@ -305,7 +305,7 @@ class ApiClient:
     # -- watch -------------------------------------------------------------------------------------
     async def watch(self, res: Resource, namespace: Optional[str] = None, resource_version: Optional[str] = None,
                     timeout_seconds: int = 300, label_selector: Optional[str] = None,
-                    bookmarks: bool = True) -> AsyncIterator[Tuple[str, dict]]:
+                    bookmarks: bool = True, field_selector: Optional[str] = None) -> AsyncIterator[Tuple[str, dict]]:
         """Yields (type, object) until the server closes the stream.  Raises ApiError(410) when
         ``resource_version`` is too old (an ERROR event with code 410 is translated too)."""
         params = {"watch": "true", "timeoutSeconds": str(timeout_seconds)}
@@ -315,6 +315,8 @@ class ApiClient:
             params["allowWatchBookmarks"] = "true"
         if label_selector:
             params["labelSelector"] = label_selector
+        if field_selector:
+            params["fieldSelector"] = field_selector
         s = await self._sess()
         self.requests += 1
         async with s.get(self.cfg.host + res.path(namespace), params=params, headers=self._headers(),

@@ -383,6 +383,26 @@ def agent_exit_reason(pod: dict, limit: int = 1500) -> Optional[str]:
     return None
 
 
+PROBE_PREFIXES = ("Readiness probe failed: ", "not ready: ")
+
+
+def probe_reason(events: List[dict], limit: int = 1500) -> Optional[str]:
+    """Why the running agent's readiness probe fails: the latest kubelet "Unhealthy" event on its
+    Pod carries the probe's output (the agent's per-NIC reason, e.g. "enp30s0np0: link down")."""
+    if not events:
+        return None
+    ev = max(events, key=lambda e: (e.get("lastTimestamp") or e.get("eventTime") or "", int(e.get("count", 0) or 0)))
+    msg = (ev.get("message") or "").strip()
+    for p in PROBE_PREFIXES:
+        if msg.startswith(p):
+            msg = msg[len(p):]
+    return msg[:limit] or None
+
+
+def _container_running(pod: dict) -> bool:
+    return any("running" in (cs.get("state") or {}) for cs in (pod.get("status") or {}).get("containerStatuses") or [])
+
+
 def policy_conditions(current: List[dict], targets: int, ready: int, errors: List[str], generation: int,
                       now: Optional[str] = None) -> List[dict]:
     """The policy's Ready / Degraded conditions (additive to the reference's state string,
@@ -626,7 +646,8 @@ class NetworkClusterPolicyReconciler:
                  list_pods: Optional[Callable[[str], List[dict]]] = None,
                  list_jobs: Optional[Callable[[str], List[dict]]] = None,
                  list_job_pods: Optional[Callable[[str], List[dict]]] = None,
-                 clock: Callable[[], float] = time.time):
+                 clock: Callable[[], float] = time.time,
+                 list_probe_events: Optional[Callable[[str], List[dict]]] = None):
         self.client = client
         self.namespace = namespace
         self.is_openshift = is_openshift
@@ -638,6 +659,8 @@ class NetworkClusterPolicyReconciler:
         self._list_pods = list_pods
         self._list_jobs = list_jobs  # validation Jobs of a policy (by its name)
         self._list_job_pods = list_job_pods  # the Pods of a validation Job (by its name)
+        self._list_probe_events = list_probe_events  # kubelet "Unhealthy" events of an agent Pod (by its name)
+        self._degraded_errors: set = set()  # status.errors entries that came from a probe, not an exit
         self._clock = clock
         self.recorder = recorder
         # keepConfigOnRestart: (policy, node) -> when the node's agent Pod was first seen missing
@@ -659,7 +682,14 @@ class NetworkClusterPolicyReconciler:
                 continue
             node = pod.get("spec", {}).get("nodeName") or pod["metadata"]["name"]
             err = f"{node}: scale-out not ready ({ready.get('reason') or pod.get('status', {}).get('phase', 'Pending')})"
-            why = agent_exit_reason(pod)
+            # A running agent that withdrew its label says why through its probe (kubelet event);
+            # an agent that exited, through its termination message.
+            probed = probe_reason(self._list_probe_events(pod["metadata"]["name"])) \
+                if self._list_probe_events is not None and (_container_running(pod) or not agent_exit_reason(pod)) \
+                else None
+            why = probed or agent_exit_reason(pod)
+            if probed:
+                self._degraded_errors.add(f"{err}: {why}")
             errs.append(f"{err}: {why}" if why else err)
         if len(errs) > limit:
             errs = errs[:limit] + [f"... and {len(errs) - limit} more"]
@@ -1059,9 +1089,11 @@ class NetworkClusterPolicyReconciler:
             raise
         if cur.state != new_state and new_state == STATE_ALL_GOOD:
             await self._event(raw, "Normal", "AllNodesReady", f"{ready}/{targets} nodes configured")
-        for e in errors:  # an agent that exited, with its reason: once per new message
+        for e in errors:  # an agent that exited / a node that degraded, with its reason: once per new message
             if e not in cur.errors and "scale-out not ready (" in e and "): " in e:
-                await self._event(raw, "Warning", "AgentFailed", e[:1024])
+                degraded = e in self._degraded_errors
+                await self._event(raw, "Warning", "NodeDegraded" if degraded else "AgentFailed", e[:1024])
+        self._degraded_errors.clear()
         return Result(requeue_after=requeue_after)
 
     # -- entry point -------------------------------------------------------------------------------

@@ -466,6 +466,13 @@ async def _scenario(tmp: Path, n_nics: int, mode: str, seed: int, interval: str,
                     return label_key not in node.node_labels() and st.get("state") != "All good" and st.get("errors")
 
                 t_deg = await _until(degraded, 10)
+                # The probe's reason reaches status.errors through the kubelet's event.
+                t_why = await _until(lambda: any("link down" in e for e in (
+                    (fake.get_object(P, name) or {}).get("status") or {}).get("errors") or []), 10)
+                res["port_down_to_reason_in_status_s"] = round(t_why - t1, 6) if t_why else None
+                await _until(lambda: any(e.get("reason") == "NodeDegraded" for e in fake.list_objects(kube.EVENTS)), 5)
+                res["policy_events_after_flap"] = sorted({e.get("reason") for e in fake.list_objects(kube.EVENTS)
+                                                          if (e.get("involvedObject") or {}).get("kind") == T.KIND})
                 res["flap_status"] = (fake.get_object(P, name) or {}).get("status")
                 # The readiness probe's output, which the kubelet puts in the Pod's events.
                 c0 = next(iter(node.containers.values()))

@@ -141,12 +141,18 @@ def match_labels(labels: dict, selector: str) -> bool:
 
 
 def _match_fields(obj: dict, selector: str) -> bool:
-    md = obj.get("metadata", {})
+    """Field selectors as the API server serves them for the fields used here: dotted paths
+    (metadata.name, spec.nodeName, status.phase, involvedObject.kind, reason, ...)."""
     for term in [t.strip() for t in selector.split(",") if t.strip()]:
         neg = "!=" in term
         k, v = re.split("!=|==|=", term, maxsplit=1)
-        actual = {"metadata.name": md.get("name"), "metadata.namespace": md.get("namespace")}.get(k)
-        if (actual == v) == neg:
+        actual = obj
+        for part in k.split("."):
+            actual = actual.get(part) if isinstance(actual, dict) else None
+        if (str(actual) if actual is not None else None) == v or (actual is None and v == ""):
+            if neg:
+                return False
+        elif not neg:
             return False
     return True
 
@@ -156,6 +162,7 @@ class _Watch:
     res: Resource
     namespace: Optional[str]
     label_selector: Optional[str]
+    field_selector: Optional[str] = None
     queue: asyncio.Queue = field(default_factory=asyncio.Queue)
 
 
@@ -270,6 +277,29 @@ class FakeApiServer:
                         "restartCount": prev.get("restartCount", -1) + 1, "terminated": dict(terminated)}
         self._sync_daemonsets()
 
+    def record_probe_failure(self, namespace: str, pod: str, message: str) -> None:
+        """The kubelet's Event for a failed probe: reason Unhealthy, type Warning, on the Pod;
+        a repeat of the same message bumps its count (the kubelet's event aggregation)."""
+        name = f"{pod}.unhealthy"
+        cur = self._table(kube.EVENTS).get((namespace, name))
+        now = _now()
+        if cur is not None and cur.get("message") == message:
+            new = copy.deepcopy(cur)
+            new["count"] = int(cur.get("count", 1)) + 1
+            new["lastTimestamp"] = now
+            self._store(kube.EVENTS, new, "MODIFIED")
+            return
+        body = {"apiVersion": "v1", "kind": "Event", "type": "Warning", "reason": "Unhealthy", "message": message,
+                "metadata": {"name": name, "namespace": namespace},
+                "involvedObject": {"apiVersion": "v1", "kind": "Pod", "name": pod, "namespace": namespace,
+                                   "fieldPath": "spec.containers{configurator}"},
+                "source": {"component": "kubelet"}, "count": 1, "firstTimestamp": now, "lastTimestamp": now}
+        if cur is not None:
+            body["metadata"] = copy.deepcopy(cur["metadata"])
+            self._store(kube.EVENTS, body, "MODIFIED")
+        else:
+            self._create(kube.EVENTS, body, namespace)
+
     def set_job_result(self, name: str, namespace: str, succeeded: bool, pod_reason: Optional[str] = None,
                        pod_message: str = "", finished: Optional[str] = None) -> None:
         """What the Job controller records when the Job's only Pod ends (backoffLimit 0).  With
@@ -337,6 +367,8 @@ class FakeApiServer:
         if w.namespace and md.get("namespace") != w.namespace:
             return False
         if w.label_selector and not match_labels(md.get("labels", {}) or {}, w.label_selector):
+            return False
+        if w.field_selector and not _match_fields(obj, w.field_selector):
             return False
         return True
 
@@ -690,7 +722,7 @@ class FakeApiServer:
                                                 "reason": "Expired", "message": f"too old resource version: {since}"}}
             await resp.write((json.dumps(err) + "\n").encode())
             return resp
-        w = _Watch(res, ns, req.query.get("labelSelector"))
+        w = _Watch(res, ns, req.query.get("labelSelector"), req.query.get("fieldSelector"))
         for rv, r, typ, obj in self.events:
             if r == res and rv > since and self._visible(w, obj):
                 w.queue.put_nowait((typ, obj))

@@ -351,10 +351,14 @@ class SimNode:
             for c in list(self.containers.values()):
                 if c.probe is None or c.proc is None or c.proc.poll() is not None:
                     continue
-                p = await asyncio.create_subprocess_exec(*c.probe, env=self._env(c), stdout=asyncio.subprocess.DEVNULL,
+                p = await asyncio.create_subprocess_exec(*c.probe, env=self._env(c), stdout=asyncio.subprocess.PIPE,
                                                          stderr=asyncio.subprocess.DEVNULL)
-                rc = await p.wait()
+                out, _ = await p.communicate()
+                rc = p.returncode
                 if c is self.containers.get(c.pod):
+                    if rc != 0:  # the kubelet's event for a failed probe, with the probe's output
+                        self.fake.record_probe_failure(c.pod[0], c.pod[1],
+                                                       "Readiness probe failed: " + out.decode(errors="replace").strip())
                     self._set_ready(c, rc == 0)
             await asyncio.sleep(self.probe_period)
 

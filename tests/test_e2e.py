@@ -131,7 +131,10 @@ def test_link_failure_is_reported_by_the_policy_and_recovers():
     assert r["port_down_to_status_degraded_s"] is not None, (r.get("flap_status"), r["agent_log"])
     st = r["flap_status"]
     assert st["state"] == "Working on it.." and st["ready"] == 0 and st["targets"] == 1
-    assert st["errors"] == ["mi355x-0: scale-out not ready (ContainersNotReady)"]
+    # why, from the agent through its readiness probe and the kubelet's event
+    assert st["errors"] == [f"mi355x-0: scale-out not ready (ContainersNotReady): {r['nics'][0]}: link down"]
+    assert r["port_down_to_reason_in_status_s"] is not None
+    assert "NodeDegraded" in r["policy_events_after_flap"] and "AgentFailed" not in r["policy_events_after_flap"]
     assert any(c["type"] == "Degraded" and c["status"] == "True" for c in st["conditions"])
     assert r["port_up_to_all_good_s"] is not None, r["agent_log"]
     # kubectl describe pod: "Readiness probe failed: not ready: <nic>: link down"

@@ -1012,3 +1012,16 @@ def test_min_link_speed_passed_in_both_layers():
     assert not any("min-link-speed" in a for a in agent_args(T.new_policy("p")))
     bad = policy(minLinkSpeedGbps=5000)
     assert any("less than or equal to 3200" in e for e in CRD.validate(bad))
+
+
+def test_probe_reason_takes_the_latest_kubelet_event():
+    from network_operator_amd.operator.informer import slim_event
+    from network_operator_amd.operator.reconciler import probe_reason
+
+    old = {"metadata": {"name": "p.1", "namespace": NS}, "involvedObject": {"kind": "Pod", "name": "p"},
+           "reason": "Unhealthy", "message": "Readiness probe failed: not ready: ens1: link down",
+           "lastTimestamp": "2026-01-01T00:00:01Z", "count": 3, "source": {"component": "kubelet"}}
+    new = dict(old, message="Readiness probe failed: not ready: ens2: waiting for LLDP", lastTimestamp="2026-01-01T00:00:09Z")
+    assert probe_reason([slim_event(old), slim_event(new)]) == "ens2: waiting for LLDP"
+    assert probe_reason([]) is None
+    assert "source" not in slim_event(old) and slim_event(old)["involvedObject"] == {"kind": "Pod", "name": "p"}
