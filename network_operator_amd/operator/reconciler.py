@@ -672,6 +672,7 @@ class NetworkClusterPolicyReconciler:
     def _node_errors(self, ds_name: str, limit: int = 16) -> List[str]:
         """Per-node agent problems from the agent Pods' Ready condition (the reference indexes
         Pods by owner but never reads them and always reports ``errors: []``)."""
+        self._degraded_errors = set()
         if self._list_pods is None:
             return []
         errs = []
@@ -1093,7 +1094,6 @@ class NetworkClusterPolicyReconciler:
             if e not in cur.errors and "scale-out not ready (" in e and "): " in e:
                 degraded = e in self._degraded_errors
                 await self._event(raw, "Warning", "NodeDegraded" if degraded else "AgentFailed", e[:1024])
-        self._degraded_errors.clear()
         return Result(requeue_after=requeue_after)
 
     # -- entry point -------------------------------------------------------------------------------
