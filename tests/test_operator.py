@@ -1025,3 +1025,71 @@ def test_probe_reason_takes_the_latest_kubelet_event():
     assert probe_reason([slim_event(old), slim_event(new)]) == "ens2: waiting for LLDP"
     assert probe_reason([]) is None
     assert "source" not in slim_event(old) and slim_event(old)["involvedObject"] == {"kind": "Pod", "name": "p"}
+
+
+def test_cleanup_survives_an_operator_restart_mid_deletion(monkeypatch):
+    """The finalizer's progress lives in the API server (status.keptNodes and the cleanup Jobs),
+    not in the operator's memory: a new leader picks the deletion up where the old one stopped,
+    without cleaning a finished node twice."""
+    from network_operator_amd.operator import reconciler as R
+
+    monkeypatch.setattr(R, "CLEANUP_POLL_S", 0.05)
+
+    async def body():
+        fake = FakeApiServer()
+        url = await fake.start()
+        client = ApiClient(KubeConfig(host=url))
+        try:
+            for i in range(3):
+                fake.add_node(f"gpu-node-{i}", {"foo": "bar"})
+            ctl = PolicyController(client, NS, is_openshift=False, workers=2)
+            await ctl.start()
+            await client.create(kube.NETWORKCLUSTERPOLICIES, policy(keepConfigOnRestart=True))
+            await eventually(lambda: (fake.get_object(kube.NETWORKCLUSTERPOLICIES, "policy").get("status") or {})
+                             .get("keptNodes") == [f"gpu-node-{i}" for i in range(3)])
+            await client.delete(kube.NETWORKCLUSTERPOLICIES, "policy")
+            await eventually(lambda: len(fake.list_objects(kube.JOBS)) == 3)
+            first = {j["metadata"]["name"] for j in fake.list_objects(kube.JOBS)}
+            await ctl.stop()  # the leader goes away; one node's cleanup finishes meanwhile
+            done = next(j for j in fake.list_objects(kube.JOBS) if j["spec"]["template"]["spec"]["nodeName"] == "gpu-node-0")
+            fake.set_job_result(done["metadata"]["name"], NS, True)
+            ctl2 = PolicyController(client, NS, is_openshift=False, workers=2)
+            await ctl2.start()
+            await eventually(lambda: (fake.get_object(kube.NETWORKCLUSTERPOLICIES, "policy").get("status") or {})
+                             .get("keptNodes") == ["gpu-node-1", "gpu-node-2"])
+            for j in fake.list_objects(kube.JOBS):
+                if not (j.get("status") or {}).get("conditions"):
+                    fake.set_job_result(j["metadata"]["name"], NS, True)
+            await eventually(lambda: fake.get_object(kube.NETWORKCLUSTERPOLICIES, "policy") is None)
+            created = [m for m, path in fake.requests if m == "POST" and path.endswith("/jobs")]
+            assert len(created) == 3 and first  # no node was cleaned twice
+            await ctl2.stop()
+        finally:
+            await client.close()
+            await fake.stop()
+    run(body())
+
+
+def test_a_node_that_rejoins_during_its_cleanup_keeps_its_agent(monkeypatch):
+    """A node leaves the policy, its cleanup Job starts, and it comes back before the Job ran:
+    the Job is withdrawn (the node lock on the node keeps the two apart if it had started) and
+    the node stays in keptNodes for its new agent."""
+    from network_operator_amd.operator import reconciler as R
+
+    monkeypatch.setattr(R, "KEPT_ORPHAN_GRACE_S", 0.2)
+    monkeypatch.setattr(R, "CLEANUP_POLL_S", 0.05)
+
+    async def body():
+        async with cluster(openshift=False) as (fake, client, ctl):
+            fake.add_node("gpu-node-0", {"foo": "bar"})
+            await client.create(kube.NETWORKCLUSTERPOLICIES, policy(keepConfigOnRestart=True))
+            await eventually(lambda: (fake.get_object(kube.NETWORKCLUSTERPOLICIES, "policy").get("status") or {})
+                             .get("keptNodes") == ["gpu-node-0"])
+            fake.set_node_labels("gpu-node-0", {"foo": "other"})
+            await eventually(lambda: len(fake.list_objects(kube.JOBS)) == 1)
+            fake.set_node_labels("gpu-node-0", {"foo": "bar"})  # back before the Job ran
+            await eventually(lambda: fake.list_objects(kube.JOBS) == [])
+            await asyncio.sleep(0.3)
+            assert fake.list_objects(kube.JOBS) == []
+            assert fake.get_object(kube.NETWORKCLUSTERPOLICIES, "policy")["status"]["keptNodes"] == ["gpu-node-0"]
+    run(body())
