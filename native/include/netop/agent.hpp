@@ -191,9 +191,11 @@ class LldpSource {
 // The LLDPDU the agent advertises for one of its NICs.  Announcing ourselves makes an
 // IEEE 802.1AB-2009 switch see a *new neighbour* and enter fast transmission (txFast), so
 // its Port Description arrives within ~1 s instead of up to msgTxInterval (30 s).
-// ttl = 0 builds the shutdown LLDPDU sent on cleanup.
+// ttl = 0 builds the shutdown LLDPDU sent on cleanup.  mtu > 0 adds the IEEE 802.3 Maximum
+// Frame Size TLV (MTU + 18: header and FCS), so the switch's neighbour table shows what frames
+// the host sends and a mismatch is visible from the switch side too.
 lldp::Frame make_node_frame(const std::string& node_name, const std::string& ifname, const MacAddr& mac,
-                            const std::string& gpu_bdf, uint16_t ttl = 120);
+                            const std::string& gpu_bdf, uint16_t ttl = 120, int mtu = 0);
 std::unique_ptr<LldpSource> make_packet_source(bool promisc);
 
 using NmFactory = std::function<std::unique_ptr<nm::NetworkManagerIf>()>;

@@ -86,7 +86,7 @@ bool fd_readable(int fd) {
 std::unique_ptr<LldpSource> make_packet_source(bool promisc) { return std::make_unique<PacketSource>(promisc); }
 
 lldp::Frame make_node_frame(const std::string& node_name, const std::string& ifname, const MacAddr& mac,
-                            const std::string& gpu_bdf, uint16_t ttl) {
+                            const std::string& gpu_bdf, uint16_t ttl, int mtu) {
     lldp::Frame f;
     f.dst = lldp::kNearestBridge;
     f.src = mac;
@@ -99,6 +99,7 @@ lldp::Frame make_node_frame(const std::string& node_name, const std::string& ifn
     f.system_name = node_name;
     f.system_description = "AMD Instinct MI355X node (amd-network-operator link discovery)";
     f.capabilities = std::make_pair(uint16_t(0x0080), uint16_t(0x0080));  // station only
+    if (mtu > 0 && ttl > 0) f.set_max_frame_size(uint16_t(std::min(mtu + 18, 0xffff)));
     return f;
 }
 
@@ -819,7 +820,8 @@ void Agent::detect_lldp(int stop_fd) {
             // fast-transmit tick.
             if ((announces[n.link.index] == 0 || retry) && cfg_.announce_shutdown_first)
                 lldp_->announce(n.ifname, lldp::encode(make_node_frame(cfg_.node_name, n.ifname, n.link.mac, n.gpu_bdf, 0)));
-            lldp_->announce(n.ifname, lldp::encode(make_node_frame(cfg_.node_name, n.ifname, n.link.mac, n.gpu_bdf)));
+            lldp_->announce(n.ifname,
+                            lldp::encode(make_node_frame(cfg_.node_name, n.ifname, n.link.mac, n.gpu_bdf, 120, cfg_.mtu)));
         } catch (const std::exception& e) {
             NLOG_V(2, "LLDP announce on %s failed: %s", n.ifname.c_str(), e.what());
         }
@@ -1710,7 +1712,8 @@ void Agent::announce_all(uint16_t ttl) {
     for (auto& n : nics_) {
         if (!n.link.up()) continue;
         try {
-            lldp_->announce(n.ifname, lldp::encode(make_node_frame(cfg_.node_name, n.ifname, n.link.mac, n.gpu_bdf, ttl)));
+            lldp_->announce(n.ifname,
+                            lldp::encode(make_node_frame(cfg_.node_name, n.ifname, n.link.mac, n.gpu_bdf, ttl, cfg_.mtu)));
         } catch (const std::exception& e) {
             NLOG_V(2, "LLDP announce on %s failed: %s", n.ifname.c_str(), e.what());
         }

@@ -1787,3 +1787,10 @@ TEST(agent_switch_port_with_a_smaller_max_frame_than_the_mtu_is_refused) {
     b.run(-1);
     CHECK_EQ(g.ops.addrs.size(), size_t(3));
 }
+
+TEST(agent_announcement_carries_the_hosts_max_frame_size) {
+    auto f = agent::make_node_frame("node-1", "ens0", *MacAddr::parse("02:00:00:00:00:10"), "0000:05:00.0", 120, 9000);
+    CHECK(f.max_frame_size() && *f.max_frame_size() == 9018);
+    CHECK(!agent::make_node_frame("node-1", "ens0", *MacAddr::parse("02:00:00:00:00:10"), "", 0, 9000).max_frame_size());
+    CHECK(!agent::make_node_frame("node-1", "ens0", *MacAddr::parse("02:00:00:00:00:10"), "").max_frame_size());
+}
