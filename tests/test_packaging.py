@@ -497,3 +497,12 @@ def test_rendered_deployments_are_up_to_date():
                                     check=True, cwd=ROOT).stdout
     stale = [n for n, text in want.items() if (ROOT / "deployments" / n).read_text() != text]
     assert not stale, f"run `make deployments`: {stale}"
+
+
+def test_prometheus_overlay_scrapes_the_operator_and_the_agents():
+    docs = kustomize_build(ROOT / "config/operator/prometheus")
+    kinds = sorted(d["kind"] for d in docs)
+    assert kinds == ["PodMonitor", "ServiceMonitor"]
+    pm = next(d for d in docs if d["kind"] == "PodMonitor")
+    assert pm["spec"]["selector"]["matchLabels"] == {"app": "amd-network-tools"}
+    assert pm["spec"]["podMetricsEndpoints"][0]["port"] == "metrics"  # the container port metricsPort opens
