@@ -399,6 +399,14 @@ def probe_reason(events: List[dict], limit: int = 1500) -> Optional[str]:
     return msg[:limit] or None
 
 
+STARTUP_REASONS = ("waiting for LLDP", "not configured yet")
+
+
+def _starting_up(reason: str) -> bool:
+    """Every NIC of the probe's reason is still coming up (no Event for a node that starts)."""
+    return all(part.split(": ", 1)[-1] in STARTUP_REASONS for part in reason.split("; "))
+
+
 def _container_running(pod: dict) -> bool:
     return any("running" in (cs.get("state") or {}) for cs in (pod.get("status") or {}).get("containerStatuses") or [])
 
@@ -689,7 +697,7 @@ class NetworkClusterPolicyReconciler:
                 if self._list_probe_events is not None and (_container_running(pod) or not agent_exit_reason(pod)) \
                 else None
             why = probed or agent_exit_reason(pod)
-            if probed:
+            if probed and not _starting_up(probed):
                 self._degraded_errors.add(f"{err}: {why}")
             errs.append(f"{err}: {why}" if why else err)
         if len(errs) > limit:
@@ -1092,8 +1100,10 @@ class NetworkClusterPolicyReconciler:
             await self._event(raw, "Normal", "AllNodesReady", f"{ready}/{targets} nodes configured")
         for e in errors:  # an agent that exited / a node that degraded, with its reason: once per new message
             if e not in cur.errors and "scale-out not ready (" in e and "): " in e:
-                degraded = e in self._degraded_errors
-                await self._event(raw, "Warning", "NodeDegraded" if degraded else "AgentFailed", e[:1024])
+                if e in self._degraded_errors:
+                    await self._event(raw, "Warning", "NodeDegraded", e[:1024])
+                elif not e.endswith(tuple(STARTUP_REASONS)):
+                    await self._event(raw, "Warning", "AgentFailed", e[:1024])
         return Result(requeue_after=requeue_after)
 
     # -- entry point -------------------------------------------------------------------------------

@@ -1093,3 +1093,10 @@ def test_a_node_that_rejoins_during_its_cleanup_keeps_its_agent(monkeypatch):
             assert fake.list_objects(kube.JOBS) == []
             assert fake.get_object(kube.NETWORKCLUSTERPOLICIES, "policy")["status"]["keptNodes"] == ["gpu-node-0"]
     run(body())
+
+
+def test_a_starting_node_is_not_reported_as_degraded():
+    from network_operator_amd.operator.reconciler import _starting_up
+
+    assert _starting_up("ens0: waiting for LLDP; ens1: not configured yet")
+    assert not _starting_up("ens0: waiting for LLDP; ens1: link down")
