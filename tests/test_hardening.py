@@ -87,6 +87,11 @@ def test_operator_image_file_set_is_self_contained(tmp_path):
                        env={"PYTHONPATH": str(app), "PATH": "/usr/bin:/bin"}, capture_output=True, text=True,
                        timeout=120)
     assert r.returncode == 0 and "--policies-file" in r.stdout, r.stderr[-2000:]
+    # The chart's pre-delete hook runs the same image with another module.
+    r = subprocess.run([sys.executable, "-m", "network_operator_amd.operator.predelete", "--help"], cwd=str(tmp_path),
+                       env={"PYTHONPATH": str(app), "PATH": "/usr/bin:/bin"}, capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode == 0 and "--owner" in r.stdout, r.stderr[-2000:]
 
 
 # What the agent image's runtime base (ubuntu:22.04) ships as shared libraries without any
