@@ -9,6 +9,7 @@
 // Built by `make fuzz-native` with amdclang++ -fsanitize=fuzzer,address,undefined (one binary
 // per target, selected by NETOP_FUZZ_TARGET at compile time).  Each target must never crash,
 // hang or trip a sanitizer on any input.
+#include <linux/dcbnl.h>
 #include <linux/netlink.h>
 #include <linux/rtnetlink.h>
 
@@ -66,6 +67,11 @@ extern "C" int LLVMFuzzerTestOneInput(const uint8_t* data, size_t size) {
     }
     try {
         (void)nl::parse_link_stats(h);
+    } catch (const std::exception&) {
+    }
+    h->nlmsg_type = RTM_GETDCB;  // the same bytes as a DCB netlink reply (dcbmsg + attributes)
+    try {
+        (void)nl::parse_dcb_u8(h, DCB_ATTR_DCBX);
     } catch (const std::exception&) {
     }
     // The same bytes as an extended-ACK error (nlmsgerr + echoed request + attributes), both with

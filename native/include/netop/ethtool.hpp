@@ -11,10 +11,16 @@
 //   ice  (E810):            fw-lldp-agent   = off
 //   anything else:          --fw-lldp-priv-flag NAME=0|1 (site-specific)
 //
-// mlx5 (ConnectX) and ionic (Pensando): no private flag is known to the agent; a firmware
-// LLDP agent there is a persistent NIC setting outside the scope of a DaemonSet (unverified on
-// this pool: parity unpinned).  The agent reports "no firmware LLDP flag" for them, and a NIC
-// that stays silent is diagnosed after --wait (Agent::diagnose_silent).
+// mlx5 (ConnectX) and ionic (Pensando): no private flag is known to the agent.  For a NIC
+// without one, the driver-neutral signal is its DCBX mode (DCB netlink, DCB_CMD_GDCBX): without
+// DCB_CAP_DCBX_HOST, an embedded agent runs DCBX, and with it the port's LLDP exchange.  Per
+// the drivers' dcbnl code, ice and i40e report DCB_CAP_DCBX_LLD_MANAGED while their firmware
+// agent runs, and mlx5_core reports no HOST bit in its firmware ("auto") DCBX mode and moves to
+// host mode on DCB_CMD_SDCBX with HOST set.  So `--disable-fw-lldp` hands DCBX to the host on
+// such a NIC and puts the original mode back on exit.  Whether that makes mlx5 firmware pass
+// LLDPDUs up is unverified on this pool (parity unpinned; the box's NICs live outside its
+// network namespace).  A NIC that stays silent is diagnosed after --wait with its DCBX mode
+// (Agent::diagnose_silent).
 #pragma once
 
 #include <cstdint>
@@ -38,7 +44,19 @@ class Ops {
     virtual std::string driver(const std::string& ifname) = 0;     // "" when unknown
     virtual PrivFlags get(const std::string& ifname) = 0;           // throws SysError
     virtual void set(const std::string& ifname, uint32_t bits) = 0;  // throws SysError
+    // DCBX mode (DCB_CAP_DCBX_* bits); nullopt when the NIC has no DCB interface.
+    virtual std::optional<uint8_t> dcbx_get(const std::string& ifname) {
+        (void)ifname;
+        return std::nullopt;
+    }
+    // false when the driver refused the mode; throws SysError.
+    virtual bool dcbx_set(const std::string& ifname, uint8_t mode);
 };
+
+// DCBX mode bits in words: "0x0c (firmware, cee, ieee)", "0x05 (host, ieee)".
+std::string dcbx_str(uint8_t mode);
+// An embedded (NIC-firmware or LLD) agent runs DCBX and the port's LLDP: no DCB_CAP_DCBX_HOST.
+bool dcbx_embedded(uint8_t mode);
 
 std::unique_ptr<Ops> make_ioctl_ops();
 
@@ -57,13 +75,16 @@ struct FwLldpResult {
     std::string flag;          // flag that was changed ("" = none applicable)
     bool changed = false;
     uint32_t original_bits = 0;
+    std::optional<uint8_t> dcbx;  // DCBX mode found (nullopt: no DCB interface, or not asked)
+    bool dcbx_changed = false;    // the agent handed DCBX to the host
     std::string error;         // non-empty on failure
     std::string summary() const;
 };
 
-// Applies the first matching rule on `ifname`; never throws (errors land in .error).
+// Applies the first matching rule on `ifname`; with no applicable private flag, hands an
+// embedded DCBX agent's port to the host (DCB_CMD_SDCBX).  Never throws (errors land in .error).
 FwLldpResult disable_fw_lldp(Ops& ops, const std::string& ifname, const std::vector<FlagRule>& rules);
-// Puts back the original private flags if disable_fw_lldp changed them.
+// Puts back the original private flags / DCBX mode if disable_fw_lldp changed them.
 void restore(Ops& ops, const FwLldpResult& r);
 
 }  // namespace netop::ethtool

@@ -161,6 +161,13 @@ class Rtnl final : public NetOps {
     void link_set_mac(int ifindex, const MacAddr& mac);
     void link_set_name(int ifindex, const std::string& name);
 
+    // DCB netlink (dcbnl, RTM_GETDCB / RTM_SETDCB): the DCBX mode of a NIC as DCB_CAP_DCBX_*
+    // bits.  nullopt when the driver has no DCB interface (EOPNOTSUPP: veth, virtio, ...).
+    // Reading needs no privileges; setting needs CAP_NET_ADMIN.
+    std::optional<uint8_t> dcbx_mode(const std::string& ifname);
+    // false when the driver refused the mode (dcbnl status byte != 0).  Throws SysError.
+    bool set_dcbx_mode(const std::string& ifname, uint8_t mode);
+
     // Number of request round trips done on this socket (observability / bench).
     uint64_t round_trips() const { return rtts_; }
 
@@ -184,5 +191,8 @@ std::optional<LinkStats> parse_link_stats(const nlmsghdr* h);
 // The NLMSGERR_ATTR_MSG string of an extended ACK (NLMSG_ERROR with NLM_F_ACK_TLVS); "" if
 // absent.  `h->nlmsg_len` bytes must be readable; every inner length is bounds-checked.
 std::string ext_ack_msg(const nlmsghdr* h);
+// The u8 attribute `type` of an RTM_GETDCB / RTM_SETDCB reply (dcbmsg header); nullopt if
+// absent.  Bounds-checked like parse_link.
+std::optional<uint8_t> parse_dcb_u8(const nlmsghdr* h, uint16_t type);
 
 }  // namespace netop::nl

@@ -66,6 +66,10 @@ struct NicState {
 
     // NIC firmware LLDP agent (--disable-fw-lldp): summary of what was done
     std::string fw_lldp;
+    // DCBX mode of the NIC (DCB netlink), in words: read by --disable-fw-lldp, or when the NIC
+    // stays silent; "" = not read / no DCB interface.
+    std::string dcbx;
+    bool dcbx_embedded = false;  // an embedded agent holds DCBX (not handed to the host by us)
     // L3, --wait expired without a frame: the NIC's driver and what it did hear meanwhile
     // (Agent::diagnose_silent), e.g. "mlx5_core: no LLDPDU in 90s while 412 frames arrived ...".
     std::string driver;

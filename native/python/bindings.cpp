@@ -184,6 +184,8 @@ PYBIND11_MODULE(_netop_native, m) {
         .def("link_set_netns_pid", &nl::Rtnl::link_set_netns_pid)
         .def("link_set_netns_fd", &nl::Rtnl::link_set_netns_fd)
         .def("link_set_name", &nl::Rtnl::link_set_name)
+        .def("dcbx_mode", &nl::Rtnl::dcbx_mode)
+        .def("set_dcbx_mode", &nl::Rtnl::set_dcbx_mode)
         .def("round_trips", &nl::Rtnl::round_trips);
 
     m.def("lldp_send", [](const std::string& ifname, const py::bytes& frame) {

@@ -200,6 +200,8 @@ void Agent::disable_fw_lldp() {
     for (auto& n : nics_) {
         auto r = ethtool::disable_fw_lldp(*ethtool_, n.ifname, rules);
         n.fw_lldp = r.summary();
+        if (r.dcbx) n.dcbx = ethtool::dcbx_str(*r.dcbx);
+        n.dcbx_embedded = r.dcbx && ethtool::dcbx_embedded(*r.dcbx) && !r.dcbx_changed;
         if (!r.error.empty()) NLOG_W("%s: firmware LLDP: %s", n.ifname.c_str(), r.error.c_str());
         NLOG_V(2, "%s: driver %s, firmware LLDP: %s", n.ifname.c_str(), r.driver.c_str(), n.fw_lldp.c_str());
         fw_lldp_.push_back(std::move(r));
@@ -946,14 +948,34 @@ void Agent::diagnose_silent() {
         auto ls = lldp_->stats_for(n.ifname);
         std::string heard = rx ? strfmt("%llu frame(s) arrived meanwhile", (unsigned long long)*rx)
                                : std::string("receive counters unavailable");
+        // Who runs DCBX (and so LLDP) on this port: the host, or an agent embedded in the NIC?
+        // Read-only, unprivileged (DCB netlink); --disable-fw-lldp has read it already.
+        if (n.dcbx.empty()) {
+            try {
+                if (!ethtool_) ethtool_ = ethtool::make_ioctl_ops();
+                if (auto m = ethtool_->dcbx_get(n.ifname)) {
+                    n.dcbx = ethtool::dcbx_str(*m);
+                    n.dcbx_embedded = ethtool::dcbx_embedded(*m);
+                }
+            } catch (const std::exception& e) {
+                NLOG_V(2, "%s: DCBX mode unreadable: %s", n.ifname.c_str(), e.what());
+            }
+        }
         std::string why;
         if (ls && ls->malformed) {
             why = strfmt("%llu LLDPDU(s) did not decode", (unsigned long long)ls->malformed);
         } else if (rx && *rx == 0) {
             why = "the link received nothing: check the cable, the switch port and its LLDP transmit setting";
+        } else if (n.dcbx_embedded) {
+            why = "the NIC's embedded agent runs DCBX and LLDP on this port (DCBX " + n.dcbx + ")" +
+                  (cfg_.disable_fw_lldp ? " although --disable-fw-lldp ran (" + n.fw_lldp + ")"
+                                        : ": run with --disable-fw-lldp to hand DCBX to the host");
         } else if (n.driver == "i40e" || n.driver == "ice") {
             why = cfg_.disable_fw_lldp ? "NIC-firmware LLDP agent suspected although --disable-fw-lldp ran (" + n.fw_lldp + ")"
                                        : "NIC-firmware LLDP agent suspected: run with --disable-fw-lldp";
+        } else if (!n.dcbx.empty()) {
+            why = "DCBX is host-managed (" + n.dcbx + "), so no NIC-firmware DCBX agent holds the port: check that the "
+                  "switch port transmits LLDP to the nearest-bridge address 01:80:c2:00:00:0e";
         } else {
             why = "NIC-firmware LLDP agent suspected (no verified switch for this driver; see the user guide, "
                   "\"Silent LLDP\")";
@@ -1335,6 +1357,16 @@ std::string Agent::render_metrics() const {
         for (auto& n : nics_)
             o += strfmt("netop_agent_lldp_silent{nic=\"%s\",driver=\"%s\"} %d\n", httpd::escape_label(n.ifname).c_str(),
                         httpd::escape_label(n.driver).c_str(), n.lldp_silent.empty() ? 0 : 1);
+        bool any_dcbx = false;
+        for (auto& n : nics_) any_dcbx |= !n.dcbx.empty();
+        if (any_dcbx) {
+            metric("netop_agent_dcbx_embedded", "gauge",
+                   "1 when an agent embedded in the NIC runs DCBX (and LLDP) on it; NICs whose DCBX mode was read");
+            for (auto& n : nics_)
+                if (!n.dcbx.empty())
+                    o += strfmt("netop_agent_dcbx_embedded{nic=\"%s\"} %d\n", httpd::escape_label(n.ifname).c_str(),
+                                n.dcbx_embedded ? 1 : 0);
+        }
     }
     auto st = lldp_ ? lldp_->stats() : pkt::ListenerStats{};
     metric("netop_agent_lldp_frames_total", "counter", "LLDP frames received, by outcome");

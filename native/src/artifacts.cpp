@@ -491,6 +491,7 @@ std::string generate_status(const std::vector<NicState>& nics, const std::map<st
         if (!n->gpu_bdf.empty()) j.key("gpu_bdf").value(n->gpu_bdf);
         if (!n->rdma_dev.empty()) j.key("rdma_dev").value(n->rdma_dev);
         if (!n->fw_lldp.empty()) j.key("fw_lldp").value(n->fw_lldp);
+        if (!n->dcbx.empty()) j.key("dcbx").value(n->dcbx);
         if (!n->driver.empty()) j.key("driver").value(n->driver);
         if (!n->lldp_silent.empty()) j.key("lldp_silent").value(n->lldp_silent);
         if (n->speed_mbps >= 0) j.key("speed_mbps").value(n->speed_mbps);

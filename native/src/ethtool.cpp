@@ -1,5 +1,6 @@
 #include "netop/ethtool.hpp"
 
+#include <linux/dcbnl.h>
 #include <linux/ethtool.h>
 #include <linux/sockios.h>
 #include <net/if.h>
@@ -14,6 +15,7 @@
 
 #include "netop/common.hpp"
 #include "netop/log.hpp"
+#include "netop/netlink.hpp"
 
 namespace netop::ethtool {
 
@@ -75,6 +77,9 @@ class IoctlOps final : public Ops {
         call(ifname, &v, true);
     }
 
+    std::optional<uint8_t> dcbx_get(const std::string& ifname) override { return rtnl().dcbx_mode(ifname); }
+    bool dcbx_set(const std::string& ifname, uint8_t mode) override { return rtnl().set_dcbx_mode(ifname, mode); }
+
    private:
     bool call(const std::string& ifname, void* data, bool throw_on_error) {
         ifreq ifr{};
@@ -85,10 +90,33 @@ class IoctlOps final : public Ops {
         if (throw_on_error) throw SysError(errno, "SIOCETHTOOL " + ifname);
         return false;
     }
+    nl::Rtnl& rtnl() {  // DCB netlink: a socket of its own, opened on first use
+        if (!rtnl_) rtnl_ = std::make_unique<nl::Rtnl>();
+        return *rtnl_;
+    }
     int fd_;
+    std::unique_ptr<nl::Rtnl> rtnl_;
 };
 
 }  // namespace
+
+bool Ops::dcbx_set(const std::string& ifname, uint8_t mode) {
+    (void)mode;
+    throw SysError(EOPNOTSUPP, "DCB " + ifname);
+}
+
+std::string dcbx_str(uint8_t mode) {
+    std::vector<std::string> w;
+    if (mode & DCB_CAP_DCBX_HOST) w.push_back("host");
+    if (mode & DCB_CAP_DCBX_LLD_MANAGED) w.push_back("lld-managed");
+    if (!(mode & (DCB_CAP_DCBX_HOST | DCB_CAP_DCBX_LLD_MANAGED))) w.push_back("firmware");
+    if (mode & DCB_CAP_DCBX_VER_CEE) w.push_back("cee");
+    if (mode & DCB_CAP_DCBX_VER_IEEE) w.push_back("ieee");
+    if (mode & DCB_CAP_DCBX_STATIC) w.push_back("static");
+    return strfmt("0x%02x (%s)", mode, join(w, ", ").c_str());
+}
+
+bool dcbx_embedded(uint8_t mode) { return !(mode & DCB_CAP_DCBX_HOST); }
 
 std::unique_ptr<Ops> make_ioctl_ops() { return std::make_unique<IoctlOps>(); }
 
@@ -118,8 +146,10 @@ std::vector<FlagRule> parse_rules(const std::string& spec) {
 
 std::string FwLldpResult::summary() const {
     if (!error.empty()) return "error: " + error;
-    if (flag.empty()) return "no firmware LLDP flag";
-    return (changed ? "set " : "already ") + flag;
+    if (!flag.empty()) return (changed ? "set " : "already ") + flag;
+    if (dcbx_changed) return "DCBX handed to the host (was " + dcbx_str(*dcbx) + ")";
+    if (dcbx) return "no firmware LLDP flag; DCBX " + dcbx_str(*dcbx);
+    return "no firmware LLDP flag";
 }
 
 FwLldpResult disable_fw_lldp(Ops& ops, const std::string& ifname, const std::vector<FlagRule>& rules) {
@@ -149,15 +179,44 @@ FwLldpResult disable_fw_lldp(Ops& ops, const std::string& ifname, const std::vec
     } catch (const std::exception& e) {
         r.error = e.what();
     }
+    if (!r.flag.empty() || !r.error.empty()) return r;
+    // No private flag for this driver: is an embedded agent running DCBX (and LLDP) here?
+    try {
+        r.dcbx = ops.dcbx_get(ifname);
+        if (r.dcbx && dcbx_embedded(*r.dcbx)) {
+            uint8_t want = uint8_t(DCB_CAP_DCBX_HOST | (*r.dcbx & (DCB_CAP_DCBX_VER_CEE | DCB_CAP_DCBX_VER_IEEE)));
+            if (!(want & (DCB_CAP_DCBX_VER_CEE | DCB_CAP_DCBX_VER_IEEE))) want |= DCB_CAP_DCBX_VER_IEEE;
+            if (ops.dcbx_set(ifname, want)) {
+                r.dcbx_changed = true;
+                NLOG_I("%s (%s): DCBX handed to the host (was %s), so the NIC's embedded agent no longer runs LLDP",
+                       ifname.c_str(), r.driver.c_str(), dcbx_str(*r.dcbx).c_str());
+            } else {
+                r.error = "the driver refused DCBX host mode " + dcbx_str(want) + " (current " + dcbx_str(*r.dcbx) + ")";
+            }
+        }
+    } catch (const std::exception& e) {
+        r.error = std::string("DCBX: ") + e.what();
+    }
     return r;
 }
 
 void restore(Ops& ops, const FwLldpResult& r) {
-    if (!r.changed) return;
-    try {
-        ops.set(r.ifname, r.original_bits);
-    } catch (const std::exception& e) {
-        NLOG_W("%s: could not restore private flags: %s", r.ifname.c_str(), e.what());
+    if (r.changed) {
+        try {
+            ops.set(r.ifname, r.original_bits);
+        } catch (const std::exception& e) {
+            NLOG_W("%s: could not restore private flags: %s", r.ifname.c_str(), e.what());
+        }
+    }
+    if (r.dcbx_changed) {
+        // The original mode first; mlx5_core takes only 0 as "back to firmware (auto)" control.
+        try {
+            bool ok = ops.dcbx_set(r.ifname, *r.dcbx);
+            if (!ok && !(*r.dcbx & DCB_CAP_DCBX_LLD_MANAGED)) ok = ops.dcbx_set(r.ifname, 0);
+            if (!ok) NLOG_W("%s: the driver refused to restore DCBX mode %s", r.ifname.c_str(), dcbx_str(*r.dcbx).c_str());
+        } catch (const std::exception& e) {
+            NLOG_W("%s: could not restore the DCBX mode: %s", r.ifname.c_str(), e.what());
+        }
     }
 }
 

@@ -1,6 +1,7 @@
 #include "netop/netlink.hpp"
 
 #include <errno.h>
+#include <linux/dcbnl.h>
 #include <linux/if.h>
 #include <linux/if_link.h>
 #include <linux/netlink.h>
@@ -188,6 +189,8 @@ static const char* msg_name(uint16_t t) {
         case RTM_NEWROUTE: return "RTM_NEWROUTE";
         case RTM_DELROUTE: return "RTM_DELROUTE";
         case RTM_GETROUTE: return "RTM_GETROUTE";
+        case RTM_GETDCB: return "RTM_GETDCB";
+        case RTM_SETDCB: return "RTM_SETDCB";
     }
     return "RTM_?";
 }
@@ -467,6 +470,54 @@ std::optional<LinkStats> Rtnl::link_stats(int ifindex) {
         return std::nullopt;
     }
     return out;
+}
+
+std::optional<uint8_t> parse_dcb_u8(const nlmsghdr* h, uint16_t type) {
+    const auto* d = fixed_header<dcbmsg>(h, "dcb");
+    size_t len = h->nlmsg_len - NLMSG_LENGTH(sizeof(dcbmsg));
+    std::optional<uint8_t> out;
+    for_each_attr(reinterpret_cast<const rtattr*>(reinterpret_cast<const uint8_t*>(d) + NLMSG_ALIGN(sizeof(dcbmsg))),
+                  len, [&](const rtattr* a) {
+                      if (a->rta_type == type && RTA_PAYLOAD(a) >= 1) out = *static_cast<const uint8_t*>(RTA_DATA(a));
+                  });
+    return out;
+}
+
+// dcbnl answers a GET/SET with a message of the request's type carrying the result attribute,
+// then the ACK; a driver without dcbnl_ops (or without the getter) fails the request with
+// EOPNOTSUPP.
+std::optional<uint8_t> Rtnl::dcbx_mode(const std::string& ifname) {
+    Msg m(RTM_GETDCB, 0);
+    dcbmsg d{};
+    d.dcb_family = AF_UNSPEC;
+    d.cmd = DCB_CMD_GDCBX;
+    m.put(d);
+    m.attr_str(DCB_ATTR_IFNAME, ifname);
+    std::optional<uint8_t> out;
+    try {
+        transact(m, [&](const nlmsghdr* h) {
+            if (h->nlmsg_type == RTM_GETDCB) out = parse_dcb_u8(h, DCB_ATTR_DCBX);
+        });
+    } catch (const SysError& e) {
+        if (e.code() == EOPNOTSUPP || e.code() == ENODEV) return std::nullopt;
+        throw;
+    }
+    return out;
+}
+
+bool Rtnl::set_dcbx_mode(const std::string& ifname, uint8_t mode) {
+    Msg m(RTM_SETDCB, 0);
+    dcbmsg d{};
+    d.dcb_family = AF_UNSPEC;
+    d.cmd = DCB_CMD_SDCBX;
+    m.put(d);
+    m.attr_str(DCB_ATTR_IFNAME, ifname);
+    m.attr(DCB_ATTR_DCBX, &mode, 1);
+    std::optional<uint8_t> status;
+    transact(m, [&](const nlmsghdr* h) {
+        if (h->nlmsg_type == RTM_SETDCB) status = parse_dcb_u8(h, DCB_ATTR_DCBX);
+    });
+    return status && *status == 0;
 }
 
 std::vector<LinkInfo> Rtnl::link_list() {

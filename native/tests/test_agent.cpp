@@ -1,3 +1,4 @@
+#include <linux/dcbnl.h>
 #include <arpa/inet.h>
 #include <ctime>
 #include <fcntl.h>
@@ -813,8 +814,110 @@ struct FakeEthtool : ethtool::Ops {
         sets.emplace_back(i, bits);
         flags[i].bits = bits;
     }
+    // DCB netlink: NICs absent from `dcbx` have no DCB interface.  Setting follows mlx5_core's
+    // dcbnl setdcbx: LLD_MANAGED refused, 0 = back to firmware control, else HOST required.
+    std::map<std::string, uint8_t> dcbx;
+    std::vector<std::pair<std::string, uint8_t>> dcbx_sets;
+    std::optional<uint8_t> dcbx_get(const std::string& i) override {
+        auto it = dcbx.find(i);
+        if (it == dcbx.end()) return std::nullopt;
+        return it->second;
+    }
+    bool dcbx_set(const std::string& i, uint8_t mode) override {
+        dcbx_sets.emplace_back(i, mode);
+        if (!dcbx.count(i)) throw SysError(EOPNOTSUPP, "DCB " + i);
+        if (mode & DCB_CAP_DCBX_LLD_MANAGED) return false;
+        if (mode == 0) {
+            dcbx[i] = DCB_CAP_DCBX_VER_CEE | DCB_CAP_DCBX_VER_IEEE;
+            return true;
+        }
+        if (!(mode & DCB_CAP_DCBX_HOST)) return false;
+        dcbx[i] = mode;
+        return true;
+    }
 };
 }  // namespace
+
+TEST(ethtool_dcbx_handed_to_the_host_and_back) {
+    // mlx5_core in firmware ("auto") DCBX mode has no private flag for its LLDP agent: the
+    // driver-neutral DCBX mode says an embedded agent holds the port, and host mode takes it back.
+    FakeEthtool e;
+    e.drivers = {{"mlx0", "mlx5_core"}, {"mlx1", "mlx5_core"}, {"ionic0", "ionic"}};
+    e.flags["mlx0"] = {{"rx_cqe_moder", "tx_cqe_moder", "rx_cqe_compress"}, 0x1};
+    e.flags["mlx1"] = e.flags["mlx0"];
+    e.dcbx["mlx0"] = DCB_CAP_DCBX_VER_CEE | DCB_CAP_DCBX_VER_IEEE;                      // firmware
+    e.dcbx["mlx1"] = DCB_CAP_DCBX_HOST | DCB_CAP_DCBX_VER_CEE | DCB_CAP_DCBX_VER_IEEE;  // host already
+    CHECK_EQ(ethtool::dcbx_str(0x0c), std::string("0x0c (firmware, cee, ieee)"));
+    CHECK_EQ(ethtool::dcbx_str(0x06), std::string("0x06 (lld-managed, cee)"));
+    CHECK(ethtool::dcbx_embedded(0x0c) && ethtool::dcbx_embedded(0x06) && !ethtool::dcbx_embedded(0x0d));
+    auto rules = ethtool::builtin_rules();
+    auto a = ethtool::disable_fw_lldp(e, "mlx0", rules);
+    CHECK(a.dcbx_changed && !a.changed && a.error.empty());
+    CHECK_EQ(int(e.dcbx["mlx0"]), 0x0d);
+    CHECK_EQ(a.summary(), std::string("DCBX handed to the host (was 0x0c (firmware, cee, ieee))"));
+    auto b = ethtool::disable_fw_lldp(e, "mlx1", rules);
+    CHECK(!b.dcbx_changed && b.summary() == "no firmware LLDP flag; DCBX 0x0d (host, cee, ieee)");
+    auto c = ethtool::disable_fw_lldp(e, "ionic0", rules);  // no private flags, no DCB interface
+    CHECK(!c.dcbx && !c.dcbx_changed && c.error.empty() && c.summary() == "no firmware LLDP flag");
+    // Restore: the original mode is refused by mlx5 (no HOST bit, not 0), so 0 hands it back.
+    ethtool::restore(e, a);
+    ethtool::restore(e, b);
+    CHECK_EQ(int(e.dcbx["mlx0"]), 0x0c);
+    CHECK_EQ(e.dcbx_sets.size(), size_t(3));
+    CHECK(e.dcbx_sets[1] == std::make_pair(std::string("mlx0"), uint8_t(0x0c)));
+    CHECK(e.dcbx_sets[2] == std::make_pair(std::string("mlx0"), uint8_t(0)));
+    // A private-flag driver (ice) never gets its DCBX mode changed by the agent.
+    e.drivers["ice0"] = "ice";
+    e.flags["ice0"] = {{"link-down-on-close", "fw-lldp-agent"}, 0x2};
+    e.dcbx["ice0"] = DCB_CAP_DCBX_LLD_MANAGED | DCB_CAP_DCBX_VER_IEEE;
+    auto d = ethtool::disable_fw_lldp(e, "ice0", rules);
+    CHECK(d.changed && !d.dcbx_changed && e.dcbx_sets.size() == size_t(3));
+    // A driver refusing host mode is an error the status shows, not an exception.
+    e.dcbx["odd0"] = DCB_CAP_DCBX_LLD_MANAGED;
+    struct Refusing : FakeEthtool {
+        bool dcbx_set(const std::string&, uint8_t) override { return false; }
+    } r;
+    r.dcbx["odd0"] = DCB_CAP_DCBX_LLD_MANAGED;
+    auto f = ethtool::disable_fw_lldp(r, "odd0", rules);
+    CHECK(!f.dcbx_changed && f.error.find("refused DCBX host mode 0x09 (host, ieee)") != std::string::npos);
+}
+
+TEST(agent_silent_nic_names_its_embedded_dcbx_agent) {
+    // A NIC hearing traffic but no LLDPDU, whose DCBX an embedded agent holds: the diagnosis says
+    // so with the mode; a host-managed one points at the switch instead.
+    Fixture f;
+    f.cfg.wait_ns = 1000000;
+    auto s = f.all_valid();
+    s->frames.erase("ens1");
+    s->frames.erase("ens2");
+    f.ops.rx[11] = 0;
+    f.ops.rx_step[11] = 40;
+    f.ops.rx[12] = 0;
+    f.ops.rx_step[12] = 40;
+    auto eth = std::make_unique<FakeEthtool>();
+    eth->drivers = {{"ens1", "mlx5_core"}, {"ens2", "mlx5_core"}};
+    eth->dcbx["ens1"] = DCB_CAP_DCBX_VER_CEE | DCB_CAP_DCBX_VER_IEEE;
+    eth->dcbx["ens2"] = DCB_CAP_DCBX_HOST | DCB_CAP_DCBX_VER_IEEE;
+    agent::Agent a(f.cfg, f.ops, std::move(s), f.nm());
+    a.set_ethtool_ops(std::move(eth));
+    std::string err;
+    try {
+        a.run(-1);
+    } catch (const agent::AgentError& e) {
+        err = e.what();
+    }
+    CHECK(err.find("ens1 (mlx5_core: no LLDPDU in 1ms, 40 frame(s) arrived meanwhile; the NIC's embedded agent runs "
+                   "DCBX and LLDP on this port (DCBX 0x0c (firmware, cee, ieee)): run with --disable-fw-lldp") !=
+          std::string::npos);
+    CHECK(err.find("ens2 (mlx5_core: no LLDPDU in 1ms, 40 frame(s) arrived meanwhile; DCBX is host-managed (0x09 "
+                   "(host, ieee))") != std::string::npos);
+    auto st = read_file(f.cfg.status_file);
+    CHECK(st && st->find("\"dcbx\":\"0x0c (firmware, cee, ieee)\"") != std::string::npos);
+    auto m = a.render_metrics();
+    CHECK(m.find("netop_agent_dcbx_embedded{nic=\"ens1\"} 1") != std::string::npos);
+    CHECK(m.find("netop_agent_dcbx_embedded{nic=\"ens2\"} 0") != std::string::npos);
+    CHECK(m.find("netop_agent_dcbx_embedded{nic=\"ens0\"}") == std::string::npos);
+}
 
 TEST(ethtool_rules_parse) {
     auto r = ethtool::parse_rules(" lldp-offload=off, my-flag=1 ");

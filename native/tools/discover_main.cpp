@@ -93,7 +93,7 @@ int main(int argc, char** argv) {
     fs.add_duration("lldp-tx-interval", &cfg.lldp_tx_interval_ns, "LLDP keep-alive transmit interval while monitoring");
     fs.add_string("metrics-bind-address", &cfg.metrics_addr, "serve /metrics, /healthz, /readyz on this address (e.g. :9102; empty = off)");
     fs.add_string("require-gdr", &cfg.require_gdr, "refuse readiness without GPUDirect RDMA: any, peermem, dmabuf (empty = report only)");
-    fs.add_bool("disable-fw-lldp", &cfg.disable_fw_lldp, "L3: turn off NIC-firmware LLDP agents (i40e disable-fw-lldp, ice fw-lldp-agent) while running");
+    fs.add_bool("disable-fw-lldp", &cfg.disable_fw_lldp, "L3: turn off NIC-firmware LLDP agents while running (i40e disable-fw-lldp, ice fw-lldp-agent; other DCB NICs, e.g. mlx5_core: DCBX handed to the host)");
     fs.add_string("fw-lldp-priv-flag", &cfg.fw_lldp_flags, "extra ethtool private-flag rules NAME=0|1[,...] for --disable-fw-lldp");
     bool ready_check = false;
     fs.add_bool("ready-check", &ready_check, "exit 0 if the readiness label is published, 1 otherwise (readinessProbe)");

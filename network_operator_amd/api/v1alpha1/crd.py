@@ -68,7 +68,8 @@ def openapi_schema() -> dict:
             "nicDrivers": {"description": "NIC driver allow-list for GPU-affinity discovery (default: common RoCE drivers).",
                            "items": {"type": "string"}, "type": "array"},
             "disableFirmwareLldp": {"description": "L3: turn off NIC-firmware LLDP agents (ethtool private flags, e.g. i40e\n"
-                                                   "disable-fw-lldp, ice fw-lldp-agent) while the agent runs, so switch\n"
+                                                   "disable-fw-lldp, ice fw-lldp-agent; on other DCB NICs such as mlx5_core\n"
+                                                   "the DCBX mode is handed to the host) while the agent runs, so switch\n"
                                                    "LLDPDUs reach the host.",
                                     "type": "boolean"},
             "gpuDirectRdma": {"description": "Require GPUDirect RDMA before labelling the node: Any, PeerMem (amdkfd\n"

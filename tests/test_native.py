@@ -1,8 +1,10 @@
 """Native agent building blocks: C++ unit suite, pybind11 bindings, property-based fuzzing,
 and discovery on a fake sysfs copy of a real 8x MI355X node."""
 
+import errno
 import ipaddress
 import json
+import os
 import subprocess
 
 import pytest
@@ -195,3 +197,17 @@ def test_gdr_detection_binding(native, tmp_path):
     (tmp_path / "module" / "ib_uverbs").mkdir(parents=True)
     d = native.detect_gdr(str(tmp_path), "6.8.0")
     assert d["mode"] == "dmabuf" and d["kernel"] == "6.8.0"
+
+
+def test_dcb_netlink_requests_reach_the_kernel(native):
+    """The DCB netlink request the agent sends to read a NIC's DCBX mode is well-formed: the
+    kernel parses it and answers for the named device.  lo has no DCB interface (EOPNOTSUPP) and
+    an unknown name has no device (ENODEV): both read as "no DCB interface", never as an error.
+    A malformed request would fail with EINVAL and raise.  Setting needs CAP_NET_ADMIN and a DCB
+    driver: on lo it is refused either way."""
+    r = native.Rtnl()
+    assert r.dcbx_mode("lo") is None
+    assert r.dcbx_mode("netop-nosuch0") is None
+    with pytest.raises(OSError) as e:
+        r.set_dcbx_mode("lo", 0x09)
+    assert any(os.strerror(c) in str(e.value) for c in (errno.EOPNOTSUPP, errno.EPERM)), e.value
