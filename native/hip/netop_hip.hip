@@ -34,11 +34,12 @@ __device__ __forceinline__ uint32_t mix(uint64_t i, uint32_t seed) {
     return x;
 }
 
-// Pattern value for (element, rank): an integer in [-4, 4] -> exact in bf16, sums of up to
-// 64 ranks stay exact (|sum| <= 256 < 2^8).
-__device__ __forceinline__ int pattern(uint64_t i, uint32_t seed, int rank) {
-    return int(mix(i, seed + 0x632BE5ABu * uint32_t(rank + 1)) % 9u) - 4;
-}
+// Pattern of (element, rank): integers in [-4, 4] -> exact in bf16, sums of up to 64 ranks
+// stay exact (|sum| <= 256 < 2^8).  One hash per group of 8 elements (one 16-byte vector; every
+// buffer and offset is a multiple of 8 elements), spent as 8 base-9 digits: element e is digit
+// (e & 7) of mix(e >> 3, seed_r).  A hash per element made fill / verify ALU-bound at ~1.6 TB/s
+// (12 hash ops + a modulo per 2 bytes); per group it is ~5 ops per element.
+__device__ __forceinline__ uint32_t rank_seed(uint32_t seed, int rank) { return seed + 0x632BE5ABu * uint32_t(rank + 1); }
 
 __device__ __forceinline__ uint16_t int_to_bf16(int v) {
     // Small integers are exact; convert through f32 bits (truncation is exact here).
@@ -48,28 +49,35 @@ __device__ __forceinline__ uint16_t int_to_bf16(int v) {
 
 __device__ __forceinline__ float bf16_to_float(uint16_t h) { return __uint_as_float(uint32_t(h) << 16); }
 
-// Σ_{r in [rank_lo, rank_lo + n_ranks)} pattern(e, r): one rank's data (n_ranks = 1) or the
-// reduction over a contiguous rank range (all-reduce / reduce-scatter expectation).
-__device__ __forceinline__ int pattern_sum(uint64_t e, uint32_t seed, int rank_lo, int n_ranks) {
-    int s = 0;
-    for (int r = rank_lo; r < rank_lo + n_ranks; ++r) s += pattern(e, seed, r);
-    return s;
+// s[k] = Σ_{r in [rank_lo, rank_lo + n_ranks)} pattern(8 g + k, r): one rank's data (n_ranks =
+// 1) or the reduction over a contiguous rank range (all-reduce / reduce-scatter expectation).
+__device__ __forceinline__ void group_sum(uint64_t g, uint32_t seed, int rank_lo, int n_ranks, int s[8]) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s[k] = 0;
+    for (int r = rank_lo; r < rank_lo + n_ranks; ++r) {
+        uint32_t x = mix(g, rank_seed(seed, r));
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const uint32_t q = x / 9u;  // constant divisor: a multiply-high and a shift
+            s[k] += int(x - q * 9u) - 4;
+            x = q;
+        }
+    }
 }
 
-// Element e of the buffer holds pattern_sum(e + elem_offset, ...): the offset lets a chunk of
-// a collective's output be checked against the slice of the global pattern it came from.
+// Element e of the buffer holds the pattern sum of element e + elem_offset: the offset lets a
+// chunk of a collective's output be checked against the slice of the global pattern it came
+// from.  elem_offset is a multiple of 8, so vector v is group (elem_offset / 8 + v).
 __global__ __launch_bounds__(kThreads) void fill_kernel(uint4* __restrict__ out, uint64_t n_vec, uint32_t seed, int rank_lo,
                                                         int n_ranks, uint64_t elem_offset) {
     const uint64_t stride = uint64_t(gridDim.x) * kThreads;
+    const uint64_t g0 = elem_offset >> 3;
     for (uint64_t v = uint64_t(blockIdx.x) * kThreads + threadIdx.x; v < n_vec; v += stride) {
+        int s[8];
+        group_sum(g0 + v, seed, rank_lo, n_ranks, s);
         uint32_t w[4];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            uint64_t e = elem_offset + v * 8 + uint64_t(k) * 2;
-            int a = pattern_sum(e, seed, rank_lo, n_ranks);
-            int b = pattern_sum(e + 1, seed, rank_lo, n_ranks);
-            w[k] = uint32_t(int_to_bf16(a)) | (uint32_t(int_to_bf16(b)) << 16);
-        }
+        for (int k = 0; k < 4; ++k) w[k] = uint32_t(int_to_bf16(s[2 * k])) | (uint32_t(int_to_bf16(s[2 * k + 1])) << 16);
         out[v] = make_uint4(w[0], w[1], w[2], w[3]);
     }
 }
@@ -79,17 +87,17 @@ __global__ __launch_bounds__(kThreads) void verify_kernel(const uint4* __restric
                                                           unsigned long long* __restrict__ errors) {
     __shared__ unsigned int wave_err[kThreads / 64];
     const uint64_t stride = uint64_t(gridDim.x) * kThreads;
+    const uint64_t g0 = elem_offset >> 3;
     unsigned int err = 0;
     for (uint64_t v = uint64_t(blockIdx.x) * kThreads + threadIdx.x; v < n_vec; v += stride) {
         uint4 q = in[v];
         uint32_t w[4] = {q.x, q.y, q.z, q.w};
+        int s[8];
+        group_sum(g0 + v, seed, rank_lo, n_ranks, s);
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            uint64_t e = elem_offset + v * 8 + uint64_t(k) * 2;
-            int a = pattern_sum(e, seed, rank_lo, n_ranks);
-            int b = pattern_sum(e + 1, seed, rank_lo, n_ranks);
-            err += bf16_to_float(uint16_t(w[k] & 0xffff)) != float(a);
-            err += bf16_to_float(uint16_t(w[k] >> 16)) != float(b);
+            err += bf16_to_float(uint16_t(w[k] & 0xffff)) != float(s[2 * k]);
+            err += bf16_to_float(uint16_t(w[k] >> 16)) != float(s[2 * k + 1]);
         }
     }
     // wave64 reduction, then one atomic per workgroup.
