@@ -91,7 +91,7 @@ def _check_buf(t):
 
 
 def fill_pattern(t, seed: int, rank: int) -> None:
-    """Fill ``t`` (bf16) with rank ``rank``'s deterministic integer pattern in [-4, 4]."""
+    """Fill ``t`` (bf16) with rank ``rank``'s deterministic integer pattern in [-4, 3]."""
     _check_buf(t)
     _check(lib().netop_fill_pattern(ctypes.c_void_p(t.data_ptr()), t.numel(), seed & 0xFFFFFFFF, rank, _stream(t)),
            "netop_fill_pattern")

@@ -14,7 +14,7 @@ def _ref_pattern(n, seed, rank):
 
     M32 = 0xFFFFFFFF
     i = torch.arange(n, dtype=torch.int64)
-    g = i >> 3  # one hash per 8-element group; element i is its base-9 digit i & 7
+    g = i >> 3  # one hash per 8-element group; element i is its 3-bit field i & 7, minus 4
     s = (seed + 0x632BE5AB * (rank + 1)) & M32
     x = ((g & M32) * 0x9E3779B1) & M32
     x = x ^ ((((g >> 32) & M32) * 0x85EBCA77) & M32)
@@ -22,8 +22,7 @@ def _ref_pattern(n, seed, rank):
     x = x ^ (x >> 15)
     x = (x * 0x2C1B3C6D) & M32
     x = x ^ (x >> 12)
-    pow9 = torch.tensor([9 ** k for k in range(8)], dtype=torch.int64)
-    return ((x // pow9[i & 7]) % 9 - 4).to(torch.float32)
+    return (((x >> (3 * (i & 7))) & 7) - 4).to(torch.float32)
 
 
 def test_fill_pattern_matches_reference(cuda_device):
