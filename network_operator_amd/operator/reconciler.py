@@ -743,7 +743,11 @@ class NetworkClusterPolicyReconciler:
             # One template for all of them (only the node differs); CLEANUP_CREATE_CONCURRENCY
             # creates in flight, so a thousand-node policy is cleaned in seconds, not minutes.
             template = cleanup_job(p, "", self.namespace)
-            set_controller_reference(raw, template)
+            if not raw["metadata"].get("deletionTimestamp"):
+                # Owned, so the garbage collector removes what is left with the policy.  Not once
+                # the policy is being deleted: under foreground deletion the collector deletes
+                # every new dependent, a cleanup Job mid-run included (_finalize deletes these).
+                set_controller_reference(raw, template)
             sem = asyncio.Semaphore(CLEANUP_CREATE_CONCURRENCY)
 
             async def create(node: str) -> None:
@@ -875,6 +879,21 @@ class NetworkClusterPolicyReconciler:
                     if not (is_conflict(e) or is_not_found(e)):
                         raise
             return Result(requeue_after=CLEANUP_POLL_S)
+        if p.status.keptNodes:
+            # Every node is clean: record that before the Jobs go (a pass reading keptNodes with
+            # no Jobs would clean the nodes again), then delete them on the next pass.
+            body = copy.deepcopy(raw)
+            body["status"] = dict(raw.get("status") or {}, keptNodes=[])
+            try:
+                await self.client.replace_status(kube.NETWORKCLUSTERPOLICIES, body)
+            except ApiError as e:
+                if is_not_found(e):
+                    return Result()
+                if not is_conflict(e):
+                    raise
+            return Result(requeue=True)
+        # The finished Jobs: those created during the deletion have no owner to take them along.
+        await self._run_cleanups(raw, p, [])
         body = copy.deepcopy(raw)
         body["metadata"]["finalizers"] = [f for f in fins if f != FINALIZER]
         try:
@@ -889,7 +908,7 @@ class NetworkClusterPolicyReconciler:
         self._cleanup_jobs_exist.discard(p.name)
         prefix = cleanup_job_name(p.name, "")[:-10]
         self._cleanups_reported = {n for n in self._cleanups_reported if not n.startswith(prefix)}
-        log.info("Policy %s: %d node(s) cleaned up, finalizer removed", p.name, len(p.status.keptNodes))
+        log.info("Policy %s: every node cleaned up, finalizer removed", p.name)
         return Result()
 
     async def _reconcile_validation(self, raw: dict, p: T.NetworkClusterPolicy, ds: dict, generation: int,

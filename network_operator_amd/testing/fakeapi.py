@@ -175,12 +175,15 @@ class _Fault:
     reason: str = "InternalError"
 
 
+FOREGROUND_DELETION = "foregroundDeletion"
+
+
 class FakeApiServer:
     STATUS_SUBRESOURCE = {kube.NETWORKCLUSTERPOLICIES, kube.DAEMONSETS}
 
     def __init__(self, openshift: bool = False, history: int = 10000, bookmark_interval: float = 1.0,
                  gc_delay: float = 0.0, agent_ready_delay: Optional[float] = None,
-                 extra_groups: Optional[List[str]] = None):
+                 extra_groups: Optional[List[str]] = None, foreground_hold: float = 0.0):
         self.resources: List[Resource] = list(kube.ALL_RESOURCES)
         self.openshift = openshift
         self.objects: Dict[Tuple[str, str, str], Dict[Tuple[str, str], dict]] = {}
@@ -192,6 +195,12 @@ class FakeApiServer:
         self.watches: List[_Watch] = []
         self.bookmark_interval = bookmark_interval
         self.gc_delay = gc_delay
+        # Foreground cascading deletion: owner uid -> (resource, namespace, name) of owners that
+        # carry the foregroundDeletion finalizer.  The garbage collector deletes their dependents,
+        # deletes any dependent created meanwhile, and releases the owner `foreground_hold`
+        # seconds after it last found no dependent (the real GC's processing latency).
+        self._foreground: Dict[str, Tuple[Resource, str, str]] = {}
+        self.foreground_hold = foreground_hold
         self.agent_ready_delay = agent_ready_delay
         # API groups of add-ons installed in the fake cluster (e.g. "nfd.k8s-sigs.io").
         self.extra_groups: List[str] = list(extra_groups or [])
@@ -413,7 +422,11 @@ class FakeApiServer:
         stored = self._store(res, obj, "ADDED")
         if res in (kube.DAEMONSETS, kube.NODES):
             self._sync_daemonsets()
-        return self._table(res)[key]
+        created = self._table(res)[key]
+        if any(r.get("uid") in self._foreground for r in md.get("ownerReferences") or []):
+            # A dependent of an owner in foreground deletion: the garbage collector deletes it.
+            self._delete_or_mark(res, md["name"], key[0])
+        return created
 
     def _delete(self, res: Resource, name: str, namespace: str) -> dict:
         key = (namespace if res.namespaced else "", name)
@@ -430,13 +443,67 @@ class FakeApiServer:
         if res == kube.DAEMONSETS:
             self.node_ready = {k: v for k, v in self.node_ready.items() if k[0] != f"{namespace}/{name}"}
             self.node_last_exit = {k: v for k, v in self.node_last_exit.items() if k[0] != f"{namespace}/{name}"}
+        self._foreground.pop(uid, None)
+        for r in obj["metadata"].get("ownerReferences") or []:
+            if r.get("uid") in self._foreground:
+                self._foreground_check(r["uid"])
         return obj
 
-    def _delete_or_mark(self, res: Resource, name: str, namespace: str) -> dict:
+    def _dependents(self, uid: str) -> list:
+        out = []
+        for res, ns, name in sorted(self._owned.get(uid, ()), key=lambda k: (k[0].plural, k[1], k[2])):
+            o = self._table(res).get((ns, name))
+            if o is not None and any(r.get("uid") == uid for r in o.get("metadata", {}).get("ownerReferences") or []):
+                out.append((res, ns, name))
+        return out
+
+    def _foreground_check(self, uid: str) -> None:
+        """Releases an owner in foreground deletion once it has no dependents left."""
+        if uid not in self._foreground or self._dependents(uid):
+            return
+        if self.foreground_hold > 0:
+            self._bg.append(asyncio.ensure_future(self._foreground_release_later(uid)))
+        else:
+            self._foreground_release(uid)
+
+    async def _foreground_release_later(self, uid: str) -> None:
+        await asyncio.sleep(self.foreground_hold)
+        if uid in self._foreground and not self._dependents(uid):
+            self._foreground_release(uid)
+
+    def _foreground_release(self, uid: str) -> None:
+        res, ns, name = self._foreground.pop(uid)
+        cur = self._table(res).get((ns, name))
+        if cur is None:
+            return
+        new = copy.deepcopy(cur)
+        new["metadata"]["finalizers"] = [f for f in cur["metadata"].get("finalizers") or [] if f != FOREGROUND_DELETION]
+        if new["metadata"]["finalizers"]:
+            self._store(res, new, "MODIFIED")
+        else:
+            self._store(res, new, "MODIFIED")
+            self._delete(res, name, ns)
+
+    def _delete_or_mark(self, res: Resource, name: str, namespace: str, propagation: str = "Background") -> dict:
         """DELETE as the API server does it: an object with finalizers is only marked
-        (deletionTimestamp) and goes once its last finalizer is removed (see _update)."""
+        (deletionTimestamp) and goes once its last finalizer is removed (see _update).
+        ``propagationPolicy: Foreground`` adds the foregroundDeletion finalizer: the object stays
+        until the garbage collector has deleted every dependent (including ones created after)."""
         key = (namespace if res.namespaced else "", name)
         cur = self._table(res)[key]
+        if propagation == "Foreground" and not cur["metadata"].get("deletionTimestamp"):
+            new = copy.deepcopy(cur)
+            new["metadata"]["finalizers"] = list(cur["metadata"].get("finalizers") or []) + [FOREGROUND_DELETION]
+            new["metadata"]["deletionTimestamp"] = _now()
+            new["metadata"]["deletionGracePeriodSeconds"] = 0
+            self._store(res, new, "MODIFIED")
+            uid = new["metadata"]["uid"]
+            self._foreground[uid] = (res, key[0], name)
+            for dres, dns, dname in self._dependents(uid):
+                if (dns, dname) in self._table(dres):
+                    self._delete_or_mark(dres, dname, dns)
+            self._foreground_check(uid)
+            return self._table(res).get(key) or new
         if not cur["metadata"].get("finalizers"):
             return self._delete(res, name, namespace)
         if not cur["metadata"].get("deletionTimestamp"):
@@ -641,7 +708,14 @@ class FakeApiServer:
             if m == "DELETE":
                 if (ns or "", name) not in self._table(res):
                     return _status(404, "NotFound", f'{res.plural} "{name}" not found')
-                return web.json_response(self._delete_or_mark(res, name, ns or ""))
+                opts = {}
+                if req.can_read_body:
+                    try:
+                        opts = json.loads(await req.text() or "{}")
+                    except ValueError:
+                        return _status(400, "BadRequest", "DeleteOptions are not JSON")
+                propagation = (opts or {}).get("propagationPolicy") or req.query.get("propagationPolicy") or "Background"
+                return web.json_response(self._delete_or_mark(res, name, ns or "", propagation))
             return _status(405, "MethodNotAllowed", m)
         except _Conflict as c:
             return _status(c.code, c.reason, c.message, c.details)

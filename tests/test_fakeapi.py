@@ -4,7 +4,8 @@ the operator relies on.
 Most control-plane tests run against this fake instead of envtest's real kube-apiserver (no
 Go toolchain or binaries here), so its fidelity bounds what those tests prove (SURVEY.md §7.7,
 hard part 4).  Each test pins one documented apiserver behaviour; where the fake deliberately
-simplifies (no strategic-merge patch, no finalizer blocking), the test says so.
+simplifies (no strategic-merge patch; the garbage collector acts at once unless gc_delay /
+foreground_hold say otherwise), the test says so.
 """
 
 import asyncio
@@ -209,3 +210,40 @@ def test_finalizers_hold_deletion_and_the_gc_respects_them():
         assert fake.get_object(P, "p") is None
         assert p["metadata"]["uid"] not in fake._owned
     _run(body)
+
+
+def test_foreground_deletion_waits_for_dependents_and_collects_new_ones():
+    """``propagationPolicy: Foreground``: the owner gets the foregroundDeletion finalizer and a
+    deletionTimestamp, the garbage collector deletes its dependents, deletes any dependent created
+    while the owner waits (kubectl delete --cascade=foreground), and releases the owner once none
+    is left; the owner's own finalizers still hold it after that."""
+    async def body(fake, c):
+        pol = _policy()
+        pol["metadata"]["finalizers"] = ["x/y"]
+        p = await c.create(P, pol)
+        ref = [{"apiVersion": T.API_VERSION, "kind": T.KIND, "name": "p", "uid": p["metadata"]["uid"], "controller": True}]
+
+        def job(name):
+            return {"apiVersion": "batch/v1", "kind": "Job", "metadata": {"name": name, "ownerReferences": ref},
+                    "spec": {"template": {"spec": {"restartPolicy": "Never", "containers": [{"name": "c"}]}}}}
+
+        await c.create(kube.JOBS, job("before"), namespace="ns")
+        await c.delete(P, "p", propagation="Foreground")
+        held = fake.get_object(P, "p")
+        assert held["metadata"]["deletionTimestamp"]
+        assert held["metadata"]["finalizers"] == ["x/y", "foregroundDeletion"]
+        assert fake.get_object(kube.JOBS, "before", "ns") is None
+        created = await c.create(kube.JOBS, job("during"), namespace="ns")  # accepted, then collected
+        assert created["metadata"]["name"] == "during" and fake.get_object(kube.JOBS, "during", "ns") is None
+        unowned = dict(job("unowned"), metadata={"name": "unowned"})
+        await c.create(kube.JOBS, unowned, namespace="ns")
+        await asyncio.sleep(0.4)  # the collector releases the owner: only its own finalizer is left
+        held = fake.get_object(P, "p")
+        assert held["metadata"]["finalizers"] == ["x/y"]
+        await c.create(kube.JOBS, job("after"), namespace="ns")  # no longer collected
+        assert fake.get_object(kube.JOBS, "after", "ns") is not None
+        await c.replace(P, dict(held, metadata=dict(held["metadata"], finalizers=[])))
+        assert fake.get_object(P, "p") is None
+        assert fake.get_object(kube.JOBS, "after", "ns") is None  # background GC once the owner is gone
+        assert fake.get_object(kube.JOBS, "unowned", "ns") is not None
+    _run(body, foreground_hold=0.2)

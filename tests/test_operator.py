@@ -1070,6 +1070,48 @@ def test_cleanup_survives_an_operator_restart_mid_deletion(monkeypatch):
     run(body())
 
 
+def test_foreground_deletion_cleans_every_node_once_and_leaves_no_jobs(monkeypatch):
+    """kubectl delete --cascade=foreground: while the policy carries foregroundDeletion the garbage
+    collector deletes every new dependent of it.  Cleanup Jobs created during the deletion are
+    therefore not owned by the policy (one owned by it would be collected mid-run and the node
+    cleaned again); the finalizer deletes them itself once every node is clean."""
+    from network_operator_amd.operator import reconciler as R
+
+    monkeypatch.setattr(R, "CLEANUP_POLL_S", 0.05)
+
+    async def body():
+        fake = FakeApiServer(foreground_hold=3.0)  # the collector's latency covers the Jobs' creation
+        url = await fake.start()
+        client = ApiClient(KubeConfig(host=url))
+        try:
+            for i in range(3):
+                fake.add_node(f"gpu-node-{i}", {"foo": "bar"})
+            ctl = PolicyController(client, NS, is_openshift=False, workers=2)
+            await ctl.start()
+            await client.create(kube.NETWORKCLUSTERPOLICIES, policy(keepConfigOnRestart=True))
+            await eventually(lambda: (fake.get_object(kube.NETWORKCLUSTERPOLICIES, "policy").get("status") or {})
+                             .get("keptNodes") == [f"gpu-node-{i}" for i in range(3)])
+            await client.delete(kube.NETWORKCLUSTERPOLICIES, "policy", propagation="Foreground")
+            await eventually(lambda: len(fake.list_objects(kube.JOBS)) == 3)
+            jobs = fake.list_objects(kube.JOBS)
+            assert all(not j["metadata"].get("ownerReferences") for j in jobs)
+            await eventually(lambda: "foregroundDeletion" not in
+                             fake.get_object(kube.NETWORKCLUSTERPOLICIES, "policy")["metadata"]["finalizers"], timeout=10)
+            # The collector has released the policy: the Jobs were left alone.
+            assert {j["metadata"]["name"] for j in fake.list_objects(kube.JOBS)} == {j["metadata"]["name"] for j in jobs}
+            for j in jobs:
+                fake.set_job_result(j["metadata"]["name"], NS, True)
+            await eventually(lambda: fake.get_object(kube.NETWORKCLUSTERPOLICIES, "policy") is None)
+            assert fake.list_objects(kube.JOBS) == []  # deleted by the finalizer, not left behind
+            created = [m for m, path in fake.requests if m == "POST" and path.endswith("/jobs")]
+            assert len(created) == 3  # every node cleaned exactly once
+            await ctl.stop()
+        finally:
+            await client.close()
+            await fake.stop()
+    run(body())
+
+
 def test_a_node_that_rejoins_during_its_cleanup_keeps_its_agent(monkeypatch):
     """A node leaves the policy, its cleanup Job starts, and it comes back before the Job ran:
     the Job is withdrawn (the node lock on the node keeps the two apart if it had started) and
