@@ -5,7 +5,8 @@
 // (SURVEY.md §7.7 "hard part 1").  The reference has no answer to this (pkg/lldp/client.go
 // just times out after --wait).  The agent's `--disable-fw-lldp` looks up the driver's
 // private flags and flips the known "firmware LLDP" flag for the duration of its run,
-// restoring the original value on exit:
+// restoring the original value when it exits cleanly (an agent that fails leaves them, like its
+// addresses, to the agent the kubelet restarts, so a crash loop does not flip them every time):
 //
 //   i40e (X710/XL710):      disable-fw-lldp = on
 //   ice  (E810):            fw-lldp-agent   = off
@@ -53,7 +54,7 @@ class Ops {
     virtual bool dcbx_set(const std::string& ifname, uint8_t mode);
 };
 
-// DCBX mode bits in words: "0x0c (firmware, cee, ieee)", "0x05 (host, ieee)".
+// DCBX mode bits in words: "0x0c (firmware, cee, ieee)", "0x09 (host, ieee)".
 std::string dcbx_str(uint8_t mode);
 // An embedded (NIC-firmware or LLD) agent runs DCBX and the port's LLDP: no DCB_CAP_DCBX_HOST.
 bool dcbx_embedded(uint8_t mode);
