@@ -105,6 +105,10 @@ struct Config {
     std::string require_gdr;
     bool disable_fw_lldp = false;
     std::string fw_lldp_flags;                        // extra rules "NAME=0|1,..."
+    // With keep_config: the originals of what --disable-fw-lldp changed are kept in this file
+    // across agent restarts (a restart does not flip the NICs back and forth: some drivers reset
+    // the port when the flag flips) and put back by --cleanup.
+    std::string fw_lldp_state;
     std::string rccl_env_extra;                       // "KEY=VALUE,..." appended to rccl.env
     // Per-rail source routing (L3): NIC k gets routing table base+k (k = its GPU index; NICs
     // without a GPU get the indices after the last GPU's) holding its /30 and its /16 via the
@@ -295,6 +299,8 @@ class Agent {
     std::vector<ethtool::FwLldpResult> fw_lldp_;
     std::vector<std::pair<std::string, std::string>> rccl_env_extra_;
     void disable_fw_lldp();
+    void restore_fw_lldp_from_state();
+    bool persist_fw_lldp() const { return cfg_.keep_config && !cfg_.fw_lldp_state.empty(); }
     void restore_network_manager();
     int apply_lldp_cache(const std::set<int>& listening);  // NICs addressed from the cache (by ifindex)
     // A frame for a NIC that already has an address: confirms a cached Port Description or moves

@@ -88,4 +88,10 @@ FwLldpResult disable_fw_lldp(Ops& ops, const std::string& ifname, const std::vec
 // Puts back the original private flags / DCBX mode if disable_fw_lldp changed them.
 void restore(Ops& ops, const FwLldpResult& r);
 
+// The originals of what was changed, kept on the node across agent restarts (--keep-config
+// with --fw-lldp-state): one line per change, "<ifname> priv 0x<bits>" or "<ifname> dcbx
+// 0x<mode>".  decode_state skips lines it does not understand.
+std::string encode_state(const std::vector<FwLldpResult>& rs);
+std::vector<FwLldpResult> decode_state(const std::string& text);
+
 }  // namespace netop::ethtool

@@ -197,6 +197,12 @@ void Agent::disable_fw_lldp() {
             return;
         }
     }
+    // An earlier agent of this node (--keep-config) may have changed them already: its record
+    // holds the real originals, which this run must neither lose nor take for "already set".
+    std::map<std::string, ethtool::FwLldpResult> earlier;
+    if (persist_fw_lldp())
+        if (auto t = read_file(cfg_.fw_lldp_state))
+            for (auto& e : ethtool::decode_state(*t)) earlier[e.ifname] = e;
     for (auto& n : nics_) {
         auto r = ethtool::disable_fw_lldp(*ethtool_, n.ifname, rules);
         n.fw_lldp = r.summary();
@@ -204,13 +210,51 @@ void Agent::disable_fw_lldp() {
         n.dcbx_embedded = r.dcbx && ethtool::dcbx_embedded(*r.dcbx) && !r.dcbx_changed;
         if (!r.error.empty()) NLOG_W("%s: firmware LLDP: %s", n.ifname.c_str(), r.error.c_str());
         NLOG_V(2, "%s: driver %s, firmware LLDP: %s", n.ifname.c_str(), r.driver.c_str(), n.fw_lldp.c_str());
+        if (auto it = earlier.find(n.ifname); it != earlier.end()) {
+            if (it->second.changed) {
+                r.changed = true;
+                r.original_bits = it->second.original_bits;
+            }
+            if (it->second.dcbx_changed) {
+                r.dcbx_changed = true;
+                r.dcbx = it->second.dcbx;
+            }
+        }
         fw_lldp_.push_back(std::move(r));
     }
+    if (persist_fw_lldp()) {
+        try {
+            const std::string text = ethtool::encode_state(fw_lldp_);
+            if (!text.empty())
+                write_file_atomic(cfg_.fw_lldp_state, text);
+            else if (::unlink(cfg_.fw_lldp_state.c_str()) != 0 && errno != ENOENT)
+                NLOG_W("Could not remove %s: %s", cfg_.fw_lldp_state.c_str(), std::strerror(errno));
+        } catch (const std::exception& e) {
+            NLOG_W("Could not record the firmware LLDP originals in %s: %s", cfg_.fw_lldp_state.c_str(), e.what());
+        }
+    }
+}
+
+void Agent::restore_fw_lldp_from_state() {
+    // --cleanup: what --keep-config agents changed on this node's NICs, from their record.
+    if (cfg_.fw_lldp_state.empty()) return;
+    auto t = read_file(cfg_.fw_lldp_state);
+    if (!t) return;
+    auto recs = ethtool::decode_state(*t);
+    if (!recs.empty() && !ethtool_) ethtool_ = ethtool::make_ioctl_ops();
+    for (const auto& r : recs) {
+        NLOG_I("%s: restoring the NIC's firmware LLDP settings%s%s", r.ifname.c_str(),
+               r.changed ? strfmt(" (private flags 0x%x)", r.original_bits).c_str() : "",
+               r.dcbx_changed ? (" (DCBX " + ethtool::dcbx_str(*r.dcbx) + ")").c_str() : "");
+        ethtool::restore(*ethtool_, r);
+    }
+    if (::unlink(cfg_.fw_lldp_state.c_str()) != 0 && errno != ENOENT)
+        NLOG_W("Could not remove %s: %s", cfg_.fw_lldp_state.c_str(), std::strerror(errno));
 }
 
 void Agent::post_cleanups() {
     NLOG_I("Clean up before exiting...");
-    if (ethtool_)
+    if (ethtool_ && !persist_fw_lldp())  // kept on the node for the next agent / --cleanup otherwise
         for (const auto& r : fw_lldp_) ethtool::restore(*ethtool_, r);
     if (cfg_.lldp_announce && cfg_.mode == "L3" && !cfg_.keep_config) {
         // Shutdown LLDPDU (TTL 0): the switch drops us from its neighbour table right away.
@@ -1726,6 +1770,12 @@ void Agent::cleanup_node() {
             NLOG_W("Could not remove systemd-networkd files: %s", e.what());
             ++errors;
         }
+    }
+    try {
+        restore_fw_lldp_from_state();
+    } catch (const std::exception& e) {
+        NLOG_W("Could not restore the NICs' firmware LLDP settings: %s", e.what());
+        ++errors;
     }
     if (cfg_.disable_nm) {
         nm_keyfile_written_ = true;  // a file of ours from an earlier run (remove_keyfile checks it)

@@ -10,6 +10,7 @@
 
 #include <cctype>
 #include <cerrno>
+#include <cstdlib>
 #include <cstring>
 #include <stdexcept>
 
@@ -218,6 +219,44 @@ void restore(Ops& ops, const FwLldpResult& r) {
             NLOG_W("%s: could not restore the DCBX mode: %s", r.ifname.c_str(), e.what());
         }
     }
+}
+
+std::string encode_state(const std::vector<FwLldpResult>& rs) {
+    std::string out;
+    for (const auto& r : rs) {
+        if (r.changed) out += strfmt("%s priv 0x%x\n", r.ifname.c_str(), r.original_bits);
+        if (r.dcbx_changed && r.dcbx) out += strfmt("%s dcbx 0x%02x\n", r.ifname.c_str(), *r.dcbx);
+    }
+    return out;
+}
+
+std::vector<FwLldpResult> decode_state(const std::string& text) {
+    std::vector<FwLldpResult> out;
+    auto find = [&](const std::string& ifname) -> FwLldpResult& {
+        for (auto& r : out)
+            if (r.ifname == ifname) return r;
+        out.emplace_back();
+        out.back().ifname = ifname;
+        return out.back();
+    };
+    for (const auto& line : split(text, '\n')) {
+        auto f = split(trim(line), ' ');
+        if (f.size() != 3 || f[0].empty() || f[0].size() >= 16) continue;
+        char* end = nullptr;
+        errno = 0;
+        unsigned long v = std::strtoul(f[2].c_str(), &end, 16);
+        if (errno || !end || *end || f[2].empty()) continue;
+        if (f[1] == "priv" && v <= 0xffffffffUL) {
+            auto& r = find(f[0]);
+            r.changed = true;
+            r.original_bits = uint32_t(v);
+        } else if (f[1] == "dcbx" && v <= 0xffUL) {
+            auto& r = find(f[0]);
+            r.dcbx_changed = true;
+            r.dcbx = uint8_t(v);
+        }
+    }
+    return out;
 }
 
 }  // namespace netop::ethtool

@@ -1740,6 +1740,77 @@ TEST(agent_cleanup_mode_removes_what_kept_agents_left) {
     CHECK(st && st->find("cleanup") != std::string::npos);
 }
 
+TEST(ethtool_state_round_trip) {
+    ethtool::FwLldpResult a, b, c;
+    a.ifname = "ens0";
+    a.changed = true;
+    a.original_bits = 0x2;
+    b.ifname = "mlx0";
+    b.dcbx = uint8_t(0x0c);
+    b.dcbx_changed = true;
+    c.ifname = "ens9";  // nothing changed: not recorded
+    auto text = ethtool::encode_state({a, b, c});
+    CHECK_EQ(text, std::string("ens0 priv 0x2\nmlx0 dcbx 0x0c\n"));
+    auto back = ethtool::decode_state(text + "garbage\nens1 priv zz\nens2 dcbx 0x1ff\n\n");
+    CHECK_EQ(back.size(), size_t(2));
+    CHECK(back[0].ifname == "ens0" && back[0].changed && back[0].original_bits == 0x2 && !back[0].dcbx_changed);
+    CHECK(back[1].ifname == "mlx0" && back[1].dcbx_changed && *back[1].dcbx == 0x0c && !back[1].changed);
+}
+
+TEST(agent_keep_config_keeps_firmware_lldp_off_across_restarts_until_cleanup) {
+    // keepConfigOnRestart + disableFirmwareLldp: a roll must not flip the NICs' firmware LLDP
+    // back and forth (some drivers reset the port on a flip), and the originals must survive
+    // agents that find the flag already set; --cleanup puts them back.
+    Fixture f;
+    f.cfg.keep_config = true;
+    f.cfg.disable_fw_lldp = true;
+    f.cfg.lldp_cache = f.tmp.path + "/lldp-cache";
+    f.cfg.fw_lldp_state = f.tmp.path + "/fw-lldp-state";
+    auto make_eth = [] {
+        auto e = std::make_unique<FakeEthtool>();
+        e->drivers = {{"ens0", "ice"}, {"ens1", "mlx5_core"}};
+        return e;
+    };
+    ethtool::PrivFlags ice{{"link-down-on-close", "fw-lldp-agent"}, 0x2};  // firmware agent on
+    uint8_t mlx = DCB_CAP_DCBX_VER_CEE | DCB_CAP_DCBX_VER_IEEE;            // firmware DCBX
+    std::vector<std::pair<std::string, uint32_t>> flag_sets;
+    for (int run = 0; run < 2; ++run) {
+        auto eth = make_eth();
+        eth->flags["ens0"] = ice;
+        eth->dcbx["ens1"] = mlx;
+        FakeEthtool* raw = eth.get();
+        Pipe stop;
+        stop.fire();
+        {
+            agent::Agent a(f.cfg, f.ops, f.all_valid(), f.nm());
+            a.set_ethtool_ops(std::move(eth));
+            a.run(stop.fd[0]);
+            CHECK(a.ready());
+            ice = raw->flags["ens0"];  // what the NIC holds when the agent has gone
+            mlx = raw->dcbx["ens1"];
+            for (auto& x : raw->sets) flag_sets.push_back(x);
+        }
+        CHECK_EQ(ice.bits, uint32_t(0));                        // left off on exit
+        CHECK_EQ(int(mlx), int(DCB_CAP_DCBX_HOST | DCB_CAP_DCBX_VER_CEE | DCB_CAP_DCBX_VER_IEEE));
+        auto st = read_file(f.cfg.fw_lldp_state);
+        CHECK(st && *st == "ens0 priv 0x2\nens1 dcbx 0x0c\n");  // the originals, also after run 2
+    }
+    CHECK_EQ(flag_sets.size(), size_t(1));  // set once, by the first agent; never flipped back
+    agent::Config c = f.cfg;
+    c.cleanup = true;
+    c.keep_config = false;
+    auto eth = make_eth();
+    eth->flags["ens0"] = ice;
+    eth->dcbx["ens1"] = mlx;
+    FakeEthtool* raw = eth.get();
+    agent::Agent k(c, f.ops, std::make_unique<ScriptedLldp>(), f.nm());
+    k.set_ethtool_ops(std::move(eth));
+    k.run(-1);
+    CHECK_EQ(raw->flags["ens0"].bits, uint32_t(0x2));
+    CHECK_EQ(int(raw->dcbx["ens1"]), 0x0c);
+    CHECK(!path_exists(f.cfg.fw_lldp_state));
+}
+
 TEST(agent_node_lock_keeps_two_agents_of_one_kind_apart) {
     // The lock is an abstract unix socket: held by a live agent (here: by the test), a second
     // agent with the same name waits, then fails naming the cause; free, it is taken at once.

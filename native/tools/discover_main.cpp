@@ -95,6 +95,7 @@ int main(int argc, char** argv) {
     fs.add_string("require-gdr", &cfg.require_gdr, "refuse readiness without GPUDirect RDMA: any, peermem, dmabuf (empty = report only)");
     fs.add_bool("disable-fw-lldp", &cfg.disable_fw_lldp, "L3: turn off NIC-firmware LLDP agents while running (i40e disable-fw-lldp, ice fw-lldp-agent; other DCB NICs, e.g. mlx5_core: DCBX handed to the host)");
     fs.add_string("fw-lldp-priv-flag", &cfg.fw_lldp_flags, "extra ethtool private-flag rules NAME=0|1[,...] for --disable-fw-lldp");
+    fs.add_string("fw-lldp-state", &cfg.fw_lldp_state, "with --keep-config: keep the originals of what --disable-fw-lldp changed in this file across restarts instead of restoring them on exit; --cleanup restores them");
     bool ready_check = false;
     fs.add_bool("ready-check", &ready_check, "exit 0 if the readiness label is published, 1 otherwise (readinessProbe)");
     fs.add_bool("help", &show_help, "help for discover");

@@ -48,6 +48,7 @@ RCCL_TOPO_FILE = "rccl-topo.xml"
 # --verify-peers: a switch answers ARP in well under a millisecond; 2 s covers a port that is
 # still coming up, and stays far below the kubelet's restart back-off.
 VERIFY_PEERS_TIMEOUT = "2s"
+FW_LLDP_STATE_FILE = "fw-lldp-state"  # --fw-lldp-state: firmware LLDP originals kept by --keep-config agents
 LLDP_CACHE_FILE = "lldp-cache"  # --lldp-cache, beside the artifacts so it survives pod restarts
 L3_WAIT = "90s"
 
@@ -182,6 +183,9 @@ def agent_args(p: T.NetworkClusterPolicy) -> List[str]:
         args.append(f"--lldp-cache={ARTIFACT_DIR_CONTAINER}/{LLDP_CACHE_FILE}")
     if so.keepConfigOnRestart:
         args.append("--keep-config")
+        if so.disableFirmwareLldp and so.layer == "L3":
+            # what --disable-fw-lldp changed stays changed across restarts; the cleanup Job restores it
+            args.append(f"--fw-lldp-state={ARTIFACT_DIR_CONTAINER}/{FW_LLDP_STATE_FILE}")
     if so.railSwitchPattern and so.layer == "L3":
         args.append(f"--rail-switch-pattern={so.railSwitchPattern}")
     if so.minLinkSpeedGbps:

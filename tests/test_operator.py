@@ -403,6 +403,18 @@ def test_agent_args_fw_lldp_and_metrics_port():
     update_amd_scale_out_daemonset(ds, p, "ns")
     assert "ports" not in c and "--disable-fw-lldp" not in c["args"]
     assert T.NetworkClusterPolicy.from_dict(p.to_dict()).spec.amdScaleOut.disableFirmwareLldp
+    # keepConfigOnRestart: the firmware LLDP originals stay recorded on the node across restarts,
+    # and the node's cleanup Job (same args, --cleanup) restores them.
+    from network_operator_amd.operator.reconciler import cleanup_job
+
+    p.spec.amdScaleOut.layer = "L3"
+    assert not any(a.startswith("--fw-lldp-state") for a in agent_args(p))
+    p.spec.amdScaleOut.keepConfigOnRestart = True
+    state = "--fw-lldp-state=/host/etc/amd/scale-out/fw-lldp-state"
+    assert state in agent_args(p)
+    assert state in cleanup_job(p, "n1", "ns")["spec"]["template"]["spec"]["containers"][0]["args"]
+    p.spec.amdScaleOut.disableFirmwareLldp = False
+    assert not any(a.startswith("--fw-lldp-state") for a in agent_args(p))
 
 
 def test_agent_args_gpudirect_rdma():
