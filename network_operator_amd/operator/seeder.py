@@ -162,6 +162,11 @@ class PolicySeeder:
                 log.warning("policy %s exists and is not this operator's (%s): left as it is", name,
                             f"owner {self.owner}" if self.owner else f"{SEEDER_KEY}={self.seed_id}")
                 continue
+            if cur["metadata"].get("deletionTimestamp"):
+                # Being deleted (by hand, or its nodes are being cleaned): editing its spec would
+                # restart agents on nodes the finalizer is cleaning.  It is created anew once gone.
+                log.info("policy %s is being deleted: it is seeded again once it is gone", name)
+                continue
             new = copy.deepcopy(cur)
             new["spec"] = desired.get("spec", {})
             md = new["metadata"]

@@ -294,6 +294,40 @@ def test_seeder_ownership_is_release_scoped(tmp_path):
     asyncio.run(asyncio.wait_for(body(), 60))
 
 
+def test_seeder_leaves_a_policy_that_is_being_deleted_alone(tmp_path):
+    """A seeded policy under deletion (its finalizer is cleaning nodes) is not edited back to the
+    file's spec, which would roll agents on nodes being cleaned; it is seeded anew once gone."""
+    from network_operator_amd.operator.seeder import PolicySeeder
+
+    async def body():
+        fake = FakeApiServer()
+        url = await fake.start()
+        try:
+            async with ApiClient(KubeConfig(host=url)) as c:
+                f = tmp_path / "p.yaml"
+                f.write_text(yaml.safe_dump({"policies": [_policy("pol", 9000)]}))
+                s = PolicySeeder(c, str(f), seed_id="ns.lease")
+                await s.sync_once()
+                cur = fake.get_object(P, "pol")
+                cur["metadata"]["finalizers"] = ["amd.com/node-cleanup"]
+                await c.replace(P, cur)
+                await c.delete(P, "pol")
+                f.write_text(yaml.safe_dump({"policies": [_policy("pol", 4200)]}))
+                writes = s.writes
+                await s.sync_once()
+                held = fake.get_object(P, "pol")
+                assert held["metadata"]["deletionTimestamp"] and held["spec"]["amdScaleOut"]["mtu"] == 9000
+                assert s.writes == writes
+                await c.replace(P, dict(held, metadata=dict(held["metadata"], finalizers=[])))  # finalized
+                assert fake.get_object(P, "pol") is None
+                await s.sync_once()
+                assert fake.get_object(P, "pol")["spec"]["amdScaleOut"]["mtu"] == 4200
+        finally:
+            await fake.stop()
+
+    asyncio.run(asyncio.wait_for(body(), 60))
+
+
 def test_seed_id_label_is_a_valid_distinct_label_value():
     from network_operator_amd.operator.seeder import seed_id_label
 
