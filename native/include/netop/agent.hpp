@@ -107,7 +107,9 @@ struct Config {
     std::string fw_lldp_flags;                        // extra rules "NAME=0|1,..."
     // With keep_config: the originals of what --disable-fw-lldp changed are kept in this file
     // across agent restarts (a restart does not flip the NICs back and forth: some drivers reset
-    // the port when the flag flips) and put back by --cleanup.
+    // the port when the flag flips) and put back by --cleanup.  Without keep_config the record
+    // still outlives an agent that fails (the next one must not take the changed flags for the
+    // originals) and is restored and removed on a clean exit.
     std::string fw_lldp_state;
     std::string rccl_env_extra;                       // "KEY=VALUE,..." appended to rccl.env
     // Per-rail source routing (L3): NIC k gets routing table base+k (k = its GPU index; NICs

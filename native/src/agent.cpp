@@ -199,8 +199,10 @@ void Agent::disable_fw_lldp() {
     }
     // An earlier agent of this node (--keep-config) may have changed them already: its record
     // holds the real originals, which this run must neither lose nor take for "already set".
+    // (Read without --keep-config too: an agent that failed left them changed, or the policy just
+    // dropped keepConfigOnRestart; this agent then restores the true originals on a clean exit.)
     std::map<std::string, ethtool::FwLldpResult> earlier;
-    if (persist_fw_lldp())
+    if (!cfg_.fw_lldp_state.empty())
         if (auto t = read_file(cfg_.fw_lldp_state))
             for (auto& e : ethtool::decode_state(*t)) earlier[e.ifname] = e;
     for (auto& n : nics_) {
@@ -222,7 +224,7 @@ void Agent::disable_fw_lldp() {
         }
         fw_lldp_.push_back(std::move(r));
     }
-    if (persist_fw_lldp()) {
+    if (!cfg_.fw_lldp_state.empty()) {  // also without --keep-config: an agent that fails leaves them changed
         try {
             const std::string text = ethtool::encode_state(fw_lldp_);
             if (!text.empty())
@@ -254,8 +256,12 @@ void Agent::restore_fw_lldp_from_state() {
 
 void Agent::post_cleanups() {
     NLOG_I("Clean up before exiting...");
-    if (ethtool_ && !persist_fw_lldp())  // kept on the node for the next agent / --cleanup otherwise
+    if (ethtool_ && !persist_fw_lldp()) {  // kept on the node for the next agent / --cleanup otherwise
         for (const auto& r : fw_lldp_) ethtool::restore(*ethtool_, r);
+        if (!cfg_.fw_lldp_state.empty() && !fw_lldp_.empty() && ::unlink(cfg_.fw_lldp_state.c_str()) != 0 &&
+            errno != ENOENT)
+            NLOG_W("Could not remove %s: %s", cfg_.fw_lldp_state.c_str(), std::strerror(errno));
+    }
     if (cfg_.lldp_announce && cfg_.mode == "L3" && !cfg_.keep_config) {
         // Shutdown LLDPDU (TTL 0): the switch drops us from its neighbour table right away.
         for (auto& n : nics_) {

@@ -1757,6 +1757,43 @@ TEST(ethtool_state_round_trip) {
     CHECK(back[1].ifname == "mlx0" && back[1].dcbx_changed && *back[1].dcbx == 0x0c && !back[1].changed);
 }
 
+TEST(agent_failed_start_keeps_the_firmware_lldp_originals_for_the_next_agent) {
+    // Without --keep-config an agent restores the NICs on a clean exit, but one that fails (here:
+    // no LLDP peer within --wait) leaves them changed: its record must keep the originals, or
+    // the next agent finds the flag "already" set and never restores it.
+    Fixture f;
+    f.cfg.wait_ns = 1000000;
+    f.cfg.disable_fw_lldp = true;
+    f.cfg.fw_lldp_state = f.tmp.path + "/fw-lldp-state";
+    ethtool::PrivFlags ice{{"link-down-on-close", "fw-lldp-agent"}, 0x2};
+    {
+        auto eth = std::make_unique<FakeEthtool>();
+        eth->drivers = {{"ens0", "ice"}};
+        eth->flags["ens0"] = ice;
+        FakeEthtool* raw = eth.get();
+        agent::Agent a(f.cfg, f.ops, std::make_unique<ScriptedLldp>(), f.nm());  // silent switch
+        a.set_ethtool_ops(std::move(eth));
+        CHECK_THROWS(a.run(-1));
+        ice = raw->flags["ens0"];
+    }
+    CHECK_EQ(ice.bits, uint32_t(0));
+    CHECK(read_file(f.cfg.fw_lldp_state) == std::optional<std::string>("ens0 priv 0x2\n"));
+    auto eth = std::make_unique<FakeEthtool>();
+    eth->drivers = {{"ens0", "ice"}};
+    eth->flags["ens0"] = ice;
+    FakeEthtool* raw = eth.get();
+    Pipe stop;
+    stop.fire();
+    {
+        agent::Agent b(f.cfg, f.ops, f.all_valid(), f.nm());
+        b.set_ethtool_ops(std::move(eth));
+        b.run(stop.fd[0]);
+        CHECK(b.ready());
+    }
+    CHECK_EQ(raw->flags["ens0"].bits, uint32_t(0x2));  // the true original, restored on the clean exit
+    CHECK(!path_exists(f.cfg.fw_lldp_state));
+}
+
 TEST(agent_keep_config_keeps_firmware_lldp_off_across_restarts_until_cleanup) {
     // keepConfigOnRestart + disableFirmwareLldp: a roll must not flip the NICs' firmware LLDP
     // back and forth (some drivers reset the port on a flip), and the originals must survive
@@ -1796,6 +1833,28 @@ TEST(agent_keep_config_keeps_firmware_lldp_off_across_restarts_until_cleanup) {
         CHECK(st && *st == "ens0 priv 0x2\nens1 dcbx 0x0c\n");  // the originals, also after run 2
     }
     CHECK_EQ(flag_sets.size(), size_t(1));  // set once, by the first agent; never flipped back
+    {
+        // keepConfigOnRestart turned off: the next agent finds the flags already set, takes the
+        // originals from the record and restores those on exit (then the record is gone).
+        agent::Config plain = f.cfg;
+        plain.keep_config = false;
+        auto eth = make_eth();
+        eth->flags["ens0"] = ice;
+        eth->dcbx["ens1"] = mlx;
+        FakeEthtool* raw = eth.get();
+        const std::string saved = *read_file(f.cfg.fw_lldp_state);
+        Pipe stop;
+        stop.fire();
+        {
+            agent::Agent a(plain, f.ops, f.all_valid(), f.nm());
+            a.set_ethtool_ops(std::move(eth));
+            a.run(stop.fd[0]);
+        }
+        CHECK_EQ(raw->flags["ens0"].bits, uint32_t(0x2));
+        CHECK_EQ(int(raw->dcbx["ens1"]), 0x0c);
+        CHECK(!path_exists(f.cfg.fw_lldp_state));
+        write_file_atomic(f.cfg.fw_lldp_state, saved);  // back to the kept state for the cleanup below
+    }
     agent::Config c = f.cfg;
     c.cleanup = true;
     c.keep_config = false;

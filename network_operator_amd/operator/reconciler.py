@@ -183,9 +183,11 @@ def agent_args(p: T.NetworkClusterPolicy) -> List[str]:
         args.append(f"--lldp-cache={ARTIFACT_DIR_CONTAINER}/{LLDP_CACHE_FILE}")
     if so.keepConfigOnRestart:
         args.append("--keep-config")
-        if so.disableFirmwareLldp and so.layer == "L3":
-            # what --disable-fw-lldp changed stays changed across restarts; the cleanup Job restores it
-            args.append(f"--fw-lldp-state={ARTIFACT_DIR_CONTAINER}/{FW_LLDP_STATE_FILE}")
+    if so.disableFirmwareLldp and so.layer == "L3":
+        # The originals of what --disable-fw-lldp changes, on the node: with --keep-config they stay
+        # changed across restarts and the cleanup Job restores them; without, they outlive an agent
+        # that fails and the next clean exit restores them.
+        args.append(f"--fw-lldp-state={ARTIFACT_DIR_CONTAINER}/{FW_LLDP_STATE_FILE}")
     if so.railSwitchPattern and so.layer == "L3":
         args.append(f"--rail-switch-pattern={so.railSwitchPattern}")
     if so.minLinkSpeedGbps:

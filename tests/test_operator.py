@@ -408,9 +408,9 @@ def test_agent_args_fw_lldp_and_metrics_port():
     from network_operator_amd.operator.reconciler import cleanup_job
 
     p.spec.amdScaleOut.layer = "L3"
-    assert not any(a.startswith("--fw-lldp-state") for a in agent_args(p))
-    p.spec.amdScaleOut.keepConfigOnRestart = True
     state = "--fw-lldp-state=/host/etc/amd/scale-out/fw-lldp-state"
+    assert state in agent_args(p)  # a record left by keepConfigOnRestart agents is restored on exit
+    p.spec.amdScaleOut.keepConfigOnRestart = True
     assert state in agent_args(p)
     assert state in cleanup_job(p, "n1", "ns")["spec"]["template"]["spec"]["containers"][0]["args"]
     p.spec.amdScaleOut.disableFirmwareLldp = False
