@@ -6,7 +6,8 @@
 // just times out after --wait).  The agent's `--disable-fw-lldp` looks up the driver's
 // private flags and flips the known "firmware LLDP" flag for the duration of its run,
 // restoring the original value when it exits cleanly (an agent that fails leaves them, like its
-// addresses, to the agent the kubelet restarts, so a crash loop does not flip them every time):
+// addresses, to the agent the kubelet restarts, so a crash loop does not flip them every time;
+// the originals wait in --fw-lldp-state meanwhile, and under --keep-config until --cleanup):
 //
 //   i40e (X710/XL710):      disable-fw-lldp = on
 //   ice  (E810):            fw-lldp-agent   = off
