@@ -2,7 +2,8 @@
 //
 //   lldp      frames from the switch (AF_PACKET) — untrusted, L2-adjacent attacker
 //   dbus      messages from the system bus peer
-//   portdesc  the switch's Port Description string (operator-configured, still untrusted)
+//   portdesc  the switch's Port Description string (operator-configured, still untrusted), and
+//             the agent's --fw-lldp-state record (a hostPath file)
 //   netlink   RTM_NEWLINK payloads (kernel, but parsed with length arithmetic)
 //   arp       ARP payloads from the switch port (--verify-peers) — untrusted, L2-adjacent
 //
@@ -20,6 +21,7 @@
 
 #include "netop/arp.hpp"
 #include "netop/dbus.hpp"
+#include "netop/ethtool.hpp"
 #include "netop/l3.hpp"
 #include "netop/lldp.hpp"
 #include "netop/netlink.hpp"
@@ -53,6 +55,16 @@ extern "C" int LLVMFuzzerTestOneInput(const uint8_t* data, size_t size) {
         auto a = l3::parse_port_description(s, p, &err);
         if (a && (a->local.v ^ a->peer.v) != 3u) __builtin_trap();
     }
+    // The firmware-LLDP record on the node (--fw-lldp-state, a hostPath file): whatever decodes
+    // re-encodes to a record that decodes to the same originals.
+    auto recs = ethtool::decode_state(s);
+    auto again = ethtool::decode_state(ethtool::encode_state(recs));
+    if (again.size() != recs.size()) __builtin_trap();
+    for (size_t i = 0; i < recs.size(); ++i)
+        if (again[i].ifname != recs[i].ifname || again[i].changed != recs[i].changed ||
+            again[i].original_bits != recs[i].original_bits || again[i].dcbx_changed != recs[i].dcbx_changed ||
+            again[i].dcbx != recs[i].dcbx)
+            __builtin_trap();
 #elif NETOP_FUZZ_TARGET == 4
     // Wrap the input as the payload of one RTM_NEWLINK message with a consistent header.
     if (size > 1 << 16) return 0;

@@ -230,6 +230,15 @@ std::string encode_state(const std::vector<FwLldpResult>& rs) {
     return out;
 }
 
+// The kernel's dev_valid_name: 1..15 bytes, not "." or "..", no '/', ':' or whitespace (and, for a
+// record written with %s, printable: a NUL would cut it short).
+static bool valid_ifname(const std::string& n) {
+    if (n.empty() || n.size() >= 16 || n == "." || n == "..") return false;
+    for (unsigned char c : n)
+        if (c <= 0x20 || c >= 0x7f || c == '/' || c == ':') return false;
+    return true;
+}
+
 std::vector<FwLldpResult> decode_state(const std::string& text) {
     std::vector<FwLldpResult> out;
     auto find = [&](const std::string& ifname) -> FwLldpResult& {
@@ -241,7 +250,7 @@ std::vector<FwLldpResult> decode_state(const std::string& text) {
     };
     for (const auto& line : split(text, '\n')) {
         auto f = split(trim(line), ' ');
-        if (f.size() != 3 || f[0].empty() || f[0].size() >= 16) continue;
+        if (f.size() != 3 || !valid_ifname(f[0])) continue;
         char* end = nullptr;
         errno = 0;
         unsigned long v = std::strtoul(f[2].c_str(), &end, 16);

@@ -1755,6 +1755,9 @@ TEST(ethtool_state_round_trip) {
     CHECK_EQ(back.size(), size_t(2));
     CHECK(back[0].ifname == "ens0" && back[0].changed && back[0].original_bits == 0x2 && !back[0].dcbx_changed);
     CHECK(back[1].ifname == "mlx0" && back[1].dcbx_changed && *back[1].dcbx == 0x0c && !back[1].changed);
+    // Names no interface can have (found by the fuzzer: a NUL inside one did not survive re-encoding).
+    CHECK(ethtool::decode_state(std::string("e\0s0 priv 0x1\na/b priv 0x1\n.. priv 0x1\nabcdefghijklmnop priv 0x1\n", 65))
+              .empty());
 }
 
 TEST(agent_failed_start_keeps_the_firmware_lldp_originals_for_the_next_agent) {
