@@ -79,13 +79,17 @@ struct FwLldpResult {
     uint32_t original_bits = 0;
     std::optional<uint8_t> dcbx;  // DCBX mode found (nullopt: no DCB interface, or not asked)
     bool dcbx_changed = false;    // the agent handed DCBX to the host
+    bool dry_run = false;         // inspected only (--dry-run): nothing was set
+    bool would_change = false;    // dry run: the flag / DCBX mode would be changed
     std::string error;         // non-empty on failure
     std::string summary() const;
 };
 
 // Applies the first matching rule on `ifname`; with no applicable private flag, hands an
 // embedded DCBX agent's port to the host (DCB_CMD_SDCBX).  Never throws (errors land in .error).
-FwLldpResult disable_fw_lldp(Ops& ops, const std::string& ifname, const std::vector<FlagRule>& rules);
+// With apply = false (the agent's --dry-run) nothing is set: .would_change says what would be.
+FwLldpResult disable_fw_lldp(Ops& ops, const std::string& ifname, const std::vector<FlagRule>& rules,
+                             bool apply = true);
 // Puts back the original private flags / DCBX mode if disable_fw_lldp changed them.
 void restore(Ops& ops, const FwLldpResult& r);
 

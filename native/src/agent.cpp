@@ -1078,6 +1078,26 @@ void Agent::write_l2_artifacts() {
 }
 
 void Agent::dry_run_report() {
+    if (cfg_.mode == "L3" && cfg_.disable_fw_lldp) {
+        // What --disable-fw-lldp would change (read-only: private flags, DCBX mode).
+        std::vector<ethtool::FlagRule> rules;
+        try {
+            rules = ethtool::parse_rules(cfg_.fw_lldp_flags);
+            if (!ethtool_) ethtool_ = ethtool::make_ioctl_ops();
+            for (auto& n : nics_) {
+                auto r = ethtool::disable_fw_lldp(*ethtool_, n.ifname, rules, false);
+                n.fw_lldp = r.summary();
+                if (r.dcbx) {
+                    n.dcbx = ethtool::dcbx_str(*r.dcbx);
+                    n.dcbx_embedded = ethtool::dcbx_embedded(*r.dcbx);
+                }
+                NLOG_I("dry run: %s (%s): firmware LLDP: %s", n.ifname.c_str(), r.driver.empty() ? "?" : r.driver.c_str(),
+                       n.fw_lldp.c_str());
+            }
+        } catch (const std::exception& e) {
+            NLOG_W("dry run: firmware LLDP not inspected: %s", e.what());
+        }
+    }
     for (const auto& n : nics_) {
         NLOG_I("dry run: %s (%s, mtu %d -> %d, %s): GPU %d %s, RDMA %s, path %s", n.ifname.c_str(),
                n.link.up() ? "up" : "down", n.link.mtu, cfg_.mtu, n.link.mac.str().c_str(), n.gpu_index,

@@ -147,15 +147,18 @@ std::vector<FlagRule> parse_rules(const std::string& spec) {
 
 std::string FwLldpResult::summary() const {
     if (!error.empty()) return "error: " + error;
+    if (dry_run && would_change)
+        return flag.empty() ? "would hand DCBX to the host (now " + dcbx_str(*dcbx) + ")" : "would set " + flag;
     if (!flag.empty()) return (changed ? "set " : "already ") + flag;
     if (dcbx_changed) return "DCBX handed to the host (was " + dcbx_str(*dcbx) + ")";
     if (dcbx) return "no firmware LLDP flag; DCBX " + dcbx_str(*dcbx);
     return "no firmware LLDP flag";
 }
 
-FwLldpResult disable_fw_lldp(Ops& ops, const std::string& ifname, const std::vector<FlagRule>& rules) {
+FwLldpResult disable_fw_lldp(Ops& ops, const std::string& ifname, const std::vector<FlagRule>& rules, bool apply) {
     FwLldpResult r;
     r.ifname = ifname;
+    r.dry_run = !apply;
     try {
         r.driver = ops.driver(ifname);
         PrivFlags pf = ops.get(ifname);
@@ -166,7 +169,9 @@ FwLldpResult disable_fw_lldp(Ops& ops, const std::string& ifname, const std::vec
             r.flag = rule.name + (rule.value ? "=on" : "=off");
             uint32_t bit = 1u << i;
             uint32_t want = rule.value ? (pf.bits | bit) : (pf.bits & ~bit);
-            if (want != pf.bits) {
+            if (want != pf.bits && !apply) {
+                r.would_change = true;
+            } else if (want != pf.bits) {
                 ops.set(ifname, want);
                 r.changed = true;
                 NLOG_I("%s (%s): firmware LLDP agent off via private flag %s", ifname.c_str(), r.driver.c_str(),
@@ -187,7 +192,9 @@ FwLldpResult disable_fw_lldp(Ops& ops, const std::string& ifname, const std::vec
         if (r.dcbx && dcbx_embedded(*r.dcbx)) {
             uint8_t want = uint8_t(DCB_CAP_DCBX_HOST | (*r.dcbx & (DCB_CAP_DCBX_VER_CEE | DCB_CAP_DCBX_VER_IEEE)));
             if (!(want & (DCB_CAP_DCBX_VER_CEE | DCB_CAP_DCBX_VER_IEEE))) want |= DCB_CAP_DCBX_VER_IEEE;
-            if (ops.dcbx_set(ifname, want)) {
+            if (!apply) {
+                r.would_change = true;
+            } else if (ops.dcbx_set(ifname, want)) {
                 r.dcbx_changed = true;
                 NLOG_I("%s (%s): DCBX handed to the host (was %s), so the NIC's embedded agent no longer runs LLDP",
                        ifname.c_str(), r.driver.c_str(), dcbx_str(*r.dcbx).c_str());

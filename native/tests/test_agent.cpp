@@ -1302,6 +1302,27 @@ TEST(agent_dry_run_changes_nothing) {
     CHECK(!a.ready());
 }
 
+TEST(agent_dry_run_reports_what_disable_fw_lldp_would_change) {
+    Fixture f;
+    f.cfg.dry_run = true;
+    f.cfg.disable_fw_lldp = true;
+    f.cfg.sysfs_root = f.tmp.path + "/sys/";
+    auto eth = std::make_unique<FakeEthtool>();
+    eth->drivers = {{"ens0", "ice"}, {"ens1", "mlx5_core"}, {"ens2", "mlx5_core"}};
+    eth->flags["ens0"] = {{"link-down-on-close", "fw-lldp-agent"}, 0x2};
+    eth->dcbx["ens1"] = DCB_CAP_DCBX_VER_CEE | DCB_CAP_DCBX_VER_IEEE;
+    eth->dcbx["ens2"] = DCB_CAP_DCBX_HOST | DCB_CAP_DCBX_VER_IEEE;
+    FakeEthtool* raw = eth.get();
+    agent::Agent a(f.cfg, f.ops, f.all_valid(), f.nm());
+    a.set_ethtool_ops(std::move(eth));
+    a.run(-1);
+    CHECK(raw->sets.empty() && raw->dcbx_sets.empty());  // nothing changed
+    auto st = read_file(f.cfg.status_file);
+    CHECK(st && st->find("\"fw_lldp\":\"would set fw-lldp-agent=off\"") != std::string::npos);
+    CHECK(st->find("\"fw_lldp\":\"would hand DCBX to the host (now 0x0c (firmware, cee, ieee))\"") != std::string::npos);
+    CHECK(st->find("\"fw_lldp\":\"no firmware LLDP flag; DCBX 0x09 (host, ieee)\"") != std::string::npos);
+}
+
 TEST(agent_dry_run_writes_intra_node_rccl_env) {
     Fixture f;
     f.cfg.dry_run = true;
