@@ -194,7 +194,8 @@ fuzz-native:                ## libFuzzer (+ASan/UBSan) on the LLDP, D-Bus, Port 
 	    -mllvm -asan-globals=0 \
 	    -DNETOP_FUZZ_TARGET=$$id -DNETOP_VERSION='"fuzz"' -Inative/include native/fuzz/fuzz_targets.cpp \
 	    native/src/common.cpp native/src/log.cpp native/src/lldp.cpp native/src/l3.cpp native/src/netlink.cpp \
-	    native/src/dbus.cpp native/src/arp.cpp native/src/ethtool.cpp -o _build-fuzz/fuzz_$$name -lpthread || exit 1; \
+	    native/src/dbus.cpp native/src/arp.cpp native/src/ethtool.cpp native/src/artifacts.cpp native/src/topology.cpp \
+	    -o _build-fuzz/fuzz_$$name -lpthread || exit 1; \
 	  mkdir -p _build-fuzz/corpus_$$name; \
 	  _build-fuzz/fuzz_$$name native/fuzz/regressions/* > _build-fuzz/$$name.replay.log 2>&1 || { tail -20 _build-fuzz/$$name.replay.log; exit 1; }; \
 	  _build-fuzz/fuzz_$$name -artifact_prefix=_build-fuzz/$$name- -max_total_time=$(FUZZ_TIME) -rss_limit_mb=2048 \

@@ -1,6 +1,7 @@
 // libFuzzer targets for every parser that reads bytes the agent does not control.
 //
-//   lldp      frames from the switch (AF_PACKET) — untrusted, L2-adjacent attacker
+//   lldp      frames from the switch (AF_PACKET) — untrusted, L2-adjacent attacker — and the
+//             LLDP cache lines made from them
 //   dbus      messages from the system bus peer
 //   portdesc  the switch's Port Description string (operator-configured, still untrusted), and
 //             the agent's --fw-lldp-state record (a hostPath file)
@@ -20,6 +21,7 @@
 #include <vector>
 
 #include "netop/arp.hpp"
+#include "netop/artifacts.hpp"
 #include "netop/dbus.hpp"
 #include "netop/ethtool.hpp"
 #include "netop/l3.hpp"
@@ -38,6 +40,15 @@ extern "C" int LLVMFuzzerTestOneInput(const uint8_t* data, size_t size) {
         auto again = lldp::decode(bytes.data(), bytes.size());
         if (!again || again->port_description != f->port_description || again->ttl != f->ttl) __builtin_trap();
         if (again->max_frame_size() != f->max_frame_size()) __builtin_trap();  // 802.3 org TLV survives
+        // The LLDP cache stores the switch's strings: whatever they hold, they stay inside their
+        // own fields of their own NIC's line (no forged entry for another NIC).
+        artifacts::LldpCacheEntry mine{"02:00:00:00:00:01", "ens0", 1, "", f->system_name.value_or(""),
+                                       f->port_id_str(), f->port_description.value_or("")};
+        artifacts::LldpCacheEntry other{"02:00:00:00:00:02", "ens1", 2, "", "leaf", "swp1", "x 10.0.0.2/30"};
+        auto back = artifacts::decode_lldp_cache(artifacts::encode_lldp_cache({mine, other}));
+        if (back.size() != 2 || back[0].ifname != "ens0" || back[1].ifname != "ens1" ||
+            back[1].port_description != other.port_description || back[0].unix_s != 1)
+            __builtin_trap();
     }
 #elif NETOP_FUZZ_TARGET == 2
     dbus::Message m;

@@ -136,6 +136,10 @@ struct LldpCacheEntry {
 };
 std::vector<LldpCacheEntry> read_lldp_cache(const std::string& path);  // [] when absent / unreadable
 void write_lldp_cache(const std::string& path, const std::vector<LldpCacheEntry>& entries);
+// The file's text (the switch controls System Name, Port ID and Port Description: a tab or line
+// break in them can never make another field or another NIC's line).
+std::string encode_lldp_cache(const std::vector<LldpCacheEntry>& entries);
+std::vector<LldpCacheEntry> decode_lldp_cache(const std::string& text);
 
 // Agent status document (phase timings, per-NIC results) for observability and the bench.
 std::string generate_status(const std::vector<NicState>& nics, const std::map<std::string, int64_t>& phases_ns,

@@ -438,10 +438,13 @@ static std::string one_field(const std::string& s) {
 }
 
 std::vector<LldpCacheEntry> read_lldp_cache(const std::string& path) {
-    std::vector<LldpCacheEntry> out;
     auto text = read_file(path);
-    if (!text) return out;
-    auto lines = split(*text, '\n');
+    return text ? decode_lldp_cache(*text) : std::vector<LldpCacheEntry>{};
+}
+
+std::vector<LldpCacheEntry> decode_lldp_cache(const std::string& text) {
+    std::vector<LldpCacheEntry> out;
+    auto lines = split(text, '\n');
     if (lines.empty() || trim(lines[0]) != kLldpCacheHeader) return out;  // unknown format: ignore
     for (size_t i = 1; i < lines.size(); ++i) {
         auto f = split(lines[i], '\t');
@@ -459,13 +462,17 @@ std::vector<LldpCacheEntry> read_lldp_cache(const std::string& path) {
     return out;
 }
 
-void write_lldp_cache(const std::string& path, const std::vector<LldpCacheEntry>& entries) {
+std::string encode_lldp_cache(const std::vector<LldpCacheEntry>& entries) {
     std::string out = std::string(kLldpCacheHeader) + "\n";
     for (const auto& e : entries)
         out += one_field(e.nic_mac) + "\t" + one_field(e.ifname) + "\t" + std::to_string(e.unix_s) + "\t" +
                one_field(e.peer_mac) + "\t" + one_field(e.system_name) + "\t" + one_field(e.port_id) + "\t" +
                one_field(e.port_description) + "\n";
-    write_file_atomic(path, out, 0644);
+    return out;
+}
+
+void write_lldp_cache(const std::string& path, const std::vector<LldpCacheEntry>& entries) {
+    write_file_atomic(path, encode_lldp_cache(entries), 0644);
 }
 
 // ---------------------------------------------------------------------------
