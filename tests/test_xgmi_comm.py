@@ -26,14 +26,37 @@ def _port():
     return p
 
 
-def _ranks(world, args, **extra):
+def _ranks(world, args, limit_s=100, **extra):
+    """Runs `world` worker ranks; a rank still running after `limit_s` (each dumps its stacks at
+    90 s) is killed and the test fails with every rank's stderr, never by the pytest timeout."""
+    import tempfile
+    import time
+
+    init = tempfile.NamedTemporaryFile(prefix="netop-store-", delete=False)
+    init.close()
+    os.unlink(init.name)  # FileStore creates it; a stale file from an earlier run would confuse it
     env = dict(os.environ, **extra, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_port()), WORLD_SIZE=str(world),
-               PYTHONPATH=str(ROOT))
+               PYTHONPATH=str(ROOT), NETOP_INIT_FILE=init.name)
     procs = [subprocess.Popen([sys.executable, str(WORKER), *args], env=dict(env, RANK=str(r)),
                               stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for r in range(world)]
-    outs = [p.communicate(timeout=120) for p in procs]
+    deadline = time.monotonic() + limit_s
+    outs, hung = [], []
+    for r, p in enumerate(procs):
+        try:
+            outs.append(p.communicate(timeout=max(deadline - time.monotonic(), 1)))
+        except subprocess.TimeoutExpired:
+            p.kill()
+            outs.append(p.communicate())
+            hung.append(r)
+    try:
+        os.unlink(init.name)
+    except OSError:
+        pass
+    report = "\n".join(f"--- rank {r} (rc {p.returncode}) stderr:\n{err[-3000:]}" for r, (p, (_, err)) in
+                       enumerate(zip(procs, outs)))
+    assert not hung, f"rank(s) {hung} still running after {limit_s} s\n{report}"
     for p, (_, err) in zip(procs, outs):
-        assert p.returncode == 0, err[-2000:]
+        assert p.returncode == 0, report
     # each rank's "RESULT ..." line (gloo logs to stdout as well)
     return [next((ln[len("RESULT "):] for ln in o.splitlines() if ln.startswith("RESULT ")), "") for o, _ in outs]
 

@@ -4,6 +4,7 @@
     ... python xgmi_barrier_worker.py timeout
 """
 
+import faulthandler
 import os
 import random
 import sys
@@ -14,9 +15,24 @@ import torch.distributed as dist
 from network_operator_amd.parallel.xgmi_comm import ShmBarrier
 
 
+# A rank that hangs prints every thread's stack and exits, well before the test's own limit, so
+# the failure says where it hung (tests/test_xgmi_comm.py::_ranks shows each rank's stderr).
+faulthandler.dump_traceback_later(float(os.environ.get("NETOP_RANK_HANG_S", "90")), exit=True)
+
+
+def _init(rank: int, world: int) -> None:
+    """gloo over a FileStore when the test gives one (no TCP port that another process on the
+    box could take between the test picking it and rank 0 binding it), else env://."""
+    f = os.environ.get("NETOP_INIT_FILE")
+    if f:
+        dist.init_process_group("gloo", init_method=f"file://{f}", rank=rank, world_size=world)
+    else:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+
+
 def main() -> None:
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    _init(rank, world)
     bar = ShmBarrier(rank, world, None)
     if sys.argv[1] == "order":
         # Every rank's marker for phase k must exist once anyone is past barrier k.
@@ -66,7 +82,7 @@ def ddp() -> None:
     from network_operator_amd.parallel.xgmi_comm import XgmiAllReduce
 
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    _init(rank, world)
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     params = {}
@@ -113,7 +129,7 @@ def collectives() -> None:
     from network_operator_amd.parallel.xgmi_comm import XgmiAllReduce
 
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    _init(rank, world)
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     comm = XgmiAllReduce(8 << 20, device=dev)
@@ -144,7 +160,7 @@ def rail_groups() -> None:
     from network_operator_amd.parallel.rail import node_and_rail_groups
 
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    _init(rank, world)
     node, rail = node_and_rail_groups()
     sums = {}
     for name, g in (("node", node), ("rail", rail)):
@@ -172,7 +188,7 @@ def rail() -> None:
     from network_operator_amd.parallel.rail import RailAllReduce, node_and_rail_groups
 
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    _init(rank, world)
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     node, rail_g = node_and_rail_groups()
