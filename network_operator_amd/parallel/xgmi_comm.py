@@ -35,6 +35,7 @@ import argparse
 import ctypes
 import json
 import os
+import shutil
 import socket
 import subprocess
 import sys
@@ -308,7 +309,8 @@ def _worker(args) -> int:
     devices = [int(x) for x in args.devices.split(",")] if args.devices else list(range(world))
     dev = torch.device("cuda", devices[rank % len(devices)])
     torch.cuda.set_device(dev)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    store = os.environ.get("NETOP_INIT_FILE")  # run(): a FileStore, no TCP port to race for
+    dist.init_process_group("gloo", init_method=f"file://{store}" if store else None, rank=rank, world_size=world)
     sizes = []
     b = args.min_bytes
     while b <= args.bytes:
@@ -394,9 +396,12 @@ def run(world: int, nbytes: int = 1 << 30, min_bytes: Optional[int] = None, iter
     """Spawns `world` rank processes (one per GPU unless `devices` maps several onto one) and
     returns rank 0's result.  Safe to call from inside another distributed job: the children
     get their own rendezvous and none of the parent's launcher variables."""
-    port = _free_port()
     base = {k: v for k, v in os.environ.items() if k not in _LAUNCHER_ENV and not k.startswith("TORCHELASTIC_")}
-    base.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world))
+    # Rendezvous over a FileStore: a free TCP port picked here could be taken by another process
+    # before rank 0 binds it, and the other ranks would then wait for a store that never comes.
+    store_dir = tempfile.mkdtemp(prefix="netop-xgmi-store-")
+    base.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), WORLD_SIZE=str(world),
+                NETOP_INIT_FILE=os.path.join(store_dir, "store"))
     cmd = [sys.executable, "-m", "network_operator_amd.parallel.xgmi_comm", "--worker", "--bytes", str(nbytes),
            "--min-bytes", str(min_bytes or nbytes), "--iters", str(iters), "--warmup", str(warmup), "--algos", algos,
            "--timeout", str(min(timeout, 60.0))]
@@ -418,12 +423,14 @@ def run(world: int, nbytes: int = 1 << 30, min_bytes: Optional[int] = None, iter
             p.kill()
         for p in procs:
             p.wait()
+        shutil.rmtree(store_dir, ignore_errors=True)
         raise TimeoutError(f"xGMI all-reduce benchmark did not finish within {timeout} s")
     outs = []
     for f in logs:
         f.seek(0)
         outs.append(f.read())
         f.close()
+    shutil.rmtree(store_dir, ignore_errors=True)
     bad = [(r, p.returncode, o[-1500:]) for r, (p, o) in enumerate(zip(procs, outs)) if p.returncode != 0]
     if bad:
         raise RuntimeError(f"rank {bad[0][0]} exited {bad[0][1]}: {bad[0][2]}")

@@ -37,17 +37,27 @@ def _ranks(world, args, limit_s=100, **extra):
     os.unlink(init.name)  # FileStore creates it; a stale file from an earlier run would confuse it
     env = dict(os.environ, **extra, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_port()), WORLD_SIZE=str(world),
                PYTHONPATH=str(ROOT), NETOP_INIT_FILE=init.name)
+    # Output to files, not pipes: waiting on rank 0 while rank 1 fills its pipe (64 KiB of
+    # warnings) would block rank 1 in write() and with it every rank's next barrier.
+    files = [(tempfile.TemporaryFile(mode="w+"), tempfile.TemporaryFile(mode="w+")) for _ in range(world)]
     procs = [subprocess.Popen([sys.executable, str(WORKER), *args], env=dict(env, RANK=str(r)),
-                              stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for r in range(world)]
+                              stdout=files[r][0], stderr=files[r][1], text=True) for r in range(world)]
     deadline = time.monotonic() + limit_s
-    outs, hung = [], []
+    hung = []
     for r, p in enumerate(procs):
         try:
-            outs.append(p.communicate(timeout=max(deadline - time.monotonic(), 1)))
+            p.wait(timeout=max(deadline - time.monotonic(), 1))
         except subprocess.TimeoutExpired:
             p.kill()
-            outs.append(p.communicate())
+            p.wait()
             hung.append(r)
+    outs = []
+    for fo, fe in files:
+        fo.seek(0)
+        fe.seek(0)
+        outs.append((fo.read(), fe.read()))
+        fo.close()
+        fe.close()
     try:
         os.unlink(init.name)
     except OSError:
