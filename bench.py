@@ -55,6 +55,7 @@ from typing import Optional
 
 METRIC = "node scale-out-ready latency (s) + rccl all-reduce busbw GB/s at 1/2/4/8 GPU"
 STORE_KEY = "netop/bench/artifacts"
+STORE_FILE_ENV = "NETOP_BENCH_STORE"  # FileStore path of a rendezvous without a launcher
 # Test hooks (CPU rehearsal of the xGMI link check): XML files read as RCCL's topology dump of the
 # run with the artifacts / of the RCCL-defaults run.
 FAKE_DUMP_ENV = "NETOP_BENCH_FAKE_RCCL_DUMP"
@@ -99,10 +100,12 @@ def _spawn_ranks(n: int, argv: list[str], device: str, deadline: float) -> int:
             print(f"bench.py --gpus {n}: only {have} GPU(s) visible", file=sys.stderr)
             return 2
     port = _free_port()
+    store_dir = tempfile.mkdtemp(prefix="netop-bench-store-")
     procs = {}
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
-                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                   **{STORE_FILE_ENV: os.path.join(store_dir, "store")})
         procs[r] = subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env)
     rc, killed = 0, set()
     try:
@@ -131,6 +134,7 @@ def _spawn_ranks(n: int, argv: list[str], device: str, deadline: float) -> int:
                 q.wait(30)
             except subprocess.TimeoutExpired:
                 q.kill()
+        shutil.rmtree(store_dir, ignore_errors=True)
     return rc
 
 
@@ -180,7 +184,7 @@ def node_ready_gpu_side(sysfs: str = "/sys/") -> dict:
 
 
 _LAUNCH_ENV = ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK", "ROLE_WORLD_SIZE",
-               "MASTER_ADDR", "MASTER_PORT")
+               "MASTER_ADDR", "MASTER_PORT", STORE_FILE_ENV)
 
 
 def _probe_cmd(world: int, nbytes: int, steps: int, device: str, warmup: int = 2) -> list:
@@ -255,14 +259,21 @@ def _rccl_autotune(store, rank: int, world: int, nbytes: int, budget_s: float = 
 # The operator's artifacts, before RCCL starts
 # ------------------------------------------------------------------------------------------
 def _store(world: int, timeout_s: float):
-    """The rendezvous store (torchrun's agent store under torchrun; rank 0 hosts it otherwise),
-    shared with init_process_group: it carries the artifacts from rank 0 to every rank before
-    any RCCL communicator exists."""
+    """The rendezvous store (torchrun's agent store under torchrun; without a launcher a
+    FileStore, so no TCP port picked here can be taken by another process before rank 0 binds
+    it: that failed a box run with EADDRINUSE), shared with init_process_group: it carries the
+    artifacts from rank 0 to every rank before any RCCL communicator exists."""
     from datetime import timedelta
 
     import torch.distributed as dist
 
-    store, _, _ = next(dist.rendezvous("env://", timeout=timedelta(seconds=timeout_s)))
+    f = os.environ.get(STORE_FILE_ENV)
+    if f:
+        rank = int(os.environ.get("RANK", "0"))
+        store, _, _ = next(dist.rendezvous(f"file://{f}", rank=rank, world_size=world,
+                                           timeout=timedelta(seconds=timeout_s)))
+    else:
+        store, _, _ = next(dist.rendezvous("env://", timeout=timedelta(seconds=timeout_s)))
     return store
 
 
@@ -473,8 +484,11 @@ def main(argv=None) -> int:
         print(f"bench.py: --gpus={args.gpus} but the launcher started WORLD_SIZE={world} ranks", file=sys.stderr)
         return 2
     base_env = dict(os.environ)  # before any artifact or knob is exported: what the extras start from
-    if "WORLD_SIZE" not in os.environ:  # one rank, no launcher: a rendezvous of its own, on a free port
-        os.environ.update(RANK="0", WORLD_SIZE="1", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    own_store = None
+    if "WORLD_SIZE" not in os.environ:  # one rank, no launcher: a rendezvous of its own (a FileStore)
+        own_store = tempfile.mkdtemp(prefix="netop-bench-store-")
+        os.environ.update(RANK="0", WORLD_SIZE="1", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()),
+                          **{STORE_FILE_ENV: os.path.join(own_store, "store")})
 
     import torch
     import torch.distributed as dist
@@ -720,6 +734,8 @@ def main(argv=None) -> int:
     dist.destroy_process_group()
     if rank == 0 and art is not None and art["doc"].get("scratch"):
         shutil.rmtree(art["doc"]["dir"], ignore_errors=True)
+    if own_store:
+        shutil.rmtree(own_store, ignore_errors=True)
     return rc
 
 

@@ -31,7 +31,7 @@ from typing import Dict, List, Optional
 HANG_ENV = "NETOP_BENCH_HANG_EXTRA"
 NAME_ENV = "NETOP_BENCH_EXTRA_NAME"
 LAUNCH_ENV = ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK", "ROLE_WORLD_SIZE",
-              "MASTER_ADDR", "MASTER_PORT", "GROUP_WORLD_SIZE", "ROLE_NAME")
+              "MASTER_ADDR", "MASTER_PORT", "GROUP_WORLD_SIZE", "ROLE_NAME", "NETOP_BENCH_STORE")
 
 
 def maybe_hang() -> None:
