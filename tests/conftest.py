@@ -54,10 +54,11 @@ def single_rank_pg(cuda_device):
     """A 1-rank RCCL process group for the whole GPU session (one init per process)."""
     import torch.distributed as dist
 
-    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-    os.environ.setdefault("MASTER_PORT", "29611")
+    import tempfile
+
+    store = os.path.join(tempfile.mkdtemp(prefix="netop-pg-"), "store")  # a FileStore: no TCP port to collide on
     if not dist.is_initialized():
-        dist.init_process_group("nccl", rank=0, world_size=1, device_id=cuda_device)
+        dist.init_process_group("nccl", init_method=f"file://{store}", rank=0, world_size=1, device_id=cuda_device)
     yield
     if dist.is_initialized():
         dist.destroy_process_group()

@@ -119,7 +119,8 @@ def test_topo_xml_extra_interface_without_rdma(native, tmp_path):
 _RCCL_INIT = textwrap.dedent("""
     import os, sys, torch, torch.distributed as dist
     d = torch.device("cuda", 0); torch.cuda.set_device(d)
-    dist.init_process_group("nccl", rank=0, world_size=1, device_id=d)
+    dist.init_process_group("nccl", init_method="file://" + os.environ["NETOP_TEST_STORE"], rank=0, world_size=1,
+                            device_id=d)
     x = torch.ones(4096, device=d); dist.all_reduce(x); torch.cuda.synchronize()
     dist.destroy_process_group()
 """)
@@ -127,7 +128,7 @@ _RCCL_INIT = textwrap.dedent("""
 
 def _rccl_dump(tmp_path, topo_file, extra_env=None, tag="run"):
     dump = tmp_path / f"dump_{tag}.xml"
-    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(29700 + hash(tag) % 200),
+    env = dict(os.environ, NETOP_TEST_STORE=str(tmp_path / f"store_{tag}"),
                NCCL_TOPO_DUMP_FILE=str(dump), NCCL_DEBUG="INFO", NCCL_DEBUG_SUBSYS="INIT,GRAPH,NET")
     if topo_file:
         env["NCCL_TOPO_FILE"] = str(topo_file)
