@@ -147,6 +147,12 @@ struct Config {
     // process dies, SIGKILL included.  "" = off (discover's --node-lock defaults it from the
     // label file, so an amd-so and a host-nic agent never wait for each other).
     std::string node_lock;
+    // One owner per NIC: an abstract unix socket per interface ("netop-nic:<ifname>"), taken in
+    // name order after discovery and held for the agent's lifetime, whatever the label file.  An
+    // amd-so and a host-nic agent (or two host-nic policies) that select the same NIC can then
+    // never configure it concurrently: the second waits node_lock_wait_ns and fails naming the
+    // NIC.  Off here (unit tests run several agents in one process); discover turns it on.
+    bool nic_locks = false;
     // Rail cabling check (L3): the NIC of GPU k must be cabled to a switch whose LLDP System Name
     // matches this ECMAScript regex with "{rail}" replaced by k (e.g. "leaf-r{rail}-.*" for a
     // rail-optimized fabric).  A NIC on the wrong leaf still works but crosses the spine, so a
@@ -230,6 +236,7 @@ class Agent {
     bool ready() const { return ready_; }
     const topo::XgmiReport& xgmi() const { return xgmi_; }
     const topo::GdrReport& gdr() const { return gdr_; }
+    const std::vector<std::pair<std::string, std::string>>& excluded() const { return excluded_; }
 
     // Replaces the ethtool ioctl table (tests inject fakes).
     void set_ethtool_ops(std::unique_ptr<ethtool::Ops> ops) { ethtool_ = std::move(ops); }
@@ -271,6 +278,9 @@ class Agent {
     void remove_rail_routing();             // every NIC's
     void write_artifacts();
     void write_l2_artifacts();
+    // L2: waits up to link_wait_ns for carrier on every up NIC; marks the others no_carrier.
+    // False when stop_fd fired meanwhile.
+    bool wait_carrier(int stop_fd);
     void write_rccl_env_file();
     std::string write_topo();  // returns the NCCL_TOPO_FILE value for rccl.env ("" = none)
     // The topology XML depends only on sysfs and the NIC set, both fixed once discovery is done:
@@ -312,7 +322,22 @@ class Agent {
     bool nm_keyfile_written_ = false;
     std::vector<std::string> nm_unmanaged_;
     int node_lock_fd_ = -1;
+    std::vector<int> nic_lock_fds_;
     void acquire_node_lock(int stop_fd);
+    void acquire_nic_locks(int stop_fd);
+    // Binds the abstract socket `name` (waiting up to `deadline` while another process holds it);
+    // the fd, or throws AgentError(busy) at the deadline.
+    int take_lock(const std::string& name, int64_t deadline, int stop_fd, const std::string& waiting,
+                  const std::string& busy);
+    // The node's own interfaces.  Every mode refuses to touch a NIC that carries a default route
+    // (refuse_uplinks); rdma discovery also leaves out NICs holding addresses or routes the agent
+    // never installs (node_owned_reason), unless --interfaces names them.
+    std::vector<int> uplinks_;
+    bool uplinks_read_ = false;
+    const std::vector<int>& uplinks();
+    std::string node_owned_reason(const nl::LinkInfo& l);
+    void refuse_uplinks();
+    std::vector<std::pair<std::string, std::string>> excluded_;  // discovered but left alone, and why
 
    public:
     // Prometheus text exposition of the agent state (served on Config::metrics_addr).

@@ -66,6 +66,8 @@ struct RouteSpec {
     uint8_t table = RT_TABLE_MAIN;
     uint8_t type = RTN_UNICAST;
     uint32_t priority = 0;
+    // Listing only: the output interfaces of a multipath route's next hops (RTA_MULTIPATH).
+    std::vector<int> nexthops;
     std::string str() const;
 };
 
@@ -126,6 +128,10 @@ class NetOps {
         (void)ifindex;
         return std::nullopt;
     }
+    // Interfaces a default route (0.0.0.0/0, and ::/0 where the source lists IPv6) leaves
+    // through, in any table but the local one: the node's own uplinks, which the agent never
+    // flushes or re-MTUs.  The base implementation reads route_list(0).
+    virtual std::vector<int> default_route_links();
 };
 
 class Rtnl final : public NetOps {
@@ -149,6 +155,7 @@ class Rtnl final : public NetOps {
     void link_set_mtu(int ifindex, int mtu) override;
     std::unique_ptr<LinkWatcher> subscribe_links() override;
     std::optional<LinkStats> link_stats(int ifindex) override;
+    std::vector<int> default_route_links() override;  // IPv4 and IPv6
 
     // Extra operations (harness / diagnostics; not part of the injectable table).
     LinkInfo link_by_index(int ifindex);

@@ -76,6 +76,10 @@ struct NicState {
     std::optional<uint64_t> rx_at_listen;  // link rx_packets when the LLDP wait began
     std::string lldp_silent;
 
+    // L2: admin-up but no carrier (IFF_LOWER_UP) within --link-wait: an unplugged cable, a dead
+    // switch port.  Not configured, not counted for readiness until the carrier comes.
+    bool no_carrier = false;
+
     // Monitor
     bool degraded = false;  // link went down / lost carrier after readiness
     int flaps = 0;

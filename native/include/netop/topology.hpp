@@ -66,8 +66,8 @@ struct GpuNicPair {
 };
 
 // Affine: GPU-paired scale-out NICs.  Accel: reference layout (netdevs under the accelerator
-// function).  Rdma: every RDMA-capable NIC of the driver allow-list, no GPU pairing (the
-// host-nic configuration type).  None: --interfaces only.
+// function).  Rdma: every RDMA-capable NIC of the driver allow-list that is not a GPU's scale-out
+// rail (the host-nic configuration type).  None: --interfaces only.
 enum class DiscoveryMode { Affine, Accel, Rdma, None };
 std::optional<DiscoveryMode> parse_discovery_mode(std::string_view s);
 
@@ -77,6 +77,12 @@ struct DiscoveryOptions {
     // Empty = any PCI network driver.
     std::vector<std::string> nic_drivers{"mlx5_core", "bnxt_en", "ionic", "ice", "irdma", "i40e", "qede", "cxgb4"};
     PathType max_path = PathType::PXB;  // NICs farther than this from every GPU are not scale-out NICs
+    // Rdma mode: leave out every NIC within `gpu_rail_path` of an accelerator function.  Those are
+    // the GPUs' scale-out rails, which the amd-so agent owns (whatever driver list it runs with);
+    // the reference can never reach them from another agent either, since it only ever enumerates
+    // netdevs under the accelerator's own PCI functions (cmd/discover/network.go:34,88-119).
+    bool exclude_gpu_rails = true;
+    PathType gpu_rail_path = PathType::PXB;
 };
 
 // `topo_attrs`: also read the subsystem ids and the link attributes, which only the topology
@@ -127,6 +133,8 @@ struct DiscoveryResult {
     std::vector<Nic> nics;            // every candidate PCI NIC seen
     std::vector<GpuNicPair> pairs;    // GPU -> NIC assignment (Affine mode)
     std::vector<std::string> ifnames; // selected scale-out interfaces, in GPU order
+    // Candidates discovery left out, with the reason (Rdma mode: the GPUs' scale-out rails).
+    std::vector<std::pair<std::string, std::string>> excluded;
 };
 DiscoveryResult discover(const DiscoveryOptions& opt, const std::string& root = sysfs_root());
 

@@ -175,6 +175,21 @@ PYBIND11_MODULE(_netop_native, m) {
             }
             return l;
         }, py::arg("table") = int(RT_TABLE_MAIN))
+        .def("route_append", [](nl::Rtnl& r, const std::string& dst, py::object gateway, int ifindex, int protocol) {
+            nl::RouteSpec rs;
+            auto d = Ipv4Prefix::parse(dst);
+            if (!d) throw py::value_error("bad CIDR");
+            rs.dst = *d;
+            if (!gateway.is_none()) {
+                auto g = Ipv4::parse(gateway.cast<std::string>());
+                if (!g) throw py::value_error("bad gateway");
+                rs.gateway = *g;
+            }
+            rs.ifindex = ifindex;
+            rs.protocol = uint8_t(protocol);
+            r.route_append(rs);
+        }, py::arg("dst"), py::arg("gateway") = py::none(), py::arg("ifindex") = 0, py::arg("protocol") = int(RTPROT_BOOT))
+        .def("default_route_links", &nl::Rtnl::default_route_links)
         .def("link_set_up", &nl::Rtnl::link_set_up)
         .def("link_set_down", &nl::Rtnl::link_set_down)
         .def("link_set_mtu", &nl::Rtnl::link_set_mtu)
@@ -197,12 +212,14 @@ PYBIND11_MODULE(_netop_native, m) {
     });
 
     // ---- topology -----------------------------------------------------------
-    m.def("discover", [](const std::string& root, const std::string& mode, py::object drivers, const std::string& accel) {
+    m.def("discover", [](const std::string& root, const std::string& mode, py::object drivers, const std::string& accel,
+                         bool include_gpu_rails) {
         topo::DiscoveryOptions o;
         auto md = topo::parse_discovery_mode(mode);
         if (!md) throw py::value_error("bad mode");
         o.mode = *md;
         o.accel_driver = accel;
+        o.exclude_gpu_rails = !include_gpu_rails;
         if (!drivers.is_none()) o.nic_drivers = drivers.cast<std::vector<std::string>>();
         auto r = topo::discover(o, root);
         py::dict d;
@@ -236,8 +253,12 @@ PYBIND11_MODULE(_netop_native, m) {
         d["nics"] = nics;
         d["pairs"] = pairs;
         d["ifnames"] = r.ifnames;
+        py::dict excluded;
+        for (auto& [n, why] : r.excluded) excluded[py::str(n)] = why;
+        d["excluded"] = excluded;
         return d;
-    }, py::arg("root"), py::arg("mode") = "affine", py::arg("drivers") = py::none(), py::arg("accel_driver") = "amdgpu");
+    }, py::arg("root"), py::arg("mode") = "affine", py::arg("drivers") = py::none(), py::arg("accel_driver") = "amdgpu",
+       py::arg("include_gpu_rails") = false);
     m.def("rccl_topo_xml", [](const std::string& root, const std::string& mode, py::object interfaces, int version,
                               py::object cpu) {
         topo::DiscoveryOptions o;

@@ -114,44 +114,63 @@ Agent::Agent(Config cfg, nl::NetOps& ops, std::unique_ptr<LldpSource> lldp, NmFa
     };
 }
 
-void Agent::acquire_node_lock(int stop_fd) {
-    if (cfg_.node_lock.empty() || node_lock_fd_ >= 0) return;
+int Agent::take_lock(const std::string& name, int64_t deadline, int stop_fd, const std::string& waiting,
+                     const std::string& busy) {
     sockaddr_un sa{};
     sa.sun_family = AF_UNIX;
-    const std::string name = "netop-agent:" + cfg_.node_lock;
     const size_t n = std::min(name.size(), sizeof sa.sun_path - 1);
     std::memcpy(sa.sun_path + 1, name.data(), n);  // abstract: sun_path[0] == 0
     const socklen_t len = socklen_t(offsetof(sockaddr_un, sun_path) + 1 + n);
-    const int64_t deadline = mono_ns() + cfg_.node_lock_wait_ns;
     bool waited = false;
     for (;;) {
         int fd = ::socket(AF_UNIX, SOCK_STREAM | SOCK_CLOEXEC, 0);
-        if (fd < 0) throw AgentError(std::string("node lock: socket: ") + std::strerror(errno));
+        if (fd < 0) throw AgentError("lock " + name + ": socket: " + std::strerror(errno));
         if (::bind(fd, reinterpret_cast<sockaddr*>(&sa), len) == 0) {
-            node_lock_fd_ = fd;
-            if (waited) NLOG_I("Node lock '%s' acquired", cfg_.node_lock.c_str());
-            return;
+            if (waited) NLOG_I("Lock '%s' acquired", name.c_str());
+            return fd;
         }
         const int err = errno;
         ::close(fd);
-        if (err != EADDRINUSE) throw AgentError(std::string("node lock: bind: ") + std::strerror(err));
-        if (!waited) NLOG_I("Node lock '%s' is held by another agent on this node: waiting", cfg_.node_lock.c_str());
+        if (err != EADDRINUSE) throw AgentError("lock " + name + ": bind: " + std::strerror(err));
+        if (!waited) NLOG_I("%s: waiting", waiting.c_str());
         waited = true;
-        if (mono_ns() >= deadline)
-            throw AgentError("Another agent (or its cleanup) holds the node lock '" + cfg_.node_lock +
-                             "': two policies of one configuration type select this node, or the previous agent is "
-                             "still exiting");
+        if (mono_ns() >= deadline) throw AgentError(busy);
         if (stop_fd >= 0) {
             pollfd p{stop_fd, POLLIN, 0};
-            if (::poll(&p, 1, 100) > 0) throw AgentError("Interrupted while waiting for the node lock");
+            if (::poll(&p, 1, 100) > 0) throw AgentError("Interrupted while waiting for lock " + name);
         } else {
             ::usleep(100000);
         }
     }
 }
 
+void Agent::acquire_node_lock(int stop_fd) {
+    if (cfg_.node_lock.empty() || node_lock_fd_ >= 0) return;
+    node_lock_fd_ = take_lock("netop-agent:" + cfg_.node_lock, mono_ns() + cfg_.node_lock_wait_ns, stop_fd,
+                              "Node lock '" + cfg_.node_lock + "' is held by another agent on this node",
+                              "Another agent (or its cleanup) holds the node lock '" + cfg_.node_lock +
+                                  "': two policies of one configuration type select this node, or the previous agent "
+                                  "is still exiting");
+}
+
+void Agent::acquire_nic_locks(int stop_fd) {
+    if (!cfg_.nic_locks || !nic_lock_fds_.empty()) return;
+    // Name order: two agents wanting overlapping NIC sets can never wait on each other in a cycle.
+    std::vector<std::string> names;
+    for (const auto& n : nics_) names.push_back(n.ifname);
+    std::sort(names.begin(), names.end());
+    const int64_t deadline = mono_ns() + cfg_.node_lock_wait_ns;
+    for (const auto& name : names)
+        nic_lock_fds_.push_back(take_lock(
+            "netop-nic:" + name, deadline, stop_fd, "NIC '" + name + "' is held by another agent on this node",
+            "Another agent holds NIC '" + name +
+                "' (its NIC lock): an amd-so and a host-nic policy, or two host-nic policies, select this NIC, or the "
+                "previous agent is still exiting.  Every NIC has one owner: select it in one policy only"));
+}
+
 Agent::~Agent() {
     if (node_lock_fd_ >= 0) ::close(node_lock_fd_);
+    for (int fd : nic_lock_fds_) ::close(fd);
     // Both socket sets wait for an RCU grace period when closed: overlap the two waits, so
     // --verify-peers adds nothing to SIGTERM -> exit.
     std::thread closing;
@@ -311,9 +330,108 @@ void Agent::restore_network_manager() {
     }
 }
 
+const std::vector<int>& Agent::uplinks() {
+    if (!uplinks_read_) {
+        try {
+            uplinks_ = ops_.default_route_links();
+        } catch (const std::exception& e) {
+            // Not knowing which NIC is the node's uplink is no reason to guess: touch nothing.
+            throw AgentError(std::string("Cannot read the node's routes (needed to leave its own uplinks alone): ") +
+                             e.what());
+        }
+        uplinks_read_ = true;
+    }
+    return uplinks_;
+}
+
+namespace {
+std::string protocol_name(uint8_t p) {
+    switch (p) {
+        case RTPROT_KERNEL: return "kernel";
+        case RTPROT_BOOT: return "boot";
+        case RTPROT_STATIC: return "static";
+        case RTPROT_RA: return "ra";
+        case RTPROT_DHCP: return "dhcp";
+    }
+    return std::to_string(int(p));
+}
+}  // namespace
+
+std::string Agent::node_owned_reason(const nl::LinkInfo& l) {
+    const auto& up = uplinks();
+    if (std::find(up.begin(), up.end(), l.index) != up.end()) return "carries the node's default route";
+    // The agent only ever assigns /30s (the LLDP point-to-point links): anything else on the NIC
+    // was put there by the node (DHCP, netplan, a static management address).
+    const auto addrs = ops_.addr_list(l.index, AF_INET);
+    for (const auto& a : addrs)
+        if (a.prefixlen != l3::kPointToPointMask)
+            return "holds " + a.prefix().str() + ", an address the agent never assigns (it only uses /30s)";
+    // Routes through it that the agent does not install: its /30 (kernel), the /16 via the switch
+    // end of a /30 of this NIC (boot), and its rail tables (kRailProtocol).
+    auto agents = [&](const nl::RouteSpec& r) {
+        if (r.protocol == kRailProtocol) return true;
+        if (r.protocol == RTPROT_KERNEL && r.dst.len == l3::kPointToPointMask) return true;
+        if (r.protocol == RTPROT_BOOT && r.dst.len == l3::kRoutedNetworkMask && r.gateway)
+            for (const auto& a : addrs)
+                if (a.prefix().contains(*r.gateway)) return true;
+        return false;
+    };
+    for (const auto& r : ops_.route_list(0)) {
+        if (r.table == RT_TABLE_LOCAL || r.type != RTN_UNICAST) continue;
+        if (r.ifindex != l.index && std::find(r.nexthops.begin(), r.nexthops.end(), l.index) == r.nexthops.end()) continue;
+        if (!agents(r))
+            return strfmt("has the route %s (protocol %s) that the agent does not install", r.dst.masked().str().c_str(),
+                          protocol_name(r.protocol).c_str());
+    }
+    return "";
+}
+
+void Agent::refuse_uplinks() {
+    // Flushing the addresses of, or re-MTUing, the NIC the node reaches its gateway through can
+    // cut the kubelet off the cluster: never, in any mode, whoever named the NIC.
+    std::vector<std::string> bad;
+    for (const auto& n : nics_) {
+        const auto& up = uplinks();
+        if (std::find(up.begin(), up.end(), n.link.index) != up.end()) bad.push_back(n.ifname);
+    }
+    if (bad.empty()) return;
+    const std::string what = join(bad, ", ");
+    if (cfg_.dry_run) {
+        NLOG_W("dry run: would refuse to configure %s: the node's default route leaves through it", what.c_str());
+        for (const auto& b : bad) excluded_.emplace_back(b, "carries the node's default route (refused)");
+        return;
+    }
+    throw AgentError("Refusing to configure " + what +
+                     ": the node's default route leaves through it (flushing its addresses or changing its MTU could "
+                     "cut the node off the network).  Select only scale-out / host RDMA NICs in the policy");
+}
+
 std::vector<std::string> Agent::collect_interfaces() {
     std::string root = cfg_.sysfs_root.empty() ? topo::sysfs_root() : cfg_.sysfs_root;
     disc_ = topo::discover(cfg_.discovery, root);
+    excluded_ = disc_.excluded;
+    for (const auto& [name, why] : disc_.excluded) NLOG_I("Leaving '%s' alone: %s", name.c_str(), why.c_str());
+    if (cfg_.discovery.mode == topo::DiscoveryMode::Rdma) {
+        // Host RDMA NICs: never the node's own management / frontend NICs.  A NIC --interfaces
+        // names explicitly is the operator's choice (below), except for the default route.
+        std::vector<std::string> kept;
+        for (const auto& name : disc_.ifnames) {
+            std::string why;
+            try {
+                why = node_owned_reason(ops_.link_by_name(name));
+            } catch (const AgentError&) {
+                throw;
+            } catch (const std::exception&) {  // not in this namespace: reported as missing later
+            }
+            if (why.empty()) {
+                kept.push_back(name);
+                continue;
+            }
+            NLOG_I("Leaving '%s' alone: it %s", name.c_str(), why.c_str());
+            excluded_.emplace_back(name, "the node's own NIC: it " + why);
+        }
+        disc_.ifnames = kept;
+    }
     std::vector<std::string> names = disc_.ifnames;
     for (auto& p : disc_.pairs) {
         const auto& g = disc_.gpus[size_t(p.gpu)];
@@ -1060,9 +1178,51 @@ std::string Agent::silent_summary() const {
     return out;
 }
 
+bool Agent::wait_carrier(int stop_fd) {
+    // Admin-up is not a link: a NIC without carrier (unplugged cable, switch port down, optic
+    // dead) carries nothing, so L2 readiness needs IFF_LOWER_UP on every NIC.  The reference
+    // publishes its label right after link-up (cmd/discover/main.go:198-206,239-246).
+    std::unique_ptr<nl::LinkWatcher> watcher;
+    try {
+        watcher = ops_.subscribe_links();
+    } catch (const std::exception& e) {
+        NLOG_W("link events unavailable, carrier read once: %s", e.what());
+    }
+    for (auto& n : nics_) {  // the state after subscribing: no transition can be missed
+        try {
+            auto l = ops_.link_by_name(n.ifname);
+            n.link.flags = l.flags;
+            n.link.operstate = l.operstate;
+        } catch (const std::exception&) {
+        }
+    }
+    auto missing = [&] {
+        return std::any_of(nics_.begin(), nics_.end(), [](const NicState& n) { return n.link.up() && !n.link.lower_up(); });
+    };
+    const int64_t deadline = mono_ns() + cfg_.link_wait_ns;
+    while (watcher && missing() && mono_ns() < deadline) {
+        if (fd_readable(stop_fd)) return false;
+        const int64_t slice = std::min<int64_t>(deadline, mono_ns() + 100000000LL);  // stop_fd checked every 100 ms
+        for (auto& ev : watcher->wait(slice))
+            for (auto& n : nics_)
+                if (!ev.deleted && n.link.index == ev.link.index) {
+                    n.link.flags = ev.link.flags;
+                    n.link.operstate = ev.link.operstate;
+                }
+    }
+    for (auto& n : nics_) {
+        n.no_carrier = n.link.up() && !n.link.lower_up();
+        n.configured = n.link.up() && !n.no_carrier;
+        if (n.no_carrier)
+            NLOG_W("Interface '%s' has no carrier after %s (%s)", n.ifname.c_str(),
+                   format_go_duration(cfg_.link_wait_ns).c_str(), n.link.operstate_str().c_str());
+    }
+    return true;
+}
+
 void Agent::write_l2_artifacts() {
     std::string root = cfg_.sysfs_root.empty() ? topo::sysfs_root() : cfg_.sysfs_root;
-    for (auto& n : nics_) n.configured = n.link.up();
+    for (auto& n : nics_) n.configured = n.link.up() && !n.no_carrier;
     const int64_t deadline = mono_ns() + cfg_.gid_wait_ns;
     for (;;) {
         bool missing = false;
@@ -1347,6 +1507,11 @@ std::map<std::string, std::string> Agent::status_node() const {
     if (cfg_.xgmi_expect_links >= 0)
         m["xgmi_pairs"] = std::to_string(xgmi_.pairs_connected) + "/" + std::to_string(xgmi_.pairs_expected);
     if (cpu_ms_at_ready_ >= 0) m["cpu_ms_at_ready"] = strfmt("%.3f", cpu_ms_at_ready_);
+    if (!excluded_.empty()) {
+        std::vector<std::string> parts;
+        for (const auto& [n, why] : excluded_) parts.push_back(n + ": " + why);
+        m["excluded"] = join(parts, "; ");
+    }
     if (cfg_.dry_run) {
         m["dry_run"] = "true";
         if (!dry_run_missing_.empty()) m["not_in_netns"] = join(dry_run_missing_, ",");
@@ -1406,7 +1571,7 @@ std::string Agent::render_metrics() const {
     for (auto& n : nics_)
         o += strfmt("netop_agent_nic_configured{nic=\"%s\",gpu=\"%s\",rdma=\"%s\"} %d\n",
                     httpd::escape_label(n.ifname).c_str(), n.gpu_bdf.c_str(), n.rdma_dev.c_str(),
-                    (cfg_.mode == "L3" ? n.configured : n.link.up()) ? 1 : 0);
+                    (cfg_.mode == "L3" ? n.configured : n.link.up() && !n.no_carrier) ? 1 : 0);
     metric("netop_agent_nic_degraded", "gauge", "1 while the NIC has lost link after readiness");
     for (auto& n : nics_)
         o += strfmt("netop_agent_nic_degraded{nic=\"%s\"} %d\n", httpd::escape_label(n.ifname).c_str(), n.degraded ? 1 : 0);
@@ -1508,6 +1673,8 @@ std::string Agent::not_ready_reason() const {
         std::string why;
         if (n.degraded)
             why = "link down";
+        else if (n.no_carrier)
+            why = "no carrier (check the cable, the switch port and the optic)";
         else if (!n.lldp_silent.empty())
             why = n.lldp_silent;
         else if (!n.config_error.empty())
@@ -1562,7 +1729,11 @@ void Agent::run(int stop_fd) {
     if (names.empty()) {
         // A dry run still describes the GPUs and their xGMI mesh (the intra-node topology file a
         // job on a node without scale-out NICs uses); configuring needs NICs.
-        if (!cfg_.dry_run || disc_.gpus.empty()) throw AgentError("No interfaces found");
+        if (!cfg_.dry_run || disc_.gpus.empty()) {
+            std::vector<std::string> parts;
+            for (const auto& [n, why] : excluded_) parts.push_back(n + ": " + why);
+            throw AgentError("No interfaces found" + (parts.empty() ? "" : " (left alone: " + join(parts, "; ") + ")"));
+        }
         NLOG_W("dry run: no scale-out interfaces found; describing the %zu GPU(s) and the xGMI mesh only",
                disc_.gpus.size());
     }
@@ -1575,7 +1746,12 @@ void Agent::run(int stop_fd) {
             if (std::none_of(nics_.begin(), nics_.end(), [&](const NicState& n) { return n.ifname == i; }))
                 dry_run_missing_.push_back(i);
     }
+    refuse_uplinks();
     mark("discover");
+    if (!cfg_.dry_run) {
+        acquire_nic_locks(stop_fd);
+        mark("nic_locks");
+    }
     if (cfg_.cleanup) {
         cleanup_node();
         return;
@@ -1637,6 +1813,26 @@ void Agent::run(int stop_fd) {
         throw AgentError(std::string("Failed to remove any existing IPs from interfaces: ") + e.what());
     }
     mark("flush");
+
+    if (cfg_.mode == "L2" && cfg_.configure) {
+        if (!wait_carrier(stop_fd)) {
+            NLOG_I("Interrupted while waiting for carrier");
+            post_cleanups();
+            return;
+        }
+        mark("carrier");
+        std::vector<std::string> dark;
+        for (const auto& n : nics_)
+            if (!n.configured) dark.push_back(n.ifname);
+        if (!dark.empty() && !(cfg_.keep_running && cfg_.monitor)) {
+            // Without the monitor nothing would ever notice the carrier coming: fail, named, and
+            // let the kubelet's restart look again.
+            write_status();
+            throw AgentError(strfmt("Not all interfaces have a link (%zu/%zu). No carrier: ", nics_.size() - dark.size(),
+                                    nics_.size()) +
+                             join(dark, ", ") + " (check the cable, the switch port and the optic)");
+        }
+    }
 
     if (cfg_.mode == "L2" && cfg_.configure && cfg_.min_link_speed_mbps > 0) {
         // L3 checks each NIC as it configures it; L2 has no per-NIC step, so all at once here.
@@ -1719,6 +1915,17 @@ void Agent::run(int stop_fd) {
     if (cfg_.xgmi_expect_links >= 0)
         labels_extra_["amd.feature.node.kubernetes.io/gpu-xgmi.pairs"] = std::to_string(xgmi_.pairs_connected);
     if (!gdr_.kernel.empty()) labels_extra_[cfg_.labels.key + ".gdr"] = gdr_.mode();
+    const bool linked = std::none_of(nics_.begin(), nics_.end(), [](const NicState& n) { return n.no_carrier; });
+    if (!linked) {
+        // L2 with the monitor: stay up unlabelled; the first carrier on the last dark NIC
+        // publishes the label (monitor()).
+        NLOG_W("Not ready: %s; the label follows once every NIC has a link", not_ready_reason().c_str());
+        write_status();
+        NLOG_I("Monitoring...");
+        monitor(stop_fd);
+        post_cleanups();
+        return;
+    }
     try {
         if (publish_label()) NLOG_I("Published readiness label %s", cfg_.labels.path().c_str());
     } catch (const std::exception& e) {
@@ -1889,7 +2096,7 @@ int Agent::verify_peers(const std::vector<NicState*>& which, int64_t timeout_ns,
 }
 
 bool Agent::nic_healthy(const NicState& n) const {
-    if (!n.link.up() || n.degraded || n.cache_stale) return false;
+    if (!n.link.up() || n.degraded || n.cache_stale || n.no_carrier) return false;
     if (cfg_.mode == "L3" && cfg_.verify_peers_ns > 0 && !n.peer_verified) return false;
     return cfg_.mode != "L3" || n.configured;
 }
@@ -1908,7 +2115,7 @@ void Agent::monitor(int stop_fd) {
     for (auto& n : nics_) carrier[n.link.index] = n.link.lower_up();
     int64_t next_tx = mono_ns() + cfg_.lldp_tx_interval_ns;
     int64_t next_verify = 0;
-    bool labelled = true;
+    bool labelled = ready_;  // false: L2 came up with a NIC still without carrier
     // One pollable fd for "stop or link event": the LLDP wait returns as soon as either
     // fires, so a link failure is acted on in about a millisecond, not at the next tick.
     int wake = ::epoll_create1(EPOLL_CLOEXEC);
@@ -1965,6 +2172,16 @@ void Agent::monitor(int stop_fd) {
                     n.link.flags = ev.link.flags;
                     n.link.operstate = ev.link.operstate;
                     bool up = n.link.up(), lower = n.link.lower_up();
+                    if (n.no_carrier) {  // never had a link since the start (L2)
+                        if (up && lower) {
+                            NLOG_I("Interface '%s' has carrier now", n.ifname.c_str());
+                            n.no_carrier = false;
+                            n.configured = true;
+                            changed = true;
+                        }
+                        if (lower) carrier[n.link.index] = true;
+                        continue;
+                    }
                     if ((was_up && !up) || (had_carrier && !lower)) {
                         if (!n.degraded) {
                             NLOG_W("Interface '%s' lost link (%s)", n.ifname.c_str(), n.link.flags_str().c_str());
@@ -2025,8 +2242,12 @@ void Agent::monitor(int stop_fd) {
         if (changed) {
             bool healthy = std::all_of(nics_.begin(), nics_.end(), [&](const NicState& n) { return nic_healthy(n); });
             if (healthy && !labelled) {
-                if (cfg_.mode == "L3") write_artifacts();
+                if (cfg_.mode == "L3")
+                    write_artifacts();
+                else if (!cfg_.rccl_env.empty() || !cfg_.rccl_topo.empty())
+                    write_l2_artifacts();  // a NIC that got its carrier only now has its GID now
                 labelled = publish_label();
+                if (labelled && !phases_.count("total_ready")) phases_["total_ready"] = mono_ns() - t0_;
                 if (labelled) NLOG_I("All scale-out interfaces healthy again: readiness label republished");
                 if (cfg_.mode == "L3") write_host_config();
                 announce_all(120);

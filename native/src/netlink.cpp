@@ -387,6 +387,20 @@ static RouteInfo parse_route(const nlmsghdr* h) {
             case RTA_PRIORITY:
                 if (RTA_PAYLOAD(a) >= 4) std::memcpy(&r.priority, RTA_DATA(a), 4);
                 break;
+            case RTA_MULTIPATH: {  // struct rtnexthop, each RTNH_ALIGNed; lengths bounds-checked
+                const auto* p = static_cast<const uint8_t*>(RTA_DATA(a));
+                size_t left = RTA_PAYLOAD(a);
+                while (left >= sizeof(rtnexthop)) {
+                    rtnexthop nh;
+                    std::memcpy(&nh, p, sizeof nh);
+                    if (nh.rtnh_len < sizeof(rtnexthop) || nh.rtnh_len > left) break;
+                    if (nh.rtnh_ifindex > 0) r.nexthops.push_back(nh.rtnh_ifindex);
+                    const size_t step = std::min<size_t>(RTNH_ALIGN(nh.rtnh_len), left);
+                    p += step;
+                    left -= step;
+                }
+                break;
+            }
             case RTA_TABLE:
                 if (RTA_PAYLOAD(a) >= 4) {
                     uint32_t t;
@@ -620,6 +634,39 @@ std::vector<RouteInfo> Rtnl::route_list(uint8_t table) {
         if (table && r.table != table) return;
         out.push_back(r);
     });
+    return out;
+}
+
+static void add_default_links(const RouteInfo& r, std::vector<int>& out) {
+    if (r.dst.len != 0 || r.type != RTN_UNICAST || r.table == RT_TABLE_LOCAL) return;
+    if (r.ifindex > 0) out.push_back(r.ifindex);
+    out.insert(out.end(), r.nexthops.begin(), r.nexthops.end());
+}
+
+std::vector<int> NetOps::default_route_links() {
+    std::vector<int> out;
+    for (const auto& r : route_list(0)) add_default_links(r, out);
+    std::sort(out.begin(), out.end());
+    out.erase(std::unique(out.begin(), out.end()), out.end());
+    return out;
+}
+
+std::vector<int> Rtnl::default_route_links() {
+    std::vector<int> out = NetOps::default_route_links();
+    // ::/0 too: a management NIC may carry only an IPv6 default route (SLAAC / RA).
+    Msg m(RTM_GETROUTE, 0);
+    rtmsg rtm{};
+    rtm.rtm_family = AF_INET6;
+    m.put(rtm);
+    try {
+        dump(m, [&](const nlmsghdr* h) {
+            if (h->nlmsg_type == RTM_NEWROUTE) add_default_links(parse_route(h), out);
+        });
+    } catch (const SysError& e) {  // IPv6 disabled on the node (ipv6.disable=1)
+        if (e.code() != EAFNOSUPPORT && e.code() != EOPNOTSUPP) throw;
+    }
+    std::sort(out.begin(), out.end());
+    out.erase(std::unique(out.begin(), out.end()), out.end());
     return out;
 }
 

@@ -348,11 +348,28 @@ DiscoveryResult discover(const DiscoveryOptions& opt, const std::string& root) {
         return r;
     }
     if (opt.mode == DiscoveryMode::Rdma) {
-        for (auto& n : discover_pci_nics(root, opt.nic_drivers))
-            if (!n.rdma_dev.empty()) {
-                r.ifnames.push_back(n.ifname);
-                r.nics.push_back(std::move(n));
+        // The accelerators are enumerated only to know which NICs are theirs.
+        const std::vector<Gpu> gpus = opt.exclude_gpu_rails ? discover_gpus(root, opt.accel_driver) : std::vector<Gpu>{};
+        for (auto& n : discover_pci_nics(root, opt.nic_drivers)) {
+            if (n.rdma_dev.empty()) continue;
+            const Gpu* rail_of = nullptr;
+            PathType path = PathType::SYS;
+            for (const auto& g : gpus) {
+                PathType p = path_between(g.pci, n.pci);
+                if (int(p) <= int(opt.gpu_rail_path) && (!rail_of || int(p) < int(path))) {
+                    rail_of = &g;
+                    path = p;
+                }
             }
+            if (rail_of) {
+                r.excluded.emplace_back(n.ifname, strfmt("scale-out rail of GPU %s (%s, path %s): the amd-so agent's NIC",
+                                                         rail_of->pci.bdf.c_str(), opt.accel_driver.c_str(),
+                                                         to_string(path)));
+                continue;
+            }
+            r.ifnames.push_back(n.ifname);
+            r.nics.push_back(std::move(n));
+        }
         return r;
     }
     r.gpus = discover_gpus(root, opt.accel_driver);

@@ -24,14 +24,28 @@ struct FakeNetOps : netop::nl::NetOps {
     std::deque<netop::nl::LinkEvent> events;
     std::map<std::string, int> calls;
 
+    // Cable state: a link that is admin-up has IFF_LOWER_UP unless its name is listed here.
+    std::set<std::string> no_carrier;
     void add_link(const std::string& name, int index, const char* mac, bool up) {
         netop::nl::LinkInfo l;
         l.name = name;
         l.index = index;
         l.mac = *netop::MacAddr::parse(mac);
-        l.flags = IFF_BROADCAST | IFF_MULTICAST | (up ? IFF_UP : 0);
+        l.flags = IFF_BROADCAST | IFF_MULTICAST | (up ? IFF_UP | IFF_LOWER_UP : 0);
         l.mtu = 1500;
         links[name] = l;
+    }
+    // The cable is plugged in (or pulled): carrier follows, with the kernel's RTM_NEWLINK.
+    void set_carrier(const std::string& name, bool on) {
+        auto& l = links[name];
+        if (on) {
+            no_carrier.erase(name);
+            if (l.flags & IFF_UP) l.flags |= IFF_LOWER_UP;
+        } else {
+            no_carrier.insert(name);
+            l.flags &= ~unsigned(IFF_LOWER_UP);
+        }
+        events.push_back({false, l});
     }
     netop::nl::LinkInfo* by_index(int idx) {
         for (auto& [n, l] : links)
@@ -128,7 +142,8 @@ struct FakeNetOps : netop::nl::NetOps {
     void set_flag(int ifindex, bool up) {
         auto* l = by_index(ifindex);
         if (!l) throw netop::SysError(ENODEV, "no link");
-        l->flags = up ? (l->flags | IFF_UP) : (l->flags & ~unsigned(IFF_UP));
+        l->flags = up ? (l->flags | IFF_UP) : (l->flags & ~unsigned(IFF_UP | IFF_LOWER_UP));
+        if (up && !no_carrier.count(l->name)) l->flags |= IFF_LOWER_UP;
         if (echo_links) events.push_back({false, *l});
     }
     void link_set_up(int ifindex) override {

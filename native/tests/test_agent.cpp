@@ -1029,6 +1029,7 @@ struct PollableNetOps : FakeNetOps {
     }
     void operational(const std::string& name) {  // linkwatch: qdisc attached, operstate UP
         auto& l = links[name];
+        no_carrier.erase(name);
         l.operstate = IF_OPER_UP;
         l.flags |= IFF_LOWER_UP | IFF_RUNNING;
         events.push_back({false, l});
@@ -1070,6 +1071,7 @@ TEST(agent_announces_each_nic_when_it_becomes_operational) {
     PollableNetOps ops;
     ops.add_link("ens0", 10, "02:00:00:00:00:10", false);
     ops.add_link("ens1", 11, "02:00:00:00:00:11", false);
+    ops.no_carrier = {"ens0", "ens1"};  // until linkwatch reports them operational
     f.cfg.interfaces = "ens0,ens1";
     f.cfg.lldp_announce = true;
     f.cfg.keep_running = false;
@@ -2050,4 +2052,232 @@ TEST(agent_announcement_carries_the_hosts_max_frame_size) {
     CHECK(f.max_frame_size() && *f.max_frame_size() == 9018);
     CHECK(!agent::make_node_frame("node-1", "ens0", *MacAddr::parse("02:00:00:00:00:10"), "", 0, 9000).max_frame_size());
     CHECK(!agent::make_node_frame("node-1", "ens0", *MacAddr::parse("02:00:00:00:00:10"), "").max_frame_size());
+}
+
+namespace {
+// Host NICs for rdma discovery: three PCI NICs on their own root ports (no GPU next to them),
+// each with an RDMA device, netdevs named like the Fixture's links.
+void host_nic_sysfs(const TmpDir& t) {
+    int k = 0;
+    for (const char* name : {"ens0", "ens1", "ens2"}) {
+        const std::string bdf = strfmt("0000:%02x:00.0", 0x40 + k);
+        const std::string dev = strfmt("devices/pci0000:%02x/0000:%02x:01.1/%s", 0x40 + k, 0x40 + k, bdf.c_str());
+        t.write(dev + "/vendor", "0x15b3\n");
+        t.write(dev + "/device", "0x1021\n");
+        t.mkdir("bus/pci/drivers/mlx5_core");
+        t.symlink("bus/pci/drivers/mlx5_core", dev + "/driver");
+        t.write(dev + "/net/" + name + "/address", strfmt("02:00:00:00:00:1%d\n", k));
+        t.symlink(dev + "/net/" + name, std::string("class/net/") + name);
+        t.mkdir(dev + "/infiniband/mlx5_" + std::to_string(k));
+        ++k;
+    }
+}
+
+nl::RouteSpec route(int ifindex, const char* dst, const char* gw, uint8_t proto) {
+    nl::RouteSpec r;
+    r.ifindex = ifindex;
+    r.dst = *Ipv4Prefix::parse(dst);
+    if (gw) r.gateway = *Ipv4::parse(gw);
+    r.protocol = proto;
+    return r;
+}
+}  // namespace
+
+TEST(agent_rdma_discovery_leaves_the_nodes_own_nics_alone) {
+    // A default host-nic policy (rdma discovery, default drivers): ens0 carries the default route
+    // and ens1 holds the node's 192.168.1.5/24, so only ens2 is taken; with a DHCP route through
+    // ens2 as well (variant 1) nothing is left, and the error lists why for each NIC.
+    for (int variant : {0, 1}) {
+        Fixture f;
+        f.cfg.mode = "L2";
+        f.cfg.keep_running = false;
+        f.cfg.interfaces = "";
+        f.cfg.discovery.mode = topo::DiscoveryMode::Rdma;
+        TmpDir sys;
+        host_nic_sysfs(sys);
+        f.cfg.sysfs_root = sys.path;
+        f.ops.routes.push_back(route(10, "0.0.0.0/0", "192.168.0.1", RTPROT_DHCP));
+        f.ops.addrs.push_back(nl::AddrInfo{11, AF_INET, *Ipv4::parse("192.168.1.5"), *Ipv4::parse("192.168.1.5"), 24, 0, ""});
+        if (variant == 1) f.ops.routes.push_back(route(12, "172.16.0.0/12", "172.16.0.1", RTPROT_DHCP));
+        agent::Agent a(f.cfg, f.ops, std::make_unique<ScriptedLldp>(), f.nm());
+        std::string err;
+        try {
+            a.run(-1);
+        } catch (const agent::AgentError& e) {
+            err = e.what();
+        }
+        if (variant == 0) {
+            CHECK(err.empty());
+            CHECK_EQ(a.nics().size(), size_t(1));
+            CHECK_EQ(a.nics()[0].ifname, std::string("ens2"));
+            CHECK_EQ(f.ops.links["ens2"].mtu, 1500);
+            CHECK(f.ops.links["ens2"].flags & IFF_UP);
+        } else {
+            CHECK(err.find("No interfaces found (left alone: ") == 0);
+            CHECK(err.find("ens2: the node's own NIC: it has the route 172.16.0.0/12 (protocol dhcp)") != std::string::npos);
+        }
+        CHECK(err.empty() == (variant == 0));
+        // The node's NICs kept everything: address, routes, MTU, admin state.
+        CHECK_EQ(f.ops.addrs.size(), size_t(1));
+        CHECK(!(f.ops.links["ens0"].flags & IFF_UP));  // was down, never brought up
+        CHECK_EQ(f.ops.calls["addr_del"], 0);
+        auto ex = a.excluded();
+        CHECK_EQ(ex.size(), size_t(variant == 0 ? 2 : 3));
+        CHECK_EQ(ex[0].first, std::string("ens0"));
+        CHECK_EQ(ex[0].second, std::string("the node's own NIC: it carries the node's default route"));
+        CHECK_EQ(ex[1].second, std::string("the node's own NIC: it holds 192.168.1.5/24, an address the agent never "
+                                           "assigns (it only uses /30s)"));
+        if (variant == 0) {
+            auto st = read_file(f.cfg.status_file);
+            CHECK(st && st->find("\"excluded\":\"ens0: the node's own NIC: it carries the node's default route; "
+                                 "ens1: ") != std::string::npos);
+        }
+    }
+}
+
+TEST(agent_rdma_discovery_keeps_the_agents_own_l3_config) {
+    // A host NIC an earlier (keep-config) agent addressed: its /30, the kernel /30 route, the /16
+    // via the switch end and the rail table are the agent's, so the NIC is still a host NIC.
+    Fixture f;
+    f.cfg.keep_running = false;
+    f.cfg.interfaces = "";
+    f.cfg.discovery.mode = topo::DiscoveryMode::Rdma;
+    TmpDir sys;
+    host_nic_sysfs(sys);
+    f.cfg.sysfs_root = sys.path;
+    f.ops.addr_add(10, *Ipv4Prefix::parse("10.200.0.1/30"));
+    f.ops.routes.push_back(route(10, "10.200.0.0/16", "10.200.0.2", RTPROT_BOOT));
+    auto rail = route(10, "10.200.0.0/16", "10.200.0.2", agent::kRailProtocol);
+    rail.table = 100;
+    f.ops.routes.push_back(rail);
+    agent::Agent a(f.cfg, f.ops, f.all_valid(), f.nm());
+    a.run(-1);
+    CHECK_EQ(a.nics().size(), size_t(3));
+    CHECK(a.excluded().empty());
+}
+
+TEST(agent_refuses_a_nic_that_carries_the_default_route_in_every_mode) {
+    // Named explicitly (--interfaces) or discovered, L2 or L3, multipath or not: the uplink is
+    // never flushed or re-MTUed; the error names it.  A dry run reports it instead.
+    for (const char* mode : {"L3", "L2"})
+        for (bool multipath : {false, true}) {
+            Fixture f;
+            f.cfg.mode = mode;
+            f.cfg.mtu = 9000;
+            f.ops.addrs.push_back(nl::AddrInfo{11, AF_INET, *Ipv4::parse("192.168.1.5"), *Ipv4::parse("192.168.1.5"), 24, 0, ""});
+            auto def = route(multipath ? 0 : 11, "0.0.0.0/0", "192.168.1.1", RTPROT_STATIC);
+            if (multipath) def.nexthops = {13, 11};
+            f.ops.routes.push_back(def);
+            agent::Agent a(f.cfg, f.ops, f.all_valid(), f.nm());
+            std::string err;
+            try {
+                a.run(-1);
+            } catch (const agent::AgentError& e) {
+                err = e.what();
+            }
+            CHECK(err.find("Refusing to configure ens1: the node's default route leaves through it") == 0);
+            CHECK_EQ(f.ops.addrs.size(), size_t(1));
+            CHECK_EQ(f.ops.links["ens1"].mtu, 1500);
+            CHECK_EQ(f.ops.calls["link_set_up"], 0);
+        }
+    Fixture d;
+    d.cfg.dry_run = true;
+    d.ops.routes.push_back(route(11, "0.0.0.0/0", "192.168.1.1", RTPROT_DHCP));
+    agent::Agent a(d.cfg, d.ops, d.all_valid(), d.nm());
+    a.run(-1);
+    CHECK_EQ(a.excluded().size(), size_t(1));
+    CHECK_EQ(a.excluded()[0].second, std::string("carries the node's default route (refused)"));
+    // Failing to read the routes is not taken for "no uplink".
+    Fixture g;
+    g.ops.fail.insert("route_list");
+    agent::Agent b(g.cfg, g.ops, g.all_valid(), g.nm());
+    std::string err;
+    try {
+        b.run(-1);
+    } catch (const agent::AgentError& e) {
+        err = e.what();
+    }
+    CHECK(err.find("Cannot read the node's routes") == 0);
+}
+
+TEST(agent_nic_lock_gives_every_nic_one_owner) {
+    // Another agent (a host-nic policy naming a rail, say) holds ens1: this agent, whatever its
+    // label file, waits, then fails naming the NIC, having changed nothing; once the holder is
+    // gone it proceeds.
+    Fixture f;
+    f.cfg.keep_running = false;
+    f.cfg.nic_locks = true;
+    f.cfg.node_lock_wait_ns = 150000000;  // 150 ms
+    f.cfg.interfaces = "ens0,ens1,ens2";
+    // Per-process names: the abstract namespace is node (network namespace) wide.
+    const std::string name = "netop-nic:ens1";
+    sockaddr_un sa{};
+    sa.sun_family = AF_UNIX;
+    std::memcpy(sa.sun_path + 1, name.data(), name.size());
+    int holder = ::socket(AF_UNIX, SOCK_STREAM, 0);
+    const bool bound =
+        ::bind(holder, reinterpret_cast<sockaddr*>(&sa), socklen_t(offsetof(sockaddr_un, sun_path) + 1 + name.size())) == 0;
+    CHECK(bound);
+    {
+        agent::Agent a(f.cfg, f.ops, f.all_valid(), f.nm());
+        std::string err;
+        try {
+            a.run(-1);
+        } catch (const agent::AgentError& e) {
+            err = e.what();
+        }
+        CHECK(err.find("Another agent holds NIC 'ens1' (its NIC lock)") == 0);
+        CHECK(f.ops.addrs.empty());
+        CHECK_EQ(f.ops.calls["link_set_up"], 0);
+    }
+    ::close(holder);
+    agent::Agent b(f.cfg, f.ops, f.all_valid(), f.nm());
+    b.run(-1);
+    CHECK_EQ(f.ops.addrs.size(), size_t(3));
+}
+
+TEST(agent_l2_waits_for_carrier_and_labels_only_when_every_nic_has_a_link) {
+    // L2 starts with ens1's cable unplugged: no label, the reason names it (status.json and the
+    // readiness probe's file); the carrier comes and the monitor publishes the label.
+    Fixture f;
+    f.cfg.mode = "L2";
+    f.cfg.monitor_tick_ns = 1000000;
+    f.ops.no_carrier = {"ens1"};
+    f.ops.links["ens1"].flags &= ~unsigned(IFF_LOWER_UP);
+    Pipe stop;
+    agent::Agent a(f.cfg, f.ops, std::make_unique<ScriptedLldp>(), f.nm());
+    bool unlabelled = false, reason = false, status = false, labelled = false;
+    a.on_monitor_tick = [&](int tick) {
+        if (tick == 1) {
+            unlabelled = !path_exists(f.cfg.labels.path());
+            auto why = read_file(agent::reason_path(f.cfg.status_file));
+            reason = why && *why == "ens1: no carrier (check the cable, the switch port and the optic)\n";
+            auto st = read_file(f.cfg.status_file);
+            status = st && st->find("\"ready\":false") != std::string::npos &&
+                     st->find("\"no_carrier\":true") != std::string::npos;
+            f.ops.set_carrier("ens1", true);
+        } else if (tick == 3) {
+            labelled = path_exists(f.cfg.labels.path()) && !path_exists(agent::reason_path(f.cfg.status_file));
+            stop.fire();
+        }
+    };
+    a.run(stop.fd[0]);
+    CHECK(unlabelled);
+    CHECK(reason);
+    CHECK(status);
+    CHECK(labelled);
+    // Without the monitor nothing would notice the carrier later: the start fails, naming it.
+    Fixture g;
+    g.cfg.mode = "L2";
+    g.cfg.keep_running = false;
+    g.ops.no_carrier = {"ens2"};
+    agent::Agent b(g.cfg, g.ops, std::make_unique<ScriptedLldp>(), g.nm());
+    std::string err;
+    try {
+        b.run(-1);
+    } catch (const agent::AgentError& e) {
+        err = e.what();
+    }
+    CHECK(err.find("Not all interfaces have a link (2/3). No carrier: ens2") == 0);
+    CHECK(!path_exists(g.cfg.labels.path()));
 }

@@ -232,3 +232,24 @@ TEST(topology_rccl_link_is_the_slower_of_device_and_port) {
     d.port_max_link_width = 0;
     CHECK_EQ(d.rccl_link_width(), 0);
 }
+
+TEST(topology_rdma_mode_leaves_the_gpu_rails_to_the_scale_out_agent) {
+    // host-nic discovery: every RDMA NIC of the driver list except the GPUs' rails, which the
+    // amd-so agent owns; each left-out rail is named with its GPU.
+    TmpDir t;
+    build_node(t);
+    t.mkdir("devices/pci0000:37/0000:37:01.1/0000:38:00.0/infiniband/mlx5_8");
+    DiscoveryOptions opt;
+    opt.mode = DiscoveryMode::Rdma;
+    auto r = discover(opt, t.path);
+    CHECK_EQ(r.ifnames.size(), size_t(1));
+    CHECK_EQ(r.ifnames[0], std::string("ens9np0"));
+    CHECK_EQ(r.excluded.size(), size_t(2));
+    CHECK_EQ(r.excluded[0].first, std::string("enp5s0np0"));
+    CHECK(r.excluded[0].second.find("scale-out rail of GPU 0000:0a:00.0 (amdgpu, path PXB)") != std::string::npos);
+    CHECK_EQ(r.excluded[1].first, std::string("enp30s0np0"));
+    opt.exclude_gpu_rails = false;  // --rdma-include-gpu-rails
+    auto all = discover(opt, t.path);
+    CHECK_EQ(all.ifnames.size(), size_t(3));
+    CHECK(all.excluded.empty());
+}

@@ -46,7 +46,7 @@ int main(int argc, char** argv) {
     fs.add_string("systemd-networkd", &cfg.networkd, "Write systemd networkd configuration files to given directory");
     fs.add_int("mtu", &cfg.mtu, "MTU value to set for interfaces");
 
-    fs.add_string("nic-discovery", &discovery_mode, "scale-out NIC discovery: affine (NICs sharing a PCIe switch with an amdgpu GPU), accel (netdevs under the accelerator PCI function), rdma (every RDMA-capable NIC of --nic-drivers: host NICs), none");
+    fs.add_string("nic-discovery", &discovery_mode, "scale-out NIC discovery: affine (NICs sharing a PCIe switch with an amdgpu GPU), accel (netdevs under the accelerator PCI function), rdma (RDMA-capable NICs of --nic-drivers that are neither a GPU's rail nor the node's own NIC -- default route, a non-/30 address or a route the agent does not install: host NICs), none");
     fs.add_string("accel-driver", &cfg.discovery.accel_driver, "accelerator PCI driver to enumerate");
     fs.add_string("nic-drivers", &nic_drivers, "comma separated NIC driver allow-list for affine discovery (default: common RoCE drivers)");
     fs.add_string("max-path", &max_path, "farthest GPU<->NIC PCIe path type accepted: PIX, PXB, PHB, NODE, SYS");
@@ -79,7 +79,11 @@ int main(int argc, char** argv) {
     fs.add_bool("cleanup", &cfg.cleanup, "one-shot: remove what --keep-config agents left on the node (IPv4 addresses of the discovered NICs, tagged rail rules and routes, label, artifacts, LLDP cache, networkd files) and exit");
     std::string node_lock = "auto";
     fs.add_string("node-lock", &node_lock, "node-wide lock (abstract unix socket) held while the agent runs, so agents configuring the same NICs never overlap (exiting vs starting agent, agent vs --cleanup, two policies on one node): auto (named after --nfd-label-file), none, or a name");
-    fs.add_duration("node-lock-wait", &cfg.node_lock_wait_ns, "how long to wait for the node lock before failing");
+    fs.add_duration("node-lock-wait", &cfg.node_lock_wait_ns, "how long to wait for the node lock (and each NIC lock) before failing");
+    cfg.nic_locks = true;
+    fs.add_bool("nic-lock", &cfg.nic_locks, "hold a node-wide lock per configured NIC (abstract unix socket netop-nic:<ifname>) so two agents, whatever their policies and label files, never configure one NIC");
+    bool include_gpu_rails = false;
+    fs.add_bool("rdma-include-gpu-rails", &include_gpu_rails, "with --nic-discovery=rdma, also take RDMA NICs that sit next to a GPU (its scale-out rail, which an amd-so agent owns); default: left alone");
     fs.add_bool("check-peer-mtu", &cfg.check_peer_mtu, "refuse a NIC whose switch port advertises (LLDP 802.3 Maximum Frame Size) frames smaller than its MTU needs");
     int min_speed_gbps = 0;
     fs.add_int("min-link-speed-gbps", &min_speed_gbps, "minimum negotiated link speed of every scale-out NIC (sysfs speed); a slower NIC is left unconfigured (L3) or fails the start (L2); 0 = off");
@@ -151,6 +155,7 @@ int main(int argc, char** argv) {
     }
     cfg.min_link_speed_mbps = int64_t(min_speed_gbps) * 1000;
     cfg.discovery.mode = *dm;
+    cfg.discovery.exclude_gpu_rails = !include_gpu_rails;
     cfg.token_policy = *tp;
     if (!nic_drivers.empty()) cfg.discovery.nic_drivers = split(nic_drivers, ',');
     static const std::map<std::string, topo::PathType> paths{{"PIX", topo::PathType::PIX}, {"PXB", topo::PathType::PXB},

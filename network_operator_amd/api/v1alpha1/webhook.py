@@ -191,7 +191,8 @@ def validate_host_nic_spec(s: Optional[T.HostNicSpec]) -> List[str]:
     warnings = []
     if not s.interfaces and not s.nicDrivers:
         warnings.append("hostNic: no interfaces or nicDrivers given; every RDMA NIC of the default driver list "
-                        "will be configured")
+                        "that is neither a GPU's scale-out rail nor the node's own NIC (default route, non-/30 "
+                        "address) will be configured")
     return warnings
 
 

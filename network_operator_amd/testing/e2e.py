@@ -296,7 +296,9 @@ async def _scenario(tmp: Path, n_nics: int, mode: str, seed: int, interval: str,
                                                 f"--metrics-bind-address=127.0.0.1:{metrics_port}",
                                                 "--dependency-check-interval=0"],
                                                stop=stop, started=started))
-    kmd = [sys.executable, "-m", "network_operator_amd.testing.fakesysfs", "bind", KMD_DRIVER,
+    # "both": the host NICs come up as mlx5 like the rails (ConnectX everywhere), and the host-nic
+    # policy keeps the default driver list, so ownership rests on discovery alone.
+    kmd = [sys.executable, "-m", "network_operator_amd.testing.fakesysfs", "bind", "mlx5_core" if both else KMD_DRIVER,
            *[n for n in nic_names if n in HOST_NICS]]
     from ..api.v1alpha1 import types as T0
 
@@ -347,7 +349,7 @@ async def _scenario(tmp: Path, n_nics: int, mode: str, seed: int, interval: str,
             t_label = await _until(lambda: node.node_labels().get(label_key) == "true", 30)
 
             if both:
-                await c.create(P, T.new_host_nic_policy("host-nics", layer=mode, mtu=9000, nicDrivers=[KMD_DRIVER],
+                await c.create(P, T.new_host_nic_policy("host-nics", layer=mode, mtu=9000,
                                                         driverImage=KMD_IMAGE).to_dict())
 
                 def host_good():
@@ -356,6 +358,16 @@ async def _scenario(tmp: Path, n_nics: int, mode: str, seed: int, interval: str,
                 t_host = await _until(host_good, 30)
                 res["host_nic_policy_all_good_s"] = round(t_host - t0, 6) if t_host else None
                 res["host_nic_status"] = (fake.get_object(P, "host-nics") or {}).get("status")
+                # What each agent took (its status file) and left alone: two disjoint NIC sets.
+                res["agent_nic_sets"], res["agent_excluded"] = {}, {}
+                for x in node.containers.values():
+                    sf = next((a.split("=", 1)[1] for a in x.argv if a.startswith("--status-file=")), None)
+                    try:
+                        st = json.loads(Path(sf).read_text()) if sf else {}
+                    except (OSError, ValueError):
+                        st = {}
+                    res["agent_nic_sets"][x.daemonset] = [i["name"] for i in st.get("interfaces", [])]
+                    res["agent_excluded"][x.daemonset] = st.get("excluded", "")
 
             def all_good():
                 st = (fake.get_object(P, name) or {}).get("status") or {}

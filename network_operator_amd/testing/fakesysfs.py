@@ -2,8 +2,9 @@
 
 ``build_mi355x_node`` reproduces the PCIe / KFD topology of a real 8x MI355X node (captured
 from a GPU box, see ``tests/fixtures/mi355x_node_topology.json``): eight 0x75a3 GPUs, each
-behind a PCIe switch shared with one mlx5 RoCE NIC, two management NICs on their own root
-ports, and the KFD io_links of the 28-pair xGMI mesh.  NIC netdev names can be remapped so
+behind a PCIe switch shared with one mlx5 RoCE NIC (its scale-out rail), two more mlx5 NICs on
+their own root ports (frontend / management / storage: host NICs), and the KFD io_links of the
+28-pair xGMI mesh.  NIC netdev names can be remapped so
 the agent's affinity discovery finds the veth "NICs" of the netns harness.
 
 The reference's equivalent is its tmpdir + ``SYSFS_ROOT`` fake tree
@@ -70,6 +71,8 @@ def build_mi355x_node(root: Path, nic_names: Optional[Dict[str, str]] = None, ni
 
     nic_names: {original ifname -> new ifname}; nic_macs: {new ifname -> MAC}.
     drop_xgmi_pairs: iterable of (gpu_i, gpu_j) KFD-order indices whose xGMI link is removed.
+    n_gpus < 8: a smaller node of the same layout, so the rails of the GPUs left out (the NICs
+    behind their PCIe switches) are left out too.
     """
     fx = json.loads(FIXTURE.read_text())
     nic_names = nic_names or {}
@@ -80,7 +83,12 @@ def build_mi355x_node(root: Path, nic_names: Optional[Dict[str, str]] = None, ni
         d = _pci(root, g["path"], "amdgpu", g["vendor"], g["device"], g["numa"], "0x120000")
         _link(d, root / "bus" / "pci" / "drivers" / "amdgpu" / g["bdf"])
     nics = []
+    built = {tuple(g["path"].split("/")[:3]) for g in gpus}
+    every = {tuple(g["path"].split("/")[:3]) for g in fx["gpus"]}
     for n in fx["nics"]:
+        under = tuple(n["pcipath"].split("/")[:3])
+        if under in every and under not in built:
+            continue  # the rail of a GPU this node does not have
         name = nic_names.get(n["ifname"], n["ifname"])
         d = _pci(root, n["pcipath"], n["driver"], "0x15b3", "0x1021", 0 if n["pcipath"] < "pci0000:80" else 1, "0x020000")
         net = d / "net" / name
@@ -89,7 +97,10 @@ def build_mi355x_node(root: Path, nic_names: Optional[Dict[str, str]] = None, ni
         _link(d, net / "device")  # /sys/class/net/<if>/device -> the PCI function, as on a host
         _link(net, root / "class" / "net" / name)
         nics.append(dict(n, ifname=name))
+    kept = {n["pcipath"] for n in nics}
     for r in fx["rdma"]:
+        if r["pcipath"] not in kept:
+            continue
         d = root / "devices" / r["pcipath"] / "infiniband" / r["dev"]
         d.mkdir(parents=True, exist_ok=True)
         _link(d, root / "class" / "infiniband" / r["dev"])

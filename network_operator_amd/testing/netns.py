@@ -315,7 +315,7 @@ def run_scenario(n_nics: int = 8, mode: str = "L3", seed: int | None = None, int
                  egress_probe: bool = False, nm_bus: bool = False, nm_restore: bool = True, lldp_cache: bool = False,
                  soak_cycles: int = 0, arp_silent_ports: int = 0, switch_name: str = "",
                  port_switch_names: dict | None = None, nic_speeds_mbps: list | None = None,
-                 switch_max_frame: int = 0) -> dict:
+                 switch_max_frame: int = 0, dark_port: int | None = None) -> dict:
     """Runs one node bring-up.  Must already be inside a private user+net namespace.
 
     nm_bus: run the agent with --disable-networkmanager against a real ``dbus-daemon`` on which a
@@ -323,7 +323,10 @@ def run_scenario(n_nics: int = 8, mode: str = "L3", seed: int | None = None, int
     and record both before and after SIGTERM.
 
     lldp_cache: run the agent with --lldp-cache; with crash_restart, also record how long after
-    the restart the switch's frames confirmed every cached Port Description."""
+    the restart the switch's frames confirmed every cached Port Description.
+
+    dark_port: that switch port is down when the agent starts (the NIC has no carrier); once the
+    agent has said why it is not ready, the port comes up and the label must follow."""
     from . import fakesysfs
 
     nat = _native()
@@ -409,14 +412,39 @@ def run_scenario(n_nics: int = 8, mode: str = "L3", seed: int | None = None, int
         def spawn():
             with open(agent_log, "a") as logf:
                 return subprocess.Popen(args, env=env, stdout=logf, stderr=subprocess.STDOUT, text=True)
+        if dark_port is not None:
+            set_switch_port(pid, sw_ports[dark_port], False)
         t0 = time.monotonic()
         agent = spawn()
         budget = 5.0 + float(wait.rstrip("s"))
-        t_ready = _wait_for(label, budget, agent)
+        dark: dict = {}
+        if dark_port is not None:
+            reason = tmp / "status.json.not-ready"
+            t_why = _wait_for(reason, budget, agent)
+            dark["reason_s"] = (t_why - t0) if t_why else None
+            dark["label_while_dark"] = label.exists()
+            dark["reason"] = reason.read_text() if reason.exists() else None
+            try:
+                st = json.loads((tmp / "status.json").read_text())
+                dark["status_ready"] = st.get("ready")
+                dark["status_no_carrier"] = [i["name"] for i in st["interfaces"] if i.get("no_carrier")]
+            except (OSError, ValueError, KeyError):
+                dark["status_ready"] = dark["status_no_carrier"] = None
+            pr = subprocess.run([str(native_bin("discover")), "--ready-check", f"--nfd-features-dir={feat}",
+                                 f"--status-file={tmp / 'status.json'}"], capture_output=True, text=True, timeout=10)
+            dark["ready_check"] = {"rc": pr.returncode, "stdout": pr.stdout.strip()}
+            t_up = time.monotonic()
+            set_switch_port(pid, sw_ports[dark_port], True)
+            t_ready = _wait_for(label, 10, agent)
+            dark["port_up_to_label_s"] = (t_ready - t_up) if t_ready else None
+        else:
+            t_ready = _wait_for(label, budget, agent)
         res: dict = {"n_nics": len(nic_names), "mode": mode, "fast_start": fast_start, "announce": announce,
                      "interval": interval, "pipeline": pipeline, "plan": plan, "nics": nic_names}
         res["ready"] = t_ready is not None
         res["latency_s"] = (t_ready - t0) if t_ready else None
+        if dark:
+            res["dark"] = dark
         try:  # CPU of the process so far (coarse: clock ticks; the status has getrusage at readiness)
             f = Path(f"/proc/{agent.pid}/stat").read_text().rsplit(")", 1)[1].split()
             res["agent_cpu_ms"] = (int(f[11]) + int(f[12])) * 1000.0 / os.sysconf("SC_CLK_TCK")
@@ -601,6 +629,92 @@ def run_scenario(n_nics: int = 8, mode: str = "L3", seed: int | None = None, int
             shutil.rmtree(tmp, ignore_errors=True)
 
 
+MGMT_NIC, HOST_NIC = "ens9np0", "ens49np1"  # the fixture node's two NICs on their own root ports
+
+
+def run_host_nic_ownership(mode: str = "L2", rails: int = 8) -> dict:
+    """A default ``host-nic`` policy's agent (rdma discovery, the default driver list) on the
+    captured MI355X node, where every NIC is mlx5 with an RDMA device:
+
+    * the GPU rails already carry what an amd-so agent gave them (a /30 each, MTU 9000);
+    * ``ens9np0`` is the node's management NIC: 192.168.77.10/24 and the default route;
+    * ``ens49np1`` is a free host NIC (down, no address).
+
+    Records the state before, while the agent is ready, and after SIGTERM; then starts an agent
+    that names the management NIC explicitly (``--interfaces``), which must refuse.  Each veth's
+    peer stays in this namespace (up: the NIC has carrier).  Must run inside ``unshare -rn``."""
+    from . import fakesysfs
+    from ..utils.paths import native_bin
+
+    nat = _native()
+    rt = nat.Rtnl()
+    rt.link_set_up(rt.link_by_name("lo")["index"])
+    tmp = Path(tempfile.mkdtemp(prefix="netop-owner-"))
+    try:
+        fakesysfs.build_mi355x_node(tmp / "sys", n_gpus=8)
+        rail_names = fakesysfs.real_nic_order()[:rails]
+        for k, nif in enumerate(rail_names + [MGMT_NIC, HOST_NIC]):
+            rt.veth_add(nif, f"peer{k}")
+            rt.link_set_up(rt.link_by_name(f"peer{k}")["index"])
+        for k, nif in enumerate(rail_names):
+            idx = rt.link_by_name(nif)["index"]
+            rt.link_set_mtu(idx, 9000)
+            rt.link_set_up(idx)
+            rt.addr_add(idx, f"10.77.{k}.1/30")
+        m = rt.link_by_name(MGMT_NIC)["index"]
+        rt.link_set_up(m)
+        rt.addr_add(m, "192.168.77.10/24")
+        rt.route_append("0.0.0.0/0", "192.168.77.1", m, 16)  # a DHCP lease's default route
+
+        def snapshot() -> dict:
+            out = {}
+            for nif in rail_names + [MGMT_NIC, HOST_NIC]:
+                link = rt.link_by_name(nif)
+                out[nif] = {"up": link["up"], "mtu": link["mtu"], "addrs": rt.addr_list(link["index"])}
+            out["default_routes"] = [r for r in rt.route_list() if r["dst"] == "0.0.0.0/0"]
+            return out
+
+        feat = tmp / "features.d"
+        feat.mkdir()
+        label = feat / "host-nic-readiness.txt"
+        base = [str(native_bin("discover")), "--configure=true", "--keep-running", f"--mode={mode}", "--mtu=9000",
+                f"--nfd-features-dir={feat}", "--nfd-label-file=host-nic-readiness.txt",
+                "--nfd-label=amd.feature.node.kubernetes.io/host-nic-ready", "--wait=3s", "-v=2"]
+        env = dict(os.environ, SYSFS_ROOT=str(tmp / "sys"), NODE_NAME="mi355x-node-0")
+        res: dict = {"rails": rail_names, "before": snapshot(),
+                     "discovery": nat.discover(str(tmp / "sys"), mode="rdma")}
+        log_path = tmp / "agent.log"
+        with open(log_path, "w") as logf:
+            agent = subprocess.Popen([*base, "--nic-discovery=rdma", f"--status-file={tmp / 'status.json'}"], env=env,
+                                     stdout=logf, stderr=subprocess.STDOUT)
+        t_ready = _wait_for(label, 15, agent)
+        res["ready"] = t_ready is not None
+        res["label"] = label.read_text() if label.exists() else None
+        time.sleep(0.05)  # status.json follows the label
+        res["while_ready"] = snapshot()
+        try:
+            res["status"] = json.loads((tmp / "status.json").read_text())
+        except (OSError, ValueError):
+            res["status"] = None
+        if agent.poll() is None:
+            agent.send_signal(signal.SIGTERM)
+        try:
+            agent.wait(timeout=20)
+        except subprocess.TimeoutExpired:
+            agent.kill()
+            agent.wait()
+        res["agent_rc"] = agent.returncode
+        res["after_sigterm"] = snapshot()
+        res["agent_log"] = log_path.read_text(errors="replace")[-6000:]
+        # The management NIC named explicitly: refused, nothing touched.
+        r = subprocess.run([*base, "--nic-discovery=none", f"--interfaces={MGMT_NIC}"], env=env, capture_output=True,
+                           text=True, timeout=30)
+        res["named_mgmt"] = {"rc": r.returncode, "stderr": r.stderr[-2000:], "after": snapshot()[MGMT_NIC]}
+        return res
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+
+
 # ---------------------------------------------------------------------------
 # From outside: spawn into a fresh namespace
 # ---------------------------------------------------------------------------
@@ -644,7 +758,8 @@ def _main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--json", default="{}", help="run_scenario kwargs")
     a = ap.parse_args(argv)
-    res = run_scenario(**json.loads(a.json))
+    kw = json.loads(a.json)
+    res = run_host_nic_ownership(**kw) if kw.pop("host_nic_ownership", False) else run_scenario(**kw)
     print(json.dumps(res))
     return 0
 

@@ -190,7 +190,8 @@ def test_agent_killed_is_restarted_and_the_node_recovers():
 def test_scale_out_and_host_nic_policies_share_a_node():
     """Both configuration types on one node: two DaemonSets, two agents with their own NIC sets,
     labels and label files, each policy "All good"; deleting the amd-so policy leaves the host
-    NICs configured."""
+    NICs configured.  Every NIC is mlx5 (the captured topology) and the host-nic policy keeps the
+    default driver list: the host-nic agent leaves the GPU rails to the amd-so agent by itself."""
     r = e2e.run_isolated(n_nics=2, mode="L3", seed=13, config_type="both")
     assert r["policy_to_all_good_s"] is not None and r["host_nic_policy_all_good_s"] is not None, r["agent_log"]
     labels = r["node_labels"]
@@ -199,6 +200,10 @@ def test_scale_out_and_host_nic_policies_share_a_node():
     assert labels["amd.feature.node.kubernetes.io/gpu-scale-out.nics"] == "2"
     _check_nics(r, "L3")  # all four NICs: the two rails and the two host NICs
     scale_out = r["nics"][:2]
+    sets = r["agent_nic_sets"]
+    assert sorted(sets["amd-network-operator/scale-out"]) == sorted(scale_out)
+    assert sorted(sets["amd-network-operator/host-nics"]) == sorted(e2e.HOST_NICS)
+    assert all(f"{n}: scale-out rail of GPU" in r["agent_excluded"]["amd-network-operator/host-nics"] for n in scale_out)
     assert all(r["after_delete"][n] == [] for n in scale_out)
     assert all(r["after_delete"][n] != [] for n in e2e.HOST_NICS)
 

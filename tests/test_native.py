@@ -124,6 +124,27 @@ def test_real_mi355x_topology_discovery(native, tmp_path):
     assert x["per_gpu_bw_mbs"] == 7 * 76000
 
 
+def test_rdma_discovery_on_the_mi355x_node_leaves_the_eight_rails_to_amd_so(native, tmp_path):
+    """host-nic discovery (rdma, default drivers) on the captured node, where all ten NICs are
+    mlx5 with an RDMA device: the eight GPU rails are left out (each named with its GPU), so an
+    amd-so and a host-nic policy on one node never share a NIC.  The reference cannot reach another
+    agent's NIC at all: it only enumerates netdevs under the accelerator's own PCI functions
+    (reference cmd/discover/network.go:34,88-119)."""
+    fx = fakesysfs.build_mi355x_node(tmp_path)
+    rails = fakesysfs.real_nic_order()
+    d = native.discover(str(tmp_path), mode="rdma")
+    assert sorted(d["ifnames"]) == ["ens49np1", "ens9np0"]
+    assert sorted(d["excluded"]) == sorted(rails)
+    pairs = {p["nic"]: p["gpu"] for p in native.discover(str(tmp_path))["pairs"]}
+    for nic, why in d["excluded"].items():
+        assert why.startswith(f"scale-out rail of GPU {pairs[nic]} (amdgpu, path PXB)"), why
+    # Disjoint from what the amd-so agent takes, and together they cover every RDMA NIC.
+    assert not set(d["ifnames"]) & set(pairs)
+    assert set(d["ifnames"]) | set(pairs) == {n["ifname"] for n in fx["nics"]}
+    # --rdma-include-gpu-rails (explicit opt-in) takes them all.
+    assert len(native.discover(str(tmp_path), mode="rdma", include_gpu_rails=True)["ifnames"]) == 10
+
+
 def test_topo_tool_json(tmp_path):
     fakesysfs.build_mi355x_node(tmp_path, drop_xgmi_pairs=[(1, 2)])
     out = subprocess.run([str(native_bin("netop-topo")), f"--sysfs-root={tmp_path}"], capture_output=True, text=True,

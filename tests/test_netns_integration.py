@@ -385,3 +385,54 @@ def test_switch_without_jumbo_frames_is_caught_before_jobs_hang():
     err = [ln for ln in bad["agent_log"].splitlines() if ln.startswith("Error: ")][-1]
     assert err.startswith("Error: Not all interfaces were configured (0/2). Not configured: "), err
     assert "its switch port accepts frames up to 1518 bytes, but MTU 9000 needs 9014" in err
+
+
+def test_default_host_nic_policy_leaves_the_management_nic_and_the_gpu_rails_alone():
+    """The captured MI355X node, every NIC mlx5 with an RDMA device: a host-nic agent with the
+    default driver list takes only the free host NIC.  The management NIC (address + default
+    route) and the eight GPU rails (an amd-so agent's /30s, MTU 9000) are untouched while it runs
+    and after it exits; naming the management NIC explicitly is refused."""
+    r = netns.run_isolated(host_nic_ownership=True)
+    assert r["ready"], r["agent_log"]
+    assert "host-nic-ready.nics=1" in r["label"]
+    rails = r["rails"]
+    assert len(rails) == 8
+    # The discovery view (no netlink): the rails are left out as the GPUs' NICs.
+    assert sorted(r["discovery"]["ifnames"]) == [netns.HOST_NIC, netns.MGMT_NIC]
+    assert sorted(r["discovery"]["excluded"]) == sorted(rails)
+    assert all("scale-out rail of GPU" in why for why in r["discovery"]["excluded"].values())
+    # The agent's view: the management NIC left out too, for its default route.
+    assert [i["name"] for i in r["status"]["interfaces"]] == [netns.HOST_NIC]
+    assert f"{netns.MGMT_NIC}: the node's own NIC: it carries the node's default route" in r["status"]["excluded"]
+    for phase in ("while_ready", "after_sigterm"):
+        for nif in rails + [netns.MGMT_NIC]:
+            assert r[phase][nif] == r["before"][nif], (phase, nif, r[phase][nif], r["before"][nif])
+        assert r[phase]["default_routes"] == r["before"]["default_routes"]
+    assert r["while_ready"][netns.HOST_NIC] == {"up": True, "mtu": 9000, "addrs": []}
+    assert r["after_sigterm"][netns.HOST_NIC]["up"] is False  # restored to its original state
+    assert r["agent_rc"] == 0
+    named = r["named_mgmt"]
+    assert named["rc"] == 1 and f"Refusing to configure {netns.MGMT_NIC}: the node's default route" in named["stderr"]
+    assert named["after"] == r["before"][netns.MGMT_NIC]
+
+
+def test_l2_waits_for_carrier_on_every_nic_before_the_label():
+    """L2 on real veths with one switch port down (an unplugged cable): admin-up is not a link.
+    No label; the reason names the NIC in status.json and the readiness probe's output; the port
+    comes up and the monitor publishes the label (the reference labels right after link-up,
+    reference cmd/discover/main.go:198-206,239-246)."""
+    r = netns.run_isolated(n_nics=3, seed=41, mode="L2", interval="1s", dark_port=1,
+                           extra_args=["--link-wait=300ms"])
+    d = r["dark"]
+    dark_nic = r["nics"][1]
+    assert d["reason_s"] is not None, r["agent_log"]
+    assert d["label_while_dark"] is False
+    assert d["reason"] == f"{dark_nic}: no carrier (check the cable, the switch port and the optic)\n"
+    assert d["status_ready"] is False and d["status_no_carrier"] == [dark_nic]
+    assert d["ready_check"]["rc"] == 1 and dark_nic + ": no carrier" in d["ready_check"]["stdout"]
+    assert r["ready"] and d["port_up_to_label_s"] is not None and d["port_up_to_label_s"] < 2.0, r["agent_log"]
+    assert "gpu-scale-out.nics=3" in r["label"]
+    assert f"Interface '{dark_nic}' has carrier now" in r["agent_log"]
+    for nic in r["nics"]:
+        assert r["state"][nic]["up"] and r["state"][nic]["addrs"] == []
+    assert r["agent_rc"] == 0

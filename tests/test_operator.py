@@ -526,7 +526,8 @@ def test_lldp_wait_validated_and_passed():
     assert not any(a.startswith("--wait") for a in agent_args(p))
     h = T.new_host_nic_policy("h", layer="L3", lldpWait="20s")
     assert "--wait=20s" in host_nic_agent_args(h) and W.validate_create(h) == [
-        "hostNic: no interfaces or nicDrivers given; every RDMA NIC of the default driver list will be configured"]
+        "hostNic: no interfaces or nicDrivers given; every RDMA NIC of the default driver list that is neither a "
+        "GPU's scale-out rail nor the node's own NIC (default route, non-/30 address) will be configured"]
     assert T.NetworkClusterPolicy.from_dict(h.to_dict()).spec.hostNic.lldpWait == "20s"
     h.spec.hostNic.lldpWait = "0s"
     with pytest.raises(W.InvalidLldpWaitError):
