@@ -104,6 +104,10 @@ struct Config {
     // "dmabuf" = require that mechanism.  Checked before LLDP, like the xGMI mesh.
     std::string require_gdr;
     bool disable_fw_lldp = false;
+    // With disable_fw_lldp, on a NIC without a firmware-LLDP private flag whose DCBX an embedded
+    // agent runs (mlx5_core in firmware mode): hand DCBX to the host.  Opt-in: the firmware then
+    // stops negotiating PFC/ETS with the switch (ethtool.hpp).
+    bool fw_lldp_dcbx_host = false;
     std::string fw_lldp_flags;                        // extra rules "NAME=0|1,..."
     // With keep_config: the originals of what --disable-fw-lldp changed are kept in this file
     // across agent restarts (a restart does not flip the NICs back and forth: some drivers reset
@@ -165,8 +169,9 @@ struct Config {
     // with a warning.  0 = off.
     int64_t min_link_speed_mbps = 0;
     // Refuse a NIC whose switch port advertises (LLDP 802.3 Maximum Frame Size TLV) a maximum
-    // frame smaller than the NIC's MTU plus its Ethernet header: jumbo RoCE frames would be
-    // dropped by the switch, which shows as hung or crawling RCCL jobs rather than as an error.
+    // frame smaller than the NIC's frames (max_frame_for_mtu: MTU + header + FCS [+ 802.1Q tag]):
+    // jumbo RoCE frames would be dropped by the switch, which shows as hung or crawling RCCL jobs
+    // rather than as an error.
     bool check_peer_mtu = true;
     int64_t node_lock_wait_ns = 60LL * 1000000000;
 };
@@ -206,6 +211,10 @@ class LldpSource {
 // ttl = 0 builds the shutdown LLDPDU sent on cleanup.  mtu > 0 adds the IEEE 802.3 Maximum
 // Frame Size TLV (MTU + 18: header and FCS), so the switch's neighbour table shows what frames
 // the host sends and a mismatch is visible from the switch side too.
+// IEEE 802.3 Maximum Frame Size for an MTU: Ethernet header (14) + payload + FCS (4), and an
+// 802.1Q tag (4) when the NIC sends tagged frames.  Both what the agent advertises and the least
+// a switch port must accept (Config::check_peer_mtu).
+int max_frame_for_mtu(int mtu, bool vlan_tagged);
 lldp::Frame make_node_frame(const std::string& node_name, const std::string& ifname, const MacAddr& mac,
                             const std::string& gpu_bdf, uint16_t ttl = 120, int mtu = 0);
 std::unique_ptr<LldpSource> make_packet_source(bool promisc);
@@ -309,6 +318,12 @@ class Agent {
     std::unique_ptr<httpd::Server> httpd_;
     std::unique_ptr<ethtool::Ops> ethtool_;
     std::vector<ethtool::FwLldpResult> fw_lldp_;
+    // Records of an earlier agent for NICs this one does not select (the policy's interface list
+    // changed, a NIC was renamed) that could not be restored at start: kept in --fw-lldp-state
+    // so --cleanup can try again.
+    std::vector<ethtool::FwLldpResult> fw_lldp_carried_;
+    // The record: this agent's changes (with_current) and the carried ones; removed when empty.
+    void save_fw_lldp_state(bool with_current = true);
     std::vector<std::pair<std::string, std::string>> rccl_env_extra_;
     void disable_fw_lldp();
     void restore_fw_lldp_from_state();

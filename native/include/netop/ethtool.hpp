@@ -18,11 +18,13 @@
 // DCB_CAP_DCBX_HOST, an embedded agent runs DCBX, and with it the port's LLDP exchange.  Per
 // the drivers' dcbnl code, ice and i40e report DCB_CAP_DCBX_LLD_MANAGED while their firmware
 // agent runs, and mlx5_core reports no HOST bit in its firmware ("auto") DCBX mode and moves to
-// host mode on DCB_CMD_SDCBX with HOST set.  So `--disable-fw-lldp` hands DCBX to the host on
-// such a NIC and puts the original mode back on exit.  Whether that makes mlx5 firmware pass
-// LLDPDUs up is unverified on this pool (parity unpinned; the box's NICs live outside its
-// network namespace).  A NIC that stays silent is diagnosed after --wait with its DCBX mode
-// (Agent::diagnose_silent).
+// host mode on DCB_CMD_SDCBX with HOST set.  Handing DCBX to the host on such a NIC is a separate
+// opt-in (`--fw-lldp-dcbx-host`, policy `handDcbxToHost`): the firmware then stops negotiating
+// PFC/ETS with the switch, which lossless RoCE depends on unless the host runs a DCBX agent of its
+// own, and whether it makes mlx5 firmware pass LLDPDUs up is unverified on this pool (parity
+// unpinned; the box's NICs live outside its network namespace).  Without it `--disable-fw-lldp`
+// only reads the DCBX mode there.  The original mode goes back on exit.  A NIC that stays silent
+// is diagnosed after --wait with its DCBX mode (Agent::diagnose_silent).
 #pragma once
 
 #include <cstdint>
@@ -85,13 +87,15 @@ struct FwLldpResult {
     std::string summary() const;
 };
 
-// Applies the first matching rule on `ifname`; with no applicable private flag, hands an
-// embedded DCBX agent's port to the host (DCB_CMD_SDCBX).  Never throws (errors land in .error).
-// With apply = false (the agent's --dry-run) nothing is set: .would_change says what would be.
+// Applies the first matching rule on `ifname`; with no applicable private flag, reads the DCBX
+// mode and, only with hand_dcbx, hands an embedded DCBX agent's port to the host
+// (DCB_CMD_SDCBX).  Never throws (errors land in .error).  With apply = false (the agent's
+// --dry-run) nothing is set: .would_change says what would be.
 FwLldpResult disable_fw_lldp(Ops& ops, const std::string& ifname, const std::vector<FlagRule>& rules,
-                             bool apply = true);
-// Puts back the original private flags / DCBX mode if disable_fw_lldp changed them.
-void restore(Ops& ops, const FwLldpResult& r);
+                             bool apply = true, bool hand_dcbx = false);
+// Puts back the original private flags / DCBX mode if disable_fw_lldp changed them; false when
+// any of it could not be put back (e.g. the interface is gone or was renamed).
+bool restore(Ops& ops, const FwLldpResult& r);
 
 // The originals of what was changed, kept on the node across agent restarts (--keep-config
 // with --fw-lldp-state): one line per change, "<ifname> priv 0x<bits>" or "<ifname> dcbx

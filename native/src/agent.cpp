@@ -85,6 +85,8 @@ bool fd_readable(int fd) {
 
 std::unique_ptr<LldpSource> make_packet_source(bool promisc) { return std::make_unique<PacketSource>(promisc); }
 
+int max_frame_for_mtu(int mtu, bool vlan_tagged) { return mtu + 18 + (vlan_tagged ? 4 : 0); }
+
 lldp::Frame make_node_frame(const std::string& node_name, const std::string& ifname, const MacAddr& mac,
                             const std::string& gpu_bdf, uint16_t ttl, int mtu) {
     lldp::Frame f;
@@ -99,7 +101,7 @@ lldp::Frame make_node_frame(const std::string& node_name, const std::string& ifn
     f.system_name = node_name;
     f.system_description = "AMD Instinct MI355X node (amd-network-operator link discovery)";
     f.capabilities = std::make_pair(uint16_t(0x0080), uint16_t(0x0080));  // station only
-    if (mtu > 0 && ttl > 0) f.set_max_frame_size(uint16_t(std::min(mtu + 18, 0xffff)));
+    if (mtu > 0 && ttl > 0) f.set_max_frame_size(uint16_t(std::min(max_frame_for_mtu(mtu, false), 0xffff)));
     return f;
 }
 
@@ -225,7 +227,7 @@ void Agent::disable_fw_lldp() {
         if (auto t = read_file(cfg_.fw_lldp_state))
             for (auto& e : ethtool::decode_state(*t)) earlier[e.ifname] = e;
     for (auto& n : nics_) {
-        auto r = ethtool::disable_fw_lldp(*ethtool_, n.ifname, rules);
+        auto r = ethtool::disable_fw_lldp(*ethtool_, n.ifname, rules, true, cfg_.fw_lldp_dcbx_host);
         n.fw_lldp = r.summary();
         if (r.dcbx) n.dcbx = ethtool::dcbx_str(*r.dcbx);
         n.dcbx_embedded = r.dcbx && ethtool::dcbx_embedded(*r.dcbx) && !r.dcbx_changed;
@@ -240,19 +242,33 @@ void Agent::disable_fw_lldp() {
                 r.dcbx_changed = true;
                 r.dcbx = it->second.dcbx;
             }
+            earlier.erase(it);
         }
         fw_lldp_.push_back(std::move(r));
     }
-    if (!cfg_.fw_lldp_state.empty()) {  // also without --keep-config: an agent that fails leaves them changed
-        try {
-            const std::string text = ethtool::encode_state(fw_lldp_);
-            if (!text.empty())
-                write_file_atomic(cfg_.fw_lldp_state, text);
-            else if (::unlink(cfg_.fw_lldp_state.c_str()) != 0 && errno != ENOENT)
-                NLOG_W("Could not remove %s: %s", cfg_.fw_lldp_state.c_str(), std::strerror(errno));
-        } catch (const std::exception& e) {
-            NLOG_W("Could not record the firmware LLDP originals in %s: %s", cfg_.fw_lldp_state.c_str(), e.what());
-        }
+    // What is left of the record belongs to NICs this agent does not select any more: they are
+    // not ours now, so their originals go back at once; one that cannot be reached (renamed,
+    // gone) stays in the record for --cleanup.
+    for (auto& [name, r] : earlier) {
+        NLOG_I("%s: no longer selected; restoring its firmware LLDP settings", name.c_str());
+        if (!ethtool::restore(*ethtool_, r)) fw_lldp_carried_.push_back(r);
+    }
+    save_fw_lldp_state();
+}
+
+void Agent::save_fw_lldp_state(bool with_current) {
+    if (cfg_.fw_lldp_state.empty()) return;  // also without --keep-config: an agent that fails leaves them changed
+    try {
+        std::vector<ethtool::FwLldpResult> all;
+        if (with_current) all = fw_lldp_;
+        all.insert(all.end(), fw_lldp_carried_.begin(), fw_lldp_carried_.end());
+        const std::string text = ethtool::encode_state(all);
+        if (!text.empty())
+            write_file_atomic(cfg_.fw_lldp_state, text);
+        else if (::unlink(cfg_.fw_lldp_state.c_str()) != 0 && errno != ENOENT)
+            NLOG_W("Could not remove %s: %s", cfg_.fw_lldp_state.c_str(), std::strerror(errno));
+    } catch (const std::exception& e) {
+        NLOG_W("Could not record the firmware LLDP originals in %s: %s", cfg_.fw_lldp_state.c_str(), e.what());
     }
 }
 
@@ -277,9 +293,7 @@ void Agent::post_cleanups() {
     NLOG_I("Clean up before exiting...");
     if (ethtool_ && !persist_fw_lldp()) {  // kept on the node for the next agent / --cleanup otherwise
         for (const auto& r : fw_lldp_) ethtool::restore(*ethtool_, r);
-        if (!cfg_.fw_lldp_state.empty() && !fw_lldp_.empty() && ::unlink(cfg_.fw_lldp_state.c_str()) != 0 &&
-            errno != ENOENT)
-            NLOG_W("Could not remove %s: %s", cfg_.fw_lldp_state.c_str(), std::strerror(errno));
+        if (!fw_lldp_.empty()) save_fw_lldp_state(false);  // only what could not be reached stays (normally: none)
     }
     if (cfg_.lldp_announce && cfg_.mode == "L3" && !cfg_.keep_config) {
         // Shutdown LLDPDU (TTL 0): the switch drops us from its neighbour table right away.
@@ -749,10 +763,13 @@ bool Agent::configure_interface(NicState& n) {
         NLOG_W("Interface '%s' not configured: %s", n.ifname.c_str(), n.config_error.c_str());
         return false;
     }
-    if (cfg_.check_peer_mtu && n.peer_max_frame > 0 && n.peer_max_frame < cfg_.mtu + 14) {
-        n.config_error = strfmt("its switch port accepts frames up to %d bytes, but MTU %d needs %d: jumbo RoCE frames "
-                                "would be dropped (raise the switch port's MTU, or lower the policy's mtu)",
-                                n.peer_max_frame, cfg_.mtu, cfg_.mtu + 14);
+    // The 802.3 Maximum Frame Size counts the whole frame: MTU + 14 (header) + 4 (FCS), + 4 more
+    // for an 802.1Q tag on a VLAN NIC -- the same count the agent advertises (make_node_frame).
+    const int need = max_frame_for_mtu(cfg_.mtu, n.link.kind == "vlan");
+    if (cfg_.check_peer_mtu && n.peer_max_frame > 0 && n.peer_max_frame < need) {
+        n.config_error = strfmt("its switch port accepts frames up to %d bytes, but MTU %d needs %d%s: jumbo RoCE "
+                                "frames would be dropped (raise the switch port's MTU, or lower the policy's mtu)",
+                                n.peer_max_frame, cfg_.mtu, need, n.link.kind == "vlan" ? " (802.1Q tagged)" : "");
         NLOG_W("Interface '%s' not configured: %s", n.ifname.c_str(), n.config_error.c_str());
         return false;
     }
@@ -1136,8 +1153,10 @@ void Agent::diagnose_silent() {
             why = "the link received nothing: check the cable, the switch port and its LLDP transmit setting";
         } else if (n.dcbx_embedded) {
             why = "the NIC's embedded agent runs DCBX and LLDP on this port (DCBX " + n.dcbx + ")" +
-                  (cfg_.disable_fw_lldp ? " although --disable-fw-lldp ran (" + n.fw_lldp + ")"
-                                        : ": run with --disable-fw-lldp to hand DCBX to the host");
+                  (cfg_.disable_fw_lldp && cfg_.fw_lldp_dcbx_host
+                       ? " although --disable-fw-lldp ran (" + n.fw_lldp + ")"
+                       : ": run with --disable-fw-lldp --fw-lldp-dcbx-host to hand DCBX to the host (the host must "
+                         "then run DCBX for PFC/ETS itself)");
         } else if (n.driver == "i40e" || n.driver == "ice") {
             why = cfg_.disable_fw_lldp ? "NIC-firmware LLDP agent suspected although --disable-fw-lldp ran (" + n.fw_lldp + ")"
                                        : "NIC-firmware LLDP agent suspected: run with --disable-fw-lldp";
@@ -1245,7 +1264,7 @@ void Agent::dry_run_report() {
             rules = ethtool::parse_rules(cfg_.fw_lldp_flags);
             if (!ethtool_) ethtool_ = ethtool::make_ioctl_ops();
             for (auto& n : nics_) {
-                auto r = ethtool::disable_fw_lldp(*ethtool_, n.ifname, rules, false);
+                auto r = ethtool::disable_fw_lldp(*ethtool_, n.ifname, rules, false, cfg_.fw_lldp_dcbx_host);
                 n.fw_lldp = r.summary();
                 if (r.dcbx) {
                     n.dcbx = ethtool::dcbx_str(*r.dcbx);

@@ -155,7 +155,8 @@ std::string FwLldpResult::summary() const {
     return "no firmware LLDP flag";
 }
 
-FwLldpResult disable_fw_lldp(Ops& ops, const std::string& ifname, const std::vector<FlagRule>& rules, bool apply) {
+FwLldpResult disable_fw_lldp(Ops& ops, const std::string& ifname, const std::vector<FlagRule>& rules, bool apply,
+                             bool hand_dcbx) {
     FwLldpResult r;
     r.ifname = ifname;
     r.dry_run = !apply;
@@ -189,7 +190,7 @@ FwLldpResult disable_fw_lldp(Ops& ops, const std::string& ifname, const std::vec
     // No private flag for this driver: is an embedded agent running DCBX (and LLDP) here?
     try {
         r.dcbx = ops.dcbx_get(ifname);
-        if (r.dcbx && dcbx_embedded(*r.dcbx)) {
+        if (hand_dcbx && r.dcbx && dcbx_embedded(*r.dcbx)) {
             uint8_t want = uint8_t(DCB_CAP_DCBX_HOST | (*r.dcbx & (DCB_CAP_DCBX_VER_CEE | DCB_CAP_DCBX_VER_IEEE)));
             if (!(want & (DCB_CAP_DCBX_VER_CEE | DCB_CAP_DCBX_VER_IEEE))) want |= DCB_CAP_DCBX_VER_IEEE;
             if (!apply) {
@@ -208,12 +209,14 @@ FwLldpResult disable_fw_lldp(Ops& ops, const std::string& ifname, const std::vec
     return r;
 }
 
-void restore(Ops& ops, const FwLldpResult& r) {
+bool restore(Ops& ops, const FwLldpResult& r) {
+    bool all = true;
     if (r.changed) {
         try {
             ops.set(r.ifname, r.original_bits);
         } catch (const std::exception& e) {
             NLOG_W("%s: could not restore private flags: %s", r.ifname.c_str(), e.what());
+            all = false;
         }
     }
     if (r.dcbx_changed) {
@@ -222,10 +225,13 @@ void restore(Ops& ops, const FwLldpResult& r) {
             bool ok = ops.dcbx_set(r.ifname, *r.dcbx);
             if (!ok && !(*r.dcbx & DCB_CAP_DCBX_LLD_MANAGED)) ok = ops.dcbx_set(r.ifname, 0);
             if (!ok) NLOG_W("%s: the driver refused to restore DCBX mode %s", r.ifname.c_str(), dcbx_str(*r.dcbx).c_str());
+            all &= ok;
         } catch (const std::exception& e) {
             NLOG_W("%s: could not restore the DCBX mode: %s", r.ifname.c_str(), e.what());
+            all = false;
         }
     }
+    return all;
 }
 
 std::string encode_state(const std::vector<FwLldpResult>& rs) {

@@ -851,13 +851,18 @@ TEST(ethtool_dcbx_handed_to_the_host_and_back) {
     CHECK_EQ(ethtool::dcbx_str(0x06), std::string("0x06 (lld-managed, cee)"));
     CHECK(ethtool::dcbx_embedded(0x0c) && ethtool::dcbx_embedded(0x06) && !ethtool::dcbx_embedded(0x0d));
     auto rules = ethtool::builtin_rules();
-    auto a = ethtool::disable_fw_lldp(e, "mlx0", rules);
+    // Without the opt-in (--fw-lldp-dcbx-host) the mode is only read: the firmware keeps
+    // negotiating PFC/ETS with the switch.
+    auto ro = ethtool::disable_fw_lldp(e, "mlx0", rules);
+    CHECK(!ro.dcbx_changed && ro.dcbx && e.dcbx_sets.empty());
+    CHECK_EQ(ro.summary(), std::string("no firmware LLDP flag; DCBX 0x0c (firmware, cee, ieee)"));
+    auto a = ethtool::disable_fw_lldp(e, "mlx0", rules, true, true);
     CHECK(a.dcbx_changed && !a.changed && a.error.empty());
     CHECK_EQ(int(e.dcbx["mlx0"]), 0x0d);
     CHECK_EQ(a.summary(), std::string("DCBX handed to the host (was 0x0c (firmware, cee, ieee))"));
-    auto b = ethtool::disable_fw_lldp(e, "mlx1", rules);
+    auto b = ethtool::disable_fw_lldp(e, "mlx1", rules, true, true);
     CHECK(!b.dcbx_changed && b.summary() == "no firmware LLDP flag; DCBX 0x0d (host, cee, ieee)");
-    auto c = ethtool::disable_fw_lldp(e, "ionic0", rules);  // no private flags, no DCB interface
+    auto c = ethtool::disable_fw_lldp(e, "ionic0", rules, true, true);  // no private flags, no DCB interface
     CHECK(!c.dcbx && !c.dcbx_changed && c.error.empty() && c.summary() == "no firmware LLDP flag");
     // Restore: the original mode is refused by mlx5 (no HOST bit, not 0), so 0 hands it back.
     ethtool::restore(e, a);
@@ -870,7 +875,7 @@ TEST(ethtool_dcbx_handed_to_the_host_and_back) {
     e.drivers["ice0"] = "ice";
     e.flags["ice0"] = {{"link-down-on-close", "fw-lldp-agent"}, 0x2};
     e.dcbx["ice0"] = DCB_CAP_DCBX_LLD_MANAGED | DCB_CAP_DCBX_VER_IEEE;
-    auto d = ethtool::disable_fw_lldp(e, "ice0", rules);
+    auto d = ethtool::disable_fw_lldp(e, "ice0", rules, true, true);
     CHECK(d.changed && !d.dcbx_changed && e.dcbx_sets.size() == size_t(3));
     // A driver refusing host mode is an error the status shows, not an exception.
     e.dcbx["odd0"] = DCB_CAP_DCBX_LLD_MANAGED;
@@ -878,7 +883,7 @@ TEST(ethtool_dcbx_handed_to_the_host_and_back) {
         bool dcbx_set(const std::string&, uint8_t) override { return false; }
     } r;
     r.dcbx["odd0"] = DCB_CAP_DCBX_LLD_MANAGED;
-    auto f = ethtool::disable_fw_lldp(r, "odd0", rules);
+    auto f = ethtool::disable_fw_lldp(r, "odd0", rules, true, true);
     CHECK(!f.dcbx_changed && f.error.find("refused DCBX host mode 0x09 (host, ieee)") != std::string::npos);
 }
 
@@ -1308,6 +1313,7 @@ TEST(agent_dry_run_reports_what_disable_fw_lldp_would_change) {
     Fixture f;
     f.cfg.dry_run = true;
     f.cfg.disable_fw_lldp = true;
+    f.cfg.fw_lldp_dcbx_host = true;
     f.cfg.sysfs_root = f.tmp.path + "/sys/";
     auto eth = std::make_unique<FakeEthtool>();
     eth->drivers = {{"ens0", "ice"}, {"ens1", "mlx5_core"}, {"ens2", "mlx5_core"}};
@@ -1827,6 +1833,7 @@ TEST(agent_keep_config_keeps_firmware_lldp_off_across_restarts_until_cleanup) {
     Fixture f;
     f.cfg.keep_config = true;
     f.cfg.disable_fw_lldp = true;
+    f.cfg.fw_lldp_dcbx_host = true;
     f.cfg.lldp_cache = f.tmp.path + "/lldp-cache";
     f.cfg.fw_lldp_state = f.tmp.path + "/fw-lldp-state";
     auto make_eth = [] {
@@ -2028,7 +2035,7 @@ TEST(agent_switch_port_with_a_smaller_max_frame_than_the_mtu_is_refused) {
         }
         if (mtu == 9000) {
             CHECK(err.find("Not configured: ens1: its switch port accepts frames up to 1518 bytes, but MTU 9000 needs "
-                           "9014") != std::string::npos);
+                           "9018") != std::string::npos);
             auto st = read_file(f.cfg.status_file);
             CHECK(st && st->find("\"peer_max_frame\":1518") != std::string::npos);
         } else {
@@ -2280,4 +2287,76 @@ TEST(agent_l2_waits_for_carrier_and_labels_only_when_every_nic_has_a_link) {
     }
     CHECK(err.find("Not all interfaces have a link (2/3). No carrier: ens2") == 0);
     CHECK(!path_exists(g.cfg.labels.path()));
+}
+
+TEST(agent_firmware_lldp_records_of_nics_no_longer_selected_are_not_lost) {
+    // The record an earlier agent left names ens0 (still selected), old0 (dropped from the
+    // policy's interface list) and gone0 (renamed: unreachable).  old0 is not ours any more, so its
+    // original goes back at once; gone0 cannot be reached and stays in the record for --cleanup,
+    // also after this agent's own clean exit.
+    for (bool keep : {true, false}) {
+        Fixture f;
+        f.cfg.keep_config = keep;
+        f.cfg.disable_fw_lldp = true;
+        f.cfg.lldp_cache = f.tmp.path + "/lldp-cache";
+        f.cfg.fw_lldp_state = f.tmp.path + "/fw-lldp-state";
+        write_file_atomic(f.cfg.fw_lldp_state, "ens0 priv 0x2\nold0 priv 0x4\ngone0 dcbx 0x0c\n");
+        auto eth = std::make_unique<FakeEthtool>();
+        eth->drivers = {{"ens0", "ice"}, {"old0", "ice"}};
+        eth->flags["ens0"] = {{"link-down-on-close", "fw-lldp-agent"}, 0x0};  // already off (by the earlier agent)
+        eth->flags["old0"] = {{"link-down-on-close", "fw-lldp-agent", "x"}, 0x0};
+        FakeEthtool* raw = eth.get();
+        Pipe stop;
+        stop.fire();
+        {
+            agent::Agent a(f.cfg, f.ops, f.all_valid(), f.nm());
+            a.set_ethtool_ops(std::move(eth));
+            a.run(stop.fd[0]);
+            CHECK(a.ready());
+            CHECK_EQ(raw->flags["old0"].bits, uint32_t(0x4));  // restored at start
+        }
+        auto st = read_file(f.cfg.fw_lldp_state);
+        if (keep) {
+            CHECK(st && *st == "ens0 priv 0x2\ngone0 dcbx 0x0c\n");
+            CHECK_EQ(raw->flags["ens0"].bits, uint32_t(0x0));  // kept off across the restart
+        } else {
+            CHECK(st && *st == "gone0 dcbx 0x0c\n");
+            CHECK_EQ(raw->flags["ens0"].bits, uint32_t(0x2));  // the true original, on the clean exit
+        }
+    }
+}
+
+TEST(agent_max_frame_boundaries_match_what_the_agent_advertises) {
+    // One definition for sending and checking (802.3: header + payload + FCS, + 802.1Q tag on a
+    // VLAN NIC): for MTU 9000, 9017 is refused and 9018 accepted; 1518 is enough for MTU 1500;
+    // a tagged NIC needs 9022.
+    CHECK_EQ(agent::max_frame_for_mtu(9000, false), 9018);
+    CHECK_EQ(agent::max_frame_for_mtu(1500, false), 1518);
+    CHECK_EQ(agent::max_frame_for_mtu(9000, true), 9022);
+    struct Case {
+        int mtu, frame;
+        bool vlan, ok;
+    };
+    for (const Case c : {Case{9000, 9017, false, false}, Case{9000, 9018, false, true}, Case{1500, 1518, false, true},
+                         Case{1500, 1517, false, false}, Case{9000, 9021, true, false}, Case{9000, 9022, true, true}}) {
+        Fixture f;
+        f.cfg.keep_running = false;
+        f.cfg.mtu = c.mtu;
+        f.cfg.interfaces = "ens1";
+        if (c.vlan) f.ops.links["ens1"].kind = "vlan";
+        auto src = f.all_valid();
+        src->frames["ens1"].set_max_frame_size(uint16_t(c.frame));
+        agent::Agent a(f.cfg, f.ops, std::move(src), f.nm());
+        std::string err;
+        try {
+            a.run(-1);
+        } catch (const agent::AgentError& e) {
+            err = e.what();
+        }
+        CHECK_EQ(err.empty(), c.ok);
+        if (!c.ok)
+            CHECK(err.find(strfmt("accepts frames up to %d bytes, but MTU %d needs %d%s", c.frame, c.mtu,
+                                  agent::max_frame_for_mtu(c.mtu, c.vlan), c.vlan ? " (802.1Q tagged)" : "")) !=
+                  std::string::npos);
+    }
 }

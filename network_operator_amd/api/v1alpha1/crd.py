@@ -68,10 +68,18 @@ def openapi_schema() -> dict:
             "nicDrivers": {"description": "NIC driver allow-list for GPU-affinity discovery (default: common RoCE drivers).",
                            "items": {"type": "string"}, "type": "array"},
             "disableFirmwareLldp": {"description": "L3: turn off NIC-firmware LLDP agents (ethtool private flags, e.g. i40e\n"
-                                                   "disable-fw-lldp, ice fw-lldp-agent; on other DCB NICs such as mlx5_core\n"
-                                                   "the DCBX mode is handed to the host) while the agent runs, so switch\n"
+                                                   "disable-fw-lldp, ice fw-lldp-agent) while the agent runs, so switch\n"
                                                    "LLDPDUs reach the host.",
                                     "type": "boolean"},
+            "handDcbxToHost": {"description": "With disableFirmwareLldp, on DCB NICs without a firmware-LLDP flag whose\n"
+                                              "DCBX an embedded agent runs (mlx5_core firmware mode): hand DCBX to the\n"
+                                              "host.  The firmware then stops negotiating PFC/ETS with the switch, so\n"
+                                              "only for hosts that run DCBX themselves.  Restored when the agent exits.",
+                               "type": "boolean"},
+            "checkPeerMtu": {"description": "L3: refuse a NIC whose switch port advertises (LLDP 802.3 Maximum Frame\n"
+                                            "Size) frames smaller than the NIC's own (MTU + 18, + 4 on a VLAN NIC).\n"
+                                            "Default true; false for switches that misreport the TLV.",
+                             "type": "boolean"},
             "gpuDirectRdma": {"description": "Require GPUDirect RDMA before labelling the node: Any, PeerMem (amdkfd\n"
                                              "peer-memory client) or DmaBuf (RDMA dma-buf MRs).  Empty: report only.",
                               "enum": ["Any", "PeerMem", "DmaBuf"], "type": "string"},
@@ -150,7 +158,9 @@ def openapi_schema() -> dict:
                            "enum": list(T.PULL_POLICIES), "type": "string"},
             "disableNetworkManager": {"description": "Take the host NICs away from NetworkManager.",
                                       "type": "boolean"},
-            "interfaces": {"description": "Host NICs to configure (default: every RDMA NIC of nicDrivers).",
+            "interfaces": {"description": "Host NICs to configure (default: every RDMA NIC of nicDrivers that is\n"
+                                          "neither a GPU's scale-out rail nor the node's own NIC: default route,\n"
+                                          "a non-/30 address, a route the agent does not install).",
                            "items": {"type": "string", "maxLength": 15}, "type": "array"},
             "nicDrivers": {"description": "NIC driver allow-list for RDMA NIC discovery.",
                            "items": {"type": "string"}, "type": "array"},
@@ -162,6 +172,7 @@ def openapi_schema() -> dict:
             "lldpWait": LLDP_WAIT_SCHEMA,
             "keepConfigOnRestart": {"description": "As amdScaleOut.keepConfigOnRestart, for the host NICs.",
                                     "type": "boolean"},
+            "checkPeerMtu": {"description": "As amdScaleOut.checkPeerMtu, for the host NICs.", "type": "boolean"},
         },
         "required": ["layer"],
     }

@@ -118,6 +118,10 @@ class AmdScaleOutSpec:
     railSwitchPattern: str = ""
     # Minimum negotiated link speed of every scale-out NIC, Gb/s (0 = off)
     minLinkSpeedGbps: int = 0
+    # L3 jumbo-frame check against the switch port's LLDP 802.3 Maximum Frame Size (None = on)
+    checkPeerMtu: Optional[bool] = None
+    # With disableFirmwareLldp: hand DCBX to the host on DCB NICs without a firmware-LLDP flag
+    handDcbxToHost: bool = False
     validation: Optional[ValidationSpec] = None
     extra: Dict[str, Any] = field(default_factory=dict)
 
@@ -128,7 +132,7 @@ class AmdScaleOutSpec:
     _FIELDS = ("disableNetworkManager", "layer", "image", "pullPolicy", "mtu", "xgmiCheck", "lldpAnnounce",
                "interfaces", "nicDrivers", "disableFirmwareLldp", "metricsPort", "gpuDirectRdma", "rcclEnv",
                "railTableBase", "rcclSocketIfname", "lldpCache", "verifyPeers", "lldpWait", "keepConfigOnRestart",
-               "railSwitchPattern", "minLinkSpeedGbps", "validation")
+               "railSwitchPattern", "minLinkSpeedGbps", "checkPeerMtu", "handDcbxToHost", "validation")
 
     def to_dict(self) -> dict:
         d: dict = {}
@@ -172,6 +176,10 @@ class AmdScaleOutSpec:
             d["railSwitchPattern"] = self.railSwitchPattern
         if self.minLinkSpeedGbps:
             d["minLinkSpeedGbps"] = self.minLinkSpeedGbps
+        if self.checkPeerMtu is not None:
+            d["checkPeerMtu"] = self.checkPeerMtu
+        if self.handDcbxToHost:
+            d["handDcbxToHost"] = True
         if self.validation is not None:
             d["validation"] = self.validation.to_dict()
         d.update(copy.deepcopy(self.extra))
@@ -200,6 +208,8 @@ class AmdScaleOutSpec:
             keepConfigOnRestart=bool(d.pop("keepConfigOnRestart", False)),
             railSwitchPattern=d.pop("railSwitchPattern", "") or "",
             minLinkSpeedGbps=int(d.pop("minLinkSpeedGbps", 0) or 0),
+            checkPeerMtu=d.pop("checkPeerMtu", None),
+            handDcbxToHost=bool(d.pop("handDcbxToHost", False)),
             verifyPeers=bool(d.pop("verifyPeers", False)),
             lldpWait=d.pop("lldpWait", "") or "",
             validation=ValidationSpec.from_dict(d.pop("validation", None)),
@@ -224,6 +234,7 @@ class HostNicSpec:
     verifyPeers: bool = False
     lldpWait: str = ""
     keepConfigOnRestart: bool = False
+    checkPeerMtu: Optional[bool] = None
     extra: Dict[str, Any] = field(default_factory=dict)
 
     def to_dict(self) -> dict:
@@ -243,6 +254,8 @@ class HostNicSpec:
             d["verifyPeers"] = True
         if self.keepConfigOnRestart:
             d["keepConfigOnRestart"] = True
+        if self.checkPeerMtu is not None:
+            d["checkPeerMtu"] = self.checkPeerMtu
         d.update(copy.deepcopy(self.extra))
         return d
 
@@ -254,7 +267,8 @@ class HostNicSpec:
                 interfaces=list(d.pop("interfaces", []) or []), nicDrivers=list(d.pop("nicDrivers", []) or []),
                 driverImage=d.pop("driverImage", "") or "", verifyPeers=bool(d.pop("verifyPeers", False)),
                 lldpWait=d.pop("lldpWait", "") or "",
-                keepConfigOnRestart=bool(d.pop("keepConfigOnRestart", False)))
+                keepConfigOnRestart=bool(d.pop("keepConfigOnRestart", False)),
+                checkPeerMtu=d.pop("checkPeerMtu", None))
         s.extra = d
         return s
 

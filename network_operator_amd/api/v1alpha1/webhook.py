@@ -174,6 +174,10 @@ def validate_amd_so_spec(s: T.AmdScaleOutSpec) -> List[str]:
     validate_rail_switch_pattern(s.railSwitchPattern)
     if s.railSwitchPattern and s.layer == "L2":
         warnings.append("railSwitchPattern has no effect in L2 mode (no LLDP)")
+    if s.handDcbxToHost and not (s.disableFirmwareLldp and s.layer == "L3"):
+        warnings.append("handDcbxToHost has no effect without disableFirmwareLldp in L3 mode")
+    if s.checkPeerMtu is not None and s.layer == "L2":
+        warnings.append("checkPeerMtu has no effect in L2 mode (no LLDP)")
     return warnings
 
 

@@ -172,6 +172,8 @@ def agent_args(p: T.NetworkClusterPolicy) -> List[str]:
         args.append("--nic-drivers=" + ",".join(so.nicDrivers))
     if so.disableFirmwareLldp and so.layer == "L3":
         args.append("--disable-fw-lldp")
+        if so.handDcbxToHost:  # opt-in: the NIC firmware stops negotiating PFC/ETS
+            args.append("--fw-lldp-dcbx-host")
     if so.metricsPort:
         args.append(f"--metrics-bind-address=:{so.metricsPort}")
     if so.railTableBase and so.layer == "L3":
@@ -192,6 +194,8 @@ def agent_args(p: T.NetworkClusterPolicy) -> List[str]:
         args.append(f"--rail-switch-pattern={so.railSwitchPattern}")
     if so.minLinkSpeedGbps:
         args.append(f"--min-link-speed-gbps={so.minLinkSpeedGbps}")
+    if so.checkPeerMtu is False and so.layer == "L3":
+        args.append("--check-peer-mtu=false")
     args.append(f"--status-file={discovery.AGENT_STATUS_FILE}")
     if so.verifyPeers and so.layer == "L3":
         args.append(f"--verify-peers={VERIFY_PEERS_TIMEOUT}")
@@ -274,6 +278,8 @@ def host_nic_agent_args(p: T.NetworkClusterPolicy) -> List[str]:
         args.append("--interfaces=" + ",".join(hn.interfaces))
     if hn.nicDrivers:
         args.append("--nic-drivers=" + ",".join(hn.nicDrivers))
+    if hn.checkPeerMtu is False and hn.layer == "L3":
+        args.append("--check-peer-mtu=false")
     if hn.keepConfigOnRestart:
         if hn.layer == "L3":  # its own cache beside the scale-out agent's
             args.append(f"--lldp-cache={ARTIFACT_DIR_CONTAINER}/{HOST_NIC_LLDP_CACHE_FILE}")

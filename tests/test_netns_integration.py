@@ -384,7 +384,7 @@ def test_switch_without_jumbo_frames_is_caught_before_jobs_hang():
     assert not bad["ready"] and bad["agent_rc"] == 1
     err = [ln for ln in bad["agent_log"].splitlines() if ln.startswith("Error: ")][-1]
     assert err.startswith("Error: Not all interfaces were configured (0/2). Not configured: "), err
-    assert "its switch port accepts frames up to 1518 bytes, but MTU 9000 needs 9014" in err
+    assert "its switch port accepts frames up to 1518 bytes, but MTU 9000 needs 9018" in err
 
 
 def test_default_host_nic_policy_leaves_the_management_nic_and_the_gpu_rails_alone():

@@ -1155,3 +1155,35 @@ def test_a_starting_node_is_not_reported_as_degraded():
 
     assert _starting_up("ens0: waiting for LLDP; ens1: not configured yet")
     assert not _starting_up("ens0: waiting for LLDP; ens1: link down")
+
+
+def test_dcbx_hand_over_and_peer_mtu_check_are_policy_fields():
+    """handing DCBX to the host (mlx5 firmware mode) is its own opt-in, off by default,
+    so disableFirmwareLldp keeps meaning "private flags only" on upgrade; checkPeerMtu: false turns
+    the jumbo-frame check off for switches that misreport the 802.3 TLV."""
+    from network_operator_amd.api.v1alpha1 import types as T
+    from network_operator_amd.api.v1alpha1 import webhook as W
+    from network_operator_amd.operator.reconciler import agent_args, host_nic_agent_args
+
+    p = T.new_policy("p", layer="L3")
+    p.spec.amdScaleOut.disableFirmwareLldp = True
+    args = agent_args(p)
+    assert "--disable-fw-lldp" in args and "--fw-lldp-dcbx-host" not in args
+    assert "--check-peer-mtu=false" not in args  # the agent's default: on
+    p.spec.amdScaleOut.handDcbxToHost = True
+    p.spec.amdScaleOut.checkPeerMtu = False
+    args = agent_args(p)
+    assert args.index("--fw-lldp-dcbx-host") == args.index("--disable-fw-lldp") + 1
+    assert "--check-peer-mtu=false" in args
+    back = T.NetworkClusterPolicy.from_dict(p.to_dict()).spec.amdScaleOut
+    assert back.handDcbxToHost is True and back.checkPeerMtu is False and not back.extra
+    assert W.validate_create(p) == []
+    p.spec.amdScaleOut.disableFirmwareLldp = False
+    assert "--fw-lldp-dcbx-host" not in agent_args(p)
+    assert W.validate_create(p) == ["handDcbxToHost has no effect without disableFirmwareLldp in L3 mode"]
+    h = T.new_host_nic_policy("h", layer="L3", checkPeerMtu=False, nicDrivers=["mlx5_core"])
+    assert "--check-peer-mtu=false" in host_nic_agent_args(h)
+    assert T.NetworkClusterPolicy.from_dict(h.to_dict()).spec.hostNic.checkPeerMtu is False
+    from network_operator_amd.api.v1alpha1 import crd as CRD
+
+    assert not CRD.validate(p.to_dict()) and not CRD.validate(h.to_dict())
