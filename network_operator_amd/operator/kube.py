@@ -246,13 +246,15 @@ class ApiClient:
         return ApiError(resp.status, body.get("reason", ""), body.get("message", ""), body)
 
     async def request(self, method: str, path: str, params: Optional[dict] = None, body: Any = None,
-                      content_type: str = "application/json") -> dict:
+                      content_type: str = "application/json", timeout: Optional[float] = None) -> dict:
+        """`timeout`: total seconds for this request (default: the client's), e.g. the lease
+        renewals, which must never outlast the leader-election renew deadline."""
         s = await self._sess()
         self.requests += 1
         data = json.dumps(body) if body is not None else None
         async with s.request(method, self.cfg.host + path, params=params, data=data,
                              headers=self._headers(content_type if data is not None else None),
-                             timeout=self._timeout) as resp:
+                             timeout=aiohttp.ClientTimeout(total=timeout) if timeout else self._timeout) as resp:
             if resp.status >= 400:
                 raise await self._error(resp)
             if resp.status == 204:
@@ -260,8 +262,9 @@ class ApiClient:
             return await resp.json(content_type=None)
 
     # -- CRUD --------------------------------------------------------------------------------------
-    async def get(self, res: Resource, name: str, namespace: Optional[str] = None) -> dict:
-        return await self.request("GET", res.path(namespace, name))
+    async def get(self, res: Resource, name: str, namespace: Optional[str] = None,
+                  timeout: Optional[float] = None) -> dict:
+        return await self.request("GET", res.path(namespace, name), timeout=timeout)
 
     async def list(self, res: Resource, namespace: Optional[str] = None, label_selector: Optional[str] = None,
                    field_selector: Optional[str] = None, resource_version: Optional[str] = None,
@@ -279,13 +282,14 @@ class ApiClient:
             params["resourceVersion"] = resource_version
         return await self.request("GET", res.path(namespace), params=params or None)
 
-    async def create(self, res: Resource, obj: dict, namespace: Optional[str] = None) -> dict:
+    async def create(self, res: Resource, obj: dict, namespace: Optional[str] = None,
+                     timeout: Optional[float] = None) -> dict:
         ns = namespace or obj.get("metadata", {}).get("namespace")
-        return await self.request("POST", res.path(ns), body=obj)
+        return await self.request("POST", res.path(ns), body=obj, timeout=timeout)
 
-    async def replace(self, res: Resource, obj: dict) -> dict:
+    async def replace(self, res: Resource, obj: dict, timeout: Optional[float] = None) -> dict:
         md = obj["metadata"]
-        return await self.request("PUT", res.path(md.get("namespace"), md["name"]), body=obj)
+        return await self.request("PUT", res.path(md.get("namespace"), md["name"]), body=obj, timeout=timeout)
 
     async def replace_status(self, res: Resource, obj: dict) -> dict:
         md = obj["metadata"]

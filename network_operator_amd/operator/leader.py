@@ -5,6 +5,15 @@ The reference manager enables it with ``--leader-elect`` and ID ``9a8a7ba6.intel
 duration 15 s, renew deadline 10 s, retry period 2 s (controller-runtime defaults).
 Expiry is judged on the *locally observed* time of the last record change, as client-go
 does, so clock skew between replicas does not matter.
+
+Safety of the renew loop (client-go's ``renew``: ``PollImmediateUntil(retryPeriod, ...,
+timeoutCtx(renewDeadline))``): another replica may take the lease ``lease_duration`` after it
+last saw it change, i.e. no earlier than our last successful renewal + ``lease_duration``.  So
+every renewal attempt -- and every API request inside it -- is bounded by what is left of
+``renew_deadline`` since that renewal (each request by at most ``retry_period`` as well), and
+when the deadline passes the leader's work is cancelled at once.  A replica whose API calls
+stall therefore stops reconciling ``lease_duration - renew_deadline`` (5 s by default) before
+anyone else can legally lead.
 """
 
 from __future__ import annotations
@@ -53,6 +62,7 @@ class LeaderElector:
         self._observed_time = 0.0
         self.is_leader = False
         self.transitions = 0
+        self.lost_at: Optional[float] = None  # loop time at which leadership was given up
 
     def _lease_body(self, prev: Optional[dict]) -> dict:
         spec_prev = (prev or {}).get("spec", {}) or {}
@@ -69,15 +79,19 @@ class LeaderElector:
             body["metadata"]["resourceVersion"] = prev["metadata"].get("resourceVersion")
         return body
 
+    def _request_timeout(self) -> float:
+        return self.retry_period
+
     async def try_acquire_or_renew(self) -> bool:
+        t = self._request_timeout()
         try:
-            lease = await self.client.get(kube.LEASES, self.name, self.namespace)
+            lease = await self.client.get(kube.LEASES, self.name, self.namespace, timeout=t)
         except ApiError as e:
             if not is_not_found(e):
                 log.warning("error retrieving lease %s: %s", self.name, e)
                 return False
             try:
-                await self.client.create(kube.LEASES, self._lease_body(None), namespace=self.namespace)
+                await self.client.create(kube.LEASES, self._lease_body(None), namespace=self.namespace, timeout=t)
             except ApiError as ce:
                 if is_already_exists(ce):
                     return False
@@ -93,7 +107,7 @@ class LeaderElector:
         if holder and holder != self.identity and self._observed_time + duration > self._loop_time():
             return False  # held by someone else and not expired
         try:
-            updated = await self.client.replace(kube.LEASES, self._lease_body(lease))
+            updated = await self.client.replace(kube.LEASES, self._lease_body(lease), timeout=t)
         except ApiError as e:
             if is_conflict(e):
                 return False
@@ -108,13 +122,14 @@ class LeaderElector:
         self._observed_time = self._loop_time()
 
     async def release(self) -> None:
+        t = self._request_timeout()
         try:
-            lease = await self.client.get(kube.LEASES, self.name, self.namespace)
+            lease = await self.client.get(kube.LEASES, self.name, self.namespace, timeout=t)
             if (lease.get("spec", {}) or {}).get("holderIdentity") != self.identity:
                 return
             lease["spec"]["holderIdentity"] = ""
             lease["spec"]["leaseDurationSeconds"] = 1
-            await self.client.replace(kube.LEASES, lease)
+            await self.client.replace(kube.LEASES, lease, timeout=t)
         except Exception as e:
             log.info("lease release failed: %s", e)
 
@@ -138,16 +153,24 @@ class LeaderElector:
                 if work.done():
                     await work  # propagate errors from the leader's work
                     return
-                await asyncio.sleep(self.retry_period)
-                try:
-                    ok = await self.try_acquire_or_renew()
-                except Exception as e:
-                    log.warning("renew failed: %s", e)
-                    ok = False
+                # Sleep until the next renewal, or until the leader's work ends.
+                await asyncio.wait({work}, timeout=self.retry_period)
+                if work.done():
+                    continue
+                left = self.renew_deadline - (self._loop_time() - last_ok)
+                ok = False
+                if left > 0:
+                    try:
+                        ok = await asyncio.wait_for(self.try_acquire_or_renew(), timeout=left)
+                    except asyncio.TimeoutError:
+                        log.warning("lease renewal still unanswered at the renew deadline")
+                    except Exception as e:
+                        log.warning("renew failed: %s", e)
                 if ok:
                     last_ok = self._loop_time()
-                elif self._loop_time() - last_ok > self.renew_deadline:
-                    log.error("leader election lost")
+                elif self._loop_time() - last_ok >= self.renew_deadline:
+                    log.error("leader election lost: no renewal within the %.1fs renew deadline", self.renew_deadline)
+                    self.lost_at = self._loop_time()
                     return
         finally:
             self.is_leader = False

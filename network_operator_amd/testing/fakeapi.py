@@ -23,7 +23,9 @@ here, so this server implements the API-server behaviour the operator depends on
 * a DaemonSet controller simulation: ``desiredNumberScheduled`` from Nodes matching the pod
   template's nodeSelector, ``numberReady`` from per-node agent readiness set by the test;
 * TokenReview / SubjectAccessReview answers from a token table (metrics authn/authz);
-* fault injection: fail the next N matching requests, drop all watch streams, compact.
+* fault injection: fail the next N matching requests, stall matching requests (a wedged API
+  server or network path, optionally for one client by its User-Agent), drop all watch
+  streams, compact.
 """
 
 from __future__ import annotations
@@ -209,6 +211,10 @@ class FakeApiServer:
         self.node_last_exit: Dict[Tuple[str, str], dict] = {}
         self.tokens: Dict[str, dict] = {}                    # bearer -> {"username", "groups", "allowed"}
         self.faults: List[_Fault] = []
+        # (method, path pattern, User-Agent or None, seconds): matching requests wait that long
+        # before they are served (the client usually gives up first)
+        self.stalls: List[tuple] = []
+        self._unstall: Optional[asyncio.Event] = None
         self.requests: List[Tuple[str, str]] = []
         self.accesses: set = set()                           # (verb, group, resource[/sub])
         self.admission_calls: List[Tuple[str, str]] = []
@@ -337,6 +343,17 @@ class FakeApiServer:
     def fail_next(self, method: str, path_regex: str, status: int = 500, count: int = 1,
                   reason: str = "InternalError") -> None:
         self.faults.append(_Fault(method.upper(), re.compile(path_regex), status, count, reason))
+
+    def stall(self, method: str, path_regex: str, seconds: float, user_agent: Optional[str] = None) -> None:
+        """Hold every matching request `seconds` before serving it, until clear_stalls()."""
+        self.stalls.append((method.upper(), re.compile(path_regex), user_agent, seconds))
+
+    def clear_stalls(self) -> None:
+        """Ends the stalls, releasing requests that are being held."""
+        self.stalls.clear()
+        if self._unstall is not None:
+            self._unstall.set()
+            self._unstall = None
 
     def drop_watches(self) -> None:
         for w in self.watches:
@@ -666,6 +683,14 @@ class FakeApiServer:
     async def _dispatch(self, req: web.Request) -> web.StreamResponse:
         path = req.path
         self.requests.append((req.method, path))
+        for method, pattern, ua, seconds in list(self.stalls):
+            if method in (req.method, "*") and pattern.search(path) and ua in (None, req.headers.get("User-Agent")):
+                if self._unstall is None:
+                    self._unstall = asyncio.Event()
+                try:
+                    await asyncio.wait_for(self._unstall.wait(), seconds)
+                except asyncio.TimeoutError:
+                    pass
         for f in list(self.faults):
             if f.method in (req.method, "*") and f.pattern.search(path):
                 f.count -= 1

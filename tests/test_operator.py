@@ -1187,3 +1187,54 @@ def test_dcbx_hand_over_and_peer_mtu_check_are_policy_fields():
     from network_operator_amd.api.v1alpha1 import crd as CRD
 
     assert not CRD.validate(p.to_dict()) and not CRD.validate(h.to_dict())
+
+
+def test_stalled_lease_renewal_stops_the_leader_before_anyone_else_can_lead():
+    """the leader's Lease PUTs stall for 20 s (a wedged API path).  Its renewal
+    attempts are bounded by the renew deadline, so it cancels its work within renew_deadline of
+    its last renewal -- before the lease (lease_duration) can expire for the standby -- and the two
+    replicas' work never overlaps.  (Unbounded, each stalled PUT ran to the client's 30 s timeout
+    while the stalled leader kept reconciling.)"""
+    lease_duration, renew_deadline, retry = 1.5, 1.0, 0.25
+
+    async def body():
+        fake = FakeApiServer()
+        url = await fake.start()
+        c1 = ApiClient(KubeConfig(host=url), user_agent="replica-one")
+        c2 = ApiClient(KubeConfig(host=url), user_agent="replica-two")
+        kw = dict(lease_duration=lease_duration, renew_deadline=renew_deadline, retry_period=retry)
+        e1 = LeaderElector(c1, NS, identity="one", **kw)
+        e2 = LeaderElector(c2, NS, identity="two", release_on_cancel=False, **kw)
+        loop = asyncio.get_event_loop()
+        ticks = {"one": [], "two": []}
+
+        async def work(name):
+            while True:  # "reconciling": a tick every 10 ms while this replica leads
+                ticks[name].append(loop.time())
+                await asyncio.sleep(0.01)
+
+        t1 = asyncio.ensure_future(e1.run(lambda: work("one")))
+        await eventually(lambda: bool(ticks["one"]))
+        t2 = asyncio.ensure_future(e2.run(lambda: work("two")))
+        await asyncio.sleep(3 * retry)
+        last_renew = fake.get_object(kube.LEASES, "9a8a7ba6.amd.com", NS)["spec"]["renewTime"]
+        fake.stall("PUT", r"/leases/", 20.0, user_agent="replica-one")
+        t_stall = loop.time()
+        await asyncio.wait_for(t1, renew_deadline + 2 * retry + 1.0)  # replica one gives up leading
+        assert e1.lost_at is not None and e1.lost_at - t_stall <= renew_deadline + retry + 0.1, e1.lost_at - t_stall
+        await eventually(lambda: bool(ticks["two"]), timeout=lease_duration + 3)
+        stop_one, start_two = max(ticks["one"]), min(ticks["two"])
+        assert stop_one < start_two, (stop_one, start_two)  # never both reconciling
+        assert stop_one - t_stall <= renew_deadline + retry + 0.1
+        lease = fake.get_object(kube.LEASES, "9a8a7ba6.amd.com", NS)
+        assert lease["spec"]["holderIdentity"] == "two" and lease["spec"]["renewTime"] != last_renew
+        fake.clear_stalls()
+        t2.cancel()
+        try:
+            await t2
+        except asyncio.CancelledError:
+            pass
+        await c1.close()
+        await c2.close()
+        await fake.stop()
+    run(body())
