@@ -187,6 +187,14 @@ constexpr uint8_t kRailProtocol = 0xa3;
 // Sanitises in place (MTU clamp to [1500, 9000], mode upper-cased); throws on a bad mode.
 void sanitize(Config& c);
 
+// The rail cabling check's regular expressions are ECMAScript (std::regex): "" when `pattern`
+// compiles, else the library's reason.  The webhook's grammar check is tested against these.
+std::string ecmascript_regex_error(const std::string& pattern);
+std::optional<bool> ecmascript_full_match(const std::string& pattern, const std::string& text);  // nullopt: no compile
+constexpr int kMaxRails = 16;  // GPU indices a rail pattern is checked for
+// "" when --rail-switch-pattern compiles for every rail index 0..kMaxRails-1.
+std::string rail_pattern_error(const std::string& pattern);
+
 // Source of LLDP frames (AF_PACKET in production, scripted in tests).
 class LldpSource {
    public:
@@ -338,6 +346,8 @@ class Agent {
     std::vector<std::string> nm_unmanaged_;
     int node_lock_fd_ = -1;
     std::vector<int> nic_lock_fds_;
+    std::string config_error_;  // a setting the agent cannot work with: it configures nothing
+    void idle(int stop_fd);
     void acquire_node_lock(int stop_fd);
     void acquire_nic_locks(int stop_fd);
     // Binds the abstract socket `name` (waiting up to `deadline` while another process holds it);

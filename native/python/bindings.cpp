@@ -5,6 +5,7 @@
 #include <pybind11/stl.h>
 #include <sys/socket.h>
 
+#include "netop/agent.hpp"
 #include "netop/artifacts.hpp"
 #include "netop/dbus.hpp"
 #include "netop/l3.hpp"
@@ -114,6 +115,10 @@ PYBIND11_MODULE(_netop_native, m) {
     });
 
     // ---- L3 ---------------------------------------------------------------
+    // The agent's regular-expression dialect (ECMAScript std::regex), for the webhook's tests.
+    m.def("ecmascript_regex_error", &agent::ecmascript_regex_error);
+    m.def("ecmascript_full_match", &agent::ecmascript_full_match);
+    m.def("rail_pattern_error", &agent::rail_pattern_error);
     m.def("parse_port_description", [](const std::string& desc, const std::string& policy) -> py::object {
         auto p = l3::parse_token_policy(policy);
         if (!p) throw py::value_error("bad token policy");

@@ -781,13 +781,14 @@ bool Agent::configure_interface(NicState& n) {
     if (!cfg_.rail_switch_pattern.empty() && n.gpu_index >= 0) {
         std::string want = cfg_.rail_switch_pattern;
         for (size_t at; (at = want.find("{rail}")) != std::string::npos;) want.replace(at, 6, std::to_string(n.gpu_index));
-        bool ok = false;
-        try {
-            ok = std::regex_match(n.peer_system_name, std::regex(want, std::regex::ECMAScript));
-        } catch (const std::regex_error& e) {
-            throw AgentError("Invalid --rail-switch-pattern '" + cfg_.rail_switch_pattern + "': " + e.what());
+        const auto ok = ecmascript_full_match(want, n.peer_system_name);
+        if (!ok) {  // (run() checked the pattern for every rail index; kept as a guard)
+            n.config_error = "invalid --rail-switch-pattern '" + cfg_.rail_switch_pattern + "' for rail " +
+                             std::to_string(n.gpu_index) + ": " + ecmascript_regex_error(want);
+            NLOG_W("Interface '%s' not configured: %s", n.ifname.c_str(), n.config_error.c_str());
+            return false;
         }
-        if (!ok) {
+        if (!*ok) {
             n.config_error = strfmt("rail %d is cabled to switch '%s' port '%s', not to one matching '%s' (a NIC on "
                                     "another rail's leaf crosses the spine: check the cabling)",
                                     n.gpu_index, n.peer_system_name.c_str(), n.peer_port_id.c_str(), want.c_str());
@@ -1687,6 +1688,7 @@ void Agent::write_status() {
 std::string reason_path(const std::string& status_file) { return status_file + ".not-ready"; }
 
 std::string Agent::not_ready_reason() const {
+    if (!config_error_.empty()) return config_error_;
     std::vector<std::string> parts;
     for (const auto& n : nics_) {
         std::string why;
@@ -1720,13 +1722,19 @@ void Agent::run(int stop_fd) {
     } catch (const std::exception& e) {
         throw AgentError(std::string("Invalid --rccl-env-extra: ") + e.what());
     }
-    if (!cfg_.rail_switch_pattern.empty()) {
-        try {
-            std::string probe = cfg_.rail_switch_pattern;
-            for (size_t at; (at = probe.find("{rail}")) != std::string::npos;) probe.replace(at, 6, "0");
-            std::regex(probe, std::regex::ECMAScript);
-        } catch (const std::regex_error& e) {
-            throw AgentError("Invalid --rail-switch-pattern '" + cfg_.rail_switch_pattern + "': " + e.what());
+    if (!cfg_.rail_switch_pattern.empty() && !cfg_.cleanup) {
+        if (std::string why = rail_pattern_error(cfg_.rail_switch_pattern); !why.empty()) {
+            // Admission checks the same grammar (webhook.validate_rail_switch_pattern); a policy
+            // that bypassed it (webhooks off) gets one clear reason and an agent that touches
+            // nothing and waits, not a crash loop on every selected node.
+            config_error_ = "invalid railSwitchPattern '" + cfg_.rail_switch_pattern + "': " + why +
+                            " (an ECMAScript regular expression, {rail} = the GPU index); nothing configured";
+            NLOG_E("%s", config_error_.c_str());
+            if (cfg_.dry_run || !cfg_.keep_running) throw AgentError(config_error_);
+            if (!artifacts::remove_labels(cfg_.labels)) NLOG_W("Failed to remove NFD label file: %s", std::strerror(errno));
+            write_status();
+            idle(stop_fd);
+            return;
         }
     }
     if (!cfg_.metrics_addr.empty() && !httpd_) {
@@ -1965,17 +1973,50 @@ void Agent::run(int stop_fd) {
     if (cfg_.monitor) {
         monitor(stop_fd);
     } else {
-        // Idle until SIGTERM / SIGINT (reference behaviour).
-        while (!fd_readable(stop_fd)) {
-            if (stop_fd < 0) {
-                ::pause();
-                continue;
-            }
-            pollfd p{stop_fd, POLLIN, 0};
-            ::poll(&p, 1, -1);
-        }
+        idle(stop_fd);  // reference behaviour
     }
     post_cleanups();
+}
+
+void Agent::idle(int stop_fd) {
+    // Until SIGTERM / SIGINT.
+    while (!fd_readable(stop_fd)) {
+        if (stop_fd < 0) {
+            ::pause();
+            continue;
+        }
+        pollfd p{stop_fd, POLLIN, 0};
+        ::poll(&p, 1, -1);
+    }
+}
+
+std::string ecmascript_regex_error(const std::string& pattern) {
+    try {
+        std::regex(pattern, std::regex::ECMAScript);
+    } catch (const std::regex_error& e) {
+        return e.what();
+    }
+    return "";
+}
+
+std::optional<bool> ecmascript_full_match(const std::string& pattern, const std::string& text) {
+    try {
+        return std::regex_match(text, std::regex(pattern, std::regex::ECMAScript));
+    } catch (const std::regex_error&) {
+        return std::nullopt;
+    }
+}
+
+std::string rail_pattern_error(const std::string& pattern) {
+    // Every rail index a node can have: "{rail}" changes the pattern ("a{{rail},3}" is fine for
+    // rail 0 and a reversed range for rail 5).
+    for (int k = 0; k < kMaxRails; ++k) {
+        std::string p = pattern;
+        for (size_t at; (at = p.find("{rail}")) != std::string::npos;) p.replace(at, 6, std::to_string(k));
+        if (std::string e = ecmascript_regex_error(p); !e.empty())
+            return k == 0 ? e : e + strfmt(" (with {rail} = %d)", k);
+    }
+    return "";
 }
 
 bool Agent::publish_label() { return artifacts::write_labels(cfg_.labels, labels_extra_); }

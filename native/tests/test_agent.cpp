@@ -2360,3 +2360,36 @@ TEST(agent_max_frame_boundaries_match_what_the_agent_advertises) {
                   std::string::npos);
     }
 }
+
+TEST(agent_invalid_rail_pattern_waits_with_one_reason_instead_of_crash_looping) {
+    // A policy that reached the agent without admission (webhooks off) with a Python-only regex:
+    // the agent touches nothing, says why in one line (status.json, the probe's reason file) and
+    // waits for SIGTERM instead of exiting into a restart loop on every node.
+    Fixture f;
+    f.cfg.rail_switch_pattern = "(?i)leaf-r{rail}";
+    f.tmp.write("features.d/scale-out-readiness.txt", "stale\n");
+    Pipe stop;
+    stop.fire();
+    agent::Agent a(f.cfg, f.ops, f.all_valid(), f.nm());
+    a.run(stop.fd[0]);  // returns on the stop, no exception
+    CHECK(!a.ready());
+    CHECK(f.ops.addrs.empty());
+    CHECK_EQ(f.ops.calls["link_set_up"], 0);
+    CHECK(!path_exists(f.cfg.labels.path()));
+    auto why = read_file(agent::reason_path(f.cfg.status_file));
+    CHECK(why && why->find("invalid railSwitchPattern '(?i)leaf-r{rail}': ") == 0);
+    CHECK(why->find("nothing configured") != std::string::npos);
+    // One-shot runs (no --keep-running) and dry runs still fail fast.
+    Fixture g;
+    g.cfg.keep_running = false;
+    g.cfg.rail_switch_pattern = "a{{rail},3}";  // fine for rails 0..3, a reversed range for rail 4
+    agent::Agent b(g.cfg, g.ops, g.all_valid(), g.nm());
+    std::string err;
+    try {
+        b.run(-1);
+    } catch (const agent::AgentError& e) {
+        err = e.what();
+    }
+    CHECK(err.find("(with {rail} = 4)") != std::string::npos);
+    CHECK_EQ(agent::rail_pattern_error("leaf-r{rail}-.*"), std::string());
+}

@@ -114,20 +114,162 @@ class InvalidRailSwitchPatternError(ValidationError):
         self.message = f"invalid railSwitchPattern {value!r}: {why}"
 
 
+# Escapes both engines read the same way: ECMAScript's character-class and control escapes
+# (std::regex, the agent) and Python's re (admission).  Any other letter or digit escape is either
+# unknown to one of them (\A \Z \z \G \Q \E \h \R \K \p \P \N \k ...) or means something
+# else (\0 followed by digits is an octal escape in Python).
+_ESCAPE_LETTERS = set("dDwWsSbfnrtv")  # not \B: on an empty name Python says no, ECMAScript yes
+_SYNTAX = set("^$\\.*+?()[]{}|/-")
+MAX_RAILS = 16  # the agent's kMaxRails: {rail} is checked for every index 0..15
+
+
+def ecmascript_subset_error(pattern: str) -> Optional[str]:
+    """None when `pattern` stays inside the regular-expression subset that ECMAScript std::regex
+    (the agent) and Python's re (this webhook) both accept and read alike; else why not.
+
+    Refused: ``(?`` groups other than ``(?:``, ``(?=``, ``(?!`` -- inline flags ``(?i)``,
+    lookbehind ``(?<=``, named groups ``(?P<n>``/``(?<n>``, atomic ``(?>``, comments ``(?#``;
+    the escapes above; possessive quantifiers (``*+``, ``++``, ``?+``, ``}+``); ``{,n}``;
+    quantified assertions; POSIX bracket expressions (``[[:alpha:]]``, an ordinary set in
+    Python) and Python's reserved set syntax in classes; multi-digit back-references.  Found by
+    sweeping random patterns through both engines (tests/test_operator.py)."""
+    i, n = 0, len(pattern)
+    in_class = False
+    prev_quant = False  # the previous token was a quantifier (for possessive detection)
+    prev_assert = False  # ... an assertion (^ $ \b \B (?= (?!): ECMAScript refuses to quantify it
+    groups: List[bool] = []  # open groups: True for lookaheads
+    while i < n:
+        c = pattern[i]
+        if not in_class and c in "*+?{" and prev_assert:
+            return "quantified assertion (^, $, \\b, \\B or a lookahead)"
+        prev_assert = False
+        if c == "\\":
+            if i + 1 >= n:
+                return "trailing backslash"
+            e = pattern[i + 1]
+            if e.isdigit():
+                if e == "0":
+                    if i + 2 < n and pattern[i + 2].isdigit():
+                        return f"octal escape \\0{pattern[i + 2]} (Python reads it as octal, ECMAScript as NUL then a digit)"
+                elif not in_class and i + 2 < n and pattern[i + 2].isdigit():
+                    return "multi-digit back-reference"
+                elif in_class:
+                    return f"back-reference \\{e} inside a character class"
+                i += 2
+            elif e == "x":
+                if not re.fullmatch(r"[0-9A-Fa-f]{2}", pattern[i + 2:i + 4]):
+                    return "\\x needs two hex digits"
+                i += 4
+            elif e == "u":
+                if not re.fullmatch(r"[0-9A-Fa-f]{4}", pattern[i + 2:i + 6]):
+                    return "\\u needs four hex digits"
+                i += 6
+            elif e == "c":
+                return "control escape \\c (not in Python's re)"
+            elif e.isalpha():
+                if e not in _ESCAPE_LETTERS:
+                    return f"escape \\{e} (not the same in ECMAScript and Python)"
+                prev_assert = e == "b" and not in_class
+                if prev_assert and any(groups):
+                    return "\\b inside a lookahead (the engines disagree at the end of the name)"
+                i += 2
+            elif e in _SYNTAX or not e.isalnum():
+                i += 2
+            else:
+                return f"escape \\{e}"
+            prev_quant = False
+            continue
+        if in_class:
+            if c == "[" and i + 1 < n and pattern[i + 1] in ":=.":
+                return "POSIX bracket expression (e.g. [[:alpha:]]) inside a character class"
+            if c == "[":  # a literal in both today; Python reserves it for nested sets (FutureWarning)
+                return "unescaped '[' inside a character class (write \\[)"
+            if pattern.startswith(("--", "&&", "~~", "||"), i):
+                return f"{pattern[i:i + 2]!r} inside a character class (reserved for set operations in Python)"
+            if c == "]":
+                in_class = False
+            i += 1
+            continue
+        if c == "[":
+            in_class = True
+            i += 1
+            if i < n and pattern[i] == "^":
+                i += 1
+            if i < n and pattern[i] == "]":  # a literal ']' first: Python only ('[]' is empty in ECMAScript)
+                return "']' first in a character class (a literal in Python, an empty class in ECMAScript)"
+            prev_quant = False
+            continue
+        if c == "(":
+            if pattern.startswith("(?", i):
+                if not pattern.startswith(("(?:", "(?=", "(?!"), i):
+                    return f"group construct {pattern[i:i + 4]!r} (only (?: (?= (?! are read alike)"
+                groups.append(pattern[i + 2] != ":")
+                i += 3
+            else:
+                groups.append(False)
+                i += 1
+            prev_quant = False
+            continue
+        if c == ")":
+            prev_assert = bool(groups) and groups.pop()
+            prev_quant = False
+            i += 1
+            continue
+        if c in "^$":
+            if any(groups):
+                return f"{c!r} inside a lookahead"
+            prev_assert = True
+            prev_quant = False
+            i += 1
+            continue
+        if c in "*+?":
+            if prev_quant and c == "+":
+                return "possessive quantifier (not in ECMAScript or this Python)"
+            if prev_quant and c == "?":
+                prev_quant = False  # lazy: fine in both
+                i += 1
+                continue
+            prev_quant = True
+            i += 1
+            continue
+        if c == "{":
+            m = re.match(r"\{(\d*)(,?)(\d*)\}", pattern[i:])
+            if m:
+                if m.group(1) == "":
+                    return "quantifier {,n} (ECMAScript needs a lower bound)"
+                prev_quant = True
+                i += m.end()
+                continue
+            return "'{' not starting a quantifier (escape it as \\{)"
+        if c == "}":
+            return "unbalanced '}' (escape it as \\})"
+        prev_quant = False
+        i += 1
+    if in_class:
+        return "unterminated character class"
+    return None
+
+
 def validate_rail_switch_pattern(value: str) -> None:
     """A regular expression over the switch's LLDP System Name, "{rail}" standing for the GPU
-    index.  The agent matches with ECMAScript std::regex; Python's re accepts the same common
-    subset, so a pattern Python rejects is refused here rather than crash-looping the agents."""
-    import re
-
+    index.  The agent matches with ECMAScript std::regex; admission accepts only what both that
+    and Python's re compile and read alike (ecmascript_subset_error), for every rail index the
+    agent substitutes, so a policy it admits never fails on the nodes (tests/test_operator.py
+    feeds one corpus to both engines)."""
     if not value:
         return
     if len(value) > 253 or any(c in value for c in "\n\r"):
         raise InvalidRailSwitchPatternError(value, "at most 253 characters on one line")
-    try:
-        re.compile(value.replace("{rail}", "0"))
-    except re.error as e:
-        raise InvalidRailSwitchPatternError(value, str(e)) from None
+    for k in range(MAX_RAILS):
+        p = value.replace("{rail}", str(k))
+        why = ecmascript_subset_error(p)
+        if why is None:
+            try:
+                re.compile(p)
+            except re.error as e:
+                why = str(e)
+        if why is not None:
+            raise InvalidRailSwitchPatternError(value, why + ("" if k == 0 else f" (with {{rail}} = {k})")) from None
 
 
 class InvalidMaxUnavailableError(ValidationError):

