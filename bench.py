@@ -64,10 +64,13 @@ FAKE_DUMP_DEFAULTS_ENV = "NETOP_BENCH_FAKE_RCCL_DUMP_DEFAULTS"
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 
+CONFIG_1 = "L3 mode, 1xMI355X: mock-switch LLDP /30 Port-Description -> one NIC up + NFD scale-out label"
+
+
 def config_name(n: int) -> str:
     """The BASELINE.json config this run measures, from the world size actually running."""
     if n == 1:  # BASELINE.json configs[1]
-        return "L3 mode, 1xMI355X: mock-switch LLDP /30 Port-Description -> one NIC up + NFD scale-out label"
+        return CONFIG_1
     if n == 8:  # BASELINE.json configs[2]
         return ("L3 mode, 8xMI355X single node: all xGMI + host RoCE links configured, "
                 "rccl-tests 8-GPU all-reduce")
@@ -326,6 +329,29 @@ class _Once:
             return True
 
 
+def run_config(args, world: int, st: dict) -> tuple:
+    """(config.model, what ran, what did not) for the line.  At n = 1 the BASELINE.json configs[1]
+    name is claimed only when its node-ready half (LLDP on the mock switch, NIC up, the NFD
+    label) was measured in this run; otherwise the line names what did run.
+    At n > 1 the name follows the world size as before."""
+    a = st.get("artifacts") or {}
+    ran = ["rccl_all_reduce"] + (["agent_artifacts"] if a.get("applied") else [])
+    skipped = []
+    if st.get("node_ready"):
+        ran += ["lldp", "nic_up", "label"]
+    else:
+        skipped += ["lldp", "nic_up", "label"]
+    if st.get("gpu_side") and "error" not in st["gpu_side"]:
+        ran.append("agent_gpu_side_phases")
+    if world != 1 or st.get("node_ready"):
+        return config_name(world), ran, skipped
+    why = st.get("node_ready_note") or ("--node-ready off" if args.node_ready == "off" else "not reached")
+    backend = "RCCL" if args.device == "cuda" else "gloo (CPU rehearsal)"
+    model = (f"{backend} all-reduce with the agent's artifacts, 1xMI355X (node-ready not run: {why})"
+             if a.get("applied") else f"{backend} all-reduce, 1xMI355X (node-ready not run: {why})")
+    return model, ran, skipped
+
+
 def _line(args, world: int, st: dict) -> dict:
     """The JSON line from whatever has been measured so far (``st``)."""
     h = st.get("headline")
@@ -334,6 +360,7 @@ def _line(args, world: int, st: dict) -> dict:
 
     ceiling = C.xgmi_busbw_ceiling_GBps(world)
     busbw = h["busbw"] if h else None
+    model, ran, skipped = run_config(args, world, st)
     line = {
         "metric": METRIC,
         "value": round(busbw, 3) if h else None,
@@ -347,7 +374,7 @@ def _line(args, world: int, st: dict) -> dict:
         "vs_baseline": None,
         "dtype": "bf16" if cuda else "fp32",
         "data": "synthetic (zeros for the timed loop; exact pattern check before timing)",
-        "config": {"model": config_name(world), "global_batch": None, "seq_len": None,
+        "config": {"model": model, "ran": ran, "skipped": skipped, "global_batch": None, "seq_len": None,
                    "parallelism": f"dp{world}", "gpus": world, "message_bytes_per_rank": h["nbytes"] if h else None,
                    "op": "all_reduce(sum)",
                    "backend": "torch.distributed nccl (RCCL)" if cuda else "torch.distributed gloo (CPU rehearsal)",

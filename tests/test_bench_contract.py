@@ -78,7 +78,13 @@ def test_bench_single_rank_reports_no_fake_bandwidth(tmp_path):
            "--bytes", str(1 << 18), "--sweep", "4096", "--node-ready", "off"]
     j = _bench_line(subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=tmp_path))
     assert j["n_gpus"] == 1 and j["value"] == 0.0
-    assert j["config"]["model"].startswith("L3 mode, 1xMI355X")
+    # No netns harness ran (--node-ready off): the line must not claim BASELINE configs[1]
+    # (LLDP + NIC up + label), only what did run.
+    import bench
+
+    assert j["config"]["model"] != bench.CONFIG_1 and "node-ready not run: --node-ready off" in j["config"]["model"]
+    assert j["config"]["model"].startswith("gloo (CPU rehearsal) all-reduce")
+    assert j["config"]["skipped"] == ["lldp", "nic_up", "label"] and "rccl_all_reduce" in j["config"]["ran"]
     assert j["algbw_GBps"] is None and "no-op" in j["algbw_note"]
     assert all(row["algbw_GBps"] is None for row in j["sweep"])
     side = j["node_ready_gpu_side"]
@@ -476,3 +482,26 @@ def test_link_deficit_seen_without_the_file_too_is_not_blamed_on_it():
     assert v["status"] == "degraded" and "with and without the agent's file" in v["why"]
     assert FA.dump_verdict(8, view, dict(view, min_xgmi_links=7))["status"] == "failed"  # the file costs a link
     assert FA.dump_verdict(8, dict(view, min_xgmi_links=7), dict(view, min_xgmi_links=7))["status"] == "ok"
+
+
+def test_bench_claims_configs_1_only_when_its_node_ready_half_ran():
+    """n = 1: the BASELINE.json configs[1] name (mock-switch LLDP -> NIC up -> NFD label) only with
+    a node-ready result in the line; a box without the netns harness gets a name for what ran and
+    the reason.  n > 1 keeps its per-world-size name."""
+    from types import SimpleNamespace
+
+    import bench
+
+    args = SimpleNamespace(node_ready="auto", device="cuda")
+    ok = {"node_ready": {"fast_start_switch": {"p50_s": 0.009}}, "artifacts": {"applied": True}}
+    model, ran, skipped = bench.run_config(args, 1, ok)
+    assert model == bench.CONFIG_1 and skipped == [] and {"lldp", "nic_up", "label", "agent_artifacts"} <= set(ran)
+    box = {"node_ready": None, "node_ready_note": "node-ready harness unavailable: unshare failed",
+           "artifacts": {"applied": True}, "gpu_side": {"total_ms": 4.6}}
+    model, ran, skipped = bench.run_config(args, 1, box)
+    assert model == ("RCCL all-reduce with the agent's artifacts, 1xMI355X (node-ready not run: node-ready harness "
+                     "unavailable: unshare failed)")
+    assert skipped == ["lldp", "nic_up", "label"] and ran == ["rccl_all_reduce", "agent_artifacts",
+                                                              "agent_gpu_side_phases"]
+    for n in (2, 4, 8):
+        assert bench.run_config(args, n, box)[0] == bench.config_name(n)
