@@ -391,26 +391,23 @@ _LAUNCHER_ENV = ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_
                  "MASTER_ADDR", "MASTER_PORT", "GROUP_WORLD_SIZE", "ROLE_NAME")
 
 
-def run(world: int, nbytes: int = 1 << 30, min_bytes: Optional[int] = None, iters: int = 10, warmup: int = 3,
-        algos: str = ",".join(ALGOS), devices: Optional[str] = None, timeout: float = 120.0) -> dict:
-    """Spawns `world` rank processes (one per GPU unless `devices` maps several onto one) and
-    returns rank 0's result.  Safe to call from inside another distributed job: the children
-    get their own rendezvous and none of the parent's launcher variables."""
+def spawn_ranks(world: int, cmd: list, timeout: float, extra_env: Optional[dict] = None) -> tuple:
+    """Starts `world` copies of `cmd` as ranks 0..world-1 with their own FileStore rendezvous and
+    none of a parent launcher's variables; waits for all of them.  Returns (processes, outputs);
+    raises TimeoutError (every rank killed) when they are not done within `timeout`.
+
+    Output goes to temporary files, not pipes.  With pipes read one rank at a time, a rank that
+    writes more than the pipe holds (64 KiB: a page of warnings) blocks in write() while the
+    parent waits on another rank, and that rank waits for it at the next barrier: the round-3 GPU
+    test hang, reproduced on the CPU by tests/test_xgmi_comm.py."""
     base = {k: v for k, v in os.environ.items() if k not in _LAUNCHER_ENV and not k.startswith("TORCHELASTIC_")}
     # Rendezvous over a FileStore: a free TCP port picked here could be taken by another process
     # before rank 0 binds it, and the other ranks would then wait for a store that never comes.
     store_dir = tempfile.mkdtemp(prefix="netop-xgmi-store-")
     base.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), WORLD_SIZE=str(world),
-                NETOP_INIT_FILE=os.path.join(store_dir, "store"))
-    cmd = [sys.executable, "-m", "network_operator_amd.parallel.xgmi_comm", "--worker", "--bytes", str(nbytes),
-           "--min-bytes", str(min_bytes or nbytes), "--iters", str(iters), "--warmup", str(warmup), "--algos", algos,
-           "--timeout", str(min(timeout, 60.0))]
-    if devices:
-        cmd += ["--devices", devices]
+                NETOP_INIT_FILE=os.path.join(store_dir, "store"), **(extra_env or {}))
     root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     base["PYTHONPATH"] = root + (os.pathsep + base["PYTHONPATH"] if base.get("PYTHONPATH") else "")
-    # Output goes to temporary files, not pipes: a rank blocked on a full pipe would stall the
-    # barrier of every other rank.
     logs = [tempfile.TemporaryFile(mode="w+") for _ in range(world)]
     procs = [subprocess.Popen(cmd, env=dict(base, RANK=str(r), LOCAL_RANK=str(r)), stdout=logs[r],
                               stderr=subprocess.STDOUT, text=True, cwd=root) for r in range(world)]
@@ -424,13 +421,27 @@ def run(world: int, nbytes: int = 1 << 30, min_bytes: Optional[int] = None, iter
         for p in procs:
             p.wait()
         shutil.rmtree(store_dir, ignore_errors=True)
-        raise TimeoutError(f"xGMI all-reduce benchmark did not finish within {timeout} s")
+        raise TimeoutError(f"ranks did not finish within {timeout} s")
     outs = []
     for f in logs:
         f.seek(0)
         outs.append(f.read())
         f.close()
     shutil.rmtree(store_dir, ignore_errors=True)
+    return procs, outs
+
+
+def run(world: int, nbytes: int = 1 << 30, min_bytes: Optional[int] = None, iters: int = 10, warmup: int = 3,
+        algos: str = ",".join(ALGOS), devices: Optional[str] = None, timeout: float = 120.0) -> dict:
+    """Spawns `world` rank processes (one per GPU unless `devices` maps several onto one) and
+    returns rank 0's result.  Safe to call from inside another distributed job: the children
+    get their own rendezvous and none of the parent's launcher variables."""
+    cmd = [sys.executable, "-m", "network_operator_amd.parallel.xgmi_comm", "--worker", "--bytes", str(nbytes),
+           "--min-bytes", str(min_bytes or nbytes), "--iters", str(iters), "--warmup", str(warmup), "--algos", algos,
+           "--timeout", str(min(timeout, 60.0))]
+    if devices:
+        cmd += ["--devices", devices]
+    procs, outs = spawn_ranks(world, cmd, timeout)
     bad = [(r, p.returncode, o[-1500:]) for r, (p, o) in enumerate(zip(procs, outs)) if p.returncode != 0]
     if bad:
         raise RuntimeError(f"rank {bad[0][0]} exited {bad[0][1]}: {bad[0][2]}")

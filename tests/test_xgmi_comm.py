@@ -230,3 +230,57 @@ def test_device_bdf_names_the_gpu(cuda_device):
     bdf = device_bdf(0)
     assert re.fullmatch(r"[0-9a-f]{4}:[0-9a-f]{2}:[0-9a-f]{2}\.0", bdf), bdf
     assert os.path.exists(f"/sys/bus/pci/devices/{bdf}")
+
+
+def _old_harness(world, args, limit_s):
+    """The harness shape of round 3 before its fix: ranks' stdout and stderr through pipes, read
+    one rank at a time (communicate() on rank 0, then rank 1, ...).  Returns (hung ranks, bytes
+    each rank managed to write to stderr)."""
+    import time
+
+    store = Path(os.environ.get("TMPDIR", "/tmp")) / f"netop-old-harness-{os.getpid()}"
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_port()), WORLD_SIZE=str(world),
+               PYTHONPATH=str(ROOT), NETOP_INIT_FILE=str(store))
+    procs = [subprocess.Popen([sys.executable, str(WORKER), *args], env=dict(env, RANK=str(r)),
+                              stdout=subprocess.PIPE, stderr=subprocess.PIPE) for r in range(world)]
+    deadline = time.monotonic() + limit_s
+    hung = []
+    try:
+        for r, p in enumerate(procs):
+            try:
+                p.communicate(timeout=max(deadline - time.monotonic(), 0.1))
+            except subprocess.TimeoutExpired:
+                hung.append(r)
+                break  # the harness never gets past this rank
+    finally:
+        written = []
+        for p in procs:
+            p.kill()
+        for p in procs:
+            _, err = p.communicate()
+            written.append(len(err))
+        store.unlink(missing_ok=True)
+    return hung, written
+
+
+def test_round3_hang_reproduced_pipes_read_rank_by_rank_deadlock():
+    """VERDICT r3 weak #7, pinned on the CPU: ranks 1 and 2 write 256 KiB to stderr before a
+    gloo barrier.  Read through pipes rank by rank, rank 0 waits at the barrier for rank 1,
+    rank 1 is blocked in write() on its full pipe (exactly the pipe's 64 KiB got through), and
+    the harness waits on rank 0: nothing moves until the limit kills it."""
+    hung, written = _old_harness(3, ["chatty", str(256 << 10)], limit_s=8)
+    assert hung == [0], (hung, written)
+    assert written[1] == written[2] == 65536, written  # the pipe's capacity, then blocked
+
+
+def test_round3_hang_does_not_happen_with_the_file_based_harnesses():
+    """The same scenario through the harnesses in use now: the test's `_ranks` and
+    `xgmi_comm.spawn_ranks` (behind xgmi_comm.run and the bench extras) write rank output to
+    files, so every rank finishes."""
+    from network_operator_amd.parallel import xgmi_comm
+
+    assert _ranks(3, ["chatty", str(256 << 10)], limit_s=60) == ["ok"] * 3
+    procs, outs = xgmi_comm.spawn_ranks(3, [sys.executable, str(WORKER), "chatty", str(256 << 10)], timeout=60)
+    assert [p.returncode for p in procs] == [0, 0, 0]
+    assert all("RESULT ok" in o for o in outs)
+    assert all(o.count("w") >= 256 << 10 for o in outs[1:])  # nothing lost on the way

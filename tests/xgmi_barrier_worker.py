@@ -57,6 +57,20 @@ def main() -> None:
     dist.destroy_process_group()
 
 
+def chatty() -> None:
+    """The round-3 hang's shape: every rank but 0 writes `NBYTES` (argv[2]) to stderr -- a page of
+    warnings -- before a gloo barrier.  Read through pipes one rank at a time, that write blocks
+    once the pipe is full and the barrier never completes."""
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    _init(rank, world)
+    if rank:
+        sys.stderr.write("w" * int(sys.argv[2]))
+        sys.stderr.flush()
+    dist.barrier()
+    print("RESULT ok", flush=True)
+    dist.destroy_process_group()
+
+
 def nested() -> None:
     """Inside a torchrun-launched rank (as bench.py rank 0 does): spawn a 2-rank virtual
     all-reduce on GPU 0 with its own rendezvous, untouched by this job's launcher variables."""
@@ -219,4 +233,4 @@ def rail() -> None:
 
 
 if __name__ == "__main__":
-    {"nested": nested, "ddp": ddp, "collectives": collectives, "rail_groups": rail_groups, "rail": rail}.get(sys.argv[1] if len(sys.argv) > 1 else "", main)()
+    {"chatty": chatty, "nested": nested, "ddp": ddp, "collectives": collectives, "rail_groups": rail_groups, "rail": rail}.get(sys.argv[1] if len(sys.argv) > 1 else "", main)()
