@@ -1,0 +1,358 @@
+// Tuning sweep for the validation pattern kernels (gfx950): fill and verify of a 1 GiB bf16
+// buffer, 1 and 8 ranks in the pattern, for
+//   * v1: the round-3 pattern (a full hash per rank per 16-byte vector, 3-bit fields extracted
+//     and summed one element at a time: ALU-bound at 8 ranks, 2.0-2.5 TB/s);
+//   * v2: the pattern netop_hip.hip uses now (one rank-independent hash per vector, one multiply
+//     per rank, the 8 fields of all ranks summed as 6-bit slots of two words: SWAR),
+// crossed with vectors in flight per lane (UNROLL 1 / 2), nontemporal stores / loads, and
+// workgroups per CU (4 / 8 / 16).  Every v2 variant is checked (fill -> verify = 0 errors; one
+// flipped element -> 1 error) before it is timed.  Prints one JSON line per variant.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+
+#define CHECK(x)                                                                           \
+    do {                                                                                   \
+        hipError_t e_ = (x);                                                               \
+        if (e_ != hipSuccess) {                                                            \
+            std::fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+            return 1;                                                                      \
+        }                                                                                  \
+    } while (0)
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+namespace {
+constexpr int kThreads = 256;
+
+// ---- v1 (round 3) ----
+__device__ __forceinline__ uint32_t mix1(uint64_t i, uint32_t seed) {
+    uint32_t x = uint32_t(i) * 0x9E3779B1u ^ uint32_t(i >> 32) * 0x85EBCA77u ^ seed * 0xC2B2AE3Du;
+    x ^= x >> 15;
+    x *= 0x2C1B3C6Du;
+    x ^= x >> 12;
+    return x;
+}
+__device__ __forceinline__ void sum_v1(uint64_t g, uint32_t seed, int n, int s[8]) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s[k] = 0;
+    for (int r = 0; r < n; ++r) {
+        const uint32_t x = mix1(g, seed + 0x632BE5ABu * uint32_t(r + 1));
+#pragma unroll
+        for (int k = 0; k < 8; ++k) s[k] += int((x >> (3 * k)) & 7u) - 4;
+    }
+}
+
+// ---- v2 ----
+__device__ __forceinline__ uint32_t group_hash(uint64_t g) {
+    uint32_t x = uint32_t(g) * 0x9E3779B1u ^ uint32_t(g >> 32) * 0x85EBCA77u;
+    x ^= x >> 15;
+    x *= 0x2C1B3C6Du;
+    x ^= x >> 12;
+    return x;
+}
+__device__ __forceinline__ uint32_t rank_mult(uint32_t seed, int r) {
+    uint32_t k = (seed + 0x632BE5ABu * uint32_t(r + 1)) * 0xC2B2AE3Du;
+    return (k ^ (k >> 16)) | 1u;
+}
+constexpr uint32_t kSlots = (7u << 8) | (7u << 14) | (7u << 20) | (7u << 26);
+__device__ __forceinline__ void sum_v2(uint64_t g, uint32_t seed, int n, int s[8]) {
+    const uint32_t h = group_hash(g);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s[k] = -4 * n;
+    for (int r0 = 0; r0 < n; r0 += 9) {  // 9 x 7 = 63: a 6-bit slot holds 9 ranks' fields
+        uint32_t e = 0, o = 0;
+        const int r1 = r0 + 9 < n ? r0 + 9 : n;
+        for (int r = r0; r < r1; ++r) {
+            const uint32_t x = h * rank_mult(seed, r);
+            e += x & kSlots;
+            o += (x >> 3) & kSlots;
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            s[2 * k] += int((e >> (8 + 6 * k)) & 63u);
+            s[2 * k + 1] += int((o >> (8 + 6 * k)) & 63u);
+        }
+    }
+}
+
+// ---- v3: v2 with a full-rate 24-bit multiply per rank (v_mul_u32_u24; the 32-bit multiply is
+// quarter rate) ----
+__device__ __forceinline__ void sum_v3(uint64_t g, uint32_t seed, int n, int s[8]) {
+    uint32_t h = group_hash(g);
+    h = (h ^ (h >> 24)) & 0xffffffu;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s[k] = -4 * n;
+    for (int r0 = 0; r0 < n; r0 += 9) {
+        uint32_t e = 0, o = 0;
+        const int r1 = r0 + 9 < n ? r0 + 9 : n;
+        for (int r = r0; r < r1; ++r) {
+            const uint32_t x = __umul24(h, rank_mult(seed, r) & 0xffffffu);
+            e += x & kSlots;
+            o += (x >> 3) & kSlots;
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            s[2 * k] += int((e >> (8 + 6 * k)) & 63u);
+            s[2 * k + 1] += int((o >> (8 + 6 * k)) & 63u);
+        }
+    }
+}
+
+__device__ __forceinline__ uint32_t bf16x2_of_ints(int lo, int hi) {
+    return (__float_as_uint(float(lo)) >> 16) | (__float_as_uint(float(hi)) & 0xffff0000u);
+}
+
+template <int V, int UNROLL, bool NT>
+__global__ __launch_bounds__(kThreads) void fill_k(u32x4* __restrict__ out, uint64_t n_vec, uint32_t seed, int n) {
+    const uint64_t stride = uint64_t(gridDim.x) * kThreads;
+    for (uint64_t v0 = uint64_t(blockIdx.x) * kThreads + threadIdx.x; v0 < n_vec; v0 += stride * UNROLL) {
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u) {
+            const uint64_t v = v0 + u * stride;
+            if (UNROLL > 1 && v >= n_vec) break;
+            int s[8];
+            if (V == 1)
+                sum_v1(v, seed, n, s);
+            else if (V == 2)
+                sum_v2(v, seed, n, s);
+            else
+                sum_v3(v, seed, n, s);
+            const u32x4 w = {bf16x2_of_ints(s[0], s[1]), bf16x2_of_ints(s[2], s[3]), bf16x2_of_ints(s[4], s[5]),
+                             bf16x2_of_ints(s[6], s[7])};
+            if (NT)
+                __builtin_nontemporal_store(w, &out[v]);
+            else
+                out[v] = w;
+        }
+    }
+}
+
+template <int V, int UNROLL, bool NT>
+__global__ __launch_bounds__(kThreads) void verify_k(const u32x4* __restrict__ in, uint64_t n_vec, uint32_t seed, int n,
+                                                     unsigned long long* __restrict__ errors) {
+    __shared__ unsigned int wave_err[kThreads / 64];
+    const uint64_t stride = uint64_t(gridDim.x) * kThreads;
+    unsigned int err = 0;
+    for (uint64_t v0 = uint64_t(blockIdx.x) * kThreads + threadIdx.x; v0 < n_vec; v0 += stride * UNROLL) {
+        u32x4 q[UNROLL];
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u) {
+            const uint64_t v = v0 + u * stride;
+            if (v < n_vec) q[u] = NT ? __builtin_nontemporal_load(&in[v]) : in[v];
+        }
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u) {
+            const uint64_t v = v0 + u * stride;
+            if (UNROLL > 1 && v >= n_vec) break;
+            int s[8];
+            if (V == 1)
+                sum_v1(v, seed, n, s);
+            else if (V == 2)
+                sum_v2(v, seed, n, s);
+            else
+                sum_v3(v, seed, n, s);
+            const uint32_t w[4] = {q[u].x, q[u].y, q[u].z, q[u].w};
+            if (V == 3) {
+                // Compare packed words; count elements only on a mismatch (rare: the slow path).
+                uint32_t d[4], any = 0;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    d[k] = w[k] ^ bf16x2_of_ints(s[2 * k], s[2 * k + 1]);
+                    any |= d[k];
+                }
+                if (any) {
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        err += __uint_as_float(w[k] << 16) != float(s[2 * k]);
+                        err += __uint_as_float(w[k] & 0xffff0000u) != float(s[2 * k + 1]);
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    err += __uint_as_float(w[k] << 16) != float(s[2 * k]);
+                    err += __uint_as_float(w[k] & 0xffff0000u) != float(s[2 * k + 1]);
+                }
+            }
+        }
+    }
+    for (int off = 32; off > 0; off >>= 1) err += __shfl_down(err, off, 64);
+    if ((threadIdx.x & 63) == 0) wave_err[threadIdx.x >> 6] = err;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned int t = 0;
+        for (int i = 0; i < kThreads / 64; ++i) t += wave_err[i];
+        if (t) atomicAdd(errors, (unsigned long long)t);
+    }
+}
+
+// The write ceiling the fill is held against: a constant 16-byte store per lane (grid-stride),
+// and hipMemsetAsync, on the same buffer.
+template <bool NT>
+__global__ __launch_bounds__(kThreads) void store_const_k(u32x4* __restrict__ out, uint64_t n_vec) {
+    const uint64_t stride = uint64_t(gridDim.x) * kThreads;
+    const u32x4 w = {0x3f803f80u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u};
+    for (uint64_t v = uint64_t(blockIdx.x) * kThreads + threadIdx.x; v < n_vec; v += stride) {
+        if (NT)
+            __builtin_nontemporal_store(w, &out[v]);
+        else
+            out[v] = w;
+    }
+}
+
+// Store shapes: each wave writes U consecutive 1-KiB spans per step (lane i: vectors i, i + 64,
+// ... of the span), grid-strided (CHUNK = 0) or over one contiguous chunk per workgroup (CHUNK = 1).
+template <int U, bool NT, bool CHUNK>
+__global__ __launch_bounds__(kThreads) void store_shape_k(u32x4* __restrict__ out, uint64_t n_vec) {
+    const u32x4 w = {0x3f803f80u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u};
+    const uint64_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint64_t span = 64 * U;  // vectors per wave per step
+    uint64_t begin = 0, end = n_vec, step, pos;
+    if (CHUNK) {
+        const uint64_t per_block = (n_vec + gridDim.x - 1) / gridDim.x;
+        begin = blockIdx.x * per_block;
+        end = begin + per_block < n_vec ? begin + per_block : n_vec;
+        pos = begin + wave * span;
+        step = (kThreads / 64) * span;
+    } else {
+        pos = (uint64_t(blockIdx.x) * (kThreads / 64) + wave) * span;
+        step = uint64_t(gridDim.x) * (kThreads / 64) * span;
+    }
+    for (; pos < end; pos += step) {
+#pragma unroll
+        for (int k = 0; k < U; ++k) {
+            const uint64_t v = pos + k * 64 + lane;
+            if (v < end) {
+                if (NT)
+                    __builtin_nontemporal_store(w, &out[v]);
+                else
+                    out[v] = w;
+            }
+        }
+    }
+}
+
+template <int U, bool NT, bool CHUNK>
+int store_shape(u32x4* buf, uint64_t n_vec, int cus, hipEvent_t a, hipEvent_t b) {
+    for (int pc : {1, 2, 4, 8}) {
+        const int blocks = cus * pc, iters = 10;
+        float ms = 0;
+        hipLaunchKernelGGL((store_shape_k<U, NT, CHUNK>), dim3(blocks), dim3(kThreads), 0, 0, buf, n_vec);
+        CHECK(hipEventRecord(a));
+        for (int i = 0; i < iters; ++i)
+            hipLaunchKernelGGL((store_shape_k<U, NT, CHUNK>), dim3(blocks), dim3(kThreads), 0, 0, buf, n_vec);
+        CHECK(hipEventRecord(b));
+        CHECK(hipEventSynchronize(b));
+        CHECK(hipEventElapsedTime(&ms, a, b));
+        std::printf("{\"ceiling\":\"store_shape\",\"span_KiB\":%d,\"nt\":%d,\"chunk\":%d,\"wg_per_cu\":%d,"
+                    "\"write_TBps\":%.3f}\n", U, int(NT), int(CHUNK), pc, double(n_vec) * 16 * iters / (ms * 1e-3) / 1e12);
+    }
+    return 0;
+}
+
+struct Ctx {
+    u32x4* buf;
+    uint64_t n_vec;
+    unsigned long long* err;
+    hipEvent_t a, b;
+    int cus;
+};
+
+template <int V, int U, bool NT>
+int run(Ctx& c, int n, int per_cu, int iters) {
+    const int blocks = c.cus * per_cu;
+    const uint32_t seed = 2024;
+    // correctness first (v2; v1 is the old definition, checked against itself)
+    hipLaunchKernelGGL((fill_k<V, U, NT>), dim3(blocks), dim3(kThreads), 0, 0, c.buf, c.n_vec, seed, n);
+    CHECK(hipMemset(c.err, 0, 8));
+    hipLaunchKernelGGL((verify_k<V, U, NT>), dim3(blocks), dim3(kThreads), 0, 0, c.buf, c.n_vec, seed, n, c.err);
+    unsigned long long e0 = 0, e1 = 0;
+    CHECK(hipMemcpy(&e0, c.err, 8, hipMemcpyDeviceToHost));
+    uint16_t bad = 0x3f00;  // 0.5: never a pattern sum (integers), so exactly one mismatch
+    CHECK(hipMemcpy(reinterpret_cast<uint16_t*>(c.buf) + 12345, &bad, 2, hipMemcpyHostToDevice));
+    CHECK(hipMemset(c.err, 0, 8));
+    hipLaunchKernelGGL((verify_k<V, U, NT>), dim3(blocks), dim3(kThreads), 0, 0, c.buf, c.n_vec, seed, n, c.err);
+    CHECK(hipMemcpy(&e1, c.err, 8, hipMemcpyDeviceToHost));
+    float ms_fill = 0, ms_verify = 0;
+    CHECK(hipEventRecord(c.a));
+    for (int i = 0; i < iters; ++i)
+        hipLaunchKernelGGL((fill_k<V, U, NT>), dim3(blocks), dim3(kThreads), 0, 0, c.buf, c.n_vec, seed, n);
+    CHECK(hipEventRecord(c.b));
+    CHECK(hipEventSynchronize(c.b));
+    CHECK(hipEventElapsedTime(&ms_fill, c.a, c.b));
+    CHECK(hipEventRecord(c.a));
+    for (int i = 0; i < iters; ++i)
+        hipLaunchKernelGGL((verify_k<V, U, NT>), dim3(blocks), dim3(kThreads), 0, 0, c.buf, c.n_vec, seed, n, c.err);
+    CHECK(hipEventRecord(c.b));
+    CHECK(hipEventSynchronize(c.b));
+    CHECK(hipEventElapsedTime(&ms_verify, c.a, c.b));
+    const double bytes = double(c.n_vec) * 16;
+    std::printf("{\"pattern\":\"v%d\",\"unroll\":%d,\"nt\":%d,\"wg_per_cu\":%d,\"ranks\":%d,\"bytes\":%.0f,"
+                "\"fill_TBps\":%.3f,\"verify_TBps\":%.3f,\"errors_clean\":%llu,\"errors_one_flip\":%llu}\n",
+                V, U, int(NT), per_cu, n, bytes, bytes * iters / (ms_fill * 1e-3) / 1e12,
+                bytes * iters / (ms_verify * 1e-3) / 1e12, e0, e1);
+    std::fflush(stdout);
+    return 0;
+}
+}  // namespace
+
+int main(int argc, char** argv) {
+    const uint64_t bytes = argc > 1 ? std::strtoull(argv[1], nullptr, 0) : (1ull << 30);
+    Ctx c{};
+    c.n_vec = bytes / 16;
+    CHECK(hipMalloc(&c.buf, bytes));
+    CHECK(hipMalloc(&c.err, 8));
+    CHECK(hipEventCreate(&c.a));
+    CHECK(hipEventCreate(&c.b));
+    CHECK(hipDeviceGetAttribute(&c.cus, hipDeviceAttributeMultiprocessorCount, 0));
+    const int iters = 10;
+    for (int pc : {2, 4, 8, 16}) {
+        for (int nt : {0, 1}) {
+            const int blocks = c.cus * pc;
+            float ms = 0;
+            CHECK(hipEventRecord(c.a));
+            for (int i = 0; i < iters; ++i) {
+                if (nt)
+                    hipLaunchKernelGGL(store_const_k<true>, dim3(blocks), dim3(kThreads), 0, 0, c.buf, c.n_vec);
+                else
+                    hipLaunchKernelGGL(store_const_k<false>, dim3(blocks), dim3(kThreads), 0, 0, c.buf, c.n_vec);
+            }
+            CHECK(hipEventRecord(c.b));
+            CHECK(hipEventSynchronize(c.b));
+            CHECK(hipEventElapsedTime(&ms, c.a, c.b));
+            std::printf("{\"ceiling\":\"store_const\",\"nt\":%d,\"wg_per_cu\":%d,\"bytes\":%.0f,\"write_TBps\":%.3f}\n", nt, pc,
+                        double(bytes), double(bytes) * iters / (ms * 1e-3) / 1e12);
+        }
+    }
+    {
+        float ms = 0;
+        CHECK(hipEventRecord(c.a));
+        for (int i = 0; i < iters; ++i) CHECK(hipMemsetAsync(c.buf, 0, bytes, nullptr));
+        CHECK(hipEventRecord(c.b));
+        CHECK(hipEventSynchronize(c.b));
+        CHECK(hipEventElapsedTime(&ms, c.a, c.b));
+        std::printf("{\"ceiling\":\"hipMemsetAsync\",\"bytes\":%.0f,\"write_TBps\":%.3f}\n", double(bytes),
+                    double(bytes) * iters / (ms * 1e-3) / 1e12);
+    }
+    if (store_shape<1, false, false>(c.buf, c.n_vec, c.cus, c.a, c.b) || store_shape<1, true, false>(c.buf, c.n_vec, c.cus, c.a, c.b) ||
+        store_shape<4, false, false>(c.buf, c.n_vec, c.cus, c.a, c.b) || store_shape<4, true, false>(c.buf, c.n_vec, c.cus, c.a, c.b) ||
+        store_shape<1, false, true>(c.buf, c.n_vec, c.cus, c.a, c.b) || store_shape<1, true, true>(c.buf, c.n_vec, c.cus, c.a, c.b) ||
+        store_shape<4, false, true>(c.buf, c.n_vec, c.cus, c.a, c.b) || store_shape<4, true, true>(c.buf, c.n_vec, c.cus, c.a, c.b) ||
+        store_shape<8, true, true>(c.buf, c.n_vec, c.cus, c.a, c.b) || store_shape<8, false, true>(c.buf, c.n_vec, c.cus, c.a, c.b))
+        return 1;
+    if (argc > 2) return 0;  // ceilings only
+    for (int n : {1, 8}) {
+        if (run<1, 1, false>(c, n, 8, iters)) return 1;
+        for (int pc : {8, 16}) {
+            if (run<2, 1, false>(c, n, pc, iters)) return 1;
+            if (run<2, 1, true>(c, n, pc, iters)) return 1;
+            if (run<3, 1, false>(c, n, pc, iters)) return 1;
+            if (run<3, 1, true>(c, n, pc, iters)) return 1;
+            if (run<3, 2, true>(c, n, pc, iters)) return 1;
+        }
+    }
+    return 0;
+}
