@@ -124,20 +124,23 @@ def sync(device) -> None:
 
 
 def pattern_reference(n: int, seed: int, rank: int):
-    """PyTorch (CPU) reference of the HIP pattern in native/hip/netop_hip.hip (mix / group_sum)."""
+    """PyTorch (CPU) reference of the HIP pattern in native/hip/netop_hip.hip (group_hash /
+    rank_mult / group_sum): element i is the 3-bit field at bit 8 + 3 (i & 7) of
+    group_hash(i >> 3) * rank_mult(seed, rank), minus 4."""
     import torch
 
     M32 = 0xFFFFFFFF
     i = torch.arange(n, dtype=torch.int64)
-    g = i >> 3  # one hash per 8-element group; element i is its 3-bit field i & 7, minus 4
-    s = (seed + 0x632BE5AB * (rank + 1)) & M32
-    x = ((g & M32) * 0x9E3779B1) & M32
-    x = x ^ ((((g >> 32) & M32) * 0x85EBCA77) & M32)
-    x = x ^ ((s * 0xC2B2AE3D) & M32)
-    x = x ^ (x >> 15)
-    x = (x * 0x2C1B3C6D) & M32
-    x = x ^ (x >> 12)
-    return (((x >> (3 * (i & 7))) & 7) - 4).to(torch.float32)
+    g = i >> 3  # one hash per 8-element group
+    h = ((g & M32) * 0x9E3779B1) & M32
+    h = h ^ ((((g >> 32) & M32) * 0x85EBCA77) & M32)
+    h = h ^ (h >> 15)
+    h = (h * 0x2C1B3C6D) & M32
+    h = h ^ (h >> 12)
+    k = (((seed + 0x632BE5AB * (rank + 1)) & M32) * 0xC2B2AE3D) & M32
+    m = (k ^ (k >> 16)) | 1
+    x = (h * m) & M32  # int64 wraps on overflow; the low 32 bits are exact
+    return (((x >> (8 + 3 * (i & 7))) & 7) - 4).to(torch.float32)
 
 
 def verify_all_reduce(numel: int, device, seed: int = 2024, group=None) -> tuple[bool, int]:

@@ -9,20 +9,20 @@ pytestmark = pytest.mark.gpu
 
 
 def _ref_pattern(n, seed, rank):
-    """fp32 reference of the device pattern (mirrors mix()/group_sum() in netop_hip.hip)."""
+    """fp32 reference of the device pattern (mirrors group_hash() / rank_mult() / group_sum() in
+    netop_hip.hip), written independently of collectives.pattern_reference."""
     import torch
 
     M32 = 0xFFFFFFFF
     i = torch.arange(n, dtype=torch.int64)
-    g = i >> 3  # one hash per 8-element group; element i is its 3-bit field i & 7, minus 4
-    s = (seed + 0x632BE5AB * (rank + 1)) & M32
-    x = ((g & M32) * 0x9E3779B1) & M32
-    x = x ^ ((((g >> 32) & M32) * 0x85EBCA77) & M32)
-    x = x ^ ((s * 0xC2B2AE3D) & M32)
-    x = x ^ (x >> 15)
-    x = (x * 0x2C1B3C6D) & M32
-    x = x ^ (x >> 12)
-    return (((x >> (3 * (i & 7))) & 7) - 4).to(torch.float32)
+    g = i >> 3  # one hash per 8-element group
+    h = ((g & M32) * 0x9E3779B1) & M32 ^ ((((g >> 32) & M32) * 0x85EBCA77) & M32)
+    h ^= h >> 15
+    h = (h * 0x2C1B3C6D) & M32
+    h ^= h >> 12
+    k = ((seed + 0x632BE5AB * (rank + 1)) & M32) * 0xC2B2AE3D & M32
+    word = (h * ((k ^ (k >> 16)) | 1)) & M32  # rank's word; element i = field at bit 8 + 3 (i % 8)
+    return (((word >> (8 + 3 * (i % 8))) & 7) - 4).to(torch.float32)
 
 
 def test_fill_pattern_matches_reference(cuda_device):
@@ -43,15 +43,15 @@ def test_expected_sum_and_verify(cuda_device):
     from network_operator_amd.ops import hip
 
     n = (1 << 20) + 8
-    world = 8
-    ref = sum(_ref_pattern(n, 5, r) for r in range(world))
-    t = torch.empty(n, dtype=torch.bfloat16, device=cuda_device)
-    hip.fill_expected_sum(t, 5, world)
-    torch.testing.assert_close(t.float().cpu(), ref, rtol=0, atol=0)
-    assert hip.verify_sum(t, 5, world) == 0
-    t[12345] += 1
-    t[-1] += 1
-    assert hip.verify_sum(t, 5, world) == 2
+    for world in (8, 20):  # 20: three 9-rank slot flushes in the SWAR sum
+        ref = sum(_ref_pattern(n, 5, r) for r in range(world))
+        t = torch.empty(n, dtype=torch.bfloat16, device=cuda_device)
+        hip.fill_expected_sum(t, 5, world)
+        torch.testing.assert_close(t.float().cpu(), ref, rtol=0, atol=0)
+        assert hip.verify_sum(t, 5, world) == 0
+        t[12345] += 1
+        t[-1] += 1
+        assert hip.verify_sum(t, 5, world) == 2
 
 
 def test_copy_matches_torch(cuda_device):

@@ -232,3 +232,50 @@ def test_dcb_netlink_requests_reach_the_kernel(native):
     with pytest.raises(OSError) as e:
         r.set_dcbx_mode("lo", 0x09)
     assert any(os.strerror(c) in str(e.value) for c in (errno.EOPNOTSUPP, errno.EPERM)), e.value
+
+
+def test_pattern_swar_sum_matches_the_per_rank_reference():
+    """The device's rank sum (netop_hip.hip group_sum: even / odd 3-bit fields of every rank
+    added as 6-bit slots, flushed every 9 ranks) equals the sum of the per-rank reference
+    (collectives.pattern_reference) for 1..64 ranks and rank ranges -- emulated here with Python
+    integers, line for line."""
+    import random
+
+    import torch
+
+    from network_operator_amd.parallel.collectives import pattern_reference
+
+    M32 = 0xFFFFFFFF
+    SLOTS = (7 << 8) | (7 << 14) | (7 << 20) | (7 << 26)
+
+    def group_hash(g):
+        x = ((g & M32) * 0x9E3779B1 & M32) ^ (((g >> 32) & M32) * 0x85EBCA77 & M32)
+        x ^= x >> 15
+        x = x * 0x2C1B3C6D & M32
+        return x ^ (x >> 12)
+
+    def rank_mult(seed, r):
+        k = ((seed + 0x632BE5AB * (r + 1)) & M32) * 0xC2B2AE3D & M32
+        return (k ^ (k >> 16)) | 1
+
+    def group_sum(g, seed, lo, n):
+        h, s = group_hash(g), [-4 * n] * 8
+        for r0 in range(lo, lo + n, 9):
+            even = odd = 0
+            for r in range(r0, min(r0 + 9, lo + n)):
+                x = h * rank_mult(seed, r) & M32
+                even = (even + (x & SLOTS)) & M32
+                odd = (odd + ((x >> 3) & SLOTS)) & M32
+            for k in range(4):
+                s[2 * k] += (even >> (8 + 6 * k)) & 63
+                s[2 * k + 1] += (odd >> (8 + 6 * k)) & 63
+        return s
+
+    rng = random.Random(7)
+    groups = 64
+    for lo, n in [(0, 1), (3, 1), (0, 8), (0, 9), (0, 10), (5, 18), (0, 64), (17, 27)]:
+        seed = rng.randrange(1 << 32)
+        ref = sum(pattern_reference(groups * 8, seed, r) for r in range(lo, lo + n))
+        dev = torch.tensor([v for g in range(groups) for v in group_sum(g, seed, lo, n)], dtype=torch.float32)
+        assert torch.equal(dev, ref), (lo, n)
+        assert ref.abs().max() <= 256  # exact in bf16
