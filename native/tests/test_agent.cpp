@@ -1821,8 +1821,9 @@ TEST(agent_failed_start_keeps_the_firmware_lldp_originals_for_the_next_agent) {
         b.set_ethtool_ops(std::move(eth));
         b.run(stop.fd[0]);
         CHECK(b.ready());
+        // (the fake belongs to the agent: read it before the agent goes)
+        CHECK_EQ(raw->flags["ens0"].bits, uint32_t(0x2));  // the true original, restored on the clean exit
     }
-    CHECK_EQ(raw->flags["ens0"].bits, uint32_t(0x2));  // the true original, restored on the clean exit
     CHECK(!path_exists(f.cfg.fw_lldp_state));
 }
 
@@ -1882,9 +1883,9 @@ TEST(agent_keep_config_keeps_firmware_lldp_off_across_restarts_until_cleanup) {
             agent::Agent a(plain, f.ops, f.all_valid(), f.nm());
             a.set_ethtool_ops(std::move(eth));
             a.run(stop.fd[0]);
+            CHECK_EQ(raw->flags["ens0"].bits, uint32_t(0x2));  // (the fake goes with the agent)
+            CHECK_EQ(int(raw->dcbx["ens1"]), 0x0c);
         }
-        CHECK_EQ(raw->flags["ens0"].bits, uint32_t(0x2));
-        CHECK_EQ(int(raw->dcbx["ens1"]), 0x0c);
         CHECK(!path_exists(f.cfg.fw_lldp_state));
         write_file_atomic(f.cfg.fw_lldp_state, saved);  // back to the kept state for the cleanup below
     }
@@ -2314,15 +2315,11 @@ TEST(agent_firmware_lldp_records_of_nics_no_longer_selected_are_not_lost) {
             a.run(stop.fd[0]);
             CHECK(a.ready());
             CHECK_EQ(raw->flags["old0"].bits, uint32_t(0x4));  // restored at start
+            // kept off across the restart / the true original back on the clean exit
+            CHECK_EQ(raw->flags["ens0"].bits, uint32_t(keep ? 0x0 : 0x2));
         }
         auto st = read_file(f.cfg.fw_lldp_state);
-        if (keep) {
-            CHECK(st && *st == "ens0 priv 0x2\ngone0 dcbx 0x0c\n");
-            CHECK_EQ(raw->flags["ens0"].bits, uint32_t(0x0));  // kept off across the restart
-        } else {
-            CHECK(st && *st == "gone0 dcbx 0x0c\n");
-            CHECK_EQ(raw->flags["ens0"].bits, uint32_t(0x2));  // the true original, on the clean exit
-        }
+        CHECK(st && *st == (keep ? "ens0 priv 0x2\ngone0 dcbx 0x0c\n" : "gone0 dcbx 0x0c\n"));
     }
 }
 
