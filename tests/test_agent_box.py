@@ -164,6 +164,30 @@ def test_pairing_matches_an_independent_sysfs_oracle(tmp_path):
              "rdma_nics": {n: {k: v for k, v in d.items() if k != "chain"} for n, d in o["nics"].items()}}, indent=1))
 
 
+@pytest.mark.gpu
+def test_rdma_discovery_on_this_node_leaves_every_gpu_rail_alone():
+    """Round 4, on the box's real PCIe tree: host-nic (rdma) discovery takes no NIC that sits
+    below a GPU's PCIe switch.  Checked against the independent oracle above: every NIC the oracle
+    finds affine to some GPU is left out (named with a GPU), and what discovery keeps is disjoint
+    from the amd-so agent's pairs."""
+    root = os.environ.get("SYSFS_ROOT", "/sys/")
+    o = sysfs_oracle(root)
+    if not o["gpus"]:
+        pytest.skip("no amdgpu GPU in this sysfs")
+    d = native().discover(root, mode="rdma", drivers=[])  # every PCI NIC driver: the widest host-nic policy
+    affine = {n for a in o["affine"].values() for n in a["all"]}
+    rdma_affine = {n for n in affine if o["nics"][n]["rdma"]}
+    assert rdma_affine <= set(d["excluded"]), (sorted(rdma_affine), d["excluded"])
+    assert all("scale-out rail of GPU" in why for why in d["excluded"].values())
+    pairs = {p["nic"] for p in native().discover(root, "affine", drivers=[])["pairs"]}
+    assert not set(d["ifnames"]) & pairs, (d["ifnames"], sorted(pairs))
+    out = Path(os.environ.get("GRAFT_REPO_ROOT", ".")) / "gpurun_out"
+    if out.is_dir():
+        (out / "rdma_discovery_box.json").write_text(json.dumps(
+            {"host_nics_kept": d["ifnames"], "left_alone": d["excluded"], "gpu_affine_rdma_nics": sorted(rdma_affine),
+             "amd_so_pairs": sorted(pairs)}, indent=1))
+
+
 def test_oracle_agrees_with_agent_on_the_captured_node(tmp_path):
     """The oracle itself, against the fake tree of the captured 8x MI355X node (CPU-side
     counterpart of the box test; the fixture's rail NICs are mlx5)."""
