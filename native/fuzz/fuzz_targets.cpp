@@ -92,6 +92,11 @@ extern "C" int LLVMFuzzerTestOneInput(const uint8_t* data, size_t size) {
         (void)nl::parse_link_stats(h);
     } catch (const std::exception&) {
     }
+    h->nlmsg_type = RTM_NEWROUTE;  // the same bytes as a route (rtmsg + attributes, RTA_MULTIPATH next hops)
+    try {
+        (void)nl::parse_route(h);
+    } catch (const std::exception&) {
+    }
     h->nlmsg_type = RTM_GETDCB;  // the same bytes as a DCB netlink reply (dcbmsg + attributes)
     try {
         (void)nl::parse_dcb_u8(h, DCB_ATTR_DCBX);

@@ -11,6 +11,7 @@
 #include <sys/socket.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <cstring>
 
 #include "netop/log.hpp"
@@ -361,7 +362,7 @@ static AddrInfo parse_addr(const nlmsghdr* h) {
     return ai;
 }
 
-static RouteInfo parse_route(const nlmsghdr* h) {
+RouteInfo parse_route(const nlmsghdr* h) {
     RouteInfo r;
     const auto* rtm = fixed_header<rtmsg>(h, "route");
     r.dst.len = rtm->rtm_dst_len;

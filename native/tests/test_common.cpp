@@ -94,6 +94,9 @@ TEST(flagset_pflag_semantics) {
 
 #include <linux/netlink.h>
 #include <linux/rtnetlink.h>
+#include <sys/socket.h>
+
+#include <cstring>
 
 #include "netop/netlink.hpp"
 
@@ -116,4 +119,46 @@ TEST(netlink_parse_link_rejects_truncated_and_unaligned_input) {
     m.back() = 'x';
     auto li = netop::nl::parse_link(h2);
     CHECK_EQ(li.name, std::string("x"));
+}
+
+TEST(netlink_parse_route_reads_multipath_next_hops_and_bounds_them) {
+    // A default route over two next hops (ifindex 3 and 7): both are uplinks.  Then the same with
+    // the second next hop's length claiming more than the attribute holds: only the first counts.
+    auto build = [](uint16_t second_len) {
+        std::vector<uint8_t> m(NLMSG_LENGTH(sizeof(rtmsg)), 0);
+        auto put_hop = [&](std::vector<uint8_t>& v, int ifindex, uint16_t len) {
+            rtnexthop nh{};
+            nh.rtnh_len = len;
+            nh.rtnh_ifindex = ifindex;
+            const size_t off = v.size();
+            v.resize(off + RTNH_ALIGN(sizeof nh), 0);
+            std::memcpy(v.data() + off, &nh, sizeof nh);
+        };
+        std::vector<uint8_t> hops;
+        put_hop(hops, 3, sizeof(rtnexthop));
+        put_hop(hops, 7, second_len);
+        const size_t aoff = m.size();
+        m.resize(aoff + RTA_LENGTH(hops.size()), 0);
+        auto* a = reinterpret_cast<rtattr*>(m.data() + aoff);
+        a->rta_type = RTA_MULTIPATH;
+        a->rta_len = uint16_t(RTA_LENGTH(hops.size()));
+        std::memcpy(RTA_DATA(a), hops.data(), hops.size());
+        auto* h = reinterpret_cast<nlmsghdr*>(m.data());
+        h->nlmsg_len = uint32_t(m.size());
+        h->nlmsg_type = RTM_NEWROUTE;
+        auto* rt = reinterpret_cast<rtmsg*>(NLMSG_DATA(h));
+        rt->rtm_family = AF_INET;
+        rt->rtm_table = RT_TABLE_MAIN;
+        rt->rtm_type = RTN_UNICAST;
+        rt->rtm_dst_len = 0;
+        return m;
+    };
+    auto ok = build(sizeof(rtnexthop));
+    auto r = netop::nl::parse_route(reinterpret_cast<nlmsghdr*>(ok.data()));
+    CHECK_EQ(r.dst.len, 0);
+    CHECK_EQ(r.nexthops.size(), size_t(2));
+    CHECK(r.nexthops == std::vector<int>({3, 7}));
+    auto bad = build(200);  // longer than what is left of the attribute
+    auto r2 = netop::nl::parse_route(reinterpret_cast<nlmsghdr*>(bad.data()));
+    CHECK(r2.nexthops == std::vector<int>({3}));
 }
