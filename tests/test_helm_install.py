@@ -417,3 +417,77 @@ def test_predelete_hook_is_rendered_whenever_the_seeded_policy_gets_the_finalize
     seeded = [T.NetworkClusterPolicy.from_dict(x) for x in yaml.safe_load(cm["data"]["policies.yaml"])["policies"]]
     assert [p.name for p in seeded] == ["netconf-amd-scale-out"]
     assert bool(hooks) == R.needs_node_cleanup(seeded[0]) == (keep or nm)
+
+
+# Non-default chart values for every field of the two policy specs, and what the seeded policy
+# must then carry.  image / pullPolicy come from config.amd.image; layer from `mode`.
+_AMD_VALUES = {
+    "mode": "L3", "mtu": 4200, "disableNetworkManager": True, "xgmiCheck": False, "lldpAnnounce": False,
+    "interfaces": ["ens1np0", "ens2np0"], "nicDrivers": ["mlx5_core", "bnxt_en"], "disableFirmwareLldp": True,
+    "metricsPort": 9501, "gpuDirectRdma": "DmaBuf", "rcclEnv": {"NCCL_IB_TC": "106"}, "railTableBase": 100,
+    "rcclSocketIfname": "eno1", "lldpCache": True, "verifyPeers": True, "lldpWait": "2m",
+    "keepConfigOnRestart": True, "railSwitchPattern": "leaf-r{rail}-.*", "minLinkSpeedGbps": 400,
+    "checkPeerMtu": False, "handDcbxToHost": True, "maxUnavailable": "25%",
+    "validation": {"enabled": True, "minBusbw": 300, "minLink": 40, "gpus": 4, "image": "reg/val:1"},
+    "image": {"repository": "reg/agent", "tag": "9.9", "imagePullPolicy": "Always"},
+}
+_HOST_NIC_VALUES = {
+    "enabled": True, "mode": "L3", "mtu": 4000, "nicDrivers": ["bnxt_en"], "driverImage": "reg/kmd:1",
+    "interfaces": ["ens9np0"], "disableNetworkManager": True, "verifyPeers": True, "lldpWait": "45s",
+    "checkPeerMtu": False, "keepConfigOnRestart": True,
+}
+
+
+def test_every_policy_field_is_settable_from_the_chart_and_documented():
+    """A user of the chart reaches every field of the CRD's amdScaleOut and hostNic specs from
+    values.yaml (round 4 added checkPeerMtu and handDcbxToHost to the CRD; the chart exposed only
+    some fields), the rendered policies pass admission without warnings, and the chart README
+    lists every config value."""
+    from network_operator_amd.api.v1alpha1 import types as T
+    from network_operator_amd.api.v1alpha1 import webhook as W
+
+    docs = helm_template(CHART, {"config": {"amd": dict(_AMD_VALUES, enabled=True),
+                                            "hostNic": _HOST_NIC_VALUES}}, NS)
+    seeded = {p["metadata"]["name"]: T.NetworkClusterPolicy.from_dict(p)
+              for p in yaml.safe_load(_configmap_text(docs))["policies"]}
+    so = seeded["netconf-amd-scale-out"].spec.amdScaleOut
+    want = {k: v for k, v in _AMD_VALUES.items() if k not in ("mode", "image", "validation", "maxUnavailable")}
+    want.update(layer="L3", image="reg/agent:9.9", pullPolicy="Always")
+    assert set(want) | {"validation"} == set(T.AmdScaleOutSpec._FIELDS), "a new amdScaleOut field needs a chart value"
+    for k, v in want.items():
+        assert getattr(so, k) == v, k
+    assert so.validation.to_dict() == _AMD_VALUES["validation"]
+    assert seeded["netconf-amd-scale-out"].spec.maxUnavailable == "25%"
+    assert not so.extra
+
+    hn = seeded["netconf-amd-host-nic"].spec.hostNic
+    fields = {f for f in T.HostNicSpec.__dataclass_fields__ if f != "extra"}
+    want = {k: v for k, v in _HOST_NIC_VALUES.items() if k not in ("enabled", "mode")}
+    want.update(layer="L3", image="reg/agent:9.9", pullPolicy="Always")
+    assert set(want) == fields, "a new hostNic field needs a chart value"
+    for k, v in want.items():
+        assert getattr(hn, k) == v, k
+    assert not hn.extra
+
+    for p in seeded.values():
+        assert W.validate_create(p) == [], p.name
+
+    # Defaults render the policy the CRD defaults describe: no optional field forced on.
+    plain = yaml.safe_load(_configmap_text(helm_template(CHART, {"config": {"amd": {"enabled": True},
+                                                                            "hostNic": {"enabled": True}}}, NS)))
+    so = plain["policies"][0]["spec"]["amdScaleOut"]
+    for k in ("checkPeerMtu", "handDcbxToHost", "lldpAnnounce", "interfaces", "nicDrivers", "gpuDirectRdma",
+              "rcclEnv", "rcclSocketIfname"):
+        assert k not in so, k
+    hn = plain["policies"][1]["spec"]["hostNic"]
+    for k in ("interfaces", "disableNetworkManager", "verifyPeers", "lldpWait", "checkPeerMtu",
+              "keepConfigOnRestart"):
+        assert k not in hn, k
+
+    readme = (CHART / "README.md").read_text()
+    values = yaml.safe_load((CHART / "values.yaml").read_text())["config"]
+    for section in ("amd", "hostNic"):
+        for k in values[section]:
+            documented = (f"`config.{section}.{k}`" in readme or f"`config.{section}.{k}." in readme
+                          or f"/ `{k}`" in readme)
+            assert documented, f"config.{section}.{k} undocumented"
