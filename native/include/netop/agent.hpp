@@ -285,6 +285,8 @@ class Agent {
     void detect_lldp(int stop_fd);
     void diagnose_silent();            // after --wait expired: why each silent NIC heard nothing
     std::string check_link_speed(NicState& n);  // "" or why n is below --min-link-speed-gbps
+    // L2: up, carrier, and fast enough (sets n.config_error to the speed shortfall, else clears it).
+    bool l2_link_ok(NicState& n);
     std::string silent_summary() const;
     std::string not_ready_reason() const;  // per NIC, for the readiness probe ("" when none known)  // "" or "LLDP silent on k NIC(s): ... Not configured: ..." for the exit error
     void on_lldp(NicState& n, const lldp::Frame& f);

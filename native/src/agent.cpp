@@ -1198,6 +1198,12 @@ std::string Agent::silent_summary() const {
     return out;
 }
 
+bool Agent::l2_link_ok(NicState& n) {
+    n.config_error = check_link_speed(n);
+    if (!n.config_error.empty()) NLOG_W("Interface '%s' not ready: %s", n.ifname.c_str(), n.config_error.c_str());
+    return n.link.up() && !n.no_carrier && n.config_error.empty();
+}
+
 bool Agent::wait_carrier(int stop_fd) {
     // Admin-up is not a link: a NIC without carrier (unplugged cable, switch port down, optic
     // dead) carries nothing, so L2 readiness needs IFF_LOWER_UP on every NIC.  The reference
@@ -1242,7 +1248,7 @@ bool Agent::wait_carrier(int stop_fd) {
 
 void Agent::write_l2_artifacts() {
     std::string root = cfg_.sysfs_root.empty() ? topo::sysfs_root() : cfg_.sysfs_root;
-    for (auto& n : nics_) n.configured = n.link.up() && !n.no_carrier;
+    for (auto& n : nics_) n.configured = n.link.up() && !n.no_carrier && n.config_error.empty();
     const int64_t deadline = mono_ns() + cfg_.gid_wait_ns;
     for (;;) {
         bool missing = false;
@@ -1591,7 +1597,7 @@ std::string Agent::render_metrics() const {
     for (auto& n : nics_)
         o += strfmt("netop_agent_nic_configured{nic=\"%s\",gpu=\"%s\",rdma=\"%s\"} %d\n",
                     httpd::escape_label(n.ifname).c_str(), n.gpu_bdf.c_str(), n.rdma_dev.c_str(),
-                    (cfg_.mode == "L3" ? n.configured : n.link.up() && !n.no_carrier) ? 1 : 0);
+                    (n.configured && (cfg_.mode == "L3" || n.link.up())) ? 1 : 0);
     metric("netop_agent_nic_degraded", "gauge", "1 while the NIC has lost link after readiness");
     for (auto& n : nics_)
         o += strfmt("netop_agent_nic_degraded{nic=\"%s\"} %d\n", httpd::escape_label(n.ifname).c_str(), n.degraded ? 1 : 0);
@@ -1862,11 +1868,12 @@ void Agent::run(int stop_fd) {
     }
 
     if (cfg_.mode == "L2" && cfg_.configure && cfg_.min_link_speed_mbps > 0) {
-        // L3 checks each NIC as it configures it; L2 has no per-NIC step, so all at once here.
+        // L3 checks each NIC as it configures it; L2 has no per-NIC step, so all at once here --
+        // for the NICs with a link (a dark NIC is checked when its carrier comes, in monitor()).
         std::vector<std::string> slow;
         for (auto& n : nics_)
-            if (std::string why = check_link_speed(n); !why.empty()) slow.push_back(n.ifname + ": " + why);
-        if (!slow.empty()) {
+            if (n.configured && !(n.configured = l2_link_ok(n))) slow.push_back(n.ifname + ": " + n.config_error);
+        if (!slow.empty() && !(cfg_.keep_running && cfg_.monitor)) {
             write_status();
             throw AgentError(strfmt("%zu NIC(s) below the required link speed: ", slow.size()) + join(slow, "; "));
         }
@@ -1942,10 +1949,11 @@ void Agent::run(int stop_fd) {
     if (cfg_.xgmi_expect_links >= 0)
         labels_extra_["amd.feature.node.kubernetes.io/gpu-xgmi.pairs"] = std::to_string(xgmi_.pairs_connected);
     if (!gdr_.kernel.empty()) labels_extra_[cfg_.labels.key + ".gdr"] = gdr_.mode();
-    const bool linked = std::none_of(nics_.begin(), nics_.end(), [](const NicState& n) { return n.no_carrier; });
+    const bool linked = cfg_.mode != "L2" ||
+                        std::all_of(nics_.begin(), nics_.end(), [](const NicState& n) { return n.configured; });
     if (!linked) {
-        // L2 with the monitor: stay up unlabelled; the first carrier on the last dark NIC
-        // publishes the label (monitor()).
+        // L2 with the monitor: stay up unlabelled; the carrier on the last dark NIC (at the
+        // required speed) publishes the label (monitor()).
         NLOG_W("Not ready: %s; the label follows once every NIC has a link", not_ready_reason().c_str());
         write_status();
         NLOG_I("Monitoring...");
@@ -2156,7 +2164,7 @@ int Agent::verify_peers(const std::vector<NicState*>& which, int64_t timeout_ns,
 }
 
 bool Agent::nic_healthy(const NicState& n) const {
-    if (!n.link.up() || n.degraded || n.cache_stale || n.no_carrier) return false;
+    if (!n.link.up() || n.degraded || n.cache_stale || n.no_carrier || !n.config_error.empty()) return false;
     if (cfg_.mode == "L3" && cfg_.verify_peers_ns > 0 && !n.peer_verified) return false;
     return cfg_.mode != "L3" || n.configured;
 }
@@ -2236,7 +2244,7 @@ void Agent::monitor(int stop_fd) {
                         if (up && lower) {
                             NLOG_I("Interface '%s' has carrier now", n.ifname.c_str());
                             n.no_carrier = false;
-                            n.configured = true;
+                            n.configured = l2_link_ok(n);  // --min-link-speed-gbps: checked now it has a speed
                             changed = true;
                         }
                         if (lower) carrier[n.link.index] = true;
@@ -2258,6 +2266,8 @@ void Agent::monitor(int stop_fd) {
                             n.configured = false;
                             n.peer_verified = false;  // the switch port may have come back different
                             configure_interface(n);
+                        } else if (cfg_.mode == "L2") {
+                            n.configured = l2_link_ok(n);  // a port may renegotiate down when it comes back
                         }
                         changed = true;
                     }

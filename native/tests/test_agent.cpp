@@ -2290,6 +2290,65 @@ TEST(agent_l2_waits_for_carrier_and_labels_only_when_every_nic_has_a_link) {
     CHECK(!path_exists(g.cfg.labels.path()));
 }
 
+TEST(agent_l2_checks_the_link_speed_when_the_carrier_comes_and_after_a_flap) {
+    // L2 with the monitor, 400G required.  ens1 has no cable at the start (the kernel reports no
+    // speed); when its carrier comes it has negotiated 200G: still no label, the speed named.  The
+    // port flaps and comes back at 400G: the label follows.  A NIC that is slow from the start
+    // keeps the node unlabelled the same way instead of failing the start.
+    Fixture f;
+    f.cfg.mode = "L2";
+    f.cfg.monitor_tick_ns = 1000000;
+    f.cfg.min_link_speed_mbps = 400000;
+    f.cfg.sysfs_root = f.tmp.path + "/sys";
+    f.tmp.write("sys/class/net/ens0/speed", "400000\n");
+    f.tmp.write("sys/class/net/ens1/speed", "-1\n");
+    f.tmp.write("sys/class/net/ens2/speed", "400000\n");
+    f.ops.no_carrier = {"ens1"};
+    f.ops.links["ens1"].flags &= ~unsigned(IFF_LOWER_UP);
+    Pipe stop;
+    agent::Agent a(f.cfg, f.ops, std::make_unique<ScriptedLldp>(), f.nm());
+    auto reason = [&] { return read_file(agent::reason_path(f.cfg.status_file)).value_or(""); };
+    bool dark = false, slow = false, labelled = false;
+    a.on_monitor_tick = [&](int tick) {
+        if (tick == 1) {
+            dark = !path_exists(f.cfg.labels.path()) && reason().find("ens1: no carrier") == 0;
+            f.tmp.write("sys/class/net/ens1/speed", "200000\n");
+            f.ops.set_carrier("ens1", true);
+        } else if (tick == 3) {
+            slow = !path_exists(f.cfg.labels.path()) &&
+                   reason().find("ens1: link negotiated at 200 Gb/s, below the required 400 Gb/s") == 0;
+            f.ops.set_carrier("ens1", false);
+        } else if (tick == 5) {
+            f.tmp.write("sys/class/net/ens1/speed", "400000\n");
+            f.ops.set_carrier("ens1", true);
+        } else if (tick == 7) {
+            labelled = path_exists(f.cfg.labels.path()) && !path_exists(agent::reason_path(f.cfg.status_file));
+            stop.fire();
+        }
+    };
+    a.run(stop.fd[0]);
+    CHECK(dark);
+    CHECK(slow);
+    CHECK(labelled);
+
+    Fixture g;
+    g.cfg.mode = "L2";
+    g.cfg.monitor_tick_ns = 1000000;
+    g.cfg.min_link_speed_mbps = 400000;
+    g.cfg.sysfs_root = g.tmp.path + "/sys";
+    g.tmp.write("sys/class/net/ens2/speed", "100000\n");
+    Pipe stop2;
+    agent::Agent b(g.cfg, g.ops, std::make_unique<ScriptedLldp>(), g.nm());
+    std::string why;
+    b.on_monitor_tick = [&](int) {
+        why = read_file(agent::reason_path(g.cfg.status_file)).value_or("");
+        stop2.fire();
+    };
+    b.run(stop2.fd[0]);
+    CHECK(why.find("ens2: link negotiated at 100 Gb/s") == 0);
+    CHECK(!path_exists(g.cfg.labels.path()));
+}
+
 TEST(agent_firmware_lldp_records_of_nics_no_longer_selected_are_not_lost) {
     // The record an earlier agent left names ens0 (still selected), old0 (dropped from the
     // policy's interface list) and gone0 (renamed: unreachable).  old0 is not ours any more, so its
