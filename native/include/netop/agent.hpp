@@ -356,13 +356,17 @@ class Agent {
     // the fd, or throws AgentError(busy) at the deadline.
     int take_lock(const std::string& name, int64_t deadline, int stop_fd, const std::string& waiting,
                   const std::string& busy);
-    // The node's own interfaces.  Every mode refuses to touch a NIC that carries a default route
-    // (refuse_uplinks); rdma discovery also leaves out NICs holding addresses or routes the agent
-    // never installs (node_owned_reason), unless --interfaces names them.
+    // The node's own interfaces.  Every mode refuses to touch a NIC that carries a default route,
+    // itself or through a device stacked on it (refuse_uplinks); rdma discovery also leaves out NICs
+    // enslaved to a bond / bridge / team and NICs holding addresses or routes the agent never
+    // installs, or carrying a stacked device that does (node_owned_reason), unless --interfaces
+    // names them.
     std::vector<int> uplinks_;
     bool uplinks_read_ = false;
     const std::vector<int>& uplinks();
-    std::string node_owned_reason(const nl::LinkInfo& l);
+    std::string node_owned_reason(const nl::LinkInfo& l, int depth = 0);
+    // "" when no default route leaves through `ifname`; else "" + the path (" via bond0", ...).
+    std::optional<std::string> uplink_path(const std::string& ifname, int index, int depth = 0);
     void refuse_uplinks();
     std::vector<std::pair<std::string, std::string>> excluded_;  // discovered but left alone, and why
 

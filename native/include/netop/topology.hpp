@@ -97,6 +97,9 @@ std::optional<PciDev> netdev_pci(const std::string& root, const std::string& ifn
 // The negotiated link speed in Mb/s (<root>/class/net/<if>/speed), or -1 when the driver does not
 // report one (link down, virtual NIC, no such file).
 int64_t netdev_speed_mbps(const std::string& root, const std::string& ifname);
+// Devices stacked on a netdev (its sysfs upper_<name> links): the bond, bridge or team it is
+// enslaved to, VLANs and macvlans on it.  Sorted; empty when there are none or no sysfs entry.
+std::vector<std::string> netdev_uppers(const std::string& root, const std::string& ifname);
 // The ancestors RCCL puts above `d` in its topology tree, outermost first.  RCCL (NCCL's
 // ncclTopoGetXmlFromSys) climbs the sysfs path two components at a time — a switch's downstream
 // port and the switch above it count as one bridge — and stops at the root complex, whose

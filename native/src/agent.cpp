@@ -371,9 +371,38 @@ std::string protocol_name(uint8_t p) {
 }
 }  // namespace
 
-std::string Agent::node_owned_reason(const nl::LinkInfo& l) {
+std::optional<std::string> Agent::uplink_path(const std::string& ifname, int index, int depth) {
     const auto& up = uplinks();
-    if (std::find(up.begin(), up.end(), l.index) != up.end()) return "carries the node's default route";
+    if (std::find(up.begin(), up.end(), index) != up.end()) return std::string();
+    if (depth >= 4) return std::nullopt;  // bond on VLAN on bond on ...: deeper stacks are not built
+    const std::string root = cfg_.sysfs_root.empty() ? topo::sysfs_root() : cfg_.sysfs_root;
+    for (const auto& u : topo::netdev_uppers(root, ifname)) {
+        int ui = 0;
+        try {
+            ui = ops_.link_by_name(u).index;
+        } catch (const std::exception&) {
+            continue;
+        }
+        if (auto via = uplink_path(u, ui, depth + 1)) return " via " + u + *via;
+    }
+    return std::nullopt;
+}
+
+std::string Agent::node_owned_reason(const nl::LinkInfo& l, int depth) {
+    if (auto via = uplink_path(l.name, l.index)) return "carries the node's default route" + *via;
+    const std::string root = cfg_.sysfs_root.empty() ? topo::sysfs_root() : cfg_.sysfs_root;
+    const auto uppers = topo::netdev_uppers(root, l.name);
+    if (l.master != 0) {
+        // A bond / bridge / team port: the master device is configured, never its ports.
+        std::string master = "ifindex " + std::to_string(l.master);
+        for (const auto& u : uppers) {
+            try {
+                if (ops_.link_by_name(u).index == l.master) master = u;
+            } catch (const std::exception&) {
+            }
+        }
+        return "is a port of " + master + " (a bond, bridge or team: the node configures the master, not its ports)";
+    }
     // The agent only ever assigns /30s (the LLDP point-to-point links): anything else on the NIC
     // was put there by the node (DHCP, netplan, a static management address).
     const auto addrs = ops_.addr_list(l.index, AF_INET);
@@ -397,22 +426,42 @@ std::string Agent::node_owned_reason(const nl::LinkInfo& l) {
             return strfmt("has the route %s (protocol %s) that the agent does not install", r.dst.masked().str().c_str(),
                           protocol_name(r.protocol).c_str());
     }
+    // VLANs / macvlans on it that the node uses (a management VLAN on a RoCE port).
+    if (depth < 4)
+        for (const auto& u : uppers) {
+            std::string why;
+            try {
+                why = node_owned_reason(ops_.link_by_name(u), depth + 1);
+            } catch (const AgentError&) {
+                throw;
+            } catch (const std::exception&) {
+                continue;
+            }
+            if (!why.empty()) return "carries " + u + ", which " + why;
+        }
     return "";
 }
 
 void Agent::refuse_uplinks() {
     // Flushing the addresses of, or re-MTUing, the NIC the node reaches its gateway through can
     // cut the kubelet off the cluster: never, in any mode, whoever named the NIC.
-    std::vector<std::string> bad;
+    // A NIC under the uplink (a bond port, the parent of a VLAN) counts: changing its MTU or
+    // bouncing it moves the device on top.
+    std::vector<std::string> bad, named;
+    std::vector<std::string> vias;
     for (const auto& n : nics_) {
-        const auto& up = uplinks();
-        if (std::find(up.begin(), up.end(), n.link.index) != up.end()) bad.push_back(n.ifname);
+        if (auto via = uplink_path(n.ifname, n.link.index)) {
+            bad.push_back(n.ifname);
+            vias.push_back(*via);
+            named.push_back(n.ifname + *via);
+        }
     }
     if (bad.empty()) return;
-    const std::string what = join(bad, ", ");
+    const std::string what = join(named, ", ");
     if (cfg_.dry_run) {
         NLOG_W("dry run: would refuse to configure %s: the node's default route leaves through it", what.c_str());
-        for (const auto& b : bad) excluded_.emplace_back(b, "carries the node's default route (refused)");
+        for (size_t i = 0; i < bad.size(); ++i)
+            excluded_.emplace_back(bad[i], "carries the node's default route" + vias[i] + " (refused)");
         return;
     }
     throw AgentError("Refusing to configure " + what +

@@ -203,6 +203,15 @@ int64_t netdev_speed_mbps(const std::string& root, const std::string& ifname) {
     }
 }
 
+std::vector<std::string> netdev_uppers(const std::string& root, const std::string& ifname) {
+    std::vector<std::string> out;
+    if (ifname.empty() || ifname.find('/') != std::string::npos) return out;
+    for (auto& e : list_dir(path_join(root, "class/net/" + ifname)))
+        if (e.rfind("upper_", 0) == 0 && e.size() > 6) out.push_back(e.substr(6));
+    std::sort(out.begin(), out.end());
+    return out;
+}
+
 std::vector<PciDev> rccl_pci_parents(const PciDev& d, std::map<std::string, PciDev>* cache) {
     std::vector<PciDev> out;
     auto pos = d.path.find("/devices/");

@@ -2143,6 +2143,65 @@ TEST(agent_rdma_discovery_leaves_the_nodes_own_nics_alone) {
     }
 }
 
+TEST(agent_rdma_discovery_leaves_bond_ports_and_vlan_parents_the_node_uses_alone) {
+    // Stacked devices: ens0 is a port of bond0; ens1 carries the VLAN ens1.100 with the node's
+    // 10.0.100.5/24 (a management VLAN on a RoCE port); ens2 carries ens2.200, which holds nothing.
+    // Variant 0: bond0 has the default route; variant 1: it has none (a port is still not ours).
+    // Named explicitly, the bond port under the default route is refused like the uplink itself.
+    for (int variant : {0, 1}) {
+        Fixture f;
+        f.cfg.mode = "L2";
+        f.cfg.keep_running = false;
+        f.cfg.interfaces = "";
+        f.cfg.discovery.mode = topo::DiscoveryMode::Rdma;
+        TmpDir sys;
+        host_nic_sysfs(sys);
+        f.cfg.sysfs_root = sys.path;
+        f.ops.add_link("bond0", 20, "02:00:00:00:00:20", true);
+        f.ops.add_link("ens1.100", 21, "02:00:00:00:00:21", true);
+        f.ops.add_link("ens2.200", 22, "02:00:00:00:00:22", true);
+        f.ops.links["ens0"].master = 20;
+        sys.mkdir("devices/virtual/net/bond0");
+        sys.symlink("devices/virtual/net/bond0", "class/net/ens0/upper_bond0");
+        sys.symlink("devices/virtual/net/ens1.100", "class/net/ens1/upper_ens1.100");
+        sys.symlink("devices/virtual/net/ens2.200", "class/net/ens2/upper_ens2.200");
+        CHECK(topo::netdev_uppers(sys.path, "ens0") == std::vector<std::string>{"bond0"});
+        if (variant == 0) f.ops.routes.push_back(route(20, "0.0.0.0/0", "192.168.0.1", RTPROT_DHCP));
+        f.ops.addrs.push_back(nl::AddrInfo{21, AF_INET, *Ipv4::parse("10.0.100.5"), *Ipv4::parse("10.0.100.5"), 24, 0, ""});
+        agent::Agent a(f.cfg, f.ops, std::make_unique<ScriptedLldp>(), f.nm());
+        a.run(-1);
+        CHECK_EQ(a.nics().size(), size_t(1));
+        CHECK_EQ(a.nics()[0].ifname, std::string("ens2"));
+        auto ex = a.excluded();
+        CHECK_EQ(ex.size(), size_t(2));
+        CHECK_EQ(ex[0].second, std::string(variant == 0 ? "the node's own NIC: it carries the node's default route via bond0"
+                                                        : "the node's own NIC: it is a port of bond0 (a bond, bridge or "
+                                                          "team: the node configures the master, not its ports)"));
+        CHECK_EQ(ex[1].second, std::string("the node's own NIC: it carries ens1.100, which holds 10.0.100.5/24, an "
+                                           "address the agent never assigns (it only uses /30s)"));
+        CHECK_EQ(f.ops.links["ens0"].mtu, 1500);
+        CHECK_EQ(f.ops.links["ens1"].mtu, 1500);
+
+        if (variant == 0) {  // named: refused, with the path
+            Fixture g;
+            g.cfg.interfaces = "ens0";
+            g.cfg.sysfs_root = sys.path;
+            g.ops.add_link("bond0", 20, "02:00:00:00:00:20", true);
+            g.ops.links["ens0"].master = 20;
+            g.ops.routes.push_back(route(20, "0.0.0.0/0", "192.168.0.1", RTPROT_DHCP));
+            agent::Agent b(g.cfg, g.ops, g.all_valid(), g.nm());
+            std::string err;
+            try {
+                b.run(-1);
+            } catch (const agent::AgentError& e) {
+                err = e.what();
+            }
+            CHECK(err.find("Refusing to configure ens0 via bond0: the node's default route leaves through it") == 0);
+            CHECK_EQ(g.ops.calls["addr_del"], 0);
+        }
+    }
+}
+
 TEST(agent_rdma_discovery_keeps_the_agents_own_l3_config) {
     // A host NIC an earlier (keep-config) agent addressed: its /30, the kernel /30 route, the /16
     // via the switch end and the rail table are the agent's, so the NIC is still a host NIC.
