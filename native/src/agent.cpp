@@ -21,9 +21,12 @@
 #include <set>
 #include <system_error>
 
+#include "agent_internal.hpp"
 #include "netop/log.hpp"
 
 namespace netop::agent {
+
+using detail::fd_readable;
 
 void sanitize(Config& c) {
     if (c.mtu < 1500) {
@@ -37,13 +40,6 @@ void sanitize(Config& c) {
     if (m != "L2" && m != "L3") throw AgentError("Invalid mode '" + c.mode + "'");
     c.mode = m;
 }
-
-namespace {
-std::string format_gbps(int64_t mbps) { return strfmt("%g", double(mbps) / 1000.0); }
-
-// Longest a --verify-peers re-probe may hold the monitor loop (see Agent::monitor).
-constexpr int64_t kMonitorVerifyNs = 250LL * 1000000;
-}  // namespace
 
 // ---------------------------------------------------------------------------
 // LLDP source over AF_PACKET
@@ -75,12 +71,6 @@ class PacketSource final : public LldpSource {
     bool promisc_;
     pkt::LldpListener listener_;
 };
-
-bool fd_readable(int fd) {
-    if (fd < 0) return false;
-    pollfd p{fd, POLLIN, 0};
-    return ::poll(&p, 1, 0) > 0;
-}
 }  // namespace
 
 std::unique_ptr<LldpSource> make_packet_source(bool promisc) { return std::make_unique<PacketSource>(promisc); }
@@ -114,71 +104,6 @@ Agent::Agent(Config cfg, nl::NetOps& ops, std::unique_ptr<LldpSource> lldp, NmFa
         if (!arp_) arp_ = std::make_unique<arp::Prober>();
         return arp_->probe(ps, timeout_ns, retry_ns, stop_fd);
     };
-}
-
-int Agent::take_lock(const std::string& name, int64_t deadline, int stop_fd, const std::string& waiting,
-                     const std::string& busy) {
-    sockaddr_un sa{};
-    sa.sun_family = AF_UNIX;
-    const size_t n = std::min(name.size(), sizeof sa.sun_path - 1);
-    std::memcpy(sa.sun_path + 1, name.data(), n);  // abstract: sun_path[0] == 0
-    const socklen_t len = socklen_t(offsetof(sockaddr_un, sun_path) + 1 + n);
-    bool waited = false;
-    for (;;) {
-        int fd = ::socket(AF_UNIX, SOCK_STREAM | SOCK_CLOEXEC, 0);
-        if (fd < 0) throw AgentError("lock " + name + ": socket: " + std::strerror(errno));
-        if (::bind(fd, reinterpret_cast<sockaddr*>(&sa), len) == 0) {
-            if (waited) NLOG_I("Lock '%s' acquired", name.c_str());
-            return fd;
-        }
-        const int err = errno;
-        ::close(fd);
-        if (err != EADDRINUSE) throw AgentError("lock " + name + ": bind: " + std::strerror(err));
-        if (!waited) NLOG_I("%s: waiting", waiting.c_str());
-        waited = true;
-        if (mono_ns() >= deadline) throw AgentError(busy);
-        if (stop_fd >= 0) {
-            pollfd p{stop_fd, POLLIN, 0};
-            if (::poll(&p, 1, 100) > 0) throw AgentError("Interrupted while waiting for lock " + name);
-        } else {
-            ::usleep(100000);
-        }
-    }
-}
-
-void Agent::acquire_node_lock(int stop_fd) {
-    if (cfg_.node_lock.empty() || node_lock_fd_ >= 0) return;
-    node_lock_fd_ = take_lock("netop-agent:" + cfg_.node_lock, mono_ns() + cfg_.node_lock_wait_ns, stop_fd,
-                              "Node lock '" + cfg_.node_lock + "' is held by another agent on this node",
-                              "Another agent (or its cleanup) holds the node lock '" + cfg_.node_lock +
-                                  "': two policies of one configuration type select this node, or the previous agent "
-                                  "is still exiting");
-}
-
-void Agent::acquire_nic_locks(int stop_fd) {
-    if (!cfg_.nic_locks || !nic_lock_fds_.empty()) return;
-    // Name order: two agents wanting overlapping NIC sets can never wait on each other in a cycle.
-    std::vector<std::string> names;
-    for (const auto& n : nics_) names.push_back(n.ifname);
-    std::sort(names.begin(), names.end());
-    const int64_t deadline = mono_ns() + cfg_.node_lock_wait_ns;
-    for (const auto& name : names)
-        nic_lock_fds_.push_back(take_lock(
-            "netop-nic:" + name, deadline, stop_fd, "NIC '" + name + "' is held by another agent on this node",
-            "Another agent holds NIC '" + name +
-                "' (its NIC lock): an amd-so and a host-nic policy, or two host-nic policies, select this NIC, or the "
-                "previous agent is still exiting.  Every NIC has one owner: select it in one policy only"));
-}
-
-Agent::~Agent() {
-    if (node_lock_fd_ >= 0) ::close(node_lock_fd_);
-    for (int fd : nic_lock_fds_) ::close(fd);
-    // Both socket sets wait for an RCU grace period when closed: overlap the two waits, so
-    // --verify-peers adds nothing to SIGTERM -> exit.
-    std::thread closing;
-    if (arp_) closing = arp_->close_async();
-    lldp_.reset();
-    if (closing.joinable()) closing.join();
 }
 
 void Agent::mark(const std::string& phase) {
@@ -342,131 +267,6 @@ void Agent::restore_network_manager() {
     } catch (const std::exception& e) {
         NLOG_W("Could not hand the interfaces back to NetworkManager: %s", e.what());
     }
-}
-
-const std::vector<int>& Agent::uplinks() {
-    if (!uplinks_read_) {
-        try {
-            uplinks_ = ops_.default_route_links();
-        } catch (const std::exception& e) {
-            // Not knowing which NIC is the node's uplink is no reason to guess: touch nothing.
-            throw AgentError(std::string("Cannot read the node's routes (needed to leave its own uplinks alone): ") +
-                             e.what());
-        }
-        uplinks_read_ = true;
-    }
-    return uplinks_;
-}
-
-namespace {
-std::string protocol_name(uint8_t p) {
-    switch (p) {
-        case RTPROT_KERNEL: return "kernel";
-        case RTPROT_BOOT: return "boot";
-        case RTPROT_STATIC: return "static";
-        case RTPROT_RA: return "ra";
-        case RTPROT_DHCP: return "dhcp";
-    }
-    return std::to_string(int(p));
-}
-}  // namespace
-
-std::optional<std::string> Agent::uplink_path(const std::string& ifname, int index, int depth) {
-    const auto& up = uplinks();
-    if (std::find(up.begin(), up.end(), index) != up.end()) return std::string();
-    if (depth >= 4) return std::nullopt;  // bond on VLAN on bond on ...: deeper stacks are not built
-    const std::string root = cfg_.sysfs_root.empty() ? topo::sysfs_root() : cfg_.sysfs_root;
-    for (const auto& u : topo::netdev_uppers(root, ifname)) {
-        int ui = 0;
-        try {
-            ui = ops_.link_by_name(u).index;
-        } catch (const std::exception&) {
-            continue;
-        }
-        if (auto via = uplink_path(u, ui, depth + 1)) return " via " + u + *via;
-    }
-    return std::nullopt;
-}
-
-std::string Agent::node_owned_reason(const nl::LinkInfo& l, int depth) {
-    if (auto via = uplink_path(l.name, l.index)) return "carries the node's default route" + *via;
-    const std::string root = cfg_.sysfs_root.empty() ? topo::sysfs_root() : cfg_.sysfs_root;
-    const auto uppers = topo::netdev_uppers(root, l.name);
-    if (l.master != 0) {
-        // A bond / bridge / team port: the master device is configured, never its ports.
-        std::string master = "ifindex " + std::to_string(l.master);
-        for (const auto& u : uppers) {
-            try {
-                if (ops_.link_by_name(u).index == l.master) master = u;
-            } catch (const std::exception&) {
-            }
-        }
-        return "is a port of " + master + " (a bond, bridge or team: the node configures the master, not its ports)";
-    }
-    // The agent only ever assigns /30s (the LLDP point-to-point links): anything else on the NIC
-    // was put there by the node (DHCP, netplan, a static management address).
-    const auto addrs = ops_.addr_list(l.index, AF_INET);
-    for (const auto& a : addrs)
-        if (a.prefixlen != l3::kPointToPointMask)
-            return "holds " + a.prefix().str() + ", an address the agent never assigns (it only uses /30s)";
-    // Routes through it that the agent does not install: its /30 (kernel), the /16 via the switch
-    // end of a /30 of this NIC (boot), and its rail tables (kRailProtocol).
-    auto agents = [&](const nl::RouteSpec& r) {
-        if (r.protocol == kRailProtocol) return true;
-        if (r.protocol == RTPROT_KERNEL && r.dst.len == l3::kPointToPointMask) return true;
-        if (r.protocol == RTPROT_BOOT && r.dst.len == l3::kRoutedNetworkMask && r.gateway)
-            for (const auto& a : addrs)
-                if (a.prefix().contains(*r.gateway)) return true;
-        return false;
-    };
-    for (const auto& r : ops_.route_list(0)) {
-        if (r.table == RT_TABLE_LOCAL || r.type != RTN_UNICAST) continue;
-        if (r.ifindex != l.index && std::find(r.nexthops.begin(), r.nexthops.end(), l.index) == r.nexthops.end()) continue;
-        if (!agents(r))
-            return strfmt("has the route %s (protocol %s) that the agent does not install", r.dst.masked().str().c_str(),
-                          protocol_name(r.protocol).c_str());
-    }
-    // VLANs / macvlans on it that the node uses (a management VLAN on a RoCE port).
-    if (depth < 4)
-        for (const auto& u : uppers) {
-            std::string why;
-            try {
-                why = node_owned_reason(ops_.link_by_name(u), depth + 1);
-            } catch (const AgentError&) {
-                throw;
-            } catch (const std::exception&) {
-                continue;
-            }
-            if (!why.empty()) return "carries " + u + ", which " + why;
-        }
-    return "";
-}
-
-void Agent::refuse_uplinks() {
-    // Flushing the addresses of, or re-MTUing, the NIC the node reaches its gateway through can
-    // cut the kubelet off the cluster: never, in any mode, whoever named the NIC.
-    // A NIC under the uplink (a bond port, the parent of a VLAN) counts: changing its MTU or
-    // bouncing it moves the device on top.
-    std::vector<std::string> bad, named;
-    std::vector<std::string> vias;
-    for (const auto& n : nics_) {
-        if (auto via = uplink_path(n.ifname, n.link.index)) {
-            bad.push_back(n.ifname);
-            vias.push_back(*via);
-            named.push_back(n.ifname + *via);
-        }
-    }
-    if (bad.empty()) return;
-    const std::string what = join(named, ", ");
-    if (cfg_.dry_run) {
-        NLOG_W("dry run: would refuse to configure %s: the node's default route leaves through it", what.c_str());
-        for (size_t i = 0; i < bad.size(); ++i)
-            excluded_.emplace_back(bad[i], "carries the node's default route" + vias[i] + " (refused)");
-        return;
-    }
-    throw AgentError("Refusing to configure " + what +
-                     ": the node's default route leaves through it (flushing its addresses or changing its MTU could "
-                     "cut the node off the network).  Select only scale-out / host RDMA NICs in the policy");
 }
 
 std::vector<std::string> Agent::collect_interfaces() {
@@ -882,417 +682,6 @@ int Agent::configure_all() {
     for (auto& n : nics_)
         if (configure_interface(n)) ++c;
     return c;
-}
-
-void Agent::on_lldp(NicState& n, const lldp::Frame& f) {
-    n.lldp_seen = true;
-    n.t_lldp = mono_ns();
-    n.port_description = f.port_description.value_or("");
-    n.peer_mac = f.peer_mac();
-    n.peer_system_name = f.system_name.value_or("");
-    n.peer_port_id = f.port_id_str();
-    n.peer_max_frame = f.max_frame_size() ? int(*f.max_frame_size()) : -1;
-    std::string err;
-    n.addr = l3::parse_port_description(n.port_description, cfg_.token_policy, &err);
-    if (!n.addr) {
-        n.addr_error = err;
-        NLOG_W("interface '%s': %s", n.ifname.c_str(), err.c_str());
-    } else {
-        n.addr_error.clear();
-    }
-}
-
-bool Agent::refresh_from_frame(NicState& n, const lldp::Frame& f) {
-    std::string desc = f.port_description.value_or("");
-    n.peer_max_frame = f.max_frame_size() ? int(*f.max_frame_size()) : -1;  // checked at the next (re)configuration
-    bool changed = false;
-    if (n.lldp_from_cache) {
-        n.lldp_from_cache = false;
-        changed = true;  // status: lldp_source and, if it was flagged, cache_unconfirmed
-        n.cache_stale = false;
-        if (desc == n.port_description) {
-            NLOG_I("interface '%s': the switch confirmed the cached Port Description", n.ifname.c_str());
-            n.peer_mac = f.peer_mac();
-            n.peer_system_name = f.system_name.value_or("");
-            n.peer_port_id = f.port_id_str();
-            save_lldp_cache();
-            return changed;
-        }
-    }
-    if (desc == n.port_description) return changed;
-    NLOG_I("Port Description of '%s' changed: '%s' -> '%s'", n.ifname.c_str(), n.port_description.c_str(), desc.c_str());
-    auto old = n.addr;
-    on_lldp(n, f);
-    if (n.addr && old && n.addr->local == old->local) return changed;
-    // drop the old address (its /30 and /16 routes go with it) and the rail rule and routes
-    // installed for it, then configure the new one
-    remove_rail_routing(n);
-    try {
-        for (auto& a : ops_.addr_list(n.link.index, AF_INET)) ops_.addr_del(a);
-    } catch (const std::exception& e) {
-        NLOG_W("could not remove old address of '%s': %s", n.ifname.c_str(), e.what());
-    }
-    n.configured = false;
-    n.peer_verified = false;  // a new /30: a new peer to ask
-    n.gid_index.reset();  // the GID follows the address
-    if (n.addr) configure_interface(n);
-    ++reconfigs_;
-    save_lldp_cache();
-    return true;
-}
-
-int Agent::apply_lldp_cache(const std::set<int>& listening) {
-    if (cfg_.lldp_cache.empty() || !cfg_.keep_running || !cfg_.monitor) return 0;
-    const auto entries = artifacts::read_lldp_cache(cfg_.lldp_cache);
-    const int64_t now = int64_t(::time(nullptr));
-    int applied = 0;
-    for (auto& n : nics_) {
-        // Only NICs with an LLDP socket: nothing else could ever confirm the entry.
-        if (!listening.count(n.link.index) || n.lldp_seen) continue;
-        for (const auto& e : entries) {
-            if (e.ifname != n.ifname || e.nic_mac != n.link.mac.str()) continue;  // another NIC now
-            if (now - e.unix_s > cfg_.lldp_cache_max_age_ns / 1000000000 || e.unix_s > now + 60) break;
-            std::string err;
-            auto addr = l3::parse_port_description(e.port_description, cfg_.token_policy, &err);
-            if (!addr) break;
-            n.lldp_seen = true;
-            n.lldp_from_cache = true;
-            n.t_lldp = n.t_cache_applied = mono_ns();
-            n.port_description = e.port_description;
-            n.peer_mac = MacAddr::parse(e.peer_mac);
-            n.peer_system_name = e.system_name;
-            n.peer_port_id = e.port_id;
-            n.addr = addr;
-            n.addr_error.clear();
-            NLOG_I("interface '%s': Port Description '%s' from the LLDP cache (%llds old), awaiting confirmation",
-                   n.ifname.c_str(), e.port_description.c_str(), (long long)(now - e.unix_s));
-            if (cfg_.pipeline && cfg_.configure) configure_interface(n);
-            ++applied;
-            break;
-        }
-    }
-    return applied;
-}
-
-void Agent::save_lldp_cache() {
-    if (cfg_.lldp_cache.empty()) return;
-    const auto old = artifacts::read_lldp_cache(cfg_.lldp_cache);
-    std::vector<artifacts::LldpCacheEntry> out;
-    const int64_t now = int64_t(::time(nullptr));
-    for (const auto& n : nics_) {
-        if (!n.lldp_seen || !n.addr) continue;
-        if (n.lldp_from_cache) {  // not confirmed yet: keep the entry (and its age) as it was
-            for (const auto& e : old)
-                if (e.ifname == n.ifname && e.nic_mac == n.link.mac.str()) out.push_back(e);
-            continue;
-        }
-        out.push_back({n.link.mac.str(), n.ifname, now, n.peer_mac ? n.peer_mac->str() : "", n.peer_system_name,
-                       n.peer_port_id, n.port_description});
-    }
-    try {
-        artifacts::write_lldp_cache(cfg_.lldp_cache, out);
-    } catch (const std::exception& e) {
-        NLOG_W("Could not write the LLDP cache: %s", e.what());
-    }
-}
-
-void Agent::detect_lldp(int stop_fd) {
-    int listening = 0;
-    std::set<int> listened;
-    for (auto& n : nics_) {
-        if (!n.link.up()) {
-            NLOG_I("Link '%s' %s, cannot start LLDP", n.ifname.c_str(), n.link.operstate_str().c_str());
-            continue;
-        }
-        try {
-            lldp_->add(n.ifname, n.link.index, n.link.mac);
-            ++listening;
-            listened.insert(n.link.index);
-            NLOG_I("Started LLDP discovery for '%s'...", n.ifname.c_str());
-        } catch (const std::exception& e) {
-            NLOG_I("Cannot start LLDP client: %s", e.what());
-        }
-    }
-    if (!listening) return;
-    for (auto& n : nics_) {  // what each NIC hears while we wait: the diagnosis of a silent one
-        if (!listened.count(n.link.index)) continue;
-        try {
-            if (auto s = ops_.link_stats(n.link.index)) n.rx_at_listen = s->rx_packets;
-        } catch (const std::exception&) {  // diagnostics only
-        }
-    }
-    int remaining = listening - apply_lldp_cache(listened);
-    if (remaining <= 0) {
-        NLOG_I("Every listening interface was configured from the LLDP cache; the switch confirms it while monitoring");
-        // Still introduce ourselves as a new neighbour, so a fast-start switch confirms now rather
-        // than at its next periodic frame.
-        if (cfg_.announce_shutdown_first) announce_all(0);
-        announce_all(120);
-        return;
-    }
-    auto cb = [&](const std::string& ifname, const lldp::Frame& f) -> bool {
-        if (f.ttl == 0) return false;  // shutdown LLDPDU: the neighbour is going away
-        for (auto& n : nics_) {
-            if (n.ifname != ifname) continue;
-            if (n.lldp_from_cache) {  // configured from the cache: confirm it, or readdress now
-                refresh_from_frame(n, f);
-                continue;
-            }
-            if (n.lldp_seen) continue;  // first frame per NIC wins (client.go:141-142)
-            on_lldp(n, f);
-            if (cfg_.pipeline && cfg_.configure && n.addr) configure_interface(n);
-            --remaining;
-        }
-        return remaining == 0;
-    };
-    const int64_t deadline = mono_ns() + cfg_.wait_ns;
-    std::map<int, int> announces;  // ifindex -> LLDPDUs sent
-    auto announce_nic = [&](NicState& n, bool retry) {
-        try {
-            // After a crash the switch still holds our old neighbour entry and would not treat us
-            // as new (no fast start).  A shutdown LLDPDU first deletes that entry (802.1AB-2009
-            // 9.2.7.7.1), so the next LLDPDU is a new neighbour again.  Retries do the same: if
-            // the switch heard us but its immediate answer was lost (its port was not
-            // transmitting yet), only a "new" neighbour makes it answer again before its next
-            // fast-transmit tick.
-            if ((announces[n.link.index] == 0 || retry) && cfg_.announce_shutdown_first)
-                lldp_->announce(n.ifname, lldp::encode(make_node_frame(cfg_.node_name, n.ifname, n.link.mac, n.gpu_bdf, 0)));
-            lldp_->announce(n.ifname,
-                            lldp::encode(make_node_frame(cfg_.node_name, n.ifname, n.link.mac, n.gpu_bdf, 120, cfg_.mtu)));
-        } catch (const std::exception& e) {
-            NLOG_V(2, "LLDP announce on %s failed: %s", n.ifname.c_str(), e.what());
-        }
-        ++announces[n.link.index];
-    };
-    // A frame sent before the kernel can transmit on the link is dropped without an error:
-    // admin-up is not enough, the device is usable once linkwatch has attached its qdisc and
-    // set operstate UP — and linkwatch batches that work up to a second apart.  So each NIC is
-    // announced the moment its own RTM_NEWLINK says it is operational, not all at link-up.
-    std::unique_ptr<nl::LinkWatcher> watcher;
-    if (cfg_.lldp_announce) {
-        try {
-            watcher = ops_.subscribe_links();
-        } catch (const std::exception& e) {
-            NLOG_V(2, "link events unavailable, announcing on admin-up links: %s", e.what());
-        }
-        if (watcher && watcher->fd() < 0) watcher.reset();  // no pollable events: announce right away
-        if (watcher) {
-            for (auto& n : nics_) {  // state after subscribing: no transition can be missed
-                try {
-                    auto l = ops_.link_by_name(n.ifname);
-                    n.link.flags = l.flags;
-                    n.link.operstate = l.operstate;
-                } catch (const std::exception&) {
-                }
-            }
-        }
-    }
-    auto can_tx = [&](const NicState& n) {
-        if (!watcher) return n.link.up();
-        return n.link.up() && (n.link.operstate == IF_OPER_UP || (n.link.operstate == IF_OPER_UNKNOWN && n.link.lower_up()));
-    };
-    int wake = -1;  // stop_fd or link events
-    if (watcher) {
-        wake = ::epoll_create1(EPOLL_CLOEXEC);
-        for (int f : {stop_fd, watcher->fd()}) {
-            if (f < 0 || wake < 0) continue;
-            epoll_event ev{};
-            ev.events = EPOLLIN;
-            ev.data.fd = f;
-            ::epoll_ctl(wake, EPOLL_CTL_ADD, f, &ev);
-        }
-    }
-    struct CloseFd {
-        int fd;
-        ~CloseFd() {
-            if (fd >= 0) ::close(fd);
-        }
-    } wake_guard{wake};
-    const int wait_fd = wake >= 0 ? wake : stop_fd;
-    int rounds = 0;
-    int64_t next_round = mono_ns();
-    pkt::ListenResult r = pkt::ListenResult::Deadline;
-    for (;;) {
-        if (cfg_.lldp_announce && rounds < cfg_.announce_count && mono_ns() >= next_round) {
-            // Round 0: every NIC that can transmit.  Later rounds (1 s apart): every NIC still
-            // silent, operational or not — a lost frame or a driver without operstate.
-            for (auto& n : nics_)
-                if (n.link.up() && !n.lldp_seen && (rounds > 0 || can_tx(n))) announce_nic(n, rounds > 0);
-            ++rounds;
-            // Retry early, then back off (25 ms, 100 ms, 300 ms, then the interval): a lost
-            // frame or answer costs tens of milliseconds, not a full interval.
-            const int64_t step = rounds == 1   ? cfg_.announce_interval_ns / 40
-                                 : rounds == 2 ? cfg_.announce_interval_ns / 10
-                                 : rounds == 3 ? cfg_.announce_interval_ns * 3 / 10
-                                               : cfg_.announce_interval_ns;
-            next_round = mono_ns() + step;
-        }
-        const int64_t slice_end = cfg_.lldp_announce && rounds < cfg_.announce_count ? std::min(deadline, next_round) : deadline;
-        r = lldp_->run(slice_end, cb, wait_fd);
-        if (r == pkt::ListenResult::Interrupted && watcher && !fd_readable(stop_fd)) {
-            for (auto& ev : watcher->wait(mono_ns())) {  // link events: announce on newly operational NICs
-                for (auto& n : nics_) {
-                    if (n.link.index != ev.link.index || ev.deleted) continue;
-                    n.link.flags = ev.link.flags;
-                    n.link.operstate = ev.link.operstate;
-                    if (!n.lldp_seen && announces[n.link.index] == 0 && can_tx(n)) announce_nic(n, false);
-                }
-            }
-            if (mono_ns() >= deadline) {
-                r = pkt::ListenResult::Deadline;
-                break;
-            }
-            continue;
-        }
-        if (r != pkt::ListenResult::Deadline || mono_ns() >= deadline) break;
-    }
-    if (r == pkt::ListenResult::Interrupted) aborted_ = true;
-    if (r == pkt::ListenResult::Deadline) {
-        NLOG_I("LLDP wait of %s expired with %d interface(s) silent", format_go_duration(cfg_.wait_ns).c_str(), remaining);
-        diagnose_silent();
-    }
-}
-
-void Agent::diagnose_silent() {
-    // The reference's barrier times out without saying why (cmd/discover/main.go:84-122).  On
-    // RoCE NICs the usual cause is the NIC firmware's own LLDP/DCBX agent consuming the
-    // switch's LLDPDUs; tell that apart from a dead link or an undecodable
-    // frame with what the NIC did hear while we waited.
-    std::string root = cfg_.sysfs_root.empty() ? topo::sysfs_root() : cfg_.sysfs_root;
-    const std::string waited = format_go_duration(cfg_.wait_ns);
-    for (auto& n : nics_) {
-        if (n.lldp_seen || n.lldp_from_cache) continue;
-        try {
-            if (auto d = topo::netdev_pci(root, n.ifname)) n.driver = d->driver;
-            if (n.driver.empty() && ethtool_) n.driver = ethtool_->driver(n.ifname);
-        } catch (const std::exception&) {
-        }
-        const std::string drv = n.driver.empty() ? "unknown driver" : n.driver;
-        if (!n.link.up()) {
-            n.lldp_silent = drv + ": link down, nothing listened";
-            NLOG_W("%s: %s", n.ifname.c_str(), n.lldp_silent.c_str());
-            continue;
-        }
-        std::optional<uint64_t> rx;
-        try {
-            if (n.rx_at_listen)
-                if (auto s = ops_.link_stats(n.link.index))
-                    rx = s->rx_packets >= *n.rx_at_listen ? s->rx_packets - *n.rx_at_listen : 0;
-        } catch (const std::exception&) {
-        }
-        auto ls = lldp_->stats_for(n.ifname);
-        std::string heard = rx ? strfmt("%llu frame(s) arrived meanwhile", (unsigned long long)*rx)
-                               : std::string("receive counters unavailable");
-        // Who runs DCBX (and so LLDP) on this port: the host, or an agent embedded in the NIC?
-        // Read-only, unprivileged (DCB netlink); --disable-fw-lldp has read it already.
-        if (n.dcbx.empty()) {
-            try {
-                if (!ethtool_) ethtool_ = ethtool::make_ioctl_ops();
-                if (auto m = ethtool_->dcbx_get(n.ifname)) {
-                    n.dcbx = ethtool::dcbx_str(*m);
-                    n.dcbx_embedded = ethtool::dcbx_embedded(*m);
-                }
-            } catch (const std::exception& e) {
-                NLOG_V(2, "%s: DCBX mode unreadable: %s", n.ifname.c_str(), e.what());
-            }
-        }
-        std::string why;
-        if (ls && ls->malformed) {
-            why = strfmt("%llu LLDPDU(s) did not decode", (unsigned long long)ls->malformed);
-        } else if (rx && *rx == 0) {
-            why = "the link received nothing: check the cable, the switch port and its LLDP transmit setting";
-        } else if (n.dcbx_embedded) {
-            why = "the NIC's embedded agent runs DCBX and LLDP on this port (DCBX " + n.dcbx + ")" +
-                  (cfg_.disable_fw_lldp && cfg_.fw_lldp_dcbx_host
-                       ? " although --disable-fw-lldp ran (" + n.fw_lldp + ")"
-                       : ": run with --disable-fw-lldp --fw-lldp-dcbx-host to hand DCBX to the host (the host must "
-                         "then run DCBX for PFC/ETS itself)");
-        } else if (n.driver == "i40e" || n.driver == "ice") {
-            why = cfg_.disable_fw_lldp ? "NIC-firmware LLDP agent suspected although --disable-fw-lldp ran (" + n.fw_lldp + ")"
-                                       : "NIC-firmware LLDP agent suspected: run with --disable-fw-lldp";
-        } else if (!n.dcbx.empty()) {
-            why = "DCBX is host-managed (" + n.dcbx + "), so no NIC-firmware DCBX agent holds the port: check that the "
-                  "switch port transmits LLDP to the nearest-bridge address 01:80:c2:00:00:0e";
-        } else {
-            why = "NIC-firmware LLDP agent suspected (no verified switch for this driver; see the user guide, "
-                  "\"Silent LLDP\")";
-        }
-        n.lldp_silent = strfmt("%s: no LLDPDU in %s, %s; %s", drv.c_str(), waited.c_str(), heard.c_str(), why.c_str());
-        NLOG_W("%s: %s", n.ifname.c_str(), n.lldp_silent.c_str());
-    }
-}
-
-std::string Agent::check_link_speed(NicState& n) {
-    if (cfg_.min_link_speed_mbps <= 0) return "";
-    const std::string root = cfg_.sysfs_root.empty() ? topo::sysfs_root() : cfg_.sysfs_root;
-    n.speed_mbps = topo::netdev_speed_mbps(root, n.ifname);
-    if (n.speed_mbps < 0) {
-        NLOG_W("Interface '%s': the driver reports no link speed; --min-link-speed-gbps not checked", n.ifname.c_str());
-        return "";
-    }
-    if (n.speed_mbps >= cfg_.min_link_speed_mbps) return "";
-    return strfmt("link negotiated at %s Gb/s, below the required %s Gb/s (a marginal cable or optic, or a port "
-                  "renegotiated down: reseat or replace it)",
-                  format_gbps(n.speed_mbps).c_str(), format_gbps(cfg_.min_link_speed_mbps).c_str());
-}
-
-std::string Agent::silent_summary() const {
-    std::vector<std::string> parts, failed;
-    for (const auto& n : nics_) {
-        if (!n.lldp_silent.empty()) parts.push_back(n.ifname + " (" + n.lldp_silent + ")");
-        if (n.addr && !n.configured && !n.config_error.empty()) failed.push_back(n.ifname + ": " + n.config_error);
-    }
-    std::string out = parts.empty() ? "" : strfmt("LLDP silent on %zu NIC(s): ", parts.size()) + join(parts, "; ");
-    if (!failed.empty()) out += (out.empty() ? "" : " ") + strfmt("Not configured: %s", join(failed, "; ").c_str());
-    return out;
-}
-
-bool Agent::l2_link_ok(NicState& n) {
-    n.config_error = check_link_speed(n);
-    if (!n.config_error.empty()) NLOG_W("Interface '%s' not ready: %s", n.ifname.c_str(), n.config_error.c_str());
-    return n.link.up() && !n.no_carrier && n.config_error.empty();
-}
-
-bool Agent::wait_carrier(int stop_fd) {
-    // Admin-up is not a link: a NIC without carrier (unplugged cable, switch port down, optic
-    // dead) carries nothing, so L2 readiness needs IFF_LOWER_UP on every NIC.  The reference
-    // publishes its label right after link-up (cmd/discover/main.go:198-206,239-246).
-    std::unique_ptr<nl::LinkWatcher> watcher;
-    try {
-        watcher = ops_.subscribe_links();
-    } catch (const std::exception& e) {
-        NLOG_W("link events unavailable, carrier read once: %s", e.what());
-    }
-    for (auto& n : nics_) {  // the state after subscribing: no transition can be missed
-        try {
-            auto l = ops_.link_by_name(n.ifname);
-            n.link.flags = l.flags;
-            n.link.operstate = l.operstate;
-        } catch (const std::exception&) {
-        }
-    }
-    auto missing = [&] {
-        return std::any_of(nics_.begin(), nics_.end(), [](const NicState& n) { return n.link.up() && !n.link.lower_up(); });
-    };
-    const int64_t deadline = mono_ns() + cfg_.link_wait_ns;
-    while (watcher && missing() && mono_ns() < deadline) {
-        if (fd_readable(stop_fd)) return false;
-        const int64_t slice = std::min<int64_t>(deadline, mono_ns() + 100000000LL);  // stop_fd checked every 100 ms
-        for (auto& ev : watcher->wait(slice))
-            for (auto& n : nics_)
-                if (!ev.deleted && n.link.index == ev.link.index) {
-                    n.link.flags = ev.link.flags;
-                    n.link.operstate = ev.link.operstate;
-                }
-    }
-    for (auto& n : nics_) {
-        n.no_carrier = n.link.up() && !n.link.lower_up();
-        n.configured = n.link.up() && !n.no_carrier;
-        if (n.no_carrier)
-            NLOG_W("Interface '%s' has no carrier after %s (%s)", n.ifname.c_str(),
-                   format_go_duration(cfg_.link_wait_ns).c_str(), n.link.operstate_str().c_str());
-    }
-    return true;
 }
 
 void Agent::write_l2_artifacts() {
@@ -2137,251 +1526,6 @@ void Agent::cleanup_node() {
     write_status();
     if (errors) throw AgentError(strfmt("Node cleanup incomplete (%d error(s))", errors));
     NLOG_I("Node cleanup done");
-}
-
-void Agent::announce_all(uint16_t ttl) {
-    if (!cfg_.lldp_announce || cfg_.mode != "L3") return;
-    for (auto& n : nics_) {
-        if (!n.link.up()) continue;
-        try {
-            lldp_->announce(n.ifname,
-                            lldp::encode(make_node_frame(cfg_.node_name, n.ifname, n.link.mac, n.gpu_bdf, ttl, cfg_.mtu)));
-        } catch (const std::exception& e) {
-            NLOG_V(2, "LLDP announce on %s failed: %s", n.ifname.c_str(), e.what());
-        }
-    }
-}
-
-int Agent::verify_peers(const std::vector<NicState*>& which, int64_t timeout_ns, int stop_fd) {
-    std::vector<arp::Probe> probes;
-    std::vector<NicState*> owners;
-    for (NicState* n : which) {
-        if (!n->addr || !n->configured) continue;
-        arp::Probe p;
-        p.ifname = n->ifname;
-        p.ifindex = n->link.index;
-        p.mac = n->link.mac;
-        p.local = n->addr->local;
-        p.peer = n->addr->peer;
-        probes.push_back(p);
-        owners.push_back(n);
-    }
-    if (probes.empty()) return 0;
-    bool finished = false;
-    try {
-        finished = arp_probe(probes, timeout_ns, std::min(cfg_.verify_peers_retry_ns, timeout_ns), stop_fd);
-    } catch (const std::exception& e) {
-        for (NicState* n : owners) {
-            n->peer_verified = false;
-            n->peer_error = e.what();
-        }
-        NLOG_W("Could not verify the switch-side peers: %s", e.what());
-        return int(owners.size());
-    }
-    if (!finished) return -1;
-    int failed = 0;
-    for (size_t i = 0; i < probes.size(); ++i) {
-        const arp::Probe& p = probes[i];
-        NicState& n = *owners[i];
-        n.peer_verified = p.answered;
-        if (p.answered) {
-            n.peer_rtt_ns = p.rtt_ns;
-            n.peer_verify_ns = p.verify_ns;
-            n.peer_arp_mac = p.peer_mac;
-            n.peer_error.clear();
-            NLOG_V(1, "interface '%s': peer %s (%s) answered ARP: rtt %.3f ms, verified after %.3f ms", n.ifname.c_str(),
-                   p.peer.str().c_str(), p.peer_mac.str().c_str(), double(p.rtt_ns) / 1e6, double(p.verify_ns) / 1e6);
-            // The LLDP peer MAC (PortID MAC over ChassisID MAC, reference pkg/lldp/client.go:114-129)
-            // is the switch port; an ARP answer from elsewhere deserves a look, not a failure.
-            const bool mismatch = n.peer_mac && !(*n.peer_mac == p.peer_mac);
-            if (mismatch && !n.peer_mac_mismatch)
-                NLOG_W("interface '%s': peer %s answered ARP from %s, but its LLDP MAC is %s (proxy ARP or a "
-                       "misaddressed port?)", n.ifname.c_str(), p.peer.str().c_str(), p.peer_mac.str().c_str(),
-                       n.peer_mac->str().c_str());
-            n.peer_mac_mismatch = mismatch;
-            continue;
-        }
-        ++failed;
-        n.peer_error = !p.error.empty() ? p.error
-                                        : strfmt("peer %s did not answer ARP within %s (%d requests): is the switch port "
-                                                 "addressed as its Port Description says?",
-                                                 p.peer.str().c_str(), format_go_duration(timeout_ns).c_str(),
-                                                 p.requests);
-        NLOG_W("interface '%s': %s", n.ifname.c_str(), n.peer_error.c_str());
-    }
-    return failed;
-}
-
-bool Agent::nic_healthy(const NicState& n) const {
-    if (!n.link.up() || n.degraded || n.cache_stale || n.no_carrier || !n.config_error.empty()) return false;
-    if (cfg_.mode == "L3" && cfg_.verify_peers_ns > 0 && !n.peer_verified) return false;
-    return cfg_.mode != "L3" || n.configured;
-}
-
-void Agent::monitor(int stop_fd) {
-    std::unique_ptr<nl::LinkWatcher> watcher;
-    try {
-        watcher = ops_.subscribe_links();
-    } catch (const std::exception& e) {
-        NLOG_W("link monitoring disabled: %s", e.what());
-    }
-    // Carrier baseline: only a 1 -> 0 transition of IFF_LOWER_UP counts as a failure (a NIC
-    // whose carrier was never reported up — e.g. a driver without carrier reporting — is not
-    // flagged), IFF_UP going away always does.
-    std::map<int, bool> carrier;
-    for (auto& n : nics_) carrier[n.link.index] = n.link.lower_up();
-    int64_t next_tx = mono_ns() + cfg_.lldp_tx_interval_ns;
-    int64_t next_verify = 0;
-    bool labelled = ready_;  // false: L2 came up with a NIC still without carrier
-    // One pollable fd for "stop or link event": the LLDP wait returns as soon as either
-    // fires, so a link failure is acted on in about a millisecond, not at the next tick.
-    int wake = ::epoll_create1(EPOLL_CLOEXEC);
-    struct CloseFd {
-        int fd;
-        ~CloseFd() {
-            if (fd >= 0) ::close(fd);
-        }
-    } wake_guard{wake};
-    for (int f : {stop_fd, watcher ? watcher->fd() : -1}) {
-        if (f < 0 || wake < 0) continue;
-        epoll_event ev{};
-        ev.events = EPOLLIN;
-        ev.data.fd = f;
-        ::epoll_ctl(wake, EPOLL_CTL_ADD, f, &ev);
-    }
-    int wait_fd = wake >= 0 ? wake : stop_fd;
-    for (int tick = 0;; ++tick) {
-        if (on_monitor_tick) on_monitor_tick(tick);
-        if (fd_readable(stop_fd)) return;
-        int64_t now = mono_ns();
-        if (now >= next_tx) {
-            announce_all(120);  // keep our neighbour entry alive on the switch (TTL 120 s)
-            next_tx = now + cfg_.lldp_tx_interval_ns;
-        }
-        // LLDP: a changed Port Description means the switch port was re-addressed.
-        bool changed = false;
-        auto on_frame = [&](const std::string& ifname, const lldp::Frame& f) -> bool {
-            if (f.ttl == 0) return false;
-            for (auto& n : nics_)
-                if (n.ifname == ifname && refresh_from_frame(n, f)) changed = true;
-            return false;
-        };
-        lldp_->run(std::min(next_tx, mono_ns() + cfg_.monitor_tick_ns), on_frame, wait_fd);
-        if (fd_readable(stop_fd)) return;
-        for (auto& n : nics_) {  // a cached Port Description the switch never confirmed
-            if (!n.lldp_from_cache || n.cache_stale || mono_ns() - n.t_cache_applied < cfg_.lldp_cache_confirm_ns) continue;
-            NLOG_W("interface '%s': no LLDP frame confirmed the cached Port Description within %s",
-                   n.ifname.c_str(), format_go_duration(cfg_.lldp_cache_confirm_ns).c_str());
-            n.cache_stale = true;
-            changed = true;
-        }
-        // Link state.
-        std::string removed;
-        if (watcher) {
-            for (auto& ev : watcher->wait(mono_ns())) {
-                for (auto& n : nics_) {
-                    if (n.link.index != ev.link.index) continue;
-                    if (ev.deleted) {  // driver reload, hot-unplug: the NIC will come back as a new ifindex
-                        removed = n.ifname;
-                        continue;
-                    }
-                    bool was_up = n.link.up(), had_carrier = carrier[n.link.index];
-                    n.link.flags = ev.link.flags;
-                    n.link.operstate = ev.link.operstate;
-                    bool up = n.link.up(), lower = n.link.lower_up();
-                    if (n.no_carrier) {  // never had a link since the start (L2)
-                        if (up && lower) {
-                            NLOG_I("Interface '%s' has carrier now", n.ifname.c_str());
-                            n.no_carrier = false;
-                            n.configured = l2_link_ok(n);  // --min-link-speed-gbps: checked now it has a speed
-                            changed = true;
-                        }
-                        if (lower) carrier[n.link.index] = true;
-                        continue;
-                    }
-                    if ((was_up && !up) || (had_carrier && !lower)) {
-                        if (!n.degraded) {
-                            NLOG_W("Interface '%s' lost link (%s)", n.ifname.c_str(), n.link.flags_str().c_str());
-                            n.degraded = true;
-                            ++n.flaps;
-                            ++flaps_;
-                            changed = true;
-                        }
-                    } else if (n.degraded && up && (lower || !had_carrier)) {
-                        NLOG_I("Interface '%s' recovered", n.ifname.c_str());
-                        n.degraded = false;
-                        // Administrative down flushes the routes: ensure address and routes again.
-                        if (cfg_.mode == "L3" && n.addr) {
-                            n.configured = false;
-                            n.peer_verified = false;  // the switch port may have come back different
-                            configure_interface(n);
-                        } else if (cfg_.mode == "L2") {
-                            n.configured = l2_link_ok(n);  // a port may renegotiate down when it comes back
-                        }
-                        changed = true;
-                    }
-                    if (lower) carrier[n.link.index] = true;
-                }
-            }
-        }
-        if (!removed.empty()) {
-            // Everything this agent knows about the NIC (ifindex, LLDP socket, RDMA device, GID) is
-            // gone with it.  Tear down and exit: the kubelet restarts the container, and the new agent
-            // discovers the node again once the NIC is back (until then it fails to start and
-            // retries; the node stays unlabelled).  Monitoring on would otherwise stay degraded for good.
-            NLOG_W("Interface '%s' was removed: cleaning up and exiting so that a restarted agent discovers the node again",
-                   removed.c_str());
-            // Its rail rule is not tied to the link and would outlive it (its routes went with the
-            // link): remove what was installed for it before forgetting the NIC.
-            for (auto& n : nics_)
-                if (n.ifname == removed) remove_rail_routing(n);
-            nics_.erase(std::remove_if(nics_.begin(), nics_.end(), [&](const NicState& n) { return n.ifname == removed; }),
-                        nics_.end());
-            ready_ = false;
-            post_cleanups();
-            write_status();
-            throw AgentError("Interface '" + removed + "' was removed");
-        }
-        if (cfg_.mode == "L3" && cfg_.verify_peers_ns > 0 && mono_ns() >= next_verify) {
-            // NICs whose peer has not answered (yet): a recovered link, a new /30, or a switch
-            // port still without its address.  Failed NICs are asked again a second later.  The
-            // probe blocks this loop, so it is capped well below the start-up timeout: a switch
-            // answers ARP in microseconds, and a port that is still coming up gets the next round
-            // instead of delaying the other NICs' link and LLDP events by the whole --verify-peers.
-            std::vector<NicState*> todo;
-            for (auto& n : nics_)
-                if (n.configured && !n.peer_verified && n.link.up() && !n.degraded) todo.push_back(&n);
-            if (!todo.empty()) {
-                const int bad = verify_peers(todo, std::min(cfg_.verify_peers_ns, kMonitorVerifyNs), stop_fd);
-                if (bad < 0) return;
-                changed = true;
-                next_verify = bad > 0 ? mono_ns() + 1000000000LL : 0;
-            }
-        }
-        if (changed) {
-            bool healthy = std::all_of(nics_.begin(), nics_.end(), [&](const NicState& n) { return nic_healthy(n); });
-            if (healthy && !labelled) {
-                if (cfg_.mode == "L3")
-                    write_artifacts();
-                else if (!cfg_.rccl_env.empty() || !cfg_.rccl_topo.empty())
-                    write_l2_artifacts();  // a NIC that got its carrier only now has its GID now
-                labelled = publish_label();
-                if (labelled && !phases_.count("total_ready")) phases_["total_ready"] = mono_ns() - t0_;
-                if (labelled) NLOG_I("All scale-out interfaces healthy again: readiness label republished");
-                if (cfg_.mode == "L3") write_host_config();
-                announce_all(120);
-            } else if (!healthy && labelled) {
-                artifacts::remove_labels(cfg_.labels);
-                labelled = false;
-                NLOG_W("Scale-out degraded: readiness label withdrawn");
-            } else if (healthy && labelled && cfg_.mode == "L3") {
-                write_artifacts();  // re-addressed NIC: refresh the RCCL artifacts
-                write_host_config();
-            }
-            ready_ = labelled;
-            write_status();
-        }
-    }
 }
 
 }  // namespace netop::agent

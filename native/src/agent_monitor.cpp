@@ -1,0 +1,272 @@
+// Agent: after readiness.  Periodic LLDP announcements, switch-side ARP verification, and the
+// monitor loop that withdraws and republishes the readiness label as links and switch ports change.
+#include "netop/agent.hpp"
+
+#include <errno.h>
+#include <linux/if.h>
+#include <linux/rtnetlink.h>
+#include <sys/epoll.h>
+#include <sys/socket.h>
+#include <sys/un.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cstring>
+#include <map>
+#include <set>
+
+#include "agent_internal.hpp"
+#include "netop/log.hpp"
+
+namespace netop::agent {
+
+using detail::fd_readable;
+using detail::format_gbps;
+using detail::kMonitorVerifyNs;
+
+void Agent::announce_all(uint16_t ttl) {
+    if (!cfg_.lldp_announce || cfg_.mode != "L3") return;
+    for (auto& n : nics_) {
+        if (!n.link.up()) continue;
+        try {
+            lldp_->announce(n.ifname,
+                            lldp::encode(make_node_frame(cfg_.node_name, n.ifname, n.link.mac, n.gpu_bdf, ttl, cfg_.mtu)));
+        } catch (const std::exception& e) {
+            NLOG_V(2, "LLDP announce on %s failed: %s", n.ifname.c_str(), e.what());
+        }
+    }
+}
+
+int Agent::verify_peers(const std::vector<NicState*>& which, int64_t timeout_ns, int stop_fd) {
+    std::vector<arp::Probe> probes;
+    std::vector<NicState*> owners;
+    for (NicState* n : which) {
+        if (!n->addr || !n->configured) continue;
+        arp::Probe p;
+        p.ifname = n->ifname;
+        p.ifindex = n->link.index;
+        p.mac = n->link.mac;
+        p.local = n->addr->local;
+        p.peer = n->addr->peer;
+        probes.push_back(p);
+        owners.push_back(n);
+    }
+    if (probes.empty()) return 0;
+    bool finished = false;
+    try {
+        finished = arp_probe(probes, timeout_ns, std::min(cfg_.verify_peers_retry_ns, timeout_ns), stop_fd);
+    } catch (const std::exception& e) {
+        for (NicState* n : owners) {
+            n->peer_verified = false;
+            n->peer_error = e.what();
+        }
+        NLOG_W("Could not verify the switch-side peers: %s", e.what());
+        return int(owners.size());
+    }
+    if (!finished) return -1;
+    int failed = 0;
+    for (size_t i = 0; i < probes.size(); ++i) {
+        const arp::Probe& p = probes[i];
+        NicState& n = *owners[i];
+        n.peer_verified = p.answered;
+        if (p.answered) {
+            n.peer_rtt_ns = p.rtt_ns;
+            n.peer_verify_ns = p.verify_ns;
+            n.peer_arp_mac = p.peer_mac;
+            n.peer_error.clear();
+            NLOG_V(1, "interface '%s': peer %s (%s) answered ARP: rtt %.3f ms, verified after %.3f ms", n.ifname.c_str(),
+                   p.peer.str().c_str(), p.peer_mac.str().c_str(), double(p.rtt_ns) / 1e6, double(p.verify_ns) / 1e6);
+            // The LLDP peer MAC (PortID MAC over ChassisID MAC, reference pkg/lldp/client.go:114-129)
+            // is the switch port; an ARP answer from elsewhere deserves a look, not a failure.
+            const bool mismatch = n.peer_mac && !(*n.peer_mac == p.peer_mac);
+            if (mismatch && !n.peer_mac_mismatch)
+                NLOG_W("interface '%s': peer %s answered ARP from %s, but its LLDP MAC is %s (proxy ARP or a "
+                       "misaddressed port?)", n.ifname.c_str(), p.peer.str().c_str(), p.peer_mac.str().c_str(),
+                       n.peer_mac->str().c_str());
+            n.peer_mac_mismatch = mismatch;
+            continue;
+        }
+        ++failed;
+        n.peer_error = !p.error.empty() ? p.error
+                                        : strfmt("peer %s did not answer ARP within %s (%d requests): is the switch port "
+                                                 "addressed as its Port Description says?",
+                                                 p.peer.str().c_str(), format_go_duration(timeout_ns).c_str(),
+                                                 p.requests);
+        NLOG_W("interface '%s': %s", n.ifname.c_str(), n.peer_error.c_str());
+    }
+    return failed;
+}
+
+bool Agent::nic_healthy(const NicState& n) const {
+    if (!n.link.up() || n.degraded || n.cache_stale || n.no_carrier || !n.config_error.empty()) return false;
+    if (cfg_.mode == "L3" && cfg_.verify_peers_ns > 0 && !n.peer_verified) return false;
+    return cfg_.mode != "L3" || n.configured;
+}
+
+void Agent::monitor(int stop_fd) {
+    std::unique_ptr<nl::LinkWatcher> watcher;
+    try {
+        watcher = ops_.subscribe_links();
+    } catch (const std::exception& e) {
+        NLOG_W("link monitoring disabled: %s", e.what());
+    }
+    // Carrier baseline: only a 1 -> 0 transition of IFF_LOWER_UP counts as a failure (a NIC
+    // whose carrier was never reported up — e.g. a driver without carrier reporting — is not
+    // flagged), IFF_UP going away always does.
+    std::map<int, bool> carrier;
+    for (auto& n : nics_) carrier[n.link.index] = n.link.lower_up();
+    int64_t next_tx = mono_ns() + cfg_.lldp_tx_interval_ns;
+    int64_t next_verify = 0;
+    bool labelled = ready_;  // false: L2 came up with a NIC still without carrier
+    // One pollable fd for "stop or link event": the LLDP wait returns as soon as either
+    // fires, so a link failure is acted on in about a millisecond, not at the next tick.
+    int wake = ::epoll_create1(EPOLL_CLOEXEC);
+    struct CloseFd {
+        int fd;
+        ~CloseFd() {
+            if (fd >= 0) ::close(fd);
+        }
+    } wake_guard{wake};
+    for (int f : {stop_fd, watcher ? watcher->fd() : -1}) {
+        if (f < 0 || wake < 0) continue;
+        epoll_event ev{};
+        ev.events = EPOLLIN;
+        ev.data.fd = f;
+        ::epoll_ctl(wake, EPOLL_CTL_ADD, f, &ev);
+    }
+    int wait_fd = wake >= 0 ? wake : stop_fd;
+    for (int tick = 0;; ++tick) {
+        if (on_monitor_tick) on_monitor_tick(tick);
+        if (fd_readable(stop_fd)) return;
+        int64_t now = mono_ns();
+        if (now >= next_tx) {
+            announce_all(120);  // keep our neighbour entry alive on the switch (TTL 120 s)
+            next_tx = now + cfg_.lldp_tx_interval_ns;
+        }
+        // LLDP: a changed Port Description means the switch port was re-addressed.
+        bool changed = false;
+        auto on_frame = [&](const std::string& ifname, const lldp::Frame& f) -> bool {
+            if (f.ttl == 0) return false;
+            for (auto& n : nics_)
+                if (n.ifname == ifname && refresh_from_frame(n, f)) changed = true;
+            return false;
+        };
+        lldp_->run(std::min(next_tx, mono_ns() + cfg_.monitor_tick_ns), on_frame, wait_fd);
+        if (fd_readable(stop_fd)) return;
+        for (auto& n : nics_) {  // a cached Port Description the switch never confirmed
+            if (!n.lldp_from_cache || n.cache_stale || mono_ns() - n.t_cache_applied < cfg_.lldp_cache_confirm_ns) continue;
+            NLOG_W("interface '%s': no LLDP frame confirmed the cached Port Description within %s",
+                   n.ifname.c_str(), format_go_duration(cfg_.lldp_cache_confirm_ns).c_str());
+            n.cache_stale = true;
+            changed = true;
+        }
+        // Link state.
+        std::string removed;
+        if (watcher) {
+            for (auto& ev : watcher->wait(mono_ns())) {
+                for (auto& n : nics_) {
+                    if (n.link.index != ev.link.index) continue;
+                    if (ev.deleted) {  // driver reload, hot-unplug: the NIC will come back as a new ifindex
+                        removed = n.ifname;
+                        continue;
+                    }
+                    bool was_up = n.link.up(), had_carrier = carrier[n.link.index];
+                    n.link.flags = ev.link.flags;
+                    n.link.operstate = ev.link.operstate;
+                    bool up = n.link.up(), lower = n.link.lower_up();
+                    if (n.no_carrier) {  // never had a link since the start (L2)
+                        if (up && lower) {
+                            NLOG_I("Interface '%s' has carrier now", n.ifname.c_str());
+                            n.no_carrier = false;
+                            n.configured = l2_link_ok(n);  // --min-link-speed-gbps: checked now it has a speed
+                            changed = true;
+                        }
+                        if (lower) carrier[n.link.index] = true;
+                        continue;
+                    }
+                    if ((was_up && !up) || (had_carrier && !lower)) {
+                        if (!n.degraded) {
+                            NLOG_W("Interface '%s' lost link (%s)", n.ifname.c_str(), n.link.flags_str().c_str());
+                            n.degraded = true;
+                            ++n.flaps;
+                            ++flaps_;
+                            changed = true;
+                        }
+                    } else if (n.degraded && up && (lower || !had_carrier)) {
+                        NLOG_I("Interface '%s' recovered", n.ifname.c_str());
+                        n.degraded = false;
+                        // Administrative down flushes the routes: ensure address and routes again.
+                        if (cfg_.mode == "L3" && n.addr) {
+                            n.configured = false;
+                            n.peer_verified = false;  // the switch port may have come back different
+                            configure_interface(n);
+                        } else if (cfg_.mode == "L2") {
+                            n.configured = l2_link_ok(n);  // a port may renegotiate down when it comes back
+                        }
+                        changed = true;
+                    }
+                    if (lower) carrier[n.link.index] = true;
+                }
+            }
+        }
+        if (!removed.empty()) {
+            // Everything this agent knows about the NIC (ifindex, LLDP socket, RDMA device, GID) is
+            // gone with it.  Tear down and exit: the kubelet restarts the container, and the new agent
+            // discovers the node again once the NIC is back (until then it fails to start and
+            // retries; the node stays unlabelled).  Monitoring on would otherwise stay degraded for good.
+            NLOG_W("Interface '%s' was removed: cleaning up and exiting so that a restarted agent discovers the node again",
+                   removed.c_str());
+            // Its rail rule is not tied to the link and would outlive it (its routes went with the
+            // link): remove what was installed for it before forgetting the NIC.
+            for (auto& n : nics_)
+                if (n.ifname == removed) remove_rail_routing(n);
+            nics_.erase(std::remove_if(nics_.begin(), nics_.end(), [&](const NicState& n) { return n.ifname == removed; }),
+                        nics_.end());
+            ready_ = false;
+            post_cleanups();
+            write_status();
+            throw AgentError("Interface '" + removed + "' was removed");
+        }
+        if (cfg_.mode == "L3" && cfg_.verify_peers_ns > 0 && mono_ns() >= next_verify) {
+            // NICs whose peer has not answered (yet): a recovered link, a new /30, or a switch
+            // port still without its address.  Failed NICs are asked again a second later.  The
+            // probe blocks this loop, so it is capped well below the start-up timeout: a switch
+            // answers ARP in microseconds, and a port that is still coming up gets the next round
+            // instead of delaying the other NICs' link and LLDP events by the whole --verify-peers.
+            std::vector<NicState*> todo;
+            for (auto& n : nics_)
+                if (n.configured && !n.peer_verified && n.link.up() && !n.degraded) todo.push_back(&n);
+            if (!todo.empty()) {
+                const int bad = verify_peers(todo, std::min(cfg_.verify_peers_ns, kMonitorVerifyNs), stop_fd);
+                if (bad < 0) return;
+                changed = true;
+                next_verify = bad > 0 ? mono_ns() + 1000000000LL : 0;
+            }
+        }
+        if (changed) {
+            bool healthy = std::all_of(nics_.begin(), nics_.end(), [&](const NicState& n) { return nic_healthy(n); });
+            if (healthy && !labelled) {
+                if (cfg_.mode == "L3")
+                    write_artifacts();
+                else if (!cfg_.rccl_env.empty() || !cfg_.rccl_topo.empty())
+                    write_l2_artifacts();  // a NIC that got its carrier only now has its GID now
+                labelled = publish_label();
+                if (labelled && !phases_.count("total_ready")) phases_["total_ready"] = mono_ns() - t0_;
+                if (labelled) NLOG_I("All scale-out interfaces healthy again: readiness label republished");
+                if (cfg_.mode == "L3") write_host_config();
+                announce_all(120);
+            } else if (!healthy && labelled) {
+                artifacts::remove_labels(cfg_.labels);
+                labelled = false;
+                NLOG_W("Scale-out degraded: readiness label withdrawn");
+            } else if (healthy && labelled && cfg_.mode == "L3") {
+                write_artifacts();  // re-addressed NIC: refresh the RCCL artifacts
+                write_host_config();
+            }
+            ready_ = labelled;
+            write_status();
+        }
+    }
+}
+
+}  // namespace netop::agent

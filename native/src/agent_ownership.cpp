@@ -1,0 +1,218 @@
+// Agent: who owns which NIC.  The node-wide locks (one per label file, one per NIC) and the
+// node's own interfaces that no agent configures: default-route NICs (directly or under a bond
+// or VLAN), bond / bridge / team ports, NICs with addresses or routes the agent never installs.
+#include "netop/agent.hpp"
+
+#include <errno.h>
+#include <linux/if.h>
+#include <linux/rtnetlink.h>
+#include <sys/epoll.h>
+#include <sys/socket.h>
+#include <sys/un.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cstring>
+#include <map>
+#include <set>
+
+#include "agent_internal.hpp"
+#include "netop/log.hpp"
+
+namespace netop::agent {
+
+using detail::fd_readable;
+using detail::format_gbps;
+using detail::kMonitorVerifyNs;
+
+int Agent::take_lock(const std::string& name, int64_t deadline, int stop_fd, const std::string& waiting,
+                     const std::string& busy) {
+    sockaddr_un sa{};
+    sa.sun_family = AF_UNIX;
+    const size_t n = std::min(name.size(), sizeof sa.sun_path - 1);
+    std::memcpy(sa.sun_path + 1, name.data(), n);  // abstract: sun_path[0] == 0
+    const socklen_t len = socklen_t(offsetof(sockaddr_un, sun_path) + 1 + n);
+    bool waited = false;
+    for (;;) {
+        int fd = ::socket(AF_UNIX, SOCK_STREAM | SOCK_CLOEXEC, 0);
+        if (fd < 0) throw AgentError("lock " + name + ": socket: " + std::strerror(errno));
+        if (::bind(fd, reinterpret_cast<sockaddr*>(&sa), len) == 0) {
+            if (waited) NLOG_I("Lock '%s' acquired", name.c_str());
+            return fd;
+        }
+        const int err = errno;
+        ::close(fd);
+        if (err != EADDRINUSE) throw AgentError("lock " + name + ": bind: " + std::strerror(err));
+        if (!waited) NLOG_I("%s: waiting", waiting.c_str());
+        waited = true;
+        if (mono_ns() >= deadline) throw AgentError(busy);
+        if (stop_fd >= 0) {
+            pollfd p{stop_fd, POLLIN, 0};
+            if (::poll(&p, 1, 100) > 0) throw AgentError("Interrupted while waiting for lock " + name);
+        } else {
+            ::usleep(100000);
+        }
+    }
+}
+
+void Agent::acquire_node_lock(int stop_fd) {
+    if (cfg_.node_lock.empty() || node_lock_fd_ >= 0) return;
+    node_lock_fd_ = take_lock("netop-agent:" + cfg_.node_lock, mono_ns() + cfg_.node_lock_wait_ns, stop_fd,
+                              "Node lock '" + cfg_.node_lock + "' is held by another agent on this node",
+                              "Another agent (or its cleanup) holds the node lock '" + cfg_.node_lock +
+                                  "': two policies of one configuration type select this node, or the previous agent "
+                                  "is still exiting");
+}
+
+void Agent::acquire_nic_locks(int stop_fd) {
+    if (!cfg_.nic_locks || !nic_lock_fds_.empty()) return;
+    // Name order: two agents wanting overlapping NIC sets can never wait on each other in a cycle.
+    std::vector<std::string> names;
+    for (const auto& n : nics_) names.push_back(n.ifname);
+    std::sort(names.begin(), names.end());
+    const int64_t deadline = mono_ns() + cfg_.node_lock_wait_ns;
+    for (const auto& name : names)
+        nic_lock_fds_.push_back(take_lock(
+            "netop-nic:" + name, deadline, stop_fd, "NIC '" + name + "' is held by another agent on this node",
+            "Another agent holds NIC '" + name +
+                "' (its NIC lock): an amd-so and a host-nic policy, or two host-nic policies, select this NIC, or the "
+                "previous agent is still exiting.  Every NIC has one owner: select it in one policy only"));
+}
+
+Agent::~Agent() {
+    if (node_lock_fd_ >= 0) ::close(node_lock_fd_);
+    for (int fd : nic_lock_fds_) ::close(fd);
+    // Both socket sets wait for an RCU grace period when closed: overlap the two waits, so
+    // --verify-peers adds nothing to SIGTERM -> exit.
+    std::thread closing;
+    if (arp_) closing = arp_->close_async();
+    lldp_.reset();
+    if (closing.joinable()) closing.join();
+}
+
+const std::vector<int>& Agent::uplinks() {
+    if (!uplinks_read_) {
+        try {
+            uplinks_ = ops_.default_route_links();
+        } catch (const std::exception& e) {
+            // Not knowing which NIC is the node's uplink is no reason to guess: touch nothing.
+            throw AgentError(std::string("Cannot read the node's routes (needed to leave its own uplinks alone): ") +
+                             e.what());
+        }
+        uplinks_read_ = true;
+    }
+    return uplinks_;
+}
+
+namespace {
+std::string protocol_name(uint8_t p) {
+    switch (p) {
+        case RTPROT_KERNEL: return "kernel";
+        case RTPROT_BOOT: return "boot";
+        case RTPROT_STATIC: return "static";
+        case RTPROT_RA: return "ra";
+        case RTPROT_DHCP: return "dhcp";
+    }
+    return std::to_string(int(p));
+}
+}  // namespace
+
+std::optional<std::string> Agent::uplink_path(const std::string& ifname, int index, int depth) {
+    const auto& up = uplinks();
+    if (std::find(up.begin(), up.end(), index) != up.end()) return std::string();
+    if (depth >= 4) return std::nullopt;  // bond on VLAN on bond on ...: deeper stacks are not built
+    const std::string root = cfg_.sysfs_root.empty() ? topo::sysfs_root() : cfg_.sysfs_root;
+    for (const auto& u : topo::netdev_uppers(root, ifname)) {
+        int ui = 0;
+        try {
+            ui = ops_.link_by_name(u).index;
+        } catch (const std::exception&) {
+            continue;
+        }
+        if (auto via = uplink_path(u, ui, depth + 1)) return " via " + u + *via;
+    }
+    return std::nullopt;
+}
+
+std::string Agent::node_owned_reason(const nl::LinkInfo& l, int depth) {
+    if (auto via = uplink_path(l.name, l.index)) return "carries the node's default route" + *via;
+    const std::string root = cfg_.sysfs_root.empty() ? topo::sysfs_root() : cfg_.sysfs_root;
+    const auto uppers = topo::netdev_uppers(root, l.name);
+    if (l.master != 0) {
+        // A bond / bridge / team port: the master device is configured, never its ports.
+        std::string master = "ifindex " + std::to_string(l.master);
+        for (const auto& u : uppers) {
+            try {
+                if (ops_.link_by_name(u).index == l.master) master = u;
+            } catch (const std::exception&) {
+            }
+        }
+        return "is a port of " + master + " (a bond, bridge or team: the node configures the master, not its ports)";
+    }
+    // The agent only ever assigns /30s (the LLDP point-to-point links): anything else on the NIC
+    // was put there by the node (DHCP, netplan, a static management address).
+    const auto addrs = ops_.addr_list(l.index, AF_INET);
+    for (const auto& a : addrs)
+        if (a.prefixlen != l3::kPointToPointMask)
+            return "holds " + a.prefix().str() + ", an address the agent never assigns (it only uses /30s)";
+    // Routes through it that the agent does not install: its /30 (kernel), the /16 via the switch
+    // end of a /30 of this NIC (boot), and its rail tables (kRailProtocol).
+    auto agents = [&](const nl::RouteSpec& r) {
+        if (r.protocol == kRailProtocol) return true;
+        if (r.protocol == RTPROT_KERNEL && r.dst.len == l3::kPointToPointMask) return true;
+        if (r.protocol == RTPROT_BOOT && r.dst.len == l3::kRoutedNetworkMask && r.gateway)
+            for (const auto& a : addrs)
+                if (a.prefix().contains(*r.gateway)) return true;
+        return false;
+    };
+    for (const auto& r : ops_.route_list(0)) {
+        if (r.table == RT_TABLE_LOCAL || r.type != RTN_UNICAST) continue;
+        if (r.ifindex != l.index && std::find(r.nexthops.begin(), r.nexthops.end(), l.index) == r.nexthops.end()) continue;
+        if (!agents(r))
+            return strfmt("has the route %s (protocol %s) that the agent does not install", r.dst.masked().str().c_str(),
+                          protocol_name(r.protocol).c_str());
+    }
+    // VLANs / macvlans on it that the node uses (a management VLAN on a RoCE port).
+    if (depth < 4)
+        for (const auto& u : uppers) {
+            std::string why;
+            try {
+                why = node_owned_reason(ops_.link_by_name(u), depth + 1);
+            } catch (const AgentError&) {
+                throw;
+            } catch (const std::exception&) {
+                continue;
+            }
+            if (!why.empty()) return "carries " + u + ", which " + why;
+        }
+    return "";
+}
+
+void Agent::refuse_uplinks() {
+    // Flushing the addresses of, or re-MTUing, the NIC the node reaches its gateway through can
+    // cut the kubelet off the cluster: never, in any mode, whoever named the NIC.
+    // A NIC under the uplink (a bond port, the parent of a VLAN) counts: changing its MTU or
+    // bouncing it moves the device on top.
+    std::vector<std::string> bad, named;
+    std::vector<std::string> vias;
+    for (const auto& n : nics_) {
+        if (auto via = uplink_path(n.ifname, n.link.index)) {
+            bad.push_back(n.ifname);
+            vias.push_back(*via);
+            named.push_back(n.ifname + *via);
+        }
+    }
+    if (bad.empty()) return;
+    const std::string what = join(named, ", ");
+    if (cfg_.dry_run) {
+        NLOG_W("dry run: would refuse to configure %s: the node's default route leaves through it", what.c_str());
+        for (size_t i = 0; i < bad.size(); ++i)
+            excluded_.emplace_back(bad[i], "carries the node's default route" + vias[i] + " (refused)");
+        return;
+    }
+    throw AgentError("Refusing to configure " + what +
+                     ": the node's default route leaves through it (flushing its addresses or changing its MTU could "
+                     "cut the node off the network).  Select only scale-out / host RDMA NICs in the policy");
+}
+
+}  // namespace netop::agent
