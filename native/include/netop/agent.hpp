@@ -365,8 +365,10 @@ class Agent {
     bool uplinks_read_ = false;
     const std::vector<int>& uplinks();
     std::string node_owned_reason(const nl::LinkInfo& l, int depth = 0);
-    // "" when no default route leaves through `ifname`; else "" + the path (" via bond0", ...).
-    std::optional<std::string> uplink_path(const std::string& ifname, int index, int depth = 0);
+    // nullopt when no default route leaves through `l`; else "" (directly) or the path through
+    // the devices stacked on it (" via bond0", " via ens1.100 via br0").
+    std::optional<std::string> uplink_path(const nl::LinkInfo& l, int depth = 0);
+    std::vector<nl::LinkInfo> stacked_on(const nl::LinkInfo& l);  // its master and sysfs upper devices
     void refuse_uplinks();
     std::vector<std::pair<std::string, std::string>> excluded_;  // discovered but left alone, and why
 

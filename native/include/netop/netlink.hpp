@@ -132,6 +132,12 @@ class NetOps {
     // through, in any table but the local one: the node's own uplinks, which the agent never
     // flushes or re-MTUs.  The base implementation reads route_list(0).
     virtual std::vector<int> default_route_links();
+    // The link with this ifindex (a bond / bridge master, ...); nullopt when there is none or the
+    // source cannot look links up by index.
+    virtual std::optional<LinkInfo> link_by_ifindex(int ifindex) {
+        (void)ifindex;
+        return std::nullopt;
+    }
 };
 
 class Rtnl final : public NetOps {
@@ -156,12 +162,16 @@ class Rtnl final : public NetOps {
     std::unique_ptr<LinkWatcher> subscribe_links() override;
     std::optional<LinkStats> link_stats(int ifindex) override;
     std::vector<int> default_route_links() override;  // IPv4 and IPv6
+    std::optional<LinkInfo> link_by_ifindex(int ifindex) override;
 
     // Extra operations (harness / diagnostics; not part of the injectable table).
     LinkInfo link_by_index(int ifindex);
     std::vector<LinkInfo> link_list();
     std::vector<RouteInfo> route_list(uint8_t table = RT_TABLE_MAIN) override;
     void veth_add(const std::string& name, const std::string& peer);
+    // A link of a kind that needs no IFLA_INFO_DATA ("bridge", "dummy", ...).
+    void link_add(const std::string& name, const std::string& kind);
+    void link_set_master(int ifindex, int master);  // 0 = release from its master
     void link_del(int ifindex);
     void link_set_netns_fd(int ifindex, int netns_fd);
     void link_set_netns_pid(int ifindex, int pid);

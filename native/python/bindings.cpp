@@ -34,6 +34,7 @@ static py::dict link_dict(const nl::LinkInfo& l) {
     d["mac"] = l.mac.str();
     d["operstate"] = l.operstate_str();
     d["kind"] = l.kind;
+    d["master"] = l.master;
     return d;
 }
 
@@ -200,6 +201,8 @@ PYBIND11_MODULE(_netop_native, m) {
         .def("link_set_mtu", &nl::Rtnl::link_set_mtu)
         .def("link_set_mac", [](nl::Rtnl& r, int idx, const std::string& mac) { r.link_set_mac(idx, mac_of(mac)); })
         .def("veth_add", &nl::Rtnl::veth_add)
+        .def("link_add", &nl::Rtnl::link_add, py::arg("name"), py::arg("kind"))
+        .def("link_set_master", &nl::Rtnl::link_set_master, py::arg("ifindex"), py::arg("master"))
         .def("link_del", &nl::Rtnl::link_del)
         .def("link_set_netns_pid", &nl::Rtnl::link_set_netns_pid)
         .def("link_set_netns_fd", &nl::Rtnl::link_set_netns_fd)

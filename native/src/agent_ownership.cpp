@@ -117,36 +117,48 @@ std::string protocol_name(uint8_t p) {
 }
 }  // namespace
 
-std::optional<std::string> Agent::uplink_path(const std::string& ifname, int index, int depth) {
-    const auto& up = uplinks();
-    if (std::find(up.begin(), up.end(), index) != up.end()) return std::string();
-    if (depth >= 4) return std::nullopt;  // bond on VLAN on bond on ...: deeper stacks are not built
-    const std::string root = cfg_.sysfs_root.empty() ? topo::sysfs_root() : cfg_.sysfs_root;
-    for (const auto& u : topo::netdev_uppers(root, ifname)) {
-        int ui = 0;
+std::vector<nl::LinkInfo> Agent::stacked_on(const nl::LinkInfo& l) {
+    // Its master from rtnetlink (IFLA_MASTER: bond, bridge, team, VRF), and whatever sysfs lists
+    // as an upper device (VLANs and macvlans too).  Unreadable ones are skipped.
+    std::vector<nl::LinkInfo> out;
+    auto add = [&](std::optional<nl::LinkInfo> u) {
+        if (u && u->index != l.index &&
+            std::none_of(out.begin(), out.end(), [&](const nl::LinkInfo& x) { return x.index == u->index; }))
+            out.push_back(std::move(*u));
+    };
+    if (l.master != 0) {
         try {
-            ui = ops_.link_by_name(u).index;
+            add(ops_.link_by_ifindex(l.master));
         } catch (const std::exception&) {
-            continue;
         }
-        if (auto via = uplink_path(u, ui, depth + 1)) return " via " + u + *via;
     }
+    const std::string root = cfg_.sysfs_root.empty() ? topo::sysfs_root() : cfg_.sysfs_root;
+    for (const auto& u : topo::netdev_uppers(root, l.name)) {
+        try {
+            add(ops_.link_by_name(u));
+        } catch (const std::exception&) {
+        }
+    }
+    return out;
+}
+
+std::optional<std::string> Agent::uplink_path(const nl::LinkInfo& l, int depth) {
+    const auto& up = uplinks();
+    if (std::find(up.begin(), up.end(), l.index) != up.end()) return std::string();
+    if (depth >= 4) return std::nullopt;  // bond on VLAN on bond on ...: deeper stacks are not built
+    for (const auto& u : stacked_on(l))
+        if (auto via = uplink_path(u, depth + 1)) return " via " + u.name + *via;
     return std::nullopt;
 }
 
 std::string Agent::node_owned_reason(const nl::LinkInfo& l, int depth) {
-    if (auto via = uplink_path(l.name, l.index)) return "carries the node's default route" + *via;
-    const std::string root = cfg_.sysfs_root.empty() ? topo::sysfs_root() : cfg_.sysfs_root;
-    const auto uppers = topo::netdev_uppers(root, l.name);
+    if (auto via = uplink_path(l)) return "carries the node's default route" + *via;
+    const auto uppers = stacked_on(l);
     if (l.master != 0) {
         // A bond / bridge / team port: the master device is configured, never its ports.
         std::string master = "ifindex " + std::to_string(l.master);
-        for (const auto& u : uppers) {
-            try {
-                if (ops_.link_by_name(u).index == l.master) master = u;
-            } catch (const std::exception&) {
-            }
-        }
+        for (const auto& u : uppers)
+            if (u.index == l.master) master = u.name;
         return "is a port of " + master + " (a bond, bridge or team: the node configures the master, not its ports)";
     }
     // The agent only ever assigns /30s (the LLDP point-to-point links): anything else on the NIC
@@ -177,13 +189,13 @@ std::string Agent::node_owned_reason(const nl::LinkInfo& l, int depth) {
         for (const auto& u : uppers) {
             std::string why;
             try {
-                why = node_owned_reason(ops_.link_by_name(u), depth + 1);
+                why = node_owned_reason(u, depth + 1);
             } catch (const AgentError&) {
                 throw;
             } catch (const std::exception&) {
                 continue;
             }
-            if (!why.empty()) return "carries " + u + ", which " + why;
+            if (!why.empty()) return "carries " + u.name + ", which " + why;
         }
     return "";
 }
@@ -196,7 +208,7 @@ void Agent::refuse_uplinks() {
     std::vector<std::string> bad, named;
     std::vector<std::string> vias;
     for (const auto& n : nics_) {
-        if (auto via = uplink_path(n.ifname, n.link.index)) {
+        if (auto via = uplink_path(n.link)) {
             bad.push_back(n.ifname);
             vias.push_back(*via);
             named.push_back(n.ifname + *via);

@@ -776,6 +776,31 @@ void Rtnl::veth_add(const std::string& name, const std::string& peer) {
     transact(m, nullptr);
 }
 
+void Rtnl::link_add(const std::string& name, const std::string& kind) {
+    Msg m(RTM_NEWLINK, NLM_F_CREATE | NLM_F_EXCL);
+    ifinfomsg ifi{};
+    ifi.ifi_family = AF_UNSPEC;
+    m.put(ifi);
+    m.attr_str(IFLA_IFNAME, name);
+    size_t li = m.nest_begin(IFLA_LINKINFO);
+    m.attr_str(IFLA_INFO_KIND, kind);
+    m.nest_end(li);
+    transact(m, nullptr);
+}
+
+void Rtnl::link_set_master(int ifindex, int master) {
+    set_link(ifindex, 0, 0, [&](Msg& m) { m.attr_u32(IFLA_MASTER, uint32_t(master)); });
+}
+
+std::optional<LinkInfo> Rtnl::link_by_ifindex(int ifindex) {
+    try {
+        return link_by_index(ifindex);
+    } catch (const SysError& e) {
+        if (e.code() == ENODEV) return std::nullopt;
+        throw;
+    }
+}
+
 void Rtnl::link_del(int ifindex) {
     Msg m(RTM_DELLINK, 0);
     ifinfomsg ifi{};

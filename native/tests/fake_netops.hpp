@@ -56,6 +56,11 @@ struct FakeNetOps : netop::nl::NetOps {
         ++calls[op];
         if (fail.count(op)) throw netop::SysError(fail_errno, "injected " + op);
     }
+    std::optional<netop::nl::LinkInfo> link_by_ifindex(int ifindex) override {
+        maybe_fail("link_by_ifindex");
+        if (auto* l = by_index(ifindex)) return *l;
+        return std::nullopt;
+    }
     netop::nl::LinkInfo link_by_name(const std::string& name) override {
         maybe_fail("link_by_name");
         auto it = links.find(name);

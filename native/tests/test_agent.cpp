@@ -2198,6 +2198,21 @@ TEST(agent_rdma_discovery_leaves_bond_ports_and_vlan_parents_the_node_uses_alone
             }
             CHECK(err.find("Refusing to configure ens0 via bond0: the node's default route leaves through it") == 0);
             CHECK_EQ(g.ops.calls["addr_del"], 0);
+
+            // Without sysfs upper links (the master from rtnetlink alone): the same refusal.
+            Fixture h;
+            h.cfg.interfaces = "ens0";
+            h.ops.add_link("br0", 30, "02:00:00:00:00:30", true);
+            h.ops.links["ens0"].master = 30;
+            h.ops.routes.push_back(route(30, "0.0.0.0/0", "192.168.0.1", RTPROT_DHCP));
+            agent::Agent c(h.cfg, h.ops, h.all_valid(), h.nm());
+            err.clear();
+            try {
+                c.run(-1);
+            } catch (const agent::AgentError& e) {
+                err = e.what();
+            }
+            CHECK(err.find("Refusing to configure ens0 via br0: ") == 0);
         }
     }
 }

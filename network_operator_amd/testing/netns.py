@@ -632,7 +632,7 @@ def run_scenario(n_nics: int = 8, mode: str = "L3", seed: int | None = None, int
 MGMT_NIC, HOST_NIC = "ens9np0", "ens49np1"  # the fixture node's two NICs on their own root ports
 
 
-def run_host_nic_ownership(mode: str = "L2", rails: int = 8) -> dict:
+def run_host_nic_ownership(mode: str = "L2", rails: int = 8, mgmt_bridge: bool = False) -> dict:
     """A default ``host-nic`` policy's agent (rdma discovery, the default driver list) on the
     captured MI355X node, where every NIC is mlx5 with an RDMA device:
 
@@ -642,7 +642,10 @@ def run_host_nic_ownership(mode: str = "L2", rails: int = 8) -> dict:
 
     Records the state before, while the agent is ready, and after SIGTERM; then starts an agent
     that names the management NIC explicitly (``--interfaces``), which must refuse.  Each veth's
-    peer stays in this namespace (up: the NIC has carrier).  Must run inside ``unshare -rn``."""
+    peer stays in this namespace (up: the NIC has carrier).  With ``mgmt_bridge`` the management
+    address and the default route sit on a bridge ``br0`` and ``ens9np0`` is only its port (the
+    kernel's IFLA_MASTER is all that links them here: this sysfs is a fake).  Must run inside
+    ``unshare -rn``."""
     from . import fakesysfs
     from ..utils.paths import native_bin
 
@@ -663,6 +666,12 @@ def run_host_nic_ownership(mode: str = "L2", rails: int = 8) -> dict:
             rt.addr_add(idx, f"10.77.{k}.1/30")
         m = rt.link_by_name(MGMT_NIC)["index"]
         rt.link_set_up(m)
+        if mgmt_bridge:
+            rt.link_add("br0", "bridge")
+            br = rt.link_by_name("br0")["index"]
+            rt.link_set_master(m, br)
+            rt.link_set_up(br)
+            m = br
         rt.addr_add(m, "192.168.77.10/24")
         rt.route_append("0.0.0.0/0", "192.168.77.1", m, 16)  # a DHCP lease's default route
 
@@ -670,7 +679,8 @@ def run_host_nic_ownership(mode: str = "L2", rails: int = 8) -> dict:
             out = {}
             for nif in rail_names + [MGMT_NIC, HOST_NIC]:
                 link = rt.link_by_name(nif)
-                out[nif] = {"up": link["up"], "mtu": link["mtu"], "addrs": rt.addr_list(link["index"])}
+                out[nif] = {"up": link["up"], "mtu": link["mtu"], "addrs": rt.addr_list(link["index"]),
+                            "master": link["master"]}
             out["default_routes"] = [r for r in rt.route_list() if r["dst"] == "0.0.0.0/0"]
             return out
 

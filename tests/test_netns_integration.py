@@ -387,12 +387,16 @@ def test_switch_without_jumbo_frames_is_caught_before_jobs_hang():
     assert "its switch port accepts frames up to 1518 bytes, but MTU 9000 needs 9018" in err
 
 
-def test_default_host_nic_policy_leaves_the_management_nic_and_the_gpu_rails_alone():
+@pytest.mark.parametrize("mgmt_bridge", [False, True])
+def test_default_host_nic_policy_leaves_the_management_nic_and_the_gpu_rails_alone(mgmt_bridge):
     """The captured MI355X node, every NIC mlx5 with an RDMA device: a host-nic agent with the
     default driver list takes only the free host NIC.  The management NIC (address + default
     route) and the eight GPU rails (an amd-so agent's /30s, MTU 9000) are untouched while it runs
-    and after it exits; naming the management NIC explicitly is refused."""
-    r = netns.run_isolated(host_nic_ownership=True)
+    and after it exits; naming the management NIC explicitly is refused.  Second case: the
+    management address and default route are on a bridge and the NIC is its port (a kernel
+    bridge; the same holds for a bond)."""
+    r = netns.run_isolated(host_nic_ownership=True, mgmt_bridge=mgmt_bridge)
+    via = " via br0" if mgmt_bridge else ""
     assert r["ready"], r["agent_log"]
     assert "host-nic-ready.nics=1" in r["label"]
     rails = r["rails"]
@@ -403,16 +407,17 @@ def test_default_host_nic_policy_leaves_the_management_nic_and_the_gpu_rails_alo
     assert all("scale-out rail of GPU" in why for why in r["discovery"]["excluded"].values())
     # The agent's view: the management NIC left out too, for its default route.
     assert [i["name"] for i in r["status"]["interfaces"]] == [netns.HOST_NIC]
-    assert f"{netns.MGMT_NIC}: the node's own NIC: it carries the node's default route" in r["status"]["excluded"]
+    assert f"{netns.MGMT_NIC}: the node's own NIC: it carries the node's default route{via}" in r["status"]["excluded"]
     for phase in ("while_ready", "after_sigterm"):
         for nif in rails + [netns.MGMT_NIC]:
             assert r[phase][nif] == r["before"][nif], (phase, nif, r[phase][nif], r["before"][nif])
         assert r[phase]["default_routes"] == r["before"]["default_routes"]
-    assert r["while_ready"][netns.HOST_NIC] == {"up": True, "mtu": 9000, "addrs": []}
+    assert r["while_ready"][netns.HOST_NIC] == {"up": True, "mtu": 9000, "addrs": [], "master": 0}
     assert r["after_sigterm"][netns.HOST_NIC]["up"] is False  # restored to its original state
     assert r["agent_rc"] == 0
     named = r["named_mgmt"]
-    assert named["rc"] == 1 and f"Refusing to configure {netns.MGMT_NIC}: the node's default route" in named["stderr"]
+    assert named["rc"] == 1 and f"Refusing to configure {netns.MGMT_NIC}{via}: the node's default route" in named["stderr"]
+    assert (r["before"][netns.MGMT_NIC]["master"] != 0) == mgmt_bridge
     assert named["after"] == r["before"][netns.MGMT_NIC]
 
 
