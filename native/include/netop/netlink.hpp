@@ -53,6 +53,7 @@ struct AddrInfo {
     int prefixlen = 0;
     uint8_t scope = 0;
     std::string label;
+    std::string address6;  // AF_INET6: the address in text form ("fd00::5"); empty for IPv4
     Ipv4Prefix prefix() const { return Ipv4Prefix{local, prefixlen}; }
 };
 

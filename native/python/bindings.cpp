@@ -149,6 +149,18 @@ PYBIND11_MODULE(_netop_native, m) {
             for (auto& a : r.addr_list(ifindex, AF_INET)) l.append(a.prefix().str());
             return l;
         }, py::arg("ifindex") = 0)
+        .def("addr6_list", [](nl::Rtnl& r, int ifindex) {
+            py::list l;
+            for (auto& a : r.addr_list(ifindex, AF_INET6)) {
+                py::dict d;
+                d["address"] = a.address6;
+                d["prefixlen"] = a.prefixlen;
+                d["scope"] = int(a.scope);
+                d["ifindex"] = a.ifindex;
+                l.append(d);
+            }
+            return l;
+        }, py::arg("ifindex") = 0)
         .def("addr_add", [](nl::Rtnl& r, int ifindex, const std::string& cidr) {
             auto p = Ipv4Prefix::parse(cidr);
             if (!p) throw py::value_error("bad CIDR");

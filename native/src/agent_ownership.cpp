@@ -167,6 +167,16 @@ std::string Agent::node_owned_reason(const nl::LinkInfo& l, int depth) {
     for (const auto& a : addrs)
         if (a.prefixlen != l3::kPointToPointMask)
             return "holds " + a.prefix().str() + ", an address the agent never assigns (it only uses /30s)";
+    // The agent never assigns IPv6 either: a global or ULA address (a storage or management
+    // network) is the node's.  Link-local ones come with every up interface.
+    try {
+        for (const auto& a : ops_.addr_list(l.index, AF_INET6))
+            if (a.family == AF_INET6 && a.ifindex == l.index && a.scope < RT_SCOPE_LINK && !a.address6.empty())
+                return "holds " + a.address6 + "/" + std::to_string(a.prefixlen) +
+                       ", an IPv6 address the agent never assigns";
+    } catch (const SysError& e) {
+        if (e.code() != EAFNOSUPPORT) throw;  // a kernel without IPv6
+    }
     // Routes through it that the agent does not install: its /30 (kernel), the /16 via the switch
     // end of a /30 of this NIC (boot), and its rail tables (kRailProtocol).
     auto agents = [&](const nl::RouteSpec& r) {

@@ -1,5 +1,6 @@
 #include "netop/netlink.hpp"
 
+#include <arpa/inet.h>
 #include <errno.h>
 #include <linux/dcbnl.h>
 #include <linux/if.h>
@@ -342,6 +343,11 @@ static AddrInfo parse_addr(const nlmsghdr* h) {
     bool have_local = false;
     size_t len = h->nlmsg_len - NLMSG_LENGTH(sizeof(ifaddrmsg));
     for_each_attr(IFA_RTA(ifa), len, [&](const rtattr* a) {
+        if (ifa->ifa_family == AF_INET6 && a->rta_type == IFA_ADDRESS && RTA_PAYLOAD(a) == 16) {
+            char buf[INET6_ADDRSTRLEN] = {};
+            if (::inet_ntop(AF_INET6, RTA_DATA(a), buf, sizeof(buf))) ai.address6 = buf;
+            return;
+        }
         if (ifa->ifa_family != AF_INET) return;
         switch (a->rta_type) {
             case IFA_ADDRESS:

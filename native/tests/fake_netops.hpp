@@ -70,8 +70,11 @@ struct FakeNetOps : netop::nl::NetOps {
     std::vector<netop::nl::AddrInfo> addr_list(int ifindex, int family) override {
         maybe_fail("addr_list");
         std::vector<netop::nl::AddrInfo> out;
-        for (auto& a : addrs)
-            if (a.ifindex == ifindex) out.push_back(a);
+        for (auto& a : addrs) {
+            // (entries without a family are IPv4, as the tests write them)
+            const bool v6 = a.family == AF_INET6;
+            if (a.ifindex == ifindex && (family == AF_UNSPEC || (family == AF_INET6) == v6)) out.push_back(a);
+        }
         return out;
     }
     void addr_add(int ifindex, const netop::Ipv4Prefix& p) override {

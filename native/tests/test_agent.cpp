@@ -2217,6 +2217,39 @@ TEST(agent_rdma_discovery_leaves_bond_ports_and_vlan_parents_the_node_uses_alone
     }
 }
 
+TEST(agent_rdma_discovery_leaves_a_nic_with_a_global_ipv6_address_alone) {
+    // An IPv6-only storage network on ens1 (a ULA address, no default route): the node's.  A
+    // link-local address (every up NIC has one) does not count.
+    Fixture f;
+    f.cfg.mode = "L2";
+    f.cfg.keep_running = false;
+    f.cfg.interfaces = "";
+    f.cfg.discovery.mode = topo::DiscoveryMode::Rdma;
+    TmpDir sys;
+    host_nic_sysfs(sys);
+    f.cfg.sysfs_root = sys.path;
+    nl::AddrInfo ula{};
+    ula.ifindex = 11;
+    ula.family = AF_INET6;
+    ula.address6 = "fd00:77::5";
+    ula.prefixlen = 64;
+    ula.scope = RT_SCOPE_UNIVERSE;
+    nl::AddrInfo ll = ula;
+    ll.ifindex = 12;
+    ll.address6 = "fe80::2";
+    ll.scope = RT_SCOPE_LINK;
+    f.ops.addrs.push_back(ula);
+    f.ops.addrs.push_back(ll);
+    agent::Agent a(f.cfg, f.ops, std::make_unique<ScriptedLldp>(), f.nm());
+    a.run(-1);
+    std::vector<std::string> got;
+    for (const auto& n : a.nics()) got.push_back(n.ifname);
+    CHECK(got == (std::vector<std::string>{"ens0", "ens2"}));
+    auto ex = a.excluded();
+    CHECK_EQ(ex.size(), size_t(1));
+    CHECK_EQ(ex[0].second, std::string("the node's own NIC: it holds fd00:77::5/64, an IPv6 address the agent never assigns"));
+}
+
 TEST(agent_rdma_discovery_keeps_the_agents_own_l3_config) {
     // A host NIC an earlier (keep-config) agent addressed: its /30, the kernel /30 route, the /16
     // via the switch end and the rail table are the agent's, so the NIC is still a host NIC.

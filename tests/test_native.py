@@ -234,6 +234,21 @@ def test_dcb_netlink_requests_reach_the_kernel(native):
     assert any(os.strerror(c) in str(e.value) for c in (errno.EOPNOTSUPP, errno.EPERM)), e.value
 
 
+def test_ipv6_addresses_are_read_from_the_kernel(native):
+    """The agent treats a global / ULA IPv6 address on a NIC as the node's (ownership check), so
+    the rtnetlink address dump must carry IPv6 addresses with their scope: lo's ::1 is host scope
+    (254), which the agent ignores like link-local (253)."""
+    if not os.path.exists("/proc/net/if_inet6"):
+        pytest.skip("kernel without IPv6")
+    r = native.Rtnl()
+    lo = r.link_by_name("lo")["index"]
+    got = r.addr6_list(lo)
+    if not got:
+        pytest.skip("no IPv6 address on lo in this namespace")
+    assert {"address": "::1", "prefixlen": 128, "scope": 254, "ifindex": lo} in got
+    assert all(a["address"] for a in r.addr6_list(0))
+
+
 def test_pattern_swar_sum_matches_the_per_rank_reference():
     """The device's rank sum (netop_hip.hip group_sum: even / odd 3-bit fields of every rank
     added as 6-bit slots, flushed every 9 ranks) equals the sum of the per-rank reference
