@@ -2456,6 +2456,69 @@ TEST(agent_l2_checks_the_link_speed_when_the_carrier_comes_and_after_a_flap) {
     CHECK(!path_exists(g.cfg.labels.path()));
 }
 
+TEST(agent_l2_label_follows_a_random_sequence_of_flaps_and_speed_changes) {
+    // Property: under any sequence of cable pulls, re-plugs and speed renegotiations, the L2 label
+    // is published exactly when every NIC is ready, where a NIC is ready when it has carrier and
+    // had the required speed when its carrier last came (the speed is read at that moment, as a
+    // port renegotiates when its link comes up).  The readiness probe's reason file exists exactly
+    // when the label does not.  200 random steps for each of three fixed seeds.
+    for (uint64_t seed : {0x9E3779B97F4A7C15ull, 0x1234567887654321ull, 0xDEADBEEFCAFEBABEull}) {
+        Fixture f;
+        f.cfg.mode = "L2";
+        f.cfg.monitor_tick_ns = 1000000;
+        f.cfg.min_link_speed_mbps = 400000;
+        f.cfg.sysfs_root = f.tmp.path + "/sys";
+        const std::vector<std::string> nics = {"ens0", "ens1", "ens2"};
+        std::map<std::string, bool> carrier, ready;
+        std::map<std::string, int64_t> speed;
+        for (const auto& n : nics) {
+            carrier[n] = ready[n] = true;
+            speed[n] = 400000;
+            f.tmp.write("sys/class/net/" + n + "/speed", "400000\n");
+        }
+        uint64_t rng = seed;
+        auto next = [&] {
+            rng ^= rng << 13;
+            rng ^= rng >> 7;
+            rng ^= rng << 17;
+            return rng;
+        };
+        Pipe stop;
+        agent::Agent a(f.cfg, f.ops, std::make_unique<ScriptedLldp>(), f.nm());
+        int checked = 0, mismatches = 0, labelled_states = 0;
+        std::string first_bad;
+        a.on_monitor_tick = [&](int tick) {
+            if (tick % 2 == 0) {  // the previous step has been processed: check
+                bool want = std::all_of(nics.begin(), nics.end(), [&](const std::string& n) { return ready[n]; });
+                bool label = path_exists(f.cfg.labels.path());
+                bool reason = path_exists(agent::reason_path(f.cfg.status_file));
+                ++checked;
+                labelled_states += want;
+                if (label != want || reason == want) {
+                    if (!mismatches) first_bad = strfmt("tick %d: want %d label %d reason %d", tick, want, label, reason);
+                    ++mismatches;
+                }
+                if (tick >= 400) stop.fire();
+                return;
+            }
+            const std::string& n = nics[next() % nics.size()];
+            if (next() % 4 == 0) {  // the port renegotiates (takes effect at the next link-up)
+                speed[n] = next() % 4 ? 400000 : 200000;
+                f.tmp.write("sys/class/net/" + n + "/speed", std::to_string(speed[n]) + "\n");
+            } else {
+                carrier[n] = !carrier[n];
+                ready[n] = carrier[n] && speed[n] >= 400000;
+                f.ops.set_carrier(n, carrier[n]);
+            }
+        };
+        a.run(stop.fd[0]);
+        if (mismatches) fprintf(stderr, "seed %llx, %s\n", (unsigned long long)seed, first_bad.c_str());
+        CHECK_EQ(mismatches, 0);
+        CHECK_EQ(checked, 201);
+        CHECK(labelled_states > 0 && labelled_states < checked);  // the sequence visits both states
+    }
+}
+
 TEST(agent_firmware_lldp_records_of_nics_no_longer_selected_are_not_lost) {
     // The record an earlier agent left names ens0 (still selected), old0 (dropped from the
     // policy's interface list) and gone0 (renamed: unreachable).  old0 is not ours any more, so its
