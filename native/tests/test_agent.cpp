@@ -2519,6 +2519,93 @@ TEST(agent_l2_label_follows_a_random_sequence_of_flaps_and_speed_changes) {
     }
 }
 
+TEST(agent_l3_label_and_addresses_follow_random_flaps_and_re_addressing) {
+    // Property (L3 with the monitor): under any sequence of cable pulls, re-plugs and switch-port
+    // re-addressing (a new /30 in the Port Description), the label is published exactly when every
+    // NIC has carrier, and every NIC with carrier holds exactly the /30 its switch port currently
+    // describes (peer ^ 3).  Frames only arrive while a NIC has carrier.  Three seeds.
+    for (uint64_t seed : {0xA5A5A5A55A5A5A5Aull, 0x0123456789ABCDEFull, 0x7777000011112222ull}) {
+        Fixture f;
+        f.cfg.monitor_tick_ns = 1000000;
+        f.cfg.lldp_tx_interval_ns = 3600LL * 1000000000LL;
+        const std::vector<std::string> nics = {"ens0", "ens1", "ens2"};
+        std::map<std::string, int> idx = {{"ens0", 10}, {"ens1", 11}, {"ens2", 12}};
+        std::map<std::string, bool> carrier;
+        std::map<std::string, int> host;  // the switch end is 10.20k.0.(4*host+2), ours +1 (^3)
+        auto src = f.all_valid();
+        ScriptedLldp* lldp_src = src.get();
+        std::map<std::string, lldp::Frame> frames;
+        auto describe = [&](const std::string& n) {
+            const int k = int(n.back() - '0');
+            auto fr = sw(strfmt("02:aa:00:00:00:0%d", k).c_str(),
+                         strfmt("no-alert 10.20%d.0.%d/30", k, 4 * host[n] + 2).c_str());
+            frames[n] = fr;
+            if (carrier[n]) lldp_src->frames[n] = fr;
+        };
+        for (const auto& n : nics) {
+            carrier[n] = true;
+            host[n] = 1;
+            describe(n);
+        }
+        uint64_t rng = seed;
+        auto next = [&] {
+            rng ^= rng << 13;
+            rng ^= rng >> 7;
+            rng ^= rng << 17;
+            return rng;
+        };
+        Pipe stop;
+        agent::Agent a(f.cfg, f.ops, std::move(src), f.nm());
+        int checked = 0, mismatches = 0, labelled_states = 0, readdressed = 0;
+        std::string first_bad;
+        a.on_monitor_tick = [&](int tick) {
+            if (tick % 2 == 0) {
+                bool want = std::all_of(nics.begin(), nics.end(), [&](const std::string& n) { return carrier[n]; });
+                bool label = path_exists(f.cfg.labels.path());
+                std::string bad;
+                if (label != want) bad = strfmt("label %d, want %d", label, want);
+                for (const auto& n : nics) {
+                    if (!carrier[n]) continue;
+                    const int k = int(n.back() - '0');
+                    const std::string expect = strfmt("10.20%d.0.%d/30", k, 4 * host[n] + 1);
+                    std::vector<std::string> have;
+                    for (const auto& x : f.ops.addrs)
+                        if (x.ifindex == idx[n]) have.push_back(x.prefix().str());
+                    if (have != std::vector<std::string>{expect}) bad += " " + n + " holds " + join(have, ",") + " not " + expect;
+                }
+                ++checked;
+                labelled_states += want;
+                if (!bad.empty()) {
+                    if (!mismatches) first_bad = strfmt("tick %d:", tick) + bad;
+                    ++mismatches;
+                }
+                if (tick >= 400) stop.fire();
+                return;
+            }
+            const std::string& n = nics[next() % nics.size()];
+            if (next() % 3 == 0) {  // the switch port is re-addressed
+                host[n] = 1 + int(next() % 8);
+                ++readdressed;
+                describe(n);
+            } else {
+                carrier[n] = !carrier[n];
+                if (carrier[n])
+                    lldp_src->frames[n] = frames[n];
+                else
+                    lldp_src->frames.erase(n);
+                f.ops.set_carrier(n, carrier[n]);
+            }
+        };
+        a.run(stop.fd[0]);
+        if (mismatches) fprintf(stderr, "seed %llx, %d mismatches, first %s\n", (unsigned long long)seed, mismatches,
+                                first_bad.c_str());
+        CHECK_EQ(mismatches, 0);
+        CHECK_EQ(checked, 201);
+        CHECK(labelled_states > 0 && labelled_states < checked);
+        CHECK(readdressed > 10);
+    }
+}
+
 TEST(agent_firmware_lldp_records_of_nics_no_longer_selected_are_not_lost) {
     // The record an earlier agent left names ens0 (still selected), old0 (dropped from the
     // policy's interface list) and gone0 (renamed: unreachable).  old0 is not ours any more, so its
