@@ -173,6 +173,10 @@ def openapi_schema() -> dict:
             "keepConfigOnRestart": {"description": "As amdScaleOut.keepConfigOnRestart, for the host NICs.",
                                     "type": "boolean"},
             "checkPeerMtu": {"description": "As amdScaleOut.checkPeerMtu, for the host NICs.", "type": "boolean"},
+            "includeGpuRails": {"description": "Let discovery take the NICs next to the GPUs (within a PCIe switch of an\n"
+                                               "amdgpu function), which an amd-so policy owns; only for nodes that run\n"
+                                               "no amd-so policy.",
+                                "type": "boolean"},
         },
         "required": ["layer"],
     }

@@ -235,6 +235,7 @@ class HostNicSpec:
     lldpWait: str = ""
     keepConfigOnRestart: bool = False
     checkPeerMtu: Optional[bool] = None
+    includeGpuRails: bool = False  # discovery may take the NICs next to the GPUs (no amd-so policy)
     extra: Dict[str, Any] = field(default_factory=dict)
 
     def to_dict(self) -> dict:
@@ -256,6 +257,8 @@ class HostNicSpec:
             d["keepConfigOnRestart"] = True
         if self.checkPeerMtu is not None:
             d["checkPeerMtu"] = self.checkPeerMtu
+        if self.includeGpuRails:
+            d["includeGpuRails"] = True
         d.update(copy.deepcopy(self.extra))
         return d
 
@@ -268,7 +271,8 @@ class HostNicSpec:
                 driverImage=d.pop("driverImage", "") or "", verifyPeers=bool(d.pop("verifyPeers", False)),
                 lldpWait=d.pop("lldpWait", "") or "",
                 keepConfigOnRestart=bool(d.pop("keepConfigOnRestart", False)),
-                checkPeerMtu=d.pop("checkPeerMtu", None))
+                checkPeerMtu=d.pop("checkPeerMtu", None),
+                includeGpuRails=bool(d.pop("includeGpuRails", False)))
         s.extra = d
         return s
 

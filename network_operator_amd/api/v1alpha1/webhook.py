@@ -339,6 +339,11 @@ def validate_host_nic_spec(s: Optional[T.HostNicSpec]) -> List[str]:
         warnings.append("hostNic: no interfaces or nicDrivers given; every RDMA NIC of the default driver list "
                         "that is neither a GPU's scale-out rail nor the node's own NIC (default route, non-/30 "
                         "address) will be configured")
+    if s.includeGpuRails and s.interfaces:
+        warnings.append("hostNic.includeGpuRails has no effect with interfaces (the named NICs are taken as named)")
+    elif s.includeGpuRails:
+        warnings.append("hostNic.includeGpuRails: the GPUs' scale-out NICs are configured by this policy; an amd-so "
+                        "policy on the same nodes would find them taken (its agent waits for their NIC locks)")
     return warnings
 
 

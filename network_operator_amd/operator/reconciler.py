@@ -278,6 +278,8 @@ def host_nic_agent_args(p: T.NetworkClusterPolicy) -> List[str]:
         args.append("--interfaces=" + ",".join(hn.interfaces))
     if hn.nicDrivers:
         args.append("--nic-drivers=" + ",".join(hn.nicDrivers))
+    if hn.includeGpuRails and not hn.interfaces:
+        args.append("--rdma-include-gpu-rails")
     if hn.checkPeerMtu is False and hn.layer == "L3":
         args.append("--check-peer-mtu=false")
     if hn.keepConfigOnRestart:

@@ -434,7 +434,7 @@ _AMD_VALUES = {
 _HOST_NIC_VALUES = {
     "enabled": True, "mode": "L3", "mtu": 4000, "nicDrivers": ["bnxt_en"], "driverImage": "reg/kmd:1",
     "interfaces": ["ens9np0"], "disableNetworkManager": True, "verifyPeers": True, "lldpWait": "45s",
-    "checkPeerMtu": False, "keepConfigOnRestart": True,
+    "checkPeerMtu": False, "keepConfigOnRestart": True, "includeGpuRails": True,
 }
 
 
@@ -469,8 +469,9 @@ def test_every_policy_field_is_settable_from_the_chart_and_documented():
         assert getattr(hn, k) == v, k
     assert not hn.extra
 
-    for p in seeded.values():
-        assert W.validate_create(p) == [], p.name
+    assert W.validate_create(seeded["netconf-amd-scale-out"]) == []
+    # (includeGpuRails next to interfaces only draws the "no effect" warning)
+    assert [w for w in W.validate_create(seeded["netconf-amd-host-nic"]) if "includeGpuRails" not in w] == []
 
     # Defaults render the policy the CRD defaults describe: no optional field forced on.
     plain = yaml.safe_load(_configmap_text(helm_template(CHART, {"config": {"amd": {"enabled": True},
@@ -481,7 +482,7 @@ def test_every_policy_field_is_settable_from_the_chart_and_documented():
         assert k not in so, k
     hn = plain["policies"][1]["spec"]["hostNic"]
     for k in ("interfaces", "disableNetworkManager", "verifyPeers", "lldpWait", "checkPeerMtu",
-              "keepConfigOnRestart"):
+              "keepConfigOnRestart", "includeGpuRails"):
         assert k not in hn, k
 
     readme = (CHART / "README.md").read_text()

@@ -1189,6 +1189,28 @@ def test_dcbx_hand_over_and_peer_mtu_check_are_policy_fields():
     assert not CRD.validate(p.to_dict()) and not CRD.validate(h.to_dict())
 
 
+def test_host_nic_policy_can_take_the_gpu_rails_only_on_request():
+    """host-nic discovery leaves the GPUs' scale-out NICs to amd-so; hostNic.includeGpuRails
+    (nodes without an amd-so policy) hands the agent --rdma-include-gpu-rails.  Named interfaces
+    are taken as named, so the field is then moot and the webhook says so."""
+    from network_operator_amd.api.v1alpha1 import crd as CRD
+    from network_operator_amd.api.v1alpha1 import types as T
+    from network_operator_amd.api.v1alpha1 import webhook as W
+    from network_operator_amd.operator.reconciler import host_nic_agent_args
+
+    h = T.new_host_nic_policy("h", layer="L2", nicDrivers=["mlx5_core"])
+    assert "--rdma-include-gpu-rails" not in host_nic_agent_args(h)
+    h.spec.hostNic.includeGpuRails = True
+    args = host_nic_agent_args(h)
+    assert "--nic-discovery=rdma" in args and "--rdma-include-gpu-rails" in args
+    assert T.NetworkClusterPolicy.from_dict(h.to_dict()).spec.hostNic.includeGpuRails is True
+    assert not CRD.validate(h.to_dict())
+    assert any("amd-so policy on the same nodes" in w for w in W.validate_create(h))
+    h.spec.hostNic.interfaces = ["ens9np0"]
+    assert "--rdma-include-gpu-rails" not in host_nic_agent_args(h)
+    assert any("no effect with interfaces" in w for w in W.validate_create(h))
+
+
 def test_stalled_lease_renewal_stops_the_leader_before_anyone_else_can_lead():
     """the leader's Lease PUTs stall for 20 s (a wedged API path).  Its renewal
     attempts are bounded by the renew deadline, so it cancels its work within renew_deadline of
