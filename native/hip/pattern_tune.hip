@@ -12,6 +12,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 
 #define CHECK(x)                                                                           \
     do {                                                                                   \
@@ -105,10 +106,32 @@ __device__ __forceinline__ uint32_t bf16x2_of_ints(int lo, int hi) {
     return (__float_as_uint(float(lo)) >> 16) | (__float_as_uint(float(hi)) & 0xffff0000u);
 }
 
-template <int V, int UNROLL, bool NT>
+// The index space of one workgroup: grid-strided over the whole buffer (CHUNK = 0), or one
+// contiguous chunk per workgroup, strided by the workgroup (CHUNK = 1).
+template <bool CHUNK>
+struct Walk {
+    uint64_t first, end, stride;
+    __device__ explicit Walk(uint64_t n_vec) {
+        if (CHUNK) {
+            const uint64_t per = ((n_vec + gridDim.x - 1) / gridDim.x + kThreads - 1) / kThreads * kThreads;
+            const uint64_t b = uint64_t(blockIdx.x) * per;
+            first = b + threadIdx.x;
+            end = b + per < n_vec ? b + per : n_vec;
+            stride = kThreads;
+        } else {
+            first = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
+            end = n_vec;
+            stride = uint64_t(gridDim.x) * kThreads;
+        }
+    }
+};
+
+template <int V, int UNROLL, bool NT, bool CHUNK = false>
 __global__ __launch_bounds__(kThreads) void fill_k(u32x4* __restrict__ out, uint64_t n_vec, uint32_t seed, int n) {
-    const uint64_t stride = uint64_t(gridDim.x) * kThreads;
-    for (uint64_t v0 = uint64_t(blockIdx.x) * kThreads + threadIdx.x; v0 < n_vec; v0 += stride * UNROLL) {
+    const Walk<CHUNK> w8(n_vec);
+    const uint64_t stride = w8.stride;
+    n_vec = w8.end;
+    for (uint64_t v0 = w8.first; v0 < n_vec; v0 += stride * UNROLL) {
 #pragma unroll
         for (int u = 0; u < UNROLL; ++u) {
             const uint64_t v = v0 + u * stride;
@@ -130,13 +153,15 @@ __global__ __launch_bounds__(kThreads) void fill_k(u32x4* __restrict__ out, uint
     }
 }
 
-template <int V, int UNROLL, bool NT>
+template <int V, int UNROLL, bool NT, bool CHUNK = false>
 __global__ __launch_bounds__(kThreads) void verify_k(const u32x4* __restrict__ in, uint64_t n_vec, uint32_t seed, int n,
                                                      unsigned long long* __restrict__ errors) {
     __shared__ unsigned int wave_err[kThreads / 64];
-    const uint64_t stride = uint64_t(gridDim.x) * kThreads;
+    const Walk<CHUNK> w8(n_vec);
+    const uint64_t stride = w8.stride;
+    n_vec = w8.end;
     unsigned int err = 0;
-    for (uint64_t v0 = uint64_t(blockIdx.x) * kThreads + threadIdx.x; v0 < n_vec; v0 += stride * UNROLL) {
+    for (uint64_t v0 = w8.first; v0 < n_vec; v0 += stride * UNROLL) {
         u32x4 q[UNROLL];
 #pragma unroll
         for (int u = 0; u < UNROLL; ++u) {
@@ -261,38 +286,39 @@ struct Ctx {
     int cus;
 };
 
-template <int V, int U, bool NT>
+template <int V, int U, bool NT, bool CHUNK = false>
 int run(Ctx& c, int n, int per_cu, int iters) {
     const int blocks = c.cus * per_cu;
     const uint32_t seed = 2024;
     // correctness first (v2; v1 is the old definition, checked against itself)
-    hipLaunchKernelGGL((fill_k<V, U, NT>), dim3(blocks), dim3(kThreads), 0, 0, c.buf, c.n_vec, seed, n);
+    hipLaunchKernelGGL((fill_k<V, U, NT, CHUNK>), dim3(blocks), dim3(kThreads), 0, 0, c.buf, c.n_vec, seed, n);
     CHECK(hipMemset(c.err, 0, 8));
-    hipLaunchKernelGGL((verify_k<V, U, NT>), dim3(blocks), dim3(kThreads), 0, 0, c.buf, c.n_vec, seed, n, c.err);
+    hipLaunchKernelGGL((verify_k<V, U, NT, CHUNK>), dim3(blocks), dim3(kThreads), 0, 0, c.buf, c.n_vec, seed, n, c.err);
     unsigned long long e0 = 0, e1 = 0;
     CHECK(hipMemcpy(&e0, c.err, 8, hipMemcpyDeviceToHost));
     uint16_t bad = 0x3f00;  // 0.5: never a pattern sum (integers), so exactly one mismatch
     CHECK(hipMemcpy(reinterpret_cast<uint16_t*>(c.buf) + 12345, &bad, 2, hipMemcpyHostToDevice));
     CHECK(hipMemset(c.err, 0, 8));
-    hipLaunchKernelGGL((verify_k<V, U, NT>), dim3(blocks), dim3(kThreads), 0, 0, c.buf, c.n_vec, seed, n, c.err);
+    hipLaunchKernelGGL((verify_k<V, U, NT, CHUNK>), dim3(blocks), dim3(kThreads), 0, 0, c.buf, c.n_vec, seed, n, c.err);
     CHECK(hipMemcpy(&e1, c.err, 8, hipMemcpyDeviceToHost));
     float ms_fill = 0, ms_verify = 0;
     CHECK(hipEventRecord(c.a));
     for (int i = 0; i < iters; ++i)
-        hipLaunchKernelGGL((fill_k<V, U, NT>), dim3(blocks), dim3(kThreads), 0, 0, c.buf, c.n_vec, seed, n);
+        hipLaunchKernelGGL((fill_k<V, U, NT, CHUNK>), dim3(blocks), dim3(kThreads), 0, 0, c.buf, c.n_vec, seed, n);
     CHECK(hipEventRecord(c.b));
     CHECK(hipEventSynchronize(c.b));
     CHECK(hipEventElapsedTime(&ms_fill, c.a, c.b));
     CHECK(hipEventRecord(c.a));
     for (int i = 0; i < iters; ++i)
-        hipLaunchKernelGGL((verify_k<V, U, NT>), dim3(blocks), dim3(kThreads), 0, 0, c.buf, c.n_vec, seed, n, c.err);
+        hipLaunchKernelGGL((verify_k<V, U, NT, CHUNK>), dim3(blocks), dim3(kThreads), 0, 0, c.buf, c.n_vec, seed, n, c.err);
     CHECK(hipEventRecord(c.b));
     CHECK(hipEventSynchronize(c.b));
     CHECK(hipEventElapsedTime(&ms_verify, c.a, c.b));
     const double bytes = double(c.n_vec) * 16;
-    std::printf("{\"pattern\":\"v%d\",\"unroll\":%d,\"nt\":%d,\"wg_per_cu\":%d,\"ranks\":%d,\"bytes\":%.0f,"
-                "\"fill_TBps\":%.3f,\"verify_TBps\":%.3f,\"errors_clean\":%llu,\"errors_one_flip\":%llu}\n",
-                V, U, int(NT), per_cu, n, bytes, bytes * iters / (ms_fill * 1e-3) / 1e12,
+    std::printf("{\"pattern\":\"v%d\",\"unroll\":%d,\"nt\":%d,\"chunk\":%d,\"wg_per_cu\":%d,\"ranks\":%d,"
+                "\"bytes\":%.0f,\"fill_TBps\":%.3f,\"verify_TBps\":%.3f,\"errors_clean\":%llu,"
+                "\"errors_one_flip\":%llu}\n",
+                V, U, int(NT), int(CHUNK), per_cu, n, bytes, bytes * iters / (ms_fill * 1e-3) / 1e12,
                 bytes * iters / (ms_verify * 1e-3) / 1e12, e0, e1);
     std::fflush(stdout);
     return 0;
@@ -309,6 +335,19 @@ int main(int argc, char** argv) {
     CHECK(hipEventCreate(&c.b));
     CHECK(hipDeviceGetAttribute(&c.cus, hipDeviceAttributeMultiprocessorCount, 0));
     const int iters = 10;
+    const std::string mode = argc > 2 ? argv[2] : "all";  // all | ceilings | chunk
+    if (mode == "chunk") {
+        // Contiguous chunk per workgroup against the grid-stride walk, v2 pattern.
+        for (int n : {1, 8}) {
+            for (int pc : {2, 4, 8, 16}) {
+                if (run<2, 1, false, false>(c, n, pc, iters) || run<2, 1, false, true>(c, n, pc, iters) ||
+                    run<2, 1, true, false>(c, n, pc, iters) || run<2, 1, true, true>(c, n, pc, iters) ||
+                    run<2, 2, true, true>(c, n, pc, iters))
+                    return 1;
+            }
+        }
+        return 0;
+    }
     for (int pc : {2, 4, 8, 16}) {
         for (int nt : {0, 1}) {
             const int blocks = c.cus * pc;
@@ -343,7 +382,7 @@ int main(int argc, char** argv) {
         store_shape<4, false, true>(c.buf, c.n_vec, c.cus, c.a, c.b) || store_shape<4, true, true>(c.buf, c.n_vec, c.cus, c.a, c.b) ||
         store_shape<8, true, true>(c.buf, c.n_vec, c.cus, c.a, c.b) || store_shape<8, false, true>(c.buf, c.n_vec, c.cus, c.a, c.b))
         return 1;
-    if (argc > 2) return 0;  // ceilings only
+    if (mode == "ceilings") return 0;
     for (int n : {1, 8}) {
         if (run<1, 1, false>(c, n, 8, iters)) return 1;
         for (int pc : {8, 16}) {
