@@ -278,6 +278,43 @@ int store_shape(u32x4* buf, uint64_t n_vec, int cus, hipEvent_t a, hipEvent_t b)
     return 0;
 }
 
+// Device copy (the xGMI probe's and the all-gather's shape), grid-strided or one contiguous chunk
+// per workgroup, UNROLL 16-byte loads in flight per lane.
+template <int UNROLL, bool CHUNK>
+__global__ __launch_bounds__(kThreads) void copy_k(const u32x4* __restrict__ src, u32x4* __restrict__ dst, uint64_t n_vec) {
+    const Walk<CHUNK> w8(n_vec);
+    for (uint64_t v0 = w8.first; v0 < w8.end; v0 += w8.stride * UNROLL) {
+        u32x4 q[UNROLL];
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u)
+            if (v0 + u * w8.stride < w8.end) q[u] = src[v0 + u * w8.stride];
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u)
+            if (v0 + u * w8.stride < w8.end) dst[v0 + u * w8.stride] = q[u];
+    }
+}
+
+template <int UNROLL, bool CHUNK>
+int copy_shape(u32x4* buf, uint64_t n_vec, int cus, hipEvent_t a, hipEvent_t b) {
+    const uint64_t half = n_vec / 2;
+    for (int pc : {2, 4, 8, 16}) {
+        const int blocks = cus * pc, iters = 10;
+        float ms = 0;
+        hipLaunchKernelGGL((copy_k<UNROLL, CHUNK>), dim3(blocks), dim3(kThreads), 0, 0, buf, buf + half, half);
+        CHECK(hipEventRecord(a));
+        for (int i = 0; i < iters; ++i)
+            hipLaunchKernelGGL((copy_k<UNROLL, CHUNK>), dim3(blocks), dim3(kThreads), 0, 0, buf, buf + half, half);
+        CHECK(hipEventRecord(b));
+        CHECK(hipEventSynchronize(b));
+        CHECK(hipEventElapsedTime(&ms, a, b));
+        std::printf("{\"copy\":1,\"unroll\":%d,\"chunk\":%d,\"wg_per_cu\":%d,\"bytes\":%.0f,\"copy_TBps\":%.3f,"
+                    "\"traffic_TBps\":%.3f}\n", UNROLL, int(CHUNK), pc, double(half) * 16,
+                    double(half) * 16 * iters / (ms * 1e-3) / 1e12, 2 * double(half) * 16 * iters / (ms * 1e-3) / 1e12);
+        std::fflush(stdout);
+    }
+    return 0;
+}
+
 struct Ctx {
     u32x4* buf;
     uint64_t n_vec;
@@ -335,7 +372,12 @@ int main(int argc, char** argv) {
     CHECK(hipEventCreate(&c.b));
     CHECK(hipDeviceGetAttribute(&c.cus, hipDeviceAttributeMultiprocessorCount, 0));
     const int iters = 10;
-    const std::string mode = argc > 2 ? argv[2] : "all";  // all | ceilings | chunk
+    const std::string mode = argc > 2 ? argv[2] : "all";  // all | ceilings | chunk | copy
+    if (mode == "copy") {
+        return copy_shape<1, false>(c.buf, c.n_vec, c.cus, c.a, c.b) || copy_shape<1, true>(c.buf, c.n_vec, c.cus, c.a, c.b) ||
+               copy_shape<2, false>(c.buf, c.n_vec, c.cus, c.a, c.b) || copy_shape<2, true>(c.buf, c.n_vec, c.cus, c.a, c.b) ||
+               copy_shape<4, true>(c.buf, c.n_vec, c.cus, c.a, c.b);
+    }
     if (mode == "chunk") {
         // Contiguous chunk per workgroup against the grid-stride walk, v2 pattern.
         for (int n : {1, 8}) {
