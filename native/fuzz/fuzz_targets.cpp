@@ -97,6 +97,11 @@ extern "C" int LLVMFuzzerTestOneInput(const uint8_t* data, size_t size) {
         (void)nl::parse_route(h);
     } catch (const std::exception&) {
     }
+    h->nlmsg_type = RTM_NEWADDR;  // as an address (ifaddrmsg + attributes, IPv4 or IPv6)
+    try {
+        (void)nl::parse_addr(h);
+    } catch (const std::exception&) {
+    }
     h->nlmsg_type = RTM_GETDCB;  // the same bytes as a DCB netlink reply (dcbmsg + attributes)
     try {
         (void)nl::parse_dcb_u8(h, DCB_ATTR_DCBX);

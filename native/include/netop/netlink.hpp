@@ -207,6 +207,9 @@ LinkInfo parse_link(const nlmsghdr* h);
 // Parses an RTM_NEWROUTE payload (IPv4 fields; dst_len, table, type, protocol, output interfaces
 // of any family, RTA_MULTIPATH next hops included).  Bounds-checked like parse_link.
 RouteInfo parse_route(const nlmsghdr* h);
+// Parses an RTM_NEWADDR payload: IPv4 fields, or for AF_INET6 the address in text form
+// (address6).  Bounds-checked like parse_link.
+AddrInfo parse_addr(const nlmsghdr* h);
 // IFLA_STATS64 (else IFLA_STATS) of an RTM_NEWLINK message; nullopt when it carries neither.
 std::optional<LinkStats> parse_link_stats(const nlmsghdr* h);
 // The NLMSGERR_ATTR_MSG string of an extended ACK (NLMSG_ERROR with NLM_F_ACK_TLVS); "" if

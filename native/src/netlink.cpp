@@ -333,7 +333,7 @@ LinkInfo parse_link(const nlmsghdr* h) {
     return li;
 }
 
-static AddrInfo parse_addr(const nlmsghdr* h) {
+AddrInfo parse_addr(const nlmsghdr* h) {
     AddrInfo ai;
     const auto* ifa = fixed_header<ifaddrmsg>(h, "address");
     ai.ifindex = int(ifa->ifa_index);

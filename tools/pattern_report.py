@@ -3,7 +3,7 @@ ranks in the pattern, kernel) the median kernel time and HBM rate from the kerne
 from the PMC passes the HBM bytes per call (FETCH_SIZE doubled: gfx950 reports half of a wide
 streaming read, MI355X_MICROARCH.md) and the VALU instructions per 16-byte vector.
 
-    python tools/pattern_report.py gpurun_out > profiles/r4_pattern_kernels.json
+    python tools/pattern_report.py gpurun_out [TAG] > profiles/r4_pattern_kernels.json
 """
 import csv
 import json
@@ -29,9 +29,9 @@ def _runs(rows):
     return out
 
 
-def main(root: str) -> dict:
+def main(root: str, tag_prefix: str = "r4") -> dict:
     root = Path(root)
-    trace = list(csv.DictReader(open(root / "r4_prof_pattern" / "kern_kernel_trace.csv")))
+    trace = list(csv.DictReader(open(root / f"{tag_prefix}_prof_pattern" / "kern_kernel_trace.csv")))
     runs = _runs(trace)
     assert [k for k, _ in runs] == [k for _, _, k in SEQ], [k for k, _ in runs]
     table = []
@@ -42,7 +42,7 @@ def main(root: str) -> dict:
                       "TBps": round(size / ns / 1e3, 2)})
     for tag, counters in (("FETCH_SIZE", ["FETCH_SIZE"]), ("WRITE_SIZE", ["WRITE_SIZE"]),
                           ("SQ_INSTS_VALU", ["SQ_INSTS_VALU", "SQ_WAVES", "SQ_INSTS_SALU", "GRBM_GUI_ACTIVE"])):
-        f = root / f"r4_pmc_{tag}" / "pmc_counter_collection.csv"
+        f = root / f"{tag_prefix}_pmc_{tag}" / "pmc_counter_collection.csv"
         if not f.exists():
             continue
         rows = list(csv.DictReader(open(f)))
@@ -75,4 +75,5 @@ def main(root: str) -> dict:
 
 
 if __name__ == "__main__":
-    print(json.dumps(main(sys.argv[1] if len(sys.argv) > 1 else "gpurun_out"), indent=1))
+    print(json.dumps(main(sys.argv[1] if len(sys.argv) > 1 else "gpurun_out", sys.argv[2] if len(sys.argv) > 2 else "r4"),
+                     indent=1))
