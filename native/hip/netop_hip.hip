@@ -6,7 +6,8 @@
 //   * netop_fill_pattern / netop_verify_sum — bf16 all-reduce correctness check.  Each rank
 //     fills a deterministic small-integer pattern (exact in bf16 for any reduction order);
 //     the verifier recomputes Σ_ranks pattern and counts mismatches.  16-byte vector
-//     accesses (8 x bf16 per lane), grid-stride, one atomic per workgroup.
+//     accesses (8 x bf16 per lane), one contiguous chunk per workgroup, one atomic per
+//     workgroup.
 //   * netop_copy — 16-B/lane streaming copy used by the xGMI link probe: with peer access
 //     enabled the loads of a peer pointer travel over the xGMI link to that peer, so one
 //     copy per peer on its own stream drives all 7 links of an MI355X concurrently.
@@ -82,20 +83,41 @@ __device__ __forceinline__ void group_sum(uint64_t g, uint32_t seed, int rank_lo
     }
 }
 
+// The vectors of one workgroup: one contiguous chunk of the buffer (a multiple of the workgroup
+// size), the workgroup's lanes striding through it together.  pattern_tune.hip ("chunk" mode,
+// profiles/r4_pattern_tune_chunk.jsonl): against a grid-stride walk over the whole buffer the
+// HBM writes of the fill run 4.6 -> 5.6 TB/s (1 GiB, 16 workgroups per CU), the one-rank verify
+// 6.1 -> 6.5 TB/s; the copy kernel below stays grid-strided (there the chunked walk was slower).
+// In the library (profiles/r4_pattern_kernels_chunk.json, rocprofv3): 1 GiB fill 4.44 -> 5.34
+// TB/s at one rank and 4.54 -> 4.89 at eight, one-rank verify 5.78 -> 6.23; the eight-rank
+// verify is ALU-bound and reads the same with either walk (4.6-4.85 TB/s from box to box).
+struct ChunkWalk {
+    uint64_t first, end;
+    __device__ explicit ChunkWalk(uint64_t n_vec) {
+        const uint64_t per = ((n_vec + gridDim.x - 1) / gridDim.x + kThreads - 1) / kThreads * kThreads;
+        const uint64_t b = uint64_t(blockIdx.x) * per;
+        first = b + threadIdx.x;
+        end = b + per < n_vec ? b + per : n_vec;
+    }
+};
+
 // Element e of the buffer holds the pattern sum of element e + elem_offset: the offset lets a
 // chunk of a collective's output be checked against the slice of the global pattern it came
 // from.  elem_offset is a multiple of 8, so vector v is group (elem_offset / 8 + v).
 __global__ __launch_bounds__(kThreads) void fill_kernel(uint4* __restrict__ out, uint64_t n_vec, uint32_t seed, int rank_lo,
                                                         int n_ranks, uint64_t elem_offset) {
-    const uint64_t stride = uint64_t(gridDim.x) * kThreads;
+    const ChunkWalk walk(n_vec);
     const uint64_t g0 = elem_offset >> 3;
-    for (uint64_t v = uint64_t(blockIdx.x) * kThreads + threadIdx.x; v < n_vec; v += stride) {
+    u32x4* __restrict__ vout = reinterpret_cast<u32x4*>(out);
+    for (uint64_t v = walk.first; v < walk.end; v += kThreads) {
         int s[8];
         group_sum(g0 + v, seed, rank_lo, n_ranks, s);
-        uint32_t w[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) w[k] = uint32_t(int_to_bf16(s[2 * k])) | (uint32_t(int_to_bf16(s[2 * k + 1])) << 16);
-        out[v] = make_uint4(w[0], w[1], w[2], w[3]);
+        u32x4 w;
+        w.x = uint32_t(int_to_bf16(s[0])) | (uint32_t(int_to_bf16(s[1])) << 16);
+        w.y = uint32_t(int_to_bf16(s[2])) | (uint32_t(int_to_bf16(s[3])) << 16);
+        w.z = uint32_t(int_to_bf16(s[4])) | (uint32_t(int_to_bf16(s[5])) << 16);
+        w.w = uint32_t(int_to_bf16(s[6])) | (uint32_t(int_to_bf16(s[7])) << 16);
+        __builtin_nontemporal_store(w, &vout[v]);  // streamed once; read back by another kernel
     }
 }
 
@@ -103,11 +125,11 @@ __global__ __launch_bounds__(kThreads) void verify_kernel(const uint4* __restric
                                                           int rank_lo, int n_ranks, uint64_t elem_offset,
                                                           unsigned long long* __restrict__ errors) {
     __shared__ unsigned int wave_err[kThreads / 64];
-    const uint64_t stride = uint64_t(gridDim.x) * kThreads;
+    const ChunkWalk walk(n_vec);
     const uint64_t g0 = elem_offset >> 3;
     unsigned int err = 0;
     const u32x4* __restrict__ vin = reinterpret_cast<const u32x4*>(in);
-    for (uint64_t v = uint64_t(blockIdx.x) * kThreads + threadIdx.x; v < n_vec; v += stride) {
+    for (uint64_t v = walk.first; v < walk.end; v += kThreads) {
         // Read once: nontemporal (pattern_tune.hip: 5.6 -> 6.1 TB/s at one rank).
         const u32x4 q = __builtin_nontemporal_load(&vin[v]);
         uint32_t w[4] = {q.x, q.y, q.z, q.w};
@@ -254,7 +276,7 @@ int netop_fill_pattern_at(void* buf, uint64_t n_elems, uint32_t seed, int rank_l
         return int(hipErrorInvalidValue);
     uint64_t nv = n_elems / 8;
     if (nv == 0) return int(hipSuccess);
-    hipLaunchKernelGGL(fill_kernel, dim3(grid_for(nv)), dim3(kThreads), 0, stream, static_cast<uint4*>(buf), nv, seed,
+    hipLaunchKernelGGL(fill_kernel, dim3(grid_for(nv, 16)), dim3(kThreads), 0, stream, static_cast<uint4*>(buf), nv, seed,
                        rank_lo, n_ranks, elem_offset);
     return int(hipGetLastError());
 }
@@ -266,8 +288,7 @@ int netop_verify_pattern_at(const void* buf, uint64_t n_elems, uint32_t seed, in
         return int(hipErrorInvalidValue);
     uint64_t nv = n_elems / 8;
     if (nv == 0) return int(hipSuccess);
-    // Several ranks in the expectation: ALU-heavier, more waves per CU hide it (16 vs 8 per CU).
-    hipLaunchKernelGGL(verify_kernel, dim3(grid_for(nv, n_ranks > 1 ? 16 : 8)), dim3(kThreads), 0, stream,
+    hipLaunchKernelGGL(verify_kernel, dim3(grid_for(nv, 16)), dim3(kThreads), 0, stream,
                        static_cast<const uint4*>(buf), nv, seed, rank_lo, n_ranks, elem_offset, errors);
     return int(hipGetLastError());
 }

@@ -54,6 +54,30 @@ def test_expected_sum_and_verify(cuda_device):
         assert hip.verify_sum(t, 5, world) == 2
 
 
+def test_pattern_kernels_cover_every_element_across_workgroup_chunks(cuda_device):
+    """The fill / verify walk gives each workgroup one contiguous chunk (a multiple of 256
+    vectors) of a buffer larger than one chunk per workgroup: every element is written once with
+    the right value, and a wrong element on either side of a chunk edge, or the very last one,
+    is counted."""
+    import torch
+
+    from network_operator_amd.ops import hip
+
+    nv = 3 * 4096 * 256 + 37  # vectors: more than 16 workgroups per CU x 256 lanes can take at once
+    n = nv * 8
+    t = torch.full((n,), float("nan"), dtype=torch.bfloat16, device=cuda_device)
+    hip.fill_expected_sum(t, 11, 3)
+    ref = sum(_ref_pattern(n, 11, r) for r in range(3))
+    torch.testing.assert_close(t.float().cpu(), ref, rtol=0, atol=0)
+    assert hip.verify_sum(t, 11, 3) == 0
+    cus = torch.cuda.get_device_properties(cuda_device).multi_processor_count
+    per = -(-(-(-nv // min(cus * 16, -(-nv // 256)))) // 256) * 256  # vectors per workgroup chunk
+    flips = sorted({8 * per - 1, 8 * per, 16 * per - 1, 16 * per, n - 1})
+    for i in flips:
+        t[i] += 1
+    assert hip.verify_sum(t, 11, 3) == len(flips)
+
+
 def test_copy_matches_torch(cuda_device):
     import torch
 
