@@ -240,8 +240,8 @@ def dump_verdict(n: int, with_file: Optional[dict], defaults: Optional[dict]) ->
 
     * ``ok`` — every GPU of the dump has >= n-1 xGMI peers among the job's GPUs (and the dump
       holds all n GPUs), and the file did not cost a link RCCL sees without it.
-    * ``failed`` — fewer, while RCCL without the file sees more (the file lost links), or the
-      dump is missing / shows fewer than n-1 with xGMI elements present.
+    * ``failed`` — fewer, while RCCL without the file sees more (the file lost links:
+      ``file_blamed``), or the dump is missing / shows fewer than n-1 with xGMI elements present.
     * ``degraded`` — fewer than n-1, but the same without the file: the node's mesh, not the file.
     * ``unverifiable`` — RCCL's dump carries no ``<xgmi>`` elements with *or* without the file
       (this RCCL build records the links elsewhere): the file cannot be blamed, say so.
@@ -261,8 +261,9 @@ def dump_verdict(n: int, with_file: Optional[dict], defaults: Optional[dict]) ->
     if got >= need and (base is None or got >= base):
         return dict(out, status="ok")
     if base is not None and base > got:
-        return dict(out, status="failed", why=f"with the agent's file RCCL sees {got} xGMI peers per GPU (min), "
-                                              f"without it {base}: the file costs links")
+        return dict(out, status="failed", file_blamed=True,
+                    why=f"with the agent's file RCCL sees {got} xGMI peers per GPU (min), without it {base}: the "
+                        "file costs links")
     if with_file["xgmi_elements"] == 0 and (base is None or defaults.get("xgmi_elements", 0) == 0):
         return dict(out, status="unverifiable",
                     why="RCCL's topology dump has no <xgmi> elements with the agent's file, and "

@@ -360,8 +360,11 @@ def test_rccl_view_counts_xgmi_links_and_compares_ancestry():
     lost = dict(full, **{"0000:0a:00.0": ["0000:23:00.0"]})
     bad = FA.rccl_view(_dump(g, lost))
     verdict = FA.links_verdict(3, bad, v)
-    assert verdict["status"] == "failed" and "costs links" in verdict["why"]
-    assert FA.links_verdict(3, bad, None)["status"] == "failed"
+    assert verdict["status"] == "failed" and "costs links" in verdict["why"] and verdict["file_blamed"]
+    # fewer than n-1 with nothing to compare: reported failed, but the file is not blamed (the
+    # bench then keeps rc 0: its number is a real measurement of this fabric)
+    alone = FA.links_verdict(3, bad, None)
+    assert alone["status"] == "failed" and not alone.get("file_blamed")
     # the dump misses a GPU of the job
     assert FA.links_verdict(4, v, None)["status"] == "failed"
     # no <xgmi> elements at all, with and without the file: this RCCL records them elsewhere
