@@ -1036,6 +1036,22 @@ std::string Agent::render_metrics() const {
         o += strfmt("netop_agent_nic_configured{nic=\"%s\",gpu=\"%s\",rdma=\"%s\"} %d\n",
                     httpd::escape_label(n.ifname).c_str(), n.gpu_bdf.c_str(), n.rdma_dev.c_str(),
                     (n.configured && (cfg_.mode == "L3" || n.link.up())) ? 1 : 0);
+    if (!excluded_.empty()) {
+        // Discovered but left alone (the node's own NICs, another agent's rails): one series per
+        // NIC with the kind of reason, so a fleet view shows which nodes hold back which NICs.
+        metric("netop_agent_nic_left_alone", "gauge", "1 for a discovered NIC this agent does not configure, by reason");
+        for (const auto& [nic, why] : excluded_) {
+            const char* kind = why.find("scale-out rail") != std::string::npos    ? "gpu_rail"
+                               : why.find("default route") != std::string::npos   ? "default_route"
+                               : why.find("is a port of") != std::string::npos    ? "bond_or_bridge_port"
+                               : why.find(", which ") != std::string::npos        ? "stacked_device"
+                               : why.find("IPv6 address") != std::string::npos    ? "ipv6_address"
+                               : why.find("an address the agent") != std::string::npos ? "address"
+                               : why.find("has the route") != std::string::npos   ? "route"
+                                                                                  : "other";
+            o += strfmt("netop_agent_nic_left_alone{nic=\"%s\",reason=\"%s\"} 1\n", httpd::escape_label(nic).c_str(), kind);
+        }
+    }
     metric("netop_agent_nic_degraded", "gauge", "1 while the NIC has lost link after readiness");
     for (auto& n : nics_)
         o += strfmt("netop_agent_nic_degraded{nic=\"%s\"} %d\n", httpd::escape_label(n.ifname).c_str(), n.degraded ? 1 : 0);

@@ -2179,6 +2179,10 @@ TEST(agent_rdma_discovery_leaves_bond_ports_and_vlan_parents_the_node_uses_alone
                                                           "team: the node configures the master, not its ports)"));
         CHECK_EQ(ex[1].second, std::string("the node's own NIC: it carries ens1.100, which holds 10.0.100.5/24, an "
                                            "address the agent never assigns (it only uses /30s)"));
+        const std::string m = a.render_metrics();
+        CHECK(m.find(std::string("netop_agent_nic_left_alone{nic=\"ens0\",reason=\"") +
+                     (variant == 0 ? "default_route" : "bond_or_bridge_port") + "\"} 1") != std::string::npos);
+        CHECK(m.find("netop_agent_nic_left_alone{nic=\"ens1\",reason=\"stacked_device\"} 1") != std::string::npos);
         CHECK_EQ(f.ops.links["ens0"].mtu, 1500);
         CHECK_EQ(f.ops.links["ens1"].mtu, 1500);
 
