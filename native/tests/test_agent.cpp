@@ -1974,6 +1974,82 @@ TEST(agent_two_ports_describing_one_link_are_refused_and_named) {
     }
 }
 
+TEST(agent_l3_start_configures_exactly_the_nics_with_a_unique_valid_port_description) {
+    // Property of the L3 start (pipelined and not): six NICs, each with a random switch port --
+    // a unique valid /30, an unusable Port Description, a copy of an earlier port's description,
+    // or silence.  Exactly the NICs with a unique valid description (the first of a copied pair)
+    // hold their /30 and nothing else; every other NIC holds nothing; the exit error counts them.
+    uint64_t rng = 0xC0FFEE1234567ull;
+    auto next = [&] {
+        rng ^= rng << 13;
+        rng ^= rng >> 7;
+        rng ^= rng << 17;
+        return rng;
+    };
+    int runs = 0, mismatches = 0;
+    for (int round = 0; round < 24; ++round) {
+        const bool pipeline = round % 2 == 0;
+        Fixture f;
+        f.cfg.keep_running = false;
+        f.cfg.pipeline = pipeline;
+        f.cfg.wait_ns = 50000000;
+        std::vector<std::string> nics = {"ens0", "ens1", "ens2", "ens3", "ens4", "ens5"};
+        for (int k = 3; k < 6; ++k) f.ops.add_link(nics[size_t(k)], 10 + k, strfmt("02:00:00:00:00:1%d", k).c_str(), true);
+        f.cfg.interfaces = "ens0,ens1,ens2,ens3,ens4,ens5";
+        auto src = std::make_unique<ScriptedLldp>();
+        std::map<std::string, std::string> want;  // NIC -> the /30 it must hold
+        std::map<std::string, std::string> desc_owner;
+        for (int k = 0; k < 6; ++k) {
+            const std::string& n = nics[size_t(k)];
+            const std::string mac = strfmt("02:aa:00:00:00:%02d", k);
+            int kind = int(next() % 4);
+            if (kind == 2 && desc_owner.empty()) kind = 0;
+            if (kind == 0) {
+                const std::string d = strfmt("no-alert 10.%d.0.%d/30", 100 + round, 4 * k + 2);
+                src->frames[n] = sw(mac.c_str(), d.c_str());
+                want[n] = strfmt("10.%d.0.%d/30", 100 + round, 4 * k + 1);
+                desc_owner[d] = n;
+            } else if (kind == 1) {
+                src->frames[n] = sw(mac.c_str(), "no-alert not-an-address");
+            } else if (kind == 2) {
+                auto it = desc_owner.begin();
+                std::advance(it, long(next() % desc_owner.size()));
+                src->frames[n] = sw(mac.c_str(), it->first.c_str());
+            }  // kind 3: silent
+        }
+        agent::Agent a(f.cfg, f.ops, std::move(src), f.nm());
+        std::string err;
+        try {
+            a.run(-1);
+        } catch (const agent::AgentError& e) {
+            err = e.what();
+        }
+        ++runs;
+        bool ok = true;
+        for (int k = 0; k < 6; ++k) {
+            const std::string& n = nics[size_t(k)];
+            std::vector<std::string> have;
+            for (const auto& x : f.ops.addrs)
+                if (x.ifindex == 10 + k) have.push_back(x.prefix().str());
+            const std::vector<std::string> expect = want.count(n) ? std::vector<std::string>{want[n]}
+                                                                  : std::vector<std::string>{};
+            if (have != expect) ok = false;
+        }
+        if (want.size() == 6)
+            ok = ok && err.empty();
+        else if (want.empty())
+            ok = ok && err.find("No LLDP peers with a /30 Port Description were found") == 0;
+        else
+            ok = ok && err.find(strfmt("Not all interfaces were configured (%zu/6).", want.size())) == 0;
+        if (!ok) {
+            if (!mismatches) fprintf(stderr, "round %d (pipeline %d): %s\n", round, pipeline, err.c_str());
+            ++mismatches;
+        }
+    }
+    CHECK_EQ(mismatches, 0);
+    CHECK_EQ(runs, 24);
+}
+
 TEST(agent_min_link_speed_refuses_a_nic_that_came_up_slow) {
     // ens1 negotiated 200G on a 400G fabric: left unconfigured (L3) and named; ens2 reports no
     // speed (allowed, warned); L2 fails the start with the same reason.
