@@ -155,11 +155,12 @@ std::string Agent::node_owned_reason(const nl::LinkInfo& l, int depth) {
     if (auto via = uplink_path(l)) return "carries the node's default route" + *via;
     const auto uppers = stacked_on(l);
     if (l.master != 0) {
-        // A bond / bridge / team port: the master device is configured, never its ports.
+        // A bond / bridge / team port, or a NIC in a VRF: the master device is configured, never
+        // its ports.
         std::string master = "ifindex " + std::to_string(l.master);
         for (const auto& u : uppers)
             if (u.index == l.master) master = u.name;
-        return "is a port of " + master + " (a bond, bridge or team: the node configures the master, not its ports)";
+        return "is a port of " + master + " (a bond, bridge, team or VRF: the node configures the master, not its ports)";
     }
     // The agent only ever assigns /30s (the LLDP point-to-point links): anything else on the NIC
     // was put there by the node (DHCP, netplan, a static management address).

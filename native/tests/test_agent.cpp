@@ -2251,8 +2251,8 @@ TEST(agent_rdma_discovery_leaves_bond_ports_and_vlan_parents_the_node_uses_alone
         auto ex = a.excluded();
         CHECK_EQ(ex.size(), size_t(2));
         CHECK_EQ(ex[0].second, std::string(variant == 0 ? "the node's own NIC: it carries the node's default route via bond0"
-                                                        : "the node's own NIC: it is a port of bond0 (a bond, bridge or "
-                                                          "team: the node configures the master, not its ports)"));
+                                                        : "the node's own NIC: it is a port of bond0 (a bond, bridge, "
+                                                          "team or VRF: the node configures the master, not its ports)"));
         CHECK_EQ(ex[1].second, std::string("the node's own NIC: it carries ens1.100, which holds 10.0.100.5/24, an "
                                            "address the agent never assigns (it only uses /30s)"));
         const std::string m = a.render_metrics();
