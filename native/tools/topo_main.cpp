@@ -1,5 +1,6 @@
 // `netop-topo` — prints the node's scale-out topology as JSON: amdgpu GPUs, candidate
-// NICs, GPU<->NIC pairing (PCIe path type), RDMA devices and the xGMI mesh from KFD.
+// NICs, GPU<->NIC pairing (PCIe path type), RDMA devices, the xGMI mesh from KFD, and which
+// RDMA NICs a host-nic policy's discovery would take (the GPU rails left to amd-so).
 // Used by the readiness tooling, the GPU-box smoke test and fake-sysfs tests.
 #include <cstdio>
 
@@ -49,6 +50,18 @@ int main(int argc, char** argv) {
         j.key("path").value(topo::to_string(p.path)).key("common_depth").value(p.common_depth).end_object();
     }
     j.end_array();
+    {
+        // What host-nic (rdma) discovery takes from sysfs alone; the agent then also leaves out
+        // the node's own NICs, which needs rtnetlink (default route, addresses, routes, bonds).
+        topo::DiscoveryOptions ro = opt;
+        ro.mode = topo::DiscoveryMode::Rdma;
+        auto r = topo::discover(ro, root);
+        j.key("host_nics").begin_object().key("ifnames").begin_array();
+        for (const auto& n : r.ifnames) j.value(n);
+        j.end_array().key("left_alone").begin_object();
+        for (const auto& [n, why] : r.excluded) j.key(n).value(why);
+        j.end_object().end_object();
+    }
     j.key("xgmi").begin_object();
     j.key("gpus").begin_array();
     for (auto& g : x.gpus) j.value(g.bdf());

@@ -152,6 +152,9 @@ def test_topo_tool_json(tmp_path):
     j = json.loads(out)
     assert len(j["gpus"]) == 8 and len(j["pairs"]) == 8
     assert j["xgmi"]["pairs_connected"] == 27 and not j["xgmi"]["full_mesh"]
+    # What a host-nic policy would take from sysfs: the two host NICs; the rails are amd-so's.
+    assert sorted(j["host_nics"]["ifnames"]) == ["ens49np1", "ens9np0"]
+    assert sorted(j["host_nics"]["left_alone"]) == sorted(p["nic"] for p in j["pairs"])
 
 
 def test_accel_mode_reference_layout(native, tmp_path):
