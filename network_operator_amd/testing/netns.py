@@ -632,7 +632,8 @@ def run_scenario(n_nics: int = 8, mode: str = "L3", seed: int | None = None, int
 MGMT_NIC, HOST_NIC = "ens9np0", "ens49np1"  # the fixture node's two NICs on their own root ports
 
 
-def run_host_nic_ownership(mode: str = "L2", rails: int = 8, mgmt_bridge: bool = False) -> dict:
+def run_host_nic_ownership(mode: str = "L2", rails: int = 8, mgmt_bridge: bool = False,
+                           include_gpu_rails: bool = False) -> dict:
     """A default ``host-nic`` policy's agent (rdma discovery, the default driver list) on the
     captured MI355X node, where every NIC is mlx5 with an RDMA device:
 
@@ -644,8 +645,9 @@ def run_host_nic_ownership(mode: str = "L2", rails: int = 8, mgmt_bridge: bool =
     that names the management NIC explicitly (``--interfaces``), which must refuse.  Each veth's
     peer stays in this namespace (up: the NIC has carrier).  With ``mgmt_bridge`` the management
     address and the default route sit on a bridge ``br0`` and ``ens9np0`` is only its port (the
-    kernel's IFLA_MASTER is all that links them here: this sysfs is a fake).  Must run inside
-    ``unshare -rn``."""
+    kernel's IFLA_MASTER is all that links them here: this sysfs is a fake).  With
+    ``include_gpu_rails`` the agent runs as ``hostNic.includeGpuRails`` makes it (a node without
+    amd-so): it takes the rails too, never the management NIC.  Must run inside ``unshare -rn``."""
     from . import fakesysfs
     from ..utils.paths import native_bin
 
@@ -695,8 +697,9 @@ def run_host_nic_ownership(mode: str = "L2", rails: int = 8, mgmt_bridge: bool =
                      "discovery": nat.discover(str(tmp / "sys"), mode="rdma")}
         log_path = tmp / "agent.log"
         with open(log_path, "w") as logf:
-            agent = subprocess.Popen([*base, "--nic-discovery=rdma", f"--status-file={tmp / 'status.json'}"], env=env,
-                                     stdout=logf, stderr=subprocess.STDOUT)
+            extra = ["--rdma-include-gpu-rails"] if include_gpu_rails else []
+            agent = subprocess.Popen([*base, "--nic-discovery=rdma", *extra, f"--status-file={tmp / 'status.json'}"],
+                                     env=env, stdout=logf, stderr=subprocess.STDOUT)
         t_ready = _wait_for(label, 15, agent)
         res["ready"] = t_ready is not None
         res["label"] = label.read_text() if label.exists() else None

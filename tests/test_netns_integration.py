@@ -421,6 +421,20 @@ def test_default_host_nic_policy_leaves_the_management_nic_and_the_gpu_rails_alo
     assert named["after"] == r["before"][netns.MGMT_NIC]
 
 
+def test_host_nic_policy_with_include_gpu_rails_takes_the_rails_but_never_the_management_nic():
+    """hostNic.includeGpuRails (a node without an amd-so policy): the host-nic agent takes the
+    eight rails and the free host NIC; the management NIC (default route) is still the node's."""
+    r = netns.run_isolated(host_nic_ownership=True, include_gpu_rails=True)
+    assert r["ready"], r["agent_log"]
+    rails = r["rails"]
+    assert sorted(i["name"] for i in r["status"]["interfaces"]) == sorted(rails + [netns.HOST_NIC])
+    assert "host-nic-ready.nics=9" in r["label"]
+    assert f"{netns.MGMT_NIC}: the node's own NIC: it carries the node's default route" in r["status"]["excluded"]
+    for nif in rails:
+        assert r["while_ready"][nif]["mtu"] == 9000 and r["while_ready"][nif]["addrs"] == []  # L2: taken, flushed
+    assert r["while_ready"][netns.MGMT_NIC] == r["before"][netns.MGMT_NIC]
+
+
 def test_l2_waits_for_carrier_on_every_nic_before_the_label():
     """L2 on real veths with one switch port down (an unplugged cable): admin-up is not a link.
     No label; the reason names the NIC in status.json and the readiness probe's output; the port
