@@ -108,13 +108,18 @@ __device__ __forceinline__ uint32_t bf16x2_of_ints(int lo, int hi) {
 
 // The index space of one workgroup: grid-strided over the whole buffer (CHUNK = 0), or one
 // contiguous chunk per workgroup, strided by the workgroup (CHUNK = 1).
-template <bool CHUNK>
+// CHUNK = 2: the contiguous chunks assigned XCD-major -- workgroups are dispatched round-robin
+// over the 8 XCDs, so workgroup b runs on XCD b % 8; chunk (b % 8) * (grid / 8) + b / 8 gives each
+// XCD one contiguous eighth of the buffer.
+template <int CHUNK>
 struct Walk {
     uint64_t first, end, stride;
     __device__ explicit Walk(uint64_t n_vec) {
         if (CHUNK) {
             const uint64_t per = ((n_vec + gridDim.x - 1) / gridDim.x + kThreads - 1) / kThreads * kThreads;
-            const uint64_t b = uint64_t(blockIdx.x) * per;
+            uint64_t chunk = blockIdx.x;
+            if (CHUNK == 2 && gridDim.x % 8 == 0) chunk = (blockIdx.x % 8) * (gridDim.x / 8) + blockIdx.x / 8;
+            const uint64_t b = chunk * per;
             first = b + threadIdx.x;
             end = b + per < n_vec ? b + per : n_vec;
             stride = kThreads;
@@ -126,7 +131,7 @@ struct Walk {
     }
 };
 
-template <int V, int UNROLL, bool NT, bool CHUNK = false>
+template <int V, int UNROLL, bool NT, int CHUNK = 0>
 __global__ __launch_bounds__(kThreads) void fill_k(u32x4* __restrict__ out, uint64_t n_vec, uint32_t seed, int n) {
     const Walk<CHUNK> w8(n_vec);
     const uint64_t stride = w8.stride;
@@ -153,7 +158,7 @@ __global__ __launch_bounds__(kThreads) void fill_k(u32x4* __restrict__ out, uint
     }
 }
 
-template <int V, int UNROLL, bool NT, bool CHUNK = false>
+template <int V, int UNROLL, bool NT, int CHUNK = 0>
 __global__ __launch_bounds__(kThreads) void verify_k(const u32x4* __restrict__ in, uint64_t n_vec, uint32_t seed, int n,
                                                      unsigned long long* __restrict__ errors) {
     __shared__ unsigned int wave_err[kThreads / 64];
@@ -280,7 +285,7 @@ int store_shape(u32x4* buf, uint64_t n_vec, int cus, hipEvent_t a, hipEvent_t b)
 
 // Device copy (the xGMI probe's and the all-gather's shape), grid-strided or one contiguous chunk
 // per workgroup, UNROLL 16-byte loads in flight per lane.
-template <int UNROLL, bool CHUNK>
+template <int UNROLL, int CHUNK>
 __global__ __launch_bounds__(kThreads) void copy_k(const u32x4* __restrict__ src, u32x4* __restrict__ dst, uint64_t n_vec) {
     const Walk<CHUNK> w8(n_vec);
     for (uint64_t v0 = w8.first; v0 < w8.end; v0 += w8.stride * UNROLL) {
@@ -294,7 +299,7 @@ __global__ __launch_bounds__(kThreads) void copy_k(const u32x4* __restrict__ src
     }
 }
 
-template <int UNROLL, bool CHUNK>
+template <int UNROLL, int CHUNK>
 int copy_shape(u32x4* buf, uint64_t n_vec, int cus, hipEvent_t a, hipEvent_t b) {
     const uint64_t half = n_vec / 2;
     for (int pc : {2, 4, 8, 16}) {
@@ -323,7 +328,7 @@ struct Ctx {
     int cus;
 };
 
-template <int V, int U, bool NT, bool CHUNK = false>
+template <int V, int U, bool NT, int CHUNK = 0>
 int run(Ctx& c, int n, int per_cu, int iters) {
     const int blocks = c.cus * per_cu;
     const uint32_t seed = 2024;
@@ -372,11 +377,18 @@ int main(int argc, char** argv) {
     CHECK(hipEventCreate(&c.b));
     CHECK(hipDeviceGetAttribute(&c.cus, hipDeviceAttributeMultiprocessorCount, 0));
     const int iters = 10;
-    const std::string mode = argc > 2 ? argv[2] : "all";  // all | ceilings | chunk | copy
+    const std::string mode = argc > 2 ? argv[2] : "all";  // all | ceilings | chunk | copy | xcd
     if (mode == "copy") {
         return copy_shape<1, false>(c.buf, c.n_vec, c.cus, c.a, c.b) || copy_shape<1, true>(c.buf, c.n_vec, c.cus, c.a, c.b) ||
                copy_shape<2, false>(c.buf, c.n_vec, c.cus, c.a, c.b) || copy_shape<2, true>(c.buf, c.n_vec, c.cus, c.a, c.b) ||
                copy_shape<4, true>(c.buf, c.n_vec, c.cus, c.a, c.b);
+    }
+    if (mode == "xcd") {
+        // Chunked walk, chunks in dispatch order (1) against XCD-major (2), NT, v2.
+        for (int n : {1, 8})
+            for (int pc : {8, 16})
+                if (run<2, 1, true, 1>(c, n, pc, iters) || run<2, 1, true, 2>(c, n, pc, iters)) return 1;
+        return copy_shape<1, 2>(c.buf, c.n_vec, c.cus, c.a, c.b) || copy_shape<1, 0>(c.buf, c.n_vec, c.cus, c.a, c.b);
     }
     if (mode == "chunk") {
         // Contiguous chunk per workgroup against the grid-stride walk, v2 pattern.
