@@ -363,7 +363,10 @@ def _line(args, world: int, st: dict) -> dict:
     model, ran, skipped = run_config(args, world, st)
     line = {
         "metric": METRIC,
-        "value": round(busbw, 3) if h else None,
+        # The driver's contract: the whole job's aggregate over its N GPUs.  rccl-tests' busbw is
+        # a per-GPU figure (what each GPU's links carry), so the job's is N times it.
+        "value": round(busbw * world, 3) if h else None,
+        "value_definition": "aggregate busbw of the job: rccl-tests busbw (per GPU) x n_gpus",
         "unit": "GB/s",
         "n_gpus": world,
         "steps": args.steps,

@@ -41,7 +41,8 @@ def test_bench_torchrun_cpu_rehearsal(n, tmp_path, node_sysfs):
     assert REQUIRED <= set(j)
     assert j["n_gpus"] == n and j["steps"] == 4 and j["warmup"] == 1
     assert j["verified"] is True and j["verify_errors"] == 0
-    assert j["value"] == pytest.approx(j["algbw_GBps"] * 2 * (n - 1) / n, abs=1e-3)
+    assert j["busbw_GBps"] == pytest.approx(j["algbw_GBps"] * 2 * (n - 1) / n, abs=1e-3)
+    assert j["value"] == pytest.approx(j["busbw_GBps"] * n, abs=1e-2) == pytest.approx(j["aggregate_busbw_GBps"], abs=1e-2)
     assert j["config"]["parallelism"] == f"dp{n}"
     assert {c["op"] for c in j["collectives"]} == {"all_gather", "reduce_scatter", "all_to_all"}
     assert j["busbw_ceiling_GBps"] == pytest.approx((n - 1) * 76.0)
@@ -69,7 +70,8 @@ def test_bench_spawns_ranks_without_launcher(n, tmp_path):
     assert j["n_gpus"] == n and j["config"]["gpus"] == n and j["config"]["parallelism"] == f"dp{n}"
     assert f"{n}xMI355X" in j["config"]["model"]
     assert j["verified"] is True and j["verify_errors"] == 0
-    assert j["value"] > 0 and j["value"] == pytest.approx(j["algbw_GBps"] * 2 * (n - 1) / n, abs=1e-3)
+    assert j["value"] > 0 and j["busbw_GBps"] == pytest.approx(j["algbw_GBps"] * 2 * (n - 1) / n, abs=1e-3)
+    assert j["value"] == pytest.approx(j["busbw_GBps"] * n, abs=1e-2)
     assert j["aggregate_busbw_GBps"] == pytest.approx(j["busbw_GBps"] * n)
 
 
