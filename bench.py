@@ -333,7 +333,8 @@ def run_config(args, world: int, st: dict) -> tuple:
     """(config.model, what ran, what did not) for the line.  At n = 1 the BASELINE.json configs[1]
     name is claimed only when its node-ready half (LLDP on the mock switch, NIC up, the NFD
     label) was measured in this run; otherwise the line names what did run.
-    At n > 1 the name follows the world size as before."""
+    At n = 2 / 4 the name follows the world size; at n = 8 the configs[2] name, which says the
+    host RoCE links are configured, carries what this run did instead when node-ready did not run."""
     a = st.get("artifacts") or {}
     ran = ["rccl_all_reduce"] + (["agent_artifacts"] if a.get("applied") else [])
     skipped = []
@@ -343,10 +344,16 @@ def run_config(args, world: int, st: dict) -> tuple:
         skipped += ["lldp", "nic_up", "label"]
     if st.get("gpu_side") and "error" not in st["gpu_side"]:
         ran.append("agent_gpu_side_phases")
-    if world != 1 or st.get("node_ready"):
-        return config_name(world), ran, skipped
     why = st.get("node_ready_note") or ("--node-ready off" if args.node_ready == "off" else "not reached")
     backend = "RCCL" if args.device == "cuda" else "gloo (CPU rehearsal)"
+    if st.get("node_ready") or world in (2, 4):
+        return config_name(world), ran, skipped
+    if world > 1:
+        # configs[2] names the node's host RoCE links as configured: keep the name (the all-reduce
+        # over xGMI is what it measures) and say that this run did not configure them.
+        via = "with the agent's artifacts" if a.get("applied") else "without the agent's artifacts"
+        return (f"{config_name(world)} [this run: {backend} all-reduce over xGMI {via}; host RoCE links not "
+                f"configured by it (node-ready not run: {why})]"), ran, skipped
     model = (f"{backend} all-reduce with the agent's artifacts, 1xMI355X (node-ready not run: {why})"
              if a.get("applied") else f"{backend} all-reduce, 1xMI355X (node-ready not run: {why})")
     return model, ran, skipped

@@ -492,7 +492,8 @@ def test_link_deficit_seen_without_the_file_too_is_not_blamed_on_it():
 def test_bench_claims_configs_1_only_when_its_node_ready_half_ran():
     """n = 1: the BASELINE.json configs[1] name (mock-switch LLDP -> NIC up -> NFD label) only with
     a node-ready result in the line; a box without the netns harness gets a name for what ran and
-    the reason.  n > 1 keeps its per-world-size name."""
+    the reason.  n = 2 / 4 keep their per-world-size names; n = 8 keeps configs[2]'s name and says
+    what this run did instead of configuring the host RoCE links."""
     from types import SimpleNamespace
 
     import bench
@@ -508,5 +509,10 @@ def test_bench_claims_configs_1_only_when_its_node_ready_half_ran():
                      "unavailable: unshare failed)")
     assert skipped == ["lldp", "nic_up", "label"] and ran == ["rccl_all_reduce", "agent_artifacts",
                                                               "agent_gpu_side_phases"]
-    for n in (2, 4, 8):
+    for n in (2, 4):
         assert bench.run_config(args, n, box)[0] == bench.config_name(n)
+    # n = 8: configs[2]'s name ("... host RoCE links configured ...") with what this run did
+    model = bench.run_config(args, 8, box)[0]
+    assert model.startswith(bench.config_name(8) + " [this run: RCCL all-reduce over xGMI with the agent's artifacts; "
+                                                   "host RoCE links not configured by it (node-ready not run: ")
+    assert bench.run_config(args, 8, ok)[0] == bench.config_name(8)
