@@ -23,21 +23,51 @@ from network_operator_amd.testing.fakeapi import FakeApiServer
 
 NS = "fuzz"
 
+def mostly(valid, invalid):
+    """Values that are valid three times in four: the churn reaches the reconciler, and the
+    invalid ones still exercise admission."""
+    return st.one_of(st.sampled_from(valid), st.sampled_from(valid), st.sampled_from(valid), st.sampled_from(invalid))
+
+
+mtu = mostly([1500, 4200, 9000], [0, 1000, 10000])
 so_strategy = st.fixed_dictionaries({}, optional={
-    "layer": st.sampled_from(["L2", "L3", "L3BGP", ""]),
-    "mtu": st.one_of(st.integers(1000, 10000), st.just(0)),
-    "image": st.sampled_from(["", "amd/x:1", "registry.local/agent@sha256:abc"]),
-    "pullPolicy": st.sampled_from(["", "Always", "Never", "IfNotPresent", "Sometimes"]),
+    "layer": mostly(["L2", "L3"], ["L3BGP", ""]),
+    "mtu": mtu,
+    "image": st.sampled_from(["amd/x:1", "registry.local/agent@sha256:abc"]),
+    "pullPolicy": mostly(["Always", "Never", "IfNotPresent"], ["", "Sometimes"]),
     "disableNetworkManager": st.booleans(),
     "xgmiCheck": st.booleans(),
     "lldpAnnounce": st.booleans(),
+    # round 3 / 4 fields
+    "disableFirmwareLldp": st.booleans(),
+    "handDcbxToHost": st.booleans(),
+    "checkPeerMtu": st.booleans(),
+    "keepConfigOnRestart": st.booleans(),
+    "minLinkSpeedGbps": mostly([0, 100, 400], [-1]),
+    "lldpWait": mostly(["2m", "90s"], ["", "0s", "soon"]),
+    "railSwitchPattern": mostly(["leaf-r{rail}-.*", "spine[0-9]+"], ["(?i)leaf", "("]),
+    "interfaces": st.lists(mostly(["ens1np0", "ens2np0"], ["bad name", ""]), max_size=2, unique=True),
+    "nicDrivers": st.lists(st.sampled_from(["mlx5_core", "bnxt_en"]), max_size=2, unique=True),
+    "rcclEnv": st.dictionaries(mostly(["NCCL_IB_TC", "RCCL_X"], ["PATH"]), mostly(["1", "106"], ["a\nb"]),
+                               max_size=2),
+})
+host_nic_strategy = st.fixed_dictionaries({"layer": mostly(["L2", "L3"], [""])}, optional={
+    "mtu": mtu,
+    "interfaces": st.lists(mostly(["ens9np0", "ens49np1"], ["x/y"]), max_size=2, unique=True),
+    "nicDrivers": st.lists(st.sampled_from(["mlx5_core", "ionic"]), max_size=2, unique=True),
+    "includeGpuRails": st.booleans(),
+    "checkPeerMtu": st.booleans(),
+    "keepConfigOnRestart": st.booleans(),
+    "verifyPeers": st.booleans(),
+    "lldpWait": mostly(["45s"], ["forever"]),
 })
 spec_strategy = st.fixed_dictionaries({
     "configurationType": st.sampled_from(["amd-so", "amd-so", "amd-so", "host-nic"]),
     "amdScaleOut": so_strategy,
     "nodeSelector": st.dictionaries(st.sampled_from(["a", "b/c", "amd.feature.node.kubernetes.io/gpu-ready"]),
-                                    st.sampled_from(["true", "x"]), min_size=0, max_size=2),
-}, optional={"logLevel": st.integers(-1, 9)})
+                                    st.sampled_from(["true", "x"]), min_size=1, max_size=2)
+                    | st.just({}),
+}, optional={"logLevel": st.integers(-1, 9), "hostNic": host_nic_strategy})
 op_strategy = st.tuples(st.sampled_from(["create", "update", "delete"]), st.sampled_from(["p0", "p1", "p2"]), spec_strategy)
 
 
