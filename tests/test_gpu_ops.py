@@ -13,8 +13,12 @@ def _ref_pattern(n, seed, rank):
     netop_hip.hip), written independently of collectives.pattern_reference."""
     import torch
 
+    return _ref_at(torch.arange(n, dtype=torch.int64), seed, rank)
+
+
+def _ref_at(i, seed, rank):
+    """The same at the element indices ``i`` (an int64 tensor; any size of index)."""
     M32 = 0xFFFFFFFF
-    i = torch.arange(n, dtype=torch.int64)
     g = i >> 3  # one hash per 8-element group
     h = ((g & M32) * 0x9E3779B1) & M32 ^ ((((g >> 32) & M32) * 0x85EBCA77) & M32)
     h ^= h >> 15
@@ -22,7 +26,7 @@ def _ref_pattern(n, seed, rank):
     h ^= h >> 12
     k = ((seed + 0x632BE5AB * (rank + 1)) & M32) * 0xC2B2AE3D & M32
     word = (h * ((k ^ (k >> 16)) | 1)) & M32  # rank's word; element i = field at bit 8 + 3 (i % 8)
-    return (((word >> (8 + 3 * (i % 8))) & 7) - 4).to(torch.float32)
+    return (((word >> (8 + 3 * (i % 8))) & 7) - 4).float()
 
 
 def test_fill_pattern_matches_reference(cuda_device):
@@ -76,6 +80,39 @@ def test_pattern_kernels_cover_every_element_across_workgroup_chunks(cuda_device
     for i in flips:
         t[i] += 1
     assert hip.verify_sum(t, 11, 3) == len(flips)
+
+
+def test_pattern_kernels_index_past_32_bits(cuda_device):
+    """64-bit indexing, sized for 288 GB of HBM: element offsets past 2^35 (group ids past 2^32,
+    where the hash takes the high word) against the reference, and -- when the GPU has the room --
+    one buffer of more than 2^32 16-byte vectors (64 GiB + 80 B) filled and verified whole, a
+    flipped element at its very end counted."""
+    import torch
+
+    from network_operator_amd.ops import hip
+
+    off = (1 << 35) + 4096
+    t = torch.empty(1 << 12, dtype=torch.bfloat16, device=cuda_device)
+    hip.fill_pattern_at(t, 21, 0, 3, elem_offset=off)
+    idx = torch.arange(1 << 12, dtype=torch.int64) + off
+    torch.testing.assert_close(t.float().cpu(), sum(_ref_at(idx, 21, r) for r in range(3)), rtol=0, atol=0)
+    assert hip.verify_pattern_at(t, 21, 0, 3, off) == 0
+
+    n = ((1 << 32) + 5) * 8
+    free, _ = torch.cuda.mem_get_info(cuda_device)
+    if free < 2 * n + (8 << 30):
+        pytest.skip(f"{free >> 30} GiB free: the > 2^32-vector buffer needs {(2 * n) >> 30} GiB")
+    big = torch.empty(n, dtype=torch.bfloat16, device=cuda_device)
+    try:
+        hip.fill_pattern(big, 3, 1)
+        assert hip.verify_pattern_at(big, 3, 1, 1, 0) == 0
+        probe = torch.tensor([0, (1 << 32) * 8 - 1, (1 << 32) * 8, n - 1], dtype=torch.int64)
+        torch.testing.assert_close(big[probe.to(cuda_device)].float().cpu(), _ref_at(probe, 3, 1), rtol=0, atol=0)
+        big[n - 1] += 1
+        assert hip.verify_pattern_at(big, 3, 1, 1, 0) == 1
+    finally:
+        del big
+        torch.cuda.empty_cache()
 
 
 def test_copy_matches_torch(cuda_device):
