@@ -316,15 +316,16 @@ def _artifacts(store, rank: int, args) -> dict:
 class _Once:
     """Rank 0's single JSON line: printed once, by the main thread or the deadline watchdog."""
 
-    def __init__(self):
+    def __init__(self, out=None):
         self.lock = threading.Lock()
         self.done = False
+        self.out = out
 
     def emit(self, line: dict) -> bool:
         with self.lock:
             if self.done:
                 return False
-            print(json.dumps(line), flush=True)
+            print(json.dumps(line), file=self.out or sys.stdout, flush=True)
             self.done = True
             return True
 
@@ -514,6 +515,12 @@ def main(argv=None) -> int:
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         return _spawn_ranks(args.gpus, raw_argv, args.device, deadline)
 
+    # A rank's stdout carries exactly the one JSON line: what libraries print there (RCCL's
+    # version banner, gloo's connection notes) and child processes that inherit it go to stderr.
+    json_out = os.fdopen(os.dup(1), "w")
+    sys.stdout.flush()
+    os.dup2(2, 1)
+
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -534,7 +541,7 @@ def main(argv=None) -> int:
     from network_operator_amd.parallel import fabric_artifacts as FA
 
     st: dict = {"t_start": t_start, "pending": []}
-    once = _Once()
+    once = _Once(json_out)
     runner_box: list = []
     _watchdog(rank, deadline, st, once, runner_box, args, world)
 
