@@ -7,7 +7,6 @@
 #include <linux/rtnetlink.h>
 #include <sys/epoll.h>
 #include <sys/socket.h>
-#include <sys/un.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -22,7 +21,6 @@ namespace netop::agent {
 
 using detail::fd_readable;
 using detail::format_gbps;
-using detail::kMonitorVerifyNs;
 
 void Agent::on_lldp(NicState& n, const lldp::Frame& f) {
     n.lldp_seen = true;

@@ -7,13 +7,11 @@
 #include <linux/rtnetlink.h>
 #include <sys/epoll.h>
 #include <sys/socket.h>
-#include <sys/un.h>
 #include <unistd.h>
 
 #include <algorithm>
 #include <cstring>
 #include <map>
-#include <set>
 
 #include "agent_internal.hpp"
 #include "netop/log.hpp"
@@ -21,7 +19,6 @@
 namespace netop::agent {
 
 using detail::fd_readable;
-using detail::format_gbps;
 using detail::kMonitorVerifyNs;
 
 void Agent::announce_all(uint16_t ttl) {

@@ -4,26 +4,21 @@
 #include "netop/agent.hpp"
 
 #include <errno.h>
-#include <linux/if.h>
 #include <linux/rtnetlink.h>
-#include <sys/epoll.h>
+#include <poll.h>
 #include <sys/socket.h>
 #include <sys/un.h>
 #include <unistd.h>
 
 #include <algorithm>
+#include <cstddef>
 #include <cstring>
-#include <map>
-#include <set>
+#include <thread>
 
 #include "agent_internal.hpp"
 #include "netop/log.hpp"
 
 namespace netop::agent {
-
-using detail::fd_readable;
-using detail::format_gbps;
-using detail::kMonitorVerifyNs;
 
 int Agent::take_lock(const std::string& name, int64_t deadline, int stop_fd, const std::string& waiting,
                      const std::string& busy) {
