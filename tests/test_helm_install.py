@@ -401,7 +401,8 @@ def test_uninstall_with_keep_config_policies_runs_the_predelete_hook_first(tmp_p
 
 
 @pytest.mark.parametrize("keep,nm", [(False, False), (True, False), (False, True), (True, True)])
-def test_predelete_hook_is_rendered_whenever_the_seeded_policy_gets_the_finalizer(keep, nm):
+@pytest.mark.parametrize("which", ["amd", "hostNic"])
+def test_predelete_hook_is_rendered_whenever_the_seeded_policy_gets_the_finalizer(keep, nm, which):
     """a release with config.amd.disableNetworkManager=true seeds a policy that
     carries the node-cleanup finalizer (the NICs are handed back to NetworkManager by cleanup
     Jobs), so it needs the pre-delete hook as much as keepConfigOnRestart does; without it
@@ -409,13 +410,14 @@ def test_predelete_hook_is_rendered_whenever_the_seeded_policy_gets_the_finalize
     from network_operator_amd.api.v1alpha1 import types as T
     from network_operator_amd.operator import reconciler as R
 
-    docs = helm_template(CHART, {"config": {"amd": {"enabled": True, "keepConfigOnRestart": keep,
+    # (the chart exposes the same two fields for the host-nic policy: the same finalizer, the same hook)
+    docs = helm_template(CHART, {"config": {which: {"enabled": True, "keepConfigOnRestart": keep,
                                                     "disableNetworkManager": nm}}}, NS)
     hooks = [d for d in docs if d["kind"] == "Job" and
              (d["metadata"].get("annotations") or {}).get("helm.sh/hook") == "pre-delete"]
     cm = [d for d in docs if d["kind"] == "ConfigMap" and d["metadata"]["name"] == M.POLICIES_CONFIGMAP][0]
     seeded = [T.NetworkClusterPolicy.from_dict(x) for x in yaml.safe_load(cm["data"]["policies.yaml"])["policies"]]
-    assert [p.name for p in seeded] == ["netconf-amd-scale-out"]
+    assert [p.name for p in seeded] == ["netconf-amd-scale-out" if which == "amd" else "netconf-amd-host-nic"]
     assert bool(hooks) == R.needs_node_cleanup(seeded[0]) == (keep or nm)
 
 
