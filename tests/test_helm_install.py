@@ -448,10 +448,13 @@ def test_every_policy_field_is_settable_from_the_chart_and_documented():
     from network_operator_amd.api.v1alpha1 import types as T
     from network_operator_amd.api.v1alpha1 import webhook as W
 
-    docs = helm_template(CHART, {"config": {"amd": dict(_AMD_VALUES, enabled=True),
-                                            "hostNic": _HOST_NIC_VALUES}}, NS)
-    seeded = {p["metadata"]["name"]: T.NetworkClusterPolicy.from_dict(p)
-              for p in yaml.safe_load(_configmap_text(docs))["policies"]}
+    # (two releases: includeGpuRails next to an enabled config.amd is refused at render time)
+    seeded = {}
+    for values in ({"amd": dict(_AMD_VALUES, enabled=True)},
+                   {"amd": {"image": _AMD_VALUES["image"]}, "hostNic": _HOST_NIC_VALUES}):
+        docs = helm_template(CHART, {"config": values}, NS)
+        seeded.update({p["metadata"]["name"]: T.NetworkClusterPolicy.from_dict(p)
+                       for p in yaml.safe_load(_configmap_text(docs))["policies"]})
     so = seeded["netconf-amd-scale-out"].spec.amdScaleOut
     want = {k: v for k, v in _AMD_VALUES.items() if k not in ("mode", "image", "validation", "maxUnavailable")}
     want.update(layer="L3", image="reg/agent:9.9", pullPolicy="Always")
@@ -494,3 +497,17 @@ def test_every_policy_field_is_settable_from_the_chart_and_documented():
             documented = (f"`config.{section}.{k}`" in readme or f"`config.{section}.{k}." in readme
                           or f"/ `{k}`" in readme)
             assert documented, f"config.{section}.{k} undocumented"
+
+
+def test_chart_refuses_to_give_the_gpu_rails_to_two_policies():
+    """config.hostNic.includeGpuRails next to config.amd.enabled (same node selector): both
+    policies' agents would want the rails, and one would fail on every node on its NIC locks.
+    The render fails instead, naming the two values."""
+    from network_operator_amd.testing.render import RenderError
+
+    with pytest.raises(RenderError) as e:
+        helm_template(CHART, {"config": {"amd": {"enabled": True},
+                                         "hostNic": {"enabled": True, "includeGpuRails": True}}}, NS)
+    assert "includeGpuRails" in str(e.value) and "config.amd" in str(e.value)
+    helm_template(CHART, {"config": {"hostNic": {"enabled": True, "includeGpuRails": True}}}, NS)  # alone: fine
+
