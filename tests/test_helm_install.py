@@ -341,11 +341,13 @@ def test_seed_id_label_is_a_valid_distinct_label_value():
     assert re.fullmatch(r"[A-Za-z0-9]([A-Za-z0-9._-]*[A-Za-z0-9])?", odd) and odd != seed_id_label("ns/with-spaces")
 
 
-def test_uninstall_with_keep_config_policies_runs_the_predelete_hook_first(tmp_path):
-    """config.amd.keepConfigOnRestart: the seeded policy carries the node-cleanup finalizer.  An
-    uninstall that removed the operator first would leave it Terminating for good (nobody to
-    clean the nodes and release it); the chart's pre-delete hook deletes the release's policies
-    while the operator runs and returns once they are finalized.  A user's policy is left alone."""
+@pytest.mark.parametrize("which", ["amd", "hostNic"])
+def test_uninstall_with_keep_config_policies_runs_the_predelete_hook_first(tmp_path, which):
+    """config.<amd|hostNic>.keepConfigOnRestart: the seeded policy carries the node-cleanup
+    finalizer.  An uninstall that removed the operator first would leave it Terminating for good
+    (nobody to clean the nodes and release it); the chart's pre-delete hook deletes the release's
+    policies while the operator runs and returns once they are finalized.  A user's policy is left
+    alone."""
     from network_operator_amd.operator import reconciler as R
     from network_operator_amd.operator.controller import PolicyController
     from network_operator_amd.operator.predelete import drain
@@ -355,7 +357,8 @@ def test_uninstall_with_keep_config_policies_runs_the_predelete_hook_first(tmp_p
         fake = FakeApiServer()
         url = await fake.start()
         fake.add_node("mi355x-0", {"amd.feature.node.kubernetes.io/gpu-ready": "true"})
-        docs = helm_template(CHART, {"config": {"amd": {"enabled": True, "keepConfigOnRestart": True}}}, NS)
+        docs = helm_template(CHART, {"config": {which: {"enabled": True, "keepConfigOnRestart": True}}}, NS)
+        seeded = "netconf-amd-scale-out" if which == "amd" else "netconf-amd-host-nic"
         hook = [d for d in docs if d["kind"] == "Job"][0]
         owner = next(a.split("=", 1)[1] for a in hook["spec"]["template"]["spec"]["containers"][0]["args"]
                      if a.startswith("--owner="))
@@ -371,9 +374,9 @@ def test_uninstall_with_keep_config_policies_runs_the_predelete_hook_first(tmp_p
             ctl = PolicyController(c, NS, is_openshift=False, workers=2)
             await ctl.start()
             try:
-                await _until(lambda: fake.get_object(kube.DAEMONSETS, "netconf-amd-scale-out", NS) is not None)
-                fake.set_agent_ready("mi355x-0", daemonset=f"{NS}/netconf-amd-scale-out")
-                await _until(lambda: (fake.get_object(P, "netconf-amd-scale-out").get("status") or {})
+                await _until(lambda: fake.get_object(kube.DAEMONSETS, seeded, NS) is not None)
+                fake.set_agent_ready("mi355x-0", daemonset=f"{NS}/{seeded}")
+                await _until(lambda: (fake.get_object(P, seeded).get("status") or {})
                              .get("keptNodes") == ["mi355x-0"])
 
                 async def kubelet():  # the node runs each cleanup Job to success
@@ -385,8 +388,8 @@ def test_uninstall_with_keep_config_policies_runs_the_predelete_hook_first(tmp_p
                 k = asyncio.ensure_future(kubelet())
                 assert await asyncio.wait_for(drain(c, owner, timeout=20, poll=0.05), 30) == 0
                 k.cancel()
-                assert fake.get_object(P, "netconf-amd-scale-out") is None
-                assert fake.get_object(kube.DAEMONSETS, "netconf-amd-scale-out", NS) is None
+                assert fake.get_object(P, seeded) is None
+                assert fake.get_object(kube.DAEMONSETS, seeded, NS) is None
                 assert fake.get_object(P, "user-policy") is not None
             finally:
                 await ctl.stop()
