@@ -202,6 +202,21 @@ def openapi_schema() -> dict:
             "nodeSelector": {"additionalProperties": {"type": "string"},
                              "description": "Select which nodes the operator should target. Align with labels created by NFD.",
                              "type": "object"},
+            "tolerations": {
+                "description": "Tolerations of the agent Pods (and of their cleanup and validation Jobs), so that\n"
+                               "they run on tainted GPU nodes (e.g. amd.com/gpu:NoSchedule).",
+                "type": "array",
+                "items": {
+                    "type": "object",
+                    "properties": {
+                        "key": {"type": "string"},
+                        "operator": {"type": "string", "enum": ["Exists", "Equal"]},
+                        "value": {"type": "string"},
+                        "effect": {"type": "string", "enum": ["NoSchedule", "PreferNoSchedule", "NoExecute"]},
+                        "tolerationSeconds": {"type": "integer", "format": "int64"},
+                    },
+                },
+            },
         },
         "required": ["configurationType"],
     }

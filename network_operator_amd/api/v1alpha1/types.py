@@ -286,6 +286,9 @@ class NetworkClusterPolicySpec:
     logLevel: int = 0
     # DaemonSet rollingUpdate.maxUnavailable: int >= 1 or "N%" (None = 1, the reference's default)
     maxUnavailable: Optional[Union[int, str]] = None
+    # Pod tolerations of the agent DaemonSet (and of its cleanup / validation Jobs): GPU nodes are
+    # often tainted (amd.com/gpu:NoSchedule) and the agent has to run on every one of them.
+    tolerations: List[Dict[str, Any]] = field(default_factory=list)
     extra: Dict[str, Any] = field(default_factory=dict)
 
     def to_dict(self) -> dict:
@@ -300,6 +303,8 @@ class NetworkClusterPolicySpec:
             d["logLevel"] = self.logLevel
         if self.maxUnavailable is not None:
             d["maxUnavailable"] = self.maxUnavailable
+        if self.tolerations:
+            d["tolerations"] = copy.deepcopy(self.tolerations)
         d.update(copy.deepcopy(self.extra))
         return d
 
@@ -313,6 +318,7 @@ class NetworkClusterPolicySpec:
             hostNic=HostNicSpec.from_dict(d.pop("hostNic")) if d.get("hostNic") is not None else None,
             logLevel=int(d.pop("logLevel", 0) or 0),
             maxUnavailable=d.pop("maxUnavailable", None),
+            tolerations=copy.deepcopy(list(d.pop("tolerations", []) or [])),
         )
         s.extra = d
         return s

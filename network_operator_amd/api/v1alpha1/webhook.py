@@ -92,6 +92,11 @@ def validate_node_selector(ns: dict) -> None:
 
 
 RCCL_ENV_KEY_RE = re.compile(r"^(NCCL|RCCL|HSA)_[A-Z0-9_]+$")
+# A Kubernetes qualified name (taint / toleration key): an optional DNS-subdomain prefix and "/",
+# then a name of at most 63 characters.  (Not the reference's labelHostRegex quirk: taint keys
+# such as node-role.kubernetes.io/... carry "-".)
+QUALIFIED_NAME_RE = re.compile(r"^([a-z0-9]([-a-z0-9]*[a-z0-9])?(\.[a-z0-9]([-a-z0-9]*[a-z0-9])?)*/)?"
+                               r"[A-Za-z0-9]([-A-Za-z0-9_.]{0,61}[A-Za-z0-9])?$")
 
 
 class InvalidRcclEnvError(ValidationError):
@@ -347,9 +352,35 @@ def validate_host_nic_spec(s: Optional[T.HostNicSpec]) -> List[str]:
     return warnings
 
 
+class InvalidTolerationError(ValidationError):
+    def __init__(self, why: str):
+        super().__init__(why)
+        self.message = f"invalid toleration: {why}"
+
+
+def validate_tolerations(tolerations: List[dict]) -> None:
+    """The API server's own rules for a Pod toleration (the DaemonSet would be refused with them
+    otherwise, long after admission): Exists takes no value; Equal (the default) needs a key; a
+    tolerationSeconds only with NoExecute; a key is a qualified name."""
+    for t in tolerations:
+        if not isinstance(t, dict):
+            raise InvalidTolerationError(f"{t!r} is not an object")
+        op = t.get("operator") or "Equal"
+        key, value, effect = t.get("key") or "", t.get("value") or "", t.get("effect") or ""
+        if op == "Exists" and value:
+            raise InvalidTolerationError(f"{key or '<any key>'}: operator Exists takes no value")
+        if op == "Equal" and not key:
+            raise InvalidTolerationError("operator Equal (the default) needs a key")
+        if t.get("tolerationSeconds") is not None and effect != "NoExecute":
+            raise InvalidTolerationError(f"{key}: tolerationSeconds only applies to effect NoExecute")
+        if key and not QUALIFIED_NAME_RE.fullmatch(key):
+            raise InvalidTolerationError(f"{key!r} is not a qualified name")
+
+
 def validate_spec(spec: T.NetworkClusterPolicySpec) -> List[str]:
     validate_node_selector(spec.nodeSelector)
     validate_max_unavailable(spec.maxUnavailable)
+    validate_tolerations(spec.tolerations)
     if spec.configurationType == T.CONFIG_AMD_SCALE_OUT:
         return validate_amd_so_spec(spec.amdScaleOut)
     if spec.configurationType == T.CONFIG_HOST_NIC:

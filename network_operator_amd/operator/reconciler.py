@@ -350,6 +350,13 @@ def update_daemonset_for(ds: dict, p: T.NetworkClusterPolicy, namespace: str) ->
         update_host_nic_daemonset(ds, p, namespace)
     else:
         raise ValueError(f"unknown configuration type {p.spec.configurationType!r}")
+    # Tainted GPU nodes (amd.com/gpu:NoSchedule, ...): the policy's tolerations, exactly (a
+    # toleration removed from the policy leaves the template; the cleanup Job copies this spec).
+    pod = ds["spec"]["template"]["spec"]
+    if p.spec.tolerations:
+        pod["tolerations"] = copy.deepcopy(p.spec.tolerations)
+    else:
+        pod.pop("tolerations", None)
 
 
 def status_for(targets: int, ready: int) -> str:
@@ -601,6 +608,7 @@ def validation_job(p: T.NetworkClusterPolicy, node: str, generation: int, namesp
                 "spec": {
                     "restartPolicy": "Never",
                     "nodeName": node,
+                    **({"tolerations": copy.deepcopy(p.spec.tolerations)} if p.spec.tolerations else {}),
                     "containers": [{
                         "name": "validate",
                         "image": v.image or T.DEFAULT_VALIDATION_IMAGE,

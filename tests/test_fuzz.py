@@ -67,7 +67,10 @@ spec_strategy = st.fixed_dictionaries({
     "nodeSelector": st.dictionaries(st.sampled_from(["a", "b/c", "amd.feature.node.kubernetes.io/gpu-ready"]),
                                     st.sampled_from(["true", "x"]), min_size=1, max_size=2)
                     | st.just({}),
-}, optional={"logLevel": st.integers(-1, 9), "hostNic": host_nic_strategy})
+}, optional={"logLevel": st.integers(-1, 9), "hostNic": host_nic_strategy,
+             "tolerations": st.lists(mostly([{"key": "amd.com/gpu", "operator": "Exists", "effect": "NoSchedule"},
+                                             {"key": "dedicated", "operator": "Equal", "value": "gpu"}],
+                                            [{"operator": "Exists", "value": "x"}, {"key": "a b"}]), max_size=2)})
 op_strategy = st.tuples(st.sampled_from(["create", "update", "delete"]), st.sampled_from(["p0", "p1", "p2"]), spec_strategy)
 
 

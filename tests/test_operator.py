@@ -1211,6 +1211,44 @@ def test_host_nic_policy_can_take_the_gpu_rails_only_on_request():
     assert any("no effect with interfaces" in w for w in W.validate_create(h))
 
 
+def test_policy_tolerations_reach_the_agent_pods_and_their_jobs():
+    """GPU nodes are often tainted (amd.com/gpu:NoSchedule): spec.tolerations goes to the agent
+    DaemonSet's Pod template, the cleanup Job (a copy of that template) and the validation Job;
+    removing it from the policy removes it from the template.  Admission applies the API
+    server's toleration rules, so a bad one fails at kubectl apply instead of at the DaemonSet."""
+    from network_operator_amd import discovery
+    from network_operator_amd.api.v1alpha1 import crd as CRD
+    from network_operator_amd.api.v1alpha1 import types as T
+    from network_operator_amd.api.v1alpha1 import webhook as W
+    from network_operator_amd.operator import reconciler as R
+
+    tol = [{"key": "amd.com/gpu", "operator": "Exists", "effect": "NoSchedule"},
+           {"key": "node.kubernetes.io/unreachable", "operator": "Exists", "effect": "NoExecute",
+            "tolerationSeconds": 300}]
+    for p in (T.new_policy("p", layer="L3"), T.new_host_nic_policy("h", layer="L2", nicDrivers=["mlx5_core"])):
+        p.spec.tolerations = tol
+        assert T.NetworkClusterPolicy.from_dict(p.to_dict()).spec.tolerations == tol
+        assert not CRD.validate(p.to_dict())
+        W.validate_create(p)
+        ds = discovery.discovery_daemonset()
+        R.update_daemonset_for(ds, p, "ns")
+        assert ds["spec"]["template"]["spec"]["tolerations"] == tol
+        assert R.cleanup_job(p, "n0", "ns")["spec"]["template"]["spec"]["tolerations"] == tol
+        p.spec.tolerations = []
+        R.update_daemonset_for(ds, p, "ns")
+        assert "tolerations" not in ds["spec"]["template"]["spec"]
+    v = T.new_policy("v", layer="L3")
+    v.spec.tolerations = tol[:1]
+    assert R.validation_job(v, "n0", 1, "ns")["spec"]["template"]["spec"]["tolerations"] == tol[:1]
+    assert "tolerations" not in R.validation_job(T.new_policy("w", layer="L3"), "n0", 1, "ns")["spec"]["template"][
+        "spec"]
+    for bad in ({"operator": "Exists", "value": "x"}, {"value": "x"}, {"key": "a b"},
+                {"key": "k", "effect": "NoSchedule", "tolerationSeconds": 5}):
+        v.spec.tolerations = [bad]
+        with pytest.raises(W.ValidationError):
+            W.validate_create(v)
+
+
 def test_stalled_lease_renewal_stops_the_leader_before_anyone_else_can_lead():
     """the leader's Lease PUTs stall for 20 s (a wedged API path).  Its renewal
     attempts are bounded by the renew deadline, so it cancels its work within renew_deadline of
