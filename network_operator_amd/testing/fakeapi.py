@@ -264,8 +264,10 @@ class FakeApiServer:
     def list_objects(self, res: Resource) -> List[dict]:
         return [copy.deepcopy(o) for o in self._table(res).values()]
 
-    def add_node(self, name: str, labels: Optional[dict] = None) -> dict:
+    def add_node(self, name: str, labels: Optional[dict] = None, taints: Optional[List[dict]] = None) -> dict:
         node = {"apiVersion": "v1", "kind": "Node", "metadata": {"name": name, "labels": dict(labels or {})}}
+        if taints:
+            node["spec"] = {"taints": [dict(t) for t in taints]}
         obj = self._create(kube.NODES, node, None)
         self._sync_daemonsets()
         return obj
@@ -544,12 +546,32 @@ class FakeApiServer:
     # ------------------------------------------------------------------------------------------
     # DaemonSet controller simulation
     # ------------------------------------------------------------------------------------------
+    @staticmethod
+    def _tolerated(taint: dict, tolerations: List[dict]) -> bool:
+        """Kubernetes' toleration match: the effect (empty = any), then Exists (an empty key
+        tolerates every taint) or Equal (the default) on key and value."""
+        for t in tolerations:
+            if t.get("effect") and t["effect"] != taint.get("effect"):
+                continue
+            if (t.get("operator") or "Equal") == "Exists":
+                if not t.get("key") or t["key"] == taint.get("key"):
+                    return True
+            elif t.get("key") == taint.get("key") and (t.get("value") or "") == (taint.get("value") or ""):
+                return True
+        return False
+
     def _sync_daemonsets(self) -> None:
         nodes = list(self._table(kube.NODES).values())
         for (ns, name), ds in list(self._table(kube.DAEMONSETS).items()):
-            sel = ds["spec"]["template"]["spec"].get("nodeSelector") or {}
+            pod_spec = ds["spec"]["template"]["spec"]
+            sel = pod_spec.get("nodeSelector") or {}
+            tols = pod_spec.get("tolerations") or []
+            # The DaemonSet controller places a Pod where the selector matches and every
+            # NoSchedule / NoExecute taint of the node is tolerated (PreferNoSchedule never blocks).
             matching = [n["metadata"]["name"] for n in nodes
-                        if all((n["metadata"].get("labels") or {}).get(k) == v for k, v in sel.items())]
+                        if all((n["metadata"].get("labels") or {}).get(k) == v for k, v in sel.items())
+                        and all(self._tolerated(t, tols) for t in (n.get("spec") or {}).get("taints") or []
+                                if t.get("effect") in ("NoSchedule", "NoExecute"))]
             ready = sum(1 for n in matching if self.node_ready.get((f"{ns}/{name}", n)))
             st = {"currentNumberScheduled": len(matching), "desiredNumberScheduled": len(matching),
                   "numberMisscheduled": 0, "numberReady": ready,

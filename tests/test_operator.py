@@ -1249,6 +1249,32 @@ def test_policy_tolerations_reach_the_agent_pods_and_their_jobs():
             W.validate_create(v)
 
 
+def test_tainted_gpu_nodes_are_targeted_once_the_policy_tolerates_the_taint():
+    """Through the controller loop: two of three selected nodes carry amd.com/gpu:NoSchedule.
+    Without tolerations the DaemonSet places agents on the untainted node only (targets 1); the
+    policy gains the toleration, the DaemonSet template follows, and all three are targeted."""
+    async def body():
+        async with cluster(openshift=False) as (fake, client, ctl):
+            taint = [{"key": "amd.com/gpu", "value": "present", "effect": "NoSchedule"}]
+            for i in range(3):
+                fake.add_node(f"gpu-node-{i}", {"foo": "bar"}, taints=taint if i else None)
+            await client.create(kube.NETWORKCLUSTERPOLICIES, policy())
+
+            def targets(n):
+                def check():
+                    assert fake.get_object(kube.NETWORKCLUSTERPOLICIES, "policy")["status"]["targets"] == n
+                return check
+            await eventually(targets(1))
+            cur = await client.get(kube.NETWORKCLUSTERPOLICIES, "policy")
+            cur["spec"]["tolerations"] = [{"key": "amd.com/gpu", "operator": "Exists", "effect": "NoSchedule"}]
+            await client.replace(kube.NETWORKCLUSTERPOLICIES, cur)
+            await eventually(targets(3))
+            ds = fake.get_object(kube.DAEMONSETS, "policy", NS)
+            assert ds["spec"]["template"]["spec"]["tolerations"] == cur["spec"]["tolerations"]
+
+    asyncio.run(asyncio.wait_for(body(), 60))
+
+
 def test_stalled_lease_renewal_stops_the_leader_before_anyone_else_can_lead():
     """the leader's Lease PUTs stall for 20 s (a wedged API path).  Its renewal
     attempts are bounded by the renew deadline, so it cancels its work within renew_deadline of
