@@ -202,6 +202,11 @@ def openapi_schema() -> dict:
             "nodeSelector": {"additionalProperties": {"type": "string"},
                              "description": "Select which nodes the operator should target. Align with labels created by NFD.",
                              "type": "object"},
+            "priorityClassName": {
+                "description": "PriorityClass of the agent Pods (e.g. system-node-critical); empty = the cluster's\n"
+                               "default priority.",
+                "type": "string", "maxLength": 253,
+                "pattern": "^[a-z0-9]([-a-z0-9]*[a-z0-9])?(\\.[a-z0-9]([-a-z0-9]*[a-z0-9])?)*$"},
             "tolerations": {
                 "description": "Tolerations of the agent Pods (and of their cleanup and validation Jobs), so that\n"
                                "they run on tainted GPU nodes (e.g. amd.com/gpu:NoSchedule).",

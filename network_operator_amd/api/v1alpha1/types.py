@@ -289,6 +289,9 @@ class NetworkClusterPolicySpec:
     # Pod tolerations of the agent DaemonSet (and of its cleanup / validation Jobs): GPU nodes are
     # often tainted (amd.com/gpu:NoSchedule) and the agent has to run on every one of them.
     tolerations: List[Dict[str, Any]] = field(default_factory=list)
+    # PriorityClass of the agent Pods (e.g. system-node-critical: a node's network agent should not
+    # be the first Pod evicted under memory pressure).  "" = the cluster default.
+    priorityClassName: str = ""
     extra: Dict[str, Any] = field(default_factory=dict)
 
     def to_dict(self) -> dict:
@@ -305,6 +308,8 @@ class NetworkClusterPolicySpec:
             d["maxUnavailable"] = self.maxUnavailable
         if self.tolerations:
             d["tolerations"] = copy.deepcopy(self.tolerations)
+        if self.priorityClassName:
+            d["priorityClassName"] = self.priorityClassName
         d.update(copy.deepcopy(self.extra))
         return d
 
@@ -319,6 +324,7 @@ class NetworkClusterPolicySpec:
             logLevel=int(d.pop("logLevel", 0) or 0),
             maxUnavailable=d.pop("maxUnavailable", None),
             tolerations=copy.deepcopy(list(d.pop("tolerations", []) or [])),
+            priorityClassName=d.pop("priorityClassName", "") or "",
         )
         s.extra = d
         return s

@@ -357,6 +357,10 @@ def update_daemonset_for(ds: dict, p: T.NetworkClusterPolicy, namespace: str) ->
         pod["tolerations"] = copy.deepcopy(p.spec.tolerations)
     else:
         pod.pop("tolerations", None)
+    if p.spec.priorityClassName:
+        pod["priorityClassName"] = p.spec.priorityClassName
+    else:
+        pod.pop("priorityClassName", None)
 
 
 def status_for(targets: int, ready: int) -> str:

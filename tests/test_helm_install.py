@@ -435,6 +435,7 @@ _AMD_VALUES = {
     "checkPeerMtu": False, "handDcbxToHost": True, "maxUnavailable": "25%",
     "validation": {"enabled": True, "minBusbw": 300, "minLink": 40, "gpus": 4, "image": "reg/val:1"},
     "tolerations": [{"key": "amd.com/gpu", "operator": "Exists", "effect": "NoSchedule"}],
+    "priorityClassName": "system-node-critical",
     "image": {"repository": "reg/agent", "tag": "9.9", "imagePullPolicy": "Always"},
 }
 _HOST_NIC_VALUES = {
@@ -461,7 +462,7 @@ def test_every_policy_field_is_settable_from_the_chart_and_documented():
                        for p in yaml.safe_load(_configmap_text(docs))["policies"]})
     so = seeded["netconf-amd-scale-out"].spec.amdScaleOut
     want = {k: v for k, v in _AMD_VALUES.items() if k not in ("mode", "image", "validation", "maxUnavailable",
-                                                               "tolerations")}
+                                                               "tolerations", "priorityClassName")}
     want.update(layer="L3", image="reg/agent:9.9", pullPolicy="Always")
     assert set(want) | {"validation"} == set(T.AmdScaleOutSpec._FIELDS), "a new amdScaleOut field needs a chart value"
     for k, v in want.items():
@@ -469,6 +470,7 @@ def test_every_policy_field_is_settable_from_the_chart_and_documented():
     assert so.validation.to_dict() == _AMD_VALUES["validation"]
     assert seeded["netconf-amd-scale-out"].spec.maxUnavailable == "25%"
     assert seeded["netconf-amd-scale-out"].spec.tolerations == _AMD_VALUES["tolerations"]
+    assert seeded["netconf-amd-scale-out"].spec.priorityClassName == "system-node-critical"
     assert not so.extra
 
     hn = seeded["netconf-amd-host-nic"].spec.hostNic

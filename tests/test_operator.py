@@ -1211,7 +1211,7 @@ def test_host_nic_policy_can_take_the_gpu_rails_only_on_request():
     assert any("no effect with interfaces" in w for w in W.validate_create(h))
 
 
-def test_policy_tolerations_reach_the_agent_pods_and_their_jobs():
+def test_policy_tolerations_and_priority_reach_the_agent_pods_and_their_jobs():
     """GPU nodes are often tainted (amd.com/gpu:NoSchedule): spec.tolerations goes to the agent
     DaemonSet's Pod template, the cleanup Job (a copy of that template) and the validation Job;
     removing it from the policy removes it from the template.  Admission applies the API
@@ -1234,9 +1234,16 @@ def test_policy_tolerations_reach_the_agent_pods_and_their_jobs():
         R.update_daemonset_for(ds, p, "ns")
         assert ds["spec"]["template"]["spec"]["tolerations"] == tol
         assert R.cleanup_job(p, "n0", "ns")["spec"]["template"]["spec"]["tolerations"] == tol
-        p.spec.tolerations = []
+        p.spec.priorityClassName = "system-node-critical"
+        R.update_daemonset_for(ds, p, "ns")
+        assert ds["spec"]["template"]["spec"]["priorityClassName"] == "system-node-critical"
+        assert R.cleanup_job(p, "n0", "ns")["spec"]["template"]["spec"]["priorityClassName"] == "system-node-critical"
+        assert T.NetworkClusterPolicy.from_dict(p.to_dict()).spec.priorityClassName == "system-node-critical"
+        assert not CRD.validate(p.to_dict())
+        p.spec.tolerations, p.spec.priorityClassName = [], ""
         R.update_daemonset_for(ds, p, "ns")
         assert "tolerations" not in ds["spec"]["template"]["spec"]
+        assert "priorityClassName" not in ds["spec"]["template"]["spec"]
     v = T.new_policy("v", layer="L3")
     v.spec.tolerations = tol[:1]
     assert R.validation_job(v, "n0", 1, "ns")["spec"]["template"]["spec"]["tolerations"] == tol[:1]
