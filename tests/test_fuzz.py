@@ -70,7 +70,8 @@ spec_strategy = st.fixed_dictionaries({
 }, optional={"logLevel": st.integers(-1, 9), "hostNic": host_nic_strategy,
              "tolerations": st.lists(mostly([{"key": "amd.com/gpu", "operator": "Exists", "effect": "NoSchedule"},
                                              {"key": "dedicated", "operator": "Equal", "value": "gpu"}],
-                                            [{"operator": "Exists", "value": "x"}, {"key": "a b"}]), max_size=2)})
+                                            [{"operator": "Exists", "value": "x"}, {"key": "a b"}]), max_size=2),
+             "priorityClassName": mostly(["system-node-critical", "gpu-infra"], ["Bad_Name"])})
 op_strategy = st.tuples(st.sampled_from(["create", "update", "delete"]), st.sampled_from(["p0", "p1", "p2"]), spec_strategy)
 
 
