@@ -51,3 +51,17 @@ def test_tests_cited_in_the_docs_exist(doc):
         if cur not in src or name not in src[cur]:
             bad.append(f"{cur}::{name}")
     assert not bad, bad
+
+
+def test_every_agent_flag_is_in_the_user_guide():
+    """`discover --help` against USER_GUIDE.md §4: a new agent flag needs its row (or a mention)."""
+    import subprocess
+
+    from network_operator_amd.utils.paths import native_bin
+
+    out = subprocess.run([str(native_bin("discover")), "--help"], capture_output=True, text=True, timeout=30)
+    flags = sorted(set(re.findall(r"^\s+(--[a-z0-9_-]+)", out.stdout + out.stderr, re.M)))
+    assert len(flags) > 50, out.stdout[:500]
+    guide = (ROOT / "docs" / "USER_GUIDE.md").read_text()
+    missing = [f for f in flags if not re.search(r"`" + re.escape(f) + r"(`|[ =,])", guide)]
+    assert not missing, missing
