@@ -89,14 +89,15 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--metrics-secure", action="store_true", help="If set the metrics endpoint is served securely")
     ap.add_argument("--enable-http2", action="store_true",
                     help="If set, HTTP/2 would be enabled for the metrics and webhook servers (HTTP/1.1 only here)")
-    ap.add_argument("--kubeconfig", default=None)
+    ap.add_argument("--kubeconfig", default=None, help="kubeconfig file (default: the in-cluster service account)")
     ap.add_argument("--master", default=None, help="API server URL (overrides kubeconfig; tests)")
-    ap.add_argument("--webhook-port", type=int, default=9443)
-    ap.add_argument("--webhook-cert-dir", default=DEFAULT_CERT_DIR)
+    ap.add_argument("--webhook-port", type=int, default=9443, help="HTTPS port of the admission webhooks")
+    ap.add_argument("--webhook-cert-dir", default=DEFAULT_CERT_DIR,
+                    help="directory with tls.crt / tls.key (cert-manager's Secret); reloaded when they change")
     ap.add_argument("--workers", type=int, default=2, help="concurrent reconciles")
     ap.add_argument("--dependency-check-interval", type=float, default=60.0,
                     help="seconds between checks for Node Feature Discovery / cert-manager (0 = off)")
-    ap.add_argument("--leader-election-id", default=DEFAULT_LEASE_ID)
+    ap.add_argument("--leader-election-id", default=DEFAULT_LEASE_ID, help="name of the Lease the replicas elect through")
     # kube-controller-manager's names for client-go's LeaderElectionConfig timings; the defaults
     # are controller-runtime's (the reference does not expose them, main.go:174-175).
     ap.add_argument("--leader-elect-lease-duration", type=float, default=15.0,
@@ -115,9 +116,9 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--policies-seed-id", default="",
                     help="without --policies-owner: the id (label amd.com/policy-seeder) marking this operator's "
                          "seeded policies (default <namespace>.<leader election id>)")
-    ap.add_argument("--zap-devel", action="store_true", default=True)
-    ap.add_argument("--zap-log-level", default="info")
-    ap.add_argument("--zap-encoder", default="console", choices=["console", "json"])
+    ap.add_argument("--zap-devel", action="store_true", default=True, help="development logging defaults (controller-runtime's flag)")
+    ap.add_argument("--zap-log-level", default="info", help="debug, info, warn or error")
+    ap.add_argument("--zap-encoder", default="console", choices=["console", "json"], help="log line format")
     return ap
 
 

@@ -65,3 +65,15 @@ def test_every_agent_flag_is_in_the_user_guide():
     guide = (ROOT / "docs" / "USER_GUIDE.md").read_text()
     missing = [f for f in flags if f != "--help" and not re.search(r"`" + re.escape(f) + r"(`|[ =,])", guide)]
     assert not missing, missing
+
+
+def test_every_operator_flag_is_in_the_user_guide():
+    """The manager's argparse flags against USER_GUIDE.md's operator flag table."""
+    from network_operator_amd.operator import manager
+
+    flags = sorted({o for a in manager.build_parser()._actions for o in a.option_strings
+                    if o.startswith("--") and o != "--help"})
+    assert len(flags) > 15
+    guide = (ROOT / "docs" / "USER_GUIDE.md").read_text()
+    missing = [f for f in flags if not re.search(r"`" + re.escape(f) + r"(`|[ =,])", guide)]
+    assert not missing, missing
