@@ -77,3 +77,16 @@ def test_every_operator_flag_is_in_the_user_guide():
     guide = (ROOT / "docs" / "USER_GUIDE.md").read_text()
     missing = [f for f in flags if not re.search(r"`" + re.escape(f) + r"(`|[ =,])", guide)]
     assert not missing, missing
+
+
+def test_every_policy_field_is_in_the_user_guide():
+    """Every field of the NetworkClusterPolicy spec (amdScaleOut, hostNic, validation included)
+    is named in USER_GUIDE.md."""
+    from network_operator_amd.api.v1alpha1 import types as T
+
+    fields = set(T.AmdScaleOutSpec._FIELDS)
+    for cls in (T.HostNicSpec, T.NetworkClusterPolicySpec, T.ValidationSpec):
+        fields |= {f for f in cls.__dataclass_fields__ if f != "extra"}
+    guide = (ROOT / "docs" / "USER_GUIDE.md").read_text()
+    missing = sorted(f for f in fields if not re.search(r"\b" + f + r"\b", guide))
+    assert not missing, missing
