@@ -108,6 +108,9 @@ struct Config {
     // agent runs (mlx5_core in firmware mode): hand DCBX to the host.  Opt-in: the firmware then
     // stops negotiating PFC/ETS with the switch (ethtool.hpp).
     bool fw_lldp_dcbx_host = false;
+    // On a clean exit (not --keep-config), put every NIC's MTU back to what it was at the start
+    // (host-nic policies: the node's own NICs).
+    bool restore_mtu = false;
     std::string fw_lldp_flags;                        // extra rules "NAME=0|1,..."
     // With keep_config: the originals of what --disable-fw-lldp changed are kept in this file
     // across agent restarts (a restart does not flip the NICs back and forth: some drivers reset

@@ -20,6 +20,7 @@ struct NicState {
     std::string ifname;
     nl::LinkInfo link;
     unsigned orig_flags = 0;
+    int orig_mtu = 0;  // at discovery: put back on a clean exit with --restore-mtu
     bool expect_response = false;
 
     // LLDP

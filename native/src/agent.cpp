@@ -243,6 +243,20 @@ void Agent::post_cleanups() {
     } catch (const std::exception& e) {
         NLOG_W("Failed to remove any existing IPs from interfaces: %s", e.what());
     }
+    if (cfg_.restore_mtu) {
+        // Host NICs are the node's general-purpose interfaces: the MTU they had goes back with
+        // the agent (the reference, and amd-so by default, leave the scale-out rails at theirs).
+        for (auto& n : nics_) {
+            if (n.orig_mtu <= 0 || n.link.mtu == n.orig_mtu) continue;
+            try {
+                ops_.link_set_mtu(n.link.index, n.orig_mtu);
+                NLOG_I("Setting MTU of '%s' back to %d", n.ifname.c_str(), n.orig_mtu);
+                n.link.mtu = n.orig_mtu;
+            } catch (const std::exception& e) {
+                NLOG_W("Cannot set MTU of '%s' back to %d: %s", n.ifname.c_str(), n.orig_mtu, e.what());
+            }
+        }
+    }
     try {
         interfaces_restore_down();
     } catch (const std::exception& e) {
@@ -324,6 +338,7 @@ void Agent::get_network_configs(const std::vector<std::string>& names) {
             continue;
         }
         n.orig_flags = n.link.flags;
+        n.orig_mtu = n.link.mtu;
         for (auto& p : disc_.pairs) {
             const auto& nic = disc_.nics[size_t(p.nic)];
             if (nic.ifname != name) continue;

@@ -2330,6 +2330,30 @@ TEST(agent_rdma_discovery_leaves_a_nic_with_a_global_ipv6_address_alone) {
     CHECK_EQ(ex[0].second, std::string("the node's own NIC: it holds fd00:77::5/64, an IPv6 address the agent never assigns"));
 }
 
+TEST(agent_restore_mtu_puts_each_nics_mtu_back_on_a_clean_exit_only) {
+    // --restore-mtu (host-nic policies): MTU 9000 while the agent runs, each NIC's own MTU (1500,
+    // 4200) back after a clean exit; with --keep-config the next agent adopts the NICs as they are.
+    for (bool keep : {false, true}) {
+        Fixture f;
+        f.cfg.mode = "L2";
+        f.cfg.mtu = 9000;
+        f.cfg.restore_mtu = true;
+        f.cfg.keep_config = keep;
+        f.ops.links["ens1"].mtu = 4200;
+        Pipe stop;
+        agent::Agent a(f.cfg, f.ops, std::make_unique<ScriptedLldp>(), f.nm());
+        bool jumbo = false;
+        a.on_monitor_tick = [&](int) {
+            jumbo = f.ops.links["ens0"].mtu == 9000 && f.ops.links["ens1"].mtu == 9000;
+            stop.fire();
+        };
+        a.run(stop.fd[0]);
+        CHECK(jumbo);
+        CHECK_EQ(f.ops.links["ens0"].mtu, keep ? 9000 : 1500);
+        CHECK_EQ(f.ops.links["ens1"].mtu, keep ? 9000 : 4200);
+    }
+}
+
 TEST(agent_rdma_discovery_keeps_the_agents_own_l3_config) {
     // A host NIC an earlier (keep-config) agent addressed: its /30, the kernel /30 route, the /16
     // via the switch end and the rail table are the agent's, so the NIC is still a host NIC.

@@ -268,6 +268,8 @@ def host_nic_agent_args(p: T.NetworkClusterPolicy) -> List[str]:
         args.append(f"--v={p.spec.logLevel}")
     if hn.mtu > 0:
         args.append(f"--mtu={hn.mtu}")
+        if not hn.keepConfigOnRestart:
+            args.append("--restore-mtu")  # the node's own NICs get their MTU back when the agent goes
     if hn.disableNetworkManager:
         args += ["--disable-networkmanager", "--nm-keyfile-dir=/etc/NetworkManager/conf.d"]
     if hn.layer == "L3":
