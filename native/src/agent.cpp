@@ -737,11 +737,15 @@ void Agent::dry_run_report() {
             NLOG_W("dry run: firmware LLDP not inspected: %s", e.what());
         }
     }
+    // NICs refuse_uplinks() recorded: a real start would fail on them, and touch nothing.
+    std::set<std::string> refused;
+    for (const auto& [name, why] : excluded_)
+        if (why.size() >= 9 && why.compare(why.size() - 9, 9, "(refused)") == 0) refused.insert(name);
     for (const auto& n : nics_) {
-        NLOG_I("dry run: %s (%s, mtu %d -> %d, %s): GPU %d %s, RDMA %s, path %s", n.ifname.c_str(),
+        NLOG_I("dry run: %s (%s, mtu %d -> %d, %s): GPU %d %s, RDMA %s, path %s%s", n.ifname.c_str(),
                n.link.up() ? "up" : "down", n.link.mtu, cfg_.mtu, n.link.mac.str().c_str(), n.gpu_index,
                n.gpu_bdf.empty() ? "-" : n.gpu_bdf.c_str(), n.rdma_dev.empty() ? "-" : n.rdma_dev.c_str(),
-               n.pcie_path.empty() ? "-" : n.pcie_path.c_str());
+               n.pcie_path.empty() ? "-" : n.pcie_path.c_str(), refused.count(n.ifname) ? " -- REFUSED" : "");
     }
     if (!cfg_.rccl_topo.empty()) {
         start_topo();
@@ -758,8 +762,12 @@ void Agent::dry_run_report() {
         NLOG_I("dry run: RCCL environment file %s", cfg_.rccl_env.c_str());
     }
     write_status();
-    NLOG_I("dry run: %zu interface(s) would be configured in %s mode; nothing was changed", nics_.size(),
-           cfg_.mode.c_str());
+    if (!refused.empty())
+        NLOG_W("dry run: a real start would fail: refusing %s (the node's default route); nothing was changed",
+               join(std::vector<std::string>(refused.begin(), refused.end()), ", ").c_str());
+    else
+        NLOG_I("dry run: %zu interface(s) would be configured in %s mode; nothing was changed", nics_.size(),
+               cfg_.mode.c_str());
 }
 
 namespace {
