@@ -292,7 +292,10 @@ def crd_manifest() -> dict:
                 "schema": {"openAPIV3Schema": openapi_schema()},
                 "subresources": {"status": {}},
                 "additionalPrinterColumns": [
+                    # amd-so and host-nic policies side by side: the type, and the layer of each.
+                    {"name": "Type", "type": "string", "jsonPath": ".spec.configurationType"},
                     {"name": "Layer", "type": "string", "jsonPath": ".spec.amdScaleOut.layer"},
+                    {"name": "Host-NIC-Layer", "type": "string", "priority": 1, "jsonPath": ".spec.hostNic.layer"},
                     {"name": "Targets", "type": "integer", "jsonPath": ".status.targets"},
                     {"name": "Ready", "type": "integer", "jsonPath": ".status.ready"},
                     {"name": "State", "type": "string", "jsonPath": ".status.state"},
