@@ -111,6 +111,9 @@ struct Config {
     // On a clean exit (not --keep-config), put every NIC's MTU back to what it was at the start
     // (host-nic policies: the node's own NICs).
     bool restore_mtu = false;
+    // With restore_mtu: "ifname mtu" lines keeping each NIC's MTU from before the first agent that
+    // changed it, across --keep-config restarts, for the last clean exit or the --cleanup Job.
+    std::string mtu_state;
     std::string fw_lldp_flags;                        // extra rules "NAME=0|1,..."
     // With keep_config: the originals of what --disable-fw-lldp changed are kept in this file
     // across agent restarts (a restart does not flip the NICs back and forth: some drivers reset
@@ -337,6 +340,9 @@ class Agent {
     std::vector<ethtool::FwLldpResult> fw_lldp_carried_;
     // The record: this agent's changes (with_current) and the carried ones; removed when empty.
     void save_fw_lldp_state(bool with_current = true);
+    void load_mtu_state();       // orig_mtu of every NIC from --mtu-state (recording new ones)
+    void restore_mtus();         // each NIC's orig_mtu back; the state file's entries with it
+    void restore_mtu_state();    // --cleanup: every entry of --mtu-state back, then the file goes
     std::vector<std::pair<std::string, std::string>> rccl_env_extra_;
     void disable_fw_lldp();
     void restore_fw_lldp_from_state();

@@ -243,26 +243,109 @@ void Agent::post_cleanups() {
     } catch (const std::exception& e) {
         NLOG_W("Failed to remove any existing IPs from interfaces: %s", e.what());
     }
-    if (cfg_.restore_mtu) {
-        // Host NICs are the node's general-purpose interfaces: the MTU they had goes back with
-        // the agent (the reference, and amd-so by default, leave the scale-out rails at theirs).
-        for (auto& n : nics_) {
-            if (n.orig_mtu <= 0 || n.link.mtu == n.orig_mtu) continue;
-            try {
-                ops_.link_set_mtu(n.link.index, n.orig_mtu);
-                NLOG_I("Setting MTU of '%s' back to %d", n.ifname.c_str(), n.orig_mtu);
-                n.link.mtu = n.orig_mtu;
-            } catch (const std::exception& e) {
-                NLOG_W("Cannot set MTU of '%s' back to %d: %s", n.ifname.c_str(), n.orig_mtu, e.what());
-            }
-        }
-    }
+    if (cfg_.restore_mtu) restore_mtus();
     try {
         interfaces_restore_down();
     } catch (const std::exception& e) {
         NLOG_W("Failed to restore interfaces to original state: %s", e.what());
     }
     restore_network_manager();
+}
+
+namespace {
+std::map<std::string, int> read_mtu_state(const std::string& path) {
+    std::map<std::string, int> out;
+    auto t = read_file(path);
+    if (!t) return out;
+    for (const auto& line : split(*t, '\n')) {
+        auto f = split(trim(line), ' ');
+        if (f.size() != 2 || f[0].empty() || f[0].size() > 15) continue;
+        try {
+            const int mtu = std::stoi(f[1]);
+            if (mtu >= 68 && mtu <= 65535) out[f[0]] = mtu;
+        } catch (const std::exception&) {
+        }
+    }
+    return out;
+}
+
+void write_mtu_state(const std::string& path, const std::map<std::string, int>& m) {
+    if (m.empty()) {
+        if (::unlink(path.c_str()) != 0 && errno != ENOENT)
+            NLOG_W("Could not remove %s: %s", path.c_str(), std::strerror(errno));
+        return;
+    }
+    std::string t;
+    for (const auto& [n, mtu] : m) t += n + " " + std::to_string(mtu) + "\n";
+    write_file_atomic(path, t);
+}
+}  // namespace
+
+void Agent::load_mtu_state() {
+    // The first agent's view of each NIC is the original; a later (--keep-config) agent finds the
+    // MTU it set itself, so the recorded value wins.
+    if (!cfg_.restore_mtu || cfg_.mtu_state.empty()) return;
+    auto m = read_mtu_state(cfg_.mtu_state);
+    for (auto& n : nics_) {
+        auto it = m.find(n.ifname);
+        if (it == m.end())
+            m[n.ifname] = n.orig_mtu;
+        else
+            n.orig_mtu = it->second;
+    }
+    try {
+        write_mtu_state(cfg_.mtu_state, m);
+    } catch (const std::exception& e) {
+        NLOG_W("Could not record the NICs' MTUs in %s: %s", cfg_.mtu_state.c_str(), e.what());
+    }
+}
+
+void Agent::restore_mtus() {
+    // Host NICs are the node's general-purpose interfaces: the MTU they had goes back with the
+    // agent (the reference, and amd-so, leave the scale-out rails at the policy's MTU).
+    std::map<std::string, int> left = cfg_.mtu_state.empty() ? std::map<std::string, int>{}
+                                                              : read_mtu_state(cfg_.mtu_state);
+    for (auto& n : nics_) {
+        if (n.orig_mtu <= 0) continue;
+        bool ok = n.link.mtu == n.orig_mtu;
+        if (!ok) {
+            try {
+                ops_.link_set_mtu(n.link.index, n.orig_mtu);
+                NLOG_I("Setting MTU of '%s' back to %d", n.ifname.c_str(), n.orig_mtu);
+                n.link.mtu = n.orig_mtu;
+                ok = true;
+            } catch (const std::exception& e) {
+                NLOG_W("Cannot set MTU of '%s' back to %d: %s", n.ifname.c_str(), n.orig_mtu, e.what());
+            }
+        }
+        if (ok) left.erase(n.ifname);
+    }
+    if (!cfg_.mtu_state.empty()) {
+        try {
+            write_mtu_state(cfg_.mtu_state, left);  // what could not be put back stays for --cleanup
+        } catch (const std::exception& e) {
+            NLOG_W("Could not update %s: %s", cfg_.mtu_state.c_str(), e.what());
+        }
+    }
+}
+
+void Agent::restore_mtu_state() {
+    if (!cfg_.restore_mtu || cfg_.mtu_state.empty()) return;
+    auto m = read_mtu_state(cfg_.mtu_state);
+    std::map<std::string, int> left;
+    for (const auto& [name, mtu] : m) {
+        try {
+            auto l = ops_.link_by_name(name);
+            if (l.mtu != mtu) {
+                ops_.link_set_mtu(l.index, mtu);
+                NLOG_I("Setting MTU of '%s' back to %d", name.c_str(), mtu);
+            }
+        } catch (const std::exception& e) {
+            NLOG_W("Cannot set MTU of '%s' back to %d: %s", name.c_str(), mtu, e.what());
+            left[name] = mtu;
+        }
+    }
+    write_mtu_state(cfg_.mtu_state, left);
 }
 
 void Agent::restore_network_manager() {
@@ -1314,6 +1397,7 @@ void Agent::run(int stop_fd) {
     }
     interfaces_up();
     mark("link_up");
+    load_mtu_state();
     interfaces_set_mtu();
     mark("mtu");
     try {
@@ -1553,6 +1637,12 @@ void Agent::cleanup_node() {
         restore_fw_lldp_from_state();
     } catch (const std::exception& e) {
         NLOG_W("Could not restore the NICs' firmware LLDP settings: %s", e.what());
+        ++errors;
+    }
+    try {
+        restore_mtu_state();
+    } catch (const std::exception& e) {
+        NLOG_W("Could not restore the NICs' MTUs: %s", e.what());
         ++errors;
     }
     if (cfg_.disable_nm) {

@@ -2354,6 +2354,51 @@ TEST(agent_restore_mtu_puts_each_nics_mtu_back_on_a_clean_exit_only) {
     }
 }
 
+TEST(agent_mtu_state_keeps_the_original_mtu_across_keep_config_restarts_for_the_cleanup) {
+    // Host NICs with keepConfigOnRestart: the first agent records ens1's own MTU (4200) before it
+    // sets 9000; a restarted agent finds 9000 on the NIC but keeps the recorded 4200; the cleanup
+    // Job puts 4200 back and removes the record.  Without --keep-config a clean exit does it.
+    Fixture f;
+    f.cfg.mode = "L2";
+    f.cfg.mtu = 9000;
+    f.cfg.restore_mtu = true;
+    f.cfg.keep_config = true;
+    f.cfg.keep_running = false;
+    f.cfg.mtu_state = f.tmp.path + "/mtu-state";
+    f.ops.links["ens1"].mtu = 4200;
+    for (int restart = 0; restart < 2; ++restart) {
+        agent::Agent a(f.cfg, f.ops, std::make_unique<ScriptedLldp>(), f.nm());
+        a.run(-1);
+        CHECK_EQ(f.ops.links["ens1"].mtu, 9000);
+        auto st = read_file(f.cfg.mtu_state);
+        CHECK(st && *st == "ens0 1500\nens1 4200\nens2 1500\n");
+    }
+    agent::Config c = f.cfg;
+    c.cleanup = true;
+    {
+        agent::Agent a(c, f.ops, std::make_unique<ScriptedLldp>(), f.nm());
+        a.run(-1);
+    }
+    CHECK_EQ(f.ops.links["ens1"].mtu, 4200);
+    CHECK_EQ(f.ops.links["ens0"].mtu, 1500);
+    CHECK(!path_exists(f.cfg.mtu_state));
+
+    Fixture g;  // no --keep-config: the clean exit (SIGTERM) restores and leaves no record
+    g.cfg.mode = "L2";
+    g.cfg.mtu = 9000;
+    g.cfg.restore_mtu = true;
+    g.cfg.mtu_state = g.tmp.path + "/mtu-state";
+    {
+        Pipe stop;
+        stop.fire();
+        agent::Agent a(g.cfg, g.ops, std::make_unique<ScriptedLldp>(), g.nm());
+        a.run(stop.fd[0]);
+        CHECK(a.ready());
+    }
+    CHECK_EQ(g.ops.links["ens0"].mtu, 1500);
+    CHECK(!path_exists(g.cfg.mtu_state));
+}
+
 TEST(agent_rdma_discovery_keeps_the_agents_own_l3_config) {
     // A host NIC an earlier (keep-config) agent addressed: its /30, the kernel /30 route, the /16
     // via the switch end and the rail table are the agent's, so the NIC is still a host NIC.

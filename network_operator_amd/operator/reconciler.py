@@ -254,6 +254,7 @@ def update_amd_scale_out_daemonset(ds: dict, p: T.NetworkClusterPolicy, namespac
 HOST_NIC_LABEL = "amd.feature.node.kubernetes.io/host-nic-ready"
 HOST_NIC_LABEL_FILE = "host-nic-readiness.txt"
 HOST_NIC_LLDP_CACHE_FILE = "host-nic-lldp-cache"
+HOST_NIC_MTU_STATE_FILE = "host-nic-mtu-state"  # --mtu-state: the host NICs' own MTUs
 DRIVER_CONTAINER = "nic-driver"
 
 
@@ -267,9 +268,9 @@ def host_nic_agent_args(p: T.NetworkClusterPolicy) -> List[str]:
     if p.spec.logLevel > 0:
         args.append(f"--v={p.spec.logLevel}")
     if hn.mtu > 0:
-        args.append(f"--mtu={hn.mtu}")
-        if not hn.keepConfigOnRestart:
-            args.append("--restore-mtu")  # the node's own NICs get their MTU back when the agent goes
+        # The node's own NICs get their MTU back when the agent goes for good: on a clean exit, or
+        # (keepConfigOnRestart) from the record the cleanup Job reads.
+        args += [f"--mtu={hn.mtu}", "--restore-mtu", f"--mtu-state={ARTIFACT_DIR_CONTAINER}/{HOST_NIC_MTU_STATE_FILE}"]
     if hn.disableNetworkManager:
         args += ["--disable-networkmanager", "--nm-keyfile-dir=/etc/NetworkManager/conf.d"]
     if hn.layer == "L3":
@@ -311,7 +312,7 @@ def update_host_nic_daemonset(ds: dict, p: T.NetworkClusterPolicy, namespace: st
         add_host_volume(ds, "var-run-dbus", "/var/run/dbus", "/var/run/dbus")
         add_host_volume(ds, "networkmanager", "/etc/NetworkManager", "/etc/NetworkManager")
         wanted |= {"var-run-dbus", "networkmanager"}
-    if hn.keepConfigOnRestart and hn.layer == "L3":  # the LLDP cache outlives the Pod
+    if (hn.keepConfigOnRestart and hn.layer == "L3") or hn.mtu > 0:  # the LLDP cache / MTU record outlive the Pod
         add_host_volume(ds, "rccl-artifacts", ARTIFACT_DIR_HOST, ARTIFACT_DIR_CONTAINER)
         wanted.add("rccl-artifacts")
     # Optional kernel-driver container: privileged, sees the host's modules, runs to completion

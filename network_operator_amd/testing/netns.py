@@ -690,7 +690,8 @@ def run_host_nic_ownership(mode: str = "L2", rails: int = 8, mgmt_bridge: bool =
         feat.mkdir()
         label = feat / "host-nic-readiness.txt"
         base = [str(native_bin("discover")), "--configure=true", "--keep-running", f"--mode={mode}", "--mtu=9000",
-                "--restore-mtu", f"--nfd-features-dir={feat}", "--nfd-label-file=host-nic-readiness.txt",
+                "--restore-mtu", f"--mtu-state={tmp / 'mtu-state'}", f"--nfd-features-dir={feat}",
+                "--nfd-label-file=host-nic-readiness.txt",
                 "--nfd-label=amd.feature.node.kubernetes.io/host-nic-ready", "--wait=3s", "-v=2"]
         env = dict(os.environ, SYSFS_ROOT=str(tmp / "sys"), NODE_NAME="mi355x-node-0")
         res: dict = {"rails": rail_names, "before": snapshot(),
@@ -718,6 +719,7 @@ def run_host_nic_ownership(mode: str = "L2", rails: int = 8, mgmt_bridge: bool =
             agent.wait()
         res["agent_rc"] = agent.returncode
         res["after_sigterm"] = snapshot()
+        res["mtu_state_left"] = (tmp / "mtu-state").exists()
         res["agent_log"] = log_path.read_text(errors="replace")[-6000:]
         # The management NIC named explicitly: refused, nothing touched.
         r = subprocess.run([*base, "--nic-discovery=none", f"--interfaces={MGMT_NIC}"], env=env, capture_output=True,

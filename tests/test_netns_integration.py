@@ -415,6 +415,7 @@ def test_default_host_nic_policy_leaves_the_management_nic_and_the_gpu_rails_alo
     assert r["while_ready"][netns.HOST_NIC] == {"up": True, "mtu": 9000, "addrs": [], "master": 0}
     assert r["after_sigterm"][netns.HOST_NIC]["up"] is False  # restored to its original state
     assert r["after_sigterm"][netns.HOST_NIC]["mtu"] == 1500  # --restore-mtu (the operator passes it for host-nic)
+    assert r["mtu_state_left"] is False  # every MTU went back: the record goes with the agent
     assert r["agent_rc"] == 0
     named = r["named_mgmt"]
     assert named["rc"] == 1 and f"Refusing to configure {netns.MGMT_NIC}{via}: the node's default route" in named["stderr"]
