@@ -21,3 +21,5 @@ timeout -k 10 120 network_operator_amd/_lib/netop-xgmi-counters > gpurun_out/xgm
 cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/prof -o bench --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --gpus 1 --steps 10 --warmup 3 > $GRAFT_REPO_ROOT/gpurun_out/prof.log 2>&1 || { tail -20 $GRAFT_REPO_ROOT/gpurun_out/prof.log; exit 1; }
 echo PROF OK
 find $GRAFT_REPO_ROOT/gpurun_out/prof -name '*stats*'
+# The default-route refusal on the box's own kernel (unprivileged dry runs).
+cd $GRAFT_REPO_ROOT && bash tools/gpu_uplink.sh && tail -2 gpurun_out/box_uplink.log
