@@ -9,7 +9,6 @@ and kubeconfig credentials.  Service-account tokens are re-read from disk so pro
 
 from __future__ import annotations
 
-import asyncio
 import base64
 import json
 import os
@@ -346,12 +345,3 @@ class ApiClient:
         return [g["name"] for g in r.get("groups", [])]
 
 
-async def retry_on_conflict(fn, attempts: int = 5, backoff: float = 0.01):
-    """client-go's retry.RetryOnConflict: re-run a read-modify-write on 409 Conflict."""
-    for i in range(attempts):
-        try:
-            return await fn()
-        except ApiError as e:
-            if not is_conflict(e) or i == attempts - 1:
-                raise
-            await asyncio.sleep(backoff * (2 ** i))
