@@ -72,7 +72,8 @@ class PolicyController:
             list_pods=lambda ds: self.pods.by_index(OWNER_KEY, ds),
             list_jobs=lambda name: self.jobs.by_index(OWNER_KEY, name),
             list_job_pods=lambda job: self.job_pods.by_index(OWNER_KEY, job),
-            list_probe_events=lambda pod: self.probe_events.by_index(PROBE_EVENT_KEY, pod))
+            list_probe_events=lambda pod: self.probe_events.by_index(PROBE_EVENT_KEY, pod),
+            list_policies=self.policies.list)
         self.reconciler.on_cleanup = lambda policy, outcome: self.metrics.node_cleanups.labels(policy, outcome).inc()
         self.policies.add_handler(self._on_policy)
         self.daemonsets.add_handler(self._on_daemonset)
@@ -100,6 +101,22 @@ class PolicyController:
             if owner and owner.get("kind") == T.KIND:
                 self._observe_readiness(owner["name"], ev, obj, old)
                 await self._enqueue(owner["name"])
+                if ev in ("ADDED", "DELETED"):
+                    await self._enqueue_others(owner["name"])
+            elif ds is None and ev in ("ADDED", "DELETED"):
+                # The DaemonSet is not in the cache (yet: the watches are separate streams; or any
+                # more: its policy is gone): every policy may share, or no longer share, this node.
+                await self._enqueue_others(None)
+
+    async def _enqueue_others(self, name: Optional[str]) -> None:
+        """An agent Pod came or went: the other policies of its type may now share (or no longer
+        share) its node, and their status says so (reconciler.conflict_errors).  Without a known
+        owner, every policy."""
+        me = self.policies.get(name) if name else None
+        ctype = ((me or {}).get("spec") or {}).get("configurationType", "") if me else None
+        for p in self.policies.list():
+            if p["metadata"]["name"] != name and (ctype is None or (p.get("spec") or {}).get("configurationType", "") == ctype):
+                await self._enqueue(p["metadata"]["name"])
 
     async def _on_job(self, ev: str, obj: dict, old: Optional[dict]) -> None:
         ref = controller_of(obj)

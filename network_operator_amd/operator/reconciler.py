@@ -30,7 +30,7 @@ import copy
 import time
 import logging
 from dataclasses import dataclass
-from typing import Callable, List, Optional
+from typing import Callable, Dict, List, Optional
 
 from .. import discovery
 from ..api.v1alpha1 import types as T
@@ -439,6 +439,29 @@ def _container_running(pod: dict) -> bool:
     return any("running" in (cs.get("state") or {}) for cs in (pod.get("status") or {}).get("containerStatuses") or [])
 
 
+# Two policies of one configurationType that select the same node run two agents there; they
+# share the node lock (named after the type's NFD label), so the later one waits and then fails.
+# The operator says so at once on the newer policy (status.errors, Degraded/PolicyConflict, a
+# Warning Event), naming the older one; the older policy's own status stays as its agents are.
+CONFLICT_MARK = ": also selected by policy "
+
+
+def conflict_errors(policy: str, ctype: str, mine: List[str], others: Dict[str, List[str]], limit: int = 3) -> List[str]:
+    """status.errors entries for the nodes ``mine`` shares with each policy in ``others`` (name ->
+    nodes of its agent Pods; same configurationType), one entry per other policy."""
+    out = []
+    own = set(mine)
+    for other in sorted(others):
+        shared = sorted(own.intersection(others[other]))
+        if not shared:
+            continue
+        nodes = ", ".join(shared[:limit]) + (f" and {len(shared) - limit} more" if len(shared) > limit else "")
+        out.append(f"{nodes}{CONFLICT_MARK}{other} ({ctype} too, created earlier): one agent per node and type "
+                   f"configures the NICs, so this policy's agent there waits for the node lock and fails; "
+                   f"narrow a nodeSelector")
+    return out
+
+
 def policy_conditions(current: List[dict], targets: int, ready: int, errors: List[str], generation: int,
                       now: Optional[str] = None) -> List[dict]:
     """The policy's Ready / Degraded conditions (additive to the reference's state string,
@@ -455,6 +478,8 @@ def policy_conditions(current: List[dict], targets: int, ready: int, errors: Lis
                        generation, now)
     if any(e.startswith("dependency missing") for e in errors):
         _set_condition(conds, COND_DEGRADED, "True", "DependencyMissing", "; ".join(errors)[:1024], generation, now)
+    elif any(CONFLICT_MARK in e for e in errors):
+        _set_condition(conds, COND_DEGRADED, "True", "PolicyConflict", "; ".join(errors)[:1024], generation, now)
     elif errors:
         _set_condition(conds, COND_DEGRADED, "True", "AgentErrors", "; ".join(errors)[:1024], generation, now)
     else:
@@ -684,7 +709,8 @@ class NetworkClusterPolicyReconciler:
                  list_jobs: Optional[Callable[[str], List[dict]]] = None,
                  list_job_pods: Optional[Callable[[str], List[dict]]] = None,
                  clock: Callable[[], float] = time.time,
-                 list_probe_events: Optional[Callable[[str], List[dict]]] = None):
+                 list_probe_events: Optional[Callable[[str], List[dict]]] = None,
+                 list_policies: Optional[Callable[[], List[dict]]] = None):
         self.client = client
         self.namespace = namespace
         self.is_openshift = is_openshift
@@ -697,6 +723,7 @@ class NetworkClusterPolicyReconciler:
         self._list_jobs = list_jobs  # validation Jobs of a policy (by its name)
         self._list_job_pods = list_job_pods  # the Pods of a validation Job (by its name)
         self._list_probe_events = list_probe_events  # kubelet "Unhealthy" events of an agent Pod (by its name)
+        self._list_policies = list_policies  # every policy (the informer cache): conflicting selections
         self._degraded_errors: set = set()  # status.errors entries that came from a probe, not an exit
         self._clock = clock
         self.recorder = recorder
@@ -732,6 +759,30 @@ class NetworkClusterPolicyReconciler:
         if len(errs) > limit:
             errs = errs[:limit] + [f"... and {len(errs) - limit} more"]
         return errs
+
+    def _conflicts(self, p: T.NetworkClusterPolicy, ds_name: str) -> List[str]:
+        """Nodes this policy's agents share with an older live policy of the same type (from the
+        agent Pods both DaemonSets placed: what the scheduler did, selector, taints and all).
+        Older: earlier creationTimestamp, the name breaking a tie (the timestamps have seconds)."""
+        if self._list_policies is None or self._list_pods is None:
+            return []
+        me = (p.metadata.get("creationTimestamp") or "", p.name)
+
+        def nodes(ds: str) -> List[str]:
+            return [n for n in ((pod.get("spec") or {}).get("nodeName") for pod in self._list_pods(ds)) if n]
+        mine = nodes(ds_name)
+        if not mine:
+            return []
+        others = {}
+        for q in self._list_policies():
+            md = q.get("metadata") or {}
+            if md.get("name") == p.name or md.get("deletionTimestamp") or \
+                    (md.get("creationTimestamp") or "", md.get("name", "")) > me:
+                continue
+            if (q.get("spec") or {}).get("configurationType", "") != p.spec.configurationType:
+                continue
+            others[md["name"]] = nodes(md["name"])
+        return conflict_errors(p.name, p.spec.configurationType, mine, others)
 
     async def _delete_job(self, j: dict) -> None:
         try:
@@ -1109,6 +1160,7 @@ class NetworkClusterPolicyReconciler:
             updated = True
         new_state = status_for(targets, ready)
         errors = [f"dependency missing: {d}" for d in self.missing_dependencies]
+        errors += self._conflicts(p, ds["metadata"]["name"])
         errors += self._node_errors(ds["metadata"]["name"]) if targets and ready < targets else []
         generation = int(raw.get("metadata", {}).get("generation", 0) or 0)
         # Validation first: it adds its failed nodes to `errors`, and the comparison with the stored
@@ -1147,7 +1199,9 @@ class NetworkClusterPolicyReconciler:
         if cur.state != new_state and new_state == STATE_ALL_GOOD:
             await self._event(raw, "Normal", "AllNodesReady", f"{ready}/{targets} nodes configured")
         for e in errors:  # an agent that exited / a node that degraded, with its reason: once per new message
-            if e not in cur.errors and "scale-out not ready (" in e and "): " in e:
+            if e not in cur.errors and CONFLICT_MARK in e:
+                await self._event(raw, "Warning", "PolicyConflict", e[:1024])
+            elif e not in cur.errors and "scale-out not ready (" in e and "): " in e:
                 if e in self._degraded_errors:
                     await self._event(raw, "Warning", "NodeDegraded", e[:1024])
                 elif not e.endswith(tuple(STARTUP_REASONS)):

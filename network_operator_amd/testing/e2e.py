@@ -402,9 +402,10 @@ async def _scenario(tmp: Path, n_nics: int, mode: str, seed: int, interval: str,
                 await c.create(P, T.new_policy("scale-out-dup", layer=mode, mtu=9000, **policy_kw).to_dict())
 
                 def dup_error():
+                    # the operator's conflict entry (at once) and the agent's own (once it gave up)
                     st = (fake.get_object(P, "scale-out-dup") or {}).get("status") or {}
                     return [e for e in st.get("errors") or [] if "node lock" in e]
-                await _until(lambda: bool(dup_error()), 20)
+                await _until(lambda: any("holds the node lock" in e for e in dup_error()), 20)
                 res["duplicate_policy_errors"] = dup_error()
                 res["duplicate_policy_status"] = (fake.get_object(P, "scale-out-dup") or {}).get("status")
                 res["first_policy_status_after_duplicate"] = (fake.get_object(P, name) or {}).get("status")

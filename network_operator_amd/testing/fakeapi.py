@@ -190,6 +190,7 @@ class FakeApiServer:
         self.openshift = openshift
         self.objects: Dict[Tuple[str, str, str], Dict[Tuple[str, str], dict]] = {}
         self._owned: Dict[str, set] = {}  # owner uid -> {(resource, namespace, name)} (garbage collector)
+        self._live_uids: set = set()  # uids of the stored objects: a dependent of none of them is collected
         self.rv = 100
         self.events: List[Tuple[int, Resource, str, dict]] = []
         self.history = history
@@ -439,13 +440,32 @@ class FakeApiServer:
             obj["status"] = {"currentNumberScheduled": 0, "desiredNumberScheduled": 0, "numberMisscheduled": 0,
                              "numberReady": 0, "observedGeneration": 1}
         stored = self._store(res, obj, "ADDED")
+        self._live_uids.add(md["uid"])
         if res in (kube.DAEMONSETS, kube.NODES):
             self._sync_daemonsets()
         created = self._table(res)[key]
-        if any(r.get("uid") in self._foreground for r in md.get("ownerReferences") or []):
+        refs = [r.get("uid") for r in md.get("ownerReferences") or []]
+        if any(u in self._foreground for u in refs):
             # A dependent of an owner in foreground deletion: the garbage collector deletes it.
             self._delete_or_mark(res, md["name"], key[0])
+        elif refs and not any(u in self._live_uids for u in refs):
+            # Every owner is gone already (a controller acting on a stale cache): the collector
+            # finds the dangling references and deletes the dependent, as it does with any other.
+            uid = md["uid"]
+            if self.gc_delay <= 0:
+                self._collect_dangling(res, key[0], md["name"], uid)
+            else:
+                self._bg.append(asyncio.ensure_future(self._collect_dangling_later(res, key[0], md["name"], uid)))
         return created
+
+    def _collect_dangling(self, res: Resource, ns: str, name: str, uid: str) -> None:
+        o = self._table(res).get((ns, name))
+        if o is not None and o["metadata"].get("uid") == uid:
+            self._delete_or_mark(res, name, ns)
+
+    async def _collect_dangling_later(self, res: Resource, ns: str, name: str, uid: str) -> None:
+        await asyncio.sleep(self.gc_delay)
+        self._collect_dangling(res, ns, name, uid)
 
     def _delete(self, res: Resource, name: str, namespace: str) -> dict:
         key = (namespace if res.namespaced else "", name)
@@ -455,6 +475,7 @@ class FakeApiServer:
         obj["metadata"]["resourceVersion"] = str(self.rv)
         self._emit(res, "DELETED", obj)
         uid = obj["metadata"].get("uid")
+        self._live_uids.discard(uid)
         if self.gc_delay <= 0:
             self._collect(uid)
         else:
@@ -599,6 +620,12 @@ class FakeApiServer:
         for pname, node in want.items():
             ready = bool(self.node_ready.get((f"{ns}/{name}", node)))
             cur = pods.get((ns, pname))
+            if cur is not None and not any(r.get("uid") == ds["metadata"]["uid"]
+                                           for r in cur["metadata"].get("ownerReferences") or []):
+                # The Pod of an earlier DaemonSet of this name that the collector has not reached
+                # yet (Pod names here are <daemonset>-<node>, not random): it goes, ours comes.
+                self._delete(kube.PODS, pname, ns)
+                cur = None
             # lastTransitionTime moves only when the condition flips (the kubelet's status manager)
             old_ready = next((c for c in ((cur or {}).get("status") or {}).get("conditions") or []
                               if c.get("type") == "Ready"), None)

@@ -247,3 +247,26 @@ def test_foreground_deletion_waits_for_dependents_and_collects_new_ones():
         assert fake.get_object(kube.JOBS, "after", "ns") is None  # background GC once the owner is gone
         assert fake.get_object(kube.JOBS, "unowned", "ns") is not None
     _run(body, foreground_hold=0.2)
+
+
+def test_a_dependent_created_after_its_owner_is_gone_is_collected():
+    """The garbage collector's dangling-reference rule: a controller acting on a stale cache
+    creates a DaemonSet owned by a policy deleted a moment before; it is accepted and then
+    deleted.  A dependent with one live owner out of two stays."""
+    async def body(fake, c):
+        p = await c.create(P, _policy())
+        q = await c.create(P, _policy("q"))
+        ref = {"apiVersion": T.API_VERSION, "kind": T.KIND, "name": "p", "uid": p["metadata"]["uid"], "controller": True}
+        await c.delete(P, "p")
+
+        def ds(name, refs):
+            return {"apiVersion": "apps/v1", "kind": "DaemonSet", "metadata": {"name": name, "ownerReferences": refs},
+                    "spec": {"selector": {"matchLabels": {"app": "x"}},
+                             "template": {"metadata": {"labels": {"app": "x"}}, "spec": {"containers": [{"name": "c"}]}}}}
+        created = await c.create(DS, ds("late", [ref]), namespace="ns")
+        assert created["metadata"]["name"] == "late"
+        assert fake.get_object(DS, "late", "ns") is None
+        live = {"apiVersion": T.API_VERSION, "kind": T.KIND, "name": "q", "uid": q["metadata"]["uid"]}
+        await c.create(DS, ds("shared", [ref, live]), namespace="ns")
+        assert fake.get_object(DS, "shared", "ns") is not None
+    _run(body)

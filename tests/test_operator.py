@@ -1410,3 +1410,168 @@ def test_rail_switch_pattern_random_corpus_never_admits_what_the_agent_rejects(n
         for name in names:
             assert native.ecmascript_full_match(q, name) == bool(re.fullmatch(q, name)), (p, name)
     assert admitted > 2000  # the sweep exercised the accepting side too (1M patterns: 0 disagreements)
+
+
+def test_conflict_errors_name_the_other_policy_and_the_shared_nodes():
+    from network_operator_amd.operator.reconciler import CONFLICT_MARK, conflict_errors
+
+    assert conflict_errors("a", "amd-so", ["n1"], {}) == []
+    assert conflict_errors("a", "amd-so", ["n1", "n2"], {"b": ["n3"]}) == []
+    errs = conflict_errors("a", "amd-so", ["n1", "n2", "n3", "n4", "n5"], {"c": ["n5"], "b": ["n5", "n4", "n3", "n2"]})
+    assert [e.split(CONFLICT_MARK)[1].split(" ")[0] for e in errs] == ["b", "c"]
+    assert errs[0].startswith("n2, n3, n4 and 1 more" + CONFLICT_MARK + "b (amd-so too, created earlier)")
+    assert errs[1].startswith("n5" + CONFLICT_MARK + "c (amd-so too, created earlier)")
+
+
+def test_two_policies_of_one_type_on_the_same_nodes_are_reported_on_both():
+    """Two amd-so policies select the same nodes: the newer one's status names the older one and
+    the shared nodes at once (Degraded/PolicyConflict, a Warning Event) instead of its agents
+    failing on the node lock a minute later; the older one's status is its agents' own.  A
+    host-nic policy on the same nodes is no conflict.  Narrowing a selector clears it, and so does
+    deleting the older policy."""
+    async def body():
+        async with cluster(openshift=False, agent_ready_delay=0.01) as (fake, client, ctl):
+            for i in range(3):
+                fake.add_node(f"n{i}", {"foo": "bar", "rack": "a" if i < 2 else "b"})
+            await client.create(kube.NETWORKCLUSTERPOLICIES, policy("one"))
+            await client.create(kube.NETWORKCLUSTERPOLICIES, policy("two"))
+            hn = T.new_host_nic_policy("hosts", node_selector={"foo": "bar"}).to_dict()
+            await client.create(kube.NETWORKCLUSTERPOLICIES, hn)
+
+            def st(name):
+                return fake.get_object(kube.NETWORKCLUSTERPOLICIES, name)["status"]
+
+            def conflicted(name, other, nodes):
+                def check():
+                    s = st(name)
+                    assert len(s["errors"]) == 1 and s["errors"][0].startswith(f"{nodes}: also selected by policy {other} "), s
+                    c = {x["type"]: x for x in s["conditions"]}
+                    assert c["Degraded"]["status"] == "True" and c["Degraded"]["reason"] == "PolicyConflict"
+                    assert s["ready"] == s["targets"]  # the conflict is not a readiness verdict
+                return check
+
+            def clean(name, targets):
+                def check():
+                    s = st(name)
+                    assert s["errors"] == [] and s["targets"] == targets, s
+                    assert {x["type"]: x for x in s["conditions"]}["Degraded"]["reason"] == "AsExpected"
+                return check
+            await eventually(conflicted("two", "one", "n0, n1, n2"))
+            await eventually(clean("one", 3))
+            await eventually(clean("hosts", 3))
+            events = [e for e in fake.list_objects(kube.EVENTS) if e.get("reason") == "PolicyConflict"]
+            assert {e["involvedObject"]["name"] for e in events} == {"two"}
+
+            await edit(client, "two", lambda cur: cur["spec"].update(nodeSelector={"rack": "b"}))
+            await eventually(conflicted("two", "one", "n2"))
+            await edit(client, "one", lambda cur: cur["spec"].update(nodeSelector={"rack": "a"}))
+            await eventually(clean("two", 1))
+            await eventually(clean("one", 2))
+
+            await edit(client, "two", lambda cur: cur["spec"].update(nodeSelector={"foo": "bar"}))
+            await eventually(conflicted("two", "one", "n0, n1"))
+            await client.delete(kube.NETWORKCLUSTERPOLICIES, "one")
+            await eventually(clean("two", 3))
+            await eventually(clean("hosts", 3))
+
+    run(body())
+
+
+@pytest.mark.parametrize("seed,gc_delay", [(s, d) for s in range(1, 7) for d in (0.0, 0.05)])
+def test_random_edits_converge_to_the_policies_the_cluster_asks_for(seed, gc_delay):
+    """Model check through the controller loop: a random sequence of policy creates / edits /
+    deletes (both types, both layers, selectors, tolerations), node relabels and DaemonSet
+    deletions, applied with and without pauses between them, with and without a garbage collector
+    that lags.  Once it settles, every live policy has exactly its DaemonSet (selector,
+    tolerations, --mode) and a status that matches a model of the cluster: targets, ready, and a
+    PolicyConflict entry for each older same-type policy it shares nodes with -- nothing left over
+    from the states it passed through."""
+    import random
+
+    rng = random.Random(seed)
+    taint = [{"key": "amd.com/gpu", "value": "present", "effect": "NoSchedule"}]
+    tol = [{"key": "amd.com/gpu", "operator": "Exists", "effect": "NoSchedule"}]
+    selectors = [{"rack": "a"}, {"rack": "b"}, {"gpu": "yes"}, {"rack": "a", "gpu": "yes"}]
+
+    async def body():
+        # agents turn ready 20 ms after their Pod is placed, on every DaemonSet the run makes
+        async with cluster(openshift=False, workers=3, gc_delay=gc_delay, agent_ready_delay=0.02) as (fake, client, ctl):
+            nodes = {}
+            for i in range(6):
+                labels = {"rack": rng.choice("ab"), **({"gpu": "yes"} if rng.random() < 0.5 else {})}
+                nodes[f"n{i}"] = (labels, i == 5)  # n5 is tainted
+                fake.add_node(f"n{i}", labels, taints=taint if i == 5 else None)
+            model = {}  # name -> (type, layer, selector, tolerates)
+
+            def spec_of(name, ctype):
+                sel, layer, tols = rng.choice(selectors), rng.choice(["L2", "L3"]), rng.random() < 0.5
+                if ctype == "amd-so":
+                    d = T.new_policy(name, layer=layer, node_selector=sel).to_dict()
+                else:
+                    d = T.new_host_nic_policy(name, layer=layer, node_selector=sel).to_dict()
+                if tols:
+                    d["spec"]["tolerations"] = tol
+                return d, (ctype, layer, sel, tols)
+
+            for _ in range(40):
+                op = rng.random()
+                names = sorted(model)
+                if op < 0.3 or not names:
+                    name = rng.choice([n for n in ("p0", "p1", "p2", "p3", "p4") if n not in model] or ["p0"])
+                    if name in model:
+                        continue
+                    body_, m = spec_of(name, rng.choice(["amd-so", "amd-so", "host-nic"]))
+                    await client.create(kube.NETWORKCLUSTERPOLICIES, body_)
+                    model[name] = m
+                elif op < 0.55:
+                    name = rng.choice(names)
+                    ctype = model[name][0]
+                    new, m = spec_of(name, ctype)
+                    await edit(client, name, lambda cur: cur.__setitem__("spec", new["spec"]))
+                    model[name] = m
+                elif op < 0.7:
+                    name = rng.choice(names)
+                    await client.delete(kube.NETWORKCLUSTERPOLICIES, name)
+                    del model[name]
+                elif op < 0.85:
+                    n = rng.choice(sorted(nodes))
+                    labels = {"rack": rng.choice("ab"), **({"gpu": "yes"} if rng.random() < 0.5 else {})}
+                    nodes[n] = (labels, nodes[n][1])
+                    fake.set_node_labels(n, labels)
+                else:
+                    name = rng.choice(names)
+                    if fake.get_object(kube.DAEMONSETS, name, NS) is not None:
+                        with contextlib.suppress(ApiError):
+                            await client.delete(kube.DAEMONSETS, name, NS)
+                if rng.random() < 0.5:
+                    await asyncio.sleep(rng.choice([0.0, 0.01, 0.05]))
+
+            def placed(m):
+                _, _, sel, tols = m
+                return sorted(n for n, (labels, tainted) in nodes.items()
+                              if all(labels.get(k) == v for k, v in sel.items()) and (tols or not tainted))
+
+            def converged():
+                dss = {d["metadata"]["name"] for d in fake.list_objects(kube.DAEMONSETS)}
+                assert dss == set(model), (dss, model)
+                for name, m in model.items():
+                    ctype, layer, sel, tols = m
+                    ds = fake.get_object(kube.DAEMONSETS, name, NS)
+                    pod = ds["spec"]["template"]["spec"]
+                    assert pod["nodeSelector"] == sel
+                    assert (pod.get("tolerations") == tol) if tols else not pod.get("tolerations")
+                    assert f"--mode={layer}" in pod["containers"][0]["args"]
+                    assert ds["metadata"]["ownerReferences"][0]["name"] == name
+                    s = fake.get_object(kube.NETWORKCLUSTERPOLICIES, name)["status"]
+                    mine = placed(m)
+                    assert s["targets"] == len(mine) and s["ready"] == len(mine), (name, s, mine)
+                    def age(n):
+                        return (fake.get_object(kube.NETWORKCLUSTERPOLICIES, n)["metadata"]["creationTimestamp"], n)
+                    others = sorted(o for o, om in model.items()
+                                    if o != name and om[0] == ctype and age(o) < age(name) and set(placed(om)) & set(mine))
+                    got = sorted(e.split(" also selected by policy ")[1].split(" ")[0] for e in s["errors"])
+                    assert got == others and len(s["errors"]) == len(others), (name, s["errors"], others)
+                return True
+            await eventually(converged, timeout=20)
+
+    run(body(), timeout=120)
