@@ -451,18 +451,28 @@ async def _scenario(tmp: Path, n_nics: int, mode: str, seed: int, interval: str,
                 # The agent dies without cleaning up (OOM kill): the kubelet restarts the container,
                 # the new agent removes the stale label, configures again and is ready again.
                 c0 = next(iter(node.containers.values()))
-                t1 = time.monotonic()
-                c0.proc.kill()
-                t_unready = await _until(lambda: not all_good(), 10)
+                # The kubelet's first restart back-off is 10 s; 1 s here keeps the outage long enough
+                # for the operator to report it on a loaded test machine (0.1 s sometimes was not).
+                c0.backoff = 1.0
 
                 def crash_errors():
                     return [e for e in ((fake.get_object(P, name) or {}).get("status") or {}).get("errors") or []
                             if "exited with code" in e]
+                seen: list = []
 
-                await _until(lambda: bool(crash_errors()), 5)
-                res["crash_status_errors"] = crash_errors()
+                async def record():  # every crash entry the status carries, however briefly
+                    while True:
+                        seen.extend(e for e in crash_errors() if e not in seen)
+                        await asyncio.sleep(0.001)
+                recorder = asyncio.ensure_future(record())
+                t1 = time.monotonic()
+                c0.proc.kill()
+                t_unready = await _until(lambda: not all_good(), 10)
+                await _until(lambda: bool(seen), 10)
                 t_back = await _until(lambda: len(c0.started_at) == 2 and c0.ready and all_good()
                                       and node.node_labels().get(label_key) == "true", 30)
+                recorder.cancel()
+                res["crash_status_errors"] = list(seen)
                 res["crash_to_unready_s"] = round(t_unready - t1, 6) if t_unready else None
                 res["crash_to_all_good_s"] = round(t_back - t1, 6) if t_back else None
                 res["agent_restarts"] = c0.restarts
