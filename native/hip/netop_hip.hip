@@ -30,13 +30,16 @@ constexpr int kThreads = 256;
 
 // Pattern of (element, rank): integers in [-4, 3] -> exact in bf16, sums of up to 64 ranks
 // stay exact (|sum| <= 256 = 2^8).  Per 16-byte vector (group g of 8 elements; every buffer and
-// offset is a multiple of 8 elements) one rank-independent hash h(g); rank r's word is
-// h(g) * m_r (m_r odd, from the seed and r), and element e of the group is its 3-bit field at
-// bit 8 + 3 (e & 7), minus 4.  Summing over ranks works on the fields in place (SWAR): the even
-// and the odd fields of every rank are added as 6-bit slots of two words (9 ranks fit a slot),
-// so a rank costs a multiply and six integer ops instead of a hash and eight extractions.
-// pattern_tune.hip measured the change on MI355X (profiles/r4_pattern_tune.jsonl): 8-rank fill
-// 2.5 -> 4.3 TB/s, 8-rank verify 2.4 -> 5.2 TB/s, 1-rank verify 5.6 -> 6.1 TB/s.
+// offset is a multiple of 8 elements) one rank-independent hash h(g); rank r's word is h(g) * m_r
+// with m_r = m_0 + r d (m_0 odd, d twice an odd number: every m_r odd; both from the seed), and
+// element e of the group is its 3-bit field at bit 5 + 3 e, minus 4.  Summing over ranks works on
+// the fields in place (SWAR): the even and the odd fields of every rank are added as 6-bit slots
+// of two words (bits 5-28 and 8-31; 9 ranks fit a slot), and rank r + 1's word is rank r's plus
+// h d, so a rank costs one add and two and-adds -- no multiply, no shift, no per-element work.
+// pattern_tune.hip measured the steps on MI355X: a hash and eight extractions per rank ("v1") ->
+// one multiply per rank ("v2", profiles/r4_pattern_tune_v1_v2.jsonl: 8-rank fill 2.5 -> 4.3 TB/s,
+// verify 2.4 -> 5.2) -> one add per rank (this, "v4", profiles/r4_pattern_tune_v4.jsonl: 8-rank
+// verify 4.95 -> 5.86 TB/s, 16 ranks fill 3.1 -> 4.6 and verify 3.1 -> 4.0).
 // PyTorch reference: network_operator_amd/parallel/collectives.py:pattern_reference.
 __device__ __forceinline__ uint32_t group_hash(uint64_t g) {
     uint32_t x = uint32_t(g) * 0x9E3779B1u ^ uint32_t(g >> 32) * 0x85EBCA77u;
@@ -46,12 +49,18 @@ __device__ __forceinline__ uint32_t group_hash(uint64_t g) {
     return x;
 }
 
-__device__ __forceinline__ uint32_t rank_mult(uint32_t seed, int rank) {
-    const uint32_t k = (seed + 0x632BE5ABu * uint32_t(rank + 1)) * 0xC2B2AE3Du;
+__device__ __forceinline__ uint32_t base_mult(uint32_t seed) {  // m_0
+    const uint32_t k = (seed + 0x632BE5ABu) * 0xC2B2AE3Du;
     return (k ^ (k >> 16)) | 1u;
 }
 
-constexpr uint32_t kFieldSlots = (7u << 8) | (7u << 14) | (7u << 20) | (7u << 26);  // fields 0, 2, 4, 6
+__device__ __forceinline__ uint32_t step_mult(uint32_t seed) {  // d
+    const uint32_t k = (seed ^ 0x27D4EB2Fu) * 0x165667B1u;
+    return ((k ^ (k >> 15)) << 1) | 2u;
+}
+
+constexpr uint32_t kEvenSlots = (7u << 5) | (7u << 11) | (7u << 17) | (7u << 23);  // fields 0, 2, 4, 6
+constexpr uint32_t kOddSlots = kEvenSlots << 3;                                     // fields 1, 3, 5, 7
 
 __device__ __forceinline__ uint16_t int_to_bf16(int v) {
     // Small integers are exact; convert through f32 bits (truncation is exact here).
@@ -65,19 +74,22 @@ __device__ __forceinline__ float bf16_to_float(uint16_t h) { return __uint_as_fl
 // 1) or the reduction over a contiguous rank range (all-reduce / reduce-scatter expectation).
 __device__ __forceinline__ void group_sum(uint64_t g, uint32_t seed, int rank_lo, int n_ranks, int s[8]) {
     const uint32_t h = group_hash(g);
+    const uint32_t d = step_mult(seed);
+    const uint32_t dx = h * d;
+    uint32_t x = h * (base_mult(seed) + uint32_t(rank_lo) * d);  // rank rank_lo's word
 #pragma unroll
     for (int k = 0; k < 8; ++k) s[k] = -4 * n_ranks;
-    for (int r0 = rank_lo; r0 < rank_lo + n_ranks; r0 += 9) {  // 9 x 7 = 63 fits a 6-bit slot
+    for (int r0 = 0; r0 < n_ranks; r0 += 9) {  // 9 x 7 = 63 fits a 6-bit slot
         uint32_t even = 0, odd = 0;
-        const int r1 = r0 + 9 < rank_lo + n_ranks ? r0 + 9 : rank_lo + n_ranks;
+        const int r1 = r0 + 9 < n_ranks ? r0 + 9 : n_ranks;
         for (int r = r0; r < r1; ++r) {
-            const uint32_t x = h * rank_mult(seed, r);
-            even += x & kFieldSlots;
-            odd += (x >> 3) & kFieldSlots;
+            even += x & kEvenSlots;
+            odd += x & kOddSlots;
+            x += dx;
         }
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            s[2 * k] += int((even >> (8 + 6 * k)) & 63u);
+            s[2 * k] += int((even >> (5 + 6 * k)) & 63u);
             s[2 * k + 1] += int((odd >> (8 + 6 * k)) & 63u);
         }
     }

@@ -2,8 +2,11 @@
 // buffer, 1 and 8 ranks in the pattern, for
 //   * v1: the round-3 pattern (a full hash per rank per 16-byte vector, 3-bit fields extracted
 //     and summed one element at a time: ALU-bound at 8 ranks, 2.0-2.5 TB/s);
-//   * v2: the pattern netop_hip.hip uses now (one rank-independent hash per vector, one multiply
-//     per rank, the 8 fields of all ranks summed as 6-bit slots of two words: SWAR),
+//   * v2: the first SWAR pattern (one rank-independent hash per vector, one multiply per rank,
+//     the 8 fields of all ranks summed as 6-bit slots of two words);
+//   * v3: v2 with 24-bit multiplies and packed compares (no gain);
+//   * v4: the pattern netop_hip.hip uses now (mode "v4"): one add per rank, fields placed so
+//     that neither slot word needs a shift,
 // crossed with vectors in flight per lane (UNROLL 1 / 2), nontemporal stores / loads, and
 // workgroups per CU (4 / 8 / 16).  Every v2 variant is checked (fill -> verify = 0 errors; one
 // flipped element -> 1 error) before it is timed.  Prints one JSON line per variant.
@@ -102,6 +105,42 @@ __device__ __forceinline__ void sum_v3(uint64_t g, uint32_t seed, int n, int s[8
     }
 }
 
+// ---- v4: rank r's word is h * (m_0 + r d), d = 2 x odd (every multiplier odd), so a rank costs
+// one add (x += h d) instead of a multiply; the 8 fields sit at bits 5 + 3 e, which puts the even
+// fields' and the odd fields' 6-bit slots inside one word each without a shift (bits 5-28 and
+// 8-31).  Per rank: an add and two and-adds (5 VALU ops against about 9 in v2). ----
+__device__ __forceinline__ uint32_t base_mult4(uint32_t seed) {
+    const uint32_t k = (seed + 0x632BE5ABu) * 0xC2B2AE3Du;
+    return (k ^ (k >> 16)) | 1u;
+}
+__device__ __forceinline__ uint32_t step_mult4(uint32_t seed) {
+    const uint32_t k = (seed ^ 0x27D4EB2Fu) * 0x165667B1u;
+    return ((k ^ (k >> 15)) << 1) | 2u;
+}
+constexpr uint32_t kEven4 = (7u << 5) | (7u << 11) | (7u << 17) | (7u << 23);
+constexpr uint32_t kOdd4 = kEven4 << 3;
+__device__ __forceinline__ void sum_v4(uint64_t g, uint32_t seed, int n, int s[8]) {
+    const uint32_t h = group_hash(g);
+    const uint32_t dx = h * step_mult4(seed);
+    uint32_t x = h * base_mult4(seed);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s[k] = -4 * n;
+    for (int r0 = 0; r0 < n; r0 += 9) {
+        uint32_t e = 0, o = 0;
+        const int r1 = r0 + 9 < n ? r0 + 9 : n;
+        for (int r = r0; r < r1; ++r) {
+            e += x & kEven4;
+            o += x & kOdd4;
+            x += dx;
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            s[2 * k] += int((e >> (5 + 6 * k)) & 63u);
+            s[2 * k + 1] += int((o >> (8 + 6 * k)) & 63u);
+        }
+    }
+}
+
 __device__ __forceinline__ uint32_t bf16x2_of_ints(int lo, int hi) {
     return (__float_as_uint(float(lo)) >> 16) | (__float_as_uint(float(hi)) & 0xffff0000u);
 }
@@ -146,6 +185,8 @@ __global__ __launch_bounds__(kThreads) void fill_k(u32x4* __restrict__ out, uint
                 sum_v1(v, seed, n, s);
             else if (V == 2)
                 sum_v2(v, seed, n, s);
+            else if (V == 4)
+                sum_v4(v, seed, n, s);
             else
                 sum_v3(v, seed, n, s);
             const u32x4 w = {bf16x2_of_ints(s[0], s[1]), bf16x2_of_ints(s[2], s[3]), bf16x2_of_ints(s[4], s[5]),
@@ -182,6 +223,8 @@ __global__ __launch_bounds__(kThreads) void verify_k(const u32x4* __restrict__ i
                 sum_v1(v, seed, n, s);
             else if (V == 2)
                 sum_v2(v, seed, n, s);
+            else if (V == 4)
+                sum_v4(v, seed, n, s);
             else
                 sum_v3(v, seed, n, s);
             const uint32_t w[4] = {q[u].x, q[u].y, q[u].z, q[u].w};
@@ -377,7 +420,7 @@ int main(int argc, char** argv) {
     CHECK(hipEventCreate(&c.b));
     CHECK(hipDeviceGetAttribute(&c.cus, hipDeviceAttributeMultiprocessorCount, 0));
     const int iters = 10;
-    const std::string mode = argc > 2 ? argv[2] : "all";  // all | ceilings | chunk | copy | xcd
+    const std::string mode = argc > 2 ? argv[2] : "all";  // all | ceilings | chunk | copy | xcd | v4
     if (mode == "copy") {
         return copy_shape<1, false>(c.buf, c.n_vec, c.cus, c.a, c.b) || copy_shape<1, true>(c.buf, c.n_vec, c.cus, c.a, c.b) ||
                copy_shape<2, false>(c.buf, c.n_vec, c.cus, c.a, c.b) || copy_shape<2, true>(c.buf, c.n_vec, c.cus, c.a, c.b) ||
@@ -389,6 +432,13 @@ int main(int argc, char** argv) {
             for (int pc : {8, 16})
                 if (run<2, 1, true, 1>(c, n, pc, iters) || run<2, 1, true, 2>(c, n, pc, iters)) return 1;
         return copy_shape<1, 2>(c.buf, c.n_vec, c.cus, c.a, c.b) || copy_shape<1, 0>(c.buf, c.n_vec, c.cus, c.a, c.b);
+    }
+    if (mode == "v4") {
+        // The one-add-per-rank pattern against the current one, chunked walk, NT, 1 / 8 / 16 ranks.
+        for (int n : {1, 8, 16})
+            for (int pc : {8, 16})
+                if (run<2, 1, true, 1>(c, n, pc, iters) || run<4, 1, true, 1>(c, n, pc, iters)) return 1;
+        return 0;
     }
     if (mode == "chunk") {
         // Contiguous chunk per workgroup against the grid-stride walk, v2 pattern.

@@ -125,8 +125,8 @@ def sync(device) -> None:
 
 def pattern_reference(n: int, seed: int, rank: int):
     """PyTorch (CPU) reference of the HIP pattern in native/hip/netop_hip.hip (group_hash /
-    rank_mult / group_sum): element i is the 3-bit field at bit 8 + 3 (i & 7) of
-    group_hash(i >> 3) * rank_mult(seed, rank), minus 4."""
+    base_mult / step_mult / group_sum): element i is the 3-bit field at bit 5 + 3 (i & 7) of
+    group_hash(i >> 3) * (base_mult(seed) + rank * step_mult(seed)), minus 4."""
     import torch
 
     M32 = 0xFFFFFFFF
@@ -137,10 +137,13 @@ def pattern_reference(n: int, seed: int, rank: int):
     h = h ^ (h >> 15)
     h = (h * 0x2C1B3C6D) & M32
     h = h ^ (h >> 12)
-    k = (((seed + 0x632BE5AB * (rank + 1)) & M32) * 0xC2B2AE3D) & M32
-    m = (k ^ (k >> 16)) | 1
+    k = (((seed + 0x632BE5AB) & M32) * 0xC2B2AE3D) & M32
+    m0 = (k ^ (k >> 16)) | 1
+    k = (((seed ^ 0x27D4EB2F) & M32) * 0x165667B1) & M32
+    d = (((k ^ (k >> 15)) << 1) | 2) & M32
+    m = (m0 + rank * d) & M32
     x = (h * m) & M32  # int64 wraps on overflow; the low 32 bits are exact
-    return (((x >> (8 + 3 * (i & 7))) & 7) - 4).to(torch.float32)
+    return (((x >> (5 + 3 * (i & 7))) & 7) - 4).to(torch.float32)
 
 
 def verify_all_reduce(numel: int, device, seed: int = 2024, group=None) -> tuple[bool, int]:

@@ -9,8 +9,8 @@ pytestmark = pytest.mark.gpu
 
 
 def _ref_pattern(n, seed, rank):
-    """fp32 reference of the device pattern (mirrors group_hash() / rank_mult() / group_sum() in
-    netop_hip.hip), written independently of collectives.pattern_reference."""
+    """fp32 reference of the device pattern (mirrors group_hash() / base_mult() / step_mult() /
+    group_sum() in netop_hip.hip), written independently of collectives.pattern_reference."""
     import torch
 
     return _ref_at(torch.arange(n, dtype=torch.int64), seed, rank)
@@ -24,9 +24,11 @@ def _ref_at(i, seed, rank):
     h ^= h >> 15
     h = (h * 0x2C1B3C6D) & M32
     h ^= h >> 12
-    k = ((seed + 0x632BE5AB * (rank + 1)) & M32) * 0xC2B2AE3D & M32
-    word = (h * ((k ^ (k >> 16)) | 1)) & M32  # rank's word; element i = field at bit 8 + 3 (i % 8)
-    return (((word >> (8 + 3 * (i % 8))) & 7) - 4).float()
+    k = ((seed + 0x632BE5AB) & M32) * 0xC2B2AE3D & M32
+    k2 = ((seed ^ 0x27D4EB2F) & M32) * 0x165667B1 & M32
+    mult = (((k ^ (k >> 16)) | 1) + rank * ((((k2 ^ (k2 >> 15)) << 1) | 2) & M32)) & M32  # m_0 + rank d
+    word = (h * mult) & M32  # rank's word; element i = field at bit 5 + 3 (i % 8)
+    return (((word >> (5 + 3 * (i % 8))) & 7) - 4).float()
 
 
 def test_fill_pattern_matches_reference(cuda_device):

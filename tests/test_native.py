@@ -254,9 +254,9 @@ def test_ipv6_addresses_are_read_from_the_kernel(native):
 
 def test_pattern_swar_sum_matches_the_per_rank_reference():
     """The device's rank sum (netop_hip.hip group_sum: even / odd 3-bit fields of every rank
-    added as 6-bit slots, flushed every 9 ranks) equals the sum of the per-rank reference
-    (collectives.pattern_reference) for 1..64 ranks and rank ranges -- emulated here with Python
-    integers, line for line."""
+    added as 6-bit slots without a shift, flushed every 9 ranks, each rank's word the previous
+    one plus h d) equals the sum of the per-rank reference (collectives.pattern_reference) for
+    1..64 ranks and rank ranges -- emulated here with Python integers, line for line."""
     import random
 
     import torch
@@ -264,7 +264,8 @@ def test_pattern_swar_sum_matches_the_per_rank_reference():
     from network_operator_amd.parallel.collectives import pattern_reference
 
     M32 = 0xFFFFFFFF
-    SLOTS = (7 << 8) | (7 << 14) | (7 << 20) | (7 << 26)
+    EVEN = (7 << 5) | (7 << 11) | (7 << 17) | (7 << 23)
+    ODD = EVEN << 3
 
     def group_hash(g):
         x = ((g & M32) * 0x9E3779B1 & M32) ^ (((g >> 32) & M32) * 0x85EBCA77 & M32)
@@ -272,20 +273,27 @@ def test_pattern_swar_sum_matches_the_per_rank_reference():
         x = x * 0x2C1B3C6D & M32
         return x ^ (x >> 12)
 
-    def rank_mult(seed, r):
-        k = ((seed + 0x632BE5AB * (r + 1)) & M32) * 0xC2B2AE3D & M32
+    def base_mult(seed):
+        k = ((seed + 0x632BE5AB) & M32) * 0xC2B2AE3D & M32
         return (k ^ (k >> 16)) | 1
+
+    def step_mult(seed):
+        k = ((seed ^ 0x27D4EB2F) & M32) * 0x165667B1 & M32
+        return (((k ^ (k >> 15)) << 1) | 2) & M32
 
     def group_sum(g, seed, lo, n):
         h, s = group_hash(g), [-4 * n] * 8
-        for r0 in range(lo, lo + n, 9):
+        d = step_mult(seed)
+        dx = h * d & M32
+        x = h * ((base_mult(seed) + lo * d) & M32) & M32
+        for r0 in range(0, n, 9):
             even = odd = 0
-            for r in range(r0, min(r0 + 9, lo + n)):
-                x = h * rank_mult(seed, r) & M32
-                even = (even + (x & SLOTS)) & M32
-                odd = (odd + ((x >> 3) & SLOTS)) & M32
+            for _ in range(r0, min(r0 + 9, n)):
+                even = (even + (x & EVEN)) & M32
+                odd = (odd + (x & ODD)) & M32
+                x = (x + dx) & M32
             for k in range(4):
-                s[2 * k] += (even >> (8 + 6 * k)) & 63
+                s[2 * k] += (even >> (5 + 6 * k)) & 63
                 s[2 * k + 1] += (odd >> (8 + 6 * k)) & 63
         return s
 
