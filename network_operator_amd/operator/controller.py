@@ -19,7 +19,7 @@ from . import kube
 from .informer import Informer, controller_of, slim_event, slim_job, slim_pod
 from .kube import ApiClient
 from .metrics import OperatorMetrics
-from .reconciler import (OWNER_KEY, VALIDATION_APP, EventRecorder, NetworkClusterPolicyReconciler,
+from .reconciler import (CONFLICT_MARK, OWNER_KEY, VALIDATION_APP, EventRecorder, NetworkClusterPolicyReconciler,
                          daemonset_owner_index, job_owner_index, policy_owner_index)
 from .workqueue import RateLimitingQueue
 
@@ -204,7 +204,8 @@ class PolicyController:
     def _export_policy(self, name: str) -> None:
         p = self.policies.get(name)
         if p is None:
-            for g in (self.metrics.policy_targets, self.metrics.policy_ready, self.metrics.nodes_owing_cleanup):
+            for g in (self.metrics.policy_targets, self.metrics.policy_ready, self.metrics.nodes_owing_cleanup,
+                      self.metrics.policy_conflicts):
                 try:
                     g.remove(name)
                 except KeyError:
@@ -214,6 +215,7 @@ class PolicyController:
         self.metrics.policy_targets.labels(name).set(st.get("targets", 0) or 0)
         self.metrics.policy_ready.labels(name).set(st.get("ready", 0) or 0)
         self.metrics.nodes_owing_cleanup.labels(name).set(len(st.get("keptNodes") or []))
+        self.metrics.policy_conflicts.labels(name).set(sum(CONFLICT_MARK in e for e in st.get("errors") or []))
 
     async def start(self) -> None:
         self._tasks.append(self.policies.start())

@@ -47,6 +47,10 @@ class OperatorMetrics:
         self.nodes_owing_cleanup = Gauge("amd_network_operator_nodes_owing_cleanup",
                                          "Nodes whose agents left configuration a cleanup Job still has to remove",
                                          ["policy"], registry=r)
+        self.policy_conflicts = Gauge("amd_network_operator_policy_conflicts",
+                                      "Older policies of the same configurationType whose agents share nodes with this "
+                                      "policy's (status.errors, Degraded reason PolicyConflict)",
+                                      ["policy"], registry=r)
         self.node_cleanups = Counter("amd_network_operator_node_cleanups_total",
                                      "Node cleanup Jobs that ended, by outcome (succeeded, failed, timed_out)",
                                      ["policy", "outcome"], registry=r)

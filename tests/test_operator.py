@@ -1462,11 +1462,16 @@ def test_two_policies_of_one_type_on_the_same_nodes_are_reported_on_both():
             events = [e for e in fake.list_objects(kube.EVENTS) if e.get("reason") == "PolicyConflict"]
             assert {e["involvedObject"]["name"] for e in events} == {"two"}
 
+            def conflicts(name):
+                return ctl.metrics.registry.get_sample_value("amd_network_operator_policy_conflicts", {"policy": name})
+            await eventually(lambda: conflicts("two") == 1 and conflicts("one") == 0)
+
             await edit(client, "two", lambda cur: cur["spec"].update(nodeSelector={"rack": "b"}))
             await eventually(conflicted("two", "one", "n2"))
             await edit(client, "one", lambda cur: cur["spec"].update(nodeSelector={"rack": "a"}))
             await eventually(clean("two", 1))
             await eventually(clean("one", 2))
+            await eventually(lambda: conflicts("two") == 0)
 
             await edit(client, "two", lambda cur: cur["spec"].update(nodeSelector={"foo": "bar"}))
             await eventually(conflicted("two", "one", "n0, n1"))
