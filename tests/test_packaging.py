@@ -502,7 +502,37 @@ def test_rendered_deployments_are_up_to_date():
 def test_prometheus_overlay_scrapes_the_operator_and_the_agents():
     docs = kustomize_build(ROOT / "config/operator/prometheus")
     kinds = sorted(d["kind"] for d in docs)
-    assert kinds == ["PodMonitor", "ServiceMonitor"]
+    assert kinds == ["PodMonitor", "PrometheusRule", "ServiceMonitor"]
     pm = next(d for d in docs if d["kind"] == "PodMonitor")
     assert pm["spec"]["selector"]["matchLabels"] == {"app": "amd-network-tools"}
     assert pm["spec"]["podMetricsEndpoints"][0]["port"] == "metrics"  # the container port metricsPort opens
+
+
+def test_alert_rules_use_only_metrics_that_exist():
+    """Every metric an alert of config/operator/prometheus/alert-rules.yaml reads is exported: the
+    operator's from its registry, the agents' from the agent's /metrics writer (agent.cpp); each
+    alert has a severity and a summary."""
+    import re
+
+    import yaml
+
+    from network_operator_amd.operator.metrics import OperatorMetrics
+
+    doc = yaml.safe_load((ROOT / "config/operator/prometheus/alert-rules.yaml").read_text())
+    assert doc["kind"] == "PrometheusRule"
+    operator_names = set()
+    for fam in OperatorMetrics().registry.collect():
+        operator_names.add(fam.name + ("_total" if fam.type == "counter" else ""))
+        operator_names.update(s.name for s in fam.samples)
+    agent_src = (ROOT / "native/src/agent.cpp").read_text()
+    rules = [r for g in doc["spec"]["groups"] for r in g["rules"]]
+    assert len(rules) >= 6
+    for r in rules:
+        assert r["labels"]["severity"] in ("warning", "critical") and r["annotations"]["summary"]
+        for name in re.findall(r"\b((?:amd_network_operator|netop_agent)_[a-z_]+)", r["expr"]):
+            if name.startswith("netop_agent_"):
+                assert f'metric("{name}"' in agent_src, (r["alert"], name)
+            else:
+                assert name in operator_names, (r["alert"], name)
+    kust = yaml.safe_load((ROOT / "config/operator/prometheus/kustomization.yaml").read_text())
+    assert "alert-rules.yaml" in kust["resources"]
