@@ -446,7 +446,7 @@ def _container_running(pod: dict) -> bool:
 CONFLICT_MARK = ": also selected by policy "
 
 
-def conflict_errors(policy: str, ctype: str, mine: List[str], others: Dict[str, List[str]], limit: int = 3) -> List[str]:
+def conflict_errors(ctype: str, mine: List[str], others: Dict[str, List[str]], limit: int = 3) -> List[str]:
     """status.errors entries for the nodes ``mine`` shares with each policy in ``others`` (name ->
     nodes of its agent Pods; same configurationType), one entry per other policy."""
     out = []
@@ -782,7 +782,7 @@ class NetworkClusterPolicyReconciler:
             if (q.get("spec") or {}).get("configurationType", "") != p.spec.configurationType:
                 continue
             others[md["name"]] = nodes(md["name"])
-        return conflict_errors(p.name, p.spec.configurationType, mine, others)
+        return conflict_errors(p.spec.configurationType, mine, others)
 
     async def _delete_job(self, j: dict) -> None:
         try:

@@ -1415,9 +1415,9 @@ def test_rail_switch_pattern_random_corpus_never_admits_what_the_agent_rejects(n
 def test_conflict_errors_name_the_other_policy_and_the_shared_nodes():
     from network_operator_amd.operator.reconciler import CONFLICT_MARK, conflict_errors
 
-    assert conflict_errors("a", "amd-so", ["n1"], {}) == []
-    assert conflict_errors("a", "amd-so", ["n1", "n2"], {"b": ["n3"]}) == []
-    errs = conflict_errors("a", "amd-so", ["n1", "n2", "n3", "n4", "n5"], {"c": ["n5"], "b": ["n5", "n4", "n3", "n2"]})
+    assert conflict_errors("amd-so", ["n1"], {}) == []
+    assert conflict_errors("amd-so", ["n1", "n2"], {"b": ["n3"]}) == []
+    errs = conflict_errors("amd-so", ["n1", "n2", "n3", "n4", "n5"], {"c": ["n5"], "b": ["n5", "n4", "n3", "n2"]})
     assert [e.split(CONFLICT_MARK)[1].split(" ")[0] for e in errs] == ["b", "c"]
     assert errs[0].startswith("n2, n3, n4 and 1 more" + CONFLICT_MARK + "b (amd-so too, created earlier)")
     assert errs[1].startswith("n5" + CONFLICT_MARK + "c (amd-so too, created earlier)")
