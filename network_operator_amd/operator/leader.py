@@ -14,6 +14,14 @@ every renewal attempt -- and every API request inside it -- is bounded by what i
 when the deadline passes the leader's work is cancelled at once.  A replica whose API calls
 stall therefore stops reconciling ``lease_duration - renew_deadline`` (5 s by default) before
 anyone else can legally lead.
+
+Order on loss: the leader's work -- which owns the reconcile workers --
+is cancelled and awaited first, then ``on_stopped_leading`` runs, and only then is the lease
+released, with ONE attempt bounded by ``retry_period`` (a stalled API cannot hold the stop up
+behind GET + PUT round trips).  The time from the deadline to the last worker gone is kept in
+``stop_latency``; ``STOP_BUDGET_S`` is what the manager's flag check reserves for it out of
+``lease_duration - renew_deadline``.  (client-go releases in ``renew()`` before its
+``OnStoppedLeading``; controller-runtime then exits 1 -- reference cmd/operator/main.go:229-232.)
 """
 
 from __future__ import annotations
@@ -33,6 +41,22 @@ from .kube import ApiClient, ApiError, is_already_exists, is_conflict, is_not_fo
 log = logging.getLogger("leaderelection")
 
 DEFAULT_LEASE_ID = "9a8a7ba6.amd.com"
+# Seconds reserved between the renew deadline and the lease's expiry for the leader's work to be
+# cancelled (workers, seeder) and for a write already on the wire to land.  Cancelling is
+# immediate in asyncio; the measured stop is milliseconds (``LeaderElector.stop_latency``).
+STOP_BUDGET_S = 1.0
+
+
+def unsafe_timings(lease_duration: float, renew_deadline: float, retry_period: float) -> str:
+    """Why these leader-election timings are unsafe, or "" when they are safe: the order
+    client-go requires, plus a margin of more than STOP_BUDGET_S between the renew deadline
+    (when a stalled leader stops) and the lease duration (when a standby may take over)."""
+    if not (lease_duration > renew_deadline > retry_period > 0):
+        return "leader election needs lease duration > renew deadline > retry period > 0"
+    if lease_duration - renew_deadline <= STOP_BUDGET_S:
+        return (f"lease duration - renew deadline = {lease_duration - renew_deadline:g}s leaves no room for the "
+                f"leader to stop ({STOP_BUDGET_S:g}s) before a standby may take over")
+    return ""
 
 
 def _now_str() -> str:
@@ -63,6 +87,7 @@ class LeaderElector:
         self.is_leader = False
         self.transitions = 0
         self.lost_at: Optional[float] = None  # loop time at which leadership was given up
+        self.stop_latency: Optional[float] = None  # seconds from lost_at until the work had ended
 
     def _lease_body(self, prev: Optional[dict]) -> dict:
         spec_prev = (prev or {}).get("spec", {}) or {}
@@ -122,16 +147,19 @@ class LeaderElector:
         self._observed_time = self._loop_time()
 
     async def release(self) -> None:
-        t = self._request_timeout()
-        try:
-            lease = await self.client.get(kube.LEASES, self.name, self.namespace, timeout=t)
+        """Best effort, one attempt: hand the lease back so a standby need not wait out its
+        duration.  Bounded by ``retry_period`` in total (GET and PUT together)."""
+        async def once() -> None:
+            lease = await self.client.get(kube.LEASES, self.name, self.namespace, timeout=self.retry_period)
             if (lease.get("spec", {}) or {}).get("holderIdentity") != self.identity:
                 return
             lease["spec"]["holderIdentity"] = ""
             lease["spec"]["leaseDurationSeconds"] = 1
-            await self.client.replace(kube.LEASES, lease, timeout=t)
+            await self.client.replace(kube.LEASES, lease, timeout=self.retry_period)
+        try:
+            await asyncio.wait_for(once(), timeout=self.retry_period)
         except Exception as e:
-            log.info("lease release failed: %s", e)
+            log.info("lease release failed: %s", e or type(e).__name__)
 
     async def run(self, on_started_leading: Callable[[], Awaitable[None]],
                   on_stopped_leading: Optional[Callable[[], Awaitable[None]]] = None) -> None:
@@ -153,8 +181,10 @@ class LeaderElector:
                 if work.done():
                     await work  # propagate errors from the leader's work
                     return
-                # Sleep until the next renewal, or until the leader's work ends.
-                await asyncio.wait({work}, timeout=self.retry_period)
+                # Sleep until the next renewal, or until the leader's work ends -- never past the
+                # renew deadline, or a stall found late would eat into the standby's margin.
+                left = self.renew_deadline - (self._loop_time() - last_ok)
+                await asyncio.wait({work}, timeout=max(0.0, min(self.retry_period, left)))
                 if work.done():
                     continue
                 left = self.renew_deadline - (self._loop_time() - last_ok)
@@ -174,12 +204,18 @@ class LeaderElector:
                     return
         finally:
             self.is_leader = False
+            # 1. the work (and with it every reconcile worker) ends first ...
             work.cancel()
-            try:
-                await work
-            except (asyncio.CancelledError, Exception):
-                pass
+            done, _ = await asyncio.wait({work}, timeout=STOP_BUDGET_S)
+            if not done:
+                log.error("the leader's work did not stop within %.1fs of losing the lease", STOP_BUDGET_S)
+            elif not work.cancelled() and work.exception() is not None:
+                log.info("leader's work ended with %r", work.exception())
             if on_stopped_leading:
                 await on_stopped_leading()
+            if self.lost_at is not None:
+                self.stop_latency = self._loop_time() - self.lost_at
+                log.info("stopped leading %.3fs after the renew deadline", self.stop_latency)
+            # 2. ... and only then is the lease handed back (one bounded attempt).
             if self.release_on_cancel:
                 await self.release()

@@ -21,7 +21,7 @@ from typing import Dict, List, Optional
 
 from .controller import PolicyController
 from .kube import ApiClient, load_config
-from .leader import DEFAULT_LEASE_ID, LeaderElector
+from .leader import DEFAULT_LEASE_ID, LeaderElector, unsafe_timings
 from .metrics import OperatorMetrics
 from .seeder import PolicySeeder
 from .servers import DEFAULT_CERT_DIR, Servers
@@ -132,7 +132,12 @@ def setup_logging(level: str, encoder: str) -> None:
 
 
 async def run(argv: Optional[List[str]] = None, stop: Optional[asyncio.Event] = None,
-              started: Optional[asyncio.Event] = None) -> int:
+              started: Optional[asyncio.Event] = None, user_agent: Optional[str] = None,
+              identity: Optional[str] = None) -> int:
+    """The manager.  Returns 0 after a stop signal and 1 on a start-up failure or when leadership
+    was lost (controller-runtime's manager exits 1 with "leader election lost", reference
+    cmd/operator/main.go:229-232).  `stop`, `started`, `user_agent` and `identity` (the Lease
+    holder; default ``<pod>_<uuid>``) let tests run several replicas in one process."""
     opts = build_parser().parse_args(argv)
     setup_logging(opts.zap_log_level, opts.zap_encoder)
     ns = os.environ.get("OPERATOR_NAMESPACE") or DEFAULT_OPERATOR_NAMESPACE
@@ -145,7 +150,14 @@ async def run(argv: Optional[List[str]] = None, stop: Optional[asyncio.Event] = 
         except (NotImplementedError, RuntimeError):  # not the main thread (tests)
             pass
 
-    client = ApiClient(load_config(opts.kubeconfig, opts.master))
+    if opts.leader_elect:
+        why = unsafe_timings(opts.leader_elect_lease_duration, opts.leader_elect_renew_deadline,
+                             opts.leader_elect_retry_period)
+        if why:
+            log.error("%s", why)
+            return 1
+    client = ApiClient(load_config(opts.kubeconfig, opts.master),
+                       **({"user_agent": user_agent} if user_agent else {}))
     try:
         try:
             openshift = await is_openshift(client)
@@ -162,6 +174,7 @@ async def run(argv: Optional[List[str]] = None, stop: Optional[asyncio.Event] = 
                             opts.webhook_port if webhooks else None, opts.webhook_cert_dir)
 
         dep_task = None
+        exit_code = 0
         if opts.dependency_check_interval > 0:
             # First result before the controller starts, so the first status already has it.
             try:
@@ -174,31 +187,35 @@ async def run(argv: Optional[List[str]] = None, stop: Optional[asyncio.Event] = 
                                                                 opts.dependency_check_interval, webhooks))
 
         async def lead() -> None:
-            await controller.start()
+            # The leader's work owns every writer: when the elector cancels it at the renew
+            # deadline, the reconcile workers and the seeder are gone before the lease is
+            # released (leader.py) -- not after, as when they outlived a cancelled wait.
             seed = None
-            if opts.policies_file:
-                # Only the leader writes policies; the webhook server is already serving, so the
-                # API server can admit them (see seeder.py for why the chart does not create them).
-                seeder = PolicySeeder(client, opts.policies_file, opts.policies_owner, opts.policies_interval,
-                                      metrics=metrics,
-                                      seed_id=opts.policies_seed_id or f"{ns}.{opts.leader_election_id}")
-                seed = asyncio.ensure_future(seeder.run(stop))
-            if started:
-                started.set()
-            log.info("starting manager")
             try:
+                await controller.start()
+                if opts.policies_file:
+                    # Only the leader writes policies; the webhook server is already serving, so the
+                    # API server can admit them (see seeder.py for why the chart does not create them).
+                    seeder = PolicySeeder(client, opts.policies_file, opts.policies_owner, opts.policies_interval,
+                                          metrics=metrics,
+                                          seed_id=opts.policies_seed_id or f"{ns}.{opts.leader_election_id}")
+                    seed = asyncio.ensure_future(seeder.run(stop))
+                if started:
+                    started.set()
+                log.info("starting manager")
                 await stop.wait()
             finally:
                 if seed is not None:
                     seed.cancel()
+                    try:
+                        await seed
+                    except (asyncio.CancelledError, Exception):
+                        pass
+                await controller.stop()
 
         try:
             if opts.leader_elect:
-                if not (opts.leader_elect_lease_duration > opts.leader_elect_renew_deadline
-                        > opts.leader_elect_retry_period > 0):
-                    log.error("leader election needs lease duration > renew deadline > retry period > 0")
-                    return 1
-                elector = LeaderElector(client, ns, opts.leader_election_id,
+                elector = LeaderElector(client, ns, opts.leader_election_id, identity=identity,
                                         lease_duration=opts.leader_elect_lease_duration,
                                         renew_deadline=opts.leader_elect_renew_deadline,
                                         retry_period=opts.leader_elect_retry_period)
@@ -208,16 +225,24 @@ async def run(argv: Optional[List[str]] = None, stop: Optional[asyncio.Event] = 
                     metrics.leader.labels(opts.leader_election_id).set(1)
                     await lead()
 
-                runner = asyncio.ensure_future(elector.run(lead_with_metric))
+                async def stopped_leading() -> None:
+                    metrics.leader.labels(opts.leader_election_id).set(0)
+                    await controller.stop()
+
+                runner = asyncio.ensure_future(elector.run(lead_with_metric, on_stopped_leading=stopped_leading))
                 stopper = asyncio.ensure_future(stop.wait())
                 done, _ = await asyncio.wait({runner, stopper}, return_when=asyncio.FIRST_COMPLETED)
+                stopper.cancel()
                 if runner not in done:
                     runner.cancel()
                     try:
                         await runner
                     except (asyncio.CancelledError, Exception):
                         pass
-                stopper.cancel()
+                elif elector.lost_at is not None or runner.exception() is not None:
+                    log.error("problem running manager: %s",
+                              "leader election lost" if elector.lost_at is not None else runner.exception())
+                    exit_code = 1
             else:
                 await lead()
         finally:
@@ -225,7 +250,7 @@ async def run(argv: Optional[List[str]] = None, stop: Optional[asyncio.Event] = 
                 dep_task.cancel()
             await controller.stop()
             await servers.stop()
-        return 0
+        return exit_code
     finally:
         await client.close()
 

@@ -217,6 +217,7 @@ class FakeApiServer:
         self.stalls: List[tuple] = []
         self._unstall: Optional[asyncio.Event] = None
         self.requests: List[Tuple[str, str]] = []
+        self.writes: List[Tuple[float, str, str, str]] = []  # (loop time, User-Agent, method, path)
         self.accesses: set = set()                           # (verb, group, resource[/sub])
         self.admission_calls: List[Tuple[str, str]] = []
         # (namespace, service) -> "https://host:port" of a ready endpoint (service-referenced webhooks)
@@ -730,6 +731,15 @@ class FakeApiServer:
         return res, ns, name, sub
 
     async def _dispatch(self, req: web.Request) -> web.StreamResponse:
+        resp = await self._serve(req)
+        if req.method in ("POST", "PUT", "PATCH", "DELETE") and resp.status < 300:
+            # When each write took effect, and whose it was: e.g. "no write of the old leader
+            # lands after the new leader's first" (two-replica leader-election tests).
+            self.writes.append((asyncio.get_event_loop().time(), req.headers.get("User-Agent", ""),
+                                req.method, req.path))
+        return resp
+
+    async def _serve(self, req: web.Request) -> web.StreamResponse:
         path = req.path
         self.requests.append((req.method, path))
         for method, pattern, ua, seconds in list(self.stalls):
