@@ -79,6 +79,10 @@ struct Config {
     bool nm_restore = false;
     int xgmi_expect_links = -1;          // -1 off; 0 = full mesh among discovered GPUs; N = exact pairs
     int64_t link_wait_ns = 3LL * 1000000000;  // netlink echo wait (network.go:251)
+    // L2: how long a NIC that is admin-up may train its link before it counts as "no carrier".
+    // Separate from the 3 s echo wait: 200/400G optics with FEC and link training commonly take
+    // 5-15 s (longer through auto-negotiation retries), so 3 s made every start look degraded.
+    int64_t carrier_wait_ns = 30LL * 1000000000;
     // The RDMA core adds the RoCE v2 GID of a new IPv4 address asynchronously (netdev notifier
     // -> GID cache work item); wait this long for it before writing rccl.env without a GID.
     int64_t gid_wait_ns = 3LL * 1000000000;
@@ -303,7 +307,8 @@ class Agent {
     void remove_rail_routing();             // every NIC's
     void write_artifacts();
     void write_l2_artifacts();
-    // L2: waits up to link_wait_ns for carrier on every up NIC; marks the others no_carrier.
+    // L2: waits up to carrier_wait_ns for carrier on every up NIC (reported as "waiting for
+    // carrier" meanwhile); marks the others no_carrier.
     // False when stop_fd fired meanwhile.
     bool wait_carrier(int stop_fd);
     void write_rccl_env_file();

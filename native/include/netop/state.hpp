@@ -77,8 +77,11 @@ struct NicState {
     std::optional<uint64_t> rx_at_listen;  // link rx_packets when the LLDP wait began
     std::string lldp_silent;
 
-    // L2: admin-up but no carrier (IFF_LOWER_UP) within --link-wait: an unplugged cable, a dead
-    // switch port.  Not configured, not counted for readiness until the carrier comes.
+    // L2: admin-up, no carrier (IFF_LOWER_UP) yet, and still within --carrier-wait: the optic
+    // and the switch port are training (seconds on 200/400G PAM4 links).  Start-up, not a fault.
+    bool awaiting_carrier = false;
+    // L2: admin-up but no carrier within --carrier-wait: an unplugged cable, a dead switch port.
+    // Not configured, not counted for readiness until the carrier comes.
     bool no_carrier = false;
 
     // Monitor

@@ -1260,6 +1260,8 @@ std::string Agent::not_ready_reason() const {
         std::string why;
         if (n.degraded)
             why = "link down";
+        else if (n.awaiting_carrier)
+            why = "waiting for carrier";
         else if (n.no_carrier)
             why = "no carrier (check the cable, the switch port and the optic)";
         else if (!n.lldp_silent.empty())
@@ -1297,7 +1299,21 @@ void Agent::run(int stop_fd) {
                             " (an ECMAScript regular expression, {rail} = the GPU index); nothing configured";
             NLOG_E("%s", config_error_.c_str());
             if (cfg_.dry_run || !cfg_.keep_running) throw AgentError(config_error_);
-            if (!artifacts::remove_labels(cfg_.labels)) NLOG_W("Failed to remove NFD label file: %s", std::strerror(errno));
+            // Our own stale label goes; but only the node lock's holder touches the label file:
+            // when another agent of this configuration type holds it (a second policy selecting
+            // this node), the label is that agent's, and it stays.  One attempt, no wait.
+            bool owner = cfg_.node_lock.empty();
+            if (!owner) {
+                try {
+                    node_lock_fd_ = take_lock("netop-agent:" + cfg_.node_lock, mono_ns(), -1, "Node lock '" + cfg_.node_lock + "'",
+                                              "node lock held by another agent");
+                    owner = true;
+                } catch (const AgentError&) {
+                    NLOG_I("Node lock '%s' is held by another agent: its label stays", cfg_.node_lock.c_str());
+                }
+            }
+            if (owner && !artifacts::remove_labels(cfg_.labels))
+                NLOG_W("Failed to remove NFD label file: %s", std::strerror(errno));
             write_status();
             idle(stop_fd);
             return;
@@ -1319,6 +1335,22 @@ void Agent::run(int stop_fd) {
     }
 
     auto names = collect_interfaces();
+    if (names.empty() && !cfg_.dry_run && !cfg_.cleanup && cfg_.configure && cfg_.keep_running &&
+        cfg_.discovery.mode == topo::DiscoveryMode::Rdma && !excluded_.empty()) {
+        // host-nic: every RDMA NIC here is the node's own (default route, its addresses) or a GPU's
+        // scale-out rail that an amd-so agent owns.  A steady state, not a fault: configure
+        // nothing, publish no label, say so once (status file, readiness probe) and wait, instead
+        // of the reference's exit for "no interfaces" (cmd/discover/main.go:171-179) and a crash
+        // loop on every such node.  (amd-so / accel discovery keep failing: no NIC there is a fault.)
+        std::vector<std::string> parts;
+        for (const auto& [n, why] : excluded_) parts.push_back(n + ": " + why);
+        config_error_ = "no host NIC of its own (left alone: " + join(parts, "; ") + ")";
+        NLOG_W("Nothing to configure: %s", config_error_.c_str());
+        mark("discover");
+        write_status();
+        idle(stop_fd);
+        return;
+    }
     if (names.empty()) {
         // A dry run still describes the GPUs and their xGMI mesh (the intra-node topology file a
         // job on a node without scale-out NICs uses); configuring needs NICs.

@@ -409,26 +409,42 @@ bool Agent::wait_carrier(int stop_fd) {
         } catch (const std::exception&) {
         }
     }
-    auto missing = [&] {
-        return std::any_of(nics_.begin(), nics_.end(), [](const NicState& n) { return n.link.up() && !n.link.lower_up(); });
-    };
-    const int64_t deadline = mono_ns() + cfg_.link_wait_ns;
+    auto dark = [](const NicState& n) { return n.link.up() && !n.link.lower_up(); };
+    auto missing = [&] { return std::any_of(nics_.begin(), nics_.end(), dark); };
+    // While the links train, the readiness probe says so ("waiting for carrier", a start-up
+    // reason for the operator), not "no carrier": that only once carrier_wait_ns has passed.
+    int waiting = 0;
+    for (auto& n : nics_) waiting += (n.awaiting_carrier = dark(n));
+    if (waiting) {
+        NLOG_I("Waiting up to %s for carrier on %d interface(s)", format_go_duration(cfg_.carrier_wait_ns).c_str(), waiting);
+        write_status();
+    }
+    const int64_t deadline = mono_ns() + cfg_.carrier_wait_ns;
     while (watcher && missing() && mono_ns() < deadline) {
         if (fd_readable(stop_fd)) return false;
         const int64_t slice = std::min<int64_t>(deadline, mono_ns() + 100000000LL);  // stop_fd checked every 100 ms
+        bool changed = false;
         for (auto& ev : watcher->wait(slice))
             for (auto& n : nics_)
                 if (!ev.deleted && n.link.index == ev.link.index) {
                     n.link.flags = ev.link.flags;
                     n.link.operstate = ev.link.operstate;
+                    if (n.awaiting_carrier && !dark(n)) {
+                        n.awaiting_carrier = false;
+                        changed = true;
+                        NLOG_I("Interface '%s' has carrier after %s", n.ifname.c_str(),
+                               format_go_duration(mono_ns() - t0_).c_str());
+                    }
                 }
+        if (changed && missing()) write_status();  // the probe's reason names only the NICs still training
     }
     for (auto& n : nics_) {
-        n.no_carrier = n.link.up() && !n.link.lower_up();
+        n.awaiting_carrier = false;
+        n.no_carrier = dark(n);
         n.configured = n.link.up() && !n.no_carrier;
         if (n.no_carrier)
             NLOG_W("Interface '%s' has no carrier after %s (%s)", n.ifname.c_str(),
-                   format_go_duration(cfg_.link_wait_ns).c_str(), n.link.operstate_str().c_str());
+                   format_go_duration(cfg_.carrier_wait_ns).c_str(), n.link.operstate_str().c_str());
     }
     return true;
 }

@@ -517,6 +517,7 @@ std::string generate_status(const std::vector<NicState>& nics, const std::map<st
         }
         if (!n->addr_error.empty()) j.key("addr_error").value(n->addr_error);
         j.key("configured").value(n->configured);
+        if (n->awaiting_carrier) j.key("awaiting_carrier").value(true);
         if (n->no_carrier) j.key("no_carrier").value(true);
         j.key("degraded").value(n->degraded);
         if (n->flaps) j.key("flaps").value(n->flaps);

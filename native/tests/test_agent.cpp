@@ -104,6 +104,7 @@ struct Fixture {
         cfg.keep_running = true;
         cfg.wait_ns = 100000000;
         cfg.link_wait_ns = 20000000;
+        cfg.carrier_wait_ns = 20000000;
         cfg.labels.dir = tmp.path + "/features.d";
         tmp.mkdir("features.d");
         cfg.rccl_net = tmp.path + "/rccl-net.json";

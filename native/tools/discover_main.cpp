@@ -69,7 +69,8 @@ int main(int argc, char** argv) {
     fs.add_string("nm-keyfile-dir", &cfg.nm_keyfile_dir, "with --disable-networkmanager, also persist an unmanaged-devices keyfile here (removed on exit)");
     fs.add_bool("nm-restore", &cfg.nm_restore, "with --disable-networkmanager: on exit, remove the keyfile and set the interfaces managed by NetworkManager again (default: they stay unmanaged across restarts)");
     fs.add_int("xgmi-expect", &cfg.xgmi_expect_links, "verify the xGMI mesh before labelling: -1 off, 0 full mesh, N GPU pairs");
-    fs.add_duration("link-wait", &cfg.link_wait_ns, "time to wait for link state echoes from the kernel, and in L2 for carrier on every NIC (with the monitor a NIC still dark is labelled when its carrier comes)");
+    fs.add_duration("link-wait", &cfg.link_wait_ns, "time to wait for link state echoes from the kernel");
+    fs.add_duration("carrier-wait", &cfg.carrier_wait_ns, "L2: time every admin-up NIC may take to get a carrier (optic and switch port link training) before it is reported as 'no carrier'; meanwhile the readiness probe says 'waiting for carrier' (with the monitor a NIC still dark afterwards is labelled when its carrier comes)");
     fs.add_duration("verify-peers", &cfg.verify_peers_ns,
                     "L3: before publishing readiness, require every NIC's switch-side /30 address to answer ARP within this time (0 = off)");
     fs.add_duration("gid-wait", &cfg.gid_wait_ns, "time to wait for the RoCE v2 GID of a newly configured address");

@@ -27,6 +27,11 @@ LLDP_WAIT_SCHEMA = {
                    "default 90s, the reference's fixed value).  Shorter with fast-start switches, so a\n"
                    "silent NIC is diagnosed sooner; longer for switches with a long transmit interval.",
     "pattern": T.LLDP_WAIT_PATTERN, "type": "string"}
+CARRIER_WAIT_SCHEMA = {
+    "description": "L2: how long each NIC may take to get a carrier after it is set up (a Go duration,\n"
+                   "1s..10m; default 30s).  200/400G optics commonly train for 5-15 s; meanwhile the\n"
+                   "node reports \"waiting for carrier\" (start-up, not Degraded), afterwards \"no carrier\".",
+    "pattern": T.LLDP_WAIT_PATTERN, "type": "string"}
 
 _API_VERSION_DESC = (
     "APIVersion defines the versioned schema of this representation of an object.\n"
@@ -124,6 +129,7 @@ def openapi_schema() -> dict:
                                            "and interface address disagree, which LLDP alone cannot.",
                             "type": "boolean"},
             "lldpWait": LLDP_WAIT_SCHEMA,
+            "carrierWait": CARRIER_WAIT_SCHEMA,
             "keepConfigOnRestart": {
                 "description": "Keep addresses, routes and links when an agent exits (rolling update, drain,\n"
                                "crash), so RCCL jobs keep their RoCE connections; the next agent adopts them\n"
@@ -170,6 +176,7 @@ def openapi_schema() -> dict:
             "verifyPeers": {"description": "L3: label only once every NIC's switch-side /30 address answers ARP.",
                             "type": "boolean"},
             "lldpWait": LLDP_WAIT_SCHEMA,
+            "carrierWait": CARRIER_WAIT_SCHEMA,
             "keepConfigOnRestart": {"description": "As amdScaleOut.keepConfigOnRestart, for the host NICs.",
                                     "type": "boolean"},
             "checkPeerMtu": {"description": "As amdScaleOut.checkPeerMtu, for the host NICs.", "type": "boolean"},

@@ -42,6 +42,8 @@ LAYERS = ("L2", "L3")
 # lldpWait: a Go duration the agent's --wait accepts (units h, m, s, ms), checked 1s..30m by the webhook
 LLDP_WAIT_PATTERN = r"^([0-9]+(\.[0-9]+)?(h|m|s|ms))+$"
 LLDP_WAIT_MIN_S, LLDP_WAIT_MAX_S = 1.0, 1800.0
+# carrierWait: the same duration grammar; L2, how long NICs may train their links (agent default 30s)
+CARRIER_WAIT_MIN_S, CARRIER_WAIT_MAX_S = 1.0, 600.0
 
 
 def parse_go_duration(s: str) -> float:
@@ -111,6 +113,7 @@ class AmdScaleOutSpec:
     lldpCache: bool = False
     verifyPeers: bool = False
     lldpWait: str = ""  # L3 LLDP wait (Go duration); "" = the reference's 90s
+    carrierWait: str = ""  # L2 link-training allowance (Go duration); "" = the agent's 30s
     # Hitless agent restarts: addresses / routes stay when an agent exits; the operator cleans the
     # nodes up (cleanup Jobs) when the policy is deleted or a node leaves it.
     keepConfigOnRestart: bool = False
@@ -131,7 +134,7 @@ class AmdScaleOutSpec:
 
     _FIELDS = ("disableNetworkManager", "layer", "image", "pullPolicy", "mtu", "xgmiCheck", "lldpAnnounce",
                "interfaces", "nicDrivers", "disableFirmwareLldp", "metricsPort", "gpuDirectRdma", "rcclEnv",
-               "railTableBase", "rcclSocketIfname", "lldpCache", "verifyPeers", "lldpWait", "keepConfigOnRestart",
+               "railTableBase", "rcclSocketIfname", "lldpCache", "verifyPeers", "lldpWait", "carrierWait", "keepConfigOnRestart",
                "railSwitchPattern", "minLinkSpeedGbps", "checkPeerMtu", "handDcbxToHost", "validation")
 
     def to_dict(self) -> dict:
@@ -170,6 +173,8 @@ class AmdScaleOutSpec:
             d["verifyPeers"] = True
         if self.lldpWait:
             d["lldpWait"] = self.lldpWait
+        if self.carrierWait:
+            d["carrierWait"] = self.carrierWait
         if self.keepConfigOnRestart:
             d["keepConfigOnRestart"] = True
         if self.railSwitchPattern:
@@ -212,6 +217,7 @@ class AmdScaleOutSpec:
             handDcbxToHost=bool(d.pop("handDcbxToHost", False)),
             verifyPeers=bool(d.pop("verifyPeers", False)),
             lldpWait=d.pop("lldpWait", "") or "",
+            carrierWait=d.pop("carrierWait", "") or "",
             validation=ValidationSpec.from_dict(d.pop("validation", None)),
         )
         s.extra = d
@@ -233,6 +239,7 @@ class HostNicSpec:
     driverImage: str = ""
     verifyPeers: bool = False
     lldpWait: str = ""
+    carrierWait: str = ""
     keepConfigOnRestart: bool = False
     checkPeerMtu: Optional[bool] = None
     includeGpuRails: bool = False  # discovery may take the NICs next to the GPUs (no amd-so policy)
@@ -240,7 +247,7 @@ class HostNicSpec:
 
     def to_dict(self) -> dict:
         d: dict = {}
-        for k in ("layer", "image", "pullPolicy", "driverImage", "lldpWait"):
+        for k in ("layer", "image", "pullPolicy", "driverImage", "lldpWait", "carrierWait"):
             if getattr(self, k):
                 d[k] = getattr(self, k)
         if self.mtu:
@@ -270,6 +277,7 @@ class HostNicSpec:
                 interfaces=list(d.pop("interfaces", []) or []), nicDrivers=list(d.pop("nicDrivers", []) or []),
                 driverImage=d.pop("driverImage", "") or "", verifyPeers=bool(d.pop("verifyPeers", False)),
                 lldpWait=d.pop("lldpWait", "") or "",
+                carrierWait=d.pop("carrierWait", "") or "",
                 keepConfigOnRestart=bool(d.pop("keepConfigOnRestart", False)),
                 checkPeerMtu=d.pop("checkPeerMtu", None),
                 includeGpuRails=bool(d.pop("includeGpuRails", False)))

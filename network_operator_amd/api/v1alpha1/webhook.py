@@ -113,6 +113,13 @@ class InvalidLldpWaitError(ValidationError):
                         f"{int(T.LLDP_WAIT_MIN_S)}s and {int(T.LLDP_WAIT_MAX_S // 60)}m")
 
 
+class InvalidCarrierWaitError(ValidationError):
+    def __init__(self, value: str):
+        super().__init__()
+        self.message = (f"invalid carrierWait {value!r}: a duration such as 30s or 1m, between "
+                        f"{int(T.CARRIER_WAIT_MIN_S)}s and {int(T.CARRIER_WAIT_MAX_S // 60)}m")
+
+
 class InvalidRailSwitchPatternError(ValidationError):
     def __init__(self, value: str, why: str):
         super().__init__()
@@ -304,6 +311,17 @@ def validate_lldp_wait(value: str) -> None:
         raise InvalidLldpWaitError(value)
 
 
+def validate_carrier_wait(value: str) -> None:
+    if not value:
+        return
+    try:
+        secs = T.parse_go_duration(value)
+    except ValueError:
+        raise InvalidCarrierWaitError(value) from None
+    if not T.CARRIER_WAIT_MIN_S <= secs <= T.CARRIER_WAIT_MAX_S:
+        raise InvalidCarrierWaitError(value)
+
+
 def validate_amd_so_spec(s: T.AmdScaleOutSpec) -> List[str]:
     """Returns admission warnings.  (The reference's validateGaudiSoSpec is a no-op, :87-89.)"""
     warnings = []
@@ -318,6 +336,9 @@ def validate_amd_so_spec(s: T.AmdScaleOutSpec) -> List[str]:
     validate_lldp_wait(s.lldpWait)
     if s.lldpWait and s.layer == "L2":
         warnings.append("lldpWait has no effect in L2 mode")
+    validate_carrier_wait(s.carrierWait)
+    if s.carrierWait and s.layer == "L3":
+        warnings.append("carrierWait has no effect in L3 mode (the LLDP wait covers link training)")
     validate_rail_switch_pattern(s.railSwitchPattern)
     if s.railSwitchPattern and s.layer == "L2":
         warnings.append("railSwitchPattern has no effect in L2 mode (no LLDP)")
@@ -339,7 +360,10 @@ def validate_host_nic_spec(s: Optional[T.HostNicSpec]) -> List[str]:
         if not i or len(i) > 15 or "/" in i or " " in i or "," in i:
             raise InvalidInterfaceError(i)
     validate_lldp_wait(s.lldpWait)
+    validate_carrier_wait(s.carrierWait)
     warnings = []
+    if s.carrierWait and s.layer == "L3":
+        warnings.append("hostNic: carrierWait has no effect in L3 mode (the LLDP wait covers link training)")
     if not s.interfaces and not s.nicDrivers:
         warnings.append("hostNic: no interfaces or nicDrivers given; every RDMA NIC of the default driver list "
                         "that is neither a GPU's scale-out rail nor the node's own NIC (default route, non-/30 "

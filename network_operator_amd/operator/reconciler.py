@@ -30,7 +30,7 @@ import copy
 import time
 import logging
 from dataclasses import dataclass
-from typing import Callable, Dict, List, Optional
+from typing import Callable, Dict, List, Optional, Set, Tuple
 
 from .. import discovery
 from ..api.v1alpha1 import types as T
@@ -157,6 +157,8 @@ def agent_args(p: T.NetworkClusterPolicy) -> List[str]:
         # MI355X: RCCL needs the HCA list and the link-local RoCE v2 GID in L2 as well (Gaudi's
         # firmware did not, so the reference passes nothing in L2).
         args.append(f"--rccl-env={ARTIFACT_DIR_CONTAINER}/{RCCL_ENV_FILE}")
+        if so.carrierWait:
+            args.append(f"--carrier-wait={so.carrierWait}")
     # NCCL_TOPO_FILE: written through the agent's mount, named in rccl.env by the host path jobs
     # mount (the reference's HCCL contract is gaudinet.json, controller.go:198-200).
     args += [f"--rccl-topo={ARTIFACT_DIR_CONTAINER}/{RCCL_TOPO_FILE}",
@@ -277,6 +279,8 @@ def host_nic_agent_args(p: T.NetworkClusterPolicy) -> List[str]:
         args.append(f"--wait={hn.lldpWait or L3_WAIT}")
         if hn.verifyPeers:
             args.append(f"--verify-peers={VERIFY_PEERS_TIMEOUT}")
+    elif hn.carrierWait:
+        args.append(f"--carrier-wait={hn.carrierWait}")
     if hn.interfaces:
         args.append("--interfaces=" + ",".join(hn.interfaces))
     if hn.nicDrivers:
@@ -427,7 +431,9 @@ def probe_reason(events: List[dict], limit: int = 1500) -> Optional[str]:
     return msg[:limit] or None
 
 
-STARTUP_REASONS = ("waiting for LLDP", "not configured yet")
+# What an agent says while its node is still coming up.  "waiting for carrier": L2, a NIC whose
+# optic / switch port is still training its link, within the agent's --carrier-wait.
+STARTUP_REASONS = ("waiting for LLDP", "not configured yet", "waiting for carrier")
 
 
 def _starting_up(reason: str) -> bool:
@@ -724,7 +730,6 @@ class NetworkClusterPolicyReconciler:
         self._list_job_pods = list_job_pods  # the Pods of a validation Job (by its name)
         self._list_probe_events = list_probe_events  # kubelet "Unhealthy" events of an agent Pod (by its name)
         self._list_policies = list_policies  # every policy (the informer cache): conflicting selections
-        self._degraded_errors: set = set()  # status.errors entries that came from a probe, not an exit
         self._clock = clock
         self.recorder = recorder
         # keepConfigOnRestart: (policy, node) -> when the node's agent Pod was first seen missing
@@ -733,12 +738,17 @@ class NetworkClusterPolicyReconciler:
         self._cleanups_reported: set = set()  # finished cleanup Jobs already counted / reported
         self._cleanup_jobs_exist: set = set()  # policies with cleanup Jobs left to finish or delete
 
-    def _node_errors(self, ds_name: str, limit: int = 16) -> List[str]:
+    def _node_errors(self, ds_name: str, limit: int = 16) -> Tuple[List[str], Set[str], Set[str]]:
         """Per-node agent problems from the agent Pods' Ready condition (the reference indexes
-        Pods by owner but never reads them and always reports ``errors: []``)."""
-        self._degraded_errors = set()
+        Pods by owner but never reads them and always reports ``errors: []``).  Also returns
+        which entries are a running node that degraded (its probe, not an exit) and which are a
+        node still starting up (a start-up reason, or a running agent not probed yet): those
+        do not make the policy Degraded.  Returned, not kept on the reconciler: two workers
+        reconcile two policies at once."""
+        degraded: Set[str] = set()
+        starting: Set[str] = set()
         if self._list_pods is None:
-            return []
+            return [], degraded, starting
         errs = []
         for pod in sorted(self._list_pods(ds_name), key=lambda p: p.get("spec", {}).get("nodeName", "")):
             conds = {c.get("type"): c for c in (pod.get("status", {}) or {}).get("conditions", []) or []}
@@ -749,16 +759,20 @@ class NetworkClusterPolicyReconciler:
             err = f"{node}: scale-out not ready ({ready.get('reason') or pod.get('status', {}).get('phase', 'Pending')})"
             # A running agent that withdrew its label says why through its probe (kubelet event);
             # an agent that exited, through its termination message.
+            running = _container_running(pod)
             probed = probe_reason(self._list_probe_events(pod["metadata"]["name"])) \
-                if self._list_probe_events is not None and (_container_running(pod) or not agent_exit_reason(pod)) \
+                if self._list_probe_events is not None and (running or not agent_exit_reason(pod)) \
                 else None
             why = probed or agent_exit_reason(pod)
+            entry = f"{err}: {why}" if why else err
             if probed and not _starting_up(probed):
-                self._degraded_errors.add(f"{err}: {why}")
-            errs.append(f"{err}: {why}" if why else err)
+                degraded.add(entry)
+            elif (probed and _starting_up(probed)) or (why is None and running):
+                starting.add(entry)
+            errs.append(entry)
         if len(errs) > limit:
             errs = errs[:limit] + [f"... and {len(errs) - limit} more"]
-        return errs
+        return errs, degraded, starting
 
     def _conflicts(self, p: T.NetworkClusterPolicy, ds_name: str) -> List[str]:
         """Nodes this policy's agents share with an older live policy of the same type (from the
@@ -1161,7 +1175,9 @@ class NetworkClusterPolicyReconciler:
         new_state = status_for(targets, ready)
         errors = [f"dependency missing: {d}" for d in self.missing_dependencies]
         errors += self._conflicts(p, ds["metadata"]["name"])
-        errors += self._node_errors(ds["metadata"]["name"]) if targets and ready < targets else []
+        node_errs, degraded, starting = self._node_errors(ds["metadata"]["name"]) if targets and ready < targets \
+            else ([], set(), set())
+        errors += node_errs
         generation = int(raw.get("metadata", {}).get("generation", 0) or 0)
         # Validation first: it adds its failed nodes to `errors`, and the comparison with the stored
         # status must see the whole list (else every reconcile rewrites an unchanged status).
@@ -1172,7 +1188,10 @@ class NetworkClusterPolicyReconciler:
             requeue_after = min(requeue_after, kept_requeue) if requeue_after else kept_requeue
         if cur.state != new_state or cur.errors != errors or cur.keptNodes != kept:
             updated = True
-        conditions = policy_conditions(cur.conditions, targets, ready, errors, generation)
+        # Nodes still starting up are in status.errors (with their reason) and keep Ready False,
+        # but they are not a degradation.
+        conditions = policy_conditions(cur.conditions, targets, ready, [e for e in errors if e not in starting],
+                                       generation)
         if validated is not None:
             now = _now_rfc3339()
             old_v = [dict(c) for c in cur.conditions if c.get("type") == COND_VALIDATED]
@@ -1202,7 +1221,7 @@ class NetworkClusterPolicyReconciler:
             if e not in cur.errors and CONFLICT_MARK in e:
                 await self._event(raw, "Warning", "PolicyConflict", e[:1024])
             elif e not in cur.errors and "scale-out not ready (" in e and "): " in e:
-                if e in self._degraded_errors:
+                if e in degraded:
                     await self._event(raw, "Warning", "NodeDegraded", e[:1024])
                 elif not e.endswith(tuple(STARTUP_REASONS)):
                     await self._event(raw, "Warning", "AgentFailed", e[:1024])

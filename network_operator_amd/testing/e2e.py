@@ -113,8 +113,9 @@ async def _scrape(port: int, names) -> dict:
     return out
 
 
-# HA run: lease timings short enough for a test (controller-runtime's are 15 s / 10 s / 2 s).
-_LEASE_ARGS = ("--leader-elect-lease-duration=2", "--leader-elect-renew-deadline=1.5",
+# HA run: lease timings short enough for a test (controller-runtime's are 15 s / 10 s / 2 s), with
+# the stop margin the flag check requires (lease - renew > leader.STOP_BUDGET_S).
+_LEASE_ARGS = ("--leader-elect-lease-duration=3", "--leader-elect-renew-deadline=1.5",
                "--leader-elect-retry-period=0.25")
 
 
@@ -247,7 +248,8 @@ async def _ha_checks(fake, c, rt, node, replicas: list, ns: str, name: str, mode
 async def _scenario(tmp: Path, n_nics: int, mode: str, seed: int, interval: str, fast_start: bool,
                     teardown: bool, node_name: str, policy_kw: dict, update_mtu: int, config_type: str,
                     flap: bool, validation: str, crash_agent: bool, driver_reload: bool, ha: bool,
-                    silent_nics: int = 0, lldp_wait: str = "", duplicate_policy: bool = False) -> dict:
+                    silent_nics: int = 0, lldp_wait: str = "", duplicate_policy: bool = False,
+                    dark_port_s: float = 0.0, host_nics_owned: bool = False) -> dict:
     from ..api.v1alpha1 import types as T
     from ..operator import kube, manager
     from ..operator.kube import ApiClient, KubeConfig
@@ -278,6 +280,19 @@ async def _scenario(tmp: Path, n_nics: int, mode: str, seed: int, interval: str,
     sw = netns.SyntheticSwitch(nic_names, plan, rng, interval=interval, phase="random", fast_start=fast_start,
                                silent_nics=silent_nics)
     sw.start(rt)
+    if host_nics_owned:
+        # Both host NICs are the node's own: the first carries its management address and
+        # default route, the second its storage network.  A host-nic policy has nothing to do.
+        for k, nif in enumerate(HOST_NICS):
+            idx = rt.link_by_name(nif)["index"]
+            rt.link_set_up(idx)
+            rt.addr_add(idx, f"192.168.{70 + k}.10/24")
+            if k == 0:
+                rt.route_append("0.0.0.0/0", "192.168.70.1", idx, 16)
+    if dark_port_s:
+        # The first NIC's switch port comes up `dark_port_s` after the agent starts: an optic
+        # still training its link (5-15 s on 200/400G).
+        netns.set_switch_port(sw.pid, sw.ports[0], False)
 
     res: dict = {"n_nics": len(nic_names), "mode": mode, "plan": plan, "nics": nic_names, "fast_start": fast_start}
     fake = FakeApiServer(extra_groups=["nfd.k8s-sigs.io", "cert-manager.io"])
@@ -333,6 +348,41 @@ async def _scenario(tmp: Path, n_nics: int, mode: str, seed: int, interval: str,
             await c.create(P, pol)
             t_ds = await _until(lambda: fake.get_object(DS, name, ns) is not None, 10)
             t_agent = await _until(lambda: any(x.proc is not None for x in node.containers.values()), 10)
+            if host_nics_owned:
+                def idle_errors():
+                    st = (fake.get_object(P, name) or {}).get("status") or {}
+                    return [e for e in st.get("errors") or [] if "no host NIC of its own" in e]
+                t_err = await _until(lambda: bool(idle_errors()), 20)
+                await asyncio.sleep(7.0)  # more than one probe period: repeated probes, one report
+                evs = [e for e in fake.list_objects(kube.EVENTS) if (e.get("involvedObject") or {}).get("kind") == T.KIND]
+                res["idle"] = {
+                    "policy_to_reason_s": round(t_err - t0, 6) if t_err else None,
+                    "status_errors": idle_errors(),
+                    "policy_events": [(e.get("reason"), e.get("count", 1), e.get("message", "")) for e in evs],
+                    "probe_failures": sum(int(e.get("count", 1)) for e in fake.list_objects(kube.EVENTS)
+                                          if e.get("reason") == "Unhealthy"),
+                    "agent_restarts": sum(x.restarts for x in node.containers.values()),
+                    "agent_running": any(x.proc is not None and x.proc.poll() is None for x in node.containers.values()),
+                    "exited": len(node.exited), "label": node.node_labels().get(label_key)}
+                res["policy_status"] = (fake.get_object(P, name) or {}).get("status")
+                return res
+            dark_watch = None
+            if dark_port_s:
+                seen: dict = {"degraded": [], "errors": []}
+
+                async def watch_policy():  # every Degraded=True and every status error, however brief
+                    while True:
+                        st = (fake.get_object(P, name) or {}).get("status") or {}
+                        for cnd in st.get("conditions") or []:
+                            d = f"{cnd.get('reason')}: {cnd.get('message')}"
+                            if cnd.get("type") == "Degraded" and cnd.get("status") == "True" and d not in seen["degraded"]:
+                                seen["degraded"].append(d)
+                        seen["errors"].extend(e for e in st.get("errors") or [] if e not in seen["errors"])
+                        await asyncio.sleep(0.005)
+                dark_watch = asyncio.ensure_future(watch_policy())
+                await asyncio.sleep(max(0.0, t_agent + dark_port_s - time.monotonic()))
+                netns.set_switch_port(sw.pid, sw.ports[0], True)
+                t_port_up = time.monotonic()
             if silent_nics:
                 # A switch port that never sends LLDP: the agent's exit error names the NIC, its
                 # driver and what it heard, and the operator puts that into status.errors.
@@ -375,6 +425,17 @@ async def _scenario(tmp: Path, n_nics: int, mode: str, seed: int, interval: str,
 
             t_good = await _until(all_good, 30)
             rel = lambda t: round(t - t0, 6) if t else None  # noqa: E731
+            if dark_watch is not None:
+                dark_watch.cancel()
+                res["dark_port"] = {
+                    "port_up_after_agent_s": round(t_port_up - t_agent, 6),
+                    "port_up_to_label_s": round(t_label - t_port_up, 6) if t_label else None,
+                    "degraded_seen": seen["degraded"], "errors_seen": seen["errors"],
+                    "policy_events": sorted({e.get("reason") for e in fake.list_objects(kube.EVENTS)
+                                             if (e.get("involvedObject") or {}).get("kind") == T.KIND}),
+                    "probe_events": [e.get("message") for e in fake.list_objects(kube.EVENTS)
+                                     if e.get("reason") == "Unhealthy"],
+                    "agent_restarts": sum(x.restarts for x in node.containers.values())}
             res.update(policy_to_daemonset_s=rel(t_ds), policy_to_agent_start_s=rel(t_agent),
                        policy_to_node_label_s=rel(t_label), policy_to_all_good_s=rel(t_good))
             res["policy_status"] = (fake.get_object(P, name) or {}).get("status")
@@ -727,13 +788,14 @@ def run_scenario(n_nics: int = 2, mode: str = "L3", seed: int = 1, interval: str
                  update_mtu: int = 0, config_type: str = "amd-so", flap: bool = False, validation: str = "",
                  crash_agent: bool = False, driver_reload: bool = False, ha: bool = False,
                  silent_nics: int = 0, lldp_wait: str = "", keep_tmp: bool = False,
-                 duplicate_policy: bool = False) -> dict:
+                 duplicate_policy: bool = False, dark_port_s: float = 0.0, host_nics_owned: bool = False) -> dict:
     """Must already run inside a private user+net namespace (``run_isolated``)."""
     tmp = Path(tempfile.mkdtemp(prefix="netop-e2e-"))
     try:
         return asyncio.run(_scenario(tmp, n_nics, mode, seed, interval, fast_start, teardown, node_name,
                                      dict(policy_kw or {}), update_mtu, config_type, flap, validation,
-                                     crash_agent, driver_reload, ha, silent_nics, lldp_wait, duplicate_policy))
+                                     crash_agent, driver_reload, ha, silent_nics, lldp_wait, duplicate_policy,
+                                     dark_port_s=dark_port_s, host_nics_owned=host_nics_owned))
     finally:
         if not keep_tmp:
             shutil.rmtree(tmp, ignore_errors=True)

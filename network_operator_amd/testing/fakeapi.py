@@ -637,10 +637,13 @@ class FakeApiServer:
                                           "message": "containers with unready status: [configurator]"})}]
             status = {"phase": "Running", "conditions": cond}
             last = self.node_last_exit.get((f"{ns}/{name}", node))
+            cname = ((ds["spec"]["template"].get("spec") or {}).get("containers") or [{}])[0].get("name", "agent")
             if last:
-                cname = ((ds["spec"]["template"].get("spec") or {}).get("containers") or [{}])[0].get("name", "agent")
                 status["containerStatuses"] = [{"name": cname, "ready": ready, "restartCount": last["restartCount"],
                                                 "lastState": {"terminated": last["terminated"]}}]
+            else:  # the agent container started and has not exited (what the kubelet reports)
+                status["containerStatuses"] = [{"name": cname, "ready": ready, "restartCount": 0,
+                                                "state": {"running": {}}}]
             labels = dict((ds["spec"]["template"].get("metadata") or {}).get("labels") or {})
             if cur is None:
                 pod = {"apiVersion": "v1", "kind": "Pod",

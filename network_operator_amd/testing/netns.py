@@ -315,7 +315,8 @@ def run_scenario(n_nics: int = 8, mode: str = "L3", seed: int | None = None, int
                  egress_probe: bool = False, nm_bus: bool = False, nm_restore: bool = True, lldp_cache: bool = False,
                  soak_cycles: int = 0, arp_silent_ports: int = 0, switch_name: str = "",
                  port_switch_names: dict | None = None, nic_speeds_mbps: list | None = None,
-                 switch_max_frame: int = 0, dark_port: int | None = None) -> dict:
+                 switch_max_frame: int = 0, dark_port: int | None = None,
+                 dark_port_up_after: float | None = None) -> dict:
     """Runs one node bring-up.  Must already be inside a private user+net namespace.
 
     nm_bus: run the agent with --disable-networkmanager against a real ``dbus-daemon`` on which a
@@ -326,7 +327,9 @@ def run_scenario(n_nics: int = 8, mode: str = "L3", seed: int | None = None, int
     the restart the switch's frames confirmed every cached Port Description.
 
     dark_port: that switch port is down when the agent starts (the NIC has no carrier); once the
-    agent has said why it is not ready, the port comes up and the label must follow."""
+    agent has said why it is not ready, the port comes up and the label must follow.
+    dark_port_up_after: instead, the port comes up that many seconds after the agent started (an
+    optic still training its link); every reason and status the agent wrote meanwhile is kept."""
     from . import fakesysfs
 
     nat = _native()
@@ -418,9 +421,41 @@ def run_scenario(n_nics: int = 8, mode: str = "L3", seed: int | None = None, int
         agent = spawn()
         budget = 5.0 + float(wait.rstrip("s"))
         dark: dict = {}
-        if dark_port is not None:
+        if dark_port is not None and dark_port_up_after is not None:
+            reason, status = tmp / "status.json.not-ready", tmp / "status.json"
+            seen_reasons, seen_flags = [], set()
+            while time.monotonic() < t0 + dark_port_up_after and agent.poll() is None:
+                try:
+                    why = reason.read_text()
+                    if why and why not in seen_reasons:
+                        seen_reasons.append(why)
+                except OSError:
+                    pass
+                try:
+                    for i in json.loads(status.read_text()).get("interfaces", []):
+                        seen_flags |= {f"{i['name']}:{k}" for k in ("awaiting_carrier", "no_carrier") if i.get(k)}
+                except (OSError, ValueError):
+                    pass
+                time.sleep(0.05)
+            dark["reasons_seen"], dark["status_flags_seen"] = seen_reasons, sorted(seen_flags)
+            dark["label_while_dark"] = label.exists()
+            t_up = time.monotonic()
+            set_switch_port(pid, sw_ports[dark_port], True)
+            t_ready = _wait_for(label, 10, agent)
+            dark["port_up_s"] = t_up - t0
+            dark["port_up_to_label_s"] = (t_ready - t_up) if t_ready else None
+        elif dark_port is not None:
             reason = tmp / "status.json.not-ready"
             t_why = _wait_for(reason, budget, agent)
+            # Past --carrier-wait: "waiting for carrier" turns into the fault.
+            while t_why and time.monotonic() < t0 + budget and agent.poll() is None:
+                try:
+                    if "waiting for carrier" not in reason.read_text():
+                        break
+                except OSError:
+                    pass
+                time.sleep(0.02)
+            t_why = time.monotonic() if t_why else None
             dark["reason_s"] = (t_why - t0) if t_why else None
             dark["label_while_dark"] = label.exists()
             dark["reason"] = reason.read_text() if reason.exists() else None
@@ -633,7 +668,7 @@ MGMT_NIC, HOST_NIC = "ens9np0", "ens49np1"  # the fixture node's two NICs on the
 
 
 def run_host_nic_ownership(mode: str = "L2", rails: int = 8, mgmt_bridge: bool = False,
-                           include_gpu_rails: bool = False) -> dict:
+                           include_gpu_rails: bool = False, host_nic_addr: str = "") -> dict:
     """A default ``host-nic`` policy's agent (rdma discovery, the default driver list) on the
     captured MI355X node, where every NIC is mlx5 with an RDMA device:
 
@@ -647,7 +682,10 @@ def run_host_nic_ownership(mode: str = "L2", rails: int = 8, mgmt_bridge: bool =
     address and the default route sit on a bridge ``br0`` and ``ens9np0`` is only its port (the
     kernel's IFLA_MASTER is all that links them here: this sysfs is a fake).  With
     ``include_gpu_rails`` the agent runs as ``hostNic.includeGpuRails`` makes it (a node without
-    amd-so): it takes the rails too, never the management NIC.  Must run inside ``unshare -rn``."""
+    amd-so): it takes the rails too, never the management NIC.  With ``host_nic_addr`` the
+    second NIC is the node's own too (e.g. its storage network, that address /24): nothing is
+    left for the agent, which must stay up unlabelled and say why (``idle``).  Must run inside
+    ``unshare -rn``."""
     from . import fakesysfs
     from ..utils.paths import native_bin
 
@@ -676,6 +714,10 @@ def run_host_nic_ownership(mode: str = "L2", rails: int = 8, mgmt_bridge: bool =
             m = br
         rt.addr_add(m, "192.168.77.10/24")
         rt.route_append("0.0.0.0/0", "192.168.77.1", m, 16)  # a DHCP lease's default route
+        if host_nic_addr:
+            h = rt.link_by_name(HOST_NIC)["index"]
+            rt.link_set_up(h)
+            rt.addr_add(h, host_nic_addr)
 
         def snapshot() -> dict:
             out = {}
@@ -701,7 +743,17 @@ def run_host_nic_ownership(mode: str = "L2", rails: int = 8, mgmt_bridge: bool =
             extra = ["--rdma-include-gpu-rails"] if include_gpu_rails else []
             agent = subprocess.Popen([*base, "--nic-discovery=rdma", *extra, f"--status-file={tmp / 'status.json'}"],
                                      env=env, stdout=logf, stderr=subprocess.STDOUT)
-        t_ready = _wait_for(label, 15, agent)
+        if host_nic_addr:
+            reason = tmp / "status.json.not-ready"
+            t_why = _wait_for(reason, 15, agent)
+            time.sleep(1.0)  # still running a second later: no exit, no restart
+            res["idle"] = {"reason_s": t_why is not None, "running": agent.poll() is None,
+                           "label": label.exists(), "reason": reason.read_text() if reason.exists() else None}
+            pr = subprocess.run([str(native_bin("discover")), "--ready-check", f"--nfd-features-dir={feat}",
+                                 "--nfd-label-file=host-nic-readiness.txt", f"--status-file={tmp / 'status.json'}"],
+                                capture_output=True, text=True, timeout=10)
+            res["idle"]["ready_check"] = {"rc": pr.returncode, "stdout": pr.stdout.strip()}
+        t_ready = _wait_for(label, 0.0 if host_nic_addr else 15, agent)
         res["ready"] = t_ready is not None
         res["label"] = label.read_text() if label.exists() else None
         time.sleep(0.05)  # status.json follows the label

@@ -351,11 +351,14 @@ class SimNode:
             for c in list(self.containers.values()):
                 if c.probe is None or c.proc is None or c.proc.poll() is not None:
                     continue
+                probed = c.proc
                 p = await asyncio.create_subprocess_exec(*c.probe, env=self._env(c), stdout=asyncio.subprocess.PIPE,
                                                          stderr=asyncio.subprocess.DEVNULL)
                 out, _ = await p.communicate()
                 rc = p.returncode
-                if c is self.containers.get(c.pod):
+                # The kubelet drops a probe result of a container that has died meanwhile (its
+                # exit already made the Pod unready): applying it would mark a dead agent ready.
+                if c is self.containers.get(c.pod) and c.proc is probed and probed.poll() is None:
                     if rc != 0:  # the kubelet's event for a failed probe, with the probe's output
                         self.fake.record_probe_failure(c.pod[0], c.pod[1],
                                                        "Readiness probe failed: " + out.decode(errors="replace").strip())

@@ -430,7 +430,7 @@ _AMD_VALUES = {
     "mode": "L3", "mtu": 4200, "disableNetworkManager": True, "xgmiCheck": False, "lldpAnnounce": False,
     "interfaces": ["ens1np0", "ens2np0"], "nicDrivers": ["mlx5_core", "bnxt_en"], "disableFirmwareLldp": True,
     "metricsPort": 9501, "gpuDirectRdma": "DmaBuf", "rcclEnv": {"NCCL_IB_TC": "106"}, "railTableBase": 100,
-    "rcclSocketIfname": "eno1", "lldpCache": True, "verifyPeers": True, "lldpWait": "2m",
+    "rcclSocketIfname": "eno1", "lldpCache": True, "verifyPeers": True, "lldpWait": "2m", "carrierWait": "45s",
     "keepConfigOnRestart": True, "railSwitchPattern": "leaf-r{rail}-.*", "minLinkSpeedGbps": 400,
     "checkPeerMtu": False, "handDcbxToHost": True, "maxUnavailable": "25%",
     "validation": {"enabled": True, "minBusbw": 300, "minLink": 40, "gpus": 4, "image": "reg/val:1"},
@@ -440,7 +440,7 @@ _AMD_VALUES = {
 }
 _HOST_NIC_VALUES = {
     "enabled": True, "mode": "L3", "mtu": 4000, "nicDrivers": ["bnxt_en"], "driverImage": "reg/kmd:1",
-    "interfaces": ["ens9np0"], "disableNetworkManager": True, "verifyPeers": True, "lldpWait": "45s",
+    "interfaces": ["ens9np0"], "disableNetworkManager": True, "verifyPeers": True, "lldpWait": "45s", "carrierWait": "1m",
     "checkPeerMtu": False, "keepConfigOnRestart": True, "includeGpuRails": True,
 }
 
@@ -482,9 +482,11 @@ def test_every_policy_field_is_settable_from_the_chart_and_documented():
         assert getattr(hn, k) == v, k
     assert not hn.extra
 
-    assert W.validate_create(seeded["netconf-amd-scale-out"]) == []
+    # (carrierWait is an L2 setting; these values are an L3 policy)
+    assert [w for w in W.validate_create(seeded["netconf-amd-scale-out"]) if "carrierWait" not in w] == []
     # (includeGpuRails next to interfaces only draws the "no effect" warning)
-    assert [w for w in W.validate_create(seeded["netconf-amd-host-nic"]) if "includeGpuRails" not in w] == []
+    assert [w for w in W.validate_create(seeded["netconf-amd-host-nic"])
+            if "includeGpuRails" not in w and "carrierWait" not in w] == []
 
     # Defaults render the policy the CRD defaults describe: no optional field forced on.
     plain = yaml.safe_load(_configmap_text(helm_template(CHART, {"config": {"amd": {"enabled": True},

@@ -443,7 +443,7 @@ def test_l2_waits_for_carrier_on_every_nic_before_the_label():
     comes up and the monitor publishes the label (the reference labels right after link-up,
     reference cmd/discover/main.go:198-206,239-246)."""
     r = netns.run_isolated(n_nics=3, seed=41, mode="L2", interval="1s", dark_port=1,
-                           extra_args=["--link-wait=300ms"])
+                           extra_args=["--carrier-wait=300ms"])
     d = r["dark"]
     dark_nic = r["nics"][1]
     assert d["reason_s"] is not None, r["agent_log"]
@@ -457,3 +457,41 @@ def test_l2_waits_for_carrier_on_every_nic_before_the_label():
     for nic in r["nics"]:
         assert r["state"][nic]["up"] and r["state"][nic]["addrs"] == []
     assert r["agent_rc"] == 0
+
+
+def test_l2_link_still_training_is_start_up_not_no_carrier():
+    """a 200/400G optic commonly trains for 5-15 s.  The switch port comes
+    up 5 s after the agent started; with the default --carrier-wait (30 s) the agent reports
+    "waiting for carrier" meanwhile (a start-up reason for the operator), never "no carrier",
+    and publishes the label milliseconds after the carrier arrives.  (The 3 s --link-wait is the
+    netlink echo wait, reference cmd/discover/network.go:242-283, not a carrier wait.)"""
+    r = netns.run_isolated(n_nics=3, seed=43, mode="L2", interval="1s", dark_port=1, dark_port_up_after=5.0)
+    d = r["dark"]
+    dark_nic = r["nics"][1]
+    assert d["port_up_s"] >= 5.0 and d["label_while_dark"] is False, r["agent_log"]
+    assert d["reasons_seen"] == [f"{dark_nic}: waiting for carrier\n"], d["reasons_seen"]
+    assert d["status_flags_seen"] == [f"{dark_nic}:awaiting_carrier"], d["status_flags_seen"]
+    assert r["ready"] and d["port_up_to_label_s"] is not None and d["port_up_to_label_s"] < 0.5, r["agent_log"]
+    assert "no carrier" not in r["agent_log"]
+    assert f"Interface '{dark_nic}' has carrier after" in r["agent_log"]
+    assert r["agent_rc"] == 0
+
+
+def test_host_nic_policy_with_nothing_of_its_own_idles_with_one_reason():
+    """a default host-nic policy on a node whose RDMA NICs are all taken --
+    the rails by amd-so, the management NIC (default route) and the storage NIC (its /24) by the
+    node.  The agent configures nothing, publishes no label, stays up (no crash loop) and says
+    why in status.json and through --ready-check.  (The reference exits for "no interfaces",
+    reference cmd/discover/main.go:171-179; for amd-so that stays a failure.)"""
+    r = netns.run_isolated(host_nic_ownership=True, host_nic_addr="10.9.8.7/24")
+    idle = r["idle"]
+    assert idle["reason_s"] and idle["running"] and not idle["label"], r["agent_log"]
+    assert idle["reason"].startswith("no host NIC of its own (left alone: "), idle["reason"]
+    assert f"{netns.MGMT_NIC}: the node's own NIC: it carries the node's default route" in idle["reason"]
+    assert f"{netns.HOST_NIC}: the node's own NIC" in idle["reason"]
+    assert idle["ready_check"]["rc"] == 1 and "no host NIC of its own" in idle["ready_check"]["stdout"]
+    assert r["ready"] is False and r["status"]["ready"] is False and r["status"]["interfaces"] == []
+    assert f"{netns.MGMT_NIC}: the node's own NIC" in r["status"]["excluded"]
+    for nif in r["rails"] + [netns.MGMT_NIC, netns.HOST_NIC]:  # nothing touched, before or after SIGTERM
+        assert r["while_ready"][nif] == r["before"][nif] and r["after_sigterm"][nif] == r["before"][nif], nif
+    assert r["agent_rc"] == 0  # SIGTERM ends the wait cleanly

@@ -552,9 +552,21 @@ def test_status_conditions_ready_degraded_and_observed_generation():
             def not_ready():
                 st, c = conds()
                 assert c["Ready"]["status"] == "False" and c["Ready"]["reason"] == "NodesNotReady"
-                assert c["Degraded"]["status"] == "True" and c["Degraded"]["reason"] == "AgentErrors"
+                # agents running, not probed yet: nodes starting up, not a degradation
+                assert c["Degraded"]["status"] == "False" and c["Degraded"]["reason"] == "AsExpected"
                 assert st["observedGeneration"] == 1 and c["Ready"]["observedGeneration"] == 1
+                assert len(st["errors"]) == 2
             await eventually(not_ready)
+            fake.record_probe_failure(NS, "policy-gpu-node-1", "Readiness probe failed: not ready: ens1: waiting for carrier")
+            await eventually(lambda: any("waiting for carrier" in e for e in conds()[0]["errors"]))
+            assert conds()[1]["Degraded"]["status"] == "False"  # a start-up reason
+            fake.record_probe_failure(NS, "policy-gpu-node-1", "Readiness probe failed: not ready: ens1: link down")
+
+            def degraded():
+                st, c = conds()
+                assert c["Degraded"]["status"] == "True" and c["Degraded"]["reason"] == "AgentErrors"
+                assert "ens1: link down" in c["Degraded"]["message"] and "gpu-node-0" not in c["Degraded"]["message"]
+            await eventually(degraded)
             degraded_since = conds()[1]["Degraded"]["lastTransitionTime"]
             fake.set_agent_ready("gpu-node-0")
 
