@@ -7,7 +7,7 @@ simulation) runs in this process with N GPU nodes; the real manager runs as a se
 Measured:
 
 * ``daemonsets_s``:  P policies created -> P agent DaemonSets exist;
-* ``targets_s``:     -> every policy's status.targets == N;
+* ``targets_s``:     -> every policy's status.targets == the nodes of its pool;
 * ``all_good_s``:    every agent on every node reports ready -> every policy "All good";
 * ``manager_rss_mib``: the manager's peak RSS (VmHWM), against the Deployment's 128Mi limit
   (reference config/operator/manager/manager.yaml:95-101);
@@ -19,6 +19,11 @@ Measured:
 With ``--keep-config`` the policies use ``keepConfigOnRestart``, and the run goes on to delete
 them: ``delete_to_cleanup_jobs_s`` (every node's cleanup Job exists), then the simulated kubelets
 complete them, and ``cleanup_done_to_gone_s`` (every policy finalized and gone).
+
+The policies alternate between ``amd-so`` and ``host-nic`` and the nodes are split into
+ceil(P/2) pools: each node runs one agent of each type (two policies of one type never share a
+node -- the newer is held off, reconciler.hold_off_terms), so a run has 2N agent Pods for P >= 2.
+(Until round 4 every policy was an amd-so on every node: P*N Pods, now a conflict by design.)
 
 The reference has no equivalent measurement (controller-runtime + envtest, no scale test).
 
@@ -77,8 +82,10 @@ async def _until(pred, timeout: float, poll: float = 0.005) -> float:
 async def run(nodes: int, policies: int, timeout: float, keep: bool = False, validation: bool = False) -> dict:
     fake = FakeApiServer(bookmark_interval=5.0)
     url = await fake.start()
+    pools = max(1, (policies + 1) // 2)
     for i in range(nodes):
-        fake.add_node(f"gpu-node-{i:04d}", {LABEL: "true"})
+        fake.add_node(f"gpu-node-{i:04d}", {LABEL: "true", "pool": str(i % pools)})
+    pool_size = {k: sum(1 for i in range(nodes) if i % pools == k) for k in range(pools)}
     env = dict(os.environ, PYTHONPATH=ROOT, OPERATOR_NAMESPACE="amd-network-operator", ENABLE_WEBHOOKS="false")
     # The manager's log goes to a file: a pipe nobody reads fills up and blocks it (one log line
     # per cleanup Job at scale).
@@ -94,16 +101,23 @@ async def run(nodes: int, policies: int, timeout: float, keep: bool = False, val
         cpu0 = _cpu_s(proc.pid)
         P = kube.NETWORKCLUSTERPOLICIES
         names = [f"policy-{k}" for k in range(policies)]
+        want = {n: pool_size[k // 2] for k, n in enumerate(names)}
+        amd = [n for k, n in enumerate(names) if k % 2 == 0]
         t0 = time.perf_counter()
-        for n in names:
-            fake._create(P, T.new_policy(n, keepConfigOnRestart=keep,
-                                         validation={"enabled": True} if validation else None).to_dict(), None)
+        for k, n in enumerate(names):
+            sel = {LABEL: "true", "pool": str(k // 2)}
+            if k % 2 == 0:
+                pol = T.new_policy(n, keepConfigOnRestart=keep, node_selector=sel,
+                                   validation={"enabled": True} if validation else None)
+            else:
+                pol = T.new_host_nic_policy(n, keepConfigOnRestart=keep, node_selector=sel)
+            fake._create(P, pol.to_dict(), None)
 
         def ds_all():
             return all(fake.get_object(kube.DAEMONSETS, n, "amd-network-operator") for n in names)
 
         def targets_all():
-            return all((fake.get_object(P, n).get("status") or {}).get("targets") == nodes for n in names)
+            return all((fake.get_object(P, n).get("status") or {}).get("targets") == want[n] for n in names)
 
         await _until(ds_all, timeout)
         t_ds = time.perf_counter() - t0
@@ -111,8 +125,9 @@ async def run(nodes: int, policies: int, timeout: float, keep: bool = False, val
         t_targets = time.perf_counter() - t0
         t1 = time.perf_counter()
         for i in range(nodes):
-            for n in names:
-                fake.node_ready[(f"amd-network-operator/{n}", f"gpu-node-{i:04d}")] = True
+            for k, n in enumerate(names):
+                if i % pools == k // 2:
+                    fake.node_ready[(f"amd-network-operator/{n}", f"gpu-node-{i:04d}")] = True
         fake._sync_daemonsets()
 
         def good_all():
@@ -122,31 +137,31 @@ async def run(nodes: int, policies: int, timeout: float, keep: bool = False, val
         t_good = time.perf_counter() - t1
         if validation:  # every ready node gets its validation Job; the simulated kubelets pass them
             t_v = time.perf_counter()
-            await _until(lambda: len(fake._table(kube.JOBS)) == nodes * policies, timeout, poll=0.05)
+            await _until(lambda: len(fake._table(kube.JOBS)) == sum(want[n] for n in amd), timeout, poll=0.05)
             jobs_s = time.perf_counter() - t_v
             for j in fake.list_objects(kube.JOBS):
                 fake.set_job_result(j["metadata"]["name"], "amd-network-operator", True)
 
             def validated_all():
-                for n in names:
+                for n in amd:
                     c = {x["type"]: x for x in (fake.get_object(P, n).get("status") or {}).get("conditions") or []}
                     if (c.get("FabricValidated") or {}).get("reason") != "AllNodesValidated":
                         return False
                 return True
             await _until(validated_all, timeout, poll=0.05)
         await asyncio.sleep(0.5)
-        out = {"nodes": nodes, "policies": policies, "pods": nodes * policies, "daemonsets_s": round(t_ds, 4),
+        out = {"nodes": nodes, "policies": policies, "pods": sum(want.values()), "daemonsets_s": round(t_ds, 4),
                "targets_s": round(t_targets, 4), "all_good_s": round(t_good, 4)}
         if validation:
             out.update(ready_to_validation_jobs_s=round(jobs_s, 4),
                        jobs_done_to_validated_s=round(time.perf_counter() - t_v - jobs_s, 4))
         if keep:
-            await _until(lambda: all(len((fake.get_object(P, n).get("status") or {}).get("keptNodes") or []) == nodes
+            await _until(lambda: all(len((fake.get_object(P, n).get("status") or {}).get("keptNodes") or []) == want[n]
                                      for n in names), timeout)
             t2 = time.perf_counter()
             for n in names:
                 fake._delete_or_mark(P, n, "")
-            await _until(lambda: len(fake._table(kube.JOBS)) == nodes * policies, timeout, poll=0.05)
+            await _until(lambda: len(fake._table(kube.JOBS)) == sum(want.values()), timeout, poll=0.05)
             out["delete_to_cleanup_jobs_s"] = round(time.perf_counter() - t2, 4)
             t3 = time.perf_counter()
             for j in fake.list_objects(kube.JOBS):

@@ -87,6 +87,20 @@ class PolicyController:
 
     async def _on_policy(self, ev: str, obj: dict, old: Optional[dict]) -> None:
         await self._enqueue(obj["metadata"]["name"])
+        # Which nodes a policy holds depends on the older policies of its type: one that comes,
+        # goes (or starts deleting) or changes its selector or type moves the others' hold-off.
+        def placement(o: Optional[dict]) -> tuple:
+            spec = (o or {}).get("spec") or {}
+            return (spec.get("configurationType", ""), spec.get("nodeSelector") or {},
+                    bool(((o or {}).get("metadata") or {}).get("deletionTimestamp")))
+        if ev != "MODIFIED" or placement(old) != placement(obj):
+            for ctype in {placement(obj)[0], placement(old)[0]} if old else {placement(obj)[0]}:
+                await self._enqueue_type(obj["metadata"]["name"], ctype)
+
+    async def _enqueue_type(self, name: str, ctype: str) -> None:
+        for p in self.policies.list():
+            if p["metadata"]["name"] != name and (p.get("spec") or {}).get("configurationType", "") == ctype:
+                await self._enqueue(p["metadata"]["name"])
 
     async def _on_daemonset(self, ev: str, obj: dict, old: Optional[dict]) -> None:
         ref = controller_of(obj)
@@ -109,9 +123,9 @@ class PolicyController:
                 await self._enqueue_others(None)
 
     async def _enqueue_others(self, name: Optional[str]) -> None:
-        """An agent Pod came or went: the other policies of its type may now share (or no longer
-        share) its node, and their status says so (reconciler.conflict_errors).  Without a known
-        owner, every policy."""
+        """An agent Pod came or went: the nodes the other policies of its type are held off may
+        have changed, and their status names them (reconciler._hold_off).  Without a known owner,
+        every policy."""
         me = self.policies.get(name) if name else None
         ctype = ((me or {}).get("spec") or {}).get("configurationType", "") if me else None
         for p in self.policies.list():

@@ -28,6 +28,9 @@ OPERATOR_CLUSTER_RULES: Tuple[Tuple[str, Tuple[str, ...], Tuple[str, ...]], ...]
     # Agent DaemonSets (owned) and their pods (per-node readiness errors in status.errors).
     ("apps", ("daemonsets",), READ + WRITE),
     ("", ("pods",), READ),
+    # Which nodes a newer policy of one type is held off (the ones an older policy selects too):
+    # a LIST by label selector, three names at most, and only while two policies overlap.
+    ("", ("nodes",), ("list",)),
     # Agent ServiceAccount + OpenShift SCC RoleBinding (created on OpenShift only).
     ("", ("serviceaccounts",), ("get", "list", "create", "update", "delete")),
     ("rbac.authorization.k8s.io", ("rolebindings",), ("get", "list", "create", "update", "delete")),

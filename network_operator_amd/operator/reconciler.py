@@ -346,9 +346,11 @@ def update_host_nic_daemonset(ds: dict, p: T.NetworkClusterPolicy, namespace: st
     c["args"] = host_nic_agent_args(p)
 
 
-def update_daemonset_for(ds: dict, p: T.NetworkClusterPolicy, namespace: str) -> None:
+def update_daemonset_for(ds: dict, p: T.NetworkClusterPolicy, namespace: str,
+                         hold_off: Optional[List[dict]] = None) -> None:
     """createDaemonSet / updateDaemonSet dispatch on configurationType (:243-265).  Also the
-    rolling-update width (spec.maxUnavailable; 1 when unset, like the reference's DaemonSet)."""
+    rolling-update width (spec.maxUnavailable; 1 when unset, like the reference's DaemonSet) and
+    the node affinity that holds the agents off nodes an older policy of the type selects."""
     ds["spec"].setdefault("updateStrategy", {"type": "RollingUpdate"}).setdefault("rollingUpdate", {})[
         "maxUnavailable"] = p.spec.maxUnavailable if p.spec.maxUnavailable is not None else 1
     if p.spec.configurationType == T.CONFIG_AMD_SCALE_OUT:
@@ -368,6 +370,7 @@ def update_daemonset_for(ds: dict, p: T.NetworkClusterPolicy, namespace: str) ->
         pod["priorityClassName"] = p.spec.priorityClassName
     else:
         pod.pop("priorityClassName", None)
+    set_hold_off(pod, hold_off)
 
 
 def status_for(targets: int, ready: int) -> str:
@@ -445,27 +448,80 @@ def _container_running(pod: dict) -> bool:
     return any("running" in (cs.get("state") or {}) for cs in (pod.get("status") or {}).get("containerStatuses") or [])
 
 
-# Two policies of one configurationType that select the same node run two agents there; they
-# share the node lock (named after the type's NFD label), so the later one waits and then fails.
-# The operator says so at once on the newer policy (status.errors, Degraded/PolicyConflict, a
-# Warning Event), naming the older one; the older policy's own status stays as its agents are.
+# Two policies of one configurationType that select the same node would run two agents there;
+# they share the node lock (named after the type's NFD label), so the later one would wait and
+# then fail, restarting forever.  Instead a node belongs to the OLDEST live policy of the type
+# whose nodeSelector matches it: every newer one's DaemonSet carries a required node-affinity
+# term that excludes the nodes the older selectors match, so its agents are never placed there.
+# The term is built from the selectors, not from a node list: it does not change when nodes come,
+# go or get relabelled (a DaemonSet template change rolls every agent of the policy), only when
+# an older policy's selector does.  The newer policy's status names the held-off nodes
+# (Degraded/PolicyConflict, a Warning Event); once the older policy goes, the term goes with it
+# and the newer policy's agents take those nodes.  (The reference has no guard at all,
+# internal/controller/networkconfiguration_controller.go:164-204,313-362.)
 CONFLICT_MARK = ": also selected by policy "
+# A node-selector term no node matches (no node carries this label): a newer policy whose
+# every node an older one selects.
+HELD_EVERYWHERE_KEY = "network.amd.com/held-off-by-an-older-policy"
+MAX_HOLD_OFF_TERMS = 64  # required terms are ORed: the hold-off expands to at most this many
 
 
-def conflict_errors(ctype: str, mine: List[str], others: Dict[str, List[str]], limit: int = 3) -> List[str]:
-    """status.errors entries for the nodes ``mine`` shares with each policy in ``others`` (name ->
-    nodes of its agent Pods; same configurationType), one entry per other policy."""
+def hold_off_terms(mine: Dict[str, str], older: List[Dict[str, str]]) -> Optional[List[dict]]:
+    """nodeSelectorTerms (ORed) of the nodes ``mine`` (a nodeSelector) selects that no selector in
+    ``older`` matches, to AND with ``mine``; None when nothing is held off.
+
+    Not matching {k1: v1, k2: v2} is (k1 NotIn [v1]) OR (k2 NotIn [v2]) (NotIn also matches a node
+    without the label).  Over several older selectors that is a conjunction of such clauses,
+    expanded here into a disjunction of terms.  A clause whose pairs all sit in ``mine`` already
+    excludes every node: nothing is left.  An older selector with a key ``mine`` requires at
+    another value is disjoint: no clause.  Raises ValueError past MAX_HOLD_OFF_TERMS."""
+    clauses = set()
+    for q in older:
+        if any(k in mine and mine[k] != v for k, v in q.items()):
+            continue  # disjoint selections
+        clause = tuple(sorted((k, v) for k, v in q.items() if mine.get(k) != v))
+        if not clause:
+            return [{"matchExpressions": [{"key": HELD_EVERYWHERE_KEY, "operator": "Exists"}]}]
+        clauses.add(clause)
+    if not clauses:
+        return None
+    kept: List[tuple] = []  # absorption: a clause implied by a shorter one adds nothing
+    for c in sorted(clauses, key=lambda c: (len(c), c)):
+        if not any(set(k) <= set(c) for k in kept):
+            kept.append(c)
+    terms: List[frozenset] = [frozenset()]
+    for c in kept:
+        terms = sorted({t | {lit} for t in terms for lit in c}, key=sorted)
+        if len(terms) > MAX_HOLD_OFF_TERMS:
+            raise ValueError(f"{len(kept)} overlapping older selectors expand to more than {MAX_HOLD_OFF_TERMS} "
+                             "node-affinity terms")
+    terms = [t for t in terms if not any(o < t for o in terms)]  # a term implied by a smaller one
     out = []
-    own = set(mine)
-    for other in sorted(others):
-        shared = sorted(own.intersection(others[other]))
-        if not shared:
-            continue
-        nodes = ", ".join(shared[:limit]) + (f" and {len(shared) - limit} more" if len(shared) > limit else "")
-        out.append(f"{nodes}{CONFLICT_MARK}{other} ({ctype} too, created earlier): one agent per node and type "
-                   f"configures the NICs, so this policy's agent there waits for the node lock and fails; "
-                   f"narrow a nodeSelector")
+    for t in terms:
+        by_key: Dict[str, List[str]] = {}
+        for k, v in sorted(t):
+            by_key.setdefault(k, []).append(v)
+        out.append({"matchExpressions": [{"key": k, "operator": "NotIn", "values": vs} for k, vs in by_key.items()]})
     return out
+
+
+def set_hold_off(pod: dict, terms: Optional[List[dict]]) -> None:
+    """The agent Pod template's required node affinity: the hold-off terms, or none.  (The policy
+    has no affinity field of its own, so the operator owns this one.)"""
+    if terms:
+        pod["affinity"] = {"nodeAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": {
+            "nodeSelectorTerms": copy.deepcopy(terms)}}}
+    else:
+        pod.pop("affinity", None)
+
+
+def held_off_error(ctype: str, nodes: List[str], more: bool, other: str) -> str:
+    """status.errors entry for the nodes this policy is kept off because ``other`` (older, same
+    configurationType) selects them too."""
+    shown = ", ".join(nodes) + (" and more" if more else "")
+    return (f"{shown}{CONFLICT_MARK}{other} ({ctype} too, created earlier): one agent per node and type "
+            f"configures the NICs, so this policy's agents are held off these nodes while {other} selects them; "
+            f"narrow a nodeSelector")
 
 
 def policy_conditions(current: List[dict], targets: int, ready: int, errors: List[str], generation: int,
@@ -587,6 +643,7 @@ def cleanup_job(p: T.NetworkClusterPolicy, node: str, namespace: str) -> dict:
     pod["restartPolicy"] = "Never"
     pod["nodeName"] = node
     pod.pop("nodeSelector", None)  # the node may have left the policy's selector
+    pod.pop("affinity", None)      # ... or be held off now
     c = pod["containers"][0]
     for k in ("readinessProbe", "livenessProbe", "startupProbe"):
         c.pop(k, None)
@@ -774,20 +831,15 @@ class NetworkClusterPolicyReconciler:
             errs = errs[:limit] + [f"... and {len(errs) - limit} more"]
         return errs, degraded, starting
 
-    def _conflicts(self, p: T.NetworkClusterPolicy, ds_name: str) -> List[str]:
-        """Nodes this policy's agents share with an older live policy of the same type (from the
-        agent Pods both DaemonSets placed: what the scheduler did, selector, taints and all).
-        Older: earlier creationTimestamp, the name breaking a tie (the timestamps have seconds)."""
-        if self._list_policies is None or self._list_pods is None:
-            return []
+    async def _hold_off(self, p: T.NetworkClusterPolicy) -> Tuple[Optional[List[dict]], List[str]]:
+        """(node-affinity terms that keep this policy's agents off the nodes older live policies of
+        its type select, status.errors naming those nodes).  Older: earlier creationTimestamp, the
+        name breaking a tie (the timestamps have seconds).  The nodes are read with one LIST per
+        overlapping older policy, by the two selectors together, three names at most."""
+        if self._list_policies is None:
+            return None, []
         me = (p.metadata.get("creationTimestamp") or "", p.name)
-
-        def nodes(ds: str) -> List[str]:
-            return [n for n in ((pod.get("spec") or {}).get("nodeName") for pod in self._list_pods(ds)) if n]
-        mine = nodes(ds_name)
-        if not mine:
-            return []
-        others = {}
+        older: Dict[str, Dict[str, str]] = {}
         for q in self._list_policies():
             md = q.get("metadata") or {}
             if md.get("name") == p.name or md.get("deletionTimestamp") or \
@@ -795,8 +847,31 @@ class NetworkClusterPolicyReconciler:
                 continue
             if (q.get("spec") or {}).get("configurationType", "") != p.spec.configurationType:
                 continue
-            others[md["name"]] = nodes(md["name"])
-        return conflict_errors(p.spec.configurationType, mine, others)
+            older[md["name"]] = dict((q.get("spec") or {}).get("nodeSelector") or {})
+        mine = dict(p.spec.nodeSelector)
+        errors: List[str] = []
+        try:
+            terms = hold_off_terms(mine, list(older.values()))
+        except ValueError as e:
+            terms = None
+            errors.append(f"shared nodes{CONFLICT_MARK}{', '.join(sorted(older))} ({p.spec.configurationType} too, "
+                          f"created earlier) are not held off: {e}; this policy's agents there wait for the node lock "
+                          f"and fail; narrow a nodeSelector")
+        for other in sorted(older):
+            sel = older[other]
+            if any(k in mine and mine[k] != v for k, v in sel.items()):
+                continue
+            both = ",".join(f"{k}={v}" for k, v in sorted({**sel, **mine}.items()))
+            try:
+                lst = await self.client.list(kube.NODES, label_selector=both or None, limit=3)
+            except ApiError as e:
+                log.warning("unable to list the nodes %s shares with %s: %s", p.name, other, e)
+                continue
+            names = sorted(n["metadata"]["name"] for n in lst.get("items") or [])
+            if names:
+                errors.append(held_off_error(p.spec.configurationType, names,
+                                             bool((lst.get("metadata") or {}).get("continue")), other))
+        return terms, errors
 
     async def _delete_job(self, j: dict) -> None:
         try:
@@ -1129,7 +1204,7 @@ class NetworkClusterPolicyReconciler:
             if not is_already_exists(e):
                 log.error("unable to create role binding: %s", e)
 
-    async def _create_daemonset(self, raw: dict, p: T.NetworkClusterPolicy) -> Result:
+    async def _create_daemonset(self, raw: dict, p: T.NetworkClusterPolicy, hold: tuple = (None, [])) -> Result:
         if p.spec.configurationType not in T.CONFIGURATION_TYPES:
             log.info("Unknown configuration type, this shouldn't happen! type=%s", p.spec.configurationType)
             raise ValueError(f"unknown configuration type {p.spec.configurationType!r}")
@@ -1137,7 +1212,7 @@ class NetworkClusterPolicyReconciler:
         sa_name = p.name + "-sa" if self.is_openshift else ""
         if sa_name:
             ds["spec"]["template"]["spec"]["serviceAccountName"] = sa_name
-        update_daemonset_for(ds, p, self.namespace)
+        update_daemonset_for(ds, p, self.namespace, hold[0])
         set_controller_reference(raw, ds)
         log.info("Creating %s DaemonSet name=%s", p.spec.configurationType, p.name)
         try:
@@ -1147,24 +1222,25 @@ class NetworkClusterPolicyReconciler:
                 raise
             # Our cache has not seen it yet: continue on the update path with the live object.
             created = await self.client.get(kube.DAEMONSETS, p.name, self.namespace)
-            return await self._update(raw, p, created)
+            return await self._update(raw, p, created, hold)
         await self._event(raw, "Normal", "DaemonSetCreated", f"Created DaemonSet {self.namespace}/{p.name}")
         if sa_name:
             await self._create_openshift_collateral(raw, sa_name)
-        return await self._update_status(raw, p, created)
+        return await self._update_status(raw, p, created, hold[1])
 
     # -- update ----------------------------------------------------------------------------------
-    async def _update(self, raw: dict, p: T.NetworkClusterPolicy, ds: dict) -> Result:
+    async def _update(self, raw: dict, p: T.NetworkClusterPolicy, ds: dict, hold: tuple = (None, [])) -> Result:
         original = copy.deepcopy(ds)
-        update_daemonset_for(ds, p, self.namespace)
+        update_daemonset_for(ds, p, self.namespace, hold[0])
         if original["spec"]["template"]["spec"] != ds["spec"]["template"]["spec"] or \
                 original["spec"].get("updateStrategy") != ds["spec"].get("updateStrategy"):
             log.info("DS difference for %s", p.name)
             ds = await self.client.replace(kube.DAEMONSETS, ds)
             await self._event(raw, "Normal", "DaemonSetUpdated", f"Updated DaemonSet {self.namespace}/{p.name}")
-        return await self._update_status(raw, p, ds)
+        return await self._update_status(raw, p, ds, hold[1])
 
-    async def _update_status(self, raw: dict, p: T.NetworkClusterPolicy, ds: dict) -> Result:
+    async def _update_status(self, raw: dict, p: T.NetworkClusterPolicy, ds: dict,
+                             held_off: Optional[List[str]] = None) -> Result:
         st = ds.get("status", {}) or {}
         targets = int(st.get("desiredNumberScheduled", 0) or 0)
         ready = int(st.get("numberReady", 0) or 0)
@@ -1174,7 +1250,7 @@ class NetworkClusterPolicyReconciler:
             updated = True
         new_state = status_for(targets, ready)
         errors = [f"dependency missing: {d}" for d in self.missing_dependencies]
-        errors += self._conflicts(p, ds["metadata"]["name"])
+        errors += held_off or []
         node_errs, degraded, starting = self._node_errors(ds["metadata"]["name"]) if targets and ready < targets \
             else ([], set(), set())
         errors += node_errs
@@ -1249,6 +1325,7 @@ class NetworkClusterPolicyReconciler:
                     return Result()
                 raise
         owned = self._list_owned(name)
+        hold = await self._hold_off(p)
         if not owned:
-            return await self._create_daemonset(raw, p)
-        return await self._update(raw, p, copy.deepcopy(owned[0]))
+            return await self._create_daemonset(raw, p, hold)
+        return await self._update(raw, p, copy.deepcopy(owned[0]), hold)

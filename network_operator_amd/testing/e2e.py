@@ -321,8 +321,7 @@ async def _scenario(tmp: Path, n_nics: int, mode: str, seed: int, interval: str,
                    sysfs_root=tmp / "sys", init_images={KMD_IMAGE: kmd},
                    env={"PYTHONPATH": str(Path(__file__).resolve().parents[2])},
                    job_images={T0.DEFAULT_VALIDATION_IMAGE: [sys.executable, "-c", _VALIDATE_STUB, validation or "pass"]},
-                   agent_arg_overrides={**({"--wait": lldp_wait} if lldp_wait else {}),
-                                        **({"--node-lock-wait": "1s"} if duplicate_policy else {})} or None)
+                   agent_arg_overrides={**({"--wait": lldp_wait} if lldp_wait else {})} or None)
     if validation and not host_nic:
         policy_kw = dict(policy_kw, validation={"enabled": True, "minBusbw": 300})
     P, DS = kube.NETWORKCLUSTERPOLICIES, kube.DAEMONSETS
@@ -457,24 +456,56 @@ async def _scenario(tmp: Path, n_nics: int, mode: str, seed: int, interval: str,
                                                                    "amd_network_operator_policy_ready"))
             if duplicate_policy:
                 # A second amd-so policy selecting the same node: its agent would flush and
-                # re-address the same NICs.  The node lock keeps it out: it fails, the reason
-                # reaches that policy's status, and the first policy's node stays configured.
+                # re-address the same NICs.  The operator holds it off the node (node affinity):
+                # no agent of it runs there, so nothing waits on the node lock or restarts.  Once
+                # the older policy goes, the newer one takes the node.
+                dup = "scale-out-dup"
                 addrs_before = {nif: rt.addr_list(rt.link_by_name(nif)["index"]) for nif in nic_names}
-                await c.create(P, T.new_policy("scale-out-dup", layer=mode, mtu=9000, **policy_kw).to_dict())
+                dup_pods_seen = []
+
+                async def watch_dup():
+                    while True:
+                        dup_pods_seen.extend(x.pod[1] for x in node.containers.values()
+                                             if x.daemonset == f"{ns}/{dup}" and x.pod[1] not in dup_pods_seen)
+                        await asyncio.sleep(0.002)
+                watcher = asyncio.ensure_future(watch_dup())
+                await c.create(P, T.new_policy(dup, layer=mode, mtu=9000, **policy_kw).to_dict())
 
                 def dup_error():
-                    # the operator's conflict entry (at once) and the agent's own (once it gave up)
-                    st = (fake.get_object(P, "scale-out-dup") or {}).get("status") or {}
-                    return [e for e in st.get("errors") or [] if "node lock" in e]
-                await _until(lambda: any("holds the node lock" in e for e in dup_error()), 20)
+                    st = (fake.get_object(P, dup) or {}).get("status") or {}
+                    return [e for e in st.get("errors") or [] if "held off" in e]
+                await _until(lambda: bool(dup_error()), 20)
+                await asyncio.sleep(2.0)  # long enough for a placed agent to show up
                 res["duplicate_policy_errors"] = dup_error()
-                res["duplicate_policy_status"] = (fake.get_object(P, "scale-out-dup") or {}).get("status")
+                res["duplicate_policy_status"] = (fake.get_object(P, dup) or {}).get("status")
+                res["duplicate_daemonset_affinity"] = (fake.get_object(DS, dup, ns) or {}).get(
+                    "spec", {}).get("template", {}).get("spec", {}).get("affinity")
+                res["duplicate_agents_while_held"] = list(dup_pods_seen)
                 res["first_policy_status_after_duplicate"] = (fake.get_object(P, name) or {}).get("status")
                 res["addrs_unchanged_by_duplicate"] = addrs_before == {
                     nif: rt.addr_list(rt.link_by_name(nif)["index"]) for nif in nic_names}
                 res["label_after_duplicate"] = node.node_labels().get(label_key)
-                await c.delete(P, "scale-out-dup")
-                await _until(lambda: not any(x.daemonset == f"{ns}/scale-out-dup" for x in node.containers.values()), 10)
+                gen0 = fake.get_object(DS, dup, ns)["metadata"]["generation"]
+                t1 = time.monotonic()
+                await c.delete(P, name)
+                t_release = await _until(lambda: not (fake.get_object(DS, dup, ns) or {}).get("spec", {}).get(
+                    "template", {}).get("spec", {}).get("affinity"), 10)
+
+                def dup_good():
+                    st = (fake.get_object(P, dup) or {}).get("status") or {}
+                    return st.get("state") == "All good" and st.get("errors") == [] and \
+                        node.node_labels().get(label_key) == "true"
+                t_dup_ready = await _until(dup_good, 60)
+                watcher.cancel()
+                dup_c = [x for x in node.containers.values() if x.daemonset == f"{ns}/{dup}"]
+                res["takeover"] = {
+                    "delete_to_hold_released_s": round(t_release - t1, 6) if t_release else None,
+                    "daemonset_updates": fake.get_object(DS, dup, ns)["metadata"]["generation"] - gen0,
+                    "delete_to_newer_ready_s": round(t_dup_ready - t1, 6) if t_dup_ready else None,
+                    "newer_agent_restarts": sum(x.restarts for x in dup_c), "newer_agents": len(dup_c),
+                    "newer_status": (fake.get_object(P, dup) or {}).get("status")}
+                res["agent_exit_codes"] = [e["rc"] for e in node.exited]
+                return res
             if ha:
                 res.update(await _ha_checks(fake, c, rt, node, replicas, ns, name, mode, nic_names, label_key,
                                             all_good, update_mtu or 4200))

@@ -180,6 +180,40 @@ class _Fault:
 FOREGROUND_DELETION = "foregroundDeletion"
 
 
+def _node_affinity_ok(node: dict, pod_spec: dict) -> bool:
+    """The template's requiredDuringSchedulingIgnoredDuringExecution node affinity, as the
+    DaemonSet controller evaluates it: terms ORed, expressions within a term ANDed (In, NotIn,
+    Exists, DoesNotExist, Gt, Lt on labels; matchFields on metadata.name); a term with no
+    expression matches nothing."""
+    terms = ((((pod_spec.get("affinity") or {}).get("nodeAffinity") or {})
+              .get("requiredDuringSchedulingIgnoredDuringExecution") or {}).get("nodeSelectorTerms"))
+    if not terms:
+        return True
+    labels = node["metadata"].get("labels") or {}
+
+    def ok(e: dict, value) -> bool:
+        op, vals = e.get("operator"), e.get("values") or []
+        if op == "In":
+            return value is not None and value in vals
+        if op == "NotIn":
+            return value is None or value not in vals
+        if op == "Exists":
+            return value is not None
+        if op == "DoesNotExist":
+            return value is None
+        if op in ("Gt", "Lt") and value is not None and vals:
+            try:
+                return int(value) > int(vals[0]) if op == "Gt" else int(value) < int(vals[0])
+            except ValueError:
+                return False
+        return False
+    name = node["metadata"]["name"]
+    return any((t.get("matchExpressions") or t.get("matchFields"))
+               and all(ok(e, labels.get(e.get("key"))) for e in t.get("matchExpressions") or [])
+               and all(ok(e, name if e.get("key") == "metadata.name" else None) for e in t.get("matchFields") or [])
+               for t in terms)
+
+
 class FakeApiServer:
     STATUS_SUBRESOURCE = {kube.NETWORKCLUSTERPOLICIES, kube.DAEMONSETS}
 
@@ -593,7 +627,8 @@ class FakeApiServer:
             matching = [n["metadata"]["name"] for n in nodes
                         if all((n["metadata"].get("labels") or {}).get(k) == v for k, v in sel.items())
                         and all(self._tolerated(t, tols) for t in (n.get("spec") or {}).get("taints") or []
-                                if t.get("effect") in ("NoSchedule", "NoExecute"))]
+                                if t.get("effect") in ("NoSchedule", "NoExecute"))
+                        and _node_affinity_ok(n, pod_spec)]
             ready = sum(1 for n in matching if self.node_ready.get((f"{ns}/{name}", n)))
             st = {"currentNumberScheduled": len(matching), "desiredNumberScheduled": len(matching),
                   "numberMisscheduled": 0, "numberReady": ready,

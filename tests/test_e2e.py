@@ -241,16 +241,30 @@ def test_two_operator_replicas_with_webhooks_fail_over():
 
 def test_second_policy_of_one_type_on_a_node_is_kept_off_the_nics():
     """Two amd-so policies select one node.  The reference would run two agents flushing and
-    re-addressing the same NICs.  Here the second agent cannot take the node lock: it fails with
-    the cause, that policy's status says so, and the first policy's addresses and label stay."""
+    re-addressing the same NICs.  Here the newer policy is held off the node:
+    its DaemonSet excludes the nodes the older selector matches, so none of its agents runs
+    there -- no wait on the node lock, no restarts -- its status names the node and the older
+    policy, and the older policy's addresses and label stay.  Deleting the older policy releases
+    the node: one DaemonSet update, and the newer policy's agent configures it."""
     r = e2e.run_isolated(n_nics=2, mode="L3", seed=24, duplicate_policy=True)
-    assert r["duplicate_policy_errors"], (r.get("duplicate_policy_status"), r["agent_log"])
     errs = r["duplicate_policy_errors"]
-    assert any("holds the node lock" in e for e in errs), errs  # the agent's own words, once it gave up
-    assert any("also selected by policy" in e and "created earlier" in e for e in errs), errs  # the operator's
+    assert len(errs) == 1 and errs[0].startswith("mi355x-0: also selected by policy scale-out (amd-so too, created "
+                                                 "earlier)"), (errs, r["agent_log"])
+    assert r["duplicate_agents_while_held"] == []
+    terms = r["duplicate_daemonset_affinity"]["nodeAffinity"]["requiredDuringSchedulingIgnoredDuringExecution"]
+    assert terms["nodeSelectorTerms"] == [{"matchExpressions": [
+        {"key": "network.amd.com/held-off-by-an-older-policy", "operator": "Exists"}]}]  # same selector: all nodes
+    dst = r["duplicate_policy_status"]
+    assert dst["targets"] == 0 and {c["type"]: c for c in dst["conditions"]}["Degraded"]["reason"] == "PolicyConflict"
     assert r["addrs_unchanged_by_duplicate"] and r["label_after_duplicate"] == "true"
     st = r["first_policy_status_after_duplicate"]
     assert (st["state"], st["errors"]) == ("All good", [])
+    t = r["takeover"]
+    assert t["delete_to_hold_released_s"] is not None and t["delete_to_hold_released_s"] < 2.0, t
+    assert t["daemonset_updates"] == 1, t
+    assert t["delete_to_newer_ready_s"] is not None, (t, r["agent_log"])
+    assert t["newer_agents"] == 1 and t["newer_agent_restarts"] == 0, t
+    assert t["newer_status"]["targets"] == 1 and t["newer_status"]["ready"] == 1
 
 
 def test_l2_link_training_for_5s_is_start_up_not_degradation():

@@ -271,9 +271,11 @@ def test_operator_requests_stay_within_generated_rbac(tmp_path, monkeypatch):
         # Test-side writes go straight into the store, so only the operator's requests are audited.
         P = kube.NETWORKCLUSTERPOLICIES
         fake._create(P, T.new_policy("l3").to_dict(), None)
-        fake._create(P, T.new_policy("l2", layer="L2", disableNetworkManager=True).to_dict(), None)
+        # (a second amd-so policy on n1: created in the same second, the name makes it the newer
+        # one, held off n1 -- which LISTs the shared nodes)
+        fake._create(P, T.new_policy("zl2", layer="L2", disableNetworkManager=True).to_dict(), None)
         fake._create(P, T.new_host_nic_policy("hn", driverImage="r/kmd:1").to_dict(), None)
-        for n in ("l3", "l2", "hn"):
+        for n in ("l3", "zl2", "hn"):
             await _until(lambda n=n: fake.get_object(kube.DAEMONSETS, n, "netop-test") is not None)
         fake.set_agent_ready("n1")
         await _until(lambda: fake.get_object(P, "l3")["status"]["state"] == "All good")
@@ -309,7 +311,8 @@ def test_operator_requests_stay_within_generated_rbac(tmp_path, monkeypatch):
 
 
 def test_control_plane_scale_bench_converges():
-    """bench/control_plane.py at a CI-sized scale: 300 nodes x 3 policies converge to "All good"
+    """bench/control_plane.py at a CI-sized scale: 300 nodes, 4 policies (one agent of each type
+    per node: 600 agent Pods) converge to "All good"
     within seconds, and the separate manager process stays inside its Deployment limit."""
     import importlib.util
     from pathlib import Path
@@ -318,8 +321,8 @@ def test_control_plane_scale_bench_converges():
     spec = importlib.util.spec_from_file_location("control_plane_bench", path)
     mod = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(mod)
-    r = asyncio.run(mod.run(300, 3, timeout=60))
-    assert r["pods"] == 900 and r["all_good_s"] < 10 and r["targets_s"] < 10, r
+    r = asyncio.run(mod.run(300, 4, timeout=60))
+    assert r["pods"] == 600 and r["all_good_s"] < 10 and r["targets_s"] < 10, r
     assert r["manager_rss_mib"] < r["manager_limit_mib"], r
 
 

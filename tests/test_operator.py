@@ -810,7 +810,9 @@ def test_keep_config_policy_cleans_nodes_through_jobs_on_deletion_and_departure(
             for i in range(3):
                 fake.add_node(f"gpu-node-{i}", {"foo": "bar"})
             await client.create(kube.NETWORKCLUSTERPOLICIES, policy(keepConfigOnRestart=True))
-            await client.create(kube.NETWORKCLUSTERPOLICIES, policy("plain"))
+            plain = policy("plain")  # on other nodes: two amd-so policies never share one
+            plain["spec"]["nodeSelector"] = {"foo": "elsewhere"}
+            await client.create(kube.NETWORKCLUSTERPOLICIES, plain)
             await eventually(lambda: fake.get_object(kube.DAEMONSETS, "policy", NS) is not None)
             args = fake.get_object(kube.DAEMONSETS, "policy", NS)["spec"]["template"]["spec"]["containers"][0]["args"]
             assert "--keep-config" in args and "--lldp-cache=/host/etc/amd/scale-out/lldp-cache" in args
@@ -1424,15 +1426,41 @@ def test_rail_switch_pattern_random_corpus_never_admits_what_the_agent_rejects(n
     assert admitted > 2000  # the sweep exercised the accepting side too (1M patterns: 0 disagreements)
 
 
-def test_conflict_errors_name_the_other_policy_and_the_shared_nodes():
-    from network_operator_amd.operator.reconciler import CONFLICT_MARK, conflict_errors
+def test_hold_off_terms_select_exactly_the_nodes_no_older_selector_matches():
+    """hold_off_terms against brute force: over random selectors and random node labels, a node
+    passes (the newer selector AND the terms, as the DaemonSet controller evaluates them) exactly
+    when the newer selector matches it and no older selector does."""
+    import random
 
-    assert conflict_errors("amd-so", ["n1"], {}) == []
-    assert conflict_errors("amd-so", ["n1", "n2"], {"b": ["n3"]}) == []
-    errs = conflict_errors("amd-so", ["n1", "n2", "n3", "n4", "n5"], {"c": ["n5"], "b": ["n5", "n4", "n3", "n2"]})
-    assert [e.split(CONFLICT_MARK)[1].split(" ")[0] for e in errs] == ["b", "c"]
-    assert errs[0].startswith("n2, n3, n4 and 1 more" + CONFLICT_MARK + "b (amd-so too, created earlier)")
-    assert errs[1].startswith("n5" + CONFLICT_MARK + "c (amd-so too, created earlier)")
+    from network_operator_amd.operator.reconciler import HELD_EVERYWHERE_KEY, hold_off_terms
+    from network_operator_amd.testing.fakeapi import _node_affinity_ok
+
+    assert hold_off_terms({"a": "1"}, []) is None
+    assert hold_off_terms({"a": "1"}, [{"a": "2"}]) is None  # disjoint
+    assert hold_off_terms({"a": "1"}, [{"a": "1"}]) == [
+        {"matchExpressions": [{"key": HELD_EVERYWHERE_KEY, "operator": "Exists"}]}]
+    assert hold_off_terms({"a": "1"}, [{"a": "1", "b": "x"}, {"c": "y"}]) == [
+        {"matchExpressions": [{"key": "b", "operator": "NotIn", "values": ["x"]},
+                              {"key": "c", "operator": "NotIn", "values": ["y"]}]}]
+    rng = random.Random(7)
+    keys, vals = ["a", "b", "c", "d"], ["0", "1"]
+
+    def sel():
+        return {k: rng.choice(vals) for k in rng.sample(keys, rng.randint(1, 3))}
+    checked = 0
+    for _ in range(400):
+        mine, older = sel(), [sel() for _ in range(rng.randint(0, 4))]
+        terms = hold_off_terms(mine, older)
+        spec = {"affinity": {"nodeAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": {
+            "nodeSelectorTerms": terms}}}} if terms else {}
+        for _ in range(30):
+            labels = {k: rng.choice(vals) for k in keys if rng.random() < 0.8}
+            node = {"metadata": {"name": "n", "labels": labels}}
+            matches = lambda s: all(labels.get(k) == v for k, v in s.items())  # noqa: E731
+            want = matches(mine) and not any(matches(q) for q in older)
+            assert (matches(mine) and _node_affinity_ok(node, spec)) == want, (mine, older, labels, terms)
+            checked += 1
+    assert checked == 12000
 
 
 def test_two_policies_of_one_type_on_the_same_nodes_are_reported_on_both():
@@ -1580,12 +1608,22 @@ def test_random_edits_converge_to_the_policies_the_cluster_asks_for(seed, gc_del
                     assert f"--mode={layer}" in pod["containers"][0]["args"]
                     assert ds["metadata"]["ownerReferences"][0]["name"] == name
                     s = fake.get_object(kube.NETWORKCLUSTERPOLICIES, name)["status"]
-                    mine = placed(m)
-                    assert s["targets"] == len(mine) and s["ready"] == len(mine), (name, s, mine)
+
                     def age(n):
                         return (fake.get_object(kube.NETWORKCLUSTERPOLICIES, n)["metadata"]["creationTimestamp"], n)
-                    others = sorted(o for o, om in model.items()
-                                    if o != name and om[0] == ctype and age(o) < age(name) and set(placed(om)) & set(mine))
+
+                    def selects(sel_, n):
+                        return all(nodes[n][0].get(k) == v for k, v in sel_.items())
+                    older = [o for o, om in model.items() if o != name and om[0] == ctype and age(o) < age(name)]
+                    # a node belongs to the oldest policy of the type whose selector matches it
+                    held = {n for n in nodes for o in older if selects(model[o][2], n)}
+                    mine = sorted(set(placed(m)) - held)
+                    assert s["targets"] == len(mine) and s["ready"] == len(mine), (name, s, mine, held)
+                    # invariant: no agent Pod of a newer policy on a node an older one of its type holds
+                    pods = [q["spec"]["nodeName"] for q in fake.list_objects(kube.PODS)
+                            if (q["metadata"].get("ownerReferences") or [{}])[0].get("uid") == ds["metadata"]["uid"]]
+                    assert sorted(pods) == mine, (name, pods, mine, held)
+                    others = sorted(o for o in older if any(selects(model[o][2], n) and selects(sel, n) for n in nodes))
                     got = sorted(e.split(" also selected by policy ")[1].split(" ")[0] for e in s["errors"])
                     assert got == others and len(s["errors"]) == len(others), (name, s["errors"], others)
                 return True
