@@ -22,12 +22,17 @@ rccl-tests 8-GPU all-reduce".
   *step* is one in-place bf16 all-reduce of ``--bytes`` per rank (default 1 GiB, rccl-tests'
   large-message regime); ``--warmup`` untimed steps, then exactly ``--steps`` timed steps
   bracketed by barrier + ``torch.cuda.synchronize()``, max over ranks.
-* ``value`` is busbw = algbw * 2(n-1)/n (rccl-tests definition, per rank) with the artifacts
-  applied; ``busbw_rccl_defaults_GBps`` is the same loop in fresh rank processes without them.
+* ``value`` is the job aggregate the driver's contract asks for: rccl-tests busbw (algbw *
+  2(n-1)/n, a per-GPU figure) times n, with the artifacts applied.  The per-GPU figures, the
+  ones rccl-tests prints and BASELINE's metric names, are ``busbw_GBps`` (artifacts) and
+  ``busbw_rccl_defaults_GBps`` (the same loop in fresh rank processes without them); the A/B on
+  the aggregate basis is ``value`` vs ``aggregate_busbw_rccl_defaults_GBps``.  The ceiling
+  ``busbw_ceiling_GBps`` is per GPU too: (n-1) xGMI links x their rate.
   ``agent_artifacts`` says what was applied (file bytes, per-rank record) and what RCCL made of
   it (its dump: xGMI links seen per GPU — n-1 expected — and GPU / NIC ancestry vs the file's).
-  At n > 1 the run exits non-zero (after printing its line) when RCCL sees fewer xGMI links
-  under the file than n-1 (or than without it).
+  At n > 1 the run exits non-zero (after printing its line) only when the file is to blame:
+  RCCL sees fewer xGMI links under it than without it (``xgmi_links_check.file_blamed``), or
+  the artifacts were not applied.  A dump that cannot settle it is reported, not failed.
 * Order and deadline: verification and the timed loop come first; every diagnostic after it
   (RCCL defaults, xGMI probe, native harness, direct / IPC all-reduce, netns node-ready) is a
   child process killed at ``--deadline-s`` (``parallel/bench_extras.py``), and a watchdog in
@@ -60,6 +65,40 @@ STORE_FILE_ENV = "NETOP_BENCH_STORE"  # FileStore path of a rendezvous without a
 # run with the artifacts / of the RCCL-defaults run.
 FAKE_DUMP_ENV = "NETOP_BENCH_FAKE_RCCL_DUMP"
 FAKE_DUMP_DEFAULTS_ENV = "NETOP_BENCH_FAKE_RCCL_DUMP_DEFAULTS"
+# CPU rehearsal of the N-GPU line (tests): plan the GPU extras as on a node with this many GPUs
+# (their stand-ins come from bench_extras.FAKE_EXTRA_ENV), give rank r the GPU BDF FAKE_BDFS[r],
+# and read amd-smi's counters around the timed loop from a JSON file {"before": .., "after": ..}.
+FAKE_GPUS_ENV = "NETOP_BENCH_FAKE_GPUS"
+FAKE_SMI_ENV = "NETOP_BENCH_FAKE_SMI"
+FAKE_BDFS = [f"0000:{0x0a + 0x19 * k:02x}:00.0" for k in range(8)]
+
+
+def plan_extras(args, world: int, gpu: bool, device_count: int) -> list:
+    """Rank 0's diagnostics after the headline, in the order they run (each bounded by the
+    deadline, so the later ones are the first to go when time runs short).  The direct xGMI
+    all-reduces (single process and IPC) run only where the job holds every GPU of the node --
+    the last of the driver's N = 1, 2, 4, 8 runs -- unless forced with --xgmi-allreduce 1."""
+    plan = []
+    if args.rccl_defaults and args.artifacts != "off":
+        plan.append("rccl_defaults")
+    if gpu and args.native_rccl:
+        plan.append("native_rccl")
+    if gpu and world > 1 and args.xgmi_probe:
+        plan.append("xgmi_probe")
+    direct = args.xgmi_allreduce == "1" or (args.xgmi_allreduce == "auto" and world == device_count)
+    if gpu and world > 1 and direct:
+        plan += ["xgmi_allreduce", "xgmi_comm"]
+    if args.node_ready != "off":
+        plan.append("node_ready")
+    return plan
+
+
+def _fake_smi() -> Optional[dict]:
+    path = os.environ.get(FAKE_SMI_ENV)
+    if not path:
+        return None
+    with open(path) as f:
+        return json.load(f)
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
@@ -395,7 +434,11 @@ def _line(args, world: int, st: dict) -> dict:
                       else "")},
         "agent_artifacts": st.get("artifacts"),
         "busbw_GBps": busbw,
+        "busbw_basis": "per GPU (rccl-tests); value and aggregate_* are x n_gpus",
         "busbw_rccl_defaults_GBps": (st.get("rccl_defaults") or {}).get("busbw_GBps"),
+        "aggregate_busbw_rccl_defaults_GBps": (
+            round(st["rccl_defaults"]["busbw_GBps"] * world, 3)
+            if (st.get("rccl_defaults") or {}).get("busbw_GBps") is not None else None),
         "rccl_defaults": st.get("rccl_defaults"),
         "algbw_GBps": h["algbw"] if h else None,
         "algbw_note": h.get("algbw_note") if h else None,
@@ -546,6 +589,7 @@ def main(argv=None) -> int:
     _watchdog(rank, deadline, st, once, runner_box, args, world)
 
     cuda = args.device == "cuda"
+    fake_gpus = 0 if cuda else int(os.environ.get(FAKE_GPUS_ENV) or 0)
     if cuda and not torch.cuda.is_available():
         print("bench.py needs an MI355X GPU (torch.cuda.is_available() is False)", file=sys.stderr)
         return 2
@@ -592,6 +636,8 @@ def main(argv=None) -> int:
         from network_operator_amd.parallel.rail import device_bdf
 
         mine["bdf"] = device_bdf(local_rank)
+    elif fake_gpus:
+        mine["bdf"] = FAKE_BDFS[local_rank % len(FAKE_BDFS)]
     dist.all_gather_object(records, mine, group=host_pg)
     job_bdfs = [r.get("bdf") for r in records if r and r.get("bdf")]
 
@@ -605,6 +651,7 @@ def main(argv=None) -> int:
     for _ in range(args.warmup):
         dist.all_reduce(buf)
     smi_before = None
+    fake_smi = _fake_smi() if rank == 0 and not cuda else None
     if rank == 0 and cuda:  # xGMI counters (amd-smi), outside the timed region
         try:
             from network_operator_amd.ops import smi
@@ -612,6 +659,10 @@ def main(argv=None) -> int:
             smi_before = smi.snapshot()
         except Exception as e:
             st["smi_note"] = f"amd-smi counters unavailable: {e}"
+    elif fake_smi is not None:
+        from network_operator_amd.ops import smi
+
+        smi_before = fake_smi["before"]
     dist.barrier()
     C.sync(device)
     t0 = time.perf_counter()
@@ -622,7 +673,7 @@ def main(argv=None) -> int:
     dist.barrier()
     if rank == 0 and smi_before is not None:
         try:
-            t = smi.traffic(smi_before, smi.snapshot())
+            t = smi.traffic(smi_before, fake_smi["after"] if fake_smi is not None else smi.snapshot())
             st["xgmi_traffic"] = {"links_up": t["links_up"], "links_with_traffic": t["links_with_traffic"],
                                   "GB_per_gpu": [round(sum(g["bytes_per_link"]) / 1e9, 3) for g in t["gpus"]],
                                   "job": FA.traffic_view(job_bdfs, t)}
@@ -659,7 +710,7 @@ def main(argv=None) -> int:
         others = []
         for op in [o.strip() for o in args.collectives.split(",") if o.strip()]:
             before = None
-            if rank == 0 and smi_before is not None:  # no collective starts before rank 0 joins it
+            if rank == 0 and smi_before is not None and fake_smi is None:  # no collective starts before rank 0 joins it
                 try:
                     before = smi.snapshot()
                 except Exception:
@@ -702,19 +753,8 @@ def main(argv=None) -> int:
         runner = bench_extras.Runner(deadline, base_env=base_env)
         runner_box.append(runner)
         art_env = art["doc"]["env"] if art and "error" not in art["doc"] else {}
-        plan = []
-        if args.rccl_defaults and args.artifacts != "off":
-            plan.append("rccl_defaults")
-        if cuda and args.native_rccl:
-            plan.append("native_rccl")
-        if cuda and world > 1 and args.xgmi_probe:
-            plan.append("xgmi_probe")
-        direct = args.xgmi_allreduce == "1" or (args.xgmi_allreduce == "auto" and world == torch.cuda.device_count()) \
-            if cuda else False
-        if cuda and world > 1 and direct:
-            plan += ["xgmi_allreduce", "xgmi_comm"]
-        if args.node_ready != "off":
-            plan.append("node_ready")
+        plan = plan_extras(args, world, gpu=cuda or fake_gpus > 0,
+                           device_count=torch.cuda.device_count() if cuda else fake_gpus)
         st["pending"] = list(plan)
         for name in plan:
             if name == "rccl_defaults":

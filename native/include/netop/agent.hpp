@@ -189,6 +189,8 @@ struct Config {
 // Where the agent leaves the one-line reason the node is not ready (beside --status-file), and
 // what `discover --ready-check --status-file=...` prints when it fails.
 std::string reason_path(const std::string& status_file);
+// --ready-check's reason while the agent has not written its status file yet.
+inline constexpr const char* kStartingReason = "agent starting";
 
 // FRA_PROTOCOL / rtm_protocol tag on the agent's rail rules and rail-table routes ("installed by
 // the AMD network operator"): cleanup only ever removes rules and routes carrying it.

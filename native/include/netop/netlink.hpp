@@ -64,7 +64,7 @@ struct RouteSpec {
     std::optional<Ipv4> prefsrc;
     uint8_t scope = RT_SCOPE_UNIVERSE;
     uint8_t protocol = RTPROT_BOOT;  // vishvananda/netlink's NewRtMsg default
-    uint8_t table = RT_TABLE_MAIN;
+    uint32_t table = RT_TABLE_MAIN;  // RTA_TABLE: ids above 255 do not fit rtm_table
     uint8_t type = RTN_UNICAST;
     uint32_t priority = 0;
     // Listing only: the output interfaces of a multipath route's next hops (RTA_MULTIPATH).
@@ -83,6 +83,12 @@ struct RuleSpec {
     // FRA_PROTOCOL (Linux >= 4.17): who installed the rule.  0 = unspecified (matches any on
     // delete).  The agent tags its rail rules so it only ever removes rules it added.
     uint8_t protocol = 0;
+    // Listing only.  action: FR_ACT_* (1 = look up `table`).  selective: the rule matches only
+    // some packets (a source or destination prefix, TOS, in/out interface, fwmark, L3 master
+    // device, uid, IP protocol or port range, or an inverted match); `from all lookup main`
+    // is not.
+    uint8_t action = 1;
+    bool selective = false;
     bool operator==(const RuleSpec& o) const {
         return src.masked() == o.src.masked() && table == o.table && priority == o.priority && protocol == o.protocol;
     }
@@ -119,7 +125,7 @@ class NetOps {
     virtual void rule_del(const RuleSpec& r) = 0;
     virtual std::vector<RuleSpec> rule_list() = 0;
     // IPv4 routes of one table (0 = every table).
-    virtual std::vector<RouteSpec> route_list(uint8_t table) = 0;
+    virtual std::vector<RouteSpec> route_list(uint32_t table) = 0;
     virtual void link_set_up(int ifindex) = 0;
     virtual void link_set_down(int ifindex) = 0;
     virtual void link_set_mtu(int ifindex, int mtu) = 0;
@@ -130,9 +136,15 @@ class NetOps {
         return std::nullopt;
     }
     // Interfaces a default route (0.0.0.0/0, and ::/0 where the source lists IPv6) leaves
-    // through, in any table but the local one: the node's own uplinks, which the agent never
-    // flushes or re-MTUs.  The base implementation reads route_list(0).
+    // through, in a table that every packet the node sends may be looked up in (reached by a
+    // rule that selects nothing: main and default, normally): the node's own uplinks, which the
+    // agent never flushes or re-MTUs.  A default route in a table that only selective rules reach
+    // (per-NIC source routing, "from 10.1.0.0/16 lookup 101") is not an uplink: see
+    // policy_default_routes().  Without the rules (unreadable) every table but local counts.
+    // The base implementation reads route_list(0) and rule_list().
     virtual std::vector<int> default_route_links();
+    // (ifindex, table) of the IPv4 default routes that only selective rules reach.
+    std::vector<std::pair<int, uint32_t>> policy_default_routes();
     // The link with this ifindex (a bond / bridge master, ...); nullopt when there is none or the
     // source cannot look links up by index.
     virtual std::optional<LinkInfo> link_by_ifindex(int ifindex) {
@@ -157,6 +169,7 @@ class Rtnl final : public NetOps {
     void rule_add(const RuleSpec& r) override;
     void rule_del(const RuleSpec& r) override;
     std::vector<RuleSpec> rule_list() override;
+    std::vector<RuleSpec> rule_list6();  // IPv6 rules (action, table, selective)
     void link_set_up(int ifindex) override;
     void link_set_down(int ifindex) override;
     void link_set_mtu(int ifindex, int mtu) override;
@@ -168,7 +181,7 @@ class Rtnl final : public NetOps {
     // Extra operations (harness / diagnostics; not part of the injectable table).
     LinkInfo link_by_index(int ifindex);
     std::vector<LinkInfo> link_list();
-    std::vector<RouteInfo> route_list(uint8_t table = RT_TABLE_MAIN) override;
+    std::vector<RouteInfo> route_list(uint32_t table = RT_TABLE_MAIN) override;
     void veth_add(const std::string& name, const std::string& peer);
     // A link of a kind that needs no IFLA_INFO_DATA ("bridge", "dummy", ...).
     void link_add(const std::string& name, const std::string& kind);
@@ -194,6 +207,7 @@ class Rtnl final : public NetOps {
     void rule_request(uint16_t type, uint16_t flags, const RuleSpec& r);
     void transact(Msg& m, const std::function<void(const nlmsghdr*)>& on_reply);
     void dump(Msg& m, const std::function<void(const nlmsghdr*)>& on_item);
+    std::vector<RuleSpec> dump_rules(uint8_t family);
     void set_link(int ifindex, unsigned flags, unsigned change, const std::function<void(Msg&)>& attrs);
 
     int fd_ = -1;

@@ -174,13 +174,14 @@ PYBIND11_MODULE(_netop_native, m) {
                 d["table"] = x.table;
                 d["priority"] = x.priority;
                 d["protocol"] = x.protocol;
+                d["selective"] = x.selective;
                 l.append(d);
             }
             return l;
         })
         .def("route_list", [](nl::Rtnl& r, int table) {
             py::list l;
-            for (auto& x : r.route_list(uint8_t(table))) {
+            for (auto& x : r.route_list(uint32_t(table))) {
                 py::dict d;
                 d["dst"] = x.dst.masked().str();
                 d["gateway"] = x.gateway ? py::object(py::str(x.gateway->str())) : py::none();
@@ -193,7 +194,17 @@ PYBIND11_MODULE(_netop_native, m) {
             }
             return l;
         }, py::arg("table") = int(RT_TABLE_MAIN))
-        .def("route_append", [](nl::Rtnl& r, const std::string& dst, py::object gateway, int ifindex, int protocol) {
+        .def("rule_add", [](nl::Rtnl& r, const std::string& src, uint32_t table, uint32_t priority) {
+            nl::RuleSpec rs;
+            auto s = Ipv4Prefix::parse(src);
+            if (!s) throw py::value_error("bad CIDR");
+            rs.src = *s;
+            rs.table = table;
+            rs.priority = priority;
+            r.rule_add(rs);
+        }, py::arg("src"), py::arg("table"), py::arg("priority"))
+        .def("route_append", [](nl::Rtnl& r, const std::string& dst, py::object gateway, int ifindex, int protocol,
+                                uint32_t table) {
             nl::RouteSpec rs;
             auto d = Ipv4Prefix::parse(dst);
             if (!d) throw py::value_error("bad CIDR");
@@ -205,8 +216,10 @@ PYBIND11_MODULE(_netop_native, m) {
             }
             rs.ifindex = ifindex;
             rs.protocol = uint8_t(protocol);
+            rs.table = table;
             r.route_append(rs);
-        }, py::arg("dst"), py::arg("gateway") = py::none(), py::arg("ifindex") = 0, py::arg("protocol") = int(RTPROT_BOOT))
+        }, py::arg("dst"), py::arg("gateway") = py::none(), py::arg("ifindex") = 0, py::arg("protocol") = int(RTPROT_BOOT),
+           py::arg("table") = uint32_t(RT_TABLE_MAIN))
         .def("default_route_links", &nl::Rtnl::default_route_links)
         .def("link_set_up", &nl::Rtnl::link_set_up)
         .def("link_set_down", &nl::Rtnl::link_set_down)

@@ -648,7 +648,7 @@ void Agent::add_rail_routing(NicState& n) {
     auto same = [](const nl::RouteSpec& a, const nl::RouteSpec& b) {
         return a.dst.masked() == b.dst.masked() && a.gateway == b.gateway && a.ifindex == b.ifindex;
     };
-    for (const auto& r : ops_.route_list(uint8_t(t))) {
+    for (const auto& r : ops_.route_list(uint32_t(t))) {
         if (r.protocol != kRailProtocol || same(r, p2p) || same(r, routed)) continue;
         try {
             ops_.route_del(r);

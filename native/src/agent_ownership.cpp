@@ -220,7 +220,23 @@ void Agent::refuse_uplinks() {
             named.push_back(n.ifname + *via);
         }
     }
-    if (bad.empty()) return;
+    if (bad.empty()) {
+        // A default route in a per-NIC policy-routing table ("from <its subnet> lookup 101") is
+        // the site's source routing for that NIC, not the node's way out: configure the NIC, but
+        // say that the route goes with the addresses it depends on.
+        std::vector<std::pair<int, uint32_t>> policy;
+        try {
+            policy = ops_.policy_default_routes();
+        } catch (const std::exception&) {
+        }
+        for (const auto& [ifindex, table] : policy)
+            for (const auto& n : nics_)
+                if (n.link.index == ifindex)
+                    NLOG_W("Interface '%s' has a default route in routing table %u, which only selective rules reach "
+                           "(policy routing): not the node's uplink; it depends on the addresses the agent replaces",
+                           n.ifname.c_str(), table);
+        return;
+    }
     const std::string what = join(named, ", ");
     if (cfg_.dry_run) {
         NLOG_W("dry run: would refuse to configure %s: the node's default route leaves through it", what.c_str());

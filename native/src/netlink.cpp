@@ -14,6 +14,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <set>
 
 #include "netop/log.hpp"
 
@@ -412,7 +413,7 @@ RouteInfo parse_route(const nlmsghdr* h) {
                 if (RTA_PAYLOAD(a) >= 4) {
                     uint32_t t;
                     std::memcpy(&t, RTA_DATA(a), 4);
-                    r.table = uint8_t(t > 255 ? 0 : t);
+                    r.table = t;
                 }
                 break;
         }
@@ -602,7 +603,7 @@ void Rtnl::route_append(const RouteSpec& r) {
     rtmsg rtm{};
     rtm.rtm_family = AF_INET;
     rtm.rtm_dst_len = uint8_t(r.dst.len);
-    rtm.rtm_table = r.table;
+    rtm.rtm_table = r.table < 256 ? uint8_t(r.table) : uint8_t(RT_TABLE_UNSPEC);
     rtm.rtm_protocol = r.protocol;
     rtm.rtm_scope = r.scope;
     rtm.rtm_type = r.type;
@@ -612,6 +613,7 @@ void Rtnl::route_append(const RouteSpec& r) {
     if (r.prefsrc) m.attr_ip(RTA_PREFSRC, *r.prefsrc);
     if (r.ifindex > 0) m.attr_u32(RTA_OIF, uint32_t(r.ifindex));
     if (r.priority) m.attr_u32(RTA_PRIORITY, r.priority);
+    m.attr_u32(RTA_TABLE, r.table);
     transact(m, nullptr);
 }
 
@@ -620,16 +622,17 @@ void Rtnl::route_del(const RouteSpec& r) {
     rtmsg rtm{};
     rtm.rtm_family = AF_INET;
     rtm.rtm_dst_len = uint8_t(r.dst.len);
-    rtm.rtm_table = r.table;
+    rtm.rtm_table = r.table < 256 ? uint8_t(r.table) : uint8_t(RT_TABLE_UNSPEC);
     rtm.rtm_scope = RT_SCOPE_NOWHERE;
     m.put(rtm);
     m.attr_ip(RTA_DST, r.dst.network());
     if (r.gateway) m.attr_ip(RTA_GATEWAY, *r.gateway);
     if (r.ifindex > 0) m.attr_u32(RTA_OIF, uint32_t(r.ifindex));
+    m.attr_u32(RTA_TABLE, r.table);
     transact(m, nullptr);
 }
 
-std::vector<RouteInfo> Rtnl::route_list(uint8_t table) {
+std::vector<RouteInfo> Rtnl::route_list(uint32_t table) {
     Msg m(RTM_GETROUTE, 0);
     rtmsg rtm{};
     rtm.rtm_family = AF_INET;
@@ -650,9 +653,44 @@ static void add_default_links(const RouteInfo& r, std::vector<int>& out) {
     out.insert(out.end(), r.nexthops.begin(), r.nexthops.end());
 }
 
+// Tables any packet may be looked up in: those of rules that look a table up and select nothing.
+// nullopt: no rules to judge by (then every table counts, as before policy routing was read).
+static std::optional<std::set<uint32_t>> lookup_all_tables(const std::vector<RuleSpec>& rules) {
+    std::set<uint32_t> out;
+    for (const auto& r : rules)
+        if (r.action == 1 && !r.selective) out.insert(r.table);
+    if (out.empty()) return std::nullopt;
+    return out;
+}
+
+static std::optional<std::set<uint32_t>> global_tables(NetOps& ops) {
+    try {
+        return lookup_all_tables(ops.rule_list());
+    } catch (const std::exception&) {
+        return std::nullopt;  // conservative: every table's default route is an uplink
+    }
+}
+
 std::vector<int> NetOps::default_route_links() {
+    const auto global = global_tables(*this);
     std::vector<int> out;
-    for (const auto& r : route_list(0)) add_default_links(r, out);
+    for (const auto& r : route_list(0))
+        if (!global || global->count(r.table)) add_default_links(r, out);
+    std::sort(out.begin(), out.end());
+    out.erase(std::unique(out.begin(), out.end()), out.end());
+    return out;
+}
+
+std::vector<std::pair<int, uint32_t>> NetOps::policy_default_routes() {
+    const auto global = global_tables(*this);
+    std::vector<std::pair<int, uint32_t>> out;
+    if (!global) return out;
+    for (const auto& r : route_list(0)) {
+        if (global->count(r.table)) continue;
+        std::vector<int> links;
+        add_default_links(r, links);
+        for (int l : links) out.emplace_back(l, r.table);
+    }
     std::sort(out.begin(), out.end());
     out.erase(std::unique(out.begin(), out.end()), out.end());
     return out;
@@ -661,13 +699,20 @@ std::vector<int> NetOps::default_route_links() {
 std::vector<int> Rtnl::default_route_links() {
     std::vector<int> out = NetOps::default_route_links();
     // ::/0 too: a management NIC may carry only an IPv6 default route (SLAAC / RA).
+    std::optional<std::set<uint32_t>> global6;
+    try {
+        global6 = lookup_all_tables(rule_list6());
+    } catch (const std::exception&) {
+    }
     Msg m(RTM_GETROUTE, 0);
     rtmsg rtm{};
     rtm.rtm_family = AF_INET6;
     m.put(rtm);
     try {
         dump(m, [&](const nlmsghdr* h) {
-            if (h->nlmsg_type == RTM_NEWROUTE) add_default_links(parse_route(h), out);
+            if (h->nlmsg_type != RTM_NEWROUTE) return;
+            auto r = parse_route(h);
+            if (!global6 || global6->count(r.table)) add_default_links(r, out);
         });
     } catch (const SysError& e) {  // IPv6 disabled on the node (ipv6.disable=1)
         if (e.code() != EAFNOSUPPORT && e.code() != EOPNOTSUPP) throw;
@@ -683,6 +728,12 @@ namespace {
 constexpr uint16_t kFraSrc = 2, kFraPriority = 6, kFraTable = 15;  // FRA_SRC, FRA_PRIORITY, FRA_TABLE
 constexpr uint16_t kFraProtocol = 21;                               // FRA_PROTOCOL (u8)
 constexpr uint8_t kFrActToTbl = 1;                                  // FR_ACT_TO_TBL
+// Attributes that make a rule match only some packets: FRA_DST 1, FRA_IIFNAME 3, FRA_FWMARK 10
+// (when non-zero), FRA_OIFNAME 17, FRA_L3MDEV 19, FRA_UID_RANGE 20, FRA_IP_PROTO 22,
+// FRA_SPORT_RANGE 23, FRA_DPORT_RANGE 24 (linux/fib_rules.h; FRA_SRC handled by src_len).
+constexpr uint16_t kFraDst = 1, kFraIifname = 3, kFraFwmark = 10, kFraOifname = 17, kFraL3mdev = 19,
+                   kFraUidRange = 20, kFraIpProto = 22, kFraSportRange = 23, kFraDportRange = 24;
+constexpr uint32_t kFibRuleInvert = 0x2;  // FIB_RULE_INVERT
 struct FibRuleHdr {
     uint8_t family, dst_len, src_len, tos, table, res1, res2, action;
     uint32_t flags;
@@ -708,10 +759,10 @@ void Rtnl::rule_add(const RuleSpec& r) { rule_request(RTM_NEWRULE, NLM_F_CREATE 
 
 void Rtnl::rule_del(const RuleSpec& r) { rule_request(RTM_DELRULE, 0, r); }
 
-std::vector<RuleSpec> Rtnl::rule_list() {
+std::vector<RuleSpec> Rtnl::dump_rules(uint8_t family) {
     Msg m(RTM_GETRULE, 0);
     FibRuleHdr frh{};
-    frh.family = AF_INET;
+    frh.family = family;
     m.put(frh);
     std::vector<RuleSpec> out;
     dump(m, [&](const nlmsghdr* h) {
@@ -720,17 +771,49 @@ std::vector<RuleSpec> Rtnl::rule_list() {
         RuleSpec r;
         r.src.len = f->src_len;
         r.table = f->table;
+        r.action = f->action;
+        r.selective = f->src_len || f->dst_len || f->tos || (f->flags & kFibRuleInvert);
         const auto* first = reinterpret_cast<const rtattr*>(reinterpret_cast<const char*>(f) + NLMSG_ALIGN(sizeof(FibRuleHdr)));
         for_each_attr(first, h->nlmsg_len - NLMSG_LENGTH(NLMSG_ALIGN(sizeof(FibRuleHdr))), [&](const rtattr* a) {
-            if (a->rta_type == kFraSrc && RTA_PAYLOAD(a) == 4) r.src.addr = Ipv4::from_net(RTA_DATA(a));
-            if (a->rta_type == kFraPriority && RTA_PAYLOAD(a) >= 4) std::memcpy(&r.priority, RTA_DATA(a), 4);
-            if (a->rta_type == kFraTable && RTA_PAYLOAD(a) >= 4) std::memcpy(&r.table, RTA_DATA(a), 4);
-            if (a->rta_type == kFraProtocol && RTA_PAYLOAD(a) >= 1) r.protocol = *static_cast<const uint8_t*>(RTA_DATA(a));
+            switch (a->rta_type) {
+                case kFraSrc:
+                    if (family == AF_INET && RTA_PAYLOAD(a) == 4) r.src.addr = Ipv4::from_net(RTA_DATA(a));
+                    break;
+                case kFraPriority:
+                    if (RTA_PAYLOAD(a) >= 4) std::memcpy(&r.priority, RTA_DATA(a), 4);
+                    break;
+                case kFraTable:
+                    if (RTA_PAYLOAD(a) >= 4) std::memcpy(&r.table, RTA_DATA(a), 4);
+                    break;
+                case kFraProtocol:
+                    if (RTA_PAYLOAD(a) >= 1) r.protocol = *static_cast<const uint8_t*>(RTA_DATA(a));
+                    break;
+                case kFraFwmark: {
+                    uint32_t mark = 0;
+                    if (RTA_PAYLOAD(a) >= 4) std::memcpy(&mark, RTA_DATA(a), 4);
+                    if (mark) r.selective = true;
+                    break;
+                }
+                case kFraDst:
+                case kFraIifname:
+                case kFraOifname:
+                case kFraL3mdev:
+                case kFraUidRange:
+                case kFraIpProto:
+                case kFraSportRange:
+                case kFraDportRange:
+                    r.selective = true;
+                    break;
+            }
         });
         out.push_back(r);
     });
     return out;
 }
+
+std::vector<RuleSpec> Rtnl::rule_list() { return dump_rules(AF_INET); }
+
+std::vector<RuleSpec> Rtnl::rule_list6() { return dump_rules(AF_INET6); }
 
 void Rtnl::set_link(int ifindex, unsigned flags, unsigned change, const std::function<void(Msg&)>& attrs) {
     Msg m(RTM_NEWLINK, 0);

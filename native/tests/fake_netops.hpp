@@ -140,7 +140,7 @@ struct FakeNetOps : netop::nl::NetOps {
         maybe_fail("rule_list");
         return rules;
     }
-    std::vector<netop::nl::RouteSpec> route_list(uint8_t table) override {
+    std::vector<netop::nl::RouteSpec> route_list(uint32_t table) override {
         maybe_fail("route_list");
         std::vector<netop::nl::RouteSpec> out;
         for (auto& r : routes)

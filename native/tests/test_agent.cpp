@@ -2465,6 +2465,50 @@ TEST(agent_refuses_a_nic_that_carries_the_default_route_in_every_mode) {
     CHECK(err.find("Cannot read the node's routes") == 0);
 }
 
+TEST(agent_configures_a_nic_whose_default_route_is_only_in_a_policy_routing_table) {
+    // multi-rail RoCE nodes give each NIC its own source-routing table with a default
+    // route in it ("from 192.168.1.0/24 lookup 101").  Only selective rules reach that table:
+    // it is not the node's uplink, and the NIC is configured.  A default route in a table that
+    // a rule selecting nothing reaches (main) still is.  Unreadable rules: every table counts.
+    auto rule = [](uint32_t table, uint32_t prio, const char* src) {
+        nl::RuleSpec r;
+        r.table = table;
+        r.priority = prio;
+        if (src) {
+            r.src = *Ipv4Prefix::parse(src);
+            r.selective = true;
+        }
+        return r;
+    };
+    for (int variant : {0, 1, 2}) {
+        Fixture f;
+        f.cfg.mode = "L3";
+        f.cfg.keep_running = false;
+        f.ops.rules = {rule(RT_TABLE_LOCAL, 0, nullptr), rule(101, 100, "192.168.1.0/24"),
+                       rule(RT_TABLE_MAIN, 32766, nullptr), rule(RT_TABLE_DEFAULT, 32767, nullptr)};
+        auto def = route(11, "0.0.0.0/0", "192.168.1.1", RTPROT_STATIC);
+        def.table = variant == 1 ? RT_TABLE_MAIN : 101;
+        f.ops.routes.push_back(def);
+        if (variant == 2) f.ops.fail.insert("rule_list");
+        std::string err;
+        try {
+            agent::Agent a(f.cfg, f.ops, f.all_valid(), f.nm());
+            a.run(-1);
+        } catch (const agent::AgentError& e) {
+            err = e.what();
+        }
+        if (variant == 0) {
+            CHECK(f.ops.default_route_links().empty());
+            CHECK(f.ops.policy_default_routes() == (std::vector<std::pair<int, uint32_t>>{{11, 101}}));
+            CHECK_EQ(err, std::string());
+            CHECK_EQ(f.ops.addrs.size(), size_t(3));  // every NIC configured, ens1 too
+        } else {
+            CHECK(err.find("Refusing to configure ens1: the node's default route leaves through it") == 0);
+            CHECK_EQ(f.ops.calls["link_set_up"], 0);
+        }
+    }
+}
+
 TEST(agent_nic_lock_gives_every_nic_one_owner) {
     // Another agent (a host-nic policy naming a rail, say) holds ens1: this agent, whatever its
     // label file, waits, then fails naming the NIC, having changed nothing; once the holder is

@@ -125,6 +125,9 @@ int main(int argc, char** argv) {
         // The kubelet keeps a failing probe's output in the Pod's events: say why.
         std::optional<std::string> why;
         if (!cfg.status_file.empty()) why = read_file(agent::reason_path(cfg.status_file));
+        // No status file yet: the agent has not got as far as writing one (a start-up state for
+        // the operator, like "waiting for LLDP"), not a failure.
+        if (!why && !cfg.status_file.empty() && !path_exists(cfg.status_file)) why = std::string(agent::kStartingReason);
         std::string line = why ? trim(*why) : "readiness label " + cfg.labels.path() + " not published";
         if (line.size() > 900) line = line.substr(0, 900) + " ...";
         std::printf("not ready: %s\n", line.c_str());

@@ -270,9 +270,12 @@ def host_nic_agent_args(p: T.NetworkClusterPolicy) -> List[str]:
     if p.spec.logLevel > 0:
         args.append(f"--v={p.spec.logLevel}")
     if hn.mtu > 0:
-        # The node's own NICs get their MTU back when the agent goes for good: on a clean exit, or
-        # (keepConfigOnRestart) from the record the cleanup Job reads.
-        args += [f"--mtu={hn.mtu}", "--restore-mtu", f"--mtu-state={ARTIFACT_DIR_CONTAINER}/{HOST_NIC_MTU_STATE_FILE}"]
+        args.append(f"--mtu={hn.mtu}")
+    # The node's own NICs get their MTU back when the agent goes for good: on a clean exit, or
+    # (keepConfigOnRestart) from the record the cleanup Job reads.  Always, not only while mtu is
+    # set: the agent applies its default MTU otherwise, and a policy that dropped mtu must still
+    # let the next agent and the cleanup Job find and restore the record.
+    args += ["--restore-mtu", f"--mtu-state={ARTIFACT_DIR_CONTAINER}/{HOST_NIC_MTU_STATE_FILE}"]
     if hn.disableNetworkManager:
         args += ["--disable-networkmanager", "--nm-keyfile-dir=/etc/NetworkManager/conf.d"]
     if hn.layer == "L3":
@@ -436,7 +439,8 @@ def probe_reason(events: List[dict], limit: int = 1500) -> Optional[str]:
 
 # What an agent says while its node is still coming up.  "waiting for carrier": L2, a NIC whose
 # optic / switch port is still training its link, within the agent's --carrier-wait.
-STARTUP_REASONS = ("waiting for LLDP", "not configured yet", "waiting for carrier")
+# "agent starting": probed before the agent wrote its status file (discover --ready-check).
+STARTUP_REASONS = ("waiting for LLDP", "not configured yet", "waiting for carrier", "agent starting")
 
 
 def _starting_up(reason: str) -> bool:

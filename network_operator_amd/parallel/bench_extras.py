@@ -13,8 +13,10 @@ all-reduce, the netns node-ready harness — runs afterwards through :class:`Run
   ``{"error": "timed out"}`` (its own cap), never silently dropped.
 
 ``python -m network_operator_amd.parallel.bench_extras NAME JSON_KWARGS`` runs one extra and
-prints its result as one JSON line.  Test hook: ``NETOP_BENCH_HANG_EXTRA=NAME`` makes that extra
-(or a bench.py started as that extra) sleep forever, to rehearse a hung first contact.
+prints its result as one JSON line.  Test hooks: ``NETOP_BENCH_HANG_EXTRA=NAME`` makes that extra
+(or a bench.py started as that extra) sleep forever, to rehearse a hung first contact;
+``NETOP_BENCH_FAKE_EXTRA_S=NAME=SECONDS[,...]`` makes the named extras stand-ins that take that
+long and report ``{"fake": true}`` (the CPU rehearsal of the GPU extras' order and deadline).
 """
 
 from __future__ import annotations
@@ -29,6 +31,7 @@ import time
 from typing import Dict, List, Optional
 
 HANG_ENV = "NETOP_BENCH_HANG_EXTRA"
+FAKE_EXTRA_ENV = "NETOP_BENCH_FAKE_EXTRA_S"
 NAME_ENV = "NETOP_BENCH_EXTRA_NAME"
 LAUNCH_ENV = ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK", "ROLE_WORLD_SIZE",
               "MASTER_ADDR", "MASTER_PORT", "GROUP_WORLD_SIZE", "ROLE_NAME", "NETOP_BENCH_STORE")
@@ -40,6 +43,15 @@ def maybe_hang() -> None:
     if want and os.environ.get(NAME_ENV) == want:
         while True:
             time.sleep(3600)
+
+
+def fake_seconds(name: str) -> Optional[float]:
+    """The test hook: how long extra NAME's stand-in takes, when it has one."""
+    for item in (os.environ.get(FAKE_EXTRA_ENV) or "").split(","):
+        k, _, v = item.partition("=")
+        if k.strip() == name and v.strip():
+            return float(v)
+    return None
 
 
 def clean_env(env: Optional[dict] = None) -> dict:
@@ -226,6 +238,11 @@ def main(argv=None) -> int:
     name = argv[0]
     kwargs = json.loads(argv[1]) if len(argv) > 1 else {}
     maybe_hang()
+    fake = fake_seconds(name)
+    if fake is not None:
+        time.sleep(fake)
+        print(json.dumps({"fake": True, "extra": name, "kwargs": kwargs}), flush=True)
+        return 0
     root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     if root not in sys.path:
         sys.path.insert(0, root)

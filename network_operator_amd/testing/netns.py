@@ -664,6 +664,54 @@ def run_scenario(n_nics: int = 8, mode: str = "L3", seed: int | None = None, int
             shutil.rmtree(tmp, ignore_errors=True)
 
 
+def run_policy_routing_uplink() -> dict:
+    """a rail NIC with its own source-routing table holding a default route
+    (``from 192.168.50.0/24 lookup 1001``, ``default via 192.168.50.1 dev rail0 table 1001``)
+    while the node's uplink is another NIC (main table).  The agent must take the rail (dry run:
+    not refused; a real L2 start: configured, with a warning about the per-NIC route) and still
+    refuse the uplink.  The table id is above 255 (RTA_TABLE).  Must run inside ``unshare -rn``."""
+    from ..utils.paths import native_bin
+
+    nat = _native()
+    rt = nat.Rtnl()
+    rt.link_set_up(rt.link_by_name("lo")["index"])
+    tmp = Path(tempfile.mkdtemp(prefix="netop-polroute-"))
+    try:
+        for nif, peer in (("rail0", "rpeer0"), ("mgmt0", "mpeer0")):
+            rt.veth_add(nif, peer)
+            rt.link_set_up(rt.link_by_name(peer)["index"])
+            rt.link_set_up(rt.link_by_name(nif)["index"])
+        rail, mgmt = rt.link_by_name("rail0")["index"], rt.link_by_name("mgmt0")["index"]
+        rt.addr_add(rail, "192.168.50.10/24")
+        rt.addr_add(mgmt, "10.0.0.5/24")
+        rt.rule_add("192.168.50.0/24", 1001, 1000)
+        rt.route_append("0.0.0.0/0", "192.168.50.1", rail, 4, table=1001)  # RTPROT_STATIC
+        rt.route_append("0.0.0.0/0", "10.0.0.1", mgmt, 4)
+        res: dict = {"default_route_links": sorted(rt.default_route_links()), "rail": rail, "mgmt": mgmt,
+                     "rules": rt.rule_list(), "table_1001": rt.route_list(1001)}
+        base = [str(native_bin("discover")), "--mode=L2", "--nic-discovery=none", "--mtu=9000", "-v=2",
+                f"--nfd-features-dir={tmp / 'features.d'}"]
+        env = dict(os.environ, SYSFS_ROOT=str(tmp / "sys"))
+        (tmp / "sys").mkdir()
+        for name, ifs in (("dry_rail", "rail0"), ("dry_mgmt", "mgmt0")):
+            st = tmp / f"{name}.json"
+            r = subprocess.run([*base, "--dry-run", f"--interfaces={ifs}", f"--status-file={st}"], env=env,
+                               capture_output=True, text=True, timeout=30)
+            res[name] = {"rc": r.returncode, "stderr": r.stderr[-2000:],
+                         "status": json.loads(st.read_text()) if st.exists() else None}
+        r = subprocess.run([*base, "--configure=true", "--interfaces=rail0", "--carrier-wait=2s"], env=env,
+                           capture_output=True, text=True, timeout=30)
+        res["configure_rail"] = {"rc": r.returncode, "stderr": r.stderr[-3000:],
+                                 "mtu": rt.link_by_name("rail0")["mtu"]}
+        r = subprocess.run([*base, "--configure=true", "--interfaces=mgmt0"], env=env, capture_output=True, text=True,
+                           timeout=30)
+        res["configure_mgmt"] = {"rc": r.returncode, "stderr": r.stderr[-2000:], "mtu": rt.link_by_name("mgmt0")["mtu"],
+                                 "addrs": rt.addr_list(mgmt)}
+        return res
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+
+
 MGMT_NIC, HOST_NIC = "ens9np0", "ens49np1"  # the fixture node's two NICs on their own root ports
 
 
@@ -826,7 +874,10 @@ def _main(argv=None) -> int:
     ap.add_argument("--json", default="{}", help="run_scenario kwargs")
     a = ap.parse_args(argv)
     kw = json.loads(a.json)
-    res = run_host_nic_ownership(**kw) if kw.pop("host_nic_ownership", False) else run_scenario(**kw)
+    if kw.pop("policy_routing_uplink", False):
+        res = run_policy_routing_uplink()
+    else:
+        res = run_host_nic_ownership(**kw) if kw.pop("host_nic_ownership", False) else run_scenario(**kw)
     print(json.dumps(res))
     return 0
 

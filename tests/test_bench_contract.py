@@ -516,3 +516,96 @@ def test_bench_claims_configs_1_only_when_its_node_ready_half_ran():
     assert model.startswith(bench.config_name(8) + " [this run: RCCL all-reduce over xGMI with the agent's artifacts; "
                                                    "host RoCE links not configured by it (node-ready not run: ")
     assert bench.run_config(args, 8, ok)[0] == bench.config_name(8)
+
+
+def test_only_the_all_gpu_run_plans_the_direct_xgmi_extras():
+    """The driver runs N = 1, 2, 4, 8 back to back on an 8-GPU node: the direct xGMI all-reduces
+    (first contact of the hand-written kernels with real peers) run only in the N = 8 run, after
+    the RCCL A/B, the native harness and the link probe; a forced --xgmi-allreduce 1 runs them at
+    any N > 1."""
+    import argparse
+
+    import bench
+
+    def args(**kw):
+        d = dict(rccl_defaults=1, artifacts="agent", native_rccl=1, xgmi_probe=1, xgmi_allreduce="auto",
+                 node_ready="auto")
+        d.update(kw)
+        return argparse.Namespace(**d)
+    plans = {n: bench.plan_extras(args(), n, gpu=True, device_count=8) for n in (1, 2, 4, 8)}
+    assert plans[1] == ["rccl_defaults", "native_rccl", "node_ready"]
+    assert plans[2] == plans[4] == ["rccl_defaults", "native_rccl", "xgmi_probe", "node_ready"]
+    assert plans[8] == ["rccl_defaults", "native_rccl", "xgmi_probe", "xgmi_allreduce", "xgmi_comm", "node_ready"]
+    assert "xgmi_allreduce" in bench.plan_extras(args(xgmi_allreduce="1"), 2, gpu=True, device_count=8)
+    assert bench.plan_extras(args(), 8, gpu=False, device_count=0) == ["rccl_defaults", "node_ready"]
+
+
+def _fake_smi_doc(bdfs, moved_bytes):
+    """Two amd-smi snapshots (ops.smi.snapshot's shape): every GPU has its 7 xGMI links up (link 0
+    is the self entry, 'X'), and moved `moved_bytes` over each between them."""
+    def snap(kb):
+        gpus = []
+        for b in bdfs:
+            peers = ["ffffffffffff:ff:1f.7"] + [p for p in bdfs if p != b]
+            gpus.append({"bdf": b, "link_status": "X" + "U" * (len(peers) - 1), "xgmi_link_width": 16,
+                         "xgmi_link_speed": 38, "xgmi_read_kb": [0] + [kb] * (len(peers) - 1),
+                         "xgmi_write_kb": [0] + [kb] * (len(peers) - 1),
+                         "links": [{"peer": p, "type": 2} for p in peers]})
+        return {"gpus": gpus}
+    return {"before": snap(1000), "after": snap(1000 + moved_bytes // 2048)}
+
+
+def test_bench_n8_line_is_what_the_scaling_run_will_be_judged_on(tmp_path, node_sysfs):
+    """the first real 8-GPU run, rehearsed on the CPU (gloo, 8 ranks) with a
+    fake RCCL topology dump (8 GPUs, 7 xGMI peers each, with and without the agent's file) and
+    fake amd-smi counters (7 links per GPU, all moving data):
+
+    * ``value`` is the job aggregate, busbw_GBps x 8; busbw_GBps is rccl-tests' per-GPU busbw;
+    * ``busbw_ceiling_GBps`` is (n-1) x 76 GB/s = 532 and busbw_vs_ceiling divides by it;
+    * the link check passes from the dump and the counters (7 of 7);
+    * autotune + headline + extras fit inside --deadline-s: the extras run in their planned order,
+      the direct xGMI ones only because N equals the node's GPU count, and the one that would
+      overrun is killed at the deadline and the next one never starts -- one line, rc 0."""
+    import bench
+
+    n = 8
+    bdfs = bench.FAKE_BDFS[:n]
+    chains = [(b, [f"0000:{int(b[5:7], 16) - 7:02x}:00.0"]) for b in bdfs]
+    full = {b: [p for p in bdfs if p != b] for b in bdfs}
+    (tmp_path / "dump.xml").write_text(_dump(chains, full))
+    (tmp_path / "smi.json").write_text(json.dumps(_fake_smi_doc(bdfs, 64 << 20)))
+    deadline = 75
+    cmd = [sys.executable, str(ROOT / "bench.py"), "--gpus", str(n), "--steps", "3", "--warmup", "1", "--device", "cpu",
+           "--bytes", str(1 << 18), "--sweep", "", "--collectives", "", "--node-ready", "off",
+           "--sysfs-root", node_sysfs, "--deadline-s", str(deadline), "--autotune-cpu-variants", "1",
+           "--rccl-autotune-budget", "60"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=deadline + 60, cwd=tmp_path, env=_spawn_env(
+        NETOP_BENCH_FAKE_GPUS=str(n), NETOP_BENCH_FAKE_SMI=str(tmp_path / "smi.json"),
+        NETOP_BENCH_FAKE_RCCL_DUMP=str(tmp_path / "dump.xml"),
+        NETOP_BENCH_FAKE_RCCL_DUMP_DEFAULTS=str(tmp_path / "dump.xml"),
+        NETOP_BENCH_FAKE_EXTRA_S="native_rccl=0.2,xgmi_probe=0.2,xgmi_allreduce=3600,xgmi_comm=0.2"))
+    j = _bench_line(r)
+    assert j["n_gpus"] == n and j["config"]["parallelism"] == "dp8" and "8xMI355X" in j["config"]["model"]
+    # per-GPU vs aggregate
+    assert j["busbw_GBps"] == pytest.approx(j["algbw_GBps"] * 2 * (n - 1) / n, abs=1e-3)
+    assert j["value"] == pytest.approx(j["busbw_GBps"] * n, abs=1e-2) == pytest.approx(j["aggregate_busbw_GBps"], abs=1e-2)
+    assert j["aggregate_busbw_rccl_defaults_GBps"] == pytest.approx(j["busbw_rccl_defaults_GBps"] * n, abs=1e-2)
+    assert j["busbw_basis"].startswith("per GPU")
+    assert j["busbw_ceiling_GBps"] == pytest.approx(7 * 76.0)
+    assert j["busbw_vs_ceiling"] == pytest.approx(j["busbw_GBps"] / 532.0)
+    # the link check: RCCL's (fake) dump and the (fake) counters both see 7 links per GPU
+    chk = j["agent_artifacts"]["xgmi_links_check"]
+    assert chk["status"] == "ok" and chk["min_with_file"] == 7 and chk["min_links_with_traffic"] == 7, chk
+    assert j["xgmi_traffic"]["job"] == {"gpus": 8, "links_with_traffic_per_gpu": {b: 7 for b in bdfs},
+                                        "min_links_with_traffic": 7}
+    # autotune ran (one variant) and was folded in before the headline
+    assert j["rccl_autotune"]["probes"] and j["rccl_autotune"]["baseline_busbw_GBps"] > 0
+    # the extras, in order, within the deadline
+    names = [e["extra"] for e in j["extras_log"]]
+    assert names == ["rccl_defaults", "native_rccl", "xgmi_probe", "xgmi_allreduce"], j["extras_log"]
+    assert j["native_rccl"]["fake"] and j["xgmi_probe"]["fake"]
+    assert j["xgmi_allreduce"]["error"] == "deadline" and j["xgmi_allreduce"]["timed_out"]
+    assert j["xgmi_allreduce_multiprocess"]["error"] == "deadline"  # never started
+    assert "not started" in j["xgmi_allreduce_multiprocess"]["detail"]
+    assert j["elapsed_s"] <= deadline + 5
+    assert r.returncode == 0

@@ -495,3 +495,23 @@ def test_host_nic_policy_with_nothing_of_its_own_idles_with_one_reason():
     for nif in r["rails"] + [netns.MGMT_NIC, netns.HOST_NIC]:  # nothing touched, before or after SIGTERM
         assert r["while_ready"][nif] == r["before"][nif] and r["after_sigterm"][nif] == r["before"][nif], nif
     assert r["agent_rc"] == 0  # SIGTERM ends the wait cleanly
+
+
+def test_per_nic_policy_routing_default_is_not_the_node_uplink():
+    """a default route in a per-NIC source-routing table (reached only by
+    ``from <subnet> lookup 1001``) is not the node's uplink.  On a real kernel the agent takes that
+    NIC -- dry run and real L2 start -- with a warning, and still refuses the NIC that carries the
+    main table's default route."""
+    r = netns.run_isolated(policy_routing_uplink=True)
+    assert r["default_route_links"] == [r["mgmt"]], r
+    assert any(x["table"] == 1001 and x["selective"] for x in r["rules"]), r["rules"]
+    assert [x["table"] for x in r["table_1001"]] == [1001]  # table ids above 255 are kept
+    assert r["dry_rail"]["rc"] == 0 and r["dry_rail"]["status"]["interfaces"][0]["name"] == "rail0", r["dry_rail"]
+    assert "rail0" not in (r["dry_rail"]["status"].get("excluded") or "")
+    assert "mgmt0: carries the node's default route (refused)" in r["dry_mgmt"]["status"]["excluded"], r["dry_mgmt"]
+    cr = r["configure_rail"]
+    assert cr["rc"] == 0 and cr["mtu"] == 9000, cr
+    assert "Interface 'rail0' has a default route in routing table 1001, which only selective rules reach" in cr["stderr"]
+    cm = r["configure_mgmt"]
+    assert cm["rc"] == 1 and "Refusing to configure mgmt0: the node's default route" in cm["stderr"]
+    assert cm["mtu"] == 1500 and cm["addrs"] == ["10.0.0.5/24"], cm
