@@ -630,6 +630,19 @@ def needs_node_cleanup(p: T.NetworkClusterPolicy) -> bool:
     return keeps_config(p) or disables_nm(p)
 
 
+def same_nics(p: T.NetworkClusterPolicy, q: T.NetworkClusterPolicy) -> bool:
+    """Whether q's agents take exactly the NICs p's agents configured on a node, and leave
+    NetworkManager as p's would (so q's agent, replacing p's config there, settles p's debt)."""
+    if p.spec.configurationType != q.spec.configurationType or (disables_nm(p) and not disables_nm(q)):
+        return False
+    if p.spec.configurationType == T.CONFIG_AMD_SCALE_OUT:
+        a, b = p.spec.amdScaleOut, q.spec.amdScaleOut
+        return (a.interfaces, a.nicDrivers) == (b.interfaces, b.nicDrivers)
+    a, b = p.spec.hostNic, q.spec.hostNic
+    return bool(a and b) and (a.interfaces, a.nicDrivers, a.includeGpuRails) == (b.interfaces, b.nicDrivers,
+                                                                                 b.includeGpuRails)
+
+
 def cleanup_job_name(policy: str, node: str) -> str:
     import hashlib
 
@@ -973,6 +986,29 @@ class NetworkClusterPolicyReconciler:
             self._cleanup_jobs_exist.discard(p.name)
         return pending
 
+    def _taken_over(self, p: T.NetworkClusterPolicy) -> Dict[str, str]:
+        """node -> another live policy of p's type whose agent runs there and takes the same NICs
+        (same_nics): it holds the node lock and replaces whatever p's agents left, so p owes that
+        node no cleanup Job (which would only wait for that lock and fail)."""
+        if self._list_policies is None or self._list_pods is None:
+            return {}
+        out: Dict[str, str] = {}
+        for q in self._list_policies():
+            md = q.get("metadata") or {}
+            if md.get("name") == p.name or md.get("deletionTimestamp"):
+                continue
+            try:
+                qp = T.NetworkClusterPolicy.from_dict(q)
+            except Exception:
+                continue
+            if not same_nics(p, qp):
+                continue
+            for pod in self._list_pods(md["name"]):
+                node = (pod.get("spec") or {}).get("nodeName")
+                if node:
+                    out.setdefault(node, md["name"])
+        return out
+
     async def _kept_nodes(self, raw: dict, p: T.NetworkClusterPolicy, ds: dict) -> tuple:
         """keepConfigOnRestart / disableNetworkManager bookkeeping: (status.keptNodes,
         requeue_after).  A node joins when an agent Pod runs there (ready or not: an agent that
@@ -986,9 +1022,15 @@ class NetworkClusterPolicyReconciler:
         kept = set(cur) | ((with_pod - {""}) if needs_node_cleanup(p) else set())
         now = self._clock()
         due, requeue_after = [], 0.0
+        taken = self._taken_over(p) if kept - with_pod else {}
         for node in sorted(kept):
             key = (p.name, node)
             if node in with_pod:
+                self._missing_since.pop(key, None)
+                continue
+            if node in taken:  # handed over (e.g. an older policy of the type holds it now)
+                log.info("Policy %s: node %s is taken over by policy %s; no cleanup owed", p.name, node, taken[node])
+                kept.discard(node)
                 self._missing_since.pop(key, None)
                 continue
             left = self._missing_since.setdefault(key, now) + KEPT_ORPHAN_GRACE_S - now
@@ -1039,7 +1081,8 @@ class NetworkClusterPolicyReconciler:
                     raise
         if self._list_pods is not None and self._list_pods(p.name):
             return Result(requeue_after=1.0)  # agents still exiting: a cleanup must not race them
-        pending = await self._run_cleanups(raw, p, list(p.status.keptNodes))
+        taken = self._taken_over(p)
+        pending = await self._run_cleanups(raw, p, [n for n in p.status.keptNodes if n not in taken])
         if pending:
             if sorted(pending) != sorted(p.status.keptNodes):
                 # Nodes whose cleanup finished leave the list now; the next pass deletes their

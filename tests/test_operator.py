@@ -1630,3 +1630,38 @@ def test_random_edits_converge_to_the_policies_the_cluster_asks_for(seed, gc_del
             await eventually(converged, timeout=20)
 
     run(body(), timeout=120)
+
+
+def test_a_node_taken_over_by_a_same_nic_policy_owes_no_cleanup(monkeypatch):
+    """A keepConfigOnRestart policy leaves a node, and another amd-so policy taking the same NICs
+    now runs its agent there (it was held off the node until then): that agent holds the node
+    lock and replaces the old configuration, so no cleanup Job is owed -- one would only wait for
+    the lock and fail.  A node nobody took still gets its Job."""
+    from network_operator_amd.operator import reconciler as R
+
+    monkeypatch.setattr(R, "KEPT_ORPHAN_GRACE_S", 0.3)
+    monkeypatch.setattr(R, "CLEANUP_POLL_S", 0.05)
+
+    async def body():
+        async with cluster(openshift=False, agent_ready_delay=0.01) as (fake, client, ctl):
+            fake.add_node("n0", {"foo": "bar", "rack": "a"})
+            fake.add_node("n1", {"foo": "bar", "rack": "b"})
+            fake.add_node("n2", {"foo": "bar", "rack": "c"})
+            keep = T.new_policy("a-keep", layer="L3", node_selector={"foo": "bar"}, keepConfigOnRestart=True).to_dict()
+            await client.create(kube.NETWORKCLUSTERPOLICIES, keep)
+            await client.create(kube.NETWORKCLUSTERPOLICIES,
+                                T.new_policy("b-plain", layer="L3", node_selector={"rack": "a"}).to_dict())
+
+            def pol(name):
+                return fake.get_object(kube.NETWORKCLUSTERPOLICIES, name)
+            await eventually(lambda: pol("a-keep")["status"].get("keptNodes") == ["n0", "n1", "n2"])
+            await eventually(lambda: pol("b-plain")["status"]["targets"] == 0)  # held off n0
+            # a-keep leaves n0 (b-plain takes it) and n2 (nobody does)
+            await edit(client, "a-keep", lambda cur: cur["spec"].update(nodeSelector={"foo": "bar", "rack": "b"}))
+            await eventually(lambda: pol("b-plain")["status"]["targets"] == 1)
+            job = await value(lambda: next(iter(fake.list_objects(kube.JOBS)), None), timeout=5)
+            assert job["spec"]["template"]["spec"]["nodeName"] == "n2"
+            await eventually(lambda: pol("a-keep")["status"].get("keptNodes") == ["n1", "n2"])
+            await asyncio.sleep(0.5)  # past the grace period: still no Job for n0
+            assert [j["spec"]["template"]["spec"]["nodeName"] for j in fake.list_objects(kube.JOBS)] == ["n2"]
+    run(body())
