@@ -468,6 +468,9 @@ CONFLICT_MARK = ": also selected by policy "
 # every node an older one selects.
 HELD_EVERYWHERE_KEY = "network.amd.com/held-off-by-an-older-policy"
 MAX_HOLD_OFF_TERMS = 64  # required terms are ORed: the hold-off expands to at most this many
+# While an older selector overlaps, the held-off nodes are read again this often: a node
+# relabelled into or out of the overlap moves no Pod of this policy, so no event would.
+HELD_OFF_REFRESH_S = 30.0
 
 
 def hold_off_terms(mine: Dict[str, str], older: List[Dict[str, str]]) -> Optional[List[dict]]:
@@ -848,13 +851,13 @@ class NetworkClusterPolicyReconciler:
             errs = errs[:limit] + [f"... and {len(errs) - limit} more"]
         return errs, degraded, starting
 
-    async def _hold_off(self, p: T.NetworkClusterPolicy) -> Tuple[Optional[List[dict]], List[str]]:
+    async def _hold_off(self, p: T.NetworkClusterPolicy) -> Tuple[Optional[List[dict]], List[str], bool]:
         """(node-affinity terms that keep this policy's agents off the nodes older live policies of
-        its type select, status.errors naming those nodes).  Older: earlier creationTimestamp, the
+        its type select, status.errors naming those nodes, whether an older selector overlaps).  Older: earlier creationTimestamp, the
         name breaking a tie (the timestamps have seconds).  The nodes are read with one LIST per
         overlapping older policy, by the two selectors together, three names at most."""
         if self._list_policies is None:
-            return None, []
+            return None, [], False
         me = (p.metadata.get("creationTimestamp") or "", p.name)
         older: Dict[str, Dict[str, str]] = {}
         for q in self._list_policies():
@@ -874,10 +877,12 @@ class NetworkClusterPolicyReconciler:
             errors.append(f"shared nodes{CONFLICT_MARK}{', '.join(sorted(older))} ({p.spec.configurationType} too, "
                           f"created earlier) are not held off: {e}; this policy's agents there wait for the node lock "
                           f"and fail; narrow a nodeSelector")
+        overlapping = False
         for other in sorted(older):
             sel = older[other]
             if any(k in mine and mine[k] != v for k, v in sel.items()):
                 continue
+            overlapping = True
             both = ",".join(f"{k}={v}" for k, v in sorted({**sel, **mine}.items()))
             try:
                 lst = await self.client.list(kube.NODES, label_selector=both or None, limit=3)
@@ -888,7 +893,7 @@ class NetworkClusterPolicyReconciler:
             if names:
                 errors.append(held_off_error(p.spec.configurationType, names,
                                              bool((lst.get("metadata") or {}).get("continue")), other))
-        return terms, errors
+        return terms, errors, overlapping
 
     async def _delete_job(self, j: dict) -> None:
         try:
@@ -1251,7 +1256,7 @@ class NetworkClusterPolicyReconciler:
             if not is_already_exists(e):
                 log.error("unable to create role binding: %s", e)
 
-    async def _create_daemonset(self, raw: dict, p: T.NetworkClusterPolicy, hold: tuple = (None, [])) -> Result:
+    async def _create_daemonset(self, raw: dict, p: T.NetworkClusterPolicy, hold: tuple = (None, [], False)) -> Result:
         if p.spec.configurationType not in T.CONFIGURATION_TYPES:
             log.info("Unknown configuration type, this shouldn't happen! type=%s", p.spec.configurationType)
             raise ValueError(f"unknown configuration type {p.spec.configurationType!r}")
@@ -1273,10 +1278,10 @@ class NetworkClusterPolicyReconciler:
         await self._event(raw, "Normal", "DaemonSetCreated", f"Created DaemonSet {self.namespace}/{p.name}")
         if sa_name:
             await self._create_openshift_collateral(raw, sa_name)
-        return await self._update_status(raw, p, created, hold[1])
+        return await self._update_status(raw, p, created, hold[1], hold[2])
 
     # -- update ----------------------------------------------------------------------------------
-    async def _update(self, raw: dict, p: T.NetworkClusterPolicy, ds: dict, hold: tuple = (None, [])) -> Result:
+    async def _update(self, raw: dict, p: T.NetworkClusterPolicy, ds: dict, hold: tuple = (None, [], False)) -> Result:
         original = copy.deepcopy(ds)
         update_daemonset_for(ds, p, self.namespace, hold[0])
         if original["spec"]["template"]["spec"] != ds["spec"]["template"]["spec"] or \
@@ -1284,10 +1289,10 @@ class NetworkClusterPolicyReconciler:
             log.info("DS difference for %s", p.name)
             ds = await self.client.replace(kube.DAEMONSETS, ds)
             await self._event(raw, "Normal", "DaemonSetUpdated", f"Updated DaemonSet {self.namespace}/{p.name}")
-        return await self._update_status(raw, p, ds, hold[1])
+        return await self._update_status(raw, p, ds, hold[1], hold[2])
 
     async def _update_status(self, raw: dict, p: T.NetworkClusterPolicy, ds: dict,
-                             held_off: Optional[List[str]] = None) -> Result:
+                             held_off: Optional[List[str]] = None, overlapping: bool = False) -> Result:
         st = ds.get("status", {}) or {}
         targets = int(st.get("desiredNumberScheduled", 0) or 0)
         ready = int(st.get("numberReady", 0) or 0)
@@ -1309,6 +1314,8 @@ class NetworkClusterPolicyReconciler:
         kept, kept_requeue = await self._kept_nodes(raw, p, ds)
         if kept_requeue:
             requeue_after = min(requeue_after, kept_requeue) if requeue_after else kept_requeue
+        if overlapping:
+            requeue_after = min(requeue_after, HELD_OFF_REFRESH_S) if requeue_after else HELD_OFF_REFRESH_S
         if cur.state != new_state or cur.errors != errors or cur.keptNodes != kept:
             updated = True
         # Nodes still starting up are in status.errors (with their reason) and keep Ready False,
