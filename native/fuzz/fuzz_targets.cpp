@@ -5,7 +5,8 @@
 //   dbus      messages from the system bus peer
 //   portdesc  the switch's Port Description string (operator-configured, still untrusted), and
 //             the agent's --fw-lldp-state record (a hostPath file)
-//   netlink   RTM_NEWLINK payloads (kernel, but parsed with length arithmetic)
+//   netlink   RTM_NEWLINK / NEWROUTE / NEWRULE / NEWADDR / DCB / extended-ACK payloads (kernel,
+//             but parsed with length arithmetic)
 //   arp       ARP payloads from the switch port (--verify-peers) — untrusted, L2-adjacent
 //
 // Built by `make fuzz-native` with amdclang++ -fsanitize=fuzzer,address,undefined (one binary
@@ -95,6 +96,11 @@ extern "C" int LLVMFuzzerTestOneInput(const uint8_t* data, size_t size) {
     h->nlmsg_type = RTM_NEWROUTE;  // the same bytes as a route (rtmsg + attributes, RTA_MULTIPATH next hops)
     try {
         (void)nl::parse_route(h);
+    } catch (const std::exception&) {
+    }
+    h->nlmsg_type = RTM_NEWRULE;  // as a FIB rule (fib_rule_hdr + FRA_* attributes)
+    try {
+        (void)nl::parse_rule(h);
     } catch (const std::exception&) {
     }
     h->nlmsg_type = RTM_NEWADDR;  // as an address (ifaddrmsg + attributes, IPv4 or IPv6)

@@ -224,6 +224,11 @@ RouteInfo parse_route(const nlmsghdr* h);
 // Parses an RTM_NEWADDR payload: IPv4 fields, or for AF_INET6 the address in text form
 // (address6).  Bounds-checked like parse_link.
 AddrInfo parse_addr(const nlmsghdr* h);
+// Parses an RTM_NEWRULE payload (struct fib_rule_hdr + FRA_* attributes): table (FRA_TABLE
+// over the header's), priority, protocol, action, the IPv4 source, and whether any selector is
+// present (RuleSpec::selective).  nullopt when the message is too short.  Bounds-checked like
+// parse_link.
+std::optional<RuleSpec> parse_rule(const nlmsghdr* h);
 // IFLA_STATS64 (else IFLA_STATS) of an RTM_NEWLINK message; nullopt when it carries neither.
 std::optional<LinkStats> parse_link_stats(const nlmsghdr* h);
 // The NLMSGERR_ATTR_MSG string of an extended ACK (NLMSG_ERROR with NLM_F_ACK_TLVS); "" if

@@ -759,6 +759,51 @@ void Rtnl::rule_add(const RuleSpec& r) { rule_request(RTM_NEWRULE, NLM_F_CREATE 
 
 void Rtnl::rule_del(const RuleSpec& r) { rule_request(RTM_DELRULE, 0, r); }
 
+std::optional<RuleSpec> parse_rule(const nlmsghdr* h) {
+    if (h->nlmsg_len < NLMSG_LENGTH(sizeof(FibRuleHdr))) return std::nullopt;
+    const auto* f = reinterpret_cast<const FibRuleHdr*>(NLMSG_DATA(h));
+    RuleSpec r;
+    r.src.len = f->src_len;
+    r.table = f->table;
+    r.action = f->action;
+    r.selective = f->src_len || f->dst_len || f->tos || (f->flags & kFibRuleInvert);
+    const auto* first = reinterpret_cast<const rtattr*>(reinterpret_cast<const char*>(f) + NLMSG_ALIGN(sizeof(FibRuleHdr)));
+    const size_t len = h->nlmsg_len - NLMSG_LENGTH(NLMSG_ALIGN(sizeof(FibRuleHdr)));
+    for_each_attr(first, len, [&](const rtattr* a) {
+        switch (a->rta_type) {
+            case kFraSrc:
+                if (f->family == AF_INET && RTA_PAYLOAD(a) == 4) r.src.addr = Ipv4::from_net(RTA_DATA(a));
+                break;
+            case kFraPriority:
+                if (RTA_PAYLOAD(a) >= 4) std::memcpy(&r.priority, RTA_DATA(a), 4);
+                break;
+            case kFraTable:
+                if (RTA_PAYLOAD(a) >= 4) std::memcpy(&r.table, RTA_DATA(a), 4);
+                break;
+            case kFraProtocol:
+                if (RTA_PAYLOAD(a) >= 1) r.protocol = *static_cast<const uint8_t*>(RTA_DATA(a));
+                break;
+            case kFraFwmark: {
+                uint32_t mark = 0;
+                if (RTA_PAYLOAD(a) >= 4) std::memcpy(&mark, RTA_DATA(a), 4);
+                if (mark) r.selective = true;
+                break;
+            }
+            case kFraDst:
+            case kFraIifname:
+            case kFraOifname:
+            case kFraL3mdev:
+            case kFraUidRange:
+            case kFraIpProto:
+            case kFraSportRange:
+            case kFraDportRange:
+                r.selective = true;
+                break;
+        }
+    });
+    return r;
+}
+
 std::vector<RuleSpec> Rtnl::dump_rules(uint8_t family) {
     Msg m(RTM_GETRULE, 0);
     FibRuleHdr frh{};
@@ -766,47 +811,8 @@ std::vector<RuleSpec> Rtnl::dump_rules(uint8_t family) {
     m.put(frh);
     std::vector<RuleSpec> out;
     dump(m, [&](const nlmsghdr* h) {
-        if (h->nlmsg_type != RTM_NEWRULE || h->nlmsg_len < NLMSG_LENGTH(sizeof(FibRuleHdr))) return;
-        const auto* f = reinterpret_cast<const FibRuleHdr*>(NLMSG_DATA(h));
-        RuleSpec r;
-        r.src.len = f->src_len;
-        r.table = f->table;
-        r.action = f->action;
-        r.selective = f->src_len || f->dst_len || f->tos || (f->flags & kFibRuleInvert);
-        const auto* first = reinterpret_cast<const rtattr*>(reinterpret_cast<const char*>(f) + NLMSG_ALIGN(sizeof(FibRuleHdr)));
-        for_each_attr(first, h->nlmsg_len - NLMSG_LENGTH(NLMSG_ALIGN(sizeof(FibRuleHdr))), [&](const rtattr* a) {
-            switch (a->rta_type) {
-                case kFraSrc:
-                    if (family == AF_INET && RTA_PAYLOAD(a) == 4) r.src.addr = Ipv4::from_net(RTA_DATA(a));
-                    break;
-                case kFraPriority:
-                    if (RTA_PAYLOAD(a) >= 4) std::memcpy(&r.priority, RTA_DATA(a), 4);
-                    break;
-                case kFraTable:
-                    if (RTA_PAYLOAD(a) >= 4) std::memcpy(&r.table, RTA_DATA(a), 4);
-                    break;
-                case kFraProtocol:
-                    if (RTA_PAYLOAD(a) >= 1) r.protocol = *static_cast<const uint8_t*>(RTA_DATA(a));
-                    break;
-                case kFraFwmark: {
-                    uint32_t mark = 0;
-                    if (RTA_PAYLOAD(a) >= 4) std::memcpy(&mark, RTA_DATA(a), 4);
-                    if (mark) r.selective = true;
-                    break;
-                }
-                case kFraDst:
-                case kFraIifname:
-                case kFraOifname:
-                case kFraL3mdev:
-                case kFraUidRange:
-                case kFraIpProto:
-                case kFraSportRange:
-                case kFraDportRange:
-                    r.selective = true;
-                    break;
-            }
-        });
-        out.push_back(r);
+        if (h->nlmsg_type != RTM_NEWRULE) return;
+        if (auto r = parse_rule(h)) out.push_back(*r);
     });
     return out;
 }

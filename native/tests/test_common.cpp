@@ -162,3 +162,54 @@ TEST(netlink_parse_route_reads_multipath_next_hops_and_bounds_them) {
     auto r2 = netop::nl::parse_route(reinterpret_cast<nlmsghdr*>(bad.data()));
     CHECK(r2.nexthops == std::vector<int>({3}));
 }
+
+TEST(netlink_parse_rule_tells_selective_rules_from_lookup_everything) {
+    // `from all lookup main` selects nothing; a source prefix, an input interface or a non-zero
+    // fwmark make a rule selective (per-NIC policy routing); FRA_TABLE overrides the header's
+    // table (ids above 255); a truncated message is no rule.
+    struct Hdr {
+        uint8_t family, dst_len, src_len, tos, table, res1, res2, action;
+        uint32_t flags;
+    };
+    auto build = [](uint8_t src_len, std::vector<std::pair<uint16_t, std::vector<uint8_t>>> attrs) {
+        std::vector<uint8_t> m(NLMSG_LENGTH(sizeof(Hdr)), 0);
+        for (auto& [type, payload] : attrs) {
+            const size_t off = m.size();
+            m.resize(off + RTA_SPACE(payload.size()), 0);
+            auto* a = reinterpret_cast<rtattr*>(m.data() + off);
+            a->rta_type = type;
+            a->rta_len = uint16_t(RTA_LENGTH(payload.size()));
+            std::memcpy(RTA_DATA(a), payload.data(), payload.size());
+        }
+        auto* h = reinterpret_cast<nlmsghdr*>(m.data());
+        h->nlmsg_len = uint32_t(m.size());
+        h->nlmsg_type = RTM_NEWRULE;
+        auto* f = reinterpret_cast<Hdr*>(NLMSG_DATA(h));
+        f->family = AF_INET;
+        f->src_len = src_len;
+        f->table = RT_TABLE_MAIN;
+        f->action = 1;
+        return m;
+    };
+    auto u32 = [](uint32_t v) {
+        std::vector<uint8_t> b(4);
+        std::memcpy(b.data(), &v, 4);
+        return b;
+    };
+    auto parse = [](std::vector<uint8_t>& m) { return netop::nl::parse_rule(reinterpret_cast<nlmsghdr*>(m.data())); };
+    auto all = build(0, {{6, u32(32766)}});  // FRA_PRIORITY
+    auto r = parse(all);
+    CHECK(r && !r->selective && r->table == RT_TABLE_MAIN && r->priority == 32766 && r->action == 1);
+    auto from = build(24, {{2, {192, 168, 50, 0}}, {15, u32(1001)}});  // FRA_SRC, FRA_TABLE
+    r = parse(from);
+    CHECK(r && r->selective && r->table == 1001u && r->src.str() == "192.168.50.0/24");
+    auto iif = build(0, {{3, {'e', 't', 'h', '0', 0}}});  // FRA_IIFNAME
+    CHECK(parse(iif)->selective);
+    auto mark0 = build(0, {{10, u32(0)}});  // FRA_FWMARK 0: matches every packet
+    CHECK(!parse(mark0)->selective);
+    auto mark = build(0, {{10, u32(7)}});
+    CHECK(parse(mark)->selective);
+    std::vector<uint8_t> shortmsg(NLMSG_LENGTH(4), 0);
+    reinterpret_cast<nlmsghdr*>(shortmsg.data())->nlmsg_len = uint32_t(shortmsg.size());
+    CHECK(!parse(shortmsg));
+}
