@@ -422,6 +422,34 @@ def validate_update(policy: T.NetworkClusterPolicy, old: Optional[T.NetworkClust
     return validate_spec(policy.spec)
 
 
+def overlap_warnings(policy: T.NetworkClusterPolicy, others: List[dict]) -> List[str]:
+    """Admission warnings for the live policies of ``policy``'s configurationType whose
+    nodeSelector can match a node ``policy``'s matches too (no key required at two values).  A
+    node belongs to the older policy of a type (operator/reconciler.py hold_off_terms): the newer
+    one's agents are held off it.  ``policy`` without a creationTimestamp is being created, so it
+    is the newest.  Which nodes actually match both is the operator's to say (status.errors)."""
+    mine = dict(policy.spec.nodeSelector)
+    me = (policy.metadata.get("creationTimestamp") or "\uffff", policy.name)
+    out = []
+    for q in sorted(others, key=lambda o: (o.get("metadata") or {}).get("name", "")):
+        md = q.get("metadata") or {}
+        spec = q.get("spec") or {}
+        if md.get("name") == policy.name or md.get("deletionTimestamp") or \
+                spec.get("configurationType", "") != policy.spec.configurationType:
+            continue
+        sel = dict(spec.get("nodeSelector") or {})
+        if any(k in mine and mine[k] != v for k, v in sel.items()):
+            continue  # disjoint selections
+        older = (md.get("creationTimestamp") or "", md.get("name", "")) < me
+        if older:
+            out.append(f"policy {md['name']} ({policy.spec.configurationType} too, created earlier) can select the same "
+                       f"nodes: those stay with it, and this policy's agents are held off them")
+        else:
+            out.append(f"policy {md['name']} ({policy.spec.configurationType} too, created later) can select the same "
+                       f"nodes: they belong to this policy, and its agents are held off them")
+    return out
+
+
 def validate_delete(policy: T.NetworkClusterPolicy) -> List[str]:
     log.info("validate delete name=%s", policy.name)
     return []

@@ -267,7 +267,7 @@ class ApiClient:
 
     async def list(self, res: Resource, namespace: Optional[str] = None, label_selector: Optional[str] = None,
                    field_selector: Optional[str] = None, resource_version: Optional[str] = None,
-                   limit: int = 0, continue_: str = "") -> dict:
+                   limit: int = 0, continue_: str = "", timeout: Optional[float] = None) -> dict:
         params = {}
         if limit:
             params["limit"] = str(limit)
@@ -279,7 +279,7 @@ class ApiClient:
             params["fieldSelector"] = field_selector
         if resource_version is not None:
             params["resourceVersion"] = resource_version
-        return await self.request("GET", res.path(namespace), params=params or None)
+        return await self.request("GET", res.path(namespace), params=params or None, timeout=timeout)
 
     async def create(self, res: Resource, obj: dict, namespace: Optional[str] = None,
                      timeout: Optional[float] = None) -> dict:

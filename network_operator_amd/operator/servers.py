@@ -21,10 +21,11 @@ import ssl
 import subprocess
 import time
 from pathlib import Path
-from typing import Callable, Dict, Optional, Tuple
+from typing import Callable, Dict, List, Optional, Tuple
 
 from aiohttp import web
 
+from ..api.v1alpha1 import types as T
 from ..api.v1alpha1 import webhook as W
 from . import kube
 from .kube import ApiClient
@@ -186,8 +187,24 @@ class Servers:
         app.router.add_get("/metrics", metrics)
         return app
 
-    @staticmethod
-    def webhook_app() -> web.Application:
+    OVERLAP_LIST_TIMEOUT_S = 2.0  # inside the API server's webhook timeout (10 s); warnings only
+
+    async def overlap_warnings(self, review: dict) -> List[str]:
+        """An admitted CREATE / UPDATE of a policy whose selector overlaps another live policy of
+        its type gets a warning naming it (kubectl prints it).  Best effort: without a client, or
+        if the LIST fails or is slow, no warning -- admission never depends on it."""
+        req = review.get("request") or {}
+        if self.client is None or req.get("operation") not in ("CREATE", "UPDATE"):
+            return []
+        try:
+            pol = T.NetworkClusterPolicy.from_dict(req.get("object") or {})
+            lst = await self.client.list(kube.NETWORKCLUSTERPOLICIES, timeout=self.OVERLAP_LIST_TIMEOUT_S)
+        except Exception as e:
+            log.debug("overlap check skipped: %s", e)
+            return []
+        return W.overlap_warnings(pol, lst.get("items") or [])
+
+    def webhook_app(self) -> web.Application:
         app = web.Application()
 
         def handler(mutate: bool):
@@ -196,7 +213,13 @@ class Servers:
                     review = await req.json()
                 except json.JSONDecodeError:
                     return web.Response(status=400, text="bad AdmissionReview")
-                return web.json_response(W.admission_review(review, mutate))
+                out = W.admission_review(review, mutate)
+                resp = out.get("response") or {}
+                if not mutate and resp.get("allowed"):
+                    extra = await self.overlap_warnings(review)
+                    if extra:
+                        resp["warnings"] = list(resp.get("warnings") or []) + extra
+                return web.json_response(out)
             return h
 
         app.router.add_post(W.MUTATE_PATH, handler(True))

@@ -408,3 +408,61 @@ def test_leader_election_flags_need_a_stop_margin(timings, ok):
                                       f"--leader-elect-renew-deadline={timings[1]}",
                                       f"--leader-elect-retry-period={timings[2]}"])
         assert asyncio.run(body()) == 1
+
+
+def test_admission_warns_about_a_policy_of_the_same_type_on_the_same_nodes(tmp_path):
+    """The validating webhook (Servers) adds a warning -- kubectl prints it -- when an admitted
+    policy's selector can match nodes an older live policy of its type selects: those nodes stay
+    with the older one, and the newer one's agents are held off them.  Another type, a disjoint
+    selector or a deleting policy gives none; without the API, no warning and still admitted."""
+    from network_operator_amd.api.v1alpha1 import webhook as W
+    from network_operator_amd.operator.metrics import OperatorMetrics
+    from network_operator_amd.operator.servers import Servers, generate_self_signed
+
+    generate_self_signed(tmp_path)
+
+    async def body():
+        fake = FakeApiServer()
+        url = await fake.start()
+        P = kube.NETWORKCLUSTERPOLICIES
+        fake._create(P, T.new_policy("old-a", node_selector={"rack": "a"}).to_dict(), None)
+        fake._create(P, T.new_policy("old-b", node_selector={"rack": "b"}).to_dict(), None)
+        fake._create(P, T.new_host_nic_policy("hosts", node_selector={"rack": "a"}).to_dict(), None)
+        client = ApiClient(KubeConfig(host=url))
+        s = Servers(OperatorMetrics(), client=client)
+        await s.start(probe_addr="0", webhook_port=0, cert_dir=str(tmp_path))
+        ctx = ssl.create_default_context()
+        ctx.check_hostname = False
+        ctx.verify_mode = ssl.CERT_NONE
+
+        async def admit(obj, op="CREATE", port=None):
+            review = {"apiVersion": "admission.k8s.io/v1", "kind": "AdmissionReview",
+                      "request": {"uid": "u1", "operation": op, "object": obj}}
+            async with aiohttp.ClientSession() as sess:
+                async with sess.post(f"https://127.0.0.1:{port or s.ports['webhook']}{W.VALIDATE_PATH}", json=review,
+                                     ssl=ctx) as r:
+                    return (await r.json())["response"]
+        r = await admit(T.new_policy("new", node_selector={"rack": "a", "gpu": "yes"}).to_dict())
+        assert r["allowed"] and r["warnings"] == [
+            "policy old-a (amd-so too, created earlier) can select the same nodes: those stay with it, and this "
+            "policy's agents are held off them"]
+        r = await admit(T.new_policy("new", node_selector={"rack": "c"}).to_dict())
+        assert r["allowed"] and "warnings" not in r
+        # an update of the older policy names the newer one it holds nodes against
+        old_a = fake.get_object(P, "old-a")
+        fake._create(P, T.new_policy("zz-later", node_selector={"rack": "a"}).to_dict(), None)
+        r = await admit(old_a, op="UPDATE")
+        assert r["warnings"] == ["policy zz-later (amd-so too, created later) can select the same nodes: they belong "
+                                 "to this policy, and its agents are held off them"]
+        await s.stop()
+        await client.close()
+        await fake.stop()
+        # no API server reachable: admitted, no overlap warning
+        s2 = Servers(OperatorMetrics(), client=ApiClient(KubeConfig(host="http://127.0.0.1:1")))
+        await s2.start(probe_addr="0", webhook_port=0, cert_dir=str(tmp_path))
+        r = await admit(T.new_policy("new", node_selector={"rack": "a"}).to_dict(), port=s2.ports["webhook"])
+        assert r["allowed"] and "warnings" not in r
+        await s2.stop()
+        await s2.client.close()
+
+    asyncio.run(asyncio.wait_for(body(), 60))
