@@ -311,6 +311,18 @@ void Agent::diagnose_silent() {
             NLOG_W("%s: %s", n.ifname.c_str(), n.lldp_silent.c_str());
             continue;
         }
+        // Admin-up without a carrier for the whole wait: no frame could come, whoever runs LLDP.
+        bool carrier = n.link.lower_up();
+        try {
+            carrier = ops_.link_by_name(n.ifname).lower_up();
+        } catch (const std::exception&) {
+        }
+        if (!carrier) {
+            n.lldp_silent = strfmt("%s: no carrier in %s (check the cable, the switch port and the optic)", drv.c_str(),
+                                   waited.c_str());
+            NLOG_W("%s: %s", n.ifname.c_str(), n.lldp_silent.c_str());
+            continue;
+        }
         std::optional<uint64_t> rx;
         try {
             if (n.rx_at_listen)

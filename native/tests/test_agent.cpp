@@ -326,6 +326,22 @@ TEST(agent_silent_nics_are_diagnosed_in_the_error_status_and_metrics) {
     CHECK(m.find("netop_agent_lldp_silent{nic=\"ens2\",driver=\"\"} 1") != std::string::npos);
     CHECK(m.find("netop_agent_lldp_silent{nic=\"ens0\",driver=\"\"} 0") != std::string::npos);
 
+    // L3 on a NIC that never got a carrier: no frame could arrive, and the reason says so.
+    Fixture d;
+    d.cfg.wait_ns = 1000000;
+    d.ops.no_carrier = {"ens2"};
+    auto sd = d.all_valid();
+    sd->frames.erase("ens2");
+    agent::Agent ad(d.cfg, d.ops, std::move(sd), d.nm());
+    std::string derr;
+    try {
+        ad.run(-1);
+    } catch (const agent::AgentError& e) {
+        derr = e.what();
+    }
+    CHECK(derr.find("ens2 (unknown driver: no carrier in 1ms (check the cable, the switch port and the optic))") !=
+          std::string::npos);
+
     // Frames that do not decode, and an i40e NIC (a known firmware-LLDP switch exists).
     Fixture g;
     g.cfg.wait_ns = 1000000;
