@@ -184,6 +184,10 @@ struct Config {
     // rather than as an error.
     bool check_peer_mtu = true;
     int64_t node_lock_wait_ns = 60LL * 1000000000;
+    // host-nic with nothing of its own to configure: how often the idle agent looks again (a NIC
+    // freed by the node, a driver loaded late); it then exits so its restart configures the NIC.
+    // 0 = never.
+    int64_t rediscover_ns = 30LL * 1000000000;
 };
 
 // Where the agent leaves the one-line reason the node is not ready (beside --status-file), and
@@ -292,7 +296,10 @@ class Agent {
     void post_cleanups();
     void cleanup_node();                    // --cleanup
     std::map<std::string, Ipv4Prefix> cached_addresses() const;  // --keep-config: addresses to adopt
-    std::vector<std::string> collect_interfaces();
+    std::vector<std::string> collect_interfaces(bool quiet = false);
+    // host-nic, nothing of its own: waits for SIGTERM, looking again every rediscover_ns.  True
+    // when a NIC of its own has appeared (the caller exits; the restart configures it).
+    bool idle_until_own_nic(int stop_fd);
     void get_network_configs(const std::vector<std::string>& names);
     void detect_lldp(int stop_fd);
     void diagnose_silent();            // after --wait expired: why each silent NIC heard nothing

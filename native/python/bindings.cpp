@@ -166,6 +166,16 @@ PYBIND11_MODULE(_netop_native, m) {
             if (!p) throw py::value_error("bad CIDR");
             r.addr_add(ifindex, *p);
         })
+        .def("addr_del", [](nl::Rtnl& r, int ifindex, const std::string& cidr) {
+            auto p = Ipv4Prefix::parse(cidr);
+            if (!p) throw py::value_error("bad CIDR");
+            for (const auto& a : r.addr_list(ifindex, AF_INET))
+                if (a.local == p->addr && a.prefixlen == p->len) {
+                    r.addr_del(a);
+                    return;
+                }
+            throw py::value_error("no such address");
+        })
         .def("rule_list", [](nl::Rtnl& r) {
             py::list l;
             for (auto& x : r.rule_list()) {

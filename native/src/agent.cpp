@@ -366,11 +366,12 @@ void Agent::restore_network_manager() {
     }
 }
 
-std::vector<std::string> Agent::collect_interfaces() {
+std::vector<std::string> Agent::collect_interfaces(bool quiet) {
     std::string root = cfg_.sysfs_root.empty() ? topo::sysfs_root() : cfg_.sysfs_root;
     disc_ = topo::discover(cfg_.discovery, root);
     excluded_ = disc_.excluded;
-    for (const auto& [name, why] : disc_.excluded) NLOG_I("Leaving '%s' alone: %s", name.c_str(), why.c_str());
+    if (!quiet)
+        for (const auto& [name, why] : disc_.excluded) NLOG_I("Leaving '%s' alone: %s", name.c_str(), why.c_str());
     if (cfg_.discovery.mode == topo::DiscoveryMode::Rdma) {
         // Host RDMA NICs: never the node's own management / frontend NICs.  A NIC --interfaces
         // names explicitly is the operator's choice (below), except for the default route.
@@ -387,13 +388,14 @@ std::vector<std::string> Agent::collect_interfaces() {
                 kept.push_back(name);
                 continue;
             }
-            NLOG_I("Leaving '%s' alone: it %s", name.c_str(), why.c_str());
+            if (!quiet) NLOG_I("Leaving '%s' alone: it %s", name.c_str(), why.c_str());
             excluded_.emplace_back(name, "the node's own NIC: it " + why);
         }
         disc_.ifnames = kept;
     }
     std::vector<std::string> names = disc_.ifnames;
     for (auto& p : disc_.pairs) {
+        if (quiet) break;
         const auto& g = disc_.gpus[size_t(p.gpu)];
         const auto& n = disc_.nics[size_t(p.nic)];
         NLOG_I("GPU %d (%s) <-> NIC %s (%s, %s, path %s)", g.index, g.pci.bdf.c_str(), n.ifname.c_str(), n.pci.bdf.c_str(),
@@ -1348,7 +1350,8 @@ void Agent::run(int stop_fd) {
         NLOG_W("Nothing to configure: %s", config_error_.c_str());
         mark("discover");
         write_status();
-        idle(stop_fd);
+        if (idle_until_own_nic(stop_fd))
+            NLOG_I("Exiting so that the restarted agent configures it");  // restartPolicy Always
         return;
     }
     if (names.empty()) {
@@ -1577,6 +1580,44 @@ void Agent::run(int stop_fd) {
         idle(stop_fd);  // reference behaviour
     }
     post_cleanups();
+}
+
+bool Agent::idle_until_own_nic(int stop_fd) {
+    if (cfg_.rediscover_ns <= 0) {
+        idle(stop_fd);
+        return false;
+    }
+    for (;;) {
+        for (int64_t until = mono_ns() + cfg_.rediscover_ns; mono_ns() < until;) {
+            if (fd_readable(stop_fd)) return false;
+            const int64_t left_ms = std::max<int64_t>(1, (until - mono_ns()) / 1000000);
+            if (stop_fd >= 0) {
+                pollfd p{stop_fd, POLLIN, 0};
+                ::poll(&p, 1, int(std::min<int64_t>(left_ms, 1000)));
+            } else {
+                ::usleep(useconds_t(std::min<int64_t>(left_ms, 1000) * 1000));
+            }
+        }
+        uplinks_read_ = false;  // the node's routes may have changed too
+        std::vector<std::string> names;
+        try {
+            names = collect_interfaces(true);
+        } catch (const std::exception& e) {
+            NLOG_V(2, "re-discovery failed: %s", e.what());
+            continue;
+        }
+        if (!names.empty()) {
+            NLOG_I("Interface(s) of its own appeared: %s", join(names, ", ").c_str());
+            return true;
+        }
+        std::vector<std::string> parts;
+        for (const auto& [n, why] : excluded_) parts.push_back(n + ": " + why);
+        const std::string why = "no host NIC of its own (left alone: " + join(parts, "; ") + ")";
+        if (why != config_error_) {  // what the node holds changed: the probe's reason follows
+            config_error_ = why;
+            write_status();
+        }
+    }
 }
 
 void Agent::idle(int stop_fd) {

@@ -80,6 +80,7 @@ int main(int argc, char** argv) {
     fs.add_bool("cleanup", &cfg.cleanup, "one-shot: remove what --keep-config agents left on the node (IPv4 addresses of the discovered NICs, tagged rail rules and routes, label, artifacts, LLDP cache, networkd files) and exit");
     std::string node_lock = "auto";
     fs.add_string("node-lock", &node_lock, "node-wide lock (abstract unix socket) held while the agent runs, so agents configuring the same NICs never overlap (exiting vs starting agent, agent vs --cleanup, two policies on one node): auto (named after --nfd-label-file), none, or a name");
+    fs.add_duration("rediscover-interval", &cfg.rediscover_ns, "host-nic discovery that left every NIC to the node or to amd-so: how often the idle agent looks again; when a NIC of its own appears it exits so that its restart configures it (0 = never)");
     fs.add_duration("node-lock-wait", &cfg.node_lock_wait_ns, "how long to wait for the node lock (and each NIC lock) before failing");
     cfg.nic_locks = true;
     fs.add_bool("nic-lock", &cfg.nic_locks, "hold a node-wide lock per configured NIC (abstract unix socket netop-nic:<ifname>) so two agents, whatever their policies and label files, never configure one NIC");

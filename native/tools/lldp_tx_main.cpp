@@ -52,6 +52,9 @@ int main(int argc, char** argv) {
         if (eq == std::string::npos) throw std::invalid_argument("--port wants IFNAME=PORT_DESCRIPTION");
         ports.emplace_back(v.substr(0, eq), v.substr(eq + 1));
     }, "IFNAME=PORT_DESCRIPTION (repeatable)");
+    std::vector<std::string> silent;
+    fs.add_func("silent-port", true, [&](const std::string& v) { silent.push_back(v); },
+                "IFNAME: a port that is up (the NIC has carrier) but never transmits LLDP (repeatable)");
     fs.add_duration("interval", &interval, "msgTxInterval");
     fs.add_string("phase", &phase, "first periodic frame: random (U[0,interval)) or zero");
     fs.add_bool("fast-start", &fast_start, "802.1AB-2009 fast transmission on new neighbours");
@@ -78,7 +81,7 @@ int main(int argc, char** argv) {
         return 2;
     }
     log::set_verbosity(verbosity);
-    if (ports.empty()) {
+    if (ports.empty() && silent.empty()) {
         std::fprintf(stderr, "Error: no --port given\n");
         return 2;
     }
@@ -128,6 +131,10 @@ int main(int argc, char** argv) {
     try {
         rtnl_holder = std::make_unique<nl::Rtnl>();
         nl::Rtnl& rtnl = *rtnl_holder;
+        for (const auto& ifname : silent) {
+            auto link = rtnl.link_by_name(ifname);
+            if (!link.up()) rtnl.link_set_up(link.index);
+        }
         int64_t now = mono_ns();
         for (auto& [ifname, desc] : ports) {
             Port p;

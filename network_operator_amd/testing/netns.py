@@ -232,7 +232,8 @@ class SyntheticSwitch:
             self.args.append(f"--port-system-name={sp}={name}")
         for i, (sp, p) in enumerate(zip(self.ports, plan)):
             if i >= len(plan) - silent_nics:
-                continue  # switch port that never sends LLDP
+                self.args.append(f"--silent-port={sp}")  # up (carrier) but never sends LLDP
+                continue
             self.args.append(f"--port={sp}={p['desc']}")
         self.pid = 0
         self.first_periodic: dict = {}  # port -> seconds (switch clock) of its first periodic frame
@@ -241,7 +242,7 @@ class SyntheticSwitch:
     def start(self, rt) -> float:
         """Creates the veth pairs (node ends keep the NIC names) and starts the switch; returns the
         monotonic time at which the switch got its ports."""
-        has_ports = any(a.startswith("--port=") for a in self.args)
+        has_ports = any(a.startswith(("--port=", "--silent-port=")) for a in self.args)
         libc = ctypes.CDLL(ctypes.util.find_library("c"), use_errno=True)
         r1, w1 = os.pipe()
         r2, w2 = os.pipe()
@@ -716,7 +717,8 @@ MGMT_NIC, HOST_NIC = "ens9np0", "ens49np1"  # the fixture node's two NICs on the
 
 
 def run_host_nic_ownership(mode: str = "L2", rails: int = 8, mgmt_bridge: bool = False,
-                           include_gpu_rails: bool = False, host_nic_addr: str = "") -> dict:
+                           include_gpu_rails: bool = False, host_nic_addr: str = "",
+                           free_host_nic: bool = False) -> dict:
     """A default ``host-nic`` policy's agent (rdma discovery, the default driver list) on the
     captured MI355X node, where every NIC is mlx5 with an RDMA device:
 
@@ -732,8 +734,9 @@ def run_host_nic_ownership(mode: str = "L2", rails: int = 8, mgmt_bridge: bool =
     ``include_gpu_rails`` the agent runs as ``hostNic.includeGpuRails`` makes it (a node without
     amd-so): it takes the rails too, never the management NIC.  With ``host_nic_addr`` the
     second NIC is the node's own too (e.g. its storage network, that address /24): nothing is
-    left for the agent, which must stay up unlabelled and say why (``idle``).  Must run inside
-    ``unshare -rn``."""
+    left for the agent, which must stay up unlabelled and say why (``idle``).  With
+    ``free_host_nic`` that address is then removed: the idle agent, looking again every 300 ms,
+    must exit so that its restart configures the NIC.  Must run inside ``unshare -rn``."""
     from . import fakesysfs
     from ..utils.paths import native_bin
 
@@ -789,6 +792,8 @@ def run_host_nic_ownership(mode: str = "L2", rails: int = 8, mgmt_bridge: bool =
         log_path = tmp / "agent.log"
         with open(log_path, "w") as logf:
             extra = ["--rdma-include-gpu-rails"] if include_gpu_rails else []
+            if host_nic_addr:
+                extra.append("--rediscover-interval=300ms")
             agent = subprocess.Popen([*base, "--nic-discovery=rdma", *extra, f"--status-file={tmp / 'status.json'}"],
                                      env=env, stdout=logf, stderr=subprocess.STDOUT)
         if host_nic_addr:
@@ -801,6 +806,17 @@ def run_host_nic_ownership(mode: str = "L2", rails: int = 8, mgmt_bridge: bool =
                                  "--nfd-label-file=host-nic-readiness.txt", f"--status-file={tmp / 'status.json'}"],
                                 capture_output=True, text=True, timeout=10)
             res["idle"]["ready_check"] = {"rc": pr.returncode, "stdout": pr.stdout.strip()}
+            if free_host_nic:
+                # The node gives the storage NIC up: the idle agent must notice and exit (rc 0),
+                # so that the kubelet's restart configures it.
+                rt.addr_del(rt.link_by_name(HOST_NIC)["index"], host_nic_addr)
+                t_free = time.monotonic()
+                try:
+                    agent.wait(timeout=5)
+                except subprocess.TimeoutExpired:
+                    pass
+                res["idle"]["after_free"] = {"exited": agent.poll() is not None, "rc": agent.poll(),
+                                             "seconds": round(time.monotonic() - t_free, 3)}
         t_ready = _wait_for(label, 0.0 if host_nic_addr else 15, agent)
         res["ready"] = t_ready is not None
         res["label"] = label.read_text() if label.exists() else None

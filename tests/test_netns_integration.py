@@ -515,3 +515,15 @@ def test_per_nic_policy_routing_default_is_not_the_node_uplink():
     cm = r["configure_mgmt"]
     assert cm["rc"] == 1 and "Refusing to configure mgmt0: the node's default route" in cm["stderr"]
     assert cm["mtu"] == 1500 and cm["addrs"] == ["10.0.0.5/24"], cm
+
+
+def test_idle_host_nic_agent_exits_when_a_nic_of_its_own_appears():
+    """The idle host-nic agent looks again every --rediscover-interval: once the node gives the
+    storage NIC up (its address removed), the agent exits 0 within about one interval, so that
+    its restart (restartPolicy Always) configures the NIC instead of idling forever."""
+    r = netns.run_isolated(host_nic_ownership=True, host_nic_addr="10.9.8.7/24", free_host_nic=True)
+    idle = r["idle"]
+    assert idle["running"] and idle["reason"].startswith("no host NIC of its own"), r["agent_log"]
+    after = idle["after_free"]
+    assert after["exited"] and after["rc"] == 0 and after["seconds"] < 2.0, (after, r["agent_log"])
+    assert f"Interface(s) of its own appeared: {netns.HOST_NIC}" in r["agent_log"]
