@@ -1163,6 +1163,13 @@ std::string Agent::render_metrics() const {
     metric("netop_agent_nic_degraded", "gauge", "1 while the NIC has lost link after readiness");
     for (auto& n : nics_)
         o += strfmt("netop_agent_nic_degraded{nic=\"%s\"} %d\n", httpd::escape_label(n.ifname).c_str(), n.degraded ? 1 : 0);
+    if (cfg_.mode == "L2") {
+        metric("netop_agent_nic_carrier", "gauge",
+               "L2: the NIC's carrier state -- 1 up, 0.5 still training within --carrier-wait, 0 no carrier after it");
+        for (auto& n : nics_)
+            o += strfmt("netop_agent_nic_carrier{nic=\"%s\"} %s\n", httpd::escape_label(n.ifname).c_str(),
+                        n.awaiting_carrier ? "0.5" : (n.no_carrier || !n.link.lower_up()) ? "0" : "1");
+    }
     if (cfg_.min_link_speed_mbps > 0) {
         metric("netop_agent_nic_speed_mbps", "gauge", "Negotiated link speed of the NIC (checked against --min-link-speed-gbps)");
         for (const auto& n : nics_)

@@ -2571,9 +2571,10 @@ TEST(agent_l2_waits_for_carrier_and_labels_only_when_every_nic_has_a_link) {
     f.ops.links["ens1"].flags &= ~unsigned(IFF_LOWER_UP);
     Pipe stop;
     agent::Agent a(f.cfg, f.ops, std::make_unique<ScriptedLldp>(), f.nm());
-    bool unlabelled = false, reason = false, status = false, labelled = false;
+    bool unlabelled = false, reason = false, status = false, labelled = false, dark_metric = false, lit_metric = false;
     a.on_monitor_tick = [&](int tick) {
         if (tick == 1) {
+            dark_metric = a.render_metrics().find("netop_agent_nic_carrier{nic=\"ens1\"} 0\n") != std::string::npos;
             unlabelled = !path_exists(f.cfg.labels.path());
             auto why = read_file(agent::reason_path(f.cfg.status_file));
             reason = why && *why == "ens1: no carrier (check the cable, the switch port and the optic)\n";
@@ -2583,10 +2584,13 @@ TEST(agent_l2_waits_for_carrier_and_labels_only_when_every_nic_has_a_link) {
             f.ops.set_carrier("ens1", true);
         } else if (tick == 3) {
             labelled = path_exists(f.cfg.labels.path()) && !path_exists(agent::reason_path(f.cfg.status_file));
+            lit_metric = a.render_metrics().find("netop_agent_nic_carrier{nic=\"ens1\"} 1\n") != std::string::npos;
             stop.fire();
         }
     };
     a.run(stop.fd[0]);
+    CHECK(dark_metric);
+    CHECK(lit_metric);
     CHECK(unlabelled);
     CHECK(reason);
     CHECK(status);
