@@ -361,11 +361,21 @@ int netop_xgmi_probe(uint64_t bytes, int iters, int max_gpus, double* bw_single,
     hipError_t e = hipGetDeviceCount(&n);
     if (e != hipSuccess) return int(e);
     if (max_gpus > 0 && n > max_gpus) n = max_gpus;
+    if (n > 64) n = 64;  // the per-GPU tables below
     *n_out = n;
     *total_errors = 0;
     bytes &= ~uint64_t(15);
     if (n == 0 || bytes == 0 || iters < 1) return int(hipErrorInvalidValue);
 
+    // Every pair must be peer-accessible before any kernel reads a peer's memory: a pull over a
+    // pair without peer access would fault the GPU (and may reset the node), so refuse instead.
+    for (int d = 0; d < n; ++d)
+        for (int p = 0; p < n; ++p) {
+            if (p == d) continue;
+            int can = 0;
+            if ((e = hipDeviceCanAccessPeer(&can, d, p)) != hipSuccess) return int(e);
+            if (!can) return int(hipErrorPeerAccessUnsupported);
+        }
     void* src[64] = {};
     void* dst[64] = {};
     unsigned long long* err[64] = {};
@@ -373,13 +383,9 @@ int netop_xgmi_probe(uint64_t bytes, int iters, int max_gpus, double* bw_single,
         if ((e = hipSetDevice(d)) != hipSuccess) return int(e);
         for (int p = 0; p < n; ++p) {
             if (p == d) continue;
-            int can = 0;
-            hipDeviceCanAccessPeer(&can, d, p);
-            if (can) {
-                hipError_t pe = hipDeviceEnablePeerAccess(p, 0);
-                if (pe != hipSuccess && pe != hipErrorPeerAccessAlreadyEnabled) return int(pe);
-                (void)hipGetLastError();
-            }
+            hipError_t pe = hipDeviceEnablePeerAccess(p, 0);
+            if (pe != hipSuccess && pe != hipErrorPeerAccessAlreadyEnabled) return int(pe);
+            (void)hipGetLastError();
         }
         // Each dst needs one receive buffer per peer for the concurrent phase.
         if ((e = hipMalloc(&src[d], bytes)) != hipSuccess) return int(e);
