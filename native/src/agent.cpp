@@ -1284,7 +1284,9 @@ std::string Agent::not_ready_reason() const {
         else if (!n.peer_error.empty())
             why = n.peer_error;
         else if (cfg_.mode == "L3" && !n.configured)
-            why = n.lldp_seen ? "not configured yet" : "waiting for LLDP";
+            why = n.lldp_seen                           ? "not configured yet"
+                  : n.link.up() && !n.link.lower_up() ? "waiting for carrier"  // no frame can come yet
+                                                        : "waiting for LLDP";
         if (!why.empty()) parts.push_back(n.ifname + ": " + why);
     }
     return join(parts, "; ");

@@ -250,6 +250,7 @@ void Agent::detect_lldp(int stop_fd) {
     int rounds = 0;
     int64_t next_round = mono_ns();
     pkt::ListenResult r = pkt::ListenResult::Deadline;
+    bool status_written = false;
     for (;;) {
         if (cfg_.lldp_announce && rounds < cfg_.announce_count && mono_ns() >= next_round) {
             // Round 0: every NIC that can transmit.  Later rounds (1 s apart): every NIC still
@@ -265,15 +266,22 @@ void Agent::detect_lldp(int stop_fd) {
                                                : cfg_.announce_interval_ns;
             next_round = mono_ns() + step;
         }
+        if (!status_written) {  // after the first announcements are out: the probe's reason per NIC
+            status_written = true;  // ("waiting for carrier" / "waiting for LLDP") while we wait
+            write_status();
+        }
         const int64_t slice_end = cfg_.lldp_announce && rounds < cfg_.announce_count ? std::min(deadline, next_round) : deadline;
         r = lldp_->run(slice_end, cb, wait_fd);
         if (r == pkt::ListenResult::Interrupted && watcher && !fd_readable(stop_fd)) {
             for (auto& ev : watcher->wait(mono_ns())) {  // link events: announce on newly operational NICs
                 for (auto& n : nics_) {
                     if (n.link.index != ev.link.index || ev.deleted) continue;
+                    const bool had_carrier = n.link.lower_up();
                     n.link.flags = ev.link.flags;
                     n.link.operstate = ev.link.operstate;
                     if (!n.lldp_seen && announces[n.link.index] == 0 && can_tx(n)) announce_nic(n, false);
+                    // "waiting for carrier" -> "waiting for LLDP" (or back) in the probe's reason
+                    if (!n.lldp_seen && had_carrier != n.link.lower_up()) write_status();
                 }
             }
             if (mono_ns() >= deadline) {

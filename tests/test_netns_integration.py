@@ -527,3 +527,15 @@ def test_idle_host_nic_agent_exits_when_a_nic_of_its_own_appears():
     after = idle["after_free"]
     assert after["exited"] and after["rc"] == 0 and after["seconds"] < 2.0, (after, r["agent_log"])
     assert f"Interface(s) of its own appeared: {netns.HOST_NIC}" in r["agent_log"]
+
+
+def test_l3_reports_waiting_for_carrier_while_a_port_trains():
+    """L3: a switch port that comes up 2 s after the agent started.  While it trains, the probe's
+    reason for that NIC is "waiting for carrier" (no frame can come yet), a start-up reason like
+    "waiting for LLDP"; once the carrier is there the switch answers and the label follows."""
+    r = netns.run_isolated(n_nics=2, seed=44, mode="L3", interval="30s", dark_port=1, dark_port_up_after=2.0)
+    d = r["dark"]
+    dark_nic = r["nics"][1]
+    assert any(f"{dark_nic}: waiting for carrier" in x for x in d["reasons_seen"]), (d["reasons_seen"], r["agent_log"])
+    assert not any("no carrier" in x for x in d["reasons_seen"])
+    assert r["ready"] and d["port_up_to_label_s"] is not None and d["port_up_to_label_s"] < 1.5, r["agent_log"]
