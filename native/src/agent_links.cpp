@@ -250,7 +250,11 @@ void Agent::detect_lldp(int stop_fd) {
     int rounds = 0;
     int64_t next_round = mono_ns();
     pkt::ListenResult r = pkt::ListenResult::Deadline;
+    // The probe's per-NIC reason ("waiting for carrier" / "waiting for LLDP") once the wait has
+    // lasted 100 ms: a fast-start switch answers within a few ms, and writing the status then
+    // would sit on the node-ready critical path (~2 ms); the kubelet probes every 5 s anyway.
     bool status_written = false;
+    const int64_t status_at = mono_ns() + 100LL * 1000000;
     for (;;) {
         if (cfg_.lldp_announce && rounds < cfg_.announce_count && mono_ns() >= next_round) {
             // Round 0: every NIC that can transmit.  Later rounds (1 s apart): every NIC still
@@ -266,11 +270,12 @@ void Agent::detect_lldp(int stop_fd) {
                                                : cfg_.announce_interval_ns;
             next_round = mono_ns() + step;
         }
-        if (!status_written) {  // after the first announcements are out: the probe's reason per NIC
-            status_written = true;  // ("waiting for carrier" / "waiting for LLDP") while we wait
+        if (!status_written && mono_ns() >= status_at) {
+            status_written = true;
             write_status();
         }
-        const int64_t slice_end = cfg_.lldp_announce && rounds < cfg_.announce_count ? std::min(deadline, next_round) : deadline;
+        int64_t slice_end = cfg_.lldp_announce && rounds < cfg_.announce_count ? std::min(deadline, next_round) : deadline;
+        if (!status_written) slice_end = std::min(slice_end, status_at);
         r = lldp_->run(slice_end, cb, wait_fd);
         if (r == pkt::ListenResult::Interrupted && watcher && !fd_readable(stop_fd)) {
             for (auto& ev : watcher->wait(mono_ns())) {  // link events: announce on newly operational NICs
@@ -281,7 +286,7 @@ void Agent::detect_lldp(int stop_fd) {
                     n.link.operstate = ev.link.operstate;
                     if (!n.lldp_seen && announces[n.link.index] == 0 && can_tx(n)) announce_nic(n, false);
                     // "waiting for carrier" -> "waiting for LLDP" (or back) in the probe's reason
-                    if (!n.lldp_seen && had_carrier != n.link.lower_up()) write_status();
+                    if (status_written && !n.lldp_seen && had_carrier != n.link.lower_up()) write_status();
                 }
             }
             if (mono_ns() >= deadline) {
