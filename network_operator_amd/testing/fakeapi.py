@@ -175,6 +175,7 @@ class _Fault:
     status: int
     count: int
     reason: str = "InternalError"
+    user_agent: Optional[str] = None  # only this client's requests (None: everyone's)
 
 
 FOREGROUND_DELETION = "foregroundDeletion"
@@ -246,6 +247,7 @@ class FakeApiServer:
         self.node_last_exit: Dict[Tuple[str, str], dict] = {}
         self.tokens: Dict[str, dict] = {}                    # bearer -> {"username", "groups", "allowed"}
         self.faults: List[_Fault] = []
+        self.faults_fired = 0  # injected failures actually served
         # (method, path pattern, User-Agent or None, seconds): matching requests wait that long
         # before they are served (the client usually gives up first)
         self.stalls: List[tuple] = []
@@ -379,8 +381,8 @@ class FakeApiServer:
         self._store(kube.JOBS, new, "MODIFIED")
 
     def fail_next(self, method: str, path_regex: str, status: int = 500, count: int = 1,
-                  reason: str = "InternalError") -> None:
-        self.faults.append(_Fault(method.upper(), re.compile(path_regex), status, count, reason))
+                  reason: str = "InternalError", user_agent: Optional[str] = None) -> None:
+        self.faults.append(_Fault(method.upper(), re.compile(path_regex), status, count, reason, user_agent))
 
     def stall(self, method: str, path_regex: str, seconds: float, user_agent: Optional[str] = None) -> None:
         """Hold every matching request `seconds` before serving it, until clear_stalls()."""
@@ -789,10 +791,12 @@ class FakeApiServer:
                 except asyncio.TimeoutError:
                     pass
         for f in list(self.faults):
-            if f.method in (req.method, "*") and f.pattern.search(path):
+            if f.method in (req.method, "*") and f.pattern.search(path) and \
+                    f.user_agent in (None, req.headers.get("User-Agent")):
                 f.count -= 1
                 if f.count <= 0:
                     self.faults.remove(f)
+                self.faults_fired += 1
                 return _status(f.status, f.reason, "injected fault")
         try:
             if path == "/api":

@@ -58,17 +58,26 @@ async def value(fn, timeout=5.0):
     return out[-1]
 
 
+OPERATOR_UA = "amd-network-operator/0.1"
+
+
 @contextlib.asynccontextmanager
-async def cluster(openshift=True, workers=2, **fake_kw):
+async def cluster(openshift=True, workers=2, user_client=None, **fake_kw):
+    """A fake API server and a running controller.  The yielded client is the controller's own,
+    or with ``user_client`` a separate one with that User-Agent (faults can then target the
+    operator's requests alone)."""
     fake = FakeApiServer(openshift=openshift, **fake_kw)
     url = await fake.start()
-    client = ApiClient(KubeConfig(host=url))
+    client = ApiClient(KubeConfig(host=url), user_agent=OPERATOR_UA)
+    user = ApiClient(KubeConfig(host=url), user_agent=user_client) if user_client else client
     ctl = PolicyController(client, NS, is_openshift=openshift, workers=workers)
     await ctl.start()
     try:
-        yield fake, client, ctl
+        yield fake, user, ctl
     finally:
         await ctl.stop()
+        if user is not client:
+            await user.close()
         await client.close()
         await fake.stop()
 
@@ -1531,16 +1540,32 @@ def test_random_edits_converge_to_the_policies_the_cluster_asks_for(seed, gc_del
     tolerations, --mode) and a status that matches a model of the cluster: targets, ready, and a
     PolicyConflict entry for each older same-type policy it shares nodes with -- nothing left over
     from the states it passed through."""
+    _model_check(seed, gc_delay)
+
+
+@pytest.mark.parametrize("seed", [11, 12, 13, 14])
+def test_random_edits_converge_through_api_faults_and_lost_watches(seed):
+    """The same model check with a hostile API server: the operator's requests (only its own --
+    the user's edits go through) randomly fail with 500 / 503 / 429 / 409 on DaemonSet writes,
+    status writes, Events, policy writes and reads; its watches are dropped, and the API server's
+    event history is compacted so the informers' resume gets 410 Gone and must relist.  Once the
+    faults stop, the cluster converges to the same model."""
+    _model_check(seed, 0.0, chaos=True)
+
+
+def _model_check(seed, gc_delay, chaos=False):
     import random
 
     rng = random.Random(seed)
+    chaos_stats = {}
     taint = [{"key": "amd.com/gpu", "value": "present", "effect": "NoSchedule"}]
     tol = [{"key": "amd.com/gpu", "operator": "Exists", "effect": "NoSchedule"}]
     selectors = [{"rack": "a"}, {"rack": "b"}, {"gpu": "yes"}, {"rack": "a", "gpu": "yes"}]
 
     async def body():
         # agents turn ready 20 ms after their Pod is placed, on every DaemonSet the run makes
-        async with cluster(openshift=False, workers=3, gc_delay=gc_delay, agent_ready_delay=0.02) as (fake, client, ctl):
+        async with cluster(openshift=False, workers=3, gc_delay=gc_delay, agent_ready_delay=0.02,
+                           user_client="kubectl" if chaos else None) as (fake, client, ctl):
             nodes = {}
             for i in range(6):
                 labels = {"rack": rng.choice("ab"), **({"gpu": "yes"} if rng.random() < 0.5 else {})}
@@ -1588,8 +1613,28 @@ def test_random_edits_converge_to_the_policies_the_cluster_asks_for(seed, gc_del
                     if fake.get_object(kube.DAEMONSETS, name, NS) is not None:
                         with contextlib.suppress(ApiError):
                             await client.delete(kube.DAEMONSETS, name, NS)
+                if chaos and rng.random() < 0.35:
+                    c = rng.random()
+                    if c < 0.7:  # the operator's next requests of one kind fail
+                        method, path = rng.choice([("PUT", r"/daemonsets/"), ("POST", r"/daemonsets"),
+                                                   ("PUT", r"/networkclusterpolicies/[^/]+/status"),
+                                                   ("POST", r"/events"), ("PUT", r"/networkclusterpolicies/[^/]+$"),
+                                                   ("GET", r"/nodes"), ("DELETE", r"/")])
+                        status, reason = rng.choice([(500, "InternalError"), (503, "ServiceUnavailable"),
+                                                     (429, "TooManyRequests"), (409, "Conflict")])
+                        fake.fail_next(method, path, status=status, count=rng.randint(1, 3), reason=reason,
+                                       user_agent=OPERATOR_UA)
+                    elif c < 0.85:
+                        fake.drop_watches()  # connection loss: the informers re-watch
+                    else:
+                        fake.compact()  # etcd compaction: resuming gets 410 Gone, the informers relist
                 if rng.random() < 0.5:
                     await asyncio.sleep(rng.choice([0.0, 0.01, 0.05]))
+            if chaos:
+                await asyncio.sleep(0.2)  # let the queued faults meet the operator's requests
+                assert fake.faults_fired > 0
+                chaos_stats["fired"] = fake.faults_fired
+            fake.faults.clear()
 
             def placed(m):
                 _, _, sel, tols = m
@@ -1627,9 +1672,9 @@ def test_random_edits_converge_to_the_policies_the_cluster_asks_for(seed, gc_del
                     got = sorted(e.split(" also selected by policy ")[1].split(" ")[0] for e in s["errors"])
                     assert got == others and len(s["errors"]) == len(others), (name, s["errors"], others)
                 return True
-            await eventually(converged, timeout=20)
+            await eventually(converged, timeout=30 if chaos else 20)
 
-    run(body(), timeout=120)
+    run(body(), timeout=150)
 
 
 def test_a_node_taken_over_by_a_same_nic_policy_owes_no_cleanup(monkeypatch):
