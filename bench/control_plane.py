@@ -79,7 +79,11 @@ async def _until(pred, timeout: float, poll: float = 0.005) -> float:
     raise TimeoutError(f"did not converge: {getattr(pred, '__name__', pred)} at line {pred.__code__.co_firstlineno}")
 
 
-async def run(nodes: int, policies: int, timeout: float, keep: bool = False, validation: bool = False) -> dict:
+async def run(nodes: int, policies: int, timeout: float, keep: bool = False, validation: bool = False,
+              overlap: bool = False) -> dict:
+    """``overlap``: every policy an amd-so on every node (the pre-round-5 layout): the oldest holds
+    the nodes, the others are held off all of them (targets 0), so the run measures what the
+    hold-off costs at scale -- its node LISTs and the conflict reports -- instead of 2N agents."""
     fake = FakeApiServer(bookmark_interval=5.0)
     url = await fake.start()
     pools = max(1, (policies + 1) // 2)
@@ -103,9 +107,17 @@ async def run(nodes: int, policies: int, timeout: float, keep: bool = False, val
         names = [f"policy-{k}" for k in range(policies)]
         want = {n: pool_size[k // 2] for k, n in enumerate(names)}
         amd = [n for k, n in enumerate(names) if k % 2 == 0]
+        if overlap:
+            want = {n: nodes if k == 0 else 0 for k, n in enumerate(names)}
+            amd = list(names)
         t0 = time.perf_counter()
         for k, n in enumerate(names):
             sel = {LABEL: "true", "pool": str(k // 2)}
+            if overlap:
+                pol = T.new_policy(n, keepConfigOnRestart=keep, node_selector={LABEL: "true"},
+                                   validation={"enabled": True} if validation else None)
+                fake._create(P, pol.to_dict(), None)
+                continue
             if k % 2 == 0:
                 pol = T.new_policy(n, keepConfigOnRestart=keep, node_selector=sel,
                                    validation={"enabled": True} if validation else None)
@@ -126,12 +138,13 @@ async def run(nodes: int, policies: int, timeout: float, keep: bool = False, val
         t1 = time.perf_counter()
         for i in range(nodes):
             for k, n in enumerate(names):
-                if i % pools == k // 2:
+                if (k == 0) if overlap else (i % pools == k // 2):
                     fake.node_ready[(f"amd-network-operator/{n}", f"gpu-node-{i:04d}")] = True
         fake._sync_daemonsets()
 
-        def good_all():
-            return all((fake.get_object(P, n).get("status") or {}).get("state") == "All good" for n in names)
+        def good_all():  # a policy held off every node has no targets (and says why in its errors)
+            return all((fake.get_object(P, n).get("status") or {}).get("state") ==
+                       ("All good" if want[n] else "No targets") for n in names)
 
         await _until(good_all, timeout)
         t_good = time.perf_counter() - t1
@@ -150,8 +163,14 @@ async def run(nodes: int, policies: int, timeout: float, keep: bool = False, val
                 return True
             await _until(validated_all, timeout, poll=0.05)
         await asyncio.sleep(0.5)
+        if overlap:
+            out_conflicts = {n: len([e for e in (fake.get_object(P, n).get("status") or {}).get("errors") or []
+                                     if "also selected by policy" in e]) for n in names}
         out = {"nodes": nodes, "policies": policies, "pods": sum(want.values()), "daemonsets_s": round(t_ds, 4),
                "targets_s": round(t_targets, 4), "all_good_s": round(t_good, 4)}
+        if overlap:
+            out["layout"] = "overlap: every policy amd-so on every node"
+            out["conflict_entries"] = out_conflicts
         if validation:
             out.update(ready_to_validation_jobs_s=round(jobs_s, 4),
                        jobs_done_to_validated_s=round(time.perf_counter() - t_v - jobs_s, 4))
@@ -193,8 +212,10 @@ def main() -> int:
     ap.add_argument("--timeout", type=float, default=300)
     ap.add_argument("--keep-config", action="store_true", help="keepConfigOnRestart policies, then delete them")
     ap.add_argument("--validation", action="store_true", help="fabric validation Jobs on every ready node")
+    ap.add_argument("--overlap", action="store_true",
+                    help="every policy an amd-so on every node: one holds them, the others are held off")
     a = ap.parse_args()
-    print(json.dumps(asyncio.run(run(a.nodes, a.policies, a.timeout, a.keep_config, a.validation))))
+    print(json.dumps(asyncio.run(run(a.nodes, a.policies, a.timeout, a.keep_config, a.validation, a.overlap))))
     return 0
 
 
