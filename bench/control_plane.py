@@ -22,7 +22,7 @@ complete them, and ``cleanup_done_to_gone_s`` (every policy finalized and gone).
 
 The policies alternate between ``amd-so`` and ``host-nic`` and the nodes are split into
 ceil(P/2) pools: each node runs one agent of each type (two policies of one type never share a
-node -- the newer is held off, reconciler.hold_off_terms), so a run has 2N agent Pods for P >= 2.
+node -- the newer is held off, holdoff.hold_off_terms), so a run has 2N agent Pods for P >= 2.
 (Until round 4 every policy was an amd-so on every node: P*N Pods, now a conflict by design.)
 
 The reference has no equivalent measurement (controller-runtime + envtest, no scale test).

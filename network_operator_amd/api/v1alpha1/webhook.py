@@ -425,7 +425,7 @@ def validate_update(policy: T.NetworkClusterPolicy, old: Optional[T.NetworkClust
 def overlap_warnings(policy: T.NetworkClusterPolicy, others: List[dict]) -> List[str]:
     """Admission warnings for the live policies of ``policy``'s configurationType whose
     nodeSelector can match a node ``policy``'s matches too (no key required at two values).  A
-    node belongs to the older policy of a type (operator/reconciler.py hold_off_terms): the newer
+    node belongs to the older policy of a type (operator/holdoff.py hold_off_terms): the newer
     one's agents are held off it.  ``policy`` without a creationTimestamp is being created, so it
     is the newest.  Which nodes actually match both is the operator's to say (status.errors)."""
     mine = dict(policy.spec.nodeSelector)

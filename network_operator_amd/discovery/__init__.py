@@ -4,7 +4,7 @@ The reference embeds YAML templates with ``go:embed`` and panics if one does not
 (reference config/discovery/discovery.go:26-81, config/discovery/base/daemonset.yaml).  Here
 the objects are constructed from the constants below, so there is nothing to parse at run
 time; the reconciler specialises a fresh copy per policy
-(``operator/reconciler.py::update_daemonset_for``).
+(``operator/templates.py::update_daemonset_for``).
 
 What the agent pod needs, and why:
 

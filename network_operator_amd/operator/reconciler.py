@@ -17,6 +17,9 @@ Behavioural counterpart of the reference controller
 * OpenShift: ServiceAccount ``<name>-sa`` + RoleBinding ``<name>-sa-rb`` to
   ``system:openshift:scc:privileged`` (:109-162).
 
+The DaemonSet template is built in ``templates.py`` and the same-type hold-off in ``holdoff.py``;
+this module reads the cluster and writes what they build.
+
 Deliberate fixes (SURVEY.md §7.6 "fix" list): ``pullPolicy`` is applied; volumes that are no
 longer wanted are removed; the agent has a readinessProbe (in the template) so ``ready``
 counts *configured* nodes; ``AlreadyExists`` on create falls back to the update path; and
@@ -36,21 +39,17 @@ from .. import discovery
 from ..api.v1alpha1 import types as T
 from . import kube
 from .kube import ApiClient, ApiError, is_already_exists, is_conflict, is_not_found
+from .holdoff import (CONFLICT_MARK, HELD_EVERYWHERE_KEY, HELD_OFF_REFRESH_S, MAX_HOLD_OFF_TERMS,  # noqa: F401
+                      held_off_error, hold_off_terms, set_hold_off)
+from .templates import (ARTIFACT_DIR_CONTAINER, ARTIFACT_DIR_HOST, DRIVER_CONTAINER, FW_LLDP_STATE_FILE,  # noqa: F401
+                        HOST_NIC_LABEL, HOST_NIC_LABEL_FILE, HOST_NIC_LLDP_CACHE_FILE, HOST_NIC_MTU_STATE_FILE, L3_WAIT,
+                        LLDP_CACHE_FILE, MANAGED_VOLUMES, RCCL_ENV_FILE, RCCL_NET_FILE, RCCL_TOPO_FILE,
+                        VERIFY_PEERS_TIMEOUT, add_host_volume, agent_args, host_nic_agent_args, order_managed_volumes,
+                        remove_volume, update_amd_scale_out_daemonset, update_daemonset_for, update_host_nic_daemonset)
 
 log = logging.getLogger("controller")
 
 OWNER_KEY = ".metadata.controller"
-ARTIFACT_DIR_HOST = "/etc/amd/scale-out"
-ARTIFACT_DIR_CONTAINER = "/host" + ARTIFACT_DIR_HOST
-RCCL_NET_FILE = "rccl-net.json"
-RCCL_ENV_FILE = "rccl.env"
-RCCL_TOPO_FILE = "rccl-topo.xml"
-# --verify-peers: a switch answers ARP in well under a millisecond; 2 s covers a port that is
-# still coming up, and stays far below the kubelet's restart back-off.
-VERIFY_PEERS_TIMEOUT = "2s"
-FW_LLDP_STATE_FILE = "fw-lldp-state"  # --fw-lldp-state: firmware LLDP originals kept by --keep-config agents
-LLDP_CACHE_FILE = "lldp-cache"  # --lldp-cache, beside the artifacts so it survives pod restarts
-L3_WAIT = "90s"
 
 STATE_NO_TARGETS = "No targets"
 STATE_WORKING = "Working on it.."
@@ -59,9 +58,6 @@ COND_READY = "Ready"
 COND_DEGRADED = "Degraded"
 COND_VALIDATED = "FabricValidated"
 VALIDATION_APP = "amd-gpu-fabric-validation"  # Job label; the operator's Job informer selects on it
-
-# Volumes the reconciler manages (the template's nfd-features is never touched).
-MANAGED_VOLUMES = ("var-run-dbus", "networkmanager", "rccl-artifacts")
 
 
 @dataclass
@@ -105,275 +101,6 @@ def daemonset_owner_index(obj: dict) -> List[str]:
         if ref.get("controller") and ref.get("apiVersion") == "apps/v1" and ref.get("kind") == "DaemonSet":
             return [ref["name"]]
     return []
-
-
-def add_host_volume(ds: dict, name: str, host_path: str, container_path: str,
-                    volume_type: str = "DirectoryOrCreate") -> None:
-    spec = ds["spec"]["template"]["spec"]
-    vols = spec.setdefault("volumes", [])
-    if any(v.get("name") == name for v in vols):
-        return
-    vols.append({"name": name, "hostPath": {"path": host_path, "type": volume_type}})
-    containers = spec.get("containers") or []
-    if containers:
-        containers[0].setdefault("volumeMounts", []).append({"name": name, "mountPath": container_path})
-
-
-def remove_volume(ds: dict, name: str) -> None:
-    spec = ds["spec"]["template"]["spec"]
-    spec["volumes"] = [v for v in spec.get("volumes", []) if v.get("name") != name]
-    for c in spec.get("containers") or []:
-        if "volumeMounts" in c:
-            c["volumeMounts"] = [m for m in c["volumeMounts"] if m.get("name") != name]
-
-
-def order_managed_volumes(ds: dict) -> None:
-    """Volumes (and the agent's mounts) in one canonical order: the template's own first, then
-    NetworkManager, then artifacts, then the driver container's -- the order the reference
-    produces from scratch (controller_test.go:170-179), kept stable however the spec evolves."""
-    rank = {n: i for i, n in enumerate(MANAGED_VOLUMES + ("host-lib-modules",))}
-    key = lambda x: (x.get("name") in rank, rank.get(x.get("name"), 0))  # noqa: E731 (stable sort)
-    pod = ds["spec"]["template"]["spec"]
-    if "volumes" in pod:
-        pod["volumes"] = sorted(pod["volumes"], key=key)
-    for c in pod.get("containers") or []:
-        if "volumeMounts" in c:
-            c["volumeMounts"] = sorted(c["volumeMounts"], key=key)
-
-
-def agent_args(p: T.NetworkClusterPolicy) -> List[str]:
-    so = p.spec.amdScaleOut
-    args = ["--configure=true", "--keep-running", f"--mode={so.layer}"]
-    if p.spec.logLevel > 0:
-        args.append(f"--v={p.spec.logLevel}")
-    if so.mtu > 0:
-        args.append(f"--mtu={so.mtu}")
-    if so.disableNetworkManager:
-        args += ["--disable-networkmanager", "--nm-keyfile-dir=/etc/NetworkManager/conf.d"]
-    if so.layer == "L3":
-        args += [f"--wait={so.lldpWait or L3_WAIT}", f"--rccl-net={ARTIFACT_DIR_CONTAINER}/{RCCL_NET_FILE}",
-                 f"--rccl-env={ARTIFACT_DIR_CONTAINER}/{RCCL_ENV_FILE}"]
-    else:
-        # MI355X: RCCL needs the HCA list and the link-local RoCE v2 GID in L2 as well (Gaudi's
-        # firmware did not, so the reference passes nothing in L2).
-        args.append(f"--rccl-env={ARTIFACT_DIR_CONTAINER}/{RCCL_ENV_FILE}")
-        if so.carrierWait:
-            args.append(f"--carrier-wait={so.carrierWait}")
-    # NCCL_TOPO_FILE: written through the agent's mount, named in rccl.env by the host path jobs
-    # mount (the reference's HCCL contract is gaudinet.json, controller.go:198-200).
-    args += [f"--rccl-topo={ARTIFACT_DIR_CONTAINER}/{RCCL_TOPO_FILE}",
-             f"--rccl-topo-env-path={ARTIFACT_DIR_HOST}/{RCCL_TOPO_FILE}"]
-    # MI355X options
-    if so.xgmiCheck:
-        args.append("--xgmi-expect=0")
-    if so.lldpAnnounce is False:
-        args.append("--lldp-announce=false")
-    if so.interfaces:
-        args.append("--interfaces=" + ",".join(so.interfaces))
-    if so.nicDrivers:
-        args.append("--nic-drivers=" + ",".join(so.nicDrivers))
-    if so.disableFirmwareLldp and so.layer == "L3":
-        args.append("--disable-fw-lldp")
-        if so.handDcbxToHost:  # opt-in: the NIC firmware stops negotiating PFC/ETS (ADVICE r3)
-            args.append("--fw-lldp-dcbx-host")
-    if so.metricsPort:
-        args.append(f"--metrics-bind-address=:{so.metricsPort}")
-    if so.railTableBase and so.layer == "L3":
-        args.append(f"--rail-table-base={so.railTableBase}")
-    if so.rcclSocketIfname:
-        args.append(f"--rccl-socket-ifname={so.rcclSocketIfname}")
-    if (so.lldpCache or so.keepConfigOnRestart) and so.layer == "L3":
-        # keepConfigOnRestart: the cache is what lets the next agent adopt the addresses it finds
-        args.append(f"--lldp-cache={ARTIFACT_DIR_CONTAINER}/{LLDP_CACHE_FILE}")
-    if so.keepConfigOnRestart:
-        args.append("--keep-config")
-    if so.disableFirmwareLldp and so.layer == "L3":
-        # The originals of what --disable-fw-lldp changes, on the node: with --keep-config they stay
-        # changed across restarts and the cleanup Job restores them; without, they outlive an agent
-        # that fails and the next clean exit restores them.
-        args.append(f"--fw-lldp-state={ARTIFACT_DIR_CONTAINER}/{FW_LLDP_STATE_FILE}")
-    if so.railSwitchPattern and so.layer == "L3":
-        args.append(f"--rail-switch-pattern={so.railSwitchPattern}")
-    if so.minLinkSpeedGbps:
-        args.append(f"--min-link-speed-gbps={so.minLinkSpeedGbps}")
-    if so.checkPeerMtu is False and so.layer == "L3":
-        args.append("--check-peer-mtu=false")
-    args.append(f"--status-file={discovery.AGENT_STATUS_FILE}")
-    if so.verifyPeers and so.layer == "L3":
-        args.append(f"--verify-peers={VERIFY_PEERS_TIMEOUT}")
-    if so.rcclEnv:
-        args.append("--rccl-env-extra=" + ",".join(f"{k}={v}" for k, v in sorted(so.rcclEnv.items())))
-    if so.gpuDirectRdma:
-        args.append("--require-gdr=" + {"Any": "any", "PeerMem": "peermem", "DmaBuf": "dmabuf"}[so.gpuDirectRdma])
-    return args
-
-
-def update_amd_scale_out_daemonset(ds: dict, p: T.NetworkClusterPolicy, namespace: str) -> None:
-    """updateGaudiScaleOutDaemonSet (:164-204) for amd-so."""
-    md = ds.setdefault("metadata", {})
-    md["name"] = p.name
-    md["namespace"] = namespace
-    pod = ds["spec"]["template"]["spec"]
-    if p.spec.nodeSelector:
-        pod["nodeSelector"] = dict(p.spec.nodeSelector)
-    c = pod["containers"][0]
-    so = p.spec.amdScaleOut
-    if so.image:
-        c["image"] = so.image
-    if so.pullPolicy:
-        c["imagePullPolicy"] = so.pullPolicy
-    wanted = set()
-    if so.disableNetworkManager:
-        add_host_volume(ds, "var-run-dbus", "/var/run/dbus", "/var/run/dbus")
-        add_host_volume(ds, "networkmanager", "/etc/NetworkManager", "/etc/NetworkManager")
-        wanted |= {"var-run-dbus", "networkmanager"}
-    add_host_volume(ds, "rccl-artifacts", ARTIFACT_DIR_HOST, ARTIFACT_DIR_CONTAINER)  # L2 too (rccl.env)
-    wanted.add("rccl-artifacts")
-    for v in MANAGED_VOLUMES + ("host-lib-modules",):
-        if v not in wanted:
-            remove_volume(ds, v)
-    order_managed_volumes(ds)
-    # A policy that switched from host-nic: no driver container, default readiness probe.
-    inits = [x for x in pod.get("initContainers", []) if x.get("name") != "nic-driver"]
-    if inits:
-        pod["initContainers"] = inits
-    else:
-        pod.pop("initContainers", None)
-    probe = c.get("readinessProbe", {}).get("exec")
-    if probe:
-        probe["command"] = probe["command"][:1] + ["--ready-check", f"--status-file={discovery.AGENT_STATUS_FILE}"]
-    # Agent metrics port (hostNetwork: the container port is the node port).
-    ports = [x for x in c.get("ports", []) if x.get("name") != "metrics"]
-    if so.metricsPort:
-        ports.append({"name": "metrics", "containerPort": so.metricsPort, "protocol": "TCP"})
-    if ports:
-        c["ports"] = ports
-    else:
-        c.pop("ports", None)
-    c["args"] = agent_args(p)
-
-
-HOST_NIC_LABEL = "amd.feature.node.kubernetes.io/host-nic-ready"
-HOST_NIC_LABEL_FILE = "host-nic-readiness.txt"
-HOST_NIC_LLDP_CACHE_FILE = "host-nic-lldp-cache"
-HOST_NIC_MTU_STATE_FILE = "host-nic-mtu-state"  # --mtu-state: the host NICs' own MTUs
-DRIVER_CONTAINER = "nic-driver"
-
-
-def host_nic_agent_args(p: T.NetworkClusterPolicy) -> List[str]:
-    """Agent flags for ``host-nic``: RDMA NIC discovery instead of GPU affinity, its own readiness
-    label and file (so it can coexist with an ``amd-so`` policy on the same node)."""
-    hn = p.spec.hostNic or T.HostNicSpec()
-    args = ["--configure=true", "--keep-running", f"--mode={hn.layer}",
-            "--nic-discovery=" + ("none" if hn.interfaces else "rdma"),
-            f"--nfd-label-file={HOST_NIC_LABEL_FILE}", f"--nfd-label={HOST_NIC_LABEL}"]
-    if p.spec.logLevel > 0:
-        args.append(f"--v={p.spec.logLevel}")
-    if hn.mtu > 0:
-        args.append(f"--mtu={hn.mtu}")
-    # The node's own NICs get their MTU back when the agent goes for good: on a clean exit, or
-    # (keepConfigOnRestart) from the record the cleanup Job reads.  Always, not only while mtu is
-    # set: the agent applies its default MTU otherwise, and a policy that dropped mtu must still
-    # let the next agent and the cleanup Job find and restore the record (ADVICE r4).
-    args += ["--restore-mtu", f"--mtu-state={ARTIFACT_DIR_CONTAINER}/{HOST_NIC_MTU_STATE_FILE}"]
-    if hn.disableNetworkManager:
-        args += ["--disable-networkmanager", "--nm-keyfile-dir=/etc/NetworkManager/conf.d"]
-    if hn.layer == "L3":
-        args.append(f"--wait={hn.lldpWait or L3_WAIT}")
-        if hn.verifyPeers:
-            args.append(f"--verify-peers={VERIFY_PEERS_TIMEOUT}")
-    elif hn.carrierWait:
-        args.append(f"--carrier-wait={hn.carrierWait}")
-    if hn.interfaces:
-        args.append("--interfaces=" + ",".join(hn.interfaces))
-    if hn.nicDrivers:
-        args.append("--nic-drivers=" + ",".join(hn.nicDrivers))
-    if hn.includeGpuRails and not hn.interfaces:
-        args.append("--rdma-include-gpu-rails")
-    if hn.checkPeerMtu is False and hn.layer == "L3":
-        args.append("--check-peer-mtu=false")
-    if hn.keepConfigOnRestart:
-        if hn.layer == "L3":  # its own cache beside the scale-out agent's
-            args.append(f"--lldp-cache={ARTIFACT_DIR_CONTAINER}/{HOST_NIC_LLDP_CACHE_FILE}")
-        args.append("--keep-config")
-    args.append(f"--status-file={discovery.AGENT_STATUS_FILE}")
-    return args
-
-
-def update_host_nic_daemonset(ds: dict, p: T.NetworkClusterPolicy, namespace: str) -> None:
-    """The ``host-nic`` branch (the reference's "Future work": Host-NIC use + KMD install)."""
-    hn = p.spec.hostNic or T.HostNicSpec()
-    md = ds.setdefault("metadata", {})
-    md["name"] = p.name
-    md["namespace"] = namespace
-    pod = ds["spec"]["template"]["spec"]
-    if p.spec.nodeSelector:
-        pod["nodeSelector"] = dict(p.spec.nodeSelector)
-    c = pod["containers"][0]
-    if hn.image:
-        c["image"] = hn.image
-    if hn.pullPolicy:
-        c["imagePullPolicy"] = hn.pullPolicy
-    wanted = set()
-    if hn.disableNetworkManager:
-        add_host_volume(ds, "var-run-dbus", "/var/run/dbus", "/var/run/dbus")
-        add_host_volume(ds, "networkmanager", "/etc/NetworkManager", "/etc/NetworkManager")
-        wanted |= {"var-run-dbus", "networkmanager"}
-    if (hn.keepConfigOnRestart and hn.layer == "L3") or hn.mtu > 0:  # the LLDP cache / MTU record outlive the Pod
-        add_host_volume(ds, "rccl-artifacts", ARTIFACT_DIR_HOST, ARTIFACT_DIR_CONTAINER)
-        wanted.add("rccl-artifacts")
-    # Optional kernel-driver container: privileged, sees the host's modules, runs to completion
-    # before the agent starts (init container), so the NICs exist when discovery runs.
-    inits = [x for x in pod.get("initContainers", []) if x.get("name") != DRIVER_CONTAINER]
-    if hn.driverImage:
-        spec_vols = pod.setdefault("volumes", [])
-        if not any(v.get("name") == "host-lib-modules" for v in spec_vols):
-            spec_vols.append({"name": "host-lib-modules", "hostPath": {"path": "/lib/modules", "type": "Directory"}})
-        wanted.add("host-lib-modules")
-        inits.append({"name": DRIVER_CONTAINER, "image": hn.driverImage,
-                      "imagePullPolicy": hn.pullPolicy or "IfNotPresent",
-                      "securityContext": {"privileged": True},
-                      "volumeMounts": [{"name": "host-lib-modules", "mountPath": "/lib/modules"}]})
-    if inits:
-        pod["initContainers"] = inits
-    else:
-        pod.pop("initContainers", None)
-    for v in MANAGED_VOLUMES + ("host-lib-modules",):
-        if v not in wanted:
-            remove_volume(ds, v)
-    order_managed_volumes(ds)
-    probe = c.get("readinessProbe", {}).get("exec")
-    if probe:
-        probe["command"] = [probe["command"][0], "--ready-check", f"--nfd-label-file={HOST_NIC_LABEL_FILE}",
-                            f"--status-file={discovery.AGENT_STATUS_FILE}"]
-    c["args"] = host_nic_agent_args(p)
-
-
-def update_daemonset_for(ds: dict, p: T.NetworkClusterPolicy, namespace: str,
-                         hold_off: Optional[List[dict]] = None) -> None:
-    """createDaemonSet / updateDaemonSet dispatch on configurationType (:243-265).  Also the
-    rolling-update width (spec.maxUnavailable; 1 when unset, like the reference's DaemonSet) and
-    the node affinity that holds the agents off nodes an older policy of the type selects."""
-    ds["spec"].setdefault("updateStrategy", {"type": "RollingUpdate"}).setdefault("rollingUpdate", {})[
-        "maxUnavailable"] = p.spec.maxUnavailable if p.spec.maxUnavailable is not None else 1
-    if p.spec.configurationType == T.CONFIG_AMD_SCALE_OUT:
-        update_amd_scale_out_daemonset(ds, p, namespace)
-    elif p.spec.configurationType == T.CONFIG_HOST_NIC:
-        update_host_nic_daemonset(ds, p, namespace)
-    else:
-        raise ValueError(f"unknown configuration type {p.spec.configurationType!r}")
-    # Tainted GPU nodes (amd.com/gpu:NoSchedule, ...): the policy's tolerations, exactly (a
-    # toleration removed from the policy leaves the template; the cleanup Job copies this spec).
-    pod = ds["spec"]["template"]["spec"]
-    if p.spec.tolerations:
-        pod["tolerations"] = copy.deepcopy(p.spec.tolerations)
-    else:
-        pod.pop("tolerations", None)
-    if p.spec.priorityClassName:
-        pod["priorityClassName"] = p.spec.priorityClassName
-    else:
-        pod.pop("priorityClassName", None)
-    set_hold_off(pod, hold_off)
 
 
 def status_for(targets: int, ready: int) -> str:
@@ -450,85 +177,6 @@ def _starting_up(reason: str) -> bool:
 
 def _container_running(pod: dict) -> bool:
     return any("running" in (cs.get("state") or {}) for cs in (pod.get("status") or {}).get("containerStatuses") or [])
-
-
-# Two policies of one configurationType that select the same node would run two agents there;
-# they share the node lock (named after the type's NFD label), so the later one would wait and
-# then fail, restarting forever.  Instead a node belongs to the OLDEST live policy of the type
-# whose nodeSelector matches it: every newer one's DaemonSet carries a required node-affinity
-# term that excludes the nodes the older selectors match, so its agents are never placed there.
-# The term is built from the selectors, not from a node list: it does not change when nodes come,
-# go or get relabelled (a DaemonSet template change rolls every agent of the policy), only when
-# an older policy's selector does.  The newer policy's status names the held-off nodes
-# (Degraded/PolicyConflict, a Warning Event); once the older policy goes, the term goes with it
-# and the newer policy's agents take those nodes.  (The reference has no guard at all,
-# internal/controller/networkconfiguration_controller.go:164-204,313-362.)
-CONFLICT_MARK = ": also selected by policy "
-# A node-selector term no node matches (no node carries this label): a newer policy whose
-# every node an older one selects.
-HELD_EVERYWHERE_KEY = "network.amd.com/held-off-by-an-older-policy"
-MAX_HOLD_OFF_TERMS = 64  # required terms are ORed: the hold-off expands to at most this many
-# While an older selector overlaps, the held-off nodes are read again this often: a node
-# relabelled into or out of the overlap moves no Pod of this policy, so no event would.
-HELD_OFF_REFRESH_S = 30.0
-
-
-def hold_off_terms(mine: Dict[str, str], older: List[Dict[str, str]]) -> Optional[List[dict]]:
-    """nodeSelectorTerms (ORed) of the nodes ``mine`` (a nodeSelector) selects that no selector in
-    ``older`` matches, to AND with ``mine``; None when nothing is held off.
-
-    Not matching {k1: v1, k2: v2} is (k1 NotIn [v1]) OR (k2 NotIn [v2]) (NotIn also matches a node
-    without the label).  Over several older selectors that is a conjunction of such clauses,
-    expanded here into a disjunction of terms.  A clause whose pairs all sit in ``mine`` already
-    excludes every node: nothing is left.  An older selector with a key ``mine`` requires at
-    another value is disjoint: no clause.  Raises ValueError past MAX_HOLD_OFF_TERMS."""
-    clauses = set()
-    for q in older:
-        if any(k in mine and mine[k] != v for k, v in q.items()):
-            continue  # disjoint selections
-        clause = tuple(sorted((k, v) for k, v in q.items() if mine.get(k) != v))
-        if not clause:
-            return [{"matchExpressions": [{"key": HELD_EVERYWHERE_KEY, "operator": "Exists"}]}]
-        clauses.add(clause)
-    if not clauses:
-        return None
-    kept: List[tuple] = []  # absorption: a clause implied by a shorter one adds nothing
-    for c in sorted(clauses, key=lambda c: (len(c), c)):
-        if not any(set(k) <= set(c) for k in kept):
-            kept.append(c)
-    terms: List[frozenset] = [frozenset()]
-    for c in kept:
-        terms = sorted({t | {lit} for t in terms for lit in c}, key=sorted)
-        if len(terms) > MAX_HOLD_OFF_TERMS:
-            raise ValueError(f"{len(kept)} overlapping older selectors expand to more than {MAX_HOLD_OFF_TERMS} "
-                             "node-affinity terms")
-    terms = [t for t in terms if not any(o < t for o in terms)]  # a term implied by a smaller one
-    out = []
-    for t in terms:
-        by_key: Dict[str, List[str]] = {}
-        for k, v in sorted(t):
-            by_key.setdefault(k, []).append(v)
-        out.append({"matchExpressions": [{"key": k, "operator": "NotIn", "values": vs} for k, vs in by_key.items()]})
-    return out
-
-
-def set_hold_off(pod: dict, terms: Optional[List[dict]]) -> None:
-    """The agent Pod template's required node affinity: the hold-off terms, or none.  (The policy
-    has no affinity field of its own, so the operator owns this one.)"""
-    if terms:
-        pod["affinity"] = {"nodeAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": {
-            "nodeSelectorTerms": copy.deepcopy(terms)}}}
-    else:
-        pod.pop("affinity", None)
-
-
-def held_off_error(ctype: str, nodes: List[str], more: bool, other: str) -> str:
-    """status.errors entry for the nodes this policy is kept off because ``other`` (older, same
-    configurationType) selects them too."""
-    shown = ", ".join(nodes) + (" and more" if more else "")
-    return (f"{shown}{CONFLICT_MARK}{other} ({ctype} too, created earlier): one agent per node and type "
-            f"configures the NICs, so this policy's agents are held off these nodes while {other} selects them; "
-            f"narrow a nodeSelector")
 
 
 def policy_conditions(current: List[dict], targets: int, ready: int, errors: List[str], generation: int,

@@ -510,7 +510,7 @@ def test_prometheus_overlay_scrapes_the_operator_and_the_agents():
 
 def test_alert_rules_use_only_metrics_that_exist():
     """Every metric an alert of config/operator/prometheus/alert-rules.yaml reads is exported: the
-    operator's from its registry, the agents' from the agent's /metrics writer (agent.cpp); each
+    operator's from its registry, the agents' from the agent's /metrics writer (agent_status.cpp); each
     alert has a severity and a summary."""
     import re
 
@@ -524,7 +524,7 @@ def test_alert_rules_use_only_metrics_that_exist():
     for fam in OperatorMetrics().registry.collect():
         operator_names.add(fam.name + ("_total" if fam.type == "counter" else ""))
         operator_names.update(s.name for s in fam.samples)
-    agent_src = (ROOT / "native/src/agent.cpp").read_text()
+    agent_src = (ROOT / "native/src/agent_status.cpp").read_text()
     rules = [r for g in doc["spec"]["groups"] for r in g["rules"]]
     assert len(rules) >= 6
     for r in rules:
