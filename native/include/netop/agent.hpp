@@ -118,6 +118,11 @@ struct Config {
     // With restore_mtu: "ifname mtu" lines keeping each NIC's MTU from before the first agent that
     // changed it, across --keep-config restarts, for the last clean exit or the --cleanup Job.
     std::string mtu_state;
+    // "ifname up|down" lines keeping each NIC's administrative state from before the first agent
+    // brought it up, across crashes and --keep-config restarts (a restarted agent finds the link up
+    // and would take that for the original).  The last clean exit, or --cleanup, puts the recorded
+    // state back and removes the file.  Empty: the state this process found (the reference).
+    std::string link_state;
     std::string fw_lldp_flags;                        // extra rules "NAME=0|1,..."
     // With keep_config: the originals of what --disable-fw-lldp changed are kept in this file
     // across agent restarts (a restart does not flip the NICs back and forth: some drivers reset
@@ -357,6 +362,9 @@ class Agent {
     void load_mtu_state();       // orig_mtu of every NIC from --mtu-state (recording new ones)
     void restore_mtus();         // each NIC's orig_mtu back; the state file's entries with it
     void restore_mtu_state();    // --cleanup: every entry of --mtu-state back, then the file goes
+    void load_link_state();      // orig_flags' IFF_UP of every NIC from --link-state (recording new ones)
+    void forget_link_state();    // after interfaces_restore_down: drop the NICs back in their original state
+    void restore_link_state();   // --cleanup: every NIC recorded down goes down, then the file goes
     std::vector<std::pair<std::string, std::string>> rccl_env_extra_;
     void disable_fw_lldp();
     void restore_fw_lldp_from_state();

@@ -277,6 +277,7 @@ void Agent::interfaces_restore_down() {
         if (n.expect_response) n.link.flags &= ~unsigned(IFF_UP);
         n.expect_response = false;
     }
+    forget_link_state();
 }
 
 void Agent::interfaces_set_mtu() {
@@ -499,6 +500,7 @@ void Agent::run(int stop_fd) {
         disable_fw_lldp();  // before link-up: some drivers reset the port when the flag flips
         mark("fw_lldp");
     }
+    load_link_state();
     interfaces_up();
     mark("link_up");
     load_mtu_state();
@@ -785,6 +787,12 @@ void Agent::cleanup_node() {
         restore_mtu_state();
     } catch (const std::exception& e) {
         NLOG_W("Could not restore the NICs' MTUs: %s", e.what());
+        ++errors;
+    }
+    try {
+        restore_link_state();
+    } catch (const std::exception& e) {
+        NLOG_W("Could not restore the NICs' link states: %s", e.what());
         ++errors;
     }
     if (cfg_.disable_nm) {

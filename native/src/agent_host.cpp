@@ -267,6 +267,87 @@ void Agent::restore_mtu_state() {
     write_mtu_state(cfg_.mtu_state, left);
 }
 
+namespace {
+std::map<std::string, bool> read_link_state(const std::string& path) {
+    std::map<std::string, bool> out;
+    auto t = read_file(path);
+    if (!t) return out;
+    for (const auto& line : split(*t, '\n')) {
+        auto f = split(trim(line), ' ');
+        if (f.size() != 2 || f[0].empty() || f[0].size() > 15 || (f[1] != "up" && f[1] != "down")) continue;
+        out[f[0]] = f[1] == "up";
+    }
+    return out;
+}
+
+void write_link_state(const std::string& path, const std::map<std::string, bool>& m) {
+    if (m.empty()) {
+        if (::unlink(path.c_str()) != 0 && errno != ENOENT)
+            NLOG_W("Could not remove %s: %s", path.c_str(), std::strerror(errno));
+        return;
+    }
+    std::string t;
+    for (const auto& [n, up] : m) t += n + (up ? " up\n" : " down\n");
+    write_file_atomic(path, t);
+}
+}  // namespace
+
+void Agent::load_link_state() {
+    // Before interfaces_up(): the first agent records what it found; a later one (after a crash or
+    // a --keep-config restart) finds the links up, and the record wins.
+    if (cfg_.link_state.empty()) return;
+    auto m = read_link_state(cfg_.link_state);
+    for (auto& n : nics_) {
+        auto it = m.find(n.ifname);
+        if (it == m.end())
+            m[n.ifname] = (n.orig_flags & IFF_UP) != 0;
+        else if (it->second)
+            n.orig_flags |= IFF_UP;
+        else
+            n.orig_flags &= ~unsigned(IFF_UP);
+    }
+    try {
+        write_link_state(cfg_.link_state, m);
+    } catch (const std::exception& e) {
+        NLOG_W("Could not record the NICs' link states in %s: %s", cfg_.link_state.c_str(), e.what());
+    }
+}
+
+void Agent::forget_link_state() {
+    if (cfg_.link_state.empty()) return;
+    auto m = read_link_state(cfg_.link_state);
+    for (const auto& n : nics_)
+        if (n.link.up() == ((n.orig_flags & IFF_UP) != 0)) m.erase(n.ifname);  // what failed stays for --cleanup
+    try {
+        write_link_state(cfg_.link_state, m);
+    } catch (const std::exception& e) {
+        NLOG_W("Could not update %s: %s", cfg_.link_state.c_str(), e.what());
+    }
+}
+
+void Agent::restore_link_state() {
+    if (cfg_.link_state.empty()) return;
+    std::map<std::string, bool> left;
+    for (const auto& [name, up] : read_link_state(cfg_.link_state)) {
+        if (up) continue;  // it was up before any agent: it stays up
+        try {
+            auto l = ops_.link_by_name(name);
+            if (l.up()) {
+                ops_.link_set_down(l.index);
+                NLOG_I("Setting link '%s' back down", name.c_str());
+            }
+        } catch (const SysError& e) {
+            if (e.code() == ENODEV) continue;  // the NIC is gone
+            NLOG_W("Cannot set link '%s' back down: %s", name.c_str(), e.what());
+            left[name] = up;
+        } catch (const std::exception& e) {
+            NLOG_W("Cannot set link '%s' back down: %s", name.c_str(), e.what());
+            left[name] = up;
+        }
+    }
+    write_link_state(cfg_.link_state, left);
+}
+
 void Agent::restore_network_manager() {
     // Only with --nm-restore: the reference leaves its runtime Managed=false behind, and this
     // agent's keyfile keeps the NICs unmanaged across agent restarts and reboots (Config::nm_restore).

@@ -175,7 +175,7 @@ TEST(agent_l3_routes_and_label_while_running) {
 
 bool has_table_route(FakeNetOps& o, int idx, const char* dst, const char* gw, int table) {
     for (auto& r : o.routes)
-        if (r.table == table && r.ifindex == idx && r.dst.masked().str() == dst &&
+        if (r.table == uint32_t(table) && r.ifindex == idx && r.dst.masked().str() == dst &&
             (gw ? (r.gateway && r.gateway->str() == gw) : !r.gateway))
             return true;
     return false;
@@ -2416,6 +2416,62 @@ TEST(agent_mtu_state_keeps_the_original_mtu_across_keep_config_restarts_for_the_
     CHECK(!path_exists(g.cfg.mtu_state));
 }
 
+TEST(agent_link_state_keeps_the_original_down_state_across_a_crash_for_the_last_exit) {
+    // ens0 and ens2 are down before any agent; the first agent brings them up and dies without
+    // cleaning up (here: a --keep-config exit, which leaves the links up just the same).  The next
+    // agent finds them up, but the record says down: its clean exit takes them down again and
+    // removes the record.  ens1 was up before any agent and stays up.  --cleanup does the same
+    // from the record alone.
+    for (bool via_cleanup : {false, true}) {
+        Fixture f;
+        f.cfg.mode = "L2";
+        f.cfg.keep_running = false;
+        f.cfg.link_state = f.tmp.path + "/link-state";
+        {
+            agent::Config c = f.cfg;
+            c.keep_config = true;
+            agent::Agent a(c, f.ops, std::make_unique<ScriptedLldp>(), f.nm());
+            a.run(-1);
+        }
+        CHECK(f.ops.links["ens0"].flags & IFF_UP);
+        CHECK(read_file(f.cfg.link_state) == std::optional<std::string>("ens0 down\nens1 up\nens2 down\n"));
+        if (via_cleanup) {
+            agent::Config c = f.cfg;
+            c.cleanup = true;
+            agent::Agent a(c, f.ops, std::make_unique<ScriptedLldp>(), f.nm());
+            a.run(-1);
+        } else {
+            agent::Config c = f.cfg;
+            c.keep_running = true;
+            Pipe stop;
+            stop.fire();
+            agent::Agent a(c, f.ops, std::make_unique<ScriptedLldp>(), f.nm());
+            a.run(stop.fd[0]);
+            CHECK(a.ready());
+        }
+        CHECK(!(f.ops.links["ens0"].flags & IFF_UP));
+        CHECK(!(f.ops.links["ens2"].flags & IFF_UP));
+        CHECK(f.ops.links["ens1"].flags & IFF_UP);
+        CHECK(!path_exists(f.cfg.link_state));
+    }
+    Fixture g;  // without the record: the restarted agent takes "up" for the original (the reference)
+    g.cfg.mode = "L2";
+    {
+        agent::Config c = g.cfg;
+        c.keep_config = true;
+        c.keep_running = false;
+        agent::Agent a(c, g.ops, std::make_unique<ScriptedLldp>(), g.nm());
+        a.run(-1);
+    }
+    {
+        Pipe stop;
+        stop.fire();
+        agent::Agent a(g.cfg, g.ops, std::make_unique<ScriptedLldp>(), g.nm());
+        a.run(stop.fd[0]);
+    }
+    CHECK(g.ops.links["ens0"].flags & IFF_UP);
+}
+
 TEST(agent_rdma_discovery_keeps_the_agents_own_l3_config) {
     // A host NIC an earlier (keep-config) agent addressed: its /30, the kernel /30 route, the /16
     // via the switch end and the rail table are the agent's, so the NIC is still a host NIC.
@@ -2503,7 +2559,7 @@ TEST(agent_configures_a_nic_whose_default_route_is_only_in_a_policy_routing_tabl
         f.ops.rules = {rule(RT_TABLE_LOCAL, 0, nullptr), rule(101, 100, "192.168.1.0/24"),
                        rule(RT_TABLE_MAIN, 32766, nullptr), rule(RT_TABLE_DEFAULT, 32767, nullptr)};
         auto def = route(11, "0.0.0.0/0", "192.168.1.1", RTPROT_STATIC);
-        def.table = variant == 1 ? RT_TABLE_MAIN : 101;
+        def.table = variant == 1 ? uint32_t(RT_TABLE_MAIN) : 101u;
         f.ops.routes.push_back(def);
         if (variant == 2) f.ops.fail.insert("rule_list");
         std::string err;

@@ -102,6 +102,7 @@ int main(int argc, char** argv) {
     fs.add_bool("disable-fw-lldp", &cfg.disable_fw_lldp, "L3: turn off NIC-firmware LLDP agents while running (i40e disable-fw-lldp, ice fw-lldp-agent, --fw-lldp-priv-flag rules); other DCB NICs (e.g. mlx5_core) only with --fw-lldp-dcbx-host");
     fs.add_bool("fw-lldp-dcbx-host", &cfg.fw_lldp_dcbx_host, "with --disable-fw-lldp: on a NIC without a firmware-LLDP private flag whose DCBX an embedded agent runs (mlx5_core firmware mode), hand DCBX to the host (the firmware stops negotiating PFC/ETS with the switch); restored on exit");
     fs.add_bool("restore-mtu", &cfg.restore_mtu, "on a clean exit (not --keep-config), put each NIC's MTU back to what it was when the agent started (host-nic policies: the node's own NICs)");
+    fs.add_string("link-state", &cfg.link_state, "file keeping each NIC's link state (up/down) from before the first agent brought it up, across crashes and --keep-config restarts (put back on the last clean exit or by --cleanup)");
     fs.add_string("mtu-state", &cfg.mtu_state, "with --restore-mtu: file keeping each NIC's MTU from before the first agent changed it, across --keep-config restarts (restored on the last clean exit or by --cleanup)");
     fs.add_string("fw-lldp-priv-flag", &cfg.fw_lldp_flags, "extra ethtool private-flag rules NAME=0|1[,...] for --disable-fw-lldp");
     fs.add_string("fw-lldp-state", &cfg.fw_lldp_state, "with --keep-config: keep the originals of what --disable-fw-lldp changed in this file across restarts instead of restoring them on exit; --cleanup restores them");

@@ -42,8 +42,8 @@ from .kube import ApiClient, ApiError, is_already_exists, is_conflict, is_not_fo
 from .holdoff import (CONFLICT_MARK, HELD_EVERYWHERE_KEY, HELD_OFF_REFRESH_S, MAX_HOLD_OFF_TERMS,  # noqa: F401
                       held_off_error, hold_off_terms, set_hold_off)
 from .templates import (ARTIFACT_DIR_CONTAINER, ARTIFACT_DIR_HOST, DRIVER_CONTAINER, FW_LLDP_STATE_FILE,  # noqa: F401
-                        HOST_NIC_LABEL, HOST_NIC_LABEL_FILE, HOST_NIC_LLDP_CACHE_FILE, HOST_NIC_MTU_STATE_FILE, L3_WAIT,
-                        LLDP_CACHE_FILE, MANAGED_VOLUMES, RCCL_ENV_FILE, RCCL_NET_FILE, RCCL_TOPO_FILE,
+                        HOST_NIC_LABEL, HOST_NIC_LABEL_FILE, HOST_NIC_LINK_STATE_FILE, HOST_NIC_LLDP_CACHE_FILE,
+                        HOST_NIC_MTU_STATE_FILE, L3_WAIT, LINK_STATE_FILE, LLDP_CACHE_FILE, MANAGED_VOLUMES, RCCL_ENV_FILE, RCCL_NET_FILE, RCCL_TOPO_FILE,
                         VERIFY_PEERS_TIMEOUT, add_host_volume, agent_args, host_nic_agent_args, order_managed_volumes,
                         remove_volume, update_amd_scale_out_daemonset, update_daemonset_for, update_host_nic_daemonset)
 

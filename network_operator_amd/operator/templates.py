@@ -28,6 +28,9 @@ RCCL_TOPO_FILE = "rccl-topo.xml"
 VERIFY_PEERS_TIMEOUT = "2s"
 FW_LLDP_STATE_FILE = "fw-lldp-state"  # --fw-lldp-state: firmware LLDP originals kept by --keep-config agents
 LLDP_CACHE_FILE = "lldp-cache"  # --lldp-cache, beside the artifacts so it survives pod restarts
+# --link-state: each NIC's up/down from before the first agent, so the agent restarted after a
+# crash (or a --keep-config restart) and the cleanup Job put back what no agent in memory saw.
+LINK_STATE_FILE = "link-state"
 L3_WAIT = "90s"
 
 # Volumes the reconciler manages (the template's nfd-features is never touched).
@@ -125,6 +128,7 @@ def agent_args(p: T.NetworkClusterPolicy) -> List[str]:
         args.append(f"--min-link-speed-gbps={so.minLinkSpeedGbps}")
     if so.checkPeerMtu is False and so.layer == "L3":
         args.append("--check-peer-mtu=false")
+    args.append(f"--link-state={ARTIFACT_DIR_CONTAINER}/{LINK_STATE_FILE}")
     args.append(f"--status-file={discovery.AGENT_STATUS_FILE}")
     if so.verifyPeers and so.layer == "L3":
         args.append(f"--verify-peers={VERIFY_PEERS_TIMEOUT}")
@@ -184,6 +188,7 @@ HOST_NIC_LABEL = "amd.feature.node.kubernetes.io/host-nic-ready"
 HOST_NIC_LABEL_FILE = "host-nic-readiness.txt"
 HOST_NIC_LLDP_CACHE_FILE = "host-nic-lldp-cache"
 HOST_NIC_MTU_STATE_FILE = "host-nic-mtu-state"  # --mtu-state: the host NICs' own MTUs
+HOST_NIC_LINK_STATE_FILE = "host-nic-link-state"  # --link-state, apart from the amd-so agent's
 DRIVER_CONTAINER = "nic-driver"
 
 
@@ -223,7 +228,8 @@ def host_nic_agent_args(p: T.NetworkClusterPolicy) -> List[str]:
         if hn.layer == "L3":  # its own cache beside the scale-out agent's
             args.append(f"--lldp-cache={ARTIFACT_DIR_CONTAINER}/{HOST_NIC_LLDP_CACHE_FILE}")
         args.append("--keep-config")
-    args.append(f"--status-file={discovery.AGENT_STATUS_FILE}")
+    args += [f"--link-state={ARTIFACT_DIR_CONTAINER}/{HOST_NIC_LINK_STATE_FILE}",
+             f"--status-file={discovery.AGENT_STATUS_FILE}"]
     return args
 
 
@@ -246,9 +252,10 @@ def update_host_nic_daemonset(ds: dict, p: T.NetworkClusterPolicy, namespace: st
         add_host_volume(ds, "var-run-dbus", "/var/run/dbus", "/var/run/dbus")
         add_host_volume(ds, "networkmanager", "/etc/NetworkManager", "/etc/NetworkManager")
         wanted |= {"var-run-dbus", "networkmanager"}
-    if (hn.keepConfigOnRestart and hn.layer == "L3") or hn.mtu > 0:  # the LLDP cache / MTU record outlive the Pod
-        add_host_volume(ds, "rccl-artifacts", ARTIFACT_DIR_HOST, ARTIFACT_DIR_CONTAINER)
-        wanted.add("rccl-artifacts")
+    # The MTU and link-state records (and the L3 LLDP cache) outlive the Pod: always mounted, so a
+    # policy that dropped mtu still lets the next agent and the cleanup Job find the record.
+    add_host_volume(ds, "rccl-artifacts", ARTIFACT_DIR_HOST, ARTIFACT_DIR_CONTAINER)
+    wanted.add("rccl-artifacts")
     # Optional kernel-driver container: privileged, sees the host's modules, runs to completion
     # before the agent starts (init container), so the NICs exist when discovery runs.
     inits = [x for x in pod.get("initContainers", []) if x.get("name") != DRIVER_CONTAINER]

@@ -655,6 +655,8 @@ async def _scenario(tmp: Path, n_nics: int, mode: str, seed: int, interval: str,
                     art = node.host_path("/etc/amd/scale-out")
                     res["artifacts_after_cleanup"] = sorted(os.listdir(art)) if art.exists() else []
                 res["after_delete"] = {nif: rt.addr_list(rt.link_by_name(nif)["index"]) for nif in nic_names}
+                res["links_up_after_delete"] = {nif: rt.link_by_name(nif)["up"] for nif in nic_names}
+                res["link_state_after_delete"] = node.host_path("/etc/amd/scale-out/link-state").exists()
                 res["agent_exit_codes"] = [e["rc"] for e in node.exited]
                 res["agent_sigterm_to_exit_s"] = [e["sigterm_to_exit_s"] for e in node.exited]
     finally:

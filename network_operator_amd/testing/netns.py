@@ -317,7 +317,7 @@ def run_scenario(n_nics: int = 8, mode: str = "L3", seed: int | None = None, int
                  soak_cycles: int = 0, arp_silent_ports: int = 0, switch_name: str = "",
                  port_switch_names: dict | None = None, nic_speeds_mbps: list | None = None,
                  switch_max_frame: int = 0, dark_port: int | None = None,
-                 dark_port_up_after: float | None = None) -> dict:
+                 dark_port_up_after: float | None = None, kill_mid_config: int = 0) -> dict:
     """Runs one node bring-up.  Must already be inside a private user+net namespace.
 
     nm_bus: run the agent with --disable-networkmanager against a real ``dbus-daemon`` on which a
@@ -330,7 +330,12 @@ def run_scenario(n_nics: int = 8, mode: str = "L3", seed: int | None = None, int
     dark_port: that switch port is down when the agent starts (the NIC has no carrier); once the
     agent has said why it is not ready, the port comes up and the label must follow.
     dark_port_up_after: instead, the port comes up that many seconds after the agent started (an
-    optic still training its link); every reason and status the agent wrote meanwhile is kept."""
+    optic still training its link); every reason and status the agent wrote meanwhile is kept.
+
+    kill_mid_config: SIGKILL the agent that many times part-way through configuring the node
+    (after 1, 2, ... of its NICs are configured, by its own log) and start it again each time;
+    the last start runs to readiness and is what the result describes.  ``mid_config_kills``
+    records the state each kill left behind."""
     from . import fakesysfs
 
     nat = _native()
@@ -392,7 +397,8 @@ def run_scenario(n_nics: int = 8, mode: str = "L3", seed: int | None = None, int
                 f"--wait={wait}", f"--rccl-net={tmp / 'rccl-net.json'}", f"--rccl-env={tmp / 'rccl.env'}",
                 f"--rccl-topo={tmp / 'rccl-topo.xml'}", f"--status-file={tmp / 'status.json'}", f"--nfd-features-dir={feat}", f"--xgmi-expect={xgmi_expect}",
                 f"--pipeline={'true' if pipeline else 'false'}", f"--lldp-announce={'true' if announce else 'false'}",
-                f"--systemd-networkd={tmp / 'networkd'}", f"-v={verbose}", *(extra_args or [])]
+                f"--systemd-networkd={tmp / 'networkd'}", f"--link-state={tmp / 'link-state'}", f"-v={verbose}",
+                *(extra_args or [])]
         if lldp_cache:
             args.append(f"--lldp-cache={tmp / 'lldp-cache'}")
         env = dict(os.environ, SYSFS_ROOT=str(tmp / "sys"), NODE_NAME="mi355x-node-0")
@@ -421,6 +427,29 @@ def run_scenario(n_nics: int = 8, mode: str = "L3", seed: int | None = None, int
         t0 = time.monotonic()
         agent = spawn()
         budget = 5.0 + float(wait.rstrip("s"))
+        mid_kills = []
+        for k in range(kill_mid_config):
+            # An OOM kill or a node-agent crash half-way: some NICs have their address (and rail
+            # rule and table), the rest nothing.  Progress is read from this run's own log, since
+            # the addresses of earlier runs are still on the links.
+            want = 1 + k % max(1, len(nic_names) - 1)
+            start = agent_log.stat().st_size if agent_log.exists() else 0
+            done = 0
+            end = time.monotonic() + budget
+            while time.monotonic() < end and agent.poll() is None and done < want:
+                with open(agent_log, errors="replace") as f:
+                    f.seek(start)
+                    tail = f.read()
+                done = tail.count("Configured address and route") + tail.count("already configured with address")
+                time.sleep(0.0005)
+            agent.kill()
+            agent.wait()
+            addressed = sum(1 for n in nic_names if rt.addr_list(rt.link_by_name(n)["index"]))
+            rules = [r for r in rt.rule_list() if 0 < r["priority"] < 32766]
+            mid_kills.append({"after_configured": done, "wanted": want, "nics_with_address": addressed,
+                              "rules": len(rules), "label": label.exists(), "rc": agent.returncode})
+            t0 = time.monotonic()
+            agent = spawn()
         dark: dict = {}
         if dark_port is not None and dark_port_up_after is not None:
             reason, status = tmp / "status.json.not-ready", tmp / "status.json"
@@ -481,6 +510,8 @@ def run_scenario(n_nics: int = 8, mode: str = "L3", seed: int | None = None, int
         res["latency_s"] = (t_ready - t0) if t_ready else None
         if dark:
             res["dark"] = dark
+        if kill_mid_config:
+            res["mid_config_kills"] = mid_kills
         try:  # CPU of the process so far (coarse: clock ticks; the status has getrusage at readiness)
             f = Path(f"/proc/{agent.pid}/stat").read_text().rsplit(")", 1)[1].split()
             res["agent_cpu_ms"] = (int(f[11]) + int(f[12])) * 1000.0 / os.sysconf("SC_CLK_TCK")
@@ -652,6 +683,7 @@ def run_scenario(n_nics: int = 8, mode: str = "L3", seed: int | None = None, int
         res["after_sigterm"] = after
         res["rules_after_sigterm"] = [r for r in rt.rule_list() if 0 < r["priority"] < 32766]
         res["label_after_sigterm"] = label.exists()
+        res["link_state_left"] = (tmp / "link-state").exists()
         if nm is not None:
             res["nm_keyfile_after_sigterm"] = keyfile.exists()
             res["nm_managed_after_sigterm"] = dict(nm.devices)

@@ -34,7 +34,8 @@ def test_l3_policy_labels_the_node_and_deletion_undoes_it():
     assert labels["amd.feature.node.kubernetes.io/gpu-scale-out.mode"] == "L3"
     assert labels["amd.feature.node.kubernetes.io/gpu-scale-out.nics"] == "4"
     _check_nics(r, "L3")
-    assert r["artifacts"] == ["rccl-net.json", "rccl-topo.xml", "rccl-topo.xml.key", "rccl.env"]
+    # link-state: the NICs' up/down from before the agent, for whoever puts them back.
+    assert r["artifacts"] == ["link-state", "rccl-net.json", "rccl-topo.xml", "rccl-topo.xml.key", "rccl.env"]
     # The operator measured the node's readiness itself (agent Pod seen -> Ready).
     m = r["operator_metrics"]
     assert m['amd_network_operator_agent_ready_seconds_count{policy="scale-out"}'] == 1
@@ -45,6 +46,7 @@ def test_l3_policy_labels_the_node_and_deletion_undoes_it():
     # Deletion: garbage collection -> SIGTERM -> addresses and the Node label gone.
     assert r["delete_to_agent_stopped_s"] is not None and r["delete_to_label_removed_s"] is not None
     assert all(a == [] for a in r["after_delete"].values())
+    assert not any(r["links_up_after_delete"].values()) and not r["link_state_after_delete"]
     assert r["agent_exit_codes"] == [0] and r["operator_rc"] == 0
 
 
@@ -53,7 +55,7 @@ def test_l2_policy_labels_the_node():
     assert r["policy_to_all_good_s"] is not None, (r["policy_status"], r["agent_log"])
     assert r["node_labels"]["amd.feature.node.kubernetes.io/gpu-scale-out.mode"] == "L2"
     _check_nics(r, "L2")
-    assert r["artifacts"] == ["rccl-topo.xml", "rccl-topo.xml.key", "rccl.env"]
+    assert r["artifacts"] == ["link-state", "rccl-topo.xml", "rccl-topo.xml.key", "rccl.env"]
     assert all(a == [] for a in r["after_delete"].values())
 
 
@@ -82,6 +84,9 @@ def test_keep_config_rolls_the_agent_without_touching_the_addresses_and_deletion
     assert r["delete_to_cleaned_and_policy_gone_s"] is not None, (r["agent_log"], r.get("cleanup_job_runs"))
     assert [j["rc"] for j in r["cleanup_job_runs"]] == [0]
     assert all(a == [] for a in r["after_delete"].values())
+    # The agent left the links up for the next one (--keep-config); the Job took them down from
+    # the record, as they were before any agent.
+    assert not any(r["links_up_after_delete"].values())
     assert r["artifacts_after_cleanup"] == []
 
 

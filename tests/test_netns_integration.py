@@ -539,3 +539,32 @@ def test_l3_reports_waiting_for_carrier_while_a_port_trains():
     assert any(f"{dark_nic}: waiting for carrier" in x for x in d["reasons_seen"]), (d["reasons_seen"], r["agent_log"])
     assert not any("no carrier" in x for x in d["reasons_seen"])
     assert r["ready"] and d["port_up_to_label_s"] is not None and d["port_up_to_label_s"] < 1.5, r["agent_log"]
+
+
+def test_agent_killed_part_way_through_configuring_converges_on_restart():
+    """SIGKILL (OOM kill, crash) after 1, 2, then 3 of 4 NICs are configured, rail tables on,
+    each time restarted over what the dead agent left: the last start reaches exactly the state
+    of a clean bring-up -- one address, one /30 and one /16 per NIC, one source rule and two
+    table routes per rail, nothing doubled -- and SIGTERM still removes all of it, links included.  The switch
+    sends periodic frames only, at a random phase per port, so the NICs configure one by one."""
+    r = netns.run_isolated(n_nics=4, seed=31, interval="1s", phase="random", fast_start=False,
+                           kill_mid_config=3, extra_args=["--rail-table-base=100"])
+    _check_configured(r)
+    kills = r["mid_config_kills"]
+    assert [k["wanted"] for k in kills] == [1, 2, 3], kills
+    assert not any(k["label"] for k in kills), kills
+    assert any(0 < k["nics_with_address"] < 4 for k in kills), kills
+    for nic in r["nics"]:
+        keys = [(x["dst"], x["gateway"]) for x in r["state"][nic]["routes"]]
+        assert len(keys) == len(set(keys)) == 2, keys
+    rules = r["rules"]
+    assert sorted(x["priority"] for x in rules) == [100, 101, 102, 103], rules
+    assert sorted(x["src"] for x in rules) == sorted(p["local"] + "/32" for p in r["plan"]), rules
+    for table, routes in r["rail_tables"].items():
+        assert len(routes) == 2, (table, routes)
+    assert r["agent_rc"] == 0 and not r["label_after_sigterm"] and r["rules_after_sigterm"] == []
+    # Down again, as before the first agent: the restarted agent found them up, and only the
+    # --link-state record (the operator passes it) says otherwise.  The record goes with them.
+    for nic in r["nics"]:
+        assert r["after_sigterm"][nic] == {"up": False, "addrs": []}
+    assert not r["link_state_left"]

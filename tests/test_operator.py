@@ -12,6 +12,7 @@ import contextlib
 import pytest
 
 from network_operator_amd.api.v1alpha1 import types as T
+from network_operator_amd import discovery
 from network_operator_amd.operator import kube
 from network_operator_amd.operator.controller import PolicyController
 from network_operator_amd.operator.kube import ApiClient, ApiError, KubeConfig
@@ -21,6 +22,8 @@ from network_operator_amd.testing.fakeapi import FakeApiServer
 
 TOPO_ARGS = ["--rccl-topo=/host/etc/amd/scale-out/rccl-topo.xml", "--rccl-topo-env-path=/etc/amd/scale-out/rccl-topo.xml"]
 STATUS_ARG = "--status-file=/run/amd-network-agent/status.json"  # the probe prints why a node is not ready
+LINK_STATE_ARG = "--link-state=/host/etc/amd/scale-out/link-state"  # the NICs' up/down from before any agent
+HOST_NIC_LINK_STATE_ARG = "--link-state=/host/etc/amd/scale-out/host-nic-link-state"
 
 NS = "amd-network-operator"
 
@@ -122,7 +125,8 @@ def test_reconcile_lifecycle_reference_parity():
                 assert len(c) == 1 and c[0]["image"] == "amd/my-linkdiscovery:latest"
                 assert c[0]["args"] == ["--configure=true", "--keep-running", "--mode=L3", "--mtu=8000", "--wait=90s",
                                         "--rccl-net=/host/etc/amd/scale-out/rccl-net.json",
-                                        "--rccl-env=/host/etc/amd/scale-out/rccl.env", *TOPO_ARGS, STATUS_ARG]
+                                        "--rccl-env=/host/etc/amd/scale-out/rccl.env", *TOPO_ARGS, LINK_STATE_ARG,
+                                        STATUS_ARG]
                 assert [v["name"] for v in pod["volumes"]] == ["nfd-features", "agent-run", "rccl-artifacts"]
                 assert [m["name"] for m in c[0]["volumeMounts"]] == ["nfd-features", "agent-run", "rccl-artifacts"]
                 assert pod["nodeSelector"] == {"foo": "bar"}
@@ -143,7 +147,8 @@ def test_reconcile_lifecycle_reference_parity():
                 ds = fake.get_object(kube.DAEMONSETS, "policy", NS)
                 c = ds["spec"]["template"]["spec"]["containers"][0]
                 assert c["args"] == ["--configure=true", "--keep-running", "--mode=L2",
-                                     "--rccl-env=/host/etc/amd/scale-out/rccl.env", *TOPO_ARGS, STATUS_ARG]
+                                     "--rccl-env=/host/etc/amd/scale-out/rccl.env", *TOPO_ARGS, LINK_STATE_ARG,
+                                     STATUS_ARG]
                 assert [v["name"] for v in ds["spec"]["template"]["spec"]["volumes"]] == ["nfd-features", "agent-run",
                                                                                           "rccl-artifacts"]
             await eventually(l2_ok)
@@ -294,8 +299,8 @@ def test_agent_args_mi355x_options():
     p = T.new_policy("x", layer="L3", xgmiCheck=True, lldpAnnounce=False, interfaces=["ens1", "ens2"],
                      nicDrivers=["mlx5_core"])
     a = agent_args(p)
-    assert a[-5:] == ["--xgmi-expect=0", "--lldp-announce=false", "--interfaces=ens1,ens2", "--nic-drivers=mlx5_core",
-                      STATUS_ARG]
+    assert a[-6:] == ["--xgmi-expect=0", "--lldp-announce=false", "--interfaces=ens1,ens2", "--nic-drivers=mlx5_core",
+                      LINK_STATE_ARG, STATUS_ARG]
 
 
 def test_leader_election_single_active_and_failover():
@@ -909,7 +914,8 @@ def test_host_nic_keep_config_args_volume_and_cleanup():
 
     p = T.new_host_nic_policy("hosts", layer="L3", keepConfigOnRestart=True, nicDrivers=["mlx5_core"])
     args = R.host_nic_agent_args(p)
-    assert args[-3:] == ["--lldp-cache=/host/etc/amd/scale-out/host-nic-lldp-cache", "--keep-config", STATUS_ARG]
+    assert args[-4:] == ["--lldp-cache=/host/etc/amd/scale-out/host-nic-lldp-cache", "--keep-config",
+                         HOST_NIC_LINK_STATE_ARG, STATUS_ARG]
     assert R.keeps_config(p) and R.needs_node_cleanup(p)
     job = R.cleanup_job(p, "n0", NS)
     spec = job["spec"]["template"]["spec"]
@@ -917,8 +923,14 @@ def test_host_nic_keep_config_args_volume_and_cleanup():
     assert "--cleanup" in c["args"] and "--keep-config" not in c["args"] and "--nm-restore" not in c["args"]
     assert "--nfd-label-file=host-nic-readiness.txt" in c["args"]  # its own lock, label and keyfile
     assert "rccl-artifacts" in [v["name"] for v in spec["volumes"]]
+    assert HOST_NIC_LINK_STATE_ARG in c["args"]  # what no agent in memory saw goes back from the record
     l2 = T.new_host_nic_policy("hosts", layer="L2", keepConfigOnRestart=True)
-    assert R.host_nic_agent_args(l2)[-2] == "--keep-config" and not any("lldp-cache" in a for a in R.host_nic_agent_args(l2))
+    assert R.host_nic_agent_args(l2)[-3] == "--keep-config" and not any("lldp-cache" in a for a in R.host_nic_agent_args(l2))
+    # The records live on the node whatever the policy says now: a policy that dropped mtu (or
+    # keepConfigOnRestart) still mounts them for the next agent and the cleanup Job.
+    ds = discovery.discovery_daemonset()
+    R.update_daemonset_for(ds, T.new_host_nic_policy("hosts", layer="L2"), NS)
+    assert "rccl-artifacts" in [v["name"] for v in ds["spec"]["template"]["spec"]["volumes"]]
     plain = T.new_host_nic_policy("hosts", layer="L3")
     assert not R.needs_node_cleanup(plain) and "--keep-config" not in R.host_nic_agent_args(plain)
 
