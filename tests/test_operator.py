@@ -1565,7 +1565,22 @@ def test_random_edits_converge_through_api_faults_and_lost_watches(seed):
     _model_check(seed, 0.0, chaos=True)
 
 
-def _model_check(seed, gc_delay, chaos=False):
+@pytest.mark.parametrize("seed", [21, 22, 23, 24])
+def test_random_edits_converge_across_operator_restarts(seed, monkeypatch):
+    """The same model check with the operator stopped at random points -- often mid-reconcile,
+    with writes half done -- and a new one started from nothing but the API server's state (no
+    queue, no hold-off or cleanup memory, fresh informers).  Together with API faults, and with
+    keepConfigOnRestart policies, whose deletion (and whose nodes leaving the selector) runs
+    cleanup Jobs behind a finalizer.  Whatever the old process left, the new one converges to the
+    same model, every deleted policy is gone and no cleanup Job is left unfinished."""
+    from network_operator_amd.operator import reconciler as R
+
+    monkeypatch.setattr(R, "KEPT_ORPHAN_GRACE_S", 0.2)
+    monkeypatch.setattr(R, "CLEANUP_POLL_S", 0.05)
+    _model_check(seed, 0.0, chaos=True, restarts=True, keep_config=True)
+
+
+def _model_check(seed, gc_delay, chaos=False, restarts=False, keep_config=False):
     import random
 
     rng = random.Random(seed)
@@ -1578,6 +1593,7 @@ def _model_check(seed, gc_delay, chaos=False):
         # agents turn ready 20 ms after their Pod is placed, on every DaemonSet the run makes
         async with cluster(openshift=False, workers=3, gc_delay=gc_delay, agent_ready_delay=0.02,
                            user_client="kubectl" if chaos else None) as (fake, client, ctl):
+            live = {"ctl": ctl, "client": None}  # the running operator (restarts replace it)
             nodes = {}
             for i in range(6):
                 labels = {"rack": rng.choice("ab"), **({"gpu": "yes"} if rng.random() < 0.5 else {})}
@@ -1593,7 +1609,19 @@ def _model_check(seed, gc_delay, chaos=False):
                     d = T.new_host_nic_policy(name, layer=layer, node_selector=sel).to_dict()
                 if tols:
                     d["spec"]["tolerations"] = tol
+                if keep_config and rng.random() < 0.4:
+                    d["spec"]["amdScaleOut" if ctype == "amd-so" else "hostNic"]["keepConfigOnRestart"] = True
                 return d, (ctype, layer, sel, tols)
+
+            async def job_controller():
+                # The cleanup Jobs' Pods run on their nodes and finish a little later.
+                while True:
+                    for j in fake.list_objects(kube.JOBS):
+                        if not (j.get("status") or {}).get("conditions"):
+                            with contextlib.suppress(KeyError):
+                                fake.set_job_result(j["metadata"]["name"], j["metadata"]["namespace"], True)
+                    await asyncio.sleep(0.01)
+            jobs_task = asyncio.ensure_future(job_controller()) if keep_config else None
 
             for _ in range(40):
                 op = rng.random()
@@ -1603,7 +1631,12 @@ def _model_check(seed, gc_delay, chaos=False):
                     if name in model:
                         continue
                     body_, m = spec_of(name, rng.choice(["amd-so", "amd-so", "host-nic"]))
-                    await client.create(kube.NETWORKCLUSTERPOLICIES, body_)
+                    try:
+                        await client.create(kube.NETWORKCLUSTERPOLICIES, body_)
+                    except ApiError as e:  # still finalizing after its deletion (keepConfigOnRestart)
+                        if e.status != 409:
+                            raise
+                        continue
                     model[name] = m
                 elif op < 0.55:
                     name = rng.choice(names)
@@ -1625,6 +1658,17 @@ def _model_check(seed, gc_delay, chaos=False):
                     if fake.get_object(kube.DAEMONSETS, name, NS) is not None:
                         with contextlib.suppress(ApiError):
                             await client.delete(kube.DAEMONSETS, name, NS)
+                if restarts and rng.random() < 0.2:
+                    # A crash or a rollout of the operator: whatever the old process was doing
+                    # stops at its next await; the new one starts from the API server alone.
+                    await asyncio.sleep(rng.choice([0.0, 0.001, 0.005, 0.02]))
+                    await live["ctl"].stop()
+                    if live["client"] is not None:
+                        await live["client"].close()
+                    live["client"] = ApiClient(KubeConfig(host=fake.url), user_agent=OPERATOR_UA)
+                    live["ctl"] = PolicyController(live["client"], NS, is_openshift=False, workers=3)
+                    await live["ctl"].start()
+                    chaos_stats["restarts"] = chaos_stats.get("restarts", 0) + 1
                 if chaos and rng.random() < 0.35:
                     c = rng.random()
                     if c < 0.7:  # the operator's next requests of one kind fail
@@ -1656,6 +1700,9 @@ def _model_check(seed, gc_delay, chaos=False):
             def converged():
                 dss = {d["metadata"]["name"] for d in fake.list_objects(kube.DAEMONSETS)}
                 assert dss == set(model), (dss, model)
+                names = {q["metadata"]["name"] for q in fake.list_objects(kube.NETWORKCLUSTERPOLICIES)}
+                assert names == set(model), (names, model)  # finalizers released
+                assert all((j.get("status") or {}).get("conditions") for j in fake.list_objects(kube.JOBS))
                 for name, m in model.items():
                     ctype, layer, sel, tols = m
                     ds = fake.get_object(kube.DAEMONSETS, name, NS)
@@ -1684,7 +1731,19 @@ def _model_check(seed, gc_delay, chaos=False):
                     got = sorted(e.split(" also selected by policy ")[1].split(" ")[0] for e in s["errors"])
                     assert got == others and len(s["errors"]) == len(others), (name, s["errors"], others)
                 return True
-            await eventually(converged, timeout=30 if chaos else 20)
+            try:
+                await eventually(converged, timeout=30 if chaos else 20)
+                if keep_config:
+                    chaos_stats["jobs"] = sum(1 for w in fake.writes if w[2] == "POST" and "/jobs" in w[3])
+                    assert chaos_stats["jobs"] >= 1, chaos_stats  # the finalizer path ran
+            finally:
+                if jobs_task is not None:
+                    jobs_task.cancel()
+                if live["client"] is not None:
+                    await live["ctl"].stop()
+                    await live["client"].close()
+        if restarts:
+            assert chaos_stats.get("restarts", 0) >= 3, chaos_stats
 
     run(body(), timeout=150)
 
