@@ -193,14 +193,15 @@ void Agent::write_status() {
     }
     if (cfg_.status_file.empty()) return;
     try {
-        write_file_atomic(cfg_.status_file, artifacts::generate_status(nics_, phases_, t0_, cfg_.mode, ready_, status_node()) + "\n");
         // Beside it, one line for the readiness probe to print while the node is not ready: the
-        // kubelet records probe output in the Pod's events ("Readiness probe failed: ...").
+        // kubelet records probe output in the Pod's events ("Readiness probe failed: ...").  The
+        // reason goes first: a probe that finds the status file must find the reason as well, or
+        // it reports a bare "label not published" -- not a start-up reason, so the operator would
+        // count a node still starting as degraded.
         const std::string why = ready_ ? "" : not_ready_reason();
-        if (why.empty())
-            ::unlink(reason_path(cfg_.status_file).c_str());
-        else
-            write_file_atomic(reason_path(cfg_.status_file), why + "\n");
+        if (!why.empty()) write_file_atomic(reason_path(cfg_.status_file), why + "\n");
+        write_file_atomic(cfg_.status_file, artifacts::generate_status(nics_, phases_, t0_, cfg_.mode, ready_, status_node()) + "\n");
+        if (why.empty()) ::unlink(reason_path(cfg_.status_file).c_str());
     } catch (const std::exception& e) {
         NLOG_W("Could not write status file: %s", e.what());
     }
