@@ -253,6 +253,8 @@ void Agent::monitor(int stop_fd) {
                 if (cfg_.mode == "L3") write_host_config();
                 announce_all(120);
             } else if (!healthy && labelled) {
+                ready_ = false;
+                write_status();  // the probe's reason first, then the label (see write_status)
                 artifacts::remove_labels(cfg_.labels);
                 labelled = false;
                 NLOG_W("Scale-out degraded: readiness label withdrawn");
