@@ -65,16 +65,34 @@ def _pci(root: Path, pcipath: str, driver: str, vendor: str, device: str, numa: 
     return d
 
 
+# NIC driver -> (PCI vendor id, RDMA device name prefix) for rail_driver.
+RAIL_DRIVERS = {"mlx5_core": ("0x15b3", "mlx5"), "ionic": ("0x1dd8", "ionic"), "bnxt_en": ("0x14e4", "bnxt_re")}
+
+
 def build_mi355x_node(root: Path, nic_names: Optional[Dict[str, str]] = None, nic_macs: Optional[Dict[str, str]] = None,
-                      n_gpus: int = 8, with_kfd: bool = True, drop_xgmi_pairs=()) -> dict:
+                      n_gpus: int = 8, with_kfd: bool = True, drop_xgmi_pairs=(), rail_driver: str = "") -> dict:
     """Writes the tree under ``root``; returns the fixture (with applied renames).
 
     nic_names: {original ifname -> new ifname}; nic_macs: {new ifname -> MAC}.
     drop_xgmi_pairs: iterable of (gpu_i, gpu_j) KFD-order indices whose xGMI link is removed.
     n_gpus < 8: a smaller node of the same layout, so the rails of the GPUs left out (the NICs
     behind their PCIe switches) are left out too.
+    rail_driver: the scale-out NICs (one behind each GPU's PCIe switch) are of this driver, with
+    its RDMA device names (``ionic``: AMD Pollara, ``ionic_<n>``; ``bnxt_en``: ``bnxt_re<n>``)
+    instead of the captured node's ConnectX-7 (``mlx5_core``); the host NICs stay mlx5.
     """
     fx = json.loads(FIXTURE.read_text())
+    if rail_driver:
+        vendor, prefix = RAIL_DRIVERS[rail_driver]
+        rails = {tuple(g["path"].split("/")[:3]) for g in fx["gpus"]}
+        for n in fx["nics"]:
+            if tuple(n["pcipath"].split("/")[:3]) in rails:
+                n.update(driver=rail_driver, vendor=vendor)
+        k = 0
+        for r in sorted(fx["rdma"], key=lambda r: r["dev"]):
+            if tuple(r["pcipath"].split("/")[:3]) in rails:
+                r["dev"] = f"{prefix}_{k}" if prefix != "bnxt_re" else f"{prefix}{k}"
+                k += 1
     nic_names = nic_names or {}
     nic_macs = nic_macs or {}
     root = Path(root)
@@ -90,7 +108,8 @@ def build_mi355x_node(root: Path, nic_names: Optional[Dict[str, str]] = None, ni
         if under in every and under not in built:
             continue  # the rail of a GPU this node does not have
         name = nic_names.get(n["ifname"], n["ifname"])
-        d = _pci(root, n["pcipath"], n["driver"], "0x15b3", "0x1021", 0 if n["pcipath"] < "pci0000:80" else 1, "0x020000")
+        d = _pci(root, n["pcipath"], n["driver"], n.get("vendor", "0x15b3"), "0x1021", 0 if n["pcipath"] < "pci0000:80" else 1,
+                 "0x020000")
         net = d / "net" / name
         _w(net / "address", nic_macs.get(name, n["mac"]) + "\n")
         _w(net / "dev_port", "0\n")

@@ -317,7 +317,7 @@ def run_scenario(n_nics: int = 8, mode: str = "L3", seed: int | None = None, int
                  soak_cycles: int = 0, arp_silent_ports: int = 0, switch_name: str = "",
                  port_switch_names: dict | None = None, nic_speeds_mbps: list | None = None,
                  switch_max_frame: int = 0, dark_port: int | None = None,
-                 dark_port_up_after: float | None = None, kill_mid_config: int = 0) -> dict:
+                 dark_port_up_after: float | None = None, kill_mid_config: int = 0, rail_driver: str = "") -> dict:
     """Runs one node bring-up.  Must already be inside a private user+net namespace.
 
     nm_bus: run the agent with --disable-networkmanager against a real ``dbus-daemon`` on which a
@@ -335,7 +335,9 @@ def run_scenario(n_nics: int = 8, mode: str = "L3", seed: int | None = None, int
     kill_mid_config: SIGKILL the agent that many times part-way through configuring the node
     (after 1, 2, ... of its NICs are configured, by its own log) and start it again each time;
     the last start runs to readiness and is what the result describes.  ``mid_config_kills``
-    records the state each kill left behind."""
+    records the state each kill left behind.
+
+    rail_driver: the scale-out NICs' driver and RDMA names (fakesysfs.build_mi355x_node)."""
     from . import fakesysfs
 
     nat = _native()
@@ -346,7 +348,7 @@ def run_scenario(n_nics: int = 8, mode: str = "L3", seed: int | None = None, int
     rt.link_set_up(rt.link_by_name("lo")["index"])
     tmp = Path(tempfile.mkdtemp(prefix="netop-sim-"))
     try:
-        fx = fakesysfs.build_mi355x_node(tmp / "sys", n_gpus=n_nics,
+        fx = fakesysfs.build_mi355x_node(tmp / "sys", n_gpus=n_nics, rail_driver=rail_driver,
                                          drop_xgmi_pairs=[tuple(p) for p in (drop_xgmi or [])])
         pairs = nat.discover(str(tmp / "sys"))["pairs"]
         nic_names = [p["nic"] for p in pairs][:n_nics]

@@ -14,7 +14,7 @@ from network_operator_amd.testing import netns
 pytestmark = pytest.mark.netns
 
 
-def _check_configured(r):
+def _check_configured(r, rdma_prefix="mlx5_"):
     assert r["ready"], r["agent_log"][-3000:]
     for nic, p in zip(r["nics"], r["plan"]):
         st = r["state"][nic]
@@ -32,7 +32,7 @@ def _check_configured(r):
         e = by_name[nic]
         assert e["NIC_IP"] == p["local"] and e["GATEWAY_IP"] == p["peer"]
         assert e["SUBNET_MASK"] == "255.255.255.252"
-        assert e["GID_INDEX"] == 3 and e["RDMA_DEV"].startswith("mlx5_")
+        assert e["GID_INDEX"] == 3 and e["RDMA_DEV"].startswith(rdma_prefix)
         assert e["PCIE_PATH"] == "PXB" and e["NUMA_NODE"] == (0 if e["GPU_INDEX"] < 4 else 1)
     # GPU order: entry i belongs to GPU i.
     assert [e["GPU_INDEX"] for e in entries] == list(range(len(entries)))
@@ -568,3 +568,16 @@ def test_agent_killed_part_way_through_configuring_converges_on_restart():
     for nic in r["nics"]:
         assert r["after_sigterm"][nic] == {"up": False, "addrs": []}
     assert not r["link_state_left"]
+
+
+@pytest.mark.parametrize("driver,prefix", [("ionic", "ionic_"), ("bnxt_en", "bnxt_re")])
+def test_pollara_and_thor_rails_configure_like_connectx(driver, prefix):
+    """The scale-out NICs of MI355X platforms are often AMD Pollara 400 (ionic) or Broadcom Thor
+    (bnxt_en) rather than ConnectX: the same L3 bring-up, with RCCL told about their RDMA devices
+    (NCCL_IB_HCA in GPU order, RDMA_DEV per rail).  The host NICs stay mlx5 and are left alone."""
+    r = netns.run_isolated(n_nics=4, seed=41, interval="30s", fast_start=True, rail_driver=driver)
+    _check_configured(r, rdma_prefix=prefix)
+    hca = [l for l in r["rccl_env"].splitlines() if l.startswith("NCCL_IB_HCA=")]
+    by_gpu = sorted(r["rccl_net"]["NIC_NET_CONFIG"], key=lambda e: e["GPU_INDEX"])
+    assert hca == ["NCCL_IB_HCA==" + ",".join(f"{e['RDMA_DEV']}:1" for e in by_gpu)], (hca, by_gpu)
+    assert "mlx5_" not in hca[0]
