@@ -89,8 +89,9 @@ bench-e2e:                  ## policy created -> Node labelled / status All good
 fmt:                        ## clang-format the native sources (if installed)
 	@command -v clang-format >/dev/null && clang-format -i native/src/*.cpp native/include/netop/*.hpp native/tests/*.cpp native/tools/*.cpp || echo "clang-format not installed"
 
-vet:                        ## byte-compile Python, warnings-as-errors C++ build of the agent
+vet:                        ## byte-compile and check Python (tools/pycheck.py), warnings-as-errors C++ build of the agent
 	$(PYTHON) -m compileall -q network_operator_amd bench bench.py __graft_entry__.py
+	$(PYTHON) tools/pycheck.py
 	cmake -S native -B _build-vet -G Ninja -DNETOP_PYTHON=OFF -DCMAKE_CXX_FLAGS=-Werror -DNETOP_OUT=$(CURDIR)/_build-vet/out && \
 	cmake --build _build-vet -j$(JOBS)
 

@@ -476,7 +476,7 @@ class FakeApiServer:
         if res == kube.DAEMONSETS:
             obj["status"] = {"currentNumberScheduled": 0, "desiredNumberScheduled": 0, "numberMisscheduled": 0,
                              "numberReady": 0, "observedGeneration": 1}
-        stored = self._store(res, obj, "ADDED")
+        self._store(res, obj, "ADDED")
         self._live_uids.add(md["uid"])
         if res in (kube.DAEMONSETS, kube.NODES):
             self._sync_daemonsets()
@@ -1094,7 +1094,7 @@ class FakeApiServer:
         if cur["metadata"].get("deletionTimestamp") and not out["metadata"].get("finalizers"):
             self._store(res, out, "MODIFIED")
             return self._delete(res, name, key[0])  # the last finalizer is gone
-        stored = self._store(res, out, "MODIFIED")
+        self._store(res, out, "MODIFIED")
         if res in (kube.DAEMONSETS, kube.NODES) and sub != "status":
             self._sync_daemonsets()
         return self._table(res)[key]
