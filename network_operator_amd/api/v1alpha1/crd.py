@@ -397,6 +397,34 @@ def validate(obj: dict) -> List[str]:
     return [e[1:] if e.startswith(".") else e for e in errs]
 
 
+def missing_fields(installed: dict) -> List[str]:
+    """Property paths of this release's schema that an installed CRD object lacks, e.g.
+    ``spec.amdScaleOut.carrierWait``.  Helm installs ``crds/`` once and never upgrades it, so
+    after ``helm upgrade`` the API server keeps the old schema and silently drops every new field
+    a user sets (structural pruning, before any webhook sees the object)."""
+    want = openapi_schema()
+    have = next((v.get("schema", {}).get("openAPIV3Schema") for v in (installed.get("spec") or {}).get("versions") or []
+                 if v.get("name") == T.VERSION), None)
+    if have is None:
+        return [f"version {T.VERSION}"]
+    out: List[str] = []
+
+    def walk(w: dict, h: dict, path: str) -> None:
+        if h.get("x-kubernetes-preserve-unknown-fields"):
+            return  # the installed schema keeps anything here
+        for k, ws in (w.get("properties") or {}).items():
+            hs = (h.get("properties") or {}).get(k)
+            if hs is None:
+                out.append(path + k)
+            else:
+                walk(ws, hs, path + k + ".")
+        for key in ("items", "additionalProperties"):
+            if isinstance(w.get(key), dict) and isinstance(h.get(key), dict):
+                walk(w[key], h[key], path + ("[]." if key == "items" else "*."))
+    walk(want, have, "")
+    return out
+
+
 def main(argv=None) -> int:
     root = Path(__file__).resolve().parents[3]
     text = render_yaml()

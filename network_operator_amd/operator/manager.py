@@ -19,8 +19,9 @@ import signal
 import sys
 from typing import Dict, List, Optional
 
+from . import kube, rbac
 from .controller import PolicyController
-from .kube import ApiClient, load_config
+from .kube import ApiClient, ApiError, load_config
 from .leader import DEFAULT_LEASE_ID, LeaderElector, unsafe_timings
 from .metrics import OperatorMetrics
 from .seeder import PolicySeeder
@@ -47,12 +48,39 @@ async def check_dependencies(client: ApiClient) -> Dict[str, bool]:
     return {name: group in groups for name, group in DEPENDENCIES.items()}
 
 
+async def check_crd(client: ApiClient) -> Optional[List[str]]:
+    """Fields of this release's schema the installed CRD lacks (crd.missing_fields), or None when
+    the CRD cannot be read (RBAC of an older release, not installed)."""
+    from ..api.v1alpha1 import crd as crd_schema
+
+    try:
+        installed = await client.get(kube.CRDS, rbac.CRD_NAME, timeout=5.0)
+    except ApiError as e:
+        log.debug("cannot read CRD %s: %s", rbac.CRD_NAME, e)
+        return None
+    return crd_schema.missing_fields(installed)
+
+
 async def watch_dependencies(client: ApiClient, controller, metrics, stop: asyncio.Event, interval: float,
                              webhooks: bool) -> None:
     """Checks the cluster add-ons now and every `interval` seconds; on a change the policies are
-    reconciled again so their status reflects it."""
+    reconciled again so their status reflects it.  Also whether the installed CRD is as new as
+    the operator: Helm never upgrades a chart's crds/."""
     last: Optional[Dict[str, bool]] = None
+    last_missing: Optional[List[str]] = None
     while not stop.is_set():
+        try:
+            missing = await check_crd(client)
+            if missing is not None:
+                metrics.crd_missing_fields.set(len(missing))
+                if missing and missing != last_missing:
+                    log.error("the installed CRD %s predates this operator: the API server drops %s from every "
+                              "policy; apply the CRD of this release (kubectl apply -f charts/network-operator/crds/ or "
+                              "config/operator/crd/bases/): helm upgrade never updates crds/",
+                              rbac.CRD_NAME, ", ".join(missing[:10]) + (" ..." if len(missing) > 10 else ""))
+                last_missing = missing
+        except Exception as e:
+            log.debug("CRD check failed: %s", e)
         try:
             present = await check_dependencies(client)
             for name, ok in present.items():

@@ -54,6 +54,9 @@ class OperatorMetrics:
         self.node_cleanups = Counter("amd_network_operator_node_cleanups_total",
                                      "Node cleanup Jobs that ended, by outcome (succeeded, failed, timed_out)",
                                      ["policy", "outcome"], registry=r)
+        self.crd_missing_fields = Gauge("amd_network_operator_crd_missing_fields",
+                                        "Fields of this release's NetworkClusterPolicy schema the installed CRD lacks "
+                                        "(helm upgrade never updates crds/: apply the release's CRD)", registry=r)
         self.seed_in_sync = Gauge("amd_network_operator_policies_file_in_sync",
                                   "1 when the policies of --policies-file (the Helm release's) match the cluster",
                                   registry=r)

@@ -59,6 +59,16 @@ def policy_owner_rule(cluster_role: str) -> dict:
             "resourceNames": [cluster_role]}
 
 
+# The installed NetworkClusterPolicy CRD, read to tell when it is older than the operator (Helm
+# never upgrades crds/; manager.py::check_crd).  Scoped to that one object by resourceNames.
+CRD_NAME = "networkclusterpolicies.amd.com"
+
+
+def crd_read_rule() -> dict:
+    return {"apiGroups": ["apiextensions.k8s.io"], "resources": ["customresourcedefinitions"], "verbs": ["get"],
+            "resourceNames": [CRD_NAME]}
+
+
 # Aggregated user-facing roles for NetworkClusterPolicy.
 POLICY_EDITOR_RULES = (
     ("amd.com", ("networkclusterpolicies",), READ + WRITE),

@@ -167,6 +167,65 @@ def test_dependency_check_reports_missing_nfd(monkeypatch):
     asyncio.run(body())
 
 
+def test_an_installed_crd_older_than_the_operator_is_reported(monkeypatch, capsys):
+    """helm upgrade never updates a chart's crds/: after an upgrade the API server keeps the old
+    schema and silently drops every new field (carrierWait, in round 5) from the policies users
+    write.  The operator compares the installed CRD with its own schema, logs the fields and the
+    fix, and exports their count (alert NetworkOperatorCrdOutdated); applying the CRD clears it."""
+    import copy
+
+    from network_operator_amd.api.v1alpha1 import crd
+
+    monkeypatch.setenv("OPERATOR_NAMESPACE", "netop-test")
+    monkeypatch.setenv("ENABLE_WEBHOOKS", "false")
+    probe, metrics = _free_port(), _free_port()
+    current = crd.crd_manifest()
+    old = copy.deepcopy(current)
+    props = old["spec"]["versions"][0]["schema"]["openAPIV3Schema"]["properties"]["spec"]["properties"]
+    for section in ("amdScaleOut", "hostNic"):
+        del props[section]["properties"]["carrierWait"]
+    assert crd.missing_fields(old) == ["spec.amdScaleOut.carrierWait", "spec.hostNic.carrierWait"]
+    assert crd.missing_fields(current) == []
+
+    async def gauge():
+        async with aiohttp.ClientSession() as s:
+            async with s.get(f"http://127.0.0.1:{metrics}/metrics") as r:
+                text = await r.text()
+        return next((line.split()[-1] for line in text.splitlines()
+                     if line.startswith("amd_network_operator_crd_missing_fields ")), None)
+
+    async def body():
+        fake = FakeApiServer(extra_groups=["cert-manager.io", "nfd.k8s-sigs.io"])
+        url = await fake.start()
+        async with ApiClient(KubeConfig(host=url)) as c:
+            await c.create(kube.CRDS, old)
+            stop, started = asyncio.Event(), asyncio.Event()
+            task = asyncio.ensure_future(manager.run(
+                ["--master", url, f"--health-probe-bind-address=127.0.0.1:{probe}",
+                 f"--metrics-bind-address=127.0.0.1:{metrics}", "--dependency-check-interval=0.1"],
+                stop=stop, started=started))
+            await asyncio.wait_for(started.wait(), 10)
+            for _ in range(100):
+                if await gauge() == "2.0":
+                    break
+                await asyncio.sleep(0.05)
+            assert await gauge() == "2.0"
+            cur = await c.get(kube.CRDS, "networkclusterpolicies.amd.com")
+            await c.replace(kube.CRDS, dict(current, metadata=cur["metadata"]))
+            for _ in range(100):
+                if await gauge() == "0.0":
+                    break
+                await asyncio.sleep(0.05)
+            assert await gauge() == "0.0"
+            stop.set()
+            assert await asyncio.wait_for(task, 10) == 0
+        await fake.stop()
+
+    asyncio.run(body())  # (the manager's logging.basicConfig(force=True) writes to the captured stderr)
+    logged = [line for line in capsys.readouterr().err.splitlines() if "predates this operator" in line]
+    assert len(logged) == 1 and "spec.amdScaleOut.carrierWait" in logged[0] and "kubectl apply" in logged[0], logged
+
+
 def test_operator_memory_within_deployment_limit(tmp_path):
     """The manager (+ the in-process fake API server, 50 nodes, 10 policies) stays far below the
     Deployment's 128Mi limit (reference config/operator/manager/manager.yaml:95-101)."""
@@ -299,7 +358,8 @@ def test_operator_requests_stay_within_generated_rbac(tmp_path, monkeypatch):
         return fake.accesses
 
     accesses = asyncio.run(asyncio.wait_for(body(), 60))
-    granted = rbac.rules(rbac.OPERATOR_CLUSTER_RULES + rbac.LEADER_ELECTION_RULES + rbac.METRICS_AUTH_RULES)
+    granted = rbac.rules(rbac.OPERATOR_CLUSTER_RULES + rbac.LEADER_ELECTION_RULES + rbac.METRICS_AUTH_RULES) + \
+        [rbac.crd_read_rule()]
     denied = sorted(a for a in accesses if not rbac.allows(granted, *a))
     assert not denied, denied
     # The audit saw the interesting paths (not a vacuous pass).
