@@ -78,6 +78,11 @@ struct Config {
     // leaves Managed=false in place too.  For handing the NICs back when the policy goes.
     bool nm_restore = false;
     int xgmi_expect_links = -1;          // -1 off; 0 = full mesh among discovered GPUs; N = exact pairs
+    // With the xGMI check, the links' trained state from gpu_metrics (topo::XgmiLinkHealth): a link
+    // down fails the check; a width below this (lanes, 0 = any) too.  The monitor reads the state
+    // again every xgmi_health_interval_ns and withdraws the label while a link is down.
+    int xgmi_min_link_width = 0;
+    int64_t xgmi_health_interval_ns = 5LL * 1000000000;
     int64_t link_wait_ns = 3LL * 1000000000;  // netlink echo wait (network.go:251)
     // L2: how long a NIC that is admin-up may train its link before it counts as "no carrier".
     // Separate from the 3 s echo wait: 200/400G optics with FEC and link training commonly take
@@ -420,6 +425,10 @@ class Agent {
     std::future<TopoResult> topo_future_;
     std::optional<TopoResult> topo_;
     topo::XgmiReport xgmi_;
+    std::vector<topo::XgmiLinkHealth> xgmi_health_;
+    std::string xgmi_error_;  // what the last gpu_metrics read found wrong (empty: fine or not read)
+    void read_xgmi_health();
+    std::string xgmi_health_problem() const;
     topo::GdrReport gdr_;
     void check_gdr();
     std::map<std::string, std::string> status_node() const;

@@ -182,6 +182,29 @@ struct XgmiReport {
 
 XgmiReport read_xgmi(const std::string& root = sysfs_root());
 
+// The trained state of one GPU's xGMI links, from amdgpu's gpu_metrics blob (sysfs, readable
+// without privileges): what amd-smi reports as link status, width and bit rate, read without the
+// library.  KFD's topology (read_xgmi) says which links exist; this says whether they are up and
+// at what width.  The blob's layout is versioned (format.content); only revisions this reader
+// knows are decoded -- 1.8, which MI355X firmware reports (layout checked against amd-smi on a
+// live node: tests/fixtures/gpu_metrics_v1_8.bin) -- anything else is reported as not read.
+constexpr int kMaxXgmiLinks = 8;
+struct XgmiLinkHealth {
+    std::string bdf;
+    std::string revision;          // "1.8"
+    bool known = false;            // decoded (a known revision, not truncated)
+    std::string error;             // why not
+    int width = 0;                 // lanes per link
+    int speed_gbps = 0;            // per-lane rate (amd-smi's bit_rate)
+    std::vector<int> status;       // per link slot: 1 up, 0 down, -1 no link in this slot
+    std::vector<uint64_t> read_kb, write_kb;  // accumulated traffic per slot
+    int links_up() const;
+    int links_down() const;
+};
+XgmiLinkHealth parse_gpu_metrics(const std::string& blob);
+// One entry per BDF, from <root>/bus/pci/devices/<bdf>/gpu_metrics.
+std::vector<XgmiLinkHealth> read_xgmi_health(const std::string& root, const std::vector<std::string>& bdfs);
+
 // GPUDirect RDMA readiness: can the RoCE NICs DMA straight into MI355X HBM?  Without it RCCL
 // stages every inter-node transfer through host memory, costing bandwidth and latency.
 // Two mechanisms exist on ROCm:

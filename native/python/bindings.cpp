@@ -350,6 +350,23 @@ PYBIND11_MODULE(_netop_native, m) {
         d["missing"] = miss;
         return d;
     });
+    m.def("read_xgmi_health", [](const std::string& root, const std::vector<std::string>& bdfs) {
+        py::list out;
+        for (const auto& h : topo::read_xgmi_health(root, bdfs)) {
+            py::dict d;
+            d["bdf"] = h.bdf;
+            d["revision"] = h.revision;
+            d["known"] = h.known;
+            d["error"] = h.error;
+            d["width"] = h.width;
+            d["speed_gbps"] = h.speed_gbps;
+            d["status"] = h.status;
+            d["read_kb"] = h.read_kb;
+            d["write_kb"] = h.write_kb;
+            out.append(d);
+        }
+        return out;
+    });
     m.def("detect_gdr", [](const std::string& root, const std::string& kernel) {
         auto g = topo::detect_gdr(root, kernel);
         py::dict d;

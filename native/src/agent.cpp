@@ -332,8 +332,47 @@ void Agent::check_xgmi() {
     NLOG_I("xGMI: %zu GPUs, %d/%d GPU pairs linked, %llu MB/s per GPU advertised", xgmi_.gpus.size(), xgmi_.pairs_connected,
            xgmi_.pairs_expected, (unsigned long long)xgmi_.per_gpu_bw_mbs());
     for (auto& [a, b] : xgmi_.missing) NLOG_W("xGMI: no link between %s and %s", a.c_str(), b.c_str());
+    // A dry run reports what a real start would fail on (status.json, the log) and goes on.
+    auto fail = [&](const std::string& why) {
+        if (!cfg_.dry_run) throw AgentError(why);
+        NLOG_W("dry run: a real start would fail: %s", why.c_str());
+    };
     if (xgmi_.pairs_connected < expect)
-        throw AgentError(strfmt("xGMI mesh incomplete: %d of %d GPU pairs linked", xgmi_.pairs_connected, expect));
+        fail(strfmt("xGMI mesh incomplete: %d of %d GPU pairs linked", xgmi_.pairs_connected, expect));
+    read_xgmi_health();
+    for (const auto& h : xgmi_health_) {
+        if (h.known)
+            NLOG_I("xGMI %s: %d link(s) up, %d down, x%d at %d Gb/s (gpu_metrics %s)", h.bdf.c_str(), h.links_up(),
+                   h.links_down(), h.width, h.speed_gbps, h.revision.c_str());
+        else
+            NLOG_V(1, "xGMI %s: %s", h.bdf.c_str(), h.error.c_str());
+    }
+    if (!xgmi_error_.empty()) fail("xGMI: " + xgmi_error_);
+}
+
+void Agent::read_xgmi_health() {
+    std::string root = cfg_.sysfs_root.empty() ? topo::sysfs_root() : cfg_.sysfs_root;
+    std::vector<std::string> bdfs;
+    for (const auto& g : xgmi_.gpus)
+        if (g.is_gpu()) bdfs.push_back(g.bdf());
+    xgmi_health_ = topo::read_xgmi_health(root, bdfs);
+    xgmi_error_ = xgmi_health_problem();
+}
+
+std::string Agent::xgmi_health_problem() const {
+    std::vector<std::string> parts;
+    for (const auto& h : xgmi_health_) {
+        if (!h.known) continue;
+        std::vector<std::string> down;
+        for (size_t i = 0; i < h.status.size(); ++i)
+            if (h.status[i] == 0) down.push_back(std::to_string(i));
+        if (!down.empty())
+            parts.push_back(strfmt("GPU %s: link%s %s down", h.bdf.c_str(), down.size() > 1 ? "s" : "", join(down, ", ").c_str()));
+        else if (cfg_.xgmi_min_link_width > 0 && h.links_up() > 0 && h.width < cfg_.xgmi_min_link_width)
+            parts.push_back(strfmt("GPU %s: links trained at x%d, below the required x%d", h.bdf.c_str(), h.width,
+                                   cfg_.xgmi_min_link_width));
+    }
+    return join(parts, "; ");
 }
 
 

@@ -114,6 +114,10 @@ void Agent::monitor(int stop_fd) {
     for (auto& n : nics_) carrier[n.link.index] = n.link.lower_up();
     int64_t next_tx = mono_ns() + cfg_.lldp_tx_interval_ns;
     int64_t next_verify = 0;
+    // The GPUs' xGMI links (gpu_metrics): only when the xGMI check runs and the layout is known.
+    const bool xgmi_watch = cfg_.xgmi_expect_links >= 0 && cfg_.xgmi_health_interval_ns > 0 &&
+                            std::any_of(xgmi_health_.begin(), xgmi_health_.end(), [](const topo::XgmiLinkHealth& h) { return h.known; });
+    int64_t next_xgmi = mono_ns() + cfg_.xgmi_health_interval_ns;
     bool labelled = ready_;  // false: L2 came up with a NIC still without carrier
     // One pollable fd for "stop or link event": the LLDP wait returns as soon as either
     // fires, so a link failure is acted on in about a millisecond, not at the next tick.
@@ -224,6 +228,18 @@ void Agent::monitor(int stop_fd) {
             write_status();
             throw AgentError("Interface '" + removed + "' was removed");
         }
+        if (xgmi_watch && mono_ns() >= next_xgmi) {
+            const std::string before = xgmi_error_;
+            read_xgmi_health();
+            if (xgmi_error_ != before) {
+                if (xgmi_error_.empty())
+                    NLOG_I("xGMI links healthy again");
+                else
+                    NLOG_W("xGMI: %s", xgmi_error_.c_str());
+                changed = true;
+            }
+            next_xgmi = mono_ns() + cfg_.xgmi_health_interval_ns;
+        }
         if (cfg_.mode == "L3" && cfg_.verify_peers_ns > 0 && mono_ns() >= next_verify) {
             // NICs whose peer has not answered (yet): a recovered link, a new /30, or a switch
             // port still without its address.  Failed NICs are asked again a second later.  The
@@ -241,7 +257,8 @@ void Agent::monitor(int stop_fd) {
             }
         }
         if (changed) {
-            bool healthy = std::all_of(nics_.begin(), nics_.end(), [&](const NicState& n) { return nic_healthy(n); });
+            bool healthy = xgmi_error_.empty() &&
+                           std::all_of(nics_.begin(), nics_.end(), [&](const NicState& n) { return nic_healthy(n); });
             if (healthy && !labelled) {
                 if (cfg_.mode == "L3")
                     write_artifacts();

@@ -37,8 +37,21 @@ std::map<std::string, std::string> Agent::status_node() const {
         m["gpudirect_rdma"] = gdr_.mode();
         m["kernel"] = gdr_.kernel;
     }
-    if (cfg_.xgmi_expect_links >= 0)
+    if (cfg_.xgmi_expect_links >= 0) {
         m["xgmi_pairs"] = std::to_string(xgmi_.pairs_connected) + "/" + std::to_string(xgmi_.pairs_expected);
+        int gpus = 0, up = 0, down = 0, width = 0, speed = 0;
+        for (const auto& h : xgmi_health_) {
+            if (!h.known) continue;
+            ++gpus;
+            up += h.links_up();
+            down += h.links_down();
+            width = width ? std::min(width, h.width) : h.width;
+            speed = speed ? std::min(speed, h.speed_gbps) : h.speed_gbps;
+        }
+        if (gpus)
+            m["xgmi_links"] = strfmt("%d up, %d down on %d GPUs, x%d at %d Gb/s (gpu_metrics)", up, down, gpus, width, speed);
+        if (!xgmi_error_.empty()) m["xgmi_error"] = xgmi_error_;
+    }
     if (cpu_ms_at_ready_ >= 0) m["cpu_ms_at_ready"] = strfmt("%.3f", cpu_ms_at_ready_);
     if (!excluded_.empty()) {
         std::vector<std::string> parts;
@@ -182,6 +195,20 @@ std::string Agent::render_metrics() const {
         metric("netop_agent_xgmi_pairs", "gauge", "GPU pairs with an xGMI link (KFD topology)");
         o += strfmt("netop_agent_xgmi_pairs{state=\"connected\"} %d\n", xgmi_.pairs_connected);
         o += strfmt("netop_agent_xgmi_pairs{state=\"expected\"} %d\n", xgmi_.pairs_expected);
+        bool any = false;
+        for (const auto& h : xgmi_health_) any |= h.known;
+        if (any) {
+            metric("netop_agent_xgmi_links", "gauge", "xGMI links of a GPU by trained state (gpu_metrics)");
+            for (const auto& h : xgmi_health_)
+                if (h.known)
+                    for (const char* st : {"up", "down"})
+                        o += strfmt("netop_agent_xgmi_links{gpu=\"%s\",state=\"%s\"} %d\n", httpd::escape_label(h.bdf).c_str(),
+                                    st, st[0] == 'u' ? h.links_up() : h.links_down());
+            metric("netop_agent_xgmi_link_width", "gauge", "Trained xGMI link width of a GPU (lanes, gpu_metrics)");
+            for (const auto& h : xgmi_health_)
+                if (h.known)
+                    o += strfmt("netop_agent_xgmi_link_width{gpu=\"%s\"} %d\n", httpd::escape_label(h.bdf).c_str(), h.width);
+        }
     }
     return o;
 }
@@ -212,6 +239,7 @@ std::string reason_path(const std::string& status_file) { return status_file + "
 std::string Agent::not_ready_reason() const {
     if (!config_error_.empty()) return config_error_;
     std::vector<std::string> parts;
+    if (!xgmi_error_.empty()) parts.push_back("xGMI: " + xgmi_error_);
     for (const auto& n : nics_) {
         std::string why;
         if (n.degraded)

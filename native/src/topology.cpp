@@ -562,6 +562,65 @@ XgmiReport read_xgmi(const std::string& root) {
 }
 
 // ---------------------------------------------------------------------------
+// xGMI link health (gpu_metrics)
+// ---------------------------------------------------------------------------
+namespace {
+// gpu_metrics 1.8: a 4-byte header (u16 structure_size, u8 format_revision, u8 content_revision),
+// then the fields; the xGMI ones sit at these offsets (little-endian, as the GPU writes them).
+constexpr size_t kGm18Width = 72, kGm18Speed = 74, kGm18Read = 136, kGm18Write = 200, kGm18Status = 264;
+constexpr size_t kGm18End = kGm18Status + 2 * kMaxXgmiLinks;
+
+template <typename T>
+T le_at(const std::string& b, size_t off) {
+    T v{};
+    std::memcpy(&v, b.data() + off, sizeof v);
+    return v;
+}
+}  // namespace
+
+int XgmiLinkHealth::links_up() const { return int(std::count(status.begin(), status.end(), 1)); }
+int XgmiLinkHealth::links_down() const { return int(std::count(status.begin(), status.end(), 0)); }
+
+XgmiLinkHealth parse_gpu_metrics(const std::string& blob) {
+    XgmiLinkHealth h;
+    if (blob.size() < 4) {
+        h.error = "gpu_metrics unreadable or empty";
+        return h;
+    }
+    const int format = uint8_t(blob[2]), content = uint8_t(blob[3]);
+    h.revision = strfmt("%d.%d", format, content);
+    if (format != 1 || content != 8) {
+        h.error = "gpu_metrics " + h.revision + " is not a layout this agent reads (1.8): xGMI link state not checked";
+        return h;
+    }
+    if (blob.size() < kGm18End || le_at<uint16_t>(blob, 0) < kGm18End) {
+        h.error = strfmt("gpu_metrics 1.8 truncated (%zu bytes)", blob.size());
+        return h;
+    }
+    h.known = true;
+    h.width = le_at<uint16_t>(blob, kGm18Width);
+    h.speed_gbps = le_at<uint16_t>(blob, kGm18Speed);
+    for (int i = 0; i < kMaxXgmiLinks; ++i) {
+        const uint16_t st = le_at<uint16_t>(blob, kGm18Status + 2 * size_t(i));
+        h.status.push_back(st == 1 ? 1 : st == 0 ? 0 : -1);  // 0xffff: no link in this slot
+        h.read_kb.push_back(le_at<uint64_t>(blob, kGm18Read + 8 * size_t(i)));
+        h.write_kb.push_back(le_at<uint64_t>(blob, kGm18Write + 8 * size_t(i)));
+    }
+    return h;
+}
+
+std::vector<XgmiLinkHealth> read_xgmi_health(const std::string& root, const std::vector<std::string>& bdfs) {
+    std::vector<XgmiLinkHealth> out;
+    for (const auto& bdf : bdfs) {
+        auto blob = read_file(path_join(root, "bus/pci/devices/" + bdf + "/gpu_metrics"));
+        XgmiLinkHealth h = parse_gpu_metrics(blob ? *blob : std::string());
+        h.bdf = bdf;
+        out.push_back(std::move(h));
+    }
+    return out;
+}
+
+// ---------------------------------------------------------------------------
 // GPUDirect RDMA
 // ---------------------------------------------------------------------------
 bool kernel_at_least(const std::string& release, int major, int minor) {

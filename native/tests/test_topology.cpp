@@ -146,6 +146,43 @@ TEST(topology_kfd_xgmi_mesh) {
     CHECK_EQ(x.per_gpu_bw_mbs(), uint64_t(2 * 76000));
 }
 
+TEST(topology_gpu_metrics_1_8_xgmi_links_as_amd_smi_reads_them) {
+    // Captured on a live MI355X (tools/gpu_metrics_dump.sh); amd-smi read the same GPU as link
+    // status XUUUUUUU, width 16, bit rate 38, link 1 read 7405369007 KB / write 7377082767 KB.
+    auto blob = read_file(std::string(NETOP_TEST_FIXTURES) + "/gpu_metrics_v1_8.bin");
+    CHECK(blob && blob->size() == 3872);
+    auto h = parse_gpu_metrics(*blob);
+    CHECK(h.known);
+    CHECK_EQ(h.revision, std::string("1.8"));
+    CHECK_EQ(h.width, 16);
+    CHECK_EQ(h.speed_gbps, 38);
+    CHECK(h.status == std::vector<int>({-1, 1, 1, 1, 1, 1, 1, 1}));
+    CHECK_EQ(h.links_up(), 7);
+    CHECK_EQ(h.links_down(), 0);
+    CHECK_EQ(h.read_kb[1], uint64_t(7405369007ULL));
+    CHECK_EQ(h.write_kb[1], uint64_t(7377082767ULL));
+    CHECK_EQ(h.read_kb[0], uint64_t(0));
+    // Link 3 down, as the firmware writes it (0), and link 5 trained at x8.
+    std::string down = *blob;
+    down[264 + 2 * 3] = 0;
+    auto d = parse_gpu_metrics(down);
+    CHECK(d.known && d.links_down() == 1 && d.links_up() == 6 && d.status[3] == 0);
+    // Another revision: not decoded, and said so; truncated and empty blobs likewise.
+    std::string other = *blob;
+    other[3] = 7;
+    auto o = parse_gpu_metrics(other);
+    CHECK(!o.known && o.revision == "1.7" && o.error.find("not a layout") != std::string::npos && o.status.empty());
+    CHECK(!parse_gpu_metrics(blob->substr(0, 200)).known);
+    CHECK(!parse_gpu_metrics("").known);
+    // From sysfs, by BDF; a GPU without the file is reported, not skipped.
+    TmpDir t;
+    t.write("bus/pci/devices/0000:0a:00.0/gpu_metrics", *blob);
+    auto all = read_xgmi_health(t.path, {"0000:0a:00.0", "0000:23:00.0"});
+    CHECK_EQ(all.size(), size_t(2));
+    CHECK(all[0].known && all[0].bdf == "0000:0a:00.0");
+    CHECK(!all[1].known && all[1].bdf == "0000:23:00.0");
+}
+
 TEST(topology_gdr_detection) {
     TmpDir t;
     auto g = topo::detect_gdr(t.path, "6.8.0-45-generic");

@@ -154,9 +154,28 @@ def build_mi355x_node(root: Path, nic_names: Optional[Dict[str, str]] = None, ni
                 _w(base / str(node) / "io_links" / str(li) / "properties",
                    f"type 11\nnode_from {node}\nnode_to {j + 2}\nweight 15\nmin_bandwidth 76000\nmax_bandwidth 76000\n")
                 li += 1
+        # amdgpu's gpu_metrics (as captured on a live MI355X, 1.8): every GPU's 7 xGMI links up.
+        blob = GPU_METRICS_FIXTURE.read_bytes()
+        for g in gpus:
+            (root / "devices" / g["path"] / "gpu_metrics").write_bytes(blob)
     fx["nics"] = nics
     fx["gpus"] = gpus
     return fx
+
+
+GPU_METRICS_FIXTURE = FIXTURE.parent / "gpu_metrics_v1_8.bin"
+_GM18_XGMI_STATUS = 264  # u16 per link slot: 1 up, 0 down, 0xffff no link
+
+
+def set_xgmi_link(root: Path, bdf: str, slot: int, up: bool) -> None:
+    """Writes one xGMI link's state into a GPU's gpu_metrics, as the firmware would when the link
+    trains or drops (the file is replaced whole, like a sysfs read sees one snapshot)."""
+    f = Path(root) / "bus" / "pci" / "devices" / bdf / "gpu_metrics"
+    b = bytearray(f.read_bytes())
+    b[_GM18_XGMI_STATUS + 2 * slot:_GM18_XGMI_STATUS + 2 * slot + 2] = (1 if up else 0).to_bytes(2, "little")
+    tmp = f.with_name("gpu_metrics.tmp")
+    tmp.write_bytes(bytes(b))
+    tmp.replace(f)
 
 
 def add_rocev2_gids(root: Path, rdma_dev: str, ips, port: int = 1) -> None:

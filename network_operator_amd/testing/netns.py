@@ -317,7 +317,8 @@ def run_scenario(n_nics: int = 8, mode: str = "L3", seed: int | None = None, int
                  soak_cycles: int = 0, arp_silent_ports: int = 0, switch_name: str = "",
                  port_switch_names: dict | None = None, nic_speeds_mbps: list | None = None,
                  switch_max_frame: int = 0, dark_port: int | None = None,
-                 dark_port_up_after: float | None = None, kill_mid_config: int = 0, rail_driver: str = "") -> dict:
+                 dark_port_up_after: float | None = None, kill_mid_config: int = 0, rail_driver: str = "",
+                 xgmi_down_at_start: tuple | None = None, xgmi_link_flap: tuple | None = None) -> dict:
     """Runs one node bring-up.  Must already be inside a private user+net namespace.
 
     nm_bus: run the agent with --disable-networkmanager against a real ``dbus-daemon`` on which a
@@ -337,7 +338,10 @@ def run_scenario(n_nics: int = 8, mode: str = "L3", seed: int | None = None, int
     the last start runs to readiness and is what the result describes.  ``mid_config_kills``
     records the state each kill left behind.
 
-    rail_driver: the scale-out NICs' driver and RDMA names (fakesysfs.build_mi355x_node)."""
+    rail_driver: the scale-out NICs' driver and RDMA names (fakesysfs.build_mi355x_node).
+
+    xgmi_down_at_start / xgmi_link_flap: (GPU index, link slot) whose xGMI link is down in the
+    GPU's gpu_metrics before the agent starts / goes down after readiness and comes back."""
     from . import fakesysfs
 
     nat = _native()
@@ -350,6 +354,8 @@ def run_scenario(n_nics: int = 8, mode: str = "L3", seed: int | None = None, int
     try:
         fx = fakesysfs.build_mi355x_node(tmp / "sys", n_gpus=n_nics, rail_driver=rail_driver,
                                          drop_xgmi_pairs=[tuple(p) for p in (drop_xgmi or [])])
+        if xgmi_down_at_start is not None:
+            fakesysfs.set_xgmi_link(tmp / "sys", fx["gpus"][xgmi_down_at_start[0]]["bdf"], xgmi_down_at_start[1], False)
         pairs = nat.discover(str(tmp / "sys"))["pairs"]
         nic_names = [p["nic"] for p in pairs][:n_nics]
         plan = random_plan(len(nic_names), rng)
@@ -620,6 +626,26 @@ def run_scenario(n_nics: int = 8, mode: str = "L3", seed: int | None = None, int
             res["flap_restore_s"] = (back - t_up) if back else None
             link = rt.link_by_name(nic_names[flap_port])
             res["flap_routes_after"] = [r for r in rt.route_list() if r["ifindex"] == link["index"]]
+        if xgmi_link_flap is not None and t_ready:
+            # A GPU's xGMI link drops after readiness (gpu_metrics): the label goes while it is
+            # down, with the reason, and comes back with the link.
+            bdf = fx["gpus"][xgmi_link_flap[0]]["bdf"]
+            time.sleep(0.05)  # status.json follows the label
+            t_down = time.monotonic()
+            fakesysfs.set_xgmi_link(tmp / "sys", bdf, xgmi_link_flap[1], False)
+            gone = None
+            while time.monotonic() < t_down + 10 and agent.poll() is None:
+                if not label.exists():
+                    gone = time.monotonic()
+                    break
+                time.sleep(0.002)
+            reason = tmp / "status.json.not-ready"
+            why = reason.read_text() if reason.exists() else None
+            t_up = time.monotonic()
+            fakesysfs.set_xgmi_link(tmp / "sys", bdf, xgmi_link_flap[1], True)
+            back = _wait_for(label, 10, agent)
+            res["xgmi_flap"] = {"gpu": bdf, "withdraw_s": (gone - t_down) if gone else None,
+                                "restore_s": (back - t_up) if back else None, "reason": why}
         if soak_cycles and t_ready:
             # Carrier loss on a random port, over and over, with the agent in monitor mode: every
             # cycle must withdraw and restore the label, and the agent must not leak descriptors,

@@ -198,3 +198,38 @@ def test_oracle_agrees_with_agent_on_the_captured_node(tmp_path):
     want = native().discover(str(tmp_path) + "/", "affine")
     assert len(o["gpus"]) == 8 and all(len(a["closest"]) == 1 for a in o["affine"].values())
     assert {p["gpu"]: p["nic"] for p in want["pairs"]} == {g: a["closest"][0] for g, a in o["affine"].items()}
+
+
+@pytest.mark.gpu
+def test_xgmi_link_state_from_gpu_metrics_matches_amd_smi(tmp_path):
+    """The agent reads each GPU's trained xGMI links from amdgpu's gpu_metrics without amd-smi;
+    on this box, for every GPU amd-smi sees (netop-xgmi-counters, the library), the link status,
+    width and bit rate agree, and the agent's dry run reports every GPU of the node."""
+    from network_operator_amd.utils.paths import LIB_DIR
+
+    root = os.environ.get("SYSFS_ROOT", "/sys/")
+    x = native().read_xgmi(root)
+    if not x["gpus"]:
+        pytest.skip("no KFD GPU in this sysfs")
+    mine = {h["bdf"]: h for h in native().read_xgmi_health(root, x["gpus"])}
+    assert all(h["known"] for h in mine.values()), {b: h["error"] for b, h in mine.items()}
+    r = subprocess.run([str(LIB_DIR / "netop-xgmi-counters")], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr[-2000:]
+    smi = json.loads(r.stdout)["gpus"]
+    assert smi, r.stdout
+    letter = {1: "U", 0: "D", -1: "X"}
+    for g in smi:
+        h = mine[g["bdf"]]
+        assert "".join(letter[s] for s in h["status"]) == g["link_status"], (h, g)
+        assert (h["width"], h["speed_gbps"]) == (g["xgmi_link_width"], g["xgmi_link_speed"]), (h, g)
+    status = tmp_path / "status.json"
+    d = subprocess.run([str(native_bin("discover")), "--dry-run", "--xgmi-expect=0", f"--status-file={status}"],
+                       capture_output=True, text=True, timeout=60)
+    assert d.returncode == 0, d.stderr[-3000:]
+    st = json.loads(status.read_text())
+    up = sum(s == 1 for h in mine.values() for s in h["status"])
+    assert st["xgmi_links"].startswith(f"{up} up, 0 down on {len(mine)} GPUs"), st
+    out = Path(os.environ.get("GRAFT_REPO_ROOT", ".")) / "gpurun_out"
+    if out.is_dir():
+        (out / "xgmi_health_box.json").write_text(json.dumps(
+            {"agent_status_xgmi_links": st["xgmi_links"], "gpu_metrics": list(mine.values()), "amd_smi": smi}, indent=1))

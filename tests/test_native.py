@@ -305,3 +305,22 @@ def test_pattern_swar_sum_matches_the_per_rank_reference():
         dev = torch.tensor([v for g in range(groups) for v in group_sum(g, seed, lo, n)], dtype=torch.float32)
         assert torch.equal(dev, ref), (lo, n)
         assert ref.abs().max() <= 256  # exact in bf16
+
+
+def test_dry_run_reports_an_xgmi_link_down_without_failing(native, tmp_path):
+    """A dry run says what a real start would fail on and goes on: with a GPU's xGMI link down in
+    gpu_metrics, it exits 0, logs "a real start would fail", and status.json names the link;
+    every other GPU's links are read and counted (the fake node's blobs are the live MI355X's)."""
+    fx = fakesysfs.build_mi355x_node(tmp_path / "sys", n_gpus=8)
+    bdfs = [g["bdf"] for g in fx["gpus"]]
+    fakesysfs.set_xgmi_link(tmp_path / "sys", bdfs[2], 6, False)
+    health = native.read_xgmi_health(str(tmp_path / "sys"), bdfs)
+    assert [h["status"].count(0) for h in health] == [0, 0, 1, 0, 0, 0, 0, 0]
+    status = tmp_path / "status.json"
+    r = subprocess.run([str(native_bin("discover")), "--dry-run", "--xgmi-expect=0", f"--status-file={status}"],
+                       capture_output=True, text=True, timeout=60, env=dict(os.environ, SYSFS_ROOT=str(tmp_path / "sys")))
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert f"dry run: a real start would fail: xGMI: GPU {bdfs[2]}: link 6 down" in r.stderr
+    st = json.loads(status.read_text())
+    assert st["xgmi_links"] == "55 up, 1 down on 8 GPUs, x16 at 38 Gb/s (gpu_metrics)"
+    assert st["xgmi_error"] == f"GPU {bdfs[2]}: link 6 down"

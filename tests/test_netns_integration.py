@@ -581,3 +581,22 @@ def test_pollara_and_thor_rails_configure_like_connectx(driver, prefix):
     by_gpu = sorted(r["rccl_net"]["NIC_NET_CONFIG"], key=lambda e: e["GPU_INDEX"])
     assert hca == ["NCCL_IB_HCA==" + ",".join(f"{e['RDMA_DEV']}:1" for e in by_gpu)], (hca, by_gpu)
     assert "mlx5_" not in hca[0]
+
+
+def test_an_xgmi_link_down_keeps_the_node_unlabelled_and_a_drop_withdraws_the_label():
+    """The xGMI check reads each GPU's trained link state from amdgpu's gpu_metrics (the layout
+    captured on a live MI355X).  A link already down at start fails the check and names the GPU
+    and the link; a link that drops after readiness withdraws the label with that reason until it
+    is back.  (KFD's topology, the mesh check, lists the link either way.)"""
+    r = netns.run_isolated(n_nics=2, seed=43, interval="30s", fast_start=True, xgmi_down_at_start=(1, 3), wait="5s")
+    assert not r["ready"] and r["agent_rc"] != 0
+    assert "xGMI: GPU 0000:23:00.0: link 3 down" in r["agent_log"], r["agent_log"][-2000:]
+    r = netns.run_isolated(n_nics=2, seed=44, interval="30s", fast_start=True, xgmi_link_flap=(0, 5),
+                           extra_args=["--xgmi-health-interval=100ms"])
+    _check_configured(r)
+    assert r["status"]["xgmi_links"] == "14 up, 0 down on 2 GPUs, x16 at 38 Gb/s (gpu_metrics)", r["status"]
+    f = r["xgmi_flap"]
+    assert f["withdraw_s"] is not None and f["withdraw_s"] < 3.0, f
+    assert f["reason"] and "xGMI: GPU 0000:0a:00.0: link 5 down" in f["reason"], f
+    assert f["restore_s"] is not None and f["restore_s"] < 3.0, f
+    assert r["agent_rc"] == 0
