@@ -352,9 +352,13 @@ void Agent::check_xgmi() {
 
 void Agent::read_xgmi_health() {
     std::string root = cfg_.sysfs_root.empty() ? topo::sysfs_root() : cfg_.sysfs_root;
+    // The amdgpu PCI functions discovery found: KFD lists a GPU the container cannot open with
+    // its properties filtered (no BDF), while its PCI device (and gpu_metrics) is still readable.
     std::vector<std::string> bdfs;
-    for (const auto& g : xgmi_.gpus)
-        if (g.is_gpu()) bdfs.push_back(g.bdf());
+    for (const auto& g : disc_.gpus) bdfs.push_back(g.pci.bdf);
+    if (bdfs.empty())
+        for (const auto& g : xgmi_.gpus)
+            if (g.is_gpu()) bdfs.push_back(g.bdf());
     xgmi_health_ = topo::read_xgmi_health(root, bdfs);
     xgmi_error_ = xgmi_health_problem();
 }

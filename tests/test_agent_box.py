@@ -208,10 +208,11 @@ def test_xgmi_link_state_from_gpu_metrics_matches_amd_smi(tmp_path):
     from network_operator_amd.utils.paths import LIB_DIR
 
     root = os.environ.get("SYSFS_ROOT", "/sys/")
-    x = native().read_xgmi(root)
-    if not x["gpus"]:
-        pytest.skip("no KFD GPU in this sysfs")
-    mine = {h["bdf"]: h for h in native().read_xgmi_health(root, x["gpus"])}
+    gpus = [g["bdf"] for g in native().discover(root, "affine")["gpus"]]  # (KFD filters the GPUs we cannot open)
+    if not gpus:
+        pytest.skip("no amdgpu GPU in this sysfs")
+    mine = {h["bdf"]: h for h in native().read_xgmi_health(root, gpus)}
+    assert len(mine) == len(gpus)
     assert all(h["known"] for h in mine.values()), {b: h["error"] for b, h in mine.items()}
     r = subprocess.run([str(LIB_DIR / "netop-xgmi-counters")], capture_output=True, text=True, timeout=60)
     assert r.returncode == 0, r.stderr[-2000:]
