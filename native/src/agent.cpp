@@ -347,7 +347,14 @@ void Agent::check_xgmi() {
         else
             NLOG_V(1, "xGMI %s: %s", h.bdf.c_str(), h.error.c_str());
     }
-    if (!xgmi_error_.empty()) fail("xGMI: " + xgmi_error_);
+    if (xgmi_error_.empty()) return;
+    if (!cfg_.dry_run && cfg_.keep_running && cfg_.monitor && cfg_.xgmi_health_interval_ns > 0) {
+        // A link can come back (retraining, a reset of the GPU): configure the NICs, stay
+        // unlabelled, and let the monitor label the node when gpu_metrics shows it up again.
+        NLOG_W("xGMI: %s; the readiness label waits for the link(s)", xgmi_error_.c_str());
+        return;
+    }
+    fail("xGMI: " + xgmi_error_);
 }
 
 void Agent::read_xgmi_health() {
@@ -659,12 +666,13 @@ void Agent::run(int stop_fd) {
     if (cfg_.xgmi_expect_links >= 0)
         labels_extra_["amd.feature.node.kubernetes.io/gpu-xgmi.pairs"] = std::to_string(xgmi_.pairs_connected);
     if (!gdr_.kernel.empty()) labels_extra_[cfg_.labels.key + ".gdr"] = gdr_.mode();
-    const bool linked = cfg_.mode != "L2" ||
-                        std::all_of(nics_.begin(), nics_.end(), [](const NicState& n) { return n.configured; });
+    const bool linked = xgmi_error_.empty() &&
+                        (cfg_.mode != "L2" ||
+                         std::all_of(nics_.begin(), nics_.end(), [](const NicState& n) { return n.configured; }));
     if (!linked) {
-        // L2 with the monitor: stay up unlabelled; the carrier on the last dark NIC (at the
-        // required speed) publishes the label (monitor()).
-        NLOG_W("Not ready: %s; the label follows once every NIC has a link", not_ready_reason().c_str());
+        // With the monitor: stay up unlabelled; the carrier on the last dark NIC (L2, at the
+        // required speed) or the xGMI link coming back publishes the label (monitor()).
+        NLOG_W("Not ready: %s; the label follows once that is resolved", not_ready_reason().c_str());
         write_status();
         NLOG_I("Monitoring...");
         monitor(stop_fd);

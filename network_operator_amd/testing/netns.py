@@ -318,7 +318,8 @@ def run_scenario(n_nics: int = 8, mode: str = "L3", seed: int | None = None, int
                  port_switch_names: dict | None = None, nic_speeds_mbps: list | None = None,
                  switch_max_frame: int = 0, dark_port: int | None = None,
                  dark_port_up_after: float | None = None, kill_mid_config: int = 0, rail_driver: str = "",
-                 xgmi_down_at_start: tuple | None = None, xgmi_link_flap: tuple | None = None) -> dict:
+                 xgmi_down_at_start: tuple | None = None, xgmi_up_after: float | None = None,
+                 xgmi_link_flap: tuple | None = None) -> dict:
     """Runs one node bring-up.  Must already be inside a private user+net namespace.
 
     nm_bus: run the agent with --disable-networkmanager against a real ``dbus-daemon`` on which a
@@ -341,7 +342,9 @@ def run_scenario(n_nics: int = 8, mode: str = "L3", seed: int | None = None, int
     rail_driver: the scale-out NICs' driver and RDMA names (fakesysfs.build_mi355x_node).
 
     xgmi_down_at_start / xgmi_link_flap: (GPU index, link slot) whose xGMI link is down in the
-    GPU's gpu_metrics before the agent starts / goes down after readiness and comes back."""
+    GPU's gpu_metrics before the agent starts / goes down after readiness and comes back.
+    xgmi_up_after: the link down at start comes up that many seconds after the agent started;
+    the reasons the agent gave meanwhile are kept."""
     from . import fakesysfs
 
     nat = _native()
@@ -510,6 +513,21 @@ def run_scenario(n_nics: int = 8, mode: str = "L3", seed: int | None = None, int
             set_switch_port(pid, sw_ports[dark_port], True)
             t_ready = _wait_for(label, 10, agent)
             dark["port_up_to_label_s"] = (t_ready - t_up) if t_ready else None
+        elif xgmi_down_at_start is not None and xgmi_up_after is not None:
+            reason, seen = tmp / "status.json.not-ready", []
+            while time.monotonic() < t0 + xgmi_up_after and agent.poll() is None:
+                try:
+                    why = reason.read_text()
+                    if why and why not in seen:
+                        seen.append(why)
+                except OSError:
+                    pass
+                time.sleep(0.05)
+            dark["reasons_seen"], dark["label_while_down"] = seen, label.exists()
+            t_up = time.monotonic()
+            fakesysfs.set_xgmi_link(tmp / "sys", fx["gpus"][xgmi_down_at_start[0]]["bdf"], xgmi_down_at_start[1], True)
+            t_ready = _wait_for(label, 10, agent)
+            dark["link_up_to_label_s"] = (t_ready - t_up) if t_ready else None
         else:
             t_ready = _wait_for(label, budget, agent)
         res: dict = {"n_nics": len(nic_names), "mode": mode, "fast_start": fast_start, "announce": announce,

@@ -588,7 +588,16 @@ def test_an_xgmi_link_down_keeps_the_node_unlabelled_and_a_drop_withdraws_the_la
     captured on a live MI355X).  A link already down at start fails the check and names the GPU
     and the link; a link that drops after readiness withdraws the label with that reason until it
     is back.  (KFD's topology, the mesh check, lists the link either way.)"""
-    r = netns.run_isolated(n_nics=2, seed=43, interval="30s", fast_start=True, xgmi_down_at_start=(1, 3), wait="5s")
+    # With the monitor (the DaemonSet's agent): configured, unlabelled with the reason, labelled
+    # when the link is back.  Without it, the start fails and names the link.
+    r = netns.run_isolated(n_nics=2, seed=43, interval="30s", fast_start=True, xgmi_down_at_start=(1, 3),
+                           xgmi_up_after=1.0, extra_args=["--xgmi-health-interval=100ms"])
+    _check_configured(r)
+    d = r["dark"]
+    assert not d["label_while_down"] and any("xGMI: GPU 0000:23:00.0: link 3 down" in w for w in d["reasons_seen"]), d
+    assert d["link_up_to_label_s"] is not None and d["link_up_to_label_s"] < 3.0, d
+    r = netns.run_isolated(n_nics=2, seed=43, interval="30s", fast_start=True, xgmi_down_at_start=(1, 3), wait="5s",
+                           extra_args=["--monitor=false"])
     assert not r["ready"] and r["agent_rc"] != 0
     assert "xGMI: GPU 0000:23:00.0: link 3 down" in r["agent_log"], r["agent_log"][-2000:]
     r = netns.run_isolated(n_nics=2, seed=44, interval="30s", fast_start=True, xgmi_link_flap=(0, 5),
