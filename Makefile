@@ -188,7 +188,7 @@ clean:
 
 FUZZ_CXX ?= /opt/rocm/lib/llvm/bin/clang++
 FUZZ_TIME ?= 60
-fuzz-native:                ## libFuzzer (+ASan/UBSan) on the LLDP, D-Bus, Port Description, netlink and ARP parsers
+fuzz-native:                ## libFuzzer (+ASan/UBSan) on the LLDP, D-Bus, Port Description / state records / gpu_metrics, netlink and ARP parsers
 	mkdir -p _build-fuzz
 	for t in 1:lldp 2:dbus 3:portdesc 4:netlink 5:arp; do id=$${t%%:*}; name=$${t##*:}; \
 	  $(FUZZ_CXX) -std=c++17 -O1 -g -fsanitize=fuzzer,address,undefined -fno-sanitize-recover=undefined \
@@ -198,6 +198,7 @@ fuzz-native:                ## libFuzzer (+ASan/UBSan) on the LLDP, D-Bus, Port 
 	    native/src/dbus.cpp native/src/arp.cpp native/src/ethtool.cpp native/src/artifacts.cpp native/src/topology.cpp \
 	    -o _build-fuzz/fuzz_$$name -lpthread || exit 1; \
 	  mkdir -p _build-fuzz/corpus_$$name; \
+	  if [ $$name = portdesc ]; then cp tests/fixtures/gpu_metrics_v1_8.bin _build-fuzz/corpus_$$name/; fi; \
 	  _build-fuzz/fuzz_$$name native/fuzz/regressions/* > _build-fuzz/$$name.replay.log 2>&1 || { tail -20 _build-fuzz/$$name.replay.log; exit 1; }; \
 	  _build-fuzz/fuzz_$$name -artifact_prefix=_build-fuzz/$$name- -max_total_time=$(FUZZ_TIME) -rss_limit_mb=2048 \
 	    -print_final_stats=1 _build-fuzz/corpus_$$name > _build-fuzz/$$name.log 2>&1; rc=$$?; \

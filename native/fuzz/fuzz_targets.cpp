@@ -3,8 +3,8 @@
 //   lldp      frames from the switch (AF_PACKET) — untrusted, L2-adjacent attacker — and the
 //             LLDP cache lines made from them
 //   dbus      messages from the system bus peer
-//   portdesc  the switch's Port Description string (operator-configured, still untrusted), and
-//             the agent's --fw-lldp-state record (a hostPath file)
+//   portdesc  the switch's Port Description string (operator-configured, still untrusted), the
+//             agent's --fw-lldp-state record (a hostPath file), and amdgpu's gpu_metrics blob
 //   netlink   RTM_NEWLINK / NEWROUTE / NEWRULE / NEWADDR / DCB / extended-ACK payloads (kernel,
 //             but parsed with length arithmetic)
 //   arp       ARP payloads from the switch port (--verify-peers) — untrusted, L2-adjacent
@@ -28,6 +28,7 @@
 #include "netop/l3.hpp"
 #include "netop/lldp.hpp"
 #include "netop/netlink.hpp"
+#include "netop/topology.hpp"
 
 using namespace netop;
 
@@ -77,6 +78,10 @@ extern "C" int LLVMFuzzerTestOneInput(const uint8_t* data, size_t size) {
             again[i].original_bits != recs[i].original_bits || again[i].dcbx_changed != recs[i].dcbx_changed ||
             again[i].dcbx != recs[i].dcbx)
             __builtin_trap();
+    // The GPU's gpu_metrics blob (sysfs): decoded only at a known revision, never read past its end.
+    auto h = topo::parse_gpu_metrics(s);
+    if (h.known && (h.status.size() != size_t(topo::kMaxXgmiLinks) || h.links_up() + h.links_down() > topo::kMaxXgmiLinks))
+        __builtin_trap();
 #elif NETOP_FUZZ_TARGET == 4
     // Wrap the input as the payload of one RTM_NEWLINK message with a consistent header.
     if (size > 1 << 16) return 0;
