@@ -95,7 +95,8 @@ def generate(out_dir: str, sysfs_root: Optional[str] = None, env_extra: str = ""
            "topo_file_bytes": topo.stat().st_size if topo.is_file() else 0, "topo_sha256": _sha256(str(topo))}
     try:
         st = json.loads(status.read_text())
-        doc["agent_status"] = {k: st[k] for k in ("xgmi_pairs", "gpudirect_rdma", "phases_ms", "not_in_netns") if k in st}
+        doc["agent_status"] = {k: st[k] for k in ("xgmi_pairs", "xgmi_links", "xgmi_error", "gpudirect_rdma", "phases_ms",
+                                                  "not_in_netns") if k in st}
     except (OSError, ValueError):
         pass
     if doc["env"].get("NCCL_TOPO_FILE") != doc["topo_file"]:
