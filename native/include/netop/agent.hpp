@@ -82,6 +82,9 @@ struct Config {
     // down fails the check; a width below this (lanes, 0 = any) too.  The monitor reads the state
     // again every xgmi_health_interval_ns and withdraws the label while a link is down.
     int xgmi_min_link_width = 0;
+    // Configure (and label) a NIC only if its PCIe link trained at the speed and width it and its
+    // slot support, and its GPU's at full width (a GPU may lower its link speed when idle).
+    bool require_full_pcie = false;
     int64_t xgmi_health_interval_ns = 5LL * 1000000000;
     int64_t link_wait_ns = 3LL * 1000000000;  // netlink echo wait (network.go:251)
     // L2: how long a NIC that is admin-up may train its link before it counts as "no carrier".
@@ -429,6 +432,7 @@ class Agent {
     std::string xgmi_error_;  // what the last gpu_metrics read found wrong (empty: fine or not read)
     void read_xgmi_health();
     std::string xgmi_health_problem() const;
+    std::string check_pcie(const NicState& n) const;  // "" when fine or not required
     topo::GdrReport gdr_;
     void check_gdr();
     std::map<std::string, std::string> status_node() const;

@@ -13,6 +13,7 @@
 #include "netop/common.hpp"
 #include "netop/l3.hpp"
 #include "netop/netlink.hpp"
+#include "netop/topology.hpp"
 
 namespace netop {
 
@@ -59,6 +60,8 @@ struct NicState {
     std::optional<int> gid_index;
     int numa_node = -1;     // NUMA node of the GPU (pin the rank's CPU threads there)
     std::string pcie_path;  // GPU <-> NIC PCIe path type (PIX / PXB / ...)
+    // PCIe links of the NIC and of its GPU as trained (read at discovery; --require-full-pcie)
+    topo::PcieLink pcie, gpu_pcie;
     // Per-rail source routing: this NIC's rail k (its GPU index; NICs without a GPU get indices
     // above every GPU's) and what the agent installed for it, so exactly that is removed later.
     int rail_index = -1;

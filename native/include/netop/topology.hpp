@@ -188,6 +188,20 @@ XgmiReport read_xgmi(const std::string& root = sysfs_root());
 // at what width.  The blob's layout is versioned (format.content); only revisions this reader
 // knows are decoded -- 1.8, which MI355X firmware reports (layout checked against amd-smi on a
 // live node: tests/fixtures/gpu_metrics_v1_8.bin) -- anything else is reported as not read.
+// Negotiated vs maximum PCIe link of a PCI function (current_link_speed / _width against
+// max_link_*).  A card that trained below what it and its slot support (a loose card or riser,
+// a bad lane, a BIOS slot setting) moves RDMA or GPUDirect traffic at a fraction of its rate.
+struct PcieLink {
+    double speed_gts = 0, max_speed_gts = 0;  // GT/s; 0 when the attribute is missing
+    int width = 0, max_width = 0;
+    bool known() const { return speed_gts > 0 && width > 0 && max_speed_gts > 0 && max_width > 0; }
+    bool slower() const { return known() && speed_gts + 1e-6 < max_speed_gts; }
+    bool narrower() const { return known() && width < max_width; }
+    bool degraded() const { return slower() || narrower(); }
+    std::string str() const;  // "32.0 GT/s x16", or "16.0 GT/s x8 of 32.0 GT/s x16" when degraded
+};
+PcieLink read_pcie_link(const std::string& root, const std::string& bdf);
+
 constexpr int kMaxXgmiLinks = 8;
 struct XgmiLinkHealth {
     std::string bdf;

@@ -350,6 +350,18 @@ PYBIND11_MODULE(_netop_native, m) {
         d["missing"] = miss;
         return d;
     });
+    m.def("read_pcie_link", [](const std::string& root, const std::string& bdf) {
+        auto l = topo::read_pcie_link(root, bdf);
+        py::dict d;
+        d["speed_gts"] = l.speed_gts;
+        d["max_speed_gts"] = l.max_speed_gts;
+        d["width"] = l.width;
+        d["max_width"] = l.max_width;
+        d["known"] = l.known();
+        d["degraded"] = l.degraded();
+        d["str"] = l.str();
+        return d;
+    });
     m.def("read_xgmi_health", [](const std::string& root, const std::vector<std::string>& bdfs) {
         py::list out;
         for (const auto& h : topo::read_xgmi_health(root, bdfs)) {

@@ -186,6 +186,16 @@ void Agent::get_network_configs(const std::vector<std::string>& names) {
             n.numa_node = disc_.gpus[size_t(p.gpu)].pci.numa;
             n.pcie_path = topo::to_string(p.path);
         }
+        {
+            const std::string root = cfg_.sysfs_root.empty() ? topo::sysfs_root() : cfg_.sysfs_root;
+            if (auto d = topo::netdev_pci(root, name)) n.pcie = topo::read_pcie_link(root, d->bdf);
+            if (!n.gpu_bdf.empty()) n.gpu_pcie = topo::read_pcie_link(root, n.gpu_bdf);
+            if (n.pcie.degraded())
+                NLOG_W("Interface '%s': PCIe link trained at %s", name.c_str(), n.pcie.str().c_str());
+            if (n.gpu_pcie.degraded())
+                NLOG_W("Interface '%s': the PCIe link of its GPU %s trained at %s", name.c_str(), n.gpu_bdf.c_str(),
+                       n.gpu_pcie.str().c_str());
+        }
         if (n.rdma_dev.empty())  // host NICs (rdma discovery): no GPU, but still an RDMA device
             for (auto& nic : disc_.nics)
                 if (nic.ifname == name) {
@@ -584,7 +594,7 @@ void Agent::run(int stop_fd) {
         }
     }
 
-    if (cfg_.mode == "L2" && cfg_.configure && cfg_.min_link_speed_mbps > 0) {
+    if (cfg_.mode == "L2" && cfg_.configure && (cfg_.min_link_speed_mbps > 0 || cfg_.require_full_pcie)) {
         // L3 checks each NIC as it configures it; L2 has no per-NIC step, so all at once here --
         // for the NICs with a link (a dark NIC is checked when its carrier comes, in monitor()).
         std::vector<std::string> slow;
@@ -592,7 +602,8 @@ void Agent::run(int stop_fd) {
             if (n.configured && !(n.configured = l2_link_ok(n))) slow.push_back(n.ifname + ": " + n.config_error);
         if (!slow.empty() && !(cfg_.keep_running && cfg_.monitor)) {
             write_status();
-            throw AgentError(strfmt("%zu NIC(s) below the required link speed: ", slow.size()) + join(slow, "; "));
+            throw AgentError(strfmt("%zu NIC(s) below the required link speed%s: ", slow.size(),
+                                    cfg_.require_full_pcie ? " or PCIe link" : "") + join(slow, "; "));
         }
     }
     if (cfg_.mode == "L3") {

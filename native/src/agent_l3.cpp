@@ -183,7 +183,7 @@ bool Agent::configure_interface(NicState& n) {
         NLOG_W("Interface '%s' not configured: %s", n.ifname.c_str(), n.config_error.c_str());
         return false;
     }
-    if (std::string why = check_link_speed(n); !why.empty()) {
+    if (std::string why = check_link_speed(n); !why.empty() || !(why = check_pcie(n)).empty()) {
         n.config_error = why;
         NLOG_W("Interface '%s' not configured: %s", n.ifname.c_str(), n.config_error.c_str());
         return false;

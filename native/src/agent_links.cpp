@@ -410,8 +410,20 @@ std::string Agent::silent_summary() const {
     return out;
 }
 
+std::string Agent::check_pcie(const NicState& n) const {
+    if (!cfg_.require_full_pcie) return "";
+    if (n.pcie.degraded())
+        return strfmt("its PCIe link trained at %s: RDMA moves at a fraction of the rail's rate (reseat the card, check the "
+                      "riser and the slot's BIOS link setting)", n.pcie.str().c_str());
+    if (n.gpu_pcie.narrower())
+        return strfmt("the PCIe link of its GPU %s trained at x%d of x%d: GPUDirect RDMA to and from it is throttled "
+                      "(reseat the GPU, check the riser)", n.gpu_bdf.c_str(), n.gpu_pcie.width, n.gpu_pcie.max_width);
+    return "";
+}
+
 bool Agent::l2_link_ok(NicState& n) {
     n.config_error = check_link_speed(n);
+    if (n.config_error.empty()) n.config_error = check_pcie(n);
     if (!n.config_error.empty()) NLOG_W("Interface '%s' not ready: %s", n.ifname.c_str(), n.config_error.c_str());
     return n.link.up() && !n.no_carrier && n.config_error.empty();
 }

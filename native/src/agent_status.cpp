@@ -136,6 +136,12 @@ std::string Agent::render_metrics() const {
                 o += strfmt("netop_agent_nic_speed_mbps{nic=\"%s\"} %lld\n", httpd::escape_label(n.ifname).c_str(),
                             (long long)n.speed_mbps);
     }
+    metric("netop_agent_nic_pcie_degraded", "gauge",
+           "1 when the NIC's PCIe link, or its GPU's, trained below the speed or width it supports");
+    for (const auto& n : nics_)
+        if (n.pcie.known() || n.gpu_pcie.known())
+            o += strfmt("netop_agent_nic_pcie_degraded{nic=\"%s\"} %d\n", httpd::escape_label(n.ifname).c_str(),
+                        n.pcie.degraded() || n.gpu_pcie.narrower() ? 1 : 0);
     metric("netop_agent_link_flaps_total", "counter", "link losses observed after readiness");
     o += strfmt("netop_agent_link_flaps_total %d\n", flaps_);
     metric("netop_agent_reconfigurations_total", "counter", "NIC re-addressings after a Port Description change");

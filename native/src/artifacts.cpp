@@ -502,6 +502,8 @@ std::string generate_status(const std::vector<NicState>& nics, const std::map<st
         if (!n->driver.empty()) j.key("driver").value(n->driver);
         if (!n->lldp_silent.empty()) j.key("lldp_silent").value(n->lldp_silent);
         if (n->speed_mbps >= 0) j.key("speed_mbps").value(n->speed_mbps);
+        if (n->pcie.known()) j.key("pcie").value(n->pcie.str());
+        if (n->gpu_pcie.known()) j.key("gpu_pcie").value(n->gpu_pcie.str());
         if (n->peer_max_frame > 0) j.key("peer_max_frame").value(n->peer_max_frame);
         j.key("lldp").value(n->lldp_seen);
         if (n->lldp_seen) {

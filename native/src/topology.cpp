@@ -562,6 +562,34 @@ XgmiReport read_xgmi(const std::string& root) {
 }
 
 // ---------------------------------------------------------------------------
+// PCIe link state
+// ---------------------------------------------------------------------------
+std::string PcieLink::str() const {
+    if (!known()) return "unknown";
+    std::string s = strfmt("%.1f GT/s x%d", speed_gts, width);
+    if (degraded()) s += strfmt(" of %.1f GT/s x%d", max_speed_gts, max_width);
+    return s;
+}
+
+PcieLink read_pcie_link(const std::string& root, const std::string& bdf) {
+    PcieLink l;
+    const std::string dir = path_join(root, "bus/pci/devices/" + bdf);
+    auto gts = [&](const char* attr) {  // "32.0 GT/s PCIe"; "Unknown" (a link that is down) reads 0
+        auto v = read_attr(path_join(dir, attr));
+        return v ? std::strtod(v->c_str(), nullptr) : 0.0;
+    };
+    auto lanes = [&](const char* attr) {
+        auto v = read_attr(path_join(dir, attr));
+        return v ? int(std::strtol(v->c_str(), nullptr, 10)) : 0;
+    };
+    l.speed_gts = gts("current_link_speed");
+    l.max_speed_gts = gts("max_link_speed");
+    l.width = lanes("current_link_width");
+    l.max_width = lanes("max_link_width");
+    return l;
+}
+
+// ---------------------------------------------------------------------------
 // xGMI link health (gpu_metrics)
 // ---------------------------------------------------------------------------
 namespace {

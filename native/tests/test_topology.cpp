@@ -183,6 +183,26 @@ TEST(topology_gpu_metrics_1_8_xgmi_links_as_amd_smi_reads_them) {
     CHECK(!all[1].known && all[1].bdf == "0000:23:00.0");
 }
 
+TEST(topology_pcie_link_trained_vs_supported) {
+    TmpDir t;
+    const std::string d = "bus/pci/devices/0000:08:00.0/";
+    t.write(d + "max_link_speed", "32.0 GT/s PCIe\n");
+    t.write(d + "max_link_width", "16\n");
+    t.write(d + "current_link_speed", "32.0 GT/s PCIe\n");
+    t.write(d + "current_link_width", "16\n");
+    auto l = read_pcie_link(t.path, "0000:08:00.0");
+    CHECK(l.known() && !l.degraded());
+    CHECK_EQ(l.str(), std::string("32.0 GT/s x16"));
+    t.write(d + "current_link_width", "8\n");
+    t.write(d + "current_link_speed", "16.0 GT/s PCIe\n");
+    l = read_pcie_link(t.path, "0000:08:00.0");
+    CHECK(l.narrower() && l.slower() && l.degraded());
+    CHECK_EQ(l.str(), std::string("16.0 GT/s x8 of 32.0 GT/s x16"));
+    t.write(d + "current_link_speed", "Unknown\n");  // a link that is down
+    CHECK(!read_pcie_link(t.path, "0000:08:00.0").known());
+    CHECK(!read_pcie_link(t.path, "0000:09:00.0").known());  // no such function / no attributes
+}
+
 TEST(topology_gdr_detection) {
     TmpDir t;
     auto g = topo::detect_gdr(t.path, "6.8.0-45-generic");

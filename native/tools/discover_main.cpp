@@ -69,6 +69,7 @@ int main(int argc, char** argv) {
     fs.add_string("nm-keyfile-dir", &cfg.nm_keyfile_dir, "with --disable-networkmanager, also persist an unmanaged-devices keyfile here (removed on exit)");
     fs.add_bool("nm-restore", &cfg.nm_restore, "with --disable-networkmanager: on exit, remove the keyfile and set the interfaces managed by NetworkManager again (default: they stay unmanaged across restarts)");
     fs.add_int("xgmi-expect", &cfg.xgmi_expect_links, "verify the xGMI mesh before labelling: -1 off, 0 full mesh, N GPU pairs; the links' trained state (amdgpu gpu_metrics) too: a link down fails the check");
+    fs.add_bool("require-full-pcie", &cfg.require_full_pcie, "configure (and label) a NIC only if its PCIe link trained at the speed and width it supports, and its GPU's at full width; degraded links are reported either way (status.json, metrics)");
     fs.add_int("xgmi-min-link-width", &cfg.xgmi_min_link_width, "with --xgmi-expect: the narrowest trained xGMI link width (lanes) a GPU may run at, from gpu_metrics; 0 = any");
     fs.add_duration("xgmi-health-interval", &cfg.xgmi_health_interval_ns, "with --xgmi-expect and the monitor: how often the xGMI links' state is read again; a link down withdraws the readiness label until it is back (0 = at start only)");
     fs.add_duration("link-wait", &cfg.link_wait_ns, "time to wait for link state echoes from the kernel");

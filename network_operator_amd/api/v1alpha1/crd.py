@@ -148,6 +148,12 @@ def openapi_schema() -> dict:
                                "came up slower (a marginal cable or optic, a port renegotiated down) is left\n"
                                "unconfigured and named in status.errors.  0 = not checked.",
                 "minimum": 0, "maximum": 3200, "type": "integer"},
+            "requireFullPcieLink": {
+                "description": "Configure a scale-out NIC only if its PCIe link trained at the speed and width it\n"
+                               "supports, and its GPU's at full width: a card in a worn slot or riser (x8, or a\n"
+                               "lower generation) moves RDMA at a fraction of the rail's rate.  Such a NIC is left\n"
+                               "unconfigured and named in status.errors.  Reported in the agent's status either way.",
+                "type": "boolean"},
         },
     }
     host_nic = {

@@ -121,6 +121,8 @@ class AmdScaleOutSpec:
     railSwitchPattern: str = ""
     # Minimum negotiated link speed of every scale-out NIC, Gb/s (0 = off)
     minLinkSpeedGbps: int = 0
+    # Every scale-out NIC's PCIe link trained at the speed and width it supports, its GPU's at full width
+    requireFullPcieLink: bool = False
     # L3 jumbo-frame check against the switch port's LLDP 802.3 Maximum Frame Size (None = on)
     checkPeerMtu: Optional[bool] = None
     # With disableFirmwareLldp: hand DCBX to the host on DCB NICs without a firmware-LLDP flag
@@ -135,7 +137,8 @@ class AmdScaleOutSpec:
     _FIELDS = ("disableNetworkManager", "layer", "image", "pullPolicy", "mtu", "xgmiCheck", "lldpAnnounce",
                "interfaces", "nicDrivers", "disableFirmwareLldp", "metricsPort", "gpuDirectRdma", "rcclEnv",
                "railTableBase", "rcclSocketIfname", "lldpCache", "verifyPeers", "lldpWait", "carrierWait", "keepConfigOnRestart",
-               "railSwitchPattern", "minLinkSpeedGbps", "checkPeerMtu", "handDcbxToHost", "validation")
+               "railSwitchPattern", "minLinkSpeedGbps", "requireFullPcieLink", "checkPeerMtu", "handDcbxToHost",
+               "validation")
 
     def to_dict(self) -> dict:
         d: dict = {}
@@ -181,6 +184,8 @@ class AmdScaleOutSpec:
             d["railSwitchPattern"] = self.railSwitchPattern
         if self.minLinkSpeedGbps:
             d["minLinkSpeedGbps"] = self.minLinkSpeedGbps
+        if self.requireFullPcieLink:
+            d["requireFullPcieLink"] = True
         if self.checkPeerMtu is not None:
             d["checkPeerMtu"] = self.checkPeerMtu
         if self.handDcbxToHost:
@@ -213,6 +218,7 @@ class AmdScaleOutSpec:
             keepConfigOnRestart=bool(d.pop("keepConfigOnRestart", False)),
             railSwitchPattern=d.pop("railSwitchPattern", "") or "",
             minLinkSpeedGbps=int(d.pop("minLinkSpeedGbps", 0) or 0),
+            requireFullPcieLink=bool(d.pop("requireFullPcieLink", False)),
             checkPeerMtu=d.pop("checkPeerMtu", None),
             handDcbxToHost=bool(d.pop("handDcbxToHost", False)),
             verifyPeers=bool(d.pop("verifyPeers", False)),

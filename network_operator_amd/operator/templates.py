@@ -126,6 +126,8 @@ def agent_args(p: T.NetworkClusterPolicy) -> List[str]:
         args.append(f"--rail-switch-pattern={so.railSwitchPattern}")
     if so.minLinkSpeedGbps:
         args.append(f"--min-link-speed-gbps={so.minLinkSpeedGbps}")
+    if so.requireFullPcieLink:
+        args.append("--require-full-pcie")
     if so.checkPeerMtu is False and so.layer == "L3":
         args.append("--check-peer-mtu=false")
     args.append(f"--link-state={ARTIFACT_DIR_CONTAINER}/{LINK_STATE_FILE}")

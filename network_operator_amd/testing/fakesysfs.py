@@ -43,6 +43,8 @@ def _pci(root: Path, pcipath: str, driver: str, vendor: str, device: str, numa: 
     _w(d / "subsystem_device", device + "\n")
     _w(d / "max_link_speed", "32.0 GT/s PCIe\n")
     _w(d / "max_link_width", "16\n")
+    _w(d / "current_link_speed", "32.0 GT/s PCIe\n")  # trained at the maximum, as on the live node
+    _w(d / "current_link_width", "16\n")
     # Bridges above the function (root port, switch up/downstream ports): the attributes RCCL's
     # topology reads from each of them (Broadcom PEX switch ports, like the live node).
     parts = pcipath.split("/")
@@ -165,6 +167,13 @@ def build_mi355x_node(root: Path, nic_names: Optional[Dict[str, str]] = None, ni
 
 GPU_METRICS_FIXTURE = FIXTURE.parent / "gpu_metrics_v1_8.bin"
 _GM18_XGMI_STATUS = 264  # u16 per link slot: 1 up, 0 down, 0xffff no link
+
+
+def set_pcie_link(root: Path, bdf: str, speed_gts: float, width: int) -> None:
+    """The PCIe link a function trained at (a card in a worn slot: 16 GT/s x8 of 32 GT/s x16)."""
+    d = Path(root) / "bus" / "pci" / "devices" / bdf
+    _w(d / "current_link_speed", f"{speed_gts:.1f} GT/s PCIe\n")
+    _w(d / "current_link_width", f"{width}\n")
 
 
 def set_xgmi_link(root: Path, bdf: str, slot: int, up: bool) -> None:

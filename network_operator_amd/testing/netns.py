@@ -319,7 +319,7 @@ def run_scenario(n_nics: int = 8, mode: str = "L3", seed: int | None = None, int
                  switch_max_frame: int = 0, dark_port: int | None = None,
                  dark_port_up_after: float | None = None, kill_mid_config: int = 0, rail_driver: str = "",
                  xgmi_down_at_start: tuple | None = None, xgmi_up_after: float | None = None,
-                 xgmi_link_flap: tuple | None = None) -> dict:
+                 xgmi_link_flap: tuple | None = None, pcie_degraded: dict | None = None) -> dict:
     """Runs one node bring-up.  Must already be inside a private user+net namespace.
 
     nm_bus: run the agent with --disable-networkmanager against a real ``dbus-daemon`` on which a
@@ -344,7 +344,10 @@ def run_scenario(n_nics: int = 8, mode: str = "L3", seed: int | None = None, int
     xgmi_down_at_start / xgmi_link_flap: (GPU index, link slot) whose xGMI link is down in the
     GPU's gpu_metrics before the agent starts / goes down after readiness and comes back.
     xgmi_up_after: the link down at start comes up that many seconds after the agent started;
-    the reasons the agent gave meanwhile are kept."""
+    the reasons the agent gave meanwhile are kept.
+
+    pcie_degraded: {NIC index (an int, or its str after JSON): (GT/s, width)} -- that rail's NIC trained its PCIe link below the
+    maximum (32 GT/s x16); {"gpu<i>": (GT/s, width)} the same for GPU i."""
     from . import fakesysfs
 
     nat = _native()
@@ -357,6 +360,12 @@ def run_scenario(n_nics: int = 8, mode: str = "L3", seed: int | None = None, int
     try:
         fx = fakesysfs.build_mi355x_node(tmp / "sys", n_gpus=n_nics, rail_driver=rail_driver,
                                          drop_xgmi_pairs=[tuple(p) for p in (drop_xgmi or [])])
+        for key, (gts, width) in (pcie_degraded or {}).items():
+            if isinstance(key, str) and key.startswith("gpu"):
+                bdf = fx["gpus"][int(key[3:])]["bdf"]
+            else:
+                bdf = fakesysfs.nic_pci_dir(tmp / "sys", nat.discover(str(tmp / "sys"))["pairs"][int(key)]["nic"]).name
+            fakesysfs.set_pcie_link(tmp / "sys", bdf, gts, width)
         if xgmi_down_at_start is not None:
             fakesysfs.set_xgmi_link(tmp / "sys", fx["gpus"][xgmi_down_at_start[0]]["bdf"], xgmi_down_at_start[1], False)
         pairs = nat.discover(str(tmp / "sys"))["pairs"]

@@ -234,3 +234,31 @@ def test_xgmi_link_state_from_gpu_metrics_matches_amd_smi(tmp_path):
     if out.is_dir():
         (out / "xgmi_health_box.json").write_text(json.dumps(
             {"agent_status_xgmi_links": st["xgmi_links"], "gpu_metrics": list(mine.values()), "amd_smi": smi}, indent=1))
+
+
+@pytest.mark.gpu
+def test_pcie_links_of_every_rail_read_as_sysfs_has_them():
+    """--require-full-pcie on the box's real PCIe tree: the agent's reading of every paired GPU's
+    and NIC's trained and maximum link agrees with the raw sysfs text, and on this pool's nodes
+    every rail trained at its maximum (so the check would not hold a healthy node back)."""
+    root = os.environ.get("SYSFS_ROOT", "/sys/")
+    o = sysfs_oracle(root)
+    want = native().discover(root, "affine")
+    if not want["pairs"]:
+        pytest.skip("no GPU <-> NIC pair in this sysfs")
+    seen = {}
+    for p in want["pairs"]:
+        for bdf in (p["gpu"], o["nics"][p["nic"]]["bdf"]):
+            got = native().read_pcie_link(root, bdf)
+            d = os.path.join(root, "bus/pci/devices", bdf)
+            raw = {a: _read(os.path.join(d, a)) for a in ("current_link_speed", "current_link_width", "max_link_speed",
+                                                          "max_link_width")}
+            assert got["known"], (bdf, raw)
+            assert got["speed_gts"] == float(raw["current_link_speed"].split()[0]), (bdf, raw, got)
+            assert got["width"] == int(raw["current_link_width"]) and got["max_width"] == int(raw["max_link_width"]), (bdf, raw)
+            seen[bdf] = got["str"]
+    degraded = {b: s for b, s in seen.items() if " of " in s}
+    assert not degraded, degraded
+    out = Path(os.environ.get("GRAFT_REPO_ROOT", ".")) / "gpurun_out"
+    if out.is_dir():
+        (out / "pcie_links_rails_box.json").write_text(json.dumps(seen, indent=1))

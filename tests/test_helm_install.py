@@ -431,7 +431,7 @@ _AMD_VALUES = {
     "interfaces": ["ens1np0", "ens2np0"], "nicDrivers": ["mlx5_core", "bnxt_en"], "disableFirmwareLldp": True,
     "metricsPort": 9501, "gpuDirectRdma": "DmaBuf", "rcclEnv": {"NCCL_IB_TC": "106"}, "railTableBase": 100,
     "rcclSocketIfname": "eno1", "lldpCache": True, "verifyPeers": True, "lldpWait": "2m", "carrierWait": "45s",
-    "keepConfigOnRestart": True, "railSwitchPattern": "leaf-r{rail}-.*", "minLinkSpeedGbps": 400,
+    "keepConfigOnRestart": True, "railSwitchPattern": "leaf-r{rail}-.*", "minLinkSpeedGbps": 400, "requireFullPcieLink": True,
     "checkPeerMtu": False, "handDcbxToHost": True, "maxUnavailable": "25%",
     "validation": {"enabled": True, "minBusbw": 300, "minLink": 40, "gpus": 4, "image": "reg/val:1"},
     "tolerations": [{"key": "amd.com/gpu", "operator": "Exists", "effect": "NoSchedule"}],

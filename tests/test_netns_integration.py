@@ -609,3 +609,23 @@ def test_an_xgmi_link_down_keeps_the_node_unlabelled_and_a_drop_withdraws_the_la
     assert f["reason"] and "xGMI: GPU 0000:0a:00.0: link 5 down" in f["reason"], f
     assert f["restore_s"] is not None and f["restore_s"] < 3.0, f
     assert r["agent_rc"] == 0
+
+
+def test_a_rail_whose_pcie_link_trained_narrow_is_reported_and_with_require_full_pcie_not_labelled():
+    """A NIC (or its GPU) whose PCIe link trained below what it supports moves RDMA at a fraction
+    of the rail's rate.  The agent reports the link of every NIC and its GPU (status.json
+    ``pcie`` / ``gpu_pcie``, ``netop_agent_nic_pcie_degraded``); with --require-full-pcie such a
+    rail is not configured and the node stays unlabelled, naming it.  A GPU's link speed alone
+    may drop while the GPU idles, so only its width counts."""
+    r = netns.run_isolated(n_nics=2, seed=45, interval="30s", fast_start=True,
+                           pcie_degraded={1: (16.0, 8), "gpu0": (2.5, 16)})
+    _check_configured(r)
+    st = {i["name"]: i for i in r["status"]["interfaces"]}
+    assert st[r["nics"][0]]["pcie"] == "32.0 GT/s x16" and st[r["nics"][1]]["pcie"] == "16.0 GT/s x8 of 32.0 GT/s x16"
+    assert st[r["nics"][0]]["gpu_pcie"] == "2.5 GT/s x16 of 32.0 GT/s x16"
+    r = netns.run_isolated(n_nics=2, seed=45, interval="30s", fast_start=True, wait="3s",
+                           pcie_degraded={1: (16.0, 8), "gpu0": (2.5, 16)}, extra_args=["--require-full-pcie"])
+    assert not r["ready"]
+    why = r["status_at_exit"]["interfaces"]
+    assert "its PCIe link trained at 16.0 GT/s x8 of 32.0 GT/s x16" in why[1].get("config_error", ""), why
+    assert not why[0].get("config_error"), why  # the idle GPU's lower speed alone is not a fault

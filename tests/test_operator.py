@@ -295,6 +295,13 @@ def test_schema_validation_rejects_bad_specs():
     run(body())
 
 
+def test_require_full_pcie_link_reaches_the_agent():
+    p = T.new_policy("x", layer="L2", requireFullPcieLink=True)
+    assert "--require-full-pcie" in agent_args(p)
+    assert "--require-full-pcie" not in agent_args(T.new_policy("x", layer="L2"))
+    assert T.NetworkClusterPolicy.from_dict(p.to_dict()).spec.amdScaleOut.requireFullPcieLink is True
+
+
 def test_agent_args_mi355x_options():
     p = T.new_policy("x", layer="L3", xgmiCheck=True, lldpAnnounce=False, interfaces=["ens1", "ens2"],
                      nicDrivers=["mlx5_core"])
