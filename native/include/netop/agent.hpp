@@ -433,6 +433,10 @@ class Agent {
     void read_xgmi_health();
     std::string xgmi_health_problem() const;
     std::string check_pcie(const NicState& n) const;  // "" when fine or not required
+    // GPU rails whose NIC has no RDMA device (its RDMA driver is not loaded): RCCL could only use
+    // them over TCP sockets.  Reported always; fatal with --require-gdr.
+    std::vector<std::string> no_rdma_;
+    void check_rdma();
     topo::GdrReport gdr_;
     void check_gdr();
     std::map<std::string, std::string> status_node() const;

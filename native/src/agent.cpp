@@ -397,6 +397,23 @@ std::string Agent::xgmi_health_problem() const {
 }
 
 
+void Agent::check_rdma() {
+    no_rdma_.clear();
+    for (const auto& p : disc_.pairs) {
+        const auto& nic = disc_.nics[size_t(p.nic)];
+        if (nic.rdma_dev.empty()) no_rdma_.push_back(nic.ifname);
+    }
+    if (no_rdma_.empty()) return;
+    const std::string why = "scale-out NIC(s) without an RDMA device: " + join(no_rdma_, ", ") +
+                            " (RCCL could only use them over TCP sockets: load the NIC's RDMA driver, e.g. ionic_rdma, "
+                            "mlx5_ib, bnxt_re)";
+    if (cfg_.require_gdr.empty() || cfg_.dry_run) {
+        NLOG_W("%s%s", cfg_.require_gdr.empty() ? "" : "dry run: a real start would fail: ", why.c_str());
+        return;
+    }
+    throw AgentError("GPUDirect RDMA required, but " + why);
+}
+
 void Agent::check_gdr() {
     std::string root = cfg_.sysfs_root.empty() ? topo::sysfs_root() : cfg_.sysfs_root;
     gdr_ = topo::detect_gdr(root);
@@ -521,6 +538,7 @@ void Agent::run(int stop_fd) {
     // milliseconds instead of after the LLDP wait, and nothing is left for the critical path.
     check_xgmi();
     mark("xgmi");
+    check_rdma();
     if (cfg_.mode == "L3" || !cfg_.require_gdr.empty()) {
         check_gdr();
         mark("gdr");

@@ -52,6 +52,7 @@ std::map<std::string, std::string> Agent::status_node() const {
             m["xgmi_links"] = strfmt("%d up, %d down on %d GPUs, x%d at %d Gb/s (gpu_metrics)", up, down, gpus, width, speed);
         if (!xgmi_error_.empty()) m["xgmi_error"] = xgmi_error_;
     }
+    if (!no_rdma_.empty()) m["nics_without_rdma"] = join(no_rdma_, ",");
     if (cpu_ms_at_ready_ >= 0) m["cpu_ms_at_ready"] = strfmt("%.3f", cpu_ms_at_ready_);
     if (!excluded_.empty()) {
         std::vector<std::string> parts;

@@ -33,6 +33,10 @@ def test_agent_dry_run_on_this_node(tmp_path):
     assert [(g, b, n) for g, b, n, _ in pairs] == [(str(index[p["gpu"]]), p["gpu"], p["nic"]) for p in want["pairs"]]
     x = native().read_xgmi(root)
     assert st["xgmi_pairs"] == f"{x['pairs_connected']}/{x['pairs_expected']}"
+    # Rails whose NIC has no RDMA device (RDMA driver not loaded) are named, exactly those.
+    bare = sorted(p["nic"] for p in want["pairs"] if not any(n["ifname"] == p["nic"] and n["rdma_dev"]
+                                                              for n in want["nics"]))
+    assert sorted(filter(None, st.get("nics_without_rdma", "").split(","))) == bare, (st, bare)
     assert st["dry_run"] == "true" and st["ready"] is False
     xml = topo.read_text()
     assert xml.startswith('<system version="2">') and xml.count("<net ") == len(want["pairs"])

@@ -324,3 +324,25 @@ def test_dry_run_reports_an_xgmi_link_down_without_failing(native, tmp_path):
     st = json.loads(status.read_text())
     assert st["xgmi_links"] == "55 up, 1 down on 8 GPUs, x16 at 38 Gb/s (gpu_metrics)"
     assert st["xgmi_error"] == f"GPU {bdfs[2]}: link 6 down"
+
+
+def test_a_rail_without_an_rdma_device_is_named(native, tmp_path):
+    """A scale-out NIC whose RDMA driver is not loaded (no /sys/class/infiniband device) leaves RCCL
+    only TCP sockets on that rail: the agent names it (log, status.json ``nics_without_rdma``);
+    with --require-gdr it is a failure.  (Boxes of this pool with Pollara NICs look like this.)"""
+    import shutil
+
+    fx = fakesysfs.build_mi355x_node(tmp_path / "sys", n_gpus=2)
+    first_rail = native.discover(str(tmp_path / "sys"))["pairs"][0]["nic"]
+    victim = next(n for n in fx["nics"] if n["ifname"] == first_rail)
+    shutil.rmtree(tmp_path / "sys" / "devices" / victim["pcipath"] / "infiniband")
+    for dev in list((tmp_path / "sys" / "class" / "infiniband").iterdir()):
+        if not dev.exists():
+            dev.unlink()
+    status = tmp_path / "status.json"
+    r = subprocess.run([str(native_bin("discover")), "--dry-run", "--xgmi-expect=0", f"--status-file={status}"],
+                       capture_output=True, text=True, timeout=60, env=dict(os.environ, SYSFS_ROOT=str(tmp_path / "sys")))
+    assert r.returncode == 0, r.stderr[-2000:]
+    st = json.loads(status.read_text())
+    assert st.get("nics_without_rdma") == victim["ifname"], (st, victim)
+    assert "without an RDMA device: " + victim["ifname"] in r.stderr
