@@ -249,7 +249,7 @@ async def _scenario(tmp: Path, n_nics: int, mode: str, seed: int, interval: str,
                     teardown: bool, node_name: str, policy_kw: dict, update_mtu: int, config_type: str,
                     flap: bool, validation: str, crash_agent: bool, driver_reload: bool, ha: bool,
                     silent_nics: int = 0, lldp_wait: str = "", duplicate_policy: bool = False,
-                    dark_port_s: float = 0.0, host_nics_owned: bool = False) -> dict:
+                    dark_port_s: float = 0.0, host_nics_owned: bool = False, pcie_narrow_nic: int = -1) -> dict:
     from ..api.v1alpha1 import types as T
     from ..operator import kube, manager
     from ..operator.kube import ApiClient, KubeConfig
@@ -273,6 +273,8 @@ async def _scenario(tmp: Path, n_nics: int, mode: str, seed: int, interval: str,
     for nif in nic_names:
         if nif in HOST_NICS:
             fakesysfs.unbind_driver(tmp / "sys", nif)
+    if pcie_narrow_nic >= 0:  # that rail's NIC trained its PCIe link at 16 GT/s x8 (a worn slot)
+        fakesysfs.set_pcie_link(tmp / "sys", fakesysfs.nic_pci_dir(tmp / "sys", nic_names[pcie_narrow_nic]).name, 16.0, 8)
     plan = netns.random_plan(len(nic_names), rng)
     for n in nat.discover(str(tmp / "sys"))["nics"]:  # RoCE v2 GIDs as the RDMA core adds them
         if n["ifname"] in nic_names and n["rdma_dev"]:
@@ -382,6 +384,17 @@ async def _scenario(tmp: Path, n_nics: int, mode: str, seed: int, interval: str,
                 await asyncio.sleep(max(0.0, t_agent + dark_port_s - time.monotonic()))
                 netns.set_switch_port(sw.pid, sw.ports[0], True)
                 t_port_up = time.monotonic()
+            if pcie_narrow_nic >= 0:
+                # The agent leaves that rail unconfigured and says why; the operator puts it into
+                # status.errors, naming the node.
+                def pcie_errors():
+                    st = (fake.get_object(P, name) or {}).get("status") or {}
+                    return [e for e in st.get("errors") or [] if "PCIe link trained" in e]
+                t_err = await _until(lambda: bool(pcie_errors()), 30)
+                res["policy_to_pcie_error_s"] = round(t_err - t0, 6) if t_err else None
+                res["policy_status"] = (fake.get_object(P, name) or {}).get("status")
+                res["node_labels"] = node.node_labels()
+                return res
             if silent_nics:
                 # A switch port that never sends LLDP: the agent's exit error names the NIC, its
                 # driver and what it heard, and the operator puts that into status.errors.
@@ -821,14 +834,16 @@ def run_scenario(n_nics: int = 2, mode: str = "L3", seed: int = 1, interval: str
                  update_mtu: int = 0, config_type: str = "amd-so", flap: bool = False, validation: str = "",
                  crash_agent: bool = False, driver_reload: bool = False, ha: bool = False,
                  silent_nics: int = 0, lldp_wait: str = "", keep_tmp: bool = False,
-                 duplicate_policy: bool = False, dark_port_s: float = 0.0, host_nics_owned: bool = False) -> dict:
+                 duplicate_policy: bool = False, dark_port_s: float = 0.0, host_nics_owned: bool = False,
+                 pcie_narrow_nic: int = -1) -> dict:
     """Must already run inside a private user+net namespace (``run_isolated``)."""
     tmp = Path(tempfile.mkdtemp(prefix="netop-e2e-"))
     try:
         return asyncio.run(_scenario(tmp, n_nics, mode, seed, interval, fast_start, teardown, node_name,
                                      dict(policy_kw or {}), update_mtu, config_type, flap, validation,
                                      crash_agent, driver_reload, ha, silent_nics, lldp_wait, duplicate_policy,
-                                     dark_port_s=dark_port_s, host_nics_owned=host_nics_owned))
+                                     dark_port_s=dark_port_s, host_nics_owned=host_nics_owned,
+                                     pcie_narrow_nic=pcie_narrow_nic))
     finally:
         if not keep_tmp:
             shutil.rmtree(tmp, ignore_errors=True)

@@ -305,3 +305,15 @@ def test_host_nic_policy_with_nothing_to_configure_idles_without_restarts():
     assert idle["probe_failures"] >= 2  # the kubelet kept probing ...
     warnings = [e for e in idle["policy_events"] if e[0] in ("NodeDegraded", "AgentFailed")]
     assert len(warnings) == 1 and warnings[0][1] == 1, idle["policy_events"]  # ... one report
+
+
+def test_require_full_pcie_link_names_the_rail_that_trained_narrow_in_the_policy_status():
+    """amdScaleOut.requireFullPcieLink through the operator: the DaemonSet passes
+    --require-full-pcie, the agent leaves the rail whose NIC trained at x8 unconfigured, and the
+    policy's status.errors names the node, the NIC and its link; the node is not labelled."""
+    r = e2e.run_isolated(n_nics=2, mode="L3", seed=27, pcie_narrow_nic=1, teardown=False,
+                         policy_kw={"requireFullPcieLink": True})
+    assert r["policy_to_pcie_error_s"] is not None, (r.get("policy_status"), r["agent_log"][-2000:])
+    errs = [e for e in r["policy_status"]["errors"] if "PCIe link trained" in e]
+    assert errs and r["nics"][1] in errs[0] and "16.0 GT/s x8 of 32.0 GT/s x16" in errs[0], errs
+    assert "amd.feature.node.kubernetes.io/gpu-scale-out" not in r["node_labels"]
