@@ -96,7 +96,7 @@ def generate(out_dir: str, sysfs_root: Optional[str] = None, env_extra: str = ""
     try:
         st = json.loads(status.read_text())
         doc["agent_status"] = {k: st[k] for k in ("xgmi_pairs", "xgmi_links", "xgmi_error", "gpudirect_rdma", "phases_ms",
-                                                  "not_in_netns") if k in st}
+                                                  "not_in_netns", "nics_without_rdma") if k in st}
     except (OSError, ValueError):
         pass
     if doc["env"].get("NCCL_TOPO_FILE") != doc["topo_file"]:
