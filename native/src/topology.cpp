@@ -586,6 +586,18 @@ PcieLink read_pcie_link(const std::string& root, const std::string& bdf) {
     l.max_speed_gts = gts("max_link_speed");
     l.width = lanes("current_link_width");
     l.max_width = lanes("max_link_width");
+    // The link can train no faster or wider than the port above it supports (a Gen5 card in a
+    // Gen4 slot is not degraded): the maximum is the lower of the two ends'.
+    char real[PATH_MAX];
+    if (::realpath(dir.c_str(), real)) {
+        const std::string up = path_dirname(real);
+        auto v = read_attr(path_join(up, "max_link_speed"));
+        const double up_gts = v ? std::strtod(v->c_str(), nullptr) : 0.0;
+        auto w = read_attr(path_join(up, "max_link_width"));
+        const int up_width = w ? int(std::strtol(w->c_str(), nullptr, 10)) : 0;
+        if (up_gts > 0) l.max_speed_gts = std::min(l.max_speed_gts, up_gts);
+        if (up_width > 0) l.max_width = std::min(l.max_width, up_width);
+    }
     return l;
 }
 

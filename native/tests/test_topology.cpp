@@ -201,6 +201,20 @@ TEST(topology_pcie_link_trained_vs_supported) {
     t.write(d + "current_link_speed", "Unknown\n");  // a link that is down
     CHECK(!read_pcie_link(t.path, "0000:08:00.0").known());
     CHECK(!read_pcie_link(t.path, "0000:09:00.0").known());  // no such function / no attributes
+    // A Gen5 x16 card below a Gen4 x8 port trained as far as the port goes: not degraded.
+    const std::string up = "devices/pci0000:40/0000:40:01.0", fn = up + "/0000:41:00.0";
+    t.write(up + "/max_link_speed", "16.0 GT/s PCIe\n");
+    t.write(up + "/max_link_width", "8\n");
+    t.write(fn + "/max_link_speed", "32.0 GT/s PCIe\n");
+    t.write(fn + "/max_link_width", "16\n");
+    t.write(fn + "/current_link_speed", "16.0 GT/s PCIe\n");
+    t.write(fn + "/current_link_width", "8\n");
+    t.symlink(fn, "bus/pci/devices/0000:41:00.0");
+    auto capped = read_pcie_link(t.path, "0000:41:00.0");
+    CHECK(capped.known() && !capped.degraded());
+    CHECK_EQ(capped.str(), std::string("16.0 GT/s x8"));
+    t.write(fn + "/current_link_width", "4\n");  // but below the port's x8: degraded
+    CHECK_EQ(read_pcie_link(t.path, "0000:41:00.0").str(), std::string("16.0 GT/s x4 of 16.0 GT/s x8"));
 }
 
 TEST(topology_gdr_detection) {
