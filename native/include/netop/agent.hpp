@@ -432,6 +432,11 @@ class Agent {
     std::string xgmi_error_;  // what the last gpu_metrics read found wrong (empty: fine or not read)
     void read_xgmi_health();
     std::string xgmi_health_problem() const;
+    // The start's read runs beside link-up and the LLDP wait (each gpu_metrics read is an SMU
+    // query, ~0.2 ms per GPU): joined by finish_xgmi_health() before the label decision.
+    std::future<std::vector<topo::XgmiLinkHealth>> xgmi_health_future_;
+    void finish_xgmi_health();
+    std::vector<std::string> xgmi_health_bdfs() const;
     std::string check_pcie(const NicState& n) const;  // "" when fine or not required
     // GPU rails whose NIC has no RDMA device (its RDMA driver is not loaded): RCCL could only use
     // them over TCP sockets.  Reported always; fatal with --require-gdr.

@@ -349,7 +349,43 @@ void Agent::check_xgmi() {
     };
     if (xgmi_.pairs_connected < expect)
         fail(strfmt("xGMI mesh incomplete: %d of %d GPU pairs linked", xgmi_.pairs_connected, expect));
-    read_xgmi_health();
+    if (cfg_.dry_run) {  // nothing to overlap with: read now
+        read_xgmi_health();
+        finish_xgmi_health();
+        return;
+    }
+    auto work = [root = cfg_.sysfs_root.empty() ? topo::sysfs_root() : cfg_.sysfs_root, bdfs = xgmi_health_bdfs()] {
+        return topo::read_xgmi_health(root, bdfs);
+    };
+    try {
+        xgmi_health_future_ = std::async(std::launch::async, work);
+    } catch (const std::system_error&) {  // no thread to spare: read when it is needed
+        xgmi_health_future_ = std::async(std::launch::deferred, work);
+    }
+}
+
+std::vector<std::string> Agent::xgmi_health_bdfs() const {
+    // The amdgpu PCI functions discovery found: KFD lists a GPU the container cannot open with
+    // its properties filtered (no BDF), while its PCI device (and gpu_metrics) is still readable.
+    std::vector<std::string> bdfs;
+    for (const auto& g : disc_.gpus) bdfs.push_back(g.pci.bdf);
+    if (bdfs.empty())
+        for (const auto& g : xgmi_.gpus)
+            if (g.is_gpu()) bdfs.push_back(g.bdf());
+    return bdfs;
+}
+
+void Agent::read_xgmi_health() {
+    std::string root = cfg_.sysfs_root.empty() ? topo::sysfs_root() : cfg_.sysfs_root;
+    xgmi_health_ = topo::read_xgmi_health(root, xgmi_health_bdfs());
+    xgmi_error_ = xgmi_health_problem();
+}
+
+void Agent::finish_xgmi_health() {
+    if (xgmi_health_future_.valid()) {
+        xgmi_health_ = xgmi_health_future_.get();
+        xgmi_error_ = xgmi_health_problem();
+    }
     for (const auto& h : xgmi_health_) {
         if (h.known)
             NLOG_I("xGMI %s: %d link(s) up, %d down, x%d at %d Gb/s (gpu_metrics %s)", h.bdf.c_str(), h.links_up(),
@@ -358,26 +394,18 @@ void Agent::check_xgmi() {
             NLOG_V(1, "xGMI %s: %s", h.bdf.c_str(), h.error.c_str());
     }
     if (xgmi_error_.empty()) return;
-    if (!cfg_.dry_run && cfg_.keep_running && cfg_.monitor && cfg_.xgmi_health_interval_ns > 0) {
-        // A link can come back (retraining, a reset of the GPU): configure the NICs, stay
-        // unlabelled, and let the monitor label the node when gpu_metrics shows it up again.
+    if (cfg_.dry_run) {
+        NLOG_W("dry run: a real start would fail: xGMI: %s", xgmi_error_.c_str());
+        return;
+    }
+    if (cfg_.keep_running && cfg_.monitor && cfg_.xgmi_health_interval_ns > 0) {
+        // A link can come back (retraining, a reset of the GPU): the NICs are configured, the node
+        // stays unlabelled, and the monitor labels it when gpu_metrics shows the link up again.
         NLOG_W("xGMI: %s; the readiness label waits for the link(s)", xgmi_error_.c_str());
         return;
     }
-    fail("xGMI: " + xgmi_error_);
-}
-
-void Agent::read_xgmi_health() {
-    std::string root = cfg_.sysfs_root.empty() ? topo::sysfs_root() : cfg_.sysfs_root;
-    // The amdgpu PCI functions discovery found: KFD lists a GPU the container cannot open with
-    // its properties filtered (no BDF), while its PCI device (and gpu_metrics) is still readable.
-    std::vector<std::string> bdfs;
-    for (const auto& g : disc_.gpus) bdfs.push_back(g.pci.bdf);
-    if (bdfs.empty())
-        for (const auto& g : xgmi_.gpus)
-            if (g.is_gpu()) bdfs.push_back(g.bdf());
-    xgmi_health_ = topo::read_xgmi_health(root, bdfs);
-    xgmi_error_ = xgmi_health_problem();
+    write_status();
+    throw AgentError("xGMI: " + xgmi_error_);
 }
 
 std::string Agent::xgmi_health_problem() const {
@@ -676,6 +704,8 @@ void Agent::run(int stop_fd) {
     }
 
     log_results();
+    finish_xgmi_health();  // the start's gpu_metrics read, beside link-up and LLDP
+    mark("xgmi_health");
 
     if (!cfg_.configure) {
         if (cfg_.mode == "L3") write_host_config();
