@@ -17,6 +17,7 @@
 #include <cstddef>
 
 #include <algorithm>
+#include <tuple>
 #include <cstring>
 #include <ctime>
 #include <sched.h>
@@ -186,16 +187,6 @@ void Agent::get_network_configs(const std::vector<std::string>& names) {
             n.numa_node = disc_.gpus[size_t(p.gpu)].pci.numa;
             n.pcie_path = topo::to_string(p.path);
         }
-        {
-            const std::string root = cfg_.sysfs_root.empty() ? topo::sysfs_root() : cfg_.sysfs_root;
-            if (auto d = topo::netdev_pci(root, name)) n.pcie = topo::read_pcie_link(root, d->bdf);
-            if (!n.gpu_bdf.empty()) n.gpu_pcie = topo::read_pcie_link(root, n.gpu_bdf);
-            if (n.pcie.degraded())
-                NLOG_W("Interface '%s': PCIe link trained at %s", name.c_str(), n.pcie.str().c_str());
-            if (n.gpu_pcie.degraded())
-                NLOG_W("Interface '%s': the PCIe link of its GPU %s trained at %s", name.c_str(), n.gpu_bdf.c_str(),
-                       n.gpu_pcie.str().c_str());
-        }
         if (n.rdma_dev.empty())  // host NICs (rdma discovery): no GPU, but still an RDMA device
             for (auto& nic : disc_.nics)
                 if (nic.ifname == name) {
@@ -206,6 +197,40 @@ void Agent::get_network_configs(const std::vector<std::string>& names) {
         nics_.push_back(std::move(n));
     }
     assign_rail_indices();
+    start_pcie();
+}
+
+void Agent::start_pcie() {
+    std::vector<std::pair<std::string, std::string>> fns;  // (NIC name, its GPU's BDF)
+    for (const auto& n : nics_) fns.emplace_back(n.ifname, n.gpu_bdf);
+    auto work = [root = cfg_.sysfs_root.empty() ? topo::sysfs_root() : cfg_.sysfs_root, fns] {
+        std::vector<std::pair<topo::PcieLink, topo::PcieLink>> out;
+        for (const auto& [ifname, gpu] : fns) {
+            topo::PcieLink nic, g;
+            if (auto d = topo::netdev_pci(root, ifname)) nic = topo::read_pcie_link(root, d->bdf);
+            if (!gpu.empty()) g = topo::read_pcie_link(root, gpu);
+            out.emplace_back(nic, g);
+        }
+        return out;
+    };
+    try {
+        pcie_future_ = std::async(std::launch::async, work);
+    } catch (const std::system_error&) {  // no thread to spare: read when it is needed
+        pcie_future_ = std::async(std::launch::deferred, work);
+    }
+}
+
+void Agent::ensure_pcie() {
+    if (!pcie_future_.valid()) return;
+    auto links = pcie_future_.get();
+    for (size_t i = 0; i < links.size() && i < nics_.size(); ++i) {
+        NicState& n = nics_[i];
+        std::tie(n.pcie, n.gpu_pcie) = links[i];
+        if (n.pcie.degraded()) NLOG_W("Interface '%s': PCIe link trained at %s", n.ifname.c_str(), n.pcie.str().c_str());
+        if (n.gpu_pcie.degraded())
+            NLOG_W("Interface '%s': the PCIe link of its GPU %s trained at %s", n.ifname.c_str(), n.gpu_bdf.c_str(),
+                   n.gpu_pcie.str().c_str());
+    }
 }
 
 void Agent::interfaces_up() {
@@ -704,6 +729,7 @@ void Agent::run(int stop_fd) {
     }
 
     log_results();
+    ensure_pcie();         // (reported in the status even where no check needed it)
     finish_xgmi_health();  // the start's gpu_metrics read, beside link-up and LLDP
     mark("xgmi_health");
 

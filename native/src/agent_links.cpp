@@ -410,7 +410,8 @@ std::string Agent::silent_summary() const {
     return out;
 }
 
-std::string Agent::check_pcie(const NicState& n) const {
+std::string Agent::check_pcie(NicState& n) {
+    ensure_pcie();
     if (!cfg_.require_full_pcie) return "";
     if (n.pcie.degraded())
         return strfmt("its PCIe link trained at %s: RDMA moves at a fraction of the rail's rate (reseat the card, check the "
