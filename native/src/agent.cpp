@@ -411,13 +411,18 @@ void Agent::finish_xgmi_health() {
         xgmi_health_ = xgmi_health_future_.get();
         xgmi_error_ = xgmi_health_problem();
     }
-    for (const auto& h : xgmi_health_) {
-        if (h.known)
-            NLOG_I("xGMI %s: %d link(s) up, %d down, x%d at %d Gb/s (gpu_metrics %s)", h.bdf.c_str(), h.links_up(),
+    int gpus = 0, up = 0;
+    for (const auto& h : xgmi_health_) {  // one line on the critical path; the details at -v=1
+        if (h.known) {
+            ++gpus;
+            up += h.links_up();
+            NLOG_V(1, "xGMI %s: %d link(s) up, %d down, x%d at %d Gb/s (gpu_metrics %s)", h.bdf.c_str(), h.links_up(),
                    h.links_down(), h.width, h.speed_gbps, h.revision.c_str());
-        else
+        } else {
             NLOG_V(1, "xGMI %s: %s", h.bdf.c_str(), h.error.c_str());
+        }
     }
+    if (gpus) NLOG_I("xGMI links: %d up on %d GPU(s) (gpu_metrics)", up, gpus);
     if (xgmi_error_.empty()) return;
     if (cfg_.dry_run) {
         NLOG_W("dry run: a real start would fail: xGMI: %s", xgmi_error_.c_str());

@@ -67,6 +67,9 @@ std::map<std::string, std::string> Agent::status_node() const {
 }
 
 void Agent::log_results() {
+    // The reference's summary (cmd/discover/main.go logResults) at -v=3 only: below that it would
+    // still cost an address dump per NIC on the way to the label.
+    if (log::verbosity() < 3) return;
     for (auto& n : nics_) {
         NLOG_V(3, "Interface '%s' %s:", n.ifname.c_str(), n.link.flags_str().c_str());
         std::string s = "\tConfigured addresses: ";

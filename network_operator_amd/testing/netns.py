@@ -319,7 +319,8 @@ def run_scenario(n_nics: int = 8, mode: str = "L3", seed: int | None = None, int
                  switch_max_frame: int = 0, dark_port: int | None = None,
                  dark_port_up_after: float | None = None, kill_mid_config: int = 0, rail_driver: str = "",
                  xgmi_down_at_start: tuple | None = None, xgmi_up_after: float | None = None,
-                 xgmi_link_flap: tuple | None = None, pcie_degraded: dict | None = None) -> dict:
+                 xgmi_link_flap: tuple | None = None, pcie_degraded: dict | None = None,
+                 link_state: bool = True) -> dict:
     """Runs one node bring-up.  Must already be inside a private user+net namespace.
 
     nm_bus: run the agent with --disable-networkmanager against a real ``dbus-daemon`` on which a
@@ -417,8 +418,9 @@ def run_scenario(n_nics: int = 8, mode: str = "L3", seed: int | None = None, int
                 f"--wait={wait}", f"--rccl-net={tmp / 'rccl-net.json'}", f"--rccl-env={tmp / 'rccl.env'}",
                 f"--rccl-topo={tmp / 'rccl-topo.xml'}", f"--status-file={tmp / 'status.json'}", f"--nfd-features-dir={feat}", f"--xgmi-expect={xgmi_expect}",
                 f"--pipeline={'true' if pipeline else 'false'}", f"--lldp-announce={'true' if announce else 'false'}",
-                f"--systemd-networkd={tmp / 'networkd'}", f"--link-state={tmp / 'link-state'}", f"-v={verbose}",
-                *(extra_args or [])]
+                f"--systemd-networkd={tmp / 'networkd'}", f"-v={verbose}", *(extra_args or [])]
+        if link_state:  # as the operator passes it (off: an agent build older than the flag, bench/agent_ab.py)
+            args.append(f"--link-state={tmp / 'link-state'}")
         if lldp_cache:
             args.append(f"--lldp-cache={tmp / 'lldp-cache'}")
         env = dict(os.environ, SYSFS_ROOT=str(tmp / "sys"), NODE_NAME="mi355x-node-0")
