@@ -343,7 +343,12 @@ class Agent {
     void dry_run_report();
     const std::string& topo_xml();  // joins the worker; "" when generation failed
     std::vector<std::string> socket_ifnames() const;
-    void check_xgmi();
+    void check_xgmi();     // dry run: join the prefetched KFD topology and gpu_metrics now
+    void join_xgmi();      // the prefetched KFD topology, evaluated (right after link-up)
+    void evaluate_xgmi();  // the mesh check
+    std::future<topo::XgmiReport> xgmi_future_;
+    std::future<void> prefetch_;  // the reader thread (start_prefetch); its futures are below
+    void start_prefetch();
     void log_results();
     void mark(const std::string& phase);
     void write_status();
@@ -432,16 +437,14 @@ class Agent {
     std::string xgmi_error_;  // what the last gpu_metrics read found wrong (empty: fine or not read)
     void read_xgmi_health();
     std::string xgmi_health_problem() const;
-    // The start's read runs beside link-up and the LLDP wait (each gpu_metrics read is an SMU
-    // query, ~0.2 ms per GPU): joined by finish_xgmi_health() before the label decision.
+    // The start's gpu_metrics read (start_prefetch; an SMU query per GPU): joined by
+    // finish_xgmi_health() before the label decision.
     std::future<std::vector<topo::XgmiLinkHealth>> xgmi_health_future_;
     void finish_xgmi_health();
     std::vector<std::string> xgmi_health_bdfs() const;
     std::string check_pcie(NicState& n);  // "" when fine or not required
-    // The NICs' and their GPUs' PCIe links, read beside link-up and the LLDP wait (~0.5 ms of
-    // config-space reads for 8 rails on the box) and joined by ensure_pcie() at first use.
+    // The NICs' and their GPUs' PCIe links (start_prefetch), joined by ensure_pcie() at first use.
     std::future<std::vector<std::pair<topo::PcieLink, topo::PcieLink>>> pcie_future_;
-    void start_pcie();
     void ensure_pcie();
     // GPU rails whose NIC has no RDMA device (its RDMA driver is not loaded): RCCL could only use
     // them over TCP sockets.  Reported always; fatal with --require-gdr.

@@ -197,26 +197,63 @@ void Agent::get_network_configs(const std::vector<std::string>& names) {
         nics_.push_back(std::move(n));
     }
     assign_rail_indices();
-    start_pcie();
+    start_prefetch();
 }
 
-void Agent::start_pcie() {
+void Agent::start_prefetch() {
+    // What the start needs from sysfs beyond discovery, read by one thread beside link-up and the
+    // LLDP wait, in the order it is needed: the KFD topology (joined right after link-up), the
+    // rails' PCIe links (first NIC configured), the GPUs' gpu_metrics (before the label).  On the
+    // box these are ~1.1, ~0.5 and ~1.65 ms of reads (profiles/r5_box_read_costs.json).
     std::vector<std::pair<std::string, std::string>> fns;  // (NIC name, its GPU's BDF)
     for (const auto& n : nics_) fns.emplace_back(n.ifname, n.gpu_bdf);
-    auto work = [root = cfg_.sysfs_root.empty() ? topo::sysfs_root() : cfg_.sysfs_root, fns] {
-        std::vector<std::pair<topo::PcieLink, topo::PcieLink>> out;
+    std::vector<std::string> gpus;
+    for (const auto& g : disc_.gpus) gpus.push_back(g.pci.bdf);
+    const bool xgmi = cfg_.xgmi_expect_links >= 0;
+    auto p_xgmi = std::make_shared<std::promise<topo::XgmiReport>>();
+    auto p_pcie = std::make_shared<std::promise<std::vector<std::pair<topo::PcieLink, topo::PcieLink>>>>();
+    auto p_health = std::make_shared<std::promise<std::vector<topo::XgmiLinkHealth>>>();
+    xgmi_future_ = xgmi ? p_xgmi->get_future() : std::future<topo::XgmiReport>();
+    pcie_future_ = p_pcie->get_future();
+    xgmi_health_future_ = xgmi ? p_health->get_future() : std::future<std::vector<topo::XgmiLinkHealth>>();
+    const int main_cpu = ::sched_getcpu();
+    auto work = [root = cfg_.sysfs_root.empty() ? topo::sysfs_root() : cfg_.sysfs_root, fns, gpus, xgmi, main_cpu,
+                 p_xgmi, p_pcie, p_health](bool pin) {
+        if (pin) {  // off the agent thread's CPU, which brings the links up meanwhile
+            cpu_set_t set;
+            if (main_cpu >= 0 && ::sched_getaffinity(0, sizeof set, &set) == 0 && CPU_COUNT(&set) > 1) {
+                CPU_CLR(main_cpu, &set);
+                (void)::sched_setaffinity(0, sizeof set, &set);
+            }
+        }
+        topo::XgmiReport x;
+        if (xgmi) {
+            x = topo::read_xgmi(root);
+            p_xgmi->set_value(x);
+        }
+        std::vector<std::pair<topo::PcieLink, topo::PcieLink>> links;
         for (const auto& [ifname, gpu] : fns) {
             topo::PcieLink nic, g;
             if (auto d = topo::netdev_pci(root, ifname)) nic = topo::read_pcie_link(root, d->bdf);
             if (!gpu.empty()) g = topo::read_pcie_link(root, gpu);
-            out.emplace_back(nic, g);
+            links.emplace_back(nic, g);
         }
-        return out;
+        p_pcie->set_value(std::move(links));
+        if (xgmi) {
+            // The amdgpu PCI functions discovery found: KFD lists a GPU the container cannot open
+            // with its properties filtered (no BDF), while its PCI device (and gpu_metrics) is
+            // still readable.  Without discovered GPUs, KFD's own list.
+            std::vector<std::string> bdfs = gpus;
+            if (bdfs.empty())
+                for (const auto& g : x.gpus)
+                    if (g.is_gpu()) bdfs.push_back(g.bdf());
+            p_health->set_value(topo::read_xgmi_health(root, bdfs));
+        }
     };
     try {
-        pcie_future_ = std::async(std::launch::async, work);
-    } catch (const std::system_error&) {  // no thread to spare: read when it is needed
-        pcie_future_ = std::async(std::launch::deferred, work);
+        prefetch_ = std::async(std::launch::async, work, true);
+    } catch (const std::system_error&) {  // no thread to spare: read everything now
+        work(false);
     }
 }
 
@@ -359,10 +396,18 @@ std::map<std::string, Ipv4Prefix> Agent::cached_addresses() const {
 }
 
 
-void Agent::check_xgmi() {
-    if (cfg_.xgmi_expect_links < 0) return;
-    std::string root = cfg_.sysfs_root.empty() ? topo::sysfs_root() : cfg_.sysfs_root;
-    xgmi_ = topo::read_xgmi(root);
+void Agent::check_xgmi() {  // dry run: everything in line
+    join_xgmi();
+    finish_xgmi_health();
+}
+
+void Agent::join_xgmi() {
+    if (!xgmi_future_.valid()) return;
+    xgmi_ = xgmi_future_.get();
+    evaluate_xgmi();
+}
+
+void Agent::evaluate_xgmi() {
     int expect = cfg_.xgmi_expect_links == 0 ? xgmi_.pairs_expected : cfg_.xgmi_expect_links;
     NLOG_I("xGMI: %zu GPUs, %d/%d GPU pairs linked, %llu MB/s per GPU advertised", xgmi_.gpus.size(), xgmi_.pairs_connected,
            xgmi_.pairs_expected, (unsigned long long)xgmi_.per_gpu_bw_mbs());
@@ -374,19 +419,6 @@ void Agent::check_xgmi() {
     };
     if (xgmi_.pairs_connected < expect)
         fail(strfmt("xGMI mesh incomplete: %d of %d GPU pairs linked", xgmi_.pairs_connected, expect));
-    if (cfg_.dry_run) {  // nothing to overlap with: read now
-        read_xgmi_health();
-        finish_xgmi_health();
-        return;
-    }
-    auto work = [root = cfg_.sysfs_root.empty() ? topo::sysfs_root() : cfg_.sysfs_root, bdfs = xgmi_health_bdfs()] {
-        return topo::read_xgmi_health(root, bdfs);
-    };
-    try {
-        xgmi_health_future_ = std::async(std::launch::async, work);
-    } catch (const std::system_error&) {  // no thread to spare: read when it is needed
-        xgmi_health_future_ = std::async(std::launch::deferred, work);
-    }
 }
 
 std::vector<std::string> Agent::xgmi_health_bdfs() const {
@@ -592,10 +624,13 @@ void Agent::run(int stop_fd) {
     // From the agent's discovery, at background priority on another CPU: overlaps the checks,
     // link-up and the LLDP wait.
     start_topo();
-    // The xGMI mesh does not depend on LLDP: verify it up front, so a broken mesh fails in
-    // milliseconds instead of after the LLDP wait, and nothing is left for the critical path.
-    check_xgmi();
-    mark("xgmi");
+    // The xGMI mesh does not depend on LLDP: its KFD topology is read beside link-up (~1 ms on
+    // the box) and checked right after it, so a broken mesh still fails before any address is
+    // touched or the LLDP wait begins.  A dry run reads it in line.
+    if (cfg_.dry_run) {
+        check_xgmi();
+        mark("xgmi");
+    }
     check_rdma();
     if (cfg_.mode == "L3" || !cfg_.require_gdr.empty()) {
         check_gdr();
@@ -639,6 +674,8 @@ void Agent::run(int stop_fd) {
     load_link_state();
     interfaces_up();
     mark("link_up");
+    join_xgmi();
+    mark("xgmi");
     load_mtu_state();
     interfaces_set_mtu();
     mark("mtu");
