@@ -167,6 +167,17 @@ def run(gpus: int, min_busbw: float, min_link_GBps: float, max_bytes: int, sysfs
         checks.append(_check("gpu_nic_affinity", bool(topo.pairs) and not topo.unpaired_gpus,
                              pairs={p.gpu_bdf: f"{p.nic} ({p.path})" for p in topo.pairs},
                              unpaired_gpus=topo.unpaired_gpus))
+        # The links' trained state (amdgpu gpu_metrics), as the agent reads it: none down.
+        from .agent import native
+
+        health = native().read_xgmi_health(sysfs_root, list(topo.gpus))
+        known = [h for h in health if h["known"]]
+        if known:
+            down = {h["bdf"]: [i for i, st in enumerate(h["status"]) if st == 0] for h in known}
+            checks.append(_check("xgmi_link_state", not any(down.values()),
+                                 links_up=sum(st == 1 for h in known for st in h["status"]),
+                                 down={b: v for b, v in down.items() if v},
+                                 width=min(h["width"] for h in known), speed_gbps=min(h["speed_gbps"] for h in known)))
         tf = Path(artifact_dir) / "rccl-topo.xml"
         if tf.exists():
             agree = topo_file_agrees(tf.read_text(), topo)
