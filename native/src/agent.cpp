@@ -226,28 +226,43 @@ void Agent::start_prefetch() {
                 (void)::sched_setaffinity(0, sizeof set, &set);
             }
         }
-        topo::XgmiReport x;
-        if (xgmi) {
-            x = topo::read_xgmi(root);
-            p_xgmi->set_value(x);
-        }
-        std::vector<std::pair<topo::PcieLink, topo::PcieLink>> links;
-        for (const auto& [ifname, gpu] : fns) {
-            topo::PcieLink nic, g;
-            if (auto d = topo::netdev_pci(root, ifname)) nic = topo::read_pcie_link(root, d->bdf);
-            if (!gpu.empty()) g = topo::read_pcie_link(root, gpu);
-            links.emplace_back(nic, g);
-        }
-        p_pcie->set_value(std::move(links));
-        if (xgmi) {
-            // The amdgpu PCI functions discovery found: KFD lists a GPU the container cannot open
-            // with its properties filtered (no BDF), while its PCI device (and gpu_metrics) is
-            // still readable.  Without discovered GPUs, KFD's own list.
-            std::vector<std::string> bdfs = gpus;
-            if (bdfs.empty())
-                for (const auto& g : x.gpus)
-                    if (g.is_gpu()) bdfs.push_back(g.bdf());
-            p_health->set_value(topo::read_xgmi_health(root, bdfs));
+        try {
+            topo::XgmiReport x;
+            if (xgmi) {
+                x = topo::read_xgmi(root);
+                p_xgmi->set_value(x);
+            }
+            std::vector<std::pair<topo::PcieLink, topo::PcieLink>> links;
+            for (const auto& [ifname, gpu] : fns) {
+                topo::PcieLink nic, g;
+                if (auto d = topo::netdev_pci(root, ifname)) nic = topo::read_pcie_link(root, d->bdf);
+                if (!gpu.empty()) g = topo::read_pcie_link(root, gpu);
+                links.emplace_back(nic, g);
+            }
+            p_pcie->set_value(std::move(links));
+            if (xgmi) {
+                // The amdgpu PCI functions discovery found: KFD lists a GPU the container cannot
+                // open with its properties filtered (no BDF), while its PCI device (and
+                // gpu_metrics) is still readable.  Without discovered GPUs, KFD's own list.
+                std::vector<std::string> bdfs = gpus;
+                if (bdfs.empty())
+                    for (const auto& g : x.gpus)
+                        if (g.is_gpu()) bdfs.push_back(g.bdf());
+                p_health->set_value(topo::read_xgmi_health(root, bdfs));
+            }
+        } catch (...) {
+            // Every join must return: the failure goes to whichever results are still owed (the
+            // callable, and with it the promises, lives as long as the async state).
+            const auto e = std::current_exception();
+            auto owe = [&](auto& promise) {
+                try {
+                    promise->set_exception(e);
+                } catch (const std::future_error&) {  // already delivered
+                }
+            };
+            owe(p_xgmi);
+            owe(p_pcie);
+            owe(p_health);
         }
     };
     try {
