@@ -62,6 +62,9 @@ struct NicState {
     std::string pcie_path;  // GPU <-> NIC PCIe path type (PIX / PXB / ...)
     // PCIe links of the NIC and of its GPU as trained (read at discovery; --require-full-pcie)
     topo::PcieLink pcie, gpu_pcie;
+    // The monitor found the link (or its GPU's) retrained below its maximum after readiness
+    // (--require-full-pcie): the label waits for it.  "" = fine.
+    std::string pcie_error;
     // Per-rail source routing: this NIC's rail k (its GPU index; NICs without a GPU get indices
     // above every GPU's) and what the agent installed for it, so exactly that is removed later.
     int rail_index = -1;

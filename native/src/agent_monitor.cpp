@@ -95,7 +95,8 @@ int Agent::verify_peers(const std::vector<NicState*>& which, int64_t timeout_ns,
 }
 
 bool Agent::nic_healthy(const NicState& n) const {
-    if (!n.link.up() || n.degraded || n.cache_stale || n.no_carrier || !n.config_error.empty()) return false;
+    if (!n.link.up() || n.degraded || n.cache_stale || n.no_carrier || !n.config_error.empty() || !n.pcie_error.empty())
+        return false;
     if (cfg_.mode == "L3" && cfg_.verify_peers_ns > 0 && !n.peer_verified) return false;
     return cfg_.mode != "L3" || n.configured;
 }
@@ -118,6 +119,7 @@ void Agent::monitor(int stop_fd) {
     const bool xgmi_watch = cfg_.xgmi_expect_links >= 0 && cfg_.xgmi_health_interval_ns > 0 &&
                             std::any_of(xgmi_health_.begin(), xgmi_health_.end(), [](const topo::XgmiLinkHealth& h) { return h.known; });
     int64_t next_xgmi = mono_ns() + cfg_.xgmi_health_interval_ns;
+    int64_t next_pcie = next_xgmi;
     bool labelled = ready_;  // false: L2 came up with a NIC still without carrier
     // One pollable fd for "stop or link event": the LLDP wait returns as soon as either
     // fires, so a link failure is acted on in about a millisecond, not at the next tick.
@@ -239,6 +241,24 @@ void Agent::monitor(int stop_fd) {
                 changed = true;
             }
             next_xgmi = mono_ns() + cfg_.xgmi_health_interval_ns;
+        }
+        if (cfg_.require_full_pcie && cfg_.xgmi_health_interval_ns > 0 && mono_ns() >= next_pcie) {
+            // A link can retrain narrower or slower at run time (after PCIe errors, a reset).
+            const std::string root = cfg_.sysfs_root.empty() ? topo::sysfs_root() : cfg_.sysfs_root;
+            for (auto& n : nics_) {
+                if (!n.configured) continue;  // left unconfigured at start: a restart re-checks it
+                if (auto d = topo::netdev_pci(root, n.ifname)) n.pcie = topo::read_pcie_link(root, d->bdf);
+                if (!n.gpu_bdf.empty()) n.gpu_pcie = topo::read_pcie_link(root, n.gpu_bdf);
+                std::string why = check_pcie(n);
+                if (why == n.pcie_error) continue;
+                if (why.empty())
+                    NLOG_I("Interface '%s': PCIe link back at %s", n.ifname.c_str(), n.pcie.str().c_str());
+                else
+                    NLOG_W("Interface '%s': %s", n.ifname.c_str(), why.c_str());
+                n.pcie_error = why;
+                changed = true;
+            }
+            next_pcie = mono_ns() + cfg_.xgmi_health_interval_ns;
         }
         if (cfg_.mode == "L3" && cfg_.verify_peers_ns > 0 && mono_ns() >= next_verify) {
             // NICs whose peer has not answered (yet): a recovered link, a new /30, or a switch

@@ -262,6 +262,8 @@ std::string Agent::not_ready_reason() const {
             why = n.lldp_silent;
         else if (!n.config_error.empty())
             why = n.config_error;
+        else if (!n.pcie_error.empty())
+            why = n.pcie_error;
         else if (!n.addr_error.empty() && !n.configured)
             why = n.addr_error;
         else if (n.cache_stale)

@@ -71,7 +71,7 @@ int main(int argc, char** argv) {
     fs.add_int("xgmi-expect", &cfg.xgmi_expect_links, "verify the xGMI mesh before labelling: -1 off, 0 full mesh, N GPU pairs; the links' trained state (amdgpu gpu_metrics) too: a link down fails the check");
     fs.add_bool("require-full-pcie", &cfg.require_full_pcie, "configure (and label) a NIC only if its PCIe link trained at the speed and width it supports, and its GPU's at full width; degraded links are reported either way (status.json, metrics)");
     fs.add_int("xgmi-min-link-width", &cfg.xgmi_min_link_width, "with --xgmi-expect: the narrowest trained xGMI link width (lanes) a GPU may run at, from gpu_metrics; 0 = any");
-    fs.add_duration("xgmi-health-interval", &cfg.xgmi_health_interval_ns, "with --xgmi-expect and the monitor: how often the xGMI links' state is read again; a link down withdraws the readiness label until it is back (0 = at start only)");
+    fs.add_duration("xgmi-health-interval", &cfg.xgmi_health_interval_ns, "with the monitor: how often the xGMI links' state (with --xgmi-expect) and the rails' PCIe links (with --require-full-pcie) are read again; a link down or retrained narrower withdraws the readiness label until it is back (0 = at start only)");
     fs.add_duration("link-wait", &cfg.link_wait_ns, "time to wait for link state echoes from the kernel");
     fs.add_duration("carrier-wait", &cfg.carrier_wait_ns, "L2: time every admin-up NIC may take to get a carrier (optic and switch port link training) before it is reported as 'no carrier'; meanwhile the readiness probe says 'waiting for carrier' (with the monitor a NIC still dark afterwards is labelled when its carrier comes)");
     fs.add_duration("verify-peers", &cfg.verify_peers_ns,

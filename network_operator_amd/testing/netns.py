@@ -320,7 +320,7 @@ def run_scenario(n_nics: int = 8, mode: str = "L3", seed: int | None = None, int
                  dark_port_up_after: float | None = None, kill_mid_config: int = 0, rail_driver: str = "",
                  xgmi_down_at_start: tuple | None = None, xgmi_up_after: float | None = None,
                  xgmi_link_flap: tuple | None = None, pcie_degraded: dict | None = None,
-                 link_state: bool = True) -> dict:
+                 link_state: bool = True, pcie_flap: int | None = None) -> dict:
     """Runs one node bring-up.  Must already be inside a private user+net namespace.
 
     nm_bus: run the agent with --disable-networkmanager against a real ``dbus-daemon`` on which a
@@ -346,6 +346,8 @@ def run_scenario(n_nics: int = 8, mode: str = "L3", seed: int | None = None, int
     GPU's gpu_metrics before the agent starts / goes down after readiness and comes back.
     xgmi_up_after: the link down at start comes up that many seconds after the agent started;
     the reasons the agent gave meanwhile are kept.
+
+    pcie_flap: after readiness that rail's NIC retrains its PCIe link at 16 GT/s x8, then back.
 
     pcie_degraded: {NIC index (an int, or its str after JSON): (GT/s, width)} -- that rail's NIC trained its PCIe link below the
     maximum (32 GT/s x16); {"gpu<i>": (GT/s, width)} the same for GPU i."""
@@ -674,6 +676,24 @@ def run_scenario(n_nics: int = 8, mode: str = "L3", seed: int | None = None, int
             fakesysfs.set_xgmi_link(tmp / "sys", bdf, xgmi_link_flap[1], True)
             back = _wait_for(label, 10, agent)
             res["xgmi_flap"] = {"gpu": bdf, "withdraw_s": (gone - t_down) if gone else None,
+                                "restore_s": (back - t_up) if back else None, "reason": why}
+        if pcie_flap is not None and t_ready:
+            bdf = fakesysfs.nic_pci_dir(tmp / "sys", nic_names[pcie_flap]).name
+            time.sleep(0.05)  # status.json follows the label
+            t_down = time.monotonic()
+            fakesysfs.set_pcie_link(tmp / "sys", bdf, 16.0, 8)
+            gone = None
+            while time.monotonic() < t_down + 10 and agent.poll() is None:
+                if not label.exists():
+                    gone = time.monotonic()
+                    break
+                time.sleep(0.002)
+            reason = tmp / "status.json.not-ready"
+            why = reason.read_text() if reason.exists() else None
+            t_up = time.monotonic()
+            fakesysfs.set_pcie_link(tmp / "sys", bdf, 32.0, 16)
+            back = _wait_for(label, 10, agent)
+            res["pcie_flap"] = {"withdraw_s": (gone - t_down) if gone else None,
                                 "restore_s": (back - t_up) if back else None, "reason": why}
         if soak_cycles and t_ready:
             # Carrier loss on a random port, over and over, with the agent in monitor mode: every

@@ -629,3 +629,12 @@ def test_a_rail_whose_pcie_link_trained_narrow_is_reported_and_with_require_full
     why = r["status_at_exit"]["interfaces"]
     assert "its PCIe link trained at 16.0 GT/s x8 of 32.0 GT/s x16" in why[1].get("config_error", ""), why
     assert not why[0].get("config_error"), why  # the idle GPU's lower speed alone is not a fault
+    # A rail that retrains narrower after readiness (PCIe errors, a reset): the monitor withdraws
+    # the label with the reason and restores it when the link is back at x16.
+    r = netns.run_isolated(n_nics=2, seed=46, interval="30s", fast_start=True, pcie_flap=0,
+                           extra_args=["--require-full-pcie", "--xgmi-health-interval=100ms"])
+    _check_configured(r)
+    f = r["pcie_flap"]
+    assert f["withdraw_s"] is not None and f["withdraw_s"] < 3.0, f
+    assert f["reason"] and "its PCIe link trained at 16.0 GT/s x8 of 32.0 GT/s x16" in f["reason"], f
+    assert f["restore_s"] is not None and f["restore_s"] < 3.0, f
