@@ -29,8 +29,9 @@ OPERATOR_CLUSTER_RULES: Tuple[Tuple[str, Tuple[str, ...], Tuple[str, ...]], ...]
     ("apps", ("daemonsets",), READ + WRITE),
     ("", ("pods",), READ),
     # Which nodes a newer policy of one type is held off (the ones an older policy selects too):
-    # a LIST by label selector, three names at most, and only while two policies overlap.
-    ("", ("nodes",), ("list",)),
+    # a LIST by label selector, three names at most, and only while two policies overlap.  GET:
+    # the uid of a node an Event is recorded on (kubectl describe node matches events by it).
+    ("", ("nodes",), ("get", "list")),
     # Agent ServiceAccount + OpenShift SCC RoleBinding (created on OpenShift only).
     ("", ("serviceaccounts",), ("get", "list", "create", "update", "delete")),
     ("rbac.authorization.k8s.io", ("rolebindings",), ("get", "list", "create", "update", "delete")),

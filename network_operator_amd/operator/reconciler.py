@@ -415,18 +415,19 @@ class EventRecorder:
         self.client, self.namespace, self.component = client, namespace, component
         self.sent = 0
 
-    async def event(self, obj: dict, type_: str, reason: str, message: str) -> None:
+    async def event(self, obj: dict, type_: str, reason: str, message: str, namespace: Optional[str] = None) -> None:
         md = obj.get("metadata", {})
+        ns = namespace or self.namespace
         body = {
             "apiVersion": "v1", "kind": "Event",
-            "metadata": {"generateName": f"{md.get('name', 'obj')}.", "namespace": self.namespace},
+            "metadata": {"generateName": f"{md.get('name', 'obj')}.", "namespace": ns},
             "involvedObject": {"apiVersion": obj.get("apiVersion"), "kind": obj.get("kind"), "name": md.get("name"),
                                "uid": md.get("uid")},
             "type": type_, "reason": reason, "message": message, "source": {"component": self.component},
             "count": 1,
         }
         try:
-            await self.client.create(kube.EVENTS, body, namespace=self.namespace)
+            await self.client.create(kube.EVENTS, body, namespace=ns)
             self.sent += 1
         except Exception as e:  # events must never fail a reconcile
             log.debug("event not recorded: %s", e)
@@ -1001,9 +1002,27 @@ class NetworkClusterPolicyReconciler:
             elif e not in cur.errors and "scale-out not ready (" in e and "): " in e:
                 if e in degraded:
                     await self._event(raw, "Warning", "NodeDegraded", e[:1024])
+                    await self._node_event(e, "ScaleOutDegraded", p.name)
                 elif not e.endswith(tuple(STARTUP_REASONS)):
                     await self._event(raw, "Warning", "AgentFailed", e[:1024])
+                    await self._node_event(e, "ScaleOutAgentFailed", p.name)
         return Result(requeue_after=requeue_after)
+
+    async def _node_event(self, error: str, reason: str, policy: str) -> None:
+        """The same news on the Node itself, so ``kubectl describe node`` shows why its scale-out
+        label went or never came.  Events of cluster-scoped objects live in "default"; describe
+        matches them by the Node's uid, hence the GET (rare: once per new message)."""
+        if not self.recorder:
+            return
+        node = error.split(": scale-out not ready (", 1)[0]
+        try:
+            obj = await self.client.get(kube.NODES, node)
+        except ApiError as e:
+            log.debug("node %s for its event: %s", node, e)
+            return
+        why = error.split("): ", 1)[1] if "): " in error else error
+        await self.recorder.event({"apiVersion": "v1", "kind": "Node", "metadata": obj.get("metadata", {})},
+                                  "Warning", reason, f"{why} (policy {policy})"[:1024], namespace="default")
 
     # -- entry point -------------------------------------------------------------------------------
     async def reconcile(self, name: str) -> Result:

@@ -601,6 +601,13 @@ async def _scenario(tmp: Path, n_nics: int, mode: str, seed: int, interval: str,
                 await _until(lambda: any(e.get("reason") == "NodeDegraded" for e in fake.list_objects(kube.EVENTS)), 5)
                 res["policy_events_after_flap"] = sorted({e.get("reason") for e in fake.list_objects(kube.EVENTS)
                                                           if (e.get("involvedObject") or {}).get("kind") == T.KIND})
+                await _until(lambda: any((e.get("involvedObject") or {}).get("kind") == "Node"
+                                         for e in fake.list_objects(kube.EVENTS)), 5)
+                node_obj = fake.get_object(kube.NODES, node_name) or {}
+                res["node_events_after_flap"] = [
+                    {"reason": e.get("reason"), "message": e.get("message"), "namespace": e["metadata"].get("namespace"),
+                     "uid_matches": (e.get("involvedObject") or {}).get("uid") == node_obj.get("metadata", {}).get("uid")}
+                    for e in fake.list_objects(kube.EVENTS) if (e.get("involvedObject") or {}).get("kind") == "Node"]
                 res["flap_status"] = (fake.get_object(P, name) or {}).get("status")
                 # The readiness probe's output, which the kubelet puts in the Pod's events.
                 c0 = next(iter(node.containers.values()))

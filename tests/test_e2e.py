@@ -140,6 +140,10 @@ def test_link_failure_is_reported_by_the_policy_and_recovers():
     assert st["errors"] == [f"mi355x-0: scale-out not ready (ContainersNotReady): {r['nics'][0]}: link down"]
     assert r["port_down_to_reason_in_status_s"] is not None
     assert "NodeDegraded" in r["policy_events_after_flap"] and "AgentFailed" not in r["policy_events_after_flap"]
+    # ... and on the Node itself, for kubectl describe node (matched by the Node's uid)
+    assert r["node_events_after_flap"] == [{"reason": "ScaleOutDegraded", "namespace": "default", "uid_matches": True,
+                                            "message": f"{r['nics'][0]}: link down (policy scale-out)"}], \
+        r["node_events_after_flap"]
     assert any(c["type"] == "Degraded" and c["status"] == "True" for c in st["conditions"])
     assert r["port_up_to_all_good_s"] is not None, r["agent_log"]
     # kubectl describe pod: "Readiness probe failed: not ready: <nic>: link down"
