@@ -1,0 +1,94 @@
+"""Is this node ready for the operator?  One read-only look, without privileges, at everything the
+agent checks before it labels a node: each GPU's scale-out rail (the NIC behind its PCIe switch,
+the NIC's driver and RDMA device), both ends' PCIe links as trained, the xGMI mesh (KFD) and
+every xGMI link's state (gpu_metrics), and GPUDirect RDMA.
+
+    python -m network_operator_amd.agent.report            # a table
+    python -m network_operator_amd.agent.report --json     # the same as one JSON document
+    SYSFS_ROOT=/path/to/sys python -m network_operator_amd.agent.report
+
+It reads what the agent reads, through the same native code (``_netop_native``), so a problem
+shown here is the reason the agent would give.  Nothing is changed.  The exit status is 1 when
+something would keep the label off the node with the policy defaults plus `requireFullPcieLink`
+and `gpuDirectRdma: Any`.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import sys
+from typing import List
+
+from . import native
+
+
+def collect(root: str) -> dict:
+    n = native()
+    d = n.discover(root)
+    nics = {x["ifname"]: x for x in d["nics"]}
+    rails = []
+    for p in d["pairs"]:
+        nic = nics.get(p["nic"], {})
+        rails.append({"gpu": p["gpu"], "nic": p["nic"], "path": p["path"], "driver": nic.get("driver", ""),
+                      "rdma_dev": nic.get("rdma_dev", ""), "nic_pcie": n.read_pcie_link(root, nic.get("bdf", "")),
+                      "gpu_pcie": n.read_pcie_link(root, p["gpu"])})
+    x = n.read_xgmi(root)
+    health = n.read_xgmi_health(root, [g["bdf"] for g in d["gpus"]])
+    gdr = n.detect_gdr(root, platform.release())
+    problems: List[str] = []
+    paired = {r["gpu"] for r in rails}
+    problems += [f"GPU {g['bdf']}: no scale-out NIC behind its PCIe switch" for g in d["gpus"] if g["bdf"] not in paired]
+    problems += [f"{r['nic']}: no RDMA device (load its RDMA driver)" for r in rails if not r["rdma_dev"]]
+    for r in rails:
+        if r["nic_pcie"]["degraded"]:
+            problems.append(f"{r['nic']}: PCIe link {r['nic_pcie']['str']}")
+        if r["gpu_pcie"]["known"] and r["gpu_pcie"]["width"] < r["gpu_pcie"]["max_width"]:
+            problems.append(f"GPU {r['gpu']}: PCIe link {r['gpu_pcie']['str']}")
+    if x["pairs_connected"] < x["pairs_expected"]:
+        problems.append(f"xGMI mesh: {x['pairs_connected']} of {x['pairs_expected']} GPU pairs linked")
+    for h in health:
+        down = [i for i, s in enumerate(h["status"]) if s == 0]
+        if down:
+            problems.append(f"GPU {h['bdf']}: xGMI link(s) {', '.join(map(str, down))} down")
+    if gdr["mode"] == "none":
+        problems.append("GPUDirect RDMA unavailable (no amdkfd peer-memory client, no RDMA dma-buf)")
+    return {"sysfs_root": root, "gpus": len(d["gpus"]), "rails": rails,
+            "xgmi": {"pairs": f"{x['pairs_connected']}/{x['pairs_expected']}", "links": health},
+            "gpudirect_rdma": gdr["mode"], "kernel": gdr["kernel"], "left_alone": d.get("excluded", {}),
+            "problems": problems}
+
+
+def render(r: dict) -> str:
+    out = [f"{r['gpus']} GPU(s), {len(r['rails'])} scale-out rail(s); xGMI pairs {r['xgmi']['pairs']}; "
+           f"GPUDirect RDMA {r['gpudirect_rdma']} (kernel {r['kernel']})", ""]
+    out.append(f"{'GPU':14} {'NIC':14} {'path':5} {'driver':10} {'RDMA':10} {'NIC PCIe':30} {'GPU PCIe':30}")
+    for x in r["rails"]:
+        out.append(f"{x['gpu']:14} {x['nic']:14} {x['path']:5} {x['driver'] or '-':10} {x['rdma_dev'] or 'none':10} "
+                   f"{x['nic_pcie']['str']:30} {x['gpu_pcie']['str']:30}")
+    known = [h for h in r["xgmi"]["links"] if h["known"]]
+    if known:
+        letter = {1: "U", 0: "D", -1: "X"}
+        out += ["", "xGMI links (gpu_metrics " + known[0]["revision"] + "; U up, D down, X no link):"]
+        for h in known:
+            out.append(f"  {h['bdf']}  {''.join(letter[s] for s in h['status'])}  x{h['width']} at {h['speed_gbps']} Gb/s")
+    elif r["xgmi"]["links"]:
+        out += ["", "xGMI link state not read: " + r["xgmi"]["links"][0]["error"]]
+    out += ["", "Problems:" if r["problems"] else "No problems found."]
+    out += [f"  - {p}" for p in r["problems"]]
+    return "\n".join(out)
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(prog="python -m network_operator_amd.agent.report", description=__doc__.split("\n\n")[0])
+    ap.add_argument("--json", action="store_true", help="one JSON document instead of the table")
+    a = ap.parse_args(argv)
+    r = collect(os.environ.get("SYSFS_ROOT", "/sys/"))
+    print(json.dumps(r, indent=1) if a.json else render(r))
+    return 1 if r["problems"] else 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -268,3 +268,26 @@ def test_pcie_links_of_every_rail_read_as_sysfs_has_them():
     out = Path(os.environ.get("GRAFT_REPO_ROOT", ".")) / "gpurun_out"
     if out.is_dir():
         (out / "pcie_links_rails_box.json").write_text(json.dumps(seen, indent=1))
+
+
+@pytest.mark.gpu
+def test_node_report_on_this_node():
+    """The read-only node report on the box: one rail per paired GPU, the xGMI link state of every
+    GPU read, GPUDirect RDMA detected; its problems (if any) are the hardware's, recorded."""
+    import sys
+
+    r = subprocess.run([sys.executable, "-m", "network_operator_amd.agent.report", "--json"], capture_output=True,
+                       text=True, timeout=60)
+    assert r.returncode in (0, 1), r.stderr[-2000:]
+    rep = json.loads(r.stdout)
+    want = native().discover(os.environ.get("SYSFS_ROOT", "/sys/"), "affine")
+    assert sorted((x["gpu"], x["nic"]) for x in rep["rails"]) == sorted((p["gpu"], p["nic"]) for p in want["pairs"])
+    assert all(h["known"] for h in rep["xgmi"]["links"]), rep["xgmi"]
+    assert rep["gpudirect_rdma"] != "none", rep
+    assert (r.returncode == 1) == bool(rep["problems"])
+    out = Path(os.environ.get("GRAFT_REPO_ROOT", ".")) / "gpurun_out"
+    if out.is_dir():
+        (out / "node_report_box.json").write_text(json.dumps(rep, indent=1))
+        (out / "node_report_box.txt").write_text(subprocess.run(
+            [sys.executable, "-m", "network_operator_amd.agent.report"], capture_output=True, text=True,
+            timeout=60).stdout)

@@ -346,3 +346,34 @@ def test_a_rail_without_an_rdma_device_is_named(native, tmp_path):
     st = json.loads(status.read_text())
     assert st.get("nics_without_rdma") == victim["ifname"], (st, victim)
     assert "without an RDMA device: " + victim["ifname"] in r.stderr
+
+
+def test_node_report_names_what_would_keep_the_label_off(tmp_path):
+    """``python -m network_operator_amd.agent.report``: the agent's own readings of a node, read
+    only.  A healthy fake node (GPUDirect RDMA via dma-buf) reports no problem and exits 0; a rail
+    trained at x8, an xGMI link down and a missing RDMA device are each named, exit 1."""
+    import shutil
+    import sys
+
+    root = tmp_path / "sys"
+    fx = fakesysfs.build_mi355x_node(root, n_gpus=4)
+    (root / "module" / "ib_uverbs").mkdir(parents=True)
+
+    def report():
+        r = subprocess.run([sys.executable, "-m", "network_operator_amd.agent.report", "--json"], capture_output=True,
+                           text=True, timeout=60, env=dict(os.environ, SYSFS_ROOT=str(root)))
+        return r.returncode, json.loads(r.stdout)
+
+    rc, rep = report()
+    assert rc == 0 and rep["problems"] == [] and len(rep["rails"]) == 4, rep
+    assert rep["gpudirect_rdma"] == "dmabuf" and rep["xgmi"]["pairs"] == "6/6"
+    rail0 = rep["rails"][0]
+    fakesysfs.set_pcie_link(root, fakesysfs.nic_pci_dir(root, rail0["nic"]).name, 16.0, 8)
+    fakesysfs.set_xgmi_link(root, fx["gpus"][1]["bdf"], 2, False)
+    victim = next(n for n in fx["nics"] if n["ifname"] == rep["rails"][3]["nic"])
+    shutil.rmtree(root / "devices" / victim["pcipath"] / "infiniband")
+    rc, rep = report()
+    assert rc == 1
+    assert rep["problems"] == [f"{victim['ifname']}: no RDMA device (load its RDMA driver)",
+                               f"{rail0['nic']}: PCIe link 16.0 GT/s x8 of 32.0 GT/s x16",
+                               f"GPU {fx['gpus'][1]['bdf']}: xGMI link(s) 2 down"], rep["problems"]
