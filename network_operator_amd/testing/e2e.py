@@ -249,7 +249,8 @@ async def _scenario(tmp: Path, n_nics: int, mode: str, seed: int, interval: str,
                     teardown: bool, node_name: str, policy_kw: dict, update_mtu: int, config_type: str,
                     flap: bool, validation: str, crash_agent: bool, driver_reload: bool, ha: bool,
                     silent_nics: int = 0, lldp_wait: str = "", duplicate_policy: bool = False,
-                    dark_port_s: float = 0.0, host_nics_owned: bool = False, pcie_narrow_nic: int = -1) -> dict:
+                    dark_port_s: float = 0.0, host_nics_owned: bool = False, pcie_narrow_nic: int = -1,
+                    xgmi_link_down: bool = False) -> dict:
     from ..api.v1alpha1 import types as T
     from ..operator import kube, manager
     from ..operator.kube import ApiClient, KubeConfig
@@ -259,7 +260,7 @@ async def _scenario(tmp: Path, n_nics: int, mode: str, seed: int, interval: str,
     rng = random.Random(seed)
     rt = netns._native().Rtnl()
     rt.link_set_up(rt.link_by_name("lo")["index"])
-    fakesysfs.build_mi355x_node(tmp / "sys", n_gpus=n_nics)
+    fx = fakesysfs.build_mi355x_node(tmp / "sys", n_gpus=n_nics)
     nat = netns._native()
     host_nic = config_type == "host-nic"
     both = config_type == "both"  # an amd-so policy and a host-nic policy on the same node
@@ -273,6 +274,8 @@ async def _scenario(tmp: Path, n_nics: int, mode: str, seed: int, interval: str,
     for nif in nic_names:
         if nif in HOST_NICS:
             fakesysfs.unbind_driver(tmp / "sys", nif)
+    if xgmi_link_down:  # GPU 1's xGMI link 3 is down in its gpu_metrics when the agent starts
+        fakesysfs.set_xgmi_link(tmp / "sys", fx["gpus"][1]["bdf"], 3, False)
     if pcie_narrow_nic >= 0:  # that rail's NIC trained its PCIe link at 16 GT/s x8 (a worn slot)
         fakesysfs.set_pcie_link(tmp / "sys", fakesysfs.nic_pci_dir(tmp / "sys", nic_names[pcie_narrow_nic]).name, 16.0, 8)
     plan = netns.random_plan(len(nic_names), rng)
@@ -384,14 +387,23 @@ async def _scenario(tmp: Path, n_nics: int, mode: str, seed: int, interval: str,
                 await asyncio.sleep(max(0.0, t_agent + dark_port_s - time.monotonic()))
                 netns.set_switch_port(sw.pid, sw.ports[0], True)
                 t_port_up = time.monotonic()
-            if pcie_narrow_nic >= 0:
-                # The agent leaves that rail unconfigured and says why; the operator puts it into
-                # status.errors, naming the node.
-                def pcie_errors():
+            if pcie_narrow_nic >= 0 or xgmi_link_down:
+                # The agent keeps the label off and says why; the operator puts it into
+                # status.errors, naming the node (and records it on the Node).
+                marker = "PCIe link trained" if pcie_narrow_nic >= 0 else "link 3 down"
+
+                def marked_errors():
                     st = (fake.get_object(P, name) or {}).get("status") or {}
-                    return [e for e in st.get("errors") or [] if "PCIe link trained" in e]
-                t_err = await _until(lambda: bool(pcie_errors()), 30)
-                res["policy_to_pcie_error_s"] = round(t_err - t0, 6) if t_err else None
+                    return [e for e in st.get("errors") or [] if marker in e]
+                t_err = await _until(lambda: bool(marked_errors()), 30)
+                res["policy_to_pcie_error_s" if pcie_narrow_nic >= 0 else "policy_to_xgmi_error_s"] = \
+                    round(t_err - t0, 6) if t_err else None
+                await _until(lambda: any((e.get("involvedObject") or {}).get("kind") == "Node"
+                                         for e in fake.list_objects(kube.EVENTS)), 5)
+                res["node_events"] = [{"reason": e.get("reason"), "message": e.get("message")}
+                                      for e in fake.list_objects(kube.EVENTS)
+                                      if (e.get("involvedObject") or {}).get("kind") == "Node"]
+                res["agent_restarts"] = sum(x.restarts for x in node.containers.values())
                 res["policy_status"] = (fake.get_object(P, name) or {}).get("status")
                 res["node_labels"] = node.node_labels()
                 return res
@@ -842,7 +854,7 @@ def run_scenario(n_nics: int = 2, mode: str = "L3", seed: int = 1, interval: str
                  crash_agent: bool = False, driver_reload: bool = False, ha: bool = False,
                  silent_nics: int = 0, lldp_wait: str = "", keep_tmp: bool = False,
                  duplicate_policy: bool = False, dark_port_s: float = 0.0, host_nics_owned: bool = False,
-                 pcie_narrow_nic: int = -1) -> dict:
+                 pcie_narrow_nic: int = -1, xgmi_link_down: bool = False) -> dict:
     """Must already run inside a private user+net namespace (``run_isolated``)."""
     tmp = Path(tempfile.mkdtemp(prefix="netop-e2e-"))
     try:
@@ -850,7 +862,7 @@ def run_scenario(n_nics: int = 2, mode: str = "L3", seed: int = 1, interval: str
                                      dict(policy_kw or {}), update_mtu, config_type, flap, validation,
                                      crash_agent, driver_reload, ha, silent_nics, lldp_wait, duplicate_policy,
                                      dark_port_s=dark_port_s, host_nics_owned=host_nics_owned,
-                                     pcie_narrow_nic=pcie_narrow_nic))
+                                     pcie_narrow_nic=pcie_narrow_nic, xgmi_link_down=xgmi_link_down))
     finally:
         if not keep_tmp:
             shutil.rmtree(tmp, ignore_errors=True)

@@ -321,3 +321,18 @@ def test_require_full_pcie_link_names_the_rail_that_trained_narrow_in_the_policy
     errs = [e for e in r["policy_status"]["errors"] if "PCIe link trained" in e]
     assert errs and r["nics"][1] in errs[0] and "16.0 GT/s x8 of 32.0 GT/s x16" in errs[0], errs
     assert "amd.feature.node.kubernetes.io/gpu-scale-out" not in r["node_labels"]
+
+
+def test_an_xgmi_link_down_reaches_the_policy_and_the_node_without_restarts():
+    """A GPU's xGMI link down in gpu_metrics (the policy's default xgmiCheck): the agent configures
+    the NICs and waits unlabelled instead of crash-looping; its reason reaches the policy's
+    status.errors and the Node's events."""
+    r = e2e.run_isolated(n_nics=2, mode="L3", seed=28, xgmi_link_down=True, teardown=False,
+                         policy_kw={"xgmiCheck": True})
+    assert r["policy_to_xgmi_error_s"] is not None, (r.get("policy_status"), r["agent_log"][-2000:])
+    errs = [e for e in r["policy_status"]["errors"] if "link 3 down" in e]
+    assert errs and "xGMI: GPU 0000:23:00.0: link 3 down" in errs[0], errs
+    assert any(e["reason"] in ("ScaleOutDegraded", "ScaleOutAgentFailed") and "link 3 down" in e["message"]
+               for e in r["node_events"]), r["node_events"]
+    assert r["agent_restarts"] == 0
+    assert "amd.feature.node.kubernetes.io/gpu-scale-out" not in r["node_labels"]
