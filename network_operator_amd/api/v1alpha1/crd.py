@@ -190,6 +190,11 @@ def openapi_schema() -> dict:
                                                "amdgpu function), which an amd-so policy owns; only for nodes that run\n"
                                                "no amd-so policy.",
                                 "type": "boolean"},
+            "minLinkSpeedGbps": {"description": "As amdScaleOut.minLinkSpeedGbps, for the host NICs.",
+                                 "minimum": 0, "maximum": 3200, "type": "integer"},
+            "requireFullPcieLink": {"description": "As amdScaleOut.requireFullPcieLink, for the host NICs (their own\n"
+                                                   "PCIe link; they have no GPU).",
+                                    "type": "boolean"},
         },
         "required": ["layer"],
     }

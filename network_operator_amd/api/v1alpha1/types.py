@@ -249,6 +249,8 @@ class HostNicSpec:
     keepConfigOnRestart: bool = False
     checkPeerMtu: Optional[bool] = None
     includeGpuRails: bool = False  # discovery may take the NICs next to the GPUs (no amd-so policy)
+    minLinkSpeedGbps: int = 0  # as amdScaleOut's, for the host NICs
+    requireFullPcieLink: bool = False  # as amdScaleOut's (host NICs have no GPU: the NIC's link)
     extra: Dict[str, Any] = field(default_factory=dict)
 
     def to_dict(self) -> dict:
@@ -272,6 +274,10 @@ class HostNicSpec:
             d["checkPeerMtu"] = self.checkPeerMtu
         if self.includeGpuRails:
             d["includeGpuRails"] = True
+        if self.minLinkSpeedGbps:
+            d["minLinkSpeedGbps"] = self.minLinkSpeedGbps
+        if self.requireFullPcieLink:
+            d["requireFullPcieLink"] = True
         d.update(copy.deepcopy(self.extra))
         return d
 
@@ -286,7 +292,9 @@ class HostNicSpec:
                 carrierWait=d.pop("carrierWait", "") or "",
                 keepConfigOnRestart=bool(d.pop("keepConfigOnRestart", False)),
                 checkPeerMtu=d.pop("checkPeerMtu", None),
-                includeGpuRails=bool(d.pop("includeGpuRails", False)))
+                includeGpuRails=bool(d.pop("includeGpuRails", False)),
+                minLinkSpeedGbps=int(d.pop("minLinkSpeedGbps", 0) or 0),
+                requireFullPcieLink=bool(d.pop("requireFullPcieLink", False)))
         s.extra = d
         return s
 

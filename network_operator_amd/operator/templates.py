@@ -226,6 +226,10 @@ def host_nic_agent_args(p: T.NetworkClusterPolicy) -> List[str]:
         args.append("--rdma-include-gpu-rails")
     if hn.checkPeerMtu is False and hn.layer == "L3":
         args.append("--check-peer-mtu=false")
+    if hn.minLinkSpeedGbps:
+        args.append(f"--min-link-speed-gbps={hn.minLinkSpeedGbps}")
+    if hn.requireFullPcieLink:
+        args.append("--require-full-pcie")
     if hn.keepConfigOnRestart:
         if hn.layer == "L3":  # its own cache beside the scale-out agent's
             args.append(f"--lldp-cache={ARTIFACT_DIR_CONTAINER}/{HOST_NIC_LLDP_CACHE_FILE}")

@@ -441,7 +441,8 @@ _AMD_VALUES = {
 _HOST_NIC_VALUES = {
     "enabled": True, "mode": "L3", "mtu": 4000, "nicDrivers": ["bnxt_en"], "driverImage": "reg/kmd:1",
     "interfaces": ["ens9np0"], "disableNetworkManager": True, "verifyPeers": True, "lldpWait": "45s", "carrierWait": "1m",
-    "checkPeerMtu": False, "keepConfigOnRestart": True, "includeGpuRails": True,
+    "checkPeerMtu": False, "keepConfigOnRestart": True, "includeGpuRails": True, "minLinkSpeedGbps": 200,
+    "requireFullPcieLink": True,
 }
 
 

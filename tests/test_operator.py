@@ -296,6 +296,11 @@ def test_schema_validation_rejects_bad_specs():
 
 
 def test_require_full_pcie_link_reaches_the_agent():
+    from network_operator_amd.operator import reconciler as R
+
+    hn = T.new_host_nic_policy("h", layer="L2", minLinkSpeedGbps=200, requireFullPcieLink=True)
+    assert {"--require-full-pcie", "--min-link-speed-gbps=200"} <= set(R.host_nic_agent_args(hn))
+    assert T.NetworkClusterPolicy.from_dict(hn.to_dict()).spec.hostNic.requireFullPcieLink is True
     p = T.new_policy("x", layer="L2", requireFullPcieLink=True)
     assert "--require-full-pcie" in agent_args(p)
     assert "--require-full-pcie" not in agent_args(T.new_policy("x", layer="L2"))
