@@ -259,6 +259,7 @@ KEPT_ORPHAN_GRACE_S = 600.0
 CLEANUP_TIMEOUT_S = 600.0  # a cleanup Job not finished by then (node gone, image missing) is given up
 CLEANUP_POLL_S = 2.0       # cleanup Jobs are not watched: poll while some are running
 CLEANUP_CREATE_CONCURRENCY = 32
+EVENT_CONCURRENCY = 16  # Events (and the Node GETs behind Node events) in flight per status update
 CLEANUP_LIST_PAGE = 500
 
 
@@ -996,16 +997,24 @@ class NetworkClusterPolicyReconciler:
             raise
         if cur.state != new_state and new_state == STATE_ALL_GOOD:
             await self._event(raw, "Normal", "AllNodesReady", f"{ready}/{targets} nodes configured")
+        sends = []
         for e in errors:  # an agent that exited / a node that degraded, with its reason: once per new message
             if e not in cur.errors and CONFLICT_MARK in e:
-                await self._event(raw, "Warning", "PolicyConflict", e[:1024])
+                sends.append(lambda e=e: self._event(raw, "Warning", "PolicyConflict", e[:1024]))
             elif e not in cur.errors and "scale-out not ready (" in e and "): " in e:
                 if e in degraded:
-                    await self._event(raw, "Warning", "NodeDegraded", e[:1024])
-                    await self._node_event(e, "ScaleOutDegraded", p.name)
+                    sends.append(lambda e=e: self._event(raw, "Warning", "NodeDegraded", e[:1024]))
+                    sends.append(lambda e=e: self._node_event(e, "ScaleOutDegraded", p.name))
                 elif not e.endswith(tuple(STARTUP_REASONS)):
-                    await self._event(raw, "Warning", "AgentFailed", e[:1024])
-                    await self._node_event(e, "ScaleOutAgentFailed", p.name)
+                    sends.append(lambda e=e: self._event(raw, "Warning", "AgentFailed", e[:1024]))
+                    sends.append(lambda e=e: self._node_event(e, "ScaleOutAgentFailed", p.name))
+        if sends:  # a switch reboot degrades every node at once: not thousands of round trips in a row
+            gate = asyncio.Semaphore(EVENT_CONCURRENCY)
+
+            async def send(make):  # (coroutines made only when sent: none left un-awaited on a cancel)
+                async with gate:
+                    await make()
+            await asyncio.gather(*(send(c) for c in sends))
         return Result(requeue_after=requeue_after)
 
     async def _node_event(self, error: str, reason: str, policy: str) -> None:
