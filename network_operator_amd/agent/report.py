@@ -1,16 +1,19 @@
 """Is this node ready for the operator?  One read-only look, without privileges, at everything the
 agent checks before it labels a node: each GPU's scale-out rail (the NIC behind its PCIe switch,
 the NIC's driver and RDMA device), both ends' PCIe links as trained, the xGMI mesh (KFD) and
-every xGMI link's state (gpu_metrics), and GPUDirect RDMA.
+every xGMI link's state (gpu_metrics), GPUDirect RDMA, and each rail's Ethernet link as the kernel
+has it now (state, negotiated speed, MTU).
 
     python -m network_operator_amd.agent.report            # a table
     python -m network_operator_amd.agent.report --json     # the same as one JSON document
+    python -m network_operator_amd.agent.report --min-link-speed-gbps 400   # the policy's floor too
     SYSFS_ROOT=/path/to/sys python -m network_operator_amd.agent.report
 
 It reads what the agent reads, through the same native code (``_netop_native``), so a problem
 shown here is the reason the agent would give.  Nothing is changed.  The exit status is 1 when
 something would keep the label off the node with the policy defaults plus `requireFullPcieLink`
-and `gpuDirectRdma: Any`.
+and `gpuDirectRdma: Any` (and `minLinkSpeedGbps`, when given).  A link that is down is not a
+problem by itself: the agent brings the rails up.
 """
 
 from __future__ import annotations
@@ -25,7 +28,35 @@ from typing import List
 from . import native
 
 
-def collect(root: str) -> dict:
+def _netdev(root: str, ifname: str) -> dict:
+    """The rail's Ethernet link from /sys/class/net/<ifname>: what ``ip link`` and ethtool show.
+    The kernel reports speed -1 (or refuses the read) while there is no carrier."""
+    d = os.path.join(root, "class", "net", ifname)
+
+    def attr(name: str) -> str:
+        try:
+            with open(os.path.join(d, name)) as f:
+                return f.read().strip()
+        except OSError:
+            return ""
+
+    speed = attr("speed")
+    mbps = int(speed) if speed.lstrip("-").isdigit() else -1
+    mtu = attr("mtu")
+    return {"operstate": attr("operstate") or "unknown", "speed_gbps": mbps / 1000 if mbps > 0 else None,
+            "mtu": int(mtu) if mtu.isdigit() else None}
+
+
+def _link_str(link: dict) -> str:
+    out = link["operstate"]
+    if link["speed_gbps"]:
+        out += f" {link['speed_gbps']:g}G"
+    if link["mtu"]:
+        out += f" mtu {link['mtu']}"
+    return out
+
+
+def collect(root: str, min_link_speed_gbps: float = 0) -> dict:
     n = native()
     d = n.discover(root)
     nics = {x["ifname"]: x for x in d["nics"]}
@@ -34,7 +65,7 @@ def collect(root: str) -> dict:
         nic = nics.get(p["nic"], {})
         rails.append({"gpu": p["gpu"], "nic": p["nic"], "path": p["path"], "driver": nic.get("driver", ""),
                       "rdma_dev": nic.get("rdma_dev", ""), "nic_pcie": n.read_pcie_link(root, nic.get("bdf", "")),
-                      "gpu_pcie": n.read_pcie_link(root, p["gpu"])})
+                      "gpu_pcie": n.read_pcie_link(root, p["gpu"]), "link": _netdev(root, p["nic"])})
     x = n.read_xgmi(root)
     health = n.read_xgmi_health(root, [g["bdf"] for g in d["gpus"]])
     gdr = n.detect_gdr(root, platform.release())
@@ -47,6 +78,9 @@ def collect(root: str) -> dict:
             problems.append(f"{r['nic']}: PCIe link {r['nic_pcie']['str']}")
         if r["gpu_pcie"]["known"] and r["gpu_pcie"]["width"] < r["gpu_pcie"]["max_width"]:
             problems.append(f"GPU {r['gpu']}: PCIe link {r['gpu_pcie']['str']}")
+        speed = r["link"]["speed_gbps"]
+        if min_link_speed_gbps and speed and speed < min_link_speed_gbps:
+            problems.append(f"{r['nic']}: link negotiated {speed:g} Gb/s, below the required {min_link_speed_gbps:g}")
     if x["pairs_connected"] < x["pairs_expected"]:
         problems.append(f"xGMI mesh: {x['pairs_connected']} of {x['pairs_expected']} GPU pairs linked")
     for h in health:
@@ -64,10 +98,10 @@ def collect(root: str) -> dict:
 def render(r: dict) -> str:
     out = [f"{r['gpus']} GPU(s), {len(r['rails'])} scale-out rail(s); xGMI pairs {r['xgmi']['pairs']}; "
            f"GPUDirect RDMA {r['gpudirect_rdma']} (kernel {r['kernel']})", ""]
-    out.append(f"{'GPU':14} {'NIC':14} {'path':5} {'driver':10} {'RDMA':10} {'NIC PCIe':30} {'GPU PCIe':30}")
+    out.append(f"{'GPU':14} {'NIC':14} {'path':5} {'driver':10} {'RDMA':10} {'link':20} {'NIC PCIe':30} {'GPU PCIe':30}")
     for x in r["rails"]:
         out.append(f"{x['gpu']:14} {x['nic']:14} {x['path']:5} {x['driver'] or '-':10} {x['rdma_dev'] or 'none':10} "
-                   f"{x['nic_pcie']['str']:30} {x['gpu_pcie']['str']:30}")
+                   f"{_link_str(x['link']):20} {x['nic_pcie']['str']:30} {x['gpu_pcie']['str']:30}")
     known = [h for h in r["xgmi"]["links"] if h["known"]]
     if known:
         letter = {1: "U", 0: "D", -1: "X"}
@@ -84,8 +118,10 @@ def render(r: dict) -> str:
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser(prog="python -m network_operator_amd.agent.report", description=__doc__.split("\n\n")[0])
     ap.add_argument("--json", action="store_true", help="one JSON document instead of the table")
+    ap.add_argument("--min-link-speed-gbps", type=float, default=0,
+                    help="also name a rail whose link negotiated below this (the policy's minLinkSpeedGbps)")
     a = ap.parse_args(argv)
-    r = collect(os.environ.get("SYSFS_ROOT", "/sys/"))
+    r = collect(os.environ.get("SYSFS_ROOT", "/sys/"), a.min_link_speed_gbps)
     print(json.dumps(r, indent=1) if a.json else render(r))
     return 1 if r["problems"] else 0
 

@@ -351,7 +351,8 @@ def test_a_rail_without_an_rdma_device_is_named(native, tmp_path):
 def test_node_report_names_what_would_keep_the_label_off(tmp_path):
     """``python -m network_operator_amd.agent.report``: the agent's own readings of a node, read
     only.  A healthy fake node (GPUDirect RDMA via dma-buf) reports no problem and exits 0; a rail
-    trained at x8, an xGMI link down and a missing RDMA device are each named, exit 1."""
+    trained at x8, an xGMI link down and a missing RDMA device are each named, exit 1; so is a link
+    below ``--min-link-speed-gbps`` (a link that is down is not: the agent brings it up)."""
     import shutil
     import sys
 
@@ -359,8 +360,8 @@ def test_node_report_names_what_would_keep_the_label_off(tmp_path):
     fx = fakesysfs.build_mi355x_node(root, n_gpus=4)
     (root / "module" / "ib_uverbs").mkdir(parents=True)
 
-    def report():
-        r = subprocess.run([sys.executable, "-m", "network_operator_amd.agent.report", "--json"], capture_output=True,
+    def report(*args):
+        r = subprocess.run([sys.executable, "-m", "network_operator_amd.agent.report", "--json", *args], capture_output=True,
                            text=True, timeout=60, env=dict(os.environ, SYSFS_ROOT=str(root)))
         return r.returncode, json.loads(r.stdout)
 
@@ -368,6 +369,18 @@ def test_node_report_names_what_would_keep_the_label_off(tmp_path):
     assert rc == 0 and rep["problems"] == [] and len(rep["rails"]) == 4, rep
     assert rep["gpudirect_rdma"] == "dmabuf" and rep["xgmi"]["pairs"] == "6/6"
     rail0 = rep["rails"][0]
+    assert rail0["link"] == {"operstate": "unknown", "speed_gbps": None, "mtu": None}
+    net = root / "class" / "net"
+    for i, x in enumerate(rep["rails"]):  # as a host shows them: rail 1 negotiated 200G, rail 2 has no carrier
+        (net / x["nic"] / "operstate").write_text("down\n" if i == 2 else "up\n")
+        (net / x["nic"] / "speed").write_text("-1\n" if i == 2 else ("200000\n" if i == 1 else "400000\n"))
+        (net / x["nic"] / "mtu").write_text("9000\n")
+    rc, rep = report()
+    assert rc == 0 and rep["rails"][0]["link"] == {"operstate": "up", "speed_gbps": 400, "mtu": 9000}
+    assert rep["rails"][2]["link"]["speed_gbps"] is None
+    rc, rep = report("--min-link-speed-gbps", "400")
+    assert rc == 1 and rep["problems"] == [f"{rep['rails'][1]['nic']}: link negotiated 200 Gb/s, below the required 400"]
+    (net / rep["rails"][1]["nic"] / "speed").write_text("400000\n")
     fakesysfs.set_pcie_link(root, fakesysfs.nic_pci_dir(root, rail0["nic"]).name, 16.0, 8)
     fakesysfs.set_xgmi_link(root, fx["gpus"][1]["bdf"], 2, False)
     victim = next(n for n in fx["nics"] if n["ifname"] == rep["rails"][3]["nic"])
