@@ -28,10 +28,13 @@ from typing import List
 from . import native
 
 
-def _netdev(root: str, ifname: str) -> dict:
-    """The rail's Ethernet link from /sys/class/net/<ifname>: what ``ip link`` and ethtool show.
+def _netdev(root: str, bdf: str, ifname: str) -> dict:
+    """The rail's Ethernet link as ``ip link`` and ethtool show it, read under its PCI function
+    (a container in its own network namespace has no /sys/class/net entry for the host's NICs).
     The kernel reports speed -1 (or refuses the read) while there is no carrier."""
-    d = os.path.join(root, "class", "net", ifname)
+    d = os.path.join(root, "bus", "pci", "devices", bdf, "net", ifname)
+    if not bdf or not os.path.isdir(d):
+        d = os.path.join(root, "class", "net", ifname)
 
     def attr(name: str) -> str:
         try:
@@ -65,7 +68,7 @@ def collect(root: str, min_link_speed_gbps: float = 0) -> dict:
         nic = nics.get(p["nic"], {})
         rails.append({"gpu": p["gpu"], "nic": p["nic"], "path": p["path"], "driver": nic.get("driver", ""),
                       "rdma_dev": nic.get("rdma_dev", ""), "nic_pcie": n.read_pcie_link(root, nic.get("bdf", "")),
-                      "gpu_pcie": n.read_pcie_link(root, p["gpu"]), "link": _netdev(root, p["nic"])})
+                      "gpu_pcie": n.read_pcie_link(root, p["gpu"]), "link": _netdev(root, nic.get("bdf", ""), p["nic"])})
     x = n.read_xgmi(root)
     health = n.read_xgmi_health(root, [g["bdf"] for g in d["gpus"]])
     gdr = n.detect_gdr(root, platform.release())

@@ -284,6 +284,7 @@ def test_node_report_on_this_node():
     assert sorted((x["gpu"], x["nic"]) for x in rep["rails"]) == sorted((p["gpu"], p["nic"]) for p in want["pairs"])
     assert all(h["known"] for h in rep["xgmi"]["links"]), rep["xgmi"]
     assert rep["gpudirect_rdma"] != "none", rep
+    assert all(x["link"]["operstate"] != "unknown" for x in rep["rails"]), rep["rails"]  # read under the PCI function
     assert (r.returncode == 1) == bool(rep["problems"])
     out = Path(os.environ.get("GRAFT_REPO_ROOT", ".")) / "gpurun_out"
     if out.is_dir():
