@@ -29,19 +29,43 @@ int main(int argc, char** argv) {
     if (all_drivers) opt.nic_drivers.clear();
     auto d = topo::discover(opt, root);
     auto x = topo::read_xgmi(root);
+    std::vector<std::string> bdfs;
+    for (auto& g : d.gpus) bdfs.push_back(g.pci.bdf);
+    auto health = topo::read_xgmi_health(root, bdfs);
 
     artifacts::Json j;
+    auto pcie = [&](const std::string& bdf) {
+        auto l = topo::read_pcie_link(root, bdf);
+        j.begin_object().key("known").value(l.known()).key("degraded").value(l.degraded()).key("str").value(l.str());
+        j.end_object();
+    };
     j.begin_object();
     j.key("gpus").begin_array();
-    for (auto& g : d.gpus) {
+    for (size_t i = 0; i < d.gpus.size(); ++i) {
+        const auto& g = d.gpus[i];
         j.begin_object().key("index").value(g.index).key("bdf").value(g.pci.bdf).key("device").value(strfmt("0x%04x", g.pci.device));
-        j.key("numa").value(g.pci.numa).key("driver").value(g.pci.driver).end_object();
+        j.key("numa").value(g.pci.numa).key("driver").value(g.pci.driver);
+        j.key("pcie");
+        pcie(g.pci.bdf);
+        const auto& h = health[i];  // xGMI links as trained: "U" up, "D" down, "X" no link in the slot
+        j.key("xgmi_links").begin_object().key("known").value(h.known);
+        if (h.known) {
+            std::string st;
+            for (int v : h.status) st += v == 1 ? 'U' : v == 0 ? 'D' : 'X';
+            j.key("revision").value(h.revision).key("status").value(st).key("up").value(h.links_up());
+            j.key("down").value(h.links_down()).key("width").value(h.width).key("speed_gbps").value(h.speed_gbps);
+        } else {
+            j.key("error").value(h.error);
+        }
+        j.end_object().end_object();
     }
     j.end_array();
     j.key("nics").begin_array();
     for (auto& n : d.nics) {
         j.begin_object().key("ifname").value(n.ifname).key("bdf").value(n.pci.bdf).key("driver").value(n.pci.driver);
-        j.key("numa").value(n.pci.numa).key("rdma_dev").value(n.rdma_dev).key("mac").value(n.mac.str()).end_object();
+        j.key("numa").value(n.pci.numa).key("rdma_dev").value(n.rdma_dev).key("mac").value(n.mac.str()).key("pcie");
+        pcie(n.pci.bdf);
+        j.end_object();
     }
     j.end_array();
     j.key("pairs").begin_array();

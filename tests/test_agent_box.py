@@ -292,3 +292,24 @@ def test_node_report_on_this_node():
         (out / "node_report_box.txt").write_text(subprocess.run(
             [sys.executable, "-m", "network_operator_amd.agent.report"], capture_output=True, text=True,
             timeout=60).stdout)
+
+
+@pytest.mark.gpu
+def test_topo_tool_on_this_node():
+    """``netop-topo`` (the agent image's look at a node): on the box, every GPU's xGMI links and
+    PCIe link read, agreeing with the report's readings (Python binding, same sysfs)."""
+    r = subprocess.run([str(native_bin("netop-topo"))], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr[-2000:]
+    j = json.loads(r.stdout)
+    root = os.environ.get("SYSFS_ROOT", "/sys/")
+    health = {h["bdf"]: h for h in native().read_xgmi_health(root, [g["bdf"] for g in j["gpus"]])}
+    assert j["gpus"]
+    for g in j["gpus"]:
+        h, x = health[g["bdf"]], g["xgmi_links"]
+        assert x["known"] == h["known"], (g, h)
+        if x["known"]:
+            assert x["up"] == sum(s == 1 for s in h["status"]) and x["width"] == h["width"], (g, h)
+        assert g["pcie"]["known"], g  # amdgpu functions carry current_link_* on every box seen
+    out = Path(os.environ.get("GRAFT_REPO_ROOT", ".")) / "gpurun_out"
+    if out.is_dir():
+        (out / "netop_topo_box.json").write_text(json.dumps(j, indent=1))

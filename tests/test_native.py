@@ -146,11 +146,24 @@ def test_rdma_discovery_on_the_mi355x_node_leaves_the_eight_rails_to_amd_so(nati
 
 
 def test_topo_tool_json(tmp_path):
-    fakesysfs.build_mi355x_node(tmp_path, drop_xgmi_pairs=[(1, 2)])
+    """``netop-topo`` (in the agent image, which has no Python): the node's topology, and each
+    GPU's and NIC's PCIe link and each GPU's xGMI links as trained."""
+    fx = fakesysfs.build_mi355x_node(tmp_path, drop_xgmi_pairs=[(1, 2)])
+    gpu1 = sorted(g["bdf"] for g in fx["gpus"])[1]
+    fakesysfs.set_xgmi_link(tmp_path, gpu1, 2, False)
+    fakesysfs.set_pcie_link(tmp_path, gpu1, 32.0, 8)
     out = subprocess.run([str(native_bin("netop-topo")), f"--sysfs-root={tmp_path}"], capture_output=True, text=True,
                          check=True).stdout
     j = json.loads(out)
     assert len(j["gpus"]) == 8 and len(j["pairs"]) == 8
+    links = {g["bdf"]: g["xgmi_links"] for g in j["gpus"]}
+    assert links[gpu1]["status"] == "XUDUUUUU" and links[gpu1]["down"] == 1 and links[gpu1]["up"] == 6, links[gpu1]
+    assert all(v["known"] and v["revision"] == "1.8" and v["width"] == 16 for v in links.values())
+    assert sum(v["down"] for v in links.values()) == 1
+    pcie = {g["bdf"]: g["pcie"] for g in j["gpus"]}
+    assert pcie[gpu1] == {"known": True, "degraded": True, "str": "32.0 GT/s x8 of 32.0 GT/s x16"}
+    assert all(n["pcie"]["known"] and not n["pcie"]["degraded"] for n in j["nics"] if n["ifname"] in
+               {p["nic"] for p in j["pairs"]})
     assert j["xgmi"]["pairs_connected"] == 27 and not j["xgmi"]["full_mesh"]
     # What a host-nic policy would take from sysfs: the two host NICs; the rails are amd-so's.
     assert sorted(j["host_nics"]["ifnames"]) == ["ens49np1", "ens9np0"]
