@@ -149,6 +149,24 @@ def rccl_links_check(gpus: int, dump: str, art_env: dict, scratch: str, timeout:
                   if base else None)
 
 
+def rail_pcie_check(topo, sysfs_root: str) -> Optional[dict]:
+    """Each rail's PCIe links as trained, judged as the agent's --require-full-pcie judges them:
+    the NIC at the speed and width both ends support, the GPU at full width (its speed drops while
+    idle).  A rail at x8 or Gen4 moves RDMA at half rate whatever the busbw test saw.  None on a
+    node without rails."""
+    from .agent import native
+
+    n = native()
+    bdf = {nic["ifname"]: nic["bdf"] for nic in n.discover(sysfs_root)["nics"]}
+    rails, slow = {}, []
+    for pr in topo.pairs:
+        nl, gl = n.read_pcie_link(sysfs_root, bdf.get(pr.nic, "")), n.read_pcie_link(sysfs_root, pr.gpu_bdf)
+        rails[pr.nic] = {"nic": nl["str"], "gpu": gl["str"]}
+        if nl["degraded"] or (gl["known"] and gl["width"] < gl["max_width"]):
+            slow.append(pr.nic)
+    return _check("rail_pcie_links", not slow, degraded=slow, links=rails) if rails else None
+
+
 def run(gpus: int, min_busbw: float, min_link_GBps: float, max_bytes: int, sysfs_root: str = "/sys/",
         nfd_dir: Optional[str] = None, timeout: float = 600, artifact_dir: str = "/etc/amd/scale-out",
         tune_rccl: bool = False) -> dict:
@@ -178,6 +196,9 @@ def run(gpus: int, min_busbw: float, min_link_GBps: float, max_bytes: int, sysfs
                                  links_up=sum(st == 1 for h in known for st in h["status"]),
                                  down={b: v for b, v in down.items() if v},
                                  width=min(h["width"] for h in known), speed_gbps=min(h["speed_gbps"] for h in known)))
+        pcie = rail_pcie_check(topo, sysfs_root)
+        if pcie:
+            checks.append(pcie)
         tf = Path(artifact_dir) / "rccl-topo.xml"
         if tf.exists():
             agree = topo_file_agrees(tf.read_text(), topo)

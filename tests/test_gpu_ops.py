@@ -289,12 +289,14 @@ def test_fabric_validation_single_gpu(cuda_device, tmp_path):
     rep = validate.run(gpus=1, min_busbw=0, min_link_GBps=0, max_bytes=64 << 20, nfd_dir=str(tmp_path),
                        artifact_dir=str(art))
     assert rep["ok"], rep
-    names = [c["check"] for c in rep["checks"] if c["check"] != "xgmi_link_state"]
+    names = [c["check"] for c in rep["checks"] if c["check"] not in ("xgmi_link_state", "rail_pcie_links")]
     assert names[:6] == ["xgmi_topology", "gpu_nic_affinity", "rccl_topology_file", "xgmi_probe", "rccl_all_reduce",
                          "rccl_xgmi_links"]
     by = {c["check"]: c for c in rep["checks"]}
     # every GPU's links in gpu_metrics (the node's 8, though the job sees one): none down
     assert by["xgmi_link_state"]["ok"] and by["xgmi_link_state"]["links_up"] >= 7, by["xgmi_link_state"]
+    # every rail's NIC and GPU PCIe link at what it supports (both box families: 32 GT/s x16)
+    assert by["rail_pcie_links"]["ok"] and len(by["rail_pcie_links"]["links"]) == 8, by["rail_pcie_links"]
     assert by["rccl_all_reduce"]["artifacts_applied"] and by["rccl_all_reduce"]["rccl_env"]["NCCL_TOPO_FILE"]
     assert by["rccl_xgmi_links"]["rccl_dump"]["gpus"] == 1 and by["rccl_xgmi_links"]["rccl_dump"]["gpu_ancestry_equal"]
     assert names[-1] == "xgmi_direct_all_reduce"

@@ -319,3 +319,24 @@ def test_bench_measures_with_the_agents_file_and_reads_rccl_dump(tmp_path):
     (ROOT / "gpurun_out").mkdir(exist_ok=True)
     (ROOT / "gpurun_out" / "bench_artifacts_n1.json").write_text(json.dumps(
         {"agent_artifacts": a, "rccl_defaults": j["rccl_defaults"], "ms_per_step": j["ms_per_step"]}, indent=1))
+
+
+def test_validation_names_a_rail_whose_pcie_link_trained_low(tmp_path):
+    """validate.py's rail_pcie_links check: every rail at full PCIe passes; a NIC trained at Gen4,
+    or a GPU at x8, fails and is named; a GPU only slower (idle downshift) does not."""
+    from network_operator_amd import validate
+    from network_operator_amd.models.topology import NodeTopology
+
+    fx = fakesysfs.build_mi355x_node(tmp_path, n_gpus=4)
+    topo = NodeTopology.discover(str(tmp_path))
+    c = validate.rail_pcie_check(topo, str(tmp_path))
+    assert c["ok"] and len(c["links"]) == 4 and c["degraded"] == []
+    gpus = sorted(g["bdf"] for g in fx["gpus"])[:4]
+    fakesysfs.set_pcie_link(tmp_path, gpus[0], 16.0, 16)  # idle GPU: speed only
+    assert validate.rail_pcie_check(topo, str(tmp_path))["ok"]
+    fakesysfs.set_pcie_link(tmp_path, gpus[1], 32.0, 8)
+    nic = topo.nic_for_gpu(gpus[2])
+    fakesysfs.set_pcie_link(tmp_path, fakesysfs.nic_pci_dir(tmp_path, nic).name, 16.0, 16)
+    c = validate.rail_pcie_check(topo, str(tmp_path))
+    assert not c["ok"] and sorted(c["degraded"]) == sorted([topo.nic_for_gpu(gpus[1]), nic]), c
+    assert c["links"][nic]["nic"] == "16.0 GT/s x16 of 32.0 GT/s x16"
