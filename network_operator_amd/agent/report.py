@@ -2,7 +2,9 @@
 agent checks before it labels a node: each GPU's scale-out rail (the NIC behind its PCIe switch,
 the NIC's driver and RDMA device), both ends' PCIe links as trained, the xGMI mesh (KFD) and
 every xGMI link's state (gpu_metrics), GPUDirect RDMA, and each rail's Ethernet link as the kernel
-has it now (state, negotiated speed, MTU).
+has it now (state, negotiated speed, MTU).  When the agent has written its RCCL topology file
+(``--artifact-dir``, default /etc/amd/scale-out), the report also checks that the file places each
+GPU and its NIC as this node's PCIe tree does.
 
     python -m network_operator_amd.agent.report            # a table
     python -m network_operator_amd.agent.report --json     # the same as one JSON document
@@ -59,7 +61,7 @@ def _link_str(link: dict) -> str:
     return out
 
 
-def collect(root: str, min_link_speed_gbps: float = 0) -> dict:
+def collect(root: str, min_link_speed_gbps: float = 0, artifact_dir: str = "") -> dict:
     n = native()
     d = n.discover(root)
     nics = {x["ifname"]: x for x in d["nics"]}
@@ -92,9 +94,22 @@ def collect(root: str, min_link_speed_gbps: float = 0) -> dict:
             problems.append(f"GPU {h['bdf']}: xGMI link(s) {', '.join(map(str, down))} down")
     if gdr["mode"] == "none":
         problems.append("GPUDirect RDMA unavailable (no amdkfd peer-memory client, no RDMA dma-buf)")
+    topo_file = None
+    tf = os.path.join(artifact_dir, "rccl-topo.xml") if artifact_dir else ""
+    if tf and os.path.isfile(tf):
+        from ..models.topology import NodeTopology
+        from ..validate import topo_file_agrees
+
+        with open(tf) as f:
+            topo_file = dict(topo_file_agrees(f.read(), NodeTopology.discover(root, with_xgmi=False)), path=tf)
+        if topo_file["gpus_missing"]:
+            problems.append(f"{tf}: GPU(s) {', '.join(topo_file['gpus_missing'])} missing (a stale file?)")
+        for gpu, nic in topo_file["pairs_split"]:
+            problems.append(f"{tf}: places {nic} under another switch than GPU {gpu} (a stale file?)")
     return {"sysfs_root": root, "gpus": len(d["gpus"]), "rails": rails,
             "xgmi": {"pairs": f"{x['pairs_connected']}/{x['pairs_expected']}", "links": health},
             "gpudirect_rdma": gdr["mode"], "kernel": gdr["kernel"], "left_alone": d.get("excluded", {}),
+            "rccl_topology_file": topo_file,
             "problems": problems}
 
 
@@ -113,6 +128,9 @@ def render(r: dict) -> str:
             out.append(f"  {h['bdf']}  {''.join(letter[s] for s in h['status'])}  x{h['width']} at {h['speed_gbps']} Gb/s")
     elif r["xgmi"]["links"]:
         out += ["", "xGMI link state not read: " + r["xgmi"]["links"][0]["error"]]
+    if r.get("rccl_topology_file"):
+        t = r["rccl_topology_file"]
+        out += ["", f"RCCL topology file {t['path']}: " + ("matches this node" if t["ok"] else "does not match this node")]
     out += ["", "Problems:" if r["problems"] else "No problems found."]
     out += [f"  - {p}" for p in r["problems"]]
     return "\n".join(out)
@@ -123,8 +141,10 @@ def main(argv=None) -> int:
     ap.add_argument("--json", action="store_true", help="one JSON document instead of the table")
     ap.add_argument("--min-link-speed-gbps", type=float, default=0,
                     help="also name a rail whose link negotiated below this (the policy's minLinkSpeedGbps)")
+    ap.add_argument("--artifact-dir", default="/etc/amd/scale-out",
+                    help="where the agent writes rccl-topo.xml (checked against this node when present)")
     a = ap.parse_args(argv)
-    r = collect(os.environ.get("SYSFS_ROOT", "/sys/"), a.min_link_speed_gbps)
+    r = collect(os.environ.get("SYSFS_ROOT", "/sys/"), a.min_link_speed_gbps, a.artifact_dir)
     print(json.dumps(r, indent=1) if a.json else render(r))
     return 1 if r["problems"] else 0
 

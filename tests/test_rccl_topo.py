@@ -340,3 +340,29 @@ def test_validation_names_a_rail_whose_pcie_link_trained_low(tmp_path):
     c = validate.rail_pcie_check(topo, str(tmp_path))
     assert not c["ok"] and sorted(c["degraded"]) == sorted([topo.nic_for_gpu(gpus[1]), nic]), c
     assert c["links"][nic]["nic"] == "16.0 GT/s x16 of 32.0 GT/s x16"
+
+
+def test_node_report_checks_the_agents_rccl_topology_file(tmp_path):
+    """The node report checks the agent's rccl-topo.xml (``--artifact-dir``) against the node: the
+    golden file matches the fixture node; a file that puts a rail NIC under another GPU's switch
+    is named as a problem (exit 1)."""
+    root, art = tmp_path / "sys", tmp_path / "scale-out"
+    fakesysfs.build_mi355x_node(root)
+    (root / "module" / "ib_uverbs").mkdir(parents=True)
+    art.mkdir()
+
+    def report():
+        r = subprocess.run([sys.executable, "-m", "network_operator_amd.agent.report", "--json", f"--artifact-dir={art}"],
+                           capture_output=True, text=True, timeout=60, env=dict(os.environ, SYSFS_ROOT=str(root)))
+        return r.returncode, json.loads(r.stdout)
+
+    rc, rep = report()
+    assert rep["rccl_topology_file"] is None  # the agent has not run here
+    good = GOLDEN.read_text()
+    (art / "rccl-topo.xml").write_text(good)
+    rc, rep = report()
+    assert rep["rccl_topology_file"]["ok"] and not [p for p in rep["problems"] if "rccl-topo" in p], rep
+    (art / "rccl-topo.xml").write_text(good.replace('<net name="mlx5_1" port="1"/>', '<net name="tmp" port="1"/>').replace(
+        '<net name="mlx5_3" port="1"/>', '<net name="mlx5_1" port="1"/>'))
+    rc, rep = report()
+    assert rc == 1 and len([p for p in rep["problems"] if "rccl-topo.xml: places" in p]) == 2, rep["problems"]
