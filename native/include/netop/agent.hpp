@@ -30,6 +30,7 @@
 
 #include "netop/arp.hpp"
 #include "netop/artifacts.hpp"
+#include "netop/bounded.hpp"
 #include "netop/ethtool.hpp"
 #include "netop/httpd.hpp"
 #include "netop/l3.hpp"
@@ -86,6 +87,19 @@ struct Config {
     // slot support, and its GPU's at full width (a GPU may lower its link speed when idle).
     bool require_full_pcie = false;
     int64_t xgmi_health_interval_ns = 5LL * 1000000000;
+    // Bound on each sysfs read that firmware or hardware answers (gpu_metrics: an SMU query per
+    // GPU; PCIe link state; the KFD topology): a read that has not returned by then is reported
+    // ("gpu_metrics of <bdf> did not answer in 5s") and the label follows the policy, instead of the
+    // start or the monitor hanging behind it (netop/bounded.hpp).
+    int64_t sysfs_read_timeout_ns = 5LL * 1000000000;
+    // Flap dampening: after the monitor withdrew the label, it is republished only once the node
+    // has been healthy for this long without a break (a flapping optic or a GPU reset would
+    // otherwise toggle the node's scheduling eligibility as fast as the link flaps).  The first
+    // publication is not delayed.  0 = republish at once.
+    int64_t label_holddown_ns = 10LL * 1000000000;
+    // The monitor counts an xGMI link as down only after this many consecutive gpu_metrics samples
+    // saw it down (a transient status during a GPU reset is not a flap); the start needs one.
+    int xgmi_down_samples = 2;
     int64_t link_wait_ns = 3LL * 1000000000;  // netlink echo wait (network.go:251)
     // L2: how long a NIC that is admin-up may train its link before it counts as "no carrier".
     // Separate from the 3 s echo wait: 200/400G optics with FEC and link training commonly take
@@ -115,6 +129,16 @@ struct Config {
     // GPUDirect RDMA: "" = report only; "any" = require peer-memory or dma-buf; "peermem" /
     // "dmabuf" = require that mechanism.  Checked before LLDP, like the xGMI mesh.
     std::string require_gdr;
+    // Every scale-out NIC must have an RDMA device before the readiness label: a RoCE NIC whose
+    // RDMA driver is not loaded leaves RCCL only TCP sockets on that rail.  (The reference labels
+    // after configuring the RDMA NICs HCCL uses, cmd/discover/main.go:212-246; Gaudi's integrated
+    // NICs are RDMA by construction.)  The NICs are configured either way; the label and rccl.env
+    // wait, the probe says "waiting for RDMA device", and the monitor publishes the label once the
+    // devices appear (a driver container loading the module).  Past rdma_wait_ns from the start the
+    // reason turns into the fault "no RDMA device (load its RDMA driver)".  Off: a warning only.
+    bool require_rdma = false;
+    int64_t rdma_wait_ns = 300LL * 1000000000;
+    int64_t rdma_poll_ns = 250LL * 1000000;  // how often the waiting agent looks for the devices
     bool disable_fw_lldp = false;
     // With disable_fw_lldp, on a NIC without a firmware-LLDP private flag whose DCBX an embedded
     // agent runs (mlx5_core in firmware mode): hand DCBX to the host.  Opt-in: the firmware then
@@ -346,8 +370,11 @@ class Agent {
     void check_xgmi();     // dry run: join the prefetched KFD topology and gpu_metrics now
     void join_xgmi();      // the prefetched KFD topology, evaluated (right after link-up)
     void evaluate_xgmi();  // the mesh check
-    std::future<topo::XgmiReport> xgmi_future_;
-    std::future<void> prefetch_;  // the reader thread (start_prefetch); its futures are below
+    // start_prefetch(): each read on its own detached thread (netop/bounded.hpp), all joined by
+    // prefetch_deadline_ at the latest (a late KFD read fails the start, a late PCIe read leaves the
+    // links unknown, a late gpu_metrics read names the GPU).
+    bounded::Call<topo::XgmiReport> xgmi_call_;
+    int64_t prefetch_deadline_ = 0;
     void start_prefetch();
     void log_results();
     void mark(const std::string& phase);
@@ -435,21 +462,46 @@ class Agent {
     topo::XgmiReport xgmi_;
     std::vector<topo::XgmiLinkHealth> xgmi_health_;
     std::string xgmi_error_;  // what the last gpu_metrics read found wrong (empty: fine or not read)
-    void read_xgmi_health();
-    std::string xgmi_health_problem() const;
+    // `min_down`: consecutive samples a link must have been seen down (xgmi_down_streak_).
+    std::string xgmi_health_problem(int min_down = 1) const;
+    void note_xgmi_sample();  // updates xgmi_down_streak_ from xgmi_health_
+    std::map<std::string, std::vector<int>> xgmi_down_streak_;  // per GPU BDF, per link slot
     // The start's gpu_metrics read (start_prefetch; an SMU query per GPU): joined by
     // finish_xgmi_health() before the label decision.
-    std::future<std::vector<topo::XgmiLinkHealth>> xgmi_health_future_;
+    bounded::Call<std::vector<topo::XgmiLinkHealth>> xgmi_health_call_;
     void finish_xgmi_health();
     std::vector<std::string> xgmi_health_bdfs() const;
     std::string check_pcie(NicState& n);  // "" when fine or not required
     // The NICs' and their GPUs' PCIe links (start_prefetch), joined by ensure_pcie() at first use.
-    std::future<std::vector<std::pair<topo::PcieLink, topo::PcieLink>>> pcie_future_;
+    bounded::Call<std::vector<std::pair<topo::PcieLink, topo::PcieLink>>> pcie_call_;
+    bool pcie_joined_ = false;
+    bool pcie_late_ = false;  // the start's PCIe link read did not answer in time
     void ensure_pcie();
+    // Monitor: the periodic gpu_metrics / PCIe reads, on a worker (results through an eventfd).
+    struct HealthSample {
+        std::vector<topo::XgmiLinkHealth> xgmi;
+        std::vector<std::pair<topo::PcieLink, topo::PcieLink>> pcie;  // per NIC (nics_ order)
+        std::vector<bool> pcie_late;  // per NIC: its read had not returned by the deadline
+        bool xgmi_read = false, pcie_read = false;
+    };
+    // Applies a sample; true when the node's health changed.
+    bool apply_health(const HealthSample& s);
+    // Label hold-down (Config::label_holddown_ns): when the node last turned healthy after a
+    // withdrawal (0 = not holding), how often a recovery was cut short by another flap, and the
+    // withdrawals.
+    int64_t holddown_until_ = 0;
+    int label_suppressed_ = 0;
+    int label_withdrawals_ = 0;
     // GPU rails whose NIC has no RDMA device (its RDMA driver is not loaded): RCCL could only use
     // them over TCP sockets.  Reported always; fatal with --require-gdr.
     std::vector<std::string> no_rdma_;
     void check_rdma();
+    // --require-rdma: the configured NICs still without an RDMA device (empty when not required).
+    std::vector<std::string> rdma_missing() const;
+    // Looks again for the RDMA device of every NIC without one; true when one appeared (the
+    // topology file, which names the HCAs, is then generated again).
+    bool refresh_rdma();
+    std::string rdma_reason() const;  // the probe's per-NIC reason while a device is missing
     topo::GdrReport gdr_;
     void check_gdr();
     std::map<std::string, std::string> status_node() const;

@@ -97,6 +97,10 @@ std::optional<PciDev> netdev_pci(const std::string& root, const std::string& ifn
 // The negotiated link speed in Mb/s (<root>/class/net/<if>/speed), or -1 when the driver does not
 // report one (link down, virtual NIC, no such file).
 int64_t netdev_speed_mbps(const std::string& root, const std::string& ifname);
+// The RDMA device of a netdev's PCI function (<root>/class/net/<ifname>/device/infiniband/*):
+// present once the NIC's RDMA driver (mlx5_ib, ionic_rdma, bnxt_re) has registered it.  "" when
+// there is none (yet).
+std::string netdev_rdma_device(const std::string& root, const std::string& ifname);
 // Devices stacked on a netdev (its sysfs upper_<name> links): the bond, bridge or team it is
 // enslaved to, VLANs and macvlans on it.  Sorted; empty when there are none or no sysfs entry.
 std::vector<std::string> netdev_uppers(const std::string& root, const std::string& ifname);
@@ -208,6 +212,7 @@ struct XgmiLinkHealth {
     std::string revision;          // "1.8"
     bool known = false;            // decoded (a known revision, not truncated)
     std::string error;             // why not
+    bool late = false;             // the read did not return in time (see the bounded overload)
     int width = 0;                 // lanes per link
     int speed_gbps = 0;            // per-lane rate (amd-smi's bit_rate)
     std::vector<int> status;       // per link slot: 1 up, 0 down, -1 no link in this slot
@@ -218,6 +223,11 @@ struct XgmiLinkHealth {
 XgmiLinkHealth parse_gpu_metrics(const std::string& blob);
 // One entry per BDF, from <root>/bus/pci/devices/<bdf>/gpu_metrics.
 std::vector<XgmiLinkHealth> read_xgmi_health(const std::string& root, const std::vector<std::string>& bdfs);
+// The same with the GPUs read concurrently (netop/bounded.hpp), for at most `timeout_ns`: a GPU
+// whose gpu_metrics has not answered by then (a wedged or resetting SMU) is reported `late`, and
+// its read is not started again until the one still blocked returns.
+std::vector<XgmiLinkHealth> read_xgmi_health(const std::string& root, const std::vector<std::string>& bdfs,
+                                             int64_t timeout_ns);
 
 // GPUDirect RDMA readiness: can the RoCE NICs DMA straight into MI355X HBM?  Without it RCCL
 // stages every inter-node transfer through host memory, costing bandwidth and latency.

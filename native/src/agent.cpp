@@ -201,80 +201,70 @@ void Agent::get_network_configs(const std::vector<std::string>& names) {
 }
 
 void Agent::start_prefetch() {
-    // What the start needs from sysfs beyond discovery, read by one thread beside link-up and the
-    // LLDP wait, in the order it is needed: the KFD topology (joined right after link-up), the
-    // rails' PCIe links (first NIC configured), the GPUs' gpu_metrics (before the label).  On the
-    // box these are ~1.1, ~0.5 and ~1.65 ms of reads (profiles/r5_box_read_costs.json).
+    // What the start needs from sysfs beyond discovery, read beside link-up and the LLDP wait,
+    // each on a thread of its own: the KFD topology (joined right after link-up), the rails' PCIe
+    // links (first NIC configured), the GPUs' gpu_metrics (before the label; one thread per GPU).
+    // On the box these are ~1.1, ~0.5 and ~1.65 ms of reads (profiles/r5_box_read_costs.json).
+    // Every join waits until prefetch_deadline_ at most (Config::sysfs_read_timeout_ns).
     std::vector<std::pair<std::string, std::string>> fns;  // (NIC name, its GPU's BDF)
     for (const auto& n : nics_) fns.emplace_back(n.ifname, n.gpu_bdf);
     std::vector<std::string> gpus;
     for (const auto& g : disc_.gpus) gpus.push_back(g.pci.bdf);
     const bool xgmi = cfg_.xgmi_expect_links >= 0;
-    auto p_xgmi = std::make_shared<std::promise<topo::XgmiReport>>();
-    auto p_pcie = std::make_shared<std::promise<std::vector<std::pair<topo::PcieLink, topo::PcieLink>>>>();
-    auto p_health = std::make_shared<std::promise<std::vector<topo::XgmiLinkHealth>>>();
-    xgmi_future_ = xgmi ? p_xgmi->get_future() : std::future<topo::XgmiReport>();
-    pcie_future_ = p_pcie->get_future();
-    xgmi_health_future_ = xgmi ? p_health->get_future() : std::future<std::vector<topo::XgmiLinkHealth>>();
+    const std::string root = cfg_.sysfs_root.empty() ? topo::sysfs_root() : cfg_.sysfs_root;
     const int main_cpu = ::sched_getcpu();
-    auto work = [root = cfg_.sysfs_root.empty() ? topo::sysfs_root() : cfg_.sysfs_root, fns, gpus, xgmi, main_cpu,
-                 p_xgmi, p_pcie, p_health](bool pin) {
-        if (pin) {  // off the agent thread's CPU, which brings the links up meanwhile
-            cpu_set_t set;
-            if (main_cpu >= 0 && ::sched_getaffinity(0, sizeof set, &set) == 0 && CPU_COUNT(&set) > 1) {
-                CPU_CLR(main_cpu, &set);
-                (void)::sched_setaffinity(0, sizeof set, &set);
-            }
-        }
-        try {
-            topo::XgmiReport x;
-            if (xgmi) {
-                x = topo::read_xgmi(root);
-                p_xgmi->set_value(x);
-            }
-            std::vector<std::pair<topo::PcieLink, topo::PcieLink>> links;
-            for (const auto& [ifname, gpu] : fns) {
-                topo::PcieLink nic, g;
-                if (auto d = topo::netdev_pci(root, ifname)) nic = topo::read_pcie_link(root, d->bdf);
-                if (!gpu.empty()) g = topo::read_pcie_link(root, gpu);
-                links.emplace_back(nic, g);
-            }
-            p_pcie->set_value(std::move(links));
-            if (xgmi) {
-                // The amdgpu PCI functions discovery found: KFD lists a GPU the container cannot
-                // open with its properties filtered (no BDF), while its PCI device (and
-                // gpu_metrics) is still readable.  Without discovered GPUs, KFD's own list.
-                std::vector<std::string> bdfs = gpus;
-                if (bdfs.empty())
-                    for (const auto& g : x.gpus)
-                        if (g.is_gpu()) bdfs.push_back(g.bdf());
-                p_health->set_value(topo::read_xgmi_health(root, bdfs));
-            }
-        } catch (...) {
-            // Every join must return: the failure goes to whichever results are still owed (the
-            // callable, and with it the promises, lives as long as the async state).
-            const auto e = std::current_exception();
-            auto owe = [&](auto& promise) {
-                try {
-                    promise->set_exception(e);
-                } catch (const std::future_error&) {  // already delivered
-                }
-            };
-            owe(p_xgmi);
-            owe(p_pcie);
-            owe(p_health);
+    auto off_main_cpu = [main_cpu] {  // the agent thread brings the links up meanwhile
+        cpu_set_t set;
+        if (main_cpu >= 0 && ::sched_getaffinity(0, sizeof set, &set) == 0 && CPU_COUNT(&set) > 1) {
+            CPU_CLR(main_cpu, &set);
+            (void)::sched_setaffinity(0, sizeof set, &set);
         }
     };
-    try {
-        prefetch_ = std::async(std::launch::async, work, true);
-    } catch (const std::system_error&) {  // no thread to spare: read everything now
-        work(false);
-    }
+    const int64_t timeout = cfg_.sysfs_read_timeout_ns;
+    prefetch_deadline_ = mono_ns() + timeout;
+    if (xgmi)
+        xgmi_call_ = bounded::Call<topo::XgmiReport>("", [root, off_main_cpu] {
+            off_main_cpu();
+            return topo::read_xgmi(root);
+        });
+    pcie_call_ = bounded::Call<std::vector<std::pair<topo::PcieLink, topo::PcieLink>>>("", [root, fns, off_main_cpu] {
+        off_main_cpu();
+        std::vector<std::pair<topo::PcieLink, topo::PcieLink>> links;
+        for (const auto& [ifname, gpu] : fns) {
+            topo::PcieLink nic, g;
+            if (auto d = topo::netdev_pci(root, ifname)) nic = topo::read_pcie_link(root, d->bdf);
+            if (!gpu.empty()) g = topo::read_pcie_link(root, gpu);
+            links.emplace_back(nic, g);
+        }
+        return links;
+    });
+    pcie_joined_ = false;
+    if (xgmi)
+        xgmi_health_call_ = bounded::Call<std::vector<topo::XgmiLinkHealth>>("", [root, gpus, timeout, off_main_cpu] {
+            off_main_cpu();
+            // The amdgpu PCI functions discovery found: KFD lists a GPU the container cannot
+            // open with its properties filtered (no BDF), while its PCI device (and gpu_metrics)
+            // is still readable.  Without discovered GPUs, KFD's own list.
+            std::vector<std::string> bdfs = gpus;
+            if (bdfs.empty())
+                for (const auto& g : topo::read_xgmi(root).gpus)
+                    if (g.is_gpu()) bdfs.push_back(g.bdf());
+            return topo::read_xgmi_health(root, bdfs, timeout);
+        });
 }
 
 void Agent::ensure_pcie() {
-    if (!pcie_future_.valid()) return;
-    auto links = pcie_future_.get();
+    if (pcie_joined_ || !pcie_call_.valid()) return;
+    pcie_joined_ = true;
+    auto got = pcie_call_.wait(prefetch_deadline_);
+    if (!got) {
+        pcie_late_ = true;
+        NLOG_W("The PCIe link state of the scale-out NICs did not answer in %s: not checked%s",
+               format_go_duration(cfg_.sysfs_read_timeout_ns).c_str(),
+               cfg_.require_full_pcie ? " (--require-full-pcie: the NICs wait for it)" : "");
+        return;
+    }
+    const auto& links = *got;
     for (size_t i = 0; i < links.size() && i < nics_.size(); ++i) {
         NicState& n = nics_[i];
         std::tie(n.pcie, n.gpu_pcie) = links[i];
@@ -417,8 +407,19 @@ void Agent::check_xgmi() {  // dry run: everything in line
 }
 
 void Agent::join_xgmi() {
-    if (!xgmi_future_.valid()) return;
-    xgmi_ = xgmi_future_.get();
+    if (!xgmi_call_.valid()) return;
+    auto x = xgmi_call_.wait(prefetch_deadline_);
+    xgmi_call_ = {};
+    if (!x) {
+        const std::string why = "the KFD topology (" + path_join(cfg_.sysfs_root.empty() ? topo::sysfs_root() : cfg_.sysfs_root,
+                                                                 "class/kfd") +
+                                ") did not answer in " + format_go_duration(cfg_.sysfs_read_timeout_ns);
+        if (!cfg_.dry_run) throw AgentError("xGMI: " + why);
+        NLOG_W("dry run: a real start would fail: xGMI: %s", why.c_str());
+        xgmi_error_ = why;
+        return;
+    }
+    xgmi_ = std::move(*x);
     evaluate_xgmi();
 }
 
@@ -447,16 +448,28 @@ std::vector<std::string> Agent::xgmi_health_bdfs() const {
     return bdfs;
 }
 
-void Agent::read_xgmi_health() {
-    std::string root = cfg_.sysfs_root.empty() ? topo::sysfs_root() : cfg_.sysfs_root;
-    xgmi_health_ = topo::read_xgmi_health(root, xgmi_health_bdfs());
-    xgmi_error_ = xgmi_health_problem();
-}
-
 void Agent::finish_xgmi_health() {
-    if (xgmi_health_future_.valid()) {
-        xgmi_health_ = xgmi_health_future_.get();
+    if (xgmi_health_call_.valid()) {
+        // The reader bounds each GPU's read itself; this deadline only covers the reader thread
+        // (and, without discovered GPUs, its KFD read) being late as a whole.
+        auto h = xgmi_health_call_.wait(prefetch_deadline_ + cfg_.sysfs_read_timeout_ns);
+        xgmi_health_call_ = {};
+        if (h) {
+            xgmi_health_ = std::move(*h);
+        } else {
+            xgmi_health_.clear();
+            for (const auto& bdf : xgmi_health_bdfs()) {
+                topo::XgmiLinkHealth l;
+                l.bdf = bdf;
+                l.late = true;
+                l.error = "gpu_metrics did not answer in " + format_go_duration(cfg_.sysfs_read_timeout_ns);
+                xgmi_health_.push_back(std::move(l));
+            }
+        }
+        note_xgmi_sample();
+        const std::string kfd_error = xgmi_error_;  // a late KFD read (dry run) stays reported
         xgmi_error_ = xgmi_health_problem();
+        if (!kfd_error.empty()) xgmi_error_ = xgmi_error_.empty() ? kfd_error : kfd_error + "; " + xgmi_error_;
     }
     int gpus = 0, up = 0;
     for (const auto& h : xgmi_health_) {  // one line on the critical path; the details at -v=1
@@ -485,13 +498,30 @@ void Agent::finish_xgmi_health() {
     throw AgentError("xGMI: " + xgmi_error_);
 }
 
-std::string Agent::xgmi_health_problem() const {
+void Agent::note_xgmi_sample() {
+    for (const auto& h : xgmi_health_) {
+        if (!h.known) continue;  // a late or unreadable sample says nothing about the links
+        auto& streak = xgmi_down_streak_[h.bdf];
+        streak.resize(h.status.size(), 0);
+        for (size_t i = 0; i < h.status.size(); ++i) streak[i] = h.status[i] == 0 ? streak[i] + 1 : 0;
+    }
+}
+
+std::string Agent::xgmi_health_problem(int min_down) const {
     std::vector<std::string> parts;
     for (const auto& h : xgmi_health_) {
+        if (h.late) {
+            parts.push_back(strfmt("gpu_metrics of %s did not answer in %s", h.bdf.c_str(),
+                                   format_go_duration(cfg_.sysfs_read_timeout_ns).c_str()));
+            continue;
+        }
         if (!h.known) continue;
+        auto streak = xgmi_down_streak_.find(h.bdf);
         std::vector<std::string> down;
         for (size_t i = 0; i < h.status.size(); ++i)
-            if (h.status[i] == 0) down.push_back(std::to_string(i));
+            if (h.status[i] == 0 && (streak == xgmi_down_streak_.end() || i >= streak->second.size() ||
+                                     streak->second[i] >= min_down))
+                down.push_back(std::to_string(i));
         if (!down.empty())
             parts.push_back(strfmt("GPU %s: link%s %s down", h.bdf.c_str(), down.size() > 1 ? "s" : "", join(down, ", ").c_str()));
         else if (cfg_.xgmi_min_link_width > 0 && h.links_up() > 0 && h.width < cfg_.xgmi_min_link_width)
@@ -512,11 +542,56 @@ void Agent::check_rdma() {
     const std::string why = "scale-out NIC(s) without an RDMA device: " + join(no_rdma_, ", ") +
                             " (RCCL could only use them over TCP sockets: load the NIC's RDMA driver, e.g. ionic_rdma, "
                             "mlx5_ib, bnxt_re)";
+    if (cfg_.require_rdma) {
+        // Not a crash loop: the NICs are configured, and the label follows the devices (a driver
+        // container loading the module while this agent runs).  See rdma_missing().
+        if (cfg_.dry_run)
+            NLOG_W("dry run: a real start would wait for RDMA devices on %zu rail%s: %s", no_rdma_.size(),
+                   no_rdma_.size() == 1 ? "" : "s", why.c_str());
+        else
+            NLOG_W("%s; the readiness label waits for them", why.c_str());
+        return;
+    }
     if (cfg_.require_gdr.empty() || cfg_.dry_run) {
         NLOG_W("%s%s", cfg_.require_gdr.empty() ? "" : "dry run: a real start would fail: ", why.c_str());
         return;
     }
     throw AgentError("GPUDirect RDMA required, but " + why);
+}
+
+std::vector<std::string> Agent::rdma_missing() const {
+    std::vector<std::string> out;
+    if (!cfg_.require_rdma) return out;
+    for (const auto& n : nics_)
+        if (n.rdma_dev.empty()) out.push_back(n.ifname);
+    return out;
+}
+
+std::string Agent::rdma_reason() const {
+    return mono_ns() - t0_ < cfg_.rdma_wait_ns ? "waiting for RDMA device" : "no RDMA device (load its RDMA driver)";
+}
+
+bool Agent::refresh_rdma() {
+    if (!cfg_.require_rdma) return false;
+    const std::string root = cfg_.sysfs_root.empty() ? topo::sysfs_root() : cfg_.sysfs_root;
+    bool found = false;
+    for (auto& n : nics_) {
+        if (!n.rdma_dev.empty()) continue;
+        std::string dev = topo::netdev_rdma_device(root, n.ifname);
+        if (dev.empty()) continue;
+        NLOG_I("Interface '%s': RDMA device %s appeared", n.ifname.c_str(), dev.c_str());
+        n.rdma_dev = dev;
+        n.gid_index.reset();
+        for (auto& d : disc_.nics)
+            if (d.ifname == n.ifname) d.rdma_dev = dev;
+        no_rdma_.erase(std::remove(no_rdma_.begin(), no_rdma_.end(), n.ifname), no_rdma_.end());
+        found = true;
+    }
+    if (found) {  // the topology file names each rail's HCA: generate it again
+        topo_future_ = std::future<TopoResult>();
+        topo_.reset();
+    }
+    return found;
 }
 
 void Agent::check_gdr() {
@@ -808,9 +883,17 @@ void Agent::run(int stop_fd) {
     if (cfg_.xgmi_expect_links >= 0)
         labels_extra_["amd.feature.node.kubernetes.io/gpu-xgmi.pairs"] = std::to_string(xgmi_.pairs_connected);
     if (!gdr_.kernel.empty()) labels_extra_[cfg_.labels.key + ".gdr"] = gdr_.mode();
-    const bool linked = xgmi_error_.empty() &&
+    refresh_rdma();  // a driver loaded during the bring-up
+    const std::vector<std::string> no_rdma = rdma_missing();
+    const bool linked = xgmi_error_.empty() && no_rdma.empty() &&
                         (cfg_.mode != "L2" ||
                          std::all_of(nics_.begin(), nics_.end(), [](const NicState& n) { return n.configured; }));
+    if (!linked && !no_rdma.empty() && !cfg_.monitor) {
+        // Nothing would look for the devices again: fail, named, and let the restart look.
+        write_status();
+        throw AgentError("No RDMA device on " + join(no_rdma, ", ") + " (load the NIC's RDMA driver, e.g. ionic_rdma, "
+                         "mlx5_ib, bnxt_re): RCCL could only use these rails over TCP sockets");
+    }
     if (!linked) {
         // With the monitor: stay up unlabelled; the carrier on the last dark NIC (L2, at the
         // required speed) or the xGMI link coming back publishes the label (monitor()).

@@ -255,6 +255,12 @@ std::vector<std::string> Agent::socket_ifnames() const {
 void Agent::write_rccl_env_file() {
     const std::string topo_env = write_topo();
     if (cfg_.rccl_env.empty()) return;
+    if (!cfg_.dry_run && !rdma_missing().empty()) {
+        // --require-rdma: no rccl.env that leaves a rail to TCP sockets.  One from an earlier run
+        // named HCAs that are gone now: it goes too (written again once the devices are back).
+        if (::unlink(cfg_.rccl_env.c_str()) == 0) NLOG_I("Removed %s until every rail has its RDMA device", cfg_.rccl_env.c_str());
+        return;
+    }
     try {
         artifacts::write_rccl_env(cfg_.rccl_env, nics_, topo_env, rccl_env_extra_, socket_ifnames(), cfg_.mode != "L3");
     } catch (const std::exception& e) {

@@ -413,6 +413,9 @@ std::string Agent::silent_summary() const {
 std::string Agent::check_pcie(NicState& n) {
     ensure_pcie();
     if (!cfg_.require_full_pcie) return "";
+    if (pcie_late_ && !n.pcie.known())
+        return "its PCIe link state did not answer in " + format_go_duration(cfg_.sysfs_read_timeout_ns) +
+               " (a function in error recovery?)";
     if (n.pcie.degraded())
         return strfmt("its PCIe link trained at %s: RDMA moves at a fraction of the rail's rate (reseat the card, check the "
                       "riser and the slot's BIOS link setting)", n.pcie.str().c_str());

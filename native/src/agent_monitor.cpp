@@ -6,6 +6,7 @@
 #include <linux/if.h>
 #include <linux/rtnetlink.h>
 #include <sys/epoll.h>
+#include <sys/eventfd.h>
 #include <sys/socket.h>
 #include <unistd.h>
 
@@ -98,8 +99,77 @@ bool Agent::nic_healthy(const NicState& n) const {
     if (!n.link.up() || n.degraded || n.cache_stale || n.no_carrier || !n.config_error.empty() || !n.pcie_error.empty())
         return false;
     if (cfg_.mode == "L3" && cfg_.verify_peers_ns > 0 && !n.peer_verified) return false;
+    if (cfg_.require_rdma && n.rdma_dev.empty()) return false;
     return cfg_.mode != "L3" || n.configured;
 }
+
+bool Agent::apply_health(const HealthSample& s) {
+    bool changed = false;
+    if (s.xgmi_read) {
+        const std::string before = xgmi_error_;
+        xgmi_health_ = s.xgmi;
+        note_xgmi_sample();
+        // A link counts as down only after xgmi_down_samples samples in a row (a status read in
+        // the middle of a GPU reset is not a flap); a GPU that did not answer counts at once.
+        xgmi_error_ = xgmi_health_problem(std::max(1, cfg_.xgmi_down_samples));
+        if (xgmi_error_ != before) {
+            if (xgmi_error_.empty())
+                NLOG_I("xGMI links healthy again");
+            else
+                NLOG_W("xGMI: %s", xgmi_error_.c_str());
+            changed = true;
+        }
+    }
+    if (s.pcie_read) {
+        const std::string late = "its PCIe link state did not answer in " + format_go_duration(cfg_.sysfs_read_timeout_ns);
+        for (size_t i = 0; i < nics_.size() && i < s.pcie.size(); ++i) {
+            NicState& n = nics_[i];
+            // What kept an unconfigured NIC back at start, with the reading it was refused on.
+            const std::string was = n.configured ? n.pcie_error : check_pcie(n);
+            std::tie(n.pcie, n.gpu_pcie) = s.pcie[i];
+            const std::string why = s.pcie_late[i] ? late : check_pcie(n);
+            if (!n.configured) {
+                // Left unconfigured only for its PCIe link: configured once the link
+                // retrains at full speed and width, instead of waiting for a restart that, with the
+                // monitor on, never comes.
+                if (was.empty() || n.config_error != was || why == was) continue;
+                changed = true;
+                if (!why.empty()) {
+                    n.config_error = why;
+                    continue;
+                }
+                NLOG_I("Interface '%s': PCIe link now at %s: configuring it", n.ifname.c_str(), n.pcie.str().c_str());
+                if (cfg_.mode == "L2") {
+                    n.configured = l2_link_ok(n);
+                } else if (n.addr) {
+                    n.config_error.clear();
+                    configure_interface(n);
+                }
+                continue;
+            }
+            if (why == n.pcie_error) continue;
+            if (why.empty())
+                NLOG_I("Interface '%s': PCIe link back at %s", n.ifname.c_str(), n.pcie.str().c_str());
+            else
+                NLOG_W("Interface '%s': %s", n.ifname.c_str(), why.c_str());
+            n.pcie_error = why;
+            changed = true;
+        }
+    }
+    return changed;
+}
+
+namespace {
+// An eventfd the health worker signals through; shared with the worker so that a worker finishing
+// after the monitor has returned never writes to a closed (or reused) descriptor.
+struct SharedFd {
+    int fd;
+    explicit SharedFd(int f) : fd(f) {}
+    ~SharedFd() {
+        if (fd >= 0) ::close(fd);
+    }
+};
+}  // namespace
 
 void Agent::monitor(int stop_fd) {
     std::unique_ptr<nl::LinkWatcher> watcher;
@@ -115,22 +185,27 @@ void Agent::monitor(int stop_fd) {
     for (auto& n : nics_) carrier[n.link.index] = n.link.lower_up();
     int64_t next_tx = mono_ns() + cfg_.lldp_tx_interval_ns;
     int64_t next_verify = 0;
-    // The GPUs' xGMI links (gpu_metrics): only when the xGMI check runs and the layout is known.
+    // The GPUs' xGMI links (gpu_metrics): only when the xGMI check runs and the layout is known
+    // (or the start's read did not answer: it is asked again).
     const bool xgmi_watch = cfg_.xgmi_expect_links >= 0 && cfg_.xgmi_health_interval_ns > 0 &&
-                            std::any_of(xgmi_health_.begin(), xgmi_health_.end(), [](const topo::XgmiLinkHealth& h) { return h.known; });
-    int64_t next_xgmi = mono_ns() + cfg_.xgmi_health_interval_ns;
-    int64_t next_pcie = next_xgmi;
+                            std::any_of(xgmi_health_.begin(), xgmi_health_.end(),
+                                        [](const topo::XgmiLinkHealth& h) { return h.known || h.late; });
+    const bool pcie_watch = cfg_.require_full_pcie && cfg_.xgmi_health_interval_ns > 0;
+    int64_t next_health = mono_ns() + cfg_.xgmi_health_interval_ns;
+    // Those reads (an SMU query per GPU, PCIe config space) run on a worker thread, never on this
+    // loop: a stalled read must not hold back link events and LLDP re-addressing.  The worker
+    // signals `done` (in the epoll set below) when its sample is ready.
+    auto done = std::make_shared<SharedFd>(::eventfd(0, EFD_CLOEXEC | EFD_NONBLOCK));
+    bounded::Call<HealthSample> poll;
+    const std::string root = cfg_.sysfs_root.empty() ? topo::sysfs_root() : cfg_.sysfs_root;
+    int64_t next_rdma = cfg_.require_rdma ? mono_ns() : 0;
+    std::string rdma_said = rdma_reason();
     bool labelled = ready_;  // false: L2 came up with a NIC still without carrier
-    // One pollable fd for "stop or link event": the LLDP wait returns as soon as either
-    // fires, so a link failure is acted on in about a millisecond, not at the next tick.
+    // One pollable fd for "stop, link event or health sample": the LLDP wait returns as soon as
+    // any fires, so a link failure is acted on in about a millisecond, not at the next tick.
     int wake = ::epoll_create1(EPOLL_CLOEXEC);
-    struct CloseFd {
-        int fd;
-        ~CloseFd() {
-            if (fd >= 0) ::close(fd);
-        }
-    } wake_guard{wake};
-    for (int f : {stop_fd, watcher ? watcher->fd() : -1}) {
+    SharedFd wake_guard(wake);
+    for (int f : {stop_fd, watcher ? watcher->fd() : -1, done->fd}) {
         if (f < 0 || wake < 0) continue;
         epoll_event ev{};
         ev.events = EPOLLIN;
@@ -146,6 +221,42 @@ void Agent::monitor(int stop_fd) {
             announce_all(120);  // keep our neighbour entry alive on the switch (TTL 120 s)
             next_tx = now + cfg_.lldp_tx_interval_ns;
         }
+        if ((xgmi_watch || pcie_watch) && !poll.valid() && now >= next_health) {
+            std::vector<std::string> bdfs = xgmi_watch ? xgmi_health_bdfs() : std::vector<std::string>{};
+            std::vector<std::pair<std::string, std::string>> fns;  // (NIC, its GPU)
+            if (pcie_watch)
+                for (const auto& n : nics_) fns.emplace_back(n.ifname, n.gpu_bdf);
+            const int64_t timeout = cfg_.sysfs_read_timeout_ns;
+            poll = bounded::Call<HealthSample>("", [root, bdfs, fns, timeout, xgmi_watch, pcie_watch] {
+                HealthSample s;
+                if (xgmi_watch) {
+                    s.xgmi = topo::read_xgmi_health(root, bdfs, timeout);
+                    s.xgmi_read = true;
+                }
+                if (pcie_watch) {
+                    // One bounded call per NIC, all started first: a stalled function costs one wait.
+                    std::vector<bounded::Call<std::pair<topo::PcieLink, topo::PcieLink>>> calls;
+                    for (const auto& [ifname, gpu] : fns)
+                        calls.emplace_back("pcie:" + ifname, [root, ifname = ifname, gpu = gpu] {
+                            topo::PcieLink nic, g;
+                            if (auto d = topo::netdev_pci(root, ifname)) nic = topo::read_pcie_link(root, d->bdf);
+                            if (!gpu.empty()) g = topo::read_pcie_link(root, gpu);
+                            return std::make_pair(nic, g);
+                        });
+                    const int64_t deadline = mono_ns() + timeout;
+                    for (auto& c : calls) {
+                        auto r = c.wait(deadline);
+                        s.pcie.push_back(r ? *r : std::make_pair(topo::PcieLink{}, topo::PcieLink{}));
+                        s.pcie_late.push_back(!r);
+                    }
+                    s.pcie_read = true;
+                }
+                return s;
+            }, [done] {
+                const uint64_t one = 1;
+                (void)!::write(done->fd, &one, sizeof one);
+            });
+        }
         // LLDP: a changed Port Description means the switch port was re-addressed.
         bool changed = false;
         auto on_frame = [&](const std::string& ifname, const lldp::Frame& f) -> bool {
@@ -154,7 +265,10 @@ void Agent::monitor(int stop_fd) {
                 if (n.ifname == ifname && refresh_from_frame(n, f)) changed = true;
             return false;
         };
-        lldp_->run(std::min(next_tx, mono_ns() + cfg_.monitor_tick_ns), on_frame, wait_fd);
+        int64_t until = std::min(next_tx, mono_ns() + cfg_.monitor_tick_ns);
+        if (holddown_until_ > 0) until = std::min(until, holddown_until_);
+        if (next_rdma > 0) until = std::min(until, next_rdma);
+        lldp_->run(until, on_frame, wait_fd);
         if (fd_readable(stop_fd)) return;
         for (auto& n : nics_) {  // a cached Port Description the switch never confirmed
             if (!n.lldp_from_cache || n.cache_stale || mono_ns() - n.t_cache_applied < cfg_.lldp_cache_confirm_ns) continue;
@@ -230,35 +344,19 @@ void Agent::monitor(int stop_fd) {
             write_status();
             throw AgentError("Interface '" + removed + "' was removed");
         }
-        if (xgmi_watch && mono_ns() >= next_xgmi) {
-            const std::string before = xgmi_error_;
-            read_xgmi_health();
-            if (xgmi_error_ != before) {
-                if (xgmi_error_.empty())
-                    NLOG_I("xGMI links healthy again");
-                else
-                    NLOG_W("xGMI: %s", xgmi_error_.c_str());
-                changed = true;
-            }
-            next_xgmi = mono_ns() + cfg_.xgmi_health_interval_ns;
+        if (poll.valid() && poll.done()) {
+            uint64_t n = 0;
+            (void)!::read(done->fd, &n, sizeof n);
+            if (auto s = poll.wait(0)) changed |= apply_health(*s);
+            poll = {};
+            next_health = mono_ns() + cfg_.xgmi_health_interval_ns;
         }
-        if (cfg_.require_full_pcie && cfg_.xgmi_health_interval_ns > 0 && mono_ns() >= next_pcie) {
-            // A link can retrain narrower or slower at run time (after PCIe errors, a reset).
-            const std::string root = cfg_.sysfs_root.empty() ? topo::sysfs_root() : cfg_.sysfs_root;
-            for (auto& n : nics_) {
-                if (!n.configured) continue;  // left unconfigured at start: a restart re-checks it
-                if (auto d = topo::netdev_pci(root, n.ifname)) n.pcie = topo::read_pcie_link(root, d->bdf);
-                if (!n.gpu_bdf.empty()) n.gpu_pcie = topo::read_pcie_link(root, n.gpu_bdf);
-                std::string why = check_pcie(n);
-                if (why == n.pcie_error) continue;
-                if (why.empty())
-                    NLOG_I("Interface '%s': PCIe link back at %s", n.ifname.c_str(), n.pcie.str().c_str());
-                else
-                    NLOG_W("Interface '%s': %s", n.ifname.c_str(), why.c_str());
-                n.pcie_error = why;
-                changed = true;
-            }
-            next_pcie = mono_ns() + cfg_.xgmi_health_interval_ns;
+        if (next_rdma > 0 && mono_ns() >= next_rdma) {
+            // --require-rdma: a driver container (or the node) loading the NICs' RDMA driver.
+            if (refresh_rdma()) changed = true;
+            if (!rdma_missing().empty() && rdma_reason() != rdma_said) changed = true;  // the wait ran out
+            rdma_said = rdma_reason();
+            next_rdma = rdma_missing().empty() ? 0 : mono_ns() + cfg_.rdma_poll_ns;
         }
         if (cfg_.mode == "L3" && cfg_.verify_peers_ns > 0 && mono_ns() >= next_verify) {
             // NICs whose peer has not answered (yet): a recovered link, a new /30, or a switch
@@ -276,25 +374,45 @@ void Agent::monitor(int stop_fd) {
                 next_verify = bad > 0 ? mono_ns() + 1000000000LL : 0;
             }
         }
-        if (changed) {
+        const bool holddown_due = holddown_until_ > 0 && mono_ns() >= holddown_until_;
+        if (changed || holddown_due) {
             bool healthy = xgmi_error_.empty() &&
                            std::all_of(nics_.begin(), nics_.end(), [&](const NicState& n) { return nic_healthy(n); });
             if (healthy && !labelled) {
-                if (cfg_.mode == "L3")
-                    write_artifacts();
-                else if (!cfg_.rccl_env.empty() || !cfg_.rccl_topo.empty())
-                    write_l2_artifacts();  // a NIC that got its carrier only now has its GID now
-                labelled = publish_label();
-                if (labelled && !phases_.count("total_ready")) phases_["total_ready"] = mono_ns() - t0_;
-                if (labelled) NLOG_I("All scale-out interfaces healthy again: readiness label republished");
-                if (cfg_.mode == "L3") write_host_config();
-                announce_all(120);
-            } else if (!healthy && labelled) {
-                ready_ = false;
-                write_status();  // the probe's reason first, then the label (see write_status)
-                artifacts::remove_labels(cfg_.labels);
-                labelled = false;
-                NLOG_W("Scale-out degraded: readiness label withdrawn");
+                // After a withdrawal: republish only once the node has stayed healthy for the
+                // hold-down (the first publication is not delayed).
+                const bool hold = label_withdrawals_ > 0 && cfg_.label_holddown_ns > 0 &&
+                                  (holddown_until_ == 0 || mono_ns() < holddown_until_);
+                if (hold && holddown_until_ == 0) {
+                    holddown_until_ = mono_ns() + cfg_.label_holddown_ns;
+                    NLOG_I("Scale-out healthy again: the readiness label follows after %s without a flap (--label-holddown)",
+                           format_go_duration(cfg_.label_holddown_ns).c_str());
+                }
+                if (!hold) {
+                    holddown_until_ = 0;
+                    if (cfg_.mode == "L3")
+                        write_artifacts();
+                    else if (!cfg_.rccl_env.empty() || !cfg_.rccl_topo.empty())
+                        write_l2_artifacts();  // a NIC that got its carrier (or RDMA device) only now has its GID now
+                    labelled = publish_label();
+                    if (labelled && !phases_.count("total_ready")) phases_["total_ready"] = mono_ns() - t0_;
+                    if (labelled) NLOG_I("All scale-out interfaces healthy again: readiness label republished");
+                    if (cfg_.mode == "L3") write_host_config();
+                    announce_all(120);
+                }
+            } else if (!healthy) {
+                if (holddown_until_ > 0) {  // flapped again within the hold-down: the clock starts over
+                    holddown_until_ = 0;
+                    ++label_suppressed_;
+                }
+                if (labelled) {
+                    ready_ = false;
+                    write_status();  // the probe's reason first, then the label (see write_status)
+                    artifacts::remove_labels(cfg_.labels);
+                    labelled = false;
+                    ++label_withdrawals_;
+                    NLOG_W("Scale-out degraded: readiness label withdrawn");
+                }
             } else if (healthy && labelled && cfg_.mode == "L3") {
                 write_artifacts();  // re-addressed NIC: refresh the RCCL artifacts
                 write_host_config();

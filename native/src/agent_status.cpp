@@ -148,6 +148,16 @@ std::string Agent::render_metrics() const {
                         n.pcie.degraded() || n.gpu_pcie.narrower() ? 1 : 0);
     metric("netop_agent_link_flaps_total", "counter", "link losses observed after readiness");
     o += strfmt("netop_agent_link_flaps_total %d\n", flaps_);
+    metric("netop_agent_label_withdrawals_total", "counter", "times the monitor withdrew the readiness label");
+    o += strfmt("netop_agent_label_withdrawals_total %d\n", label_withdrawals_);
+    metric("netop_agent_label_suppressed_total", "counter",
+           "recoveries not republished because the node flapped again within --label-holddown");
+    o += strfmt("netop_agent_label_suppressed_total %d\n", label_suppressed_);
+    if (cfg_.require_rdma) {
+        metric("netop_agent_nic_rdma", "gauge", "1 when the NIC has an RDMA device (--require-rdma: the label waits for every NIC's)");
+        for (const auto& n : nics_)
+            o += strfmt("netop_agent_nic_rdma{nic=\"%s\"} %d\n", httpd::escape_label(n.ifname).c_str(), n.rdma_dev.empty() ? 0 : 1);
+    }
     metric("netop_agent_reconfigurations_total", "counter", "NIC re-addressings after a Port Description change");
     o += strfmt("netop_agent_reconfigurations_total %d\n", reconfigs_);
     if (cfg_.mode == "L3") {
@@ -270,12 +280,17 @@ std::string Agent::not_ready_reason() const {
             why = "the switch has not confirmed the cached Port Description";
         else if (!n.peer_error.empty())
             why = n.peer_error;
+        else if (cfg_.require_rdma && n.rdma_dev.empty() && (cfg_.mode != "L3" || n.configured))
+            why = rdma_reason();
         else if (cfg_.mode == "L3" && !n.configured)
             why = n.lldp_seen                           ? "not configured yet"
                   : n.link.up() && !n.link.lower_up() ? "waiting for carrier"  // no frame can come yet
                                                         : "waiting for LLDP";
         if (!why.empty()) parts.push_back(n.ifname + ": " + why);
     }
+    if (parts.empty() && holddown_until_ > 0)
+        parts.push_back(strfmt("label hold-down: healthy again after %d withdrawal(s), republished in %.1fs without a flap",
+                               label_withdrawals_, double(std::max<int64_t>(0, holddown_until_ - mono_ns())) / 1e9));
     return join(parts, "; ");
 }
 

@@ -1,5 +1,7 @@
 #include "netop/topology.hpp"
 
+#include "netop/bounded.hpp"
+
 #include <fcntl.h>
 #include <sys/utsname.h>
 #include <unistd.h>
@@ -201,6 +203,12 @@ int64_t netdev_speed_mbps(const std::string& root, const std::string& ifname) {
     } catch (const std::exception&) {
         return -1;
     }
+}
+
+std::string netdev_rdma_device(const std::string& root, const std::string& ifname) {
+    if (ifname.empty() || ifname.find('/') != std::string::npos) return "";
+    auto ib = list_dir(path_join(root, "class/net/" + ifname + "/device/infiniband"));
+    return ib.empty() ? std::string() : ib.front();
 }
 
 std::vector<std::string> netdev_uppers(const std::string& root, const std::string& ifname) {
@@ -655,6 +663,26 @@ std::vector<XgmiLinkHealth> read_xgmi_health(const std::string& root, const std:
         auto blob = read_file(path_join(root, "bus/pci/devices/" + bdf + "/gpu_metrics"));
         XgmiLinkHealth h = parse_gpu_metrics(blob ? *blob : std::string());
         h.bdf = bdf;
+        out.push_back(std::move(h));
+    }
+    return out;
+}
+
+std::vector<XgmiLinkHealth> read_xgmi_health(const std::string& root, const std::vector<std::string>& bdfs,
+                                             int64_t timeout_ns) {
+    std::vector<std::string> paths;
+    for (const auto& bdf : bdfs) paths.push_back(path_join(root, "bus/pci/devices/" + bdf + "/gpu_metrics"));
+    const auto reads = bounded::read_files(paths, mono_ns() + timeout_ns);
+    std::vector<XgmiLinkHealth> out;
+    for (size_t i = 0; i < bdfs.size(); ++i) {
+        XgmiLinkHealth h;
+        if (reads[i].late) {
+            h.late = true;
+            h.error = "gpu_metrics did not answer in " + format_go_duration(timeout_ns);
+        } else {
+            h = parse_gpu_metrics(reads[i].data ? *reads[i].data : std::string());
+        }
+        h.bdf = bdfs[i];
         out.push_back(std::move(h));
     }
     return out;

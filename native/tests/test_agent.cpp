@@ -105,6 +105,7 @@ struct Fixture {
         cfg.wait_ns = 100000000;
         cfg.link_wait_ns = 20000000;
         cfg.carrier_wait_ns = 20000000;
+        cfg.label_holddown_ns = 0;  // republished at once (the hold-down tests set their own)
         cfg.labels.dir = tmp.path + "/features.d";
         tmp.mkdir("features.d");
         cfg.rccl_net = tmp.path + "/rccl-net.json";
@@ -2975,4 +2976,152 @@ TEST(agent_invalid_rail_pattern_waits_with_one_reason_instead_of_crash_looping) 
     }
     CHECK(err.find("(with {rail} = 4)") != std::string::npos);
     CHECK_EQ(agent::rail_pattern_error("leaf-r{rail}-.*"), std::string());
+}
+
+// ---------------------------------------------------------------------------------------------
+// --require-rdma: the label (and rccl.env) wait for every NIC's RDMA device
+// ---------------------------------------------------------------------------------------------
+namespace {
+struct RdmaFixture : Fixture {
+    RdmaFixture() {
+        cfg.require_rdma = true;
+        cfg.sysfs_root = tmp.path + "/sys/";
+        tmp.mkdir("sys/class/net");
+        cfg.rccl_env = tmp.path + "/rccl.env";
+        cfg.rdma_poll_ns = 1000000;
+        cfg.monitor_tick_ns = 1000000;
+        cfg.gid_wait_ns = 1000000;  // no GID tables in this sysfs
+    }
+    void bind(const std::string& nic, const std::string& dev) { tmp.mkdir("sys/class/net/" + nic + "/device/infiniband/" + dev); }
+};
+}  // namespace
+
+TEST(agent_require_rdma_configures_waits_unlabelled_then_labels_when_the_devices_appear) {
+    RdmaFixture f;
+    f.tmp.write("rccl.env", "NCCL_IB_HCA==mlx5_9:1\n");  // an earlier run's, naming a device that is gone
+    Pipe stop;
+    agent::Agent a(f.cfg, f.ops, f.all_valid(), f.nm());
+    bool waited = false, labelled = false;
+    std::string reason;
+    a.on_monitor_tick = [&](int tick) {
+        if (tick == 1) {
+            auto why = read_file(agent::reason_path(f.cfg.status_file));
+            reason = why ? *why : "";
+            waited = !path_exists(f.cfg.labels.path()) && !path_exists(f.cfg.rccl_env);
+            for (int i = 0; i < 3; ++i) CHECK(a.nics()[size_t(i)].configured);  // the NICs are not held back
+            f.bind("ens0", "mlx5_0");
+            f.bind("ens1", "mlx5_1");
+        } else if (tick == 20) {
+            CHECK(!path_exists(f.cfg.labels.path()));  // ens2 still has none
+            f.bind("ens2", "mlx5_2");
+        } else if (tick > 20 && path_exists(f.cfg.labels.path())) {
+            labelled = true;
+            stop.fire();
+        } else if (tick > 2000) {
+            stop.fire();
+        }
+    };
+    a.run(stop.fd[0]);
+    CHECK(waited);
+    CHECK_EQ(reason, std::string("ens0: waiting for RDMA device; ens1: waiting for RDMA device; ens2: waiting for RDMA device\n"));
+    CHECK(labelled);
+    auto env = read_file(f.cfg.rccl_env);
+    CHECK(env && env->find("NCCL_IB_HCA==mlx5_0:1,mlx5_1:1,mlx5_2:1\n") != std::string::npos);
+    CHECK(a.render_metrics().find("netop_agent_nic_rdma{nic=\"ens2\"} 1") != std::string::npos);
+}
+
+TEST(agent_require_rdma_past_the_wait_names_the_fault) {
+    RdmaFixture f;
+    f.cfg.rdma_wait_ns = 0;
+    f.bind("ens1", "mlx5_1");
+    Pipe stop;
+    agent::Agent a(f.cfg, f.ops, f.all_valid(), f.nm());
+    std::string reason;
+    a.on_monitor_tick = [&](int tick) {
+        if (tick == 2) {
+            auto why = read_file(agent::reason_path(f.cfg.status_file));
+            reason = why ? *why : "";
+            stop.fire();
+        }
+    };
+    a.run(stop.fd[0]);
+    CHECK_EQ(reason, std::string("ens0: no RDMA device (load its RDMA driver); ens2: no RDMA device (load its RDMA driver)\n"));
+    CHECK(!path_exists(f.cfg.labels.path()));
+}
+
+TEST(agent_require_rdma_without_the_monitor_fails_naming_the_nics) {
+    RdmaFixture f;
+    f.cfg.monitor = false;
+    f.bind("ens0", "mlx5_0");
+    agent::Agent a(f.cfg, f.ops, f.all_valid(), f.nm());
+    std::string err;
+    try {
+        a.run(-1);
+    } catch (const agent::AgentError& e) {
+        err = e.what();
+    }
+    CHECK(err.find("No RDMA device on ens1, ens2 (load the NIC's RDMA driver") == 0);
+    CHECK(!path_exists(f.cfg.labels.path()));
+}
+
+TEST(agent_without_require_rdma_labels_nics_without_rdma_devices) {  // the reference's behaviour
+    Fixture f;
+    f.cfg.keep_running = false;
+    f.cfg.rccl_env = f.tmp.path + "/rccl.env";
+    f.cfg.gid_wait_ns = 1000000;
+    agent::Agent a(f.cfg, f.ops, f.all_valid(), f.nm());
+    a.run(-1);
+    auto env = read_file(f.cfg.rccl_env);
+    CHECK(env && env->find("NCCL_IB_HCA") == std::string::npos);
+}
+
+// ---------------------------------------------------------------------------------------------
+// --label-holddown: one withdrawal and one republish for a burst of flaps
+// ---------------------------------------------------------------------------------------------
+TEST(agent_label_holddown_republishes_once_after_the_last_flap) {
+    Fixture f;
+    f.cfg.monitor_tick_ns = 1000000;
+    f.cfg.label_holddown_ns = 150LL * 1000000;
+    Pipe stop;
+    agent::Agent a(f.cfg, f.ops, f.all_valid(), f.nm());
+    int withdrawals = 0, publishes = 0, flaps = 0;
+    bool was = true;
+    int64_t t_last_up = 0, t_back = 0, t_next = 0;
+    std::string reason_in_holddown;
+    a.on_monitor_tick = [&](int) {
+        const bool now = path_exists(f.cfg.labels.path());
+        if (was && !now) ++withdrawals;
+        if (!was && now) {
+            ++publishes;
+            t_back = mono_ns();
+        }
+        was = now;
+        auto& l = f.ops.links["ens1"];
+        const int64_t t = mono_ns();
+        if (flaps < 10 && t >= t_next) {  // ten flaps, 10 ms apart (down 5 ms, up 5 ms)
+            const bool up = l.flags & IFF_UP;
+            if (up) {
+                l.flags &= ~unsigned(IFF_UP);
+            } else {
+                l.flags |= IFF_UP;
+                ++flaps;
+                t_last_up = t;
+            }
+            f.ops.events.push_back({false, l});
+            t_next = t + 5000000;
+        } else if (flaps == 10 && t_last_up && t - t_last_up > 20000000 && reason_in_holddown.empty()) {
+            auto why = read_file(agent::reason_path(f.cfg.status_file));
+            reason_in_holddown = why ? *why : "-";
+        }
+        if (publishes || (t_last_up && t - t_last_up > 2000000000LL)) stop.fire();
+    };
+    a.run(stop.fd[0]);
+    CHECK_EQ(flaps, 10);
+    CHECK_EQ(withdrawals, 1);
+    CHECK_EQ(publishes, 1);
+    CHECK(t_back - t_last_up >= f.cfg.label_holddown_ns);
+    CHECK(t_back - t_last_up < f.cfg.label_holddown_ns + 100000000LL);
+    CHECK(reason_in_holddown.rfind("label hold-down: healthy again after 1 withdrawal(s)", 0) == 0);
+    CHECK(a.render_metrics().find("netop_agent_label_suppressed_total 9\n") != std::string::npos);
+    CHECK(a.render_metrics().find("netop_agent_label_withdrawals_total 1\n") != std::string::npos);
 }

@@ -72,6 +72,12 @@ int main(int argc, char** argv) {
     fs.add_bool("require-full-pcie", &cfg.require_full_pcie, "configure (and label) a NIC only if its PCIe link trained at the speed and width it supports, and its GPU's at full width; degraded links are reported either way (status.json, metrics)");
     fs.add_int("xgmi-min-link-width", &cfg.xgmi_min_link_width, "with --xgmi-expect: the narrowest trained xGMI link width (lanes) a GPU may run at, from gpu_metrics; 0 = any");
     fs.add_duration("xgmi-health-interval", &cfg.xgmi_health_interval_ns, "with the monitor: how often the xGMI links' state (with --xgmi-expect) and the rails' PCIe links (with --require-full-pcie) are read again; a link down or retrained narrower withdraws the readiness label until it is back (0 = at start only)");
+    fs.add_duration("sysfs-read-timeout", &cfg.sysfs_read_timeout_ns, "bound on each sysfs read firmware or hardware answers (gpu_metrics: an SMU query per GPU; PCIe link state; the KFD topology): a read still blocked then is reported and the label follows the policy, the start and the monitor never wait behind it");
+    fs.add_duration("label-holddown", &cfg.label_holddown_ns, "with the monitor: after the readiness label was withdrawn, republish it only once the node has been healthy this long without a flap (0 = at once; the first publication is never delayed)");
+    fs.add_int("xgmi-down-samples", &cfg.xgmi_down_samples, "with the monitor: consecutive gpu_metrics samples that must see an xGMI link down before it counts (a status read during a GPU reset is not a flap)");
+    fs.add_bool("require-rdma", &cfg.require_rdma, "every scale-out NIC must have an RDMA device (its RDMA driver loaded) before the readiness label and rccl.env: the NICs are configured, the probe says 'waiting for RDMA device', and the monitor labels the node once the devices appear");
+    fs.add_duration("rdma-wait", &cfg.rdma_wait_ns, "with --require-rdma: how long after the start a missing RDMA device is 'waiting' (start-up) before it is reported as the fault 'no RDMA device (load its RDMA driver)'");
+    fs.add_duration("rdma-poll-interval", &cfg.rdma_poll_ns, "with --require-rdma: how often the waiting agent looks for the RDMA devices", true);
     fs.add_duration("link-wait", &cfg.link_wait_ns, "time to wait for link state echoes from the kernel");
     fs.add_duration("carrier-wait", &cfg.carrier_wait_ns, "L2: time every admin-up NIC may take to get a carrier (optic and switch port link training) before it is reported as 'no carrier'; meanwhile the readiness probe says 'waiting for carrier' (with the monitor a NIC still dark afterwards is labelled when its carrier comes)");
     fs.add_duration("verify-peers", &cfg.verify_peers_ns,

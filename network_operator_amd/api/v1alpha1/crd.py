@@ -49,6 +49,7 @@ _KIND_DESC = (
 def openapi_schema() -> dict:
     amd_so = {
         "description": "AMD MI355X scale-out specific settings. Only valid when configuration type is 'amd-so'",
+        "default": {},
         "type": "object",
         "properties": {
             "disableNetworkManager": {
@@ -63,8 +64,24 @@ def openapi_schema() -> dict:
             "pullPolicy": {"description": "Image pull policy used in the resulting daemonset.",
                            "enum": list(T.PULL_POLICIES), "type": "string"},
             "xgmiCheck": {"description": "Publish the readiness label only when the node's xGMI mesh is complete\n"
-                                         "(every GPU pair linked, read from the KFD topology).",
-                          "type": "boolean"},
+                                         "(every GPU pair linked, read from the KFD topology) and every link is up\n"
+                                         "(amdgpu gpu_metrics).  Default true; false for nodes without an xGMI mesh.",
+                          "default": True, "type": "boolean"},
+            "requireRdma": {"description": "Scale-out ready means RDMA ready: publish the readiness label (and write\n"
+                                           "rccl.env) only once every scale-out NIC has an RDMA device, i.e. its RDMA\n"
+                                           "driver (ionic_rdma, mlx5_ib, bnxt_re) is loaded.  Meanwhile the NICs are\n"
+                                           "configured and the node reports \"waiting for RDMA device\"; it is labelled\n"
+                                           "as soon as the devices appear.  Default true; false labels nodes whose rails\n"
+                                           "RCCL could use only over TCP sockets.",
+                            "default": True, "type": "boolean"},
+            "rdmaWait": {"description": "With requireRdma: how long a missing RDMA device counts as start-up (a Go\n"
+                                        "duration, 1s..1h; default 5m).  Afterwards the node reports \"no RDMA device\n"
+                                        "(load its RDMA driver)\" and the policy is Degraded.",
+                         "pattern": T.LLDP_WAIT_PATTERN, "type": "string"},
+            "driverImage": {"description": "Optional NIC RDMA-driver (KMD) container, run as a privileged init container\n"
+                                           "before the agent with the host's /lib/modules; it must load the driver\n"
+                                           "(e.g. ionic_rdma for AMD Pollara) and exit 0.",
+                            "type": "string"},
             "lldpAnnounce": {"description": "Transmit an LLDPDU from every scale-out NIC so IEEE 802.1AB-2009 switches\n"
                                             "answer with fast transmission (default true).",
                              "type": "boolean"},
@@ -394,6 +411,22 @@ def prune(value: Any, schema: dict) -> Any:
         return out
     if isinstance(value, list) and "items" in schema:
         return [prune(v, schema["items"]) for v in value]
+    return value
+
+
+def apply_defaults(value: Any, schema: dict) -> Any:
+    """Fills the schema's ``default`` values into objects that lack the field, in place -- what
+    the API server does for a structural schema, on every read and write, before mutating
+    admission (so a minimal policy written with kubectl gets them even with webhooks off)."""
+    if isinstance(value, dict) and schema.get("type") == "object":
+        for k, ps in (schema.get("properties") or {}).items():
+            if k not in value and "default" in ps:
+                value[k] = ps["default"]
+            if k in value:
+                apply_defaults(value[k], ps)
+    elif isinstance(value, list) and isinstance(schema.get("items"), dict):
+        for v in value:
+            apply_defaults(v, schema["items"])
     return value
 
 

@@ -19,6 +19,8 @@ What changes (docs/USER_GUIDE.md section 7):
 - The NFD labels the reference selects on (``intel.feature.node.kubernetes.io/gaudi-ready``,
   ``.../gaudi``) become the AMD rule's (``amd.feature.node.kubernetes.io/gpu-ready``, ``.../gpu``).
   Other selector keys are kept as they are.
+- ``xgmiCheck`` and ``requireRdma`` are written out as true, this operator's defaults: the label
+  also waits for the xGMI mesh and for an RDMA device on every scale-out NIC.
 - Server-written metadata (uid, resourceVersion, status, managedFields, finalizers, the last-applied
   annotation) is dropped: the result is something to apply, not a copy of the old object.
 """
@@ -107,6 +109,14 @@ def convert_policy(obj: dict, image: Optional[str] = None) -> Tuple[dict, List[s
         notes.append(f"{where}: image {old_image} is the Gaudi agent -> {T.DEFAULT_AGENT_IMAGE} (the webhook's default)")
     for k in sorted(gso):
         notes.append(f"{where}: gaudiScaleOut.{k} has no counterpart and was dropped")
+    # Written out, so the converted object says what it does: the MI355X defaults (the CRD's and
+    # the webhook's).  requireRdma keeps the reference's meaning of the label -- its NICs are RDMA
+    # NICs by construction (reference cmd/discover/network.go:34) -- on nodes whose RoCE NICs need
+    # an RDMA driver loaded.
+    so["xgmiCheck"] = True
+    so["requireRdma"] = True
+    notes.append(f"{where}: amdScaleOut.xgmiCheck and requireRdma set true (this operator's defaults): the readiness "
+                 "label also waits for a complete xGMI mesh and an RDMA device on every scale-out NIC")
     new_spec: Dict[str, Any] = {"configurationType": T.CONFIG_AMD_SCALE_OUT, "amdScaleOut": so}
     if "nodeSelector" in spec:
         new_spec["nodeSelector"] = _selector(spec.pop("nodeSelector"), where, notes)

@@ -13,9 +13,10 @@ spec.gaudiScaleOut                     spec.amdScaleOut (same sub-fields)
 status {targets, ready, state, errors} identical
 =====================================  ==============================================
 
-``amdScaleOut`` adds optional MI355X fields (all additive, absent = previous behaviour):
-``xgmiCheck`` (gate readiness on the xGMI mesh), ``lldpAnnounce`` (self-announce to trigger
-switch fast start), ``interfaces`` (extra NICs) and ``nicDrivers`` (affinity allow-list).
+``amdScaleOut`` adds optional MI355X fields (all additive): ``xgmiCheck`` (gate readiness on the
+xGMI mesh; on unless set false), ``requireRdma`` (gate it on every rail's RDMA device; on unless
+set false), ``driverImage`` (the NICs' RDMA driver container), ``lldpAnnounce`` (self-announce to
+trigger switch fast start), ``interfaces`` (extra NICs) and ``nicDrivers`` (affinity allow-list).
 
 Objects are plain dataclasses with lossless ``to_dict`` / ``from_dict`` (unknown fields are
 preserved in ``extra`` so a round trip never drops data written by a newer client).
@@ -44,6 +45,8 @@ LLDP_WAIT_PATTERN = r"^([0-9]+(\.[0-9]+)?(h|m|s|ms))+$"
 LLDP_WAIT_MIN_S, LLDP_WAIT_MAX_S = 1.0, 1800.0
 # carrierWait: the same duration grammar; L2, how long NICs may train their links (agent default 30s)
 CARRIER_WAIT_MIN_S, CARRIER_WAIT_MAX_S = 1.0, 600.0
+# rdmaWait: the same grammar; how long a missing RDMA device is start-up (agent default 5m)
+RDMA_WAIT_MIN_S, RDMA_WAIT_MAX_S = 1.0, 3600.0
 
 
 def parse_go_duration(s: str) -> float:
@@ -59,6 +62,7 @@ PULL_POLICIES = ("Never", "Always", "IfNotPresent")
 MTU_MIN, MTU_MAX = 1500, 9000
 LOG_LEVEL_MIN, LOG_LEVEL_MAX = 0, 8
 DEFAULT_AGENT_IMAGE = "amd/amd-network-linkdiscovery:latest"
+OPERATOR_VERSION = "0.1.0"  # the agent release whose flags the operator passes (Makefile VERSION)
 
 
 DEFAULT_VALIDATION_IMAGE = "amd/amd-network-validation:0.1.0"
@@ -100,7 +104,7 @@ class AmdScaleOutSpec:
     pullPolicy: str = ""
     mtu: int = 0
     # MI355X additions
-    xgmiCheck: bool = False
+    xgmiCheck: Optional[bool] = None  # None = on (the CRD default, the mutating webhook): verify the mesh
     lldpAnnounce: Optional[bool] = None
     interfaces: List[str] = field(default_factory=list)
     nicDrivers: List[str] = field(default_factory=list)
@@ -127,6 +131,12 @@ class AmdScaleOutSpec:
     checkPeerMtu: Optional[bool] = None
     # With disableFirmwareLldp: hand DCBX to the host on DCB NICs without a firmware-LLDP flag
     handDcbxToHost: bool = False
+    # Scale-out ready means RDMA ready: every rail needs an RDMA device before the label and
+    # rccl.env (None = on, like xgmiCheck).  rdmaWait: how long that is start-up (Go duration).
+    requireRdma: Optional[bool] = None
+    rdmaWait: str = ""
+    # The NICs' RDMA driver (KMD) container, a privileged init container as for hostNic.driverImage
+    driverImage: str = ""
     validation: Optional[ValidationSpec] = None
     extra: Dict[str, Any] = field(default_factory=dict)
 
@@ -138,7 +148,7 @@ class AmdScaleOutSpec:
                "interfaces", "nicDrivers", "disableFirmwareLldp", "metricsPort", "gpuDirectRdma", "rcclEnv",
                "railTableBase", "rcclSocketIfname", "lldpCache", "verifyPeers", "lldpWait", "carrierWait", "keepConfigOnRestart",
                "railSwitchPattern", "minLinkSpeedGbps", "requireFullPcieLink", "checkPeerMtu", "handDcbxToHost",
-               "validation")
+               "requireRdma", "rdmaWait", "driverImage", "validation")
 
     def to_dict(self) -> dict:
         d: dict = {}
@@ -150,8 +160,8 @@ class AmdScaleOutSpec:
                 d[k] = getattr(self, k)
         if self.mtu:
             d["mtu"] = self.mtu
-        if self.xgmiCheck:
-            d["xgmiCheck"] = True
+        if self.xgmiCheck is not None:
+            d["xgmiCheck"] = self.xgmiCheck
         if self.lldpAnnounce is not None:
             d["lldpAnnounce"] = self.lldpAnnounce
         if self.interfaces:
@@ -190,6 +200,12 @@ class AmdScaleOutSpec:
             d["checkPeerMtu"] = self.checkPeerMtu
         if self.handDcbxToHost:
             d["handDcbxToHost"] = True
+        if self.requireRdma is not None:
+            d["requireRdma"] = self.requireRdma
+        if self.rdmaWait:
+            d["rdmaWait"] = self.rdmaWait
+        if self.driverImage:
+            d["driverImage"] = self.driverImage
         if self.validation is not None:
             d["validation"] = self.validation.to_dict()
         d.update(copy.deepcopy(self.extra))
@@ -204,7 +220,7 @@ class AmdScaleOutSpec:
             image=d.pop("image", "") or "",
             pullPolicy=d.pop("pullPolicy", "") or "",
             mtu=int(d.pop("mtu", 0) or 0),
-            xgmiCheck=bool(d.pop("xgmiCheck", False)),
+            xgmiCheck=d.pop("xgmiCheck", None),
             lldpAnnounce=d.pop("lldpAnnounce", None),
             interfaces=list(d.pop("interfaces", []) or []),
             nicDrivers=list(d.pop("nicDrivers", []) or []),
@@ -221,6 +237,9 @@ class AmdScaleOutSpec:
             requireFullPcieLink=bool(d.pop("requireFullPcieLink", False)),
             checkPeerMtu=d.pop("checkPeerMtu", None),
             handDcbxToHost=bool(d.pop("handDcbxToHost", False)),
+            requireRdma=d.pop("requireRdma", None),
+            rdmaWait=d.pop("rdmaWait", "") or "",
+            driverImage=d.pop("driverImage", "") or "",
             verifyPeers=bool(d.pop("verifyPeers", False)),
             lldpWait=d.pop("lldpWait", "") or "",
             carrierWait=d.pop("carrierWait", "") or "",

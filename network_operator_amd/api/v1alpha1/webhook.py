@@ -63,9 +63,18 @@ class InvalidInterfaceError(ValidationError):
 
 
 def default(policy: T.NetworkClusterPolicy) -> T.NetworkClusterPolicy:
+    """The reference's Default (:65-74): the agent image.  MI355X-first defaults as well (the CRD
+    schema carries them too, for webhooks-off installs): an amd-so policy verifies the node's
+    xGMI mesh and requires every rail's RDMA device unless it says otherwise."""
     log.info("default name=%s", policy.name)
-    if policy.spec.configurationType == T.CONFIG_AMD_SCALE_OUT and not policy.spec.amdScaleOut.image:
-        policy.spec.amdScaleOut.image = T.DEFAULT_AGENT_IMAGE
+    so = policy.spec.amdScaleOut
+    if policy.spec.configurationType == T.CONFIG_AMD_SCALE_OUT:
+        if not so.image:
+            so.image = T.DEFAULT_AGENT_IMAGE
+        if so.xgmiCheck is None:
+            so.xgmiCheck = True
+        if so.requireRdma is None:
+            so.requireRdma = True
     if policy.spec.configurationType == T.CONFIG_HOST_NIC and policy.spec.hostNic is not None \
             and not policy.spec.hostNic.image:
         policy.spec.hostNic.image = T.DEFAULT_AGENT_IMAGE
@@ -118,6 +127,13 @@ class InvalidCarrierWaitError(ValidationError):
         super().__init__()
         self.message = (f"invalid carrierWait {value!r}: a duration such as 30s or 1m, between "
                         f"{int(T.CARRIER_WAIT_MIN_S)}s and {int(T.CARRIER_WAIT_MAX_S // 60)}m")
+
+
+class InvalidRdmaWaitError(ValidationError):
+    def __init__(self, value: str):
+        super().__init__()
+        self.message = (f"invalid rdmaWait {value!r}: a duration such as 5m or 10m, between "
+                        f"{int(T.RDMA_WAIT_MIN_S)}s and {int(T.RDMA_WAIT_MAX_S // 60)}m")
 
 
 class InvalidRailSwitchPatternError(ValidationError):
@@ -322,6 +338,25 @@ def validate_carrier_wait(value: str) -> None:
         raise InvalidCarrierWaitError(value)
 
 
+def validate_rdma_wait(value: str) -> None:
+    if not value:
+        return
+    try:
+        secs = T.parse_go_duration(value)
+    except ValueError:
+        raise InvalidRdmaWaitError(value) from None
+    if not T.RDMA_WAIT_MIN_S <= secs <= T.RDMA_WAIT_MAX_S:
+        raise InvalidRdmaWaitError(value)
+
+
+def image_tag(image: str) -> str:
+    """The tag of an image reference ("" for a digest or no tag)."""
+    if "@" in image:
+        return ""
+    name = image.rsplit("/", 1)[-1]
+    return name.split(":", 1)[1] if ":" in name else ""
+
+
 def validate_amd_so_spec(s: T.AmdScaleOutSpec) -> List[str]:
     """Returns admission warnings.  (The reference's validateGaudiSoSpec is a no-op, :87-89.)"""
     warnings = []
@@ -346,6 +381,19 @@ def validate_amd_so_spec(s: T.AmdScaleOutSpec) -> List[str]:
         warnings.append("handDcbxToHost has no effect without disableFirmwareLldp in L3 mode")
     if s.checkPeerMtu is not None and s.layer == "L2":
         warnings.append("checkPeerMtu has no effect in L2 mode (no LLDP)")
+    validate_rdma_wait(s.rdmaWait)
+    if s.rdmaWait and s.requireRdma is False:
+        warnings.append("rdmaWait has no effect with requireRdma false")
+    if s.requireRdma is False:
+        warnings.append("requireRdma false: nodes whose scale-out NICs have no RDMA device are labelled scale-out "
+                        "ready, and RCCL falls back to TCP sockets on those rails")
+    tag = image_tag(s.image)
+    if s.image and tag not in ("", "latest", T.OPERATOR_VERSION):
+        # the operator passes the flags of its own agent release; an older agent binary
+        # exits on the first flag it does not know, on every selected node.
+        warnings.append(f"image pins agent tag {tag!r}: this operator ({T.OPERATOR_VERSION}) passes flags of its own agent "
+                        "release (e.g. --link-state, --require-rdma, --label-holddown); an older agent exits on a flag "
+                        "it does not know")
     return warnings
 
 

@@ -167,7 +167,8 @@ def probe_reason(events: List[dict], limit: int = 1500) -> Optional[str]:
 # What an agent says while its node is still coming up.  "waiting for carrier": L2, a NIC whose
 # optic / switch port is still training its link, within the agent's --carrier-wait.
 # "agent starting": probed before the agent wrote its status file (discover --ready-check).
-STARTUP_REASONS = ("waiting for LLDP", "not configured yet", "waiting for carrier", "agent starting")
+STARTUP_REASONS = ("waiting for LLDP", "not configured yet", "waiting for carrier", "agent starting",
+                   "waiting for RDMA device")
 
 
 def _starting_up(reason: str) -> bool:

@@ -93,9 +93,14 @@ def agent_args(p: T.NetworkClusterPolicy) -> List[str]:
     # mount (the reference's HCCL contract is gaudinet.json, controller.go:198-200).
     args += [f"--rccl-topo={ARTIFACT_DIR_CONTAINER}/{RCCL_TOPO_FILE}",
              f"--rccl-topo-env-path={ARTIFACT_DIR_HOST}/{RCCL_TOPO_FILE}"]
-    # MI355X options
-    if so.xgmiCheck:
+    # MI355X options.  xgmiCheck and requireRdma are on unless the policy turns them off (the
+    # webhook and the CRD default them; a policy stored before they existed reads them as unset).
+    if so.xgmiCheck is not False:
         args.append("--xgmi-expect=0")
+    if so.requireRdma is not False:
+        args.append("--require-rdma")
+        if so.rdmaWait:
+            args.append(f"--rdma-wait={so.rdmaWait}")
     if so.lldpAnnounce is False:
         args.append("--lldp-announce=false")
     if so.interfaces:
@@ -162,16 +167,14 @@ def update_amd_scale_out_daemonset(ds: dict, p: T.NetworkClusterPolicy, namespac
         wanted |= {"var-run-dbus", "networkmanager"}
     add_host_volume(ds, "rccl-artifacts", ARTIFACT_DIR_HOST, ARTIFACT_DIR_CONTAINER)  # L2 too (rccl.env)
     wanted.add("rccl-artifacts")
+    # The rails' RDMA driver (KMD) container, as for host-nic: the RDMA devices exist when the
+    # agent starts, and --require-rdma finds them without waiting.
+    if set_driver_container(pod, so.driverImage, so.pullPolicy):
+        wanted.add("host-lib-modules")
     for v in MANAGED_VOLUMES + ("host-lib-modules",):
         if v not in wanted:
             remove_volume(ds, v)
     order_managed_volumes(ds)
-    # A policy that switched from host-nic: no driver container, default readiness probe.
-    inits = [x for x in pod.get("initContainers", []) if x.get("name") != "nic-driver"]
-    if inits:
-        pod["initContainers"] = inits
-    else:
-        pod.pop("initContainers", None)
     probe = c.get("readinessProbe", {}).get("exec")
     if probe:
         probe["command"] = probe["command"][:1] + ["--ready-check", f"--status-file={discovery.AGENT_STATUS_FILE}"]
@@ -192,6 +195,25 @@ HOST_NIC_LLDP_CACHE_FILE = "host-nic-lldp-cache"
 HOST_NIC_MTU_STATE_FILE = "host-nic-mtu-state"  # --mtu-state: the host NICs' own MTUs
 HOST_NIC_LINK_STATE_FILE = "host-nic-link-state"  # --link-state, apart from the amd-so agent's
 DRIVER_CONTAINER = "nic-driver"
+
+
+def set_driver_container(pod: dict, image: str, pull_policy: str) -> bool:
+    """The optional kernel-driver (KMD) init container: privileged, sees the host's modules, runs
+    to completion before the agent starts, so the NICs (host-nic) or their RDMA devices (amd-so)
+    exist when discovery runs.  Removed when `image` is empty; True when it is there."""
+    inits = [x for x in pod.get("initContainers", []) if x.get("name") != DRIVER_CONTAINER]
+    if image:
+        spec_vols = pod.setdefault("volumes", [])
+        if not any(v.get("name") == "host-lib-modules" for v in spec_vols):
+            spec_vols.append({"name": "host-lib-modules", "hostPath": {"path": "/lib/modules", "type": "Directory"}})
+        inits.append({"name": DRIVER_CONTAINER, "image": image, "imagePullPolicy": pull_policy or "IfNotPresent",
+                      "securityContext": {"privileged": True},
+                      "volumeMounts": [{"name": "host-lib-modules", "mountPath": "/lib/modules"}]})
+    if inits:
+        pod["initContainers"] = inits
+    else:
+        pod.pop("initContainers", None)
+    return bool(image)
 
 
 def host_nic_agent_args(p: T.NetworkClusterPolicy) -> List[str]:
@@ -262,22 +284,8 @@ def update_host_nic_daemonset(ds: dict, p: T.NetworkClusterPolicy, namespace: st
     # policy that dropped mtu still lets the next agent and the cleanup Job find the record.
     add_host_volume(ds, "rccl-artifacts", ARTIFACT_DIR_HOST, ARTIFACT_DIR_CONTAINER)
     wanted.add("rccl-artifacts")
-    # Optional kernel-driver container: privileged, sees the host's modules, runs to completion
-    # before the agent starts (init container), so the NICs exist when discovery runs.
-    inits = [x for x in pod.get("initContainers", []) if x.get("name") != DRIVER_CONTAINER]
-    if hn.driverImage:
-        spec_vols = pod.setdefault("volumes", [])
-        if not any(v.get("name") == "host-lib-modules" for v in spec_vols):
-            spec_vols.append({"name": "host-lib-modules", "hostPath": {"path": "/lib/modules", "type": "Directory"}})
+    if set_driver_container(pod, hn.driverImage, hn.pullPolicy):
         wanted.add("host-lib-modules")
-        inits.append({"name": DRIVER_CONTAINER, "image": hn.driverImage,
-                      "imagePullPolicy": hn.pullPolicy or "IfNotPresent",
-                      "securityContext": {"privileged": True},
-                      "volumeMounts": [{"name": "host-lib-modules", "mountPath": "/lib/modules"}]})
-    if inits:
-        pod["initContainers"] = inits
-    else:
-        pod.pop("initContainers", None)
     for v in MANAGED_VOLUMES + ("host-lib-modules",):
         if v not in wanted:
             remove_volume(ds, v)

@@ -47,6 +47,8 @@ HOST_NIC_READY_LABEL = "amd.feature.node.kubernetes.io/host-nic-ready"
 # driver container (the KMD install of BASELINE.json configs[4]) binds them.
 HOST_NICS = ("ens9np0", "ens49np1")
 KMD_IMAGE = "example.com/amd/ionic-kmd:1.0"
+# amd-so driverImage: the rails' RDMA driver (ionic_rdma on Pollara), simulated by fakesysfs bind-rdma
+RDMA_KMD_IMAGE = "example.com/amd/ionic-rdma-kmd:1.0"
 KMD_DRIVER = "ionic"
 VALIDATED_LABEL = "amd.feature.node.kubernetes.io/gpu-fabric-validated"
 # Stand-in for the validation image on a CPU-only harness: what validate.py does with its verdict
@@ -250,7 +252,7 @@ async def _scenario(tmp: Path, n_nics: int, mode: str, seed: int, interval: str,
                     flap: bool, validation: str, crash_agent: bool, driver_reload: bool, ha: bool,
                     silent_nics: int = 0, lldp_wait: str = "", duplicate_policy: bool = False,
                     dark_port_s: float = 0.0, host_nics_owned: bool = False, pcie_narrow_nic: int = -1,
-                    xgmi_link_down: bool = False) -> dict:
+                    xgmi_link_down: bool = False, rdma: str = "", flap_burst: int = 0) -> dict:
     from ..api.v1alpha1 import types as T
     from ..operator import kube, manager
     from ..operator.kube import ApiClient, KubeConfig
@@ -278,6 +280,10 @@ async def _scenario(tmp: Path, n_nics: int, mode: str, seed: int, interval: str,
         fakesysfs.set_xgmi_link(tmp / "sys", fx["gpus"][1]["bdf"], 3, False)
     if pcie_narrow_nic >= 0:  # that rail's NIC trained its PCIe link at 16 GT/s x8 (a worn slot)
         fakesysfs.set_pcie_link(tmp / "sys", fakesysfs.nic_pci_dir(tmp / "sys", nic_names[pcie_narrow_nic]).name, 16.0, 8)
+    # rdma: the rails have no RDMA device when the agent starts (ionic without ionic_rdma);
+    # "driver-image": the policy's driverImage loads it (init container); "late": nothing does
+    # until the harness registers the devices, with the agent running.
+    rdma_removed = {nif: fakesysfs.remove_rdma(tmp / "sys", nif) for nif in (nic_names if rdma else [])}
     plan = netns.random_plan(len(nic_names), rng)
     for n in nat.discover(str(tmp / "sys"))["nics"]:  # RoCE v2 GIDs as the RDMA core adds them
         if n["ifname"] in nic_names and n["rdma_dev"]:
@@ -320,13 +326,18 @@ async def _scenario(tmp: Path, n_nics: int, mode: str, seed: int, interval: str,
     # policy keeps the default driver list, so ownership rests on discovery alone.
     kmd = [sys.executable, "-m", "network_operator_amd.testing.fakesysfs", "bind", "mlx5_core" if both else KMD_DRIVER,
            *[n for n in nic_names if n in HOST_NICS]]
+    rdma_kmd = [sys.executable, "-m", "network_operator_amd.testing.fakesysfs", "bind-rdma",
+                *[f"{nif}={dev}@{plan[nic_names.index(nif)]['local']}" for nif, dev in rdma_removed.items()]]
     from ..api.v1alpha1 import types as T0
 
+    overrides = {**({"--wait": lldp_wait} if lldp_wait else {}), **({"--label-holddown": "2s"} if flap_burst else {})}
     node = SimNode(fake, node_name, {"amd.feature.node.kubernetes.io/gpu-ready": "true"}, tmp / "host",
-                   sysfs_root=tmp / "sys", init_images={KMD_IMAGE: kmd},
+                   sysfs_root=tmp / "sys", init_images={KMD_IMAGE: kmd, RDMA_KMD_IMAGE: rdma_kmd},
                    env={"PYTHONPATH": str(Path(__file__).resolve().parents[2])},
                    job_images={T0.DEFAULT_VALIDATION_IMAGE: [sys.executable, "-c", _VALIDATE_STUB, validation or "pass"]},
-                   agent_arg_overrides={**({"--wait": lldp_wait} if lldp_wait else {})} or None)
+                   agent_arg_overrides=overrides or None)
+    if rdma == "driver-image":
+        policy_kw = dict(policy_kw, driverImage=RDMA_KMD_IMAGE)
     if validation and not host_nic:
         policy_kw = dict(policy_kw, validation={"enabled": True, "minBusbw": 300})
     P, DS = kube.NETWORKCLUSTERPOLICIES, kube.DAEMONSETS
@@ -407,6 +418,40 @@ async def _scenario(tmp: Path, n_nics: int, mode: str, seed: int, interval: str,
                 res["policy_status"] = (fake.get_object(P, name) or {}).get("status")
                 res["node_labels"] = node.node_labels()
                 return res
+            if rdma == "late":
+                # No RDMA driver yet: the agent configures the rails and waits, running and
+                # unlabelled; "waiting for RDMA device" is a start-up reason, not an error.  Then
+                # the driver is loaded (the devices appear) and the label follows.
+                seen: dict = {"degraded": [], "errors": [], "reasons": []}
+
+                async def watch_waiting():
+                    while True:
+                        st = (fake.get_object(P, name) or {}).get("status") or {}
+                        for cnd in st.get("conditions") or []:
+                            d = f"{cnd.get('reason')}: {cnd.get('message')}"
+                            if cnd.get("type") == "Degraded" and cnd.get("status") == "True" and d not in seen["degraded"]:
+                                seen["degraded"].append(d)
+                        seen["errors"].extend(e for e in st.get("errors") or [] if e not in seen["errors"])
+                        await asyncio.sleep(0.005)
+                watcher = asyncio.ensure_future(watch_waiting())
+                await asyncio.sleep(3.0)
+                c0 = next(iter(node.containers.values()))
+                pr = subprocess.run(c0.probe, capture_output=True, text=True, timeout=10)
+                res["rdma_wait"] = {"probe": {"rc": pr.returncode, "stdout": pr.stdout.strip()},
+                                    "label": node.node_labels().get(label_key),
+                                    "agent_running": c0.proc is not None and c0.proc.poll() is None,
+                                    "rccl_env": node.host_path("/etc/amd/scale-out/rccl.env").exists(),
+                                    "addrs": {nif: rt.addr_list(rt.link_by_name(nif)["index"]) for nif in nic_names},
+                                    "policy_status": (fake.get_object(P, name) or {}).get("status")}
+                t_bind = time.monotonic()
+                for nif, dev in rdma_removed.items():
+                    fakesysfs.bind_rdma(tmp / "sys", nif, dev, [plan[nic_names.index(nif)]["local"]])
+                t_lab = await _until(lambda: node.node_labels().get(label_key) == "true", 10)
+                watcher.cancel()
+                res["rdma_wait"].update(bind_to_label_s=round(t_lab - t_bind, 6) if t_lab else None,
+                                        degraded_seen=seen["degraded"], errors_seen=seen["errors"],
+                                        policy_events=sorted({e.get("reason") for e in fake.list_objects(kube.EVENTS)
+                                                              if (e.get("involvedObject") or {}).get("kind") == T.KIND}))
             if silent_nics:
                 # A switch port that never sends LLDP: the agent's exit error names the NIC, its
                 # driver and what it heard, and the operator puts that into status.errors.
@@ -627,9 +672,42 @@ async def _scenario(tmp: Path, n_nics: int, mode: str, seed: int, interval: str,
                 res["probe_while_degraded"] = {"rc": pr.returncode, "stdout": pr.stdout.strip()}
                 t2 = time.monotonic()
                 netns.set_switch_port(sw.pid, sw.ports[0], True)
-                t_back = await _until(lambda: node.node_labels().get(label_key) == "true" and all_good(), 10)
+                # (the agent's default --label-holddown, 10 s, delays the republication)
+                t_back = await _until(lambda: node.node_labels().get(label_key) == "true" and all_good(), 30)
                 res["port_down_to_status_degraded_s"] = round(t_deg - t1, 6) if t_deg else None
                 res["port_up_to_all_good_s"] = round(t_back - t2, 6) if t_back else None
+            if flap_burst:
+                # A flapping optic: port 0 goes down and up `flap_burst` times in a row.  With the
+                # agent's label hold-down the node is withdrawn once and republished once, so the
+                # policy goes Degraded once -- not once per flap.
+                edges: dict = {"degraded": [], "label": []}
+
+                async def watch_edges():
+                    was_deg, was_lab = False, True
+                    while True:
+                        st = (fake.get_object(P, name) or {}).get("status") or {}
+                        deg = any(x.get("type") == "Degraded" and x.get("status") == "True" for x in st.get("conditions") or [])
+                        lab = node.node_labels().get(label_key) == "true"
+                        if deg != was_deg:
+                            edges["degraded"].append((round(time.monotonic() - t0, 4), deg))
+                            was_deg = deg
+                        if lab != was_lab:
+                            edges["label"].append((round(time.monotonic() - t0, 4), lab))
+                            was_lab = lab
+                        await asyncio.sleep(0.002)
+                w = asyncio.ensure_future(watch_edges())
+                for _ in range(flap_burst):
+                    netns.set_switch_port(sw.pid, sw.ports[0], False)
+                    await asyncio.sleep(0.25)
+                    netns.set_switch_port(sw.pid, sw.ports[0], True)
+                    await asyncio.sleep(0.25)
+                t_last = time.monotonic()
+                t_back = await _until(lambda: node.node_labels().get(label_key) == "true" and all_good(), 30)
+                await asyncio.sleep(0.5)
+                w.cancel()
+                res["flap_burst"] = {"flaps": flap_burst, "degraded_edges": edges["degraded"], "label_edges": edges["label"],
+                                     "last_flap_to_all_good_s": round(t_back - t_last, 6) if t_back else None,
+                                     "agent_restarts": sum(x.restarts for x in node.containers.values())}
             if update_mtu:
                 # `kubectl edit`: new MTU -> DaemonSet template changes -> the kubelet replaces the
                 # agent -> the new agent configures the NICs again and republishes the label.
@@ -854,7 +932,8 @@ def run_scenario(n_nics: int = 2, mode: str = "L3", seed: int = 1, interval: str
                  crash_agent: bool = False, driver_reload: bool = False, ha: bool = False,
                  silent_nics: int = 0, lldp_wait: str = "", keep_tmp: bool = False,
                  duplicate_policy: bool = False, dark_port_s: float = 0.0, host_nics_owned: bool = False,
-                 pcie_narrow_nic: int = -1, xgmi_link_down: bool = False) -> dict:
+                 pcie_narrow_nic: int = -1, xgmi_link_down: bool = False, rdma: str = "",
+                 flap_burst: int = 0) -> dict:
     """Must already run inside a private user+net namespace (``run_isolated``)."""
     tmp = Path(tempfile.mkdtemp(prefix="netop-e2e-"))
     try:
@@ -862,7 +941,8 @@ def run_scenario(n_nics: int = 2, mode: str = "L3", seed: int = 1, interval: str
                                      dict(policy_kw or {}), update_mtu, config_type, flap, validation,
                                      crash_agent, driver_reload, ha, silent_nics, lldp_wait, duplicate_policy,
                                      dark_port_s=dark_port_s, host_nics_owned=host_nics_owned,
-                                     pcie_narrow_nic=pcie_narrow_nic, xgmi_link_down=xgmi_link_down))
+                                     pcie_narrow_nic=pcie_narrow_nic, xgmi_link_down=xgmi_link_down, rdma=rdma,
+                                     flap_burst=flap_burst))
     finally:
         if not keep_tmp:
             shutil.rmtree(tmp, ignore_errors=True)

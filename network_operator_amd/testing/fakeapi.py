@@ -1030,7 +1030,8 @@ class FakeApiServer:
         if errs:
             raise _Conflict(422, "Invalid", f'{T.KIND} "{obj.get("metadata", {}).get("name")}" is invalid: '
                             + "; ".join(errs), {"causes": [{"message": e} for e in errs]})
-        pruned = CRD.prune(obj, CRD.openapi_schema())
+        schema = CRD.openapi_schema()
+        pruned = CRD.apply_defaults(CRD.prune(obj, schema), schema)
         pruned["metadata"] = obj["metadata"]
         return pruned
 

@@ -228,20 +228,55 @@ def bind_driver(root: Path, ifname: str, driver: str) -> None:
     os.symlink(os.path.relpath(drv, link.parent), link)
 
 
+def remove_rdma(root: Path, ifname: str) -> str:
+    """The NIC's RDMA driver (mlx5_ib, ionic_rdma, bnxt_re) is not loaded: its function has no
+    ``infiniband/`` device.  Returns the device name it had ("" if none)."""
+    import shutil
+
+    ib = nic_pci_dir(root, ifname) / "infiniband"
+    devs = sorted(os.listdir(ib)) if ib.is_dir() else []
+    shutil.rmtree(ib, ignore_errors=True)
+    for d in devs:
+        (Path(root) / "class" / "infiniband" / d).unlink(missing_ok=True)
+    return devs[0] if devs else ""
+
+
+def bind_rdma(root: Path, ifname: str, dev: str, ips=()) -> None:
+    """What loading the NIC's RDMA driver does to sysfs: the function gets its ``infiniband/<dev>``
+    device (and /sys/class/infiniband/<dev>), and the RDMA core fills the port's GID table from the
+    netdev's addresses (RoCE v2 GIDs of `ips`)."""
+    d = nic_pci_dir(root, ifname) / "infiniband" / dev
+    d.mkdir(parents=True, exist_ok=True)
+    _link(d, Path(root) / "class" / "infiniband" / dev)
+    if ips:
+        add_rocev2_gids(root, dev, list(ips))
+
+
 def _main(argv=None) -> int:
-    """``python -m network_operator_amd.testing.fakesysfs bind <driver> <ifname>...`` against
-    $SYSFS_ROOT: the simulated driver container of the end-to-end harness (testing/e2e.py)."""
+    """Against $SYSFS_ROOT, the simulated driver containers of the end-to-end harness
+    (testing/e2e.py):
+
+    * ``bind <driver> <ifname>...``: the NIC kernel driver binds the functions (host-nic KMD);
+    * ``bind-rdma <ifname>=<rdma-dev>[@<ipv4>] ...``: the NICs' RDMA driver registers their RDMA
+      devices (amd-so ``driverImage``)."""
     import argparse
 
     ap = argparse.ArgumentParser()
-    ap.add_argument("op", choices=["bind"])
-    ap.add_argument("driver")
-    ap.add_argument("ifnames", nargs="+")
+    ap.add_argument("op", choices=["bind", "bind-rdma"])
+    ap.add_argument("args", nargs="+")
     a = ap.parse_args(argv)
     root = Path(os.environ["SYSFS_ROOT"])
-    for i in a.ifnames:
-        bind_driver(root, i, a.driver)
-    print(f"bound {', '.join(a.ifnames)} to {a.driver}")
+    if a.op == "bind":
+        driver, ifnames = a.args[0], a.args[1:]
+        for i in ifnames:
+            bind_driver(root, i, driver)
+        print(f"bound {', '.join(ifnames)} to {driver}")
+        return 0
+    for spec in a.args:
+        ifname, rest = spec.split("=", 1)
+        dev, _, ip = rest.partition("@")
+        bind_rdma(root, ifname, dev, [ip] if ip else [])
+    print(f"registered RDMA devices for {', '.join(x.split('=')[0] for x in a.args)}")
     return 0
 
 

@@ -320,7 +320,10 @@ def run_scenario(n_nics: int = 8, mode: str = "L3", seed: int | None = None, int
                  dark_port_up_after: float | None = None, kill_mid_config: int = 0, rail_driver: str = "",
                  xgmi_down_at_start: tuple | None = None, xgmi_up_after: float | None = None,
                  xgmi_link_flap: tuple | None = None, pcie_degraded: dict | None = None,
-                 link_state: bool = True, pcie_flap: int | None = None) -> dict:
+                 link_state: bool = True, pcie_flap: int | None = None, rails_without_rdma: int = 0,
+                 rdma_bind_after: float | None = None, label_holddown: str | None = None,
+                 flap_burst: tuple | None = None, gpu_metrics_stall: bool = False,
+                 sysfs_read_timeout: str = "") -> dict:
     """Runs one node bring-up.  Must already be inside a private user+net namespace.
 
     nm_bus: run the agent with --disable-networkmanager against a real ``dbus-daemon`` on which a
@@ -350,7 +353,20 @@ def run_scenario(n_nics: int = 8, mode: str = "L3", seed: int | None = None, int
     pcie_flap: after readiness that rail's NIC retrains its PCIe link at 16 GT/s x8, then back.
 
     pcie_degraded: {NIC index (an int, or its str after JSON): (GT/s, width)} -- that rail's NIC trained its PCIe link below the
-    maximum (32 GT/s x16); {"gpu<i>": (GT/s, width)} the same for GPU i."""
+    maximum (32 GT/s x16); {"gpu<i>": (GT/s, width)} the same for GPU i.
+
+    rails_without_rdma: the first k rails' NICs have no RDMA device (their RDMA driver is not
+    loaded) when the agent starts; with rdma_bind_after, the devices (and their GIDs) appear that
+    many seconds after the agent started, and the reasons and files meanwhile are kept ("rdma").
+
+    label_holddown: the agent's --label-holddown (default: "0s" for the scenarios that time a
+    republication, else the agent's own).  flap_burst: (switch port, count, period s) -- after
+    readiness that port flaps `count` times, one period each; every label transition is recorded.
+
+    gpu_metrics_stall: after readiness GPU 0's gpu_metrics becomes a FIFO nobody writes (a wedged
+    SMU: the read never returns) and switch port 0 then loses carrier: how fast the label goes
+    while the read is stalled, and what the agent says once the read times out
+    (sysfs_read_timeout, the agent's --sysfs-read-timeout)."""
     from . import fakesysfs
 
     nat = _native()
@@ -373,6 +389,7 @@ def run_scenario(n_nics: int = 8, mode: str = "L3", seed: int | None = None, int
             fakesysfs.set_xgmi_link(tmp / "sys", fx["gpus"][xgmi_down_at_start[0]]["bdf"], xgmi_down_at_start[1], False)
         pairs = nat.discover(str(tmp / "sys"))["pairs"]
         nic_names = [p["nic"] for p in pairs][:n_nics]
+        rdma_removed = {nif: fakesysfs.remove_rdma(tmp / "sys", nif) for nif in nic_names[:rails_without_rdma]}
         plan = random_plan(len(nic_names), rng)
         for nif, mbps in zip(nic_names, nic_speeds_mbps or []):  # what the NIC driver negotiated
             (tmp / "sys" / "class" / "net" / nif / "speed").write_text(f"{mbps}\n")
@@ -423,6 +440,13 @@ def run_scenario(n_nics: int = 8, mode: str = "L3", seed: int | None = None, int
                 f"--systemd-networkd={tmp / 'networkd'}", f"-v={verbose}", *(extra_args or [])]
         if link_state:  # as the operator passes it (off: an agent build older than the flag, bench/agent_ab.py)
             args.append(f"--link-state={tmp / 'link-state'}")
+        if label_holddown is None and (flap_port is not None or soak_cycles or xgmi_link_flap is not None
+                                       or pcie_flap is not None or gpu_metrics_stall):
+            label_holddown = "0s"  # these time the republication itself
+        if label_holddown is not None:
+            args.append(f"--label-holddown={label_holddown}")
+        if sysfs_read_timeout:
+            args.append(f"--sysfs-read-timeout={sysfs_read_timeout}")
         if lldp_cache:
             args.append(f"--lldp-cache={tmp / 'lldp-cache'}")
         env = dict(os.environ, SYSFS_ROOT=str(tmp / "sys"), NODE_NAME="mi355x-node-0")
@@ -526,6 +550,31 @@ def run_scenario(n_nics: int = 8, mode: str = "L3", seed: int | None = None, int
             set_switch_port(pid, sw_ports[dark_port], True)
             t_ready = _wait_for(label, 10, agent)
             dark["port_up_to_label_s"] = (t_ready - t_up) if t_ready else None
+        elif rails_without_rdma and rdma_bind_after is not None:
+            # The rails' RDMA driver is loaded while the agent runs (a driver container, the node):
+            # until then the agent configures, stays up unlabelled and says why; then it labels.
+            reason, seen, env_seen = tmp / "status.json.not-ready", [], False
+            while time.monotonic() < t0 + rdma_bind_after and agent.poll() is None:
+                try:
+                    why = reason.read_text()
+                    if why and why not in seen:
+                        seen.append(why)
+                except OSError:
+                    pass
+                env_seen |= (tmp / "rccl.env").exists()
+                time.sleep(0.02)
+            dark["reasons_seen"], dark["label_while_missing"] = seen, label.exists()
+            dark["rccl_env_while_missing"], dark["running_while_missing"] = env_seen, agent.poll() is None
+            try:
+                st = json.loads((tmp / "status.json").read_text())
+                dark["configured_while_missing"] = [i["name"] for i in st["interfaces"] if i.get("configured")]
+            except (OSError, ValueError, KeyError):
+                dark["configured_while_missing"] = None
+            t_bind = time.monotonic()
+            for nif, dev in rdma_removed.items():
+                fakesysfs.bind_rdma(tmp / "sys", nif, dev, [plan[nic_names.index(nif)]["local"]])
+            t_ready = _wait_for(label, 10, agent)
+            dark["bind_to_label_s"] = (t_ready - t_bind) if t_ready else None
         elif xgmi_down_at_start is not None and xgmi_up_after is not None:
             reason, seen = tmp / "status.json.not-ready", []
             while time.monotonic() < t0 + xgmi_up_after and agent.poll() is None:
@@ -695,6 +744,128 @@ def run_scenario(n_nics: int = 8, mode: str = "L3", seed: int | None = None, int
             back = _wait_for(label, 10, agent)
             res["pcie_flap"] = {"withdraw_s": (gone - t_down) if gone else None,
                                 "restore_s": (back - t_up) if back else None, "reason": why}
+        if flap_burst is not None and t_ready:
+            # A flapping optic: the port goes down and up `count` times.  Every label transition
+            # is recorded (polled every 0.5 ms); with a hold-down the label goes once and comes back
+            # once, hold-down seconds after the last flap.
+            import threading
+
+            port, count, period = int(flap_burst[0]), int(flap_burst[1]), float(flap_burst[2])
+            time.sleep(0.05)  # status.json follows the label
+            edges, done = [], threading.Event()
+
+            def watch():
+                was = label.exists()
+                while not done.is_set():
+                    now = label.exists()
+                    if now != was:
+                        edges.append((time.monotonic(), now))
+                        was = now
+                    time.sleep(0.0005)
+            w = threading.Thread(target=watch)
+            w.start()
+            t_first = time.monotonic()
+            reasons = []
+            for _ in range(count):
+                set_switch_port(pid, sw_ports[port], False)
+                time.sleep(period / 2)
+                set_switch_port(pid, sw_ports[port], True)
+                t_last_up = time.monotonic()
+                time.sleep(period / 2)
+                try:
+                    reasons.append((tmp / "status.json.not-ready").read_text())
+                except OSError:
+                    pass
+            back = None
+            end = t_last_up + 30
+            while time.monotonic() < end and agent.poll() is None:
+                if edges and edges[-1][1]:
+                    back = edges[-1][0]
+                    break
+                time.sleep(0.005)
+            done.set()
+            w.join()
+            res["flap_burst"] = {"flaps": count, "burst_s": t_last_up - t_first,
+                                 "withdrawals": sum(1 for _, up in edges if not up),
+                                 "publishes": sum(1 for _, up in edges if up),
+                                 "last_up_to_label_s": (back - t_last_up) if back else None,
+                                 "reasons": sorted(set(reasons))}
+            try:
+                res["flap_burst"]["metrics_status"] = json.loads((tmp / "status.json").read_text()).get("ready")
+            except (OSError, ValueError):
+                pass
+        if gpu_metrics_stall and t_ready:
+            # A wedged SMU: GPU 0's gpu_metrics read never returns (a FIFO nobody writes).  The
+            # monitor must keep handling link events at once; once the read times out it names the
+            # GPU and withholds the label; when the SMU answers again, the label comes back.
+            bdf = fx["gpus"][0]["bdf"]
+            gm = tmp / "sys" / "bus" / "pci" / "devices" / bdf / "gpu_metrics"
+            blob = gm.read_bytes()
+            time.sleep(0.05)
+
+            def withdraw_after_carrier_loss(port):
+                # Timed from the carrier loss: set_switch_port returns once the switch end is down
+                # (its netns hop, a fork, costs a few ms and is not the agent's).
+                set_switch_port(pid, sw_ports[port], False)
+                t = time.monotonic()
+                while time.monotonic() < t + 10 and agent.poll() is None:
+                    if not label.exists():
+                        return time.monotonic() - t
+                    time.sleep(0.0002)
+                return None
+
+            def flaps(n):  # carrier losses, each withdrawal timed; the port back up, the label back
+                out = []
+                for k in range(n):
+                    out.append(withdraw_after_carrier_loss(k % 2))
+                    set_switch_port(pid, sw_ports[k % 2], True)
+                    _wait_for(label, 5, agent)
+                    time.sleep(0.02)
+                return out
+            base = flaps(5)  # the same, with no read stalled
+            gm.unlink()
+            os.mkfifo(gm)
+            t_stall = time.monotonic()
+            time.sleep(0.3)  # several --xgmi-health-interval periods: a read is stuck by now
+            during = flaps(5)  # all within the read timeout: the label is still up before each
+            flaps_done = time.monotonic() - t_stall
+            reason = tmp / "status.json.not-ready"
+            t_why, why = None, None
+            while time.monotonic() < t_stall + 30 and agent.poll() is None:
+                try:
+                    why = reason.read_text()
+                    if "did not answer" in why:
+                        t_why = time.monotonic()
+                        break
+                except OSError:
+                    pass
+                time.sleep(0.01)
+            gone = _wait_gone(label, 1.0)  # the label follows the reason (write_status goes first)
+
+            def med(xs):
+                xs = [x for x in xs if x is not None]
+                return _pct(xs, 0.5) if xs else None
+            stall = {"withdraw_during_stall_s": during, "withdraw_during_stall_p50_s": med(during),
+                     "withdraw_without_stall_s": base, "withdraw_without_stall_p50_s": med(base),
+                     "flaps_done_s": flaps_done, "reason": why,
+                     "stall_to_reason_s": (t_why - t_stall) if t_why else None, "label_while_stalled": not gone}
+            # The SMU answers again: the blocked read gets its data, the file is a file again.
+            try:  # ENXIO when no read is blocked on it
+                fd = os.open(gm, os.O_WRONLY | os.O_NONBLOCK)
+            except OSError:
+                fd = -1
+            if fd >= 0:
+                try:
+                    os.write(fd, blob)
+                finally:
+                    os.close(fd)
+            tmpf = gm.with_name("gpu_metrics.tmp")
+            tmpf.write_bytes(blob)
+            tmpf.replace(gm)
+            t_ans = time.monotonic()
+            back = _wait_for(label, 15, agent)
+            stall["answer_to_label_s"] = (back - t_ans) if back else None
+            res["gpu_metrics_stall"] = stall
         if soak_cycles and t_ready:
             # Carrier loss on a random port, over and over, with the agent in monitor mode: every
             # cycle must withdraw and restore the label, and the agent must not leak descriptors,
@@ -967,6 +1138,15 @@ def run_isolated(timeout: float = 300, **kw) -> dict:
     if r.returncode != 0:
         raise RuntimeError(f"scenario failed rc={r.returncode}: {r.stderr[-3000:]}")
     return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+def _wait_gone(path: Path, timeout: float) -> bool:
+    end = time.monotonic() + timeout
+    while time.monotonic() < end:
+        if not path.exists():
+            return True
+        time.sleep(0.0005)
+    return not path.exists()
 
 
 def _pct(xs, q):

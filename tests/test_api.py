@@ -259,3 +259,49 @@ def test_lldp_cache_field_passed_to_the_agent_in_l3_only():
     l2 = T.new_policy("p", lldpCache=True, layer="L2")
     assert "--lldp-cache" not in " ".join(agent_args(l2))
     assert CRD2.validate(dict(p, spec=dict(p["spec"], amdScaleOut={"lldpCache": "yes"})))
+
+
+@pytest.mark.parametrize("resource", ["networkclusterpolicies", "networkclusterpolicy"])
+def test_a_minimal_amd_so_policy_verifies_the_xgmi_mesh_and_rdma_by_default(tmp_path, resource):
+    """MI355X-first defaults: a policy written with kubectl as just a type and a
+    selector -- no amdScaleOut at all -- comes back with xgmiCheck and requireRdma true, from the
+    real webhook server (plural registration) and, with the webhooks never called (the singular),
+    from the CRD schema's defaults alone; its DaemonSet's agent checks the mesh and the RDMA devices."""
+    from network_operator_amd import discovery
+    from network_operator_amd.operator import kube
+    from network_operator_amd.operator.kube import ApiClient, KubeConfig
+    from network_operator_amd.operator.metrics import OperatorMetrics
+    from network_operator_amd.operator.servers import Servers, generate_self_signed
+    from network_operator_amd.operator.templates import update_daemonset_for
+    from network_operator_amd.testing.fakeapi import FakeApiServer
+
+    crt, _ = generate_self_signed(tmp_path / "certs")
+    minimal = {"apiVersion": T.API_VERSION, "kind": T.KIND, "metadata": {"name": "minimal"},
+               "spec": {"configurationType": "amd-so", "nodeSelector": {"amd.feature.node.kubernetes.io/gpu-ready": "true"}}}
+
+    async def body():
+        fake = FakeApiServer()
+        url = await fake.start()
+        srv = Servers(OperatorMetrics())
+        await srv.start(probe_addr="127.0.0.1:0", webhook_port=0, cert_dir=str(tmp_path / "certs"))
+        wurl = f"https://127.0.0.1:{srv.ports['webhook']}"
+        async with ApiClient(KubeConfig(host=url)) as c:
+            await c.create(kube.MUTATINGWEBHOOKS, _webhook_config("Mutating", wurl, crt.read_bytes(), resource))
+            await c.create(kube.VALIDATINGWEBHOOKS, _webhook_config("Validating", wurl, crt.read_bytes(), resource))
+            created = await c.create(kube.NETWORKCLUSTERPOLICIES, copy.deepcopy(minimal))
+        await srv.stop()
+        await fake.stop()
+        return created
+
+    created = asyncio.run(asyncio.wait_for(body(), 60))
+    so = created["spec"]["amdScaleOut"]
+    assert so["xgmiCheck"] is True and so["requireRdma"] is True, so
+    ds = discovery.discovery_daemonset()
+    update_daemonset_for(ds, T.NetworkClusterPolicy.from_dict(created), "amd-network-operator")
+    args = ds["spec"]["template"]["spec"]["containers"][0]["args"]
+    assert "--xgmi-expect=0" in args and "--require-rdma" in args, args
+    # Turned off explicitly, they stay off (the defaults fill only what is absent).
+    off = copy.deepcopy(minimal)
+    off["spec"]["amdScaleOut"] = {"xgmiCheck": False, "requireRdma": False}
+    CRD.apply_defaults(off, CRD.openapi_schema())
+    assert off["spec"]["amdScaleOut"] == {"xgmiCheck": False, "requireRdma": False}

@@ -146,6 +146,9 @@ def test_link_failure_is_reported_by_the_policy_and_recovers():
         r["node_events_after_flap"]
     assert any(c["type"] == "Degraded" and c["status"] == "True" for c in st["conditions"])
     assert r["port_up_to_all_good_s"] is not None, r["agent_log"]
+    # The label comes back after the agent's default hold-down (--label-holddown 10 s): a port
+    # that flaps again within it does not toggle the node's scheduling eligibility.
+    assert 10.0 <= r["port_up_to_all_good_s"] < 16.0, r["port_up_to_all_good_s"]
     # kubectl describe pod: "Readiness probe failed: not ready: <nic>: link down"
     assert r["probe_while_degraded"] == {"rc": 1, "stdout": f"not ready: {r['nics'][0]}: link down"}
 
@@ -336,3 +339,46 @@ def test_an_xgmi_link_down_reaches_the_policy_and_the_node_without_restarts():
                for e in r["node_events"]), r["node_events"]
     assert r["agent_restarts"] == 0
     assert "amd.feature.node.kubernetes.io/gpu-scale-out" not in r["node_labels"]
+
+
+def test_amd_so_driver_image_loads_the_rdma_driver_before_the_agent_labels_the_node():
+    """the Pollara case.  The rails' NICs have no RDMA device until their RDMA driver
+    is loaded; the policy's driverImage does that as a privileged init container, so the agent
+    finds the devices at once: labelled, every rail's HCA in rccl.env, no restart."""
+    r = e2e.run_isolated(n_nics=2, mode="L3", seed=61, rdma="driver-image", teardown=False)
+    assert r["policy_to_all_good_s"] is not None, (r["policy_status"], r["agent_log"])
+    assert [x["name"] for x in r["init_runs"]] == ["nic-driver"] and r["init_runs"][0]["rc"] == 0, r["init_runs"]
+    assert "--require-rdma" in r["agent_argv"] and "--xgmi-expect=0" in r["agent_argv"], r["agent_argv"]
+    hca = [l for l in r["rccl_env"].splitlines() if l.startswith("NCCL_IB_HCA=")]
+    assert len(hca) == 1 and hca[0].count("mlx5_") == 2, r["rccl_env"]
+    assert r["policy_status"]["errors"] == []
+
+
+def test_a_node_waiting_for_rdma_devices_is_starting_not_degraded_and_labels_when_they_appear():
+    """without a driver container the agent configures the rails and waits, running
+    and unlabelled; its probe says "waiting for RDMA device", a start-up reason (no Degraded, no
+    status error).  Once the RDMA driver registers the devices, the label follows within a second,
+    without an agent restart."""
+    r = e2e.run_isolated(n_nics=2, mode="L3", seed=62, rdma="late", teardown=False)
+    w = r["rdma_wait"]
+    assert w["agent_running"] and w["label"] is None and not w["rccl_env"], w
+    assert w["probe"]["rc"] != 0 and w["probe"]["stdout"].count("waiting for RDMA device") == 2, w["probe"]
+    assert all(len(a) == 1 for a in w["addrs"].values()), w["addrs"]  # configured meanwhile
+    assert w["degraded_seen"] == [], w
+    assert not {"NodeDegraded", "AgentFailed"} & set(w["policy_events"]), w["policy_events"]
+    assert any("waiting for RDMA device" in e for e in w["errors_seen"]), w["errors_seen"]  # starting, named
+    assert not any("no RDMA device" in e for e in w["errors_seen"]), w["errors_seen"]
+    assert w["bind_to_label_s"] is not None and w["bind_to_label_s"] < 1.0, w
+    assert r["policy_to_all_good_s"] is not None, (r["policy_status"], r["agent_log"])
+    assert r["agent_started_s"] and len(r["agent_started_s"]) == 1, r["agent_started_s"]
+
+
+def test_a_flapping_port_makes_one_degraded_transition_not_ten():
+    """ten carrier flaps in five seconds.  The agent withdraws the label at the
+    first and republishes it once, its hold-down after the last; the policy goes Degraded once and
+    back to All good once."""
+    r = e2e.run_isolated(n_nics=2, mode="L3", seed=63, flap_burst=10, teardown=False)
+    f = r["flap_burst"]
+    assert [up for _, up in f["degraded_edges"]] == [True, False], f
+    assert [up for _, up in f["label_edges"]] == [False, True], f
+    assert f["last_flap_to_all_good_s"] is not None and f["agent_restarts"] == 0, f

@@ -432,7 +432,8 @@ _AMD_VALUES = {
     "metricsPort": 9501, "gpuDirectRdma": "DmaBuf", "rcclEnv": {"NCCL_IB_TC": "106"}, "railTableBase": 100,
     "rcclSocketIfname": "eno1", "lldpCache": True, "verifyPeers": True, "lldpWait": "2m", "carrierWait": "45s",
     "keepConfigOnRestart": True, "railSwitchPattern": "leaf-r{rail}-.*", "minLinkSpeedGbps": 400, "requireFullPcieLink": True,
-    "checkPeerMtu": False, "handDcbxToHost": True, "maxUnavailable": "25%",
+    "checkPeerMtu": False, "handDcbxToHost": True, "maxUnavailable": "25%", "requireRdma": True, "rdmaWait": "7m",
+    "driverImage": "reg/rdma-kmd:1",
     "validation": {"enabled": True, "minBusbw": 300, "minLink": 40, "gpus": 4, "image": "reg/val:1"},
     "tolerations": [{"key": "amd.com/gpu", "operator": "Exists", "effect": "NoSchedule"}],
     "priorityClassName": "system-node-critical",
@@ -484,7 +485,9 @@ def test_every_policy_field_is_settable_from_the_chart_and_documented():
     assert not hn.extra
 
     # (carrierWait is an L2 setting; these values are an L3 policy)
-    assert [w for w in W.validate_create(seeded["netconf-amd-scale-out"]) if "carrierWait" not in w] == []
+    # (and the pinned agent tag 9.9 draws the older-agent warning)
+    assert [w for w in W.validate_create(seeded["netconf-amd-scale-out"])
+            if "carrierWait" not in w and "pins agent tag '9.9'" not in w] == []
     # (includeGpuRails next to interfaces only draws the "no effect" warning)
     assert [w for w in W.validate_create(seeded["netconf-amd-host-nic"])
             if "includeGpuRails" not in w and "carrierWait" not in w] == []

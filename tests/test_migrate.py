@@ -62,13 +62,15 @@ def test_a_gaudi_policy_becomes_an_amd_so_policy_that_is_admitted():
         "metadata": {"name": "netconf-gaudi-scale-out-l3", "labels": {"team": "infra"},
                      "annotations": {"owner": "platform"}},
         "spec": {"configurationType": "amd-so",
-                 "amdScaleOut": {"disableNetworkManager": True, "layer": "L3", "pullPolicy": "IfNotPresent", "mtu": 8000},
+                 "amdScaleOut": {"disableNetworkManager": True, "layer": "L3", "pullPolicy": "IfNotPresent", "mtu": 8000,
+                                 "xgmiCheck": True, "requireRdma": True},
                  "nodeSelector": {"amd.feature.node.kubernetes.io/gpu-ready": "true", "rack": "a"},
                  "logLevel": 1}}]
     text = "\n".join(notes)
     assert "is the Gaudi agent -> amd/amd-network-linkdiscovery" in text
     assert "gaudi-ready -> amd.feature.node.kubernetes.io/gpu-ready" in text
     assert "last-applied-configuration" in text and "gpu-scale-out=true" in text and "rccl.env" in text
+    assert "xgmiCheck and requireRdma set true" in text
     assert M.admission_errors(objs[0]) == []
     # An explicit image wins; a non-Gaudi image is kept, with a note to check it.
     objs, notes, _ = M.convert_policies(GAUDI_L3, image="reg/agent:2")

@@ -403,3 +403,47 @@ def test_node_report_names_what_would_keep_the_label_off(tmp_path):
     assert rep["problems"] == [f"{victim['ifname']}: no RDMA device (load its RDMA driver)",
                                f"{rail0['nic']}: PCIe link 16.0 GT/s x8 of 32.0 GT/s x16",
                                f"GPU {fx['gpus'][1]['bdf']}: xGMI link(s) 2 down"], rep["problems"]
+
+
+def test_a_gpu_metrics_read_that_never_returns_neither_hangs_the_start_nor_hides_the_reason(native, tmp_path):
+    """every start-path sysfs join has a deadline.  GPU 2's gpu_metrics is a FIFO
+    nobody writes (a wedged SMU: the read never returns).  The dry run ends after
+    --sysfs-read-timeout, names the GPU in status.json and its log, and the other GPUs' links are
+    still read (concurrently)."""
+    import time
+
+    fakesysfs.build_mi355x_node(tmp_path / "sys", n_gpus=8)
+    bdfs = sorted(g["bdf"] for g in native.discover(str(tmp_path / "sys"))["gpus"])
+    gm = tmp_path / "sys" / "bus" / "pci" / "devices" / bdfs[2] / "gpu_metrics"
+    gm.unlink()
+    os.mkfifo(gm)
+    status = tmp_path / "status.json"
+    t0 = time.monotonic()
+    r = subprocess.run([str(native_bin("discover")), "--dry-run", "--xgmi-expect=0", "--sysfs-read-timeout=1s",
+                        f"--status-file={status}"], capture_output=True, text=True, timeout=30,
+                       env=dict(os.environ, SYSFS_ROOT=str(tmp_path / "sys")))
+    took = time.monotonic() - t0
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert took < 5, took
+    st = json.loads(status.read_text())
+    assert st["xgmi_error"] == f"gpu_metrics of {bdfs[2]} did not answer in 1s", st
+    assert st["xgmi_links"] == "49 up, 0 down on 7 GPUs, x16 at 38 Gb/s (gpu_metrics)", st
+    assert f"a real start would fail: xGMI: gpu_metrics of {bdfs[2]} did not answer in 1s" in r.stderr
+
+
+def test_a_pollara_node_without_ionic_rdma_would_wait_for_rdma_devices(native, tmp_path):
+    """VERDICT r5 #1, the box's case (profiles/r5_agent_dry_run_box_ionic.json): every rail is an
+    ionic NIC without an RDMA device.  With --require-rdma (what the operator passes by default)
+    the dry run says a real start would wait for RDMA devices on all 8 rails."""
+    fx = fakesysfs.build_mi355x_node(tmp_path / "sys", n_gpus=8, rail_driver="ionic")
+    rails = [p["nic"] for p in native.discover(str(tmp_path / "sys"))["pairs"]]
+    for nif in rails:
+        fakesysfs.remove_rdma(tmp_path / "sys", nif)
+    status = tmp_path / "status.json"
+    r = subprocess.run([str(native_bin("discover")), "--dry-run", "--require-rdma", "--xgmi-expect=0",
+                        f"--status-file={status}"], capture_output=True, text=True, timeout=30,
+                       env=dict(os.environ, SYSFS_ROOT=str(tmp_path / "sys")))
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "dry run: a real start would wait for RDMA devices on 8 rails" in r.stderr, r.stderr[-2000:]
+    assert sorted(json.loads(status.read_text())["nics_without_rdma"].split(",")) == sorted(rails)
+    assert fx["nics"]

@@ -638,3 +638,53 @@ def test_a_rail_whose_pcie_link_trained_narrow_is_reported_and_with_require_full
     assert f["withdraw_s"] is not None and f["withdraw_s"] < 3.0, f
     assert f["reason"] and "its PCIe link trained at 16.0 GT/s x8 of 32.0 GT/s x16" in f["reason"], f
     assert f["restore_s"] is not None and f["restore_s"] < 3.0, f
+
+
+def test_rails_without_rdma_devices_stay_unlabelled_until_the_rdma_driver_loads():
+    """scale-out ready means RDMA ready.  Rails whose NIC has no RDMA device (the
+    Pollara boxes of this pool: ionic without ionic_rdma) are configured, but the agent keeps the
+    label and rccl.env back and says "waiting for RDMA device" (a start-up reason).  When the RDMA
+    driver registers the devices (fakesysfs bind), the label follows within a second and rccl.env
+    names every rail's HCA."""
+    r = netns.run_isolated(n_nics=4, seed=51, interval="30s", fast_start=True, rail_driver="ionic",
+                           rails_without_rdma=4, rdma_bind_after=2.0, extra_args=["--require-rdma"])
+    d = r["dark"]
+    assert d["running_while_missing"] and not d["label_while_missing"] and not d["rccl_env_while_missing"], d
+    assert sorted(d["configured_while_missing"]) == sorted(r["nics"]), d
+    want = "; ".join(f"{n}: waiting for RDMA device" for n in r["nics"]) + "\n"
+    assert want in d["reasons_seen"], d["reasons_seen"]
+    assert d["bind_to_label_s"] is not None and d["bind_to_label_s"] < 1.0, d
+    _check_configured(r, rdma_prefix="ionic_")
+    hca = [l for l in r["rccl_env"].splitlines() if l.startswith("NCCL_IB_HCA=")]
+    assert len(hca) == 1 and hca[0].count("ionic_") == 4, r["rccl_env"]
+    # Without --require-rdma (requireRdma: false): the reference's behaviour, labelled at once.
+    r = netns.run_isolated(n_nics=2, seed=52, interval="30s", fast_start=True, rail_driver="ionic", rails_without_rdma=2)
+    assert r["ready"] and "NCCL_IB_HCA" not in r["rccl_env"], r["rccl_env"]
+
+
+def test_a_flapping_port_withdraws_the_label_once_and_republishes_it_after_the_holddown():
+    """ten flaps in five seconds withdraw the label once; it comes back once, the
+    hold-down after the last flap (not ten withdrawals and republications)."""
+    r = netns.run_isolated(n_nics=2, seed=53, interval="30s", fast_start=True, label_holddown="2s",
+                           flap_burst=(0, 10, 0.5))
+    assert r["ready"]
+    f = r["flap_burst"]
+    assert f["withdrawals"] == 1 and f["publishes"] == 1, f
+    assert 2.0 <= f["last_up_to_label_s"] < 3.0, f
+    assert any("label hold-down" in x or "link down" in x for x in f["reasons"]), f
+
+
+def test_a_stalled_gpu_metrics_read_neither_holds_back_link_events_nor_hides_its_reason():
+    """the monitor reads gpu_metrics on a worker.  While GPU 0's read is stalled (a
+    FIFO nobody writes: a wedged SMU), carrier losses still withdraw the label within milliseconds,
+    as fast as with no read stalled; once the read times out the reason names the GPU and the
+    label stays off; when the SMU answers again the label comes back."""
+    r = netns.run_isolated(n_nics=2, seed=54, interval="30s", fast_start=True, gpu_metrics_stall=True,
+                           sysfs_read_timeout="3s", extra_args=["--xgmi-health-interval=100ms"])
+    assert r["ready"]
+    s = r["gpu_metrics_stall"]
+    assert None not in s["withdraw_during_stall_s"] and s["withdraw_during_stall_p50_s"] < 0.010, s
+    assert s["stall_to_reason_s"] is not None and s["stall_to_reason_s"] > s["flaps_done_s"], s  # stalled throughout
+    assert s["reason"] and "gpu_metrics of 0000:0a:00.0 did not answer in 3s" in s["reason"], s
+    assert not s["label_while_stalled"], s
+    assert s["answer_to_label_s"] is not None and s["answer_to_label_s"] < 3.0, s

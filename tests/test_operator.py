@@ -100,6 +100,10 @@ async def edit(client, name, change, attempts=20):
     raise AssertionError(f"edit of {name} kept conflicting")
 
 
+# The CRD's (and the mutating webhook's) MI355X-first defaults: xgmiCheck and requireRdma on.
+MI355X_DEFAULTS = ["--xgmi-expect=0", "--require-rdma"]
+
+
 def policy(name="policy", layer="L3", **so):
     p = T.new_policy(name, layer=layer, node_selector={"foo": "bar"}, **so)
     return p.to_dict()
@@ -125,8 +129,8 @@ def test_reconcile_lifecycle_reference_parity():
                 assert len(c) == 1 and c[0]["image"] == "amd/my-linkdiscovery:latest"
                 assert c[0]["args"] == ["--configure=true", "--keep-running", "--mode=L3", "--mtu=8000", "--wait=90s",
                                         "--rccl-net=/host/etc/amd/scale-out/rccl-net.json",
-                                        "--rccl-env=/host/etc/amd/scale-out/rccl.env", *TOPO_ARGS, LINK_STATE_ARG,
-                                        STATUS_ARG]
+                                        "--rccl-env=/host/etc/amd/scale-out/rccl.env", *TOPO_ARGS, *MI355X_DEFAULTS,
+                                        LINK_STATE_ARG, STATUS_ARG]
                 assert [v["name"] for v in pod["volumes"]] == ["nfd-features", "agent-run", "rccl-artifacts"]
                 assert [m["name"] for m in c[0]["volumeMounts"]] == ["nfd-features", "agent-run", "rccl-artifacts"]
                 assert pod["nodeSelector"] == {"foo": "bar"}
@@ -147,8 +151,8 @@ def test_reconcile_lifecycle_reference_parity():
                 ds = fake.get_object(kube.DAEMONSETS, "policy", NS)
                 c = ds["spec"]["template"]["spec"]["containers"][0]
                 assert c["args"] == ["--configure=true", "--keep-running", "--mode=L2",
-                                     "--rccl-env=/host/etc/amd/scale-out/rccl.env", *TOPO_ARGS, LINK_STATE_ARG,
-                                     STATUS_ARG]
+                                     "--rccl-env=/host/etc/amd/scale-out/rccl.env", *TOPO_ARGS, *MI355X_DEFAULTS,
+                                     LINK_STATE_ARG, STATUS_ARG]
                 assert [v["name"] for v in ds["spec"]["template"]["spec"]["volumes"]] == ["nfd-features", "agent-run",
                                                                                           "rccl-artifacts"]
             await eventually(l2_ok)
@@ -311,8 +315,17 @@ def test_agent_args_mi355x_options():
     p = T.new_policy("x", layer="L3", xgmiCheck=True, lldpAnnounce=False, interfaces=["ens1", "ens2"],
                      nicDrivers=["mlx5_core"])
     a = agent_args(p)
-    assert a[-6:] == ["--xgmi-expect=0", "--lldp-announce=false", "--interfaces=ens1,ens2", "--nic-drivers=mlx5_core",
-                      LINK_STATE_ARG, STATUS_ARG]
+    assert a[-7:] == ["--xgmi-expect=0", "--require-rdma", "--lldp-announce=false", "--interfaces=ens1,ens2",
+                      "--nic-drivers=mlx5_core", LINK_STATE_ARG, STATUS_ARG]
+
+
+def test_xgmi_check_and_require_rdma_are_on_unless_the_policy_turns_them_off():
+    """MI355X-first: unset means on -- a policy stored before the fields
+    existed, or written without them, still verifies the mesh and waits for RDMA devices."""
+    assert "--xgmi-expect=0" in agent_args(T.new_policy("x")) and "--require-rdma" in agent_args(T.new_policy("x"))
+    off = agent_args(T.new_policy("x", xgmiCheck=False, requireRdma=False, rdmaWait="10m"))
+    assert not any(a.startswith(("--xgmi-expect", "--require-rdma", "--rdma-wait")) for a in off), off
+    assert "--rdma-wait=10m" in agent_args(T.new_policy("x", rdmaWait="10m"))
 
 
 def test_leader_election_single_active_and_failover():
