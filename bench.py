@@ -456,6 +456,7 @@ def _line(args, world: int, st: dict) -> dict:
         "xgmi_allreduce": st.get("xgmi_allreduce"),
         "xgmi_allreduce_multiprocess": st.get("xgmi_comm"),
         "node_ready": st.get("node_ready"),
+        "node_ready_unavailable": st.get("node_ready_unavailable"),
         "node_ready_gpu_side": st.get("gpu_side"),
         "xgmi_traffic": st.get("xgmi_traffic"),
         "deadline_s": args.deadline_s,
@@ -776,7 +777,10 @@ def main(argv=None) -> int:
             else:  # node_ready
                 res = runner.extra(name, 150, n_nics=world, runs=args.node_ready_runs, required=args.node_ready == "on")
                 if "unavailable" in res:
-                    st["node_ready_note"] = f"node-ready harness unavailable: {res['unavailable']}"
+                    u = res["unavailable"]
+                    st["node_ready_note"] = f"node-ready harness unavailable: {u['why']}" if isinstance(u, dict) \
+                        else f"node-ready harness unavailable: {u}"
+                    st["node_ready_unavailable"] = u
                     res = None
                 elif "result" in res:
                     res = res["result"]

@@ -104,14 +104,40 @@ int netop_ipc_export(const void* ptr, void* handle, uint64_t* offset) {
 
 int netop_ipc_handle_size() { return int(sizeof(hipIpcMemHandle_t)); }
 
+// The PCI bus id ("0000:0d:00.0") of the GPU whose memory `ptr` is: what an exporter publishes
+// beside its handle, so the importer can check peer access to that GPU before mapping.
+int netop_ipc_device_bus_id(const void* ptr, char* out, int len) {
+    if (!ptr || !out || len < 13) return int(hipErrorInvalidValue);
+    hipPointerAttribute_t a{};
+    hipError_t e = hipPointerGetAttributes(&a, ptr);
+    if (e != hipSuccess) return int(e);
+    return int(hipDeviceGetPCIBusId(out, len, a.device));
+}
+
 // Maps a peer's exported allocation into this process (peer access enabled lazily) and
 // returns the address of the exported pointer (*base is what netop_ipc_close needs).
-int netop_ipc_open(const void* handle, uint64_t offset, void** ptr, void** base) {
-    if (!handle || !ptr || !base) return int(hipErrorInvalidValue);
+// `peer_bus_id` names the exporter's GPU: like the single-process probe (netop_hip.hip), nothing
+// is mapped unless this process's GPU can access it -- the exporter's GPU not visible here, or a
+// pair without peer access, is refused with hipErrorPeerAccessUnsupported before any kernel could
+// read across it (a pull over a pair without peer access faults the GPU and may reset the node).
+int netop_ipc_open(const void* handle, uint64_t offset, const char* peer_bus_id, void** ptr, void** base) {
+    if (!handle || !ptr || !base || !peer_bus_id) return int(hipErrorInvalidValue);
+    int cur = 0, peer = -1;
+    hipError_t e = hipGetDevice(&cur);
+    if (e != hipSuccess) return int(e);
+    if (hipDeviceGetByPCIBusId(&peer, peer_bus_id) != hipSuccess || peer < 0) {
+        (void)hipGetLastError();  // the lookup's error is the refusal below, not a sticky one
+        return int(hipErrorPeerAccessUnsupported);
+    }
+    if (peer != cur) {
+        int can = 0;
+        if ((e = hipDeviceCanAccessPeer(&can, cur, peer)) != hipSuccess) return int(e);
+        if (!can) return int(hipErrorPeerAccessUnsupported);
+    }
     hipIpcMemHandle_t h;
     std::memcpy(&h, handle, sizeof h);
     void* b = nullptr;
-    hipError_t e = hipIpcOpenMemHandle(&b, h, hipIpcMemLazyEnablePeerAccess);
+    e = hipIpcOpenMemHandle(&b, h, hipIpcMemLazyEnablePeerAccess);
     if (e != hipSuccess) return int(e);
     *base = b;
     *ptr = static_cast<char*>(b) + offset;

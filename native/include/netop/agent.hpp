@@ -225,6 +225,10 @@ struct Config {
     // freed by the node, a driver loaded late); it then exits so its restart configures the NIC.
     // 0 = never.
     int64_t rediscover_ns = 30LL * 1000000000;
+    // A NIC with a default route in a per-NIC policy-routing table that also holds the node's own
+    // address (not a /30, or the source its rule selects) is refused like an uplink; this takes
+    // it anyway (a rail whose site routing the operator knows to be its own).
+    bool allow_policy_routed = false;
 };
 
 // Where the agent leaves the one-line reason the node is not ready (beside --status-file), and
@@ -462,6 +466,7 @@ class Agent {
     topo::XgmiReport xgmi_;
     std::vector<topo::XgmiLinkHealth> xgmi_health_;
     std::string xgmi_error_;  // what the last gpu_metrics read found wrong (empty: fine or not read)
+    std::string xgmi_unread_;  // why no GPU's link state could be decoded (an unknown gpu_metrics layout)
     // `min_down`: consecutive samples a link must have been seen down (xgmi_down_streak_).
     std::string xgmi_health_problem(int min_down = 1) const;
     void note_xgmi_sample();  // updates xgmi_down_streak_ from xgmi_health_

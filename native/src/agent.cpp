@@ -483,6 +483,17 @@ void Agent::finish_xgmi_health() {
         }
     }
     if (gpus) NLOG_I("xGMI links: %d up on %d GPU(s) (gpu_metrics)", up, gpus);
+    xgmi_unread_.clear();
+    if (!gpus && !xgmi_health_.empty() &&
+        std::none_of(xgmi_health_.begin(), xgmi_health_.end(), [](const topo::XgmiLinkHealth& h) { return h.late; })) {
+        // No GPU's gpu_metrics layout is one this agent decodes (other firmware): the links'
+        // trained state is not checked, and not watched (said once, at warning level,
+        // and in status.json, instead of only at -v=1).  The KFD mesh check still runs.
+        std::set<std::string> why;
+        for (const auto& h : xgmi_health_) why.insert(h.error);
+        xgmi_unread_ = join(std::vector<std::string>(why.begin(), why.end()), "; ");
+        NLOG_W("xGMI link state not checked on any of the %zu GPU(s): %s", xgmi_health_.size(), xgmi_unread_.c_str());
+    }
     if (xgmi_error_.empty()) return;
     if (cfg_.dry_run) {
         NLOG_W("dry run: a real start would fail: xGMI: %s", xgmi_error_.c_str());

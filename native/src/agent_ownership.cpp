@@ -211,42 +211,89 @@ void Agent::refuse_uplinks() {
     // cut the kubelet off the cluster: never, in any mode, whoever named the NIC.
     // A NIC under the uplink (a bond port, the parent of a VLAN) counts: changing its MTU or
     // bouncing it moves the device on top.
-    std::vector<std::string> bad, named;
-    std::vector<std::string> vias;
+    std::vector<std::string> bad;   // refused NICs
+    std::vector<std::string> why;   // per refused NIC: what it carries ("the node's default route via bond0")
     for (const auto& n : nics_) {
         if (auto via = uplink_path(n.link)) {
             bad.push_back(n.ifname);
-            vias.push_back(*via);
-            named.push_back(n.ifname + *via);
+            why.push_back("the node's default route" + *via);
         }
     }
-    if (bad.empty()) {
-        // A default route in a per-NIC policy-routing table ("from <its subnet> lookup 101") is
-        // the site's source routing for that NIC, not the node's way out: configure the NIC, but
-        // say that the route goes with the addresses it depends on.
-        std::vector<std::pair<int, uint32_t>> policy;
+    const size_t uplinks = bad.size();
+    // A default route in a per-NIC policy-routing table ("from <its subnet> lookup 101") is the
+    // site's source routing for that NIC, not the node's way out through the main table.  But a
+    // NIC that routes that way *and* holds the node's own address -- one the agent never installs
+    // (not a /30), or the source the rule selects -- is how the node reaches some network (a
+    // source-routed management or storage NIC): flushing it can cut the node off just as well
+    // (ADVICE r5).  Refused like an uplink, unless --allow-policy-routed; a rail whose policy
+    // table only serves the agent's own /30 is configured, with a warning.
+    std::vector<std::pair<int, uint32_t>> policy;
+    try {
+        policy = ops_.policy_default_routes();
+    } catch (const std::exception&) {
+    }
+    std::vector<nl::RuleSpec> rules;
+    if (!policy.empty()) {
         try {
-            policy = ops_.policy_default_routes();
+            rules = ops_.rule_list();
         } catch (const std::exception&) {
         }
-        for (const auto& [ifindex, table] : policy)
-            for (const auto& n : nics_)
-                if (n.link.index == ifindex)
-                    NLOG_W("Interface '%s' has a default route in routing table %u, which only selective rules reach "
-                           "(policy routing): not the node's uplink; it depends on the addresses the agent replaces",
-                           n.ifname.c_str(), table);
-        return;
     }
-    const std::string what = join(named, ", ");
+    for (const auto& [ifindex, table] : policy) {
+        for (const auto& n : nics_) {
+            if (n.link.index != ifindex || std::find(bad.begin(), bad.end(), n.ifname) != bad.end()) continue;
+            std::string owned;
+            std::vector<nl::AddrInfo> addrs;
+            try {
+                addrs = ops_.addr_list(ifindex, AF_INET);
+            } catch (const std::exception&) {
+            }
+            for (const auto& a : addrs) {
+                for (const auto& r : rules)
+                    if (r.table == table && r.selective && r.src.len > 0 && r.src.contains(a.local)) {
+                        owned = strfmt("%s, the source its rule 'from %s lookup %u' selects", a.prefix().str().c_str(),
+                                       r.src.masked().str().c_str(), table);
+                        break;
+                    }
+                if (owned.empty() && a.prefixlen != 30)
+                    owned = a.prefix().str() + ", an address the agent never installs (not a /30)";
+                if (!owned.empty()) break;
+            }
+            if (owned.empty() || cfg_.allow_policy_routed) {
+                NLOG_W("Interface '%s' has a default route in routing table %u, which only selective rules reach "
+                       "(policy routing): not the node's uplink; it depends on the addresses the agent replaces%s",
+                       n.ifname.c_str(), table, owned.empty() ? "" : (" (--allow-policy-routed; it holds " + owned + ")").c_str());
+                continue;
+            }
+            bad.push_back(n.ifname);
+            why.push_back(strfmt("a default route in policy-routing table %u and the node's address %s", table, owned.c_str()));
+        }
+    }
+    if (bad.empty()) return;
+    // Uplinks keep the reference-era wording ("ens0 via bond0: the node's default route leaves
+    // through it"); policy-routed NICs say what they hold.
+    std::vector<std::string> up_named, pol_named;
+    for (size_t i = 0; i < bad.size(); ++i) {
+        if (i < uplinks)
+            up_named.push_back(bad[i] + why[i].substr(std::string("the node's default route").size()));
+        else
+            pol_named.push_back(bad[i] + " (" + why[i] + ")");
+    }
+    std::string what;
+    if (!up_named.empty()) what = join(up_named, ", ") + ": the node's default route leaves through it";
+    if (!pol_named.empty())
+        what += (what.empty() ? "" : "; ") + join(pol_named, ", ") + ": the node reaches a network through it";
     if (cfg_.dry_run) {
-        NLOG_W("dry run: would refuse to configure %s: the node's default route leaves through it", what.c_str());
-        for (size_t i = 0; i < bad.size(); ++i)
-            excluded_.emplace_back(bad[i], "carries the node's default route" + vias[i] + " (refused)");
+        NLOG_W("dry run: would refuse to configure %s", what.c_str());
+        for (size_t i = 0; i < bad.size(); ++i) excluded_.emplace_back(bad[i], "carries " + why[i] + " (refused)");
         return;
     }
     throw AgentError("Refusing to configure " + what +
-                     ": the node's default route leaves through it (flushing its addresses or changing its MTU could "
-                     "cut the node off the network).  Select only scale-out / host RDMA NICs in the policy");
+                     " (flushing its addresses or changing its MTU could cut the node off the network).  Select only "
+                     "scale-out / host RDMA NICs in the policy" +
+                     (pol_named.empty() ? std::string()
+                                        : std::string(" (a NIC whose policy-routing table is only its own rail's: "
+                                                      "--allow-policy-routed)")));
 }
 
 }  // namespace netop::agent

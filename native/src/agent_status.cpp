@@ -50,6 +50,8 @@ std::map<std::string, std::string> Agent::status_node() const {
         }
         if (gpus)
             m["xgmi_links"] = strfmt("%d up, %d down on %d GPUs, x%d at %d Gb/s (gpu_metrics)", up, down, gpus, width, speed);
+        else if (!xgmi_unread_.empty())
+            m["xgmi_links"] = "not checked: " + xgmi_unread_;
         if (!xgmi_error_.empty()) m["xgmi_error"] = xgmi_error_;
     }
     if (!no_rdma_.empty()) m["nics_without_rdma"] = join(no_rdma_, ",");

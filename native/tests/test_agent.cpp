@@ -3125,3 +3125,68 @@ TEST(agent_label_holddown_republishes_once_after_the_last_flap) {
     CHECK(a.render_metrics().find("netop_agent_label_suppressed_total 9\n") != std::string::npos);
     CHECK(a.render_metrics().find("netop_agent_label_withdrawals_total 1\n") != std::string::npos);
 }
+
+TEST(agent_refuses_a_policy_routed_nic_that_holds_the_nodes_own_address) {
+    // a NIC whose default route sits in a per-NIC policy-routing table is not the main
+    // table's uplink -- but when it also holds the node's own address (the source its rule selects,
+    // or any non-/30 the agent never installs) it is how the node reaches that network (a
+    // source-routed management or storage NIC), and flushing it could cut the node off.  Refused,
+    // naming the table and the address, unless --allow-policy-routed; a rail whose policy table
+    // only serves a /30 of the agent's is configured.
+    auto rule = [](uint32_t table, uint32_t prio, const char* src) {
+        nl::RuleSpec r;
+        r.table = table;
+        r.priority = prio;
+        if (src) {
+            r.src = *Ipv4Prefix::parse(src);
+            r.selective = true;
+        }
+        return r;
+    };
+    for (int variant : {0, 1, 2}) {
+        Fixture f;
+        f.cfg.mode = "L3";
+        f.cfg.keep_running = false;
+        f.cfg.allow_policy_routed = variant == 1;
+        f.ops.rules = {rule(RT_TABLE_LOCAL, 0, nullptr), rule(101, 100, "192.168.1.0/24"),
+                       rule(RT_TABLE_MAIN, 32766, nullptr), rule(RT_TABLE_DEFAULT, 32767, nullptr)};
+        auto def = route(11, "0.0.0.0/0", "192.168.1.1", RTPROT_STATIC);
+        def.table = 101;
+        f.ops.routes.push_back(def);
+        // variant 2: the agent's own /30 from an earlier run (not in the rule's source)
+        f.ops.addr_add(11, *Ipv4Prefix::parse(variant == 2 ? "10.200.0.5/30" : "192.168.1.5/24"));
+        std::string err;
+        try {
+            agent::Agent a(f.cfg, f.ops, f.all_valid(), f.nm());
+            a.run(-1);
+        } catch (const agent::AgentError& e) {
+            err = e.what();
+        }
+        if (variant == 0) {
+            CHECK(err.find("Refusing to configure ens1 (a default route in policy-routing table 101 and the node's address "
+                           "192.168.1.5/24, the source its rule 'from 192.168.1.0/24 lookup 101' selects): the node "
+                           "reaches a network through it") == 0);
+            CHECK(err.find("--allow-policy-routed") != std::string::npos);
+            CHECK_EQ(f.ops.calls["link_set_up"], 0);
+            CHECK_EQ(f.ops.addrs.size(), size_t(1));  // its address untouched
+        } else {
+            CHECK_EQ(err, std::string());
+            CHECK_EQ(f.ops.addrs.size(), size_t(3));  // every NIC configured, ens1 too
+        }
+    }
+    // A dry run names it as refused.
+    Fixture f;
+    f.cfg.mode = "L3";
+    f.cfg.dry_run = true;
+    f.ops.rules = {rule(101, 100, "192.168.1.0/24"), rule(RT_TABLE_MAIN, 32766, nullptr)};
+    auto def = route(11, "0.0.0.0/0", "192.168.1.1", RTPROT_STATIC);
+    def.table = 101;
+    f.ops.routes.push_back(def);
+    f.ops.addr_add(11, *Ipv4Prefix::parse("172.16.9.3/16"));  // not the rule's source, but no /30 either
+    agent::Agent a(f.cfg, f.ops, f.all_valid(), f.nm());
+    a.run(-1);
+    CHECK_EQ(a.excluded().size(), size_t(1));
+    CHECK_EQ(a.excluded()[0].second, std::string("carries a default route in policy-routing table 101 and the node's "
+                                                 "address 172.16.9.3/16, an address the agent never installs (not a "
+                                                 "/30) (refused)"));
+}

@@ -75,6 +75,7 @@ int main(int argc, char** argv) {
     fs.add_duration("sysfs-read-timeout", &cfg.sysfs_read_timeout_ns, "bound on each sysfs read firmware or hardware answers (gpu_metrics: an SMU query per GPU; PCIe link state; the KFD topology): a read still blocked then is reported and the label follows the policy, the start and the monitor never wait behind it");
     fs.add_duration("label-holddown", &cfg.label_holddown_ns, "with the monitor: after the readiness label was withdrawn, republish it only once the node has been healthy this long without a flap (0 = at once; the first publication is never delayed)");
     fs.add_int("xgmi-down-samples", &cfg.xgmi_down_samples, "with the monitor: consecutive gpu_metrics samples that must see an xGMI link down before it counts (a status read during a GPU reset is not a flap)");
+    fs.add_bool("allow-policy-routed", &cfg.allow_policy_routed, "configure a NIC that has a default route in a per-NIC policy-routing table even when it holds the node's own address (not a /30, or the source its rule selects); by default such a NIC is refused like the node's uplink");
     fs.add_bool("require-rdma", &cfg.require_rdma, "every scale-out NIC must have an RDMA device (its RDMA driver loaded) before the readiness label and rccl.env: the NICs are configured, the probe says 'waiting for RDMA device', and the monitor labels the node once the devices appear");
     fs.add_duration("rdma-wait", &cfg.rdma_wait_ns, "with --require-rdma: how long after the start a missing RDMA device is 'waiting' (start-up) before it is reported as the fault 'no RDMA device (load its RDMA driver)'");
     fs.add_duration("rdma-poll-interval", &cfg.rdma_poll_ns, "with --require-rdma: how often the waiting agent looks for the RDMA devices", true);

@@ -88,6 +88,7 @@ class LeaderElector:
         self.transitions = 0
         self.lost_at: Optional[float] = None  # loop time at which leadership was given up
         self.stop_latency: Optional[float] = None  # seconds from lost_at until the work had ended
+        self.work_stopped = True  # the leader's work ended within STOP_BUDGET_S of the stop
 
     def _lease_body(self, prev: Optional[dict]) -> dict:
         spec_prev = (prev or {}).get("spec", {}) or {}
@@ -207,8 +208,10 @@ class LeaderElector:
             # 1. the work (and with it every reconcile worker) ends first ...
             work.cancel()
             done, _ = await asyncio.wait({work}, timeout=STOP_BUDGET_S)
+            self.work_stopped = bool(done)
             if not done:
-                log.error("the leader's work did not stop within %.1fs of losing the lease", STOP_BUDGET_S)
+                log.error("the leader's work did not stop within %.1fs of losing the lease: the lease is not "
+                          "released, a standby takes it only once it has expired", STOP_BUDGET_S)
             elif not work.cancelled() and work.exception() is not None:
                 log.info("leader's work ended with %r", work.exception())
             if on_stopped_leading:
@@ -216,6 +219,9 @@ class LeaderElector:
             if self.lost_at is not None:
                 self.stop_latency = self._loop_time() - self.lost_at
                 log.info("stopped leading %.3fs after the renew deadline", self.stop_latency)
-            # 2. ... and only then is the lease handed back (one bounded attempt).
-            if self.release_on_cancel:
+            # 2. ... and only then is the lease handed back (one bounded attempt).  Work still
+            # running (a worker that swallowed its cancellation) may still write: then the lease
+            # is left to expire on its own (lease_duration), so the margin unsafe_timings() checks
+            # between this replica's writes and a standby's still holds.
+            if self.release_on_cancel and self.work_stopped:
                 await self.release()

@@ -18,7 +18,6 @@ import json
 import logging
 import os
 import ssl
-import subprocess
 import time
 from pathlib import Path
 from typing import Callable, Dict, List, Optional, Tuple
@@ -27,7 +26,7 @@ from aiohttp import web
 
 from ..api.v1alpha1 import types as T
 from ..api.v1alpha1 import webhook as W
-from . import kube
+from . import kube, selfsigned
 from .kube import ApiClient
 from .metrics import OperatorMetrics
 
@@ -37,13 +36,37 @@ TLS_CIPHERS = "ECDHE-RSA-AES256-GCM-SHA384:ECDHE-ECDSA-AES256-GCM-SHA384"
 DEFAULT_CERT_DIR = "/tmp/k8s-webhook-server/serving-certs"
 
 
-def server_tls_context(cert_file: str, key_file: str) -> ssl.SSLContext:
+def _tls_context() -> ssl.SSLContext:
+    """TLS 1.2 only, two ciphers, HTTP/1.1 (reference cmd/operator/main.go:122-147)."""
     ctx = ssl.SSLContext(ssl.PROTOCOL_TLS_SERVER)
     ctx.minimum_version = ssl.TLSVersion.TLSv1_2
     ctx.maximum_version = ssl.TLSVersion.TLSv1_2
     ctx.set_ciphers(TLS_CIPHERS)
     ctx.set_alpn_protocols(["http/1.1"])
+    return ctx
+
+
+def server_tls_context(cert_file: str, key_file: str) -> ssl.SSLContext:
+    ctx = _tls_context()
     ctx.load_cert_chain(cert_file, key_file)
+    return ctx
+
+
+def self_signed_tls_context(cn: str = "amd-network-operator-metrics",
+                            sans=("DNS:localhost", "IP:127.0.0.1")) -> ssl.SSLContext:
+    """A serving context with a certificate made in memory (selfsigned.py), as controller-runtime
+    self-signs the metrics certificate when none is mounted (reference cmd/operator/main.go:157-167).
+    Nothing touches the filesystem (the operator's root filesystem is read-only): the PEM pair goes
+    through an anonymous memfd that ``load_cert_chain`` reads by its /proc path."""
+    ctx = _tls_context()
+    cert, key = selfsigned.make_certificate(cn, sans)
+    pem = (selfsigned.pem("CERTIFICATE", cert) + selfsigned.pem("EC PRIVATE KEY", key)).encode()
+    fd = os.memfd_create("netop-self-signed", os.MFD_CLOEXEC)
+    try:
+        os.write(fd, pem)
+        ctx.load_cert_chain(f"/proc/self/fd/{fd}")
+    finally:
+        os.close(fd)
     return ctx
 
 
@@ -98,13 +121,9 @@ class CertWatcher:
 
 
 def generate_self_signed(cert_dir: Path, cn: str = "localhost", sans=("DNS:localhost", "IP:127.0.0.1")) -> Tuple[Path, Path]:
-    """Self-signed serving certificate (tests / local runs; in clusters cert-manager issues it)."""
-    cert_dir.mkdir(parents=True, exist_ok=True)
-    crt, key = cert_dir / "tls.crt", cert_dir / "tls.key"
-    subprocess.run(["openssl", "req", "-x509", "-newkey", "rsa:2048", "-nodes", "-keyout", str(key), "-out", str(crt),
-                    "-days", "2", "-subj", f"/CN={cn}", "-addext", "subjectAltName=" + ",".join(sans)],
-                   check=True, capture_output=True)
-    return crt, key
+    """Self-signed serving certificate files tls.crt / tls.key (tests / local runs; in clusters
+    cert-manager issues it).  Made in process (selfsigned.py): no openssl binary needed."""
+    return selfsigned.write_self_signed(Path(cert_dir), cn, sans, days=2)
 
 
 def parse_bind(addr: str) -> Optional[Tuple[str, int]]:
@@ -249,9 +268,13 @@ class Servers:
             ctx = None
             if metrics_secure:
                 cd = Path(cert_dir)
-                if not (cd / "tls.crt").exists():
-                    generate_self_signed(cd)  # controller-runtime also self-signs the metrics cert
-                ctx = server_tls_context(str(cd / "tls.crt"), str(cd / "tls.key"))
+                if (cd / "tls.crt").exists() and (cd / "tls.key").exists():
+                    ctx = server_tls_context(str(cd / "tls.crt"), str(cd / "tls.key"))
+                else:
+                    # controller-runtime self-signs the metrics certificate too; the watcher below
+                    # switches to a mounted pair as soon as one appears.
+                    log.info("no serving certificate in %s: /metrics uses a self-signed one made in memory", cd)
+                    ctx = self_signed_tls_context()
                 self._watch(ctx, cd)
             await self._serve("metrics", self.metrics_app(metrics_secure), *b, ssl_ctx=ctx)
         if webhook_port is not None:

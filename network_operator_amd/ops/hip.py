@@ -52,7 +52,9 @@ def lib() -> ctypes.CDLL:
             L.netop_ipc_handle_size.restype = i32
             L.netop_ipc_export.argtypes = [vp, vp, ctypes.POINTER(u64)]
             L.netop_ipc_export.restype = i32
-            L.netop_ipc_open.argtypes = [vp, u64, ctypes.POINTER(vp), ctypes.POINTER(vp)]
+            L.netop_ipc_device_bus_id.argtypes = [vp, ctypes.c_char_p, i32]
+            L.netop_ipc_device_bus_id.restype = i32
+            L.netop_ipc_open.argtypes = [vp, u64, ctypes.c_char_p, ctypes.POINTER(vp), ctypes.POINTER(vp)]
             L.netop_ipc_open.restype = i32
             L.netop_ipc_close.argtypes = [vp]
             L.netop_ipc_close.restype = i32

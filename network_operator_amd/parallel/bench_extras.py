@@ -215,10 +215,10 @@ def xgmi_comm(world: int, nbytes: int) -> dict:
 def node_ready(n_nics: int, runs: int, required: bool = False) -> dict:
     from ..testing import netns
 
-    ok, why = netns.available()
-    if not ok:
+    why = netns.unavailable()  # structured: {"code", "why"}, never scraped from a child's last line
+    if why is not None:
         if required:
-            raise RuntimeError(why)
+            raise RuntimeError(why["why"])
         return {"unavailable": why}
     return {"result": netns.node_ready_bench(n_nics=max(n_nics, 1), runs=runs, legacy=False)}
 

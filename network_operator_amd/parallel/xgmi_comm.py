@@ -133,8 +133,11 @@ class XgmiAllReduce:
             off = ctypes.c_uint64()
             H._check(L.netop_ipc_export(ctypes.c_void_p(t.data_ptr()), h, ctypes.byref(off)), "netop_ipc_export")
             mine.append((h.raw, off.value))
+        # The exporter's GPU, so every importer checks peer access to it before mapping.
+        bus = ctypes.create_string_buffer(32)
+        H._check(L.netop_ipc_device_bus_id(ctypes.c_void_p(self.inp.data_ptr()), bus, 32), "netop_ipc_device_bus_id")
         allh: List[Optional[list]] = [None] * self.world
-        dist.all_gather_object(allh, mine, group=group)
+        dist.all_gather_object(allh, {"bus_id": bus.value, "handles": mine}, group=group)
         self._opened: List[int] = []
         self.peer_in: List[int] = []
         self.peer_out: List[int] = []
@@ -147,10 +150,11 @@ class XgmiAllReduce:
                 # Small buffers can share one caching-allocator segment, i.e. one IPC handle:
                 # map each distinct handle once and address both buffers inside it.
                 bases = {}
-                for (raw, off), dst in zip(allh[p], (self.peer_in, self.peer_out)):
+                for (raw, off), dst in zip(allh[p]["handles"], (self.peer_in, self.peer_out)):
                     if raw not in bases:
                         ptr, base = ctypes.c_void_p(), ctypes.c_void_p()
-                        H._check(L.netop_ipc_open(raw, 0, ctypes.byref(ptr), ctypes.byref(base)), "netop_ipc_open")
+                        H._check(L.netop_ipc_open(raw, 0, allh[p]["bus_id"], ctypes.byref(ptr), ctypes.byref(base)),
+                                 f"netop_ipc_open (rank {p}'s GPU {allh[p]['bus_id'].decode()})")
                         self._opened.append(base.value)
                         bases[raw] = base.value
                     dst.append(bases[raw] + off)

@@ -47,19 +47,44 @@ def unshare_cmd() -> list[str]:
     return ["unshare", "-n"] if os.geteuid() == 0 else ["unshare", "-rn"]
 
 
-def available() -> tuple[bool, str]:
-    """True when a private network namespace with AF_PACKET sockets can be created."""
+def unavailable() -> dict | None:
+    """None when a private network namespace with AF_PACKET and netlink sockets can be made; else
+    ``{"code": ..., "why": ...}``.  The reason is taken from what failed, never from whatever a
+    process happened to print last: a child under a profiler (rocprofv3's preloaded tool logs at
+    exit) or any other wrapper adds lines of its own.
+
+    codes: ``no-unshare`` (util-linux missing), ``unshare`` (the kernel refused the namespace:
+    no user namespaces, a container without CAP_SYS_ADMIN), ``sockets`` (namespace made, but no
+    AF_PACKET / netlink socket in it), ``timeout``, ``spawn``."""
     if not shutil.which("unshare"):
-        return False, "unshare(1) not installed"
-    probe = ("import socket; s=socket.socket(socket.AF_PACKET, socket.SOCK_RAW, 0); "
-             "n=socket.socket(socket.AF_NETLINK, socket.SOCK_RAW, 0); print('ok')")
+        return {"code": "no-unshare", "why": "unshare(1) not installed"}
+    probe = ("import socket\n"
+             "try:\n"
+             " socket.socket(socket.AF_PACKET, socket.SOCK_RAW, 0); socket.socket(socket.AF_NETLINK, socket.SOCK_RAW, 0)\n"
+             "except OSError as e:\n"
+             " print('NETOP-PROBE sockets ' + str(e)); raise SystemExit(3)\n"
+             "print('NETOP-PROBE ok')")
     try:
         r = subprocess.run([*unshare_cmd(), sys.executable, "-c", probe], capture_output=True, text=True, timeout=60)
-    except Exception as e:  # pragma: no cover
-        return False, f"unshare failed: {e}"
-    if r.returncode != 0 or "ok" not in r.stdout:
-        return False, (r.stderr.strip().splitlines() or ["unshare -rn failed"])[-1]
-    return True, "ok"
+    except subprocess.TimeoutExpired:
+        return {"code": "timeout", "why": "unshare: the probe did not finish in 60 s"}
+    except OSError as e:  # pragma: no cover
+        return {"code": "spawn", "why": f"unshare: {e}"}
+    marks = [ln.split(" ", 2)[1:] for ln in r.stdout.splitlines() if ln.startswith("NETOP-PROBE ")]
+    if r.returncode == 0 and ["ok"] in marks:
+        return None
+    for m in marks:
+        if m and m[0] == "sockets":
+            return {"code": "sockets", "why": "no AF_PACKET / netlink socket in the namespace: " + (m[1] if len(m) > 1 else "")}
+    # unshare(1) itself failed: its own message ("unshare: unshare failed: Operation not permitted").
+    own = [ln.strip() for ln in r.stderr.splitlines() if ln.strip().startswith("unshare:")]
+    return {"code": "unshare", "why": own[0] if own else f"unshare exited with status {r.returncode}"}
+
+
+def available() -> tuple[bool, str]:
+    """True when a private network namespace with AF_PACKET sockets can be created; else why not."""
+    u = unavailable()
+    return (True, "ok") if u is None else (False, u["why"])
 
 
 # ---------------------------------------------------------------------------
@@ -980,10 +1005,28 @@ def run_policy_routing_uplink() -> dict:
                                capture_output=True, text=True, timeout=30)
             res[name] = {"rc": r.returncode, "stderr": r.stderr[-2000:],
                          "status": json.loads(st.read_text()) if st.exists() else None}
+        # rail0 holds 192.168.50.10/24, the source its rule selects: the node reaches 192.168.50/24
+        # through it: refused unless --allow-policy-routed.
         r = subprocess.run([*base, "--configure=true", "--interfaces=rail0", "--carrier-wait=2s"], env=env,
                            capture_output=True, text=True, timeout=30)
+        res["configure_rail_refused"] = {"rc": r.returncode, "stderr": r.stderr[-3000:],
+                                         "mtu": rt.link_by_name("rail0")["mtu"], "addrs": rt.addr_list(rail)}
+        r = subprocess.run([*base, "--configure=true", "--interfaces=rail0", "--carrier-wait=2s", "--allow-policy-routed"],
+                           env=env, capture_output=True, text=True, timeout=30)
         res["configure_rail"] = {"rc": r.returncode, "stderr": r.stderr[-3000:],
                                  "mtu": rt.link_by_name("rail0")["mtu"]}
+        # rail1: its own policy table serves only a /30 of the agent's (an earlier --keep-config
+        # run): configured without the opt-in, with the warning.
+        rt.veth_add("rail1", "rpeer1")
+        rt.link_set_up(rt.link_by_name("rpeer1")["index"])
+        r1 = rt.link_by_name("rail1")["index"]
+        rt.link_set_up(r1)
+        rt.addr_add(r1, "10.77.1.1/30")
+        rt.rule_add("10.99.0.0/16", 1002, 1001)
+        rt.route_append("0.0.0.0/0", "10.77.1.2", r1, 4, table=1002)
+        r = subprocess.run([*base, "--configure=true", "--interfaces=rail1", "--carrier-wait=2s"], env=env,
+                           capture_output=True, text=True, timeout=30)
+        res["configure_own_rail"] = {"rc": r.returncode, "stderr": r.stderr[-3000:], "mtu": rt.link_by_name("rail1")["mtu"]}
         r = subprocess.run([*base, "--configure=true", "--interfaces=mgmt0"], env=env, capture_output=True, text=True,
                            timeout=30)
         res["configure_mgmt"] = {"rc": r.returncode, "stderr": r.stderr[-2000:], "mtu": rt.link_by_name("mgmt0")["mtu"],

@@ -313,3 +313,25 @@ def test_topo_tool_on_this_node():
     out = Path(os.environ.get("GRAFT_REPO_ROOT", ".")) / "gpurun_out"
     if out.is_dir():
         (out / "netop_topo_box.json").write_text(json.dumps(j, indent=1))
+
+
+@pytest.mark.gpu
+def test_require_rdma_dry_run_on_this_node_names_every_rail_without_an_rdma_device(tmp_path):
+    """VERDICT r5 #1 on the box: with --require-rdma (the operator's default), a dry run says which
+    rails a real start would wait for -- on this pool's Pollara boxes all 8 (ionic, no
+    ionic_rdma) -- and, where every rail has its device, nothing.  The bounded gpu_metrics reads
+    (--sysfs-read-timeout) answer within the timeout on a healthy SMU."""
+    status = tmp_path / "status.json"
+    r = subprocess.run([str(native_bin("discover")), "--dry-run", "--require-rdma", "--mode=L3", "--xgmi-expect=0",
+                        "--sysfs-read-timeout=5s", f"--status-file={status}", "-v=1"],
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr[-3000:]
+    st = json.loads(status.read_text())
+    bare = sorted(filter(None, st.get("nics_without_rdma", "").split(",")))
+    waits = re.findall(r"a real start would wait for RDMA devices on (\d+) rails?", r.stderr)
+    assert (waits == [str(len(bare))]) if bare else not waits, (waits, bare, r.stderr[-2000:])
+    assert "did not answer" not in st.get("xgmi_error", ""), st
+    out = Path(os.environ.get("GRAFT_REPO_ROOT", ".")) / "gpurun_out"
+    if out.is_dir():
+        (out / "agent_dry_run_require_rdma_box.json").write_text(json.dumps(
+            {"status": st, "waits_for": waits, "log_tail": r.stderr[-4000:]}, indent=1))

@@ -447,3 +447,24 @@ def test_a_pollara_node_without_ionic_rdma_would_wait_for_rdma_devices(native, t
     assert "dry run: a real start would wait for RDMA devices on 8 rails" in r.stderr, r.stderr[-2000:]
     assert sorted(json.loads(status.read_text())["nics_without_rdma"].split(",")) == sorted(rails)
     assert fx["nics"]
+
+
+def test_an_unknown_gpu_metrics_layout_is_said_once_and_in_the_status(native, tmp_path):
+    """gpu_metrics layouts other than 1.8 (other firmware) are not decoded.  The agent
+    says so at warning level and in status.json's xgmi_links, not only at -v=1; the KFD mesh check
+    still runs and passes."""
+    fakesysfs.build_mi355x_node(tmp_path / "sys", n_gpus=2)
+    for g in native.discover(str(tmp_path / "sys"))["gpus"]:
+        f = tmp_path / "sys" / "bus" / "pci" / "devices" / g["bdf"] / "gpu_metrics"
+        b = bytearray(f.read_bytes())
+        b[3] = 9  # content revision 1.9
+        f.write_bytes(bytes(b))
+    status = tmp_path / "status.json"
+    r = subprocess.run([str(native_bin("discover")), "--dry-run", "--xgmi-expect=0", f"--status-file={status}"],
+                       capture_output=True, text=True, timeout=60, env=dict(os.environ, SYSFS_ROOT=str(tmp_path / "sys")))
+    assert r.returncode == 0, r.stderr[-2000:]
+    st = json.loads(status.read_text())
+    assert st["xgmi_links"] == ("not checked: gpu_metrics 1.9 is not a layout this agent reads (1.8): xGMI link state "
+                                "not checked"), st
+    assert st["xgmi_pairs"] == "1/1" and "xgmi_error" not in st
+    assert r.stderr.count("xGMI link state not checked on any of the 2 GPU(s)") == 1, r.stderr[-2000:]

@@ -499,16 +499,26 @@ def test_host_nic_policy_with_nothing_of_its_own_idles_with_one_reason():
 
 def test_per_nic_policy_routing_default_is_not_the_node_uplink():
     """a default route in a per-NIC source-routing table (reached only by
-    ``from <subnet> lookup 1001``) is not the node's uplink.  On a real kernel the agent takes that
-    NIC -- dry run and real L2 start -- with a warning, and still refuses the NIC that carries the
-    main table's default route."""
+    ``from <subnet> lookup 1001``) is not the main table's uplink.  ADVICE r5 (medium): but the NIC
+    holding the address that rule selects (192.168.50.10/24) is how the node reaches that network:
+    on a real kernel the agent refuses it (dry run: named as refused; real start: nothing touched)
+    unless --allow-policy-routed, and takes a rail whose policy table serves only its own /30,
+    with a warning.  The NIC with the main table's default route is refused either way."""
     r = netns.run_isolated(policy_routing_uplink=True)
     assert r["default_route_links"] == [r["mgmt"]], r
     assert any(x["table"] == 1001 and x["selective"] for x in r["rules"]), r["rules"]
     assert [x["table"] for x in r["table_1001"]] == [1001]  # table ids above 255 are kept
     assert r["dry_rail"]["rc"] == 0 and r["dry_rail"]["status"]["interfaces"][0]["name"] == "rail0", r["dry_rail"]
-    assert "rail0" not in (r["dry_rail"]["status"].get("excluded") or "")
+    assert ("rail0: carries a default route in policy-routing table 1001 and the node's address 192.168.50.10/24, the "
+            "source its rule 'from 192.168.50.0/24 lookup 1001' selects (refused)") in r["dry_rail"]["status"]["excluded"]
     assert "mgmt0: carries the node's default route (refused)" in r["dry_mgmt"]["status"]["excluded"], r["dry_mgmt"]
+    refused = r["configure_rail_refused"]
+    assert refused["rc"] == 1 and "Refusing to configure rail0 (a default route in policy-routing table 1001" in \
+        refused["stderr"], refused
+    assert refused["mtu"] == 1500 and refused["addrs"] == ["192.168.50.10/24"], refused
+    own = r["configure_own_rail"]
+    assert own["rc"] == 0 and own["mtu"] == 9000, own
+    assert "Interface 'rail1' has a default route in routing table 1002, which only selective rules reach" in own["stderr"]
     cr = r["configure_rail"]
     assert cr["rc"] == 0 and cr["mtu"] == 9000, cr
     assert "Interface 'rail0' has a default route in routing table 1001, which only selective rules reach" in cr["stderr"]

@@ -536,3 +536,50 @@ def test_alert_rules_use_only_metrics_that_exist():
                 assert name in operator_names, (r["alert"], name)
     kust = yaml.safe_load((ROOT / "config/operator/prometheus/kustomization.yaml").read_text())
     assert "alert-rules.yaml" in kust["resources"]
+
+
+def test_ci_builds_and_scans_the_three_images():
+    """the reference CI builds its operator and agent images and runs Trivy on them
+    (reference .github/workflows/validate-common.yaml:49-65).  The images job builds the operator,
+    link-discovery and validation images (their in-build gates run there) and scans each."""
+    ci = yaml.safe_load((ROOT / ".github" / "workflows" / "ci.yaml").read_text())["jobs"]["images"]
+    images = ci["strategy"]["matrix"]["image"]
+    assert sorted(images) == ["linkdiscovery", "operator", "validation"]
+    for img in images:
+        assert (ROOT / "build" / f"Dockerfile.{img}").exists(), img
+    build = [s for s in ci["steps"] if str(s.get("uses", "")).startswith("docker/build-push-action")]
+    scan = [s for s in ci["steps"] if str(s.get("uses", "")).startswith("aquasecurity/trivy-action")]
+    assert len(build) == 1 and build[0]["with"]["file"] == "build/Dockerfile.${{ matrix.image }}"
+    assert build[0]["with"]["load"] is True and build[0]["with"]["push"] is False
+    assert len(scan) == 1 and scan[0]["with"]["scan-type"] == "image"
+    assert scan[0]["with"]["image-ref"] == build[0]["with"]["tags"]
+    assert scan[0]["with"]["exit-code"] == "1" and scan[0]["with"]["severity"] == "HIGH,CRITICAL"
+
+
+def test_operator_image_dependencies_are_pinned_exactly():
+    """the operator image installs from a file of exact pins (no floating
+    ``==N.*``), with --no-deps, so two builds of one tag are the same; the pins cover every
+    module the operator imports and match the versions this suite runs with."""
+    import importlib.metadata as md
+    import re as _re
+
+    dockerfiles = {p.name: p.read_text() for p in (ROOT / "build").glob("Dockerfile.*")}
+    for name, text in dockerfiles.items():
+        assert not _re.search(r"==\d+\.\*", text), name
+    op = dockerfiles["Dockerfile.operator"]
+    assert "COPY build/requirements-operator.txt" in op and "--no-deps" in op and "-r /tmp/requirements.txt" in op
+    pins = {}
+    for line in (ROOT / "build" / "requirements-operator.txt").read_text().splitlines():
+        line = line.split("#", 1)[0].strip()
+        if line:
+            name, _, ver = line.partition("==")
+            assert ver and _re.fullmatch(r"[0-9][0-9A-Za-z.]*", ver), line
+            pins[name.lower().replace("_", "-")] = ver
+    assert {"aiohttp", "pyyaml", "prometheus-client"} <= set(pins)
+    for req in md.requires("aiohttp") or []:  # aiohttp's own unconditional dependencies are pinned too
+        if "extra ==" in req or "python_version" in req:
+            continue
+        dep = _re.split(r"[<>=!~; \[]", req, 1)[0].lower().replace("_", "-")
+        assert dep in pins, dep
+    for name, ver in pins.items():
+        assert md.version(name) == ver, (name, md.version(name), ver)

@@ -232,6 +232,36 @@ def test_device_bdf_names_the_gpu(cuda_device):
     assert os.path.exists(f"/sys/bus/pci/devices/{bdf}")
 
 
+@pytest.mark.gpu
+def test_ipc_open_refuses_a_gpu_it_cannot_reach_before_mapping(cuda_device):
+    """netop_ipc_open checks peer access to the exporter's GPU (its PCI bus id,
+    published beside the handle) before mapping anything, like the single-process probe.  A GPU
+    that is not visible here (or a pair without peer access) is refused with
+    hipErrorPeerAccessUnsupported and nothing is mapped; the exporter's own bus id is the GPU's."""
+    import ctypes
+
+    import torch
+
+    from network_operator_amd.ops import hip as H
+    from network_operator_amd.parallel.rail import device_bdf
+
+    L = H.lib()
+    t = torch.empty(1 << 20, dtype=torch.uint8, device=cuda_device)
+    h = ctypes.create_string_buffer(L.netop_ipc_handle_size())
+    off = ctypes.c_uint64()
+    H._check(L.netop_ipc_export(ctypes.c_void_p(t.data_ptr()), h, ctypes.byref(off)), "netop_ipc_export")
+    bus = ctypes.create_string_buffer(32)
+    H._check(L.netop_ipc_device_bus_id(ctypes.c_void_p(t.data_ptr()), bus, 32), "netop_ipc_device_bus_id")
+    assert bus.value.decode().lower() == device_bdf(cuda_device.index or 0), bus.value
+    ptr, base = ctypes.c_void_p(), ctypes.c_void_p()
+    for unreachable in (b"0000:ff:1f.7", b"not-a-bus-id"):
+        rc = L.netop_ipc_open(h.raw, 0, unreachable, ctypes.byref(ptr), ctypes.byref(base))
+        assert rc == 217, rc  # hipErrorPeerAccessUnsupported
+        assert ptr.value is None and base.value is None  # nothing mapped
+    assert L.netop_ipc_open(h.raw, 0, None, ctypes.byref(ptr), ctypes.byref(base)) == 1  # hipErrorInvalidValue
+    torch.cuda.synchronize()  # no sticky error left behind
+
+
 def _old_harness(world, args, limit_s):
     """The harness shape of round 3 before its fix: ranks' stdout and stderr through pipes, read
     one rank at a time (communicate() on rank 0, then rank 1, ...).  Returns (hung ranks, bytes
