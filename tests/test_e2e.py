@@ -352,6 +352,7 @@ def test_amd_so_driver_image_loads_the_rdma_driver_before_the_agent_labels_the_n
     hca = [l for l in r["rccl_env"].splitlines() if l.startswith("NCCL_IB_HCA=")]
     assert len(hca) == 1 and hca[0].count("mlx5_") == 2, r["rccl_env"]
     assert r["policy_status"]["errors"] == []
+    assert len(r["agent_started_s"]) == 1, r["agent_started_s"]  # no agent restart
 
 
 def test_a_node_waiting_for_rdma_devices_is_starting_not_degraded_and_labels_when_they_appear():
