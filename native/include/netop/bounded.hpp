@@ -14,8 +14,11 @@
 // nothing here blocks in a destructor.
 #pragma once
 
-#include <chrono>
-#include <condition_variable>
+#include <pthread.h>
+#include <time.h>
+
+#include <cerrno>
+#include <algorithm>
 #include <cstdint>
 #include <exception>
 #include <functional>
@@ -28,9 +31,38 @@
 namespace netop::bounded {
 
 namespace detail {
+// A condition variable on CLOCK_MONOTONIC, waited for with pthread_cond_timedwait.  (libstdc++'s
+// steady_clock wait_until goes through pthread_cond_clockwait, which this toolchain's
+// ThreadSanitizer does not intercept: every timed wait would read as a double lock.)
+class MonoCond {
+   public:
+    MonoCond() {
+        pthread_condattr_t a;
+        pthread_condattr_init(&a);
+        pthread_condattr_setclock(&a, CLOCK_MONOTONIC);
+        pthread_cond_init(&c_, &a);
+        pthread_condattr_destroy(&a);
+    }
+    ~MonoCond() { pthread_cond_destroy(&c_); }
+    MonoCond(const MonoCond&) = delete;
+    MonoCond& operator=(const MonoCond&) = delete;
+    // Waits (lk held) until pred() or CLOCK_MONOTONIC `deadline_ns`; pred()'s value at the end.
+    template <class Pred>
+    bool wait_until(std::unique_lock<std::mutex>& lk, int64_t deadline_ns, Pred pred) {
+        const timespec ts{time_t(deadline_ns / 1000000000), long(deadline_ns % 1000000000)};
+        while (!pred())
+            if (pthread_cond_timedwait(&c_, lk.mutex()->native_handle(), &ts) == ETIMEDOUT) return pred();
+        return true;
+    }
+    void notify_all() { pthread_cond_broadcast(&c_); }
+
+   private:
+    pthread_cond_t c_;
+};
+
 struct SlotBase {
     std::mutex m;
-    std::condition_variable cv;
+    MonoCond cv;
     bool done = false;
     virtual ~SlotBase() = default;
 };
@@ -83,8 +115,7 @@ class Call {
     std::optional<T> wait(int64_t deadline_ns) const {
         if (!slot_) return std::nullopt;
         std::unique_lock<std::mutex> lk(slot_->m);
-        const auto tp = std::chrono::steady_clock::time_point(std::chrono::nanoseconds(deadline_ns));
-        if (!slot_->cv.wait_until(lk, tp, [&] { return slot_->done; })) return std::nullopt;
+        if (!slot_->cv.wait_until(lk, std::max<int64_t>(deadline_ns, 0), [&] { return slot_->done; })) return std::nullopt;
         if (slot_->error) std::rethrow_exception(slot_->error);
         return slot_->value;
     }

@@ -3190,3 +3190,71 @@ TEST(agent_refuses_a_policy_routed_nic_that_holds_the_nodes_own_address) {
                                                  "address 172.16.9.3/16, an address the agent never installs (not a "
                                                  "/30) (refused)"));
 }
+
+// ---------------------------------------------------------------------------------------------
+// The monitor's gpu_metrics reads run on a worker; a link counts as down only on
+// --xgmi-down-samples consecutive samples.
+// ---------------------------------------------------------------------------------------------
+namespace {
+void write_two_gpu_kfd(const TmpDir& t) {
+    const std::string base = "sys/class/kfd/kfd/topology/nodes/";
+    t.write(base + "0/properties", "cpu_cores_count 96\nsimd_count 0\n");
+    for (int g = 1; g <= 2; ++g) {
+        t.write(base + std::to_string(g) + "/properties",
+                strfmt("simd_count 1024\nvendor_id 4098\ndevice_id 30115\nlocation_id %d\ndomain 0\nhive_id 77\n", (g * 0x10) << 8));
+        t.write(base + std::to_string(g) + "/io_links/0/properties",
+                strfmt("type 11\nnode_from %d\nnode_to %d\nweight 15\nmin_bandwidth 76000\nmax_bandwidth 76000\n", g, 3 - g));
+    }
+    auto blob = read_file(std::string(NETOP_TEST_FIXTURES) + "/gpu_metrics_v1_8.bin");
+    for (const char* bdf : {"0000:10:00.0", "0000:20:00.0"}) t.write(std::string("sys/bus/pci/devices/") + bdf + "/gpu_metrics", *blob);
+}
+
+void set_link(const TmpDir& t, const char* bdf, int slot, bool up) {
+    const std::string path = t.path + "/sys/bus/pci/devices/" + bdf + "/gpu_metrics";
+    std::string b = *read_file(path);
+    b[264 + 2 * size_t(slot)] = up ? 1 : 0;
+    b[265 + 2 * size_t(slot)] = 0;
+    write_file_atomic(path, b);
+}
+}  // namespace
+
+TEST(agent_monitor_reads_gpu_metrics_on_a_worker_and_dampens_a_single_down_sample) {
+    for (int samples : {2, 1000000}) {
+        Fixture f;
+        f.cfg.sysfs_root = f.tmp.path + "/sys/";
+        f.cfg.xgmi_expect_links = 0;
+        f.cfg.xgmi_health_interval_ns = 2000000;  // 2 ms
+        f.cfg.xgmi_down_samples = samples;
+        f.cfg.monitor_tick_ns = 1000000;
+        write_two_gpu_kfd(f.tmp);
+        Pipe stop;
+        agent::Agent a(f.cfg, f.ops, f.all_valid(), f.nm());
+        int64_t t_down = 0;
+        bool withdrawn = false, back = false;
+        std::string reason;
+        a.on_monitor_tick = [&](int tick) {
+            if (tick == 1) {
+                CHECK(path_exists(f.cfg.labels.path()));
+                set_link(f.tmp, "0000:20:00.0", 3, false);
+                t_down = mono_ns();
+            } else if (t_down && !withdrawn && !path_exists(f.cfg.labels.path())) {
+                withdrawn = true;
+                auto why = read_file(agent::reason_path(f.cfg.status_file));
+                reason = why ? *why : "";
+                set_link(f.tmp, "0000:20:00.0", 3, true);
+            } else if (withdrawn && path_exists(f.cfg.labels.path())) {
+                back = true;
+                stop.fire();
+            } else if (t_down && mono_ns() - t_down > 300000000LL) {
+                stop.fire();  // 300 ms: ~150 samples
+            }
+        };
+        a.run(stop.fd[0]);
+        if (samples == 2) {
+            CHECK(withdrawn && back);
+            CHECK_EQ(reason, std::string("xGMI: GPU 0000:20:00.0: link 3 down\n"));
+        } else {
+            CHECK(!withdrawn);  // never enough consecutive samples
+        }
+    }
+}

@@ -213,3 +213,73 @@ TEST(netlink_parse_rule_tells_selective_rules_from_lookup_everything) {
     reinterpret_cast<nlmsghdr*>(shortmsg.data())->nlmsg_len = uint32_t(shortmsg.size());
     CHECK(!parse(shortmsg));
 }
+
+// ---------------------------------------------------------------------------------------------
+// bounded.hpp: reads that may never return (a wedged SMU behind gpu_metrics), waited for with a
+// deadline; a read still blocked is joined, never started twice.
+// ---------------------------------------------------------------------------------------------
+#include <fcntl.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include "netop/bounded.hpp"
+#include "tmpdir.hpp"
+
+TEST(bounded_reads_return_at_the_deadline_and_join_a_read_still_blocked) {
+    TmpDir t;
+    t.write("plain", "1.8 metrics");
+    const std::string fifo = t.path + "/stalled";
+    CHECK_EQ(::mkfifo(fifo.c_str(), 0600), 0);
+    const size_t before = bounded::in_flight();
+    int64_t t0 = mono_ns();
+    auto r = bounded::read_files({t.path + "/plain", fifo, t.path + "/missing"}, mono_ns() + 100000000LL);
+    const int64_t took = mono_ns() - t0;
+    CHECK(took >= 90000000LL && took < 1000000000LL);  // the deadline, not the stalled read
+    CHECK(r[0].data && *r[0].data == "1.8 metrics" && !r[0].late);
+    CHECK(!r[1].data && r[1].late);
+    CHECK(!r[2].data && !r[2].late);  // unreadable is not late
+    CHECK_EQ(bounded::in_flight(), before + 1);
+    // Asked again while still blocked: joined (no second thread), late again.
+    auto again = bounded::read_files({fifo}, mono_ns() + 20000000LL);
+    CHECK(again[0].late);
+    CHECK_EQ(bounded::in_flight(), before + 1);
+    // The "SMU" answers: the blocked read returns its data, and the next read starts afresh.
+    int w = ::open(fifo.c_str(), O_WRONLY | O_NONBLOCK);
+    CHECK(w >= 0);
+    CHECK_EQ(::write(w, "late answer", 11), 11);
+    ::close(w);
+    for (int i = 0; i < 200 && bounded::in_flight() > before; ++i) ::usleep(1000);
+    CHECK_EQ(bounded::in_flight(), before);
+    ::unlink(fifo.c_str());
+    t.write("stalled", "fresh");
+    auto fresh = bounded::read_files({fifo}, mono_ns() + 100000000LL);
+    CHECK(fresh[0].data && *fresh[0].data == "fresh");
+}
+
+TEST(bounded_call_rethrows_and_notifies_after_the_result_is_in_place) {
+    bool done_seen = false;
+    std::mutex m;
+    bounded::detail::MonoCond cv;
+    bool notified = false;
+    bounded::Call<int> c("", [] { return 42; }, [&] {
+        std::lock_guard<std::mutex> g(m);
+        notified = true;
+        cv.notify_all();
+    });
+    {
+        std::unique_lock<std::mutex> lk(m);
+        cv.wait_until(lk, mono_ns() + 5000000000LL, [&] { return notified; });
+        done_seen = c.done();  // done() is already true when notify runs
+    }
+    CHECK(notified && done_seen);
+    CHECK(c.wait(mono_ns()) == std::optional<int>(42));
+    bounded::Call<int> bad("", []() -> int { throw std::runtime_error("sysfs gone"); });
+    std::string err;
+    try {
+        (void)bad.wait(mono_ns() + 1000000000LL);
+    } catch (const std::runtime_error& e) {
+        err = e.what();
+    }
+    CHECK_EQ(err, std::string("sysfs gone"));
+    CHECK(!bounded::Call<int>().wait(mono_ns()));  // an empty call never blocks
+}
