@@ -201,7 +201,11 @@ def helm_package(out_dir: Path, chart_dir: Optional[Path] = None) -> Path:
     name, version = meta["name"], str(meta["version"])
     out_dir.mkdir(parents=True, exist_ok=True)
     out = out_dir / f"{name}-{version}.tgz"
-    with tarfile.open(out, "w:gz", format=tarfile.PAX_FORMAT) as tar:
+    import gzip
+
+    # The gzip header carries a timestamp too ("w:gz" writes the current time): mtime 0, no name.
+    with open(out, "wb") as raw, gzip.GzipFile(filename="", mode="wb", fileobj=raw, mtime=0) as gz, \
+            tarfile.open(fileobj=gz, mode="w", format=tarfile.PAX_FORMAT) as tar:
         for f in sorted(p for p in chart_dir.rglob("*") if p.is_file()):
             data = f.read_bytes()
             ti = tarfile.TarInfo(f"{name}/{f.relative_to(chart_dir).as_posix()}")

@@ -348,7 +348,8 @@ def run_scenario(n_nics: int = 8, mode: str = "L3", seed: int | None = None, int
                  link_state: bool = True, pcie_flap: int | None = None, rails_without_rdma: int = 0,
                  rdma_bind_after: float | None = None, label_holddown: str | None = None,
                  flap_burst: tuple | None = None, gpu_metrics_stall: bool = False,
-                 sysfs_read_timeout: str = "") -> dict:
+                 sysfs_read_timeout: str = "", require_rdma: bool = True,
+                 pcie_restored_after: float | None = None) -> dict:
     """Runs one node bring-up.  Must already be inside a private user+net namespace.
 
     nm_bus: run the agent with --disable-networkmanager against a real ``dbus-daemon`` on which a
@@ -378,7 +379,11 @@ def run_scenario(n_nics: int = 8, mode: str = "L3", seed: int | None = None, int
     pcie_flap: after readiness that rail's NIC retrains its PCIe link at 16 GT/s x8, then back.
 
     pcie_degraded: {NIC index (an int, or its str after JSON): (GT/s, width)} -- that rail's NIC trained its PCIe link below the
-    maximum (32 GT/s x16); {"gpu<i>": (GT/s, width)} the same for GPU i.
+    maximum (32 GT/s x16); {"gpu<i>": (GT/s, width)} the same for GPU i.  pcie_restored_after:
+    those links retrain at the maximum that many seconds after the agent started ("pcie_restore").
+
+    require_rdma: pass --require-rdma, as the operator does for every amd-so policy unless
+    ``requireRdma: false`` (off: that policy, or an agent build older than the flag).
 
     rails_without_rdma: the first k rails' NICs have no RDMA device (their RDMA driver is not
     loaded) when the agent starts; with rdma_bind_after, the devices (and their GIDs) appear that
@@ -404,12 +409,14 @@ def run_scenario(n_nics: int = 8, mode: str = "L3", seed: int | None = None, int
     try:
         fx = fakesysfs.build_mi355x_node(tmp / "sys", n_gpus=n_nics, rail_driver=rail_driver,
                                          drop_xgmi_pairs=[tuple(p) for p in (drop_xgmi or [])])
+        degraded_bdfs = []
         for key, (gts, width) in (pcie_degraded or {}).items():
             if isinstance(key, str) and key.startswith("gpu"):
                 bdf = fx["gpus"][int(key[3:])]["bdf"]
             else:
                 bdf = fakesysfs.nic_pci_dir(tmp / "sys", nat.discover(str(tmp / "sys"))["pairs"][int(key)]["nic"]).name
             fakesysfs.set_pcie_link(tmp / "sys", bdf, gts, width)
+            degraded_bdfs.append(bdf)
         if xgmi_down_at_start is not None:
             fakesysfs.set_xgmi_link(tmp / "sys", fx["gpus"][xgmi_down_at_start[0]]["bdf"], xgmi_down_at_start[1], False)
         pairs = nat.discover(str(tmp / "sys"))["pairs"]
@@ -465,6 +472,8 @@ def run_scenario(n_nics: int = 8, mode: str = "L3", seed: int | None = None, int
                 f"--systemd-networkd={tmp / 'networkd'}", f"-v={verbose}", *(extra_args or [])]
         if link_state:  # as the operator passes it (off: an agent build older than the flag, bench/agent_ab.py)
             args.append(f"--link-state={tmp / 'link-state'}")
+        if require_rdma:  # likewise (the CRD default requireRdma: true)
+            args.append("--require-rdma")
         if label_holddown is None and (flap_port is not None or soak_cycles or xgmi_link_flap is not None
                                        or pcie_flap is not None or gpu_metrics_stall):
             label_holddown = "0s"  # these time the republication itself
@@ -575,6 +584,26 @@ def run_scenario(n_nics: int = 8, mode: str = "L3", seed: int | None = None, int
             set_switch_port(pid, sw_ports[dark_port], True)
             t_ready = _wait_for(label, 10, agent)
             dark["port_up_to_label_s"] = (t_ready - t_up) if t_ready else None
+        elif pcie_degraded and pcie_restored_after is not None:
+            # The narrow link retrains at full width while the agent runs (a reseat needs none,
+            # but PCIe error recovery or a hot reset can): the monitor configures the NIC it left
+            # unconfigured and labels the node, no restart needed.
+            reason, seen = tmp / "status.json.not-ready", []
+            while time.monotonic() < t0 + pcie_restored_after and agent.poll() is None:
+                try:
+                    why = reason.read_text()
+                    if why and why not in seen:
+                        seen.append(why)
+                except OSError:
+                    pass
+                time.sleep(0.02)
+            dark["reasons_seen"], dark["label_while_narrow"] = seen, label.exists()
+            dark["running_while_narrow"] = agent.poll() is None
+            t_fix = time.monotonic()
+            for bdf in degraded_bdfs:
+                fakesysfs.set_pcie_link(tmp / "sys", bdf, 32.0, 16)
+            t_ready = _wait_for(label, 10, agent)
+            dark["restore_to_label_s"] = (t_ready - t_fix) if t_ready else None
         elif rails_without_rdma and rdma_bind_after is not None:
             # The rails' RDMA driver is loaded while the agent runs (a driver container, the node):
             # until then the agent configures, stays up unlabelled and says why; then it labels.
@@ -681,6 +710,7 @@ def run_scenario(n_nics: int = 8, mode: str = "L3", seed: int | None = None, int
             res["stale_label_after_crash"] = label.exists()
             wall = time.time_ns()
             t_r = time.monotonic()
+            restart_log_at = agent_log.stat().st_size if agent_log.exists() else 0
             agent = spawn()
             back = None
             end = t_r + budget
@@ -701,8 +731,14 @@ def run_scenario(n_nics: int = 8, mode: str = "L3", seed: int | None = None, int
                         return None
                     return [i.get("lldp_source") for i in st["interfaces"]]
 
-                time.sleep(0.05)  # status.json follows the label
-                res["restart_lldp_sources"] = sources()
+                # How each NIC was configured at the restart, from the restarted agent's own log: a
+                # fast-start switch may confirm the cache before status.json is read.
+                with open(agent_log, errors="replace") as f:
+                    f.seek(restart_log_at)
+                    restart_log = f.read()
+                res["restart_lldp_sources"] = [
+                    "cache" if f"interface '{n}': Port Description" in restart_log and "from the LLDP cache" in restart_log
+                    .split(f"interface '{n}': Port Description", 1)[1].split("\n", 1)[0] else "frame" for n in nic_names]
                 confirmed = None
                 while time.monotonic() < end and agent.poll() is None:
                     if sources() == ["frame"] * len(nic_names):

@@ -657,7 +657,7 @@ def test_rails_without_rdma_devices_stay_unlabelled_until_the_rdma_driver_loads(
     driver registers the devices (fakesysfs bind), the label follows within a second and rccl.env
     names every rail's HCA."""
     r = netns.run_isolated(n_nics=4, seed=51, interval="30s", fast_start=True, rail_driver="ionic",
-                           rails_without_rdma=4, rdma_bind_after=2.0, extra_args=["--require-rdma"])
+                           rails_without_rdma=4, rdma_bind_after=2.0)  # --require-rdma: the operator's default
     d = r["dark"]
     assert d["running_while_missing"] and not d["label_while_missing"] and not d["rccl_env_while_missing"], d
     assert sorted(d["configured_while_missing"]) == sorted(r["nics"]), d
@@ -668,7 +668,8 @@ def test_rails_without_rdma_devices_stay_unlabelled_until_the_rdma_driver_loads(
     hca = [l for l in r["rccl_env"].splitlines() if l.startswith("NCCL_IB_HCA=")]
     assert len(hca) == 1 and hca[0].count("ionic_") == 4, r["rccl_env"]
     # Without --require-rdma (requireRdma: false): the reference's behaviour, labelled at once.
-    r = netns.run_isolated(n_nics=2, seed=52, interval="30s", fast_start=True, rail_driver="ionic", rails_without_rdma=2)
+    r = netns.run_isolated(n_nics=2, seed=52, interval="30s", fast_start=True, rail_driver="ionic", rails_without_rdma=2,
+                           require_rdma=False)
     assert r["ready"] and "NCCL_IB_HCA" not in r["rccl_env"], r["rccl_env"]
 
 
@@ -680,7 +681,9 @@ def test_a_flapping_port_withdraws_the_label_once_and_republishes_it_after_the_h
     assert r["ready"]
     f = r["flap_burst"]
     assert f["withdrawals"] == 1 and f["publishes"] == 1, f
-    assert 2.0 <= f["last_up_to_label_s"] < 3.0, f
+    # (timed from when the harness's port-up call returned; the agent sees the carrier a little
+    # earlier, so the 2 s hold-down can end a few ms before "2.0")
+    assert 1.9 <= f["last_up_to_label_s"] < 3.0, f
     assert any("label hold-down" in x or "link down" in x for x in f["reasons"]), f
 
 
@@ -698,3 +701,19 @@ def test_a_stalled_gpu_metrics_read_neither_holds_back_link_events_nor_hides_its
     assert s["reason"] and "gpu_metrics of 0000:0a:00.0 did not answer in 3s" in s["reason"], s
     assert not s["label_while_stalled"], s
     assert s["answer_to_label_s"] is not None and s["answer_to_label_s"] < 3.0, s
+
+
+def test_an_l2_rail_left_unconfigured_for_its_pcie_link_is_configured_when_the_link_retrains():
+    """with --require-full-pcie, an L2 rail whose PCIe link trained at x8 is left
+    unconfigured at start and the node unlabelled.  With the monitor the L2 agent never exits, so
+    no restart would re-check it: the monitor's PCIe sample does, and once the link is back at
+    32 GT/s x16 the NIC is configured and the node labelled.  (L3 fails the start instead, and the
+    kubelet's restart re-checks.)"""
+    r = netns.run_isolated(n_nics=2, seed=47, interval="30s", fast_start=True, mode="L2", wait="5s",
+                           pcie_degraded={1: (16.0, 8)}, pcie_restored_after=1.5,
+                           extra_args=["--require-full-pcie", "--xgmi-health-interval=100ms"])
+    d = r["dark"]
+    assert d["running_while_narrow"] and not d["label_while_narrow"], d
+    assert any("its PCIe link trained at 16.0 GT/s x8 of 32.0 GT/s x16" in w for w in d["reasons_seen"]), d
+    assert d["restore_to_label_s"] is not None and d["restore_to_label_s"] < 2.0, d
+    assert r["ready"] and r["agent_rc"] == 0, r["agent_log"][-2000:]
