@@ -579,30 +579,38 @@ std::vector<std::string> Agent::rdma_missing() const {
 }
 
 std::string Agent::rdma_reason() const {
-    return mono_ns() - t0_ < cfg_.rdma_wait_ns ? "waiting for RDMA device" : "no RDMA device (load its RDMA driver)";
+    // Start-up only before the node was ever ready: a device that goes away under a labelled node
+    // (a driver unloaded) is a fault at once.
+    const bool starting = !phases_.count("total_ready") && mono_ns() - t0_ < cfg_.rdma_wait_ns;
+    return starting ? "waiting for RDMA device" : "no RDMA device (load its RDMA driver)";
 }
 
 bool Agent::refresh_rdma() {
     if (!cfg_.require_rdma) return false;
     const std::string root = cfg_.sysfs_root.empty() ? topo::sysfs_root() : cfg_.sysfs_root;
-    bool found = false;
+    bool changed = false;
     for (auto& n : nics_) {
-        if (!n.rdma_dev.empty()) continue;
         std::string dev = topo::netdev_rdma_device(root, n.ifname);
-        if (dev.empty()) continue;
-        NLOG_I("Interface '%s': RDMA device %s appeared", n.ifname.c_str(), dev.c_str());
+        if (dev == n.rdma_dev) continue;
+        if (dev.empty())  // the RDMA driver was unloaded (or is reloading): RCCL loses the rail
+            NLOG_W("Interface '%s': its RDMA device %s went away", n.ifname.c_str(), n.rdma_dev.c_str());
+        else if (n.rdma_dev.empty())
+            NLOG_I("Interface '%s': RDMA device %s appeared", n.ifname.c_str(), dev.c_str());
+        else  // a driver reload may number the devices anew
+            NLOG_I("Interface '%s': RDMA device is %s now (was %s)", n.ifname.c_str(), dev.c_str(), n.rdma_dev.c_str());
         n.rdma_dev = dev;
         n.gid_index.reset();
         for (auto& d : disc_.nics)
             if (d.ifname == n.ifname) d.rdma_dev = dev;
         no_rdma_.erase(std::remove(no_rdma_.begin(), no_rdma_.end(), n.ifname), no_rdma_.end());
-        found = true;
+        if (dev.empty()) no_rdma_.push_back(n.ifname);
+        changed = true;
     }
-    if (found) {  // the topology file names each rail's HCA: generate it again
+    if (changed) {  // the topology file names each rail's HCA: generate it again
         topo_future_ = std::future<TopoResult>();
         topo_.reset();
     }
-    return found;
+    return changed;
 }
 
 void Agent::check_gdr() {

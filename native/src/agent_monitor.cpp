@@ -351,12 +351,17 @@ void Agent::monitor(int stop_fd) {
             poll = {};
             next_health = mono_ns() + cfg_.xgmi_health_interval_ns;
         }
+        bool rdma_changed = false;
         if (next_rdma > 0 && mono_ns() >= next_rdma) {
-            // --require-rdma: a driver container (or the node) loading the NICs' RDMA driver.
-            if (refresh_rdma()) changed = true;
+            // --require-rdma: a driver container (or the node) loading the NICs' RDMA driver, and
+            // after readiness a driver unloaded or reloaded under a labelled node.
+            rdma_changed = refresh_rdma();
+            if (rdma_changed) changed = true;
             if (!rdma_missing().empty() && rdma_reason() != rdma_said) changed = true;  // the wait ran out
             rdma_said = rdma_reason();
-            next_rdma = rdma_missing().empty() ? 0 : mono_ns() + cfg_.rdma_poll_ns;
+            // Quickly while a device is missing; at the health interval once every rail has one.
+            const int64_t every = rdma_missing().empty() ? cfg_.xgmi_health_interval_ns : cfg_.rdma_poll_ns;
+            next_rdma = every > 0 ? mono_ns() + every : 0;
         }
         if (cfg_.mode == "L3" && cfg_.verify_peers_ns > 0 && mono_ns() >= next_verify) {
             // NICs whose peer has not answered (yet): a recovered link, a new /30, or a switch
@@ -414,8 +419,10 @@ void Agent::monitor(int stop_fd) {
                     NLOG_W("Scale-out degraded: readiness label withdrawn");
                 }
             } else if (healthy && labelled && cfg_.mode == "L3") {
-                write_artifacts();  // re-addressed NIC: refresh the RCCL artifacts
+                write_artifacts();  // re-addressed NIC (or a renumbered RDMA device): refresh the RCCL artifacts
                 write_host_config();
+            } else if (healthy && labelled && rdma_changed && (!cfg_.rccl_env.empty() || !cfg_.rccl_topo.empty())) {
+                write_l2_artifacts();  // L2: a renumbered RDMA device, its link-local GID
             }
             ready_ = labelled;
             write_status();

@@ -3258,3 +3258,42 @@ TEST(agent_monitor_reads_gpu_metrics_on_a_worker_and_dampens_a_single_down_sampl
         }
     }
 }
+
+TEST(agent_require_rdma_withdraws_the_label_when_a_device_goes_away_and_follows_a_renumbered_one) {
+    // After readiness the RDMA driver is unloaded under a labelled node: the label goes at the
+    // next look (the health interval), with a fault reason (not start-up); the driver is loaded
+    // again and numbers the device anew: the label comes back and rccl.env names the new HCA.
+    RdmaFixture f;
+    f.cfg.xgmi_health_interval_ns = 5000000;  // how often a labelled node looks again
+    f.bind("ens0", "mlx5_0");
+    f.bind("ens1", "mlx5_1");
+    f.bind("ens2", "mlx5_2");
+    Pipe stop;
+    agent::Agent a(f.cfg, f.ops, f.all_valid(), f.nm());
+    int phase = 0;
+    std::string reason;
+    int64_t t_unload = 0;
+    a.on_monitor_tick = [&](int tick) {
+        const bool labelled = path_exists(f.cfg.labels.path());
+        if (phase == 0 && labelled) {
+            ::system(("rm -rf " + f.tmp.path + "/sys/class/net/ens1/device/infiniband").c_str());
+            t_unload = mono_ns();
+            phase = 1;
+        } else if (phase == 1 && !labelled) {
+            auto why = read_file(agent::reason_path(f.cfg.status_file));
+            reason = why ? *why : "";
+            f.bind("ens1", "mlx5_7");
+            phase = 2;
+        } else if (phase == 2 && labelled) {
+            phase = 3;
+            stop.fire();
+        } else if (tick > 5000 || (t_unload && mono_ns() - t_unload > 2000000000LL)) {
+            stop.fire();
+        }
+    };
+    a.run(stop.fd[0]);
+    CHECK_EQ(phase, 3);
+    CHECK_EQ(reason, std::string("ens1: no RDMA device (load its RDMA driver)\n"));
+    auto env = read_file(f.cfg.rccl_env);
+    CHECK(env && env->find("NCCL_IB_HCA==mlx5_0:1,mlx5_7:1,mlx5_2:1\n") != std::string::npos);
+}

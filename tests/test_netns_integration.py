@@ -696,7 +696,11 @@ def test_a_stalled_gpu_metrics_read_neither_holds_back_link_events_nor_hides_its
                            sysfs_read_timeout="3s", extra_args=["--xgmi-health-interval=100ms"])
     assert r["ready"]
     s = r["gpu_metrics_stall"]
-    assert None not in s["withdraw_during_stall_s"] and s["withdraw_during_stall_p50_s"] < 0.010, s
+    # Under 10 ms on a quiet machine (~2 ms here); on a loaded one (the suite runs -n 8) no slower
+    # than twice the same carrier losses with no read stalled.  A loop blocked behind the read
+    # would take the whole 3 s timeout.
+    assert None not in s["withdraw_during_stall_s"], s
+    assert s["withdraw_during_stall_p50_s"] < max(0.010, 2 * s["withdraw_without_stall_p50_s"]), s
     assert s["stall_to_reason_s"] is not None and s["stall_to_reason_s"] > s["flaps_done_s"], s  # stalled throughout
     assert s["reason"] and "gpu_metrics of 0000:0a:00.0 did not answer in 3s" in s["reason"], s
     assert not s["label_while_stalled"], s

@@ -1215,6 +1215,11 @@ def test_a_starting_node_is_not_reported_as_degraded():
 
     assert _starting_up("ens0: waiting for LLDP; ens1: not configured yet")
     assert not _starting_up("ens0: waiting for LLDP; ens1: link down")
+    # requireRdma: waiting for the RDMA devices is start-up until rdmaWait, then a fault; the
+    # label hold-down after a flap is a degraded node recovering, not one starting.
+    assert _starting_up("ens0: waiting for RDMA device; ens1: waiting for LLDP")
+    assert not _starting_up("ens0: no RDMA device (load its RDMA driver); ens1: waiting for RDMA device")
+    assert not _starting_up("label hold-down: healthy again after 1 withdrawal(s), republished in 7.5s without a flap")
 
 
 def test_dcbx_hand_over_and_peer_mtu_check_are_policy_fields():
