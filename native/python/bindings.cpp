@@ -362,13 +362,20 @@ PYBIND11_MODULE(_netop_native, m) {
         d["str"] = l.str();
         return d;
     });
-    m.def("read_xgmi_health", [](const std::string& root, const std::vector<std::string>& bdfs) {
+    // timeout_ms > 0: the agent's bounded read (one thread per GPU, late GPUs reported "late").
+    m.def("read_xgmi_health", [](const std::string& root, const std::vector<std::string>& bdfs, int64_t timeout_ms) {
         py::list out;
-        for (const auto& h : topo::read_xgmi_health(root, bdfs)) {
+        std::vector<topo::XgmiLinkHealth> hs;
+        {
+            py::gil_scoped_release nogil;
+            hs = timeout_ms > 0 ? topo::read_xgmi_health(root, bdfs, timeout_ms * 1000000) : topo::read_xgmi_health(root, bdfs);
+        }
+        for (const auto& h : hs) {
             py::dict d;
             d["bdf"] = h.bdf;
             d["revision"] = h.revision;
             d["known"] = h.known;
+            d["late"] = h.late;
             d["error"] = h.error;
             d["width"] = h.width;
             d["speed_gbps"] = h.speed_gbps;
@@ -378,7 +385,7 @@ PYBIND11_MODULE(_netop_native, m) {
             out.append(d);
         }
         return out;
-    });
+    }, py::arg("root"), py::arg("bdfs"), py::arg("timeout_ms") = 0);
     m.def("detect_gdr", [](const std::string& root, const std::string& kernel) {
         auto g = topo::detect_gdr(root, kernel);
         py::dict d;

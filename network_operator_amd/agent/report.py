@@ -72,7 +72,8 @@ def collect(root: str, min_link_speed_gbps: float = 0, artifact_dir: str = "") -
                       "rdma_dev": nic.get("rdma_dev", ""), "nic_pcie": n.read_pcie_link(root, nic.get("bdf", "")),
                       "gpu_pcie": n.read_pcie_link(root, p["gpu"]), "link": _netdev(root, nic.get("bdf", ""), p["nic"])})
     x = n.read_xgmi(root)
-    health = n.read_xgmi_health(root, [g["bdf"] for g in d["gpus"]])
+    # Bounded like the agent's own read: a wedged SMU is a finding, not a hung report.
+    health = n.read_xgmi_health(root, [g["bdf"] for g in d["gpus"]], 5000)
     gdr = n.detect_gdr(root, platform.release())
     problems: List[str] = []
     paired = {r["gpu"] for r in rails}
@@ -89,6 +90,8 @@ def collect(root: str, min_link_speed_gbps: float = 0, artifact_dir: str = "") -
     if x["pairs_connected"] < x["pairs_expected"]:
         problems.append(f"xGMI mesh: {x['pairs_connected']} of {x['pairs_expected']} GPU pairs linked")
     for h in health:
+        if h.get("late"):
+            problems.append(f"GPU {h['bdf']}: gpu_metrics did not answer in 5s (a wedged or resetting SMU?)")
         down = [i for i, s in enumerate(h["status"]) if s == 0]
         if down:
             problems.append(f"GPU {h['bdf']}: xGMI link(s) {', '.join(map(str, down))} down")

@@ -188,8 +188,11 @@ def run(gpus: int, min_busbw: float, min_link_GBps: float, max_bytes: int, sysfs
         # The links' trained state (amdgpu gpu_metrics), as the agent reads it: none down.
         from .agent import native
 
-        health = native().read_xgmi_health(sysfs_root, list(topo.gpus))
+        health = native().read_xgmi_health(sysfs_root, list(topo.gpus), 5000)  # bounded: a wedged SMU fails, never hangs
         known = [h for h in health if h["known"]]
+        late = [h["bdf"] for h in health if h.get("late")]
+        if late:
+            checks.append(_check("gpu_metrics_answers", False, late=late, why="gpu_metrics did not answer in 5s"))
         if known:
             down = {h["bdf"]: [i for i, st in enumerate(h["status"]) if st == 0] for h in known}
             checks.append(_check("xgmi_link_state", not any(down.values()),
