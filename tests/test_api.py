@@ -305,3 +305,29 @@ def test_a_minimal_amd_so_policy_verifies_the_xgmi_mesh_and_rdma_by_default(tmp_
     off["spec"]["amdScaleOut"] = {"xgmiCheck": False, "requireRdma": False}
     CRD.apply_defaults(off, CRD.openapi_schema())
     assert off["spec"]["amdScaleOut"] == {"xgmiCheck": False, "requireRdma": False}
+
+
+def test_every_sample_policy_is_admitted_and_renders_its_agent():
+    """config/operator/samples/*.yaml: each passes the CRD schema and the webhooks, and its
+    DaemonSet passes what the sample asks for (the Pollara sample: the RDMA driver container and
+    --require-rdma / --rdma-wait)."""
+    from network_operator_amd import discovery
+    from network_operator_amd.operator.templates import update_daemonset_for
+
+    root = Path(__file__).resolve().parent.parent / "config" / "operator" / "samples"
+    seen = {}
+    for f in sorted(root.glob("*.yaml")):
+        if f.name == "kustomization.yaml":
+            continue
+        obj = yaml.safe_load(f.read_text())
+        assert CRD.validate(obj) == [], (f.name, CRD.validate(obj))
+        pol = W.default(T.NetworkClusterPolicy.from_dict(obj))
+        assert [w for w in W.validate_create(pol) if "no interfaces or nicDrivers" not in w] == [], f.name
+        ds = discovery.discovery_daemonset()
+        update_daemonset_for(ds, pol, "amd-network-operator")
+        seen[f.name] = ds["spec"]["template"]["spec"]
+    pollara = seen["amd-l3-pollara.yaml"]
+    args = pollara["containers"][0]["args"]
+    assert "--require-rdma" in args and "--rdma-wait=10m" in args and "--nic-drivers=ionic" in args, args
+    assert [c["name"] for c in pollara["initContainers"]] == ["nic-driver"]
+    assert pollara["initContainers"][0]["securityContext"] == {"privileged": True}
