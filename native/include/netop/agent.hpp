@@ -461,7 +461,8 @@ class Agent {
     topo::DiscoveryResult disc_;
     double cpu_ms_at_ready_ = -1;  // user + system CPU of the process when the label went up
     std::vector<std::string> dry_run_missing_;  // discovered, but not in this network namespace
-    std::future<TopoResult> topo_future_;
+    bounded::Call<TopoResult> topo_call_;  // the topology worker (start_topo), joined with a deadline
+    bool topo_late_ = false;                // it missed that deadline once: later joins only look
     std::optional<TopoResult> topo_;
     topo::XgmiReport xgmi_;
     std::vector<topo::XgmiLinkHealth> xgmi_health_;

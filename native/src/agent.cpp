@@ -607,8 +607,9 @@ bool Agent::refresh_rdma() {
         changed = true;
     }
     if (changed) {  // the topology file names each rail's HCA: generate it again
-        topo_future_ = std::future<TopoResult>();
+        topo_call_ = {};
         topo_.reset();
+        topo_late_ = false;
     }
     return changed;
 }

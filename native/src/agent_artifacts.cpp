@@ -23,6 +23,7 @@
 #include <regex>
 #include <set>
 #include <system_error>
+#include <thread>
 
 #include "agent_internal.hpp"
 #include "netop/log.hpp"
@@ -153,7 +154,7 @@ Agent::TopoResult make_topology(const topo::DiscoveryResult& disc, const std::st
 }  // namespace
 
 void Agent::start_topo() {
-    if (cfg_.rccl_topo.empty() || topo_future_.valid() || topo_) return;
+    if (cfg_.rccl_topo.empty() || topo_call_.valid() || topo_) return;
     std::string root = cfg_.sysfs_root.empty() ? topo::sysfs_root() : cfg_.sysfs_root;
     // Inputs are copied: the worker shares nothing with the agent thread.
     const int main_cpu = ::sched_getcpu();
@@ -178,19 +179,33 @@ void Agent::start_topo() {
             NLOG_V(2, "topology worker: setpriority(19): %s", std::strerror(errno));
         return make_topology(disc, interfaces, root, path);
     };
-    try {
-        topo_future_ = std::async(std::launch::async, work, true);
-    } catch (const std::system_error& e) {  // no thread to spare: generate it when it is needed
-        NLOG_V(2, "topology worker thread unavailable (%s): generating on demand", e.what());
-        topo_future_ = std::async(std::launch::deferred, work, false);
-    }
+    // A detached worker (netop/bounded.hpp): the walk reads every bridge's PCI attributes, and a
+    // function in error recovery can stall such a read; the join below is bounded, and nothing
+    // waits for a stalled worker when the agent exits.  Without a thread, it runs here.
+    topo_call_ = bounded::Call<TopoResult>("", [work, agent_thread = std::this_thread::get_id()] {
+        return work(std::this_thread::get_id() != agent_thread);  // in line: no affinity or nice change
+    });
 }
 
 const std::string& Agent::topo_xml() {
+    static const std::string none;
     if (!topo_) {
-        if (!topo_future_.valid()) start_topo();
+        if (!topo_call_.valid()) start_topo();
+        // Bounded like every sysfs read of the start; once late, later artifact writes only look.
+        const int64_t deadline = topo_late_ ? mono_ns() : mono_ns() + cfg_.sysfs_read_timeout_ns;
         try {
-            topo_ = topo_future_.get();
+            auto r = topo_call_.wait(deadline);
+            if (!r) {
+                if (!topo_late_)
+                    NLOG_W("The RCCL topology file was not generated within %s (a PCI attribute read stalled?): "
+                           "rccl.env names no NCCL_TOPO_FILE until it is (RCCL then reads the topology itself)",
+                           format_go_duration(cfg_.sysfs_read_timeout_ns).c_str());
+                topo_late_ = true;
+                return none;
+            }
+            topo_ = std::move(*r);
+            if (topo_late_) NLOG_I("The RCCL topology file was generated late: rccl.env names it now");
+            topo_late_ = false;
             // The worker's interface list is the agent's (same discovery); kept as a guard.
             std::vector<std::string> mine = topo_names(disc_, cfg_.interfaces);
             if (topo_->names != mine) {

@@ -351,6 +351,8 @@ void Agent::monitor(int stop_fd) {
             poll = {};
             next_health = mono_ns() + cfg_.xgmi_health_interval_ns;
         }
+        if (topo_late_ && labelled && topo_call_.done())
+            write_rccl_env_file();  // the topology worker answered after the start's deadline after all
         bool rdma_changed = false;
         if (next_rdma > 0 && mono_ns() >= next_rdma) {
             // --require-rdma: a driver container (or the node) loading the NICs' RDMA driver, and

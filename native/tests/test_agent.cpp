@@ -5,6 +5,7 @@
 #include <poll.h>
 #include <netinet/in.h>
 #include <sys/socket.h>
+#include <sys/stat.h>
 #include <sys/un.h>
 #include <unistd.h>
 
@@ -1304,6 +1305,49 @@ TEST(agent_topology_file_generated_off_the_critical_path) {
     CHECK(xml && xml->rfind("<system version=\"2\">", 0) == 0);
     auto env = read_file(f.cfg.rccl_env);
     CHECK(env && env->find("NCCL_TOPO_FILE=/etc/amd/scale-out/rccl-topo.xml\n") != std::string::npos);
+}
+
+TEST(agent_late_topology_worker_is_not_waited_for_and_rccl_env_names_its_file_once_it_answers) {
+    // The topology worker stalls (here: its reuse key is a FIFO nobody writes yet, as a bridge
+    // attribute in PCIe error recovery would): the start waits --sysfs-read-timeout for it, labels
+    // the node with an rccl.env that names no NCCL_TOPO_FILE, and the monitor writes the file and
+    // names it once the worker answers.
+    Fixture f;
+    f.cfg.monitor_tick_ns = 1000000;
+    f.cfg.sysfs_read_timeout_ns = 20000000;  // 20 ms
+    f.cfg.rccl_topo = f.tmp.path + "/rccl-topo.xml";
+    f.cfg.rccl_env = f.tmp.path + "/rccl.env";
+    f.cfg.sysfs_root = f.tmp.path + "/sys/";
+    const std::string key = f.cfg.rccl_topo + ".key";
+    CHECK_EQ(::mkfifo(key.c_str(), 0600), 0);
+    auto release = [&] {  // the worker is blocked opening the FIFO: a writer lets it read "no match"
+        int w = ::open(key.c_str(), O_WRONLY | O_NONBLOCK | O_CLOEXEC);
+        if (w < 0) return false;
+        (void)!::write(w, "another boot\n", 13);
+        ::close(w);
+        return true;
+    };
+    Pipe stop;
+    agent::Agent a(f.cfg, f.ops, f.all_valid(), f.nm());
+    bool labelled_without = false, released = false, named = false;
+    const int64_t t0 = mono_ns();
+    a.on_monitor_tick = [&](int) {
+        auto env = read_file(f.cfg.rccl_env);
+        if (!released) {
+            labelled_without = path_exists(f.cfg.labels.path()) && env && env->find("NCCL_TOPO_FILE") == std::string::npos;
+            released = release();
+        } else if (env && env->find("NCCL_TOPO_FILE=" + f.cfg.rccl_topo + "\n") != std::string::npos) {
+            named = true;
+            stop.fire();
+        }
+        if (mono_ns() - t0 > 5000000000LL) stop.fire();
+    };
+    a.run(stop.fd[0]);
+    if (!released) release();
+    CHECK(labelled_without);
+    CHECK(released && named);
+    auto xml = read_file(f.cfg.rccl_topo);
+    CHECK(xml && xml->rfind("<system version=\"2\">", 0) == 0);
 }
 
 TEST(agent_dry_run_changes_nothing) {

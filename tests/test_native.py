@@ -468,3 +468,29 @@ def test_an_unknown_gpu_metrics_layout_is_said_once_and_in_the_status(native, tm
                                 "not checked"), st
     assert st["xgmi_pairs"] == "1/1" and "xgmi_error" not in st
     assert r.stderr.count("xGMI link state not checked on any of the 2 GPU(s)") == 1, r.stderr[-2000:]
+
+
+def test_a_stalled_bridge_read_leaves_the_topology_file_out_instead_of_hanging(native, tmp_path):
+    """Bound every wait on the start path, the topology worker's included: its walk
+    reads every bridge's PCI attributes above the GPUs and NICs, and a function in error recovery
+    can stall such a read.  Here the root port above GPU 0 has a max_link_speed that never answers
+    (a FIFO): the dry run finishes after --sysfs-read-timeout, rccl.env names no NCCL_TOPO_FILE
+    (RCCL then reads the topology itself), and the log says why."""
+    import time
+
+    fx = fakesysfs.build_mi355x_node(tmp_path / "sys", n_gpus=2)
+    parts = fx["gpus"][0]["path"].split("/")
+    attr = tmp_path / "sys" / "devices" / "/".join(parts[:2]) / "max_link_speed"
+    attr.unlink()
+    os.mkfifo(attr)
+    t0 = time.monotonic()
+    r = subprocess.run([str(native_bin("discover")), "--dry-run", "--xgmi-expect=0", "--sysfs-read-timeout=1s",
+                        f"--rccl-topo={tmp_path / 'rccl-topo.xml'}", f"--rccl-env={tmp_path / 'rccl.env'}",
+                        f"--status-file={tmp_path / 'status.json'}"], capture_output=True, text=True, timeout=30,
+                       env=dict(os.environ, SYSFS_ROOT=str(tmp_path / "sys")))
+    took = time.monotonic() - t0
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert took < 5, took
+    assert "The RCCL topology file was not generated within 1s" in r.stderr, r.stderr[-2000:]
+    assert not (tmp_path / "rccl-topo.xml").exists()
+    assert "NCCL_TOPO_FILE" not in (tmp_path / "rccl.env").read_text()
