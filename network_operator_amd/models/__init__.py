@@ -1,6 +1,7 @@
 """Data models of the operator.
 
-* ``policy``   — the ``NetworkClusterPolicy`` object model (re-exported from ``api.v1alpha1``);
+* the ``NetworkClusterPolicy`` object model, re-exported here from ``api.v1alpha1.types`` (no module
+  of its own);
 * ``topology`` — the node scale-out topology model: GPUs, NICs, GPU<->NIC PCIe pairing and the
   xGMI mesh, built from the native agent's sysfs / KFD discovery.
 """
