@@ -222,6 +222,7 @@ const std::string& Agent::topo_xml() {
         } catch (const std::exception& e) {
             NLOG_E("Error generating the RCCL topology file: %s", e.what());
             topo_ = TopoResult{};
+            topo_late_ = false;  // answered (with an error): the monitor has nothing left to wait for
         }
     }
     return topo_->xml;
