@@ -571,12 +571,19 @@ def run_scenario(n_nics: int = 8, mode: str = "L3", seed: int | None = None, int
             dark["reason_s"] = (t_why - t0) if t_why else None
             dark["label_while_dark"] = label.exists()
             dark["reason"] = reason.read_text() if reason.exists() else None
-            try:
-                st = json.loads((tmp / "status.json").read_text())
-                dark["status_ready"] = st.get("ready")
-                dark["status_no_carrier"] = [i["name"] for i in st["interfaces"] if i.get("no_carrier")]
-            except (OSError, ValueError, KeyError):
-                dark["status_ready"] = dark["status_no_carrier"] = None
+            # The agent writes the probe's reason first and status.json right after it: give the
+            # second write its moment (a sanitizer build widens the gap).
+            t_end = time.monotonic() + 2.0
+            while True:
+                try:
+                    st = json.loads((tmp / "status.json").read_text())
+                    dark["status_ready"] = st.get("ready")
+                    dark["status_no_carrier"] = [i["name"] for i in st["interfaces"] if i.get("no_carrier")]
+                except (OSError, ValueError, KeyError):
+                    dark["status_ready"] = dark["status_no_carrier"] = None
+                if dark["status_no_carrier"] or time.monotonic() >= t_end:
+                    break
+                time.sleep(0.02)
             pr = subprocess.run([str(native_bin("discover")), "--ready-check", f"--nfd-features-dir={feat}",
                                  f"--status-file={tmp / 'status.json'}"], capture_output=True, text=True, timeout=10)
             dark["ready_check"] = {"rc": pr.returncode, "stdout": pr.stdout.strip()}
