@@ -284,6 +284,7 @@ def write_self_signed(cert_dir: Path, cn: str = "localhost", sans: Iterable[str]
     der, key = make_certificate(cn, sans, days)
     crt_path, key_path = cert_dir / "tls.crt", cert_dir / "tls.key"
     fd = os.open(key_path, os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o600)
+    os.fchmod(fd, 0o600)  # a key file that already existed keeps its mode through O_CREAT
     with os.fdopen(fd, "w") as f:
         f.write(pem("EC PRIVATE KEY", key))
     crt_path.write_text(pem("CERTIFICATE", der))

@@ -614,6 +614,19 @@ def test_self_signed_certificates_are_standard_ecdsa_p256():
         lsock.close()
 
 
+def test_self_signed_key_file_is_private_even_when_it_existed(tmp_path):
+    """write_self_signed over a world-readable tls.key left by something else: the new key is
+    written into a 0600 file, never into the old mode."""
+    from network_operator_amd.operator import selfsigned as S
+
+    (tmp_path / "tls.key").write_text("old")
+    os.chmod(tmp_path / "tls.key", 0o644)
+    crt, key = S.write_self_signed(tmp_path)
+    assert os.stat(key).st_mode & 0o777 == 0o600
+    assert key.read_text().startswith("-----BEGIN EC PRIVATE KEY-----")
+    assert crt.read_text().startswith("-----BEGIN CERTIFICATE-----")
+
+
 @pytest.mark.parametrize("swallows", [False, True])
 def test_lease_is_released_only_after_the_leaders_work_has_ended(monkeypatch, swallows):
     """the lease is handed back only once the leader's work has ended.  Work that
