@@ -360,7 +360,7 @@ def image_tag(image: str) -> str:
 def validate_amd_so_spec(s: T.AmdScaleOutSpec) -> List[str]:
     """Returns admission warnings.  (The reference's validateGaudiSoSpec is a no-op, :87-89.)"""
     warnings = []
-    if s.layer == "L2" and s.xgmiCheck is False and s.lldpAnnounce is not None:
+    if s.layer == "L2" and s.lldpAnnounce is not None:  # the agent announces only in L3 (agent_monitor.cpp)
         warnings.append("lldpAnnounce has no effect in L2 mode")
     for i in s.interfaces:
         if not i or len(i) > 15 or "/" in i or " " in i or "," in i:

@@ -563,6 +563,13 @@ def test_lldp_wait_validated_and_passed():
     p.spec.amdScaleOut.lldpWait, p.spec.amdScaleOut.layer = "5s", "L2"
     assert W.validate_create(p) == ["lldpWait has no effect in L2 mode"]
     assert not any(a.startswith("--wait") for a in agent_args(p))
+    # lldpAnnounce likewise (the agent announces only in L3), whatever xgmiCheck says
+    p.spec.amdScaleOut.lldpWait = ""
+    for xgmi in (None, True, False):
+        p.spec.amdScaleOut.lldpAnnounce, p.spec.amdScaleOut.xgmiCheck = False, xgmi
+        assert W.validate_create(p) == ["lldpAnnounce has no effect in L2 mode"]
+    p.spec.amdScaleOut.layer = "L3"
+    assert W.validate_create(p) == []
     h = T.new_host_nic_policy("h", layer="L3", lldpWait="20s")
     assert "--wait=20s" in host_nic_agent_args(h) and W.validate_create(h) == [
         "hostNic: no interfaces or nicDrivers given; every RDMA NIC of the default driver list that is neither a "
