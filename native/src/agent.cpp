@@ -903,7 +903,14 @@ void Agent::run(int stop_fd) {
     if (cfg_.xgmi_expect_links >= 0)
         labels_extra_["amd.feature.node.kubernetes.io/gpu-xgmi.pairs"] = std::to_string(xgmi_.pairs_connected);
     if (!gdr_.kernel.empty()) labels_extra_[cfg_.labels.key + ".gdr"] = gdr_.mode();
-    refresh_rdma();  // a driver loaded during the bring-up
+    if (refresh_rdma() && (!cfg_.rccl_env.empty() || !cfg_.rccl_topo.empty())) {
+        // A driver loaded during the bring-up, after the artifacts were written without its
+        // devices (rccl.env held back): write them again with the HCAs before the label.
+        if (cfg_.mode == "L3")
+            write_artifacts();
+        else
+            write_l2_artifacts();
+    }
     const std::vector<std::string> no_rdma = rdma_missing();
     const bool linked = xgmi_error_.empty() && no_rdma.empty() &&
                         (cfg_.mode != "L2" ||

@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <deque>
+#include <functional>
 #include <map>
 #include <set>
 
@@ -52,8 +53,10 @@ struct FakeNetOps : netop::nl::NetOps {
             if (l.index == idx) return &l;
         return nullptr;
     }
+    std::function<void(const std::string&)> on_op;  // runs at every operation, before it acts
     void maybe_fail(const std::string& op) {
         ++calls[op];
+        if (on_op) on_op(op);
         if (fail.count(op)) throw netop::SysError(fail_errno, "injected " + op);
     }
     std::optional<netop::nl::LinkInfo> link_by_ifindex(int ifindex) override {

@@ -3074,6 +3074,36 @@ TEST(agent_require_rdma_configures_waits_unlabelled_then_labels_when_the_devices
     CHECK(a.render_metrics().find("netop_agent_nic_rdma{nic=\"ens2\"} 1") != std::string::npos);
 }
 
+TEST(agent_require_rdma_devices_that_appear_during_the_bring_up_are_in_rccl_env_before_the_label) {
+    // The RDMA driver finishes loading while the NICs are being configured: the artifacts were
+    // written without the devices (rccl.env held back), the final check finds them all, and the
+    // label must not be published over a missing rccl.env.
+    RdmaFixture f;
+    f.cfg.keep_running = true;
+    bool bound = false;
+    f.ops.on_op = [&](const std::string& op) {
+        if (op == "addr_add" && !bound) {
+            bound = true;
+            f.bind("ens0", "mlx5_0");
+            f.bind("ens1", "mlx5_1");
+            f.bind("ens2", "mlx5_2");
+        }
+    };
+    Pipe stop;
+    agent::Agent a(f.cfg, f.ops, f.all_valid(), f.nm());
+    bool labelled = false;
+    std::optional<std::string> env;
+    a.on_monitor_tick = [&](int) {  // the state the start left, before the monitor changes anything
+        labelled = path_exists(f.cfg.labels.path());
+        env = read_file(f.cfg.rccl_env);
+        stop.fire();
+    };
+    a.run(stop.fd[0]);
+    CHECK(bound);
+    CHECK(labelled);
+    CHECK(env && env->find("NCCL_IB_HCA==mlx5_0:1,mlx5_1:1,mlx5_2:1\n") != std::string::npos);
+}
+
 TEST(agent_require_rdma_past_the_wait_names_the_fault) {
     RdmaFixture f;
     f.cfg.rdma_wait_ns = 0;
