@@ -420,6 +420,8 @@ void Agent::monitor(int stop_fd) {
                     ++label_withdrawals_;
                     NLOG_W("Scale-out degraded: readiness label withdrawn");
                 }
+                if (rdma_changed && !rdma_missing().empty() && !cfg_.rccl_env.empty())
+                    write_rccl_env_file();  // it names an HCA that is gone: removed until the devices are back
             } else if (healthy && labelled && cfg_.mode == "L3") {
                 write_artifacts();  // re-addressed NIC (or a renumbered RDMA device): refresh the RCCL artifacts
                 write_host_config();

@@ -3347,6 +3347,7 @@ TEST(agent_require_rdma_withdraws_the_label_when_a_device_goes_away_and_follows_
     int phase = 0;
     std::string reason;
     int64_t t_unload = 0;
+    bool env_while_gone = true;
     a.on_monitor_tick = [&](int tick) {
         const bool labelled = path_exists(f.cfg.labels.path());
         if (phase == 0 && labelled) {
@@ -3356,6 +3357,7 @@ TEST(agent_require_rdma_withdraws_the_label_when_a_device_goes_away_and_follows_
         } else if (phase == 1 && !labelled) {
             auto why = read_file(agent::reason_path(f.cfg.status_file));
             reason = why ? *why : "";
+            env_while_gone = path_exists(f.cfg.rccl_env);
             f.bind("ens1", "mlx5_7");
             phase = 2;
         } else if (phase == 2 && labelled) {
@@ -3368,6 +3370,7 @@ TEST(agent_require_rdma_withdraws_the_label_when_a_device_goes_away_and_follows_
     a.run(stop.fd[0]);
     CHECK_EQ(phase, 3);
     CHECK_EQ(reason, std::string("ens1: no RDMA device (load its RDMA driver)\n"));
+    CHECK(!env_while_gone);  // no rccl.env naming mlx5_1 while it is gone
     auto env = read_file(f.cfg.rccl_env);
     CHECK(env && env->find("NCCL_IB_HCA==mlx5_0:1,mlx5_7:1,mlx5_2:1\n") != std::string::npos);
 }
