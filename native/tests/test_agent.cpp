@@ -11,6 +11,7 @@
 
 #include <cstddef>
 #include <cstring>
+#include <filesystem>
 
 #include "check.hpp"
 #include "fake_netops.hpp"
@@ -3351,7 +3352,7 @@ TEST(agent_require_rdma_withdraws_the_label_when_a_device_goes_away_and_follows_
     a.on_monitor_tick = [&](int tick) {
         const bool labelled = path_exists(f.cfg.labels.path());
         if (phase == 0 && labelled) {
-            ::system(("rm -rf " + f.tmp.path + "/sys/class/net/ens1/device/infiniband").c_str());
+            std::filesystem::remove_all(f.tmp.path + "/sys/class/net/ens1/device/infiniband");
             t_unload = mono_ns();
             phase = 1;
         } else if (phase == 1 && !labelled) {
