@@ -195,7 +195,7 @@ fuzz-native:                ## libFuzzer (+ASan/UBSan) on the LLDP, D-Bus, Port 
 	    -mllvm -asan-globals=0 \
 	    -DNETOP_FUZZ_TARGET=$$id -DNETOP_VERSION='"fuzz"' -Inative/include native/fuzz/fuzz_targets.cpp \
 	    native/src/common.cpp native/src/log.cpp native/src/lldp.cpp native/src/l3.cpp native/src/netlink.cpp \
-	    native/src/dbus.cpp native/src/arp.cpp native/src/ethtool.cpp native/src/artifacts.cpp native/src/topology.cpp \
+	    native/src/dbus.cpp native/src/arp.cpp native/src/ethtool.cpp native/src/artifacts.cpp native/src/topology.cpp native/src/bounded.cpp \
 	    -o _build-fuzz/fuzz_$$name -lpthread || exit 1; \
 	  mkdir -p _build-fuzz/corpus_$$name; \
 	  if [ $$name = portdesc ]; then cp tests/fixtures/gpu_metrics_v1_8.bin _build-fuzz/corpus_$$name/; fi; \
