@@ -293,7 +293,7 @@ void Agent::refuse_uplinks() {
                      "scale-out / host RDMA NICs in the policy" +
                      (pol_named.empty() ? std::string()
                                         : std::string(" (a NIC whose policy-routing table is only its own rail's: "
-                                                      "--allow-policy-routed)")));
+                                                      "allowPolicyRouted in the policy, --allow-policy-routed)")));
 }
 
 }  // namespace netop::agent

@@ -171,6 +171,12 @@ def openapi_schema() -> dict:
                                "lower generation) moves RDMA at a fraction of the rail's rate.  Such a NIC is left\n"
                                "unconfigured and named in status.errors.  Reported in the agent's status either way.",
                 "type": "boolean"},
+            "allowPolicyRouted": {
+                "description": "Configure a selected NIC that has a default route in a per-NIC policy-routing table\n"
+                               "even when it holds the node's own address (the source its rule selects, or any\n"
+                               "address that is not a /30).  Such a NIC is how the node reaches a network, so by\n"
+                               "default it is refused like the node's uplink.",
+                "type": "boolean"},
         },
     }
     host_nic = {
@@ -212,6 +218,7 @@ def openapi_schema() -> dict:
             "requireFullPcieLink": {"description": "As amdScaleOut.requireFullPcieLink, for the host NICs (their own\n"
                                                    "PCIe link; they have no GPU).",
                                     "type": "boolean"},
+            "allowPolicyRouted": {"description": "As amdScaleOut.allowPolicyRouted, for the host NICs.", "type": "boolean"},
         },
         "required": ["layer"],
     }

@@ -137,6 +137,9 @@ class AmdScaleOutSpec:
     rdmaWait: str = ""
     # The NICs' RDMA driver (KMD) container, a privileged init container as for hostNic.driverImage
     driverImage: str = ""
+    # Configure a NIC whose default route lives in a per-NIC policy-routing table even when it
+    # holds the node's own address (refused by default, like the node's uplink)
+    allowPolicyRouted: bool = False
     validation: Optional[ValidationSpec] = None
     extra: Dict[str, Any] = field(default_factory=dict)
 
@@ -148,7 +151,7 @@ class AmdScaleOutSpec:
                "interfaces", "nicDrivers", "disableFirmwareLldp", "metricsPort", "gpuDirectRdma", "rcclEnv",
                "railTableBase", "rcclSocketIfname", "lldpCache", "verifyPeers", "lldpWait", "carrierWait", "keepConfigOnRestart",
                "railSwitchPattern", "minLinkSpeedGbps", "requireFullPcieLink", "checkPeerMtu", "handDcbxToHost",
-               "requireRdma", "rdmaWait", "driverImage", "validation")
+               "requireRdma", "rdmaWait", "driverImage", "allowPolicyRouted", "validation")
 
     def to_dict(self) -> dict:
         d: dict = {}
@@ -206,6 +209,8 @@ class AmdScaleOutSpec:
             d["rdmaWait"] = self.rdmaWait
         if self.driverImage:
             d["driverImage"] = self.driverImage
+        if self.allowPolicyRouted:
+            d["allowPolicyRouted"] = True
         if self.validation is not None:
             d["validation"] = self.validation.to_dict()
         d.update(copy.deepcopy(self.extra))
@@ -240,6 +245,7 @@ class AmdScaleOutSpec:
             requireRdma=d.pop("requireRdma", None),
             rdmaWait=d.pop("rdmaWait", "") or "",
             driverImage=d.pop("driverImage", "") or "",
+            allowPolicyRouted=bool(d.pop("allowPolicyRouted", False)),
             verifyPeers=bool(d.pop("verifyPeers", False)),
             lldpWait=d.pop("lldpWait", "") or "",
             carrierWait=d.pop("carrierWait", "") or "",
@@ -270,6 +276,7 @@ class HostNicSpec:
     includeGpuRails: bool = False  # discovery may take the NICs next to the GPUs (no amd-so policy)
     minLinkSpeedGbps: int = 0  # as amdScaleOut's, for the host NICs
     requireFullPcieLink: bool = False  # as amdScaleOut's (host NICs have no GPU: the NIC's link)
+    allowPolicyRouted: bool = False  # as amdScaleOut's
     extra: Dict[str, Any] = field(default_factory=dict)
 
     def to_dict(self) -> dict:
@@ -297,6 +304,8 @@ class HostNicSpec:
             d["minLinkSpeedGbps"] = self.minLinkSpeedGbps
         if self.requireFullPcieLink:
             d["requireFullPcieLink"] = True
+        if self.allowPolicyRouted:
+            d["allowPolicyRouted"] = True
         d.update(copy.deepcopy(self.extra))
         return d
 
@@ -313,7 +322,8 @@ class HostNicSpec:
                 checkPeerMtu=d.pop("checkPeerMtu", None),
                 includeGpuRails=bool(d.pop("includeGpuRails", False)),
                 minLinkSpeedGbps=int(d.pop("minLinkSpeedGbps", 0) or 0),
-                requireFullPcieLink=bool(d.pop("requireFullPcieLink", False)))
+                requireFullPcieLink=bool(d.pop("requireFullPcieLink", False)),
+                allowPolicyRouted=bool(d.pop("allowPolicyRouted", False)))
         s.extra = d
         return s
 

@@ -133,6 +133,8 @@ def agent_args(p: T.NetworkClusterPolicy) -> List[str]:
         args.append(f"--min-link-speed-gbps={so.minLinkSpeedGbps}")
     if so.requireFullPcieLink:
         args.append("--require-full-pcie")
+    if so.allowPolicyRouted:
+        args.append("--allow-policy-routed")
     if so.checkPeerMtu is False and so.layer == "L3":
         args.append("--check-peer-mtu=false")
     args.append(f"--link-state={ARTIFACT_DIR_CONTAINER}/{LINK_STATE_FILE}")
@@ -252,6 +254,8 @@ def host_nic_agent_args(p: T.NetworkClusterPolicy) -> List[str]:
         args.append(f"--min-link-speed-gbps={hn.minLinkSpeedGbps}")
     if hn.requireFullPcieLink:
         args.append("--require-full-pcie")
+    if hn.allowPolicyRouted:
+        args.append("--allow-policy-routed")
     if hn.keepConfigOnRestart:
         if hn.layer == "L3":  # its own cache beside the scale-out agent's
             args.append(f"--lldp-cache={ARTIFACT_DIR_CONTAINER}/{HOST_NIC_LLDP_CACHE_FILE}")

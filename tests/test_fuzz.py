@@ -41,6 +41,7 @@ so_strategy = st.fixed_dictionaries({}, optional={
     # round 3 / 4 fields
     "disableFirmwareLldp": st.booleans(),
     "handDcbxToHost": st.booleans(),
+    "allowPolicyRouted": st.booleans(),
     "checkPeerMtu": st.booleans(),
     "keepConfigOnRestart": st.booleans(),
     "minLinkSpeedGbps": mostly([0, 100, 400], [-1]),
@@ -56,6 +57,7 @@ host_nic_strategy = st.fixed_dictionaries({"layer": mostly(["L2", "L3"], [""])},
     "interfaces": st.lists(mostly(["ens9np0", "ens49np1"], ["x/y"]), max_size=2, unique=True),
     "nicDrivers": st.lists(st.sampled_from(["mlx5_core", "ionic"]), max_size=2, unique=True),
     "includeGpuRails": st.booleans(),
+    "allowPolicyRouted": st.booleans(),
     "checkPeerMtu": st.booleans(),
     "keepConfigOnRestart": st.booleans(),
     "verifyPeers": st.booleans(),

@@ -433,7 +433,7 @@ _AMD_VALUES = {
     "rcclSocketIfname": "eno1", "lldpCache": True, "verifyPeers": True, "lldpWait": "2m", "carrierWait": "45s",
     "keepConfigOnRestart": True, "railSwitchPattern": "leaf-r{rail}-.*", "minLinkSpeedGbps": 400, "requireFullPcieLink": True,
     "checkPeerMtu": False, "handDcbxToHost": True, "maxUnavailable": "25%", "requireRdma": True, "rdmaWait": "7m",
-    "driverImage": "reg/rdma-kmd:1",
+    "driverImage": "reg/rdma-kmd:1", "allowPolicyRouted": True,
     "validation": {"enabled": True, "minBusbw": 300, "minLink": 40, "gpus": 4, "image": "reg/val:1"},
     "tolerations": [{"key": "amd.com/gpu", "operator": "Exists", "effect": "NoSchedule"}],
     "priorityClassName": "system-node-critical",
@@ -443,7 +443,7 @@ _HOST_NIC_VALUES = {
     "enabled": True, "mode": "L3", "mtu": 4000, "nicDrivers": ["bnxt_en"], "driverImage": "reg/kmd:1",
     "interfaces": ["ens9np0"], "disableNetworkManager": True, "verifyPeers": True, "lldpWait": "45s", "carrierWait": "1m",
     "checkPeerMtu": False, "keepConfigOnRestart": True, "includeGpuRails": True, "minLinkSpeedGbps": 200,
-    "requireFullPcieLink": True,
+    "requireFullPcieLink": True, "allowPolicyRouted": True,
 }
 
 

@@ -311,6 +311,21 @@ def test_require_full_pcie_link_reaches_the_agent():
     assert T.NetworkClusterPolicy.from_dict(p.to_dict()).spec.amdScaleOut.requireFullPcieLink is True
 
 
+def test_allow_policy_routed_reaches_the_agent_from_either_policy_type():
+    """The agent's refusal of a policy-routed NIC that holds the node's address names its opt-in;
+    the policy carries it (amdScaleOut / hostNic.allowPolicyRouted), off by default."""
+    from network_operator_amd.operator import reconciler as R
+
+    p = T.new_policy("x", layer="L3", allowPolicyRouted=True)
+    assert "--allow-policy-routed" in agent_args(p)
+    assert T.NetworkClusterPolicy.from_dict(p.to_dict()).spec.amdScaleOut.allowPolicyRouted is True
+    assert "--allow-policy-routed" not in agent_args(T.new_policy("x", layer="L3"))
+    hn = T.new_host_nic_policy("h", layer="L3", allowPolicyRouted=True)
+    assert "--allow-policy-routed" in R.host_nic_agent_args(hn)
+    assert T.NetworkClusterPolicy.from_dict(hn.to_dict()).spec.hostNic.allowPolicyRouted is True
+    assert "--allow-policy-routed" not in R.host_nic_agent_args(T.new_host_nic_policy("h", layer="L3"))
+
+
 def test_agent_args_mi355x_options():
     p = T.new_policy("x", layer="L3", xgmiCheck=True, lldpAnnounce=False, interfaces=["ens1", "ens2"],
                      nicDrivers=["mlx5_core"])
