@@ -262,10 +262,21 @@ def test_ipc_open_refuses_a_gpu_it_cannot_reach_before_mapping(cuda_device):
     torch.cuda.synchronize()  # no sticky error left behind
 
 
-def _old_harness(world, args, limit_s):
+def _pipe_write_blocked(pid):
+    """True / False from the kernel's wait channel; None where it does not say (no wchan)."""
+    try:
+        w = Path(f"/proc/{pid}/wchan").read_text().strip()
+    except OSError:
+        return None
+    return None if w in ("", "0") else "pipe_write" in w
+
+
+def _old_harness(world, args, limit_s, blocked_ranks=()):
     """The harness shape of round 3 before its fix: ranks' stdout and stderr through pipes, read
     one rank at a time (communicate() on rank 0, then rank 1, ...).  Returns (hung ranks, bytes
-    each rank managed to write to stderr)."""
+    each rank managed to write to stderr).  `blocked_ranks`: the limit starts once these are
+    blocked writing their pipes (the kernel's wait channel says so), not at the spawn: on a
+    loaded machine the ranks' own start (import torch) can take longer than the limit."""
     import time
 
     store = Path(os.environ.get("TMPDIR", "/tmp")) / f"netop-old-harness-{os.getpid()}"
@@ -273,7 +284,17 @@ def _old_harness(world, args, limit_s):
                PYTHONPATH=str(ROOT), NETOP_INIT_FILE=str(store))
     procs = [subprocess.Popen([sys.executable, str(WORKER), *args], env=dict(env, RANK=str(r)),
                               stdout=subprocess.PIPE, stderr=subprocess.PIPE) for r in range(world)]
-    deadline = time.monotonic() + limit_s
+    t_start = time.monotonic()
+    deadline = t_start + limit_s
+    while blocked_ranks and time.monotonic() < t_start + 120 and all(p.poll() is None for p in procs):
+        states = [_pipe_write_blocked(procs[r].pid) for r in blocked_ranks]
+        if None in states:  # no wait channel here: the limit runs from the spawn, with the old margin
+            deadline = t_start + max(limit_s, 8)
+            break
+        if all(states):
+            deadline = time.monotonic() + limit_s
+            break
+        time.sleep(0.05)
     hung = []
     try:
         for r, p in enumerate(procs):
@@ -298,7 +319,7 @@ def test_round3_hang_reproduced_pipes_read_rank_by_rank_deadlock():
     gloo barrier.  Read through pipes rank by rank, rank 0 waits at the barrier for rank 1,
     rank 1 is blocked in write() on its full pipe (exactly the pipe's 64 KiB got through), and
     the harness waits on rank 0: nothing moves until the limit kills it."""
-    hung, written = _old_harness(3, ["chatty", str(256 << 10)], limit_s=8)
+    hung, written = _old_harness(3, ["chatty", str(256 << 10)], limit_s=3, blocked_ranks=(1, 2))
     assert hung == [0], (hung, written)
     assert written[1] == written[2] == 65536, written  # the pipe's capacity, then blocked
 
