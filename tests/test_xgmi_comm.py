@@ -263,12 +263,16 @@ def test_ipc_open_refuses_a_gpu_it_cannot_reach_before_mapping(cuda_device):
 
 
 def _pipe_write_blocked(pid):
-    """True / False from the kernel's wait channel; None where it does not say (no wchan)."""
+    """True / False from the kernel's wait channel; None where it does not say (no wchan, or a
+    sleeping process without one).  A running process has none: not blocked (yet)."""
     try:
         w = Path(f"/proc/{pid}/wchan").read_text().strip()
-    except OSError:
+        state = Path(f"/proc/{pid}/stat").read_text().rsplit(")", 1)[1].split()[0]
+    except (OSError, IndexError):
         return None
-    return None if w in ("", "0") else "pipe_write" in w
+    if w in ("", "0"):
+        return False if state == "R" else None
+    return "pipe_write" in w
 
 
 def _old_harness(world, args, limit_s, blocked_ranks=()):
@@ -285,16 +289,12 @@ def _old_harness(world, args, limit_s, blocked_ranks=()):
     procs = [subprocess.Popen([sys.executable, str(WORKER), *args], env=dict(env, RANK=str(r)),
                               stdout=subprocess.PIPE, stderr=subprocess.PIPE) for r in range(world)]
     t_start = time.monotonic()
-    deadline = t_start + limit_s
-    while blocked_ranks and time.monotonic() < t_start + 120 and all(p.poll() is None for p in procs):
-        states = [_pipe_write_blocked(procs[r].pid) for r in blocked_ranks]
-        if None in states:  # no wait channel here: the limit runs from the spawn, with the old margin
-            deadline = t_start + max(limit_s, 8)
-            break
-        if all(states):
-            deadline = time.monotonic() + limit_s
+    # (a kernel that never names the wait channel costs this loop's 60 s, not a wrong verdict)
+    while blocked_ranks and time.monotonic() < t_start + 60 and all(p.poll() is None for p in procs):
+        if all(_pipe_write_blocked(procs[r].pid) for r in blocked_ranks):
             break
         time.sleep(0.05)
+    deadline = time.monotonic() + limit_s
     hung = []
     try:
         for r, p in enumerate(procs):
