@@ -498,6 +498,10 @@ class Agent {
     int64_t holddown_until_ = 0;
     int label_suppressed_ = 0;
     int label_withdrawals_ = 0;
+    // Bounded sysfs reads that missed --sysfs-read-timeout, by what was read ("gpu_metrics",
+    // "pcie", "kfd", "topology"): a wedged SMU or a function in error recovery, as a counter.
+    std::map<std::string, uint64_t> late_reads_;
+    uint64_t late_reads_total() const;
     // GPU rails whose NIC has no RDMA device (its RDMA driver is not loaded): RCCL could only use
     // them over TCP sockets.  Reported always; fatal with --require-gdr.
     std::vector<std::string> no_rdma_;

@@ -259,6 +259,7 @@ void Agent::ensure_pcie() {
     auto got = pcie_call_.wait(prefetch_deadline_);
     if (!got) {
         pcie_late_ = true;
+        ++late_reads_["pcie"];
         NLOG_W("The PCIe link state of the scale-out NICs did not answer in %s: not checked%s",
                format_go_duration(cfg_.sysfs_read_timeout_ns).c_str(),
                cfg_.require_full_pcie ? " (--require-full-pcie: the NICs wait for it)" : "");
@@ -411,6 +412,7 @@ void Agent::join_xgmi() {
     auto x = xgmi_call_.wait(prefetch_deadline_);
     xgmi_call_ = {};
     if (!x) {
+        ++late_reads_["kfd"];
         const std::string why = "the KFD topology (" + path_join(cfg_.sysfs_root.empty() ? topo::sysfs_root() : cfg_.sysfs_root,
                                                                  "class/kfd") +
                                 ") did not answer in " + format_go_duration(cfg_.sysfs_read_timeout_ns);
@@ -466,6 +468,7 @@ void Agent::finish_xgmi_health() {
                 xgmi_health_.push_back(std::move(l));
             }
         }
+        for (const auto& l : xgmi_health_) late_reads_["gpu_metrics"] += l.late ? 1 : 0;
         note_xgmi_sample();
         const std::string kfd_error = xgmi_error_;  // a late KFD read (dry run) stays reported
         xgmi_error_ = xgmi_health_problem();

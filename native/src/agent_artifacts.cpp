@@ -196,6 +196,7 @@ const std::string& Agent::topo_xml() {
         try {
             auto r = topo_call_.wait(deadline);
             if (!r) {
+                if (!topo_late_) ++late_reads_["topology"];
                 if (!topo_late_)
                     NLOG_W("The RCCL topology file was not generated within %s (a PCI attribute read stalled?): "
                            "rccl.env names no NCCL_TOPO_FILE until it is (RCCL then reads the topology itself)",

@@ -97,6 +97,12 @@ void Agent::log_results() {
 
 int Agent::metrics_port() const { return httpd_ ? httpd_->port() : 0; }
 
+uint64_t Agent::late_reads_total() const {
+    uint64_t n = 0;
+    for (const auto& [what, count] : late_reads_) n += count;
+    return n;
+}
+
 std::string Agent::render_metrics() const {
     std::string o;
     auto metric = [&](const char* name, const char* type, const char* help) {
@@ -155,6 +161,13 @@ std::string Agent::render_metrics() const {
     metric("netop_agent_label_suppressed_total", "counter",
            "recoveries not republished because the node flapped again within --label-holddown");
     o += strfmt("netop_agent_label_suppressed_total %d\n", label_suppressed_);
+    metric("netop_agent_sysfs_reads_late_total", "counter",
+           "sysfs reads that did not answer within --sysfs-read-timeout (a wedged SMU, a function in PCIe error recovery)");
+    for (const char* what : {"gpu_metrics", "pcie", "kfd", "topology"}) {
+        auto it = late_reads_.find(what);
+        o += strfmt("netop_agent_sysfs_reads_late_total{read=\"%s\"} %llu\n", what,
+                    (unsigned long long)(it == late_reads_.end() ? 0 : it->second));
+    }
     if (cfg_.require_rdma) {
         metric("netop_agent_nic_rdma", "gauge", "1 when the NIC has an RDMA device (--require-rdma: the label waits for every NIC's)");
         for (const auto& n : nics_)

@@ -3334,6 +3334,86 @@ TEST(agent_monitor_reads_gpu_metrics_on_a_worker_and_dampens_a_single_down_sampl
     }
 }
 
+namespace {
+size_t count_dir(const std::string& dir) {
+    size_t n = 0;
+    for (const auto& e : std::filesystem::directory_iterator(dir)) (void)e, ++n;
+    return n;
+}
+}  // namespace
+
+TEST(agent_monitor_health_worker_soak_leaves_no_threads_or_descriptors_behind) {
+    // The monitor's xGMI / PCIe poll runs on a detached worker per sample, signalled through an
+    // eventfd: a poll every 100 us for a second is thousands of workers.  Threads and descriptors
+    // stay flat, and the monitor still acts on a link that goes down afterwards.
+    Fixture f;
+    f.cfg.sysfs_root = f.tmp.path + "/sys/";
+    f.cfg.xgmi_expect_links = 0;
+    f.cfg.xgmi_health_interval_ns = 100000;  // 100 us
+    f.cfg.require_full_pcie = true;          // the PCIe half of the sample too
+    f.cfg.monitor_tick_ns = 1000000;
+    write_two_gpu_kfd(f.tmp);
+    Pipe stop;
+    agent::Agent a(f.cfg, f.ops, f.all_valid(), f.nm());
+    size_t threads0 = 0, fds0 = 0, threads1 = 0, fds1 = 0;
+    int64_t t_base = 0, t_down = 0;
+    bool withdrawn = false;
+    a.on_monitor_tick = [&](int tick) {
+        if (tick == 5) {
+            threads0 = count_dir("/proc/self/task");
+            fds0 = count_dir("/proc/self/fd");
+            t_base = mono_ns();
+        } else if (t_base && !t_down && mono_ns() - t_base > 1000000000LL) {
+            threads1 = count_dir("/proc/self/task");
+            fds1 = count_dir("/proc/self/fd");
+            set_link(f.tmp, "0000:10:00.0", 2, false);
+            t_down = mono_ns();
+        } else if (t_down && !path_exists(f.cfg.labels.path())) {
+            withdrawn = true;
+            stop.fire();
+        } else if (t_down && mono_ns() - t_down > 2000000000LL) {
+            stop.fire();
+        }
+    };
+    a.run(stop.fd[0]);
+    CHECK(threads0 > 0 && fds0 > 0);
+    CHECK(threads1 <= threads0 + 2);  // (a worker may be running at either look)
+    CHECK(fds1 <= fds0 + 2);
+    CHECK(withdrawn);
+    CHECK(a.render_metrics().find("netop_agent_sysfs_reads_late_total{read=\"gpu_metrics\"} 0\n") != std::string::npos);
+}
+
+TEST(agent_counts_sysfs_reads_that_miss_the_deadline) {
+    // GPU 0000:20:00.0's gpu_metrics never answers (a FIFO nobody writes, as a wedged SMU): every
+    // sample counts it late, by what was read, in netop_agent_sysfs_reads_late_total.
+    Fixture f;
+    f.cfg.sysfs_root = f.tmp.path + "/sys/";
+    f.cfg.xgmi_expect_links = 0;
+    f.cfg.xgmi_health_interval_ns = 2000000;
+    f.cfg.sysfs_read_timeout_ns = 20000000;  // 20 ms
+    f.cfg.monitor_tick_ns = 1000000;
+    write_two_gpu_kfd(f.tmp);
+    const std::string fifo = f.tmp.path + "/sys/bus/pci/devices/0000:20:00.0/gpu_metrics";
+    ::unlink(fifo.c_str());
+    CHECK_EQ(::mkfifo(fifo.c_str(), 0600), 0);
+    Pipe stop;
+    agent::Agent a(f.cfg, f.ops, f.all_valid(), f.nm());
+    std::string metrics;
+    const int64_t t0 = mono_ns();
+    a.on_monitor_tick = [&](int) {
+        metrics = a.render_metrics();
+        if (metrics.find("netop_agent_sysfs_reads_late_total{read=\"gpu_metrics\"} 3\n") != std::string::npos ||
+            mono_ns() - t0 > 3000000000LL)
+            stop.fire();
+    };
+    a.run(stop.fd[0]);
+    int w = ::open(fifo.c_str(), O_WRONLY | O_NONBLOCK | O_CLOEXEC);  // let the blocked reader go
+    if (w >= 0) ::close(w);
+    CHECK(metrics.find("netop_agent_sysfs_reads_late_total{read=\"gpu_metrics\"} 3\n") != std::string::npos);
+    CHECK(metrics.find("netop_agent_sysfs_reads_late_total{read=\"pcie\"} 0\n") != std::string::npos);
+    CHECK(!path_exists(f.cfg.labels.path()));  // a GPU whose links cannot be read is not labelled
+}
+
 TEST(agent_require_rdma_withdraws_the_label_when_a_device_goes_away_and_follows_a_renumbered_one) {
     // After readiness the RDMA driver is unloaded under a labelled node: the label goes at the
     // next look (the health interval), with a fault reason (not start-up); the driver is loaded
