@@ -105,10 +105,8 @@ bool Agent::nic_healthy(const NicState& n) const {
 
 bool Agent::apply_health(const HealthSample& s) {
     bool changed = false;
-    const uint64_t late_before = late_reads_total();
     for (const auto& h : s.xgmi) late_reads_["gpu_metrics"] += h.late ? 1 : 0;
     for (bool l : s.pcie_late) late_reads_["pcie"] += l ? 1 : 0;
-    if (late_reads_total() != late_before) changed = true;  // (status and metrics say so at once)
     if (s.xgmi_read) {
         const std::string before = xgmi_error_;
         xgmi_health_ = s.xgmi;
@@ -351,7 +349,9 @@ void Agent::monitor(int stop_fd) {
         if (poll.valid() && poll.done()) {
             uint64_t n = 0;
             (void)!::read(done->fd, &n, sizeof n);
+            const uint64_t late_before = late_reads_total();
             if (auto s = poll.wait(0)) changed |= apply_health(*s);
+            if (!changed && late_reads_total() != late_before) write_status();  // the late-read counter, at once
             poll = {};
             next_health = mono_ns() + cfg_.xgmi_health_interval_ns;
         }
