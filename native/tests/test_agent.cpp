@@ -3343,44 +3343,46 @@ size_t count_dir(const std::string& dir) {
 }  // namespace
 
 TEST(agent_monitor_health_worker_soak_leaves_no_threads_or_descriptors_behind) {
-    // The monitor's xGMI / PCIe poll runs on a detached worker per sample, signalled through an
-    // eventfd: a poll every 100 us for a second is thousands of workers.  Threads and descriptors
-    // stay flat, and the monitor still acts on a link that goes down afterwards.
-    Fixture f;
-    f.cfg.sysfs_root = f.tmp.path + "/sys/";
-    f.cfg.xgmi_expect_links = 0;
-    f.cfg.xgmi_health_interval_ns = 100000;  // 100 us
-    f.cfg.require_full_pcie = true;          // the PCIe half of the sample too
-    f.cfg.monitor_tick_ns = 1000000;
-    write_two_gpu_kfd(f.tmp);
-    Pipe stop;
-    agent::Agent a(f.cfg, f.ops, f.all_valid(), f.nm());
-    size_t threads0 = 0, fds0 = 0, threads1 = 0, fds1 = 0;
-    int64_t t_base = 0, t_down = 0;
+    // The monitor's xGMI / PCIe poll runs on detached workers per sample, signalled through an
+    // eventfd: a poll every millisecond for a second is a thousand samples.  Once the agent is
+    // gone, so are its threads and descriptors, and the monitor still acted on a link that went
+    // down after the soak.
+    const size_t threads_before = count_dir("/proc/self/task"), fds_before = count_dir("/proc/self/fd");
     bool withdrawn = false;
-    a.on_monitor_tick = [&](int tick) {
-        if (tick == 5) {
-            threads0 = count_dir("/proc/self/task");
-            fds0 = count_dir("/proc/self/fd");
-            t_base = mono_ns();
-        } else if (t_base && !t_down && mono_ns() - t_base > 1000000000LL) {
-            threads1 = count_dir("/proc/self/task");
-            fds1 = count_dir("/proc/self/fd");
-            set_link(f.tmp, "0000:10:00.0", 2, false);
-            t_down = mono_ns();
-        } else if (t_down && !path_exists(f.cfg.labels.path())) {
-            withdrawn = true;
-            stop.fire();
-        } else if (t_down && mono_ns() - t_down > 2000000000LL) {
-            stop.fire();
-        }
-    };
-    a.run(stop.fd[0]);
-    CHECK(threads0 > 0 && fds0 > 0);
-    CHECK(threads1 <= threads0 + 2);  // (a worker may be running at either look)
-    CHECK(fds1 <= fds0 + 2);
+    {
+        Fixture f;
+        f.cfg.sysfs_root = f.tmp.path + "/sys/";
+        f.cfg.xgmi_expect_links = 0;
+        f.cfg.xgmi_health_interval_ns = 1000000;  // 1 ms
+        f.cfg.require_full_pcie = true;           // the PCIe half of the sample too
+        f.cfg.monitor_tick_ns = 1000000;
+        write_two_gpu_kfd(f.tmp);
+        Pipe stop;
+        agent::Agent a(f.cfg, f.ops, f.all_valid(), f.nm());
+        int64_t t_base = 0, t_down = 0;
+        a.on_monitor_tick = [&](int tick) {
+            if (tick == 1) {
+                t_base = mono_ns();
+            } else if (t_base && !t_down && mono_ns() - t_base > 1000000000LL) {
+                set_link(f.tmp, "0000:10:00.0", 2, false);
+                t_down = mono_ns();
+            } else if (t_down && !path_exists(f.cfg.labels.path())) {
+                withdrawn = true;
+                stop.fire();
+            } else if (t_down && mono_ns() - t_down > 3000000000LL) {
+                stop.fire();
+            }
+        };
+        a.run(stop.fd[0]);
+        CHECK(a.render_metrics().find("netop_agent_sysfs_reads_late_total{read=\"gpu_metrics\"} 0\n") != std::string::npos);
+    }
     CHECK(withdrawn);
-    CHECK(a.render_metrics().find("netop_agent_sysfs_reads_late_total{read=\"gpu_metrics\"} 0\n") != std::string::npos);
+    // Detached workers finish on their own: give the last ones a moment.
+    const int64_t until = mono_ns() + 3000000000LL;
+    while ((count_dir("/proc/self/task") > threads_before || count_dir("/proc/self/fd") > fds_before) && mono_ns() < until)
+        ::usleep(5000);
+    CHECK(count_dir("/proc/self/task") <= threads_before);
+    CHECK(count_dir("/proc/self/fd") <= fds_before);
 }
 
 TEST(agent_counts_sysfs_reads_that_miss_the_deadline) {

@@ -76,7 +76,8 @@ def test_first_announce_waits_for_operstate_up():
     that fix, 2 of 10 runs on a fresh machine took ~1.03 s)."""
     lat = [netns.run_isolated(n_nics=8, seed=400 + k, interval="30s", fast_start=True, verbose=0)["latency_s"]
            for k in range(6)]
-    assert all(x is not None and x < 0.5 for x in lat), lat
+    # (the fallback this pins is the 1 s re-announce, ~1.03 s; a loaded machine adds tenths)
+    assert all(x is not None and x < 0.9 for x in lat), lat
 
 
 def test_l3_legacy_switch_periodic_only():
