@@ -3105,6 +3105,96 @@ TEST(agent_require_rdma_devices_that_appear_during_the_bring_up_are_in_rccl_env_
     CHECK(env && env->find("NCCL_IB_HCA==mlx5_0:1,mlx5_1:1,mlx5_2:1\n") != std::string::npos);
 }
 
+TEST(agent_l3_label_and_rccl_env_follow_random_rdma_driver_reloads_and_flaps) {
+    // Property (L3, --require-rdma, monitor): under any sequence of RDMA driver unloads, reloads
+    // (which may number a device anew) and cable pulls, once the agent has caught up:
+    //   the label is there exactly when every NIC has carrier and an RDMA device;
+    //   while it is, rccl.env names exactly the current devices, in GPU order;
+    //   while a device is missing, there is no rccl.env (no rail left to TCP sockets).
+    // 120 random steps for each of three seeds.
+    for (uint64_t seed : {0x0F1E2D3C4B5A6978ull, 0x1111222233334444ull, 0x9999AAAABBBBCCCCull}) {
+        RdmaFixture f;
+        f.cfg.xgmi_health_interval_ns = 1000000;  // a labelled node looks for its devices every 1 ms
+        const std::vector<std::string> nics = {"ens0", "ens1", "ens2"};
+        std::map<std::string, bool> carrier;
+        std::map<std::string, std::string> dev;
+        int next_dev = 0;
+        for (const auto& n : nics) {
+            carrier[n] = true;
+            dev[n] = "mlx5_" + std::to_string(next_dev++);
+            f.bind(n, dev[n]);
+        }
+        uint64_t rng = seed;
+        auto next = [&] {
+            rng ^= rng << 13;
+            rng ^= rng >> 7;
+            rng ^= rng << 17;
+            return rng;
+        };
+        Pipe stop;
+        agent::Agent a(f.cfg, f.ops, f.all_valid(), f.nm());
+        int steps = 0, mismatches = 0, labelled_states = 0;
+        int64_t t_step = 0;
+        std::string first_bad;
+        a.on_monitor_tick = [&](int) {
+            if (t_step && mono_ns() - t_step < 20000000LL) return;  // 20 ms to catch up
+            if (t_step) {  // check the state the last step led to
+                const bool all_rdma = std::all_of(nics.begin(), nics.end(), [&](const std::string& n) { return !dev[n].empty(); });
+                const bool want = all_rdma && std::all_of(nics.begin(), nics.end(), [&](const std::string& n) { return carrier[n]; });
+                const bool label = path_exists(f.cfg.labels.path());
+                auto env = read_file(f.cfg.rccl_env);
+                std::string bad;
+                if (label != want) bad = strfmt("label %d, want %d", label, want);
+                if (!all_rdma && env) bad += " rccl.env while a device is missing";
+                if (label) {
+                    std::vector<std::string> hcas;
+                    for (const auto& n : nics) hcas.push_back(dev[n] + ":1");
+                    const std::string line = "NCCL_IB_HCA==" + join(hcas, ",") + "\n";
+                    if (!env || env->find(line) == std::string::npos) bad += " rccl.env does not name " + join(hcas, ",");
+                }
+                labelled_states += want;
+                if (!bad.empty()) {
+                    if (!mismatches) first_bad = strfmt("step %d:", steps) + bad;
+                    ++mismatches;
+                }
+                if (++steps >= 120) {
+                    stop.fire();
+                    return;
+                }
+            }
+            // Half the steps repair something broken (so the walk keeps coming back to a ready
+            // node), the others break or repair at random.
+            std::vector<std::string> broken;
+            for (const auto& m : nics)
+                if (!carrier[m] || dev[m].empty()) broken.push_back(m);
+            const bool repair = !broken.empty() && next() % 2 == 0;
+            const std::string& n = repair ? *std::find(nics.begin(), nics.end(), broken[next() % broken.size()])
+                                          : nics[next() % nics.size()];
+            if (repair ? !carrier[n] && (dev[n].size() || next() % 2) : next() % 3 == 0) {
+                carrier[n] = !carrier[n];
+                f.ops.set_carrier(n, carrier[n]);
+            } else if (dev[n].empty()) {  // the driver loads again; a reload may renumber
+                dev[n] = next() % 2 ? "mlx5_" + std::to_string(next_dev++) : "mlx5_" + std::to_string(&n - &nics[0]);
+                bool taken = false;
+                for (const auto& m : nics)
+                    if (&m != &n && dev[m] == dev[n]) taken = true;
+                if (taken) dev[n] = "mlx5_" + std::to_string(next_dev++);
+                f.bind(n, dev[n]);
+            } else {  // unloaded
+                std::filesystem::remove_all(f.tmp.path + "/sys/class/net/" + n + "/device/infiniband");
+                dev[n].clear();
+            }
+            t_step = mono_ns();
+        };
+        a.run(stop.fd[0]);
+        if (mismatches) fprintf(stderr, "seed %llx, %s\n", (unsigned long long)seed, first_bad.c_str());
+        CHECK_EQ(mismatches, 0);
+        CHECK_EQ(steps, 120);
+        if (labelled_states == 0 || labelled_states >= steps) fprintf(stderr, "seed %llx: %d labelled states\n", (unsigned long long)seed, labelled_states);
+        CHECK(labelled_states > 0 && labelled_states < steps);  // the sequence visits both states
+    }
+}
+
 TEST(agent_require_rdma_past_the_wait_names_the_fault) {
     RdmaFixture f;
     f.cfg.rdma_wait_ns = 0;
