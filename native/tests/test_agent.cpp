@@ -3506,6 +3506,100 @@ TEST(agent_counts_sysfs_reads_that_miss_the_deadline) {
     CHECK(!path_exists(f.cfg.labels.path()));  // a GPU whose links cannot be read is not labelled
 }
 
+TEST(agent_label_holddown_and_xgmi_dampening_follow_random_link_and_carrier_flaps) {
+    // Property (L3, monitor, --label-holddown 100 ms, --xgmi-down-samples 2): under any sequence
+    // of cable pulls and xGMI links going down / up, checked 10 ms or 150 ms after each step:
+    //   unhealthy (a NIC without carrier or a GPU link down): no label;
+    //   healthy and never withdrawn: the label (the first publication is not held);
+    //   healthy after a withdrawal: the label only once the hold-down has passed since the last
+    //   change (so not at 10 ms, and at 150 ms).
+    // 60 random steps for each of two seeds.
+    for (uint64_t seed : {0x2468ACE013579BDFull, 0x0DDBA11C0FFEE000ull}) {
+        Fixture f;
+        f.cfg.sysfs_root = f.tmp.path + "/sys/";
+        f.cfg.xgmi_expect_links = 0;
+        f.cfg.xgmi_health_interval_ns = 1000000;
+        f.cfg.xgmi_down_samples = 2;
+        f.cfg.label_holddown_ns = 100000000;  // 100 ms
+        f.cfg.monitor_tick_ns = 1000000;
+        write_two_gpu_kfd(f.tmp);
+        const std::vector<std::string> nics = {"ens0", "ens1", "ens2"};
+        const std::vector<const char*> gpus = {"0000:10:00.0", "0000:20:00.0"};
+        std::map<std::string, bool> carrier, link;
+        for (const auto& n : nics) carrier[n] = true;
+        for (const char* g : gpus) link[g] = true;
+        uint64_t rng = seed;
+        auto next = [&] {
+            rng ^= rng << 13;
+            rng ^= rng >> 7;
+            rng ^= rng << 17;
+            return rng;
+        };
+        auto healthy = [&] {
+            return std::all_of(nics.begin(), nics.end(), [&](const std::string& n) { return carrier[n]; }) &&
+                   std::all_of(gpus.begin(), gpus.end(), [&](const char* g) { return link[g]; });
+        };
+        Pipe stop;
+        agent::Agent a(f.cfg, f.ops, f.all_valid(), f.nm());
+        bool labelled = true;  // the model: the start labels a healthy node
+        int withdrawals = 0, steps = 0, mismatches = 0, held = 0;
+        int64_t t_step = 0, wait = 0;
+        std::string first_bad;
+        a.on_monitor_tick = [&](int) {
+            if (t_step && mono_ns() - t_step < wait) return;
+            if (t_step) {
+                bool want;
+                if (!healthy())
+                    want = false;
+                else if (labelled || withdrawals == 0)
+                    want = true;
+                else
+                    want = wait > f.cfg.label_holddown_ns;  // healthy since this step
+                held += healthy() && !want;
+                if (want) labelled = true;
+                const bool label = path_exists(f.cfg.labels.path());
+                if (label != want) {
+                    if (!mismatches)
+                        first_bad = strfmt("step %d (waited %lld ms, %d withdrawal(s)): label %d, want %d", steps,
+                                           (long long)(wait / 1000000), withdrawals, label, want);
+                    ++mismatches;
+                }
+                if (++steps >= 60) {
+                    stop.fire();
+                    return;
+                }
+            }
+            // A balanced walk: half the steps repair something broken.
+            std::vector<int> broken;  // 0..2 NICs, 3..4 GPUs
+            for (int i = 0; i < 3; ++i)
+                if (!carrier[nics[size_t(i)]]) broken.push_back(i);
+            for (int i = 0; i < 2; ++i)
+                if (!link[gpus[size_t(i)]]) broken.push_back(3 + i);
+            const int what = !broken.empty() && next() % 2 ? broken[next() % broken.size()] : int(next() % 5);
+            if (what < 3) {
+                const std::string& n = nics[size_t(what)];
+                carrier[n] = !carrier[n];
+                f.ops.set_carrier(n, carrier[n]);
+            } else {
+                const char* g = gpus[size_t(what - 3)];
+                link[g] = !link[g];
+                set_link(f.tmp, g, 3, link[g]);
+            }
+            if (!healthy() && labelled) {
+                labelled = false;
+                ++withdrawals;
+            }
+            wait = next() % 2 ? 10000000LL : 150000000LL;
+            t_step = mono_ns();
+        };
+        a.run(stop.fd[0]);
+        if (mismatches) fprintf(stderr, "seed %llx, %s\n", (unsigned long long)seed, first_bad.c_str());
+        CHECK_EQ(mismatches, 0);
+        CHECK_EQ(steps, 60);
+        CHECK(withdrawals > 0 && held > 0);  // the walk withdrew the label and held it back
+    }
+}
+
 TEST(agent_require_rdma_withdraws_the_label_when_a_device_goes_away_and_follows_a_renumbered_one) {
     // After readiness the RDMA driver is unloaded under a labelled node: the label goes at the
     // next look (the health interval), with a fault reason (not start-up); the driver is loaded
