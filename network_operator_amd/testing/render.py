@@ -30,7 +30,9 @@ class RenderError(Exception):
 # ---------------------------------------------------------------------------
 # Helm (Go template subset)
 # ---------------------------------------------------------------------------
-_ACTION = re.compile(r"{{(-?)\s*(.*?)\s*(-?)}}", re.S)
+# An action may hold a raw string (`...`), whose text may itself contain "{{" / "}}" (how a chart
+# writes Prometheus' own {{ $labels.x }} templates).
+_ACTION = re.compile(r"{{(-?)\s*((?:`[^`]*`|.)*?)\s*(-?)}}", re.S)
 
 
 def _tokenize(src: str):
@@ -130,7 +132,7 @@ def _split_pipeline(expr: str) -> List[str]:
             if ch == q:
                 q = None
             continue
-        if ch in "\"'":
+        if ch in "\"'`":
             q = ch
         elif ch == "(":
             depth += 1
@@ -153,7 +155,7 @@ def _terms(cmd: str) -> List[str]:
             if ch == q:
                 q = None
             continue
-        if ch in "\"'":
+        if ch in "\"'`":
             q = ch
             cur += ch
             continue
@@ -175,6 +177,8 @@ def _terms(cmd: str) -> List[str]:
 def _eval_term(t: str, ctx: _Ctx):
     if t.startswith("(") and t.endswith(")"):
         return _eval_pipeline(t[1:-1], ctx)
+    if t[0] == "`" and t.endswith("`") and len(t) >= 2:  # a raw string: its text as it is
+        return t[1:-1]
     if t[0] in "\"'":
         return shlex.split(t)[0]
     if re.fullmatch(r"-?\d+", t):

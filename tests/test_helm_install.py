@@ -525,3 +525,25 @@ def test_chart_refuses_to_give_the_gpu_rails_to_two_policies():
     assert "includeGpuRails" in str(e.value) and "config.amd" in str(e.value)
     helm_template(CHART, {"config": {"hostNic": {"enabled": True, "includeGpuRails": True}}}, NS)  # alone: fine
 
+
+
+def test_monitoring_objects_render_only_when_enabled_and_keep_prometheus_templates():
+    """`monitoring.enabled` renders the kustomize tree's prometheus/ objects for Helm users: the
+    operator's ServiceMonitor, the agents' PodMonitor and the alert rules, named and placed like
+    the release's other objects.  The alerts' own {{ $labels.x }} / {{ $value }} templates reach
+    Prometheus as written (Helm raw strings), and the rules are the generator's."""
+    kinds = {"ServiceMonitor", "PodMonitor", "PrometheusRule"}
+    plain = helm_template(CHART, {}, NS)
+    assert not [d for d in plain if d["kind"] in kinds]
+    docs = [d for d in helm_template(CHART, {"monitoring": {"enabled": True}}, NS) if d["kind"] in kinds]
+    assert sorted(d["kind"] for d in docs) == sorted(kinds)
+    for d in docs:
+        assert d["metadata"]["name"].startswith(M.PREFIX) and d["metadata"]["namespace"] == NS
+    rules = next(d for d in docs if d["kind"] == "PrometheusRule")
+    assert rules["spec"] == M.prometheus_rules()["spec"]  # every alert, its {{ $labels.x }} text intact
+    summaries = [r["annotations"]["summary"] for g in rules["spec"]["groups"] for r in g["rules"]]
+    assert any("{{ $labels.nic }}" in s for s in summaries) and any("{{ $value }}" in s for s in summaries)
+    svc = next(d for d in helm_template(CHART, {}, NS) if d["kind"] == "Service" and d["metadata"]["name"].endswith("metrics"))
+    monitor = next(d for d in docs if d["kind"] == "ServiceMonitor")
+    assert monitor["spec"]["endpoints"][0]["port"] in [p["name"] for p in svc["spec"]["ports"]]
+    assert monitor["spec"]["selector"]["matchLabels"].items() <= svc["metadata"]["labels"].items()
