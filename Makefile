@@ -4,6 +4,7 @@ JOBS   ?= 8
 IMG_OPERATOR ?= amd/amd-network-operator:0.1.0
 IMG_AGENT    ?= amd/amd-network-linkdiscovery:0.1.0
 IMG_VALIDATION ?= amd/amd-network-validation:0.1.0
+IMG_RDMA_DRIVER ?= amd/amd-network-rdma-driver:0.1.0
 
 KUBECTL ?= kubectl
 CONTAINER_TOOL ?= docker
@@ -18,7 +19,7 @@ BUNDLE_IMG ?= amd/amd-network-operator-bundle:v$(VERSION)
         images sanitize tsan clean fmt vet lint fuzz run build-installer install uninstall deploy undeploy bundle \
         bundle-build helm-package-chart fuzz-native check-hardening catalog-build catalog-push bundle-push \
         generate test-e2e lint-fix operator-image operator-push discover-image discover-push validation-image \
-        validation-push docker-buildx helm-update-dependencies helm-push-chart
+        validation-push rdma-driver-image rdma-driver-push docker-buildx helm-update-dependencies helm-push-chart
 
 all: build
 
@@ -174,6 +175,12 @@ validation-image:           ## fabric validation Job image (RCCL + HIP, gfx950)
 
 validation-push:
 	$(CONTAINER_TOOL) push $(IMG_VALIDATION)
+
+rdma-driver-image:          ## RDMA driver init container (driverImage): modprobe of the NICs' RDMA drivers
+	$(CONTAINER_TOOL) build -f build/Dockerfile.rdma-driver -t $(IMG_RDMA_DRIVER) .
+
+rdma-driver-push:
+	$(CONTAINER_TOOL) push $(IMG_RDMA_DRIVER)
 
 # Multi-platform build and push of the operator image.  The Dockerfile already names its
 # stages' bases, so buildx only needs --platform; a throwaway builder keeps the host's default.

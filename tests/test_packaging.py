@@ -538,13 +538,15 @@ def test_alert_rules_use_only_metrics_that_exist():
     assert "alert-rules.yaml" in kust["resources"]
 
 
-def test_ci_builds_and_scans_the_three_images():
+def test_ci_builds_and_scans_every_image():
     """the reference CI builds its operator and agent images and runs Trivy on them
     (reference .github/workflows/validate-common.yaml:49-65).  The images job builds the operator,
-    link-discovery and validation images (their in-build gates run there) and scans each."""
+    link-discovery, validation and RDMA-driver images (their in-build gates run there) and scans
+    each; every Dockerfile in build/ is in the matrix."""
     ci = yaml.safe_load((ROOT / ".github" / "workflows" / "ci.yaml").read_text())["jobs"]["images"]
     images = ci["strategy"]["matrix"]["image"]
-    assert sorted(images) == ["linkdiscovery", "operator", "validation"]
+    assert sorted(images) == ["linkdiscovery", "operator", "rdma-driver", "validation"]
+    assert sorted(images) == sorted(p.name.split(".", 1)[1] for p in (ROOT / "build").glob("Dockerfile.*"))
     for img in images:
         assert (ROOT / "build" / f"Dockerfile.{img}").exists(), img
     build = [s for s in ci["steps"] if str(s.get("uses", "")).startswith("docker/build-push-action")]
@@ -583,3 +585,39 @@ def test_operator_image_dependencies_are_pinned_exactly():
         assert dep in pins, dep
     for name, ver in pins.items():
         assert md.version(name) == ver, (name, md.version(name), ver)
+
+
+def test_rdma_driver_container_loads_the_rdma_driver_of_each_bound_nic_driver(tmp_path):
+    """build/Dockerfile.rdma-driver's entrypoint (the driverImage init container): the RDMA
+    module of every RoCE NIC driver bound on the node, each once, none already loaded; arguments
+    override; a module modprobe cannot load fails the container naming it."""
+    import os
+    import subprocess
+
+    script = ROOT / "build" / "rdma-driver" / "load-rdma-modules.sh"
+    sysfs = tmp_path / "sys"
+    drivers = sysfs / "bus" / "pci" / "drivers"
+    for nic, drv in (("enp8s0np0", "ionic"), ("enp33s0np0", "ionic"), ("ens1np0", "mlx5_core"), ("eno1", "igb")):
+        (drivers / drv).mkdir(parents=True, exist_ok=True)
+        dev = sysfs / "devices" / nic
+        dev.mkdir(parents=True)
+        (dev / "driver").symlink_to(drivers / drv)
+        (sysfs / "class" / "net" / nic).mkdir(parents=True)
+        (sysfs / "class" / "net" / nic / "device").symlink_to(dev)
+    (sysfs / "module" / "mlx5_ib").mkdir(parents=True)  # already loaded
+    bin_dir = tmp_path / "bin"
+    bin_dir.mkdir()
+    log = tmp_path / "modprobe.log"
+    (bin_dir / "modprobe").write_text(f'#!/bin/sh\necho "$@" >> {log}\n[ "$1" != broken_rdma ]\n')
+    (bin_dir / "modprobe").chmod(0o755)
+    env = dict(os.environ, SYSFS_ROOT=str(sysfs), PATH=f"{bin_dir}:{os.environ['PATH']}")
+    r = subprocess.run(["sh", str(script)], capture_output=True, text=True, env=env, timeout=30)
+    assert r.returncode == 0, r.stderr
+    assert log.read_text() == "ionic_rdma\n"  # once for both ionic NICs; mlx5_ib is there; igb is no RoCE NIC
+    assert "ionic_rdma: loaded" in r.stdout and "mlx5_ib: already loaded" in r.stdout
+    r = subprocess.run(["sh", str(script), "broken_rdma"], capture_output=True, text=True, env=env, timeout=30)
+    assert r.returncode == 1 and "broken_rdma: modprobe failed" in r.stderr
+    dockerfile = (ROOT / "build" / "Dockerfile.rdma-driver").read_text()
+    assert "load-rdma-modules.sh /usr/local/bin/load-rdma-modules" in dockerfile and "kmod" in dockerfile
+    sample = yaml.safe_load((ROOT / "config" / "operator" / "samples" / "amd-l3-pollara.yaml").read_text())
+    assert sample["spec"]["amdScaleOut"]["driverImage"] == "amd/amd-network-rdma-driver:0.1.0"
