@@ -322,8 +322,8 @@ def test_trivy_ignores_reference_rendered_files():
     paths = {p for m in ign["misconfigurations"] for p in m.get("paths", [])}
     rendered = {"deployments/operator.yaml", "deployments/helm-default.yaml", "deployments/discovery.yaml",
                 "deployments/discovery-host-nic.yaml"}
-    assert paths - rendered == {"build/Dockerfile.linkdiscovery"}
-    assert (ROOT / "build/Dockerfile.linkdiscovery").exists()
+    assert paths - rendered == {"build/Dockerfile.linkdiscovery", "build/Dockerfile.rdma-driver"}
+    assert all((ROOT / p).exists() for p in paths - rendered)
     docs = discovery_for(ROOT / "config/operator/samples/amd-l3.yaml")
     ds = _by_kind(docs, "DaemonSet")[0]
     pod = ds["spec"]["template"]["spec"]
