@@ -3152,6 +3152,7 @@ TEST(agent_l3_label_and_rccl_env_follow_random_rdma_driver_reloads_and_flaps) {
                     const std::string line = "NCCL_IB_HCA==" + join(hcas, ",") + "\n";
                     if (!env || env->find(line) == std::string::npos) bad += " rccl.env does not name " + join(hcas, ",");
                 }
+                if (!bad.empty() && mono_ns() - t_step < 320000000LL) return;  // a loaded machine: more time
                 labelled_states += want;
                 if (!bad.empty()) {
                     if (!mismatches) first_bad = strfmt("step %d:", steps) + bad;
@@ -3555,9 +3556,15 @@ TEST(agent_label_holddown_and_xgmi_dampening_follow_random_link_and_carrier_flap
                     want = true;
                 else
                     want = wait > f.cfg.label_holddown_ns;  // healthy since this step
-                held += healthy() && !want;
-                if (want) labelled = true;
                 const bool label = path_exists(f.cfg.labels.path());
+                // A held label is checked at once (the agent's hold-down starts when it sees the
+                // health, after the step, so lateness can only keep it off longer).  Every other
+                // expectation is a state the agent converges to: on a loaded machine it gets up to
+                // 300 ms more to reach it.
+                const bool holding = healthy() && !want;
+                if (label != want && !holding && mono_ns() - t_step < wait + 300000000LL) return;
+                held += holding;
+                if (want) labelled = true;
                 if (label != want) {
                     if (!mismatches)
                         first_bad = strfmt("step %d (waited %lld ms, %d withdrawal(s)): label %d, want %d", steps,
