@@ -3563,6 +3563,13 @@ TEST(agent_label_holddown_and_xgmi_dampening_follow_random_link_and_carrier_flap
                 // 300 ms more to reach it.
                 const bool holding = healthy() && !want;
                 if (label != want && !holding && mono_ns() - t_step < wait + 300000000LL) return;
+                // An unhealthy node: the agent must have seen it before the next step (an xGMI link
+                // down for less than two samples is no flap, by design; on a loaded machine 10 ms
+                // may hold one sample).  Its reason names the fault, not the hold-down.
+                if (!healthy() && mono_ns() - t_step < wait + 300000000LL) {
+                    auto why = read_file(agent::reason_path(f.cfg.status_file));
+                    if (!why || why->find("label hold-down") != std::string::npos) return;
+                }
                 held += holding;
                 if (want) labelled = true;
                 if (label != want) {
