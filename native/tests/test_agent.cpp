@@ -3105,15 +3105,17 @@ TEST(agent_require_rdma_devices_that_appear_during_the_bring_up_are_in_rccl_env_
     CHECK(env && env->find("NCCL_IB_HCA==mlx5_0:1,mlx5_1:1,mlx5_2:1\n") != std::string::npos);
 }
 
-TEST(agent_l3_label_and_rccl_env_follow_random_rdma_driver_reloads_and_flaps) {
-    // Property (L3, --require-rdma, monitor): under any sequence of RDMA driver unloads, reloads
+TEST(agent_label_and_rccl_env_follow_random_rdma_driver_reloads_and_flaps_in_l3_and_l2) {
+    // Property (L3 and L2, --require-rdma, monitor): under any sequence of RDMA driver unloads, reloads
     // (which may number a device anew) and cable pulls, once the agent has caught up:
     //   the label is there exactly when every NIC has carrier and an RDMA device;
     //   while it is, rccl.env names exactly the current devices, in GPU order;
     //   while a device is missing, there is no rccl.env (no rail left to TCP sockets).
     // 120 random steps for each of three seeds.
+    for (const char* mode : {"L3", "L2"})
     for (uint64_t seed : {0x0F1E2D3C4B5A6978ull, 0x1111222233334444ull, 0x9999AAAABBBBCCCCull}) {
         RdmaFixture f;
+        f.cfg.mode = mode;
         f.cfg.xgmi_health_interval_ns = 1000000;  // a labelled node looks for its devices every 1 ms
         const std::vector<std::string> nics = {"ens0", "ens1", "ens2"};
         std::map<std::string, bool> carrier;
@@ -3188,7 +3190,7 @@ TEST(agent_l3_label_and_rccl_env_follow_random_rdma_driver_reloads_and_flaps) {
             t_step = mono_ns();
         };
         a.run(stop.fd[0]);
-        if (mismatches) fprintf(stderr, "seed %llx, %s\n", (unsigned long long)seed, first_bad.c_str());
+        if (mismatches) fprintf(stderr, "%s, seed %llx, %s\n", mode, (unsigned long long)seed, first_bad.c_str());
         CHECK_EQ(mismatches, 0);
         CHECK_EQ(steps, 120);
         if (labelled_states == 0 || labelled_states >= steps) fprintf(stderr, "seed %llx: %d labelled states\n", (unsigned long long)seed, labelled_states);
