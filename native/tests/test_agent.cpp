@@ -3198,6 +3198,86 @@ TEST(agent_label_and_rccl_env_follow_random_rdma_driver_reloads_and_flaps_in_l3_
     }
 }
 
+TEST(agent_label_follows_random_pcie_retrains_and_cable_pulls_with_require_full_pcie) {
+    // Property (L3 and L2, --require-full-pcie, monitor): under any sequence of a rail's PCIe link
+    // retraining narrower (x8 of x16) or back to full width, and cable pulls, once the agent has
+    // caught up the label is there exactly when every NIC has carrier and a full PCIe link.  The
+    // monitor re-reads the links every 1 ms.  80 random steps for each of two seeds and modes.
+    for (const char* mode : {"L3", "L2"})
+    for (uint64_t seed : {0x5555AAAA5555AAAAull, 0x0123FEDC4567BA98ull}) {
+        Fixture f;
+        f.cfg.mode = mode;
+        f.cfg.sysfs_root = f.tmp.path + "/sys/";
+        f.cfg.require_full_pcie = true;
+        f.cfg.xgmi_health_interval_ns = 1000000;
+        f.cfg.monitor_tick_ns = 1000000;
+        const std::vector<std::string> nics = {"ens0", "ens1", "ens2"};
+        auto fn = [&](size_t k) { return strfmt("sys/devices/pci0000:00/0000:00:0%zu.0/0000:0%zu:00.0", k + 1, k + 1); };
+        for (size_t k = 0; k < nics.size(); ++k) {
+            const std::string port = strfmt("sys/devices/pci0000:00/0000:00:0%zu.0", k + 1);
+            f.tmp.write(port + "/max_link_speed", "32.0 GT/s PCIe\n");
+            f.tmp.write(port + "/max_link_width", "16\n");
+            for (const char* a : {"max_link_speed", "current_link_speed"}) f.tmp.write(fn(k) + "/" + a, "32.0 GT/s PCIe\n");
+            f.tmp.write(fn(k) + "/max_link_width", "16\n");
+            f.tmp.write(fn(k) + "/current_link_width", "16\n");
+            f.tmp.write(fn(k) + "/vendor", "0x15b3\n");
+            f.tmp.mkdir("sys/class/net/" + nics[k]);
+            f.tmp.mkdir("sys/bus/pci/devices");
+            f.tmp.symlink(fn(k), "sys/class/net/" + nics[k] + "/device");
+            f.tmp.symlink(fn(k), strfmt("sys/bus/pci/devices/0000:0%zu:00.0", k + 1));
+        }
+        std::map<std::string, bool> carrier, full;
+        for (const auto& n : nics) carrier[n] = full[n] = true;
+        uint64_t rng = seed;
+        auto next = [&] {
+            rng ^= rng << 13;
+            rng ^= rng >> 7;
+            rng ^= rng << 17;
+            return rng;
+        };
+        Pipe stop;
+        agent::Agent a(f.cfg, f.ops, f.all_valid(), f.nm());
+        int steps = 0, mismatches = 0, labelled_states = 0;
+        int64_t t_step = 0;
+        std::string first_bad;
+        a.on_monitor_tick = [&](int) {
+            if (t_step && mono_ns() - t_step < 20000000LL) return;
+            if (t_step) {
+                const bool want = std::all_of(nics.begin(), nics.end(), [&](const std::string& n) { return carrier[n] && full[n]; });
+                const bool label = path_exists(f.cfg.labels.path());
+                if (label != want && mono_ns() - t_step < 320000000LL) return;  // a loaded machine: more time
+                labelled_states += want;
+                if (label != want) {
+                    if (!mismatches) first_bad = strfmt("step %d: label %d, want %d", steps, label, want);
+                    ++mismatches;
+                }
+                if (++steps >= 80) {
+                    stop.fire();
+                    return;
+                }
+            }
+            std::vector<size_t> broken;
+            for (size_t k = 0; k < nics.size(); ++k)
+                if (!carrier[nics[k]] || !full[nics[k]]) broken.push_back(k);
+            const size_t k = !broken.empty() && next() % 2 ? broken[next() % broken.size()] : next() % nics.size();
+            const std::string& n = nics[k];
+            if ((!full[n] && (carrier[n] || next() % 2)) || (full[n] && carrier[n] && next() % 2)) {
+                full[n] = !full[n];
+                f.tmp.write(fn(k) + "/current_link_width", full[n] ? "16\n" : "8\n");
+            } else {
+                carrier[n] = !carrier[n];
+                f.ops.set_carrier(n, carrier[n]);
+            }
+            t_step = mono_ns();
+        };
+        a.run(stop.fd[0]);
+        if (mismatches) fprintf(stderr, "%s, seed %llx, %s\n", mode, (unsigned long long)seed, first_bad.c_str());
+        CHECK_EQ(mismatches, 0);
+        CHECK_EQ(steps, 80);
+        CHECK(labelled_states > 0 && labelled_states < steps);
+    }
+}
+
 TEST(agent_require_rdma_past_the_wait_names_the_fault) {
     RdmaFixture f;
     f.cfg.rdma_wait_ns = 0;
