@@ -198,7 +198,12 @@ __device__ __forceinline__ uint32_t pack_bf16x2_rne(float a, float b) {
 
 // dst[i] = Σ_s src[s][i] in fp32 (s = 0..NSRC-1, in order), bf16 RNE out.  All NSRC x UNROLL
 // 16-B loads of a lane are issued before the adds: with peer pointers those are remote xGMI
-// reads, and having many in flight per lane is what hides the link round trip.
+// reads, and having many in flight per lane is what hides the link round trip.  The sources are
+// read once: nontemporal loads.  Shape from sum_tune.hip on the box (local HBM, 256 MiB per
+// buffer, profiles/r6_sum_tune.jsonl): nontemporal loads, UNROLL 2 up to 4 sources and 1 above
+// (8 loads in flight per lane already), 2 workgroups per CU: (n + 1) x buffer bytes at 6.45 / 6.12
+// / 5.88 TB/s for 2 / 4 / 8 sources, against 5.24 / 4.86 / 4.83 with regular loads, UNROLL 2 and
+// 4 workgroups per CU; every variant bit-identical.
 template <int NSRC, int UNROLL>
 __global__ __launch_bounds__(kThreads) void sum_bf16_kernel(SrcPtrs src, uint4* __restrict__ dst, uint64_t n_vec) {
     const uint64_t stride = uint64_t(gridDim.x) * kThreads * UNROLL;
@@ -209,7 +214,10 @@ __global__ __launch_bounds__(kThreads) void sum_bf16_kernel(SrcPtrs src, uint4* 
             const uint64_t i = base + uint64_t(u) * kThreads;
             if (i < n_vec) {
 #pragma unroll
-                for (int s = 0; s < NSRC; ++s) v[u][s] = src.p[s][i];
+                for (int s = 0; s < NSRC; ++s) {
+                    const u32x4 q = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src.p[s]) + i);
+                    v[u][s] = make_uint4(q.x, q.y, q.z, q.w);
+                }
             }
         }
 #pragma unroll
@@ -226,9 +234,10 @@ __global__ __launch_bounds__(kThreads) void sum_bf16_kernel(SrcPtrs src, uint4* 
 }
 
 using SumFn = void (*)(SrcPtrs, uint4*, uint64_t);
+constexpr int sum_unroll(int n) { return n <= 4 ? 2 : 1; }
 template <int N>
 SumFn sum_for() {
-    return sum_bf16_kernel<N, 2>;
+    return sum_bf16_kernel<N, sum_unroll(N)>;
 }
 SumFn sum_fn(int n) {
     switch (n) {
@@ -332,8 +341,9 @@ int netop_sum_bf16(const void* const* srcs, int nsrc, void* dst, uint64_t n_elem
     }
     const uint64_t nv = n_elems / 8;
     if (nv == 0) return int(hipSuccess);
-    hipLaunchKernelGGL(sum_fn(nsrc), dim3(grid_for((nv + 1) / 2, wg_per_cu > 0 ? wg_per_cu : 4)), dim3(kThreads), 0,
-                       stream, p, static_cast<uint4*>(dst), nv);
+    const uint64_t unroll = uint64_t(sum_unroll(nsrc));
+    hipLaunchKernelGGL(sum_fn(nsrc), dim3(grid_for((nv + unroll - 1) / unroll, wg_per_cu > 0 ? wg_per_cu : 2)),
+                       dim3(kThreads), 0, stream, p, static_cast<uint4*>(dst), nv);
     return int(hipGetLastError());
 }
 
