@@ -168,9 +168,14 @@ __global__ __launch_bounds__(kThreads) void copy_kernel(const uint4* __restrict_
                                                         uint64_t n_vec) {
     // One 16-B load per lane per iteration with 4 workgroups per CU: the best of the
     // unroll {1,2,4,8} x workgroups/CU {4,8,16,32} x {regular, nontemporal store} sweep on
-    // MI355X HBM (2.86 TB/s copy = 5.7 TB/s of traffic, profiles/r1_copy_tune.jsonl).
+    // MI355X HBM (2.86 TB/s copy = 5.7 TB/s of traffic, profiles/r1_copy_tune.jsonl).  Round 6
+    // added nontemporal loads to the sweep: with nontemporal loads and stores 3.08 TB/s
+    // (profiles/r6_copy_tune.jsonl).  Every byte is moved once.
+    const u32x4* __restrict__ s = reinterpret_cast<const u32x4*>(src);
+    u32x4* __restrict__ d = reinterpret_cast<u32x4*>(dst);
     const uint64_t stride = uint64_t(gridDim.x) * kThreads;
-    for (uint64_t v = uint64_t(blockIdx.x) * kThreads + threadIdx.x; v < n_vec; v += stride) dst[v] = src[v];
+    for (uint64_t v = uint64_t(blockIdx.x) * kThreads + threadIdx.x; v < n_vec; v += stride)
+        __builtin_nontemporal_store(__builtin_nontemporal_load(&s[v]), &d[v]);
 }
 
 // ---- n-way bf16 sum (reduce-scatter step of the direct xGMI all-reduce) ----------------------

@@ -35,21 +35,25 @@ struct CopyPairs {
     uint4* dst[kMaxPairs];
 };
 
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
 // blockIdx.y selects the (src, dst) pair; within a pair, a grid-stride loop of 16-B vectors.
-// Two loads in flight per lane: with peer sources each is an xGMI round trip.
+// Two loads in flight per lane: with peer sources each is an xGMI round trip.  Every byte is
+// moved once: nontemporal loads and stores (copy_tune.hip on the box, profiles/r6_copy_tune.jsonl:
+// 3.08 against 2.86 TB/s of copy with regular ones, HBM loopback).
 __global__ __launch_bounds__(kThreads) void multi_copy_kernel(CopyPairs pairs, uint64_t n_vec) {
-    const uint4* __restrict__ s = pairs.src[blockIdx.y];
-    uint4* __restrict__ d = pairs.dst[blockIdx.y];
+    const u32x4* __restrict__ s = reinterpret_cast<const u32x4*>(pairs.src[blockIdx.y]);
+    u32x4* __restrict__ d = reinterpret_cast<u32x4*>(pairs.dst[blockIdx.y]);
     // Each workgroup covers 2 x kThreads consecutive vectors per step.
     const uint64_t stride = uint64_t(gridDim.x) * kThreads * 2;
     for (uint64_t i = uint64_t(blockIdx.x) * kThreads * 2 + threadIdx.x; i < n_vec; i += stride) {
         const uint64_t j = i + uint64_t(kThreads);
-        uint4 a = s[i];
-        uint4 b;
+        const u32x4 a = __builtin_nontemporal_load(&s[i]);
+        u32x4 b;
         const bool two = j < n_vec;
-        if (two) b = s[j];
-        d[i] = a;
-        if (two) d[j] = b;
+        if (two) b = __builtin_nontemporal_load(&s[j]);
+        __builtin_nontemporal_store(a, &d[i]);
+        if (two) __builtin_nontemporal_store(b, &d[j]);
     }
 }
 
