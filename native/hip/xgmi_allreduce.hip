@@ -66,12 +66,16 @@ struct DstPtrs {
     uint4* p[kMaxRanks];
 };
 
-// Several independent copies in one launch: blockIdx.y selects the (src, dst) pair.
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+// Several independent copies in one launch: blockIdx.y selects the (src, dst) pair.  Every byte
+// is moved once: nontemporal loads and stores (copy_tune.hip, profiles/r6_copy_tune.jsonl).
 __global__ __launch_bounds__(kThreads) void multi_copy_kernel(Ptrs src, DstPtrs dst, uint64_t n_vec) {
-    const uint4* __restrict__ s = src.p[blockIdx.y];
-    uint4* __restrict__ d = dst.p[blockIdx.y];
+    const u32x4* __restrict__ s = reinterpret_cast<const u32x4*>(src.p[blockIdx.y]);
+    u32x4* __restrict__ d = reinterpret_cast<u32x4*>(dst.p[blockIdx.y]);
     const uint64_t stride = uint64_t(gridDim.x) * kThreads;
-    for (uint64_t i = uint64_t(blockIdx.x) * kThreads + threadIdx.x; i < n_vec; i += stride) d[i] = s[i];
+    for (uint64_t i = uint64_t(blockIdx.x) * kThreads + threadIdx.x; i < n_vec; i += stride)
+        __builtin_nontemporal_store(__builtin_nontemporal_load(&s[i]), &d[i]);
 }
 
 struct Rank {

@@ -99,6 +99,18 @@ def test_xgmi_allreduce_multiprocess_virtual_ranks(cuda_device, world):
 
 
 @pytest.mark.gpu
+def test_single_process_xgmi_allreduce_virtual_ranks_exact(cuda_device):
+    """netop-xgmi-allreduce (the single-process two-shot bench.py runs on the whole-node run):
+    four ranks mapped onto the one GPU run the full algorithm, pull and push, with every chunk,
+    cross-stream event and reused buffer; every size exact for three seeds (rc 0, wrong 0)."""
+    from network_operator_amd.parallel import xgmi_allreduce
+
+    rows = xgmi_allreduce.run(timeout=110, ranks=4, min_bytes=1 << 20, max_bytes=16 << 20, factor=4, iters=3, warmup=1)
+    assert {x["mode"] for x in rows} == {"pull", "push"} and len(rows) == 6
+    assert all(x["wrong"] == 0 and x["ranks"] == 4 and x["gpus"] == 1 and x["time_us"] > 0 for x in rows), rows
+
+
+@pytest.mark.gpu
 def test_xgmi_allreduce_small_buffers_share_one_ipc_segment(cuda_device):
     """64 KiB symmetric buffers come from one caching-allocator segment, so both have the same
     IPC handle: each peer maps it once and addresses both buffers inside it."""
