@@ -217,8 +217,10 @@ bool Agent::configure_interface(NicState& n) {
     bool existing = std::any_of(addrs.begin(), addrs.end(), [&](const nl::AddrInfo& a) { return a.local == n.addr->local; });
     try {
         if (!existing) {
-            // The kernel adds the /30 connected route along with the address.
+            // The kernel adds the /30 connected route along with the address (and the RDMA core
+            // a RoCE GID for it, in a slot of its choosing: the index is looked up again).
             ops_.addr_add(n.link.index, n.addr->local_prefix());
+            n.gid_index.reset();
             NLOG_I("Configured address and route %s for interface '%s'", n.addr->local_prefix().str().c_str(), n.ifname.c_str());
         } else {
             NLOG_I("Interface '%s' already configured with address %s", n.ifname.c_str(), n.addr->local_prefix().str().c_str());

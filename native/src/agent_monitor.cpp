@@ -314,6 +314,10 @@ void Agent::monitor(int stop_fd) {
                     } else if (n.degraded && up && (lower || !had_carrier)) {
                         NLOG_I("Interface '%s' recovered", n.ifname.c_str());
                         n.degraded = false;
+                        // The RDMA core drops a netdev's IP GIDs when it goes down and adds them
+                        // again when it comes up, in whatever GID slots are free then: look the
+                        // index up again before rccl.env is written for the republished label.
+                        n.gid_index.reset();
                         // Administrative down flushes the routes: ensure address and routes again.
                         if (cfg_.mode == "L3" && n.addr) {
                             n.configured = false;

@@ -3278,6 +3278,60 @@ TEST(agent_label_follows_random_pcie_retrains_and_cable_pulls_with_require_full_
     }
 }
 
+TEST(agent_looks_up_the_gid_index_again_after_a_link_comes_back) {
+    // The RDMA core drops a netdev's IP GIDs when the link goes down and adds them again when it
+    // comes back, in whatever slot is free: ens1's RoCE v2 GID moves from index 3 to 5 during its
+    // flap.  The republished rccl.env must not keep the stale NCCL_IB_GID_INDEX=3 (RCCL would use
+    // another GID, or none, on that rail).
+    RdmaFixture f;
+    const std::map<std::string, std::string> ips = {{"ens0", "10.200.0.1"}, {"ens1", "10.200.0.5"}, {"ens2", "10.200.0.10"}};
+    auto put_gid = [&](const std::string& dev, int idx, const std::string& ip, bool present) {
+        const std::string d = "sys/class/infiniband/" + dev + "/ports/1/";
+        auto ipv = *Ipv4::parse(ip);
+        uint8_t b[4];
+        ipv.to_net(b);
+        f.tmp.write(d + "gids/" + std::to_string(idx),
+                    present ? strfmt("0000:0000:0000:0000:0000:ffff:%02x%02x:%02x%02x\n", b[0], b[1], b[2], b[3])
+                            : std::string("0000:0000:0000:0000:0000:0000:0000:0000\n"));
+        f.tmp.write(d + "gid_attrs/types/" + std::to_string(idx), "RoCE v2\n");
+    };
+    for (int k = 0; k < 3; ++k) {
+        const std::string nic = "ens" + std::to_string(k), dev = "mlx5_" + std::to_string(k);
+        f.bind(nic, dev);
+        put_gid(dev, 3, ips.at(nic), true);
+    }
+    Pipe stop;
+    agent::Agent a(f.cfg, f.ops, f.all_valid(), f.nm());
+    int phase = 0;
+    std::string env_before, env_after;
+    const int64_t t0 = mono_ns();
+    a.on_monitor_tick = [&](int) {
+        const bool labelled = path_exists(f.cfg.labels.path());
+        if (phase == 0 && labelled) {
+            env_before = read_file(f.cfg.rccl_env).value_or("");
+            f.ops.set_carrier("ens1", false);
+            phase = 1;
+        } else if (phase == 1 && !labelled) {
+            put_gid("mlx5_1", 3, ips.at("ens1"), false);  // gone with the link, back in another slot
+            put_gid("mlx5_1", 5, ips.at("ens1"), true);
+            f.ops.set_carrier("ens1", true);
+            phase = 2;
+        } else if (phase == 2 && labelled) {
+            env_after = read_file(f.cfg.rccl_env).value_or("");
+            phase = 3;
+            stop.fire();
+        } else if (mono_ns() - t0 > 5000000000LL) {
+            stop.fire();
+        }
+    };
+    a.run(stop.fd[0]);
+    CHECK_EQ(phase, 3);
+    CHECK(env_before.find("NCCL_IB_GID_INDEX=3\n") != std::string::npos);
+    CHECK(env_after.find("NCCL_IB_GID_INDEX=3\n") == std::string::npos);  // not the stale index
+    CHECK(env_after.find("NCCL_IB_ROCE_VERSION_NUM=2\n") != std::string::npos);  // 3 and 5: RCCL picks per HCA
+    CHECK(env_after.find("NCCL_IB_HCA==mlx5_0:1,mlx5_1:1,mlx5_2:1\n") != std::string::npos);
+}
+
 TEST(agent_require_rdma_past_the_wait_names_the_fault) {
     RdmaFixture f;
     f.cfg.rdma_wait_ns = 0;
