@@ -3154,7 +3154,7 @@ TEST(agent_label_and_rccl_env_follow_random_rdma_driver_reloads_and_flaps_in_l3_
                     const std::string line = "NCCL_IB_HCA==" + join(hcas, ",") + "\n";
                     if (!env || env->find(line) == std::string::npos) bad += " rccl.env does not name " + join(hcas, ",");
                 }
-                if (!bad.empty() && mono_ns() - t_step < 320000000LL) return;  // a loaded machine: more time
+                if (!bad.empty() && mono_ns() - t_step < 2000000000LL) return;  // a loaded machine: up to 2 s more
                 labelled_states += want;
                 if (!bad.empty()) {
                     if (!mismatches) first_bad = strfmt("step %d:", steps) + bad;
@@ -3245,10 +3245,14 @@ TEST(agent_label_follows_random_pcie_retrains_and_cable_pulls_with_require_full_
             if (t_step) {
                 const bool want = std::all_of(nics.begin(), nics.end(), [&](const std::string& n) { return carrier[n] && full[n]; });
                 const bool label = path_exists(f.cfg.labels.path());
-                if (label != want && mono_ns() - t_step < 320000000LL) return;  // a loaded machine: more time
+                if (label != want && mono_ns() - t_step < 2000000000LL) return;  // a loaded machine: up to 2 s more
                 labelled_states += want;
                 if (label != want) {
-                    if (!mismatches) first_bad = strfmt("step %d: label %d, want %d", steps, label, want);
+                    if (!mismatches) {
+                        first_bad = strfmt("step %d: label %d, want %d;", steps, label, want);
+                        for (const auto& n : nics) first_bad += strfmt(" %s carrier %d full %d", n.c_str(), carrier[n], full[n]);
+                        first_bad += "\n" + read_file(f.cfg.status_file).value_or("");
+                    }
                     ++mismatches;
                 }
                 if (++steps >= 80) {
@@ -3696,13 +3700,13 @@ TEST(agent_label_holddown_and_xgmi_dampening_follow_random_link_and_carrier_flap
                 // A held label is checked at once (the agent's hold-down starts when it sees the
                 // health, after the step, so lateness can only keep it off longer).  Every other
                 // expectation is a state the agent converges to: on a loaded machine it gets up to
-                // 300 ms more to reach it.
+                // 2 s more to reach it.
                 const bool holding = healthy() && !want;
-                if (label != want && !holding && mono_ns() - t_step < wait + 300000000LL) return;
+                if (label != want && !holding && mono_ns() - t_step < wait + 2000000000LL) return;
                 // An unhealthy node: the agent must have seen it before the next step (an xGMI link
                 // down for less than two samples is no flap, by design; on a loaded machine 10 ms
                 // may hold one sample).  Its reason names the fault, not the hold-down.
-                if (!healthy() && mono_ns() - t_step < wait + 300000000LL) {
+                if (!healthy() && mono_ns() - t_step < wait + 2000000000LL) {
                     auto why = read_file(agent::reason_path(f.cfg.status_file));
                     if (!why || why->find("label hold-down") != std::string::npos) return;
                 }
