@@ -53,7 +53,8 @@ struct FakeNetOps : netop::nl::NetOps {
             if (l.index == idx) return &l;
         return nullptr;
     }
-    std::function<void(const std::string&)> on_op;  // runs at every operation, before it acts
+    std::function<void(const std::string&)> on_op;     // runs at every operation, before it acts
+    std::function<void(const std::string&)> after_op;  // after an address change took effect
     void maybe_fail(const std::string& op) {
         ++calls[op];
         if (on_op) on_op(op);
@@ -98,6 +99,7 @@ struct FakeNetOps : netop::nl::NetOps {
         r.protocol = RTPROT_KERNEL;
         r.scope = RT_SCOPE_LINK;
         routes.push_back(r);
+        if (after_op) after_op("addr_add");
     }
     void addr_del(const netop::nl::AddrInfo& a) override {
         maybe_fail("addr_del");
@@ -111,6 +113,7 @@ struct FakeNetOps : netop::nl::NetOps {
                      }),
                      routes.end());
         addrs.erase(it);
+        if (after_op) after_op("addr_del");
     }
     void route_append(const netop::nl::RouteSpec& r) override {
         maybe_fail("route_append");

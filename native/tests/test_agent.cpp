@@ -12,6 +12,7 @@
 #include <cstddef>
 #include <cstring>
 #include <filesystem>
+#include <set>
 
 #include "check.hpp"
 #include "fake_netops.hpp"
@@ -3334,6 +3335,144 @@ TEST(agent_looks_up_the_gid_index_again_after_a_link_comes_back) {
     CHECK(env_after.find("NCCL_IB_GID_INDEX=3\n") == std::string::npos);  // not the stale index
     CHECK(env_after.find("NCCL_IB_ROCE_VERSION_NUM=2\n") != std::string::npos);  // 3 and 5: RCCL picks per HCA
     CHECK(env_after.find("NCCL_IB_HCA==mlx5_0:1,mlx5_1:1,mlx5_2:1\n") != std::string::npos);
+}
+
+TEST(agent_rccl_env_gid_index_is_never_stale_under_random_readdressing_and_flaps) {
+    // Property (L3, RDMA on every rail, monitor): a simulated RDMA core keeps each device's RoCE v2
+    // GID table -- an IPv4 GID appears in a free slot when the address is added, goes when it is
+    // removed or its link goes down, and comes back (in whatever slot is free then) when the link
+    // is up again.  Under random switch-port re-addressing and cable pulls, whenever the node is
+    // labelled and rccl.env names NCCL_IB_GID_INDEX=k, slot k of every rail holds that rail's own
+    // current address.  Three seeds, 100 steps each.
+    for (uint64_t seed : {0x13579BDF2468ACE0ull, 0x0A0B0C0D0E0F1011ull, 0xFEEDFACECAFEF00Dull}) {
+        RdmaFixture f;
+        f.cfg.xgmi_health_interval_ns = 1000000;
+        f.cfg.lldp_tx_interval_ns = 3600LL * 1000000000LL;
+        f.cfg.gid_wait_ns = 50000000;  // the simulated core answers at once
+        const std::vector<std::string> nics = {"ens0", "ens1", "ens2"};
+        const std::map<int, std::string> by_index = {{10, "ens0"}, {11, "ens1"}, {12, "ens2"}};
+        std::map<std::string, bool> carrier;
+        std::map<std::string, int> host;
+        std::map<std::string, std::map<int, uint32_t>> table;  // nic -> slot -> IPv4 (host order)
+        uint64_t rng = seed;
+        auto next = [&] {
+            rng ^= rng << 13;
+            rng ^= rng >> 7;
+            rng ^= rng << 17;
+            return rng;
+        };
+        auto write_table = [&](const std::string& n) {
+            const std::string dev = "mlx5_" + std::string(1, n.back());
+            for (int slot = 0; slot < 8; ++slot) {
+                const std::string d = "sys/class/infiniband/" + dev + "/ports/1/";
+                auto it = table[n].find(slot);
+                std::string gid = "0000:0000:0000:0000:0000:0000:0000:0000\n";
+                if (it != table[n].end()) {
+                    const uint32_t v = it->second;
+                    gid = strfmt("0000:0000:0000:0000:0000:ffff:%04x:%04x\n", v >> 16, v & 0xffff);
+                }
+                f.tmp.write(d + "gids/" + std::to_string(slot), gid);
+                f.tmp.write(d + "gid_attrs/types/" + std::to_string(slot), "RoCE v2\n");
+            }
+        };
+        // The RDMA core: the GIDs follow each NIC's IPv4 addresses while its link is up.
+        auto sync = [&] {
+            for (const auto& n : nics) {
+                std::set<uint32_t> want;
+                if (carrier[n])
+                    for (const auto& x : f.ops.addrs)
+                        if (by_index.count(x.ifindex) && by_index.at(x.ifindex) == n && x.family == AF_INET) want.insert(x.local.v);
+                auto& t = table[n];
+                for (auto it = t.begin(); it != t.end();) it = want.count(it->second) ? std::next(it) : t.erase(it);
+                for (uint32_t ip : want) {
+                    bool have = false;
+                    for (auto& [slot, v] : t) have |= v == ip;
+                    if (have) continue;
+                    // The lowest free slot half the time, a free slot from a random start otherwise.
+                    for (int k = 0, start = next() % 2 ? 2 : 2 + int(next() % 6); k < 6; ++k) {
+                        const int slot = 2 + (start - 2 + k) % 6;
+                        if (!t.count(slot)) {
+                            t[slot] = ip;
+                            break;
+                        }
+                    }
+                }
+                write_table(n);
+            }
+        };
+        f.ops.after_op = [&](const std::string&) { sync(); };
+        auto src = f.all_valid();
+        ScriptedLldp* lldp_src = src.get();
+        std::map<std::string, lldp::Frame> frames;
+        auto describe = [&](const std::string& n) {
+            const int k = int(n.back() - '0');
+            frames[n] = sw(strfmt("02:aa:00:00:00:0%d", k).c_str(), strfmt("no-alert 10.20%d.0.%d/30", k, 4 * host[n] + 2).c_str());
+            if (carrier[n]) lldp_src->frames[n] = frames[n];
+        };
+        for (const auto& n : nics) {
+            carrier[n] = true;
+            host[n] = 1;
+            describe(n);
+            f.bind(n, "mlx5_" + std::string(1, n.back()));
+            write_table(n);
+        }
+        Pipe stop;
+        agent::Agent a(f.cfg, f.ops, std::move(src), f.nm());
+        int steps = 0, mismatches = 0, indexed = 0;
+        int64_t t_step = 0;
+        std::string first_bad;
+        a.on_monitor_tick = [&](int) {
+            if (t_step && mono_ns() - t_step < 20000000LL) return;
+            if (t_step) {
+                const bool want = std::all_of(nics.begin(), nics.end(), [&](const std::string& n) { return carrier[n]; });
+                const bool label = path_exists(f.cfg.labels.path());
+                std::string bad;
+                if (label != want) bad = strfmt("label %d, want %d", label, want);
+                auto env = read_file(f.cfg.rccl_env);
+                if (label && env) {
+                    const auto at = env->find("NCCL_IB_GID_INDEX=");
+                    if (at != std::string::npos) {
+                        const int k = std::atoi(env->c_str() + at + 18);
+                        ++indexed;
+                        for (const auto& n : nics) {
+                            const int h = 4 * host[n] + 1, r = int(n.back() - '0');
+                            const uint32_t ip = (10u << 24) | (uint32_t(200 + r) << 16) | uint32_t(h);
+                            auto it = table[n].find(k);
+                            if (it == table[n].end() || it->second != ip) bad += strfmt(" %s: slot %d is not its address", n.c_str(), k);
+                        }
+                    }
+                }
+                if (!bad.empty() && mono_ns() - t_step < 2000000000LL) return;
+                if (!bad.empty()) {
+                    if (!mismatches) first_bad = strfmt("step %d: ", steps) + bad;
+                    ++mismatches;
+                }
+                if (++steps >= 100) {
+                    stop.fire();
+                    return;
+                }
+            }
+            const std::string& n = nics[next() % nics.size()];
+            if (carrier[n] && next() % 3 == 0) {  // the switch port is re-addressed
+                host[n] = 1 + int(next() % 8);
+                describe(n);
+            } else {
+                carrier[n] = !carrier[n];
+                if (carrier[n])
+                    lldp_src->frames[n] = frames[n];
+                else
+                    lldp_src->frames.erase(n);
+                f.ops.set_carrier(n, carrier[n]);
+                sync();  // the core drops / re-adds the link's GIDs
+            }
+            t_step = mono_ns();
+        };
+        a.run(stop.fd[0]);
+        if (mismatches) fprintf(stderr, "seed %llx, %s\n", (unsigned long long)seed, first_bad.c_str());
+        CHECK_EQ(mismatches, 0);
+        CHECK_EQ(steps, 100);
+        CHECK(indexed > 0);  // the walk did reach states with one index for every rail
+    }
 }
 
 TEST(agent_require_rdma_past_the_wait_names_the_fault) {
