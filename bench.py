@@ -218,6 +218,14 @@ def node_ready_gpu_side(sysfs: str = "/sys/") -> dict:
 
         timed("label", label)
     out["total_ms"] = round(sum(out["phases_ms"].values()), 4)
+    # The agent binary itself, 10 dry runs with the operator's flags (its own phase timings and
+    # the process wall time, exec to exit): network_operator_amd/agent/start_timing.py.
+    try:
+        from network_operator_amd.agent import start_timing
+
+        out["agent_binary"] = start_timing.measure(runs=10, sysfs=sysfs if sysfs != "/sys/" else "")
+    except Exception as e:  # reported, never fatal to the line
+        out["agent_binary"] = {"error": str(e)[-300:]}
     out["gpus"] = len(d["gpus"])
     out["nics_paired"] = len(d["pairs"])
     out["xgmi_pairs"] = f"{x['pairs_connected']}/{x['pairs_expected']}"

@@ -91,6 +91,11 @@ def test_bench_single_rank_reports_no_fake_bandwidth(tmp_path):
     assert all(row["algbw_GBps"] is None for row in j["sweep"])
     side = j["node_ready_gpu_side"]
     assert set(side["phases_ms"]) >= {"discover", "xgmi", "gdr", "label"} and side["total_ms"] >= 0
+    binary = side["agent_binary"]  # the real discover binary, 10 dry runs with the operator's flags
+    if "error" in binary:  # a machine without GPUs and NICs (this container): said, not fatal
+        assert "No interfaces found" in binary["stderr"], binary
+    else:
+        assert binary["runs"] == 10 and binary["process_wall_ms"]["p50"] > 0 and "discover" in binary["phases_ms"], binary
 
 
 def test_bench_rejects_world_mismatch(tmp_path):

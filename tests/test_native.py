@@ -494,3 +494,18 @@ def test_a_stalled_bridge_read_leaves_the_topology_file_out_instead_of_hanging(n
     assert "The RCCL topology file was not generated within 1s" in r.stderr, r.stderr[-2000:]
     assert not (tmp_path / "rccl-topo.xml").exists()
     assert "NCCL_TOPO_FILE" not in (tmp_path / "rccl.env").read_text()
+
+
+def test_agent_start_timing_on_a_fake_mi355x_node(native, tmp_path):
+    """network_operator_amd/agent/start_timing.py (bench.py's node_ready_gpu_side.agent_binary,
+    tools/agent_start_box.py): the real discover binary's dry run, repeated, on a fake sysfs copy
+    of an 8-GPU node: its own phase timings and the process wall time."""
+    from network_operator_amd.agent import start_timing
+
+    fakesysfs.build_mi355x_node(tmp_path / "sys", n_gpus=8)
+    r = start_timing.measure(runs=3, sysfs=str(tmp_path / "sys") + "/")
+    assert "error" not in r, r
+    assert r["runs"] == 3 and r["xgmi_pairs"] == "28/28"
+    assert {"discover", "xgmi", "gdr", "rccl_topo"} <= set(r["phases_ms"])
+    assert 0 < r["process_wall_ms"]["p50"] <= r["process_wall_ms"]["max"]
+    assert len(r["nics_not_in_this_netns"]) == 8  # the fake node's rails are not in this namespace
