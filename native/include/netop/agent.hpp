@@ -355,8 +355,13 @@ class Agent {
     void add_rail_routing(NicState& n);
     void remove_rail_routing(NicState& n);  // what was installed for n
     void remove_rail_routing();             // every NIC's
-    void write_artifacts();
-    void write_l2_artifacts();
+    // gid_wait_ns < 0: --gid-wait.  The monitor passes 0 (one look, never blocking its loop) and
+    // looks again for the GIDs still missing (gid_retry_until_).
+    void write_artifacts(int64_t gid_wait_ns = -1);
+    void write_l2_artifacts(int64_t gid_wait_ns = -1);
+    bool look_up_gids();        // one look for every configured RDMA NIC's missing GID; true if one was found
+    bool gids_missing() const;  // a configured RDMA NIC without its GID index
+    int64_t gid_retry_until_ = 0;
     // L2: waits up to carrier_wait_ns for carrier on every up NIC (reported as "waiting for
     // carrier" meanwhile); marks the others no_carrier.
     // False when stop_fd fired meanwhile.

@@ -32,18 +32,35 @@ namespace netop::agent {
 
 using detail::fd_readable;
 
-void Agent::write_l2_artifacts() {
-    std::string root = cfg_.sysfs_root.empty() ? topo::sysfs_root() : cfg_.sysfs_root;
-    for (auto& n : nics_) n.configured = n.link.up() && !n.no_carrier && n.config_error.empty();
-    const int64_t deadline = mono_ns() + cfg_.gid_wait_ns;
-    for (;;) {
-        bool missing = false;
-        for (auto& n : nics_) {
-            if (n.rdma_dev.empty() || !n.configured || n.gid_index) continue;
+bool Agent::gids_missing() const {
+    return std::any_of(nics_.begin(), nics_.end(), [&](const NicState& n) {
+        return !n.rdma_dev.empty() && n.configured && (cfg_.mode != "L3" || n.addr) && !n.gid_index;
+    });
+}
+
+bool Agent::look_up_gids() {
+    // L3: the RoCE v2 GID of the NIC's /30 address; L2: of its IPv6 link-local address.
+    const std::string root = cfg_.sysfs_root.empty() ? topo::sysfs_root() : cfg_.sysfs_root;
+    bool found = false;
+    for (auto& n : nics_) {
+        if (n.rdma_dev.empty() || !n.configured || n.gid_index) continue;
+        if (cfg_.mode == "L3") {
+            if (!n.addr) continue;
+            n.gid_index = topo::find_rocev2_gid_index(root, n.rdma_dev, n.rdma_port, n.addr->local);
+        } else {
             n.gid_index = topo::find_rocev2_linklocal_gid_index(root, n.rdma_dev, n.rdma_port);
-            missing |= !n.gid_index;
         }
-        if (!missing || mono_ns() >= deadline) break;
+        found |= bool(n.gid_index);
+    }
+    return found;
+}
+
+void Agent::write_l2_artifacts(int64_t gid_wait_ns) {
+    for (auto& n : nics_) n.configured = n.link.up() && !n.no_carrier && n.config_error.empty();
+    const int64_t deadline = mono_ns() + (gid_wait_ns < 0 ? cfg_.gid_wait_ns : gid_wait_ns);
+    for (;;) {
+        look_up_gids();
+        if (!gids_missing() || mono_ns() >= deadline) break;
         ::usleep(2000);
     }
     write_rccl_env_file();
@@ -285,25 +302,20 @@ void Agent::write_rccl_env_file() {
     }
 }
 
-void Agent::write_artifacts() {
-    std::string root = cfg_.sysfs_root.empty() ? topo::sysfs_root() : cfg_.sysfs_root;
+void Agent::write_artifacts(int64_t gid_wait_ns) {
     // Poll all configured RDMA NICs together until each has its RoCE v2 GID or the wait ends.
-    const int64_t gid_deadline = mono_ns() + cfg_.gid_wait_ns;
+    const int64_t gid_deadline = mono_ns() + (gid_wait_ns < 0 ? cfg_.gid_wait_ns : gid_wait_ns);
     for (;;) {
-        bool missing = false;
-        for (auto& n : nics_) {
-            if (n.rdma_dev.empty() || !n.addr || !n.configured || n.gid_index) continue;
-            n.gid_index = topo::find_rocev2_gid_index(root, n.rdma_dev, n.rdma_port, n.addr->local);
-            missing |= !n.gid_index;
-        }
-        if (!missing || mono_ns() >= gid_deadline) break;
+        look_up_gids();
+        if (!gids_missing() || mono_ns() >= gid_deadline) break;
         ::usleep(2000);
     }
-    for (auto& n : nics_)
-        if (!n.rdma_dev.empty() && n.addr && n.configured && !n.gid_index)
-            NLOG_W("%s (%s): no RoCE v2 GID for %s after %s; rccl.env gets no NCCL_IB_GID_INDEX for it",
-                   n.ifname.c_str(), n.rdma_dev.c_str(), n.addr->local.str().c_str(),
-                   format_go_duration(cfg_.gid_wait_ns).c_str());
+    if (gid_wait_ns != 0)  // (the monitor's one look is followed by more: it warns when they end)
+        for (auto& n : nics_)
+            if (!n.rdma_dev.empty() && n.addr && n.configured && !n.gid_index)
+                NLOG_W("%s (%s): no RoCE v2 GID for %s after %s; rccl.env gets no NCCL_IB_GID_INDEX for it",
+                       n.ifname.c_str(), n.rdma_dev.c_str(), n.addr->local.str().c_str(),
+                       format_go_duration(cfg_.gid_wait_ns).c_str());
     if (!cfg_.rccl_net.empty()) {
         try {
             artifacts::write_rccl_net(cfg_.rccl_net, nics_);

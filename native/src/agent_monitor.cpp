@@ -201,6 +201,8 @@ void Agent::monitor(int stop_fd) {
     bounded::Call<HealthSample> poll;
     const std::string root = cfg_.sysfs_root.empty() ? topo::sysfs_root() : cfg_.sysfs_root;
     int64_t next_rdma = cfg_.require_rdma ? mono_ns() : 0;
+    int64_t next_gid_look = 0;
+    constexpr int64_t kGidLookNs = 100LL * 1000000;
     std::string rdma_said = rdma_reason();
     bool labelled = ready_;  // false: L2 came up with a NIC still without carrier
     // One pollable fd for "stop, link event or health sample": the LLDP wait returns as soon as
@@ -270,6 +272,7 @@ void Agent::monitor(int stop_fd) {
         int64_t until = std::min(next_tx, mono_ns() + cfg_.monitor_tick_ns);
         if (holddown_until_ > 0) until = std::min(until, holddown_until_);
         if (next_rdma > 0) until = std::min(until, next_rdma);
+        if (gid_retry_until_ > 0) until = std::min(until, std::max(next_gid_look, mono_ns()));
         lldp_->run(until, on_frame, wait_fd);
         if (fd_readable(stop_fd)) return;
         for (auto& n : nics_) {  // a cached Port Description the switch never confirmed
@@ -361,6 +364,22 @@ void Agent::monitor(int stop_fd) {
         }
         if (topo_late_ && labelled && topo_call_.done())
             write_rccl_env_file();  // the topology worker answered after the start's deadline after all
+        if (gid_retry_until_ > 0 && mono_ns() >= next_gid_look) {
+            // GIDs the RDMA core had not (re)added when the artifacts were written: looked up again
+            // every 100 ms until --gid-wait has passed, never by blocking this loop.  Meanwhile
+            // rccl.env names no NCCL_IB_GID_INDEX (RCCL picks each HCA's RoCE v2 GID itself).
+            next_gid_look = mono_ns() + kGidLookNs;
+            if (look_up_gids() && labelled) write_rccl_env_file();
+            if (!gids_missing() || !labelled) {
+                gid_retry_until_ = 0;
+            } else if (mono_ns() >= gid_retry_until_) {
+                for (const auto& n : nics_)
+                    if (!n.rdma_dev.empty() && n.configured && !n.gid_index)
+                        NLOG_W("%s (%s): no RoCE v2 GID after %s; rccl.env gets no NCCL_IB_GID_INDEX for it", n.ifname.c_str(),
+                               n.rdma_dev.c_str(), format_go_duration(cfg_.gid_wait_ns).c_str());
+                gid_retry_until_ = 0;
+            }
+        }
         bool rdma_changed = false;
         if (next_rdma > 0 && mono_ns() >= next_rdma) {
             // --require-rdma: a driver container (or the node) loading the NICs' RDMA driver, and
@@ -406,9 +425,10 @@ void Agent::monitor(int stop_fd) {
                 if (!hold) {
                     holddown_until_ = 0;
                     if (cfg_.mode == "L3")
-                        write_artifacts();
+                        write_artifacts(0);
                     else if (!cfg_.rccl_env.empty() || !cfg_.rccl_topo.empty())
-                        write_l2_artifacts();  // a NIC that got its carrier (or RDMA device) only now has its GID now
+                        write_l2_artifacts(0);  // a NIC that got its carrier (or RDMA device) only now has its GID now
+                    gid_retry_until_ = gids_missing() ? mono_ns() + cfg_.gid_wait_ns : 0;
                     labelled = publish_label();
                     if (labelled && !phases_.count("total_ready")) phases_["total_ready"] = mono_ns() - t0_;
                     if (labelled) NLOG_I("All scale-out interfaces healthy again: readiness label republished");
@@ -431,10 +451,12 @@ void Agent::monitor(int stop_fd) {
                 if (rdma_changed && !rdma_missing().empty() && !cfg_.rccl_env.empty())
                     write_rccl_env_file();  // it names an HCA that is gone: removed until the devices are back
             } else if (healthy && labelled && cfg_.mode == "L3") {
-                write_artifacts();  // re-addressed NIC (or a renumbered RDMA device): refresh the RCCL artifacts
+                write_artifacts(0);  // re-addressed NIC (or a renumbered RDMA device): refresh the RCCL artifacts
+                gid_retry_until_ = gids_missing() ? mono_ns() + cfg_.gid_wait_ns : 0;
                 write_host_config();
             } else if (healthy && labelled && rdma_changed && (!cfg_.rccl_env.empty() || !cfg_.rccl_topo.empty())) {
-                write_l2_artifacts();  // L2: a renumbered RDMA device, its link-local GID
+                write_l2_artifacts(0);  // L2: a renumbered RDMA device, its link-local GID
+                gid_retry_until_ = gids_missing() ? mono_ns() + cfg_.gid_wait_ns : 0;
             }
             ready_ = labelled;
             write_status();

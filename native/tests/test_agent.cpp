@@ -3475,6 +3475,64 @@ TEST(agent_rccl_env_gid_index_is_never_stale_under_random_readdressing_and_flaps
     }
 }
 
+TEST(agent_monitor_never_blocks_on_a_gid_the_rdma_core_has_not_added_yet) {
+    // After ens1's flap the RDMA core has not re-added its RoCE v2 GID yet.  The monitor
+    // republishes the label at once (rccl.env without NCCL_IB_GID_INDEX: RCCL then picks each
+    // HCA's RoCE v2 GID itself) instead of waiting out --gid-wait (2 s here) on its loop, and
+    // names the index once the GID is there.
+    RdmaFixture f;
+    f.cfg.gid_wait_ns = 2000000000LL;
+    const std::map<std::string, std::string> ips = {{"ens0", "10.200.0.1"}, {"ens1", "10.200.0.5"}, {"ens2", "10.200.0.10"}};
+    auto put_gid = [&](const std::string& dev, const std::string& ip, bool present) {
+        const std::string d = "sys/class/infiniband/" + dev + "/ports/1/";
+        uint8_t b[4];
+        Ipv4::parse(ip)->to_net(b);
+        f.tmp.write(d + "gids/3", present ? strfmt("0000:0000:0000:0000:0000:ffff:%02x%02x:%02x%02x\n", b[0], b[1], b[2], b[3])
+                                          : std::string("0000:0000:0000:0000:0000:0000:0000:0000\n"));
+        f.tmp.write(d + "gid_attrs/types/3", "RoCE v2\n");
+    };
+    for (int k = 0; k < 3; ++k) {
+        f.bind("ens" + std::to_string(k), "mlx5_" + std::to_string(k));
+        put_gid("mlx5_" + std::to_string(k), ips.at("ens" + std::to_string(k)), true);
+    }
+    Pipe stop;
+    agent::Agent a(f.cfg, f.ops, f.all_valid(), f.nm());
+    int phase = 0;
+    int64_t t_up = 0, t_gid = 0, up_to_label = -1, gid_to_env = -1;
+    std::string env_without;
+    const int64_t t0 = mono_ns();
+    a.on_monitor_tick = [&](int) {
+        const bool labelled = path_exists(f.cfg.labels.path());
+        if (phase == 0 && labelled) {
+            put_gid("mlx5_1", ips.at("ens1"), false);  // gone with the link
+            f.ops.set_carrier("ens1", false);
+            phase = 1;
+        } else if (phase == 1 && !labelled) {
+            f.ops.set_carrier("ens1", true);  // back, its GID not yet
+            t_up = mono_ns();
+            phase = 2;
+        } else if (phase == 2 && labelled) {
+            up_to_label = mono_ns() - t_up;
+            env_without = read_file(f.cfg.rccl_env).value_or("");
+            put_gid("mlx5_1", ips.at("ens1"), true);  // the core adds it now
+            t_gid = mono_ns();
+            phase = 3;
+        } else if (phase == 3 && read_file(f.cfg.rccl_env).value_or("").find("NCCL_IB_GID_INDEX=3\n") != std::string::npos) {
+            gid_to_env = mono_ns() - t_gid;
+            phase = 4;
+            stop.fire();
+        } else if (mono_ns() - t0 > 8000000000LL) {
+            stop.fire();
+        }
+    };
+    a.run(stop.fd[0]);
+    CHECK_EQ(phase, 4);
+    CHECK(up_to_label >= 0 && up_to_label < 500000000LL);  // not the 2 s --gid-wait
+    CHECK(env_without.find("NCCL_IB_GID_INDEX") == std::string::npos);
+    CHECK(env_without.find("NCCL_IB_ROCE_VERSION_NUM=2\n") != std::string::npos);
+    CHECK(gid_to_env >= 0 && gid_to_env < 1000000000LL);  // looked up again every 100 ms
+}
+
 TEST(agent_require_rdma_past_the_wait_names_the_fault) {
     RdmaFixture f;
     f.cfg.rdma_wait_ns = 0;
