@@ -468,6 +468,7 @@ class Agent {
     std::vector<std::string> dry_run_missing_;  // discovered, but not in this network namespace
     bounded::Call<TopoResult> topo_call_;  // the topology worker (start_topo), joined with a deadline
     bool topo_late_ = false;                // it missed that deadline once: later joins only look
+    bool monitoring_ = false;               // in monitor(): joins wait briefly, a late file follows
     std::optional<TopoResult> topo_;
     topo::XgmiReport xgmi_;
     std::vector<topo::XgmiLinkHealth> xgmi_health_;

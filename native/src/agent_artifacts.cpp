@@ -209,15 +209,22 @@ const std::string& Agent::topo_xml() {
     if (!topo_) {
         if (!topo_call_.valid()) start_topo();
         // Bounded like every sysfs read of the start; once late, later artifact writes only look.
-        const int64_t deadline = topo_late_ ? mono_ns() : mono_ns() + cfg_.sysfs_read_timeout_ns;
+        // In the monitor (the file generated again for a renumbered RDMA device) the loop waits
+        // 20 ms at most (the walk takes 1-3 ms on the box): a late file is written when the
+        // worker answers (monitor(), topo_late_).
+        const int64_t wait = monitoring_ ? std::min<int64_t>(cfg_.sysfs_read_timeout_ns, 20000000) : cfg_.sysfs_read_timeout_ns;
+        const int64_t deadline = topo_late_ ? mono_ns() : mono_ns() + wait;
         try {
             auto r = topo_call_.wait(deadline);
             if (!r) {
-                if (!topo_late_) ++late_reads_["topology"];
-                if (!topo_late_)
+                if (!topo_late_ && monitoring_)  // (not a stall yet: the loop only does not wait for it)
+                    NLOG_V(1, "RCCL topology file still being generated: rccl.env names it when it is ready");
+                else if (!topo_late_) {
+                    ++late_reads_["topology"];
                     NLOG_W("The RCCL topology file was not generated within %s (a PCI attribute read stalled?): "
                            "rccl.env names no NCCL_TOPO_FILE until it is (RCCL then reads the topology itself)",
                            format_go_duration(cfg_.sysfs_read_timeout_ns).c_str());
+                }
                 topo_late_ = true;
                 return none;
             }

@@ -174,6 +174,7 @@ struct SharedFd {
 }  // namespace
 
 void Agent::monitor(int stop_fd) {
+    monitoring_ = true;
     std::unique_ptr<nl::LinkWatcher> watcher;
     try {
         watcher = ops_.subscribe_links();
