@@ -4,7 +4,8 @@ the NIC's driver and RDMA device), both ends' PCIe links as trained, the xGMI me
 every xGMI link's state (gpu_metrics), GPUDirect RDMA, and each rail's Ethernet link as the kernel
 has it now (state, negotiated speed, MTU).  When the agent has written its RCCL topology file
 (``--artifact-dir``, default /etc/amd/scale-out), the report also checks that the file places each
-GPU and its NIC as this node's PCIe tree does.
+GPU and its NIC as this node's PCIe tree does, and that ``rccl.env`` names the rails' current RDMA
+devices and, when it pins ``NCCL_IB_GID_INDEX``, a slot that holds a RoCE v2 GID on every one.
 
     python -m network_operator_amd.agent.report            # a table
     python -m network_operator_amd.agent.report --json     # the same as one JSON document
@@ -109,11 +110,53 @@ def collect(root: str, min_link_speed_gbps: float = 0, artifact_dir: str = "") -
             problems.append(f"{tf}: GPU(s) {', '.join(topo_file['gpus_missing'])} missing (a stale file?)")
         for gpu, nic in topo_file["pairs_split"]:
             problems.append(f"{tf}: places {nic} under another switch than GPU {gpu} (a stale file?)")
+    rccl_env = _check_rccl_env(root, os.path.join(artifact_dir, "rccl.env") if artifact_dir else "", rails, problems)
     return {"sysfs_root": root, "gpus": len(d["gpus"]), "rails": rails,
             "xgmi": {"pairs": f"{x['pairs_connected']}/{x['pairs_expected']}", "links": health},
             "gpudirect_rdma": gdr["mode"], "kernel": gdr["kernel"], "left_alone": d.get("excluded", {}),
-            "rccl_topology_file": topo_file,
+            "rccl_topology_file": topo_file, "rccl_env": rccl_env,
             "problems": problems}
+
+
+def _check_rccl_env(root: str, path: str, rails: List[dict], problems: List[str]):
+    """The agent's rccl.env against the node as it is now: every rail's current RDMA device named
+    (a driver reload renumbers them), none that is gone, and, when it pins NCCL_IB_GID_INDEX=k,
+    slot k of every named device holding a RoCE v2 GID (the RDMA core re-adds a netdev's GIDs in
+    whatever slot is free after its link went down)."""
+    if not path or not os.path.isfile(path):
+        return None
+    env = {}
+    with open(path) as f:
+        for line in f:
+            k, sep, v = line.strip().partition("=")
+            if sep and not k.startswith("#"):
+                env[k] = v
+    named = [h for h in env.get("NCCL_IB_HCA", "").lstrip("=^").split(",") if h]
+    devs = {h.split(":", 1)[0]: int(h.split(":", 1)[1]) if ":" in h and h.split(":", 1)[1].isdigit() else 1 for h in named}
+    current = {r["rdma_dev"] for r in rails if r["rdma_dev"]}
+    out = {"path": path, "hcas": sorted(devs), "gid_index": env.get("NCCL_IB_GID_INDEX"), "bad_gid_slots": []}
+    for dev in sorted(set(devs) - current):
+        problems.append(f"{path}: names RDMA device {dev}, which no rail has now (a driver reload renumbered it?)")
+    for r in rails:
+        if r["rdma_dev"] and devs and r["rdma_dev"] not in devs:
+            problems.append(f"{path}: does not name {r['nic']}'s RDMA device {r['rdma_dev']}")
+    gid = env.get("NCCL_IB_GID_INDEX", "")
+    if gid.isdigit():
+        for dev, port in sorted(devs.items()):
+            base = os.path.join(root, "class", "infiniband", dev, "ports", str(port))
+            try:
+                with open(os.path.join(base, "gids", gid)) as f:
+                    value = f.read().strip()
+                with open(os.path.join(base, "gid_attrs", "types", gid)) as f:
+                    kind = f.read().strip()
+            except OSError:
+                value, kind = "", ""
+            # (L3 pins an IPv4-mapped GID, L2 the link-local one: either, as long as it is RoCE v2)
+            if kind != "RoCE v2" or not value or set(value) <= {"0", ":"}:
+                out["bad_gid_slots"].append(dev)
+                problems.append(f"{path}: NCCL_IB_GID_INDEX={gid}, but slot {gid} of {dev} port {port} holds no RoCE v2 "
+                                f"GID ({value or 'unreadable'}{', ' + kind if kind else ''}): a stale index?")
+    return out
 
 
 def render(r: dict) -> str:
@@ -134,6 +177,9 @@ def render(r: dict) -> str:
     if r.get("rccl_topology_file"):
         t = r["rccl_topology_file"]
         out += ["", f"RCCL topology file {t['path']}: " + ("matches this node" if t["ok"] else "does not match this node")]
+    if r.get("rccl_env"):
+        e = r["rccl_env"]
+        out += [f"RCCL environment {e['path']}: HCAs {', '.join(e['hcas']) or '-'}, GID index {e['gid_index'] or 'not pinned'}"]
     out += ["", "Problems:" if r["problems"] else "No problems found."]
     out += [f"  - {p}" for p in r["problems"]]
     return "\n".join(out)

@@ -405,6 +405,47 @@ def test_node_report_names_what_would_keep_the_label_off(tmp_path):
                                f"GPU {fx['gpus'][1]['bdf']}: xGMI link(s) 2 down"], rep["problems"]
 
 
+def test_node_report_checks_rccl_env_against_the_rails_devices_and_gid_slots(tmp_path):
+    """The report reads the agent's rccl.env against the node as it is now: an HCA renumbered by a
+    driver reload (named but gone, the new one not named) and a pinned NCCL_IB_GID_INDEX whose slot
+    holds no RoCE v2 IPv4 GID on a device are each a problem; a current file is not."""
+    import sys
+
+    root = tmp_path / "sys"
+    fakesysfs.build_mi355x_node(root, n_gpus=2)
+    (root / "module" / "ib_uverbs").mkdir(parents=True)
+    art = tmp_path / "art"
+    art.mkdir()
+
+    def report():
+        r = subprocess.run([sys.executable, "-m", "network_operator_amd.agent.report", "--json", "--artifact-dir", str(art)],
+                           capture_output=True, text=True, timeout=60, env=dict(os.environ, SYSFS_ROOT=str(root)))
+        return r.returncode, json.loads(r.stdout)
+
+    rc, rep = report()
+    devs = [x["rdma_dev"] for x in rep["rails"]]
+    assert rc == 0 and all(devs) and rep["rccl_env"] is None
+    for i, dev in enumerate(devs):
+        fakesysfs.add_rocev2_gids(root, dev, [f"10.20{i}.0.1"])  # IPv4 RoCE v2 GID at slot 3
+    (art / "rccl.env").write_text(f"NCCL_IB_HCA=={devs[0]}:1,{devs[1]}:1\nNCCL_IB_GID_INDEX=3\n")
+    rc, rep = report()
+    assert rc == 0 and rep["problems"] == [] and rep["rccl_env"]["hcas"] == sorted(devs), rep
+    (art / "rccl.env").write_text(f"NCCL_IB_HCA=={devs[0]}:1,mlx5_9:1\nNCCL_IB_GID_INDEX=2\n")  # slot 2: RoCE v1
+    rc, rep = report()
+    env = str(art / "rccl.env")
+    assert rc == 1
+    assert f"{env}: names RDMA device mlx5_9, which no rail has now (a driver reload renumbered it?)" in rep["problems"]
+    assert f"{env}: does not name {rep['rails'][1]['nic']}'s RDMA device {devs[1]}" in rep["problems"]
+    assert any(p.startswith(f"{env}: NCCL_IB_GID_INDEX=2, but slot 2 of {devs[0]} port 1 holds no RoCE v2 GID")
+               for p in rep["problems"]), rep["problems"]
+    (art / "rccl.env").write_text(f"NCCL_IB_HCA=={devs[0]}:1,{devs[1]}:1\nNCCL_IB_GID_INDEX=1\n")  # L2: link-local v2
+    rc, rep = report()
+    assert rc == 0 and rep["problems"] == [], rep["problems"]
+    (art / "rccl.env").write_text(f"NCCL_IB_HCA=={devs[0]}:1,{devs[1]}:1\nNCCL_IB_GID_INDEX=7\n")  # an empty slot
+    rc, rep = report()
+    assert rc == 1 and len(rep["rccl_env"]["bad_gid_slots"]) == 2
+
+
 def test_a_gpu_metrics_read_that_never_returns_neither_hangs_the_start_nor_hides_the_reason(native, tmp_path):
     """every start-path sysfs join has a deadline.  GPU 2's gpu_metrics is a FIFO
     nobody writes (a wedged SMU: the read never returns).  The dry run ends after
