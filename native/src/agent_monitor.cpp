@@ -370,7 +370,12 @@ void Agent::monitor(int stop_fd) {
             // every 100 ms until --gid-wait has passed, never by blocking this loop.  Meanwhile
             // rccl.env names no NCCL_IB_GID_INDEX (RCCL picks each HCA's RoCE v2 GID itself).
             next_gid_look = mono_ns() + kGidLookNs;
-            if (look_up_gids() && labelled) write_rccl_env_file();
+            if (look_up_gids() && labelled) {  // every artifact that names a GID index: rccl.env, L3's rccl-net.json
+                if (cfg_.mode == "L3")
+                    write_artifacts(0);
+                else
+                    write_l2_artifacts(0);
+            }
             if (!gids_missing() || !labelled) {
                 gid_retry_until_ = 0;
             } else if (mono_ns() >= gid_retry_until_) {

@@ -3531,6 +3531,11 @@ TEST(agent_monitor_never_blocks_on_a_gid_the_rdma_core_has_not_added_yet) {
     CHECK(env_without.find("NCCL_IB_GID_INDEX") == std::string::npos);
     CHECK(env_without.find("NCCL_IB_ROCE_VERSION_NUM=2\n") != std::string::npos);
     CHECK(gid_to_env >= 0 && gid_to_env < 1000000000LL);  // looked up again every 100 ms
+    // rccl-net.json names each NIC's GID index too: rewritten with it (all three rails at 3)
+    auto net = read_file(f.cfg.rccl_net).value_or("");
+    size_t count = 0;
+    for (size_t at = net.find("\"GID_INDEX\":3"); at != std::string::npos; at = net.find("\"GID_INDEX\":3", at + 1)) ++count;
+    CHECK_EQ(count, size_t(3));
 }
 
 TEST(agent_require_rdma_past_the_wait_names_the_fault) {
