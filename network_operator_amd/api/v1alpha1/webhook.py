@@ -357,6 +357,11 @@ def image_tag(image: str) -> str:
     return name.split(":", 1)[1] if ":" in name else ""
 
 
+ALLOW_POLICY_ROUTED_WARNING = ("allowPolicyRouted: the agent flushes and re-MTUs a selected NIC even when its default route in a "
+                               "policy-routing table carries the node's own address; if the node reaches a network through "
+                               "it, configuring it can cut the node off")
+
+
 def validate_amd_so_spec(s: T.AmdScaleOutSpec) -> List[str]:
     """Returns admission warnings.  (The reference's validateGaudiSoSpec is a no-op, :87-89.)"""
     warnings = []
@@ -387,6 +392,8 @@ def validate_amd_so_spec(s: T.AmdScaleOutSpec) -> List[str]:
     if s.requireRdma is False:
         warnings.append("requireRdma false: nodes whose scale-out NICs have no RDMA device are labelled scale-out "
                         "ready, and RCCL falls back to TCP sockets on those rails")
+    if s.allowPolicyRouted:
+        warnings.append(ALLOW_POLICY_ROUTED_WARNING)
     tag = image_tag(s.image)
     if s.image and tag not in ("", "latest", T.OPERATOR_VERSION):
         # the operator passes the flags of its own agent release; an older agent binary
@@ -416,6 +423,8 @@ def validate_host_nic_spec(s: Optional[T.HostNicSpec]) -> List[str]:
         warnings.append("hostNic: no interfaces or nicDrivers given; every RDMA NIC of the default driver list "
                         "that is neither a GPU's scale-out rail nor the node's own NIC (default route, non-/30 "
                         "address) will be configured")
+    if s.allowPolicyRouted:
+        warnings.append("hostNic." + ALLOW_POLICY_ROUTED_WARNING)
     if s.includeGpuRails and s.interfaces:
         warnings.append("hostNic.includeGpuRails has no effect with interfaces (the named NICs are taken as named)")
     elif s.includeGpuRails:

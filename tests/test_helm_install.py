@@ -486,11 +486,12 @@ def test_every_policy_field_is_settable_from_the_chart_and_documented():
 
     # (carrierWait is an L2 setting; these values are an L3 policy)
     # (and the pinned agent tag 9.9 draws the older-agent warning)
+    # (and allowPolicyRouted draws its safety warning)
     assert [w for w in W.validate_create(seeded["netconf-amd-scale-out"])
-            if "carrierWait" not in w and "pins agent tag '9.9'" not in w] == []
+            if "carrierWait" not in w and "pins agent tag '9.9'" not in w and "allowPolicyRouted" not in w] == []
     # (includeGpuRails next to interfaces only draws the "no effect" warning)
     assert [w for w in W.validate_create(seeded["netconf-amd-host-nic"])
-            if "includeGpuRails" not in w and "carrierWait" not in w] == []
+            if "includeGpuRails" not in w and "carrierWait" not in w and "allowPolicyRouted" not in w] == []
 
     # Defaults render the policy the CRD defaults describe: no optional field forced on.
     plain = yaml.safe_load(_configmap_text(helm_template(CHART, {"config": {"amd": {"enabled": True},

@@ -316,8 +316,11 @@ def test_allow_policy_routed_reaches_the_agent_from_either_policy_type():
     the policy carries it (amdScaleOut / hostNic.allowPolicyRouted), off by default."""
     from network_operator_amd.operator import reconciler as R
 
+    from network_operator_amd.api.v1alpha1 import webhook as W
+
     p = T.new_policy("x", layer="L3", allowPolicyRouted=True)
     assert "--allow-policy-routed" in agent_args(p)
+    assert W.validate_create(p) == [W.ALLOW_POLICY_ROUTED_WARNING]  # said at kubectl apply
     assert T.NetworkClusterPolicy.from_dict(p.to_dict()).spec.amdScaleOut.allowPolicyRouted is True
     assert "--allow-policy-routed" not in agent_args(T.new_policy("x", layer="L3"))
     hn = T.new_host_nic_policy("h", layer="L3", allowPolicyRouted=True)
