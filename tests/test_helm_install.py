@@ -544,6 +544,9 @@ def test_monitoring_objects_render_only_when_enabled_and_keep_prometheus_templat
     assert rules["spec"] == M.prometheus_rules()["spec"]  # every alert, its {{ $labels.x }} text intact
     summaries = [r["annotations"]["summary"] for g in rules["spec"]["groups"] for r in g["rules"]]
     assert any("{{ $labels.nic }}" in s for s in summaries) and any("{{ $value }}" in s for s in summaries)
+    dash = [d for d in helm_template(CHART, {"monitoring": {"enabled": True}}, NS)
+            if d["kind"] == "ConfigMap" and d["metadata"]["name"] == M.PREFIX + "dashboard"]
+    assert len(dash) == 1 and dash[0]["data"] == M.grafana_dashboard_configmap()["data"]  # the JSON survives Helm
     svc = next(d for d in helm_template(CHART, {}, NS) if d["kind"] == "Service" and d["metadata"]["name"].endswith("metrics"))
     monitor = next(d for d in docs if d["kind"] == "ServiceMonitor")
     assert monitor["spec"]["endpoints"][0]["port"] in [p["name"] for p in svc["spec"]["ports"]]

@@ -502,7 +502,7 @@ def test_rendered_deployments_are_up_to_date():
 def test_prometheus_overlay_scrapes_the_operator_and_the_agents():
     docs = kustomize_build(ROOT / "config/operator/prometheus")
     kinds = sorted(d["kind"] for d in docs)
-    assert kinds == ["PodMonitor", "PrometheusRule", "ServiceMonitor"]
+    assert kinds == ["ConfigMap", "PodMonitor", "PrometheusRule", "ServiceMonitor"]  # (the ConfigMap: the dashboard)
     pm = next(d for d in docs if d["kind"] == "PodMonitor")
     assert pm["spec"]["selector"]["matchLabels"] == {"app": "amd-network-tools"}
     assert pm["spec"]["podMetricsEndpoints"][0]["port"] == "metrics"  # the container port metricsPort opens
@@ -536,6 +536,37 @@ def test_alert_rules_use_only_metrics_that_exist():
                 assert name in operator_names, (r["alert"], name)
     kust = yaml.safe_load((ROOT / "config/operator/prometheus/kustomization.yaml").read_text())
     assert "alert-rules.yaml" in kust["resources"]
+
+
+def test_grafana_dashboard_reads_only_metrics_that_exist():
+    """The dashboard ConfigMap (config/operator/prometheus/dashboard.yaml, and the chart's with
+    monitoring.enabled): valid Grafana JSON whose every panel queries exported series, labelled
+    for the Grafana sidecar."""
+    import re
+
+    from network_operator_amd.operator.metrics import OperatorMetrics
+
+    cm = yaml.safe_load((ROOT / "config/operator/prometheus/dashboard.yaml").read_text())
+    assert cm["kind"] == "ConfigMap" and cm["metadata"]["labels"]["grafana_dashboard"] == "1"
+    dash = json.loads(cm["data"]["amd-network-operator.json"])
+    assert dash["uid"] == "amd-network-operator"
+    operator_names = set()
+    for fam in OperatorMetrics().registry.collect():
+        operator_names.add(fam.name + ("_total" if fam.type == "counter" else ""))
+        if fam.type == "histogram":  # (labelled: no samples before the first observation)
+            operator_names.update(fam.name + x for x in ("_bucket", "_sum", "_count"))
+        operator_names.update(s.name for s in fam.samples)
+    agent_src = (ROOT / "native/src/agent_status.cpp").read_text()
+    panels = [p for p in dash["panels"] if p["type"] == "timeseries"]
+    assert len(panels) >= 12 and len({p["id"] for p in dash["panels"]}) == len(dash["panels"])
+    for p in panels:
+        for name in re.findall(r"\b((?:amd_network_operator|netop_agent)_[a-z_]+)", p["targets"][0]["expr"]):
+            if name.startswith("netop_agent_"):
+                assert f'metric("{name}"' in agent_src, (p["title"], name)
+            else:
+                assert name in operator_names, (p["title"], name)
+    kust = yaml.safe_load((ROOT / "config/operator/prometheus/kustomization.yaml").read_text())
+    assert "dashboard.yaml" in kust["resources"]
 
 
 def test_ci_builds_and_scans_every_image():
