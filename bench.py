@@ -40,7 +40,8 @@ rccl-tests 8-GPU all-reduce".
   line, always.
 * At n = 1 there are no links and busbw is 0 by definition; the single-rank all-reduce is a
   no-op, so algbw is reported as null with the reason, and ``node_ready_gpu_side`` times the
-  agent phases that run unprivileged on the box.  The netns node-ready harness needs a private
+  agent phases that run unprivileged on the box (``agent_binary``: ten dry runs of the real
+  ``discover`` with the operator's flags, its own phase timings and the process wall time).  The netns node-ready harness needs a private
   network namespace and is reported null with the reason where that is unavailable.
 * Data are synthetic (RCCL moves the same bytes whatever their values).
 """
