@@ -1764,6 +1764,84 @@ TEST(agent_keep_config_leaves_the_data_plane_and_the_next_agent_adopts_it) {
     CHECK_EQ(f.ops.rules.size(), size_t(3));
 }
 
+TEST(agent_keep_config_restarts_and_readdressing_keep_every_nic_on_its_switch_ports_address) {
+    // Property (L3, --keep-config, LLDP cache, rail tables): under any sequence of switch-port
+    // re-addressing and agent restarts (a rolling update; half of them with the switch silent at
+    // first, so the new agent starts from its cache), once an agent has caught up every NIC holds
+    // exactly the /30 its switch port describes now, one rail rule each, and the node is labelled.
+    // Three seeds, 30 checked steps each.
+    for (uint64_t seed : {0x5EED0001ull, 0x5EED0002ull, 0x5EED0003ull}) {
+        Fixture f;
+        f.cfg.keep_config = true;
+        f.cfg.rail_table_base = 100;
+        f.cfg.monitor_tick_ns = 1000000;
+        f.cfg.lldp_tx_interval_ns = 3600LL * 1000000000LL;
+        f.cfg.lldp_cache = f.tmp.path + "/lldp-cache";
+        const std::vector<std::string> nics = {"ens0", "ens1", "ens2"};
+        const std::map<std::string, int> idx = {{"ens0", 10}, {"ens1", 11}, {"ens2", 12}};
+        std::map<std::string, int> host = {{"ens0", 1}, {"ens1", 1}, {"ens2", 1}};
+        auto frame = [&](const std::string& n) {
+            const int k = int(n.back() - '0');
+            return sw(strfmt("02:aa:00:00:00:0%d", k).c_str(), strfmt("no-alert 10.20%d.0.%d/30", k, 4 * host.at(n) + 2).c_str());
+        };
+        uint64_t rng = seed;
+        auto next = [&] {
+            rng ^= rng << 13;
+            rng ^= rng >> 7;
+            rng ^= rng << 17;
+            return rng;
+        };
+        int steps = 0, mismatches = 0, restarts = 0, readdressed = 0;
+        std::string first_bad;
+        for (int run = 0; steps < 30 && run < 40; ++run) {
+            auto src = std::make_unique<ScriptedLldp>();
+            ScriptedLldp* raw = src.get();
+            const bool silent = run > 0 && next() % 2;  // the new agent starts from its cache
+            if (!silent)
+                for (const auto& n : nics) raw->frames[n] = frame(n);
+            Pipe stop;
+            agent::Agent a(f.cfg, f.ops, std::move(src), f.nm());
+            int64_t t_step = mono_ns();
+            a.on_monitor_tick = [&](int tick) {
+                if (silent && tick == 3)
+                    for (const auto& n : nics) raw->frames[n] = frame(n);  // the switch speaks again
+                if (mono_ns() - t_step < 20000000LL) return;
+                std::string bad;
+                for (const auto& n : nics) {
+                    const int k = int(n.back() - '0');
+                    const std::string expect = strfmt("10.20%d.0.%d/30", k, 4 * host.at(n) + 1);
+                    std::vector<std::string> have;
+                    for (const auto& x : f.ops.addrs)
+                        if (x.ifindex == idx.at(n)) have.push_back(x.prefix().str());
+                    if (have != std::vector<std::string>{expect}) bad += " " + n + " holds " + join(have, ",") + " not " + expect;
+                }
+                if (f.ops.rules.size() != nics.size()) bad += strfmt(" %zu rail rules", f.ops.rules.size());
+                if (!path_exists(f.cfg.labels.path())) bad += " no label";
+                if (!bad.empty() && mono_ns() - t_step < 2000000000LL) return;  // a loaded machine: up to 2 s more
+                if (!bad.empty()) {
+                    if (!mismatches) first_bad = strfmt("step %d (run %d%s):", steps, run, silent ? ", cache start" : "") + bad;
+                    ++mismatches;
+                }
+                if (++steps >= 30 || next() % 3 == 0) {  // a rolling update: this agent goes, the next comes
+                    ++restarts;
+                    stop.fire();
+                    return;
+                }
+                const std::string& n = nics[next() % nics.size()];
+                host[n] = 1 + int(next() % 8);
+                raw->frames[n] = frame(n);
+                ++readdressed;
+                t_step = mono_ns();
+            };
+            a.run(stop.fd[0]);
+        }
+        if (mismatches) fprintf(stderr, "seed %llx, %s\n", (unsigned long long)seed, first_bad.c_str());
+        CHECK_EQ(mismatches, 0);
+        CHECK_EQ(steps, 30);
+        CHECK(restarts > 3 && readdressed > 3);
+    }
+}
+
 TEST(agent_keep_config_does_not_adopt_a_stale_or_foreign_cache_entry) {
     Fixture f;
     f.cfg.keep_config = true;
