@@ -28,6 +28,25 @@ def test_discover_help_lists_reference_flags():
         assert flag in out, flag
 
 
+def test_every_agent_flag_is_documented():
+    """Each flag `discover --help` lists is explained in the docs (USER_GUIDE / ARCHITECTURE / README)."""
+    import re
+    from pathlib import Path
+    out = subprocess.run([str(native_bin("discover")), "--help"], capture_output=True, text=True).stdout
+    flags = re.findall(r"^\s+(--[a-z0-9_-]+)", out, re.M)
+    assert len(flags) > 60
+    root = Path(__file__).resolve().parent.parent
+    docs = "".join(p.read_text() for p in [root / "README.md", *sorted((root / "docs").glob("*.md"))])
+    assert [f for f in flags if not re.search(re.escape(f) + r"(?![a-z0-9-])", docs)] == []
+    # and the operator manager's
+    import sys
+    out = subprocess.run([sys.executable, "-m", "network_operator_amd.operator.manager", "--help"],
+                         capture_output=True, text=True).stdout
+    flags = re.findall(r"^\s+(--[a-z0-9_-]+)", out, re.M)
+    assert len(flags) > 15
+    assert [f for f in flags if not re.search(re.escape(f) + r"(?![a-z0-9-])", docs)] == []
+
+
 def test_discover_rejects_bad_flags():
     r = subprocess.run([str(native_bin("discover")), "--wait=90"], capture_output=True, text=True)
     assert r.returncode == 2 and "invalid duration" in r.stderr
