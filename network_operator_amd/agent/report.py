@@ -126,7 +126,7 @@ def _check_rccl_env(root: str, path: str, rails: List[dict], problems: List[str]
     if not path or not os.path.isfile(path):
         return None
     env = {}
-    with open(path) as f:
+    with open(path, errors="replace") as f:  # whatever is in the file, the report says what it found
         for line in f:
             k, sep, v = line.strip().partition("=")
             if sep and not k.startswith("#"):
@@ -145,11 +145,11 @@ def _check_rccl_env(root: str, path: str, rails: List[dict], problems: List[str]
         for dev, port in sorted(devs.items()):
             base = os.path.join(root, "class", "infiniband", dev, "ports", str(port))
             try:
-                with open(os.path.join(base, "gids", gid)) as f:
+                with open(os.path.join(base, "gids", gid), errors="replace") as f:
                     value = f.read().strip()
-                with open(os.path.join(base, "gid_attrs", "types", gid)) as f:
+                with open(os.path.join(base, "gid_attrs", "types", gid), errors="replace") as f:
                     kind = f.read().strip()
-            except OSError:
+            except (OSError, ValueError):  # (ValueError: a NUL in a device name from the file)
                 value, kind = "", ""
             # (L3 pins an IPv4-mapped GID, L2 the link-local one: either, as long as it is RoCE v2)
             if kind != "RoCE v2" or not value or set(value) <= {"0", ":"}:

@@ -465,6 +465,25 @@ def test_node_report_checks_rccl_env_against_the_rails_devices_and_gid_slots(tmp
     assert rc == 1 and len(rep["rccl_env"]["bad_gid_slots"]) == 2
 
 
+@settings(max_examples=150, deadline=None)
+@given(data=st.one_of(st.binary(max_size=300),
+                      st.lists(st.sampled_from(["NCCL_IB_HCA==mlx5_0:1,mlx5_9", "NCCL_IB_HCA=^", "NCCL_IB_HCA=a:b:c,,",
+                                                "NCCL_IB_GID_INDEX=3", "NCCL_IB_GID_INDEX=99999999999", "NCCL_IB_GID_INDEX=-1",
+                                                "NCCL_IB_HCA=../../..:1", "NCCL_IB_HCA=x\x00y:1", "# c", "=", "\xff\xfe"]),
+                               max_size=6).map(lambda ls: "\n".join(ls).encode("utf-8", "surrogatepass"))))
+def test_node_report_rccl_env_check_never_crashes_on_a_garbled_file(tmp_path_factory, data):
+    """Whatever bytes sit in rccl.env (a torn write, another tool's file), the report's check returns
+    what it found and names problems; it never raises."""
+    from network_operator_amd.agent.report import _check_rccl_env
+
+    d = tmp_path_factory.mktemp("env")
+    (d / "rccl.env").write_bytes(data)
+    problems = []
+    out = _check_rccl_env(str(d / "sys"), str(d / "rccl.env"),
+                          [{"nic": "ens0", "rdma_dev": "mlx5_0"}, {"nic": "ens1", "rdma_dev": ""}], problems)
+    assert isinstance(out["hcas"], list) and all(isinstance(p, str) for p in problems)
+
+
 def test_a_gpu_metrics_read_that_never_returns_neither_hangs_the_start_nor_hides_the_reason(native, tmp_path):
     """every start-path sysfs join has a deadline.  GPU 2's gpu_metrics is a FIFO
     nobody writes (a wedged SMU: the read never returns).  The dry run ends after
