@@ -104,8 +104,15 @@ def collect(root: str, min_link_speed_gbps: float = 0, artifact_dir: str = "") -
         from ..models.topology import NodeTopology
         from ..validate import topo_file_agrees
 
-        with open(tf) as f:
-            topo_file = dict(topo_file_agrees(f.read(), NodeTopology.discover(root, with_xgmi=False)), path=tf)
+        import xml.etree.ElementTree as ET
+
+        with open(tf, errors="replace") as f:
+            text = f.read()
+        try:
+            topo_file = dict(topo_file_agrees(text, NodeTopology.discover(root, with_xgmi=False)), path=tf)
+        except ET.ParseError as e:  # torn or foreign: RCCL would refuse it too
+            topo_file = {"ok": False, "gpus_missing": [], "pairs_split": [], "path": tf, "error": str(e)}
+            problems.append(f"{tf}: not a topology file RCCL can read ({e})")
         if topo_file["gpus_missing"]:
             problems.append(f"{tf}: GPU(s) {', '.join(topo_file['gpus_missing'])} missing (a stale file?)")
         for gpu, nic in topo_file["pairs_split"]:

@@ -465,6 +465,21 @@ def test_node_report_checks_rccl_env_against_the_rails_devices_and_gid_slots(tmp
     assert rc == 1 and len(rep["rccl_env"]["bad_gid_slots"]) == 2
 
 
+def test_node_report_names_a_torn_topology_file(tmp_path):
+    import sys
+
+    root = tmp_path / "sys"
+    fakesysfs.build_mi355x_node(root, n_gpus=2)
+    art = tmp_path / "art"
+    art.mkdir()
+    (art / "rccl-topo.xml").write_bytes(b'<system version="1"><cpu numaid="0"><pci busid="0000:0')
+    r = subprocess.run([sys.executable, "-m", "network_operator_amd.agent.report", "--json", "--artifact-dir", str(art)],
+                       capture_output=True, text=True, timeout=60, env=dict(os.environ, SYSFS_ROOT=str(root)))
+    rep = json.loads(r.stdout)
+    assert r.returncode == 1 and rep["rccl_topology_file"]["ok"] is False
+    assert any("not a topology file RCCL can read" in p for p in rep["problems"]), rep["problems"]
+
+
 @settings(max_examples=150, deadline=None)
 @given(data=st.one_of(st.binary(max_size=300),
                       st.lists(st.sampled_from(["NCCL_IB_HCA==mlx5_0:1,mlx5_9", "NCCL_IB_HCA=^", "NCCL_IB_HCA=a:b:c,,",
