@@ -16,7 +16,7 @@ from network_operator_amd.utils import native_bin
 
 
 def test_cpp_unit_suite():
-    r = subprocess.run([str(native_bin("netop-unit-tests"))], capture_output=True, text=True, timeout=900)
+    r = subprocess.run([str(native_bin("netop-unit-tests"))], capture_output=True, text=True, timeout=540)  # (pytest-timeout: 600)
     assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-2000:]
     assert "FAIL" not in r.stdout
 
