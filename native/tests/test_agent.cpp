@@ -1842,6 +1842,69 @@ TEST(agent_keep_config_restarts_and_readdressing_keep_every_nic_on_its_switch_po
     }
 }
 
+TEST(agent_l2_keep_config_rolling_restarts_under_random_cable_pulls_never_take_a_link_down) {
+    // Property (L2, --keep-config, the monitor): under random cable pulls and re-plugs interleaved
+    // with agent restarts (a rolling update), no agent ever sets a scale-out link down -- jobs keep
+    // their links through the roll -- and once an agent has caught up the label is published
+    // exactly when every NIC has carrier.  Three seeds, 60 checked steps each.
+    for (uint64_t seed : {0x4C32000000000001ull, 0x4C32000000000002ull, 0x4C32000000000003ull}) {
+        Fixture f;
+        f.cfg.mode = "L2";
+        f.cfg.keep_config = true;
+        f.cfg.monitor_tick_ns = 1000000;
+        f.cfg.carrier_wait_ns = 20000000;  // a restart with a pulled cable goes on to the monitor
+        const std::vector<std::string> nics = {"ens0", "ens1", "ens2"};
+        std::map<std::string, bool> carrier = {{"ens0", true}, {"ens1", true}, {"ens2", true}};
+        uint64_t rng = seed;
+        auto next = [&] {
+            rng ^= rng << 13;
+            rng ^= rng >> 7;
+            rng ^= rng << 17;
+            return rng;
+        };
+        int steps = 0, mismatches = 0, restarts = 0, pulls = 0, labelled_states = 0;
+        std::string first_bad;
+        for (int run = 0; steps < 60 && run < 80; ++run) {
+            Pipe stop;
+            agent::Agent a(f.cfg, f.ops, std::make_unique<ScriptedLldp>(), f.nm());
+            int64_t t_step = mono_ns();
+            a.on_monitor_tick = [&](int) {
+                if (mono_ns() - t_step < 10000000LL) return;
+                const bool want = std::all_of(nics.begin(), nics.end(), [&](const std::string& n) { return carrier[n]; });
+                const bool label = path_exists(f.cfg.labels.path());
+                std::string bad;
+                if (label != want) bad += strfmt(" label %d, want %d", label, want);
+                for (const auto& n : nics)
+                    if (!(f.ops.links[n].flags & IFF_UP)) bad += " " + n + " admin-down";
+                if (f.ops.calls["link_set_down"]) bad += " a link was set down";
+                if (!bad.empty() && mono_ns() - t_step < 2000000000LL) return;  // a loaded machine: up to 2 s more
+                if (!bad.empty()) {
+                    if (!mismatches) first_bad = strfmt("step %d (run %d):", steps, run) + bad;
+                    ++mismatches;
+                }
+                labelled_states += want;
+                if (++steps >= 60 || next() % 4 == 0) {  // this agent goes, the next comes
+                    ++restarts;
+                    stop.fire();
+                    return;
+                }
+                const std::string& n = nics[next() % nics.size()];
+                carrier[n] = !carrier[n];
+                f.ops.set_carrier(n, carrier[n]);
+                ++pulls;
+                t_step = mono_ns();
+            };
+            a.run(stop.fd[0]);
+        }
+        if (mismatches) fprintf(stderr, "seed %llx, %s\n", (unsigned long long)seed, first_bad.c_str());
+        CHECK_EQ(mismatches, 0);
+        CHECK_EQ(steps, 60);
+        CHECK(restarts > 5 && pulls > 20);
+        CHECK(labelled_states > 0 && labelled_states < steps);  // both states visited
+        CHECK_EQ(f.ops.calls["link_set_down"], 0);
+    }
+}
+
 TEST(agent_keep_config_does_not_adopt_a_stale_or_foreign_cache_entry) {
     Fixture f;
     f.cfg.keep_config = true;
