@@ -323,6 +323,8 @@ def _worker(args) -> int:
     if not sizes or sizes[-1] != args.bytes:
         sizes.append(args.bytes)
     comm = XgmiAllReduce(args.bytes, device=dev, timeout_s=args.timeout)
+    if args.soak:
+        return _soak(args, comm, rank, world)
 
     def measure(fn, check, nbytes: int, factor: float, **row) -> dict:
         """Three exact checks (seeds on reused buffers), warmup, `iters` timed calls; max time
@@ -383,6 +385,46 @@ def _worker(args) -> int:
     return 0
 
 
+def _soak(args, comm, rank: int, world: int) -> int:
+    """`--soak N`: N all-reduces, each on a fresh pattern and each checked exactly, cycling the
+    algorithms over sizes drawn (same seed on every rank) from 4 KiB to --bytes, every third
+    call straight after the previous one without a host round trip in between.  What a timed
+    loop cannot show: a flag, barrier or buffer-reuse race that corrupts one call in hundreds."""
+    import random
+
+    import torch
+    import torch.distributed as dist
+
+    rng = random.Random(20261018)
+    algos = args.algos.split(",")
+    wrong = {a: 0 for a in algos}
+    calls = {a: 0 for a in algos}
+    t0 = time.perf_counter()
+    for i in range(args.soak):
+        algo = algos[i % len(algos)]
+        align = 8 if algo == "one_shot" else 8 * world
+        numel = max(align, rng.randrange(2048, args.bytes // 2 + 1) // align * align)
+        seed = 1000 + i
+        H.fill_pattern(comm.input(numel), seed, rank)
+        out = comm.all_reduce(numel, algo)
+        if i % 3 == 2:  # back to back: the next call's fill and exchange race this one's readers
+            H.fill_pattern(comm.input(numel), seed + 7, rank)
+            out = comm.all_reduce(numel, algo)
+            seed += 7
+        wrong[algo] += H.verify_sum(out, seed, world)
+        calls[algo] += 1
+    torch.cuda.synchronize()
+    w = torch.tensor([wrong[a] for a in algos], dtype=torch.int64)
+    dist.all_reduce(w, op=dist.ReduceOp.SUM)
+    if rank == 0:
+        print(json.dumps({"ranks": world, "soak": args.soak, "seconds": round(time.perf_counter() - t0, 2),
+                          "calls": calls, "wrong_by_algo": {a: int(x) for a, x in zip(algos, w.tolist())},
+                          "wrong": int(w.sum())}), flush=True)
+    comm.close()
+    dist.destroy_process_group()
+    return 0
+
+
 def _free_port() -> int:
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -436,7 +478,7 @@ def spawn_ranks(world: int, cmd: list, timeout: float, extra_env: Optional[dict]
 
 
 def run(world: int, nbytes: int = 1 << 30, min_bytes: Optional[int] = None, iters: int = 10, warmup: int = 3,
-        algos: str = ",".join(ALGOS), devices: Optional[str] = None, timeout: float = 120.0) -> dict:
+        algos: str = ",".join(ALGOS), devices: Optional[str] = None, timeout: float = 120.0, soak: int = 0) -> dict:
     """Spawns `world` rank processes (one per GPU unless `devices` maps several onto one) and
     returns rank 0's result.  Safe to call from inside another distributed job: the children
     get their own rendezvous and none of the parent's launcher variables."""
@@ -445,6 +487,8 @@ def run(world: int, nbytes: int = 1 << 30, min_bytes: Optional[int] = None, iter
            "--timeout", str(min(timeout, 60.0))]
     if devices:
         cmd += ["--devices", devices]
+    if soak:
+        cmd += ["--soak", str(soak)]
     procs, outs = spawn_ranks(world, cmd, timeout)
     bad = [(r, p.returncode, o[-1500:]) for r, (p, o) in enumerate(zip(procs, outs)) if p.returncode != 0]
     if bad:
@@ -466,6 +510,7 @@ def main(argv=None) -> int:
     ap.add_argument("--algos", default=",".join(ALGOS))
     ap.add_argument("--devices", default="", help="comma list of GPU ids per rank (repeats allowed: virtual ranks)")
     ap.add_argument("--timeout", type=float, default=120.0)
+    ap.add_argument("--soak", type=int, default=0, help="instead of timing: this many all-reduces, each checked exactly")
     a = ap.parse_args(argv)
     if a.worker:
         if not a.min_bytes:
@@ -477,7 +522,7 @@ def main(argv=None) -> int:
 
         world = torch.cuda.device_count()
     print(json.dumps(run(world, a.bytes, a.min_bytes or None, a.iters, a.warmup, a.algos, a.devices or None,
-                         a.timeout)))
+                         a.timeout, a.soak)))
     return 0
 
 

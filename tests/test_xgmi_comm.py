@@ -99,6 +99,18 @@ def test_xgmi_allreduce_multiprocess_virtual_ranks(cuda_device, world):
 
 
 @pytest.mark.gpu
+def test_xgmi_allreduce_multiprocess_soak_every_call_exact(cuda_device):
+    """150 all-reduces over 4 rank processes on the one GPU, each on a fresh pattern and checked
+    exactly: the three algorithms in turn, random sizes, every third call straight after the
+    previous one (its input refilled while peers may still be reading the last one's)."""
+    from network_operator_amd.parallel import xgmi_comm
+
+    r = xgmi_comm.run(4, nbytes=4 << 20, devices="0,0,0,0", timeout=110, soak=150)
+    assert r["soak"] == 150 and sum(r["calls"].values()) == 150, json.dumps(r)
+    assert r["wrong"] == 0, json.dumps(r)
+
+
+@pytest.mark.gpu
 def test_single_process_xgmi_allreduce_virtual_ranks_exact(cuda_device):
     """netop-xgmi-allreduce (the single-process two-shot bench.py runs on the whole-node run):
     four ranks mapped onto the one GPU run the full algorithm, pull and push, with every chunk,
