@@ -1,6 +1,6 @@
 #!/bin/bash
 # Soak of the multi-process direct xGMI all-reduce on the 1-GPU box: the GPU test, then 8 virtual
-# ranks x 600 calls (random sizes up to 64 MiB, the three algorithms), every call checked exactly.
+# ranks x 20000 calls (random sizes up to 64 MiB, the three algorithms), every call checked exactly.
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -8,6 +8,6 @@ timeout -k 10 200 python3 -u -m pytest tests/test_xgmi_comm.py -k soak -m gpu -x
 tail -4 gpurun_out/xcomm_soak_pytest.log
 [ $rc -eq 0 ] || exit $rc
 timeout -k 10 400 python3 -m network_operator_amd.parallel.xgmi_comm --world 8 --devices 0,0,0,0,0,0,0,0 \
-  --bytes 67108864 --soak 600 --timeout 380 > gpurun_out/xcomm_soak_virtual8.json 2> gpurun_out/xcomm_soak_virtual8.err; rc=$?
+  --bytes 67108864 --soak 20000 --timeout 380 > gpurun_out/xcomm_soak_virtual8.json 2> gpurun_out/xcomm_soak_virtual8.err; rc=$?
 cat gpurun_out/xcomm_soak_virtual8.json
 [ $rc -eq 0 ] || { tail -30 gpurun_out/xcomm_soak_virtual8.err; exit $rc; }
