@@ -317,6 +317,7 @@ uint64_t parse_size(const char* s) {
 
 int main(int argc, char** argv) {
     Args a;
+    int soak = 0;
     for (int i = 1; i < argc; ++i) {
         std::string k = argv[i];
         auto val = [&]() -> const char* {
@@ -334,15 +335,17 @@ int main(int argc, char** argv) {
         else if (k == "--ranks") a.ranks = std::atoi(val());
         else if (k == "--mode") a.mode = val();
         else if (k == "--wg-per-cu") a.per_cu = std::atoi(val());
+        else if (k == "--soak") soak = std::atoi(val());
         else {
             std::fprintf(stderr,
                          "usage: netop-xgmi-allreduce [-b min] [-e max] [-f factor] [-n iters] [-w warmup]\n"
-                         "         [--ranks N (default: all GPUs, <= 8)] [--mode pull|push|both] [--wg-per-cu K]\n");
+                         "         [--ranks N (default: all GPUs, <= 8)] [--mode pull|push|both] [--wg-per-cu K]\n"
+                         "         [--soak N (N calls of random sizes up to -e, pull and push in turn, each checked)]\n");
             return k == "-h" || k == "--help" ? 0 : 2;
         }
     }
     if (a.mode != "pull" && a.mode != "push" && a.mode != "both") return 2;
-    if (a.factor <= 1 || a.iters < 1 || a.min_bytes > a.max_bytes || a.per_cu < 1) return 2;
+    if (a.factor <= 1 || a.iters < 1 || a.min_bytes > a.max_bytes || a.per_cu < 1 || soak < 0) return 2;
     int ngpu = 0;
     HIPCHECK(hipGetDeviceCount(&ngpu));
     if (ngpu < 1) return 1;
@@ -357,6 +360,38 @@ int main(int argc, char** argv) {
                  a.per_cu);
     std::fprintf(stderr, "#%5s %12s %10s %10s %10s %8s\n", "mode", "size(B)", "time(us)", "algbw", "busbw", "#wrong");
     unsigned long long total_wrong = 0;
+    if (soak > 0) {
+        // Every call on fresh data and checked exactly: random sizes (the same sequence on every
+        // run), pull and push in turn, every third call issued again straight after the previous
+        // one on the same buffers.  What a timed loop cannot show: a cross-stream event or
+        // buffer-reuse race that corrupts one call in thousands.
+        uint64_t rng = 0x5eed5eed5eedull;
+        auto t0 = std::chrono::steady_clock::now();
+        unsigned long long calls[2] = {0, 0}, wrong[2] = {0, 0};
+        for (int i = 0; i < soak; ++i) {
+            rng ^= rng << 13;
+            rng ^= rng >> 7;
+            rng ^= rng << 17;
+            const bool push = a.mode == "push" || (a.mode == "both" && (i & 1));
+            const uint64_t bytes = node.round_bytes(16ull * n + rng % a.max_bytes);
+            uint32_t seed = 0x50a10000u + uint32_t(i);
+            node.fill(seed, bytes);
+            node.allreduce(bytes, push);
+            if (i % 3 == 2) {
+                seed ^= 0x00ff00ffu;
+                node.fill(seed, bytes);
+                node.allreduce(bytes, push);
+            }
+            wrong[push] += node.verify(seed, bytes);
+            ++calls[push];
+        }
+        const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        total_wrong = wrong[0] + wrong[1];
+        std::printf("{\"op\":\"xgmi_all_reduce_soak\",\"ranks\":%d,\"gpus\":%d,\"max_bytes\":%llu,\"calls\":{\"pull\":%llu,"
+                    "\"push\":%llu},\"wrong\":{\"pull\":%llu,\"push\":%llu},\"seconds\":%.2f}\n",
+                    n, gpus_used, (unsigned long long)a.max_bytes, calls[0], calls[1], wrong[0], wrong[1], secs);
+        return total_wrong ? 3 : 0;
+    }
     std::vector<std::string> modes;
     if (a.mode != "push") modes.push_back("pull");
     if (a.mode != "pull") modes.push_back("push");

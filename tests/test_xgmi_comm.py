@@ -123,6 +123,21 @@ def test_single_process_xgmi_allreduce_virtual_ranks_exact(cuda_device):
 
 
 @pytest.mark.gpu
+def test_single_process_xgmi_allreduce_soak_every_call_exact(cuda_device):
+    """netop-xgmi-allreduce --soak: 300 calls over 4 ranks on the one GPU, random sizes, pull and
+    push in turn, every call on fresh data and checked exactly (rc 3 on any wrong element)."""
+    import subprocess
+
+    from network_operator_amd.utils.paths import native_bin
+
+    r = subprocess.run([str(native_bin("netop-xgmi-allreduce")), "--ranks", "4", "-e", str(8 << 20), "--mode", "both",
+                        "--soak", "300"], capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    doc = json.loads(r.stdout.strip().splitlines()[-1])
+    assert doc["calls"] == {"pull": 150, "push": 150} and doc["wrong"] == {"pull": 0, "push": 0}, doc
+
+
+@pytest.mark.gpu
 def test_xgmi_allreduce_small_buffers_share_one_ipc_segment(cuda_device):
     """64 KiB symmetric buffers come from one caching-allocator segment, so both have the same
     IPC handle: each peer maps it once and addresses both buffers inside it."""
