@@ -200,16 +200,28 @@ def native_rccl(world: int, env_probe: bool = False) -> dict:
     return out
 
 
+def _soak(fn) -> dict:
+    try:
+        return fn()
+    except Exception as e:  # the timed rows stand without it
+        return {"error": str(e)[-300:]}
+
+
 def xgmi_allreduce(world: int, nbytes: int) -> dict:
     from . import xgmi_allreduce as XA
 
-    return {"rows": XA.run(ranks=world, min_bytes=nbytes, max_bytes=nbytes, iters=10, warmup=3, timeout=110)}
+    out = {"rows": XA.run(ranks=world, min_bytes=nbytes, max_bytes=nbytes, iters=10, warmup=3, timeout=80)}
+    # Then 1000 calls over the real links, every one checked (random sizes up to 64 MiB).
+    out["soak"] = _soak(lambda: XA.soak(ranks=world, max_bytes=min(nbytes, 64 << 20), calls=1000, timeout=30))
+    return out
 
 
 def xgmi_comm(world: int, nbytes: int) -> dict:
     from . import xgmi_comm as XC
 
-    return XC.run(world, nbytes=nbytes, min_bytes=1 << 20, iters=10, warmup=3, timeout=110)
+    out = XC.run(world, nbytes=nbytes, min_bytes=1 << 20, iters=10, warmup=3, timeout=80)
+    out["soak"] = _soak(lambda: XC.run(world, nbytes=min(nbytes, 64 << 20), timeout=30, soak=1000))
+    return out
 
 
 def node_ready(n_nics: int, runs: int, required: bool = False) -> dict:

@@ -31,3 +31,17 @@ def run(timeout: float = 300, **kw) -> List[dict]:
     if r.returncode not in (0, 3):
         raise RuntimeError(f"netop-xgmi-allreduce failed ({r.returncode}): {r.stderr[-2000:]}")
     return parse(r.stdout)
+
+
+def soak(ranks: Optional[int] = None, max_bytes: int = 64 << 20, calls: int = 1000, timeout: float = 60) -> dict:
+    """``--soak``: `calls` all-reduces of random sizes up to `max_bytes`, pull and push in turn,
+    every one on fresh data and checked exactly.  Returns the binary's document (``wrong`` per
+    mode; the binary exits 3 when any element was wrong, which is reported, not raised)."""
+    cmd = [str(native_bin("netop-xgmi-allreduce")), "-e", str(max_bytes), "--mode", "both", "--soak", str(calls)]
+    if ranks:
+        cmd += ["--ranks", str(ranks)]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout)
+    docs = parse(r.stdout)
+    if r.returncode not in (0, 3) or not docs:
+        raise RuntimeError(f"netop-xgmi-allreduce --soak failed ({r.returncode}): {r.stderr[-2000:]}")
+    return docs[-1]
